@@ -1,0 +1,153 @@
+// Argument block for the GPU inbound-pipeline engine (csrc/hip/swgpu.hip).
+//
+// Every field is 8 bytes (pointer or int64) so the ctypes mirror in
+// sitewhere_amd/ops/engine_abi.py has no padding ambiguity.  The Python side
+// allocates every buffer as a torch tensor (so the caching allocator owns HBM)
+// and passes raw pointers; the library never allocates.
+#pragma once
+#include <stdint.h>
+#include "swtypes.h"
+
+typedef struct SwNameRef {
+  uint64_t hash;
+  uint32_t off;
+  uint16_t len;
+  uint8_t src_rank;
+  uint8_t pad;
+} SwNameRef;
+
+typedef struct SwEngineArgs {
+  // ---------------------------------------------------------------- batch input
+  const uint8_t* raw;          // raw wire bytes of the batch (device)
+  const uint32_t* msg_off;     // n_msgs + 1 offsets into raw (device)
+  int64_t n_msgs;
+  int64_t now_ms;              // receive time of the batch
+  int64_t rank;
+  int64_t world;
+  int64_t batch_seq;           // step counter of this rank (raw-log addressing)
+  // ---------------------------------------------------------------- decode
+  uint32_t* msg_cnt;           // [msg_cap]
+  uint32_t* msg_evoff;         // [msg_cap]
+  uint32_t* scan_tmp;          // [scan_tmp_len] block sums
+  int64_t scan_tmp_len;
+  SwEventRec* recs;            // [rec_cap] decoded records (pre-shuffle)
+  int64_t rec_cap;
+  uint32_t* n_recs;            // device scalar
+  // new-name capture on the source rank (strings live in this rank's raw batch)
+  uint64_t* seen_key;
+  int64_t seen_mask;
+  SwNameRef* new_names;        // [names_cap]
+  uint32_t* n_new_names;
+  int64_t names_cap;
+  // ---------------------------------------------------------------- shuffle (world > 1)
+  SwEventRec* send;            // [world * shuf_cap]
+  SwEventRec* recv;            // [world * shuf_cap]
+  int64_t shuf_cap;
+  uint32_t* send_cnt;          // [world]
+  uint32_t* recv_cnt;          // [world]
+  uint32_t* part_tmp;          // [world * n_tiles]
+  int64_t part_tmp_len;
+  uint32_t* overflow;          // device scalar: records dropped by the bounded shuffle
+  // ---------------------------------------------------------------- validated batch
+  SwEventRec* work;            // records after shuffle (== recs when world == 1)
+  uint32_t* n_work;            // device scalar
+  uint8_t* status;             // [rec_cap]
+  int32_t* ev_dev;             // [rec_cap]
+  int32_t* ev_asg;             // [rec_cap]
+  uint32_t* ok_idx;            // [rec_cap]
+  uint32_t* n_ok;
+  uint32_t* rej_idx;           // [rec_cap]
+  uint32_t* n_rej;
+  uint32_t* cmp_tmp;           // [scan_tmp_len]
+  // ---------------------------------------------------------------- registry (host-built, read-only here)
+  const uint64_t* reg_lo;
+  const uint64_t* reg_hi;
+  const int32_t* reg_val;
+  int64_t reg_mask;
+  const int32_t* dev_asg;      // active assignment per device (-1 none)
+  const int32_t* dev_type;
+  const int32_t* asg_device;
+  const int32_t* asg_customer;
+  const int32_t* asg_area;
+  const int32_t* asg_asset;
+  const uint8_t* asg_active;
+  int64_t n_asg;
+  // ---------------------------------------------------------------- dedup window
+  uint64_t* dd_key;
+  int64_t* dd_seq;
+  int64_t dd_mask;
+  int64_t* seq_base;           // device scalar: events seen so far on this rank
+  // ---------------------------------------------------------------- names intern (state-map keys)
+  uint64_t* nm_key;
+  int32_t* nm_id;
+  int32_t* nm_first;
+  int64_t nm_mask;
+  int32_t* nm_counter;
+  // ---------------------------------------------------------------- device state (per assignment)
+  uint64_t* st_last;           // last interaction
+  uint64_t* st_missing;        // presence missing date (0 = present)
+  uint64_t* st_loc_date;
+  int64_t* st_loc_eid;
+  uint64_t* ms_key;            // (asg << 32 | name_id << 1 | kind) ; kind 0 = measurement, 1 = alert
+  uint64_t* ms_date;
+  int64_t* ms_eid;
+  int64_t ms_mask;
+  // ---------------------------------------------------------------- event store (HBM ring, SoA)
+  int64_t store_cap;
+  int64_t* store_cursor;       // device scalar: events persisted so far on this rank
+  int64_t* step_cursor0;       // device scalar: cursor at step start
+  uint8_t* s_etype;
+  uint8_t* s_level;
+  int64_t* s_date;
+  int64_t* s_recv;
+  int32_t* s_dev;
+  int32_t* s_asg;
+  int32_t* s_cust;
+  int32_t* s_area;
+  int32_t* s_asset;
+  uint64_t* s_name;
+  double* s_v0;
+  double* s_v1;
+  double* s_v2;
+  uint64_t* s_alt;
+  uint64_t* s_aux;             // src_rank << 48 | len << 32 | batch-relative offset
+  int32_t* s_batch;            // batch_seq of the source rank when decoded
+  // ---------------------------------------------------------------- outbound (D2H to connectors)
+  SwOutRec* out;               // [rec_cap + gen_cap]
+  uint32_t* n_out;
+  // ---------------------------------------------------------------- rules (zone tests)
+  const double* zone_vtx;      // [2 * n_vertices] (lat, lon) pairs
+  const int32_t* zone_off;     // [n_zones + 1]
+  const double* zone_bbox;     // [4 * n_zones] min_lat, min_lon, max_lat, max_lon
+  int64_t n_zones;
+  const SwZoneTest* tests;
+  int64_t n_tests;
+  const uint64_t* test_name_hash; // alert type hash per test
+  // generated events (rule alerts, presence state changes)
+  SwEventRec* gen;
+  int32_t* gen_dev;
+  int32_t* gen_asg;
+  uint32_t* n_gen;
+  int64_t gen_cap;
+  // ---------------------------------------------------------------- presence
+  int64_t presence_missing_ms; // <= 0 disables the scan this step
+  uint64_t presence_name_hash; // hash of "presence"
+  // ---------------------------------------------------------------- stats
+  uint64_t* stats;             // [16] cumulative counters (see SW_STAT_*)
+} SwEngineArgs;
+
+enum {
+  SW_STAT_MSGS = 0,
+  SW_STAT_EVENTS = 1,
+  SW_STAT_PERSISTED = 2,
+  SW_STAT_UNREGISTERED = 3,
+  SW_STAT_UNASSIGNED = 4,
+  SW_STAT_DUPLICATE = 5,
+  SW_STAT_DECODE_ERROR = 6,
+  SW_STAT_CONTROL = 7,
+  SW_STAT_RULE_ALERTS = 8,
+  SW_STAT_PRESENCE = 9,
+  SW_STAT_SHUFFLE_OVERFLOW = 10,
+  SW_STAT_NEW_NAMES = 11,
+  SW_STAT_N = 16,
+};

@@ -1,0 +1,198 @@
+// Shared record layouts and hash functions for the SiteWhere-AMD data plane.
+//
+// Compiled both by hipcc (device kernels, csrc/hip/*.hip) and by g++ (host
+// runtime, csrc/native/*.cpp).  Every layout here is mirrored by a numpy
+// dtype in sitewhere_amd/models/columnar.py; tests/test_columnar.py pins the
+// offsets so the two never drift.
+//
+// Design notes (MI355X-first, see docs/ARCHITECTURE.md):
+//  * Device tokens (reference: hardwareId / device token strings, e.g.
+//    sitewhere-communication/src/main/proto/sitewhere.proto:14-60) are reduced
+//    to a 128-bit fingerprint at decode time.  The registry, the shuffle and the
+//    state tables only ever carry the fingerprint, so every hot record is fixed
+//    width (80 B) and no variable-length token bytes cross xGMI.
+//  * Records are 16-B aligned so a wave moves them with dwordx4 loads.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SW_HD __host__ __device__ __forceinline__
+#else
+#define SW_HD static inline
+#endif
+
+// ---------------------------------------------------------------- event types
+// Matches GDeviceEventType (sitewhere-grpc-event-management/.../device-event-model.proto).
+enum SwEventType : uint8_t {
+  SW_EV_MEASUREMENT = 0,
+  SW_EV_LOCATION = 1,
+  SW_EV_ALERT = 2,
+  SW_EV_COMMAND_INVOCATION = 3,
+  SW_EV_COMMAND_RESPONSE = 4,
+  SW_EV_STATE_CHANGE = 5,
+  // control messages (not persisted by the GPU path; routed to the host)
+  SW_EV_REGISTRATION = 16,
+  SW_EV_ACK = 17,
+  SW_EV_STREAM_CREATE = 18,
+  SW_EV_STREAM_DATA = 19,
+  SW_EV_STREAM_DATA_REQUEST = 20,
+  SW_EV_DECODE_ERROR = 255,
+};
+
+// Processing status of an event after inbound validation
+// (reference: InboundPayloadProcessingLogic.java:119-218).
+enum SwStatus : uint8_t {
+  SW_ST_OK = 0,
+  SW_ST_UNREGISTERED = 1,   // no device with this token -> unregistered topic
+  SW_ST_UNASSIGNED = 2,     // device has no active assignment -> unregistered topic
+  SW_ST_DUPLICATE = 3,      // alternate id seen before (AlternateIdDeduplicator)
+  SW_ST_DECODE_ERROR = 4,   // failed-decode topic
+  SW_ST_CONTROL = 5,        // registration / ack / stream: host path
+};
+
+// record flags
+#define SW_F_HAS_UPDATE_STATE 0x1
+#define SW_F_UPDATE_STATE 0x2
+#define SW_F_HAS_DATE 0x4
+#define SW_F_HAS_ELEVATION 0x8
+
+// Decoded event record, 80 bytes.  Output of the decoder, unit of the
+// multi-GPU all-to-all, input of validation.
+typedef struct __attribute__((aligned(16))) SwEventRec {
+  uint64_t fp_lo;       // 0  device token fingerprint (low)
+  uint64_t fp_hi;       // 8  device token fingerprint (high)
+  int64_t event_date;   // 16 epoch ms
+  uint64_t name_hash;   // 24 measurement name / alert type hash (0 if none)
+  double v0;            // 32 measurement value | latitude
+  double v1;            // 40 longitude
+  double v2;            // 48 elevation
+  uint64_t alt_hash;    // 56 alternate-id hash for dedup (0 = none)
+  uint32_t aux_off;     // 64 offset of name/type string in source raw batch (control: msg start)
+  uint32_t aux2_off;    // 68 offset of alert message string (control: msg end)
+  uint16_t aux_len;     // 72
+  uint16_t aux2_len;    // 74
+  uint8_t etype;        // 76 SwEventType
+  uint8_t flags;        // 77 SW_F_*
+  uint8_t src_rank;     // 78 rank whose raw batch holds the aux bytes
+  uint8_t level;        // 79 alert level (GAlertLevel)
+} SwEventRec;
+
+// Enriched, persisted event as delivered to outbound consumers (D2H), 48 bytes.
+// Reference: GEnrichedEventPayload (event + device/assignment context).
+typedef struct __attribute__((aligned(16))) SwOutRec {
+  int64_t event_id;     // 0  global event id (rank-striped, see engine)
+  int64_t event_date;   // 8
+  double v0;            // 16
+  double v1;            // 24
+  int32_t assignment;   // 32
+  int32_t device;       // 36
+  int32_t name_id;      // 40 interned name / alert type id (-1 none)
+  uint8_t etype;        // 44
+  uint8_t level;        // 45
+  uint16_t status;      // 46 reserved
+} SwOutRec;
+
+// Zone-test rule (reference: ZoneTestRuleProcessor.java:47-62).
+typedef struct SwZoneTest {
+  int32_t zone;         // index into zone polygon table
+  int32_t condition;    // 0 = alert when INSIDE, 1 = alert when OUTSIDE
+  int32_t alert_name_id;// interned alert type
+  int32_t level;        // alert level
+} SwZoneTest;
+
+// ---------------------------------------------------------------- hashing
+#define SW_FNV_OFFSET 0xcbf29ce484222325ULL
+#define SW_FNV_PRIME 0x100000001b3ULL
+#define SW_POLY_SEED 0x9e3779b97f4a7c15ULL
+#define SW_POLY_MUL 0xff51afd7ed558ccdULL
+
+SW_HD uint64_t sw_mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ULL;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebULL;
+  x ^= x >> 31;
+  return x;
+}
+
+// 128-bit fingerprint of a byte string: FNV-1a-64 and an independent odd-multiplier
+// polynomial hash, both finalised with splitmix64.  (0,0) is reserved as "empty".
+SW_HD void sw_fingerprint(const uint8_t* p, uint32_t n, uint64_t* lo, uint64_t* hi) {
+  uint64_t a = SW_FNV_OFFSET, b = SW_POLY_SEED ^ (uint64_t)n;
+  for (uint32_t i = 0; i < n; ++i) {
+    a = (a ^ p[i]) * SW_FNV_PRIME;
+    b = (b + p[i] + 1) * SW_POLY_MUL;
+  }
+  a = sw_mix64(a);
+  b = sw_mix64(b ^ (b >> 29));
+  if (a == 0 && b == 0) a = 1;
+  *lo = a;
+  *hi = b;
+}
+
+// 64-bit string hash (names, alert types, alternate ids). 0 is reserved.
+SW_HD uint64_t sw_hash64(const uint8_t* p, uint32_t n) {
+  uint64_t a = SW_FNV_OFFSET;
+  for (uint32_t i = 0; i < n; ++i) a = (a ^ p[i]) * SW_FNV_PRIME;
+  a = sw_mix64(a ^ ((uint64_t)n << 56));
+  return a ? a : 1;
+}
+
+// Which rank owns a device (multi-GPU sharding of registry/state/store).
+SW_HD uint32_t sw_owner(uint64_t fp_hi, uint32_t world) {
+  return (uint32_t)((fp_hi >> 32) % (uint64_t)world);
+}
+
+// ------------------------------------------------------- protobuf wire helpers
+// Wire protocol: reference sitewhere-communication/src/main/proto/sitewhere.proto.
+// Each payload = varint-delimited SiteWhere.Header + varint-delimited body.
+#define SW_CMD_SEND_REGISTRATION 1
+#define SW_CMD_SEND_ACKNOWLEDGEMENT 2
+#define SW_CMD_SEND_DEVICE_LOCATION 3
+#define SW_CMD_SEND_DEVICE_ALERT 4
+#define SW_CMD_SEND_DEVICE_MEASUREMENTS 5
+#define SW_CMD_SEND_DEVICE_STREAM 6
+#define SW_CMD_SEND_DEVICE_STREAM_DATA 7
+#define SW_CMD_REQUEST_DEVICE_STREAM_DATA 8
+// Extension field (not in the reference schema; ignored by reference parsers as an
+// unknown field): string alternateId = 15 on DeviceLocation/DeviceAlert/DeviceMeasurements.
+#define SW_FIELD_ALTERNATE_ID 15
+
+// Read a varint in [*pos, end). Returns false on truncation/overlong.
+SW_HD bool sw_read_varint(const uint8_t* buf, uint32_t* pos, uint32_t end, uint64_t* out) {
+  uint64_t v = 0;
+  uint32_t shift = 0, p = *pos;
+  while (p < end && shift < 64) {
+    uint8_t b = buf[p++];
+    v |= (uint64_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) {
+      *pos = p;
+      *out = v;
+      return true;
+    }
+    shift += 7;
+  }
+  return false;
+}
+
+SW_HD uint64_t sw_load_le64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+
+// Skip one field of the given wire type. Returns false on malformed input.
+SW_HD bool sw_skip_field(const uint8_t* buf, uint32_t* pos, uint32_t end, uint32_t wt) {
+  uint64_t tmp;
+  switch (wt) {
+    case 0: return sw_read_varint(buf, pos, end, &tmp);
+    case 1: if (*pos + 8 > end) return false; *pos += 8; return true;
+    case 2:
+      if (!sw_read_varint(buf, pos, end, &tmp)) return false;
+      if (tmp > (uint64_t)(end - *pos)) return false;
+      *pos += (uint32_t)tmp;
+      return true;
+    case 5: if (*pos + 4 > end) return false; *pos += 4; return true;
+    default: return false;
+  }
+}

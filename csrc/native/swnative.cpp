@@ -1,0 +1,619 @@
+// SiteWhere-AMD native host runtime (C ABI, loaded with ctypes).
+//
+//  1. swlog_*      partitioned, append-only, durable commit log with consumer-group
+//                  offsets: the in-process replacement for the Kafka data plane
+//                  (reference: sitewhere-microservice/.../kafka/MicroserviceKafkaConsumer.java,
+//                  MicroserviceKafkaProducer.java, KafkaTopicNaming.java).  Kafka-compatible
+//                  murmur2 key partitioning so records keyed by device token land on the
+//                  same partition they would in the reference.
+//  2. sw_reg_*     host-side builder of the device registry hash table that the GPU
+//                  engine probes (exact 128-bit keys, deterministic layout).
+//  3. sw_cpu_decode multithreaded protobuf batch decoder sharing csrc/include/swdecode.h
+//                  with the GPU kernel (CPU fallback engine + parity oracle).
+//  4. sw_gen_*     synthetic device-fleet payload generator (benchmarks / tests).
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <errno.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <unistd.h>
+#include <fcntl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "swtypes.h"
+#include "swdecode.h"
+
+// ============================================================================ hashing helpers
+extern "C" {
+
+void sw_fingerprint_batch(const uint8_t* heap, const int64_t* offs, int64_t n, uint64_t* lo, uint64_t* hi) {
+  for (int64_t i = 0; i < n; ++i) sw_fingerprint(heap + offs[i], (uint32_t)(offs[i + 1] - offs[i]), lo + i, hi + i);
+}
+
+void sw_hash64_batch(const uint8_t* heap, const int64_t* offs, int64_t n, uint64_t* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = sw_hash64(heap + offs[i], (uint32_t)(offs[i + 1] - offs[i]));
+}
+
+// Kafka's default partitioner hash (murmur2, seed 0x9747b28c).
+int32_t sw_murmur2(const uint8_t* data, int32_t length) {
+  const uint32_t seed = 0x9747b28c, m = 0x5bd1e995;
+  const int r = 24;
+  uint32_t h = seed ^ (uint32_t)length;
+  int32_t length4 = length / 4;
+  for (int32_t i = 0; i < length4; i++) {
+    const int32_t i4 = i * 4;
+    uint32_t k = (data[i4 + 0] & 0xff) + ((uint32_t)(data[i4 + 1] & 0xff) << 8) + ((uint32_t)(data[i4 + 2] & 0xff) << 16) +
+                 ((uint32_t)(data[i4 + 3] & 0xff) << 24);
+    k *= m;
+    k ^= k >> r;
+    k *= m;
+    h *= m;
+    h ^= k;
+  }
+  switch (length % 4) {
+    case 3: h ^= (uint32_t)(data[(length & ~3) + 2] & 0xff) << 16; /* fallthrough */
+    case 2: h ^= (uint32_t)(data[(length & ~3) + 1] & 0xff) << 8; /* fallthrough */
+    case 1: h ^= (uint32_t)(data[length & ~3] & 0xff); h *= m;
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+
+int32_t sw_partition_for_key(const uint8_t* key, int32_t len, int32_t n_partitions) {
+  return (int32_t)(((uint32_t)sw_murmur2(key, len) & 0x7fffffffu) % (uint32_t)n_partitions);
+}
+
+// ============================================================================ registry builder
+// Open addressing with linear probing over (lo, hi); (0,0) = empty.  Returns the slot
+// written (>= 0), or -1 if the table is full.  Upsert semantics.
+int64_t sw_reg_upsert(uint64_t* tlo, uint64_t* thi, int32_t* tval, int64_t mask, uint64_t lo, uint64_t hi, int32_t val) {
+  int64_t slot = (int64_t)(lo & (uint64_t)mask);
+  for (int64_t p = 0; p <= mask; ++p) {
+    if (tlo[slot] == lo && thi[slot] == hi) { tval[slot] = val; return slot; }
+    if (tlo[slot] == 0 && thi[slot] == 0) { tlo[slot] = lo; thi[slot] = hi; tval[slot] = val; return slot; }
+    slot = (slot + 1) & mask;
+  }
+  return -1;
+}
+
+int64_t sw_reg_find(const uint64_t* tlo, const uint64_t* thi, const int32_t* tval, int64_t mask, uint64_t lo, uint64_t hi) {
+  int64_t slot = (int64_t)(lo & (uint64_t)mask);
+  for (int64_t p = 0; p <= mask; ++p) {
+    if (tlo[slot] == lo && thi[slot] == hi) return tval[slot];
+    if (tlo[slot] == 0 && thi[slot] == 0) return -1;
+    slot = (slot + 1) & mask;
+  }
+  return -1;
+}
+
+// Bulk upsert; writes the slot of every key into slots_out (may be null).  Returns #failed.
+int64_t sw_reg_build(uint64_t* tlo, uint64_t* thi, int32_t* tval, int64_t mask, const uint64_t* lo, const uint64_t* hi,
+                     const int32_t* val, int64_t n, int64_t* slots_out) {
+  int64_t failed = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t s = sw_reg_upsert(tlo, thi, tval, mask, lo[i], hi[i], val[i]);
+    if (s < 0) ++failed;
+    if (slots_out) slots_out[i] = s;
+  }
+  return failed;
+}
+
+// ============================================================================ CPU decode
+// Two-pass (count, scan, emit) exactly like the GPU path; parallel over message ranges.
+int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, int64_t now_ms, int32_t rank,
+                      SwEventRec* out, int64_t cap, int32_t n_threads) {
+  if (n_msgs <= 0) return 0;
+  std::vector<uint32_t> cnt(n_msgs);
+  if (n_threads < 1) n_threads = 1;
+  auto run = [&](auto&& fn) {
+    std::vector<std::thread> th;
+    int64_t chunk = (n_msgs + n_threads - 1) / n_threads;
+    for (int t = 0; t < n_threads; ++t) {
+      int64_t b = t * chunk, e = std::min<int64_t>(n_msgs, b + chunk);
+      if (b >= e) break;
+      th.emplace_back([&, b, e] { fn(b, e); });
+    }
+    for (auto& x : th) x.join();
+  };
+  run([&](int64_t b, int64_t e) {
+    for (int64_t m = b; m < e; ++m) cnt[m] = sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, nullptr, 0);
+  });
+  std::vector<int64_t> pre(n_msgs + 1, 0);
+  for (int64_t m = 0; m < n_msgs; ++m) pre[m + 1] = pre[m] + cnt[m];
+  run([&](int64_t b, int64_t e) {
+    for (int64_t m = b; m < e; ++m) {
+      int64_t o = pre[m];
+      if (o >= cap) continue;
+      sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, out + o, (uint32_t)std::min<int64_t>(cap - o, 0xffffffffll));
+    }
+  });
+  return std::min<int64_t>(pre[n_msgs], cap);
+}
+
+// ============================================================================ fleet generator
+// Encodes SiteWhere device-protocol payloads (delimited Header + delimited body).
+struct Enc {
+  std::vector<uint8_t>& b;
+  void varint(uint64_t v) { while (v >= 0x80) { b.push_back((uint8_t)(v | 0x80)); v >>= 7; } b.push_back((uint8_t)v); }
+  void key(uint32_t f, uint32_t wt) { varint(((uint64_t)f << 3) | wt); }
+  void str(uint32_t f, const char* s, size_t n) { key(f, 2); varint(n); b.insert(b.end(), (const uint8_t*)s, (const uint8_t*)s + n); }
+  void fixed64(uint32_t f, uint64_t v) { key(f, 1); for (int i = 0; i < 8; ++i) b.push_back((uint8_t)(v >> (8 * i))); }
+  void dbl(uint32_t f, double d) { uint64_t v; memcpy(&v, &d, 8); fixed64(f, v); }
+};
+
+static inline uint64_t xs64(uint64_t& s) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+
+// kinds: 0 measurement, 1 location, 2 alert, 3 registration (control)
+// Generates n messages into a caller buffer; returns bytes written or -needed if too small.
+// Device tokens are "<prefix><index zero-padded to 10>"; unregistered devices use indices >= n_devices.
+int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, double p_loc, double p_alert,
+                        double p_unreg, int32_t mx_per_msg, int32_t n_names, int64_t ts0, uint64_t seed,
+                        int32_t with_alt_id, double lat0, double lon0, double span_deg, uint8_t* out, int64_t out_cap,
+                        uint32_t* offs) {
+  std::vector<uint8_t> buf;
+  buf.reserve(96);
+  Enc e{buf};
+  std::vector<uint8_t> body;
+  body.reserve(128);
+  Enc eb{body};
+  uint64_t s = seed * 0x9e3779b97f4a7c15ULL + 1;
+  const size_t plen = strlen(prefix);
+  char tok[128];
+  char name[32];
+  int64_t pos = 0;
+  for (int64_t m = 0; m < n_msgs; ++m) {
+    buf.clear();
+    body.clear();
+    const double u = (double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0);
+    const double u2 = (double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0);
+    int64_t dev = (int64_t)(xs64(s) % (uint64_t)n_devices);
+    if (u2 < p_unreg) dev = n_devices + (int64_t)(xs64(s) % 1000003ULL);
+    memcpy(tok, prefix, plen);
+    snprintf(tok + plen, sizeof(tok) - plen, "%010lld", (long long)dev);
+    const size_t tlen = plen + 10;
+    const int64_t ts = ts0 + (int64_t)(xs64(s) % 60000ULL);
+    uint32_t cmd;
+    char alt[48];
+    size_t alen = 0;
+    if (with_alt_id) alen = (size_t)snprintf(alt, sizeof(alt), "a%llx-%lld", (unsigned long long)seed, (long long)m);
+    if (u < p_loc) {
+      cmd = SW_CMD_SEND_DEVICE_LOCATION;
+      eb.str(1, tok, tlen);
+      eb.dbl(2, lat0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0)));
+      eb.dbl(3, lon0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0)));
+      eb.dbl(4, 10.0);
+      eb.fixed64(5, (uint64_t)ts);
+    } else if (u < p_loc + p_alert) {
+      cmd = SW_CMD_SEND_DEVICE_ALERT;
+      eb.str(1, tok, tlen);
+      int k = (int)(xs64(s) % 4);
+      int nl = snprintf(name, sizeof(name), "alert.type%d", k);
+      eb.str(2, name, (size_t)nl);
+      eb.str(3, "threshold exceeded", 18);
+      eb.fixed64(4, (uint64_t)ts);
+    } else {
+      cmd = SW_CMD_SEND_DEVICE_MEASUREMENTS;
+      eb.str(1, tok, tlen);
+      for (int q = 0; q < mx_per_msg; ++q) {
+        std::vector<uint8_t> mx;
+        Enc em{mx};
+        int nl = snprintf(name, sizeof(name), "mx.metric%d", (int)((xs64(s) % (uint64_t)std::max(1, n_names))));
+        em.str(1, name, (size_t)nl);
+        em.dbl(2, (double)(xs64(s) % 100000ULL) * 0.01);
+        eb.key(2, 2);
+        eb.varint(mx.size());
+        body.insert(body.end(), mx.begin(), mx.end());
+      }
+      eb.fixed64(3, (uint64_t)ts);
+    }
+    if (alen) eb.str(SW_FIELD_ALTERNATE_ID, alt, alen);
+    // header
+    std::vector<uint8_t> hdr;
+    Enc eh{hdr};
+    eh.key(1, 0);
+    eh.varint(cmd);
+    e.varint(hdr.size());
+    buf.insert(buf.end(), hdr.begin(), hdr.end());
+    e.varint(body.size());
+    buf.insert(buf.end(), body.begin(), body.end());
+    if (pos + (int64_t)buf.size() > out_cap) return -(pos + (int64_t)buf.size());
+    offs[m] = (uint32_t)pos;
+    memcpy(out + pos, buf.data(), buf.size());
+    pos += (int64_t)buf.size();
+  }
+  offs[n_msgs] = (uint32_t)pos;
+  return pos;
+}
+
+// Token heap for devices [0, n): "<prefix><index:010>"; offs has n+1 entries.
+int64_t sw_gen_tokens(const char* prefix, int64_t first, int64_t n, uint8_t* heap, int64_t cap, int64_t* offs) {
+  const size_t plen = strlen(prefix);
+  int64_t pos = 0;
+  char tok[128];
+  for (int64_t i = 0; i < n; ++i) {
+    memcpy(tok, prefix, plen);
+    snprintf(tok + plen, sizeof(tok) - plen, "%010lld", (long long)(first + i));
+    size_t tl = plen + 10;
+    if (pos + (int64_t)tl > cap) return -1;
+    offs[i] = pos;
+    memcpy(heap + pos, tok, tl);
+    pos += (int64_t)tl;
+  }
+  offs[n] = pos;
+  return pos;
+}
+
+}  // extern "C"
+
+// ============================================================================ partitioned log
+namespace swlog {
+
+static uint32_t crc32c_table[256];
+static std::once_flag crc_once;
+static void crc_init() {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0x82f63b78u ^ (c >> 1) : c >> 1;
+    crc32c_table[i] = c;
+  }
+}
+static uint32_t crc32c(const uint8_t* p, size_t n, uint32_t c = 0) {
+  std::call_once(crc_once, crc_init);
+  c = ~c;
+  for (size_t i = 0; i < n; ++i) c = crc32c_table[(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return ~c;
+}
+
+#pragma pack(push, 1)
+struct RecHdr {
+  uint32_t len;    // bytes after this header (key + value)
+  uint32_t crc;    // crc32c of (ts, klen, key, value)
+  int64_t ts;
+  uint16_t klen;
+};
+#pragma pack(pop)
+
+struct Partition {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<uint8_t> data;       // in-memory image of the partition log
+  std::vector<int64_t> index;      // record offset -> byte position in data
+  int64_t base_offset = 0;         // first retained offset
+  int fd = -1;                     // durable backing file (append-only), -1 = memory only
+};
+
+struct Topic {
+  std::string name;
+  std::vector<std::unique_ptr<Partition>> parts;
+};
+
+struct Log {
+  std::string dir;                 // empty = in-memory
+  int fsync_each = 0;
+  std::mutex mu;
+  std::vector<std::unique_ptr<Topic>> topics;
+  std::map<std::string, int> by_name;
+  // group -> (topic name, partition) -> committed offset
+  std::mutex gmu;
+  std::map<std::string, std::map<std::pair<std::string, int>, int64_t>> groups;
+};
+
+static void mkdirs(const std::string& p) {
+  std::string cur;
+  for (size_t i = 0; i < p.size(); ++i) {
+    cur.push_back(p[i]);
+    if (p[i] == '/' || i + 1 == p.size()) mkdir(cur.c_str(), 0755);
+  }
+}
+
+static void load_partition(Partition* pt, const std::string& path) {
+  int fd = open(path.c_str(), O_RDWR | O_CREAT, 0644);
+  if (fd < 0) return;
+  struct stat st;
+  fstat(fd, &st);
+  pt->data.resize((size_t)st.st_size);
+  size_t got = 0;
+  while (got < pt->data.size()) {
+    ssize_t r = pread(fd, pt->data.data() + got, pt->data.size() - got, (off_t)got);
+    if (r <= 0) break;
+    got += (size_t)r;
+  }
+  pt->data.resize(got);
+  // rebuild index, truncating a torn tail record (crash during append)
+  size_t pos = 0;
+  while (pos + sizeof(RecHdr) <= pt->data.size()) {
+    RecHdr h;
+    memcpy(&h, pt->data.data() + pos, sizeof(h));
+    size_t end = pos + sizeof(RecHdr) + h.len;
+    if (end > pt->data.size()) break;
+    uint32_t c = crc32c((const uint8_t*)&h.ts, sizeof(h.ts) + sizeof(h.klen));
+    c = crc32c(pt->data.data() + pos + sizeof(RecHdr), h.len, c);
+    if (c != h.crc) break;
+    pt->index.push_back((int64_t)pos);
+    pos = end;
+  }
+  if (pos != pt->data.size()) {
+    pt->data.resize(pos);
+    if (ftruncate(fd, (off_t)pos) != 0) { /* best effort */ }
+  }
+  pt->fd = fd;
+}
+
+static void load_groups(Log* L) {
+  if (L->dir.empty()) return;
+  FILE* f = fopen((L->dir + "/__consumer_offsets").c_str(), "r");
+  if (!f) return;
+  char g[512], t[512];
+  int p;
+  long long o;
+  while (fscanf(f, "%511s %511s %d %lld", g, t, &p, &o) == 4) L->groups[g][{std::string(t), p}] = o;
+  fclose(f);
+}
+
+static void save_groups(Log* L) {
+  if (L->dir.empty()) return;
+  std::string tmp = L->dir + "/__consumer_offsets.tmp";
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) return;
+  for (auto& g : L->groups)
+    for (auto& kv : g.second)
+      fprintf(f, "%s %s %d %lld\n", g.first.c_str(), kv.first.first.c_str(), kv.first.second, (long long)kv.second);
+  fflush(f);
+  if (L->fsync_each) fsync(fileno(f));
+  fclose(f);
+  rename(tmp.c_str(), (L->dir + "/__consumer_offsets").c_str());
+}
+
+}  // namespace swlog
+
+using namespace swlog;
+
+extern "C" {
+
+void* swlog_open(const char* dir, int32_t fsync_each) {
+  Log* L = new Log();
+  if (dir && dir[0]) {
+    L->dir = dir;
+    mkdirs(L->dir);
+  }
+  L->fsync_each = fsync_each;
+  load_groups(L);
+  return L;
+}
+
+void swlog_close(void* h) {
+  Log* L = (Log*)h;
+  if (!L) return;
+  for (auto& t : L->topics)
+    for (auto& p : t->parts) {
+      std::lock_guard<std::mutex> g(p->mu);
+      if (p->fd >= 0) { fsync(p->fd); close(p->fd); p->fd = -1; }
+      p->cv.notify_all();
+    }
+  delete L;
+}
+
+// Create or open a topic; returns topic id.  Partition count is fixed at creation.
+int32_t swlog_topic(void* h, const char* name, int32_t partitions) {
+  Log* L = (Log*)h;
+  std::lock_guard<std::mutex> g(L->mu);
+  auto it = L->by_name.find(name);
+  if (it != L->by_name.end()) return it->second;
+  auto t = std::make_unique<Topic>();
+  t->name = name;
+  std::string tdir = L->dir.empty() ? "" : L->dir + "/" + name;
+  if (!tdir.empty()) {
+    mkdirs(tdir);
+    // a topic created earlier keeps its partition count (count files)
+    int existing = 0;
+    while (true) {
+      std::string pth = tdir + "/" + std::to_string(existing) + ".log";
+      struct stat st;
+      if (stat(pth.c_str(), &st) != 0) break;
+      ++existing;
+    }
+    if (existing > partitions) partitions = existing;
+  }
+  for (int p = 0; p < partitions; ++p) {
+    auto pt = std::make_unique<Partition>();
+    if (!tdir.empty()) load_partition(pt.get(), tdir + "/" + std::to_string(p) + ".log");
+    t->parts.push_back(std::move(pt));
+  }
+  int id = (int)L->topics.size();
+  L->topics.push_back(std::move(t));
+  L->by_name[name] = id;
+  return id;
+}
+
+int32_t swlog_partitions(void* h, int32_t topic) {
+  Log* L = (Log*)h;
+  std::lock_guard<std::mutex> g(L->mu);
+  if (topic < 0 || topic >= (int)L->topics.size()) return -1;
+  return (int32_t)L->topics[topic]->parts.size();
+}
+
+static Partition* part_of(Log* L, int32_t topic, int32_t p) {
+  std::lock_guard<std::mutex> g(L->mu);
+  if (topic < 0 || topic >= (int)L->topics.size()) return nullptr;
+  auto& t = L->topics[topic];
+  if (p < 0 || p >= (int)t->parts.size()) return nullptr;
+  return t->parts[p].get();
+}
+
+// Append a batch of n records to one partition.  keys/vals are concatenated with
+// n+1 offset arrays.  Returns the offset of the first record, or -1.
+int64_t swlog_append_batch(void* h, int32_t topic, int32_t p, const uint8_t* keys, const int64_t* koff,
+                           const uint8_t* vals, const int64_t* voff, const int64_t* ts, int64_t n) {
+  Log* L = (Log*)h;
+  Partition* pt = part_of(L, topic, p);
+  if (!pt) return -1;
+  std::vector<uint8_t> enc;
+  size_t total = 0;
+  for (int64_t i = 0; i < n; ++i) total += sizeof(RecHdr) + (koff[i + 1] - koff[i]) + (voff[i + 1] - voff[i]);
+  enc.resize(total);
+  std::vector<int64_t> rel(n);
+  size_t pos = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t kl = koff[i + 1] - koff[i], vl = voff[i + 1] - voff[i];
+    RecHdr hd;
+    hd.len = (uint32_t)(kl + vl);
+    hd.ts = ts ? ts[i] : 0;
+    hd.klen = (uint16_t)kl;
+    uint8_t* dst = enc.data() + pos + sizeof(RecHdr);
+    memcpy(dst, keys + koff[i], (size_t)kl);
+    memcpy(dst + kl, vals + voff[i], (size_t)vl);
+    uint32_t c = crc32c((const uint8_t*)&hd.ts, sizeof(hd.ts) + sizeof(hd.klen));
+    hd.crc = crc32c(dst, (size_t)(kl + vl), c);
+    memcpy(enc.data() + pos, &hd, sizeof(hd));
+    rel[i] = (int64_t)pos;
+    pos += sizeof(RecHdr) + (size_t)(kl + vl);
+  }
+  std::unique_lock<std::mutex> g(pt->mu);
+  const int64_t first = pt->base_offset + (int64_t)pt->index.size();
+  const int64_t base = (int64_t)pt->data.size();
+  if (pt->fd >= 0) {
+    size_t w = 0;
+    while (w < enc.size()) {
+      ssize_t r = pwrite(pt->fd, enc.data() + w, enc.size() - w, (off_t)(base + (int64_t)w));
+      if (r <= 0) return -1;
+      w += (size_t)r;
+    }
+    if (L->fsync_each) fdatasync(pt->fd);
+  }
+  pt->data.insert(pt->data.end(), enc.begin(), enc.end());
+  for (int64_t i = 0; i < n; ++i) pt->index.push_back(base + rel[i]);
+  g.unlock();
+  pt->cv.notify_all();
+  return first;
+}
+
+int64_t swlog_append(void* h, int32_t topic, int32_t p, const uint8_t* key, int64_t klen, const uint8_t* val,
+                     int64_t vlen, int64_t ts) {
+  int64_t ko[2] = {0, klen}, vo[2] = {0, vlen};
+  return swlog_append_batch(h, topic, p, key, ko, val, vo, &ts, 1);
+}
+
+int64_t swlog_end_offset(void* h, int32_t topic, int32_t p) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  return pt->base_offset + (int64_t)pt->index.size();
+}
+
+int64_t swlog_begin_offset(void* h, int32_t topic, int32_t p) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  return pt->base_offset;
+}
+
+// Block until end_offset > offset or timeout; returns the end offset.
+int64_t swlog_wait(void* h, int32_t topic, int32_t p, int64_t offset, int32_t timeout_ms) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::unique_lock<std::mutex> g(pt->mu);
+  pt->cv.wait_for(g, std::chrono::milliseconds(timeout_ms),
+                  [&] { return pt->base_offset + (int64_t)pt->index.size() > offset; });
+  return pt->base_offset + (int64_t)pt->index.size();
+}
+
+// Read up to max_records starting at offset into out as frames:
+//   [i64 offset][i64 ts][u32 klen][u32 vlen][key][value]
+// Returns bytes written (0 = nothing available), or -needed when the first record does not fit.
+int64_t swlog_read(void* h, int32_t topic, int32_t p, int64_t offset, int64_t max_records, uint8_t* out,
+                   int64_t out_cap, int64_t* n_out) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  *n_out = 0;
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  if (offset < pt->base_offset) offset = pt->base_offset;
+  int64_t i = offset - pt->base_offset, w = 0, cnt = 0;
+  while (i < (int64_t)pt->index.size() && cnt < max_records) {
+    RecHdr hd;
+    memcpy(&hd, pt->data.data() + pt->index[i], sizeof(hd));
+    const int64_t need = 24 + (int64_t)hd.len;
+    if (w + need > out_cap) {
+      if (cnt == 0) return -need;
+      break;
+    }
+    const int64_t off = pt->base_offset + i;
+    uint32_t kl = hd.klen, vl = hd.len - hd.klen;
+    memcpy(out + w, &off, 8);
+    memcpy(out + w + 8, &hd.ts, 8);
+    memcpy(out + w + 16, &kl, 4);
+    memcpy(out + w + 20, &vl, 4);
+    memcpy(out + w + 24, pt->data.data() + pt->index[i] + sizeof(RecHdr), hd.len);
+    w += need;
+    ++cnt;
+    ++i;
+  }
+  *n_out = cnt;
+  return w;
+}
+
+// Drop records before `offset` from memory (retention).  The file keeps them.
+int64_t swlog_retain_from(void* h, int32_t topic, int32_t p, int64_t offset) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  int64_t drop = offset - pt->base_offset;
+  if (drop <= 0) return pt->base_offset;
+  if (drop > (int64_t)pt->index.size()) drop = (int64_t)pt->index.size();
+  if (pt->fd >= 0) return pt->base_offset;  // durable logs keep the in-memory image aligned with the file
+  const int64_t cut = drop < (int64_t)pt->index.size() ? pt->index[drop] : (int64_t)pt->data.size();
+  pt->data.erase(pt->data.begin(), pt->data.begin() + cut);
+  pt->index.erase(pt->index.begin(), pt->index.begin() + drop);
+  for (auto& x : pt->index) x -= cut;
+  pt->base_offset += drop;
+  return pt->base_offset;
+}
+
+static std::string topic_name(Log* L, int32_t topic) {
+  std::lock_guard<std::mutex> g(L->mu);
+  return (topic >= 0 && topic < (int)L->topics.size()) ? L->topics[topic]->name : std::string();
+}
+
+int32_t swlog_commit(void* h, const char* group, int32_t topic, int32_t p, int64_t offset) {
+  Log* L = (Log*)h;
+  const std::string tn = topic_name(L, topic);
+  std::lock_guard<std::mutex> g(L->gmu);
+  L->groups[group][{tn, p}] = offset;
+  save_groups(L);
+  return 0;
+}
+
+int64_t swlog_committed(void* h, const char* group, int32_t topic, int32_t p) {
+  Log* L = (Log*)h;
+  const std::string tn = topic_name(L, topic);
+  std::lock_guard<std::mutex> g(L->gmu);
+  auto it = L->groups.find(group);
+  if (it == L->groups.end()) return -1;
+  auto j = it->second.find({tn, p});
+  return j == it->second.end() ? -1 : j->second;
+}
+
+int32_t swlog_flush(void* h) {
+  Log* L = (Log*)h;
+  std::lock_guard<std::mutex> g(L->mu);
+  for (auto& t : L->topics)
+    for (auto& p : t->parts) {
+      std::lock_guard<std::mutex> gp(p->mu);
+      if (p->fd >= 0) fdatasync(p->fd);
+    }
+  return 0;
+}
+
+}  // extern "C"

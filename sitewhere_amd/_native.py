@@ -1,0 +1,171 @@
+"""Build and load the native libraries of SiteWhere-AMD.
+
+Two shared objects are built **in-tree** under ``sitewhere_amd/_lib``:
+
+* ``libswnative.so`` (g++): the host runtime -- partitioned commit log
+  (Kafka replacement), registry builder, CPU batch decoder, fleet generator.
+* ``libswgpu.so`` (hipcc ``--offload-arch=gfx950``): the CDNA4 data-plane kernels.
+
+Both expose a plain C ABI and are loaded with :mod:`ctypes`; there is no
+hipify step and no torch C++ ABI dependency.  ``libswgpu.so`` links the HIP
+runtime by soname (``libamdhip64.so.7``); torch must be imported first so the
+process uses torch's already-loaded runtime (one HIP runtime per process).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import subprocess
+import threading
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+LIB_DIR = Path(__file__).resolve().parent / "_lib"
+CSRC = ROOT / "csrc"
+GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
+
+_NATIVE_SRC = [CSRC / "native" / "swnative.cpp"]
+_GPU_SRC = [CSRC / "hip" / "swgpu.hip"]
+_HEADERS = sorted((CSRC / "include").glob("*.h"))
+
+_lock = threading.Lock()
+_native = None
+_gpu = None
+
+
+class NativeBuildError(RuntimeError):
+    pass
+
+
+def _stale(target: Path, sources) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(s.stat().st_mtime > t for s in list(sources) + _HEADERS)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise NativeBuildError(f"build failed: {' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+
+
+def build_native(force: bool = False) -> Path:
+    """Compile libswnative.so with g++ (C++17, -O3)."""
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    out = LIB_DIR / "libswnative.so"
+    if force or _stale(out, _NATIVE_SRC):
+        cxx = shutil.which("g++") or shutil.which("c++") or "g++"
+        tmp = out.with_suffix(".so.tmp")
+        _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{CSRC / 'include'}", "-o", str(tmp),
+              *map(str, _NATIVE_SRC), "-lpthread"])
+        os.replace(tmp, out)
+    return out
+
+
+def hipcc_path() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise NativeBuildError("hipcc not found (ROCm is required to build the gfx950 kernels)")
+
+
+def build_gpu(force: bool = False) -> Path:
+    """Cross-compile libswgpu.so for gfx950 with hipcc (works without a GPU)."""
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    out = LIB_DIR / "libswgpu.so"
+    if force or _stale(out, _GPU_SRC):
+        tmp = out.with_suffix(".so.tmp")
+        _run([hipcc_path(), f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+              f"-I{CSRC / 'include'}", "-o", str(tmp), *map(str, _GPU_SRC)])
+        os.replace(tmp, out)
+    return out
+
+
+def build_all(force: bool = False):
+    return build_native(force), build_gpu(force)
+
+
+# ----------------------------------------------------------------------------- prototypes
+c_void_p, c_int32, c_int64, c_uint64, c_double, c_char_p = (
+    ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_char_p)
+
+
+def _proto(lib, name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+
+
+def native():
+    """Load (building if needed) the host runtime library."""
+    global _native
+    if _native is not None:
+        return _native
+    with _lock:
+        if _native is not None:
+            return _native
+        path = LIB_DIR / "libswnative.so"
+        if _stale(path, _NATIVE_SRC):
+            build_native()
+        lib = ctypes.CDLL(str(path))
+        P = c_void_p
+        _proto(lib, "sw_fingerprint_batch", None, P, P, c_int64, P, P)
+        _proto(lib, "sw_hash64_batch", None, P, P, c_int64, P)
+        _proto(lib, "sw_murmur2", c_int32, P, c_int32)
+        _proto(lib, "sw_partition_for_key", c_int32, P, c_int32, c_int32)
+        _proto(lib, "sw_reg_upsert", c_int64, P, P, P, c_int64, c_uint64, c_uint64, c_int32)
+        _proto(lib, "sw_reg_find", c_int64, P, P, P, c_int64, c_uint64, c_uint64)
+        _proto(lib, "sw_reg_build", c_int64, P, P, P, c_int64, P, P, P, c_int64, P)
+        _proto(lib, "sw_cpu_decode", c_int64, P, P, c_int64, c_int64, c_int32, P, c_int64, c_int32)
+        _proto(lib, "sw_gen_payloads", c_int64, c_int64, c_char_p, c_int64, c_double, c_double, c_double, c_int32,
+               c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, P, c_int64, P)
+        _proto(lib, "sw_gen_tokens", c_int64, c_char_p, c_int64, c_int64, P, c_int64, P)
+        _proto(lib, "swlog_open", P, c_char_p, c_int32)
+        _proto(lib, "swlog_close", None, P)
+        _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)
+        _proto(lib, "swlog_partitions", c_int32, P, c_int32)
+        _proto(lib, "swlog_append_batch", c_int64, P, c_int32, c_int32, P, P, P, P, P, c_int64)
+        _proto(lib, "swlog_append", c_int64, P, c_int32, c_int32, P, c_int64, P, c_int64, c_int64)
+        _proto(lib, "swlog_end_offset", c_int64, P, c_int32, c_int32)
+        _proto(lib, "swlog_begin_offset", c_int64, P, c_int32, c_int32)
+        _proto(lib, "swlog_wait", c_int64, P, c_int32, c_int32, c_int64, c_int32)
+        _proto(lib, "swlog_read", c_int64, P, c_int32, c_int32, c_int64, c_int64, P, c_int64, P)
+        _proto(lib, "swlog_retain_from", c_int64, P, c_int32, c_int32, c_int64)
+        _proto(lib, "swlog_commit", c_int32, P, c_char_p, c_int32, c_int32, c_int64)
+        _proto(lib, "swlog_committed", c_int64, P, c_char_p, c_int32, c_int32)
+        _proto(lib, "swlog_flush", c_int32, P)
+        _native = lib
+        return lib
+
+
+def gpu():
+    """Load the gfx950 kernel library.  Raises if it is missing -- never falls back silently."""
+    global _gpu
+    if _gpu is not None:
+        return _gpu
+    import torch  # noqa: F401  -- one HIP runtime per process: torch's, loaded first
+
+    with _lock:
+        if _gpu is not None:
+            return _gpu
+        path = LIB_DIR / "libswgpu.so"
+        if _stale(path, _GPU_SRC):
+            build_gpu()
+        lib = ctypes.CDLL(str(path))
+        P = c_void_p
+        _proto(lib, "sw_phase_decode", c_int32, P, P)
+        _proto(lib, "sw_phase_partition", c_int32, P, P)
+        _proto(lib, "sw_phase_unpack", c_int32, P, P)
+        _proto(lib, "sw_phase_process", c_int32, P, P, P)
+        _proto(lib, "sw_registry_patch", c_int32, P, P, P, P, P, P, P, c_int64, P)
+        _proto(lib, "sw_pip_batch", c_int32, P, c_int64, P, P, c_int64, P, P)
+        _proto(lib, "sw_scan_u32", c_int32, P, c_int64, P, P, P, c_int64, P)
+        _proto(lib, "sw_abi_sizes", c_int32, P)
+        _gpu = lib
+        return lib
+
+
+def gpu_library_path() -> Path:
+    return LIB_DIR / "libswgpu.so"

@@ -1,0 +1,74 @@
+"""Columnar / fixed-width record layouts shared by the host runtime and the gfx950 kernels.
+
+These numpy dtypes mirror the C structs in ``csrc/include/swtypes.h`` and
+``csrc/include/swengine.h`` byte for byte (``tests/test_columnar.py`` checks
+them against ``sw_abi_sizes`` and field offsets).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# Event types (GDeviceEventType in the reference's device-event-model.proto).
+EV_MEASUREMENT = 0
+EV_LOCATION = 1
+EV_ALERT = 2
+EV_COMMAND_INVOCATION = 3
+EV_COMMAND_RESPONSE = 4
+EV_STATE_CHANGE = 5
+EV_REGISTRATION = 16
+EV_ACK = 17
+EV_STREAM_CREATE = 18
+EV_STREAM_DATA = 19
+EV_STREAM_DATA_REQUEST = 20
+EV_DECODE_ERROR = 255
+
+# Validation status (InboundPayloadProcessingLogic outcomes).
+ST_OK = 0
+ST_UNREGISTERED = 1
+ST_UNASSIGNED = 2
+ST_DUPLICATE = 3
+ST_DECODE_ERROR = 4
+ST_CONTROL = 5
+
+F_HAS_UPDATE_STATE = 0x1
+F_UPDATE_STATE = 0x2
+F_HAS_DATE = 0x4
+F_HAS_ELEVATION = 0x8
+
+EVENT_REC = np.dtype([
+    ("fp_lo", "<u8"), ("fp_hi", "<u8"), ("event_date", "<i8"), ("name_hash", "<u8"),
+    ("v0", "<f8"), ("v1", "<f8"), ("v2", "<f8"), ("alt_hash", "<u8"),
+    ("aux_off", "<u4"), ("aux2_off", "<u4"), ("aux_len", "<u2"), ("aux2_len", "<u2"),
+    ("etype", "u1"), ("flags", "u1"), ("src_rank", "u1"), ("level", "u1"),
+], align=True)
+assert EVENT_REC.itemsize == 80
+
+OUT_REC = np.dtype([
+    ("event_id", "<i8"), ("event_date", "<i8"), ("v0", "<f8"), ("v1", "<f8"),
+    ("assignment", "<i4"), ("device", "<i4"), ("name_id", "<i4"),
+    ("etype", "u1"), ("level", "u1"), ("status", "<u2"),
+], align=True)
+# C struct is aligned(16) -> sizeof 48
+OUT_REC_SIZE = 48
+OUT_REC = np.dtype({"names": list(OUT_REC.names), "formats": [OUT_REC.fields[n][0] for n in OUT_REC.names],
+                    "offsets": [OUT_REC.fields[n][1] for n in OUT_REC.names], "itemsize": OUT_REC_SIZE})
+
+NAME_REF = np.dtype([("hash", "<u8"), ("off", "<u4"), ("len", "<u2"), ("src_rank", "u1"), ("etype", "u1")])
+assert NAME_REF.itemsize == 16
+
+ZONE_TEST = np.dtype([("zone", "<i4"), ("condition", "<i4"), ("alert_name_id", "<i4"), ("level", "<i4")])
+
+# Stats slots (SW_STAT_* in swengine.h).
+STAT_NAMES = [
+    "messages", "events", "persisted", "unregistered", "unassigned", "duplicates", "decode_errors",
+    "control", "rule_alerts", "presence_events", "shuffle_overflow", "new_names",
+]
+
+# Alert levels (GAlertLevel) and sources.
+ALERT_LEVELS = ["Info", "Warning", "Error", "Critical"]
+
+EVENT_TYPE_NAMES = {
+    EV_MEASUREMENT: "Measurement", EV_LOCATION: "Location", EV_ALERT: "Alert",
+    EV_COMMAND_INVOCATION: "CommandInvocation", EV_COMMAND_RESPONSE: "CommandResponse",
+    EV_STATE_CHANGE: "StateChange",
+}

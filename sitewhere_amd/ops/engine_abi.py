@@ -1,0 +1,64 @@
+"""ctypes mirror of ``SwEngineArgs`` (csrc/include/swengine.h).
+
+Every field is 8 bytes; the order below must match the header exactly.
+``tests/test_columnar.py`` compares ``ctypes.sizeof(SwEngineArgs)`` with the
+library's own ``sizeof`` (``sw_abi_sizes``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+P = ctypes.c_void_p
+I = ctypes.c_int64
+U = ctypes.c_uint64
+
+FIELDS = [
+    # batch input
+    ("raw", P), ("msg_off", P), ("n_msgs", I), ("now_ms", I), ("rank", I), ("world", I), ("batch_seq", I),
+    # decode
+    ("msg_cnt", P), ("msg_evoff", P), ("scan_tmp", P), ("scan_tmp_len", I),
+    ("recs", P), ("rec_cap", I), ("n_recs", P),
+    ("seen_key", P), ("seen_mask", I), ("new_names", P), ("n_new_names", P), ("names_cap", I),
+    # shuffle
+    ("send", P), ("recv", P), ("shuf_cap", I), ("send_cnt", P), ("recv_cnt", P), ("part_tmp", P),
+    ("part_tmp_len", I), ("overflow", P),
+    # validated batch
+    ("work", P), ("n_work", P), ("status", P), ("ev_dev", P), ("ev_asg", P),
+    ("ok_idx", P), ("n_ok", P), ("rej_idx", P), ("n_rej", P), ("cmp_tmp", P),
+    # registry
+    ("reg_lo", P), ("reg_hi", P), ("reg_val", P), ("reg_mask", I),
+    ("dev_asg", P), ("dev_type", P),
+    ("asg_device", P), ("asg_customer", P), ("asg_area", P), ("asg_asset", P), ("asg_active", P), ("n_asg", I),
+    # dedup
+    ("dd_key", P), ("dd_seq", P), ("dd_mask", I), ("seq_base", P),
+    # names intern
+    ("nm_key", P), ("nm_id", P), ("nm_first", P), ("nm_mask", I), ("nm_counter", P),
+    # state
+    ("st_last", P), ("st_missing", P), ("st_loc_date", P), ("st_loc_eid", P),
+    ("ms_key", P), ("ms_date", P), ("ms_eid", P), ("ms_mask", I),
+    # store
+    ("store_cap", I), ("store_cursor", P), ("step_cursor0", P),
+    ("s_etype", P), ("s_level", P), ("s_date", P), ("s_recv", P), ("s_dev", P), ("s_asg", P),
+    ("s_cust", P), ("s_area", P), ("s_asset", P), ("s_name", P), ("s_v0", P), ("s_v1", P), ("s_v2", P),
+    ("s_alt", P), ("s_aux", P), ("s_batch", P),
+    # outbound
+    ("out", P), ("n_out", P),
+    # rules
+    ("zone_vtx", P), ("zone_off", P), ("zone_bbox", P), ("n_zones", I), ("tests", P), ("n_tests", I),
+    ("test_name_hash", P),
+    ("gen", P), ("gen_dev", P), ("gen_asg", P), ("n_gen", P), ("gen_cap", I),
+    # presence
+    ("presence_missing_ms", I), ("presence_name_hash", U),
+    # stats
+    ("stats", P),
+]
+
+
+class SwEngineArgs(ctypes.Structure):
+    _fields_ = FIELDS
+
+
+def abi_sizes(lib) -> dict:
+    buf = (ctypes.c_int64 * 8)()
+    lib.sw_abi_sizes(ctypes.cast(buf, ctypes.c_void_p))
+    return {"event_rec": buf[0], "out_rec": buf[1], "engine_args": buf[2], "name_ref": buf[3], "zone_test": buf[4]}

@@ -1,0 +1,56 @@
+"""Sizing of the inbound pipeline engine (HBM/host tables and batch capacities)."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+
+def pow2_at_least(n: int) -> int:
+    p = 1
+    while p < n:
+        p <<= 1
+    return p
+
+
+@dataclass
+class EngineConfig:
+    """Capacities of one engine shard (one tenant engine on one GPU / rank).
+
+    Defaults are sized for MI355X (288 GB HBM3E): the event store alone holds
+    2^27 events (~12 GB) so a shard keeps hours of hot events resident.
+    """
+
+    max_msgs: int = 1 << 20          # payloads per micro-batch
+    rec_cap: int = 0                 # decoded events per micro-batch (0 = 2 * max_msgs)
+    gen_cap: int = 1 << 16           # rule alerts + presence events per step
+    max_devices: int = 1 << 20
+    max_assignments: int = 1 << 20
+    store_cap: int = 1 << 27         # HBM event-store ring capacity (events)
+    dedup_slots: int = 1 << 22       # alternate-id window (slots; window = slots / 2)
+    name_slots: int = 1 << 16        # distinct measurement names / alert types
+    state_slots: int = 0             # (assignment, name) state map slots (0 = 4 * max_assignments)
+    names_cap: int = 4096            # new-name reports per step
+    shuffle_slack: float = 1.25      # per-destination slab = slack * rec_cap / world
+    presence_missing_ms: int = 8 * 3600 * 1000   # DevicePresenceManager default (8h)
+    presence_check_ms: int = 10 * 60 * 1000      # DevicePresenceManager default (10 min)
+    rank: int = 0
+    world: int = 1
+    extra: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        if self.rec_cap <= 0:
+            self.rec_cap = 2 * self.max_msgs
+        if self.state_slots <= 0:
+            self.state_slots = 4 * self.max_assignments
+        self.reg_slots = pow2_at_least(2 * self.max_devices)
+        self.dedup_slots = pow2_at_least(self.dedup_slots)
+        self.name_slots = pow2_at_least(self.name_slots)
+        self.state_slots = pow2_at_least(self.state_slots)
+        self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + 1024
+
+    @classmethod
+    def small(cls, **kw):
+        """Test-sized configuration (fits easily on CPU)."""
+        base = dict(max_msgs=4096, gen_cap=4096, max_devices=4096, max_assignments=4096, store_cap=1 << 16,
+                    dedup_slots=1 << 14, name_slots=1 << 10, names_cap=1024)
+        base.update(kw)
+        return cls(**base)

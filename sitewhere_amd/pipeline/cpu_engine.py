@@ -1,0 +1,297 @@
+"""CPU implementation of the inbound pipeline (reference oracle + CPU fallback).
+
+Implements exactly the stage semantics of ``csrc/hip/swgpu.hip`` with numpy and
+the shared C++ decoder, one micro-batch at a time.  It is the parity oracle for
+the GPU engine (tests/test_gpu_engine.py) and runs the multi-rank path over the
+``gloo`` backend (tests/test_distributed_cpu.py), so the owner-partition +
+all-to-all protocol is covered without GPUs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..models.columnar import (EVENT_REC, OUT_REC, EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE,
+                               EV_DECODE_ERROR, ST_OK, ST_UNREGISTERED, ST_UNASSIGNED, ST_DUPLICATE,
+                               ST_DECODE_ERROR, ST_CONTROL, STAT_NAMES)
+from .config import EngineConfig
+from .engine_base import EngineBase, StepResult
+from .fleet import cpu_decode
+
+STORE_COLS = {
+    "etype": np.uint8, "level": np.uint8, "date": np.int64, "recv": np.int64, "dev": np.int32, "asg": np.int32,
+    "cust": np.int32, "area": np.int32, "asset": np.int32, "name": np.uint64, "v0": np.float64, "v1": np.float64,
+    "v2": np.float64, "alt": np.uint64, "aux": np.uint64, "batch": np.int32,
+}
+
+
+def pip(vtx: np.ndarray, x: float, y: float) -> bool:
+    """Even-odd crossing-number point-in-polygon (same predicate as the kernel)."""
+    inside = False
+    n = len(vtx)
+    j = n - 1
+    for i in range(n):
+        xi, yi = vtx[i]
+        xj, yj = vtx[j]
+        if ((yi > y) != (yj > y)) and (x < (xj - xi) * (y - yi) / (yj - yi) + xi):
+            inside = not inside
+        j = i
+    return inside
+
+
+class CpuInboundEngine(EngineBase):
+    """Numpy engine shard; same interface as :class:`GpuInboundEngine`."""
+
+    def __init__(self, cfg: EngineConfig, group=None):
+        super().__init__(cfg)
+        self.group = group
+        self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
+        self.cursor = 0
+        self.seq_base = 0
+        self.dedup: dict[int, int] = {}
+        self.intern: dict[int, int] = {}
+        self.st_last = np.zeros(cfg.max_assignments, np.uint64)
+        self.st_missing = np.zeros(cfg.max_assignments, np.uint64)
+        self.st_loc_date = np.zeros(cfg.max_assignments, np.uint64)
+        self.st_loc_eid = np.zeros(cfg.max_assignments, np.int64)   # eid + 1, 0 = none
+        self.ms: dict[tuple, list] = {}                               # (asg, name_id, kind) -> [date, eid+1]
+        self.stats = np.zeros(16, np.uint64)
+        self._seen: set[int] = set()
+
+    # ------------------------------------------------------------------ stages
+    def _shuffle(self, recs: np.ndarray) -> np.ndarray:
+        if self.world == 1:
+            return recs
+        import torch
+        import torch.distributed as dist
+
+        owner = np.where(recs["etype"] >= 16, self.rank, (recs["fp_hi"] >> np.uint64(32)) % np.uint64(self.world))
+        cap = self.cfg.shuf_cap
+        send = np.zeros((self.world, cap), EVENT_REC)
+        cnt = np.zeros(self.world, np.int64)
+        for o in range(self.world):
+            sel = recs[owner == o]
+            k = min(len(sel), cap)
+            self.stats[10] += len(sel) - k
+            send[o, :k] = sel[:k]
+            cnt[o] = k
+        send_t = torch.from_numpy(send.view(np.uint8).reshape(-1).copy())
+        recv_t = torch.empty_like(send_t)
+        cnt_t = torch.from_numpy(cnt)
+        rcnt_t = torch.empty_like(cnt_t)
+        dist.all_to_all_single(rcnt_t, cnt_t, group=self.group)
+        dist.all_to_all_single(recv_t, send_t, group=self.group)
+        recv = recv_t.numpy().view(EVENT_REC).reshape(self.world, cap)
+        rc = rcnt_t.numpy()
+        return np.concatenate([recv[q, :rc[q]] for q in range(self.world)])
+
+    def _lookup(self, recs):
+        n = len(recs)
+        status = np.zeros(n, np.uint8)
+        dev = np.full(n, -1, np.int32)
+        asg = np.full(n, -1, np.int32)
+        for i in range(n):
+            r = recs[i]
+            et = int(r["etype"])
+            if et == EV_DECODE_ERROR:
+                status[i] = ST_DECODE_ERROR
+                continue
+            d = self.lookup_device(int(r["fp_lo"]), int(r["fp_hi"]))
+            dev[i] = d
+            if et >= 16:
+                status[i] = ST_CONTROL
+            elif d < 0:
+                status[i] = ST_UNREGISTERED
+            else:
+                a = int(self.dev_asg[d])
+                asg[i] = a
+                status[i] = ST_OK if (a >= 0 and self.asg_active[a]) else ST_UNASSIGNED
+        return status, dev, asg
+
+    def _dedup(self, recs, status):
+        seen_now: dict[int, int] = {}
+        for i in range(len(recs)):
+            h = int(recs[i]["alt_hash"])
+            if h == 0 or status[i] != ST_OK:
+                continue
+            seq = self.seq_base + i
+            if h in self.dedup and self.dedup[h] < self.seq_base:
+                status[i] = ST_DUPLICATE
+            elif h in seen_now:
+                status[i] = ST_DUPLICATE
+            else:
+                seen_now[h] = seq
+        self.dedup.update(seen_now)
+
+    def _intern_id(self, h: int) -> int:
+        if h not in self.intern:
+            self.intern[h] = len(self.intern)
+        return self.intern[h]
+
+    def _persist(self, recs, dev, asg, now_ms, out_rows):
+        for j in range(len(recs)):
+            r = recs[j]
+            seq = self.cursor + j
+            row = seq % self.cfg.store_cap
+            eid = seq * self.world + self.rank
+            a = int(asg[j])
+            s = self.store
+            s["etype"][row] = r["etype"]
+            s["level"][row] = r["level"]
+            s["date"][row] = r["event_date"]
+            s["recv"][row] = now_ms
+            s["dev"][row] = dev[j]
+            s["asg"][row] = a
+            s["cust"][row] = self.asg_customer[a]
+            s["area"][row] = self.asg_area[a]
+            s["asset"][row] = self.asg_asset[a]
+            s["name"][row] = r["name_hash"]
+            s["v0"][row] = r["v0"]
+            s["v1"][row] = r["v1"]
+            s["v2"][row] = r["v2"]
+            s["alt"][row] = r["alt_hash"]
+            s["aux"][row] = (int(r["src_rank"]) << 48) | (int(r["aux_len"]) << 32) | int(r["aux_off"])
+            s["batch"][row] = self.batch_seq
+            h = int(r["name_hash"])
+            nid = self.intern.get(h, -1) if h else -1
+            out_rows.append((eid, int(r["event_date"]), float(r["v0"]), float(r["v1"]), a, int(dev[j]), nid,
+                             int(r["etype"]), int(r["level"]), 0))
+
+    def _state(self, recs, asg, now_ms):
+        base = self.cursor
+        for j in range(len(recs)):
+            r = recs[j]
+            et = int(r["etype"])
+            if et not in (EV_MEASUREMENT, EV_LOCATION, EV_ALERT):
+                continue
+            a = int(asg[j])
+            self.st_last[a] = max(int(self.st_last[a]), now_ms)
+            self.st_missing[a] = 0
+            d = int(r["event_date"])
+            eid1 = (base + j) * self.world + self.rank + 1
+            if et == EV_LOCATION:
+                if d > int(self.st_loc_date[a]):
+                    self.st_loc_date[a] = d
+                    self.st_loc_eid[a] = eid1
+                elif d == int(self.st_loc_date[a]):
+                    self.st_loc_eid[a] = max(int(self.st_loc_eid[a]), eid1)
+            elif int(r["name_hash"]):
+                key = (a, self.intern[int(r["name_hash"])], 1 if et == EV_ALERT else 0)
+                cur = self.ms.get(key)
+                if cur is None or d > cur[0]:
+                    self.ms[key] = [d, eid1]
+                elif d == cur[0]:
+                    cur[1] = max(cur[1], eid1)
+
+    # ------------------------------------------------------------------ step
+    def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
+        n_msgs = len(offs) - 1
+        recs = cpu_decode(raw, offs, now_ms, self.rank, cap=self.cfg.rec_cap)
+        # new-name capture on the source rank
+        refs = []
+        for r in recs:
+            h = int(r["name_hash"])
+            if h and r["etype"] < 16 and h not in self._seen:
+                self._seen.add(h)
+                refs.append((h, int(r["aux_off"]), int(r["aux_len"]), int(r["src_rank"]), int(r["etype"])))
+        from ..models.columnar import NAME_REF
+        new = self.learn_names(np.array(refs, NAME_REF), raw) if refs else {}
+        work = self._shuffle(recs)
+        status, dev, asg = self._lookup(work)
+        self._dedup(work, status)
+        ok = np.nonzero(status == ST_OK)[0]
+        rej = np.nonzero(status != ST_OK)[0]
+        for i in ok:
+            h = int(work[i]["name_hash"])
+            if h:
+                self._intern_id(h)
+        out_rows: list = []
+        self._persist(work[ok], dev[ok], asg[ok], now_ms, out_rows)
+        self._state(work[ok], asg[ok], now_ms)
+        self.cursor += len(ok)
+        # rules on persisted locations
+        gen, gen_dev, gen_asg = [], [], []
+        if self.tests:
+            vtx, zoff, _, tests, hashes = self.zone_arrays()
+            polys = [vtx.reshape(-1, 2)[zoff[z]:zoff[z + 1]] for z in range(len(zoff) - 1)]
+            for o in out_rows:
+                if o[7] != EV_LOCATION:
+                    continue
+                for t, zt in enumerate(tests):
+                    inside = pip(polys[int(zt["zone"])], o[2], o[3])
+                    if (int(zt["condition"]) == 0) == inside:
+                        if len(gen) < self.cfg.gen_cap:
+                            gen.append((0, 0, now_ms, int(hashes[t]), 0.0, 0.0, 0.0, 0, t, 0, 0, 0, EV_ALERT, 0,
+                                        self.rank, int(zt["level"])))
+                            gen_dev.append(o[5])
+                            gen_asg.append(o[4])
+        n_rule = len(gen)
+        do_presence = self.presence_due(now_ms) if presence is None else presence
+        if do_presence and self.cfg.presence_missing_ms > 0:
+            limit = now_ms - self.cfg.presence_missing_ms
+            miss = np.nonzero((self.asg_active[:self.n_assignments] > 0) & (self.st_last[:self.n_assignments] > 0) &
+                              (self.st_last[:self.n_assignments] < np.uint64(max(limit, 0))) &
+                              (self.st_missing[:self.n_assignments] == 0))[0]
+            for a in miss:
+                self.st_missing[a] = now_ms
+                if len(gen) < self.cfg.gen_cap:
+                    gen.append((0, 0, now_ms, self.presence_hash, 0.0, 0.0, 0.0, 0, 0, 0, 0, 0, EV_STATE_CHANGE, 0,
+                                self.rank, 0))
+                    gen_dev.append(int(self.asg_device[a]))
+                    gen_asg.append(int(a))
+        if gen:
+            g = np.array(gen, EVENT_REC)
+            for r in g:
+                if int(r["name_hash"]):
+                    self._intern_id(int(r["name_hash"]))
+            gd = np.asarray(gen_dev, np.int32)
+            ga = np.asarray(gen_asg, np.int32)
+            self._persist(g, gd, ga, now_ms, out_rows)
+            self._state(g, ga, now_ms)
+            self.cursor += len(g)
+        # bookkeeping
+        self.seq_base += len(work)
+        st = self.stats
+        st[0] += n_msgs
+        st[1] += len(work)
+        st[2] += len(out_rows)
+        for code, slot in ((ST_UNREGISTERED, 3), (ST_UNASSIGNED, 4), (ST_DUPLICATE, 5), (ST_DECODE_ERROR, 6),
+                           (ST_CONTROL, 7)):
+            st[slot] += int((status == code).sum())
+        st[8] += n_rule
+        st[9] += len(gen) - n_rule
+        st[11] += len(new)
+        self.batch_seq += 1
+        return StepResult(n_msgs=n_msgs, n_events=len(work), n_persisted=len(out_rows),
+                          out=np.array(out_rows, OUT_REC), rejects=work[rej], reject_status=status[rej],
+                          new_names=new)
+
+    # ------------------------------------------------------------------ queries
+    def stats_dict(self) -> dict:  # type: ignore[override]
+        return {n: int(self.stats[i]) for i, n in enumerate(STAT_NAMES)}
+
+    def device_state(self, asg: int) -> dict:
+        mx = {}
+        al = {}
+        inv = {v: k for k, v in self.intern.items()}
+        for (a, nid, kind), (d, e1) in self.ms.items():
+            if a != asg:
+                continue
+            name = self.names.get(inv[nid], str(inv[nid]))
+            (al if kind else mx)[name] = (e1 - 1, d)
+        return {
+            "assignment": asg,
+            "last_interaction": int(self.st_last[asg]),
+            "presence_missing": int(self.st_missing[asg]),
+            "last_location": (int(self.st_loc_eid[asg]) - 1, int(self.st_loc_date[asg])) if self.st_loc_eid[asg] else None,
+            "measurements": mx,
+            "alerts": al,
+        }
+
+    def store_rows(self):
+        n = min(self.cursor, self.cfg.store_cap)
+        if self.cursor <= self.cfg.store_cap:
+            idx = np.arange(n)
+        else:
+            start = self.cursor % self.cfg.store_cap
+            idx = (np.arange(n) + start) % self.cfg.store_cap
+        return {k: v[idx] for k, v in self.store.items()}, (np.arange(self.cursor - n, self.cursor) * self.world + self.rank)

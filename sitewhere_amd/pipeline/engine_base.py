@@ -1,0 +1,222 @@
+"""Host-side state shared by the GPU and CPU inbound-pipeline engines.
+
+An *engine shard* owns one tenant's hot data on one rank: the device registry
+(token fingerprint -> device index), the active assignment and its context
+(customer / area / asset), the HBM event store, device state, the dedup window,
+the zone-test rules and the presence settings.  The control plane (device
+management service) pushes registry / assignment / zone changes here; the data
+plane (``step``) consumes raw payload batches.
+
+Reference counterparts: the per-tenant engines of service-inbound-processing,
+service-event-management, service-device-state and service-rule-processing
+(``*TenantEngine.java``), collapsed into one fused micro-batch pipeline.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .._native import native
+from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, STAT_NAMES
+from .config import EngineConfig
+from .fleet import hash64
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+@dataclass
+class Zone:
+    """A polygon zone; vertices are (latitude, longitude) pairs (reference IZone bounds)."""
+    token: str
+    vertices: list
+
+
+@dataclass
+class ZoneTest:
+    """Zone-test rule (reference: service-rule-processing/.../geospatial/ZoneTest.java)."""
+    zone_token: str
+    condition: str = "inside"       # "inside" | "outside" (ZoneContainment)
+    alert_type: str = "zone.alert"
+    alert_level: int = 1            # Info=0, Warning=1, Error=2, Critical=3
+    alert_message: str = ""
+
+
+@dataclass
+class StepResult:
+    """What one micro-batch produced (host copies; filled by ``finalize``)."""
+    n_msgs: int = 0
+    n_events: int = 0
+    n_persisted: int = 0
+    out: np.ndarray | None = None          # OUT_REC rows (persisted, enriched)
+    rejects: np.ndarray | None = None      # EVENT_REC rows not persisted
+    reject_status: np.ndarray | None = None
+    new_names: dict = field(default_factory=dict)
+
+
+class EngineBase:
+    """Registry / assignment / zone mirrors + names dictionary (host side)."""
+
+    PRESENCE = "presence"
+
+    def __init__(self, cfg: EngineConfig):
+        self.cfg = cfg
+        self.rank, self.world = cfg.rank, cfg.world
+        self._lock = threading.RLock()
+        # registry mirror (exact 128-bit keys)
+        self.reg_lo = np.zeros(cfg.reg_slots, np.uint64)
+        self.reg_hi = np.zeros(cfg.reg_slots, np.uint64)
+        self.reg_val = np.full(cfg.reg_slots, -1, np.int32)
+        self.n_devices = 0
+        self.dev_asg = np.full(cfg.max_devices, -1, np.int32)
+        self.dev_type = np.full(cfg.max_devices, -1, np.int32)
+        self.asg_device = np.full(cfg.max_assignments, -1, np.int32)
+        self.asg_customer = np.full(cfg.max_assignments, -1, np.int32)
+        self.asg_area = np.full(cfg.max_assignments, -1, np.int32)
+        self.asg_asset = np.full(cfg.max_assignments, -1, np.int32)
+        self.asg_active = np.zeros(cfg.max_assignments, np.uint8)
+        self.n_assignments = 0
+        # names: global hash -> string dictionary
+        self.names: dict[int, str] = {}
+        self.presence_hash = hash64(self.PRESENCE)
+        self.names[self.presence_hash] = self.PRESENCE
+        # zones
+        self.zones: list[Zone] = []
+        self.tests: list[ZoneTest] = []
+        self.batch_seq = 0
+        self.presence_enabled = True
+        self._last_presence_check = None
+
+    # ------------------------------------------------------------------ registry
+    def _dirty_registry(self, slots: np.ndarray):
+        """Hook: GPU engine pushes changed slots to HBM."""
+
+    def _dirty_assignments(self, idx: np.ndarray):
+        """Hook: GPU engine pushes changed assignment rows."""
+
+    def _dirty_devices(self, idx: np.ndarray):
+        """Hook: GPU engine pushes changed device rows."""
+
+    def register_devices(self, fp_lo, fp_hi, dev_idx=None, dev_type=None) -> np.ndarray:
+        """Upsert devices by token fingerprint; returns device indices."""
+        fp_lo = np.ascontiguousarray(fp_lo, np.uint64)
+        fp_hi = np.ascontiguousarray(fp_hi, np.uint64)
+        n = len(fp_lo)
+        with self._lock:
+            if dev_idx is None:
+                dev_idx = np.arange(self.n_devices, self.n_devices + n, dtype=np.int32)
+            dev_idx = np.ascontiguousarray(dev_idx, np.int32)
+            if n and int(dev_idx.max()) >= self.cfg.max_devices:
+                raise ValueError("device capacity exceeded (EngineConfig.max_devices)")
+            slots = np.empty(n, np.int64)
+            failed = native().sw_reg_build(_p(self.reg_lo), _p(self.reg_hi), _p(self.reg_val), self.cfg.reg_slots - 1,
+                                           _p(fp_lo), _p(fp_hi), _p(dev_idx), n, _p(slots))
+            if failed:
+                raise RuntimeError("registry table full")
+            self.n_devices = max(self.n_devices, int(dev_idx.max()) + 1 if n else 0)
+            if dev_type is not None:
+                self.dev_type[dev_idx] = np.asarray(dev_type, np.int32)
+                self._dirty_devices(dev_idx)
+            self._dirty_registry(slots)
+            return dev_idx
+
+    def lookup_device(self, fp_lo: int, fp_hi: int) -> int:
+        return int(native().sw_reg_find(_p(self.reg_lo), _p(self.reg_hi), _p(self.reg_val), self.cfg.reg_slots - 1,
+                                        fp_lo, fp_hi))
+
+    def set_assignments(self, asg_idx, dev_idx, customer=None, area=None, asset=None, active=None):
+        """Create/update assignments and make them the device's active assignment when active."""
+        asg_idx = np.atleast_1d(np.asarray(asg_idx, np.int32))
+        dev_idx = np.atleast_1d(np.asarray(dev_idx, np.int32))
+        n = len(asg_idx)
+        if n and int(asg_idx.max()) >= self.cfg.max_assignments:
+            raise ValueError("assignment capacity exceeded (EngineConfig.max_assignments)")
+
+        def col(v, fill):
+            return np.full(n, fill, np.int32) if v is None else np.broadcast_to(np.asarray(v, np.int32), (n,))
+
+        act = np.ones(n, np.uint8) if active is None else np.broadcast_to(np.asarray(active, np.uint8), (n,))
+        with self._lock:
+            self.asg_device[asg_idx] = dev_idx
+            self.asg_customer[asg_idx] = col(customer, -1)
+            self.asg_area[asg_idx] = col(area, -1)
+            self.asg_asset[asg_idx] = col(asset, -1)
+            self.asg_active[asg_idx] = act
+            on = act.astype(bool)
+            self.dev_asg[dev_idx[on]] = asg_idx[on]
+            # ending an assignment releases the device
+            off_dev = dev_idx[~on]
+            cur = self.dev_asg[off_dev]
+            self.dev_asg[off_dev] = np.where(cur == asg_idx[~on], -1, cur)
+            self.n_assignments = max(self.n_assignments, int(asg_idx.max()) + 1 if n else 0)
+            self._dirty_assignments(asg_idx)
+            self._dirty_devices(dev_idx)
+
+    # ------------------------------------------------------------------ zones / rules
+    def set_zone_rules(self, zones: list[Zone], tests: list[ZoneTest]):
+        with self._lock:
+            self.zones = list(zones)
+            self.tests = list(tests)
+            for t in tests:
+                self.names[hash64(t.alert_type)] = t.alert_type
+            self._zones_changed()
+
+    def _zones_changed(self):
+        pass
+
+    def zone_arrays(self):
+        """Flattened zone polygons: vtx [2*V] f64, off [Z+1] i32, bbox [4*Z] f64, tests ZONE_TEST[T]."""
+        from ..models.columnar import ZONE_TEST
+
+        idx = {z.token: i for i, z in enumerate(self.zones)}
+        off = [0]
+        vtx = []
+        bbox = []
+        for z in self.zones:
+            v = np.asarray(z.vertices, np.float64).reshape(-1, 2)
+            vtx.append(v.ravel())
+            off.append(off[-1] + len(v))
+            bbox.extend([v[:, 0].min(), v[:, 1].min(), v[:, 0].max(), v[:, 1].max()])
+        tests = np.zeros(len(self.tests), ZONE_TEST)
+        hashes = np.zeros(len(self.tests), np.uint64)
+        for i, t in enumerate(self.tests):
+            if t.zone_token not in idx:
+                raise KeyError(f"zone test references unknown zone {t.zone_token!r}")
+            tests[i] = (idx[t.zone_token], 0 if t.condition == "inside" else 1, -1, int(t.alert_level))
+            hashes[i] = hash64(t.alert_type)
+        return (np.concatenate(vtx) if vtx else np.zeros(2, np.float64), np.asarray(off, np.int32),
+                np.asarray(bbox if bbox else [0.0] * 4, np.float64), tests, hashes)
+
+    # ------------------------------------------------------------------ names
+    def learn_names(self, refs: np.ndarray, raw: np.ndarray):
+        """Record strings for newly seen name/type hashes (from this rank's raw batch)."""
+        new = {}
+        for r in refs:
+            h = int(r["hash"])
+            if h not in self.names:
+                s = bytes(raw[int(r["off"]):int(r["off"]) + int(r["len"])]).decode("utf-8", "replace")
+                self.names[h] = s
+                new[h] = s
+        return new
+
+    def name_of(self, h: int) -> str | None:
+        return self.names.get(int(h))
+
+    def presence_due(self, now_ms: int) -> bool:
+        if not self.presence_enabled or self.cfg.presence_missing_ms <= 0:
+            return False
+        if self._last_presence_check is None or now_ms - self._last_presence_check >= self.cfg.presence_check_ms:
+            self._last_presence_check = now_ms
+            return True
+        return False
+
+    @staticmethod
+    def stats_dict(arr) -> dict:
+        return {n: int(arr[i]) for i, n in enumerate(STAT_NAMES)}
+
+
+_ = (ctypes, EVENT_REC, OUT_REC, NAME_REF)

@@ -1,0 +1,133 @@
+"""Synthetic device fleets: tokens, fingerprints and protobuf wire payloads.
+
+Thin numpy wrappers over ``libswnative`` (``sw_gen_payloads`` / ``sw_gen_tokens`` /
+``sw_fingerprint_batch``).  Payloads use the reference device protocol
+(``sitewhere-communication/src/main/proto/sitewhere.proto``): a delimited
+``SiteWhere.Header`` followed by a delimited body message.  Used by bench.py,
+the tests and the load-generator edge (the reference's equivalents are the
+manual harnesses ``MqttTests.java`` / ``SiteWhereClientTester.java``).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from .._native import native
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def gen_tokens(prefix: str, first: int, n: int):
+    """Device tokens ``<prefix><index:010d>`` as (heap uint8, offsets int64[n+1])."""
+    lib = native()
+    cap = n * (len(prefix.encode()) + 10) + 16
+    heap = np.empty(cap, np.uint8)
+    offs = np.empty(n + 1, np.int64)
+    r = lib.sw_gen_tokens(prefix.encode(), first, n, _ptr(heap), cap, _ptr(offs))
+    if r < 0:
+        raise RuntimeError("token heap overflow")
+    return heap[:r], offs
+
+
+def token_list(prefix: str, first: int, n: int):
+    heap, offs = gen_tokens(prefix, first, n)
+    b = heap.tobytes()
+    return [b[offs[i]:offs[i + 1]].decode() for i in range(n)]
+
+
+def fingerprints(heap: np.ndarray, offs: np.ndarray):
+    """128-bit device-token fingerprints (same function the GPU decoder uses)."""
+    lib = native()
+    n = len(offs) - 1
+    lo = np.empty(n, np.uint64)
+    hi = np.empty(n, np.uint64)
+    heap = np.ascontiguousarray(heap, np.uint8)
+    offs = np.ascontiguousarray(offs, np.int64)
+    lib.sw_fingerprint_batch(_ptr(heap), _ptr(offs), n, _ptr(lo), _ptr(hi))
+    return lo, hi
+
+
+def fingerprint_str(s: str):
+    b = np.frombuffer(s.encode(), np.uint8)
+    lo, hi = fingerprints(b, np.array([0, len(b)], np.int64))
+    return int(lo[0]), int(hi[0])
+
+
+def hash64_strs(strs):
+    lib = native()
+    enc = [s.encode() for s in strs]
+    offs = np.zeros(len(enc) + 1, np.int64)
+    offs[1:] = np.cumsum([len(e) for e in enc])
+    heap = np.frombuffer(b"".join(enc) or b"\0", np.uint8).copy()
+    out = np.empty(len(enc), np.uint64)
+    lib.sw_hash64_batch(_ptr(heap), _ptr(offs), len(enc), _ptr(out))
+    return out
+
+
+def hash64(s: str) -> int:
+    return int(hash64_strs([s])[0])
+
+
+@dataclass
+class FleetSpec:
+    prefix: str = "dev-"
+    n_devices: int = 1 << 20
+    p_location: float = 0.25
+    p_alert: float = 0.05
+    p_unregistered: float = 0.0
+    mx_per_msg: int = 1
+    n_names: int = 16
+    with_alternate_id: bool = False
+    lat0: float = 33.75
+    lon0: float = -84.39
+    span_deg: float = 0.5
+
+
+def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndarray | None = None,
+                 offs: np.ndarray | None = None):
+    """Generate ``n_msgs`` encoded payloads. Returns (raw uint8[nbytes], offs uint32[n+1])."""
+    lib = native()
+    per = 48 + len(spec.prefix) + 10 + spec.mx_per_msg * 32 + (40 if spec.with_alternate_id else 0)
+    cap = n_msgs * per + 64
+    if out is None or out.nbytes < cap:
+        out = np.empty(cap, np.uint8)
+    if offs is None or offs.size < n_msgs + 1:
+        offs = np.empty(n_msgs + 1, np.uint32)
+    r = lib.sw_gen_payloads(n_msgs, spec.prefix.encode(), spec.n_devices, spec.p_location, spec.p_alert,
+                            spec.p_unregistered, spec.mx_per_msg, spec.n_names, ts0, seed,
+                            1 if spec.with_alternate_id else 0, spec.lat0, spec.lon0, spec.span_deg,
+                            _ptr(out), out.nbytes, _ptr(offs))
+    if r < 0:
+        raise RuntimeError(f"payload buffer too small (need {-r})")
+    return out[:r], offs[:n_msgs + 1]
+
+
+def cpu_decode(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, cap: int | None = None,
+               threads: int = 4):
+    """Decode a raw batch on the CPU with the shared decoder; returns an EVENT_REC array."""
+    from ..models.columnar import EVENT_REC
+
+    lib = native()
+    n_msgs = len(offs) - 1
+    if cap is None:
+        cap = max(16, n_msgs * 4)
+    out = np.zeros(cap, EVENT_REC)
+    raw = np.ascontiguousarray(raw, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint32)
+    n = lib.sw_cpu_decode(_ptr(raw) if raw.size else 0, _ptr(offs), n_msgs, now_ms, rank, _ptr(out), cap, threads)
+    return out[:n]
+
+
+def pack_messages(messages):
+    """Concatenate a list of payload byte strings into (raw, offs)."""
+    offs = np.zeros(len(messages) + 1, np.uint32)
+    offs[1:] = np.cumsum([len(m) for m in messages])
+    raw = np.frombuffer(b"".join(messages) + b"\0" * 64, np.uint8).copy()
+    return raw, offs
+
+
+_ = ctypes  # keep import for type users

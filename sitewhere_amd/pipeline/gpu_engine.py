@@ -1,0 +1,425 @@
+"""GPU inbound-pipeline engine shard (MI355X / gfx950).
+
+Owns every hot table of one tenant shard in HBM and drives the kernels of
+``csrc/hip/swgpu.hip`` through ``libswgpu.so``:
+
+    H2D(raw batch)  ->  decode  ->  [owner partition -> RCCL all_to_all_single -> unpack]
+                    ->  validate + dedup + persist/enrich + state + rules + presence
+                    ->  D2H(outbound records)
+
+``step_async`` only enqueues work on the current HIP stream (no host sync, so a
+step can be captured into a hipGraph); :class:`PipelinedRunner` overlaps the
+H2D copy of batch k+1 and the D2H copy of batch k-1 with the compute of batch k
+on three streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+
+import numpy as np
+import torch
+
+from .._native import gpu as gpu_lib
+from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE
+from ..ops.engine_abi import SwEngineArgs
+from .config import EngineConfig
+from .engine_base import EngineBase, StepResult
+
+_ALIGN = 64
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+class GpuInboundEngine(EngineBase):
+    def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", group=None):
+        super().__init__(cfg)
+        self.lib = gpu_lib()
+        self.device = torch.device(device)
+        self.group = group
+        d = self.device
+        c = cfg
+        i32, i64, u8 = torch.int32, torch.int64, torch.uint8
+
+        def z(n, dt):
+            return torch.zeros(int(n), dtype=dt, device=d)
+
+        def full(n, v, dt):
+            return torch.full((int(n),), v, dtype=dt, device=d)
+
+        tile = 1024
+        ntiles = (c.rec_cap + tile - 1) // tile
+        mtiles = (c.max_msgs + tile - 1) // tile
+        scan_tmp = max(ntiles * 2 * max(1, c.world), mtiles, 2 * ntiles) + 64
+        self.t = t = {}
+        # decode
+        t["msg_cnt"] = z(c.max_msgs + 1, i32)
+        t["msg_evoff"] = z(c.max_msgs + 1, i32)
+        t["scan_tmp"] = z(scan_tmp, i32)
+        t["recs"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
+        t["seen_key"] = z(c.name_slots, i64)
+        t["new_names"] = z(c.names_cap * NAME_REF.itemsize, u8)
+        t["scalars"] = z(64, i32)  # n_recs, n_new_names, overflow, n_work, n_ok, n_rej, n_gen, n_out, n_rule
+        # shuffle
+        if c.world > 1:
+            t["send"] = z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8)
+            t["recv"] = z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8)
+            t["send_cnt"] = z(c.world, i32)
+            t["recv_cnt"] = z(c.world, i32)
+            t["part_tmp"] = z(2 * c.world * ntiles + 64, i32)
+            t["work"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
+        # validated
+        t["status"] = z(c.rec_cap, u8)
+        t["ev_dev"] = z(c.rec_cap, i32)
+        t["ev_asg"] = z(c.rec_cap, i32)
+        t["ok_idx"] = z(c.rec_cap, i32)
+        t["rej_idx"] = z(c.rec_cap, i32)
+        t["cmp_tmp"] = z(4 * ntiles + 64, i32)
+        # registry + assignment tables
+        t["reg_lo"] = z(c.reg_slots, i64)
+        t["reg_hi"] = z(c.reg_slots, i64)
+        t["reg_val"] = full(c.reg_slots, -1, i32)
+        t["dev_asg"] = full(c.max_devices, -1, i32)
+        t["dev_type"] = full(c.max_devices, -1, i32)
+        for k in ("asg_device", "asg_customer", "asg_area", "asg_asset"):
+            t[k] = full(c.max_assignments, -1, i32)
+        t["asg_active"] = z(c.max_assignments, u8)
+        # dedup window
+        t["dd_key"] = z(c.dedup_slots, i64)
+        t["dd_seq"] = full(c.dedup_slots, -1, i64)
+        t["seq_base"] = z(1, i64)
+        # names intern
+        t["nm_key"] = z(c.name_slots, i64)
+        t["nm_id"] = full(c.name_slots, -1, i32)
+        t["nm_first"] = full(c.name_slots, 0x7FFFFFFF, i32)
+        t["nm_counter"] = z(1, i32)
+        # device state
+        t["st_last"] = z(c.max_assignments, i64)
+        t["st_missing"] = z(c.max_assignments, i64)
+        t["st_loc_date"] = z(c.max_assignments, i64)
+        t["st_loc_eid"] = z(c.max_assignments, i64)
+        t["ms_key"] = z(c.state_slots, i64)
+        t["ms_date"] = z(c.state_slots, i64)
+        t["ms_eid"] = z(c.state_slots, i64)
+        # event store (SoA ring)
+        sc = c.store_cap
+        t["cursor"] = z(2, i64)  # [store_cursor, step_cursor0]
+        self.store = {
+            "etype": z(sc, u8), "level": z(sc, u8), "date": z(sc, i64), "recv": z(sc, i64), "dev": z(sc, i32),
+            "asg": z(sc, i32), "cust": z(sc, i32), "area": z(sc, i32), "asset": z(sc, i32), "name": z(sc, i64),
+            "v0": z(sc, torch.float64), "v1": z(sc, torch.float64), "v2": z(sc, torch.float64), "alt": z(sc, i64),
+            "aux": z(sc, i64), "batch": z(sc, i32),
+        }
+        # outbound (double-buffered for the pipelined runner)
+        out_cap = c.rec_cap + c.gen_cap
+        self.out_cap = out_cap
+        t["out0"] = z(out_cap * OUT_REC_SIZE, u8)
+        t["out1"] = z(out_cap * OUT_REC_SIZE, u8)
+        # rules
+        t["gen"] = z(c.gen_cap * EVENT_REC.itemsize, u8)
+        t["gen_dev"] = z(c.gen_cap, i32)
+        t["gen_asg"] = z(c.gen_cap, i32)
+        t["stats"] = z(16, i64)
+        self._set_zone_tensors()
+        self.args = a = SwEngineArgs()
+        sc_ptr = _ptr(t["scalars"])
+        S = lambda k: sc_ptr + 4 * k  # noqa: E731
+        a.rank, a.world = c.rank, c.world
+        a.msg_cnt, a.msg_evoff = _ptr(t["msg_cnt"]), _ptr(t["msg_evoff"])
+        a.scan_tmp, a.scan_tmp_len = _ptr(t["scan_tmp"]), scan_tmp
+        a.recs, a.rec_cap, a.n_recs = _ptr(t["recs"]), c.rec_cap, S(0)
+        a.seen_key, a.seen_mask = _ptr(t["seen_key"]), c.name_slots - 1
+        a.new_names, a.n_new_names, a.names_cap = _ptr(t["new_names"]), S(1), c.names_cap
+        a.overflow = S(2)
+        if c.world > 1:
+            a.send, a.recv, a.shuf_cap = _ptr(t["send"]), _ptr(t["recv"]), c.shuf_cap
+            a.send_cnt, a.recv_cnt = _ptr(t["send_cnt"]), _ptr(t["recv_cnt"])
+            a.part_tmp, a.part_tmp_len = _ptr(t["part_tmp"]), t["part_tmp"].numel() // 2
+            a.work = _ptr(t["work"])
+        else:
+            a.work = a.recs
+        a.n_work = S(3)
+        a.status, a.ev_dev, a.ev_asg = _ptr(t["status"]), _ptr(t["ev_dev"]), _ptr(t["ev_asg"])
+        a.ok_idx, a.n_ok, a.rej_idx, a.n_rej = _ptr(t["ok_idx"]), S(4), _ptr(t["rej_idx"]), S(5)
+        a.cmp_tmp = _ptr(t["cmp_tmp"])
+        a.reg_lo, a.reg_hi, a.reg_val, a.reg_mask = _ptr(t["reg_lo"]), _ptr(t["reg_hi"]), _ptr(t["reg_val"]), c.reg_slots - 1
+        a.dev_asg, a.dev_type = _ptr(t["dev_asg"]), _ptr(t["dev_type"])
+        a.asg_device, a.asg_customer = _ptr(t["asg_device"]), _ptr(t["asg_customer"])
+        a.asg_area, a.asg_asset, a.asg_active = _ptr(t["asg_area"]), _ptr(t["asg_asset"]), _ptr(t["asg_active"])
+        a.n_asg = c.max_assignments
+        a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_key"]), _ptr(t["dd_seq"]), c.dedup_slots - 1, _ptr(t["seq_base"])
+        a.nm_key, a.nm_id, a.nm_first = _ptr(t["nm_key"]), _ptr(t["nm_id"]), _ptr(t["nm_first"])
+        a.nm_mask, a.nm_counter = c.name_slots - 1, _ptr(t["nm_counter"])
+        a.st_last, a.st_missing = _ptr(t["st_last"]), _ptr(t["st_missing"])
+        a.st_loc_date, a.st_loc_eid = _ptr(t["st_loc_date"]), _ptr(t["st_loc_eid"])
+        a.ms_key, a.ms_date, a.ms_eid, a.ms_mask = _ptr(t["ms_key"]), _ptr(t["ms_date"]), _ptr(t["ms_eid"]), c.state_slots - 1
+        a.store_cap = sc
+        a.store_cursor = _ptr(t["cursor"])
+        a.step_cursor0 = _ptr(t["cursor"]) + 8
+        st = self.store
+        (a.s_etype, a.s_level, a.s_date, a.s_recv, a.s_dev, a.s_asg, a.s_cust, a.s_area, a.s_asset, a.s_name,
+         a.s_v0, a.s_v1, a.s_v2, a.s_alt, a.s_aux, a.s_batch) = [
+            _ptr(st[k]) for k in ("etype", "level", "date", "recv", "dev", "asg", "cust", "area", "asset", "name",
+                                  "v0", "v1", "v2", "alt", "aux", "batch")]
+        a.out, a.n_out = _ptr(t["out0"]), S(7)
+        a.gen, a.gen_dev, a.gen_asg, a.n_gen, a.gen_cap = _ptr(t["gen"]), _ptr(t["gen_dev"]), _ptr(t["gen_asg"]), S(6), c.gen_cap
+        a.presence_missing_ms = 0
+        a.presence_name_hash = self.presence_hash
+        a.stats = _ptr(t["stats"])
+        self._rule_scratch = S(8)
+        self._out_sel = 0
+        self._apply_zone_ptrs()
+
+    # ------------------------------------------------------------------ control-plane hooks
+    def _h2d(self, dst: torch.Tensor, src: np.ndarray):
+        dst.copy_(torch.from_numpy(np.ascontiguousarray(src)).view(dst.dtype).reshape(dst.shape), non_blocking=False)
+
+    def _dirty_registry(self, slots: np.ndarray):
+        if len(slots) > self.cfg.reg_slots // 4:
+            self._h2d(self.t["reg_lo"], self.reg_lo.view(np.int64))
+            self._h2d(self.t["reg_hi"], self.reg_hi.view(np.int64))
+            self._h2d(self.t["reg_val"], self.reg_val)
+            return
+        sl = torch.from_numpy(np.ascontiguousarray(slots, np.int64)).to(self.device)
+        for k, src in (("reg_lo", self.reg_lo.view(np.int64)), ("reg_hi", self.reg_hi.view(np.int64)),
+                       ("reg_val", self.reg_val)):
+            vals = torch.from_numpy(np.ascontiguousarray(src[slots])).to(self.device)
+            self.t[k].index_copy_(0, sl, vals)
+
+    def _dirty_rows(self, idx: np.ndarray, names):
+        idx = np.unique(np.asarray(idx, np.int64))
+        it = torch.from_numpy(idx).to(self.device)
+        for k in names:
+            src = getattr(self, k)
+            self.t[k].index_copy_(0, it, torch.from_numpy(np.ascontiguousarray(src[idx])).to(self.device))
+
+    def _dirty_assignments(self, idx):
+        self._dirty_rows(idx, ("asg_device", "asg_customer", "asg_area", "asg_asset", "asg_active"))
+
+    def _dirty_devices(self, idx):
+        self._dirty_rows(idx, ("dev_asg", "dev_type"))
+
+    def _set_zone_tensors(self):
+        vtx, off, bbox, tests, hashes = self.zone_arrays()
+        d = self.device
+        self.t["zone_vtx"] = torch.from_numpy(vtx).to(d)
+        self.t["zone_off"] = torch.from_numpy(off).to(d)
+        self.t["zone_bbox"] = torch.from_numpy(bbox).to(d)
+        self.t["tests"] = torch.from_numpy(tests.view(np.uint8).copy() if len(tests) else np.zeros(16, np.uint8)).to(d)
+        self.t["test_hash"] = torch.from_numpy(hashes.view(np.int64).copy() if len(hashes) else np.zeros(1, np.int64)).to(d)
+        self._n_zones, self._n_tests = len(off) - 1, len(tests)
+
+    def _apply_zone_ptrs(self):
+        a = self.args
+        a.zone_vtx, a.zone_off, a.zone_bbox = _ptr(self.t["zone_vtx"]), _ptr(self.t["zone_off"]), _ptr(self.t["zone_bbox"])
+        a.n_zones, a.tests, a.n_tests = self._n_zones, _ptr(self.t["tests"]), self._n_tests
+        a.test_name_hash = _ptr(self.t["test_hash"])
+
+    def _zones_changed(self):
+        if hasattr(self, "args"):
+            self._set_zone_tensors()
+            self._apply_zone_ptrs()
+
+    # ------------------------------------------------------------------ data plane
+    def step_async(self, raw_dev: torch.Tensor, off_dev: torch.Tensor, n_msgs: int, now_ms: int,
+                   presence: bool = False, out_sel: int | None = None):
+        """Enqueue one micro-batch on the current stream.  raw_dev needs >= 16 B of tail padding."""
+        if n_msgs > self.cfg.max_msgs:
+            raise ValueError(f"batch of {n_msgs} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
+        a = self.args
+        a.raw, a.msg_off, a.n_msgs, a.now_ms = _ptr(raw_dev), _ptr(off_dev), int(n_msgs), int(now_ms)
+        a.batch_seq = self.batch_seq
+        a.presence_missing_ms = self.cfg.presence_missing_ms if presence else 0
+        sel = self._out_sel if out_sel is None else out_sel
+        a.out = _ptr(self.t["out1" if sel else "out0"])
+        s = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        ap = ctypes.byref(a)
+        rc = self.lib.sw_phase_decode(ap, s)
+        if rc:
+            raise RuntimeError(f"sw_phase_decode failed ({rc})")
+        if self.world > 1:
+            import torch.distributed as dist
+
+            rc = self.lib.sw_phase_partition(ap, s)
+            if rc:
+                raise RuntimeError(f"sw_phase_partition failed ({rc})")
+            dist.all_to_all_single(self.t["recv_cnt"], self.t["send_cnt"], group=self.group)
+            dist.all_to_all_single(self.t["recv"], self.t["send"], group=self.group)
+            rc = self.lib.sw_phase_unpack(ap, s)
+            if rc:
+                raise RuntimeError(f"sw_phase_unpack failed ({rc})")
+        rc = self.lib.sw_phase_process(ap, ctypes.c_void_p(self._rule_scratch), s)
+        if rc:
+            raise RuntimeError(f"sw_phase_process failed ({rc})")
+        self.batch_seq += 1
+        return sel
+
+    def scalars(self) -> dict:
+        v = self.t["scalars"][:9].cpu().numpy()
+        return dict(n_recs=int(v[0]), n_new_names=int(v[1]), overflow=int(v[2]), n_work=int(v[3]), n_ok=int(v[4]),
+                    n_rej=int(v[5]), n_gen=int(v[6]), n_out=int(v[7]), n_rule=int(v[8]))
+
+    def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
+        """Synchronous convenience step (tests, control-plane use): H2D, run, D2H, learn names."""
+        n_msgs = len(offs) - 1
+        raw_pad = np.zeros(len(raw) + _ALIGN, np.uint8)
+        raw_pad[:len(raw)] = raw
+        raw_dev = torch.from_numpy(raw_pad).to(self.device)
+        off_dev = torch.from_numpy(np.ascontiguousarray(offs, np.uint32).view(np.int32)).to(self.device)
+        do_presence = self.presence_due(now_ms) if presence is None else presence
+        sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence)
+        torch.cuda.synchronize(self.device)
+        return self.collect(sel, raw)
+
+    def collect(self, sel: int, raw_host: np.ndarray | None) -> StepResult:
+        sc = self.scalars()
+        nn = min(sc["n_new_names"], self.cfg.names_cap)
+        new = {}
+        if nn and raw_host is not None:
+            refs = self.t["new_names"][:nn * NAME_REF.itemsize].cpu().numpy().view(NAME_REF)
+            new = self.learn_names(refs, raw_host)
+        n_out = sc["n_out"]
+        out = self.t["out1" if sel else "out0"][:n_out * OUT_REC_SIZE].cpu().numpy().view(OUT_REC)
+        n_rej = sc["n_rej"]
+        work = self.t["work"] if self.world > 1 else self.t["recs"]
+        rej_idx = self.t["rej_idx"][:n_rej].long()
+        rows = work.view(-1, EVENT_REC.itemsize)[rej_idx].cpu().numpy().reshape(-1).view(EVENT_REC)
+        rst = self.t["status"][rej_idx].cpu().numpy()
+        return StepResult(n_msgs=int(self.args.n_msgs), n_events=sc["n_work"], n_persisted=n_out, out=out,
+                          rejects=rows, reject_status=rst, new_names=new)
+
+    # ------------------------------------------------------------------ queries
+    def stats_dict(self) -> dict:  # type: ignore[override]
+        return EngineBase.stats_dict(self.t["stats"].cpu().numpy().view(np.uint64))
+
+    @property
+    def cursor(self) -> int:
+        return int(self.t["cursor"][0].item())
+
+    def intern_table(self) -> dict:
+        keys = self.t["nm_key"].cpu().numpy().view(np.uint64)
+        ids = self.t["nm_id"].cpu().numpy()
+        sel = (keys != 0) & (ids >= 0)
+        return {int(k): int(i) for k, i in zip(keys[sel], ids[sel])}
+
+    def device_state(self, asg: int) -> dict:
+        intern = self.intern_table()
+        inv = {v: k for k, v in intern.items()}
+        keys = self.t["ms_key"].cpu().numpy().view(np.uint64)
+        dates = self.t["ms_date"].cpu().numpy()
+        eids = self.t["ms_eid"].cpu().numpy()
+        mx, al = {}, {}
+        sel = np.nonzero(keys != 0)[0]
+        for s in sel:
+            k = int(keys[s]) - 1
+            a, nid, kind = k >> 32, (k & 0xFFFFFFFF) >> 1, k & 1
+            if a != asg:
+                continue
+            h = inv.get(nid)
+            name = self.names.get(h, str(h))
+            (al if kind else mx)[name] = (int(eids[s]) - 1, int(dates[s]))
+        le = int(self.t["st_loc_eid"][asg].item())
+        return {
+            "assignment": asg,
+            "last_interaction": int(self.t["st_last"][asg].item()),
+            "presence_missing": int(self.t["st_missing"][asg].item()),
+            "last_location": (le - 1, int(self.t["st_loc_date"][asg].item())) if le else None,
+            "measurements": mx,
+            "alerts": al,
+        }
+
+    def store_rows(self):
+        cur = self.cursor
+        cap = self.cfg.store_cap
+        n = min(cur, cap)
+        idx = torch.arange(n, device=self.device)
+        if cur > cap:
+            idx = (idx + cur % cap) % cap
+        cols = {k: v[idx].cpu().numpy() for k, v in self.store.items()}
+        for k in ("name", "alt", "aux"):
+            cols[k] = cols[k].view(np.uint64)
+        return cols, (np.arange(cur - n, cur) * self.world + self.rank)
+
+    def reset_dedup(self):
+        self.t["dd_key"].zero_()
+        self.t["dd_seq"].fill_(-1)
+
+
+class PipelinedRunner:
+    """Overlaps H2D (batch k+1), compute (batch k) and D2H (batch k-1) on three HIP streams.
+
+    Host batches are pinned ``torch.uint8`` / ``torch.int32`` tensors.  Device raw
+    buffers and outbound buffers are double-buffered; stream events order reuse.
+    """
+
+    def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True):
+        self.e = engine
+        dev = engine.device
+        self.h2d = torch.cuda.Stream(dev)
+        self.comp = torch.cuda.current_stream(dev)
+        self.d2h = torch.cuda.Stream(dev)
+        self.raw = [torch.empty(max_raw_bytes + _ALIGN, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.off = [torch.empty(engine.cfg.max_msgs + 1, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.out_host = [torch.empty(engine.out_cap * OUT_REC_SIZE, dtype=torch.uint8, pin_memory=True)
+                         for _ in range(2)]
+        self.n_out_host = torch.zeros(2, 16, dtype=torch.int32, pin_memory=True)
+        self.ev_h2d = [torch.cuda.Event() for _ in range(2)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(2)]
+        self.ev_d2h = [torch.cuda.Event() for _ in range(2)]
+        self.deliver = deliver_outbound
+        self.k = 0
+        self.delivered = 0
+        self.pending = None
+
+    def submit(self, raw_host: torch.Tensor, off_host: torch.Tensor, n_msgs: int, now_ms: int | None = None,
+               presence: bool = False):
+        k = self.k
+        b = k & 1
+        now_ms = int(time.time() * 1000) if now_ms is None else now_ms
+        nbytes = int(raw_host.numel())
+        # H2D into buffer b once compute k-2 (the last reader of b) is done
+        with torch.cuda.stream(self.h2d):
+            if k >= 2:
+                self.h2d.wait_event(self.ev_comp[b])
+            self.raw[b][:nbytes].copy_(raw_host, non_blocking=True)
+            self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
+            self.ev_h2d[b].record(self.h2d)
+        # compute k once its inputs landed and D2H k-2 released out buffer b
+        self.comp.wait_event(self.ev_h2d[b])
+        if k >= 2:
+            self.comp.wait_event(self.ev_d2h[b])
+        self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b)
+        self.n_out_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
+        self.ev_comp[b].record(self.comp)
+        # deliver k-1 (host learns its exact count, then one D2H of exactly that many rows)
+        self._drain()
+        self.pending = b
+        self.k += 1
+
+    def _drain(self):
+        if self.pending is None:
+            return
+        pb = self.pending
+        self.ev_comp[pb].synchronize()
+        n_out = int(self.n_out_host[pb][7])
+        if self.deliver and n_out:
+            with torch.cuda.stream(self.d2h):
+                self.d2h.wait_event(self.ev_comp[pb])
+                src = self.e.t["out1" if pb else "out0"][:n_out * OUT_REC_SIZE]
+                self.out_host[pb][:n_out * OUT_REC_SIZE].copy_(src, non_blocking=True)
+                self.ev_d2h[pb].record(self.d2h)
+        else:
+            self.ev_d2h[pb].record(self.d2h)
+        self.delivered += n_out
+        self.pending = None
+
+    def flush(self):
+        self._drain()
+        self.d2h.synchronize()
+        self.comp.synchronize()
+
+    def outbound(self, b: int) -> np.ndarray:
+        n = int(self.n_out_host[b][7])
+        return self.out_host[b][:n * OUT_REC_SIZE].numpy().view(OUT_REC)
