@@ -32,6 +32,7 @@
 #define TILE (BLK * TILE_ITEMS)
 #define MAX_GRID 2048
 #define STAGE_BYTES (32 * 1024)
+#define MAX_PROBE 4096  // open-addressing probe bound (tables are sized for load <= 0.5)
 
 typedef unsigned long long ull;
 
@@ -126,99 +127,91 @@ static int launch_scan(const uint32_t* in, int64_t n, uint32_t* out, uint32_t* t
 }
 
 // ============================================================================ decode
-// Stage the block's 256 consecutive payloads into LDS with 16-B loads, then parse
-// each payload from LDS (one lane per payload).  Oversized windows parse from global.
-struct StageWin {
-  const uint8_t* buf;   // base pointer parsed from
-  uint32_t base_abs;    // absolute raw offset of buf[0]
-};
-
-__device__ __forceinline__ StageWin stage_window(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
-                                                 int64_t n_msgs, uint8_t* lds) {
+// Stage the block's 256 consecutive payloads into LDS with 16-B loads, then parse each
+// payload from LDS (one lane per payload).  The parse is instantiated separately for the
+// LDS and the global source so the compiler emits ds_read (not flat) loads on the fast path.
+// Oversized windows (mean payload > 128 B) parse straight from global memory.
+__device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
+                                             int64_t n_msgs, uint8_t* lds, uint32_t* base_abs) {
   const int64_t m0 = (int64_t)blockIdx.x * BLK;
   int64_t m1 = m0 + BLK;
   if (m1 > n_msgs) m1 = n_msgs;
   const uint32_t s = off[m0], e = off[m1];
   const uint32_t a0 = s & ~15u;
   const uint32_t span = e - a0;
-  StageWin w;
-  if (span <= STAGE_BYTES) {
-    const uint32_t nvec = (span + 15) >> 4;
-    const uint4* src = reinterpret_cast<const uint4*>(raw + a0);
-    uint4* dst = reinterpret_cast<uint4*>(lds);
-    for (uint32_t v = threadIdx.x; v < nvec; v += BLK) dst[v] = src[v];
-    __syncthreads();
-    w.buf = lds;
-    w.base_abs = a0;
-  } else {
-    w.buf = raw;
-    w.base_abs = 0;
-  }
-  return w;
+  if (span > STAGE_BYTES) return false;
+  const uint32_t nvec = (span + 15) >> 4;
+  const uint4* src = reinterpret_cast<const uint4*>(raw + a0);
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  for (uint32_t v = threadIdx.x; v < nvec; v += BLK) dst[v] = src[v];
+  __syncthreads();
+  *base_abs = a0;
+  return true;
 }
 
 __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
                                                       int64_t n_msgs, uint32_t* __restrict__ cnt) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
-  StageWin w = stage_window(raw, off, n_msgs, lds);
+  uint32_t base = 0;
+  const bool staged = stage_window(raw, off, n_msgs, lds, &base);
   const int64_t m = (int64_t)blockIdx.x * BLK + threadIdx.x;
   if (m >= n_msgs) return;
-  const uint32_t s = off[m] - w.base_abs, e = off[m + 1] - w.base_abs;
-  cnt[m] = sw_decode_payload(w.buf, s, e, w.base_abs, 0, 0, nullptr, 0);
+  if (staged) cnt[m] = sw_decode_payload(lds, off[m] - base, off[m + 1] - base, base, 0, 0, nullptr, 0);
+  else cnt[m] = sw_decode_payload(raw, off[m], off[m + 1], 0, 0, 0, nullptr, 0);
 }
 
-__global__ __launch_bounds__(BLK) void k_decode_emit(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
-                                                     int64_t n_msgs, const uint32_t* __restrict__ evoff,
-                                                     const uint32_t* __restrict__ n_total, SwEventRec* __restrict__ recs,
-                                                     int64_t cap, int64_t now_ms, int rank) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
-  StageWin w = stage_window(raw, off, n_msgs, lds);
-  const int64_t m = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  if (m >= n_msgs) return;
-  const uint32_t s = off[m] - w.base_abs, e = off[m + 1] - w.base_abs;
-  const int64_t o = evoff[m];
-  if (o >= cap) return;
-  const uint32_t room = (uint32_t)((cap - o) < 0xffffffffll ? (cap - o) : 0xffffffffll);
-  sw_decode_payload(w.buf, s, e, w.base_abs, now_ms, (uint8_t)rank, recs + o, room);
-}
-
-__global__ void k_clamp_count(uint32_t* n, int64_t cap, ull* stats) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    if (*n > cap) *n = (uint32_t)cap;
+// First sighting of a name/type hash on this rank: report (hash, offset, len) so the host can read
+// the string from its raw batch (strings never travel with the fixed-width records).
+__device__ __forceinline__ void note_name(const SwEventRec& r, ull* __restrict__ key, int64_t mask,
+                                          SwNameRef* __restrict__ list, uint32_t* __restrict__ n_list, int64_t cap) {
+  if (r.name_hash == 0 || r.etype >= 16) return;
+  const ull h = r.name_hash;
+  int64_t slot = (int64_t)(h & (ull)mask);
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    ull old = key[slot];
+    if (old == h) return;
+    if (old == 0) {
+      old = atomicCAS(&key[slot], 0ull, h);
+      if (old == 0) {
+        const uint32_t k = atomicAdd(n_list, 1u);
+        if (k < cap) {
+          SwNameRef ref;
+          ref.hash = h; ref.off = r.aux_off; ref.len = r.aux_len; ref.src_rank = r.src_rank; ref.pad = r.etype;
+          list[k] = ref;
+        } else {
+          atomicExch(&key[slot], 0ull);  // list full: forget, retry in a later batch
+        }
+        return;
+      }
+      if (old == h) return;
+    }
+    slot = (slot + 1) & mask;
   }
 }
 
-// New-name capture: the first time this rank's decoder sees a name/type hash, report
-// (hash, offset, len) so the host can read the string from its raw batch.
-__global__ void k_names_seen(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                             ull* __restrict__ key, int64_t mask, SwNameRef* __restrict__ list,
-                             uint32_t* __restrict__ n_list, int64_t cap) {
-  const uint32_t n = *n_ptr;
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
-    const SwEventRec& r = recs[i];
-    if (r.name_hash == 0 || r.etype >= 16) continue;
-    ull h = r.name_hash;
-    int64_t slot = (int64_t)(h & (ull)mask);
-    for (int64_t p = 0; p <= mask; ++p) {
-      ull old = key[slot];
-      if (old == h) break;
-      if (old == 0) {
-        old = atomicCAS(&key[slot], 0ull, h);
-        if (old == 0) {
-          uint32_t k = atomicAdd(n_list, 1u);
-          if (k < cap) {
-            SwNameRef ref;
-            ref.hash = h; ref.off = r.aux_off; ref.len = r.aux_len; ref.src_rank = r.src_rank; ref.pad = r.etype;
-            list[k] = ref;
-          } else {
-            atomicExch(&key[slot], 0ull);  // list full: forget, retry in a later batch
-          }
-          break;
-        }
-        if (old == h) break;
-      }
-      slot = (slot + 1) & mask;
-    }
+__global__ __launch_bounds__(BLK) void k_decode_emit(SwEngineArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
+  uint32_t base = 0;
+  const bool staged = stage_window(a.raw, a.msg_off, a.n_msgs, lds, &base);
+  const int64_t m = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (m >= a.n_msgs) return;
+  const int64_t o = a.msg_evoff[m];
+  if (o >= a.rec_cap) return;
+  const uint32_t room = (uint32_t)((a.rec_cap - o) < 0xffffffffll ? (a.rec_cap - o) : 0xffffffffll);
+  SwEventRec* out = a.recs + o;
+  uint32_t n;
+  if (staged)
+    n = sw_decode_payload(lds, a.msg_off[m] - base, a.msg_off[m + 1] - base, base, a.now_ms, (uint8_t)a.rank, out, room);
+  else
+    n = sw_decode_payload(a.raw, a.msg_off[m], a.msg_off[m + 1], 0, a.now_ms, (uint8_t)a.rank, out, room);
+  // fused new-name capture (one probe of a small L2-resident table per named record)
+  for (uint32_t k = 0; k < n && k < room; ++k)
+    note_name(out[k], (ull*)a.seen_key, a.seen_mask, a.new_names, a.n_new_names, a.names_cap);
+}
+
+__global__ void k_clamp_count(uint32_t* n, int64_t cap) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (*n > cap) *n = (uint32_t)cap;
   }
 }
 
@@ -318,35 +311,51 @@ __global__ void k_unpack(const SwEventRec* __restrict__ recv, const uint32_t* __
 }
 
 // ============================================================================ validate
-__global__ void k_lookup(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                         const ull* __restrict__ reg_lo, const ull* __restrict__ reg_hi, const int32_t* __restrict__ reg_val,
-                         int64_t reg_mask, const int32_t* __restrict__ dev_asg, const uint8_t* __restrict__ asg_active,
-                         uint8_t* __restrict__ status, int32_t* __restrict__ ev_dev, int32_t* __restrict__ ev_asg) {
-  const uint32_t n = *n_ptr;
+__device__ __forceinline__ void intern_insert(ull* __restrict__ key, int64_t mask, ull h) {
+  int64_t slot = (int64_t)(h & (ull)mask);
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    ull old = key[slot];
+    if (old == h) return;
+    if (old == 0) {
+      old = atomicCAS(&key[slot], 0ull, h);
+      if (old == 0 || old == h) return;
+    }
+    slot = (slot + 1) & mask;
+  }
+}
+
+// One probe of the packed registry resolves device AND active assignment; names of every
+// decodable event are interned here too (fused: one pass over the records).
+__global__ void k_lookup(SwEngineArgs a) {
+  const uint32_t n = *a.n_work;
+  const SwEventRec* __restrict__ recs = a.work;
   for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull lo = recs[i].fp_lo, hi = recs[i].fp_hi;
     const uint8_t et = recs[i].etype;
+    const ull nh = recs[i].name_hash;
     uint8_t st;
     int32_t dev = -1, asg = -1;
     if (et == SW_EV_DECODE_ERROR) st = SW_ST_DECODE_ERROR;
     else {
-      int64_t slot = (int64_t)(lo & (ull)reg_mask);
-      for (int64_t p = 0; p <= reg_mask; ++p) {
-        const ull k = reg_lo[slot];
-        if (k == lo && reg_hi[slot] == hi) { dev = reg_val[slot]; break; }
-        if (k == 0 && reg_hi[slot] == 0) break;
-        slot = (slot + 1) & reg_mask;
+      int64_t slot = (int64_t)(lo & (ull)a.reg_mask);
+      for (int64_t p = 0; p <= a.reg_mask && p < MAX_PROBE; ++p) {
+        const ulonglong2 k = *reinterpret_cast<const ulonglong2*>(&a.reg[slot].lo);
+        if (k.x == lo && k.y == hi) {
+          const int2 v = *reinterpret_cast<const int2*>(&a.reg[slot].dev);
+          dev = v.x; asg = v.y;
+          break;
+        }
+        if (k.x == 0 && k.y == 0) break;
+        slot = (slot + 1) & a.reg_mask;
       }
-      if (et >= 16) st = SW_ST_CONTROL;
+      if (et >= 16) { st = SW_ST_CONTROL; asg = -1; }
       else if (dev < 0) st = SW_ST_UNREGISTERED;
-      else {
-        asg = dev_asg[dev];
-        st = (asg >= 0 && asg_active[asg]) ? SW_ST_OK : SW_ST_UNASSIGNED;
-      }
+      else st = asg >= 0 ? SW_ST_OK : SW_ST_UNASSIGNED;
+      if (st == SW_ST_OK && nh) intern_insert((ull*)a.nm_key, a.nm_mask, nh);
     }
-    status[i] = st;
-    ev_dev[i] = dev;
-    ev_asg[i] = asg;
+    a.status[i] = st;
+    a.ev_dev[i] = dev;
+    a.ev_asg[i] = asg;
   }
 }
 
@@ -361,7 +370,7 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
     int64_t slot = (int64_t)(h & (ull)mask);
-    for (int64_t p = 0; p <= mask; ++p) {
+    for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
       ull old = atomicCAS(&key[slot], 0ull, h);
       if (old == 0 || old == h) { atomicMin(&seq[slot], sb + (ull)i); break; }
       slot = (slot + 1) & mask;
@@ -378,7 +387,7 @@ __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
     int64_t slot = (int64_t)(h & (ull)mask);
-    for (int64_t p = 0; p <= mask; ++p) {
+    for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
       const ull k = key[slot];
       if (k == h) { if (seq[slot] != sb + (ull)i) status[i] = SW_ST_DUPLICATE; break; }
       if (k == 0) break;
@@ -391,18 +400,22 @@ __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_
 // Stable split of [0, n) into ok (status == OK) and rejected lists.
 __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
                             uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles) {
-  __shared__ uint32_t lds[WAVES + 1];
+  __shared__ uint32_t c[2];
+  if (threadIdx.x < 2) c[threadIdx.x] = 0;
+  __syncthreads();
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)blockIdx.x * TILE;
-  uint32_t ok = 0, rj = 0;
+  uint32_t ok = 0, all = 0;
+#pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
-    int64_t i = base + (int64_t)k * BLK + threadIdx.x;
-    if (i < n) { if (status[i] == SW_ST_OK) ++ok; else ++rj; }
+    const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
+    const bool v = i < n;
+    ok += __popcll(__ballot(v && status[i] == SW_ST_OK));
+    all += __popcll(__ballot(v));
   }
-  uint32_t t_ok, t_rj;
-  block_excl_scan(ok, &t_ok, lds);
-  block_excl_scan(rj, &t_rj, lds);
-  if (threadIdx.x == 0) { tcnt[blockIdx.x] = t_ok; tcnt[ntiles + blockIdx.x] = t_rj; }
+  if (lane_id() == 0) { atomicAdd(&c[0], ok); atomicAdd(&c[1], all - ok); }
+  __syncthreads();
+  if (threadIdx.x == 0) { tcnt[blockIdx.x] = c[0]; tcnt[ntiles + blockIdx.x] = c[1]; }
 }
 
 __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
@@ -439,7 +452,7 @@ __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* 
 template <typename K>
 __device__ __forceinline__ int64_t nm_probe(const K* __restrict__ key, int64_t mask, ull h) {
   int64_t slot = (int64_t)(h & (ull)mask);
-  for (int64_t p = 0; p <= mask; ++p) {
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
     const ull k = key[slot];
     if (k == h) return slot;
     if (k == 0) return -1;
@@ -448,40 +461,18 @@ __device__ __forceinline__ int64_t nm_probe(const K* __restrict__ key, int64_t m
   return -1;
 }
 
-__global__ void k_intern_insert(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ idx,
-                                const uint32_t* __restrict__ n_ptr, ull* __restrict__ key, int32_t* __restrict__ first,
-                                int64_t mask) {
+__global__ void k_intern_insert_list(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
+                                     ull* __restrict__ key, int64_t mask) {
   const uint32_t n = *n_ptr;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
-    const uint32_t i = idx ? idx[j] : (uint32_t)j;
-    const ull h = recs[i].name_hash;
-    if (h == 0) continue;
-    int64_t slot = (int64_t)(h & (ull)mask);
-    for (int64_t p = 0; p <= mask; ++p) {
-      ull old = key[slot];
-      if (old == 0) old = atomicCAS(&key[slot], 0ull, h);
-      if (old == 0) { atomicMin(&first[slot], (int32_t)j); break; }
-      if (old == h) break;
-      slot = (slot + 1) & mask;
-    }
-  }
+  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
+    if (recs[j].name_hash) intern_insert(key, mask, recs[j].name_hash);
 }
 
-__global__ void k_intern_assign(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ idx,
-                                const uint32_t* __restrict__ n_ptr, const ull* __restrict__ key,
-                                int32_t* __restrict__ ids, int32_t* __restrict__ first, int64_t mask,
+// Give every newly inserted name slot a dense id (ids are rank-local state-map keys).
+__global__ void k_intern_assign(const ull* __restrict__ key, int32_t* __restrict__ ids, int64_t slots,
                                 int32_t* __restrict__ counter) {
-  const uint32_t n = *n_ptr;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
-    const uint32_t i = idx ? idx[j] : (uint32_t)j;
-    const ull h = recs[i].name_hash;
-    if (h == 0) continue;
-    const int64_t slot = nm_probe(key, mask, h);
-    if (slot >= 0 && ids[slot] < 0 && first[slot] == (int32_t)j) {
-      ids[slot] = atomicAdd(counter, 1);
-      first[slot] = 0x7fffffff;
-    }
-  }
+  for (int64_t s = (int64_t)blockIdx.x * BLK + threadIdx.x; s < slots; s += (int64_t)gridDim.x * BLK)
+    if (key[s] != 0 && ids[s] < 0) ids[s] = atomicAdd(counter, 1);
 }
 
 // ============================================================================ persist + enrich
@@ -497,16 +488,16 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     const int32_t dev = devs[i], asg = asgs[i];
     const int64_t seq = cur + j;
     const int64_t row = seq % a.store_cap;
-    const int64_t eid = seq * a.world + a.rank;
     a.s_etype[row] = r.etype;
     a.s_level[row] = r.level;
     a.s_date[row] = r.event_date;
     a.s_recv[row] = a.now_ms;
     a.s_dev[row] = dev;
     a.s_asg[row] = asg;
-    a.s_cust[row] = a.asg_customer[asg];
-    a.s_area[row] = a.asg_area[asg];
-    a.s_asset[row] = a.asg_asset[asg];
+    const int4 ctx = *reinterpret_cast<const int4*>(&a.asg_ctx[asg]);
+    a.s_cust[row] = ctx.y;
+    a.s_area[row] = ctx.z;
+    a.s_asset[row] = ctx.w;
     a.s_name[row] = r.name_hash;
     a.s_v0[row] = r.v0;
     a.s_v1[row] = r.v1;
@@ -515,30 +506,28 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     a.s_aux[row] = ((ull)r.src_rank << 48) | ((ull)r.aux_len << 32) | (ull)r.aux_off;
     a.s_batch[row] = (int32_t)a.batch_seq;
     SwOutRec o;
-    o.event_id = eid;
     o.event_date = r.event_date;
     o.v0 = r.v0;
     o.v1 = r.v1;
     o.assignment = asg;
-    o.device = dev;
     const int64_t ns = r.name_hash ? nm_probe(a.nm_key, a.nm_mask, r.name_hash) : -1;
-    o.name_id = ns >= 0 ? a.nm_id[ns] : -1;
+    const int32_t nid = ns >= 0 ? a.nm_id[ns] : -1;
+    o.name_id = (nid >= 0 && nid < 0xffff) ? (uint16_t)nid : (uint16_t)0xffff;
     o.etype = r.etype;
     o.level = r.level;
-    o.status = 0;
     a.out[seq - c0] = o;
   }
 }
 
 // ============================================================================ device state
-__device__ __forceinline__ int64_t ms_slot(uint64_t* __restrict__ key_, int64_t mask, ull k) {
-  ull* key = (ull*)key_;
+__device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t mask, ull k) {
   int64_t slot = (int64_t)(sw_mix64(k) & (ull)mask);
-  for (int64_t p = 0; p <= mask; ++p) {
-    ull old = key[slot];
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    ull* kp = (ull*)&ms[slot].key;
+    ull old = *kp;
     if (old == k) return slot;
     if (old == 0) {
-      old = atomicCAS(&key[slot], 0ull, k);
+      old = atomicCAS(kp, 0ull, k);
       if (old == 0 || old == k) return slot;
     }
     slot = (slot + 1) & mask;
@@ -555,7 +544,7 @@ __device__ __forceinline__ ull state_key(const SwEngineArgs& a, const SwEventRec
   return (((ull)(uint32_t)asg) << 32 | ((ull)(uint32_t)id << 1) | (r.etype == SW_EV_ALERT ? 1ull : 0ull)) + 1ull;
 }
 
-// Pass 1: max event date per (assignment) location and per (assignment, name) measurement/alert.
+// Pass 1: max event date per assignment location and per (assignment, name) measurement/alert.
 __global__ void k_state_p1(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                            const int32_t* __restrict__ asgs, const uint32_t* __restrict__ n_ptr) {
   const uint32_t n = *n_ptr;
@@ -564,16 +553,18 @@ __global__ void k_state_p1(SwEngineArgs a, const SwEventRec* __restrict__ R, con
     const SwEventRec r = R[i];
     const int32_t asg = asgs[i];
     if (r.etype != SW_EV_MEASUREMENT && r.etype != SW_EV_LOCATION && r.etype != SW_EV_ALERT) continue;
-    atomicMax((ull*)&a.st_last[asg], (ull)a.now_ms);
-    if (a.st_missing[asg]) a.st_missing[asg] = 0;  // presence detected again
+    SwAsgState* st = &a.st[asg];
+    atomicMax((ull*)&st->last, (ull)a.now_ms);
+    if (st->missing) st->missing = 0;  // presence detected again
     const ull d = (ull)r.event_date;
     if (r.etype == SW_EV_LOCATION) {
-      atomicMax((ull*)&a.st_loc_date[asg], d);
+      atomicMax((ull*)&st->loc_date, d);
     } else if (r.name_hash) {
       const ull k = state_key(a, r, asg);
       if (!k) continue;
-      const int64_t s = ms_slot(a.ms_key, a.ms_mask, k);
-      if (s >= 0) atomicMax((ull*)&a.ms_date[s], d);
+      const int64_t s = ms_slot(a.ms, a.ms_mask, k);
+      if (s >= 0) atomicMax((ull*)&a.ms[s].date, d);
+      else atomicAdd((ull*)&a.stats[SW_STAT_STATE_OVERFLOW], 1ull);
     }
   }
 }
@@ -590,12 +581,13 @@ __global__ void k_state_p2(SwEngineArgs a, const SwEventRec* __restrict__ R, con
     const ull eid1 = (ull)((cur + j) * a.world + a.rank) + 1ull;  // stored +1, 0 = none
     const ull d = (ull)r.event_date;
     if (r.etype == SW_EV_LOCATION) {
-      if (a.st_loc_date[asg] == d) atomicMax((ull*)&a.st_loc_eid[asg], eid1);
+      SwAsgState* st = &a.st[asg];
+      if (st->loc_date == d) atomicMax((ull*)&st->loc_eid1, eid1);
     } else if ((r.etype == SW_EV_MEASUREMENT || r.etype == SW_EV_ALERT) && r.name_hash) {
       const ull k = state_key(a, r, asg);
       if (!k) continue;
-      const int64_t s = ms_slot(a.ms_key, a.ms_mask, k);
-      if (s >= 0 && a.ms_date[s] == d) atomicMax((ull*)&a.ms_eid[s], eid1);
+      const int64_t s = ms_slot(a.ms, a.ms_mask, k);
+      if (s >= 0 && a.ms[s].date == d) atomicMax((ull*)&a.ms[s].eid1, eid1);
     }
   }
 }
@@ -605,10 +597,28 @@ __global__ void k_advance(int64_t* __restrict__ cursor, const uint32_t* __restri
 }
 
 // ============================================================================ zone-test rules
-#define ZONE_LDS_VTX 3072  // 48 KiB of (lat, lon) doubles
+#define ZONE_LDS_VTX 2048  // 32 KiB of (lat, lon) doubles
+#define ZONE_LDS_TESTS 64
 
 __device__ __forceinline__ bool pip(const double* __restrict__ v, int n, double x, double y) {
-  // even-odd crossing number; v = [lat0, lon0, lat1, lon1, ...], x = lat, y = lon
+  // even-odd crossing number; v = [lat0, lon0, lat1, lon1, ...], x = lat, y = lon.
+  // Division-free form of  x < (xj - xi) * (y - yi) / (yj - yi) + xi  (sign of (yj - yi) folded in).
+  bool inside = false;
+  double xj = v[2 * (n - 1)], yj = v[2 * (n - 1) + 1];
+  for (int i = 0; i < n; ++i) {
+    const double xi = v[2 * i], yi = v[2 * i + 1];
+    if ((yi > y) != (yj > y)) {
+      const double lhs = (x - xi) * (yj - yi);
+      const double rhs = (xj - xi) * (y - yi);
+      if ((yj > yi) ? (lhs < rhs) : (lhs > rhs)) inside = !inside;
+    }
+    xj = xi; yj = yi;
+  }
+  return inside;
+}
+
+// Same predicate with the division (reference form, for the standalone batch kernel parity).
+__device__ __forceinline__ bool pip_div(const double* __restrict__ v, int n, double x, double y) {
   bool inside = false;
   for (int i = 0, j = n - 1; i < n; j = i++) {
     const double xi = v[2 * i], yi = v[2 * i + 1], xj = v[2 * j], yj = v[2 * j + 1];
@@ -617,32 +627,96 @@ __device__ __forceinline__ bool pip(const double* __restrict__ v, int n, double 
   return inside;
 }
 
-__global__ __launch_bounds__(BLK) void k_zones(SwEngineArgs a) {
-  __shared__ double lv[2 * ZONE_LDS_VTX];
+struct ZoneLds {
+  double v[2 * ZONE_LDS_VTX];
+  double bb[4 * ZONE_LDS_TESTS];
+  int4 t[ZONE_LDS_TESTS];
+  int2 zo[ZONE_LDS_TESTS];
+};
+
+__device__ __forceinline__ int zone_lds_load(const SwEngineArgs& a, ZoneLds& L, bool* vtx_lds) {
+  const int nt = a.n_tests < ZONE_LDS_TESTS ? (int)a.n_tests : ZONE_LDS_TESTS;
   const int64_t nv = a.n_zones ? a.zone_off[a.n_zones] : 0;
-  const bool in_lds = nv <= ZONE_LDS_VTX;
-  if (in_lds) {
-    for (int64_t t = threadIdx.x; t < 2 * nv; t += BLK) lv[t] = a.zone_vtx[t];
-    __syncthreads();
+  *vtx_lds = nv <= ZONE_LDS_VTX;
+  for (int64_t t = threadIdx.x; *vtx_lds && t < 2 * nv; t += BLK) L.v[t] = a.zone_vtx[t];
+  for (int t = threadIdx.x; t < nt; t += BLK) {
+    const SwZoneTest zt = a.tests[t];
+    L.t[t] = make_int4(zt.zone, zt.condition, zt.alert_name_id, zt.level);
+    L.zo[t] = make_int2(a.zone_off[zt.zone], a.zone_off[zt.zone + 1]);
+    for (int q = 0; q < 4; ++q) L.bb[4 * t + q] = a.zone_bbox[4 * zt.zone + q];
   }
-  const double* V = in_lds ? lv : a.zone_vtx;
+  __syncthreads();
+  return nt;
+}
+
+// Pass 1: per persisted row, the bitmask of zone tests that fire (row-major, test-ascending order is
+// the alert order, identical to the CPU oracle); per-tile alert counts.
+__global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restrict__ zmask, uint32_t* __restrict__ ztile) {
+  __shared__ ZoneLds L;
+  __shared__ uint32_t c;
+  bool vtx_lds;
+  const int nt = zone_lds_load(a, L, &vtx_lds);
+  const double* V = vtx_lds ? L.v : a.zone_vtx;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
   const int64_t c0 = *a.step_cursor0;
-  const uint32_t n = (uint32_t)(*a.store_cursor - c0);  // events persisted so far this step
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
-    const SwOutRec o = a.out[j];
-    if (o.etype != SW_EV_LOCATION) continue;
-    const double x = o.v0, y = o.v1;
-    for (int t = 0; t < a.n_tests; ++t) {
-      const SwZoneTest zt = a.tests[t];
-      const int z = zt.zone;
-      const double* bb = a.zone_bbox + 4 * z;
-      bool inside = x >= bb[0] && y >= bb[1] && x <= bb[2] && y <= bb[3];
-      if (inside) {
-        const int v0 = a.zone_off[z], v1 = a.zone_off[z + 1];
-        inside = pip(V + 2 * v0, v1 - v0, x, y);
+  const uint32_t n = (uint32_t)(*a.store_cursor - c0);
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < TILE_ITEMS; ++k) {
+    const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
+    ull fired = 0;
+    if (j < n) {
+      const int64_t row = (c0 + j) % a.store_cap;
+      if (a.s_etype[row] == SW_EV_LOCATION) {
+        const double x = a.s_v0[row], y = a.s_v1[row];
+        for (int t = 0; t < nt; ++t) {
+          const double* bb = L.bb + 4 * t;
+          bool inside = x >= bb[0] && y >= bb[1] && x <= bb[2] && y <= bb[3];
+          if (inside) inside = pip(V + 2 * L.zo[t].x, L.zo[t].y - L.zo[t].x, x, y);
+          if ((L.t[t].y == 0) == inside) fired |= 1ull << t;
+        }
       }
-      if ((zt.condition == 0) == inside) {
-        const uint32_t g = atomicAdd(a.n_gen, 1u);
+      zmask[j] = fired;
+    }
+    cnt += __popcll(fired);
+  }
+  // block reduce of the tile's alert count
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+  if (lane_id() == 0 && cnt) atomicAdd(&c, cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) ztile[blockIdx.x] = c;
+}
+
+// Pass 2: write the alerts at their scanned offsets (stable, no global atomics).
+__global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __restrict__ zmask,
+                                                   const uint32_t* __restrict__ zoff) {
+  __shared__ uint32_t lds[WAVES + 1];
+  __shared__ int4 lt[ZONE_LDS_TESTS];
+  const int nt = a.n_tests < ZONE_LDS_TESTS ? (int)a.n_tests : ZONE_LDS_TESTS;
+  for (int t = threadIdx.x; t < nt; t += BLK) {
+    const SwZoneTest zt = a.tests[t];
+    lt[t] = make_int4(zt.zone, zt.condition, zt.alert_name_id, zt.level);
+  }
+  __syncthreads();
+  const int64_t c0 = *a.step_cursor0;
+  const uint32_t n = (uint32_t)(*a.store_cursor - c0);
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  uint32_t run = zoff[blockIdx.x];
+  for (int k = 0; k < TILE_ITEMS; ++k) {
+    const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
+    ull fired = j < n ? zmask[j] : 0ull;
+    const uint32_t cnt = __popcll(fired);
+    uint32_t tot;
+    uint32_t g = run + block_excl_scan(cnt, &tot, lds);
+    if (fired) {
+      const int64_t row = (c0 + j) % a.store_cap;
+      const int32_t odev = a.s_dev[row], oasg = a.s_asg[row];
+      while (fired) {
+        const int t = __ffsll(fired) - 1;
+        fired &= fired - 1;
         if (g < a.gen_cap) {
           SwEventRec r;
           r.fp_lo = 0; r.fp_hi = 0;
@@ -650,13 +724,15 @@ __global__ __launch_bounds__(BLK) void k_zones(SwEngineArgs a) {
           r.name_hash = a.test_name_hash[t];
           r.v0 = 0; r.v1 = 0; r.v2 = 0; r.alt_hash = 0;
           r.aux_off = (uint32_t)t; r.aux2_off = 0; r.aux_len = 0; r.aux2_len = 0;
-          r.etype = SW_EV_ALERT; r.flags = 0; r.src_rank = (uint8_t)a.rank; r.level = (uint8_t)zt.level;
+          r.etype = SW_EV_ALERT; r.flags = 0; r.src_rank = (uint8_t)a.rank; r.level = (uint8_t)lt[t].w;
           a.gen[g] = r;
-          a.gen_dev[g] = o.device;
-          a.gen_asg[g] = o.assignment;
+          a.gen_dev[g] = odev;
+          a.gen_asg[g] = oasg;
         }
+        ++g;
       }
     }
+    run += tot;
   }
 }
 
@@ -664,10 +740,11 @@ __global__ __launch_bounds__(BLK) void k_zones(SwEngineArgs a) {
 __global__ void k_presence(SwEngineArgs a) {
   const ull limit = (ull)(a.now_ms - a.presence_missing_ms);
   for (int64_t s = (int64_t)blockIdx.x * BLK + threadIdx.x; s < a.n_asg; s += (int64_t)gridDim.x * BLK) {
-    const ull last = a.st_last[s];
-    const bool miss = a.asg_active[s] && last != 0 && last < limit && a.st_missing[s] == 0;
+    SwAsgState* st = &a.st[s];
+    const ull last = st->last;
+    const bool miss = last != 0 && last < limit && st->missing == 0 && a.asg_active[s];
     if (!miss) continue;
-    a.st_missing[s] = (ull)a.now_ms;  // send-once strategy
+    st->missing = (ull)a.now_ms;  // send-once strategy
     const uint32_t g = atomicAdd(a.n_gen, 1u);
     if (g < a.gen_cap) {
       SwEventRec r;
@@ -676,7 +753,7 @@ __global__ void k_presence(SwEngineArgs a) {
       r.aux_off = 0; r.aux2_off = 0; r.aux_len = 0; r.aux2_len = 0;
       r.etype = SW_EV_STATE_CHANGE; r.flags = 0; r.src_rank = (uint8_t)a.rank; r.level = 0;
       a.gen[g] = r;
-      a.gen_dev[g] = a.asg_device[s];
+      a.gen_dev[g] = a.asg_ctx[s].device;
       a.gen_asg[g] = (int32_t)s;
     }
   }
@@ -720,16 +797,16 @@ __global__ void k_reject_stats(SwEngineArgs a) {
   if (threadIdx.x < 8) c[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *a.n_rej;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
     atomicAdd(&c[a.status[a.rej_idx[j]] & 7], 1u);
-  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd((ull*)&a.stats[SW_STAT_UNREGISTERED], (ull)c[SW_ST_UNREGISTERED]);
-    atomicAdd((ull*)&a.stats[SW_STAT_UNASSIGNED], (ull)c[SW_ST_UNASSIGNED]);
-    atomicAdd((ull*)&a.stats[SW_STAT_DUPLICATE], (ull)c[SW_ST_DUPLICATE]);
-    atomicAdd((ull*)&a.stats[SW_STAT_DECODE_ERROR], (ull)c[SW_ST_DECODE_ERROR]);
-    atomicAdd((ull*)&a.stats[SW_STAT_CONTROL], (ull)c[SW_ST_CONTROL]);
+  if (threadIdx.x < 8 && c[threadIdx.x]) {
+    const int slot = threadIdx.x == SW_ST_UNREGISTERED ? SW_STAT_UNREGISTERED
+                   : threadIdx.x == SW_ST_UNASSIGNED ? SW_STAT_UNASSIGNED
+                   : threadIdx.x == SW_ST_DUPLICATE ? SW_STAT_DUPLICATE
+                   : threadIdx.x == SW_ST_DECODE_ERROR ? SW_STAT_DECODE_ERROR
+                   : threadIdx.x == SW_ST_CONTROL ? SW_STAT_CONTROL : -1;
+    if (slot >= 0) atomicAdd((ull*)&a.stats[slot], (ull)c[threadIdx.x]);
   }
 }
 
@@ -748,11 +825,8 @@ int sw_phase_decode(const SwEngineArgs* ap, hipStream_t s) {
   k_decode_count<<<nb, BLK, 0, s>>>(a.raw, a.msg_off, a.n_msgs, a.msg_cnt);
   int rc = launch_scan(a.msg_cnt, a.n_msgs, a.msg_evoff, a.n_recs, a.scan_tmp, a.scan_tmp_len, s);
   if (rc) return rc;
-  k_decode_emit<<<nb, BLK, 0, s>>>(a.raw, a.msg_off, a.n_msgs, a.msg_evoff, a.n_recs, a.recs, a.rec_cap, a.now_ms,
-                                   (int)a.rank);
-  k_clamp_count<<<1, 64, 0, s>>>(a.n_recs, a.rec_cap, (ull*)a.stats);
-  k_names_seen<<<grid_for(a.rec_cap), BLK, 0, s>>>(a.recs, a.n_recs, (ull*)a.seen_key, a.seen_mask, a.new_names,
-                                                    a.n_new_names, a.names_cap);
+  k_decode_emit<<<nb, BLK, 0, s>>>(a);
+  k_clamp_count<<<1, 64, 0, s>>>(a.n_recs, a.rec_cap);
   return (int)hipGetLastError();
 }
 
@@ -789,8 +863,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
   if (2 * ntiles > a.scan_tmp_len) return -4;
   if (a.world == 1) (void)hipMemcpyAsync(a.n_work, a.n_recs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
-  k_lookup<<<g, BLK, 0, s>>>(a.work, a.n_work, (const ull*)a.reg_lo, (const ull*)a.reg_hi, a.reg_val, a.reg_mask,
-                             a.dev_asg, a.asg_active, a.status, a.ev_dev, a.ev_asg);
+  k_lookup<<<g, BLK, 0, s>>>(a);
   k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base);
   k_dedup_check<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (const ull*)a.dd_key, (const ull*)a.dd_seq, a.dd_mask,
                                   a.seq_base);
@@ -801,11 +874,9 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   if (rc) return rc;
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, cmp_off, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx,
                                                a.n_ok, a.n_rej);
-  k_reject_stats<<<g, BLK, 0, s>>>(a);
-  // names intern for state keys
-  k_intern_insert<<<g, BLK, 0, s>>>(a.work, a.ok_idx, a.n_ok, (ull*)a.nm_key, a.nm_first, a.nm_mask);
-  k_intern_assign<<<g, BLK, 0, s>>>(a.work, a.ok_idx, a.n_ok, (const ull*)a.nm_key, a.nm_id, a.nm_first, a.nm_mask,
-                                    a.nm_counter);
+  k_reject_stats<<<64, BLK, 0, s>>>(a);
+  // dense ids for names interned by k_lookup (state-map keys)
+  k_intern_assign<<<grid_for(a.nm_mask + 1), BLK, 0, s>>>((const ull*)a.nm_key, a.nm_id, a.nm_mask + 1, a.nm_counter);
   // persist + enrich + state for the validated events
   k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok);
   k_state_p1<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_asg, a.n_ok);
@@ -813,14 +884,21 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_ok);
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
-  if (a.n_tests > 0) k_zones<<<g, BLK, 0, s>>>(a);
+  if (a.n_tests > 0) {
+    const int64_t otiles = (a.rec_cap + TILE - 1) / TILE;
+    ull* zmask = (ull*)a.zmask;
+    uint32_t* ztile = a.ztile;
+    k_zone_mask<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile);
+    rc = launch_scan(ztile, otiles, ztile + otiles, a.n_gen, a.scan_tmp, a.scan_tmp_len, s);
+    if (rc) return rc;
+    k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile + otiles);
+  }
   k_gen_clamp<<<1, 64, 0, s>>>(a, n_rule);
   if (a.presence_missing_ms > 0) k_presence<<<grid_for(a.n_asg), BLK, 0, s>>>(a);
   k_gen_clamp<<<1, 64, 0, s>>>(a, nullptr);
   const int gg = grid_for(a.gen_cap);
-  k_intern_insert<<<gg, BLK, 0, s>>>(a.gen, nullptr, a.n_gen, (ull*)a.nm_key, a.nm_first, a.nm_mask);
-  k_intern_assign<<<gg, BLK, 0, s>>>(a.gen, nullptr, a.n_gen, (const ull*)a.nm_key, a.nm_id, a.nm_first, a.nm_mask,
-                                     a.nm_counter);
+  k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_mask);
+  k_intern_assign<<<grid_for(a.nm_mask + 1), BLK, 0, s>>>((const ull*)a.nm_key, a.nm_id, a.nm_mask + 1, a.nm_counter);
   k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen);
   k_state_p1<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_asg, a.n_gen);
   k_state_p2<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_asg, a.n_gen);
@@ -829,19 +907,14 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   return (int)hipGetLastError();
 }
 
-// Registry patch: scatter host-built table slots (bulk load and incremental upserts).
-__global__ void k_reg_patch(ull* lo, ull* hi, int32_t* val, const int64_t* slots, const ull* plo, const ull* phi,
-                            const int32_t* pval, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
-    const int64_t s = slots[i];
-    lo[s] = plo[i]; hi[s] = phi[i]; val[s] = pval[i];
-  }
+// Registry patch: scatter host-built packed slots (bulk load and incremental upserts).
+__global__ void k_reg_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* vals, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) reg[slots[i]] = vals[i];
 }
 
-int sw_registry_patch(uint64_t* lo, uint64_t* hi, int32_t* val, const int64_t* slots, const uint64_t* plo,
-                      const uint64_t* phi, const int32_t* pval, int64_t n, hipStream_t s) {
+int sw_registry_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* vals, int64_t n, hipStream_t s) {
   if (n <= 0) return 0;
-  k_reg_patch<<<grid_for(n), BLK, 0, s>>>((ull*)lo, (ull*)hi, val, slots, (const ull*)plo, (const ull*)phi, pval, n);
+  k_reg_patch<<<grid_for(n), BLK, 0, s>>>(reg, slots, vals, n);
   return (int)hipGetLastError();
 }
 
@@ -850,7 +923,7 @@ __global__ void k_pip_batch(const double* pts, int64_t n_pts, const double* vtx,
                             uint8_t* out) {
   for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n_pts * n_zones; i += (int64_t)gridDim.x * BLK) {
     const int64_t p = i / n_zones, z = i % n_zones;
-    out[i] = pip(vtx + 2 * off[z], off[z + 1] - off[z], pts[2 * p], pts[2 * p + 1]);
+    out[i] = pip(vtx + 2 * off[z], off[z + 1] - off[z], pts[2 * p], pts[2 * p + 1]) ? 1 : 0;
   }
 }
 
@@ -868,12 +941,39 @@ int sw_scan_u32(const uint32_t* in, int64_t n, uint32_t* out, uint32_t* total, u
   return (int)hipGetLastError();
 }
 
+// Outbound push: copy this step's enriched rows (count read on the device, no host sync) from
+// HBM into the mapped host ring.  Runs on its own stream, overlapping the next step's compute;
+// a few blocks with 16-B stores saturate the PCIe write direction while H2D uses SDMA.
+__global__ void k_push_out(const uint4* __restrict__ src, uint4* __restrict__ dst, const uint32_t* __restrict__ n_ptr,
+                           int64_t cap) {
+  const int64_t n = (int64_t)(*n_ptr < cap ? *n_ptr : cap) * (int64_t)(sizeof(SwOutRec) / 16);
+  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) dst[i] = src[i];
+}
+
+int sw_push_out(const void* src, void* dst_dev, const uint32_t* n_ptr, int64_t cap, int32_t blocks, hipStream_t s) {
+  k_push_out<<<blocks > 0 ? blocks : 256, BLK, 0, s>>>((const uint4*)src, (uint4*)dst_dev, n_ptr, cap);
+  return (int)hipGetLastError();
+}
+
+// Mapped pinned host memory the kernels can store into directly (zero-copy outbound ring).
+int sw_host_alloc(int64_t bytes, void** host, void** dev) {
+  hipError_t e = hipHostMalloc(host, (size_t)bytes, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) return (int)e;
+  e = hipHostGetDevicePointer(dev, *host, 0);
+  return (int)e;
+}
+
+int sw_host_free(void* host) { return (int)hipHostFree(host); }
+
 int sw_abi_sizes(int64_t* out) {
   out[0] = sizeof(SwEventRec);
   out[1] = sizeof(SwOutRec);
   out[2] = sizeof(SwEngineArgs);
   out[3] = sizeof(SwNameRef);
   out[4] = sizeof(SwZoneTest);
+  out[5] = sizeof(SwRegSlot);
+  out[6] = sizeof(SwAsgState);
+  out[7] = sizeof(SwMsSlot);
   return 0;
 }
 

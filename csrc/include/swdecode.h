@@ -63,7 +63,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
     if (f == 1 && wt == 2) {  // hardwareId in every body message
       ok = sw_read_varint(buf, &pos, bend, &v) && v <= (uint64_t)(bend - pos);
       if (!ok) break;
-      sw_fingerprint(buf + pos, (uint32_t)v, &lo, &hi);
+      if (out) sw_fingerprint(buf + pos, (uint32_t)v, &lo, &hi);  // count pass skips hashing
       has_dev = true;
       pos += (uint32_t)v;
       continue;
@@ -73,7 +73,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
          cmd == SW_CMD_SEND_DEVICE_ALERT)) {
       ok = sw_read_varint(buf, &pos, bend, &v) && v <= (uint64_t)(bend - pos);
       if (!ok) break;
-      alt = sw_hash64(buf + pos, (uint32_t)v);
+      if (out) alt = sw_hash64(buf + pos, (uint32_t)v);
       pos += (uint32_t)v;
       continue;
     }

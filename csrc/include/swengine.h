@@ -16,6 +16,40 @@ typedef struct SwNameRef {
   uint8_t pad;
 } SwNameRef;
 
+// Registry slot (32 B, one cache-line quarter): exact 128-bit token fingerprint -> device and
+// its *active* assignment (-1 when unassigned or released), so validation is one probe.
+typedef struct __attribute__((aligned(16))) SwRegSlot {
+  uint64_t lo;
+  uint64_t hi;
+  int32_t dev;
+  int32_t asg;
+  uint64_t pad;
+} SwRegSlot;
+
+// Assignment context gathered by enrichment (one 16-B load).
+typedef struct __attribute__((aligned(16))) SwAsgCtx {
+  int32_t device;
+  int32_t customer;
+  int32_t area;
+  int32_t asset;
+} SwAsgCtx;
+
+// Device state per assignment (reference IDeviceState), 32 B.
+typedef struct __attribute__((aligned(16))) SwAsgState {
+  uint64_t last;       // last interaction (ms)
+  uint64_t missing;    // presence missing date (0 = present)
+  uint64_t loc_date;   // date of the latest location
+  uint64_t loc_eid1;   // event id + 1 of that location (0 = none)
+} SwAsgState;
+
+// (assignment, name, kind) -> latest measurement / alert, 32 B.
+typedef struct __attribute__((aligned(16))) SwMsSlot {
+  uint64_t key;        // (asg << 32 | name_id << 1 | kind) + 1, 0 = empty
+  uint64_t date;
+  uint64_t eid1;
+  uint64_t pad;
+} SwMsSlot;
+
 typedef struct SwEngineArgs {
   // ---------------------------------------------------------------- batch input
   const uint8_t* raw;          // raw wire bytes of the batch (device)
@@ -60,16 +94,9 @@ typedef struct SwEngineArgs {
   uint32_t* n_rej;
   uint32_t* cmp_tmp;           // [scan_tmp_len]
   // ---------------------------------------------------------------- registry (host-built, read-only here)
-  const uint64_t* reg_lo;
-  const uint64_t* reg_hi;
-  const int32_t* reg_val;
+  const SwRegSlot* reg;
   int64_t reg_mask;
-  const int32_t* dev_asg;      // active assignment per device (-1 none)
-  const int32_t* dev_type;
-  const int32_t* asg_device;
-  const int32_t* asg_customer;
-  const int32_t* asg_area;
-  const int32_t* asg_asset;
+  const SwAsgCtx* asg_ctx;
   const uint8_t* asg_active;
   int64_t n_asg;
   // ---------------------------------------------------------------- dedup window
@@ -84,13 +111,8 @@ typedef struct SwEngineArgs {
   int64_t nm_mask;
   int32_t* nm_counter;
   // ---------------------------------------------------------------- device state (per assignment)
-  uint64_t* st_last;           // last interaction
-  uint64_t* st_missing;        // presence missing date (0 = present)
-  uint64_t* st_loc_date;
-  int64_t* st_loc_eid;
-  uint64_t* ms_key;            // (asg << 32 | name_id << 1 | kind) ; kind 0 = measurement, 1 = alert
-  uint64_t* ms_date;
-  int64_t* ms_eid;
+  SwAsgState* st;
+  SwMsSlot* ms;
   int64_t ms_mask;
   // ---------------------------------------------------------------- event store (HBM ring, SoA)
   int64_t store_cap;
@@ -123,6 +145,8 @@ typedef struct SwEngineArgs {
   const SwZoneTest* tests;
   int64_t n_tests;
   const uint64_t* test_name_hash; // alert type hash per test
+  uint64_t* zmask;             // [rec_cap] fired-test bitmask per persisted row
+  uint32_t* ztile;             // [2 * ntiles] tile counts + scanned offsets
   // generated events (rule alerts, presence state changes)
   SwEventRec* gen;
   int32_t* gen_dev;
@@ -149,5 +173,6 @@ enum {
   SW_STAT_PRESENCE = 9,
   SW_STAT_SHUFFLE_OVERFLOW = 10,
   SW_STAT_NEW_NAMES = 11,
+  SW_STAT_STATE_OVERFLOW = 12,
   SW_STAT_N = 16,
 };

@@ -77,19 +77,18 @@ typedef struct __attribute__((aligned(16))) SwEventRec {
   uint8_t level;        // 79 alert level (GAlertLevel)
 } SwEventRec;
 
-// Enriched, persisted event as delivered to outbound consumers (D2H), 48 bytes.
-// Reference: GEnrichedEventPayload (event + device/assignment context).
+// Enriched, persisted event as delivered to outbound consumers, 32 bytes, written by the GPU
+// straight into mapped pinned host memory (zero-copy outbound, no D2H copy stage).
+// The event id is implicit: row j of a step is event (cursor0 + j) * world + rank; the device
+// follows from the assignment on the host.  Reference: GEnrichedEventPayload.
 typedef struct __attribute__((aligned(16))) SwOutRec {
-  int64_t event_id;     // 0  global event id (rank-striped, see engine)
-  int64_t event_date;   // 8
-  double v0;            // 16
-  double v1;            // 24
-  int32_t assignment;   // 32
-  int32_t device;       // 36
-  int32_t name_id;      // 40 interned name / alert type id (-1 none)
-  uint8_t etype;        // 44
-  uint8_t level;        // 45
-  uint16_t status;      // 46 reserved
+  int64_t event_date;   // 0
+  double v0;            // 8  value | latitude
+  double v1;            // 16 longitude
+  int32_t assignment;   // 24
+  uint16_t name_id;     // 28 interned name / alert type id (0xffff none)
+  uint8_t etype;        // 30
+  uint8_t level;        // 31
 } SwOutRec;
 
 // Zone-test rule (reference: ZoneTestRuleProcessor.java:47-62).

@@ -44,24 +44,27 @@ EVENT_REC = np.dtype([
 assert EVENT_REC.itemsize == 80
 
 OUT_REC = np.dtype([
-    ("event_id", "<i8"), ("event_date", "<i8"), ("v0", "<f8"), ("v1", "<f8"),
-    ("assignment", "<i4"), ("device", "<i4"), ("name_id", "<i4"),
-    ("etype", "u1"), ("level", "u1"), ("status", "<u2"),
-], align=True)
-# C struct is aligned(16) -> sizeof 48
-OUT_REC_SIZE = 48
-OUT_REC = np.dtype({"names": list(OUT_REC.names), "formats": [OUT_REC.fields[n][0] for n in OUT_REC.names],
-                    "offsets": [OUT_REC.fields[n][1] for n in OUT_REC.names], "itemsize": OUT_REC_SIZE})
+    ("event_date", "<i8"), ("v0", "<f8"), ("v1", "<f8"), ("assignment", "<i4"), ("name_id", "<u2"),
+    ("etype", "u1"), ("level", "u1"),
+])
+OUT_REC_SIZE = 32
+assert OUT_REC.itemsize == OUT_REC_SIZE
+NO_NAME = 0xFFFF
 
 NAME_REF = np.dtype([("hash", "<u8"), ("off", "<u4"), ("len", "<u2"), ("src_rank", "u1"), ("etype", "u1")])
 assert NAME_REF.itemsize == 16
+
+REG_SLOT = np.dtype([("lo", "<u8"), ("hi", "<u8"), ("dev", "<i4"), ("asg", "<i4"), ("pad", "<u8")])
+assert REG_SLOT.itemsize == 32
+ASG_STATE = np.dtype([("last", "<u8"), ("missing", "<u8"), ("loc_date", "<u8"), ("loc_eid1", "<u8")])
+MS_SLOT = np.dtype([("key", "<u8"), ("date", "<u8"), ("eid1", "<u8"), ("pad", "<u8")])
 
 ZONE_TEST = np.dtype([("zone", "<i4"), ("condition", "<i4"), ("alert_name_id", "<i4"), ("level", "<i4")])
 
 # Stats slots (SW_STAT_* in swengine.h).
 STAT_NAMES = [
     "messages", "events", "persisted", "unregistered", "unassigned", "duplicates", "decode_errors",
-    "control", "rule_alerts", "presence_events", "shuffle_overflow", "new_names",
+    "control", "rule_alerts", "presence_events", "shuffle_overflow", "new_names", "state_overflow",
 ]
 
 # Alert levels (GAlertLevel) and sources.

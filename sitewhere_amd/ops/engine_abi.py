@@ -26,16 +26,13 @@ FIELDS = [
     ("work", P), ("n_work", P), ("status", P), ("ev_dev", P), ("ev_asg", P),
     ("ok_idx", P), ("n_ok", P), ("rej_idx", P), ("n_rej", P), ("cmp_tmp", P),
     # registry
-    ("reg_lo", P), ("reg_hi", P), ("reg_val", P), ("reg_mask", I),
-    ("dev_asg", P), ("dev_type", P),
-    ("asg_device", P), ("asg_customer", P), ("asg_area", P), ("asg_asset", P), ("asg_active", P), ("n_asg", I),
+    ("reg", P), ("reg_mask", I), ("asg_ctx", P), ("asg_active", P), ("n_asg", I),
     # dedup
     ("dd_key", P), ("dd_seq", P), ("dd_mask", I), ("seq_base", P),
     # names intern
     ("nm_key", P), ("nm_id", P), ("nm_first", P), ("nm_mask", I), ("nm_counter", P),
     # state
-    ("st_last", P), ("st_missing", P), ("st_loc_date", P), ("st_loc_eid", P),
-    ("ms_key", P), ("ms_date", P), ("ms_eid", P), ("ms_mask", I),
+    ("st", P), ("ms", P), ("ms_mask", I),
     # store
     ("store_cap", I), ("store_cursor", P), ("step_cursor0", P),
     ("s_etype", P), ("s_level", P), ("s_date", P), ("s_recv", P), ("s_dev", P), ("s_asg", P),
@@ -45,7 +42,7 @@ FIELDS = [
     ("out", P), ("n_out", P),
     # rules
     ("zone_vtx", P), ("zone_off", P), ("zone_bbox", P), ("n_zones", I), ("tests", P), ("n_tests", I),
-    ("test_name_hash", P),
+    ("test_name_hash", P), ("zmask", P), ("ztile", P),
     ("gen", P), ("gen_dev", P), ("gen_asg", P), ("n_gen", P), ("gen_cap", I),
     # presence
     ("presence_missing_ms", I), ("presence_name_hash", U),
@@ -61,4 +58,5 @@ class SwEngineArgs(ctypes.Structure):
 def abi_sizes(lib) -> dict:
     buf = (ctypes.c_int64 * 8)()
     lib.sw_abi_sizes(ctypes.cast(buf, ctypes.c_void_p))
-    return {"event_rec": buf[0], "out_rec": buf[1], "engine_args": buf[2], "name_ref": buf[3], "zone_test": buf[4]}
+    return {"event_rec": buf[0], "out_rec": buf[1], "engine_args": buf[2], "name_ref": buf[3], "zone_test": buf[4],
+            "reg_slot": buf[5], "asg_state": buf[6], "ms_slot": buf[7]}

@@ -27,7 +27,7 @@ class EngineConfig:
     store_cap: int = 1 << 27         # HBM event-store ring capacity (events)
     dedup_slots: int = 1 << 22       # alternate-id window (slots; window = slots / 2)
     name_slots: int = 1 << 16        # distinct measurement names / alert types
-    state_slots: int = 0             # (assignment, name) state map slots (0 = 4 * max_assignments)
+    state_slots: int = 0             # (assignment, name) state map slots (0 = 16 * max_assignments)
     names_cap: int = 4096            # new-name reports per step
     shuffle_slack: float = 1.25      # per-destination slab = slack * rec_cap / world
     presence_missing_ms: int = 8 * 3600 * 1000   # DevicePresenceManager default (8h)
@@ -40,7 +40,7 @@ class EngineConfig:
         if self.rec_cap <= 0:
             self.rec_cap = 2 * self.max_msgs
         if self.state_slots <= 0:
-            self.state_slots = 4 * self.max_assignments
+            self.state_slots = 16 * self.max_assignments
         self.reg_slots = pow2_at_least(2 * self.max_devices)
         self.dedup_slots = pow2_at_least(self.dedup_slots)
         self.name_slots = pow2_at_least(self.name_slots)

@@ -132,7 +132,6 @@ class CpuInboundEngine(EngineBase):
             r = recs[j]
             seq = self.cursor + j
             row = seq % self.cfg.store_cap
-            eid = seq * self.world + self.rank
             a = int(asg[j])
             s = self.store
             s["etype"][row] = r["etype"]
@@ -153,8 +152,8 @@ class CpuInboundEngine(EngineBase):
             s["batch"][row] = self.batch_seq
             h = int(r["name_hash"])
             nid = self.intern.get(h, -1) if h else -1
-            out_rows.append((eid, int(r["event_date"]), float(r["v0"]), float(r["v1"]), a, int(dev[j]), nid,
-                             int(r["etype"]), int(r["level"]), 0))
+            out_rows.append((int(r["event_date"]), float(r["v0"]), float(r["v1"]), a,
+                             nid if 0 <= nid < 0xFFFF else 0xFFFF, int(r["etype"]), int(r["level"])))
 
     def _state(self, recs, asg, now_ms):
         base = self.cursor
@@ -185,6 +184,7 @@ class CpuInboundEngine(EngineBase):
     # ------------------------------------------------------------------ step
     def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
         n_msgs = len(offs) - 1
+        first_seq = self.cursor
         recs = cpu_decode(raw, offs, now_ms, self.rank, cap=self.cfg.rec_cap)
         # new-name capture on the source rank
         refs = []
@@ -214,16 +214,16 @@ class CpuInboundEngine(EngineBase):
             vtx, zoff, _, tests, hashes = self.zone_arrays()
             polys = [vtx.reshape(-1, 2)[zoff[z]:zoff[z + 1]] for z in range(len(zoff) - 1)]
             for o in out_rows:
-                if o[7] != EV_LOCATION:
+                if o[5] != EV_LOCATION:
                     continue
                 for t, zt in enumerate(tests):
-                    inside = pip(polys[int(zt["zone"])], o[2], o[3])
+                    inside = pip(polys[int(zt["zone"])], o[1], o[2])
                     if (int(zt["condition"]) == 0) == inside:
                         if len(gen) < self.cfg.gen_cap:
                             gen.append((0, 0, now_ms, int(hashes[t]), 0.0, 0.0, 0.0, 0, t, 0, 0, 0, EV_ALERT, 0,
                                         self.rank, int(zt["level"])))
-                            gen_dev.append(o[5])
-                            gen_asg.append(o[4])
+                            gen_dev.append(int(self.asg_device[o[3]]))
+                            gen_asg.append(o[3])
         n_rule = len(gen)
         do_presence = self.presence_due(now_ms) if presence is None else presence
         if do_presence and self.cfg.presence_missing_ms > 0:
@@ -263,7 +263,7 @@ class CpuInboundEngine(EngineBase):
         self.batch_seq += 1
         return StepResult(n_msgs=n_msgs, n_events=len(work), n_persisted=len(out_rows),
                           out=np.array(out_rows, OUT_REC), rejects=work[rej], reject_status=status[rej],
-                          new_names=new)
+                          new_names=new, first_seq=first_seq, world=self.world, rank=self.rank)
 
     # ------------------------------------------------------------------ queries
     def stats_dict(self) -> dict:  # type: ignore[override]

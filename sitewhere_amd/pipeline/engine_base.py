@@ -20,7 +20,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .._native import native
-from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, STAT_NAMES
+from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, STAT_NAMES, REG_SLOT
 from .config import EngineConfig
 from .fleet import hash64
 
@@ -56,6 +56,13 @@ class StepResult:
     rejects: np.ndarray | None = None      # EVENT_REC rows not persisted
     reject_status: np.ndarray | None = None
     new_names: dict = field(default_factory=dict)
+    first_seq: int = 0                     # store sequence of out[0]; ids are implicit
+    world: int = 1
+    rank: int = 0
+
+    def event_ids(self) -> np.ndarray:
+        n = 0 if self.out is None else len(self.out)
+        return (self.first_seq + np.arange(n, dtype=np.int64)) * self.world + self.rank
 
 
 class EngineBase:
@@ -72,6 +79,7 @@ class EngineBase:
         self.reg_hi = np.zeros(cfg.reg_slots, np.uint64)
         self.reg_val = np.full(cfg.reg_slots, -1, np.int32)
         self.n_devices = 0
+        self.dev_slot = np.full(cfg.max_devices, -1, np.int64)   # registry slot of each device
         self.dev_asg = np.full(cfg.max_devices, -1, np.int32)
         self.dev_type = np.full(cfg.max_devices, -1, np.int32)
         self.asg_device = np.full(cfg.max_assignments, -1, np.int32)
@@ -117,12 +125,25 @@ class EngineBase:
                                            _p(fp_lo), _p(fp_hi), _p(dev_idx), n, _p(slots))
             if failed:
                 raise RuntimeError("registry table full")
+            self.dev_slot[dev_idx] = slots
             self.n_devices = max(self.n_devices, int(dev_idx.max()) + 1 if n else 0)
             if dev_type is not None:
                 self.dev_type[dev_idx] = np.asarray(dev_type, np.int32)
                 self._dirty_devices(dev_idx)
             self._dirty_registry(slots)
             return dev_idx
+
+    def packed_registry(self, slots: np.ndarray) -> np.ndarray:
+        """SwRegSlot rows for the given slots: fingerprint, device and *active* assignment."""
+        rows = np.zeros(len(slots), REG_SLOT)
+        rows["lo"] = self.reg_lo[slots]
+        rows["hi"] = self.reg_hi[slots]
+        dev = self.reg_val[slots]
+        rows["dev"] = dev
+        asg = np.where(dev >= 0, self.dev_asg[np.maximum(dev, 0)], -1)
+        ok = (asg >= 0) & (self.asg_active[np.maximum(asg, 0)] > 0)
+        rows["asg"] = np.where(ok, asg, -1)
+        return rows
 
     def lookup_device(self, fp_lo: int, fp_hi: int) -> int:
         return int(native().sw_reg_find(_p(self.reg_lo), _p(self.reg_hi), _p(self.reg_val), self.cfg.reg_slots - 1,

@@ -33,6 +33,31 @@ def _ptr(t: torch.Tensor) -> int:
     return t.data_ptr()
 
 
+class HostBuffer:
+    """Mapped pinned host memory (hipHostMalloc Mapped): kernels store outbound rows into it directly."""
+
+    def __init__(self, lib, nbytes: int):
+        self.lib = lib
+        self.nbytes = int(nbytes)
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        rc = lib.sw_host_alloc(self.nbytes, ctypes.byref(h), ctypes.byref(d))
+        if rc:
+            raise RuntimeError(f"hipHostMalloc failed ({rc})")
+        self.host, self.dev = h.value, d.value
+        self._arr = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.host))
+
+    def view(self, dtype, n: int) -> np.ndarray:
+        return self._arr[:n * np.dtype(dtype).itemsize].view(dtype)
+
+    def __del__(self):
+        try:
+            if self.host:
+                self.lib.sw_host_free(ctypes.c_void_p(self.host))
+                self.host = None
+        except Exception:
+            pass
+
+
 class GpuInboundEngine(EngineBase):
     def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", group=None):
         super().__init__(cfg)
@@ -77,14 +102,9 @@ class GpuInboundEngine(EngineBase):
         t["ok_idx"] = z(c.rec_cap, i32)
         t["rej_idx"] = z(c.rec_cap, i32)
         t["cmp_tmp"] = z(4 * ntiles + 64, i32)
-        # registry + assignment tables
-        t["reg_lo"] = z(c.reg_slots, i64)
-        t["reg_hi"] = z(c.reg_slots, i64)
-        t["reg_val"] = full(c.reg_slots, -1, i32)
-        t["dev_asg"] = full(c.max_devices, -1, i32)
-        t["dev_type"] = full(c.max_devices, -1, i32)
-        for k in ("asg_device", "asg_customer", "asg_area", "asg_asset"):
-            t[k] = full(c.max_assignments, -1, i32)
+        # registry (packed SwRegSlot: lo, hi, dev, asg, pad) + assignment context (device, customer, area, asset)
+        t["reg"] = z(c.reg_slots * 4, i64)
+        t["asg_ctx"] = full(c.max_assignments * 4, -1, i32)
         t["asg_active"] = z(c.max_assignments, u8)
         # dedup window
         t["dd_key"] = z(c.dedup_slots, i64)
@@ -95,14 +115,9 @@ class GpuInboundEngine(EngineBase):
         t["nm_id"] = full(c.name_slots, -1, i32)
         t["nm_first"] = full(c.name_slots, 0x7FFFFFFF, i32)
         t["nm_counter"] = z(1, i32)
-        # device state
-        t["st_last"] = z(c.max_assignments, i64)
-        t["st_missing"] = z(c.max_assignments, i64)
-        t["st_loc_date"] = z(c.max_assignments, i64)
-        t["st_loc_eid"] = z(c.max_assignments, i64)
-        t["ms_key"] = z(c.state_slots, i64)
-        t["ms_date"] = z(c.state_slots, i64)
-        t["ms_eid"] = z(c.state_slots, i64)
+        # device state (packed SwAsgState per assignment, SwMsSlot map)
+        t["st"] = z(c.max_assignments * 4, i64)
+        t["ms"] = z(c.state_slots * 4, i64)
         # event store (SoA ring)
         sc = c.store_cap
         t["cursor"] = z(2, i64)  # [store_cursor, step_cursor0]
@@ -112,15 +127,18 @@ class GpuInboundEngine(EngineBase):
             "v0": z(sc, torch.float64), "v1": z(sc, torch.float64), "v2": z(sc, torch.float64), "alt": z(sc, i64),
             "aux": z(sc, i64), "batch": z(sc, i32),
         }
-        # outbound (double-buffered for the pipelined runner)
+        # outbound ring: mapped pinned host memory the kernels store into (zero-copy), double-buffered
         out_cap = c.rec_cap + c.gen_cap
         self.out_cap = out_cap
-        t["out0"] = z(out_cap * OUT_REC_SIZE, u8)
-        t["out1"] = z(out_cap * OUT_REC_SIZE, u8)
+        self.out_host = [HostBuffer(self.lib, out_cap * OUT_REC_SIZE) for _ in range(2)]
+        # device-side staging for the outbound push (see PipelinedRunner); OUTBOUND_MODE=direct stores to host
+        self.out_dev = [z(out_cap * OUT_REC_SIZE, u8) for _ in range(2)]
         # rules
         t["gen"] = z(c.gen_cap * EVENT_REC.itemsize, u8)
         t["gen_dev"] = z(c.gen_cap, i32)
         t["gen_asg"] = z(c.gen_cap, i32)
+        t["zmask"] = z(c.rec_cap, i64)
+        t["ztile"] = z(2 * ntiles + 64, i32)
         t["stats"] = z(16, i64)
         self._set_zone_tensors()
         self.args = a = SwEngineArgs()
@@ -144,17 +162,12 @@ class GpuInboundEngine(EngineBase):
         a.status, a.ev_dev, a.ev_asg = _ptr(t["status"]), _ptr(t["ev_dev"]), _ptr(t["ev_asg"])
         a.ok_idx, a.n_ok, a.rej_idx, a.n_rej = _ptr(t["ok_idx"]), S(4), _ptr(t["rej_idx"]), S(5)
         a.cmp_tmp = _ptr(t["cmp_tmp"])
-        a.reg_lo, a.reg_hi, a.reg_val, a.reg_mask = _ptr(t["reg_lo"]), _ptr(t["reg_hi"]), _ptr(t["reg_val"]), c.reg_slots - 1
-        a.dev_asg, a.dev_type = _ptr(t["dev_asg"]), _ptr(t["dev_type"])
-        a.asg_device, a.asg_customer = _ptr(t["asg_device"]), _ptr(t["asg_customer"])
-        a.asg_area, a.asg_asset, a.asg_active = _ptr(t["asg_area"]), _ptr(t["asg_asset"]), _ptr(t["asg_active"])
-        a.n_asg = c.max_assignments
+        a.reg, a.reg_mask = _ptr(t["reg"]), c.reg_slots - 1
+        a.asg_ctx, a.asg_active, a.n_asg = _ptr(t["asg_ctx"]), _ptr(t["asg_active"]), c.max_assignments
         a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_key"]), _ptr(t["dd_seq"]), c.dedup_slots - 1, _ptr(t["seq_base"])
         a.nm_key, a.nm_id, a.nm_first = _ptr(t["nm_key"]), _ptr(t["nm_id"]), _ptr(t["nm_first"])
         a.nm_mask, a.nm_counter = c.name_slots - 1, _ptr(t["nm_counter"])
-        a.st_last, a.st_missing = _ptr(t["st_last"]), _ptr(t["st_missing"])
-        a.st_loc_date, a.st_loc_eid = _ptr(t["st_loc_date"]), _ptr(t["st_loc_eid"])
-        a.ms_key, a.ms_date, a.ms_eid, a.ms_mask = _ptr(t["ms_key"]), _ptr(t["ms_date"]), _ptr(t["ms_eid"]), c.state_slots - 1
+        a.st, a.ms, a.ms_mask = _ptr(t["st"]), _ptr(t["ms"]), c.state_slots - 1
         a.store_cap = sc
         a.store_cursor = _ptr(t["cursor"])
         a.step_cursor0 = _ptr(t["cursor"]) + 8
@@ -163,8 +176,9 @@ class GpuInboundEngine(EngineBase):
          a.s_v0, a.s_v1, a.s_v2, a.s_alt, a.s_aux, a.s_batch) = [
             _ptr(st[k]) for k in ("etype", "level", "date", "recv", "dev", "asg", "cust", "area", "asset", "name",
                                   "v0", "v1", "v2", "alt", "aux", "batch")]
-        a.out, a.n_out = _ptr(t["out0"]), S(7)
+        a.out, a.n_out = self.out_host[0].dev, S(7)
         a.gen, a.gen_dev, a.gen_asg, a.n_gen, a.gen_cap = _ptr(t["gen"]), _ptr(t["gen_dev"]), _ptr(t["gen_asg"]), S(6), c.gen_cap
+        a.zmask, a.ztile = _ptr(t["zmask"]), _ptr(t["ztile"])
         a.presence_missing_ms = 0
         a.presence_name_hash = self.presence_hash
         a.stats = _ptr(t["stats"])
@@ -176,30 +190,32 @@ class GpuInboundEngine(EngineBase):
     def _h2d(self, dst: torch.Tensor, src: np.ndarray):
         dst.copy_(torch.from_numpy(np.ascontiguousarray(src)).view(dst.dtype).reshape(dst.shape), non_blocking=False)
 
-    def _dirty_registry(self, slots: np.ndarray):
-        if len(slots) > self.cfg.reg_slots // 4:
-            self._h2d(self.t["reg_lo"], self.reg_lo.view(np.int64))
-            self._h2d(self.t["reg_hi"], self.reg_hi.view(np.int64))
-            self._h2d(self.t["reg_val"], self.reg_val)
+    def _upload_slots(self, slots: np.ndarray):
+        slots = np.unique(np.asarray(slots, np.int64))
+        slots = slots[slots >= 0]
+        if not len(slots):
             return
-        sl = torch.from_numpy(np.ascontiguousarray(slots, np.int64)).to(self.device)
-        for k, src in (("reg_lo", self.reg_lo.view(np.int64)), ("reg_hi", self.reg_hi.view(np.int64)),
-                       ("reg_val", self.reg_val)):
-            vals = torch.from_numpy(np.ascontiguousarray(src[slots])).to(self.device)
-            self.t[k].index_copy_(0, sl, vals)
+        rows = self.packed_registry(slots).view(np.int64).reshape(-1, 4)
+        reg = self.t["reg"].view(-1, 4)
+        if len(slots) > self.cfg.reg_slots // 4:
+            full = self.packed_registry(np.arange(self.cfg.reg_slots)).view(np.int64)
+            self.t["reg"].copy_(torch.from_numpy(full))
+            return
+        reg.index_copy_(0, torch.from_numpy(slots).to(self.device), torch.from_numpy(np.ascontiguousarray(rows)).to(self.device))
 
-    def _dirty_rows(self, idx: np.ndarray, names):
-        idx = np.unique(np.asarray(idx, np.int64))
-        it = torch.from_numpy(idx).to(self.device)
-        for k in names:
-            src = getattr(self, k)
-            self.t[k].index_copy_(0, it, torch.from_numpy(np.ascontiguousarray(src[idx])).to(self.device))
+    def _dirty_registry(self, slots: np.ndarray):
+        self._upload_slots(slots)
 
     def _dirty_assignments(self, idx):
-        self._dirty_rows(idx, ("asg_device", "asg_customer", "asg_area", "asg_asset", "asg_active"))
+        idx = np.unique(np.asarray(idx, np.int64))
+        ctx = np.stack([self.asg_device[idx], self.asg_customer[idx], self.asg_area[idx], self.asg_asset[idx]], 1)
+        it = torch.from_numpy(idx).to(self.device)
+        self.t["asg_ctx"].view(-1, 4).index_copy_(0, it, torch.from_numpy(np.ascontiguousarray(ctx, np.int32)).to(self.device))
+        self.t["asg_active"].index_copy_(0, it, torch.from_numpy(np.ascontiguousarray(self.asg_active[idx])).to(self.device))
 
     def _dirty_devices(self, idx):
-        self._dirty_rows(idx, ("dev_asg", "dev_type"))
+        idx = np.asarray(idx, np.int64)
+        self._upload_slots(self.dev_slot[idx])
 
     def _set_zone_tensors(self):
         vtx, off, bbox, tests, hashes = self.zone_arrays()
@@ -224,7 +240,7 @@ class GpuInboundEngine(EngineBase):
 
     # ------------------------------------------------------------------ data plane
     def step_async(self, raw_dev: torch.Tensor, off_dev: torch.Tensor, n_msgs: int, now_ms: int,
-                   presence: bool = False, out_sel: int | None = None):
+                   presence: bool = False, out_sel: int | None = None, out_to_device: bool = False):
         """Enqueue one micro-batch on the current stream.  raw_dev needs >= 16 B of tail padding."""
         if n_msgs > self.cfg.max_msgs:
             raise ValueError(f"batch of {n_msgs} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
@@ -233,7 +249,7 @@ class GpuInboundEngine(EngineBase):
         a.batch_seq = self.batch_seq
         a.presence_missing_ms = self.cfg.presence_missing_ms if presence else 0
         sel = self._out_sel if out_sel is None else out_sel
-        a.out = _ptr(self.t["out1" if sel else "out0"])
+        a.out = _ptr(self.out_dev[sel]) if out_to_device else self.out_host[sel].dev
         s = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         ap = ctypes.byref(a)
         rc = self.lib.sw_phase_decode(ap, s)
@@ -281,14 +297,16 @@ class GpuInboundEngine(EngineBase):
             refs = self.t["new_names"][:nn * NAME_REF.itemsize].cpu().numpy().view(NAME_REF)
             new = self.learn_names(refs, raw_host)
         n_out = sc["n_out"]
-        out = self.t["out1" if sel else "out0"][:n_out * OUT_REC_SIZE].cpu().numpy().view(OUT_REC)
+        out = self.out_host[sel].view(OUT_REC, n_out).copy()
+        first_seq = int(self.t["cursor"][1].item())
         n_rej = sc["n_rej"]
         work = self.t["work"] if self.world > 1 else self.t["recs"]
         rej_idx = self.t["rej_idx"][:n_rej].long()
         rows = work.view(-1, EVENT_REC.itemsize)[rej_idx].cpu().numpy().reshape(-1).view(EVENT_REC)
         rst = self.t["status"][rej_idx].cpu().numpy()
         return StepResult(n_msgs=int(self.args.n_msgs), n_events=sc["n_work"], n_persisted=n_out, out=out,
-                          rejects=rows, reject_status=rst, new_names=new)
+                          rejects=rows, reject_status=rst, new_names=new, first_seq=first_seq,
+                          world=self.world, rank=self.rank)
 
     # ------------------------------------------------------------------ queries
     def stats_dict(self) -> dict:  # type: ignore[override]
@@ -305,27 +323,26 @@ class GpuInboundEngine(EngineBase):
         return {int(k): int(i) for k, i in zip(keys[sel], ids[sel])}
 
     def device_state(self, asg: int) -> dict:
+        from ..models.columnar import ASG_STATE, MS_SLOT
         intern = self.intern_table()
         inv = {v: k for k, v in intern.items()}
-        keys = self.t["ms_key"].cpu().numpy().view(np.uint64)
-        dates = self.t["ms_date"].cpu().numpy()
-        eids = self.t["ms_eid"].cpu().numpy()
+        ms = self.t["ms"].cpu().numpy().view(MS_SLOT)
         mx, al = {}, {}
-        sel = np.nonzero(keys != 0)[0]
-        for s in sel:
-            k = int(keys[s]) - 1
+        for s in np.nonzero(ms["key"] != 0)[0]:
+            k = int(ms["key"][s]) - 1
             a, nid, kind = k >> 32, (k & 0xFFFFFFFF) >> 1, k & 1
             if a != asg:
                 continue
             h = inv.get(nid)
             name = self.names.get(h, str(h))
-            (al if kind else mx)[name] = (int(eids[s]) - 1, int(dates[s]))
-        le = int(self.t["st_loc_eid"][asg].item())
+            (al if kind else mx)[name] = (int(ms["eid1"][s]) - 1, int(ms["date"][s]))
+        st = self.t["st"].view(-1, 4)[asg].cpu().numpy().view(ASG_STATE)[0]
+        le = int(st["loc_eid1"])
         return {
             "assignment": asg,
-            "last_interaction": int(self.t["st_last"][asg].item()),
-            "presence_missing": int(self.t["st_missing"][asg].item()),
-            "last_location": (le - 1, int(self.t["st_loc_date"][asg].item())) if le else None,
+            "last_interaction": int(st["last"]),
+            "presence_missing": int(st["missing"]),
+            "last_location": (le - 1, int(st["loc_date"])) if le else None,
             "measurements": mx,
             "alerts": al,
         }
@@ -348,27 +365,34 @@ class GpuInboundEngine(EngineBase):
 
 
 class PipelinedRunner:
-    """Overlaps H2D (batch k+1), compute (batch k) and D2H (batch k-1) on three HIP streams.
+    """Three-stream pipeline: H2D(k+1) || compute(k) || outbound push(k-1).
 
-    Host batches are pinned ``torch.uint8`` / ``torch.int32`` tensors.  Device raw
-    buffers and outbound buffers are double-buffered; stream events order reuse.
+    * copy stream: SDMA H2D of the raw payload batch and its offsets (double-buffered device buffers)
+    * compute stream: the fused step; enriched rows land in a device staging ring
+    * push stream: ``k_push_out`` stores the rows into the mapped host ring over PCIe writes,
+      overlapping the next step (the row count is read on the device: no host sync)
+    ``mode="direct"`` instead lets the persist kernel store straight to host memory.
     """
 
-    def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True):
+    def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
+                 on_outbound=None, mode: str | None = None, push_blocks: int = 128):
+        import os
         self.e = engine
         dev = engine.device
+        self.mode = mode or os.environ.get("SW_OUTBOUND_MODE", "direct")
         self.h2d = torch.cuda.Stream(dev)
         self.comp = torch.cuda.current_stream(dev)
-        self.d2h = torch.cuda.Stream(dev)
+        self.push = torch.cuda.Stream(dev)
+        self.push_blocks = push_blocks
         self.raw = [torch.empty(max_raw_bytes + _ALIGN, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.off = [torch.empty(engine.cfg.max_msgs + 1, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.out_host = [torch.empty(engine.out_cap * OUT_REC_SIZE, dtype=torch.uint8, pin_memory=True)
-                         for _ in range(2)]
-        self.n_out_host = torch.zeros(2, 16, dtype=torch.int32, pin_memory=True)
+        self.nout = [torch.zeros(4, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.scal_host = torch.zeros(2, 16, dtype=torch.int32, pin_memory=True)
         self.ev_h2d = [torch.cuda.Event() for _ in range(2)]
         self.ev_comp = [torch.cuda.Event() for _ in range(2)]
-        self.ev_d2h = [torch.cuda.Event() for _ in range(2)]
+        self.ev_push = [torch.cuda.Event() for _ in range(2)]
         self.deliver = deliver_outbound
+        self.on_outbound = on_outbound
         self.k = 0
         self.delivered = 0
         self.pending = None
@@ -379,21 +403,30 @@ class PipelinedRunner:
         b = k & 1
         now_ms = int(time.time() * 1000) if now_ms is None else now_ms
         nbytes = int(raw_host.numel())
-        # H2D into buffer b once compute k-2 (the last reader of b) is done
         with torch.cuda.stream(self.h2d):
             if k >= 2:
-                self.h2d.wait_event(self.ev_comp[b])
+                self.h2d.wait_event(self.ev_comp[b])      # compute k-2 was the last reader of buffer b
             self.raw[b][:nbytes].copy_(raw_host, non_blocking=True)
             self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
             self.ev_h2d[b].record(self.h2d)
-        # compute k once its inputs landed and D2H k-2 released out buffer b
         self.comp.wait_event(self.ev_h2d[b])
-        if k >= 2:
-            self.comp.wait_event(self.ev_d2h[b])
-        self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b)
-        self.n_out_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
+        if k >= 2 and self.mode == "push":
+            self.comp.wait_event(self.ev_push[b])         # push k-2 was the last reader of staging ring b
+        self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
+                          out_to_device=(self.mode == "push"))
+        self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
+        self.scal_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
         self.ev_comp[b].record(self.comp)
-        # deliver k-1 (host learns its exact count, then one D2H of exactly that many rows)
+        if self.mode == "push" and self.deliver:
+            with torch.cuda.stream(self.push):
+                self.push.wait_event(self.ev_comp[b])
+                rc = self.e.lib.sw_push_out(ctypes.c_void_p(_ptr(self.e.out_dev[b])),
+                                            ctypes.c_void_p(self.e.out_host[b].dev),
+                                            ctypes.c_void_p(_ptr(self.nout[b])), self.e.out_cap, self.push_blocks,
+                                            ctypes.c_void_p(self.push.cuda_stream))
+                if rc:
+                    raise RuntimeError(f"sw_push_out failed ({rc})")
+                self.ev_push[b].record(self.push)
         self._drain()
         self.pending = b
         self.k += 1
@@ -403,23 +436,19 @@ class PipelinedRunner:
             return
         pb = self.pending
         self.ev_comp[pb].synchronize()
-        n_out = int(self.n_out_host[pb][7])
-        if self.deliver and n_out:
-            with torch.cuda.stream(self.d2h):
-                self.d2h.wait_event(self.ev_comp[pb])
-                src = self.e.t["out1" if pb else "out0"][:n_out * OUT_REC_SIZE]
-                self.out_host[pb][:n_out * OUT_REC_SIZE].copy_(src, non_blocking=True)
-                self.ev_d2h[pb].record(self.d2h)
-        else:
-            self.ev_d2h[pb].record(self.d2h)
+        if self.mode == "push" and self.deliver:
+            self.ev_push[pb].synchronize()
+        n_out = int(self.scal_host[pb][7])
+        if self.deliver and self.on_outbound is not None and n_out:
+            self.on_outbound(self.e.out_host[pb].view(OUT_REC, n_out))
         self.delivered += n_out
         self.pending = None
 
     def flush(self):
         self._drain()
-        self.d2h.synchronize()
         self.comp.synchronize()
+        self.push.synchronize()
 
     def outbound(self, b: int) -> np.ndarray:
-        n = int(self.n_out_host[b][7])
-        return self.out_host[b][:n * OUT_REC_SIZE].numpy().view(OUT_REC)
+        n = int(self.scal_host[b][7])
+        return self.e.out_host[b].view(OUT_REC, n)

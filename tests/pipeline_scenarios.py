@@ -56,6 +56,6 @@ def canon_out(out, names):
     """Order-independent view of outbound rows (event ids of generated rows are order dependent)."""
     rows = []
     for r in out:
-        rows.append((int(r["etype"]), int(r["assignment"]), int(r["device"]), int(r["event_date"]),
+        rows.append((int(r["etype"]), int(r["assignment"]), int(r["event_date"]),
                      round(float(r["v0"]), 9), round(float(r["v1"]), 9), int(r["level"])))
     return sorted(rows)

@@ -84,10 +84,10 @@ def test_event_ids_and_store():
     e = make()
     raw, offs = fleet_batch(2000, seed=11, n_dev=100)
     r = e.step(raw, offs, NOW, presence=False)
-    assert len(np.unique(r.out["event_id"])) == len(r.out)
+    assert len(np.unique(r.event_ids())) == len(r.out)
     cols, eids = e.store_rows()
     assert len(eids) == r.n_persisted
-    assert np.array_equal(np.sort(eids), np.sort(r.out["event_id"]))
+    assert np.array_equal(np.sort(eids), np.sort(r.event_ids()))
     # enrichment: customer/area/asset are the assignment's
     asg = cols["asg"]
     assert (cols["cust"] == asg % 7).all() and (cols["area"] == asg % 5).all() and (cols["asset"] == asg % 3).all()

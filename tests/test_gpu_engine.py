@@ -43,8 +43,11 @@ def test_abi_sizes_match():
     from sitewhere_amd.ops.engine_abi import abi_sizes, SwEngineArgs
     import ctypes
     s = abi_sizes(gpu())
-    assert s["event_rec"] == 80 and s["out_rec"] == 48 and s["name_ref"] == 16
+    assert s["event_rec"] == 80 and s["out_rec"] == 32 and s["name_ref"] == 16
     assert s["engine_args"] == ctypes.sizeof(SwEngineArgs)
+    buf = (ctypes.c_int64 * 8)()
+    gpu().sw_abi_sizes(ctypes.cast(buf, ctypes.c_void_p))
+    assert list(buf[5:8]) == [32, 32, 32]  # SwRegSlot, SwAsgState, SwMsSlot
 
 
 def test_hand_batch_parity():
@@ -97,7 +100,8 @@ def test_presence_parity():
 
 def test_pipelined_runner_matches_sync():
     g, c = pair()
-    runner = PipelinedRunner(g, max_raw_bytes=1 << 20)
+    seen = []
+    runner = PipelinedRunner(g, max_raw_bytes=1 << 20, on_outbound=lambda rows: seen.append(rows.copy()))
     batches = [fleet_batch(2000, seed=300 + k) for k in range(5)]
     total = 0
     for k, (raw, offs) in enumerate(batches):
@@ -106,7 +110,7 @@ def test_pipelined_runner_matches_sync():
         runner.submit(rh, oh, len(offs) - 1, now_ms=NOW + k)
         total += c.step(raw, offs, NOW + k, presence=False).n_persisted
     runner.flush()
-    assert runner.delivered == total
+    assert runner.delivered == total == sum(len(x) for x in seen)
     assert g.stats_dict() == c.stats_dict()
 
 
