@@ -1,0 +1,327 @@
+"""Event bus over the native partitioned commit log (the Kafka data plane, rebuilt).
+
+Reference behaviour reproduced:
+  * keyed records, Kafka-compatible murmur2 partitioning (records for one device token stay
+    ordered on one partition) -- ``MicroserviceKafkaProducer.java:89-107``
+  * consumer groups with partition assignment and rebalance on join/leave, manual offset
+    commits (``enable.auto.commit=false``), at-least-once ``commitAsync`` after processing --
+    ``MicroserviceKafkaConsumer.java:53-133``, ``DirectKafkaConsumer.java:28-41``
+  * independent groups each see the full stream (fan-out: state / rules / connectors)
+  * durable logs + committed offsets survive restarts (``SURVEY §5.4``)
+The storage engine is ``libswnative``'s ``swlog_*`` (C++, CRC-checked append-only segments,
+torn-tail recovery).  Topics are auto-created on first use, as the reference relied on broker
+auto-creation.
+"""
+from __future__ import annotations
+
+import ctypes
+import itertools
+import struct
+import threading
+import time
+import uuid
+from dataclasses import dataclass
+
+import numpy as np
+
+from .._native import native
+
+_FRAME = struct.Struct("<qqII")
+
+
+@dataclass
+class Record:
+    topic: str
+    partition: int
+    offset: int
+    key: bytes | None
+    value: bytes
+    timestamp: int
+
+
+class _Group:
+    def __init__(self):
+        self.members: dict[str, tuple] = {}   # member_id -> (topics tuple, last heartbeat)
+        self.generation = 0
+        self.assignment: dict[str, list[tuple[str, int]]] = {}
+
+
+class EventBus:
+    """In-process broker: topics, partitions, consumer-group coordinator, committed offsets."""
+
+    def __init__(self, directory: str | None = None, default_partitions: int = 8, fsync: bool = False,
+                 session_timeout_s: float = 30.0):
+        self.lib = native()
+        self.h = self.lib.swlog_open(directory.encode() if directory else None, 1 if fsync else 0)
+        self.directory = directory
+        self.default_partitions = default_partitions
+        self.session_timeout_s = session_timeout_s
+        self._topics: dict[str, int] = {}
+        self._lock = threading.RLock()
+        self._cond = threading.Condition(self._lock)
+        self._groups: dict[str, _Group] = {}
+        self._closed = False
+
+    # ------------------------------------------------------------------ topics
+    def topic(self, name: str, partitions: int | None = None) -> int:
+        with self._lock:
+            t = self._topics.get(name)
+            if t is None:
+                t = self.lib.swlog_topic(self.h, name.encode(), partitions or self.default_partitions)
+                self._topics[name] = t
+            return t
+
+    def partitions(self, name: str) -> int:
+        return self.lib.swlog_partitions(self.h, self.topic(name))
+
+    def topics(self) -> list[str]:
+        with self._lock:
+            return sorted(self._topics)
+
+    def end_offset(self, name: str, partition: int) -> int:
+        return self.lib.swlog_end_offset(self.h, self.topic(name), partition)
+
+    def begin_offset(self, name: str, partition: int) -> int:
+        return self.lib.swlog_begin_offset(self.h, self.topic(name), partition)
+
+    def partition_for(self, name: str, key: bytes | None) -> int:
+        n = self.partitions(name)
+        if key is None:
+            return next(self._rr) % n
+        kb = (ctypes.c_char * len(key)).from_buffer_copy(key) if key else None
+        return self.lib.sw_partition_for_key(ctypes.cast(kb, ctypes.c_void_p) if kb else None, len(key), n)
+
+    _rr = itertools.count()
+
+    # ------------------------------------------------------------------ produce
+    def append(self, name: str, partition: int, records: list[tuple[bytes | None, bytes]], ts: int | None = None) -> int:
+        if not records:
+            return -1
+        t = self.topic(name)
+        keys = [k or b"" for k, _ in records]
+        vals = [v for _, v in records]
+        koff = np.zeros(len(records) + 1, np.int64)
+        koff[1:] = np.cumsum([len(k) for k in keys])
+        voff = np.zeros(len(records) + 1, np.int64)
+        voff[1:] = np.cumsum([len(v) for v in vals])
+        kb = np.frombuffer(b"".join(keys) + b"\0", np.uint8)
+        vb = np.frombuffer(b"".join(vals) + b"\0", np.uint8)
+        tsa = np.full(len(records), ts if ts is not None else int(time.time() * 1000), np.int64)
+        first = self.lib.swlog_append_batch(self.h, t, partition, kb.ctypes.data, koff.ctypes.data, vb.ctypes.data,
+                                            voff.ctypes.data, tsa.ctypes.data, len(records))
+        if first < 0:
+            raise RuntimeError(f"append to {name}[{partition}] failed")
+        with self._cond:
+            self._cond.notify_all()
+        return first
+
+    # ------------------------------------------------------------------ fetch
+    def read(self, name: str, partition: int, offset: int, max_records: int = 500, max_bytes: int = 1 << 20):
+        t = self.topic(name)
+        buf = np.empty(max_bytes, np.uint8)
+        n = ctypes.c_int64(0)
+        w = self.lib.swlog_read(self.h, t, partition, offset, max_records, buf.ctypes.data, max_bytes, ctypes.byref(n))
+        if w < 0:
+            return self.read(name, partition, offset, max_records, -w + 64)
+        out = []
+        raw = buf[:w].tobytes()
+        pos = 0
+        for _ in range(n.value):
+            off, ts, kl, vl = _FRAME.unpack_from(raw, pos)
+            pos += _FRAME.size
+            key = raw[pos:pos + kl] if kl else None
+            pos += kl
+            val = raw[pos:pos + vl]
+            pos += vl
+            out.append(Record(name, partition, off, key, val, ts))
+        return out
+
+    def wait(self, timeout_s: float):
+        with self._cond:
+            self._cond.wait(timeout_s)
+
+    # ------------------------------------------------------------------ offsets
+    def commit(self, group: str, name: str, partition: int, offset: int):
+        self.lib.swlog_commit(self.h, group.encode(), self.topic(name), partition, offset)
+
+    def committed(self, group: str, name: str, partition: int) -> int:
+        return self.lib.swlog_committed(self.h, group.encode(), self.topic(name), partition)
+
+    def retain_from(self, name: str, partition: int, offset: int) -> int:
+        return self.lib.swlog_retain_from(self.h, self.topic(name), partition, offset)
+
+    # ------------------------------------------------------------------ group coordinator
+    def join(self, group: str, member_id: str, topics: list[str]) -> int:
+        with self._lock:
+            g = self._groups.setdefault(group, _Group())
+            g.members[member_id] = (tuple(topics), time.time())
+            self._rebalance(group, g)
+            return g.generation
+
+    def leave(self, group: str, member_id: str):
+        with self._lock:
+            g = self._groups.get(group)
+            if g and member_id in g.members:
+                del g.members[member_id]
+                self._rebalance(group, g)
+
+    def heartbeat(self, group: str, member_id: str) -> int:
+        with self._lock:
+            g = self._groups.get(group)
+            if g is None or member_id not in g.members:
+                return -1
+            topics, _ = g.members[member_id]
+            g.members[member_id] = (topics, time.time())
+            # evict members whose session expired (crashed consumers)
+            dead = [m for m, (_, hb) in g.members.items() if time.time() - hb > self.session_timeout_s]
+            if dead:
+                for m in dead:
+                    del g.members[m]
+                self._rebalance(group, g)
+            return g.generation
+
+    def _rebalance(self, group: str, g: _Group):
+        """Range assignor per topic over the sorted member ids."""
+        g.generation += 1
+        g.assignment = {m: [] for m in g.members}
+        topics = sorted({t for ts, _ in g.members.values() for t in ts})
+        for t in topics:
+            subs = sorted(m for m, (ts, _) in g.members.items() if t in ts)
+            if not subs:
+                continue
+            n = self.partitions(t)
+            per, extra = divmod(n, len(subs))
+            p = 0
+            for i, m in enumerate(subs):
+                cnt = per + (1 if i < extra else 0)
+                g.assignment[m].extend((t, q) for q in range(p, p + cnt))
+                p += cnt
+        self._cond.notify_all()
+
+    def assignment(self, group: str, member_id: str) -> tuple[int, list]:
+        with self._lock:
+            g = self._groups.get(group)
+            if g is None:
+                return -1, []
+            return g.generation, list(g.assignment.get(member_id, []))
+
+    def group_members(self, group: str) -> list[str]:
+        with self._lock:
+            g = self._groups.get(group)
+            return sorted(g.members) if g else []
+
+    # ------------------------------------------------------------------ clients
+    def producer(self) -> "Producer":
+        return Producer(self)
+
+    def consumer(self, group: str, topics: list[str], auto_offset_reset: str = "earliest",
+                 member_id: str | None = None) -> "Consumer":
+        return Consumer(self, group, topics, auto_offset_reset, member_id)
+
+    def flush(self):
+        self.lib.swlog_flush(self.h)
+
+    def close(self):
+        if not self._closed:
+            self._closed = True
+            self.lib.swlog_close(self.h)
+
+
+class Producer:
+    def __init__(self, bus: EventBus):
+        self.bus = bus
+        self.sent = 0
+
+    def send(self, topic: str, key: str | bytes | None, value: bytes, partition: int | None = None) -> tuple[int, int]:
+        kb = key.encode() if isinstance(key, str) else key
+        p = self.bus.partition_for(topic, kb) if partition is None else partition
+        off = self.bus.append(topic, p, [(kb, value)])
+        self.sent += 1
+        return p, off
+
+    def send_batch(self, topic: str, records: list[tuple[str | bytes | None, bytes]]):
+        """Group by partition and append each group in one native call (batched produce)."""
+        groups: dict[int, list] = {}
+        for k, v in records:
+            kb = k.encode() if isinstance(k, str) else k
+            groups.setdefault(self.bus.partition_for(topic, kb), []).append((kb, v))
+        for p, recs in groups.items():
+            self.bus.append(topic, p, recs)
+        self.sent += len(records)
+
+
+class Consumer:
+    """Group member: polls its assigned partitions from committed positions; manual commit."""
+
+    def __init__(self, bus: EventBus, group: str, topics: list[str], auto_offset_reset: str = "earliest",
+                 member_id: str | None = None):
+        self.bus, self.group, self.topics = bus, group, list(topics)
+        for t in self.topics:
+            bus.topic(t)
+        self.member_id = member_id or f"{group}-{uuid.uuid4().hex[:8]}"
+        self.reset = auto_offset_reset
+        self.generation = bus.join(group, self.member_id, self.topics)
+        self.positions: dict[tuple[str, int], int] = {}
+        self._assigned: list = []
+        self._refresh()
+        self.closed = False
+
+    def _refresh(self):
+        gen, asg = self.bus.assignment(self.group, self.member_id)
+        self.generation = gen
+        self._assigned = asg
+        newpos = {}
+        for tp in asg:
+            if tp in self.positions:
+                newpos[tp] = self.positions[tp]
+                continue
+            c = self.bus.committed(self.group, *tp)
+            if c >= 0:
+                newpos[tp] = c
+            else:
+                newpos[tp] = self.bus.begin_offset(*tp) if self.reset == "earliest" else self.bus.end_offset(*tp)
+        self.positions = newpos
+
+    def assignment(self) -> list:
+        return list(self._assigned)
+
+    def poll(self, timeout_ms: int = 1000, max_records: int = 500) -> dict[tuple[str, int], list[Record]]:
+        deadline = time.time() + timeout_ms / 1000.0
+        while True:
+            gen = self.bus.heartbeat(self.group, self.member_id)
+            if gen < 0:
+                self.generation = self.bus.join(self.group, self.member_id, self.topics)
+                gen = self.generation
+            if gen != self.generation:
+                self._refresh()
+            out = {}
+            budget = max_records
+            for tp in self._assigned:
+                if budget <= 0:
+                    break
+                recs = self.bus.read(tp[0], tp[1], self.positions[tp], budget)
+                if recs:
+                    out[tp] = recs
+                    self.positions[tp] = recs[-1].offset + 1
+                    budget -= len(recs)
+            if out or time.time() >= deadline:
+                return out
+            self.bus.wait(min(0.05, max(0.0, deadline - time.time())))
+
+    def commit(self, offsets: dict[tuple[str, int], int] | None = None):
+        """Commit positions (next offset to read); default: current positions of all partitions."""
+        for tp, off in (offsets or self.positions).items():
+            self.bus.commit(self.group, tp[0], tp[1], off)
+
+    commit_async = commit
+
+    def seek(self, topic: str, partition: int, offset: int):
+        self.positions[(topic, partition)] = offset
+
+    def lag(self) -> int:
+        return sum(self.bus.end_offset(*tp) - self.positions.get(tp, 0) for tp in self._assigned)
+
+    def close(self):
+        if not self.closed:
+            self.closed = True
+            self.bus.leave(self.group, self.member_id)

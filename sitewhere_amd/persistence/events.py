@@ -1,0 +1,365 @@
+"""Device-event persistence backends for the event-management service.
+
+Reference: ``service-event-management/.../persistence/**``:
+  * MongoDB (``MongoDeviceEventManagement.java``) with the bulk ``DeviceEventBuffer``
+    (10,000-entry queue, flush every 250 ms or 200 docs, ``DeviceEventBuffer.java:40-43, 99-135``)
+  * Cassandra (``CassandraDeviceEventManagement.java``): 7 denormalised tables partitioned by
+    ``(entity, event_type, bucket)`` clustered by ``event_date DESC`` (``:374-398, 419-495``)
+  * InfluxDB (``InfluxDbDeviceEventManagement.java``): batched points (``InfluxDbClient.java:77``)
+Here: :class:`MemoryEventStore` (indexed, bisect-sorted), :class:`SQLiteEventStore` (durable),
+:class:`BucketedEventStore` (the Cassandra time-bucket layout, in memory), :class:`InfluxLineWriter`
+(line protocol over HTTP, batched) and :class:`BufferedEventWriter` (the bulk buffer).  The GPU
+engine's HBM column store is queried through :mod:`sitewhere_amd.persistence.gpu_events`.
+"""
+from __future__ import annotations
+
+import bisect
+import json
+import queue
+import sqlite3
+import threading
+import time
+from collections import defaultdict
+
+from ..models.domain import (DateRangeSearchCriteria, DeviceEvent, DeviceEventIndex, DeviceEventType, SearchResults,
+                             event_from_dict)
+
+_INDEX_FIELD = {
+    DeviceEventIndex.Assignment: "device_assignment_id",
+    DeviceEventIndex.Customer: "customer_id",
+    DeviceEventIndex.Area: "area_id",
+    DeviceEventIndex.Asset: "asset_id",
+}
+
+
+def _in_range(e: DeviceEvent, c: DateRangeSearchCriteria | None) -> bool:
+    if c is None:
+        return True
+    d = e.event_date or 0
+    if c.start_date is not None and d < c.start_date:
+        return False
+    if c.end_date is not None and d > c.end_date:
+        return False
+    return True
+
+
+class DeviceEventStore:
+    def add_events(self, events: list[DeviceEvent]) -> list[DeviceEvent]:
+        raise NotImplementedError
+
+    def get_event_by_id(self, id: str) -> DeviceEvent | None:
+        raise NotImplementedError
+
+    def get_event_by_alternate_id(self, alt: str) -> DeviceEvent | None:
+        raise NotImplementedError
+
+    def list_events(self, event_type: DeviceEventType, index: DeviceEventIndex, entity_ids: list[str],
+                    criteria: DateRangeSearchCriteria | None = None) -> SearchResults:
+        raise NotImplementedError
+
+    def list_command_responses_for_invocation(self, invocation_id: str,
+                                              criteria: DateRangeSearchCriteria | None = None) -> SearchResults:
+        raise NotImplementedError
+
+    def count(self) -> int:
+        raise NotImplementedError
+
+
+class MemoryEventStore(DeviceEventStore):
+    def __init__(self):
+        self._lock = threading.RLock()
+        self._by_id: dict[str, DeviceEvent] = {}
+        self._by_alt: dict[str, str] = {}
+        # (event_type, index, entity_id) -> sorted list of (-date, seq, id)
+        self._idx: dict[tuple, list] = defaultdict(list)
+        self._resp: dict[str, list] = defaultdict(list)
+        self._seq = 0
+
+    def add_events(self, events):
+        with self._lock:
+            for e in events:
+                self._by_id[e.id] = e
+                if e.alternate_id:
+                    self._by_alt[e.alternate_id] = e.id
+                self._seq += 1
+                key = (-(e.event_date or 0), self._seq, e.id)
+                for ix, f in _INDEX_FIELD.items():
+                    v = getattr(e, f)
+                    if v:
+                        bisect.insort(self._idx[(e.event_type, ix, v)], key)
+                if e.event_type == DeviceEventType.CommandResponse and getattr(e, "originating_event_id", None):
+                    bisect.insort(self._resp[e.originating_event_id], key)
+        return events
+
+    def get_event_by_id(self, id):
+        with self._lock:
+            return self._by_id.get(id)
+
+    def get_event_by_alternate_id(self, alt):
+        with self._lock:
+            i = self._by_alt.get(alt)
+            return self._by_id.get(i) if i else None
+
+    def _collect(self, keys_lists, criteria):
+        merged = sorted(set(k for lst in keys_lists for k in lst))
+        with self._lock:
+            evs = [self._by_id[k[2]] for k in merged]
+        evs = [e for e in evs if _in_range(e, criteria)]
+        c = criteria or DateRangeSearchCriteria()
+        return SearchResults(len(evs), c.slice(evs))
+
+    def list_events(self, event_type, index, entity_ids, criteria=None):
+        with self._lock:
+            lists = [list(self._idx.get((event_type, index, i), [])) for i in entity_ids]
+        return self._collect(lists, criteria)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        with self._lock:
+            lst = list(self._resp.get(invocation_id, []))
+        return self._collect([lst], criteria)
+
+    def count(self):
+        with self._lock:
+            return len(self._by_id)
+
+
+class SQLiteEventStore(DeviceEventStore):
+    def __init__(self, path: str = ":memory:"):
+        self._lock = threading.RLock()
+        self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+        self._db.execute("PRAGMA journal_mode=WAL")
+        self._db.execute("""CREATE TABLE IF NOT EXISTS events (id TEXT PRIMARY KEY, alt TEXT, type TEXT,
+                            asg TEXT, cust TEXT, area TEXT, asset TEXT, orig TEXT, date INTEGER, doc TEXT)""")
+        for c in ("alt", "orig"):
+            self._db.execute(f"CREATE INDEX IF NOT EXISTS ev_{c} ON events({c})")
+        for c in ("asg", "cust", "area", "asset"):
+            self._db.execute(f"CREATE INDEX IF NOT EXISTS ev_{c} ON events(type, {c}, date DESC)")
+
+    def add_events(self, events):
+        rows = [(e.id, e.alternate_id, e.event_type.value, e.device_assignment_id, e.customer_id, e.area_id,
+                 e.asset_id, getattr(e, "originating_event_id", None), e.event_date or 0, json.dumps(e.to_dict()))
+                for e in events]
+        with self._lock:
+            self._db.execute("BEGIN")
+            self._db.executemany("INSERT OR REPLACE INTO events VALUES (?,?,?,?,?,?,?,?,?,?)", rows)
+            self._db.execute("COMMIT")
+        return events
+
+    def _one(self, where, arg):
+        with self._lock:
+            r = self._db.execute(f"SELECT doc FROM events WHERE {where}=?", (arg,)).fetchone()
+        return event_from_dict(json.loads(r[0])) if r else None
+
+    def get_event_by_id(self, id):
+        return self._one("id", id)
+
+    def get_event_by_alternate_id(self, alt):
+        return self._one("alt", alt)
+
+    def _search(self, where, args, criteria):
+        c = criteria or DateRangeSearchCriteria()
+        if c.start_date is not None:
+            where += " AND date >= ?"
+            args.append(c.start_date)
+        if c.end_date is not None:
+            where += " AND date <= ?"
+            args.append(c.end_date)
+        with self._lock:
+            total = self._db.execute(f"SELECT COUNT(*) FROM events WHERE {where}", args).fetchone()[0]
+            q = f"SELECT doc FROM events WHERE {where} ORDER BY date DESC"
+            if c.page_size > 0:
+                q += f" LIMIT {int(c.page_size)} OFFSET {int((max(1, c.page_number) - 1) * c.page_size)}"
+            rows = self._db.execute(q, args).fetchall()
+        return SearchResults(total, [event_from_dict(json.loads(r[0])) for r in rows])
+
+    def list_events(self, event_type, index, entity_ids, criteria=None):
+        col = {DeviceEventIndex.Assignment: "asg", DeviceEventIndex.Customer: "cust", DeviceEventIndex.Area: "area",
+               DeviceEventIndex.Asset: "asset"}[index]
+        if not entity_ids:
+            return SearchResults(0, [])
+        qs = ",".join("?" for _ in entity_ids)
+        return self._search(f"type=? AND {col} IN ({qs})", [event_type.value, *entity_ids], criteria)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        return self._search("type=? AND orig=?", [DeviceEventType.CommandResponse.value, invocation_id], criteria)
+
+    def count(self):
+        with self._lock:
+            return self._db.execute("SELECT COUNT(*) FROM events").fetchone()[0]
+
+
+class BucketedEventStore(DeviceEventStore):
+    """Cassandra layout: partition = (entity, event type, time bucket); rows clustered by date DESC.
+
+    Range queries walk buckets newest-first and stop once the page is full, exactly like the
+    reference's bucketed CQL reads (``CassandraDeviceEventManagement.java:419-495``).
+    """
+
+    def __init__(self, bucket_ms: int = 60 * 60 * 1000):
+        self.bucket_ms = bucket_ms
+        self._lock = threading.RLock()
+        self._parts: dict[tuple, list] = defaultdict(list)        # (ix, entity, type, bucket) -> [(-date, id)]
+        self._buckets: dict[tuple, list] = defaultdict(list)      # (ix, entity, type) -> sorted buckets
+        self._by_id: dict[str, DeviceEvent] = {}
+        self._by_alt: dict[str, str] = {}
+        self._resp: dict[str, list] = defaultdict(list)
+
+    def bucket_of(self, date_ms: int) -> int:
+        return int(date_ms // self.bucket_ms)
+
+    def add_events(self, events):
+        with self._lock:
+            for e in events:
+                self._by_id[e.id] = e
+                if e.alternate_id:
+                    self._by_alt[e.alternate_id] = e.id
+                d = e.event_date or 0
+                b = self.bucket_of(d)
+                for ix, f in _INDEX_FIELD.items():
+                    v = getattr(e, f)
+                    if not v:
+                        continue
+                    pk = (ix, v, e.event_type)
+                    bl = self._buckets[pk]
+                    j = bisect.bisect_left(bl, b)
+                    if j == len(bl) or bl[j] != b:
+                        bl.insert(j, b)
+                    bisect.insort(self._parts[pk + (b,)], (-d, e.id))
+                if e.event_type == DeviceEventType.CommandResponse and getattr(e, "originating_event_id", None):
+                    bisect.insort(self._resp[e.originating_event_id], (-d, e.id))
+        return events
+
+    def get_event_by_id(self, id):
+        return self._by_id.get(id)
+
+    def get_event_by_alternate_id(self, alt):
+        i = self._by_alt.get(alt)
+        return self._by_id.get(i) if i else None
+
+    def list_events(self, event_type, index, entity_ids, criteria=None):
+        c = criteria or DateRangeSearchCriteria()
+        rows = []
+        with self._lock:
+            for ent in entity_ids:
+                pk = (index, ent, event_type)
+                for b in reversed(self._buckets.get(pk, [])):
+                    if c.end_date is not None and b * self.bucket_ms > c.end_date:
+                        continue
+                    if c.start_date is not None and (b + 1) * self.bucket_ms <= c.start_date:
+                        break
+                    rows.extend(self._parts[pk + (b,)])
+        rows.sort()
+        evs = [self._by_id[i] for _, i in rows]
+        evs = [e for e in evs if _in_range(e, c)]
+        return SearchResults(len(evs), c.slice(evs))
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        c = criteria or DateRangeSearchCriteria()
+        evs = [self._by_id[i] for _, i in self._resp.get(invocation_id, [])]
+        return SearchResults(len(evs), c.slice(evs))
+
+    def count(self):
+        return len(self._by_id)
+
+
+class BufferedEventWriter:
+    """Bulk write buffer in front of any store (reference DeviceEventBuffer: queue 10,000,
+    flush at 200 docs or every 250 ms).  ``add`` blocks when the queue is full (back-pressure)."""
+
+    def __init__(self, store: DeviceEventStore, max_queue: int = 10_000, chunk: int = 200, interval_ms: int = 250):
+        self.store, self.chunk, self.interval = store, chunk, interval_ms / 1000.0
+        self.q: queue.Queue = queue.Queue(max_queue)
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True, name="event-buffer")
+        self.flushes = 0
+        self._t.start()
+
+    def add(self, events):
+        for e in events:
+            self.q.put(e)
+
+    def _run(self):
+        buf = []
+        last = time.time()
+        while not self._stop.is_set() or not self.q.empty():
+            try:
+                buf.append(self.q.get(timeout=self.interval / 4))
+            except queue.Empty:
+                pass
+            if buf and (len(buf) >= self.chunk or time.time() - last >= self.interval):
+                self.store.add_events(buf)
+                self.flushes += 1
+                buf = []
+                last = time.time()
+        if buf:
+            self.store.add_events(buf)
+            self.flushes += 1
+
+    def flush(self, timeout: float = 5.0):
+        end = time.time() + timeout
+        while not self.q.empty() and time.time() < end:
+            time.sleep(0.01)
+        time.sleep(self.interval * 1.5)
+
+    def close(self):
+        self._stop.set()
+        self._t.join(timeout=5)
+
+
+class InfluxLineWriter:
+    """InfluxDB line-protocol writer with batching (reference InfluxDbClient enableBatch)."""
+
+    def __init__(self, url: str, database: str = "sitewhere", batch: int = 1000, post=None):
+        self.url = url.rstrip("/") + f"/write?db={database}&precision=ms"
+        self.batch = batch
+        self.buf: list[str] = []
+        self._post = post
+        self.sent = 0
+
+    @staticmethod
+    def _esc(s: str) -> str:
+        return str(s).replace(" ", r"\ ").replace(",", r"\,").replace("=", r"\=")
+
+    def line(self, e: DeviceEvent) -> str:
+        tags = {"type": e.event_type.value, "assignment": e.device_assignment_id or "", "device": e.device_id or "",
+                "customer": e.customer_id or "", "area": e.area_id or "", "asset": e.asset_id or ""}
+        fields = {"eid": f'"{e.id}"'}
+        if e.event_type == DeviceEventType.Measurement:
+            fields[f"mx_{self._esc(e.name)}"] = repr(float(e.value))
+        elif e.event_type == DeviceEventType.Location:
+            fields.update(latitude=repr(e.latitude), longitude=repr(e.longitude))
+        elif e.event_type == DeviceEventType.Alert:
+            fields.update(alertType=f'"{e.type}"', alertLevel=f'"{e.level.value}"',
+                          message=json.dumps(e.message))
+        tag_s = ",".join(f"{k}={self._esc(v)}" for k, v in tags.items() if v)
+        field_s = ",".join(f"{k}={v}" for k, v in fields.items())
+        return f"events,{tag_s} {field_s} {int(e.event_date or 0)}"
+
+    def add_events(self, events):
+        self.buf.extend(self.line(e) for e in events)
+        if len(self.buf) >= self.batch:
+            self.flush()
+        return events
+
+    def flush(self):
+        if not self.buf:
+            return
+        body = "\n".join(self.buf).encode()
+        if self._post is not None:
+            self._post(self.url, body)
+        else:
+            import urllib.request
+            urllib.request.urlopen(urllib.request.Request(self.url, data=body, method="POST"), timeout=10).read()
+        self.sent += len(self.buf)
+        self.buf = []
+
+
+def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
+    kind = (kind or "memory").lower()
+    if kind == "memory":
+        return MemoryEventStore()
+    if kind == "sqlite":
+        return SQLiteEventStore(kw.get("path", ":memory:"))
+    if kind in ("cassandra", "bucketed"):
+        return BucketedEventStore(kw.get("bucket_ms", 3600_000))
+    raise ValueError(f"unknown event store {kind!r}")

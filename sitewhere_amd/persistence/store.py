@@ -1,0 +1,300 @@
+"""Entity persistence: one document-store interface with in-memory and SQLite backends.
+
+Reference: the per-service ``persistence/mongodb/*`` implementations over ``sitewhere-mongodb``
+(``MongoDbClient``, ``MongoPersistence``) and the datastore selection of
+``DatastoreConfigurationType.java:18-33``.  MongoDB itself is optional here
+(:class:`MongoEntityStore`, used when ``pymongo`` can reach a server); the in-memory store backs
+tests and single-process deployments, SQLite gives a durable zero-dependency store.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import sqlite3
+import threading
+from typing import Callable, Iterable
+
+from ..models.domain import Model
+
+
+class EntityStore:
+    """Collections of :class:`Model` documents addressed by id and (optionally) unique token."""
+
+    def register(self, collection: str, cls: type[Model], unique_fields: Iterable[str] = ("token",)):
+        raise NotImplementedError
+
+    def put(self, collection: str, entity: Model) -> Model:
+        raise NotImplementedError
+
+    def get(self, collection: str, id: str) -> Model | None:
+        raise NotImplementedError
+
+    def get_by(self, collection: str, field: str, value) -> Model | None:
+        raise NotImplementedError
+
+    def get_by_token(self, collection: str, token: str) -> Model | None:
+        return self.get_by(collection, "token", token)
+
+    def delete(self, collection: str, id: str) -> Model | None:
+        raise NotImplementedError
+
+    def query(self, collection: str, predicate: Callable[[Model], bool] | None = None,
+              sort_key: Callable[[Model], object] | None = None, reverse: bool = False) -> list:
+        raise NotImplementedError
+
+    def count(self, collection: str) -> int:
+        return len(self.query(collection))
+
+    def clear(self):
+        raise NotImplementedError
+
+
+class MemoryEntityStore(EntityStore):
+    def __init__(self):
+        self._lock = threading.RLock()
+        self._data: dict[str, dict[str, Model]] = {}
+        self._idx: dict[str, dict[str, dict]] = {}
+        self._unique: dict[str, tuple] = {}
+
+    def register(self, collection, cls, unique_fields=("token",)):
+        with self._lock:
+            self._data.setdefault(collection, {})
+            self._unique[collection] = tuple(unique_fields)
+            self._idx.setdefault(collection, {f: {} for f in unique_fields})
+
+    def _coll(self, c):
+        if c not in self._data:
+            self.register(c, Model)
+        return self._data[c]
+
+    def put(self, collection, entity):
+        with self._lock:
+            data = self._coll(collection)
+            old = data.get(entity.id)
+            for f in self._unique.get(collection, ()):
+                idx = self._idx[collection][f]
+                if old is not None:
+                    ov = getattr(old, f, None)
+                    if ov is not None and idx.get(ov) == old.id:
+                        del idx[ov]
+                v = getattr(entity, f, None)
+                if v is not None:
+                    other = idx.get(v)
+                    if other is not None and other != entity.id:
+                        from ..core.errors import ErrorCode, SiteWhereSystemException
+                        raise SiteWhereSystemException(ErrorCode.DuplicateToken, detail=f"{collection}.{f}={v} exists")
+                    idx[v] = entity.id
+            data[entity.id] = copy.deepcopy(entity)
+            return copy.deepcopy(entity)
+
+    def get(self, collection, id):
+        with self._lock:
+            e = self._coll(collection).get(id)
+            return copy.deepcopy(e) if e is not None else None
+
+    def get_by(self, collection, field, value):
+        with self._lock:
+            self._coll(collection)
+            idx = self._idx.get(collection, {}).get(field)
+            if idx is not None:
+                i = idx.get(value)
+                return self.get(collection, i) if i is not None else None
+            for e in self._data[collection].values():
+                if getattr(e, field, None) == value:
+                    return copy.deepcopy(e)
+            return None
+
+    def delete(self, collection, id):
+        with self._lock:
+            e = self._coll(collection).pop(id, None)
+            if e is not None:
+                for f in self._unique.get(collection, ()):
+                    v = getattr(e, f, None)
+                    if v is not None:
+                        self._idx[collection][f].pop(v, None)
+            return e
+
+    def query(self, collection, predicate=None, sort_key=None, reverse=False):
+        with self._lock:
+            items = [e for e in self._coll(collection).values() if predicate is None or predicate(e)]
+            items = [copy.deepcopy(e) for e in items]
+        if sort_key is not None:
+            items.sort(key=sort_key, reverse=reverse)
+        return items
+
+    def count(self, collection):
+        with self._lock:
+            return len(self._coll(collection))
+
+    def clear(self):
+        with self._lock:
+            for c in self._data:
+                self._data[c].clear()
+                for f in self._idx[c]:
+                    self._idx[c][f].clear()
+
+
+class SQLiteEntityStore(EntityStore):
+    """Durable JSON-document store (one table per collection, unique-field indexes)."""
+
+    def __init__(self, path: str = ":memory:"):
+        self.path = path
+        self._lock = threading.RLock()
+        self._db = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+        self._db.execute("PRAGMA journal_mode=WAL")
+        self._cls: dict[str, type] = {}
+        self._unique: dict[str, tuple] = {}
+
+    def _t(self, c):
+        return "c_" + "".join(ch if ch.isalnum() else "_" for ch in c)
+
+    def register(self, collection, cls, unique_fields=("token",)):
+        with self._lock:
+            self._cls[collection] = cls
+            self._unique[collection] = tuple(unique_fields)
+            t = self._t(collection)
+            cols = "".join(f", u_{f} TEXT" for f in unique_fields)
+            self._db.execute(f"CREATE TABLE IF NOT EXISTS {t} (id TEXT PRIMARY KEY, doc TEXT NOT NULL{cols})")
+            for f in unique_fields:
+                self._db.execute(f"CREATE UNIQUE INDEX IF NOT EXISTS {t}_u_{f} ON {t}(u_{f})")
+
+    def _ensure(self, c):
+        if c not in self._cls:
+            raise KeyError(f"collection {c!r} not registered")
+
+    def put(self, collection, entity):
+        self._ensure(collection)
+        with self._lock:
+            t = self._t(collection)
+            uf = self._unique[collection]
+            vals = [getattr(entity, f, None) for f in uf]
+            cols = "".join(f", u_{f}" for f in uf)
+            qs = "".join(", ?" for _ in uf)
+            for f, v in zip(uf, vals):
+                if v is None:
+                    continue
+                r = self._db.execute(f"SELECT id FROM {t} WHERE u_{f}=?", (v,)).fetchone()
+                if r and r[0] != entity.id:
+                    from ..core.errors import ErrorCode, SiteWhereSystemException
+                    raise SiteWhereSystemException(ErrorCode.DuplicateToken, detail=f"{collection}.{f}={v} exists")
+            try:
+                self._db.execute(f"INSERT OR REPLACE INTO {t} (id, doc{cols}) VALUES (?, ?{qs})",
+                                 [entity.id, json.dumps(entity.to_dict())] + vals)
+            except sqlite3.IntegrityError as e:
+                from ..core.errors import ErrorCode, SiteWhereSystemException
+                raise SiteWhereSystemException(ErrorCode.DuplicateToken, detail=str(e)) from e
+        return entity
+
+    def _load(self, collection, doc):
+        return self._cls[collection].from_dict(json.loads(doc))
+
+    def get(self, collection, id):
+        self._ensure(collection)
+        with self._lock:
+            r = self._db.execute(f"SELECT doc FROM {self._t(collection)} WHERE id=?", (id,)).fetchone()
+        return self._load(collection, r[0]) if r else None
+
+    def get_by(self, collection, field, value):
+        self._ensure(collection)
+        if field in self._unique[collection]:
+            with self._lock:
+                r = self._db.execute(f"SELECT doc FROM {self._t(collection)} WHERE u_{field}=?", (value,)).fetchone()
+            return self._load(collection, r[0]) if r else None
+        for e in self.query(collection):
+            if getattr(e, field, None) == value:
+                return e
+        return None
+
+    def delete(self, collection, id):
+        e = self.get(collection, id)
+        if e is not None:
+            with self._lock:
+                self._db.execute(f"DELETE FROM {self._t(collection)} WHERE id=?", (id,))
+        return e
+
+    def query(self, collection, predicate=None, sort_key=None, reverse=False):
+        self._ensure(collection)
+        with self._lock:
+            rows = self._db.execute(f"SELECT doc FROM {self._t(collection)}").fetchall()
+        items = [self._load(collection, r[0]) for r in rows]
+        if predicate is not None:
+            items = [e for e in items if predicate(e)]
+        if sort_key is not None:
+            items.sort(key=sort_key, reverse=reverse)
+        return items
+
+    def count(self, collection):
+        self._ensure(collection)
+        with self._lock:
+            return self._db.execute(f"SELECT COUNT(*) FROM {self._t(collection)}").fetchone()[0]
+
+    def clear(self):
+        with self._lock:
+            for c in self._cls:
+                self._db.execute(f"DELETE FROM {self._t(c)}")
+
+
+class MongoEntityStore(EntityStore):
+    """MongoDB backend (reference default).  Requires ``pymongo`` and a reachable server."""
+
+    def __init__(self, uri: str = "mongodb://localhost:27017", database: str = "sitewhere", timeout_ms: int = 3000):
+        import pymongo  # noqa: F401 -- optional dependency
+
+        self._client = pymongo.MongoClient(uri, serverSelectionTimeoutMS=timeout_ms)
+        self._db = self._client[database]
+        self._cls: dict[str, type] = {}
+
+    def register(self, collection, cls, unique_fields=("token",)):
+        import pymongo
+        self._cls[collection] = cls
+        for f in unique_fields:
+            self._db[collection].create_index([(f, pymongo.ASCENDING)], unique=True, sparse=True)
+
+    def put(self, collection, entity):
+        d = entity.to_dict()
+        d["_id"] = entity.id
+        self._db[collection].replace_one({"_id": entity.id}, d, upsert=True)
+        return entity
+
+    def _load(self, collection, d):
+        if d is None:
+            return None
+        d = dict(d)
+        d.pop("_id", None)
+        return self._cls[collection].from_dict(d)
+
+    def get(self, collection, id):
+        return self._load(collection, self._db[collection].find_one({"_id": id}))
+
+    def get_by(self, collection, field, value):
+        from ..models.domain import camel
+        return self._load(collection, self._db[collection].find_one({camel(field): value}))
+
+    def delete(self, collection, id):
+        e = self.get(collection, id)
+        self._db[collection].delete_one({"_id": id})
+        return e
+
+    def query(self, collection, predicate=None, sort_key=None, reverse=False):
+        items = [self._load(collection, d) for d in self._db[collection].find({})]
+        if predicate is not None:
+            items = [e for e in items if predicate(e)]
+        if sort_key is not None:
+            items.sort(key=sort_key, reverse=reverse)
+        return items
+
+    def clear(self):
+        for c in self._cls:
+            self._db[c].delete_many({})
+
+
+def create_store(kind: str = "memory", **kw) -> EntityStore:
+    """Datastore factory (reference DatastoreConfigurationParser): memory | sqlite | mongodb."""
+    kind = (kind or "memory").lower()
+    if kind == "memory":
+        return MemoryEntityStore()
+    if kind == "sqlite":
+        return SQLiteEntityStore(kw.get("path", ":memory:"))
+    if kind in ("mongo", "mongodb"):
+        return MongoEntityStore(kw.get("uri", "mongodb://localhost:27017"), kw.get("database", "sitewhere"))
+    raise ValueError(f"unknown datastore type {kind!r}")

@@ -44,6 +44,7 @@ class CpuInboundEngine(EngineBase):
     def __init__(self, cfg: EngineConfig, group=None):
         super().__init__(cfg)
         self.group = group
+        self.exchange = None
         self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
         self.cursor = 0
         self.seq_base = 0
@@ -58,12 +59,8 @@ class CpuInboundEngine(EngineBase):
         self._seen: set[int] = set()
 
     # ------------------------------------------------------------------ stages
-    def _shuffle(self, recs: np.ndarray) -> np.ndarray:
-        if self.world == 1:
-            return recs
-        import torch
-        import torch.distributed as dist
-
+    def partition(self, recs: np.ndarray):
+        """Stable owner partition into [world, shuf_cap] slabs (same as k_part_count/k_part_write)."""
         owner = np.where(recs["etype"] >= 16, self.rank, (recs["fp_hi"] >> np.uint64(32)) % np.uint64(self.world))
         cap = self.cfg.shuf_cap
         send = np.zeros((self.world, cap), EVENT_REC)
@@ -74,15 +71,29 @@ class CpuInboundEngine(EngineBase):
             self.stats[10] += len(sel) - k
             send[o, :k] = sel[:k]
             cnt[o] = k
+        return send, cnt
+
+    @staticmethod
+    def unpack(recv: np.ndarray, rcnt) -> np.ndarray:
+        return np.concatenate([recv[q, :int(rcnt[q])] for q in range(recv.shape[0])])
+
+    def _shuffle(self, recs: np.ndarray) -> np.ndarray:
+        if self.world == 1:
+            return recs
+        if self.exchange is not None:          # loopback / custom transport
+            return self.exchange(self, recs)
+        import torch
+        import torch.distributed as dist
+
+        send, cnt = self.partition(recs)
         send_t = torch.from_numpy(send.view(np.uint8).reshape(-1).copy())
         recv_t = torch.empty_like(send_t)
         cnt_t = torch.from_numpy(cnt)
         rcnt_t = torch.empty_like(cnt_t)
         dist.all_to_all_single(rcnt_t, cnt_t, group=self.group)
         dist.all_to_all_single(recv_t, send_t, group=self.group)
-        recv = recv_t.numpy().view(EVENT_REC).reshape(self.world, cap)
-        rc = rcnt_t.numpy()
-        return np.concatenate([recv[q, :rc[q]] for q in range(self.world)])
+        recv = recv_t.numpy().view(EVENT_REC).reshape(self.world, self.cfg.shuf_cap)
+        return self.unpack(recv, rcnt_t.numpy())
 
     def _lookup(self, recs):
         n = len(recs)
@@ -183,8 +194,11 @@ class CpuInboundEngine(EngineBase):
 
     # ------------------------------------------------------------------ step
     def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
-        n_msgs = len(offs) - 1
-        first_seq = self.cursor
+        recs, new = self.decode_phase(raw, offs, now_ms)
+        work = self._shuffle(recs)
+        return self.process_phase(work, len(offs) - 1, now_ms, new, presence)
+
+    def decode_phase(self, raw, offs, now_ms):
         recs = cpu_decode(raw, offs, now_ms, self.rank, cap=self.cfg.rec_cap)
         # new-name capture on the source rank
         refs = []
@@ -195,7 +209,10 @@ class CpuInboundEngine(EngineBase):
                 refs.append((h, int(r["aux_off"]), int(r["aux_len"]), int(r["src_rank"]), int(r["etype"])))
         from ..models.columnar import NAME_REF
         new = self.learn_names(np.array(refs, NAME_REF), raw) if refs else {}
-        work = self._shuffle(recs)
+        return recs, new
+
+    def process_phase(self, work, n_msgs, now_ms, new, presence=None) -> StepResult:
+        first_seq = self.cursor
         status, dev, asg = self._lookup(work)
         self._dedup(work, status)
         ok = np.nonzero(status == ST_OK)[0]

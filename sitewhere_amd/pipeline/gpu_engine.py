@@ -242,6 +242,14 @@ class GpuInboundEngine(EngineBase):
     def step_async(self, raw_dev: torch.Tensor, off_dev: torch.Tensor, n_msgs: int, now_ms: int,
                    presence: bool = False, out_sel: int | None = None, out_to_device: bool = False):
         """Enqueue one micro-batch on the current stream.  raw_dev needs >= 16 B of tail padding."""
+        sel = self.prepare(raw_dev, off_dev, n_msgs, now_ms, presence, out_sel, out_to_device)
+        self.phase_decode()
+        if self.world > 1:
+            self.phase_exchange()
+        self.phase_process()
+        return sel
+
+    def prepare(self, raw_dev, off_dev, n_msgs, now_ms, presence=False, out_sel=None, out_to_device=False):
         if n_msgs > self.cfg.max_msgs:
             raise ValueError(f"batch of {n_msgs} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
         a = self.args
@@ -249,28 +257,50 @@ class GpuInboundEngine(EngineBase):
         a.batch_seq = self.batch_seq
         a.presence_missing_ms = self.cfg.presence_missing_ms if presence else 0
         sel = self._out_sel if out_sel is None else out_sel
+        self._last_sel = sel
         a.out = _ptr(self.out_dev[sel]) if out_to_device else self.out_host[sel].dev
-        s = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        ap = ctypes.byref(a)
-        rc = self.lib.sw_phase_decode(ap, s)
+        return sel
+
+    # The three phases of a step (split so a multi-rank step can be driven without torch.distributed,
+    # e.g. the loopback test that runs W engine shards on one GPU).
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def phase_decode(self):
+        ap = ctypes.byref(self.args)
+        rc = self.lib.sw_phase_decode(ap, self._stream())
         if rc:
             raise RuntimeError(f"sw_phase_decode failed ({rc})")
         if self.world > 1:
-            import torch.distributed as dist
-
-            rc = self.lib.sw_phase_partition(ap, s)
+            rc = self.lib.sw_phase_partition(ap, self._stream())
             if rc:
                 raise RuntimeError(f"sw_phase_partition failed ({rc})")
-            dist.all_to_all_single(self.t["recv_cnt"], self.t["send_cnt"], group=self.group)
-            dist.all_to_all_single(self.t["recv"], self.t["send"], group=self.group)
-            rc = self.lib.sw_phase_unpack(ap, s)
+
+    def phase_exchange(self):
+        """RCCL all-to-all re-keying of the per-owner slabs (the Kafka key-partitioning analogue)."""
+        import torch.distributed as dist
+
+        dist.all_to_all_single(self.t["recv_cnt"], self.t["send_cnt"], group=self.group)
+        dist.all_to_all_single(self.t["recv"], self.t["send"], group=self.group)
+
+    def phase_process(self):
+        ap = ctypes.byref(self.args)
+        if self.world > 1:
+            rc = self.lib.sw_phase_unpack(ap, self._stream())
             if rc:
                 raise RuntimeError(f"sw_phase_unpack failed ({rc})")
-        rc = self.lib.sw_phase_process(ap, ctypes.c_void_p(self._rule_scratch), s)
+        rc = self.lib.sw_phase_process(ap, ctypes.c_void_p(self._rule_scratch), self._stream())
         if rc:
             raise RuntimeError(f"sw_phase_process failed ({rc})")
         self.batch_seq += 1
-        return sel
+
+    def send_slab(self, q: int) -> torch.Tensor:
+        n = self.cfg.shuf_cap * EVENT_REC.itemsize
+        return self.t["send"][q * n:(q + 1) * n]
+
+    def recv_slab(self, q: int) -> torch.Tensor:
+        n = self.cfg.shuf_cap * EVENT_REC.itemsize
+        return self.t["recv"][q * n:(q + 1) * n]
 
     def scalars(self) -> dict:
         v = self.t["scalars"][:9].cpu().numpy()

@@ -1,0 +1,333 @@
+"""Unit tests: lifecycle FSM, JWT, tracing, metrics, bus, coordination, persistence."""
+import threading
+import time
+
+import pytest
+
+from sitewhere_amd.core.errors import ServerStartupException, SiteWhereException, UnauthorizedException
+from sitewhere_amd.core.lifecycle import (CompositeLifecycleStep, LifecycleComponent, LifecycleProgressMonitor,
+                                          LifecycleStatus, LifecycleComponentParameter, SimpleLifecycleStep)
+from sitewhere_amd.core.metrics import MetricRegistry
+from sitewhere_amd.core.security import (Authentication, TokenManagement, current_tenant, security_context,
+                                         hash_password, verify_password)
+from sitewhere_amd.core.tracing import Tracer
+
+
+class Boom(LifecycleComponent):
+    def __init__(self, where):
+        super().__init__("boom")
+        self.where = where
+
+    def initialize(self, m):
+        if self.where == "init":
+            raise RuntimeError("init failed")
+
+    def start(self, m):
+        if self.where == "start":
+            raise RuntimeError("start failed")
+
+
+class Parent(LifecycleComponent):
+    def __init__(self, child, require):
+        super().__init__("parent")
+        self.child, self.require = child, require
+
+    def initialize(self, m):
+        self.initialize_nested_component(self.child, m, self.require)
+
+    def start(self, m):
+        self.start_nested_component(self.child, m, self.require)
+
+
+def test_lifecycle_happy_path_and_terminate():
+    c = LifecycleComponent("c")
+    seen = []
+    c.add_status_listener(lambda comp, old, new: seen.append(new))
+    c.lifecycle_initialize()
+    assert c.status == LifecycleStatus.Stopped
+    c.lifecycle_start()
+    assert c.status == LifecycleStatus.Started
+    c.lifecycle_stop()
+    c.lifecycle_terminate()
+    assert c.status == LifecycleStatus.Terminated
+    assert seen[:2] == [LifecycleStatus.Initializing, LifecycleStatus.Stopped]
+
+
+def test_lifecycle_errors_and_required_children():
+    b = Boom("init")
+    b.lifecycle_initialize()
+    assert b.status == LifecycleStatus.InitializationError and b.lifecycle_error
+    p = Parent(Boom("init"), require=True)
+    p.lifecycle_initialize()
+    assert p.status == LifecycleStatus.InitializationError
+    assert isinstance(p.lifecycle_error.__cause__, ServerStartupException)
+    # optional child failing at start -> StartedWithErrors
+    p2 = Parent(Boom("start"), require=False)
+    p2.lifecycle_initialize()
+    p2.lifecycle_start()
+    assert p2.status == LifecycleStatus.StartedWithErrors
+    p2.lifecycle_stop()
+    assert p2.status == LifecycleStatus.StoppedWithErrors
+
+
+def test_required_parameter_validation():
+    c = LifecycleComponent("p")
+    c.parameters.append(LifecycleComponentParameter("host", required=True))
+    c.lifecycle_initialize()
+    assert c.status == LifecycleStatus.InitializationError
+
+
+def test_composite_step_aborts_and_reports():
+    msgs = []
+    mon = LifecycleProgressMonitor(listener=msgs.append)
+    order = []
+    step = CompositeLifecycleStep("boot", [SimpleLifecycleStep("a", lambda m: order.append("a")),
+                                           SimpleLifecycleStep("b", lambda m: (_ for _ in ()).throw(SiteWhereException("x"))),
+                                           SimpleLifecycleStep("c", lambda m: order.append("c"))])
+    with pytest.raises(SiteWhereException):
+        step.execute(mon)
+    assert order == ["a"] and [m["task"] for m in msgs] == ["a", "b"]
+
+
+def test_jwt_roundtrip_and_tamper():
+    tm = TokenManagement("s3cret", expiration_minutes=5)
+    tok = tm.generate_token("admin", ["REST", "ADMINISTER_USERS"])
+    assert tm.get_username(tok) == "admin"
+    assert tm.get_granted_authorities(tok) == ["REST", "ADMINISTER_USERS"]
+    with pytest.raises(UnauthorizedException):
+        TokenManagement("other").get_claims(tok)
+    with pytest.raises(UnauthorizedException):
+        tm.get_claims(TokenManagement("s3cret", expiration_minutes=-1).generate_token("a", []))
+
+
+def test_security_context_is_scoped_per_thread():
+    out = {}
+
+    def worker(name):
+        with security_context(Authentication(name, tenant=name)):
+            time.sleep(0.01)
+            out[name] = current_tenant()
+
+    ts = [threading.Thread(target=worker, args=(f"t{i}",)) for i in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert out == {f"t{i}": f"t{i}" for i in range(8)}
+    assert current_tenant() is None
+
+
+def test_password_hashing():
+    h = hash_password("pw")
+    assert verify_password("pw", h) and not verify_password("nope", h)
+
+
+def test_tracing_propagation_and_errors():
+    tr = Tracer(sample_rate=1.0)
+    with tr.start_span("outer") as o:
+        with tr.start_span("inner") as i:
+            pass
+        hdr = o.context_header()
+    remote = tr.start_span("remote-child", child_of=hdr)
+    remote.finish()
+    spans = tr.export()
+    names = [s["name"] for s in spans]
+    assert names == ["inner", "outer", "remote-child"]
+    assert spans[0]["parentId"] == spans[1]["spanId"]
+    assert spans[2]["traceId"] == spans[1]["traceId"]
+    with pytest.raises(ValueError):
+        with tr.start_span("bad"):
+            raise ValueError("x")
+    assert tr.export()[-1]["tags"]["error"] is True
+
+
+def test_metrics_and_prometheus():
+    r = MetricRegistry()
+    r.meter("t1.decodedEvents").mark(5)
+    with r.timer("t1.eventStorage").time():
+        pass
+    r.counter("c").inc(3)
+    snap = r.snapshot()
+    assert snap["t1.decodedEvents"]["count"] == 5 and snap["c"]["count"] == 3
+    text = r.prometheus()
+    assert "sitewhere_t1_decodedEvents_total 5" in text
+
+
+# ------------------------------------------------------------------------------ bus
+def test_bus_key_partitioning_groups_and_commit(tmp_path):
+    from sitewhere_amd.bus.log import EventBus
+    bus = EventBus(str(tmp_path / "log"), default_partitions=4)
+    p = bus.producer()
+    for i in range(200):
+        p.send("t", f"dev-{i % 10}", f"v{i}".encode())
+    # same key -> same partition, in order
+    parts = {}
+    c = bus.consumer("g1", ["t"])
+    got = []
+    while True:
+        batch = c.poll(200)
+        if not batch:
+            break
+        for tp, recs in batch.items():
+            for r in recs:
+                parts.setdefault(r.key, set()).add(tp[1])
+                got.append(r.value)
+    assert len(got) == 200 and all(len(v) == 1 for v in parts.values())
+    c.commit()
+    # an independent group sees the full stream (fan-out)
+    c2 = bus.consumer("g2", ["t"])
+    n2 = sum(len(r) for r in c2.poll(500, max_records=1000).values())
+    assert n2 == 200
+    c.close()
+    c2.close()
+    bus.close()
+    # durability: reopen, committed offsets resume where g1 left
+    bus2 = EventBus(str(tmp_path / "log"), default_partitions=4)
+    p2 = bus2.producer()
+    p2.send("t", "dev-1", b"after-restart")
+    c3 = bus2.consumer("g1", ["t"])
+    vals = [r.value for recs in c3.poll(500).values() for r in recs]
+    assert vals == [b"after-restart"]
+    bus2.close()
+
+
+def test_bus_rebalance_splits_partitions():
+    from sitewhere_amd.bus.log import EventBus
+    bus = EventBus(None, default_partitions=8)
+    bus.topic("x")
+    a = bus.consumer("g", ["x"], member_id="a")
+    b = bus.consumer("g", ["x"], member_id="b")
+    a.poll(10)
+    b.poll(10)
+    pa, pb = {p for _, p in a.assignment()}, {p for _, p in b.assignment()}
+    assert len(pa) == len(pb) == 4 and not (pa & pb)
+    b.close()
+    a.poll(10)
+    assert len(a.assignment()) == 8
+
+
+def test_bus_at_least_once_redelivery_after_crash():
+    from sitewhere_amd.bus.log import EventBus
+    bus = EventBus(None, default_partitions=1)
+    prod = bus.producer()
+    for i in range(10):
+        prod.send("q", "k", str(i).encode())
+    c = bus.consumer("g", ["q"], member_id="m1")
+    first = [r.value for recs in c.poll(100, max_records=5).values() for r in recs]
+    c.commit()
+    c.poll(100, max_records=5)  # processed but NOT committed -> "crash"
+    c.close()
+    c2 = bus.consumer("g", ["q"], member_id="m2")
+    again = [r.value for recs in c2.poll(100).values() for r in recs]
+    assert first == [b"0", b"1", b"2", b"3", b"4"] and again[0] == b"5" and len(again) == 5
+
+
+def test_murmur2_matches_kafka_reference_values(native_lib):
+    import ctypes
+    # Kafka's Utils.murmur2 test vectors
+    vecs = {b"21": -973932308, b"foobar": -790332482, b"a-little-bit-long-string": -985981536,
+            b"a-little-bit-longer-string": -1486304829, b"lkjh234lh9fiuh90y23oiuhsafujhadof229phr9h19h89h8": -58897971,
+            b"abc": 479470107}
+    for k, want in vecs.items():
+        buf = ctypes.create_string_buffer(k, len(k))
+        assert native_lib.sw_murmur2(ctypes.cast(buf, ctypes.c_void_p), len(k)) == want
+
+
+# ------------------------------------------------------------------------------ coordination
+def test_coordination_watch_versions_ephemeral_and_mutex(tmp_path):
+    from sitewhere_amd.coord.store import (BadVersionError, Coordination, InterProcessMutex, NODE_ADDED,
+                                           NODE_UPDATED, NODE_REMOVED, INITIALIZED)
+    co = Coordination(str(tmp_path / "zk.json"))
+    co.create("/sw/conf/a.xml", b"1")
+    events = []
+    co.watch_tree("/sw/conf", lambda k, p, d: events.append((k, p)))
+    time.sleep(0.05)
+    st = co.set("/sw/conf/a.xml", b"2")
+    with pytest.raises(BadVersionError):
+        co.set("/sw/conf/a.xml", b"3", version=st.version - 1)
+    s = co.open_session()
+    co.create("/sw/live/m1", b"", ephemeral=True, session=s)
+    co.delete("/sw/conf/a.xml")
+    time.sleep(0.1)
+    kinds = [k for k, _ in events]
+    assert INITIALIZED in kinds and NODE_UPDATED in kinds and NODE_REMOVED in kinds and NODE_ADDED in kinds
+    co.close_session(s)
+    assert co.exists("/sw/live/m1") is None
+    # mutex contention: only one holder at a time
+    holders = []
+    lock_log = []
+
+    def worker(i):
+        with InterProcessMutex(co, "/sw/locks/boot"):
+            holders.append(i)
+            lock_log.append(len(holders))
+            time.sleep(0.02)
+            holders.remove(i)
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert max(lock_log) == 1 and len(lock_log) == 4
+    # snapshot durability
+    co.put("/sw/conf/b.xml", b"keep")
+    co2 = Coordination(str(tmp_path / "zk.json"))
+    assert co2.get_data("/sw/conf/b.xml") == b"keep"
+    assert co2.exists("/sw/live/m1") is None
+
+
+# ------------------------------------------------------------------------------ persistence
+@pytest.mark.parametrize("kind", ["memory", "sqlite"])
+def test_entity_store(kind):
+    from sitewhere_amd.models.domain import Device, DeviceType
+    from sitewhere_amd.persistence.store import create_store
+    from sitewhere_amd.core.errors import SiteWhereSystemException
+    s = create_store(kind)
+    s.register("devices", Device)
+    s.register("types", DeviceType)
+    d = Device(token="d1", comments="x", metadata={"a": "b"})
+    s.put("devices", d)
+    assert s.get_by_token("devices", "d1").metadata == {"a": "b"}
+    with pytest.raises(SiteWhereSystemException):
+        s.put("devices", Device(token="d1"))
+    d2 = s.get("devices", d.id)
+    d2.comments = "y"
+    s.put("devices", d2)
+    assert s.get("devices", d.id).comments == "y"
+    assert len(s.query("devices", lambda e: e.comments == "y")) == 1
+    s.delete("devices", d.id)
+    assert s.get_by_token("devices", "d1") is None
+
+
+@pytest.mark.parametrize("kind", ["memory", "sqlite", "bucketed"])
+def test_event_store_queries(kind):
+    from sitewhere_amd.models.domain import (DateRangeSearchCriteria, DeviceEventIndex, DeviceEventType,
+                                             DeviceMeasurement, DeviceCommandResponse)
+    from sitewhere_amd.persistence.events import create_event_store
+    es = create_event_store(kind, bucket_ms=1000)
+    evs = [DeviceMeasurement(device_assignment_id="a1" if i % 2 else "a2", customer_id="c", name="t", value=i,
+                             event_date=1000 * i, alternate_id=f"alt{i}") for i in range(20)]
+    es.add_events(evs)
+    r = es.list_events(DeviceEventType.Measurement, DeviceEventIndex.Assignment, ["a1"],
+                       DateRangeSearchCriteria(page_size=3, start_date=2000, end_date=15000))
+    assert r.num_results == 7 and [e.value for e in r.results] == [15, 13, 11]
+    r2 = es.list_events(DeviceEventType.Measurement, DeviceEventIndex.Customer, ["c"], DateRangeSearchCriteria(page_size=0))
+    assert r2.num_results == 20 and r2.results[0].value == 19
+    assert es.get_event_by_alternate_id("alt4").value == 4
+    resp = DeviceCommandResponse(originating_event_id=evs[0].id, device_assignment_id="a2", response="ok",
+                                 event_date=5)
+    es.add_events([resp])
+    assert es.list_command_responses_for_invocation(evs[0].id).results[0].response == "ok"
+
+
+def test_buffered_writer_and_influx_lines():
+    from sitewhere_amd.models.domain import DeviceLocation, DeviceMeasurement
+    from sitewhere_amd.persistence.events import BufferedEventWriter, InfluxLineWriter, MemoryEventStore
+    st = MemoryEventStore()
+    w = BufferedEventWriter(st, chunk=50, interval_ms=50)
+    w.add([DeviceMeasurement(device_assignment_id="a", name="x", value=i, event_date=i) for i in range(120)])
+    w.flush()
+    w.close()
+    assert st.count() == 120 and w.flushes >= 3
+    posted = []
+    iw = InfluxLineWriter("http://influx:8086", batch=2, post=lambda url, body: posted.append((url, body)))
+    iw.add_events([DeviceMeasurement(device_assignment_id="a", name="temp", value=1.5, event_date=7),
+                   DeviceLocation(device_assignment_id="a", latitude=1.0, longitude=2.0, event_date=8)])
+    assert posted and b"mx_temp=1.5" in posted[0][1] and b"latitude=1.0" in posted[0][1]
