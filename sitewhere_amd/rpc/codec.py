@@ -1,0 +1,87 @@
+"""Wire codec for the RPC plane and bus payloads: JSON with tagged domain models.
+
+Every :class:`~sitewhere_amd.models.domain.Model` travels as ``{"__t": "<ClassName>", ...camelCase}``
+and is rebuilt on the other side, so service APIs exchange the same typed objects in-process and
+over gRPC.  (The reference used generated protobuf ``G*`` messages + hand-written ``*ModelConverter``
+classes per service; one generic codec replaces ~20k lines of converters.)
+"""
+from __future__ import annotations
+
+import base64
+import enum
+import json
+
+from ..models import domain
+
+_REGISTRY: dict[str, type] = {}
+
+
+def register_models(module=domain):
+    for name in dir(module):
+        obj = getattr(module, name)
+        if isinstance(obj, type) and issubclass(obj, domain.Model) and obj is not domain.Model:
+            _REGISTRY[obj.__name__] = obj
+
+
+register_models()
+
+
+def to_wire(obj):
+    if isinstance(obj, domain.SearchResults):
+        return {"__t": "SearchResults", "numResults": obj.num_results, "results": [to_wire(r) for r in obj.results]}
+    if isinstance(obj, domain.Model):
+        d = {"__t": type(obj).__name__}
+        for k, v in obj.to_dict().items():
+            d[k] = v
+        # nested models keep their own tags for polymorphic fields
+        import dataclasses
+        for f in dataclasses.fields(obj):
+            v = getattr(obj, f.name)
+            if isinstance(v, domain.Model):
+                d[domain.camel(f.name)] = to_wire(v)
+            elif isinstance(v, list) and v and isinstance(v[0], domain.Model):
+                d[domain.camel(f.name)] = [to_wire(x) for x in v]
+            elif isinstance(v, bytes):
+                d[domain.camel(f.name)] = {"__b": base64.b64encode(v).decode()}
+        return d
+    if isinstance(obj, bytes):
+        return {"__b": base64.b64encode(obj).decode()}
+    if isinstance(obj, enum.Enum):
+        return obj.value
+    if isinstance(obj, (list, tuple)):
+        return [to_wire(x) for x in obj]
+    if isinstance(obj, dict):
+        return {k: to_wire(v) for k, v in obj.items()}
+    return obj
+
+
+def from_wire(obj):
+    if isinstance(obj, list):
+        return [from_wire(x) for x in obj]
+    if isinstance(obj, dict):
+        if "__b" in obj and len(obj) == 1:
+            return base64.b64decode(obj["__b"])
+        t = obj.get("__t")
+        if t == "SearchResults":
+            return domain.SearchResults(obj.get("numResults", 0), [from_wire(r) for r in obj.get("results", [])])
+        if t is not None and t in _REGISTRY:
+            body = {k: (from_wire(v) if isinstance(v, (dict, list)) else v) for k, v in obj.items() if k != "__t"}
+            cls = _REGISTRY[t]
+            m = cls.from_dict({k: v for k, v in body.items() if not isinstance(v, domain.Model)})
+            import dataclasses
+            names = {domain.camel(f.name): f.name for f in dataclasses.fields(cls)}
+            for k, v in body.items():
+                if k in names and (isinstance(v, (domain.Model, bytes)) or
+                                   (isinstance(v, list) and v and isinstance(v[0], domain.Model))):
+                    setattr(m, names[k], v)
+            return m
+        return {k: from_wire(v) for k, v in obj.items()}
+    return obj
+
+
+def dumps(obj) -> bytes:
+    return json.dumps(to_wire(obj), separators=(",", ":")).encode()
+
+
+def loads(b: bytes):
+    return from_wire(json.loads(b)) if b else None

@@ -1,0 +1,144 @@
+"""Bus consumer/producer components and the near cache.
+
+Reference:
+  * ``kafka/MicroserviceKafkaConsumer.java:53-133`` -- one consumer per component on its own poll
+    thread, manual commits, per-partition ``process()``, shutdown via wakeup
+  * ``kafka/DirectKafkaConsumer.java:28-41`` -- process then ``commitAsync`` (at-least-once)
+  * ``KafkaOutboundConnectorHost.java:144-217`` -- pool hand-off (the reference commits *before*
+    the async batch completes = at-most-once; here the commit waits for the batch: at-least-once)
+  * ``sitewhere-grpc-client/.../cache/CacheProvider.java`` + ``NearCacheManager.java:77-165`` --
+    near caches (LRU 10,000, TTL 60 s) for device / assignment / type lookups; invalidated by the
+    device-model change feed instead of a Hazelcast grid.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from collections import OrderedDict
+from concurrent.futures import ThreadPoolExecutor, wait
+
+from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
+
+
+class BusConsumer(TenantEngineLifecycleComponent):
+    component_type = LifecycleComponentType.Other
+
+    def __init__(self, engine, name: str, topics: list[str], handler, threads: int = 0, max_records: int = 500,
+                 group: str | None = None):
+        super().__init__(name)
+        self.tenant_engine = engine
+        self.engine = engine
+        self.topics = topics
+        self.handler = handler            # handler(list[Record]) per partition batch
+        self.threads = threads
+        self.max_records = max_records
+        inst = engine.ms.instance
+        self.group = group or f"{inst.naming.prefix()}.{engine.tenant.token}.{engine.ms.identifier}.{name}"
+        self._stop = threading.Event()
+        self._t = None
+        self.processed = 0
+        self.failures = 0
+
+    def start(self, monitor):
+        bus = self.engine.ms.instance.bus
+        self.consumer = bus.consumer(self.group, self.topics, auto_offset_reset="earliest")
+        self.pool = ThreadPoolExecutor(max_workers=self.threads, thread_name_prefix=self.component_name) if self.threads else None
+        self._stop.clear()
+        self._t = threading.Thread(target=self._run, daemon=True, name=f"consumer-{self.component_name}")
+        self._t.start()
+
+    def _call(self, recs):
+        try:
+            self.handler(recs)
+            self.processed += len(recs)
+        except Exception:
+            self.failures += len(recs)
+            self.logger.exception("consumer %s failed to process %d records", self.component_name, len(recs))
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                batch = self.consumer.poll(100, self.max_records)
+            except Exception:
+                self.logger.exception("poll failed")
+                time.sleep(0.1)
+                continue
+            if not batch:
+                continue
+            if self.pool is None:
+                for recs in batch.values():
+                    self._call(recs)
+            else:
+                futs = []
+                for recs in batch.values():
+                    step = max(1, len(recs) // self.threads)
+                    futs += [self.pool.submit(self._call, recs[i:i + step]) for i in range(0, len(recs), step)]
+                wait(futs)
+            self.consumer.commit()   # after processing: at-least-once
+
+    def stop(self, monitor):
+        self._stop.set()
+        if self._t:
+            self._t.join(timeout=3)
+        if getattr(self, "consumer", None):
+            self.consumer.close()
+        if self.pool:
+            self.pool.shutdown(wait=True)
+
+    def drain(self, timeout_s: float = 10.0) -> bool:
+        """Wait until every assigned partition is consumed and committed (tests / shutdown)."""
+        end = time.time() + timeout_s
+        bus = self.engine.ms.instance.bus
+        while time.time() < end:
+            lag = 0
+            for t in self.topics:
+                for p in range(bus.partitions(t)):
+                    c = bus.committed(self.group, t, p)
+                    lag += bus.end_offset(t, p) - max(c, 0)
+            if lag == 0:
+                return True
+            time.sleep(0.02)
+        return False
+
+
+class NearCache:
+    """Thread-safe LRU with TTL (reference near cache: 10,000 entries, TTL 60 s)."""
+
+    def __init__(self, capacity: int = 10_000, ttl_s: float = 60.0):
+        self.capacity, self.ttl = capacity, ttl_s
+        self._d: OrderedDict = OrderedDict()
+        self._lock = threading.Lock()
+        self.hits = self.misses = 0
+
+    def get(self, key, loader=None):
+        now = time.time()
+        with self._lock:
+            v = self._d.get(key)
+            if v is not None and now - v[1] < self.ttl:
+                self._d.move_to_end(key)
+                self.hits += 1
+                return v[0]
+            self.misses += 1
+        if loader is None:
+            return None
+        val = loader(key)
+        if val is not None:
+            self.put(key, val)
+        return val
+
+    def put(self, key, val):
+        with self._lock:
+            self._d[key] = (val, time.time())
+            self._d.move_to_end(key)
+            while len(self._d) > self.capacity:
+                self._d.popitem(last=False)
+
+    def invalidate(self, key=None):
+        with self._lock:
+            if key is None:
+                self._d.clear()
+            else:
+                self._d.pop(key, None)
+
+    def __len__(self):
+        return len(self._d)

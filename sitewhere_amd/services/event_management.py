@@ -1,0 +1,215 @@
+"""service-event-management: device-event persistence + the persisted-event trigger (multitenant).
+
+Reference: ``EventManagementImpl.java`` routed by ``EventManagementRouter.java:80-150``; backend chosen
+by ``spring/EventManagementParser.java:72-160`` (MongoDB / Cassandra / InfluxDB); the store is wrapped
+by ``KafkaEventPersistenceTriggers.java:72-97`` which forwards every stored event to
+``inbound-persisted-events`` keyed by assignment id.  RPCs (``device-event-management.proto``, 16):
+AddDeviceEventBatch, GetDeviceEventById, GetDeviceEventByAlternateId, Add/List{Measurements, Locations,
+Alerts, CommandInvocations, StateChanges}(ForIndex), AddCommandResponses,
+ListCommandResponsesForInvocation, ListCommandResponsesForIndex.
+"""
+from __future__ import annotations
+
+import json
+
+from ..core.errors import ErrorCode, NotFoundException
+from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceCommandInvocation,
+                             DeviceCommandResponse, DeviceEvent, DeviceEventIndex, DeviceEventType, DeviceLocation,
+                             DeviceMeasurement, DeviceStateChange, now_ms)
+from ..persistence.events import BufferedEventWriter, DeviceEventStore, create_event_store
+from ..rpc import codec
+from ..runtime.config import simple_model
+from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+
+_BASE = ("alternateId", "eventDate", "metadata", "updateState")
+
+
+def _dr(c) -> DateRangeSearchCriteria:
+    if c is None:
+        return DateRangeSearchCriteria(page_size=100)
+    if isinstance(c, DateRangeSearchCriteria):
+        return c
+    return DateRangeSearchCriteria(c.get("pageNumber", 1), c.get("pageSize", 100), c.get("startDate"), c.get("endDate"))
+
+
+class DeviceEventManagement:
+    """IDeviceEventManagement: validates the assignment, stamps context, stores, fires triggers."""
+
+    def __init__(self, store: DeviceEventStore, assignment_lookup, on_persisted=None, buffered: bool = False):
+        self.store = store
+        self._writer = BufferedEventWriter(store) if buffered else None
+        self._lookup = assignment_lookup           # id -> DeviceAssignment | None
+        self._on_persisted = on_persisted or (lambda events: None)
+
+    def _context(self, assignment_id: str):
+        a = self._lookup(assignment_id)
+        if a is None:
+            raise NotFoundException(ErrorCode.InvalidDeviceAssignmentToken, assignment_id)
+        return a
+
+    def _stamp(self, e: DeviceEvent, a, req: dict) -> DeviceEvent:
+        e.device_id, e.device_assignment_id = a.device_id, a.id
+        e.customer_id, e.area_id, e.asset_id = a.customer_id, a.area_id, a.asset_id
+        e.alternate_id = req.get("alternateId")
+        e.event_date = req.get("eventDate") or now_ms()
+        e.received_date = now_ms()
+        e.metadata = dict(req.get("metadata") or {})
+        return e
+
+    def _persist(self, events: list[DeviceEvent]) -> list[DeviceEvent]:
+        if self._writer is not None:
+            self._writer.add(events)
+        else:
+            self.store.add_events(events)
+        self._on_persisted(events)
+        return events
+
+    def _add(self, assignment_id: str, requests, build) -> list:
+        a = self._context(assignment_id)
+        reqs = requests if isinstance(requests, list) else [requests]
+        return self._persist([self._stamp(build(r), a, r) for r in reqs])
+
+    # ---- adds ------------------------------------------------------------------
+    def add_measurements(self, assignment_id: str, *requests):
+        return self._add(assignment_id, _flat(requests),
+                         lambda r: DeviceMeasurement(name=r.get("name", ""), value=float(r.get("value", 0.0))))
+
+    def add_locations(self, assignment_id: str, *requests):
+        return self._add(assignment_id, _flat(requests),
+                         lambda r: DeviceLocation(latitude=float(r.get("latitude", 0)), longitude=float(r.get("longitude", 0)),
+                                                  elevation=r.get("elevation")))
+
+    def add_alerts(self, assignment_id: str, *requests):
+        return self._add(assignment_id, _flat(requests),
+                         lambda r: DeviceAlert(source=AlertSource(r.get("source", "Device")),
+                                               level=AlertLevel(r.get("level", "Info")), type=r.get("type", ""),
+                                               message=r.get("message", "")))
+
+    def add_command_invocations(self, assignment_id: str, *requests):
+        return self._add(assignment_id, _flat(requests),
+                         lambda r: DeviceCommandInvocation(initiator=r.get("initiator", "REST"),
+                                                           initiator_id=r.get("initiatorId"),
+                                                           target=r.get("target", "Assignment"),
+                                                           target_id=r.get("targetId") or assignment_id,
+                                                           command_token=r.get("commandToken"),
+                                                           device_command_id=r.get("deviceCommandId"),
+                                                           parameter_values=dict(r.get("parameterValues") or {})))
+
+    def add_command_responses(self, assignment_id: str, *requests):
+        return self._add(assignment_id, _flat(requests),
+                         lambda r: DeviceCommandResponse(originating_event_id=r.get("originatingEventId"),
+                                                         response_event_id=r.get("responseEventId"),
+                                                         response=r.get("response")))
+
+    def add_state_changes(self, assignment_id: str, *requests):
+        return self._add(assignment_id, _flat(requests),
+                         lambda r: DeviceStateChange(attribute=r.get("attribute", ""), type=r.get("type", ""),
+                                                     previous_state=r.get("previousState"),
+                                                     new_state=r.get("newState")))
+
+    def add_enriched_events(self, events: list, fire_triggers: bool = False) -> int:
+        """Bulk insert of events already stamped and enriched upstream (the GPU inbound engine does
+        lookup/validation/enrichment on device, so persisted triggers are normally not re-fired)."""
+        if self._writer is not None:
+            self._writer.add(events)
+        else:
+            self.store.add_events(events)
+        if fire_triggers:
+            self._on_persisted(events)
+        return len(events)
+
+    def add_device_event_batch(self, assignment_id: str, batch: dict) -> dict:
+        """Measurements + locations + alerts in one call (reference AddDeviceEventBatch)."""
+        return {"measurements": self.add_measurements(assignment_id, batch.get("measurements", [])),
+                "locations": self.add_locations(assignment_id, batch.get("locations", [])),
+                "alerts": self.add_alerts(assignment_id, batch.get("alerts", []))}
+
+    # ---- reads -----------------------------------------------------------------
+    def get_device_event_by_id(self, id: str):
+        return self.store.get_event_by_id(id)
+
+    def get_device_event_by_alternate_id(self, alt: str):
+        return self.store.get_event_by_alternate_id(alt)
+
+    def _list(self, et, index, ids, criteria):
+        return self.store.list_events(et, DeviceEventIndex(index) if isinstance(index, str) else index, list(ids),
+                                      _dr(criteria))
+
+    def list_measurements_for_index(self, index, entity_ids, criteria=None):
+        return self._list(DeviceEventType.Measurement, index, entity_ids, criteria)
+
+    def list_locations_for_index(self, index, entity_ids, criteria=None):
+        return self._list(DeviceEventType.Location, index, entity_ids, criteria)
+
+    def list_alerts_for_index(self, index, entity_ids, criteria=None):
+        return self._list(DeviceEventType.Alert, index, entity_ids, criteria)
+
+    def list_command_invocations_for_index(self, index, entity_ids, criteria=None):
+        return self._list(DeviceEventType.CommandInvocation, index, entity_ids, criteria)
+
+    def list_command_responses_for_invocation(self, invocation_id: str, criteria=None):
+        return self.store.list_command_responses_for_invocation(invocation_id, _dr(criteria))
+
+    def list_command_responses_for_index(self, index, entity_ids, criteria=None):
+        return self._list(DeviceEventType.CommandResponse, index, entity_ids, criteria)
+
+    def list_state_changes_for_index(self, index, entity_ids, criteria=None):
+        return self._list(DeviceEventType.StateChange, index, entity_ids, criteria)
+
+    def flush(self):
+        if self._writer is not None:
+            self._writer.flush()
+
+
+def _flat(requests):
+    out = []
+    for r in requests:
+        if isinstance(r, list):
+            out.extend(r)
+        else:
+            out.append(r)
+    return out
+
+
+class EventManagementTenantEngine(MicroserviceTenantEngine):
+    def tenant_initialize(self, monitor):
+        ds = self.config.get("datastore", {"type": "memory"})
+        self.store = create_event_store(ds.get("type", "memory"), **{k: v for k, v in ds.items() if k != "type"})
+        topic = self.ms.instance.naming.inbound_persisted_events(self.tenant.token)
+        self.ms.instance.bus.topic(topic)
+        prod = self.ms.producer
+
+        def triggers(events):
+            """KafkaEventPersistenceTriggers: forward each persisted event keyed by assignment id."""
+            prod.send_batch(topic, [(e.device_assignment_id, json.dumps({"event": codec.to_wire(e)}).encode())
+                                    for e in events])
+
+        dm_api = lambda: self.ms.api("DeviceManagement", self.tenant.token)  # noqa: E731
+        cache: dict = {}
+
+        def lookup(aid):
+            a = cache.get(aid)
+            if a is None:
+                a = dm_api().get_device_assignment(aid)
+                if a is not None:
+                    cache[aid] = a
+            return a
+
+        self.management = DeviceEventManagement(self.store, lookup, triggers, bool(self.config.get("buffered")))
+        self.api = {"DeviceEventManagement": self.management}
+
+
+class EventManagementMicroservice(MultitenantMicroservice):
+    identifier = "event-management"
+    name = "Event Management"
+
+    def service_names(self):
+        return ["DeviceEventManagement"]
+
+    def create_tenant_engine(self, tenant):
+        return EventManagementTenantEngine(self, tenant)
+
+    def configuration_model(self):
+        return simple_model(self.identifier, "Event Management",
+                            [("datastore", "Datastore", "memory | sqlite | bucketed (Cassandra layout)", True),
+                             ("buffered", "Boolean", "bulk buffer (DeviceEventBuffer)", False)])

@@ -1,0 +1,441 @@
+"""service-event-sources: protocol receivers -> decoders -> dedup -> decoded-events topic (multitenant).
+
+Reference: ``service-event-sources`` --
+  * ``InboundEventSource.java:40-283``: one decoder, optional deduplicator, N receivers;
+    ``onEncodedEventReceived`` -> decode -> meter -> dedup -> ``EventSourcesManager.handleDecodedEvent``
+  * ``EventSourcesManager.java:153-197``: event requests -> decoded-events topic keyed by device token,
+    registrations -> registration topic, decode failures -> failed-decode topic
+  * decoders: protobuf (``ProtobufDeviceEventDecoder.java:79-281``), JSON ``DeviceRequest``
+    (``JsonDeviceRequestMarshaler.java:62-148``), JSON batch, scripted (Groovy -> Python), composite
+    (per-device-type choice with a metadata extractor), echo / payload logger (debug)
+  * deduplicators: ``AlternateIdDeduplicator``, scripted
+  * receivers: MQTT, CoAP, socket, WebSocket, REST polling, ActiveMQ/RabbitMQ/EventHub (see
+    :mod:`sitewhere_amd.edges`); plus an in-process ``direct`` receiver for embedding and tests.
+The MI355X path: a source configured with ``"forward": "raw"`` skips per-message decoding and ships
+raw payload batches to ``event-source-raw-payloads`` for the GPU inbound engine.
+"""
+from __future__ import annotations
+
+import json
+import threading
+import time
+
+from ..core.errors import EventDecodeException
+from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
+from ..models import wire
+from ..rpc import codec
+from ..runtime.config import simple_model
+from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+
+RAW_PAYLOADS = "event-source-raw-payloads"
+
+REQUEST_TYPES = ("DeviceMeasurement", "DeviceLocation", "DeviceAlert", "DeviceCommandResponse", "DeviceStateChange",
+                 "RegisterDevice", "Acknowledge", "DeviceStream", "DeviceStreamData", "SendDeviceStreamData")
+
+
+def decoded(token: str, type_: str, request: dict, originator: str | None = None) -> dict:
+    return {"deviceToken": token, "type": type_, "request": request, "originator": originator}
+
+
+# ------------------------------------------------------------------------------ decoders
+class Decoder:
+    def decode(self, payload: bytes, metadata: dict) -> list[dict]:
+        raise NotImplementedError
+
+
+class ProtobufDecoder(Decoder):
+    """SiteWhere device protocol (delimited Header + body)."""
+
+    def decode(self, payload, metadata):
+        try:
+            cmd, orig, b = wire.decode(bytes(payload))
+        except Exception as e:
+            raise EventDecodeException(f"protobuf decode failed: {e}") from e
+        md = {m.name: m.value for m in getattr(b, "metadata", [])}
+        base = {"metadata": md}
+        if hasattr(b, "HasField") and "updateState" in b.DESCRIPTOR.fields_by_name and b.HasField("updateState"):
+            base["updateState"] = b.updateState
+        if "eventDate" in b.DESCRIPTOR.fields_by_name and b.HasField("eventDate"):
+            base["eventDate"] = b.eventDate
+        if "alternateId" in b.DESCRIPTOR.fields_by_name and b.HasField("alternateId"):
+            base["alternateId"] = b.alternateId
+        if cmd == wire.SEND_DEVICE_MEASUREMENTS:
+            out = []
+            for i, m in enumerate(b.measurement):
+                r = dict(base, name=m.measurementId, value=m.measurementValue)
+                if "alternateId" in base:
+                    r["alternateId"] = f"{base['alternateId']}:{i}" if len(b.measurement) > 1 else base["alternateId"]
+                out.append(decoded(b.hardwareId, "DeviceMeasurement", r, orig))
+            return out
+        if cmd == wire.SEND_DEVICE_LOCATION:
+            r = dict(base, latitude=b.latitude, longitude=b.longitude)
+            if b.HasField("elevation"):
+                r["elevation"] = b.elevation
+            return [decoded(b.hardwareId, "DeviceLocation", r, orig)]
+        if cmd == wire.SEND_DEVICE_ALERT:
+            return [decoded(b.hardwareId, "DeviceAlert", dict(base, type=b.alertType, message=b.alertMessage,
+                                                               level="Info"), orig)]
+        if cmd == wire.SEND_REGISTRATION:
+            r = {"deviceTypeToken": b.deviceTypeToken, "metadata": md}
+            if b.HasField("areaToken"):
+                r["areaToken"] = b.areaToken
+            return [decoded(b.hardwareId, "RegisterDevice", r, orig)]
+        if cmd == wire.SEND_ACKNOWLEDGEMENT:
+            return [decoded(b.hardwareId, "Acknowledge", {"originatingEventId": orig, "response": b.message}, orig)]
+        if cmd == wire.SEND_DEVICE_STREAM:
+            return [decoded(b.hardwareId, "DeviceStream", {"streamId": b.streamId, "contentType": b.contentType,
+                                                            "metadata": md}, orig)]
+        if cmd == wire.SEND_DEVICE_STREAM_DATA:
+            return [decoded(b.hardwareId, "DeviceStreamData", {"streamId": b.streamId, "sequenceNumber": b.sequenceNumber,
+                                                                "data": b.data, "eventDate": base.get("eventDate")}, orig)]
+        if cmd == wire.REQUEST_DEVICE_STREAM_DATA:
+            return [decoded(b.hardwareId, "SendDeviceStreamData", {"streamId": b.streamId,
+                                                                    "sequenceNumber": b.sequenceNumber}, orig)]
+        raise EventDecodeException(f"unsupported command {cmd}")
+
+
+class JsonDeviceRequestDecoder(Decoder):
+    """``{"deviceToken", "originator", "type", "request"}`` (reference JsonDeviceRequestMarshaler)."""
+
+    def decode(self, payload, metadata):
+        try:
+            d = json.loads(payload)
+        except Exception as e:
+            raise EventDecodeException(f"invalid JSON: {e}") from e
+        return [self._one(d)]
+
+    @staticmethod
+    def _one(d: dict) -> dict:
+        t = d.get("type")
+        if t not in REQUEST_TYPES:
+            raise EventDecodeException(f"unknown request type {t!r}")
+        if not d.get("deviceToken"):
+            raise EventDecodeException("deviceToken missing")
+        if d.get("request") is None:
+            raise EventDecodeException("request missing")
+        return decoded(d["deviceToken"], t, d["request"], d.get("originator"))
+
+
+class JsonBatchDecoder(Decoder):
+    """``{"deviceToken", "measurements": [...], "locations": [...], "alerts": [...]}`` (DeviceEventBatch)."""
+
+    def decode(self, payload, metadata):
+        try:
+            d = json.loads(payload)
+        except Exception as e:
+            raise EventDecodeException(f"invalid JSON: {e}") from e
+        tok = d.get("hardwareId") or d.get("deviceToken")
+        if not tok:
+            raise EventDecodeException("deviceToken missing")
+        out = [decoded(tok, "DeviceMeasurement", m) for m in d.get("measurements", [])]
+        out += [decoded(tok, "DeviceLocation", m) for m in d.get("locations", [])]
+        out += [decoded(tok, "DeviceAlert", m) for m in d.get("alerts", [])]
+        return out
+
+
+class ScriptedDecoder(Decoder):
+    """User script ``decode(payload, metadata) -> list[dict]`` (reference Groovy decoders)."""
+
+    def __init__(self, runner, source: str, name: str = "decoder"):
+        self.runner, self.source, self.name = runner, source, name
+
+    def decode(self, payload, metadata):
+        try:
+            res = self.runner.call(self.source, "decode", payload, metadata, name=self.name)
+        except Exception as e:
+            raise EventDecodeException(f"script decoder failed: {e}") from e
+        return [JsonDeviceRequestDecoder._one(r) for r in (res or [])]
+
+
+class CompositeDecoder(Decoder):
+    """Metadata extractor picks the device token, then a decoder chosen by device type
+    (reference ``decoder/composite/*``)."""
+
+    def __init__(self, extractor, choices: dict, device_type_of, default: Decoder | None = None):
+        self.extractor, self.choices, self.device_type_of, self.default = extractor, choices, device_type_of, default
+
+    def decode(self, payload, metadata):
+        token, inner = self.extractor(payload, metadata)
+        dt = self.device_type_of(token)
+        dec = self.choices.get(dt, self.default)
+        if dec is None:
+            raise EventDecodeException(f"no decoder for device type {dt!r}")
+        out = dec.decode(inner, metadata)
+        for r in out:
+            r.setdefault("deviceToken", token)
+        return out
+
+
+class EchoStringDecoder(Decoder):
+    def __init__(self, logger):
+        self.logger = logger
+
+    def decode(self, payload, metadata):
+        self.logger.info("echo payload: %r", bytes(payload)[:256])
+        return []
+
+
+class PayloadLoggerDecoder(Decoder):
+    """Debug wrapper: log the payload, then delegate."""
+
+    def __init__(self, inner: Decoder, logger):
+        self.inner, self.logger = inner, logger
+
+    def decode(self, payload, metadata):
+        self.logger.info("payload (%d bytes): %r", len(payload), bytes(payload)[:128])
+        return self.inner.decode(payload, metadata)
+
+
+# ------------------------------------------------------------------------------ deduplicators
+class AlternateIdDeduplicator:
+    """Drop requests whose alternate id already exists (event store lookup + recent-id window)."""
+
+    def __init__(self, event_lookup, window: int = 100_000):
+        self.lookup = event_lookup
+        self.window = window
+        self._recent: dict[str, float] = {}
+        self._lock = threading.Lock()
+
+    def is_duplicate(self, req: dict) -> bool:
+        alt = (req.get("request") or {}).get("alternateId")
+        if not alt:
+            return False
+        with self._lock:
+            if alt in self._recent:
+                return True
+            self._recent[alt] = time.time()
+            if len(self._recent) > self.window:
+                for k in list(self._recent)[: self.window // 10]:
+                    del self._recent[k]
+        try:
+            return self.lookup(alt) is not None
+        except Exception:
+            return False
+
+
+class ScriptedDeduplicator:
+    def __init__(self, runner, source: str):
+        self.runner, self.source = runner, source
+
+    def is_duplicate(self, req: dict) -> bool:
+        return bool(self.runner.call(self.source, "is_duplicate", req, name="deduplicator"))
+
+
+# ------------------------------------------------------------------------------ sources
+class DirectReceiver(TenantEngineLifecycleComponent):
+    """In-process receiver: ``inject(payload)`` hands bytes to the owning source."""
+
+    component_type = LifecycleComponentType.InboundEventReceiver
+
+    def __init__(self, rid: str = "direct"):
+        super().__init__(f"receiver:{rid}")
+        self.source = None
+        self.received = 0
+
+    def inject(self, payload: bytes, metadata: dict | None = None):
+        self.received += 1
+        return self.source.on_encoded_event_received(self, payload, metadata or {})
+
+
+class InboundEventSource(TenantEngineLifecycleComponent):
+    component_type = LifecycleComponentType.InboundEventSource
+
+    def __init__(self, source_id: str, decoder: Decoder | None, deduplicator=None, receivers=(), manager=None,
+                 forward_raw: bool = False):
+        super().__init__(f"source:{source_id}")
+        self.source_id = source_id
+        self.decoder = decoder
+        self.deduplicator = deduplicator
+        self.receivers = list(receivers)
+        self.manager = manager
+        self.forward_raw = forward_raw
+        for r in self.receivers:
+            r.source = self
+
+    def initialize(self, monitor):
+        self.decoded_events = self.create_meter("decodedEvents")
+        self.decode_failures = self.create_meter("decodeFailures")
+        self.duplicates = self.create_meter("duplicates")
+        for r in self.receivers:
+            r.tenant_engine = self.tenant_engine
+            self.initialize_nested_component(r, monitor, require=True)
+
+    def start(self, monitor):
+        for r in self.receivers:
+            self.start_nested_component(r, monitor, require=False)
+
+    def stop(self, monitor):
+        for r in self.receivers:
+            r.lifecycle_stop(monitor)
+
+    def on_encoded_event_received(self, receiver, payload: bytes, metadata: dict) -> int:
+        if self.forward_raw:
+            self.manager.handle_raw_payload(self.source_id, payload)
+            return 1
+        try:
+            reqs = self.decoder.decode(payload, metadata)
+        except Exception as e:
+            self.decode_failures.mark()
+            self.manager.handle_failed_decode(self.source_id, payload, e)
+            return 0
+        n = 0
+        for r in reqs:
+            self.decoded_events.mark()
+            if self.deduplicator is not None and self.deduplicator.is_duplicate(r):
+                self.duplicates.mark()
+                continue
+            self.manager.handle_decoded_event(self.source_id, r)
+            n += 1
+        return n
+
+
+class EventSourcesManager(TenantEngineLifecycleComponent):
+    """Routes decoded requests to the bus (EventSourcesManager.java:153-197)."""
+
+    def __init__(self, engine: "EventSourcesTenantEngine"):
+        super().__init__("event-sources-manager")
+        self.engine = engine
+        self.tenant_engine = engine
+        ms = engine.ms
+        t = engine.tenant.token
+        self.producer = ms.producer
+        self.t_decoded = ms.instance.naming.decoded_events(t)
+        self.t_failed = ms.instance.naming.failed_decode_events(t)
+        self.t_registration = ms.instance.naming.device_registration_events(t)
+        self.t_raw = ms.instance.naming.tenant_prefix(t) + RAW_PAYLOADS
+        self.sources: dict[str, InboundEventSource] = {}
+        self._raw_buf: list = []
+        self._raw_lock = threading.Lock()
+
+    def handle_decoded_event(self, source_id: str, req: dict):
+        payload = {"sourceId": source_id, "deviceToken": req["deviceToken"], "originator": req.get("originator"),
+                   "eventCreateRequest": {"type": req["type"], "request": req["request"]}}
+        body = json.dumps(codec.to_wire(payload)).encode()
+        if req["type"] == "RegisterDevice":
+            self.producer.send(self.t_registration, req["deviceToken"], body)
+        else:
+            self.producer.send(self.t_decoded, req["deviceToken"], body)
+
+    def handle_failed_decode(self, source_id: str, payload: bytes, err: Exception):
+        self.producer.send(self.t_failed, source_id, json.dumps(
+            {"sourceId": source_id, "error": str(err), "payload": codec.to_wire(bytes(payload))}).encode())
+
+    def handle_raw_payload(self, source_id: str, payload: bytes, flush_at: int = 4096):
+        with self._raw_lock:
+            self._raw_buf.append(bytes(payload))
+            if len(self._raw_buf) >= flush_at:
+                self.flush_raw()
+
+    def flush_raw(self):
+        """Ship the buffered raw payloads as one batch record: u32 count, u32 lengths[], bytes."""
+        import struct
+        with self._raw_lock:
+            buf, self._raw_buf = self._raw_buf, []
+        if not buf:
+            return
+        head = struct.pack(f"<I{len(buf)}I", len(buf), *[len(b) for b in buf])
+        self.producer.send(self.t_raw, None, head + b"".join(buf))
+
+
+class EventSourcesTenantEngine(MicroserviceTenantEngine):
+    def tenant_initialize(self, monitor):
+        self.manager = EventSourcesManager(self)
+        ms = self.ms
+        for sc in self.config.get("sources", []):
+            src = self.build_source(sc)
+            src.tenant_engine = self
+            self.manager.sources[src.source_id] = src
+            self.initialize_nested_component(src, monitor, require=False)
+        self.api = {"EventSources": EventSourcesApi(self)}
+
+    def build_source(self, sc: dict) -> InboundEventSource:
+        from ..edges.receivers import build_receiver
+        dec = self.build_decoder(sc.get("decoder", "json"))
+        if sc.get("logPayloads"):
+            dec = PayloadLoggerDecoder(dec, self.logger)
+        dd = None
+        dcfg = sc.get("deduplicator", self.config.get("deduplicator"))
+        if dcfg:
+            if dcfg.get("type") == "alternate-id":
+                ev = lambda alt: self.ms.api("DeviceEventManagement", self.tenant.token).get_device_event_by_alternate_id(alt)  # noqa
+                dd = AlternateIdDeduplicator(ev)
+            elif dcfg.get("type") == "script":
+                dd = ScriptedDeduplicator(self.ms.scripts, dcfg["script"])
+        recs = [DirectReceiver("direct")] + [build_receiver(rc) for rc in sc.get("receivers", [])]
+        return InboundEventSource(sc["id"], dec, dd, recs, self.manager, forward_raw=sc.get("forward") == "raw")
+
+    def build_decoder(self, d) -> Decoder:
+        if isinstance(d, str):
+            d = {"type": d}
+        t = d.get("type")
+        if t == "protobuf":
+            return ProtobufDecoder()
+        if t == "json":
+            return JsonDeviceRequestDecoder()
+        if t == "json-batch":
+            return JsonBatchDecoder()
+        if t == "script":
+            return ScriptedDecoder(self.ms.scripts, d["script"])
+        if t == "echo":
+            return EchoStringDecoder(self.logger)
+        if t == "composite":
+            choices = {k: self.build_decoder(v) for k, v in d.get("choices", {}).items()}
+            dm = lambda tok: self.ms.api("DeviceManagement", self.tenant.token)  # noqa: E731
+
+            def dtype_of(tok):
+                dev = dm(tok).get_device_by_token(tok)
+                if dev is None:
+                    return None
+                dt = dm(tok).get_device_type(dev.device_type_id)
+                return dt.token if dt else None
+
+            def extractor(payload, md):
+                obj = json.loads(payload)
+                return obj[d.get("tokenField", "deviceToken")], json.dumps(obj.get(d.get("payloadField", "payload"), obj)).encode()
+            return CompositeDecoder(extractor, choices, dtype_of, self.build_decoder(d["default"]) if d.get("default") else None)
+        raise ValueError(f"unknown decoder {t!r}")
+
+    def tenant_start(self, monitor):
+        for s in self.manager.sources.values():
+            self.start_nested_component(s, monitor, require=False)
+
+    def tenant_stop(self, monitor):
+        for s in self.manager.sources.values():
+            s.lifecycle_stop(monitor)
+        self.manager.flush_raw()
+
+    def source(self, sid: str) -> InboundEventSource:
+        return self.manager.sources[sid]
+
+    def inject(self, source_id: str, payload: bytes, metadata: dict | None = None) -> int:
+        return self.source(source_id).receivers[0].inject(payload, metadata)
+
+
+class EventSourcesApi:
+    """Management view of the tenant's sources (used by the admin REST API)."""
+
+    def __init__(self, engine: EventSourcesTenantEngine):
+        self._e = engine
+
+    def list_event_sources(self) -> list[dict]:
+        return [{"id": s.source_id, "status": s.status.value, "decoder": type(s.decoder).__name__ if s.decoder else None,
+                 "receivers": [r.component_name for r in s.receivers],
+                 "decodedEvents": s.decoded_events.count, "decodeFailures": s.decode_failures.count,
+                 "duplicates": s.duplicates.count} for s in self._e.manager.sources.values()]
+
+    def inject(self, source_id: str, payload: bytes, metadata: dict | None = None) -> int:
+        return self._e.inject(source_id, payload, metadata)
+
+
+class EventSourcesMicroservice(MultitenantMicroservice):
+    identifier = "event-sources"
+    name = "Event Sources"
+
+    def service_names(self):
+        return ["EventSources"]
+
+    def create_tenant_engine(self, tenant):
+        return EventSourcesTenantEngine(self, tenant)
+
+    def configuration_model(self):
+        return simple_model(self.identifier, "Event Sources", [("sources", "EventSourceList", "", True)])

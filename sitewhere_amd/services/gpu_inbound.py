@@ -1,0 +1,326 @@
+"""MI355X inbound tenant engine: the fused micro-batch pipeline behind service-inbound-processing.
+
+Replaces the per-event path of the reference (``DecodedEventsConsumer.java:79-204`` ->
+``InboundPayloadProcessingLogic.java:101-218`` -> ``UnaryEventStorageStrategy.java:53-90`` ->
+``KafkaEventPersistenceTriggers`` -> ``PersistedEventsConsumer`` / ``OutboundPayloadEnrichmentLogic``)
+with one engine step per batch of raw payloads:
+
+  raw batch record (``<tenant>event-source-raw-payloads``, written by event sources configured with
+  ``"forward": "raw"``) -> :class:`GpuInboundEngine` (decode, registry lookup + assignment validation,
+  alternate-id dedup, persist into the HBM event ring, enrichment, device-state merge, zone rules,
+  presence) -> enriched events on ``inbound-enriched-events`` + bulk insert into event management.
+
+The registry mirror is kept current from the device-model change feed (``device-model-updates``)
+that device management publishes on every mutation, so no per-event RPC happens.  Messages the
+engine does not persist but that need a control-plane decision (unregistered devices, registration,
+acknowledgements, streams) take a slow path: the batch is re-decoded on the host and those messages
+are routed exactly like the reference routes them (unregistered / registration topics).
+
+``device`` config: ``"gpu"`` (fail loudly without a GPU), ``"cpu"`` (the oracle engine) or ``"auto"``.
+"""
+from __future__ import annotations
+
+import json
+import struct
+import threading
+import time
+
+import numpy as np
+
+from ..models.columnar import (EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, ST_CONTROL,
+                               ST_UNASSIGNED, ST_UNREGISTERED)
+from ..models.domain import (AlertLevel, AlertSource, DeviceAlert, DeviceAssignmentStatus, DeviceLocation,
+                             DeviceMeasurement, DeviceStateChange, now_ms)
+from ..pipeline.config import EngineConfig
+from ..pipeline.engine_base import Zone, ZoneTest
+from ..pipeline.fleet import fingerprint_str, pack_messages
+from ..rpc import codec
+from ..runtime.consumers import BusConsumer
+from ..runtime.microservice import MicroserviceTenantEngine
+from .event_sources import RAW_PAYLOADS, ProtobufDecoder
+
+_LEVELS = [AlertLevel.Info, AlertLevel.Warning, AlertLevel.Error, AlertLevel.Critical]
+
+
+def unpack_raw_batch(value: bytes):
+    """Inverse of ``EventSourcesManager.flush_raw``: -> (raw uint8, offs uint32[n+1])."""
+    n = struct.unpack_from("<I", value, 0)[0]
+    lens = np.frombuffer(value, np.uint32, n, 4)
+    offs = np.zeros(n + 1, np.uint32)
+    np.cumsum(lens, out=offs[1:])
+    start = 4 + 4 * n
+    raw = np.zeros(int(offs[-1]) + 64, np.uint8)
+    raw[:offs[-1]] = np.frombuffer(value, np.uint8, int(offs[-1]), start)
+    return raw, offs
+
+
+class IndexMap:
+    """Stable dense indices for entity ids (device / assignment / customer / area / asset)."""
+
+    def __init__(self):
+        self.idx: dict[str, int] = {}
+        self.ids: list[str] = []
+
+    def get(self, key: str | None) -> int:
+        if key is None:
+            return -1
+        i = self.idx.get(key)
+        if i is None:
+            i = self.idx[key] = len(self.ids)
+            self.ids.append(key)
+        return i
+
+    def id_of(self, i: int) -> str | None:
+        return self.ids[i] if 0 <= i < len(self.ids) else None
+
+
+class GpuInboundTenantEngine(MicroserviceTenantEngine):
+    def tenant_initialize(self, monitor):
+        cfg = self.config
+        ms, t = self.ms, self.tenant.token
+        n = ms.instance.naming
+        self.t_enriched = n.inbound_enriched_events(t)
+        self.t_unregistered = n.unregistered_device_events(t)
+        self.t_registration = n.device_registration_events(t)
+        self.t_decoded = n.decoded_events(t)
+        ecfg = EngineConfig.small(**{k: int(v) for k, v in cfg.get("capacity", {}).items()}) \
+            if cfg.get("sizing", "small") == "small" else EngineConfig(**cfg.get("capacity", {}))
+        ecfg.presence_missing_ms = int(cfg.get("presenceMissingMs", ecfg.presence_missing_ms))
+        ecfg.presence_check_ms = int(cfg.get("presenceCheckMs", ecfg.presence_check_ms))
+        self.engine_cfg = ecfg
+        self.engine = self._make_engine(cfg.get("device", "auto"), ecfg)
+        self.devices, self.assignments = IndexMap(), IndexMap()
+        self.customers, self.areas, self.assets = IndexMap(), IndexMap(), IndexMap()
+        self._asg_entities: dict[int, object] = {}
+        self._dev_tokens: dict[int, str] = {}
+        self._nid2name: dict[int, str] = {}
+        self._lock = threading.RLock()
+        self.boot = f"{int(time.time() * 1000):x}"
+        self.zone_tests = [ZoneTest(z["zoneToken"], z.get("condition", "inside"), z.get("alertType", "zone.alert"),
+                                    int(z.get("alertLevel", 1)), z.get("alertMessage", ""))
+                           for z in cfg.get("zoneTests", [])]
+        self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
+                                        self._process_raw, max_records=16)
+        self.model_consumer = BusConsumer(self, "model-updates", [n.tenant_prefix(t) + "device-model-updates"],
+                                          self._on_model_update)
+        self.processed_events = self.create_meter("processedEvents")
+        self.persisted_events = self.create_meter("persistedEvents")
+        self.unregistered = self.create_meter("unregisteredEvents")
+        self.step_timer = self.create_timer("engineStep")
+        self.api = {"InboundProcessing": GpuInboundApi(self)}
+
+    def _make_engine(self, device: str, ecfg: EngineConfig):
+        want_gpu = device == "gpu"
+        if device in ("gpu", "auto"):
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    from ..pipeline.gpu_engine import GpuInboundEngine
+                    self.engine_kind = "gpu"
+                    return GpuInboundEngine(ecfg, device="cuda")
+            except Exception:
+                if want_gpu:
+                    raise
+            if want_gpu:
+                raise RuntimeError("inbound-processing configured with device=gpu but no GPU is available")
+        from ..pipeline.cpu_engine import CpuInboundEngine
+        self.engine_kind = "cpu"
+        return CpuInboundEngine(ecfg)
+
+    # ---------------------------------------------------------------- registry mirror
+    def _dm(self):
+        return self.ms.api("DeviceManagement", self.tenant.token)
+
+    def _em(self):
+        return self.ms.api("DeviceEventManagement", self.tenant.token)
+
+    def load_model(self):
+        """Full registry load (device management list APIs), then the change feed keeps it current."""
+        dm = self._dm()
+        for d in dm.list_devices({"pageSize": 0}).results:
+            self._upsert_device(d)
+        for a in dm.list_device_assignments({"pageSize": 0}).results:
+            self._upsert_assignment(a)
+        self._load_zones()
+
+    def _load_zones(self):
+        if not self.zone_tests:
+            return
+        dm = self._dm()
+        zones = []
+        for tok in sorted({zt.zone_token for zt in self.zone_tests}):
+            z = dm.get_zone_by_token(tok)
+            if z is not None:
+                zones.append(Zone(z.token, [(p["latitude"], p["longitude"]) if isinstance(p, dict)
+                                            else (p.latitude, p.longitude) for p in z.bounds]))
+        known = {z.token for z in zones}
+        self.engine.set_zone_rules(zones, [zt for zt in self.zone_tests if zt.zone_token in known])
+
+    def _upsert_device(self, d):
+        with self._lock:
+            di = self.devices.get(d.id)
+            lo, hi = fingerprint_str(d.token)
+            self.engine.register_devices(np.array([lo], np.uint64), np.array([hi], np.uint64), np.array([di], np.int32))
+            self._dev_tokens[di] = d.token
+
+    def _upsert_assignment(self, a):
+        with self._lock:
+            ai = self.assignments.get(a.id)
+            di = self.devices.get(a.device_id)
+            active = a.status != DeviceAssignmentStatus.Released
+            self.engine.set_assignments([ai], [di], customer=[self.customers.get(a.customer_id)],
+                                        area=[self.areas.get(a.area_id)], asset=[self.assets.get(a.asset_id)],
+                                        active=[1 if active else 0])
+            self._asg_entities[ai] = a
+
+    def _on_model_update(self, recs):
+        for r in recs:
+            m = json.loads(r.value)
+            kind, e = m["kind"], codec.from_wire(m["entity"])
+            if kind in ("device.created", "device.updated"):
+                self._upsert_device(e)
+            elif kind == "device.deleted":
+                with self._lock:
+                    # tombstone: the fingerprint keeps its slot but resolves to no active assignment
+                    di = self.devices.get(e.id)
+                    self.engine.dev_asg[di] = -1
+                    self.engine._dirty_devices(np.array([di], np.int32))
+            elif kind.startswith("assignment."):
+                if kind == "assignment.deleted":
+                    e.status = DeviceAssignmentStatus.Released
+                self._upsert_assignment(e)
+            elif kind.startswith("zone."):
+                self._load_zones()
+
+    # ---------------------------------------------------------------- lifecycle
+    def tenant_start(self, monitor):
+        self.load_model()
+        self.start_nested_component(self.model_consumer, monitor, require=True)
+        self.start_nested_component(self.raw_consumer, monitor, require=True)
+
+    def tenant_stop(self, monitor):
+        for c in (self.raw_consumer, self.model_consumer):
+            c.lifecycle_stop(monitor)
+
+    # ---------------------------------------------------------------- data plane
+    def _process_raw(self, recs):
+        for r in recs:
+            raw, offs = unpack_raw_batch(r.value)
+            self.process_batch(raw, offs)
+
+    def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None):
+        now = now or now_ms()
+        with self._lock, self.step_timer.time():
+            res = self.engine.step(raw, offs, now)
+        self.processed_events.mark(res.n_events)
+        events = self._to_events(res, now)
+        if events:
+            self._em().add_enriched_events(events)
+            self.persisted_events.mark(len(events))
+            self.ms.producer.send_batch(self.t_enriched, [
+                (self._dev_tokens.get(self.devices.idx.get(e.device_id, -1)) or e.device_id,
+                 json.dumps({"event": codec.to_wire(e), "context": self._context(e)}).encode()) for e in events])
+        if res.rejects is not None and len(res.rejects):
+            self._slow_path(raw, offs, res)
+        return res
+
+    def _name(self, nid: int) -> str:
+        if nid == NO_NAME:
+            return ""
+        s = self._nid2name.get(nid)
+        if s is None:
+            table = self.engine.intern if hasattr(self.engine, "intern") and isinstance(self.engine.intern, dict) \
+                else self.engine.intern_table()
+            self._nid2name = {i: self.engine.names.get(h, str(h)) for h, i in table.items()}
+            s = self._nid2name.get(nid, "")
+        return s
+
+    def _to_events(self, res, now: int) -> list:
+        out = res.out
+        if out is None or not len(out):
+            return []
+        eids = res.event_ids()
+        tests = self.engine.tests
+        events = []
+        for r, eid in zip(out, eids):
+            a = self._asg_entities.get(int(r["assignment"]))
+            if a is None:
+                continue
+            et = int(r["etype"])
+            base = dict(id=f"{self.boot}-{int(eid)}", device_id=a.device_id, device_assignment_id=a.id,
+                        customer_id=a.customer_id, area_id=a.area_id, asset_id=a.asset_id,
+                        event_date=int(r["event_date"]), received_date=now)
+            if et == EV_MEASUREMENT:
+                e = DeviceMeasurement(name=self._name(int(r["name_id"])), value=float(r["v0"]), **base)
+            elif et == EV_LOCATION:
+                e = DeviceLocation(latitude=float(r["v0"]), longitude=float(r["v1"]), **base)
+            elif et == EV_ALERT:
+                typ = self._name(int(r["name_id"]))
+                rule = next((t for t in tests if t.alert_type == typ), None)
+                e = DeviceAlert(source=AlertSource.System if rule else AlertSource.Device,
+                                level=_LEVELS[min(int(r["level"]), 3)], type=typ,
+                                message=rule.alert_message if rule else "", **base)
+            elif et == EV_STATE_CHANGE:
+                e = DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
+                                      new_state="NOT_PRESENT", **base)
+            else:
+                continue
+            events.append(e)
+        return events
+
+    def _context(self, e) -> dict:
+        di = self.devices.idx.get(e.device_id, -1)
+        return {"deviceId": e.device_id, "deviceToken": self._dev_tokens.get(di),
+                "assignmentStatus": "Active", "engine": self.engine_kind}
+
+    def _slow_path(self, raw, offs, res):
+        st = res.reject_status
+        need = (st == ST_UNREGISTERED) | (st == ST_UNASSIGNED) | (st == ST_CONTROL)
+        if not need.any():
+            return
+        fps = {(int(r["fp_lo"]), int(r["fp_hi"])) for r in res.rejects[need]}
+        dec = ProtobufDecoder()
+        for i in range(len(offs) - 1):
+            payload = bytes(raw[offs[i]:offs[i + 1]])
+            try:
+                reqs = dec.decode(payload, {})
+            except Exception:
+                continue
+            for q in reqs:
+                if fingerprint_str(q["deviceToken"]) not in fps:
+                    continue
+                body = {"sourceId": "gpu-inbound", "deviceToken": q["deviceToken"], "originator": q.get("originator"),
+                        "eventCreateRequest": {"type": q["type"], "request": q["request"]}}
+                wire_body = json.dumps(codec.to_wire(body)).encode()
+                if q["type"] == "RegisterDevice":
+                    self.ms.producer.send(self.t_registration, q["deviceToken"], wire_body)
+                elif q["type"] in ("Acknowledge", "DeviceStream", "DeviceStreamData", "SendDeviceStreamData"):
+                    self.ms.producer.send(self.t_decoded, q["deviceToken"], wire_body)
+                else:
+                    self.unregistered.mark()
+                    self.ms.producer.send(self.t_unregistered, q["deviceToken"], wire_body)
+
+
+class GpuInboundApi:
+    def __init__(self, engine: GpuInboundTenantEngine):
+        self._e = engine
+
+    def get_statistics(self) -> dict:
+        e = self._e
+        d = {"processedEvents": e.processed_events.count, "persistedEvents": e.persisted_events.count,
+             "unregisteredEvents": e.unregistered.count, "engine": e.engine_kind}
+        d.update({f"engine.{k}": v for k, v in e.engine.stats_dict().items()})
+        return d
+
+    def get_device_state(self, assignment_id: str) -> dict | None:
+        ai = self._e.assignments.idx.get(assignment_id)
+        return None if ai is None else self._e.engine.device_state(ai)
+
+    def process_payloads(self, payloads: list) -> dict:
+        """Synchronous injection (tests / REST): one engine step over the given wire payloads."""
+        raw, offs = pack_messages([bytes(p) for p in payloads])
+        r = self._e.process_batch(raw, offs)
+        return {"messages": r.n_msgs, "events": r.n_events, "persisted": r.n_persisted}
+
+
+_ = ST_UNASSIGNED

@@ -1,0 +1,168 @@
+"""service-inbound-processing: validate decoded events, persist them, enrich persisted events.
+
+Reference: ``service-inbound-processing`` --
+  * ``DecodedEventsConsumer.java:79-204`` subscribes to decoded + reprocess topics and runs
+    ``InboundPayloadProcessingLogic.java:101-218`` per record: device lookup by token, then the
+    active assignment; unregistered/unassigned devices go to the unregistered topic; otherwise
+    ``UnaryEventStorageStrategy.java:53-90`` calls event-management ``add*`` by event type.
+    (The reference runs this on the poll thread although 25 threads are configured; here
+    ``processingThreadCount`` is honoured.)
+  * ``PersistedEventsConsumer.java:50-142`` (10 threads) + ``OutboundPayloadEnrichmentLogic.java:54-92``:
+    attach device + assignment context, send to the enriched topic keyed by device token, and
+    command invocations additionally to the enriched-command-invocations topic.
+  * ``CachedDeviceManagementApiChannel`` + near cache for the lookups.
+The MI355X mode (``"engine": "gpu"``) replaces both consumers with :class:`GpuInboundEngine` over raw
+payload batches (see :mod:`sitewhere_amd.services.gpu_inbound`).
+"""
+from __future__ import annotations
+
+import json
+
+from ..models.domain import DeviceAssignmentStatus, DeviceEventType
+from ..rpc import codec
+from ..runtime.consumers import BusConsumer, NearCache
+from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+
+_ADDERS = {
+    "DeviceMeasurement": "add_measurements", "DeviceLocation": "add_locations", "DeviceAlert": "add_alerts",
+    "DeviceCommandResponse": "add_command_responses", "Acknowledge": "add_command_responses",
+    "DeviceStateChange": "add_state_changes", "DeviceCommandInvocation": "add_command_invocations",
+}
+
+
+class InboundProcessingTenantEngine(MicroserviceTenantEngine):
+    def tenant_initialize(self, monitor):
+        ms, t = self.ms, self.tenant.token
+        n = ms.instance.naming
+        self.t_unregistered = n.unregistered_device_events(t)
+        self.t_enriched = n.inbound_enriched_events(t)
+        self.t_enriched_cmd = n.enriched_command_invocations(t)
+        self.devices = NearCache(5000, 60.0)
+        self.assignments = NearCache(5000, 60.0)
+        threads = int(self.config.get("processingThreadCount", 25))
+        self.decoded_consumer = BusConsumer(self, "decoded-event-consumers", [n.decoded_events(t), n.inbound_reprocess_events(t)],
+                                            self._process_decoded, threads=min(threads, 8))
+        self.persisted_consumer = BusConsumer(self, "persisted-event-consumers", [n.inbound_persisted_events(t)],
+                                              self._process_persisted, threads=10)
+        self.processed_events = self.create_meter("processedEvents")
+        self.failed_events = self.create_meter("failedEvents")
+        self.device_lookup = self.create_timer("deviceLookup")
+        self.assignment_lookup = self.create_timer("assignmentLookup")
+        self.event_storage = self.create_timer("eventStorage")
+        self.unregistered = self.create_meter("unregisteredEvents")
+        # invalidate near caches from the device-model change feed
+        self.model_consumer = BusConsumer(self, "model-updates", [n.tenant_prefix(t) + "device-model-updates"],
+                                          self._on_model_update)
+        self.api = {"InboundProcessing": InboundProcessingApi(self)}
+
+    def tenant_start(self, monitor):
+        for c in (self.model_consumer, self.decoded_consumer, self.persisted_consumer):
+            self.start_nested_component(c, monitor, require=True)
+
+    def tenant_stop(self, monitor):
+        for c in (self.decoded_consumer, self.persisted_consumer, self.model_consumer):
+            c.lifecycle_stop(monitor)
+
+    def _dm(self):
+        return self.ms.api("DeviceManagement", self.tenant.token)
+
+    def _em(self):
+        return self.ms.api("DeviceEventManagement", self.tenant.token)
+
+    def _on_model_update(self, recs):
+        for r in recs:
+            m = json.loads(r.value)
+            e = codec.from_wire(m["entity"])
+            if m["kind"].startswith("device."):
+                self.devices.invalidate(getattr(e, "token", None))
+                self.devices.invalidate(("id", e.id))
+            elif m["kind"].startswith("assignment."):
+                self.assignments.invalidate(e.id)
+                self.devices.invalidate(("id", e.device_id))
+                self.devices.invalidate(None)
+
+    def device_by_token(self, token):
+        with self.device_lookup.time():
+            return self.devices.get(token, lambda k: self._dm().get_device_by_token(k))
+
+    def assignment(self, aid):
+        with self.assignment_lookup.time():
+            return self.assignments.get(aid, lambda k: self._dm().get_device_assignment(k))
+
+    # ---- InboundPayloadProcessingLogic -----------------------------------------------
+    def _process_decoded(self, recs):
+        em = self._em()
+        for r in recs:
+            try:
+                p = codec.from_wire(json.loads(r.value))
+                self.process_payload(p, em)
+                self.processed_events.mark()
+            except Exception:
+                self.failed_events.mark()
+                self.logger.exception("failed to process inbound payload")
+
+    def process_payload(self, p: dict, em=None):
+        token = p["deviceToken"]
+        device = self.device_by_token(token)
+        a = None
+        if device is not None and device.device_assignment_id:
+            a = self.assignment(device.device_assignment_id)
+        if device is None or a is None or a.status == DeviceAssignmentStatus.Released:
+            self.unregistered.mark()
+            self.ms.producer.send(self.t_unregistered, token, json.dumps(codec.to_wire(p)).encode())
+            return None
+        req = p["eventCreateRequest"]
+        fn = _ADDERS.get(req["type"])
+        if fn is None:
+            return None
+        with self.event_storage.time():
+            return getattr(em or self._em(), fn)(a.id, req["request"])
+
+    # ---- OutboundPayloadEnrichmentLogic -------------------------------------------
+    def _process_persisted(self, recs):
+        out, cmds = [], []
+        for r in recs:
+            ev = codec.from_wire(json.loads(r.value)["event"])
+            a = self.assignment(ev.device_assignment_id)
+            if a is None:
+                continue
+            dev = self.devices.get(("id", a.device_id), lambda k: self._dm().get_device(k[1]))
+            ctx = {"deviceId": a.device_id, "deviceToken": dev.token if dev else None,
+                   "deviceTypeId": a.device_type_id, "parentDeviceId": dev.parent_device_id if dev else None,
+                   "deviceStatus": dev.status if dev else None, "deviceMetadata": dev.metadata if dev else {},
+                   "assignmentStatus": a.status.value, "assignmentMetadata": a.metadata}
+            body = json.dumps({"event": codec.to_wire(ev), "context": ctx}).encode()
+            key = ctx["deviceToken"] or a.device_id
+            out.append((key, body))
+            if ev.event_type == DeviceEventType.CommandInvocation:
+                cmds.append((key, body))
+        if out:
+            self.ms.producer.send_batch(self.t_enriched, out)
+        if cmds:
+            self.ms.producer.send_batch(self.t_enriched_cmd, cmds)
+
+
+class InboundProcessingApi:
+    def __init__(self, engine):
+        self._e = engine
+
+    def get_statistics(self) -> dict:
+        e = self._e
+        return {"processedEvents": e.processed_events.count, "failedEvents": e.failed_events.count,
+                "unregisteredEvents": e.unregistered.count, "deviceCacheHits": e.devices.hits,
+                "deviceCacheMisses": e.devices.misses}
+
+
+class InboundProcessingMicroservice(MultitenantMicroservice):
+    identifier = "inbound-processing"
+    name = "Inbound Processing"
+
+    def service_names(self):
+        return ["InboundProcessing"]
+
+    def create_tenant_engine(self, tenant):
+        cfg = self.tenant_configuration(tenant.token)
+        if cfg.get("engine") == "gpu":
+            from .gpu_inbound import GpuInboundTenantEngine
+            return GpuInboundTenantEngine(self, tenant)
+        return InboundProcessingTenantEngine(self, tenant)

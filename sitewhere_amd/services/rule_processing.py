@@ -1,0 +1,185 @@
+"""service-rule-processing: per-event rule processors on the enriched stream (multitenant).
+
+Reference: ``KafkaRuleProcessorHost.java:77-250`` (one consumer group per processor, thread pool,
+dispatch by event type to ``onMeasurement/onLocation/onAlert/...``), ``RuleProcessor`` base,
+``ZoneTestRuleProcessor.java:47-62`` (JTS ``Polygon.contains`` per zone test -> alert through
+event management, ``alert.setEventDate(new Date())``).  Added: a scripted processor and a threshold
+processor; the zone test batches its point-in-polygon work onto the GPU when available
+(:func:`sitewhere_amd.core.geo.batch_contains`).
+"""
+from __future__ import annotations
+
+import json
+
+from ..core.geo import batch_contains, polygon_of
+from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
+from ..models.domain import DeviceEventType
+from ..rpc import codec
+from ..runtime.consumers import BusConsumer
+from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+
+
+class RuleProcessor(TenantEngineLifecycleComponent):
+    component_type = LifecycleComponentType.RuleProcessor
+
+    def __init__(self, pid: str):
+        super().__init__(f"rule:{pid}")
+        self.pid = pid
+
+    def process_batch(self, items: list[tuple]):
+        for ev, ctx in items:
+            h = {DeviceEventType.Measurement: self.on_measurement, DeviceEventType.Location: self.on_location,
+                 DeviceEventType.Alert: self.on_alert, DeviceEventType.CommandInvocation: self.on_command_invocation,
+                 DeviceEventType.CommandResponse: self.on_command_response,
+                 DeviceEventType.StateChange: self.on_state_change}[ev.event_type]
+            h(ctx, ev)
+
+    def on_measurement(self, ctx, ev): pass
+    def on_location(self, ctx, ev): pass
+    def on_alert(self, ctx, ev): pass
+    def on_command_invocation(self, ctx, ev): pass
+    def on_command_response(self, ctx, ev): pass
+    def on_state_change(self, ctx, ev): pass
+
+    def events_api(self):
+        e = self.tenant_engine
+        return e.ms.api("DeviceEventManagement", e.tenant.token)
+
+
+class ZoneTestRuleProcessor(RuleProcessor):
+    """zoneTests: [{zoneToken, condition: inside|outside, alertType, alertLevel, alertMessage}]."""
+
+    def __init__(self, pid: str, tests: list[dict]):
+        super().__init__(pid)
+        self.tests = tests
+        self._polys: dict[str, object] = {}
+        self.alerts = 0
+
+    def _poly(self, token: str):
+        p = self._polys.get(token)
+        if p is None:
+            e = self.tenant_engine
+            z = e.ms.api("DeviceManagement", e.tenant.token).get_zone_by_token(token)
+            if z is None:
+                raise ValueError(f"Invalid zone token in zone test: {token}")
+            p = self._polys[token] = polygon_of(z.bounds)
+        return p
+
+    def process_batch(self, items):
+        locs = [(ev, ctx) for ev, ctx in items if ev.event_type == DeviceEventType.Location]
+        if not locs or not self.tests:
+            return
+        polys = [self._poly(t["zoneToken"]) for t in self.tests]
+        inside = batch_contains(polys, [(ev.latitude, ev.longitude) for ev, _ in locs])
+        api = self.events_api()
+        for i, (ev, _) in enumerate(locs):
+            for j, t in enumerate(self.tests):
+                if (t.get("condition", "inside") == "inside") == bool(inside[i, j]):
+                    api.add_alerts(ev.device_assignment_id, {"type": t.get("alertType", "zone.alert"),
+                                                             "level": t.get("alertLevel", "Warning"),
+                                                             "message": t.get("alertMessage", ""),
+                                                             "source": "System", "updateState": False})
+                    self.alerts += 1
+
+
+class ThresholdRuleProcessor(RuleProcessor):
+    """Alert when a named measurement crosses a bound: {measurement, min?, max?, alertType, alertLevel}."""
+
+    def __init__(self, pid: str, rules: list[dict]):
+        super().__init__(pid)
+        self.rules = rules
+        self.alerts = 0
+
+    def on_measurement(self, ctx, ev):
+        for r in self.rules:
+            if r["measurement"] != ev.name:
+                continue
+            lo, hi = r.get("min"), r.get("max")
+            if (lo is not None and ev.value < lo) or (hi is not None and ev.value > hi):
+                self.events_api().add_alerts(ev.device_assignment_id, {
+                    "type": r.get("alertType", f"{ev.name}.threshold"), "level": r.get("alertLevel", "Warning"),
+                    "message": f"{ev.name}={ev.value} outside [{lo}, {hi}]", "source": "System"})
+                self.alerts += 1
+
+
+class ScriptedRuleProcessor(RuleProcessor):
+    """User script defining any of ``on_measurement(ctx, ev, api)`` ... ``on_state_change``."""
+
+    def __init__(self, pid: str, source: str):
+        super().__init__(pid)
+        self.source = source
+
+    def _call(self, name, ctx, ev):
+        ns = self.tenant_engine.ms.scripts.compile(self.source, f"rule-{self.pid}")
+        if name in ns:
+            self.tenant_engine.ms.scripts.call(self.source, name, ctx, ev.to_dict(), self.events_api(),
+                                               name=f"rule-{self.pid}")
+
+    def on_measurement(self, ctx, ev): self._call("on_measurement", ctx, ev)
+    def on_location(self, ctx, ev): self._call("on_location", ctx, ev)
+    def on_alert(self, ctx, ev): self._call("on_alert", ctx, ev)
+
+
+def build_processor(cfg: dict) -> RuleProcessor:
+    t = cfg.get("type")
+    if t == "zone-test":
+        return ZoneTestRuleProcessor(cfg["id"], cfg.get("zoneTests", []))
+    if t == "threshold":
+        return ThresholdRuleProcessor(cfg["id"], cfg.get("rules", []))
+    if t == "script":
+        return ScriptedRuleProcessor(cfg["id"], cfg["script"])
+    raise ValueError(f"unknown rule processor {t!r}")
+
+
+class RuleProcessingTenantEngine(MicroserviceTenantEngine):
+    def tenant_initialize(self, monitor):
+        self.processors = []
+        self.hosts = []
+        topic = self.ms.instance.naming.inbound_enriched_events(self.tenant.token)
+        for pc in self.config.get("processors", []):
+            p = build_processor(pc)
+            p.tenant_engine = self
+            self.initialize_nested_component(p, monitor, require=False)
+            self.processors.append(p)
+            # one consumer group per processor: each sees the full enriched stream
+            self.hosts.append(BusConsumer(self, f"rule-{p.pid}", [topic], self._handler(p),
+                                          threads=int(pc.get("numThreads", 0))))
+        self.api = {"RuleProcessing": RuleProcessingApi(self)}
+
+    @staticmethod
+    def _handler(p: RuleProcessor):
+        def handle(recs):
+            items = []
+            for r in recs:
+                m = json.loads(r.value)
+                items.append((codec.from_wire(m["event"]), m.get("context", {})))
+            p.process_batch(items)
+        return handle
+
+    def tenant_start(self, monitor):
+        for h in self.hosts:
+            self.start_nested_component(h, monitor, require=True)
+
+    def tenant_stop(self, monitor):
+        for h in self.hosts:
+            h.lifecycle_stop(monitor)
+
+
+class RuleProcessingApi:
+    def __init__(self, e):
+        self._e = e
+
+    def list_rule_processors(self) -> list[dict]:
+        return [{"id": p.pid, "type": type(p).__name__, "status": p.status.value,
+                 "alerts": getattr(p, "alerts", 0)} for p in self._e.processors]
+
+
+class RuleProcessingMicroservice(MultitenantMicroservice):
+    identifier = "rule-processing"
+    name = "Rule Processing"
+
+    def service_names(self):
+        return ["RuleProcessing"]
+
+    def create_tenant_engine(self, tenant):
+        return RuleProcessingTenantEngine(self, tenant)

@@ -1,0 +1,216 @@
+"""service-tenant-management: tenant CRUD, tenant templates, tenant configuration bootstrap (global).
+
+Reference: ``TenantManagementMicroservice.java`` (484), ``TenantTemplateManager.java`` (344),
+``TenantBootstrapModelConsumer.java:40-225`` (copy the chosen template into
+``/conf/tenants/<id>/`` and write the ``bootstrapped`` marker), ``TenantModelProducer`` (publish
+tenant-model updates on ``tenant-model-updates``); RPCs from ``tenant-management.proto`` (8):
+CreateTenant, UpdateTenant, GetTenantById, GetTenantByToken, ListTenants, DeleteTenant,
+GetTenantTemplates, GetDatasetTemplates.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import secrets
+import threading
+
+from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
+from ..models.domain import SearchCriteria, SearchResults, Tenant, stamp_created, stamp_updated
+from ..persistence.store import EntityStore, create_store
+from ..runtime.config import dump_document
+from ..runtime.microservice import GlobalMicroservice
+
+MULTITENANT_SERVICES = [
+    "event-sources", "inbound-processing", "event-management", "device-management", "device-registration",
+    "device-state", "rule-processing", "outbound-connectors", "command-delivery", "asset-management",
+    "batch-operations", "schedule-management", "label-generation", "streaming-media", "event-search",
+]
+
+_MEM = {"datastore": {"type": "memory"}}
+
+# Tenant configuration templates: service identifier -> configuration document.
+TENANT_TEMPLATES: dict[str, dict] = {
+    "default": {
+        "name": "Default (in-memory datastores)",
+        "services": {
+            "event-sources": {"sources": [{"id": "default-json", "decoder": "json", "receivers": []},
+                                          {"id": "default-protobuf", "decoder": "protobuf", "receivers": []}],
+                              "deduplicator": {"type": "alternate-id"}},
+            "inbound-processing": {"processingThreadCount": 25},
+            "event-management": {"datastore": {"type": "memory"}, "buffered": False},
+            "device-management": _MEM, "asset-management": _MEM, "batch-operations": _MEM,
+            "schedule-management": _MEM, "device-state": _MEM | {"presence": {"checkInterval": "PT10M",
+                                                                              "missingInterval": "PT8H"}},
+            "device-registration": {"allowNewDevices": True, "defaultDeviceTypeToken": None,
+                                    "defaultCustomerToken": None, "defaultAreaToken": None, "autoAssign": True},
+            "rule-processing": {"processors": []},
+            "outbound-connectors": {"connectors": []},
+            "command-delivery": {"router": {"type": "single-choice", "destination": "default"},
+                                 "destinations": [{"id": "default", "encoder": "json", "provider": "log"}]},
+            "label-generation": {"generators": [{"id": "qrcode", "type": "qrcode"}]},
+            "streaming-media": _MEM, "event-search": {"providers": []},
+        },
+    },
+}
+TENANT_TEMPLATES["sqlite"] = copy.deepcopy(TENANT_TEMPLATES["default"])
+TENANT_TEMPLATES["sqlite"]["name"] = "Durable SQLite datastores"
+for _svc in ("device-management", "asset-management", "batch-operations", "schedule-management", "device-state",
+             "streaming-media"):
+    TENANT_TEMPLATES["sqlite"]["services"][_svc] = {"datastore": {"type": "sqlite",
+                                                                  "path": f"/tmp/sitewhere/[[tenant.token]]-{_svc}.db"}}
+TENANT_TEMPLATES["sqlite"]["services"]["event-management"] = {
+    "datastore": {"type": "sqlite", "path": "/tmp/sitewhere/[[tenant.token]]-events.db"}, "buffered": True}
+TENANT_TEMPLATES["cassandra"] = copy.deepcopy(TENANT_TEMPLATES["default"])
+TENANT_TEMPLATES["cassandra"]["name"] = "Time-bucketed event store (Cassandra layout)"
+TENANT_TEMPLATES["cassandra"]["services"]["event-management"] = {"datastore": {"type": "bucketed",
+                                                                               "bucket_ms": 3600000}}
+TENANT_TEMPLATES["mongodb"] = copy.deepcopy(TENANT_TEMPLATES["default"])
+TENANT_TEMPLATES["mongodb"]["name"] = "MongoDB datastores"
+for _svc in ("device-management", "asset-management", "batch-operations", "schedule-management", "device-state",
+             "streaming-media"):
+    TENANT_TEMPLATES["mongodb"]["services"][_svc] = {"datastore": {"type": "mongodb",
+                                                                   "uri": "${mongodb.uri:mongodb://localhost:27017}",
+                                                                   "database": "tenant-[[tenant.token]]"}}
+TENANT_TEMPLATES["gpu"] = copy.deepcopy(TENANT_TEMPLATES["default"])
+TENANT_TEMPLATES["gpu"]["name"] = "MI355X-accelerated inbound pipeline"
+TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5}
+
+DATASET_TEMPLATES = {
+    "empty": {"name": "Empty dataset", "description": "No data is created."},
+    "construction": {"name": "Construction site", "description": "Device types, devices, assignments, areas, zones, "
+                                                                  "assets and schedules for a construction site."},
+    "airtraffic": {"name": "Air traffic", "description": "Aircraft tracking devices with a flight-zone model."},
+}
+
+
+class TenantManagement:
+    TENANTS = "tenants"
+
+    def __init__(self, store: EntityStore | None = None, on_change=None):
+        self._s = store or create_store("memory")
+        self._s.register(self.TENANTS, Tenant, ("token",))
+        self._on_change = on_change or (lambda kind, t: None)
+
+    def create_tenant(self, request: dict) -> Tenant:
+        token = request.get("token")
+        if not token:
+            raise SiteWhereSystemException(ErrorCode.IncompleteData, detail="tenant token required")
+        if self._s.get_by_token(self.TENANTS, token):
+            raise SiteWhereSystemException(ErrorCode.DuplicateTenantToken, detail=token)
+        tpl = request.get("configurationTemplateId", "default")
+        if tpl not in TENANT_TEMPLATES:
+            raise SiteWhereSystemException(ErrorCode.InvalidTemplate, detail=tpl)
+        t = Tenant(token=token, name=request.get("name", token),
+                   authentication_token=request.get("authenticationToken") or secrets.token_hex(12),
+                   authorized_user_ids=list(request.get("authorizedUserIds", [])),
+                   configuration_template_id=tpl,
+                   dataset_template_id=request.get("datasetTemplateId", "empty"),
+                   image_url=request.get("imageUrl"), metadata=dict(request.get("metadata", {})))
+        stamp_created(t)
+        t = self._s.put(self.TENANTS, t)
+        self._on_change("created", t)
+        return t
+
+    def update_tenant(self, id: str, request: dict) -> Tenant:
+        t = self._require_id(id)
+        for k, f in (("name", "name"), ("authenticationToken", "authentication_token"), ("imageUrl", "image_url"),
+                     ("authorizedUserIds", "authorized_user_ids"), ("metadata", "metadata")):
+            if k in request:
+                setattr(t, f, request[k])
+        stamp_updated(t)
+        t = self._s.put(self.TENANTS, t)
+        self._on_change("updated", t)
+        return t
+
+    def get_tenant(self, id: str) -> Tenant | None:
+        return self._s.get(self.TENANTS, id)
+
+    get_tenant_by_id = get_tenant
+
+    def get_tenant_by_token(self, token: str) -> Tenant | None:
+        return self._s.get_by_token(self.TENANTS, token)
+
+    def list_tenants(self, criteria: SearchCriteria | None = None, text_search: str | None = None,
+                     user_id: str | None = None) -> SearchResults:
+        c = criteria or SearchCriteria(page_size=0)
+
+        def pred(t: Tenant):
+            if text_search and text_search.lower() not in (t.name + t.token).lower():
+                return False
+            if user_id and user_id not in t.authorized_user_ids:
+                return False
+            return True
+
+        ts = self._s.query(self.TENANTS, pred, sort_key=lambda t: t.name)
+        return SearchResults(len(ts), c.slice(ts))
+
+    def delete_tenant(self, id: str) -> Tenant:
+        t = self._require_id(id)
+        self._s.delete(self.TENANTS, id)
+        self._on_change("deleted", t)
+        return t
+
+    def get_tenant_templates(self) -> list[dict]:
+        return [{"id": k, "name": v["name"]} for k, v in sorted(TENANT_TEMPLATES.items())]
+
+    def get_dataset_templates(self) -> list[dict]:
+        return [{"id": k, **v} for k, v in sorted(DATASET_TEMPLATES.items())]
+
+    def _require_id(self, id: str) -> Tenant:
+        t = self._s.get(self.TENANTS, id)
+        if t is None:
+            raise NotFoundException(ErrorCode.InvalidTenantToken, id)
+        return t
+
+
+class TenantManagementMicroservice(GlobalMicroservice):
+    identifier = "tenant-management"
+    name = "Tenant Management"
+
+    def __init__(self, instance, hostname=None, store: EntityStore | None = None):
+        super().__init__(instance, hostname)
+        self._store = store
+        self.tenants: TenantManagement | None = None
+        self._lock = threading.Lock()
+
+    def default_configuration(self) -> dict:
+        return {"datastore": {"type": "memory"}}
+
+    def register_services(self, resolver):
+        self.tenants = TenantManagement(self._store, on_change=self._tenant_changed)
+        resolver.add_global("TenantManagement", self.tenants)
+
+    # TenantModelProducer + TenantBootstrapModelConsumer, fused: publish the model update and
+    # (idempotently) copy the template into the tenant's configuration subtree.
+    def _tenant_changed(self, kind: str, t: Tenant):
+        inst = self.instance
+        self.producer.send(inst.naming.tenant_model_updates(), t.token,
+                           json.dumps({"type": kind, "tenant": t.to_dict()}).encode())
+        if kind == "created":
+            self.bootstrap_tenant_configuration(t)
+        elif kind == "deleted":
+            try:
+                inst.coord.delete(inst.tenant_conf_path(t.token), recursive=True)
+            except KeyError:
+                pass
+
+    def bootstrap_tenant_configuration(self, t: Tenant):
+        inst = self.instance
+        with self._lock:
+            if inst.coord.exists(inst.tenant_conf_path(t.token, "bootstrapped")):
+                return
+            tpl = TENANT_TEMPLATES[t.configuration_template_id]
+            for svc, doc in tpl["services"].items():
+                inst.coord.put(inst.tenant_conf_path(t.token, f"{svc}.json"), dump_document(doc))
+            inst.coord.ensure(inst.tenant_conf_path(t.token, "bootstrapped"))
+
+    def configuration_updated(self, doc):
+        pass
+
+
+def bootstrap_default_tenant(tm: TenantManagement):
+    """Instance template initializer (reference tenantModel.groovy)."""
+    if tm.get_tenant_by_token("default") is None:
+        tm.create_tenant({"token": "default", "name": "Default Tenant", "authenticationToken": "sitewhere1234567890",
+                          "authorizedUserIds": ["admin", "noadmin"], "configurationTemplateId": "default",
+                          "datasetTemplateId": "construction"})

@@ -1,0 +1,190 @@
+"""End-to-end service tests over a whole co-located instance (all microservices in one process).
+
+Mirrors the reference's behavioural expectations: bootstrap of users / tenants /
+datasets, the inbound event flow decode -> validate -> persist -> enrich -> device state / rules /
+connectors, registration of unknown devices, command delivery, batch operations, schedules, labels.
+"""
+from __future__ import annotations
+
+import time
+
+import pytest
+
+from sitewhere_amd.assembly import SiteWhereInstance
+from sitewhere_amd.models import wire
+from sitewhere_amd.models.domain import DeviceEventType
+
+
+def wait_until(cond, timeout=10.0, step=0.02):
+    end = time.time() + timeout
+    while time.time() < end:
+        v = cond()
+        if v:
+            return v
+        time.sleep(step)
+    return cond()
+
+
+@pytest.fixture(scope="module")
+def sw():
+    inst = SiteWhereInstance().start()
+    inst.wait_for_tenant("default", 60)
+    yield inst
+    inst.stop()
+
+
+def as_system(sw, fn, tenant="default"):
+    return sw.instance.system_user.run(fn, tenant)
+
+
+def test_instance_bootstrap(sw):
+    um = sw.api("UserManagement")
+    tm = sw.api("TenantManagement")
+    users = as_system(sw, lambda: um.list_users())
+    assert {u.username for u in users.results} >= {"admin", "noadmin"}
+    t = as_system(sw, lambda: tm.get_tenant_by_token("default"))
+    assert t is not None and t.dataset_template_id == "construction"
+    dm = sw.api("DeviceManagement", "default")
+    assert as_system(sw, lambda: dm.list_devices({"pageSize": 0}).num_results) == 20
+    am = sw.api("AssetManagement", "default")
+    assert as_system(sw, lambda: am.list_assets().num_results) == 6
+    sm = sw.api("ScheduleManagement", "default")
+    assert as_system(sw, lambda: sm.get_schedule_by_token("every-hour")) is not None
+
+
+def test_authentication(sw):
+    um = sw.api("UserManagement")
+    u = as_system(sw, lambda: um.authenticate("admin", "password", True))
+    assert u.username == "admin"
+    with pytest.raises(Exception):
+        as_system(sw, lambda: um.authenticate("admin", "wrong", False))
+
+
+def test_event_flow_measurement_to_state(sw):
+    es = sw.tenant_engine("event-sources")
+    dm = sw.api("DeviceManagement", "default")
+    em = sw.api("DeviceEventManagement", "default")
+    dev = as_system(sw, lambda: dm.get_device_by_token("meitrack-001"))
+    aid = dev.device_assignment_id
+    n = es.inject("default-protobuf", wire.measurements("meitrack-001", {"engine.temp": 91.5}, event_date=1_700_000_000_000))
+    assert n == 1
+    res = wait_until(lambda: as_system(sw, lambda: em.list_measurements_for_index("Assignment", [aid])).results)
+    assert res and res[0].name == "engine.temp" and res[0].value == 91.5
+    assert res[0].device_id == dev.id and res[0].customer_id is not None
+    ds = sw.api("DeviceStateManagement", "default")
+    st = wait_until(lambda: as_system(sw, lambda: ds.get_device_state_by_device_assignment_id(aid)))
+    assert st is not None
+    assert wait_until(lambda: "engine.temp" in (as_system(sw, lambda: ds.get_device_state_by_device_assignment_id(aid))
+                                                .last_measurement_event_ids or {}))
+
+
+def test_event_flow_location_and_alert(sw):
+    es = sw.tenant_engine("event-sources")
+    dm = sw.api("DeviceManagement", "default")
+    em = sw.api("DeviceEventManagement", "default")
+    aid = as_system(sw, lambda: dm.get_device_by_token("meitrack-002")).device_assignment_id
+    es.inject("default-protobuf", wire.location("meitrack-002", 34.1025, -84.2420, 300.0))
+    es.inject("default-protobuf", wire.alert("meitrack-002", "engine.overheat", "too hot"))
+    locs = wait_until(lambda: as_system(sw, lambda: em.list_locations_for_index("Assignment", [aid])).results)
+    assert abs(locs[0].latitude - 34.1025) < 1e-9 and locs[0].elevation == 300.0
+    alerts = wait_until(lambda: as_system(sw, lambda: em.list_alerts_for_index("Assignment", [aid])).results)
+    assert alerts[0].type == "engine.overheat" and alerts[0].message == "too hot"
+
+
+def test_json_decoder_and_duplicates(sw):
+    es = sw.tenant_engine("event-sources")
+    dm = sw.api("DeviceManagement", "default")
+    em = sw.api("DeviceEventManagement", "default")
+    aid = as_system(sw, lambda: dm.get_device_by_token("iphone6s-000")).device_assignment_id
+    import json
+    body = json.dumps({"deviceToken": "iphone6s-000", "type": "DeviceMeasurement",
+                       "request": {"name": "battery", "value": 0.5, "alternateId": "alt-batt-1"}}).encode()
+    es.inject("default-json", body)
+    got = wait_until(lambda: as_system(sw, lambda: em.get_device_event_by_alternate_id("alt-batt-1")))
+    assert got is not None and got.device_assignment_id == aid
+    es.inject("default-json", body)       # duplicate alternate id -> dropped by the deduplicator
+    time.sleep(0.3)
+    res = as_system(sw, lambda: em.list_measurements_for_index("Assignment", [aid])).results
+    assert sum(1 for e in res if e.alternate_id == "alt-batt-1") == 1
+
+
+def test_unregistered_device_registration(sw):
+    es = sw.tenant_engine("event-sources")
+    dm = sw.api("DeviceManagement", "default")
+    es.inject("default-protobuf", wire.registration("new-device-001", "raspberrypi"))
+    dev = wait_until(lambda: as_system(sw, lambda: dm.get_device_by_token("new-device-001")), timeout=10)
+    assert dev is not None
+    assert wait_until(lambda: as_system(sw, lambda: dm.get_device_by_token("new-device-001")).device_assignment_id)
+
+
+def test_command_invocation_delivery(sw):
+    dm = sw.api("DeviceManagement", "default")
+    em = sw.api("DeviceEventManagement", "default")
+    dev = as_system(sw, lambda: dm.get_device_by_token("galaxytab-000"))
+    cmd = as_system(sw, lambda: dm.get_device_command_by_token("galaxytab-ping"))
+    inv = as_system(sw, lambda: em.add_command_invocations(dev.device_assignment_id, {
+        "initiator": "REST", "initiatorId": "admin", "target": "Assignment", "commandToken": cmd.token,
+        "deviceCommandId": cmd.id, "parameterValues": {}}))
+    assert inv[0].event_type == DeviceEventType.CommandInvocation
+    cd = sw.tenant_engine("command-delivery")
+    prov = cd.destinations["default"].provider
+    assert wait_until(lambda: len(prov.delivered) >= 1)
+
+
+def test_batch_operation(sw):
+    dm = sw.api("DeviceManagement", "default")
+    bm = sw.api("BatchManagement", "default")
+    ids = [as_system(sw, lambda t=t: dm.get_device_by_token(t)).id for t in ("openhab-000", "openhab-001")]
+    op = as_system(sw, lambda: bm.create_batch_command_invocation({"token": "batch-1", "commandToken": "openhab-ping",
+                                                                  "deviceIds": ids}))
+    done = wait_until(lambda: as_system(sw, lambda: bm.get_batch_operation(op.id)).processing_status.value
+                      .startswith("Finished"))
+    assert done
+    els = as_system(sw, lambda: bm.list_batch_operation_elements(op.id)).results
+    assert [e.processing_status.value for e in els] == ["Succeeded", "Succeeded"]
+
+
+def test_label_generation_png(sw):
+    lg = sw.api("LabelGeneration", "default")
+    dm = sw.api("DeviceManagement", "default")
+    dev = as_system(sw, lambda: dm.get_device_by_token("galaxytab-001"))
+    label = as_system(sw, lambda: lg.get_device_label("qrcode", dev.id))
+    assert label.content.startswith(b"\x89PNG")
+
+
+def test_tenant_engine_state_and_topology(sw):
+    dm_ms = sw["device-management"]
+    assert dm_ms.mt_management.check_tenant_engine_available("default")
+    tree = dm_ms.state_tree()
+    assert tree["tenantEngines"]["default"] in ("Started", "StartedWithErrors")
+
+
+def test_new_tenant_gpu_template_cpu_engine():
+    """Tenant on the MI355X template: inbound runs the fused engine (CPU oracle when no GPU)."""
+    inst = SiteWhereInstance().start()
+    try:
+        inst.wait_for_tenant("default", 60)
+        tm = inst.api("TenantManagement")
+        inst.instance.system_user.run(lambda: tm.create_tenant({"token": "fast", "name": "Fast",
+                                                                "configurationTemplateId": "gpu",
+                                                                "datasetTemplateId": "construction"}))
+        inst.wait_for_tenant("fast", 60)
+        # route the protobuf source through the raw path
+        ib = inst.tenant_engine("inbound-processing", "fast")
+        assert ib.engine_kind in ("cpu", "gpu")
+        dm = inst.api("DeviceManagement", "fast")
+        em = inst.api("DeviceEventManagement", "fast")
+        run = lambda f: inst.instance.system_user.run(f, "fast")  # noqa: E731
+        dev = run(lambda: dm.get_device_by_token("meitrack-000"))
+        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None)
+        api = inst.api("InboundProcessing", "fast")
+        r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
+                                              wire.location("meitrack-000", 34.10, -84.24),
+                                              wire.measurements("nobody", {"x": 1.0})]))
+        assert r["persisted"] == 2
+        ms = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id])).results
+        assert ms and ms[0].name == "rpm" and ms[0].value == 1200.0
+        st = run(lambda: api.get_statistics())
+        assert st["engine.unregistered"] >= 1
+    finally:
+        inst.stop()
