@@ -965,6 +965,12 @@ int sw_host_alloc(int64_t bytes, void** host, void** dev) {
 
 int sw_host_free(void* host) { return (int)hipHostFree(host); }
 
+// Stream-ordered SDMA copy device -> pinned host (outbound rows of a finished step, overlapped with
+// the next step's kernels and H2D on a third stream; PCIe is full duplex).
+int sw_copy_d2h(void* dst_host, const void* src_dev, int64_t bytes, hipStream_t s) {
+  return (int)hipMemcpyAsync(dst_host, src_dev, (size_t)bytes, hipMemcpyDeviceToHost, s);
+}
+
 int sw_abi_sizes(int64_t* out) {
   out[0] = sizeof(SwEventRec);
   out[1] = sizeof(SwOutRec);

@@ -166,6 +166,7 @@ def gpu():
         _proto(lib, "sw_host_alloc", c_int32, c_int64, P, P)
         _proto(lib, "sw_host_free", c_int32, P)
         _proto(lib, "sw_push_out", c_int32, P, P, P, c_int64, c_int32, P)
+        _proto(lib, "sw_copy_d2h", c_int32, P, P, c_int64, P)
         _gpu = lib
         return lib
 

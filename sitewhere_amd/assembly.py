@@ -31,6 +31,7 @@ from .services.rule_processing import RuleProcessingMicroservice
 from .services.schedule_management import ScheduleManagementMicroservice
 from .services.tenant_management import TenantManagementMicroservice
 from .services.user_management import UserManagementMicroservice
+from .web.rest import WebRestMicroservice
 
 GLOBAL_SERVICES = [UserManagementMicroservice, TenantManagementMicroservice]
 MULTITENANT_SERVICES = [
@@ -40,20 +41,24 @@ MULTITENANT_SERVICES = [
     CommandDeliveryMicroservice, BatchOperationsMicroservice, ScheduleManagementMicroservice,
     LabelGenerationMicroservice, StreamingMediaMicroservice, EventSearchMicroservice,
 ]
-SERVICES_BY_ID = {c.identifier: c for c in [InstanceManagementMicroservice, *GLOBAL_SERVICES, *MULTITENANT_SERVICES]}
+SERVICES_BY_ID = {c.identifier: c for c in [InstanceManagementMicroservice, *GLOBAL_SERVICES, *MULTITENANT_SERVICES,
+                                            WebRestMicroservice]}
 
 
 class SiteWhereInstance:
     """All microservices of one instance sharing the in-process bus, coordination store and RPC resolver."""
 
     def __init__(self, settings: InstanceSettings | None = None, template: str = "default",
-                 services: list[str] | None = None, instance: Instance | None = None, **instance_kw):
+                 services: list[str] | None = None, instance: Instance | None = None, rest_port: int = 0,
+                 **instance_kw):
         self.instance = instance or Instance(settings or InstanceSettings(heartbeat_s=5.0), **instance_kw)
         self.template = template
         wanted = set(services) if services else None
         self.instance_management = InstanceManagementMicroservice(self.instance, template=template)
         self.services = [c(self.instance) for c in GLOBAL_SERVICES + MULTITENANT_SERVICES
                          if wanted is None or c.identifier in wanted]
+        if wanted is None or "web-rest" in wanted:
+            self.services.append(WebRestMicroservice(self.instance, port=rest_port))
         self.started = False
 
     def __getitem__(self, identifier: str):
@@ -86,6 +91,10 @@ class SiteWhereInstance:
                     time.sleep(0.02)
                 _ = e
         return self
+
+    @property
+    def rest_app(self):
+        return self["web-rest"].app
 
     def tenant_engine(self, identifier: str, token: str = "default"):
         return self[identifier].get_tenant_engine(token)

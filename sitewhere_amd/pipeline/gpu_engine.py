@@ -402,6 +402,10 @@ class PipelinedRunner:
     * push stream: ``k_push_out`` stores the rows into the mapped host ring over PCIe writes,
       overlapping the next step (the row count is read on the device: no host sync)
     ``mode="direct"`` instead lets the persist kernel store straight to host memory.
+    ``mode="sdma"``: rows land in HBM; once step k's row count is known (the host already syncs on
+    step k while step k+1 runs) an SDMA ``hipMemcpyAsync`` of exactly those rows goes out on the push
+    stream, concurrent with step k+1's kernels and step k+2's H2D (PCIe full duplex); step k is
+    delivered one step later.
     """
 
     def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
@@ -426,6 +430,7 @@ class PipelinedRunner:
         self.k = 0
         self.delivered = 0
         self.pending = None
+        self.copying = None          # sdma mode: (buffer, n_out) whose D2H copy is in flight
 
     def submit(self, raw_host: torch.Tensor, off_host: torch.Tensor, n_msgs: int, now_ms: int | None = None,
                presence: bool = False):
@@ -440,10 +445,10 @@ class PipelinedRunner:
             self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
             self.ev_h2d[b].record(self.h2d)
         self.comp.wait_event(self.ev_h2d[b])
-        if k >= 2 and self.mode == "push":
+        if k >= 2 and self.mode in ("push", "sdma"):
             self.comp.wait_event(self.ev_push[b])         # push k-2 was the last reader of staging ring b
         self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
-                          out_to_device=(self.mode == "push"))
+                          out_to_device=(self.mode in ("push", "sdma")))
         self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
         self.scal_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
         self.ev_comp[b].record(self.comp)
@@ -461,6 +466,18 @@ class PipelinedRunner:
         self.pending = b
         self.k += 1
 
+    def _deliver(self, b: int, n_out: int):
+        if self.deliver and self.on_outbound is not None and n_out:
+            self.on_outbound(self.e.out_host[b].view(OUT_REC, n_out))
+        self.delivered += n_out
+
+    def _finish_copy(self):
+        if self.copying is not None:
+            cb, cn = self.copying
+            self.ev_push[cb].synchronize()
+            self._deliver(cb, cn)
+            self.copying = None
+
     def _drain(self):
         if self.pending is None:
             return
@@ -469,13 +486,23 @@ class PipelinedRunner:
         if self.mode == "push" and self.deliver:
             self.ev_push[pb].synchronize()
         n_out = int(self.scal_host[pb][7])
-        if self.deliver and self.on_outbound is not None and n_out:
-            self.on_outbound(self.e.out_host[pb].view(OUT_REC, n_out))
-        self.delivered += n_out
         self.pending = None
+        if self.mode != "sdma":
+            self._deliver(pb, n_out)
+            return
+        self._finish_copy()
+        if self.deliver and n_out:
+            rc = self.e.lib.sw_copy_d2h(ctypes.c_void_p(self.e.out_host[pb].host),
+                                        ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
+                                        ctypes.c_void_p(self.push.cuda_stream))
+            if rc:
+                raise RuntimeError(f"sw_copy_d2h failed ({rc})")
+        self.ev_push[pb].record(self.push)
+        self.copying = (pb, n_out)
 
     def flush(self):
         self._drain()
+        self._finish_copy()
         self.comp.synchronize()
         self.push.synchronize()
 

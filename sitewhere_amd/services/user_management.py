@@ -201,8 +201,8 @@ def bootstrap_default_users(um: UserManagement):
         all_auths = list(AUTHORITY_DESCRIPTIONS)
         um.create_user({"username": "admin", "password": "password", "firstName": "Admin", "lastName": "User",
                         "authorities": all_auths})
-        limited = [a for a in all_auths if a not in (SiteWhereAuthority.ViewServerInfo, SiteWhereAuthority.AdminTenants,
-                                                     SiteWhereAuthority.AdminUsers)]
+        limited = [a for a in all_auths if a not in (SiteWhereAuthority.AdminServer, SiteWhereAuthority.ViewServerInfo,
+                                                     SiteWhereAuthority.AdminTenants, SiteWhereAuthority.AdminUsers)]
         um.create_user({"username": "noadmin", "password": "noadmin", "firstName": "Non-Admin", "lastName": "User",
                         "authorities": limited})
 

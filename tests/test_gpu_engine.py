@@ -98,20 +98,25 @@ def test_presence_parity():
     assert sorted(rg.out["assignment"].tolist()) == sorted(rc.out["assignment"].tolist())
 
 
-def test_pipelined_runner_matches_sync():
+@pytest.mark.parametrize("mode", ["direct", "push", "sdma"])
+def test_pipelined_runner_matches_sync(mode):
     g, c = pair()
     seen = []
-    runner = PipelinedRunner(g, max_raw_bytes=1 << 20, on_outbound=lambda rows: seen.append(rows.copy()))
+    runner = PipelinedRunner(g, max_raw_bytes=1 << 20, on_outbound=lambda rows: seen.append(rows.copy()), mode=mode)
     batches = [fleet_batch(2000, seed=300 + k) for k in range(5)]
     total = 0
+    cpu_rows = []
     for k, (raw, offs) in enumerate(batches):
         rh = torch.from_numpy(raw).pin_memory()
         oh = torch.from_numpy(offs.view(np.int32)).pin_memory()
         runner.submit(rh, oh, len(offs) - 1, now_ms=NOW + k)
-        total += c.step(raw, offs, NOW + k, presence=False).n_persisted
+        r = c.step(raw, offs, NOW + k, presence=False)
+        total += r.n_persisted
+        cpu_rows.append(r.out)
     runner.flush()
     assert runner.delivered == total == sum(len(x) for x in seen)
     assert g.stats_dict() == c.stats_dict()
+    assert canon_out(np.concatenate(seen), None) == canon_out(np.concatenate(cpu_rows), None)
 
 
 def test_standalone_pip_kernel():

@@ -188,3 +188,33 @@ def test_new_tenant_gpu_template_cpu_engine():
         assert st["engine.unregistered"] >= 1
     finally:
         inst.stop()
+
+
+@pytest.mark.gpu
+def test_gpu_tenant_engine_on_device():
+    """On an MI355X the MI355X tenant template runs the HIP engine (no silent CPU fallback)."""
+    inst = SiteWhereInstance().start()
+    try:
+        inst.wait_for_tenant("default", 60)
+        tm = inst.api("TenantManagement")
+        inst.instance.system_user.run(lambda: tm.create_tenant({"token": "fastgpu", "name": "Fast",
+                                                                "configurationTemplateId": "gpu",
+                                                                "datasetTemplateId": "construction"}))
+        inst.wait_for_tenant("fastgpu", 120)
+        ib = inst.tenant_engine("inbound-processing", "fastgpu")
+        assert ib.engine_kind == "gpu"
+        run = lambda f: inst.instance.system_user.run(f, "fastgpu")  # noqa: E731
+        dm = inst.api("DeviceManagement", "fastgpu")
+        em = inst.api("DeviceEventManagement", "fastgpu")
+        dev = run(lambda: dm.get_device_by_token("meitrack-000"))
+        api = inst.api("InboundProcessing", "fastgpu")
+        r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
+                                              wire.location("meitrack-000", 34.10, -84.24),
+                                              wire.measurements("nobody", {"x": 1.0})]))
+        assert r["persisted"] == 2
+        ms = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id])).results
+        assert ms and ms[0].name == "rpm" and ms[0].value == 1200.0
+        st = run(lambda: api.get_device_state(dev.device_assignment_id))
+        assert "rpm" in st["measurements"]
+    finally:
+        inst.stop()
