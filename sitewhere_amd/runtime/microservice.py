@@ -35,7 +35,7 @@ from ..core.metrics import MetricRegistry, MetricsReporter
 from ..core.security import SystemUser, TokenManagement
 from ..core.tracing import Tracer, global_tracer
 from ..models.domain import Tenant
-from ..rpc.transport import GrpcChannel, LocalChannel, RpcServer, ServiceResolver
+from ..rpc.transport import GrpcChannel, LocalChannel, RpcServer, ServiceProxy, ServiceResolver
 from .config import InstanceSettings, dump_document, parse_document, substitute
 from .scripting import SCRIPT_TEMPLATES, ScriptManagement, ScriptRunner
 from .topology import ApiDemux, TopologyStateAggregator
@@ -74,6 +74,25 @@ class Instance:
 
     def system_jwt(self) -> str:
         return self.system_user.authentication().jwt
+
+
+class _WaitingChannel:
+    """Retries calls that fail with TenantEngineNotAvailable (100 ms -> 3 s backoff, bounded)."""
+
+    def __init__(self, channel, wait_s: float):
+        self.ch, self.wait_s = channel, wait_s
+
+    def call(self, service, method, *args, **kwargs):
+        end = time.time() + self.wait_s
+        delay = 0.1
+        while True:
+            try:
+                return self.ch.call(service, method, *args, **kwargs)
+            except TenantEngineNotAvailableException:
+                if time.time() + delay > end:
+                    raise
+                time.sleep(delay)
+                delay = min(3.0, delay * 2)
 
 
 # ------------------------------------------------------------------------------ log forwarding
@@ -242,9 +261,11 @@ class Microservice(LifecycleComponent):
             self._demuxes[identifier] = d
         return d
 
-    def api(self, service: str, tenant: str | None = None):
-        """Typed proxy to a service (co-located: in-process channel; remote: gRPC)."""
-        return self.instance.local_channel.proxy(service, tenant)
+    def api(self, service: str, tenant: str | None = None, wait_s: float = 30.0):
+        """Typed proxy to a service (co-located: in-process channel; remote: gRPC).  Calls made while
+        the target tenant engine is still starting wait for it with backoff, like the reference's
+        ``MultitenantApiDemux.waitForCorrespondingTenantEngineAvailable``."""
+        return ServiceProxy(_WaitingChannel(self.instance.local_channel, wait_s), service, tenant)
 
     # ---- hooks ----------------------------------------------------------------
     def register_services(self, resolver: ServiceResolver):

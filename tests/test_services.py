@@ -191,6 +191,7 @@ def test_new_tenant_gpu_template_cpu_engine():
 
 
 @pytest.mark.gpu
+@pytest.mark.skipif(not __import__("conftest").gpu_available(), reason="needs an MI355X GPU")
 def test_gpu_tenant_engine_on_device():
     """On an MI355X the MI355X tenant template runs the HIP engine (no silent CPU fallback)."""
     inst = SiteWhereInstance().start()
