@@ -21,6 +21,8 @@
 // are read from device scalars so the host never synchronises inside a step
 // (the whole step is hipGraph-capturable).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <stdint.h>
 #include "swtypes.h"
 #include "swdecode.h"
@@ -969,6 +971,59 @@ int sw_host_free(void* host) { return (int)hipHostFree(host); }
 // the next step's kernels and H2D on a third stream; PCIe is full duplex).
 int sw_copy_d2h(void* dst_host, const void* src_dev, int64_t bytes, hipStream_t s) {
   return (int)hipMemcpyAsync(dst_host, src_dev, (size_t)bytes, hipMemcpyDeviceToHost, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Explicit SDMA copies through the HSA runtime.  hipMemcpyAsync D2H into pinned memory is served by
+// a blit *kernel* on this ROCm (it occupies CUs for the whole PCIe-bound transfer and slows the
+// pipeline's kernels); hsa_amd_memory_async_copy_on_engine puts the transfer on a copy engine that
+// uses no CUs.  The caller orders the copy after the producing step by host sync (the runner has
+// already waited for the step), so no dependency signal is needed.
+static hsa_agent_t g_cpu_agent = {0};
+static hsa_status_t sw_find_cpu(hsa_agent_t a, void*) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    g_cpu_agent = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// engine: 0 = runtime's choice (hsa_amd_memory_async_copy), k>0 = SDMA engine bit (1 << (k-1)).
+int sw_sdma_copy(void* dst_host, const void* src_dev, int64_t bytes, int32_t engine, uint64_t* signal_out) {
+  if (g_cpu_agent.handle == 0) {
+    hsa_status_t st = hsa_iterate_agents(sw_find_cpu, nullptr);
+    if (st != HSA_STATUS_SUCCESS && st != HSA_STATUS_INFO_BREAK) return 1000 + (int)st;
+    if (g_cpu_agent.handle == 0) return 999;
+  }
+  hsa_amd_pointer_info_t info;
+  info.size = sizeof(info);
+  hsa_status_t st = hsa_amd_pointer_info(src_dev, &info, nullptr, nullptr, nullptr);
+  if (st != HSA_STATUS_SUCCESS) return 2000 + (int)st;
+  hsa_agent_t gpu_agent = info.agentOwner;
+  hsa_signal_t sig;
+  st = hsa_signal_create(1, 0, nullptr, &sig);
+  if (st != HSA_STATUS_SUCCESS) return 3000 + (int)st;
+  if (engine > 0) {
+    st = hsa_amd_memory_async_copy_on_engine(dst_host, g_cpu_agent, src_dev, gpu_agent, (size_t)bytes, 0, nullptr,
+                                             sig, (hsa_amd_sdma_engine_id_t)(1u << (engine - 1)), true);
+  } else {
+    st = hsa_amd_memory_async_copy(dst_host, g_cpu_agent, src_dev, gpu_agent, (size_t)bytes, 0, nullptr, sig);
+  }
+  if (st != HSA_STATUS_SUCCESS) {
+    hsa_signal_destroy(sig);
+    return 4000 + (int)st;
+  }
+  *signal_out = sig.handle;
+  return 0;
+}
+
+int sw_sdma_wait(uint64_t handle) {
+  hsa_signal_t sig;
+  sig.handle = handle;
+  while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
+  }
+  return (int)hsa_signal_destroy(sig);
 }
 
 int sw_abi_sizes(int64_t* out) {

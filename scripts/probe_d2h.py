@@ -5,7 +5,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+import os; sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from sitewhere_amd._native import gpu  # noqa: E402
 from sitewhere_amd.pipeline.gpu_engine import HostBuffer  # noqa: E402
 

@@ -78,7 +78,7 @@ def build_gpu(force: bool = False) -> Path:
     if force or _stale(out, _GPU_SRC):
         tmp = out.with_suffix(".so.tmp")
         _run([hipcc_path(), f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-              f"-I{CSRC / 'include'}", "-o", str(tmp), *map(str, _GPU_SRC)])
+              f"-I{CSRC / 'include'}", "-o", str(tmp), *map(str, _GPU_SRC), "-lhsa-runtime64"])
         os.replace(tmp, out)
     return out
 
@@ -167,6 +167,8 @@ def gpu():
         _proto(lib, "sw_host_free", c_int32, P)
         _proto(lib, "sw_push_out", c_int32, P, P, P, c_int64, c_int32, P)
         _proto(lib, "sw_copy_d2h", c_int32, P, P, c_int64, P)
+        _proto(lib, "sw_sdma_copy", c_int32, P, P, c_int64, c_int32, ctypes.POINTER(ctypes.c_uint64))
+        _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
         _gpu = lib
         return lib
 

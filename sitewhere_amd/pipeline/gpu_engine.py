@@ -130,9 +130,10 @@ class GpuInboundEngine(EngineBase):
         # outbound ring: mapped pinned host memory the kernels store into (zero-copy), double-buffered
         out_cap = c.rec_cap + c.gen_cap
         self.out_cap = out_cap
-        self.out_host = [HostBuffer(self.lib, out_cap * OUT_REC_SIZE) for _ in range(2)]
+        self.n_out_bufs = int(c.extra.get("out_buffers", 3))
+        self.out_host = [HostBuffer(self.lib, out_cap * OUT_REC_SIZE) for _ in range(self.n_out_bufs)]
         # device-side staging for the outbound push (see PipelinedRunner); OUTBOUND_MODE=direct stores to host
-        self.out_dev = [z(out_cap * OUT_REC_SIZE, u8) for _ in range(2)]
+        self.out_dev = [z(out_cap * OUT_REC_SIZE, u8) for _ in range(self.n_out_bufs)]
         # rules
         t["gen"] = z(c.gen_cap * EVENT_REC.itemsize, u8)
         t["gen_dev"] = z(c.gen_cap, i32)
@@ -395,36 +396,41 @@ class GpuInboundEngine(EngineBase):
 
 
 class PipelinedRunner:
-    """Three-stream pipeline: H2D(k+1) || compute(k) || outbound push(k-1).
+    """Multi-buffered pipeline: H2D(k+1) || compute(k) || outbound D2H(k-1).
 
-    * copy stream: SDMA H2D of the raw payload batch and its offsets (double-buffered device buffers)
-    * compute stream: the fused step; enriched rows land in a device staging ring
-    * push stream: ``k_push_out`` stores the rows into the mapped host ring over PCIe writes,
-      overlapping the next step (the row count is read on the device: no host sync)
-    ``mode="direct"`` instead lets the persist kernel store straight to host memory.
-    ``mode="sdma"``: rows land in HBM; once step k's row count is known (the host already syncs on
-    step k while step k+1 runs) an SDMA ``hipMemcpyAsync`` of exactly those rows goes out on the push
-    stream, concurrent with step k+1's kernels and step k+2's H2D (PCIe full duplex); step k is
-    delivered one step later.
+    * copy stream: SDMA H2D of the raw payload batch and its offsets (``nbuf`` device buffers, so the
+      H2D of later batches runs ahead of compute -- the step is then bound by max(H2D, compute))
+    * compute stream: the fused step; enriched rows land in an HBM staging ring
+    * outbound, by ``mode``:
+      - ``"hsa"`` (default): once step k's row count is known (the host syncs on step k while k+1
+        runs) an explicit copy-engine transfer (``hsa_amd_memory_async_copy``) moves exactly those
+        rows to pinned host memory -- no CUs used (measured on MI355X: the HIP runtime serves
+        ``hipMemcpyAsync`` D2H with a blit *kernel* that occupies CUs for the whole PCIe transfer
+        and slows the pipeline's kernels); delivered one step later
+      - ``"sdma"``: same schedule through ``hipMemcpyAsync`` on a third stream
+      - ``"push"``: ``k_push_out`` stores rows into mapped host memory from a side stream
+      - ``"direct"``: the persist kernel stores rows straight into mapped host memory
     """
 
     def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
-                 on_outbound=None, mode: str | None = None, push_blocks: int = 128):
+                 on_outbound=None, mode: str | None = None, push_blocks: int = 128, nbuf: int = 3):
         import os
         self.e = engine
         dev = engine.device
-        self.mode = mode or os.environ.get("SW_OUTBOUND_MODE", "direct")
+        self.mode = mode or os.environ.get("SW_OUTBOUND_MODE", "hsa")
         self.h2d = torch.cuda.Stream(dev)
         self.comp = torch.cuda.current_stream(dev)
         self.push = torch.cuda.Stream(dev)
-        self.push_blocks = push_blocks
-        self.raw = [torch.empty(max_raw_bytes + _ALIGN, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.off = [torch.empty(engine.cfg.max_msgs + 1, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.nout = [torch.zeros(4, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.scal_host = torch.zeros(2, 16, dtype=torch.int32, pin_memory=True)
-        self.ev_h2d = [torch.cuda.Event() for _ in range(2)]
-        self.ev_comp = [torch.cuda.Event() for _ in range(2)]
-        self.ev_push = [torch.cuda.Event() for _ in range(2)]
+        self.push_blocks = int(os.environ.get("SW_PUSH_BLOCKS", push_blocks))
+        self.sdma_engine = int(os.environ.get("SW_SDMA_ENGINE", 0))
+        nb = self.nbuf = max(2, min(int(os.environ.get("SW_PIPELINE_BUFFERS", nbuf)), engine.n_out_bufs))
+        self.raw = [torch.empty(max_raw_bytes + _ALIGN, dtype=torch.uint8, device=dev) for _ in range(nb)]
+        self.off = [torch.empty(engine.cfg.max_msgs + 1, dtype=torch.int32, device=dev) for _ in range(nb)]
+        self.nout = [torch.zeros(4, dtype=torch.int32, device=dev) for _ in range(nb)]
+        self.scal_host = torch.zeros(nb, 16, dtype=torch.int32, pin_memory=True)
+        self.ev_h2d = [torch.cuda.Event() for _ in range(nb)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(nb)]
+        self.ev_push = [torch.cuda.Event() for _ in range(nb)]
         self.deliver = deliver_outbound
         self.on_outbound = on_outbound
         self.k = 0
@@ -435,20 +441,22 @@ class PipelinedRunner:
     def submit(self, raw_host: torch.Tensor, off_host: torch.Tensor, n_msgs: int, now_ms: int | None = None,
                presence: bool = False):
         k = self.k
-        b = k & 1
+        b = k % self.nbuf
         now_ms = int(time.time() * 1000) if now_ms is None else now_ms
         nbytes = int(raw_host.numel())
         with torch.cuda.stream(self.h2d):
-            if k >= 2:
-                self.h2d.wait_event(self.ev_comp[b])      # compute k-2 was the last reader of buffer b
+            if k >= self.nbuf:
+                self.h2d.wait_event(self.ev_comp[b])      # compute k-nbuf was the last reader of buffer b
             self.raw[b][:nbytes].copy_(raw_host, non_blocking=True)
             self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
             self.ev_h2d[b].record(self.h2d)
+        if self.mode == "hsa" and self.copying is not None and self.copying[0] == b:
+            self._finish_copy()                           # SDMA copy k-2 still reads staging ring b
         self.comp.wait_event(self.ev_h2d[b])
-        if k >= 2 and self.mode in ("push", "sdma"):
+        if k >= self.nbuf and self.mode in ("push", "sdma"):
             self.comp.wait_event(self.ev_push[b])         # push k-2 was the last reader of staging ring b
         self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
-                          out_to_device=(self.mode in ("push", "sdma")))
+                          out_to_device=(self.mode in ("push", "sdma", "hsa")))
         self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
         self.scal_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
         self.ev_comp[b].record(self.comp)
@@ -473,8 +481,13 @@ class PipelinedRunner:
 
     def _finish_copy(self):
         if self.copying is not None:
-            cb, cn = self.copying
-            self.ev_push[cb].synchronize()
+            cb, cn, sig = self.copying
+            if sig is not None:
+                rc = self.e.lib.sw_sdma_wait(sig)
+                if rc:
+                    raise RuntimeError(f"sw_sdma_wait failed ({rc})")
+            else:
+                self.ev_push[cb].synchronize()
             self._deliver(cb, cn)
             self.copying = None
 
@@ -487,10 +500,24 @@ class PipelinedRunner:
             self.ev_push[pb].synchronize()
         n_out = int(self.scal_host[pb][7])
         self.pending = None
-        if self.mode != "sdma":
+        if self.mode not in ("sdma", "hsa"):
             self._deliver(pb, n_out)
             return
         self._finish_copy()
+        if self.mode == "hsa":
+            sig = None
+            if self.deliver and n_out:
+                h = ctypes.c_uint64()
+                rc = self.e.lib.sw_sdma_copy(ctypes.c_void_p(self.e.out_host[pb].host),
+                                             ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
+                                             self.sdma_engine, ctypes.byref(h))
+                if rc:
+                    raise RuntimeError(f"sw_sdma_copy failed ({rc})")
+                sig = h.value
+            self.copying = (pb, n_out, sig)
+            if sig is None:
+                self._finish_copy()
+            return
         if self.deliver and n_out:
             rc = self.e.lib.sw_copy_d2h(ctypes.c_void_p(self.e.out_host[pb].host),
                                         ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
@@ -498,7 +525,7 @@ class PipelinedRunner:
             if rc:
                 raise RuntimeError(f"sw_copy_d2h failed ({rc})")
         self.ev_push[pb].record(self.push)
-        self.copying = (pb, n_out)
+        self.copying = (pb, n_out, None)
 
     def flush(self):
         self._drain()

@@ -38,7 +38,63 @@ from ..models.domain import Tenant
 from ..rpc.transport import GrpcChannel, LocalChannel, RpcServer, ServiceProxy, ServiceResolver
 from .config import InstanceSettings, dump_document, parse_document, substitute
 from .scripting import SCRIPT_TEMPLATES, ScriptManagement, ScriptRunner
-from .topology import ApiDemux, TopologyStateAggregator
+from .topology import ApiDemux, NoLiveReplicaException, TopologyStateAggregator
+
+
+# RPC service name -> owning microservice identifier (used to discover remote replicas).
+SERVICE_OWNERS = {
+    "DeviceManagement": "device-management", "DeviceEventManagement": "event-management",
+    "AssetManagement": "asset-management", "BatchManagement": "batch-operations",
+    "ScheduleManagement": "schedule-management", "TenantManagement": "tenant-management",
+    "UserManagement": "user-management", "DeviceStateManagement": "device-state",
+    "LabelGeneration": "label-generation", "StreamingMedia": "streaming-media", "EventSearch": "event-search",
+    "EventSources": "event-sources", "InboundProcessing": "inbound-processing",
+    "DeviceRegistration": "device-registration", "CommandDelivery": "command-delivery",
+    "OutboundConnectors": "outbound-connectors", "RuleProcessing": "rule-processing",
+}
+
+
+def service_owner(service: str) -> str | None:
+    if service.startswith(("MicroserviceManagement.", "MultitenantManagement.")):
+        return service.split(".", 1)[1]
+    return SERVICE_OWNERS.get(service)
+
+
+class RoutingChannel:
+    """Co-located services go through the in-process channel; everything else through an ApiDemux
+    (topology-discovered gRPC replicas, round-robin, tenant-availability checks)."""
+
+    def __init__(self, instance: "Instance"):
+        self.instance = instance
+        self.topology: TopologyStateAggregator | None = None
+        self._demux: dict[str, ApiDemux] = {}
+        self._lock = threading.Lock()
+
+    def demux(self, identifier: str) -> ApiDemux:
+        with self._lock:
+            d = self._demux.get(identifier)
+            if d is None:
+                if self.topology is None:
+                    raise SiteWhereException("no topology available for remote service discovery")
+                jwt = self.instance.system_jwt()
+                d = ApiDemux(identifier, self.topology, lambda addr: GrpcChannel(addr, jwt))
+                self._demux[identifier] = d
+            return d
+
+    def call(self, service, method, *args, tenant=None, **kwargs):
+        inst = self.instance
+        if service in inst.resolver.names() or not inst.network_rpc:
+            return inst.local_channel.call(service, method, *args, tenant=tenant, **kwargs)
+        owner = service_owner(service)
+        if owner is None:
+            raise SiteWhereException(f"unknown service {service}")
+        from ..rpc.transport import _tenant_for_call
+        ch = self.demux(owner).get_channel(_tenant_for_call(tenant) if SERVICE_OWNERS.get(service) and
+                                           service not in ("TenantManagement", "UserManagement") else None)
+        return ch.call(service, method, *args, tenant=tenant, **kwargs)
+
+    def proxy(self, service: str, tenant: str | None = None):
+        return ServiceProxy(self, service, tenant)
 
 
 class Instance:
@@ -55,6 +111,7 @@ class Instance:
         self.resolver = ServiceResolver()
         self.system_user = SystemUser(self.tokens)
         self.local_channel = LocalChannel(self.resolver, self.tokens, self.system_user.authentication().jwt)
+        self.router = RoutingChannel(self)
         self.network_rpc = network_rpc
         self.microservices: dict[str, "Microservice"] = {}
         self.scripts = ScriptManagement(self.coord, self.path("scripts"))
@@ -88,7 +145,7 @@ class _WaitingChannel:
         while True:
             try:
                 return self.ch.call(service, method, *args, **kwargs)
-            except TenantEngineNotAvailableException:
+            except (TenantEngineNotAvailableException, NoLiveReplicaException):
                 if time.time() + delay > end:
                     raise
                 time.sleep(delay)
@@ -265,7 +322,7 @@ class Microservice(LifecycleComponent):
         """Typed proxy to a service (co-located: in-process channel; remote: gRPC).  Calls made while
         the target tenant engine is still starting wait for it with backoff, like the reference's
         ``MultitenantApiDemux.waitForCorrespondingTenantEngineAvailable``."""
-        return ServiceProxy(_WaitingChannel(self.instance.local_channel, wait_s), service, tenant)
+        return ServiceProxy(_WaitingChannel(self.instance.router, wait_s), service, tenant)
 
     # ---- hooks ----------------------------------------------------------------
     def register_services(self, resolver: ServiceResolver):
@@ -311,6 +368,8 @@ class Microservice(LifecycleComponent):
         steps.add_step(SimpleLifecycleStep("Coordination", lambda m: inst.coord.ensure(inst.conf_path())))
         steps.add_step(SimpleLifecycleStep("Register RPC services", lambda m: self._register_rpc()))
         steps.add_initialize_step(self, self.topology, require=True)
+        if inst.router.topology is None:
+            inst.router.topology = self.topology
         steps.execute(monitor)
         if inst.settings.log_metrics:
             self._reporter = MetricsReporter(self.metrics, lambda s: self.logger.info("metrics %s", s),

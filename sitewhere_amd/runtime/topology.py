@@ -21,6 +21,10 @@ from ..core.errors import SiteWhereException, TenantEngineNotAvailableException
 from ..core.lifecycle import LifecycleComponent, LifecycleStatus
 
 
+class NoLiveReplicaException(SiteWhereException):
+    """No replica of the target microservice is in the topology (yet)."""
+
+
 @dataclass
 class TenantEngineState:
     tenant: str
@@ -190,7 +194,7 @@ class ApiDemux:
         if not chans:
             if self.local is not None:
                 return self.local
-            raise SiteWhereException(f"no live replica of {self.identifier}")
+            raise NoLiveReplicaException(f"no live replica of {self.identifier}")
         n = len(chans)
         start = next(self._rr)
         for i in range(n):

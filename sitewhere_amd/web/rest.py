@@ -116,7 +116,7 @@ class Ctx:
 class WebRest:
     def __init__(self, instance, topology=None):
         self.instance = instance
-        self.channel = instance.local_channel
+        self.channel = instance.router
         self.tokens = instance.tokens
         self.topology = topology
 

@@ -98,7 +98,7 @@ def test_presence_parity():
     assert sorted(rg.out["assignment"].tolist()) == sorted(rc.out["assignment"].tolist())
 
 
-@pytest.mark.parametrize("mode", ["direct", "push", "sdma"])
+@pytest.mark.parametrize("mode", ["direct", "push", "sdma", "hsa"])
 def test_pipelined_runner_matches_sync(mode):
     g, c = pair()
     seen = []

@@ -183,3 +183,23 @@ def test_topology_websocket(env):
     with client.websocket_connect("/sitewhere/ws/topology") as ws:
         msg = ws.receive_json()
         assert msg["type"] == "topology" and "device-management" in msg["topology"]
+
+
+def test_python_client_sdk(env):
+    from sitewhere_amd.client import SiteWhereClient, SiteWhereClientError
+    _, client, _ = env
+    c = SiteWhereClient("http://testserver", transport=client)
+    assert c.get_version()["edition"] == "MI355X"
+    c.create_device({"token": "sdk-dev", "deviceTypeToken": "meitrack"})
+    a = c.create_device_assignment({"token": "sdk-asg", "deviceToken": "sdk-dev", "customerToken": "acme"})
+    assert a["token"] == "sdk-asg"
+    c.add_measurement("sdk-asg", "speed", 42.0)
+    c.add_location("sdk-asg", 33.1, -84.1)
+    assert c.list_measurements("sdk-asg")["results"][0]["value"] == 42.0
+    assert c.get_device_label("sdk-dev").startswith(b"\x89PNG")
+    with pytest.raises(SiteWhereClientError) as ei:
+        c.get_device("does-not-exist")
+    assert ei.value.status == 404
+    bad = SiteWhereClient("http://testserver", password="wrong", transport=client)
+    with pytest.raises(SiteWhereClientError):
+        bad.list_devices()
