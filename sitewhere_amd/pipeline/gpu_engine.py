@@ -511,13 +511,18 @@ class PipelinedRunner:
                 rc = self.e.lib.sw_sdma_copy(ctypes.c_void_p(self.e.out_host[pb].host),
                                              ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
                                              self.sdma_engine, ctypes.byref(h))
-                if rc:
-                    raise RuntimeError(f"sw_sdma_copy failed ({rc})")
-                sig = h.value
-            self.copying = (pb, n_out, sig)
-            if sig is None:
-                self._finish_copy()
-            return
+                if rc == 0:
+                    sig = h.value
+                else:
+                    # copy engine unavailable on this node: degrade to the HIP runtime path (loudly)
+                    import warnings
+                    warnings.warn(f"sw_sdma_copy failed ({rc}); falling back to hipMemcpyAsync outbound")
+                    self.mode = "sdma"
+            if self.mode == "hsa":
+                self.copying = (pb, n_out, sig)
+                if sig is None:
+                    self._finish_copy()
+                return
         if self.deliver and n_out:
             rc = self.e.lib.sw_copy_d2h(ctypes.c_void_p(self.e.out_host[pb].host),
                                         ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
