@@ -29,6 +29,47 @@ from .._native import native
 _FRAME = struct.Struct("<qqII")
 
 
+def murmur2(data: bytes) -> int:
+    """Kafka's murmur2 (``Utils.murmur2``, seed 0x9747b28c) -- same values as the native sw_murmur2."""
+    m, r = 0x5BD1E995, 24
+    length = len(data)
+    h = (0x9747B28C ^ length) & 0xFFFFFFFF
+    n4 = length & ~3
+    for i in range(0, n4, 4):
+        k = data[i] | (data[i + 1] << 8) | (data[i + 2] << 16) | (data[i + 3] << 24)
+        k = (k * m) & 0xFFFFFFFF
+        k ^= k >> r
+        k = (k * m) & 0xFFFFFFFF
+        h = (h * m) & 0xFFFFFFFF
+        h ^= k
+    rem = length & 3
+    if rem == 3:
+        h ^= data[n4 + 2] << 16
+    if rem >= 2:
+        h ^= data[n4 + 1] << 8
+    if rem >= 1:
+        h ^= data[n4]
+        h = (h * m) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * m) & 0xFFFFFFFF
+    h ^= h >> 15
+    return h
+
+
+_PART_CACHE: dict = {}
+
+
+def kafka_partition(key: bytes, n: int) -> int:
+    """``toPositive(murmur2(key)) % n`` with a bounded memo (device tokens repeat)."""
+    ck = (key, n)
+    p = _PART_CACHE.get(ck)
+    if p is None:
+        if len(_PART_CACHE) > 200_000:
+            _PART_CACHE.clear()
+        p = _PART_CACHE[ck] = (murmur2(key) & 0x7FFFFFFF) % n
+    return p
+
+
 @dataclass
 class Record:
     topic: str
@@ -60,6 +101,8 @@ class EventBus:
         self._lock = threading.RLock()
         self._cond = threading.Condition(self._lock)
         self._groups: dict[str, _Group] = {}
+        self._nparts: dict[str, int] = {}
+        self._waiters: dict[str, set] = {}       # topic -> Events of consumers subscribed to it
         self._closed = False
 
     # ------------------------------------------------------------------ topics
@@ -72,7 +115,10 @@ class EventBus:
             return t
 
     def partitions(self, name: str) -> int:
-        return self.lib.swlog_partitions(self.h, self.topic(name))
+        n = self._nparts.get(name)
+        if n is None:
+            n = self._nparts[name] = self.lib.swlog_partitions(self.h, self.topic(name))
+        return n
 
     def topics(self) -> list[str]:
         with self._lock:
@@ -88,8 +134,7 @@ class EventBus:
         n = self.partitions(name)
         if key is None:
             return next(self._rr) % n
-        kb = (ctypes.c_char * len(key)).from_buffer_copy(key) if key else None
-        return self.lib.sw_partition_for_key(ctypes.cast(kb, ctypes.c_void_p) if kb else None, len(key), n)
+        return kafka_partition(bytes(key), n)
 
     _rr = itertools.count()
 
@@ -98,6 +143,15 @@ class EventBus:
         if not records:
             return -1
         t = self.topic(name)
+        if len(records) == 1:
+            k, v = records[0]
+            k = k or b""
+            first = self.lib.swlog_append(self.h, t, partition, k, len(k), v, len(v),
+                                          ts if ts is not None else int(time.time() * 1000))
+            if first < 0:
+                raise RuntimeError(f"append to {name}[{partition}] failed")
+            self._wake(name)
+            return first
         keys = [k or b"" for k, _ in records]
         vals = [v for _, v in records]
         koff = np.zeros(len(records) + 1, np.int64)
@@ -111,8 +165,7 @@ class EventBus:
                                             voff.ctypes.data, tsa.ctypes.data, len(records))
         if first < 0:
             raise RuntimeError(f"append to {name}[{partition}] failed")
-        with self._cond:
-            self._cond.notify_all()
+        self._wake(name)
         return first
 
     # ------------------------------------------------------------------ fetch
@@ -139,6 +192,30 @@ class EventBus:
     def wait(self, timeout_s: float):
         with self._cond:
             self._cond.wait(timeout_s)
+
+    # Targeted wake-ups: an append wakes only consumers subscribed to that topic (a global
+    # notify_all per record woke every poller in the process -- a GIL storm under load).
+    def _wake(self, name: str):
+        for ev in list(self._waiters.get(name, ())):
+            ev.set()
+
+    def subscribe_event(self, topics, ev: threading.Event):
+        with self._lock:
+            for t in topics:
+                self._waiters.setdefault(t, set()).add(ev)
+
+    def unsubscribe_event(self, topics, ev: threading.Event):
+        with self._lock:
+            for t in topics:
+                self._waiters.get(t, set()).discard(ev)
+
+    def wait_topics(self, topics, timeout_s: float) -> bool:
+        ev = threading.Event()
+        self.subscribe_event(topics, ev)
+        try:
+            return ev.wait(timeout_s)
+        finally:
+            self.unsubscribe_event(topics, ev)
 
     # ------------------------------------------------------------------ offsets
     def commit(self, group: str, name: str, partition: int, offset: int):
@@ -197,6 +274,9 @@ class EventBus:
                 g.assignment[m].extend((t, q) for q in range(p, p + cnt))
                 p += cnt
         self._cond.notify_all()
+        for evs in self._waiters.values():
+            for ev in evs:
+                ev.set()
 
     def assignment(self, group: str, member_id: str) -> tuple[int, list]:
         with self._lock:
@@ -260,6 +340,10 @@ class Consumer:
             bus.topic(t)
         self.member_id = member_id or f"{group}-{uuid.uuid4().hex[:8]}"
         self.reset = auto_offset_reset
+        self._ev = threading.Event()
+        self._local = hasattr(bus, "subscribe_event")
+        if self._local:
+            bus.subscribe_event(self.topics, self._ev)
         self.generation = bus.join(group, self.member_id, self.topics)
         self.positions: dict[tuple[str, int], int] = {}
         self._assigned: list = []
@@ -288,6 +372,7 @@ class Consumer:
     def poll(self, timeout_ms: int = 1000, max_records: int = 500) -> dict[tuple[str, int], list[Record]]:
         deadline = time.time() + timeout_ms / 1000.0
         while True:
+            self._ev.clear()
             gen = self.bus.heartbeat(self.group, self.member_id)
             if gen < 0:
                 self.generation = self.bus.join(self.group, self.member_id, self.topics)
@@ -306,7 +391,11 @@ class Consumer:
                     budget -= len(recs)
             if out or time.time() >= deadline:
                 return out
-            self.bus.wait(min(0.05, max(0.0, deadline - time.time())))
+            left = max(0.0, deadline - time.time())
+            if self._local:
+                self._ev.wait(min(1.0, left))
+            else:
+                self.bus.wait_topics(self.topics, min(1.0, left))
 
     def commit(self, offsets: dict[tuple[str, int], int] | None = None):
         """Commit positions (next offset to read); default: current positions of all partitions."""
@@ -324,4 +413,6 @@ class Consumer:
     def close(self):
         if not self.closed:
             self.closed = True
+            if self._local:
+                self.bus.unsubscribe_event(self.topics, self._ev)
             self.bus.leave(self.group, self.member_id)

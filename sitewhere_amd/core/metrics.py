@@ -54,10 +54,13 @@ class Meter:
             self._last_tick += 5.0
 
     def mark(self, n: int = 1):
-        with self._lock:
-            self._tick_if_needed()
-            self._count += n
-            self._uncounted += n
+        # no lock on the hot path: += on ints is effectively atomic for these counters under the GIL
+        # (a lost update can only skew a rate estimate); ticking takes the lock
+        self._count += n
+        self._uncounted += n
+        if time.time() - self._last_tick >= 5.0:
+            with self._lock:
+                self._tick_if_needed()
 
     @property
     def count(self):

@@ -7,6 +7,7 @@ Field parity with ``sitewhere-core-api/.../spi/**`` and ``rest/model/**`` (e.g. 
 from __future__ import annotations
 
 import dataclasses
+import functools
 import enum
 import re
 import time
@@ -17,12 +18,25 @@ from typing import Any, get_type_hints
 _camel_re = re.compile(r"_([a-z0-9])")
 
 
+@functools.lru_cache(maxsize=4096)
 def camel(s: str) -> str:
     return _camel_re.sub(lambda m: m.group(1).upper(), s)
 
 
+@functools.lru_cache(maxsize=4096)
 def snake(s: str) -> str:
     return re.sub(r"(?<!^)(?=[A-Z])", "_", s).lower()
+
+
+_field_cache: dict = {}
+
+
+def _fields(cls):
+    """(name, camelName) per dataclass field, computed once per class."""
+    f = _field_cache.get(cls)
+    if f is None:
+        f = _field_cache[cls] = tuple((x.name, camel(x.name)) for x in dataclasses.fields(cls))
+    return f
 
 
 def now_ms() -> int:
@@ -37,11 +51,7 @@ class Model:
     """Mixin: camelCase dict (de)serialization for dataclasses."""
 
     def to_dict(self) -> dict:
-        out = {}
-        for f in dataclasses.fields(self):
-            v = getattr(self, f.name)
-            out[camel(f.name)] = _ser(v)
-        return out
+        return {c: _ser(getattr(self, n)) for n, c in _fields(type(self))}
 
     @classmethod
     def from_dict(cls, d: dict | None):
@@ -49,7 +59,7 @@ class Model:
             return None
         hints = _hints(cls)
         kw = {}
-        names = {f.name for f in dataclasses.fields(cls)}
+        names = _names(cls)
         for k, v in d.items():
             n = snake(k) if k not in names else k
             if n in names:
@@ -61,6 +71,14 @@ class Model:
 
 
 _hint_cache: dict = {}
+_names_cache: dict = {}
+
+
+def _names(cls) -> frozenset:
+    n = _names_cache.get(cls)
+    if n is None:
+        n = _names_cache[cls] = frozenset(x.name for x in dataclasses.fields(cls))
+    return n
 
 
 def _hints(cls):

@@ -97,6 +97,9 @@ class _BusFacade:
     def wait(self, timeout_s):
         self.b.wait(min(float(timeout_s), 1.0))
 
+    def wait_topics(self, topics, timeout_s):
+        return self.b.wait_topics(topics, min(float(timeout_s), 1.0))
+
     def commit(self, group, name, p, offset):
         self.b.commit(group, name, p, offset)
 
@@ -359,6 +362,9 @@ class RemoteEventBus:
 
     def wait(self, timeout_s):
         self.r.call("wait", timeout_s)
+
+    def wait_topics(self, topics, timeout_s):
+        return self.r.call("wait_topics", list(topics), timeout_s)
 
     def commit(self, group, name, p, offset):
         self.r.call("commit", group, name, p, offset)

@@ -111,14 +111,14 @@ class NearCache:
         self.hits = self.misses = 0
 
     def get(self, key, loader=None):
-        now = time.time()
-        with self._lock:
-            v = self._d.get(key)
-            if v is not None and now - v[1] < self.ttl:
-                self._d.move_to_end(key)
-                self.hits += 1
-                return v[0]
-            self.misses += 1
+        # Lock-free hit path (dict reads are atomic under the GIL); recency is refreshed on put, so
+        # eviction is insertion-ordered with TTL -- taking a lock per hit serialised every consumer
+        # thread on this cache.
+        v = self._d.get(key)
+        if v is not None and time.time() - v[1] < self.ttl:
+            self.hits += 1
+            return v[0]
+        self.misses += 1
         if loader is None:
             return None
         val = loader(key)
