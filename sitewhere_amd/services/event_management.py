@@ -65,9 +65,27 @@ class DeviceEventManagement:
         return events
 
     def _add(self, assignment_id: str, requests, build) -> list:
+        """Idempotent by alternate id: a redelivered request whose alternate id is already stored
+        returns the stored event instead of persisting a second copy (at-least-once delivery +
+        alternate-id dedup = exactly-once storage)."""
         a = self._context(assignment_id)
         reqs = requests if isinstance(requests, list) else [requests]
-        return self._persist([self._stamp(build(r), a, r) for r in reqs])
+        out, new, seen = [], [], {}
+        for r in reqs:
+            alt = r.get("alternateId")
+            if alt:
+                ex = seen.get(alt) or self.store.get_event_by_alternate_id(alt)
+                if ex is not None:
+                    out.append(ex)
+                    continue
+            e = self._stamp(build(r), a, r)
+            if alt:
+                seen[alt] = e
+            new.append(e)
+            out.append(e)
+        if new:
+            self._persist(new)
+        return out
 
     # ---- adds ------------------------------------------------------------------
     def add_measurements(self, assignment_id: str, *requests):
