@@ -6,7 +6,8 @@ Reference ``service-event-sources/.../sources/*``:
   * ``websocket/*`` -- WebSocket client/server receivers (string / binary)
   * ``coap/*`` -- CoAP server
   * ``rest/PollingRestInboundEventReceiver.java`` -- periodic HTTP poll
-  * ``activemq/*``, ``rabbitmq/*``, ``azure/*`` -- broker clients (need client libraries; gated)
+  * ``activemq/*`` -- STOMP client receiver (:mod:`.stomp`); ``rabbitmq/*`` -- AMQP 0-9-1 (:mod:`.amqp`);
+    ``azure/*`` -- gated (AMQP 1.0 not implemented)
 All receivers hand raw bytes to ``source.on_encoded_event_received(receiver, payload, metadata)``.
 """
 from __future__ import annotations
@@ -335,10 +336,10 @@ class PollingRestReceiver(Receiver):
 
 
 class GatedReceiver(Receiver):
-    """Broker receivers whose client libraries are not in this image (ActiveMQ/JMS, RabbitMQ/AMQP,
-    Azure EventHub).  They fail loudly at initialize, naming the missing module."""
+    """Azure Event Hubs consumption needs AMQP 1.0 (not implemented here; Event Hubs' REST API is
+    send-only).  Fails loudly at initialize, naming the missing module."""
 
-    MODULES = {"activemq": "stomp", "rabbitmq": "pika", "eventhub": "azure.eventhub", "amqp": "pika"}
+    MODULES = {"eventhub": "azure.eventhub"}
 
     def __init__(self, kind: str, cfg: dict):
         super().__init__(f"{kind}-receiver")
@@ -367,6 +368,16 @@ def build_receiver(rc: dict) -> Receiver:
         return CoapReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 0)))
     if t == "rest-poll":
         return PollingRestReceiver(rc["url"], float(rc.get("interval", 10.0)), rc.get("headers"))
+    if t in ("activemq", "stomp"):
+        from .stomp import StompReceiver
+        return StompReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 61613)),
+                             rc.get("destination", "/queue/SITEWHERE.IN"), rc.get("login"), rc.get("passcode"),
+                             int(rc.get("numThreads", 2)))
+    if t in ("rabbitmq", "amqp"):
+        from .amqp import RabbitMqReceiver
+        return RabbitMqReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 5672)), rc.get("queue", "sitewhere.input"),
+                                rc.get("username", "guest"), rc.get("password", "guest"), rc.get("vhost", "/"),
+                                bool(rc.get("durable", False)))
     if t in GatedReceiver.MODULES:
         return GatedReceiver(t, rc)
     raise ValueError(f"unknown receiver type {t!r}")

@@ -154,22 +154,6 @@ class ScriptConnector(OutboundConnector):
         self.tenant_engine.ms.scripts.call(self.source, "process", ev.to_dict(), ctx, name=f"connector-{self.cid}")
 
 
-class GatedConnector(OutboundConnector):
-    MODULES = {"sqs": "boto3", "eventhub": "azure.eventhub", "rabbitmq": "pika"}
-
-    def __init__(self, kind, cid, cfg, filters=None):
-        super().__init__(cid, filters)
-        self.kind = kind
-
-    def initialize(self, monitor):
-        import importlib
-        try:
-            importlib.import_module(self.MODULES[self.kind])
-        except ImportError as e:
-            raise SiteWhereException(f"{self.kind} connector needs python module {self.MODULES[self.kind]!r}") from e
-        raise SiteWhereException(f"{self.kind} connector: client wiring not configured")
-
-
 def build_filters(engine, cfgs) -> list:
     out = []
     for f in cfgs or []:
@@ -216,16 +200,18 @@ def build_connector(engine, cfg) -> OutboundConnector:
     if t == "mqtt":
         return MqttConnector(cid, cfg.get("host", "127.0.0.1"), int(cfg.get("port", 1883)),
                              cfg.get("topic", "SiteWhere/{tenant}/outbound/{deviceToken}"), int(cfg.get("qos", 0)), filters)
-    if t in ("http", "dweet", "initialstate"):
+    if t == "http":
         return HttpConnector(cid, cfg["url"], cfg.get("headers"), cfg.get("batch", True), filters)
+    from .cloud_connectors import build_cloud_connector
+    cloud = build_cloud_connector(t, cid, cfg, filters)
+    if cloud is not None:
+        return cloud
     if t == "solr":
         return SolrConnector(cid, cfg["url"], cfg.get("collection", "SiteWhere"), filters)
     if t == "file":
         return FileArchiveConnector(cid, cfg["path"], filters)
     if t == "script":
         return ScriptConnector(cid, cfg["script"], filters)
-    if t in GatedConnector.MODULES:
-        return GatedConnector(t, cid, cfg, filters)
     raise ValueError(f"unknown connector {t!r}")
 
 
