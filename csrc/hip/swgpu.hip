@@ -653,43 +653,103 @@ __device__ __forceinline__ int zone_lds_load(const SwEngineArgs& a, ZoneLds& L, 
 
 // Pass 1: per persisted row, the bitmask of zone tests that fire (row-major, test-ascending order is
 // the alert order, identical to the CPU oracle); per-tile alert counts.
+//
+// Block-cooperative so the expensive FP64 point-in-polygon work runs on dense lanes: a thread per
+// row would leave ~3/4 of every wave idle (only ~25 % of rows are locations) and run each PIP for
+// the whole wave whenever one lane's point falls in a zone's bbox.  Instead the block
+//   1. compacts its tile's location rows into LDS (block scan),
+//   2. expands (location, test) pairs in rounds, keeping the bbox hits as a dense candidate list,
+//   3. runs one candidate PIP per lane and ORs "inside" bits into the row's LDS mask,
+//   4. fires = inside ^ outside-condition mask (location rows only), writes zmask + the tile count.
+#define ZM_ROUND (BLK * 8)
+struct ZoneMaskLds {
+  double x[TILE], y[TILE];
+  ull inside[TILE];
+  uint16_t loc_j[TILE];
+  uint32_t cand[ZM_ROUND];
+  uint32_t ncand, count;
+  uint32_t scan[WAVES + 1];
+};
+
 __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restrict__ zmask, uint32_t* __restrict__ ztile) {
   __shared__ ZoneLds L;
-  __shared__ uint32_t c;
+  __shared__ ZoneMaskLds M;
   bool vtx_lds;
   const int nt = zone_lds_load(a, L, &vtx_lds);
   const double* V = vtx_lds ? L.v : a.zone_vtx;
-  if (threadIdx.x == 0) c = 0;
-  __syncthreads();
+  ull outside_mask = 0;
+  for (int t = 0; t < nt; ++t) outside_mask |= (L.t[t].y != 0) ? (1ull << t) : 0ull;
   const int64_t c0 = *a.step_cursor0;
   const uint32_t n = (uint32_t)(*a.store_cursor - c0);
   const int64_t base = (int64_t)blockIdx.x * TILE;
-  uint32_t cnt = 0;
+  if (base >= n) {                       // tile past this step's rows
+    if (threadIdx.x == 0) ztile[blockIdx.x] = 0;
+    return;
+  }
+  // 1. compact location rows (stable) into LDS
+  bool isloc[TILE_ITEMS];
+  uint32_t myloc = 0;
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
-    ull fired = 0;
+    isloc[k] = false;
     if (j < n) {
       const int64_t row = (c0 + j) % a.store_cap;
-      if (a.s_etype[row] == SW_EV_LOCATION) {
-        const double x = a.s_v0[row], y = a.s_v1[row];
-        for (int t = 0; t < nt; ++t) {
-          const double* bb = L.bb + 4 * t;
-          bool inside = x >= bb[0] && y >= bb[1] && x <= bb[2] && y <= bb[3];
-          if (inside) inside = pip(V + 2 * L.zo[t].x, L.zo[t].y - L.zo[t].x, x, y);
-          if ((L.t[t].y == 0) == inside) fired |= 1ull << t;
-        }
-      }
-      zmask[j] = fired;
+      isloc[k] = a.s_etype[row] == SW_EV_LOCATION;
     }
-    cnt += __popcll(fired);
+    myloc += isloc[k];
   }
-  // block reduce of the tile's alert count
+  uint32_t nloc;
+  uint32_t pos = block_excl_scan(myloc, &nloc, M.scan);
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
-  if (lane_id() == 0 && cnt) atomicAdd(&c, cnt);
+  for (int k = 0; k < TILE_ITEMS; ++k) {
+    if (isloc[k]) {
+      const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
+      const int64_t row = (c0 + j) % a.store_cap;
+      M.x[pos] = a.s_v0[row];
+      M.y[pos] = a.s_v1[row];
+      M.loc_j[pos] = (uint16_t)(k * BLK + threadIdx.x);
+      M.inside[pos] = 0;
+      ++pos;
+    }
+  }
+  if (threadIdx.x == 0) M.count = 0;
   __syncthreads();
-  if (threadIdx.x == 0) ztile[blockIdx.x] = c;
+  // 2 + 3. rounds of (location, test) bbox expansion -> dense PIP candidates
+  const uint32_t npairs = nloc * (uint32_t)nt;
+  for (uint32_t r0 = 0; r0 < npairs; r0 += ZM_ROUND) {
+    if (threadIdx.x == 0) M.ncand = 0;
+    __syncthreads();
+    for (uint32_t p = r0 + threadIdx.x; p < r0 + ZM_ROUND && p < npairs; p += BLK) {
+      const uint32_t li = p / (uint32_t)nt, t = p - li * (uint32_t)nt;
+      const double* bb = L.bb + 4 * t;
+      const double x = M.x[li], y = M.y[li];
+      if (x >= bb[0] && y >= bb[1] && x <= bb[2] && y <= bb[3]) M.cand[atomicAdd(&M.ncand, 1u)] = p;
+    }
+    __syncthreads();
+    const uint32_t nc = M.ncand;
+    for (uint32_t c = threadIdx.x; c < nc; c += BLK) {
+      const uint32_t p = M.cand[c];
+      const uint32_t li = p / (uint32_t)nt, t = p - li * (uint32_t)nt;
+      if (pip(V + 2 * L.zo[t].x, L.zo[t].y - L.zo[t].x, M.x[li], M.y[li])) atomicOr(&M.inside[li], 1ull << t);
+    }
+    __syncthreads();
+  }
+  // 4. fired masks for every row of the tile (0 for non-locations), tile alert count
+  for (uint32_t i = threadIdx.x; i < nloc; i += BLK) {
+    const ull fired = M.inside[i] ^ outside_mask;
+    M.inside[i] = fired;
+    if (fired) atomicAdd(&M.count, (uint32_t)__popcll(fired));
+  }
+  __syncthreads();
+  // scatter: default 0, then the location rows' masks
+#pragma unroll
+  for (int k = 0; k < TILE_ITEMS; ++k) {
+    const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
+    if (j < n && !isloc[k]) zmask[j] = 0ull;
+  }
+  for (uint32_t i = threadIdx.x; i < nloc; i += BLK) zmask[base + M.loc_j[i]] = M.inside[i];
+  if (threadIdx.x == 0) ztile[blockIdx.x] = M.count;
 }
 
 // Pass 2: write the alerts at their scanned offsets (stable, no global atomics).
