@@ -203,3 +203,24 @@ def test_python_client_sdk(env):
     bad = SiteWhereClient("http://testserver", password="wrong", transport=client)
     with pytest.raises(SiteWhereClientError):
         bad.list_devices()
+
+
+def test_rest_surface_matches_reference_controllers(env):
+    """25 reference controllers / 193 endpoint methods (SURVEY §2.3 Web/REST)."""
+    sw, _, _ = env
+    spec = sw.rest_app.openapi()
+    paths = {p for p in spec["paths"] if p.startswith("/sitewhere/api")}
+    n = sum(len([m for m in ops if m in ("get", "post", "put", "delete")]) for p, ops in spec["paths"].items()
+            if p in paths)
+    assert n >= 193
+    controllers = ["areatypes", "areas", "assettypes", "assets", "assignments", "authorities", "batch", "invocations",
+                   "customertypes", "customers", "commands", "events", "devicegroups", "devicestates", "statuses",
+                   "devicetypes", "devices", "search", "instance", "jobs", "schedules", "system", "tenants", "users",
+                   "zones"]
+    assert len(controllers) == 25
+    for c in controllers:
+        assert any(p == f"/sitewhere/api/{c}" or p.startswith(f"/sitewhere/api/{c}/") for p in paths), c
+    for must in ("/sitewhere/api/assignments/{token}/measurements/series", "/sitewhere/api/devicetypes/{token}/spec.proto",
+                 "/sitewhere/api/instance/microservice/{ident}/tenants/{tenantToken}/scripting/scripts/{scriptId}/versions/{versionId}/activate",
+                 "/sitewhere/api/batch/command/criteria", "/sitewhere/api/search/{providerId}/raw"):
+        assert must in paths, must
