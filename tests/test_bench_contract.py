@@ -1,0 +1,50 @@
+"""bench.py contract (driver-facing): one JSON line from rank 0 with the required keys, for N=1 and for
+N=2 ranks under torch.distributed.run (gloo + the CPU oracle engine, so it runs without a GPU)."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+SMALL = ["--engine", "cpu", "--msgs", "1500", "--devices", "1500", "--steps", "2", "--warmup", "1", "--store", "65536",
+         "--batches", "2"]
+
+
+def _json_lines(out: str):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_single_rank_json():
+    r = subprocess.run([sys.executable, "bench.py", *SMALL], cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert KEYS <= set(d) and d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["metric"] == "device_events_per_sec" and d["value"] > 0 and d["higher_is_better"] is True
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_torchrun():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *SMALL],
+                       cwd=REPO, capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 3000 and d["config"]["parallelism"].startswith("dp2")
+    assert d["detail"]["payloads"] == 2 * 2 * 1500
