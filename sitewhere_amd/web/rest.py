@@ -343,6 +343,17 @@ def create_app(instance, topology=None) -> FastAPI:
     app.include_router(misc_router(web))
     app.include_router(admin_router(web))
 
+    @app.get("/metrics")
+    def metrics():
+        """Prometheus text exposition of every co-located microservice's registry (the reference only
+        logs Dropwizard metrics every 20 s, ``Microservice.java:242-250``)."""
+        text = []
+        for ms in list(web.instance.microservices.values()):
+            body = ms.metrics.prometheus(prefix=f"sitewhere_{ms.identifier.replace('-', '_')}_")
+            if body:
+                text.append(body)
+        return Response("\n".join(text) + "\n", media_type="text/plain; version=0.0.4")
+
     @app.websocket("/sitewhere/ws/topology")
     async def topology_ws(ws: WebSocket):
         await ws.accept()

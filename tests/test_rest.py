@@ -224,3 +224,12 @@ def test_rest_surface_matches_reference_controllers(env):
                  "/sitewhere/api/instance/microservice/{ident}/tenants/{tenantToken}/scripting/scripts/{scriptId}/versions/{versionId}/activate",
                  "/sitewhere/api/batch/command/criteria", "/sitewhere/api/search/{providerId}/raw"):
         assert must in paths, must
+
+
+def test_prometheus_metrics_endpoint(env):
+    sw, client, h = env
+    client.post(f"{API}/assignments/{client.get(f'{API}/devices/meitrack-000/assignment', headers=h).json()['token']}"
+                "/measurements", headers=h, json={"name": "m", "value": 1.0})
+    text = client.get("/metrics").text
+    assert "sitewhere_event_sources_" in text or "sitewhere_inbound_processing_" in text
+    assert "# TYPE" in text
