@@ -1,0 +1,114 @@
+"""Configuration models (role / element trees) for every microservice.
+
+Reference: each service's ``*ModelProvider`` + ``*Roles`` + ``*RoleKeys`` under
+``sitewhere-configuration/.../configuration/model`` (``ConfigurationModelProvider.java:37-280``),
+returned by the management RPC ``GetConfigurationModel`` so an editor can render and validate the
+service's configuration.  Here the trees describe the JSON documents the services actually read
+(``services/*.py`` ``self.config.get(...)``) and ``ConfigurationModel.validate`` checks them.
+"""
+from __future__ import annotations
+
+from .config import AttributeNode as A
+from .config import ConfigurationModel, ElementNode as E
+
+DATASTORE = E("Datastore", "datastore", "Entity / event persistence backend", [
+    A("type", "String", "memory | sqlite | mongodb | bucketed | influx", True, "memory",
+      ["memory", "sqlite", "mongodb", "bucketed", "influx"]),
+    A("path", "String", "SQLite file (supports [[tenant.token]])"),
+    A("uri", "String", "MongoDB connection URI (${mongodb.uri:...})"),
+    A("database", "String", "database name"),
+    A("bucket_ms", "Integer", "time bucket for the Cassandra-layout event store", default=3600000)])
+
+DECODER = E("Decoder", "event-source-decoder", "Payload decoder", [
+    A("type", "String", "protobuf | json | json-batch | script | echo | composite", True, "json",
+      ["protobuf", "json", "json-batch", "script", "echo", "composite"]),
+    A("script", "Script", "decoder script id (type=script)")])
+RECEIVER = E("Receiver", "event-source-receiver", "Protocol receiver", [
+    A("type", "String", "mqtt | socket | websocket | coap | rest-poll | activemq | rabbitmq", True,
+      choices=["mqtt", "socket", "websocket", "coap", "rest-poll", "activemq", "rabbitmq"]),
+    A("host", "String", "broker / bind host", default="127.0.0.1"), A("port", "Integer", "port"),
+    A("topic", "String", "MQTT topic"), A("queue", "String", "AMQP queue"), A("destination", "String", "STOMP destination"),
+    A("qos", "Integer", "MQTT QoS", default=1), A("numThreads", "Integer", "processing threads", default=4)])
+SOURCE = E("Event Source", "event-source", "Decoder + deduplicator + receivers", [
+    A("id", "String", "source id", True), A("decoder", "String", "decoder type or element", True),
+    A("forward", "String", "'raw' forwards undecoded payload batches to the MI355X inbound engine"),
+    A("logPayloads", "Boolean", "log every payload", default=False)], [DECODER, RECEIVER])
+
+FILTER = E("Filter", "outbound-filter", "Event filter", [
+    A("type", "String", "area | device-type | event-type | script", True),
+    A("operation", "String", "include | exclude", default="include", choices=["include", "exclude"])])
+CONNECTOR = E("Connector", "outbound-connector", "Outbound connector", [
+    A("id", "String", "connector id", True),
+    A("type", "String", "log | mqtt | http | solr | file | script | sqs | eventhub | dweet | initialstate | rabbitmq",
+      True), A("numProcessingThreads", "Integer", "processing threads", default=0)], [FILTER])
+PROCESSOR = E("Rule Processor", "rule-processor", "Rule processor", [
+    A("id", "String", "processor id", True), A("type", "String", "zone-test | threshold | script", True),
+    A("numThreads", "Integer", "processing threads", default=0)], [
+    E("Zone Test", "zone-test", "Geofence test", [
+        A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside", True, "inside"),
+        A("alertType", "String", "alert type", True), A("alertLevel", "String", "Info | Warning | Error | Critical"),
+        A("alertMessage", "String", "alert message")])])
+DESTINATION = E("Command Destination", "command-destination", "Encoder + provider", [
+    A("id", "String", "destination id", True), A("encoder", "String", "json | protobuf | script", True, "json"),
+    A("provider", "String", "log | mqtt | coap | sms", True, "log"), A("host", "String", "MQTT host"),
+    A("port", "Integer", "MQTT port"), A("commandTopic", "String", "MQTT command topic template")])
+ROUTER = E("Command Router", "command-router", "Destination choice", [
+    A("type", "String", "single-choice | device-type-mapping | script | no-op", True, "single-choice"),
+    A("destination", "String", "destination id (single-choice)")])
+
+MODELS: dict[str, ConfigurationModel] = {}
+
+
+def _m(identifier: str, title: str, attrs: list, children: list | None = None):
+    MODELS[identifier] = ConfigurationModel(identifier, title, E(title, identifier, attributes=attrs,
+                                                                 children=children or []))
+
+
+_m("instance-management", "Instance Management", [A("instanceTemplate", "String", "instance template", True, "default")])
+_m("user-management", "User Management", [], [DATASTORE])
+_m("tenant-management", "Tenant Management", [], [DATASTORE])
+_m("web-rest", "Web/REST", [A("port", "Integer", "HTTP port", default=8080), A("cors", "Boolean", "CORS", default=True)])
+_m("event-sources", "Event Sources", [], [SOURCE, E("Deduplicator", "deduplicator", "alternate-id | script", [
+    A("type", "String", "alternate-id | script", True), A("script", "Script", "script id")])])
+_m("inbound-processing", "Inbound Processing", [
+    A("processingThreadCount", "Integer", "decoded-event processing threads", default=25),
+    A("engine", "String", "cpu (per-event path) | gpu (fused MI355X micro-batch engine)", default="cpu",
+      choices=["cpu", "gpu"]),
+    A("device", "String", "gpu engine placement: auto | gpu | cpu", default="auto", choices=["auto", "gpu", "cpu"]),
+    A("batchSize", "Integer", "micro-batch payloads (gpu engine)", default=65536),
+    A("maxDelayMs", "Integer", "micro-batch latency bound (gpu engine)", default=5)], [
+    E("Zone Tests", "gpu-zone-tests", "zone tests evaluated inside the GPU engine", [
+        A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")])])
+_m("event-management", "Event Management", [A("buffered", "Boolean", "bulk buffer (DeviceEventBuffer)", default=False)],
+   [DATASTORE])
+_m("device-management", "Device Management", [], [DATASTORE])
+_m("asset-management", "Asset Management", [], [DATASTORE])
+_m("batch-operations", "Batch Operations", [A("threads", "Integer", "operation threads", default=10),
+                                            A("throttleDelayMs", "Integer", "delay between elements", default=0)],
+   [DATASTORE])
+_m("schedule-management", "Schedule Management", [A("tickSeconds", "Decimal", "scheduler tick", default=1.0)], [DATASTORE])
+_m("device-state", "Device State", [], [DATASTORE, E("Presence", "presence", "DevicePresenceManager", [
+    A("checkInterval", "String", "ISO-8601 period", default="PT10M"),
+    A("missingInterval", "String", "ISO-8601 period", default="PT8H")])])
+_m("device-registration", "Device Registration", [
+    A("allowNewDevices", "Boolean", "auto-register unknown devices", default=True),
+    A("defaultDeviceTypeToken", "String", "device type for new devices"),
+    A("defaultCustomerToken", "String", "customer for new assignments"),
+    A("defaultAreaToken", "String", "area for new assignments"),
+    A("autoAssign", "Boolean", "create an assignment on registration", default=True)])
+_m("rule-processing", "Rule Processing", [], [PROCESSOR])
+_m("outbound-connectors", "Outbound Connectors", [], [CONNECTOR])
+_m("command-delivery", "Command Delivery", [A("processingThreads", "Integer", "delivery threads", default=5)],
+   [ROUTER, DESTINATION])
+_m("label-generation", "Label Generation", [], [E("Generator", "label-generator", "QR code generator", [
+    A("id", "String", "generator id", True), A("type", "String", "qrcode", True, "qrcode"),
+    A("ecLevel", "String", "L | M | Q | H", default="M"), A("scale", "Integer", "pixels per module", default=6),
+    A("baseUrl", "String", "encoded URL template")])])
+_m("streaming-media", "Streaming Media", [], [DATASTORE])
+_m("event-search", "Event Search", [], [E("Search Provider", "search-provider", "external search provider", [
+    A("id", "String", "provider id", True), A("type", "String", "solr", True), A("url", "String", "Solr base URL"),
+    A("collection", "String", "collection", default="SiteWhere")])])
+
+
+def model_for(identifier: str) -> ConfigurationModel | None:
+    return MODELS.get(identifier)

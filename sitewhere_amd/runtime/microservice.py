@@ -299,7 +299,8 @@ class Microservice(LifecycleComponent):
         return substitute(doc, self.instance.settings.extra)
 
     def configuration_model(self):
-        return None
+        from .config_models import model_for
+        return model_for(self.identifier)
 
     def tenant_config_path(self, tenant: str) -> str:
         return self.instance.tenant_conf_path(tenant, f"{self.identifier}.json")

@@ -21,7 +21,6 @@ from ..models.domain import (Area, AreaType, Customer, CustomerType, Device, Dev
                              DeviceGroup, DeviceGroupElement, DeviceStatus, DeviceStream, DeviceType, SearchResults,
                              Zone, now_ms)
 from ..persistence.store import EntityStore, create_store
-from ..runtime.config import simple_model
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
 from .common import Crud, apply_request, criteria_of
 
@@ -693,8 +692,6 @@ class DeviceManagementMicroservice(MultitenantMicroservice):
     def create_tenant_engine(self, tenant):
         return DeviceManagementTenantEngine(self, tenant)
 
-    def configuration_model(self):
-        return simple_model(self.identifier, "Device Management", [("datastore", "Datastore", "", True)])
 
 
 _ = apply_request, criteria_of

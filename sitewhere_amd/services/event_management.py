@@ -18,7 +18,6 @@ from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, D
                              DeviceMeasurement, DeviceStateChange, now_ms)
 from ..persistence.events import BufferedEventWriter, DeviceEventStore, create_event_store
 from ..rpc import codec
-from ..runtime.config import simple_model
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
 
 _BASE = ("alternateId", "eventDate", "metadata", "updateState")
@@ -226,8 +225,3 @@ class EventManagementMicroservice(MultitenantMicroservice):
 
     def create_tenant_engine(self, tenant):
         return EventManagementTenantEngine(self, tenant)
-
-    def configuration_model(self):
-        return simple_model(self.identifier, "Event Management",
-                            [("datastore", "Datastore", "memory | sqlite | bucketed (Cassandra layout)", True),
-                             ("buffered", "Boolean", "bulk buffer (DeviceEventBuffer)", False)])

@@ -24,7 +24,6 @@ from ..core.errors import EventDecodeException
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..models import wire
 from ..rpc import codec
-from ..runtime.config import simple_model
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
 
 RAW_PAYLOADS = "event-source-raw-payloads"
@@ -436,6 +435,3 @@ class EventSourcesMicroservice(MultitenantMicroservice):
 
     def create_tenant_engine(self, tenant):
         return EventSourcesTenantEngine(self, tenant)
-
-    def configuration_model(self):
-        return simple_model(self.identifier, "Event Sources", [("sources", "EventSourceList", "", True)])

@@ -14,7 +14,6 @@ from ..core.security import SiteWhereAuthority, hash_password, verify_password
 from ..models.domain import (AccountStatus, GrantedAuthority, SearchCriteria, SearchResults, User, now_ms,
                              stamp_created, stamp_updated)
 from ..persistence.store import EntityStore, create_store
-from ..runtime.config import simple_model
 from ..runtime.microservice import GlobalMicroservice
 
 AUTHORITY_DESCRIPTIONS = {
@@ -218,9 +217,6 @@ class UserManagementMicroservice(GlobalMicroservice):
 
     def default_configuration(self) -> dict:
         return {"datastore": {"type": "memory"}}
-
-    def configuration_model(self):
-        return simple_model(self.identifier, "User Management", [("datastore", "Datastore", "User datastore", True)])
 
     def register_services(self, resolver):
         from ..persistence.store import create_store as cs

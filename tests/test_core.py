@@ -331,3 +331,17 @@ def test_buffered_writer_and_influx_lines():
     iw.add_events([DeviceMeasurement(device_assignment_id="a", name="temp", value=1.5, event_date=7),
                    DeviceLocation(device_assignment_id="a", latitude=1.0, longitude=2.0, event_date=8)])
     assert posted and b"mx_temp=1.5" in posted[0][1] and b"latitude=1.0" in posted[0][1]
+
+
+def test_every_microservice_has_a_configuration_model():
+    from sitewhere_amd.assembly import SERVICES_BY_ID
+    from sitewhere_amd.runtime.config_models import model_for
+    from sitewhere_amd.services.tenant_management import TENANT_TEMPLATES
+    assert len(SERVICES_BY_ID) == 19
+    for ident in SERVICES_BY_ID:
+        m = model_for(ident)
+        assert m is not None and m.to_dict()["root"]["role"] == ident
+    # every tenant template document validates against its service's model
+    for tpl in TENANT_TEMPLATES.values():
+        for svc, doc in tpl["services"].items():
+            assert model_for(svc).validate(doc) == [], (svc, doc)
