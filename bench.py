@@ -61,17 +61,13 @@ def zone_polys(n, lat0, lon0, span, rng):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
 
+    from sitewhere_amd.parallel.sharding import init_distributed, shard_mask
+
     use_gpu = args.engine == "gpu"
-    if use_gpu:
-        torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl" if use_gpu else "gloo", device_id=torch.device("cuda", local) if use_gpu else None)
+    rank, local, world, _ = init_distributed(use_gpu)
     from sitewhere_amd.pipeline.config import EngineConfig
     from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads, gen_tokens, fingerprints
 
@@ -97,7 +93,7 @@ def main():
     t0 = time.time()
     heap, offs = gen_tokens("dev-", 0, n_total_dev)
     lo, hi = fingerprints(heap, offs)
-    mine = ((hi >> np.uint64(32)) % np.uint64(world)) == rank
+    mine = shard_mask(hi, world, rank)
     lo, hi = lo[mine], hi[mine]
     dev = eng.register_devices(lo, hi)
     n_dev = len(dev)

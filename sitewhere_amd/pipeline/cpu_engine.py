@@ -83,15 +83,14 @@ class CpuInboundEngine(EngineBase):
         if self.exchange is not None:          # loopback / custom transport
             return self.exchange(self, recs)
         import torch
-        import torch.distributed as dist
 
+        from ..parallel.sharding import exchange_slabs
         send, cnt = self.partition(recs)
         send_t = torch.from_numpy(send.view(np.uint8).reshape(-1).copy())
         recv_t = torch.empty_like(send_t)
         cnt_t = torch.from_numpy(cnt)
         rcnt_t = torch.empty_like(cnt_t)
-        dist.all_to_all_single(rcnt_t, cnt_t, group=self.group)
-        dist.all_to_all_single(recv_t, send_t, group=self.group)
+        exchange_slabs(cnt_t, rcnt_t, send_t, recv_t, self.group)
         recv = recv_t.numpy().view(EVENT_REC).reshape(self.world, self.cfg.shuf_cap)
         return self.unpack(recv, rcnt_t.numpy())
 

@@ -279,10 +279,8 @@ class GpuInboundEngine(EngineBase):
 
     def phase_exchange(self):
         """RCCL all-to-all re-keying of the per-owner slabs (the Kafka key-partitioning analogue)."""
-        import torch.distributed as dist
-
-        dist.all_to_all_single(self.t["recv_cnt"], self.t["send_cnt"], group=self.group)
-        dist.all_to_all_single(self.t["recv"], self.t["send"], group=self.group)
+        from ..parallel.sharding import exchange_slabs
+        exchange_slabs(self.t["send_cnt"], self.t["recv_cnt"], self.t["send"], self.t["recv"], self.group)
 
     def phase_process(self):
         ap = ctypes.byref(self.args)
