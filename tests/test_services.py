@@ -219,3 +219,49 @@ def test_gpu_tenant_engine_on_device():
         assert "rpm" in st["measurements"]
     finally:
         inst.stop()
+
+
+def test_streaming_media_chunks(sw):
+    sm = sw.api("StreamingMedia", "default")
+    dm = sw.api("DeviceManagement", "default")
+    dev = as_system(sw, lambda: dm.get_device_by_token("openhab-002"))
+    ack = as_system(sw, lambda: sm.handle_device_stream_request("openhab-002", {"streamId": "cam1",
+                                                                                 "contentType": "video/mp4"}))
+    assert ack["state"] == "STREAM_CREATED"
+    assert as_system(sw, lambda: sm.handle_device_stream_request("openhab-002", {"streamId": "cam1"}))["state"] == \
+        "STREAM_EXISTS"
+    for seq, chunk in ((2, b"world"), (1, b"hello ")):          # out of order
+        as_system(sw, lambda seq=seq, chunk=chunk: sm.add_device_stream_data(dev.device_assignment_id, "cam1", seq, chunk))
+    assert as_system(sw, lambda: sm.get_stream_content(dev.device_assignment_id, "cam1")) == b"hello world"
+    with pytest.raises(Exception):
+        as_system(sw, lambda: sm.add_device_stream_data(dev.device_assignment_id, "nope", 1, b"x"))
+
+
+def test_event_search_providers(sw):
+    es = sw.tenant_engine("event-sources")
+    dm = sw.api("DeviceManagement", "default")
+    aid = as_system(sw, lambda: dm.get_device_by_token("raspberrypi-002")).device_assignment_id
+    es.inject("default-protobuf", wire.measurements("raspberrypi-002", {"humidity": 55.0}))
+    search = sw.api("EventSearch", "default")
+    assert [p["id"] for p in as_system(sw, lambda: search.list_search_providers())] == ["events"]
+    hits = wait_until(lambda: as_system(sw, lambda: search.search("events", f"assignment:{aid} name:humidity")))
+    assert hits and hits[0]["value"] == 55.0
+    # Solr provider against a canned response (no Solr in the image)
+    from sitewhere_amd.services.labels_media_search import SolrSearchProvider
+    urls = []
+    p = SolrSearchProvider("solr", "http://solr:8983/solr", get=lambda u: (urls.append(u) or
+                           b'{"response": {"docs": [{"id": "e1"}]}}'))
+    assert p.search("eventType:Measurement", 10) == [{"id": "e1"}]
+    assert "q=eventType%3AMeasurement" in urls[0] and "rows=10" in urls[0]
+
+
+def test_global_configuration_update_restarts_engines(sw):
+    """Global config change -> every tenant engine of that service restarts (MultitenantMicroservice:381-409)."""
+    from sitewhere_amd.runtime.config import dump_document
+    ms = sw["asset-management"]
+    before = ms.get_tenant_engine("default")
+    sw.instance.coord.put(ms.config_path(), dump_document({"note": "changed"}))
+    assert wait_until(lambda: ms.get_tenant_engine("default") is not None and
+                      ms.get_tenant_engine("default") is not before and
+                      ms.get_tenant_engine("default").status.value == "Started", 20)
+    assert ms.config.get("note") == "changed"
