@@ -1,0 +1,78 @@
+"""Service-level MI355X path: events/s through a ``gpu-columnar`` tenant of a whole co-located instance.
+
+raw payload batches (the ``event-source-raw-payloads`` record format) -> inbound-processing GPU tenant
+engine (decode, validate, dedup, persist, state, zone rules on the MI355X) -> columnar batch ->
+event-management columnar store (RPC) + ``inbound-enriched-batches`` topic.  Devices and assignments
+are created through the device-management API and mirrored into the engine by the change feed.
+
+    python scripts/bench_tenant_path.py --devices 20000 --batch 65536 --batches 40
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--devices", type=int, default=20000)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--batches", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=3)
+    args = ap.parse_args()
+    import logging
+    logging.basicConfig(level=logging.ERROR)
+    import numpy as np
+
+    from sitewhere_amd.assembly import SiteWhereInstance
+    from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
+
+    sw = SiteWhereInstance().start()
+    sw.wait_for_tenant("default", 60)
+    tm = sw.api("TenantManagement")
+    sw.instance.system_user.run(lambda: tm.create_tenant({"token": "fast", "name": "fast",
+                                                          "configurationTemplateId": "gpu-columnar",
+                                                          "datasetTemplateId": "empty"}))
+    sw.wait_for_tenant("fast", 120)
+    run = lambda f: sw.instance.system_user.run(f, "fast")  # noqa: E731
+    dm = sw.api("DeviceManagement", "fast")
+    t0 = time.time()
+    run(lambda: dm.create_device_type({"token": "sensor", "name": "Sensor"}))
+    for i in range(args.devices):
+        tok = f"dev-{i:010d}"
+        run(lambda tok=tok: dm.create_device({"token": tok, "deviceTypeToken": "sensor"}))
+        run(lambda tok=tok: dm.create_device_assignment({"deviceToken": tok}))
+    ib = sw.tenant_engine("inbound-processing", "fast")
+    while ib.engine.n_assignments < args.devices and time.time() - t0 < 600:
+        time.sleep(0.1)
+    setup_s = time.time() - t0
+    spec = FleetSpec(prefix="dev-", n_devices=args.devices, p_location=0.25, p_alert=0.05, mx_per_msg=1)
+    now0 = int(time.time() * 1000)
+    batches = []
+    for b in range(4):
+        raw, offs = gen_payloads(spec, args.batch, now0 - 1000, seed=7 + b)
+        batches.append((np.concatenate([raw, np.zeros(64, np.uint8)]), offs))
+    for k in range(args.warmup):
+        ib.process_batch(*batches[k % 4])
+    base = ib.persisted_events.count
+    t = time.perf_counter()
+    ev = 0
+    for k in range(args.batches):
+        r = ib.process_batch(*batches[k % 4])
+        ev += r.n_events
+    dt = time.perf_counter() - t
+    em_store = sw.tenant_engine("event-management", "fast").store
+    print(json.dumps({"metric": "tenant_path_events_per_sec", "engine": ib.engine_kind, "events": ev,
+                      "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,
+                      "ms_per_batch": round(1000 * dt / args.batches, 3), "batch": args.batch,
+                      "devices": args.devices, "store_rows": em_store.rows, "setup_s": round(setup_s, 1)}))
+    sw.stop()
+
+
+if __name__ == "__main__":
+    main()

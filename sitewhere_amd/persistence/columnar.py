@@ -1,0 +1,179 @@
+"""Columnar event store for MI355X tenants: enriched GPU output rows kept as numpy columns.
+
+The fused inbound engine emits 32-byte ``OUT_REC`` rows (date, value(s), assignment index, interned
+name, type, level) with implicit event ids.  Turning each into a Python event object before storage
+caps a tenant at ~10^5 events/s on the host; this store appends the rows as columns (zero-copy
+``frombuffer`` of the batch payload) plus small dictionaries (assignment index -> assignment /
+device / customer / area / asset ids, name id -> name), and materialises domain objects only for
+the page a query returns.  It implements :class:`~sitewhere_amd.persistence.events.DeviceEventStore`
+(object events -- e.g. command invocations added over REST -- go to an embedded memory store and
+are merged into query results), so event management serves GPU tenants through the same 16 RPCs.
+
+Batch wire format (:func:`encode_batch` / :func:`decode_batch`, msgpack): ``{"boot", "first_seq",
+"world", "rank", "now", "rows": OUT_REC bytes, "asg": {idx: [assignment, device, customer, area,
+asset]}, "names": {name_id: name}, "rules": {alert_type: message}}``.
+"""
+from __future__ import annotations
+
+import threading
+
+import msgpack
+import numpy as np
+
+from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC
+from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceEventIndex,
+                             DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults)
+from .events import DeviceEventStore, MemoryEventStore
+
+_ETYPE = {DeviceEventType.Measurement: EV_MEASUREMENT, DeviceEventType.Location: EV_LOCATION,
+          DeviceEventType.Alert: EV_ALERT, DeviceEventType.StateChange: EV_STATE_CHANGE}
+_LEVELS = [AlertLevel.Info, AlertLevel.Warning, AlertLevel.Error, AlertLevel.Critical]
+_CTX = {DeviceEventIndex.Assignment: 0, DeviceEventIndex.Customer: 2, DeviceEventIndex.Area: 3,
+        DeviceEventIndex.Asset: 4}
+
+
+def encode_batch(boot: str, first_seq: int, world: int, rank: int, now: int, rows: np.ndarray, asg: dict,
+                 names: dict, rules: dict | None = None) -> bytes:
+    return msgpack.packb({"boot": boot, "first_seq": int(first_seq), "world": int(world), "rank": int(rank),
+                          "now": int(now), "rows": np.ascontiguousarray(rows).tobytes(),
+                          "asg": {int(k): list(v) for k, v in asg.items()},
+                          "names": {int(k): v for k, v in names.items()}, "rules": rules or {}}, use_bin_type=True)
+
+
+def decode_batch(payload: bytes) -> dict:
+    d = msgpack.unpackb(payload, raw=False, strict_map_key=False)
+    d["rows"] = np.frombuffer(d["rows"], OUT_REC)
+    return d
+
+
+class ColumnarEventStore(DeviceEventStore):
+    def __init__(self, consolidate_every: int = 64):
+        self._objects = MemoryEventStore()
+        self._chunks: list[dict] = []
+        self._pending: list[dict] = []
+        self._asg: dict[int, list] = {}         # assignment index -> [assignment, device, customer, area, asset]
+        self._names: dict[int, str] = {}
+        self._rules: dict[str, str] = {}
+        self._boots: list[str] = []
+        self._lock = threading.RLock()
+        self.consolidate_every = consolidate_every
+        self.rows = 0
+
+    # ------------------------------------------------------------------ ingest
+    def add_columnar(self, payload: bytes | dict) -> int:
+        d = decode_batch(payload) if isinstance(payload, (bytes, bytearray)) else payload
+        rows = d["rows"]
+        n = len(rows)
+        with self._lock:
+            self._asg.update({int(k): v for k, v in d["asg"].items()})
+            self._names.update({int(k): v for k, v in d["names"].items()})
+            self._rules.update(d.get("rules") or {})
+            if d["boot"] not in self._boots:
+                self._boots.append(d["boot"])
+            if n:
+                eid = (d["first_seq"] + np.arange(n, dtype=np.int64)) * d["world"] + d["rank"]
+                self._pending.append({"boot": np.full(n, self._boots.index(d["boot"]), np.int16), "eid": eid,
+                                      "rows": rows, "recv": np.full(n, d["now"], np.int64)})
+                self.rows += n
+                if len(self._pending) >= self.consolidate_every:
+                    self._consolidate()
+        return n
+
+    def _consolidate(self):
+        if not self._pending:
+            return
+        parts = self._pending
+        self._pending = []
+        self._chunks.append({"boot": np.concatenate([p["boot"] for p in parts]),
+                             "eid": np.concatenate([p["eid"] for p in parts]),
+                             "rows": np.concatenate([p["rows"] for p in parts]),
+                             "recv": np.concatenate([p["recv"] for p in parts])})
+
+    def _all_chunks(self) -> list[dict]:
+        with self._lock:
+            self._consolidate()
+            return list(self._chunks)
+
+    # ------------------------------------------------------------------ DeviceEventStore
+    def add_events(self, events):
+        return self._objects.add_events(events)
+
+    def count(self) -> int:
+        return self.rows + self._objects.count()
+
+    def get_event_by_alternate_id(self, alt: str):
+        return self._objects.get_event_by_alternate_id(alt)   # GPU rows carry only the alt-id hash
+
+    def get_event_by_id(self, id: str):
+        boot, sep, num = id.rpartition("-")
+        if sep and boot in self._boots and num.isdigit():
+            b, eid = self._boots.index(boot), int(num)
+            for c in self._all_chunks():
+                hit = np.nonzero((c["eid"] == eid) & (c["boot"] == b))[0]
+                if len(hit):
+                    return self._materialize(c, int(hit[0]))
+            return None
+        return self._objects.get_event_by_id(id)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        return self._objects.list_command_responses_for_invocation(invocation_id, criteria)
+
+    def list_events(self, event_type, index, entity_ids, criteria: DateRangeSearchCriteria | None = None):
+        c = criteria or DateRangeSearchCriteria(page_size=100)
+        et = _ETYPE.get(DeviceEventType(event_type))
+        objs = self._objects.list_events(event_type, index, entity_ids, DateRangeSearchCriteria(page_size=0,
+                                         start_date=c.start_date, end_date=c.end_date)).results
+        if et is None:
+            return SearchResults(len(objs), c.slice(objs))
+        pos = _CTX[DeviceEventIndex(index)]
+        want = set(entity_ids)
+        with self._lock:
+            asg_idx = np.array([i for i, ctx in self._asg.items() if ctx[pos] in want], np.int32)
+        hits = []                                   # (date, chunk, row)
+        for ci, ch in enumerate(self._all_chunks()):
+            r = ch["rows"]
+            m = (r["etype"] == et) & np.isin(r["assignment"], asg_idx)
+            if c.start_date is not None:
+                m &= r["event_date"] >= c.start_date
+            if c.end_date is not None:
+                m &= r["event_date"] <= c.end_date
+            idx = np.nonzero(m)[0]
+            if len(idx):
+                hits.append((r["event_date"][idx], np.full(len(idx), ci, np.int32), idx, ch["eid"][idx]))
+        total = sum(len(h[0]) for h in hits) + len(objs)
+        if not hits:
+            return SearchResults(total, c.slice(objs))
+        dates = np.concatenate([h[0] for h in hits])
+        cis = np.concatenate([h[1] for h in hits])
+        ris = np.concatenate([h[2] for h in hits])
+        eids = np.concatenate([h[3] for h in hits])
+        order = np.lexsort((-eids, -dates))         # newest first, then latest id
+        chunks = self._all_chunks()
+        if objs:
+            merged = [self._materialize(chunks[cis[o]], int(ris[o])) for o in order] + objs
+            merged.sort(key=lambda e: -(e.event_date or 0))
+            return SearchResults(total, c.slice(merged))
+        if c.page_size > 0:
+            start = (max(1, c.page_number) - 1) * c.page_size
+            order = order[start:start + c.page_size]
+        return SearchResults(total, [self._materialize(chunks[cis[o]], int(ris[o])) for o in order])
+
+    # ------------------------------------------------------------------ materialisation
+    def _materialize(self, ch: dict, i: int):
+        r = ch["rows"][i]
+        ctx = self._asg.get(int(r["assignment"]), [None] * 5)
+        base = dict(id=f"{self._boots[int(ch['boot'][i])]}-{int(ch['eid'][i])}", device_assignment_id=ctx[0],
+                    device_id=ctx[1], customer_id=ctx[2], area_id=ctx[3], asset_id=ctx[4],
+                    event_date=int(r["event_date"]), received_date=int(ch["recv"][i]))
+        et = int(r["etype"])
+        name = self._names.get(int(r["name_id"]), "") if int(r["name_id"]) != NO_NAME else ""
+        if et == EV_MEASUREMENT:
+            return DeviceMeasurement(name=name, value=float(r["v0"]), **base)
+        if et == EV_LOCATION:
+            return DeviceLocation(latitude=float(r["v0"]), longitude=float(r["v1"]), **base)
+        if et == EV_ALERT:
+            rule = self._rules.get(name)
+            return DeviceAlert(source=AlertSource.System if rule is not None else AlertSource.Device,
+                               level=_LEVELS[min(int(r["level"]), 3)], type=name, message=rule or "", **base)
+        return DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
+                                 new_state="NOT_PRESENT", **base)

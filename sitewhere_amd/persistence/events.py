@@ -9,7 +9,7 @@ Reference: ``service-event-management/.../persistence/**``:
 Here: :class:`MemoryEventStore` (indexed, bisect-sorted), :class:`SQLiteEventStore` (durable),
 :class:`BucketedEventStore` (the Cassandra time-bucket layout, in memory), :class:`InfluxLineWriter`
 (line protocol over HTTP, batched) and :class:`BufferedEventWriter` (the bulk buffer).  The GPU
-engine's HBM column store is queried through :mod:`sitewhere_amd.persistence.gpu_events`.
+engine's enriched rows are stored column-wise by :mod:`sitewhere_amd.persistence.columnar`.
 """
 from __future__ import annotations
 
@@ -362,4 +362,7 @@ def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
         return SQLiteEventStore(kw.get("path", ":memory:"))
     if kind in ("cassandra", "bucketed"):
         return BucketedEventStore(kw.get("bucket_ms", 3600_000))
+    if kind == "columnar":
+        from .columnar import ColumnarEventStore
+        return ColumnarEventStore()
     raise ValueError(f"unknown event store {kind!r}")

@@ -12,8 +12,8 @@ from .config import AttributeNode as A
 from .config import ConfigurationModel, ElementNode as E
 
 DATASTORE = E("Datastore", "datastore", "Entity / event persistence backend", [
-    A("type", "String", "memory | sqlite | mongodb | bucketed | influx", True, "memory",
-      ["memory", "sqlite", "mongodb", "bucketed", "influx"]),
+    A("type", "String", "memory | sqlite | mongodb | bucketed | influx | columnar", True, "memory",
+      ["memory", "sqlite", "mongodb", "bucketed", "influx", "columnar"]),
     A("path", "String", "SQLite file (supports [[tenant.token]])"),
     A("uri", "String", "MongoDB connection URI (${mongodb.uri:...})"),
     A("database", "String", "database name"),
@@ -76,6 +76,9 @@ _m("inbound-processing", "Inbound Processing", [
       choices=["cpu", "gpu"]),
     A("device", "String", "gpu engine placement: auto | gpu | cpu", default="auto", choices=["auto", "gpu", "cpu"]),
     A("batchSize", "Integer", "micro-batch payloads (gpu engine)", default=65536),
+    A("storage", "String", "objects | columnar (gpu engine)", default="objects", choices=["objects", "columnar"]),
+    A("publishEnriched", "String", "events | batches | none (gpu engine)", default="events",
+      choices=["events", "batches", "none"]),
     A("maxDelayMs", "Integer", "micro-batch latency bound (gpu engine)", default=5)], [
     E("Zone Tests", "gpu-zone-tests", "zone tests evaluated inside the GPU engine", [
         A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")])])

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import json
 
-from ..core.errors import ErrorCode, NotFoundException
+from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
 from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceCommandInvocation,
                              DeviceCommandResponse, DeviceEvent, DeviceEventIndex, DeviceEventType, DeviceLocation,
                              DeviceMeasurement, DeviceStateChange, now_ms)
@@ -134,6 +134,12 @@ class DeviceEventManagement:
         if fire_triggers:
             self._on_persisted(events)
         return len(events)
+
+    def add_columnar_batch(self, payload: bytes) -> int:
+        """Append a columnar batch of GPU-enriched rows (MI355X tenants; needs the columnar datastore)."""
+        if not hasattr(self.store, "add_columnar"):
+            raise SiteWhereSystemException(ErrorCode.Error, detail="event store is not columnar")
+        return self.store.add_columnar(payload)
 
     def add_device_event_batch(self, assignment_id: str, batch: dict) -> dict:
         """Measurements + locations + alerts in one call (reference AddDeviceEventBatch)."""

@@ -27,8 +27,9 @@ import time
 
 import numpy as np
 
-from ..models.columnar import (EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, ST_CONTROL,
-                               ST_UNASSIGNED, ST_UNREGISTERED)
+from ..models.columnar import (EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC,
+                               ST_CONTROL, ST_UNASSIGNED, ST_UNREGISTERED)
+from ..persistence.columnar import encode_batch
 from ..models.domain import (AlertLevel, AlertSource, DeviceAlert, DeviceAssignmentStatus, DeviceLocation,
                              DeviceMeasurement, DeviceStateChange, now_ms)
 from ..pipeline.config import EngineConfig
@@ -40,6 +41,7 @@ from ..runtime.microservice import MicroserviceTenantEngine
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
 
 _LEVELS = [AlertLevel.Info, AlertLevel.Warning, AlertLevel.Error, AlertLevel.Critical]
+ENRICHED_BATCHES = "inbound-enriched-batches"     # columnar enriched output (publishEnriched = "batches")
 
 
 def unpack_raw_batch(value: bytes):
@@ -83,6 +85,11 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
         self.t_unregistered = n.unregistered_device_events(t)
         self.t_registration = n.device_registration_events(t)
         self.t_decoded = n.decoded_events(t)
+        self.t_enriched_batches = n.tenant_prefix(t) + ENRICHED_BATCHES
+        self.storage = cfg.get("storage", "objects")            # objects | columnar
+        self.publish = cfg.get("publishEnriched", "events")     # events | batches | none
+        self._asg_dirty: set[int] = set()
+        self._names_sent = 0
         ecfg = EngineConfig.small(**{k: int(v) for k, v in cfg.get("capacity", {}).items()}) \
             if cfg.get("sizing", "small") == "small" else EngineConfig(**cfg.get("capacity", {}))
         ecfg.presence_missing_ms = int(cfg.get("presenceMissingMs", ecfg.presence_missing_ms))
@@ -172,6 +179,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
                                         area=[self.areas.get(a.area_id)], asset=[self.assets.get(a.asset_id)],
                                         active=[1 if active else 0])
             self._asg_entities[ai] = a
+            self._asg_dirty.add(ai)
 
     def _on_model_update(self, recs):
         for r in recs:
@@ -213,27 +221,69 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
         with self._lock, self.step_timer.time():
             res = self.engine.step(raw, offs, now)
         self.processed_events.mark(res.n_events)
+        if self.storage == "columnar":
+            self._store_columnar(res, now)
+        else:
+            self._store_objects(res, now)
+        if res.rejects is not None and len(res.rejects):
+            self._slow_path(raw, offs, res)
+        return res
+
+    def columnar_payload(self, res, now: int) -> bytes:
+        """Rows + the dictionary entries the receiver has not seen yet (assignment context, names)."""
+        with self._lock:
+            asg = {}
+            for ai in self._asg_dirty:
+                a = self._asg_entities.get(ai)
+                if a is not None:
+                    asg[ai] = [a.id, a.device_id, a.customer_id, a.area_id, a.asset_id]
+            self._asg_dirty.clear()
+            if res.out is not None and len(res.out):
+                ids = set(np.unique(res.out["name_id"]).tolist()) - {NO_NAME}
+                if ids - self._nid2name.keys():
+                    self._reload_names()
+            names = dict(self._nid2name) if len(self._nid2name) != self._names_sent else {}
+            self._names_sent = len(self._nid2name)
+        rules = {t.alert_type: t.alert_message for t in self.engine.tests}
+        out = res.out if res.out is not None else np.zeros(0, OUT_REC)
+        return encode_batch(self.boot, res.first_seq, res.world, res.rank, now, out, asg, names, rules)
+
+    def _store_columnar(self, res, now: int):
+        payload = self.columnar_payload(res, now)
+        n = self._em().add_columnar_batch(payload)
+        self.persisted_events.mark(n)
+        if self.publish == "batches":
+            self.ms.producer.send(self.t_enriched_batches, None, payload)
+        elif self.publish == "events":
+            self._publish_events(self._to_events(res, now))
+
+    def _publish_events(self, events):
+        if events:
+            self.ms.producer.send_batch(self.t_enriched, [
+                (self._dev_tokens.get(self.devices.idx.get(e.device_id, -1)) or e.device_id,
+                 json.dumps({"event": codec.to_wire(e), "context": self._context(e)}).encode()) for e in events])
+
+    def _store_objects(self, res, now: int):
         events = self._to_events(res, now)
         if events:
             self._em().add_enriched_events(events)
             self.persisted_events.mark(len(events))
-            self.ms.producer.send_batch(self.t_enriched, [
-                (self._dev_tokens.get(self.devices.idx.get(e.device_id, -1)) or e.device_id,
-                 json.dumps({"event": codec.to_wire(e), "context": self._context(e)}).encode()) for e in events])
-        if res.rejects is not None and len(res.rejects):
-            self._slow_path(raw, offs, res)
-        return res
+            if self.publish == "events":
+                self._publish_events(events)
 
     def _name(self, nid: int) -> str:
         if nid == NO_NAME:
             return ""
         s = self._nid2name.get(nid)
         if s is None:
-            table = self.engine.intern if hasattr(self.engine, "intern") and isinstance(self.engine.intern, dict) \
-                else self.engine.intern_table()
-            self._nid2name = {i: self.engine.names.get(h, str(h)) for h, i in table.items()}
+            self._reload_names()
             s = self._nid2name.get(nid, "")
         return s
+
+    def _reload_names(self):
+        table = self.engine.intern if hasattr(self.engine, "intern") and isinstance(self.engine.intern, dict) \
+            else self.engine.intern_table()
+        self._nid2name = {i: self.engine.names.get(h, str(h)) for h, i in table.items()}
 
     def _to_events(self, res, now: int) -> list:
         out = res.out

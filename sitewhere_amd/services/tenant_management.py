@@ -73,7 +73,16 @@ for _svc in ("device-management", "asset-management", "batch-operations", "sched
                                                                    "database": "tenant-[[tenant.token]]"}}
 TENANT_TEMPLATES["gpu"] = copy.deepcopy(TENANT_TEMPLATES["default"])
 TENANT_TEMPLATES["gpu"]["name"] = "MI355X-accelerated inbound pipeline"
-TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5}
+TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5,
+                                                             "storage": "objects", "publishEnriched": "events"}
+# High-throughput MI355X tenant: enriched rows stay columnar end to end (no per-event host objects).
+TENANT_TEMPLATES["gpu-columnar"] = copy.deepcopy(TENANT_TEMPLATES["gpu"])
+TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event store"
+TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
+    storage="columnar", publishEnriched="batches",
+    capacity={"max_msgs": 65536, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
+              "dedup_slots": 1 << 18, "gen_cap": 32768})
+TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {"datastore": {"type": "columnar"}}
 
 DATASET_TEMPLATES = {
     "empty": {"name": "Empty dataset", "description": "No data is created."},

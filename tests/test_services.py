@@ -265,3 +265,52 @@ def test_global_configuration_update_restarts_engines(sw):
                       ms.get_tenant_engine("default") is not before and
                       ms.get_tenant_engine("default").status.value == "Started", 20)
     assert ms.config.get("note") == "changed"
+
+
+def test_columnar_tenant_end_to_end():
+    """gpu-columnar template: engine rows stored as columns, queried through the normal event API."""
+    inst = SiteWhereInstance().start()
+    try:
+        inst.wait_for_tenant("default", 60)
+        tm = inst.api("TenantManagement")
+        inst.instance.system_user.run(lambda: tm.create_tenant({"token": "col", "name": "Columnar",
+                                                                "configurationTemplateId": "gpu-columnar",
+                                                                "datasetTemplateId": "construction"}))
+        inst.wait_for_tenant("col", 60)
+        run = lambda f: inst.instance.system_user.run(f, "col")  # noqa: E731
+        dm = inst.api("DeviceManagement", "col")
+        em = inst.api("DeviceEventManagement", "col")
+        ib = inst.tenant_engine("inbound-processing", "col")
+        dev = run(lambda: dm.get_device_by_token("galaxytab-001"))
+        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None)
+        topic = inst.instance.naming.tenant_prefix("col") + "inbound-enriched-batches"
+        cons = inst.instance.bus.consumer("col-batches", [topic])
+        api = inst.api("InboundProcessing", "col")
+        msgs = [wire.measurements("galaxytab-001", {"temp": 20.0 + i}, event_date=1_700_000_000_000 + i)
+                for i in range(50)] + [wire.location("galaxytab-001", 34.0, -84.0, event_date=1_700_000_001_000)]
+        r = run(lambda: api.process_payloads(msgs))
+        assert r["persisted"] == 51
+        res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
+                                                         {"pageSize": 10}))
+        assert res.num_results == 50 and len(res.results) == 10
+        assert [m.value for m in res.results[:3]] == [69.0, 68.0, 67.0]          # newest first
+        assert res.results[0].name == "temp" and res.results[0].customer_id is not None
+        loc = run(lambda: em.list_locations_for_index("Customer", [res.results[0].customer_id])).results
+        assert loc and loc[0].latitude == 34.0
+        one = run(lambda: em.get_device_event_by_id(res.results[0].id))
+        assert one.value == 69.0
+        rng = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
+                                                         {"startDate": 1_700_000_000_010, "endDate": 1_700_000_000_019,
+                                                          "pageSize": 0}))
+        assert rng.num_results == 10
+        got = []
+        end = time.time() + 5
+        while not got and time.time() < end:
+            for recs in cons.poll(200).values():
+                got += recs
+        from sitewhere_amd.persistence.columnar import decode_batch
+        b = decode_batch(got[0].value)
+        assert len(b["rows"]) == 51 and "temp" in b["names"].values()
+        cons.close()
+    finally:
+        inst.stop()
