@@ -493,7 +493,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     a.s_etype[row] = r.etype;
     a.s_level[row] = r.level;
     a.s_date[row] = r.event_date;
-    a.s_recv[row] = a.now_ms;
+    a.s_recv[row] = a.sp->now_ms;
     a.s_dev[row] = dev;
     a.s_asg[row] = asg;
     const int4 ctx = *reinterpret_cast<const int4*>(&a.asg_ctx[asg]);
@@ -506,7 +506,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     a.s_v2[row] = r.v2;
     a.s_alt[row] = r.alt_hash;
     a.s_aux[row] = ((ull)r.src_rank << 48) | ((ull)r.aux_len << 32) | (ull)r.aux_off;
-    a.s_batch[row] = (int32_t)a.batch_seq;
+    a.s_batch[row] = (int32_t)a.sp->batch_seq;
     SwOutRec o;
     o.event_date = r.event_date;
     o.v0 = r.v0;
@@ -517,7 +517,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     o.name_id = (nid >= 0 && nid < 0xffff) ? (uint16_t)nid : (uint16_t)0xffff;
     o.etype = r.etype;
     o.level = r.level;
-    a.out[seq - c0] = o;
+    a.sp->out[seq - c0] = o;
   }
 }
 
@@ -556,7 +556,7 @@ __global__ void k_state_p1(SwEngineArgs a, const SwEventRec* __restrict__ R, con
     const int32_t asg = asgs[i];
     if (r.etype != SW_EV_MEASUREMENT && r.etype != SW_EV_LOCATION && r.etype != SW_EV_ALERT) continue;
     SwAsgState* st = &a.st[asg];
-    atomicMax((ull*)&st->last, (ull)a.now_ms);
+    atomicMax((ull*)&st->last, (ull)a.sp->now_ms);
     if (st->missing) st->missing = 0;  // presence detected again
     const ull d = (ull)r.event_date;
     if (r.etype == SW_EV_LOCATION) {
@@ -782,7 +782,7 @@ __global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __
         if (g < a.gen_cap) {
           SwEventRec r;
           r.fp_lo = 0; r.fp_hi = 0;
-          r.event_date = a.now_ms;  // reference: alert.setEventDate(new Date())
+          r.event_date = a.sp->now_ms;  // reference: alert.setEventDate(new Date())
           r.name_hash = a.test_name_hash[t];
           r.v0 = 0; r.v1 = 0; r.v2 = 0; r.alt_hash = 0;
           r.aux_off = (uint32_t)t; r.aux2_off = 0; r.aux_len = 0; r.aux2_len = 0;
@@ -800,17 +800,19 @@ __global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __
 
 // ============================================================================ presence
 __global__ void k_presence(SwEngineArgs a) {
-  const ull limit = (ull)(a.now_ms - a.presence_missing_ms);
+  const SwStepParams P = *a.sp;
+  if (P.presence_missing_ms <= 0) return;
+  const ull limit = (ull)(P.now_ms - P.presence_missing_ms);
   for (int64_t s = (int64_t)blockIdx.x * BLK + threadIdx.x; s < a.n_asg; s += (int64_t)gridDim.x * BLK) {
     SwAsgState* st = &a.st[s];
     const ull last = st->last;
     const bool miss = last != 0 && last < limit && st->missing == 0 && a.asg_active[s];
     if (!miss) continue;
-    st->missing = (ull)a.now_ms;  // send-once strategy
+    st->missing = (ull)P.now_ms;  // send-once strategy
     const uint32_t g = atomicAdd(a.n_gen, 1u);
     if (g < a.gen_cap) {
       SwEventRec r;
-      r.fp_lo = 0; r.fp_hi = 0; r.event_date = a.now_ms; r.name_hash = a.presence_name_hash;
+      r.fp_lo = 0; r.fp_hi = 0; r.event_date = P.now_ms; r.name_hash = a.presence_name_hash;
       r.v0 = 0; r.v1 = 0; r.v2 = 0; r.alt_hash = 0;
       r.aux_off = 0; r.aux2_off = 0; r.aux_len = 0; r.aux2_len = 0;
       r.etype = SW_EV_STATE_CHANGE; r.flags = 0; r.src_rank = (uint8_t)a.rank; r.level = 0;
@@ -829,6 +831,7 @@ __global__ void k_step_begin(SwEngineArgs a) {
     *a.n_new_names = 0;
     *a.n_out = 0;
     *a.overflow = 0;
+    ((ull*)a.stats)[SW_STAT_MSGS] += (ull)a.n_msgs;   // decode phase: by-value batch size
   }
 }
 
@@ -844,7 +847,6 @@ __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
     *a.n_out = (uint32_t)(*a.store_cursor - *a.step_cursor0);
     *a.seq_base += *a.n_work;
     ull* st = (ull*)a.stats;
-    st[SW_STAT_MSGS] += (ull)a.n_msgs;
     st[SW_STAT_EVENTS] += *a.n_work;
     st[SW_STAT_PERSISTED] += *a.n_out;
     st[SW_STAT_RULE_ALERTS] += *n_rule_alerts;
@@ -956,7 +958,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
     k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile + otiles);
   }
   k_gen_clamp<<<1, 64, 0, s>>>(a, n_rule);
-  if (a.presence_missing_ms > 0) k_presence<<<grid_for(a.n_asg), BLK, 0, s>>>(a);
+  k_presence<<<grid_for(a.n_asg), BLK, 0, s>>>(a);   // exits at once when presence is off this step
   k_gen_clamp<<<1, 64, 0, s>>>(a, nullptr);
   const int gg = grid_for(a.gen_cap);
   k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_mask);
@@ -968,6 +970,45 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
 }
+
+__global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int64_t presence_ms,
+                                  SwOutRec* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    sp->now_ms = now_ms; sp->batch_seq = batch_seq; sp->presence_missing_ms = presence_ms; sp->out = out;
+  }
+}
+
+// Stream-ordered write of this step's params (before the decode / process phases of the step).
+int sw_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int64_t presence_ms, void* out,
+                       hipStream_t s) {
+  k_set_step_params<<<1, 64, 0, s>>>(sp, now_ms, batch_seq, presence_ms, (SwOutRec*)out);
+  return (int)hipGetLastError();
+}
+
+// hipGraph of the process phase (unpack when world > 1, then ~30 kernels + scans): captured once per
+// engine configuration, replayed every step -- one launch instead of ~35 from the host.
+int sw_graph_capture_process(const SwEngineArgs* ap, uint32_t* scratch4, int32_t with_unpack, hipStream_t s,
+                             void** exec_out) {
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) return 5000 + (int)e;
+  int rc = 0;
+  if (with_unpack) rc = sw_phase_unpack(ap, s);
+  if (!rc) rc = sw_phase_process(ap, scratch4, s);
+  e = hipStreamEndCapture(s, &g);
+  if (rc) { if (g) hipGraphDestroy(g); return rc; }
+  if (e != hipSuccess) return 6000 + (int)e;
+  hipGraphExec_t x = nullptr;
+  e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return 7000 + (int)e;
+  *exec_out = (void*)x;
+  return 0;
+}
+
+int sw_graph_launch(void* exec, hipStream_t s) { return (int)hipGraphLaunch((hipGraphExec_t)exec, s); }
+
+int sw_graph_destroy(void* exec) { return exec ? (int)hipGraphExecDestroy((hipGraphExec_t)exec) : 0; }
 
 // Registry patch: scatter host-built packed slots (bulk load and incremental upserts).
 __global__ void k_reg_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* vals, int64_t n) {

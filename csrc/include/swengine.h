@@ -50,6 +50,16 @@ typedef struct __attribute__((aligned(16))) SwMsSlot {
   uint64_t pad;
 } SwMsSlot;
 
+// Per-step values read by the process-phase kernels from device memory (written in-stream by
+// sw_set_step_params before each step), so the process phase can be captured once as a hipGraph and
+// replayed: graph nodes keep their by-value SwEngineArgs, these change every step.
+typedef struct SwStepParams {
+  int64_t now_ms;
+  int64_t batch_seq;
+  int64_t presence_missing_ms;  // <= 0: no presence scan this step
+  SwOutRec* out;                // outbound rows of this step
+} SwStepParams;
+
 typedef struct SwEngineArgs {
   // ---------------------------------------------------------------- batch input
   const uint8_t* raw;          // raw wire bytes of the batch (device)
@@ -158,6 +168,8 @@ typedef struct SwEngineArgs {
   uint64_t presence_name_hash; // hash of "presence"
   // ---------------------------------------------------------------- stats
   uint64_t* stats;             // [16] cumulative counters (see SW_STAT_*)
+  // ---------------------------------------------------------------- per-step params (device)
+  SwStepParams* sp;
 } SwEngineArgs;
 
 enum {

@@ -48,6 +48,8 @@ FIELDS = [
     ("presence_missing_ms", I), ("presence_name_hash", U),
     # stats
     ("stats", P),
+    # per-step params (device SwStepParams, written in-stream each step)
+    ("sp", P),
 ]
 
 

@@ -141,6 +141,7 @@ class GpuInboundEngine(EngineBase):
         t["zmask"] = z(c.rec_cap, i64)
         t["ztile"] = z(2 * ntiles + 64, i32)
         t["stats"] = z(16, i64)
+        t["sp"] = z(8, i64)                      # SwStepParams (per-step values read by the process phase)
         self._set_zone_tensors()
         self.args = a = SwEngineArgs()
         sc_ptr = _ptr(t["scalars"])
@@ -183,7 +184,14 @@ class GpuInboundEngine(EngineBase):
         a.presence_missing_ms = 0
         a.presence_name_hash = self.presence_hash
         a.stats = _ptr(t["stats"])
+        a.sp = _ptr(t["sp"])
         self._rule_scratch = S(8)
+        # hipGraph of the process phase: captured on first use, replayed each step, re-captured
+        # whenever a by-value argument of its kernels changes (zone rules)
+        import os
+        self.use_graph = os.environ.get("SW_GRAPH", "1") != "0"
+        self._graph = None
+        self._cap_stream = torch.cuda.Stream(self.device) if self.use_graph else None
         self._out_sel = 0
         self._apply_zone_ptrs()
 
@@ -238,6 +246,13 @@ class GpuInboundEngine(EngineBase):
         if hasattr(self, "args"):
             self._set_zone_tensors()
             self._apply_zone_ptrs()
+            self._drop_graph()
+
+    def _drop_graph(self):
+        if getattr(self, "_graph", None) is not None:
+            torch.cuda.synchronize(self.device)
+            self.lib.sw_graph_destroy(ctypes.c_void_p(self._graph))
+            self._graph = None
 
     # ------------------------------------------------------------------ data plane
     def step_async(self, raw_dev: torch.Tensor, off_dev: torch.Tensor, n_msgs: int, now_ms: int,
@@ -260,6 +275,10 @@ class GpuInboundEngine(EngineBase):
         sel = self._out_sel if out_sel is None else out_sel
         self._last_sel = sel
         a.out = _ptr(self.out_dev[sel]) if out_to_device else self.out_host[sel].dev
+        rc = self.lib.sw_set_step_params(ctypes.c_void_p(a.sp), a.now_ms, a.batch_seq, a.presence_missing_ms,
+                                         ctypes.c_void_p(a.out), self._stream())
+        if rc:
+            raise RuntimeError(f"sw_set_step_params failed ({rc})")
         return sel
 
     # The three phases of a step (split so a multi-rank step can be driven without torch.distributed,
@@ -284,6 +303,23 @@ class GpuInboundEngine(EngineBase):
 
     def phase_process(self):
         ap = ctypes.byref(self.args)
+        if self.use_graph:
+            if self._graph is None:
+                ex = ctypes.c_void_p()
+                rc = self.lib.sw_graph_capture_process(ap, ctypes.c_void_p(self._rule_scratch), int(self.world > 1),
+                                                       ctypes.c_void_p(self._cap_stream.cuda_stream), ctypes.byref(ex))
+                if rc:
+                    import warnings
+                    warnings.warn(f"hipGraph capture of the process phase failed ({rc}); using direct launches")
+                    self.use_graph = False
+                else:
+                    self._graph = ex.value
+            if self._graph is not None:
+                rc = self.lib.sw_graph_launch(ctypes.c_void_p(self._graph), self._stream())
+                if rc:
+                    raise RuntimeError(f"sw_graph_launch failed ({rc})")
+                self.batch_seq += 1
+                return
         if self.world > 1:
             rc = self.lib.sw_phase_unpack(ap, self._stream())
             if rc:

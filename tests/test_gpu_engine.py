@@ -137,3 +137,25 @@ def test_standalone_pip_kernel():
     got = out.cpu().numpy().astype(bool)
     want = np.array([pip(poly, x, y) for x, y in pts])
     assert (got == want).all()
+
+
+def test_graph_replay_matches_direct_launches_and_recaptures_on_zone_change():
+    """The hipGraph-captured process phase gives the same results as direct launches, including
+    across a zone-rule change (which must re-capture: zone pointers are by-value kernel args)."""
+    from sitewhere_amd.pipeline.engine_base import Zone, ZoneTest
+    g = GpuInboundEngine(small_cfg())
+    d = GpuInboundEngine(small_cfg())
+    d.use_graph = False
+    for e in (g, d):
+        setup_fleet(e, n_dev=1000)
+    for k in range(6):
+        if k == 3:
+            for e in (g, d):
+                e.set_zone_rules([Zone("z2", [(32.0, -86.0), (32.0, -84.0), (34.5, -84.0), (34.5, -86.0)])],
+                                 [ZoneTest("z2", "inside", "zone2.enter", 3)])
+        raw, offs = fleet_batch(2500, seed=700 + k)
+        rg = g.step(raw, offs, NOW + k * 1000, presence=(k == 5))
+        rd = d.step(raw, offs, NOW + k * 1000, presence=(k == 5))
+        assert canon_out(rg.out, None) == canon_out(rd.out, None)
+        assert g.stats_dict() == d.stats_dict()
+    assert g._graph is not None

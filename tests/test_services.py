@@ -176,7 +176,8 @@ def test_new_tenant_gpu_template_cpu_engine():
         em = inst.api("DeviceEventManagement", "fast")
         run = lambda f: inst.instance.system_user.run(f, "fast")  # noqa: E731
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
-        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None)
+        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None and
+                          ib.assignments.idx.get(dev.device_assignment_id) is not None)
         api = inst.api("InboundProcessing", "fast")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
@@ -208,6 +209,8 @@ def test_gpu_tenant_engine_on_device():
         dm = inst.api("DeviceManagement", "fastgpu")
         em = inst.api("DeviceEventManagement", "fastgpu")
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
+        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None and
+                          ib.assignments.idx.get(dev.device_assignment_id) is not None)
         api = inst.api("InboundProcessing", "fastgpu")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
@@ -282,7 +285,8 @@ def test_columnar_tenant_end_to_end():
         em = inst.api("DeviceEventManagement", "col")
         ib = inst.tenant_engine("inbound-processing", "col")
         dev = run(lambda: dm.get_device_by_token("galaxytab-001"))
-        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None)
+        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None and
+                          ib.assignments.idx.get(dev.device_assignment_id) is not None)
         topic = inst.instance.naming.tenant_prefix("col") + "inbound-enriched-batches"
         cons = inst.instance.bus.consumer("col-batches", [topic])
         api = inst.api("InboundProcessing", "col")
