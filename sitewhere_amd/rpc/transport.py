@@ -109,9 +109,15 @@ class ServiceResolver:
         return sorted(set(self._global) | set(self._tenant))
 
 
-def invoke(resolver: ServiceResolver, tokens: TokenManagement, service: str, method: str, body: bytes,
-           jwt: str | None, tenant: str | None, trace: str | None, require_jwt: bool = True):
-    """Common server-side dispatch (network and local): auth -> tenant -> span -> call."""
+_IMMUTABLE = (bytes, str, int, float, bool, type(None))
+
+
+def invoke(resolver: ServiceResolver, tokens: TokenManagement, service: str, method: str, body: bytes | None,
+           jwt: str | None, tenant: str | None, trace: str | None, require_jwt: bool = True, direct=None):
+    """Common server-side dispatch (network and local): auth -> tenant -> span -> call.
+
+    ``direct=(args, kwargs)`` skips the body codec (in-process calls whose arguments are all
+    immutable scalars / bytes -- e.g. columnar batch payloads -- need no isolation copy)."""
     if jwt is None:
         if require_jwt:
             raise UnauthorizedException("No JWT in request metadata")
@@ -129,6 +135,8 @@ def invoke(resolver: ServiceResolver, tokens: TokenManagement, service: str, met
             fn = getattr(impl, snake_method(method), None)
             if fn is None or not callable(fn) or isinstance(fn, type) or snake_method(method).startswith("_"):
                 raise NotFoundException(ErrorCode.Error, f"{service} has no method {method}")
+            if direct is not None:
+                return fn(*direct[0], **direct[1])
             req = codec.loads(body) or {}
             return fn(*req.get("args", []), **req.get("kwargs", {}))
 
@@ -292,7 +300,13 @@ class LocalChannel(ApiChannel):
         jwt = _jwt_for_call(self.tokens, self.system_jwt)
         t = _tenant_for_call(tenant)
         span = global_tracer().active()
-        body = codec.dumps({"args": list(args), "kwargs": kwargs})
-        out = invoke(self.resolver, self.tokens, service, camel_method(method) if "_" in method else method, body,
-                     jwt, t, span.context_header() if span else None)
-        return codec.loads(codec.dumps(out)) if self.serialize else out
+        m = camel_method(method) if "_" in method else method
+        trace = span.context_header() if span else None
+        if all(isinstance(x, _IMMUTABLE) for x in args) and all(isinstance(x, _IMMUTABLE) for x in kwargs.values()):
+            out = invoke(self.resolver, self.tokens, service, m, None, jwt, t, trace, direct=(args, kwargs))
+        else:
+            out = invoke(self.resolver, self.tokens, service, m, codec.dumps({"args": list(args), "kwargs": kwargs}),
+                         jwt, t, trace)
+        if not self.serialize or isinstance(out, _IMMUTABLE):
+            return out
+        return codec.loads(codec.dumps(out))
