@@ -18,7 +18,7 @@ import logging
 import threading
 import time
 import uuid
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Any, Callable
 
 from .errors import ServerStartupException, SiteWhereException
@@ -489,6 +489,3 @@ class CompositeLifecycleStep(LifecycleStep):
         finally:
             LifecycleProgressMonitor.finish_span(span)
             monitor.pop_context()
-
-
-_ = field

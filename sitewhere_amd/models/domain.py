@@ -13,7 +13,7 @@ import re
 import time
 import uuid
 from dataclasses import dataclass, field
-from typing import Any, get_type_hints
+from typing import get_type_hints
 
 _camel_re = re.compile(r"_([a-z0-9])")
 
@@ -714,6 +714,3 @@ def stamp_updated(e: PersistentEntity, user: str | None = None):
     e.updated_date = now_ms()
     e.updated_by = user
     return e
-
-
-_ = Any

@@ -13,14 +13,13 @@ service-event-management, service-device-state and service-rule-processing
 """
 from __future__ import annotations
 
-import ctypes
 import threading
 from dataclasses import dataclass, field
 
 import numpy as np
 
 from .._native import native
-from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, STAT_NAMES, REG_SLOT
+from ..models.columnar import STAT_NAMES, REG_SLOT
 from .config import EngineConfig
 from .fleet import hash64
 
@@ -238,6 +237,3 @@ class EngineBase:
     @staticmethod
     def stats_dict(arr) -> dict:
         return {n: int(arr[i]) for i, n in enumerate(STAT_NAMES)}
-
-
-_ = (ctypes, EVENT_REC, OUT_REC, NAME_REF)

@@ -9,7 +9,6 @@ manual harnesses ``MqttTests.java`` / ``SiteWhereClientTester.java``).
 """
 from __future__ import annotations
 
-import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -128,6 +127,3 @@ def pack_messages(messages):
     offs[1:] = np.cumsum([len(m) for m in messages])
     raw = np.frombuffer(b"".join(messages) + b"\0" * 64, np.uint8).copy()
     return raw, offs
-
-
-_ = ctypes  # keep import for type users

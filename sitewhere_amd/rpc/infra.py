@@ -27,7 +27,7 @@ import grpc
 import msgpack
 
 from ..bus.log import _FRAME, Consumer, EventBus, Producer, Record
-from ..coord.store import (INITIALIZED, BadVersionError, Coordination, NodeExistsError, NoNodeError,
+from ..coord.store import (BadVersionError, Coordination, NodeExistsError, NoNodeError,
                            NotEmptyError, Stat)
 
 _ERRORS = {c.__name__: c for c in (NoNodeError, NodeExistsError, BadVersionError, NotEmptyError, KeyError,
@@ -518,6 +518,3 @@ class RemoteCoordination:
             except Exception:
                 pass
         self.r.close()
-
-
-_ = INITIALIZED

@@ -26,14 +26,14 @@ import uuid
 
 from ..bus.log import EventBus
 from ..bus.naming import TopicNaming
-from ..coord.store import INITIALIZED, NODE_ADDED, NODE_REMOVED, NODE_UPDATED, Coordination, InterProcessMutex
+from ..coord.store import NODE_ADDED, NODE_REMOVED, NODE_UPDATED, Coordination, InterProcessMutex
 from ..core.errors import SiteWhereException, TenantEngineNotAvailableException
 from ..core.lifecycle import (CompositeLifecycleStep, LifecycleComponent, LifecycleComponentType,
                               LifecycleProgressMonitor, LifecycleStatus, SimpleLifecycleStep,
                               TenantEngineLifecycleComponent)
 from ..core.metrics import MetricRegistry, MetricsReporter
 from ..core.security import SystemUser, TokenManagement
-from ..core.tracing import Tracer, global_tracer
+from ..core.tracing import global_tracer
 from ..models.domain import Tenant
 from ..rpc.transport import GrpcChannel, LocalChannel, RpcServer, ServiceProxy, ServiceResolver
 from .config import InstanceSettings, dump_document, parse_document, substitute
@@ -700,6 +700,3 @@ def shutdown_microservice(ms: Microservice):
     mon = LifecycleProgressMonitor(ms.identifier)
     ms.lifecycle_stop(mon)
     ms.lifecycle_terminate(mon)
-
-
-_ = (INITIALIZED, Tracer)

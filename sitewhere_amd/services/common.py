@@ -6,7 +6,7 @@ import uuid
 
 from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
 from ..core.security import current_authentication
-from ..models.domain import Model, SearchCriteria, SearchResults, camel, snake, stamp_created, stamp_updated
+from ..models.domain import Model, SearchCriteria, SearchResults, snake, stamp_created, stamp_updated
 
 
 def _user():
@@ -102,6 +102,3 @@ class Crud:
         c = criteria_of(criteria)
         items = self.query(pred, sort, reverse)
         return SearchResults(len(items), c.slice(items))
-
-
-_ = camel

@@ -22,7 +22,7 @@ from ..models.domain import (Area, AreaType, Customer, CustomerType, Device, Dev
                              Zone, now_ms)
 from ..persistence.store import EntityStore, create_store
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
-from .common import Crud, apply_request, criteria_of
+from .common import Crud
 
 
 def _ids(v):
@@ -691,7 +691,3 @@ class DeviceManagementMicroservice(MultitenantMicroservice):
 
     def create_tenant_engine(self, tenant):
         return DeviceManagementTenantEngine(self, tenant)
-
-
-
-_ = apply_request, criteria_of

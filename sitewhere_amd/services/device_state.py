@@ -16,7 +16,6 @@ from __future__ import annotations
 import json
 import re
 import threading
-import time
 
 from ..core.errors import ErrorCode
 from ..models.domain import DeviceEventType, DeviceState, SearchResults, now_ms
@@ -184,6 +183,3 @@ class DeviceStateMicroservice(MultitenantMicroservice):
 
     def create_tenant_engine(self, tenant):
         return DeviceStateTenantEngine(self, tenant)
-
-
-_ = time

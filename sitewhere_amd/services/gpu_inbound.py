@@ -371,6 +371,3 @@ class GpuInboundApi:
         raw, offs = pack_messages([bytes(p) for p in payloads])
         r = self._e.process_batch(raw, offs)
         return {"messages": r.n_msgs, "events": r.n_events, "persisted": r.n_persisted}
-
-
-_ = ST_UNASSIGNED

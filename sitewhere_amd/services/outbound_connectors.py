@@ -16,7 +16,6 @@ import os
 import threading
 import urllib.request
 
-from ..core.errors import SiteWhereException
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..edges.mqtt import MqttClient
 from ..rpc import codec

@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import datetime as _dt
 import threading
-import time
 
 from ..core.errors import ErrorCode
 from ..models.domain import (CommandInitiator, Schedule, ScheduledJob, ScheduledJobState, ScheduledJobType,
@@ -234,6 +233,3 @@ class ScheduleManagementMicroservice(MultitenantMicroservice):
 
     def create_tenant_engine(self, tenant):
         return ScheduleManagementTenantEngine(self, tenant)
-
-
-_ = time
