@@ -68,7 +68,9 @@ _m("instance-management", "Instance Management", [A("instanceTemplate", "String"
 _m("user-management", "User Management", [], [DATASTORE])
 _m("tenant-management", "Tenant Management", [], [DATASTORE])
 _m("web-rest", "Web/REST", [A("port", "Integer", "HTTP port", default=8080), A("cors", "Boolean", "CORS", default=True)])
-_m("event-sources", "Event Sources", [], [SOURCE, E("Deduplicator", "deduplicator", "alternate-id | script", [
+_m("event-sources", "Event Sources", [
+    A("rawBatchSize", "Integer", "payloads per raw micro-batch for the MI355X engine", default=4096),
+    A("rawMaxDelayMs", "Integer", "latency bound of a raw micro-batch", default=5)], [SOURCE, E("Deduplicator", "deduplicator", "alternate-id | script", [
     A("type", "String", "alternate-id | script", True), A("script", "Script", "script id")])])
 _m("inbound-processing", "Inbound Processing", [
     A("processingThreadCount", "Integer", "decoded-event processing threads", default=25),

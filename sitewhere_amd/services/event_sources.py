@@ -269,7 +269,8 @@ class InboundEventSource(TenantEngineLifecycleComponent):
 
     def on_encoded_event_received(self, receiver, payload: bytes, metadata: dict) -> int:
         if self.forward_raw:
-            self.manager.handle_raw_payload(self.source_id, payload)
+            self.manager.handle_raw_payload(self.source_id, payload,
+                                            getattr(self.tenant_engine, "raw_batch", 4096))
             return 1
         try:
             reqs = self.decoder.decode(payload, metadata)
@@ -339,6 +340,10 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
 class EventSourcesTenantEngine(MicroserviceTenantEngine):
     def tenant_initialize(self, monitor):
         self.manager = EventSourcesManager(self)
+        # raw batches for the MI355X engine are shipped at rawBatchSize payloads or every rawMaxDelayMs
+        self.raw_batch = int(self.config.get("rawBatchSize", 4096))
+        self.raw_delay_s = float(self.config.get("rawMaxDelayMs", 5)) / 1000.0
+        self._flush_stop = threading.Event()
         ms = self.ms
         for sc in self.config.get("sources", []):
             src = self.build_source(sc)
@@ -397,8 +402,20 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
     def tenant_start(self, monitor):
         for s in self.manager.sources.values():
             self.start_nested_component(s, monitor, require=False)
+        if any(s.forward_raw for s in self.manager.sources.values()):
+            self._flush_stop.clear()
+            threading.Thread(target=self._flusher, daemon=True, name=f"raw-flush-{self.tenant.token}").start()
+
+    def _flusher(self):
+        """Latency bound of the raw micro-batches (the count bound is checked on every payload)."""
+        while not self._flush_stop.wait(self.raw_delay_s):
+            try:
+                self.manager.flush_raw()
+            except Exception:
+                self.logger.exception("raw batch flush failed")
 
     def tenant_stop(self, monitor):
+        self._flush_stop.set()
         for s in self.manager.sources.values():
             s.lifecycle_stop(monitor)
         self.manager.flush_raw()

@@ -37,8 +37,8 @@ from ..pipeline.engine_base import Zone, ZoneTest
 from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
 from ..runtime.consumers import BusConsumer
-from ..runtime.microservice import MicroserviceTenantEngine
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
+from .inbound_processing import InboundProcessingTenantEngine
 
 _LEVELS = [AlertLevel.Info, AlertLevel.Warning, AlertLevel.Error, AlertLevel.Critical]
 ENRICHED_BATCHES = "inbound-enriched-batches"     # columnar enriched output (publishEnriched = "batches")
@@ -76,8 +76,12 @@ class IndexMap:
         return self.ids[i] if 0 <= i < len(self.ids) else None
 
 
-class GpuInboundTenantEngine(MicroserviceTenantEngine):
+class GpuInboundTenantEngine(InboundProcessingTenantEngine):
+    """Raw protobuf batches run through the fused engine; decoded requests that did not come through
+    the raw path (JSON sources, reprocessed events) keep the inherited per-event path."""
+
     def tenant_initialize(self, monitor):
+        super().tenant_initialize(monitor)      # decoded / persisted consumers, near caches, meters
         cfg = self.config
         ms, t = self.ms, self.tenant.token
         n = ms.instance.naming
@@ -96,7 +100,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
         ecfg.presence_check_ms = int(cfg.get("presenceCheckMs", ecfg.presence_check_ms))
         self.engine_cfg = ecfg
         self.engine = self._make_engine(cfg.get("device", "auto"), ecfg)
-        self.devices, self.assignments = IndexMap(), IndexMap()
+        self.dev_index, self.asg_index = IndexMap(), IndexMap()
         self.customers, self.areas, self.assets = IndexMap(), IndexMap(), IndexMap()
         self._asg_entities: dict[int, object] = {}
         self._dev_tokens: dict[int, str] = {}
@@ -108,11 +112,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
                            for z in cfg.get("zoneTests", [])]
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
                                         self._process_raw, max_records=16)
-        self.model_consumer = BusConsumer(self, "model-updates", [n.tenant_prefix(t) + "device-model-updates"],
-                                          self._on_model_update)
-        self.processed_events = self.create_meter("processedEvents")
         self.persisted_events = self.create_meter("persistedEvents")
-        self.unregistered = self.create_meter("unregisteredEvents")
         self.step_timer = self.create_timer("engineStep")
         self.api = {"InboundProcessing": GpuInboundApi(self)}
 
@@ -165,15 +165,15 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
 
     def _upsert_device(self, d):
         with self._lock:
-            di = self.devices.get(d.id)
+            di = self.dev_index.get(d.id)
             lo, hi = fingerprint_str(d.token)
             self.engine.register_devices(np.array([lo], np.uint64), np.array([hi], np.uint64), np.array([di], np.int32))
             self._dev_tokens[di] = d.token
 
     def _upsert_assignment(self, a):
         with self._lock:
-            ai = self.assignments.get(a.id)
-            di = self.devices.get(a.device_id)
+            ai = self.asg_index.get(a.id)
+            di = self.dev_index.get(a.device_id)
             active = a.status != DeviceAssignmentStatus.Released
             self.engine.set_assignments([ai], [di], customer=[self.customers.get(a.customer_id)],
                                         area=[self.areas.get(a.area_id)], asset=[self.assets.get(a.asset_id)],
@@ -182,6 +182,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
             self._asg_dirty.add(ai)
 
     def _on_model_update(self, recs):
+        super()._on_model_update(recs)          # near-cache invalidation for the per-event path
         for r in recs:
             m = json.loads(r.value)
             kind, e = m["kind"], codec.from_wire(m["entity"])
@@ -190,7 +191,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
             elif kind == "device.deleted":
                 with self._lock:
                     # tombstone: the fingerprint keeps its slot but resolves to no active assignment
-                    di = self.devices.get(e.id)
+                    di = self.dev_index.get(e.id)
                     self.engine.dev_asg[di] = -1
                     self.engine._dirty_devices(np.array([di], np.int32))
             elif kind.startswith("assignment."):
@@ -203,12 +204,12 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
     # ---------------------------------------------------------------- lifecycle
     def tenant_start(self, monitor):
         self.load_model()
-        self.start_nested_component(self.model_consumer, monitor, require=True)
+        super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         self.start_nested_component(self.raw_consumer, monitor, require=True)
 
     def tenant_stop(self, monitor):
-        for c in (self.raw_consumer, self.model_consumer):
-            c.lifecycle_stop(monitor)
+        self.raw_consumer.lifecycle_stop(monitor)
+        super().tenant_stop(monitor)
 
     # ---------------------------------------------------------------- data plane
     def _process_raw(self, recs):
@@ -260,7 +261,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
     def _publish_events(self, events):
         if events:
             self.ms.producer.send_batch(self.t_enriched, [
-                (self._dev_tokens.get(self.devices.idx.get(e.device_id, -1)) or e.device_id,
+                (self._dev_tokens.get(self.dev_index.idx.get(e.device_id, -1)) or e.device_id,
                  json.dumps({"event": codec.to_wire(e), "context": self._context(e)}).encode()) for e in events])
 
     def _store_objects(self, res, now: int):
@@ -319,7 +320,7 @@ class GpuInboundTenantEngine(MicroserviceTenantEngine):
         return events
 
     def _context(self, e) -> dict:
-        di = self.devices.idx.get(e.device_id, -1)
+        di = self.dev_index.idx.get(e.device_id, -1)
         return {"deviceId": e.device_id, "deviceToken": self._dev_tokens.get(di),
                 "assignmentStatus": "Active", "engine": self.engine_kind}
 
@@ -363,7 +364,7 @@ class GpuInboundApi:
         return d
 
     def get_device_state(self, assignment_id: str) -> dict | None:
-        ai = self._e.assignments.idx.get(assignment_id)
+        ai = self._e.asg_index.idx.get(assignment_id)
         return None if ai is None else self._e.engine.device_state(ai)
 
     def process_payloads(self, payloads: list) -> dict:

@@ -75,6 +75,9 @@ TENANT_TEMPLATES["gpu"] = copy.deepcopy(TENANT_TEMPLATES["default"])
 TENANT_TEMPLATES["gpu"]["name"] = "MI355X-accelerated inbound pipeline"
 TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5,
                                                              "storage": "objects", "publishEnriched": "events"}
+# protobuf payloads go to the engine undecoded, in micro-batches; JSON keeps the per-event path
+TENANT_TEMPLATES["gpu"]["services"]["event-sources"]["sources"][1]["forward"] = "raw"
+TENANT_TEMPLATES["gpu"]["services"]["event-sources"].update(rawBatchSize=65536, rawMaxDelayMs=5)
 # High-throughput MI355X tenant: enriched rows stay columnar end to end (no per-event host objects).
 TENANT_TEMPLATES["gpu-columnar"] = copy.deepcopy(TENANT_TEMPLATES["gpu"])
 TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event store"

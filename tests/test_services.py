@@ -176,8 +176,8 @@ def test_new_tenant_gpu_template_cpu_engine():
         em = inst.api("DeviceEventManagement", "fast")
         run = lambda f: inst.instance.system_user.run(f, "fast")  # noqa: E731
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
-        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None and
-                          ib.assignments.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: ib.dev_index.idx.get(dev.id) is not None and
+                          ib.asg_index.idx.get(dev.device_assignment_id) is not None)
         api = inst.api("InboundProcessing", "fast")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
@@ -209,8 +209,8 @@ def test_gpu_tenant_engine_on_device():
         dm = inst.api("DeviceManagement", "fastgpu")
         em = inst.api("DeviceEventManagement", "fastgpu")
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
-        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None and
-                          ib.assignments.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: ib.dev_index.idx.get(dev.id) is not None and
+                          ib.asg_index.idx.get(dev.device_assignment_id) is not None)
         api = inst.api("InboundProcessing", "fastgpu")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
@@ -285,8 +285,8 @@ def test_columnar_tenant_end_to_end():
         em = inst.api("DeviceEventManagement", "col")
         ib = inst.tenant_engine("inbound-processing", "col")
         dev = run(lambda: dm.get_device_by_token("galaxytab-001"))
-        assert wait_until(lambda: ib.devices.idx.get(dev.id) is not None and
-                          ib.assignments.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: ib.dev_index.idx.get(dev.id) is not None and
+                          ib.asg_index.idx.get(dev.device_assignment_id) is not None)
         topic = inst.instance.naming.tenant_prefix("col") + "inbound-enriched-batches"
         cons = inst.instance.bus.consumer("col-batches", [topic])
         api = inst.api("InboundProcessing", "col")
@@ -316,5 +316,39 @@ def test_columnar_tenant_end_to_end():
         b = decode_batch(got[0].value)
         assert len(b["rows"]) == 51 and "temp" in b["names"].values()
         cons.close()
+    finally:
+        inst.stop()
+
+
+def test_gpu_template_routes_protobuf_raw_and_json_per_event():
+    """gpu template: protobuf payloads reach the fused engine as raw micro-batches (size- or
+    time-flushed); JSON payloads keep the per-event inbound path.  Both end up persisted."""
+    import json as _json
+    inst = SiteWhereInstance().start()
+    try:
+        inst.wait_for_tenant("default", 60)
+        tm = inst.api("TenantManagement")
+        inst.instance.system_user.run(lambda: tm.create_tenant({"token": "mix", "name": "Mixed",
+                                                                "configurationTemplateId": "gpu",
+                                                                "datasetTemplateId": "construction"}))
+        inst.wait_for_tenant("mix", 60)
+        run = lambda f: inst.instance.system_user.run(f, "mix")  # noqa: E731
+        dm = inst.api("DeviceManagement", "mix")
+        em = inst.api("DeviceEventManagement", "mix")
+        ib = inst.tenant_engine("inbound-processing", "mix")
+        es = inst.tenant_engine("event-sources", "mix")
+        dev = run(lambda: dm.get_device_by_token("iphone6s-001"))
+        assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        for i in range(7):                                   # < rawBatchSize: flushed by the timer
+            es.inject("default-protobuf", wire.measurements("iphone6s-001", {"pb": float(i)}))
+        es.inject("default-json", _json.dumps({"deviceToken": "iphone6s-001", "type": "DeviceMeasurement",
+                                               "request": {"name": "js", "value": 9.0}}).encode())
+
+        def names():
+            res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
+                                                             {"pageSize": 0})).results
+            return sorted(m.name for m in res)
+        assert wait_until(lambda: names() == ["js"] + ["pb"] * 7, 20), names()
+        assert ib.engine.stats_dict()["events"] >= 7
     finally:
         inst.stop()
