@@ -258,9 +258,13 @@ def add_index_event_routes(r: APIRouter, index: str, getter):
 
 
 # ------------------------------------------------------------------------------ app
-def create_app(instance, topology=None) -> FastAPI:
+def create_app(instance, topology=None, cors: bool = True) -> FastAPI:
     app = FastAPI(title="SiteWhere (MI355X) REST API", version=VERSION["versionIdentifier"],
                   docs_url=f"{API}/docs", openapi_url=f"{API}/openapi.json")
+    if cors:   # reference RestSecurity/CORS filter: the admin UI is served from another origin
+        from fastapi.middleware.cors import CORSMiddleware
+        app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_methods=["*"], allow_headers=["*"],
+                           expose_headers=[HEADER_JWT, HEADER_ERROR, HEADER_ERROR_CODE])
     web = WebRest(instance, topology)
     app.state.web = web
 
@@ -932,7 +936,7 @@ class WebRestMicroservice(GlobalMicroservice):
         return {"port": 8080}
 
     def microservice_initialize(self, monitor):
-        self.app = create_app(self.instance, self.topology)
+        self.app = create_app(self.instance, self.topology, bool(self.config.get("cors", True)))
 
     def microservice_start(self, monitor):
         port = self.port_override if self.port_override is not None else int(self.config.get("port", 8080))
