@@ -3,12 +3,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
-
-def pow2_at_least(n: int) -> int:
-    p = 1
-    while p < n:
-        p <<= 1
-    return p
+from ..utils import pow2_at_least
 
 
 @dataclass

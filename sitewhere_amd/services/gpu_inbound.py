@@ -36,6 +36,7 @@ from ..pipeline.config import EngineConfig
 from ..pipeline.engine_base import Zone, ZoneTest
 from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
+from ..utils import IndexMap
 from ..runtime.consumers import BusConsumer
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
 from .inbound_processing import InboundProcessingTenantEngine
@@ -54,26 +55,6 @@ def unpack_raw_batch(value: bytes):
     raw = np.zeros(int(offs[-1]) + 64, np.uint8)
     raw[:offs[-1]] = np.frombuffer(value, np.uint8, int(offs[-1]), start)
     return raw, offs
-
-
-class IndexMap:
-    """Stable dense indices for entity ids (device / assignment / customer / area / asset)."""
-
-    def __init__(self):
-        self.idx: dict[str, int] = {}
-        self.ids: list[str] = []
-
-    def get(self, key: str | None) -> int:
-        if key is None:
-            return -1
-        i = self.idx.get(key)
-        if i is None:
-            i = self.idx[key] = len(self.ids)
-            self.ids.append(key)
-        return i
-
-    def id_of(self, i: int) -> str | None:
-        return self.ids[i] if 0 <= i < len(self.ids) else None
 
 
 class GpuInboundTenantEngine(InboundProcessingTenantEngine):
