@@ -159,3 +159,20 @@ def test_graph_replay_matches_direct_launches_and_recaptures_on_zone_change():
         assert canon_out(rg.out, None) == canon_out(rd.out, None)
         assert g.stats_dict() == d.stats_dict()
     assert g._graph is not None
+
+
+def test_store_ring_wraparound_parity():
+    """The HBM event ring wraps (store_cap << events): GPU ring contents and ids match the oracle."""
+    g, c = pair(store_cap=4096)
+    for k in range(5):
+        raw, offs = fleet_batch(1500, seed=900 + k)
+        rg = g.step(raw, offs, NOW + k * 1000, presence=False)
+        rc = c.step(raw, offs, NOW + k * 1000, presence=False)
+        assert rg.first_seq == rc.first_seq
+        assert canon_out(rg.out, None) == canon_out(rc.out, None)
+    assert g.cursor == c.cursor > 4096
+    cg, eg = g.store_rows()
+    cc, ec = c.store_rows()
+    assert len(eg) == 4096 and np.array_equal(eg, ec)
+    for k in ("etype", "asg", "date"):
+        assert sorted(cg[k].tolist()) == sorted(cc[k].tolist()), k
