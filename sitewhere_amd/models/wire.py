@@ -265,3 +265,17 @@ def acknowledge(hardware_id: str, message: str | None = None, originator: str | 
     if message is not None:
         b.message = message
     return encode(SEND_ACKNOWLEDGEMENT, b, originator)
+
+
+def stream_create(hardware_id: str, stream_id: str, content_type: str = "application/octet-stream",
+                  originator: str | None = None) -> bytes:
+    return encode(SEND_DEVICE_STREAM, DeviceStream(hardwareId=hardware_id, streamId=stream_id,
+                                                   contentType=content_type), originator)
+
+
+def stream_data(hardware_id: str, stream_id: str, sequence_number: int, data: bytes,
+                event_date: int | None = None, originator: str | None = None) -> bytes:
+    b = DeviceStreamData(hardwareId=hardware_id, streamId=stream_id, sequenceNumber=sequence_number, data=data)
+    if event_date is not None:
+        b.eventDate = event_date
+    return encode(SEND_DEVICE_STREAM_DATA, b, originator)

@@ -109,6 +109,7 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
                 req = p["eventCreateRequest"]
                 fn = _ADDERS.get(req["type"])
                 if fn is None:
+                    self._route_stream(p, a)
                     continue
                 key = (a.id, fn)
                 if key not in groups:
@@ -139,6 +140,22 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
             self.ms.producer.send(self.t_unregistered, token, json.dumps(codec.to_wire(p)).encode())
             return None
         return a
+
+    def _route_stream(self, p: dict, a):
+        """Device stream requests go to streaming media (reference IInboundEventProcessor
+        onDeviceStreamCreateRequest / onDeviceStreamDataCreateRequest)."""
+        req = p["eventCreateRequest"]
+        t = req["type"]
+        if t not in ("DeviceStream", "DeviceStreamData"):
+            return
+        sm = self.ms.api("StreamingMedia", self.tenant.token)
+        r = req["request"]
+        if t == "DeviceStream":
+            sm.handle_device_stream_request(p["deviceToken"], r)
+        else:
+            data = r.get("data") or b""
+            sm.add_device_stream_data(a.id, r["streamId"], int(r.get("sequenceNumber", 0)),
+                                      data if isinstance(data, bytes) else bytes(data), r.get("eventDate"))
 
     def process_payload(self, p: dict, em=None):
         a = self._validate(p)

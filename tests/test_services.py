@@ -352,3 +352,16 @@ def test_gpu_template_routes_protobuf_raw_and_json_per_event():
         assert ib.engine.stats_dict()["events"] >= 7
     finally:
         inst.stop()
+
+
+def test_device_stream_over_the_wire(sw):
+    """Stream create + out-of-order chunks sent as protobuf device messages reach streaming media."""
+    es = sw.tenant_engine("event-sources")
+    dm = sw.api("DeviceManagement", "default")
+    sm = sw.api("StreamingMedia", "default")
+    dev = as_system(sw, lambda: dm.get_device_by_token("openhab-003"))
+    es.inject("default-protobuf", wire.stream_create("openhab-003", "mic", "audio/wav"))
+    assert wait_until(lambda: as_system(sw, lambda: dm.get_device_stream_by_stream_id(dev.device_assignment_id, "mic")))
+    es.inject("default-protobuf", wire.stream_data("openhab-003", "mic", 2, b"-two"))
+    es.inject("default-protobuf", wire.stream_data("openhab-003", "mic", 1, b"one"))
+    assert wait_until(lambda: as_system(sw, lambda: sm.get_stream_content(dev.device_assignment_id, "mic")) == b"one-two")
