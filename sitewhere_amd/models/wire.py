@@ -211,6 +211,17 @@ def encode_device_command(command: int, body, originator: str | None = None, nes
     return delimited(h) + delimited(body)
 
 
+def decode_device_command(payload: bytes):
+    """Device-side decode of a system downlink -> (command, nested path or None, body message)."""
+    h, pos = read_delimited(payload, 0, DeviceHeader)
+    cls = {ACK_REGISTRATION: RegistrationAck, ACK_DEVICE_STREAM: DeviceStreamAck,
+           RECEIVE_DEVICE_STREAM_DATA: DeviceStreamData}.get(h.command)
+    if cls is None:
+        raise ValueError(f"unknown downlink command {h.command}")
+    body, _ = read_delimited(payload, pos, cls)
+    return h.command, (h.nestedPath if h.HasField("nestedPath") else None), body
+
+
 # convenience builders -----------------------------------------------------------
 def measurements(hardware_id: str, values: dict, event_date: int | None = None, alternate_id: str | None = None,
                  metadata: dict | None = None, update_state: bool | None = None, originator: str | None = None) -> bytes:
@@ -279,3 +290,9 @@ def stream_data(hardware_id: str, stream_id: str, sequence_number: int, data: by
     if event_date is not None:
         b.eventDate = event_date
     return encode(SEND_DEVICE_STREAM_DATA, b, originator)
+
+
+def stream_data_request(hardware_id: str, stream_id: str, sequence_number: int,
+                        originator: str | None = None) -> bytes:
+    return encode(REQUEST_DEVICE_STREAM_DATA, DeviceStreamDataRequest(hardwareId=hardware_id, streamId=stream_id,
+                                                                      sequenceNumber=sequence_number), originator)

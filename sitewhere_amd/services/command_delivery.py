@@ -10,6 +10,7 @@ Twilio SMS), routers (single-choice, device-type mapping, Groovy, no-op); failur
 """
 from __future__ import annotations
 
+import base64
 import json
 import threading
 
@@ -78,7 +79,8 @@ class JsonEncoder:
                            "assignmentId": assignment.id if assignment else None}).encode()
 
     def encode_system(self, command: dict, nesting) -> bytes:
-        return json.dumps({"systemCommand": command, "nestedPath": nesting.get("path")}).encode()
+        cmd = {k: ({"base64": base64.b64encode(v).decode()} if isinstance(v, bytes) else v) for k, v in command.items()}
+        return json.dumps({"systemCommand": cmd, "nestedPath": nesting.get("path")}).encode()
 
 
 class ProtobufEncoder:
@@ -100,6 +102,16 @@ class ProtobufEncoder:
                 ack.errorType = {"INVALID_SPECIFICATION": 1, "SITE_TOKEN_REQUIRED": 2,
                                  "NEW_DEVICES_NOT_ALLOWED": 3}[command["errorType"]]
             return wire.encode_device_command(wire.ACK_REGISTRATION, ack, nested_path=nesting.get("path"))
+        if command.get("type") == "DeviceStreamAck":
+            st = {"STREAM_CREATED": 1, "STREAM_EXISTS": 2, "STREAM_FAILED": 3}[command["state"]]
+            return wire.encode_device_command(wire.ACK_DEVICE_STREAM,
+                                              wire.DeviceStreamAck(streamId=command["streamId"], state=st),
+                                              nested_path=nesting.get("path"))
+        if command.get("type") == "DeviceStreamData":
+            # reference Device.proto RECEIVE_DEVICE_STREAM_DATA carries the Model.DeviceStreamData chunk
+            body = wire.DeviceStreamData(hardwareId=nesting["gateway"].token, streamId=command["streamId"],
+                                         sequenceNumber=command["sequenceNumber"], data=command.get("data") or b"")
+            return wire.encode_device_command(wire.RECEIVE_DEVICE_STREAM_DATA, body, nested_path=nesting.get("path"))
         return JsonEncoder().encode_system(command, nesting)
 
 

@@ -146,16 +146,30 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
         onDeviceStreamCreateRequest / onDeviceStreamDataCreateRequest)."""
         req = p["eventCreateRequest"]
         t = req["type"]
-        if t not in ("DeviceStream", "DeviceStreamData"):
+        if t not in ("DeviceStream", "DeviceStreamData", "SendDeviceStreamData"):
             return
         sm = self.ms.api("StreamingMedia", self.tenant.token)
         r = req["request"]
         if t == "DeviceStream":
-            sm.handle_device_stream_request(p["deviceToken"], r)
+            ack = sm.handle_device_stream_request(p["deviceToken"], r)
+            self._system_command(p["deviceToken"], {"type": "DeviceStreamAck", **ack})
+        elif t == "SendDeviceStreamData":
+            # device asks for a chunk: answer with a system command carrying the stored bytes
+            chunk = sm.get_device_stream_data(a.id, r["streamId"], int(r.get("sequenceNumber", 0)))
+            self._system_command(p["deviceToken"], {
+                "type": "DeviceStreamData", "streamId": r["streamId"],
+                "sequenceNumber": int(r.get("sequenceNumber", 0)),
+                "data": chunk.data if chunk is not None else b""})
         else:
             data = r.get("data") or b""
             sm.add_device_stream_data(a.id, r["streamId"], int(r.get("sequenceNumber", 0)),
                                       data if isinstance(data, bytes) else bytes(data), r.get("eventDate"))
+
+    def _system_command(self, device_token: str, command: dict):
+        try:
+            self.ms.api("CommandDelivery", self.tenant.token, wait_s=1.0).deliver_system_command(device_token, command)
+        except Exception:
+            self.logger.warning("system command %s to %s not delivered", command.get("type"), device_token)
 
     def process_payload(self, p: dict, em=None):
         a = self._validate(p)

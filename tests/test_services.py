@@ -6,6 +6,8 @@ connectors, registration of unknown devices, command delivery, batch operations,
 """
 from __future__ import annotations
 
+import base64
+import json
 import time
 
 import pytest
@@ -365,3 +367,29 @@ def test_device_stream_over_the_wire(sw):
     es.inject("default-protobuf", wire.stream_data("openhab-003", "mic", 2, b"-two"))
     es.inject("default-protobuf", wire.stream_data("openhab-003", "mic", 1, b"one"))
     assert wait_until(lambda: as_system(sw, lambda: sm.get_stream_content(dev.device_assignment_id, "mic")) == b"one-two")
+    # the device requests chunk 2 back: delivered as a system command through command delivery
+    prov = sw.tenant_engine("command-delivery").destinations["default"].provider
+    es.inject("default-protobuf", wire.stream_data_request("openhab-003", "mic", 2))
+
+    def _chunk(p):
+        body = json.loads(p[2]).get("systemCommand", {})
+        return base64.b64decode(body["data"]["base64"]) if body.get("type") == "DeviceStreamData" else None
+    assert wait_until(lambda: any(_chunk(p) == b"-two" for p in prov.delivered))
+
+
+def test_protobuf_system_command_downlinks():
+    """Stream acks / chunks use the typed Device.proto downlinks (ACK_DEVICE_STREAM, RECEIVE_DEVICE_STREAM_DATA)."""
+    from types import SimpleNamespace
+
+    from sitewhere_amd.services.command_delivery import ProtobufEncoder
+    enc = ProtobufEncoder()
+    nest = {"gateway": SimpleNamespace(token="gw-1"), "path": "bus/sensor"}
+    cmd, path, body = wire.decode_device_command(
+        enc.encode_system({"type": "DeviceStreamAck", "streamId": "mic", "state": "STREAM_EXISTS"}, nest))
+    assert (cmd, path, body.streamId, body.state) == (wire.ACK_DEVICE_STREAM, "bus/sensor", "mic", 2)
+    cmd, path, body = wire.decode_device_command(
+        enc.encode_system({"type": "DeviceStreamData", "streamId": "mic", "sequenceNumber": 7, "data": b"\x00\x01"}, nest))
+    assert cmd == wire.RECEIVE_DEVICE_STREAM_DATA and body.hardwareId == "gw-1"
+    assert (body.streamId, body.sequenceNumber, body.data) == ("mic", 7, b"\x00\x01")
+    cmd, _, body = wire.decode_device_command(enc.encode_system({"type": "RegistrationAck", "state": "NEW_REGISTRATION"}, {}))
+    assert cmd == wire.ACK_REGISTRATION and body.state == 1
