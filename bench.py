@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--zones", type=int, default=16)
     ap.add_argument("--store", type=int, default=1 << 27, help="HBM event-store capacity per GPU (events)")
     ap.add_argument("--engine", choices=["gpu", "cpu"], default="gpu")
+    ap.add_argument("--framing", choices=["varint", "offsets"], default="varint",
+                    help="raw-batch framing on the wire to the GPU (varint lengths or u32 offsets)")
     ap.add_argument("--no-outbound", action="store_true", help="(diagnostic) skip the D2H outbound copy")
     return ap.parse_args()
 
@@ -70,6 +72,7 @@ def main():
     rank, local, world, _ = init_distributed(use_gpu)
     from sitewhere_amd.pipeline.config import EngineConfig
     from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads, gen_tokens, fingerprints
+    from sitewhere_amd.pipeline.framing import varint_lengths
 
     n_total_dev = args.devices * world
     spec = FleetSpec(prefix="dev-", n_devices=n_total_dev, p_location=0.25, p_alert=0.05, p_unregistered=0.0,
@@ -108,10 +111,12 @@ def main():
         raw, offs_b = gen_payloads(spec, args.msgs, now0 - 30_000, seed=1 + rank * 1000 + b)
         raw = np.concatenate([raw, np.zeros(64, np.uint8)])
         if use_gpu:
+            # wire framing: payload bytes + a varint length per payload (offsets are rebuilt on the GPU)
+            lens = varint_lengths(offs_b) if args.framing == "varint" else None
             batches.append((torch.from_numpy(raw).pin_memory(), torch.from_numpy(offs_b.view(np.int32)).pin_memory(),
-                            raw, offs_b))
+                            raw, offs_b, None if lens is None else torch.from_numpy(lens).pin_memory()))
         else:
-            batches.append((None, None, raw, offs_b))
+            batches.append((None, None, raw, offs_b, None))
     setup_s = time.time() - t0
     max_raw = max(int(b[2].size) for b in batches)
 
@@ -125,14 +130,18 @@ def main():
         runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound)
 
         def run(k):
-            rh, oh, _, o = batches[k % len(batches)]
-            runner.submit(rh, oh, len(o) - 1, now_ms=now0 + k, presence=True)
+            rh, oh, r, o, lh = batches[k % len(batches)]
+            if lh is not None:
+                runner.submit(rh, None, len(o) - 1, now_ms=now0 + k, presence=True, lens_host=lh,
+                              raw_bytes=int(o[-1]))
+            else:
+                runner.submit(rh, oh, len(o) - 1, now_ms=now0 + k, presence=True)
 
         def finish():
             runner.flush()
     else:
         def run(k):
-            _, _, r, o = batches[k % len(batches)]
+            _, _, r, o, _ = batches[k % len(batches)]
             eng.step(r, o, now0 + k, presence=True)
 
         def finish():
@@ -190,11 +199,14 @@ def main():
                 "tenants": 1,
                 "zones": args.zones,
                 "engine": args.engine,
+                "framing": args.framing,
             },
             "detail": {
                 "events": ev, "persisted": persisted, "payloads": msgs, "rule_alerts": rule_alerts,
                 "persisted_per_sec": round(persisted / elapsed, 1),
                 "payload_bytes_per_gpu_step": int(max_raw), "setup_s": round(setup_s, 1),
+                "h2d_bytes_per_gpu_step": int(max_raw) + int(max(
+                    (b[4].numel() if b[4] is not None else 4 * len(b[3])) for b in batches)),
                 "registered_devices_rank0": n_dev,
             },
         }

@@ -170,6 +170,15 @@ typedef struct SwEngineArgs {
   uint64_t* stats;             // [16] cumulative counters (see SW_STAT_*)
   // ---------------------------------------------------------------- per-step params (device)
   SwStepParams* sp;
+  // ---------------------------------------------------------------- shuffle spill (world > 1)
+  // Records that did not fit their destination slab are not dropped: they are written (in
+  // deterministic destination/position order) to `spill` and sent first by the next partition,
+  // which reads them back as `carry`.  Only records beyond carry_cap are dropped (counted).
+  const SwEventRec* carry;
+  const uint32_t* n_carry;
+  SwEventRec* spill;
+  uint32_t* n_spill;
+  int64_t carry_cap;
 } SwEngineArgs;
 
 enum {
@@ -186,5 +195,6 @@ enum {
   SW_STAT_SHUFFLE_OVERFLOW = 10,
   SW_STAT_NEW_NAMES = 11,
   SW_STAT_STATE_OVERFLOW = 12,
+  SW_STAT_SHUFFLE_DEFERRED = 13,   // records spilled to the next step's exchange
   SW_STAT_N = 16,
 };

@@ -65,6 +65,7 @@ ZONE_TEST = np.dtype([("zone", "<i4"), ("condition", "<i4"), ("alert_name_id", "
 STAT_NAMES = [
     "messages", "events", "persisted", "unregistered", "unassigned", "duplicates", "decode_errors",
     "control", "rule_alerts", "presence_events", "shuffle_overflow", "new_names", "state_overflow",
+    "shuffle_deferred",
 ]
 
 # Alert levels (GAlertLevel) and sources.

@@ -50,6 +50,8 @@ FIELDS = [
     ("stats", P),
     # per-step params (device SwStepParams, written in-stream each step)
     ("sp", P),
+    # shuffle spill (records deferred to the next step's exchange)
+    ("carry", P), ("n_carry", P), ("spill", P), ("n_spill", P), ("carry_cap", I),
 ]
 
 

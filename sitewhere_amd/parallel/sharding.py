@@ -14,9 +14,17 @@ registry to every consumer.  MI355X form:
   producing to the key's partition).  Control records (registration, acks, streams) stay on the
   receiving rank, whose host owns their raw bytes.
 * **slab sizing** -- fixed-size slabs keep the exchange free of host synchronisation: capacity per
-  destination = ``shuffle_slack * rec_cap / world + 1024`` (``EngineConfig.shuf_cap``); a uniform
-  key hash puts ~rec_cap/world records per destination, so 1.25x leaves > 25 sigma of headroom at
-  1M records/step; overflow is counted in the ``overflow`` scalar, never silent.
+  destination = ``shuffle_slack * rec_cap / world + 1024`` (``EngineConfig.shuf_cap``, slack 1.1).
+  A uniform key hash puts ~rec_cap/world records per destination (sigma ~ sqrt of that, so 1.1x
+  is > 30 sigma at 1M records/step).  Skewed keys cannot lose records: whatever does not fit a slab
+  is *spilled* in deterministic order and sent first by the next step's exchange (``carry``);
+  only records beyond ``carry_cap`` are dropped, counted in ``shuffle_overflow``.  Slack is kept
+  small because xGMI is point-to-point: at N=2 every slab byte crosses one link.
+* **pipelined exchange** -- ``GpuInboundEngine.round_async`` software-pipelines the step across
+  two streams: the compute stream runs decode+partition of batch k and then unpack+process of
+  batch k-1, while the all-to-all of batch k runs on a communication stream, overlapped with the
+  process phase of batch k-1 (double-buffered send slabs; one receive buffer, released by unpack).
+  A step then costs max(H2D, compute, exchange) instead of compute + exchange.
 """
 from __future__ import annotations
 

@@ -24,7 +24,9 @@ class EngineConfig:
     name_slots: int = 1 << 16        # distinct measurement names / alert types
     state_slots: int = 0             # (assignment, name) state map slots (0 = 16 * max_assignments)
     names_cap: int = 4096            # new-name reports per step
-    shuffle_slack: float = 1.25      # per-destination slab = slack * rec_cap / world
+    shuffle_slack: float = 1.1       # per-destination slab = slack * rec_cap / world (+1024)
+    shuffle_pad: int = 1024          # records added to every slab (small-batch headroom)
+    carry_cap: int = 0               # records a full slab can defer to the next exchange (0 = rec_cap)
     presence_missing_ms: int = 8 * 3600 * 1000   # DevicePresenceManager default (8h)
     presence_check_ms: int = 10 * 60 * 1000      # DevicePresenceManager default (10 min)
     rank: int = 0
@@ -40,7 +42,9 @@ class EngineConfig:
         self.dedup_slots = pow2_at_least(self.dedup_slots)
         self.name_slots = pow2_at_least(self.name_slots)
         self.state_slots = pow2_at_least(self.state_slots)
-        self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + 1024
+        self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + self.shuffle_pad
+        if self.carry_cap <= 0:
+            self.carry_cap = self.rec_cap
 
     @classmethod
     def small(cls, **kw):

@@ -45,6 +45,7 @@ class CpuInboundEngine(EngineBase):
         super().__init__(cfg)
         self.group = group
         self.exchange = None
+        self.carry = np.zeros(0, EVENT_REC)    # records deferred to the next exchange (full slabs)
         self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
         self.cursor = 0
         self.seq_base = 0
@@ -60,17 +61,27 @@ class CpuInboundEngine(EngineBase):
 
     # ------------------------------------------------------------------ stages
     def partition(self, recs: np.ndarray):
-        """Stable owner partition into [world, shuf_cap] slabs (same as k_part_count/k_part_write)."""
+        """Stable owner partition into [world, shuf_cap] slabs (same as k_part_count/k_part_write).
+
+        The input is the previous partition's carry followed by ``recs``; records beyond a slab are
+        spilled destination-major into the next carry (up to ``carry_cap``, the rest dropped)."""
+        recs = np.concatenate([self.carry, recs]) if len(self.carry) else recs
         owner = np.where(recs["etype"] >= 16, self.rank, (recs["fp_hi"] >> np.uint64(32)) % np.uint64(self.world))
         cap = self.cfg.shuf_cap
         send = np.zeros((self.world, cap), EVENT_REC)
         cnt = np.zeros(self.world, np.int64)
+        spill = []
         for o in range(self.world):
             sel = recs[owner == o]
             k = min(len(sel), cap)
-            self.stats[10] += len(sel) - k
             send[o, :k] = sel[:k]
             cnt[o] = k
+            spill.append(sel[k:])
+        spill = np.concatenate(spill)
+        kept = min(len(spill), self.cfg.carry_cap)
+        self.stats[13] += kept
+        self.stats[10] += len(spill) - kept
+        self.carry = spill[:kept].copy()
         return send, cnt
 
     @staticmethod

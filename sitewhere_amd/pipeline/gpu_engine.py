@@ -77,7 +77,8 @@ class GpuInboundEngine(EngineBase):
         tile = 1024
         ntiles = (c.rec_cap + tile - 1) // tile
         mtiles = (c.max_msgs + tile - 1) // tile
-        scan_tmp = max(ntiles * 2 * max(1, c.world), mtiles, 2 * ntiles) + 64
+        ptiles = (c.carry_cap + c.rec_cap + tile - 1) // tile     # partition input: carry + records
+        scan_tmp = max(ptiles * 2 * max(1, c.world), mtiles, 2 * ntiles) + 64
         self.t = t = {}
         # decode
         t["msg_cnt"] = z(c.max_msgs + 1, i32)
@@ -86,15 +87,20 @@ class GpuInboundEngine(EngineBase):
         t["recs"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
         t["seen_key"] = z(c.name_slots, i64)
         t["new_names"] = z(c.names_cap * NAME_REF.itemsize, u8)
+        t["vlen_tmp"] = z(2 * ((5 * c.max_msgs + tile - 1) // tile) + 64, i32)   # varint framing scan
         t["scalars"] = z(64, i32)  # n_recs, n_new_names, overflow, n_work, n_ok, n_rej, n_gen, n_out, n_rule
         # shuffle
         if c.world > 1:
-            t["send"] = z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8)
+            # send slabs are double-buffered (the pipelined exchange of batch k reads one while batch
+            # k+1 is partitioned into the other); carry/spill alternate roles every partition
+            self.send_bufs = [z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8) for _ in range(2)]
+            self.send_cnts = [z(c.world, i32) for _ in range(2)]
             t["recv"] = z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8)
-            t["send_cnt"] = z(c.world, i32)
             t["recv_cnt"] = z(c.world, i32)
-            t["part_tmp"] = z(2 * c.world * ntiles + 64, i32)
+            t["part_tmp"] = z(2 * c.world * ptiles + 64, i32)
             t["work"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
+            self.carry_bufs = [z(c.carry_cap * EVENT_REC.itemsize, u8) for _ in range(2)]
+            t["n_carry"] = z(2, i32)
         # validated
         t["status"] = z(c.rec_cap, u8)
         t["ev_dev"] = z(c.rec_cap, i32)
@@ -154,10 +160,10 @@ class GpuInboundEngine(EngineBase):
         a.new_names, a.n_new_names, a.names_cap = _ptr(t["new_names"]), S(1), c.names_cap
         a.overflow = S(2)
         if c.world > 1:
-            a.send, a.recv, a.shuf_cap = _ptr(t["send"]), _ptr(t["recv"]), c.shuf_cap
-            a.send_cnt, a.recv_cnt = _ptr(t["send_cnt"]), _ptr(t["recv_cnt"])
+            a.recv, a.shuf_cap, a.recv_cnt = _ptr(t["recv"]), c.shuf_cap, _ptr(t["recv_cnt"])
             a.part_tmp, a.part_tmp_len = _ptr(t["part_tmp"]), t["part_tmp"].numel() // 2
             a.work = _ptr(t["work"])
+            a.carry_cap = c.carry_cap
         else:
             a.work = a.recs
         a.n_work = S(3)
@@ -193,6 +199,17 @@ class GpuInboundEngine(EngineBase):
         self._graph = None
         self._cap_stream = torch.cuda.Stream(self.device) if self.use_graph else None
         self._out_sel = 0
+        # multi-rank exchange state: parity of the send slabs / carry buffer the next partition uses
+        self._send_par = 0
+        self._carry_par = 0
+        self._last_send_par = 0
+        # pipelined exchange (round_async): the batch whose exchange is in flight, and its events
+        self._pend = None
+        self._comm = torch.cuda.Stream(self.device) if c.world > 1 else None
+        self._ev_part = torch.cuda.Event()
+        self._ev_unp = torch.cuda.Event()
+        self._ev_x = torch.cuda.Event()
+        self._graph_nu = None                  # process graph without unpack (pipelined rounds)
         self._apply_zone_ptrs()
 
     # ------------------------------------------------------------------ control-plane hooks
@@ -249,10 +266,11 @@ class GpuInboundEngine(EngineBase):
             self._drop_graph()
 
     def _drop_graph(self):
-        if getattr(self, "_graph", None) is not None:
-            torch.cuda.synchronize(self.device)
-            self.lib.sw_graph_destroy(ctypes.c_void_p(self._graph))
-            self._graph = None
+        for attr in ("_graph", "_graph_nu"):
+            if getattr(self, attr, None) is not None:
+                torch.cuda.synchronize(self.device)
+                self.lib.sw_graph_destroy(ctypes.c_void_p(getattr(self, attr)))
+                setattr(self, attr, None)
 
     # ------------------------------------------------------------------ data plane
     def step_async(self, raw_dev: torch.Tensor, off_dev: torch.Tensor, n_msgs: int, now_ms: int,
@@ -266,16 +284,25 @@ class GpuInboundEngine(EngineBase):
         return sel
 
     def prepare(self, raw_dev, off_dev, n_msgs, now_ms, presence=False, out_sel=None, out_to_device=False):
+        self._set_batch(raw_dev, off_dev, n_msgs, now_ms)
+        return self._set_step_params(now_ms, presence, out_sel, out_to_device)
+
+    def _set_batch(self, raw_dev, off_dev, n_msgs, now_ms):
+        """By-value decode arguments of the next decode phase."""
         if n_msgs > self.cfg.max_msgs:
             raise ValueError(f"batch of {n_msgs} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
         a = self.args
         a.raw, a.msg_off, a.n_msgs, a.now_ms = _ptr(raw_dev), _ptr(off_dev), int(n_msgs), int(now_ms)
+
+    def _set_step_params(self, now_ms, presence=False, out_sel=None, out_to_device=False):
+        """Stream-ordered SwStepParams of the next process phase (receive time, batch, presence, rows)."""
+        a = self.args
         a.batch_seq = self.batch_seq
         a.presence_missing_ms = self.cfg.presence_missing_ms if presence else 0
         sel = self._out_sel if out_sel is None else out_sel
         self._last_sel = sel
         a.out = _ptr(self.out_dev[sel]) if out_to_device else self.out_host[sel].dev
-        rc = self.lib.sw_set_step_params(ctypes.c_void_p(a.sp), a.now_ms, a.batch_seq, a.presence_missing_ms,
+        rc = self.lib.sw_set_step_params(ctypes.c_void_p(a.sp), int(now_ms), a.batch_seq, a.presence_missing_ms,
                                          ctypes.c_void_p(a.out), self._stream())
         if rc:
             raise RuntimeError(f"sw_set_step_params failed ({rc})")
@@ -286,52 +313,137 @@ class GpuInboundEngine(EngineBase):
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def frame_varint(self, lens_dev: torch.Tensor, nbytes: int, n_msgs: int, off_dev: torch.Tensor, raw_bytes: int):
+        """Rebuild u32 payload offsets from the varint length stream on the current stream."""
+        if n_msgs > self.cfg.max_msgs or nbytes > lens_dev.numel() or off_dev.numel() < n_msgs + 1:
+            raise ValueError("varint framing buffers too small for this batch")
+        rc = self.lib.sw_frame_varint(ctypes.c_void_p(_ptr(lens_dev)), int(nbytes), int(n_msgs),
+                                      ctypes.c_void_p(_ptr(off_dev)), int(raw_bytes),
+                                      ctypes.c_void_p(_ptr(self.t["vlen_tmp"])), self.t["vlen_tmp"].numel(),
+                                      self._stream())
+        if rc:
+            raise RuntimeError(f"sw_frame_varint failed ({rc})")
+
     def phase_decode(self):
         ap = ctypes.byref(self.args)
         rc = self.lib.sw_phase_decode(ap, self._stream())
         if rc:
             raise RuntimeError(f"sw_phase_decode failed ({rc})")
         if self.world > 1:
+            a = self.args
+            sp, cp = self._send_par, self._carry_par
+            a.send, a.send_cnt = _ptr(self.send_bufs[sp]), _ptr(self.send_cnts[sp])
+            a.carry, a.n_carry = _ptr(self.carry_bufs[cp]), _ptr(self.t["n_carry"]) + 4 * cp
+            a.spill, a.n_spill = _ptr(self.carry_bufs[1 - cp]), _ptr(self.t["n_carry"]) + 4 * (1 - cp)
             rc = self.lib.sw_phase_partition(ap, self._stream())
             if rc:
                 raise RuntimeError(f"sw_phase_partition failed ({rc})")
+            self._last_send_par = sp
+            self._send_par, self._carry_par = 1 - sp, 1 - cp
 
     def phase_exchange(self):
         """RCCL all-to-all re-keying of the per-owner slabs (the Kafka key-partitioning analogue)."""
         from ..parallel.sharding import exchange_slabs
-        exchange_slabs(self.t["send_cnt"], self.t["recv_cnt"], self.t["send"], self.t["recv"], self.group)
+        p = self._last_send_par
+        exchange_slabs(self.send_cnts[p], self.t["recv_cnt"], self.send_bufs[p], self.t["recv"], self.group)
 
-    def phase_process(self):
+    def phase_unpack(self):
+        rc = self.lib.sw_phase_unpack(ctypes.byref(self.args), self._stream())
+        if rc:
+            raise RuntimeError(f"sw_phase_unpack failed ({rc})")
+
+    def _capture(self, with_unpack: bool):
+        ex = ctypes.c_void_p()
+        rc = self.lib.sw_graph_capture_process(ctypes.byref(self.args), ctypes.c_void_p(self._rule_scratch),
+                                               int(with_unpack), ctypes.c_void_p(self._cap_stream.cuda_stream),
+                                               ctypes.byref(ex))
+        if rc:
+            import warnings
+            warnings.warn(f"hipGraph capture of the process phase failed ({rc}); using direct launches")
+            self.use_graph = False
+            return None
+        return ex.value
+
+    def phase_process(self, with_unpack: bool | None = None):
+        """Process phase of the batch in ``work`` (unpacked from the receive slabs first when world > 1,
+        unless the caller already ran :meth:`phase_unpack`)."""
+        unpack = self.world > 1 if with_unpack is None else with_unpack
         ap = ctypes.byref(self.args)
         if self.use_graph:
-            if self._graph is None:
-                ex = ctypes.c_void_p()
-                rc = self.lib.sw_graph_capture_process(ap, ctypes.c_void_p(self._rule_scratch), int(self.world > 1),
-                                                       ctypes.c_void_p(self._cap_stream.cuda_stream), ctypes.byref(ex))
-                if rc:
-                    import warnings
-                    warnings.warn(f"hipGraph capture of the process phase failed ({rc}); using direct launches")
-                    self.use_graph = False
-                else:
-                    self._graph = ex.value
-            if self._graph is not None:
-                rc = self.lib.sw_graph_launch(ctypes.c_void_p(self._graph), self._stream())
+            attr = "_graph" if unpack or self.world == 1 else "_graph_nu"
+            if getattr(self, attr) is None:
+                setattr(self, attr, self._capture(unpack))
+            g = getattr(self, attr)
+            if g is not None:
+                rc = self.lib.sw_graph_launch(ctypes.c_void_p(g), self._stream())
                 if rc:
                     raise RuntimeError(f"sw_graph_launch failed ({rc})")
                 self.batch_seq += 1
                 return
-        if self.world > 1:
-            rc = self.lib.sw_phase_unpack(ap, self._stream())
-            if rc:
-                raise RuntimeError(f"sw_phase_unpack failed ({rc})")
+        if unpack:
+            self.phase_unpack()
         rc = self.lib.sw_phase_process(ap, ctypes.c_void_p(self._rule_scratch), self._stream())
         if rc:
             raise RuntimeError(f"sw_phase_process failed ({rc})")
         self.batch_seq += 1
 
+    # ------------------------------------------------------------------ pipelined exchange (world > 1)
+    def round_async(self, raw_dev=None, off_dev=None, n_msgs: int = 0, now_ms: int = 0, presence: bool = False,
+                    out_sel: int | None = None, out_to_device: bool = False, exchange: bool = True):
+        """One round of the software-pipelined multi-rank step (see ``parallel/sharding.py``).
+
+        On the current (compute) stream: decode + partition of the new batch (if ``raw_dev`` is given),
+        then unpack + process of the previous batch, whose all-to-all ran on the communication stream
+        meanwhile.  Then the all-to-all of the new batch is enqueued on the communication stream; it
+        overlaps this round's process phase.  ``out_sel`` names the outbound buffer of the rows this
+        round produces.  Returns True when a batch was processed (False on the first round).
+        ``exchange=False`` leaves the exchange to the caller (loopback tests), who then calls
+        :meth:`exchange_done` on the stream that performed it.
+        """
+        if self.world == 1:
+            raise RuntimeError("round_async is the multi-rank pipeline; use step_async for world == 1")
+        cur = torch.cuda.current_stream(self.device)
+        new = None
+        if raw_dev is not None:
+            self._set_batch(raw_dev, off_dev, n_msgs, now_ms)
+            self.phase_decode()
+            self._ev_part.record(cur)
+            new = (int(now_ms), bool(presence))
+        processed = False
+        if self._pend is not None:
+            p_now, p_presence = self._pend
+            cur.wait_event(self._ev_x)
+            self._set_step_params(p_now, p_presence, out_sel, out_to_device)
+            self.phase_unpack()
+            self._ev_unp.record(cur)
+            self.phase_process(with_unpack=False)
+            processed = True
+        self._pend = new
+        if new is not None and exchange:
+            comm = self._comm
+            comm.wait_event(self._ev_part)
+            if processed:
+                comm.wait_event(self._ev_unp)      # the single receive buffer is free once unpacked
+            with torch.cuda.stream(comm):
+                self.phase_exchange()
+                self._ev_x.record(comm)
+        return processed
+
+    def exchange_done(self, stream=None):
+        """Mark the pending batch's exchange complete at this point of ``stream`` (manual exchange)."""
+        self._ev_x.record(stream or torch.cuda.current_stream(self.device))
+
+    @property
+    def exchange_pending(self) -> bool:
+        return self._pend is not None
+
     def send_slab(self, q: int) -> torch.Tensor:
+        """Destination-q slab of the most recent partition."""
         n = self.cfg.shuf_cap * EVENT_REC.itemsize
-        return self.t["send"][q * n:(q + 1) * n]
+        return self.send_bufs[self._last_send_par][q * n:(q + 1) * n]
+
+    def send_count(self, q: int) -> torch.Tensor:
+        return self.send_cnts[self._last_send_par][q]
 
     def recv_slab(self, q: int) -> torch.Tensor:
         n = self.cfg.shuf_cap * EVENT_REC.itemsize
@@ -444,6 +556,10 @@ class PipelinedRunner:
       - ``"sdma"``: same schedule through ``hipMemcpyAsync`` on a third stream
       - ``"push"``: ``k_push_out`` stores rows into mapped host memory from a side stream
       - ``"direct"``: the persist kernel stores rows straight into mapped host memory
+    * world > 1: each submit is one :meth:`GpuInboundEngine.round_async` (decode batch k, process
+      batch k-1, all-to-all of batch k on a communication stream overlapped with that process
+      phase); rows of a round belong to the previous batch and :meth:`flush` runs the last round.
+      ``SW_PIPELINE_EXCHANGE=0`` falls back to the serial decode -> exchange -> process step.
     """
 
     def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
@@ -460,6 +576,7 @@ class PipelinedRunner:
         nb = self.nbuf = max(2, min(int(os.environ.get("SW_PIPELINE_BUFFERS", nbuf)), engine.n_out_bufs))
         self.raw = [torch.empty(max_raw_bytes + _ALIGN, dtype=torch.uint8, device=dev) for _ in range(nb)]
         self.off = [torch.empty(engine.cfg.max_msgs + 1, dtype=torch.int32, device=dev) for _ in range(nb)]
+        self.lens = [torch.empty(5 * engine.cfg.max_msgs + 64, dtype=torch.uint8, device=dev) for _ in range(nb)]
         self.nout = [torch.zeros(4, dtype=torch.int32, device=dev) for _ in range(nb)]
         self.scal_host = torch.zeros(nb, 16, dtype=torch.int32, pin_memory=True)
         self.ev_h2d = [torch.cuda.Event() for _ in range(nb)]
@@ -471,27 +588,53 @@ class PipelinedRunner:
         self.delivered = 0
         self.pending = None
         self.copying = None          # sdma mode: (buffer, n_out) whose D2H copy is in flight
+        self.rounds = engine.world > 1 and os.environ.get("SW_PIPELINE_EXCHANGE", "1") != "0"
+        self.produced = [False] * nb  # rounds mode: did the round in slot b process a batch
 
-    def submit(self, raw_host: torch.Tensor, off_host: torch.Tensor, n_msgs: int, now_ms: int | None = None,
-               presence: bool = False):
+    def submit(self, raw_host: torch.Tensor | None, off_host: torch.Tensor | None, n_msgs: int,
+               now_ms: int | None = None, presence: bool = False, lens_host: torch.Tensor | None = None,
+               raw_bytes: int | None = None):
+        """Enqueue one batch (``raw_host=None``: a drain round of the pipelined exchange, no new batch).
+
+        The batch is framed either by u32 offsets (``off_host``) or by a varint length stream
+        (``lens_host``, see ``pipeline/framing.py``; ``raw_bytes`` = payload bytes without padding),
+        which crosses PCIe in ~1 B per payload and is turned into offsets on the GPU."""
         k = self.k
         b = k % self.nbuf
         now_ms = int(time.time() * 1000) if now_ms is None else now_ms
-        nbytes = int(raw_host.numel())
-        with torch.cuda.stream(self.h2d):
-            if k >= self.nbuf:
-                self.h2d.wait_event(self.ev_comp[b])      # compute k-nbuf was the last reader of buffer b
-            self.raw[b][:nbytes].copy_(raw_host, non_blocking=True)
-            self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
-            self.ev_h2d[b].record(self.h2d)
+        if raw_host is not None:
+            nbytes = int(raw_host.numel())
+            with torch.cuda.stream(self.h2d):
+                if k >= self.nbuf:
+                    self.h2d.wait_event(self.ev_comp[b])  # compute k-nbuf was the last reader of buffer b
+                self.raw[b][:nbytes].copy_(raw_host, non_blocking=True)
+                if lens_host is not None:
+                    self.lens[b][:lens_host.numel()].copy_(lens_host, non_blocking=True)
+                else:
+                    self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
+                self.ev_h2d[b].record(self.h2d)
         if self.mode == "hsa" and self.copying is not None and self.copying[0] == b:
             self._finish_copy()                           # SDMA copy k-2 still reads staging ring b
-        self.comp.wait_event(self.ev_h2d[b])
+        if raw_host is not None:
+            self.comp.wait_event(self.ev_h2d[b])
+            if lens_host is not None:
+                self.e.frame_varint(self.lens[b], lens_host.numel(), n_msgs, self.off[b],
+                                    nbytes if raw_bytes is None else raw_bytes)
         if k >= self.nbuf and self.mode in ("push", "sdma"):
             self.comp.wait_event(self.ev_push[b])         # push k-2 was the last reader of staging ring b
-        self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
-                          out_to_device=(self.mode in ("push", "sdma", "hsa")))
-        self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
+        to_dev = self.mode in ("push", "sdma", "hsa")
+        if self.rounds:
+            src = (self.raw[b], self.off[b]) if raw_host is not None else (None, None)
+            self.produced[b] = self.e.round_async(src[0], src[1], n_msgs, now_ms, presence=presence, out_sel=b,
+                                                  out_to_device=to_dev)
+        else:
+            self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
+                              out_to_device=to_dev)
+            self.produced[b] = True
+        if not self.produced[b]:
+            self.nout[b].zero_()
+        else:
+            self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
         self.scal_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
         self.ev_comp[b].record(self.comp)
         if self.mode == "push" and self.deliver:
@@ -532,7 +675,7 @@ class PipelinedRunner:
         self.ev_comp[pb].synchronize()
         if self.mode == "push" and self.deliver:
             self.ev_push[pb].synchronize()
-        n_out = int(self.scal_host[pb][7])
+        n_out = int(self.scal_host[pb][7]) if self.produced[pb] else 0
         self.pending = None
         if self.mode not in ("sdma", "hsa"):
             self._deliver(pb, n_out)
@@ -567,11 +710,13 @@ class PipelinedRunner:
         self.copying = (pb, n_out, None)
 
     def flush(self):
+        if self.rounds and self.e.exchange_pending:
+            self.submit(None, None, 0)                    # last round: process the batch in flight
         self._drain()
         self._finish_copy()
         self.comp.synchronize()
         self.push.synchronize()
 
     def outbound(self, b: int) -> np.ndarray:
-        n = int(self.scal_host[b][7])
+        n = int(self.scal_host[b][7]) if self.produced[b] else 0
         return self.e.out_host[b].view(OUT_REC, n)

@@ -119,6 +119,44 @@ def test_pipelined_runner_matches_sync(mode):
     assert canon_out(np.concatenate(seen), None) == canon_out(np.concatenate(cpu_rows), None)
 
 
+def test_varint_framing_kernel_matches_host_offsets():
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    g = GpuInboundEngine(small_cfg(max_msgs=8192))
+    rng = np.random.default_rng(5)
+    lens = np.concatenate([rng.integers(0, 128, 5000), rng.integers(128, 70000, 200), [0, 127, 128, 16383, 16384]])
+    rng.shuffle(lens)
+    offs = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    stream = varint_lengths(offs)
+    assert len(stream) > len(lens)              # some multi-byte varints cross tile boundaries
+    ld = torch.from_numpy(stream).cuda()
+    od = torch.full((len(lens) + 8,), -1, dtype=torch.int32, device="cuda")
+    g.frame_varint(ld, len(stream), len(lens), od, int(offs[-1]))
+    torch.cuda.synchronize()
+    assert np.array_equal(od[:len(lens) + 1].cpu().numpy().view(np.uint32).astype(np.int64), offs)
+
+
+def test_pipelined_runner_varint_framing_matches_sync():
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    g, c = pair()
+    seen = []
+    runner = PipelinedRunner(g, max_raw_bytes=1 << 20, on_outbound=lambda rows: seen.append(rows.copy()))
+    total = 0
+    cpu_rows = []
+    for k in range(4):
+        raw, offs = fleet_batch(2000, seed=700 + k)
+        rh = torch.from_numpy(raw).pin_memory()
+        lh = torch.from_numpy(varint_lengths(offs)).pin_memory()
+        runner.submit(rh, None, len(offs) - 1, now_ms=NOW + k, lens_host=lh, raw_bytes=int(offs[-1]))
+        r = c.step(raw, offs, NOW + k, presence=False)
+        total += r.n_persisted
+        cpu_rows.append(r.out)
+    runner.flush()
+    assert runner.delivered == total == sum(len(x) for x in seen)
+    assert g.stats_dict() == c.stats_dict()
+    assert canon_out(np.concatenate(seen), None) == canon_out(np.concatenate(cpu_rows), None)
+
+
 def test_standalone_pip_kernel():
     import ctypes
     from sitewhere_amd._native import gpu

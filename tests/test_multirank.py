@@ -91,7 +91,7 @@ def test_gpu_loopback_matches_cpu_oracle():
         for q in range(W):
             for r in range(W):
                 g[q].recv_slab(r).copy_(g[r].send_slab(q))
-                g[q].t["recv_cnt"][r] = g[r].t["send_cnt"][q]
+                g[q].t["recv_cnt"][r] = g[r].send_count(q)
         for e in g:
             e.phase_process()
         torch.cuda.synchronize()
@@ -102,6 +102,125 @@ def test_gpu_loopback_matches_cpu_oracle():
             assert gres[r].n_persisted == cres[r].n_persisted
             assert canon_out(gres[r].out, None) == canon_out(cres[r].out, None)
             assert np.array_equal(gres[r].event_ids(), cres[r].event_ids())
+    for r in range(W):
+        assert g[r].stats_dict() == c[r].stats_dict()
+
+
+SPILL = dict(shuffle_slack=0.1, shuffle_pad=0)     # slabs of ~270 records: every step spills
+
+
+def test_cpu_spill_defers_and_conserves_events():
+    """Records beyond a full slab are carried to the next exchange (never dropped): after drain
+    steps with empty batches the shards have processed exactly the single-shard event count."""
+    shards = [CpuInboundEngine(EngineConfig.small(world=W, rank=r, **SPILL)) for r in range(W)]
+    for r, e in enumerate(shards):
+        shard_fleet(e, W, r)
+    steps = [[fleet_batch(1500, seed=40 + 10 * k + r, n_dev=N_DEV) for r in range(W)] for k in range(3)]
+    got = 0
+    for k, batches in enumerate(steps):
+        got += sum(r.n_events for r in cpu_loopback_step(shards, batches, NOW + k))
+    assert sum(int(e.stats[13]) for e in shards) > 0 and sum(len(e.carry) for e in shards) > 0
+    empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint32))
+    for k in range(20):
+        if not any(len(e.carry) for e in shards):
+            break
+        got += sum(r.n_events for r in cpu_loopback_step(shards, [empty] * W, NOW + 10 + k))
+    assert not any(len(e.carry) for e in shards)
+    single = CpuInboundEngine(EngineConfig.small(max_msgs=8192))
+    shard_fleet(single, 1, 0)
+    ref = sum(single.step(raw, offs, NOW, presence=False).n_events for b in steps for raw, offs in b)
+    assert got == ref
+    assert sum(e.stats_dict()["shuffle_overflow"] for e in shards) == 0
+
+
+def _gpu_shards(**kw):
+    from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
+    g = [GpuInboundEngine(EngineConfig.small(world=W, rank=r, **kw)) for r in range(W)]
+    for r, e in enumerate(g):
+        shard_fleet(e, W, r)
+    c = [CpuInboundEngine(EngineConfig.small(world=W, rank=r, **kw)) for r in range(W)]
+    for r, e in enumerate(c):
+        shard_fleet(e, W, r)
+    return g, c
+
+
+def _dev_batch(raw, offs):
+    import torch
+    return (torch.from_numpy(np.concatenate([raw, np.zeros(64, np.uint8)])).cuda(),
+            torch.from_numpy(np.ascontiguousarray(offs, np.uint32).view(np.int32)).cuda())
+
+
+def _loopback_copy(g):
+    for q in range(W):
+        for r in range(W):
+            g[q].recv_slab(r).copy_(g[r].send_slab(q))
+            g[q].t["recv_cnt"][r] = g[r].send_count(q)
+
+
+def _assert_same(gres, cres):
+    for r in range(W):
+        assert gres[r].n_events == cres[r].n_events
+        assert gres[r].n_persisted == cres[r].n_persisted
+        assert canon_out(gres[r].out, None) == canon_out(cres[r].out, None)
+        assert np.array_equal(gres[r].event_ids(), cres[r].event_ids())
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X GPU")
+def test_gpu_loopback_spill_matches_cpu_oracle():
+    """Spilled records (full slabs) are carried in the same deterministic order as the oracle."""
+    import torch
+    g, c = _gpu_shards(**SPILL)
+    empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint32))
+    for step in range(5):
+        batches = ([fleet_batch(1500, seed=90 + 10 * step + r, n_dev=N_DEV) for r in range(W)] if step < 3
+                   else [empty] * W)
+        now = NOW + step * 1000
+        keep = []
+        for e, (raw, offs) in zip(g, batches):
+            rd, od = _dev_batch(raw, offs)
+            keep.append((rd, od))
+            e.prepare(rd, od, len(offs) - 1, now)
+            e.phase_decode()
+        _loopback_copy(g)
+        for e in g:
+            e.phase_process()
+        torch.cuda.synchronize()
+        _assert_same([e.collect(e._last_sel, raw) for e, (raw, _) in zip(g, batches)],
+                     cpu_loopback_step(c, batches, now))
+    for r in range(W):
+        assert g[r].stats_dict() == c[r].stats_dict()
+    assert sum(e.stats_dict()["shuffle_deferred"] for e in g) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X GPU")
+def test_gpu_pipelined_rounds_match_serial_oracle():
+    """round_async (decode k | process k-1, exchange overlapped) gives each batch exactly the serial
+    step's result, one round later; the final round drains the batch in flight."""
+    import torch
+    g, c = _gpu_shards()
+    steps = [[fleet_batch(1500, seed=170 + 10 * k + r, n_dev=N_DEV) for r in range(W)] for k in range(4)]
+    cpu = [cpu_loopback_step(c, b, NOW + k * 1000) for k, b in enumerate(steps)]
+    keep = []
+    for k in range(len(steps) + 1):
+        for r, e in enumerate(g):
+            if k < len(steps):
+                raw, offs = steps[k][r]
+                rd, od = _dev_batch(raw, offs)
+                keep.append((rd, od))
+                done = e.round_async(rd, od, len(offs) - 1, NOW + k * 1000, out_sel=k % 2, exchange=False)
+            else:
+                done = e.round_async(None, out_sel=k % 2, exchange=False)
+            assert done == (k > 0)
+        if k < len(steps):
+            _loopback_copy(g)
+            for e in g:
+                e.exchange_done()
+        torch.cuda.synchronize()
+        if k > 0:
+            _assert_same([e.collect(k % 2, None) for e in g], cpu[k - 1])
+    assert not any(e.exchange_pending for e in g)
     for r in range(W):
         assert g[r].stats_dict() == c[r].stats_dict()
 
