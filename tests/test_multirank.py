@@ -261,3 +261,15 @@ def test_gloo_two_ranks():
     assert sum(o[1] for o in outs) == sum(t.n_events for t in tot)
     assert sum(o[2] for o in outs) == sum(t.n_persisted for t in tot)
     assert all(o[3] for o in outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X GPU")
+def test_numa_binding_is_safe():
+    """bind_numa never leaves the process without CPUs (node -1 when the topology is unknown)."""
+    from sitewhere_amd.parallel.sharding import bind_numa, gpu_numa_node
+    before = os.sched_getaffinity(0)
+    node = bind_numa(0)
+    assert node == -1 or node == gpu_numa_node(0)
+    assert os.sched_getaffinity(0)
+    os.sched_setaffinity(0, before)
