@@ -55,6 +55,7 @@ class ColumnarEventStore(DeviceEventStore):
         self._names: dict[int, str] = {}
         self._rules: dict[str, str] = {}
         self._boots: list[str] = []
+        self._high: dict[tuple, int] = {}       # (boot, rank) -> next store sequence not yet held
         self._lock = threading.RLock()
         self.consolidate_every = consolidate_every
         self.rows = 0
@@ -70,7 +71,17 @@ class ColumnarEventStore(DeviceEventStore):
             self._rules.update(d.get("rules") or {})
             if d["boot"] not in self._boots:
                 self._boots.append(d["boot"])
+            # idempotent by store sequence: a shard restored from a checkpoint replays the batches
+            # after it with the same (boot, sequence) ids -- rows already held are skipped
+            key = (d["boot"], int(d["rank"]))
+            high = self._high.get(key, 0)
+            first = int(d["first_seq"])
+            if first < high:
+                skip = min(n, high - first)
+                rows, first, n = rows[skip:], first + skip, n - skip
+                d = dict(d, first_seq=first)
             if n:
+                self._high[key] = max(high, first + n)
                 eid = (d["first_seq"] + np.arange(n, dtype=np.int64)) * d["world"] + d["rank"]
                 self._pending.append({"boot": np.full(n, self._boots.index(d["boot"]), np.int16), "eid": eid,
                                       "rows": rows, "recv": np.full(n, d["now"], np.int64)})

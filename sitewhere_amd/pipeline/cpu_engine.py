@@ -292,6 +292,42 @@ class CpuInboundEngine(EngineBase):
                           out=np.array(out_rows, OUT_REC), rejects=work[rej], reject_status=status[rej],
                           new_names=new, first_seq=first_seq, world=self.world, rank=self.rank)
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    kind = "cpu"
+
+    def checkpoint_state(self, include_store: bool = False) -> dict:
+        u64 = lambda xs: np.array(list(xs), np.uint64)  # noqa: E731
+        ms_keys = list(self.ms.keys())
+        st = {
+            "scalars": np.array([self.cursor, self.seq_base], np.int64),
+            "stats": self.stats.copy(),
+            "dedup_key": u64(self.dedup.keys()), "dedup_seq": np.array(list(self.dedup.values()), np.int64),
+            "intern_key": u64(self.intern.keys()), "intern_id": np.array(list(self.intern.values()), np.int64),
+            "seen": u64(self._seen),
+            "st_last": self.st_last, "st_missing": self.st_missing, "st_loc_date": self.st_loc_date,
+            "st_loc_eid": self.st_loc_eid,
+            "ms_key": np.array(ms_keys, np.int64).reshape(-1, 3),
+            "ms_val": np.array([self.ms[k] for k in ms_keys], np.int64).reshape(-1, 2),
+            "carry": self.carry.view(np.uint8).reshape(-1).copy(),
+        }
+        if include_store:
+            st.update({f"store.{k}": v for k, v in self.store.items()})
+        return st
+
+    def restore_state(self, a: dict, include_store: bool):
+        self.cursor, self.seq_base = (int(x) for x in a["scalars"])
+        self.stats[:] = a["stats"]
+        self.dedup = dict(zip((int(x) for x in a["dedup_key"]), (int(x) for x in a["dedup_seq"])))
+        self.intern = dict(zip((int(x) for x in a["intern_key"]), (int(x) for x in a["intern_id"])))
+        self._seen = {int(x) for x in a["seen"]}
+        for k in ("st_last", "st_missing", "st_loc_date", "st_loc_eid"):
+            getattr(self, k)[:] = a[k]
+        self.ms = {tuple(int(x) for x in k): [int(v[0]), int(v[1])] for k, v in zip(a["ms_key"], a["ms_val"])}
+        self.carry = a["carry"].view(EVENT_REC).copy()
+        if include_store:
+            for k in self.store:
+                self.store[k][:] = a[f"store.{k}"]
+
     # ------------------------------------------------------------------ queries
     def stats_dict(self) -> dict:  # type: ignore[override]
         return {n: int(self.stats[i]) for i, n in enumerate(STAT_NAMES)}

@@ -234,6 +234,24 @@ class EngineBase:
             return True
         return False
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    kind = "base"
+
+    def checkpoint_state(self, include_store: bool = False) -> dict:
+        """Engine tables to snapshot (name -> numpy array); see ``pipeline/checkpoint.py``."""
+        raise NotImplementedError
+
+    def restore_state(self, arrays: dict, include_store: bool):
+        raise NotImplementedError
+
+    def save_checkpoint(self, path: str, include_store: bool = False, extra: dict | None = None) -> int:
+        from .checkpoint import save_engine
+        return save_engine(self, path, include_store, extra)
+
+    def load_checkpoint(self, path: str) -> dict:
+        from .checkpoint import load_engine
+        return load_engine(self, path)
+
     @staticmethod
     def stats_dict(arr) -> dict:
         return {n: int(arr[i]) for i, n in enumerate(STAT_NAMES)}

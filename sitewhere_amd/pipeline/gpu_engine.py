@@ -536,6 +536,39 @@ class GpuInboundEngine(EngineBase):
             cols[k] = cols[k].view(np.uint64)
         return cols, (np.arange(cur - n, cur) * self.world + self.rank)
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    kind = "gpu"
+    _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_key", "dd_seq", "seq_base", "nm_key", "nm_id", "nm_first",
+                    "nm_counter", "seen_key", "st", "ms", "stats", "cursor")
+
+    def checkpoint_state(self, include_store: bool = False) -> dict:
+        if self._pend is not None:
+            raise RuntimeError("checkpoint with a pipelined exchange in flight: drain the round first")
+        torch.cuda.synchronize(self.device)
+        st = {k: self.t[k].cpu().numpy() for k in self._CKPT_TABLES}
+        if self.world > 1:
+            cp = self._carry_par
+            n = int(self.t["n_carry"][cp].item())
+            st["carry"] = self.carry_bufs[cp][:n * EVENT_REC.itemsize].cpu().numpy()
+        if include_store:
+            st.update({f"store.{k}": v.cpu().numpy() for k, v in self.store.items()})
+        return st
+
+    def restore_state(self, a: dict, include_store: bool):
+        torch.cuda.synchronize(self.device)
+        for k in self._CKPT_TABLES:
+            self.t[k].copy_(torch.from_numpy(a[k]))       # in place: captured graphs keep their pointers
+        if self.world > 1 and "carry" in a:
+            cp = self._carry_par
+            c = torch.from_numpy(a["carry"])
+            self.carry_bufs[cp][:c.numel()].copy_(c)
+            self.t["n_carry"].zero_()
+            self.t["n_carry"][cp] = c.numel() // EVENT_REC.itemsize
+        if include_store:
+            for k, v in self.store.items():
+                v.copy_(torch.from_numpy(a[f"store.{k}"]))
+        torch.cuda.synchronize(self.device)
+
     def reset_dedup(self):
         self.t["dd_key"].zero_()
         self.t["dd_seq"].fill_(-1)

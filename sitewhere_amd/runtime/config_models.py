@@ -83,7 +83,11 @@ _m("inbound-processing", "Inbound Processing", [
       choices=["events", "batches", "none"]),
     A("maxDelayMs", "Integer", "micro-batch latency bound (gpu engine)", default=5)], [
     E("Zone Tests", "gpu-zone-tests", "zone tests evaluated inside the GPU engine", [
-        A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")])])
+        A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")]),
+    E("Checkpoint", "checkpoint", "engine-shard snapshots; raw offsets commit only when covered", [
+        A("path", "String", "safetensors file (supports [[tenant.token]])", True),
+        A("everyBatches", "Integer", "raw batches between snapshots", default=64),
+        A("includeStore", "Boolean", "also snapshot the HBM event ring", default=False)])])
 _m("event-management", "Event Management", [A("buffered", "Boolean", "bulk buffer (DeviceEventBuffer)", default=False)],
    [DATASTORE])
 _m("device-management", "Device Management", [], [DATASTORE])

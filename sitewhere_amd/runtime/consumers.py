@@ -24,7 +24,7 @@ class BusConsumer(TenantEngineLifecycleComponent):
     component_type = LifecycleComponentType.Other
 
     def __init__(self, engine, name: str, topics: list[str], handler, threads: int = 0, max_records: int = 500,
-                 group: str | None = None):
+                 group: str | None = None, auto_commit: bool = True):
         super().__init__(name)
         self.tenant_engine = engine
         self.engine = engine
@@ -38,6 +38,8 @@ class BusConsumer(TenantEngineLifecycleComponent):
         self._t = None
         self.processed = 0
         self.failures = 0
+        # False: the handler commits explicit offsets itself (checkpoint-aligned commits)
+        self.auto_commit = auto_commit
 
     def start(self, monitor):
         bus = self.engine.ms.instance.bus
@@ -74,7 +76,8 @@ class BusConsumer(TenantEngineLifecycleComponent):
                     step = max(1, len(recs) // self.threads)
                     futs += [self.pool.submit(self._call, recs[i:i + step]) for i in range(0, len(recs), step)]
                 wait(futs)
-            self.consumer.commit()   # after processing: at-least-once
+            if self.auto_commit:
+                self.consumer.commit()   # after processing: at-least-once
 
     def stop(self, monitor):
         self._stop.set()

@@ -91,8 +91,17 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.zone_tests = [ZoneTest(z["zoneToken"], z.get("condition", "inside"), z.get("alertType", "zone.alert"),
                                     int(z.get("alertLevel", 1)), z.get("alertMessage", ""))
                            for z in cfg.get("zoneTests", [])]
+        # checkpoint / resume: {"path": ..., "everyBatches": N, "includeStore": false}.
+        # With a checkpoint the raw consumer commits only the offsets a snapshot on disk covers.
+        ck = cfg.get("checkpoint") or {}
+        self.ckpt_path = ck.get("path") or None      # already [[tenant.token]]-substituted
+        self.ckpt_every = int(ck.get("everyBatches", 64))
+        self.ckpt_store = bool(ck.get("includeStore", False))
+        self._ckpt_offsets: dict[tuple[str, int], int] = {}
+        self._since_ckpt = 0
+        self.checkpoints = 0
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
-                                        self._process_raw, max_records=16)
+                                        self._process_raw, max_records=16, auto_commit=self.ckpt_path is None)
         self.persisted_events = self.create_meter("persistedEvents")
         self.step_timer = self.create_timer("engineStep")
         self.api = {"InboundProcessing": GpuInboundApi(self)}
@@ -184,19 +193,63 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
 
     # ---------------------------------------------------------------- lifecycle
     def tenant_start(self, monitor):
+        self.restore_checkpoint()
         self.load_model()
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         self.start_nested_component(self.raw_consumer, monitor, require=True)
 
     def tenant_stop(self, monitor):
         self.raw_consumer.lifecycle_stop(monitor)
+        if self.ckpt_path and self._since_ckpt:
+            self.checkpoint()
         super().tenant_stop(monitor)
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    def checkpoint(self):
+        """Snapshot the shard + the raw-topic offsets it covers, then commit those offsets."""
+        import os
+        with self._lock:
+            extra = {"boot": self.boot, "offsets": [[t, p, o] for (t, p), o in self._ckpt_offsets.items()],
+                     "dev_index": self.dev_index.ids, "asg_index": self.asg_index.ids,
+                     "customers": self.customers.ids, "areas": self.areas.ids, "assets": self.assets.ids}
+            os.makedirs(os.path.dirname(os.path.abspath(self.ckpt_path)), exist_ok=True)
+            self.engine.save_checkpoint(self.ckpt_path, include_store=self.ckpt_store, extra=extra)
+            self._since_ckpt = 0
+            self.checkpoints += 1
+        bus = self.ms.instance.bus
+        for (t, p), o in dict(self._ckpt_offsets).items():
+            bus.commit(self.raw_consumer.group, t, p, o)
+
+    def restore_checkpoint(self) -> bool:
+        import os
+        if not self.ckpt_path or not os.path.exists(self.ckpt_path):
+            return False
+        with self._lock:
+            extra = self.engine.load_checkpoint(self.ckpt_path)
+            self.boot = extra["boot"]
+            for name in ("dev_index", "asg_index", "customers", "areas", "assets"):
+                m = getattr(self, name)
+                for key in extra[name]:
+                    m.get(key)
+            self._ckpt_offsets = {(t, int(p)): int(o) for t, p, o in extra["offsets"]}
+        # the snapshot's offsets are authoritative: replay starts right after what it covers
+        bus = self.ms.instance.bus
+        for (t, p), o in self._ckpt_offsets.items():
+            bus.commit(self.raw_consumer.group, t, p, o)
+        self.logger.info("restored engine shard from %s (%d offsets)", self.ckpt_path, len(self._ckpt_offsets))
+        return True
 
     # ---------------------------------------------------------------- data plane
     def _process_raw(self, recs):
         for r in recs:
             raw, offs = unpack_raw_batch(r.value)
-            self.process_batch(raw, offs)
+            # the record timestamp is the batch's receive time: replay after a restore is deterministic
+            self.process_batch(raw, offs, now=r.timestamp or None)
+            if self.ckpt_path:
+                self._ckpt_offsets[(r.topic, r.partition)] = r.offset + 1
+                self._since_ckpt += 1
+                if self._since_ckpt >= self.ckpt_every:
+                    self.checkpoint()
 
     def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None):
         now = now or now_ms()
