@@ -323,7 +323,7 @@ __device__ __forceinline__ uint32_t part_total(const uint32_t* __restrict__ toff
 __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
                              const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr, int world,
                              int rank, const uint32_t* __restrict__ toff /*scanned [world][ntiles]*/,
-                             const uint32_t* __restrict__ tcount, int64_t ntiles, SwEventRec* __restrict__ send,
+                             const uint32_t* __restrict__ tcount, int64_t ntiles, SwWireRec* __restrict__ send,
                              int64_t shuf_cap, SwEventRec* __restrict__ spill, int64_t carry_cap) {
   __shared__ uint32_t run[64];
   __shared__ uint32_t spill_base[64];
@@ -362,7 +362,7 @@ __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_
       for (uint32_t w = 0; w < wid; ++w) pre += wcnt[w][o];
       pre += my_rank;
       if (pre < shuf_cap) {
-        send[(int64_t)o * shuf_cap + pre] = part_in(carry, nc, recs, i);
+        send[(int64_t)o * shuf_cap + pre] = sw_wire_pack(part_in(carry, nc, recs, i));
       } else {
         const int64_t j = (int64_t)spill_base[o] + (pre - shuf_cap);
         if (j < carry_cap) spill[j] = part_in(carry, nc, recs, i);
@@ -397,7 +397,7 @@ __global__ void k_part_counts(const uint32_t* __restrict__ toff, const uint32_t*
 }
 
 // Concatenate the received [world][shuf_cap] slabs into one dense batch (rank order).
-__global__ void k_unpack(const SwEventRec* __restrict__ recv, const uint32_t* __restrict__ recv_cnt, int world,
+__global__ void k_unpack(const SwWireRec* __restrict__ recv, const uint32_t* __restrict__ recv_cnt, int world,
                          int64_t shuf_cap, SwEventRec* __restrict__ work, uint32_t* __restrict__ n_work, int64_t cap) {
   __shared__ uint32_t pre[65];
   if (threadIdx.x == 0) {
@@ -410,7 +410,7 @@ __global__ void k_unpack(const SwEventRec* __restrict__ recv, const uint32_t* __
   for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLK) {
     int q = 0;
     while (q + 1 < world && i >= pre[q + 1]) ++q;
-    work[i] = recv[(int64_t)q * shuf_cap + (i - pre[q])];
+    work[i] = sw_wire_unpack(recv[(int64_t)q * shuf_cap + (i - pre[q])], (uint8_t)q);
   }
 }
 
@@ -1293,6 +1293,7 @@ int sw_abi_sizes(int64_t* out) {
   out[5] = sizeof(SwRegSlot);
   out[6] = sizeof(SwAsgState);
   out[7] = sizeof(SwMsSlot);
+  out[8] = sizeof(SwWireRec);
   return 0;
 }
 

@@ -84,8 +84,8 @@ typedef struct SwEngineArgs {
   uint32_t* n_new_names;
   int64_t names_cap;
   // ---------------------------------------------------------------- shuffle (world > 1)
-  SwEventRec* send;            // [world * shuf_cap]
-  SwEventRec* recv;            // [world * shuf_cap]
+  SwWireRec* send;             // [world * shuf_cap] packed exchange records
+  SwWireRec* recv;             // [world * shuf_cap]
   int64_t shuf_cap;
   uint32_t* send_cnt;          // [world]
   uint32_t* recv_cnt;          // [world]

@@ -14,6 +14,7 @@
 //  * Records are 16-B aligned so a wave moves them with dwordx4 loads.
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #define SW_HD __host__ __device__ __forceinline__
@@ -76,6 +77,60 @@ typedef struct __attribute__((aligned(16))) SwEventRec {
   uint8_t src_rank;     // 78 rank whose raw batch holds the aux bytes
   uint8_t level;        // 79 alert level (GAlertLevel)
 } SwEventRec;
+
+// Exchange form of a decoded record, 64 bytes: what crosses xGMI in the owner all-to-all.  The
+// 80-byte record carries fields no event type uses together, so the exchange packs them
+// losslessly (tests/test_multirank.py checks pack/unpack on every decoded type):
+//   w0 = location ? elevation : name hash
+//   w1 = measurement|location ? v0 : aux2_off | aux2_len << 32 | level << 48
+//   w2 = v1 (longitude; 0 for the other types)
+// src_rank is not sent: the receiving slab index is the source rank.
+typedef struct __attribute__((aligned(16))) SwWireRec {
+  uint64_t fp_lo;       // 0
+  uint64_t fp_hi;       // 8
+  int64_t event_date;   // 16
+  uint64_t w0;          // 24
+  uint64_t w1;          // 32
+  uint64_t w2;          // 40
+  uint64_t alt_hash;    // 48
+  uint32_t aux_off;     // 56
+  uint16_t aux_len;     // 60
+  uint8_t etype;        // 62
+  uint8_t flags;        // 63
+} SwWireRec;
+
+SW_HD uint64_t sw_f64_bits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+SW_HD double sw_bits_f64(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+
+SW_HD SwWireRec sw_wire_pack(const SwEventRec& r) {
+  SwWireRec w;
+  const bool loc = r.etype == SW_EV_LOCATION;
+  const bool val = r.etype == SW_EV_MEASUREMENT || loc;
+  w.fp_lo = r.fp_lo; w.fp_hi = r.fp_hi; w.event_date = r.event_date;
+  w.w0 = loc ? sw_f64_bits(r.v2) : r.name_hash;
+  w.w1 = val ? sw_f64_bits(r.v0)
+             : ((uint64_t)r.aux2_off | ((uint64_t)r.aux2_len << 32) | ((uint64_t)r.level << 48));
+  w.w2 = sw_f64_bits(r.v1);
+  w.alt_hash = r.alt_hash; w.aux_off = r.aux_off; w.aux_len = r.aux_len; w.etype = r.etype; w.flags = r.flags;
+  return w;
+}
+
+SW_HD SwEventRec sw_wire_unpack(const SwWireRec& w, uint8_t src_rank) {
+  SwEventRec r;
+  const bool loc = w.etype == SW_EV_LOCATION;
+  const bool val = w.etype == SW_EV_MEASUREMENT || loc;
+  r.fp_lo = w.fp_lo; r.fp_hi = w.fp_hi; r.event_date = w.event_date;
+  r.name_hash = loc ? 0 : w.w0;
+  r.v2 = loc ? sw_bits_f64(w.w0) : 0.0;
+  r.v0 = val ? sw_bits_f64(w.w1) : 0.0;
+  r.v1 = sw_bits_f64(w.w2);
+  r.aux2_off = val ? 0u : (uint32_t)w.w1;
+  r.aux2_len = val ? (uint16_t)0 : (uint16_t)(w.w1 >> 32);
+  r.level = val ? (uint8_t)0 : (uint8_t)(w.w1 >> 48);
+  r.alt_hash = w.alt_hash; r.aux_off = w.aux_off; r.aux_len = w.aux_len; r.etype = w.etype; r.flags = w.flags;
+  r.src_rank = src_rank;
+  return r;
+}
 
 // Enriched, persisted event as delivered to outbound consumers, 32 bytes, written by the GPU
 // straight into mapped pinned host memory (zero-copy outbound, no D2H copy stage).

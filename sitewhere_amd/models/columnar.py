@@ -43,6 +43,48 @@ EVENT_REC = np.dtype([
 ], align=True)
 assert EVENT_REC.itemsize == 80
 
+# Exchange form (SwWireRec, csrc/include/swtypes.h): lossless 64-byte packing of EVENT_REC.
+WIRE_REC = np.dtype([
+    ("fp_lo", "<u8"), ("fp_hi", "<u8"), ("event_date", "<i8"), ("w0", "<u8"), ("w1", "<u8"), ("w2", "<u8"),
+    ("alt_hash", "<u8"), ("aux_off", "<u4"), ("aux_len", "<u2"), ("etype", "u1"), ("flags", "u1"),
+], align=True)
+assert WIRE_REC.itemsize == 64
+
+
+def wire_pack(r: np.ndarray) -> np.ndarray:
+    """EVENT_REC -> WIRE_REC (same rule as ``sw_wire_pack``)."""
+    w = np.zeros(len(r), WIRE_REC)
+    for k in ("fp_lo", "fp_hi", "event_date", "alt_hash", "aux_off", "aux_len", "etype", "flags"):
+        w[k] = r[k]
+    loc = r["etype"] == 1
+    val = (r["etype"] == 0) | loc
+    w["w0"] = np.where(loc, r["v2"].view(np.uint64), r["name_hash"])
+    aux2 = (r["aux2_off"].astype(np.uint64) | (r["aux2_len"].astype(np.uint64) << np.uint64(32)) |
+            (r["level"].astype(np.uint64) << np.uint64(48)))
+    w["w1"] = np.where(val, r["v0"].view(np.uint64), aux2)
+    w["w2"] = r["v1"].view(np.uint64)
+    return w
+
+
+def wire_unpack(w: np.ndarray, src_rank: int) -> np.ndarray:
+    """WIRE_REC -> EVENT_REC (``sw_wire_unpack``); ``src_rank`` = the slab the records came from."""
+    r = np.zeros(len(w), EVENT_REC)
+    for k in ("fp_lo", "fp_hi", "event_date", "alt_hash", "aux_off", "aux_len", "etype", "flags"):
+        r[k] = w[k]
+    loc = w["etype"] == 1
+    val = (w["etype"] == 0) | loc
+    r["name_hash"] = np.where(loc, np.uint64(0), w["w0"])
+    r["v2"] = np.where(loc, w["w0"], np.uint64(0)).view(np.float64)
+    r["v0"] = np.where(val, w["w1"], np.uint64(0)).view(np.float64)
+    r["v1"] = w["w2"].view(np.float64)
+    aux = np.where(val, np.uint64(0), w["w1"])
+    r["aux2_off"] = (aux & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    r["aux2_len"] = ((aux >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.uint16)
+    r["level"] = ((aux >> np.uint64(48)) & np.uint64(0xFF)).astype(np.uint8)
+    r["src_rank"] = src_rank
+    return r
+
+
 OUT_REC = np.dtype([
     ("event_date", "<i8"), ("v0", "<f8"), ("v1", "<f8"), ("assignment", "<i4"), ("name_id", "<u2"),
     ("etype", "u1"), ("level", "u1"),

@@ -60,7 +60,7 @@ class SwEngineArgs(ctypes.Structure):
 
 
 def abi_sizes(lib) -> dict:
-    buf = (ctypes.c_int64 * 8)()
+    buf = (ctypes.c_int64 * 9)()
     lib.sw_abi_sizes(ctypes.cast(buf, ctypes.c_void_p))
     return {"event_rec": buf[0], "out_rec": buf[1], "engine_args": buf[2], "name_ref": buf[3], "zone_test": buf[4],
-            "reg_slot": buf[5], "asg_state": buf[6], "ms_slot": buf[7]}
+            "reg_slot": buf[5], "asg_state": buf[6], "ms_slot": buf[7], "wire_rec": buf[8]}

@@ -12,7 +12,7 @@ import numpy as np
 
 from ..models.columnar import (EVENT_REC, OUT_REC, EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE,
                                EV_DECODE_ERROR, ST_OK, ST_UNREGISTERED, ST_UNASSIGNED, ST_DUPLICATE,
-                               ST_DECODE_ERROR, ST_CONTROL, STAT_NAMES)
+                               ST_DECODE_ERROR, ST_CONTROL, STAT_NAMES, WIRE_REC, wire_pack, wire_unpack)
 from .config import EngineConfig
 from .engine_base import EngineBase, StepResult
 from .fleet import cpu_decode
@@ -97,12 +97,14 @@ class CpuInboundEngine(EngineBase):
 
         from ..parallel.sharding import exchange_slabs
         send, cnt = self.partition(recs)
-        send_t = torch.from_numpy(send.view(np.uint8).reshape(-1).copy())
+        # the exchange carries the packed 64-byte form, like the GPU all-to-all
+        send_t = torch.from_numpy(wire_pack(send.reshape(-1)).view(np.uint8))
         recv_t = torch.empty_like(send_t)
         cnt_t = torch.from_numpy(cnt)
         rcnt_t = torch.empty_like(cnt_t)
         exchange_slabs(cnt_t, rcnt_t, send_t, recv_t, self.group)
-        recv = recv_t.numpy().view(EVENT_REC).reshape(self.world, self.cfg.shuf_cap)
+        wire = recv_t.numpy().view(WIRE_REC).reshape(self.world, self.cfg.shuf_cap)
+        recv = np.stack([wire_unpack(wire[q], q) for q in range(self.world)])
         return self.unpack(recv, rcnt_t.numpy())
 
     def _lookup(self, recs):

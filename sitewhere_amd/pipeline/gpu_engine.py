@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from .._native import gpu as gpu_lib
-from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE
+from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE, WIRE_REC
 from ..ops.engine_abi import SwEngineArgs
 from .config import EngineConfig
 from .engine_base import EngineBase, StepResult
@@ -93,9 +93,9 @@ class GpuInboundEngine(EngineBase):
         if c.world > 1:
             # send slabs are double-buffered (the pipelined exchange of batch k reads one while batch
             # k+1 is partitioned into the other); carry/spill alternate roles every partition
-            self.send_bufs = [z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8) for _ in range(2)]
+            self.send_bufs = [z(c.world * c.shuf_cap * WIRE_REC.itemsize, u8) for _ in range(2)]
             self.send_cnts = [z(c.world, i32) for _ in range(2)]
-            t["recv"] = z(c.world * c.shuf_cap * EVENT_REC.itemsize, u8)
+            t["recv"] = z(c.world * c.shuf_cap * WIRE_REC.itemsize, u8)
             t["recv_cnt"] = z(c.world, i32)
             t["part_tmp"] = z(2 * c.world * ptiles + 64, i32)
             t["work"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
@@ -438,15 +438,15 @@ class GpuInboundEngine(EngineBase):
         return self._pend is not None
 
     def send_slab(self, q: int) -> torch.Tensor:
-        """Destination-q slab of the most recent partition."""
-        n = self.cfg.shuf_cap * EVENT_REC.itemsize
+        """Destination-q slab (packed WIRE_REC) of the most recent partition."""
+        n = self.cfg.shuf_cap * WIRE_REC.itemsize
         return self.send_bufs[self._last_send_par][q * n:(q + 1) * n]
 
     def send_count(self, q: int) -> torch.Tensor:
         return self.send_cnts[self._last_send_par][q]
 
     def recv_slab(self, q: int) -> torch.Tensor:
-        n = self.cfg.shuf_cap * EVENT_REC.itemsize
+        n = self.cfg.shuf_cap * WIRE_REC.itemsize
         return self.t["recv"][q * n:(q + 1) * n]
 
     def scalars(self) -> dict:

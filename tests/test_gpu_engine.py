@@ -45,9 +45,9 @@ def test_abi_sizes_match():
     s = abi_sizes(gpu())
     assert s["event_rec"] == 80 and s["out_rec"] == 32 and s["name_ref"] == 16
     assert s["engine_args"] == ctypes.sizeof(SwEngineArgs)
-    buf = (ctypes.c_int64 * 8)()
-    gpu().sw_abi_sizes(ctypes.cast(buf, ctypes.c_void_p))
-    assert list(buf[5:8]) == [32, 32, 32]  # SwRegSlot, SwAsgState, SwMsSlot
+    assert [s["reg_slot"], s["asg_state"], s["ms_slot"]] == [32, 32, 32]
+    from sitewhere_amd.models.columnar import WIRE_REC
+    assert s["wire_rec"] == WIRE_REC.itemsize == 64
 
 
 def test_hand_batch_parity():

@@ -273,3 +273,19 @@ def test_numa_binding_is_safe():
     assert node == -1 or node == gpu_numa_node(0)
     assert os.sched_getaffinity(0)
     os.sched_setaffinity(0, before)
+
+
+def test_wire_pack_is_lossless_for_every_decoded_type():
+    """The 64-byte exchange form round-trips every record the decoder emits (all event types,
+    control and decode-error records) -- the packing may not change any result."""
+    from sitewhere_amd.models.columnar import EVENT_REC, wire_pack, wire_unpack
+    from sitewhere_amd.pipeline.fleet import cpu_decode
+    from pipeline_scenarios import hand_batch
+    recs = [cpu_decode(*fleet_batch(3000, seed=s, n_dev=N_DEV), NOW, 2, cap=1 << 16) for s in (1, 2)]
+    raw, offs = hand_batch()
+    recs.append(cpu_decode(raw, offs, NOW, 2, cap=1 << 12))
+    r = np.concatenate(recs)
+    assert {0, 1, 2}.issubset(set(r["etype"].tolist())) and (r["etype"] >= 16).any()
+    back = wire_unpack(wire_pack(r), 2)
+    assert back.tobytes() == r.tobytes()
+    assert EVENT_REC.itemsize == 80
