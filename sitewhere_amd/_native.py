@@ -140,6 +140,36 @@ def native():
         return lib
 
 
+_native_gil = None
+
+
+def native_gil():
+    """The host runtime library bound with ``ctypes.PyDLL``: calls keep the GIL.
+
+    For the bus's microsecond calls (append, read, offsets, commit).  Through ``CDLL`` every such
+    call releases the GIL and must win it back from the busy service threads -- measured at
+    0.1-1 ms per call on the per-event path (a convoy), for 4-80 us of native work."""
+    global _native_gil
+    if _native_gil is not None:
+        return _native_gil
+    lib0 = native()
+    with _lock:
+        if _native_gil is None:
+            lib = ctypes.PyDLL(lib0._name)
+            P = c_void_p
+            _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)
+            _proto(lib, "swlog_partitions", c_int32, P, c_int32)
+            _proto(lib, "swlog_append_batch", c_int64, P, c_int32, c_int32, P, P, P, P, P, c_int64)
+            _proto(lib, "swlog_append", c_int64, P, c_int32, c_int32, P, c_int64, P, c_int64, c_int64)
+            _proto(lib, "swlog_end_offset", c_int64, P, c_int32, c_int32)
+            _proto(lib, "swlog_begin_offset", c_int64, P, c_int32, c_int32)
+            _proto(lib, "swlog_read", c_int64, P, c_int32, c_int32, c_int64, c_int64, P, c_int64, P)
+            _proto(lib, "swlog_commit", c_int32, P, c_char_p, c_int32, c_int32, c_int64)
+            _proto(lib, "swlog_committed", c_int64, P, c_char_p, c_int32, c_int32)
+            _native_gil = lib
+    return _native_gil
+
+
 def gpu():
     """Load the gfx950 kernel library.  Raises if it is missing -- never falls back silently."""
     global _gpu

@@ -24,7 +24,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .._native import native
+from .._native import native, native_gil
 
 _FRAME = struct.Struct("<qqII")
 
@@ -94,6 +94,9 @@ class EventBus:
                  session_timeout_s: float = 30.0):
         self.lib = native()
         self.h = self.lib.swlog_open(directory.encode() if directory else None, 1 if fsync else 0)
+        # microsecond calls keep the GIL (PyDLL); opening, flushing and closing go through CDLL
+        self.fast = native_gil() if not fsync else self.lib
+        self._tls = threading.local()
         self.directory = directory
         self.default_partitions = default_partitions
         self.session_timeout_s = session_timeout_s
@@ -110,14 +113,14 @@ class EventBus:
         with self._lock:
             t = self._topics.get(name)
             if t is None:
-                t = self.lib.swlog_topic(self.h, name.encode(), partitions or self.default_partitions)
+                t = self.fast.swlog_topic(self.h, name.encode(), partitions or self.default_partitions)
                 self._topics[name] = t
             return t
 
     def partitions(self, name: str) -> int:
         n = self._nparts.get(name)
         if n is None:
-            n = self._nparts[name] = self.lib.swlog_partitions(self.h, self.topic(name))
+            n = self._nparts[name] = self.fast.swlog_partitions(self.h, self.topic(name))
         return n
 
     def topics(self) -> list[str]:
@@ -125,10 +128,10 @@ class EventBus:
             return sorted(self._topics)
 
     def end_offset(self, name: str, partition: int) -> int:
-        return self.lib.swlog_end_offset(self.h, self.topic(name), partition)
+        return self.fast.swlog_end_offset(self.h, self.topic(name), partition)
 
     def begin_offset(self, name: str, partition: int) -> int:
-        return self.lib.swlog_begin_offset(self.h, self.topic(name), partition)
+        return self.fast.swlog_begin_offset(self.h, self.topic(name), partition)
 
     def partition_for(self, name: str, key: bytes | None) -> int:
         n = self.partitions(name)
@@ -146,7 +149,7 @@ class EventBus:
         if len(records) == 1:
             k, v = records[0]
             k = k or b""
-            first = self.lib.swlog_append(self.h, t, partition, k, len(k), v, len(v),
+            first = self.fast.swlog_append(self.h, t, partition, k, len(k), v, len(v),
                                           ts if ts is not None else int(time.time() * 1000))
             if first < 0:
                 raise RuntimeError(f"append to {name}[{partition}] failed")
@@ -161,7 +164,7 @@ class EventBus:
         kb = np.frombuffer(b"".join(keys) + b"\0", np.uint8)
         vb = np.frombuffer(b"".join(vals) + b"\0", np.uint8)
         tsa = np.full(len(records), ts if ts is not None else int(time.time() * 1000), np.int64)
-        first = self.lib.swlog_append_batch(self.h, t, partition, kb.ctypes.data, koff.ctypes.data, vb.ctypes.data,
+        first = self.fast.swlog_append_batch(self.h, t, partition, kb.ctypes.data, koff.ctypes.data, vb.ctypes.data,
                                             voff.ctypes.data, tsa.ctypes.data, len(records))
         if first < 0:
             raise RuntimeError(f"append to {name}[{partition}] failed")
@@ -171,9 +174,13 @@ class EventBus:
     # ------------------------------------------------------------------ fetch
     def read(self, name: str, partition: int, offset: int, max_records: int = 500, max_bytes: int = 1 << 20):
         t = self.topic(name)
-        buf = np.empty(max_bytes, np.uint8)
+        if offset >= self.fast.swlog_end_offset(self.h, t, partition):
+            return []                                   # nothing new: no buffer, no copy
+        buf = getattr(self._tls, "buf", None)           # per-thread fetch buffer, reused
+        if buf is None or len(buf) < max_bytes:
+            buf = self._tls.buf = np.empty(max_bytes, np.uint8)
         n = ctypes.c_int64(0)
-        w = self.lib.swlog_read(self.h, t, partition, offset, max_records, buf.ctypes.data, max_bytes, ctypes.byref(n))
+        w = self.fast.swlog_read(self.h, t, partition, offset, max_records, buf.ctypes.data, max_bytes, ctypes.byref(n))
         if w < 0:
             return self.read(name, partition, offset, max_records, -w + 64)
         out = []
@@ -219,10 +226,10 @@ class EventBus:
 
     # ------------------------------------------------------------------ offsets
     def commit(self, group: str, name: str, partition: int, offset: int):
-        self.lib.swlog_commit(self.h, group.encode(), self.topic(name), partition, offset)
+        self.fast.swlog_commit(self.h, group.encode(), self.topic(name), partition, offset)
 
     def committed(self, group: str, name: str, partition: int) -> int:
-        return self.lib.swlog_committed(self.h, group.encode(), self.topic(name), partition)
+        return self.fast.swlog_committed(self.h, group.encode(), self.topic(name), partition)
 
     def retain_from(self, name: str, partition: int, offset: int) -> int:
         return self.lib.swlog_retain_from(self.h, self.topic(name), partition, offset)

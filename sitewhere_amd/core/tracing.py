@@ -12,9 +12,9 @@ import contextvars
 import random
 import threading
 import time
-import uuid
 from collections import deque
 from dataclasses import dataclass, field
+from ..utils import fast_hex
 
 _current: contextvars.ContextVar["Span | None"] = contextvars.ContextVar("sw_span", default=None)
 HEADER = "uber-trace-id"
@@ -92,9 +92,9 @@ class Tracer:
         if parent is not None:
             trace_id, parent_id, sampled = parent.trace_id, parent.span_id, parent.sampled
         else:
-            trace_id, parent_id = uuid.uuid4().hex[:16], None
+            trace_id, parent_id = fast_hex(64), None
             sampled = force_sample or random.random() < self.sample_rate
-        return Span(self, name, trace_id, uuid.uuid4().hex[:16], parent_id, sampled,
+        return Span(self, name, trace_id, fast_hex(64), parent_id, sampled,
                     tags={"service": self.service})
 
     def extract(self, header: str | None) -> Span | None:

@@ -11,9 +11,9 @@ import functools
 import enum
 import re
 import time
-import uuid
 from dataclasses import dataclass, field
 from typing import get_type_hints
+from ..utils import fast_uuid4
 
 _camel_re = re.compile(r"_([a-z0-9])")
 
@@ -44,7 +44,7 @@ def now_ms() -> int:
 
 
 def new_id() -> str:
-    return str(uuid.uuid4())
+    return fast_uuid4()
 
 
 class Model:

@@ -9,12 +9,37 @@ tests and single-process deployments, SQLite gives a durable zero-dependency sto
 from __future__ import annotations
 
 import copy
+import enum
+import dataclasses
 import json
 import sqlite3
 import threading
 from typing import Callable, Iterable
 
 from ..models.domain import Model
+
+
+_ATOMIC = (str, int, float, bool, bytes, type(None), enum.Enum)
+
+
+def _clone(v):
+    """Isolation copy of a stored entity: dataclass models, dicts and lists are copied, everything
+    else is immutable.  ~10x cheaper than ``copy.deepcopy`` (no memo, no reduce protocol) -- it runs
+    on every read and write of the in-memory store."""
+    if isinstance(v, _ATOMIC):
+        return v
+    if isinstance(v, dict):
+        return {k: _clone(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_clone(x) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_clone(x) for x in v)
+    d = getattr(v, "__dict__", None)
+    if d is not None and dataclasses.is_dataclass(v):
+        o = object.__new__(type(v))
+        o.__dict__.update({k: _clone(x) for k, x in d.items()})
+        return o
+    return copy.deepcopy(v)
 
 
 class EntityStore:
@@ -84,13 +109,13 @@ class MemoryEntityStore(EntityStore):
                         from ..core.errors import ErrorCode, SiteWhereSystemException
                         raise SiteWhereSystemException(ErrorCode.DuplicateToken, detail=f"{collection}.{f}={v} exists")
                     idx[v] = entity.id
-            data[entity.id] = copy.deepcopy(entity)
-            return copy.deepcopy(entity)
+            data[entity.id] = _clone(entity)
+            return _clone(entity)
 
     def get(self, collection, id):
         with self._lock:
             e = self._coll(collection).get(id)
-            return copy.deepcopy(e) if e is not None else None
+            return _clone(e) if e is not None else None
 
     def get_by(self, collection, field, value):
         with self._lock:
@@ -101,7 +126,7 @@ class MemoryEntityStore(EntityStore):
                 return self.get(collection, i) if i is not None else None
             for e in self._data[collection].values():
                 if getattr(e, field, None) == value:
-                    return copy.deepcopy(e)
+                    return _clone(e)
             return None
 
     def delete(self, collection, id):
@@ -117,7 +142,7 @@ class MemoryEntityStore(EntityStore):
     def query(self, collection, predicate=None, sort_key=None, reverse=False):
         with self._lock:
             items = [e for e in self._coll(collection).values() if predicate is None or predicate(e)]
-            items = [copy.deepcopy(e) for e in items]
+            items = [_clone(e) for e in items]
         if sort_key is not None:
             items.sort(key=sort_key, reverse=reverse)
         return items

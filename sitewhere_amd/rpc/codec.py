@@ -31,18 +31,17 @@ def to_wire(obj):
         return {"__t": "SearchResults", "numResults": obj.num_results, "results": [to_wire(r) for r in obj.results]}
     if isinstance(obj, domain.Model):
         d = {"__t": type(obj).__name__}
-        for k, v in obj.to_dict().items():
-            d[k] = v
-        # nested models keep their own tags for polymorphic fields
-        import dataclasses
-        for f in dataclasses.fields(obj):
-            v = getattr(obj, f.name)
+        # one pass over the (cached) fields; nested models keep their own tags (polymorphic fields)
+        for name, key in domain._fields(type(obj)):
+            v = getattr(obj, name)
             if isinstance(v, domain.Model):
-                d[domain.camel(f.name)] = to_wire(v)
+                d[key] = to_wire(v)
             elif isinstance(v, list) and v and isinstance(v[0], domain.Model):
-                d[domain.camel(f.name)] = [to_wire(x) for x in v]
+                d[key] = [to_wire(x) for x in v]
             elif isinstance(v, bytes):
-                d[domain.camel(f.name)] = {"__b": base64.b64encode(v).decode()}
+                d[key] = {"__b": base64.b64encode(v).decode()}
+            else:
+                d[key] = domain._ser(v)
         return d
     if isinstance(obj, bytes):
         return {"__b": base64.b64encode(obj).decode()}
@@ -53,6 +52,16 @@ def to_wire(obj):
     if isinstance(obj, dict):
         return {k: to_wire(v) for k, v in obj.items()}
     return obj
+
+
+_camel_cache: dict = {}
+
+
+def _camel_names(cls) -> dict:
+    n = _camel_cache.get(cls)
+    if n is None:
+        n = _camel_cache[cls] = {c: f for f, c in domain._fields(cls)}
+    return n
 
 
 def from_wire(obj):
@@ -68,8 +77,7 @@ def from_wire(obj):
             body = {k: (from_wire(v) if isinstance(v, (dict, list)) else v) for k, v in obj.items() if k != "__t"}
             cls = _REGISTRY[t]
             m = cls.from_dict({k: v for k, v in body.items() if not isinstance(v, domain.Model)})
-            import dataclasses
-            names = {domain.camel(f.name): f.name for f in dataclasses.fields(cls)}
+            names = _camel_names(cls)
             for k, v in body.items():
                 if k in names and (isinstance(v, (domain.Model, bytes)) or
                                    (isinstance(v, list) and v and isinstance(v[0], domain.Model))):

@@ -2,11 +2,11 @@
 from __future__ import annotations
 
 import dataclasses
-import uuid
 
 from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
 from ..core.security import current_authentication
 from ..models.domain import Model, SearchCriteria, SearchResults, snake, stamp_created, stamp_updated
+from ..utils import fast_uuid4
 
 
 def _user():
@@ -52,7 +52,7 @@ class Crud:
         for k, v in fixed.items():
             setattr(e, k, v)
         if not getattr(e, "token", None):
-            e.token = str(uuid.uuid4())
+            e.token = fast_uuid4()
         if self.s.get_by_token(self.c, e.token) is not None:
             raise SiteWhereSystemException(ErrorCode.DuplicateToken, detail=f"{self.c} token {e.token} in use")
         stamp_created(e, _user())

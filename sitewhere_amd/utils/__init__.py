@@ -1,6 +1,9 @@
 """Small shared helpers (dense id maps, power-of-two sizing, wall-clock timing)."""
 from __future__ import annotations
 
+import os
+import random
+
 import time
 
 
@@ -10,6 +13,28 @@ def pow2_at_least(n: int) -> int:
     while p < n:
         p <<= 1
     return p
+
+
+_rng = random.Random(int.from_bytes(os.urandom(16), "little"))
+if hasattr(os, "register_at_fork"):
+    os.register_at_fork(after_in_child=lambda: _rng.seed(int.from_bytes(os.urandom(16), "little")))
+
+
+def fast_uuid4() -> str:
+    """Random (version 4) UUID string from a process-local PRNG seeded by ``os.urandom``.
+
+    Entity and event ids need uniqueness, not unpredictability.  ``uuid.uuid4()`` reads
+    ``os.urandom`` per call, and that syscall releases the GIL: with the service threads busy,
+    re-acquiring it costs ~200 us per id (measured on the per-event path) -- more than the rest of
+    the event's processing.  ``getrandbits`` never releases the GIL."""
+    n = (_rng.getrandbits(128) & ~(0xF000 << 64) | (0x4000 << 64)) & ~(0xC000 << 48) | (0x8000 << 48)
+    h = f"{n:032x}"
+    return f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:]}"
+
+
+def fast_hex(bits: int = 64) -> str:
+    """Random hex id of ``bits`` bits (trace / span ids)."""
+    return f"{_rng.getrandbits(bits):0{bits // 4}x}"
 
 
 class IndexMap:
