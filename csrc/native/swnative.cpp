@@ -19,6 +19,8 @@
 #include <sys/types.h>
 #include <unistd.h>
 #include <fcntl.h>
+#include <deque>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -270,10 +272,44 @@ static void crc_init() {
     crc32c_table[i] = c;
   }
 }
-static uint32_t crc32c(const uint8_t* p, size_t n, uint32_t c = 0) {
+static uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t c) {
   std::call_once(crc_once, crc_init);
-  c = ~c;
   for (size_t i = 0; i < n; ++i) c = crc32c_table[(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return c;
+}
+
+#if defined(__x86_64__)
+// SSE4.2 crc32 instruction, 8 bytes per step (~8 GB/s vs ~0.3 GB/s for the byte table: the table
+// capped bus appends of multi-MB columnar batches at ~200 MB/s).
+__attribute__((target("sse4.2"))) static uint32_t crc32c_hw(const uint8_t* p, size_t n, uint32_t c) {
+  uint64_t c64 = c;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    c64 = __builtin_ia32_crc32di(c64, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c64;
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return c32;
+}
+static bool crc_hw_available() {
+  static const bool ok = [] {
+    __builtin_cpu_init();          // required before __builtin_cpu_supports during static init
+    return __builtin_cpu_supports("sse4.2") != 0;
+  }();
+  return ok;
+}
+#endif
+
+static uint32_t crc32c(const uint8_t* p, size_t n, uint32_t c = 0) {
+  c = ~c;
+#if defined(__x86_64__)
+  c = crc_hw_available() ? crc32c_hw(p, n, c) : crc32c_sw(p, n, c);
+#else
+  c = crc32c_sw(p, n, c);
+#endif
   return ~c;
 }
 
@@ -286,13 +322,110 @@ struct RecHdr {
 };
 #pragma pack(pop)
 
+// The in-memory image of a partition is a chain of segments (64 MB, huge-page backed, recycled
+// through a per-log pool) instead of one growing vector: growth never re-copies the log, and
+// retention frees whole segments whose memory the next appends reuse (first-touch page faults
+// of fresh memory measured at 0.6-1.8 GB/s in containers, versus memcpy speed for reused pages).
+static const size_t SEG_BYTES = 64u << 20;
+
+struct Segment {
+  uint8_t* buf = nullptr;
+  size_t cap = 0;
+  size_t used = 0;
+};
+
+static uint8_t* seg_map(size_t cap) {
+  void* p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+#ifdef MADV_HUGEPAGE
+  madvise(p, cap, MADV_HUGEPAGE);
+#endif
+  return (uint8_t*)p;
+}
+
+struct SegPool {
+  std::mutex mu;
+  std::vector<uint8_t*> free;      // standard-size segments ready for reuse
+  uint8_t* get(size_t cap) {
+    if (cap == SEG_BYTES) {
+      std::lock_guard<std::mutex> g(mu);
+      if (!free.empty()) {
+        uint8_t* b = free.back();
+        free.pop_back();
+        return b;
+      }
+    }
+    return seg_map(cap);
+  }
+  void put(uint8_t* b, size_t cap) {
+    if (!b) return;
+    if (cap == SEG_BYTES) {
+      std::lock_guard<std::mutex> g(mu);
+      if (free.size() < 16) {
+        free.push_back(b);
+        return;
+      }
+    }
+    munmap(b, cap);
+  }
+  ~SegPool() {
+    for (auto* b : free) munmap(b, SEG_BYTES);
+  }
+};
+
 struct Partition {
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<uint8_t> data;       // in-memory image of the partition log
-  std::vector<int64_t> index;      // record offset -> byte position in data
+  std::deque<Segment> segs;        // in-memory image of the retained log
+  int64_t seg0 = 0;                // ordinal of segs.front()
+  std::deque<int64_t> index;       // per retained record: (segment ordinal << 32) | byte offset in it
   int64_t base_offset = 0;         // first retained offset
+  int64_t bytes = 0;               // record bytes held by retained segments
+  int64_t retention_bytes = 0;     // memory-only logs: drop oldest segments beyond this (0 = keep all)
+  int64_t file_pos = 0;            // durable log: file length
   int fd = -1;                     // durable backing file (append-only), -1 = memory only
+  SegPool* pool = nullptr;
+
+  const uint8_t* rec(int64_t i) const {
+    const int64_t e = index[(size_t)i];
+    return segs[(size_t)((e >> 32) - seg0)].buf + (e & 0xffffffffLL);
+  }
+  // room for `total` contiguous bytes; returns (segment ordinal, offset)
+  bool reserve(size_t total, int64_t* ord, size_t* off) {
+    if (segs.empty() || segs.back().cap - segs.back().used < total) {
+      Segment sg;
+      sg.cap = total > SEG_BYTES ? total : SEG_BYTES;
+      sg.buf = pool->get(sg.cap);
+      if (!sg.buf) return false;
+      segs.push_back(sg);
+    }
+    *ord = seg0 + (int64_t)segs.size() - 1;
+    *off = segs.back().used;
+    segs.back().used += total;
+    bytes += (int64_t)total;
+    return true;
+  }
+  // drop the oldest segment and the records it holds
+  void drop_front_segment() {
+    int64_t n = 0;
+    while (!index.empty() && (index.front() >> 32) == seg0) {
+      index.pop_front();
+      ++n;
+    }
+    base_offset += n;
+    bytes -= (int64_t)segs.front().used;
+    pool->put(segs.front().buf, segs.front().cap);
+    segs.pop_front();
+    ++seg0;
+  }
+  void enforce_retention() {
+    if (fd >= 0 || retention_bytes <= 0) return;
+    // segment-granular like Kafka: the retained log stays >= retention_bytes
+    while (segs.size() > 1 && bytes - (int64_t)segs.front().used >= retention_bytes) drop_front_segment();
+  }
+  ~Partition() {
+    for (auto& sg : segs) pool->put(sg.buf, sg.cap);
+  }
 };
 
 struct Topic {
@@ -303,6 +436,8 @@ struct Topic {
 struct Log {
   std::string dir;                 // empty = in-memory
   int fsync_each = 0;
+  SegPool pool;                    // declared before topics: destroyed after every partition
+  int64_t default_retention = 0;
   std::mutex mu;
   std::vector<std::unique_ptr<Topic>> topics;
   std::map<std::string, int> by_name;
@@ -324,31 +459,36 @@ static void load_partition(Partition* pt, const std::string& path) {
   if (fd < 0) return;
   struct stat st;
   fstat(fd, &st);
-  pt->data.resize((size_t)st.st_size);
+  const size_t fsize = (size_t)st.st_size;
   size_t got = 0;
-  while (got < pt->data.size()) {
-    ssize_t r = pread(fd, pt->data.data() + got, pt->data.size() - got, (off_t)got);
-    if (r <= 0) break;
-    got += (size_t)r;
+  int64_t ord = 0;
+  size_t off = 0;
+  if (fsize > 0 && pt->reserve(fsize, &ord, &off)) {
+    uint8_t* img = pt->segs.back().buf;
+    while (got < fsize) {
+      ssize_t r = pread(fd, img + got, fsize - got, (off_t)got);
+      if (r <= 0) break;
+      got += (size_t)r;
+    }
+    // rebuild the index, truncating a torn tail record (crash during append)
+    size_t pos = 0;
+    while (pos + sizeof(RecHdr) <= got) {
+      RecHdr h;
+      memcpy(&h, img + pos, sizeof(h));
+      size_t end = pos + sizeof(RecHdr) + h.len;
+      if (end > got) break;
+      uint32_t c = crc32c((const uint8_t*)&h.ts, sizeof(h.ts) + sizeof(h.klen));
+      c = crc32c(img + pos + sizeof(RecHdr), h.len, c);
+      if (c != h.crc) break;
+      pt->index.push_back((ord << 32) | (int64_t)pos);
+      pos = end;
+    }
+    pt->segs.back().used = pos;
+    pt->bytes -= (int64_t)(fsize - pos);
+    if (pos != fsize && ftruncate(fd, (off_t)pos) != 0) { /* best effort */ }
+    got = pos;
   }
-  pt->data.resize(got);
-  // rebuild index, truncating a torn tail record (crash during append)
-  size_t pos = 0;
-  while (pos + sizeof(RecHdr) <= pt->data.size()) {
-    RecHdr h;
-    memcpy(&h, pt->data.data() + pos, sizeof(h));
-    size_t end = pos + sizeof(RecHdr) + h.len;
-    if (end > pt->data.size()) break;
-    uint32_t c = crc32c((const uint8_t*)&h.ts, sizeof(h.ts) + sizeof(h.klen));
-    c = crc32c(pt->data.data() + pos + sizeof(RecHdr), h.len, c);
-    if (c != h.crc) break;
-    pt->index.push_back((int64_t)pos);
-    pos = end;
-  }
-  if (pos != pt->data.size()) {
-    pt->data.resize(pos);
-    if (ftruncate(fd, (off_t)pos) != 0) { /* best effort */ }
-  }
+  pt->file_pos = (int64_t)got;
   pt->fd = fd;
 }
 
@@ -429,6 +569,8 @@ int32_t swlog_topic(void* h, const char* name, int32_t partitions) {
   }
   for (int p = 0; p < partitions; ++p) {
     auto pt = std::make_unique<Partition>();
+    pt->pool = &L->pool;
+    pt->retention_bytes = L->default_retention;
     if (!tdir.empty()) load_partition(pt.get(), tdir + "/" + std::to_string(p) + ".log");
     t->parts.push_back(std::move(pt));
   }
@@ -460,11 +602,17 @@ int64_t swlog_append_batch(void* h, int32_t topic, int32_t p, const uint8_t* key
   Log* L = (Log*)h;
   Partition* pt = part_of(L, topic, p);
   if (!pt) return -1;
-  std::vector<uint8_t> enc;
   size_t total = 0;
   for (int64_t i = 0; i < n; ++i) total += sizeof(RecHdr) + (koff[i + 1] - koff[i]) + (voff[i + 1] - voff[i]);
-  enc.resize(total);
+  if (total >= (1ull << 32)) return -1;           // a batch must fit one segment (32-bit offsets)
   std::vector<int64_t> rel(n);
+  // encode straight into the partition image (one pass: copy + crc), no staging buffer
+  std::unique_lock<std::mutex> g(pt->mu);
+  const int64_t first = pt->base_offset + (int64_t)pt->index.size();
+  int64_t ord = 0;
+  size_t soff = 0;
+  if (!pt->reserve(total, &ord, &soff)) return -1;
+  uint8_t* enc = pt->segs.back().buf + soff;
   size_t pos = 0;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t kl = koff[i + 1] - koff[i], vl = voff[i + 1] - voff[i];
@@ -472,29 +620,31 @@ int64_t swlog_append_batch(void* h, int32_t topic, int32_t p, const uint8_t* key
     hd.len = (uint32_t)(kl + vl);
     hd.ts = ts ? ts[i] : 0;
     hd.klen = (uint16_t)kl;
-    uint8_t* dst = enc.data() + pos + sizeof(RecHdr);
+    uint8_t* dst = enc + pos + sizeof(RecHdr);
     memcpy(dst, keys + koff[i], (size_t)kl);
     memcpy(dst + kl, vals + voff[i], (size_t)vl);
     uint32_t c = crc32c((const uint8_t*)&hd.ts, sizeof(hd.ts) + sizeof(hd.klen));
     hd.crc = crc32c(dst, (size_t)(kl + vl), c);
-    memcpy(enc.data() + pos, &hd, sizeof(hd));
+    memcpy(enc + pos, &hd, sizeof(hd));
     rel[i] = (int64_t)pos;
     pos += sizeof(RecHdr) + (size_t)(kl + vl);
   }
-  std::unique_lock<std::mutex> g(pt->mu);
-  const int64_t first = pt->base_offset + (int64_t)pt->index.size();
-  const int64_t base = (int64_t)pt->data.size();
   if (pt->fd >= 0) {
     size_t w = 0;
-    while (w < enc.size()) {
-      ssize_t r = pwrite(pt->fd, enc.data() + w, enc.size() - w, (off_t)(base + (int64_t)w));
-      if (r <= 0) return -1;
+    while (w < total) {
+      ssize_t r = pwrite(pt->fd, enc + w, total - w, (off_t)(pt->file_pos + (int64_t)w));
+      if (r <= 0) {
+        pt->segs.back().used = soff;               // nothing becomes visible
+        pt->bytes -= (int64_t)total;
+        return -1;
+      }
       w += (size_t)r;
     }
+    pt->file_pos += (int64_t)total;
     if (L->fsync_each) fdatasync(pt->fd);
   }
-  pt->data.insert(pt->data.end(), enc.begin(), enc.end());
-  for (int64_t i = 0; i < n; ++i) pt->index.push_back(base + rel[i]);
+  for (int64_t i = 0; i < n; ++i) pt->index.push_back((ord << 32) | (int64_t)(soff + rel[i]));
+  pt->enforce_retention();
   g.unlock();
   pt->cv.notify_all();
   return first;
@@ -543,7 +693,8 @@ int64_t swlog_read(void* h, int32_t topic, int32_t p, int64_t offset, int64_t ma
   int64_t i = offset - pt->base_offset, w = 0, cnt = 0;
   while (i < (int64_t)pt->index.size() && cnt < max_records) {
     RecHdr hd;
-    memcpy(&hd, pt->data.data() + pt->index[i], sizeof(hd));
+    const uint8_t* r = pt->rec(i);
+    memcpy(&hd, r, sizeof(hd));
     const int64_t need = 24 + (int64_t)hd.len;
     if (w + need > out_cap) {
       if (cnt == 0) return -need;
@@ -555,7 +706,7 @@ int64_t swlog_read(void* h, int32_t topic, int32_t p, int64_t offset, int64_t ma
     memcpy(out + w + 8, &hd.ts, 8);
     memcpy(out + w + 16, &kl, 4);
     memcpy(out + w + 20, &vl, 4);
-    memcpy(out + w + 24, pt->data.data() + pt->index[i] + sizeof(RecHdr), hd.len);
+    memcpy(out + w + 24, r + sizeof(RecHdr), hd.len);
     w += need;
     ++cnt;
     ++i;
@@ -571,14 +722,36 @@ int64_t swlog_retain_from(void* h, int32_t topic, int32_t p, int64_t offset) {
   std::lock_guard<std::mutex> g(pt->mu);
   int64_t drop = offset - pt->base_offset;
   if (drop <= 0) return pt->base_offset;
-  if (drop > (int64_t)pt->index.size()) drop = (int64_t)pt->index.size();
   if (pt->fd >= 0) return pt->base_offset;  // durable logs keep the in-memory image aligned with the file
-  const int64_t cut = drop < (int64_t)pt->index.size() ? pt->index[drop] : (int64_t)pt->data.size();
-  pt->data.erase(pt->data.begin(), pt->data.begin() + cut);
-  pt->index.erase(pt->index.begin(), pt->index.begin() + drop);
-  for (auto& x : pt->index) x -= cut;
+  if (drop > (int64_t)pt->index.size()) drop = (int64_t)pt->index.size();
+  for (int64_t k = 0; k < drop; ++k) pt->index.pop_front();
   pt->base_offset += drop;
+  // free whole segments that no retained record points into (keep the tail segment for appends)
+  while (pt->segs.size() > 1 && (pt->index.empty() || (pt->index.front() >> 32) > pt->seg0)) pt->drop_front_segment();
   return pt->base_offset;
+}
+
+// Memory-only logs: cap the retained bytes of every partition of `topic` (0 = unlimited);
+// topic < 0 sets the default for topics created later.
+int32_t swlog_set_retention(void* h, int32_t topic, int64_t bytes) {
+  Log* L = (Log*)h;
+  if (topic < 0) {
+    std::lock_guard<std::mutex> g(L->mu);
+    L->default_retention = bytes;
+    return 0;
+  }
+  std::vector<Partition*> ps;
+  {
+    std::lock_guard<std::mutex> g(L->mu);
+    if (topic >= (int)L->topics.size()) return -1;
+    for (auto& pt : L->topics[topic]->parts) ps.push_back(pt.get());
+  }
+  for (auto* pt : ps) {
+    std::lock_guard<std::mutex> g(pt->mu);
+    pt->retention_bytes = bytes;
+    pt->enforce_retention();
+  }
+  return 0;
 }
 
 static std::string topic_name(Log* L, int32_t topic) {

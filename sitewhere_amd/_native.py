@@ -136,6 +136,7 @@ def native():
         _proto(lib, "swlog_commit", c_int32, P, c_char_p, c_int32, c_int32, c_int64)
         _proto(lib, "swlog_committed", c_int64, P, c_char_p, c_int32, c_int32)
         _proto(lib, "swlog_flush", c_int32, P)
+        _proto(lib, "swlog_set_retention", c_int32, P, c_int32, c_int64)
         _native = lib
         return lib
 

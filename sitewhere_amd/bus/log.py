@@ -91,12 +91,17 @@ class EventBus:
     """In-process broker: topics, partitions, consumer-group coordinator, committed offsets."""
 
     def __init__(self, directory: str | None = None, default_partitions: int = 8, fsync: bool = False,
-                 session_timeout_s: float = 30.0):
+                 session_timeout_s: float = 30.0, retention_bytes: int | None = None):
         self.lib = native()
         self.h = self.lib.swlog_open(directory.encode() if directory else None, 1 if fsync else 0)
         # microsecond calls keep the GIL (PyDLL); opening, flushing and closing go through CDLL
         self.fast = native_gil() if not fsync else self.lib
         self._tls = threading.local()
+        # memory-only logs keep at most this many bytes per partition (Kafka retention.bytes);
+        # lagging consumers resume at the oldest retained offset.  Durable logs keep everything.
+        if retention_bytes is None:
+            retention_bytes = 0 if directory else (1 << 30)
+        self.lib.swlog_set_retention(self.h, -1, int(retention_bytes))
         self.directory = directory
         self.default_partitions = default_partitions
         self.session_timeout_s = session_timeout_s
@@ -230,6 +235,10 @@ class EventBus:
 
     def committed(self, group: str, name: str, partition: int) -> int:
         return self.fast.swlog_committed(self.h, group.encode(), self.topic(name), partition)
+
+    def set_retention(self, name: str, retention_bytes: int):
+        """Cap the retained bytes of every partition of a memory-only topic (0 = unlimited)."""
+        self.lib.swlog_set_retention(self.h, self.topic(name), int(retention_bytes))
 
     def retain_from(self, name: str, partition: int, offset: int) -> int:
         return self.lib.swlog_retain_from(self.h, self.topic(name), partition, offset)

@@ -104,6 +104,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                                         self._process_raw, max_records=16, auto_commit=self.ckpt_path is None)
         self.persisted_events = self.create_meter("persistedEvents")
         self.step_timer = self.create_timer("engineStep")
+        self.store_timer = self.create_timer("columnarStore")       # payload build + event-management call
+        self.publish_timer = self.create_timer("enrichedPublish")
         self.api = {"InboundProcessing": GpuInboundApi(self)}
 
     def _make_engine(self, device: str, ecfg: EngineConfig):
@@ -284,13 +286,15 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         return encode_batch(self.boot, res.first_seq, res.world, res.rank, now, out, asg, names, rules)
 
     def _store_columnar(self, res, now: int):
-        payload = self.columnar_payload(res, now)
-        n = self._em().add_columnar_batch(payload)
+        with self.store_timer.time():
+            payload = self.columnar_payload(res, now)
+            n = self._em().add_columnar_batch(payload)
         self.persisted_events.mark(n)
-        if self.publish == "batches":
-            self.ms.producer.send(self.t_enriched_batches, None, payload)
-        elif self.publish == "events":
-            self._publish_events(self._to_events(res, now))
+        with self.publish_timer.time():
+            if self.publish == "batches":
+                self.ms.producer.send(self.t_enriched_batches, None, payload)
+            elif self.publish == "events":
+                self._publish_events(self._to_events(res, now))
 
     def _publish_events(self, events):
         if events:

@@ -345,3 +345,41 @@ def test_every_microservice_has_a_configuration_model():
     for tpl in TENANT_TEMPLATES.values():
         for svc, doc in tpl["services"].items():
             assert model_for(svc).validate(doc) == [], (svc, doc)
+
+
+def test_bus_memory_retention_frees_whole_segments():
+    """Memory-only logs keep at most retention_bytes per partition (64 MB segments are freed and
+    recycled whole); a consumer behind the retained range resumes at the oldest retained record."""
+    import os
+    from sitewhere_amd.bus.log import EventBus
+    bus = EventBus(None, default_partitions=1, retention_bytes=100 << 20)
+    v = os.urandom(1 << 20)
+    for i in range(300):
+        bus.append("big", 0, [(f"k{i}".encode(), v[:-8] + i.to_bytes(8, "little"))])
+    begin, end = bus.begin_offset("big", 0), bus.end_offset("big", 0)
+    assert end == 300 and 0 < begin and end - begin >= 100       # ~100-164 MB retained
+    first = bus.read("big", 0, 0, 1, 2 << 20)[0]                  # behind the range: clamped
+    assert first.offset == begin and first.value[-8:] == begin.to_bytes(8, "little")
+    last = bus.read("big", 0, 299, 1, 2 << 20)[0]
+    assert last.key == b"k299" and last.value[:-8] == v[:-8]
+    bus.retain_from("big", 0, 290)
+    assert bus.begin_offset("big", 0) == 290
+    assert [r.offset for r in bus.read("big", 0, 0, 20, 32 << 20)] == list(range(290, 300))
+    bus.close()
+
+
+def test_bus_durable_reload_after_large_batches(tmp_path):
+    """Durable partitions survive reopen with records spanning several appends (segments)."""
+    import os
+    from sitewhere_amd.bus.log import EventBus
+    bus = EventBus(str(tmp_path / "d"), default_partitions=1)
+    vals = [os.urandom(3 << 20) for _ in range(5)]
+    for v in vals:
+        bus.append("t", 0, [(None, v)])
+    bus.close()
+    bus2 = EventBus(str(tmp_path / "d"), default_partitions=1)
+    assert bus2.end_offset("t", 0) == 5
+    assert [r.value for r in bus2.read("t", 0, 0, 10, 32 << 20)] == vals
+    bus2.append("t", 0, [(None, b"tail")])
+    assert bus2.read("t", 0, 5, 1)[0].value == b"tail"
+    bus2.close()
