@@ -47,7 +47,7 @@ def decode_batch(payload: bytes) -> dict:
 
 
 class ColumnarEventStore(DeviceEventStore):
-    def __init__(self, consolidate_every: int = 64):
+    def __init__(self, consolidate_every: int = 64, dense_rows: int = 4096):
         self._objects = MemoryEventStore()
         self._chunks: list[dict] = []
         self._pending: list[dict] = []
@@ -58,6 +58,7 @@ class ColumnarEventStore(DeviceEventStore):
         self._high: dict[tuple, int] = {}       # (boot, rank) -> next store sequence not yet held
         self._lock = threading.RLock()
         self.consolidate_every = consolidate_every
+        self.dense_rows = dense_rows
         self.rows = 0
 
     # ------------------------------------------------------------------ ingest
@@ -82,13 +83,45 @@ class ColumnarEventStore(DeviceEventStore):
                 d = dict(d, first_seq=first)
             if n:
                 self._high[key] = max(high, first + n)
-                eid = (d["first_seq"] + np.arange(n, dtype=np.int64)) * d["world"] + d["rank"]
-                self._pending.append({"boot": np.full(n, self._boots.index(d["boot"]), np.int16), "eid": eid,
-                                      "rows": rows, "recv": np.full(n, d["now"], np.int64)})
+                bi = self._boots.index(d["boot"])
+                if n >= self.dense_rows:
+                    # large batch: zero-copy rows + scalar metadata, ids computed when queried
+                    self._chunks.append({"rows": rows, "boot_i": bi, "first": first, "world": int(d["world"]),
+                                         "rank": int(d["rank"]), "now": int(d["now"])})
+                else:
+                    eid = (first + np.arange(n, dtype=np.int64)) * d["world"] + d["rank"]
+                    self._pending.append({"boot": np.full(n, bi, np.int16), "eid": eid,
+                                          "rows": rows, "recv": np.full(n, d["now"], np.int64)})
+                    if len(self._pending) >= self.consolidate_every:
+                        self._consolidate()
                 self.rows += n
-                if len(self._pending) >= self.consolidate_every:
-                    self._consolidate()
         return n
+
+    # chunk accessors: dense chunks (scalar metadata) and consolidated small batches (per-row arrays)
+    @staticmethod
+    def _eids(ch: dict, idx: np.ndarray) -> np.ndarray:
+        if "eid" in ch:
+            return ch["eid"][idx]
+        return (ch["first"] + np.asarray(idx, np.int64)) * ch["world"] + ch["rank"]
+
+    @staticmethod
+    def _boot_of(ch: dict, i: int) -> int:
+        return int(ch["boot"][i]) if "boot" in ch else ch["boot_i"]
+
+    @staticmethod
+    def _recv_of(ch: dict, i: int) -> int:
+        return int(ch["recv"][i]) if "recv" in ch else ch["now"]
+
+    @staticmethod
+    def _find_eid(ch: dict, b: int, eid: int) -> int:
+        """Row of event id ``eid`` (boot index ``b``) in ``ch``, -1 if absent."""
+        if "eid" in ch:
+            hit = np.nonzero((ch["eid"] == eid) & (ch["boot"] == b))[0]
+            return int(hit[0]) if len(hit) else -1
+        if ch["boot_i"] != b or (eid - ch["rank"]) % ch["world"]:
+            return -1
+        row = (eid - ch["rank"]) // ch["world"] - ch["first"]
+        return int(row) if 0 <= row < len(ch["rows"]) else -1
 
     def _consolidate(self):
         if not self._pending:
@@ -120,9 +153,9 @@ class ColumnarEventStore(DeviceEventStore):
         if sep and boot in self._boots and num.isdigit():
             b, eid = self._boots.index(boot), int(num)
             for c in self._all_chunks():
-                hit = np.nonzero((c["eid"] == eid) & (c["boot"] == b))[0]
-                if len(hit):
-                    return self._materialize(c, int(hit[0]))
+                row = self._find_eid(c, b, eid)
+                if row >= 0:
+                    return self._materialize(c, row)
             return None
         return self._objects.get_event_by_id(id)
 
@@ -150,7 +183,7 @@ class ColumnarEventStore(DeviceEventStore):
                 m &= r["event_date"] <= c.end_date
             idx = np.nonzero(m)[0]
             if len(idx):
-                hits.append((r["event_date"][idx], np.full(len(idx), ci, np.int32), idx, ch["eid"][idx]))
+                hits.append((r["event_date"][idx], np.full(len(idx), ci, np.int32), idx, self._eids(ch, idx)))
         total = sum(len(h[0]) for h in hits) + len(objs)
         if not hits:
             return SearchResults(total, c.slice(objs))
@@ -173,9 +206,9 @@ class ColumnarEventStore(DeviceEventStore):
     def _materialize(self, ch: dict, i: int):
         r = ch["rows"][i]
         ctx = self._asg.get(int(r["assignment"]), [None] * 5)
-        base = dict(id=f"{self._boots[int(ch['boot'][i])]}-{int(ch['eid'][i])}", device_assignment_id=ctx[0],
-                    device_id=ctx[1], customer_id=ctx[2], area_id=ctx[3], asset_id=ctx[4],
-                    event_date=int(r["event_date"]), received_date=int(ch["recv"][i]))
+        base = dict(id=f"{self._boots[self._boot_of(ch, i)]}-{int(self._eids(ch, np.array([i]))[0])}",
+                    device_assignment_id=ctx[0], device_id=ctx[1], customer_id=ctx[2], area_id=ctx[3],
+                    asset_id=ctx[4], event_date=int(r["event_date"]), received_date=self._recv_of(ch, i))
         et = int(r["etype"])
         name = self._names.get(int(r["name_id"]), "") if int(r["name_id"]) != NO_NAME else ""
         if et == EV_MEASUREMENT:

@@ -383,3 +383,33 @@ def test_bus_durable_reload_after_large_batches(tmp_path):
     bus2.append("t", 0, [(None, b"tail")])
     assert bus2.read("t", 0, 5, 1)[0].value == b"tail"
     bus2.close()
+
+
+def test_columnar_store_dense_and_small_batches():
+    """Large batches are kept zero-copy with ids computed on query; small ones are consolidated.
+    Both serve get-by-id and index queries (newest first), and replays are skipped."""
+    import numpy as np
+    from sitewhere_amd.models.columnar import OUT_REC
+    from sitewhere_amd.models.domain import DeviceEventIndex, DeviceEventType, DateRangeSearchCriteria
+    from sitewhere_amd.persistence.columnar import ColumnarEventStore, encode_batch
+    st = ColumnarEventStore(dense_rows=100)
+    asg = {0: ["a0", "d0", "c0", "ar0", None], 1: ["a1", "d1", "c1", "ar1", None]}
+
+    def rows(n, d0):
+        r = np.zeros(n, OUT_REC)
+        r["event_date"] = d0 + np.arange(n)
+        r["v0"] = np.arange(n, dtype=np.float64)
+        r["assignment"] = np.arange(n) % 2
+        r["name_id"] = 0
+        return r
+    assert st.add_columnar(encode_batch("b", 0, 2, 1, 5, rows(500, 1000), asg, {0: "t"})) == 500     # dense
+    assert st.add_columnar(encode_batch("b", 500, 2, 1, 6, rows(10, 9000), {}, {})) == 10            # small
+    assert st.add_columnar(encode_batch("b", 0, 2, 1, 5, rows(500, 1000), {}, {})) == 0              # replay
+    e = st.get_event_by_id(f"b-{(7 * 2) + 1}")                 # seq 7 of the dense batch
+    assert e.value == 7.0 and e.device_assignment_id == "a1" and e.received_date == 5
+    e = st.get_event_by_id(f"b-{(503 * 2) + 1}")               # seq 503 = row 3 of the small batch
+    assert e.event_date == 9003 and e.received_date == 6
+    assert st.get_event_by_id("b-2") is None                   # rank 0 id: not this shard's
+    res = st.list_events(DeviceEventType.Measurement, DeviceEventIndex.Assignment, ["a0"],
+                         DateRangeSearchCriteria(page_size=3))
+    assert res.num_results == 255 and [m.event_date for m in res.results] == [9008, 9006, 9004]
