@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--batches", type=int, default=4, help="distinct pre-generated batches to cycle")
     ap.add_argument("--zones", type=int, default=16)
     ap.add_argument("--store", type=int, default=1 << 27, help="HBM event-store capacity per GPU (events)")
-    ap.add_argument("--engine", choices=["gpu", "cpu"], default="gpu")
+    ap.add_argument("--engine", choices=["gpu", "cpu", "oracle"], default="gpu",
+                    help="gpu: MI355X kernels; cpu: native multi-threaded C++ engine; oracle: Python reference")
     ap.add_argument("--framing", choices=["varint", "offsets"], default="varint",
                     help="raw-batch framing on the wire to the GPU (varint lengths or u32 offsets)")
     ap.add_argument("--no-outbound", action="store_true", help="(diagnostic) skip the D2H outbound copy")
@@ -88,6 +89,9 @@ def main():
     if use_gpu:
         from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine, PipelinedRunner
         eng = GpuInboundEngine(cfg, device=torch.device("cuda", local), group=None)
+    elif args.engine == "cpu":
+        from sitewhere_amd.pipeline.native_engine import NativeCpuEngine
+        eng = NativeCpuEngine(cfg)
     else:
         from sitewhere_amd.pipeline.cpu_engine import CpuInboundEngine
         eng = CpuInboundEngine(cfg)
@@ -199,6 +203,7 @@ def main():
                 "tenants": 1,
                 "zones": args.zones,
                 "engine": args.engine,
+                "cpu_threads": getattr(eng, "threads", None),
                 "framing": args.framing,
             },
             "detail": {

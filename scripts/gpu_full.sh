@@ -3,7 +3,7 @@
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O=gpurun_out/full
 cd "$R" && export TMPDIR=/tmp && mkdir -p $O/prof
-timeout -k 10 900 python -m pytest tests -m gpu -q > $O/pytest_gpu.log 2>&1 && echo "pytest gpu ok" && tail -1 $O/pytest_gpu.log &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo "pytest gpu ok" && tail -1 $O/pytest_gpu.log &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log &&
 timeout -k 10 400 python bench.py > $O/bench_default.log 2>&1 && tail -1 $O/bench_default.log | cut -c1-160 &&
 timeout -k 10 400 python bench.py --steps 50 --warmup 10 > $O/bench_50.log 2>&1 && tail -1 $O/bench_50.log | cut -c1-160 &&

@@ -3,7 +3,8 @@
 Two shared objects are built **in-tree** under ``sitewhere_amd/_lib``:
 
 * ``libswnative.so`` (g++): the host runtime -- partitioned commit log
-  (Kafka replacement), registry builder, CPU batch decoder, fleet generator.
+  (Kafka replacement), registry builder, CPU batch decoder, fleet generator,
+  and the multi-threaded native CPU engine shard (``swce_*``).
 * ``libswgpu.so`` (hipcc ``--offload-arch=gfx950``): the CDNA4 data-plane kernels.
 
 Both expose a plain C ABI and are loaded with :mod:`ctypes`; there is no
@@ -25,7 +26,7 @@ LIB_DIR = Path(__file__).resolve().parent / "_lib"
 CSRC = ROOT / "csrc"
 GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
 
-_NATIVE_SRC = [CSRC / "native" / "swnative.cpp"]
+_NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp"]
 _GPU_SRC = [CSRC / "hip" / "swgpu.hip"]
 _HEADERS = sorted((CSRC / "include").glob("*.h"))
 
@@ -137,6 +138,24 @@ def native():
         _proto(lib, "swlog_committed", c_int64, P, c_char_p, c_int32, c_int32)
         _proto(lib, "swlog_flush", c_int32, P)
         _proto(lib, "swlog_set_retention", c_int32, P, c_int32, c_int64)
+        # native CPU engine shard (csrc/native/swcpuengine.cpp)
+        _proto(lib, "swce_create", P, c_int32)
+        _proto(lib, "swce_destroy", None, P)
+        _proto(lib, "swce_threads", c_int32, P)
+        _proto(lib, "swce_reserve", None, P, c_int64, c_int64)
+        _proto(lib, "swce_capture_names", c_int64, P, P, c_int64, P, c_int64)
+        _proto(lib, "swce_process", c_int32, P, P, P, P, c_int64, c_int64, c_int32, P, P)
+        for kind in ("dedup", "intern", "seen", "ms"):
+            _proto(lib, f"swce_{kind}_size", c_int64, P)
+        _proto(lib, "swce_dedup_export", c_int64, P, P, P)
+        _proto(lib, "swce_dedup_import", None, P, P, P, c_int64)
+        _proto(lib, "swce_intern_export", c_int64, P, P, P)
+        _proto(lib, "swce_intern_import", None, P, P, P, c_int64)
+        _proto(lib, "swce_seen_export", c_int64, P, P)
+        _proto(lib, "swce_seen_import", None, P, P, c_int64)
+        _proto(lib, "swce_ms_export", c_int64, P, P)
+        _proto(lib, "swce_ms_import", None, P, P, c_int64)
+        _proto(lib, "swce_ms_of", c_int64, P, c_int32, P, c_int64)
         _native = lib
         return lib
 

@@ -106,15 +106,21 @@ def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndar
 
 
 def cpu_decode(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, cap: int | None = None,
-               threads: int = 4):
-    """Decode a raw batch on the CPU with the shared decoder; returns an EVENT_REC array."""
+               threads: int = 4, out: np.ndarray | None = None):
+    """Decode a raw batch on the CPU with the shared decoder; returns an EVENT_REC array.
+
+    ``out`` (EVENT_REC, reused across batches) avoids a fresh allocation per batch; the decoder
+    writes every byte of each record it returns, so it need not be zeroed."""
     from ..models.columnar import EVENT_REC
 
     lib = native()
     n_msgs = len(offs) - 1
-    if cap is None:
-        cap = max(16, n_msgs * 4)
-    out = np.zeros(cap, EVENT_REC)
+    if out is not None:
+        cap = len(out) if cap is None else min(cap, len(out))
+    else:
+        if cap is None:
+            cap = max(16, n_msgs * 4)
+        out = np.zeros(cap, EVENT_REC)
     raw = np.ascontiguousarray(raw, np.uint8)
     offs = np.ascontiguousarray(offs, np.uint32)
     n = lib.sw_cpu_decode(_ptr(raw) if raw.size else 0, _ptr(offs), n_msgs, now_ms, rank, _ptr(out), cap, threads)

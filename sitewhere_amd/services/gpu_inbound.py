@@ -16,7 +16,8 @@ engine does not persist but that need a control-plane decision (unregistered dev
 acknowledgements, streams) take a slow path: the batch is re-decoded on the host and those messages
 are routed exactly like the reference routes them (unregistered / registration topics).
 
-``device`` config: ``"gpu"`` (fail loudly without a GPU), ``"cpu"`` (the oracle engine) or ``"auto"``.
+``device`` config: ``"gpu"`` (fail loudly without a GPU), ``"cpu"`` (the native multi-threaded C++ engine,
+``pipeline/native_engine.py``), ``"oracle"`` (the Python reference engine) or ``"auto"`` (GPU if present).
 """
 from __future__ import annotations
 
@@ -122,9 +123,12 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     raise
             if want_gpu:
                 raise RuntimeError("inbound-processing configured with device=gpu but no GPU is available")
-        from ..pipeline.cpu_engine import CpuInboundEngine
         self.engine_kind = "cpu"
-        return CpuInboundEngine(ecfg)
+        if device == "oracle":
+            from ..pipeline.cpu_engine import CpuInboundEngine
+            return CpuInboundEngine(ecfg)
+        from ..pipeline.native_engine import NativeCpuEngine
+        return NativeCpuEngine(ecfg, threads=int(self.config.get("cpuThreads", 0)) or None)
 
     # ---------------------------------------------------------------- registry mirror
     def _dm(self):
