@@ -1,0 +1,337 @@
+"""BASELINE.json config #1 on CPU: events/s and ingest -> enriched latency through the reference
+architecture, plus the same tenant on the fused engine path.
+
+BASELINE.md asks the rebuild to produce this first baseline itself (the reference publishes none):
+1 tenant, synthetic device events, decode -> inbound validation -> event persistence -> enrichment ->
+consumers, reporting sustained events/s and p50/p99 ingest -> enriched latency, at 1, 2, 4 and 8
+consumer replicas.
+
+Paths measured (``--path``):
+
+* ``per-event`` -- the reference design: event-sources decode each protobuf payload ->
+  ``event-source-decoded-events`` -> inbound-processing (device + assignment lookup through the
+  near cache / device-management RPC) -> event-management persist -> ``inbound-persisted-events``
+  -> enrichment -> ``inbound-enriched-events`` -> device-state, rule-processing, outbound connectors.
+  ``--replicas N`` runs N inbound-processing replicas as separate processes (one consumer group,
+  partitions split between them) against a shared infra server, with device/event management,
+  device state and event sources in their own processes -- the reference's deployment shape.
+  ``--replicas 0`` runs everything in this process over the in-process bus.
+* ``engine`` -- a ``gpu-columnar`` tenant (fused engine; the native CPU engine without a GPU):
+  raw payload batches -> engine -> columnar store -> ``inbound-enriched-batches``.
+
+Latency: each event carries its sequence number in ``alternateId``; a consumer group of this
+script on the enriched topic stamps arrival.  Throughput phase: a burst of ``--events`` injected
+back to back, rate = events / time until the last one is enriched.  Latency phase: a paced stream
+at ``--load`` x the measured throughput, so the percentiles describe the pipeline, not a queue.
+
+    python scripts/bench_reference_config.py --path per-event --replicas 0 --events 1000
+    python scripts/bench_reference_config.py --path per-event --replicas 4 --events 5000
+    python scripts/bench_reference_config.py --path engine --events 200000
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+_ALT = re.compile(rb'"alternateId": "([bp])-(\d+)"')
+TOKENS = [f"{t}-{i:03d}" for t in ("galaxytab", "meitrack", "raspberrypi", "iphone6s", "openhab") for i in range(4)]
+
+
+def percentiles(lat_ms: np.ndarray) -> dict:
+    if not len(lat_ms):
+        return {}
+    p50, p90, p99 = np.percentile(lat_ms, [50, 90, 99])
+    return {"p50_ms": round(float(p50), 3), "p90_ms": round(float(p90), 3), "p99_ms": round(float(p99), 3),
+            "max_ms": round(float(lat_ms.max()), 3), "n": int(len(lat_ms))}
+
+
+class EnrichedWatcher:
+    """Consumer group on the enriched topic; records arrival time per alternate id."""
+
+    def __init__(self, bus, topic: str, n_burst: int, n_paced: int):
+        self.c = bus.consumer(f"bench-latency-{os.getpid()}-{time.time_ns()}", [topic], auto_offset_reset="latest")
+        self.arr = {b"b": np.zeros(n_burst), b"p": np.zeros(n_paced)}
+        self.seen = {b"b": 0, b"p": 0}
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def start(self):
+        self.c.poll(10)     # join + position at the end before anything is injected
+        self._t.start()
+        return self
+
+    def _run(self):
+        while not self._stop.is_set():
+            recs = self.c.poll(100, max_records=2000)
+            now = time.perf_counter()
+            for rs in recs.values():
+                for r in rs:
+                    m = _ALT.search(r.value)
+                    if m:
+                        kind, i = m.group(1), int(m.group(2))
+                        a = self.arr[kind]
+                        if i < len(a) and a[i] == 0:
+                            a[i] = now
+                            self.seen[kind] += 1
+
+    def wait(self, kind: bytes, n: int, timeout_s: float) -> bool:
+        end = time.time() + timeout_s
+        while self.seen[kind] < n and time.time() < end:
+            time.sleep(0.005)
+        return self.seen[kind] >= n
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(2)
+
+
+def payloads(kind: str, n: int):
+    from sitewhere_amd.models import wire
+    return [wire.measurements(TOKENS[i % len(TOKENS)], {"m": float(i)}, event_date=1_700_000_000_000 + i,
+                              alternate_id=f"{kind}-{i}") for i in range(n)]
+
+
+def decoded_records(kind: str, n: int):
+    """``event-source-decoded-events`` records (what EventSourcesManager.handle_decoded_event writes),
+    keyed by device token: the Kafka ingress of inbound processing."""
+    from sitewhere_amd.rpc import codec
+    out = []
+    for i in range(n):
+        tok = TOKENS[i % len(TOKENS)]
+        req = {"eventDate": 1_700_000_000_000 + i, "alternateId": f"{kind}-{i}", "name": "m", "value": float(i),
+               "metadata": {}}
+        body = {"sourceId": "bench", "deviceToken": tok, "originator": None,
+                "eventCreateRequest": {"type": "DeviceMeasurement", "request": req}}
+        out.append((tok, json.dumps(codec.to_wire(body)).encode()))
+    return out
+
+
+def run_phases(inject, watcher, n_burst: int, n_paced: int, load: float, timeout_s: float,
+               make=None, inject_many=None) -> dict:
+    """inject(payload) per event; with ``inject_many`` the burst goes in chunks of 200."""
+    make = make or payloads
+    burst = make("b", n_burst)
+    t0 = time.perf_counter()
+    if inject_many is not None:
+        for i in range(0, n_burst, 200):
+            inject_many(burst[i:i + 200])
+    else:
+        for p in burst:
+            inject(p)
+    t_inj = time.perf_counter() - t0
+    ok = watcher.wait(b"b", n_burst, timeout_s)
+    arr = watcher.arr[b"b"]
+    t_done = (arr.max() - t0) if ok else float("nan")
+    rate = n_burst / t_done if ok else 0.0
+    out = {"burst_events": n_burst, "burst_complete": ok, "inject_s": round(t_inj, 3),
+           "events_per_sec": round(rate, 1),
+           "burst_latency": percentiles(1000 * (arr[arr > 0] - t0))}
+    if ok and n_paced:
+        paced = make("p", n_paced)
+        r = max(1.0, load * rate)
+        sent = np.zeros(n_paced)
+        t0 = time.perf_counter()
+        for i, p in enumerate(paced):
+            target = t0 + i / r
+            while True:
+                now = time.perf_counter()
+                if now >= target:
+                    break
+                time.sleep(min(0.001, target - now))
+            sent[i] = time.perf_counter()
+            inject(p)
+        okp = watcher.wait(b"p", n_paced, timeout_s)
+        a = watcher.arr[b"p"]
+        sel = a > 0
+        out.update({"paced_rate_per_sec": round(r, 1), "paced_complete": okp,
+                    "latency_ingest_to_enriched": percentiles(1000 * (a[sel] - sent[sel]))})
+    return out
+
+
+# ---------------------------------------------------------------------------------- in-process
+def per_event_inproc(args) -> dict:
+    from sitewhere_amd.assembly import SiteWhereInstance
+    sw = SiteWhereInstance().start()
+    try:
+        sw.wait_for_tenant("default", 60)
+        es = sw.tenant_engine("event-sources")
+        topic = sw.instance.naming.inbound_enriched_events("default")
+        w = EnrichedWatcher(sw.instance.bus, topic, args.events, args.paced).start()
+        res = run_phases(lambda p: es.inject("default-protobuf", p), w, args.events, args.paced, args.load,
+                         args.timeout)
+        w.stop()
+        res.update({"replicas": 0, "deployment": "all 19 services in one process, in-process bus"})
+        return res
+    finally:
+        sw.stop()
+
+
+# ---------------------------------------------------------------------------------- multi-process
+def _spawn(argv, log):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.Popen([sys.executable, "-m", "sitewhere_amd.serve", "--log-level", "WARNING", "--heartbeat", "1",
+                             *argv], stdout=log, stderr=subprocess.STDOUT, env=env, cwd=ROOT)
+
+
+def per_event_replicas(args) -> dict:
+    """Reference deployment shape: infra (bus + coordination) and services in separate processes."""
+    import tempfile
+
+    from sitewhere_amd.core.lifecycle import LifecycleProgressMonitor
+    from sitewhere_amd.rpc.infra import InfraServer, RemoteCoordination, RemoteEventBus
+    from sitewhere_amd.bus.log import EventBus
+    from sitewhere_amd.coord.store import Coordination
+    from sitewhere_amd.runtime.config import InstanceSettings
+    from sitewhere_amd.runtime.microservice import Instance
+    from sitewhere_amd.runtime.topology import TopologyStateAggregator
+
+    logdir = tempfile.mkdtemp(prefix="swbench-")
+    infra = InfraServer(EventBus(None, default_partitions=8), Coordination(None), port=0).start()
+    groups = [["instance-management", "user-management", "tenant-management"],
+              ["device-management", "event-management"],
+              ["event-sources"], ["device-state"]] + [["inbound-processing"]] * args.replicas
+    logs = [open(os.path.join(logdir, f"p{i}.log"), "w") for i in range(len(groups))]
+    procs = [_spawn(["service", *g, "--infra", infra.address], logs[i]) for i, g in enumerate(groups)]
+    try:
+        inst = Instance(InstanceSettings(heartbeat_s=1.0), bus=RemoteEventBus(infra.address),
+                        coord=RemoteCoordination(infra.address), jwt_secret="sitewhere-instance-secret",
+                        network_rpc=True)
+        topo = TopologyStateAggregator(inst.bus, inst.naming.microservice_state_updates(), "bench", 30.0)
+        topo.lifecycle_start(LifecycleProgressMonitor())
+        inst.router.topology = topo
+        for ident in ("device-management", "event-management", "event-sources", "device-state", "inbound-processing"):
+            if not topo.wait_for(ident, 120, tenant="default"):
+                raise RuntimeError(f"{ident} never came up (logs in {logdir})")
+        # every inbound replica must be up before the burst (they share the consumer group)
+        end = time.time() + 120
+        while time.time() < end:
+            up = [s for s in topo.snapshot.hosts("inbound-processing")
+                  if "default" in s.tenant_engines and s.tenant_engines["default"].status == "Started"]
+            if len(up) >= args.replicas:
+                break
+            time.sleep(0.5)
+        else:
+            raise RuntimeError(f"only {len(up)} of {args.replicas} inbound replicas came up (logs in {logdir})")
+        time.sleep(3.0)   # consumer-group rebalance settles
+        topic = inst.naming.inbound_enriched_events("default")
+        w = EnrichedWatcher(inst.bus, topic, args.events, args.paced).start()
+        if args.ingress == "event-sources":
+            es = inst.router.proxy("EventSources", "default")
+            inject = lambda p: inst.system_user.run(lambda: es.inject("default-protobuf", p), "default")  # noqa: E731
+            res = run_phases(inject, w, args.events, args.paced, args.load, args.timeout)
+        else:
+            prod = inst.bus.producer()
+            t_dec = inst.naming.decoded_events("default")
+            res = run_phases(lambda r: prod.send(t_dec, r[0], r[1]), w, args.events, args.paced, args.load,
+                             args.timeout, make=decoded_records,
+                             inject_many=lambda rs: prod.send_batch(t_dec, rs))
+        res["ingress"] = args.ingress
+        w.stop()
+        topo.lifecycle_stop(LifecycleProgressMonitor())
+        res.update({"replicas": args.replicas,
+                    "deployment": f"{len(groups)} service processes + infra server; {args.replicas} inbound-processing "
+                                  "replica process(es) in one consumer group"})
+        return res
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for f in logs:
+            f.close()
+        infra.stop()
+
+
+# ---------------------------------------------------------------------------------- engine path
+def engine_path(args) -> dict:
+    from sitewhere_amd.assembly import SiteWhereInstance
+    from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
+    sw = SiteWhereInstance().start()
+    try:
+        sw.wait_for_tenant("default", 60)
+        tm = sw.api("TenantManagement")
+        sw.instance.system_user.run(lambda: tm.create_tenant({"token": "fast", "name": "fast",
+                                                              "configurationTemplateId": "gpu-columnar",
+                                                              "datasetTemplateId": "empty"}))
+        sw.wait_for_tenant("fast", 120)
+        run = lambda f: sw.instance.system_user.run(f, "fast")  # noqa: E731
+        dm = sw.api("DeviceManagement", "fast")
+        run(lambda: dm.create_device_type({"token": "sensor", "name": "Sensor"}))
+        for i in range(args.devices):
+            tok = f"dev-{i:010d}"
+            run(lambda tok=tok: dm.create_device({"token": tok, "deviceTypeToken": "sensor"}))
+            run(lambda tok=tok: dm.create_device_assignment({"deviceToken": tok}))
+        ib = sw.tenant_engine("inbound-processing", "fast")
+        while ib.engine.n_assignments < args.devices:
+            time.sleep(0.05)
+        spec = FleetSpec(prefix="dev-", n_devices=args.devices, p_location=0.25, p_alert=0.05, mx_per_msg=1)
+        now0 = int(time.time() * 1000)
+        nb = max(1, args.events // args.batch)
+        batches = []
+        for b in range(min(nb, 4)):
+            raw, offs = gen_payloads(spec, args.batch, now0 - 1000, seed=11 + b)
+            batches.append((np.concatenate([raw, np.zeros(64, np.uint8)]), offs))
+        ib.process_batch(*batches[0])                    # warm-up (first-touch, name dictionary)
+        lat = []
+        t0 = time.perf_counter()
+        ev = 0
+        for k in range(nb):
+            s = time.perf_counter()
+            r = ib.process_batch(*batches[k % len(batches)])
+            lat.append(1000 * (time.perf_counter() - s))
+            ev += r.n_events
+        dt = time.perf_counter() - t0
+        return {"path": "engine", "engine": ib.engine_kind, "events": ev, "events_per_sec": round(ev / dt, 1),
+                "batch_payloads": args.batch,
+                "batch_latency_ingest_to_enriched": percentiles(np.asarray(lat)),
+                "note": "latency of a batch from engine entry to columnar store + enriched-batch publish; "
+                        "add the source's flush interval for end-to-end"}
+    finally:
+        sw.stop()
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--path", choices=["per-event", "engine"], default="per-event")
+    ap.add_argument("--replicas", type=int, default=0, help="inbound-processing processes (0 = all in-process)")
+    ap.add_argument("--events", type=int, default=1000, help="burst size (config #1: 1k)")
+    ap.add_argument("--paced", type=int, default=1000, help="events in the paced latency phase")
+    ap.add_argument("--load", type=float, default=0.5, help="paced rate as a fraction of the burst throughput")
+    ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--ingress", choices=["decoded-topic", "event-sources"], default="decoded-topic",
+                    help="replicas mode: produce decoded events onto the bus (Kafka ingress of inbound "
+                         "processing) or call the event-sources API once per payload")
+    ap.add_argument("--devices", type=int, default=20000, help="engine path: registered devices")
+    ap.add_argument("--batch", type=int, default=65536, help="engine path: payloads per raw batch")
+    args = ap.parse_args()
+    import logging
+    logging.basicConfig(level=logging.ERROR)
+    if args.path == "engine":
+        res = engine_path(args)
+    elif args.replicas > 0:
+        res = per_event_replicas(args)
+        res["path"] = "per-event"
+    else:
+        res = per_event_inproc(args)
+        res["path"] = "per-event"
+    res["metric"] = "config1_reference_architecture"
+    res["cpus"] = len(os.sched_getaffinity(0))
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -70,6 +70,19 @@ def kafka_partition(key: bytes, n: int) -> int:
     return p
 
 
+def parse_frames(name: str, partition: int, n: int, raw: bytes) -> list:
+    """Framed records (``EventBus.read_framed``) -> Record objects."""
+    out, pos = [], 0
+    for _ in range(n):
+        off, ts, kl, vl = _FRAME.unpack_from(raw, pos)
+        pos += _FRAME.size
+        key = raw[pos:pos + kl] if kl else None
+        pos += kl
+        out.append(Record(name, partition, off, key, raw[pos:pos + vl], ts))
+        pos += vl
+    return out
+
+
 @dataclass
 class Record:
     topic: str
@@ -229,7 +242,67 @@ class EventBus:
         finally:
             self.unsubscribe_event(topics, ev)
 
+    def fetch_raw(self, reads, max_records: int, timeout_s: float, group: str | None = None,
+                  member: str | None = None):
+        """One consumer round trip (the Kafka Fetch request): group heartbeat, then up to
+        ``max_records`` framed records from ``reads`` = [(topic, partition, offset)], blocking up to
+        ``timeout_s`` until one of them has data.  The waiter is subscribed *before* the first read,
+        so an append landing between the read and the wait still wakes it.  Returns
+        (generation, [(topic, partition, n, framed bytes)]); an empty batch is also returned as soon
+        as the group generation changes (the member must refresh its assignment)."""
+        gen = self.heartbeat(group, member) if group else 0
+        deadline = time.time() + timeout_s
+        topics = {r[0] for r in reads}
+        ev = threading.Event()
+        self.subscribe_event(topics, ev)
+        try:
+            while True:
+                ev.clear()
+                out, budget = [], max_records
+                for name, p, off in reads:
+                    if budget <= 0:
+                        break
+                    n, raw = self.read_framed(name, p, off, budget)
+                    if n:
+                        out.append((name, p, n, raw))
+                        budget -= n
+                if out:
+                    return gen, out
+                left = deadline - time.time()
+                if left <= 0:
+                    return gen, out
+                ev.wait(min(left, 0.25))
+                if group and self.heartbeat(group, member) != gen:
+                    return -2, []
+        finally:
+            self.unsubscribe_event(topics, ev)
+
+    def read_framed(self, name: str, partition: int, offset: int, max_records: int = 500,
+                    max_bytes: int = 1 << 20) -> tuple[int, bytes]:
+        """(count, framed bytes) -- the wire form of :meth:`read` (``_FRAME`` header + key + value)."""
+        t = self.topic(name)
+        if offset >= self.fast.swlog_end_offset(self.h, t, partition):
+            return 0, b""
+        buf = getattr(self._tls, "buf", None)
+        if buf is None or len(buf) < max_bytes:
+            buf = self._tls.buf = np.empty(max_bytes, np.uint8)
+        n = ctypes.c_int64(0)
+        w = self.fast.swlog_read(self.h, t, partition, offset, max_records, buf.ctypes.data, max_bytes, ctypes.byref(n))
+        if w < 0:
+            return self.read_framed(name, partition, offset, max_records, -w + 64)
+        return n.value, buf[:w].tobytes()
+
+    def append_many(self, batches, ts: int | None = None):
+        """[(topic, partition, [(key, value)])] in one call (a producer's flushed batches)."""
+        for name, p, recs in batches:
+            self.append(name, p, recs, ts)
+
     # ------------------------------------------------------------------ offsets
+    def commit_many(self, group: str, offsets):
+        """[(topic, partition, offset)] in one call."""
+        for name, p, off in offsets:
+            self.commit(group, name, p, off)
+
     def commit(self, group: str, name: str, partition: int, offset: int):
         self.fast.swlog_commit(self.h, group.encode(), self.topic(name), partition, offset)
 
@@ -324,16 +397,36 @@ class EventBus:
 
 
 class Producer:
+    """Keyed producer.  Inside ``with producer.batching():`` sends made by the *calling thread* are
+    buffered and appended per (topic, partition) when the block exits -- one round trip for a whole
+    poll batch on a remote bus (Kafka's producer batching).  Per-partition order is preserved, and a
+    consumer that wraps its handler in the block commits only after the flush (at-least-once)."""
+
     def __init__(self, bus: EventBus):
         self.bus = bus
         self.sent = 0
+        self._tls = threading.local()
+
+    def batching(self):
+        return _ProducerBatch(self)
 
     def send(self, topic: str, key: str | bytes | None, value: bytes, partition: int | None = None) -> tuple[int, int]:
         kb = key.encode() if isinstance(key, str) else key
         p = self.bus.partition_for(topic, kb) if partition is None else partition
+        buf = getattr(self._tls, "buf", None)
+        if buf is not None:
+            buf.setdefault((topic, p), []).append((kb, value))
+            self.sent += 1
+            return p, -1
         off = self.bus.append(topic, p, [(kb, value)])
         self.sent += 1
         return p, off
+
+    def _flush_tls(self):
+        buf = getattr(self._tls, "buf", None)
+        if buf:
+            self._tls.buf = {}
+            self.bus.append_many([(t, p, recs) for (t, p), recs in buf.items()])
 
     def send_batch(self, topic: str, records: list[tuple[str | bytes | None, bytes]]):
         """Group by partition and append each group in one native call (batched produce)."""
@@ -341,9 +434,35 @@ class Producer:
         for k, v in records:
             kb = k.encode() if isinstance(k, str) else k
             groups.setdefault(self.bus.partition_for(topic, kb), []).append((kb, v))
-        for p, recs in groups.items():
-            self.bus.append(topic, p, recs)
+        buf = getattr(self._tls, "buf", None)
+        if buf is not None:
+            for p, recs in groups.items():
+                buf.setdefault((topic, p), []).extend(recs)
+        else:
+            self.bus.append_many([(topic, p, recs) for p, recs in groups.items()])
         self.sent += len(records)
+
+
+class _ProducerBatch:
+    def __init__(self, producer: Producer):
+        self.p = producer
+        self.outer = False
+
+    def __enter__(self):
+        tls = self.p._tls
+        self.outer = getattr(tls, "buf", None) is None
+        if self.outer:
+            tls.buf = {}
+        return self.p
+
+    def __exit__(self, et, ev, tb):
+        if self.outer:
+            try:
+                if et is None:
+                    self.p._flush_tls()
+            finally:
+                self.p._tls.buf = None
+        return False
 
 
 class Consumer:
@@ -385,7 +504,34 @@ class Consumer:
     def assignment(self) -> list:
         return list(self._assigned)
 
+    def _poll_fetch(self, timeout_ms: int, max_records: int) -> dict[tuple[str, int], list[Record]]:
+        """Remote bus: heartbeat + wait + read of every assigned partition in one round trip."""
+        deadline = time.time() + timeout_ms / 1000.0
+        while True:
+            reads = [(t, p, self.positions[(t, p)]) for t, p in self._assigned]
+            gen, got = self.bus.fetch_raw(reads, max_records, max(0.0, deadline - time.time()), self.group,
+                                          self.member_id)
+            if gen == -1:
+                self.generation = self.bus.join(self.group, self.member_id, self.topics)
+                self._refresh()
+            elif gen == -2 or gen != self.generation:
+                self._refresh()
+            out = {}
+            for name, p, n, raw in got:
+                tp = (name, p)
+                if tp not in self.positions:      # reassigned while the fetch was in flight
+                    continue
+                recs = parse_frames(name, p, n, raw)
+                recs = [r for r in recs if r.offset >= self.positions[tp]]
+                if recs:
+                    out[tp] = recs
+                    self.positions[tp] = recs[-1].offset + 1
+            if out or time.time() >= deadline:
+                return out
+
     def poll(self, timeout_ms: int = 1000, max_records: int = 500) -> dict[tuple[str, int], list[Record]]:
+        if not self._local and hasattr(self.bus, "fetch_raw"):
+            return self._poll_fetch(timeout_ms, max_records)
         deadline = time.time() + timeout_ms / 1000.0
         while True:
             self._ev.clear()
@@ -415,7 +561,11 @@ class Consumer:
 
     def commit(self, offsets: dict[tuple[str, int], int] | None = None):
         """Commit positions (next offset to read); default: current positions of all partitions."""
-        for tp, off in (offsets or self.positions).items():
+        items = (offsets or self.positions).items()
+        if hasattr(self.bus, "commit_many"):
+            self.bus.commit_many(self.group, [(tp[0], tp[1], off) for tp, off in items])
+            return
+        for tp, off in items:
             self.bus.commit(self.group, tp[0], tp[1], off)
 
     commit_async = commit

@@ -100,6 +100,17 @@ class _BusFacade:
     def wait_topics(self, topics, timeout_s):
         return self.b.wait_topics(topics, min(float(timeout_s), 1.0))
 
+    def fetch_raw(self, reads, max_records, timeout_s, group=None, member=None):
+        gen, got = self.b.fetch_raw([tuple(r) for r in reads], int(max_records), min(float(timeout_s), 1.0),
+                                    group, member)
+        return [gen, [list(x) for x in got]]
+
+    def append_many(self, batches, ts=None):
+        self.b.append_many([(t, p, [tuple(r) for r in recs]) for t, p, recs in batches], ts)
+
+    def commit_many(self, group, offsets):
+        self.b.commit_many(group, [tuple(o) for o in offsets])
+
     def commit(self, group, name, p, offset):
         self.b.commit(group, name, p, offset)
 
@@ -359,6 +370,17 @@ class RemoteEventBus:
             out.append(Record(name, p, off, key, raw[pos:pos + vl], ts))
             pos += vl
         return out
+
+    def fetch_raw(self, reads, max_records, timeout_s, group=None, member=None):
+        gen, got = self.r.call("fetch_raw", [list(r) for r in reads], max_records, min(float(timeout_s), 1.0),
+                               group, member)
+        return gen, [tuple(x) for x in got]
+
+    def append_many(self, batches, ts=None):
+        self.r.call("append_many", [[t, p, [[k, v] for k, v in recs]] for t, p, recs in batches], ts)
+
+    def commit_many(self, group, offsets):
+        self.r.call("commit_many", group, [list(o) for o in offsets])
 
     def wait(self, timeout_s):
         self.r.call("wait", timeout_s)

@@ -51,7 +51,9 @@ class BusConsumer(TenantEngineLifecycleComponent):
 
     def _call(self, recs):
         try:
-            self.handler(recs)
+            # sends made while handling this batch go out in one produce round trip, before the commit
+            with self.engine.ms.producer.batching():
+                self.handler(recs)
             self.processed += len(recs)
         except Exception:
             self.failures += len(recs)
