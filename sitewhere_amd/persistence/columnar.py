@@ -9,12 +9,16 @@ the page a query returns.  It implements :class:`~sitewhere_amd.persistence.even
 (object events -- e.g. command invocations added over REST -- go to an embedded memory store and
 are merged into query results), so event management serves GPU tenants through the same 16 RPCs.
 
-Batch wire format (:func:`encode_batch` / :func:`decode_batch`, msgpack): ``{"boot", "first_seq",
-"world", "rank", "now", "rows": OUT_REC bytes, "asg": {idx: [assignment, device, customer, area,
-asset]}, "names": {name_id: name}, "rules": {alert_type: message}}``.
+Batch wire format (:func:`encode_batch` / :func:`decode_batch`): ``b"SWC1"``, a u32 header length,
+a msgpack header ``{"boot", "first_seq", "world", "rank", "now", "asg": {idx: [assignment, device,
+customer, area, asset]}, "names": {name_id: name}, "rules": {alert_type: message}}``, then the
+OUT_REC rows as raw bytes.  The rows are copied once when the batch is built and viewed in place
+(``np.frombuffer``) when it is read -- a 64K-row batch is 2 MB, and packing it inside msgpack cost
+two more copies (0.45 ms per batch on the MI355X tenant path).
 """
 from __future__ import annotations
 
+import struct
 import threading
 
 import msgpack
@@ -32,17 +36,26 @@ _CTX = {DeviceEventIndex.Assignment: 0, DeviceEventIndex.Customer: 2, DeviceEven
         DeviceEventIndex.Asset: 4}
 
 
+_MAGIC = b"SWC1"
+
+
 def encode_batch(boot: str, first_seq: int, world: int, rank: int, now: int, rows: np.ndarray, asg: dict,
                  names: dict, rules: dict | None = None) -> bytes:
-    return msgpack.packb({"boot": boot, "first_seq": int(first_seq), "world": int(world), "rank": int(rank),
-                          "now": int(now), "rows": np.ascontiguousarray(rows).tobytes(),
-                          "asg": {int(k): list(v) for k, v in asg.items()},
-                          "names": {int(k): v for k, v in names.items()}, "rules": rules or {}}, use_bin_type=True)
+    hdr = msgpack.packb({"boot": boot, "first_seq": int(first_seq), "world": int(world), "rank": int(rank),
+                         "now": int(now), "asg": {int(k): list(v) for k, v in asg.items()},
+                         "names": {int(k): v for k, v in names.items()}, "rules": rules or {}}, use_bin_type=True)
+    rows = np.ascontiguousarray(rows, OUT_REC)
+    return b"".join((_MAGIC, struct.pack("<I", len(hdr)), hdr, memoryview(rows).cast("B")))
 
 
 def decode_batch(payload: bytes) -> dict:
-    d = msgpack.unpackb(payload, raw=False, strict_map_key=False)
-    d["rows"] = np.frombuffer(d["rows"], OUT_REC)
+    if payload[:4] != _MAGIC:                 # batches written before the framed format
+        d = msgpack.unpackb(payload, raw=False, strict_map_key=False)
+        d["rows"] = np.frombuffer(d["rows"], OUT_REC)
+        return d
+    (n,) = struct.unpack_from("<I", payload, 4)
+    d = msgpack.unpackb(payload[8:8 + n], raw=False, strict_map_key=False)
+    d["rows"] = np.frombuffer(payload, OUT_REC, offset=8 + n)
     return d
 
 

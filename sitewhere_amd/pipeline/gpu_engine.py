@@ -457,16 +457,36 @@ class GpuInboundEngine(EngineBase):
     def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
         """Synchronous convenience step (tests, control-plane use): H2D, run, D2H, learn names."""
         n_msgs = len(offs) - 1
-        raw_pad = np.zeros(len(raw) + _ALIGN, np.uint8)
-        raw_pad[:len(raw)] = raw
-        raw_dev = torch.from_numpy(raw_pad).to(self.device)
-        off_dev = torch.from_numpy(np.ascontiguousarray(offs, np.uint32).view(np.int32)).to(self.device)
+        raw_dev, off_dev = self._stage(raw, offs)
         do_presence = self.presence_due(now_ms) if presence is None else presence
-        sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence)
+        # rows land in HBM and come back in one DMA: reading them out of the mapped host buffer
+        # is CPU-uncached (~2.6 GB/s measured, 0.8 ms per 64K rows; profiles/r1_tenant_step)
+        sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence, out_to_device=True)
         torch.cuda.synchronize(self.device)
-        return self.collect(sel, raw)
+        return self.collect(sel, raw, from_device=True)
 
-    def collect(self, sel: int, raw_host: np.ndarray | None) -> StepResult:
+    def _stage(self, raw: np.ndarray, offs: np.ndarray):
+        """H2D of a host batch through persistent pinned staging (a pageable ``.to(device)`` ran at
+        ~6 GB/s plus a fresh padded copy per batch).  Only for the synchronous :meth:`step`: the
+        staging buffers are reused by the next call."""
+        nb, no = len(raw) + _ALIGN, len(offs)
+        st = getattr(self, "_stg", None)
+        if st is None or st[0].numel() < nb or st[1].numel() < no:
+            cap_b = max(nb, int(getattr(self, "_stg_hint", 0)))
+            pin_r = torch.empty(cap_b, dtype=torch.uint8).pin_memory()
+            pin_o = torch.empty(max(no, self.cfg.max_msgs + 1), dtype=torch.int32).pin_memory()
+            st = self._stg = (pin_r, pin_o, torch.empty(cap_b, dtype=torch.uint8, device=self.device),
+                              torch.empty(pin_o.numel(), dtype=torch.int32, device=self.device))
+        pin_r, pin_o, dev_r, dev_o = st
+        pr = pin_r.numpy()
+        pr[:len(raw)] = raw
+        pr[len(raw):nb] = 0
+        pin_o.numpy()[:no] = np.asarray(offs, np.uint32).view(np.int32)
+        dev_r[:nb].copy_(pin_r[:nb], non_blocking=True)
+        dev_o[:no].copy_(pin_o[:no], non_blocking=True)
+        return dev_r[:nb], dev_o[:no]
+
+    def collect(self, sel: int, raw_host: np.ndarray | None, from_device: bool = False) -> StepResult:
         sc = self.scalars()
         nn = min(sc["n_new_names"], self.cfg.names_cap)
         new = {}
@@ -474,13 +494,19 @@ class GpuInboundEngine(EngineBase):
             refs = self.t["new_names"][:nn * NAME_REF.itemsize].cpu().numpy().view(NAME_REF)
             new = self.learn_names(refs, raw_host)
         n_out = sc["n_out"]
-        out = self.out_host[sel].view(OUT_REC, n_out).copy()
+        if from_device:
+            out = self.out_dev[sel][:n_out * OUT_REC_SIZE].cpu().numpy().view(OUT_REC)
+        else:
+            out = self.out_host[sel].view(OUT_REC, n_out).copy()
         first_seq = int(self.t["cursor"][1].item())
         n_rej = sc["n_rej"]
-        work = self.t["work"] if self.world > 1 else self.t["recs"]
-        rej_idx = self.t["rej_idx"][:n_rej].long()
-        rows = work.view(-1, EVENT_REC.itemsize)[rej_idx].cpu().numpy().reshape(-1).view(EVENT_REC)
-        rst = self.t["status"][rej_idx].cpu().numpy()
+        if n_rej:
+            work = self.t["work"] if self.world > 1 else self.t["recs"]
+            rej_idx = self.t["rej_idx"][:n_rej].long()
+            rows = work.view(-1, EVENT_REC.itemsize)[rej_idx].cpu().numpy().reshape(-1).view(EVENT_REC)
+            rst = self.t["status"][rej_idx].cpu().numpy()
+        else:
+            rows, rst = np.zeros(0, EVENT_REC), np.zeros(0, np.uint8)
         return StepResult(n_msgs=int(self.args.n_msgs), n_events=sc["n_work"], n_persisted=n_out, out=out,
                           rejects=rows, reject_status=rst, new_names=new, first_seq=first_seq,
                           world=self.world, rank=self.rank)

@@ -83,7 +83,7 @@ TENANT_TEMPLATES["gpu-columnar"] = copy.deepcopy(TENANT_TEMPLATES["gpu"])
 TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event store"
 TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
     storage="columnar", publishEnriched="batches",
-    capacity={"max_msgs": 65536, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
+    capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
               "dedup_slots": 1 << 18, "gen_cap": 32768})
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {"datastore": {"type": "columnar"}}
 
