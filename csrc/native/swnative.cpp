@@ -523,6 +523,9 @@ using namespace swlog;
 
 extern "C" {
 
+// CRC-32C (Castagnoli) of a buffer: Kafka RecordBatch v2 checksums (bus/kafka_wire.py).
+uint32_t sw_crc32c(const uint8_t* p, int64_t n) { return swlog::crc32c(p, (size_t)n); }
+
 void* swlog_open(const char* dir, int32_t fsync_each) {
   Log* L = new Log();
   if (dir && dir[0]) {

@@ -115,6 +115,7 @@ def native():
         _proto(lib, "sw_fingerprint_batch", None, P, P, c_int64, P, P)
         _proto(lib, "sw_hash64_batch", None, P, P, c_int64, P)
         _proto(lib, "sw_murmur2", c_int32, P, c_int32)
+        _proto(lib, "sw_crc32c", ctypes.c_uint32, ctypes.c_char_p, c_int64)
         _proto(lib, "sw_partition_for_key", c_int32, P, c_int32, c_int32)
         _proto(lib, "sw_reg_upsert", c_int64, P, P, P, c_int64, c_uint64, c_uint64, c_int32)
         _proto(lib, "sw_reg_find", c_int64, P, P, P, c_int64, c_uint64, c_uint64)

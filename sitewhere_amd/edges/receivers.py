@@ -335,24 +335,62 @@ class PollingRestReceiver(Receiver):
         self._stop.set()
 
 
-class GatedReceiver(Receiver):
-    """Azure Event Hubs consumption needs AMQP 1.0 (not implemented here; Event Hubs' REST API is
-    send-only).  Fails loudly at initialize, naming the missing module."""
+class KafkaReceiver(Receiver):
+    """Consume payloads from a Kafka topic (one record value = one encoded device payload) in a
+    consumer group, committing after hand-off (at-least-once).  Also the Azure Event Hubs receiver
+    (reference ``sources/azure/EventHubInboundEventReceiver``): Event Hubs exposes the Kafka protocol
+    on ``<namespace>.servicebus.windows.net:9093`` with TLS and SASL/PLAIN (user ``$ConnectionString``,
+    password = the namespace connection string); the event hub is the topic."""
 
-    MODULES = {"eventhub": "azure.eventhub"}
+    def __init__(self, bootstrap: str, topic: str, group: str = "sitewhere", tls: bool = False,
+                 sasl_plain: tuple[str, str] | None = None, kind: str = "kafka"):
+        super().__init__(f"{kind}-receiver:{topic}")
+        self.bootstrap, self.topic, self.group = bootstrap, topic, group
+        self.tls, self.sasl_plain, self.kind = tls, sasl_plain, kind
+        self._stop = threading.Event()
+        self._t = None
+        self.bus = None
 
-    def __init__(self, kind: str, cfg: dict):
-        super().__init__(f"{kind}-receiver")
-        self.kind, self.cfg = kind, cfg
+    def start(self, monitor):
+        from ..bus.kafka_client import KafkaEventBus
+        self.bus = KafkaEventBus(self.bootstrap, client_id=f"sitewhere-{self.kind}", tls=self.tls,
+                                 sasl_plain=self.sasl_plain)
+        consumer = self.bus.consumer(self.group, [self.topic])
+        self._stop.clear()
 
-    def initialize(self, monitor):
-        import importlib
-        mod = self.MODULES[self.kind]
-        try:
-            importlib.import_module(mod)
-        except ImportError as e:
-            raise SiteWhereException(f"{self.kind} receiver needs python module {mod!r}") from e
-        raise SiteWhereException(f"{self.kind} receiver: client wiring not configured")
+        def run():
+            while not self._stop.is_set():
+                try:
+                    batch = consumer.poll(500)
+                except Exception as e:  # noqa: BLE001
+                    self.logger.warning("%s poll failed: %s", self.kind, e)
+                    time.sleep(1.0)
+                    continue
+                for recs in batch.values():
+                    for r in recs:
+                        self.deliver(r.value, {"topic": r.topic, "partition": r.partition, "offset": r.offset,
+                                               "key": r.key.decode(errors="replace") if r.key else None})
+                if batch:
+                    consumer.commit()
+            consumer.close()
+        self._t = threading.Thread(target=run, daemon=True, name=f"{self.kind}-receiver")
+        self._t.start()
+
+    def stop(self, monitor):
+        self._stop.set()
+        if self._t:
+            self._t.join(5)
+        if self.bus:
+            self.bus.client.close()
+
+
+def event_hub_receiver(rc: dict) -> KafkaReceiver:
+    """Event Hubs over its Kafka endpoint: ``namespace`` (or ``bootstrap``), ``eventHub``,
+    ``connectionString``, ``consumerGroup``."""
+    ns = rc.get("namespace")
+    bootstrap = rc.get("bootstrap") or f"{ns}.servicebus.windows.net:9093"
+    return KafkaReceiver(bootstrap, rc["eventHub"], rc.get("consumerGroup", "$Default"), bool(rc.get("tls", True)),
+                         ("$ConnectionString", rc["connectionString"]), kind="eventhub")
 
 
 def build_receiver(rc: dict) -> Receiver:
@@ -378,6 +416,10 @@ def build_receiver(rc: dict) -> Receiver:
         return RabbitMqReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 5672)), rc.get("queue", "sitewhere.input"),
                                 rc.get("username", "guest"), rc.get("password", "guest"), rc.get("vhost", "/"),
                                 bool(rc.get("durable", False)))
-    if t in GatedReceiver.MODULES:
-        return GatedReceiver(t, rc)
+    if t == "kafka":
+        sasl = (rc["username"], rc["password"]) if rc.get("username") else None
+        return KafkaReceiver(rc.get("bootstrap", "127.0.0.1:9092"), rc["topic"], rc.get("group", "sitewhere"),
+                             bool(rc.get("tls", False)), sasl)
+    if t in ("eventhub", "azure-eventhub"):
+        return event_hub_receiver(rc)
     raise ValueError(f"unknown receiver type {t!r}")

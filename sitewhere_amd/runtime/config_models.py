@@ -24,8 +24,8 @@ DECODER = E("Decoder", "event-source-decoder", "Payload decoder", [
       ["protobuf", "json", "json-batch", "script", "echo", "composite"]),
     A("script", "Script", "decoder script id (type=script)")])
 RECEIVER = E("Receiver", "event-source-receiver", "Protocol receiver", [
-    A("type", "String", "mqtt | socket | websocket | coap | rest-poll | activemq | rabbitmq", True,
-      choices=["mqtt", "socket", "websocket", "coap", "rest-poll", "activemq", "rabbitmq"]),
+    A("type", "String", "mqtt | socket | websocket | coap | rest-poll | activemq | rabbitmq | kafka | eventhub", True,
+      choices=["mqtt", "socket", "websocket", "coap", "rest-poll", "activemq", "rabbitmq", "kafka", "eventhub"]),
     A("host", "String", "broker / bind host", default="127.0.0.1"), A("port", "Integer", "port"),
     A("topic", "String", "MQTT topic"), A("queue", "String", "AMQP queue"), A("destination", "String", "STOMP destination"),
     A("qos", "Integer", "MQTT QoS", default=1), A("numThreads", "Integer", "processing threads", default=4)])
@@ -39,7 +39,7 @@ FILTER = E("Filter", "outbound-filter", "Event filter", [
     A("operation", "String", "include | exclude", default="include", choices=["include", "exclude"])])
 CONNECTOR = E("Connector", "outbound-connector", "Outbound connector", [
     A("id", "String", "connector id", True),
-    A("type", "String", "log | mqtt | http | solr | file | script | sqs | eventhub | dweet | initialstate | rabbitmq",
+    A("type", "String", "log | mqtt | http | solr | file | script | sqs | eventhub | dweet | initialstate | rabbitmq | kafka",
       True), A("numProcessingThreads", "Integer", "processing threads", default=0)], [FILTER])
 PROCESSOR = E("Rule Processor", "rule-processor", "Rule processor", [
     A("id", "String", "processor id", True), A("type", "String", "zone-test | threshold | script", True),

@@ -1,10 +1,12 @@
 """Process entry points (the reference's per-service Spring Boot ``*Application`` mains + docker-compose).
 
-  python -m sitewhere_amd.serve infra   --port 9092 [--data DIR]
-      bus (Kafka role, native commit log) + coordination (ZooKeeper role) server
-  python -m sitewhere_amd.serve service <identifier> [<identifier> ...] --infra HOST:PORT
+  python -m sitewhere_amd.serve infra   --port 9092 [--data DIR] [--kafka-port 9093]
+      bus (Kafka role, native commit log) + coordination (ZooKeeper role) server; --kafka-port also
+      serves the bus over the Kafka wire protocol (bus/kafka_broker.py) to any Kafka client
+  python -m sitewhere_amd.serve service <identifier> [<identifier> ...] --infra HOST:PORT [--kafka BOOTSTRAP]
       one or more microservices in this process, talking to the shared infra and to other
-      processes' services over gRPC (topology-discovered replicas)
+      processes' services over gRPC (topology-discovered replicas); with --kafka the data plane is
+      a Kafka cluster (bus/kafka_client.KafkaEventBus), as in the reference deployment
   python -m sitewhere_amd.serve all [--rest-port 8080] [--mqtt-port 1883] [--data DIR]
       a whole instance in one process (single-node deployment; GPU inbound engine per tenant)
 
@@ -38,11 +40,18 @@ def cmd_infra(args) -> int:
     snap = os.path.join(args.data, "coordination.json") if args.data else None
     if args.data:
         os.makedirs(bus_dir, exist_ok=True)
-    srv = InfraServer(EventBus(bus_dir, default_partitions=args.partitions), Coordination(snap), port=args.port,
-                      host=args.host).start()
+    bus = EventBus(bus_dir, default_partitions=args.partitions)
+    srv = InfraServer(bus, Coordination(snap), port=args.port, host=args.host).start()
     print(f"infra listening on {srv.address}", flush=True)
+    kafka = None
+    if args.kafka_port is not None:
+        from .bus.kafka_broker import KafkaBrokerServer
+        kafka = KafkaBrokerServer(bus, host=args.host, port=args.kafka_port).start()
+        print(f"kafka protocol listening on {kafka.address}", flush=True)
     stop = threading.Event()
     _wait_forever(stop)
+    if kafka:
+        kafka.stop()
     srv.stop()
     return 0
 
@@ -56,6 +65,10 @@ def build_instance(args, network: bool):
     if getattr(args, "infra", None):
         kw["bus"] = RemoteEventBus(args.infra)
         kw["coord"] = RemoteCoordination(args.infra)
+    kafka = getattr(args, "kafka", None) or os.environ.get("SITEWHERE_KAFKA_BOOTSTRAP")
+    if kafka:
+        from .bus.kafka_client import KafkaEventBus
+        kw["bus"] = KafkaEventBus(kafka)
     secret = os.environ.get("SITEWHERE_JWT_SECRET") or args.jwt_secret
     return Instance(settings, jwt_secret=secret, network_rpc=network, **kw)
 
@@ -117,9 +130,11 @@ def main(argv=None) -> int:
     p.add_argument("--host", default="127.0.0.1")
     p.add_argument("--data", default=None)
     p.add_argument("--partitions", type=int, default=8)
+    p.add_argument("--kafka-port", type=int, default=None, help="also serve the bus over the Kafka protocol")
     p = sub.add_parser("service")
     p.add_argument("identifiers", nargs="+")
     p.add_argument("--infra", required=True)
+    p.add_argument("--kafka", default=None, help="Kafka bootstrap servers for the data plane")
     p.add_argument("--grpc-port", type=int, default=0)
     p.add_argument("--rest-port", type=int, default=0)
     p = sub.add_parser("all")

@@ -182,7 +182,38 @@ class RabbitMqConnector(OutboundConnector):
         self.client.publish(self.exchange, rk, json.dumps(event_json(ev, ctx)).encode(), "application/json")
 
 
+# ------------------------------------------------------------------------------------ Kafka
+class KafkaConnector(OutboundConnector):
+    """Publish enriched events as JSON to a Kafka topic keyed by device token (the reference's
+    downstream integrations read the enriched stream straight off Kafka); a batch per delivery."""
+
+    def __init__(self, cid, bootstrap="127.0.0.1:9092", topic="sitewhere.{tenant}.enriched", tls=False,
+                 sasl_plain=None, filters=None):
+        super().__init__(cid, filters)
+        self.bootstrap, self.topic, self.tls, self.sasl_plain = bootstrap, topic, tls, sasl_plain
+        self.bus = None
+
+    def start(self, monitor):
+        from ..bus.kafka_client import KafkaEventBus
+        self.bus = KafkaEventBus(self.bootstrap, client_id="sitewhere-connector", tls=self.tls,
+                                 sasl_plain=self.sasl_plain)
+        self.producer = self.bus.producer()
+
+    def stop(self, monitor):
+        if self.bus:
+            self.bus.client.close()
+
+    def deliver(self, items):
+        topic = self.topic.format(tenant=self.tenant_prefix.rstrip("."))
+        self.producer.send_batch(topic, [(ctx.get("deviceToken") or ev.device_id,
+                                          json.dumps(event_json(ev, ctx)).encode()) for ev, ctx in items])
+
+
 def build_cloud_connector(t: str, cid: str, cfg: dict, filters):
+    if t == "kafka":
+        sasl = (cfg["username"], cfg["password"]) if cfg.get("username") else None
+        return KafkaConnector(cid, cfg.get("bootstrap", "127.0.0.1:9092"), cfg.get("topic", "sitewhere.{tenant}.enriched"),
+                              bool(cfg.get("tls", False)), sasl, filters)
     if t == "sqs":
         return SqsConnector(cid, cfg["queueUrl"], cfg.get("region", "us-east-1"), cfg["accessKey"], cfg["secretKey"],
                             cfg.get("endpoint"), filters)
