@@ -7,6 +7,7 @@ Reference: ``service-event-management/.../persistence/**``:
     ``(entity, event_type, bucket)`` clustered by ``event_date DESC`` (``:374-398, 419-495``)
   * InfluxDB (``InfluxDbDeviceEventManagement.java``): batched points (``InfluxDbClient.java:77``)
 Here: :class:`MemoryEventStore` (indexed, bisect-sorted), :class:`SQLiteEventStore` (durable),
+:class:`MongoEventStore` (the reference's MongoDB layout over the native wire client),
 :class:`BucketedEventStore` (the Cassandra time-bucket layout, in memory), :class:`InfluxLineWriter`
 (line protocol over HTTP, batched) and :class:`BufferedEventWriter` (the bulk buffer).  The GPU
 engine's enriched rows are stored column-wise by :mod:`sitewhere_amd.persistence.columnar`.
@@ -188,6 +189,78 @@ class SQLiteEventStore(DeviceEventStore):
             return self._db.execute("SELECT COUNT(*) FROM events").fetchone()[0]
 
 
+class MongoEventStore(DeviceEventStore):
+    """The reference's MongoDB event layout (``MongoDeviceEventManagement.java``): one ``events``
+    collection, one document per event (``_id`` = event id) with the index fields at top level,
+    compound indexes (type, entity, date desc) per index, alternate-id and originating-event
+    indexes.  Writes are bulk inserts (wrap in :class:`BufferedEventWriter` for the reference's
+    200-document / 250 ms buffer).  Over the native wire client (``mongo_wire.py``)."""
+
+    _FIELD = {DeviceEventIndex.Assignment: "deviceAssignmentId", DeviceEventIndex.Customer: "customerId",
+              DeviceEventIndex.Area: "areaId", DeviceEventIndex.Asset: "assetId"}
+
+    def __init__(self, uri: str = "mongodb://localhost:27017", database: str = "sitewhere", collection: str = "events"):
+        from .mongo_wire import MongoClient
+        self._client = MongoClient(uri)
+        self._c = self._client[database][collection]
+        for f in self._FIELD.values():
+            self._c.create_index({"eventType": 1, f: 1, "eventDate": -1})
+        self._c.create_index({"alternateId": 1}, sparse=True)
+        self._c.create_index({"originatingEventId": 1}, sparse=True)
+
+    def add_events(self, events):
+        docs = []
+        for e in events:
+            d = e.to_dict()
+            d["_id"] = e.id
+            d["eventType"] = e.event_type.value
+            d["eventDate"] = e.event_date or 0
+            docs.append(d)
+        if docs:
+            self._c.bulk_replace(docs)
+        return events
+
+    @staticmethod
+    def _load(d):
+        if d is None:
+            return None
+        d = dict(d)
+        d.pop("_id", None)
+        return event_from_dict(d)
+
+    def get_event_by_id(self, id):
+        return self._load(self._c.find_one({"_id": id}))
+
+    def get_event_by_alternate_id(self, alt):
+        return self._load(self._c.find_one({"alternateId": alt}))
+
+    def _search(self, flt, criteria):
+        c = criteria or DateRangeSearchCriteria()
+        rng = {}
+        if c.start_date is not None:
+            rng["$gte"] = c.start_date
+        if c.end_date is not None:
+            rng["$lte"] = c.end_date
+        if rng:
+            flt["eventDate"] = rng
+        total = self._c.count_documents(flt)
+        skip = (max(1, c.page_number) - 1) * c.page_size if c.page_size > 0 else 0
+        docs = self._c.find(flt, sort={"eventDate": -1}, skip=skip, limit=c.page_size if c.page_size > 0 else 0)
+        return SearchResults(total, [self._load(d) for d in docs])
+
+    def list_events(self, event_type, index, entity_ids, criteria=None):
+        if not entity_ids:
+            return SearchResults(0, [])
+        return self._search({"eventType": event_type.value, self._FIELD[index]: {"$in": list(entity_ids)}}, criteria)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        return self._search({"eventType": DeviceEventType.CommandResponse.value,
+                             "originatingEventId": invocation_id}, criteria)
+
+    def count(self):
+        return self._c.count_documents({})
+
+
 class BucketedEventStore(DeviceEventStore):
     """Cassandra layout: partition = (entity, event type, time bucket); rows clustered by date DESC.
 
@@ -365,4 +438,6 @@ def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
     if kind == "columnar":
         from .columnar import ColumnarEventStore
         return ColumnarEventStore()
+    if kind in ("mongo", "mongodb"):
+        return MongoEventStore(kw.get("uri", "mongodb://localhost:27017"), kw.get("database", "sitewhere"))
     raise ValueError(f"unknown event store {kind!r}")

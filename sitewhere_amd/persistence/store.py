@@ -2,9 +2,9 @@
 
 Reference: the per-service ``persistence/mongodb/*`` implementations over ``sitewhere-mongodb``
 (``MongoDbClient``, ``MongoPersistence``) and the datastore selection of
-``DatastoreConfigurationType.java:18-33``.  MongoDB itself is optional here
-(:class:`MongoEntityStore`, used when ``pymongo`` can reach a server); the in-memory store backs
-tests and single-process deployments, SQLite gives a durable zero-dependency store.
+``DatastoreConfigurationType.java:18-33``.  :class:`MongoEntityStore` talks to MongoDB through the
+native wire-protocol client (``mongo_wire.py``, SCRAM auth, no driver dependency); the in-memory
+store backs tests and single-process deployments, SQLite gives a durable zero-dependency store.
 """
 from __future__ import annotations
 
@@ -260,25 +260,35 @@ class SQLiteEntityStore(EntityStore):
 
 
 class MongoEntityStore(EntityStore):
-    """MongoDB backend (reference default).  Requires ``pymongo`` and a reachable server."""
+    """MongoDB backend (the reference default) over the native wire-protocol client
+    (``persistence/mongo_wire.py``; no driver dependency).  One collection per entity type, ``_id`` =
+    entity id, unique sparse indexes on the unique fields (E11000 -> DuplicateToken)."""
 
     def __init__(self, uri: str = "mongodb://localhost:27017", database: str = "sitewhere", timeout_ms: int = 3000):
-        import pymongo  # noqa: F401 -- optional dependency
-
-        self._client = pymongo.MongoClient(uri, serverSelectionTimeoutMS=timeout_ms)
+        from .mongo_wire import MongoClient
+        self._client = MongoClient(uri, timeout_s=timeout_ms / 1000.0)
         self._db = self._client[database]
         self._cls: dict[str, type] = {}
+        self._unique: dict[str, tuple] = {}
 
     def register(self, collection, cls, unique_fields=("token",)):
-        import pymongo
+        from ..models.domain import camel
         self._cls[collection] = cls
+        self._unique[collection] = tuple(unique_fields)
         for f in unique_fields:
-            self._db[collection].create_index([(f, pymongo.ASCENDING)], unique=True, sparse=True)
+            self._db[collection].create_index({camel(f): 1}, unique=True, sparse=True)
 
     def put(self, collection, entity):
+        from .mongo_wire import DUPLICATE_KEY, MongoError
         d = entity.to_dict()
         d["_id"] = entity.id
-        self._db[collection].replace_one({"_id": entity.id}, d, upsert=True)
+        try:
+            self._db[collection].replace_one({"_id": entity.id}, d, upsert=True)
+        except MongoError as e:
+            if e.code == DUPLICATE_KEY:
+                from ..core.errors import ErrorCode, SiteWhereSystemException
+                raise SiteWhereSystemException(ErrorCode.DuplicateToken, detail=str(e)) from e
+            raise
         return entity
 
     def _load(self, collection, d):
@@ -307,6 +317,9 @@ class MongoEntityStore(EntityStore):
         if sort_key is not None:
             items.sort(key=sort_key, reverse=reverse)
         return items
+
+    def count(self, collection):
+        return self._db[collection].count_documents({})
 
     def clear(self):
         for c in self._cls:

@@ -71,6 +71,10 @@ for _svc in ("device-management", "asset-management", "batch-operations", "sched
     TENANT_TEMPLATES["mongodb"]["services"][_svc] = {"datastore": {"type": "mongodb",
                                                                    "uri": "${mongodb.uri:mongodb://localhost:27017}",
                                                                    "database": "tenant-[[tenant.token]]"}}
+# events: the reference's MongoDeviceEventManagement layout with its bulk buffer (200 docs / 250 ms)
+TENANT_TEMPLATES["mongodb"]["services"]["event-management"] = {
+    "datastore": {"type": "mongodb", "uri": "${mongodb.uri:mongodb://localhost:27017}",
+                  "database": "tenant-[[tenant.token]]"}, "buffered": True}
 TENANT_TEMPLATES["gpu"] = copy.deepcopy(TENANT_TEMPLATES["default"])
 TENANT_TEMPLATES["gpu"]["name"] = "MI355X-accelerated inbound pipeline"
 TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5,
