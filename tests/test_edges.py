@@ -168,3 +168,55 @@ def test_build_receiver_and_connector_types():
     assert type(build_receiver({"type": "rabbitmq", "port": 1})).__name__ == "RabbitMqReceiver"
     with pytest.raises(ValueError):
         build_receiver({"type": "nope"})
+
+
+def test_solr_connector_indexes_and_search_provider_queries():
+    """SolrOutboundConnector -> Solr JSON update handler; SolrSearchProvider -> /select (SURVEY §2.1
+    sitewhere-solr, service-event-search).  Against a local HTTP stand-in for a Solr core."""
+    import http.server
+    import json as _json
+    import threading as _th
+    import urllib.parse as up
+
+    from sitewhere_amd.models.domain import DeviceMeasurement
+    from sitewhere_amd.services.labels_media_search import SolrSearchProvider
+    from sitewhere_amd.services.outbound_connectors import SolrConnector
+
+    docs = []
+
+    class Solr(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_POST(self):
+            assert self.path.startswith("/SiteWhere/update")
+            docs.extend(_json.loads(self.rfile.read(int(self.headers["Content-Length"]))))
+            self.send_response(200)
+            self.end_headers()
+            self.wfile.write(b'{"responseHeader":{"status":0}}')
+
+        def do_GET(self):
+            u = up.urlparse(self.path)
+            q = dict(up.parse_qsl(u.query))
+            assert u.path == "/SiteWhere/select" and q["wt"] == "json"
+            f, v = q["q"].split(":", 1)
+            hits = [d for d in docs if str(d.get(f)) == v][:int(q["rows"])]
+            body = _json.dumps({"response": {"numFound": len(hits), "docs": hits}}).encode()
+            self.send_response(200)
+            self.end_headers()
+            self.wfile.write(body)
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), Solr)
+    _th.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}"
+        con = SolrConnector("solr", url)
+        evs = [DeviceMeasurement(device_assignment_id="a1", device_id="d1", name="temp", value=float(i),
+                                 event_date=1000 + i) for i in range(3)]
+        con.deliver([(e, {}) for e in evs])
+        assert {d["id"] for d in docs} == {e.id for e in evs}
+        assert docs[0]["eventType"] == "Measurement" and docs[0]["name_s"] == "temp" and "value_d" in docs[0]
+        hits = SolrSearchProvider("solr", url).search("assignmentId:a1", rows=2)
+        assert len(hits) == 2 and all(h["assignmentId"] == "a1" for h in hits)
+    finally:
+        srv.shutdown()
