@@ -393,10 +393,20 @@ class InfluxLineWriter:
     def _esc(s: str) -> str:
         return str(s).replace(" ", r"\ ").replace(",", r"\,").replace("=", r"\=")
 
+    @staticmethod
+    def _str_field(v: str) -> str:
+        return '"' + str(v).replace("\\", "\\\\").replace('"', '\\"') + '"'
+
     def line(self, e: DeviceEvent) -> str:
         tags = {"type": e.event_type.value, "assignment": e.device_assignment_id or "", "device": e.device_id or "",
                 "customer": e.customer_id or "", "area": e.area_id or "", "asset": e.asset_id or ""}
         fields = {"eid": f'"{e.id}"'}
+        if e.alternate_id:
+            fields["alt"] = self._str_field(e.alternate_id)
+        orig = getattr(e, "originating_event_id", None)
+        if orig:
+            fields["orig"] = self._str_field(orig)
+        fields["doc"] = self._str_field(json.dumps(e.to_dict(), separators=(",", ":")))
         if e.event_type == DeviceEventType.Measurement:
             fields[f"mx_{self._esc(e.name)}"] = repr(float(e.value))
         elif e.event_type == DeviceEventType.Location:
@@ -427,6 +437,103 @@ class InfluxLineWriter:
         self.buf = []
 
 
+class InfluxEventStore(DeviceEventStore):
+    """Events in InfluxDB, the reference's layout (``InfluxDbDeviceEvent.java``): measurement
+    ``events``, tags type/assignment/device/customer/area/asset, field ``eid``; written in batched
+    line protocol (:class:`InfluxLineWriter`) and read back with the reference's InfluxQL queries
+    (``SELECT * FROM events WHERE type='..' AND (assignment='..' OR ..) AND time >= .. ORDER BY time
+    DESC LIMIT .. OFFSET ..`` and ``SELECT count(eid) ...``) over the HTTP ``/query`` API.  Each point
+    also carries the full event document (``doc``) so reads are lossless."""
+
+    _TAG = {DeviceEventIndex.Assignment: "assignment", DeviceEventIndex.Customer: "customer",
+            DeviceEventIndex.Area: "area", DeviceEventIndex.Asset: "asset"}
+
+    def __init__(self, url: str = "http://localhost:8086", database: str = "sitewhere", batch: int = 1000, http=None):
+        self.base, self.database = url.rstrip("/"), database
+        self._http = http
+        self.writer = InfluxLineWriter(self.base, database, batch, post=self._post if http else None)
+        self._lock = threading.RLock()
+        self.query_raw(f"CREATE DATABASE {database}", db=None)
+
+    def _post(self, url, body):
+        return self._http("POST", url, body)
+
+    def query_raw(self, q: str, db: str | None = "") -> list:
+        import urllib.parse
+        import urllib.request
+        params = {"q": q, "epoch": "ms"}
+        if db is not None:
+            params["db"] = db or self.database
+        url = f"{self.base}/query?{urllib.parse.urlencode(params)}"
+        if self._http:
+            body = self._http("POST" if q.upper().startswith("CREATE") else "GET", url, None)
+        else:
+            req = urllib.request.Request(url, method="POST" if q.upper().startswith("CREATE") else "GET")
+            body = urllib.request.urlopen(req, timeout=10).read()
+        res = json.loads(body)["results"][0]
+        if "error" in res:
+            raise RuntimeError(f"influxdb: {res['error']}")
+        return res.get("series", [])
+
+    @staticmethod
+    def _q(v) -> str:
+        return "'" + str(v).replace("\\", "\\\\").replace("'", "\\'") + "'"
+
+    def add_events(self, events):
+        with self._lock:
+            self.writer.add_events(events)
+            self.writer.flush()                  # the buffered writer batches upstream
+        return events
+
+    def _rows(self, series) -> list:
+        out = []
+        for s in series:
+            cols = s["columns"]
+            for v in s.get("values", []):
+                d = dict(zip(cols, v))
+                if d.get("doc"):
+                    out.append(event_from_dict(json.loads(d["doc"])))
+        return out
+
+    def _one(self, where: str):
+        r = self._rows(self.query_raw(f"SELECT * FROM events WHERE {where} LIMIT 1"))
+        return r[0] if r else None
+
+    def get_event_by_id(self, id):
+        return self._one(f"eid={self._q(id)}")
+
+    def get_event_by_alternate_id(self, alt):
+        return self._one(f"alt={self._q(alt)}")
+
+    def _search(self, where: str, criteria):
+        c = criteria or DateRangeSearchCriteria()
+        if c.start_date is not None:
+            where += f" AND time >= {int(c.start_date)}ms"
+        if c.end_date is not None:
+            where += f" AND time <= {int(c.end_date)}ms"
+        cnt = self.query_raw(f"SELECT count(eid) FROM events WHERE {where}")
+        total = int(cnt[0]["values"][0][1]) if cnt and cnt[0].get("values") else 0
+        q = f"SELECT * FROM events WHERE {where} ORDER BY time DESC"
+        if c.page_size > 0:
+            q += f" LIMIT {int(c.page_size)} OFFSET {int((max(1, c.page_number) - 1) * c.page_size)}"
+        return SearchResults(total, self._rows(self.query_raw(q)))
+
+    def list_events(self, event_type, index, entity_ids, criteria=None):
+        if not entity_ids:
+            return SearchResults(0, [])
+        tag = self._TAG[index]
+        ors = " OR ".join(f"{tag}={self._q(i)}" for i in entity_ids)
+        return self._search(f"type={self._q(event_type.value)} AND ({ors})", criteria)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        return self._search(f"type={self._q(DeviceEventType.CommandResponse.value)} AND orig={self._q(invocation_id)}",
+                            criteria)
+
+    def count(self):
+        cnt = self.query_raw("SELECT count(eid) FROM events")
+        return int(cnt[0]["values"][0][1]) if cnt and cnt[0].get("values") else 0
+
+
 def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
     kind = (kind or "memory").lower()
     if kind == "memory":
@@ -440,4 +547,6 @@ def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
         return ColumnarEventStore()
     if kind in ("mongo", "mongodb"):
         return MongoEventStore(kw.get("uri", "mongodb://localhost:27017"), kw.get("database", "sitewhere"))
+    if kind == "influxdb":
+        return InfluxEventStore(kw.get("url", "http://localhost:8086"), kw.get("database", "sitewhere"))
     raise ValueError(f"unknown event store {kind!r}")

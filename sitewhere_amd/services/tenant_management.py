@@ -75,6 +75,11 @@ for _svc in ("device-management", "asset-management", "batch-operations", "sched
 TENANT_TEMPLATES["mongodb"]["services"]["event-management"] = {
     "datastore": {"type": "mongodb", "uri": "${mongodb.uri:mongodb://localhost:27017}",
                   "database": "tenant-[[tenant.token]]"}, "buffered": True}
+TENANT_TEMPLATES["influxdb"] = copy.deepcopy(TENANT_TEMPLATES["default"])
+TENANT_TEMPLATES["influxdb"]["name"] = "InfluxDB event store"
+TENANT_TEMPLATES["influxdb"]["services"]["event-management"] = {
+    "datastore": {"type": "influxdb", "url": "${influxdb.url:http://localhost:8086}",
+                  "database": "tenant-[[tenant.token]]"}, "buffered": True}
 TENANT_TEMPLATES["gpu"] = copy.deepcopy(TENANT_TEMPLATES["default"])
 TENANT_TEMPLATES["gpu"]["name"] = "MI355X-accelerated inbound pipeline"
 TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5,
