@@ -982,6 +982,43 @@ __global__ void k_reject_stats(SwEngineArgs a) {
 }
 
 // ============================================================================ C ABI
+// ============================================================================ hot-store query
+// Event-management reads over the HBM event ring (DeviceEventManagement.list*ForIndex,
+// EventManagementImpl.java): rows of one event type whose assignment is in a bitmap and whose
+// event date lies in [lo, hi].  One pass over the ring: the 1-byte type column is read for every
+// row, assignment and date only where the type matches.  Matches are compacted per wave (ballot +
+// one atomic per wave that has any) into out_rows -- unordered; the host orders the (usually small)
+// match set by (date desc, event id desc).  *n_match receives the total even past cap.
+__global__ __launch_bounds__(BLK) void k_store_filter(const uint8_t* __restrict__ etype, const int32_t* __restrict__ asg,
+                                                      const int64_t* __restrict__ date, int64_t n_rows, int32_t et,
+                                                      const uint32_t* __restrict__ bits, int64_t n_asg, int64_t lo,
+                                                      int64_t hi, uint32_t* __restrict__ out_rows, int64_t cap,
+                                                      uint32_t* __restrict__ n_match) {
+  const int64_t stride = (int64_t)gridDim.x * BLK;
+  // every lane of a wave iterates the same number of times (ballot needs the whole wave)
+  const int64_t iters = (n_rows + stride - 1) / stride;
+  int64_t r = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  for (int64_t it = 0; it < iters; ++it, r += stride) {
+    bool hit = false;
+    if (r < n_rows && etype[r] == (uint8_t)et) {
+      const int32_t a = asg[r];
+      if (a >= 0 && a < n_asg && ((bits[a >> 5] >> (a & 31)) & 1u)) {
+        const int64_t d = date[r];
+        hit = d >= lo && d <= hi;
+      }
+    }
+    const ull mask = __ballot(hit);
+    if (!mask) continue;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(n_match, (uint32_t)__popcll(mask));
+    base = __shfl(base, 0, 64);
+    if (hit) {
+      const uint64_t pos = (uint64_t)base + (uint64_t)__popcll(mask & lanemask_lt());
+      if ((int64_t)pos < cap) out_rows[pos] = (uint32_t)r;
+    }
+  }
+}
+
 extern "C" {
 
 // Framing: varint length stream -> msg_off[n_msgs + 1].  tmp needs 2 * ceil(nbytes / 1024) u32.
@@ -1156,6 +1193,17 @@ __global__ void k_pip_batch(const double* pts, int64_t n_pts, const double* vtx,
     const int64_t p = i / n_zones, z = i % n_zones;
     out[i] = pip(vtx + 2 * off[z], off[z + 1] - off[z], pts[2 * p], pts[2 * p + 1]) ? 1 : 0;
   }
+}
+
+int sw_store_filter(const uint8_t* etype, const int32_t* asg, const int64_t* date, int64_t n_rows, int32_t et,
+                    const uint32_t* bits, int64_t n_asg, int64_t lo, int64_t hi, uint32_t* out_rows, int64_t cap,
+                    uint32_t* n_match, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(n_match, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return (int)e;
+  if (n_rows > 0)
+    k_store_filter<<<grid_for(n_rows), BLK, 0, s>>>(etype, asg, date, n_rows, et, bits, n_asg, lo, hi, out_rows, cap,
+                                                    n_match);
+  return (int)hipGetLastError();
 }
 
 int sw_pip_batch(const double* pts, int64_t n_pts, const double* vtx, const int32_t* off, int64_t n_zones,

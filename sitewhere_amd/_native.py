@@ -212,6 +212,8 @@ def gpu():
         _proto(lib, "sw_phase_process", c_int32, P, P, P)
         _proto(lib, "sw_registry_patch", c_int32, P, P, P, c_int64, P)
         _proto(lib, "sw_pip_batch", c_int32, P, c_int64, P, P, c_int64, P, P)
+        _proto(lib, "sw_store_filter", c_int32, P, P, P, c_int64, c_int32, P, c_int64, c_int64, c_int64, P, c_int64,
+               P, P)
         _proto(lib, "sw_scan_u32", c_int32, P, c_int64, P, P, P, c_int64, P)
         _proto(lib, "sw_abi_sizes", c_int32, P)
         _proto(lib, "sw_host_alloc", c_int32, c_int64, P, P)

@@ -352,6 +352,24 @@ class CpuInboundEngine(EngineBase):
             "alerts": al,
         }
 
+    def query_store(self, event_type, asg_idx, start=None, end=None, page_number=1, page_size=100):
+        n = min(self.cursor, self.cfg.store_cap)
+        s = self.store
+        m = s["etype"][:n] == event_type
+        m &= np.isin(s["asg"][:n], np.asarray(list(asg_idx), np.int32))
+        d = s["date"][:n]
+        if start is not None:
+            m &= d >= start
+        if end is not None:
+            m &= d <= end
+        rows = np.nonzero(m)[0]
+        seq = self._row_seq(rows.astype(np.int64), self.cursor)
+        order = np.lexsort((-seq, -d[rows]))
+        lo, hi = self._window(page_number, page_size, len(rows))
+        page = rows[order[lo:hi]]
+        cols = {k: v[page] for k, v in s.items()}
+        return len(rows), cols, seq[order[lo:hi]] * self.world + self.rank
+
     def store_rows(self):
         n = min(self.cursor, self.cfg.store_cap)
         if self.cursor <= self.cfg.store_cap:

@@ -234,6 +234,28 @@ class EngineBase:
             return True
         return False
 
+    # ------------------------------------------------------------------ hot-store queries
+    def query_store(self, event_type: int, asg_idx, start: int | None = None, end: int | None = None,
+                    page_number: int = 1, page_size: int = 100):
+        """Events of one type for a set of assignment indices in a date range, newest first (ties:
+        latest event id first), straight from this shard's event ring -- the hot half of
+        ``DeviceEventManagement.list*ForIndex``.  Returns (total, page columns dict, page event ids)."""
+        raise NotImplementedError
+
+    @staticmethod
+    def _window(page_number: int, page_size: int, total: int) -> tuple[int, int]:
+        if page_size <= 0:
+            return 0, total
+        lo = (max(1, page_number) - 1) * page_size
+        return min(lo, total), min(lo + page_size, total)
+
+    def _row_seq(self, rows, cursor: int):
+        """Store sequence of ring rows (works on numpy and torch integer arrays)."""
+        cap = self.cfg.store_cap
+        if cursor <= cap:
+            return rows
+        return (cursor - cap) + (rows - (cursor % cap)) % cap
+
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "base"
 

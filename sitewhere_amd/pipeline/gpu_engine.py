@@ -550,6 +550,45 @@ class GpuInboundEngine(EngineBase):
             "alerts": al,
         }
 
+    def query_store(self, event_type, asg_idx, start=None, end=None, page_number=1, page_size=100):
+        """Hot-store query on the MI355X: one k_store_filter pass over the HBM ring (assignment set
+        as a bitmap), then the match set is ordered on the device and only the page comes back."""
+        cur = self.cursor
+        n = min(cur, self.cfg.store_cap)
+        nbits = self.cfg.max_assignments
+        words = np.zeros((nbits + 31) // 32, np.uint32)
+        a = np.asarray(list(asg_idx), np.int64)
+        a = a[(a >= 0) & (a < nbits)]
+        np.bitwise_or.at(words, a >> 5, (np.uint32(1) << (a & 31).astype(np.uint32)))
+        bits = torch.from_numpy(words.view(np.int32)).to(self.device)
+        if getattr(self, "_q_rows", None) is None or self._q_rows.numel() < max(n, 1):
+            self._q_rows = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+            self._q_n = torch.zeros(1, dtype=torch.int32, device=self.device)
+        i64 = np.iinfo(np.int64)
+        st = self.store
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        rc = self.lib.sw_store_filter(ctypes.c_void_p(_ptr(st["etype"])), ctypes.c_void_p(_ptr(st["asg"])),
+                                      ctypes.c_void_p(_ptr(st["date"])), n, int(event_type),
+                                      ctypes.c_void_p(_ptr(bits)), nbits, i64.min if start is None else int(start),
+                                      i64.max if end is None else int(end), ctypes.c_void_p(_ptr(self._q_rows)),
+                                      self._q_rows.numel(), ctypes.c_void_p(_ptr(self._q_n)), stream)
+        if rc:
+            raise RuntimeError(f"sw_store_filter failed ({rc})")
+        total = int(self._q_n.item())
+        rows = self._q_rows[:total].long()
+        seq = self._row_seq(rows, cur)
+        # newest first, ties by latest id: stable sort by seq desc, then stable by date desc
+        o1 = torch.sort(seq, descending=True, stable=True).indices
+        dates = st["date"][rows[o1]]
+        o2 = torch.sort(dates, descending=True, stable=True).indices
+        lo, hi = self._window(page_number, page_size, total)
+        sel = o1[o2[lo:hi]]
+        page = rows[sel]
+        cols = {k: v[page].cpu().numpy() for k, v in st.items()}
+        for k in ("name", "alt", "aux"):
+            cols[k] = cols[k].view(np.uint64)
+        return total, cols, seq[sel].cpu().numpy() * self.world + self.rank
+
     def store_rows(self):
         cur = self.cursor
         cap = self.cfg.store_cap

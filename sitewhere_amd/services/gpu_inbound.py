@@ -409,6 +409,48 @@ class GpuInboundApi:
         ai = self._e.asg_index.idx.get(assignment_id)
         return None if ai is None else self._e.engine.device_state(ai)
 
+    _INDEX = {"Assignment": 0, "Customer": 2, "Area": 3, "Asset": 4}
+    _ETYPE = {"Measurement": EV_MEASUREMENT, "Location": EV_LOCATION, "Alert": EV_ALERT, "StateChange": EV_STATE_CHANGE}
+
+    def list_hot_events(self, event_type: str, index: str, entity_ids: list, start_date: int | None = None,
+                        end_date: int | None = None, page_number: int = 1, page_size: int = 100) -> dict:
+        """Hot-store read of ``DeviceEventManagement.list*ForIndex`` served from the engine's event ring
+        (HBM on the MI355X: one filter kernel over the ring, only the page crosses PCIe).  Events in
+        the ring's retention window; older ones live in event management's store."""
+        e = self._e
+        pos = self._INDEX[index]
+        want = set(entity_ids)
+        with e._lock:
+            asg = [ai for ai, a in e._asg_entities.items()
+                   if (a.id, a.device_id, a.customer_id, a.area_id, a.asset_id)[pos] in want]
+        total, cols, eids = e.engine.query_store(self._ETYPE[event_type], asg, start_date, end_date, page_number,
+                                                 page_size)
+        out = []
+        rules = {t.alert_type: t.alert_message for t in e.engine.tests}
+        for i in range(len(eids)):
+            a = e._asg_entities.get(int(cols["asg"][i]))
+            if a is None:
+                continue
+            base = dict(id=f"{e.boot}-{int(eids[i])}", device_id=a.device_id, device_assignment_id=a.id,
+                        customer_id=a.customer_id, area_id=a.area_id, asset_id=a.asset_id,
+                        event_date=int(cols["date"][i]), received_date=int(cols["recv"][i]))
+            et = int(cols["etype"][i])
+            name = e.engine.names.get(int(cols["name"][i]), "") if int(cols["name"][i]) else ""
+            if et == EV_MEASUREMENT:
+                ev = DeviceMeasurement(name=name, value=float(cols["v0"][i]), **base)
+            elif et == EV_LOCATION:
+                ev = DeviceLocation(latitude=float(cols["v0"][i]), longitude=float(cols["v1"][i]),
+                                    elevation=float(cols["v2"][i]), **base)
+            elif et == EV_ALERT:
+                ev = DeviceAlert(source=AlertSource.System if name in rules else AlertSource.Device,
+                                 level=_LEVELS[min(int(cols["level"][i]), 3)], type=name,
+                                 message=rules.get(name, ""), **base)
+            else:
+                ev = DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
+                                       new_state="NOT_PRESENT", **base)
+            out.append(ev)
+        return {"numResults": int(total), "results": out}
+
     def process_payloads(self, payloads: list) -> dict:
         """Synchronous injection (tests / REST): one engine step over the given wire payloads."""
         raw, offs = pack_messages([bytes(p) for p in payloads])

@@ -91,3 +91,25 @@ def test_event_ids_and_store():
     # enrichment: customer/area/asset are the assignment's
     asg = cols["asg"]
     assert (cols["cust"] == asg % 7).all() and (cols["area"] == asg % 5).all() and (cols["asset"] == asg % 3).all()
+
+
+def test_hot_store_query_matches_brute_force_with_wraparound():
+    """query_store (the hot half of list*ForIndex) vs a brute-force scan of store_rows, after the ring
+    wrapped: filter by type / assignment set / date range, newest first, ties by latest event id."""
+    from sitewhere_amd.pipeline.native_engine import NativeCpuEngine
+    for eng in (CpuInboundEngine(small_cfg(store_cap=1 << 12)), NativeCpuEngine(small_cfg(store_cap=1 << 12))):
+        setup_fleet(eng, n_dev=100)
+        for k in range(4):
+            raw, offs = fleet_batch(1500, seed=40 + k, n_dev=100)
+            eng.step(raw, offs, NOW + k, presence=False)
+        assert eng.cursor > eng.cfg.store_cap
+        cols, eids = eng.store_rows()
+        asg = [3, 7, 11, 50]
+        lo, hi = NOW - 50_000, NOW - 10_000
+        sel = np.nonzero((cols["etype"] == EV_MEASUREMENT) & np.isin(cols["asg"], asg) &
+                         (cols["date"] >= lo) & (cols["date"] <= hi))[0]
+        order = sel[np.lexsort((-eids[sel], -cols["date"][sel]))]
+        total, page, peids = eng.query_store(EV_MEASUREMENT, asg, lo, hi, page_number=2, page_size=7)
+        assert total == len(sel) and total > 14
+        assert np.array_equal(peids, eids[order[7:14]])
+        assert np.array_equal(page["v0"], cols["v0"][order[7:14]])

@@ -214,3 +214,26 @@ def test_store_ring_wraparound_parity():
     assert len(eg) == 4096 and np.array_equal(eg, ec)
     for k in ("etype", "asg", "date"):
         assert sorted(cg[k].tolist()) == sorted(cc[k].tolist()), k
+
+
+@pytest.mark.gpu
+def test_hot_store_query_kernel_matches_cpu_oracle():
+    """k_store_filter + device ordering vs the CPU oracle's query_store after the HBM ring wrapped."""
+    from sitewhere_amd.models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT
+    g = GpuInboundEngine(small_cfg(store_cap=1 << 12), device="cuda:0")
+    c = CpuInboundEngine(small_cfg(store_cap=1 << 12))
+    for e in (g, c):
+        setup_fleet(e, n_dev=200)
+    for k in range(5):
+        raw, offs = fleet_batch(1500, seed=70 + k, n_dev=200)
+        g.step(raw, offs, NOW + k, presence=False)
+        c.step(raw, offs, NOW + k, presence=False)
+    assert g.cursor == c.cursor > g.cfg.store_cap
+    for et, asg, lo, hi, pn, ps in ((EV_MEASUREMENT, [1, 2, 3, 150], None, None, 1, 10),
+                                    (EV_LOCATION, list(range(0, 200, 3)), NOW - 40_000, NOW, 2, 25),
+                                    (EV_ALERT, list(range(200)), None, None, 1, 0)):
+        tg, pg, eg = g.query_store(et, asg, lo, hi, pn, ps)
+        tc, pc, ec = c.query_store(et, asg, lo, hi, pn, ps)
+        assert tg == tc and np.array_equal(eg, ec)
+        for k in ("date", "asg", "v0", "v1", "etype"):
+            assert np.array_equal(pg[k], pc[k]), k

@@ -309,6 +309,13 @@ def test_columnar_tenant_end_to_end():
                                                          {"startDate": 1_700_000_000_010, "endDate": 1_700_000_000_019,
                                                           "pageSize": 0}))
         assert rng.num_results == 10
+        # the same reads served from the engine's event ring (hot store) agree with event management
+        hot = run(lambda: api.list_hot_events("Measurement", "Assignment", [dev.device_assignment_id], None, None,
+                                              1, 10))
+        assert hot["numResults"] == 50
+        assert [(h.id, h.value, h.name) for h in hot["results"]] == [(m.id, m.value, m.name) for m in res.results]
+        hl = run(lambda: api.list_hot_events("Location", "Customer", [res.results[0].customer_id]))
+        assert hl["results"][0].latitude == 34.0 and hl["results"][0].id == loc[0].id
         got = []
         end = time.time() + 5
         while not got and time.time() < end:
