@@ -261,6 +261,128 @@ class MongoEventStore(DeviceEventStore):
         return self._c.count_documents({})
 
 
+class CassandraEventStore(DeviceEventStore):
+    """Events in Cassandra over the native CQL client (``persistence/cql_wire.py``), in the
+    reference's denormalised layout (``CassandraEventManagementClient.java:138-160``): one table per
+    index partitioned by ``(entity, event_type, bucket)`` and clustered by ``event_date DESC``,
+    plus ``events_by_id`` / ``events_by_alt_id``; the bucket is ``event_date // bucket_ms``
+    (``CassandraDeviceEventManagement.getBucketValue``).  Event bodies are stored as JSON documents
+    (the reference uses frozen UDTs per event type).  ``event_buckets`` lists the buckets written per
+    entity so unbounded ranges know which partitions to read."""
+
+    _IDX = {DeviceEventIndex.Assignment: ("events_by_assignment", "assignment_id", 0),
+            DeviceEventIndex.Customer: ("events_by_customer", "customer_id", 1),
+            DeviceEventIndex.Area: ("events_by_area", "area_id", 2),
+            DeviceEventIndex.Asset: ("events_by_asset", "asset_id", 3)}
+    _TYPES = [t for t in DeviceEventType]
+
+    def __init__(self, address: str = "127.0.0.1:9042", keyspace: str = "sitewhere", bucket_ms: int = 3600_000,
+                 username: str | None = None, password: str | None = None):
+        from .cql_wire import CqlSession
+        self.bucket_ms = int(bucket_ms)
+        self.s = CqlSession(address, None, username, password)
+        keyspace = "".join(ch if ch.isalnum() else "_" for ch in keyspace).lower()
+        self.ks = keyspace
+        self._lock = threading.RLock()
+        self.s.execute(f"CREATE KEYSPACE IF NOT EXISTS {keyspace} WITH replication = "
+                       "{'class': 'SimpleStrategy', 'replication_factor': 1}")
+        self.s.execute(f"USE {keyspace}")
+        self.s.execute("CREATE TABLE IF NOT EXISTS events_by_id (event_id text PRIMARY KEY, event_type tinyint, "
+                       "doc text)")
+        self.s.execute("CREATE TABLE IF NOT EXISTS events_by_alt_id (alt_id text PRIMARY KEY, event_id text, doc text)")
+        for table, col, _ in self._IDX.values():
+            self.s.execute(f"CREATE TABLE IF NOT EXISTS {table} ({col} text, event_type tinyint, bucket int, "
+                           f"event_date timestamp, event_id text, doc text, PRIMARY KEY (({col}, event_type, bucket), "
+                           "event_date, event_id)) WITH CLUSTERING ORDER BY (event_date DESC, event_id ASC)")
+        self.s.execute("CREATE TABLE IF NOT EXISTS responses_by_invocation (orig_id text, event_date timestamp, "
+                       "event_id text, doc text, PRIMARY KEY ((orig_id), event_date, event_id)) "
+                       "WITH CLUSTERING ORDER BY (event_date DESC, event_id ASC)")
+        self.s.execute("CREATE TABLE IF NOT EXISTS event_buckets (entity_id text, index_kind tinyint, "
+                       "event_type tinyint, bucket int, PRIMARY KEY ((entity_id, index_kind, event_type), bucket)) "
+                       "WITH CLUSTERING ORDER BY (bucket DESC)")
+        self.s.execute("CREATE TABLE IF NOT EXISTS event_counts (k text PRIMARY KEY, n bigint)")
+
+    def bucket_of(self, date_ms: int) -> int:
+        return int(date_ms) // self.bucket_ms
+
+    def _tcode(self, et) -> int:
+        return self._TYPES.index(et)
+
+    def add_events(self, events):
+        with self._lock:
+            for e in events:
+                doc = json.dumps(e.to_dict(), separators=(",", ":"))
+                d = int(e.event_date or 0)
+                b = self.bucket_of(d)
+                tc = self._tcode(e.event_type)
+                new = not self.s.execute("SELECT event_id FROM events_by_id WHERE event_id = ?", [e.id])
+                self.s.execute("INSERT INTO events_by_id (event_id, event_type, doc) VALUES (?, ?, ?)", [e.id, tc, doc])
+                if e.alternate_id:
+                    self.s.execute("INSERT INTO events_by_alt_id (alt_id, event_id, doc) VALUES (?, ?, ?)",
+                                   [e.alternate_id, e.id, doc])
+                for idx, (table, col, kind) in self._IDX.items():
+                    ent = getattr(e, _INDEX_FIELD[idx])
+                    if not ent:
+                        continue
+                    self.s.execute(f"INSERT INTO {table} ({col}, event_type, bucket, event_date, event_id, doc) "
+                                   "VALUES (?, ?, ?, ?, ?, ?)", [ent, tc, b, d, e.id, doc])
+                    self.s.execute("INSERT INTO event_buckets (entity_id, index_kind, event_type, bucket) "
+                                   "VALUES (?, ?, ?, ?)", [ent, kind, tc, b])
+                orig = getattr(e, "originating_event_id", None)
+                if orig and e.event_type == DeviceEventType.CommandResponse:
+                    self.s.execute("INSERT INTO responses_by_invocation (orig_id, event_date, event_id, doc) "
+                                   "VALUES (?, ?, ?, ?)", [orig, d, e.id, doc])
+                if new:
+                    cur = self.s.execute("SELECT n FROM event_counts WHERE k = ?", ["events"])
+                    self.s.execute("INSERT INTO event_counts (k, n) VALUES (?, ?)",
+                                   ["events", (cur[0]["n"] if cur else 0) + 1])
+        return events
+
+    def get_event_by_id(self, id):
+        r = self.s.execute("SELECT doc FROM events_by_id WHERE event_id = ?", [id])
+        return event_from_dict(json.loads(r[0]["doc"])) if r else None
+
+    def get_event_by_alternate_id(self, alt):
+        r = self.s.execute("SELECT doc FROM events_by_alt_id WHERE alt_id = ?", [alt])
+        return event_from_dict(json.loads(r[0]["doc"])) if r else None
+
+    @staticmethod
+    def _page(rows, c):
+        rows.sort(key=lambda r: (-r["event_date"], r["event_id"]))
+        total = len(rows)
+        if c.page_size > 0:
+            lo = (max(1, c.page_number) - 1) * c.page_size
+            rows = rows[lo:lo + c.page_size]
+        return SearchResults(total, [event_from_dict(json.loads(r["doc"])) for r in rows])
+
+    def list_events(self, event_type, index, entity_ids, criteria=None):
+        c = criteria or DateRangeSearchCriteria()
+        table, col, kind = self._IDX[index]
+        tc = self._tcode(event_type)
+        lo = c.start_date if c.start_date is not None else -(1 << 62)
+        hi = c.end_date if c.end_date is not None else (1 << 62)
+        blo = max(self.bucket_of(max(lo, -(1 << 50))), -(1 << 31))
+        bhi = min(self.bucket_of(min(hi, 1 << 50)), (1 << 31) - 1)
+        rows = []
+        for ent in entity_ids:
+            buckets = self.s.execute("SELECT bucket FROM event_buckets WHERE entity_id = ? AND index_kind = ? AND "
+                                     "event_type = ? AND bucket >= ? AND bucket <= ?", [ent, kind, tc, blo, bhi])
+            for bk in buckets:                    # newest bucket first (clustering order)
+                rows += self.s.execute(f"SELECT event_date, event_id, doc FROM {table} WHERE {col} = ? AND "
+                                       "event_type = ? AND bucket = ? AND event_date >= ? AND event_date <= ?",
+                                       [ent, tc, bk["bucket"], lo, hi])
+        return self._page(rows, c)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        rows = self.s.execute("SELECT event_date, event_id, doc FROM responses_by_invocation WHERE orig_id = ?",
+                              [invocation_id])
+        return self._page(rows, criteria or DateRangeSearchCriteria())
+
+    def count(self):
+        r = self.s.execute("SELECT n FROM event_counts WHERE k = ?", ["events"])
+        return int(r[0]["n"]) if r else 0
+
+
 class BucketedEventStore(DeviceEventStore):
     """Cassandra layout: partition = (entity, event type, time bucket); rows clustered by date DESC.
 
@@ -540,6 +662,9 @@ def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
         return MemoryEventStore()
     if kind == "sqlite":
         return SQLiteEventStore(kw.get("path", ":memory:"))
+    if kind == "cassandra" and kw.get("address"):
+        return CassandraEventStore(kw["address"], kw.get("keyspace", "sitewhere"), kw.get("bucket_ms", 3600_000),
+                                   kw.get("username"), kw.get("password"))
     if kind in ("cassandra", "bucketed"):
         return BucketedEventStore(kw.get("bucket_ms", 3600_000))
     if kind == "columnar":

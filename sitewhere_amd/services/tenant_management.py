@@ -61,9 +61,12 @@ for _svc in ("device-management", "asset-management", "batch-operations", "sched
 TENANT_TEMPLATES["sqlite"]["services"]["event-management"] = {
     "datastore": {"type": "sqlite", "path": "/tmp/sitewhere/[[tenant.token]]-events.db"}, "buffered": True}
 TENANT_TEMPLATES["cassandra"] = copy.deepcopy(TENANT_TEMPLATES["default"])
-TENANT_TEMPLATES["cassandra"]["name"] = "Time-bucketed event store (Cassandra layout)"
-TENANT_TEMPLATES["cassandra"]["services"]["event-management"] = {"datastore": {"type": "bucketed",
-                                                                               "bucket_ms": 3600000}}
+TENANT_TEMPLATES["cassandra"]["name"] = "Cassandra event store (time-bucketed partitions)"
+# with cassandra.address set (env CASSANDRA_ADDRESS) events go to Cassandra over the native CQL client in the
+# reference's table layout; without it the same partition layout is kept in memory (BucketedEventStore)
+TENANT_TEMPLATES["cassandra"]["services"]["event-management"] = {
+    "datastore": {"type": "cassandra", "address": "${cassandra.address:}", "keyspace": "tenant_[[tenant.token]]",
+                  "bucket_ms": 3600000}}
 TENANT_TEMPLATES["mongodb"] = copy.deepcopy(TENANT_TEMPLATES["default"])
 TENANT_TEMPLATES["mongodb"]["name"] = "MongoDB datastores"
 for _svc in ("device-management", "asset-management", "batch-operations", "schedule-management", "device-state",
