@@ -69,12 +69,14 @@ def main():
         batches.append((np.concatenate([raw, np.zeros(64, np.uint8)]), offs))
     for k in range(args.warmup):
         ib.process_batch(*batches[k % 4])
+    ib.flush()
     base = ib.persisted_events.count
     t = time.perf_counter()
     ev = 0
     for k in range(args.batches):
         r = ib.process_batch(*batches[k % 4])
         ev += r.n_events
+    ib.flush()
     dt = time.perf_counter() - t
     em_store = sw.tenant_engine("event-management", "fast").store
     breakdown = {name: round(t.hist.snapshot()["mean"], 3)

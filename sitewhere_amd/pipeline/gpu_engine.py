@@ -486,6 +486,21 @@ class GpuInboundEngine(EngineBase):
         dev_o[:no].copy_(pin_o[:no], non_blocking=True)
         return dev_r[:nb], dev_o[:no]
 
+    def _pinned_out(self, nbytes: int):
+        """A pinned host buffer (torch tensor + its full numpy view) that no earlier StepResult still
+        references: a live ``result.out`` view pins its base array, so results are returned without a
+        copy and without fresh pageable pages per step."""
+        import sys
+        pool = self.__dict__.setdefault("_pin_pool", [])
+        for pin, arr in pool:
+            if arr.nbytes >= nbytes and sys.getrefcount(arr) <= 3:   # pool tuple, loop variable, the call
+                return pin, arr
+        pin = torch.empty(max(nbytes, self.out_cap * OUT_REC_SIZE), dtype=torch.uint8).pin_memory()
+        arr = pin.numpy()
+        if len(pool) < 4:
+            pool.append((pin, arr))
+        return pin, arr
+
     def collect(self, sel: int, raw_host: np.ndarray | None, from_device: bool = False) -> StepResult:
         sc = self.scalars()
         nn = min(sc["n_new_names"], self.cfg.names_cap)
@@ -495,7 +510,11 @@ class GpuInboundEngine(EngineBase):
             new = self.learn_names(refs, raw_host)
         n_out = sc["n_out"]
         if from_device:
-            out = self.out_dev[sel][:n_out * OUT_REC_SIZE].cpu().numpy().view(OUT_REC)
+            nb = n_out * OUT_REC_SIZE
+            pin, arr = self._pinned_out(nb)
+            if nb:
+                pin[:nb].copy_(self.out_dev[sel][:nb])      # pinned target: a full-rate DMA
+            out = arr[:nb].view(OUT_REC)
         else:
             out = self.out_host[sel].view(OUT_REC, n_out).copy()
         first_seq = int(self.t["cursor"][1].item())

@@ -22,6 +22,7 @@ are routed exactly like the reference routes them (unregistered / registration t
 from __future__ import annotations
 
 import json
+import queue
 import struct
 import threading
 import time
@@ -101,8 +102,17 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._ckpt_offsets: dict[tuple[str, int], int] = {}
         self._since_ckpt = 0
         self.checkpoints = 0
+        # Host-side storage of a step's rows (columnar encode, event-management RPC, enriched publish)
+        # runs on a store thread, overlapped with the next engine step.  Raw-topic offsets are then
+        # committed by that thread once a batch is stored (at-least-once holds); with a checkpoint
+        # the snapshot owns the commits.
+        self.async_store = bool(cfg.get("asyncStore", self.storage == "columnar"))
+        self._store_q: queue.Queue = queue.Queue(maxsize=2)
+        self._store_thread = None
+        self._store_error = None
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
-                                        self._process_raw, max_records=16, auto_commit=self.ckpt_path is None)
+                                        self._process_raw, max_records=16,
+                                        auto_commit=self.ckpt_path is None and not self.async_store)
         self.persisted_events = self.create_meter("persistedEvents")
         self.step_timer = self.create_timer("engineStep")
         self.store_timer = self.create_timer("columnarStore")       # payload build + event-management call
@@ -202,10 +212,19 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.restore_checkpoint()
         self.load_model()
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
+        if self.async_store:
+            self._store_thread = threading.Thread(target=self._store_loop, daemon=True,
+                                                  name=f"engine-store-{self.tenant.token}")
+            self._store_thread.start()
         self.start_nested_component(self.raw_consumer, monitor, require=True)
 
     def tenant_stop(self, monitor):
         self.raw_consumer.lifecycle_stop(monitor)
+        if self._store_thread is not None:
+            self.flush()
+            self._store_q.put(None)
+            self._store_thread.join(10)
+            self._store_thread = None
         if self.ckpt_path and self._since_ckpt:
             self.checkpoint()
         super().tenant_stop(monitor)
@@ -250,25 +269,57 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         for r in recs:
             raw, offs = unpack_raw_batch(r.value)
             # the record timestamp is the batch's receive time: replay after a restore is deterministic
-            self.process_batch(raw, offs, now=r.timestamp or None)
+            commit = (r.topic, r.partition, r.offset + 1) if self.async_store and not self.ckpt_path else None
+            self.process_batch(raw, offs, now=r.timestamp or None, commit=commit)
             if self.ckpt_path:
                 self._ckpt_offsets[(r.topic, r.partition)] = r.offset + 1
                 self._since_ckpt += 1
                 if self._since_ckpt >= self.ckpt_every:
                     self.checkpoint()
 
-    def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None):
+    def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None, commit=None):
+        """One engine step; storing its rows happens here or, with ``asyncStore``, on the store thread
+        while the next step runs (call :meth:`flush` to wait for it)."""
         now = now or now_ms()
         with self._lock, self.step_timer.time():
             res = self.engine.step(raw, offs, now)
         self.processed_events.mark(res.n_events)
+        if self._store_thread is not None:
+            if self._store_error is not None:
+                err, self._store_error = self._store_error, None
+                raise RuntimeError("engine store thread failed") from err
+            self._store_q.put((res, now, raw, offs, commit))
+        else:
+            self._store_step(res, now, raw, offs, commit)
+        return res
+
+    def _store_step(self, res, now, raw, offs, commit):
         if self.storage == "columnar":
             self._store_columnar(res, now)
         else:
             self._store_objects(res, now)
         if res.rejects is not None and len(res.rejects):
             self._slow_path(raw, offs, res)
-        return res
+        if commit is not None:
+            self.ms.instance.bus.commit(self.raw_consumer.group, *commit)
+
+    def _store_loop(self):
+        while True:
+            item = self._store_q.get()
+            try:
+                if item is None:
+                    return
+                self._store_step(*item)
+            except Exception as e:  # noqa: BLE001 -- surfaced on the next process_batch
+                self._store_error = e
+                self.logger.exception("engine store step failed")
+            finally:
+                self._store_q.task_done()
+
+    def flush(self):
+        """Wait until every stepped batch is stored (and its raw offset committed)."""
+        if self._store_thread is not None:
+            self._store_q.join()
 
     def columnar_payload(self, res, now: int) -> bytes:
         """Rows + the dictionary entries the receiver has not seen yet (assignment context, names)."""
@@ -455,4 +506,5 @@ class GpuInboundApi:
         """Synchronous injection (tests / REST): one engine step over the given wire payloads."""
         raw, offs = pack_messages([bytes(p) for p in payloads])
         r = self._e.process_batch(raw, offs)
+        self._e.flush()
         return {"messages": r.n_msgs, "events": r.n_events, "persisted": r.n_persisted}
