@@ -4,9 +4,11 @@
       bus (Kafka role, native commit log) + coordination (ZooKeeper role) server; --kafka-port also
       serves the bus over the Kafka wire protocol (bus/kafka_broker.py) to any Kafka client
   python -m sitewhere_amd.serve service <identifier> [<identifier> ...] --infra HOST:PORT [--kafka BOOTSTRAP]
+                                         [--zookeeper HOST:PORT/CHROOT]
       one or more microservices in this process, talking to the shared infra and to other
       processes' services over gRPC (topology-discovered replicas); with --kafka the data plane is
-      a Kafka cluster (bus/kafka_client.KafkaEventBus), as in the reference deployment
+      a Kafka cluster (bus/kafka_client.KafkaEventBus) and with --zookeeper the coordination is a
+      ZooKeeper ensemble (coord/zk.py), as in the reference deployment
   python -m sitewhere_amd.serve all [--rest-port 8080] [--mqtt-port 1883] [--data DIR]
       a whole instance in one process (single-node deployment; GPU inbound engine per tenant)
 
@@ -69,6 +71,10 @@ def build_instance(args, network: bool):
     if kafka:
         from .bus.kafka_client import KafkaEventBus
         kw["bus"] = KafkaEventBus(kafka)
+    zk = getattr(args, "zookeeper", None) or os.environ.get("SITEWHERE_ZOOKEEPER")
+    if zk:
+        from .coord.zk import ZooKeeperCoordination
+        kw["coord"] = ZooKeeperCoordination(zk if "/" in zk else zk + "/sitewhere")
     secret = os.environ.get("SITEWHERE_JWT_SECRET") or args.jwt_secret
     return Instance(settings, jwt_secret=secret, network_rpc=network, **kw)
 
@@ -135,6 +141,7 @@ def main(argv=None) -> int:
     p.add_argument("identifiers", nargs="+")
     p.add_argument("--infra", required=True)
     p.add_argument("--kafka", default=None, help="Kafka bootstrap servers for the data plane")
+    p.add_argument("--zookeeper", default=None, help="ZooKeeper connect string (host:port[,..][/chroot])")
     p.add_argument("--grpc-port", type=int, default=0)
     p.add_argument("--rest-port", type=int, default=0)
     p = sub.add_parser("all")
