@@ -233,6 +233,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     def checkpoint(self):
         """Snapshot the shard + the raw-topic offsets it covers, then commit those offsets."""
         import os
+        self.flush()            # every batch the snapshot covers must be stored before its offset commits
         with self._lock:
             extra = {"boot": self.boot, "offsets": [[t, p, o] for (t, p), o in self._ckpt_offsets.items()],
                      "dev_index": self.dev_index.ids, "asg_index": self.asg_index.ids,
