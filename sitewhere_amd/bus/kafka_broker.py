@@ -11,6 +11,9 @@ One broker node (id 0) owns every partition.  Topics, offsets and committed grou
 same streams and consumer groups.  The group coordinator implements the Kafka group protocol
 (JoinGroup / SyncGroup / Heartbeat / LeaveGroup): members are assigned partitions by their elected
 leader, exactly as with a real broker.  Optional SASL/PLAIN authentication (``users``).
+Each API is served at one version (``kafka_wire.VERSIONS``), which clients from 0.11 through 3.x
+negotiate through ApiVersions; clients that dropped those versions (4.x removed JoinGroup v0-v1)
+are refused at negotiation rather than misunderstood.
 
     srv = KafkaBrokerServer(bus, port=9092).start()
 """
