@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import bisect
 import json
+import logging
 import queue
 import sqlite3
 import threading
@@ -459,19 +460,56 @@ class BucketedEventStore(DeviceEventStore):
 
 class BufferedEventWriter:
     """Bulk write buffer in front of any store (reference DeviceEventBuffer: queue 10,000,
-    flush at 200 docs or every 250 ms).  ``add`` blocks when the queue is full (back-pressure)."""
+    flush at 200 docs or every 250 ms).  ``add`` blocks when the queue is full (back-pressure).
+
+    A failed bulk write is retried with backoff (0.05 s doubling to 2 s) until it succeeds -- the
+    events stay buffered, never dropped, while the store is unavailable.  Buffered events are
+    indexed by alternate id (``pending_alternate``) so a redelivery arriving before the flush is
+    still deduplicated."""
 
     def __init__(self, store: DeviceEventStore, max_queue: int = 10_000, chunk: int = 200, interval_ms: int = 250):
         self.store, self.chunk, self.interval = store, chunk, interval_ms / 1000.0
         self.q: queue.Queue = queue.Queue(max_queue)
         self._stop = threading.Event()
+        self._pending: dict = {}
+        self._plock = threading.Lock()
         self._t = threading.Thread(target=self._run, daemon=True, name="event-buffer")
         self.flushes = 0
+        self.failed_writes = 0
         self._t.start()
 
     def add(self, events):
+        with self._plock:
+            for e in events:
+                if e.alternate_id:
+                    self._pending[e.alternate_id] = e
         for e in events:
             self.q.put(e)
+
+    def pending_alternate(self, alt: str):
+        with self._plock:
+            return self._pending.get(alt)
+
+    def _write(self, buf):
+        backoff = 0.05
+        while True:
+            try:
+                self.store.add_events(buf)
+                break
+            except Exception:
+                self.failed_writes += 1
+                if self._stop.is_set() and backoff >= 2.0:
+                    logging.getLogger(__name__).exception("dropping %d buffered events at shutdown", len(buf))
+                    break
+                logging.getLogger(__name__).warning("bulk write of %d events failed; retrying in %.2fs",
+                                                    len(buf), backoff, exc_info=True)
+                time.sleep(backoff)
+                backoff = min(2.0, backoff * 2)
+        self.flushes += 1
+        with self._plock:
+            for e in buf:
+                if e.alternate_id and self._pending.get(e.alternate_id) is e:
+                    del self._pending[e.alternate_id]
 
     def _run(self):
         buf = []
@@ -482,17 +520,15 @@ class BufferedEventWriter:
             except queue.Empty:
                 pass
             if buf and (len(buf) >= self.chunk or time.time() - last >= self.interval):
-                self.store.add_events(buf)
-                self.flushes += 1
+                self._write(buf)
                 buf = []
                 last = time.time()
         if buf:
-            self.store.add_events(buf)
-            self.flushes += 1
+            self._write(buf)
 
     def flush(self, timeout: float = 5.0):
         end = time.time() + timeout
-        while not self.q.empty() and time.time() < end:
+        while (not self.q.empty() or self._pending) and time.time() < end:
             time.sleep(0.01)
         time.sleep(self.interval * 1.5)
 

@@ -38,6 +38,8 @@ class BusConsumer(TenantEngineLifecycleComponent):
         self._t = None
         self.processed = 0
         self.failures = 0
+        self.retries = 0          # batches re-read after a handler failure
+        self.dropped = 0          # records of poison batches skipped after max_attempts
         # False: the handler commits explicit offsets itself (checkpoint-aligned commits)
         self.auto_commit = auto_commit
 
@@ -49,17 +51,26 @@ class BusConsumer(TenantEngineLifecycleComponent):
         self._t = threading.Thread(target=self._run, daemon=True, name=f"consumer-{self.component_name}")
         self._t.start()
 
-    def _call(self, recs):
+    # A failed batch is re-read from its first record (the partition is not committed past it) with
+    # exponential backoff: transient faults (RPC unavailable, storage hiccups) cost retries, never
+    # records.  A batch failing ``max_attempts`` times in a row is a poison batch: it is logged,
+    # counted in ``dropped`` and skipped so the partition is not wedged forever.
+    max_attempts = 10
+
+    def _call(self, recs) -> bool:
         try:
             # sends made while handling this batch go out in one produce round trip, before the commit
             with self.engine.ms.producer.batching():
                 self.handler(recs)
             self.processed += len(recs)
+            return True
         except Exception:
             self.failures += len(recs)
             self.logger.exception("consumer %s failed to process %d records", self.component_name, len(recs))
+            return False
 
     def _run(self):
+        backoff, attempts = 0.05, {}
         while not self._stop.is_set():
             try:
                 batch = self.consumer.poll(100, self.max_records)
@@ -69,17 +80,43 @@ class BusConsumer(TenantEngineLifecycleComponent):
                 continue
             if not batch:
                 continue
+            ok: dict = {}
             if self.pool is None:
-                for recs in batch.values():
-                    self._call(recs)
+                for tp, recs in batch.items():
+                    ok[tp] = self._call(recs)
             else:
-                futs = []
-                for recs in batch.values():
+                futs = {}
+                for tp, recs in batch.items():
                     step = max(1, len(recs) // self.threads)
-                    futs += [self.pool.submit(self._call, recs[i:i + step]) for i in range(0, len(recs), step)]
-                wait(futs)
+                    futs[tp] = [self.pool.submit(self._call, recs[i:i + step]) for i in range(0, len(recs), step)]
+                wait([f for fs in futs.values() for f in fs])
+                ok = {tp: all(f.result() for f in fs) for tp, fs in futs.items()}
+            failed = {}
+            for tp, good in ok.items():
+                first = batch[tp][0].offset
+                if good:
+                    attempts.pop(tp, None)
+                    continue
+                n = attempts.get(tp, (first, 0))[1] + 1 if attempts.get(tp, (None,))[0] == first else 1
+                if n >= self.max_attempts:
+                    attempts.pop(tp, None)
+                    self.dropped += len(batch[tp])
+                    self.logger.error("consumer %s: dropping poison batch %s@%d after %d attempts",
+                                      self.component_name, tp, first, n)
+                    continue
+                attempts[tp] = (first, n)
+                failed[tp] = first
+                self.consumer.seek(tp[0], tp[1], first)         # re-read it: at-least-once
             if self.auto_commit:
-                self.consumer.commit()   # after processing: at-least-once
+                offsets = {tp: pos for tp, pos in self.consumer.positions.items() if tp not in failed}
+                if offsets:
+                    self.consumer.commit(offsets)               # after processing: at-least-once
+            if failed:
+                self.retries += 1
+                self._stop.wait(backoff)
+                backoff = min(2.0, backoff * 2)
+            else:
+                backoff = 0.05
 
     def stop(self, monitor):
         self._stop.set()

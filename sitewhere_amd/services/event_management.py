@@ -73,7 +73,8 @@ class DeviceEventManagement:
         for r in reqs:
             alt = r.get("alternateId")
             if alt:
-                ex = seen.get(alt) or self.store.get_event_by_alternate_id(alt)
+                ex = seen.get(alt) or (self._writer is not None and self._writer.pending_alternate(alt)) \
+                    or self.store.get_event_by_alternate_id(alt)
                 if ex is not None:
                     out.append(ex)
                     continue
@@ -152,7 +153,8 @@ class DeviceEventManagement:
         return self.store.get_event_by_id(id)
 
     def get_device_event_by_alternate_id(self, alt: str):
-        return self.store.get_event_by_alternate_id(alt)
+        return (self._writer is not None and self._writer.pending_alternate(alt)) or \
+            self.store.get_event_by_alternate_id(alt)
 
     def _list(self, et, index, ids, criteria):
         return self.store.list_events(et, DeviceEventIndex(index) if isinstance(index, str) else index, list(ids),

@@ -17,6 +17,7 @@ payload batches (see :mod:`sitewhere_amd.services.gpu_inbound`).
 from __future__ import annotations
 
 import json
+import time
 
 from ..models.domain import DeviceAssignmentStatus, DeviceEventType
 from ..rpc import codec
@@ -121,13 +122,21 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
                 self.logger.exception("failed to process inbound payload")
         for key in order:
             reqs = groups[key]
-            try:
-                with self.event_storage.time():
-                    getattr(em, key[1])(key[0], reqs)
-                self.processed_events.mark(len(reqs))
-            except Exception:
-                self.failed_events.mark(len(reqs))
-                self.logger.exception("failed to store %d events", len(reqs))
+            # A storage failure is transient (event management unavailable / restarting): retry the
+            # call in place, then fail the batch so the consumer re-reads it from its first record
+            # (at-least-once; alternate-id idempotent storage absorbs the replayed prefix).  Only
+            # malformed payloads (above) are counted as failed and skipped.
+            for attempt in range(4):
+                try:
+                    with self.event_storage.time():
+                        getattr(em, key[1])(key[0], reqs)
+                    self.processed_events.mark(len(reqs))
+                    break
+                except Exception:
+                    if attempt == 3:
+                        self.logger.warning("storing %d events failed; batch will be redelivered", len(reqs))
+                        raise
+                    time.sleep(0.02 * (1 << attempt))
 
     def _validate(self, p: dict):
         token = p["deviceToken"]

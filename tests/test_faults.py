@@ -1,0 +1,126 @@
+"""Delivery semantics under injected faults: consumer redelivery after handler
+failures, poison-batch skipping, buffered-writer retries, and the seeded fault injector itself."""
+from __future__ import annotations
+
+import threading
+import time
+from types import SimpleNamespace
+
+import pytest
+
+from sitewhere_amd.bus.log import EventBus
+from sitewhere_amd.models.domain import DeviceMeasurement
+from sitewhere_amd.persistence.events import BufferedEventWriter, MemoryEventStore
+from sitewhere_amd.runtime.consumers import BusConsumer
+from sitewhere_amd.utils.faults import FaultInjector, InjectedFault
+
+
+def _engine(bus):
+    return SimpleNamespace(ms=SimpleNamespace(instance=SimpleNamespace(bus=bus), producer=bus.producer()))
+
+
+def _wait(cond, timeout=10.0):
+    end = time.time() + timeout
+    while time.time() < end and not cond():
+        time.sleep(0.01)
+    return cond()
+
+
+@pytest.mark.parametrize("threads", [0, 3])
+def test_consumer_redelivers_failed_batches(threads):
+    bus = EventBus(default_partitions=2)
+    prod = bus.producer()
+    for i in range(300):
+        prod.send("t", f"k{i % 7}", str(i).encode())
+    seen, lock = [], threading.Lock()
+    fi = FaultInjector(seed=3)
+
+    def handler(recs):
+        if fi._roll(0.4 if threads == 0 else 0.15):      # threaded: a batch needs every slice to succeed
+            raise InjectedFault("transient")
+        with lock:
+            seen.extend(int(r.value) for r in recs)
+    c = BusConsumer(_engine(bus), "c", ["t"], handler, threads=threads, max_records=40, group="g-redeliver")
+    c.max_attempts = 1000
+    c.start(None)
+    try:
+        assert _wait(lambda: set(seen) == set(range(300)), 30)
+        assert c.retries > 0 and c.failures > 0 and c.dropped == 0
+        # committed positions cover everything once the last batch succeeded
+        assert _wait(lambda: sum(bus.committed("g-redeliver", "t", p) for p in range(2)) == 300)
+    finally:
+        c._stop.set()
+        c._t.join(5)
+    # a fresh member of the group resumes after the committed positions: nothing redelivered
+    c2 = bus.consumer("g-redeliver", ["t"])
+    assert not any(c2.poll(50).values())
+
+
+def test_consumer_skips_poison_batch():
+    bus = EventBus(default_partitions=1)
+    prod = bus.producer()
+    for i in range(30):
+        prod.send("p", "k", str(i).encode())
+    ok = []
+
+    def handler(recs):
+        if any(r.value == b"13" for r in recs):
+            raise ValueError("poison")
+        ok.extend(int(r.value) for r in recs)
+    c = BusConsumer(_engine(bus), "c", ["p"], handler, max_records=10, group="g-poison")
+    c.max_attempts = 3
+    c.start(None)
+    try:
+        assert _wait(lambda: c.dropped == 10 and len(ok) == 20, 30)
+        assert sorted(ok) == list(range(10)) + list(range(20, 30))
+        assert c.retries == 2
+    finally:
+        c._stop.set()
+        c._t.join(5)
+
+
+def _events(n, prefix):
+    out = []
+    for i in range(n):
+        e = DeviceMeasurement(name="m", value=float(i))
+        e.id, e.alternate_id, e.device_assignment_id, e.event_date = f"{prefix}{i}", f"{prefix}alt{i}", "a", i
+        out.append(e)
+    return out
+
+
+def test_buffered_writer_retries_until_store_recovers():
+    store = MemoryEventStore()
+    w = BufferedEventWriter(store, chunk=50, interval_ms=20)
+    with FaultInjector(seed=1) as fi:
+        fi.fail(store, "add_events", 1.0)                  # store down
+        evs = _events(120, "bw")
+        w.add(evs)
+        assert w.pending_alternate("bwalt5") is evs[5]     # dedup sees buffered events
+        assert _wait(lambda: w.failed_writes >= 3, 10)
+        assert store.count() == 0
+    assert _wait(lambda: store.count() == 120, 10)         # store back: everything written once
+    assert _wait(lambda: w.pending_alternate("bwalt5") is None)
+    w.close()
+
+
+def test_fault_injector_is_seeded_and_restores():
+    class Obj:
+        def f(self):
+            return 1
+    o = Obj()
+    runs = []
+    for _ in range(2):
+        with FaultInjector(seed=42) as fi:
+            fi.fail(o, "f", 0.5)
+            seq = []
+            for _ in range(50):
+                try:
+                    seq.append(o.f())
+                except InjectedFault:
+                    seq.append(0)
+            runs.append(seq)
+        assert "f" not in o.__dict__ and o.f() == 1
+    assert runs[0] == runs[1] and 0 < sum(runs[0]) < 50
+    with FaultInjector(seed=0) as fi:
+        fi.drop(o, "f", 1.0, empty=[])
+        assert o.f() == []
