@@ -406,6 +406,11 @@ def build_receiver(rc: dict) -> Receiver:
         return CoapReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 0)))
     if t == "rest-poll":
         return PollingRestReceiver(rc["url"], float(rc.get("interval", 10.0)), rc.get("headers"))
+    if t == "activemq-broker" or (t in ("activemq", "stomp") and rc.get("transportUri")):
+        from .stomp import StompBrokerReceiver
+        return StompBrokerReceiver(rc.get("transportUri", "stomp://127.0.0.1:61613"),
+                                   rc.get("queueName", "SITEWHERE.IN"), int(rc.get("numConsumers", 3)),
+                                   rc.get("brokerName"))
     if t in ("activemq", "stomp"):
         from .stomp import StompReceiver
         return StompReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 61613)),

@@ -307,3 +307,37 @@ class StompReceiver(TenantEngineLifecycleComponent):
         self._stop.set()
         if self.client:
             self.client.close()
+
+
+def parse_transport_uri(uri: str, default_port: int = 61613) -> tuple[str, int]:
+    """``stomp://host:port?opts`` (or ``tcp://``) -> (host, port); query options are ignored."""
+    rest = uri.split("://", 1)[-1].split("?", 1)[0].rstrip("/")
+    host, _, port = rest.rpartition(":")
+    if not host:
+        return rest or "127.0.0.1", default_port
+    return host, int(port)
+
+
+class StompBrokerReceiver(StompReceiver):
+    """Embedded-broker receiver (reference ``ActiveMQBrokerEventReceiver.java:60-120``, selected by
+    ``transportUri`` in ``EventSourcesParser.java:481-491``): the receiver itself hosts the message
+    broker on ``transportUri`` so devices connect straight to the event source, then consumes the
+    configured queue with ``numConsumers`` workers."""
+
+    def __init__(self, transport_uri: str = "stomp://127.0.0.1:61613", queue_name: str = "SITEWHERE.IN",
+                 num_consumers: int = 3, broker_name: str | None = None):
+        host, port = parse_transport_uri(transport_uri)
+        dest = queue_name if queue_name.startswith("/") else f"/queue/{queue_name}"
+        super().__init__("127.0.0.1" if host in ("0.0.0.0", "") else host, port, dest, num_threads=num_consumers)
+        self.bind_host, self.transport_uri, self.broker_name = host, transport_uri, broker_name
+        self.broker = None
+
+    def start(self, monitor):
+        self.broker = StompBroker(self.bind_host, self.port).start()
+        self.port = self.broker.port                  # port 0: the broker picked one
+        super().start(monitor)
+
+    def stop(self, monitor):
+        super().stop(monitor)
+        if self.broker is not None:
+            self.broker.stop()

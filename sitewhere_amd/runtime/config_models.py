@@ -24,10 +24,14 @@ DECODER = E("Decoder", "event-source-decoder", "Payload decoder", [
       ["protobuf", "json", "json-batch", "script", "echo", "composite"]),
     A("script", "Script", "decoder script id (type=script)")])
 RECEIVER = E("Receiver", "event-source-receiver", "Protocol receiver", [
-    A("type", "String", "mqtt | socket | websocket | coap | rest-poll | activemq | rabbitmq | kafka | eventhub", True,
-      choices=["mqtt", "socket", "websocket", "coap", "rest-poll", "activemq", "rabbitmq", "kafka", "eventhub"]),
+    A("type", "String", "mqtt | socket | websocket | coap | rest-poll | activemq | activemq-broker | rabbitmq | kafka | "
+      "eventhub", True, choices=["mqtt", "socket", "websocket", "coap", "rest-poll", "activemq", "activemq-broker",
+                                  "rabbitmq", "kafka", "eventhub"]),
     A("host", "String", "broker / bind host", default="127.0.0.1"), A("port", "Integer", "port"),
     A("topic", "String", "MQTT topic"), A("queue", "String", "AMQP queue"), A("destination", "String", "STOMP destination"),
+    A("transportUri", "String", "embedded broker transport (activemq-broker), e.g. stomp://0.0.0.0:2345"),
+    A("queueName", "String", "embedded broker queue (activemq-broker)"),
+    A("numConsumers", "Integer", "embedded broker queue consumers", default=3),
     A("qos", "Integer", "MQTT QoS", default=1), A("numThreads", "Integer", "processing threads", default=4)])
 SOURCE = E("Event Source", "event-source", "Decoder + deduplicator + receivers", [
     A("id", "String", "source id", True), A("decoder", "String", "decoder type or element", True),

@@ -83,6 +83,14 @@ TENANT_TEMPLATES["influxdb"]["name"] = "InfluxDB event store"
 TENANT_TEMPLATES["influxdb"]["services"]["event-management"] = {
     "datastore": {"type": "influxdb", "url": "${influxdb.url:http://localhost:8086}",
                   "database": "tenant-[[tenant.token]]"}, "buffered": True}
+# reference templates/stomp: one event source hosting an ActiveMQ-style broker (STOMP transport) and
+# decoding JSON batches from its queue
+TENANT_TEMPLATES["stomp"] = copy.deepcopy(TENANT_TEMPLATES["default"])
+TENANT_TEMPLATES["stomp"]["name"] = "STOMP event source"
+TENANT_TEMPLATES["stomp"]["services"]["event-sources"]["sources"] = [
+    {"id": "stomp", "decoder": "json-batch",
+     "receivers": [{"type": "activemq-broker", "transportUri": "stomp://${stomp.host:127.0.0.1}:${stomp.port:2345}",
+                    "queueName": "SITEWHERE.STOMP", "numConsumers": 5}]}]
 TENANT_TEMPLATES["gpu"] = copy.deepcopy(TENANT_TEMPLATES["default"])
 TENANT_TEMPLATES["gpu"]["name"] = "MI355X-accelerated inbound pipeline"
 TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "batchSize": 65536, "maxDelayMs": 5,

@@ -220,3 +220,41 @@ def test_solr_connector_indexes_and_search_provider_queries():
         assert len(hits) == 2 and all(h["assignmentId"] == "a1" for h in hits)
     finally:
         srv.shutdown()
+
+
+def test_stomp_template_tenant_hosts_broker(monkeypatch):
+    """Reference templates/stomp: the tenant's event source hosts the broker; a STOMP client sends a
+    JSON batch to SITEWHERE.STOMP and the measurements are stored."""
+    import json
+    import socket
+    import time
+
+    from sitewhere_amd.assembly import SiteWhereInstance
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    monkeypatch.setenv("STOMP_PORT", str(port))
+    sw = SiteWhereInstance().start()
+    try:
+        sw.wait_for_tenant("default", 60)
+        tm = sw.api("TenantManagement")
+        sw.instance.system_user.run(lambda: tm.create_tenant({"token": "st", "name": "st",
+                                                              "configurationTemplateId": "stomp",
+                                                              "datasetTemplateId": "construction"}))
+        sw.wait_for_tenant("st", 120)
+        run = lambda f: sw.instance.system_user.run(f, "st")  # noqa: E731
+        dm, em = sw.api("DeviceManagement", "st"), sw.api("DeviceEventManagement", "st")
+        aid = run(lambda: dm.get_device_by_token("meitrack-001")).device_assignment_id
+        c = StompClient("127.0.0.1", port).connect()
+        c.send("/queue/SITEWHERE.STOMP", json.dumps({"deviceToken": "meitrack-001", "measurements": [
+            {"name": "stomp.t", "value": 4.5}, {"name": "stomp.h", "value": 0.5}]}).encode(), receipt=True)
+        end, res = time.time() + 30, []
+        while len(res) < 2 and time.time() < end:
+            res = [e for e in run(lambda: em.list_measurements_for_index("Assignment", [aid])).results
+                   if e.name.startswith("stomp.")]
+            time.sleep(0.1)
+        assert sorted((e.name, e.value) for e in res) == [("stomp.h", 0.5), ("stomp.t", 4.5)]
+        c.close()
+    finally:
+        sw.stop()
