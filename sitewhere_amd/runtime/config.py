@@ -86,6 +86,9 @@ class InstanceSettings:
     log_metrics: bool = False
     metrics_period_s: float = 20.0
     tracer_sample_rate: float = 0.01
+    # reference sitewhere.tracer.server: "host[:port]" -> Jaeger agent (UDP compact emitBatch, 6831);
+    # "http(s)://host:4318" -> OTLP/HTTP JSON; empty -> spans stay in the in-process ring only
+    tracer_server: str = ""
     filesystem_storage_root: str = "/tmp/sitewhere"
     tenant_ops_threads: int = 5
     extra: dict = field(default_factory=dict)
@@ -93,7 +96,7 @@ class InstanceSettings:
     @classmethod
     def from_env(cls, **over):
         s = cls(**over)
-        for f in ("product_id", "instance_id", "filesystem_storage_root"):
+        for f in ("product_id", "instance_id", "filesystem_storage_root", "tracer_server"):
             v = os.environ.get("SITEWHERE_" + f.upper())
             if v:
                 setattr(s, f, v)
@@ -101,6 +104,9 @@ class InstanceSettings:
             v = os.environ.get("SITEWHERE_" + f.upper())
             if v:
                 setattr(s, f, int(v))
+        v = os.environ.get("SITEWHERE_TRACER_SAMPLE_RATE")
+        if v:
+            s.tracer_sample_rate = float(v)
         return s
 
 

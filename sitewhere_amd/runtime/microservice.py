@@ -33,6 +33,7 @@ from ..core.lifecycle import (CompositeLifecycleStep, LifecycleComponent, Lifecy
                               TenantEngineLifecycleComponent)
 from ..core.metrics import MetricRegistry, MetricsReporter
 from ..core.security import SystemUser, TokenManagement
+from ..core.trace_export import configure_tracing
 from ..core.tracing import global_tracer
 from ..models.domain import Tenant
 from ..rpc.transport import GrpcChannel, LocalChannel, RpcServer, ServiceProxy, ServiceResolver
@@ -249,6 +250,9 @@ class Microservice(LifecycleComponent):
         self.microservice = self
         self.metrics = MetricRegistry()
         self.tracer = global_tracer()
+        if instance.settings.tracer_server:
+            configure_tracing(instance.settings.tracer_server, instance.settings.tracer_sample_rate,
+                              instance.settings.product_id)
         self.producer = instance.bus.producer()
         self.topology = TopologyStateAggregator(instance.bus, instance.naming.microservice_state_updates(),
                                                 self.hostname, instance.settings.topology_eviction_s)
