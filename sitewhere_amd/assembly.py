@@ -51,7 +51,7 @@ class SiteWhereInstance:
     def __init__(self, settings: InstanceSettings | None = None, template: str = "default",
                  services: list[str] | None = None, instance: Instance | None = None, rest_port: int = 0,
                  **instance_kw):
-        self.instance = instance or Instance(settings or InstanceSettings(heartbeat_s=5.0), **instance_kw)
+        self.instance = instance or Instance(settings or InstanceSettings.from_env(heartbeat_s=5.0), **instance_kw)
         self.template = template
         wanted = set(services) if services else None
         self.instance_management = InstanceManagementMicroservice(self.instance, template=template)

@@ -128,6 +128,9 @@ class EventBus:
 
     # ------------------------------------------------------------------ topics
     def topic(self, name: str, partitions: int | None = None) -> int:
+        t = self._topics.get(name)            # hot path: no lock once the topic exists
+        if t is not None:
+            return t
         with self._lock:
             t = self._topics.get(name)
             if t is None:
@@ -561,12 +564,16 @@ class Consumer:
 
     def commit(self, offsets: dict[tuple[str, int], int] | None = None):
         """Commit positions (next offset to read); default: current positions of all partitions."""
-        items = (offsets or self.positions).items()
+        last = self.__dict__.setdefault("_last_commit", {})
+        items = [(tp, off) for tp, off in (offsets or self.positions).items() if last.get(tp) != off]
+        if not items:
+            return                               # nothing moved since the last commit
         if hasattr(self.bus, "commit_many"):
             self.bus.commit_many(self.group, [(tp[0], tp[1], off) for tp, off in items])
-            return
-        for tp, off in items:
-            self.bus.commit(self.group, tp[0], tp[1], off)
+        else:
+            for tp, off in items:
+                self.bus.commit(self.group, tp[0], tp[1], off)
+        last.update(items)
 
     commit_async = commit
 

@@ -70,7 +70,25 @@ class TokenManagement:
         sig = hmac.new(self.secret, f"{h}.{p}".encode(), hashlib.sha512).digest()
         return f"{h}.{p}.{_b64e(sig)}"
 
+    _CACHE_MAX = 4096
+
     def get_claims(self, token: str) -> dict:
+        """Verified claims of ``token``.  Signature checks are memoised per token (a bounded map
+        replaced wholesale when full; reads and writes are single dict operations, so concurrent
+        RPC threads cannot corrupt it -- unlike the reference's static HashMap, SURVEY §5.2);
+        expiry is checked on every call."""
+        cache = self.__dict__.setdefault("_verified", {})
+        claims = cache.get(token)
+        if claims is None:
+            claims = self._verify(token)
+            if len(cache) >= self._CACHE_MAX:
+                self._verified = cache = {}
+            cache[token] = claims
+        if claims.get("exp", 0) < time.time():
+            raise UnauthorizedException("JWT expired")
+        return dict(claims)
+
+    def _verify(self, token: str) -> dict:
         try:
             h, p, s = token.split(".")
         except ValueError as e:
@@ -81,10 +99,7 @@ class TokenManagement:
         want = hmac.new(self.secret, f"{h}.{p}".encode(), hashlib.sha512).digest()
         if not hmac.compare_digest(want, _b64d(s)):
             raise UnauthorizedException("Invalid JWT signature")
-        claims = json.loads(_b64d(p))
-        if claims.get("exp", 0) < time.time():
-            raise UnauthorizedException("JWT expired")
-        return claims
+        return json.loads(_b64d(p))
 
     def get_username(self, token: str) -> str:
         return self.get_claims(token)["sub"]

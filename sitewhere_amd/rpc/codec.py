@@ -8,6 +8,8 @@ classes per service; one generic codec replaces ~20k lines of converters.)
 from __future__ import annotations
 
 import base64
+import copy
+import dataclasses
 import enum
 import json
 
@@ -93,3 +95,25 @@ def dumps(obj) -> bytes:
 
 def loads(b: bytes):
     return from_wire(json.loads(b)) if b else None
+
+
+_ATOMIC_TYPES = {str, int, float, bool, bytes, type(None)}
+
+
+def clone(v):
+    """Isolation copy with the result of ``loads(dumps(v))`` but no text round trip: models, dicts,
+    lists and tuples are copied, scalars / enums / bytes shared.  Co-located services exchange RPC
+    arguments and results through this (``LocalChannel`` in ``clone`` mode)."""
+    t = type(v)
+    if t in _ATOMIC_TYPES or isinstance(v, enum.Enum):
+        return v
+    if t is dict:
+        return {k: clone(x) for k, x in v.items()}
+    if t is list or t is tuple:
+        return [clone(x) for x in v]
+    d = getattr(v, "__dict__", None)
+    if d is not None and dataclasses.is_dataclass(v):
+        o = object.__new__(t)
+        o.__dict__.update({k: clone(x) for k, x in d.items()})
+        return o
+    return copy.deepcopy(v)

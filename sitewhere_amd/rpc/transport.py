@@ -289,12 +289,20 @@ class GrpcChannel(ApiChannel):
 
 
 class LocalChannel(ApiChannel):
-    """In-process channel with the exact server-side semantics (auth, tenant, spans, codec)."""
+    """In-process channel with the server-side semantics (auth, tenant, spans) and isolated values.
+
+    ``mode="clone"`` (default) copies non-scalar arguments and results structurally
+    (:func:`codec.clone`, same result as a wire round trip, ~10x cheaper); ``mode="codec"`` sends
+    them through the JSON wire codec exactly as a network call would (``SITEWHERE_LOCAL_RPC=codec``
+    -- useful to shake out values that would not survive the wire)."""
 
     def __init__(self, resolver: ServiceResolver, tokens: TokenManagement, system_jwt: str | None = None,
-                 serialize: bool = True):
+                 serialize: bool = True, mode: str = "clone"):
         self.resolver, self.tokens, self.system_jwt = resolver, tokens, system_jwt
         self.serialize = serialize
+        if mode not in ("clone", "codec"):
+            raise ValueError(f"local rpc mode {mode!r}")
+        self.mode = mode
 
     def call(self, service, method, *args, tenant=None, timeout=30.0, **kwargs):
         jwt = _jwt_for_call(self.tokens, self.system_jwt)
@@ -304,9 +312,12 @@ class LocalChannel(ApiChannel):
         trace = span.context_header() if span else None
         if all(isinstance(x, _IMMUTABLE) for x in args) and all(isinstance(x, _IMMUTABLE) for x in kwargs.values()):
             out = invoke(self.resolver, self.tokens, service, m, None, jwt, t, trace, direct=(args, kwargs))
+        elif self.mode == "clone":
+            out = invoke(self.resolver, self.tokens, service, m, None, jwt, t, trace,
+                         direct=(codec.clone(list(args)), codec.clone(kwargs)))
         else:
             out = invoke(self.resolver, self.tokens, service, m, codec.dumps({"args": list(args), "kwargs": kwargs}),
                          jwt, t, trace)
         if not self.serialize or isinstance(out, _IMMUTABLE):
             return out
-        return codec.loads(codec.dumps(out))
+        return codec.clone(out) if self.mode == "clone" else codec.loads(codec.dumps(out))

@@ -89,6 +89,8 @@ class InstanceSettings:
     # reference sitewhere.tracer.server: "host[:port]" -> Jaeger agent (UDP compact emitBatch, 6831);
     # "http(s)://host:4318" -> OTLP/HTTP JSON; empty -> spans stay in the in-process ring only
     tracer_server: str = ""
+    # co-located RPC isolation: "clone" (structural copy) or "codec" (full JSON wire round trip)
+    local_rpc: str = "clone"
     filesystem_storage_root: str = "/tmp/sitewhere"
     tenant_ops_threads: int = 5
     extra: dict = field(default_factory=dict)
@@ -96,7 +98,7 @@ class InstanceSettings:
     @classmethod
     def from_env(cls, **over):
         s = cls(**over)
-        for f in ("product_id", "instance_id", "filesystem_storage_root", "tracer_server"):
+        for f in ("product_id", "instance_id", "filesystem_storage_root", "tracer_server", "local_rpc"):
             v = os.environ.get("SITEWHERE_" + f.upper())
             if v:
                 setattr(s, f, v)

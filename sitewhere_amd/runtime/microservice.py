@@ -111,7 +111,8 @@ class Instance:
         self.naming = TopicNaming(self.settings.product_id, self.settings.instance_id)
         self.resolver = ServiceResolver()
         self.system_user = SystemUser(self.tokens)
-        self.local_channel = LocalChannel(self.resolver, self.tokens, self.system_user.authentication().jwt)
+        self.local_channel = LocalChannel(self.resolver, self.tokens, self.system_user.authentication().jwt,
+                                          mode=self.settings.local_rpc)
         self.router = RoutingChannel(self)
         self.network_rpc = network_rpc
         self.microservices: dict[str, "Microservice"] = {}

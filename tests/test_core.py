@@ -413,3 +413,29 @@ def test_columnar_store_dense_and_small_batches():
     res = st.list_events(DeviceEventType.Measurement, DeviceEventIndex.Assignment, ["a0"],
                          DateRangeSearchCriteria(page_size=3))
     assert res.num_results == 255 and [m.event_date for m in res.results] == [9008, 9006, 9004]
+
+
+def test_codec_clone_matches_wire_round_trip():
+    """LocalChannel's clone mode returns what a wire round trip would, without sharing mutables."""
+    from sitewhere_amd.models import domain
+    from sitewhere_amd.rpc import codec
+    n = 0
+    for cls in codec._REGISTRY.values():
+        try:
+            obj = cls()
+        except TypeError:
+            continue
+        if hasattr(obj, "metadata"):
+            obj.metadata = {"k": "v", "n": "1"}
+        c = codec.clone(obj)
+        assert type(c) is cls and c == codec.loads(codec.dumps(obj)) and c is not obj
+        if hasattr(obj, "metadata"):
+            c.metadata["k"] = "changed"
+            assert obj.metadata["k"] == "v"
+        n += 1
+    assert n > 40
+    m = domain.DeviceMeasurement(name="t", value=1.5, metadata={"a": "b"})
+    payload = {"args": [[{"name": "x", "value": 2.0}], m, (1, 2), b"\x00\x01"], "kwargs": {"res": domain.SearchResults(1, [m])}}
+    c = codec.clone(payload)
+    assert c == codec.loads(codec.dumps(payload))
+    assert c["args"][1] is not m and c["kwargs"]["res"].results[0] is not m
