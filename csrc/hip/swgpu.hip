@@ -38,6 +38,24 @@
 
 typedef unsigned long long ull;
 
+// Workgroup id as the kernels see it.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (each with its own L2); with SW_XCD_REMAP the ids are permuted (bijectively, any grid size) so the
+// workgroups that share an XCD own one contiguous range of tiles / grid-stride slots.  Every kernel
+// uses BID for all its block-id arithmetic, so either numbering is correct; it is a speed choice,
+// measured in profiles/r1_xcd.
+#ifndef SW_XCD_REMAP
+#define SW_XCD_REMAP 0
+#endif
+__device__ __forceinline__ uint32_t sw_block_id() {
+#if SW_XCD_REMAP
+  const uint32_t nwg = gridDim.x, orig = blockIdx.x, x = orig % 8u, q = nwg / 8u, r = nwg % 8u;
+  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + orig / 8u;
+#else
+  return blockIdx.x;
+#endif
+}
+#define BID sw_block_id()
+
 static inline int grid_for(int64_t n) {
   int64_t g = (n + BLK - 1) / BLK;
   if (g < 1) g = 1;
@@ -75,7 +93,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
 // Exclusive scan of u32[n] -> out, total -> *total.  n <= TILE * (BLK * 64).
 __global__ void k_scan_tiles(const uint32_t* __restrict__ in, int64_t n, uint32_t* __restrict__ tsum) {
   __shared__ uint32_t lds[WAVES + 1];
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
@@ -84,7 +102,7 @@ __global__ void k_scan_tiles(const uint32_t* __restrict__ in, int64_t n, uint32_
   }
   uint32_t tot;
   block_excl_scan(s, &tot, lds);
-  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+  if (threadIdx.x == 0) tsum[BID] = tot;
 }
 
 __global__ void k_scan_sums(uint32_t* __restrict__ tsum, int64_t nt, uint32_t* __restrict__ total) {
@@ -104,8 +122,8 @@ __global__ void k_scan_sums(uint32_t* __restrict__ tsum, int64_t nt, uint32_t* _
 __global__ void k_scan_apply(const uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ tsum,
                              uint32_t* __restrict__ out) {
   __shared__ uint32_t lds[WAVES + 1];
-  const int64_t base = (int64_t)blockIdx.x * TILE;
-  uint32_t run = tsum[blockIdx.x];
+  const int64_t base = (int64_t)BID * TILE;
+  uint32_t run = tsum[BID];
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
     int64_t i = base + (int64_t)k * BLK + threadIdx.x;
@@ -145,7 +163,7 @@ __device__ __forceinline__ uint32_t vlen_value(const uint8_t* __restrict__ L, in
 __global__ void k_vlen_tiles(const uint8_t* __restrict__ L, int64_t nbytes, uint32_t* __restrict__ tcnt,
                              uint32_t* __restrict__ tlen) {
   __shared__ uint32_t lds[WAVES + 1];
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   uint32_t c = 0, v = 0;
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
@@ -155,15 +173,15 @@ __global__ void k_vlen_tiles(const uint8_t* __restrict__ L, int64_t nbytes, uint
   uint32_t tc, tv;
   block_excl_scan(c, &tc, lds);
   block_excl_scan(v, &tv, lds);
-  if (threadIdx.x == 0) { tcnt[blockIdx.x] = tc; tlen[blockIdx.x] = tv; }
+  if (threadIdx.x == 0) { tcnt[BID] = tc; tlen[BID] = tv; }
 }
 
 __global__ void k_vlen_apply(const uint8_t* __restrict__ L, int64_t nbytes, const uint32_t* __restrict__ tcnt,
                              const uint32_t* __restrict__ tlen, uint32_t* __restrict__ msg_off, int64_t n_msgs,
                              uint32_t raw_bytes) {
   __shared__ uint32_t lds[WAVES + 1];
-  const int64_t base = (int64_t)blockIdx.x * TILE;
-  uint32_t run_c = tcnt[blockIdx.x], run_v = tlen[blockIdx.x];
+  const int64_t base = (int64_t)BID * TILE;
+  uint32_t run_c = tcnt[BID], run_v = tlen[BID];
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
@@ -182,7 +200,7 @@ __global__ void k_vlen_apply(const uint8_t* __restrict__ L, int64_t nbytes, cons
 }
 
 __global__ void k_vlen_total(uint32_t* __restrict__ msg_off, int64_t n_msgs, uint32_t raw_bytes) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     if (msg_off[n_msgs] > raw_bytes) msg_off[n_msgs] = raw_bytes;
   }
 }
@@ -194,7 +212,7 @@ __global__ void k_vlen_total(uint32_t* __restrict__ msg_off, int64_t n_msgs, uin
 // Oversized windows (mean payload > 128 B) parse straight from global memory.
 __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
                                              int64_t n_msgs, uint8_t* lds, uint32_t* base_abs) {
-  const int64_t m0 = (int64_t)blockIdx.x * BLK;
+  const int64_t m0 = (int64_t)BID * BLK;
   int64_t m1 = m0 + BLK;
   if (m1 > n_msgs) m1 = n_msgs;
   const uint32_t s = off[m0], e = off[m1];
@@ -215,7 +233,7 @@ __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict_
   __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
   uint32_t base = 0;
   const bool staged = stage_window(raw, off, n_msgs, lds, &base);
-  const int64_t m = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const int64_t m = (int64_t)BID * BLK + threadIdx.x;
   if (m >= n_msgs) return;
   if (staged) cnt[m] = sw_decode_payload(lds, off[m] - base, off[m + 1] - base, base, 0, 0, nullptr, 0);
   else cnt[m] = sw_decode_payload(raw, off[m], off[m + 1], 0, 0, 0, nullptr, 0);
@@ -254,7 +272,7 @@ __global__ __launch_bounds__(BLK) void k_decode_emit(SwEngineArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
   uint32_t base = 0;
   const bool staged = stage_window(a.raw, a.msg_off, a.n_msgs, lds, &base);
-  const int64_t m = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const int64_t m = (int64_t)BID * BLK + threadIdx.x;
   if (m >= a.n_msgs) return;
   const int64_t o = a.msg_evoff[m];
   if (o >= a.rec_cap) return;
@@ -272,7 +290,7 @@ __global__ __launch_bounds__(BLK) void k_decode_emit(SwEngineArgs a) {
 
 // End of the decode phase: clamp the record count, account the names first seen in this batch.
 __global__ void k_decode_end(SwEngineArgs a) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     if (*a.n_recs > a.rec_cap) *a.n_recs = (uint32_t)a.rec_cap;
     ((ull*)a.stats)[SW_STAT_NEW_NAMES] += *a.n_new_names;
   }
@@ -300,7 +318,7 @@ __global__ void k_part_count(const SwEventRec* __restrict__ carry, const uint32_
   __syncthreads();
   const uint32_t nc = *nc_ptr;
   const int64_t n = (int64_t)nc + *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   for (int k = 0; k < TILE_ITEMS; ++k) {
     int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     if (i < n) {
@@ -310,7 +328,7 @@ __global__ void k_part_count(const SwEventRec* __restrict__ carry, const uint32_
     }
   }
   __syncthreads();
-  if (threadIdx.x < world) tcount[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < world) tcount[(int64_t)threadIdx.x * ntiles + BID] = cnt[threadIdx.x];
 }
 
 // Records per destination from the scanned [world][ntiles] matrix.
@@ -330,10 +348,10 @@ __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_
   __shared__ uint32_t wcnt[WAVES][64];
   const uint32_t nc = *nc_ptr;
   const int64_t n = (int64_t)nc + *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   const uint32_t wid = threadIdx.x >> 6;
   if (threadIdx.x < world) {
-    run[threadIdx.x] = toff[(int64_t)threadIdx.x * ntiles + blockIdx.x] - toff[(int64_t)threadIdx.x * ntiles];
+    run[threadIdx.x] = toff[(int64_t)threadIdx.x * ntiles + BID] - toff[(int64_t)threadIdx.x * ntiles];
   }
   if (threadIdx.x == 0) {
     // records beyond a destination's slab go to the spill list, destination-major (deterministic)
@@ -381,7 +399,7 @@ __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_
 __global__ void k_part_counts(const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tcount, int64_t ntiles,
                               int world, int64_t shuf_cap, uint32_t* __restrict__ send_cnt, uint32_t* __restrict__ n_spill,
                               int64_t carry_cap, uint32_t* __restrict__ dropped, ull* __restrict__ stats) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     uint64_t over = 0;
     for (int o = 0; o < world; ++o) {
       const uint32_t tot = part_total(toff, tcount, ntiles, o);
@@ -406,8 +424,8 @@ __global__ void k_unpack(const SwWireRec* __restrict__ recv, const uint32_t* __r
   }
   __syncthreads();
   const uint32_t total = pre[world] < cap ? pre[world] : (uint32_t)cap;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_work = total;
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLK) {
+  if (BID == 0 && threadIdx.x == 0) *n_work = total;
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLK) {
     int q = 0;
     while (q + 1 < world && i >= pre[q + 1]) ++q;
     work[i] = sw_wire_unpack(recv[(int64_t)q * shuf_cap + (i - pre[q])], (uint8_t)q);
@@ -433,7 +451,7 @@ __device__ __forceinline__ void intern_insert(ull* __restrict__ key, int64_t mas
 __global__ void k_lookup(SwEngineArgs a) {
   const uint32_t n = *a.n_work;
   const SwEventRec* __restrict__ recs = a.work;
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull lo = recs[i].fp_lo, hi = recs[i].fp_hi;
     const uint8_t et = recs[i].etype;
     const ull nh = recs[i].name_hash;
@@ -470,7 +488,7 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
                                int64_t mask, const int64_t* __restrict__ seq_base) {
   const uint32_t n = *n_ptr;
   const ull sb = (ull)*seq_base;
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
     int64_t slot = (int64_t)(h & (ull)mask);
@@ -487,7 +505,7 @@ __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_
                               int64_t mask, const int64_t* __restrict__ seq_base) {
   const uint32_t n = *n_ptr;
   const ull sb = (ull)*seq_base;
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
     int64_t slot = (int64_t)(h & (ull)mask);
@@ -508,7 +526,7 @@ __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* 
   if (threadIdx.x < 2) c[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   uint32_t ok = 0, all = 0;
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
@@ -519,7 +537,7 @@ __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* 
   }
   if (lane_id() == 0) { atomicAdd(&c[0], ok); atomicAdd(&c[1], all - ok); }
   __syncthreads();
-  if (threadIdx.x == 0) { tcnt[blockIdx.x] = c[0]; tcnt[ntiles + blockIdx.x] = c[1]; }
+  if (threadIdx.x == 0) { tcnt[BID] = c[0]; tcnt[ntiles + BID] = c[1]; }
 }
 
 __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
@@ -528,10 +546,10 @@ __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* 
                             uint32_t* __restrict__ n_ok, uint32_t* __restrict__ n_rej) {
   __shared__ uint32_t lds[WAVES + 1];
   const uint32_t n = *n_ptr;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   const uint32_t rej_base = toff[ntiles];  // rejected region starts after all ok counts in the flat scan
-  uint32_t run_ok = toff[blockIdx.x];
-  uint32_t run_rj = toff[ntiles + blockIdx.x] - rej_base;
+  uint32_t run_ok = toff[BID];
+  uint32_t run_rj = toff[ntiles + BID] - rej_base;
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool valid = i < n;
@@ -545,7 +563,7 @@ __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* 
     run_ok += tot_ok;
     run_rj += tot_rj;
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+  if (BID == gridDim.x - 1 && threadIdx.x == 0) {
     const int64_t last = ntiles - 1;
     *n_ok = toff[last] + tcnt[last];
     *n_rej = toff[ntiles + last] + tcnt[ntiles + last] - rej_base;
@@ -568,14 +586,14 @@ __device__ __forceinline__ int64_t nm_probe(const K* __restrict__ key, int64_t m
 __global__ void k_intern_insert_list(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                                      ull* __restrict__ key, int64_t mask) {
   const uint32_t n = *n_ptr;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
     if (recs[j].name_hash) intern_insert(key, mask, recs[j].name_hash);
 }
 
 // Give every newly inserted name slot a dense id (ids are rank-local state-map keys).
 __global__ void k_intern_assign(const ull* __restrict__ key, int32_t* __restrict__ ids, int64_t slots,
                                 int32_t* __restrict__ counter) {
-  for (int64_t s = (int64_t)blockIdx.x * BLK + threadIdx.x; s < slots; s += (int64_t)gridDim.x * BLK)
+  for (int64_t s = (int64_t)BID * BLK + threadIdx.x; s < slots; s += (int64_t)gridDim.x * BLK)
     if (key[s] != 0 && ids[s] < 0) ids[s] = atomicAdd(counter, 1);
 }
 
@@ -586,7 +604,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
   const uint32_t n = *n_ptr;
   const int64_t cur = *a.store_cursor;
   const int64_t c0 = *a.step_cursor0;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const uint32_t i = idx ? idx[j] : (uint32_t)j;
     const SwEventRec r = R[i];
     const int32_t dev = devs[i], asg = asgs[i];
@@ -652,7 +670,7 @@ __device__ __forceinline__ ull state_key(const SwEngineArgs& a, const SwEventRec
 __global__ void k_state_p1(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                            const int32_t* __restrict__ asgs, const uint32_t* __restrict__ n_ptr) {
   const uint32_t n = *n_ptr;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const uint32_t i = idx ? idx[j] : (uint32_t)j;
     const SwEventRec r = R[i];
     const int32_t asg = asgs[i];
@@ -678,7 +696,7 @@ __global__ void k_state_p2(SwEngineArgs a, const SwEventRec* __restrict__ R, con
                            const int32_t* __restrict__ asgs, const uint32_t* __restrict__ n_ptr) {
   const uint32_t n = *n_ptr;
   const int64_t cur = *a.store_cursor;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const uint32_t i = idx ? idx[j] : (uint32_t)j;
     const SwEventRec r = R[i];
     const int32_t asg = asgs[i];
@@ -697,7 +715,7 @@ __global__ void k_state_p2(SwEngineArgs a, const SwEventRec* __restrict__ R, con
 }
 
 __global__ void k_advance(int64_t* __restrict__ cursor, const uint32_t* __restrict__ n_ptr) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *cursor += *n_ptr;
+  if (threadIdx.x == 0 && BID == 0) *cursor += *n_ptr;
 }
 
 // ============================================================================ zone-test rules
@@ -783,9 +801,9 @@ __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restri
   for (int t = 0; t < nt; ++t) outside_mask |= (L.t[t].y != 0) ? (1ull << t) : 0ull;
   const int64_t c0 = *a.step_cursor0;
   const uint32_t n = (uint32_t)(*a.store_cursor - c0);
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t base = (int64_t)BID * TILE;
   if (base >= n) {                       // tile past this step's rows
-    if (threadIdx.x == 0) ztile[blockIdx.x] = 0;
+    if (threadIdx.x == 0) ztile[BID] = 0;
     return;
   }
   // 1. compact location rows (stable) into LDS
@@ -851,7 +869,7 @@ __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restri
     if (j < n && !isloc[k]) zmask[j] = 0ull;
   }
   for (uint32_t i = threadIdx.x; i < nloc; i += BLK) zmask[base + M.loc_j[i]] = M.inside[i];
-  if (threadIdx.x == 0) ztile[blockIdx.x] = M.count;
+  if (threadIdx.x == 0) ztile[BID] = M.count;
 }
 
 // Pass 2: write the alerts at their scanned offsets (stable, no global atomics).
@@ -867,8 +885,8 @@ __global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __
   __syncthreads();
   const int64_t c0 = *a.step_cursor0;
   const uint32_t n = (uint32_t)(*a.store_cursor - c0);
-  const int64_t base = (int64_t)blockIdx.x * TILE;
-  uint32_t run = zoff[blockIdx.x];
+  const int64_t base = (int64_t)BID * TILE;
+  uint32_t run = zoff[BID];
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
     ull fired = j < n ? zmask[j] : 0ull;
@@ -905,7 +923,7 @@ __global__ void k_presence(SwEngineArgs a) {
   const SwStepParams P = *a.sp;
   if (P.presence_missing_ms <= 0) return;
   const ull limit = (ull)(P.now_ms - P.presence_missing_ms);
-  for (int64_t s = (int64_t)blockIdx.x * BLK + threadIdx.x; s < a.n_asg; s += (int64_t)gridDim.x * BLK) {
+  for (int64_t s = (int64_t)BID * BLK + threadIdx.x; s < a.n_asg; s += (int64_t)gridDim.x * BLK) {
     SwAsgState* st = &a.st[s];
     const ull last = st->last;
     const bool miss = last != 0 && last < limit && st->missing == 0 && a.asg_active[s];
@@ -929,7 +947,7 @@ __global__ void k_presence(SwEngineArgs a) {
 // Decode-side and process-side resets are separate kernels: with the pipelined exchange the
 // decode of batch k runs before the process phase of batch k-1 on the same stream.
 __global__ void k_decode_begin(SwEngineArgs a) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     *a.n_new_names = 0;
     *a.overflow = 0;
     ((ull*)a.stats)[SW_STAT_MSGS] += (ull)a.n_msgs;   // by-value batch size
@@ -937,7 +955,7 @@ __global__ void k_decode_begin(SwEngineArgs a) {
 }
 
 __global__ void k_process_begin(SwEngineArgs a) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     *a.step_cursor0 = *a.store_cursor;
     *a.n_gen = 0;
     *a.n_out = 0;
@@ -945,14 +963,14 @@ __global__ void k_process_begin(SwEngineArgs a) {
 }
 
 __global__ void k_gen_clamp(SwEngineArgs a, uint32_t* gen_rules) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     if (*a.n_gen > a.gen_cap) *a.n_gen = (uint32_t)a.gen_cap;
     if (gen_rules) *gen_rules = *a.n_gen;
   }
 }
 
 __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     *a.n_out = (uint32_t)(*a.store_cursor - *a.step_cursor0);
     *a.seq_base += *a.n_work;
     ull* st = (ull*)a.stats;
@@ -968,7 +986,7 @@ __global__ void k_reject_stats(SwEngineArgs a) {
   if (threadIdx.x < 8) c[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *a.n_rej;
-  for (int64_t j = (int64_t)blockIdx.x * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
     atomicAdd(&c[a.status[a.rej_idx[j]] & 7], 1u);
   __syncthreads();
   if (threadIdx.x < 8 && c[threadIdx.x]) {
@@ -997,7 +1015,7 @@ __global__ __launch_bounds__(BLK) void k_store_filter(const uint8_t* __restrict_
   const int64_t stride = (int64_t)gridDim.x * BLK;
   // every lane of a wave iterates the same number of times (ballot needs the whole wave)
   const int64_t iters = (n_rows + stride - 1) / stride;
-  int64_t r = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  int64_t r = (int64_t)BID * BLK + threadIdx.x;
   for (int64_t it = 0; it < iters; ++it, r += stride) {
     bool hit = false;
     if (r < n_rows && etype[r] == (uint8_t)et) {
@@ -1138,7 +1156,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
 
 __global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int64_t presence_ms,
                                   SwOutRec* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (threadIdx.x == 0 && BID == 0) {
     sp->now_ms = now_ms; sp->batch_seq = batch_seq; sp->presence_missing_ms = presence_ms; sp->out = out;
   }
 }
@@ -1161,11 +1179,11 @@ int sw_graph_capture_process(const SwEngineArgs* ap, uint32_t* scratch4, int32_t
   if (with_unpack) rc = sw_phase_unpack(ap, s);
   if (!rc) rc = sw_phase_process(ap, scratch4, s);
   e = hipStreamEndCapture(s, &g);
-  if (rc) { if (g) hipGraphDestroy(g); return rc; }
+  if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
   if (e != hipSuccess) return 6000 + (int)e;
   hipGraphExec_t x = nullptr;
   e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
-  hipGraphDestroy(g);
+  (void)hipGraphDestroy(g);
   if (e != hipSuccess) return 7000 + (int)e;
   *exec_out = (void*)x;
   return 0;
@@ -1177,7 +1195,7 @@ int sw_graph_destroy(void* exec) { return exec ? (int)hipGraphExecDestroy((hipGr
 
 // Registry patch: scatter host-built packed slots (bulk load and incremental upserts).
 __global__ void k_reg_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* vals, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) reg[slots[i]] = vals[i];
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) reg[slots[i]] = vals[i];
 }
 
 int sw_registry_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* vals, int64_t n, hipStream_t s) {
@@ -1189,7 +1207,7 @@ int sw_registry_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* val
 // Standalone batched point-in-polygon (used by the rule service for ad-hoc zone queries).
 __global__ void k_pip_batch(const double* pts, int64_t n_pts, const double* vtx, const int32_t* off, int64_t n_zones,
                             uint8_t* out) {
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n_pts * n_zones; i += (int64_t)gridDim.x * BLK) {
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n_pts * n_zones; i += (int64_t)gridDim.x * BLK) {
     const int64_t p = i / n_zones, z = i % n_zones;
     out[i] = pip(vtx + 2 * off[z], off[z + 1] - off[z], pts[2 * p], pts[2 * p + 1]) ? 1 : 0;
   }
@@ -1226,7 +1244,7 @@ int sw_scan_u32(const uint32_t* in, int64_t n, uint32_t* out, uint32_t* total, u
 __global__ void k_push_out(const uint4* __restrict__ src, uint4* __restrict__ dst, const uint32_t* __restrict__ n_ptr,
                            int64_t cap) {
   const int64_t n = (int64_t)(*n_ptr < cap ? *n_ptr : cap) * (int64_t)(sizeof(SwOutRec) / 16);
-  for (int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) dst[i] = src[i];
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) dst[i] = src[i];
 }
 
 int sw_push_out(const void* src, void* dst_dev, const uint32_t* n_ptr, int64_t cap, int32_t blocks, hipStream_t s) {

@@ -201,8 +201,9 @@ def gpu():
     with _lock:
         if _gpu is not None:
             return _gpu
-        path = LIB_DIR / "libswgpu.so"
-        if _stale(path, _GPU_SRC):
+        override = os.environ.get("SW_GPU_LIB")       # an experiment build (e.g. scripts/build_xcd_variant.sh)
+        path = Path(override) if override else LIB_DIR / "libswgpu.so"
+        if not override and _stale(path, _GPU_SRC):
             build_gpu()
         lib = ctypes.CDLL(str(path))
         P = c_void_p
