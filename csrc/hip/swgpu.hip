@@ -750,17 +750,25 @@ __device__ __forceinline__ bool pip_div(const double* __restrict__ v, int n, dou
 }
 
 struct ZoneLds {
-  double v[2 * ZONE_LDS_VTX];
   double bb[4 * ZONE_LDS_TESTS];
   int4 t[ZONE_LDS_TESTS];
   int2 zo[ZONE_LDS_TESTS];
 };
+// The vertex table lives in dynamic LDS sized to the zones actually configured (16 B per vertex;
+// none when it exceeds ZONE_LDS_VTX and the PIP reads global memory): a static 32 KiB table held
+// k_zone_mask to 2 workgroups per CU.
+extern __shared__ double zone_vtx_lds[];
 
-__device__ __forceinline__ int zone_lds_load(const SwEngineArgs& a, ZoneLds& L, bool* vtx_lds) {
+__host__ __device__ __forceinline__ bool zone_vtx_in_lds(const SwEngineArgs& a) {
+  return a.n_zone_vtx <= ZONE_LDS_VTX;
+}
+
+__device__ __forceinline__ int zone_lds_load(const SwEngineArgs& a, ZoneLds& L, const double** V) {
   const int nt = a.n_tests < ZONE_LDS_TESTS ? (int)a.n_tests : ZONE_LDS_TESTS;
-  const int64_t nv = a.n_zones ? a.zone_off[a.n_zones] : 0;
-  *vtx_lds = nv <= ZONE_LDS_VTX;
-  for (int64_t t = threadIdx.x; *vtx_lds && t < 2 * nv; t += BLK) L.v[t] = a.zone_vtx[t];
+  const int64_t nv = a.n_zone_vtx;
+  const bool in_lds = zone_vtx_in_lds(a);
+  for (int64_t t = threadIdx.x; in_lds && t < 2 * nv; t += BLK) zone_vtx_lds[t] = a.zone_vtx[t];
+  *V = in_lds ? zone_vtx_lds : a.zone_vtx;
   for (int t = threadIdx.x; t < nt; t += BLK) {
     const SwZoneTest zt = a.tests[t];
     L.t[t] = make_int4(zt.zone, zt.condition, zt.alert_name_id, zt.level);
@@ -794,9 +802,8 @@ struct ZoneMaskLds {
 __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restrict__ zmask, uint32_t* __restrict__ ztile) {
   __shared__ ZoneLds L;
   __shared__ ZoneMaskLds M;
-  bool vtx_lds;
-  const int nt = zone_lds_load(a, L, &vtx_lds);
-  const double* V = vtx_lds ? L.v : a.zone_vtx;
+  const double* V;
+  const int nt = zone_lds_load(a, L, &V);
   ull outside_mask = 0;
   for (int t = 0; t < nt; ++t) outside_mask |= (L.t[t].y != 0) ? (1ull << t) : 0ull;
   const int64_t c0 = *a.step_cursor0;
@@ -1135,7 +1142,8 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
     const int64_t otiles = (a.rec_cap + TILE - 1) / TILE;
     ull* zmask = (ull*)a.zmask;
     uint32_t* ztile = a.ztile;
-    k_zone_mask<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile);
+    const size_t vtx_bytes = zone_vtx_in_lds(a) ? (size_t)a.n_zone_vtx * 2 * sizeof(double) : 0;
+    k_zone_mask<<<(unsigned)otiles, BLK, vtx_bytes, s>>>(a, zmask, ztile);
     rc = launch_scan(ztile, otiles, ztile + otiles, a.n_gen, a.scan_tmp, a.scan_tmp_len, s);
     if (rc) return rc;
     k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile + otiles);

@@ -179,6 +179,8 @@ typedef struct SwEngineArgs {
   SwEventRec* spill;
   uint32_t* n_spill;
   int64_t carry_cap;
+  // ---------------------------------------------------------------- rules, host-side sizes
+  int64_t n_zone_vtx;          // zone_off[n_zones]: sizes k_zone_mask's dynamic LDS vertex table
 } SwEngineArgs;
 
 enum {

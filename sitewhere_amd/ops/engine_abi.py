@@ -52,6 +52,8 @@ FIELDS = [
     ("sp", P),
     # shuffle spill (records deferred to the next step's exchange)
     ("carry", P), ("n_carry", P), ("spill", P), ("n_spill", P), ("carry_cap", I),
+    # rules, host-side sizes
+    ("n_zone_vtx", I),
 ]
 
 

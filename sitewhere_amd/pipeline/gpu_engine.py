@@ -252,11 +252,13 @@ class GpuInboundEngine(EngineBase):
         self.t["tests"] = torch.from_numpy(tests.view(np.uint8).copy() if len(tests) else np.zeros(16, np.uint8)).to(d)
         self.t["test_hash"] = torch.from_numpy(hashes.view(np.int64).copy() if len(hashes) else np.zeros(1, np.int64)).to(d)
         self._n_zones, self._n_tests = len(off) - 1, len(tests)
+        self._n_zone_vtx = int(off[-1]) if len(off) else 0
 
     def _apply_zone_ptrs(self):
         a = self.args
         a.zone_vtx, a.zone_off, a.zone_bbox = _ptr(self.t["zone_vtx"]), _ptr(self.t["zone_off"]), _ptr(self.t["zone_bbox"])
         a.n_zones, a.tests, a.n_tests = self._n_zones, _ptr(self.t["tests"]), self._n_tests
+        a.n_zone_vtx = self._n_zone_vtx
         a.test_name_hash = _ptr(self.t["test_hash"])
 
     def _zones_changed(self):
