@@ -597,13 +597,34 @@ __global__ void k_intern_assign(const ull* __restrict__ key, int32_t* __restrict
     if (key[s] != 0 && ids[s] < 0) ids[s] = atomicAdd(counter, 1);
 }
 
-// ============================================================================ persist + enrich
+// ============================================================================ device state map
+__device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t mask, ull k) {
+  int64_t slot = (int64_t)(sw_mix64(k) & (ull)mask);
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    ull* kp = (ull*)&ms[slot].key;
+    ull old = *kp;
+    if (old == k) return slot;
+    if (old == 0) {
+      old = atomicCAS(kp, 0ull, k);
+      if (old == 0 || old == k) return slot;
+    }
+    slot = (slot + 1) & mask;
+  }
+  return -1;
+}
+
+// ============================================================================ persist + enrich + state pass 1
+// One pass over the validated events: write the HBM ring row and the outbound row, and run pass 1
+// of the device-state merge (max event date per assignment location / per (assignment, name)
+// slot).  The (assignment, name) slot found or claimed here is kept in ev_slot[j] for pass 2, so
+// the name probe and the state-map probe run once per event instead of once per pass.
 __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                           const int32_t* __restrict__ devs, const int32_t* __restrict__ asgs,
                           const uint32_t* __restrict__ n_ptr) {
   const uint32_t n = *n_ptr;
   const int64_t cur = *a.store_cursor;
   const int64_t c0 = *a.step_cursor0;
+  const int64_t now = a.sp->now_ms;
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const uint32_t i = idx ? idx[j] : (uint32_t)j;
     const SwEventRec r = R[i];
@@ -613,7 +634,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     a.s_etype[row] = r.etype;
     a.s_level[row] = r.level;
     a.s_date[row] = r.event_date;
-    a.s_recv[row] = a.sp->now_ms;
+    a.s_recv[row] = now;
     a.s_dev[row] = dev;
     a.s_asg[row] = asg;
     const int4 ctx = *reinterpret_cast<const int4*>(&a.asg_ctx[asg]);
@@ -638,78 +659,55 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     o.etype = r.etype;
     o.level = r.level;
     a.sp->out[seq - c0] = o;
+    // ---- state pass 1
+    int64_t slot = -1;
+    if (r.etype == SW_EV_MEASUREMENT || r.etype == SW_EV_LOCATION || r.etype == SW_EV_ALERT) {
+      // Read the 32 B state once; issue an atomic only where it can change something.  Every
+      // writer of `last` in this kernel stores the same step time, so a checked plain store gives
+      // max(last, now) without an atomic per event.
+      SwAsgState* st = &a.st[asg];
+      const ulonglong2 lm = *reinterpret_cast<const ulonglong2*>(&st->last);   // last, missing
+      if (lm.x < (ull)now) st->last = (ull)now;
+      if (lm.y) st->missing = 0;  // presence detected again
+      const ull d = (ull)r.event_date;
+      if (r.etype == SW_EV_LOCATION) {
+        if (d > st->loc_date) atomicMax((ull*)&st->loc_date, d);
+      } else if (nid >= 0) {
+        // +1 keeps key 0 reserved as empty
+        const ull k = ((((ull)(uint32_t)asg) << 32) | ((ull)(uint32_t)nid << 1) | (r.etype == SW_EV_ALERT ? 1ull : 0ull)) + 1ull;
+        slot = ms_slot(a.ms, a.ms_mask, k);
+        if (slot >= 0) {
+          if (d > a.ms[slot].date) atomicMax((ull*)&a.ms[slot].date, d);
+        } else {
+          atomicAdd((ull*)&a.stats[SW_STAT_STATE_OVERFLOW], 1ull);
+        }
+      }
+    }
+    // pass-2 work item, coalesced: (ms slot | -2 - assignment for a location | -1, event date)
+    if (r.etype == SW_EV_LOCATION) slot = -2 - (int64_t)asg;
+    reinterpret_cast<longlong2*>(a.ev_slot)[j] = make_longlong2(slot, (int64_t)r.event_date);
   }
 }
 
 // ============================================================================ device state
-__device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t mask, ull k) {
-  int64_t slot = (int64_t)(sw_mix64(k) & (ull)mask);
-  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-    ull* kp = (ull*)&ms[slot].key;
-    ull old = *kp;
-    if (old == k) return slot;
-    if (old == 0) {
-      old = atomicCAS(kp, 0ull, k);
-      if (old == 0 || old == k) return slot;
-    }
-    slot = (slot + 1) & mask;
-  }
-  return -1;
-}
-
-__device__ __forceinline__ ull state_key(const SwEngineArgs& a, const SwEventRec& r, int32_t asg) {
-  const int64_t ns = nm_probe(a.nm_key, a.nm_mask, r.name_hash);
-  if (ns < 0) return 0;
-  const int32_t id = a.nm_id[ns];
-  if (id < 0) return 0;
-  // +1 keeps key 0 reserved as empty
-  return (((ull)(uint32_t)asg) << 32 | ((ull)(uint32_t)id << 1) | (r.etype == SW_EV_ALERT ? 1ull : 0ull)) + 1ull;
-}
-
-// Pass 1: max event date per assignment location and per (assignment, name) measurement/alert.
-__global__ void k_state_p1(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
-                           const int32_t* __restrict__ asgs, const uint32_t* __restrict__ n_ptr) {
-  const uint32_t n = *n_ptr;
-  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
-    const uint32_t i = idx ? idx[j] : (uint32_t)j;
-    const SwEventRec r = R[i];
-    const int32_t asg = asgs[i];
-    if (r.etype != SW_EV_MEASUREMENT && r.etype != SW_EV_LOCATION && r.etype != SW_EV_ALERT) continue;
-    SwAsgState* st = &a.st[asg];
-    atomicMax((ull*)&st->last, (ull)a.sp->now_ms);
-    if (st->missing) st->missing = 0;  // presence detected again
-    const ull d = (ull)r.event_date;
-    if (r.etype == SW_EV_LOCATION) {
-      atomicMax((ull*)&st->loc_date, d);
-    } else if (r.name_hash) {
-      const ull k = state_key(a, r, asg);
-      if (!k) continue;
-      const int64_t s = ms_slot(a.ms, a.ms_mask, k);
-      if (s >= 0) atomicMax((ull*)&a.ms[s].date, d);
-      else atomicAdd((ull*)&a.stats[SW_STAT_STATE_OVERFLOW], 1ull);
-    }
-  }
-}
-
 // Pass 2: among events carrying the max date, the highest event id wins (ids are monotonic).
-__global__ void k_state_p2(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
-                           const int32_t* __restrict__ asgs, const uint32_t* __restrict__ n_ptr) {
+// Reads only k_persist's coalesced (slot, date) work items -- no event records, no probes.
+__global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr) {
   const uint32_t n = *n_ptr;
   const int64_t cur = *a.store_cursor;
+  const longlong2* __restrict__ work = reinterpret_cast<const longlong2*>(a.ev_slot);
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
-    const uint32_t i = idx ? idx[j] : (uint32_t)j;
-    const SwEventRec r = R[i];
-    const int32_t asg = asgs[i];
+    const longlong2 w = work[j];
+    if (w.x == -1) continue;
     const ull eid1 = (ull)((cur + j) * a.world + a.rank) + 1ull;  // stored +1, 0 = none
-    const ull d = (ull)r.event_date;
-    if (r.etype == SW_EV_LOCATION) {
-      SwAsgState* st = &a.st[asg];
-      if (st->loc_date == d) atomicMax((ull*)&st->loc_eid1, eid1);
-    } else if ((r.etype == SW_EV_MEASUREMENT || r.etype == SW_EV_ALERT) && r.name_hash) {
-      const ull k = state_key(a, r, asg);
-      if (!k) continue;
-      const int64_t s = ms_slot(a.ms, a.ms_mask, k);
-      if (s >= 0 && a.ms[s].date == d) atomicMax((ull*)&a.ms[s].eid1, eid1);
+    const ull d = (ull)w.y;
+    if (w.x <= -2) {                         // location: assignment -2 - w.x
+      SwAsgState* st = &a.st[-2 - w.x];
+      const ulonglong2 le = *reinterpret_cast<const ulonglong2*>(&st->loc_date);   // loc_date, loc_eid1
+      if (le.x == d && le.y < eid1) atomicMax((ull*)&st->loc_eid1, eid1);
+    } else {
+      const ulonglong2 de = *reinterpret_cast<const ulonglong2*>(&a.ms[w.x].date);  // date, eid1
+      if (de.x == d && de.y < eid1) atomicMax((ull*)&a.ms[w.x].eid1, eid1);
     }
   }
 }
@@ -1133,8 +1131,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_intern_assign<<<grid_for(a.nm_mask + 1), BLK, 0, s>>>((const ull*)a.nm_key, a.nm_id, a.nm_mask + 1, a.nm_counter);
   // persist + enrich + state for the validated events
   k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok);
-  k_state_p1<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_asg, a.n_ok);
-  k_state_p2<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_asg, a.n_ok);
+  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok);
   k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_ok);
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
@@ -1155,8 +1152,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_mask);
   k_intern_assign<<<grid_for(a.nm_mask + 1), BLK, 0, s>>>((const ull*)a.nm_key, a.nm_id, a.nm_mask + 1, a.nm_counter);
   k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen);
-  k_state_p1<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_asg, a.n_gen);
-  k_state_p2<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_asg, a.n_gen);
+  k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen);
   k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_gen);
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();

@@ -181,6 +181,8 @@ typedef struct SwEngineArgs {
   int64_t carry_cap;
   // ---------------------------------------------------------------- rules, host-side sizes
   int64_t n_zone_vtx;          // zone_off[n_zones]: sizes k_zone_mask's dynamic LDS vertex table
+  // ---------------------------------------------------------------- state merge scratch
+  int64_t* ev_slot;            // [2 * max(rec_cap, gen_cap)] state pass-2 items: (ms slot | -2 - asg | -1, date)
 } SwEngineArgs;
 
 enum {

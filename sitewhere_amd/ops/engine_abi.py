@@ -54,6 +54,8 @@ FIELDS = [
     ("carry", P), ("n_carry", P), ("spill", P), ("n_spill", P), ("carry_cap", I),
     # rules, host-side sizes
     ("n_zone_vtx", I),
+    # state merge scratch
+    ("ev_slot", P),
 ]
 
 

@@ -144,6 +144,7 @@ class GpuInboundEngine(EngineBase):
         t["gen"] = z(c.gen_cap * EVENT_REC.itemsize, u8)
         t["gen_dev"] = z(c.gen_cap, i32)
         t["gen_asg"] = z(c.gen_cap, i32)
+        t["ev_slot"] = z(2 * max(c.rec_cap, c.gen_cap), torch.int64)   # (slot, date) state pass-2 items
         t["zmask"] = z(c.rec_cap, i64)
         t["ztile"] = z(2 * ntiles + 64, i32)
         t["stats"] = z(16, i64)
@@ -176,6 +177,7 @@ class GpuInboundEngine(EngineBase):
         a.nm_key, a.nm_id, a.nm_first = _ptr(t["nm_key"]), _ptr(t["nm_id"]), _ptr(t["nm_first"])
         a.nm_mask, a.nm_counter = c.name_slots - 1, _ptr(t["nm_counter"])
         a.st, a.ms, a.ms_mask = _ptr(t["st"]), _ptr(t["ms"]), c.state_slots - 1
+        a.ev_slot = _ptr(t["ev_slot"])
         a.store_cap = sc
         a.store_cursor = _ptr(t["cursor"])
         a.step_cursor0 = _ptr(t["cursor"]) + 8
