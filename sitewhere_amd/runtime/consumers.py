@@ -53,9 +53,20 @@ class BusConsumer(TenantEngineLifecycleComponent):
 
     # A failed batch is re-read from its first record (the partition is not committed past it) with
     # exponential backoff: transient faults (RPC unavailable, storage hiccups) cost retries, never
-    # records.  A batch failing ``max_attempts`` times in a row is a poison batch: it is logged,
-    # counted in ``dropped`` and skipped so the partition is not wedged forever.
+    # records.  A batch failing ``max_attempts`` times in a row is a poison batch: its records are
+    # moved to ``<topic>.dead-letter`` (same keys and values, so they can be inspected and
+    # re-injected), counted in ``dropped`` and skipped, so the partition is not wedged forever.
     max_attempts = 10
+    DEAD_LETTER_SUFFIX = ".dead-letter"
+
+    def _dead_letter(self, recs):
+        try:
+            self.engine.ms.producer.send_batch(recs[0].topic + self.DEAD_LETTER_SUFFIX,
+                                               [(r.key, r.value) for r in recs])
+            return True
+        except Exception:
+            self.logger.exception("consumer %s: dead-letter publish failed", self.component_name)
+            return False
 
     def _call(self, recs) -> bool:
         try:
@@ -98,11 +109,11 @@ class BusConsumer(TenantEngineLifecycleComponent):
                     attempts.pop(tp, None)
                     continue
                 n = attempts.get(tp, (first, 0))[1] + 1 if attempts.get(tp, (None,))[0] == first else 1
-                if n >= self.max_attempts:
+                if n >= self.max_attempts and self._dead_letter(batch[tp]):
                     attempts.pop(tp, None)
                     self.dropped += len(batch[tp])
-                    self.logger.error("consumer %s: dropping poison batch %s@%d after %d attempts",
-                                      self.component_name, tp, first, n)
+                    self.logger.error("consumer %s: poison batch %s@%d moved to %s%s after %d attempts",
+                                      self.component_name, tp, first, tp[0], self.DEAD_LETTER_SUFFIX, n)
                     continue
                 attempts[tp] = (first, n)
                 failed[tp] = first

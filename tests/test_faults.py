@@ -74,6 +74,10 @@ def test_consumer_skips_poison_batch():
         assert _wait(lambda: c.dropped == 10 and len(ok) == 20, 30)
         assert sorted(ok) == list(range(10)) + list(range(20, 30))
         assert c.retries == 2
+        dl = bus.consumer("dlq-reader", ["p.dead-letter"])
+        got = []
+        assert _wait(lambda: got.extend(r.value for rs in dl.poll(50).values() for r in rs) or len(got) == 10)
+        assert sorted(int(v) for v in got) == list(range(10, 20))
     finally:
         c._stop.set()
         c._t.join(5)
