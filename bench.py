@@ -14,7 +14,7 @@ One step = one micro-batch of ``--msgs`` protobuf device payloads per GPU, run e
   persisted too) -> presence scan -> D2H of every enriched event to the outbound host ring.
 Weak scaling: per-GPU payloads and per-GPU device shard are fixed as N grows.
 
-Launch: ``python bench.py --gpus 1 --steps 20 --warmup 5`` or under torch.distributed.run
+Launch: ``python bench.py --gpus 1 --steps 200 --warmup 20`` or under torch.distributed.run
 for N > 1 (one rank per GPU, RCCL).
 """
 from __future__ import annotations
@@ -31,8 +31,8 @@ import numpy as np
 def parse():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)   # ~0.2 s timed at N=1: steady state, not warm-up
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--msgs", type=int, default=1 << 20, help="payloads per GPU per step")
     ap.add_argument("--devices", type=int, default=1 << 20, help="registered devices per GPU")
     ap.add_argument("--mx-per-msg", type=int, default=1)
