@@ -13,6 +13,7 @@ inbound engine can mirror devices/assignments into HBM (new capability).
 from __future__ import annotations
 
 import json
+import logging
 import threading
 
 from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
@@ -57,8 +58,8 @@ class DeviceManagement:
         for cb in list(self._listeners):
             try:
                 cb(kind, entity)
-            except Exception:
-                pass
+            except Exception:   # one listener must not block the others; make the failure visible
+                logging.getLogger(__name__).warning("device-model listener failed on %s", kind, exc_info=True)
 
     # ================================================================== device types
     def create_device_type(self, request: dict) -> DeviceType:
@@ -657,7 +658,8 @@ class DeviceManagementTriggers:
                                          "previousState": None if kind == "assignment.created" else "Active",
                                          "newState": "Active" if kind == "assignment.created" else "Released"})
         except Exception:
-            pass
+            logging.getLogger(__name__).warning("assignment state-change event for %s not recorded", kind,
+                                                exc_info=True)
 
 
 class DeviceManagementTenantEngine(MicroserviceTenantEngine):
