@@ -10,6 +10,7 @@ GetTenantTemplates, GetDatasetTemplates.
 from __future__ import annotations
 
 import copy
+import os
 import json
 import secrets
 import threading
@@ -204,6 +205,11 @@ class TenantManagementMicroservice(GlobalMicroservice):
         self._store = store
         self.tenants: TenantManagement | None = None
         self._lock = threading.Lock()
+        # a reference deployment's Spring XML tenant templates, imported as ref-<name>
+        ref = os.environ.get("SITEWHERE_REFERENCE_TEMPLATES")
+        if ref:
+            from ..runtime.xml_import import register_reference_templates
+            register_reference_templates(ref)
 
     def default_configuration(self) -> dict:
         return {"datastore": {"type": "memory"}}

@@ -1,0 +1,101 @@
+"""Reference Spring XML tenant templates -> JSON configuration (runtime/xml_import.py).
+
+Reads the reference's own template files (``service-tenant-management/dockerimage/templates``);
+the end-to-end case boots a tenant from the imported ``default`` template -- MongoDB datastores on
+the in-process MongoDB server, MQTT event sources on the in-process broker -- and delivers a
+protobuf measurement over MQTT to the topic the reference's XML names."""
+from __future__ import annotations
+
+import os
+import time
+
+import pytest
+
+from sitewhere_amd.runtime.xml_import import convert_service, import_tenant_template, register_reference_templates
+
+REF = "/root/reference/service-tenant-management/dockerimage/templates"
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference templates not present")
+
+
+def test_all_reference_templates_import_cleanly():
+    for name in ("default", "mongodb", "influxdb", "cassandra", "stomp"):
+        t = import_tenant_template(os.path.join(REF, name))
+        assert t["warnings"] == [], (name, t["warnings"])
+        assert set(t["services"]) >= {"event-sources", "event-management", "device-management", "inbound-processing"}
+    d = import_tenant_template(os.path.join(REF, "default"))["services"]
+    srcs = d["event-sources"]["sources"]
+    assert [s["id"] for s in srcs] == ["protobuf", "json"]
+    assert srcs[0]["decoder"] == "protobuf" and srcs[1]["decoder"] == "json"
+    assert srcs[0]["receivers"][0] == {"type": "mqtt", "host": "${mqtt.host:localhost}", "port": "${mqtt.port:1883}",
+                                       "topic": "SiteWhere/[[tenant.token]]/input/protobuf", "qos": 1, "numThreads": 1}
+    assert d["inbound-processing"]["processingThreadCount"] == 25
+    assert d["device-state"]["presence"] == {"checkInterval": "PT10M", "missingInterval": "PT8H"}
+    assert d["device-registration"]["allowNewDevices"] is False
+    assert d["event-management"]["datastore"]["type"] == "mongodb" and d["event-management"]["buffered"] is True
+    assert d["command-delivery"]["router"] == {"type": "single-choice", "destination": "default"}
+    assert d["command-delivery"]["destinations"][0]["provider"] == "mqtt"
+    st = import_tenant_template(os.path.join(REF, "stomp"))["services"]["event-sources"]["sources"]
+    assert st == [{"id": "stomp", "decoder": "json-batch", "receivers": [
+        {"type": "activemq-broker", "transportUri": "stomp://localhost:2345?trace=true", "queueName": "SITEWHERE.STOMP",
+         "numConsumers": 5, "brokerName": None}]}]
+    cq = import_tenant_template(os.path.join(REF, "cassandra"))["services"]
+    assert cq["event-management"]["datastore"]["type"] == "cassandra"
+    # overlays keep the reference default's other services (MQTT sources, MongoDB registries)
+    assert cq["event-sources"]["sources"][0]["id"] == "protobuf" and cq["device-management"]["datastore"]["type"] == "mongodb"
+    assert import_tenant_template(os.path.join(REF, "influxdb"))["services"]["event-management"]["datastore"]["type"] \
+        == "influxdb"
+
+
+def test_unknown_elements_are_reported():
+    xml = b"""<beans xmlns:op="x"><op:outbound-connectors>
+        <op:mqtt-connector connectorId="m1" hostname="h" port="1884" outboundTopic="out/${tenant.token}"/>
+        <op:mystery-connector connectorId="z"/></op:outbound-connectors></beans>"""
+    from sitewhere_amd.runtime.xml_import import _Ctx
+    ctx = _Ctx()
+    doc = convert_service("outbound-connectors", xml, ctx)
+    assert doc == {"connectors": [{"id": "m1", "type": "mqtt", "host": "h", "port": 1884,
+                                   "topic": "out/[[tenant.token]]"}]}
+    assert ctx.warnings == ["outbound-connectors: <mystery-connector> not imported"]
+
+
+def test_tenant_boots_from_imported_reference_default_template(monkeypatch):
+    from sitewhere_amd.assembly import SiteWhereInstance
+    from sitewhere_amd.edges.mqtt import MqttBroker, MqttClient
+    from sitewhere_amd.models import wire
+    from sitewhere_amd.persistence.mongo_server import MiniMongoServer
+    from sitewhere_amd.services.tenant_management import TENANT_TEMPLATES
+    mongo = MiniMongoServer(port=0).start()
+    broker = MqttBroker().start()
+    monkeypatch.setenv("MONGODB_URI", f"mongodb://127.0.0.1:{mongo.port}")
+    monkeypatch.setenv("MQTT_HOST", "127.0.0.1")
+    monkeypatch.setenv("MQTT_PORT", str(broker.port))
+    ids = register_reference_templates(REF)
+    sw = None
+    try:
+        assert {"ref-default", "ref-stomp", "ref-mongodb"} <= set(ids)
+        sw = SiteWhereInstance().start()
+        sw.wait_for_tenant("default", 60)
+        tm = sw.api("TenantManagement")
+        sw.instance.system_user.run(lambda: tm.create_tenant({"token": "xr", "name": "xr",
+                                                              "configurationTemplateId": "ref-default",
+                                                              "datasetTemplateId": "construction"}))
+        sw.wait_for_tenant("xr", 120)
+        run = lambda f: sw.instance.system_user.run(f, "xr")  # noqa: E731
+        dm, em = sw.api("DeviceManagement", "xr"), sw.api("DeviceEventManagement", "xr")
+        aid = run(lambda: dm.get_device_by_token("meitrack-002")).device_assignment_id
+        c = MqttClient("127.0.0.1", broker.port).connect()
+        end, res = time.time() + 30, []
+        while not res and time.time() < end:
+            c.publish("SiteWhere/xr/input/protobuf", wire.measurements("meitrack-002", {"xml.t": 7.25}), qos=1)
+            time.sleep(0.5)
+            res = [e for e in run(lambda: em.list_measurements_for_index("Assignment", [aid])).results
+                   if e.name == "xml.t"]
+        assert res and res[0].value == 7.25
+        c.disconnect()
+    finally:
+        if sw is not None:
+            sw.stop()
+        for k in ids:
+            TENANT_TEMPLATES.pop(k, None)
+        broker.stop()
+        mongo.stop()
