@@ -10,8 +10,8 @@ GetTenantTemplates, GetDatasetTemplates.
 from __future__ import annotations
 
 import copy
-import os
 import json
+import os
 import secrets
 import threading
 
