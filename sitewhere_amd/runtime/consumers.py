@@ -195,3 +195,26 @@ class NearCache:
 
     def __len__(self):
         return len(self._d)
+
+
+def replay_dead_letter(bus, topic: str, group: str = "dead-letter-replay", limit: int | None = None,
+                       timeout_ms: int = 200) -> int:
+    """Move records parked in ``<topic>.dead-letter`` (poison batches, see ``BusConsumer``) back onto
+    ``topic`` -- e.g. after the bug or the bad reference data that made them fail was fixed.  The
+    replay consumer group commits what it moved, so a second call resumes after it.  Returns the
+    number of records re-published."""
+    c = bus.consumer(group, [topic + BusConsumer.DEAD_LETTER_SUFFIX], auto_offset_reset="earliest")
+    prod = bus.producer()
+    moved = 0
+    try:
+        while limit is None or moved < limit:
+            batch = c.poll(timeout_ms, 500 if limit is None else min(500, limit - moved))
+            if not batch:
+                break
+            for recs in batch.values():
+                prod.send_batch(topic, [(r.key, r.value) for r in recs])
+                moved += len(recs)
+            c.commit()
+    finally:
+        c.close()
+    return moved

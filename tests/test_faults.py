@@ -78,6 +78,18 @@ def test_consumer_skips_poison_batch():
         got = []
         assert _wait(lambda: got.extend(r.value for rs in dl.poll(50).values() for r in rs) or len(got) == 10)
         assert sorted(int(v) for v in got) == list(range(10, 20))
+        # once the cause is fixed, the parked records go back onto the topic and are processed
+        from sitewhere_amd.runtime.consumers import replay_dead_letter
+        poisoned = {b"13"}
+        handler_ok = ok
+
+        def fixed(recs):
+            handler_ok.extend(int(r.value) for r in recs if r.value not in poisoned)
+        c.handler = fixed
+        poisoned.clear()
+        assert replay_dead_letter(bus, "p") == 10
+        assert _wait(lambda: sorted(ok) == list(range(30)))
+        assert replay_dead_letter(bus, "p") == 0
     finally:
         c._stop.set()
         c._t.join(5)
