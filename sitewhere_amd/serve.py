@@ -130,6 +130,8 @@ def main(argv=None) -> int:
     ap.add_argument("--log-level", default="INFO")
     ap.add_argument("--heartbeat", type=float, default=5.0)
     ap.add_argument("--jwt-secret", default="sitewhere-instance-secret")
+    ap.add_argument("--reference-templates", default=None,
+                    help="a SiteWhere 2.x templates directory: its Spring XML tenant templates become ref-<name>")
     sub = ap.add_subparsers(dest="cmd", required=True)
     p = sub.add_parser("infra")
     p.add_argument("--port", type=int, default=9092)
@@ -151,6 +153,8 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    if args.reference_templates:                 # read by tenant management when it starts
+        os.environ["SITEWHERE_REFERENCE_TEMPLATES"] = args.reference_templates
     return {"infra": cmd_infra, "service": cmd_service, "all": cmd_all}[args.cmd](args)
 
 
