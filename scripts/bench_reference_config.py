@@ -205,7 +205,7 @@ def per_event_replicas(args) -> dict:
     procs = [_spawn(["service", *g, "--infra", infra.address], logs[i]) for i, g in enumerate(groups)]
     try:
         inst = Instance(InstanceSettings(heartbeat_s=1.0), bus=RemoteEventBus(infra.address),
-                        coord=RemoteCoordination(infra.address), jwt_secret="sitewhere-instance-secret",
+                        coord=RemoteCoordination(infra.address),
                         network_rpc=True)
         topo = TopologyStateAggregator(inst.bus, inst.naming.microservice_state_updates(), "bench", 30.0)
         topo.lifecycle_start(LifecycleProgressMonitor())

@@ -436,7 +436,14 @@ class ZooKeeperCoordination:
     def watch_tree(self, prefix: str, callback, initial: bool = True):
         t = _TreeCache(self, _norm(prefix), callback)
         self._trees.append(t)
-        self._pool.submit(t.start, initial)
+        if initial:
+            self._pool.submit(t.start, True)
+        else:
+            # load the current tree before returning: a node created after this call must fire
+            # NODE_ADDED.  Loading in the background let a node created between the caller's own
+            # listing and the cache's first read be absorbed silently into the initial state (a
+            # tenant bootstrapped in that window never started an engine).
+            t.start(False)
 
         def cancel():
             if t in self._trees:

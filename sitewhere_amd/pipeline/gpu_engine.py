@@ -461,13 +461,14 @@ class GpuInboundEngine(EngineBase):
     def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
         """Synchronous convenience step (tests, control-plane use): H2D, run, D2H, learn names."""
         n_msgs = len(offs) - 1
-        raw_dev, off_dev = self._stage(raw, offs)
-        do_presence = self.presence_due(now_ms) if presence is None else presence
-        # rows land in HBM and come back in one DMA: reading them out of the mapped host buffer
-        # is CPU-uncached (~2.6 GB/s measured, 0.8 ms per 64K rows; profiles/r1_tenant_step)
-        sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence, out_to_device=True)
-        torch.cuda.synchronize(self.device)
-        return self.collect(sel, raw, from_device=True)
+        with self._lock:            # serialised against hot-store queries (cursor + shared scratch)
+            raw_dev, off_dev = self._stage(raw, offs)
+            do_presence = self.presence_due(now_ms) if presence is None else presence
+            # rows land in HBM and come back in one DMA: reading them out of the mapped host buffer
+            # is CPU-uncached (~2.6 GB/s measured, 0.8 ms per 64K rows; profiles/r1_tenant_step)
+            sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence, out_to_device=True)
+            torch.cuda.synchronize(self.device)
+            return self.collect(sel, raw, from_device=True)
 
     def _stage(self, raw: np.ndarray, offs: np.ndarray):
         """H2D of a host batch through persistent pinned staging (a pageable ``.to(device)`` ran at
@@ -549,20 +550,30 @@ class GpuInboundEngine(EngineBase):
         return {int(k): int(i) for k, i in zip(keys[sel], ids[sel])}
 
     def device_state(self, asg: int) -> dict:
-        from ..models.columnar import ASG_STATE, MS_SLOT
-        intern = self.intern_table()
-        inv = {v: k for k, v in intern.items()}
-        ms = self.t["ms"].cpu().numpy().view(MS_SLOT)
+        """Last-known state of one assignment.  The merged-state table is filtered on the device and
+        only the assignment's slots (and their name-table entries) cross PCIe -- the table is
+        ``state_slots`` x 32 B, GBs at bench sizing."""
+        from ..models.columnar import ASG_STATE
+        with self._lock:
+            ms = self.t["ms"].view(-1, 4)
+            keys = ms[:, 0]
+            hit = torch.nonzero((keys != 0) & (((keys - 1) >> 32) == int(asg))).flatten()
+            rows = ms[hit].cpu().numpy().view(np.uint64)
+            st = self.t["st"].view(-1, 4)[asg].cpu().numpy().view(ASG_STATE)[0]
+            nids = np.unique(((rows[:, 0] - np.uint64(1)) & np.uint64(0xFFFFFFFF)) >> np.uint64(1)).astype(np.int64)
+            inv = {}
+            if len(nids):
+                sel = torch.nonzero(torch.isin(self.t["nm_id"].long(), torch.from_numpy(nids).to(self.device))).flatten()
+                ks = self.t["nm_key"][sel].cpu().numpy().view(np.uint64)
+                ids = self.t["nm_id"][sel].cpu().numpy()
+                inv = {int(i): int(k) for k, i in zip(ks, ids) if k != 0}
         mx, al = {}, {}
-        for s in np.nonzero(ms["key"] != 0)[0]:
-            k = int(ms["key"][s]) - 1
-            a, nid, kind = k >> 32, (k & 0xFFFFFFFF) >> 1, k & 1
-            if a != asg:
-                continue
+        for key, date, eid1, _ in rows:
+            k = int(key) - 1
+            nid, kind = (k & 0xFFFFFFFF) >> 1, k & 1
             h = inv.get(nid)
             name = self.names.get(h, str(h))
-            (al if kind else mx)[name] = (int(ms["eid1"][s]) - 1, int(ms["date"][s]))
-        st = self.t["st"].view(-1, 4)[asg].cpu().numpy().view(ASG_STATE)[0]
+            (al if kind else mx)[name] = (int(eid1) - 1, int(date))
         le = int(st["loc_eid1"])
         return {
             "assignment": asg,
@@ -575,7 +586,13 @@ class GpuInboundEngine(EngineBase):
 
     def query_store(self, event_type, asg_idx, start=None, end=None, page_number=1, page_size=100):
         """Hot-store query on the MI355X: one k_store_filter pass over the HBM ring (assignment set
-        as a bitmap), then the match set is ordered on the device and only the page comes back."""
+        as a bitmap), then the match set is ordered on the device and only the page comes back.
+        Holds the engine lock: the cursor read, the filter into the shared match buffer and the
+        gather are one unit against concurrent queries and steps."""
+        with self._lock:
+            return self._query_store(event_type, asg_idx, start, end, page_number, page_size)
+
+    def _query_store(self, event_type, asg_idx, start, end, page_number, page_size):
         cur = self.cursor
         n = min(cur, self.cfg.store_cap)
         nbits = self.cfg.max_assignments

@@ -19,12 +19,26 @@ from concurrent.futures import ThreadPoolExecutor, wait
 
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 
+_DEFAULT = object()
+
+
+class RetryFrom(Exception):
+    """Raised by a handler whose earlier batches have side effects still pending (e.g. rows stepped
+    through the inbound engine but not yet stored): re-read each ``(topic, partition)`` in ``offsets``
+    from the given offset instead of from the current batch's first record.  Such a rewind is a
+    transient condition by construction, so it never counts towards dead-lettering."""
+
+    def __init__(self, offsets: dict, cause: BaseException | None = None):
+        super().__init__(f"re-read from {offsets}: {cause!r}")
+        self.offsets = dict(offsets)
+        self.cause = cause
+
 
 class BusConsumer(TenantEngineLifecycleComponent):
     component_type = LifecycleComponentType.Other
 
     def __init__(self, engine, name: str, topics: list[str], handler, threads: int = 0, max_records: int = 500,
-                 group: str | None = None, auto_commit: bool = True):
+                 group: str | None = None, auto_commit: bool = True, max_attempts=_DEFAULT, idle=None):
         super().__init__(name)
         self.tenant_engine = engine
         self.engine = engine
@@ -42,6 +56,15 @@ class BusConsumer(TenantEngineLifecycleComponent):
         self.dropped = 0          # records of poison batches skipped after max_attempts
         # False: the handler commits explicit offsets itself (checkpoint-aligned commits)
         self.auto_commit = auto_commit
+        # None: a control-plane consumer (registry change feed, registration): a batch is retried
+        # until it succeeds, with an error logged every ``alert_every`` attempts -- skipping it would
+        # leave the consumer's state silently diverged from its source of truth
+        if max_attempts is not _DEFAULT:
+            self.max_attempts = max_attempts
+        self.rewinds = 0
+        # called on the poll thread when a poll returns nothing; may raise RetryFrom (a failure that
+        # surfaced after its batch was handed off, e.g. on a store thread, with no new records due)
+        self.idle = idle
 
     def start(self, monitor):
         bus = self.engine.ms.instance.bus
@@ -55,8 +78,10 @@ class BusConsumer(TenantEngineLifecycleComponent):
     # exponential backoff: transient faults (RPC unavailable, storage hiccups) cost retries, never
     # records.  A batch failing ``max_attempts`` times in a row is a poison batch: its records are
     # moved to ``<topic>.dead-letter`` (same keys and values, so they can be inspected and
-    # re-injected), counted in ``dropped`` and skipped, so the partition is not wedged forever.
-    max_attempts = 10
+    # re-injected with :func:`replay_dead_letter`), counted in ``dropped`` and skipped, so the
+    # partition is not wedged forever.
+    max_attempts: int | None = 10
+    alert_every = 10
     DEAD_LETTER_SUFFIX = ".dead-letter"
 
     def _dead_letter(self, recs):
@@ -68,13 +93,18 @@ class BusConsumer(TenantEngineLifecycleComponent):
             self.logger.exception("consumer %s: dead-letter publish failed", self.component_name)
             return False
 
-    def _call(self, recs) -> bool:
+    def _call(self, recs):
+        """True on success, False on failure, or the ``{tp: offset}`` rewind of a :class:`RetryFrom`."""
         try:
             # sends made while handling this batch go out in one produce round trip, before the commit
             with self.engine.ms.producer.batching():
                 self.handler(recs)
             self.processed += len(recs)
             return True
+        except RetryFrom as e:
+            self.failures += len(recs)
+            self.logger.warning("consumer %s: re-reading %s (%r)", self.component_name, e.offsets, e.cause)
+            return e.offsets
         except Exception:
             self.failures += len(recs)
             self.logger.exception("consumer %s failed to process %d records", self.component_name, len(recs))
@@ -90,6 +120,19 @@ class BusConsumer(TenantEngineLifecycleComponent):
                 time.sleep(0.1)
                 continue
             if not batch:
+                if self.idle is not None:
+                    try:
+                        self.idle()
+                    except RetryFrom as e:
+                        self.logger.warning("consumer %s: re-reading %s (%r)", self.component_name, e.offsets, e.cause)
+                        for tp, pos in e.offsets.items():
+                            self.consumer.seek(tp[0], tp[1], pos)
+                        self.rewinds += 1
+                        self.retries += 1
+                        self._stop.wait(backoff)
+                        backoff = min(2.0, backoff * 2)
+                    except Exception:
+                        self.logger.exception("consumer %s: idle check failed", self.component_name)
                 continue
             ok: dict = {}
             if self.pool is None:
@@ -101,15 +144,31 @@ class BusConsumer(TenantEngineLifecycleComponent):
                     step = max(1, len(recs) // self.threads)
                     futs[tp] = [self.pool.submit(self._call, recs[i:i + step]) for i in range(0, len(recs), step)]
                 wait([f for fs in futs.values() for f in fs])
-                ok = {tp: all(f.result() for f in fs) for tp, fs in futs.items()}
-            failed = {}
+                ok = {}
+                for tp, fs in futs.items():
+                    rs = [f.result() for f in fs]
+                    ok[tp] = next((r for r in rs if isinstance(r, dict)), all(r is True for r in rs))
+            failed, rewind = {}, {}
+            for tp, good in ok.items():
+                if isinstance(good, dict):
+                    rewind.update(good)
+                    if tp not in good:
+                        rewind[tp] = batch[tp][0].offset
+            for tp, pos in rewind.items():
+                failed[tp] = min(pos, failed.get(tp, pos))
             for tp, good in ok.items():
                 first = batch[tp][0].offset
-                if good:
-                    attempts.pop(tp, None)
+                if good is True or tp in rewind:
+                    if tp not in rewind:
+                        attempts.pop(tp, None)
                     continue
                 n = attempts.get(tp, (first, 0))[1] + 1 if attempts.get(tp, (None,))[0] == first else 1
-                if n >= self.max_attempts and self._dead_letter(batch[tp]):
+                if self.max_attempts is None:
+                    if n % self.alert_every == 0:
+                        self.logger.error("consumer %s: batch %s@%d still failing after %d attempts "
+                                          "(control-plane consumer: retried until it succeeds)",
+                                          self.component_name, tp, first, n)
+                elif n >= self.max_attempts and self._dead_letter(batch[tp]):
                     attempts.pop(tp, None)
                     self.dropped += len(batch[tp])
                     self.logger.error("consumer %s: poison batch %s@%d moved to %s%s after %d attempts",
@@ -117,7 +176,10 @@ class BusConsumer(TenantEngineLifecycleComponent):
                     continue
                 attempts[tp] = (first, n)
                 failed[tp] = first
-                self.consumer.seek(tp[0], tp[1], first)         # re-read it: at-least-once
+            for tp, pos in failed.items():
+                self.consumer.seek(tp[0], tp[1], pos)           # re-read it: at-least-once
+            if rewind:
+                self.rewinds += 1
             if self.auto_commit:
                 offsets = {tp: pos for tp, pos in self.consumer.positions.items() if tp not in failed}
                 if offsets:
@@ -202,7 +264,12 @@ def replay_dead_letter(bus, topic: str, group: str = "dead-letter-replay", limit
     """Move records parked in ``<topic>.dead-letter`` (poison batches, see ``BusConsumer``) back onto
     ``topic`` -- e.g. after the bug or the bad reference data that made them fail was fixed.  The
     replay consumer group commits what it moved, so a second call resumes after it.  Returns the
-    number of records re-published."""
+    number of records re-published.
+
+    Ordering is NOT preserved: replayed records are appended after everything written to ``topic``
+    since they were parked, so a consumer sees them after newer records of the same key.  That is
+    why control-plane consumers (registry change feed, registration) never dead-letter
+    (``max_attempts=None``): an old ``device.updated`` replayed after a newer one would win."""
     c = bus.consumer(group, [topic + BusConsumer.DEAD_LETTER_SUFFIX], auto_offset_reset="earliest")
     prod = bus.producer()
     moved = 0

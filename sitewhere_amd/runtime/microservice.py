@@ -18,7 +18,9 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import queue
+import secrets
 import socket
 import threading
 import time
@@ -26,7 +28,7 @@ import uuid
 
 from ..bus.log import EventBus
 from ..bus.naming import TopicNaming
-from ..coord.store import NODE_ADDED, NODE_REMOVED, NODE_UPDATED, Coordination, InterProcessMutex
+from ..coord.store import NODE_ADDED, NODE_REMOVED, NODE_UPDATED, Coordination, InterProcessMutex, NodeExistsError
 from ..core.errors import SiteWhereException, TenantEngineNotAvailableException
 from ..core.lifecycle import (CompositeLifecycleStep, LifecycleComponent, LifecycleComponentType,
                               LifecycleProgressMonitor, LifecycleStatus, SimpleLifecycleStep,
@@ -107,7 +109,8 @@ class Instance:
         self.settings = settings or InstanceSettings.from_env()
         self.bus = bus or EventBus(None, default_partitions=8)
         self.coord = coord or Coordination()
-        self.tokens = tokens or TokenManagement(jwt_secret or "sitewhere-instance-secret")
+        self.tokens = tokens or TokenManagement(jwt_secret or os.environ.get("SITEWHERE_JWT_SECRET")
+                                                or self._shared_jwt_secret())
         self.naming = TopicNaming(self.settings.product_id, self.settings.instance_id)
         self.resolver = ServiceResolver()
         self.system_user = SystemUser(self.tokens)
@@ -117,6 +120,19 @@ class Instance:
         self.network_rpc = network_rpc
         self.microservices: dict[str, "Microservice"] = {}
         self.scripts = ScriptManagement(self.coord, self.path("scripts"))
+
+    def _shared_jwt_secret(self) -> str:
+        """One random HS512 secret per instance, created by whichever process gets there first and
+        shared with every other process through the coordination store (the reference hard-codes
+        "secret", ``TokenManagement.java:42-45``; a fixed default would let anyone who reads the source
+        forge tokens).  Access to the coordination store is the trust boundary, as ZooKeeper is for
+        the reference's configuration."""
+        path = self.path("security", "jwt-secret")
+        try:
+            self.coord.create(path, secrets.token_hex(32).encode())
+        except NodeExistsError:
+            pass
+        return self.coord.get(path)[0].decode()
 
     # coordination paths ---------------------------------------------------------
     def path(self, *parts) -> str:

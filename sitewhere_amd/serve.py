@@ -129,7 +129,9 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="sitewhere_amd.serve")
     ap.add_argument("--log-level", default="INFO")
     ap.add_argument("--heartbeat", type=float, default=5.0)
-    ap.add_argument("--jwt-secret", default="sitewhere-instance-secret")
+    ap.add_argument("--jwt-secret", default=None,
+                    help="HS512 signing secret (or SITEWHERE_JWT_SECRET); default: a random secret created "
+                         "once per instance and shared through the coordination store")
     ap.add_argument("--reference-templates", default=None,
                     help="a SiteWhere 2.x templates directory: its Spring XML tenant templates become ref-<name>")
     sub = ap.add_subparsers(dest="cmd", required=True)

@@ -75,7 +75,9 @@ class DeviceRegistrationTenantEngine(MicroserviceTenantEngine):
     def tenant_initialize(self, monitor):
         self.manager = RegistrationManager(self, self.config)
         n, t = self.ms.instance.naming, self.tenant.token
-        self.reg_consumer = BusConsumer(self, "registration-events", [n.device_registration_events(t)], self._on_reg)
+        # registration is control plane: a failing registration is retried, never dead-lettered
+        self.reg_consumer = BusConsumer(self, "registration-events", [n.device_registration_events(t)], self._on_reg,
+                                        max_attempts=None)
         self.unreg_consumer = BusConsumer(self, "unregistered-events", [n.unregistered_device_events(t)], self._on_unreg)
         self.api = {"DeviceRegistration": RegistrationApi(self)}
 

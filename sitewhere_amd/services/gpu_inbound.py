@@ -39,7 +39,7 @@ from ..pipeline.engine_base import Zone, ZoneTest
 from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
 from ..utils import IndexMap
-from ..runtime.consumers import BusConsumer
+from ..runtime.consumers import BusConsumer, RetryFrom
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
 from .inbound_processing import InboundProcessingTenantEngine
 
@@ -57,6 +57,16 @@ def unpack_raw_batch(value: bytes):
     raw = np.zeros(int(offs[-1]) + 64, np.uint8)
     raw[:offs[-1]] = np.frombuffer(value, np.uint8, int(offs[-1]), start)
     return raw, offs
+
+
+class _Stepped:
+    """A raw batch the engine has stepped, with the storage stages it has completed."""
+    __slots__ = ("key", "res", "now", "raw", "offs", "stored", "published", "routed", "queued", "payload", "events")
+
+    def __init__(self, key, res, now, raw, offs):
+        self.key, self.res, self.now, self.raw, self.offs = key, res, now, raw, offs
+        self.stored = self.published = self.routed = self.queued = False
+        self.payload = self.events = None
 
 
 class GpuInboundTenantEngine(InboundProcessingTenantEngine):
@@ -110,8 +120,19 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._store_q: queue.Queue = queue.Queue(maxsize=2)
         self._store_thread = None
         self._store_error = None
+        # Replay safety.  engine.step is not idempotent (cursor, event ids, dedup table and device
+        # state advance), so a raw record is stepped at most once per engine lifetime: its StepResult
+        # stays in ``_stepped`` until every storage stage succeeded, and a re-read record (consumer
+        # retry / rewind) reuses it and retries only the stages still missing.  ``_stored_hw`` is,
+        # per partition, the offset below which every record is fully stored (stores run in step
+        # order), so a replayed prefix is skipped outright.
+        self._stepped: dict[tuple, _Stepped] = {}
+        self._stored_hw: dict[tuple, int] = {}
+        self.replayed_batches = 0
+        # never dead-lettered: a stepped batch cannot be re-stepped, only its storage retried
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
-                                        self._process_raw, max_records=16,
+                                        self._process_raw, max_records=16, max_attempts=None,
+                                        idle=self._raise_store_error,
                                         auto_commit=self.ckpt_path is None and not self.async_store)
         self.persisted_events = self.create_meter("persistedEvents")
         self.step_timer = self.create_timer("engineStep")
@@ -226,7 +247,10 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             self._store_thread.join(10)
             self._store_thread = None
         if self.ckpt_path and self._since_ckpt:
-            self.checkpoint()
+            if self._store_error is None and not self._stepped:
+                self.checkpoint()
+            else:               # the next start replays from the last good checkpoint instead
+                self.logger.error("not checkpointing on stop: %d stepped batches are not stored", len(self._stepped))
         super().tenant_stop(monitor)
 
     # ---------------------------------------------------------------- checkpoint / resume
@@ -234,6 +258,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         """Snapshot the shard + the raw-topic offsets it covers, then commit those offsets."""
         import os
         self.flush()            # every batch the snapshot covers must be stored before its offset commits
+        self._raise_store_error()
+        if self._stepped:
+            # the snapshot would cover engine state whose rows were never stored: committing its
+            # offsets would lose them.  The raw consumer re-reads and re-stores first.
+            raise RuntimeError(f"refusing to checkpoint: {len(self._stepped)} stepped batches not stored")
         with self._lock:
             extra = {"boot": self.boot, "offsets": [[t, p, o] for (t, p), o in self._ckpt_offsets.items()],
                      "dev_index": self.dev_index.ids, "asg_index": self.asg_index.ids,
@@ -268,57 +297,114 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     # ---------------------------------------------------------------- data plane
     def _process_raw(self, recs):
         for r in recs:
-            raw, offs = unpack_raw_batch(r.value)
-            # the record timestamp is the batch's receive time: replay after a restore is deterministic
+            tp = (r.topic, r.partition)
+            self._raise_store_error()                   # before any new step, never after
+            if r.offset < self._stored_hw.get(tp, -1):
+                continue                                # fully stored on an earlier read
+            key = (r.topic, r.partition, r.offset)
             commit = (r.topic, r.partition, r.offset + 1) if self.async_store and not self.ckpt_path else None
-            self.process_batch(raw, offs, now=r.timestamp or None, commit=commit)
+            item = self._stepped.get(key)
+            if item is None:
+                raw, offs = unpack_raw_batch(r.value)
+                # the record timestamp is the batch's receive time: replay after a restore is deterministic
+                self.process_batch(raw, offs, now=r.timestamp or None, commit=commit, key=key)
+            else:
+                self.replayed_batches += 1
+                self._submit(item, commit)
             if self.ckpt_path:
-                self._ckpt_offsets[(r.topic, r.partition)] = r.offset + 1
+                self._ckpt_offsets[tp] = r.offset + 1
                 self._since_ckpt += 1
                 if self._since_ckpt >= self.ckpt_every:
                     self.checkpoint()
 
-    def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None, commit=None):
+    def _raise_store_error(self):
+        """A store step failed on the store thread: stop stepping and have the raw consumer re-read
+        from the oldest stepped-but-unstored batch of each partition (their results are reused)."""
+        if self._store_error is None:
+            return
+        self.flush()                    # the store thread skips everything queued after the failure
+        err, self._store_error = self._store_error, None
+        rewind: dict = {}
+        for (t, p, o) in self._stepped:
+            rewind[(t, p)] = min(o, rewind.get((t, p), o))
+        raise RetryFrom(rewind, err)
+
+    def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None, commit=None, key=None):
         """One engine step; storing its rows happens here or, with ``asyncStore``, on the store thread
-        while the next step runs (call :meth:`flush` to wait for it)."""
+        while the next step runs (call :meth:`flush` to wait for it).  ``key`` = (topic, partition,
+        offset) of the raw record: the result is then kept until stored (see ``_stepped``)."""
         now = now or now_ms()
         with self._lock, self.step_timer.time():
             res = self.engine.step(raw, offs, now)
         self.processed_events.mark(res.n_events)
-        if self._store_thread is not None:
-            if self._store_error is not None:
-                err, self._store_error = self._store_error, None
-                raise RuntimeError("engine store thread failed") from err
-            self._store_q.put((res, now, raw, offs, commit))
-        else:
-            self._store_step(res, now, raw, offs, commit)
+        item = _Stepped(key, res, now, raw, offs)
+        if key is not None:
+            self._stepped[key] = item
+        self._submit(item, commit)
         return res
 
-    def _store_step(self, res, now, raw, offs, commit):
-        if self.storage == "columnar":
-            self._store_columnar(res, now)
+    def _submit(self, item: "_Stepped", commit):
+        if self._store_thread is not None:
+            if not item.queued:
+                item.queued = True
+                self._store_q.put((item, commit))
         else:
-            self._store_objects(res, now)
-        if res.rejects is not None and len(res.rejects):
-            self._slow_path(raw, offs, res)
+            self._store_step(item, commit)
+
+    def _store_step(self, item: "_Stepped", commit):
+        """Storage stages of one stepped batch; each runs once even when the batch is retried."""
+        res, now = item.res, item.now
+        if not item.stored:
+            if self.storage == "columnar":
+                with self.store_timer.time():
+                    if item.payload is None:    # built once: it carries the dictionary deltas
+                        item.payload = self.columnar_payload(res, now)
+                    n = self._em().add_columnar_batch(item.payload)
+                self.persisted_events.mark(n)
+            else:
+                if item.events is None:
+                    item.events = self._to_events(res, now)
+                if item.events:
+                    self._em().add_enriched_events(item.events)
+                    self.persisted_events.mark(len(item.events))
+            item.stored = True
+        if not item.published:
+            with self.publish_timer.time():
+                if self.storage == "columnar" and self.publish == "batches":
+                    self.ms.producer.send(self.t_enriched_batches, None, item.payload)
+                elif self.publish == "events":
+                    self._publish_events(item.events if item.events is not None else self._to_events(res, now))
+            item.published = True
+        if not item.routed:
+            if res.rejects is not None and len(res.rejects):
+                self._slow_path(item.raw, item.offs, res)
+            item.routed = True
+        if item.key is not None:
+            t, p, o = item.key
+            self._stepped.pop(item.key, None)
+            self._stored_hw[(t, p)] = max(self._stored_hw.get((t, p), -1), o + 1)
         if commit is not None:
             self.ms.instance.bus.commit(self.raw_consumer.group, *commit)
 
     def _store_loop(self):
         while True:
-            item = self._store_q.get()
+            entry = self._store_q.get()
             try:
-                if item is None:
+                if entry is None:
                     return
-                self._store_step(*item)
-            except Exception as e:  # noqa: BLE001 -- surfaced on the next process_batch
+                item, commit = entry
+                item.queued = False
+                if self._store_error is None:   # after a failure nothing is stored (or committed) past it
+                    self._store_step(item, commit)
+            except Exception as e:  # noqa: BLE001 -- surfaced before the next engine step
                 self._store_error = e
                 self.logger.exception("engine store step failed")
             finally:
                 self._store_q.task_done()
 
     def flush(self):
-        """Wait until every stepped batch is stored (and its raw offset committed)."""
+        """Wait until every queued batch is stored (and its raw offset committed) or skipped after a
+        store failure."""
         if self._store_thread is not None:
             self._store_q.join()
 
@@ -341,30 +427,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         out = res.out if res.out is not None else np.zeros(0, OUT_REC)
         return encode_batch(self.boot, res.first_seq, res.world, res.rank, now, out, asg, names, rules)
 
-    def _store_columnar(self, res, now: int):
-        with self.store_timer.time():
-            payload = self.columnar_payload(res, now)
-            n = self._em().add_columnar_batch(payload)
-        self.persisted_events.mark(n)
-        with self.publish_timer.time():
-            if self.publish == "batches":
-                self.ms.producer.send(self.t_enriched_batches, None, payload)
-            elif self.publish == "events":
-                self._publish_events(self._to_events(res, now))
-
     def _publish_events(self, events):
         if events:
             self.ms.producer.send_batch(self.t_enriched, [
                 (self._dev_tokens.get(self.dev_index.idx.get(e.device_id, -1)) or e.device_id,
                  json.dumps({"event": codec.to_wire(e), "context": self._context(e)}).encode()) for e in events])
-
-    def _store_objects(self, res, now: int):
-        events = self._to_events(res, now)
-        if events:
-            self._em().add_enriched_events(events)
-            self.persisted_events.mark(len(events))
-            if self.publish == "events":
-                self._publish_events(events)
 
     def _name(self, nid: int) -> str:
         if nid == NO_NAME:
@@ -508,4 +575,7 @@ class GpuInboundApi:
         raw, offs = pack_messages([bytes(p) for p in payloads])
         r = self._e.process_batch(raw, offs)
         self._e.flush()
+        if self._e._store_error is not None:
+            err, self._e._store_error = self._e._store_error, None
+            raise err
         return {"messages": r.n_msgs, "events": r.n_events, "persisted": r.n_persisted}

@@ -54,9 +54,10 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
         self.assignment_lookup = self.create_timer("assignmentLookup")
         self.event_storage = self.create_timer("eventStorage")
         self.unregistered = self.create_meter("unregisteredEvents")
-        # invalidate near caches from the device-model change feed
+        # invalidate near caches from the device-model change feed; a control-plane consumer: an
+        # update that keeps failing is retried (and alerted on), never dead-lettered and skipped
         self.model_consumer = BusConsumer(self, "model-updates", [n.tenant_prefix(t) + "device-model-updates"],
-                                          self._on_model_update)
+                                          self._on_model_update, max_attempts=None)
         self.api = {"InboundProcessing": InboundProcessingApi(self)}
 
     def tenant_start(self, monitor):

@@ -5,6 +5,7 @@ transient storage / RPC failures).
 
 * ``fail(obj, "add_events", rate)``  -- the call raises :class:`InjectedFault` with probability ``rate``
   (before the real method runs, i.e. the side effect does not happen: a transient outage);
+* ``fail_next(obj, "add_events", n)`` -- the next ``n`` calls raise (a deterministic outage);
 * ``drop(obj, "read", rate, empty=[])`` -- the call returns ``empty`` instead (a lost / late delivery:
   for a log read the records come back on a later poll);
 * ``delay(obj, "read", rate, seconds)`` -- the call sleeps first.
@@ -49,6 +50,23 @@ class FaultInjector:
         def make(orig):
             def wrapped(*a, **kw):
                 if self._roll(rate):
+                    self.injected[(name, "fail")] += 1
+                    raise InjectedFault(f"injected failure in {type(obj).__name__}.{name}")
+                return orig(*a, **kw)
+            return wrapped
+        self._patch(obj, name, make)
+        return self
+
+    def fail_next(self, obj, name: str, n: int = 1):
+        left = [n]
+
+        def make(orig):
+            def wrapped(*a, **kw):
+                with self._lock:
+                    hit = self.enabled and left[0] > 0
+                    if hit:
+                        left[0] -= 1
+                if hit:
                     self.injected[(name, "fail")] += 1
                     raise InjectedFault(f"injected failure in {type(obj).__name__}.{name}")
                 return orig(*a, **kw)

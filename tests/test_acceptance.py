@@ -267,6 +267,7 @@ def test_transient_faults_no_loss_no_duplicates(sw):
     retries0 = ib.decoded_consumer.retries
     with FaultInjector(seed=7) as fi:
         fi.fail(em_engine.store, "add_events", 0.6)
+        fi.fail_next(em_engine.store, "add_events", 7)     # 2 consumer threads: one exhausts its 4 in-place attempts
         fi.drop(sw.instance.bus, "read", 0.2, empty=[])
         fi.delay(sw.instance.bus, "read", 0.05, 0.02)
         for m in msgs:

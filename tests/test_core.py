@@ -100,6 +100,27 @@ def test_jwt_roundtrip_and_tamper():
         tm.get_claims(TokenManagement("s3cret", expiration_minutes=-1).generate_token("a", []))
 
 
+def test_instance_jwt_secret_is_random_and_shared_through_coordination(monkeypatch):
+    """No literal default secret: each instance gets a random one, created once in the coordination
+    store, so every process of the instance verifies the others' tokens and nobody else can."""
+    from sitewhere_amd.coord.store import Coordination
+    from sitewhere_amd.runtime.config import InstanceSettings
+    from sitewhere_amd.runtime.microservice import Instance
+    monkeypatch.delenv("SITEWHERE_JWT_SECRET", raising=False)
+    coord = Coordination()
+    a = Instance(InstanceSettings(), coord=coord)
+    b = Instance(InstanceSettings(), coord=coord)          # a second process of the same instance
+    other = Instance(InstanceSettings())                    # a different instance
+    assert a.tokens.secret == b.tokens.secret and len(a.tokens.secret) == 64
+    assert other.tokens.secret != a.tokens.secret
+    assert b.tokens.get_username(a.system_jwt())
+    with pytest.raises(UnauthorizedException):
+        other.tokens.get_claims(a.system_jwt())
+    assert TokenManagement("sitewhere-instance-secret").secret != a.tokens.secret
+    monkeypatch.setenv("SITEWHERE_JWT_SECRET", "from-env")
+    assert Instance(InstanceSettings(), coord=Coordination()).tokens.secret == b"from-env"
+
+
 def test_security_context_is_scoped_per_thread():
     out = {}
 

@@ -1,0 +1,117 @@
+"""Replay safety of the fused inbound engine tenant (services/gpu_inbound.py).
+
+engine.step advances the event cursor, the alternate-id dedup table and device state, so it must
+run once per raw record: when storing a stepped batch fails, the raw consumer re-reads the batch
+and only the storage is retried with the kept StepResult.  These tests run on the CPU engine (the
+same tenant code drives the MI355X engine) and check that a failed store loses nothing, stores
+nothing twice and never drops a replayed event as an alternate-id duplicate."""
+from __future__ import annotations
+
+import struct
+import time
+
+import pytest
+
+from sitewhere_amd.assembly import SiteWhereInstance
+from sitewhere_amd.models import wire
+from sitewhere_amd.services.event_sources import RAW_PAYLOADS
+from sitewhere_amd.utils.faults import FaultInjector
+
+
+def wait_until(cond, timeout=20.0, step=0.02):
+    end = time.time() + timeout
+    while time.time() < end:
+        if cond():
+            return True
+        time.sleep(step)
+    return bool(cond())
+
+
+def _raw_batch(b, n=20, token="galaxytab-001"):
+    msgs = [wire.measurements(token, {"v": float(100 * b + i)}, event_date=1_700_000_000_000 + 100 * b + i,
+                              alternate_id=f"rp-{b}-{i}") for i in range(n)]
+    return struct.pack(f"<I{len(msgs)}I", len(msgs), *[len(m) for m in msgs]) + b"".join(msgs)
+
+
+@pytest.fixture(scope="module")
+def inst():
+    sw = SiteWhereInstance().start()
+    sw.wait_for_tenant("default", 60)
+    yield sw
+    sw.stop()
+
+
+def _tenant(inst, token, template):
+    tm = inst.api("TenantManagement")
+    inst.instance.system_user.run(lambda: tm.create_tenant({"token": token, "name": token,
+                                                            "configurationTemplateId": template,
+                                                            "datasetTemplateId": "construction"}))
+    inst.wait_for_tenant(token, 60)
+    ib = inst.tenant_engine("inbound-processing", token)
+    run = lambda f: inst.instance.system_user.run(f, token)  # noqa: E731
+    dev = run(lambda: inst.api("DeviceManagement", token).get_device_by_token("galaxytab-001"))
+    assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+    return ib, run, dev
+
+
+def _values(inst, run, token, dev):
+    em = inst.api("DeviceEventManagement", token)
+    res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id], {"pageSize": 0}))
+    return res.results
+
+
+def test_async_store_failure_rewinds_and_stores_once(inst):
+    """gpu-columnar (asyncStore on): the store thread fails batch k while batch k+1 is queued.
+    Nothing is committed past k, the consumer rewinds to k, both batches are stored from their kept
+    results (not re-stepped) and every event lands exactly once."""
+    ib, run, dev = _tenant(inst, "rpa", "gpu-columnar")
+    assert ib.async_store
+    store = inst.tenant_engine("event-management", "rpa").store
+    topic = inst.instance.naming.tenant_prefix("rpa") + RAW_PAYLOADS
+    group = ib.raw_consumer.group
+    with FaultInjector() as fi:
+        fi.fail_next(store, "add_columnar", 2)
+        for b in range(6):
+            inst.instance.bus.append(topic, 0, [(None, _raw_batch(b))], ts=1_700_000_100_000 + b)
+        assert wait_until(lambda: store.rows == 120, 30), store.rows
+        assert fi.injected[("add_columnar", "fail")] == 2
+    assert ib.engine.stats_dict()["persisted"] == 120          # each batch stepped exactly once
+    assert ib.replayed_batches >= 1 and ib.raw_consumer.rewinds >= 1
+    assert wait_until(lambda: inst.instance.bus.committed(group, topic, 0) == 6)
+    res = _values(inst, run, "rpa", dev)
+    assert sorted(m.value for m in res) == sorted(float(100 * b + i) for b in range(6) for i in range(20))
+    assert len({m.id for m in res}) == 120
+    assert not ib._stepped
+
+
+def test_sync_store_failure_retries_store_not_step(inst):
+    """gpu template (synchronous object storage): the event-management call fails after the step.
+    The re-read batch reuses its StepResult -- before the fix it was re-stepped and every event with
+    an alternate id was rejected as a duplicate of itself and silently lost."""
+    ib, run, dev = _tenant(inst, "rps", "gpu")
+    assert not ib.async_store
+    mgmt = inst.tenant_engine("event-management", "rps").management
+    topic = inst.instance.naming.tenant_prefix("rps") + RAW_PAYLOADS
+    with FaultInjector() as fi:
+        fi.fail_next(mgmt, "add_enriched_events", 2)
+        for b in range(4):
+            inst.instance.bus.append(topic, 0, [(None, _raw_batch(b))], ts=1_700_000_200_000 + b)
+        assert wait_until(lambda: len(_values(inst, run, "rps", dev)) >= 80, 30)
+    assert ib.engine.stats_dict()["persisted"] == 80
+    assert ib.engine.stats_dict().get("duplicates", 0) == 0
+    res = _values(inst, run, "rps", dev)
+    assert sorted(m.value for m in res) == sorted(float(100 * b + i) for b in range(4) for i in range(20))
+    assert len({m.id for m in res}) == 80
+    assert ib.replayed_batches >= 1
+
+
+def test_checkpoint_refuses_unstored_batches(inst, tmp_path):
+    ib, _, _ = _tenant(inst, "rpc", "gpu-columnar")
+    ib.ckpt_path = str(tmp_path / "shard.safetensors")
+    ib._stepped[("t", 0, 5)] = object()
+    try:
+        with pytest.raises(RuntimeError, match="refusing to checkpoint"):
+            ib.checkpoint()
+    finally:
+        ib._stepped.clear()
+        ib.ckpt_path = None

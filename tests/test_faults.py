@@ -140,3 +140,57 @@ def test_fault_injector_is_seeded_and_restores():
     with FaultInjector(seed=0) as fi:
         fi.drop(o, "f", 1.0, empty=[])
         assert o.f() == []
+
+
+def test_control_plane_consumer_never_dead_letters():
+    """max_attempts=None (registry change feed, registration): a failing batch is retried until it
+    succeeds -- skipping it would leave the consumer's mirror diverged from device management."""
+    bus = EventBus(default_partitions=1)
+    prod = bus.producer()
+    for i in range(5):
+        prod.send("cp", "k", str(i).encode())
+    seen, fails = [], [0]
+
+    def handler(recs):
+        if fails[0] < 14:
+            fails[0] += 1
+            raise InjectedFault("model store down")
+        seen.extend(int(r.value) for r in recs)
+    c = BusConsumer(_engine(bus), "c", ["cp"], handler, max_records=10, group="g-cp", max_attempts=None)
+    c.alert_every = 5
+    c._stop.wait = lambda t: time.sleep(min(t, 0.01))      # keep the backoff short for the test
+    c.start(None)
+    try:
+        assert _wait(lambda: seen == list(range(5)), 20)
+        assert c.dropped == 0 and c.retries == 14
+        assert bus.end_offset("cp.dead-letter", 0) == 0
+    finally:
+        c._stop.set()
+        c._t.join(5)
+
+
+def test_retry_from_rewinds_before_the_current_batch():
+    """A handler may ask to re-read from an earlier offset (work handed off for batch k failed while
+    batch k+1 is being handled): the consumer seeks there, and that never counts as a poison batch."""
+    from sitewhere_amd.runtime.consumers import RetryFrom
+    bus = EventBus(default_partitions=1)
+    prod = bus.producer()
+    for i in range(6):
+        prod.send("rw", "k", str(i).encode())
+    reads, state = [], {"rewound": False}
+
+    def handler(recs):
+        reads.extend(r.offset for r in recs)
+        if recs[0].offset == 3 and not state["rewound"]:
+            state["rewound"] = True
+            raise RetryFrom({("rw", 0): 1}, InjectedFault("store of offset 1 failed"))
+    c = BusConsumer(_engine(bus), "c", ["rw"], handler, max_records=3, group="g-rw")
+    c.max_attempts = 1                                      # a RetryFrom must not dead-letter
+    c.start(None)
+    try:
+        assert _wait(lambda: bus.committed("g-rw", "rw", 0) == 6, 10)
+        assert reads[:6] == [0, 1, 2, 3, 4, 5] and reads[6:9] == [1, 2, 3]
+        assert c.rewinds == 1 and c.dropped == 0
+    finally:
+        c._stop.set()
+        c._t.join(5)

@@ -126,7 +126,7 @@ def test_multiprocess_instance(infra, tmp_path):
                      infra.address], logs[1])]
     try:
         inst = Instance(InstanceSettings(heartbeat_s=0.5), bus=RemoteEventBus(infra.address),
-                        coord=RemoteCoordination(infra.address), jwt_secret="sitewhere-instance-secret",
+                        coord=RemoteCoordination(infra.address),
                         network_rpc=True)
         topo = TopologyStateAggregator(inst.bus, inst.naming.microservice_state_updates(), "test-client", 30.0)
         from sitewhere_amd.core.lifecycle import LifecycleProgressMonitor
