@@ -96,18 +96,26 @@ def bind_numa(index: int) -> int:
 
 def init_distributed(use_gpu: bool = True):
     """One process per GPU: bind the local device (and its NUMA node's CPUs), create the RCCL (or
-    gloo) process group."""
+    gloo) process group.  Returns (rank, local device index, world, device).
+
+    Rehearsal knobs (not for production runs): ``SW_SHARED_DEVICE=1`` puts every rank on GPU 0 and
+    ``SW_DIST_BACKEND=gloo`` exchanges through gloo (RCCL refuses two ranks on one GPU), so the
+    N>1 engine path -- partition, pipelined exchange on the comm stream, spill carry, cross-rank
+    stats -- runs on a one-GPU box with real kernels."""
     import torch
     import torch.distributed as dist
     rank, local, world = env_rank()
     device = None
     if use_gpu:
+        if os.environ.get("SW_SHARED_DEVICE", "0") == "1":
+            local = 0
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
         if world > 1:
             bind_numa(local)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl" if use_gpu else "gloo", device_id=device)
+        backend = os.environ.get("SW_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
     return rank, local, world, device
 
 
