@@ -7,11 +7,13 @@ decode -> inbound validation -> event persistence -> enrichment -> consumers
 number, so ``vs_baseline`` is null.
 
 One step = one micro-batch of ``--msgs`` protobuf device payloads per GPU, run end to end:
-  H2D of the raw wire bytes (pinned host) -> GPU decode -> [N>1: owner partition + RCCL
+  raw batch produced to the raw-payload topic of the native commit log (zero-copy, pinned record)
+  -> consumed in place -> H2D of the raw wire bytes straight from the topic -> GPU decode -> [N>1: owner partition + RCCL
   all-to-all re-keying by device token, the analogue of Kafka key partitioning] -> registry
   lookup + assignment validation -> alternate-id dedup -> persist into the HBM event store
   with enrichment -> device-state merge -> zone-test rules (point-in-polygon, generated alerts
-  persisted too) -> presence scan -> D2H of every enriched event to the outbound host ring.
+  persisted too) -> presence scan -> D2H of every enriched event into a pinned record published
+  to the enriched-batch topic -> consumer offset commit (``--no-bus``: pinned batches in, host ring out).
 Weak scaling: per-GPU payloads and per-GPU device shard are fixed as N grows.
 
 Launch: ``python bench.py --gpus 1 --steps 200 --warmup 20`` or under torch.distributed.run
@@ -44,6 +46,9 @@ def parse():
     ap.add_argument("--framing", choices=["varint", "offsets"], default="varint",
                     help="raw-batch framing on the wire to the GPU (varint lengths or u32 offsets)")
     ap.add_argument("--no-outbound", action="store_true", help="(diagnostic) skip the D2H outbound copy")
+    ap.add_argument("--bus", action=argparse.BooleanOptionalAction, default=True,
+                    help="GPU engine: consume raw batches from, and publish enriched batches to, commit-log "
+                         "topics in place (pipeline/bus_io.py); --no-bus feeds pinned batches directly")
     return ap.parse_args()
 
 
@@ -130,7 +135,53 @@ def main():
         if use_gpu:
             torch.cuda.synchronize()
 
-    if use_gpu:
+    bus_stats = None
+    if use_gpu and args.bus and args.framing == "varint":
+        # Through the bus: each step the producer side hands raw batch k to the raw-payload topic
+        # (zero-copy: the record is the pinned buffer), the engine's consumer reads it in place and
+        # DMAs it to HBM, and the step's enriched rows are DMA'd into a pinned record published to
+        # the enriched-batch topic.  Consumer offsets are committed once a batch's rows are out.
+        from collections import deque
+
+        from sitewhere_amd.bus.log import EventBus
+        from sitewhere_amd.bus.naming import TopicNaming
+        from sitewhere_amd.pipeline.bus_io import OutboundPublisher, RawBatchRecord, raw_view
+        bus = EventBus(None, default_partitions=1)
+        prefix = TopicNaming("sitewhere", f"bench-rank{rank}").tenant_prefix("default")
+        t_raw, t_out = prefix + "event-source-raw-payloads", prefix + "inbound-enriched-batches"
+        group = prefix + "inbound-processing.raw-payload-consumers"
+        bus.topic(t_raw, 1)
+        bus.set_retention(t_raw, 4 * max_raw)
+        records = [RawBatchRecord(b[2][:int(b[3][-1])], b[4].numpy(), len(b[3]) - 1) for b in batches]
+        assert raw_view(bus.view(t_raw, 0, records[0].publish(bus, t_raw)))[0].is_pinned(), \
+            "raw-batch records must be pinned: the H2D reads them in place"
+        pub = OutboundPublisher(bus, t_out, eng.lib, eng.out_cap, rank=rank, world=world)
+        runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound,
+                                 out_target=pub.target, on_outbound=pub.publish)
+        cursor = {"next": bus.end_offset(t_raw, 0)}
+        inflight = deque()
+        bus_stats = {"bus": bus, "pub": pub, "t_raw": t_raw, "group": group, "cursor": cursor}
+
+        def run(k):
+            records[k % len(records)].publish(bus, t_raw, 0, ts=now0 + k)     # producer: batch k arrives
+            off = cursor["next"]
+            cursor["next"] = off + 1
+            payload, lens, n, pb = raw_view(bus.view(t_raw, 0, off))           # consumer: read in place
+            slot = runner.k % runner.nbuf
+            pub.now_ms = now0 + k
+            runner.submit(payload, None, n, now_ms=now0 + k, presence=True, lens_host=lens, raw_bytes=pb)
+            inflight.append((off, runner.ev_h2d[slot]))
+            while inflight and inflight[0][1].query():
+                inflight.popleft()
+            bus.hold(t_raw, 0, inflight[0][0] if inflight else None)          # in-flight H2D sources stay
+            if off >= 2:
+                bus.commit(group, t_raw, 0, off - 1)     # batches < off-1: processed and rows published
+
+        def finish():
+            runner.flush()
+            bus.hold(t_raw, 0, None)
+            bus.commit(group, t_raw, 0, cursor["next"])
+    elif use_gpu:
         runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound)
 
         def run(k):
@@ -205,6 +256,7 @@ def main():
                 "engine": args.engine,
                 "cpu_threads": getattr(eng, "threads", None),
                 "framing": args.framing,
+                "bus": bool(bus_stats),
             },
             "detail": {
                 "events": ev, "persisted": persisted, "payloads": msgs, "rule_alerts": rule_alerts,
@@ -213,6 +265,11 @@ def main():
                 "h2d_bytes_per_gpu_step": int(max_raw) + int(max(
                     (b[4].numel() if b[4] is not None else 4 * len(b[3])) for b in batches)),
                 "registered_devices_rank0": n_dev,
+                **({"bus": {"raw_topic_records": bus_stats["bus"].end_offset(bus_stats["t_raw"], 0),
+                            "raw_committed": bus_stats["bus"].committed(bus_stats["group"], bus_stats["t_raw"], 0),
+                            "enriched_batches_published": bus_stats["pub"].published,
+                            "enriched_rows_published": bus_stats["pub"].rows,
+                            "enriched_buffers": bus_stats["pub"].n_alloc}} if bus_stats else {}),
             },
         }
         print(json.dumps(out), flush=True)

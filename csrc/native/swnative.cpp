@@ -332,6 +332,7 @@ struct Segment {
   uint8_t* buf = nullptr;
   size_t cap = 0;
   size_t used = 0;
+  int64_t ext = -1;     // >= 0: caller-owned buffer adopted by swlog_append_external (never freed here)
 };
 
 static uint8_t* seg_map(size_t cap) {
@@ -346,6 +347,15 @@ static uint8_t* seg_map(size_t cap) {
 struct SegPool {
   std::mutex mu;
   std::vector<uint8_t*> free;      // standard-size segments ready for reuse
+  std::vector<int64_t> released;   // ids of adopted external buffers that retention let go of
+  void release(const Segment& sg) {
+    if (sg.ext >= 0) {
+      std::lock_guard<std::mutex> g(mu);
+      released.push_back(sg.ext);
+    } else {
+      put(sg.buf, sg.cap);
+    }
+  }
   uint8_t* get(size_t cap) {
     if (cap == SEG_BYTES) {
       std::lock_guard<std::mutex> g(mu);
@@ -384,6 +394,7 @@ struct Partition {
   int64_t retention_bytes = 0;     // memory-only logs: drop oldest segments beyond this (0 = keep all)
   int64_t file_pos = 0;            // durable log: file length
   int fd = -1;                     // durable backing file (append-only), -1 = memory only
+  int64_t hold = INT64_MAX;        // retention never drops a segment holding an offset >= hold
   SegPool* pool = nullptr;
 
   const uint8_t* rec(int64_t i) const {
@@ -392,7 +403,7 @@ struct Partition {
   }
   // room for `total` contiguous bytes; returns (segment ordinal, offset)
   bool reserve(size_t total, int64_t* ord, size_t* off) {
-    if (segs.empty() || segs.back().cap - segs.back().used < total) {
+    if (segs.empty() || segs.back().ext >= 0 || segs.back().cap - segs.back().used < total) {
       Segment sg;
       sg.cap = total > SEG_BYTES ? total : SEG_BYTES;
       sg.buf = pool->get(sg.cap);
@@ -414,17 +425,24 @@ struct Partition {
     }
     base_offset += n;
     bytes -= (int64_t)segs.front().used;
-    pool->put(segs.front().buf, segs.front().cap);
+    pool->release(segs.front());
     segs.pop_front();
     ++seg0;
   }
+  // offset one past the last record held by the front segment
+  int64_t front_segment_end() const {
+    size_t k = 0;
+    while (k < index.size() && (index[k] >> 32) == seg0) ++k;
+    return base_offset + (int64_t)k;
+  }
+  bool front_droppable() const { return segs.size() > 1 && front_segment_end() <= hold; }
   void enforce_retention() {
     if (fd >= 0 || retention_bytes <= 0) return;
     // segment-granular like Kafka: the retained log stays >= retention_bytes
-    while (segs.size() > 1 && bytes - (int64_t)segs.front().used >= retention_bytes) drop_front_segment();
+    while (front_droppable() && bytes - (int64_t)segs.front().used >= retention_bytes) drop_front_segment();
   }
   ~Partition() {
-    for (auto& sg : segs) pool->put(sg.buf, sg.cap);
+    for (auto& sg : segs) pool->release(sg);
   }
 };
 
@@ -738,6 +756,85 @@ int64_t swlog_retain_from(void* h, int32_t topic, int32_t p, int64_t offset) {
   // free whole segments that no retained record points into (keep the tail segment for appends)
   while (pt->segs.size() > 1 && (pt->index.empty() || (pt->index.front() >> 32) > pt->seg0)) pt->drop_front_segment();
   return pt->base_offset;
+}
+
+// ---- zero-copy records (memory-only partitions) -------------------------------------------
+// A producer that already holds a record's bytes in DMA-able (pinned) memory hands the buffer to
+// the log instead of copying it: buf = [RecHdr (filled here)][key][value], total bytes in all.
+// The buffer becomes a segment of its own; the caller keeps it alive until retention releases
+// `ext_id` (swlog_take_released).  Consumers read such records in place (swlog_view), so an
+// MI355X consumer DMAs a raw batch straight from the topic, and enriched rows DMA'd from the GPU
+// into a pinned buffer are published without a host copy.  Returns the offset, -1 on error,
+// -2 for a durable partition (its records must live in the file).
+int64_t swlog_append_external(void* h, int32_t topic, int32_t p, uint8_t* buf, int64_t total, int64_t klen,
+                              int64_t ts, int64_t ext_id) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt || !buf || ext_id < 0 || klen < 0 || klen > 0xffff || total < (int64_t)sizeof(RecHdr) + klen ||
+      total - (int64_t)sizeof(RecHdr) >= (1ll << 32))
+    return -1;
+  RecHdr hd;
+  hd.len = (uint32_t)(total - (int64_t)sizeof(RecHdr));
+  hd.crc = 0;
+  hd.ts = ts;
+  hd.klen = (uint16_t)klen;
+  std::unique_lock<std::mutex> g(pt->mu);
+  if (pt->fd >= 0) return -2;
+  memcpy(buf, &hd, sizeof(hd));
+  const int64_t first = pt->base_offset + (int64_t)pt->index.size();
+  Segment sg;
+  sg.buf = buf;
+  sg.cap = sg.used = (size_t)total;
+  sg.ext = ext_id;
+  pt->segs.push_back(sg);
+  const int64_t ord = pt->seg0 + (int64_t)pt->segs.size() - 1;
+  pt->bytes += total;
+  pt->index.push_back(ord << 32);
+  pt->enforce_retention();
+  g.unlock();
+  pt->cv.notify_all();
+  return first;
+}
+
+// In-place view of one retained record's value (and key length / timestamp).  The pointer stays
+// valid while the record is retained: consumers that DMA from it set a hold (swlog_hold) first.
+// Returns 0, or -1 when the offset is not retained.
+int32_t swlog_view(void* h, int32_t topic, int32_t p, int64_t offset, const uint8_t** val, int64_t* vlen,
+                   int64_t* ts) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  const int64_t i = offset - pt->base_offset;
+  if (i < 0 || i >= (int64_t)pt->index.size()) return -1;
+  RecHdr hd;
+  const uint8_t* r = pt->rec(i);
+  memcpy(&hd, r, sizeof(hd));
+  *val = r + sizeof(RecHdr) + hd.klen;
+  *vlen = (int64_t)(hd.len - hd.klen);
+  *ts = hd.ts;
+  return 0;
+}
+
+// Retention keeps every record at or after `offset` (INT64_MAX = no hold) -- a consumer's in-flight
+// zero-copy reads.  Raising the hold applies any retention it was deferring.
+int32_t swlog_hold(void* h, int32_t topic, int32_t p, int64_t offset) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  pt->hold = offset;
+  pt->enforce_retention();
+  return 0;
+}
+
+// Ids of adopted buffers the log no longer references (retention dropped their records).
+int64_t swlog_take_released(void* h, int64_t* out, int64_t max) {
+  Log* L = (Log*)h;
+  std::lock_guard<std::mutex> g(L->pool.mu);
+  int64_t n = 0;
+  while (n < max && !L->pool.released.empty()) {
+    out[n++] = L->pool.released.back();
+    L->pool.released.pop_back();
+  }
+  return n;
 }
 
 // Memory-only logs: cap the retained bytes of every partition of `topic` (0 = unlimited);

@@ -139,6 +139,7 @@ def native():
         _proto(lib, "swlog_committed", c_int64, P, c_char_p, c_int32, c_int32)
         _proto(lib, "swlog_flush", c_int32, P)
         _proto(lib, "swlog_set_retention", c_int32, P, c_int32, c_int64)
+        _proto(lib, "swlog_take_released", c_int64, P, P, c_int64)
         # native CPU engine shard (csrc/native/swcpuengine.cpp)
         _proto(lib, "swce_create", P, c_int32)
         _proto(lib, "swce_destroy", None, P)
@@ -187,6 +188,10 @@ def native_gil():
             _proto(lib, "swlog_read", c_int64, P, c_int32, c_int32, c_int64, c_int64, P, c_int64, P)
             _proto(lib, "swlog_commit", c_int32, P, c_char_p, c_int32, c_int32, c_int64)
             _proto(lib, "swlog_committed", c_int64, P, c_char_p, c_int32, c_int32)
+            _proto(lib, "swlog_append_external", c_int64, P, c_int32, c_int32, P, c_int64, c_int64, c_int64,
+                   c_int64)
+            _proto(lib, "swlog_view", c_int32, P, c_int32, c_int32, c_int64, P, P, P)
+            _proto(lib, "swlog_hold", c_int32, P, c_int32, c_int32, c_int64)
             _native_gil = lib
     return _native_gil
 

@@ -124,6 +124,8 @@ class EventBus:
         self._groups: dict[str, _Group] = {}
         self._nparts: dict[str, int] = {}
         self._waiters: dict[str, set] = {}       # topic -> Events of consumers subscribed to it
+        self._ext: dict[int, object] = {}        # zero-copy record id -> buffer owner (kept alive)
+        self._ext_ids = itertools.count()
         self._closed = False
 
     # ------------------------------------------------------------------ topics
@@ -191,6 +193,56 @@ class EventBus:
             raise RuntimeError(f"append to {name}[{partition}] failed")
         self._wake(name)
         return first
+
+    # ------------------------------------------------------------------ zero-copy records
+    # swlog record header in front of every record: [u32 len][u32 crc][i64 ts][u16 key length].
+    REC_HDR = 18
+
+    def append_external(self, name: str, partition: int, owner, ptr: int, total: int, key_len: int = 0,
+                        ts: int | None = None) -> int:
+        """Publish a record whose bytes already sit in caller memory, without copying them.
+
+        ``ptr`` points at ``total`` bytes laid out as [``REC_HDR`` header bytes, filled in here][key
+        (``key_len``)][value].  The log references the memory in place (its own segment), so the
+        buffer must be DMA-able for the consumers that read it in place (pinned host memory for an
+        MI355X consumer).  ``owner`` (the buffer object) is kept alive until retention drops the
+        record; :meth:`reclaim` then hands it back for reuse.  Memory-only partitions only."""
+        ext = next(self._ext_ids)
+        with self._lock:
+            self._ext[ext] = owner
+        first = self.fast.swlog_append_external(self.h, self.topic(name), partition, ptr, int(total), int(key_len),
+                                               ts if ts is not None else int(time.time() * 1000), ext)
+        if first < 0:
+            with self._lock:
+                self._ext.pop(ext, None)
+            raise RuntimeError(f"zero-copy append to {name}[{partition}] failed ({first}): "
+                               "durable partitions copy their records (use append)")
+        self._wake(name)
+        return first
+
+    def view(self, name: str, partition: int, offset: int):
+        """(address, length, timestamp) of a retained record's value, read in place, or None.  The
+        address stays valid while the record is retained; DMA readers :meth:`hold` it first."""
+        ptr, n, ts = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
+        if self.fast.swlog_view(self.h, self.topic(name), partition, offset, ctypes.byref(ptr), ctypes.byref(n),
+                                ctypes.byref(ts)):
+            return None
+        return ptr.value, n.value, ts.value
+
+    def hold(self, name: str, partition: int, offset: int | None):
+        """Retention keeps every record at or after ``offset`` (None releases the hold)."""
+        self.fast.swlog_hold(self.h, self.topic(name), partition, (1 << 63) - 1 if offset is None else int(offset))
+
+    def reclaim(self) -> list:
+        """Owners of zero-copy records that retention has dropped (the log no longer reads them)."""
+        ids = np.zeros(256, np.int64)
+        out = []
+        while True:
+            n = self.lib.swlog_take_released(self.h, ids.ctypes.data, len(ids))
+            with self._lock:
+                out += [self._ext.pop(int(i), None) for i in ids[:n]]
+            if n < len(ids):
+                return [o for o in out if o is not None]
 
     # ------------------------------------------------------------------ fetch
     def read(self, name: str, partition: int, offset: int, max_records: int = 500, max_bytes: int = 1 << 20):

@@ -1,0 +1,152 @@
+"""The MI355X engine on the event bus without host copies.
+
+The reference moves every event through Kafka topics: event sources produce to
+``event-source-decoded-events``, inbound processing consumes it, and enriched events are produced to
+``inbound-enriched-events`` for the downstream consumer groups.  Here whole micro-batches move
+through the native commit log (``bus/log.py``) in place:
+
+* **raw batches in.**  A producer (event sources, or the bench's synthetic fleet) frames a batch of
+  device payloads into one pinned host buffer laid out as a commit-log record
+  (:class:`RawBatchRecord`) and publishes it with ``EventBus.append_external``: the log references
+  the buffer instead of copying it.  The engine's consumer reads the record in place
+  (:func:`raw_view`) and the copy engine DMAs the payload bytes and their varint lengths straight
+  from the topic to HBM.  A retention hold covers the records whose H2D is still in flight.
+* **enriched rows out.**  :class:`OutboundPublisher` hands the runner a pinned buffer with room for
+  a record header in front (``PipelinedRunner(out_target=...)``); the copy engine writes the step's
+  32-byte rows into it and the buffer is published to the enriched-batch topic as is.  Retention
+  returns released buffers to the publisher's pool, so the topic's retention window bounds the
+  pinned memory and a lagging reader is the only thing that can make the pool grow.
+
+Record formats (little endian, 64-byte headers so the payload and row regions stay aligned):
+
+* raw batch value: ``b"SWRB", version, n_msgs, payload_bytes, payload_off, lens_bytes, lens_off``
+  then the payload bytes (plus 64 zero bytes the decoder may over-read) and the LEB128 varint length
+  of every payload (``pipeline/framing.py``);
+* enriched batch value: ``b"SWOB", version, n_rows, rank, world, step, now_ms`` then ``n_rows``
+  :data:`~sitewhere_amd.models.columnar.OUT_REC` rows.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+
+import numpy as np
+import torch
+
+from ..bus.log import EventBus
+from ..models.columnar import OUT_REC
+
+RAW_MAGIC = b"SWRB"
+OUT_MAGIC = b"SWOB"
+VALUE_HDR = 64
+_RAW = struct.Struct("<4sIIIIII")
+_OUT = struct.Struct("<4sIIIIqq")
+_PAD = 64
+
+
+class RawBatchRecord:
+    """A framed raw batch in pinned host memory, shaped as a commit-log record (no key)."""
+
+    def __init__(self, payload: np.ndarray, lens: np.ndarray, n_msgs: int):
+        payload = np.ascontiguousarray(payload, np.uint8)
+        lens = np.ascontiguousarray(lens, np.uint8)
+        self.n_msgs = int(n_msgs)
+        self.payload_bytes = int(payload.size)
+        p_off = VALUE_HDR
+        l_off = p_off + self.payload_bytes + _PAD
+        self.value_len = l_off + int(lens.size)
+        self.total = EventBus.REC_HDR + self.value_len
+        self.buf = torch.zeros(self.total, dtype=torch.uint8).pin_memory()
+        a = self.buf.numpy()
+        v = EventBus.REC_HDR
+        a[v:v + VALUE_HDR] = np.frombuffer(_RAW.pack(RAW_MAGIC, 1, self.n_msgs, self.payload_bytes, p_off,
+                                                     int(lens.size), l_off).ljust(VALUE_HDR, b"\0"), np.uint8)
+        a[v + p_off:v + p_off + self.payload_bytes] = payload
+        a[v + l_off:v + l_off + lens.size] = lens
+        self.ptr = self.buf.data_ptr()
+
+    def publish(self, bus: EventBus, topic: str, partition: int = 0, ts: int | None = None) -> int:
+        return bus.append_external(topic, partition, self, self.ptr, self.total, ts=ts)
+
+
+def _host_tensor(addr: int, n: int) -> torch.Tensor:
+    return torch.frombuffer((ctypes.c_uint8 * n).from_address(addr), dtype=torch.uint8)
+
+
+def raw_view(view) -> tuple[torch.Tensor, torch.Tensor, int, int]:
+    """(payload incl. padding, varint lengths, n_msgs, payload bytes) of a raw-batch record read in
+    place -- CPU tensors over the topic's own (pinned) memory, ready for a non-blocking H2D."""
+    addr, vlen, _ = view
+    magic, ver, n, pb, poff, lb, loff = _RAW.unpack(ctypes.string_at(addr, _RAW.size))
+    if magic != RAW_MAGIC or ver != 1 or loff + lb > vlen or poff + pb + _PAD > loff:
+        raise ValueError("not a framed raw batch record")
+    return _host_tensor(addr + poff, pb + _PAD), _host_tensor(addr + loff, lb), n, pb
+
+
+class _OutBuf:
+    __slots__ = ("host", "nbytes", "hb")
+
+    def __init__(self, hb):
+        self.hb, self.host, self.nbytes = hb, hb.host, hb.nbytes
+
+
+class OutboundPublisher:
+    """Pinned row buffers for ``PipelinedRunner(out_target=..., on_outbound=...)`` that become
+    enriched-batch records of ``topic`` in place."""
+
+    def __init__(self, bus: EventBus, topic: str, lib, row_capacity: int, partition: int = 0, rank: int = 0,
+                 world: int = 1, max_buffers: int = 32, retention_bytes: int | None = None):
+        from .gpu_engine import HostBuffer
+        self._HostBuffer = HostBuffer
+        self.bus, self.topic, self.lib, self.partition = bus, topic, lib, partition
+        self.rank, self.world = rank, world
+        self.nbytes = EventBus.REC_HDR + VALUE_HDR + row_capacity * OUT_REC.itemsize
+        self.max_buffers = max_buffers
+        self.free: list[_OutBuf] = []
+        self.n_alloc = 0
+        self.step = 0
+        self.published = 0
+        self.rows = 0
+        self.now_ms = 0
+        bus.topic(topic, partition + 1)
+        # the topic keeps about two full batches by default; older records release their buffers
+        bus.set_retention(topic, 2 * self.nbytes if retention_bytes is None else int(retention_bytes))
+
+    def _acquire(self) -> _OutBuf:
+        if not self.free:
+            for o in self.bus.reclaim():
+                if isinstance(o, _OutBuf):
+                    self.free.append(o)
+        if self.free:
+            return self.free.pop()
+        if self.n_alloc >= self.max_buffers:
+            raise RuntimeError(f"enriched-batch buffers exhausted ({self.max_buffers}): a hold or a reader keeps "
+                               f"{self.topic} from releasing them")
+        self.n_alloc += 1
+        return _OutBuf(self._HostBuffer(self.lib, self.nbytes))
+
+    def target(self, nbytes: int):
+        """Runner hook: (address the rows are copied to, token)."""
+        if EventBus.REC_HDR + VALUE_HDR + nbytes > self.nbytes:
+            raise ValueError(f"{nbytes} row bytes exceed the outbound buffer ({self.nbytes})")
+        ob = self._acquire()
+        return ob.host + EventBus.REC_HDR + VALUE_HDR, ob
+
+    def publish(self, ob: _OutBuf, n_rows: int):
+        """Runner hook: the rows are in ``ob``; write the value header and publish the record."""
+        hdr = _OUT.pack(OUT_MAGIC, 1, int(n_rows), self.rank, self.world, self.step, int(self.now_ms))
+        ctypes.memmove(ob.host + EventBus.REC_HDR, hdr, len(hdr))
+        total = EventBus.REC_HDR + VALUE_HDR + int(n_rows) * OUT_REC.itemsize
+        self.bus.append_external(self.topic, self.partition, ob, ob.host, total, ts=int(self.now_ms) or None)
+        self.step += 1
+        self.published += 1
+        self.rows += int(n_rows)
+
+
+def read_out_batch(value: bytes) -> tuple[dict, np.ndarray]:
+    """Decode an enriched-batch record value (a copy read through ``EventBus.read``)."""
+    magic, ver, n, rank, world, step, now = _OUT.unpack_from(value, 0)
+    if magic != OUT_MAGIC or ver != 1:
+        raise ValueError("not an enriched-batch record")
+    rows = np.frombuffer(value, OUT_REC, n, VALUE_HDR)
+    return {"rank": rank, "world": world, "step": step, "now": now}, rows

@@ -701,11 +701,19 @@ class PipelinedRunner:
     """
 
     def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
-                 on_outbound=None, mode: str | None = None, push_blocks: int = 128, nbuf: int = 3):
+                 on_outbound=None, mode: str | None = None, push_blocks: int = 128, nbuf: int = 3,
+                 out_target=None):
+        """``out_target(n_bytes) -> (host address, token)`` (copy-engine modes): where each step's rows
+        land, e.g. a pinned buffer a bus topic then publishes in place; ``on_outbound(token, n_rows)``
+        is called once they are there.  Without it rows land in the engine's outbound ring and
+        ``on_outbound(rows)`` gets a view of them."""
         import os
         self.e = engine
+        self.out_target = out_target
         dev = engine.device
         self.mode = mode or os.environ.get("SW_OUTBOUND_MODE", "hsa")
+        if out_target is not None and self.mode not in ("hsa", "sdma"):
+            raise ValueError("out_target needs a copy-engine outbound mode (hsa or sdma)")
         self.h2d = torch.cuda.Stream(dev)
         self.comp = torch.cuda.current_stream(dev)
         self.push = torch.cuda.Stream(dev)
@@ -789,21 +797,30 @@ class PipelinedRunner:
         self.pending = b
         self.k += 1
 
-    def _deliver(self, b: int, n_out: int):
+    def _deliver(self, b: int, n_out: int, token=None):
         if self.deliver and self.on_outbound is not None and n_out:
-            self.on_outbound(self.e.out_host[b].view(OUT_REC, n_out))
+            if self.out_target is not None:
+                self.on_outbound(token, n_out)
+            else:
+                self.on_outbound(self.e.out_host[b].view(OUT_REC, n_out))
         self.delivered += n_out
+
+    def _dest(self, b: int, n_out: int):
+        """(host address, token) the rows of staging slot ``b`` are copied to."""
+        if self.out_target is None:
+            return self.e.out_host[b].host, None
+        return self.out_target(n_out * OUT_REC.itemsize)
 
     def _finish_copy(self):
         if self.copying is not None:
-            cb, cn, sig = self.copying
+            cb, cn, sig, tok = self.copying
             if sig is not None:
                 rc = self.e.lib.sw_sdma_wait(sig)
                 if rc:
                     raise RuntimeError(f"sw_sdma_wait failed ({rc})")
             else:
                 self.ev_push[cb].synchronize()
-            self._deliver(cb, cn)
+            self._deliver(cb, cn, tok)
             self.copying = None
 
     def _drain(self):
@@ -819,11 +836,12 @@ class PipelinedRunner:
             self._deliver(pb, n_out)
             return
         self._finish_copy()
+        dst, tok = self._dest(pb, n_out) if self.deliver and n_out else (None, None)
         if self.mode == "hsa":
             sig = None
             if self.deliver and n_out:
                 h = ctypes.c_uint64()
-                rc = self.e.lib.sw_sdma_copy(ctypes.c_void_p(self.e.out_host[pb].host),
+                rc = self.e.lib.sw_sdma_copy(ctypes.c_void_p(dst),
                                              ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
                                              self.sdma_engine, ctypes.byref(h))
                 if rc == 0:
@@ -834,18 +852,18 @@ class PipelinedRunner:
                     warnings.warn(f"sw_sdma_copy failed ({rc}); falling back to hipMemcpyAsync outbound")
                     self.mode = "sdma"
             if self.mode == "hsa":
-                self.copying = (pb, n_out, sig)
+                self.copying = (pb, n_out, sig, tok)
                 if sig is None:
                     self._finish_copy()
                 return
         if self.deliver and n_out:
-            rc = self.e.lib.sw_copy_d2h(ctypes.c_void_p(self.e.out_host[pb].host),
+            rc = self.e.lib.sw_copy_d2h(ctypes.c_void_p(dst),
                                         ctypes.c_void_p(_ptr(self.e.out_dev[pb])), n_out * OUT_REC.itemsize,
                                         ctypes.c_void_p(self.push.cuda_stream))
             if rc:
                 raise RuntimeError(f"sw_copy_d2h failed ({rc})")
         self.ev_push[pb].record(self.push)
-        self.copying = (pb, n_out, None)
+        self.copying = (pb, n_out, None, tok)
 
     def flush(self):
         if self.rounds and self.e.exchange_pending:
