@@ -332,7 +332,8 @@ struct Segment {
   uint8_t* buf = nullptr;
   size_t cap = 0;
   size_t used = 0;
-  int64_t ext = -1;     // >= 0: caller-owned buffer adopted by swlog_append_external (never freed here)
+  int64_t ext = -1;     // >= 0: caller-owned record body adopted by swlog_append_external (never freed here)
+  RecHdr xhdr;          // external record: its header lives here, its key + value at buf
 };
 
 static uint8_t* seg_map(size_t cap) {
@@ -400,6 +401,18 @@ struct Partition {
   const uint8_t* rec(int64_t i) const {
     const int64_t e = index[(size_t)i];
     return segs[(size_t)((e >> 32) - seg0)].buf + (e & 0xffffffffLL);
+  }
+  // header and key+value bytes of record i (external records keep them apart)
+  const uint8_t* rec_parts(int64_t i, RecHdr* hd) const {
+    const int64_t e = index[(size_t)i];
+    const Segment& sg = segs[(size_t)((e >> 32) - seg0)];
+    if (sg.ext >= 0) {
+      *hd = sg.xhdr;
+      return sg.buf;
+    }
+    const uint8_t* r = sg.buf + (e & 0xffffffffLL);
+    memcpy(hd, r, sizeof(RecHdr));
+    return r + sizeof(RecHdr);
   }
   // room for `total` contiguous bytes; returns (segment ordinal, offset)
   bool reserve(size_t total, int64_t* ord, size_t* off) {
@@ -540,6 +553,29 @@ static void save_groups(Log* L) {
 using namespace swlog;
 
 extern "C" {
+
+// Large host copies (columnar batches of enriched rows: ~37 MB per 1M-payload step) split over
+// threads: one core moves ~8 GB/s, the socket several times that.  Called without the GIL.
+void sw_memcpy_mt(void* dst, const void* src, int64_t n, int32_t threads) {
+  const int64_t min_chunk = 4 << 20;
+  int64_t t = threads > 0 ? threads : (int64_t)std::thread::hardware_concurrency();
+  if (t > 16) t = 16;
+  if (t > n / min_chunk) t = n / min_chunk;
+  if (t <= 1) {
+    memcpy(dst, src, (size_t)n);
+    return;
+  }
+  const int64_t chunk = ((n + t - 1) / t + 63) & ~(int64_t)63;
+  std::vector<std::thread> th;
+  for (int64_t i = 1; i < t; ++i) {
+    const int64_t off = i * chunk;
+    if (off >= n) break;
+    const int64_t len = off + chunk > n ? n - off : chunk;
+    th.emplace_back([=] { memcpy((uint8_t*)dst + off, (const uint8_t*)src + off, (size_t)len); });
+  }
+  memcpy(dst, src, (size_t)(chunk < n ? chunk : n));
+  for (auto& x : th) x.join();
+}
 
 // CRC-32C (Castagnoli) of a buffer: Kafka RecordBatch v2 checksums (bus/kafka_wire.py).
 uint32_t sw_crc32c(const uint8_t* p, int64_t n) { return swlog::crc32c(p, (size_t)n); }
@@ -720,8 +756,7 @@ int64_t swlog_read(void* h, int32_t topic, int32_t p, int64_t offset, int64_t ma
   int64_t i = offset - pt->base_offset, w = 0, cnt = 0;
   while (i < (int64_t)pt->index.size() && cnt < max_records) {
     RecHdr hd;
-    const uint8_t* r = pt->rec(i);
-    memcpy(&hd, r, sizeof(hd));
+    const uint8_t* body = pt->rec_parts(i, &hd);
     const int64_t need = 24 + (int64_t)hd.len;
     if (w + need > out_cap) {
       if (cnt == 0) return -need;
@@ -733,7 +768,7 @@ int64_t swlog_read(void* h, int32_t topic, int32_t p, int64_t offset, int64_t ma
     memcpy(out + w + 8, &hd.ts, 8);
     memcpy(out + w + 16, &kl, 4);
     memcpy(out + w + 20, &vl, 4);
-    memcpy(out + w + 24, r + sizeof(RecHdr), hd.len);
+    memcpy(out + w + 24, body, hd.len);
     w += need;
     ++cnt;
     ++i;
@@ -759,35 +794,31 @@ int64_t swlog_retain_from(void* h, int32_t topic, int32_t p, int64_t offset) {
 }
 
 // ---- zero-copy records (memory-only partitions) -------------------------------------------
-// A producer that already holds a record's bytes in DMA-able (pinned) memory hands the buffer to
-// the log instead of copying it: buf = [RecHdr (filled here)][key][value], total bytes in all.
-// The buffer becomes a segment of its own; the caller keeps it alive until retention releases
-// `ext_id` (swlog_take_released).  Consumers read such records in place (swlog_view), so an
-// MI355X consumer DMAs a raw batch straight from the topic, and enriched rows DMA'd from the GPU
-// into a pinned buffer are published without a host copy.  Returns the offset, -1 on error,
-// -2 for a durable partition (its records must live in the file).
-int64_t swlog_append_external(void* h, int32_t topic, int32_t p, uint8_t* buf, int64_t total, int64_t klen,
+// A producer that already holds a record's key + value bytes (``body``, ``len`` bytes, the first
+// ``klen`` of them the key) hands them to the log instead of copying them: the body becomes a
+// segment of its own and its header is kept beside it.  The caller keeps the memory alive and
+// unchanged until retention releases ``ext_id`` (swlog_take_released).  Consumers read such
+// records in place (swlog_view) -- an MI355X consumer DMAs a raw batch straight from the topic
+// when the body is pinned -- or by copy like any record.  Returns the offset, -1 on error, -2 for
+// a durable partition (its records must live in the file).
+int64_t swlog_append_external(void* h, int32_t topic, int32_t p, const uint8_t* body, int64_t len, int64_t klen,
                               int64_t ts, int64_t ext_id) {
   Partition* pt = part_of((Log*)h, topic, p);
-  if (!pt || !buf || ext_id < 0 || klen < 0 || klen > 0xffff || total < (int64_t)sizeof(RecHdr) + klen ||
-      total - (int64_t)sizeof(RecHdr) >= (1ll << 32))
-    return -1;
-  RecHdr hd;
-  hd.len = (uint32_t)(total - (int64_t)sizeof(RecHdr));
-  hd.crc = 0;
-  hd.ts = ts;
-  hd.klen = (uint16_t)klen;
+  if (!pt || !body || ext_id < 0 || klen < 0 || klen > 0xffff || len < klen || len >= (1ll << 32)) return -1;
   std::unique_lock<std::mutex> g(pt->mu);
   if (pt->fd >= 0) return -2;
-  memcpy(buf, &hd, sizeof(hd));
   const int64_t first = pt->base_offset + (int64_t)pt->index.size();
   Segment sg;
-  sg.buf = buf;
-  sg.cap = sg.used = (size_t)total;
+  sg.buf = const_cast<uint8_t*>(body);
+  sg.cap = sg.used = (size_t)len;
   sg.ext = ext_id;
+  sg.xhdr.len = (uint32_t)len;
+  sg.xhdr.crc = 0;
+  sg.xhdr.ts = ts;
+  sg.xhdr.klen = (uint16_t)klen;
   pt->segs.push_back(sg);
   const int64_t ord = pt->seg0 + (int64_t)pt->segs.size() - 1;
-  pt->bytes += total;
+  pt->bytes += len;
   pt->index.push_back(ord << 32);
   pt->enforce_retention();
   g.unlock();
@@ -806,9 +837,8 @@ int32_t swlog_view(void* h, int32_t topic, int32_t p, int64_t offset, const uint
   const int64_t i = offset - pt->base_offset;
   if (i < 0 || i >= (int64_t)pt->index.size()) return -1;
   RecHdr hd;
-  const uint8_t* r = pt->rec(i);
-  memcpy(&hd, r, sizeof(hd));
-  *val = r + sizeof(RecHdr) + hd.klen;
+  const uint8_t* body = pt->rec_parts(i, &hd);
+  *val = body + hd.klen;
   *vlen = (int64_t)(hd.len - hd.klen);
   *ts = hd.ts;
   return 0;

@@ -116,6 +116,7 @@ def native():
         _proto(lib, "sw_hash64_batch", None, P, P, c_int64, P)
         _proto(lib, "sw_murmur2", c_int32, P, c_int32)
         _proto(lib, "sw_crc32c", ctypes.c_uint32, ctypes.c_char_p, c_int64)
+        _proto(lib, "sw_memcpy_mt", None, P, P, c_int64, c_int32)
         _proto(lib, "sw_partition_for_key", c_int32, P, c_int32, c_int32)
         _proto(lib, "sw_reg_upsert", c_int64, P, P, P, c_int64, c_uint64, c_uint64, c_int32)
         _proto(lib, "sw_reg_find", c_int64, P, P, P, c_int64, c_uint64, c_uint64)
@@ -192,6 +193,7 @@ def native_gil():
                    c_int64)
             _proto(lib, "swlog_view", c_int32, P, c_int32, c_int32, c_int64, P, P, P)
             _proto(lib, "swlog_hold", c_int32, P, c_int32, c_int32, c_int64)
+            _proto(lib, "swlog_take_released", c_int64, P, P, c_int64)
             _native_gil = lib
     return _native_gil
 

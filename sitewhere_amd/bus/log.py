@@ -126,6 +126,7 @@ class EventBus:
         self._waiters: dict[str, set] = {}       # topic -> Events of consumers subscribed to it
         self._ext: dict[int, object] = {}        # zero-copy record id -> buffer owner (kept alive)
         self._ext_ids = itertools.count()
+        self._holds: dict[tuple[str, int], dict] = {}
         self._closed = False
 
     # ------------------------------------------------------------------ topics
@@ -195,22 +196,22 @@ class EventBus:
         return first
 
     # ------------------------------------------------------------------ zero-copy records
-    # swlog record header in front of every record: [u32 len][u32 crc][i64 ts][u16 key length].
-    REC_HDR = 18
-
-    def append_external(self, name: str, partition: int, owner, ptr: int, total: int, key_len: int = 0,
-                        ts: int | None = None) -> int:
+    def append_external(self, name: str, partition: int, owner, ptr: int, nbytes: int, key_len: int = 0,
+                        ts: int | None = None, on_release=None) -> int:
         """Publish a record whose bytes already sit in caller memory, without copying them.
 
-        ``ptr`` points at ``total`` bytes laid out as [``REC_HDR`` header bytes, filled in here][key
-        (``key_len``)][value].  The log references the memory in place (its own segment), so the
-        buffer must be DMA-able for the consumers that read it in place (pinned host memory for an
-        MI355X consumer).  ``owner`` (the buffer object) is kept alive until retention drops the
-        record; :meth:`reclaim` then hands it back for reuse.  Memory-only partitions only."""
+        ``ptr`` points at ``nbytes`` bytes: the key (``key_len`` bytes, usually none) then the value.
+        The log references them in place, so consumers that read the record in place see that
+        memory (pinned host memory lets an MI355X consumer DMA it straight from the topic).
+        ``owner`` (the object owning the bytes: a pinned tensor, a ``bytes`` object, ...) is kept
+        alive, and must not change, until retention drops the record; then ``on_release(owner)`` is
+        called (a buffer pool takes it back) or, without a callback, the reference is dropped.
+        Memory-only partitions only."""
+        self._drain_released()
         ext = next(self._ext_ids)
         with self._lock:
-            self._ext[ext] = owner
-        first = self.fast.swlog_append_external(self.h, self.topic(name), partition, ptr, int(total), int(key_len),
+            self._ext[ext] = (owner, on_release)
+        first = self.fast.swlog_append_external(self.h, self.topic(name), partition, ptr, int(nbytes), int(key_len),
                                                ts if ts is not None else int(time.time() * 1000), ext)
         if first < 0:
             with self._lock:
@@ -219,6 +220,11 @@ class EventBus:
                                "durable partitions copy their records (use append)")
         self._wake(name)
         return first
+
+    def append_bytes(self, name: str, partition: int, value: bytes, ts: int | None = None) -> int:
+        """Publish an immutable ``bytes`` value by reference (no copy into the log)."""
+        addr = ctypes.cast(ctypes.c_char_p(value), ctypes.c_void_p).value
+        return self.append_external(name, partition, value, addr, len(value), ts=ts)
 
     def view(self, name: str, partition: int, offset: int):
         """(address, length, timestamp) of a retained record's value, read in place, or None.  The
@@ -229,20 +235,61 @@ class EventBus:
             return None
         return ptr.value, n.value, ts.value
 
-    def hold(self, name: str, partition: int, offset: int | None):
-        """Retention keeps every record at or after ``offset`` (None releases the hold)."""
-        self.fast.swlog_hold(self.h, self.topic(name), partition, (1 << 63) - 1 if offset is None else int(offset))
+    def hold(self, name: str, partition: int, offset: int | None, holder=None):
+        """Retention keeps every record at or after ``offset`` (None releases the hold).  Each
+        ``holder`` (e.g. one zero-copy consumer) has its own hold; the partition honours the lowest."""
+        with self._lock:
+            hs = self._holds.setdefault((name, partition), {})
+            if offset is None:
+                hs.pop(holder, None)
+            else:
+                hs[holder] = int(offset)
+            low = min(hs.values()) if hs else (1 << 63) - 1
+            self.fast.swlog_hold(self.h, self.topic(name), partition, low)
 
-    def reclaim(self) -> list:
-        """Owners of zero-copy records that retention has dropped (the log no longer reads them)."""
-        ids = np.zeros(256, np.int64)
+    def _drain_released(self) -> list:
+        """Hand zero-copy records that retention dropped back to their owners' ``on_release``;
+        returns the owners that had none (their references are dropped once the caller lets go)."""
+        ids = self.__dict__.get("_rel_ids")
+        if ids is None:
+            ids = self._rel_ids = np.zeros(256, np.int64)
         out = []
         while True:
-            n = self.lib.swlog_take_released(self.h, ids.ctypes.data, len(ids))
-            with self._lock:
-                out += [self._ext.pop(int(i), None) for i in ids[:n]]
+            n = self.fast.swlog_take_released(self.h, ids.ctypes.data, len(ids))
+            if n:
+                with self._lock:
+                    got = [self._ext.pop(int(i), None) for i in ids[:n]]
+                for e in got:
+                    if e is None:
+                        continue
+                    if e[1] is not None:
+                        e[1](e[0])
+                    else:
+                        out.append(e[0])
             if n < len(ids):
-                return [o for o in out if o is not None]
+                return out
+
+    def reclaim(self) -> list:
+        """Release what retention dropped (see :meth:`append_external`); returns the owners that
+        registered no ``on_release``."""
+        return self._drain_released()
+
+    def read_views(self, name: str, partition: int, offset: int, max_records: int = 500) -> list:
+        """Like :meth:`read` but zero-copy: each record's ``value`` is a read-only memoryview of the
+        log's own memory (keys are not returned).  A view is valid while the record is retained --
+        take a :meth:`hold` at ``offset`` before reading and release it when done."""
+        t = self.topic(name)
+        end = self.fast.swlog_end_offset(self.h, t, partition)
+        out = []
+        ptr, n, ts = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
+        for off in range(max(offset, self.fast.swlog_begin_offset(self.h, t, partition)),
+                         min(end, offset + max_records)):
+            if self.fast.swlog_view(self.h, t, partition, off, ctypes.byref(ptr), ctypes.byref(n), ctypes.byref(ts)):
+                continue
+            mv = memoryview((ctypes.c_uint8 * n.value).from_address(ptr.value)).cast("B").toreadonly() \
+                if n.value else memoryview(b"")
+            out.append(Record(name, partition, off, None, mv, ts.value))
+        return out
 
     # ------------------------------------------------------------------ fetch
     def read(self, name: str, partition: int, offset: int, max_records: int = 500, max_bytes: int = 1 << 20):
@@ -584,9 +631,13 @@ class Consumer:
             if out or time.time() >= deadline:
                 return out
 
-    def poll(self, timeout_ms: int = 1000, max_records: int = 500) -> dict[tuple[str, int], list[Record]]:
+    def poll(self, timeout_ms: int = 1000, max_records: int = 500,
+             views: bool = False) -> dict[tuple[str, int], list[Record]]:
+        """``views=True`` on the in-process bus: record values are zero-copy views of the log
+        (:meth:`EventBus.read_views`); other buses return copies as usual."""
         if not self._local and hasattr(self.bus, "fetch_raw"):
             return self._poll_fetch(timeout_ms, max_records)
+        read = self.bus.read_views if views and hasattr(self.bus, "read_views") else self.bus.read
         deadline = time.time() + timeout_ms / 1000.0
         while True:
             self._ev.clear()
@@ -601,7 +652,7 @@ class Consumer:
             for tp in self._assigned:
                 if budget <= 0:
                     break
-                recs = self.bus.read(tp[0], tp[1], self.positions[tp], budget)
+                recs = read(tp[0], tp[1], self.positions[tp], budget)
                 if recs:
                     out[tp] = recs
                     self.positions[tp] = recs[-1].offset + 1

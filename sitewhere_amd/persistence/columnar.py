@@ -18,12 +18,14 @@ two more copies (0.45 ms per batch on the MI355X tenant path).
 """
 from __future__ import annotations
 
+import ctypes
 import struct
 import threading
 
 import msgpack
 import numpy as np
 
+from .._native import native
 from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC
 from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceEventIndex,
                              DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults)
@@ -39,13 +41,27 @@ _CTX = {DeviceEventIndex.Assignment: 0, DeviceEventIndex.Customer: 2, DeviceEven
 _MAGIC = b"SWC1"
 
 
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = (ctypes.c_void_p, ctypes.c_ssize_t)
+
+
 def encode_batch(boot: str, first_seq: int, world: int, rank: int, now: int, rows: np.ndarray, asg: dict,
                  names: dict, rules: dict | None = None) -> bytes:
     hdr = msgpack.packb({"boot": boot, "first_seq": int(first_seq), "world": int(world), "rank": int(rank),
                          "now": int(now), "asg": {int(k): list(v) for k, v in asg.items()},
                          "names": {int(k): v for k, v in names.items()}, "rules": rules or {}}, use_bin_type=True)
     rows = np.ascontiguousarray(rows, OUT_REC)
-    return b"".join((_MAGIC, struct.pack("<I", len(hdr)), hdr, memoryview(rows).cast("B")))
+    head = b"".join((_MAGIC, struct.pack("<I", len(hdr)), hdr))
+    if rows.nbytes < (1 << 20):
+        return head + memoryview(rows).cast("B")
+    # a fresh (not yet shared) bytes object filled in place: the rows are copied once, over several
+    # threads and without the GIL (one core copied ~7 GB/s: 5 ms per 1M-row batch)
+    out = _new_bytes(None, len(head) + rows.nbytes)
+    base = ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p).value
+    ctypes.memmove(base, head, len(head))
+    native().sw_memcpy_mt(base + len(head), rows.ctypes.data, rows.nbytes, 0)
+    return out
 
 
 def decode_batch(payload: bytes) -> dict:

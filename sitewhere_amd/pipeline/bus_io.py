@@ -11,9 +11,9 @@ through the native commit log (``bus/log.py``) in place:
   the buffer instead of copying it.  The engine's consumer reads the record in place
   (:func:`raw_view`) and the copy engine DMAs the payload bytes and their varint lengths straight
   from the topic to HBM.  A retention hold covers the records whose H2D is still in flight.
-* **enriched rows out.**  :class:`OutboundPublisher` hands the runner a pinned buffer with room for
-  a record header in front (``PipelinedRunner(out_target=...)``); the copy engine writes the step's
-  32-byte rows into it and the buffer is published to the enriched-batch topic as is.  Retention
+* **enriched rows out.**  :class:`OutboundPublisher` hands the runner a pinned buffer
+  (``PipelinedRunner(out_target=...)``); the copy engine writes the step's 32-byte rows into it
+  behind a 64-byte batch header and the buffer is published to the enriched-batch topic as is.  Retention
   returns released buffers to the publisher's pool, so the topic's retention window bounds the
   pinned memory and a lagging reader is the only thing that can make the pool grow.
 
@@ -31,10 +31,10 @@ import ctypes
 import struct
 
 import numpy as np
-import torch
 
 from ..bus.log import EventBus
 from ..models.columnar import OUT_REC
+from .framing import offsets_from_varint, varint_lengths
 
 RAW_MAGIC = b"SWRB"
 OUT_MAGIC = b"SWOB"
@@ -44,10 +44,26 @@ _OUT = struct.Struct("<4sIIIIqq")
 _PAD = 64
 
 
-class RawBatchRecord:
-    """A framed raw batch in pinned host memory, shaped as a commit-log record (no key)."""
+_PINNED = None
 
-    def __init__(self, payload: np.ndarray, lens: np.ndarray, n_msgs: int):
+
+def pinned_available() -> bool:
+    """Pinned (DMA-able) host memory is there when a GPU runtime is (checked once)."""
+    global _PINNED
+    if _PINNED is None:
+        try:
+            import torch
+            _PINNED = bool(torch.cuda.is_available())
+        except Exception:  # noqa: BLE001
+            _PINNED = False
+    return _PINNED
+
+
+class RawBatchRecord:
+    """A framed raw batch: the value of one raw-payload topic record, in pinned host memory when
+    ``pinned`` (torch's caching host allocator, so steady-state batches reuse pinned blocks)."""
+
+    def __init__(self, payload: np.ndarray, lens: np.ndarray, n_msgs: int, pinned: bool = True):
         payload = np.ascontiguousarray(payload, np.uint8)
         lens = np.ascontiguousarray(lens, np.uint8)
         self.n_msgs = int(n_msgs)
@@ -55,25 +71,81 @@ class RawBatchRecord:
         p_off = VALUE_HDR
         l_off = p_off + self.payload_bytes + _PAD
         self.value_len = l_off + int(lens.size)
-        self.total = EventBus.REC_HDR + self.value_len
-        self.buf = torch.zeros(self.total, dtype=torch.uint8).pin_memory()
-        a = self.buf.numpy()
-        v = EventBus.REC_HDR
-        a[v:v + VALUE_HDR] = np.frombuffer(_RAW.pack(RAW_MAGIC, 1, self.n_msgs, self.payload_bytes, p_off,
-                                                     int(lens.size), l_off).ljust(VALUE_HDR, b"\0"), np.uint8)
-        a[v + p_off:v + p_off + self.payload_bytes] = payload
-        a[v + l_off:v + l_off + lens.size] = lens
-        self.ptr = self.buf.data_ptr()
+        if pinned:
+            import torch
+            self.buf = torch.empty(self.value_len, dtype=torch.uint8, pin_memory=True)
+            a = self.buf.numpy()
+            self.ptr = self.buf.data_ptr()
+        else:
+            self.buf = a = np.empty(self.value_len, np.uint8)
+            self.ptr = a.ctypes.data
+        a[:VALUE_HDR] = np.frombuffer(_RAW.pack(RAW_MAGIC, 1, self.n_msgs, self.payload_bytes, p_off,
+                                                int(lens.size), l_off).ljust(VALUE_HDR, b"\0"), np.uint8)
+        a[p_off:p_off + self.payload_bytes] = payload
+        a[p_off + self.payload_bytes:l_off] = 0
+        a[l_off:l_off + lens.size] = lens
+
+    @classmethod
+    def from_payloads(cls, payloads: list, pinned: bool | None = None) -> "RawBatchRecord":
+        lens = np.fromiter(map(len, payloads), np.int64, len(payloads))
+        offs = np.zeros(len(payloads) + 1, np.int64)
+        np.cumsum(lens, out=offs[1:])
+        return cls(np.frombuffer(b"".join(payloads), np.uint8), varint_lengths(offs), len(payloads),
+                   pinned_available() if pinned is None else pinned)
+
+    def value(self) -> bytes:
+        """The record value as bytes (a copy: for buses that cannot publish in place)."""
+        return ctypes.string_at(self.ptr, self.value_len)
 
     def publish(self, bus: EventBus, topic: str, partition: int = 0, ts: int | None = None) -> int:
-        return bus.append_external(topic, partition, self, self.ptr, self.total, ts=ts)
+        return bus.append_external(topic, partition, self, self.ptr, self.value_len, ts=ts)
 
 
-def _host_tensor(addr: int, n: int) -> torch.Tensor:
+class RawBatch:
+    """A raw batch read from a record value (bytes, or a zero-copy view of the topic): payload bytes
+    (with 64 bytes of padding), varint lengths or u32 offsets."""
+    __slots__ = ("n_msgs", "payload_bytes", "payload", "lens", "_offs")
+
+    def __init__(self, n_msgs, payload_bytes, payload, lens=None, offs=None):
+        self.n_msgs, self.payload_bytes, self.payload, self.lens, self._offs = \
+            n_msgs, payload_bytes, payload, lens, offs
+
+    def offsets(self) -> np.ndarray:
+        if self._offs is None:
+            self._offs = offsets_from_varint(self.lens)
+        return self._offs
+
+    def copy(self) -> "RawBatch":
+        """Detached copy (the record's memory may be released once the step is done)."""
+        return RawBatch(self.n_msgs, self.payload_bytes, np.array(self.payload), None, self.offsets().copy())
+
+
+def parse_raw_batch(value) -> RawBatch:
+    """A raw-payload record value: the framed ``SWRB`` form, or the legacy ``u32 n, u32 lengths[n],
+    bytes`` form (records written by older event sources / remote producers)."""
+    mv = memoryview(value).cast("B")
+    if len(mv) >= _RAW.size and bytes(mv[:4]) == RAW_MAGIC:
+        magic, ver, n, pb, poff, lb, loff = _RAW.unpack_from(mv, 0)
+        if ver != 1 or loff + lb > len(mv) or poff + pb + _PAD > loff:
+            raise ValueError("corrupt raw batch record")
+        a = np.frombuffer(mv, np.uint8)
+        return RawBatch(n, pb, a[poff:poff + pb + _PAD], lens=a[loff:loff + lb])
+    (n,) = struct.unpack_from("<I", mv, 0)
+    lens = np.frombuffer(mv, np.uint32, n, 4)
+    offs = np.zeros(n + 1, np.uint32)
+    np.cumsum(lens, out=offs[1:])
+    start = 4 + 4 * n
+    raw = np.zeros(int(offs[-1]) + _PAD, np.uint8)
+    raw[:offs[-1]] = np.frombuffer(mv, np.uint8, int(offs[-1]), start)
+    return RawBatch(n, int(offs[-1]), raw, offs=offs)
+
+
+def _host_tensor(addr: int, n: int):
+    import torch
     return torch.frombuffer((ctypes.c_uint8 * n).from_address(addr), dtype=torch.uint8)
 
 
-def raw_view(view) -> tuple[torch.Tensor, torch.Tensor, int, int]:
+def raw_view(view):
     """(payload incl. padding, varint lengths, n_msgs, payload bytes) of a raw-batch record read in
     place -- CPU tensors over the topic's own (pinned) memory, ready for a non-blocking H2D."""
     addr, vlen, _ = view
@@ -100,7 +172,7 @@ class OutboundPublisher:
         self._HostBuffer = HostBuffer
         self.bus, self.topic, self.lib, self.partition = bus, topic, lib, partition
         self.rank, self.world = rank, world
-        self.nbytes = EventBus.REC_HDR + VALUE_HDR + row_capacity * OUT_REC.itemsize
+        self.nbytes = VALUE_HDR + row_capacity * OUT_REC.itemsize
         self.max_buffers = max_buffers
         self.free: list[_OutBuf] = []
         self.n_alloc = 0
@@ -114,9 +186,7 @@ class OutboundPublisher:
 
     def _acquire(self) -> _OutBuf:
         if not self.free:
-            for o in self.bus.reclaim():
-                if isinstance(o, _OutBuf):
-                    self.free.append(o)
+            self.bus.reclaim()              # released row buffers come back through on_release
         if self.free:
             return self.free.pop()
         if self.n_alloc >= self.max_buffers:
@@ -127,17 +197,18 @@ class OutboundPublisher:
 
     def target(self, nbytes: int):
         """Runner hook: (address the rows are copied to, token)."""
-        if EventBus.REC_HDR + VALUE_HDR + nbytes > self.nbytes:
+        if VALUE_HDR + nbytes > self.nbytes:
             raise ValueError(f"{nbytes} row bytes exceed the outbound buffer ({self.nbytes})")
         ob = self._acquire()
-        return ob.host + EventBus.REC_HDR + VALUE_HDR, ob
+        return ob.host + VALUE_HDR, ob
 
     def publish(self, ob: _OutBuf, n_rows: int):
         """Runner hook: the rows are in ``ob``; write the value header and publish the record."""
         hdr = _OUT.pack(OUT_MAGIC, 1, int(n_rows), self.rank, self.world, self.step, int(self.now_ms))
-        ctypes.memmove(ob.host + EventBus.REC_HDR, hdr, len(hdr))
-        total = EventBus.REC_HDR + VALUE_HDR + int(n_rows) * OUT_REC.itemsize
-        self.bus.append_external(self.topic, self.partition, ob, ob.host, total, ts=int(self.now_ms) or None)
+        ctypes.memmove(ob.host, hdr, len(hdr))
+        total = VALUE_HDR + int(n_rows) * OUT_REC.itemsize
+        self.bus.append_external(self.topic, self.partition, ob, ob.host, total, ts=int(self.now_ms) or None,
+                                 on_release=self.free.append)
         self.step += 1
         self.published += 1
         self.rows += int(n_rows)

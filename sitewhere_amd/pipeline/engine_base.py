@@ -234,6 +234,12 @@ class EngineBase:
             return True
         return False
 
+    def step_framed(self, batch, now_ms: int, presence: bool | None = None) -> StepResult:
+        """Step a :class:`~sitewhere_amd.pipeline.bus_io.RawBatch` (a raw-payload record read from the
+        bus, possibly in place).  Host engines rebuild the offsets; the MI355X engine overrides this
+        to DMA the payload and its varint lengths straight from the record."""
+        return self.step(np.asarray(batch.payload)[:batch.payload_bytes], batch.offsets(), now_ms, presence=presence)
+
     # ------------------------------------------------------------------ hot-store queries
     def query_store(self, event_type: int, asg_idx, start: int | None = None, end: int | None = None,
                     page_number: int = 1, page_size: int = 100):

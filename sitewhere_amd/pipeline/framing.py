@@ -33,16 +33,19 @@ def varint_lengths(offs: np.ndarray) -> np.ndarray:
 
 
 def offsets_from_varint(stream: np.ndarray) -> np.ndarray:
-    """Inverse of :func:`varint_lengths` (CPU reference of the GPU framing kernels)."""
+    """Inverse of :func:`varint_lengths` (CPU reference of the GPU framing kernels), vectorised:
+    a byte without the continuation bit ends a length; each byte contributes its low 7 bits shifted
+    by 7 x its position inside its length."""
     b = np.asarray(stream, np.uint8)
-    lens, v, shift = [], 0, 0
-    for x in b.tolist():
-        v |= (x & 0x7F) << shift
-        if x & 0x80:
-            shift += 7
-        else:
-            lens.append(v)
-            v, shift = 0, 0
-    offs = np.zeros(len(lens) + 1, np.int64)
-    np.cumsum(lens, out=offs[1:])
+    end = (b & 0x80) == 0
+    n = int(end.sum())
+    offs = np.zeros(n + 1, np.int64)
+    if n:
+        grp = np.zeros(len(b), np.int64)
+        np.cumsum(end[:-1], out=grp[1:])                   # length index of every byte
+        first = np.zeros(n, np.int64)
+        first[1:] = np.nonzero(end)[0][:-1] + 1            # first byte of every length
+        shift = 7 * (np.arange(len(b), dtype=np.int64) - first[grp])
+        vals = (b & 0x7F).astype(np.int64) << shift
+        np.cumsum(np.bincount(grp, weights=vals, minlength=n).astype(np.int64), out=offs[1:])
     return offs.astype(np.uint32)

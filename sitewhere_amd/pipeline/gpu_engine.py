@@ -470,6 +470,41 @@ class GpuInboundEngine(EngineBase):
             torch.cuda.synchronize(self.device)
             return self.collect(sel, raw, from_device=True)
 
+    def step_framed(self, batch, now_ms: int, presence: bool | None = None) -> StepResult:
+        """Synchronous step of a raw-payload record read from the bus: the payload (with its padding)
+        and the varint lengths are DMA'd straight from the record -- in place when the record is a
+        pinned zero-copy record of the topic, no host staging copy -- and the offsets are rebuilt on
+        the GPU (``sw_frame_varint``)."""
+        if batch.lens is None:
+            return EngineBase.step_framed(self, batch, now_ms, presence)
+        import warnings
+        n, nb, nl = batch.n_msgs, len(batch.payload), len(batch.lens)
+        if n > self.cfg.max_msgs:
+            raise ValueError(f"batch of {n} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
+        if nb < batch.payload_bytes + _ALIGN:
+            raise ValueError("raw batch payload lacks its tail padding")
+        with self._lock:
+            st = getattr(self, "_stg_framed", None)
+            if st is None or st[0].numel() < nb or st[1].numel() < nl:
+                st = self._stg_framed = (
+                    torch.empty(max(nb, int(getattr(self, "_stg_hint", 0))), dtype=torch.uint8, device=self.device),
+                    torch.empty(max(nl, 5 * self.cfg.max_msgs + 64), dtype=torch.uint8, device=self.device),
+                    torch.empty(self.cfg.max_msgs + 1, dtype=torch.int32, device=self.device))
+            dev_r, dev_l, dev_o = st
+            with warnings.catch_warnings():       # read-only topic views: torch only reads them here
+                warnings.simplefilter("ignore", UserWarning)
+                pt = torch.frombuffer(batch.payload, dtype=torch.uint8) if nb else None
+                lt = torch.frombuffer(batch.lens, dtype=torch.uint8) if nl else None
+            if pt is not None:
+                dev_r[:nb].copy_(pt, non_blocking=True)
+            if lt is not None:
+                dev_l[:nl].copy_(lt, non_blocking=True)
+            self.frame_varint(dev_l, nl, n, dev_o, batch.payload_bytes)
+            do_presence = self.presence_due(now_ms) if presence is None else presence
+            sel = self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_to_device=True)
+            torch.cuda.synchronize(self.device)
+            return self.collect(sel, np.asarray(batch.payload), from_device=True)
+
     def _stage(self, raw: np.ndarray, offs: np.ndarray):
         """H2D of a host batch through persistent pinned staging (a pageable ``.to(device)`` ran at
         ~6 GB/s plus a fresh padded copy per batch).  Only for the synchronous :meth:`step`: the

@@ -38,7 +38,8 @@ class BusConsumer(TenantEngineLifecycleComponent):
     component_type = LifecycleComponentType.Other
 
     def __init__(self, engine, name: str, topics: list[str], handler, threads: int = 0, max_records: int = 500,
-                 group: str | None = None, auto_commit: bool = True, max_attempts=_DEFAULT, idle=None):
+                 group: str | None = None, auto_commit: bool = True, max_attempts=_DEFAULT, idle=None,
+                 views: bool = False):
         super().__init__(name)
         self.tenant_engine = engine
         self.engine = engine
@@ -65,6 +66,9 @@ class BusConsumer(TenantEngineLifecycleComponent):
         # called on the poll thread when a poll returns nothing; may raise RetryFrom (a failure that
         # surfaced after its batch was handed off, e.g. on a store thread, with no new records due)
         self.idle = idle
+        # zero-copy: on the in-process bus the handler gets memoryviews of the log itself, valid
+        # until it returns (a retention hold covers the partition's batch meanwhile)
+        self.views = views
 
     def start(self, monitor):
         bus = self.engine.ms.instance.bus
@@ -112,14 +116,24 @@ class BusConsumer(TenantEngineLifecycleComponent):
 
     def _run(self):
         backoff, attempts = 0.05, {}
+        bus = self.engine.ms.instance.bus
+        views = self.views and hasattr(bus, "read_views") and hasattr(bus, "hold")
         while not self._stop.is_set():
             try:
-                batch = self.consumer.poll(100, self.max_records)
+                if views:
+                    for tp in self.consumer.assignment():       # hold before reading in place
+                        bus.hold(tp[0], tp[1], self.consumer.positions.get(tp, 0), holder=self)
+                    batch = self.consumer.poll(100, self.max_records, views=True)
+                else:
+                    batch = self.consumer.poll(100, self.max_records)
             except Exception:
                 self.logger.exception("poll failed")
                 time.sleep(0.1)
                 continue
             if not batch:
+                if views:
+                    for tp in self.consumer.assignment():
+                        bus.hold(tp[0], tp[1], None, holder=self)
                 if self.idle is not None:
                     try:
                         self.idle()
@@ -180,6 +194,9 @@ class BusConsumer(TenantEngineLifecycleComponent):
                 self.consumer.seek(tp[0], tp[1], pos)           # re-read it: at-least-once
             if rewind:
                 self.rewinds += 1
+            if views:
+                for tp in self.consumer.assignment():
+                    bus.hold(tp[0], tp[1], None, holder=self)    # the handler is done with the views
             if self.auto_commit:
                 offsets = {tp: pos for tp, pos in self.consumer.positions.items() if tp not in failed}
                 if offsets:

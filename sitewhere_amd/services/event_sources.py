@@ -327,14 +327,20 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
                 self.flush_raw()
 
     def flush_raw(self):
-        """Ship the buffered raw payloads as one batch record: u32 count, u32 lengths[], bytes."""
-        import struct
+        """Ship the buffered raw payloads as one framed batch record (``pipeline/bus_io.py``).  On
+        the in-process bus the record is published in place: its bytes sit in pinned host memory
+        when a GPU is present, so the MI355X engine DMAs the batch straight out of the topic."""
+        from ..pipeline.bus_io import RawBatchRecord
         with self._raw_lock:
             buf, self._raw_buf = self._raw_buf, []
         if not buf:
             return
-        head = struct.pack(f"<I{len(buf)}I", len(buf), *[len(b) for b in buf])
-        self.producer.send(self.t_raw, None, head + b"".join(buf))
+        bus = self.engine.ms.instance.bus
+        if hasattr(bus, "append_external"):
+            rec = RawBatchRecord.from_payloads(buf)
+            bus.append_external(self.t_raw, bus.partition_for(self.t_raw, None), rec, rec.ptr, rec.value_len)
+        else:
+            self.producer.send(self.t_raw, None, RawBatchRecord.from_payloads(buf, pinned=False).value())
 
 
 class EventSourcesTenantEngine(MicroserviceTenantEngine):

@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import json
 import queue
-import struct
 import threading
 import time
 
@@ -36,9 +35,10 @@ from ..models.domain import (AlertLevel, AlertSource, DeviceAlert, DeviceAssignm
                              DeviceMeasurement, DeviceStateChange, now_ms)
 from ..pipeline.config import EngineConfig
 from ..pipeline.engine_base import Zone, ZoneTest
+from ..pipeline.bus_io import RawBatch, parse_raw_batch
 from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
-from ..utils import IndexMap
+from ..utils import IndexMap, retain_large_allocations
 from ..runtime.consumers import BusConsumer, RetryFrom
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
 from .inbound_processing import InboundProcessingTenantEngine
@@ -48,23 +48,18 @@ ENRICHED_BATCHES = "inbound-enriched-batches"     # columnar enriched output (pu
 
 
 def unpack_raw_batch(value: bytes):
-    """Inverse of ``EventSourcesManager.flush_raw``: -> (raw uint8, offs uint32[n+1])."""
-    n = struct.unpack_from("<I", value, 0)[0]
-    lens = np.frombuffer(value, np.uint32, n, 4)
-    offs = np.zeros(n + 1, np.uint32)
-    np.cumsum(lens, out=offs[1:])
-    start = 4 + 4 * n
-    raw = np.zeros(int(offs[-1]) + 64, np.uint8)
-    raw[:offs[-1]] = np.frombuffer(value, np.uint8, int(offs[-1]), start)
-    return raw, offs
+    """A raw-payload record value -> (raw uint8 with 64 bytes of padding, offs uint32[n+1])."""
+    rb = parse_raw_batch(value)
+    return np.array(rb.payload), rb.offsets()
 
 
 class _Stepped:
-    """A raw batch the engine has stepped, with the storage stages it has completed."""
-    __slots__ = ("key", "res", "now", "raw", "offs", "stored", "published", "routed", "queued", "payload", "events")
+    """A raw batch the engine has stepped, with the storage stages it has completed.  ``batch`` (the
+    raw bytes, for the host slow path) is kept only when the step rejected messages."""
+    __slots__ = ("key", "res", "now", "batch", "stored", "published", "routed", "queued", "payload", "events")
 
-    def __init__(self, key, res, now, raw, offs):
-        self.key, self.res, self.now, self.raw, self.offs = key, res, now, raw, offs
+    def __init__(self, key, res, now, batch):
+        self.key, self.res, self.now, self.batch = key, res, now, batch
         self.stored = self.published = self.routed = self.queued = False
         self.payload = self.events = None
 
@@ -87,12 +82,15 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.publish = cfg.get("publishEnriched", "events")     # events | batches | none
         self._asg_dirty: set[int] = set()
         self._names_sent = 0
+        self._names_known = -1
         ecfg = EngineConfig.small(**{k: int(v) for k, v in cfg.get("capacity", {}).items()}) \
             if cfg.get("sizing", "small") == "small" else EngineConfig(**cfg.get("capacity", {}))
         ecfg.presence_missing_ms = int(cfg.get("presenceMissingMs", ecfg.presence_missing_ms))
         ecfg.presence_check_ms = int(cfg.get("presenceCheckMs", ecfg.presence_check_ms))
         self.engine_cfg = ecfg
         self.engine = self._make_engine(cfg.get("device", "auto"), ecfg)
+        if self.storage == "columnar" and cfg.get("retainHostAllocations", True):
+            retain_large_allocations()          # multi-MB columnar batches per step: no fresh mmaps
         self.dev_index, self.asg_index = IndexMap(), IndexMap()
         self.customers, self.areas, self.assets = IndexMap(), IndexMap(), IndexMap()
         self._asg_entities: dict[int, object] = {}
@@ -132,7 +130,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # never dead-lettered: a stepped batch cannot be re-stepped, only its storage retried
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
                                         self._process_raw, max_records=16, max_attempts=None,
-                                        idle=self._raise_store_error,
+                                        idle=self._raise_store_error, views=True,
                                         auto_commit=self.ckpt_path is None and not self.async_store)
         self.persisted_events = self.create_meter("persistedEvents")
         self.step_timer = self.create_timer("engineStep")
@@ -305,9 +303,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             commit = (r.topic, r.partition, r.offset + 1) if self.async_store and not self.ckpt_path else None
             item = self._stepped.get(key)
             if item is None:
-                raw, offs = unpack_raw_batch(r.value)
-                # the record timestamp is the batch's receive time: replay after a restore is deterministic
-                self.process_batch(raw, offs, now=r.timestamp or None, commit=commit, key=key)
+                # r.value is a zero-copy view of the topic on the in-process bus: a pinned raw-batch
+                # record is DMA'd to the MI355X in place.  The record timestamp is the batch's receive
+                # time, so replay after a restore is deterministic.
+                self.process_raw_batch(parse_raw_batch(r.value), now=r.timestamp or None, commit=commit,
+                                       key=key, detach=isinstance(r.value, memoryview))
             else:
                 self.replayed_batches += 1
                 self._submit(item, commit)
@@ -330,14 +330,23 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         raise RetryFrom(rewind, err)
 
     def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None, commit=None, key=None):
+        """One engine step over host arrays (raw payload bytes, u32 offsets); see :meth:`process_raw_batch`."""
+        return self.process_raw_batch(RawBatch(len(offs) - 1, int(offs[-1]), raw, offs=offs), now, commit, key)
+
+    def process_raw_batch(self, batch: RawBatch, now: int | None = None, commit=None, key=None, detach=False):
         """One engine step; storing its rows happens here or, with ``asyncStore``, on the store thread
         while the next step runs (call :meth:`flush` to wait for it).  ``key`` = (topic, partition,
-        offset) of the raw record: the result is then kept until stored (see ``_stepped``)."""
+        offset) of the raw record: the result is then kept until stored (see ``_stepped``).
+        ``detach``: ``batch`` views memory that is released after this call (a topic record read in
+        place), so the bytes the slow path needs are copied."""
         now = now or now_ms()
         with self._lock, self.step_timer.time():
-            res = self.engine.step(raw, offs, now)
+            res = self.engine.step_framed(batch, now)
         self.processed_events.mark(res.n_events)
-        item = _Stepped(key, res, now, raw, offs)
+        keep = None
+        if res.rejects is not None and len(res.rejects):
+            keep = batch.copy() if detach else batch
+        item = _Stepped(key, res, now, keep)
         if key is not None:
             self._stepped[key] = item
         self._submit(item, commit)
@@ -371,13 +380,18 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if not item.published:
             with self.publish_timer.time():
                 if self.storage == "columnar" and self.publish == "batches":
-                    self.ms.producer.send(self.t_enriched_batches, None, item.payload)
+                    bus = self.ms.instance.bus
+                    if hasattr(bus, "append_bytes"):   # in place: the log references the payload
+                        bus.append_bytes(self.t_enriched_batches, bus.partition_for(self.t_enriched_batches, None),
+                                         item.payload, ts=now)
+                    else:
+                        self.ms.producer.send(self.t_enriched_batches, None, item.payload)
                 elif self.publish == "events":
                     self._publish_events(item.events if item.events is not None else self._to_events(res, now))
             item.published = True
         if not item.routed:
             if res.rejects is not None and len(res.rejects):
-                self._slow_path(item.raw, item.offs, res)
+                self._slow_path(np.asarray(item.batch.payload), item.batch.offsets(), res)
             item.routed = True
         if item.key is not None:
             t, p, o = item.key
@@ -417,10 +431,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 if a is not None:
                     asg[ai] = [a.id, a.device_id, a.customer_id, a.area_id, a.asset_id]
             self._asg_dirty.clear()
-            if res.out is not None and len(res.out):
-                ids = set(np.unique(res.out["name_id"]).tolist()) - {NO_NAME}
-                if ids - self._nid2name.keys():
-                    self._reload_names()
+            # the engine's host name dictionary grows when a step learns names or rules add alert
+            # types (an np.unique over the rows' name ids cost ~10 ms per 1M-row batch)
+            if len(self.engine.names) != self._names_known:
+                self._names_known = len(self.engine.names)
+                self._reload_names()
             names = dict(self._nid2name) if len(self._nid2name) != self._names_sent else {}
             self._names_sent = len(self._nid2name)
         rules = {t.alert_type: t.alert_message for t in self.engine.tests}

@@ -72,3 +72,26 @@ class Stopwatch:
         self.s = time.perf_counter() - self.t0
         self.ms = 1000.0 * self.s
         return False
+
+
+_MALLOC_TUNED = False
+
+
+def retain_large_allocations() -> bool:
+    """Keep multi-MB host allocations in the heap instead of fresh mmaps (glibc ``mallopt``).
+
+    An engine tenant builds one tens-of-MB columnar batch per step; with glibc's default dynamic
+    mmap threshold each one is a fresh mapping whose first touch page-faults at 1-2 GB/s in a
+    container (4.3 ms per 37 MB batch measured, 1.5-2.7 ms once the heap keeps and reuses the
+    memory).  Process-wide and idempotent; ``SW_MALLOC_RETAIN=0`` disables it."""
+    global _MALLOC_TUNED
+    if _MALLOC_TUNED or os.environ.get("SW_MALLOC_RETAIN", "1") == "0":
+        return _MALLOC_TUNED
+    try:
+        import ctypes
+        libc = ctypes.CDLL("libc.so.6")
+        m_trim_threshold, m_mmap_threshold = -1, -3
+        _MALLOC_TUNED = bool(libc.mallopt(m_mmap_threshold, 1 << 30)) and bool(libc.mallopt(m_trim_threshold, 1 << 31))
+    except (OSError, AttributeError):
+        _MALLOC_TUNED = False
+    return _MALLOC_TUNED

@@ -11,14 +11,13 @@ import pytest
 
 from sitewhere_amd.bus.log import EventBus
 
-H = EventBus.REC_HDR
+H = 0
 
 
-def _ext(bus, topic, payload: bytes, key: bytes = b""):
-    buf = np.zeros(H + len(key) + len(payload), np.uint8)
-    buf[H:H + len(key)] = np.frombuffer(key, np.uint8) if key else []
-    buf[H + len(key):] = np.frombuffer(payload, np.uint8)
-    off = bus.append_external(topic, 0, buf, buf.ctypes.data, buf.nbytes, key_len=len(key), ts=123)
+def _ext(bus, topic, payload: bytes, key: bytes = b"", released=None):
+    buf = np.frombuffer(key + payload, np.uint8).copy()
+    off = bus.append_external(topic, 0, buf, buf.ctypes.data, buf.nbytes, key_len=len(key), ts=123,
+                              on_release=None if released is None else released.append)
     return buf, off
 
 
@@ -42,17 +41,51 @@ def test_retention_releases_external_buffers_and_hold_defers_it():
     bus = EventBus(default_partitions=1)
     bus.topic("r")
     bus.set_retention("r", 1)                               # keep as little as possible
-    bufs = [_ext(bus, "r", bytes([i]) * 1000)[0] for i in range(2)]
+    rel = []
+    bufs = [_ext(bus, "r", bytes([i]) * 1000, released=rel)[0] for i in range(2)]
     bus.hold("r", 0, 2)                                     # a consumer has records >= 2 in flight
-    b2, off2 = _ext(bus, "r", b"x" * 1000)
-    b3, off3 = _ext(bus, "r", b"y" * 1000)
-    got = bus.reclaim()
-    assert [id(o) for o in got] == [id(bufs[1]), id(bufs[0])] or {id(o) for o in got} == {id(b) for b in bufs}
+    b2, off2 = _ext(bus, "r", b"x" * 1000, released=rel)
+    b3, off3 = _ext(bus, "r", b"y" * 1000, released=rel)
+    bus.reclaim()
+    assert {id(o) for o in rel} == {id(b) for b in bufs}    # handed back to their pool
     assert bus.begin_offset("r", 0) == 2 and bus.view("r", 0, off2) is not None
     bus.hold("r", 0, None)                                  # released: retention catches up
-    assert {id(o) for o in bus.reclaim()} == {id(b2)}
+    bus.reclaim()
+    assert {id(o) for o in rel[2:]} == {id(b2)}
     assert bus.begin_offset("r", 0) == off3
     assert bus.read("r", 0, off3)[0].value == b"y" * 1000
+    # owners without a pool are dropped by the log once released
+    import weakref
+    tmp = np.frombuffer(b"z" * 100, np.uint8).copy()
+    ref = weakref.ref(tmp)
+    bus.append_external("r", 0, tmp, tmp.ctypes.data, tmp.nbytes)
+    del tmp
+    _ext(bus, "r", b"w" * 1000)                             # pushes the previous record out
+    bus.reclaim()
+    assert ref() is None
+
+
+def test_zero_copy_views_through_a_consumer():
+    bus = EventBus(default_partitions=1)
+    vals = [bytes([65 + i]) * (10 + i) for i in range(5)]
+    keep = [_ext(bus, "v", v)[0] for v in vals]
+    bus.append("v", 0, [(b"k", b"copied")])
+    c = bus.consumer("g", ["v"])
+    got = c.poll(100, views=True)[("v", 0)]
+    assert [bytes(r.value) for r in got] == vals + [b"copied"]
+    assert isinstance(got[0].value, memoryview) and got[0].value.readonly
+    assert np.frombuffer(got[0].value, np.uint8).ctypes.data == keep[0].ctypes.data
+
+
+def test_bytes_values_are_published_by_reference():
+    bus = EventBus(default_partitions=1)
+    v = b"immutable-columnar-batch" * 100
+    off = bus.append_bytes("b", 0, v, ts=7)
+    ptr, n, ts = bus.view("b", 0, off)
+    import ctypes
+    assert n == len(v) and ts == 7 and ctypes.string_at(ptr, n) == v
+    assert ptr == ctypes.cast(ctypes.c_char_p(v), ctypes.c_void_p).value     # the bytes object itself
+    assert bus.read("b", 0, off)[0].value == v
 
 
 def test_durable_partitions_refuse_zero_copy(tmp_path):

@@ -36,7 +36,7 @@ def test_engine_consumes_and_publishes_topics_in_place():
         off = rec.publish(bus, "raw", ts=NOW + k)
         payload, lens, n, pb = raw_view(bus.view("raw", 0, off))
         assert payload.is_pinned() and n == len(offs) - 1 and pb == int(offs[-1])
-        assert payload.data_ptr() == rec.ptr + EventBus.REC_HDR + 64         # read in place, not copied
+        assert payload.data_ptr() == rec.ptr + 64         # read in place, not copied
         runner.submit(payload, None, n, now_ms=NOW + k, lens_host=lens, raw_bytes=pb)
         r = c.step(raw, offs, NOW + k, presence=False)
         cpu_rows.append(r.out)
