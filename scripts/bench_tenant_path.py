@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--via-bus", action="store_true",
                     help="publish the batches to the tenant's raw-payload topic (zero-copy pinned records, as "
                          "event sources do) and time until the raw consumer has stored and committed them all")
+    ap.add_argument("--store-retention", type=int, default=0,
+                    help="rows the columnar event store holds (0 = the template's); older batches are evicted "
+                         "and their memory reused -- a store that only grows page-faults fresh memory per batch")
     args = ap.parse_args()
     import logging
     logging.basicConfig(level=logging.ERROR)
@@ -52,6 +55,12 @@ def main():
         sw.instance.coord.put(ms.tenant_config_path("fast"), dump_document(cfg))
         while ms.get_tenant_engine("fast") in (None, before) or ms.get_tenant_engine("fast").status.value != "Started":
             time.sleep(0.1)
+    if args.store_retention:
+        # the same window on the enriched-batch topic, which references the same batch payloads
+        sw.tenant_engine("event-management", "fast").store.retention_rows = args.store_retention
+        t_out = sw.instance.naming.tenant_prefix("fast") + "inbound-enriched-batches"
+        sw.instance.bus.topic(t_out)
+        sw.instance.bus.set_retention(t_out, 32 * args.store_retention)
     run = lambda f: sw.instance.system_user.run(f, "fast")  # noqa: E731
     dm = sw.api("DeviceManagement", "fast")
     t0 = time.time()
@@ -107,15 +116,28 @@ def main():
         ib.flush()
         dt = time.perf_counter() - t
     em_store = sw.tenant_engine("event-management", "fast").store
+    trace = None
+    if ib.trace:                # SW_TENANT_TRACE=1: medians over the second half of the timed batches
+        tr = [t for t in ib.trace if len(t) == 9][-(args.batches // 2):]
+        if tr:
+            import numpy as np
+            d = np.diff(np.asarray(tr), axis=1) * 1000
+            gap = np.diff(np.asarray([t[0] for t in tr])) * 1000
+            trace = {"submit_ms": d[:, 0], "to_complete_ms": d[:, 1], "queue_wait_ms": d[:, 2],
+                     "payload_lock_ms": d[:, 3], "payload_dicts_ms": d[:, 4], "payload_encode_ms": d[:, 5],
+                     "rpc_ms": d[:, 6], "publish_commit_ms": d[:, 7], "submit_interval_ms": gap}
+            trace = {k: round(float(np.median(v)), 3) for k, v in trace.items() if len(v)}
     breakdown = {name: round(t.hist.snapshot()["mean"], 3)
                  for name, t in (("engine_step_ms", ib.step_timer), ("columnar_store_ms", ib.store_timer),
                                  ("publish_ms", ib.publish_timer))}
     print(json.dumps({"metric": "tenant_path_events_per_sec", "engine": ib.engine_kind, "via_bus": args.via_bus,
+                      "overlap_steps": ib.overlap,
                       "events": ev,
                       "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,
                       "ms_per_batch": round(1000 * dt / args.batches, 3), "batch": args.batch,
-                      "devices": args.devices, "store_rows": em_store.rows, "setup_s": round(setup_s, 1),
-                      "mean_ms": breakdown}))
+                      "devices": args.devices, "store_rows": em_store.rows,
+                      "store_retention_rows": em_store.retention_rows, "store_evicted_rows": em_store.evicted_rows, "setup_s": round(setup_s, 1),
+                      "mean_ms": breakdown, **({"median_ms_second_half": trace} if trace else {})}))
     sw.stop()
 
 

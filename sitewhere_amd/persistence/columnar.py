@@ -39,6 +39,7 @@ _CTX = {DeviceEventIndex.Assignment: 0, DeviceEventIndex.Customer: 2, DeviceEven
 
 
 _MAGIC = b"SWC1"
+_COPY_THREADS = int(__import__("os").environ.get("SW_MEMCPY_THREADS", "0"))     # 0: one per 4 MB, <= 16
 
 
 _new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
@@ -60,7 +61,7 @@ def encode_batch(boot: str, first_seq: int, world: int, rank: int, now: int, row
     out = _new_bytes(None, len(head) + rows.nbytes)
     base = ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p).value
     ctypes.memmove(base, head, len(head))
-    native().sw_memcpy_mt(base + len(head), rows.ctypes.data, rows.nbytes, 0)
+    native().sw_memcpy_mt(base + len(head), rows.ctypes.data, rows.nbytes, _COPY_THREADS)
     return out
 
 
@@ -76,7 +77,14 @@ def decode_batch(payload: bytes) -> dict:
 
 
 class ColumnarEventStore(DeviceEventStore):
-    def __init__(self, consolidate_every: int = 64, dense_rows: int = 4096):
+    """``retention_rows`` bounds the rows held (oldest batches are evicted first, whole batches at a
+    time): an MI355X tenant stores ~32 B x 10^8 events/s, so an unbounded in-memory store is a
+    test/bench setting.  Evicted memory goes back to the allocator and is reused by the next
+    batches -- fresh pages cost a page fault and a zeroing each, which halves the store's copy rate
+    (4.8 vs 1.8 ms per 1M-row batch on 8 cores).  Durable history belongs to a persistent event
+    store or to a consumer of the enriched-batch topic."""
+
+    def __init__(self, consolidate_every: int = 64, dense_rows: int = 4096, retention_rows: int | None = None):
         self._objects = MemoryEventStore()
         self._chunks: list[dict] = []
         self._pending: list[dict] = []
@@ -88,7 +96,9 @@ class ColumnarEventStore(DeviceEventStore):
         self._lock = threading.RLock()
         self.consolidate_every = consolidate_every
         self.dense_rows = dense_rows
-        self.rows = 0
+        self.retention_rows = int(retention_rows) if retention_rows else None
+        self.rows = 0               # rows held
+        self.evicted_rows = 0
 
     # ------------------------------------------------------------------ ingest
     def add_columnar(self, payload: bytes | dict) -> int:
@@ -124,7 +134,18 @@ class ColumnarEventStore(DeviceEventStore):
                     if len(self._pending) >= self.consolidate_every:
                         self._consolidate()
                 self.rows += n
+                if self.retention_rows is not None and self.rows > self.retention_rows:
+                    self._evict()
         return n
+
+    def _evict(self):
+        """Drop the oldest whole chunks until the rows held fit ``retention_rows`` (the newest chunk
+        always stays)."""
+        self._consolidate()
+        while len(self._chunks) > 1 and self.rows > self.retention_rows:
+            n = len(self._chunks.pop(0)["rows"])
+            self.rows -= n
+            self.evicted_rows += n
 
     # chunk accessors: dense chunks (scalar metadata) and consolidated small batches (per-row arrays)
     @staticmethod

@@ -705,7 +705,7 @@ def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
         return BucketedEventStore(kw.get("bucket_ms", 3600_000))
     if kind == "columnar":
         from .columnar import ColumnarEventStore
-        return ColumnarEventStore()
+        return ColumnarEventStore(retention_rows=kw.get("retentionRows"))
     if kind in ("mongo", "mongodb"):
         return MongoEventStore(kw.get("uri", "mongodb://localhost:27017"), kw.get("database", "sitewhere"))
     if kind == "influxdb":

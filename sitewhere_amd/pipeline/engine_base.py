@@ -240,6 +240,33 @@ class EngineBase:
         to DMA the payload and its varint lengths straight from the record."""
         return self.step(np.asarray(batch.payload)[:batch.payload_bytes], batch.offsets(), now_ms, presence=presence)
 
+    # ------------------------------------------------------------------ overlapped (lagged) steps
+    # A service tenant feeds batches one at a time from its raw-payload consumer.  On the MI355X the
+    # H2D of batch k overlaps the compute of batch k-1 and the D2H of k-1's rows overlaps the compute
+    # of batch k, so a submitted batch's result comes back on a LATER submission (or on
+    # ``drain_framed``), always in submission order.  Host engines keep a one-deep lag -- they run a
+    # batch when the next arrives -- so callers are written (and tested on CPU) once.  The batch's
+    # memory (a topic record read in place) must stay valid until its result is returned.
+    def submit_framed(self, batch, now_ms: int, token=None, presence: bool | None = None) -> list:
+        """Enqueue one raw batch; returns ``[(token, StepResult)]`` of the submissions completed."""
+        done = self.drain_framed()
+        self._lagged = (batch, now_ms, token, presence)
+        return done
+
+    def drain_framed(self) -> list:
+        """Complete every submitted batch; ``[(token, StepResult)]`` in submission order."""
+        lag = getattr(self, "_lagged", None)
+        if lag is None:
+            return []
+        self._lagged = None
+        batch, now_ms, token, presence = lag
+        return [(token, self.step_framed(batch, now_ms, presence))]
+
+    @property
+    def framed_pending(self) -> int:
+        """Submitted batches whose results have not been returned yet."""
+        return 0 if getattr(self, "_lagged", None) is None else 1
+
     # ------------------------------------------------------------------ hot-store queries
     def query_store(self, event_type: int, asg_idx, start: int | None = None, end: int | None = None,
                     page_number: int = 1, page_size: int = 100):

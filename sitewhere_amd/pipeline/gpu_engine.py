@@ -58,6 +58,47 @@ class HostBuffer:
             pass
 
 
+class _Submitted:
+    """One batch in :meth:`GpuInboundEngine.submit_framed`'s pipeline."""
+    __slots__ = ("slot", "batch", "token", "small", "rows", "sig", "ev")
+
+    def __init__(self, slot, batch, token):
+        self.slot, self.batch, self.token = slot, batch, token
+        self.small = self.rows = self.sig = self.ev = None
+
+
+class _FramedSlots:
+    """Slot state of :meth:`GpuInboundEngine.submit_framed`: device raw / varint-length / offset
+    buffers per slot (grown on demand), the H2D copy stream and its events, and the batches still in
+    flight (oldest first)."""
+    SLOTS = 3
+
+    def __init__(self, e: "GpuInboundEngine"):
+        from collections import deque
+        if e.n_out_bufs < self.SLOTS:
+            raise ValueError(f"overlapped framed steps need {self.SLOTS} outbound buffers")
+        self.e = e
+        self.h2d = torch.cuda.Stream(e.device)
+        self.d2h = torch.cuda.Stream(e.device)      # rows when the SDMA engine is unavailable
+        self.ev_h2d = [torch.cuda.Event() for _ in range(self.SLOTS)]
+        self.ev_comp = [torch.cuda.Event() for _ in range(self.SLOTS)]
+        self.bufs = [None] * self.SLOTS
+        self.inflight = deque()
+        self.k = 0
+        self.no_sdma = False
+
+    def buffers(self, b: int, nb: int, nl: int):
+        e = self.e
+        cur = self.bufs[b]
+        if cur is None or cur[0].numel() < nb or cur[1].numel() < nl:
+            self.ev_comp[b].synchronize()           # the old slot buffers may still be read
+            cur = self.bufs[b] = (
+                torch.empty(max(nb, int(getattr(e, "_stg_hint", 0))), dtype=torch.uint8, device=e.device),
+                torch.empty(max(nl, 5 * e.cfg.max_msgs + 64), dtype=torch.uint8, device=e.device),
+                torch.empty(e.cfg.max_msgs + 1, dtype=torch.int32, device=e.device))
+        return cur
+
+
 class GpuInboundEngine(EngineBase):
     def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", group=None):
         super().__init__(cfg)
@@ -462,6 +503,7 @@ class GpuInboundEngine(EngineBase):
         """Synchronous convenience step (tests, control-plane use): H2D, run, D2H, learn names."""
         n_msgs = len(offs) - 1
         with self._lock:            # serialised against hot-store queries (cursor + shared scratch)
+            self._no_framed_pending()
             raw_dev, off_dev = self._stage(raw, offs)
             do_presence = self.presence_due(now_ms) if presence is None else presence
             # rows land in HBM and come back in one DMA: reading them out of the mapped host buffer
@@ -484,6 +526,7 @@ class GpuInboundEngine(EngineBase):
         if nb < batch.payload_bytes + _ALIGN:
             raise ValueError("raw batch payload lacks its tail padding")
         with self._lock:
+            self._no_framed_pending()
             st = getattr(self, "_stg_framed", None)
             if st is None or st[0].numel() < nb or st[1].numel() < nl:
                 st = self._stg_framed = (
@@ -504,6 +547,11 @@ class GpuInboundEngine(EngineBase):
             sel = self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_to_device=True)
             torch.cuda.synchronize(self.device)
             return self.collect(sel, np.asarray(batch.payload), from_device=True)
+
+    def _no_framed_pending(self):
+        fp = self.__dict__.get("_fp")
+        if fp is not None and fp.inflight:
+            raise RuntimeError("a submitted framed batch is pending: drain_framed() before a synchronous step")
 
     def _stage(self, raw: np.ndarray, offs: np.ndarray):
         """H2D of a host batch through persistent pinned staging (a pageable ``.to(device)`` ran at
@@ -537,18 +585,13 @@ class GpuInboundEngine(EngineBase):
                 return pin, arr
         pin = torch.empty(max(nbytes, self.out_cap * OUT_REC_SIZE), dtype=torch.uint8).pin_memory()
         arr = pin.numpy()
-        if len(pool) < 4:
+        if len(pool) < 8:       # results held by an overlapped tenant: in flight + store queue + storing
             pool.append((pin, arr))
         return pin, arr
 
     def collect(self, sel: int, raw_host: np.ndarray | None, from_device: bool = False) -> StepResult:
-        sc = self.scalars()
-        nn = min(sc["n_new_names"], self.cfg.names_cap)
-        new = {}
-        if nn and raw_host is not None:
-            refs = self.t["new_names"][:nn * NAME_REF.itemsize].cpu().numpy().view(NAME_REF)
-            new = self.learn_names(refs, raw_host)
-        n_out = sc["n_out"]
+        part = self._collect_small(raw_host)
+        n_out = part["n_persisted"]
         if from_device:
             nb = n_out * OUT_REC_SIZE
             pin, arr = self._pinned_out(nb)
@@ -557,6 +600,18 @@ class GpuInboundEngine(EngineBase):
             out = arr[:nb].view(OUT_REC)
         else:
             out = self.out_host[sel].view(OUT_REC, n_out).copy()
+        return StepResult(out=out, world=self.world, rank=self.rank, **part)
+
+    def _collect_small(self, raw_host: np.ndarray | None) -> dict:
+        """Everything of the last step but its rows: counts, learned names, first store sequence and
+        rejected records.  Reads tables the next step overwrites, so it runs before that step is
+        enqueued."""
+        sc = self.scalars()
+        nn = min(sc["n_new_names"], self.cfg.names_cap)
+        new = {}
+        if nn and raw_host is not None:
+            refs = self.t["new_names"][:nn * NAME_REF.itemsize].cpu().numpy().view(NAME_REF)
+            new = self.learn_names(refs, raw_host)
         first_seq = int(self.t["cursor"][1].item())
         n_rej = sc["n_rej"]
         if n_rej:
@@ -566,9 +621,120 @@ class GpuInboundEngine(EngineBase):
             rst = self.t["status"][rej_idx].cpu().numpy()
         else:
             rows, rst = np.zeros(0, EVENT_REC), np.zeros(0, np.uint8)
-        return StepResult(n_msgs=int(self.args.n_msgs), n_events=sc["n_work"], n_persisted=n_out, out=out,
-                          rejects=rows, reject_status=rst, new_names=new, first_seq=first_seq,
-                          world=self.world, rank=self.rank)
+        return dict(n_msgs=int(self.args.n_msgs), n_events=sc["n_work"], n_persisted=sc["n_out"], rejects=rows,
+                    reject_status=rst, new_names=new, first_seq=first_seq)
+
+    # ------------------------------------------------------------------ overlapped framed steps
+    def submit_framed(self, batch, now_ms: int, token=None, presence: bool | None = None) -> list:
+        """Overlapped form of :meth:`step_framed` for service tenants (see ``EngineBase``).  Three
+        slots of raw / offsets / outbound buffers rotate; submitting batch k
+
+        1. enqueues the H2D of k's payload and lengths straight from the record on a copy stream
+           (it runs while batch k-1 computes),
+        2. returns batch k-2, whose rows the SDMA engine has been copying meanwhile,
+        3. waits for batch k-1's compute and reads its counts, learned names and rejects (tables
+           the next step overwrites),
+        4. enqueues batch k's step and starts the SDMA copy of k-1's rows (no CUs: a HIP runtime
+           D2H here runs as a blit kernel beside the step's kernels).
+
+        The host never waits on a copy it just started, so PCIe stays busy in both directions."""
+        if batch.lens is None or self.world > 1:
+            return EngineBase.submit_framed(self, batch, now_ms, token, presence)
+        import warnings
+        n, nb, nl = batch.n_msgs, len(batch.payload), len(batch.lens)
+        if n > self.cfg.max_msgs:
+            raise ValueError(f"batch of {n} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
+        if nb < batch.payload_bytes + _ALIGN:
+            raise ValueError("raw batch payload lacks its tail padding")
+        with self._lock:
+            if getattr(self, "_lagged", None) is not None:      # a host-lagged batch (no lens) first
+                done = EngineBase.drain_framed(self)
+            else:
+                done = []
+            fp = self.__dict__.get("_fp")
+            if fp is None:
+                fp = self._fp = _FramedSlots(self)
+            b = fp.k % _FramedSlots.SLOTS
+            dev_r, dev_l, dev_o = fp.buffers(b, nb, nl)
+            with warnings.catch_warnings():       # read-only topic views: torch only reads them here
+                warnings.simplefilter("ignore", UserWarning)
+                pt = torch.frombuffer(batch.payload, dtype=torch.uint8) if nb else None
+                lt = torch.frombuffer(batch.lens, dtype=torch.uint8) if nl else None
+            with torch.cuda.stream(fp.h2d):
+                fp.h2d.wait_event(fp.ev_comp[b])           # step k-3 was the last reader of slot b
+                if pt is not None:
+                    dev_r[:nb].copy_(pt, non_blocking=True)
+                if lt is not None:
+                    dev_l[:nl].copy_(lt, non_blocking=True)
+                fp.ev_h2d[b].record(fp.h2d)
+            while len(fp.inflight) > 1 or (fp.inflight and fp.inflight[0].rows is not None):
+                done.append(self._framed_finish(fp.inflight.popleft()))      # batch k-2
+            prev = fp.inflight[0] if fp.inflight else None
+            if prev is not None:                                             # batch k-1
+                fp.ev_comp[prev.slot].synchronize()
+                prev.small = self._collect_small(np.asarray(prev.batch.payload))
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(fp.ev_h2d[b])
+            self.frame_varint(dev_l, nl, n, dev_o, batch.payload_bytes)
+            do_presence = self.presence_due(now_ms) if presence is None else presence
+            self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_sel=b,
+                            out_to_device=True)
+            fp.ev_comp[b].record(cur)
+            if prev is not None:
+                self._framed_rows_start(prev)
+            fp.inflight.append(_Submitted(b, batch, token))
+            fp.k += 1
+            return done
+
+    def drain_framed(self) -> list:
+        with self._lock:
+            done = EngineBase.drain_framed(self) if getattr(self, "_lagged", None) is not None else []
+            fp = self.__dict__.get("_fp")
+            while fp is not None and fp.inflight:
+                s = fp.inflight.popleft()
+                if s.small is None:
+                    fp.ev_comp[s.slot].synchronize()
+                    s.small = self._collect_small(np.asarray(s.batch.payload))
+                    self._framed_rows_start(s)
+                done.append(self._framed_finish(s))
+            return done
+
+    @property
+    def framed_pending(self) -> int:
+        fp = self.__dict__.get("_fp")
+        return EngineBase.framed_pending.fget(self) + (len(fp.inflight) if fp is not None else 0)
+
+    def _framed_rows_start(self, s: "_Submitted"):
+        """Start copying the rows of completed step ``s`` to a pinned host buffer."""
+        nb = s.small["n_persisted"] * OUT_REC_SIZE
+        s.rows = self._pinned_out(nb)
+        if not nb:
+            return
+        fp = self._fp
+        h = ctypes.c_uint64()
+        rc = 1 if fp.no_sdma else self.lib.sw_sdma_copy(ctypes.c_void_p(s.rows[0].data_ptr()),
+                                                         ctypes.c_void_p(_ptr(self.out_dev[s.slot])), nb, 0,
+                                                         ctypes.byref(h))
+        if rc == 0:
+            s.sig = h.value
+            return
+        fp.no_sdma = True                       # no copy engine on this node: HIP runtime copy
+        with torch.cuda.stream(fp.d2h):
+            s.rows[0][:nb].copy_(self.out_dev[s.slot][:nb], non_blocking=True)
+            s.ev = torch.cuda.Event()
+            s.ev.record(fp.d2h)
+
+    def _framed_finish(self, s: "_Submitted"):
+        if s.sig is not None:
+            rc = self.lib.sw_sdma_wait(s.sig)
+            s.sig = None
+            if rc:
+                raise RuntimeError(f"sw_sdma_wait failed ({rc})")
+        elif s.ev is not None:
+            s.ev.synchronize()
+        nb = s.small["n_persisted"] * OUT_REC_SIZE
+        res = StepResult(out=s.rows[1][:nb].view(OUT_REC), world=self.world, rank=self.rank, **s.small)
+        return s.token, res
 
     # ------------------------------------------------------------------ queries
     def stats_dict(self) -> dict:  # type: ignore[override]

@@ -56,12 +56,15 @@ def unpack_raw_batch(value: bytes):
 class _Stepped:
     """A raw batch the engine has stepped, with the storage stages it has completed.  ``batch`` (the
     raw bytes, for the host slow path) is kept only when the step rejected messages."""
-    __slots__ = ("key", "res", "now", "batch", "stored", "published", "routed", "queued", "payload", "events")
+    __slots__ = ("key", "res", "now", "batch", "stored", "published", "routed", "queued", "payload", "events",
+                 "detach", "hold", "commit", "trace")
 
     def __init__(self, key, res, now, batch):
         self.key, self.res, self.now, self.batch = key, res, now, batch
         self.stored = self.published = self.routed = self.queued = False
         self.payload = self.events = None
+        self.detach, self.hold, self.commit = False, None, None
+        self.trace = None
 
 
 class GpuInboundTenantEngine(InboundProcessingTenantEngine):
@@ -118,6 +121,18 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._store_q: queue.Queue = queue.Queue(maxsize=2)
         self._store_thread = None
         self._store_error = None
+        # Overlapped engine steps (``overlapSteps``, default on for MI355X columnar tenants): a raw
+        # batch is submitted to the engine and completes when the next one is submitted, so its H2D
+        # and row D2H overlap the neighbouring batches' compute (``EngineBase.submit_framed``).  A
+        # submitted batch's record stays readable through a retention hold of this engine until its
+        # result is back; the pipeline is drained whenever the raw topic has nothing more queued.
+        self.overlap = bool(cfg.get("overlapSteps", self.async_store and self.engine_kind == "gpu"))
+        self._order_lock = threading.Lock()    # engine submit/drain + completion hand-off, in step order
+        self._holds: dict[tuple, dict] = {}    # (topic, partition) -> {offset: in-flight batches}
+        # SW_TENANT_TRACE=1: per-batch timestamps (submit, submitted, completed, store start, payload,
+        # stored, published) for the tenant-path bench's breakdown
+        import os
+        self.trace = [] if os.environ.get("SW_TENANT_TRACE") == "1" else None
         # Replay safety.  engine.step is not idempotent (cursor, event ids, dedup table and device
         # state advance), so a raw record is stepped at most once per engine lifetime: its StepResult
         # stays in ``_stepped`` until every storage stage succeeded, and a re-read record (consumer
@@ -130,7 +145,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # never dead-lettered: a stepped batch cannot be re-stepped, only its storage retried
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
                                         self._process_raw, max_records=16, max_attempts=None,
-                                        idle=self._raise_store_error, views=True,
+                                        idle=self._on_idle, views=True,
                                         auto_commit=self.ckpt_path is None and not self.async_store)
         self.persisted_events = self.create_meter("persistedEvents")
         self.step_timer = self.create_timer("engineStep")
@@ -302,12 +317,15 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             key = (r.topic, r.partition, r.offset)
             commit = (r.topic, r.partition, r.offset + 1) if self.async_store and not self.ckpt_path else None
             item = self._stepped.get(key)
+            if item is not None and item.res is None:   # still in the engine: complete it first
+                self._drain_engine()
             if item is None:
                 # r.value is a zero-copy view of the topic on the in-process bus: a pinned raw-batch
                 # record is DMA'd to the MI355X in place.  The record timestamp is the batch's receive
                 # time, so replay after a restore is deterministic.
+                view = isinstance(r.value, memoryview)
                 self.process_raw_batch(parse_raw_batch(r.value), now=r.timestamp or None, commit=commit,
-                                       key=key, detach=isinstance(r.value, memoryview))
+                                       key=key, detach=view, hold=(r.topic, r.partition, r.offset) if view else None)
             else:
                 self.replayed_batches += 1
                 self._submit(item, commit)
@@ -316,6 +334,49 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 self._since_ckpt += 1
                 if self._since_ckpt >= self.ckpt_every:
                     self.checkpoint()
+        if recs and self.engine.framed_pending:
+            last = recs[-1]
+            end = getattr(self.ms.instance.bus, "end_offset", None)
+            if end is None or end(last.topic, last.partition) <= last.offset + 1:
+                self._drain_engine()                    # nothing more queued: complete the last batch
+
+    def _on_idle(self):
+        self._drain_engine()
+        self._raise_store_error()
+
+    def _drain_engine(self):
+        """Complete every batch submitted to the engine (overlapped steps)."""
+        if self.engine.framed_pending:
+            with self._order_lock:
+                self._complete(self.engine.drain_framed())
+
+    def _complete(self, done):
+        """Results of overlapped steps, in step order: keep what the storage stages need, release the
+        record hold and hand the batch to storage."""
+        for item, res in done:
+            if item.trace is not None:
+                item.trace.append(time.perf_counter())
+            self.processed_events.mark(res.n_events)
+            keep = None
+            if res.rejects is not None and len(res.rejects):
+                keep = item.batch.copy() if item.detach else item.batch
+            item.res, item.batch = res, keep
+            if item.hold is not None:
+                self._hold(item.hold, -1)
+                item.hold = None
+            self._submit(item, item.commit)
+
+    def _hold(self, at, delta: int):
+        """Retention hold (per partition, at its oldest in-flight record) for records the engine
+        reads after the consumer's handler returned."""
+        t, p, o = at
+        hs = self._holds.setdefault((t, p), {})
+        n = hs.get(o, 0) + delta
+        if n > 0:
+            hs[o] = n
+        else:
+            hs.pop(o, None)
+        self.ms.instance.bus.hold(t, p, min(hs) if hs else None, holder=self)
 
     def _raise_store_error(self):
         """A store step failed on the store thread: stop stepping and have the raw consumer re-read
@@ -323,6 +384,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if self._store_error is None:
             return
         self.flush()                    # the store thread skips everything queued after the failure
+                                        # (batches still in the engine complete first: their results are kept)
         err, self._store_error = self._store_error, None
         rewind: dict = {}
         for (t, p, o) in self._stepped:
@@ -330,16 +392,44 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         raise RetryFrom(rewind, err)
 
     def process_batch(self, raw: np.ndarray, offs: np.ndarray, now: int | None = None, commit=None, key=None):
-        """One engine step over host arrays (raw payload bytes, u32 offsets); see :meth:`process_raw_batch`."""
-        return self.process_raw_batch(RawBatch(len(offs) - 1, int(offs[-1]), raw, offs=offs), now, commit, key)
+        """One synchronous engine step over host arrays (raw payload bytes, u32 offsets); see
+        :meth:`process_raw_batch`."""
+        with self._order_lock:          # no overlapped submission slips in between the drain and the step
+            with self._lock:
+                done = self.engine.drain_framed()
+            self._complete(done)
+            return self.process_raw_batch(RawBatch(len(offs) - 1, int(offs[-1]), raw, offs=offs), now, commit,
+                                          key, overlap=False)
 
-    def process_raw_batch(self, batch: RawBatch, now: int | None = None, commit=None, key=None, detach=False):
+    def process_raw_batch(self, batch: RawBatch, now: int | None = None, commit=None, key=None, detach=False,
+                          hold=None, overlap: bool | None = None):
         """One engine step; storing its rows happens here or, with ``asyncStore``, on the store thread
         while the next step runs (call :meth:`flush` to wait for it).  ``key`` = (topic, partition,
         offset) of the raw record: the result is then kept until stored (see ``_stepped``).
         ``detach``: ``batch`` views memory that is released after this call (a topic record read in
-        place), so the bytes the slow path needs are copied."""
+        place), so the bytes the slow path needs are copied.  With overlapped steps the batch is
+        only submitted (returns None): it completes when the next batch is submitted or on a drain,
+        ``hold`` = (topic, partition, offset) keeps its record retained until then."""
         now = now or now_ms()
+        if self.overlap if overlap is None else overlap:
+            item = _Stepped(key, None, now, batch)
+            item.detach, item.commit = detach, commit
+            if self.trace is not None:
+                item.trace = [time.perf_counter()]
+            if key is not None:
+                self._stepped[key] = item
+            with self._order_lock:
+                if hold is not None:
+                    item.hold = hold
+                    self._hold(hold, +1)
+                # not under the tenant lock: the submit waits on the GPU, and the store thread needs
+                # that lock to build payloads meanwhile (the engine serialises on its own lock)
+                with self.step_timer.time():
+                    done = self.engine.submit_framed(batch, now, token=item)
+                if item.trace is not None:
+                    item.trace.append(time.perf_counter())
+                self._complete(done)
+            return None
         with self._lock, self.step_timer.time():
             res = self.engine.step_framed(batch, now)
         self.processed_events.mark(res.n_events)
@@ -363,12 +453,19 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     def _store_step(self, item: "_Stepped", commit):
         """Storage stages of one stepped batch; each runs once even when the batch is retried."""
         res, now = item.res, item.now
+        tr = item.trace
+        if tr is not None:
+            tr.append(time.perf_counter())
         if not item.stored:
             if self.storage == "columnar":
                 with self.store_timer.time():
                     if item.payload is None:    # built once: it carries the dictionary deltas
-                        item.payload = self.columnar_payload(res, now)
+                        item.payload = self.columnar_payload(res, now, tr)
+                    if tr is not None:
+                        tr.append(time.perf_counter())
                     n = self._em().add_columnar_batch(item.payload)
+                    if tr is not None:
+                        tr.append(time.perf_counter())
                 self.persisted_events.mark(n)
             else:
                 if item.events is None:
@@ -399,6 +496,9 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             self._stored_hw[(t, p)] = max(self._stored_hw.get((t, p), -1), o + 1)
         if commit is not None:
             self.ms.instance.bus.commit(self.raw_consumer.group, *commit)
+        if tr is not None and self.trace is not None:
+            tr.append(time.perf_counter())
+            self.trace.append(tr)
 
     def _store_loop(self):
         while True:
@@ -417,14 +517,17 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 self._store_q.task_done()
 
     def flush(self):
-        """Wait until every queued batch is stored (and its raw offset committed) or skipped after a
-        store failure."""
+        """Complete the batches in the engine, then wait until every queued batch is stored (and its
+        raw offset committed) or skipped after a store failure."""
+        self._drain_engine()
         if self._store_thread is not None:
             self._store_q.join()
 
-    def columnar_payload(self, res, now: int) -> bytes:
+    def columnar_payload(self, res, now: int, tr: list | None = None) -> bytes:
         """Rows + the dictionary entries the receiver has not seen yet (assignment context, names)."""
         with self._lock:
+            if tr is not None:
+                tr.append(time.perf_counter())
             asg = {}
             for ai in self._asg_dirty:
                 a = self._asg_entities.get(ai)
@@ -440,6 +543,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             self._names_sent = len(self._nid2name)
         rules = {t.alert_type: t.alert_message for t in self.engine.tests}
         out = res.out if res.out is not None else np.zeros(0, OUT_REC)
+        if tr is not None:
+            tr.append(time.perf_counter())
         return encode_batch(self.boot, res.first_seq, res.world, res.rank, now, out, asg, names, rules)
 
     def _publish_events(self, events):

@@ -106,7 +106,9 @@ TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
     storage="columnar", publishEnriched="batches",
     capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
               "dedup_slots": 1 << 18, "gen_cap": 32768})
-TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {"datastore": {"type": "columnar"}}
+# in-memory columnar store: newest 2^28 rows (8 GB of 32 B rows) held, older batches evicted
+TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {"datastore": {"type": "columnar",
+                                                                                  "retentionRows": 1 << 28}}
 
 DATASET_TEMPLATES = {
     "empty": {"name": "Empty dataset", "description": "No data is created."},

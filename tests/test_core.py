@@ -460,3 +460,30 @@ def test_codec_clone_matches_wire_round_trip():
     c = codec.clone(payload)
     assert c == codec.loads(codec.dumps(payload))
     assert c["args"][1] is not m and c["kwargs"]["res"].results[0] is not m
+
+
+def test_columnar_store_retention_evicts_oldest_batches():
+    """The in-memory columnar store holds at most ``retentionRows`` rows: whole oldest batches go,
+    queries and id lookups see only what is held, and the newest batch always stays."""
+    import numpy as np
+
+    from sitewhere_amd.models.columnar import EV_MEASUREMENT, OUT_REC
+    from sitewhere_amd.models.domain import DateRangeSearchCriteria
+    from sitewhere_amd.persistence.columnar import encode_batch
+    from sitewhere_amd.persistence.events import create_event_store
+    st = create_event_store("columnar", retentionRows=10_000)
+    for b in range(5):
+        rows = np.zeros(4096, OUT_REC)
+        rows["etype"], rows["assignment"], rows["name_id"] = EV_MEASUREMENT, 0, 1
+        rows["event_date"] = 1_700_000_000_000 + b * 10_000 + np.arange(4096)
+        rows["v0"] = b
+        st.add_columnar(encode_batch("boot", b * 4096, 1, 0, 1, rows, {0: ["a0", "d0", None, None, None]},
+                                     {1: "m"} if b == 0 else {}))
+    assert st.rows == 8192 and st.evicted_rows == 3 * 4096 and st.count() == 8192
+    res = st.list_events("Measurement", "Assignment", ["a0"], DateRangeSearchCriteria(page_size=0))
+    assert res.num_results == 8192 and {e.value for e in res.results} == {3.0, 4.0}
+    assert st.get_event_by_id("boot-0") is None and st.get_event_by_id(f"boot-{4 * 4096}").value == 4.0
+    one = create_event_store("columnar", retentionRows=10)
+    rows = np.zeros(4096, OUT_REC)
+    one.add_columnar(encode_batch("b", 0, 1, 0, 1, rows, {}, {}))
+    assert one.rows == 4096                              # a batch larger than the window is kept whole

@@ -60,14 +60,19 @@ def _values(inst, run, token, dev):
     return res.results
 
 
-def test_async_store_failure_rewinds_and_stores_once(inst):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_async_store_failure_rewinds_and_stores_once(inst, overlap):
     """gpu-columnar (asyncStore on): the store thread fails batch k while batch k+1 is queued.
     Nothing is committed past k, the consumer rewinds to k, both batches are stored from their kept
-    results (not re-stepped) and every event lands exactly once."""
-    ib, run, dev = _tenant(inst, "rpa", "gpu-columnar")
+    results (not re-stepped) and every event lands exactly once.  ``overlap``: the engine completes
+    each batch when the next is submitted (the MI355X overlapped steps; the CPU engine keeps the
+    same one-deep lag), so a rewind also has to complete the batch still in the engine."""
+    tok = "rpo" if overlap else "rpa"
+    ib, run, dev = _tenant(inst, tok, "gpu-columnar")
+    ib.overlap = overlap
     assert ib.async_store
-    store = inst.tenant_engine("event-management", "rpa").store
-    topic = inst.instance.naming.tenant_prefix("rpa") + RAW_PAYLOADS
+    store = inst.tenant_engine("event-management", tok).store
+    topic = inst.instance.naming.tenant_prefix(tok) + RAW_PAYLOADS
     group = ib.raw_consumer.group
     with FaultInjector() as fi:
         fi.fail_next(store, "add_columnar", 2)
@@ -78,10 +83,43 @@ def test_async_store_failure_rewinds_and_stores_once(inst):
     assert ib.engine.stats_dict()["persisted"] == 120          # each batch stepped exactly once
     assert ib.replayed_batches >= 1 and ib.raw_consumer.rewinds >= 1
     assert wait_until(lambda: inst.instance.bus.committed(group, topic, 0) == 6)
-    res = _values(inst, run, "rpa", dev)
+    res = _values(inst, run, tok, dev)
     assert sorted(m.value for m in res) == sorted(float(100 * b + i) for b in range(6) for i in range(20))
     assert len({m.id for m in res}) == 120
-    assert not ib._stepped
+    assert not ib._stepped and not ib.engine.framed_pending
+
+
+def test_overlapped_steps_on_zero_copy_records(inst):
+    """Raw batches published as zero-copy framed records (what event sources write) through a tenant
+    with overlapped engine steps: each record is read in place, stays retained (engine hold) until the
+    engine returned its result, unregistered devices still reach the slow path from the held bytes,
+    and every offset is committed once its batch is stored."""
+    from sitewhere_amd.pipeline.bus_io import RawBatchRecord
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    ib, run, dev = _tenant(inst, "rpz", "gpu-columnar")
+    ib.overlap = True
+    bus = inst.instance.bus
+    store = inst.tenant_engine("event-management", "rpz").store
+    topic = inst.instance.naming.tenant_prefix("rpz") + RAW_PAYLOADS
+    unreg = bus.consumer("rpz-unreg", [inst.instance.naming.unregistered_device_events("rpz")])
+    recs = []
+    for b in range(5):
+        msgs = [wire.measurements("galaxytab-001", {"v": float(100 * b + i)}, event_date=1_700_000_300_000 + 100 * b + i)
+                for i in range(30)] + [wire.measurements(f"stranger-{b}", {"v": 1.0})]
+        raw, offs = pack_messages(msgs)
+        rec = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1, pinned=False)
+        recs.append(rec)
+        rec.publish(bus, topic, 0, ts=1_700_000_400_000 + b)
+    assert wait_until(lambda: store.rows == 150, 30), store.rows
+    assert wait_until(lambda: bus.committed(ib.raw_consumer.group, topic, 0) == bus.end_offset(topic, 0))
+    assert not ib.engine.framed_pending and not ib._stepped
+    assert not ib._holds.get((topic, 0))                     # every engine hold released
+    seen = []
+    assert wait_until(lambda: seen.extend(r.key for rs in unreg.poll(50).values() for r in rs) or len(seen) >= 5)
+    assert sorted(seen) == [f"stranger-{b}".encode() for b in range(5)]
+    res = _values(inst, run, "rpz", dev)
+    assert sorted(m.value for m in res) == sorted(float(100 * b + i) for b in range(5) for i in range(30))
 
 
 def test_sync_store_failure_retries_store_not_step(inst):

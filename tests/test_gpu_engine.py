@@ -237,3 +237,33 @@ def test_hot_store_query_kernel_matches_cpu_oracle():
         assert tg == tc and np.array_equal(eg, ec)
         for k in ("date", "asg", "v0", "v1", "etype"):
             assert np.array_equal(pg[k], pc[k]), k
+
+
+def test_overlapped_framed_steps_match_sync_oracle():
+    """submit_framed / drain_framed (the service tenant's overlapped steps): batch k is returned when
+    batch k+2 is submitted, from pinned zero-copy records.  Every result -- rows, rejects, learned
+    names, first store sequence -- equals the CPU oracle's synchronous step of the same batch, and a
+    synchronous step is refused while a submission is pending."""
+    from sitewhere_amd.pipeline.bus_io import RawBatchRecord, parse_raw_batch
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    g, c = pair()
+    recs, want, got = [], [], []
+    for k in range(6):
+        raw, offs = fleet_batch(2500, seed=700 + k)
+        rec = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1)
+        recs.append(rec)
+        want.append(c.step(raw, offs, NOW + k, presence=False))
+        got += g.submit_framed(parse_raw_batch(rec.buf.numpy()[:rec.value_len]), NOW + k, token=k, presence=False)
+        assert [t for t, _ in got] == list(range(max(0, k - 1)))   # rows of k-1 are still copying
+        assert g.framed_pending == min(k + 1, 2)
+        if k == 2:
+            with pytest.raises(RuntimeError, match="pending"):
+                g.step(raw, offs, NOW, presence=False)
+    got += g.drain_framed()
+    assert [t for t, _ in got] == list(range(6)) and not g.framed_pending
+    for (_, rg), rc in zip(got, want):
+        assert_same_step(rg, rc, c.names)
+        assert rg.first_seq == rc.first_seq and rg.new_names == rc.new_names
+        assert rg.n_msgs == rc.n_msgs and rg.n_events == rc.n_events
+    assert g.stats_dict() == c.stats_dict()
+    assert sum(len(r.rejects) for _, r in got) > 0                # unregistered devices were rejected

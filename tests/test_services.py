@@ -460,3 +460,52 @@ def test_gpu_tenant_checkpoint_resume_replays_exactly(tmp_path):
         assert len({m.id for m in res.results}) == 100
     finally:
         inst.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not __import__("conftest").gpu_available(), reason="needs an MI355X GPU")
+def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records():
+    """The MI355X columnar tenant steps raw batches overlapped (H2D of batch k+1 and the row D2H of
+    batch k-1 beside the compute of batch k), straight from pinned zero-copy topic records: every
+    measurement stored once, unregistered devices routed, offsets committed, record holds released."""
+    from sitewhere_amd.pipeline.bus_io import RawBatchRecord
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    from sitewhere_amd.services.event_sources import RAW_PAYLOADS
+    inst = SiteWhereInstance().start()
+    try:
+        inst.wait_for_tenant("default", 60)
+        tm = inst.api("TenantManagement")
+        inst.instance.system_user.run(lambda: tm.create_tenant({"token": "ovl", "name": "ovl",
+                                                                "configurationTemplateId": "gpu-columnar",
+                                                                "datasetTemplateId": "construction"}))
+        inst.wait_for_tenant("ovl", 120)
+        ib = inst.tenant_engine("inbound-processing", "ovl")
+        assert ib.engine_kind == "gpu" and ib.overlap and ib.async_store
+        run = lambda f: inst.instance.system_user.run(f, "ovl")  # noqa: E731
+        dev = run(lambda: inst.api("DeviceManagement", "ovl").get_device_by_token("galaxytab-001"))
+        assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        bus = inst.instance.bus
+        topic = inst.instance.naming.tenant_prefix("ovl") + RAW_PAYLOADS
+        unreg = bus.consumer("ovl-unreg", [inst.instance.naming.unregistered_device_events("ovl")])
+        store = inst.tenant_engine("event-management", "ovl").store
+        recs = []
+        for b in range(8):
+            msgs = [wire.measurements("galaxytab-001", {"v": float(1000 * b + i)},
+                                      event_date=1_700_000_000_000 + 1000 * b + i) for i in range(200)]
+            msgs.append(wire.measurements(f"stranger-{b}", {"v": 1.0}))
+            raw, offs = pack_messages(msgs)
+            rec = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1)
+            recs.append(rec)
+            rec.publish(bus, topic, 0, ts=1_700_000_500_000 + b)
+        assert wait_until(lambda: store.rows == 1600, 60), store.rows
+        assert wait_until(lambda: bus.committed(ib.raw_consumer.group, topic, 0) == bus.end_offset(topic, 0), 30)
+        assert not ib.engine.framed_pending and not ib._stepped and not ib._holds.get((topic, 0))
+        seen = []
+        assert wait_until(lambda: seen.extend(r.key for rs in unreg.poll(50).values() for r in rs) or len(seen) >= 8)
+        assert sorted(seen) == sorted(f"stranger-{b}".encode() for b in range(8))
+        em = inst.api("DeviceEventManagement", "ovl")
+        res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id], {"pageSize": 0}))
+        assert sorted(m.value for m in res.results) == sorted(float(1000 * b + i) for b in range(8) for i in range(200))
+    finally:
+        inst.stop()
