@@ -132,6 +132,24 @@ class JsonBatchDecoder(Decoder):
         return out
 
 
+class CoapJsonDecoder(Decoder):
+    """Body of a CoAP request routed by the receiver's path (reference
+    ``decoder/coap/CoapJsonDecoder.java``): ``eventType`` / ``token`` come from the receiver's
+    metadata, the JSON body is the request itself."""
+
+    def decode(self, payload, metadata):
+        t, tok = metadata.get("eventType"), metadata.get("token")
+        if t not in REQUEST_TYPES or not tok:
+            raise EventDecodeException(f"CoAP payload without a routed event type/token ({t!r}, {tok!r})")
+        try:
+            req = json.loads(payload) if payload else {}
+        except Exception as e:
+            raise EventDecodeException(f"invalid JSON: {e}") from e
+        if not isinstance(req, dict):
+            raise EventDecodeException("CoAP request body must be a JSON object")
+        return [decoded(tok, t, req)]
+
+
 class ScriptedDecoder(Decoder):
     """User script ``decode(payload, metadata) -> list[dict]`` (reference Groovy decoders)."""
 
@@ -371,7 +389,7 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
                 dd = AlternateIdDeduplicator(ev)
             elif dcfg.get("type") == "script":
                 dd = ScriptedDeduplicator(self.ms.scripts, dcfg["script"])
-        recs = [DirectReceiver("direct")] + [build_receiver(rc) for rc in sc.get("receivers", [])]
+        recs = [DirectReceiver("direct")] + [build_receiver(rc, self.ms.scripts) for rc in sc.get("receivers", [])]
         return InboundEventSource(sc["id"], dec, dd, recs, self.manager, forward_raw=sc.get("forward") == "raw")
 
     def build_decoder(self, d) -> Decoder:
@@ -380,8 +398,10 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
         t = d.get("type")
         if t == "protobuf":
             return ProtobufDecoder()
-        if t == "json":
+        if t in ("json", "json-string"):          # JsonStringDeviceRequestDecoder: same document as text
             return JsonDeviceRequestDecoder()
+        if t == "coap-json":
+            return CoapJsonDecoder()
         if t == "json-batch":
             return JsonBatchDecoder()
         if t == "script":
