@@ -29,7 +29,7 @@ import numpy as np
 
 from ..core.errors import SiteWhereException
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
-from .mqtt import MqttClient
+from .mqtt import MQTT_OPTIONS
 
 
 class Receiver(TenantEngineLifecycleComponent):
@@ -47,17 +47,27 @@ class Receiver(TenantEngineLifecycleComponent):
 
 
 class MqttReceiver(Receiver):
-    def __init__(self, host: str, port: int, topic: str = "SiteWhere/default/input/json", qos: int = 1,
-                 num_threads: int = 4):
+    """MQTT subscription receiver (reference ``mqtt/MqttInboundEventReceiver.java``): one client
+    subscription, payloads handed to a pool of ``num_threads`` processors; a QoS 1/2 message is
+    acknowledged once it has been handed off.  ``mqtt`` carries the ``MqttLifecycleComponent``
+    attributes (protocol, username, password, trustStorePath, keyStorePath, clientId,
+    cleanSession); the client reconnects and re-subscribes by itself."""
+
+    def __init__(self, host: str, port: int, topic: str = "SiteWhere/default/input/json", qos=1,
+                 num_threads: int = 4, **mqtt):
         super().__init__(f"mqtt-receiver:{topic}")
-        self.host, self.port, self.topic, self.qos, self.num_threads = host, port, topic, qos, num_threads
+        from .mqtt import parse_qos
+        self.host, self.port, self.topic, self.qos, self.num_threads = host, port, topic, parse_qos(qos), num_threads
+        self.mqtt = {k: v for k, v in mqtt.items() if v is not None}
         self.client = None
         self.pool = None
 
     def start(self, monitor):
+        from .mqtt import client_from_config
         self.pool = ThreadPoolExecutor(max_workers=self.num_threads, thread_name_prefix="mqtt-proc")
-        self.client = MqttClient(self.host, self.port).connect()
+        self.client = client_from_config(dict(self.mqtt, host=self.host, port=self.port), reconnect=True)
         self.client.on_message(lambda t, p: self.pool.submit(self.deliver, p, {"topic": t}))
+        self.client.connect()
         self.client.subscribe(self.topic, self.qos)
 
     def stop(self, monitor):
@@ -844,8 +854,9 @@ def build_receiver(rc: dict, scripts=None) -> Receiver:
     scripted socket handlers and polling scripts)."""
     t = rc.get("type")
     if t == "mqtt":
-        return MqttReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 1883)), rc.get("topic", "SiteWhere/input"),
-                            int(rc.get("qos", 1)), int(rc.get("numThreads", 4)))
+        return MqttReceiver(rc.get("hostname") or rc.get("host", "127.0.0.1"), int(rc.get("port", 1883)),
+                            rc.get("topic", "SiteWhere/input"), rc.get("qos", 1), int(rc.get("numThreads", 4)),
+                            **{k: rc.get(k) for k in MQTT_OPTIONS})
     if t == "socket":
         return SocketReceiver(rc.get("host", "127.0.0.1"), int(rc.get("port", 0)), rc.get("handler", "read-all"),
                               int(rc.get("numThreads", 4)), rc.get("script"), scripts)

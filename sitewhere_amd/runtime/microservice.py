@@ -455,6 +455,9 @@ class GlobalMicroservice(Microservice):
     """Single-configuration service (instance, tenant, user management, web-rest)."""
 
 
+_SCRIPT_ID = __import__("re").compile(r"^[A-Za-z0-9_.\-]+$")
+
+
 class MicroserviceTenantEngine(TenantEngineLifecycleComponent):
     """Per-tenant engine of a multitenant microservice."""
 
@@ -468,6 +471,25 @@ class MicroserviceTenantEngine(TenantEngineLifecycleComponent):
         self.tenant = tenant
         self.config: dict = {}
         self.api = None  # RPC implementation for this tenant
+
+    def script_source(self, ref) -> str:
+        """Source of a configured script.  ``{"scriptId": id[, "version": v]}`` or a bare script id
+        names a versioned script in script management (tenant scope, then global, of this
+        microservice; the active version unless pinned) -- the reference's ``scriptId`` attributes
+        (``ZookeeperScriptManagement``); anything else is inline source."""
+        from ..core.errors import NotFoundException
+        sid, ver = (ref.get("scriptId") or ref.get("id"), ref.get("version")) if isinstance(ref, dict) else (ref, None)
+        if isinstance(sid, str) and _SCRIPT_ID.match(sid):
+            for scope in (self.tenant.token, "global"):
+                try:
+                    return self.ms.instance.scripts.get_content(scope, self.ms.identifier, sid, ver)
+                except NotFoundException:
+                    continue
+            raise SiteWhereException(f"script {sid!r} not found for {self.ms.identifier} "
+                                     f"(tenant {self.tenant.token} or global scope)")
+        if isinstance(ref, dict):
+            raise SiteWhereException(f"invalid script reference {ref!r}")
+        return ref
 
     # hooks ----------------------------------------------------------------------
     def tenant_initialize(self, monitor):

@@ -104,12 +104,22 @@ _DECODERS = {"protobuf-event-decoder": "protobuf", "json-device-request-decoder"
              "composite-event-decoder": "composite"}
 
 
+def _mqtt_attrs(el: ET.Element) -> dict:
+    """``cn:mqtt-broker-attributes`` (``connector-common.xsd``) of an MQTT receiver, connector or
+    command destination: connection, credentials, trust / key stores, client id, session, QoS."""
+    out = {"host": _sub(el.get("hostname", "localhost")), "port": _num(el.get("port"), 1883)}
+    for k in ("protocol", "username", "password", "trustStorePath", "keyStorePath", "clientId", "cleanSession",
+              "qos"):
+        if el.get(k) is not None:
+            out[k] = _sub(el.get(k))
+    return out
+
+
 def _receiver(n: str, el: ET.Element) -> dict | None:
     g = lambda k, d=None: _sub(el.get(k, d))   # noqa: E731
     if n == "mqtt-event-source":
-        return {"type": "mqtt", "host": g("hostname", "localhost"), "port": _num(el.get("port"), 1883),
-                "topic": g("topic", "SiteWhere/input"), "qos": _num(el.get("qos"), 1),
-                "numThreads": _num(el.get("numThreads"), 4)}
+        return dict(_mqtt_attrs(el), type="mqtt", topic=g("topic", "SiteWhere/input"),
+                    numThreads=_num(el.get("numThreads"), 4))
     if n == "activemq-event-source":
         if el.get("transportUri"):
             return {"type": "activemq-broker", "transportUri": g("transportUri"),
@@ -128,14 +138,36 @@ def _receiver(n: str, el: ET.Element) -> dict | None:
                 "port": int(m.group(2) or 5672) if m else 5672, "queue": g("queueName", "sitewhere.input"),
                 "durable": _bool(el.get("durable"), False)}
     if n == "socket-event-source":
-        return {"type": "socket", "host": "0.0.0.0", "port": _num(el.get("port"), 8484)}
+        rc = {"type": "socket", "host": "0.0.0.0", "port": _num(el.get("port"), 8484),
+              "numThreads": _num(el.get("numThreads"), 4), "handler": "read-all"}
+        for c in el.iter():             # interaction handler factory (read-all / http / groovy)
+            cn = _local(c.tag)
+            if cn == "http-interaction-handler-factory":
+                rc["handler"] = "http"
+            elif cn in ("groovy-interaction-handler-factory", "groovy-socket-interaction-handler-factory"):
+                rc.update(handler="script", script=_sub(c.get("scriptId") or c.get("scriptPath")))
+        return rc
     if n in ("web-socket-event-source", "websocket-event-source"):
-        return {"type": "websocket", "host": "0.0.0.0", "port": _num(el.get("port"), 8585)}
+        rc = {"type": "websocket", "host": "0.0.0.0", "port": _num(el.get("port"), 8585),
+              "payloadType": (g("payloadType") or "binary").lower()}
+        if el.get("webSocketUrl"):
+            rc["webSocketUrl"] = g("webSocketUrl")
+        headers = {_sub(h.get("name")): _sub(h.get("value")) for h in el.iter() if _local(h.tag) == "header"}
+        if headers:
+            rc["headers"] = headers
+        return rc
     if n == "coap-event-source" or n == "coap-server-event-source":
         return {"type": "coap", "host": g("hostname", "0.0.0.0"), "port": _num(el.get("port"), 5683)}
     if n in ("polling-rest-event-source", "rest-event-source"):
         ms = _num(el.get("pollIntervalMs"), 10000)
-        return {"type": "rest-poll", "url": g("baseUrl") or g("url"), "interval": ms / 1000.0 if isinstance(ms, int) else 10.0}
+        rc = {"type": "rest-poll", "baseUrl": g("baseUrl") or g("url"),
+              "interval": ms / 1000.0 if isinstance(ms, int) else 10.0}
+        for k in ("username", "password"):
+            if el.get(k):
+                rc[k] = g(k)
+        if el.get("scriptId"):
+            rc["scriptId"] = g("scriptId")
+        return rc
     if n in ("azure-eventhub-event-source", "eventhub-event-source"):
         ns, hub = g("namespace"), g("eventHubName") or g("targetFqn")
         return {"type": "eventhub", "namespace": ns, "eventHub": hub, "consumerGroup": g("consumerGroupName", "$Default"),
@@ -182,8 +214,8 @@ def _outbound(root: ET.Element, ctx: _Ctx) -> dict:
         g = lambda k, d=None: _sub(el.get(k, d))   # noqa: E731
         cid = g("connectorId") or f"connector-{len(out) + 1}"
         if n == "mqtt-connector":
-            out.append({"id": cid, "type": "mqtt", "host": g("hostname", "localhost"), "port": _num(el.get("port"), 1883),
-                        "topic": g("outboundTopic") or g("topic", "SiteWhere/output")})
+            out.append(dict(_mqtt_attrs(el), id=cid, type="mqtt",
+                            topic=g("outboundTopic") or g("topic", "SiteWhere/output")))
         elif n == "solr-connector":
             out.append({"id": cid, "type": "solr", "url": g("solrServerUrl") or g("url")})
         elif n in ("rabbit-mq-connector", "rabbitmq-connector"):
@@ -247,7 +279,7 @@ def _command_delivery(root: ET.Element, ctx: _Ctx) -> dict:
                     enc = "json"
             d = {"id": g("destinationId") or "default", "encoder": enc}
             if n == "mqtt-command-destination":
-                d.update(provider="mqtt", host=g("hostname", "localhost"), port=_num(el.get("port"), 1883))
+                d.update(_mqtt_attrs(el), provider="mqtt")
             elif n == "coap-command-destination":
                 d.update(provider="coap")
             elif n in ("twilio-command-destination", "sms-command-destination"):

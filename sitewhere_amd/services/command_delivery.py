@@ -16,7 +16,7 @@ import threading
 
 from ..core.errors import SiteWhereException
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
-from ..edges.mqtt import MqttClient
+from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
 from ..edges.receivers import coap_post
 from ..models import wire
 from ..models.domain import ParameterType
@@ -142,15 +142,20 @@ class LogProvider:
 
 
 class MqttProvider:
-    def __init__(self, host, port, qos=1):
-        self.host, self.port, self.qos = host, port, qos
+    """MQTT publish of encoded commands (reference ``MqttCommandDeliveryProvider.java:87-111``, QoS 1
+    by default); ``mqtt``: the ``MqttLifecycleComponent`` attributes (TLS, credentials, client id)."""
+
+    def __init__(self, host, port, qos=1, **mqtt):
+        self.host, self.port, self.qos = host, port, parse_qos(qos)
+        self.mqtt = {k: v for k, v in mqtt.items() if v is not None}
         self.client = None
         self._lock = threading.Lock()
 
     def deliver(self, nesting, assignment, payload, params):
         with self._lock:
             if self.client is None:
-                self.client = MqttClient(self.host, self.port).connect()
+                self.client = client_from_config(dict(self.mqtt, host=self.host, port=self.port),
+                                                 reconnect=True).connect()
         self.client.publish(params["topic"], payload, qos=self.qos)
 
 
@@ -254,7 +259,7 @@ class CommandDeliveryTenantEngine(MicroserviceTenantEngine):
         elif rt == "device-type-mapping":
             self.router = DeviceTypeMappingRouter(rc.get("mappings", {}), rc.get("default"))
         elif rt == "script":
-            self.router = ScriptRouter(self.ms.scripts, rc["script"])
+            self.router = ScriptRouter(self.ms.scripts, self.script_source(rc["script"]))
         else:
             self.router = NoOpRouter()
         n = self.ms.instance.naming
@@ -266,10 +271,11 @@ class CommandDeliveryTenantEngine(MicroserviceTenantEngine):
 
     def build_destination(self, dc) -> CommandDestination:
         enc = {"json": JsonEncoder, "protobuf": ProtobufEncoder}.get(dc.get("encoder", "json"))
-        encoder = enc() if enc else ScriptEncoder(self.ms.scripts, dc["encoderScript"])
+        encoder = enc() if enc else ScriptEncoder(self.ms.scripts, self.script_source(dc["encoderScript"]))
         p = dc.get("provider", "log")
         if p == "mqtt":
-            provider = MqttProvider(dc.get("host", "127.0.0.1"), int(dc.get("port", 1883)), int(dc.get("qos", 1)))
+            provider = MqttProvider(dc.get("hostname") or dc.get("host", "127.0.0.1"), int(dc.get("port", 1883)),
+                                    dc.get("qos", 1), **{k: dc.get(k) for k in MQTT_OPTIONS})
             extractor = mqtt_extractor(self.tenant.token, dc.get("commandTopic", "SiteWhere/{tenant}/command/{deviceToken}"),
                                        dc.get("systemTopic", "SiteWhere/{tenant}/system/{deviceToken}"))
         elif p == "coap":

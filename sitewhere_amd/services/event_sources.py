@@ -378,7 +378,10 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
 
     def build_source(self, sc: dict) -> InboundEventSource:
         from ..edges.receivers import build_receiver
-        dec = self.build_decoder(sc.get("decoder", "json"))
+        d = sc.get("decoder", "json")
+        if sc.get("script") and (d == "script" or isinstance(d, dict) and d.get("type") == "script" and "script" not in d):
+            d = {"type": "script", "script": sc["script"]}      # source-level script (imported templates)
+        dec = self.build_decoder(d)
         if sc.get("logPayloads"):
             dec = PayloadLoggerDecoder(dec, self.logger)
         dd = None
@@ -388,9 +391,15 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
                 ev = lambda alt: self.ms.api("DeviceEventManagement", self.tenant.token).get_device_event_by_alternate_id(alt)  # noqa
                 dd = AlternateIdDeduplicator(ev)
             elif dcfg.get("type") == "script":
-                dd = ScriptedDeduplicator(self.ms.scripts, dcfg["script"])
-        recs = [DirectReceiver("direct")] + [build_receiver(rc, self.ms.scripts) for rc in sc.get("receivers", [])]
+                dd = ScriptedDeduplicator(self.ms.scripts, self.script_source(dcfg["script"]))
+        recs = [DirectReceiver("direct")] + [build_receiver(self._resolve_receiver_scripts(rc), self.ms.scripts)
+                                            for rc in sc.get("receivers", [])]
         return InboundEventSource(sc["id"], dec, dd, recs, self.manager, forward_raw=sc.get("forward") == "raw")
+
+    def _resolve_receiver_scripts(self, rc: dict) -> dict:
+        """Receiver script references (socket interaction handler, REST polling ``scriptId``) -> source."""
+        ref = rc.get("script") or rc.get("scriptId")
+        return dict(rc, script=self.script_source(ref)) if ref else rc
 
     def build_decoder(self, d) -> Decoder:
         if isinstance(d, str):
@@ -405,7 +414,7 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
         if t == "json-batch":
             return JsonBatchDecoder()
         if t == "script":
-            return ScriptedDecoder(self.ms.scripts, d["script"])
+            return ScriptedDecoder(self.ms.scripts, self.script_source(d["script"]))
         if t == "echo":
             return EchoStringDecoder(self.logger)
         if t == "composite":

@@ -17,7 +17,7 @@ import threading
 import urllib.request
 
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
-from ..edges.mqtt import MqttClient
+from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
 from ..rpc import codec
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
@@ -68,15 +68,19 @@ class LogConnector(OutboundConnector):
 
 
 class MqttConnector(OutboundConnector):
-    """Publish each event as JSON to ``topic`` (``{deviceToken}``/``{eventType}`` placeholders)."""
+    """Publish each event as JSON to ``topic`` (``{deviceToken}``/``{eventType}`` placeholders);
+    ``mqtt`` carries the reference's ``MqttLifecycleComponent`` attributes (TLS, credentials, client
+    id, clean session).  The client reconnects and retransmits unacknowledged QoS>0 publishes."""
 
-    def __init__(self, cid, host, port, topic="SiteWhere/{tenant}/outbound/{deviceToken}", qos=0, filters=None):
+    def __init__(self, cid, host, port, topic="SiteWhere/{tenant}/outbound/{deviceToken}", qos=0, filters=None,
+                 **mqtt):
         super().__init__(cid, filters)
-        self.host, self.port, self.topic, self.qos = host, port, topic, qos
+        self.host, self.port, self.topic, self.qos = host, port, topic, parse_qos(qos)
+        self.mqtt = {k: v for k, v in mqtt.items() if v is not None}
         self.client = None
 
     def start(self, monitor):
-        self.client = MqttClient(self.host, self.port).connect()
+        self.client = client_from_config(dict(self.mqtt, host=self.host, port=self.port), reconnect=True).connect()
 
     def on_event(self, ev, ctx):
         t = self.topic.format(tenant=self.tenant_engine.tenant.token, deviceToken=ctx.get("deviceToken"),
@@ -185,7 +189,7 @@ def build_filters(engine, cfgs) -> list:
             types = set(f["eventTypes"])
             out.append(lambda ev, ctx, types=types: ev.event_type.value not in types)
         elif t == "script":
-            src = f["script"]
+            src = engine.script_source(f["script"])
             out.append(lambda ev, ctx, src=src: bool(engine.ms.scripts.call(src, "filter", ev.to_dict(), ctx,
                                                                             name="connector-filter")))
     return out
@@ -198,7 +202,8 @@ def build_connector(engine, cfg) -> OutboundConnector:
         return LogConnector(cid, filters)
     if t == "mqtt":
         return MqttConnector(cid, cfg.get("host", "127.0.0.1"), int(cfg.get("port", 1883)),
-                             cfg.get("topic", "SiteWhere/{tenant}/outbound/{deviceToken}"), int(cfg.get("qos", 0)), filters)
+                             cfg.get("topic", "SiteWhere/{tenant}/outbound/{deviceToken}"), cfg.get("qos", 0), filters,
+                             **{k: cfg.get(k) for k in MQTT_OPTIONS})
     if t == "http":
         return HttpConnector(cid, cfg["url"], cfg.get("headers"), cfg.get("batch", True), filters)
     from .cloud_connectors import build_cloud_connector
@@ -210,7 +215,7 @@ def build_connector(engine, cfg) -> OutboundConnector:
     if t == "file":
         return FileArchiveConnector(cid, cfg["path"], filters)
     if t == "script":
-        return ScriptConnector(cid, cfg["script"], filters)
+        return ScriptConnector(cid, engine.script_source(cfg["script"]), filters)
     raise ValueError(f"unknown connector {t!r}")
 
 

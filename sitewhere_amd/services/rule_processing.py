@@ -120,14 +120,14 @@ class ScriptedRuleProcessor(RuleProcessor):
     def on_alert(self, ctx, ev): self._call("on_alert", ctx, ev)
 
 
-def build_processor(cfg: dict) -> RuleProcessor:
+def build_processor(cfg: dict, engine=None) -> RuleProcessor:
     t = cfg.get("type")
     if t == "zone-test":
         return ZoneTestRuleProcessor(cfg["id"], cfg.get("zoneTests", []))
     if t == "threshold":
         return ThresholdRuleProcessor(cfg["id"], cfg.get("rules", []))
     if t == "script":
-        return ScriptedRuleProcessor(cfg["id"], cfg["script"])
+        return ScriptedRuleProcessor(cfg["id"], engine.script_source(cfg["script"]) if engine else cfg["script"])
     raise ValueError(f"unknown rule processor {t!r}")
 
 
@@ -137,7 +137,7 @@ class RuleProcessingTenantEngine(MicroserviceTenantEngine):
         self.hosts = []
         topic = self.ms.instance.naming.inbound_enriched_events(self.tenant.token)
         for pc in self.config.get("processors", []):
-            p = build_processor(pc)
+            p = build_processor(pc, self)
             p.tenant_engine = self
             self.initialize_nested_component(p, monitor, require=False)
             self.processors.append(p)

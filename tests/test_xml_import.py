@@ -27,7 +27,7 @@ def test_all_reference_templates_import_cleanly():
     assert [s["id"] for s in srcs] == ["protobuf", "json"]
     assert srcs[0]["decoder"] == "protobuf" and srcs[1]["decoder"] == "json"
     assert srcs[0]["receivers"][0] == {"type": "mqtt", "host": "${mqtt.host:localhost}", "port": "${mqtt.port:1883}",
-                                       "topic": "SiteWhere/[[tenant.token]]/input/protobuf", "qos": 1, "numThreads": 1}
+                                       "topic": "SiteWhere/[[tenant.token]]/input/protobuf", "numThreads": 1}
     assert d["inbound-processing"]["processingThreadCount"] == 25
     assert d["device-state"]["presence"] == {"checkInterval": "PT10M", "missingInterval": "PT8H"}
     assert d["device-registration"]["allowNewDevices"] is False
@@ -56,6 +56,82 @@ def test_unknown_elements_are_reported():
     assert doc == {"connectors": [{"id": "m1", "type": "mqtt", "host": "h", "port": 1884,
                                    "topic": "out/[[tenant.token]]"}]}
     assert ctx.warnings == ["outbound-connectors: <mystery-connector> not imported"]
+
+
+def test_receiver_attributes_and_script_ids_import():
+    """MQTT broker attributes (``connector-common.xsd`` mqtt-broker-attributes), socket interaction
+    handler factories, WebSocket client receivers and scripted REST polling come through the import;
+    script ids resolve against script management when the tenant engine builds the source."""
+    xml = b"""<beans xmlns:es="x"><es:event-sources>
+      <es:mqtt-event-source sourceId="m" protocol="tls" hostname="broker" port="8883" username="u" password="p"
+          trustStorePath="/etc/ca.pem" clientId="sw-${tenant.token}" cleanSession="false" qos="EXACTLY_ONCE"
+          topic="in/${tenant.token}" numThreads="3"><es:json-device-request-decoder/></es:mqtt-event-source>
+      <es:socket-event-source sourceId="s" port="9000">
+          <es:groovy-interaction-handler-factory scriptId="sock-handler"/>
+          <es:groovy-event-decoder scriptId="my-decoder"/></es:socket-event-source>
+      <es:web-socket-event-source sourceId="w" webSocketUrl="ws://feed:80/x" payloadType="STRING">
+          <es:header name="Authorization" value="Bearer t"/><es:json-device-request-decoder/>
+      </es:web-socket-event-source>
+      <es:polling-rest-event-source sourceId="r" baseUrl="http://api/v1" pollIntervalMs="5000" scriptId="poller"
+          username="a" password="b"><es:json-device-request-decoder/></es:polling-rest-event-source>
+    </es:event-sources></beans>"""
+    from sitewhere_amd.runtime.xml_import import _Ctx
+    ctx = _Ctx()
+    srcs = {s["id"]: s for s in convert_service("event-sources", xml, ctx)["sources"]}
+    assert ctx.warnings == []
+    assert srcs["m"]["receivers"][0] == {
+        "type": "mqtt", "host": "broker", "port": 8883, "protocol": "tls", "username": "u", "password": "p",
+        "trustStorePath": "/etc/ca.pem", "clientId": "sw-[[tenant.token]]", "cleanSession": "false",
+        "qos": "EXACTLY_ONCE", "topic": "in/[[tenant.token]]", "numThreads": 3}
+    assert srcs["s"]["receivers"][0] == {"type": "socket", "host": "0.0.0.0", "port": 9000, "numThreads": 4,
+                                         "handler": "script", "script": "sock-handler"}
+    assert srcs["s"]["decoder"] == "script" and srcs["s"]["script"] == "my-decoder"
+    assert srcs["w"]["receivers"][0] == {"type": "websocket", "host": "0.0.0.0", "port": 8585, "payloadType": "string",
+                                         "webSocketUrl": "ws://feed:80/x", "headers": {"Authorization": "Bearer t"}}
+    assert srcs["r"]["receivers"][0] == {"type": "rest-poll", "baseUrl": "http://api/v1", "interval": 5.0,
+                                         "username": "a", "password": "b", "scriptId": "poller"}
+
+
+def test_script_ids_resolve_through_script_management():
+    """A source configured with a script id (as imported from the reference) runs the active
+    version stored in script management; activating another version changes the next engine."""
+    import json
+
+    from sitewhere_amd.assembly import SiteWhereInstance
+    from sitewhere_amd.runtime.config import dump_document
+    sw = SiteWhereInstance().start()
+    try:
+        sw.wait_for_tenant("default", 60)
+        sm = sw.instance.scripts
+        v1 = ("import json\ndef decode(payload, metadata):\n    d = json.loads(payload)\n"
+              "    return [{'deviceToken': d['t'], 'type': 'DeviceMeasurement', 'request': {'name': 'v1', 'value': d['v']}}]\n")
+        meta = sm.create_script("default", "event-sources", "my-decoder", "My decoder", v1)
+        es_ms = sw["event-sources"]
+        before = es_ms.get_tenant_engine("default")
+        doc = json.loads(json.dumps(es_ms.tenant_configuration("default")))
+        doc["sources"].append({"id": "scripted", "decoder": "script", "script": "my-decoder", "receivers": []})
+        doc["sources"].append({"id": "inline", "decoder": {"type": "script", "script": v1}, "receivers": []})
+        sw.instance.coord.put(es_ms.tenant_config_path("default"), dump_document(doc))
+        assert wait_for(lambda: (e := es_ms.get_tenant_engine("default")) is not None and e is not before
+                        and e.status.value == "Started" and "scripted" in e.manager.sources)
+        eng = es_ms.get_tenant_engine("default")
+        assert eng.manager.sources["scripted"].decoder.source == v1 == eng.manager.sources["inline"].decoder.source
+        v2 = sm.clone_script("default", "event-sources", "my-decoder", meta.active_version).versions[-1]["versionId"]
+        sm.update_script("default", "event-sources", "my-decoder", v2, v1.replace("'v1'", "'v2'"))
+        sm.activate_script("default", "event-sources", "my-decoder", v2)
+        assert eng.script_source("my-decoder") == v1.replace("'v1'", "'v2'")
+        assert eng.script_source({"scriptId": "my-decoder", "version": meta.active_version}) == v1
+        with pytest.raises(Exception, match="not found"):
+            eng.script_source("no-such-script")
+    finally:
+        sw.stop()
+
+
+def wait_for(cond, t=30.0):
+    end = time.time() + t
+    while time.time() < end and not cond():
+        time.sleep(0.05)
+    return cond()
 
 
 def test_tenant_boots_from_imported_reference_default_template(monkeypatch):
