@@ -17,7 +17,6 @@ import threading
 from ..core.errors import SiteWhereException
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
-from ..edges.receivers import coap_post
 from ..models import wire
 from ..models.domain import ParameterType
 from ..rpc import codec
@@ -160,20 +159,70 @@ class MqttProvider:
 
 
 class CoapProvider:
+    """CoAP request to the device (reference ``CoapCommandDeliveryProvider`` with
+    ``MetadataCoapParameterExtractor``: host, port, resource path and method from device metadata)."""
+
+    _METHODS = {"POST": 2, "PUT": 3}
+
     def deliver(self, nesting, assignment, payload, params):
-        if not coap_post(params["hostname"], int(params["port"]), params.get("path", "commands"), payload):
-            raise SiteWhereException("CoAP delivery not acknowledged")
+        host, port = params.get("hostname"), params.get("port")
+        if not host:
+            raise SiteWhereException("Hostname not found in device metadata. Unable to deliver command.")
+        method = self._METHODS.get(str(params.get("method") or "POST").upper())
+        if method is None:
+            raise SiteWhereException(f"unsupported CoAP delivery method {params.get('method')!r}")
+        from ..edges.receivers import coap_request
+        r = coap_request(host, int(port or 5683), params.get("path") or "commands", payload, method)
+        if r is None or (r["code"] >> 5) != 2:
+            raise SiteWhereException("CoAP delivery not acknowledged" if r is None else
+                                     f"CoAP delivery refused: {r['code'] >> 5}.{r['code'] & 31:02d}")
 
 
 class SmsProvider:
-    """Twilio SMS (reference TwilioCommandDeliveryProvider) -- needs the ``twilio`` module."""
+    """Twilio SMS over its REST API (reference ``twilio/TwilioCommandDeliveryProvider``: the encoded
+    command is the message body, sent ``From`` the configured number ``To`` the number in the
+    gateway's metadata).  ``POST {api}/2010-04-01/Accounts/{sid}/Messages.json`` with HTTP basic
+    auth -- no Twilio SDK needed.  System commands are not delivered by SMS (as in the reference)."""
+
+    def __init__(self, account_sid: str | None, auth_token: str | None, from_phone: str | None,
+                 api_base: str = "https://api.twilio.com", timeout: float = 10.0):
+        if not account_sid:
+            raise SiteWhereException("Twilio command delivery provider missing account SID.")
+        if not auth_token:
+            raise SiteWhereException("Twilio command delivery provider missing auth token.")
+        self.sid, self.from_phone, self.api, self.timeout = account_sid, from_phone, api_base.rstrip("/"), timeout
+        self._auth = "Basic " + base64.b64encode(f"{account_sid}:{auth_token}".encode()).decode()
+        self.sent: list = []
 
     def deliver(self, nesting, assignment, payload, params):
+        import urllib.error
+        import urllib.parse
+        import urllib.request
+        to = params.get("phone")
+        if not to:
+            raise SiteWhereException("No phone number found in device metadata. Unable to deliver.")
+        body = payload.decode() if isinstance(payload, (bytes, bytearray)) else str(payload)
+        req = urllib.request.Request(f"{self.api}/2010-04-01/Accounts/{urllib.parse.quote(self.sid)}/Messages.json",
+                                     data=urllib.parse.urlencode({"To": to, "From": self.from_phone or "",
+                                                                  "Body": body}).encode(),
+                                     headers={"Authorization": self._auth,
+                                              "Content-Type": "application/x-www-form-urlencoded"}, method="POST")
         try:
-            import twilio  # noqa: F401
-        except ImportError as e:
-            raise SiteWhereException("SMS delivery needs the 'twilio' python module") from e
-        raise SiteWhereException("SMS delivery: account credentials not configured")
+            with urllib.request.urlopen(req, timeout=self.timeout) as r:
+                res = json.loads(r.read() or b"{}")
+        except urllib.error.HTTPError as e:
+            try:
+                msg = json.loads(e.read()).get("message", "")
+            except ValueError:
+                msg = ""
+            raise SiteWhereException(f"Unable to send Twilio SMS message: HTTP {e.code} {msg}".strip()) from e
+        except OSError as e:
+            raise SiteWhereException(f"Unable to send Twilio SMS message: {e}") from e
+        self.sent.append(res.get("sid"))
+        return res
+
+    def deliver_system(self, nesting, assignment, payload, params):
+        raise SiteWhereException("system commands are not delivered by SMS")
 
 
 def mqtt_extractor(tenant: str, command_topic: str, system_topic: str):
@@ -206,7 +255,8 @@ class CommandDestination(TenantEngineLifecycleComponent):
 
     def deliver_system_command(self, command, nesting, assignment):
         payload = self.encoder.encode_system(command, nesting)
-        self.provider.deliver(nesting, assignment, payload, self.extractor(nesting, assignment, True))
+        deliver = getattr(self.provider, "deliver_system", self.provider.deliver)
+        deliver(nesting, assignment, payload, self.extractor(nesting, assignment, True))
         self.delivered += 1
 
 
@@ -279,12 +329,15 @@ class CommandDeliveryTenantEngine(MicroserviceTenantEngine):
             extractor = mqtt_extractor(self.tenant.token, dc.get("commandTopic", "SiteWhere/{tenant}/command/{deviceToken}"),
                                        dc.get("systemTopic", "SiteWhere/{tenant}/system/{deviceToken}"))
         elif p == "coap":
-            provider = CoapProvider()
-            extractor = metadata_extractor({"hostname": dc.get("hostnameMetadata", "hostname"),
-                                            "port": dc.get("portMetadata", "port")})
+            provider = CoapProvider()       # metadata field names: MetadataCoapParameterExtractor defaults
+            extractor = metadata_extractor({"hostname": dc.get("hostnameMetadata", "coap_hostname"),
+                                            "port": dc.get("portMetadata", "coap_port"),
+                                            "path": dc.get("urlMetadata", "coap_url"),
+                                            "method": dc.get("methodMetadata", "coap_method")})
         elif p == "sms":
-            provider = SmsProvider()
-            extractor = metadata_extractor({"phone": dc.get("phoneMetadata", "phone")})
+            provider = SmsProvider(dc.get("accountSid"), dc.get("authToken"), dc.get("fromPhone"),
+                                   dc.get("apiBase", "https://api.twilio.com"))
+            extractor = metadata_extractor({"phone": dc.get("phoneMetadata", "sms_phone")})
         else:
             provider = LogProvider()
             extractor = lambda nesting, a, system=False: {}  # noqa: E731
