@@ -1,5 +1,9 @@
 """Python REST client SDK (reference ``sitewhere-client``: ``ISiteWhereClient.java`` / ``SiteWhereClient.java``).
 
+Every ``ISiteWhereClient`` method has a snake_case counterpart here.  The reference SDK predates
+parts of the 2.0 REST API, so its names map onto 2.0 resources: *site* -> area, *hardware id* ->
+device token, asset *module* -> asset type.
+
 Obtains a JWT from ``/sitewhere/authapi/jwt`` with basic credentials, then sends it as a bearer
 token together with the tenant id / tenant auth headers.  ``transport`` may be any object with a
 ``request(method, url, headers=, json=, params=)`` returning an httpx-like response -- an
@@ -76,6 +80,9 @@ class SiteWhereClient:
     # ---- system / users / tenants --------------------------------------------------------------
     def get_version(self):
         return self._call("GET", "/system/version", tenant=False)
+
+    def get_site_where_version(self):
+        return self.get_version()
 
     def list_users(self, page: int = 1, page_size: int = 100):
         return self._call("GET", "/users", params={"page": page, "pageSize": page_size}, tenant=False)
@@ -159,7 +166,122 @@ class SiteWhereClient:
     def create_asset(self, request: dict):
         return self.post("/assets", request)
 
+    def get_device_type_by_token(self, token: str):
+        return self.get_device_type(token)
+
+    def update_device_type(self, token: str, request: dict):
+        return self.put(f"/devicetypes/{token}", request)
+
+    def delete_device_type(self, token: str):
+        return self.delete(f"/devicetypes/{token}")
+
+    def get_device_by_hardware_id(self, token: str):
+        return self.get_device(token)
+
+    def get_current_assignment_for_device(self, device_token: str):
+        return self.get_current_assignment(device_token)
+
+    def list_device_assignment_history(self, device_token: str, **crit):
+        return self.get(f"/devices/{device_token}/assignments", **crit)
+
+    def get_device_assignment_by_token(self, token: str):
+        return self.get_device_assignment(token)
+
+    def update_device_assignment(self, token: str, request: dict):
+        return self.put(f"/assignments/{token}", request)
+
+    def update_device_assignment_metadata(self, token: str, metadata: dict):
+        return self.update_device_assignment(token, {"metadata": metadata})
+
+    def delete_device_assignment(self, token: str):
+        return self.delete(f"/assignments/{token}")
+
+    def get_area_by_token(self, token: str):
+        return self.get(f"/areas/{token}")
+
+    def list_areas(self, **crit):
+        return self.get("/areas", **crit)
+
+    def list_assignments_for_site(self, area_token: str, **crit):
+        return self.get(f"/areas/{area_token}/assignments", **crit)
+
+    def list_zones_for_site(self, area_token: str, **crit):
+        return self.get("/zones", areaToken=area_token, **crit)
+
+    def get_device_group_by_token(self, token: str):
+        return self.get(f"/devicegroups/{token}")
+
+    def list_device_groups(self, **crit):
+        return self.get("/devicegroups", **crit)
+
+    def delete_device_group(self, token: str):
+        return self.delete(f"/devicegroups/{token}")
+
+    def list_device_group_elements(self, group_token: str, **crit):
+        return self.get(f"/devicegroups/{group_token}/elements", **crit)
+
+    def delete_device_group_elements(self, group_token: str, element_ids: list):
+        return self._call("DELETE", f"/devicegroups/{group_token}/elements", element_ids)
+
+    def get_assets_by_module_id(self, asset_type_token: str, **crit):
+        return self.get("/assets", assetTypeToken=asset_type_token, **crit)
+
+    def get_assignments_for_asset(self, asset_token: str, **crit):
+        return self.get("/assignments", assetToken=asset_token, **crit)
+
     # ---- events ------------------------------------------------------------------------------------------
+    def add_device_event_batch(self, device_token: str, batch: dict):
+        """Measurements / locations / alerts for a device's active assignment in one call."""
+        return self.post(f"/devices/{device_token}/batch", batch)
+
+    def create_device_measurements(self, assignment_token: str, request: dict):
+        return self.post(f"/assignments/{assignment_token}/measurements", request)
+
+    def create_device_location(self, assignment_token: str, request: dict):
+        return self.post(f"/assignments/{assignment_token}/locations", request)
+
+    def create_device_alert(self, assignment_token: str, request: dict):
+        return self.post(f"/assignments/{assignment_token}/alerts", request)
+
+    def create_device_command_invocation(self, assignment_token: str, request: dict):
+        return self.post(f"/assignments/{assignment_token}/invocations", request)
+
+    def list_device_measurements(self, assignment_token: str, **crit):
+        return self.list_measurements(assignment_token, **crit)
+
+    def list_device_locations(self, assignment_token: str, **crit):
+        return self.list_locations(assignment_token, **crit)
+
+    def list_device_alerts(self, assignment_token: str, **crit):
+        return self.list_alerts(assignment_token, **crit)
+
+    def list_device_command_invocations(self, assignment_token: str, **crit):
+        return self.get(f"/assignments/{assignment_token}/invocations", **crit)
+
+    def create_device_stream(self, assignment_token: str, request: dict):
+        return self.post(f"/assignments/{assignment_token}/streams", request)
+
+    def get_device_stream(self, assignment_token: str, stream_id: str):
+        return self.get(f"/assignments/{assignment_token}/streams/{stream_id}")
+
+    def list_device_streams(self, assignment_token: str, **crit):
+        return self.get(f"/assignments/{assignment_token}/streams", **crit)
+
+    def add_device_stream_data(self, assignment_token: str, stream_id: str, sequence_number: int, data: bytes):
+        r = self.http.request("POST", f"{self.base}{API}/assignments/{assignment_token}/streams/{stream_id}",
+                              headers=dict(self._headers(), **{"Content-Type": "application/octet-stream"}),
+                              params={"sequenceNumber": int(sequence_number)}, content=bytes(data))
+        self._check(r)
+        return r.json()
+
+    def get_device_stream_data(self, assignment_token: str, stream_id: str, sequence_number: int) -> bytes:
+        return self._call("GET", f"/assignments/{assignment_token}/streams/{stream_id}/data/{int(sequence_number)}",
+                          raw=True)
+
+    def list_device_stream_data(self, assignment_token: str, stream_id: str) -> bytes:
+        """The stream's chunks in sequence order, concatenated."""
+        return self._call("GET", f"/assignments/{assignment_token}/streams/{stream_id}/data", raw=True)
+
     def add_measurement(self, assignment_token: str, name: str, value: float, event_date: int | None = None, **extra):
         return self.post(f"/assignments/{assignment_token}/measurements",
                          {"name": name, "value": value, "eventDate": event_date, **extra})

@@ -389,8 +389,10 @@ class DeviceManagement:
         c = criteria or {}
         st = c.get("status") if isinstance(c, dict) else None
         dev = c.get("deviceId") if isinstance(c, dict) else None
-        dts, cus, ars, ass = (_ids(c.get(k)) if isinstance(c, dict) else set()
-                              for k in ("deviceTypeIds", "customerIds", "areaIds", "assetIds"))
+        # reference criteria carry id lists (DeviceAssignmentSearchCriteria); REST / client filters
+        # name one entity (customerId, areaId, ...) -- both narrow the result
+        dts, cus, ars, ass = ((_ids(c.get(k + "s")) | ({c[k]} if c.get(k) else set())) if isinstance(c, dict)
+                              else set() for k in ("deviceTypeId", "customerId", "areaId", "assetId"))
 
         def pred(a: DeviceAssignment):
             return ((not st or a.status.value == st) and (not dev or a.device_id == dev) and

@@ -492,6 +492,9 @@ def assignments_router() -> APIRouter:
                       ("areaToken", c.dm.get_area_by_token)):
             if crit.get(k):
                 crit[k.replace("Token", "Id")] = _nf(fn(crit.pop(k)), k).id
+        if crit.get("assetToken"):      # assignments reference an asset by id or (cross-service) by token
+            tok = crit.pop("assetToken")
+            crit["assetIds"] = [_nf(c.svc("AssetManagement").get_asset_by_token(tok), "assetToken").id, tok]
         return out(c.dm.list_device_assignments(crit))
 
     @r.get("/{token}")
@@ -587,6 +590,26 @@ def assignments_router() -> APIRouter:
     @r.get("/{token}/streams/{streamId}")
     def get_stream(token: str, streamId: str, c: Ctx = TENANT):
         return out(_nf(c.dm.get_device_stream_by_stream_id(asg(c, token).id, streamId), f"stream {streamId}"))
+
+    # stream chunks as the reference client sends / reads them (``SiteWhereClient.addDeviceStreamData``:
+    # binary POST with ?sequenceNumber, ``getDeviceStreamData`` / ``listDeviceStreamData``)
+    @r.post("/{token}/streams/{streamId}")
+    async def add_stream_data(token: str, streamId: str, sequenceNumber: int, request: Request, c: Ctx = TENANT):
+        data = await request.body()
+        a = asg(c, token)
+        _nf(c.dm.get_device_stream_by_stream_id(a.id, streamId), f"stream {streamId}")
+        return out(c.svc("StreamingMedia").add_device_stream_data(a.id, streamId, sequenceNumber, data))
+
+    @r.get("/{token}/streams/{streamId}/data/{sequenceNumber}")
+    def get_stream_data(token: str, streamId: str, sequenceNumber: int, c: Ctx = TENANT):
+        d = _nf(c.svc("StreamingMedia").get_device_stream_data(asg(c, token).id, streamId, sequenceNumber),
+                f"stream {streamId} chunk {sequenceNumber}")
+        return Response(d.data, media_type="application/octet-stream")
+
+    @r.get("/{token}/streams/{streamId}/data")
+    def list_stream_data(token: str, streamId: str, c: Ctx = TENANT):
+        return Response(c.svc("StreamingMedia").get_stream_content(asg(c, token).id, streamId),
+                        media_type="application/octet-stream")
 
     return r
 

@@ -205,6 +205,69 @@ def test_python_client_sdk(env):
         bad.list_devices()
 
 
+REF_CLIENT = "/root/reference/sitewhere-client/src/main/java/com/sitewhere/spi/ISiteWhereClient.java"
+
+
+def test_python_client_covers_the_reference_client_interface(env):
+    """Every ``ISiteWhereClient`` method has a counterpart, and the ones beyond CRUD basics work
+    against the server: device-type update/delete, assignment history + metadata, per-area
+    assignments and zones, group elements, event batches, invocation lists, stream data."""
+    import os
+    import re
+
+    from sitewhere_amd.client import SiteWhereClient
+    if os.path.exists(REF_CLIENT):
+        names = re.findall(r"^\s*[\w<>, ]+\s([a-z]\w*)\(", open(REF_CLIENT).read(), re.M)
+        snake = {re.sub(r"(?<!^)(?=[A-Z])", "_", n).lower() for n in names}
+        assert len(snake) >= 45
+        missing = sorted(n for n in snake if not hasattr(SiteWhereClient, n))
+        assert missing == [], missing
+    _, client, _ = env
+    c = SiteWhereClient("http://testserver", transport=client)
+    assert c.get_site_where_version()["edition"] == "MI355X"
+    dt = c.create_device_type({"token": "sdk2-type", "name": "SDK2"})
+    assert c.update_device_type("sdk2-type", {"name": "SDK2 renamed"})["name"] == "SDK2 renamed"
+    assert c.get_device_type_by_token("sdk2-type")["id"] == dt["id"]
+    c.create_device({"token": "sdk2-dev", "deviceTypeToken": "sdk2-type"})
+    area = c.list_areas(pageSize=1)["results"][0]
+    a1 = c.create_device_assignment({"token": "sdk2-a1", "deviceToken": "sdk2-dev", "areaToken": area["token"]})
+    c.end_device_assignment("sdk2-a1")
+    c.create_device_assignment({"token": "sdk2-a2", "deviceToken": "sdk2-dev"})
+    hist = [a["token"] for a in c.list_device_assignment_history("sdk2-dev")["results"]]
+    assert set(hist) == {"sdk2-a1", "sdk2-a2"}
+    assert c.get_current_assignment_for_device("sdk2-dev")["token"] == "sdk2-a2"
+    assert c.update_device_assignment_metadata("sdk2-a2", {"k": "v"})["metadata"] == {"k": "v"}
+    in_area = [a["token"] for a in c.list_assignments_for_site(area["token"], pageSize=0)["results"]]
+    assert "sdk2-a1" in in_area and "sdk2-a2" not in in_area
+    assert all(z["areaId"] == area["id"] for z in c.list_zones_for_site(area["token"])["results"])
+    # groups
+    c.create_device_group({"token": "sdk2-g", "name": "G"})
+    els = c.add_device_group_elements("sdk2-g", [{"deviceToken": "sdk2-dev"}])
+    assert c.list_device_group_elements("sdk2-g")["numResults"] == 1
+    c.delete_device_group_elements("sdk2-g", [e["id"] for e in (els["results"] if isinstance(els, dict) else els)])
+    assert c.list_device_group_elements("sdk2-g")["numResults"] == 0
+    c.delete_device_group("sdk2-g")
+    # events
+    c.add_device_event_batch("sdk2-dev", {"measurements": [{"name": "t", "value": 1.5}],
+                                          "locations": [{"latitude": 1.0, "longitude": 2.0}]})
+    assert c.list_device_measurements("sdk2-a2")["results"][0]["value"] == 1.5
+    assert c.list_device_locations("sdk2-a2")["numResults"] == 1
+    c.create_device_alert("sdk2-a2", {"type": "hot", "message": "m", "level": "Warning"})
+    assert c.list_device_alerts("sdk2-a2")["results"][0]["type"] == "hot"
+    # streams + chunks, as the reference client sends them
+    c.create_device_stream("sdk2-a2", {"streamId": "cam", "contentType": "video/h264"})
+    assert c.get_device_stream("sdk2-a2", "cam")["streamId"] == "cam"
+    for seq, chunk in ((1, b"\x00\x01"), (0, b"\xfe\xff"), (2, b"end")):
+        c.add_device_stream_data("sdk2-a2", "cam", seq, chunk)
+    assert c.get_device_stream_data("sdk2-a2", "cam", 1) == b"\x00\x01"
+    assert c.list_device_stream_data("sdk2-a2", "cam") == b"\xfe\xff\x00\x01end"
+    c.delete_device_assignment("sdk2-a1")
+    c.end_device_assignment("sdk2-a2")
+    c.delete_device_assignment("sdk2-a2")
+    c.delete_device("sdk2-dev")
+    c.delete_device_type("sdk2-type")
+
+
 def test_rest_surface_matches_reference_controllers(env):
     """25 reference controllers / 193 endpoint methods (SURVEY §2.3 Web/REST)."""
     sw, _, _ = env
