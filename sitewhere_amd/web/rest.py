@@ -64,6 +64,27 @@ def _date(s):
         return int(_dt.datetime.fromisoformat(str(s).replace("Z", "+00:00")).timestamp() * 1000)
 
 
+_QUERY_ALIASES = {"deviceType": "deviceTypeToken", "customer": "customerToken", "area": "areaToken",
+                  "asset": "assetToken", "areaType": "areaTypeToken", "customerType": "customerTypeToken",
+                  "assetType": "assetTypeToken"}
+
+
+def query_criteria(request: Request, page: int, pageSize: int) -> dict:
+    """Query string -> search criteria: the reference's parameter names (``deviceType``, ...) map
+    to token criteria, ``true``/``false`` become booleans and epoch / ISO-8601 dates integers
+    (query values are strings: ``excludeAssigned=false`` must not read as true)."""
+    crit: dict = {}
+    for k, v in request.query_params.items():
+        k = _QUERY_ALIASES.get(k, k)
+        if isinstance(v, str) and v.lower() in ("true", "false"):
+            v = v.lower() == "true"
+        elif k.endswith(("Date", "After", "Before")) and v:
+            v = _date(v)
+        crit[k] = v
+    crit.update(paging(page, pageSize))
+    return crit
+
+
 def paging(page: int = 1, pageSize: int = 100) -> dict:
     return {"pageNumber": page, "pageSize": pageSize}
 
@@ -206,8 +227,7 @@ def crud_router(path, service, noun, plural, label, by_token, before=None) -> AP
 
     @r.get("")
     def list_(request: Request, page: int = 1, pageSize: int = 100, c: Ctx = TENANT):
-        crit = dict(request.query_params)
-        crit.update(paging(page, pageSize))
+        crit = query_criteria(request, page, pageSize)
         return out(getattr(c.svc(service), f"list_{plural}")(crit))
 
     @r.get("/{token}")
@@ -399,6 +419,43 @@ def device_type_proto(c: Ctx, token: str) -> str:
     return "\n".join(lines) + "\n"
 
 
+def marshal_device(c, d, include_type: bool = False, include_assignment: bool = False) -> dict:
+    """Device JSON with the reference's optional nested objects (``DeviceMarshalHelper``:
+    ``deviceType``, ``assignment`` -- the assignment with its customer / area / asset)."""
+    doc = out(d)
+    if include_type and d.device_type_id:
+        t = c.dm.get_device_type(d.device_type_id)
+        doc["deviceType"] = out(t) if t else None
+    if include_assignment and d.device_assignment_id:
+        a = c.dm.get_device_assignment(d.device_assignment_id)
+        doc["assignment"] = marshal_assignment(c, a, False, True, True, True) if a else None
+    return doc
+
+
+def marshal_assignment(c, a, include_device=False, include_customer=False, include_area=False,
+                       include_asset=False) -> dict:
+    """Assignment JSON with optional ``device`` / ``customer`` / ``area`` / ``asset`` objects
+    (``DeviceAssignmentMarshalHelper``); the asset is looked up by id or token."""
+    doc = out(a)
+    if include_device and a.device_id:
+        d = c.dm.get_device(a.device_id)
+        doc["device"] = out(d) if d else None
+    if include_customer and a.customer_id:
+        cu = c.dm.get_customer(a.customer_id)
+        doc["customer"] = out(cu) if cu else None
+    if include_area and a.area_id:
+        ar = c.dm.get_area(a.area_id)
+        doc["area"] = out(ar) if ar else None
+    if include_asset and a.asset_id:
+        am = c.svc("AssetManagement")
+        asset = am.get_asset(a.asset_id) or am.get_asset_by_token(a.asset_id)
+        if asset is not None:
+            doc["asset"] = out(asset)
+            doc["assetName"] = asset.name
+            doc["assetImageUrl"] = getattr(asset, "image_url", None)
+    return doc
+
+
 def devices_router() -> APIRouter:
     r = APIRouter(prefix=f"{API}/devices", tags=["devices"])
 
@@ -410,10 +467,12 @@ def devices_router() -> APIRouter:
         return out(c.dm.create_device(body))
 
     @r.get("")
-    def list_(request: Request, page: int = 1, pageSize: int = 100, c: Ctx = TENANT):
-        crit = dict(request.query_params)
-        crit.update(paging(page, pageSize))
-        return out(c.dm.list_devices(crit))
+    def list_(request: Request, page: int = 1, pageSize: int = 100, includeDeviceType: bool = False,
+              includeAssignment: bool = False, c: Ctx = TENANT):
+        crit = query_criteria(request, page, pageSize)
+        res = c.dm.list_devices(crit)
+        return {"numResults": res.num_results,
+                "results": [marshal_device(c, d, includeDeviceType, includeAssignment) for d in res.results]}
 
     @r.get("/group/{groupToken}")
     def in_group(groupToken: str, role: str | None = None, c: Ctx = TENANT):
@@ -431,8 +490,8 @@ def devices_router() -> APIRouter:
         return out(SearchResults(len(devs), [d for d in devs if d]))
 
     @r.get("/{token}")
-    def read(token: str, c: Ctx = TENANT):
-        return out(dev(c, token))
+    def read(token: str, includeDeviceType: bool = True, includeAssignment: bool = True, c: Ctx = TENANT):
+        return marshal_device(c, dev(c, token), includeDeviceType, includeAssignment)
 
     @r.put("/{token}")
     def update(token: str, body: dict = Body(...), c: Ctx = TENANT):
@@ -486,8 +545,7 @@ def assignments_router() -> APIRouter:
 
     @r.get("")
     def list_(request: Request, page: int = 1, pageSize: int = 100, c: Ctx = TENANT):
-        crit = dict(request.query_params)
-        crit.update(paging(page, pageSize))
+        crit = query_criteria(request, page, pageSize)
         for k, fn in (("deviceToken", c.dm.get_device_by_token), ("customerToken", c.dm.get_customer_by_token),
                       ("areaToken", c.dm.get_area_by_token)):
             if crit.get(k):
@@ -495,11 +553,14 @@ def assignments_router() -> APIRouter:
         if crit.get("assetToken"):      # assignments reference an asset by id or (cross-service) by token
             tok = crit.pop("assetToken")
             crit["assetIds"] = [_nf(c.svc("AssetManagement").get_asset_by_token(tok), "assetToken").id, tok]
-        return out(c.dm.list_device_assignments(crit))
+        res = c.dm.list_device_assignments(crit)
+        inc = [bool(crit.get(k)) for k in ("includeDevice", "includeCustomer", "includeArea", "includeAsset")]
+        return {"numResults": res.num_results, "results": [marshal_assignment(c, a, *inc) for a in res.results]}
 
     @r.get("/{token}")
-    def read(token: str, c: Ctx = TENANT):
-        return out(asg(c, token))
+    def read(token: str, includeDevice: bool = False, includeCustomer: bool = False, includeArea: bool = False,
+             includeAsset: bool = False, c: Ctx = TENANT):
+        return marshal_assignment(c, asg(c, token), includeDevice, includeCustomer, includeArea, includeAsset)
 
     @r.put("/{token}")
     def update(token: str, body: dict = Body(...), c: Ctx = TENANT):

@@ -268,6 +268,41 @@ def test_python_client_covers_the_reference_client_interface(env):
     c.delete_device_type("sdk2-type")
 
 
+def test_list_query_parameters_and_nested_marshaling(env):
+    """Query strings are typed like the reference's @RequestParam (``excludeAssigned=false`` keeps
+    assigned devices, ``deviceType`` filters by token) and ``include*`` flags nest the related
+    objects (``DeviceMarshalHelper`` / ``DeviceAssignmentMarshalHelper``)."""
+    _, client, h = env
+    allv = client.get(f"{API}/devices", headers=h, params={"pageSize": 0}).json()
+    kept = client.get(f"{API}/devices", headers=h, params={"pageSize": 0, "excludeAssigned": "false"}).json()
+    assert kept["numResults"] == allv["numResults"]
+    free = client.get(f"{API}/devices", headers=h, params={"pageSize": 0, "excludeAssigned": "true"}).json()
+    assert all(not d.get("deviceAssignmentId") for d in free["results"])
+    assert free["numResults"] < allv["numResults"]
+    dt = client.get(f"{API}/devices/meitrack-000", headers=h).json()
+    typed = client.get(f"{API}/devices", headers=h, params={"pageSize": 0, "deviceType": dt["deviceType"]["token"],
+                                                            "includeAssignment": "true"}).json()
+    assert typed["numResults"] >= 1 and all(d["deviceTypeId"] == dt["deviceTypeId"] for d in typed["results"])
+    assert all("assignment" in d for d in typed["results"] if d.get("deviceAssignmentId"))
+    # single device: type + assignment by default, with the assignment's customer / area
+    assert dt["deviceType"]["id"] == dt["deviceTypeId"]
+    assert dt["assignment"]["id"] == dt["deviceAssignmentId"]
+    bare = client.get(f"{API}/devices/meitrack-000", headers=h,
+                      params={"includeDeviceType": "false", "includeAssignment": "false"}).json()
+    assert "deviceType" not in bare and "assignment" not in bare
+    tok = dt["assignment"]["token"]
+    a = client.get(f"{API}/assignments/{tok}", headers=h, params={"includeDevice": "true", "includeCustomer": "true",
+                                                                  "includeArea": "true"}).json()
+    assert a["device"]["token"] == "meitrack-000"
+    if a.get("customerId"):
+        assert a["customer"]["id"] == a["customerId"]
+    if a.get("areaId"):
+        assert a["area"]["id"] == a["areaId"]
+    listed = client.get(f"{API}/assignments", headers=h, params={"deviceToken": "meitrack-000",
+                                                                 "includeDevice": "true"}).json()
+    assert listed["results"] and all(x["device"]["token"] == "meitrack-000" for x in listed["results"])
+
+
 def test_rest_surface_matches_reference_controllers(env):
     """25 reference controllers / 193 endpoint methods (SURVEY §2.3 Web/REST)."""
     sw, _, _ = env
