@@ -212,6 +212,78 @@ FAMILIES = [
 ]
 
 
+def _one(field, getter, service="DeviceManagement"):
+    def resolve(c, e):
+        v = getattr(e, field, None)
+        return getattr(c.svc(service), getter)(v) if v else None
+    return resolve
+
+
+def _many(field, getter, service="DeviceManagement"):
+    def resolve(c, e):
+        fn = getattr(c.svc(service), getter)
+        return [x for x in (fn(i) for i in (getattr(e, field, None) or [])) if x is not None]
+    return resolve
+
+
+def _asset(c, e):
+    if not getattr(e, "asset_id", None):
+        return None
+    am = c.svc("AssetManagement")
+    return am.get_asset(e.asset_id) or am.get_asset_by_token(e.asset_id)
+
+
+def _state_events(c, s):
+    """DeviceStateMarshalHelper includeEventDetails: the events behind the state's last-event ids."""
+    get = c.em.get_device_event_by_id
+    loc = get(s.last_location_event_id) if s.last_location_event_id else None
+    return {"lastLocationEvent": out(loc) if loc else None,
+            "lastMeasurementEvents": {k: out(get(v)) for k, v in (s.last_measurement_event_ids or {}).items()},
+            "lastAlertEvents": {k: out(get(v)) for k, v in (s.last_alert_event_ids or {}).items()}}
+
+
+# the reference's marshal helpers: query flag -> (JSON key, resolver) per resource
+INCLUDES = {
+    "areas": {"includeAreaType": ("areaType", _one("area_type_id", "get_area_type")),
+              "includeParentArea": ("parentArea", _one("parent_area_id", "get_area")),
+              "includeZones": ("zones", lambda c, e: c.dm.list_zones({"areaId": e.id, "pageSize": 0}).results)},
+    "customers": {"includeCustomerType": ("customerType", _one("customer_type_id", "get_customer_type")),
+                  "includeParentCustomer": ("parentCustomer", _one("parent_customer_id", "get_customer"))},
+    "assets": {"includeAssetType": ("assetType", _one("asset_type_id", "get_asset_type", "AssetManagement"))},
+    "areatypes": {"includeContainedAreaTypes": ("containedAreaTypes", _many("contained_area_type_ids",
+                                                                             "get_area_type"))},
+    "customertypes": {"includeContainedCustomerTypes": ("containedCustomerTypes",
+                                                        _many("contained_customer_type_ids", "get_customer_type"))},
+    "devicestates": {"includeDevice": ("device", _one("device_id", "get_device")),
+                     "includeDeviceType": ("deviceType", _one("device_type_id", "get_device_type")),
+                     "includeDeviceAssignment": ("deviceAssignment", _one("device_assignment_id", "get_device_assignment")),
+                     "includeCustomer": ("customer", _one("customer_id", "get_customer")),
+                     "includeArea": ("area", _one("area_id", "get_area")),
+                     "includeAsset": ("asset", _asset),
+                     "includeEventDetails": (None, _state_events)},
+    "batchelements": {"includeDevice": ("device", _one("device_id", "get_device"))},
+    "invocations": {"includeCommand": ("command", _one("device_command_id", "get_device_command"))},
+}
+
+
+def nested(c, kind: str, entity, flags) -> dict:
+    """``out(entity)`` plus the related objects the truthy ``include*`` flags ask for."""
+    doc = out(entity)
+    for flag, (key, resolve) in INCLUDES.get(kind, {}).items():
+        v = flags.get(flag)
+        if v is True or (isinstance(v, str) and v.lower() == "true"):
+            r = resolve(c, entity)
+            if key is None:
+                doc.update(r)
+            else:
+                doc[key] = out(r) if r is not None else None
+    return doc
+
+
+def nested_results(c, kind: str, res, flags) -> dict:
+    return {"numResults": res.num_results, "results": [nested(c, kind, e, flags) for e in res.results]}
+
+
 def crud_router(path, service, noun, plural, label, by_token, before=None) -> APIRouter:
     r = APIRouter(prefix=f"{API}/{path}", tags=[path])
 
@@ -228,11 +300,11 @@ def crud_router(path, service, noun, plural, label, by_token, before=None) -> AP
     @r.get("")
     def list_(request: Request, page: int = 1, pageSize: int = 100, c: Ctx = TENANT):
         crit = query_criteria(request, page, pageSize)
-        return out(getattr(c.svc(service), f"list_{plural}")(crit))
+        return nested_results(c, path, getattr(c.svc(service), f"list_{plural}")(crit), crit)
 
     @r.get("/{token}")
-    def read(token: str, c: Ctx = TENANT):
-        return out(get(c, token))
+    def read(token: str, request: Request, c: Ctx = TENANT):
+        return nested(c, path, get(c, token), request.query_params)
 
     @r.put("/{token}")
     def update(token: str, body: dict = Body(...), c: Ctx = TENANT):
@@ -268,12 +340,16 @@ def add_index_event_routes(r: APIRouter, index: str, getter):
             return handler
         r.add_api_route(f"/{{token}}/{kind}", make(), methods=["GET"])
 
-    def assignments(token: str, page: int = 1, pageSize: int = 100, status: str | None = None, c: Ctx = TENANT):
+    def assignments(token: str, page: int = 1, pageSize: int = 100, status: str | None = None,
+                    includeDevice: bool = False, includeCustomer: bool = False, includeArea: bool = False,
+                    includeAsset: bool = False, c: Ctx = TENANT):
         ent = getter(c, token)
         crit = {f"{index.lower()}Id": ent.id, **paging(page, pageSize)}
         if status:
             crit["status"] = status
-        return out(c.dm.list_device_assignments(crit))
+        res = c.dm.list_device_assignments(crit)
+        return {"numResults": res.num_results, "results": [
+            marshal_assignment(c, a, includeDevice, includeCustomer, includeArea, includeAsset) for a in res.results]}
     r.add_api_route("/{token}/assignments", assignments, methods=["GET"])
 
 
@@ -589,11 +665,12 @@ def assignments_router() -> APIRouter:
     adders = {"measurements": "add_measurements", "locations": "add_locations", "alerts": "add_alerts",
               "statechanges": "add_state_changes", "responses": "add_command_responses"}
     for kind, fn in EVENT_KINDS.items():
-        def make_get(fn=fn):
-            def h(token: str, page: int = 1, pageSize: int = 100, startDate: str | None = None,
+        def make_get(fn=fn, kind=kind):
+            def h(token: str, request: Request, page: int = 1, pageSize: int = 100, startDate: str | None = None,
                   endDate: str | None = None, c: Ctx = TENANT):
-                return out(getattr(c.em, fn)("Assignment", [asg(c, token).id],
-                                             date_paging(page, pageSize, startDate, endDate)))
+                return nested_results(c, kind, getattr(c.em, fn)("Assignment", [asg(c, token).id],
+                                                                 date_paging(page, pageSize, startDate, endDate)),
+                                      request.query_params)
             return h
         r.add_api_route(f"/{{token}}/{kind}", make_get(), methods=["GET"])
         if kind in adders:
@@ -708,8 +785,9 @@ def misc_router(web: WebRest) -> APIRouter:
 
     # device states ----------------------------------------------------------------------
     @r.post("/devicestates/search")
-    def states(body: dict = Body({}), c: Ctx = TENANT):
-        return out(c.svc("DeviceStateManagement").search_device_states(body))
+    def states(request: Request, body: dict = Body({}), c: Ctx = TENANT):
+        return nested_results(c, "devicestates", c.svc("DeviceStateManagement").search_device_states(body),
+                              request.query_params)
 
     # batch operations ----------------------------------------------------------------------
     @r.get("/batch")
@@ -721,9 +799,10 @@ def misc_router(web: WebRest) -> APIRouter:
         return out(_nf(c.svc("BatchManagement").get_batch_operation_by_token(token), f"batch {token}"))
 
     @r.get("/batch/{token}/elements")
-    def batch_elements(token: str, page: int = 1, pageSize: int = 100, c: Ctx = TENANT):
+    def batch_elements(token: str, request: Request, page: int = 1, pageSize: int = 100, c: Ctx = TENANT):
         op = _nf(c.svc("BatchManagement").get_batch_operation_by_token(token), f"batch {token}")
-        return out(c.svc("BatchManagement").list_batch_operation_elements(op.id, paging(page, pageSize)))
+        return nested_results(c, "batchelements", c.svc("BatchManagement").list_batch_operation_elements(
+            op.id, paging(page, pageSize)), request.query_params)
 
     def _device_ids(c, tokens):
         return [_nf(c.dm.get_device_by_token(t), f"device {t}").id for t in tokens]

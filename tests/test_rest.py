@@ -303,6 +303,45 @@ def test_list_query_parameters_and_nested_marshaling(env):
     assert listed["results"] and all(x["device"]["token"] == "meitrack-000" for x in listed["results"])
 
 
+def test_include_flags_on_areas_customers_states_and_invocations(env):
+    _, client, h = env
+    area = client.get(f"{API}/areas", headers=h, params={"pageSize": 1}).json()["results"][0]
+    a = client.get(f"{API}/areas/{area['token']}", headers=h,
+                   params={"includeAreaType": "true", "includeZones": "true"}).json()
+    assert a["areaType"]["id"] == a["areaTypeId"]
+    assert all(z["areaId"] == a["id"] for z in a["zones"])
+    cus = client.get(f"{API}/customers", headers=h, params={"pageSize": 0, "includeCustomerType": "true"}).json()
+    assert cus["results"] and all(x["customerType"]["id"] == x["customerTypeId"]
+                                  for x in cus["results"] if x.get("customerTypeId"))
+    asg = client.get(f"{API}/areas/{area['token']}/assignments", headers=h, params={"includeDevice": "true"}).json()
+    assert all(x["device"]["id"] == x["deviceId"] for x in asg["results"])
+    # a measurement makes a device state; the state nests its device and the event behind it
+    tok = client.get(f"{API}/devices/meitrack-001", headers=h).json()["assignment"]["token"]
+    client.post(f"{API}/assignments/{tok}/measurements", headers=h, json={"name": "fuel", "value": 0.5})
+    import time
+    end, states = time.time() + 20, []
+    while time.time() < end:
+        states = [st for st in client.post(f"{API}/devicestates/search", headers=h, json={"pageSize": 0},
+                                           params={"includeDevice": "true", "includeEventDetails": "true"}).json()[
+            "results"] if (st.get("device") or {}).get("token") == "meitrack-001" and
+            "fuel" in (st.get("lastMeasurementEvents") or {})]
+        if states:
+            break
+        time.sleep(0.1)
+    assert states and states[0]["lastMeasurementEvents"]["fuel"]["value"] == 0.5
+    cmd = client.get(f"{API}/commands", headers=h, params={"pageSize": 1}).json()["results"][0]
+    dev_type = client.get(f"{API}/devicetypes", headers=h, params={"pageSize": 0}).json()["results"]
+    dt = next(t for t in dev_type if t["id"] == cmd["deviceTypeId"])
+    dev = client.get(f"{API}/devices", headers=h, params={"deviceType": dt["token"], "excludeAssigned": "false",
+                                                          "includeAssignment": "true", "pageSize": 0}).json()
+    target = next(d for d in dev["results"] if d.get("assignment"))
+    client.post(f"{API}/assignments/{target['assignment']['token']}/invocations", headers=h,
+                json={"commandToken": cmd["token"], "parameterValues": {}})
+    inv = client.get(f"{API}/assignments/{target['assignment']['token']}/invocations", headers=h,
+                     params={"includeCommand": "true"}).json()
+    assert inv["results"] and inv["results"][0]["command"]["token"] == cmd["token"]
+
+
 def test_rest_surface_matches_reference_controllers(env):
     """25 reference controllers / 193 endpoint methods (SURVEY §2.3 Web/REST)."""
     sw, _, _ = env
