@@ -19,9 +19,9 @@ from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleCompon
 from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
 from ..models import wire
 from ..models.domain import ParameterType
-from ..rpc import codec
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 _CONVERT = {
     ParameterType.Double: float, ParameterType.Float: float, ParameterType.Bool: lambda v: str(v).lower() in ("1", "true"),
@@ -348,14 +348,12 @@ class CommandDeliveryTenantEngine(MicroserviceTenantEngine):
 
     def _process(self, recs):
         for r in recs:
-            m = json.loads(r.value)
-            ev = codec.from_wire(m["event"])
+            ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
             try:
                 self.deliver_command(ev)
             except Exception as e:  # noqa: BLE001
                 self.undelivered += 1
-                self.ms.producer.send(self.t_undelivered, ev.device_id,
-                                      json.dumps({"event": m["event"], "context": m.get("context"), "error": str(e)}).encode())
+                self.ms.producer.send(self.t_undelivered, ev.device_id, payloads.encode_enriched(ev, ctx, str(e)))
 
     def deliver_command(self, invocation) -> int:
         dm = self._dm()

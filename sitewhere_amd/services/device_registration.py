@@ -7,12 +7,11 @@ default device type / customer / area), assign it if unassigned, acknowledge to 
 """
 from __future__ import annotations
 
-import json
 
 from ..core.errors import SiteWhereException
-from ..rpc import codec
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 NEW_REGISTRATION, ALREADY_REGISTERED, REGISTRATION_ERROR = "NEW_REGISTRATION", "ALREADY_REGISTERED", "REGISTRATION_ERROR"
 
@@ -67,7 +66,7 @@ class RegistrationManager:
             return False
         n = self.engine.ms.instance.naming
         self.engine.ms.producer.send(n.inbound_reprocess_events(self.engine.tenant.token), payload["deviceToken"],
-                                     json.dumps(codec.to_wire(payload)).encode())
+                                     payloads.encode_inbound(payload))
         return True
 
 
@@ -83,7 +82,7 @@ class DeviceRegistrationTenantEngine(MicroserviceTenantEngine):
 
     def _on_reg(self, recs):
         for r in recs:
-            p = codec.from_wire(json.loads(r.value))
+            p = payloads.decode_inbound(r.value, registration=True)
             try:
                 self.manager.handle_device_registration(p["deviceToken"], p["eventCreateRequest"]["request"])
             except SiteWhereException:
@@ -91,7 +90,7 @@ class DeviceRegistrationTenantEngine(MicroserviceTenantEngine):
 
     def _on_unreg(self, recs):
         for r in recs:
-            self.manager.handle_unregistered_event(codec.from_wire(json.loads(r.value)))
+            self.manager.handle_unregistered_event(payloads.decode_inbound(r.value))
 
     def tenant_start(self, monitor):
         self.start_nested_component(self.reg_consumer, monitor, require=True)

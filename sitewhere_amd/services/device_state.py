@@ -13,16 +13,15 @@ engine's two-pass merge, so batch and stream processing agree; the reference kee
 """
 from __future__ import annotations
 
-import json
 import re
 import threading
 
 from ..core.errors import ErrorCode
 from ..models.domain import DeviceEventType, DeviceState, SearchResults, now_ms
 from ..persistence.store import create_store
-from ..rpc import codec
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 from .common import Crud, criteria_of
 
 _ISO = re.compile(r"P(?:(\d+)D)?(?:T(?:(\d+)H)?(?:(\d+)M)?(?:(\d+)S)?)?")
@@ -162,8 +161,8 @@ class DeviceStateTenantEngine(MicroserviceTenantEngine):
 
     def _process(self, recs):
         for r in recs:
-            m = json.loads(r.value)
-            self.management.merge_event(codec.from_wire(m["event"]), m.get("context", {}))
+            ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
+            self.management.merge_event(ev, ctx)
 
     def tenant_start(self, monitor):
         self.start_nested_component(self.consumer, monitor, require=True)

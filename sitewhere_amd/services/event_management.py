@@ -10,15 +10,14 @@ ListCommandResponsesForInvocation, ListCommandResponsesForIndex.
 """
 from __future__ import annotations
 
-import json
 
 from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
 from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceCommandInvocation,
                              DeviceCommandResponse, DeviceEvent, DeviceEventIndex, DeviceEventType, DeviceLocation,
                              DeviceMeasurement, DeviceStateChange, now_ms)
 from ..persistence.events import BufferedEventWriter, DeviceEventStore, create_event_store
-from ..rpc import codec
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 _BASE = ("alternateId", "eventDate", "metadata", "updateState")
 
@@ -206,8 +205,7 @@ class EventManagementTenantEngine(MicroserviceTenantEngine):
 
         def triggers(events):
             """KafkaEventPersistenceTriggers: forward each persisted event keyed by assignment id."""
-            prod.send_batch(topic, [(e.device_assignment_id, json.dumps({"event": codec.to_wire(e)}).encode())
-                                    for e in events])
+            prod.send_batch(topic, [(e.device_assignment_id, payloads.encode_persisted(e)) for e in events])
 
         dm_api = lambda: self.ms.api("DeviceManagement", self.tenant.token)  # noqa: E731
         cache: dict = {}

@@ -25,6 +25,7 @@ from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleCompon
 from ..models import wire
 from ..rpc import codec
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 RAW_PAYLOADS = "event-source-raw-payloads"
 
@@ -328,7 +329,7 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
     def handle_decoded_event(self, source_id: str, req: dict):
         payload = {"sourceId": source_id, "deviceToken": req["deviceToken"], "originator": req.get("originator"),
                    "eventCreateRequest": {"type": req["type"], "request": req["request"]}}
-        body = json.dumps(codec.to_wire(payload)).encode()
+        body = payloads.encode_inbound(payload)
         if req["type"] == "RegisterDevice":
             self.producer.send(self.t_registration, req["deviceToken"], body)
         else:

@@ -40,6 +40,7 @@ from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
 from ..utils import IndexMap, retain_large_allocations
 from ..runtime.consumers import BusConsumer, RetryFrom
+from ..bus import payloads
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
 from .inbound_processing import InboundProcessingTenantEngine
 
@@ -551,7 +552,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if events:
             self.ms.producer.send_batch(self.t_enriched, [
                 (self._dev_tokens.get(self.dev_index.idx.get(e.device_id, -1)) or e.device_id,
-                 json.dumps({"event": codec.to_wire(e), "context": self._context(e)}).encode()) for e in events])
+                 payloads.encode_enriched(e, self._context(e))) for e in events])
 
     def _name(self, nid: int) -> str:
         if nid == NO_NAME:
@@ -623,7 +624,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     continue
                 body = {"sourceId": "gpu-inbound", "deviceToken": q["deviceToken"], "originator": q.get("originator"),
                         "eventCreateRequest": {"type": q["type"], "request": q["request"]}}
-                wire_body = json.dumps(codec.to_wire(body)).encode()
+                wire_body = payloads.encode_inbound(body)
                 if q["type"] == "RegisterDevice":
                     self.ms.producer.send(self.t_registration, q["deviceToken"], wire_body)
                 elif q["type"] in ("Acknowledge", "DeviceStream", "DeviceStreamData", "SendDeviceStreamData"):

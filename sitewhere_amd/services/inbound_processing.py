@@ -23,6 +23,7 @@ from ..models.domain import DeviceAssignmentStatus, DeviceEventType
 from ..rpc import codec
 from ..runtime.consumers import BusConsumer, NearCache
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 _ADDERS = {
     "DeviceMeasurement": "add_measurements", "DeviceLocation": "add_locations", "DeviceAlert": "add_alerts",
@@ -104,7 +105,7 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
         order: list = []
         for r in recs:
             try:
-                p = codec.from_wire(json.loads(r.value))
+                p = payloads.decode_inbound(r.value)
                 a = self._validate(p)
                 if a is None:
                     continue
@@ -147,7 +148,7 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
             a = self.assignment(device.device_assignment_id)
         if device is None or a is None or a.status == DeviceAssignmentStatus.Released:
             self.unregistered.mark()
-            self.ms.producer.send(self.t_unregistered, token, json.dumps(codec.to_wire(p)).encode())
+            self.ms.producer.send(self.t_unregistered, token, payloads.encode_inbound(p))
             return None
         return a
 
@@ -196,7 +197,7 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
     def _process_persisted(self, recs):
         out, cmds = [], []
         for r in recs:
-            ev = codec.from_wire(json.loads(r.value)["event"])
+            ev = payloads.decode_persisted(r.value)
             a = self.assignment(ev.device_assignment_id)
             if a is None:
                 continue
@@ -205,7 +206,7 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
                    "deviceTypeId": a.device_type_id, "parentDeviceId": dev.parent_device_id if dev else None,
                    "deviceStatus": dev.status if dev else None, "deviceMetadata": dev.metadata if dev else {},
                    "assignmentStatus": a.status.value, "assignmentMetadata": a.metadata}
-            body = json.dumps({"event": codec.to_wire(ev), "context": ctx}).encode()
+            body = payloads.encode_enriched(ev, ctx)
             key = ctx["deviceToken"] or a.device_id
             out.append((key, body))
             if ev.event_type == DeviceEventType.CommandInvocation:

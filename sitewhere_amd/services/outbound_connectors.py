@@ -18,9 +18,9 @@ import urllib.request
 
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
-from ..rpc import codec
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 
 class OutboundConnector(TenantEngineLifecycleComponent):
@@ -237,8 +237,8 @@ class OutboundConnectorsTenantEngine(MicroserviceTenantEngine):
         def handle(recs):
             items = []
             for r in recs:
-                m = json.loads(r.value)
-                items.append((codec.from_wire(m["event"]), m.get("context", {})))
+                ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
+                items.append((ev, ctx))
             c.process_batch(items)
         return handle
 

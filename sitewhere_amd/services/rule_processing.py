@@ -9,14 +9,13 @@ processor; the zone test batches its point-in-polygon work onto the GPU when ava
 """
 from __future__ import annotations
 
-import json
 
 from ..core.geo import batch_contains, polygon_of
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..models.domain import DeviceEventType
-from ..rpc import codec
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
+from ..bus import payloads
 
 
 class RuleProcessor(TenantEngineLifecycleComponent):
@@ -151,8 +150,8 @@ class RuleProcessingTenantEngine(MicroserviceTenantEngine):
         def handle(recs):
             items = []
             for r in recs:
-                m = json.loads(r.value)
-                items.append((codec.from_wire(m["event"]), m.get("context", {})))
+                ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
+                items.append((ev, ctx))
             p.process_batch(items)
         return handle
 
