@@ -349,6 +349,14 @@ class DeviceStreamData(Model):
         d["data"] = base64.b64encode(self.data or b"").decode()
         return d
 
+    @classmethod
+    def from_dict(cls, d: dict | None):
+        m = super().from_dict(d)
+        if m is not None and isinstance(m.data, str):      # stored documents carry the chunk as base64
+            import base64
+            m.data = base64.b64decode(m.data)
+        return m
+
 
 @dataclass
 class CustomerType(BrandedEntity):

@@ -10,12 +10,12 @@
 from __future__ import annotations
 
 import json
-import threading
 import urllib.parse
 import urllib.request
 
 from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
 from ..models.domain import DeviceStreamData, Label, SearchResults, now_ms
+from ..persistence.store import create_store
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
 from .qrcode import QrCode
 
@@ -86,12 +86,17 @@ class LabelGenerationMicroservice(MultitenantMicroservice):
 
 # ============================================================================ streaming media
 class DeviceStreamManager:
-    """Stream data chunks per (assignment, stream) with ordered reassembly."""
+    """Stream data chunks per (assignment, stream), reassembled in sequence order
+    (``DeviceStreamManager.java``).  Chunks live in the tenant's configured datastore (memory, SQLite,
+    MongoDB...; the reference's Mongo / Cassandra stream stores throw "not supported"), keyed by
+    (assignment, stream, sequence number) so a re-sent chunk replaces itself."""
 
-    def __init__(self, engine):
+    COLLECTION = "deviceStreamData"
+
+    def __init__(self, engine, store=None):
         self._e = engine
-        self._data: dict[tuple, dict[int, DeviceStreamData]] = {}
-        self._lock = threading.Lock()
+        self._store = store or create_store("memory")
+        self._store.register(self.COLLECTION, DeviceStreamData, ())
 
     def _dm(self):
         return self._e.ms.api("DeviceManagement", self._e.tenant.token)
@@ -108,23 +113,26 @@ class DeviceStreamManager:
                                                            "metadata": request.get("metadata", {})})
         return {"streamId": request["streamId"], "state": "STREAM_CREATED"}
 
+    @staticmethod
+    def _key(assignment_id: str, stream_id: str, seq: int) -> str:
+        return f"{assignment_id}:{stream_id}:{int(seq)}"
+
     def add_device_stream_data(self, assignment_id: str, stream_id: str, sequence_number: int, data: bytes,
                                event_date: int | None = None) -> DeviceStreamData:
         if self._dm().get_device_stream_by_stream_id(assignment_id, stream_id) is None:
             raise SiteWhereSystemException(ErrorCode.InvalidStreamId, detail=stream_id)
-        d = DeviceStreamData(device_assignment_id=assignment_id, stream_id=stream_id, sequence_number=int(sequence_number),
-                             data=bytes(data), event_date=event_date or now_ms(), received_date=now_ms())
-        with self._lock:
-            self._data.setdefault((assignment_id, stream_id), {})[d.sequence_number] = d
-        return d
+        d = DeviceStreamData(id=self._key(assignment_id, stream_id, sequence_number),
+                             device_assignment_id=assignment_id, stream_id=stream_id,
+                             sequence_number=int(sequence_number), data=bytes(data),
+                             event_date=event_date or now_ms(), received_date=now_ms())
+        return self._store.put(self.COLLECTION, d)
 
     def get_device_stream_data(self, assignment_id: str, stream_id: str, sequence_number: int):
-        with self._lock:
-            return self._data.get((assignment_id, stream_id), {}).get(int(sequence_number))
+        return self._store.get(self.COLLECTION, self._key(assignment_id, stream_id, sequence_number))
 
     def list_device_stream_data(self, assignment_id: str, stream_id: str) -> SearchResults:
-        with self._lock:
-            chunks = sorted(self._data.get((assignment_id, stream_id), {}).values(), key=lambda d: d.sequence_number)
+        chunks = self._store.query(self.COLLECTION, lambda d: d.device_assignment_id == assignment_id and
+                                   d.stream_id == stream_id, sort_key=lambda d: d.sequence_number)
         return SearchResults(len(chunks), chunks)
 
     def get_stream_content(self, assignment_id: str, stream_id: str) -> bytes:
@@ -133,7 +141,9 @@ class DeviceStreamManager:
 
 class StreamingMediaTenantEngine(MicroserviceTenantEngine):
     def tenant_initialize(self, monitor):
-        self.api = {"StreamingMedia": DeviceStreamManager(self)}
+        ds = self.config.get("datastore", {"type": "memory"})
+        store = create_store(ds.get("type", "memory"), **{k: v for k, v in ds.items() if k != "type"})
+        self.api = {"StreamingMedia": DeviceStreamManager(self, store)}
 
 
 class StreamingMediaMicroservice(MultitenantMicroservice):

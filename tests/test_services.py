@@ -242,6 +242,25 @@ def test_streaming_media_chunks(sw):
         as_system(sw, lambda: sm.add_device_stream_data(dev.device_assignment_id, "nope", 1, b"x"))
 
 
+def test_stream_chunks_are_durable_in_the_configured_datastore(tmp_path):
+    """Chunks go to the tenant's datastore (SQLite here): a new manager over the same file --
+    a restarted streaming-media engine -- reassembles the stream; a re-sent chunk replaces itself."""
+    from types import SimpleNamespace
+
+    from sitewhere_amd.persistence.store import create_store
+    from sitewhere_amd.services.labels_media_search import DeviceStreamManager
+    dm = SimpleNamespace(get_device_stream_by_stream_id=lambda a, s: object())
+    eng = SimpleNamespace(ms=SimpleNamespace(api=lambda *a: dm), tenant=SimpleNamespace(token="t"))
+    path = str(tmp_path / "media.db")
+    m1 = DeviceStreamManager(eng, create_store("sqlite", path=path))
+    for seq, chunk in ((3, b"!"), (1, b"\x00bin"), (2, b"ary"), (2, b"ARY")):
+        m1.add_device_stream_data("asg-1", "cam", seq, chunk)
+    m2 = DeviceStreamManager(eng, create_store("sqlite", path=path))
+    assert m2.get_stream_content("asg-1", "cam") == b"\x00binARY!"
+    assert m2.get_device_stream_data("asg-1", "cam", 1).data == b"\x00bin"
+    assert m2.list_device_stream_data("asg-1", "cam").num_results == 3
+
+
 def test_event_search_providers(sw):
     es = sw.tenant_engine("event-sources")
     dm = sw.api("DeviceManagement", "default")
