@@ -234,22 +234,27 @@ class BusConsumer(TenantEngineLifecycleComponent):
 
 
 class NearCache:
-    """Thread-safe LRU with TTL (reference near cache: 10,000 entries, TTL 60 s)."""
+    """Thread-safe LRU with TTL and max-idle expiry (reference near cache,
+    ``HazelcastManager.java:107-120``: LRU 10,000 entries, TTL 60 s, max-idle 20 s).  Entries are
+    also invalidated explicitly from the device-model change feed."""
 
-    def __init__(self, capacity: int = 10_000, ttl_s: float = 60.0):
-        self.capacity, self.ttl = capacity, ttl_s
-        self._d: OrderedDict = OrderedDict()
+    def __init__(self, capacity: int = 10_000, ttl_s: float = 60.0, max_idle_s: float | None = 20.0):
+        self.capacity, self.ttl, self.max_idle = capacity, ttl_s, max_idle_s
+        self._d: OrderedDict = OrderedDict()        # key -> [value, created, last access]
         self._lock = threading.Lock()
         self.hits = self.misses = 0
 
     def get(self, key, loader=None):
         # Lock-free hit path (dict reads are atomic under the GIL); recency is refreshed on put, so
         # eviction is insertion-ordered with TTL -- taking a lock per hit serialised every consumer
-        # thread on this cache.
+        # thread on this cache.  The access stamp is a plain store into the entry.
         v = self._d.get(key)
-        if v is not None and time.time() - v[1] < self.ttl:
-            self.hits += 1
-            return v[0]
+        if v is not None:
+            now = time.time()
+            if now - v[1] < self.ttl and (self.max_idle is None or now - v[2] < self.max_idle):
+                v[2] = now
+                self.hits += 1
+                return v[0]
         self.misses += 1
         if loader is None:
             return None
@@ -260,7 +265,8 @@ class NearCache:
 
     def put(self, key, val):
         with self._lock:
-            self._d[key] = (val, time.time())
+            now = time.time()
+            self._d[key] = [val, now, now]
             self._d.move_to_end(key)
             while len(self._d) > self.capacity:
                 self._d.popitem(last=False)

@@ -487,3 +487,29 @@ def test_columnar_store_retention_evicts_oldest_batches():
     rows = np.zeros(4096, OUT_REC)
     one.add_columnar(encode_batch("b", 0, 1, 0, 1, rows, {}, {}))
     assert one.rows == 4096                              # a batch larger than the window is kept whole
+
+
+def test_near_cache_lru_ttl_and_max_idle(monkeypatch):
+    """Reference near-cache policy (HazelcastManager: LRU, TTL 60 s, max-idle 20 s)."""
+    import sitewhere_amd.runtime.consumers as cons
+    now = [1000.0]
+    monkeypatch.setattr(cons.time, "time", lambda: now[0])
+    c = cons.NearCache(capacity=2, ttl_s=60.0, max_idle_s=20.0)
+    loads = []
+    load = lambda k: loads.append(k) or f"v-{k}"  # noqa: E731
+    assert c.get("a", load) == "v-a" and c.get("a", load) == "v-a" and loads == ["a"]
+    now[0] += 15
+    assert c.get("a", load) == "v-a" and loads == ["a"]          # touched: idle clock restarts
+    now[0] += 15
+    assert c.get("a", load) == "v-a" and loads == ["a"]
+    now[0] += 21
+    assert c.get("a", load) == "v-a" and loads == ["a", "a"]     # idle > 20 s: reloaded
+    for _ in range(5):                                           # busy entry still expires at the TTL
+        now[0] += 15
+        c.get("a", load)
+    assert loads.count("a") == 3
+    c.get("b", load)
+    c.get("c", load)                                             # capacity 2: oldest insert evicted
+    assert len(c) == 2 and c.get("a") is None
+    c.invalidate("b")
+    assert c.get("b") is None
