@@ -78,6 +78,39 @@ int32_t sw_partition_for_key(const uint8_t* key, int32_t len, int32_t n_partitio
   return (int32_t)(((uint32_t)sw_murmur2(key, len) & 0x7fffffffu) % (uint32_t)n_partitions);
 }
 
+// Device token (body field 1, hardwareId) of one delimited Header + body device payload; false when
+// the payload does not parse that far.
+static bool sw_payload_token(const uint8_t* buf, uint32_t start, uint32_t end, uint32_t* off, uint32_t* len) {
+  uint32_t pos = start;
+  uint64_t hlen = 0, blen = 0;
+  if (!sw_read_varint(buf, &pos, end, &hlen) || hlen > (uint64_t)(end - pos)) return false;
+  pos += (uint32_t)hlen;
+  if (!sw_read_varint(buf, &pos, end, &blen) || blen > (uint64_t)(end - pos)) return false;
+  const uint32_t bend = pos + (uint32_t)blen;
+  while (pos < bend) {
+    uint64_t key, v;
+    if (!sw_read_varint(buf, &pos, bend, &key)) return false;
+    if ((key >> 3) == 1 && (key & 7) == 2) {
+      if (!sw_read_varint(buf, &pos, bend, &v) || v > (uint64_t)(bend - pos)) return false;
+      *off = pos; *len = (uint32_t)v;
+      return true;
+    }
+    if (!sw_skip_field(buf, &pos, bend, (uint32_t)(key & 7))) return false;
+  }
+  return false;
+}
+
+// Kafka key partitioning of raw device payloads: partition = toPositive(murmur2(device token)) % n,
+// the partition the reference's decoded-events producer would pick for the payload's events
+// (EventSourcesManager keys by device token).  Payloads without a readable token go to -1.
+void sw_partition_payloads(const uint8_t* raw, const uint32_t* offs, int64_t n, int32_t n_partitions, int32_t* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t off = 0, len = 0;
+    out[i] = sw_payload_token(raw, offs[i], offs[i + 1], &off, &len)
+                 ? sw_partition_for_key(raw + off, (int32_t)len, n_partitions) : -1;
+  }
+}
+
 // ============================================================================ registry builder
 // Open addressing with linear probing over (lo, hi); (0,0) = empty.  Returns the slot
 // written (>= 0), or -1 if the table is full.  Upsert semantics.

@@ -118,6 +118,7 @@ def native():
         _proto(lib, "sw_crc32c", ctypes.c_uint32, ctypes.c_char_p, c_int64)
         _proto(lib, "sw_memcpy_mt", None, P, P, c_int64, c_int32)
         _proto(lib, "sw_partition_for_key", c_int32, P, c_int32, c_int32)
+        _proto(lib, "sw_partition_payloads", None, P, P, c_int64, c_int32, P)
         _proto(lib, "sw_reg_upsert", c_int64, P, P, P, c_int64, c_uint64, c_uint64, c_int32)
         _proto(lib, "sw_reg_find", c_int64, P, P, P, c_int64, c_uint64, c_uint64)
         _proto(lib, "sw_reg_build", c_int64, P, P, P, c_int64, P, P, P, c_int64, P)

@@ -47,6 +47,22 @@ _PAD = 64
 _PINNED = None
 
 
+def partition_payloads(payloads: list, n_partitions: int) -> np.ndarray:
+    """Kafka key partition of each raw device payload by its device token (native
+    ``sw_partition_payloads``: ``toPositive(murmur2(token)) % n``); -1 where no token parses.
+    Event sources split raw batches with it so every device's payloads reach one partition, and
+    so one engine replica, as the reference keys decoded events by device token."""
+    from .fleet import pack_messages
+    from .._native import native
+    out = np.zeros(len(payloads), np.int32)
+    if not payloads:
+        return out
+    raw, offs = pack_messages([bytes(p) for p in payloads])
+    native().sw_partition_payloads(raw.ctypes.data, offs.ctypes.data, len(payloads), int(n_partitions),
+                                   out.ctypes.data)
+    return out
+
+
 def pinned_available() -> bool:
     """Pinned (DMA-able) host memory is there when a GPU runtime is (checked once)."""
     global _PINNED

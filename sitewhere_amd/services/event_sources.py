@@ -346,20 +346,33 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
                 self.flush_raw()
 
     def flush_raw(self):
-        """Ship the buffered raw payloads as one framed batch record (``pipeline/bus_io.py``).  On
-        the in-process bus the record is published in place: its bytes sit in pinned host memory
-        when a GPU is present, so the MI355X engine DMAs the batch straight out of the topic."""
-        from ..pipeline.bus_io import RawBatchRecord
+        """Ship the buffered raw payloads as framed batch records (``pipeline/bus_io.py``), one per
+        partition of the raw-payload topic: payloads are key-partitioned by device token, so with
+        several engine replicas in the consumer group each device is processed -- its state merged,
+        its alternate ids deduplicated -- by exactly one of them.  On the in-process bus a record is
+        published in place: its bytes sit in pinned host memory when a GPU is present, so the
+        MI355X engine DMAs the batch straight out of the topic."""
+        from ..pipeline.bus_io import RawBatchRecord, partition_payloads
         with self._raw_lock:
             buf, self._raw_buf = self._raw_buf, []
         if not buf:
             return
         bus = self.engine.ms.instance.bus
-        if hasattr(bus, "append_external"):
-            rec = RawBatchRecord.from_payloads(buf)
-            bus.append_external(self.t_raw, bus.partition_for(self.t_raw, None), rec, rec.ptr, rec.value_len)
+        n = bus.partitions(self.t_raw) if hasattr(bus, "partitions") else 1
+        if n > 1:
+            parts = partition_payloads(buf, n)
+            groups: dict[int, list] = {}
+            for payload, p in zip(buf, parts.tolist()):
+                groups.setdefault(max(p, 0), []).append(payload)      # unparsable: partition 0
         else:
-            self.producer.send(self.t_raw, None, RawBatchRecord.from_payloads(buf, pinned=False).value())
+            groups = {0: buf}
+        for p, payloads in sorted(groups.items()):
+            if hasattr(bus, "append_external"):
+                rec = RawBatchRecord.from_payloads(payloads)
+                bus.append_external(self.t_raw, p, rec, rec.ptr, rec.value_len)
+            else:
+                self.producer.send(self.t_raw, None, RawBatchRecord.from_payloads(payloads, pinned=False).value(),
+                                   partition=p)
 
 
 class EventSourcesTenantEngine(MicroserviceTenantEngine):

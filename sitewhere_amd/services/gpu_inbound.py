@@ -160,9 +160,15 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             try:
                 import torch
                 if torch.cuda.is_available():
+                    import os
                     from ..pipeline.gpu_engine import GpuInboundEngine
                     self.engine_kind = "gpu"
-                    return GpuInboundEngine(ecfg, device="cuda")
+                    # one inbound-processing replica per GPU: the replica's device comes from its
+                    # configuration, SITEWHERE_GPU_DEVICE, or the launcher's LOCAL_RANK
+                    idx = self.config.get("gpuDevice", os.environ.get("SITEWHERE_GPU_DEVICE",
+                                                                      os.environ.get("LOCAL_RANK", 0)))
+                    self.gpu_device = int(idx) % torch.cuda.device_count()
+                    return GpuInboundEngine(ecfg, device=f"cuda:{self.gpu_device}")
             except Exception:
                 if want_gpu:
                     raise
