@@ -173,12 +173,16 @@ class CompositeDecoder(Decoder):
         self.extractor, self.choices, self.device_type_of, self.default = extractor, choices, device_type_of, default
 
     def decode(self, payload, metadata):
-        token, inner = self.extractor(payload, metadata)
+        try:
+            token, inner = self.extractor(payload, metadata)
+        except Exception as e:
+            raise EventDecodeException(f"composite decoder metadata extraction failed: {e}") from e
         dt = self.device_type_of(token)
         dec = self.choices.get(dt, self.default)
-        if dec is None:
-            raise EventDecodeException(f"no decoder for device type {dt!r}")
-        out = dec.decode(inner, metadata)
+        if dec is None:         # reference: no choice applies -> nothing decoded
+            return []
+        # the chosen decoder sees the device context too (CompositeDeviceEventDecoder META_DEVICE*)
+        out = dec.decode(inner, dict(metadata or {}, deviceToken=token, deviceTypeToken=dt))
         for r in out:
             r.setdefault("deviceToken", token)
         return out
@@ -442,9 +446,19 @@ class EventSourcesTenantEngine(MicroserviceTenantEngine):
                 dt = dm(tok).get_device_type(dev.device_type_id)
                 return dt.token if dt else None
 
-            def extractor(payload, md):
-                obj = json.loads(payload)
-                return obj[d.get("tokenField", "deviceToken")], json.dumps(obj.get(d.get("payloadField", "payload"), obj)).encode()
+            if d.get("extractorScript"):
+                # GroovyMessageMetadataExtractor: extract(payload, metadata) -> (token, payload) or
+                # {"deviceToken": ..., "payload": ...}; works on binary payloads
+                src, runner = self.script_source(d["extractorScript"]), self.ms.scripts
+
+                def extractor(payload, md):
+                    r = runner.call(src, "extract", bytes(payload), dict(md or {}), name="metadata-extractor")
+                    tok, inner = (r["deviceToken"], r["payload"]) if isinstance(r, dict) else r
+                    return tok, inner if isinstance(inner, (bytes, bytearray)) else str(inner).encode()
+            else:
+                def extractor(payload, md):
+                    obj = json.loads(payload)
+                    return obj[d.get("tokenField", "deviceToken")], json.dumps(obj.get(d.get("payloadField", "payload"), obj)).encode()
             return CompositeDecoder(extractor, choices, dtype_of, self.build_decoder(d["default"]) if d.get("default") else None)
         raise ValueError(f"unknown decoder {t!r}")
 

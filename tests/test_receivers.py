@@ -362,3 +362,50 @@ def test_tenant_receivers_after_hot_reconfiguration():
         assert got == [("edge.coap", 1.0), ("edge.http", 3.0), ("edge.ws", 2.0)]
     finally:
         sw.stop()
+
+
+def test_composite_decoder_with_scripted_metadata_extractor():
+    """Reference BinaryCompositeDeviceEventDecoder + GroovyMessageMetadataExtractor: a script pulls
+    the device token out of a binary frame, the device's type picks the inner decoder, and a device
+    type with no choice decodes to nothing."""
+    from sitewhere_amd.assembly import SiteWhereInstance
+    from sitewhere_amd.runtime.config import dump_document
+    sw = SiteWhereInstance().start()
+    try:
+        sw.wait_for_tenant("default", 60)
+        run = lambda f: sw.instance.system_user.run(f, "default")  # noqa: E731
+        dm, em = sw.api("DeviceManagement", "default"), sw.api("DeviceEventManagement", "default")
+        tab = run(lambda: dm.get_device_by_token("galaxytab-001"))
+        hab = run(lambda: dm.get_device_by_token("openhab-001"))
+        tab_type = run(lambda: dm.get_device_type(tab.device_type_id)).token
+        extractor = ("def extract(payload, metadata):\n"
+                     "    n = payload[0]\n"
+                     "    return payload[1:1 + n].decode(), payload[1 + n:]\n")
+        inner = ("import json\n"
+                 "def decode(payload, metadata):\n"
+                 "    v = json.loads(payload)\n"
+                 "    return [{'deviceToken': metadata['deviceToken'], 'type': 'DeviceMeasurement',\n"
+                 "             'request': {'name': 'composite.' + metadata['deviceTypeToken'], 'value': v}}]\n")
+        es_ms = sw["event-sources"]
+        before = es_ms.get_tenant_engine("default")
+        doc = json.loads(json.dumps(es_ms.tenant_configuration("default")))
+        doc["sources"].append({"id": "binary", "receivers": [], "decoder": {
+            "type": "composite", "extractorScript": extractor,
+            "choices": {tab_type: {"type": "script", "script": inner}}}})
+        sw.instance.coord.put(es_ms.tenant_config_path("default"), dump_document(doc))
+        assert wait(lambda: (e := es_ms.get_tenant_engine("default")) is not None and e is not before
+                    and e.status.value == "Started" and "binary" in e.manager.sources, 30)
+        es = es_ms.get_tenant_engine("default")
+        frame = lambda tok, body: bytes([len(tok)]) + tok.encode() + body  # noqa: E731
+        assert es.inject("binary", frame("galaxytab-001", b"42.5")) == 1
+        assert es.inject("binary", frame("openhab-001", b"1.0")) == 0          # no choice for its type
+        end, got = time.time() + 20, []
+        while not got and time.time() < end:
+            got = [m for m in run(lambda: em.list_measurements_for_index(
+                "Assignment", [tab.device_assignment_id], {"pageSize": 0})).results if m.name.startswith("composite.")]
+            time.sleep(0.05)
+        assert [(m.name, m.value) for m in got] == [(f"composite.{tab_type}", 42.5)]
+        assert not [m for m in run(lambda: em.list_measurements_for_index(
+            "Assignment", [hab.device_assignment_id], {"pageSize": 0})).results if m.name.startswith("composite.")]
+    finally:
+        sw.stop()
