@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--via-bus", action="store_true",
                     help="publish the batches to the tenant's raw-payload topic (zero-copy pinned records, as "
                          "event sources do) and time until the raw consumer has stored and committed them all")
+    ap.add_argument("--gc", choices=["default", "freeze"], default="default",
+                    help="freeze: gc.freeze() the start-up heap and raise the gen-0 threshold before the timed run")
     ap.add_argument("--store-retention", type=int, default=0,
                     help="rows the columnar event store holds (0 = the template's); older batches are evicted "
                          "and their memory reused -- a store that only grows page-faults fresh memory per batch")
@@ -79,6 +81,11 @@ def main():
     for b in range(4):
         raw, offs = gen_payloads(spec, args.batch, now0 - 1000, seed=7 + b)
         batches.append((np.concatenate([raw, np.zeros(64, np.uint8)]), offs))
+    if args.gc == "freeze":
+        import gc
+        gc.collect()
+        gc.freeze()                         # start-up objects leave the collector's generations
+        gc.set_threshold(50_000, 20, 100)
     if args.via_bus:
         from sitewhere_amd.pipeline.bus_io import RawBatchRecord
         from sitewhere_amd.pipeline.framing import varint_lengths
@@ -126,11 +133,15 @@ def main():
             trace = {"submit_ms": d[:, 0], "to_complete_ms": d[:, 1], "queue_wait_ms": d[:, 2],
                      "payload_lock_ms": d[:, 3], "payload_dicts_ms": d[:, 4], "payload_encode_ms": d[:, 5],
                      "rpc_ms": d[:, 6], "publish_commit_ms": d[:, 7], "submit_interval_ms": gap}
+            gap_pct = {f"submit_interval_p{q}_ms": round(float(np.percentile(gap, q)), 3) for q in (90, 99)} \
+                if len(gap) else {}
             trace = {k: round(float(np.median(v)), 3) for k, v in trace.items() if len(v)}
+            trace.update(gap_pct)
     breakdown = {name: round(t.hist.snapshot()["mean"], 3)
                  for name, t in (("engine_step_ms", ib.step_timer), ("columnar_store_ms", ib.store_timer),
                                  ("publish_ms", ib.publish_timer))}
     print(json.dumps({"metric": "tenant_path_events_per_sec", "engine": ib.engine_kind, "via_bus": args.via_bus,
+                      "gc": args.gc,
                       "overlap_steps": ib.overlap,
                       "events": ev,
                       "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,
