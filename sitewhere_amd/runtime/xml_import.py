@@ -101,7 +101,28 @@ _DECODERS = {"protobuf-event-decoder": "protobuf", "json-device-request-decoder"
              "json-event-decoder": "json", "json-batch-event-decoder": "json-batch",
              "groovy-event-decoder": "script", "groovy-string-event-decoder": "script",
              "scripted-event-decoder": "script", "echo-string-decoder": "echo", "payload-logger-decoder": "echo",
-             "composite-event-decoder": "composite"}
+             "coap-json-decoder": "coap-json", "composite-decoder": "composite", "composite-event-decoder": "composite"}
+
+
+def _decoder(c: ET.Element):
+    """A decoder element -> decoder spec: a name, or a dict for scripted / composite decoders
+    (``composite-decoder``: ``groovy-device-metadata-extractor`` + ``choices`` of
+    ``device-specification-decoder-choice token=...`` each wrapping a decoder)."""
+    kind = _DECODERS[_local(c.tag)]
+    if kind == "script":
+        return {"type": "script", "script": _sub(c.get("scriptId") or c.get("scriptPath"))}
+    if kind == "composite":
+        spec: dict = {"type": "composite", "choices": {}}
+        for x in c.iter():
+            xn = _local(x.tag)
+            if xn in ("groovy-device-metadata-extractor", "scripted-device-metadata-extractor"):
+                spec["extractorScript"] = _sub(x.get("scriptId") or x.get("scriptPath"))
+            elif xn == "device-specification-decoder-choice":
+                inner = [d for d in x if _local(d.tag) in _DECODERS]
+                if inner:
+                    spec["choices"][_sub(x.get("token"))] = _decoder(inner[0])
+        return spec
+    return kind
 
 
 def _mqtt_attrs(el: ET.Element) -> dict:
@@ -120,7 +141,7 @@ def _receiver(n: str, el: ET.Element) -> dict | None:
     if n == "mqtt-event-source":
         return dict(_mqtt_attrs(el), type="mqtt", topic=g("topic", "SiteWhere/input"),
                     numThreads=_num(el.get("numThreads"), 4))
-    if n == "activemq-event-source":
+    if n in ("activemq-event-source", "activemq-client-event-source"):
         if el.get("transportUri"):
             return {"type": "activemq-broker", "transportUri": g("transportUri"),
                     "queueName": g("queueName", "SITEWHERE.IN"), "numConsumers": _num(el.get("numConsumers"), 3),
@@ -194,9 +215,11 @@ def _event_sources(root: ET.Element, ctx: _Ctx) -> dict:
         for c in el:
             cn = _local(c.tag)
             if cn in _DECODERS:
-                src["decoder"] = _DECODERS[cn]
-                if src["decoder"] == "script":
-                    src["script"] = _sub(c.get("scriptId") or c.get("scriptPath"))
+                d = _decoder(c)
+                if isinstance(d, dict) and d["type"] == "script":
+                    src["decoder"], src["script"] = "script", d["script"]
+                else:
+                    src["decoder"] = d
             elif cn.endswith("-decoder") or cn.endswith("-event-decoder"):
                 ctx.warn("event-sources", c)
         sources.append(src)

@@ -92,6 +92,31 @@ def test_receiver_attributes_and_script_ids_import():
                                          "username": "a", "password": "b", "scriptId": "poller"}
 
 
+def test_composite_and_coap_decoders_import():
+    xml = b"""<beans xmlns:es="x"><es:event-sources>
+      <es:socket-event-source sourceId="bin" port="9001"><es:composite-decoder>
+        <es:groovy-device-metadata-extractor scriptId="extract"/>
+        <es:choices>
+          <es:device-specification-decoder-choice token="tracker"><es:groovy-event-decoder scriptId="trk"/>
+          </es:device-specification-decoder-choice>
+          <es:device-specification-decoder-choice token="gw"><es:json-device-request-decoder/>
+          </es:device-specification-decoder-choice>
+        </es:choices></es:composite-decoder></es:socket-event-source>
+      <es:coap-server-event-source sourceId="coap" port="5683"><es:coap-json-decoder/></es:coap-server-event-source>
+      <es:activemq-client-event-source sourceId="amq" remoteUri="tcp://broker:61613" queueName="Q" numConsumers="2">
+        <es:json-device-request-decoder/></es:activemq-client-event-source>
+    </es:event-sources></beans>"""
+    from sitewhere_amd.runtime.xml_import import _Ctx
+    ctx = _Ctx()
+    srcs = {s["id"]: s for s in convert_service("event-sources", xml, ctx)["sources"]}
+    assert ctx.warnings == []
+    assert srcs["bin"]["decoder"] == {"type": "composite", "extractorScript": "extract",
+                                      "choices": {"tracker": {"type": "script", "script": "trk"}, "gw": "json"}}
+    assert srcs["coap"]["decoder"] == "coap-json" and srcs["coap"]["receivers"][0]["type"] == "coap"
+    assert srcs["amq"]["receivers"][0] == {"type": "activemq", "host": "broker", "port": 61613,
+                                           "destination": "/queue/Q", "numThreads": 2}
+
+
 def test_script_ids_resolve_through_script_management():
     """A source configured with a script id (as imported from the reference) runs the active
     version stored in script management; activating another version changes the next engine."""
