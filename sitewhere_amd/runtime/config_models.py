@@ -19,10 +19,22 @@ DATASTORE = E("Datastore", "datastore", "Entity / event persistence backend", [
     A("database", "String", "database name"),
     A("bucket_ms", "Integer", "time bucket for the Cassandra-layout event store", default=3600000)])
 
+MQTT_ATTRS = [
+    A("protocol", "String", "tcp | ssl | tls", default="tcp", choices=["tcp", "ssl", "tls"]),
+    A("username", "String", "MQTT user name"), A("password", "String", "MQTT password"),
+    A("trustStorePath", "String", "PEM CA file for TLS (the reference's trust store)"),
+    A("keyStorePath", "String", "PEM client certificate for mutual TLS (the reference's key store)"),
+    A("keyPath", "String", "PEM client key (defaults to keyStorePath)"),
+    A("clientId", "String", "MQTT client id"), A("cleanSession", "Boolean", "MQTT clean session", default=True),
+    A("qos", "String", "0 | 1 | 2 or AT_MOST_ONCE | AT_LEAST_ONCE | EXACTLY_ONCE", default="1")]
 DECODER = E("Decoder", "event-source-decoder", "Payload decoder", [
-    A("type", "String", "protobuf | json | json-batch | script | echo | composite", True, "json",
-      ["protobuf", "json", "json-batch", "script", "echo", "composite"]),
-    A("script", "Script", "decoder script id (type=script)")])
+    A("type", "String", "protobuf | json | json-string | json-batch | coap-json | script | echo | composite", True, "json",
+      ["protobuf", "json", "json-string", "json-batch", "coap-json", "script", "echo", "composite"]),
+    A("script", "Script", "decoder script id or source (type=script)"),
+    A("extractorScript", "Script", "composite: extract(payload, metadata) -> (deviceToken, payload)"),
+    A("tokenField", "String", "composite without a script: JSON field holding the device token",
+      default="deviceToken"),
+    A("payloadField", "String", "composite without a script: JSON field holding the inner payload", default="payload")])
 RECEIVER = E("Receiver", "event-source-receiver", "Protocol receiver", [
     A("type", "String", "mqtt | socket | websocket | coap | rest-poll | activemq | activemq-broker | rabbitmq | kafka | "
       "eventhub", True, choices=["mqtt", "socket", "websocket", "coap", "rest-poll", "activemq", "activemq-broker",
@@ -32,7 +44,17 @@ RECEIVER = E("Receiver", "event-source-receiver", "Protocol receiver", [
     A("transportUri", "String", "embedded broker transport (activemq-broker), e.g. stomp://0.0.0.0:2345"),
     A("queueName", "String", "embedded broker queue (activemq-broker)"),
     A("numConsumers", "Integer", "embedded broker queue consumers", default=3),
-    A("qos", "Integer", "MQTT QoS", default=1), A("numThreads", "Integer", "processing threads", default=4)])
+    A("numThreads", "Integer", "processing threads", default=4),
+    A("handler", "String", "socket interaction handler: read-all | line | http | script", default="read-all",
+      choices=["read-all", "line", "http", "script"]),
+    A("script", "Script", "socket interaction script interact(socket, receiver) / REST polling script "
+      "poll(rest, payloads, logger)"),
+    A("webSocketUrl", "String", "websocket: connect to this ws:// URL (client receiver) instead of listening"),
+    A("payloadType", "String", "websocket: binary | string", default="binary", choices=["binary", "string"]),
+    A("paths", "String", "coap: reference (devices/{token}/...) | any", default="reference",
+      choices=["reference", "any"]),
+    A("baseUrl", "String", "rest-poll: API base URL"), A("interval", "Double", "rest-poll: seconds", default=10.0),
+    *MQTT_ATTRS])
 SOURCE = E("Event Source", "event-source", "Decoder + deduplicator + receivers", [
     A("id", "String", "source id", True), A("decoder", "String", "decoder type or element", True),
     A("forward", "String", "'raw' forwards undecoded payload batches to the MI355X inbound engine"),
@@ -55,7 +77,15 @@ PROCESSOR = E("Rule Processor", "rule-processor", "Rule processor", [
 DESTINATION = E("Command Destination", "command-destination", "Encoder + provider", [
     A("id", "String", "destination id", True), A("encoder", "String", "json | protobuf | script", True, "json"),
     A("provider", "String", "log | mqtt | coap | sms", True, "log"), A("host", "String", "MQTT host"),
-    A("port", "Integer", "MQTT port"), A("commandTopic", "String", "MQTT command topic template")])
+    A("port", "Integer", "MQTT port"), A("commandTopic", "String", "MQTT command topic template"),
+    A("accountSid", "String", "sms: Twilio account SID"), A("authToken", "String", "sms: Twilio auth token"),
+    A("fromPhone", "String", "sms: sending number"), A("phoneMetadata", "String", "sms: device metadata field",
+                                                          default="sms_phone"),
+    A("hostnameMetadata", "String", "coap: device metadata field", default="coap_hostname"),
+    A("portMetadata", "String", "coap: device metadata field", default="coap_port"),
+    A("urlMetadata", "String", "coap: device metadata field", default="coap_url"),
+    A("methodMetadata", "String", "coap: device metadata field", default="coap_method"),
+    *MQTT_ATTRS])
 ROUTER = E("Command Router", "command-router", "Destination choice", [
     A("type", "String", "single-choice | device-type-mapping | script | no-op", True, "single-choice"),
     A("destination", "String", "destination id (single-choice)")])
@@ -85,7 +115,11 @@ _m("inbound-processing", "Inbound Processing", [
     A("storage", "String", "objects | columnar (gpu engine)", default="objects", choices=["objects", "columnar"]),
     A("publishEnriched", "String", "events | batches | none (gpu engine)", default="events",
       choices=["events", "batches", "none"]),
-    A("maxDelayMs", "Integer", "micro-batch latency bound (gpu engine)", default=5)], [
+    A("maxDelayMs", "Integer", "micro-batch latency bound (gpu engine)", default=5),
+    A("gpuDevice", "Integer", "GPU of this replica (default SITEWHERE_GPU_DEVICE / LOCAL_RANK / 0)"),
+    A("overlapSteps", "Boolean", "overlapped engine steps (default on for MI355X columnar tenants)"),
+    A("asyncStore", "Boolean", "store rows on a store thread (default on for columnar storage)"),
+    A("tuneGc", "Boolean", "freeze the start-up heap out of the cyclic GC (columnar tenants)", default=True)], [
     E("Zone Tests", "gpu-zone-tests", "zone tests evaluated inside the GPU engine", [
         A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")]),
     E("Checkpoint", "checkpoint", "engine-shard snapshots; raw offsets commit only when covered", [

@@ -38,7 +38,7 @@ from ..pipeline.engine_base import Zone, ZoneTest
 from ..pipeline.bus_io import RawBatch, parse_raw_batch
 from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
-from ..utils import IndexMap, retain_large_allocations
+from ..utils import IndexMap, retain_large_allocations, tune_gc_for_streaming
 from ..runtime.consumers import BusConsumer, RetryFrom
 from ..bus import payloads
 from .event_sources import RAW_PAYLOADS, ProtobufDecoder
@@ -252,6 +252,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     def tenant_start(self, monitor):
         self.restore_checkpoint()
         self.load_model()
+        if self.storage == "columnar" and self.config.get("tuneGc", True):
+            tune_gc_for_streaming()             # the registry mirror just loaded is long-lived
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         if self.async_store:
             self._store_thread = threading.Thread(target=self._store_loop, daemon=True,

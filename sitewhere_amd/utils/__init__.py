@@ -95,3 +95,26 @@ def retain_large_allocations() -> bool:
     except (OSError, AttributeError):
         _MALLOC_TUNED = False
     return _MALLOC_TUNED
+
+
+_GC_TUNED = False
+
+
+def tune_gc_for_streaming() -> bool:
+    """Freeze the start-up heap out of the cyclic collector and raise the gen-0 threshold.
+
+    An engine tenant holds tens of thousands of long-lived objects (the registry mirror, domain
+    entities, service state) while its data plane allocates few Python objects per batch; every
+    full collection still walked the whole heap under the GIL and stalled the consumer and store
+    threads.  Measured on the MI355X tenant path at 1M-payload batches: 281M -> 417M events/s,
+    payload encode 3.1 -> 1.7 ms median (``profiles/r2_tenant_gc``).  Objects created later are
+    collected as usual.  Process-wide and idempotent; ``SW_GC_TUNE=0`` disables it."""
+    global _GC_TUNED
+    if _GC_TUNED or os.environ.get("SW_GC_TUNE", "1") == "0":
+        return _GC_TUNED
+    import gc
+    gc.collect()
+    gc.freeze()
+    gc.set_threshold(50_000, 20, 100)
+    _GC_TUNED = True
+    return True
