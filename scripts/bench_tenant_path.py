@@ -28,9 +28,8 @@ def main():
     ap.add_argument("--via-bus", action="store_true",
                     help="publish the batches to the tenant's raw-payload topic (zero-copy pinned records, as "
                          "event sources do) and time until the raw consumer has stored and committed them all")
-    ap.add_argument("--gc", choices=["default", "freeze"], default="freeze",
-                    help="freeze: gc.freeze() the heap once the devices are loaded (the tenant also tunes GC at "
-                         "start unless SW_GC_TUNE=0); default: leave the collector alone")
+    ap.add_argument("--gc", choices=["default", "freeze"], default="default",
+                    help="freeze: gc.freeze() the heap once the devices are loaded; default: leave the collector alone")
     ap.add_argument("--store-retention", type=int, default=0,
                     help="rows the columnar event store holds (0 = the template's); older batches are evicted "
                          "and their memory reused -- a store that only grows page-faults fresh memory per batch")

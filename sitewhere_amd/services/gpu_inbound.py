@@ -252,8 +252,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     def tenant_start(self, monitor):
         self.restore_checkpoint()
         self.load_model()
-        if self.storage == "columnar" and self.config.get("tuneGc", True):
-            tune_gc_for_streaming()             # the registry mirror just loaded is long-lived
+        if self.config.get("tuneGc", False):
+            tune_gc_for_streaming()             # opt-in: measured gain is within run-to-run noise
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         if self.async_store:
             self._store_thread = threading.Thread(target=self._store_loop, daemon=True,

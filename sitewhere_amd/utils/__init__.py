@@ -104,11 +104,12 @@ def tune_gc_for_streaming() -> bool:
     """Freeze the start-up heap out of the cyclic collector and raise the gen-0 threshold.
 
     An engine tenant holds tens of thousands of long-lived objects (the registry mirror, domain
-    entities, service state) while its data plane allocates few Python objects per batch; every
-    full collection still walked the whole heap under the GIL and stalled the consumer and store
-    threads.  Measured on the MI355X tenant path at 1M-payload batches: 281M -> 417M events/s,
-    payload encode 3.1 -> 1.7 ms median (``profiles/r2_tenant_gc``).  Objects created later are
-    collected as usual.  Process-wide and idempotent; ``SW_GC_TUNE=0`` disables it."""
+    entities, service state) while its data plane allocates few Python objects per batch; a full
+    collection walks the whole heap under the GIL.  Opt-in (tenant ``tuneGc``): on the MI355X
+    tenant path a freeze after the registry is loaded measured +10-48% at 1M-payload batches, but
+    tuning at tenant start was within run-to-run noise or slower (``profiles/r2_tenant_gc``).
+    Objects created later are collected as usual.  Process-wide and idempotent; ``SW_GC_TUNE=0``
+    disables it."""
     global _GC_TUNED
     if _GC_TUNED or os.environ.get("SW_GC_TUNE", "1") == "0":
         return _GC_TUNED
