@@ -103,7 +103,9 @@ _m("user-management", "User Management", [], [DATASTORE])
 _m("tenant-management", "Tenant Management", [], [DATASTORE])
 _m("web-rest", "Web/REST", [A("port", "Integer", "HTTP port", default=8080), A("cors", "Boolean", "CORS", default=True)])
 _m("event-sources", "Event Sources", [
-    A("rawBatchSize", "Integer", "payloads per raw micro-batch for the MI355X engine", default=4096),
+    A("rawBatchSize", "Integer", "payloads per raw micro-batch (per partition) for the MI355X engine", default=4096),
+    A("rawPartitioning", "Boolean", "split raw batches over the raw topic's partitions by device token "
+      "(engine replicas own disjoint devices)", default=True),
     A("rawMaxDelayMs", "Integer", "latency bound of a raw micro-batch", default=5)], [SOURCE, E("Deduplicator", "deduplicator", "alternate-id | script", [
     A("type", "String", "alternate-id | script", True), A("script", "Script", "script id")])])
 _m("inbound-processing", "Inbound Processing", [

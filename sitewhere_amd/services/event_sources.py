@@ -328,7 +328,8 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
         self.t_raw = ms.instance.naming.tenant_prefix(t) + RAW_PAYLOADS
         self.sources: dict[str, InboundEventSource] = {}
         self._raw_buf: list = []
-        self._raw_lock = threading.Lock()
+        self._raw_lock = threading.Lock()      # the payload buffer
+        self._pub_lock = threading.Lock()      # cut + publish of raw batches, in order
 
     def handle_decoded_event(self, source_id: str, req: dict):
         payload = {"sourceId": source_id, "deviceToken": req["deviceToken"], "originator": req.get("originator"),
@@ -343,11 +344,25 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
         self.producer.send(self.t_failed, source_id, json.dumps(
             {"sourceId": source_id, "error": str(err), "payload": codec.to_wire(bytes(payload))}).encode())
 
+    def _raw_partitions(self) -> int:
+        """Partitions raw batches are split over (1 with ``rawPartitioning: false``)."""
+        n = getattr(self, "_raw_nparts", None)
+        if n is None:
+            bus = self.engine.ms.instance.bus
+            n = bus.partitions(self.t_raw) if hasattr(bus, "partitions") else 1
+            if not self.engine.config.get("rawPartitioning", True):
+                n = 1
+            self._raw_nparts = n
+        return n
+
     def handle_raw_payload(self, source_id: str, payload: bytes, flush_at: int = 4096):
+        """Buffer a raw payload; the count bound is per partition (a flush splits the buffer over
+        the partitions, so each record still carries ~``flush_at`` payloads at full rate)."""
         with self._raw_lock:
             self._raw_buf.append(bytes(payload))
-            if len(self._raw_buf) >= flush_at:
-                self.flush_raw()
+            full = len(self._raw_buf) >= flush_at * self._raw_partitions()
+        if full:
+            self.flush_raw()
 
     def flush_raw(self):
         """Ship the buffered raw payloads as framed batch records (``pipeline/bus_io.py``), one per
@@ -356,13 +371,16 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
         its alternate ids deduplicated -- by exactly one of them.  On the in-process bus a record is
         published in place: its bytes sit in pinned host memory when a GPU is present, so the
         MI355X engine DMAs the batch straight out of the topic."""
+        with self._pub_lock:            # batches are published in the order they were cut
+            with self._raw_lock:
+                buf, self._raw_buf = self._raw_buf, []
+            if buf:
+                self._publish_raw(buf)
+
+    def _publish_raw(self, buf: list):
         from ..pipeline.bus_io import RawBatchRecord, partition_payloads
-        with self._raw_lock:
-            buf, self._raw_buf = self._raw_buf, []
-        if not buf:
-            return
         bus = self.engine.ms.instance.bus
-        n = bus.partitions(self.t_raw) if hasattr(bus, "partitions") else 1
+        n = self._raw_partitions()
         if n > 1:
             parts = partition_payloads(buf, n)
             groups: dict[int, list] = {}

@@ -111,3 +111,37 @@ def _replicas_scenario(kind: str | None = None):
         if replica is not None:
             shutdown_microservice(replica)
         sw.stop()
+
+
+def test_raw_batches_cut_at_the_count_bound_per_partition():
+    """A source reaching rawBatchSize x partitions cuts a batch at once (not only on the delay
+    timer), splits it by device token and publishes it -- concurrently injecting threads included."""
+    import threading
+    sw = SiteWhereInstance().start()
+    try:
+        sw.wait_for_tenant("default", 60)
+        es_ms = sw["event-sources"]
+        eng = es_ms.get_tenant_engine("default")
+        eng.raw_batch, eng.raw_delay_s = 16, 3600.0             # count bound only
+        src = eng.manager.sources["default-protobuf"]
+        src.forward_raw = True
+        t_raw = eng.manager.t_raw
+        bus = sw.instance.bus
+        nparts = bus.partitions(t_raw)
+        before = sum(bus.end_offset(t_raw, p) for p in range(nparts))
+
+        def inject(k):
+            for i in range(16 * nparts):
+                eng.inject("default-protobuf", wire.measurements(f"cnt-{k}-{i % 40}", {"x": float(i)}))
+        ths = [threading.Thread(target=inject, args=(k,)) for k in range(4)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(30)
+        assert not any(t.is_alive() for t in ths), "raw batch cut deadlocked"
+        eng.manager.flush_raw()
+        recs = [r for p in range(nparts) for r in bus.read(t_raw, p, 0, max_records=100_000, max_bytes=64 << 20)]
+        assert sum(bus.end_offset(t_raw, p) for p in range(nparts)) - before == len(recs) > nparts
+        assert sum(parse_raw_batch(r.value).n_msgs for r in recs) == 4 * 16 * nparts
+    finally:
+        sw.stop()
