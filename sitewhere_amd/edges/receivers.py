@@ -150,6 +150,8 @@ class SocketReceiver(Receiver):
         self._srv = None
         self._pool = None
         self._stop = threading.Event()
+        self._conns: set = set()
+        self._conns_lock = threading.Lock()
 
     def start(self, monitor):
         if self.handler == "script":
@@ -182,6 +184,8 @@ class SocketReceiver(Receiver):
 
     def _handle(self, c, addr):
         md = {"remote": f"{addr[0]}:{addr[1]}"}
+        with self._conns_lock:
+            self._conns.add(c)
         try:
             c.settimeout(30)
             st = SocketStream(c, md["remote"])
@@ -201,8 +205,11 @@ class SocketReceiver(Receiver):
                 if body:
                     self.deliver(body, md)
         except Exception as e:  # noqa: BLE001 -- one bad connection never stops the receiver
-            self.logger.warning("socket interaction with %s failed: %s", md["remote"], e)
+            if not self._stop.is_set():
+                self.logger.warning("socket interaction with %s failed: %s", md["remote"], e)
         finally:
+            with self._conns_lock:
+                self._conns.discard(c)
             c.close()
 
     def _http(self, st: SocketStream, md: dict):
@@ -237,6 +244,7 @@ class SocketReceiver(Receiver):
         self._stop.set()
         if self._srv:
             self._srv.close()
+        _shutdown_all(self._conns, self._conns_lock)     # open conversations end with the receiver
         if self._pool:
             self._pool.shutdown(wait=False)
 
@@ -357,6 +365,8 @@ class WebSocketReceiver(Receiver):
         self._srv = None
         self._client_sock = None
         self.connected = threading.Event()
+        self._conns: set = set()
+        self._conns_lock = threading.Lock()
 
     def start(self, monitor):
         self._stop.clear()
@@ -408,6 +418,8 @@ class WebSocketReceiver(Receiver):
             threading.Thread(target=self._serve, args=(c,), daemon=True).start()
 
     def _serve(self, c):
+        with self._conns_lock:
+            self._conns.add(c)
         try:
             data = b""
             while b"\r\n\r\n" not in data:
@@ -426,6 +438,8 @@ class WebSocketReceiver(Receiver):
         except (OSError, ConnectionError, ValueError):
             pass
         finally:
+            with self._conns_lock:
+                self._conns.discard(c)
             c.close()
 
     def _pump(self, conn: WsConnection):
@@ -442,11 +456,22 @@ class WebSocketReceiver(Receiver):
         self._stop.set()
         if self._srv is not None:
             self._srv.close()
+        _shutdown_all(self._conns, self._conns_lock)
         if self._client_sock is not None:
             try:
                 self._client_sock.shutdown(socket.SHUT_RDWR)
             except OSError:
                 pass
+
+
+def _shutdown_all(conns: set, lock):
+    with lock:
+        live = list(conns)
+    for c in live:
+        try:
+            c.shutdown(socket.SHUT_RDWR)
+        except OSError:
+            pass
 
 
 def _recv(c, n):
