@@ -389,3 +389,48 @@ def decode_enriched(value, key=None) -> tuple[domain.DeviceEvent, dict, str | No
            "deviceMetadata": dmeta, "assignmentStatus": _ASSN_BACK.get(c.assignmentStatus),
            "assignmentMetadata": dict(c.assignmentMetadata), "deviceToken": token}
     return ev, ctx, error
+
+
+# ------------------------------------------------------------------------------ instance logging
+_LOG_LEVELS = {"TRACE": 0, "DEBUG": 1, "INFO": 2, "WARNING": 3, "WARN": 3, "ERROR": 4, "CRITICAL": 4}
+_LOG_BACK = {0: "TRACE", 1: "DEBUG", 2: "INFO", 3: "WARNING", 4: "ERROR"}
+
+
+def encode_log(m: dict) -> bytes:
+    """Log record (``BusLogHandler``) -> ``instance-logging`` value; ``GMicroserviceLogMessage`` in
+    protobuf mode (the tenant travels as ``tenantId`` when it is a UUID, otherwise as a
+    ``[tenant]`` prefix of the text)."""
+    if _MODE != "protobuf":
+        return json.dumps(m).encode()
+    p = messages()["GMicroserviceLogMessage"](microserviceIdentifier=m.get("microservice") or "",
+                                              microserviceContainerId=m.get("hostname") or "",
+                                              timestamp=int(m.get("timestamp") or 0),
+                                              level=_LOG_LEVELS.get(str(m.get("level", "INFO")).upper(), 2))
+    text, tenant = m.get("message") or "", m.get("tenant")
+    if tenant:
+        meta: dict = {}
+        _set_uuid(p, "tenantId", tenant, meta)
+        if meta:
+            text = f"[{tenant}] {text}"
+    p.messageText = text
+    exc = m.get("exception")
+    if exc:
+        p.exception.messageText = exc.get("message", "")
+        for fr in exc.get("frames", []):
+            p.exception.elements.add(clazz=fr.get("module", ""), method=fr.get("function", ""),
+                                     file=fr.get("file", ""), lineNumber=int(fr.get("line") or 0))
+    return p.SerializeToString()
+
+
+def decode_log(value) -> dict:
+    if _is_json(value):
+        return json.loads(value)
+    p = messages()["GMicroserviceLogMessage"].FromString(bytes(value))
+    out = {"microservice": p.microserviceIdentifier, "hostname": p.microserviceContainerId,
+           "level": _LOG_BACK.get(p.level, "INFO"), "message": p.messageText, "timestamp": p.timestamp,
+           "tenant": _get_uuid(p, "tenantId", {})}
+    if p.HasField("exception"):
+        out["exception"] = {"message": p.exception.messageText, "frames": [
+            {"module": e.clazz, "function": e.method, "file": e.file, "line": e.lineNumber}
+            for e in p.exception.elements]}
+    return out

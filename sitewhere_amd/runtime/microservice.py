@@ -26,6 +26,7 @@ import threading
 import time
 import uuid
 
+from ..bus import payloads
 from ..bus.log import EventBus
 from ..bus.naming import TopicNaming
 from ..coord.store import NODE_ADDED, NODE_REMOVED, NODE_UPDATED, Coordination, InterProcessMutex, NodeExistsError
@@ -184,9 +185,16 @@ class BusLogHandler(logging.Handler):
 
     def emit(self, record):
         try:
-            self.q.put_nowait({"microservice": self.identifier, "hostname": self.hostname, "level": record.levelname,
-                               "logger": record.name, "message": record.getMessage(), "timestamp": int(record.created * 1000),
-                               "tenant": getattr(record, "tenant", None)})
+            m = {"microservice": self.identifier, "hostname": self.hostname, "level": record.levelname,
+                 "logger": record.name, "message": record.getMessage(), "timestamp": int(record.created * 1000),
+                 "tenant": getattr(record, "tenant", None)}
+            if record.exc_info and record.exc_info[1] is not None:
+                import traceback
+                e = record.exc_info[1]
+                m["exception"] = {"message": f"{type(e).__name__}: {e}", "frames": [
+                    {"module": f.filename.rsplit("/", 1)[-1].removesuffix(".py"), "function": f.name,
+                     "file": f.filename, "line": f.lineno} for f in traceback.extract_tb(record.exc_info[2])]}
+            self.q.put_nowait(m)
         except queue.Full:
             pass
 
@@ -198,7 +206,7 @@ class BusLogHandler(logging.Handler):
             except queue.Empty:
                 continue
             try:
-                prod.send(self.topic, self.hostname, json.dumps(m).encode())
+                prod.send(self.topic, self.hostname, payloads.encode_log(m))
             except Exception:
                 pass
 

@@ -207,3 +207,18 @@ def test_whole_instance_on_protobuf_topics(protobuf_codec):
             c.close()
     finally:
         sw.stop()
+
+
+def test_instance_log_messages(protobuf_codec):
+    m = {"microservice": "event-sources", "hostname": "es-1", "level": "ERROR", "logger": "x",
+         "message": "decode failed", "timestamp": 1_700_000_000_000, "tenant": "default",
+         "exception": {"message": "ValueError: bad", "frames": [
+             {"module": "event_sources", "function": "decode", "file": "/a/event_sources.py", "line": 42}]}}
+    b = payloads.encode_log(m)
+    p = payloads.messages()["GMicroserviceLogMessage"].FromString(b)
+    assert p.level == 4 and p.microserviceContainerId == "es-1" and p.exception.elements[0].lineNumber == 42
+    back = payloads.decode_log(b)
+    assert back["message"] == "[default] decode failed" and back["level"] == "ERROR"
+    assert back["exception"]["frames"][0]["function"] == "decode"
+    tid = domain.new_id()
+    assert payloads.decode_log(payloads.encode_log(dict(m, tenant=tid)))["tenant"] == tid
