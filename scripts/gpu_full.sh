@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU validation: GPU tests -> smoke -> headline bench -> tenant-path bench -> rocprofv3 kernel stats
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O=gpurun_out/full
+O=gpurun_out/${1:-full}
 cd "$R" && export TMPDIR=/tmp && mkdir -p $O/prof
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo "pytest gpu ok" && tail -1 $O/pytest_gpu.log &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log &&

@@ -313,7 +313,7 @@ class GpuInboundEngine(EngineBase):
     def _drop_graph(self):
         for attr in ("_graph", "_graph_nu"):
             if getattr(self, attr, None) is not None:
-                torch.cuda.synchronize(self.device)
+                self._sync_streams()
                 self.lib.sw_graph_destroy(ctypes.c_void_p(getattr(self, attr)))
                 setattr(self, attr, None)
 
@@ -357,6 +357,20 @@ class GpuInboundEngine(EngineBase):
     # e.g. the loopback test that runs W engine shards on one GPU).
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _sync_streams(self):
+        """Wait for this engine's work only: the caller's current stream plus the engine's own
+        streams.  Never a device-wide synchronize -- several engines (tenants, replicas) can share a
+        GPU, and a device sync both waits on their work and breaks a hipGraph capture another
+        engine has in progress ("operation not permitted when stream is capturing")."""
+        torch.cuda.current_stream(self.device).synchronize()
+        for s in (getattr(self, "_comm", None), getattr(self, "_cap_stream", None)):
+            if s is not None:
+                s.synchronize()
+        fp = self.__dict__.get("_fp")
+        if fp is not None:
+            fp.h2d.synchronize()
+            fp.d2h.synchronize()
 
     def frame_varint(self, lens_dev: torch.Tensor, nbytes: int, n_msgs: int, off_dev: torch.Tensor, raw_bytes: int):
         """Rebuild u32 payload offsets from the varint length stream on the current stream."""
@@ -509,7 +523,7 @@ class GpuInboundEngine(EngineBase):
             # rows land in HBM and come back in one DMA: reading them out of the mapped host buffer
             # is CPU-uncached (~2.6 GB/s measured, 0.8 ms per 64K rows; profiles/r1_tenant_step)
             sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence, out_to_device=True)
-            torch.cuda.synchronize(self.device)
+            self._sync_streams()
             return self.collect(sel, raw, from_device=True)
 
     def step_framed(self, batch, now_ms: int, presence: bool | None = None) -> StepResult:
@@ -545,7 +559,7 @@ class GpuInboundEngine(EngineBase):
             self.frame_varint(dev_l, nl, n, dev_o, batch.payload_bytes)
             do_presence = self.presence_due(now_ms) if presence is None else presence
             sel = self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_to_device=True)
-            torch.cuda.synchronize(self.device)
+            self._sync_streams()
             return self.collect(sel, np.asarray(batch.payload), from_device=True)
 
     def _no_framed_pending(self):
@@ -850,7 +864,7 @@ class GpuInboundEngine(EngineBase):
     def checkpoint_state(self, include_store: bool = False) -> dict:
         if self._pend is not None:
             raise RuntimeError("checkpoint with a pipelined exchange in flight: drain the round first")
-        torch.cuda.synchronize(self.device)
+        self._sync_streams()
         st = {k: self.t[k].cpu().numpy() for k in self._CKPT_TABLES}
         if self.world > 1:
             cp = self._carry_par
@@ -861,7 +875,7 @@ class GpuInboundEngine(EngineBase):
         return st
 
     def restore_state(self, a: dict, include_store: bool):
-        torch.cuda.synchronize(self.device)
+        self._sync_streams()
         for k in self._CKPT_TABLES:
             self.t[k].copy_(torch.from_numpy(a[k]))       # in place: captured graphs keep their pointers
         if self.world > 1 and "carry" in a:
@@ -873,7 +887,7 @@ class GpuInboundEngine(EngineBase):
         if include_store:
             for k, v in self.store.items():
                 v.copy_(torch.from_numpy(a[f"store.{k}"]))
-        torch.cuda.synchronize(self.device)
+        self._sync_streams()
 
     def reset_dedup(self):
         self.t["dd_key"].zero_()
