@@ -354,7 +354,32 @@ def add_index_event_routes(r: APIRouter, index: str, getter):
 
 
 # ------------------------------------------------------------------------------ app
-def create_app(instance, topology=None, cors: bool = True) -> FastAPI:
+ADMIN_UI_BUILTIN = __import__("pathlib").Path(__file__).resolve().parent / "admin"
+
+
+def mount_admin_ui(app: FastAPI, directory: str | None = None):
+    """Serve an admin UI build at ``/admin/`` (``directory``, else ``SITEWHERE_ADMIN_UI_DIR``, else the
+    built-in console in ``web/admin``); ``/`` and ``/admin`` redirect to it, as the reference's
+    web-rest does for its Vue app (``VueConfiguration``, ``RedirectServlet``)."""
+    import os
+
+    from fastapi.responses import RedirectResponse
+    from fastapi.staticfiles import StaticFiles
+    d = directory or os.environ.get("SITEWHERE_ADMIN_UI_DIR") or str(ADMIN_UI_BUILTIN)
+    if not os.path.isdir(d):
+        raise SiteWhereException(f"admin UI directory {d!r} does not exist")
+
+    @app.get("/", include_in_schema=False)
+    def root():
+        return RedirectResponse("/admin/")
+
+    @app.get("/admin", include_in_schema=False)
+    def admin():
+        return RedirectResponse("/admin/")
+    app.mount("/admin", StaticFiles(directory=d, html=True), name="admin")
+
+
+def create_app(instance, topology=None, cors: bool = True, admin_ui_dir: str | None = None) -> FastAPI:
     app = FastAPI(title="SiteWhere (MI355X) REST API", version=VERSION["versionIdentifier"],
                   docs_url=f"{API}/docs", openapi_url=f"{API}/openapi.json")
     if cors:   # reference RestSecurity/CORS filter: the admin UI is served from another origin
@@ -442,6 +467,9 @@ def create_app(instance, topology=None, cors: bool = True) -> FastAPI:
     app.include_router(assignments_router())
     app.include_router(misc_router(web))
     app.include_router(admin_router(web))
+
+    # ---- admin UI (reference VueConfiguration: static UI under /admin/, "/" forwards to it) --------
+    mount_admin_ui(app, admin_ui_dir)
 
     @app.get("/metrics")
     def metrics():
@@ -1099,7 +1127,8 @@ class WebRestMicroservice(GlobalMicroservice):
         return {"port": 8080}
 
     def microservice_initialize(self, monitor):
-        self.app = create_app(self.instance, self.topology, bool(self.config.get("cors", True)))
+        self.app = create_app(self.instance, self.topology, bool(self.config.get("cors", True)),
+                              self.config.get("adminUiDir"))
 
     def microservice_start(self, monitor):
         port = self.port_override if self.port_override is not None else int(self.config.get("port", 8080))

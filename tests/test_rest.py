@@ -370,3 +370,24 @@ def test_prometheus_metrics_endpoint(env):
     text = client.get("/metrics").text
     assert "sitewhere_event_sources_" in text or "sitewhere_inbound_processing_" in text
     assert "# TYPE" in text
+
+
+def test_admin_ui_is_hosted(env, tmp_path):
+    """web-rest hosts an admin UI under /admin/ (reference VueConfiguration); the built-in console
+    is served when no UI build is configured, and a configured build directory replaces it."""
+    _, client, _ = env
+    r = client.get("/", follow_redirects=False)
+    assert r.status_code in (302, 307) and r.headers["location"] == "/admin/"
+    page = client.get("/admin/")
+    assert page.status_code == 200 and "SiteWhere (MI355X) console" in page.text
+    assert client.get("/admin", follow_redirects=True).status_code == 200
+    from fastapi import FastAPI
+    from fastapi.testclient import TestClient
+
+    from sitewhere_amd.web.rest import mount_admin_ui
+    (tmp_path / "index.html").write_text("<html>custom build</html>")
+    (tmp_path / "app.js").write_text("console.log(1)")
+    app = FastAPI()
+    mount_admin_ui(app, str(tmp_path))
+    c = TestClient(app)
+    assert c.get("/admin/").text == "<html>custom build</html>" and c.get("/admin/app.js").status_code == 200
