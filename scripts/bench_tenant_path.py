@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--via-bus", action="store_true",
                     help="publish the batches to the tenant's raw-payload topic (zero-copy pinned records, as "
                          "event sources do) and time until the raw consumer has stored and committed them all")
+    ap.add_argument("--zero-copy", action=argparse.BooleanOptionalAction, default=False,
+                    help="frame columnar payloads around the rows in the engine's pinned buffers (zeroCopyRows)")
     ap.add_argument("--gc", choices=["default", "freeze"], default="default",
                     help="freeze: gc.freeze() the heap once the devices are loaded; default: leave the collector alone")
     ap.add_argument("--store-retention", type=int, default=0,
@@ -48,12 +50,14 @@ def main():
                                                           "configurationTemplateId": "gpu-columnar",
                                                           "datasetTemplateId": "empty"}))
     sw.wait_for_tenant("fast", 120)
-    if args.max_msgs:
+    if args.max_msgs or args.zero_copy:
         from sitewhere_amd.runtime.config import dump_document
         ms = sw["inbound-processing"]
         before = ms.get_tenant_engine("fast")
         cfg = dict(before.config)
-        cfg["capacity"] = dict(cfg.get("capacity", {}), max_msgs=args.max_msgs)
+        if args.max_msgs:
+            cfg["capacity"] = dict(cfg.get("capacity", {}), max_msgs=args.max_msgs)
+        cfg["zeroCopyRows"] = bool(args.zero_copy)
         sw.instance.coord.put(ms.tenant_config_path("fast"), dump_document(cfg))
         while ms.get_tenant_engine("fast") in (None, before) or ms.get_tenant_engine("fast").status.value != "Started":
             time.sleep(0.1)
@@ -123,6 +127,18 @@ def main():
         ib.flush()
         dt = time.perf_counter() - t
     em_store = sw.tenant_engine("event-management", "fast").store
+    if os.environ.get("SW_PIN_REFERRERS") == "1":         # diagnostic: who holds the pooled row buffers
+        import gc
+        import sys as _sys
+        for _pin, arr in getattr(ib.engine, "_pin_pool", [])[:3]:
+            refs = gc.get_referrers(arr)
+            print("pool buffer refcount", _sys.getrefcount(arr), [
+                (type(r).__name__, getattr(r, "shape", None), str(type(getattr(r, "base", None)).__name__))
+                for r in refs][:12], file=sys.stderr)
+            for r in refs:
+                if type(r).__name__ == "ndarray":
+                    print("  view referrers:", [type(x).__name__ + ":" + str(x)[:60] for x in gc.get_referrers(r)
+                                                if not isinstance(x, list) or len(x) < 50][:8], file=sys.stderr)
     trace = None
     if ib.trace:                # SW_TENANT_TRACE=1: medians over the second half of the timed batches
         tr = [t for t in ib.trace if len(t) == 9][-(args.batches // 2):]
@@ -141,7 +157,9 @@ def main():
                  for name, t in (("engine_step_ms", ib.step_timer), ("columnar_store_ms", ib.store_timer),
                                  ("publish_ms", ib.publish_timer))}
     print(json.dumps({"metric": "tenant_path_events_per_sec", "engine": ib.engine_kind, "via_bus": args.via_bus,
-                      "gc": args.gc,
+                      "gc": args.gc, "zero_copy_rows": ib.zero_copy_rows,
+                      "payloads_framed": ib.zc_framed, "payloads_copied": ib.zc_copied,
+                      "pinned_rows": getattr(ib.engine, "pin_stats", None),
                       "overlap_steps": ib.overlap,
                       "events": ev,
                       "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,

@@ -47,11 +47,16 @@ _new_bytes.restype = ctypes.py_object
 _new_bytes.argtypes = (ctypes.c_void_p, ctypes.c_ssize_t)
 
 
+def _header(boot: str, first_seq: int, world: int, rank: int, now: int, asg: dict, names: dict,
+            rules: dict | None) -> bytes:
+    return msgpack.packb({"boot": boot, "first_seq": int(first_seq), "world": int(world), "rank": int(rank),
+                          "now": int(now), "asg": {int(k): list(v) for k, v in asg.items()},
+                          "names": {int(k): v for k, v in names.items()}, "rules": rules or {}}, use_bin_type=True)
+
+
 def encode_batch(boot: str, first_seq: int, world: int, rank: int, now: int, rows: np.ndarray, asg: dict,
                  names: dict, rules: dict | None = None) -> bytes:
-    hdr = msgpack.packb({"boot": boot, "first_seq": int(first_seq), "world": int(world), "rank": int(rank),
-                         "now": int(now), "asg": {int(k): list(v) for k, v in asg.items()},
-                         "names": {int(k): v for k, v in names.items()}, "rules": rules or {}}, use_bin_type=True)
+    hdr = _header(boot, first_seq, world, rank, now, asg, names, rules)
     rows = np.ascontiguousarray(rows, OUT_REC)
     head = b"".join((_MAGIC, struct.pack("<I", len(hdr)), hdr))
     if rows.nbytes < (1 << 20):
@@ -65,14 +70,35 @@ def encode_batch(boot: str, first_seq: int, world: int, rank: int, now: int, row
     return out
 
 
-def decode_batch(payload: bytes) -> dict:
-    if payload[:4] != _MAGIC:                 # batches written before the framed format
-        d = msgpack.unpackb(payload, raw=False, strict_map_key=False)
+def frame_batch(frame: tuple, rows_nbytes: int, boot: str, first_seq: int, world: int, rank: int, now: int,
+                asg: dict, names: dict, rules: dict | None = None) -> np.ndarray | None:
+    """Zero-copy form of :func:`encode_batch` for rows that sit at ``offset`` of a host buffer with
+    free bytes in front of them (``frame = (buffer, offset)``, the MI355X engine's pinned row
+    buffers): the header is written right before the rows and the payload is the read-only view
+    header + rows -- no row copy.  None when the header does not fit the free bytes."""
+    buf, off = frame
+    hdr = _header(boot, first_seq, world, rank, now, asg, names, rules)
+    start = off - 8 - len(hdr)
+    if start < 0:
+        return None
+    buf[start:start + 4] = np.frombuffer(_MAGIC, np.uint8)
+    buf[start + 4:start + 8] = np.frombuffer(struct.pack("<I", len(hdr)), np.uint8)
+    buf[start + 8:off] = np.frombuffer(hdr, np.uint8)
+    view = buf[start:off + rows_nbytes]
+    view.flags.writeable = False
+    return view
+
+
+def decode_batch(payload) -> dict:
+    """``bytes`` or a zero-copy buffer (read-only array / memoryview) -> header dict + row view."""
+    buf = payload if isinstance(payload, (bytes, bytearray)) else memoryview(payload).cast("B")
+    if bytes(buf[:4]) != _MAGIC:              # batches written before the framed format
+        d = msgpack.unpackb(bytes(buf), raw=False, strict_map_key=False)
         d["rows"] = np.frombuffer(d["rows"], OUT_REC)
         return d
-    (n,) = struct.unpack_from("<I", payload, 4)
-    d = msgpack.unpackb(payload[8:8 + n], raw=False, strict_map_key=False)
-    d["rows"] = np.frombuffer(payload, OUT_REC, offset=8 + n)
+    (n,) = struct.unpack_from("<I", buf, 4)
+    d = msgpack.unpackb(bytes(buf[8:8 + n]), raw=False, strict_map_key=False)
+    d["rows"] = np.frombuffer(buf, OUT_REC, offset=8 + n)
     return d
 
 
@@ -102,7 +128,7 @@ class ColumnarEventStore(DeviceEventStore):
 
     # ------------------------------------------------------------------ ingest
     def add_columnar(self, payload: bytes | dict) -> int:
-        d = decode_batch(payload) if isinstance(payload, (bytes, bytearray)) else payload
+        d = payload if isinstance(payload, dict) else decode_batch(payload)
         rows = d["rows"]
         n = len(rows)
         with self._lock:

@@ -58,6 +58,9 @@ class StepResult:
     first_seq: int = 0                     # store sequence of out[0]; ids are implicit
     world: int = 1
     rank: int = 0
+    # (buffer, offset) when ``out`` sits at ``offset`` of a pooled pinned buffer with free bytes in
+    # front of it: a columnar batch can be framed around the rows in place (``frame_columnar``)
+    frame_base: tuple | None = None
 
     def event_ids(self) -> np.ndarray:
         n = 0 if self.out is None else len(self.out)

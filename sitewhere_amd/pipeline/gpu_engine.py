@@ -588,33 +588,51 @@ class GpuInboundEngine(EngineBase):
         dev_o[:no].copy_(pin_o[:no], non_blocking=True)
         return dev_r[:nb], dev_o[:no]
 
+    ROW_HEADROOM = 1 << 16      # bytes kept free in front of the rows: a columnar batch header is
+                                # written there, making header + rows one contiguous payload
+
     def _pinned_out(self, nbytes: int):
-        """A pinned host buffer (torch tensor + its full numpy view) that no earlier StepResult still
-        references: a live ``result.out`` view pins its base array, so results are returned without a
-        copy and without fresh pageable pages per step."""
+        """A pinned host buffer (torch tensor + its full numpy view) with ``ROW_HEADROOM`` bytes in
+        front of the rows, that no earlier StepResult still references: a live ``result.out`` view
+        pins its base array, so results are returned without a copy and without fresh pageable pages
+        per step.  Returns (tensor, array, pooled); a result whose buffer is not pooled must not be
+        retained (``StepResult.frame_base`` is left unset)."""
         import sys
+        need = nbytes + self.ROW_HEADROOM
         pool = self.__dict__.setdefault("_pin_pool", [])
+        st = self.__dict__.setdefault("pin_stats", {"reused": 0, "new_pooled": 0, "new_unpooled": 0})
         for pin, arr in pool:
-            if arr.nbytes >= nbytes and sys.getrefcount(arr) <= 3:   # pool tuple, loop variable, the call
-                return pin, arr
-        pin = torch.empty(max(nbytes, self.out_cap * OUT_REC_SIZE), dtype=torch.uint8).pin_memory()
+            if arr.nbytes >= need and sys.getrefcount(arr) <= 3:   # pool tuple, loop variable, the call
+                st["reused"] += 1
+                return pin, arr, True
+        pin = torch.empty(max(need, self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM), dtype=torch.uint8).pin_memory()
         arr = pin.numpy()
-        if len(pool) < 8:       # results held by an overlapped tenant: in flight + store queue + storing
+        # results held by an overlapped tenant: in flight + store queue + storing, and -- with zero-copy
+        # columnar payloads -- the batches the store and the enriched-batch topic retain
+        if len(pool) < self.PIN_POOL:
             pool.append((pin, arr))
-        return pin, arr
+            st["new_pooled"] += 1
+            return pin, arr, True
+        st["new_unpooled"] += 1
+        return pin, arr, False
+
+    PIN_POOL = 24
 
     def collect(self, sel: int, raw_host: np.ndarray | None, from_device: bool = False) -> StepResult:
         part = self._collect_small(raw_host)
         n_out = part["n_persisted"]
+        frame = None
         if from_device:
             nb = n_out * OUT_REC_SIZE
-            pin, arr = self._pinned_out(nb)
+            h = self.ROW_HEADROOM
+            pin, arr, pooled = self._pinned_out(nb)
             if nb:
-                pin[:nb].copy_(self.out_dev[sel][:nb])      # pinned target: a full-rate DMA
-            out = arr[:nb].view(OUT_REC)
+                pin[h:h + nb].copy_(self.out_dev[sel][:nb])      # pinned target: a full-rate DMA
+            out = arr[h:h + nb].view(OUT_REC)
+            frame = (arr, h) if pooled else None
         else:
             out = self.out_host[sel].view(OUT_REC, n_out).copy()
-        return StepResult(out=out, world=self.world, rank=self.rank, **part)
+        return StepResult(out=out, world=self.world, rank=self.rank, frame_base=frame, **part)
 
     def _collect_small(self, raw_host: np.ndarray | None) -> dict:
         """Everything of the last step but its rows: counts, learned names, first store sequence and
@@ -726,7 +744,7 @@ class GpuInboundEngine(EngineBase):
             return
         fp = self._fp
         h = ctypes.c_uint64()
-        rc = 1 if fp.no_sdma else self.lib.sw_sdma_copy(ctypes.c_void_p(s.rows[0].data_ptr()),
+        rc = 1 if fp.no_sdma else self.lib.sw_sdma_copy(ctypes.c_void_p(s.rows[0].data_ptr() + self.ROW_HEADROOM),
                                                          ctypes.c_void_p(_ptr(self.out_dev[s.slot])), nb, 0,
                                                          ctypes.byref(h))
         if rc == 0:
@@ -734,7 +752,8 @@ class GpuInboundEngine(EngineBase):
             return
         fp.no_sdma = True                       # no copy engine on this node: HIP runtime copy
         with torch.cuda.stream(fp.d2h):
-            s.rows[0][:nb].copy_(self.out_dev[s.slot][:nb], non_blocking=True)
+            hr = self.ROW_HEADROOM
+            s.rows[0][hr:hr + nb].copy_(self.out_dev[s.slot][:nb], non_blocking=True)
             s.ev = torch.cuda.Event()
             s.ev.record(fp.d2h)
 
@@ -747,7 +766,11 @@ class GpuInboundEngine(EngineBase):
         elif s.ev is not None:
             s.ev.synchronize()
         nb = s.small["n_persisted"] * OUT_REC_SIZE
-        res = StepResult(out=s.rows[1][:nb].view(OUT_REC), world=self.world, rank=self.rank, **s.small)
+        hr = self.ROW_HEADROOM
+        pin, arr, pooled = s.rows
+        res = StepResult(out=arr[hr:hr + nb].view(OUT_REC), world=self.world, rank=self.rank,
+                         frame_base=(arr, hr) if pooled else None, **s.small)
+        s.rows = None
         return s.token, res
 
     # ------------------------------------------------------------------ queries

@@ -47,6 +47,8 @@ def to_wire(obj):
         return d
     if isinstance(obj, bytes):
         return {"__b": base64.b64encode(obj).decode()}
+    if type(obj).__name__ == "ndarray":         # buffers travel as bytes over the network
+        return {"__b": base64.b64encode(obj.tobytes()).decode()}
     if isinstance(obj, enum.Enum):
         return obj.value
     if isinstance(obj, (list, tuple)):
@@ -107,6 +109,8 @@ def clone(v):
     t = type(v)
     if t in _ATOMIC_TYPES or isinstance(v, enum.Enum):
         return v
+    if t.__name__ == "ndarray" and not v.flags.writeable:
+        return v            # read-only arrays are shared like bytes (zero-copy columnar payloads)
     if t is dict:
         return {k: clone(x) for k, x in v.items()}
     if t is list or t is tuple:

@@ -30,7 +30,7 @@ import numpy as np
 
 from ..models.columnar import (EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC,
                                ST_CONTROL, ST_UNASSIGNED, ST_UNREGISTERED)
-from ..persistence.columnar import encode_batch
+from ..persistence.columnar import encode_batch, frame_batch
 from ..models.domain import (AlertLevel, AlertSource, DeviceAlert, DeviceAssignmentStatus, DeviceLocation,
                              DeviceMeasurement, DeviceStateChange, now_ms)
 from ..pipeline.config import EngineConfig
@@ -119,6 +119,12 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # committed by that thread once a batch is stored (at-least-once holds); with a checkpoint
         # the snapshot owns the commits.
         self.async_store = bool(cfg.get("asyncStore", self.storage == "columnar"))
+        # opt-in: columnar payloads framed around the rows in the engine's pinned row buffers (no host
+        # copy).  Off by default: on the MI355X tenant path the framed row buffers were not handed
+        # back to the engine's pool after the store and topic let go of them, so the pool ran dry
+        # and every later step paid a fresh pinned allocation (profiles/r2_tenant_zcrows)
+        self.zero_copy_rows = bool(cfg.get("zeroCopyRows", False))
+        self.zc_framed = self.zc_copied = 0
         self._store_q: queue.Queue = queue.Queue(maxsize=2)
         self._store_thread = None
         self._store_error = None
@@ -487,11 +493,16 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             with self.publish_timer.time():
                 if self.storage == "columnar" and self.publish == "batches":
                     bus = self.ms.instance.bus
-                    if hasattr(bus, "append_bytes"):   # in place: the log references the payload
-                        bus.append_bytes(self.t_enriched_batches, bus.partition_for(self.t_enriched_batches, None),
-                                         item.payload, ts=now)
+                    pl = item.payload
+                    if hasattr(bus, "append_external"):   # in place: the log references the payload
+                        part = bus.partition_for(self.t_enriched_batches, None)
+                        if isinstance(pl, bytes):
+                            bus.append_bytes(self.t_enriched_batches, part, pl, ts=now)
+                        else:
+                            bus.append_external(self.t_enriched_batches, part, pl, pl.ctypes.data, pl.nbytes, ts=now)
                     else:
-                        self.ms.producer.send(self.t_enriched_batches, None, item.payload)
+                        self.ms.producer.send(self.t_enriched_batches, None,
+                                              pl if isinstance(pl, bytes) else pl.tobytes())
                 elif self.publish == "events":
                     self._publish_events(item.events if item.events is not None else self._to_events(res, now))
             item.published = True
@@ -554,6 +565,14 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         out = res.out if res.out is not None else np.zeros(0, OUT_REC)
         if tr is not None:
             tr.append(time.perf_counter())
+        if self.zero_copy_rows and res.frame_base is not None:
+            # header framed in front of the rows in their pinned buffer: no row copy on the host
+            v = frame_batch(res.frame_base, out.nbytes, self.boot, res.first_seq, res.world, res.rank, now, asg,
+                            names, rules)
+            if v is not None:
+                self.zc_framed += 1
+                return v
+        self.zc_copied += 1
         return encode_batch(self.boot, res.first_seq, res.world, res.rank, now, out, asg, names, rules)
 
     def _publish_events(self, events):

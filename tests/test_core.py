@@ -513,3 +513,33 @@ def test_near_cache_lru_ttl_and_max_idle(monkeypatch):
     assert len(c) == 2 and c.get("a") is None
     c.invalidate("b")
     assert c.get("b") is None
+
+
+def test_zero_copy_columnar_frame_matches_encoded_batch():
+    """A columnar batch framed in place around rows that already sit in a buffer (the MI355X
+    engine's pinned row buffers) reads back like the copied encoding, is shared (not copied) by the
+    in-process RPC codec, travels as bytes over the network codec, and is stored without a copy."""
+    import numpy as np
+
+    from sitewhere_amd.models.columnar import OUT_REC
+    from sitewhere_amd.persistence.columnar import ColumnarEventStore, decode_batch, encode_batch, frame_batch
+    from sitewhere_amd.rpc import codec
+    n, head = 5000, 1 << 16
+    buf = np.zeros(head + n * OUT_REC.itemsize, np.uint8)
+    rows = buf[head:].view(OUT_REC)
+    rows["event_date"] = 1000 + np.arange(n)
+    rows["assignment"] = np.arange(n) % 2
+    rows["v0"] = np.arange(n) * 0.5
+    asg = {0: ["a0", "d0", "c0", "ar0", None], 1: ["a1", "d1", "c1", "ar1", None]}
+    names = {1: "temp"}
+    v = frame_batch((buf, head), rows.nbytes, "boot1", 7, 1, 0, 99, asg, names, {"zone.x": "in zone"})
+    assert v is not None and not v.flags.writeable and np.shares_memory(v, buf)
+    a, b = decode_batch(v), decode_batch(encode_batch("boot1", 7, 1, 0, 99, rows, asg, names, {"zone.x": "in zone"}))
+    assert {k: a[k] for k in a if k != "rows"} == {k: b[k] for k in b if k != "rows"}
+    assert np.array_equal(a["rows"], b["rows"]) and np.shares_memory(a["rows"], buf)
+    assert codec.clone(v) is v                                   # in-process RPC: shared
+    assert codec.from_wire(codec.to_wire(v)) == bytes(v)         # network RPC: bytes
+    st = ColumnarEventStore(dense_rows=100)
+    assert st.add_columnar(v) == n and st.rows == n
+    assert np.shares_memory(st._chunks[-1]["rows"], buf)       # stored without a copy
+    assert frame_batch((buf, 16), rows.nbytes, "boot1", 7, 1, 0, 99, asg, names) is None   # header too big
