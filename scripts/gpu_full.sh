@@ -8,4 +8,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 timeout -k 10 400 python bench.py > $O/bench_default.log 2>&1 && tail -1 $O/bench_default.log | cut -c1-160 &&
 timeout -k 10 400 python bench.py --steps 50 --warmup 10 > $O/bench_50.log 2>&1 && tail -1 $O/bench_50.log | cut -c1-160 &&
 timeout -k 10 600 python scripts/bench_tenant_path.py --devices 20000 --batch 65536 --batches 30 > $O/bench_tenant.log 2>&1 && tail -1 $O/bench_tenant.log &&
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 > "$R/$O/prof/log" 2>&1 && echo "prof ok"
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 > "$R/$O/prof/log" 2>&1 && echo "prof ok" &&
+cd "$R" && python scripts/summarize_prof.py "$O/prof/run_kernel_trace.csv" > "$O/top_kernels.md"
