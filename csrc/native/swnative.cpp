@@ -771,8 +771,11 @@ int64_t swlog_wait(void* h, int32_t topic, int32_t p, int64_t offset, int32_t ti
   Partition* pt = part_of((Log*)h, topic, p);
   if (!pt) return -1;
   std::unique_lock<std::mutex> g(pt->mu);
-  pt->cv.wait_for(g, std::chrono::milliseconds(timeout_ms),
-                  [&] { return pt->base_offset + (int64_t)pt->index.size() > offset; });
+  // a system_clock deadline waits in pthread_cond_timedwait; libstdc++'s steady_clock wait_for uses
+  // pthread_cond_clockwait, which this toolchain's ThreadSanitizer does not intercept (it then sees
+  // the partition mutex as never released and reports every later lock as a race)
+  pt->cv.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
+                    [&] { return pt->base_offset + (int64_t)pt->index.size() > offset; });
   return pt->base_offset + (int64_t)pt->index.size();
 }
 
