@@ -402,6 +402,10 @@ class MqttClient:
             self._send(packet(DISCONNECT, 0, b""))
         except (OSError, AttributeError):
             pass
+        try:      # shutdown first: the reader thread blocked in recv returns now, before the fd can be reused
+            self.sock.shutdown(socket.SHUT_RDWR)
+        except (OSError, AttributeError):
+            pass
         try:
             self.sock.close()
         except (OSError, AttributeError):

@@ -121,7 +121,8 @@ _m("inbound-processing", "Inbound Processing", [
     A("gpuDevice", "Integer", "GPU of this replica (default SITEWHERE_GPU_DEVICE / LOCAL_RANK / 0)"),
     A("overlapSteps", "Boolean", "overlapped engine steps (default on for MI355X columnar tenants)"),
     A("asyncStore", "Boolean", "store rows on a store thread (default on for columnar storage)"),
-    A("tuneGc", "Boolean", "freeze the start-up heap out of the cyclic GC", default=False)], [
+    A("tuneGc", "Boolean", "freeze the start-up heap out of the cyclic GC", default=False),
+    A("zeroCopyRows", "Boolean", "columnar payloads framed in place around the engine's pinned rows", default=True)], [
     E("Zone Tests", "gpu-zone-tests", "zone tests evaluated inside the GPU engine", [
         A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")]),
     E("Checkpoint", "checkpoint", "engine-shard snapshots; raw offsets commit only when covered", [

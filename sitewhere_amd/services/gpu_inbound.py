@@ -119,11 +119,12 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # committed by that thread once a batch is stored (at-least-once holds); with a checkpoint
         # the snapshot owns the commits.
         self.async_store = bool(cfg.get("asyncStore", self.storage == "columnar"))
-        # opt-in: columnar payloads framed around the rows in the engine's pinned row buffers (no host
-        # copy).  Off by default: on the MI355X tenant path the framed row buffers were not handed
-        # back to the engine's pool after the store and topic let go of them, so the pool ran dry
-        # and every later step paid a fresh pinned allocation (profiles/r2_tenant_zcrows)
-        self.zero_copy_rows = bool(cfg.get("zeroCopyRows", False))
+        # columnar payloads framed around the rows in the engine's pinned row buffers (no host copy);
+        # the enriched-batch topic and the store then hold those buffers until their retention
+        # drops them, so batches stick to one topic partition (_batch_partition) to keep that
+        # window inside the engine's buffer pool (profiles/r2_tenant_zcrows)
+        self.zero_copy_rows = bool(cfg.get("zeroCopyRows", True))
+        self._sticky_part: int | None = None
         self.zc_framed = self.zc_copied = 0
         self._store_q: queue.Queue = queue.Queue(maxsize=2)
         self._store_thread = None
@@ -465,6 +466,19 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         else:
             self._store_step(item, commit)
 
+    def _batch_partition(self, bus) -> int:
+        """Partition of the next enriched batch.  Unkeyed batches go round-robin, except with
+        zero-copy payloads: the topic then holds the engine's pinned row buffers until retention
+        drops them, and per-partition retention over round-robin batches would hold partitions x
+        the retention window of them -- more than the engine's buffer pool, which then falls back
+        to a fresh pinned allocation per step.  Those batches stick to one partition per engine
+        (Kafka's sticky partitioner for null keys), so the window is one partition's."""
+        if not self.zero_copy_rows:
+            return bus.partition_for(self.t_enriched_batches, None)
+        if self._sticky_part is None:
+            self._sticky_part = bus.partition_for(self.t_enriched_batches, None)
+        return self._sticky_part
+
     def _store_step(self, item: "_Stepped", commit):
         """Storage stages of one stepped batch; each runs once even when the batch is retried."""
         res, now = item.res, item.now
@@ -495,7 +509,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     bus = self.ms.instance.bus
                     pl = item.payload
                     if hasattr(bus, "append_external"):   # in place: the log references the payload
-                        part = bus.partition_for(self.t_enriched_batches, None)
+                        part = self._batch_partition(bus)
                         if isinstance(pl, bytes):
                             bus.append_bytes(self.t_enriched_batches, part, pl, ts=now)
                         else:
