@@ -473,7 +473,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         the retention window of them -- more than the engine's buffer pool, which then falls back
         to a fresh pinned allocation per step.  Those batches stick to one partition per engine
         (Kafka's sticky partitioner for null keys), so the window is one partition's."""
-        if not self.zero_copy_rows:
+        if not (self.zero_copy_rows and self.engine_kind == "gpu"):
             return bus.partition_for(self.t_enriched_batches, None)
         if self._sticky_part is None:
             self._sticky_part = bus.partition_for(self.t_enriched_batches, None)

@@ -526,5 +526,11 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records():
         em = inst.api("DeviceEventManagement", "ovl")
         res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id], {"pageSize": 0}))
         assert sorted(m.value for m in res.results) == sorted(float(1000 * b + i) for b in range(8) for i in range(200))
+        # zero-copy columnar payloads (the default): batches framed in the engine's pinned rows, all
+        # on the engine's one enriched-batch partition
+        assert ib.zero_copy_rows and ib.zc_framed > 0
+        t_out = inst.instance.naming.tenant_prefix("ovl") + "inbound-enriched-batches"
+        used = [p for p in range(bus.partitions(t_out)) if bus.end_offset(t_out, p) > 0]
+        assert used == [ib._sticky_part]
     finally:
         inst.stop()
