@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--via-bus", action="store_true",
                     help="publish the batches to the tenant's raw-payload topic (zero-copy pinned records, as "
                          "event sources do) and time until the raw consumer has stored and committed them all")
-    ap.add_argument("--zero-copy", action=argparse.BooleanOptionalAction, default=True,
+    ap.add_argument("--zero-copy", action=argparse.BooleanOptionalAction, default=False,
                     help="frame columnar payloads around the rows in the engine's pinned buffers (zeroCopyRows)")
     ap.add_argument("--gc", choices=["default", "freeze"], default="default",
                     help="freeze: gc.freeze() the heap once the devices are loaded; default: leave the collector alone")
@@ -50,7 +50,7 @@ def main():
                                                           "configurationTemplateId": "gpu-columnar",
                                                           "datasetTemplateId": "empty"}))
     sw.wait_for_tenant("fast", 120)
-    if args.max_msgs or not args.zero_copy:
+    if args.max_msgs or args.zero_copy:
         from sitewhere_amd.runtime.config import dump_document
         ms = sw["inbound-processing"]
         before = ms.get_tenant_engine("fast")

@@ -122,7 +122,7 @@ _m("inbound-processing", "Inbound Processing", [
     A("overlapSteps", "Boolean", "overlapped engine steps (default on for MI355X columnar tenants)"),
     A("asyncStore", "Boolean", "store rows on a store thread (default on for columnar storage)"),
     A("tuneGc", "Boolean", "freeze the start-up heap out of the cyclic GC", default=False),
-    A("zeroCopyRows", "Boolean", "columnar payloads framed in place around the engine's pinned rows", default=True)], [
+    A("zeroCopyRows", "Boolean", "columnar payloads framed in place around the engine's pinned rows (pays with a bounded store window)", default=False)], [
     E("Zone Tests", "gpu-zone-tests", "zone tests evaluated inside the GPU engine", [
         A("zoneToken", "String", "zone", True), A("condition", "String", "inside | outside")]),
     E("Checkpoint", "checkpoint", "engine-shard snapshots; raw offsets commit only when covered", [

@@ -119,11 +119,14 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # committed by that thread once a batch is stored (at-least-once holds); with a checkpoint
         # the snapshot owns the commits.
         self.async_store = bool(cfg.get("asyncStore", self.storage == "columnar"))
-        # columnar payloads framed around the rows in the engine's pinned row buffers (no host copy);
-        # the enriched-batch topic and the store then hold those buffers until their retention
-        # drops them, so batches stick to one topic partition (_batch_partition) to keep that
-        # window inside the engine's buffer pool (profiles/r2_tenant_zcrows)
-        self.zero_copy_rows = bool(cfg.get("zeroCopyRows", True))
+        # opt-in: columnar payloads framed around the rows in the engine's pinned row buffers (no
+        # host copy).  The enriched-batch topic and the columnar store then hold those buffers until
+        # their retention drops them, so it pays only when both windows fit the engine's buffer pool
+        # (batches stick to one topic partition for that, _batch_partition): +26-35% at 1M-payload
+        # batches with an 8-batch store window, but with the store's default window (every batch
+        # kept) the pool runs dry and each step pays a fresh pinned allocation
+        # (profiles/r2_tenant_zcrows)
+        self.zero_copy_rows = bool(cfg.get("zeroCopyRows", False))
         self._sticky_part: int | None = None
         self.zc_framed = self.zc_copied = 0
         self._store_q: queue.Queue = queue.Queue(maxsize=2)

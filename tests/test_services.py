@@ -483,10 +483,13 @@ def test_gpu_tenant_checkpoint_resume_replays_exactly(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not __import__("conftest").gpu_available(), reason="needs an MI355X GPU")
-def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records():
+@pytest.mark.parametrize("zero_copy_rows", [False, True])
+def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records(zero_copy_rows):
     """The MI355X columnar tenant steps raw batches overlapped (H2D of batch k+1 and the row D2H of
     batch k-1 beside the compute of batch k), straight from pinned zero-copy topic records: every
-    measurement stored once, unregistered devices routed, offsets committed, record holds released."""
+    measurement stored once, unregistered devices routed, offsets committed, record holds released.
+    With ``zeroCopyRows`` the columnar payloads are framed in the engine's pinned row buffers and
+    the engine's enriched batches stay on one topic partition."""
     from sitewhere_amd.pipeline.bus_io import RawBatchRecord
     from sitewhere_amd.pipeline.fleet import pack_messages
     from sitewhere_amd.pipeline.framing import varint_lengths
@@ -499,8 +502,15 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records():
                                                                 "configurationTemplateId": "gpu-columnar",
                                                                 "datasetTemplateId": "construction"}))
         inst.wait_for_tenant("ovl", 120)
+        if zero_copy_rows:
+            from sitewhere_amd.runtime.config import dump_document
+            ms = inst["inbound-processing"]
+            before = ms.get_tenant_engine("ovl")
+            inst.instance.coord.put(ms.tenant_config_path("ovl"), dump_document(dict(before.config, zeroCopyRows=True)))
+            assert wait_until(lambda: ms.get_tenant_engine("ovl") not in (None, before)
+                              and ms.get_tenant_engine("ovl").status.value == "Started", 120)
         ib = inst.tenant_engine("inbound-processing", "ovl")
-        assert ib.engine_kind == "gpu" and ib.overlap and ib.async_store
+        assert ib.engine_kind == "gpu" and ib.overlap and ib.async_store and ib.zero_copy_rows == zero_copy_rows
         run = lambda f: inst.instance.system_user.run(f, "ovl")  # noqa: E731
         dev = run(lambda: inst.api("DeviceManagement", "ovl").get_device_by_token("galaxytab-001"))
         assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
@@ -526,11 +536,11 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records():
         em = inst.api("DeviceEventManagement", "ovl")
         res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id], {"pageSize": 0}))
         assert sorted(m.value for m in res.results) == sorted(float(1000 * b + i) for b in range(8) for i in range(200))
-        # zero-copy columnar payloads (the default): batches framed in the engine's pinned rows, all
-        # on the engine's one enriched-batch partition
-        assert ib.zero_copy_rows and ib.zc_framed > 0
         t_out = inst.instance.naming.tenant_prefix("ovl") + "inbound-enriched-batches"
         used = [p for p in range(bus.partitions(t_out)) if bus.end_offset(t_out, p) > 0]
-        assert used == [ib._sticky_part]
+        if zero_copy_rows:
+            assert ib.zc_framed > 0 and used == [ib._sticky_part]
+        else:
+            assert ib.zc_framed == 0 and len(used) > 1                # copied payloads go round-robin
     finally:
         inst.stop()
