@@ -600,23 +600,37 @@ class GpuInboundEngine(EngineBase):
         import sys
         need = nbytes + self.ROW_HEADROOM
         pool = self.__dict__.setdefault("_pin_pool", [])
-        st = self.__dict__.setdefault("pin_stats", {"reused": 0, "new_pooled": 0, "new_unpooled": 0})
+        spill = self.__dict__.setdefault("_pin_spill", [])
+        st = self.__dict__.setdefault("pin_stats", {"reused": 0, "new_pooled": 0, "spill": 0, "new_unpooled": 0})
         for pin, arr in pool:
             if arr.nbytes >= need and sys.getrefcount(arr) <= 3:   # pool tuple, loop variable, the call
                 st["reused"] += 1
                 return pin, arr, True
-        pin = torch.empty(max(need, self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM), dtype=torch.uint8).pin_memory()
-        arr = pin.numpy()
+        size = max(need, self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM)
         # results held by an overlapped tenant: in flight + store queue + storing, and -- with zero-copy
         # columnar payloads -- the batches the store and the enriched-batch topic retain
         if len(pool) < self.PIN_POOL:
-            pool.append((pin, arr))
+            pin = torch.empty(size, dtype=torch.uint8).pin_memory()
+            pool.append((pin, pin.numpy()))
             st["new_pooled"] += 1
-            return pin, arr, True
+            return pin, pool[-1][1], True
+        # every pooled buffer is retained downstream: hand out a spill buffer that must not be
+        # retained (the caller copies its rows), so a full pool costs a copy, not a pinned
+        # allocation per step
+        for pin, arr in spill:
+            if arr.nbytes >= need and sys.getrefcount(arr) <= 3:
+                st["spill"] += 1
+                return pin, arr, False
+        pin = torch.empty(size, dtype=torch.uint8).pin_memory()
+        if len(spill) < self.PIN_SPILL:
+            spill.append((pin, pin.numpy()))
+            st["spill"] += 1
+            return pin, spill[-1][1], False
         st["new_unpooled"] += 1
-        return pin, arr, False
+        return pin, pin.numpy(), False
 
     PIN_POOL = 24
+    PIN_SPILL = 6
 
     def collect(self, sel: int, raw_host: np.ndarray | None, from_device: bool = False) -> StepResult:
         part = self._collect_small(raw_host)
