@@ -606,7 +606,10 @@ class GpuInboundEngine(EngineBase):
             if arr.nbytes >= need and sys.getrefcount(arr) <= 3:   # pool tuple, loop variable, the call
                 st["reused"] += 1
                 return pin, arr, True
-        size = max(need, self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM)
+        # sized to this step's rows plus slack (steps of one tenant are about the same size), not to
+        # the engine's full output capacity: pinning a buffer costs time in proportion to its size
+        full = self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM
+        size = max(need, min(full, -(-(need + need // 4) // (1 << 20)) * (1 << 20)))
         # results held by an overlapped tenant: in flight + store queue + storing, and -- with zero-copy
         # columnar payloads -- the batches the store and the enriched-batch topic retain
         if len(pool) < self.PIN_POOL:
