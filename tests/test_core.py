@@ -543,3 +543,38 @@ def test_zero_copy_columnar_frame_matches_encoded_batch():
     assert st.add_columnar(v) == n and st.rows == n
     assert np.shares_memory(st._chunks[-1]["rows"], buf)       # stored without a copy
     assert frame_batch((buf, 16), rows.nbytes, "boot1", 7, 1, 0, 99, asg, names) is None   # header too big
+
+
+def test_pinned_row_pool_sizes_recycles_and_spills(monkeypatch):
+    """The engine's pinned row buffers (GpuInboundEngine._pinned_out): sized to the step's rows plus
+    slack (not the full output capacity), reused once nothing references them, and -- when every
+    pooled buffer is held downstream (zero-copy payloads retained by the store / topic) -- a small
+    set of recycled spill buffers marked not-retainable instead of a pinned allocation per step.
+    Pinning itself is stubbed: the pool logic is host code."""
+    import torch
+
+    from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
+    monkeypatch.setattr(torch.Tensor, "pin_memory", lambda self: self)
+    eng = object.__new__(GpuInboundEngine)
+    eng.out_cap = 1 << 20                                     # 32 MB of rows at full capacity
+    eng.PIN_POOL, eng.PIN_SPILL = 3, 2
+    need = 65536 * 32
+    pin, arr, pooled = eng._pinned_out(need)
+    assert pooled and need + eng.ROW_HEADROOM <= arr.nbytes <= 4 << 20
+    del pin, arr
+    _, again, pooled = eng._pinned_out(need)                  # released: the same buffer comes back
+    assert pooled and eng.pin_stats["reused"] == 1
+    held = [again] + [eng._pinned_out(need)[1] for _ in range(2)]   # the pool (3) is now all held
+    assert eng.pin_stats["new_pooled"] == 3
+    s1 = eng._pinned_out(need)
+    assert s1[2] is False and eng.pin_stats["spill"] == 1
+    addr = s1[1].ctypes.data
+    del s1
+    s2 = eng._pinned_out(need)                                 # the spill buffer is recycled
+    assert s2[2] is False and s2[1].ctypes.data == addr and eng.pin_stats["new_unpooled"] == 0
+    s3 = eng._pinned_out(need)
+    s4 = eng._pinned_out(need)                                 # spill set exhausted: unpooled, last resort
+    assert s3[2] is False and s4[2] is False and eng.pin_stats["new_unpooled"] == 1
+    big = eng._pinned_out(eng.out_cap * 32)                    # a full-capacity step fits too
+    assert big[1].nbytes >= eng.out_cap * 32 + eng.ROW_HEADROOM
+    del held
