@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import json
 import re
+import socket
 import threading
 from concurrent.futures import ThreadPoolExecutor
 from typing import Callable
@@ -148,10 +149,11 @@ class RpcServer(LifecycleComponent):
     component_type = LifecycleComponentType.Other
 
     def __init__(self, resolver: ServiceResolver, tokens: TokenManagement, port: int = 0, host: str = "127.0.0.1",
-                 workers: int = 16):
+                 workers: int = 16, advertise_host: str = ""):
         super().__init__("rpc-server")
         self.resolver, self.tokens = resolver, tokens
         self.host, self.port, self.workers = host, port, workers
+        self.advertise_host = advertise_host or (socket.gethostname() if host in ("0.0.0.0", "::") else host)
         self._server = None
         self.calls = 0
 
@@ -197,7 +199,8 @@ class RpcServer(LifecycleComponent):
 
     @property
     def address(self) -> str:
-        return f"{self.host}:{self.port}"
+        """Where other processes dial this server (advertised in the topology)."""
+        return f"{self.advertise_host}:{self.port}"
 
 
 class ApiChannel:

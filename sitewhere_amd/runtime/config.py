@@ -81,6 +81,11 @@ class InstanceSettings:
     instance_id: str = "sitewhere1"
     grpc_port: int = 0
     management_grpc_port: int = 0
+    # gRPC bind address, and the address other processes are told to dial (topology apiAddress);
+    # an empty advertise address means the bind address, or this host's name when binding 0.0.0.0
+    # (one container / pod per service, as the reference deploys)
+    grpc_host: str = "127.0.0.1"
+    grpc_advertise_host: str = ""
     heartbeat_s: float = 20.0
     topology_eviction_s: float = 60.0
     log_metrics: bool = False
@@ -98,7 +103,8 @@ class InstanceSettings:
     @classmethod
     def from_env(cls, **over):
         s = cls(**over)
-        for f in ("product_id", "instance_id", "filesystem_storage_root", "tracer_server", "local_rpc"):
+        for f in ("product_id", "instance_id", "filesystem_storage_root", "tracer_server", "local_rpc", "grpc_host",
+                  "grpc_advertise_host"):
             v = os.environ.get("SITEWHERE_" + f.upper())
             if v:
                 setattr(s, f, v)

@@ -419,7 +419,9 @@ class Microservice(LifecycleComponent):
         self.register_services(res)
         res.add_global(f"MicroserviceManagement.{self.identifier}", self.management)
         if self.instance.network_rpc:
-            self.rpc_server = RpcServer(res, self.instance.tokens, port=self.instance.settings.grpc_port)
+            st = self.instance.settings
+            self.rpc_server = RpcServer(res, self.instance.tokens, port=st.grpc_port, host=st.grpc_host,
+                                        advertise_host=st.grpc_advertise_host)
 
     def start(self, monitor):
         if self.rpc_server is not None:

@@ -4,7 +4,7 @@
       bus (Kafka role, native commit log) + coordination (ZooKeeper role) server; --kafka-port also
       serves the bus over the Kafka wire protocol (bus/kafka_broker.py) to any Kafka client
   python -m sitewhere_amd.serve service <identifier> [<identifier> ...] --infra HOST:PORT [--kafka BOOTSTRAP]
-                                         [--zookeeper HOST:PORT/CHROOT]
+                                         [--zookeeper HOST:PORT/CHROOT] [--bind 0.0.0.0 --advertise NAME]
       one or more microservices in this process, talking to the shared infra and to other
       processes' services over gRPC (topology-discovered replicas); with --kafka the data plane is
       a Kafka cluster (bus/kafka_client.KafkaEventBus) and with --zookeeper the coordination is a
@@ -63,6 +63,10 @@ def build_instance(args, network: bool):
     from .runtime.config import InstanceSettings
     from .runtime.microservice import Instance
     settings = InstanceSettings.from_env(heartbeat_s=args.heartbeat, grpc_port=getattr(args, "grpc_port", 0))
+    if getattr(args, "bind", None):
+        settings.grpc_host = args.bind
+    if getattr(args, "advertise", None):
+        settings.grpc_advertise_host = args.advertise
     kw = {}
     if getattr(args, "infra", None):
         kw["bus"] = RemoteEventBus(args.infra)
@@ -89,7 +93,7 @@ def cmd_service(args) -> int:
         if cls is None:
             print(f"unknown microservice {ident}; choose from {sorted(SERVICES_BY_ID)}", file=sys.stderr)
             return 2
-        kw = {"port": args.rest_port} if ident == "web-rest" else {}
+        kw = {"port": args.rest_port, "host": args.bind or "127.0.0.1"} if ident == "web-rest" else {}
         ms = cls(inst, **kw)
         if run_microservice(ms) != 0:
             print(f"{ident} failed: {ms.lifecycle_error}", file=sys.stderr)
@@ -125,7 +129,7 @@ def cmd_all(args) -> int:
     return 0
 
 
-def main(argv=None) -> int:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="sitewhere_amd.serve")
     ap.add_argument("--log-level", default="INFO")
     ap.add_argument("--heartbeat", type=float, default=5.0)
@@ -148,11 +152,21 @@ def main(argv=None) -> int:
     p.add_argument("--zookeeper", default=None, help="ZooKeeper connect string (host:port[,..][/chroot])")
     p.add_argument("--grpc-port", type=int, default=0)
     p.add_argument("--rest-port", type=int, default=0)
+    p.add_argument("--bind", default=None,
+                   help="bind address of this process's gRPC and REST servers (0.0.0.0 in a container; "
+                        "env SITEWHERE_GRPC_HOST); default 127.0.0.1")
+    p.add_argument("--advertise", default=None,
+                   help="host other processes dial for this process's gRPC services (env "
+                        "SITEWHERE_GRPC_ADVERTISE_HOST); default: the bind address, or the host name for 0.0.0.0")
     p = sub.add_parser("all")
     p.add_argument("--rest-port", type=int, default=8080)
     p.add_argument("--mqtt-port", type=int, default=0)
     p.add_argument("--data", default=None)
-    args = ap.parse_args(argv)
+    return ap
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     if args.reference_templates:                 # read by tenant management when it starts
