@@ -73,9 +73,11 @@ def _replicas_scenario(kind: str | None = None):
             assert wait(lambda e=e: all(e.asg_index.idx.get(d.device_assignment_id) is not None for d in devs))
         t_raw = sw.instance.naming.tenant_prefix("rep") + "event-source-raw-payloads"
         bus = sw.instance.bus
-        assert wait(lambda: r1.raw_consumer.consumer.assignment() and r2.raw_consumer.consumer.assignment())
-        a1, a2 = set(r1.raw_consumer.consumer.assignment()), set(r2.raw_consumer.consumer.assignment())
-        assert a1 and a2 and not (a1 & a2) and len(a1 | a2) == bus.partitions(t_raw)
+
+        def split():    # the group has converged: disjoint non-empty assignments covering every partition
+            a1, a2 = set(r1.raw_consumer.consumer.assignment()), set(r2.raw_consumer.consumer.assignment())
+            return a1 and a2 and not (a1 & a2) and len(a1 | a2) == bus.partitions(t_raw)
+        assert wait(split), (r1.raw_consumer.consumer.assignment(), r2.raw_consumer.consumer.assignment())
         es = sw.tenant_engine("event-sources", "rep")
         n = 400
         for i in range(n):
