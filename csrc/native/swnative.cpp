@@ -475,17 +475,22 @@ struct Partition {
     segs.pop_front();
     ++seg0;
   }
-  // offset one past the last record held by the front segment
+  // offset one past the last record held by the front segment: index entries are (ordinal << 32 |
+  // byte offset) in append order, so the front segment's records are a sorted prefix -- a binary
+  // search, not a walk over (up to ~10^5) small records under the partition mutex on every append
   int64_t front_segment_end() const {
-    size_t k = 0;
-    while (k < index.size() && (index[k] >> 32) == seg0) ++k;
-    return base_offset + (int64_t)k;
+    auto it = std::lower_bound(index.begin(), index.end(), (int64_t)((uint64_t)(seg0 + 1) << 32));
+    return base_offset + (int64_t)(it - index.begin());
   }
-  bool front_droppable() const { return segs.size() > 1 && front_segment_end() <= hold; }
+  // cheap conditions first; the hold test only runs when a zero-copy reader holds the partition
+  bool front_droppable() const {
+    return segs.size() > 1 && (hold == INT64_MAX || front_segment_end() <= hold);
+  }
   void enforce_retention() {
     if (fd >= 0 || retention_bytes <= 0) return;
     // segment-granular like Kafka: the retained log stays >= retention_bytes
-    while (front_droppable() && bytes - (int64_t)segs.front().used >= retention_bytes) drop_front_segment();
+    while (segs.size() > 1 && bytes - (int64_t)segs.front().used >= retention_bytes && front_droppable())
+      drop_front_segment();
   }
   ~Partition() {
     for (auto& sg : segs) pool->release(sg);
@@ -818,6 +823,7 @@ int64_t swlog_retain_from(void* h, int32_t topic, int32_t p, int64_t offset) {
   Partition* pt = part_of((Log*)h, topic, p);
   if (!pt) return -1;
   std::lock_guard<std::mutex> g(pt->mu);
+  if (offset > pt->hold) offset = pt->hold;   // never under a zero-copy reader's in-flight records
   int64_t drop = offset - pt->base_offset;
   if (drop <= 0) return pt->base_offset;
   if (pt->fd >= 0) return pt->base_offset;  // durable logs keep the in-memory image aligned with the file

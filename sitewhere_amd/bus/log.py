@@ -250,9 +250,10 @@ class EventBus:
     def _drain_released(self) -> list:
         """Hand zero-copy records that retention dropped back to their owners' ``on_release``;
         returns the owners that had none (their references are dropped once the caller lets go)."""
-        ids = self.__dict__.get("_rel_ids")
-        if ids is None:
-            ids = self._rel_ids = np.zeros(256, np.int64)
+        # a scratch array per call: the event-source flush thread and the tenant store thread both
+        # append externally, and a shared array could be overwritten between the native take and
+        # the read below -- those owners would never be released
+        ids = np.zeros(256, np.int64)
         out = []
         while True:
             n = self.fast.swlog_take_released(self.h, ids.ctypes.data, len(ids))
@@ -584,6 +585,7 @@ class Consumer:
         self.generation = bus.join(group, self.member_id, self.topics)
         self.positions: dict[tuple[str, int], int] = {}
         self._assigned: list = []
+        self._held: set = set()             # partitions poll() holds for a zero-copy reader
         self._refresh()
         self.closed = False
 
@@ -631,13 +633,19 @@ class Consumer:
             if out or time.time() >= deadline:
                 return out
 
-    def poll(self, timeout_ms: int = 1000, max_records: int = 500,
-             views: bool = False) -> dict[tuple[str, int], list[Record]]:
+    def poll(self, timeout_ms: int = 1000, max_records: int = 500, views: bool = False,
+             holder=None) -> dict[tuple[str, int], list[Record]]:
         """``views=True`` on the in-process bus: record values are zero-copy views of the log
-        (:meth:`EventBus.read_views`); other buses return copies as usual."""
+        (:meth:`EventBus.read_views`); other buses return copies as usual.  With ``holder`` the poll
+        takes a retention hold (owned by ``holder``) on every partition before reading it in place --
+        after any rebalance refresh, so a partition gained mid-poll is held too -- and remembers
+        which it holds; :meth:`release_holds` drops exactly those, including partitions the
+        rebalance took away."""
         if not self._local and hasattr(self.bus, "fetch_raw"):
             return self._poll_fetch(timeout_ms, max_records)
-        read = self.bus.read_views if views and hasattr(self.bus, "read_views") else self.bus.read
+        views = views and hasattr(self.bus, "read_views")
+        read = self.bus.read_views if views else self.bus.read
+        hold = views and holder is not None and hasattr(self.bus, "hold")
         deadline = time.time() + timeout_ms / 1000.0
         while True:
             self._ev.clear()
@@ -652,6 +660,9 @@ class Consumer:
             for tp in self._assigned:
                 if budget <= 0:
                     break
+                if hold:
+                    self.bus.hold(tp[0], tp[1], self.positions[tp], holder=holder)
+                    self._held.add(tp)
                 recs = read(tp[0], tp[1], self.positions[tp], budget)
                 if recs:
                     out[tp] = recs
@@ -664,6 +675,12 @@ class Consumer:
                 self._ev.wait(min(1.0, left))
             else:
                 self.bus.wait_topics(self.topics, min(1.0, left))
+
+    def release_holds(self, holder):
+        """Drop the retention holds :meth:`poll` took for ``holder``."""
+        held, self._held = self._held, set()
+        for tp in held:
+            self.bus.hold(tp[0], tp[1], None, holder=holder)
 
     def commit(self, offsets: dict[tuple[str, int], int] | None = None):
         """Commit positions (next offset to read); default: current positions of all partitions."""

@@ -128,8 +128,19 @@ class RawBatch:
 
     def offsets(self) -> np.ndarray:
         if self._offs is None:
-            self._offs = offsets_from_varint(self.lens)
+            offs = offsets_from_varint(self.lens)
+            if len(offs) != self.n_msgs + 1 or int(offs[-1]) != self.payload_bytes:
+                raise ValueError(f"raw batch framing mismatch: {len(offs) - 1} lengths summing to {int(offs[-1])} "
+                                 f"for {self.n_msgs} payloads of {self.payload_bytes} bytes")
+            self._offs = offs
         return self._offs
+
+    def validate(self):
+        """Raise ValueError unless the framing is self-consistent (checked before a batch is stepped:
+        a record that fails here is a poison record, dead-lettered instead of retried)."""
+        if self.n_msgs < 0 or self.payload_bytes < 0 or len(self.payload) < self.payload_bytes:
+            raise ValueError("corrupt raw batch header")
+        self.offsets()
 
     def copy(self) -> "RawBatch":
         """Detached copy (the record's memory may be released once the step is done)."""

@@ -38,6 +38,8 @@ def offsets_from_varint(stream: np.ndarray) -> np.ndarray:
     by 7 x its position inside its length."""
     b = np.asarray(stream, np.uint8)
     end = (b & 0x80) == 0
+    if len(b) and not end[-1]:
+        raise ValueError("truncated varint length stream")
     n = int(end.sum())
     offs = np.zeros(n + 1, np.int64)
     if n:
@@ -46,6 +48,8 @@ def offsets_from_varint(stream: np.ndarray) -> np.ndarray:
         first = np.zeros(n, np.int64)
         first[1:] = np.nonzero(end)[0][:-1] + 1            # first byte of every length
         shift = 7 * (np.arange(len(b), dtype=np.int64) - first[grp])
+        if len(shift) and int(shift.max()) > 28:           # > 5 bytes: not a u32 length
+            raise ValueError("over-long varint length")
         vals = (b & 0x7F).astype(np.int64) << shift
         np.cumsum(np.bincount(grp, weights=vals, minlength=n).astype(np.int64), out=offs[1:])
     return offs.astype(np.uint32)

@@ -120,10 +120,8 @@ class BusConsumer(TenantEngineLifecycleComponent):
         views = self.views and hasattr(bus, "read_views") and hasattr(bus, "hold")
         while not self._stop.is_set():
             try:
-                if views:
-                    for tp in self.consumer.assignment():       # hold before reading in place
-                        bus.hold(tp[0], tp[1], self.consumer.positions.get(tp, 0), holder=self)
-                    batch = self.consumer.poll(100, self.max_records, views=True)
+                if views:       # the poll holds each partition before reading it in place
+                    batch = self.consumer.poll(100, self.max_records, views=True, holder=self)
                 else:
                     batch = self.consumer.poll(100, self.max_records)
             except Exception:
@@ -132,8 +130,7 @@ class BusConsumer(TenantEngineLifecycleComponent):
                 continue
             if not batch:
                 if views:
-                    for tp in self.consumer.assignment():
-                        bus.hold(tp[0], tp[1], None, holder=self)
+                    self.consumer.release_holds(self)
                 if self.idle is not None:
                     try:
                         self.idle()
@@ -195,8 +192,7 @@ class BusConsumer(TenantEngineLifecycleComponent):
             if rewind:
                 self.rewinds += 1
             if views:
-                for tp in self.consumer.assignment():
-                    bus.hold(tp[0], tp[1], None, holder=self)    # the handler is done with the views
+                self.consumer.release_holds(self)               # the handler is done with the views
             if self.auto_commit:
                 offsets = {tp: pos for tp, pos in self.consumer.positions.items() if tp not in failed}
                 if offsets:
@@ -213,6 +209,8 @@ class BusConsumer(TenantEngineLifecycleComponent):
         if self._t:
             self._t.join(timeout=3)
         if getattr(self, "consumer", None):
+            if hasattr(self.consumer, "release_holds"):
+                self.consumer.release_holds(self)
             self.consumer.close()
         if self.pool:
             self.pool.shutdown(wait=True)

@@ -153,7 +153,10 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._stepped: dict[tuple, _Stepped] = {}
         self._stored_hw: dict[tuple, int] = {}
         self.replayed_batches = 0
-        # never dead-lettered: a stepped batch cannot be re-stepped, only its storage retried
+        self.dead_lettered = 0                 # raw records that failed validation before a step
+        # the consumer itself never dead-letters: a stepped batch cannot be re-stepped, only its
+        # storage retried; records that fail validation before a step are dead-lettered by the
+        # handler (_dead_letter_raw)
         self.raw_consumer = BusConsumer(self, "raw-payload-consumers", [n.tenant_prefix(t) + RAW_PAYLOADS],
                                         self._process_raw, max_records=16, max_attempts=None,
                                         idle=self._on_idle, views=True,
@@ -343,8 +346,20 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 # record is DMA'd to the MI355X in place.  The record timestamp is the batch's receive
                 # time, so replay after a restore is deterministic.
                 view = isinstance(r.value, memoryview)
-                self.process_raw_batch(parse_raw_batch(r.value), now=r.timestamp or None, commit=commit,
-                                       key=key, detach=view, hold=(r.topic, r.partition, r.offset) if view else None)
+                try:
+                    batch = parse_raw_batch(r.value)
+                    batch.validate()
+                    if batch.n_msgs > self.engine_cfg.max_msgs:
+                        raise ValueError(f"raw batch of {batch.n_msgs} payloads exceeds the engine's "
+                                         f"max_msgs={self.engine_cfg.max_msgs}")
+                except ValueError as e:
+                    # never stepped, so nothing to keep: a poison record is dead-lettered, not retried
+                    # forever (the unlimited retries below are only for stepped-but-unstored batches)
+                    batch = None
+                    self._dead_letter_raw(r, e, commit)
+                if batch is not None:
+                    self.process_raw_batch(batch, now=r.timestamp or None, commit=commit, key=key, detach=view,
+                                           hold=(r.topic, r.partition, r.offset) if view else None)
             else:
                 self.replayed_batches += 1
                 self._submit(item, commit)
@@ -358,6 +373,17 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             end = getattr(self.ms.instance.bus, "end_offset", None)
             if end is None or end(last.topic, last.partition) <= last.offset + 1:
                 self._drain_engine()                    # nothing more queued: complete the last batch
+
+    def _dead_letter_raw(self, r, err, commit):
+        """Park a raw record that cannot be stepped (corrupt framing, over-size batch) on
+        ``<topic>.dead-letter``; its offset is committed in order with the batches around it."""
+        self.ms.producer.send(r.topic + BusConsumer.DEAD_LETTER_SUFFIX, r.key, bytes(r.value))
+        self.dead_lettered += 1
+        self.logger.error("raw batch %s[%d]@%d dead-lettered: %s", r.topic, r.partition, r.offset, err)
+        if commit is not None:
+            done = _Stepped(None, None, 0, None)
+            done.stored = done.published = done.routed = True
+            self._submit(done, commit)
 
     def _on_idle(self):
         self._drain_engine()

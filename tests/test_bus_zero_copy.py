@@ -94,3 +94,15 @@ def test_durable_partitions_refuse_zero_copy(tmp_path):
         _ext(bus, "d", b"v")
     assert bus.end_offset("d", 0) == 0 and not bus._ext
     bus.close()
+
+
+def test_varint_framing_rejects_truncated_and_overlong():
+    import numpy as np
+    import pytest as _pt
+    from sitewhere_amd.pipeline.framing import offsets_from_varint, varint_lengths
+    ok = varint_lengths(np.array([0, 5, 300, 70000], np.int64))
+    assert list(offsets_from_varint(ok)) == [0, 5, 300, 70000]
+    with _pt.raises(ValueError):
+        offsets_from_varint(np.concatenate([ok, np.array([0x85], np.uint8)]))      # truncated
+    with _pt.raises(ValueError):
+        offsets_from_varint(np.array([0xff] * 6 + [0x01], np.uint8))               # > 5 bytes

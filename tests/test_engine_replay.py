@@ -153,3 +153,28 @@ def test_checkpoint_refuses_unstored_batches(inst, tmp_path):
     finally:
         ib._stepped.clear()
         ib.ckpt_path = None
+
+
+def test_poison_raw_record_is_dead_lettered_not_retried(inst):
+    """A raw record that fails validation before it is stepped (truncated varint lengths, framing that
+    does not add up) goes to ``<topic>.dead-letter`` and its offset is committed in order; the good
+    batches around it are stored exactly once."""
+    from sitewhere_amd.pipeline.bus_io import RawBatchRecord
+    from sitewhere_amd.runtime.consumers import BusConsumer
+    ib, run, dev = _tenant(inst, "rpp", "gpu-columnar")
+    topic = inst.instance.naming.tenant_prefix("rpp") + RAW_PAYLOADS
+    bus = inst.instance.bus
+    good = [wire.measurements("galaxytab-001", {"v": float(i)}, event_date=1_700_000_000_000 + i,
+                              alternate_id=f"pp-{i}") for i in range(10)]
+    rec = RawBatchRecord.from_payloads(good, pinned=False).value()
+    bad = bytearray(rec)
+    bad[-1] |= 0x80                     # the last varint length now has its continuation bit set
+    bus.append(topic, 0, [(None, rec[:64] + b"")], ts=1_700_000_200_000)   # header only: corrupt
+    bus.append(topic, 0, [(None, bytes(bad))], ts=1_700_000_200_001)
+    bus.append(topic, 0, [(None, rec)], ts=1_700_000_200_002)
+    end = bus.end_offset(topic, 0)
+    assert wait_until(lambda: bus.committed(ib.raw_consumer.group, topic, 0) == end)
+    assert ib.dead_lettered == 2
+    dl = topic + BusConsumer.DEAD_LETTER_SUFFIX
+    assert sum(bus.end_offset(dl, p) for p in range(bus.partitions(dl))) == 2
+    assert wait_until(lambda: sorted(e.value for e in _values(inst, run, "rpp", dev)) == [float(i) for i in range(10)])
