@@ -53,7 +53,8 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
   bool has_dev = false, has_date = false, has_us = false, us = false, has_elev = false;
   uint32_t n_mx = 0;
   double lat = 0, lon = 0, elev = 0;
-  uint32_t t_off = 0, t_len = 0, m_off = 0, m_len = 0;  // alert type / message
+  // alert type / message; offsets default to the payload start so every record points into its payload
+  uint32_t t_off = start, t_len = 0, m_off = start, m_len = 0;
   pos = bstart;
   while (ok && pos < bend) {
     uint64_t key;
@@ -133,7 +134,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
       if (!(f == 2 && wt == 2)) { if (!sw_skip_field(buf, &pos, bend, wt)) break; continue; }
       sw_read_varint(buf, &pos, bend, &v);
       uint32_t mend = pos + (uint32_t)v;
-      uint32_t n_off = 0, n_len = 0;
+      uint32_t n_off = start, n_len = 0;
       double val = 0;
       while (pos < mend) {
         uint64_t k2;
@@ -168,7 +169,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
   if (cmd == SW_CMD_SEND_DEVICE_LOCATION) {
     out->fp_lo = lo; out->fp_hi = hi; out->event_date = edate; out->name_hash = 0;
     out->v0 = lat; out->v1 = lon; out->v2 = elev; out->alt_hash = alt;
-    out->aux_off = 0; out->aux2_off = 0; out->aux_len = 0; out->aux2_len = 0;
+    out->aux_off = abs_base + start; out->aux2_off = 0; out->aux_len = 0; out->aux2_len = 0;
     out->etype = SW_EV_LOCATION; out->flags = flags; out->src_rank = src_rank; out->level = 0;
     return 1;
   }

@@ -23,6 +23,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -227,8 +228,9 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
     if (u < p_loc) {
       cmd = SW_CMD_SEND_DEVICE_LOCATION;
       eb.str(1, tok, tlen);
-      eb.dbl(2, lat0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0)));
-      eb.dbl(3, lon0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0)));
+      // GPS fixes as devices report them: 6 decimals (~0.1 m), parsed to the nearest double
+      eb.dbl(2, std::nearbyint((lat0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0))) * 1e6) / 1e6);
+      eb.dbl(3, std::nearbyint((lon0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0))) * 1e6) / 1e6);
       eb.dbl(4, 10.0);
       eb.fixed64(5, (uint64_t)ts);
     } else if (u < p_loc + p_alert) {
@@ -247,7 +249,7 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
         Enc em{mx};
         int nl = snprintf(name, sizeof(name), "mx.metric%d", (int)((xs64(s) % (uint64_t)std::max(1, n_names))));
         em.str(1, name, (size_t)nl);
-        em.dbl(2, (double)(xs64(s) % 100000ULL) * 0.01);
+        em.dbl(2, (double)(xs64(s) % 100000ULL) / 100.0);     // a reading with two decimals
         eb.key(2, 2);
         eb.varint(mx.size());
         body.insert(body.end(), mx.begin(), mx.end());

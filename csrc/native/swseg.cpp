@@ -1,0 +1,802 @@
+// Durable columnar event segments (host side): block encoder / decoder / verifier and the
+// segment store -- append-only segment files written by a group-commit writer thread.
+//
+// Format: csrc/include/swseg.h.  The MI355X engine encodes blocks on the GPU (swgpu.hip,
+// k_seg_encode); swseg_encode here is the CPU encoder for host engines and the bit-exact reference
+// the GPU encoder is tested against.
+//
+// Segment store (reference counterpart: the event store behind DeviceEventManagement --
+// MongoDeviceEventManagement + DeviceEventBuffer.java:99-135, bulk writes every 250 ms / 200 docs):
+//   * one directory per engine shard, files "<rank>-<first_seq:020>.sweg", rotated at rotate_bytes;
+//   * every block starts at a 4 KiB boundary (O_DIRECT writes straight from the caller's pinned
+//     buffer when it is aligned, a bounce copy otherwise);
+//   * group commit: the writer drains everything queued, writes it, then one fdatasync; a block's
+//     token is durable once that sync returned (the caller commits its input offsets only then);
+//   * recovery on open: every block is verified (header + page checksums); the first bad or short
+//     block ends its file, which is truncated there (torn tail after a crash);
+//   * optional retention: oldest whole files are deleted beyond retention_bytes.
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "swseg.h"
+
+#define SEG_ALIGN 4096
+
+namespace {
+
+inline uint32_t rd8(uint32_t x) { return (x + 7u) & ~7u; }
+
+// ----------------------------------------------------------------------------- encoder
+struct ColPlan {
+  uint64_t base = 0;
+  uint32_t count = 0, n_exc = 0;
+  int bits = 0, exp = -1;
+};
+
+// Order-preserving unsigned value of column c for row i (integer columns).
+inline uint64_t int_value(int c, const SwOutRec& r, uint64_t alt) {
+  switch (c) {
+    case SEG_ETYPE: return seg_ord((int64_t)r.etype);
+    case SEG_LEVEL: return seg_ord((int64_t)r.level);
+    case SEG_DATE: return seg_ord(r.event_date);
+    case SEG_ASG: return seg_ord((int64_t)r.assignment);
+    case SEG_NAME: return seg_ord((int64_t)r.name_id);
+    case SEG_HASALT: return seg_ord(alt != 0 ? 1 : 0);
+    case SEG_ALT: return alt;          // a hash: already unsigned, stored as is
+    default: return 0;
+  }
+}
+
+inline double dbl_value(int c, const SwOutRec& r, double v2) {
+  return c == SEG_MXV || c == SEG_LAT ? r.v0 : c == SEG_LON ? r.v1 : v2;
+}
+
+struct PageEnc {
+  ColPlan plan[SEG_NCOL];
+  uint32_t bytes = 0;
+};
+
+void plan_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t r0, int m, PageEnc* pe) {
+  uint32_t off = SEG_PAGE_HDR;
+  for (int c = 0; c < SEG_NCOL; ++c) {
+    ColPlan& p = pe->plan[c];
+    if (!seg_is_double(c)) {
+      uint64_t lo = ~0ull, hi = 0;
+      for (int k = 0; k < m; ++k) {
+        const SwOutRec& r = R[r0 + k];
+        if (!seg_member(c, r.etype, A[r0 + k])) continue;
+        const uint64_t u = int_value(c, r, A[r0 + k]);
+        lo = std::min(lo, u);
+        hi = std::max(hi, u);
+        ++p.count;
+      }
+      p.base = p.count ? lo : 0;
+      p.bits = p.count ? seg_bitwidth(hi - lo) : 0;
+      p.exp = -1;
+    } else {
+      int e = 0;
+      for (int k = 0; k < m; ++k) {
+        const SwOutRec& r = R[r0 + k];
+        if (!seg_member(c, r.etype, A[r0 + k])) continue;
+        ++p.count;
+        const int ei = seg_dec_exp(dbl_value(c, r, V2[r0 + k]));
+        if (ei != SEG_EXC_NONE && ei > e) e = ei;
+      }
+      uint64_t lo = ~0ull, hi = 0;
+      for (int k = 0; k < m; ++k) {
+        const SwOutRec& r = R[r0 + k];
+        if (!seg_member(c, r.etype, A[r0 + k])) continue;
+        int64_t q;
+        if (seg_dec_at(dbl_value(c, r, V2[r0 + k]), e, &q)) {
+          lo = std::min(lo, seg_ord(q));
+          hi = std::max(hi, seg_ord(q));
+        } else {
+          ++p.n_exc;
+        }
+      }
+      const bool any = p.count > p.n_exc;
+      p.base = any ? lo : 0;
+      p.bits = any ? seg_bitwidth(hi - lo) : 0;
+      p.exp = e;
+    }
+    off += seg_col_bytes(p.count, p.bits, p.n_exc);
+  }
+  pe->bytes = off;
+}
+
+struct WordSink {
+  uint8_t* page;
+  uint64_t cs = 0;
+  void put(uint32_t byte_off, uint64_t w) {
+    memcpy(page + byte_off, &w, 8);
+    cs ^= seg_mix_word(w, byte_off >> 3);
+  }
+};
+
+void write_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t r0, int m, const PageEnc& pe,
+                uint8_t* page) {
+  WordSink ws{page};
+  std::vector<uint64_t> vals(SEG_PAGE_ROWS);
+  std::vector<uint16_t> exc_idx(SEG_PAGE_ROWS);
+  std::vector<uint64_t> exc_raw(SEG_PAGE_ROWS);
+  SwSegPageHdr hdr;
+  memset(&hdr, 0, sizeof(hdr));
+  hdr.n_rows = (uint32_t)m;
+  hdr.bytes = pe.bytes;
+  uint32_t off = SEG_PAGE_HDR;
+  for (int c = 0; c < SEG_NCOL; ++c) {
+    const ColPlan& p = pe.plan[c];
+    SwSegCol& cd = hdr.cols[c];
+    cd.base = p.base;
+    cd.data_off = off;
+    cd.count = (uint16_t)p.count;
+    cd.n_exc = (uint16_t)p.n_exc;
+    cd.bits = (uint8_t)p.bits;
+    cd.exp = (int8_t)p.exp;
+    uint32_t n = 0, ne = 0;
+    for (int k = 0; k < m; ++k) {
+      const SwOutRec& r = R[r0 + k];
+      if (!seg_member(c, r.etype, A[r0 + k])) continue;
+      if (!seg_is_double(c)) {
+        vals[n++] = int_value(c, r, A[r0 + k]) - p.base;
+      } else {
+        const double v = dbl_value(c, r, V2[r0 + k]);
+        int64_t q;
+        if (seg_dec_at(v, p.exp, &q)) {
+          vals[n] = seg_ord(q) - p.base;
+        } else {
+          vals[n] = 0;
+          exc_idx[ne] = (uint16_t)n;
+          exc_raw[ne++] = sw_f64_bits(v);
+        }
+        ++n;
+      }
+    }
+    const uint32_t nw = seg_col_words(n, p.bits);
+    for (uint32_t w = 0; w < nw; ++w) {
+      uint64_t word = 0;
+      const uint64_t bit0 = (uint64_t)w * 64;
+      uint32_t i = (uint32_t)(bit0 / (uint64_t)p.bits);
+      for (; i < n; ++i) {
+        const uint64_t b = (uint64_t)i * (uint64_t)p.bits;
+        if (b >= bit0 + 64) break;
+        if (b >= bit0) {
+          word |= vals[i] << (b - bit0);
+        } else {                        // value starts in the previous word
+          word |= vals[i] >> (bit0 - b);
+        }
+      }
+      ws.put(off + 8 * w, word);
+    }
+    off += 8 * nw;
+    if (ne) {
+      const uint32_t nidx = (2 * ne + 7) / 8;
+      for (uint32_t w = 0; w < nidx; ++w) {
+        uint64_t word = 0;
+        for (uint32_t j = 0; j < 4; ++j)
+          if (4 * w + j < ne) word |= (uint64_t)exc_idx[4 * w + j] << (16 * j);
+        ws.put(off + 8 * w, word);
+      }
+      off += 8 * nidx;
+      for (uint32_t j = 0; j < ne; ++j) ws.put(off + 8 * j, exc_raw[j]);
+      off += 8 * ne;
+    }
+  }
+  // header words (the checksum word, index 1, is excluded)
+  uint64_t hw[sizeof(SwSegPageHdr) / 8];
+  memcpy(hw, &hdr, sizeof(hdr));
+  for (uint32_t i = 0; i < sizeof(SwSegPageHdr) / 8; ++i)
+    if (i != 1) ws.cs ^= seg_mix_word(hw[i], i);
+  hdr.checksum = ws.cs;
+  memcpy(page, &hdr, sizeof(hdr));
+}
+
+uint64_t header_checksum(const uint8_t* block) {
+  SwSegBlockHdr h;
+  memcpy(&h, block, sizeof(h));
+  h.checksum = 0;
+  uint64_t w[8];
+  memcpy(w, &h, 64);
+  uint64_t cs = 0;
+  for (int i = 0; i < 8; ++i) cs ^= seg_mix_word(w[i], i);
+  const uint32_t pt = rd8(4u * (h.n_pages + 1));
+  for (uint32_t i = 0; i < pt / 8; ++i) {
+    uint64_t x;
+    memcpy(&x, block + 64 + 8 * i, 8);
+    cs ^= seg_mix_word(x, 8 + i);
+  }
+  return cs;
+}
+
+uint64_t unpack(const uint8_t* words, uint32_t i, int bits) {
+  if (bits == 0) return 0;
+  const uint64_t b = (uint64_t)i * (uint64_t)bits;
+  uint64_t w0;
+  memcpy(&w0, words + 8 * (b >> 6), 8);
+  const uint32_t s = (uint32_t)(b & 63);
+  uint64_t v = w0 >> s;
+  if (s + bits > 64) {
+    uint64_t w1;
+    memcpy(&w1, words + 8 * ((b >> 6) + 1), 8);
+    v |= w1 << (64 - s);
+  }
+  return bits == 64 ? v : (v & ((1ull << bits) - 1));
+}
+
+}  // namespace
+
+extern "C" {
+
+// Encode n rows (step order) into `out` (cap bytes).  Writes the block's n_rows / n_pages / bytes
+// and the page table; swseg_seal fills the rest of the header.  Returns the block bytes, or
+// -(bytes needed) when cap is too small.
+int64_t swseg_encode(const SwOutRec* rows, const double* v2, const uint64_t* alt, int64_t n, uint8_t* out,
+                     int64_t cap) {
+  const int64_t np = (n + SEG_PAGE_ROWS - 1) / SEG_PAGE_ROWS;
+  std::vector<PageEnc> pe((size_t)np);
+  const uint32_t start = 64 + rd8(4u * (uint32_t)(np + 1));
+  uint64_t total = start;
+  for (int64_t p = 0; p < np; ++p) {
+    const int m = (int)std::min<int64_t>(SEG_PAGE_ROWS, n - p * SEG_PAGE_ROWS);
+    plan_page(rows, v2, alt, p * SEG_PAGE_ROWS, m, &pe[(size_t)p]);
+    total += pe[(size_t)p].bytes;
+  }
+  if ((int64_t)total > cap) return -(int64_t)total;
+  memset(out, 0, start);
+  uint32_t* pt = (uint32_t*)(out + 64);
+  uint64_t off = start;
+  for (int64_t p = 0; p < np; ++p) {
+    pt[p] = (uint32_t)off;
+    const int m = (int)std::min<int64_t>(SEG_PAGE_ROWS, n - p * SEG_PAGE_ROWS);
+    write_page(rows, v2, alt, p * SEG_PAGE_ROWS, m, pe[(size_t)p], out + off);
+    off += pe[(size_t)p].bytes;
+  }
+  pt[np] = (uint32_t)off;
+  SwSegBlockHdr h;
+  memset(&h, 0, sizeof(h));
+  h.n_rows = (uint32_t)n;
+  h.n_pages = (uint32_t)np;
+  h.bytes = total;
+  memcpy(out, &h, sizeof(h));
+  return (int64_t)total;
+}
+
+// Fill the block header (identity of the batch) and its checksum.
+void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot, int32_t rank, int32_t world) {
+  SwSegBlockHdr h;
+  memcpy(&h, block, sizeof(h));
+  h.magic = SEG_MAGIC;
+  h.version = SEG_VERSION;
+  h.flags = 0;
+  h.first_seq = first_seq;
+  h.recv_ms = recv_ms;
+  h.boot = boot;
+  h.rank = rank;
+  h.world = world;
+  h.checksum = 0;
+  memcpy(block, &h, sizeof(h));
+  h.checksum = header_checksum(block);
+  memcpy(block, &h, sizeof(h));
+}
+
+// 0 = valid; 1 bad header, 2 bad page table, 3 bad page header, 4 page checksum, 5 short.
+int32_t swseg_verify(const uint8_t* b, int64_t len) {
+  if (len < 64) return 5;
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  if (h.magic != SEG_MAGIC || h.version != SEG_VERSION) return 1;
+  const uint64_t start = 64 + rd8(4u * (h.n_pages + 1));
+  if ((int64_t)h.bytes > len || h.bytes < start) return 5;
+  if ((uint64_t)h.n_pages != ((uint64_t)h.n_rows + SEG_PAGE_ROWS - 1) / SEG_PAGE_ROWS) return 1;
+  if (header_checksum(b) != h.checksum) return 1;
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  if (h.n_pages && pt[0] != start) return 2;
+  if (pt[h.n_pages] != h.bytes) return 2;
+  for (uint32_t p = 0; p < h.n_pages; ++p) {
+    const uint32_t o = pt[p], e = pt[p + 1];
+    if (e < o + SEG_PAGE_HDR || e > h.bytes || (o & 7)) return 2;
+    SwSegPageHdr ph;
+    memcpy(&ph, b + o, sizeof(ph));
+    if (ph.bytes != e - o) return 3;
+    const uint32_t want = p + 1 < h.n_pages ? SEG_PAGE_ROWS : h.n_rows - p * SEG_PAGE_ROWS;
+    if (ph.n_rows != want) return 3;
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < ph.bytes / 8; ++i) {
+      if (i == 1) continue;
+      uint64_t w;
+      memcpy(&w, b + o + 8 * i, 8);
+      cs ^= seg_mix_word(w, i);
+    }
+    if (cs != ph.checksum) return 4;
+    for (int c = 0; c < SEG_NCOL; ++c) {
+      const SwSegCol& cd = ph.cols[c];
+      if (cd.bits > 64 || cd.data_off + seg_col_bytes(cd.count, cd.bits, cd.n_exc) > ph.bytes) return 3;
+    }
+  }
+  return 0;
+}
+
+// Decode a (verified) block into per-row arrays of n_rows entries.  Any output may be null.
+// name = 0xffff where the row has none; v0/v1/v2 = 0 where the type has no such value.
+int64_t swseg_decode(const uint8_t* b, uint8_t* etype, uint8_t* level, int64_t* date, int32_t* asg, uint16_t* name,
+                     double* v0, double* v1, double* v2, uint64_t* alt) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  std::vector<uint8_t> et(SEG_PAGE_ROWS);
+  std::vector<double> dv(SEG_PAGE_ROWS);
+  for (uint32_t p = 0; p < h.n_pages; ++p) {
+    const uint8_t* pg = b + pt[p];
+    SwSegPageHdr ph;
+    memcpy(&ph, pg, sizeof(ph));
+    const int64_t r0 = (int64_t)p * SEG_PAGE_ROWS;
+    const uint32_t m = ph.n_rows;
+    // etype first: every other column's membership depends on it
+    {
+      const SwSegCol& cd = ph.cols[SEG_ETYPE];
+      for (uint32_t k = 0; k < m; ++k)
+        et[k] = (uint8_t)seg_unord(cd.base + unpack(pg + cd.data_off, k, cd.bits));
+      if (etype) memcpy(etype + r0, et.data(), m);
+    }
+    std::vector<uint64_t> has(m, 0);
+    {
+      const SwSegCol& cd = ph.cols[SEG_HASALT];
+      for (uint32_t k = 0; k < m; ++k) has[k] = (uint64_t)seg_unord(cd.base + unpack(pg + cd.data_off, k, cd.bits));
+    }
+    for (int c = 0; c < SEG_NCOL; ++c) {
+      if (c == SEG_ETYPE || c == SEG_HASALT) continue;
+      const SwSegCol& cd = ph.cols[c];
+      const uint8_t* words = pg + cd.data_off;
+      if (seg_is_double(c)) {
+        const uint8_t* xi = words + 8 * seg_col_words(cd.count, cd.bits);
+        const uint8_t* xr = xi + ((2u * cd.n_exc + 7u) & ~7u);
+        for (uint32_t i = 0; i < cd.count; ++i)
+          dv[i] = seg_dec_value(seg_unord(cd.base + unpack(words, i, cd.bits)), cd.exp);
+        for (uint32_t j = 0; j < cd.n_exc; ++j) {
+          uint16_t ix;
+          uint64_t raw;
+          memcpy(&ix, xi + 2 * j, 2);
+          memcpy(&raw, xr + 8 * j, 8);
+          if (ix < cd.count) dv[ix] = sw_bits_f64(raw);
+        }
+      }
+      uint32_t i = 0;
+      for (uint32_t k = 0; k < m; ++k) {
+        const int64_t r = r0 + k;
+        const bool mem = seg_member(c, et[k], c == SEG_ALT ? has[k] : 0);
+        switch (c) {
+          case SEG_LEVEL:
+            if (level) level[r] = mem ? (uint8_t)seg_unord(cd.base + unpack(words, i, cd.bits)) : 0;
+            break;
+          case SEG_DATE:
+            if (date) date[r] = seg_unord(cd.base + unpack(words, i, cd.bits));
+            break;
+          case SEG_ASG:
+            if (asg) asg[r] = (int32_t)seg_unord(cd.base + unpack(words, i, cd.bits));
+            break;
+          case SEG_NAME:
+            if (name) name[r] = mem ? (uint16_t)seg_unord(cd.base + unpack(words, i, cd.bits)) : (uint16_t)0xffff;
+            break;
+          case SEG_MXV:                 // runs before SEG_LAT: zero v0 of every non-measurement
+            if (v0) v0[r] = mem ? dv[i] : 0.0;
+            break;
+          case SEG_LAT:
+            if (v0 && mem) v0[r] = dv[i];
+            break;
+          case SEG_LON:
+            if (v1) v1[r] = mem ? dv[i] : 0.0;
+            break;
+          case SEG_ELEV:
+            if (v2) v2[r] = mem ? dv[i] : 0.0;
+            break;
+          case SEG_ALT:
+            if (alt) alt[r] = mem ? cd.base + unpack(words, i, cd.bits) : 0;
+            break;
+        }
+        if (mem) ++i;
+      }
+    }
+  }
+  return h.n_rows;
+}
+
+}  // extern "C"
+
+// ----------------------------------------------------------------------------- segment store
+struct SegFile {
+  std::string path;
+  int64_t first_seq;
+  int64_t bytes;
+  int32_t id;
+};
+
+// Block index entry (kept in memory by the store, rebuilt by the recovery scan).
+typedef struct SwSegIndexEnt {
+  int64_t first_seq;
+  int64_t recv_ms;
+  int64_t offset;
+  int64_t bytes;
+  int32_t file;          // SegFile::id
+  int32_t n_rows;
+  int32_t rank;
+  int32_t world;
+  int64_t min_date;
+  int64_t max_date;
+  int64_t boot;
+} SwSegIndexEnt;
+
+static void block_dates(const uint8_t* b, int64_t* lo, int64_t* hi) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  *lo = INT64_MAX;
+  *hi = INT64_MIN;
+  for (uint32_t p = 0; p < h.n_pages; ++p) {
+    SwSegPageHdr ph;
+    memcpy(&ph, b + pt[p], sizeof(ph));
+    const SwSegCol& cd = ph.cols[SEG_DATE];
+    const uint64_t span = cd.bits >= 64 ? ~0ull : ((1ull << cd.bits) - 1);
+    const uint64_t top = cd.base + span < cd.base ? ~0ull : cd.base + span;
+    *lo = std::min(*lo, seg_unord(cd.base));
+    *hi = std::max(*hi, seg_unord(top));
+  }
+}
+
+static SwSegIndexEnt index_entry(const SwSegBlockHdr& hd, const uint8_t* b, int32_t file, int64_t off) {
+  SwSegIndexEnt e;
+  e.first_seq = hd.first_seq;
+  e.recv_ms = hd.recv_ms;
+  e.offset = off;
+  e.bytes = (int64_t)hd.bytes;
+  e.file = file;
+  e.n_rows = (int32_t)hd.n_rows;
+  e.rank = hd.rank;
+  e.world = hd.world;
+  e.boot = hd.boot;
+  block_dates(b, &e.min_date, &e.max_date);
+  return e;
+}
+
+struct SegItem {
+  const uint8_t* ptr;
+  int64_t len;          // block bytes (unpadded)
+  int64_t token;
+};
+
+struct SegStore {
+  std::string dir;
+  int32_t rank = 0;
+  int64_t rotate_bytes = 1ll << 30;
+  int64_t retention_bytes = 0;
+  bool direct = true;
+  std::mutex mu;
+  std::condition_variable cv, cv_done;
+  std::deque<SegItem> q;
+  std::vector<SegFile> files;
+  std::vector<SwSegIndexEnt> index;      // every retained block, in write order
+  int32_t next_file_id = 0;
+  int64_t next_number = 0;                // file name number of the next new file
+  int fd = -1;
+  int fd_direct = 0;
+  int64_t cur_bytes = 0;
+  std::atomic<int64_t> durable{-1};
+  std::atomic<int64_t> bytes_written{0}, blocks_written{0}, syncs{0}, deleted_files{0}, deleted_bytes{0};
+  std::atomic<int32_t> error{0};
+  bool stop = false;
+  std::thread th;
+  uint8_t* bounce = nullptr;
+  int64_t bounce_cap = 0;
+  int64_t total_bytes = 0;
+};
+
+// Files are numbered in write order ("<rank>-<number>.sweg"): sequences restart with a new engine
+// incarnation, so they cannot name files.
+static std::string seg_name(const std::string& dir, int32_t rank, int64_t number) {
+  char b[64];
+  snprintf(b, sizeof(b), "/%d-%012lld.sweg", rank, (long long)number);
+  return dir + b;
+}
+
+static int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+static bool seg_open_file(SegStore* s, int64_t first) {
+  const std::string p = seg_name(s->dir, s->rank, s->next_number++);
+  int flags = O_WRONLY | O_CREAT | O_EXCL | O_APPEND;
+  int fd = -1;
+  s->fd_direct = 0;
+  if (s->direct) {
+    fd = open(p.c_str(), flags | O_DIRECT, 0644);
+    if (fd >= 0) s->fd_direct = 1;
+  }
+  if (fd < 0) fd = open(p.c_str(), flags, 0644);
+  if (fd < 0) return false;
+  s->fd = fd;
+  s->cur_bytes = 0;
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->files.push_back({p, first, 0, s->next_file_id++});
+  }
+  int dfd = open(s->dir.c_str(), O_RDONLY);
+  if (dfd >= 0) {
+    fsync(dfd);
+    close(dfd);
+  }
+  return true;
+}
+
+static void seg_close_file(SegStore* s) {
+  if (s->fd >= 0) {
+    fdatasync(s->fd);
+    close(s->fd);
+    s->fd = -1;
+  }
+}
+
+static void seg_retention(SegStore* s) {
+  if (s->retention_bytes <= 0) return;
+  std::lock_guard<std::mutex> g(s->mu);
+  while (s->files.size() > 1 && s->total_bytes > s->retention_bytes) {
+    const SegFile f = s->files.front();
+    if (unlink(f.path.c_str()) != 0) break;
+    s->files.erase(s->files.begin());
+    s->index.erase(std::remove_if(s->index.begin(), s->index.end(),
+                                  [&](const SwSegIndexEnt& e) { return e.file == f.id; }),
+                   s->index.end());
+    s->total_bytes -= f.bytes;
+    s->deleted_files += 1;
+    s->deleted_bytes += f.bytes;
+  }
+}
+
+static bool seg_write_all(int fd, const uint8_t* p, int64_t n) {
+  while (n > 0) {
+    ssize_t w = write(fd, p, (size_t)n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += w;
+    n -= w;
+  }
+  return true;
+}
+
+static void seg_writer(SegStore* s) {
+  std::vector<SegItem> batch;
+  while (true) {
+    {
+      std::unique_lock<std::mutex> lk(s->mu);
+      s->cv.wait(lk, [&] { return s->stop || !s->q.empty(); });
+      if (s->q.empty() && s->stop) return;
+      batch.assign(s->q.begin(), s->q.end());
+      s->q.clear();
+    }
+    int64_t last = -1;
+    for (const SegItem& it : batch) {
+      SwSegBlockHdr h;
+      memcpy(&h, it.ptr, sizeof(h));
+      const int64_t padded = round_up(it.len, SEG_ALIGN);
+      if (s->fd < 0 || s->cur_bytes + padded > s->rotate_bytes) {
+        seg_close_file(s);
+        seg_retention(s);
+        if (!seg_open_file(s, h.first_seq)) {
+          s->error = errno ? errno : -1;
+          break;
+        }
+      }
+      const bool aligned = ((uintptr_t)it.ptr % SEG_ALIGN) == 0;
+      bool ok;
+      if (s->fd_direct && aligned) {
+        // the caller padded the buffer to a 4 KiB multiple (swss_append contract)
+        ok = seg_write_all(s->fd, it.ptr, padded);
+      } else {
+        if (s->bounce_cap < padded) {
+          free(s->bounce);
+          s->bounce = (uint8_t*)aligned_alloc(SEG_ALIGN, (size_t)padded);
+          s->bounce_cap = s->bounce ? padded : 0;
+        }
+        if (!s->bounce) {
+          s->error = ENOMEM;
+          break;
+        }
+        memcpy(s->bounce, it.ptr, (size_t)it.len);
+        memset(s->bounce + it.len, 0, (size_t)(padded - it.len));
+        ok = seg_write_all(s->fd, s->bounce, padded);
+      }
+      if (!ok) {
+        s->error = errno ? errno : -1;
+        break;
+      }
+      {
+        std::lock_guard<std::mutex> g(s->mu);
+        s->index.push_back(index_entry(h, it.ptr, s->files.back().id, s->cur_bytes));
+        s->files.back().bytes += padded;
+        s->total_bytes += padded;
+      }
+      s->cur_bytes += padded;
+      s->bytes_written += padded;
+      s->blocks_written += 1;
+      last = it.token;
+    }
+    if (s->error) {
+      s->cv_done.notify_all();
+      continue;                         // tokens stop advancing; the caller sees the error
+    }
+    if (s->fd >= 0 && fdatasync(s->fd) != 0) {
+      s->error = errno ? errno : -1;
+      s->cv_done.notify_all();
+      continue;
+    }
+    s->syncs += 1;
+    if (last >= 0) {
+      std::lock_guard<std::mutex> g(s->mu);
+      if (last > s->durable) s->durable = last;
+    }
+    s->cv_done.notify_all();
+  }
+}
+
+// Scan one segment file: verify every block, truncate a torn tail.  Calls emit(offset, header).
+template <typename F>
+static int64_t seg_scan_file(const std::string& path, bool truncate, F emit) {
+  int fd = open(path.c_str(), truncate ? O_RDWR : O_RDONLY);
+  if (fd < 0) return -1;
+  struct stat st;
+  fstat(fd, &st);
+  const int64_t size = st.st_size;
+  int64_t off = 0;
+  std::vector<uint8_t> buf;
+  while (off + 64 <= size) {
+    SwSegBlockHdr h;
+    if (pread(fd, &h, sizeof(h), off) != (ssize_t)sizeof(h)) break;
+    if (h.magic != SEG_MAGIC || h.version != SEG_VERSION || h.bytes < 64 || off + (int64_t)h.bytes > size) break;
+    buf.resize(h.bytes);
+    if (pread(fd, buf.data(), h.bytes, off) != (ssize_t)h.bytes) break;
+    if (swseg_verify(buf.data(), (int64_t)h.bytes) != 0) break;
+    emit(off, h, buf.data());
+    off += round_up((int64_t)h.bytes, SEG_ALIGN);
+  }
+  if (off > size) off = size;
+  if (truncate && off < size) {
+    if (ftruncate(fd, off) == 0) fdatasync(fd);
+  }
+  close(fd);
+  return off;
+}
+
+extern "C" {
+
+void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t retention_bytes, int32_t direct) {
+  SegStore* s = new SegStore();
+  s->dir = dir;
+  s->rank = rank;
+  if (rotate_bytes > 0) s->rotate_bytes = rotate_bytes;
+  s->retention_bytes = retention_bytes;
+  s->direct = direct != 0;
+  mkdir(dir, 0755);
+  // recovery: existing files of this rank, oldest first, torn tails truncated
+  std::vector<SegFile> found;
+  if (DIR* d = opendir(dir)) {
+    while (dirent* e = readdir(d)) {
+      int r;
+      long long first;
+      char tail[8];
+      if (sscanf(e->d_name, "%d-%lld.%7s", &r, &first, tail) == 3 && r == rank && strcmp(tail, "sweg") == 0) {
+        found.push_back({s->dir + "/" + e->d_name, (int64_t)first, 0, 0});
+        s->next_number = std::max<int64_t>(s->next_number, (int64_t)first + 1);
+      }
+    }
+    closedir(d);
+  }
+  std::sort(found.begin(), found.end(), [](const SegFile& a, const SegFile& b) { return a.first_seq < b.first_seq; });
+  for (auto& f : found) {
+    f.id = s->next_file_id;
+    f.bytes = seg_scan_file(f.path, true, [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) {
+      s->index.push_back(index_entry(hd, b, f.id, off));
+    });
+    if (f.bytes < 0) continue;
+    ++s->next_file_id;
+    s->files.push_back(f);
+    s->total_bytes += f.bytes;
+  }
+  s->th = std::thread(seg_writer, s);
+  return s;
+}
+
+// Queue a sealed block for writing.  `ptr` must stay valid and unchanged until swss_durable() >=
+// token; when it is 4 KiB aligned it should be readable up to the next 4 KiB multiple of len
+// (O_DIRECT writes the padding straight from it; the caller zeroes it).  Tokens must increase.
+int32_t swss_append(void* h, const uint8_t* ptr, int64_t len, int64_t token) {
+  SegStore* s = (SegStore*)h;
+  if (s->error) return s->error;
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->q.push_back({ptr, len, token});
+  }
+  s->cv.notify_one();
+  return 0;
+}
+
+int64_t swss_durable(void* h) { return ((SegStore*)h)->durable.load(); }
+
+int32_t swss_error(void* h) { return ((SegStore*)h)->error.load(); }
+
+// Wait until `token` is durable (or an error / timeout).  Returns 0 when durable.
+int32_t swss_wait(void* h, int64_t token, int64_t timeout_ms) {
+  SegStore* s = (SegStore*)h;
+  std::unique_lock<std::mutex> lk(s->mu);
+  const auto until = std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (s->durable.load() < token && !s->error) {
+    if (s->cv_done.wait_until(lk, until) == std::cv_status::timeout) break;
+  }
+  if (s->error) return s->error;
+  return s->durable.load() >= token ? 0 : -1;
+}
+
+// Counters: bytes written, blocks written, syncs, deleted files, deleted bytes, retained bytes, files.
+void swss_stats(void* h, int64_t* out) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  out[0] = s->bytes_written;
+  out[1] = s->blocks_written;
+  out[2] = s->syncs;
+  out[3] = s->deleted_files;
+  out[4] = s->deleted_bytes;
+  out[5] = s->total_bytes;
+  out[6] = (int64_t)s->files.size();
+  out[7] = s->fd_direct;
+}
+
+void swss_close(void* h) {
+  SegStore* s = (SegStore*)h;
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->stop = true;
+  }
+  s->cv.notify_all();
+  if (s->th.joinable()) s->th.join();
+  seg_close_file(s);
+  free(s->bounce);
+  delete s;
+}
+
+// Index of every retained block, in write order (durable or queued-and-written).  Returns the
+// entry count; fills at most cap entries.
+int64_t swss_index(void* h, SwSegIndexEnt* out, int64_t cap) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  const int64_t n = (int64_t)s->index.size();
+  for (int64_t i = 0; i < n && i < cap; ++i) out[i] = s->index[(size_t)i];
+  return n;
+}
+
+// Path of segment file `id` (SwSegIndexEnt::file) into buf; returns its length, -1 if deleted.
+int32_t swss_file(void* h, int32_t id, char* buf, int32_t cap) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  for (const SegFile& f : s->files)
+    if (f.id == id) return snprintf(buf, (size_t)cap, "%s", f.path.c_str());
+  return -1;
+}
+
+// Summary of a block already in memory (min / max event date bounds) for index entries.
+void swseg_dates(const uint8_t* b, int64_t* lo, int64_t* hi) { block_dates(b, lo, hi); }
+
+}  // extern "C"

@@ -26,8 +26,9 @@ LIB_DIR = Path(__file__).resolve().parent / "_lib"
 CSRC = ROOT / "csrc"
 GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
 
-_NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp"]
-_GPU_SRC = [CSRC / "hip" / "swgpu.hip"]
+_NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp", CSRC / "native" / "swseg.cpp",
+               CSRC / "native" / "swroute.cpp"]
+_GPU_SRC = [CSRC / "hip" / "swgpu.hip", CSRC / "hip" / "swseg.hip"]
 _HEADERS = sorted((CSRC / "include").glob("*.h"))
 
 _lock = threading.Lock()
@@ -160,6 +161,25 @@ def native():
         _proto(lib, "swce_ms_export", c_int64, P, P)
         _proto(lib, "swce_ms_import", None, P, P, c_int64)
         _proto(lib, "swce_ms_of", c_int64, P, c_int32, P, c_int64)
+        # durable columnar segments (csrc/native/swseg.cpp)
+        _proto(lib, "swseg_encode", c_int64, P, P, P, c_int64, P, c_int64)
+        _proto(lib, "swseg_seal", None, P, c_int64, c_int64, c_int64, c_int32, c_int32)
+        _proto(lib, "swseg_verify", c_int32, P, c_int64)
+        _proto(lib, "swseg_decode", c_int64, P, P, P, P, P, P, P, P, P, P)
+        _proto(lib, "swseg_dates", None, P, P, P)
+        _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)
+        _proto(lib, "swss_append", c_int32, P, P, c_int64, c_int64)
+        _proto(lib, "swss_durable", c_int64, P)
+        _proto(lib, "swss_error", c_int32, P)
+        _proto(lib, "swss_wait", c_int32, P, c_int64, c_int64)
+        _proto(lib, "swss_stats", None, P, P)
+        _proto(lib, "swss_close", None, P)
+        _proto(lib, "swss_index", c_int64, P, P, c_int64)
+        _proto(lib, "swss_file", c_int32, P, c_int32, c_char_p, c_int32)
+        _proto(lib, "sw_route_rejects", c_int64, P, P, c_int64, P, P, c_int64, c_char_p, P, P, c_int64, P,
+               c_int64, P, c_int64, P, P)
+        _proto(lib, "sw_route_refs", c_int64, P, P, c_int64, c_int32, c_char_p, P, P, c_int64, P, c_int64, P,
+               c_int64, P, P)
         _native = lib
         return lib
 
@@ -237,6 +257,7 @@ def gpu():
         _proto(lib, "sw_graph_launch", c_int32, P, P)
         _proto(lib, "sw_graph_destroy", c_int32, P)
         _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
+        _proto(lib, "sw_seg_encode", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _gpu = lib
         return lib
 

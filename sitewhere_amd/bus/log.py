@@ -395,6 +395,26 @@ class EventBus:
             return self.read_framed(name, partition, offset, max_records, -w + 64)
         return n.value, buf[:w].tobytes()
 
+    def append_arrays(self, name: str, partition: int, keys: np.ndarray, key_off: np.ndarray, vals: np.ndarray,
+                      val_off: np.ndarray, ts: int | None = None) -> int:
+        """Append len(key_off) - 1 records whose keys / values sit back to back in two heaps (offsets
+        [n+1] into each) in one native call -- natively built record batches (routed rejects)."""
+        n = len(key_off) - 1
+        if n <= 0:
+            return -1
+        t = self.topic(name)
+        kb = np.ascontiguousarray(keys, np.uint8) if len(keys) else np.zeros(1, np.uint8)
+        vb = np.ascontiguousarray(vals, np.uint8) if len(vals) else np.zeros(1, np.uint8)
+        ko = np.ascontiguousarray(key_off, np.int64)
+        vo = np.ascontiguousarray(val_off, np.int64)
+        tsa = np.full(n, ts if ts is not None else int(time.time() * 1000), np.int64)
+        first = self.fast.swlog_append_batch(self.h, t, partition, kb.ctypes.data, ko.ctypes.data, vb.ctypes.data,
+                                            vo.ctypes.data, tsa.ctypes.data, n)
+        if first < 0:
+            raise RuntimeError(f"append to {name}[{partition}] failed")
+        self._wake(name)
+        return first
+
     def append_many(self, batches, ts: int | None = None):
         """[(topic, partition, [(key, value)])] in one call (a producer's flushed batches)."""
         for name, p, recs in batches:
@@ -530,6 +550,24 @@ class Producer:
         if buf:
             self._tls.buf = {}
             self.bus.append_many([(t, p, recs) for (t, p), recs in buf.items()])
+
+    def send_arrays(self, topic: str, partition: int, keys, key_off, vals, val_off):
+        """Records of one partition from a key heap and a value heap (offsets [n+1] into each): one
+        native append on the in-process bus, (key, value) pairs elsewhere."""
+        n = len(key_off) - 1
+        if n <= 0:
+            return
+        buf = getattr(self._tls, "buf", None)
+        if buf is None and hasattr(self.bus, "append_arrays"):
+            self.bus.append_arrays(topic, partition, keys, key_off, vals, val_off)
+        else:
+            kb, vb = bytes(keys), bytes(vals)
+            recs = [(kb[key_off[i]:key_off[i + 1]] or None, vb[val_off[i]:val_off[i + 1]]) for i in range(n)]
+            if buf is not None:
+                buf.setdefault((topic, partition), []).extend(recs)
+            else:
+                self.bus.append_many([(topic, partition, recs)])
+        self.sent += n
 
     def send_batch(self, topic: str, records: list[tuple[str | bytes | None, bytes]]):
         """Group by partition and append each group in one native call (batched produce)."""

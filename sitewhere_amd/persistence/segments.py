@@ -1,0 +1,581 @@
+"""Durable columnar event segments: the persistent event store of MI355X (and native CPU) tenants.
+
+Each engine step's persisted events become one *block* (format: ``csrc/include/swseg.h``): ~8 B per
+event, frame-of-reference + decimal coded columns, page checksums.  On the MI355X the block is
+encoded by ``k_seg_encode`` right after the step and only the compressed block crosses PCIe; host
+engines encode the same bytes with :func:`encode_block`.  :class:`SegmentStore` appends blocks to
+segment files through the native group-commit writer (``csrc/native/swseg.cpp``: O_DIRECT when the
+buffer allows it, one ``fdatasync`` per drained group, torn-tail recovery on open).  A block's token
+is durable once its sync returned: input offsets are committed only then (at-least-once across a
+crash; replayed blocks are skipped by sequence).
+
+:class:`DurableEventStore` is the ``DeviceEventStore`` over a segment store: it keeps the
+dictionaries the rows refer to (assignment index -> ids, name id -> name, rule alert messages) in a
+small fsync'd JSON-lines log beside the segments, answers the event-management queries by decoding
+the blocks whose date range overlaps, and survives restarts (everything is reloaded from disk).
+
+Reference: ``DeviceEventBuffer.java:99-135`` (buffered bulk writes, flushed every 250 ms / 200
+documents, lost on a crash: ``SURVEY §5.4``) and ``MongoDeviceEventManagement`` (queries by index
+and date range).  Here nothing is acknowledged before it is on disk.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import threading
+from collections import OrderedDict
+
+import numpy as np
+
+from .._native import native
+from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC
+from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceEventIndex,
+                             DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults)
+from .events import DeviceEventStore, MemoryEventStore
+
+SEG_ALIGN = 4096
+PAGE_ROWS = 1024
+HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("flags", "<u2"), ("n_rows", "<u4"), ("n_pages", "<u4"),
+                ("bytes", "<u8"), ("first_seq", "<i8"), ("recv_ms", "<i8"), ("boot", "<i8"), ("rank", "<i4"),
+                ("world", "<i4"), ("checksum", "<u8")])
+assert HDR.itemsize == 64
+INDEX_ENT = np.dtype([("first_seq", "<i8"), ("recv_ms", "<i8"), ("offset", "<i8"), ("bytes", "<i8"),
+                      ("file", "<i4"), ("n_rows", "<i4"), ("rank", "<i4"), ("world", "<i4"),
+                      ("min_date", "<i8"), ("max_date", "<i8"), ("boot", "<i8")])
+assert INDEX_ENT.itemsize == 72
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def max_block_bytes(n_rows: int) -> int:
+    """Upper bound of an encoded block (every column at 64 bits plus exceptions), padded."""
+    pages = (n_rows + PAGE_ROWS - 1) // PAGE_ROWS
+    worst = 64 + 8 * (pages + 2) + pages * (16 + 11 * 24) + n_rows * (11 * 8 + 4 * 10) + 8 * 4 * 11 * pages
+    return -(-worst // SEG_ALIGN) * SEG_ALIGN
+
+
+def encode_block(rows: np.ndarray, v2: np.ndarray | None = None, alt: np.ndarray | None = None) -> np.ndarray:
+    """CPU encoder (bit-identical to the MI355X ``k_seg_encode``): OUT_REC rows + elevation + alt-id
+    hash columns -> block bytes (header sealed separately by :func:`seal`)."""
+    rows = np.ascontiguousarray(rows, OUT_REC)
+    n = len(rows)
+    v2 = np.zeros(n, np.float64) if v2 is None else np.ascontiguousarray(v2, np.float64)
+    alt = np.zeros(n, np.uint64) if alt is None else np.ascontiguousarray(alt, np.uint64)
+    cap = max_block_bytes(n)
+    out = np.zeros(cap, np.uint8)
+    r = native().swseg_encode(_p(rows) if n else None, _p(v2) if n else None, _p(alt) if n else None, n, _p(out),
+                              cap)
+    if r < 0:
+        raise RuntimeError(f"block needs {-r} bytes")
+    return out[:r]
+
+
+def seal(block: np.ndarray, first_seq: int, recv_ms: int, boot: int, rank: int, world: int):
+    """Fill the header: the block's first store sequence, receive time and engine incarnation."""
+    native().swseg_seal(_p(block), int(first_seq), int(recv_ms), int(boot), int(rank), int(world))
+
+
+def verify(block) -> int:
+    b = np.frombuffer(block, np.uint8) if not isinstance(block, np.ndarray) else block
+    return int(native().swseg_verify(_p(b), len(b)))
+
+
+def header(block) -> dict:
+    b = np.frombuffer(block, np.uint8, 64) if not isinstance(block, np.ndarray) else block[:64]
+    h = b.view(HDR)[0]
+    return {k: int(h[k]) for k in HDR.names}
+
+
+def decode_block(block) -> dict:
+    """Block -> per-row columns (etype, level, date, asg, name, v0, v1, v2, alt) + header fields."""
+    b = np.ascontiguousarray(np.frombuffer(block, np.uint8) if not isinstance(block, np.ndarray) else block)
+    rc = verify(b)
+    if rc:
+        raise ValueError(f"corrupt event block (code {rc})")
+    h = header(b)
+    n = h["n_rows"]
+    cols = {"etype": np.empty(n, np.uint8), "level": np.empty(n, np.uint8), "date": np.empty(n, np.int64),
+            "asg": np.empty(n, np.int32), "name": np.empty(n, np.uint16), "v0": np.empty(n, np.float64),
+            "v1": np.empty(n, np.float64), "v2": np.empty(n, np.float64), "alt": np.empty(n, np.uint64)}
+    if n:
+        native().swseg_decode(_p(b), *[_p(cols[k]) for k in ("etype", "level", "date", "asg", "name", "v0", "v1",
+                                                             "v2", "alt")])
+    cols["header"] = h
+    return cols
+
+
+def rows_of(cols: dict) -> np.ndarray:
+    """Decoded columns -> OUT_REC rows (the enriched-row form consumers use)."""
+    out = np.zeros(len(cols["date"]), OUT_REC)
+    out["event_date"], out["v0"], out["v1"] = cols["date"], cols["v0"], cols["v1"]
+    out["assignment"], out["name_id"], out["etype"], out["level"] = cols["asg"], cols["name"], cols["etype"], cols["level"]
+    return out
+
+
+class SegmentStore:
+    """Native durable segment store of one engine shard (see module docstring)."""
+
+    def __init__(self, directory: str, rank: int = 0, rotate_bytes: int = 1 << 30, retention_bytes: int = 0,
+                 direct: bool = True):
+        os.makedirs(directory, exist_ok=True)
+        self.lib = native()
+        self.dir = directory
+        self.rank = rank
+        self.h = self.lib.swss_open(directory.encode(), int(rank), int(rotate_bytes), int(retention_bytes),
+                                    1 if direct else 0)
+        self._owners: OrderedDict[int, object] = OrderedDict()     # token -> buffer owner (kept until durable)
+        self._lock = threading.Lock()
+        self._token = int(self.lib.swss_durable(self.h))
+        self.closed = False
+
+    def append(self, ptr: int, nbytes: int, owner=None) -> int:
+        """Queue a sealed block at ``ptr`` (``nbytes``, readable up to the next 4 KiB multiple with
+        zeroed padding when ``ptr`` is 4 KiB aligned).  ``owner`` is kept alive until the block is
+        durable.  Returns the block's token (see :meth:`durable`)."""
+        with self._lock:
+            self._token += 1
+            tok = self._token
+            self._owners[tok] = owner
+            rc = self.lib.swss_append(self.h, ptr, int(nbytes), tok)
+        if rc:
+            raise OSError(rc, f"segment store append failed: {os.strerror(rc) if rc > 0 else rc}")
+        return tok
+
+    def append_block(self, block: np.ndarray) -> int:
+        return self.append(_p(block), len(block), block)
+
+    def durable(self) -> int:
+        """Highest token whose block (and every earlier one) is on disk."""
+        d = int(self.lib.swss_durable(self.h))
+        with self._lock:
+            while self._owners and next(iter(self._owners)) <= d:
+                self._owners.popitem(last=False)
+        err = int(self.lib.swss_error(self.h))
+        if err:
+            raise OSError(err, f"segment store write failed: {os.strerror(err) if err > 0 else err}")
+        return d
+
+    def wait(self, token: int, timeout_s: float = 60.0) -> bool:
+        rc = int(self.lib.swss_wait(self.h, int(token), int(timeout_s * 1000)))
+        if rc > 0:
+            raise OSError(rc, f"segment store write failed: {os.strerror(rc)}")
+        self.durable()
+        return rc == 0
+
+    def flush(self, timeout_s: float = 60.0) -> bool:
+        return self.wait(self._token, timeout_s)
+
+    @property
+    def last_token(self) -> int:
+        return self._token
+
+    def stats(self) -> dict:
+        a = np.zeros(8, np.int64)
+        self.lib.swss_stats(self.h, _p(a))
+        return dict(zip(("bytes_written", "blocks_written", "syncs", "deleted_files", "deleted_bytes", "retained_bytes",
+                         "files", "direct_io"), (int(x) for x in a)))
+
+    def index(self) -> np.ndarray:
+        cap = 1024
+        while True:
+            out = np.zeros(cap, INDEX_ENT)
+            n = int(self.lib.swss_index(self.h, _p(out), cap))
+            if n <= cap:
+                return out[:n]
+            cap = n + 1024
+
+    def file_path(self, file_id: int) -> str | None:
+        buf = ctypes.create_string_buffer(4096)
+        n = self.lib.swss_file(self.h, int(file_id), buf, 4096)
+        return None if n < 0 else buf.value.decode()
+
+    def read_block(self, ent) -> np.ndarray:
+        path = self.file_path(int(ent["file"]))
+        if path is None:
+            raise KeyError("segment file deleted by retention")
+        with open(path, "rb", buffering=0) as f:
+            f.seek(int(ent["offset"]))
+            return np.frombuffer(f.read(int(ent["bytes"])), np.uint8)
+
+    def close(self):
+        if not self.closed:
+            self.closed = True
+            self.lib.swss_close(self.h)
+            self._owners.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class _BlockBuf:
+    __slots__ = ("hb", "host", "nbytes", "refs", "token")
+
+    def __init__(self, hb):
+        self.hb, self.host, self.nbytes = hb, hb.host, hb.nbytes
+        self.refs = 0
+        self.token = -1
+
+
+class DurableBlockSink:
+    """Pinned, page-aligned host buffers for the MI355X runner's encoded blocks
+    (``PipelinedRunner(block_sink=...)``).  Each step's block is DMA'd by the copy engine into one,
+    sealed, queued to the durable store (O_DIRECT straight from the buffer) and, with a bus, published
+    in place to the enriched-batch topic.  A buffer goes back to the pool once the store has made its
+    block durable and the topic's retention has released it.  ``publish`` returns the store token;
+    ``committable(tag)`` lists the caller tags (e.g. raw-topic offsets) whose blocks are durable."""
+
+    def __init__(self, store: "DurableEventStore", lib, boot: int, rank: int = 0, world: int = 1, bus=None,
+                 topic: str | None = None, partition: int = 0, max_buffers: int = 64):
+        from ..pipeline.gpu_engine import HostBuffer
+        self._HostBuffer = HostBuffer
+        self.store, self.lib, self.boot, self.rank, self.world = store, lib, int(boot), rank, world
+        self.bus, self.topic, self.partition = bus, topic, partition
+        self.max_buffers = max_buffers
+        self.free: list[_BlockBuf] = []
+        self.pending: list[_BlockBuf] = []            # queued to the store, not yet durable
+        self.tags: list[tuple[int, object]] = []      # (store token, caller tag), in order
+        self.n_alloc = 0
+        self.blocks = self.bytes = self.rows = 0
+        self._size = 0
+        self._lock = threading.Lock()
+        if bus is not None and topic is not None:
+            bus.topic(topic, partition + 1)
+
+    def _release(self, b: _BlockBuf):
+        with self._lock:
+            b.refs -= 1
+            if b.refs == 0:
+                self.free.append(b)
+
+    def _reap(self):
+        d = self.store.durable()
+        keep = []
+        for b in self.pending:
+            if b.token <= d:
+                self._release(b)
+            else:
+                keep.append(b)
+        self.pending = keep
+        if self.bus is not None:
+            self.bus.reclaim()
+
+    def target(self, nbytes: int):
+        """(host address, buffer) for a block of ``nbytes`` (the copy engine writes it there)."""
+        need = -(-int(nbytes) // SEG_ALIGN) * SEG_ALIGN
+        self._reap()
+        with self._lock:
+            for i, b in enumerate(self.free):
+                if b.nbytes >= need:
+                    b = self.free.pop(i)
+                    b.refs = 1
+                    return b.host, b
+        if self.n_alloc >= self.max_buffers:
+            self.store.seg.wait(self.pending[0].token if self.pending else self.store.seg.last_token)
+            return self.target(nbytes)
+        # sized with headroom: steps of one engine produce blocks of about the same size
+        self._size = max(self._size, need + need // 2)
+        self.n_alloc += 1
+        b = _BlockBuf(self._HostBuffer(self.lib, self._size))
+        b.refs = 1
+        return b.host, b
+
+    def publish(self, b: _BlockBuf, nbytes: int, first_seq: int, now_ms: int, tag=None) -> int:
+        """The block is in ``b``: zero its padding, seal it, queue it to the store, publish it."""
+        nbytes = int(nbytes)
+        pad = -(-nbytes // SEG_ALIGN) * SEG_ALIGN
+        if pad > nbytes:
+            ctypes.memset(b.host + nbytes, 0, pad - nbytes)
+        native().swseg_seal(b.host, int(first_seq), int(now_ms), self.boot, self.rank, self.world)
+        n_rows = int(np.frombuffer((ctypes.c_uint8 * 64).from_address(b.host), np.uint8).view(HDR)[0]["n_rows"])
+        with self._lock:
+            b.refs += 1                                    # the store's reference
+        tok = self.store.add_block(b.host, nbytes, owner=b)
+        if tok < 0:                     # a replayed block the store already holds
+            self._release(b)
+            self.tags.append((self.store.seg.last_token, tag))   # durable with everything before it
+        else:
+            b.token = tok
+            self.pending.append(b)
+            self.tags.append((tok, tag))
+        if self.bus is not None and self.topic is not None:
+            with self._lock:
+                b.refs += 1                                # the topic's reference
+            self.bus.append_external(self.topic, self.partition, b, b.host, nbytes, ts=int(now_ms),
+                                     on_release=self._release)
+        self._release(b)                                   # the copy's reference
+        self.blocks += 1
+        self.bytes += nbytes
+        self.rows += n_rows
+        return tok
+
+    def committable(self) -> list:
+        """Tags of the blocks that are durable now (removed from the pending list)."""
+        d = self.store.durable()
+        out = []
+        while self.tags and self.tags[0][0] <= d:
+            out.append(self.tags.pop(0)[1])
+        return out
+
+    def flush(self, timeout_s: float = 120.0) -> bool:
+        ok = self.store.flush(timeout_s)
+        self._reap()
+        return ok
+
+
+_ETYPE = {DeviceEventType.Measurement: EV_MEASUREMENT, DeviceEventType.Location: EV_LOCATION,
+          DeviceEventType.Alert: EV_ALERT, DeviceEventType.StateChange: EV_STATE_CHANGE}
+_LEVELS = [AlertLevel.Info, AlertLevel.Warning, AlertLevel.Error, AlertLevel.Critical]
+_CTX = {DeviceEventIndex.Assignment: 0, DeviceEventIndex.Customer: 2, DeviceEventIndex.Area: 3,
+        DeviceEventIndex.Asset: 4}
+
+
+def boot_id(boot) -> int:
+    """Numeric engine incarnation of a tenant's boot string (hex ms timestamp) or number."""
+    return int(boot, 16) if isinstance(boot, str) else int(boot or 0)
+
+
+class DurableEventStore(DeviceEventStore):
+    """Event store of engine tenants on durable segments (see module docstring).
+
+    Ingest: :meth:`add_block` (an encoded, sealed block + the dictionary deltas its rows need).
+    Events are identified by (boot, rank, store sequence): a block whose rows the store already
+    holds for its (boot, rank) is skipped (a shard replaying after a restore).  Assignment and name
+    indices are engine-local, so the dictionaries are kept per boot; their deltas are fsync'd to
+    ``dict-<rank>.log`` before the block is queued, so a durable block never refers to an unknown
+    entry."""
+
+    def __init__(self, directory: str, rank: int = 0, rotate_bytes: int = 1 << 30, retention_bytes: int = 0,
+                 direct: bool = True, cache_blocks: int = 8):
+        self.dir = directory
+        os.makedirs(directory, exist_ok=True)
+        self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
+        self._objects = MemoryEventStore()
+        self._asg: dict[int, dict[int, list]] = {}       # boot -> assignment index -> [asg, dev, cust, area, asset]
+        self._names: dict[int, dict[int, str]] = {}      # boot -> name id -> name
+        self._rules: dict[str, str] = {}                 # alert type -> rule message
+        self._lock = threading.RLock()
+        self._dict_path = os.path.join(directory, f"dict-{rank}.log")
+        self._load_dict()
+        self._dict_f = open(self._dict_path, "ab")
+        self._high: dict[tuple, int] = {}
+        for e in self.seg.index():
+            key = (int(e["boot"]), int(e["rank"]))
+            self._high[key] = max(self._high.get(key, 0), int(e["first_seq"]) + int(e["n_rows"]))
+        self._cache: OrderedDict = OrderedDict()       # (file, offset) -> decoded columns
+        self.cache_blocks = cache_blocks
+        self.skipped_rows = 0
+
+    # ------------------------------------------------------------------ dictionaries
+    def _load_dict(self):
+        if not os.path.exists(self._dict_path):
+            return
+        with open(self._dict_path, "rb") as f:
+            for line in f:
+                try:
+                    d = json.loads(line)
+                except ValueError:
+                    break                                  # torn last line
+                self._apply_dict(d)
+
+    def _apply_dict(self, d: dict):
+        b = int(d.get("boot", 0))
+        self._asg.setdefault(b, {}).update({int(k): v for k, v in (d.get("asg") or {}).items()})
+        self._names.setdefault(b, {}).update({int(k): v for k, v in (d.get("names") or {}).items()})
+        self._rules.update(d.get("rules") or {})
+
+    def add_dictionary(self, boot, asg: dict | None = None, names: dict | None = None, rules: dict | None = None):
+        b = boot_id(boot)
+        d = {"boot": b}
+        if asg:
+            d["asg"] = {int(k): list(v) for k, v in asg.items()}
+        if names:
+            d["names"] = {int(k): v for k, v in names.items()}
+        if rules and any(self._rules.get(k) != v for k, v in rules.items()):
+            d["rules"] = dict(rules)
+        if len(d) == 1:
+            return
+        with self._lock:
+            self._apply_dict(d)
+            self._dict_f.write((json.dumps(d, separators=(",", ":")) + "\n").encode())
+            self._dict_f.flush()
+            os.fdatasync(self._dict_f.fileno())
+
+    # ------------------------------------------------------------------ ingest
+    def add_block(self, ptr: int, nbytes: int, owner=None, boot=None, asg=None, names=None, rules=None) -> int:
+        """Queue a sealed block for the disk; returns its token (-1 when skipped as a replay)."""
+        h = np.frombuffer((ctypes.c_uint8 * 64).from_address(ptr), np.uint8).view(HDR)[0]
+        b = int(h["boot"])
+        if boot is not None and boot_id(boot) != b:
+            raise ValueError("dictionary boot differs from the block's")
+        self.add_dictionary(b, asg, names, rules)
+        key, first, n = (b, int(h["rank"])), int(h["first_seq"]), int(h["n_rows"])
+        with self._lock:
+            if n and first + n <= self._high.get(key, 0):
+                self.skipped_rows += n
+                return -1
+            self._high[key] = max(self._high.get(key, 0), first + n)
+        return self.seg.append(ptr, nbytes, owner)
+
+    def add_encoded(self, block: np.ndarray, **dicts) -> int:
+        return self.add_block(_p(block), len(block), block, **dicts)
+
+    def durable(self) -> int:
+        return self.seg.durable()
+
+    def wait(self, token: int, timeout_s: float = 60.0) -> bool:
+        return self.seg.wait(token, timeout_s)
+
+    def flush(self, timeout_s: float = 60.0) -> bool:
+        return self.seg.flush(timeout_s)
+
+    def close(self):
+        self.seg.close()
+        try:
+            self._dict_f.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    # ------------------------------------------------------------------ reads
+    def _decoded(self, ent) -> dict:
+        key = (int(ent["file"]), int(ent["offset"]))
+        with self._lock:
+            c = self._cache.get(key)
+            if c is not None:
+                self._cache.move_to_end(key)
+                return c
+        c = decode_block(self.seg.read_block(ent))
+        with self._lock:
+            self._cache[key] = c
+            while len(self._cache) > self.cache_blocks:
+                self._cache.popitem(last=False)
+        return c
+
+    def rows(self) -> int:
+        return int(self.seg.index()["n_rows"].sum())
+
+    def count(self) -> int:
+        return self.rows() + self._objects.count()
+
+    def add_events(self, events):
+        return self._objects.add_events(events)
+
+    def get_event_by_alternate_id(self, alt: str):
+        return self._objects.get_event_by_alternate_id(alt)
+
+    @staticmethod
+    def _eids(h: dict, idx) -> np.ndarray:
+        return (h["first_seq"] + np.asarray(idx, np.int64)) * h["world"] + h["rank"]
+
+    def find_alternate_hashes(self, hashes) -> dict:
+        """alt-id hash -> event id string for the hashes present on disk (dedup beyond the engine's
+        window: ``AlternateIdDeduplicator`` asks the event store whether the id was ever seen)."""
+        want = np.unique(np.asarray(list(hashes), np.uint64))
+        found = {}
+        if not len(want):
+            return found
+        for e in self.seg.index():
+            c = self._decoded(e)
+            m = np.isin(c["alt"], want)
+            if m.any():
+                h = c["header"]
+                for i in np.nonzero(m)[0]:
+                    found.setdefault(int(c["alt"][i]), f"{h['boot']:x}-{int(self._eids(h, [i])[0])}")
+        return found
+
+    def get_event_by_id(self, id: str):
+        boot, sep, num = id.rpartition("-")
+        try:
+            b = int(boot, 16)
+        except ValueError:
+            b = None
+        if not (sep and num.isdigit()) or b is None:
+            return self._objects.get_event_by_id(id)
+        eid = int(num)
+        for e in self.seg.index():
+            if int(e["boot"]) != b:
+                continue
+            w, r = int(e["world"]), int(e["rank"])
+            if (eid - r) % w:
+                continue
+            row = (eid - r) // w - int(e["first_seq"])
+            if 0 <= row < int(e["n_rows"]):
+                return self._materialize(self._decoded(e), int(row))
+        return self._objects.get_event_by_id(id)
+
+    def list_command_responses_for_invocation(self, invocation_id, criteria=None):
+        return self._objects.list_command_responses_for_invocation(invocation_id, criteria)
+
+    def list_events(self, event_type, index, entity_ids, criteria: DateRangeSearchCriteria | None = None):
+        c = criteria or DateRangeSearchCriteria(page_size=100)
+        et = _ETYPE.get(DeviceEventType(event_type))
+        objs = self._objects.list_events(event_type, index, entity_ids, DateRangeSearchCriteria(
+            page_size=0, start_date=c.start_date, end_date=c.end_date)).results
+        if et is None:
+            return SearchResults(len(objs), c.slice(objs))
+        pos = _CTX[DeviceEventIndex(index)]
+        want = set(entity_ids)
+        with self._lock:
+            asg_idx = {b: np.array([i for i, ctx in d.items() if ctx[pos] in want], np.int32)
+                       for b, d in self._asg.items()}
+        hits = []
+        for e in self.seg.index():
+            a = asg_idx.get(int(e["boot"]))
+            if a is None or not len(a):
+                continue
+            if c.start_date is not None and int(e["max_date"]) < c.start_date:
+                continue
+            if c.end_date is not None and int(e["min_date"]) > c.end_date:
+                continue
+            cols = self._decoded(e)
+            m = (cols["etype"] == et) & np.isin(cols["asg"], a)
+            if c.start_date is not None:
+                m &= cols["date"] >= c.start_date
+            if c.end_date is not None:
+                m &= cols["date"] <= c.end_date
+            idx = np.nonzero(m)[0]
+            if len(idx):
+                hits.append((cols["date"][idx], self._eids(cols["header"], idx), cols, idx))
+        total = sum(len(x[0]) for x in hits) + len(objs)
+        if not hits:
+            return SearchResults(total, c.slice(objs))
+        dates = np.concatenate([x[0] for x in hits])
+        eids = np.concatenate([x[1] for x in hits])
+        which = np.concatenate([np.full(len(x[0]), k, np.int32) for k, x in enumerate(hits)])
+        rows = np.concatenate([x[3] for x in hits])
+        order = np.lexsort((-eids, -dates))
+        if objs:
+            merged = [self._materialize(hits[which[o]][2], int(rows[o])) for o in order] + objs
+            merged.sort(key=lambda ev: -(ev.event_date or 0))
+            return SearchResults(total, c.slice(merged))
+        if c.page_size > 0:
+            start = (max(1, c.page_number) - 1) * c.page_size
+            order = order[start:start + c.page_size]
+        return SearchResults(total, [self._materialize(hits[which[o]][2], int(rows[o])) for o in order])
+
+    def _materialize(self, cols: dict, i: int):
+        h = cols["header"]
+        b = h["boot"]
+        ctx = self._asg.get(b, {}).get(int(cols["asg"][i]), [None] * 5)
+        eid = int(self._eids(h, [i])[0])
+        base = dict(id=f"{b:x}-{eid}", device_assignment_id=ctx[0], device_id=ctx[1], customer_id=ctx[2],
+                    area_id=ctx[3], asset_id=ctx[4], event_date=int(cols["date"][i]), received_date=h["recv_ms"])
+        et = int(cols["etype"][i])
+        nid = int(cols["name"][i])
+        name = self._names.get(b, {}).get(nid, "") if nid != NO_NAME else ""
+        if et == EV_MEASUREMENT:
+            return DeviceMeasurement(name=name, value=float(cols["v0"][i]), **base)
+        if et == EV_LOCATION:
+            return DeviceLocation(latitude=float(cols["v0"][i]), longitude=float(cols["v1"][i]),
+                                  elevation=float(cols["v2"][i]), **base)
+        if et == EV_ALERT:
+            rule = self._rules.get(name)
+            return DeviceAlert(source=AlertSource.System if rule is not None else AlertSource.Device,
+                               level=_LEVELS[min(int(cols["level"][i]), 3)], type=name, message=rule or "", **base)
+        return DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
+                                 new_state="NOT_PRESENT", **base)

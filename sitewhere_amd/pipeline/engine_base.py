@@ -292,6 +292,23 @@ class EngineBase:
             return rows
         return (cursor - cap) + (rows - (cursor % cap)) % cap
 
+    # ------------------------------------------------------------------ durable blocks
+    def block_columns(self, res: StepResult):
+        """(rows, elevation, alt-id hash) of a step's persisted events, from the host event ring."""
+        n = 0 if res.out is None else len(res.out)
+        idx = (res.first_seq + np.arange(n, dtype=np.int64)) % self.cfg.store_cap
+        return res.out, self.store["v2"][idx], self.store["alt"][idx]
+
+    def encode_block(self, now_ms: int, res: StepResult | None = None, slot: int | None = None,
+                     boot: int = 0) -> np.ndarray:
+        """Durable block (``persistence/segments.py``) of a step: encoded and sealed on the host.
+        The MI355X engine overrides this with its GPU encoder (same bytes)."""
+        from ..persistence.segments import encode_block, seal
+        rows, v2, alt = self.block_columns(res)
+        blk = encode_block(rows, v2, alt)
+        seal(blk, res.first_seq, now_ms, boot, self.rank, self.world)
+        return blk
+
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "base"
 

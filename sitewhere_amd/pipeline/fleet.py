@@ -84,6 +84,9 @@ class FleetSpec:
     lat0: float = 33.75
     lon0: float = -84.39
     span_deg: float = 0.5
+    p_register: float = 0.0          # registration requests from new devices (control plane)
+    p_ack: float = 0.0               # command acknowledgements (control plane)
+    device_type: str = "default-type"
 
 
 def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndarray | None = None,
@@ -102,7 +105,42 @@ def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndar
                             _ptr(out), out.nbytes, _ptr(offs))
     if r < 0:
         raise RuntimeError(f"payload buffer too small (need {-r})")
-    return out[:r], offs[:n_msgs + 1]
+    raw, offs = out[:r], offs[:n_msgs + 1]
+    if spec.p_register > 0 or spec.p_ack > 0:
+        raw, offs = _splice_control(spec, raw, offs, seed)
+    return raw, offs
+
+
+def _splice_control(spec: FleetSpec, raw: np.ndarray, offs: np.ndarray, seed: int):
+    """Replace a fraction of the payloads with registrations (new devices, reference
+    ``SendRegistration``) and acknowledgements (registered devices) -- messages the engine hands to
+    the control plane."""
+    from ..models import wire
+    n = len(offs) - 1
+    rng = np.random.default_rng(seed + 0x5eed)
+    u = rng.random(n)
+    reg = np.nonzero(u < spec.p_register)[0]
+    ack = np.nonzero((u >= spec.p_register) & (u < spec.p_register + spec.p_ack))[0]
+    repl = {}
+    for i in reg:
+        repl[int(i)] = wire.registration(f"{spec.prefix}new-{seed}-{int(i)}", spec.device_type)
+    for i in ack:
+        d = int(rng.integers(0, spec.n_devices))
+        repl[int(i)] = wire.acknowledge(f"{spec.prefix}{d:010d}", "ok", originator=f"cmd-{seed}-{int(i)}")
+    if not repl:
+        return raw, offs
+    idx = np.array(sorted(repl), np.int64)
+    lens = np.diff(offs.astype(np.int64))
+    lens[idx] = [len(repl[int(i)]) for i in idx]
+    new_offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=new_offs[1:])
+    parts, prev = [], 0
+    for i in idx:
+        parts.append(raw[offs[prev]:offs[i]])
+        parts.append(np.frombuffer(repl[int(i)], np.uint8))
+        prev = int(i) + 1
+    parts.append(raw[offs[prev]:offs[n]])
+    return np.concatenate(parts), new_offs.astype(np.uint32)
 
 
 def cpu_decode(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, cap: int | None = None,

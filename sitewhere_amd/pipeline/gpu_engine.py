@@ -343,6 +343,7 @@ class GpuInboundEngine(EngineBase):
         """Stream-ordered SwStepParams of the next process phase (receive time, batch, presence, rows)."""
         a = self.args
         a.batch_seq = self.batch_seq
+        self._step_now = int(now_ms)           # receive time of the batch this process phase runs
         a.presence_missing_ms = self.cfg.presence_missing_ms if presence else 0
         sel = self._out_sel if out_sel is None else out_sel
         self._last_sel = sel
@@ -790,6 +791,52 @@ class GpuInboundEngine(EngineBase):
         s.rows = None
         return s.token, res
 
+    # ------------------------------------------------------------------ durable blocks
+    def _seg_buffers(self, slot: int):
+        """(HBM block buffer, encoder state, max pages, capacity) of outbound slot ``slot``: each slot
+        keeps its block until the copy engine has moved it to the host."""
+        segs = self.__dict__.setdefault("_segs", {})
+        s = segs.get(slot)
+        if s is None:
+            from ..persistence.segments import PAGE_ROWS, max_block_bytes
+            cap = max_block_bytes(self.out_cap)
+            pages = -(-self.out_cap // PAGE_ROWS)
+            s = segs[slot] = (torch.empty(cap, dtype=torch.uint8, device=self.device),
+                              torch.zeros(pages + 4, dtype=torch.int64, device=self.device), pages, cap)
+        return s
+
+    def encode_block_async(self, slot: int) -> torch.Tensor:
+        """Enqueue ``k_seg_encode`` of the step just processed (its rows in ``out_dev[slot]``, its
+        elevation and alternate-id columns in the ring) on the current stream.  Returns the device
+        view (block bytes, encoder errors, first store sequence) the host reads once the step is done."""
+        dev, state, pages, cap = self._seg_buffers(slot)
+        st = self.store
+        rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(_ptr(st["v2"])),
+                                    ctypes.c_void_p(_ptr(st["alt"])), self.cfg.store_cap,
+                                    ctypes.c_void_p(_ptr(self.t["cursor"])), ctypes.c_void_p(_ptr(dev)), cap,
+                                    ctypes.c_void_p(_ptr(state)), pages, self._stream())
+        if rc:
+            raise RuntimeError(f"sw_seg_encode failed ({rc})")
+        return state[pages + 1:pages + 4]
+
+    def block_device(self, slot: int) -> torch.Tensor:
+        return self._seg_buffers(slot)[0]
+
+    def encode_block(self, now_ms: int, res=None, slot: int | None = None, boot: int = 0) -> np.ndarray:
+        """Synchronous durable block of the last step (after :meth:`step`): encoded on the MI355X,
+        copied back, sealed.  The bytes equal ``persistence.segments.encode_block`` of the step's rows."""
+        from ..persistence.segments import seal
+        slot = self._last_sel if slot is None else slot
+        with self._lock:
+            meta = self.encode_block_async(slot)
+            self._sync_streams()
+            nb, err, first = (int(x) for x in meta.cpu().numpy())
+            if err or nb <= 0 or nb > self._seg_buffers(slot)[3]:
+                raise RuntimeError(f"block encoder failed (bytes={nb}, errors={err})")
+            blk = self.block_device(slot)[:nb].cpu().numpy().copy()
+        seal(blk, first, now_ms, boot, self.rank, self.world)
+        return blk
+
     # ------------------------------------------------------------------ queries
     def stats_dict(self) -> dict:  # type: ignore[override]
         return EngineBase.stats_dict(self.t["stats"].cpu().numpy().view(np.uint64))
@@ -957,11 +1004,17 @@ class PipelinedRunner:
 
     def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
                  on_outbound=None, mode: str | None = None, push_blocks: int = 128, nbuf: int = 3,
-                 out_target=None):
+                 out_target=None, block_sink=None):
         """``out_target(n_bytes) -> (host address, token)`` (copy-engine modes): where each step's rows
         land, e.g. a pinned buffer a bus topic then publishes in place; ``on_outbound(token, n_rows)``
         is called once they are there.  Without it rows land in the engine's outbound ring and
-        ``on_outbound(rows)`` gets a view of them."""
+        ``on_outbound(rows)`` gets a view of them.
+
+        ``block_sink`` (``persistence.segments.DurableBlockSink``): every step's persisted events are
+        also encoded on the GPU into a durable block (``k_seg_encode``, right after the step on the
+        compute stream); the copy engine moves the compressed block to the sink's pinned buffer and
+        the sink seals it, queues it to the durable store and publishes it.  ``submit(tag=...)``
+        labels a batch; ``block_sink.committable()`` returns the labels whose blocks are durable."""
         import os
         self.e = engine
         self.out_target = out_target
@@ -991,10 +1044,19 @@ class PipelinedRunner:
         self.copying = None          # sdma mode: (buffer, n_out) whose D2H copy is in flight
         self.rounds = engine.world > 1 and os.environ.get("SW_PIPELINE_EXCHANGE", "1") != "0"
         self.produced = [False] * nb  # rounds mode: did the round in slot b process a batch
+        self.block_sink = block_sink
+        if block_sink is not None:
+            if self.mode != "hsa":
+                raise ValueError("durable blocks need the copy-engine outbound mode (hsa)")
+            self.seg_host = torch.zeros(nb, 4, dtype=torch.int64, pin_memory=True)
+            self.btag = [None] * nb       # caller tag of the batch whose block slot b holds
+            self.bnow = [0] * nb
+            self._prev_tag = None
+        self.bcopying = None              # (slot, signal, buffer, bytes, first_seq, now, tag)
 
     def submit(self, raw_host: torch.Tensor | None, off_host: torch.Tensor | None, n_msgs: int,
                now_ms: int | None = None, presence: bool = False, lens_host: torch.Tensor | None = None,
-               raw_bytes: int | None = None):
+               raw_bytes: int | None = None, tag=None):
         """Enqueue one batch (``raw_host=None``: a drain round of the pipelined exchange, no new batch).
 
         The batch is framed either by u32 offsets (``off_host``) or by a varint length stream
@@ -1014,7 +1076,8 @@ class PipelinedRunner:
                 else:
                     self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
                 self.ev_h2d[b].record(self.h2d)
-        if self.mode == "hsa" and self.copying is not None and self.copying[0] == b:
+        if self.mode == "hsa" and ((self.copying is not None and self.copying[0] == b) or
+                                   (self.bcopying is not None and self.bcopying[0] == b)):
             self._finish_copy()                           # SDMA copy k-2 still reads staging ring b
         if raw_host is not None:
             self.comp.wait_event(self.ev_h2d[b])
@@ -1037,6 +1100,13 @@ class PipelinedRunner:
         else:
             self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
         self.scal_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
+        if self.block_sink is not None:
+            # in rounds mode the round processes the batch submitted by the previous call
+            done_tag = self._prev_tag if self.rounds else tag
+            self._prev_tag = tag
+            if self.produced[b]:
+                self.seg_host[b][:3].copy_(self.e.encode_block_async(b), non_blocking=True)
+                self.btag[b], self.bnow[b] = done_tag, self.e._step_now
         self.ev_comp[b].record(self.comp)
         if self.mode == "push" and self.deliver:
             with torch.cuda.stream(self.push):
@@ -1067,6 +1137,19 @@ class PipelinedRunner:
         return self.out_target(n_out * OUT_REC.itemsize)
 
     def _finish_copy(self):
+        self._finish_block()
+        self._finish_rows()
+
+    def _finish_block(self):
+        if self.bcopying is not None:
+            _, sig, buf, nb, first, now, tag = self.bcopying
+            self.bcopying = None
+            rc = self.e.lib.sw_sdma_wait(sig)
+            if rc:
+                raise RuntimeError(f"sw_sdma_wait failed ({rc})")
+            self.block_sink.publish(buf, nb, first, now, tag)
+
+    def _finish_rows(self):
         if self.copying is not None:
             cb, cn, sig, tok = self.copying
             if sig is not None:
@@ -1091,6 +1174,17 @@ class PipelinedRunner:
             self._deliver(pb, n_out)
             return
         self._finish_copy()
+        if self.block_sink is not None and self.produced[pb]:
+            nb, err, first = (int(x) for x in self.seg_host[pb][:3])
+            if err or nb <= 0 or nb > self.e._seg_buffers(pb)[3]:
+                raise RuntimeError(f"durable block encoder failed (bytes={nb}, errors={err})")
+            dst, buf = self.block_sink.target(nb)
+            h = ctypes.c_uint64()
+            rc = self.e.lib.sw_sdma_copy(ctypes.c_void_p(dst), ctypes.c_void_p(_ptr(self.e.block_device(pb))), nb,
+                                         self.sdma_engine, ctypes.byref(h))
+            if rc:
+                raise RuntimeError(f"sw_sdma_copy of the durable block failed ({rc})")
+            self.bcopying = (pb, h.value, buf, nb, first, self.bnow[pb], self.btag[pb])
         dst, tok = self._dest(pb, n_out) if self.deliver and n_out else (None, None)
         if self.mode == "hsa":
             sig = None
@@ -1109,7 +1203,7 @@ class PipelinedRunner:
             if self.mode == "hsa":
                 self.copying = (pb, n_out, sig, tok)
                 if sig is None:
-                    self._finish_copy()
+                    self._finish_rows()
                 return
         if self.deliver and n_out:
             rc = self.e.lib.sw_copy_d2h(ctypes.c_void_p(dst),

@@ -1,0 +1,85 @@
+"""Routing of the messages an engine step rejected, per payload and in native code.
+
+``csrc/native/swroute.cpp`` finds the payload of every reject record (its offset points into it),
+parses only those payloads and writes the reference's Kafka payloads: ``GInboundEventPayload`` per
+event of an unregistered / unassigned device (``InboundPayloadProcessingLogic.java:199-218``),
+``GDeviceRegistationPayload`` for registrations (``EventSourcesManager.java:153-182``), the payload
+itself for acknowledgements / streams (decoded on the host: the reference message has no member for
+them) and for undecodable payloads (failed-decode topic, ``EventSourcesManager.java:189-197``).
+Records come back grouped by (kind, Kafka partition of the device token), keys and values in two
+heaps, so each group is one native append to its topic.  Duplicates are dropped (dedup)."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .._native import native
+
+UNREGISTERED, REGISTRATION, CONTROL, FAILED = 0, 1, 2, 3
+
+
+@dataclass
+class RoutedRejects:
+    rec: np.ndarray          # int32 [n, 4]: kind, partition, key length, value length
+    keys: np.ndarray         # uint8 heap
+    vals: np.ndarray         # uint8 heap
+    payloads: int            # payloads looked at
+
+    def __len__(self):
+        return len(self.rec)
+
+    def groups(self):
+        """(kind, partition, key heap, key offsets [m+1], value heap, value offsets [m+1]) per group."""
+        n = len(self.rec)
+        if not n:
+            return
+        koff = np.zeros(n + 1, np.int64)
+        voff = np.zeros(n + 1, np.int64)
+        np.cumsum(self.rec[:, 2], out=koff[1:])
+        np.cumsum(self.rec[:, 3], out=voff[1:])
+        kp = self.rec[:, 0].astype(np.int64) << 32 | (self.rec[:, 1].astype(np.int64) & 0xFFFFFFFF)
+        cut = np.nonzero(np.diff(kp))[0] + 1
+        starts = np.concatenate([[0], cut])
+        ends = np.concatenate([cut, [n]])
+        for a, b in zip(starts, ends):
+            ko, vo = koff[a:b + 1], voff[a:b + 1]
+            yield (int(self.rec[a, 0]), int(self.rec[a, 1]), self.keys[ko[0]:ko[-1]], ko - ko[0],
+                   self.vals[vo[0]:vo[-1]], vo - vo[0])
+
+    def values(self, kind: int):
+        """(key bytes, value bytes) of every record of one kind (small kinds: control, failed)."""
+        n = len(self.rec)
+        koff = np.concatenate([[0], np.cumsum(self.rec[:, 2], dtype=np.int64)])
+        voff = np.concatenate([[0], np.cumsum(self.rec[:, 3], dtype=np.int64)])
+        for i in np.nonzero(self.rec[:, 0] == kind)[0] if n else []:
+            yield bytes(self.keys[koff[i]:koff[i + 1]]), bytes(self.vals[voff[i]:voff[i + 1]])
+
+
+def route_rejects(raw: np.ndarray, offs: np.ndarray, rej_off: np.ndarray, rej_status: np.ndarray,
+                  source_id: str = "gpu-inbound", partitions=(1, 1, 1, 1)) -> RoutedRejects:
+    """``raw`` / ``offs``: the raw batch; ``rej_off`` / ``rej_status``: the step's reject records
+    (``EVENT_REC["aux_off"]``, engine status).  ``partitions``: partition counts of the
+    unregistered, registration, decoded and failed-decode topics."""
+    lib = native()
+    raw = np.ascontiguousarray(raw, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint32)
+    ro = np.ascontiguousarray(rej_off, np.uint32)
+    rs = np.ascontiguousarray(rej_status, np.uint8)
+    parts = np.asarray(partitions, np.int32)
+    need = np.zeros(3, np.int64)
+    npay = np.zeros(1, np.int64)
+    n_rej = len(ro)
+    cap = (max(16, 4 * n_rej), max(1024, 64 * n_rej), max(4096, 256 * n_rej))
+    for _ in range(2):
+        rec = np.zeros((cap[0], 4), np.int32)
+        keys = np.empty(cap[1], np.uint8)
+        vals = np.empty(cap[2], np.uint8)
+        n = lib.sw_route_rejects(raw.ctypes.data, offs.ctypes.data, len(offs) - 1, ro.ctypes.data if n_rej else None,
+                                 rs.ctypes.data if n_rej else None, n_rej, source_id.encode(), parts.ctypes.data,
+                                 rec.ctypes.data, cap[0], keys.ctypes.data, cap[1], vals.ctypes.data, cap[2],
+                                 need.ctypes.data, npay.ctypes.data)
+        if n >= 0:
+            return RoutedRejects(rec[:n], keys[:need[1]], vals[:need[2]], int(npay[0]))
+        cap = tuple(int(x) for x in need)
+    raise RuntimeError("sw_route_rejects: output sizing failed")

@@ -55,10 +55,10 @@ def unpack_raw_batch(value: bytes):
 
 
 class _Stepped:
-    """A raw batch the engine has stepped, with the storage stages it has completed.  ``batch`` (the
-    raw bytes, for the host slow path) is kept only when the step rejected messages."""
+    """A raw batch the engine has stepped, with the storage stages it has completed.  The raw bytes
+    are not kept: rejected messages are routed (``_route``) as soon as the step completes."""
     __slots__ = ("key", "res", "now", "batch", "stored", "published", "routed", "queued", "payload", "events",
-                 "detach", "hold", "commit", "trace")
+                 "detach", "hold", "commit", "trace", "routed_recs")
 
     def __init__(self, key, res, now, batch):
         self.key, self.res, self.now, self.batch = key, res, now, batch
@@ -66,6 +66,7 @@ class _Stepped:
         self.payload = self.events = None
         self.detach, self.hold, self.commit = False, None, None
         self.trace = None
+        self.routed_recs = None                 # the rejects, routed while the raw record was readable
 
 
 class GpuInboundTenantEngine(InboundProcessingTenantEngine):
@@ -81,6 +82,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.t_unregistered = n.unregistered_device_events(t)
         self.t_registration = n.device_registration_events(t)
         self.t_decoded = n.decoded_events(t)
+        self.t_failed_decode = n.failed_decode_events(t)
+        self.routed_payloads = 0                # payloads the slow path parsed (per payload, not per batch)
         self.t_enriched_batches = n.tenant_prefix(t) + ENRICHED_BATCHES
         self.storage = cfg.get("storage", "objects")            # objects | columnar
         self.publish = cfg.get("publishEnriched", "events")     # events | batches | none
@@ -402,10 +405,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             if item.trace is not None:
                 item.trace.append(time.perf_counter())
             self.processed_events.mark(res.n_events)
-            keep = None
-            if res.rejects is not None and len(res.rejects):
-                keep = item.batch.copy() if item.detach else item.batch
-            item.res, item.batch = res, keep
+            item.res, item.routed_recs, item.batch = res, self._route(item.batch, res), None
             if item.hold is not None:
                 self._hold(item.hold, -1)
                 item.hold = None
@@ -478,10 +478,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         with self._lock, self.step_timer.time():
             res = self.engine.step_framed(batch, now)
         self.processed_events.mark(res.n_events)
-        keep = None
-        if res.rejects is not None and len(res.rejects):
-            keep = batch.copy() if detach else batch
-        item = _Stepped(key, res, now, keep)
+        item = _Stepped(key, res, now, None)
+        item.routed_recs = self._route(batch, res)
         if key is not None:
             self._stepped[key] = item
         self._submit(item, commit)
@@ -550,8 +548,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     self._publish_events(item.events if item.events is not None else self._to_events(res, now))
             item.published = True
         if not item.routed:
-            if res.rejects is not None and len(res.rejects):
-                self._slow_path(np.asarray(item.batch.payload), item.batch.offsets(), res)
+            self._send_routed(item.routed_recs)
             item.routed = True
         if item.key is not None:
             t, p, o = item.key
@@ -676,32 +673,51 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         return {"deviceId": e.device_id, "deviceToken": self._dev_tokens.get(di),
                 "assignmentStatus": "Active", "engine": self.engine_kind}
 
-    def _slow_path(self, raw, offs, res):
+    def _route(self, batch, res):
+        """Route the step's rejected messages like the reference does, per payload: only the payloads
+        the reject records point into are parsed (natively, ``pipeline/routing.py``).  Runs while the
+        raw record is still readable; the result (the routed records, small) is what the storage
+        stage keeps -- never a copy of the batch."""
+        from ..pipeline import routing
         st = res.reject_status
-        need = (st == ST_UNREGISTERED) | (st == ST_UNASSIGNED) | (st == ST_CONTROL)
-        if not need.any():
+        if st is None or not len(st):
+            return None
+        bus = self.ms.instance.bus
+        topics = (self.t_unregistered, self.t_registration, self.t_decoded, self.t_failed_decode)
+        parts = [bus.partitions(t) if hasattr(bus, "partitions") else 1 for t in topics]
+        rr = routing.route_rejects(np.asarray(batch.payload), batch.offsets(), res.rejects["aux_off"], st,
+                                   "gpu-inbound", parts)
+        self.routed_payloads += rr.payloads
+        return rr
+
+    def _send_routed(self, rr):
+        """Publish routed rejects: one native append per (topic, partition) group; acknowledgements /
+        streams (rare) are decoded here."""
+        from ..pipeline import routing
+        if rr is None or not len(rr):
             return
-        fps = {(int(r["fp_lo"]), int(r["fp_hi"])) for r in res.rejects[need]}
-        dec = ProtobufDecoder()
-        for i in range(len(offs) - 1):
-            payload = bytes(raw[offs[i]:offs[i + 1]])
+        bus = self.ms.instance.bus
+        topics = (self.t_unregistered, self.t_registration, self.t_decoded, self.t_failed_decode)
+        prod = self.ms.producer
+        for kind, part, kh, ko, vh, vo in rr.groups():
+            if kind == routing.CONTROL:
+                continue
+            if part < 0:                    # no device token (undecodable payload): round-robin
+                part = bus.partition_for(topics[kind], None) if hasattr(bus, "partition_for") else 0
+            prod.send_arrays(topics[kind], part, kh, ko, vh, vo)
+            if kind == routing.UNREGISTERED:
+                self.unregistered.mark(len(ko) - 1)
+        dec = None
+        for _, payload in rr.values(routing.CONTROL):
+            dec = dec or ProtobufDecoder()
             try:
                 reqs = dec.decode(payload, {})
-            except Exception:
+            except Exception:               # noqa: BLE001 -- the router already parsed it
                 continue
             for q in reqs:
-                if fingerprint_str(q["deviceToken"]) not in fps:
-                    continue
                 body = {"sourceId": "gpu-inbound", "deviceToken": q["deviceToken"], "originator": q.get("originator"),
                         "eventCreateRequest": {"type": q["type"], "request": q["request"]}}
-                wire_body = payloads.encode_inbound(body)
-                if q["type"] == "RegisterDevice":
-                    self.ms.producer.send(self.t_registration, q["deviceToken"], wire_body)
-                elif q["type"] in ("Acknowledge", "DeviceStream", "DeviceStreamData", "SendDeviceStreamData"):
-                    self.ms.producer.send(self.t_decoded, q["deviceToken"], wire_body)
-                else:
-                    self.unregistered.mark()
-                    self.ms.producer.send(self.t_unregistered, q["deviceToken"], wire_body)
+                prod.send(self.t_decoded, q["deviceToken"], payloads.encode_inbound(body))
 
 
 class GpuInboundApi:

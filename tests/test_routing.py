@@ -1,0 +1,105 @@
+"""Native per-payload routing of rejected messages (csrc/native/swroute.cpp, pipeline/routing.py)
+against the Python path it replaces: the device payload decoded by ``ProtobufDecoder`` and encoded
+by ``bus.payloads.encode_inbound`` must carry the same request as the natively routed record."""
+from __future__ import annotations
+
+import numpy as np
+
+from sitewhere_amd.bus import payloads
+from sitewhere_amd.bus.log import kafka_partition
+from sitewhere_amd.models import wire
+from sitewhere_amd.pipeline import routing
+from sitewhere_amd.pipeline.fleet import cpu_decode, pack_messages
+from sitewhere_amd.services.event_sources import ProtobufDecoder
+
+ST_UNREG, ST_UNASSIGNED, ST_DUP, ST_DECODE, ST_CONTROL = 1, 2, 3, 4, 5
+
+
+def _python_route(payload: bytes):
+    out = []
+    for q in ProtobufDecoder().decode(payload, {}):
+        body = {"sourceId": "gpu-inbound", "deviceToken": q["deviceToken"], "originator": q.get("originator"),
+                "eventCreateRequest": {"type": q["type"], "request": q["request"]}}
+        out.append(body)
+    return out
+
+
+def _norm(d: dict) -> dict:
+    ecr = d.get("eventCreateRequest") or {}
+    req = {k: v for k, v in (ecr.get("request") or {}).items() if v not in (None, {}, "")}
+    import json
+    return json.dumps({"deviceToken": d.get("deviceToken"), "originator": d.get("originator") or None,
+                       "type": ecr.get("type"), "request": req}, sort_keys=True, default=str)
+
+
+def test_route_matches_python_path(monkeypatch):
+    monkeypatch.setattr(payloads, "_MODE", "protobuf")
+    msgs = [
+        wire.measurements("dev-a", {"t": 21.5, "h": 40.25}, event_date=1_700_000_000_001, alternate_id="m-1",
+                          metadata={"k": "v"}, update_state=True, originator="orig-1"),
+        wire.location("dev-b", 33.123456, -84.5, elevation=12.5, event_date=1_700_000_000_002, alternate_id="l-1"),
+        wire.alert("dev-c", "engine.hot", "too hot", event_date=1_700_000_000_003),
+        wire.measurements("dev-ok", {"x": 1.0}),                     # persisted: not routed
+        wire.registration("dev-new", "type-1", area_token="area-9", metadata={"a": "b"}),
+        wire.acknowledge("dev-d", "done", originator="cmd-7"),
+        b"\x05garbage!!",                                            # undecodable
+        wire.location("dev-e", 0.0, 1.0),                            # zero latitude: proto3 default
+    ]
+    raw, offs = pack_messages(msgs)
+    recs = cpu_decode(raw, offs, 1_700_000_100_000)
+    st = np.full(len(recs), ST_UNREG, np.uint8)
+    tok = {0: ST_UNREG, 1: ST_UNASSIGNED, 2: ST_UNREG, 3: 0, 4: ST_CONTROL, 5: ST_CONTROL, 6: ST_DECODE, 7: ST_UNREG}
+    payload_of = np.searchsorted(offs, recs["aux_off"], side="right") - 1
+    for i, m in enumerate(payload_of):
+        st[i] = tok[int(m)]
+    keep = st != 0
+    parts = (8, 4, 8, 2)
+    rr = routing.route_rejects(raw, offs, recs["aux_off"][keep], st[keep], "gpu-inbound", parts)
+    assert rr.payloads == 7
+    got = {k: [] for k in range(4)}
+    for kind, part, kh, ko, vh, vo in rr.groups():
+        for i in range(len(ko) - 1):
+            key, val = bytes(kh[ko[i]:ko[i + 1]]), bytes(vh[vo[i]:vo[i + 1]])
+            if key:
+                assert part == kafka_partition(key, parts[kind])
+            got[kind].append((key, val))
+    # unregistered data: one GInboundEventPayload per event, same request as the Python path
+    want = [payloads.decode_inbound(payloads.encode_inbound(b))
+            for m in (msgs[0], msgs[1], msgs[2], msgs[7]) for b in _python_route(m)]
+    have = [payloads.decode_inbound(v) for _, v in got[routing.UNREGISTERED]]
+    assert sorted(map(_norm, have)) == sorted(map(_norm, want))
+    assert {k for k, _ in got[routing.UNREGISTERED]} == {b"dev-a", b"dev-b", b"dev-c", b"dev-e"}
+    # registration: GDeviceRegistationPayload
+    (k, v), = got[routing.REGISTRATION]
+    reg = payloads.decode_inbound(v, registration=True)
+    want_reg = payloads.decode_inbound(payloads.encode_inbound(_python_route(msgs[4])[0]), registration=True)
+    assert k == b"dev-new" and _norm(reg) == _norm(want_reg)
+    # acknowledgement: the payload itself, decoded on the host
+    assert [v for _, v in got[routing.CONTROL]] == [msgs[5]]
+    # undecodable: the raw payload for the failed-decode topic
+    assert [v for _, v in got[routing.FAILED]] == [msgs[6]]
+
+
+def test_route_skips_duplicates_and_handles_empty():
+    msgs = [wire.measurements("dev-a", {"t": 1.0}, alternate_id="x")]
+    raw, offs = pack_messages(msgs)
+    recs = cpu_decode(raw, offs, 1)
+    rr = routing.route_rejects(raw, offs, recs["aux_off"], np.full(len(recs), ST_DUP, np.uint8))
+    assert len(rr) == 0 and rr.payloads == 0
+    rr = routing.route_rejects(raw, offs, np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+    assert len(rr) == 0 and list(rr.groups()) == []
+
+
+def test_route_throughput():
+    """5K unregistered payloads out of a 1M-payload batch: milliseconds, not seconds."""
+    import time
+    from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
+    spec = FleetSpec(n_devices=100_000, with_alternate_id=True, p_unregistered=0.005)
+    raw, offs = gen_payloads(spec, 1 << 20, 1_700_000_000_000, seed=3)
+    raw = np.concatenate([raw, np.zeros(64, np.uint8)])
+    pick = np.random.default_rng(0).choice(len(offs) - 1, 5000, replace=False)
+    t = time.perf_counter()
+    rr = routing.route_rejects(raw, offs, offs[pick], np.full(len(pick), ST_UNREG, np.uint8), "s", (8, 8, 8, 8))
+    dt = time.perf_counter() - t
+    assert rr.payloads == 5000 and len(rr) >= 5000
+    assert dt < 0.05, dt
