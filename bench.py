@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Headline benchmark: device events/sec through the SiteWhere inbound pipeline on MI355X.
+"""Headline benchmark: device events/sec through the SiteWhere inbound pipeline to durable storage.
 
 Reference headline (BASELINE.json): "device events/sec through the Kafka pipeline" --
 decode -> inbound validation -> event persistence -> enrichment -> consumers
@@ -8,12 +8,18 @@ number, so ``vs_baseline`` is null.
 
 One step = one micro-batch of ``--msgs`` protobuf device payloads per GPU, run end to end:
   raw batch produced to the raw-payload topic of the native commit log (zero-copy, pinned record)
-  -> consumed in place -> H2D of the raw wire bytes straight from the topic -> GPU decode -> [N>1: owner partition + RCCL
-  all-to-all re-keying by device token, the analogue of Kafka key partitioning] -> registry
-  lookup + assignment validation -> alternate-id dedup -> persist into the HBM event store
-  with enrichment -> device-state merge -> zone-test rules (point-in-polygon, generated alerts
-  persisted too) -> presence scan -> D2H of every enriched event into a pinned record published
-  to the enriched-batch topic -> consumer offset commit (``--no-bus``: pinned batches in, host ring out).
+  -> consumed in place -> H2D of the raw wire bytes straight from the topic -> GPU decode -> [N>1:
+  owner partition + RCCL all-to-all re-keying by device token, the analogue of Kafka key
+  partitioning] -> registry lookup + assignment validation -> alternate-id dedup -> persist into
+  the HBM event store with enrichment -> device-state merge -> zone-test rules (point-in-polygon,
+  generated alerts persisted too) -> presence scan -> durable block encoded on the GPU
+  (``k_seg_encode``) -> copy-engine D2H of the compressed block -> fdatasync'd segment file
+  (O_DIRECT, group commit) + the same block published in place to the enriched-batch topic ->
+  rejected messages (unregistered devices, registrations, acks) routed per payload to their topics
+  -> raw offsets committed once their block is durable.  The timed region ends when every block
+  of the timed steps is on disk.
+The fleet is the realistic mix: every event carries an alternate id (dedup active), ~0.5% of the
+payloads come from unregistered devices, and registrations / acknowledgements are mixed in.
 Weak scaling: per-GPU payloads and per-GPU device shard are fixed as N grows.
 
 Launch: ``python bench.py --gpus 1 --steps 200 --warmup 20`` or under torch.distributed.run
@@ -24,7 +30,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -33,7 +41,7 @@ import numpy as np
 def parse():
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)   # ~0.2 s timed at N=1: steady state, not warm-up
+    ap.add_argument("--steps", type=int, default=200)   # ~0.3 s timed at N=1: steady state, not warm-up
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--msgs", type=int, default=1 << 20, help="payloads per GPU per step")
     ap.add_argument("--devices", type=int, default=1 << 20, help="registered devices per GPU")
@@ -45,11 +53,55 @@ def parse():
                     help="gpu: MI355X kernels; cpu: native multi-threaded C++ engine; oracle: Python reference")
     ap.add_argument("--framing", choices=["varint", "offsets"], default="varint",
                     help="raw-batch framing on the wire to the GPU (varint lengths or u32 offsets)")
+    ap.add_argument("--alt-ids", action=argparse.BooleanOptionalAction, default=True,
+                    help="every event carries an alternate id (dedup active)")
+    ap.add_argument("--p-unregistered", type=float, default=0.005)
+    ap.add_argument("--p-register", type=float, default=0.0005)
+    ap.add_argument("--p-ack", type=float, default=0.0005)
+    ap.add_argument("--durable", action=argparse.BooleanOptionalAction, default=True,
+                    help="persist every step's events to fdatasync'd segment files (the headline)")
+    ap.add_argument("--durable-dir", default=os.environ.get("SW_DURABLE_DIR"),
+                    help="segment directory (default: a fresh directory under the temp dir, removed at exit)")
+    ap.add_argument("--durable-retention-gb", type=float, default=48.0,
+                    help="oldest segment files beyond this are deleted (bounded disk use); 0 = keep all")
+    ap.add_argument("--direct-io", action=argparse.BooleanOptionalAction, default=True)
     ap.add_argument("--no-outbound", action="store_true", help="(diagnostic) skip the D2H outbound copy")
     ap.add_argument("--bus", action=argparse.BooleanOptionalAction, default=True,
                     help="GPU engine: consume raw batches from, and publish enriched batches to, commit-log "
                          "topics in place (pipeline/bus_io.py); --no-bus feeds pinned batches directly")
     return ap.parse_args()
+
+
+def open_durable(args, rank, dev):
+    """(directory to remove at exit or None, DurableEventStore, boot id) of this rank's segments."""
+    from sitewhere_amd.persistence.segments import DurableEventStore
+    tmpdir = args.durable_dir or tempfile.mkdtemp(prefix=f"sw-bench-durable-r{rank}-")
+    seg_dir = os.path.join(tmpdir, f"rank{rank}") if args.durable_dir else tmpdir
+    if os.path.exists(seg_dir) and args.durable_dir:
+        shutil.rmtree(seg_dir)
+    store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30,
+                              retention_bytes=int(args.durable_retention_gb * (1 << 30)), direct=args.direct_io)
+    boot = int(time.time() * 1000)
+    store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
+                                             f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})
+    return (None if args.durable_dir else tmpdir), store, boot
+
+
+class _HostSink:
+    """Block accounting of the host-engine path (same fields as DurableBlockSink)."""
+
+    def __init__(self, store):
+        self.store = store
+        self.bytes = self.rows = self.blocks = 0
+
+    def add(self, blk):
+        self.store.add_encoded(blk)
+        self.bytes += len(blk)
+        self.rows += int(blk[8:12].view(np.uint32)[0])
+        self.blocks += 1
+
+    def flush(self):
+        self.store.flush()
 
 
 def zone_polys(n, lat0, lon0, span, rng):
@@ -81,13 +133,15 @@ def main():
     from sitewhere_amd.pipeline.framing import varint_lengths
 
     n_total_dev = args.devices * world
-    spec = FleetSpec(prefix="dev-", n_devices=n_total_dev, p_location=0.25, p_alert=0.05, p_unregistered=0.0,
-                     mx_per_msg=args.mx_per_msg, n_names=16, with_alternate_id=False,
-                     lat0=33.0, lon0=-85.0, span_deg=2.0)
+    spec = FleetSpec(prefix="dev-", n_devices=n_total_dev, p_location=0.25, p_alert=0.05,
+                     p_unregistered=args.p_unregistered, mx_per_msg=args.mx_per_msg, n_names=16,
+                     with_alternate_id=args.alt_ids, lat0=33.0, lon0=-85.0, span_deg=2.0,
+                     p_register=args.p_register, p_ack=args.p_ack)
     cfg = EngineConfig(max_msgs=args.msgs, rec_cap=args.msgs * args.mx_per_msg + 4096,
                        gen_cap=max(1 << 16, args.msgs // 2), max_devices=int(args.devices * 1.1) + 1024,
                        max_assignments=int(args.devices * 1.1) + 1024, store_cap=args.store,
-                       dedup_slots=1 << 20, name_slots=1 << 12, rank=rank, world=world,
+                       # alternate-id window: 2^24 slots = the last ~8M distinct ids per GPU
+                       dedup_slots=1 << 24, name_slots=1 << 12, rank=rank, world=world,
                        # (assignment, name) state map: 16 measurement names + 4 alert types + zone alerts per device
                        state_slots=2 * (16 + 4 + args.zones) * int(args.devices * 1.1),
                        presence_missing_ms=8 * 3600 * 1000)
@@ -136,51 +190,131 @@ def main():
             torch.cuda.synchronize()
 
     bus_stats = None
+    dur = None
+    tmpdir = None
+    boot = 0
     if use_gpu and args.bus and args.framing == "varint":
         # Through the bus: each step the producer side hands raw batch k to the raw-payload topic
         # (zero-copy: the record is the pinned buffer), the engine's consumer reads it in place and
-        # DMAs it to HBM, and the step's enriched rows are DMA'd into a pinned record published to
-        # the enriched-batch topic.  Consumer offsets are committed once a batch's rows are out.
+        # DMAs it to HBM.  The step's persisted events are encoded on the GPU into one durable block,
+        # the copy engine moves the compressed block to a pinned buffer that is written to the
+        # segment store (O_DIRECT + fdatasync) and published in place to the enriched-batch topic.
+        # Rejected messages are routed per payload while their raw record is still held.  Raw
+        # offsets are committed once the batch's block is durable.
         from collections import deque
 
         from sitewhere_amd.bus.log import EventBus
         from sitewhere_amd.bus.naming import TopicNaming
+        from sitewhere_amd.persistence.segments import DurableBlockSink, DurableEventStore
+        from sitewhere_amd.pipeline import routing
         from sitewhere_amd.pipeline.bus_io import OutboundPublisher, RawBatchRecord, raw_view
         bus = EventBus(None, default_partitions=1)
-        prefix = TopicNaming("sitewhere", f"bench-rank{rank}").tenant_prefix("default")
+        naming = TopicNaming("sitewhere", f"bench-rank{rank}")
+        prefix = naming.tenant_prefix("default")
         t_raw, t_out = prefix + "event-source-raw-payloads", prefix + "inbound-enriched-batches"
         group = prefix + "inbound-processing.raw-payload-consumers"
+        route_topics = (naming.unregistered_device_events("default"), naming.device_registration_events("default"),
+                        naming.decoded_events("default"), naming.failed_decode_events("default"))
+        for t in route_topics:
+            bus.topic(t, 8)
+            bus.set_retention(t, 64 << 20)
+        route_parts = [bus.partitions(t) for t in route_topics]
         bus.topic(t_raw, 1)
-        bus.set_retention(t_raw, 4 * max_raw)
+        bus.set_retention(t_raw, 16 * max_raw)
         records = [RawBatchRecord(b[2][:int(b[3][-1])], b[4].numpy(), len(b[3]) - 1) for b in batches]
         assert raw_view(bus.view(t_raw, 0, records[0].publish(bus, t_raw)))[0].is_pinned(), \
             "raw-batch records must be pinned: the H2D reads them in place"
-        pub = OutboundPublisher(bus, t_out, eng.lib, eng.out_cap, rank=rank, world=world)
-        runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound,
-                                 out_target=pub.target, on_outbound=pub.publish)
-        cursor = {"next": bus.end_offset(t_raw, 0)}
+        routed = {"records": 0, "payloads": 0, "by_kind": [0, 0, 0, 0], "control_decoded": 0}
+
+        def on_rejects(off, refs, compact):
+            # the GPU copied the rejected payloads into `compact`; the router parses only those and
+            # writes the reference's Kafka payloads natively (the held record serves overflow refs)
+            payload = raw_view(bus.view(t_raw, 0, off))[0]
+            rr = routing.route_refs(compact, refs, rank, "bench", route_parts, raw=payload.data_ptr())
+            routed["payloads"] += rr.payloads
+            for kind, part, kh, ko, vh, vo in rr.groups():
+                bus.append_arrays(route_topics[kind], max(part, 0), kh, ko, vh, vo)
+                routed["records"] += len(ko) - 1
+                routed["by_kind"][kind] += len(ko) - 1
+
+        if args.durable:
+            tmpdir, store, boot = open_durable(args, rank, dev)
+            sink = DurableBlockSink(store, eng.lib, boot, rank=rank, world=world, bus=bus, topic=t_out)
+            bus.set_retention(t_out, 64 << 20)
+            dur = {"store": store, "sink": sink}
+            runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=False, block_sink=sink,
+                                     on_rejects=on_rejects)
+        else:
+            pub = OutboundPublisher(bus, t_out, eng.lib, eng.out_cap, rank=rank, world=world)
+            runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound,
+                                     out_target=pub.target, on_outbound=pub.publish, on_rejects=on_rejects)
+        # The synthetic producer: every event carries a fresh alternate id (the replayed batches get a
+        # new id epoch stamped in place, natively, one step ahead on a producer thread) -- otherwise
+        # dedup would rightly discard every replayed event.
+        from concurrent.futures import ThreadPoolExecutor
+
+        from sitewhere_amd.pipeline.bus_io import VALUE_HDR
+        from sitewhere_amd.pipeline.fleet import stamp_alt_epoch
+        producer = ThreadPoolExecutor(1, thread_name_prefix="producer") if args.alt_ids else None
+        stamps = {}
+
+        def stamp(k):
+            rec = records[k % len(records)]
+            return stamp_alt_epoch(rec.ptr + VALUE_HDR, batches[k % len(batches)][3],
+                                   (0x5717 << 48) | (rank << 32) | k, threads=6)
+
+        if producer is not None:
+            stamps[0] = producer.submit(stamp, 0)
+        cursor = {"next": bus.end_offset(t_raw, 0), "committed": bus.end_offset(t_raw, 0)}
         inflight = deque()
-        bus_stats = {"bus": bus, "pub": pub, "t_raw": t_raw, "group": group, "cursor": cursor}
+        bus_stats = {"bus": bus, "t_raw": t_raw, "group": group, "cursor": cursor, "routed": routed,
+                     "route_topics": route_topics}
+
+        def commit_durable():
+            if dur is None:
+                return
+            done = dur["sink"].committable()
+            if done:
+                cursor["durable"] = max(cursor.get("durable", 0), max(o for o in done if o is not None) + 1)
+            # commit what is durable AND whose rejects are routed (the router runs on its own thread)
+            floor = runner.rejects_floor()
+            upto = cursor.get("durable", cursor["committed"]) if floor is None else min(cursor.get("durable", 0), floor)
+            if upto > cursor["committed"]:
+                cursor["committed"] = upto
+                bus.commit(group, t_raw, 0, upto)
 
         def run(k):
+            if producer is not None:
+                stamps.pop(k).result()                        # batch k's fresh alternate ids
             records[k % len(records)].publish(bus, t_raw, 0, ts=now0 + k)     # producer: batch k arrives
+            if producer is not None:
+                stamps[k + 1] = producer.submit(stamp, k + 1)
             off = cursor["next"]
             cursor["next"] = off + 1
+            # the consumer holds every record not yet committed: H2D in flight, rejects to route,
+            # block not yet durable
+            bus.hold(t_raw, 0, cursor["committed"] if dur is not None else off)
             payload, lens, n, pb = raw_view(bus.view(t_raw, 0, off))           # consumer: read in place
             slot = runner.k % runner.nbuf
-            pub.now_ms = now0 + k
-            runner.submit(payload, None, n, now_ms=now0 + k, presence=True, lens_host=lens, raw_bytes=pb)
-            inflight.append((off, runner.ev_h2d[slot]))
-            while inflight and inflight[0][1].query():
-                inflight.popleft()
-            bus.hold(t_raw, 0, inflight[0][0] if inflight else None)          # in-flight H2D sources stay
-            if off >= 2:
-                bus.commit(group, t_raw, 0, off - 1)     # batches < off-1: processed and rows published
+            runner.submit(payload, None, n, now_ms=now0 + k, presence=True, lens_host=lens, raw_bytes=pb, tag=off)
+            if dur is None:
+                inflight.append((off, runner.ev_h2d[slot]))
+                while inflight and inflight[0][1].query():
+                    inflight.popleft()
+                bus.hold(t_raw, 0, inflight[0][0] if inflight else None)
+                if off >= 2:
+                    bus.commit(group, t_raw, 0, off - 1)     # batches < off-1: processed and rows published
+            else:
+                commit_durable()
 
         def finish():
             runner.flush()
+            if dur is not None:
+                dur["sink"].flush()                           # every block of the run is on disk
+                commit_durable()
             bus.hold(t_raw, 0, None)
-            bus.commit(group, t_raw, 0, cursor["next"])
+            if dur is None:
+                bus.commit(group, t_raw, 0, cursor["next"])
     elif use_gpu:
         runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound)
 
@@ -195,18 +329,28 @@ def main():
         def finish():
             runner.flush()
     else:
+        if args.durable:        # host engines encode the same blocks on the CPU (swseg_encode)
+            tmpdir, store, boot = open_durable(args, rank, dev)
+            dur = {"store": store, "sink": _HostSink(store)}
+
         def run(k):
             _, _, r, o, _ = batches[k % len(batches)]
-            eng.step(r, o, now0 + k, presence=True)
+            res = eng.step(r, o, now0 + k, presence=True)
+            if dur is not None:
+                dur["sink"].add(eng.encode_block(now0 + k, res, boot=boot))
 
         def finish():
-            pass
+            if dur is not None:
+                dur["sink"].flush()
 
     for k in range(args.warmup):
         run(k)
     finish()
     barrier()
     s0 = eng.stats_dict()
+    d0 = dur["store"].seg.stats() if dur else None
+    sk0 = (dur["sink"].bytes, dur["sink"].rows, dur["sink"].blocks) if dur else None
+    r0 = dict(bus_stats["routed"], by_kind=list(bus_stats["routed"]["by_kind"])) if bus_stats else None
     barrier()
     t_start = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
@@ -219,16 +363,63 @@ def main():
     persisted = s1["persisted"] - s0["persisted"]
     msgs = s1["messages"] - s0["messages"]
     rule_alerts = s1["rule_alerts"] - s0["rule_alerts"]
+    rank_elapsed = elapsed
     # whole-job aggregate: max time over ranks, sum of events
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed, ev, persisted, msgs, rule_alerts], dtype=torch.float64,
-                         device=torch.device("cuda", local) if use_gpu else "cpu")
+        dev_t = torch.device("cuda", local) if use_gpu else "cpu"
+        t = torch.tensor([elapsed, ev, persisted, msgs, rule_alerts], dtype=torch.float64, device=dev_t)
         tmax = t[:1].clone()
+        gathered = [torch.zeros(1, dtype=torch.float64, device=dev_t) for _ in range(world)]
+        dist.all_gather(gathered, t[:1].clone())
+        per_rank = [round(float(x.item()), 6) for x in gathered]
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(tmax.item())
         ev, persisted, msgs, rule_alerts = (int(x) for x in t[1:].tolist())
     value = ev / elapsed
+    detail = {
+        "events": ev, "persisted": persisted, "payloads": msgs, "rule_alerts": rule_alerts,
+        "persisted_per_sec": round(persisted / elapsed, 1),
+        "payload_bytes_per_gpu_step": int(max_raw), "setup_s": round(setup_s, 1),
+        "h2d_bytes_per_gpu_step": int(max_raw) + int(max(
+            (b[4].numel() if b[4] is not None else 4 * len(b[3])) for b in batches)),
+        "registered_devices_rank0": n_dev,
+        "rejected_rank0": {k: s1[k] - s0[k] for k in ("unregistered", "unassigned", "duplicates", "decode_errors",
+                                                       "control")},
+        "backend": dist.get_backend() if world > 1 else None,
+        "world": dist.get_world_size() if world > 1 else 1,
+        "rank_elapsed_s": per_rank if per_rank is not None else [round(rank_elapsed, 6)],
+    }
+    if world > 1:
+        from sitewhere_amd.parallel.sharding import exchange_bytes_per_rank
+        detail["exchange_bytes_per_rank_step"] = exchange_bytes_per_rank(cfg.rec_cap, world)
+        detail["shuffle_deferred"] = s1.get("shuffle_deferred", 0) - s0.get("shuffle_deferred", 0)
+        detail["shuffle_overflow"] = s1.get("shuffle_overflow", 0) - s0.get("shuffle_overflow", 0)
+    if bus_stats:
+        r1 = bus_stats["routed"]
+        bus = bus_stats["bus"]
+        detail["bus"] = {"raw_topic_records": bus.end_offset(bus_stats["t_raw"], 0),
+                         "raw_committed": bus.committed(bus_stats["group"], bus_stats["t_raw"], 0),
+                         "rejects_routed_records": r1["records"] - r0["records"],
+                         "rejects_routed_payloads": r1["payloads"] - r0["payloads"],
+                         "routed_by_topic": {t.rsplit(".", 1)[-1]: r1["by_kind"][i] - r0["by_kind"][i]
+                                             for i, t in enumerate(bus_stats["route_topics"])}}
+    if use_gpu and getattr(runner, "trace", None) is not None:
+        detail["runner_trace_ms_per_step"] = {k: round(1000 * v / (args.steps + args.warmup), 3)
+                                              for k, v in runner.trace.items()}
+    if dur:
+        d1 = dur["store"].seg.stats()
+        sk = dur["sink"]
+        nbytes, nrows, nblocks = sk.bytes - sk0[0], sk.rows - sk0[1], sk.blocks - sk0[2]
+        detail["durable"] = {
+            "blocks": nblocks, "rows": nrows, "block_bytes": nbytes,
+            "bytes_per_event": round(nbytes / max(1, nrows), 3),
+            "durable_bytes_per_s": round((d1["bytes_written"] - d0["bytes_written"]) / elapsed, 1),
+            "disk_bytes_written": d1["bytes_written"] - d0["bytes_written"],
+            "fdatasyncs": d1["syncs"] - d0["syncs"], "direct_io": bool(d1["direct_io"]),
+            "retention_deleted_bytes": d1["deleted_bytes"], "all_durable": sk.store.durable() >= sk.store.seg.last_token,
+        }
     if rank == 0:
         out = {
             "metric": "device_events_per_sec",
@@ -242,10 +433,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp64/int64 (event values as in the reference; no reduced precision)",
-            "data": "synthetic: protobuf device payloads (reference sitewhere.proto) from a random-token fleet",
+            "data": "synthetic: protobuf device payloads (reference sitewhere.proto) from a random-token fleet; "
+                    f"alternate ids {'on' if args.alt_ids else 'off'}, {args.p_unregistered:.2%} unregistered, "
+                    f"{args.p_register:.2%} registrations, {args.p_ack:.2%} acks",
             "config": {
                 "model": "sitewhere-inbound-pipeline",
-                "stages": "decode>rekey>validate>dedup>persist+enrich>device-state>zone-rules>presence>outbound",
+                "stages": "decode>rekey>validate>dedup>persist+enrich>device-state>zone-rules>presence>"
+                          + ("gpu-encode>durable-store(fdatasync)>" if dur else "outbound>") + "reject-routing",
                 "global_batch": args.msgs * world,
                 "seq_len": 1,
                 "parallelism": f"dp{world} (device-sharded, all-to-all re-key)",
@@ -257,22 +451,15 @@ def main():
                 "cpu_threads": getattr(eng, "threads", None),
                 "framing": args.framing,
                 "bus": bool(bus_stats),
+                "durable": bool(dur),
             },
-            "detail": {
-                "events": ev, "persisted": persisted, "payloads": msgs, "rule_alerts": rule_alerts,
-                "persisted_per_sec": round(persisted / elapsed, 1),
-                "payload_bytes_per_gpu_step": int(max_raw), "setup_s": round(setup_s, 1),
-                "h2d_bytes_per_gpu_step": int(max_raw) + int(max(
-                    (b[4].numel() if b[4] is not None else 4 * len(b[3])) for b in batches)),
-                "registered_devices_rank0": n_dev,
-                **({"bus": {"raw_topic_records": bus_stats["bus"].end_offset(bus_stats["t_raw"], 0),
-                            "raw_committed": bus_stats["bus"].committed(bus_stats["group"], bus_stats["t_raw"], 0),
-                            "enriched_batches_published": bus_stats["pub"].published,
-                            "enriched_rows_published": bus_stats["pub"].rows,
-                            "enriched_buffers": bus_stats["pub"].n_alloc}} if bus_stats else {}),
-            },
+            "detail": detail,
         }
         print(json.dumps(out), flush=True)
+    if dur:
+        dur["store"].close()
+        if tmpdir:
+            shutil.rmtree(tmpdir, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
 

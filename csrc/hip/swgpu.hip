@@ -481,37 +481,113 @@ __global__ void k_lookup(SwEngineArgs a) {
   }
 }
 
-// Alternate-id dedup window: first occurrence (lowest global sequence) wins; anything
-// seen in an earlier batch is a duplicate.  Only events that would be persisted insert.
+// Alternate-id dedup window (reference AlternateIdDeduplicator.java:41-56), generational: two
+// open-addressing tables, `cur` (ids first seen in the current generation) and `prev` (the
+// generation before).  An event whose id is in `prev` is a duplicate; otherwise it is inserted into
+// `cur`, where the first occurrence (lowest global sequence) wins and every later one -- in this
+// batch or any later batch of the generation -- is a duplicate.  Before a step whose ids could push
+// `cur` past half its slots, the generations rotate (k_dedup_rotate): `prev` is forgotten and
+// cleared to become the new `cur`.  The window therefore covers the last slots/2 - rec_cap to
+// slots - rec_cap distinct ids, probes stay short (load <= 0.5), and a probe that still hits
+// MAX_PROBE is counted (SW_STAT_DEDUP_OVERFLOW) rather than silently ignored.
+__device__ __forceinline__ bool dd_find(const ull* __restrict__ key, int64_t mask, ull h) {
+  int64_t slot = (int64_t)(h & (ull)mask);
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    const ull k = key[slot];
+    if (k == h) return true;
+    if (k == 0) return false;
+    slot = (slot + 1) & mask;
+  }
+  return false;
+}
+
+// Rotation decision (one thread) at the start of the dedup phase; k_dedup_clear does the clearing.
+// dd_meta = [generation, ids in cur, rotate flag, pad].
+__global__ void k_dedup_rotate(int64_t* __restrict__ meta, int64_t half, int64_t batch_cap, ull* __restrict__ stats) {
+  if (threadIdx.x == 0 && BID == 0) {
+    if (meta[1] + batch_cap > half) {
+      meta[0] ^= 1;
+      meta[1] = 0;
+      meta[2] = 1;
+      stats[SW_STAT_DEDUP_ROTATIONS] += 1;
+    } else {
+      meta[2] = 0;
+    }
+  }
+}
+
+__global__ void k_dedup_clear(ull* __restrict__ key, ull* __restrict__ seq, int64_t slots,
+                              const int64_t* __restrict__ meta) {
+  if (meta[2] == 0) return;
+  const int64_t g = meta[0];
+  ull* k = key + g * slots;
+  ull* q = seq + g * slots;
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK) {
+    k[i] = 0ull;
+    q[i] = ~0ull;
+  }
+}
+
 __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                               const uint8_t* __restrict__ status, ull* __restrict__ key, ull* __restrict__ seq,
-                               int64_t mask, const int64_t* __restrict__ seq_base) {
+                               uint8_t* __restrict__ status, ull* __restrict__ key, ull* __restrict__ seq,
+                               int64_t mask, const int64_t* __restrict__ seq_base, int64_t* __restrict__ meta,
+                               ull* __restrict__ stats) {
+  __shared__ uint32_t blk_new, blk_over;
+  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; }
+  __syncthreads();
   const uint32_t n = *n_ptr;
   const ull sb = (ull)*seq_base;
+  const int64_t slots = mask + 1;
+  const int64_t g = meta[0];
+  ull* ck = key + g * slots;
+  ull* cq = seq + g * slots;
+  const ull* pk = key + (1 - g) * slots;
+  uint32_t my_new = 0, my_over = 0;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
+    if (dd_find(pk, mask, h)) { status[i] = SW_ST_DUPLICATE; continue; }
     int64_t slot = (int64_t)(h & (ull)mask);
+    bool placed = false;
     for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-      ull old = atomicCAS(&key[slot], 0ull, h);
-      if (old == 0 || old == h) { atomicMin(&seq[slot], sb + (ull)i); break; }
+      const ull old = atomicCAS(&ck[slot], 0ull, h);
+      if (old == 0 || old == h) {
+        my_new += old == 0 ? 1u : 0u;
+        atomicMin(&cq[slot], sb + (ull)i);
+        placed = true;
+        break;
+      }
       slot = (slot + 1) & mask;
     }
+    my_over += placed ? 0u : 1u;
+  }
+  // counters aggregated per workgroup: one global atomic per block, not one per id (1M same-address
+  // atomics per step serialised this kernel, profiles/r3_dedup)
+  if (my_new) atomicAdd(&blk_new, my_new);
+  if (my_over) atomicAdd(&blk_over, my_over);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (blk_new) atomicAdd((unsigned long long*)&meta[1], (ull)blk_new);
+    if (blk_over) atomicAdd(&stats[SW_STAT_DEDUP_OVERFLOW], (ull)blk_over);
   }
 }
 
 __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                               uint8_t* __restrict__ status, const ull* __restrict__ key, const ull* __restrict__ seq,
-                              int64_t mask, const int64_t* __restrict__ seq_base) {
+                              int64_t mask, const int64_t* __restrict__ seq_base, const int64_t* __restrict__ meta) {
   const uint32_t n = *n_ptr;
   const ull sb = (ull)*seq_base;
+  const int64_t slots = mask + 1;
+  const int64_t g = meta[0];
+  const ull* ck = key + g * slots;
+  const ull* cq = seq + g * slots;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
     int64_t slot = (int64_t)(h & (ull)mask);
     for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-      const ull k = key[slot];
-      if (k == h) { if (seq[slot] != sb + (ull)i) status[i] = SW_ST_DUPLICATE; break; }
+      const ull k = ck[slot];
+      if (k == h) { if (cq[slot] != sb + (ull)i) status[i] = SW_ST_DUPLICATE; break; }
       if (k == 0) break;
       slot = (slot + 1) & mask;
     }
@@ -1042,7 +1118,83 @@ __global__ __launch_bounds__(BLK) void k_store_filter(const uint8_t* __restrict_
   }
 }
 
+// ============================================================================ reject refs
+// Snapshot of a step's rejected events for the host slow path, taken on the compute stream right
+// after the process phase (the next step overwrites the reject list).  Duplicates are dropped here
+// (dedup discards them).  Every other reject of a locally received payload gets a ref
+//   (payload start in the batch, payload end, status | src_rank << 8, offset of its copy)
+// and the payload bytes are copied into a compact buffer, so only those bytes cross PCIe and the
+// host parses them sequentially (csrc/native/swroute.cpp), never the scattered raw batch.
+// out = u32[4] device counters: out[0] = refs (may exceed cap), out[1] = bytes used (may exceed
+// bytes_cap: such refs carry copy offset ~0 and the host reads the raw record instead).  `refs`
+// (u32[4 * cap]) and `bytes` are usually mapped pinned host memory: written straight over PCIe, no
+// copy call.  Refs are in any order; events decoded on another rank keep start = end = 0.
+__global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_t* __restrict__ rej_idx,
+                              const uint32_t* __restrict__ n_rej_ptr, const uint8_t* __restrict__ status,
+                              const uint8_t* __restrict__ raw, const uint32_t* __restrict__ msg_off, int64_t n_msgs,
+                              int rank, uint32_t* __restrict__ out, uint32_t* __restrict__ refs, int64_t cap,
+                              uint8_t* __restrict__ bytes, int64_t bytes_cap) {
+  const uint32_t n = *n_rej_ptr;
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+    const uint32_t i = rej_idx[j];
+    const uint8_t st = status[i];
+    if (st == SW_ST_DUPLICATE) continue;
+    const SwEventRec& r = work[i];
+    uint32_t s = 0, e = 0, copy = 0xffffffffu;
+    if (r.src_rank == (uint8_t)rank && n_msgs > 0) {
+      int64_t lo = 0, hi = n_msgs;              // msg_off[lo] <= off < msg_off[hi]
+      const uint32_t off = r.aux_off;
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (msg_off[mid] <= off) lo = mid; else hi = mid;
+      }
+      s = msg_off[lo];
+      e = msg_off[lo + 1];
+      const uint32_t len = e > s ? e - s : 0u;
+      const uint32_t at = atomicAdd(out + 1, len);
+      if ((int64_t)at + len <= bytes_cap) {
+        for (uint32_t b = 0; b < len; ++b) bytes[at + b] = raw[s + b];
+        copy = at;
+      }
+    }
+    const uint32_t k = atomicAdd(out, 1u);
+    if (k < cap) {
+      refs[4 * k] = s;
+      refs[4 * k + 1] = e;
+      refs[4 * k + 2] = (uint32_t)st | ((uint32_t)r.src_rank << 8);
+      refs[4 * k + 3] = copy;
+    }
+  }
+}
+
 extern "C" {
+
+int sw_reject_refs(const SwEngineArgs* ap, const uint8_t* raw, const uint32_t* msg_off, int64_t n_msgs, uint32_t* out,
+                   uint32_t* refs, int64_t cap, uint8_t* bytes, int64_t bytes_cap, hipStream_t s) {
+  const SwEngineArgs a = *ap;
+  hipError_t e = hipMemsetAsync(out, 0, 16, s);
+  if (e != hipSuccess) return (int)e;
+  k_reject_refs<<<grid_for(a.rec_cap), BLK, 0, s>>>(a.work, a.rej_idx, a.n_rej, a.status, raw, msg_off, n_msgs,
+                                                    (int)a.rank, out, refs, cap, bytes, bytes_cap);
+  return (int)hipGetLastError();
+}
+
+// End-of-step snapshot into mapped host memory (one launch instead of one copy per value): the
+// step's u32 scalars (n_out at [7], n_rej at [5]) -> host[0..15]; the durable-block encoder's
+// (bytes, errors, first sequence) u64s -> host[16..21]; the reject-ref counters -> host[24..25].
+__global__ void k_step_snapshot(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ seg_meta,
+                                const uint32_t* __restrict__ rej_cnt, int produced, uint32_t* __restrict__ host) {
+  const uint32_t t = threadIdx.x;
+  if (t < 16) host[t] = produced ? scalars[t] : 0u;
+  else if (t < 22) host[t] = (produced && seg_meta) ? seg_meta[t - 16] : 0u;
+  else if (t == 24 || t == 25) host[t] = (produced && rej_cnt) ? rej_cnt[t - 24] : 0u;
+}
+
+int sw_step_snapshot(const uint32_t* scalars, const uint32_t* seg_meta, const uint32_t* rej_cnt, int32_t produced,
+                     uint32_t* host, hipStream_t s) {
+  k_step_snapshot<<<1, 64, 0, s>>>(scalars, seg_meta, rej_cnt, produced, host);
+  return (int)hipGetLastError();
+}
 
 // Framing: varint length stream -> msg_off[n_msgs + 1].  tmp needs 2 * ceil(nbytes / 1024) u32.
 int sw_frame_varint(const uint8_t* lens, int64_t nbytes, int64_t n_msgs, uint32_t* msg_off, uint32_t raw_bytes,
@@ -1116,9 +1268,12 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_process_begin<<<1, 64, 0, s>>>(a);
   if (a.world == 1) (void)hipMemcpyAsync(a.n_work, a.n_recs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
   k_lookup<<<g, BLK, 0, s>>>(a);
-  k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base);
+  k_dedup_rotate<<<1, 64, 0, s>>>(a.dd_meta, (a.dd_mask + 1) / 2, a.rec_cap, (ull*)a.stats);
+  k_dedup_clear<<<grid_for(a.dd_mask + 1), BLK, 0, s>>>((ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask + 1, a.dd_meta);
+  k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base,
+                                   a.dd_meta, (ull*)a.stats);
   k_dedup_check<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (const ull*)a.dd_key, (const ull*)a.dd_seq, a.dd_mask,
-                                  a.seq_base);
+                                  a.seq_base, a.dd_meta);
   // stable split ok / rejected
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles);
   uint32_t* cmp_off = a.cmp_tmp + 2 * ntiles;

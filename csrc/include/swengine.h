@@ -183,6 +183,9 @@ typedef struct SwEngineArgs {
   int64_t n_zone_vtx;          // zone_off[n_zones]: sizes k_zone_mask's dynamic LDS vertex table
   // ---------------------------------------------------------------- state merge scratch
   int64_t* ev_slot;            // [2 * max(rec_cap, gen_cap)] state pass-2 items: (ms slot | -2 - asg | -1, date)
+  // ---------------------------------------------------------------- dedup generations
+  int64_t* dd_meta;            // [generation, ids in the current table, rotate flag, pad]; dd_key / dd_seq
+                               // hold two tables of dd_mask + 1 slots (current = dd_meta[0])
 } SwEngineArgs;
 
 enum {
@@ -200,5 +203,7 @@ enum {
   SW_STAT_NEW_NAMES = 11,
   SW_STAT_STATE_OVERFLOW = 12,
   SW_STAT_SHUFFLE_DEFERRED = 13,   // records spilled to the next step's exchange
+  SW_STAT_DEDUP_OVERFLOW = 14,     // alternate ids the window could not place (probe bound hit)
+  SW_STAT_DEDUP_ROTATIONS = 15,    // dedup generations retired
   SW_STAT_N = 16,
 };

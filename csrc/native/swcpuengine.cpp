@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "swtypes.h"
+#include "swengine.h"   // SW_STAT_* slots
 
 namespace {
 
@@ -273,7 +274,9 @@ typedef struct SwCeStep {
 
 struct SwCpuEngine {
   Pool pool;
-  std::vector<U64Map<int64_t>> dedup;  // sharded by hash % T
+  std::vector<U64Map<int64_t>> dedup;       // current generation of the alternate-id window, by hash % T
+  std::vector<U64Map<int64_t>> dedup_prev;  // previous generation (see the rotation in swce_process)
+  int64_t dd_slots = 0, dd_batch = 0;       // window slots and the largest batch (rotation rule)
   U64Map<int32_t> intern;
   int32_t n_intern = 0;
   std::vector<U64Map<MsVal>> ms;       // sharded by assignment % T
@@ -283,7 +286,7 @@ struct SwCpuEngine {
   std::vector<int64_t> ok_idx;
   std::vector<std::vector<int32_t>> lists;  // [chunk * T + shard] -> record / row indices
   std::vector<std::vector<int64_t>> scratch64;
-  explicit SwCpuEngine(int n) : pool(n), dedup(pool.size()), ms(pool.size()) {
+  explicit SwCpuEngine(int n) : pool(n), dedup(pool.size()), dedup_prev(pool.size()), ms(pool.size()) {
     const int T = pool.size();
     lists.resize((size_t)T * T);
     scratch64.resize(T);
@@ -493,7 +496,18 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   });
   lap("lookup");
 
-  // 2. alternate-id dedup, sharded by hash; each shard walks its records in batch order
+  // 2. alternate-id dedup, sharded by hash; each shard walks its records in batch order.  The window
+  // is generational like the GPU's (k_dedup_rotate): before a batch that could push the current
+  // generation past half the window's slots, the previous generation is forgotten.
+  if (e->dd_slots > 0) {
+    int64_t cur = 0;
+    for (auto& m : e->dedup) cur += (int64_t)m.n;
+    if (cur + e->dd_batch > e->dd_slots / 2) {
+      std::swap(e->dedup, e->dedup_prev);
+      for (auto& m : e->dedup) m.reset((size_t)std::max<int64_t>(64, e->dd_slots / T));
+      t->stats[SW_STAT_DEDUP_ROTATIONS] += 1;
+    }
+  }
   bool any_alt = false;
   for (int w = 0; w < T; ++w) any_alt |= has_alt[w] != 0;
   if (any_alt) {
@@ -508,8 +522,13 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
     const int64_t seq_base = st->seq_base;
     e->pool.run([&](int sh) {
       U64Map<int64_t>& m = e->dedup[sh];
+      const U64Map<int64_t>& prev = e->dedup_prev[sh];
       for (int w = 0; w < T; ++w)
         for (int32_t i : e->lists[(size_t)w * T + sh]) {
+          if (prev.n && prev.find(work[i].alt_hash)) {
+            status[i] = SW_ST_DUPLICATE;
+            continue;
+          }
           auto ins = m.insert(work[i].alt_hash);
           if (ins.second) *ins.first = seq_base + i;
           else status[i] = SW_ST_DUPLICATE;
@@ -693,6 +712,35 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   st->n_rule = n_rule;
   st->n_rej = n - n_ok;
   return 0;
+}
+
+// Window sizing of the generational dedup (slots per generation, largest batch in records).
+void swce_dedup_window(void* p, int64_t slots, int64_t batch) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  e->dd_slots = slots;
+  e->dd_batch = batch;
+}
+
+// Previous dedup generation (checkpoints carry both).
+int64_t swce_dedup_prev_size(void* p) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  int64_t n = 0;
+  for (auto& m : e->dedup_prev) n += (int64_t)m.n;
+  return n;
+}
+
+int64_t swce_dedup_prev_export(void* p, uint64_t* keys, int64_t* seqs) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  int64_t k = 0;
+  for (auto& m : e->dedup_prev) m.for_each([&](uint64_t key, int64_t v) { keys[k] = key; seqs[k] = v; ++k; });
+  return k;
+}
+
+void swce_dedup_prev_import(void* p, const uint64_t* keys, const int64_t* seqs, int64_t n) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  for (auto& m : e->dedup_prev) m.reset(64);
+  for (int64_t i = 0; i < n; ++i)
+    *e->dedup_prev[sw_mix64(keys[i]) % (uint64_t)e->T()].insert(keys[i]).first = seqs[i];
 }
 
 // ---------------------------------------------------------------- checkpoint export / import

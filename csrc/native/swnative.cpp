@@ -224,7 +224,11 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
     uint32_t cmd;
     char alt[48];
     size_t alen = 0;
-    if (with_alt_id) alen = (size_t)snprintf(alt, sizeof(alt), "a%llx-%lld", (unsigned long long)seed, (long long)m);
+    // fixed width "<16 hex epoch>-<8 hex sequence>", the body's last field: a producer replaying a
+    // pre-generated batch stamps a fresh epoch in place (sw_stamp_alt_epoch)
+    if (with_alt_id)
+      alen = (size_t)snprintf(alt, sizeof(alt), "%016llx-%08llx", (unsigned long long)seed,
+                              (unsigned long long)(m & 0xffffffffLL));
     if (u < p_loc) {
       cmd = SW_CMD_SEND_DEVICE_LOCATION;
       eb.str(1, tok, tlen);
@@ -273,6 +277,35 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
   }
   offs[n_msgs] = (uint32_t)pos;
   return pos;
+}
+
+// Stamp a new 16-hex-digit epoch into the fixed-width alternate ids of a generated batch (see
+// sw_gen_payloads): every payload whose body ends with field 15 = "<16 hex>-<8 hex>" gets `epoch`,
+// so a replayed batch carries fresh alternate ids.  Split over `threads` threads (0 = 8).
+// Returns the number of payloads stamped.
+int64_t sw_stamp_alt_epoch(uint8_t* raw, const uint32_t* offs, int64_t n, uint64_t epoch, int32_t threads) {
+  char hex[17];
+  snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)epoch);
+  const int T = threads > 0 ? threads : 8;
+  std::vector<std::thread> th;
+  std::atomic<int64_t> stamped{0};
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([&, t] {
+      int64_t c = 0;
+      const int64_t a = n * t / T, b = n * (t + 1) / T;
+      for (int64_t m = a; m < b; ++m) {
+        const uint32_t e = offs[m + 1];
+        if (e < offs[m] + 27) continue;
+        uint8_t* p = raw + e - 27;                     // key 0x7a (field 15, bytes), length 25
+        if (p[0] != 0x7a || p[1] != 25 || p[2 + 16] != '-') continue;
+        memcpy(p + 2, hex, 16);
+        ++c;
+      }
+      stamped += c;
+    });
+  }
+  for (auto& x : th) x.join();
+  return stamped.load();
 }
 
 // Token heap for devices [0, n): "<prefix><index:010>"; offs has n+1 entries.

@@ -15,10 +15,12 @@
 //     EventSourcesManager.java:189-197)
 // Output records are keyed by device token and carry the Kafka partition of the key.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "swtypes.h"
@@ -57,88 +59,111 @@ struct Parsed {
 };
 
 // ---------------------------------------------------------------- protobuf writer
+// Appends into a reused buffer (clear() keeps the capacity): no allocation per record once warm.
 struct W {
-  std::vector<uint8_t> b;
+  std::vector<uint8_t> buf;
+  size_t n = 0;
+  void clear() { n = 0; }
+  size_t size() const { return n; }
+  const uint8_t* data() const { return buf.data(); }
+  uint8_t* at(size_t k) {                    // room for k more bytes, returns the write cursor
+    if (n + k > buf.size()) buf.resize(std::max<size_t>(2 * buf.size(), n + k + 4096));
+    return buf.data() + n;
+  }
+  void raw(const uint8_t* p, size_t k) {
+    memcpy(at(k), p, k);
+    n += k;
+  }
   void varint(uint64_t v) {
+    uint8_t* o = at(10);
+    size_t i = 0;
     while (v >= 0x80) {
-      b.push_back((uint8_t)(v | 0x80));
+      o[i++] = (uint8_t)(v | 0x80);
       v >>= 7;
     }
-    b.push_back((uint8_t)v);
+    o[i++] = (uint8_t)v;
+    n += i;
   }
   void key(uint32_t f, uint32_t wt) { varint(((uint64_t)f << 3) | wt); }
   void str(uint32_t f, const Str& s) {
     key(f, 2);
     varint(s.n);
-    b.insert(b.end(), s.p, s.p + s.n);
+    raw(s.p, s.n);
   }
-  void bytes(uint32_t f, const std::vector<uint8_t>& m) {
+  void sub(uint32_t f, const W& m) {
     key(f, 2);
-    varint(m.size());
-    b.insert(b.end(), m.begin(), m.end());
+    varint(m.n);
+    raw(m.buf.data(), m.n);
+  }
+  void fixed64(uint64_t u) {
+    memcpy(at(8), &u, 8);                    // little-endian host
+    n += 8;
   }
   void dbl(uint32_t f, double d) {
     key(f, 1);
     uint64_t u;
     memcpy(&u, &d, 8);
-    for (int i = 0; i < 8; ++i) b.push_back((uint8_t)(u >> (8 * i)));
+    fixed64(u);
   }
   void u64(uint32_t f, uint64_t v) {
     key(f, 0);
     varint(v);
   }
+  // proto3 wrappers GOptionalString / GOptionalDouble / GOptionalBoolean {value = 1}, written inline
+  void opt_str(uint32_t f, const Str& s) {
+    key(f, 2);
+    if (!s.n) { varint(0); return; }
+    varint(1 + vlen(s.n) + s.n);
+    str(1, s);
+  }
+  void opt_dbl(uint32_t f, double d) {
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    key(f, 2);
+    if (!u) { varint(0); return; }
+    varint(9);
+    dbl(1, d);
+  }
+  void opt_bool(uint32_t f, bool v) {
+    key(f, 2);
+    if (!v) { varint(0); return; }
+    varint(2);
+    u64(1, 1);
+  }
+  static size_t vlen(uint64_t v) {
+    size_t n = 1;
+    while (v >= 0x80) { v >>= 7; ++n; }
+    return n;
+  }
 };
-
-// proto3 wrappers: GOptionalString / GOptionalDouble / GOptionalBoolean {value = 1}
-std::vector<uint8_t> opt_str(const Str& s) {
-  W w;
-  if (s.n) w.str(1, s);
-  return w.b;
-}
-
-std::vector<uint8_t> opt_dbl(double d) {
-  W w;
-  uint64_t u;
-  memcpy(&u, &d, 8);
-  if (u) w.dbl(1, d);
-  return w.b;
-}
-
-std::vector<uint8_t> opt_bool(bool v) {
-  W w;
-  if (v) w.u64(1, 1);
-  return w.b;
-}
 
 void map_entries(W& w, uint32_t f, const std::vector<Meta>& meta) {
   for (const Meta& m : meta) {
-    W e;
-    if (m.k.n) e.str(1, m.k);
-    if (m.v.n) e.str(2, m.v);
-    w.bytes(f, e.b);
+    const size_t n = (m.k.n ? 1 + W::vlen(m.k.n) + m.k.n : 0) + (m.v.n ? 1 + W::vlen(m.v.n) + m.v.n : 0);
+    w.key(f, 2);
+    w.varint(n);
+    if (m.k.n) w.str(1, m.k);
+    if (m.v.n) w.str(2, m.v);
   }
 }
 
 // GDeviceEventCreateRequest (alternateId = 1, eventDate = 5, updateState = 6, metadata = 7)
-std::vector<uint8_t> event_header(const Parsed& p, const Str& alt) {
-  W w;
-  if (alt.has) w.bytes(1, opt_str(alt));
+void event_header(W& w, const Parsed& p, const Str& alt) {
+  w.clear();
+  if (alt.has) w.opt_str(1, alt);
   if (p.has_date && p.date) w.u64(5, p.date);
-  if (p.has_us) w.bytes(6, opt_bool(p.us));
+  if (p.has_us) w.opt_bool(6, p.us);
   map_entries(w, 7, p.meta);
-  return w.b;
 }
 
-// GInboundEventPayload {sourceId = 1, deviceToken = 2, originator = 3, event = 4}
-std::vector<uint8_t> inbound(const Str& source, const Parsed& p, uint32_t member, const std::vector<uint8_t>& req) {
-  W any;
-  any.bytes(member, req);
-  W w;
-  if (source.n) w.str(1, source);
-  if (p.token.n) w.str(2, p.token);
-  if (p.originator.has) w.bytes(3, opt_str(p.originator));
-  w.bytes(4, any.b);
-  return w.b;
+// GInboundEventPayload {sourceId = 1, deviceToken = 2, originator = 3, event = 4 {member = req}}
+void inbound(W& out, const Str& source, const Parsed& p, uint32_t member, const W& req) {
+  if (source.n) out.str(1, source);
+  if (p.token.n) out.str(2, p.token);
+  if (p.originator.has) out.opt_str(3, p.originator);
+  out.key(4, 2);
+  out.varint(1 + W::vlen(req.size()) + req.size());
+  out.sub(member, req);
 }
 
 // ---------------------------------------------------------------- device protocol reader
@@ -249,23 +274,27 @@ bool parse(const uint8_t* b, uint32_t s, uint32_t e, Parsed* p) {
   return p->token.n > 0;
 }
 
-struct Rec {
-  int32_t kind, part;
-  std::vector<uint8_t> key, val;
+// One routed record: key = device token (bytes in the raw batch), value in a worker's arena.
+struct RecRef {
+  uint64_t order;           // kind << 62 | partition << 46 | payload rank << 14 | sub-record
+  const uint8_t* key;
+  uint32_t klen;
+  uint32_t worker;
+  uint64_t voff;
+  uint64_t vlen;
 };
 
-struct Out {
-  std::vector<Rec> recs;
-  int32_t parts[4];
-  void emit(int kind, const Str& key, const uint8_t* v, int64_t vn) {
-    Rec r;
-    r.kind = kind;
-    r.part = key.n ? sw_partition_for_key(key.p, (int32_t)key.n, parts[kind] > 0 ? parts[kind] : 1) : -1;
-    r.key.assign(key.p, key.p + key.n);
-    r.val.assign(v, v + vn);
-    recs.push_back(std::move(r));
-  }
+struct Worker {
+  W arena, h, m, reg;       // output values + reused scratch
+  std::vector<RecRef> recs;
+  Parsed p;
+  std::string alt;
 };
+
+static inline uint64_t order_of(int kind, int32_t part, uint64_t rank, uint64_t sub) {
+  return ((uint64_t)kind << 62) | ((uint64_t)(part < 0 ? 0 : part & 0xffff) << 46) | ((rank & 0xffffffffull) << 14) |
+         (sub & 0x3fff);
+}
 
 }  // namespace
 
@@ -279,105 +308,204 @@ struct Out {
 // that order in key_heap / val_heap.  Returns the record count, or -1 when a heap or rec is too
 // small (need[0] = records, need[1] = key bytes, need[2] = value bytes: call again with those).
 // Duplicates are dropped (dedup).  payloads_out = payloads looked at.
-static int64_t route_hits(const uint8_t* raw, std::vector<std::pair<uint64_t, uint8_t>>& hit, const char* source_id,
+static void route_one(Worker& wk, uint32_t wid, const uint8_t* raw, uint32_t s, uint32_t e, uint8_t st,
+                      uint64_t rank, const Str& source, const int32_t* parts) {
+  Parsed& p = wk.p;
+  p.cmd = 0;
+  p.originator = p.token = p.alt = p.type = p.message = p.dtype = p.area = Str();
+  p.has_lat = p.has_lon = p.has_elev = p.has_date = p.us = p.has_us = false;
+  p.lat = p.lon = p.elev = 0;
+  p.date = 0;
+  p.mx.clear();
+  p.meta.clear();
+  auto emit = [&](int kind, const Str& key, const uint8_t* v, size_t vn, uint64_t sub, bool in_arena) {
+    RecRef r;
+    const int32_t part = key.n ? sw_partition_for_key(key.p, (int32_t)key.n, parts[kind] > 0 ? parts[kind] : 1) : -1;
+    r.order = order_of(kind, part, rank, sub);
+    r.key = key.p;
+    r.klen = key.n;
+    r.worker = wid;
+    if (in_arena) {
+      r.voff = (uint64_t)(v - wk.arena.data());
+    } else {                                  // raw payload bytes: copy into the arena
+      r.voff = wk.arena.size();
+      wk.arena.raw(v, vn);
+    }
+    r.vlen = vn;
+    wk.recs.push_back(r);
+  };
+  const bool ok = parse(raw, s, e, &p);
+  if (!ok || st == 4) {
+    emit(RK_FAILED, Str(), raw + s, e - s, 0, false);
+    return;
+  }
+  const size_t v0 = wk.arena.size();
+  if (p.cmd == SW_CMD_SEND_REGISTRATION) {
+    W& reg = wk.reg;
+    reg.clear();
+    if (p.dtype.n) reg.opt_str(1, p.dtype);
+    if (p.area.n) reg.opt_str(3, p.area);
+    map_entries(reg, 4, p.meta);
+    W& w = wk.arena;                           // GDeviceRegistationPayload
+    if (source.n) w.str(1, source);
+    w.str(2, p.token);
+    if (p.originator.has) w.opt_str(3, p.originator);
+    if (reg.size()) w.sub(4, reg);
+    emit(RK_REGISTRATION, p.token, w.data() + v0, w.size() - v0, 0, true);
+  } else if (p.cmd == SW_CMD_SEND_DEVICE_MEASUREMENTS) {
+    const size_t n = p.mx.size();
+    for (size_t i = 0; i < n; ++i) {
+      Str alt = p.alt;
+      if (alt.has && n > 1) {                // ProtobufDecoder: "<alternateId>:<index>" per measurement
+        wk.alt.assign((const char*)alt.p, alt.n);
+        wk.alt += ':';
+        wk.alt += std::to_string(i);
+        alt.p = (const uint8_t*)wk.alt.data();
+        alt.n = (uint32_t)wk.alt.size();
+      }
+      event_header(wk.h, p, alt);
+      W& m = wk.m;                            // GDeviceMeasurementCreateRequest
+      m.clear();
+      if (p.mx[i].name.n) m.str(1, p.mx[i].name);
+      uint64_t u;
+      memcpy(&u, &p.mx[i].value, 8);
+      if (u) m.dbl(2, p.mx[i].value);
+      m.sub(3, wk.h);
+      const size_t a = wk.arena.size();
+      inbound(wk.arena, source, p, 1, m);
+      emit(RK_UNREGISTERED, p.token, wk.arena.data() + a, wk.arena.size() - a, i, true);
+    }
+  } else if (p.cmd == SW_CMD_SEND_DEVICE_LOCATION) {
+    event_header(wk.h, p, p.alt);
+    W& m = wk.m;                              // GDeviceLocationCreateRequest
+    m.clear();
+    m.opt_dbl(1, p.lat);
+    m.opt_dbl(2, p.lon);
+    if (p.has_elev) m.opt_dbl(3, p.elev);
+    m.sub(4, wk.h);
+    inbound(wk.arena, source, p, 3, m);
+    emit(RK_UNREGISTERED, p.token, wk.arena.data() + v0, wk.arena.size() - v0, 0, true);
+  } else if (p.cmd == SW_CMD_SEND_DEVICE_ALERT) {
+    event_header(wk.h, p, p.alt);
+    W& m = wk.m;                              // GDeviceAlertCreateRequest (source Device, level Info)
+    m.clear();
+    if (p.type.n) m.str(3, p.type);
+    if (p.message.n) m.str(4, p.message);
+    m.sub(5, wk.h);
+    inbound(wk.arena, source, p, 2, m);
+    emit(RK_UNREGISTERED, p.token, wk.arena.data() + v0, wk.arena.size() - v0, 0, true);
+  } else {
+    emit(RK_CONTROL, p.token, raw + s, e - s, 0, false);
+  }
+}
+
+// Route the rejected messages of one raw batch (see the entry points below for the inputs).
+// Output: records grouped by (kind, partition) -- within a group in batch order, so per-key order
+// is preserved -- with rec[i] = (kind, partition, key length, value length) and the keys / values
+// concatenated in that order in key_heap / val_heap.  Returns the record count, or -1 when a heap or
+// rec is too small (need[0] = records, need[1] = key bytes, need[2] = value bytes: call again with
+// those).  Payloads are parsed on up to 8 threads; duplicates never get here (dedup drops them).
+struct Hit {
+  uint64_t key;            // payload start << 32 | end in the batch: order and identity
+  uint32_t ps, pe;         // where its bytes are in `raw` (the batch, or a compact copy)
+  uint8_t st;
+  bool operator<(const Hit& o) const { return key < o.key; }
+};
+
+static int64_t route_hits(const uint8_t* raw, std::vector<Hit>& hit, const char* source_id,
                           const int32_t* parts, int32_t* rec, int64_t rec_cap, uint8_t* key_heap, int64_t key_cap,
                           uint8_t* val_heap, int64_t val_cap, int64_t* need, int64_t* payloads_out) {
-  // hit: ((start << 32 | end), status), one per affected payload after the dedupe below
+  // one hit per affected payload after the dedupe below; sorted by batch position, so a payload's
+  // rank in `hit` is its batch order
   std::sort(hit.begin(), hit.end());
-  hit.erase(std::unique(hit.begin(), hit.end(),
-                        [](const std::pair<uint64_t, uint8_t>& a, const std::pair<uint64_t, uint8_t>& b) {
-                          return a.first == b.first;
-                        }),
+  hit.erase(std::unique(hit.begin(), hit.end(), [](const Hit& a, const Hit& b) { return a.key == b.key; }),
             hit.end());
-  Out o;
-  for (int k = 0; k < 4; ++k) o.parts[k] = parts[k];
+  if (payloads_out) *payloads_out = (int64_t)hit.size();
   Str source;
   source.p = (const uint8_t*)source_id;
   source.n = (uint32_t)strlen(source_id);
-  for (const auto& h : hit) {
-    const uint32_t s = (uint32_t)(h.first >> 32), e = (uint32_t)h.first;
-    Parsed p;
-    const bool ok = parse(raw, s, e, &p);
-    if (!ok || h.second == 4) {
-      Str none;
-      o.emit(RK_FAILED, none, raw + s, e - s);
-      continue;
+  const size_t nh = hit.size();
+  static const int max_t = getenv("SW_ROUTE_THREADS") ? std::max(1, atoi(getenv("SW_ROUTE_THREADS"))) : 8;
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)max_t, nh / 512));
+  static thread_local std::vector<Worker> tl_workers;
+  std::vector<Worker>& workers = tl_workers;   // the caller's: worker threads must not see their own
+  if ((int)workers.size() < T) workers.resize((size_t)T);
+  auto work = [&workers, &hit, nh, T, raw, &source, parts](int t) {
+    Worker& wk = workers[(size_t)t];
+    wk.arena.clear();
+    wk.recs.clear();
+    const size_t a = nh * (size_t)t / (size_t)T, b = nh * (size_t)(t + 1) / (size_t)T;
+    // payloads are scattered over the batch: prefetch a few ahead so their misses overlap
+    constexpr size_t AHEAD = 16;
+    for (size_t i = a; i < b && i < a + AHEAD; ++i) {
+      __builtin_prefetch(raw + hit[i].ps);
+      __builtin_prefetch(raw + hit[i].ps + 64);
     }
-    if (p.cmd == SW_CMD_SEND_REGISTRATION) {
-      W reg;
-      if (p.dtype.n) reg.bytes(1, opt_str(p.dtype));
-      if (p.area.n) reg.bytes(3, opt_str(p.area));
-      map_entries(reg, 4, p.meta);
-      W w;                                  // GDeviceRegistationPayload
-      if (source.n) w.str(1, source);
-      w.str(2, p.token);
-      if (p.originator.has) w.bytes(3, opt_str(p.originator));
-      if (!reg.b.empty()) w.bytes(4, reg.b);
-      o.emit(RK_REGISTRATION, p.token, w.b.data(), (int64_t)w.b.size());
-    } else if (p.cmd == SW_CMD_SEND_DEVICE_MEASUREMENTS) {
-      const size_t n = p.mx.size();
-      for (size_t i = 0; i < n; ++i) {
-        Str alt = p.alt;
-        std::string suffixed;
-        if (alt.has && n > 1) {            // ProtobufDecoder: "<alternateId>:<index>" per measurement
-          suffixed.assign((const char*)alt.p, alt.n);
-          suffixed += ":" + std::to_string(i);
-          alt.p = (const uint8_t*)suffixed.data();
-          alt.n = (uint32_t)suffixed.size();
-        }
-        W m;                                // GDeviceMeasurementCreateRequest
-        if (p.mx[i].name.n) m.str(1, p.mx[i].name);
-        uint64_t u;
-        memcpy(&u, &p.mx[i].value, 8);
-        if (u) m.dbl(2, p.mx[i].value);
-        m.bytes(3, event_header(p, alt));
-        const std::vector<uint8_t> v = inbound(source, p, 1, m.b);
-        o.emit(RK_UNREGISTERED, p.token, v.data(), (int64_t)v.size());
+    for (size_t i = a; i < b; ++i) {
+      if (i + AHEAD < b) {
+        const uint8_t* q = raw + hit[i + AHEAD].ps;
+        __builtin_prefetch(q);
+        __builtin_prefetch(q + 64);
       }
-    } else if (p.cmd == SW_CMD_SEND_DEVICE_LOCATION) {
-      W m;                                  // GDeviceLocationCreateRequest
-      m.bytes(1, opt_dbl(p.lat));
-      m.bytes(2, opt_dbl(p.lon));
-      if (p.has_elev) m.bytes(3, opt_dbl(p.elev));
-      m.bytes(4, event_header(p, p.alt));
-      const std::vector<uint8_t> v = inbound(source, p, 3, m.b);
-      o.emit(RK_UNREGISTERED, p.token, v.data(), (int64_t)v.size());
-    } else if (p.cmd == SW_CMD_SEND_DEVICE_ALERT) {
-      W m;                                  // GDeviceAlertCreateRequest (source Device, level Info)
-      if (p.type.n) m.str(3, p.type);
-      if (p.message.n) m.str(4, p.message);
-      m.bytes(5, event_header(p, p.alt));
-      const std::vector<uint8_t> v = inbound(source, p, 2, m.b);
-      o.emit(RK_UNREGISTERED, p.token, v.data(), (int64_t)v.size());
-    } else {
-      o.emit(RK_CONTROL, p.token, raw + s, e - s);
+      route_one(wk, (uint32_t)t, raw, hit[i].ps, hit[i].pe, hit[i].st, i, source, parts);
     }
+  };
+  if (T == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
   }
-  if (payloads_out) *payloads_out = (int64_t)hit.size();
-  std::stable_sort(o.recs.begin(), o.recs.end(), [](const Rec& a, const Rec& b) {
-    return a.kind != b.kind ? a.kind < b.kind : a.part < b.part;
-  });
-  int64_t kb = 0, vb = 0;
-  for (const Rec& r : o.recs) {
-    kb += (int64_t)r.key.size();
-    vb += (int64_t)r.val.size();
-  }
-  const int64_t n = (int64_t)o.recs.size();
+  // stable counting sort into (kind, partition) groups: workers hold consecutive hit ranges and
+  // emit in hit order, so walking them in order is batch order
+  int32_t pmax = 1;
+  for (int k = 0; k < 4; ++k) pmax = std::max(pmax, parts[k]);
+  const size_t nb = (size_t)4 * (size_t)pmax;
+  std::vector<int64_t> cnt(nb + 1, 0), kbytes(nb + 1, 0), vbytes(nb + 1, 0);
+  auto bucket = [pmax](const RecRef& r) {
+    const int kind = (int)(r.order >> 62);
+    const int32_t part = r.klen ? (int32_t)((r.order >> 46) & 0xffff) : 0;
+    return (size_t)kind * (size_t)pmax + (size_t)std::min(part, pmax - 1);
+  };
+  int64_t n = 0, kb = 0, vb = 0;
+  for (int t = 0; t < T; ++t)
+    for (const RecRef& r : workers[(size_t)t].recs) {
+      const size_t bk = bucket(r);
+      ++cnt[bk + 1];
+      kbytes[bk + 1] += r.klen;
+      vbytes[bk + 1] += (int64_t)r.vlen;
+      ++n;
+      kb += r.klen;
+      vb += (int64_t)r.vlen;
+    }
   need[0] = n;
   need[1] = kb;
   need[2] = vb;
   if (n > rec_cap || kb > key_cap || vb > val_cap) return -1;
-  int64_t ko = 0, vo = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const Rec& r = o.recs[(size_t)i];
-    rec[4 * i] = r.kind;
-    rec[4 * i + 1] = r.part;
-    rec[4 * i + 2] = (int32_t)r.key.size();
-    rec[4 * i + 3] = (int32_t)r.val.size();
-    if (!r.key.empty()) memcpy(key_heap + ko, r.key.data(), r.key.size());
-    if (!r.val.empty()) memcpy(val_heap + vo, r.val.data(), r.val.size());
-    ko += (int64_t)r.key.size();
-    vo += (int64_t)r.val.size();
+  for (size_t b = 0; b < nb; ++b) {
+    cnt[b + 1] += cnt[b];
+    kbytes[b + 1] += kbytes[b];
+    vbytes[b + 1] += vbytes[b];
+  }
+  // every record's slot and byte offsets: a prefix within its bucket
+  std::vector<int64_t> ri(cnt.begin(), cnt.end() - 1), ko(kbytes.begin(), kbytes.end() - 1),
+      vo(vbytes.begin(), vbytes.end() - 1);
+  for (int t = 0; t < T; ++t) {
+    const Worker& wk = workers[(size_t)t];
+    for (const RecRef& r : wk.recs) {
+      const size_t bk = bucket(r);
+      const int64_t i = ri[bk]++;
+      rec[4 * i] = (int32_t)(r.order >> 62);
+      rec[4 * i + 1] = r.klen ? (int32_t)((r.order >> 46) & 0xffff) : -1;
+      rec[4 * i + 2] = (int32_t)r.klen;
+      rec[4 * i + 3] = (int32_t)r.vlen;
+      if (r.klen) memcpy(key_heap + ko[bk], r.key, r.klen);
+      memcpy(val_heap + vo[bk], wk.arena.data() + r.voff, r.vlen);
+      ko[bk] += r.klen;
+      vo[bk] += (int64_t)r.vlen;
+    }
   }
   return n;
 }
@@ -389,7 +517,7 @@ int64_t sw_route_rejects(const uint8_t* raw, const uint32_t* offs, int64_t n_msg
                          const uint8_t* rej_st, int64_t n_rej, const char* source_id, const int32_t* parts,
                          int32_t* rec, int64_t rec_cap, uint8_t* key_heap, int64_t key_cap, uint8_t* val_heap,
                          int64_t val_cap, int64_t* need, int64_t* payloads_out) {
-  std::vector<std::pair<uint64_t, uint8_t>> hit;
+  std::vector<Hit> hit;
   hit.reserve((size_t)n_rej);
   for (int64_t i = 0; i < n_rej; ++i) {
     const uint8_t st = rej_st[i];
@@ -397,25 +525,48 @@ int64_t sw_route_rejects(const uint8_t* raw, const uint32_t* offs, int64_t n_msg
     const uint32_t* it = std::upper_bound(offs, offs + n_msgs + 1, rej_off[i]);
     const int64_t m = (int64_t)(it - offs) - 1;
     if (m < 0 || m >= n_msgs) continue;
-    hit.push_back({((uint64_t)offs[m] << 32) | offs[m + 1], st});
+    hit.push_back({((uint64_t)offs[m] << 32) | offs[m + 1], offs[m], offs[m + 1], st});
   }
   return route_hits(raw, hit, source_id, parts, rec, rec_cap, key_heap, key_cap, val_heap, val_cap, need,
                     payloads_out);
 }
 
-// refs: n x (payload start, payload end, status | src_rank << 8) as the MI355X step snapshot them
-// (k_reject_refs); only refs whose src_rank == rank are routed (their bytes are in `raw`).
-int64_t sw_route_refs(const uint8_t* raw, const uint32_t* refs, int64_t n, int32_t rank, const char* source_id,
-                      const int32_t* parts, int32_t* rec, int64_t rec_cap, uint8_t* key_heap, int64_t key_cap,
-                      uint8_t* val_heap, int64_t val_cap, int64_t* need, int64_t* payloads_out) {
-  std::vector<std::pair<uint64_t, uint8_t>> hit;
+// refs: n x (payload start, payload end, status | src_rank << 8, copy offset) as the MI355X step
+// snapshot them (k_reject_refs).  Payloads are parsed from `compact` at their copy offset, or from
+// the raw batch `raw` (may be null) when the copy did not fit (offset ~0).  Only refs whose
+// src_rank == rank are routed.
+int64_t sw_route_refs(const uint8_t* compact, const uint8_t* raw, const uint32_t* refs, int64_t n, int32_t rank,
+                      const char* source_id, const int32_t* parts, int32_t* rec, int64_t rec_cap, uint8_t* key_heap,
+                      int64_t key_cap, uint8_t* val_heap, int64_t val_cap, int64_t* need, int64_t* payloads_out) {
+  std::vector<Hit> hit, spill;
   hit.reserve((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
-    const uint32_t s = refs[3 * i], e = refs[3 * i + 1], st = refs[3 * i + 2] & 0xff, src = refs[3 * i + 2] >> 8;
+    const uint32_t s = refs[4 * i], e = refs[4 * i + 1], st = refs[4 * i + 2] & 0xff, src = refs[4 * i + 2] >> 8;
+    const uint32_t c = refs[4 * i + 3];
     if (st == 3 || st == 0 || (int32_t)src != rank || e <= s) continue;
-    hit.push_back({((uint64_t)s << 32) | e, (uint8_t)st});
+    if (c != 0xffffffffu) hit.push_back({((uint64_t)s << 32) | e, c, c + (e - s), (uint8_t)st});
+    else spill.push_back({((uint64_t)s << 32) | e, s, e, (uint8_t)st});
   }
-  return route_hits(raw, hit, source_id, parts, rec, rec_cap, key_heap, key_cap, val_heap, val_cap, need,
+  if (spill.empty() || !raw)
+    return route_hits(compact, hit, source_id, parts, rec, rec_cap, key_heap, key_cap, val_heap, val_cap, need,
+                      payloads_out);
+  // rare: the compact buffer overflowed -- those payloads come from the raw batch (routed with the
+  // raw base; all offsets rebased onto it by copying the compact ones there is not possible, so
+  // the two sets are routed in one pass over a merged view: copies first, then the raw spill)
+  std::vector<uint8_t> merged;
+  size_t total = 0;
+  for (const Hit& h : hit) total = std::max<size_t>(total, h.pe);
+  merged.resize(total + 64);
+  if (total) memcpy(merged.data(), compact, total);
+  for (Hit& h : spill) {
+    const size_t at = merged.size();
+    merged.insert(merged.end(), raw + h.ps, raw + h.pe);
+    h.pe = (uint32_t)(at + (h.pe - h.ps));
+    h.ps = (uint32_t)at;
+    hit.push_back(h);
+  }
+  merged.resize(merged.size() + 64);
+  return route_hits(merged.data(), hit, source_id, parts, rec, rec_cap, key_heap, key_cap, val_heap, val_cap, need,
                     payloads_out);
 }
 

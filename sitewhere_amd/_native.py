@@ -127,6 +127,7 @@ def native():
         _proto(lib, "sw_gen_payloads", c_int64, c_int64, c_char_p, c_int64, c_double, c_double, c_double, c_int32,
                c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, P, c_int64, P)
         _proto(lib, "sw_gen_tokens", c_int64, c_char_p, c_int64, c_int64, P, c_int64, P)
+        _proto(lib, "sw_stamp_alt_epoch", c_int64, P, P, c_int64, c_uint64, c_int32)
         _proto(lib, "swlog_open", P, c_char_p, c_int32)
         _proto(lib, "swlog_close", None, P)
         _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)
@@ -153,6 +154,10 @@ def native():
         for kind in ("dedup", "intern", "seen", "ms"):
             _proto(lib, f"swce_{kind}_size", c_int64, P)
         _proto(lib, "swce_dedup_export", c_int64, P, P, P)
+        _proto(lib, "swce_dedup_window", None, P, c_int64, c_int64)
+        _proto(lib, "swce_dedup_prev_size", c_int64, P)
+        _proto(lib, "swce_dedup_prev_export", c_int64, P, P, P)
+        _proto(lib, "swce_dedup_prev_import", None, P, P, P, c_int64)
         _proto(lib, "swce_dedup_import", None, P, P, P, c_int64)
         _proto(lib, "swce_intern_export", c_int64, P, P, P)
         _proto(lib, "swce_intern_import", None, P, P, P, c_int64)
@@ -178,7 +183,7 @@ def native():
         _proto(lib, "swss_file", c_int32, P, c_int32, c_char_p, c_int32)
         _proto(lib, "sw_route_rejects", c_int64, P, P, c_int64, P, P, c_int64, c_char_p, P, P, c_int64, P,
                c_int64, P, c_int64, P, P)
-        _proto(lib, "sw_route_refs", c_int64, P, P, c_int64, c_int32, c_char_p, P, P, c_int64, P, c_int64, P,
+        _proto(lib, "sw_route_refs", c_int64, P, P, P, c_int64, c_int32, c_char_p, P, P, c_int64, P, c_int64, P,
                c_int64, P, P)
         _native = lib
         return lib
@@ -258,6 +263,8 @@ def gpu():
         _proto(lib, "sw_graph_destroy", c_int32, P)
         _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
         _proto(lib, "sw_seg_encode", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
+        _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
+        _proto(lib, "sw_step_snapshot", c_int32, P, P, P, c_int32, P, P)
         _gpu = lib
         return lib
 

@@ -107,7 +107,7 @@ ZONE_TEST = np.dtype([("zone", "<i4"), ("condition", "<i4"), ("alert_name_id", "
 STAT_NAMES = [
     "messages", "events", "persisted", "unregistered", "unassigned", "duplicates", "decode_errors",
     "control", "rule_alerts", "presence_events", "shuffle_overflow", "new_names", "state_overflow",
-    "shuffle_deferred",
+    "shuffle_deferred", "dedup_overflow", "dedup_rotations",
 ]
 
 # Alert levels (GAlertLevel) and sources.

@@ -56,6 +56,7 @@ FIELDS = [
     ("n_zone_vtx", I),
     # state merge scratch
     ("ev_slot", P),
+    ("dd_meta", P),
 ]
 
 

@@ -265,25 +265,44 @@ class DurableBlockSink:
         if self.bus is not None:
             self.bus.reclaim()
 
-    def target(self, nbytes: int):
-        """(host address, buffer) for a block of ``nbytes`` (the copy engine writes it there)."""
+    def target(self, nbytes: int, timeout_s: float = 60.0):
+        """(host address, buffer) for a block of ``nbytes`` (the copy engine writes it there).  When
+        every buffer is in use the caller waits for the disk (backpressure), never for more memory
+        than ``max_buffers`` buffers."""
+        import time as _time
         need = -(-int(nbytes) // SEG_ALIGN) * SEG_ALIGN
-        self._reap()
-        with self._lock:
-            for i, b in enumerate(self.free):
-                if b.nbytes >= need:
-                    b = self.free.pop(i)
-                    b.refs = 1
-                    return b.host, b
-        if self.n_alloc >= self.max_buffers:
-            self.store.seg.wait(self.pending[0].token if self.pending else self.store.seg.last_token)
-            return self.target(nbytes)
-        # sized with headroom: steps of one engine produce blocks of about the same size
-        self._size = max(self._size, need + need // 2)
-        self.n_alloc += 1
-        b = _BlockBuf(self._HostBuffer(self.lib, self._size))
-        b.refs = 1
-        return b.host, b
+        deadline = _time.monotonic() + timeout_s
+        while True:
+            self._reap()
+            with self._lock:
+                for i, b in enumerate(self.free):
+                    if b.nbytes >= need:
+                        b = self.free.pop(i)
+                        b.refs = 1
+                        return b.host, b
+                small = self.free.pop(0) if self.free else None
+            # buffers only the topic still references are bounded by its retention (bytes), not by
+            # the disk: those never count against max_buffers (a reader window of small blocks
+            # would otherwise starve the pool, as retention only runs on the next append)
+            topic_only = self.n_alloc - len(self.free) - len(self.pending) - 1
+            if small is not None or self.n_alloc - max(0, topic_only) < self.max_buffers:
+                if small is not None:           # too small for this block: replace it
+                    self.n_alloc -= 1
+                    del small
+                # sized with headroom: steps of one engine produce blocks of about the same size
+                self._size = max(self._size, need + need // 2)
+                self.n_alloc += 1
+                b = _BlockBuf(self._HostBuffer(self.lib, self._size))
+                b.refs = 1
+                return b.host, b
+            if _time.monotonic() > deadline:
+                raise RuntimeError(f"durable block buffers exhausted ({self.n_alloc} allocated, {len(self.pending)} "
+                                   f"waiting for the disk, durable token {self.store.seg.durable()} of "
+                                   f"{self.store.seg.last_token}, store {self.store.seg.stats()})")
+            if self.pending:
+                self.store.seg.wait(self.pending[0].token, 1.0)
+            else:
+                _time.sleep(0.001)              # only the topic holds buffers: wait for its retention
 
     def publish(self, b: _BlockBuf, nbytes: int, first_seq: int, now_ms: int, tag=None) -> int:
         """The block is in ``b``: zero its padding, seal it, queue it to the store, publish it."""

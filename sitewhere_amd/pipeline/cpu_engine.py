@@ -49,7 +49,8 @@ class CpuInboundEngine(EngineBase):
         self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
         self.cursor = 0
         self.seq_base = 0
-        self.dedup: dict[int, int] = {}
+        self.dedup: dict[int, int] = {}          # current generation of the alternate-id window
+        self.dedup_prev: dict[int, int] = {}     # previous generation
         self.intern: dict[int, int] = {}
         self.st_last = np.zeros(cfg.max_assignments, np.uint64)
         self.st_missing = np.zeros(cfg.max_assignments, np.uint64)
@@ -131,19 +132,24 @@ class CpuInboundEngine(EngineBase):
         return status, dev, asg
 
     def _dedup(self, recs, status):
-        seen_now: dict[int, int] = {}
+        """Generational window, the oracle of k_dedup_rotate / k_dedup_insert / k_dedup_check: ids of
+        the previous generation are duplicates; otherwise the first occurrence in the current
+        generation wins.  Before a batch that could push the current generation past half the
+        window's slots, the generations rotate and the oldest is forgotten."""
+        if len(self.dedup) + self.cfg.rec_cap > self.cfg.dedup_slots // 2:
+            self.dedup_prev = self.dedup
+            self.dedup = {}
+            self.stats[15] += 1
+        prev = self.dedup_prev
+        cur = self.dedup
         for i in range(len(recs)):
             h = int(recs[i]["alt_hash"])
             if h == 0 or status[i] != ST_OK:
                 continue
-            seq = self.seq_base + i
-            if h in self.dedup and self.dedup[h] < self.seq_base:
-                status[i] = ST_DUPLICATE
-            elif h in seen_now:
+            if h in prev or h in cur:
                 status[i] = ST_DUPLICATE
             else:
-                seen_now[h] = seq
-        self.dedup.update(seen_now)
+                cur[h] = self.seq_base + i
 
     def _intern_id(self, h: int) -> int:
         if h not in self.intern:
@@ -304,6 +310,8 @@ class CpuInboundEngine(EngineBase):
             "scalars": np.array([self.cursor, self.seq_base], np.int64),
             "stats": self.stats.copy(),
             "dedup_key": u64(self.dedup.keys()), "dedup_seq": np.array(list(self.dedup.values()), np.int64),
+            "dedup_prev_key": u64(self.dedup_prev.keys()),
+            "dedup_prev_seq": np.array(list(self.dedup_prev.values()), np.int64),
             "intern_key": u64(self.intern.keys()), "intern_id": np.array(list(self.intern.values()), np.int64),
             "seen": u64(self._seen),
             "st_last": self.st_last, "st_missing": self.st_missing, "st_loc_date": self.st_loc_date,
@@ -320,6 +328,8 @@ class CpuInboundEngine(EngineBase):
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
         self.stats[:] = a["stats"]
         self.dedup = dict(zip((int(x) for x in a["dedup_key"]), (int(x) for x in a["dedup_seq"])))
+        self.dedup_prev = dict(zip((int(x) for x in a.get("dedup_prev_key", [])),
+                                   (int(x) for x in a.get("dedup_prev_seq", []))))
         self.intern = dict(zip((int(x) for x in a["intern_key"]), (int(x) for x in a["intern_id"])))
         self._seen = {int(x) for x in a["seen"]}
         for k in ("st_last", "st_missing", "st_loc_date", "st_loc_eid"):
@@ -369,6 +379,10 @@ class CpuInboundEngine(EngineBase):
         page = rows[order[lo:hi]]
         cols = {k: v[page] for k, v in s.items()}
         return len(rows), cols, seq[order[lo:hi]] * self.world + self.rank
+
+    def intern_table(self) -> dict:
+        """name hash -> dense name id (same form as the GPU and native engines)."""
+        return dict(self.intern)
 
     def store_rows(self):
         n = min(self.cursor, self.cfg.store_cap)

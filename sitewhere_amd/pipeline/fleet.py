@@ -93,7 +93,7 @@ def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndar
                  offs: np.ndarray | None = None):
     """Generate ``n_msgs`` encoded payloads. Returns (raw uint8[nbytes], offs uint32[n+1])."""
     lib = native()
-    per = 48 + len(spec.prefix) + 10 + spec.mx_per_msg * 32 + (40 if spec.with_alternate_id else 0)
+    per = 48 + len(spec.prefix) + 10 + spec.mx_per_msg * 32 + (48 if spec.with_alternate_id else 0)
     cap = n_msgs * per + 64
     if out is None or out.nbytes < cap:
         out = np.empty(cap, np.uint8)
@@ -163,6 +163,16 @@ def cpu_decode(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, ca
     offs = np.ascontiguousarray(offs, np.uint32)
     n = lib.sw_cpu_decode(_ptr(raw) if raw.size else 0, _ptr(offs), n_msgs, now_ms, rank, _ptr(out), cap, threads)
     return out[:n]
+
+
+def stamp_alt_epoch(raw, offs: np.ndarray, epoch: int, threads: int = 8) -> int:
+    """Give a generated batch fresh alternate ids in place (a producer replaying pre-generated
+    payloads): the 16-hex-digit epoch of every fixed-width id (``sw_gen_payloads``) becomes
+    ``epoch``.  ``raw`` is a numpy array or a host address.  Returns the payloads stamped."""
+    offs = np.ascontiguousarray(offs, np.uint32)
+    ptr = raw if isinstance(raw, int) else raw.ctypes.data
+    return int(native().sw_stamp_alt_epoch(ptr, offs.ctypes.data, len(offs) - 1, int(epoch) & (2 ** 64 - 1),
+                                           int(threads)))
 
 
 def pack_messages(messages):

@@ -154,8 +154,9 @@ class GpuInboundEngine(EngineBase):
         t["asg_ctx"] = full(c.max_assignments * 4, -1, i32)
         t["asg_active"] = z(c.max_assignments, u8)
         # dedup window
-        t["dd_key"] = z(c.dedup_slots, i64)
-        t["dd_seq"] = full(c.dedup_slots, -1, i64)
+        t["dd_key"] = z(2 * c.dedup_slots, i64)            # two generations (see k_dedup_rotate)
+        t["dd_seq"] = full(2 * c.dedup_slots, -1, i64)
+        t["dd_meta"] = z(4, i64)
         t["seq_base"] = z(1, i64)
         # names intern
         t["nm_key"] = z(c.name_slots, i64)
@@ -215,6 +216,7 @@ class GpuInboundEngine(EngineBase):
         a.reg, a.reg_mask = _ptr(t["reg"]), c.reg_slots - 1
         a.asg_ctx, a.asg_active, a.n_asg = _ptr(t["asg_ctx"]), _ptr(t["asg_active"]), c.max_assignments
         a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_key"]), _ptr(t["dd_seq"]), c.dedup_slots - 1, _ptr(t["seq_base"])
+        a.dd_meta = _ptr(t["dd_meta"])
         a.nm_key, a.nm_id, a.nm_first = _ptr(t["nm_key"]), _ptr(t["nm_id"]), _ptr(t["nm_first"])
         a.nm_mask, a.nm_counter = c.name_slots - 1, _ptr(t["nm_counter"])
         a.st, a.ms, a.ms_mask = _ptr(t["st"]), _ptr(t["ms"]), c.state_slots - 1
@@ -819,6 +821,41 @@ class GpuInboundEngine(EngineBase):
             raise RuntimeError(f"sw_seg_encode failed ({rc})")
         return state[pages + 1:pages + 4]
 
+    REJECT_BYTES = 8 << 20          # compact copies of rejected payloads per step (beyond: host reads the record)
+
+    def reject_refs_async(self, slot: int, raw_dev: torch.Tensor, off_dev: torch.Tensor, n_msgs: int):
+        """Snapshot this step's routable rejects (duplicates dropped) for outbound slot ``slot``
+        (``k_reject_refs``, current stream): device counters ``[refs, bytes]`` and, written straight
+        into mapped pinned host memory, the refs ``(start, end, status | src_rank << 8, copy offset)``
+        and the compact copies of their payloads.  ``raw_dev`` / ``off_dev`` / ``n_msgs``: the batch
+        whose local events this step processed.  Returns (counters, host buffer); the refs start at
+        byte 0 of the host buffer, the copies at ``16 * rec_cap``."""
+        refs = self.__dict__.setdefault("_rej_refs", {})
+        bufs = refs.get(slot)
+        cap = self.cfg.rec_cap
+        if bufs is None:
+            bufs = refs[slot] = (torch.zeros(4, dtype=torch.int32, device=self.device),
+                                 HostBuffer(self.lib, 16 * cap + self.REJECT_BYTES))
+        cnt, hb = bufs
+        rc = self.lib.sw_reject_refs(ctypes.byref(self.args), ctypes.c_void_p(_ptr(raw_dev)),
+                                     ctypes.c_void_p(_ptr(off_dev)), int(n_msgs), ctypes.c_void_p(_ptr(cnt)),
+                                     ctypes.c_void_p(hb.dev), cap, ctypes.c_void_p(hb.dev + 16 * cap),
+                                     self.REJECT_BYTES, self._stream())
+        if rc:
+            raise RuntimeError(f"sw_reject_refs failed ({rc})")
+        return bufs
+
+    def reject_snapshot(self, slot: int, n_refs: int, n_bytes: int):
+        """(refs u32 [n, 4], compact payload bytes) of slot ``slot``'s snapshot (host views, valid
+        until the slot's next snapshot)."""
+        cnt, hb = self._rej_refs[slot]
+        cap = self.cfg.rec_cap
+        n_refs = min(int(n_refs), cap)
+        refs = hb.view(np.uint32, 4 * n_refs).reshape(-1, 4)
+        nb = min(int(n_bytes), self.REJECT_BYTES)
+        comp = hb._arr[16 * cap:16 * cap + max(1, nb)]
+        return refs, comp
+
     def block_device(self, slot: int) -> torch.Tensor:
         return self._seg_buffers(slot)[0]
 
@@ -945,7 +982,7 @@ class GpuInboundEngine(EngineBase):
 
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "gpu"
-    _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_key", "dd_seq", "seq_base", "nm_key", "nm_id", "nm_first",
+    _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_key", "dd_seq", "dd_meta", "seq_base", "nm_key", "nm_id", "nm_first",
                     "nm_counter", "seen_key", "st", "ms", "stats", "cursor")
 
     def checkpoint_state(self, include_store: bool = False) -> dict:
@@ -979,6 +1016,7 @@ class GpuInboundEngine(EngineBase):
     def reset_dedup(self):
         self.t["dd_key"].zero_()
         self.t["dd_seq"].fill_(-1)
+        self.t["dd_meta"].zero_()
 
 
 class PipelinedRunner:
@@ -1004,7 +1042,7 @@ class PipelinedRunner:
 
     def __init__(self, engine: GpuInboundEngine, max_raw_bytes: int, deliver_outbound: bool = True,
                  on_outbound=None, mode: str | None = None, push_blocks: int = 128, nbuf: int = 3,
-                 out_target=None, block_sink=None):
+                 out_target=None, block_sink=None, on_rejects=None):
         """``out_target(n_bytes) -> (host address, token)`` (copy-engine modes): where each step's rows
         land, e.g. a pinned buffer a bus topic then publishes in place; ``on_outbound(token, n_rows)``
         is called once they are there.  Without it rows land in the engine's outbound ring and
@@ -1032,7 +1070,6 @@ class PipelinedRunner:
         self.off = [torch.empty(engine.cfg.max_msgs + 1, dtype=torch.int32, device=dev) for _ in range(nb)]
         self.lens = [torch.empty(5 * engine.cfg.max_msgs + 64, dtype=torch.uint8, device=dev) for _ in range(nb)]
         self.nout = [torch.zeros(4, dtype=torch.int32, device=dev) for _ in range(nb)]
-        self.scal_host = torch.zeros(nb, 16, dtype=torch.int32, pin_memory=True)
         self.ev_h2d = [torch.cuda.Event() for _ in range(nb)]
         self.ev_comp = [torch.cuda.Event() for _ in range(nb)]
         self.ev_push = [torch.cuda.Event() for _ in range(nb)]
@@ -1048,11 +1085,30 @@ class PipelinedRunner:
         if block_sink is not None:
             if self.mode != "hsa":
                 raise ValueError("durable blocks need the copy-engine outbound mode (hsa)")
-            self.seg_host = torch.zeros(nb, 4, dtype=torch.int64, pin_memory=True)
             self.btag = [None] * nb       # caller tag of the batch whose block slot b holds
             self.bnow = [0] * nb
             self._prev_tag = None
         self.bcopying = None              # (slot, signal, buffer, bytes, first_seq, now, tag)
+        # SW_RUNNER_TRACE=1: host wall-clock per phase (bench attribution)
+        self.trace = {} if os.environ.get("SW_RUNNER_TRACE") == "1" else None
+        # on_rejects(tag, refs u32 [n, 4], compact payload bytes): the slow path of each step
+        # (see reject_refs_async; refs whose copy offset is ~0 need the raw record named by tag)
+        self.on_rejects = on_rejects
+        self.rtag = [None] * nb
+        # per-slot end-of-step snapshot in mapped host memory (k_step_snapshot): scalars, encoder
+        # meta, reject counters -- read after the step's event, no copy calls
+        self.snap = [HostBuffer(engine.lib, 256) for _ in range(nb)]
+        # the slow path runs off the submit thread: the GPU writes the snapshot into mapped host
+        # memory, routing runs on one worker thread in batch order; rejects_floor() tells callers the
+        # oldest batch whose rejects are not routed yet (its input offset must not be committed)
+        if on_rejects is not None:
+            from collections import deque
+            from concurrent.futures import ThreadPoolExecutor
+            self.rej_pool = ThreadPoolExecutor(1, thread_name_prefix="reject-router")
+            self.rej_job = [None] * nb
+            self.rej_inflight = deque()           # (tag, future)
+        self._prev_batch = None           # rounds mode: (slot, n_msgs, tag) of the batch in flight
+        self.rejects_seen = 0
 
     def submit(self, raw_host: torch.Tensor | None, off_host: torch.Tensor | None, n_msgs: int,
                now_ms: int | None = None, presence: bool = False, lens_host: torch.Tensor | None = None,
@@ -1064,6 +1120,7 @@ class PipelinedRunner:
         which crosses PCIe in ~1 B per payload and is turned into offsets on the GPU."""
         k = self.k
         b = k % self.nbuf
+        t_sub = time.perf_counter()
         now_ms = int(time.time() * 1000) if now_ms is None else now_ms
         if raw_host is not None:
             nbytes = int(raw_host.numel())
@@ -1095,18 +1152,37 @@ class PipelinedRunner:
             self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
                               out_to_device=to_dev)
             self.produced[b] = True
-        if not self.produced[b]:
-            self.nout[b].zero_()
-        else:
-            self.nout[b].copy_(self.e.t["scalars"][7:11])    # snapshot n_out on the device (stream-ordered)
-        self.scal_host[b].copy_(self.e.t["scalars"][:16], non_blocking=True)
-        if self.block_sink is not None:
+        if self.mode == "push":
+            if not self.produced[b]:
+                self.nout[b].zero_()
+            else:
+                self.nout[b].copy_(self.e.t["scalars"][7:11])    # n_out on the device (stream-ordered)
+        rej_cnt = seg_meta = None
+        if self.on_rejects is not None:
+            self.rtag[b] = None
             # in rounds mode the round processes the batch submitted by the previous call
+            cur = (b, n_msgs, tag) if raw_host is not None else None
+            done = self._prev_batch if self.rounds else cur
+            if self.rounds:
+                self._prev_batch = cur
+            if self.produced[b] and done is not None:
+                if self.rej_job[b] is not None:
+                    self.rej_job[b].result()           # the router is done with slot b's host buffer
+                rej_cnt, _ = self.e.reject_refs_async(b, self.raw[done[0]], self.off[done[0]], done[1])
+                self.rtag[b] = done[2]
+        if self.block_sink is not None:
             done_tag = self._prev_tag if self.rounds else tag
             self._prev_tag = tag
             if self.produced[b]:
-                self.seg_host[b][:3].copy_(self.e.encode_block_async(b), non_blocking=True)
+                seg_meta = self.e.encode_block_async(b)
                 self.btag[b], self.bnow[b] = done_tag, self.e._step_now
+        rc = self.e.lib.sw_step_snapshot(ctypes.c_void_p(self.e.t["scalars"].data_ptr()),
+                                         ctypes.c_void_p(0 if seg_meta is None else seg_meta.data_ptr()),
+                                         ctypes.c_void_p(0 if rej_cnt is None else rej_cnt.data_ptr()),
+                                         int(self.produced[b]), ctypes.c_void_p(self.snap[b].dev),
+                                         ctypes.c_void_p(self.comp.cuda_stream))
+        if rc:
+            raise RuntimeError(f"sw_step_snapshot failed ({rc})")
         self.ev_comp[b].record(self.comp)
         if self.mode == "push" and self.deliver:
             with torch.cuda.stream(self.push):
@@ -1118,9 +1194,29 @@ class PipelinedRunner:
                 if rc:
                     raise RuntimeError(f"sw_push_out failed ({rc})")
                 self.ev_push[b].record(self.push)
+        self._t("enqueue", t_sub)
         self._drain()
         self.pending = b
         self.k += 1
+
+    def _rejects_async(self, pb: int, n_rej: int, n_bytes: int):
+        """Route slot pb's reject snapshot (already in mapped host memory) on the worker thread, in
+        batch order; the slot is not overwritten before the job is done (see submit)."""
+        if n_rej > self.e.cfg.rec_cap:
+            raise RuntimeError(f"reject snapshot overflow ({n_rej} refs > rec_cap)")
+        refs, comp = self.e.reject_snapshot(pb, n_rej, n_bytes)
+        tag = self.rtag[pb]
+        self.rejects_seen += n_rej
+        fut = self.rej_job[pb] = self.rej_pool.submit(self.on_rejects, tag, refs, comp)
+        self.rej_inflight.append((tag, fut))
+
+    def rejects_floor(self):
+        """Tag of the oldest batch whose rejects are still being routed (None when all are done);
+        routing failures surface here."""
+        q = getattr(self, "rej_inflight", None)
+        while q and q[0][1].done():
+            q.popleft()[1].result()
+        return q[0][0] if q else None
 
     def _deliver(self, b: int, n_out: int, token=None):
         if self.deliver and self.on_outbound is not None and n_out:
@@ -1144,10 +1240,13 @@ class PipelinedRunner:
         if self.bcopying is not None:
             _, sig, buf, nb, first, now, tag = self.bcopying
             self.bcopying = None
+            t0 = time.perf_counter()
             rc = self.e.lib.sw_sdma_wait(sig)
             if rc:
                 raise RuntimeError(f"sw_sdma_wait failed ({rc})")
+            t0 = self._t("block_copy_wait", t0)
             self.block_sink.publish(buf, nb, first, now, tag)
+            self._t("block_publish", t0)
 
     def _finish_rows(self):
         if self.copying is not None:
@@ -1161,21 +1260,37 @@ class PipelinedRunner:
             self._deliver(cb, cn, tok)
             self.copying = None
 
+    def _t(self, name, t0):
+        if self.trace is not None:
+            t1 = time.perf_counter()
+            self.trace[name] = self.trace.get(name, 0.0) + (t1 - t0)
+            return t1
+        return t0
+
     def _drain(self):
         if self.pending is None:
             return
         pb = self.pending
+        t0 = time.perf_counter()
         self.ev_comp[pb].synchronize()
+        t0 = self._t("wait_step", t0)
         if self.mode == "push" and self.deliver:
             self.ev_push[pb].synchronize()
-        n_out = int(self.scal_host[pb][7]) if self.produced[pb] else 0
+        snap = self.snap[pb].view(np.uint32, 32)
+        n_out = int(snap[7]) if self.produced[pb] else 0
         self.pending = None
+        if self.on_rejects is not None and self.produced[pb] and self.rtag[pb] is not None:
+            n_rej = int(snap[24])
+            if n_rej:
+                self._rejects_async(pb, n_rej, int(snap[25]))
+                t0 = self._t("rejects_enqueue", t0)
         if self.mode not in ("sdma", "hsa"):
             self._deliver(pb, n_out)
             return
         self._finish_copy()
+        t0 = self._t("finish_copy", t0)
         if self.block_sink is not None and self.produced[pb]:
-            nb, err, first = (int(x) for x in self.seg_host[pb][:3])
+            nb, err, first = (int(x) for x in self.snap[pb].view(np.uint64, 11)[8:11])
             if err or nb <= 0 or nb > self.e._seg_buffers(pb)[3]:
                 raise RuntimeError(f"durable block encoder failed (bytes={nb}, errors={err})")
             dst, buf = self.block_sink.target(nb)
@@ -1185,6 +1300,7 @@ class PipelinedRunner:
             if rc:
                 raise RuntimeError(f"sw_sdma_copy of the durable block failed ({rc})")
             self.bcopying = (pb, h.value, buf, nb, first, self.bnow[pb], self.btag[pb])
+            t0 = self._t("block_copy_start", t0)
         dst, tok = self._dest(pb, n_out) if self.deliver and n_out else (None, None)
         if self.mode == "hsa":
             sig = None
@@ -1221,7 +1337,10 @@ class PipelinedRunner:
         self._finish_copy()
         self.comp.synchronize()
         self.push.synchronize()
+        for _, fut in list(getattr(self, "rej_inflight", ())):
+            fut.result()                                  # every reject routed
+        self.rejects_floor()
 
     def outbound(self, b: int) -> np.ndarray:
-        n = int(self.scal_host[b][7]) if self.produced[b] else 0
+        n = int(self.snap[b].view(np.uint32, 32)[7]) if self.produced[b] else 0
         return self.e.out_host[b].view(OUT_REC, n)

@@ -86,6 +86,7 @@ class NativeCpuEngine(CpuInboundEngine):
         self._lib = native()
         self._h = self._lib.swce_create(self.threads)
         self._lib.swce_reserve(self._h, cfg.state_slots, cfg.dedup_slots)
+        self._lib.swce_dedup_window(self._h, cfg.dedup_slots, cfg.rec_cap)
         for v in self.store.values():      # touch the ring now (the GPU's HBM store is resident too)
             v.fill(0)
         self._out_pool: list = []       # recycled outbound buffers (see _out_buffer)
@@ -212,6 +213,10 @@ class NativeCpuEngine(CpuInboundEngine):
         dk, ds = np.zeros(nd, np.uint64), np.zeros(nd, np.int64)
         if nd:
             lib.swce_dedup_export(h, _ptr(dk), _ptr(ds))
+        npv = lib.swce_dedup_prev_size(h)
+        pk, ps = np.zeros(npv, np.uint64), np.zeros(npv, np.int64)
+        if npv:
+            lib.swce_dedup_prev_export(h, _ptr(pk), _ptr(ps))
         intern = self.intern_table()
         ns = lib.swce_seen_size(h)
         seen = np.zeros(ns, np.uint64)
@@ -221,7 +226,7 @@ class NativeCpuEngine(CpuInboundEngine):
         st = {
             "scalars": np.array([self.cursor, self.seq_base], np.int64),
             "stats": self.stats.copy(),
-            "dedup_key": dk, "dedup_seq": ds,
+            "dedup_key": dk, "dedup_seq": ds, "dedup_prev_key": pk, "dedup_prev_seq": ps,
             "intern_key": np.array(list(intern.keys()), np.uint64),
             "intern_id": np.array(list(intern.values()), np.int64),
             "seen": seen,
@@ -241,6 +246,9 @@ class NativeCpuEngine(CpuInboundEngine):
         dk = np.ascontiguousarray(a["dedup_key"], np.uint64)
         ds = np.ascontiguousarray(a["dedup_seq"], np.int64)
         lib.swce_dedup_import(h, _ptr(dk), _ptr(ds), len(dk))
+        pk = np.ascontiguousarray(a.get("dedup_prev_key", np.zeros(0, np.uint64)), np.uint64)
+        ps = np.ascontiguousarray(a.get("dedup_prev_seq", np.zeros(0, np.int64)), np.int64)
+        lib.swce_dedup_prev_import(h, _ptr(pk), _ptr(ps), len(pk))
         ik = np.ascontiguousarray(a["intern_key"], np.uint64)
         ii = np.ascontiguousarray(a["intern_id"], np.int32)
         lib.swce_intern_import(h, _ptr(ik), _ptr(ii), len(ik))

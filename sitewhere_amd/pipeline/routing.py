@@ -56,30 +56,49 @@ class RoutedRejects:
             yield bytes(self.keys[koff[i]:koff[i + 1]]), bytes(self.vals[voff[i]:voff[i + 1]])
 
 
-def route_rejects(raw: np.ndarray, offs: np.ndarray, rej_off: np.ndarray, rej_status: np.ndarray,
-                  source_id: str = "gpu-inbound", partitions=(1, 1, 1, 1)) -> RoutedRejects:
-    """``raw`` / ``offs``: the raw batch; ``rej_off`` / ``rej_status``: the step's reject records
-    (``EVENT_REC["aux_off"]``, engine status).  ``partitions``: partition counts of the
-    unregistered, registration, decoded and failed-decode topics."""
-    lib = native()
-    raw = np.ascontiguousarray(raw, np.uint8)
-    offs = np.ascontiguousarray(offs, np.uint32)
-    ro = np.ascontiguousarray(rej_off, np.uint32)
-    rs = np.ascontiguousarray(rej_status, np.uint8)
-    parts = np.asarray(partitions, np.int32)
+def _call(fn, args_head: tuple, n_rej: int) -> RoutedRejects:
     need = np.zeros(3, np.int64)
     npay = np.zeros(1, np.int64)
-    n_rej = len(ro)
     cap = (max(16, 4 * n_rej), max(1024, 64 * n_rej), max(4096, 256 * n_rej))
     for _ in range(2):
         rec = np.zeros((cap[0], 4), np.int32)
         keys = np.empty(cap[1], np.uint8)
         vals = np.empty(cap[2], np.uint8)
-        n = lib.sw_route_rejects(raw.ctypes.data, offs.ctypes.data, len(offs) - 1, ro.ctypes.data if n_rej else None,
-                                 rs.ctypes.data if n_rej else None, n_rej, source_id.encode(), parts.ctypes.data,
-                                 rec.ctypes.data, cap[0], keys.ctypes.data, cap[1], vals.ctypes.data, cap[2],
-                                 need.ctypes.data, npay.ctypes.data)
+        n = fn(*args_head, rec.ctypes.data, cap[0], keys.ctypes.data, cap[1], vals.ctypes.data, cap[2],
+               need.ctypes.data, npay.ctypes.data)
         if n >= 0:
             return RoutedRejects(rec[:n], keys[:need[1]], vals[:need[2]], int(npay[0]))
         cap = tuple(int(x) for x in need)
-    raise RuntimeError("sw_route_rejects: output sizing failed")
+    raise RuntimeError("reject routing: output sizing failed")
+
+
+def route_refs(compact, refs: np.ndarray, rank: int = 0, source_id: str = "gpu-inbound",
+               partitions=(1, 1, 1, 1), raw=None) -> RoutedRejects:
+    """Route the MI355X step's reject snapshot (``k_reject_refs``: u32 [n, 4] = payload start, end,
+    status | src_rank << 8, copy offset) from the compact payload copies ``compact`` the GPU made;
+    ``raw`` (the batch bytes, a numpy array or address) only serves refs whose copy did not fit."""
+    refs = np.ascontiguousarray(refs, np.uint32).reshape(-1)
+    n = len(refs) // 4
+
+    def ptr(x):
+        return None if x is None else (x if isinstance(x, int) else np.asarray(x).ctypes.data)
+    comp = np.ascontiguousarray(compact, np.uint8) if not isinstance(compact, int) else compact
+    parts = np.asarray(partitions, np.int32)
+    return _call(native().sw_route_refs, (ptr(comp), ptr(raw), refs.ctypes.data if n else None, n, int(rank),
+                                          source_id.encode(), parts.ctypes.data), n)
+
+
+def route_rejects(raw: np.ndarray, offs: np.ndarray, rej_off: np.ndarray, rej_status: np.ndarray,
+                  source_id: str = "gpu-inbound", partitions=(1, 1, 1, 1)) -> RoutedRejects:
+    """``raw`` / ``offs``: the raw batch; ``rej_off`` / ``rej_status``: the step's reject records
+    (``EVENT_REC["aux_off"]``, engine status).  ``partitions``: partition counts of the
+    unregistered, registration, decoded and failed-decode topics."""
+    raw = np.ascontiguousarray(raw, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint32)
+    ro = np.ascontiguousarray(rej_off, np.uint32)
+    rs = np.ascontiguousarray(rej_status, np.uint8)
+    parts = np.asarray(partitions, np.int32)
+    n_rej = len(ro)
+    return _call(native().sw_route_rejects, (raw.ctypes.data, offs.ctypes.data, len(offs) - 1,
+                                             ro.ctypes.data if n_rej else None, rs.ctypes.data if n_rej else None,
+                                             n_rej, source_id.encode(), parts.ctypes.data), n_rej)

@@ -30,6 +30,10 @@ def test_bench_single_rank_json():
     assert KEYS <= set(d) and d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
     assert d["metric"] == "device_events_per_sec" and d["value"] > 0 and d["higher_is_better"] is True
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
+    # the timed region ends with every block of the run durable on disk
+    dd = d["detail"]["durable"]
+    assert d["config"]["durable"] and dd["all_durable"] and dd["rows"] == d["detail"]["persisted"]
+    assert dd["bytes_per_event"] > 0 and dd["durable_bytes_per_s"] > 0 and dd["fdatasyncs"] >= 1
 
 
 @pytest.mark.slow
@@ -48,3 +52,7 @@ def test_bench_two_ranks_torchrun():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 3000 and d["config"]["parallelism"].startswith("dp2")
     assert d["detail"]["payloads"] == 2 * 2 * 1500
+    # self-checking multi-rank record: the backend and world the process group really had, per-rank time
+    det = d["detail"]
+    assert det["backend"] == "gloo" and det["world"] == 2 and len(det["rank_elapsed_s"]) == 2
+    assert det["exchange_bytes_per_rank_step"] > 0 and det["shuffle_overflow"] == 0

@@ -104,7 +104,8 @@ def test_sms_and_coap_destinations_routed_by_device_type():
         assert json.loads(sms["Body"])["command"]["token"] == "galaxytab-ping"
         payload, path = got[0]
         assert path == "cmd/in" and json.loads(payload)["command"]["token"] == "openhab-ping"
-        assert cd.destinations["sms"].delivered == 1 and cd.destinations["coap"].delivered == 1
+        # the counters move after the provider returns: wait for them rather than racing the worker
+        assert wait(lambda: cd.destinations["sms"].delivered == 1 and cd.destinations["coap"].delivered == 1)
         # an API refusal is an undelivered command (reference: undelivered-command-invocations topic)
         _Twilio.fail = True
         u0 = cd.undelivered

@@ -113,3 +113,43 @@ def test_gpu_engine_step_block_matches_oracle():
         np.testing.assert_array_equal(cols["date"], rc.out["event_date"])
         np.testing.assert_array_equal(cols["v0"].view(np.uint64), rc.out["v0"].view(np.uint64))
         assert cols["header"]["first_seq"] == rc.first_seq
+
+
+def test_gpu_reject_snapshot_routes_like_host():
+    """k_reject_refs + compact payload copies -> native routing equals routing the CPU oracle's
+    rejects against the raw batch (unregistered devices, registrations, acks; duplicates dropped)."""
+    import torch
+    from sitewhere_amd.pipeline import routing
+    from sitewhere_amd.pipeline.config import EngineConfig
+    from sitewhere_amd.pipeline.cpu_engine import CpuInboundEngine
+    from sitewhere_amd.pipeline.fleet import FleetSpec, fingerprints, gen_payloads, gen_tokens
+    from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
+    cfg = dict(max_msgs=8192, gen_cap=8192, max_devices=4096, max_assignments=4096, store_cap=1 << 15,
+               dedup_slots=1 << 15, name_slots=1 << 10, names_cap=1024)
+    g = GpuInboundEngine(EngineConfig.small(**cfg), device="cuda:0")
+    c = CpuInboundEngine(EngineConfig.small(**cfg))
+    heap, offs = gen_tokens("dev-", 0, 3000)
+    lo, hi = fingerprints(heap, offs)
+    for e in (g, c):
+        d = e.register_devices(lo, hi)
+        e.set_assignments(d, d)
+    spec = FleetSpec(prefix="dev-", n_devices=3000, p_unregistered=0.03, mx_per_msg=2, with_alternate_id=True,
+                     p_register=0.01, p_ack=0.01)
+    raw, off = gen_payloads(spec, 4000, 1_700_000_000_000, seed=5)
+    raw = np.concatenate([raw, np.zeros(64, np.uint8)])
+    parts = (8, 4, 8, 2)
+    for b in range(2):                      # the second step replays the batch: all duplicates dropped
+        rg = g.step(raw, off, 1_700_000_001_000 + b, presence=False)
+        rc = c.step(raw, off, 1_700_000_001_000 + b, presence=False)
+        assert rg.n_persisted == rc.n_persisted
+        cnt, _ = g.reject_refs_async(0, g._stg[2], g._stg[3], len(off) - 1)
+        torch.cuda.synchronize()
+        hdr = cnt.cpu().numpy().view(np.uint32)
+        refs, comp = g.reject_snapshot(0, int(hdr[0]), int(hdr[1]))
+        refs, comp = refs.copy(), comp.copy()
+        gpu = routing.route_refs(comp, refs, 0, "gpu-inbound", parts)
+        host = routing.route_rejects(raw, off, rc.rejects["aux_off"], rc.reject_status, "gpu-inbound", parts)
+        assert len(gpu) > 0 and gpu.payloads == host.payloads
+        gk = sorted((k, p, bytes(kh), bytes(vh)) for k, p, kh, ko, vh, vo in gpu.groups())
+        hk = sorted((k, p, bytes(kh), bytes(vh)) for k, p, kh, ko, vh, vo in host.groups())
+        assert gk == hk

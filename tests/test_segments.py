@@ -197,3 +197,43 @@ def test_durable_event_store_queries_and_restart(tmp_path):
     assert both.num_results == len(want) + len(want2)
     assert {e.id.split("-")[0] for e in both.results} == {"b0", "b1"}
     es2.close()
+
+
+class _FakeHostBuffer:
+    """Page-aligned host memory standing in for the MI355X pinned buffers (no GPU needed)."""
+
+    def __init__(self, lib, n):
+        import ctypes
+        import mmap
+        self.m = mmap.mmap(-1, n)
+        self.nbytes = n
+        self.host = ctypes.addressof(ctypes.c_char.from_buffer(self.m))
+
+
+def test_block_sink_pool_bounded_and_commits_in_order(tmp_path):
+    """DurableBlockSink: blocks published zero-copy to the enriched topic and queued to the store;
+    buffers come back when both let go (growing blocks replace undersized buffers), and the caller
+    tags come back as committable in order once durable."""
+    import ctypes
+    from sitewhere_amd.bus.log import EventBus
+    store = sg.DurableEventStore(str(tmp_path / "s"))
+    bus = EventBus(None, default_partitions=1)
+    sink = sg.DurableBlockSink(store, None, 5, bus=bus, topic="t.out", max_buffers=16)
+    sink._HostBuffer = _FakeHostBuffer
+    bus.set_retention("t.out", 4 << 20)
+    tags = []
+    for k in range(60):
+        rows, v2, alt = synth_rows(20000 + 1000 * k, seed=k)
+        blk = sg.encode_block(rows, v2, alt)
+        host, buf = sink.target(len(blk))
+        ctypes.memmove(host, blk.ctypes.data, len(blk))
+        sink.publish(buf, len(blk), k * 200_000, 1, tag=k)
+        tags += sink.committable()
+    sink.flush()
+    tags += sink.committable()
+    assert tags == list(range(60))
+    assert sink.n_alloc <= 16 and store.rows() == sum(20000 + 1000 * k for k in range(60))
+    # the topic carries the sealed blocks
+    v = bus.read_views("t.out", 0, bus.begin_offset("t.out", 0), 1)[0].value
+    assert sg.verify(np.frombuffer(v, np.uint8)) == 0
+    store.close()
