@@ -64,6 +64,25 @@ typedef struct __attribute__((aligned(8))) SwSegBlockHdr {
   uint64_t checksum;     // header (checksum = 0) + page table
 } SwSegBlockHdr;
 
+// Commit record (exactly-once ingest): a block sealed with SEG_FLAG_COMMIT is followed, in the same
+// group write, by one 4 KiB record naming the input offsets the block completes (key = 64-bit hash
+// of the source, e.g. topic + partition; offset = next input offset).  Recovery drops a flagged
+// block whose record is missing or torn, so a block is on disk exactly when its offsets are.
+#define SEG_COMMIT_MAGIC 0x43455753u   // "SWEC"
+#define SEG_FLAG_COMMIT 1
+#define SEG_COMMIT_BYTES 4096
+#define SEG_MAX_SRC 252
+
+typedef struct __attribute__((aligned(8))) SwSegCommitHdr {
+  uint32_t magic;
+  uint16_t version;
+  uint16_t n_src;
+  uint64_t bytes;        // 64 + 16 * n_src
+  int64_t token;
+  uint64_t pad[4];
+  uint64_t checksum;     // header (checksum = 0) + entries
+} SwSegCommitHdr;        // then n_src x {uint64 key, int64 offset}
+
 typedef struct __attribute__((aligned(8))) SwSegCol {
   uint64_t base;         // FOR base (min of the order-preserving unsigned values)
   uint32_t data_off;     // from the page start

@@ -30,6 +30,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -296,6 +297,17 @@ void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot
   memcpy(block, &h, sizeof(h));
 }
 
+// Set the header flags of a sealed block (SEG_FLAG_COMMIT) and redo its checksum.
+void swseg_set_flags(uint8_t* block, int32_t flags) {
+  SwSegBlockHdr h;
+  memcpy(&h, block, sizeof(h));
+  h.flags = (uint16_t)flags;
+  h.checksum = 0;
+  memcpy(block, &h, sizeof(h));
+  h.checksum = header_checksum(block);
+  memcpy(block, &h, sizeof(h));
+}
+
 // 0 = valid; 1 bad header, 2 bad page table, 3 bad page header, 4 page checksum, 5 short.
 int32_t swseg_verify(const uint8_t* b, int64_t len) {
   if (len < 64) return 5;
@@ -478,7 +490,30 @@ struct SegItem {
   const uint8_t* ptr;
   int64_t len;          // block bytes (unpadded)
   int64_t token;
+  std::vector<std::pair<uint64_t, int64_t>> src;   // commit record entries (flagged blocks)
 };
+
+static uint64_t commit_checksum(const uint8_t* rec, uint32_t n_src) {
+  uint64_t cs = 0;
+  const uint32_t words = (64 + 16 * n_src) / 8;
+  for (uint32_t i = 0; i < words; ++i) {
+    if (i == 7) continue;                 // the checksum word
+    uint64_t w;
+    memcpy(&w, rec + 8 * i, 8);
+    cs ^= seg_mix_word(w, i);
+  }
+  return cs;
+}
+
+// 0 when rec (len bytes available) is a valid commit record
+static int commit_valid(const uint8_t* rec, int64_t len) {
+  if (len < 64) return 1;
+  SwSegCommitHdr c;
+  memcpy(&c, rec, sizeof(c));
+  if (c.magic != SEG_COMMIT_MAGIC || c.version != SEG_VERSION || c.n_src > SEG_MAX_SRC) return 1;
+  if (c.bytes != 64 + 16ull * c.n_src || (int64_t)c.bytes > len) return 1;
+  return commit_checksum(rec, c.n_src) == c.checksum ? 0 : 1;
+}
 
 struct SegStore {
   std::string dir;
@@ -504,6 +539,8 @@ struct SegStore {
   uint8_t* bounce = nullptr;
   int64_t bounce_cap = 0;
   int64_t total_bytes = 0;
+  uint8_t* commit_buf = nullptr;          // one SEG_COMMIT_BYTES record, aligned for O_DIRECT
+  std::map<uint64_t, int64_t> sources;    // durable input offsets (max per key)
 };
 
 // Files are numbered in write order ("<rank>-<number>.sweg"): sequences restart with a new engine
@@ -580,6 +617,7 @@ static bool seg_write_all(int fd, const uint8_t* p, int64_t n) {
 
 static void seg_writer(SegStore* s) {
   std::vector<SegItem> batch;
+  std::vector<std::pair<uint64_t, int64_t>> done_src;
   while (true) {
     {
       std::unique_lock<std::mutex> lk(s->mu);
@@ -589,11 +627,14 @@ static void seg_writer(SegStore* s) {
       s->q.clear();
     }
     int64_t last = -1;
+    done_src.clear();
     for (const SegItem& it : batch) {
       SwSegBlockHdr h;
       memcpy(&h, it.ptr, sizeof(h));
+      const bool commit = (h.flags & SEG_FLAG_COMMIT) != 0;
       const int64_t padded = round_up(it.len, SEG_ALIGN);
-      if (s->fd < 0 || s->cur_bytes + padded > s->rotate_bytes) {
+      const int64_t extra = commit ? SEG_COMMIT_BYTES : 0;
+      if (s->fd < 0 || s->cur_bytes + padded + extra > s->rotate_bytes) {
         seg_close_file(s);
         seg_retention(s);
         if (!seg_open_file(s, h.first_seq)) {
@@ -620,6 +661,31 @@ static void seg_writer(SegStore* s) {
         memset(s->bounce + it.len, 0, (size_t)(padded - it.len));
         ok = seg_write_all(s->fd, s->bounce, padded);
       }
+      if (ok && commit) {
+        // the commit record right behind the block, before the group's fdatasync
+        if (!s->commit_buf) s->commit_buf = (uint8_t*)aligned_alloc(SEG_ALIGN, SEG_COMMIT_BYTES);
+        if (!s->commit_buf) {
+          s->error = ENOMEM;
+          break;
+        }
+        memset(s->commit_buf, 0, SEG_COMMIT_BYTES);
+        SwSegCommitHdr c;
+        memset(&c, 0, sizeof(c));
+        c.magic = SEG_COMMIT_MAGIC;
+        c.version = SEG_VERSION;
+        c.n_src = (uint16_t)it.src.size();
+        c.bytes = 64 + 16ull * c.n_src;
+        c.token = it.token;
+        memcpy(s->commit_buf, &c, sizeof(c));
+        for (size_t k = 0; k < it.src.size(); ++k) {
+          memcpy(s->commit_buf + 64 + 16 * k, &it.src[k].first, 8);
+          memcpy(s->commit_buf + 64 + 16 * k + 8, &it.src[k].second, 8);
+        }
+        c.checksum = commit_checksum(s->commit_buf, c.n_src);
+        memcpy(s->commit_buf, &c, sizeof(c));
+        ok = seg_write_all(s->fd, s->commit_buf, SEG_COMMIT_BYTES);
+        done_src.insert(done_src.end(), it.src.begin(), it.src.end());
+      }
       if (!ok) {
         s->error = errno ? errno : -1;
         break;
@@ -627,11 +693,11 @@ static void seg_writer(SegStore* s) {
       {
         std::lock_guard<std::mutex> g(s->mu);
         s->index.push_back(index_entry(h, it.ptr, s->files.back().id, s->cur_bytes));
-        s->files.back().bytes += padded;
-        s->total_bytes += padded;
+        s->files.back().bytes += padded + extra;
+        s->total_bytes += padded + extra;
       }
-      s->cur_bytes += padded;
-      s->bytes_written += padded;
+      s->cur_bytes += padded + extra;
+      s->bytes_written += padded + extra;
       s->blocks_written += 1;
       last = it.token;
     }
@@ -647,15 +713,20 @@ static void seg_writer(SegStore* s) {
     s->syncs += 1;
     if (last >= 0) {
       std::lock_guard<std::mutex> g(s->mu);
+      for (const auto& kv : done_src) {
+        auto f = s->sources.find(kv.first);
+        if (f == s->sources.end() || f->second < kv.second) s->sources[kv.first] = kv.second;
+      }
       if (last > s->durable) s->durable = last;
     }
     s->cv_done.notify_all();
   }
 }
 
-// Scan one segment file: verify every block, truncate a torn tail.  Calls emit(offset, header).
-template <typename F>
-static int64_t seg_scan_file(const std::string& path, bool truncate, F emit) {
+// Scan one segment file: verify every block (and the commit record of a flagged block), truncate a
+// torn tail.  Calls emit(offset, header, block) and on_commit(record) for each commit record.
+template <typename F, typename G>
+static int64_t seg_scan_file(const std::string& path, bool truncate, F emit, G on_commit) {
   int fd = open(path.c_str(), truncate ? O_RDWR : O_RDONLY);
   if (fd < 0) return -1;
   struct stat st;
@@ -670,8 +741,20 @@ static int64_t seg_scan_file(const std::string& path, bool truncate, F emit) {
     buf.resize(h.bytes);
     if (pread(fd, buf.data(), h.bytes, off) != (ssize_t)h.bytes) break;
     if (swseg_verify(buf.data(), (int64_t)h.bytes) != 0) break;
-    emit(off, h, buf.data());
-    off += round_up((int64_t)h.bytes, SEG_ALIGN);
+    int64_t next = off + round_up((int64_t)h.bytes, SEG_ALIGN);
+    if (h.flags & SEG_FLAG_COMMIT) {
+      uint8_t rec[SEG_COMMIT_BYTES];
+      if (next + SEG_COMMIT_BYTES > size ||
+          pread(fd, rec, SEG_COMMIT_BYTES, next) != (ssize_t)SEG_COMMIT_BYTES ||
+          commit_valid(rec, SEG_COMMIT_BYTES) != 0)
+        break;                            // the block's offsets never made it: the block goes too
+      emit(off, h, buf.data());
+      on_commit(rec);
+      next += SEG_COMMIT_BYTES;
+    } else {
+      emit(off, h, buf.data());
+    }
+    off = next;
   }
   if (off > size) off = size;
   if (truncate && off < size) {
@@ -708,9 +791,21 @@ void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t ret
   std::sort(found.begin(), found.end(), [](const SegFile& a, const SegFile& b) { return a.first_seq < b.first_seq; });
   for (auto& f : found) {
     f.id = s->next_file_id;
-    f.bytes = seg_scan_file(f.path, true, [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) {
-      s->index.push_back(index_entry(hd, b, f.id, off));
-    });
+    f.bytes = seg_scan_file(
+        f.path, true,
+        [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) { s->index.push_back(index_entry(hd, b, f.id, off)); },
+        [&](const uint8_t* rec) {
+          SwSegCommitHdr c;
+          memcpy(&c, rec, sizeof(c));
+          for (uint32_t k = 0; k < c.n_src; ++k) {
+            uint64_t key;
+            int64_t o;
+            memcpy(&key, rec + 64 + 16 * k, 8);
+            memcpy(&o, rec + 64 + 16 * k + 8, 8);
+            auto it = s->sources.find(key);
+            if (it == s->sources.end() || it->second < o) s->sources[key] = o;
+          }
+        });
     if (f.bytes < 0) continue;
     ++s->next_file_id;
     s->files.push_back(f);
@@ -728,10 +823,45 @@ int32_t swss_append(void* h, const uint8_t* ptr, int64_t len, int64_t token) {
   if (s->error) return s->error;
   {
     std::lock_guard<std::mutex> g(s->mu);
-    s->q.push_back({ptr, len, token});
+    s->q.push_back({ptr, len, token, {}});
   }
   s->cv.notify_one();
   return 0;
+}
+
+// Append a block sealed with SEG_FLAG_COMMIT plus its commit record: the n_src input offsets
+// (keys[i] -> offs[i]) become durable with the block, atomically across a crash.
+int32_t swss_append_commit(void* h, const uint8_t* ptr, int64_t len, int64_t token, const uint64_t* keys,
+                           const int64_t* offs, int32_t n_src) {
+  SegStore* s = (SegStore*)h;
+  if (s->error) return s->error;
+  if (n_src < 0 || n_src > SEG_MAX_SRC || len < 64) return -EINVAL;
+  SwSegBlockHdr hd;
+  memcpy(&hd, ptr, sizeof(hd));
+  if (!(hd.flags & SEG_FLAG_COMMIT)) return -EINVAL;
+  SegItem it{ptr, len, token, {}};
+  for (int32_t k = 0; k < n_src; ++k) it.src.emplace_back(keys[k], offs[k]);
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->q.push_back(std::move(it));
+  }
+  s->cv.notify_one();
+  return 0;
+}
+
+// Durable input offsets (max per key, from commit records); returns the count, fills <= cap.
+int64_t swss_sources(void* h, uint64_t* keys, int64_t* offs, int64_t cap) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  int64_t i = 0;
+  for (const auto& kv : s->sources) {
+    if (i < cap) {
+      keys[i] = kv.first;
+      offs[i] = kv.second;
+    }
+    ++i;
+  }
+  return (int64_t)s->sources.size();
 }
 
 int64_t swss_durable(void* h) { return ((SegStore*)h)->durable.load(); }
@@ -774,6 +904,7 @@ void swss_close(void* h) {
   if (s->th.joinable()) s->th.join();
   seg_close_file(s);
   free(s->bounce);
+  free(s->commit_buf);
   delete s;
 }
 

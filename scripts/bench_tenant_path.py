@@ -1,9 +1,12 @@
 """Service-level MI355X path: events/s through a ``gpu-columnar`` tenant of a whole co-located instance.
 
 raw payload batches (the ``event-source-raw-payloads`` record format) -> inbound-processing GPU tenant
-engine (decode, validate, dedup, persist, state, zone rules on the MI355X) -> columnar batch ->
-event-management columnar store (RPC) + ``inbound-enriched-batches`` topic.  Devices and assignments
-are created through the device-management API and mirrored into the engine by the change feed.
+engine (decode, validate, dedup, persist, state, zone rules on the MI355X, block encode) -> durable
+batch -> event-management segment store (fdatasync'd before the raw offset commits) +
+``inbound-enriched-batches`` topic; rejected payloads routed per payload to the unregistered /
+registration topics.  Devices and assignments are created through the device-management API and
+mirrored into the engine by the change feed.  Every timed batch carries fresh alternate ids
+(``--alt-ids``), so dedup does real work and nothing is dropped as a replay.
 
     python scripts/bench_tenant_path.py --devices 20000 --batch 65536 --batches 40
 """
@@ -32,6 +35,11 @@ def main():
                     help="frame columnar payloads around the rows in the engine's pinned buffers (zeroCopyRows)")
     ap.add_argument("--gc", choices=["default", "freeze"], default="default",
                     help="freeze: gc.freeze() the heap once the devices are loaded; default: leave the collector alone")
+    ap.add_argument("--template", default="gpu-columnar", help="tenant template (gpu-memory: volatile store)")
+    ap.add_argument("--alt-ids", action=argparse.BooleanOptionalAction, default=True)
+    ap.add_argument("--p-unregistered", type=float, default=0.0, help="share of payloads from unknown devices")
+    ap.add_argument("--p-register", type=float, default=0.0)
+    ap.add_argument("--p-ack", type=float, default=0.0)
     ap.add_argument("--store-retention", type=int, default=0,
                     help="rows the columnar event store holds (0 = the template's); older batches are evicted "
                          "and their memory reused -- a store that only grows page-faults fresh memory per batch")
@@ -47,7 +55,7 @@ def main():
     sw.wait_for_tenant("default", 60)
     tm = sw.api("TenantManagement")
     sw.instance.system_user.run(lambda: tm.create_tenant({"token": "fast", "name": "fast",
-                                                          "configurationTemplateId": "gpu-columnar",
+                                                          "configurationTemplateId": args.template,
                                                           "datasetTemplateId": "empty"}))
     sw.wait_for_tenant("fast", 120)
     if args.max_msgs or args.zero_copy:
@@ -61,7 +69,7 @@ def main():
         sw.instance.coord.put(ms.tenant_config_path("fast"), dump_document(cfg))
         while ms.get_tenant_engine("fast") in (None, before) or ms.get_tenant_engine("fast").status.value != "Started":
             time.sleep(0.1)
-    if args.store_retention:
+    if args.store_retention and hasattr(sw.tenant_engine("event-management", "fast").store, "retention_rows"):
         # the same window on the enriched-batch topic, which references the same batch payloads
         sw.tenant_engine("event-management", "fast").store.retention_rows = args.store_retention
         t_out = sw.instance.naming.tenant_prefix("fast") + "inbound-enriched-batches"
@@ -79,12 +87,25 @@ def main():
     while ib.engine.n_assignments < args.devices and time.time() - t0 < 600:
         time.sleep(0.1)
     setup_s = time.time() - t0
-    spec = FleetSpec(prefix="dev-", n_devices=args.devices, p_location=0.25, p_alert=0.05, mx_per_msg=1)
+    from sitewhere_amd.pipeline.fleet import stamp_alt_epoch
+    spec = FleetSpec(prefix="dev-", n_devices=args.devices, p_location=0.25, p_alert=0.05, mx_per_msg=1,
+                     with_alternate_id=args.alt_ids, p_unregistered=args.p_unregistered, p_register=args.p_register,
+                     p_ack=args.p_ack)
     now0 = int(time.time() * 1000)
     batches = []
     for b in range(4):
         raw, offs = gen_payloads(spec, args.batch, now0 - 1000, seed=7 + b)
         batches.append((np.concatenate([raw, np.zeros(64, np.uint8)]), offs))
+    n_total = args.warmup + args.batches
+    if args.alt_ids:
+        # every batch its own alternate ids (stamped before the clock starts): cycling the 4
+        # generated batches would otherwise make every batch after the 4th a set of duplicates
+        base = batches
+        batches = []
+        for k in range(n_total):
+            raw = base[k % 4][0].copy()
+            stamp_alt_epoch(raw, base[k % 4][1], (0x7E17 << 48) | k)
+            batches.append((raw, base[k % 4][1]))
     if args.gc == "freeze":
         import gc
         gc.collect()
@@ -95,13 +116,15 @@ def main():
         from sitewhere_amd.pipeline.framing import varint_lengths
         bus = sw.instance.bus
         t_raw = sw.instance.naming.tenant_prefix("fast") + "event-source-raw-payloads"
-        recs = [RawBatchRecord(r[:int(o[-1])], varint_lengths(o), len(o) - 1) for r, o in batches]
+        import torch
+        pin = torch.cuda.is_available()
+        recs = [RawBatchRecord(r[:int(o[-1])], varint_lengths(o), len(o) - 1, pinned=pin) for r, o in batches]
         parts = bus.partitions(t_raw)
 
         def pump(n, k0):
             start = {p: bus.end_offset(t_raw, p) for p in range(parts)}
             for k in range(n):
-                recs[(k0 + k) % 4].publish(bus, t_raw, (k0 + k) % parts, ts=now0 + k0 + k)
+                recs[(k0 + k) % len(recs)].publish(bus, t_raw, (k0 + k) % parts, ts=now0 + k0 + k)
             end = {p: bus.end_offset(t_raw, p) for p in range(parts)}
             while any(bus.committed(ib.raw_consumer.group, t_raw, p) < end[p] for p in range(parts)
                       if end[p] > start[p]):
@@ -116,13 +139,13 @@ def main():
         ev = ib.processed_events.count - ev0
     else:
         for k in range(args.warmup):
-            ib.process_batch(*batches[k % 4])
+            ib.process_batch(*batches[k % len(batches)])
         ib.flush()
         base = ib.persisted_events.count
         t = time.perf_counter()
         ev = 0
         for k in range(args.batches):
-            r = ib.process_batch(*batches[k % 4])
+            r = ib.process_batch(*batches[(args.warmup + k) % len(batches)])
             ev += r.n_events
         ib.flush()
         dt = time.perf_counter() - t
@@ -164,8 +187,14 @@ def main():
                       "events": ev,
                       "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,
                       "ms_per_batch": round(1000 * dt / args.batches, 3), "batch": args.batch,
-                      "devices": args.devices, "store_rows": em_store.rows,
-                      "store_retention_rows": em_store.retention_rows, "store_evicted_rows": em_store.evicted_rows, "setup_s": round(setup_s, 1),
+                      "devices": args.devices, "store_rows": em_store.rows, "template": args.template,
+                      "store": type(em_store).__name__,
+                      "store_disk": em_store.seg.stats() if hasattr(em_store, "seg") else None,
+                      "alt_ids": args.alt_ids, "p_unregistered": args.p_unregistered,
+                      "duplicates": ib.engine.stats_dict().get("duplicates"),
+                      "routed_payloads": ib.routed_payloads, "unregistered": ib.unregistered.count,
+                      "store_retention_rows": getattr(em_store, "retention_rows", None),
+                      "store_evicted_rows": getattr(em_store, "evicted_rows", None), "setup_s": round(setup_s, 1),
                       "mean_ms": breakdown, **({"median_ms_second_half": trace} if trace else {})}))
     sw.stop()
 

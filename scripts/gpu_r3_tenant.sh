@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU tests, then the durable tenant path (gpu-columnar) at 256K and 1M-payload batches with 0% and
+# 1% rejected payloads (unregistered devices).  Results under gpurun_out/<name>.
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+O="$R/gpurun_out/${1:-r3_tenant}"
+mkdir -p "$O" && cd "$R" && export TMPDIR=/tmp
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1; rc=$?
+  tail -3 "$O/pytest.log"
+  [ $rc -eq 0 ] || exit $rc
+fi
+for B in 262144 1048576; do
+  for P in 0 0.01; do
+    timeout -k 10 400 python -u scripts/bench_tenant_path.py --devices 100000 --batch $B --batches 30 --warmup 4 \
+      --via-bus --max-msgs $B --p-unregistered $P > "$O/tenant_${B}_${P}.log" 2>&1 || { tail -20 "$O/tenant_${B}_${P}.log"; exit 1; }
+    tail -1 "$O/tenant_${B}_${P}.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["batch"], d["p_unregistered"], round(d["events_per_sec"]/1e6,1), "M/s", d["ms_per_batch"], "ms", d["store"], d["mean_ms"])'
+  done
+done

@@ -206,18 +206,25 @@ class EventBus:
         ``owner`` (the object owning the bytes: a pinned tensor, a ``bytes`` object, ...) is kept
         alive, and must not change, until retention drops the record; then ``on_release(owner)`` is
         called (a buffer pool takes it back) or, without a callback, the reference is dropped.
-        Memory-only partitions only."""
+        A durable partition (files) copies the record instead and releases ``owner`` at once."""
         self._drain_released()
         ext = next(self._ext_ids)
         with self._lock:
             self._ext[ext] = (owner, on_release)
         first = self.fast.swlog_append_external(self.h, self.topic(name), partition, ptr, int(nbytes), int(key_len),
                                                ts if ts is not None else int(time.time() * 1000), ext)
+        if first == -2:                 # durable partition: the record goes to its files (a copy)
+            with self._lock:
+                self._ext.pop(ext, None)
+            raw = ctypes.string_at(ptr, int(nbytes))
+            first = self.append(name, partition, [(raw[:key_len] or None, raw[key_len:])], ts=ts)
+            if on_release is not None:
+                on_release(owner)
+            return first
         if first < 0:
             with self._lock:
                 self._ext.pop(ext, None)
-            raise RuntimeError(f"zero-copy append to {name}[{partition}] failed ({first}): "
-                               "durable partitions copy their records (use append)")
+            raise RuntimeError(f"zero-copy append to {name}[{partition}] failed ({first})")
         self._wake(name)
         return first
 

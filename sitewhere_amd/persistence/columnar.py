@@ -92,6 +92,14 @@ def frame_batch(frame: tuple, rows_nbytes: int, boot: str, first_seq: int, world
 def decode_batch(payload) -> dict:
     """``bytes`` or a zero-copy buffer (read-only array / memoryview) -> header dict + row view."""
     buf = payload if isinstance(payload, (bytes, bytearray)) else memoryview(payload).cast("B")
+    if bytes(buf[:4]) == b"SWD1":             # durable batch: an encoded block (persistence/segments.py)
+        from .segments import decode_block, decode_durable_batch, rows_of
+        d, blk = decode_durable_batch(payload)
+        cols = decode_block(blk)
+        h = cols["header"]
+        d.update(boot=f"{h['boot']:x}", first_seq=h["first_seq"], world=h["world"], rank=h["rank"],
+                 now=h["recv_ms"], rows=rows_of(cols))
+        return d
     if bytes(buf[:4]) != _MAGIC:              # batches written before the framed format
         d = msgpack.unpackb(bytes(buf), raw=False, strict_map_key=False)
         d["rows"] = np.frombuffer(d["rows"], OUT_REC)

@@ -706,6 +706,13 @@ def create_event_store(kind: str = "memory", **kw) -> DeviceEventStore:
     if kind == "columnar":
         from .columnar import ColumnarEventStore
         return ColumnarEventStore(retention_rows=kw.get("retentionRows"))
+    if kind in ("segments", "durable"):
+        # durable columnar segments of engine tenants (persistence/segments.py)
+        from .segments import DurableEventStore
+        return DurableEventStore(kw.get("path", "/tmp/sitewhere/segments"), int(kw.get("rank", 0)),
+                                 rotate_bytes=int(kw.get("rotateBytes", 1 << 30)),
+                                 retention_bytes=int(kw.get("retentionBytes", 0)),
+                                 direct=bool(kw.get("directIo", True)))
     if kind in ("mongo", "mongodb"):
         return MongoEventStore(kw.get("uri", "mongodb://localhost:27017"), kw.get("database", "sitewhere"))
     if kind == "influxdb":

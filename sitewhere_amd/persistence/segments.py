@@ -36,6 +36,8 @@ from .events import DeviceEventStore, MemoryEventStore
 
 SEG_ALIGN = 4096
 PAGE_ROWS = 1024
+FLAG_COMMIT = 1             # the block is followed by a commit record of input offsets (swseg.h)
+MAX_SRC = 252
 HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("flags", "<u2"), ("n_rows", "<u4"), ("n_pages", "<u4"),
                 ("bytes", "<u8"), ("first_seq", "<i8"), ("recv_ms", "<i8"), ("boot", "<i8"), ("rank", "<i4"),
                 ("world", "<i4"), ("checksum", "<u8")])
@@ -78,6 +80,17 @@ def seal(block: np.ndarray, first_seq: int, recv_ms: int, boot: int, rank: int, 
     native().swseg_seal(_p(block), int(first_seq), int(recv_ms), int(boot), int(rank), int(world))
 
 
+def source_key(topic: str, partition: int) -> int:
+    """64-bit key of an input (topic, partition) in commit records (stable across processes)."""
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(f"{topic}/{int(partition)}".encode(), digest_size=8).digest(), "little")
+
+
+def set_commit_flag(block: np.ndarray):
+    """Mark a sealed block as carrying a commit record (see :meth:`SegmentStore.append`)."""
+    native().swseg_set_flags(_p(block), FLAG_COMMIT)
+
+
 def verify(block) -> int:
     b = np.frombuffer(block, np.uint8) if not isinstance(block, np.ndarray) else block
     return int(native().swseg_verify(_p(b), len(b)))
@@ -115,6 +128,66 @@ def rows_of(cols: dict) -> np.ndarray:
     return out
 
 
+# ---------------------------------------------------------------------- durable batch wire format
+# What an engine tenant sends event management (and publishes on the enriched-batch topic):
+# b"SWD1", u32 header length, msgpack {"boot", "asg", "names", "rules"} (the dictionary deltas the
+# rows need), zero padding up to a 64-byte multiple, then the sealed block.  When the block sits at a
+# 4 KiB boundary of a pinned buffer the header is framed in front of it (:func:`frame_durable_batch`)
+# and the block goes to the disk with O_DIRECT straight from that buffer.
+DURABLE_MAGIC = b"SWD1"
+
+
+def _durable_head(boot, asg: dict, names: dict, rules: dict | None, src=None) -> bytes:
+    import msgpack
+    import struct
+    d = {"boot": boot_id(boot), "asg": {int(k): list(v) for k, v in (asg or {}).items()},
+         "names": {int(k): v for k, v in (names or {}).items()}, "rules": rules or {}}
+    if src:
+        d["src"] = [[str(t), int(p), int(o)] for t, p, o in src]
+    hdr = msgpack.packb(d, use_bin_type=True)
+    head = DURABLE_MAGIC + struct.pack("<I", len(hdr)) + hdr
+    return head + bytes(-len(head) % 64)
+
+
+def encode_durable_batch(block: np.ndarray, boot, asg: dict | None = None, names: dict | None = None,
+                         rules: dict | None = None, src=None) -> bytes:
+    """``src``: ``[(topic, partition, next offset)]`` of the input the block completes (the block
+    should then carry ``FLAG_COMMIT``, see :func:`set_commit_flag`)."""
+    return _durable_head(boot, asg, names, rules, src) + memoryview(np.ascontiguousarray(block, np.uint8)).cast("B")
+
+
+def frame_durable_batch(frame: tuple, nbytes: int, boot, asg: dict | None = None, names: dict | None = None,
+                        rules: dict | None = None, src=None) -> np.ndarray | None:
+    """Zero-copy :func:`encode_durable_batch` for a block at ``offset`` of ``buffer`` (``frame``)
+    with free bytes in front of it; None when the header does not fit."""
+    buf, off = frame
+    head = _durable_head(boot, asg, names, rules, src)
+    start = off - len(head)
+    if start < 0:
+        return None
+    buf[start:off] = np.frombuffer(head, np.uint8)
+    view = buf[start:off + int(nbytes)]
+    view.flags.writeable = False
+    return view
+
+
+def is_durable_batch(payload) -> bool:
+    return bytes(memoryview(payload)[:4]) == DURABLE_MAGIC
+
+
+def decode_durable_batch(payload) -> tuple[dict, np.ndarray]:
+    """(header dict, block bytes view) of a durable batch (bytes or a zero-copy buffer)."""
+    import msgpack
+    import struct
+    buf = np.frombuffer(payload, np.uint8) if not isinstance(payload, np.ndarray) else payload
+    if bytes(buf[:4]) != DURABLE_MAGIC:
+        raise ValueError("not a durable event batch")
+    (n,) = struct.unpack_from("<I", bytes(buf[4:8]))
+    d = msgpack.unpackb(bytes(buf[8:8 + n]), raw=False, strict_map_key=False)
+    start = -(-(8 + n) // 64) * 64
+    return d, buf[start:]
+
+
 class SegmentStore:
     """Native durable segment store of one engine shard (see module docstring)."""
 
@@ -131,21 +204,45 @@ class SegmentStore:
         self._token = int(self.lib.swss_durable(self.h))
         self.closed = False
 
-    def append(self, ptr: int, nbytes: int, owner=None) -> int:
+    def append(self, ptr: int, nbytes: int, owner=None, src=None) -> int:
         """Queue a sealed block at ``ptr`` (``nbytes``, readable up to the next 4 KiB multiple with
         zeroed padding when ``ptr`` is 4 KiB aligned).  ``owner`` is kept alive until the block is
-        durable.  Returns the block's token (see :meth:`durable`)."""
+        durable.  ``src``: ``[(topic, partition, next offset)]`` the block completes -- written as a
+        commit record with the block (it must carry ``FLAG_COMMIT``), so after a crash the block is
+        on disk exactly when these offsets are (:meth:`sources`).  Returns the block's token."""
+        if src is not None:
+            if len(src) > MAX_SRC:
+                raise ValueError("too many input offsets for one commit record")
+            keys = np.array([source_key(t, p) for t, p, _ in src], np.uint64)
+            offs = np.array([int(o) for _, _, o in src], np.int64)
         with self._lock:
             self._token += 1
             tok = self._token
             self._owners[tok] = owner
-            rc = self.lib.swss_append(self.h, ptr, int(nbytes), tok)
+            if src is not None:
+                rc = self.lib.swss_append_commit(self.h, ptr, int(nbytes), tok, _p(keys) if len(keys) else None,
+                                                 _p(offs) if len(offs) else None, len(keys))
+            else:
+                rc = self.lib.swss_append(self.h, ptr, int(nbytes), tok)
         if rc:
             raise OSError(rc, f"segment store append failed: {os.strerror(rc) if rc > 0 else rc}")
         return tok
 
     def append_block(self, block: np.ndarray) -> int:
         return self.append(_p(block), len(block), block)
+
+    def sources(self) -> dict:
+        """Durable input offsets: source key -> next offset (max over commit records)."""
+        cap = 64
+        while True:
+            keys, offs = np.zeros(cap, np.uint64), np.zeros(cap, np.int64)
+            n = int(self.lib.swss_sources(self.h, _p(keys), _p(offs), cap))
+            if n <= cap:
+                return {int(k): int(o) for k, o in zip(keys[:n], offs[:n])}
+            cap = n + 64
+
+    def source_offset(self, topic: str, partition: int) -> int | None:
+        return self.sources().get(source_key(topic, partition))
 
     def durable(self) -> int:
         """Highest token whose block (and every earlier one) is on disk."""
@@ -426,8 +523,11 @@ class DurableEventStore(DeviceEventStore):
             os.fdatasync(self._dict_f.fileno())
 
     # ------------------------------------------------------------------ ingest
-    def add_block(self, ptr: int, nbytes: int, owner=None, boot=None, asg=None, names=None, rules=None) -> int:
-        """Queue a sealed block for the disk; returns its token (-1 when skipped as a replay)."""
+    def add_block(self, ptr: int, nbytes: int, owner=None, boot=None, asg=None, names=None, rules=None,
+                  src=None) -> int:
+        """Queue a sealed block for the disk; returns its token (-1 when skipped as a replay).
+        ``src``: input offsets the block completes (see :meth:`SegmentStore.append`; the block must
+        carry ``FLAG_COMMIT``)."""
         h = np.frombuffer((ctypes.c_uint8 * 64).from_address(ptr), np.uint8).view(HDR)[0]
         b = int(h["boot"])
         if boot is not None and boot_id(boot) != b:
@@ -439,7 +539,14 @@ class DurableEventStore(DeviceEventStore):
                 self.skipped_rows += n
                 return -1
             self._high[key] = max(self._high.get(key, 0), first + n)
-        return self.seg.append(ptr, nbytes, owner)
+        if src is not None and not int(h["flags"]) & FLAG_COMMIT:
+            raise ValueError("a block with input offsets must be sealed with FLAG_COMMIT")
+        return self.seg.append(ptr, nbytes, owner, src)
+
+    def source_offset(self, topic: str, partition: int) -> int | None:
+        """Next input offset of (topic, partition) whose events are all durable here (None: none
+        recorded).  A restarted tenant resumes there: nothing lost, nothing stored twice."""
+        return self.seg.source_offset(topic, partition)
 
     def add_encoded(self, block: np.ndarray, **dicts) -> int:
         return self.add_block(_p(block), len(block), block, **dicts)
@@ -475,11 +582,50 @@ class DurableEventStore(DeviceEventStore):
                 self._cache.popitem(last=False)
         return c
 
+    def add_columnar(self, payload, wait: bool = True) -> int:
+        """Event management's batch ingest (``add_columnar_batch``): a durable batch (GPU-encoded
+        block) or a row batch (``persistence/columnar.py`` format, encoded here).  Returns the rows
+        added (0 for a replay the store already holds) once they are on disk (``wait``)."""
+        if is_durable_batch(payload):
+            d, blk = decode_durable_batch(payload)
+            if len(blk) < 64:
+                raise ValueError("durable batch without a block")
+            n = int(blk[:64].view(HDR)[0]["n_rows"])
+            if verify(blk):
+                raise ValueError("corrupt event block in a durable batch")
+            owner = payload
+            src = d.get("src") or None
+            if src is not None and not int(blk[:64].view(HDR)[0]["flags"]) & FLAG_COMMIT:
+                blk = blk.copy()                # the sender did not flag it: flag a copy
+                set_commit_flag(blk)
+                owner = blk
+            tok = self.add_block(blk.ctypes.data, len(blk), owner=owner, boot=d["boot"], asg=d.get("asg"),
+                                 names=d.get("names"), rules=d.get("rules"), src=src)
+        else:
+            from .columnar import decode_batch
+            d = decode_batch(payload)
+            rows = d["rows"]
+            n = len(rows)
+            blk = encode_block(rows)
+            seal(blk, int(d["first_seq"]), int(d["now"]), boot_id(d["boot"]), int(d["rank"]), int(d["world"]))
+            src = d.get("src") or None
+            if src is not None:
+                set_commit_flag(blk)
+            tok = self.add_block(blk.ctypes.data, len(blk), owner=blk, boot=d["boot"], asg=d.get("asg"),
+                                 names=d.get("names"), rules=d.get("rules"), src=src)
+        if tok < 0:
+            return 0
+        if wait and not self.wait(tok):
+            raise TimeoutError("event block not durable in time")
+        return n
+
+    @property
     def rows(self) -> int:
+        """Rows on disk (retention included)."""
         return int(self.seg.index()["n_rows"].sum())
 
     def count(self) -> int:
-        return self.rows() + self._objects.count()
+        return self.rows + self._objects.count()
 
     def add_events(self, events):
         return self._objects.add_events(events)

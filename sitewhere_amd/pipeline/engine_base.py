@@ -61,6 +61,10 @@ class StepResult:
     # (buffer, offset) when ``out`` sits at ``offset`` of a pooled pinned buffer with free bytes in
     # front of it: a columnar batch can be framed around the rows in place (``frame_columnar``)
     frame_base: tuple | None = None
+    # the step's sealed durable block (``persistence/segments.py``) when the engine encodes blocks
+    # (``encode_blocks``); ``block_frame`` = (buffer, offset) as for ``frame_base``
+    block: np.ndarray | None = None
+    block_frame: tuple | None = None
 
     def event_ids(self) -> np.ndarray:
         n = 0 if self.out is None else len(self.out)

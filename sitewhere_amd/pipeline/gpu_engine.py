@@ -60,11 +60,13 @@ class HostBuffer:
 
 class _Submitted:
     """One batch in :meth:`GpuInboundEngine.submit_framed`'s pipeline."""
-    __slots__ = ("slot", "batch", "token", "small", "rows", "sig", "ev")
+    __slots__ = ("slot", "batch", "token", "small", "rows", "sig", "ev", "bmeta", "bbuf", "bsig", "bev", "now")
 
     def __init__(self, slot, batch, token):
         self.slot, self.batch, self.token = slot, batch, token
         self.small = self.rows = self.sig = self.ev = None
+        self.bmeta = self.bbuf = self.bsig = self.bev = None
+        self.now = 0
 
 
 class _FramedSlots:
@@ -527,7 +529,7 @@ class GpuInboundEngine(EngineBase):
             # is CPU-uncached (~2.6 GB/s measured, 0.8 ms per 64K rows; profiles/r1_tenant_step)
             sel = self.step_async(raw_dev, off_dev, n_msgs, now_ms, presence=do_presence, out_to_device=True)
             self._sync_streams()
-            return self.collect(sel, raw, from_device=True)
+            return self._with_block(self.collect(sel, raw, from_device=True), sel, now_ms)
 
     def step_framed(self, batch, now_ms: int, presence: bool | None = None) -> StepResult:
         """Synchronous step of a raw-payload record read from the bus: the payload (with its padding)
@@ -563,7 +565,17 @@ class GpuInboundEngine(EngineBase):
             do_presence = self.presence_due(now_ms) if presence is None else presence
             sel = self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_to_device=True)
             self._sync_streams()
-            return self.collect(sel, np.asarray(batch.payload), from_device=True)
+            return self._with_block(self.collect(sel, np.asarray(batch.payload), from_device=True), sel, now_ms)
+
+    # durable blocks of service tenants (``storage: durable``): every step's block is encoded on the
+    # MI355X and returned with its result (``StepResult.block``), sealed with ``block_boot``
+    encode_blocks = False
+    block_boot = 0
+
+    def _with_block(self, res: StepResult, sel: int, now_ms: int) -> StepResult:
+        if self.encode_blocks:
+            res.block = self.encode_block(now_ms, res, slot=sel, boot=self.block_boot)
+        return res
 
     def _no_framed_pending(self):
         fp = self.__dict__.get("_fp")
@@ -594,7 +606,7 @@ class GpuInboundEngine(EngineBase):
     ROW_HEADROOM = 1 << 16      # bytes kept free in front of the rows: a columnar batch header is
                                 # written there, making header + rows one contiguous payload
 
-    def _pinned_out(self, nbytes: int):
+    def _pinned_out(self, nbytes: int, kind: str = "rows"):
         """A pinned host buffer (torch tensor + its full numpy view) with ``ROW_HEADROOM`` bytes in
         front of the rows, that no earlier StepResult still references: a live ``result.out`` view
         pins its base array, so results are returned without a copy and without fresh pageable pages
@@ -602,16 +614,22 @@ class GpuInboundEngine(EngineBase):
         retained (``StepResult.frame_base`` is left unset)."""
         import sys
         need = nbytes + self.ROW_HEADROOM
-        pool = self.__dict__.setdefault("_pin_pool", [])
-        spill = self.__dict__.setdefault("_pin_spill", [])
-        st = self.__dict__.setdefault("pin_stats", {"reused": 0, "new_pooled": 0, "spill": 0, "new_unpooled": 0})
+        sfx = "" if kind == "rows" else "_" + kind
+        pool = self.__dict__.setdefault("_pin_pool" + sfx, [])
+        spill = self.__dict__.setdefault("_pin_spill" + sfx, [])
+        st = self.__dict__.setdefault("pin_stats" + sfx, {"reused": 0, "new_pooled": 0, "spill": 0,
+                                                          "new_unpooled": 0})
         for pin, arr in pool:
             if arr.nbytes >= need and sys.getrefcount(arr) <= 3:   # pool tuple, loop variable, the call
                 st["reused"] += 1
                 return pin, arr, True
         # sized to this step's rows plus slack (steps of one tenant are about the same size), not to
         # the engine's full output capacity: pinning a buffer costs time in proportion to its size
-        full = self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM
+        if kind == "rows":
+            full = self.out_cap * OUT_REC_SIZE + self.ROW_HEADROOM
+        else:
+            from ..persistence.segments import max_block_bytes
+            full = max_block_bytes(self.out_cap) + self.ROW_HEADROOM
         size = max(need, min(full, -(-(need + need // 4) // (1 << 20)) * (1 << 20)))
         # results held by an overlapped tenant: in flight + store queue + storing, and -- with zero-copy
         # columnar payloads -- the batches the store and the enriched-batch topic retain
@@ -731,10 +749,13 @@ class GpuInboundEngine(EngineBase):
             do_presence = self.presence_due(now_ms) if presence is None else presence
             self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_sel=b,
                             out_to_device=True)
+            sub = _Submitted(b, batch, token)
+            if self.encode_blocks:
+                sub.bmeta, sub.now = self.encode_block_async(b), now_ms
             fp.ev_comp[b].record(cur)
             if prev is not None:
                 self._framed_rows_start(prev)
-            fp.inflight.append(_Submitted(b, batch, token))
+            fp.inflight.append(sub)
             fp.k += 1
             return done
 
@@ -757,7 +778,10 @@ class GpuInboundEngine(EngineBase):
         return EngineBase.framed_pending.fget(self) + (len(fp.inflight) if fp is not None else 0)
 
     def _framed_rows_start(self, s: "_Submitted"):
-        """Start copying the rows of completed step ``s`` to a pinned host buffer."""
+        """Start copying the rows (and the durable block) of completed step ``s`` to pinned host
+        buffers."""
+        if s.bmeta is not None:
+            self._framed_block_start(s)
         nb = s.small["n_persisted"] * OUT_REC_SIZE
         s.rows = self._pinned_out(nb)
         if not nb:
@@ -777,6 +801,47 @@ class GpuInboundEngine(EngineBase):
             s.ev = torch.cuda.Event()
             s.ev.record(fp.d2h)
 
+    def _framed_block_start(self, s: "_Submitted"):
+        nb, err, first = (int(x) for x in s.bmeta.cpu().numpy())
+        if err or nb <= 0 or nb > self._seg_buffers(s.slot)[3]:
+            raise RuntimeError(f"durable block encoder failed (bytes={nb}, errors={err})")
+        s.bmeta = (nb, first)
+        s.bbuf = self._pinned_out(nb, kind="blocks")
+        dst = s.bbuf[0].data_ptr() + self.ROW_HEADROOM
+        fp = self._fp
+        h = ctypes.c_uint64()
+        rc = 1 if fp.no_sdma else self.lib.sw_sdma_copy(ctypes.c_void_p(dst), ctypes.c_void_p(_ptr(self.block_device(s.slot))),
+                                                         nb, 0, ctypes.byref(h))
+        if rc == 0:
+            s.bsig = h.value
+            return
+        fp.no_sdma = True
+        with torch.cuda.stream(fp.d2h):
+            hr = self.ROW_HEADROOM
+            s.bbuf[0][hr:hr + nb].copy_(self.block_device(s.slot)[:nb], non_blocking=True)
+            s.bev = torch.cuda.Event()
+            s.bev.record(fp.d2h)
+
+    def _framed_block_finish(self, s: "_Submitted", res: StepResult):
+        from ..persistence.segments import seal
+        if s.bsig is not None:
+            rc = self.lib.sw_sdma_wait(s.bsig)
+            s.bsig = None
+            if rc:
+                raise RuntimeError(f"sw_sdma_wait failed ({rc})")
+        elif s.bev is not None:
+            s.bev.synchronize()
+        nb, first = s.bmeta
+        hr = self.ROW_HEADROOM
+        pin, arr, pooled = s.bbuf
+        blk = arr[hr:hr + nb]
+        seal(blk, first, s.now, self.block_boot, self.rank, self.world)
+        if pooled:
+            res.block, res.block_frame = blk, (arr, hr)
+        else:
+            res.block = blk.copy()          # spill buffer: reused by the next step
+        s.bbuf = s.bmeta = None
+
     def _framed_finish(self, s: "_Submitted"):
         if s.sig is not None:
             rc = self.lib.sw_sdma_wait(s.sig)
@@ -791,6 +856,8 @@ class GpuInboundEngine(EngineBase):
         res = StepResult(out=arr[hr:hr + nb].view(OUT_REC), world=self.world, rank=self.rank,
                          frame_base=(arr, hr) if pooled else None, **s.small)
         s.rows = None
+        if s.bmeta is not None:
+            self._framed_block_finish(s, res)
         return s.token, res
 
     # ------------------------------------------------------------------ durable blocks

@@ -135,6 +135,12 @@ class DeviceEventManagement:
             self._on_persisted(events)
         return len(events)
 
+    def durable_source_offset(self, topic: str, partition: int) -> int | None:
+        """Next input offset of (topic, partition) whose events the durable store holds (commit
+        records of engine tenants' blocks); None when the store keeps no such record."""
+        f = getattr(self.store, "source_offset", None)
+        return None if f is None else f(topic, int(partition))
+
     def add_columnar_batch(self, payload: bytes) -> int:
         """Append a columnar batch of GPU-enriched rows (MI355X tenants; needs the columnar datastore)."""
         if not hasattr(self.store, "add_columnar"):
@@ -220,6 +226,13 @@ class EventManagementTenantEngine(MicroserviceTenantEngine):
 
         self.management = DeviceEventManagement(self.store, lookup, triggers, bool(self.config.get("buffered")))
         self.api = {"DeviceEventManagement": self.management}
+
+    def tenant_stop(self, monitor):
+        self.management.flush()
+        close = getattr(self.store, "close", None)
+        if close is not None and hasattr(self.store, "seg"):
+            close()                     # durable segments: a restarted engine reopens the directory
+        super().tenant_stop(monitor)
 
 
 class EventManagementMicroservice(MultitenantMicroservice):

@@ -85,7 +85,9 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.t_failed_decode = n.failed_decode_events(t)
         self.routed_payloads = 0                # payloads the slow path parsed (per payload, not per batch)
         self.t_enriched_batches = n.tenant_prefix(t) + ENRICHED_BATCHES
-        self.storage = cfg.get("storage", "objects")            # objects | columnar
+        # objects: per-event host objects; columnar: row batches; durable: encoded blocks (GPU-encoded
+        # on the MI355X) to a durable segment store, offsets committed once on disk
+        self.storage = cfg.get("storage", "objects")            # objects | columnar | durable
         self.publish = cfg.get("publishEnriched", "events")     # events | batches | none
         self._asg_dirty: set[int] = set()
         self._names_sent = 0
@@ -96,7 +98,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         ecfg.presence_check_ms = int(cfg.get("presenceCheckMs", ecfg.presence_check_ms))
         self.engine_cfg = ecfg
         self.engine = self._make_engine(cfg.get("device", "auto"), ecfg)
-        if self.storage == "columnar" and cfg.get("retainHostAllocations", True):
+        if self.storage in ("columnar", "durable") and cfg.get("retainHostAllocations", True):
             retain_large_allocations()          # multi-MB columnar batches per step: no fresh mmaps
         self.dev_index, self.asg_index = IndexMap(), IndexMap()
         self.customers, self.areas, self.assets = IndexMap(), IndexMap(), IndexMap()
@@ -105,6 +107,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._nid2name: dict[int, str] = {}
         self._lock = threading.RLock()
         self.boot = f"{int(time.time() * 1000):x}"
+        self._set_boot(self.boot)
         self.zone_tests = [ZoneTest(z["zoneToken"], z.get("condition", "inside"), z.get("alertType", "zone.alert"),
                                     int(z.get("alertLevel", 1)), z.get("alertMessage", ""))
                            for z in cfg.get("zoneTests", [])]
@@ -121,7 +124,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # runs on a store thread, overlapped with the next engine step.  Raw-topic offsets are then
         # committed by that thread once a batch is stored (at-least-once holds); with a checkpoint
         # the snapshot owns the commits.
-        self.async_store = bool(cfg.get("asyncStore", self.storage == "columnar"))
+        self.async_store = bool(cfg.get("asyncStore", self.storage in ("columnar", "durable")))
         # opt-in: columnar payloads framed around the rows in the engine's pinned row buffers (no
         # host copy).  The enriched-batch topic and the columnar store then hold those buffers until
         # their retention drops them, so it pays only when both windows fit the engine's buffer pool
@@ -197,6 +200,21 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         from ..pipeline.native_engine import NativeCpuEngine
         return NativeCpuEngine(ecfg, threads=int(self.config.get("cpuThreads", 0)) or None)
 
+    def _set_boot(self, boot: str):
+        """Engine incarnation: event ids are ``<boot>-<id>``; durable blocks carry it numerically."""
+        from ..persistence.segments import boot_id
+        self.boot = boot
+        self.block_boot = boot_id(boot)
+        if self.storage == "durable" and hasattr(self.engine, "encode_blocks"):
+            self.engine.encode_blocks = True            # MI355X: blocks encoded on the GPU per step
+            self.engine.block_boot = self.block_boot
+
+    def _ensure_block(self, res, now: int):
+        """Host engines encode the step's block on the completing thread (their event ring is
+        overwritten by later steps)."""
+        if self.storage == "durable" and res is not None and res.block is None:
+            res.block = self.engine.encode_block(now, res, boot=self.block_boot)
+
     # ---------------------------------------------------------------- registry mirror
     def _dm(self):
         return self.ms.api("DeviceManagement", self.tenant.token)
@@ -271,6 +289,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if self.config.get("tuneGc", False):
             tune_gc_for_streaming()             # opt-in: measured gain is within run-to-run noise
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
+        self._resume_from_store()
         if self.async_store:
             self._store_thread = threading.Thread(target=self._store_loop, daemon=True,
                                                   name=f"engine-store-{self.tenant.token}")
@@ -319,7 +338,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             return False
         with self._lock:
             extra = self.engine.load_checkpoint(self.ckpt_path)
-            self.boot = extra["boot"]
+            self._set_boot(extra["boot"])
             for name in ("dev_index", "asg_index", "customers", "areas", "assets"):
                 m = getattr(self, name)
                 for key in extra[name]:
@@ -405,6 +424,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             if item.trace is not None:
                 item.trace.append(time.perf_counter())
             self.processed_events.mark(res.n_events)
+            self._ensure_block(res, item.now)
             item.res, item.routed_recs, item.batch = res, self._route(item.batch, res), None
             if item.hold is not None:
                 self._hold(item.hold, -1)
@@ -478,6 +498,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         with self._lock, self.step_timer.time():
             res = self.engine.step_framed(batch, now)
         self.processed_events.mark(res.n_events)
+        self._ensure_block(res, now)
         item = _Stepped(key, res, now, None)
         item.routed_recs = self._route(batch, res)
         if key is not None:
@@ -513,10 +534,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if tr is not None:
             tr.append(time.perf_counter())
         if not item.stored:
-            if self.storage == "columnar":
+            if self.storage in ("columnar", "durable"):
                 with self.store_timer.time():
                     if item.payload is None:    # built once: it carries the dictionary deltas
-                        item.payload = self.columnar_payload(res, now, tr)
+                        item.payload = self.durable_payload(res, item.key) if self.storage == "durable" \
+                            else self.columnar_payload(res, now, tr)
                     if tr is not None:
                         tr.append(time.perf_counter())
                     n = self._em().add_columnar_batch(item.payload)
@@ -532,7 +554,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             item.stored = True
         if not item.published:
             with self.publish_timer.time():
-                if self.storage == "columnar" and self.publish == "batches":
+                if self.storage in ("columnar", "durable") and self.publish == "batches":
                     bus = self.ms.instance.bus
                     pl = item.payload
                     if hasattr(bus, "append_external"):   # in place: the log references the payload
@@ -583,8 +605,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if self._store_thread is not None:
             self._store_q.join()
 
-    def columnar_payload(self, res, now: int, tr: list | None = None) -> bytes:
-        """Rows + the dictionary entries the receiver has not seen yet (assignment context, names)."""
+    def _dict_deltas(self, tr: list | None = None):
+        """(assignment contexts, names) the receiver has not seen yet, and the rule messages."""
         with self._lock:
             if tr is not None:
                 tr.append(time.perf_counter())
@@ -602,6 +624,51 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             names = dict(self._nid2name) if len(self._nid2name) != self._names_sent else {}
             self._names_sent = len(self._nid2name)
         rules = {t.alert_type: t.alert_message for t in self.engine.tests}
+        return asg, names, rules
+
+    def durable_payload(self, res, key=None):
+        """The step's sealed block + dictionary deltas (``segments.encode_durable_batch``), framed in
+        front of the block in its pinned buffer when there is room (no copy; the block then goes to
+        the disk with O_DIRECT from that buffer).  ``key`` = (topic, partition, offset) of the raw
+        record: the store writes the next offset as the block's commit record, so after a crash the
+        tenant resumes exactly behind the last durable block (:meth:`_resume_from_store`)."""
+        from ..persistence.segments import encode_durable_batch, frame_durable_batch, set_commit_flag
+        asg, names, rules = self._dict_deltas()
+        src = None
+        if key is not None:
+            src = [(key[0], key[1], key[2] + 1)]
+            set_commit_flag(res.block)
+        if res.block_frame is not None:
+            v = frame_durable_batch(res.block_frame, len(res.block), self.boot, asg, names, rules, src)
+            if v is not None:
+                self.zc_framed += 1
+                return v
+        self.zc_copied += 1
+        return encode_durable_batch(res.block, self.boot, asg, names, rules, src)
+
+    def _resume_from_store(self):
+        """Durable storage: move the raw consumer's committed offsets up to what the event store's
+        commit records say is on disk (the bus commit trails the disk by one store step, and is lost
+        with a volatile bus).  Records behind that offset are never stepped again.  With a checkpoint
+        the snapshot owns the offsets instead: the batches after it are replayed to rebuild engine
+        state, and the store skips their rows by (boot, sequence)."""
+        if self.storage != "durable" or self.ckpt_path:
+            return
+        bus = self.ms.instance.bus
+        em = self._em()
+        if not hasattr(em, "durable_source_offset"):
+            return
+        group = self.raw_consumer.group
+        for topic in self.raw_consumer.topics:
+            for p in range(bus.partitions(topic) if hasattr(bus, "partitions") else 1):
+                o = em.durable_source_offset(topic, p)
+                if o is not None and o > (bus.committed(group, topic, p) or 0):
+                    bus.commit(group, topic, p, o)
+                    self.logger.info("resuming %s[%d] at %d (durable in the event store)", topic, p, o)
+
+    def columnar_payload(self, res, now: int, tr: list | None = None) -> bytes:
+        """Rows + the dictionary entries the receiver has not seen yet (assignment context, names)."""
+        asg, names, rules = self._dict_deltas(tr)
         out = res.out if res.out is not None else np.zeros(0, OUT_REC)
         if tr is not None:
             tr.append(time.perf_counter())

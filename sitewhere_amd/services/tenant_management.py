@@ -102,13 +102,22 @@ TENANT_TEMPLATES["gpu"]["services"]["event-sources"].update(rawBatchSize=65536, 
 # High-throughput MI355X tenant: enriched rows stay columnar end to end (no per-event host objects).
 TENANT_TEMPLATES["gpu-columnar"] = copy.deepcopy(TENANT_TEMPLATES["gpu"])
 TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event store"
+# Each engine step's events become one compressed block (~8-16 B/event, encoded on the MI355X) that
+# event management appends to durable segment files (O_DIRECT + fdatasync group commit); raw-topic
+# offsets are committed once the block is on disk.  Retention by bytes (0 = keep everything).
 TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
-    storage="columnar", publishEnriched="batches",
+    storage="durable", publishEnriched="batches",
     capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
               "dedup_slots": 1 << 18, "gen_cap": 32768})
-# in-memory columnar store: newest 2^28 rows (8 GB of 32 B rows) held, older batches evicted
-TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {"datastore": {"type": "columnar",
-                                                                                  "retentionRows": 1 << 28}}
+TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
+    "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
+                  "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}
+# volatile variant (benchmarks of the pipeline alone): rows kept in host memory, newest 2^28 held
+TENANT_TEMPLATES["gpu-memory"] = copy.deepcopy(TENANT_TEMPLATES["gpu-columnar"])
+TENANT_TEMPLATES["gpu-memory"]["name"] = "MI355X pipeline, in-memory columnar event store"
+TENANT_TEMPLATES["gpu-memory"]["services"]["inbound-processing"]["storage"] = "columnar"
+TENANT_TEMPLATES["gpu-memory"]["services"]["event-management"] = {"datastore": {"type": "columnar",
+                                                                                "retentionRows": 1 << 28}}
 
 DATASET_TEMPLATES = {
     "empty": {"name": "Empty dataset", "description": "No data is created."},

@@ -9,6 +9,10 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # durable tenant stores (segments) of this test process go to a fresh directory
+    if "SITEWHERE_DATA_DIR" not in os.environ:
+        import tempfile
+        os.environ["SITEWHERE_DATA_DIR"] = tempfile.mkdtemp(prefix="sw-test-data-")
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")
 

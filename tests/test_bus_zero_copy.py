@@ -88,11 +88,19 @@ def test_bytes_values_are_published_by_reference():
     assert bus.read("b", 0, off)[0].value == v
 
 
-def test_durable_partitions_refuse_zero_copy(tmp_path):
+def test_durable_partitions_copy_zero_copy_records(tmp_path):
+    """A durable partition writes a zero-copy record to its files (a copy) and releases the owner
+    at once; the record survives a reopen."""
+    released = []
     bus = EventBus(str(tmp_path / "log"), default_partitions=1)
-    with pytest.raises(RuntimeError, match="durable"):
-        _ext(bus, "d", b"v")
-    assert bus.end_offset("d", 0) == 0 and not bus._ext
+    buf, off = _ext(bus, "d", b"value", key=b"k", released=released)
+    assert off == 0 and bus.end_offset("d", 0) == 1 and not bus._ext and len(released) == 1
+    buf[:] = 0                                  # the owner is free: the log holds its own copy
+    r = bus.read("d", 0, 0)[0]
+    assert (r.key, r.value) == (b"k", b"value")
+    bus.close()
+    bus = EventBus(str(tmp_path / "log"), default_partitions=1)
+    assert bus.read("d", 0, 0)[0].value == b"value"
     bus.close()
 
 

@@ -165,8 +165,12 @@ def test_whole_instance_on_protobuf_topics(protobuf_codec):
         es = sw.tenant_engine("event-sources")
         em_engine = sw.tenant_engine("event-management")
         base = em_engine.store.count()
+        t0 = int(time.time() * 1000)
         for i in range(40):
-            es.inject("default-protobuf", wire.measurements("meitrack-002", {"pb": float(i)}, alternate_id=f"pb-{i}"))
+            # strictly increasing event dates: device state keeps the newest by date, and events
+            # injected within one millisecond would tie
+            es.inject("default-protobuf", wire.measurements("meitrack-002", {"pb": float(i)}, alternate_id=f"pb-{i}",
+                                                            event_date=t0 + i))
         es.inject("default-protobuf", wire.measurements("ghost-pb", {"x": 1.0}))
         end = time.time() + 30
         while em_engine.store.count() - base < 40 and time.time() < end:

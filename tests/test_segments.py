@@ -232,7 +232,7 @@ def test_block_sink_pool_bounded_and_commits_in_order(tmp_path):
     sink.flush()
     tags += sink.committable()
     assert tags == list(range(60))
-    assert sink.n_alloc <= 16 and store.rows() == sum(20000 + 1000 * k for k in range(60))
+    assert sink.n_alloc <= 16 and store.rows == sum(20000 + 1000 * k for k in range(60))
     # the topic carries the sealed blocks
     v = bus.read_views("t.out", 0, bus.begin_offset("t.out", 0), 1)[0].value
     assert sg.verify(np.frombuffer(v, np.uint8)) == 0

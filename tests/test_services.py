@@ -466,7 +466,7 @@ def test_gpu_tenant_checkpoint_resume_replays_exactly(tmp_path):
         assert wait_until(lambda: ib.engine.stats_dict()["persisted"] == 100, 20)
         assert ib.checkpoints == 2                       # after batches 2 and 4; batch 5 not yet covered
         store = inst.tenant_engine("event-management", "ck").store
-        assert store.rows == 100
+        assert wait_until(lambda: store.rows == 100, 20)      # stored (on disk) on the store thread
         ib._since_ckpt = 0                               # "crash": no final snapshot on stop
         ib2 = reconfigure(2)
         assert ib2 is not ib
