@@ -283,6 +283,34 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
 // sw_gen_payloads): every payload whose body ends with field 15 = "<16 hex>-<8 hex>" gets `epoch`,
 // so a replayed batch carries fresh alternate ids.  Split over `threads` threads (0 = 8).
 // Returns the number of payloads stamped.
+// Varint length stream (pipeline/framing.py) -> u32 offsets[n_msgs + 1] in one pass, validating
+// the framing of a raw batch record: 0 ok, -1 truncated stream, -2 over-long varint, -3 length
+// count != n_msgs, -4 lengths do not sum to payload_bytes.
+int32_t sw_varint_offsets(const uint8_t* lens, int64_t nbytes, int64_t n_msgs, int64_t payload_bytes, uint32_t* offs) {
+  int64_t k = 0;
+  uint64_t cur = 0, acc = 0;
+  int shift = 0;
+  offs[0] = 0;
+  for (int64_t i = 0; i < nbytes; ++i) {
+    const uint8_t b = lens[i];
+    if (shift > 28) return -2;
+    cur |= (uint64_t)(b & 0x7f) << shift;
+    if (b & 0x80) {
+      shift += 7;
+      continue;
+    }
+    if (k >= n_msgs) return -3;
+    acc += cur;
+    if (acc > 0xffffffffull) return -4;
+    offs[++k] = (uint32_t)acc;
+    cur = 0;
+    shift = 0;
+  }
+  if (shift) return -1;
+  if (k != n_msgs) return -3;
+  return (int64_t)acc == payload_bytes ? 0 : -4;
+}
+
 int64_t sw_stamp_alt_epoch(uint8_t* raw, const uint32_t* offs, int64_t n, uint64_t epoch, int32_t threads) {
   char hex[17];
   snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)epoch);

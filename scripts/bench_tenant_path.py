@@ -183,6 +183,9 @@ def main():
                       "gc": args.gc, "zero_copy_rows": ib.zero_copy_rows,
                       "payloads_framed": ib.zc_framed, "payloads_copied": ib.zc_copied,
                       "pinned_rows": getattr(ib.engine, "pin_stats", None),
+                      "pinned_blocks": getattr(ib.engine, "pin_stats_blocks", None),
+                      "framed_trace_ms_per_batch": {k: round(1000 * v / (args.warmup + args.batches), 3)
+                                                    for k, v in (getattr(ib.engine, "framed_trace", None) or {}).items()},
                       "overlap_steps": ib.overlap,
                       "events": ev,
                       "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,

@@ -11,8 +11,8 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 for B in 262144 1048576; do
   for P in 0 0.01; do
-    timeout -k 10 400 python -u scripts/bench_tenant_path.py --devices 100000 --batch $B --batches 30 --warmup 4 \
+    SW_FRAMED_TRACE=1 SW_TENANT_TRACE=1 timeout -k 10 400 python -u scripts/bench_tenant_path.py --devices 50000 --batch $B --batches 30 --warmup 4 \
       --via-bus --max-msgs $B --p-unregistered $P > "$O/tenant_${B}_${P}.log" 2>&1 || { tail -20 "$O/tenant_${B}_${P}.log"; exit 1; }
-    tail -1 "$O/tenant_${B}_${P}.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["batch"], d["p_unregistered"], round(d["events_per_sec"]/1e6,1), "M/s", d["ms_per_batch"], "ms", d["store"], d["mean_ms"])'
+    tail -1 "$O/tenant_${B}_${P}.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["batch"], d["p_unregistered"], round(d["events_per_sec"]/1e6,1), "M/s", d["ms_per_batch"], "ms", d["mean_ms"], d.get("median_ms_second_half"), d["framed_trace_ms_per_batch"])'
   done
 done

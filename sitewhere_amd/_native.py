@@ -174,6 +174,7 @@ def native():
         _proto(lib, "swseg_dates", None, P, P, P)
         _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)
         _proto(lib, "swss_append", c_int32, P, P, c_int64, c_int64)
+        _proto(lib, "sw_varint_offsets", c_int32, P, c_int64, c_int64, c_int64, P)
         _proto(lib, "swss_append_commit", c_int32, P, P, c_int64, c_int64, P, P, c_int32)
         _proto(lib, "swss_sources", c_int64, P, P, P, c_int64)
         _proto(lib, "swseg_set_flags", None, P, c_int32)

@@ -15,6 +15,7 @@ auto-creation.
 from __future__ import annotations
 
 import ctypes
+import os
 import itertools
 import struct
 import threading
@@ -116,6 +117,9 @@ class EventBus:
             retention_bytes = 0 if directory else (1 << 30)
         self.lib.swlog_set_retention(self.h, -1, int(retention_bytes))
         self.directory = directory
+        # identity of this log's offsets: a memory-only log starts over at offset 0 each time, so
+        # offsets recorded elsewhere (durable commit records) are scoped by it
+        self.incarnation = self._incarnation(directory)
         self.default_partitions = default_partitions
         self.session_timeout_s = session_timeout_s
         self._topics: dict[str, int] = {}
@@ -146,6 +150,26 @@ class EventBus:
         if n is None:
             n = self._nparts[name] = self.fast.swlog_partitions(self.h, self.topic(name))
         return n
+
+    @staticmethod
+    def _incarnation(directory: str | None) -> str:
+        import uuid
+        if not directory:
+            return uuid.uuid4().hex
+        path = os.path.join(directory, "bus.id")
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except FileNotFoundError:
+            os.makedirs(directory, exist_ok=True)
+            ident = uuid.uuid4().hex
+            tmp = path + ".tmp"
+            with open(tmp, "w") as f:
+                f.write(ident)
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, path)
+            return ident
 
     def topics(self) -> list[str]:
         with self._lock:
@@ -415,8 +439,10 @@ class EventBus:
         ko = np.ascontiguousarray(key_off, np.int64)
         vo = np.ascontiguousarray(val_off, np.int64)
         tsa = np.full(n, ts if ts is not None else int(time.time() * 1000), np.int64)
-        first = self.fast.swlog_append_batch(self.h, t, partition, kb.ctypes.data, ko.ctypes.data, vb.ctypes.data,
-                                            vo.ctypes.data, tsa.ctypes.data, n)
+        # a multi-MB copy releases the GIL (CDLL); small batches stay on the GIL-holding fast path
+        fn = self.lib if vb.nbytes >= (1 << 20) else self.fast
+        first = fn.swlog_append_batch(self.h, t, partition, kb.ctypes.data, ko.ctypes.data, vb.ctypes.data,
+                                      vo.ctypes.data, tsa.ctypes.data, n)
         if first < 0:
             raise RuntimeError(f"append to {name}[{partition}] failed")
         self._wake(name)

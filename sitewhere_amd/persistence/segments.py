@@ -586,12 +586,24 @@ class DurableEventStore(DeviceEventStore):
         """Event management's batch ingest (``add_columnar_batch``): a durable batch (GPU-encoded
         block) or a row batch (``persistence/columnar.py`` format, encoded here).  Returns the rows
         added (0 for a replay the store already holds) once they are on disk (``wait``)."""
+        n, tok = self.add_batch(payload)
+        if tok < 0:
+            return 0
+        if wait and not self.wait(tok):
+            raise TimeoutError("event block not durable in time")
+        return n
+
+    def add_batch(self, payload) -> tuple[int, int]:
+        """:meth:`add_columnar` without the wait: (rows, store token; -1 = a replay already held).
+        The rows are durable once :meth:`durable` reaches the token."""
         if is_durable_batch(payload):
             d, blk = decode_durable_batch(payload)
             if len(blk) < 64:
                 raise ValueError("durable batch without a block")
             n = int(blk[:64].view(HDR)[0]["n_rows"])
-            if verify(blk):
+            # bytes crossed a process boundary (RPC / Kafka): check every page; an in-process view
+            # of the engine's buffer was sealed here a moment ago
+            if isinstance(payload, (bytes, bytearray, memoryview)) and verify(blk):
                 raise ValueError("corrupt event block in a durable batch")
             owner = payload
             src = d.get("src") or None
@@ -613,11 +625,7 @@ class DurableEventStore(DeviceEventStore):
                 set_commit_flag(blk)
             tok = self.add_block(blk.ctypes.data, len(blk), owner=blk, boot=d["boot"], asg=d.get("asg"),
                                  names=d.get("names"), rules=d.get("rules"), src=src)
-        if tok < 0:
-            return 0
-        if wait and not self.wait(tok):
-            raise TimeoutError("event block not durable in time")
-        return n
+        return (n, tok) if tok >= 0 else (0, -1)
 
     @property
     def rows(self) -> int:

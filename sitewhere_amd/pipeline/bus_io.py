@@ -34,7 +34,8 @@ import numpy as np
 
 from ..bus.log import EventBus
 from ..models.columnar import OUT_REC
-from .framing import offsets_from_varint, varint_lengths
+from .._native import native
+from .framing import varint_lengths
 
 RAW_MAGIC = b"SWRB"
 OUT_MAGIC = b"SWOB"
@@ -126,12 +127,22 @@ class RawBatch:
         self.n_msgs, self.payload_bytes, self.payload, self.lens, self._offs = \
             n_msgs, payload_bytes, payload, lens, offs
 
+    _ERR = {-1: "truncated varint length stream", -2: "over-long varint length",
+            -3: "length count does not match the payload count", -4: "lengths do not sum to the payload bytes"}
+
     def offsets(self) -> np.ndarray:
+        """u32 offsets [n + 1] of the payloads, validating the framing (one native pass; the numpy
+        form, ``framing.offsets_from_varint``, is the reference)."""
         if self._offs is None:
-            offs = offsets_from_varint(self.lens)
-            if len(offs) != self.n_msgs + 1 or int(offs[-1]) != self.payload_bytes:
-                raise ValueError(f"raw batch framing mismatch: {len(offs) - 1} lengths summing to {int(offs[-1])} "
-                                 f"for {self.n_msgs} payloads of {self.payload_bytes} bytes")
+            if self.n_msgs < 0:
+                raise ValueError("corrupt raw batch header")
+            offs = np.empty(self.n_msgs + 1, np.uint32)
+            lens = np.ascontiguousarray(self.lens, np.uint8)
+            rc = native().sw_varint_offsets(lens.ctypes.data if len(lens) else None, len(lens), self.n_msgs,
+                                            self.payload_bytes, offs.ctypes.data)
+            if rc:
+                raise ValueError(f"raw batch framing mismatch: {self._ERR.get(rc, rc)} "
+                                 f"({self.n_msgs} payloads of {self.payload_bytes} bytes)")
             self._offs = offs
         return self._offs
 

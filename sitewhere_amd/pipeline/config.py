@@ -39,7 +39,9 @@ class EngineConfig:
         if self.state_slots <= 0:
             self.state_slots = 16 * self.max_assignments
         self.reg_slots = pow2_at_least(2 * self.max_devices)
-        self.dedup_slots = pow2_at_least(self.dedup_slots)
+        # a generation must take a whole batch at <= 50% load (rotation happens before a step that
+        # would pass that): smaller tables overflow on every step and probe to their limit
+        self.dedup_slots = pow2_at_least(max(self.dedup_slots, 2 * self.rec_cap))
         self.name_slots = pow2_at_least(self.name_slots)
         self.state_slots = pow2_at_least(self.state_slots)
         self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + self.shuffle_pad

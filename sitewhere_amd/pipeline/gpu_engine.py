@@ -15,6 +15,7 @@ on three streams.
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -716,6 +717,8 @@ class GpuInboundEngine(EngineBase):
             raise ValueError(f"batch of {n} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
         if nb < batch.payload_bytes + _ALIGN:
             raise ValueError("raw batch payload lacks its tail padding")
+        tr = self.framed_trace
+        t0 = time.perf_counter() if tr is not None else 0.0
         with self._lock:
             if getattr(self, "_lagged", None) is not None:      # a host-lagged batch (no lens) first
                 done = EngineBase.drain_framed(self)
@@ -737,12 +740,18 @@ class GpuInboundEngine(EngineBase):
                 if lt is not None:
                     dev_l[:nl].copy_(lt, non_blocking=True)
                 fp.ev_h2d[b].record(fp.h2d)
+            t0 = self._ft("h2d_enqueue", t0)
             while len(fp.inflight) > 1 or (fp.inflight and fp.inflight[0].rows is not None):
                 done.append(self._framed_finish(fp.inflight.popleft()))      # batch k-2
+            t0 = self._ft("finish_k2", t0)
             prev = fp.inflight[0] if fp.inflight else None
             if prev is not None:                                             # batch k-1
                 fp.ev_comp[prev.slot].synchronize()
+                t0 = self._ft("wait_k1", t0)
                 prev.small = self._collect_small(np.asarray(prev.batch.payload))
+                t0 = self._ft("collect_k1", t0)
+                self._block_meta(prev)              # before batch k is queued: no wait on it
+                t0 = self._ft("block_meta_k1", t0)
             cur = torch.cuda.current_stream(self.device)
             cur.wait_event(fp.ev_h2d[b])
             self.frame_varint(dev_l, nl, n, dev_o, batch.payload_bytes)
@@ -753,11 +762,24 @@ class GpuInboundEngine(EngineBase):
             if self.encode_blocks:
                 sub.bmeta, sub.now = self.encode_block_async(b), now_ms
             fp.ev_comp[b].record(cur)
+            t0 = self._ft("step_enqueue", t0)
             if prev is not None:
                 self._framed_rows_start(prev)
+            t0 = self._ft("copies_start_k1", t0)
             fp.inflight.append(sub)
             fp.k += 1
             return done
+
+    # SW_FRAMED_TRACE=1: host wall-clock per phase of submit_framed (seconds, summed)
+    framed_trace = {} if os.environ.get("SW_FRAMED_TRACE") == "1" else None
+
+    def _ft(self, name: str, t0: float) -> float:
+        tr = self.framed_trace
+        if tr is None:
+            return t0
+        t1 = time.perf_counter()
+        tr[name] = tr.get(name, 0.0) + (t1 - t0)
+        return t1
 
     def drain_framed(self) -> list:
         with self._lock:
@@ -768,6 +790,7 @@ class GpuInboundEngine(EngineBase):
                 if s.small is None:
                     fp.ev_comp[s.slot].synchronize()
                     s.small = self._collect_small(np.asarray(s.batch.payload))
+                    self._block_meta(s)
                     self._framed_rows_start(s)
                 done.append(self._framed_finish(s))
             return done
@@ -801,11 +824,18 @@ class GpuInboundEngine(EngineBase):
             s.ev = torch.cuda.Event()
             s.ev.record(fp.d2h)
 
-    def _framed_block_start(self, s: "_Submitted"):
+    def _block_meta(self, s: "_Submitted"):
+        """Encoder result of completed step ``s`` (read while nothing newer is queued)."""
+        if s.bmeta is None or isinstance(s.bmeta, tuple):
+            return
         nb, err, first = (int(x) for x in s.bmeta.cpu().numpy())
         if err or nb <= 0 or nb > self._seg_buffers(s.slot)[3]:
             raise RuntimeError(f"durable block encoder failed (bytes={nb}, errors={err})")
         s.bmeta = (nb, first)
+
+    def _framed_block_start(self, s: "_Submitted"):
+        self._block_meta(s)
+        nb = s.bmeta[0]
         s.bbuf = self._pinned_out(nb, kind="blocks")
         dst = s.bbuf[0].data_ptr() + self.ROW_HEADROOM
         fp = self._fp

@@ -141,6 +141,22 @@ class DeviceEventManagement:
         f = getattr(self.store, "source_offset", None)
         return None if f is None else f(topic, int(partition))
 
+    def add_durable_batch(self, payload) -> tuple[int, int]:
+        """Queue an engine tenant's durable batch: (rows, token).  The rows are on disk once
+        :meth:`durable_token` reaches the token (-1: a replay the store already holds)."""
+        add = getattr(self.store, "add_batch", None)
+        if add is None:                 # a store without durability tokens: synchronous
+            return self.add_columnar_batch(payload), -1
+        return add(payload)
+
+    def durable_token(self) -> int:
+        f = getattr(self.store, "durable", None)
+        return f() if f is not None else 1 << 62
+
+    def wait_durable(self, token: int, timeout_s: float = 60.0) -> bool:
+        f = getattr(self.store, "wait", None)
+        return True if f is None or token < 0 else bool(f(int(token), timeout_s))
+
     def add_columnar_batch(self, payload: bytes) -> int:
         """Append a columnar batch of GPU-enriched rows (MI355X tenants; needs the columnar datastore)."""
         if not hasattr(self.store, "add_columnar"):

@@ -58,7 +58,7 @@ class _Stepped:
     """A raw batch the engine has stepped, with the storage stages it has completed.  The raw bytes
     are not kept: rejected messages are routed (``_route``) as soon as the step completes."""
     __slots__ = ("key", "res", "now", "batch", "stored", "published", "routed", "queued", "payload", "events",
-                 "detach", "hold", "commit", "trace", "routed_recs")
+                 "detach", "hold", "commit", "trace", "routed_recs", "token")
 
     def __init__(self, key, res, now, batch):
         self.key, self.res, self.now, self.batch = key, res, now, batch
@@ -67,6 +67,7 @@ class _Stepped:
         self.detach, self.hold, self.commit = False, None, None
         self.trace = None
         self.routed_recs = None                 # the rejects, routed while the raw record was readable
+        self.token = None                       # durable storage: the store's token of the block
 
 
 class GpuInboundTenantEngine(InboundProcessingTenantEngine):
@@ -136,6 +137,12 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._sticky_part: int | None = None
         self.zc_framed = self.zc_copied = 0
         self._store_q: queue.Queue = queue.Queue(maxsize=2)
+        # durable storage: stored batches whose block is not on disk yet, in order -- their raw
+        # offsets commit (and the batch leaves _stepped) once the store's durable token passes theirs,
+        # so the store thread never sits in an fdatasync
+        from collections import deque
+        self._durable_wait: deque = deque()
+        self._durable_lock = threading.Lock()
         self._store_thread = None
         self._store_error = None
         # Overlapped engine steps (``overlapSteps``, default on for MI355X columnar tenants): a raw
@@ -534,10 +541,20 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if tr is not None:
             tr.append(time.perf_counter())
         if not item.stored:
-            if self.storage in ("columnar", "durable"):
+            if self.storage == "durable":
                 with self.store_timer.time():
                     if item.payload is None:    # built once: it carries the dictionary deltas
-                        item.payload = self.durable_payload(res, item.key) if self.storage == "durable" \
+                        item.payload = self.durable_payload(res, item.key, tr)
+                    if tr is not None:
+                        tr.append(time.perf_counter())
+                    n, item.token = self._em().add_durable_batch(item.payload)
+                    if tr is not None:
+                        tr.append(time.perf_counter())
+                self.persisted_events.mark(n)
+            elif self.storage == "columnar":
+                with self.store_timer.time():
+                    if item.payload is None:    # built once: it carries the dictionary deltas
+                        item.payload = self.durable_payload(res, item.key, tr) if self.storage == "durable" \
                             else self.columnar_payload(res, now, tr)
                     if tr is not None:
                         tr.append(time.perf_counter())
@@ -557,7 +574,13 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 if self.storage in ("columnar", "durable") and self.publish == "batches":
                     bus = self.ms.instance.bus
                     pl = item.payload
-                    if hasattr(bus, "append_external"):   # in place: the log references the payload
+                    if self.storage == "durable" and hasattr(bus, "append_arrays") and not isinstance(pl, bytes):
+                        # a copy into the log: the topic's retention would otherwise hold the engine's
+                        # pinned block buffers (the store releases them as soon as they are on disk)
+                        v = np.asarray(pl).reshape(-1)
+                        bus.append_arrays(self.t_enriched_batches, self._batch_partition(bus), np.zeros(1, np.uint8),
+                                          np.zeros(2, np.int64), v, np.array([0, v.nbytes], np.int64), ts=now)
+                    elif hasattr(bus, "append_external"):   # in place: the log references the payload
                         part = self._batch_partition(bus)
                         if isinstance(pl, bytes):
                             bus.append_bytes(self.t_enriched_batches, part, pl, ts=now)
@@ -572,6 +595,44 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if not item.routed:
             self._send_routed(item.routed_recs)
             item.routed = True
+        if self.storage == "durable" and (self._durable_wait or (item.token or 0) >= 0):
+            with self._durable_lock:
+                self._durable_wait.append((item, commit))
+            if self._store_thread is None:
+                self._reap_durable(block=True)
+            return
+        self._finalize(item, commit)
+
+    def _reap_durable(self, block: bool):
+        """Finalize the stored batches whose blocks are durable now (``block``: wait for all)."""
+        with self._durable_lock:
+            if not self._durable_wait:
+                return
+            em = self._em()
+            try:
+                d = em.durable_token()
+                while self._durable_wait:
+                    item, commit = self._durable_wait[0]
+                    if (item.token or 0) > d:
+                        if not block:
+                            return
+                        if not em.wait_durable(item.token, 60.0):
+                            raise TimeoutError("event block not durable after 60 s")
+                        d = em.durable_token()
+                        continue
+                    self._durable_wait.popleft()
+                    self._finalize(item, commit)
+            except Exception:
+                # nothing after the failure is durable: those batches are stored again on retry
+                for item, _ in self._durable_wait:
+                    item.stored = item.published = item.routed = False
+                    item.token = None
+                self._durable_wait.clear()
+                raise
+
+    def _finalize(self, item: "_Stepped", commit):
+        """A batch is fully stored: it leaves ``_stepped`` and its raw offset commits."""
+        tr = item.trace
         if item.key is not None:
             t, p, o = item.key
             self._stepped.pop(item.key, None)
@@ -584,14 +645,26 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
 
     def _store_loop(self):
         while True:
-            entry = self._store_q.get()
+            try:
+                # durable blocks in flight: wake up to commit their offsets once they are on disk
+                entry = self._store_q.get(timeout=0.002) if self._durable_wait else self._store_q.get()
+            except queue.Empty:
+                try:
+                    self._reap_durable(block=True)
+                except Exception as e:  # noqa: BLE001
+                    self._store_error = e
+                    self.logger.exception("engine store: durable wait failed")
+                continue
             try:
                 if entry is None:
+                    if self._store_error is None:
+                        self._reap_durable(block=True)
                     return
                 item, commit = entry
                 item.queued = False
                 if self._store_error is None:   # after a failure nothing is stored (or committed) past it
                     self._store_step(item, commit)
+                    self._reap_durable(block=False)
             except Exception as e:  # noqa: BLE001 -- surfaced before the next engine step
                 self._store_error = e
                 self.logger.exception("engine store step failed")
@@ -604,6 +677,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self._drain_engine()
         if self._store_thread is not None:
             self._store_q.join()
+            if self._store_error is None:
+                try:
+                    self._reap_durable(block=True)          # every stored block on disk, offsets committed
+                except Exception as e:  # noqa: BLE001
+                    self._store_error = e
 
     def _dict_deltas(self, tr: list | None = None):
         """(assignment contexts, names) the receiver has not seen yet, and the rule messages."""
@@ -626,17 +704,19 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         rules = {t.alert_type: t.alert_message for t in self.engine.tests}
         return asg, names, rules
 
-    def durable_payload(self, res, key=None):
+    def durable_payload(self, res, key=None, tr: list | None = None):
         """The step's sealed block + dictionary deltas (``segments.encode_durable_batch``), framed in
         front of the block in its pinned buffer when there is room (no copy; the block then goes to
         the disk with O_DIRECT from that buffer).  ``key`` = (topic, partition, offset) of the raw
         record: the store writes the next offset as the block's commit record, so after a crash the
         tenant resumes exactly behind the last durable block (:meth:`_resume_from_store`)."""
         from ..persistence.segments import encode_durable_batch, frame_durable_batch, set_commit_flag
-        asg, names, rules = self._dict_deltas()
+        asg, names, rules = self._dict_deltas(tr)
+        if tr is not None:
+            tr.append(time.perf_counter())
         src = None
         if key is not None:
-            src = [(key[0], key[1], key[2] + 1)]
+            src = [(self._src_topic(key[0]), key[1], key[2] + 1)]
             set_commit_flag(res.block)
         if res.block_frame is not None:
             v = frame_durable_batch(res.block_frame, len(res.block), self.boot, asg, names, rules, src)
@@ -645,6 +725,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 return v
         self.zc_copied += 1
         return encode_durable_batch(res.block, self.boot, asg, names, rules, src)
+
+    def _src_topic(self, topic: str) -> str:
+        """Input name in commit records: offsets only mean something within one incarnation of the
+        bus (a memory-only bus restarts at 0)."""
+        return f"{getattr(self.ms.instance.bus, 'incarnation', '')}/{topic}"
 
     def _resume_from_store(self):
         """Durable storage: move the raw consumer's committed offsets up to what the event store's
@@ -661,7 +746,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         group = self.raw_consumer.group
         for topic in self.raw_consumer.topics:
             for p in range(bus.partitions(topic) if hasattr(bus, "partitions") else 1):
-                o = em.durable_source_offset(topic, p)
+                o = em.durable_source_offset(self._src_topic(topic), p)
                 if o is not None and o > (bus.committed(group, topic, p) or 0):
                     bus.commit(group, topic, p, o)
                     self.logger.info("resuming %s[%d] at %d (durable in the event store)", topic, p, o)

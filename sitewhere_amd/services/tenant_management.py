@@ -108,7 +108,7 @@ TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event stor
 TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
     storage="durable", publishEnriched="batches",
     capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
-              "dedup_slots": 1 << 18, "gen_cap": 32768})
+              "dedup_slots": 1 << 21, "gen_cap": 32768})
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
     "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
                   "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}

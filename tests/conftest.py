@@ -25,6 +25,13 @@ def gpu_available():
         return False
 
 
+@pytest.fixture(autouse=True)
+def _fresh_data_dir(tmp_path_factory, monkeypatch):
+    """Each test's durable tenant stores (``${sitewhere.data.dir}``) start empty: tests reuse tenant
+    tokens across instances, and a store reopened from an earlier test would hold its events."""
+    monkeypatch.setenv("SITEWHERE_DATA_DIR", str(tmp_path_factory.mktemp("sw-data")))
+
+
 @pytest.fixture(scope="session")
 def native_lib():
     from sitewhere_amd._native import native

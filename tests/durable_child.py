@@ -44,7 +44,7 @@ def main():
     ib = sw.tenant_engine("inbound-processing", "dur")
     topic = sw.instance.naming.tenant_prefix("dur") + RAW_PAYLOADS
     group = ib.raw_consumer.group
-    print(json.dumps({"group": group, "topic": topic, "boot": ib.boot}), flush=True)
+    print(json.dumps({"group": group, "topic": topic, "src_topic": ib._src_topic(topic), "boot": ib.boot}), flush=True)
     dev = sw.instance.system_user.run(lambda: sw.api("DeviceManagement", "dur").get_device_by_token("galaxytab-001"),
                                       "dur")
     end = time.time() + 60
@@ -64,7 +64,7 @@ def main():
         for b in range(n_batches):
             bus.append(topic, 0, [(None, raw_batch(b, per))], ts=1_700_000_100_000 + b)
         end = time.time() + 120
-        while (store.source_offset(topic, 0) or 0) < kill_after + 3 and time.time() < end:
+        while (store.source_offset(ib._src_topic(topic), 0) or 0) < kill_after + 3 and time.time() < end:
             time.sleep(0.001)
         os._exit(9)                                 # killed: nothing flushed, nothing closed
     end = time.time() + 120

@@ -114,3 +114,23 @@ def test_varint_framing_rejects_truncated_and_overlong():
         offsets_from_varint(np.concatenate([ok, np.array([0x85], np.uint8)]))      # truncated
     with _pt.raises(ValueError):
         offsets_from_varint(np.array([0xff] * 6 + [0x01], np.uint8))               # > 5 bytes
+
+
+def test_native_varint_offsets_match_reference():
+    """RawBatch.offsets (one native pass, sw_varint_offsets) == the numpy reference, and framing
+    errors (truncated / over-long / wrong count / wrong total) are rejected."""
+    import numpy as np
+    import pytest as _pt
+    from sitewhere_amd.pipeline.bus_io import RawBatch
+    from sitewhere_amd.pipeline.framing import offsets_from_varint, varint_lengths
+    rng = np.random.default_rng(3)
+    lens = rng.choice([0, 1, 90, 127, 128, 300, 16383, 16384, 70000], 5000).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
+    st = varint_lengths(offs)
+    b = RawBatch(len(lens), int(offs[-1]), None, lens=st)
+    np.testing.assert_array_equal(b.offsets(), offsets_from_varint(st))
+    for bad, n, total in ((st[:-1], len(lens), int(offs[-1])), (st, len(lens) + 1, int(offs[-1])),
+                          (st, len(lens), int(offs[-1]) + 1),
+                          (np.array([0xff] * 6 + [0x01], np.uint8), 1, 1)):
+        with _pt.raises(ValueError):
+            RawBatch(n, total, None, lens=bad).offsets()

@@ -60,7 +60,7 @@ def test_durable_tenant_survives_kill_exactly_once(tmp_path):
     # ---- after the kill: what is on disk is exactly what the commit records name
     vals, st = _values_on_disk(store_dir)
     try:
-        durable = st.source_offset(info["topic"], 0)
+        durable = st.source_offset(info["src_topic"], 0)
     finally:
         st.close()
     bus = EventBus(bus_dir, default_partitions=1)
@@ -79,7 +79,7 @@ def test_durable_tenant_survives_kill_exactly_once(tmp_path):
     assert out2[-1]["persisted"] == (N_BATCHES - durable) * PER   # nothing before the offset re-stepped
     vals, st = _values_on_disk(store_dir)
     try:
-        assert st.source_offset(info["topic"], 0) == N_BATCHES
+        assert st.source_offset(info["src_topic"], 0) == N_BATCHES
         boots = {int(e["boot"]) for e in st.seg.index()}
     finally:
         st.close()

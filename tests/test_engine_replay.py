@@ -74,12 +74,13 @@ def test_async_store_failure_rewinds_and_stores_once(inst, overlap):
     store = inst.tenant_engine("event-management", tok).store
     topic = inst.instance.naming.tenant_prefix(tok) + RAW_PAYLOADS
     group = ib.raw_consumer.group
+    ingest = "add_batch" if hasattr(store, "add_batch") else "add_columnar"     # durable / in-memory store
     with FaultInjector() as fi:
-        fi.fail_next(store, "add_columnar", 2)
+        fi.fail_next(store, ingest, 2)
         for b in range(6):
             inst.instance.bus.append(topic, 0, [(None, _raw_batch(b))], ts=1_700_000_100_000 + b)
         assert wait_until(lambda: store.rows == 120, 30), store.rows
-        assert fi.injected[("add_columnar", "fail")] == 2
+        assert fi.injected[(ingest, "fail")] == 2
     assert ib.engine.stats_dict()["persisted"] == 120          # each batch stepped exactly once
     assert ib.replayed_batches >= 1 and ib.raw_consumer.rewinds >= 1
     assert wait_until(lambda: inst.instance.bus.committed(group, topic, 0) == 6)
@@ -178,3 +179,23 @@ def test_poison_raw_record_is_dead_lettered_not_retried(inst):
     dl = topic + BusConsumer.DEAD_LETTER_SUFFIX
     assert sum(bus.end_offset(dl, p) for p in range(bus.partitions(dl))) == 2
     assert wait_until(lambda: sorted(e.value for e in _values(inst, run, "rpp", dev)) == [float(i) for i in range(10)])
+
+
+def test_durable_wait_failure_rewinds_without_loss_or_duplicates(inst):
+    """The durable store's token check fails while blocks are in flight: every batch not yet
+    finalized is stored again after the rewind (replayed blocks the store already holds are skipped
+    by sequence), offsets commit only behind durable blocks, and each event is on disk once."""
+    ib, run, dev = _tenant(inst, "rpd", "gpu-columnar")
+    store = inst.tenant_engine("event-management", "rpd").store
+    assert ib.storage == "durable" and hasattr(store, "add_batch")
+    topic = inst.instance.naming.tenant_prefix("rpd") + RAW_PAYLOADS
+    with FaultInjector() as fi:
+        fi.fail_next(store, "durable", 2)
+        for b in range(6):
+            inst.instance.bus.append(topic, 0, [(None, _raw_batch(b))], ts=1_700_000_700_000 + b)
+        assert wait_until(lambda: inst.instance.bus.committed(ib.raw_consumer.group, topic, 0) == 6, 30)
+        assert fi.injected[("durable", "fail")] == 2
+    assert store.rows == 120
+    res = _values(inst, run, "rpd", dev)
+    assert sorted(m.value for m in res) == sorted(float(100 * b + i) for b in range(6) for i in range(20))
+    assert not ib._stepped and not ib._durable_wait
