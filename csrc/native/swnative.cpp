@@ -780,7 +780,10 @@ int64_t swlog_append_batch(void* h, int32_t topic, int32_t p, const uint8_t* key
     hd.klen = (uint16_t)kl;
     uint8_t* dst = enc + pos + sizeof(RecHdr);
     memcpy(dst, keys + koff[i], (size_t)kl);
-    memcpy(dst + kl, vals + voff[i], (size_t)vl);
+    if (vl >= (8 << 20) && pt->fd < 0)
+      sw_memcpy_mt(dst + kl, vals + voff[i], vl, 0);   // multi-MB record (an encoded block): parallel copy
+    else
+      memcpy(dst + kl, vals + voff[i], (size_t)vl);
     // the checksum guards the durable file (verified on recovery); a memory-only log has no torn
     // tails to detect, and skipping it halves the cost of multi-MB columnar appends
     if (pt->fd >= 0) {

@@ -61,7 +61,7 @@ def _call(fn, args_head: tuple, n_rej: int) -> RoutedRejects:
     npay = np.zeros(1, np.int64)
     cap = (max(16, 4 * n_rej), max(1024, 64 * n_rej), max(4096, 256 * n_rej))
     for _ in range(2):
-        rec = np.zeros((cap[0], 4), np.int32)
+        rec = np.empty((cap[0], 4), np.int32)         # the first n rows are written
         keys = np.empty(cap[1], np.uint8)
         vals = np.empty(cap[2], np.uint8)
         n = fn(*args_head, rec.ctypes.data, cap[0], keys.ctypes.data, cap[1], vals.ctypes.data, cap[2],

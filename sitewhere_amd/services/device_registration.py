@@ -116,7 +116,8 @@ class DeviceRegistrationTenantEngine(MicroserviceTenantEngine):
 
     def tenant_stop(self, monitor):
         self.reg_consumer.lifecycle_stop(monitor)
-        self.unreg_consumer.lifecycle_stop(monitor)
+        if self.unreg_consumer.status.value == "Started":
+            self.unreg_consumer.lifecycle_stop(monitor)
 
 
 class RegistrationApi:

@@ -153,6 +153,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.overlap = bool(cfg.get("overlapSteps", self.async_store and self.engine_kind == "gpu"))
         self._order_lock = threading.Lock()    # engine submit/drain + completion hand-off, in step order
         self._holds: dict[tuple, dict] = {}    # (topic, partition) -> {offset: in-flight batches}
+        self._hold_lock = threading.Lock()      # the consumer and the reject router both release holds
         # SW_TENANT_TRACE=1: per-batch timestamps (submit, submitted, completed, store start, payload,
         # stored, published) for the tenant-path bench's breakdown
         import os
@@ -310,6 +311,9 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             self._store_q.put(None)
             self._store_thread.join(10)
             self._store_thread = None
+        pool = self.__dict__.pop("_route_pool", None)
+        if pool is not None:
+            pool.shutdown(wait=True)
         if self.ckpt_path and self._since_ckpt:
             if self._store_error is None and not self._stepped:
                 self.checkpoint()
@@ -432,23 +436,44 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 item.trace.append(time.perf_counter())
             self.processed_events.mark(res.n_events)
             self._ensure_block(res, item.now)
-            item.res, item.routed_recs, item.batch = res, self._route(item.batch, res), None
-            if item.hold is not None:
-                self._hold(item.hold, -1)
-                item.hold = None
+            hold, item.hold = item.hold, None
+            if res.reject_status is not None and len(res.reject_status):
+                # per-payload routing runs on a worker thread, in step order; the raw record stays
+                # held (readable) until it is done, and the store stage waits for its result
+                item.routed_recs = self._router().submit(self._route_and_release, item.batch, res, hold)
+            else:
+                item.routed_recs = None
+                if hold is not None:
+                    self._hold(hold, -1)
+            item.res, item.batch = res, None
             self._submit(item, item.commit)
+
+    def _router(self):
+        pool = self.__dict__.get("_route_pool")
+        if pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            pool = self._route_pool = ThreadPoolExecutor(1, thread_name_prefix=f"reject-router-{self.tenant.token}")
+        return pool
+
+    def _route_and_release(self, batch, res, hold):
+        try:
+            return self._route(batch, res)
+        finally:
+            if hold is not None:
+                self._hold(hold, -1)
 
     def _hold(self, at, delta: int):
         """Retention hold (per partition, at its oldest in-flight record) for records the engine
         reads after the consumer's handler returned."""
         t, p, o = at
-        hs = self._holds.setdefault((t, p), {})
-        n = hs.get(o, 0) + delta
-        if n > 0:
-            hs[o] = n
-        else:
-            hs.pop(o, None)
-        self.ms.instance.bus.hold(t, p, min(hs) if hs else None, holder=self)
+        with self._hold_lock:
+            hs = self._holds.setdefault((t, p), {})
+            n = hs.get(o, 0) + delta
+            if n > 0:
+                hs[o] = n
+            else:
+                hs.pop(o, None)
+            self.ms.instance.bus.hold(t, p, min(hs) if hs else None, holder=self)
 
     def _raise_store_error(self):
         """A store step failed on the store thread: stop stepping and have the raw consumer re-read
@@ -593,7 +618,10 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     self._publish_events(item.events if item.events is not None else self._to_events(res, now))
             item.published = True
         if not item.routed:
-            self._send_routed(item.routed_recs)
+            rr = item.routed_recs
+            if hasattr(rr, "result"):           # routed on the reject-router thread
+                rr = item.routed_recs = rr.result()
+            self._send_routed(rr)
             item.routed = True
         if self.storage == "durable" and (self._durable_wait or (item.token or 0) >= 0):
             with self._durable_lock:
