@@ -1,9 +1,10 @@
 """Load a ``.proto`` (proto3 subset) into protobuf message classes at run time -- no protoc.
 
 Supports what this framework's interface schemas use: ``syntax``, ``package``, top-level and
-nested ``message`` / ``enum``, scalar / message / enum fields, ``repeated``, ``map<k, v>`` and
-``oneof``.  Names resolve within the file's package (``import`` lines are ignored: a schema
-file is self-contained).
+nested ``message`` / ``enum``, scalar / message / enum fields, ``repeated``, ``map<k, v>``,
+``oneof`` and ``service`` / ``rpc`` (unary).  :func:`load_proto` takes one self-contained file;
+:func:`load_proto_files` a set of files that ``import`` each other (names resolve across files,
+innermost scope first, as protoc does).
 """
 from __future__ import annotations
 
@@ -37,7 +38,9 @@ class _Parser:
         self.t, self.i = _tokens(text), 0
         self.fd = descriptor_pb2.FileDescriptorProto(name=name, syntax="proto3")
         self._enums: set[str] = set()        # fully qualified enum names
+        self._messages: set[str] = set()     # fully qualified message names
         self._fields: list = []              # (field proto, type name, scope) resolved at the end
+        self._methods: list = []             # (method proto, input name, output name, scope)
 
     def peek(self):
         return self.t[self.i] if self.i < len(self.t) else None
@@ -60,22 +63,72 @@ class _Parser:
             elif tok == "package":
                 self.fd.package = self.take()
                 self.take(";")
-            elif tok in ("import", "option"):
+            elif tok == "import":
+                dep = self.take().strip('"')
+                while self.take() != ";":
+                    pass
+                if not dep.startswith("google/"):
+                    self.fd.dependency.append(dep)
+            elif tok == "option":
                 while self.take() != ";":
                     pass
             elif tok == "message":
                 self.message(self.fd.message_type.add(), self.fd.package)
             elif tok == "enum":
                 self.enum(self.fd.enum_type.add(), self.fd.package)
+            elif tok == "service":
+                self.service(self.fd.service.add())
             else:
                 raise SyntaxError(f"unexpected {tok!r}")
+        return self
+
+    def resolve_all(self, enums: set, messages: set):
+        """Resolve field / method types against the symbols of every file loaded together."""
+        self._enums_all, self._messages_all = enums, messages
         for f, tname, scope in self._fields:
             self._resolve(f, tname, scope)
+        for m, tin, tout, scope in self._methods:
+            m.input_type = self._resolve_message(tin, scope)
+            m.output_type = self._resolve_message(tout, scope)
         return self.fd
+
+    def service(self, sv):
+        sv.name = self.take()
+        self.take("{")
+        while self.peek() != "}":
+            tok = self.take()
+            if tok == "option":
+                while self.take() != ";":
+                    pass
+                continue
+            if tok != "rpc":
+                raise SyntaxError(f"unexpected {tok!r} in service {sv.name}")
+            m = sv.method.add()
+            m.name = self.take()
+            self.take("(")
+            tin = self.take()
+            if tin == "stream":
+                raise SyntaxError("streaming rpcs are not supported")
+            self.take(")")
+            self.take("returns")
+            self.take("(")
+            tout = self.take()
+            self.take(")")
+            if self.peek() == "{":
+                depth = 0
+                while True:
+                    t = self.take()
+                    depth += (t == "{") - (t == "}")
+                    if depth == 0:
+                        break
+            if self.peek() == ";":
+                self.take()
+            self._methods.append((m, tin, tout, self.fd.package))
+        self.take("}")
 
     def enum(self, e, scope):
         e.name = self.take()
-        self._enums.add(f"{scope}.{e.name}")
+        self._enums.add(f"{scope}.{e.name}".lstrip("."))
         self.take("{")
         while self.peek() != "}":
             if self.peek() == "option":
@@ -92,6 +145,7 @@ class _Parser:
     def message(self, m, scope):
         m.name = self.take()
         here = f"{scope}.{m.name}"
+        self._messages.add(here.lstrip("."))
         self.take("{")
         while self.peek() != "}":
             tok = self.peek()
@@ -163,7 +217,7 @@ class _Parser:
         for k in range(len(parts), -1, -1):
             cand = ".".join(parts[:k] + [tname]) if k else tname
             cand = cand.lstrip(".")
-            if cand in self._enums:
+            if cand in getattr(self, "_enums_all", self._enums):
                 f.type, f.type_name = _F.TYPE_ENUM, f".{cand}"
                 return
             if self._has_message(cand):
@@ -171,7 +225,17 @@ class _Parser:
                 return
         raise SyntaxError(f"unknown type {tname!r} in {scope}")
 
+    def _resolve_message(self, tname: str, scope: str) -> str:
+        parts = scope.split(".")
+        for k in range(len(parts), -1, -1):
+            cand = (".".join(parts[:k] + [tname]) if k else tname).lstrip(".")
+            if self._has_message(cand):
+                return f".{cand}"
+        raise SyntaxError(f"unknown message {tname!r} in {scope}")
+
     def _has_message(self, full: str) -> bool:
+        if hasattr(self, "_messages_all"):
+            return full in self._messages_all
         pkg = self.fd.package
         if pkg and not full.startswith(pkg + "."):
             return False
@@ -189,7 +253,8 @@ def load_proto(text: str, name: str, pool: descriptor_pool.DescriptorPool | None
     """Parse ``text`` and return ``{message name: class}`` for its top-level messages (nested ones
     are attributes of their parents) plus ``{enum name: EnumTypeWrapper}`` entries."""
     from google.protobuf.internal.enum_type_wrapper import EnumTypeWrapper
-    fd = _Parser(text, name).parse()
+    p = _Parser(text, name).parse()
+    fd = p.resolve_all(p._enums, p._messages)
     pool = pool or descriptor_pool.DescriptorPool()
     pool.Add(fd)
     fdesc = pool.FindFileByName(name)
@@ -199,3 +264,31 @@ def load_proto(text: str, name: str, pool: descriptor_pool.DescriptorPool | None
     for e in fd.enum_type:
         out[e.name] = EnumTypeWrapper(fdesc.enum_types_by_name[e.name])
     return out
+
+
+def load_proto_files(files: dict, pool: descriptor_pool.DescriptorPool | None = None):
+    """Parse ``{file name: text}`` (files that import each other) into one descriptor pool; returns
+    the pool.  Message classes: ``message_factory.GetMessageClass(pool.FindMessageTypeByName(...))``."""
+    parsers = {name: _Parser(text, name).parse() for name, text in files.items()}
+    enums = set().union(*(p._enums for p in parsers.values()))
+    messages = set().union(*(p._messages for p in parsers.values()))
+    fds = {name: p.resolve_all(enums, messages) for name, p in parsers.items()}
+    pool = pool or descriptor_pool.DescriptorPool()
+    added: set = set()
+
+    def add(name):
+        if name in added:
+            return
+        added.add(name)
+        for dep in fds[name].dependency:
+            if dep in fds:
+                add(dep)
+        fd = fds[name]
+        # keep only the dependencies actually loaded here (e.g. google/*.proto are dropped)
+        keep = [d for d in fd.dependency if d in fds]
+        del fd.dependency[:]
+        fd.dependency.extend(keep)
+        pool.Add(fd)
+    for name in fds:
+        add(name)
+    return pool

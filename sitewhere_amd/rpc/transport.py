@@ -6,10 +6,13 @@ Reference: ``sitewhere-microservice/.../grpc/GrpcServer.java:57-117`` and
 ``TenantTokenClientInterceptor.java:42-58``, and ``ServerTracingInterceptor`` /
 ``ClientTracingInterceptor`` (never enabled in the reference; always on here).
 
-Services are plain Python objects; every public method becomes ``/sitewhere.<Service>/<CamelName>``
-(e.g. ``create_device_type`` -> ``CreateDeviceType``), with the JSON model codec of
-:mod:`.codec`.  :class:`LocalChannel` short-circuits the network when caller and service share a
-process (same headers, same security semantics).
+Two planes on one server.  The reference services' RPCs are served on their own wire schemas:
+``/com.sitewhere.grpc.service.<Service>/<Rpc>`` with the ``G*`` protobuf messages (:mod:`.protoplane`),
+so reference clients and services interoperate.  Every public method of every service (the
+reference RPCs and this framework's additions) is also served as ``/sitewhere.<Service>/<CamelName>``
+(e.g. ``create_device_type`` -> ``CreateDeviceType``) with the JSON model codec of :mod:`.codec`,
+the internal plane between this framework's processes.  :class:`LocalChannel` short-circuits the
+network when caller and service share a process (same headers, same security semantics).
 """
 from __future__ import annotations
 
@@ -113,8 +116,25 @@ class ServiceResolver:
 _IMMUTABLE = (bytes, str, int, float, bool, type(None))
 
 
+def _trim_optional_tail(fn, args: list) -> list:
+    """Drop trailing ``None`` arguments the method has defaults for (unset proto3 fields)."""
+    import inspect
+    try:
+        params = [p for p in inspect.signature(fn).parameters.values()
+                  if p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)]
+    except (TypeError, ValueError):
+        return args
+    required = sum(1 for p in params if p.default is p.empty)
+    args = list(args[:len(params)]) if not any(p.kind == p.VAR_POSITIONAL for p in
+                                                inspect.signature(fn).parameters.values()) else list(args)
+    while len(args) > required and args[-1] is None:
+        args.pop()
+    return args
+
+
 def invoke(resolver: ServiceResolver, tokens: TokenManagement, service: str, method: str, body: bytes | None,
-           jwt: str | None, tenant: str | None, trace: str | None, require_jwt: bool = True, direct=None):
+           jwt: str | None, tenant: str | None, trace: str | None, require_jwt: bool = True, direct=None,
+           trim: bool = False):
     """Common server-side dispatch (network and local): auth -> tenant -> span -> call.
 
     ``direct=(args, kwargs)`` skips the body codec (in-process calls whose arguments are all
@@ -137,7 +157,8 @@ def invoke(resolver: ServiceResolver, tokens: TokenManagement, service: str, met
             if fn is None or not callable(fn) or isinstance(fn, type) or snake_method(method).startswith("_"):
                 raise NotFoundException(ErrorCode.Error, f"{service} has no method {method}")
             if direct is not None:
-                return fn(*direct[0], **direct[1])
+                args = _trim_optional_tail(fn, direct[0]) if trim else direct[0]
+                return fn(*args, **direct[1])
             req = codec.loads(body) or {}
             return fn(*req.get("args", []), **req.get("kwargs", {}))
 
@@ -149,9 +170,10 @@ class RpcServer(LifecycleComponent):
     component_type = LifecycleComponentType.Other
 
     def __init__(self, resolver: ServiceResolver, tokens: TokenManagement, port: int = 0, host: str = "127.0.0.1",
-                 workers: int = 16, advertise_host: str = ""):
+                 workers: int = 16, advertise_host: str = "", identifier: str | None = None):
         super().__init__("rpc-server")
         self.resolver, self.tokens = resolver, tokens
+        self.identifier = identifier          # the microservice serving (its MicroserviceManagement)
         self.host, self.port, self.workers = host, port, workers
         self.advertise_host = advertise_host or (socket.gethostname() if host in ("0.0.0.0", "::") else host)
         self._server = None
@@ -173,6 +195,37 @@ class RpcServer(LifecycleComponent):
                 context.abort(grpc.StatusCode.INTERNAL, _error_payload(e))
         return grpc.unary_unary_rpc_method_handler(handle, request_deserializer=None, response_serializer=None)
 
+    def _proto_handler(self, service: str, rpc: str):
+        """Handler of a reference RPC on its protobuf schema (see :mod:`.protoplane`)."""
+        from . import protoplane as pp
+        md = pp.method(service, rpc)
+        if md is None:
+            return None
+        req_cls, resp_cls = pp.message_class(md.input_type.full_name), pp.message_class(md.output_type.full_name)
+        ours = pp.SERVICE_ALIASES.get(service, service)
+        if ours == "MicroserviceManagement" and self.identifier:
+            ours = f"MicroserviceManagement.{self.identifier}"
+        fields = list(md.input_type.fields)
+
+        def handle(request, context: grpc.ServicerContext):
+            meta = dict(context.invocation_metadata())
+            self.calls += 1
+            try:
+                args = [pp.arg_of(request, f) for f in fields]
+                out = invoke(self.resolver, self.tokens, ours, rpc, None, meta.get(JWT_HEADER), meta.get(TENANT_HEADER),
+                             meta.get(TRACE_HEADER), direct=(args, {}), trim=True)
+                return pp.set_response(resp_cls(), out)
+            except SiteWhereSystemException as e:
+                context.abort(_STATUS.get(e.http_status, grpc.StatusCode.INVALID_ARGUMENT), _error_payload(e))
+            except SiteWhereException as e:
+                context.abort(grpc.StatusCode.INTERNAL, _error_payload(e))
+            except (TypeError, ValueError, KeyError) as e:
+                context.abort(grpc.StatusCode.INVALID_ARGUMENT, _error_payload(e))
+            except Exception as e:  # noqa: BLE001
+                context.abort(grpc.StatusCode.INTERNAL, _error_payload(e))
+        return grpc.unary_unary_rpc_method_handler(handle, request_deserializer=req_cls.FromString,
+                                                   response_serializer=resp_cls.SerializeToString)
+
     def start(self, monitor):
         srv = self
 
@@ -183,6 +236,8 @@ class RpcServer(LifecycleComponent):
                     svc, meth = path.lstrip("/").split("/", 1)
                 except ValueError:
                     return None
+                if svc.startswith("com.sitewhere.grpc.service."):
+                    return srv._proto_handler(svc[len("com.sitewhere.grpc.service."):], meth)
                 if not svc.startswith("sitewhere."):
                     return None
                 return srv._handler(svc[len("sitewhere."):], meth)

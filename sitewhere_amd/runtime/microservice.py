@@ -35,7 +35,7 @@ from ..core.lifecycle import (CompositeLifecycleStep, LifecycleComponent, Lifecy
                               LifecycleProgressMonitor, LifecycleStatus, SimpleLifecycleStep,
                               TenantEngineLifecycleComponent)
 from ..core.metrics import MetricRegistry, MetricsReporter
-from ..core.security import SystemUser, TokenManagement
+from ..core.security import SystemUser, TokenManagement, current_authentication
 from ..core.trace_export import configure_tracing
 from ..core.tracing import global_tracer
 from ..models.domain import Tenant
@@ -254,7 +254,10 @@ class MultitenantManagementApi:
     def __init__(self, ms: "MultitenantMicroservice"):
         self._ms = ms
 
-    def check_tenant_engine_available(self, tenant: str) -> bool:
+    def check_tenant_engine_available(self, tenant: str | None = None) -> bool:
+        if tenant is None:                  # reference form: the tenant travels in the call metadata
+            auth = current_authentication()
+            tenant = auth.tenant if auth is not None else None
         e = self._ms.tenant_engines.get(tenant)
         return e is not None and e.status == LifecycleStatus.Started
 
@@ -421,7 +424,7 @@ class Microservice(LifecycleComponent):
         if self.instance.network_rpc:
             st = self.instance.settings
             self.rpc_server = RpcServer(res, self.instance.tokens, port=st.grpc_port, host=st.grpc_host,
-                                        advertise_host=st.grpc_advertise_host)
+                                        advertise_host=st.grpc_advertise_host, identifier=self.identifier)
 
     def start(self, monitor):
         if self.rpc_server is not None:

@@ -55,6 +55,10 @@ class UserManagement:
         return _public(self._s.put(self.USERS, u))
 
     def import_user(self, user: User, overwrite: bool = False) -> User:
+        if isinstance(user, dict):          # wire form (GImportUserRequest carries a GUser)
+            user = User.from_dict(user)
+        if not user.username:
+            raise SiteWhereSystemException(ErrorCode.InvalidUsername, detail="user without a username")
         existing = self._s.get_by(self.USERS, "username", user.username)
         if existing and not overwrite:
             raise SiteWhereSystemException(ErrorCode.DuplicateUser, detail=user.username)
