@@ -28,28 +28,50 @@ class _Coll:
     def __init__(self):
         self.docs: dict = {}                      # _id key -> document
         self.indexes: dict[str, dict] = {"_id_": {"key": {"_id": 1}, "unique": True, "sparse": False}}
+        self.uniq: dict[str, dict] = {}           # unique index name -> value tuple -> _id key
 
     @staticmethod
     def idkey(v):
         return v.binary if isinstance(v, bson.ObjectId) else (type(v).__name__, v)
 
+    @staticmethod
+    def _ukey(doc: dict, ix: dict):
+        """Hashable key of ``doc`` in unique index ``ix`` (None: not indexed, sparse and absent)."""
+        vals = tuple(get_path(doc, f) for f in ix["key"])
+        if ix["sparse"] and all(v is _MISSING for v in vals):
+            return None
+        vals = tuple(None if v is _MISSING else v for v in vals)
+        try:
+            hash(vals)
+            return vals
+        except TypeError:
+            return repr(vals)
+
+    def _unique_indexes(self):
+        return [(n, ix) for n, ix in self.indexes.items() if ix["unique"] and n != "_id_"]
+
     def check_unique(self, doc: dict, ignore_id=None):
-        for name, ix in self.indexes.items():
-            if not ix["unique"] or name == "_id_":
+        """Hash lookups per unique index (a duplicate raises E11000)."""
+        for name, ix in self._unique_indexes():
+            key = self._ukey(doc, ix)
+            if key is None:
                 continue
-            fields = list(ix["key"])
-            vals = tuple(get_path(doc, f) for f in fields)
-            if ix["sparse"] and all(v is _MISSING for v in vals):
-                continue
-            vals = tuple(None if v is _MISSING else v for v in vals)
-            for k, other in self.docs.items():
-                if k == ignore_id:
-                    continue
-                ov = tuple(None if get_path(other, f) is _MISSING else get_path(other, f) for f in fields)
-                if ix["sparse"] and all(get_path(other, f) is _MISSING for f in fields):
-                    continue
-                if ov == vals:
-                    raise MongoError(f"E11000 duplicate key error index: {name} dup key: {vals}", DUPLICATE_KEY)
+            other = self.uniq.get(name, {}).get(key)
+            if other is not None and other != ignore_id:
+                raise MongoError(f"E11000 duplicate key error index: {name} dup key: {key}", DUPLICATE_KEY)
+
+    def index_add(self, doc: dict, k):
+        for name, ix in self._unique_indexes():
+            key = self._ukey(doc, ix)
+            if key is not None:
+                self.uniq.setdefault(name, {})[key] = k
+
+    def index_remove(self, doc: dict, k):
+        for name, ix in self._unique_indexes():
+            key = self._ukey(doc, ix)
+            m = self.uniq.get(name)
+            if key is not None and m is not None and m.get(key) == k:
+                del m[key]
 
 
 class _Handler(socketserver.BaseRequestHandler):
@@ -144,10 +166,14 @@ class MiniMongoServer:
                 raise MongoError(f"E11000 duplicate key error index: _id_ dup key: {d['_id']}", DUPLICATE_KEY)
             c.check_unique(d)
             c.docs[k] = d
+            c.index_add(d, k)
             n += 1
         return {"n": n, "ok": 1.0}
 
     def _select(self, c: _Coll | None, flt, sort=None, skip=0, limit=0):
+        if c is not None and flt and set(flt) == {"_id"} and not isinstance(flt["_id"], dict):
+            d = c.docs.get(c.idkey(flt["_id"]))          # by primary key: no scan
+            return [d] if d is not None and not skip else []
         docs = [d for d in (c.docs.values() if c else ()) if matches(d, flt)]
         docs = sort_docs(docs, sort)
         if skip:
@@ -201,7 +227,9 @@ class MiniMongoServer:
                     new = apply_update(d, u["u"])
                     k = c.idkey(d["_id"])
                     c.check_unique(new, ignore_id=k)
+                    c.index_remove(d, k)
                     c.docs[k] = new
+                    c.index_add(new, k)
                     n += 1
                     nmod += 1
             elif u.get("upsert"):
@@ -212,6 +240,7 @@ class MiniMongoServer:
                 new.setdefault("_id", bson.ObjectId())
                 c.check_unique(new)
                 c.docs[c.idkey(new["_id"])] = new
+                c.index_add(new, c.idkey(new["_id"]))
                 n += 1
                 upserted.append({"index": i, "_id": new["_id"]})
         out = {"n": n, "nModified": nmod, "ok": 1.0}
@@ -224,7 +253,9 @@ class MiniMongoServer:
         n = 0
         for d in cmd.get("deletes", []):
             for doc in self._select(c, d.get("q"), limit=int(d.get("limit", 0))):
-                del c.docs[c.idkey(doc["_id"])]
+                k = c.idkey(doc["_id"])
+                del c.docs[k]
+                c.index_remove(doc, k)
                 n += 1
         return {"n": n, "ok": 1.0}
 
@@ -233,10 +264,18 @@ class MiniMongoServer:
         before = len(c.indexes)
         for ix in cmd.get("indexes", []):
             spec = {"key": dict(ix["key"]), "unique": bool(ix.get("unique")), "sparse": bool(ix.get("sparse"))}
+            if spec["unique"] and ix["name"] not in c.uniq:
+                m: dict = {}
+                for k, d in c.docs.items():
+                    key = c._ukey(d, spec)
+                    if key is None:
+                        continue
+                    if key in m:
+                        raise MongoError(f"E11000 duplicate key error index: {ix['name']} dup key: {key}",
+                                         DUPLICATE_KEY)
+                    m[key] = k
+                c.uniq[ix["name"]] = m
             c.indexes[ix["name"]] = spec
-            if spec["unique"]:
-                for k, d in list(c.docs.items()):
-                    c.check_unique(d, ignore_id=k)
         return {"numIndexesBefore": before, "numIndexesAfter": len(c.indexes), "ok": 1.0}
 
     def _cmd_listIndexes(self, db, cmd):

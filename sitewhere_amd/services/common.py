@@ -42,9 +42,9 @@ def criteria_of(c) -> SearchCriteria:
 class Crud:
     """Entity CRUD with token uniqueness and not-found error codes."""
 
-    def __init__(self, store, collection: str, cls: type, not_found: ErrorCode, unique=("token",)):
+    def __init__(self, store, collection: str, cls: type, not_found: ErrorCode, unique=("token",), indexed=()):
         self.s, self.c, self.cls, self.nf = store, collection, cls, not_found
-        store.register(collection, cls, unique)
+        store.register(collection, cls, unique, indexed=indexed)
 
     def create(self, request: dict, **fixed) -> Model:
         e = self.cls()
@@ -97,6 +97,14 @@ class Crud:
 
     def query(self, pred=None, sort=None, reverse=False):
         return self.s.query(self.c, pred, sort_key=sort or (lambda e: (getattr(e, "created_date", None) or 0, e.id)), reverse=reverse)
+
+    def search(self, q, criteria=None) -> SearchResults:
+        """Filter / sort / page pushed down into the store (``persistence/query.py``); the page of
+        ``criteria`` (pageNumber / pageSize) is applied there too."""
+        c = criteria_of(criteria)
+        q.page(c.page_number, c.page_size)
+        total, items = self.s.find(self.c, q)
+        return SearchResults(total, items)
 
     def list(self, criteria=None, pred=None, sort=None, reverse=False) -> SearchResults:
         c = criteria_of(criteria)

@@ -21,6 +21,7 @@ from ..models.domain import (Area, AreaType, Customer, CustomerType, Device, Dev
                              DeviceAssignment, DeviceAssignmentStatus, DeviceCommand, DeviceElementMapping,
                              DeviceGroup, DeviceGroupElement, DeviceStatus, DeviceStream, DeviceType, SearchResults,
                              Zone, now_ms)
+from ..persistence.query import Query
 from ..persistence.store import EntityStore, create_store
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
 from .common import Crud
@@ -33,20 +34,32 @@ def _ids(v):
 class DeviceManagement:
     def __init__(self, store: EntityStore | None = None):
         s = self._store = store or create_store("memory")
-        self.device_types = Crud(s, "deviceTypes", DeviceType, ErrorCode.InvalidDeviceTypeToken)
-        self.commands = Crud(s, "deviceCommands", DeviceCommand, ErrorCode.InvalidDeviceCommandToken)
-        self.statuses = Crud(s, "deviceStatuses", DeviceStatus, ErrorCode.InvalidDeviceStatusCode)
-        self.devices = Crud(s, "devices", Device, ErrorCode.InvalidDeviceToken)
-        self.assignments = Crud(s, "assignments", DeviceAssignment, ErrorCode.InvalidDeviceAssignmentToken)
-        self.groups = Crud(s, "deviceGroups", DeviceGroup, ErrorCode.InvalidDeviceGroupToken)
-        self.group_elements = Crud(s, "deviceGroupElements", DeviceGroupElement, ErrorCode.InvalidDeviceGroupToken, ())
-        self.streams = Crud(s, "deviceStreams", DeviceStream, ErrorCode.InvalidStreamId)
-        self.alarms = Crud(s, "deviceAlarms", DeviceAlarm, ErrorCode.InvalidAlarmId)
-        self.customer_types = Crud(s, "customerTypes", CustomerType, ErrorCode.InvalidCustomerTypeToken)
-        self.customers = Crud(s, "customers", Customer, ErrorCode.InvalidCustomerToken)
-        self.area_types = Crud(s, "areaTypes", AreaType, ErrorCode.InvalidAreaTypeToken)
-        self.areas = Crud(s, "areas", Area, ErrorCode.InvalidAreaToken)
-        self.zones = Crud(s, "zones", Zone, ErrorCode.InvalidZoneToken)
+        # indexed: the fields list / search criteria filter and sort on, pushed down into the store
+        # (persistence/query.py; the reference's MongoDeviceManagement list* queries)
+        self.device_types = Crud(s, "deviceTypes", DeviceType, ErrorCode.InvalidDeviceTypeToken, indexed=("name",))
+        self.commands = Crud(s, "deviceCommands", DeviceCommand, ErrorCode.InvalidDeviceCommandToken,
+                             indexed=("device_type_id",))
+        self.statuses = Crud(s, "deviceStatuses", DeviceStatus, ErrorCode.InvalidDeviceStatusCode,
+                             indexed=("device_type_id",))
+        self.devices = Crud(s, "devices", Device, ErrorCode.InvalidDeviceToken,
+                            indexed=("device_type_id", "device_assignment_id", "parent_device_id", "created_date"))
+        self.assignments = Crud(s, "assignments", DeviceAssignment, ErrorCode.InvalidDeviceAssignmentToken,
+                                indexed=("device_id", "device_type_id", "customer_id", "area_id", "asset_id", "status",
+                                         "active_date"))
+        self.groups = Crud(s, "deviceGroups", DeviceGroup, ErrorCode.InvalidDeviceGroupToken, indexed=("name",))
+        self.group_elements = Crud(s, "deviceGroupElements", DeviceGroupElement, ErrorCode.InvalidDeviceGroupToken, (),
+                                   indexed=("group_id",))
+        self.streams = Crud(s, "deviceStreams", DeviceStream, ErrorCode.InvalidStreamId, indexed=("assignment_id",))
+        self.alarms = Crud(s, "deviceAlarms", DeviceAlarm, ErrorCode.InvalidAlarmId,
+                           indexed=("device_id", "device_assignment_id", "customer_id", "area_id", "asset_id",
+                                    "triggering_event_id", "state", "triggered_date"))
+        self.customer_types = Crud(s, "customerTypes", CustomerType, ErrorCode.InvalidCustomerTypeToken,
+                                   indexed=("name",))
+        self.customers = Crud(s, "customers", Customer, ErrorCode.InvalidCustomerToken,
+                              indexed=("parent_customer_id", "customer_type_id", "name"))
+        self.area_types = Crud(s, "areaTypes", AreaType, ErrorCode.InvalidAreaTypeToken, indexed=("name",))
+        self.areas = Crud(s, "areas", Area, ErrorCode.InvalidAreaToken, indexed=("parent_area_id", "area_type_id", "name"))
+        self.zones = Crud(s, "zones", Zone, ErrorCode.InvalidZoneToken, indexed=("area_id", "name"))
         self._listeners = []
         self._lock = threading.RLock()
 
@@ -77,10 +90,10 @@ class DeviceManagement:
         return self.device_types.update(id, request)
 
     def list_device_types(self, criteria=None) -> SearchResults:
-        return self.device_types.list(criteria, sort=lambda e: e.name)
+        return self.device_types.search(Query().order("name"), criteria)
 
     def delete_device_type(self, id: str) -> DeviceType:
-        if self.devices.query(lambda d: d.device_type_id == id):
+        if self.devices.s.find(self.devices.c, Query(limit=1).eq("device_type_id", id))[0]:
             raise SiteWhereSystemException(ErrorCode.DeviceTypeInUse, detail=id)
         return self.device_types.delete(id)
 
@@ -106,8 +119,7 @@ class DeviceManagement:
         dt = c.get("deviceTypeId") if isinstance(c, dict) else None
         if isinstance(c, dict) and c.get("deviceTypeToken"):
             dt = self.device_types.require_token(c["deviceTypeToken"]).id
-        return self.commands.list(c, (lambda e: e.device_type_id == dt) if dt else None,
-                                  sort=lambda e: (e.namespace, e.name))
+        return self.commands.search(Query().eq("device_type_id", dt).order("namespace").order("name"), c)
 
     def delete_device_command(self, id: str):
         return self.commands.delete(id)
@@ -135,8 +147,7 @@ class DeviceManagement:
         if isinstance(c, dict) and c.get("deviceTypeToken"):
             dt = self.device_types.require_token(c["deviceTypeToken"]).id
         code = c.get("code") if isinstance(c, dict) else None
-        return self.statuses.list(c, lambda e: (not dt or e.device_type_id == dt) and (not code or e.code == code),
-                                  sort=lambda e: e.code)
+        return self.statuses.search(Query().eq("device_type_id", dt).eq("code", code).order("code"), c)
 
     def delete_device_status(self, id: str):
         return self.statuses.delete(id)
@@ -204,18 +215,10 @@ class DeviceManagement:
         excl = bool(c.get("excludeAssigned")) if isinstance(c, dict) else False
         after = c.get("createdAfter") if isinstance(c, dict) else None
         before = c.get("createdBefore") if isinstance(c, dict) else None
-
-        def pred(d: Device):
-            if dt and d.device_type_id != dt:
-                return False
-            if excl and d.device_assignment_id:
-                return False
-            if after and (d.created_date or 0) < after:
-                return False
-            if before and (d.created_date or 0) > before:
-                return False
-            return True
-        return self.devices.list(c, pred, sort=lambda d: (d.created_date or 0, d.token), reverse=True)
+        q = Query().eq("device_type_id", dt).gte("created_date", after or None).lte("created_date", before or None)
+        if excl:
+            q.null("device_assignment_id")
+        return self.devices.search(q.order("created_date", True).order("token", True), c)
 
     def create_device_element_mapping(self, device_id: str, mapping) -> Device:
         """Nest a child device under a path of the parent's element schema (reference NestedDeviceSupport)."""
@@ -266,7 +269,7 @@ class DeviceManagement:
         return self.groups.update(id, request)
 
     def list_device_groups(self, criteria=None):
-        return self.groups.list(criteria, sort=lambda g: g.name)
+        return self.groups.search(Query().order("name"), criteria)
 
     def list_device_groups_with_role(self, role: str, criteria=None):
         return self.groups.list(criteria, lambda g: role in g.roles, sort=lambda g: g.name)
@@ -305,7 +308,7 @@ class DeviceManagement:
 
     def list_device_group_elements(self, group_id: str, criteria=None):
         self.groups.require(group_id)
-        return self.group_elements.list(criteria, lambda e: e.group_id == group_id, sort=lambda e: e.id)
+        return self.group_elements.search(Query().eq("group_id", group_id).order("id"), criteria)
 
     def expand_group_devices(self, group_id: str, roles: list[str] | None = None) -> list[str]:
         """Device ids of a group, recursing into nested groups (reference GroupUtils)."""
@@ -391,14 +394,15 @@ class DeviceManagement:
         dev = c.get("deviceId") if isinstance(c, dict) else None
         # reference criteria carry id lists (DeviceAssignmentSearchCriteria); REST / client filters
         # name one entity (customerId, areaId, ...) -- both narrow the result
-        dts, cus, ars, ass = ((_ids(c.get(k + "s")) | ({c[k]} if c.get(k) else set())) if isinstance(c, dict)
-                              else set() for k in ("deviceTypeId", "customerId", "areaId", "assetId"))
-
-        def pred(a: DeviceAssignment):
-            return ((not st or a.status.value == st) and (not dev or a.device_id == dev) and
-                    (not dts or a.device_type_id in dts) and (not cus or a.customer_id in cus) and
-                    (not ars or a.area_id in ars) and (not ass or a.asset_id in ass))
-        return self.assignments.list(c, pred, sort=lambda a: (a.active_date or 0, a.id), reverse=True)
+        q = Query().eq("status", st or None).eq("device_id", dev or None)
+        for k, f in (("deviceTypeId", "device_type_id"), ("customerId", "customer_id"), ("areaId", "area_id"),
+                     ("assetId", "asset_id")):
+            # reference criteria carry id lists (DeviceAssignmentSearchCriteria); REST / client
+            # filters name one entity (customerId, areaId, ...) -- both narrow the result
+            ids = (_ids(c.get(k + "s")) | ({c[k]} if c.get(k) else set())) if isinstance(c, dict) else set()
+            if ids:
+                q.in_(f, sorted(ids))
+        return self.assignments.search(q.order("active_date", True).order("id", True), c)
 
     def end_device_assignment(self, id: str):
         with self._lock:
@@ -433,7 +437,7 @@ class DeviceManagement:
         return r[0] if r else None
 
     def list_device_streams(self, assignment_id: str, criteria=None):
-        return self.streams.list(criteria, lambda s: s.assignment_id == assignment_id, sort=lambda s: s.stream_id)
+        return self.streams.search(Query().eq("assignment_id", assignment_id).order("stream_id"), criteria)
 
     # ================================================================== alarms
     def create_device_alarm(self, request: dict) -> DeviceAlarm:
@@ -461,12 +465,12 @@ class DeviceManagement:
         c = criteria or {}
         keys = {"deviceId": "device_id", "deviceAssignmentId": "device_assignment_id", "customerId": "customer_id",
                 "areaId": "area_id", "assetId": "asset_id", "triggeringEventId": "triggering_event_id"}
-        want = {f: c[k] for k, f in keys.items() if isinstance(c, dict) and c.get(k)}
+        q = Query()
+        for k, f in keys.items():
+            if isinstance(c, dict) and c.get(k):
+                q.eq(f, c[k])
         st = c.get("state") if isinstance(c, dict) else None
-
-        def pred(al):
-            return all(getattr(al, f) == v for f, v in want.items()) and (not st or al.state.value == st)
-        return self.alarms.list(c, pred, sort=lambda al: al.triggered_date or 0, reverse=True)
+        return self.alarms.search(q.eq("state", st or None).order("triggered_date", True), c)
 
     def delete_device_alarm(self, id: str):
         return self.alarms.delete(id)
@@ -492,7 +496,7 @@ class DeviceManagement:
                                                if k != "containedCustomerTypeTokens"}, **fixed)
 
     def list_customer_types(self, criteria=None):
-        return self.customer_types.list(criteria, sort=lambda e: e.name)
+        return self.customer_types.search(Query().order("name"), criteria)
 
     def delete_customer_type(self, id: str):
         return self.customer_types.delete(id)
@@ -526,9 +530,10 @@ class DeviceManagement:
         root = bool(c.get("rootOnly")) if isinstance(c, dict) else False
         parent = c.get("parentCustomerId") if isinstance(c, dict) else None
         ct = c.get("customerTypeId") if isinstance(c, dict) else None
-        return self.customers.list(c, lambda e: (not root or e.parent_customer_id is None) and
-                                   (not parent or e.parent_customer_id == parent) and
-                                   (not ct or e.customer_type_id == ct), sort=lambda e: e.name)
+        q = Query().eq("parent_customer_id", parent or None).eq("customer_type_id", ct or None)
+        if root:
+            q.null("parent_customer_id")
+        return self.customers.search(q.order("name"), c)
 
     def delete_customer(self, id: str):
         return self.customers.delete(id)
@@ -556,7 +561,7 @@ class DeviceManagement:
         return self.area_types.update(id, {k: v for k, v in request.items() if k != "containedAreaTypeTokens"}, **fixed)
 
     def list_area_types(self, criteria=None):
-        return self.area_types.list(criteria, sort=lambda e: e.name)
+        return self.area_types.search(Query().order("name"), criteria)
 
     def delete_area_type(self, id: str):
         return self.area_types.delete(id)
@@ -590,9 +595,10 @@ class DeviceManagement:
         root = bool(c.get("rootOnly")) if isinstance(c, dict) else False
         parent = c.get("parentAreaId") if isinstance(c, dict) else None
         at = c.get("areaTypeId") if isinstance(c, dict) else None
-        return self.areas.list(c, lambda e: (not root or e.parent_area_id is None) and
-                               (not parent or e.parent_area_id == parent) and (not at or e.area_type_id == at),
-                               sort=lambda e: e.name)
+        q = Query().eq("parent_area_id", parent or None).eq("area_type_id", at or None)
+        if root:
+            q.null("parent_area_id")
+        return self.areas.search(q.order("name"), c)
 
     def delete_area(self, id: str):
         return self.areas.delete(id)
@@ -623,7 +629,7 @@ class DeviceManagement:
         area = c.get("areaId") if isinstance(c, dict) else None
         if isinstance(c, dict) and c.get("areaToken"):
             area = self.areas.require_token(c["areaToken"]).id
-        return self.zones.list(c, (lambda z: z.area_id == area) if area else None, sort=lambda z: z.name)
+        return self.zones.search(Query().eq("area_id", area or None).order("name"), c)
 
     def delete_zone(self, id: str):
         z = self.zones.delete(id)
