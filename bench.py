@@ -191,6 +191,16 @@ def main():
 
     bus_stats = None
     dur = None
+    # lossless multi-GPU re-keying: while this rank's carry of spilled records is high, its next
+    # round is exchange-only (EngineBase.should_stall) -- the input slows down, nothing is dropped
+    stalls = {"rounds": 0}
+
+    def stall(runner) -> bool:
+        if world > 1 and getattr(runner, "rounds", False) and eng.should_stall():
+            stalls["rounds"] += 1
+            runner.submit(None, None, 0, now_ms=now0)
+            return True
+        return False
     tmpdir = None
     boot = 0
     if use_gpu and args.bus and args.framing == "varint":
@@ -284,6 +294,9 @@ def main():
                 bus.commit(group, t_raw, 0, upto)
 
         def run(k):
+            if stall(runner):
+                commit_durable()
+                return
             if producer is not None:
                 stamps.pop(k).result()                        # batch k's fresh alternate ids
             records[k % len(records)].publish(bus, t_raw, 0, ts=now0 + k)     # producer: batch k arrives
@@ -319,6 +332,8 @@ def main():
         runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=not args.no_outbound)
 
         def run(k):
+            if stall(runner):
+                return
             rh, oh, r, o, lh = batches[k % len(batches)]
             if lh is not None:
                 runner.submit(rh, None, len(o) - 1, now_ms=now0 + k, presence=True, lens_host=lh,
@@ -335,6 +350,9 @@ def main():
 
         def run(k):
             _, _, r, o, _ = batches[k % len(batches)]
+            if eng.should_stall():                  # skewed keys: an exchange-only round instead
+                stalls["rounds"] += 1
+                r, o = np.zeros(64, np.uint8), np.zeros(1, np.uint32)
             res = eng.step(r, o, now0 + k, presence=True)
             if dur is not None:
                 dur["sink"].add(eng.encode_block(now0 + k, res, boot=boot))
@@ -396,6 +414,7 @@ def main():
         detail["exchange_bytes_per_rank_step"] = exchange_bytes_per_rank(cfg.rec_cap, world)
         detail["shuffle_deferred"] = s1.get("shuffle_deferred", 0) - s0.get("shuffle_deferred", 0)
         detail["shuffle_overflow"] = s1.get("shuffle_overflow", 0) - s0.get("shuffle_overflow", 0)
+        detail["stall_rounds"] = stalls["rounds"]
     if bus_stats:
         r1 = bus_stats["routed"]
         bus = bus_stats["bus"]

@@ -1183,16 +1183,18 @@ int sw_reject_refs(const SwEngineArgs* ap, const uint8_t* raw, const uint32_t* m
 // step's u32 scalars (n_out at [7], n_rej at [5]) -> host[0..15]; the durable-block encoder's
 // (bytes, errors, first sequence) u64s -> host[16..21]; the reject-ref counters -> host[24..25].
 __global__ void k_step_snapshot(const uint32_t* __restrict__ scalars, const uint32_t* __restrict__ seg_meta,
-                                const uint32_t* __restrict__ rej_cnt, int produced, uint32_t* __restrict__ host) {
+                                const uint32_t* __restrict__ rej_cnt, const uint32_t* __restrict__ n_carry,
+                                int produced, uint32_t* __restrict__ host) {
   const uint32_t t = threadIdx.x;
   if (t < 16) host[t] = produced ? scalars[t] : 0u;
   else if (t < 22) host[t] = (produced && seg_meta) ? seg_meta[t - 16] : 0u;
+  else if (t == 22 || t == 23) host[t] = n_carry ? n_carry[t - 22] : 0u;     // re-key carry (both parities)
   else if (t == 24 || t == 25) host[t] = (produced && rej_cnt) ? rej_cnt[t - 24] : 0u;
 }
 
-int sw_step_snapshot(const uint32_t* scalars, const uint32_t* seg_meta, const uint32_t* rej_cnt, int32_t produced,
-                     uint32_t* host, hipStream_t s) {
-  k_step_snapshot<<<1, 64, 0, s>>>(scalars, seg_meta, rej_cnt, produced, host);
+int sw_step_snapshot(const uint32_t* scalars, const uint32_t* seg_meta, const uint32_t* rej_cnt,
+                     const uint32_t* n_carry, int32_t produced, uint32_t* host, hipStream_t s) {
+  k_step_snapshot<<<1, 64, 0, s>>>(scalars, seg_meta, rej_cnt, n_carry, produced, host);
   return (int)hipGetLastError();
 }
 

@@ -830,6 +830,21 @@ int64_t swlog_end_offset(void* h, int32_t topic, int32_t p) {
   return pt->base_offset + (int64_t)pt->index.size();
 }
 
+// Retained record bytes at or after `offset` (what a consumer at `offset` has still to read).
+int64_t swlog_bytes_from(void* h, int32_t topic, int32_t p, int64_t offset) {
+  Partition* pt = part_of((Log*)h, topic, p);
+  if (!pt) return -1;
+  std::lock_guard<std::mutex> g(pt->mu);
+  const int64_t end = pt->base_offset + (int64_t)pt->index.size();
+  if (offset <= pt->base_offset) return pt->bytes;
+  if (offset >= end) return 0;
+  const int64_t e = pt->index[(size_t)(offset - pt->base_offset)];
+  const int64_t ord = e >> 32;
+  int64_t before = e & 0xffffffffLL;
+  for (int64_t o = pt->seg0; o < ord; ++o) before += (int64_t)pt->segs[(size_t)(o - pt->seg0)].used;
+  return pt->bytes - before;
+}
+
 int64_t swlog_begin_offset(void* h, int32_t topic, int32_t p) {
   Partition* pt = part_of((Log*)h, topic, p);
   if (!pt) return -1;

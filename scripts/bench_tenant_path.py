@@ -196,6 +196,8 @@ def main():
                       "alt_ids": args.alt_ids, "p_unregistered": args.p_unregistered,
                       "duplicates": ib.engine.stats_dict().get("duplicates"),
                       "routed_payloads": ib.routed_payloads, "unregistered": ib.unregistered.count,
+                      "raw_records_lost": getattr(ib.raw_consumer.consumer, "lost", None),
+                      "backpressure_waits": getattr(sw.instance.bus, "backpressure_waits", None),
                       "store_retention_rows": getattr(em_store, "retention_rows", None),
                       "store_evicted_rows": getattr(em_store, "evicted_rows", None), "setup_s": round(setup_s, 1),
                       "mean_ms": breakdown, **({"median_ms_second_half": trace} if trace else {})}))

@@ -136,6 +136,7 @@ def native():
         _proto(lib, "swlog_append", c_int64, P, c_int32, c_int32, P, c_int64, P, c_int64, c_int64)
         _proto(lib, "swlog_end_offset", c_int64, P, c_int32, c_int32)
         _proto(lib, "swlog_begin_offset", c_int64, P, c_int32, c_int32)
+        _proto(lib, "swlog_bytes_from", c_int64, P, c_int32, c_int32, c_int64)
         _proto(lib, "swlog_wait", c_int64, P, c_int32, c_int32, c_int64, c_int32)
         _proto(lib, "swlog_read", c_int64, P, c_int32, c_int32, c_int64, c_int64, P, c_int64, P)
         _proto(lib, "swlog_retain_from", c_int64, P, c_int32, c_int32, c_int64)
@@ -268,7 +269,7 @@ def gpu():
         _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
         _proto(lib, "sw_seg_encode", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
-        _proto(lib, "sw_step_snapshot", c_int32, P, P, P, c_int32, P, P)
+        _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
         _gpu = lib
         return lib
 

@@ -101,6 +101,10 @@ class _Group:
         self.assignment: dict[str, list[tuple[str, int]]] = {}
 
 
+class BackpressureTimeout(RuntimeError):
+    """A producer waited too long for a protected topic's consumer (see :meth:`EventBus.protect`)."""
+
+
 class EventBus:
     """In-process broker: topics, partitions, consumer-group coordinator, committed offsets."""
 
@@ -116,6 +120,12 @@ class EventBus:
         if retention_bytes is None:
             retention_bytes = 0 if directory else (1 << 30)
         self.lib.swlog_set_retention(self.h, -1, int(retention_bytes))
+        self._ret_default = int(retention_bytes)
+        self._ret_topic: dict[str, int] = {}
+        # protected topics (protect): consumer group -> longest a producer waits for room
+        self._protected: dict[str, dict[str, float]] = {}
+        self._room = threading.Condition(threading.Lock())
+        self.backpressure_waits = 0
         self.directory = directory
         # identity of this log's offsets: a memory-only log starts over at offset 0 each time, so
         # offsets recorded elsewhere (durable commit records) are scoped by it
@@ -193,6 +203,8 @@ class EventBus:
     def append(self, name: str, partition: int, records: list[tuple[bytes | None, bytes]], ts: int | None = None) -> int:
         if not records:
             return -1
+        if name in self._protected:
+            self._await_room(name, partition, sum(len(v) + len(k or b"") for k, v in records))
         t = self.topic(name)
         if len(records) == 1:
             k, v = records[0]
@@ -231,6 +243,8 @@ class EventBus:
         alive, and must not change, until retention drops the record; then ``on_release(owner)`` is
         called (a buffer pool takes it back) or, without a callback, the reference is dropped.
         A durable partition (files) copies the record instead and releases ``owner`` at once."""
+        if name in self._protected:
+            self._await_room(name, partition, int(nbytes))
         self._drain_released()
         ext = next(self._ext_ids)
         with self._lock:
@@ -433,6 +447,8 @@ class EventBus:
         n = len(key_off) - 1
         if n <= 0:
             return -1
+        if name in self._protected:
+            self._await_room(name, partition, int(val_off[-1]) + int(key_off[-1]))
         t = self.topic(name)
         kb = np.ascontiguousarray(keys, np.uint8) if len(keys) else np.zeros(1, np.uint8)
         vb = np.ascontiguousarray(vals, np.uint8) if len(vals) else np.zeros(1, np.uint8)
@@ -461,6 +477,11 @@ class EventBus:
 
     def commit(self, group: str, name: str, partition: int, offset: int):
         self.fast.swlog_commit(self.h, group.encode(), self.topic(name), partition, offset)
+        prot = self._protected.get(name)
+        if prot and group in prot:
+            self.hold(name, partition, offset, holder=("group", group))
+            with self._room:
+                self._room.notify_all()
 
     def committed(self, group: str, name: str, partition: int) -> int:
         return self.fast.swlog_committed(self.h, group.encode(), self.topic(name), partition)
@@ -468,6 +489,61 @@ class EventBus:
     def set_retention(self, name: str, retention_bytes: int):
         """Cap the retained bytes of every partition of a memory-only topic (0 = unlimited)."""
         self.lib.swlog_set_retention(self.h, self.topic(name), int(retention_bytes))
+        self._ret_topic[name] = int(retention_bytes)
+
+    # ------------------------------------------------------------------ backpressure
+    def protect(self, group: str, name: str, max_wait_s: float = 60.0):
+        """No silent loss on ``name`` for consumer ``group``: retention never drops a record the
+        group has not committed (a hold at its committed offset), and producers appending to the
+        topic wait -- up to ``max_wait_s``, then :class:`BackpressureTimeout` -- while the group's
+        unread bytes in the partition would pass the topic's retention.  Event sources then throttle
+        (an MQTT publisher is acknowledged only after the hand-off) instead of the log dropping
+        batches nobody read (reference: ``MqttInboundEventReceiver.java:166-215``)."""
+        with self._room:
+            self._protected.setdefault(name, {})[group] = float(max_wait_s)
+        for p in range(self.partitions(name)):
+            c = self.committed(group, name, p)
+            self.hold(name, p, c if c >= 0 else self.begin_offset(name, p), holder=("group", group))
+
+    def unprotect(self, group: str, name: str):
+        with self._room:
+            self._protected.get(name, {}).pop(group, None)
+            if not self._protected.get(name):
+                self._protected.pop(name, None)
+            self._room.notify_all()
+        for p in range(self.partitions(name)):
+            self.hold(name, p, None, holder=("group", group))
+
+    def unread_bytes(self, group: str, name: str, partition: int) -> int:
+        c = self.committed(group, name, partition)
+        return int(self.lib.swlog_bytes_from(self.h, self.topic(name), partition, c if c >= 0 else 0))
+
+    def _await_room(self, name: str, partition: int, nbytes: int):
+        groups = self._protected.get(name)
+        if not groups:
+            return
+        limit = self._ret_topic.get(name, self._ret_default)
+        if limit <= 0:
+            return
+        import time as _t
+        deadline = _t.monotonic() + max(groups.values())
+        waited = False
+        while True:
+            unread = max(self.unread_bytes(g, name, partition) for g in list(groups))
+            if unread == 0 or unread + nbytes <= limit:
+                return
+            if not waited:
+                self.backpressure_waits += 1
+                waited = True
+            left = deadline - _t.monotonic()
+            if left <= 0:
+                raise BackpressureTimeout(f"{name}[{partition}]: {unread} unread bytes of {limit} for "
+                                          f"{sorted(groups)}; the consumer is not keeping up")
+            with self._room:
+                self._room.wait(min(left, 0.05))
+            groups = self._protected.get(name)
+            if not groups:
+                return
 
     def retain_from(self, name: str, partition: int, offset: int) -> int:
         return self.lib.swlog_retain_from(self.h, self.topic(name), partition, offset)
@@ -657,6 +733,7 @@ class Consumer:
         self.positions: dict[tuple[str, int], int] = {}
         self._assigned: list = []
         self._held: set = set()             # partitions poll() holds for a zero-copy reader
+        self.lost = 0                       # records retention dropped before this consumer read them
         self._refresh()
         self.closed = False
 
@@ -736,6 +813,10 @@ class Consumer:
                     self._held.add(tp)
                 recs = read(tp[0], tp[1], self.positions[tp], budget)
                 if recs:
+                    if recs[0].offset > self.positions[tp]:
+                        # retention dropped records this group never read (an unprotected topic
+                        # whose consumer fell behind): counted, never silent
+                        self.lost += recs[0].offset - self.positions[tp]
                     out[tp] = recs
                     self.positions[tp] = recs[-1].offset + 1
                     budget -= len(recs)

@@ -26,7 +26,8 @@ class EngineConfig:
     names_cap: int = 4096            # new-name reports per step
     shuffle_slack: float = 1.1       # per-destination slab = slack * rec_cap / world (+1024)
     shuffle_pad: int = 1024          # records added to every slab (small-batch headroom)
-    carry_cap: int = 0               # records a full slab can defer to the next exchange (0 = rec_cap)
+    carry_cap: int = 0               # records full slabs can defer to the next exchange (0 = 3 * rec_cap)
+    carry_high: int = 0              # drivers stall new input while the carry exceeds this (0 = rec_cap)
     presence_missing_ms: int = 8 * 3600 * 1000   # DevicePresenceManager default (8h)
     presence_check_ms: int = 10 * 60 * 1000      # DevicePresenceManager default (10 min)
     rank: int = 0
@@ -45,8 +46,18 @@ class EngineConfig:
         self.name_slots = pow2_at_least(self.name_slots)
         self.state_slots = pow2_at_least(self.state_slots)
         self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + self.shuffle_pad
+        local = self.rec_cap
+        if self.world > 1:
+            # a rank can receive a full slab from every rank: the work batch after the exchange
+            # must hold world * shuf_cap records (skewed keys), or the surplus would be cut
+            self.rec_cap = max(self.rec_cap, self.world * self.shuf_cap)
+        # Lossless re-keying: spilled records carry over (up to carry_cap) and drivers feed an empty
+        # round instead of a new batch while the carry is above carry_high (should_stall), so with
+        # two rounds in flight the carry stays below carry_high + 2 * local <= carry_cap
+        if self.carry_high <= 0:
+            self.carry_high = local
         if self.carry_cap <= 0:
-            self.carry_cap = self.rec_cap
+            self.carry_cap = self.carry_high + 2 * local
 
     @classmethod
     def small(cls, **kw):

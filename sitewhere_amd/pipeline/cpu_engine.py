@@ -85,6 +85,9 @@ class CpuInboundEngine(EngineBase):
         self.carry = spill[:kept].copy()
         return send, cnt
 
+    def carry_count(self) -> int:
+        return len(self.carry)
+
     @staticmethod
     def unpack(recv: np.ndarray, rcnt) -> np.ndarray:
         return np.concatenate([recv[q, :int(rcnt[q])] for q in range(recv.shape[0])])

@@ -269,6 +269,16 @@ class EngineBase:
         batch, now_ms, token, presence = lag
         return [(token, self.step_framed(batch, now_ms, presence))]
 
+    def carry_count(self) -> int:
+        """Records deferred to the next exchange (host-known; multi-rank engines)."""
+        return 0
+
+    def should_stall(self) -> bool:
+        """Multi-rank drivers feed an empty round (exchange only) instead of a new batch while this
+        is true: skewed keys then slow the input down instead of losing records at ``carry_cap``.
+        Every rank still runs one round per iteration, so the collective stays in step."""
+        return self.world > 1 and self.carry_count() > self.cfg.carry_high
+
     @property
     def framed_pending(self) -> int:
         """Submitted batches whose results have not been returned yet."""

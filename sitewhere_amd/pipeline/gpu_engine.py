@@ -971,6 +971,13 @@ class GpuInboundEngine(EngineBase):
         seal(blk, first, now_ms, boot, self.rank, self.world)
         return blk
 
+    def carry_count(self) -> int:
+        """Re-key carry: from the pipelined runner's last snapshot, else read (a sync)."""
+        if self.world == 1:
+            return 0
+        v = self.__dict__.get("_carry_seen")
+        return v if v is not None else int(self.t["n_carry"].max().item())
+
     # ------------------------------------------------------------------ queries
     def stats_dict(self) -> dict:  # type: ignore[override]
         return EngineBase.stats_dict(self.t["stats"].cpu().numpy().view(np.uint64))
@@ -1195,6 +1202,7 @@ class PipelinedRunner:
         # per-slot end-of-step snapshot in mapped host memory (k_step_snapshot): scalars, encoder
         # meta, reject counters -- read after the step's event, no copy calls
         self.snap = [HostBuffer(engine.lib, 256) for _ in range(nb)]
+        self.cpar = [0] * nb              # live carry parity when slot b's snapshot was taken
         # the slow path runs off the submit thread: the GPU writes the snapshot into mapped host
         # memory, routing runs on one worker thread in batch order; rejects_floor() tells callers the
         # oldest batch whose rejects are not routed yet (its input offset must not be committed)
@@ -1273,9 +1281,12 @@ class PipelinedRunner:
             if self.produced[b]:
                 seg_meta = self.e.encode_block_async(b)
                 self.btag[b], self.bnow[b] = done_tag, self.e._step_now
+        nc = self.e.t.get("n_carry")
+        self.cpar[b] = getattr(self.e, "_carry_par", 0)
         rc = self.e.lib.sw_step_snapshot(ctypes.c_void_p(self.e.t["scalars"].data_ptr()),
                                          ctypes.c_void_p(0 if seg_meta is None else seg_meta.data_ptr()),
                                          ctypes.c_void_p(0 if rej_cnt is None else rej_cnt.data_ptr()),
+                                         ctypes.c_void_p(0 if nc is None else nc.data_ptr()),
                                          int(self.produced[b]), ctypes.c_void_p(self.snap[b].dev),
                                          ctypes.c_void_p(self.comp.cuda_stream))
         if rc:
@@ -1375,6 +1386,9 @@ class PipelinedRunner:
             self.ev_push[pb].synchronize()
         snap = self.snap[pb].view(np.uint32, 32)
         n_out = int(snap[7]) if self.produced[pb] else 0
+        if self.e.world > 1:
+            # re-key carry after this round: the parity its partition spilled into
+            self.e._carry_seen = int(snap[22 + self.cpar[pb]])
         self.pending = None
         if self.on_rejects is not None and self.produced[pb] and self.rtag[pb] is not None:
             n_rej = int(snap[24])

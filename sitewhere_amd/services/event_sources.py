@@ -388,13 +388,23 @@ class EventSourcesManager(TenantEngineLifecycleComponent):
                 groups.setdefault(max(p, 0), []).append(payload)      # unparsable: partition 0
         else:
             groups = {0: buf}
-        for p, payloads in sorted(groups.items()):
-            if hasattr(bus, "append_external"):
-                rec = RawBatchRecord.from_payloads(payloads)
-                bus.append_external(self.t_raw, p, rec, rec.ptr, rec.value_len)
-            else:
-                self.producer.send(self.t_raw, None, RawBatchRecord.from_payloads(payloads, pinned=False).value(),
-                                   partition=p)
+        items = sorted(groups.items())
+        for i, (p, payloads) in enumerate(items):
+            try:
+                if hasattr(bus, "append_external"):
+                    # on a protected raw topic this waits while the engine's consumer is behind
+                    # (EventBus.protect): the receiving thread -- and so the device -- is throttled
+                    rec = RawBatchRecord.from_payloads(payloads)
+                    bus.append_external(self.t_raw, p, rec, rec.ptr, rec.value_len)
+                else:
+                    self.producer.send(self.t_raw, None, RawBatchRecord.from_payloads(payloads, pinned=False).value(),
+                                       partition=p)
+            except Exception:
+                # nothing is dropped: the unpublished payloads go back to the front of the buffer
+                rest = [x for _, ps in items[i:] for x in ps]
+                with self._raw_lock:
+                    self._raw_buf[:0] = rest
+                raise
 
 
 class EventSourcesTenantEngine(MicroserviceTenantEngine):

@@ -298,6 +298,12 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             tune_gc_for_streaming()             # opt-in: measured gain is within run-to-run noise
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         self._resume_from_store()
+        bus = self.ms.instance.bus
+        if self.config.get("rawBackpressure", True) and hasattr(bus, "protect"):
+            # raw batches this engine has not committed are never dropped by retention; event
+            # sources wait for room instead (EventBus.protect)
+            for t in self.raw_consumer.topics:
+                bus.protect(self.raw_consumer.group, t, float(self.config.get("rawBackpressureWaitS", 60)))
         if self.async_store:
             self._store_thread = threading.Thread(target=self._store_loop, daemon=True,
                                                   name=f"engine-store-{self.tenant.token}")
@@ -306,6 +312,10 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
 
     def tenant_stop(self, monitor):
         self.raw_consumer.lifecycle_stop(monitor)
+        bus = self.ms.instance.bus
+        if hasattr(bus, "unprotect"):
+            for t in self.raw_consumer.topics:
+                bus.unprotect(self.raw_consumer.group, t)
         if self._store_thread is not None:
             self.flush()
             self._store_q.put(None)

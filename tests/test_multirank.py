@@ -289,3 +289,75 @@ def test_wire_pack_is_lossless_for_every_decoded_type():
     back = wire_unpack(wire_pack(r), 2)
     assert back.tobytes() == r.tobytes()
     assert EVENT_REC.itemsize == 80
+
+
+def _skewed_batch(world, rank, k, n=1200):
+    """Payloads of devices all owned by the other rank (every record crosses the exchange)."""
+    from sitewhere_amd.models import wire
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    heap, offs = gen_tokens("dev-", 0, N_DEV)
+    lo, hi = fingerprints(heap, offs)
+    theirs = np.nonzero(((hi >> np.uint64(32)) % np.uint64(world)) == (rank + 1) % world)[0]
+    msgs = [wire.measurements(f"dev-{int(theirs[(k * 131 + i) % len(theirs)])}", {"v": float(i)},
+                              event_date=NOW - 1000 + i, alternate_id=f"sk-{rank}-{k}-{i}") for i in range(n)]
+    return pack_messages(msgs)
+
+
+def _gloo_skew_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # slabs of ~250 records for ~1200 records per batch: every round spills, the carry would pass
+    # carry_cap (= carry_high + 2 * rec_cap) within a few rounds without the stall rule
+    e = CpuInboundEngine(EngineConfig.small(world=world, rank=rank, max_msgs=1200, shuffle_slack=0.2,
+                                            shuffle_pad=0))
+    shard_fleet(e, world, rank)
+    batches = [_skewed_batch(world, rank, k) for k in range(12)]
+    empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))
+    nxt = stalls = rounds = events = 0
+    peak = 0
+    while True:
+        if nxt < len(batches) and not e.should_stall():
+            raw, offs = batches[nxt]
+            nxt += 1
+        else:
+            stalls += nxt < len(batches)
+            raw, offs = empty
+        events += e.step(raw, offs, NOW, presence=False).n_events
+        rounds += 1
+        peak = max(peak, e.carry_count())
+        left = torch.tensor([len(batches) - nxt + e.carry_count()], dtype=torch.int64)
+        dist.all_reduce(left)                   # every rank runs the same number of rounds
+        if int(left) == 0 or rounds > 400:
+            break
+    s = e.stats_dict()
+    q.put((rank, events, s["shuffle_overflow"], s["shuffle_deferred"], stalls, peak, e.cfg.carry_cap, rounds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_skewed_keys_stall_instead_of_dropping():
+    """Two gloo ranks whose payloads all belong to the other rank, through slabs far smaller than a
+    batch: the carry would overflow carry_cap, so the drivers feed exchange-only rounds while it is
+    high (EngineBase.should_stall) -- shuffle_overflow stays 0 and every event is processed once."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_skew_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(o[2] == 0 for o in outs), outs                 # nothing dropped
+    assert all(o[3] > 0 for o in outs) and any(o[4] > 0 for o in outs), outs   # spilled, and stalled
+    assert all(o[5] <= o[6] for o in outs), outs              # carry stayed within carry_cap
+    assert sum(o[1] for o in outs) == 2 * 12 * 1200           # every event processed exactly once
