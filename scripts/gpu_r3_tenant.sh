@@ -16,3 +16,10 @@ for B in 262144 1048576; do
     tail -1 "$O/tenant_${B}_${P}.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["batch"], d["p_unregistered"], round(d["events_per_sec"]/1e6,1), "M/s", d["ms_per_batch"], "ms", d["mean_ms"], d.get("median_ms_second_half"), d["framed_trace_ms_per_batch"])'
   done
 done
+# 1M-payload, 200-batch soak through the bus: the producer outruns the engine, the protected raw
+# topic must throttle it (0 records lost)
+if [ "${SOAK:-1}" = "1" ]; then
+  timeout -k 10 600 python -u scripts/bench_tenant_path.py --devices 50000 --batch 1048576 --batches 200 --warmup 4 \
+    --via-bus --max-msgs 1048576 --no-alt-ids > "$O/soak_1m_200.log" 2>&1 || { tail -20 "$O/soak_1m_200.log"; exit 1; }
+  tail -1 "$O/soak_1m_200.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("soak", round(d["events_per_sec"]/1e6,1), "M/s lost", d["raw_records_lost"], "waits", d["backpressure_waits"], "events", d["events"])'
+fi

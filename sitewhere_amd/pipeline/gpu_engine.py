@@ -634,7 +634,7 @@ class GpuInboundEngine(EngineBase):
         size = max(need, min(full, -(-(need + need // 4) // (1 << 20)) * (1 << 20)))
         # results held by an overlapped tenant: in flight + store queue + storing, and -- with zero-copy
         # columnar payloads -- the batches the store and the enriched-batch topic retain
-        if len(pool) < self.PIN_POOL:
+        if len(pool) < (self.PIN_POOL if kind == "rows" else self.PIN_POOL_BLOCKS):
             pin = torch.empty(size, dtype=torch.uint8).pin_memory()
             pool.append((pin, pin.numpy()))
             st["new_pooled"] += 1
@@ -655,6 +655,7 @@ class GpuInboundEngine(EngineBase):
         return pin, pin.numpy(), False
 
     PIN_POOL = 24
+    PIN_POOL_BLOCKS = 64        # durable blocks: also held by the enriched-batch topic's retention window
     PIN_SPILL = 6
 
     def collect(self, sel: int, raw_host: np.ndarray | None, from_device: bool = False) -> StepResult:

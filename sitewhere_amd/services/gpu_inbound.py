@@ -610,8 +610,10 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     bus = self.ms.instance.bus
                     pl = item.payload
                     if self.storage == "durable" and hasattr(bus, "append_arrays") and not isinstance(pl, bytes):
-                        # a copy into the log: the topic's retention would otherwise hold the engine's
-                        # pinned block buffers (the store releases them as soon as they are on disk)
+                        # a copy into the log (parallel, GIL released): published in place, the
+                        # topic's retention window would hold the engine's pinned block buffers and
+                        # grow its pool to that window (measured: slower until it is warm); the
+                        # store releases them as soon as they are on disk
                         v = np.asarray(pl).reshape(-1)
                         bus.append_arrays(self.t_enriched_batches, self._batch_partition(bus), np.zeros(1, np.uint8),
                                           np.zeros(2, np.int64), v, np.array([0, v.nbytes], np.int64), ts=now)
