@@ -135,14 +135,89 @@ __global__ void k_scan_apply(const uint32_t* __restrict__ in, int64_t n, const u
   }
 }
 
+// Single-pass exclusive scan (decoupled look-back): one dispatch instead of tiles + sums + apply.
+// Workgroups take tiles in ticket order, publish their tile aggregate, then walk back over their
+// predecessors' 64-bit state words (flag in the top bits) until an inclusive prefix.  The
+// workgroup that finishes last zeroes the state (ticket, done counter, tile words), so the next
+// launch -- including a hipGraph replay with the same arguments -- starts clean: no memset node.
+// state = u64[2 + nt]: [0] ticket, [1] done, [2..] tile words.
+#define SLB_AGG (1ull << 62)
+#define SLB_INC (2ull << 62)
+#define SLB_VAL ((1ull << 62) - 1)
+#define SLB_SPIN_LIMIT (1u << 26)
+
+__device__ __forceinline__ ull slb_load(const ull* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void slb_store(ull* p, ull v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_scan_lb(const uint32_t* __restrict__ in, int64_t n, uint32_t* __restrict__ out,
+                          uint32_t* __restrict__ total, ull* __restrict__ state, int64_t nt) {
+  __shared__ uint32_t lds[WAVES + 1];
+  __shared__ uint32_t s_tile;
+  __shared__ ull s_excl;
+  if (threadIdx.x == 0) s_tile = (uint32_t)atomicAdd(&state[0], 1ull);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t base = tile * TILE + (int64_t)threadIdx.x * TILE_ITEMS;
+  uint32_t v[TILE_ITEMS];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < TILE_ITEMS; ++k) {
+    const int64_t i = base + k;
+    v[k] = i < n ? in[i] : 0u;
+    sum += v[k];
+  }
+  uint32_t agg;
+  const uint32_t pre = block_excl_scan(sum, &agg, lds);
+  if (threadIdx.x == 0) {
+    ull excl = 0;
+    ull* tw = state + 2;
+    if (tile == 0) {
+      slb_store(&tw[0], SLB_INC | agg);
+    } else {
+      slb_store(&tw[tile], SLB_AGG | agg);
+      for (int64_t p = tile - 1; p >= 0;) {
+        ull w = slb_load(&tw[p]);
+        uint32_t spins = 0;
+        while ((w >> 62) == 0 && ++spins < SLB_SPIN_LIMIT) {
+          __builtin_amdgcn_s_sleep(1);
+          w = slb_load(&tw[p]);
+        }
+        excl += w & SLB_VAL;
+        if ((w >> 62) == 2) break;
+        --p;
+      }
+      slb_store(&tw[tile], SLB_INC | (excl + agg));
+    }
+    s_excl = excl;
+    if (tile == nt - 1 && total) *total = (uint32_t)(excl + agg);
+  }
+  __syncthreads();
+  uint32_t run = (uint32_t)s_excl + pre;
+#pragma unroll
+  for (int k = 0; k < TILE_ITEMS; ++k) {
+    const int64_t i = base + k;
+    if (i < n) out[i] = run;
+    run += v[k];
+  }
+  __syncthreads();
+  // the last workgroup to finish resets the state for the next launch (nobody reads it any more)
+  if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(&state[1], 1ull) == (ull)(nt - 1));
+  __syncthreads();
+  if (s_tile) {
+    for (int64_t i = threadIdx.x; i < nt + 2; i += BLK) state[i] = 0;
+  }
+}
+
 static int launch_scan(const uint32_t* in, int64_t n, uint32_t* out, uint32_t* total, uint32_t* tmp,
                        int64_t tmp_len, hipStream_t s) {
   int64_t nt = (n + TILE - 1) / TILE;
   if (nt < 1) nt = 1;
-  if (nt > tmp_len) return -2;
-  k_scan_tiles<<<(unsigned)nt, BLK, 0, s>>>(in, n, tmp);
-  k_scan_sums<<<1, BLK, 0, s>>>(tmp, nt, total);
-  k_scan_apply<<<(unsigned)nt, BLK, 0, s>>>(in, n, tmp, out);
+  if (2 * (nt + 2) > tmp_len || ((uintptr_t)tmp & 7)) return -2;     // tmp holds u64[2 + nt]
+  k_scan_lb<<<(unsigned)nt, BLK, 0, s>>>(in, n, out, total, reinterpret_cast<ull*>(tmp), nt);
   return 0;
 }
 
@@ -433,14 +508,21 @@ __global__ void k_unpack(const SwWireRec* __restrict__ recv, const uint32_t* __r
 }
 
 // ============================================================================ validate
-__device__ __forceinline__ void intern_insert(ull* __restrict__ key, int64_t mask, ull h) {
+// Intern a name hash; the thread that claims a new slot gives it the next dense id (the ids are
+// rank-local state-map keys, read by later kernels of the step -- no table-wide assign pass).
+__device__ __forceinline__ void intern_insert(ull* __restrict__ key, int32_t* __restrict__ ids,
+                                              int32_t* __restrict__ counter, int64_t mask, ull h) {
   int64_t slot = (int64_t)(h & (ull)mask);
   for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
     ull old = key[slot];
     if (old == h) return;
     if (old == 0) {
       old = atomicCAS(&key[slot], 0ull, h);
-      if (old == 0 || old == h) return;
+      if (old == 0) {
+        ids[slot] = atomicAdd(counter, 1);
+        return;
+      }
+      if (old == h) return;
     }
     slot = (slot + 1) & mask;
   }
@@ -473,7 +555,7 @@ __global__ void k_lookup(SwEngineArgs a) {
       if (et >= 16) { st = SW_ST_CONTROL; asg = -1; }
       else if (dev < 0) st = SW_ST_UNREGISTERED;
       else st = asg >= 0 ? SW_ST_OK : SW_ST_UNASSIGNED;
-      if (st == SW_ST_OK && nh) intern_insert((ull*)a.nm_key, a.nm_mask, nh);
+      if (st == SW_ST_OK && nh) intern_insert((ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, nh);
     }
     a.status[i] = st;
     a.ev_dev[i] = dev;
@@ -486,7 +568,7 @@ __global__ void k_lookup(SwEngineArgs a) {
 // generation before).  An event whose id is in `prev` is a duplicate; otherwise it is inserted into
 // `cur`, where the first occurrence (lowest global sequence) wins and every later one -- in this
 // batch or any later batch of the generation -- is a duplicate.  Before a step whose ids could push
-// `cur` past half its slots, the generations rotate (k_dedup_rotate): `prev` is forgotten and
+// `cur` past half its slots, the generations rotate (k_process_begin): `prev` is forgotten and
 // cleared to become the new `cur`.  The window therefore covers the last slots/2 - rec_cap to
 // slots - rec_cap distinct ids, probes stay short (load <= 0.5), and a probe that still hits
 // MAX_PROBE is counted (SW_STAT_DEDUP_OVERFLOW) rather than silently ignored.
@@ -503,19 +585,6 @@ __device__ __forceinline__ bool dd_find(const ull* __restrict__ key, int64_t mas
 
 // Rotation decision (one thread) at the start of the dedup phase; k_dedup_clear does the clearing.
 // dd_meta = [generation, ids in cur, rotate flag, pad].
-__global__ void k_dedup_rotate(int64_t* __restrict__ meta, int64_t half, int64_t batch_cap, ull* __restrict__ stats) {
-  if (threadIdx.x == 0 && BID == 0) {
-    if (meta[1] + batch_cap > half) {
-      meta[0] ^= 1;
-      meta[1] = 0;
-      meta[2] = 1;
-      stats[SW_STAT_DEDUP_ROTATIONS] += 1;
-    } else {
-      meta[2] = 0;
-    }
-  }
-}
-
 __global__ void k_dedup_clear(ull* __restrict__ key, ull* __restrict__ seq, int64_t slots,
                               const int64_t* __restrict__ meta) {
   if (meta[2] == 0) return;
@@ -660,17 +729,11 @@ __device__ __forceinline__ int64_t nm_probe(const K* __restrict__ key, int64_t m
 }
 
 __global__ void k_intern_insert_list(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                                     ull* __restrict__ key, int64_t mask) {
+                                     ull* __restrict__ key, int32_t* __restrict__ ids, int32_t* __restrict__ counter,
+                                     int64_t mask) {
   const uint32_t n = *n_ptr;
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
-    if (recs[j].name_hash) intern_insert(key, mask, recs[j].name_hash);
-}
-
-// Give every newly inserted name slot a dense id (ids are rank-local state-map keys).
-__global__ void k_intern_assign(const ull* __restrict__ key, int32_t* __restrict__ ids, int64_t slots,
-                                int32_t* __restrict__ counter) {
-  for (int64_t s = (int64_t)BID * BLK + threadIdx.x; s < slots; s += (int64_t)gridDim.x * BLK)
-    if (key[s] != 0 && ids[s] < 0) ids[s] = atomicAdd(counter, 1);
+    if (recs[j].name_hash) intern_insert(key, ids, counter, mask, recs[j].name_hash);
 }
 
 // ============================================================================ device state map
@@ -1035,11 +1098,28 @@ __global__ void k_decode_begin(SwEngineArgs a) {
   }
 }
 
+// Start of the process phase, one thread: (world == 1) the end of the decode phase -- record
+// clamp, new-name stats, the work batch is the decoded batch --, the step's cursor / counters, and
+// the dedup window rotation (before a step that could pass the live generation's half load).
 __global__ void k_process_begin(SwEngineArgs a) {
   if (threadIdx.x == 0 && BID == 0) {
+    if (a.world == 1) {
+      if (*a.n_recs > a.rec_cap) *a.n_recs = (uint32_t)a.rec_cap;
+      ((ull*)a.stats)[SW_STAT_NEW_NAMES] += *a.n_new_names;
+      *a.n_work = *a.n_recs;
+    }
     *a.step_cursor0 = *a.store_cursor;
     *a.n_gen = 0;
     *a.n_out = 0;
+    int64_t* meta = a.dd_meta;
+    if (meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) {
+      meta[0] ^= 1;
+      meta[1] = 0;
+      meta[2] = 1;
+      ((ull*)a.stats)[SW_STAT_DEDUP_ROTATIONS] += 1;
+    } else {
+      meta[2] = 0;
+    }
   }
 }
 
@@ -1052,6 +1132,7 @@ __global__ void k_gen_clamp(SwEngineArgs a, uint32_t* gen_rules) {
 
 __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
   if (threadIdx.x == 0 && BID == 0) {
+    *a.store_cursor += *a.n_gen;                 // the generated events persisted last
     *a.n_out = (uint32_t)(*a.store_cursor - *a.step_cursor0);
     *a.seq_base += *a.n_work;
     ull* st = (ull*)a.stats;
@@ -1228,7 +1309,7 @@ int sw_phase_decode(const SwEngineArgs* ap, hipStream_t s) {
   int rc = launch_scan(a.msg_cnt, a.n_msgs, a.msg_evoff, a.n_recs, a.scan_tmp, a.scan_tmp_len, s);
   if (rc) return rc;
   k_decode_emit<<<nb, BLK, 0, s>>>(a);
-  k_decode_end<<<1, 64, 0, s>>>(a);
+  if (a.world > 1) k_decode_end<<<1, 64, 0, s>>>(a);     // world == 1: k_process_begin does it
   return (int)hipGetLastError();
 }
 
@@ -1268,9 +1349,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
   if (2 * ntiles > a.scan_tmp_len) return -4;
   k_process_begin<<<1, 64, 0, s>>>(a);
-  if (a.world == 1) (void)hipMemcpyAsync(a.n_work, a.n_recs, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
   k_lookup<<<g, BLK, 0, s>>>(a);
-  k_dedup_rotate<<<1, 64, 0, s>>>(a.dd_meta, (a.dd_mask + 1) / 2, a.rec_cap, (ull*)a.stats);
   k_dedup_clear<<<grid_for(a.dd_mask + 1), BLK, 0, s>>>((ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask + 1, a.dd_meta);
   k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base,
                                    a.dd_meta, (ull*)a.stats);
@@ -1284,8 +1363,6 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, cmp_off, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx,
                                                a.n_ok, a.n_rej);
   k_reject_stats<<<64, BLK, 0, s>>>(a);
-  // dense ids for names interned by k_lookup (state-map keys)
-  k_intern_assign<<<grid_for(a.nm_mask + 1), BLK, 0, s>>>((const ull*)a.nm_key, a.nm_id, a.nm_mask + 1, a.nm_counter);
   // persist + enrich + state for the validated events
   k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok);
   k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok);
@@ -1306,11 +1383,9 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_presence<<<grid_for(a.n_asg), BLK, 0, s>>>(a);   // exits at once when presence is off this step
   k_gen_clamp<<<1, 64, 0, s>>>(a, nullptr);
   const int gg = grid_for(a.gen_cap);
-  k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_mask);
-  k_intern_assign<<<grid_for(a.nm_mask + 1), BLK, 0, s>>>((const ull*)a.nm_key, a.nm_id, a.nm_mask + 1, a.nm_counter);
+  k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask);
   k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen);
   k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen);
-  k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_gen);
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
 }

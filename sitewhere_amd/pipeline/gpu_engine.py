@@ -122,7 +122,8 @@ class GpuInboundEngine(EngineBase):
         ntiles = (c.rec_cap + tile - 1) // tile
         mtiles = (c.max_msgs + tile - 1) // tile
         ptiles = (c.carry_cap + c.rec_cap + tile - 1) // tile     # partition input: carry + records
-        scan_tmp = max(ptiles * 2 * max(1, c.world), mtiles, 2 * ntiles) + 64
+        # single-pass scans keep u64 look-back state (2 + tiles words) in it, zeroed by each scan
+        scan_tmp = 2 * (max(ptiles * 2 * max(1, c.world), mtiles, 2 * ntiles) + 64)
         self.t = t = {}
         # decode
         t["msg_cnt"] = z(c.max_msgs + 1, i32)
