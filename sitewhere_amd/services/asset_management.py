@@ -78,8 +78,9 @@ class AssetManagementTenantEngine(MicroserviceTenantEngine):
         self.api = {"AssetManagement": self.management}
 
     def tenant_bootstrap(self, dataset_template, monitor):
-        from .datasets import bootstrap_asset_model
-        bootstrap_asset_model(self.management, dataset_template)
+        from .builders import AssetBuilder
+        from .dataset_runner import run_initializers
+        run_initializers(self, "assetManagement", dataset_template, {"asset_builder": AssetBuilder(self.management)})
 
 
 class AssetManagementMicroservice(MultitenantMicroservice):

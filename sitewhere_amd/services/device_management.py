@@ -688,8 +688,13 @@ class DeviceManagementTenantEngine(MicroserviceTenantEngine):
                               json.dumps({"kind": kind, "entity": codec.to_wire(entity)}).encode())
 
     def tenant_bootstrap(self, dataset_template, monitor):
-        from .datasets import bootstrap_device_model
-        bootstrap_device_model(self.management, dataset_template)
+        from .builders import DeviceBuilder, EventBuilder
+        from .dataset_runner import run_initializers
+        token = self.tenant.token
+        run_initializers(self, "deviceManagement", dataset_template, {
+            "device_builder": DeviceBuilder(self.management, self.ms.logger),
+            "event_builder": EventBuilder(lambda: self.ms.api("DeviceEventManagement", token), self.management,
+                                          logger=self.ms.logger)})
 
 
 class DeviceManagementMicroservice(MultitenantMicroservice):

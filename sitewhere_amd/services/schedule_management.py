@@ -220,8 +220,10 @@ class ScheduleManagementTenantEngine(MicroserviceTenantEngine):
         self.scheduler.stop()
 
     def tenant_bootstrap(self, dataset_template, monitor):
-        from .datasets import bootstrap_schedule_model
-        bootstrap_schedule_model(self.management, dataset_template)
+        from .builders import ScheduleBuilder
+        from .dataset_runner import run_initializers
+        run_initializers(self, "scheduleManagement", dataset_template,
+                         {"schedule_builder": ScheduleBuilder(self.management)})
 
 
 class ScheduleManagementMicroservice(MultitenantMicroservice):

@@ -119,14 +119,6 @@ TENANT_TEMPLATES["gpu-memory"]["services"]["inbound-processing"]["storage"] = "c
 TENANT_TEMPLATES["gpu-memory"]["services"]["event-management"] = {"datastore": {"type": "columnar",
                                                                                 "retentionRows": 1 << 28}}
 
-DATASET_TEMPLATES = {
-    "empty": {"name": "Empty dataset", "description": "No data is created."},
-    "construction": {"name": "Construction site", "description": "Device types, devices, assignments, areas, zones, "
-                                                                  "assets and schedules for a construction site."},
-    "airtraffic": {"name": "Air traffic", "description": "Aircraft tracking devices with a flight-zone model."},
-}
-
-
 class TenantManagement:
     TENANTS = "tenants"
 
@@ -198,7 +190,9 @@ class TenantManagement:
         return [{"id": k, "name": v["name"]} for k, v in sorted(TENANT_TEMPLATES.items())]
 
     def get_dataset_templates(self) -> list[dict]:
-        return [{"id": k, **v} for k, v in sorted(DATASET_TEMPLATES.items())]
+        from .dataset_runner import dataset_templates
+        return [{k: v for k, v in meta.items() if k != "initializers"} for _, meta in
+                sorted(dataset_templates().items())]
 
     def _require_id(self, id: str) -> Tenant:
         t = self._s.get(self.TENANTS, id)

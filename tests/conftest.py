@@ -13,6 +13,10 @@ def pytest_configure(config):
     if "SITEWHERE_DATA_DIR" not in os.environ:
         import tempfile
         os.environ["SITEWHERE_DATA_DIR"] = tempfile.mkdtemp(prefix="sw-test-data-")
+    # dataset initializers (sitewhere_amd/datasets) build small tenants under test
+    for k, v in (("DEVICES_PER_SITE", "3"), ("MEASUREMENTS_PER_ASSIGNMENT", "10"), ("LOCATIONS_PER_ASSIGNMENT", "8"),
+                 ("FLIGHTS", "4"), ("POSITIONS_PER_FLIGHT", "6")):
+        os.environ.setdefault("SITEWHERE_DATASET_" + k, v)
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")
 

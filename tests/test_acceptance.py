@@ -18,6 +18,7 @@ import time
 import pytest
 
 from sitewhere_amd.assembly import SiteWhereInstance
+from sitewhere_amd.services.dataset_runner import params
 from sitewhere_amd.models import wire
 from sitewhere_amd.runtime.config import dump_document
 
@@ -208,9 +209,10 @@ def test_rpc_waits_for_starting_tenant_engine(sw):
                                                           "datasetTemplateId": "construction"}))
     dm = sw["event-sources"].api("DeviceManagement", "late")
     n = sw.instance.system_user.run(lambda: dm.list_devices({"pageSize": 0}).num_results, "late")
-    assert 0 <= n <= 20          # engine up (bootstrap may still be creating the dataset)
+    full = 20 + params()["devices_per_site"]          # demo fleet + scripted devices of the dataset
+    assert 0 <= n <= full        # engine up (bootstrap may still be creating the dataset)
     assert wait_until(lambda: sw.instance.system_user.run(lambda: dm.list_devices({"pageSize": 0}).num_results,
-                                                          "late") == 20, 30)
+                                                          "late") == full, 30)
 
 
 def test_concurrent_rpc_race_check(sw):

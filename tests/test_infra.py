@@ -14,6 +14,7 @@ import pytest
 
 from sitewhere_amd.bus.log import EventBus
 from sitewhere_amd.coord.store import NODE_ADDED, NODE_REMOVED, Coordination, InterProcessMutex, NoNodeError
+from sitewhere_amd.services.dataset_runner import params as dataset_params
 from sitewhere_amd.rpc.infra import InfraServer, RemoteCoordination, RemoteEventBus
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -139,12 +140,12 @@ def test_multiprocess_instance(infra, tmp_path):
         while time.time() < end:
             try:
                 n = inst.system_user.run(lambda: dm.list_devices({"pageSize": 0}).num_results, "default")
-                if n == 20:
+                if n == 20 + dataset_params()["devices_per_site"]:          # demo fleet + scripted
                     break
             except Exception:
                 pass
             time.sleep(0.2)
-        assert n == 20
+        assert n == 20 + dataset_params()["devices_per_site"]
         um = inst.router.proxy("UserManagement")
         assert inst.system_user.run(lambda: um.get_user_by_username("admin")).username == "admin"
         em = inst.router.proxy("DeviceEventManagement", "default")

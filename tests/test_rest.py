@@ -8,6 +8,7 @@ import pytest
 from fastapi.testclient import TestClient
 
 from sitewhere_amd.assembly import SiteWhereInstance
+from sitewhere_amd.services.dataset_runner import params as dataset_params
 
 API = "/sitewhere/api"
 
@@ -46,7 +47,8 @@ def test_tenant_headers_required(env):
 def test_device_crud_and_assignment_events(env):
     _, client, h = env
     r = client.get(f"{API}/devices", headers=h, params={"pageSize": 5})
-    assert r.status_code == 200 and r.json()["numResults"] == 20 and len(r.json()["results"]) == 5
+    assert r.status_code == 200 and r.json()["numResults"] == 20 + dataset_params()["devices_per_site"] \
+        and len(r.json()["results"]) == 5
     r = client.post(f"{API}/devices", headers=h, json={"token": "rest-dev-1", "deviceTypeToken": "raspberrypi"})
     assert r.status_code == 200, r.text
     assert client.get(f"{API}/devices/rest-dev-1", headers=h).json()["token"] == "rest-dev-1"
@@ -329,7 +331,8 @@ def test_include_flags_on_areas_customers_states_and_invocations(env):
             break
         time.sleep(0.1)
     assert states and states[0]["lastMeasurementEvents"]["fuel"]["value"] == 0.5
-    cmd = client.get(f"{API}/commands", headers=h, params={"pageSize": 1}).json()["results"][0]
+    cmd = next(c for c in client.get(f"{API}/commands", headers=h, params={"pageSize": 0}).json()["results"]
+               if c["token"] == "meitrack-ping")
     dev_type = client.get(f"{API}/devicetypes", headers=h, params={"pageSize": 0}).json()["results"]
     dt = next(t for t in dev_type if t["id"] == cmd["deviceTypeId"])
     dev = client.get(f"{API}/devices", headers=h, params={"deviceType": dt["token"], "excludeAssigned": "false",

@@ -47,9 +47,9 @@ def test_instance_bootstrap(sw):
     t = as_system(sw, lambda: tm.get_tenant_by_token("default"))
     assert t is not None and t.dataset_template_id == "construction"
     dm = sw.api("DeviceManagement", "default")
-    assert as_system(sw, lambda: dm.list_devices({"pageSize": 0}).num_results) == 20
+    assert as_system(sw, lambda: dm.list_devices({"pageSize": 0}).num_results) == 23      # 3 scripted + 20 demo
     am = sw.api("AssetManagement", "default")
-    assert as_system(sw, lambda: am.list_assets().num_results) == 6
+    assert as_system(sw, lambda: am.list_assets().num_results) == 21
     sm = sw.api("ScheduleManagement", "default")
     assert as_system(sw, lambda: sm.get_schedule_by_token("every-hour")) is not None
 
@@ -320,8 +320,10 @@ def test_columnar_tenant_end_to_end():
         assert res.num_results == 50 and len(res.results) == 10
         assert [m.value for m in res.results[:3]] == [69.0, 68.0, 67.0]          # newest first
         assert res.results[0].name == "temp" and res.results[0].customer_id is not None
-        loc = run(lambda: em.list_locations_for_index("Customer", [res.results[0].customer_id])).results
-        assert loc and loc[0].latitude == 34.0
+        loc = run(lambda: em.list_locations_for_index("Customer", [res.results[0].customer_id],
+                                                      {"pageSize": 0})).results
+        loc = [x for x in loc if x.latitude == 34.0 and x.device_assignment_id == dev.device_assignment_id]
+        assert len(loc) == 1              # (the rest is the construction dataset's location history)
         one = run(lambda: em.get_device_event_by_id(res.results[0].id))
         assert one.value == 69.0
         rng = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
