@@ -1440,6 +1440,24 @@ int sw_registry_patch(SwRegSlot* reg, const int64_t* slots, const SwRegSlot* val
   return (int)hipGetLastError();
 }
 
+// Per-assignment device-state lookup: one thread per candidate (name id, kind) probes the state map
+// read-only for its (assignment, name, kind) key.  Name ids are dense (claim-time counter), so the
+// candidates are 2 x names -- a few thousand probes instead of a pass over all state_slots (GBs at
+// bench sizing).  Hits are appended to `out` (at most 2 x n_ids rows).
+__global__ void k_state_lookup(const SwMsSlot* __restrict__ ms, int64_t mask, int32_t asg, int32_t n_ids,
+                               SwMsSlot* __restrict__ out, uint32_t* __restrict__ n_out) {
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < 2 * (int64_t)n_ids; i += (int64_t)gridDim.x * BLK) {
+    const ull k = ((((ull)(uint32_t)asg) << 32) | ((ull)(uint32_t)(i >> 1) << 1) | (ull)(i & 1)) + 1ull;
+    int64_t slot = (int64_t)(sw_mix64(k) & (ull)mask);
+    for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+      const ull kk = ms[slot].key;
+      if (kk == k) { out[atomicAdd(n_out, 1u)] = ms[slot]; break; }
+      if (kk == 0) break;
+      slot = (slot + 1) & mask;
+    }
+  }
+}
+
 // Standalone batched point-in-polygon (used by the rule service for ad-hoc zone queries).
 __global__ void k_pip_batch(const double* pts, int64_t n_pts, const double* vtx, const int32_t* off, int64_t n_zones,
                             uint8_t* out) {
@@ -1457,6 +1475,14 @@ int sw_store_filter(const uint8_t* etype, const int32_t* asg, const int64_t* dat
   if (n_rows > 0)
     k_store_filter<<<grid_for(n_rows), BLK, 0, s>>>(etype, asg, date, n_rows, et, bits, n_asg, lo, hi, out_rows, cap,
                                                     n_match);
+  return (int)hipGetLastError();
+}
+
+int sw_state_lookup(const SwMsSlot* ms, int64_t mask, int32_t asg, int32_t n_ids, SwMsSlot* out, uint32_t* n_out,
+                    hipStream_t s) {
+  hipError_t e = hipMemsetAsync(n_out, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return (int)e;
+  if (n_ids > 0) k_state_lookup<<<grid_for(2 * (int64_t)n_ids), BLK, 0, s>>>(ms, mask, asg, n_ids, out, n_out);
   return (int)hipGetLastError();
 }
 

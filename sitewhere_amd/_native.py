@@ -27,7 +27,7 @@ CSRC = ROOT / "csrc"
 GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
 
 _NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp", CSRC / "native" / "swseg.cpp",
-               CSRC / "native" / "swroute.cpp"]
+               CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp"]
 _GPU_SRC = [CSRC / "hip" / "swgpu.hip", CSRC / "hip" / "swseg.hip"]
 _HEADERS = sorted((CSRC / "include").glob("*.h"))
 
@@ -254,6 +254,7 @@ def gpu():
         _proto(lib, "sw_store_filter", c_int32, P, P, P, c_int64, c_int32, P, c_int64, c_int64, c_int64, P, c_int64,
                P, P)
         _proto(lib, "sw_scan_u32", c_int32, P, c_int64, P, P, P, c_int64, P)
+        _proto(lib, "sw_state_lookup", c_int32, P, c_int64, c_int32, c_int32, P, P, P)
         _proto(lib, "sw_abi_sizes", c_int32, P)
         _proto(lib, "sw_host_alloc", c_int32, c_int64, P, P)
         _proto(lib, "sw_host_free", c_int32, P)

@@ -211,7 +211,7 @@ for tok in ("galaxytab", "meitrack", "raspberrypi", "iphone6s", "openhab"):
                                   ("bannerMessage", "Show a banner", [("message", "String", True)])):
         c = db.new_command(tok, f"{tok}-{suffix}", ns, suffix).with_description(desc)
         for pname, ptype, req in params_:
-            c._param(pname, ptype, req)
+            {"String": c.with_string_parameter, "Int32": c.with_int32_parameter}[ptype](pname, req)
         db.persist(c)
     for code, sname, color in (("ok", "Operational", "#dcf5dc"), ("warn", "Warning", "#f5f5dc"),
                                ("err", "Error", "#f5dcdc")):

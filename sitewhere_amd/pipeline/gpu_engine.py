@@ -995,15 +995,23 @@ class GpuInboundEngine(EngineBase):
         return {int(k): int(i) for k, i in zip(keys[sel], ids[sel])}
 
     def device_state(self, asg: int) -> dict:
-        """Last-known state of one assignment.  The merged-state table is filtered on the device and
-        only the assignment's slots (and their name-table entries) cross PCIe -- the table is
-        ``state_slots`` x 32 B, GBs at bench sizing."""
+        """Last-known state of one assignment.  ``k_state_lookup`` probes the merged-state map for
+        the assignment's (name id, kind) keys -- 2 x names read-only probes, not a pass over the
+        ``state_slots`` x 32 B table (GBs at bench sizing) -- and only the hits (and their
+        name-table entries) cross PCIe."""
         from ..models.columnar import ASG_STATE
         with self._lock:
-            ms = self.t["ms"].view(-1, 4)
-            keys = ms[:, 0]
-            hit = torch.nonzero((keys != 0) & (((keys - 1) >> 32) == int(asg))).flatten()
-            rows = ms[hit].cpu().numpy().view(np.uint64)
+            stream = torch.cuda.current_stream(self.device)
+            n_ids = int(self.t["nm_counter"].item())
+            if getattr(self, "_sl_rows", None) is None or self._sl_rows.shape[0] < 2 * max(n_ids, 1):
+                self._sl_rows = torch.zeros((2 * max(n_ids, 64), 4), dtype=torch.int64, device=self.device)
+                self._sl_n = torch.zeros(1, dtype=torch.int32, device=self.device)
+            rc = self.lib.sw_state_lookup(ctypes.c_void_p(_ptr(self.t["ms"])), self.cfg.state_slots - 1, int(asg),
+                                          n_ids, ctypes.c_void_p(_ptr(self._sl_rows)), ctypes.c_void_p(_ptr(self._sl_n)),
+                                          ctypes.c_void_p(stream.cuda_stream))
+            if rc:
+                raise RuntimeError(f"sw_state_lookup failed ({rc})")
+            rows = self._sl_rows[:int(self._sl_n.item())].cpu().numpy().view(np.uint64)
             st = self.t["st"].view(-1, 4)[asg].cpu().numpy().view(ASG_STATE)[0]
             nids = np.unique(((rows[:, 0] - np.uint64(1)) & np.uint64(0xFFFFFFFF)) >> np.uint64(1)).astype(np.int64)
             inv = {}

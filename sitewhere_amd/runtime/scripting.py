@@ -7,6 +7,20 @@ management gRPC ``GetScriptTemplates`` / ``GetScriptTemplateContent``.  Groovy d
 filters, routers and dataset initializers become Python scripts; each script defines the entry
 point its extension point expects (``decode(payload, metadata)``, ``encode(execution)``,
 ``filter(event)``, ``route(execution)``, ``initialize(api)``...).
+
+Trust model (the reference runs Groovy with full JVM privileges):
+
+* ``isolation="thread"`` (default): scripts run in this process with restricted builtins, a module
+  allow-list and a source check (``check_source``: no ``_``-prefixed attributes or dunder names, no
+  frame / code / traceback introspection attributes).  That stops accidents and the well-known
+  ``().__class__.__base__.__subclasses__()`` escape, but CPython offers no in-process sandbox:
+  scripts in this mode are tenant-administrator code and are trusted like the reference's Groovy.
+* ``isolation="process"`` (``SITEWHERE_SCRIPT_ISOLATION=process``): data-in / data-out entry points
+  (decoders, deduplicators, metadata extractors, command encoders / routers, connector filters)
+  run in a worker process (``runtime/script_sandbox.py``) under rlimits and a seccomp-BPF syscall
+  allow-list (``csrc/native/swsandbox.cpp``): no files, sockets, exec or fork, whatever the script
+  does to the interpreter.  A call that times out kills the worker.  Entry points handed live API
+  objects (rule scripts, REST poll scripts, dataset initializers) always run in-process.
 """
 from __future__ import annotations
 
@@ -34,6 +48,34 @@ def _restricted_import(name, globals=None, locals=None, fromlist=(), level=0):
     if name.split(".")[0] not in _ALLOWED_MODULES:
         raise ImportError(f"module {name!r} is not available to scripts")
     return __import__(name, globals, locals, fromlist, level)
+
+
+# attributes that reach frames, code objects or module globals without a leading underscore
+_DENIED_ATTRS = frozenset((
+    "gi_frame", "gi_code", "gi_yieldfrom", "cr_frame", "cr_code", "cr_await", "ag_frame", "ag_code", "ag_await",
+    "f_back", "f_globals", "f_locals", "f_builtins", "f_code", "f_trace", "tb_frame", "tb_next", "func_globals",
+    "co_code", "co_consts", "mro"))
+
+
+def check_source(source: str, name: str = "<script>"):
+    """Reject script source that reaches interpreter internals (see the module docstring): any
+    ``_``-prefixed attribute, any dunder name other than ``__name__``, and the introspection
+    attributes in ``_DENIED_ATTRS``.  Raises ``SiteWhereException`` naming the line."""
+    import ast
+    try:
+        tree = ast.parse(source, name)
+    except SyntaxError as e:
+        raise SiteWhereException(f"script {name}: {e}") from e
+    for node in ast.walk(tree):
+        bad = None
+        if isinstance(node, ast.Attribute) and (node.attr.startswith("_") or node.attr in _DENIED_ATTRS):
+            bad = node.attr
+        elif isinstance(node, ast.Name) and node.id.startswith("__") and node.id != "__name__":
+            bad = node.id
+        elif isinstance(node, (ast.FunctionDef, ast.ClassDef)) and node.name.startswith("__"):
+            bad = node.name
+        if bad is not None:
+            raise SiteWhereException(f"script {name} line {node.lineno}: access to {bad!r} is not allowed")
 
 
 class ScriptManagement:
@@ -120,13 +162,19 @@ class ScriptManagement:
 
 
 class ScriptRunner:
-    """Compile + run scripts in a restricted namespace on a small pool with a time limit."""
+    """Compile + run scripts in a restricted namespace on a small pool with a time limit; with
+    ``isolation="process"`` the data-only entry points go to the sandboxed worker instead."""
 
-    def __init__(self, threads: int = 3, timeout_s: float = 5.0):
+    def __init__(self, threads: int = 3, timeout_s: float = 5.0, isolation: str | None = None):
+        import os
         self.pool = ThreadPoolExecutor(max_workers=threads, thread_name_prefix="script")
         self.timeout = timeout_s
         self._cache: dict[str, dict] = {}
         self._lock = threading.Lock()
+        self.isolation = isolation or os.environ.get("SITEWHERE_SCRIPT_ISOLATION", "thread")
+        if self.isolation not in ("thread", "process"):
+            raise ValueError(f"script isolation {self.isolation!r}: expected 'thread' or 'process'")
+        self._sandbox = None
 
     def compile(self, source: str, name: str = "<script>", extra_globals: dict | None = None) -> dict:
         key = f"{name}:{hash(source)}"
@@ -136,6 +184,7 @@ class ScriptRunner:
             ns = {"__builtins__": dict(_SAFE_BUILTINS, __import__=_restricted_import), "__name__": name}
             if extra_globals:
                 ns.update(extra_globals)
+            check_source(source, name)
             code = compile(source, name, "exec")
             exec(code, ns)  # noqa: S102 -- restricted builtins, module allow-list
             with self._lock:
@@ -143,6 +192,10 @@ class ScriptRunner:
         return ns
 
     def call(self, source: str, entry: str, *args, name: str = "<script>", extra_globals=None, **kwargs):
+        if self.isolation == "process" and not extra_globals:
+            from .script_sandbox import is_plain
+            if is_plain(args) and is_plain(kwargs):
+                return self.sandbox().call(source, entry, args, kwargs, name=name, timeout_s=self.timeout)
         ns = self.compile(source, name, extra_globals)
         fn = ns.get(entry)
         if not callable(fn):
@@ -153,8 +206,17 @@ class ScriptRunner:
         except FutTimeout as e:
             raise SiteWhereException(f"script {name}.{entry} timed out") from e
 
+    def sandbox(self):
+        with self._lock:
+            if self._sandbox is None:
+                from .script_sandbox import SandboxedScripts
+                self._sandbox = SandboxedScripts()
+            return self._sandbox
+
     def close(self):
         self.pool.shutdown(wait=False)
+        if self._sandbox is not None:
+            self._sandbox.close()
 
 
 SCRIPT_TEMPLATES = {

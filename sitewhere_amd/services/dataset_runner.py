@@ -11,7 +11,8 @@ tenant engine runs the scripts of its section with the builders bound (``device_
 ``geo`` (point-in-polygon helpers).  A script stored in the script manager for the tenant and this
 microservice under ``initializer-<name>`` (any version made active) replaces the packaged one --
 the versioned user initializers of the reference.  Scripts run with the restricted builtins of
-``runtime/scripting.py``, as trusted tenant-administrator code (see that module)."""
+``runtime/scripting.py`` and its source check, in-process, as trusted tenant-administrator code
+(they drive the management APIs directly; see that module's trust model)."""
 from __future__ import annotations
 
 import json
@@ -75,7 +76,7 @@ def _source(engine, script: str, path: str) -> str:
 def run_initializers(engine, section: str, template: str | None, bindings: dict, seed: int = 7) -> int:
     """Run the ``section`` initializers of dataset ``template`` for ``engine``'s tenant; returns how
     many scripts ran."""
-    from ..runtime.scripting import _SAFE_BUILTINS, _restricted_import
+    from ..runtime.scripting import _SAFE_BUILTINS, _restricted_import, check_source
     if not template or template == "empty":
         return 0
     meta = dataset_templates().get(template)
@@ -87,6 +88,8 @@ def run_initializers(engine, section: str, template: str | None, bindings: dict,
         path = os.path.join(DATASET_DIR, template, script)
         ns = {"__builtins__": dict(_SAFE_BUILTINS, __import__=_restricted_import), "__name__": f"initializer:{script}",
               "logger": log, "rnd": random.Random(seed), "params": params(), "geo": _Geo(), **bindings}
-        exec(compile(_source(engine, script, path), path, "exec"), ns)  # noqa: S102 -- restricted builtins
+        src = _source(engine, script, path)
+        check_source(src, path)
+        exec(compile(src, path, "exec"), ns)  # noqa: S102 -- restricted builtins, checked source
         ran += 1
     return ran
