@@ -212,8 +212,31 @@ __global__ void k_scan_lb(const uint32_t* __restrict__ in, int64_t n, uint32_t* 
   }
 }
 
+// One-workgroup exclusive scan for short arrays (tile counters: a few thousand entries): each thread
+// scans a contiguous run.  Cheaper than any multi-workgroup scheme at this size -- the look-back
+// below pays cross-XCD flag latency even for 2 tiles (10-15 us measured against ~5 us here).
+__global__ void k_scan_block(const uint32_t* __restrict__ in, int64_t n, uint32_t* __restrict__ out,
+                             uint32_t* __restrict__ total) {
+  __shared__ uint32_t lds[WAVES + 1];
+  const int64_t per = (n + BLK - 1) / BLK;
+  const int64_t b = (int64_t)threadIdx.x * per;
+  uint32_t s = 0;
+  for (int64_t i = 0; i < per; ++i) if (b + i < n) s += in[b + i];
+  uint32_t tot;
+  uint32_t pre = block_excl_scan(s, &tot, lds);
+  for (int64_t i = 0; i < per; ++i) {
+    if (b + i < n) { const uint32_t t = in[b + i]; out[b + i] = pre; pre += t; }
+  }
+  if (threadIdx.x == 0 && total) *total = tot;
+}
+#define SCAN_BLOCK_MAX (BLK * 64)
+
 static int launch_scan(const uint32_t* in, int64_t n, uint32_t* out, uint32_t* total, uint32_t* tmp,
                        int64_t tmp_len, hipStream_t s) {
+  if (n <= SCAN_BLOCK_MAX) {
+    k_scan_block<<<1, BLK, 0, s>>>(in, n, out, total);
+    return 0;
+  }
   int64_t nt = (n + TILE - 1) / TILE;
   if (nt < 1) nt = 1;
   if (2 * (nt + 2) > tmp_len || ((uintptr_t)tmp & 7)) return -2;     // tmp holds u64[2 + nt]
@@ -304,14 +327,26 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ raw, co
 }
 
 __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
-                                                      int64_t n_msgs, uint32_t* __restrict__ cnt) {
+                                                      int64_t n_msgs, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ tsum) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
   uint32_t base = 0;
   const bool staged = stage_window(raw, off, n_msgs, lds, &base);
+  __shared__ uint32_t red[WAVES + 1];
   const int64_t m = (int64_t)BID * BLK + threadIdx.x;
-  if (m >= n_msgs) return;
-  if (staged) cnt[m] = sw_decode_payload(lds, off[m] - base, off[m + 1] - base, base, 0, 0, nullptr, 0);
-  else cnt[m] = sw_decode_payload(raw, off[m], off[m + 1], 0, 0, 0, nullptr, 0);
+  uint32_t c = 0;
+  if (m < n_msgs) {
+    c = staged ? sw_decode_payload(lds, off[m] - base, off[m + 1] - base, base, 0, 0, nullptr, 0)
+               : sw_decode_payload(raw, off[m], off[m + 1], 0, 0, 0, nullptr, 0);
+    cnt[m] = c;
+  }
+  // per-block record total: the block sums are scanned by one workgroup (k_scan_sums) and
+  // k_decode_emit rebuilds the in-block prefix itself -- reduce-then-scan with no look-back chain
+  // across the 4K blocks of a 1M batch (the single-pass scan serialised on cross-XCD flag polls,
+  // ~350 us per step: profiles/r3_fold)
+  uint32_t tot;
+  block_excl_scan(c, &tot, red);
+  if (threadIdx.x == 0) tsum[BID] = tot;
 }
 
 // First sighting of a name/type hash on this rank: report (hash, offset, len) so the host can read
@@ -347,9 +382,12 @@ __global__ __launch_bounds__(BLK) void k_decode_emit(SwEngineArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
   uint32_t base = 0;
   const bool staged = stage_window(a.raw, a.msg_off, a.n_msgs, lds, &base);
+  __shared__ uint32_t red[WAVES + 1];
   const int64_t m = (int64_t)BID * BLK + threadIdx.x;
+  uint32_t tot;
+  const uint32_t pre = block_excl_scan(m < a.n_msgs ? a.msg_cnt[m] : 0u, &tot, red);
   if (m >= a.n_msgs) return;
-  const int64_t o = a.msg_evoff[m];
+  const int64_t o = (int64_t)a.msg_evoff[BID] + pre;      // msg_evoff holds the scanned block sums
   if (o >= a.rec_cap) return;
   const uint32_t room = (uint32_t)((a.rec_cap - o) < 0xffffffffll ? (a.rec_cap - o) : 0xffffffffll);
   SwEventRec* out = a.recs + o;
@@ -1305,9 +1343,8 @@ int sw_phase_decode(const SwEngineArgs* ap, hipStream_t s) {
     return (int)hipGetLastError();
   }
   const unsigned nb = (unsigned)((a.n_msgs + BLK - 1) / BLK);
-  k_decode_count<<<nb, BLK, 0, s>>>(a.raw, a.msg_off, a.n_msgs, a.msg_cnt);
-  int rc = launch_scan(a.msg_cnt, a.n_msgs, a.msg_evoff, a.n_recs, a.scan_tmp, a.scan_tmp_len, s);
-  if (rc) return rc;
+  k_decode_count<<<nb, BLK, 0, s>>>(a.raw, a.msg_off, a.n_msgs, a.msg_cnt, a.msg_evoff);
+  k_scan_sums<<<1, BLK, 0, s>>>(a.msg_evoff, (int64_t)nb, a.n_recs);
   k_decode_emit<<<nb, BLK, 0, s>>>(a);
   if (a.world > 1) k_decode_end<<<1, 64, 0, s>>>(a);     // world == 1: k_process_begin does it
   return (int)hipGetLastError();

@@ -71,7 +71,7 @@ typedef struct SwEngineArgs {
   int64_t batch_seq;           // step counter of this rank (raw-log addressing)
   // ---------------------------------------------------------------- decode
   uint32_t* msg_cnt;           // [msg_cap]
-  uint32_t* msg_evoff;         // [msg_cap]
+  uint32_t* msg_evoff;         // [msg_cap] decode: scanned per-workgroup record sums
   uint32_t* scan_tmp;          // [scan_tmp_len] block sums
   int64_t scan_tmp_len;
   SwEventRec* recs;            // [rec_cap] decoded records (pre-shuffle)
