@@ -229,7 +229,17 @@ class MicroserviceManagementApi:
     def get_global_configuration(self) -> dict:
         return self._ms.global_configuration()
 
+    def _check(self, doc: dict, scope: str):
+        """Reject a document the service's configuration model does not accept (the reference
+        parses tenant XML against the service schema before applying it)."""
+        m = self._ms.configuration_model()
+        if m is not None and self._ms.multitenant == (scope == "tenant"):
+            errs = m.validate(doc)
+            if errs:
+                raise SiteWhereException(f"invalid {self._ms.identifier} {scope} configuration: " + "; ".join(errs))
+
     def update_global_configuration(self, doc: dict) -> dict:
+        self._check(doc, "global")
         self._ms.instance.coord.put(self._ms.config_path(), dump_document(doc))
         return doc
 
@@ -237,6 +247,7 @@ class MicroserviceManagementApi:
         return self._ms.tenant_configuration(tenant)
 
     def update_tenant_configuration(self, tenant: str, doc: dict) -> dict:
+        self._check(doc, "tenant")
         self._ms.instance.coord.put(self._ms.tenant_config_path(tenant), dump_document(doc))
         return doc
 
@@ -331,7 +342,7 @@ class Microservice(LifecycleComponent):
         return substitute(doc, self.instance.settings.extra)
 
     def configuration_model(self):
-        from .config_models import model_for
+        from ..configuration import model_for
         return model_for(self.identifier)
 
     def tenant_config_path(self, tenant: str) -> str:

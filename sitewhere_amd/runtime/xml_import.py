@@ -412,7 +412,10 @@ def import_tenant_template(directory: str, base: dict | None = None) -> dict:
             merged.update(doc)                 # list-valued sections replace, not merge
             services[svc] = merged
         else:
-            services[svc] = deep_merge(services.get(svc, {}), doc)
+            merged = deep_merge(services.get(svc, {}), doc)
+            if "datastore" in doc:             # a different store type: none of the base store's keys apply
+                merged["datastore"] = doc["datastore"]
+            services[svc] = merged
     return {"name": f"{name} (imported)", "services": services, "warnings": ctx.warnings}
 
 

@@ -356,7 +356,7 @@ def test_buffered_writer_and_influx_lines():
 
 def test_every_microservice_has_a_configuration_model():
     from sitewhere_amd.assembly import SERVICES_BY_ID
-    from sitewhere_amd.runtime.config_models import model_for
+    from sitewhere_amd.configuration import model_for
     from sitewhere_amd.services.tenant_management import TENANT_TEMPLATES
     assert len(SERVICES_BY_ID) == 19
     for ident in SERVICES_BY_ID:
