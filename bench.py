@@ -144,7 +144,10 @@ def main():
                        dedup_slots=1 << 24, name_slots=1 << 12, rank=rank, world=world,
                        # (assignment, name) state map: 16 measurement names + 4 alert types + zone alerts per device
                        state_slots=2 * (16 + 4 + args.zones) * int(args.devices * 1.1),
-                       presence_missing_ms=8 * 3600 * 1000)
+                       presence_missing_ms=8 * 3600 * 1000,
+                       # 4 staging slots: the runner drains two steps behind (SW_PIPELINE_DEPTH) and the
+                       # reject router gets two step periods per batch
+                       extra={"out_buffers": int(os.environ.get("SW_OUT_BUFFERS", 4))})
     if use_gpu:
         from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine, PipelinedRunner
         eng = GpuInboundEngine(cfg, device=torch.device("cuda", local), group=None)
@@ -239,20 +242,25 @@ def main():
         def on_rejects(off, refs, compact):
             # the GPU copied the rejected payloads into `compact`; the router parses only those and
             # writes the reference's Kafka payloads natively (the held record serves overflow refs)
+            t0 = time.perf_counter()
             payload = raw_view(bus.view(t_raw, 0, off))[0]
             rr = routing.route_refs(compact, refs, rank, "bench", route_parts, raw=payload.data_ptr())
+            t1 = time.perf_counter()
             routed["payloads"] += rr.payloads
-            for kind, part, kh, ko, vh, vo in rr.groups():
-                bus.append_arrays(route_topics[kind], max(part, 0), kh, ko, vh, vo)
-                routed["records"] += len(ko) - 1
-                routed["by_kind"][kind] += len(ko) - 1
+            per = bus.append_routed(route_topics, rr)
+            routed["records"] += sum(per)
+            for kind, c in enumerate(per):
+                routed["by_kind"][kind] += c
+            routed["route_s"] = routed.get("route_s", 0.0) + (t1 - t0)
+            routed["publish_s"] = routed.get("publish_s", 0.0) + (time.perf_counter() - t1)
+            routed["jobs"] = routed.get("jobs", 0) + 1
 
         if args.durable:
             tmpdir, store, boot = open_durable(args, rank, dev)
             sink = DurableBlockSink(store, eng.lib, boot, rank=rank, world=world, bus=bus, topic=t_out)
             bus.set_retention(t_out, 64 << 20)
             dur = {"store": store, "sink": sink}
-            runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=False, block_sink=sink,
+            runner = PipelinedRunner(eng, max_raw_bytes=max_raw, deliver_outbound=False, block_sink=sink, nbuf=4,
                                      on_rejects=on_rejects)
         else:
             pub = OutboundPublisher(bus, t_out, eng.lib, eng.out_cap, rank=rank, world=world)
@@ -424,6 +432,9 @@ def main():
                          "rejects_routed_payloads": r1["payloads"] - r0["payloads"],
                          "routed_by_topic": {t.rsplit(".", 1)[-1]: r1["by_kind"][i] - r0["by_kind"][i]
                                              for i, t in enumerate(bus_stats["route_topics"])}}
+        if r1.get("jobs"):
+            detail["bus"]["router_ms_per_job"] = {"route": round(1000 * r1["route_s"] / r1["jobs"], 3),
+                                                  "publish": round(1000 * r1["publish_s"] / r1["jobs"], 3)}
     if use_gpu and getattr(runner, "trace", None) is not None:
         detail["runner_trace_ms_per_step"] = {k: round(1000 * v / (args.steps + args.warmup), 3)
                                               for k, v in runner.trace.items()}

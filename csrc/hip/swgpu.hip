@@ -297,10 +297,28 @@ __global__ void k_vlen_apply(const uint8_t* __restrict__ L, int64_t nbytes, cons
   }
 }
 
-__global__ void k_vlen_total(uint32_t* __restrict__ msg_off, int64_t n_msgs, uint32_t raw_bytes) {
-  if (threadIdx.x == 0 && BID == 0) {
-    if (msg_off[n_msgs] > raw_bytes) msg_off[n_msgs] = raw_bytes;
+// Both tile-sum scans of the framing (message counts, byte lengths) in one workgroup; the byte
+// total, clamped to the batch, is the terminal offset msg_off[n_msgs].
+__global__ void k_vlen_sums(uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tlen, int64_t nt,
+                            uint32_t* __restrict__ msg_off, int64_t n_msgs, uint32_t raw_bytes) {
+  __shared__ uint32_t lds[WAVES + 1];
+  const int64_t per = (nt + BLK - 1) / BLK;
+  const int64_t b = (int64_t)threadIdx.x * per;
+  uint32_t sc = 0, sl = 0;
+  for (int64_t i = 0; i < per; ++i) {
+    if (b + i < nt) { sc += tcnt[b + i]; sl += tlen[b + i]; }
   }
+  uint32_t tc, tl;
+  uint32_t pc = block_excl_scan(sc, &tc, lds);
+  uint32_t pl = block_excl_scan(sl, &tl, lds);
+  for (int64_t i = 0; i < per; ++i) {
+    if (b + i < nt) {
+      const uint32_t c = tcnt[b + i], l = tlen[b + i];
+      tcnt[b + i] = pc; tlen[b + i] = pl;
+      pc += c; pl += l;
+    }
+  }
+  if (threadIdx.x == 0) msg_off[n_msgs] = tl < raw_bytes ? tl : raw_bytes;
 }
 
 // ============================================================================ decode
@@ -569,6 +587,17 @@ __device__ __forceinline__ void intern_insert(ull* __restrict__ key, int32_t* __
 // One probe of the packed registry resolves device AND active assignment; names of every
 // decodable event are interned here too (fused: one pass over the records).
 __global__ void k_lookup(SwEngineArgs a) {
+  // generation rotation decided by k_process_begin: clear the table that becomes `cur` (dedup runs
+  // after this kernel); folded here instead of a dispatch that exits at once on most steps
+  if (a.dd_meta[2]) {
+    const int64_t slots = a.dd_mask + 1;
+    ull* k = (ull*)a.dd_key + a.dd_meta[0] * slots;
+    ull* q = (ull*)a.dd_seq + a.dd_meta[0] * slots;
+    for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK) {
+      k[i] = 0ull;
+      q[i] = ~0ull;
+    }
+  }
   const uint32_t n = *a.n_work;
   const SwEventRec* __restrict__ recs = a.work;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
@@ -621,20 +650,8 @@ __device__ __forceinline__ bool dd_find(const ull* __restrict__ key, int64_t mas
   return false;
 }
 
-// Rotation decision (one thread) at the start of the dedup phase; k_dedup_clear does the clearing.
-// dd_meta = [generation, ids in cur, rotate flag, pad].
-__global__ void k_dedup_clear(ull* __restrict__ key, ull* __restrict__ seq, int64_t slots,
-                              const int64_t* __restrict__ meta) {
-  if (meta[2] == 0) return;
-  const int64_t g = meta[0];
-  ull* k = key + g * slots;
-  ull* q = seq + g * slots;
-  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK) {
-    k[i] = 0ull;
-    q[i] = ~0ull;
-  }
-}
-
+// dd_meta = [generation, ids in cur, rotate flag, pad]: k_process_begin decides the rotation,
+// k_lookup clears the retired generation.
 __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                                uint8_t* __restrict__ status, ull* __restrict__ key, ull* __restrict__ seq,
                                int64_t mask, const int64_t* __restrict__ seq_base, int64_t* __restrict__ meta,
@@ -704,9 +721,11 @@ __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_
 // ============================================================================ compaction
 // Stable split of [0, n) into ok (status == OK) and rejected lists.
 __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
-                            uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles) {
+                            uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles, ull* __restrict__ stats) {
   __shared__ uint32_t c[2];
+  __shared__ uint32_t rs[8];          // rejects by status (the reject counters of the step)
   if (threadIdx.x < 2) c[threadIdx.x] = 0;
+  if (threadIdx.x < 8) rs[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)BID * TILE;
@@ -715,12 +734,22 @@ __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* 
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool v = i < n;
-    ok += __popcll(__ballot(v && status[i] == SW_ST_OK));
+    const uint8_t st = v ? status[i] : (uint8_t)SW_ST_OK;
+    ok += __popcll(__ballot(v && st == SW_ST_OK));
     all += __popcll(__ballot(v));
+    if (st != SW_ST_OK) atomicAdd(&rs[st & 7], 1u);       // rare: ~1% of events
   }
   if (lane_id() == 0) { atomicAdd(&c[0], ok); atomicAdd(&c[1], all - ok); }
   __syncthreads();
   if (threadIdx.x == 0) { tcnt[BID] = c[0]; tcnt[ntiles + BID] = c[1]; }
+  if (threadIdx.x < 8 && rs[threadIdx.x]) {
+    const int slot = threadIdx.x == SW_ST_UNREGISTERED ? SW_STAT_UNREGISTERED
+                   : threadIdx.x == SW_ST_UNASSIGNED ? SW_STAT_UNASSIGNED
+                   : threadIdx.x == SW_ST_DUPLICATE ? SW_STAT_DUPLICATE
+                   : threadIdx.x == SW_ST_DECODE_ERROR ? SW_STAT_DECODE_ERROR
+                   : threadIdx.x == SW_ST_CONTROL ? SW_STAT_CONTROL : -1;
+    if (slot >= 0) atomicAdd(&stats[slot], (ull)rs[threadIdx.x]);
+  }
 }
 
 __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
@@ -768,8 +797,8 @@ __device__ __forceinline__ int64_t nm_probe(const K* __restrict__ key, int64_t m
 
 __global__ void k_intern_insert_list(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                                      ull* __restrict__ key, int32_t* __restrict__ ids, int32_t* __restrict__ counter,
-                                     int64_t mask) {
-  const uint32_t n = *n_ptr;
+                                     int64_t mask, uint32_t cap) {
+  const uint32_t n = *n_ptr < cap ? *n_ptr : cap;
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
     if (recs[j].name_hash) intern_insert(key, ids, counter, mask, recs[j].name_hash);
 }
@@ -797,8 +826,8 @@ __device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t ma
 // the name probe and the state-map probe run once per event instead of once per pass.
 __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                           const int32_t* __restrict__ devs, const int32_t* __restrict__ asgs,
-                          const uint32_t* __restrict__ n_ptr) {
-  const uint32_t n = *n_ptr;
+                          const uint32_t* __restrict__ n_ptr, uint32_t cap) {
+  const uint32_t n = *n_ptr < cap ? *n_ptr : cap;     // generated events: n_gen may pass gen_cap
   const int64_t cur = *a.store_cursor;
   const int64_t c0 = *a.step_cursor0;
   const int64_t now = a.sp->now_ms;
@@ -869,8 +898,8 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
 // ============================================================================ device state
 // Pass 2: among events carrying the max date, the highest event id wins (ids are monotonic).
 // Reads only k_persist's coalesced (slot, date) work items -- no event records, no probes.
-__global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr) {
-  const uint32_t n = *n_ptr;
+__global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, uint32_t cap) {
+  const uint32_t n = *n_ptr < cap ? *n_ptr : cap;
   const int64_t cur = *a.store_cursor;
   const longlong2* __restrict__ work = reinterpret_cast<const longlong2*>(a.ev_slot);
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
@@ -1056,9 +1085,12 @@ __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restri
 
 // Pass 2: write the alerts at their scanned offsets (stable, no global atomics).
 __global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __restrict__ zmask,
-                                                   const uint32_t* __restrict__ zoff) {
+                                                   const uint32_t* __restrict__ zoff, uint32_t* __restrict__ n_rule) {
   __shared__ uint32_t lds[WAVES + 1];
   __shared__ int4 lt[ZONE_LDS_TESTS];
+  // rule alerts of this step = the zone scan total (in n_gen), clamped; every block writes the same
+  // value, before k_presence appends to n_gen (no separate clamp dispatch)
+  if (threadIdx.x == 0) *n_rule = *a.n_gen < a.gen_cap ? *a.n_gen : (uint32_t)a.gen_cap;
   const int nt = a.n_tests < ZONE_LDS_TESTS ? (int)a.n_tests : ZONE_LDS_TESTS;
   for (int t = threadIdx.x; t < nt; t += BLK) {
     const SwZoneTest zt = a.tests[t];
@@ -1170,6 +1202,7 @@ __global__ void k_gen_clamp(SwEngineArgs a, uint32_t* gen_rules) {
 
 __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
   if (threadIdx.x == 0 && BID == 0) {
+    if (*a.n_gen > a.gen_cap) *a.n_gen = (uint32_t)a.gen_cap;   // presence appends past the cap were dropped
     *a.store_cursor += *a.n_gen;                 // the generated events persisted last
     *a.n_out = (uint32_t)(*a.store_cursor - *a.step_cursor0);
     *a.seq_base += *a.n_work;
@@ -1178,24 +1211,6 @@ __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
     st[SW_STAT_PERSISTED] += *a.n_out;
     st[SW_STAT_RULE_ALERTS] += *n_rule_alerts;
     st[SW_STAT_PRESENCE] += *a.n_gen - *n_rule_alerts;
-  }
-}
-
-__global__ void k_reject_stats(SwEngineArgs a) {
-  __shared__ uint32_t c[8];
-  if (threadIdx.x < 8) c[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t n = *a.n_rej;
-  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK)
-    atomicAdd(&c[a.status[a.rej_idx[j]] & 7], 1u);
-  __syncthreads();
-  if (threadIdx.x < 8 && c[threadIdx.x]) {
-    const int slot = threadIdx.x == SW_ST_UNREGISTERED ? SW_STAT_UNREGISTERED
-                   : threadIdx.x == SW_ST_UNASSIGNED ? SW_STAT_UNASSIGNED
-                   : threadIdx.x == SW_ST_DUPLICATE ? SW_STAT_DUPLICATE
-                   : threadIdx.x == SW_ST_DECODE_ERROR ? SW_STAT_DECODE_ERROR
-                   : threadIdx.x == SW_ST_CONTROL ? SW_STAT_CONTROL : -1;
-    if (slot >= 0) atomicAdd((ull*)&a.stats[slot], (ull)c[threadIdx.x]);
   }
 }
 
@@ -1327,10 +1342,8 @@ int sw_frame_varint(const uint8_t* lens, int64_t nbytes, int64_t n_msgs, uint32_
   uint32_t* tcnt = tmp;
   uint32_t* tlen = tmp + nt;
   k_vlen_tiles<<<(unsigned)nt, BLK, 0, s>>>(lens, nbytes, tcnt, tlen);
-  k_scan_sums<<<1, BLK, 0, s>>>(tcnt, nt, nullptr);
-  k_scan_sums<<<1, BLK, 0, s>>>(tlen, nt, msg_off + n_msgs);
+  k_vlen_sums<<<1, BLK, 0, s>>>(tcnt, tlen, nt, msg_off, n_msgs, raw_bytes);
   k_vlen_apply<<<(unsigned)nt, BLK, 0, s>>>(lens, nbytes, tcnt, tlen, msg_off, n_msgs, raw_bytes);
-  k_vlen_total<<<1, 64, 0, s>>>(msg_off, n_msgs, raw_bytes);
   return (int)hipGetLastError();
 }
 
@@ -1387,22 +1400,20 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   if (2 * ntiles > a.scan_tmp_len) return -4;
   k_process_begin<<<1, 64, 0, s>>>(a);
   k_lookup<<<g, BLK, 0, s>>>(a);
-  k_dedup_clear<<<grid_for(a.dd_mask + 1), BLK, 0, s>>>((ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask + 1, a.dd_meta);
   k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base,
                                    a.dd_meta, (ull*)a.stats);
   k_dedup_check<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (const ull*)a.dd_key, (const ull*)a.dd_seq, a.dd_mask,
                                   a.seq_base, a.dd_meta);
   // stable split ok / rejected
-  k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles);
+  k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats);
   uint32_t* cmp_off = a.cmp_tmp + 2 * ntiles;
   int rc = launch_scan(a.cmp_tmp, 2 * ntiles, cmp_off, nullptr, a.scan_tmp, a.scan_tmp_len, s);
   if (rc) return rc;
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, cmp_off, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx,
                                                a.n_ok, a.n_rej);
-  k_reject_stats<<<64, BLK, 0, s>>>(a);
   // persist + enrich + state for the validated events
-  k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok);
-  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok);
+  k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap);
+  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap);
   k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_ok);
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
@@ -1414,15 +1425,17 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
     k_zone_mask<<<(unsigned)otiles, BLK, vtx_bytes, s>>>(a, zmask, ztile);
     rc = launch_scan(ztile, otiles, ztile + otiles, a.n_gen, a.scan_tmp, a.scan_tmp_len, s);
     if (rc) return rc;
-    k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile + otiles);
+    k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile + otiles, n_rule);
+  } else {
+    k_gen_clamp<<<1, 64, 0, s>>>(a, n_rule);        // no zone tests: n_rule = n_gen = 0
   }
-  k_gen_clamp<<<1, 64, 0, s>>>(a, n_rule);
   k_presence<<<grid_for(a.n_asg), BLK, 0, s>>>(a);   // exits at once when presence is off this step
-  k_gen_clamp<<<1, 64, 0, s>>>(a, nullptr);
+  // consumers of the generated events clamp n_gen to gen_cap themselves; k_step_end stores it
   const int gg = grid_for(a.gen_cap);
-  k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask);
-  k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen);
-  k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen);
+  const uint32_t gcap = (uint32_t)a.gen_cap;
+  k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, gcap);
+  k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap);
+  k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen, gcap);
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
 }

@@ -817,6 +817,38 @@ int64_t swlog_append_batch(void* h, int32_t topic, int32_t p, const uint8_t* key
   return first;
 }
 
+// Append routed rejects (pipeline/routing.py) in one call: rec = n x (kind, partition, key length,
+// value length), records grouped by (kind, partition) with keys / values back to back in two heaps;
+// topics[kind] is the topic of each kind.  One swlog_append_batch per group, no per-group trip
+// through Python.  per_kind[4] += records appended per kind.  Returns n, or -1 on a failed append.
+int64_t swlog_append_routed(void* h, const int32_t* topics, const int32_t* rec, int64_t n, const uint8_t* keys,
+                            const uint8_t* vals, int64_t ts, int64_t* per_kind) {
+  std::vector<int64_t> ko, vo, tsv;
+  int64_t i = 0, kpos = 0, vpos = 0;
+  while (i < n) {
+    const int32_t kind = rec[4 * i], part = rec[4 * i + 1];
+    if (kind < 0 || kind > 3) return -1;
+    ko.assign(1, 0);
+    vo.assign(1, 0);
+    int64_t j = i;
+    while (j < n && rec[4 * j] == kind && rec[4 * j + 1] == part) {
+      ko.push_back(ko.back() + rec[4 * j + 2]);
+      vo.push_back(vo.back() + rec[4 * j + 3]);
+      ++j;
+    }
+    const int64_t m = j - i;
+    tsv.assign((size_t)m, ts);
+    if (swlog_append_batch(h, topics[kind], part < 0 ? 0 : part, keys + kpos, ko.data(), vals + vpos, vo.data(),
+                           tsv.data(), m) < 0)
+      return -1;
+    kpos += ko.back();
+    vpos += vo.back();
+    if (per_kind) per_kind[kind] += m;
+    i = j;
+  }
+  return n;
+}
+
 int64_t swlog_append(void* h, int32_t topic, int32_t p, const uint8_t* key, int64_t klen, const uint8_t* val,
                      int64_t vlen, int64_t ts) {
   int64_t ko[2] = {0, klen}, vo[2] = {0, vlen};

@@ -133,6 +133,7 @@ def native():
         _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)
         _proto(lib, "swlog_partitions", c_int32, P, c_int32)
         _proto(lib, "swlog_append_batch", c_int64, P, c_int32, c_int32, P, P, P, P, P, c_int64)
+        _proto(lib, "swlog_append_routed", c_int64, P, P, P, c_int64, P, P, c_int64, P)
         _proto(lib, "swlog_append", c_int64, P, c_int32, c_int32, P, c_int64, P, c_int64, c_int64)
         _proto(lib, "swlog_end_offset", c_int64, P, c_int32, c_int32)
         _proto(lib, "swlog_begin_offset", c_int64, P, c_int32, c_int32)
@@ -214,6 +215,7 @@ def native_gil():
             _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)
             _proto(lib, "swlog_partitions", c_int32, P, c_int32)
             _proto(lib, "swlog_append_batch", c_int64, P, c_int32, c_int32, P, P, P, P, P, c_int64)
+            _proto(lib, "swlog_append_routed", c_int64, P, P, P, c_int64, P, P, c_int64, P)
             _proto(lib, "swlog_append", c_int64, P, c_int32, c_int32, P, c_int64, P, c_int64, c_int64)
             _proto(lib, "swlog_end_offset", c_int64, P, c_int32, c_int32)
             _proto(lib, "swlog_begin_offset", c_int64, P, c_int32, c_int32)

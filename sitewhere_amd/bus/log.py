@@ -464,6 +464,34 @@ class EventBus:
         self._wake(name)
         return first
 
+    def append_routed(self, names, routed, ts: int | None = None) -> list:
+        """Append a router's output (``pipeline.routing.RoutedRejects``: records grouped by (kind,
+        partition), heaps back to back) to ``names[kind]`` in one native call.  Returns the records
+        appended per kind.  Protected topics take the per-group path (producer backpressure)."""
+        n = len(routed)
+        counts = [0, 0, 0, 0]
+        if not n:
+            return counts
+        if any(nm in self._protected for nm in names):
+            for kind, part, kh, ko, vh, vo in routed.groups():
+                self.append_arrays(names[kind], max(part, 0), kh, ko, vh, vo, ts)
+                counts[kind] += len(ko) - 1
+            return counts
+        tids = np.array([self.topic(nm) for nm in names], np.int32)
+        rec = np.ascontiguousarray(routed.rec, np.int32)
+        kb = routed.keys if len(routed.keys) else np.zeros(1, np.uint8)
+        vb = routed.vals if len(routed.vals) else np.zeros(1, np.uint8)
+        per = np.zeros(4, np.int64)
+        fn = self.lib if vb.nbytes >= (1 << 20) else self.fast
+        r = fn.swlog_append_routed(self.h, tids.ctypes.data, rec.ctypes.data, n, kb.ctypes.data, vb.ctypes.data,
+                                   ts if ts is not None else int(time.time() * 1000), per.ctypes.data)
+        if r < 0:
+            raise RuntimeError("append of routed rejects failed")
+        for kind, nm in enumerate(names):
+            if per[kind]:
+                self._wake(nm)
+        return [int(x) for x in per]
+
     def append_many(self, batches, ts: int | None = None):
         """[(topic, partition, [(key, value)])] in one call (a producer's flushed batches)."""
         for name, p, recs in batches:

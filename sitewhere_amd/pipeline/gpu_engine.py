@@ -1191,10 +1191,16 @@ class PipelinedRunner:
         self.on_outbound = on_outbound
         self.k = 0
         self.delivered = 0
-        self.pending = None
+        # steps enqueued but not yet drained.  Draining step k-depth (not k-1) when submitting k
+        # leaves the host a whole extra step of slack: the H2D of the next batch is enqueued while
+        # the copy stream is still busy, so the PCIe-bound copy stream never idles on host jitter.
+        # The multi-GPU exchange keeps depth 1 (its stall decisions read the carry of the last round).
+        from collections import deque
+        self.pending = deque()
         self.copying = None          # sdma mode: (buffer, n_out) whose D2H copy is in flight
         self.rounds = engine.world > 1 and os.environ.get("SW_PIPELINE_EXCHANGE", "1") != "0"
         self.produced = [False] * nb  # rounds mode: did the round in slot b process a batch
+        self.depth = 1 if self.rounds else max(1, min(int(os.environ.get("SW_PIPELINE_DEPTH", 2)), nb - 1))
         self.block_sink = block_sink
         if block_sink is not None:
             if self.mode != "hsa":
@@ -1205,6 +1211,8 @@ class PipelinedRunner:
         self.bcopying = None              # (slot, signal, buffer, bytes, first_seq, now, tag)
         # SW_RUNNER_TRACE=1: host wall-clock per phase (bench attribution)
         self.trace = {} if os.environ.get("SW_RUNNER_TRACE") == "1" else None
+        if self.trace is not None:      # device-side H2D and step time per slot (CUDA events)
+            self.tev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(nb)]
         # on_rejects(tag, refs u32 [n, 4], compact payload bytes): the slow path of each step
         # (see reject_refs_async; refs whose copy offset is ~0 need the raw record named by tag)
         self.on_rejects = on_rejects
@@ -1242,15 +1250,21 @@ class PipelinedRunner:
             with torch.cuda.stream(self.h2d):
                 if k >= self.nbuf:
                     self.h2d.wait_event(self.ev_comp[b])  # compute k-nbuf was the last reader of buffer b
+                if self.trace is not None:
+                    self.tev[b][0].record(self.h2d)
                 self.raw[b][:nbytes].copy_(raw_host, non_blocking=True)
                 if lens_host is not None:
                     self.lens[b][:lens_host.numel()].copy_(lens_host, non_blocking=True)
                 else:
                     self.off[b][:n_msgs + 1].copy_(off_host[:n_msgs + 1], non_blocking=True)
                 self.ev_h2d[b].record(self.h2d)
+                if self.trace is not None:
+                    self.tev[b][1].record(self.h2d)
+        t_sub = self._t("sub_h2d", t_sub)
         if self.mode == "hsa" and ((self.copying is not None and self.copying[0] == b) or
                                    (self.bcopying is not None and self.bcopying[0] == b)):
             self._finish_copy()                           # SDMA copy k-2 still reads staging ring b
+        t_sub = self._t("sub_copy_wait", t_sub)
         if raw_host is not None:
             self.comp.wait_event(self.ev_h2d[b])
             if lens_host is not None:
@@ -1267,6 +1281,7 @@ class PipelinedRunner:
             self.e.step_async(self.raw[b], self.off[b], n_msgs, now_ms, presence=presence, out_sel=b,
                               out_to_device=to_dev)
             self.produced[b] = True
+        t_sub = self._t("sub_step", t_sub)
         if self.mode == "push":
             if not self.produced[b]:
                 self.nout[b].zero_()
@@ -1283,6 +1298,7 @@ class PipelinedRunner:
             if self.produced[b] and done is not None:
                 if self.rej_job[b] is not None:
                     self.rej_job[b].result()           # the router is done with slot b's host buffer
+                t_sub = self._t("sub_router_wait", t_sub)
                 rej_cnt, _ = self.e.reject_refs_async(b, self.raw[done[0]], self.off[done[0]], done[1])
                 self.rtag[b] = done[2]
         if self.block_sink is not None:
@@ -1302,6 +1318,8 @@ class PipelinedRunner:
         if rc:
             raise RuntimeError(f"sw_step_snapshot failed ({rc})")
         self.ev_comp[b].record(self.comp)
+        if self.trace is not None:
+            self.tev[b][2].record(self.comp)
         if self.mode == "push" and self.deliver:
             with torch.cuda.stream(self.push):
                 self.push.wait_event(self.ev_comp[b])
@@ -1313,8 +1331,9 @@ class PipelinedRunner:
                     raise RuntimeError(f"sw_push_out failed ({rc})")
                 self.ev_push[b].record(self.push)
         self._t("enqueue", t_sub)
-        self._drain()
-        self.pending = b
+        self.pending.append(b)
+        while len(self.pending) > self.depth:
+            self._drain()
         self.k += 1
 
     def _rejects_async(self, pb: int, n_rej: int, n_bytes: int):
@@ -1386,12 +1405,17 @@ class PipelinedRunner:
         return t0
 
     def _drain(self):
-        if self.pending is None:
+        if not self.pending:
             return
-        pb = self.pending
+        pb = self.pending.popleft()
         t0 = time.perf_counter()
         self.ev_comp[pb].synchronize()
         t0 = self._t("wait_step", t0)
+        if self.trace is not None and self.produced[pb]:
+            ev = self.tev[pb]
+            self.trace["gpu_h2d"] = self.trace.get("gpu_h2d", 0.0) + ev[0].elapsed_time(ev[1]) / 1000
+            self.trace["gpu_h2d_to_step_end"] = self.trace.get("gpu_h2d_to_step_end", 0.0) + \
+                ev[1].elapsed_time(ev[2]) / 1000
         if self.mode == "push" and self.deliver:
             self.ev_push[pb].synchronize()
         snap = self.snap[pb].view(np.uint32, 32)
@@ -1399,7 +1423,6 @@ class PipelinedRunner:
         if self.e.world > 1:
             # re-key carry after this round: the parity its partition spilled into
             self.e._carry_seen = int(snap[22 + self.cpar[pb]])
-        self.pending = None
         if self.on_rejects is not None and self.produced[pb] and self.rtag[pb] is not None:
             n_rej = int(snap[24])
             if n_rej:
@@ -1454,7 +1477,8 @@ class PipelinedRunner:
     def flush(self):
         if self.rounds and self.e.exchange_pending:
             self.submit(None, None, 0)                    # last round: process the batch in flight
-        self._drain()
+        while self.pending:
+            self._drain()
         self._finish_copy()
         self.comp.synchronize()
         self.push.synchronize()

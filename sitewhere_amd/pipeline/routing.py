@@ -59,7 +59,9 @@ class RoutedRejects:
 def _call(fn, args_head: tuple, n_rej: int) -> RoutedRejects:
     need = np.zeros(3, np.int64)
     npay = np.zeros(1, np.int64)
-    cap = (max(16, 4 * n_rej), max(1024, 64 * n_rej), max(4096, 256 * n_rej))
+    # generous first guess (np.empty does not touch the pages): a too-small heap makes the native
+    # router do all its work twice (a payload with several measurements routes to several records)
+    cap = (max(16, 8 * n_rej), max(1024, 160 * n_rej), max(4096, 1024 * n_rej))
     for _ in range(2):
         rec = np.empty((cap[0], 4), np.int32)         # the first n rows are written
         keys = np.empty(cap[1], np.uint8)

@@ -103,3 +103,34 @@ def test_route_throughput():
     dt = time.perf_counter() - t
     assert rr.payloads == 5000 and len(rr) >= 5000
     assert dt < 0.05, dt
+
+
+def test_append_routed_matches_per_group_appends():
+    """``EventBus.append_routed`` (one native call) writes exactly what the per-group appends do."""
+    from sitewhere_amd.bus.log import EventBus
+    from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
+    spec = FleetSpec(n_devices=5000, with_alternate_id=True, p_unregistered=0.05)
+    raw, offs = gen_payloads(spec, 20000, 1_700_000_000_000, seed=5)
+    raw = np.concatenate([raw, np.zeros(64, np.uint8)])
+    pick = np.sort(np.random.default_rng(1).choice(len(offs) - 1, 800, replace=False))
+    st = np.where(np.arange(len(pick)) % 7 == 0, ST_CONTROL, ST_UNREG).astype(np.uint8)
+    rr = routing.route_rejects(raw, offs, offs[pick], st, "s", (4, 2, 3, 1))
+    names = ("unreg", "reg", "decoded", "failed")
+    a, b = EventBus(default_partitions=4), EventBus(default_partitions=4)
+    for bus in (a, b):
+        for nm, n in zip(names, (4, 2, 3, 1)):
+            bus.topic(nm, n)
+    per = a.append_routed(names, rr, ts=7)
+    want = [0, 0, 0, 0]
+    for kind, part, kh, ko, vh, vo in rr.groups():
+        b.append_arrays(names[kind], max(part, 0), kh, ko, vh, vo, ts=7)
+        want[kind] += len(ko) - 1
+    assert per == want and sum(per) == len(rr)
+    total = 0
+    for nm, n in zip(names, (4, 2, 3, 1)):
+        for p in range(n):
+            ra = [(r.key, bytes(r.value)) for r in a.read(nm, p, 0, 1 << 20)]
+            rb = [(r.key, bytes(r.value)) for r in b.read(nm, p, 0, 1 << 20)]
+            assert ra == rb, (nm, p)
+            total += len(ra)
+    assert total == len(rr) > 700
