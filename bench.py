@@ -272,14 +272,17 @@ def main():
         from concurrent.futures import ThreadPoolExecutor
 
         from sitewhere_amd.pipeline.bus_io import VALUE_HDR
-        from sitewhere_amd.pipeline.fleet import stamp_alt_epoch
+        from sitewhere_amd.pipeline.fleet import alt_positions, stamp_positions
         producer = ThreadPoolExecutor(1, thread_name_prefix="producer") if args.alt_ids else None
         stamps = {}
+        # where each batch's alternate-id epochs sit, found once: stamping then only writes
+        alt_pos = [alt_positions(rec.ptr + VALUE_HDR, b[3]) for rec, b in zip(records, batches)] \
+            if args.alt_ids else None
 
         def stamp(k):
             rec = records[k % len(records)]
-            return stamp_alt_epoch(rec.ptr + VALUE_HDR, batches[k % len(batches)][3],
-                                   (0x5717 << 48) | (rank << 32) | k, threads=6)
+            return stamp_positions(rec.ptr + VALUE_HDR, alt_pos[k % len(records)],
+                                   (0x5717 << 48) | (rank << 32) | k, threads=int(os.environ.get("SW_STAMP_THREADS", 4)))
 
         if producer is not None:
             stamps[0] = producer.submit(stamp, 0)

@@ -128,6 +128,8 @@ def native():
                c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, P, c_int64, P)
         _proto(lib, "sw_gen_tokens", c_int64, c_char_p, c_int64, c_int64, P, c_int64, P)
         _proto(lib, "sw_stamp_alt_epoch", c_int64, P, P, c_int64, c_uint64, c_int32)
+        _proto(lib, "sw_alt_positions", c_int64, P, P, c_int64, P)
+        _proto(lib, "sw_stamp_positions", c_int64, P, P, c_int64, c_uint64, c_int32)
         _proto(lib, "swlog_open", P, c_char_p, c_int32)
         _proto(lib, "swlog_close", None, P)
         _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)

@@ -175,6 +175,22 @@ def stamp_alt_epoch(raw, offs: np.ndarray, epoch: int, threads: int = 8) -> int:
                                            int(threads)))
 
 
+def alt_positions(raw, offs: np.ndarray) -> np.ndarray:
+    """Positions of the alternate-id epochs of a generated batch (``stamp_positions``); -1: none."""
+    offs = np.ascontiguousarray(offs, np.uint32)
+    pos = np.empty(len(offs) - 1, np.int64)
+    ptr = raw if isinstance(raw, int) else raw.ctypes.data
+    native().sw_alt_positions(ptr, offs.ctypes.data, len(offs) - 1, pos.ctypes.data)
+    return pos
+
+
+def stamp_positions(raw, pos: np.ndarray, epoch: int, threads: int = 4) -> int:
+    """``stamp_alt_epoch`` at precomputed positions with streaming stores (no reads of the batch)."""
+    ptr = raw if isinstance(raw, int) else raw.ctypes.data
+    return int(native().sw_stamp_positions(ptr, pos.ctypes.data, len(pos), int(epoch) & (2 ** 64 - 1),
+                                           int(threads)))
+
+
 def pack_messages(messages):
     """Concatenate a list of payload byte strings into (raw, offs)."""
     offs = np.zeros(len(messages) + 1, np.uint32)

@@ -1213,6 +1213,7 @@ class PipelinedRunner:
         self.trace = {} if os.environ.get("SW_RUNNER_TRACE") == "1" else None
         if self.trace is not None:      # device-side H2D and step time per slot (CUDA events)
             self.tev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(nb)]
+            self.tev_on = [False] * nb
         # on_rejects(tag, refs u32 [n, 4], compact payload bytes): the slow path of each step
         # (see reject_refs_async; refs whose copy offset is ~0 need the raw record named by tag)
         self.on_rejects = on_rejects
@@ -1320,6 +1321,7 @@ class PipelinedRunner:
         self.ev_comp[b].record(self.comp)
         if self.trace is not None:
             self.tev[b][2].record(self.comp)
+            self.tev_on[b] = raw_host is not None
         if self.mode == "push" and self.deliver:
             with torch.cuda.stream(self.push):
                 self.push.wait_event(self.ev_comp[b])
@@ -1411,8 +1413,9 @@ class PipelinedRunner:
         t0 = time.perf_counter()
         self.ev_comp[pb].synchronize()
         t0 = self._t("wait_step", t0)
-        if self.trace is not None and self.produced[pb]:
+        if self.trace is not None and self.tev_on[pb]:
             ev = self.tev[pb]
+            ev[2].synchronize()                 # recorded just after ev_comp: may complete a moment later
             self.trace["gpu_h2d"] = self.trace.get("gpu_h2d", 0.0) + ev[0].elapsed_time(ev[1]) / 1000
             self.trace["gpu_h2d_to_step_end"] = self.trace.get("gpu_h2d_to_step_end", 0.0) + \
                 ev[1].elapsed_time(ev[2]) / 1000

@@ -134,3 +134,18 @@ def test_append_routed_matches_per_group_appends():
             assert ra == rb, (nm, p)
             total += len(ra)
     assert total == len(rr) > 700
+
+
+def test_positional_stamping_matches_checked_stamping():
+    """The bench producer's streaming-store stamp (positions found once) writes exactly what the
+    checked in-place stamp writes."""
+    from sitewhere_amd.pipeline.fleet import FleetSpec, alt_positions, gen_payloads, stamp_alt_epoch, stamp_positions
+    spec = FleetSpec(n_devices=1000, with_alternate_id=True, p_unregistered=0.01)
+    raw, offs = gen_payloads(spec, 5000, 1_700_000_000_000, seed=9)
+    a, b = raw.copy(), raw.copy()
+    pos = alt_positions(a, offs)
+    assert (pos >= 0).sum() > 4000
+    for epoch in (7, 0x5717_0000_0000_0042):
+        assert stamp_alt_epoch(a, offs, epoch, threads=3) == stamp_positions(b, pos, epoch, threads=3)
+        assert np.array_equal(a, b)
+    assert not np.array_equal(a, raw)
