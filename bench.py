@@ -128,6 +128,11 @@ def main():
 
     use_gpu = args.engine == "gpu"
     rank, local, world, _ = init_distributed(use_gpu)
+    numa_node = None
+    if use_gpu and os.environ.get("SW_NUMA_BIND", "1") != "0":
+        # host threads and pinned buffers next to this GPU's PCIe root (before anything is allocated)
+        from sitewhere_amd.utils.numa import bind_to_gpu_node
+        numa_node = bind_to_gpu_node(local)
     from sitewhere_amd.pipeline.config import EngineConfig
     from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads, gen_tokens, fingerprints
     from sitewhere_amd.pipeline.framing import varint_lengths
@@ -416,6 +421,7 @@ def main():
         "registered_devices_rank0": n_dev,
         "rejected_rank0": {k: s1[k] - s0[k] for k in ("unregistered", "unassigned", "duplicates", "decode_errors",
                                                        "control")},
+        "numa_node": numa_node,
         "backend": dist.get_backend() if world > 1 else None,
         "world": dist.get_world_size() if world > 1 else 1,
         "rank_elapsed_s": per_rank if per_rank is not None else [round(rank_elapsed, 6)],

@@ -156,14 +156,26 @@ class EventSourcesProvider(ModelProvider):
             Attr("username", "String", "SASL PLAIN user", group="auth"),
             Attr("password", "String", "SASL PLAIN password", group="auth")], icon="sign-in-alt"))
         e(Element("Azure EventHub Event Source", "event-receiver", ("eventhub", "azure-eventhub"),
-                  "Consume an Event Hub.", [
+                  "Consume every partition of an Event Hub over AMQP 1.0 (EventProcessorHost: partition leases "
+                  "balanced over hosts, offsets checkpointed per consumer group), or over its Kafka endpoint.", [
+                      Attr("protocol", "String", "amqp (SAS key) | kafka (connection string)", default="amqp",
+                           choices=("amqp", "kafka"), group="conn"),
                       Attr("namespace", "String", "Event Hubs namespace", group="conn"),
-                      Attr("bootstrap", "String", "host:port (default <namespace>.servicebus.windows.net:9093)",
+                      Attr("host", "String", "endpoint host (default <namespace>.servicebus.windows.net)",
+                           group="conn"),
+                      Attr("port", "Integer", "AMQP port", default=5671, group="conn"),
+                      Attr("bootstrap", "String", "kafka: host:port (default <namespace>.servicebus.windows.net:9093)",
                            group="conn"),
                       Attr("eventHub", "String", "event hub name", required=True, group="conn"),
-                      Attr("connectionString", "String", "namespace connection string", required=True, group="auth"),
                       Attr("consumerGroup", "String", "consumer group", default="$Default", group="conn"),
-                      Attr("tls", "Boolean", "TLS", default=True, group="auth")], icon="cloud"))
+                      Attr("sasKeyName", "String", "amqp: shared access key name", group="auth"),
+                      Attr("sasKey", "String", "amqp: shared access key", group="auth"),
+                      Attr("connectionString", "String", "kafka: namespace connection string", group="auth"),
+                      Attr("tls", "Boolean", "TLS", default=True, group="auth"),
+                      Attr("hostNamePrefix", "String", "prefix of this host's lease owner name", default="sitewhere"),
+                      Attr("partitionCount", "Integer", "partitions (default: asked from $management)"),
+                      Attr("checkpointEvery", "Integer", "events between partition checkpoints", default=100,
+                           group="perf")], icon="cloud"))
 
 
 class InboundProcessingProvider(ModelProvider):

@@ -915,5 +915,12 @@ def build_receiver(rc: dict, scripts=None) -> Receiver:
         return KafkaReceiver(rc.get("bootstrap", "127.0.0.1:9092"), rc["topic"], rc.get("group", "sitewhere"),
                              bool(rc.get("tls", False)), sasl)
     if t in ("eventhub", "azure-eventhub"):
-        return event_hub_receiver(rc)
+        # AMQP 1.0 (the reference's EventProcessorHost path) unless the Kafka endpoint is asked for
+        if rc.get("protocol") == "kafka" or (rc.get("connectionString") and not rc.get("sasKeyName")):
+            return event_hub_receiver(rc)
+        from .eventhub import EventHubAmqpReceiver
+        return EventHubAmqpReceiver(rc.get("namespace"), rc["eventHub"], rc["sasKeyName"], rc["sasKey"],
+                                    rc.get("consumerGroup", "$Default"), rc.get("host"), int(rc.get("port", 5671)),
+                                    bool(rc.get("tls", True)), rc.get("hostNamePrefix", "sitewhere"),
+                                    rc.get("partitionCount"), checkpoint_every=int(rc.get("checkpointEvery", 100)))
     raise ValueError(f"unknown receiver type {t!r}")
