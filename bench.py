@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--msgs", type=int, default=1 << 20, help="payloads per GPU per step")
     ap.add_argument("--devices", type=int, default=1 << 20, help="registered devices per GPU")
     ap.add_argument("--mx-per-msg", type=int, default=1)
-    ap.add_argument("--batches", type=int, default=4, help="distinct pre-generated batches to cycle")
+    ap.add_argument("--batches", type=int, default=6, help="distinct pre-generated batches to cycle")
     ap.add_argument("--zones", type=int, default=16)
     ap.add_argument("--store", type=int, default=1 << 27, help="HBM event-store capacity per GPU (events)")
     ap.add_argument("--engine", choices=["gpu", "cpu", "oracle"], default="gpu",
@@ -278,7 +278,12 @@ def main():
 
         from sitewhere_amd.pipeline.bus_io import VALUE_HDR
         from sitewhere_amd.pipeline.fleet import alt_positions, stamp_positions
-        producer = ThreadPoolExecutor(1, thread_name_prefix="producer") if args.alt_ids else None
+        # the producer stamps batch k+AHEAD while k is published: two stamps in flight, each on
+        # several threads, so generating fresh ids never paces the pipeline; a batch is re-stamped
+        # only once every step that read its record (H2D, compute, reject routing) is long done
+        AHEAD = 2
+        assert not args.alt_ids or len(batches) >= AHEAD + 4, "the producer lookahead needs >= 6 distinct batches"
+        producer = ThreadPoolExecutor(AHEAD, thread_name_prefix="producer") if args.alt_ids else None
         stamps = {}
         # where each batch's alternate-id epochs sit, found once: stamping then only writes
         alt_pos = [alt_positions(rec.ptr + VALUE_HDR, b[3]) for rec, b in zip(records, batches)] \
@@ -287,10 +292,11 @@ def main():
         def stamp(k):
             rec = records[k % len(records)]
             return stamp_positions(rec.ptr + VALUE_HDR, alt_pos[k % len(records)],
-                                   (0x5717 << 48) | (rank << 32) | k, threads=int(os.environ.get("SW_STAMP_THREADS", 4)))
+                                   (0x5717 << 48) | (rank << 32) | k, threads=int(os.environ.get("SW_STAMP_THREADS", 8)))
 
         if producer is not None:
-            stamps[0] = producer.submit(stamp, 0)
+            for j in range(AHEAD):
+                stamps[j] = producer.submit(stamp, j)
         cursor = {"next": bus.end_offset(t_raw, 0), "committed": bus.end_offset(t_raw, 0)}
         inflight = deque()
         bus_stats = {"bus": bus, "t_raw": t_raw, "group": group, "cursor": cursor, "routed": routed,
@@ -317,7 +323,7 @@ def main():
                 stamps.pop(k).result()                        # batch k's fresh alternate ids
             records[k % len(records)].publish(bus, t_raw, 0, ts=now0 + k)     # producer: batch k arrives
             if producer is not None:
-                stamps[k + 1] = producer.submit(stamp, k + 1)
+                stamps[k + AHEAD] = producer.submit(stamp, k + AHEAD)
             off = cursor["next"]
             cursor["next"] = off + 1
             # the consumer holds every record not yet committed: H2D in flight, rejects to route,
