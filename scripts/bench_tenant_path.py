@@ -51,6 +51,12 @@ def main():
     from sitewhere_amd.assembly import SiteWhereInstance
     from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
 
+    numa_node = None
+    if os.environ.get("SW_NUMA_BIND", "1") != "0":
+        import torch
+        if torch.cuda.is_available():   # the instance's threads and pinned pools next to the GPU
+            from sitewhere_amd.utils.numa import bind_to_gpu_node
+            numa_node = bind_to_gpu_node(0)
     sw = SiteWhereInstance().start()
     sw.wait_for_tenant("default", 60)
     tm = sw.api("TenantManagement")
@@ -198,6 +204,7 @@ def main():
                       "routed_payloads": ib.routed_payloads, "unregistered": ib.unregistered.count,
                       "raw_records_lost": getattr(ib.raw_consumer.consumer, "lost", None),
                       "backpressure_waits": getattr(sw.instance.bus, "backpressure_waits", None),
+                      "numa_node": numa_node,
                       "store_retention_rows": getattr(em_store, "retention_rows", None),
                       "store_evicted_rows": getattr(em_store, "evicted_rows", None), "setup_s": round(setup_s, 1),
                       "mean_ms": breakdown, **({"median_ms_second_half": trace} if trace else {})}))

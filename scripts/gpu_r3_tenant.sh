@@ -9,7 +9,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   tail -3 "$O/pytest.log"
   [ $rc -eq 0 ] || exit $rc
 fi
-for B in 262144 1048576; do
+for B in ${SIZES:-65536 262144 1048576}; do
   for P in 0 0.01; do
     SW_FRAMED_TRACE=1 SW_TENANT_TRACE=1 timeout -k 10 400 python -u scripts/bench_tenant_path.py --devices 50000 --batch $B --batches 30 --warmup 4 \
       --via-bus --max-msgs $B --p-unregistered $P > "$O/tenant_${B}_${P}.log" 2>&1 || { tail -20 "$O/tenant_${B}_${P}.log"; exit 1; }
