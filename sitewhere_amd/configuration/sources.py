@@ -214,6 +214,8 @@ class InboundProcessingProvider(ModelProvider):
                  group="perf"),
             Attr("zeroCopyRows", "Boolean", "columnar payloads framed in place around the engine's pinned rows",
                  default=False, group="perf"),
+            Attr("coalesceRaw", "Boolean", "step raw records already waiting in a partition together (up to "
+                 "the engine's batch capacity; overlapped steps)", default=True, group="perf"),
             Attr("retainHostAllocations", "Boolean", "keep pinned host pools between steps", default=True,
                  group="perf"),
             Attr("tuneGc", "Boolean", "freeze the start-up heap out of the cyclic GC", default=False, group="perf"),

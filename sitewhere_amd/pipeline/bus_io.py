@@ -158,6 +158,72 @@ class RawBatch:
         return RawBatch(self.n_msgs, self.payload_bytes, np.array(self.payload), None, self.offsets().copy())
 
 
+class _SegView:
+    """Byte slicing across the parts of a :class:`MultiRawBatch` (names are read from the payload
+    bytes by offset; a name never spans two payloads, so never two parts)."""
+    __slots__ = ("parts", "starts")
+
+    def __init__(self, parts, starts):
+        self.parts, self.starts = parts, starts
+
+    def __getitem__(self, sl):
+        a, b = sl.start, sl.stop
+        k = int(np.searchsorted(self.starts, a, side="right")) - 1
+        base = int(self.starts[k])
+        return bytes(self.parts[k].payload[a - base:b - base])
+
+
+class MultiRawBatch:
+    """Consecutive raw batches of one partition stepped as one (the raw consumer coalesces records
+    that are already waiting, so small micro-batches share one engine step's fixed cost).  The GPU
+    engine DMAs each part's payload and varint lengths back to back (``parts``); host engines and
+    the slow path see the concatenation (``payload`` is materialised on first use)."""
+
+    def __init__(self, parts: list):
+        self.parts = list(parts)
+        self.n_msgs = sum(b.n_msgs for b in self.parts)
+        self.payload_bytes = sum(b.payload_bytes for b in self.parts)
+        self.starts = np.cumsum([0] + [b.payload_bytes for b in self.parts[:-1]]).astype(np.int64)
+        self.msg_starts = np.cumsum([0] + [b.n_msgs for b in self.parts[:-1]]).astype(np.int64)
+        self.lens = np.concatenate([np.asarray(b.lens, np.uint8) for b in self.parts]) \
+            if all(b.lens is not None for b in self.parts) else None
+        self._payload = None
+        self._offs = None
+
+    @property
+    def payload(self) -> np.ndarray:
+        if self._payload is None:
+            out = np.zeros(self.payload_bytes + _PAD, np.uint8)
+            for b, st in zip(self.parts, self.starts):
+                out[st:st + b.payload_bytes] = np.asarray(b.payload)[:b.payload_bytes]
+            self._payload = out
+        return self._payload
+
+    def host_view(self):
+        return _SegView(self.parts, self.starts)
+
+    def offsets(self) -> np.ndarray:
+        if self._offs is None:
+            offs = np.empty(self.n_msgs + 1, np.uint32)
+            for b, st, ms in zip(self.parts, self.starts, self.msg_starts):
+                offs[ms:ms + b.n_msgs + 1] = b.offsets() + np.uint32(st)
+            self._offs = offs
+        return self._offs
+
+    def validate(self):
+        for b in self.parts:
+            b.validate()
+
+    def copy(self) -> "MultiRawBatch":
+        return MultiRawBatch([b.copy() for b in self.parts])
+
+
+def host_view(batch):
+    """What name lookups slice: the payload array, or a segmented view of a coalesced batch."""
+    hv = getattr(batch, "host_view", None)
+    return hv() if hv is not None else np.asarray(batch.payload)
+
+
 def parse_raw_batch(value) -> RawBatch:
     """A raw-payload record value: the framed ``SWRB`` form, or the legacy ``u32 n, u32 lengths[n],
     bytes`` form (records written by older event sources / remote producers)."""

@@ -25,6 +25,7 @@ from .._native import gpu as gpu_lib
 from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE, WIRE_REC
 from ..ops.engine_abi import SwEngineArgs
 from .config import EngineConfig
+from .bus_io import host_view
 from .engine_base import EngineBase, StepResult
 
 _ALIGN = 64
@@ -714,7 +715,9 @@ class GpuInboundEngine(EngineBase):
         if batch.lens is None or self.world > 1:
             return EngineBase.submit_framed(self, batch, now_ms, token, presence)
         import warnings
-        n, nb, nl = batch.n_msgs, len(batch.payload), len(batch.lens)
+        parts = getattr(batch, "parts", None)          # coalesced records: DMA'd back to back
+        n, nl = batch.n_msgs, len(batch.lens)
+        nb = batch.payload_bytes + _ALIGN if parts is not None else len(batch.payload)
         if n > self.cfg.max_msgs:
             raise ValueError(f"batch of {n} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
         if nb < batch.payload_bytes + _ALIGN:
@@ -731,16 +734,30 @@ class GpuInboundEngine(EngineBase):
                 fp = self._fp = _FramedSlots(self)
             b = fp.k % _FramedSlots.SLOTS
             dev_r, dev_l, dev_o = fp.buffers(b, nb, nl)
+            segs = []                                      # (device offset, host payload, payload bytes)
             with warnings.catch_warnings():       # read-only topic views: torch only reads them here
                 warnings.simplefilter("ignore", UserWarning)
-                pt = torch.frombuffer(batch.payload, dtype=torch.uint8) if nb else None
-                lt = torch.frombuffer(batch.lens, dtype=torch.uint8) if nl else None
+                if parts is None:
+                    pt = torch.frombuffer(batch.payload, dtype=torch.uint8) if nb else None
+                    lsegs = [torch.frombuffer(batch.lens, dtype=torch.uint8)] if nl else []
+                    if pt is not None:
+                        segs.append((0, pt, nb))
+                else:
+                    for part, st in zip(parts, batch.starts):
+                        if part.payload_bytes:
+                            segs.append((int(st), torch.frombuffer(part.payload, dtype=torch.uint8),
+                                         part.payload_bytes))
+                    lsegs = [torch.frombuffer(part.lens, dtype=torch.uint8) for part in parts if len(part.lens)]
             with torch.cuda.stream(fp.h2d):
                 fp.h2d.wait_event(fp.ev_comp[b])           # step k-3 was the last reader of slot b
-                if pt is not None:
-                    dev_r[:nb].copy_(pt, non_blocking=True)
-                if lt is not None:
-                    dev_l[:nl].copy_(lt, non_blocking=True)
+                for st, t, m in segs:
+                    dev_r[st:st + m].copy_(t[:m], non_blocking=True)
+                if parts is not None:                      # the records' zero padding, after the last part
+                    dev_r[batch.payload_bytes:batch.payload_bytes + _ALIGN].zero_()
+                lo = 0
+                for t in lsegs:
+                    dev_l[lo:lo + t.numel()].copy_(t, non_blocking=True)
+                    lo += t.numel()
                 fp.ev_h2d[b].record(fp.h2d)
             t0 = self._ft("h2d_enqueue", t0)
             while len(fp.inflight) > 1 or (fp.inflight and fp.inflight[0].rows is not None):
@@ -750,7 +767,7 @@ class GpuInboundEngine(EngineBase):
             if prev is not None:                                             # batch k-1
                 fp.ev_comp[prev.slot].synchronize()
                 t0 = self._ft("wait_k1", t0)
-                prev.small = self._collect_small(np.asarray(prev.batch.payload))
+                prev.small = self._collect_small(host_view(prev.batch))
                 t0 = self._ft("collect_k1", t0)
                 self._block_meta(prev)              # before batch k is queued: no wait on it
                 t0 = self._ft("block_meta_k1", t0)
@@ -791,7 +808,7 @@ class GpuInboundEngine(EngineBase):
                 s = fp.inflight.popleft()
                 if s.small is None:
                     fp.ev_comp[s.slot].synchronize()
-                    s.small = self._collect_small(np.asarray(s.batch.payload))
+                    s.small = self._collect_small(host_view(s.batch))
                     self._block_meta(s)
                     self._framed_rows_start(s)
                 done.append(self._framed_finish(s))

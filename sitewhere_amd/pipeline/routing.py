@@ -56,6 +56,17 @@ class RoutedRejects:
             yield bytes(self.keys[koff[i]:koff[i + 1]]), bytes(self.vals[voff[i]:voff[i + 1]])
 
 
+def concat(parts: list) -> RoutedRejects:
+    """Routed rejects of several records, in record order (each record's groups stay contiguous,
+    so per-key order holds)."""
+    if not parts:
+        return RoutedRejects(np.zeros((0, 4), np.int32), np.zeros(0, np.uint8), np.zeros(0, np.uint8), 0)
+    if len(parts) == 1:
+        return parts[0]
+    return RoutedRejects(np.concatenate([p.rec for p in parts]), np.concatenate([p.keys for p in parts]),
+                         np.concatenate([p.vals for p in parts]), sum(p.payloads for p in parts))
+
+
 def _call(fn, args_head: tuple, n_rej: int) -> RoutedRejects:
     need = np.zeros(3, np.int64)
     npay = np.zeros(1, np.int64)

@@ -35,7 +35,7 @@ from ..models.domain import (AlertLevel, AlertSource, DeviceAlert, DeviceAssignm
                              DeviceMeasurement, DeviceStateChange, now_ms)
 from ..pipeline.config import EngineConfig
 from ..pipeline.engine_base import Zone, ZoneTest
-from ..pipeline.bus_io import RawBatch, parse_raw_batch
+from ..pipeline.bus_io import MultiRawBatch, RawBatch, parse_raw_batch
 from ..pipeline.fleet import fingerprint_str, pack_messages
 from ..rpc import codec
 from ..utils import IndexMap, retain_large_allocations, tune_gc_for_streaming
@@ -58,10 +58,13 @@ class _Stepped:
     """A raw batch the engine has stepped, with the storage stages it has completed.  The raw bytes
     are not kept: rejected messages are routed (``_route``) as soon as the step completes."""
     __slots__ = ("key", "res", "now", "batch", "stored", "published", "routed", "queued", "payload", "events",
-                 "detach", "hold", "commit", "trace", "routed_recs", "token")
+                 "detach", "hold", "commit", "trace", "routed_recs", "token", "first")
 
-    def __init__(self, key, res, now, batch):
+    def __init__(self, key, res, now, batch, first=None):
         self.key, self.res, self.now, self.batch = key, res, now, batch
+        # key = (topic, partition, offset) of the batch's last raw record; first = offset of its first
+        # (records coalesced into one step, see _process_raw)
+        self.first = first if first is not None or key is None else key[2]
         self.stored = self.published = self.routed = self.queued = False
         self.payload = self.events = None
         self.detach, self.hold, self.commit = False, None, None
@@ -151,6 +154,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # submitted batch's record stays readable through a retention hold of this engine until its
         # result is back; the pipeline is drained whenever the raw topic has nothing more queued.
         self.overlap = bool(cfg.get("overlapSteps", self.async_store and self.engine_kind == "gpu"))
+        # step raw records that are already waiting in one partition together (overlapped steps only)
+        self.coalesce = bool(cfg.get("coalesceRaw", True))
         self._order_lock = threading.Lock()    # engine submit/drain + completion hand-off, in step order
         self._holds: dict[tuple, dict] = {}    # (topic, partition) -> {offset: in-flight batches}
         self._hold_lock = threading.Lock()      # the consumer and the reject router both release holds
@@ -373,44 +378,85 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         return True
 
     # ---------------------------------------------------------------- data plane
+    COALESCE_MAX_RECORDS = 16
+
     def _process_raw(self, recs):
+        """Step the raw records of one poll.  Records of one partition that are already waiting are
+        coalesced into one engine step (up to the engine's batch capacity): under load, small
+        micro-batches then share one step's fixed cost; an idle partition still steps each record as
+        it arrives (the event sources' latency bound holds)."""
+        group = []                                      # [(record, parsed batch)] of one partition, consecutive
+        resubmitted = set()
+
+        def flush():
+            if not group:
+                return
+            first_r, last_r = group[0][0], group[-1][0]
+            view = isinstance(first_r.value, memoryview)
+            batch = group[0][1] if len(group) == 1 else MultiRawBatch([b for _, b in group])
+            commit = (last_r.topic, last_r.partition, last_r.offset + 1) \
+                if self.async_store and not self.ckpt_path else None
+            self.process_raw_batch(batch, now=last_r.timestamp or None, commit=commit,
+                                   key=(last_r.topic, last_r.partition, last_r.offset), detach=view,
+                                   hold=(first_r.topic, first_r.partition, first_r.offset) if view else None,
+                                   first=first_r.offset)
+            if self.ckpt_path:
+                for r, _ in group:
+                    self._ckpt_offsets[(r.topic, r.partition)] = r.offset + 1
+                    self._since_ckpt += 1
+                if self._since_ckpt >= self.ckpt_every:
+                    self.checkpoint()
+            group.clear()
+
         for r in recs:
             tp = (r.topic, r.partition)
             self._raise_store_error()                   # before any new step, never after
             if r.offset < self._stored_hw.get(tp, -1):
                 continue                                # fully stored on an earlier read
             key = (r.topic, r.partition, r.offset)
-            commit = (r.topic, r.partition, r.offset + 1) if self.async_store and not self.ckpt_path else None
             item = self._stepped.get(key)
-            if item is not None and item.res is None:   # still in the engine: complete it first
-                self._drain_engine()
-            if item is None:
-                # r.value is a zero-copy view of the topic on the in-process bus: a pinned raw-batch
-                # record is DMA'd to the MI355X in place.  The record timestamp is the batch's receive
-                # time, so replay after a restore is deterministic.
-                view = isinstance(r.value, memoryview)
-                try:
-                    batch = parse_raw_batch(r.value)
-                    batch.validate()
-                    if batch.n_msgs > self.engine_cfg.max_msgs:
-                        raise ValueError(f"raw batch of {batch.n_msgs} payloads exceeds the engine's "
-                                         f"max_msgs={self.engine_cfg.max_msgs}")
-                except ValueError as e:
-                    # never stepped, so nothing to keep: a poison record is dead-lettered, not retried
-                    # forever (the unlimited retries below are only for stepped-but-unstored batches)
-                    batch = None
-                    self._dead_letter_raw(r, e, commit)
-                if batch is not None:
-                    self.process_raw_batch(batch, now=r.timestamp or None, commit=commit, key=key, detach=view,
-                                           hold=(r.topic, r.partition, r.offset) if view else None)
-            else:
+            if item is not None:
+                flush()
+                if id(item) in resubmitted:
+                    continue                            # a later record of a group already resubmitted
+                resubmitted.add(id(item))
+                if item.res is None:                    # still in the engine: complete it first
+                    self._drain_engine()
                 self.replayed_batches += 1
-                self._submit(item, commit)
-            if self.ckpt_path:
-                self._ckpt_offsets[tp] = r.offset + 1
-                self._since_ckpt += 1
-                if self._since_ckpt >= self.ckpt_every:
-                    self.checkpoint()
+                t, p, o = item.key
+                self._submit(item, (t, p, o + 1) if self.async_store and not self.ckpt_path else None)
+                if self.ckpt_path:
+                    self._ckpt_offsets[tp] = o + 1
+                continue
+            # r.value is a zero-copy view of the topic on the in-process bus: a pinned raw-batch
+            # record is DMA'd to the MI355X in place.  The record timestamp is the batch's receive
+            # time, so replay after a restore is deterministic.
+            try:
+                batch = parse_raw_batch(r.value)
+                batch.validate()
+                if batch.n_msgs > self.engine_cfg.max_msgs:
+                    raise ValueError(f"raw batch of {batch.n_msgs} payloads exceeds the engine's "
+                                     f"max_msgs={self.engine_cfg.max_msgs}")
+            except ValueError as e:
+                # never stepped, so nothing to keep: a poison record is dead-lettered, not retried
+                # forever (the unlimited retries below are only for stepped-but-unstored batches)
+                flush()
+                self._dead_letter_raw(r, e, (r.topic, r.partition, r.offset + 1)
+                                      if self.async_store and not self.ckpt_path else None)
+                if self.ckpt_path:
+                    self._ckpt_offsets[tp] = r.offset + 1
+                continue
+            if group:
+                g0, gl = group[0][0], group[-1][0]
+                fits = (self.coalesce and self.overlap and batch.lens is not None
+                        and all(b.lens is not None for _, b in group)
+                        and (r.topic, r.partition) == (g0.topic, g0.partition) and r.offset == gl.offset + 1
+                        and len(group) < self.COALESCE_MAX_RECORDS
+                        and sum(b.n_msgs for _, b in group) + batch.n_msgs <= self.engine_cfg.max_msgs)
+                if not fits:
+                    flush()
+            group.append((r, batch))
+        flush()
         if recs and self.engine.framed_pending:
             last = recs[-1]
             end = getattr(self.ms.instance.bus, "end_offset", None)
@@ -509,7 +555,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                                           key, overlap=False)
 
     def process_raw_batch(self, batch: RawBatch, now: int | None = None, commit=None, key=None, detach=False,
-                          hold=None, overlap: bool | None = None):
+                          hold=None, overlap: bool | None = None, first: int | None = None):
         """One engine step; storing its rows happens here or, with ``asyncStore``, on the store thread
         while the next step runs (call :meth:`flush` to wait for it).  ``key`` = (topic, partition,
         offset) of the raw record: the result is then kept until stored (see ``_stepped``).
@@ -519,12 +565,13 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         ``hold`` = (topic, partition, offset) keeps its record retained until then."""
         now = now or now_ms()
         if self.overlap if overlap is None else overlap:
-            item = _Stepped(key, None, now, batch)
+            item = _Stepped(key, None, now, batch, first)
             item.detach, item.commit = detach, commit
             if self.trace is not None:
                 item.trace = [time.perf_counter()]
             if key is not None:
-                self._stepped[key] = item
+                for off in range(item.first, key[2] + 1):
+                    self._stepped[(key[0], key[1], off)] = item
             with self._order_lock:
                 if hold is not None:
                     item.hold = hold
@@ -541,10 +588,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             res = self.engine.step_framed(batch, now)
         self.processed_events.mark(res.n_events)
         self._ensure_block(res, now)
-        item = _Stepped(key, res, now, None)
+        item = _Stepped(key, res, now, None, first)
         item.routed_recs = self._route(batch, res)
         if key is not None:
-            self._stepped[key] = item
+            for off in range(item.first, key[2] + 1):
+                self._stepped[(key[0], key[1], off)] = item
         self._submit(item, commit)
         return res
 
@@ -675,7 +723,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         tr = item.trace
         if item.key is not None:
             t, p, o = item.key
-            self._stepped.pop(item.key, None)
+            for off in range(item.first, o + 1):
+                self._stepped.pop((t, p, off), None)
             self._stored_hw[(t, p)] = max(self._stored_hw.get((t, p), -1), o + 1)
         if commit is not None:
             self.ms.instance.bus.commit(self.raw_consumer.group, *commit)
@@ -877,8 +926,17 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         bus = self.ms.instance.bus
         topics = (self.t_unregistered, self.t_registration, self.t_decoded, self.t_failed_decode)
         parts = [bus.partitions(t) if hasattr(bus, "partitions") else 1 for t in topics]
-        rr = routing.route_rejects(np.asarray(batch.payload), batch.offsets(), res.rejects["aux_off"], st,
-                                   "gpu-inbound", parts)
+        aux = res.rejects["aux_off"]
+        if getattr(batch, "parts", None) is None:
+            rr = routing.route_rejects(np.asarray(batch.payload), batch.offsets(), aux, st, "gpu-inbound", parts)
+        else:                           # coalesced records: route each record's rejects from its own bytes
+            rrs = []
+            for part, base in zip(batch.parts, batch.starts):
+                m = (aux >= base) & (aux < base + part.payload_bytes)
+                if m.any():
+                    rrs.append(routing.route_rejects(np.asarray(part.payload), part.offsets(),
+                                                     (aux[m] - base).astype(np.uint32), st[m], "gpu-inbound", parts))
+            rr = routing.concat(rrs)
         self.routed_payloads += rr.payloads
         return rr
 

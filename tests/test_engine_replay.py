@@ -199,3 +199,45 @@ def test_durable_wait_failure_rewinds_without_loss_or_duplicates(inst):
     res = _values(inst, run, "rpd", dev)
     assert sorted(m.value for m in res) == sorted(float(100 * b + i) for b in range(6) for i in range(20))
     assert not ib._stepped and not ib._durable_wait
+
+
+def test_waiting_records_coalesce_into_one_step_and_store_once(inst):
+    """Framed raw records already waiting in a partition are stepped together (``coalesceRaw``): one
+    engine step for several records, the rejects of each routed from its own bytes, and -- with the
+    first store of the coalesced batch failing -- a rewind to its first record that stores every
+    event exactly once and commits every offset."""
+    from sitewhere_amd.pipeline.bus_io import RawBatchRecord
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    ib, run, dev = _tenant(inst, "rpk", "gpu-columnar")
+    ib.overlap = True
+    bus = inst.instance.bus
+    store = inst.tenant_engine("event-management", "rpk").store
+    topic = inst.instance.naming.tenant_prefix("rpk") + RAW_PAYLOADS
+    unreg = bus.consumer("rpk-unreg", [inst.instance.naming.unregistered_device_events("rpk")])
+    ingest = "add_batch" if hasattr(store, "add_batch") else "add_columnar"
+    values, batch_values = [], []
+    for b in range(8):
+        msgs = [wire.measurements("galaxytab-001", {"v": float(100 * b + i)}, event_date=1_700_000_500_000 + 100 * b + i,
+                                  alternate_id=f"ck-{b}-{i}") for i in range(25)] + \
+               [wire.measurements(f"newcomer-{b}", {"v": 1.0})]
+        values += [float(100 * b + i) for i in range(25)]
+        raw, offs = pack_messages(msgs)
+        rec = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1, pinned=False)
+        batch_values.append(rec.value())
+    steps0 = ib.step_timer.count
+    with FaultInjector() as fi:
+        fi.fail_next(store, ingest, 1)
+        # all eight records in one append: the consumer finds them waiting together
+        bus.append(topic, 0, [(None, v) for v in batch_values], ts=1_700_000_600_000)
+        assert wait_until(lambda: store.rows == 200, 30), store.rows
+        assert fi.injected[(ingest, "fail")] == 1
+    assert wait_until(lambda: bus.committed(ib.raw_consumer.group, topic, 0) == bus.end_offset(topic, 0))
+    assert ib.step_timer.count - steps0 < 8                    # coalesced: fewer steps than records
+    assert ib.engine.stats_dict()["persisted"] == 200           # each record stepped exactly once
+    assert not ib._stepped and not ib.engine.framed_pending
+    res = _values(inst, run, "rpk", dev)
+    assert sorted(m.value for m in res) == sorted(values) and len({m.id for m in res}) == 200
+    seen = []
+    assert wait_until(lambda: seen.extend(r.key for rs in unreg.poll(50).values() for r in rs) or len(seen) >= 8)
+    assert sorted(seen) == sorted(f"newcomer-{b}".encode() for b in range(8))
