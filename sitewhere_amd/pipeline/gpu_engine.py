@@ -96,8 +96,11 @@ class _FramedSlots:
         cur = self.bufs[b]
         if cur is None or cur[0].numel() < nb or cur[1].numel() < nl:
             self.ev_comp[b].synchronize()           # the old slot buffers may still be read
+            # grow geometrically: coalesced steps vary in size, and a reallocation per new maximum
+            # (device memory + a sync) would land in the middle of a burst
+            grow = 2 * cur[0].numel() if cur is not None else 0
             cur = self.bufs[b] = (
-                torch.empty(max(nb, int(getattr(e, "_stg_hint", 0))), dtype=torch.uint8, device=e.device),
+                torch.empty(max(nb, grow, int(getattr(e, "_stg_hint", 0))), dtype=torch.uint8, device=e.device),
                 torch.empty(max(nl, 5 * e.cfg.max_msgs + 64), dtype=torch.uint8, device=e.device),
                 torch.empty(e.cfg.max_msgs + 1, dtype=torch.int32, device=e.device))
         return cur
@@ -634,6 +637,10 @@ class GpuInboundEngine(EngineBase):
             from ..persistence.segments import max_block_bytes
             full = max_block_bytes(self.out_cap) + self.ROW_HEADROOM
         size = max(need, min(full, -(-(need + need // 4) // (1 << 20)) * (1 << 20)))
+        # never smaller than the largest pooled buffer: steps of a tenant that coalesces records vary
+        # in size, and pinning a fresh buffer for each new maximum costs milliseconds per step
+        if pool:
+            size = max(size, min(full, max(a.nbytes for _, a in pool)))
         # results held by an overlapped tenant: in flight + store queue + storing, and -- with zero-copy
         # columnar payloads -- the batches the store and the enriched-batch topic retain
         if len(pool) < (self.PIN_POOL if kind == "rows" else self.PIN_POOL_BLOCKS):
