@@ -301,6 +301,10 @@ class Microservice(LifecycleComponent):
         self._reporter: MetricsReporter | None = None
         self.log_handler: BusLogHandler | None = None
         self.scripts = ScriptRunner()
+        if self.scripts.isolation == "process":
+            # start the sandboxed worker now, before any tenant engine initialises a GPU in this
+            # process (a process that has opened the GPU should not fork + exec children)
+            self.scripts.sandbox().ensure_started()
         self.management = MicroserviceManagementApi(self)
         self.config: dict = {}
         self._demuxes: dict[str, ApiDemux] = {}

@@ -12,7 +12,9 @@ and routers, connector filters -- to this worker instead.  The worker
 
 then serves length-prefixed msgpack requests on stdin/stdout.  Scripts are compiled with the same
 restricted builtins and source check as in-process ones and cached per (name, source).  A call
-that outlives its time limit kills the worker; the next call starts a fresh one.
+that outlives its time limit kills the worker; the next call starts a fresh one.  Microservices
+start the worker when they are created (``ensure_started``), before a tenant engine opens a GPU in
+the process: a replacement after a timeout is forked from a process that may have opened one.
 """
 from __future__ import annotations
 
@@ -78,6 +80,11 @@ class SandboxedScripts:
         self._lock = threading.Lock()
         self.mode = None
         self.restarts = 0
+
+    def ensure_started(self):
+        with self._lock:
+            if self._p is None or self._p.poll() is not None:
+                self._start()
 
     def _start(self):
         import msgpack
