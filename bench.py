@@ -389,7 +389,8 @@ def main():
     barrier()
     s0 = eng.stats_dict()
     d0 = dur["store"].seg.stats() if dur else None
-    sk0 = (dur["sink"].bytes, dur["sink"].rows, dur["sink"].blocks) if dur else None
+    sk0 = (dur["sink"].bytes, dur["sink"].rows, dur["sink"].blocks, getattr(dur["sink"], "disk_wait_s", 0.0)) \
+        if dur else None
     r0 = dict(bus_stats["routed"], by_kind=list(bus_stats["routed"]["by_kind"])) if bus_stats else None
     barrier()
     t_start = time.perf_counter()
@@ -464,6 +465,9 @@ def main():
             "disk_bytes_written": d1["bytes_written"] - d0["bytes_written"],
             "fdatasyncs": d1["syncs"] - d0["syncs"], "direct_io": bool(d1["direct_io"]),
             "retention_deleted_bytes": d1["deleted_bytes"], "all_durable": sk.store.durable() >= sk.store.seg.last_token,
+            # time the pipeline waited for the disk (block buffers all queued, not yet durable):
+            # > 0 means this rank's step was storage-bound, e.g. several ranks sharing one disk
+            "disk_wait_ms_per_step": round(1000 * (getattr(sk, "disk_wait_s", 0.0) - sk0[3]) / args.steps, 3),
         }
     if rank == 0:
         out = {

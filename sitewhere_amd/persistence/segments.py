@@ -339,6 +339,7 @@ class DurableBlockSink:
         self.tags: list[tuple[int, object]] = []      # (store token, caller tag), in order
         self.n_alloc = 0
         self.blocks = self.bytes = self.rows = 0
+        self.disk_wait_s = 0.0                        # time target() waited for the disk (backpressure)
         self._size = 0
         self._lock = threading.Lock()
         if bus is not None and topic is not None:
@@ -396,10 +397,12 @@ class DurableBlockSink:
                 raise RuntimeError(f"durable block buffers exhausted ({self.n_alloc} allocated, {len(self.pending)} "
                                    f"waiting for the disk, durable token {self.store.seg.durable()} of "
                                    f"{self.store.seg.last_token}, store {self.store.seg.stats()})")
+            t0 = _time.monotonic()
             if self.pending:
                 self.store.seg.wait(self.pending[0].token, 1.0)
             else:
                 _time.sleep(0.001)              # only the topic holds buffers: wait for its retention
+            self.disk_wait_s += _time.monotonic() - t0
 
     def publish(self, b: _BlockBuf, nbytes: int, first_seq: int, now_ms: int, tag=None) -> int:
         """The block is in ``b``: zero its padding, seal it, queue it to the store, publish it."""
