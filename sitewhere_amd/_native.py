@@ -27,7 +27,7 @@ CSRC = ROOT / "csrc"
 GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
 
 _NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp", CSRC / "native" / "swseg.cpp",
-               CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp"]
+               CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp", CSRC / "native" / "swjson.cpp"]
 _GPU_SRC = [CSRC / "hip" / "swgpu.hip", CSRC / "hip" / "swseg.hip"]
 _HEADERS = sorted((CSRC / "include").glob("*.h"))
 
@@ -130,6 +130,8 @@ def native():
         _proto(lib, "sw_stamp_alt_epoch", c_int64, P, P, c_int64, c_uint64, c_int32)
         _proto(lib, "sw_alt_positions", c_int64, P, P, c_int64, P)
         _proto(lib, "sw_stamp_positions", c_int64, P, P, c_int64, c_uint64, c_int32)
+        _proto(lib, "sw_json_to_pb", c_int64, P, c_int64, P, c_int64)
+        _proto(lib, "sw_json_to_pb_batch", c_int64, P, P, c_int64, P, c_int64, P, P)
         _proto(lib, "swlog_open", P, c_char_p, c_int32)
         _proto(lib, "swlog_close", None, P)
         _proto(lib, "swlog_topic", c_int32, P, c_char_p, c_int32)

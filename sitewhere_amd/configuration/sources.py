@@ -53,7 +53,8 @@ class EventSourcesProvider(ModelProvider):
             icon="sign-in-alt"))
         e(Element("Event Source", "event-source", (), "One decoder, an optional deduplicator and its receivers.", [
             Attr("id", "String", "unique source id", required=True, index=True),
-            Attr("forward", "String", "'raw' forwards undecoded payload batches to the MI355X inbound engine",
+            Attr("forward", "String", "'raw' forwards undecoded payload batches to the MI355X inbound engine "
+                 "(JSON device requests are transcoded to protobuf natively; the rest keep the per-event path)",
                  choices=("raw",), group="engn"),
             Attr("logPayloads", "Boolean", "log every payload", default=False),
             Attr("script", "Script", "decoder script when decoder is 'script' (shorthand)", group="scrp")],

@@ -271,6 +271,7 @@ class InboundEventSource(TenantEngineLifecycleComponent):
         self.receivers = list(receivers)
         self.manager = manager
         self.forward_raw = forward_raw
+        self.transcoded = 0                   # JSON payloads forwarded to the engine as protobuf
         for r in self.receivers:
             r.source = self
 
@@ -292,9 +293,18 @@ class InboundEventSource(TenantEngineLifecycleComponent):
 
     def on_encoded_event_received(self, receiver, payload: bytes, metadata: dict) -> int:
         if self.forward_raw:
-            self.manager.handle_raw_payload(self.source_id, payload,
-                                            getattr(self.tenant_engine, "raw_batch", 4096))
-            return 1
+            raw = payload
+            if isinstance(self.decoder, JsonDeviceRequestDecoder):
+                # JSON devices join the fused engine path as the protobuf payloads they are
+                # equivalent to; a request the engine path cannot represent exactly (metadata,
+                # registrations, ...) or an invalid one keeps the per-event path below
+                from ..pipeline.json_transcode import to_protobuf
+                raw = to_protobuf(payload)
+                if raw is not None:
+                    self.transcoded += 1
+            if raw is not None:
+                self.manager.handle_raw_payload(self.source_id, raw, getattr(self.tenant_engine, "raw_batch", 4096))
+                return 1
         try:
             reqs = self.decoder.decode(payload, metadata)
         except Exception as e:

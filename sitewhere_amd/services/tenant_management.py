@@ -98,6 +98,8 @@ TENANT_TEMPLATES["gpu"]["services"]["inbound-processing"] = {"engine": "gpu", "b
                                                              "storage": "objects", "publishEnriched": "events"}
 # protobuf payloads go to the engine undecoded, in micro-batches; JSON keeps the per-event path
 TENANT_TEMPLATES["gpu"]["services"]["event-sources"]["sources"][1]["forward"] = "raw"
+# JSON device requests reach the engine too, transcoded natively to the protobuf payloads they equal
+TENANT_TEMPLATES["gpu"]["services"]["event-sources"]["sources"][0]["forward"] = "raw"
 TENANT_TEMPLATES["gpu"]["services"]["event-sources"].update(rawBatchSize=65536, rawMaxDelayMs=5)
 # High-throughput MI355X tenant: enriched rows stay columnar end to end (no per-event host objects).
 TENANT_TEMPLATES["gpu-columnar"] = copy.deepcopy(TENANT_TEMPLATES["gpu"])

@@ -352,7 +352,9 @@ def test_columnar_tenant_end_to_end():
 
 def test_gpu_template_routes_protobuf_raw_and_json_per_event():
     """gpu template: protobuf payloads reach the fused engine as raw micro-batches (size- or
-    time-flushed); JSON payloads keep the per-event inbound path.  Both end up persisted."""
+    time-flushed); JSON measurements join them transcoded to protobuf (``pipeline/json_transcode``),
+    while a JSON request the engine path cannot represent (metadata) keeps the per-event path.
+    All end up persisted."""
     import json as _json
     inst = SiteWhereInstance().start()
     try:
@@ -373,13 +375,20 @@ def test_gpu_template_routes_protobuf_raw_and_json_per_event():
             es.inject("default-protobuf", wire.measurements("iphone6s-001", {"pb": float(i)}))
         es.inject("default-json", _json.dumps({"deviceToken": "iphone6s-001", "type": "DeviceMeasurement",
                                                "request": {"name": "js", "value": 9.0}}).encode())
+        es.inject("default-json", _json.dumps({"deviceToken": "iphone6s-001", "type": "DeviceMeasurement",
+                                               "request": {"name": "jm", "value": 3.0,
+                                                           "metadata": {"unit": "C"}}}).encode())
 
         def names():
             res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
                                                              {"pageSize": 0})).results
             return sorted(m.name for m in res)
-        assert wait_until(lambda: names() == ["js"] + ["pb"] * 7, 20), names()
-        assert ib.engine.stats_dict()["events"] >= 7
+        assert wait_until(lambda: names() == ["jm", "js"] + ["pb"] * 7, 20), names()
+        assert ib.engine.stats_dict()["events"] >= 8               # 7 protobuf + the transcoded JSON
+        assert es.manager.sources["default-json"].transcoded == 1
+        res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
+                                                         {"pageSize": 0})).results
+        assert next(m for m in res if m.name == "jm").metadata == {"unit": "C"}   # per-event path kept it
     finally:
         inst.stop()
 
