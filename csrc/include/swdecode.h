@@ -21,7 +21,44 @@ SW_HD void sw_fill_control(SwEventRec* r, uint8_t etype, uint32_t abs_start, uin
   r->etype = etype; r->flags = 0; r->src_rank = src_rank; r->level = 0;
 }
 
+// Read a field tag.  False on truncation and on tags protobuf refuses: field number 0 or a
+// key past 32 bits.
+SW_HD bool sw_read_tag(const uint8_t* buf, uint32_t* pos, uint32_t end, uint32_t* f, uint32_t* wt) {
+  uint64_t key;
+  if (!sw_read_varint(buf, pos, end, &key) || key > 0xffffffffull || (key >> 3) == 0) return false;
+  *f = (uint32_t)(key >> 3);
+  *wt = (uint32_t)(key & 7);
+  return true;
+}
+
+// One embedded {required string 1; required <wt2> 2} message at the cursor (Model.Measurement with
+// wt2 = fixed64, Model.Metadata with wt2 = length-delimited): well-formed and both required fields
+// present, else protobuf-java's parseDelimitedFrom refuses the enclosing payload
+// (ProtobufDeviceEventDecoder.java:79-95).  Advances the cursor past it.
+SW_HD bool sw_check_pair(const uint8_t* buf, uint32_t* pos, uint32_t end, uint32_t wt2) {
+  uint64_t len;
+  if (!sw_read_varint(buf, pos, end, &len) || len > (uint64_t)(end - *pos)) return false;
+  uint32_t p = *pos;
+  const uint32_t e = p + (uint32_t)len;
+  bool h1 = false, h2 = false;
+  while (p < e) {
+    uint32_t f, wt;
+    if (!sw_read_tag(buf, &p, e, &f, &wt) || !sw_skip_field(buf, &p, e, wt)) return false;
+    h1 |= f == 1 && wt == 2;
+    h2 |= f == 2 && wt == wt2;
+  }
+  *pos = e;
+  return h1 && h2;
+}
+
 // Decode one payload [start, end).  If `out` is null only counts records.
+//
+// Validity follows protobuf-java on the reference schema (proto2, `required` fields): a payload
+// is a decode error when it is malformed, when the header has no known command, or when an event
+// body misses a required field (hardwareId; latitude/longitude; alertType/alertMessage; the
+// measurementId/measurementValue and Metadata name/value of every embedded entry).  Control bodies
+// only need their hardwareId here: the host decodes those payloads in full.  Deprecated groups
+// (wire types 3/4, unused by the schema) are refused.  Independent oracle: tests/decode_oracle.py.
 // Returns the number of records produced (never more than max_out when out != null;
 // a message whose expansion does not fit is reported as one decode error).
 SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t end, uint32_t abs_base,
@@ -33,12 +70,15 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
   if (ok) {
     uint32_t hend = pos + (uint32_t)hlen;
     while (ok && pos < hend) {
-      uint64_t key;
-      ok = sw_read_varint(buf, &pos, hend, &key);
+      uint32_t f, wt;
+      ok = sw_read_tag(buf, &pos, hend, &f, &wt);
       if (!ok) break;
-      uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
-      if (f == 1 && wt == 0) ok = sw_read_varint(buf, &pos, hend, &cmd);
-      else ok = sw_skip_field(buf, &pos, hend, wt);
+      if (f == 1 && wt == 0) {
+        ok = sw_read_varint(buf, &pos, hend, &v);
+        if (v >= 1 && v <= 8) cmd = v;  // an unknown enum value is an unknown field (proto2)
+      } else {
+        ok = sw_skip_field(buf, &pos, hend, wt);
+      }
     }
     ok = ok && sw_read_varint(buf, &pos, end, &blen) && blen <= (uint64_t)(end - pos);
   }
@@ -51,16 +91,16 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
   // ---- pass over body: common fields
   uint64_t lo = 0, hi = 0, alt = 0, date = 0;
   bool has_dev = false, has_date = false, has_us = false, us = false, has_elev = false;
+  bool req_a = false, req_b = false;  // latitude/longitude | alertType/alertMessage
   uint32_t n_mx = 0;
   double lat = 0, lon = 0, elev = 0;
   // alert type / message; offsets default to the payload start so every record points into its payload
   uint32_t t_off = start, t_len = 0, m_off = start, m_len = 0;
   pos = bstart;
   while (ok && pos < bend) {
-    uint64_t key;
-    ok = sw_read_varint(buf, &pos, bend, &key);
+    uint32_t f, wt;
+    ok = sw_read_tag(buf, &pos, bend, &f, &wt);
     if (!ok) break;
-    uint32_t f = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
     if (f == 1 && wt == 2) {  // hardwareId in every body message
       ok = sw_read_varint(buf, &pos, bend, &v) && v <= (uint64_t)(bend - pos);
       if (!ok) break;
@@ -80,8 +120,9 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
     }
     switch (cmd) {
       case SW_CMD_SEND_DEVICE_MEASUREMENTS:
-        if (f == 2 && wt == 2) { n_mx++; ok = sw_skip_field(buf, &pos, bend, wt); }
+        if (f == 2 && wt == 2) { n_mx++; ok = sw_check_pair(buf, &pos, bend, 1); }
         else if (f == 3 && wt == 1) { if (pos + 8 > bend) { ok = false; break; } date = sw_load_le64(buf + pos); pos += 8; has_date = true; }
+        else if (f == 4 && wt == 2) ok = sw_check_pair(buf, &pos, bend, 2);
         else if (f == 5 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
         else ok = sw_skip_field(buf, &pos, bend, wt);
         break;
@@ -91,18 +132,21 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
           uint64_t bits = sw_load_le64(buf + pos); pos += 8;
           double d;
           __builtin_memcpy(&d, &bits, 8);
-          if (f == 2) lat = d; else if (f == 3) lon = d; else if (f == 4) { elev = d; has_elev = true; }
+          if (f == 2) { lat = d; req_a = true; } else if (f == 3) { lon = d; req_b = true; }
+          else if (f == 4) { elev = d; has_elev = true; }
           else { date = bits; has_date = true; }
-        } else if (f == 7 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
+        } else if (f == 6 && wt == 2) ok = sw_check_pair(buf, &pos, bend, 2);
+        else if (f == 7 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
         else ok = sw_skip_field(buf, &pos, bend, wt);
         break;
       case SW_CMD_SEND_DEVICE_ALERT:
         if ((f == 2 || f == 3) && wt == 2) {
           ok = sw_read_varint(buf, &pos, bend, &v) && v <= (uint64_t)(bend - pos);
           if (!ok) break;
-          if (f == 2) { t_off = pos; t_len = (uint32_t)v; } else { m_off = pos; m_len = (uint32_t)v; }
+          if (f == 2) { t_off = pos; t_len = (uint32_t)v; req_a = true; } else { m_off = pos; m_len = (uint32_t)v; req_b = true; }
           pos += (uint32_t)v;
         } else if (f == 4 && wt == 1) { if (pos + 8 > bend) { ok = false; break; } date = sw_load_le64(buf + pos); pos += 8; has_date = true; }
+        else if (f == 5 && wt == 2) ok = sw_check_pair(buf, &pos, bend, 2);
         else if (f == 6 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
         else ok = sw_skip_field(buf, &pos, bend, wt);
         break;
@@ -111,6 +155,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
         break;
     }
   }
+  if ((cmd == SW_CMD_SEND_DEVICE_LOCATION || cmd == SW_CMD_SEND_DEVICE_ALERT) && !(req_a && req_b)) ok = false;
   if (!ok || !has_dev) {
     if (out && max_out) sw_fill_control(out, SW_EV_DECODE_ERROR, abs_base + start, abs_base + end, 0, 0, now_ms, src_rank);
     return 1;

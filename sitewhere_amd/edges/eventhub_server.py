@@ -125,9 +125,10 @@ class EventHubServer:
             p, _, _ = self._read_frame(s)
             mech, resp = str(p.value[0]), p.value[1] or b""
             ok = mech == "PLAIN" and resp.split(b"\x00")[1:] == [x.encode() for x in self.sas]
+            if not ok:  # counted before the outcome goes out, so a refused client sees it
+                self.auth_failures += 1
             send(perf(SASL_OUTCOME, [UByte(0 if ok else 1)]), ftype=1)
             if not ok:
-                self.auth_failures += 1
                 return
             if self._read_exact(s, 8) != AMQP_HEADER:
                 return

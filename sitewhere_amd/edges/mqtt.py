@@ -570,11 +570,13 @@ class MqttBroker:
             c.settimeout(keepalive * 1.5 if keepalive else None)
             with sess.wlock:
                 pending = [(pid, ent[0], ent[1]) for pid, ent in sess.out.items()]
+                queued = list(sess.queue)
+                sess.queue.clear()
             for pid, stage, pkt in pending:                 # retransmit what the client never acked
                 self._send(sess, c, packet(PUBREL, 2, struct.pack("!H", pid)) if stage == "pubcomp"
                            else bytes([pkt[0] | 0x08]) + pkt[1:])
-            while sess.queue:
-                self._deliver(sess, *sess.queue.popleft())
+            for q in queued:                                # then what arrived while it was offline
+                self._deliver(sess, *q)
             while not self._stop.is_set():
                 t, flags, body = read_packet(c)
                 if t == PUBLISH:
@@ -657,18 +659,21 @@ class MqttBroker:
                 pass
 
     def _deliver(self, sess: _Session, topic: str, payload: bytes, qos: int, retain: bool = False):
-        c = sess.conn
-        if c is None:
-            if qos and not sess.clean:
-                sess.queue.append((topic, payload, qos, retain))
-            return
-        if not qos:
-            self._send(sess, c, publish_packet(topic, payload, 0, retain=retain))
-            return
+        # the connection check and the in-flight / offline bookkeeping happen under the session's
+        # write lock, the lock a (re)connecting session drains both under: a message racing a
+        # reconnect is either retransmitted or queued there, never parked on the old connection
         with sess.wlock:
-            pid = sess.next_pid()
-            pkt = publish_packet(topic, payload, qos, pid, retain)
-            sess.out[pid] = ["puback" if qos == 1 else "pubrec", pkt]
+            c = sess.conn
+            if c is None:
+                if qos and not sess.clean:
+                    sess.queue.append((topic, payload, qos, retain))
+                return
+            if qos:
+                pid = sess.next_pid()
+                pkt = publish_packet(topic, payload, qos, pid, retain)
+                sess.out[pid] = ["puback" if qos == 1 else "pubrec", pkt]
+            else:
+                pkt = publish_packet(topic, payload, 0, retain=retain)
         self._send(sess, c, pkt)
 
     def route(self, topic: str, payload: bytes, qos: int = 0, retain: bool = False):

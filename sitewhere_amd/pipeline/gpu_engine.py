@@ -537,6 +537,23 @@ class GpuInboundEngine(EngineBase):
             self._sync_streams()
             return self._with_block(self.collect(sel, raw, from_device=True), sel, now_ms)
 
+    def decode_only(self, raw: np.ndarray, offs: np.ndarray, now_ms: int) -> np.ndarray:
+        """Run only the decode phase (``k_decode_count`` / ``k_scan_sums`` / ``k_decode_emit``) of a
+        host batch and return the decoded ``EVENT_REC`` records in batch order.  A test hook: it
+        checks the device decoder against an independent decoder (``tests/decode_oracle.py``)
+        without validation rewriting the records.  Names it sees count as seen by later steps."""
+        n_msgs = len(offs) - 1
+        with self._lock:
+            self._no_framed_pending()
+            raw_dev, off_dev = self._stage(raw, offs)
+            self._set_batch(raw_dev, off_dev, n_msgs, now_ms)
+            rc = self.lib.sw_phase_decode(ctypes.byref(self.args), self._stream())
+            if rc:
+                raise RuntimeError(f"sw_phase_decode failed ({rc})")
+            self._sync_streams()
+            n = min(int(self.t["scalars"][0].item()), self.cfg.rec_cap)
+            return self.t["recs"][:n * EVENT_REC.itemsize].cpu().numpy().view(EVENT_REC).copy()
+
     def step_framed(self, batch, now_ms: int, presence: bool | None = None) -> StepResult:
         """Synchronous step of a raw-payload record read from the bus: the payload (with its padding)
         and the varint lengths are DMA'd straight from the record -- in place when the record is a

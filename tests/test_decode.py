@@ -87,3 +87,72 @@ def test_threaded_decode_is_deterministic():
     a = cpu_decode(raw, offs, NOW, threads=1)
     b = cpu_decode(raw, offs, NOW, threads=8)
     assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+# ---------------------------------------------------------------- independent oracle (decode_oracle.py)
+from decode_oracle import decode, decode_batch, edge_payloads, mutated_payloads, runtime_verdict  # noqa: E402
+from decode_oracle import fingerprint as py_fingerprint, hash64 as py_hash64  # noqa: E402
+
+
+def oracle_batch(seed=11):
+    """Generator payloads (alternate ids, control messages, multi-measurement) + edge cases +
+    random corruptions, and one payload larger than a workgroup's 32 KB LDS window."""
+    spec = FleetSpec(prefix="o-", n_devices=500, mx_per_msg=3, with_alternate_id=True, p_register=0.02,
+                     p_ack=0.02)
+    raw, offs = gen_payloads(spec, 3000, NOW, seed=seed)
+    b = raw.tobytes()
+    msgs = [b[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    msgs += edge_payloads(NOW) + mutated_payloads(seed, 3000, NOW)
+    msgs.append(wire.measurements("big-1", {f"m{i:05d}": float(i) for i in range(3000)}, alternate_id="big"))
+    return pack_messages(msgs)
+
+
+def test_hashes_match_the_independent_implementation():
+    for s in ["", "a", "dev-0000000001", "x" * 300, "ünïcode"]:
+        assert fingerprint_str(s) == py_fingerprint(s.encode())
+        assert hash64(s) == py_hash64(s.encode())
+
+
+def test_host_decoder_matches_independent_oracle_bitwise():
+    raw, offs = oracle_batch()
+    want, why = decode_batch(raw, offs, NOW)
+    got = cpu_decode(raw, offs, NOW, cap=len(want) + 16)
+    assert len(got) == len(want)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    assert sum(w is not None for w in why) > 1000        # the corruptions do reach the error paths
+
+
+def test_oracle_agrees_with_the_protobuf_runtime_on_validity():
+    """Event payloads are valid exactly when the protobuf runtime parses them with every required
+    field (protobuf-java's rule); the one deliberate divergence is refusing groups."""
+    for seed in (1, 2):
+        for p in edge_payloads(NOW) + mutated_payloads(seed, 2000, NOW):
+            cmd, ok = runtime_verdict(p)
+            if cmd is not None and cmd not in (3, 4, 5):
+                continue                       # control bodies: decoded in full on the host
+            recs, why = decode(p, 0, len(p), NOW)
+            if ok and why is not None:
+                assert why.startswith("group"), (p, why)
+            else:
+                assert ok == (why is None), (p, why)
+
+
+def test_oracle_fields_match_the_protobuf_runtime():
+    spec = FleetSpec(prefix="f-", n_devices=50, mx_per_msg=2, with_alternate_id=True)
+    raw, offs = gen_payloads(spec, 300, NOW, seed=5)
+    b = raw.tobytes()
+    for i in range(300):
+        p = b[offs[i]:offs[i + 1]]
+        cmd, _, body = wire.decode(p)
+        recs, why = decode(p, 0, len(p), NOW)
+        assert why is None
+        fp = py_fingerprint(body.hardwareId.encode())
+        date = body.eventDate if body.HasField("eventDate") else NOW
+        assert all((r["fp_lo"], r["fp_hi"], r["event_date"]) == (*fp, date) for r in recs)
+        if cmd == wire.SEND_DEVICE_MEASUREMENTS:
+            assert [(r["name_hash"], r["v0"]) for r in recs] == [
+                (py_hash64(m.measurementId.encode()), m.measurementValue) for m in body.measurement]
+        elif cmd == wire.SEND_DEVICE_LOCATION:
+            assert (recs[0]["v0"], recs[0]["v1"]) == (body.latitude, body.longitude)
+        else:
+            assert recs[0]["name_hash"] == py_hash64(body.alertType.encode())

@@ -130,6 +130,7 @@ def test_persistent_session_queues_while_offline(broker):
     c = MqttClient("127.0.0.1", broker.port, client_id="dev-7", clean_session=False).connect()
     c.subscribe("cmd/dev-7", 1)
     c.disconnect()
+    assert wait(lambda: broker.session("dev-7").conn is None)    # the broker saw it go offline
     pub = MqttClient("127.0.0.1", broker.port).connect()
     for i in range(5):
         pub.publish("cmd/dev-7", b"c%d" % i, qos=1)
