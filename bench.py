@@ -79,8 +79,18 @@ def open_durable(args, rank, dev):
     seg_dir = os.path.join(tmpdir, f"rank{rank}") if args.durable_dir else tmpdir
     if os.path.exists(seg_dir) and args.durable_dir:
         shutil.rmtree(seg_dir)
-    store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30,
-                              retention_bytes=int(args.durable_retention_gb * (1 << 30)), direct=args.direct_io)
+    retention = int(args.durable_retention_gb * (1 << 30))
+    if retention:
+        # the ranks of a node share its disk: each keeps at most half the free space / local ranks
+        # (a long run then recycles its oldest segments instead of filling the disk)
+        local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        probe = os.path.abspath(tmpdir)
+        while not os.path.exists(probe):
+            probe = os.path.dirname(probe)
+        free = shutil.disk_usage(probe).free
+        retention = max(2 << 30, min(retention, free // (2 * local)))
+    store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30, retention_bytes=retention,
+                              direct=args.direct_io)
     boot = int(time.time() * 1000)
     store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
                                              f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})
