@@ -61,8 +61,23 @@ SW_HD bool sw_check_pair(const uint8_t* buf, uint32_t* pos, uint32_t end, uint32
 // (wire types 3/4, unused by the schema) are refused.  Independent oracle: tests/decode_oracle.py.
 // Returns the number of records produced (never more than max_out when out != null;
 // a message whose expansion does not fit is reported as one decode error).
+//
+// `verdict` (optional) carries the validity between the two passes of the GPU decode: the count
+// pass (out == null) stores SW_DEC_VALID or SW_DEC_ERROR there; an emit pass given that verdict
+// writes a known error's record without parsing it again and skips re-validating the embedded
+// entries of a known-valid payload (the same bytes were checked by the count pass).
+#define SW_DEC_UNKNOWN 0u
+#define SW_DEC_VALID 1u
+#define SW_DEC_ERROR 2u
 SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t end, uint32_t abs_base,
-                                 int64_t now_ms, uint8_t src_rank, SwEventRec* out, uint32_t max_out) {
+                                 int64_t now_ms, uint8_t src_rank, SwEventRec* out, uint32_t max_out,
+                                 uint32_t* verdict = nullptr) {
+  const uint32_t known = verdict ? *verdict : SW_DEC_UNKNOWN;
+  if (out && known == SW_DEC_ERROR) {
+    if (max_out) sw_fill_control(out, SW_EV_DECODE_ERROR, abs_base + start, abs_base + end, 0, 0, now_ms, src_rank);
+    return 1;
+  }
+  const bool trusted = out && known == SW_DEC_VALID;
   uint32_t pos = start;
   uint64_t hlen = 0, blen = 0, v = 0;
   uint64_t cmd = 0;
@@ -84,6 +99,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
   }
   if (!ok || cmd < 1 || cmd > 8) {
     if (out && max_out) sw_fill_control(out, SW_EV_DECODE_ERROR, abs_base + start, abs_base + end, 0, 0, now_ms, src_rank);
+    if (!out && verdict) *verdict = SW_DEC_ERROR;
     return 1;
   }
   const uint32_t bstart = pos, bend = pos + (uint32_t)blen;
@@ -120,9 +136,9 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
     }
     switch (cmd) {
       case SW_CMD_SEND_DEVICE_MEASUREMENTS:
-        if (f == 2 && wt == 2) { n_mx++; ok = sw_check_pair(buf, &pos, bend, 1); }
+        if (f == 2 && wt == 2) { n_mx++; ok = trusted ? sw_skip_field(buf, &pos, bend, wt) : sw_check_pair(buf, &pos, bend, 1); }
         else if (f == 3 && wt == 1) { if (pos + 8 > bend) { ok = false; break; } date = sw_load_le64(buf + pos); pos += 8; has_date = true; }
-        else if (f == 4 && wt == 2) ok = sw_check_pair(buf, &pos, bend, 2);
+        else if (f == 4 && wt == 2) ok = trusted ? sw_skip_field(buf, &pos, bend, wt) : sw_check_pair(buf, &pos, bend, 2);
         else if (f == 5 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
         else ok = sw_skip_field(buf, &pos, bend, wt);
         break;
@@ -135,7 +151,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
           if (f == 2) { lat = d; req_a = true; } else if (f == 3) { lon = d; req_b = true; }
           else if (f == 4) { elev = d; has_elev = true; }
           else { date = bits; has_date = true; }
-        } else if (f == 6 && wt == 2) ok = sw_check_pair(buf, &pos, bend, 2);
+        } else if (f == 6 && wt == 2) ok = trusted ? sw_skip_field(buf, &pos, bend, wt) : sw_check_pair(buf, &pos, bend, 2);
         else if (f == 7 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
         else ok = sw_skip_field(buf, &pos, bend, wt);
         break;
@@ -146,7 +162,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
           if (f == 2) { t_off = pos; t_len = (uint32_t)v; req_a = true; } else { m_off = pos; m_len = (uint32_t)v; req_b = true; }
           pos += (uint32_t)v;
         } else if (f == 4 && wt == 1) { if (pos + 8 > bend) { ok = false; break; } date = sw_load_le64(buf + pos); pos += 8; has_date = true; }
-        else if (f == 5 && wt == 2) ok = sw_check_pair(buf, &pos, bend, 2);
+        else if (f == 5 && wt == 2) ok = trusted ? sw_skip_field(buf, &pos, bend, wt) : sw_check_pair(buf, &pos, bend, 2);
         else if (f == 6 && wt == 0) { ok = sw_read_varint(buf, &pos, bend, &v); has_us = true; us = v != 0; }
         else ok = sw_skip_field(buf, &pos, bend, wt);
         break;
@@ -157,6 +173,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
   }
   if ((cmd == SW_CMD_SEND_DEVICE_LOCATION || cmd == SW_CMD_SEND_DEVICE_ALERT) && !(req_a && req_b)) ok = false;
   if (!ok || !has_dev) {
+    if (!out && verdict) *verdict = SW_DEC_ERROR;
     if (out && max_out) sw_fill_control(out, SW_EV_DECODE_ERROR, abs_base + start, abs_base + end, 0, 0, now_ms, src_rank);
     return 1;
   }
@@ -164,6 +181,7 @@ SW_HD uint32_t sw_decode_payload(const uint8_t* buf, uint32_t start, uint32_t en
                   (has_date ? SW_F_HAS_DATE : 0) | (has_elev ? SW_F_HAS_ELEVATION : 0);
   int64_t edate = has_date ? (int64_t)date : now_ms;
 
+  if (!out && verdict) *verdict = SW_DEC_VALID;
   if (cmd == SW_CMD_SEND_DEVICE_MEASUREMENTS) {
     if (!out) return n_mx;
     if (n_mx > max_out) {

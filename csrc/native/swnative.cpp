@@ -153,7 +153,7 @@ int64_t sw_reg_build(uint64_t* tlo, uint64_t* thi, int32_t* tval, int64_t mask, 
 int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, int64_t now_ms, int32_t rank,
                       SwEventRec* out, int64_t cap, int32_t n_threads) {
   if (n_msgs <= 0) return 0;
-  std::vector<uint32_t> cnt(n_msgs);
+  std::vector<uint32_t> cnt(n_msgs), verdict(n_msgs, SW_DEC_UNKNOWN);   // verdicts: as the GPU passes
   if (n_threads < 1) n_threads = 1;
   auto run = [&](auto&& fn) {
     std::vector<std::thread> th;
@@ -166,7 +166,8 @@ int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, i
     for (auto& x : th) x.join();
   };
   run([&](int64_t b, int64_t e) {
-    for (int64_t m = b; m < e; ++m) cnt[m] = sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, nullptr, 0);
+    for (int64_t m = b; m < e; ++m)
+      cnt[m] = sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, nullptr, 0, &verdict[m]);
   });
   std::vector<int64_t> pre(n_msgs + 1, 0);
   for (int64_t m = 0; m < n_msgs; ++m) pre[m + 1] = pre[m] + cnt[m];
@@ -174,7 +175,8 @@ int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, i
     for (int64_t m = b; m < e; ++m) {
       int64_t o = pre[m];
       if (o >= cap) continue;
-      sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, out + o, (uint32_t)std::min<int64_t>(cap - o, 0xffffffffll));
+      sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, out + o,
+                        (uint32_t)std::min<int64_t>(cap - o, 0xffffffffll), &verdict[m]);
     }
   });
   return std::min<int64_t>(pre[n_msgs], cap);
