@@ -192,9 +192,13 @@ def decode(payload: bytes):
     """Decode one payload -> (command, originator or None, body message)."""
     h, pos = read_delimited(payload, 0, Header)
     cls = _BODY.get(h.command)
-    if cls is None:
-        raise ValueError(f"unknown command {h.command}")
+    if cls is None or not h.IsInitialized():
+        raise ValueError(f"unknown command {h.command if h.HasField('command') else None}")
     body, _ = read_delimited(payload, pos, cls)
+    if not body.IsInitialized():
+        # protobuf-java's parseDelimitedFrom refuses a message missing a `required` field
+        # (ProtobufDeviceEventDecoder.java:79-95); the python runtime parses it, so check here
+        raise ValueError(f"{cls.DESCRIPTOR.name} misses required fields: {body.FindInitializationErrors()}")
     return h.command, (h.originator if h.HasField("originator") else None), body
 
 
