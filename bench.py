@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--p-unregistered", type=float, default=0.005)
     ap.add_argument("--p-register", type=float, default=0.0005)
     ap.add_argument("--p-ack", type=float, default=0.0005)
+    ap.add_argument("--p-meta", type=float, default=0.1,
+                    help="share of events carrying metadata entries (stored with the event, like the reference)")
     ap.add_argument("--durable", action=argparse.BooleanOptionalAction, default=True,
                     help="persist every step's events to fdatasync'd segment files (the headline)")
     ap.add_argument("--durable-dir", default=os.environ.get("SW_DURABLE_DIR"),
@@ -151,7 +153,7 @@ def main():
     spec = FleetSpec(prefix="dev-", n_devices=n_total_dev, p_location=0.25, p_alert=0.05,
                      p_unregistered=args.p_unregistered, mx_per_msg=args.mx_per_msg, n_names=16,
                      with_alternate_id=args.alt_ids, lat0=33.0, lon0=-85.0, span_deg=2.0,
-                     p_register=args.p_register, p_ack=args.p_ack)
+                     p_register=args.p_register, p_ack=args.p_ack, p_meta=args.p_meta)
     cfg = EngineConfig(max_msgs=args.msgs, rec_cap=args.msgs * args.mx_per_msg + 4096,
                        gen_cap=max(1 << 16, args.msgs // 2), max_devices=int(args.devices * 1.1) + 1024,
                        max_assignments=int(args.devices * 1.1) + 1024, store_cap=args.store,

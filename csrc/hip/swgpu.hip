@@ -347,6 +347,7 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ raw, co
 // k_decode_count's per-message count carries the count pass's decode verdict in its top bit
 // (a payload never expands to 2^31 records)
 #define CNT_ERR 0x80000000u
+#define CNT_OVR 0x40000000u   // oversize event (SW_DEC_OVERSIZE): one host-routed record
 
 __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
                                                       int64_t n_msgs, uint32_t* __restrict__ cnt,
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict_
     uint32_t verdict = SW_DEC_UNKNOWN;
     c = staged ? sw_decode_payload(lds, off[m] - base, off[m + 1] - base, base, 0, 0, nullptr, 0, &verdict)
                : sw_decode_payload(raw, off[m], off[m + 1], 0, 0, 0, nullptr, 0, &verdict);
-    cnt[m] = c | (verdict == SW_DEC_ERROR ? CNT_ERR : 0u);   // the emit pass reuses the verdict
+    cnt[m] = c | (verdict == SW_DEC_ERROR ? CNT_ERR : 0u) | (verdict == SW_DEC_OVERSIZE ? CNT_OVR : 0u);  // reused by emit
   }
   // per-block record total: the block sums are scanned by one workgroup (k_scan_sums) and
   // k_decode_emit rebuilds the in-block prefix itself -- reduce-then-scan with no look-back chain
@@ -409,19 +410,20 @@ __global__ __launch_bounds__(BLK) void k_decode_emit(SwEngineArgs a) {
   const int64_t m = (int64_t)BID * BLK + threadIdx.x;
   uint32_t tot;
   const uint32_t cv = m < a.n_msgs ? a.msg_cnt[m] : 0u;
-  const uint32_t pre = block_excl_scan(cv & ~CNT_ERR, &tot, red);
+  const uint32_t pre = block_excl_scan(cv & ~(CNT_ERR | CNT_OVR), &tot, red);
   if (m >= a.n_msgs) return;
-  uint32_t verdict = (cv & CNT_ERR) ? SW_DEC_ERROR : SW_DEC_VALID;
+  uint32_t verdict = (cv & CNT_ERR) ? SW_DEC_ERROR : (cv & CNT_OVR) ? SW_DEC_OVERSIZE : SW_DEC_VALID;
   const int64_t o = (int64_t)a.msg_evoff[BID] + pre;      // msg_evoff holds the scanned block sums
   if (o >= a.rec_cap) return;
   const uint32_t room = (uint32_t)((a.rec_cap - o) < 0xffffffffll ? (a.rec_cap - o) : 0xffffffffll);
   SwEventRec* out = a.recs + o;
   uint32_t n;
+  SwStrRef* sp = a.spans ? a.spans + o : nullptr;
   if (staged)
     n = sw_decode_payload(lds, a.msg_off[m] - base, a.msg_off[m + 1] - base, base, a.now_ms, (uint8_t)a.rank, out, room,
-                          &verdict);
+                          &verdict, sp);
   else
-    n = sw_decode_payload(a.raw, a.msg_off[m], a.msg_off[m + 1], 0, a.now_ms, (uint8_t)a.rank, out, room, &verdict);
+    n = sw_decode_payload(a.raw, a.msg_off[m], a.msg_off[m + 1], 0, a.now_ms, (uint8_t)a.rank, out, room, &verdict, sp);
   // fused new-name capture (one probe of a small L2-resident table per named record)
   for (uint32_t k = 0; k < n && k < room; ++k)
     note_name(out[k], (ull*)a.seen_key, a.seen_mask, a.new_names, a.n_new_names, a.names_cap);
@@ -1680,6 +1682,7 @@ int sw_abi_sizes(int64_t* out) {
   out[6] = sizeof(SwAsgState);
   out[7] = sizeof(SwMsSlot);
   out[8] = sizeof(SwWireRec);
+  out[9] = sizeof(SwStrRef);
   return 0;
 }
 

@@ -1,18 +1,24 @@
-// Durable-block encoder on the MI355X: one engine step's persisted rows -> one compressed columnar
+// Durable-block encoder on the MI355X: one engine step's persisted events -> one compressed columnar
 // block (format: csrc/include/swseg.h), written into HBM so only the compressed bytes cross PCIe
 // to the segment store.  Bit-identical to the CPU encoder (csrc/native/swseg.cpp, swseg_encode).
 //
-// One 256-thread workgroup (4 wave64) per 1024-row page, 4 consecutive rows per thread:
-//   A. plan: per column, block scans give each row its index within the column (the column's
-//      member rows, e.g. locations for latitude) and block reductions the frame-of-reference base,
-//      bit width, decimal exponent and exception count -> the page's byte size;
-//   B. single-pass decoupled look-back over the pages (ticketed workgroups, 64-bit state words:
-//      flag | value in one agent-scope atomic, so no payload hand-off and no fence) -> the page's
-//      offset in the block, without a separate scan launch;
-//   C. write: member values are staged in LDS, then each thread assembles whole u64 words of the
-//      bit-packed stream (no atomics, coalesced 8-byte stores) and folds them into the page
-//      checksum; a block xor-reduction writes it.
-// The grid is sized for the largest step (rows known on the device only); surplus tickets exit.
+// Input per row j of the step: the enriched row (rows[j]), its decoded record -- work[ok_idx[j]]
+// for the validated events, gen[j - n_ok] for the generated ones -- and, for device events, the
+// record's string refs (spans) into the raw batch still resident in HBM.  The strings (alternate id,
+// alert message, metadata span) are copied from the raw batch into the page's string heap here.
+//
+// One 256-thread workgroup (4 wave64) per 1024-row page, 4 consecutive rows per thread.  The plan
+// is a few fused block-wide rounds instead of one scan / reduction per column:
+//   R1  first row with an alternate id; per double column the decimal exponent (max of the rows'
+//       exponents, searched from a per-column hint: ~2 trials per value instead of up to 16)
+//   R2  alternate-id common prefix + hex test (one LCP / last-non-hex / length reduction), every
+//       integer column's min / max, the double columns' quantised min / max
+//   R3  one multi-column scan: member indices of all 15 columns, exception indices, heap offsets
+// then thread 0 lays the page out and finds its offset in the block with a single-pass decoupled
+// look-back (ticketed workgroups, 64-bit flag|value state words).  The write stages two columns at
+// a time in LDS (each thread assembles whole u64 words: no atomics, coalesced 8-byte stores) and
+// gathers the string heap word by word straight from the raw batch; every word is folded into the
+// page checksum on the way out.  The grid is sized for the largest step; surplus tickets exit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "swtypes.h"
@@ -20,15 +26,19 @@
 
 #define SBLK 256
 #define SWAVES (SBLK / 64)
-#define ROWS_PER_THREAD 4
+#define RPT 4
 
 typedef unsigned long long ull;
 
 struct SwSegArgs {
   const SwOutRec* rows;        // this step's rows (device)
-  const double* ring_v2;       // event ring elevation column
-  const uint64_t* ring_alt;    // event ring alternate-id hash column
-  int64_t store_cap;
+  const SwEventRec* work;      // validated records of the step
+  const uint32_t* ok_idx;      // row j < *n_ok <-> work[ok_idx[j]]
+  const uint32_t* n_ok;
+  const SwEventRec* gen;       // row j >= *n_ok <-> gen[j - n_ok]
+  const SwStrRef* spans;       // string refs of the work records (null: none carry strings)
+  const uint8_t* raw;          // the batch the work records were decoded from (null: no strings)
+  int64_t raw_bytes;
   const int64_t* cursor;       // [store_cursor, step_cursor0]: rows = cursor[0] - cursor[1]
   uint8_t* out;                // block (device)
   int64_t out_cap;
@@ -43,250 +53,131 @@ struct SwSegArgs {
 
 __device__ __forceinline__ uint32_t lane64() { return threadIdx.x & 63; }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-
-__device__ __forceinline__ ull wave_min(ull v) {
+__device__ __forceinline__ ull wmin(ull v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) { const ull o = __shfl_xor(v, d, 64); v = o < v ? o : v; }
   return v;
 }
-
-__device__ __forceinline__ ull wave_max(ull v) {
+__device__ __forceinline__ ull wmax(ull v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) { const ull o = __shfl_xor(v, d, 64); v = o > v ? o : v; }
   return v;
 }
-
-__device__ __forceinline__ ull wave_xor(ull v) {
+__device__ __forceinline__ ull wxor(ull v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
   return v;
 }
 
-struct SegRed {
-  ull a[SWAVES], b[SWAVES];
-  uint32_t s[SWAVES + 1];
-};
-
-// Exclusive block scan of one u32 per thread (returns the prefix; *total = block sum).
-__device__ __forceinline__ uint32_t seg_scan(uint32_t v, uint32_t* total, SegRed& R) {
-  const uint32_t lane = lane64(), wid = threadIdx.x >> 6;
-  uint32_t inc = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(inc, d, 64);
-    if (lane >= (uint32_t)d) inc += t;
-  }
-  if (lane == 63) R.s[wid] = inc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int w = 0; w < SWAVES; ++w) { const uint32_t t = R.s[w]; R.s[w] = acc; acc += t; }
-    R.s[SWAVES] = acc;
-  }
-  __syncthreads();
-  const uint32_t res = inc - v + R.s[wid];
-  *total = R.s[SWAVES];
-  __syncthreads();
-  return res;
-}
-
-// Block min and max of u64 values (threads without members pass ~0 / 0).
-__device__ __forceinline__ void seg_minmax(ull lo, ull hi, ull* blo, ull* bhi, SegRed& R) {
-  lo = wave_min(lo);
-  hi = wave_max(hi);
-  const uint32_t wid = threadIdx.x >> 6;
-  if (lane64() == 0) { R.a[wid] = lo; R.b[wid] = hi; }
-  __syncthreads();
-  ull l = R.a[0], h = R.b[0];
-#pragma unroll
-  for (int w = 1; w < SWAVES; ++w) { l = R.a[w] < l ? R.a[w] : l; h = R.b[w] > h ? R.b[w] : h; }
-  *blo = l;
-  *bhi = h;
-  __syncthreads();
-}
-
-struct SegRow {
+// ----------------------------------------------------------------------------- page row
+struct SRow {
   int64_t date;
   double v0, v1, v2;
-  uint64_t alt;
   int32_t asg;
   uint16_t name;
   uint8_t et, level;
+  SegRowStr s;
+  bool valid;
 };
 
-template <int C>
-__device__ __forceinline__ uint64_t seg_int_value(const SegRow& r) {
-  if (C == SEG_ETYPE) return seg_ord((int64_t)r.et);
-  if (C == SEG_LEVEL) return seg_ord((int64_t)r.level);
-  if (C == SEG_DATE) return seg_ord(r.date);
-  if (C == SEG_ASG) return seg_ord((int64_t)r.asg);
-  if (C == SEG_NAME) return seg_ord((int64_t)r.name);
-  if (C == SEG_HASALT) return seg_ord(r.alt != 0 ? 1 : 0);
-  return r.alt;   // SEG_ALT
+// integer value (order-preserving unsigned) of column c; altnum given by the caller
+__device__ __forceinline__ ull sval(int c, const SRow& r, uint32_t pfx, ull altnum) {
+  switch (c) {
+    case SEG_ETYPE: return seg_ord((int64_t)r.et);
+    case SEG_LEVEL: return seg_ord((int64_t)r.level);
+    case SEG_DATE: return seg_ord(r.date);
+    case SEG_ASG: return seg_ord((int64_t)r.asg);
+    case SEG_NAME: return seg_ord((int64_t)r.name);
+    case SEG_FLAGS: return seg_ord((int64_t)r.s.flags);
+    case SEG_ALTK: return seg_ord((int64_t)r.s.altk);
+    case SEG_ALTLEN: return seg_ord((int64_t)(r.s.alt_len - pfx));
+    case SEG_ALTNUM: return altnum;
+    case SEG_MSGLEN: return seg_ord((int64_t)r.s.msg_len);
+    case SEG_METALEN: return seg_ord((int64_t)r.s.meta_len);
+    default: return 0;
+  }
 }
 
-template <int C>
-__device__ __forceinline__ double seg_dbl_value(const SegRow& r) {
-  return (C == SEG_MXV || C == SEG_LAT) ? r.v0 : (C == SEG_LON ? r.v1 : r.v2);
+__device__ __forceinline__ double sdbl(int c, const SRow& r) {
+  return (c == SEG_MXV || c == SEG_LAT) ? r.v0 : (c == SEG_LON ? r.v1 : r.v2);
 }
+
+__device__ __forceinline__ int exp_hint(int c) { return c == SEG_MXV ? 2 : c == SEG_ELEV ? 1 : 6; }
+
+__device__ __forceinline__ bool smem(int c, const SRow& r, int mode) {
+  return r.valid && seg_member(c, r.et, r.s.flags, mode);
+}
+
+// block-scanned counters: 15 member counts, 4 exception counts (u16 prefixes); heap bytes (u32)
+#define NCNT (SEG_NCOL + 4)
+#define NDBL 4
+#define NSLOT 48
+
+// Columns are written two at a time; no pair holds two double columns (one exception stage).
+__device__ static const int8_t seg_pairs[8][2] = {{SEG_ETYPE, SEG_LEVEL}, {SEG_DATE, SEG_ASG}, {SEG_NAME, SEG_MXV},
+                                                  {SEG_LAT, SEG_FLAGS},   {SEG_LON, SEG_ALTK}, {SEG_ELEV, SEG_ALTLEN},
+                                                  {SEG_ALTNUM, SEG_MSGLEN}, {SEG_METALEN, -1}};
 
 struct SegLds {
-  ull vals[SEG_PAGE_ROWS];
-  ull xraw[SEG_PAGE_ROWS];
-  uint16_t xidx[SEG_PAGE_ROWS];
+  ull red[SWAVES][NSLOT];      // per-wave partial reductions
+  ull res[NSLOT];              // block results
+  uint32_t wtot[SWAVES][NCNT + 1];
+  uint16_t pre[NCNT][SBLK];    // exclusive member / exception prefixes of each thread
+  uint32_t hpre[SBLK];         // exclusive heap-byte prefix of each thread
+  uint32_t tot[NCNT + 1];
+  // staging (two columns, one exception list), or the heap gather tables
+  union {
+    struct {
+      ull vals[2][SEG_PAGE_ROWS];
+      ull xraw[SEG_PAGE_ROWS];
+      uint16_t xidx[SEG_PAGE_ROWS];
+    } st;
+    struct {
+      uint32_t hoff[SEG_PAGE_ROWS + 1];    // row heap offsets (after the prefix)
+      uint32_t src[SEG_PAGE_ROWS][3];      // alt remainder / msg / meta source offsets in raw
+      uint16_t len[SEG_PAGE_ROWS][3];
+    } hp;
+  } u;
   SwSegPageHdr hdr;
-  SegRed red;
+  int first_alt;
+  uint32_t alt_off0, alt_len0;
   uint32_t page;
-  uint32_t pad;
   ull page_base;
+  int exps[NDBL];
 };
-
-// Plan column C: count, base, bits, exponent, exceptions; per-thread member / exception prefixes.
-template <int C>
-__device__ __forceinline__ void seg_plan(const SegRow (&R)[ROWS_PER_THREAD], const bool (&valid)[ROWS_PER_THREAD],
-                                         SegLds& L, uint32_t* pre, uint32_t* xpre) {
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int k = 0; k < ROWS_PER_THREAD; ++k) cnt += (valid[k] && seg_member(C, R[k].et, R[k].alt)) ? 1u : 0u;
-  uint32_t count;
-  *pre = seg_scan(cnt, &count, L.red);
-  SwSegCol& cd = L.hdr.cols[C];
-  if (!seg_is_double(C)) {
-    ull lo = ~0ull, hi = 0;
-#pragma unroll
-    for (int k = 0; k < ROWS_PER_THREAD; ++k) {
-      if (!(valid[k] && seg_member(C, R[k].et, R[k].alt))) continue;
-      const ull u = seg_int_value<C>(R[k]);
-      lo = u < lo ? u : lo;
-      hi = u > hi ? u : hi;
-    }
-    ull blo, bhi;
-    seg_minmax(lo, hi, &blo, &bhi, L.red);
-    *xpre = 0;
-    if (threadIdx.x == 0) {
-      cd.base = count ? blo : 0;
-      cd.bits = (uint8_t)(count ? seg_bitwidth(bhi - blo) : 0);
-      cd.exp = -1;
-      cd.count = (uint16_t)count;
-      cd.n_exc = 0;
-    }
-  } else {
-    // page exponent = the largest per-value exponent among decimal-exact values
-    ull emax = 0;
-#pragma unroll
-    for (int k = 0; k < ROWS_PER_THREAD; ++k) {
-      if (!(valid[k] && seg_member(C, R[k].et, R[k].alt))) continue;
-      const int e = seg_dec_exp(seg_dbl_value<C>(R[k]));
-      if (e != SEG_EXC_NONE && (ull)e > emax) emax = (ull)e;
-    }
-    ull dummy, be;
-    seg_minmax(~0ull, emax, &dummy, &be, L.red);
-    const int e = (int)be;
-    ull lo = ~0ull, hi = 0;
-    uint32_t nx = 0;
-#pragma unroll
-    for (int k = 0; k < ROWS_PER_THREAD; ++k) {
-      if (!(valid[k] && seg_member(C, R[k].et, R[k].alt))) continue;
-      int64_t q;
-      if (seg_dec_at(seg_dbl_value<C>(R[k]), e, &q)) {
-        const ull u = seg_ord(q);
-        lo = u < lo ? u : lo;
-        hi = u > hi ? u : hi;
-      } else {
-        ++nx;
-      }
-    }
-    uint32_t n_exc;
-    *xpre = seg_scan(nx, &n_exc, L.red);
-    ull blo, bhi;
-    seg_minmax(lo, hi, &blo, &bhi, L.red);
-    if (threadIdx.x == 0) {
-      const bool any = count > n_exc;
-      cd.base = any ? blo : 0;
-      cd.bits = (uint8_t)(any ? seg_bitwidth(bhi - blo) : 0);
-      cd.exp = (int8_t)e;
-      cd.count = (uint16_t)count;
-      cd.n_exc = (uint16_t)n_exc;
-    }
-  }
-}
-
-// Stage column C's packed values in LDS, then write its words (+ exceptions); returns this thread's
-// checksum contribution.
-template <int C>
-__device__ __forceinline__ ull seg_write(const SegRow (&R)[ROWS_PER_THREAD], const bool (&valid)[ROWS_PER_THREAD],
-                                         SegLds& L, uint32_t pre, uint32_t xpre, uint8_t* page) {
-  const SwSegCol cd = L.hdr.cols[C];
-  uint32_t i = pre, x = xpre;
-#pragma unroll
-  for (int k = 0; k < ROWS_PER_THREAD; ++k) {
-    if (!(valid[k] && seg_member(C, R[k].et, R[k].alt))) continue;
-    if (!seg_is_double(C)) {
-      L.vals[i] = seg_int_value<C>(R[k]) - cd.base;
-    } else {
-      const double v = seg_dbl_value<C>(R[k]);
-      int64_t q;
-      if (seg_dec_at(v, cd.exp, &q)) {
-        L.vals[i] = seg_ord(q) - cd.base;
-      } else {
-        L.vals[i] = 0;
-        L.xidx[x] = (uint16_t)i;
-        L.xraw[x] = sw_f64_bits(v);
-        ++x;
-      }
-    }
-    ++i;
-  }
-  __syncthreads();
-  ull cs = 0;
-  const uint32_t bits = cd.bits, n = cd.count;
-  const uint32_t nw = seg_col_words(n, (int)bits);
-  for (uint32_t w = threadIdx.x; w < nw; w += SBLK) {
-    ull word = 0;
-    const ull bit0 = (ull)w * 64ull;
-    for (uint32_t j = (uint32_t)(bit0 / bits); j < n; ++j) {
-      const ull b = (ull)j * bits;
-      if (b >= bit0 + 64) break;
-      word |= b >= bit0 ? (L.vals[j] << (b - bit0)) : (L.vals[j] >> (bit0 - b));
-    }
-    const uint32_t off = cd.data_off + 8u * w;
-    *reinterpret_cast<ull*>(page + off) = word;
-    cs ^= seg_mix_word(word, off >> 3);
-  }
-  if (seg_is_double(C) && cd.n_exc) {
-    const uint32_t ne = cd.n_exc;
-    const uint32_t xo = cd.data_off + 8u * nw;
-    const uint32_t nidx = (2u * ne + 7u) / 8u;
-    for (uint32_t w = threadIdx.x; w < nidx; w += SBLK) {
-      ull word = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < 4; ++j)
-        if (4 * w + j < ne) word |= (ull)L.xidx[4 * w + j] << (16 * j);
-      *reinterpret_cast<ull*>(page + xo + 8u * w) = word;
-      cs ^= seg_mix_word(word, (xo >> 3) + w);
-    }
-    const uint32_t ro = xo + 8u * nidx;
-    for (uint32_t j = threadIdx.x; j < ne; j += SBLK) {
-      *reinterpret_cast<ull*>(page + ro + 8u * j) = L.xraw[j];
-      cs ^= seg_mix_word(L.xraw[j], (ro >> 3) + j);
-    }
-  }
-  __syncthreads();         // the next column reuses the staging arrays
-  return cs;
-}
 
 __device__ __forceinline__ ull lb_load(uint64_t* p) {
   return __hip_atomic_load((ull*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
 __device__ __forceinline__ void lb_store(uint64_t* p, ull v) {
   __hip_atomic_store((ull*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave partial of one reduction slot (lane 0 stores it); block_finish combines the waves.
+__device__ __forceinline__ void wave_put(SegLds& L, int slot, ull v, bool mx) {
+  const ull r = mx ? wmax(v) : wmin(v);
+  if (lane64() == 0) L.red[threadIdx.x >> 6][slot] = r;
+}
+
+// Slots [0, ns): bit i of maxmask = max, else min.  Two barriers; L.res valid for every thread after.
+__device__ __forceinline__ void block_finish(SegLds& L, int ns, uint64_t maxmask) {
+  __syncthreads();
+  if ((int)threadIdx.x < ns) {
+    const int i = threadIdx.x;
+    const bool mx = (maxmask >> i) & 1;
+    ull r = L.red[0][i];
+#pragma unroll
+    for (int w = 1; w < SWAVES; ++w) { const ull o = L.red[w][i]; r = mx ? (o > r ? o : r) : (o < r ? o : r); }
+    L.res[i] = r;
+  }
+  __syncthreads();
+}
+
+// hex value of a row's alternate-id remainder
+__device__ __forceinline__ ull alt_hex(const uint8_t* raw, const SRow& r, uint32_t pfx) {
+  ull v = 0;
+  for (uint32_t i = pfx; i < r.s.alt_len; ++i) v = (v << 4) | seg_hex_value(raw[r.s.alt_off + i]);
+  return v;
 }
 
 __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
@@ -320,15 +211,17 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   if ((int64_t)page >= np) return;
   const int64_t r0 = (int64_t)page * SEG_PAGE_ROWS;
   const int m = (int)(n - r0 < SEG_PAGE_ROWS ? n - r0 : SEG_PAGE_ROWS);
-  // ---- load 4 consecutive rows per thread
-  SegRow R[ROWS_PER_THREAD];
-  bool valid[ROWS_PER_THREAD];
+  const uint32_t nok = *a.n_ok;
+  const int64_t rawb = a.raw ? a.raw_bytes : 0;
+
+  // ---- load 4 consecutive rows per thread: enriched row, record, string refs
+  SRow R[RPT];
 #pragma unroll
-  for (int k = 0; k < ROWS_PER_THREAD; ++k) {
-    const int idx = ROWS_PER_THREAD * (int)threadIdx.x + k;
-    valid[k] = idx < m;
-    SegRow& r = R[k];
-    if (valid[k]) {
+  for (int k = 0; k < RPT; ++k) {
+    const int idx = RPT * (int)threadIdx.x + k;
+    SRow& r = R[k];
+    r.valid = idx < m;
+    if (r.valid) {
       const int64_t j = r0 + idx;
       const uint4 q0 = *reinterpret_cast<const uint4*>(&a.rows[j]);
       const uint4 q1 = *(reinterpret_cast<const uint4*>(&a.rows[j]) + 1);
@@ -339,40 +232,254 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
       r.name = (uint16_t)(q1.w & 0xffffu);
       r.et = (uint8_t)((q1.w >> 16) & 0xffu);
       r.level = (uint8_t)(q1.w >> 24);
-      const int64_t row = (c0 + j) % a.store_cap;
-      r.v2 = a.ring_v2[row];
-      r.alt = a.ring_alt[row];
+      SwStrRef sp;
+      sp.alt_off = 0; sp.meta_off = 0; sp.alt_len = 0; sp.meta_len = 0; sp.k = 0; sp.has = 0; sp.pad = 0;
+      const SwEventRec* rec;
+      if (j < (int64_t)nok) {
+        const uint32_t i = a.ok_idx[j];
+        rec = a.work + i;
+        if (a.spans) sp = a.spans[i];
+      } else {
+        rec = a.gen + (j - nok);
+      }
+      r.v2 = rec->v2;
+      r.s = seg_row_strings(*rec, sp, rawb);
     } else {
-      r.date = 0; r.v0 = r.v1 = r.v2 = 0.0; r.alt = 0; r.asg = 0; r.name = 0; r.et = 0; r.level = 0;
+      r.date = 0; r.v0 = r.v1 = r.v2 = 0.0; r.asg = 0; r.name = 0; r.et = 0; r.level = 0;
+      r.s.alt_off = r.s.alt_len = r.s.msg_off = r.s.msg_len = r.s.meta_off = r.s.meta_len = r.s.altk = r.s.flags = 0;
     }
   }
-  // ---- A. plan every column
-  uint32_t pre[SEG_NCOL], xpre[SEG_NCOL];
-  seg_plan<SEG_ETYPE>(R, valid, L, &pre[SEG_ETYPE], &xpre[SEG_ETYPE]);
-  seg_plan<SEG_LEVEL>(R, valid, L, &pre[SEG_LEVEL], &xpre[SEG_LEVEL]);
-  seg_plan<SEG_DATE>(R, valid, L, &pre[SEG_DATE], &xpre[SEG_DATE]);
-  seg_plan<SEG_ASG>(R, valid, L, &pre[SEG_ASG], &xpre[SEG_ASG]);
-  seg_plan<SEG_NAME>(R, valid, L, &pre[SEG_NAME], &xpre[SEG_NAME]);
-  seg_plan<SEG_MXV>(R, valid, L, &pre[SEG_MXV], &xpre[SEG_MXV]);
-  seg_plan<SEG_LAT>(R, valid, L, &pre[SEG_LAT], &xpre[SEG_LAT]);
-  seg_plan<SEG_LON>(R, valid, L, &pre[SEG_LON], &xpre[SEG_LON]);
-  seg_plan<SEG_ELEV>(R, valid, L, &pre[SEG_ELEV], &xpre[SEG_ELEV]);
-  seg_plan<SEG_HASALT>(R, valid, L, &pre[SEG_HASALT], &xpre[SEG_HASALT]);
-  seg_plan<SEG_ALT>(R, valid, L, &pre[SEG_ALT], &xpre[SEG_ALT]);
-  // ---- B. page size, offsets; look-back for the page's place in the block
+
+  // ---- R1: first row with an alternate id; decimal exponent per double column
+  {
+    ull fa_local = ~0ull;
+#pragma unroll
+    for (int k = RPT - 1; k >= 0; --k)
+      if (R[k].valid && (R[k].s.flags & SEGF_HAS_ALT)) fa_local = (ull)(RPT * threadIdx.x + k);
+    wave_put(L, 0, fa_local, false);
+#pragma unroll
+    for (int d = 0; d < NDBL; ++d) {
+      const int c = SEG_MXV + d;
+      int e = 0;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        if (!smem(c, R[k], SEG_ALT_RAW)) continue;
+        const int ei = seg_dec_exp_from(sdbl(c, R[k]), exp_hint(c));
+        if (ei != SEG_EXC_NONE && ei > e) e = ei;
+      }
+      wave_put(L, 1 + d, (ull)e, true);
+    }
+    block_finish(L, 1 + NDBL, 0x1eull);
+    if (threadIdx.x == 0) {
+      L.first_alt = L.res[0] == ~0ull ? -1 : (int)L.res[0];
+#pragma unroll
+      for (int d = 0; d < NDBL; ++d) L.exps[d] = (int)L.res[1 + d];
+    }
+    // the row's owner publishes the first alternate id's location
+    const int fa = L.res[0] == ~0ull ? -1 : (int)L.res[0];
+    if (fa >= 0 && fa / RPT == (int)threadIdx.x) {
+#pragma unroll
+      for (int k = 0; k < RPT; ++k)
+        if (RPT * (int)threadIdx.x + k == fa) { L.alt_off0 = R[k].s.alt_off; L.alt_len0 = R[k].s.alt_len; }
+    }
+    __syncthreads();
+  }
+  const int first_alt = L.first_alt;
+  const uint32_t a_off0 = first_alt >= 0 ? L.alt_off0 : 0u, a_len0 = first_alt >= 0 ? L.alt_len0 : 0u;
+
+  // ---- R2: alternate-id prefix / hex test; integer min / max; quantised double min / max
+  // slots: [0] min LCP, [1] max last-non-hex+1, [2] min alt len, [3] max alt len,
+  //        [4 + 2c] / [5 + 2c] min / max of integer column c (ALTLEN follows from [2] / [3], ALTNUM
+  //        needs the mode: R3), [34 + 2d] / [35 + 2d] min / max of the quantised double column d
+  {
+    const uint32_t plim = a_len0 < SEG_ALT_PFX_MAX ? a_len0 : SEG_ALT_PFX_MAX;
+    ull lcp = ~0ull, lnh = 0, lmin = ~0ull, lmax = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const SRow& r = R[k];
+      if (!(r.valid && (r.s.flags & SEGF_HAS_ALT))) continue;
+      const uint8_t* sa = a.raw + r.s.alt_off;
+      const uint8_t* s0 = a.raw + a_off0;
+      const uint32_t lim = plim < r.s.alt_len ? plim : r.s.alt_len;
+      uint32_t l = 0;
+      while (l < lim && sa[l] == s0[l]) ++l;
+      lcp = (ull)l < lcp ? (ull)l : lcp;
+      uint32_t last = 0;
+      for (uint32_t i = 0; i < r.s.alt_len; ++i)
+        if (!seg_is_hex_digit(sa[i])) last = i + 1;
+      lnh = (ull)last > lnh ? (ull)last : lnh;
+      lmin = (ull)r.s.alt_len < lmin ? (ull)r.s.alt_len : lmin;
+      lmax = (ull)r.s.alt_len > lmax ? (ull)r.s.alt_len : lmax;
+    }
+    wave_put(L, 0, lcp, false);
+    wave_put(L, 1, lnh, true);
+    wave_put(L, 2, lmin, false);
+    wave_put(L, 3, lmax, true);
+#pragma unroll
+    for (int c = 0; c < SEG_NCOL; ++c) {
+      if (seg_is_double(c) || c == SEG_ALTLEN || c == SEG_ALTNUM) continue;
+      ull lo = ~0ull, hi = 0;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        if (!smem(c, R[k], SEG_ALT_RAW)) continue;
+        const ull u = sval(c, R[k], 0, 0);
+        lo = u < lo ? u : lo;
+        hi = u > hi ? u : hi;
+      }
+      wave_put(L, 4 + 2 * c, lo, false);
+      wave_put(L, 5 + 2 * c, hi, true);
+    }
+#pragma unroll
+    for (int d = 0; d < NDBL; ++d) {
+      const int c = SEG_MXV + d;
+      const int e = L.exps[d];
+      ull lo = ~0ull, hi = 0;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        if (!smem(c, R[k], SEG_ALT_RAW)) continue;
+        int64_t q;
+        if (seg_dec_at(sdbl(c, R[k]), e, &q)) {
+          const ull u = seg_ord(q);
+          lo = u < lo ? u : lo;
+          hi = u > hi ? u : hi;
+        }
+      }
+      wave_put(L, 34 + 2 * d, lo, false);
+      wave_put(L, 35 + 2 * d, hi, true);
+    }
+    // max slots: 1, 3, every odd slot from 5 (unused slots reduce garbage nobody reads)
+    block_finish(L, 42, 0x2aaaaaaaaaaull);
+  }
+  // prefix and mode (every thread computes the same from L.res)
+  uint32_t pfx = 0, mode = SEG_ALT_RAW, width = 0;
+  if (first_alt >= 0) {
+    pfx = (uint32_t)L.res[0];
+    const uint32_t wmn = (uint32_t)L.res[2] - pfx, wmx = (uint32_t)L.res[3] - pfx;
+    if ((uint32_t)L.res[1] <= pfx && wmn == wmx && wmn >= 1 && wmn <= 16) { mode = SEG_ALT_HEX; width = wmn; }
+  }
+
+  // ---- R3: member / exception / heap scans (+ ALTNUM min / max in hex mode)
+  ull altnum[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k)
+    altnum[k] = (mode == SEG_ALT_HEX && R[k].valid && (R[k].s.flags & SEGF_HAS_ALT)) ? alt_hex(a.raw, R[k], pfx) : 0;
+  {
+    const uint32_t lane = lane64(), wid = threadIdx.x >> 6;
+    uint32_t hb = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const SRow& r = R[k];
+      if (!r.valid) continue;
+      if (mode == SEG_ALT_RAW && (r.s.flags & SEGF_HAS_ALT)) hb += r.s.alt_len - pfx;
+      hb += r.s.msg_len + r.s.meta_len;
+    }
+    uint32_t ex[NCNT + 1];
+#pragma unroll
+    for (int c = 0; c <= NCNT; ++c) {
+      uint32_t x = 0;
+      if (c < SEG_NCOL) {
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) x += smem(c, R[k], (int)mode) ? 1u : 0u;
+      } else if (c < NCNT) {
+        const int d = c - SEG_NCOL;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+          int64_t q;
+          if (smem(SEG_MXV + d, R[k], (int)mode) && !seg_dec_at(sdbl(SEG_MXV + d, R[k]), L.exps[d], &q)) ++x;
+        }
+      } else {
+        x = hb;
+      }
+      uint32_t inc = x;
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t t = __shfl_up(inc, dd, 64);
+        if (lane >= (uint32_t)dd) inc += t;
+      }
+      if (lane == 63) L.wtot[wid][c] = inc;
+      ex[c] = inc - x;                 // exclusive within the wave
+    }
+    // ALTNUM min / max rides along (hex mode only)
+    ull lo = ~0ull, hi = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+      if (smem(SEG_ALTNUM, R[k], (int)mode)) { lo = altnum[k] < lo ? altnum[k] : lo; hi = altnum[k] > hi ? altnum[k] : hi; }
+    wave_put(L, 44, lo, false);
+    wave_put(L, 45, hi, true);
+    __syncthreads();
+    if (threadIdx.x <= NCNT) {
+      const int c = threadIdx.x;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int w = 0; w < SWAVES; ++w) { const uint32_t t = L.wtot[w][c]; L.wtot[w][c] = acc; acc += t; }
+      L.tot[c] = acc;
+    } else if (threadIdx.x == 64) {
+      ull l2 = L.red[0][44], h2 = L.red[0][45];
+#pragma unroll
+      for (int w = 1; w < SWAVES; ++w) {
+        l2 = L.red[w][44] < l2 ? L.red[w][44] : l2;
+        h2 = L.red[w][45] > h2 ? L.red[w][45] : h2;
+      }
+      L.res[44] = l2;
+      L.res[45] = h2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NCNT; ++c) L.pre[c][threadIdx.x] = (uint16_t)(ex[c] + L.wtot[wid][c]);
+    L.hpre[threadIdx.x] = ex[NCNT] + L.wtot[wid][NCNT];
+  }
+
+  // ---- layout (thread 0) + look-back for the page's place in the block
   if (threadIdx.x == 0) {
+    SwSegPageHdr& H = L.hdr;
     uint32_t off = SEG_PAGE_HDR;
     for (int c = 0; c < SEG_NCOL; ++c) {
-      SwSegCol& cd = L.hdr.cols[c];
-      cd.data_off = off;
+      SwSegCol& cd = H.cols[c];
+      const uint32_t count = L.tot[c];
+      cd.count = (uint16_t)count;
       cd.pad0 = 0;
       cd.pad1 = 0;
+      if (!seg_is_double(c)) {
+        ull lo, hi;
+        if (c == SEG_ALTLEN) {            // remainder lengths: the alt length bounds minus the prefix
+          lo = seg_ord((int64_t)((uint32_t)L.res[2] - pfx));
+          hi = seg_ord((int64_t)((uint32_t)L.res[3] - pfx));
+        } else if (c == SEG_ALTNUM) {
+          lo = L.res[44];
+          hi = L.res[45];
+        } else {
+          lo = L.res[4 + 2 * c];
+          hi = L.res[5 + 2 * c];
+        }
+        cd.base = count ? lo : 0;
+        cd.bits = (uint8_t)(count ? seg_bitwidth(hi - lo) : 0);
+        cd.exp = -1;
+        cd.n_exc = 0;
+      } else {
+        const int d = c - SEG_MXV;
+        const uint32_t ne = L.tot[SEG_NCOL + d];
+        const bool any = count > ne;
+        cd.base = any ? L.res[34 + 2 * d] : 0;
+        cd.bits = (uint8_t)(any ? seg_bitwidth(L.res[35 + 2 * d] - L.res[34 + 2 * d]) : 0);
+        cd.exp = (int8_t)L.exps[d];
+        cd.n_exc = (uint16_t)ne;
+      }
+      cd.data_off = off;
       off += seg_col_bytes(cd.count, cd.bits, cd.n_exc);
     }
-    L.hdr.n_rows = (uint32_t)m;
-    L.hdr.bytes = off;
-    L.hdr.checksum = 0;
-    const ull size = off;
+    const uint32_t heap = pfx + L.tot[NCNT];
+    H.n_rows = (uint32_t)m;
+    H.heap_off = off;
+    H.heap_bytes = heap;
+    H.alt_pfx = (uint8_t)pfx;
+    H.alt_mode = (uint8_t)mode;
+    H.alt_width = (uint8_t)width;
+    H.pad0 = 0;
+    H.asg_max = (int32_t)seg_unord(L.res[5 + 2 * SEG_ASG]);
+    H.date_max = seg_unord(L.res[5 + 2 * SEG_DATE]);
+    H.bytes = off + ((heap + 7u) & ~7u);
+    H.checksum = 0;
+    const ull size = H.bytes;
     ull excl = 0;
     bool failed = false;
     if (page == 0) {
@@ -415,20 +522,151 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   __syncthreads();
   if (L.page_base == ~0ull) return;
   uint8_t* pg = a.out + L.page_base;
-  // ---- C. write the columns
   ull cs = 0;
-  cs ^= seg_write<SEG_ETYPE>(R, valid, L, pre[SEG_ETYPE], xpre[SEG_ETYPE], pg);
-  cs ^= seg_write<SEG_LEVEL>(R, valid, L, pre[SEG_LEVEL], xpre[SEG_LEVEL], pg);
-  cs ^= seg_write<SEG_DATE>(R, valid, L, pre[SEG_DATE], xpre[SEG_DATE], pg);
-  cs ^= seg_write<SEG_ASG>(R, valid, L, pre[SEG_ASG], xpre[SEG_ASG], pg);
-  cs ^= seg_write<SEG_NAME>(R, valid, L, pre[SEG_NAME], xpre[SEG_NAME], pg);
-  cs ^= seg_write<SEG_MXV>(R, valid, L, pre[SEG_MXV], xpre[SEG_MXV], pg);
-  cs ^= seg_write<SEG_LAT>(R, valid, L, pre[SEG_LAT], xpre[SEG_LAT], pg);
-  cs ^= seg_write<SEG_LON>(R, valid, L, pre[SEG_LON], xpre[SEG_LON], pg);
-  cs ^= seg_write<SEG_ELEV>(R, valid, L, pre[SEG_ELEV], xpre[SEG_ELEV], pg);
-  cs ^= seg_write<SEG_HASALT>(R, valid, L, pre[SEG_HASALT], xpre[SEG_HASALT], pg);
-  cs ^= seg_write<SEG_ALT>(R, valid, L, pre[SEG_ALT], xpre[SEG_ALT], pg);
-  // page header words (word 1, the checksum, is written last and not summed)
+
+  // ---- write the columns, two at a time through LDS
+  for (int pr = 0; pr < 8; ++pr) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int c = seg_pairs[pr][g];
+      if (c < 0) break;
+      const SwSegCol& cd = L.hdr.cols[c];
+      uint32_t i = L.pre[c][threadIdx.x];
+      uint32_t x = seg_is_double(c) ? L.pre[SEG_NCOL + (c - SEG_MXV)][threadIdx.x] : 0u;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        if (!smem(c, R[k], (int)mode)) continue;
+        if (!seg_is_double(c)) {
+          L.u.st.vals[g][i] = sval(c, R[k], pfx, altnum[k]) - cd.base;
+        } else {
+          const double v = sdbl(c, R[k]);
+          int64_t q;
+          if (seg_dec_at(v, cd.exp, &q)) {
+            L.u.st.vals[g][i] = seg_ord(q) - cd.base;
+          } else {
+            L.u.st.vals[g][i] = 0;
+            L.u.st.xidx[x] = (uint16_t)i;
+            L.u.st.xraw[x] = sw_f64_bits(v);
+            ++x;
+          }
+        }
+        ++i;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int c = seg_pairs[pr][g];
+      if (c < 0) break;
+      const SwSegCol cd = L.hdr.cols[c];
+      const uint32_t bits = cd.bits, cnt = cd.count;
+      const uint32_t nw = seg_col_words(cnt, (int)bits);
+      for (uint32_t w = threadIdx.x; w < nw; w += SBLK) {
+        ull word = 0;
+        const ull bit0 = (ull)w * 64ull;
+        for (uint32_t j = (uint32_t)(bit0 / bits); j < cnt; ++j) {
+          const ull b = (ull)j * bits;
+          if (b >= bit0 + 64) break;
+          word |= b >= bit0 ? (L.u.st.vals[g][j] << (b - bit0)) : (L.u.st.vals[g][j] >> (bit0 - b));
+        }
+        const uint32_t off = cd.data_off + 8u * w;
+        *reinterpret_cast<ull*>(pg + off) = word;
+        cs ^= seg_mix_word(word, off >> 3);
+      }
+      if (seg_is_double(c) && cd.n_exc) {
+        const uint32_t ne = cd.n_exc;
+        const uint32_t xo = cd.data_off + 8u * nw;
+        const uint32_t nidx = (2u * ne + 7u) / 8u;
+        for (uint32_t w = threadIdx.x; w < nidx; w += SBLK) {
+          ull word = 0;
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j)
+            if (4 * w + j < ne) word |= (ull)L.u.st.xidx[4 * w + j] << (16 * j);
+          *reinterpret_cast<ull*>(pg + xo + 8u * w) = word;
+          cs ^= seg_mix_word(word, (xo >> 3) + w);
+        }
+        const uint32_t ro = xo + 8u * nidx;
+        for (uint32_t j = threadIdx.x; j < ne; j += SBLK) {
+          *reinterpret_cast<ull*>(pg + ro + 8u * j) = L.u.st.xraw[j];
+          cs ^= seg_mix_word(L.u.st.xraw[j], (ro >> 3) + j);
+        }
+      }
+    }
+    __syncthreads();         // the next pair reuses the staging arrays
+  }
+
+  // ---- string heap: row sources into LDS, then a word-parallel gather from the raw batch
+  const uint32_t heap_bytes = L.hdr.heap_bytes;
+  if (heap_bytes) {
+    {
+      uint32_t h = L.hpre[threadIdx.x];
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int idx = RPT * (int)threadIdx.x + k;
+        const SRow& r = R[k];
+        if (idx > m) break;
+        if (idx < m) {
+          L.u.hp.hoff[idx] = h;
+          const uint32_t alen = (mode == SEG_ALT_RAW && (r.s.flags & SEGF_HAS_ALT)) ? r.s.alt_len - pfx : 0u;
+          L.u.hp.src[idx][0] = r.s.alt_off + pfx;
+          L.u.hp.src[idx][1] = r.s.msg_off;
+          L.u.hp.src[idx][2] = r.s.meta_off;
+          L.u.hp.len[idx][0] = (uint16_t)alen;
+          L.u.hp.len[idx][1] = (uint16_t)r.s.msg_len;
+          L.u.hp.len[idx][2] = (uint16_t)r.s.meta_len;
+          h += alen + r.s.msg_len + r.s.meta_len;
+        } else {
+          L.u.hp.hoff[m] = h;           // sentinel: heap bytes after the prefix
+        }
+      }
+      if (m == RPT * SBLK && threadIdx.x == SBLK - 1) L.u.hp.hoff[m] = h;
+    }
+    __syncthreads();
+    const uint32_t hwords = (heap_bytes + 7u) >> 3;
+    const uint32_t hbase = L.hdr.heap_off;
+    for (uint32_t w = threadIdx.x; w < hwords; w += SBLK) {
+      ull word = 0;
+      const uint32_t b0 = 8u * w;
+      // row of the first body byte of the word (binary search over the heap offsets)
+      int row = 0;
+      uint32_t rel = 0;
+      if (b0 + 8u > pfx) {
+        const uint32_t t = b0 > pfx ? b0 - pfx : 0u;
+        int lo = 0, hi = m;                // hoff[lo] <= t < hoff[hi]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (L.u.hp.hoff[mid] <= t) lo = mid; else hi = mid;
+        }
+        row = lo;
+        rel = t - L.u.hp.hoff[row];
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t b = b0 + i;
+        if (b >= heap_bytes) break;
+        uint8_t byte;
+        if (b < pfx) {
+          byte = a.raw[a_off0 + b];
+        } else {
+          // advance to the row / segment holding this byte
+          while (row < m && rel >= (uint32_t)L.u.hp.len[row][0] + L.u.hp.len[row][1] + L.u.hp.len[row][2]) {
+            rel -= (uint32_t)L.u.hp.len[row][0] + L.u.hp.len[row][1] + L.u.hp.len[row][2];
+            ++row;
+          }
+          uint32_t q = rel, seg = 0;
+          while (seg < 2 && q >= L.u.hp.len[row][seg]) { q -= L.u.hp.len[row][seg]; ++seg; }
+          byte = a.raw[L.u.hp.src[row][seg] + q];
+          ++rel;
+        }
+        word |= (ull)byte << (8 * i);
+      }
+      const uint32_t off = hbase + 8u * w;
+      *reinterpret_cast<ull*>(pg + off) = word;
+      cs ^= seg_mix_word(word, off >> 3);
+    }
+  }
+
+  // ---- page header words (word 1, the checksum, is written last and not summed)
   const ull* hw = reinterpret_cast<const ull*>(&L.hdr);
   for (uint32_t i = threadIdx.x; i < SEG_PAGE_HDR / 8; i += SBLK) {
     if (i == 1) continue;
@@ -436,13 +674,14 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     *reinterpret_cast<ull*>(pg + 8u * i) = w;
     cs ^= seg_mix_word(w, i);
   }
-  cs = wave_xor(cs);
-  if (lane64() == 0) L.red.a[threadIdx.x >> 6] = cs;
+  cs = wxor(cs);
+  __syncthreads();
+  if (lane64() == 0) L.red[threadIdx.x >> 6][0] = cs;
   __syncthreads();
   if (threadIdx.x == 0) {
     ull t = 0;
 #pragma unroll
-    for (int w = 0; w < SWAVES; ++w) t ^= L.red.a[w];
+    for (int w = 0; w < SWAVES; ++w) t ^= L.red[w][0];
     *reinterpret_cast<ull*>(pg + 8) = t;
   }
 }
@@ -452,16 +691,20 @@ extern "C" {
 // Encode this step's rows into `out`.  state = u64[max_pages + 4], zeroed here (a memset node when
 // captured); afterwards state[max_pages + 1] = block bytes (~0 on error), state[max_pages + 2] = errors,
 // state[max_pages + 3] = the store sequence of the block's first row.
-int sw_seg_encode(const void* rows, const double* ring_v2, const uint64_t* ring_alt, int64_t store_cap,
-                  const int64_t* cursor, uint8_t* out, int64_t out_cap, uint64_t* state, int64_t max_pages,
-                  hipStream_t s) {
+int sw_seg_encode(const void* rows, const void* work, const uint32_t* ok_idx, const uint32_t* n_ok, const void* gen,
+                  const void* spans, const uint8_t* raw, int64_t raw_bytes, const int64_t* cursor, uint8_t* out,
+                  int64_t out_cap, uint64_t* state, int64_t max_pages, hipStream_t s) {
   hipError_t e = hipMemsetAsync(state, 0, sizeof(uint64_t) * (size_t)(max_pages + 4), s);
   if (e != hipSuccess) return (int)e;
   SwSegArgs a;
   a.rows = (const SwOutRec*)rows;
-  a.ring_v2 = ring_v2;
-  a.ring_alt = ring_alt;
-  a.store_cap = store_cap;
+  a.work = (const SwEventRec*)work;
+  a.ok_idx = ok_idx;
+  a.n_ok = n_ok;
+  a.gen = (const SwEventRec*)gen;
+  a.spans = (const SwStrRef*)spans;
+  a.raw = raw;
+  a.raw_bytes = raw ? raw_bytes : 0;
   a.cursor = cursor;
   a.out = out;
   a.out_cap = out_cap;

@@ -186,6 +186,8 @@ typedef struct SwEngineArgs {
   // ---------------------------------------------------------------- dedup generations
   int64_t* dd_meta;            // [generation, ids in the current table, rotate flag, pad]; dd_key / dd_seq
                                // hold two tables of dd_mask + 1 slots (current = dd_meta[0])
+  // ---------------------------------------------------------------- string refs
+  SwStrRef* spans;             // [rec_cap] per decoded record (decode writes, the block encoder reads)
 } SwEngineArgs;
 
 enum {

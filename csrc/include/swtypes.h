@@ -37,6 +37,10 @@ enum SwEventType : uint8_t {
   SW_EV_STREAM_CREATE = 18,
   SW_EV_STREAM_DATA = 19,
   SW_EV_STREAM_DATA_REQUEST = 20,
+  // an event whose alternate id, alert message or metadata span does not fit the engine's 16-bit
+  // string lengths: handed to the host like a control message, which forwards the payload to the
+  // per-event path (decoded-events topic) -- stored losslessly there instead of truncated here
+  SW_EV_OVERSIZE = 21,
   SW_EV_DECODE_ERROR = 255,
 };
 
@@ -77,6 +81,25 @@ typedef struct __attribute__((aligned(16))) SwEventRec {
   uint8_t src_rank;     // 78 rank whose raw batch holds the aux bytes
   uint8_t level;        // 79 alert level (GAlertLevel)
 } SwEventRec;
+
+// Where the strings of a decoded event sit in its raw batch (written by the decoder beside each
+// record, read by the durable-block encoder, csrc/include/swseg.h): the alternate id, the span of
+// the body's metadata entries (first entry's tag to the last entry's end, wire bytes), and which
+// measurement of a multi-measurement payload the record is.  The alert message is the record's
+// aux2 string.  Offsets are absolute in the batch; lengths fit 16 bits (SW_EV_OVERSIZE otherwise).
+// Reference fields: alternateId and metadata of every event (MongoDeviceEvent.java:64-82).
+typedef struct __attribute__((aligned(16))) SwStrRef {
+  uint32_t alt_off;
+  uint32_t meta_off;
+  uint16_t alt_len;
+  uint16_t meta_len;
+  uint16_t k;           // measurement index within its payload
+  uint8_t has;          // SW_SR_* bits
+  uint8_t pad;
+} SwStrRef;
+#define SW_SR_ALT 0x1     // the body carries an alternate id
+#define SW_SR_META 0x2    // the body carries metadata entries
+#define SW_SR_MULTI 0x4   // the payload has more than one measurement: alternate id "<alt>:<k>"
 
 // Exchange form of a decoded record, 64 bytes: what crosses xGMI in the owner all-to-all.  The
 // 80-byte record carries fields no event type uses together, so the exchange packs them
@@ -189,6 +212,20 @@ SW_HD uint64_t sw_hash64(const uint8_t* p, uint32_t n) {
   uint64_t a = SW_FNV_OFFSET;
   for (uint32_t i = 0; i < n; ++i) a = (a ^ p[i]) * SW_FNV_PRIME;
   a = sw_mix64(a ^ ((uint64_t)n << 56));
+  return a ? a : 1;
+}
+
+// sw_hash64 of the string p[0..n) + ":" + decimal(k) without building it: the alternate id of
+// measurement k of a multi-measurement payload (the per-event path names it "<alt>:<k>",
+// services/event_sources.py), so both paths deduplicate and index the same ids.
+SW_HD uint64_t sw_hash64_sfx(const uint8_t* p, uint32_t n, uint32_t k) {
+  uint64_t a = SW_FNV_OFFSET;
+  for (uint32_t i = 0; i < n; ++i) a = (a ^ p[i]) * SW_FNV_PRIME;
+  a = (a ^ (uint8_t)':') * SW_FNV_PRIME;
+  uint32_t div = 1, nd = 1;
+  while (k / div >= 10u) { div *= 10u; ++nd; }
+  for (; div; div /= 10u) a = (a ^ (uint8_t)('0' + (k / div) % 10u)) * SW_FNV_PRIME;
+  a = sw_mix64(a ^ ((uint64_t)(n + 1u + nd) << 56));
   return a ? a : 1;
 }
 

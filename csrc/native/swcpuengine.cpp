@@ -314,10 +314,16 @@ static inline bool pip(const double* v, int32_t n, double x, double y) {
 template <typename AsgOf>
 static void persist_range(const SwCpuEngine* e, const SwCeTables* t, const SwEventRec* recs, const int64_t* idx,
                           const int32_t* dev, AsgOf asg_of, int64_t cursor, int64_t now_ms, SwOutRec* out, int64_t b,
-                          int64_t end) {
+                          int64_t end, const SwStrRef* spans, SwEventRec* prec, SwStrRef* pspans) {
   int64_t row = (cursor + b) % t->store_cap;
   for (int64_t j = b; j < end; ++j) {
     const SwEventRec& r = recs[idx ? idx[j] : j];
+    // the persisted record and its string refs, row-aligned with `out` (durable-block encoder input)
+    if (prec) prec[j] = r;
+    if (pspans) {
+      if (spans) pspans[j] = spans[idx ? idx[j] : j];
+      else memset(&pspans[j], 0, sizeof(SwStrRef));
+    }
     const int32_t a = asg_of(j);
     const SwCeCtx c = t->ctx[a];
     t->s_etype[row] = r.etype;
@@ -452,8 +458,11 @@ int64_t swce_capture_names(void* p, const SwEventRec* recs, int64_t n, uint8_t* 
 
 // One process phase over the (already exchanged) work records.  status [n] receives each record's
 // validation outcome; out [n + gen_cap] the enriched rows (persisted first, then generated).
+// spans [n] (nullable): the work records' string refs; prec / pspans [n + gen_cap] (nullable) receive
+// the persisted records and their string refs, row-aligned with out.
 int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRec* work, int64_t n, int64_t now_ms,
-                     int32_t presence, uint8_t* status, SwOutRec* out) {
+                     int32_t presence, uint8_t* status, SwOutRec* out, const SwStrRef* spans, SwEventRec* prec,
+                     SwStrRef* pspans) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
   const int T = e->T();
   static const bool trace = getenv("SW_CE_TRACE") != nullptr;
@@ -572,7 +581,8 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   e->pool.run([&](int w) {
     int64_t b, end;
     chunk_of(n_ok, w, T, &b, &end);
-    persist_range(e, t, work, ok_idx, dev, [&](int64_t j) { return asg[ok_idx[j]]; }, cursor0, now_ms, out, b, end);
+    persist_range(e, t, work, ok_idx, dev, [&](int64_t j) { return asg[ok_idx[j]]; }, cursor0, now_ms, out, b, end,
+                  spans, prec, pspans);
     if (T > 1) {
       for (int sh = 0; sh < T; ++sh) e->lists[(size_t)w * T + sh].clear();
       for (int64_t j = b; j < end; ++j) e->lists[(size_t)w * T + (uint32_t)out[j].assignment % (uint32_t)T].push_back((int32_t)j);
@@ -680,7 +690,7 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
       int64_t b, end;
       chunk_of(n_gen, w, T, &b, &end);
       persist_range(e, t, gen.data(), nullptr, nullptr, [&](int64_t j) { return gen_asg[j]; }, cursor, now_ms, gout, b,
-                    end);
+                    end, nullptr, prec ? prec + n_ok : nullptr, pspans ? pspans + n_ok : nullptr);
     });
     e->pool.run([&](int sh) {
       for (int64_t j = 0; j < n_gen; ++j)

@@ -49,6 +49,11 @@ void sw_hash64_batch(const uint8_t* heap, const int64_t* offs, int64_t n, uint64
   for (int64_t i = 0; i < n; ++i) out[i] = sw_hash64(heap + offs[i], (uint32_t)(offs[i + 1] - offs[i]));
 }
 
+// sw_hash64 of heap[start[i], end[i]) (strings decoded from durable blocks).
+void sw_hash64_ranges(const uint8_t* heap, const int64_t* start, const int64_t* end, int64_t n, uint64_t* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = sw_hash64(heap + start[i], (uint32_t)(end[i] - start[i]));
+}
+
 // Kafka's default partitioner hash (murmur2, seed 0x9747b28c).
 int32_t sw_murmur2(const uint8_t* data, int32_t length) {
   const uint32_t seed = 0x9747b28c, m = 0x5bd1e995;
@@ -151,7 +156,7 @@ int64_t sw_reg_build(uint64_t* tlo, uint64_t* thi, int32_t* tval, int64_t mask, 
 // ============================================================================ CPU decode
 // Two-pass (count, scan, emit) exactly like the GPU path; parallel over message ranges.
 int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, int64_t now_ms, int32_t rank,
-                      SwEventRec* out, int64_t cap, int32_t n_threads) {
+                      SwEventRec* out, SwStrRef* spans, int64_t cap, int32_t n_threads) {
   if (n_msgs <= 0) return 0;
   std::vector<uint32_t> cnt(n_msgs), verdict(n_msgs, SW_DEC_UNKNOWN);   // verdicts: as the GPU passes
   if (n_threads < 1) n_threads = 1;
@@ -176,7 +181,7 @@ int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, i
       int64_t o = pre[m];
       if (o >= cap) continue;
       sw_decode_payload(raw, off[m], off[m + 1], 0, now_ms, (uint8_t)rank, out + o,
-                        (uint32_t)std::min<int64_t>(cap - o, 0xffffffffll), &verdict[m]);
+                        (uint32_t)std::min<int64_t>(cap - o, 0xffffffffll), &verdict[m], spans ? spans + o : nullptr);
     }
   });
   return std::min<int64_t>(pre[n_msgs], cap);
@@ -198,10 +203,12 @@ static inline uint64_t xs64(uint64_t& s) { s ^= s << 13; s ^= s >> 7; s ^= s << 
 // kinds: 0 measurement, 1 location, 2 alert, 3 registration (control)
 // Generates n messages into a caller buffer; returns bytes written or -needed if too small.
 // Device tokens are "<prefix><index zero-padded to 10>"; unregistered devices use indices >= n_devices.
+// p_meta: share of events carrying metadata (firmware version + gateway, 2 Metadata entries); alert
+// messages vary per event ("<type> threshold exceeded: <reading>").
 int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, double p_loc, double p_alert,
                         double p_unreg, int32_t mx_per_msg, int32_t n_names, int64_t ts0, uint64_t seed,
-                        int32_t with_alt_id, double lat0, double lon0, double span_deg, uint8_t* out, int64_t out_cap,
-                        uint32_t* offs) {
+                        int32_t with_alt_id, double lat0, double lon0, double span_deg, double p_meta, uint8_t* out,
+                        int64_t out_cap, uint32_t* offs) {
   std::vector<uint8_t> buf;
   buf.reserve(96);
   Enc e{buf};
@@ -232,6 +239,29 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
     if (with_alt_id)
       alen = (size_t)snprintf(alt, sizeof(alt), "%016llx-%08llx", (unsigned long long)seed,
                               (unsigned long long)(m & 0xffffffffLL));
+    // metadata entries (field 4 / 6 / 5 by event type), emitted before the alternate id
+    const bool meta = p_meta > 0 && (double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0) < p_meta;
+    char fw[16], gw[16];
+    int fwl = 0, gwl = 0;
+    if (meta) {
+      fwl = snprintf(fw, sizeof(fw), "1.%d.%d", (int)(dev % 5), (int)(dev % 17));
+      gwl = snprintf(gw, sizeof(gw), "gw-%04d", (int)(dev % 1000));
+    }
+    auto put_meta = [&](uint32_t field) {
+      if (!meta) return;
+      const char* keys[2] = {"fw", "gw"};
+      const char* vals[2] = {fw, gw};
+      const int vl[2] = {fwl, gwl};
+      for (int q = 0; q < 2; ++q) {
+        std::vector<uint8_t> md;
+        Enc emd{md};
+        emd.str(1, keys[q], 2);
+        emd.str(2, vals[q], (size_t)vl[q]);
+        eb.key(field, 2);
+        eb.varint(md.size());
+        body.insert(body.end(), md.begin(), md.end());
+      }
+    };
     if (u < p_loc) {
       cmd = SW_CMD_SEND_DEVICE_LOCATION;
       eb.str(1, tok, tlen);
@@ -240,14 +270,19 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
       eb.dbl(3, std::nearbyint((lon0 + span_deg * ((double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0))) * 1e6) / 1e6);
       eb.dbl(4, 10.0);
       eb.fixed64(5, (uint64_t)ts);
+      put_meta(6);
     } else if (u < p_loc + p_alert) {
       cmd = SW_CMD_SEND_DEVICE_ALERT;
       eb.str(1, tok, tlen);
       int k = (int)(xs64(s) % 4);
       int nl = snprintf(name, sizeof(name), "alert.type%d", k);
       eb.str(2, name, (size_t)nl);
-      eb.str(3, "threshold exceeded", 18);
+      char msg[64];
+      const int ml = snprintf(msg, sizeof(msg), "%s threshold exceeded: %.1f", name,
+                              (double)(xs64(s) % 10000ULL) / 10.0);
+      eb.str(3, msg, (size_t)ml);
       eb.fixed64(4, (uint64_t)ts);
+      put_meta(5);
     } else {
       cmd = SW_CMD_SEND_DEVICE_MEASUREMENTS;
       eb.str(1, tok, tlen);
@@ -262,6 +297,7 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
         body.insert(body.end(), mx.begin(), mx.end());
       }
       eb.fixed64(3, (uint64_t)ts);
+      put_meta(4);
     }
     if (alen) eb.str(SW_FIELD_ALTERNATE_ID, alt, alen);
     // header

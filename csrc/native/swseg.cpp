@@ -45,45 +45,111 @@ namespace {
 inline uint32_t rd8(uint32_t x) { return (x + 7u) & ~7u; }
 
 // ----------------------------------------------------------------------------- encoder
+// One row as the encoder sees it: the enriched outbound row, its record's elevation and strings.
+struct Row {
+  SwOutRec o;
+  double v2;
+  SegRowStr s;
+};
+
 struct ColPlan {
   uint64_t base = 0;
   uint32_t count = 0, n_exc = 0;
   int bits = 0, exp = -1;
 };
 
-// Order-preserving unsigned value of column c for row i (integer columns).
-inline uint64_t int_value(int c, const SwOutRec& r, uint64_t alt) {
+struct PageEnc {
+  ColPlan plan[SEG_NCOL];
+  uint32_t heap_off = 0, heap_bytes = 0, bytes = 0;
+  uint32_t pfx = 0, mode = SEG_ALT_RAW, width = 0;
+  int64_t pfx_src = 0;        // raw offset of the prefix bytes (the page's first alternate id)
+  int32_t asg_max = 0;
+  int64_t date_max = 0;
+};
+
+// Exponent search start per double column (a hint only: the result is seg_dec_exp's exponent).
+inline int exp_hint(int c) { return c == SEG_MXV ? 2 : c == SEG_ELEV ? 1 : 6; }
+
+inline double dbl_value(int c, const Row& r) {
+  return c == SEG_MXV || c == SEG_LAT ? r.o.v0 : c == SEG_LON ? r.o.v1 : r.v2;
+}
+
+// Order-preserving unsigned value of integer column c (ALTNUM is filled by the caller).
+inline uint64_t int_value(int c, const Row& r, uint32_t pfx, uint64_t altnum) {
   switch (c) {
-    case SEG_ETYPE: return seg_ord((int64_t)r.etype);
-    case SEG_LEVEL: return seg_ord((int64_t)r.level);
-    case SEG_DATE: return seg_ord(r.event_date);
-    case SEG_ASG: return seg_ord((int64_t)r.assignment);
-    case SEG_NAME: return seg_ord((int64_t)r.name_id);
-    case SEG_HASALT: return seg_ord(alt != 0 ? 1 : 0);
-    case SEG_ALT: return alt;          // a hash: already unsigned, stored as is
+    case SEG_ETYPE: return seg_ord((int64_t)r.o.etype);
+    case SEG_LEVEL: return seg_ord((int64_t)r.o.level);
+    case SEG_DATE: return seg_ord(r.o.event_date);
+    case SEG_ASG: return seg_ord((int64_t)r.o.assignment);
+    case SEG_NAME: return seg_ord((int64_t)r.o.name_id);
+    case SEG_FLAGS: return seg_ord((int64_t)r.s.flags);
+    case SEG_ALTK: return seg_ord((int64_t)r.s.altk);
+    case SEG_ALTLEN: return seg_ord((int64_t)(r.s.alt_len - pfx));
+    case SEG_ALTNUM: return altnum;
+    case SEG_MSGLEN: return seg_ord((int64_t)r.s.msg_len);
+    case SEG_METALEN: return seg_ord((int64_t)r.s.meta_len);
     default: return 0;
   }
 }
 
-inline double dbl_value(int c, const SwOutRec& r, double v2) {
-  return c == SEG_MXV || c == SEG_LAT ? r.v0 : c == SEG_LON ? r.v1 : v2;
+// hex value of an alternate id's remainder (hex-mode pages only)
+inline uint64_t alt_hex(const uint8_t* raw, const Row& r, uint32_t pfx) {
+  uint64_t v = 0;
+  for (uint32_t i = pfx; i < r.s.alt_len; ++i) v = (v << 4) | seg_hex_value(raw[r.s.alt_off + i]);
+  return v;
 }
 
-struct PageEnc {
-  ColPlan plan[SEG_NCOL];
-  uint32_t bytes = 0;
-};
-
-void plan_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t r0, int m, PageEnc* pe) {
+void plan_page(const Row* R, int m, const uint8_t* raw, PageEnc* pe, std::vector<uint64_t>& altnum) {
+  // alternate ids: common prefix with the page's first one, then hex mode if every remainder is a
+  // fixed-width lowercase hex number
+  int first = -1;
+  for (int k = 0; k < m; ++k)
+    if (R[k].s.flags & SEGF_HAS_ALT) { first = k; break; }
+  pe->pfx = 0;
+  pe->mode = SEG_ALT_RAW;
+  pe->width = 0;
+  pe->pfx_src = 0;
+  if (first >= 0) {
+    const uint8_t* a0 = raw + R[first].s.alt_off;
+    uint32_t p = std::min<uint32_t>(R[first].s.alt_len, SEG_ALT_PFX_MAX);
+    uint32_t wmin = 0xffffffffu, wmax = 0;
+    bool hex = true;
+    for (int k = first; k < m; ++k) {
+      if (!(R[k].s.flags & SEGF_HAS_ALT)) continue;
+      const uint8_t* a = raw + R[k].s.alt_off;
+      uint32_t l = 0;
+      const uint32_t lim = std::min(p, R[k].s.alt_len);
+      while (l < lim && a[l] == a0[l]) ++l;
+      p = l;
+    }
+    for (int k = first; k < m; ++k) {
+      if (!(R[k].s.flags & SEGF_HAS_ALT)) continue;
+      const uint32_t w = R[k].s.alt_len - p;
+      wmin = std::min(wmin, w);
+      wmax = std::max(wmax, w);
+      const uint8_t* a = raw + R[k].s.alt_off;
+      for (uint32_t i = p; i < R[k].s.alt_len && hex; ++i) hex = seg_is_hex_digit(a[i]);
+    }
+    pe->pfx = p;
+    pe->pfx_src = R[first].s.alt_off;
+    if (hex && wmin == wmax && wmin >= 1 && wmin <= 16) {
+      pe->mode = SEG_ALT_HEX;
+      pe->width = wmin;
+    }
+  }
+  altnum.assign((size_t)m, 0);
+  if (pe->mode == SEG_ALT_HEX)
+    for (int k = 0; k < m; ++k)
+      if (R[k].s.flags & SEGF_HAS_ALT) altnum[k] = alt_hex(raw, R[k], pe->pfx);
   uint32_t off = SEG_PAGE_HDR;
   for (int c = 0; c < SEG_NCOL; ++c) {
     ColPlan& p = pe->plan[c];
     if (!seg_is_double(c)) {
       uint64_t lo = ~0ull, hi = 0;
       for (int k = 0; k < m; ++k) {
-        const SwOutRec& r = R[r0 + k];
-        if (!seg_member(c, r.etype, A[r0 + k])) continue;
-        const uint64_t u = int_value(c, r, A[r0 + k]);
+        const Row& r = R[k];
+        if (!seg_member(c, r.o.etype, r.s.flags, (int)pe->mode)) continue;
+        const uint64_t u = int_value(c, r, pe->pfx, altnum[k]);
         lo = std::min(lo, u);
         hi = std::max(hi, u);
         ++p.count;
@@ -94,18 +160,18 @@ void plan_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t r
     } else {
       int e = 0;
       for (int k = 0; k < m; ++k) {
-        const SwOutRec& r = R[r0 + k];
-        if (!seg_member(c, r.etype, A[r0 + k])) continue;
+        const Row& r = R[k];
+        if (!seg_member(c, r.o.etype, r.s.flags, (int)pe->mode)) continue;
         ++p.count;
-        const int ei = seg_dec_exp(dbl_value(c, r, V2[r0 + k]));
+        const int ei = seg_dec_exp_from(dbl_value(c, r), exp_hint(c));
         if (ei != SEG_EXC_NONE && ei > e) e = ei;
       }
       uint64_t lo = ~0ull, hi = 0;
       for (int k = 0; k < m; ++k) {
-        const SwOutRec& r = R[r0 + k];
-        if (!seg_member(c, r.etype, A[r0 + k])) continue;
+        const Row& r = R[k];
+        if (!seg_member(c, r.o.etype, r.s.flags, (int)pe->mode)) continue;
         int64_t q;
-        if (seg_dec_at(dbl_value(c, r, V2[r0 + k]), e, &q)) {
+        if (seg_dec_at(dbl_value(c, r), e, &q)) {
           lo = std::min(lo, seg_ord(q));
           hi = std::max(hi, seg_ord(q));
         } else {
@@ -119,7 +185,21 @@ void plan_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t r
     }
     off += seg_col_bytes(p.count, p.bits, p.n_exc);
   }
-  pe->bytes = off;
+  uint32_t heap = pe->pfx;
+  int32_t amax = INT32_MIN;
+  int64_t dmax = INT64_MIN;
+  for (int k = 0; k < m; ++k) {
+    const Row& r = R[k];
+    if (pe->mode == SEG_ALT_RAW && (r.s.flags & SEGF_HAS_ALT)) heap += r.s.alt_len - pe->pfx;
+    heap += r.s.msg_len + r.s.meta_len;
+    amax = std::max(amax, r.o.assignment);
+    dmax = std::max(dmax, r.o.event_date);
+  }
+  pe->heap_off = off;
+  pe->heap_bytes = heap;
+  pe->bytes = off + rd8(heap);
+  pe->asg_max = m ? amax : 0;
+  pe->date_max = m ? dmax : 0;
 }
 
 struct WordSink {
@@ -131,7 +211,7 @@ struct WordSink {
   }
 };
 
-void write_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t r0, int m, const PageEnc& pe,
+void write_page(const Row* R, int m, const uint8_t* raw, const PageEnc& pe, const std::vector<uint64_t>& altnum,
                 uint8_t* page) {
   WordSink ws{page};
   std::vector<uint64_t> vals(SEG_PAGE_ROWS);
@@ -141,6 +221,13 @@ void write_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t 
   memset(&hdr, 0, sizeof(hdr));
   hdr.n_rows = (uint32_t)m;
   hdr.bytes = pe.bytes;
+  hdr.heap_off = pe.heap_off;
+  hdr.heap_bytes = pe.heap_bytes;
+  hdr.alt_pfx = (uint8_t)pe.pfx;
+  hdr.alt_mode = (uint8_t)pe.mode;
+  hdr.alt_width = (uint8_t)pe.width;
+  hdr.asg_max = pe.asg_max;
+  hdr.date_max = pe.date_max;
   uint32_t off = SEG_PAGE_HDR;
   for (int c = 0; c < SEG_NCOL; ++c) {
     const ColPlan& p = pe.plan[c];
@@ -153,12 +240,12 @@ void write_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t 
     cd.exp = (int8_t)p.exp;
     uint32_t n = 0, ne = 0;
     for (int k = 0; k < m; ++k) {
-      const SwOutRec& r = R[r0 + k];
-      if (!seg_member(c, r.etype, A[r0 + k])) continue;
+      const Row& r = R[k];
+      if (!seg_member(c, r.o.etype, r.s.flags, (int)pe.mode)) continue;
       if (!seg_is_double(c)) {
-        vals[n++] = int_value(c, r, A[r0 + k]) - p.base;
+        vals[n++] = int_value(c, r, pe.pfx, altnum[k]) - p.base;
       } else {
-        const double v = dbl_value(c, r, V2[r0 + k]);
+        const double v = dbl_value(c, r);
         int64_t q;
         if (seg_dec_at(v, p.exp, &q)) {
           vals[n] = seg_ord(q) - p.base;
@@ -199,6 +286,25 @@ void write_page(const SwOutRec* R, const double* V2, const uint64_t* A, int64_t 
       for (uint32_t j = 0; j < ne; ++j) ws.put(off + 8 * j, exc_raw[j]);
       off += 8 * ne;
     }
+  }
+  // string heap (zero padded to a word)
+  std::vector<uint8_t> heap(rd8(pe.heap_bytes), 0);
+  uint32_t h = 0;
+  if (pe.pfx) memcpy(heap.data(), raw + pe.pfx_src, pe.pfx);
+  h = pe.pfx;
+  for (int k = 0; k < m; ++k) {
+    const SegRowStr& s = R[k].s;
+    if (pe.mode == SEG_ALT_RAW && (s.flags & SEGF_HAS_ALT)) {
+      memcpy(heap.data() + h, raw + s.alt_off + pe.pfx, s.alt_len - pe.pfx);
+      h += s.alt_len - pe.pfx;
+    }
+    if (s.msg_len) { memcpy(heap.data() + h, raw + s.msg_off, s.msg_len); h += s.msg_len; }
+    if (s.meta_len) { memcpy(heap.data() + h, raw + s.meta_off, s.meta_len); h += s.meta_len; }
+  }
+  for (uint32_t w = 0; w < heap.size() / 8; ++w) {
+    uint64_t word;
+    memcpy(&word, heap.data() + 8 * w, 8);
+    ws.put(pe.heap_off + 8 * w, word);
   }
   // header words (the checksum word, index 1, is excluded)
   uint64_t hw[sizeof(SwSegPageHdr) / 8];
@@ -241,22 +347,45 @@ uint64_t unpack(const uint8_t* words, uint32_t i, int bits) {
   return bits == 64 ? v : (v & ((1ull << bits) - 1));
 }
 
+inline uint64_t col_int(const uint8_t* pg, const SwSegCol& cd, uint32_t i) {
+  return cd.base + unpack(pg + cd.data_off, i, cd.bits);
+}
+
 }  // namespace
 
 extern "C" {
 
-// Encode n rows (step order) into `out` (cap bytes).  Writes the block's n_rows / n_pages / bytes
-// and the page table; swseg_seal fills the rest of the header.  Returns the block bytes, or
-// -(bytes needed) when cap is too small.
-int64_t swseg_encode(const SwOutRec* rows, const double* v2, const uint64_t* alt, int64_t n, uint8_t* out,
-                     int64_t cap) {
+// Encode n rows (step order) into `out` (cap bytes).  rows[j] = the enriched row, recs[j] / spans[j]
+// = its decoded record and string refs (may be null: rows without record carry no strings, no
+// elevation, no flags), raw = the batch the records were decoded from (raw_bytes long; may be
+// null when no row has strings).  Writes the block's n_rows / n_pages / bytes and the page table;
+// swseg_seal fills the rest of the header.  Returns the block bytes, or -(bytes needed) when cap is
+// too small.
+int64_t swseg_encode(const SwOutRec* rows, const SwEventRec* recs, const SwStrRef* spans, const uint8_t* raw,
+                     int64_t raw_bytes, int64_t n, uint8_t* out, int64_t cap) {
   const int64_t np = (n + SEG_PAGE_ROWS - 1) / SEG_PAGE_ROWS;
+  std::vector<Row> R((size_t)n);
+  SwEventRec zr;
+  memset(&zr, 0, sizeof(zr));
+  SwStrRef zs;
+  memset(&zs, 0, sizeof(zs));
+  for (int64_t j = 0; j < n; ++j) {
+    R[j].o = rows[j];
+    const SwEventRec& r = recs ? recs[j] : zr;
+    R[j].v2 = recs ? r.v2 : 0.0;
+    if (recs) {
+      R[j].s = seg_row_strings(r, spans ? spans[j] : zs, raw ? raw_bytes : 0);
+    } else {
+      memset(&R[j].s, 0, sizeof(R[j].s));
+    }
+  }
   std::vector<PageEnc> pe((size_t)np);
+  std::vector<std::vector<uint64_t>> altnum((size_t)np);
   const uint32_t start = 64 + rd8(4u * (uint32_t)(np + 1));
   uint64_t total = start;
   for (int64_t p = 0; p < np; ++p) {
     const int m = (int)std::min<int64_t>(SEG_PAGE_ROWS, n - p * SEG_PAGE_ROWS);
-    plan_page(rows, v2, alt, p * SEG_PAGE_ROWS, m, &pe[(size_t)p]);
+    plan_page(R.data() + p * SEG_PAGE_ROWS, m, raw, &pe[(size_t)p], altnum[(size_t)p]);
     total += pe[(size_t)p].bytes;
   }
   if ((int64_t)total > cap) return -(int64_t)total;
@@ -266,7 +395,7 @@ int64_t swseg_encode(const SwOutRec* rows, const double* v2, const uint64_t* alt
   for (int64_t p = 0; p < np; ++p) {
     pt[p] = (uint32_t)off;
     const int m = (int)std::min<int64_t>(SEG_PAGE_ROWS, n - p * SEG_PAGE_ROWS);
-    write_page(rows, v2, alt, p * SEG_PAGE_ROWS, m, pe[(size_t)p], out + off);
+    write_page(R.data() + p * SEG_PAGE_ROWS, m, raw, pe[(size_t)p], altnum[(size_t)p], out + off);
     off += pe[(size_t)p].bytes;
   }
   pt[np] = (uint32_t)off;
@@ -341,39 +470,64 @@ int32_t swseg_verify(const uint8_t* b, int64_t len) {
       const SwSegCol& cd = ph.cols[c];
       if (cd.bits > 64 || cd.data_off + seg_col_bytes(cd.count, cd.bits, cd.n_exc) > ph.bytes) return 3;
     }
+    if ((uint64_t)ph.heap_off + ph.heap_bytes > ph.bytes || ph.alt_mode > SEG_ALT_HEX || ph.alt_pfx > ph.heap_bytes ||
+        ph.alt_width > 16)
+      return 3;
   }
   return 0;
 }
 
-// Decode a (verified) block into per-row arrays of n_rows entries.  Any output may be null.
-// name = 0xffff where the row has none; v0/v1/v2 = 0 where the type has no such value.
-int64_t swseg_decode(const uint8_t* b, uint8_t* etype, uint8_t* level, int64_t* date, int32_t* asg, uint16_t* name,
-                     double* v0, double* v1, double* v2, uint64_t* alt) {
+// Upper bound of the string bytes swseg_decode writes for pages [p0, p1).
+int64_t swseg_string_bytes(const uint8_t* b, int64_t p0, int64_t p1) {
   SwSegBlockHdr h;
   memcpy(&h, b, sizeof(h));
   const uint32_t* pt = (const uint32_t*)(b + 64);
+  if (p1 > (int64_t)h.n_pages) p1 = h.n_pages;
+  int64_t total = 0;
+  for (int64_t p = p0; p < p1; ++p) {
+    SwSegPageHdr ph;
+    memcpy(&ph, b + pt[p], sizeof(ph));
+    total += ph.heap_bytes + (int64_t)ph.n_rows * (SEG_ALT_PFX_MAX + 16 + 8);
+  }
+  return total;
+}
+
+// Decode pages [p0, p1) of a (verified) block into per-row arrays (row 0 = the first row of page p0).
+// Any output may be null.  name = 0xffff where the row has none; v0/v1/v2 = 0 where the type has no
+// such value (flags tell whether an elevation was sent).  Strings (str_heap non-null, str_cap bytes,
+// see swseg_string_bytes): per row its alternate id (full form, "<alt>:<k>" for measurement k of a
+// multi-measurement payload), alert message and metadata span, back to back; str_off[3 r + 0..3]
+// delimit them.  Returns the rows decoded, -1 if str_cap is too small.
+int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, uint8_t* level, int64_t* date,
+                     int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2, uint8_t* flags,
+                     uint8_t* str_heap, int64_t str_cap, int64_t* str_off) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  if (p1 > (int64_t)h.n_pages) p1 = h.n_pages;
   std::vector<uint8_t> et(SEG_PAGE_ROWS);
+  std::vector<uint32_t> fl(SEG_PAGE_ROWS);
   std::vector<double> dv(SEG_PAGE_ROWS);
-  for (uint32_t p = 0; p < h.n_pages; ++p) {
+  std::vector<uint64_t> ak(SEG_PAGE_ROWS), al(SEG_PAGE_ROWS), an(SEG_PAGE_ROWS), ml(SEG_PAGE_ROWS),
+      dl(SEG_PAGE_ROWS);
+  int64_t r0 = 0, so = 0;
+  if (str_off) str_off[0] = 0;
+  for (int64_t p = p0; p < p1; ++p) {
     const uint8_t* pg = b + pt[p];
     SwSegPageHdr ph;
     memcpy(&ph, pg, sizeof(ph));
-    const int64_t r0 = (int64_t)p * SEG_PAGE_ROWS;
     const uint32_t m = ph.n_rows;
-    // etype first: every other column's membership depends on it
-    {
-      const SwSegCol& cd = ph.cols[SEG_ETYPE];
-      for (uint32_t k = 0; k < m; ++k)
-        et[k] = (uint8_t)seg_unord(cd.base + unpack(pg + cd.data_off, k, cd.bits));
-      if (etype) memcpy(etype + r0, et.data(), m);
+    const int mode = ph.alt_mode;
+    // etype and flags first: every other column's membership depends on them
+    for (uint32_t k = 0; k < m; ++k) {
+      et[k] = (uint8_t)seg_unord(col_int(pg, ph.cols[SEG_ETYPE], k));
+      fl[k] = (uint32_t)seg_unord(col_int(pg, ph.cols[SEG_FLAGS], k));
     }
-    std::vector<uint64_t> has(m, 0);
-    {
-      const SwSegCol& cd = ph.cols[SEG_HASALT];
-      for (uint32_t k = 0; k < m; ++k) has[k] = (uint64_t)seg_unord(cd.base + unpack(pg + cd.data_off, k, cd.bits));
-    }
+    if (etype) memcpy(etype + r0, et.data(), m);
+    if (flags)
+      for (uint32_t k = 0; k < m; ++k) flags[r0 + k] = (uint8_t)fl[k];
     for (int c = 0; c < SEG_NCOL; ++c) {
-      if (c == SEG_ETYPE || c == SEG_HASALT) continue;
+      if (c == SEG_ETYPE || c == SEG_FLAGS) continue;
       const SwSegCol& cd = ph.cols[c];
       const uint8_t* words = pg + cd.data_off;
       if (seg_is_double(c)) {
@@ -392,19 +546,20 @@ int64_t swseg_decode(const uint8_t* b, uint8_t* etype, uint8_t* level, int64_t* 
       uint32_t i = 0;
       for (uint32_t k = 0; k < m; ++k) {
         const int64_t r = r0 + k;
-        const bool mem = seg_member(c, et[k], c == SEG_ALT ? has[k] : 0);
+        const bool mem = seg_member(c, et[k], fl[k], mode);
+        const uint64_t u = mem && !seg_is_double(c) ? cd.base + unpack(words, i, cd.bits) : 0;
         switch (c) {
           case SEG_LEVEL:
-            if (level) level[r] = mem ? (uint8_t)seg_unord(cd.base + unpack(words, i, cd.bits)) : 0;
+            if (level) level[r] = mem ? (uint8_t)seg_unord(u) : 0;
             break;
           case SEG_DATE:
-            if (date) date[r] = seg_unord(cd.base + unpack(words, i, cd.bits));
+            if (date) date[r] = seg_unord(u);
             break;
           case SEG_ASG:
-            if (asg) asg[r] = (int32_t)seg_unord(cd.base + unpack(words, i, cd.bits));
+            if (asg) asg[r] = (int32_t)seg_unord(u);
             break;
           case SEG_NAME:
-            if (name) name[r] = mem ? (uint16_t)seg_unord(cd.base + unpack(words, i, cd.bits)) : (uint16_t)0xffff;
+            if (name) name[r] = mem ? (uint16_t)seg_unord(u) : (uint16_t)0xffff;
             break;
           case SEG_MXV:                 // runs before SEG_LAT: zero v0 of every non-measurement
             if (v0) v0[r] = mem ? dv[i] : 0.0;
@@ -418,15 +573,77 @@ int64_t swseg_decode(const uint8_t* b, uint8_t* etype, uint8_t* level, int64_t* 
           case SEG_ELEV:
             if (v2) v2[r] = mem ? dv[i] : 0.0;
             break;
-          case SEG_ALT:
-            if (alt) alt[r] = mem ? cd.base + unpack(words, i, cd.bits) : 0;
-            break;
+          case SEG_ALTK: ak[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+          case SEG_ALTLEN: al[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+          case SEG_ALTNUM: an[k] = mem ? u : 0; break;
+          case SEG_MSGLEN: ml[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+          case SEG_METALEN: dl[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
         }
         if (mem) ++i;
       }
     }
+    if (str_heap) {
+      const uint8_t* heap = pg + ph.heap_off;
+      uint32_t ho = ph.alt_pfx;
+      for (uint32_t k = 0; k < m; ++k) {
+        const int64_t r = r0 + k;
+        // alternate id
+        if (fl[k] & SEGF_HAS_ALT) {
+          const int64_t need = so + ph.alt_pfx + (mode == SEG_ALT_HEX ? ph.alt_width : al[k]) + 8;
+          if (need > str_cap) return -1;
+          memcpy(str_heap + so, heap, ph.alt_pfx);
+          so += ph.alt_pfx;
+          if (mode == SEG_ALT_HEX) {
+            for (int d = (int)ph.alt_width - 1; d >= 0; --d)
+              str_heap[so++] = "0123456789abcdef"[(an[k] >> (4 * d)) & 15];
+          } else {
+            memcpy(str_heap + so, heap + ho, al[k]);
+            so += (int64_t)al[k];
+            ho += (uint32_t)al[k];
+          }
+          if (ak[k]) {
+            char sfx[8];
+            const int n = snprintf(sfx, sizeof(sfx), ":%u", (unsigned)(ak[k] - 1));
+            if (so + n > str_cap) return -1;
+            memcpy(str_heap + so, sfx, (size_t)n);
+            so += n;
+          }
+        }
+        if (str_off) str_off[3 * r + 1] = so;
+        if (so + (int64_t)ml[k] + (int64_t)dl[k] > str_cap) return -1;
+        memcpy(str_heap + so, heap + ho, ml[k]);
+        so += (int64_t)ml[k];
+        ho += (uint32_t)ml[k];
+        if (str_off) str_off[3 * r + 2] = so;
+        memcpy(str_heap + so, heap + ho, dl[k]);
+        so += (int64_t)dl[k];
+        ho += (uint32_t)dl[k];
+        if (str_off) str_off[3 * r + 3] = so;
+      }
+    }
+    r0 += m;
   }
-  return h.n_rows;
+  return r0;
+}
+
+// Per-page summaries of a block (pages in order): first row, rows, assignment min / max, event date
+// min / max -- the store's page index for indexed reads.  out = int64[6 * n_pages].
+int64_t swseg_page_summary(const uint8_t* b, int64_t* out) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  for (uint32_t p = 0; p < h.n_pages; ++p) {
+    SwSegPageHdr ph;
+    memcpy(&ph, b + pt[p], sizeof(ph));
+    int64_t* o = out + 6 * p;
+    o[0] = (int64_t)p * SEG_PAGE_ROWS;
+    o[1] = ph.n_rows;
+    o[2] = seg_unord(ph.cols[SEG_ASG].base);
+    o[3] = ph.asg_max;
+    o[4] = seg_unord(ph.cols[SEG_DATE].base);
+    o[5] = ph.date_max;
+  }
+  return h.n_pages;
 }
 
 }  // extern "C"
@@ -463,11 +680,8 @@ static void block_dates(const uint8_t* b, int64_t* lo, int64_t* hi) {
   for (uint32_t p = 0; p < h.n_pages; ++p) {
     SwSegPageHdr ph;
     memcpy(&ph, b + pt[p], sizeof(ph));
-    const SwSegCol& cd = ph.cols[SEG_DATE];
-    const uint64_t span = cd.bits >= 64 ? ~0ull : ((1ull << cd.bits) - 1);
-    const uint64_t top = cd.base + span < cd.base ? ~0ull : cd.base + span;
-    *lo = std::min(*lo, seg_unord(cd.base));
-    *hi = std::max(*hi, seg_unord(top));
+    *lo = std::min(*lo, seg_unord(ph.cols[SEG_DATE].base));
+    *hi = std::max(*hi, ph.date_max);
   }
 }
 
@@ -765,6 +979,11 @@ static int64_t seg_scan_file(const std::string& path, bool truncate, F emit, G o
   if (off > size) off = size;
   if (truncate && off < size) {
     if (ftruncate(fd, off) == 0) fdatasync(fd);
+  } else if (truncate) {
+    // an intact file may still hold the writer's extent reservation past EOF (fallocate KEEP_SIZE,
+    // released only by seg_close_file): a crash would otherwise leave it allocated and uncounted by
+    // retention.  Growing by a byte and truncating back frees every block past the scanned end.
+    if (ftruncate(fd, off + 1) == 0 && ftruncate(fd, off) == 0) fdatasync(fd);
   }
   close(fd);
   return off;

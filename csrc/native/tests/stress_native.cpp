@@ -51,11 +51,19 @@ void swce_destroy(void* p);
 void swce_reserve(void* p, int64_t state_slots, int64_t dedup_slots);
 int64_t swce_capture_names(void* p, const SwEventRec* recs, int64_t n, uint8_t* refs, int64_t cap);
 int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, int64_t now_ms, int32_t rank,
-                      SwEventRec* out, int64_t cap, int32_t n_threads);
+                      SwEventRec* out, SwStrRef* spans, int64_t cap, int32_t n_threads);
 int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, double p_loc, double p_alert,
                         double p_unreg, int32_t mx_per_msg, int32_t n_names, int64_t ts0, uint64_t seed,
-                        int32_t with_alt_id, double lat0, double lon0, double span_deg, uint8_t* out, int64_t out_cap,
-                        uint32_t* offs);
+                        int32_t with_alt_id, double lat0, double lon0, double span_deg, double p_meta, uint8_t* out,
+                        int64_t out_cap, uint32_t* offs);
+int64_t swseg_encode(const SwOutRec* rows, const SwEventRec* recs, const SwStrRef* spans, const uint8_t* raw,
+                     int64_t raw_bytes, int64_t n, uint8_t* out, int64_t cap);
+void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot, int32_t rank, int32_t world);
+int32_t swseg_verify(const uint8_t* b, int64_t len);
+int64_t swseg_string_bytes(const uint8_t* b, int64_t p0, int64_t p1);
+int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, uint8_t* level, int64_t* date,
+                     int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2, uint8_t* flags,
+                     uint8_t* str_heap, int64_t str_cap, int64_t* str_off);
 }
 
 static std::atomic<int> g_fail{0};
@@ -258,11 +266,46 @@ static void decode_fuzz() {
   std::vector<uint8_t> raw(n * 256);
   std::vector<uint32_t> off(n + 1);
   const int64_t bytes = sw_gen_payloads(n, "dev-", 500, 0.3, 0.1, 0.05, 3, 16, 1700000000000, 7, 1, 33.0, -85.0, 1.0,
-                                        raw.data(), (int64_t)raw.size(), off.data());
+                                        0.3, raw.data(), (int64_t)raw.size(), off.data());
   CHECK(bytes > 0, "payload generation failed");
   std::vector<SwEventRec> out(n * 8);
-  const int64_t good = sw_cpu_decode(raw.data(), off.data(), n, 1700000001000, 0, out.data(), (int64_t)out.size(), 4);
+  std::vector<SwStrRef> spans(n * 8);
+  const int64_t good = sw_cpu_decode(raw.data(), off.data(), n, 1700000001000, 0, out.data(), spans.data(),
+                                     (int64_t)out.size(), 4);
   CHECK(good >= n, "decoded %lld events from %lld messages", (long long)good, (long long)n);
+  // the lossless durable block of the decoded events: encode from an exactly sized batch, verify,
+  // decode every column and string (the sanitizer sees any read past the batch or the block)
+  {
+    std::vector<uint8_t> exact(raw.begin(), raw.begin() + bytes);
+    std::vector<SwOutRec> rows((size_t)good);
+    for (int64_t i = 0; i < good; ++i) {
+      rows[i].event_date = out[i].event_date;
+      rows[i].v0 = out[i].v0;
+      rows[i].v1 = out[i].v1;
+      rows[i].assignment = (int32_t)(i % 97);
+      rows[i].name_id = out[i].etype == SW_EV_LOCATION ? 0xffff : 1;
+      rows[i].etype = out[i].etype < 16 ? out[i].etype : SW_EV_MEASUREMENT;
+      rows[i].level = 0;
+    }
+    std::vector<uint8_t> blk((size_t)(good * 600 + (1 << 20)));
+    const int64_t nb = swseg_encode(rows.data(), out.data(), spans.data(), exact.data(), (int64_t)exact.size(), good,
+                                    blk.data(), (int64_t)blk.size());
+    CHECK(nb > 0, "block encode failed (%lld)", (long long)nb);
+    if (nb > 0) {
+      swseg_seal(blk.data(), 0, 1700000001000, 1, 0, 1);
+      std::vector<uint8_t> b2(blk.begin(), blk.begin() + nb);
+      CHECK(swseg_verify(b2.data(), nb) == 0, "block does not verify");
+      const int64_t cap = swseg_string_bytes(b2.data(), 0, 1 << 30);
+      std::vector<uint8_t> et(good), lv(good), fl(good), heap((size_t)cap);
+      std::vector<int64_t> dt(good), so(3 * good + 1);
+      std::vector<int32_t> as(good);
+      std::vector<uint16_t> nm(good);
+      std::vector<double> a0(good), a1(good), a2(good);
+      const int64_t got = swseg_decode(b2.data(), 0, 1 << 30, et.data(), lv.data(), dt.data(), as.data(), nm.data(),
+                                       a0.data(), a1.data(), a2.data(), fl.data(), heap.data(), cap, so.data());
+      CHECK(got == good, "block decode returned %lld of %lld rows", (long long)got, (long long)good);
+    }
+  }
   uint64_t s = 12345;
   auto rnd = [&] { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
   int64_t events = 0;
@@ -279,7 +322,8 @@ static void decode_fuzz() {
     std::vector<uint8_t> heap(msg);              // exact size: no slack for an over-read to hide in
     const uint32_t o[2] = {0, (uint32_t)heap.size()};
     SwEventRec ev[64];
-    const int64_t k = sw_cpu_decode(heap.data(), o, 1, 1700000001000, 0, ev, 64, 1);
+    SwStrRef sp[64];
+    const int64_t k = sw_cpu_decode(heap.data(), o, 1, 1700000001000, 0, ev, sp, 64, 1);
     CHECK(k >= 0 && k <= 64, "decode of a corrupt message returned %lld", (long long)k);
     events += k;
   }

@@ -115,6 +115,7 @@ def native():
         P = c_void_p
         _proto(lib, "sw_fingerprint_batch", None, P, P, c_int64, P, P)
         _proto(lib, "sw_hash64_batch", None, P, P, c_int64, P)
+        _proto(lib, "sw_hash64_ranges", None, P, P, P, c_int64, P)
         _proto(lib, "sw_murmur2", c_int32, P, c_int32)
         _proto(lib, "sw_crc32c", ctypes.c_uint32, ctypes.c_char_p, c_int64)
         _proto(lib, "sw_memcpy_mt", None, P, P, c_int64, c_int32)
@@ -123,9 +124,9 @@ def native():
         _proto(lib, "sw_reg_upsert", c_int64, P, P, P, c_int64, c_uint64, c_uint64, c_int32)
         _proto(lib, "sw_reg_find", c_int64, P, P, P, c_int64, c_uint64, c_uint64)
         _proto(lib, "sw_reg_build", c_int64, P, P, P, c_int64, P, P, P, c_int64, P)
-        _proto(lib, "sw_cpu_decode", c_int64, P, P, c_int64, c_int64, c_int32, P, c_int64, c_int32)
+        _proto(lib, "sw_cpu_decode", c_int64, P, P, c_int64, c_int64, c_int32, P, P, c_int64, c_int32)
         _proto(lib, "sw_gen_payloads", c_int64, c_int64, c_char_p, c_int64, c_double, c_double, c_double, c_int32,
-               c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, P, c_int64, P)
+               c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, c_double, P, c_int64, P)
         _proto(lib, "sw_gen_tokens", c_int64, c_char_p, c_int64, c_int64, P, c_int64, P)
         _proto(lib, "sw_stamp_alt_epoch", c_int64, P, P, c_int64, c_uint64, c_int32)
         _proto(lib, "sw_alt_positions", c_int64, P, P, c_int64, P)
@@ -156,7 +157,7 @@ def native():
         _proto(lib, "swce_threads", c_int32, P)
         _proto(lib, "swce_reserve", None, P, c_int64, c_int64)
         _proto(lib, "swce_capture_names", c_int64, P, P, c_int64, P, c_int64)
-        _proto(lib, "swce_process", c_int32, P, P, P, P, c_int64, c_int64, c_int32, P, P)
+        _proto(lib, "swce_process", c_int32, P, P, P, P, c_int64, c_int64, c_int32, P, P, P, P, P)
         for kind in ("dedup", "intern", "seen", "ms"):
             _proto(lib, f"swce_{kind}_size", c_int64, P)
         _proto(lib, "swce_dedup_export", c_int64, P, P, P)
@@ -173,10 +174,12 @@ def native():
         _proto(lib, "swce_ms_import", None, P, P, c_int64)
         _proto(lib, "swce_ms_of", c_int64, P, c_int32, P, c_int64)
         # durable columnar segments (csrc/native/swseg.cpp)
-        _proto(lib, "swseg_encode", c_int64, P, P, P, c_int64, P, c_int64)
+        _proto(lib, "swseg_encode", c_int64, P, P, P, P, c_int64, c_int64, P, c_int64)
         _proto(lib, "swseg_seal", None, P, c_int64, c_int64, c_int64, c_int32, c_int32)
         _proto(lib, "swseg_verify", c_int32, P, c_int64)
-        _proto(lib, "swseg_decode", c_int64, P, P, P, P, P, P, P, P, P, P)
+        _proto(lib, "swseg_decode", c_int64, P, c_int64, c_int64, P, P, P, P, P, P, P, P, P, P, c_int64, P)
+        _proto(lib, "swseg_string_bytes", c_int64, P, c_int64, c_int64)
+        _proto(lib, "swseg_page_summary", c_int64, P, P)
         _proto(lib, "swseg_dates", None, P, P, P)
         _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)
         _proto(lib, "swss_append", c_int32, P, P, c_int64, c_int64)
@@ -274,7 +277,7 @@ def gpu():
         _proto(lib, "sw_graph_launch", c_int32, P, P)
         _proto(lib, "sw_graph_destroy", c_int32, P)
         _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
-        _proto(lib, "sw_seg_encode", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
+        _proto(lib, "sw_seg_encode", c_int32, P, P, P, P, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
         _gpu = lib

@@ -43,6 +43,14 @@ EVENT_REC = np.dtype([
 ], align=True)
 assert EVENT_REC.itemsize == 80
 
+# String refs of a decoded event (SwStrRef, csrc/include/swtypes.h): where its alternate id and
+# metadata span sit in the raw batch, and its measurement index (alternate id "<alt>:<k>").
+STR_REF = np.dtype([("alt_off", "<u4"), ("meta_off", "<u4"), ("alt_len", "<u2"), ("meta_len", "<u2"),
+                    ("k", "<u2"), ("has", "u1"), ("pad", "u1")], align=True)
+assert STR_REF.itemsize == 16
+SR_ALT, SR_META, SR_MULTI = 0x1, 0x2, 0x4
+EV_OVERSIZE = 21
+
 # Exchange form (SwWireRec, csrc/include/swtypes.h): lossless 64-byte packing of EVENT_REC.
 WIRE_REC = np.dtype([
     ("fp_lo", "<u8"), ("fp_hi", "<u8"), ("event_date", "<i8"), ("w0", "<u8"), ("w1", "<u8"), ("w2", "<u8"),

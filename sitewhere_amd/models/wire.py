@@ -181,6 +181,39 @@ def read_delimited(buf: bytes, pos: int, cls):
     return m, pos + n
 
 
+def iter_fields(buf: bytes):
+    """Raw protobuf fields of ``buf``: (field number, wire type, value) with value = int (varint),
+    bytes (length-delimited, fixed64, fixed32).  Stops at the first malformed field."""
+    p, n = 0, len(buf)
+    while p < n:
+        try:
+            key, p = _pbdec._DecodeVarint(buf, p)
+        except Exception:  # noqa: BLE001
+            return
+        f, wt = key >> 3, key & 7
+        if wt == 0:
+            try:
+                v, p = _pbdec._DecodeVarint(buf, p)
+            except Exception:  # noqa: BLE001
+                return
+        elif wt == 2:
+            try:
+                ln, p = _pbdec._DecodeVarint(buf, p)
+            except Exception:  # noqa: BLE001
+                return
+            if p + ln > n:
+                return
+            v, p = bytes(buf[p:p + ln]), p + ln
+        elif wt == 1 or wt == 5:
+            w = 8 if wt == 1 else 4
+            if p + w > n:
+                return
+            v, p = bytes(buf[p:p + w]), p + w
+        else:
+            return
+        yield f, wt, v
+
+
 def encode(command: int, body, originator: str | None = None) -> bytes:
     h = Header(command=command)
     if originator is not None:
@@ -244,22 +277,32 @@ def measurements(hardware_id: str, values: dict, event_date: int | None = None, 
 
 
 def location(hardware_id: str, lat: float, lon: float, elevation: float | None = None, event_date: int | None = None,
-             alternate_id: str | None = None, originator: str | None = None) -> bytes:
+             alternate_id: str | None = None, originator: str | None = None, metadata: dict | None = None,
+             update_state: bool | None = None) -> bytes:
     b = DeviceLocation(hardwareId=hardware_id, latitude=lat, longitude=lon)
     if elevation is not None:
         b.elevation = elevation
     if event_date is not None:
         b.eventDate = int(event_date)
+    for k, v in (metadata or {}).items():
+        b.metadata.add(name=k, value=v)
+    if update_state is not None:
+        b.updateState = update_state
     if alternate_id is not None:
         b.alternateId = alternate_id
     return encode(SEND_DEVICE_LOCATION, b, originator)
 
 
 def alert(hardware_id: str, alert_type: str, message: str, event_date: int | None = None,
-          alternate_id: str | None = None, originator: str | None = None) -> bytes:
+          alternate_id: str | None = None, originator: str | None = None, metadata: dict | None = None,
+          update_state: bool | None = None) -> bytes:
     b = DeviceAlert(hardwareId=hardware_id, alertType=alert_type, alertMessage=message)
     if event_date is not None:
         b.eventDate = int(event_date)
+    for k, v in (metadata or {}).items():
+        b.metadata.add(name=k, value=v)
+    if update_state is not None:
+        b.updateState = update_state
     if alternate_id is not None:
         b.alternateId = alternate_id
     return encode(SEND_DEVICE_ALERT, b, originator)

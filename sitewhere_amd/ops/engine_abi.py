@@ -57,6 +57,8 @@ FIELDS = [
     # state merge scratch
     ("ev_slot", P),
     ("dd_meta", P),
+    # string refs of the decoded records (SwStrRef, read by the durable-block encoder)
+    ("spans", P),
 ]
 
 
@@ -65,7 +67,8 @@ class SwEngineArgs(ctypes.Structure):
 
 
 def abi_sizes(lib) -> dict:
-    buf = (ctypes.c_int64 * 9)()
+    buf = (ctypes.c_int64 * 10)()
     lib.sw_abi_sizes(ctypes.cast(buf, ctypes.c_void_p))
     return {"event_rec": buf[0], "out_rec": buf[1], "engine_args": buf[2], "name_ref": buf[3], "zone_test": buf[4],
-            "reg_slot": buf[5], "asg_state": buf[6], "ms_slot": buf[7], "wire_rec": buf[8]}
+            "reg_slot": buf[5], "asg_state": buf[6], "ms_slot": buf[7], "wire_rec": buf[8],
+            "str_ref": buf[9]}

@@ -34,8 +34,11 @@ from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, D
                              DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults)
 from .events import DeviceEventStore, MemoryEventStore
 
+# SEG_FLAGS bits (csrc/include/swseg.h)
+SEGF_HAS_US, SEGF_US, SEGF_HAS_ELEV, SEGF_HAS_ALT, SEGF_HAS_META, SEGF_GEN = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
 SEG_ALIGN = 4096
 PAGE_ROWS = 1024
+PAGE_HDR = 400              # sizeof(SwSegPageHdr), csrc/include/swseg.h
 FLAG_COMMIT = 1             # the block is followed by a commit record of input offsets (swseg.h)
 MAX_SRC = 252
 HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("flags", "<u2"), ("n_rows", "<u4"), ("n_pages", "<u4"),
@@ -52,24 +55,44 @@ def _p(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
-def max_block_bytes(n_rows: int) -> int:
-    """Upper bound of an encoded block (every column at 64 bits plus exceptions), padded."""
+def max_block_bytes(n_rows: int, string_bytes: int = 0) -> int:
+    """Upper bound of an encoded block (every column at 64 bits plus exceptions, every string of the
+    rows in the heap: ``string_bytes``), padded."""
     pages = (n_rows + PAGE_ROWS - 1) // PAGE_ROWS
-    worst = 64 + 8 * (pages + 2) + pages * (16 + 11 * 24) + n_rows * (11 * 8 + 4 * 10) + 8 * 4 * 11 * pages
+    worst = (64 + 8 * (pages + 2) + pages * (PAGE_HDR + 8 + 16 * 16) + n_rows * (15 * 8 + 4 * 10)
+             + 8 * 4 * 15 * pages + int(string_bytes))
     return -(-worst // SEG_ALIGN) * SEG_ALIGN
 
 
-def encode_block(rows: np.ndarray, v2: np.ndarray | None = None, alt: np.ndarray | None = None) -> np.ndarray:
-    """CPU encoder (bit-identical to the MI355X ``k_seg_encode``): OUT_REC rows + elevation + alt-id
-    hash columns -> block bytes (header sealed separately by :func:`seal`)."""
+def max_string_bytes(n_rows: int, raw_bytes: int) -> int:
+    """Heap bound of a step's block: every row's strings come from its own payload, so the heap holds
+    at most the batch's bytes once per row of a payload -- bounded by 3 x 64 KiB per row and, for
+    the usual one row per payload, by the batch itself."""
+    return min(3 * 0xFFFF * int(n_rows), 2 * int(raw_bytes) + 64 * int(n_rows)) + 8 * PAGE_ROWS
+
+
+def encode_block(rows: np.ndarray, recs: np.ndarray | None = None, spans: np.ndarray | None = None,
+                 raw: np.ndarray | None = None) -> np.ndarray:
+    """CPU encoder (bit-identical to the MI355X ``k_seg_encode``): OUT_REC rows, each with its
+    persisted EVENT_REC record and STR_REF string refs (row-aligned; None: rows without record
+    data -- no strings, elevation or flags) into the raw batch ``raw`` -> block bytes (header sealed
+    separately by :func:`seal`)."""
+    from ..models.columnar import EVENT_REC, STR_REF
     rows = np.ascontiguousarray(rows, OUT_REC)
     n = len(rows)
-    v2 = np.zeros(n, np.float64) if v2 is None else np.ascontiguousarray(v2, np.float64)
-    alt = np.zeros(n, np.uint64) if alt is None else np.ascontiguousarray(alt, np.uint64)
-    cap = max_block_bytes(n)
+    if recs is not None:
+        recs = np.ascontiguousarray(recs, EVENT_REC)
+        assert len(recs) >= n
+    if spans is not None:
+        spans = np.ascontiguousarray(spans, STR_REF)
+        assert len(spans) >= n
+    raw_a = None if raw is None else np.ascontiguousarray(raw, np.uint8)
+    cap = max_block_bytes(n, 0 if raw_a is None else max_string_bytes(n, len(raw_a)))
     out = np.zeros(cap, np.uint8)
-    r = native().swseg_encode(_p(rows) if n else None, _p(v2) if n else None, _p(alt) if n else None, n, _p(out),
-                              cap)
+    r = native().swseg_encode(_p(rows) if n else None, _p(recs) if recs is not None and n else None,
+                              _p(spans) if spans is not None and n else None,
+                              _p(raw_a) if raw_a is not None and len(raw_a) else None,
+                              0 if raw_a is None else len(raw_a), n, _p(out), cap)
     if r < 0:
         raise RuntimeError(f"block needs {-r} bytes")
     return out[:r]
@@ -102,22 +125,76 @@ def header(block) -> dict:
     return {k: int(h[k]) for k in HDR.names}
 
 
-def decode_block(block) -> dict:
-    """Block -> per-row columns (etype, level, date, asg, name, v0, v1, v2, alt) + header fields."""
+def decode_block(block, pages: tuple[int, int] | None = None, strings: bool = True, check: bool = True) -> dict:
+    """Block -> per-row columns (etype, level, date, asg, name, v0, v1, v2, flags) + header fields,
+    and with ``strings`` the rows' alternate ids, alert messages and metadata spans (see
+    :func:`row_strings`).  ``pages`` = (first, end) decodes only those pages (rows from the first
+    row of ``first``; ``cols["row0"]`` is that row's index in the block)."""
     b = np.ascontiguousarray(np.frombuffer(block, np.uint8) if not isinstance(block, np.ndarray) else block)
-    rc = verify(b)
-    if rc:
-        raise ValueError(f"corrupt event block (code {rc})")
+    if check:
+        rc = verify(b)
+        if rc:
+            raise ValueError(f"corrupt event block (code {rc})")
     h = header(b)
-    n = h["n_rows"]
+    lib = native()
+    p0, p1 = (0, h["n_pages"]) if pages is None else (max(0, int(pages[0])), min(h["n_pages"], int(pages[1])))
+    n = max(0, min(h["n_rows"], p1 * PAGE_ROWS) - p0 * PAGE_ROWS) if p1 > p0 else 0
     cols = {"etype": np.empty(n, np.uint8), "level": np.empty(n, np.uint8), "date": np.empty(n, np.int64),
             "asg": np.empty(n, np.int32), "name": np.empty(n, np.uint16), "v0": np.empty(n, np.float64),
-            "v1": np.empty(n, np.float64), "v2": np.empty(n, np.float64), "alt": np.empty(n, np.uint64)}
+            "v1": np.empty(n, np.float64), "v2": np.empty(n, np.float64), "flags": np.empty(n, np.uint8)}
+    heap = offs = None
     if n:
-        native().swseg_decode(_p(b), *[_p(cols[k]) for k in ("etype", "level", "date", "asg", "name", "v0", "v1",
-                                                             "v2", "alt")])
+        if strings:
+            cap = int(lib.swseg_string_bytes(_p(b), p0, p1))
+            heap = np.empty(max(cap, 8), np.uint8)
+            offs = np.zeros(3 * n + 1, np.int64)
+        got = lib.swseg_decode(_p(b), p0, p1, *[_p(cols[k]) for k in ("etype", "level", "date", "asg", "name", "v0",
+                                                                        "v1", "v2", "flags")],
+                               _p(heap) if heap is not None else None, 0 if heap is None else len(heap),
+                               _p(offs) if offs is not None else None)
+        if got != n:
+            raise ValueError(f"event block decode failed ({got} of {n} rows)")
     cols["header"] = h
+    cols["row0"] = p0 * PAGE_ROWS
+    cols["str_heap"], cols["str_off"] = heap, offs
     return cols
+
+
+def _str(cols: dict, i: int, part: int) -> bytes:
+    o = cols["str_off"]
+    if o is None:
+        return b""
+    return cols["str_heap"][o[3 * i + part]:o[3 * i + part + 1]].tobytes()
+
+
+_META_FIELD = {EV_MEASUREMENT: 4, EV_LOCATION: 6, EV_ALERT: 5}
+
+
+def parse_metadata(span: bytes, field: int) -> dict:
+    """Metadata entries of a body's wire span (``Model.Metadata {name = 1; value = 2}`` as field
+    ``field``) -> dict; other fields interleaved in the span are skipped."""
+    from ..models.wire import iter_fields
+    md = {}
+    for f, wt, v in iter_fields(span):
+        if f == field and wt == 2:
+            name = value = None
+            for f2, wt2, v2 in iter_fields(v):
+                if f2 == 1 and wt2 == 2:
+                    name = v2.decode("utf-8", "replace")
+                elif f2 == 2 and wt2 == 2:
+                    value = v2.decode("utf-8", "replace")
+            if name is not None:
+                md[name] = value if value is not None else ""
+    return md
+
+
+def row_strings(cols: dict, i: int) -> tuple[str | None, str, dict]:
+    """(alternate id or None, alert message, metadata dict) of decoded row ``i``."""
+    f = int(cols["flags"][i])
+    alt = _str(cols, i, 0).decode("utf-8", "replace") if f & SEGF_HAS_ALT else None
+    msg = _str(cols, i, 1).decode("utf-8", "replace")
+    md = parse_metadata(_str(cols, i, 2), _META_FIELD.get(int(cols["etype"][i]), 0)) if f & SEGF_HAS_META else {}
+    return alt, msg, md
 
 
 def rows_of(cols: dict) -> np.ndarray:
@@ -125,6 +202,16 @@ def rows_of(cols: dict) -> np.ndarray:
     out = np.zeros(len(cols["date"]), OUT_REC)
     out["event_date"], out["v0"], out["v1"] = cols["date"], cols["v0"], cols["v1"]
     out["assignment"], out["name_id"], out["etype"], out["level"] = cols["asg"], cols["name"], cols["etype"], cols["level"]
+    return out
+
+
+def page_summary(block) -> np.ndarray:
+    """Per-page (first row, rows, assignment min, max, date min, max) of a block: the page index."""
+    b = np.ascontiguousarray(np.frombuffer(block, np.uint8) if not isinstance(block, np.ndarray) else block)
+    n = header(b)["n_pages"]
+    out = np.zeros((n, 6), np.int64)
+    if n:
+        native().swseg_page_summary(_p(b), _p(out))
     return out
 
 
@@ -641,12 +728,27 @@ class DurableEventStore(DeviceEventStore):
     def add_events(self, events):
         return self._objects.add_events(events)
 
-    def get_event_by_alternate_id(self, alt: str):
-        return self._objects.get_event_by_alternate_id(alt)
-
     @staticmethod
     def _eids(h: dict, idx) -> np.ndarray:
         return (h["first_seq"] + np.asarray(idx, np.int64)) * h["world"] + h["rank"]
+
+    def _alt_hashes(self, ent) -> np.ndarray:
+        """64-bit hashes of a block's alternate ids (0 where a row has none), computed from the stored
+        strings once per block and cached with the decoded columns."""
+        c = self._decoded(ent)
+        h = c.get("alt_hash")
+        if h is None:
+            from ..pipeline.fleet import hash64_heap
+            n = len(c["date"])
+            o = c["str_off"]
+            h = np.zeros(n, np.uint64)
+            if o is not None and n:
+                has = (c["flags"] & SEGF_HAS_ALT) != 0
+                idx = np.nonzero(has)[0]
+                if len(idx):
+                    h[idx] = hash64_heap(c["str_heap"], o[3 * idx], o[3 * idx + 1])
+            c["alt_hash"] = h
+        return h
 
     def find_alternate_hashes(self, hashes) -> dict:
         """alt-id hash -> event id string for the hashes present on disk (dedup beyond the engine's
@@ -655,14 +757,31 @@ class DurableEventStore(DeviceEventStore):
         found = {}
         if not len(want):
             return found
-        for e in self.seg.index():
-            c = self._decoded(e)
-            m = np.isin(c["alt"], want)
+        for e in self.seg.index()[::-1]:
+            ah = self._alt_hashes(e)
+            m = np.isin(ah, want)
             if m.any():
-                h = c["header"]
+                h = self._decoded(e)["header"]
                 for i in np.nonzero(m)[0]:
-                    found.setdefault(int(c["alt"][i]), f"{h['boot']:x}-{int(self._eids(h, [i])[0])}")
+                    found.setdefault(int(ah[i]), f"{h['boot']:x}-{int(self._eids(h, [i])[0])}")
+            if len(found) == len(want):
+                break
         return found
+
+    def get_event_by_alternate_id(self, alt: str):
+        from ..pipeline.fleet import hash64
+        ev = self._objects.get_event_by_alternate_id(alt)
+        if ev is not None:
+            return ev
+        h = np.uint64(hash64(alt))
+        for e in self.seg.index()[::-1]:             # newest first: the latest event with the id
+            ah = self._alt_hashes(e)
+            hit = np.nonzero(ah == h)[0]
+            for i in hit[::-1]:
+                c = self._decoded(e)
+                if row_strings(c, int(i))[0] == alt:
+                    return self._materialize(c, int(i))
+        return None
 
     def get_event_by_id(self, id: str):
         boot, sep, num = id.rpartition("-")
@@ -735,12 +854,19 @@ class DurableEventStore(DeviceEventStore):
         return SearchResults(total, [self._materialize(hits[which[o]][2], int(rows[o])) for o in order])
 
     def _materialize(self, cols: dict, i: int):
+        """Decoded row -> the reference event: ids and assignment context, alternate id, metadata,
+        and per type the name / value, coordinates (elevation when sent), alert source / level /
+        type / message, or the engine's presence state change."""
         h = cols["header"]
         b = h["boot"]
         ctx = self._asg.get(b, {}).get(int(cols["asg"][i]), [None] * 5)
-        eid = int(self._eids(h, [i])[0])
+        row = int(cols.get("row0", 0)) + i
+        eid = int(self._eids(h, [row])[0])
+        alt, msg, md = row_strings(cols, i)
+        f = int(cols["flags"][i])
         base = dict(id=f"{b:x}-{eid}", device_assignment_id=ctx[0], device_id=ctx[1], customer_id=ctx[2],
-                    area_id=ctx[3], asset_id=ctx[4], event_date=int(cols["date"][i]), received_date=h["recv_ms"])
+                    area_id=ctx[3], asset_id=ctx[4], event_date=int(cols["date"][i]), received_date=h["recv_ms"],
+                    alternate_id=alt, metadata=md)
         et = int(cols["etype"][i])
         nid = int(cols["name"][i])
         name = self._names.get(b, {}).get(nid, "") if nid != NO_NAME else ""
@@ -748,10 +874,12 @@ class DurableEventStore(DeviceEventStore):
             return DeviceMeasurement(name=name, value=float(cols["v0"][i]), **base)
         if et == EV_LOCATION:
             return DeviceLocation(latitude=float(cols["v0"][i]), longitude=float(cols["v1"][i]),
-                                  elevation=float(cols["v2"][i]), **base)
+                                  elevation=float(cols["v2"][i]) if f & SEGF_HAS_ELEV else None, **base)
         if et == EV_ALERT:
-            rule = self._rules.get(name)
-            return DeviceAlert(source=AlertSource.System if rule is not None else AlertSource.Device,
-                               level=_LEVELS[min(int(cols["level"][i]), 3)], type=name, message=rule or "", **base)
+            gen = bool(f & SEGF_GEN)
+            return DeviceAlert(source=AlertSource.System if gen else AlertSource.Device,
+                               level=_LEVELS[min(int(cols["level"][i]), 3)], type=name,
+                               message=(self._rules.get(name) or "") if gen else msg, **base)
+        # the engine's state changes are its presence scan (DevicePresenceManager.java:110-200)
         return DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
                                  new_state="NOT_PRESENT", **base)

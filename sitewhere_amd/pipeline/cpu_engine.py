@@ -12,7 +12,7 @@ import numpy as np
 
 from ..models.columnar import (EVENT_REC, OUT_REC, EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE,
                                EV_DECODE_ERROR, ST_OK, ST_UNREGISTERED, ST_UNASSIGNED, ST_DUPLICATE,
-                               ST_DECODE_ERROR, ST_CONTROL, STAT_NAMES, WIRE_REC, wire_pack, wire_unpack)
+                               ST_DECODE_ERROR, ST_CONTROL, STAT_NAMES, STR_REF, WIRE_REC, wire_pack, wire_unpack)
 from .config import EngineConfig
 from .engine_base import EngineBase, StepResult
 from .fleet import cpu_decode
@@ -217,10 +217,15 @@ class CpuInboundEngine(EngineBase):
     def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
         recs, new = self.decode_phase(raw, offs, now_ms)
         work = self._shuffle(recs)
-        return self.process_phase(work, len(offs) - 1, now_ms, new, presence)
+        # string refs point into this rank's batch: they hold for the records it processes itself
+        spans = self._dec_spans if self.world == 1 else None
+        res = self.process_phase(work, len(offs) - 1, now_ms, new, presence, spans=spans)
+        if spans is not None:
+            res.raw = raw
+        return res
 
     def decode_phase(self, raw, offs, now_ms):
-        recs = cpu_decode(raw, offs, now_ms, self.rank, cap=self.cfg.rec_cap)
+        recs, self._dec_spans = cpu_decode(raw, offs, now_ms, self.rank, cap=self.cfg.rec_cap, spans=True)
         # new-name capture on the source rank
         refs = []
         for r in recs:
@@ -232,7 +237,7 @@ class CpuInboundEngine(EngineBase):
         new = self.learn_names(np.array(refs, NAME_REF), raw) if refs else {}
         return recs, new
 
-    def process_phase(self, work, n_msgs, now_ms, new, presence=None) -> StepResult:
+    def process_phase(self, work, n_msgs, now_ms, new, presence=None, spans=None) -> StepResult:
         first_seq = self.cursor
         status, dev, asg = self._lookup(work)
         self._dedup(work, status)
@@ -276,6 +281,7 @@ class CpuInboundEngine(EngineBase):
                                 self.rank, 0))
                     gen_dev.append(int(self.asg_device[a]))
                     gen_asg.append(int(a))
+        g = np.zeros(0, EVENT_REC)
         if gen:
             g = np.array(gen, EVENT_REC)
             for r in g:
@@ -299,9 +305,12 @@ class CpuInboundEngine(EngineBase):
         st[9] += len(gen) - n_rule
         st[11] += len(new)
         self.batch_seq += 1
+        prec = np.concatenate([work[ok], g])
+        pspans = np.concatenate([spans[ok], np.zeros(len(g), STR_REF)]) if spans is not None else None
         return StepResult(n_msgs=n_msgs, n_events=len(work), n_persisted=len(out_rows),
                           out=np.array(out_rows, OUT_REC), rejects=work[rej], reject_status=status[rej],
-                          new_names=new, first_seq=first_seq, world=self.world, rank=self.rank)
+                          new_names=new, first_seq=first_seq, world=self.world, rank=self.rank, prec=prec,
+                          pspans=pspans)
 
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "cpu"

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .._native import native
-from ..models.columnar import STAT_NAMES, REG_SLOT
+from ..models.columnar import OUT_REC, STAT_NAMES, REG_SLOT
 from .config import EngineConfig
 from .fleet import hash64
 
@@ -65,6 +65,12 @@ class StepResult:
     # (``encode_blocks``); ``block_frame`` = (buffer, offset) as for ``frame_base``
     block: np.ndarray | None = None
     block_frame: tuple | None = None
+    # host engines: what the durable-block encoder needs beside ``out`` -- the persisted records and
+    # their string refs (row-aligned with ``out``) and the raw batch the strings live in (dropped
+    # once the block is encoded: it may view a topic record)
+    prec: np.ndarray | None = None
+    pspans: np.ndarray | None = None
+    raw: np.ndarray | None = None
 
     def event_ids(self) -> np.ndarray:
         n = 0 if self.out is None else len(self.out)
@@ -307,19 +313,15 @@ class EngineBase:
         return (cursor - cap) + (rows - (cursor % cap)) % cap
 
     # ------------------------------------------------------------------ durable blocks
-    def block_columns(self, res: StepResult):
-        """(rows, elevation, alt-id hash) of a step's persisted events, from the host event ring."""
-        n = 0 if res.out is None else len(res.out)
-        idx = (res.first_seq + np.arange(n, dtype=np.int64)) % self.cfg.store_cap
-        return res.out, self.store["v2"][idx], self.store["alt"][idx]
-
     def encode_block(self, now_ms: int, res: StepResult | None = None, slot: int | None = None,
                      boot: int = 0) -> np.ndarray:
-        """Durable block (``persistence/segments.py``) of a step: encoded and sealed on the host.
-        The MI355X engine overrides this with its GPU encoder (same bytes)."""
+        """Durable block (``persistence/segments.py``) of a step: encoded and sealed on the host from
+        the step's rows, persisted records, string refs and raw batch (the whole event: alternate
+        ids, alert messages, metadata).  The MI355X engine overrides this with its GPU encoder
+        (same bytes)."""
         from ..persistence.segments import encode_block, seal
-        rows, v2, alt = self.block_columns(res)
-        blk = encode_block(rows, v2, alt)
+        blk = encode_block(res.out if res.out is not None else np.zeros(0, OUT_REC), res.prec, res.pspans, res.raw)
+        res.raw = None
         seal(blk, res.first_seq, now_ms, boot, self.rank, self.world)
         return blk
 

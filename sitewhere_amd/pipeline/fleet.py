@@ -71,6 +71,20 @@ def hash64(s: str) -> int:
     return int(hash64_strs([s])[0])
 
 
+def hash64_heap(heap: np.ndarray, start: np.ndarray, end: np.ndarray) -> np.ndarray:
+    """sw_hash64 of the strings heap[start[i]:end[i]] (vectorised over a string heap)."""
+    lib = native()
+    n = len(start)
+    offs = np.empty(2 * n, np.int64)
+    out = np.empty(n, np.uint64)
+    if not n:
+        return out
+    heap = np.ascontiguousarray(heap, np.uint8)
+    lib.sw_hash64_ranges(_ptr(heap), _ptr(np.ascontiguousarray(start, np.int64)),
+                         _ptr(np.ascontiguousarray(end, np.int64)), n, _ptr(out))
+    return out
+
+
 @dataclass
 class FleetSpec:
     prefix: str = "dev-"
@@ -87,13 +101,15 @@ class FleetSpec:
     p_register: float = 0.0          # registration requests from new devices (control plane)
     p_ack: float = 0.0               # command acknowledgements (control plane)
     device_type: str = "default-type"
+    p_meta: float = 0.0              # events carrying metadata (firmware version + gateway entries)
 
 
 def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndarray | None = None,
                  offs: np.ndarray | None = None):
     """Generate ``n_msgs`` encoded payloads. Returns (raw uint8[nbytes], offs uint32[n+1])."""
     lib = native()
-    per = 48 + len(spec.prefix) + 10 + spec.mx_per_msg * 32 + (48 if spec.with_alternate_id else 0)
+    per = 112 + len(spec.prefix) + 10 + spec.mx_per_msg * 32 + (48 if spec.with_alternate_id else 0) + \
+        (48 if spec.p_meta > 0 else 0)
     cap = n_msgs * per + 64
     if out is None or out.nbytes < cap:
         out = np.empty(cap, np.uint8)
@@ -102,7 +118,7 @@ def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndar
     r = lib.sw_gen_payloads(n_msgs, spec.prefix.encode(), spec.n_devices, spec.p_location, spec.p_alert,
                             spec.p_unregistered, spec.mx_per_msg, spec.n_names, ts0, seed,
                             1 if spec.with_alternate_id else 0, spec.lat0, spec.lon0, spec.span_deg,
-                            _ptr(out), out.nbytes, _ptr(offs))
+                            float(spec.p_meta), _ptr(out), out.nbytes, _ptr(offs))
     if r < 0:
         raise RuntimeError(f"payload buffer too small (need {-r})")
     raw, offs = out[:r], offs[:n_msgs + 1]
@@ -144,12 +160,13 @@ def _splice_control(spec: FleetSpec, raw: np.ndarray, offs: np.ndarray, seed: in
 
 
 def cpu_decode(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, cap: int | None = None,
-               threads: int = 4, out: np.ndarray | None = None):
-    """Decode a raw batch on the CPU with the shared decoder; returns an EVENT_REC array.
+               threads: int = 4, out: np.ndarray | None = None, spans: np.ndarray | bool | None = None):
+    """Decode a raw batch on the CPU with the shared decoder; returns an EVENT_REC array, or
+    ``(records, STR_REF string refs)`` when ``spans`` is True or an array to fill.
 
     ``out`` (EVENT_REC, reused across batches) avoids a fresh allocation per batch; the decoder
     writes every byte of each record it returns, so it need not be zeroed."""
-    from ..models.columnar import EVENT_REC
+    from ..models.columnar import EVENT_REC, STR_REF
 
     lib = native()
     n_msgs = len(offs) - 1
@@ -159,10 +176,15 @@ def cpu_decode(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, ca
         if cap is None:
             cap = max(16, n_msgs * 4)
         out = np.zeros(cap, EVENT_REC)
+    want = spans is not None and spans is not False
+    sp = None
+    if want:
+        sp = spans if isinstance(spans, np.ndarray) and len(spans) >= cap else np.zeros(cap, STR_REF)
     raw = np.ascontiguousarray(raw, np.uint8)
     offs = np.ascontiguousarray(offs, np.uint32)
-    n = lib.sw_cpu_decode(_ptr(raw) if raw.size else 0, _ptr(offs), n_msgs, now_ms, rank, _ptr(out), cap, threads)
-    return out[:n]
+    n = lib.sw_cpu_decode(_ptr(raw) if raw.size else 0, _ptr(offs), n_msgs, now_ms, rank, _ptr(out),
+                          _ptr(sp) if sp is not None else 0, cap, threads)
+    return (out[:n], sp[:n]) if want else out[:n]
 
 
 def stamp_alt_epoch(raw, offs: np.ndarray, epoch: int, threads: int = 8) -> int:

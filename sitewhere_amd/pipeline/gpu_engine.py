@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .._native import gpu as gpu_lib
-from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE, WIRE_REC
+from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE, STR_REF, WIRE_REC
 from ..ops.engine_abi import SwEngineArgs
 from .config import EngineConfig
 from .bus_io import host_view
@@ -134,6 +134,7 @@ class GpuInboundEngine(EngineBase):
         t["msg_evoff"] = z(c.max_msgs + 1, i32)
         t["scan_tmp"] = z(scan_tmp, i32)
         t["recs"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
+        t["spans"] = z(c.rec_cap * STR_REF.itemsize, u8)          # string refs beside each record
         t["seen_key"] = z(c.name_slots, i64)
         t["new_names"] = z(c.names_cap * NAME_REF.itemsize, u8)
         t["vlen_tmp"] = z(2 * ((5 * c.max_msgs + tile - 1) // tile) + 64, i32)   # varint framing scan
@@ -207,6 +208,7 @@ class GpuInboundEngine(EngineBase):
         a.msg_cnt, a.msg_evoff = _ptr(t["msg_cnt"]), _ptr(t["msg_evoff"])
         a.scan_tmp, a.scan_tmp_len = _ptr(t["scan_tmp"]), scan_tmp
         a.recs, a.rec_cap, a.n_recs = _ptr(t["recs"]), c.rec_cap, S(0)
+        a.spans = _ptr(t["spans"])
         a.seen_key, a.seen_mask = _ptr(t["seen_key"]), c.name_slots - 1
         a.new_names, a.n_new_names, a.names_cap = _ptr(t["new_names"]), S(1), c.names_cap
         a.overflow = S(2)
@@ -348,6 +350,7 @@ class GpuInboundEngine(EngineBase):
             raise ValueError(f"batch of {n_msgs} payloads exceeds EngineConfig.max_msgs={self.cfg.max_msgs}")
         a = self.args
         a.raw, a.msg_off, a.n_msgs, a.now_ms = _ptr(raw_dev), _ptr(off_dev), int(n_msgs), int(now_ms)
+        self._raw_bytes = int(raw_dev.numel())      # bound of the batch's strings (block encoder)
 
     def _set_step_params(self, now_ms, presence=False, out_sel=None, out_to_device=False):
         """Stream-ordered SwStepParams of the next process phase (receive time, batch, presence, rows)."""
@@ -537,11 +540,12 @@ class GpuInboundEngine(EngineBase):
             self._sync_streams()
             return self._with_block(self.collect(sel, raw, from_device=True), sel, now_ms)
 
-    def decode_only(self, raw: np.ndarray, offs: np.ndarray, now_ms: int) -> np.ndarray:
+    def decode_only(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, spans: bool = False):
         """Run only the decode phase (``k_decode_count`` / ``k_scan_sums`` / ``k_decode_emit``) of a
         host batch and return the decoded ``EVENT_REC`` records in batch order.  A test hook: it
         checks the device decoder against an independent decoder (``tests/decode_oracle.py``)
-        without validation rewriting the records.  Names it sees count as seen by later steps."""
+        without validation rewriting the records.  Names it sees count as seen by later steps.
+        ``spans``: also return the records' string refs (STR_REF)."""
         n_msgs = len(offs) - 1
         with self._lock:
             self._no_framed_pending()
@@ -552,7 +556,10 @@ class GpuInboundEngine(EngineBase):
                 raise RuntimeError(f"sw_phase_decode failed ({rc})")
             self._sync_streams()
             n = min(int(self.t["scalars"][0].item()), self.cfg.rec_cap)
-            return self.t["recs"][:n * EVENT_REC.itemsize].cpu().numpy().view(EVENT_REC).copy()
+            recs = self.t["recs"][:n * EVENT_REC.itemsize].cpu().numpy().view(EVENT_REC).copy()
+            if not spans:
+                return recs
+            return recs, self.t["spans"][:n * STR_REF.itemsize].cpu().numpy().view(STR_REF).copy()
 
     def step_framed(self, batch, now_ms: int, presence: bool | None = None) -> StepResult:
         """Synchronous step of a raw-payload record read from the bus: the payload (with its padding)
@@ -934,6 +941,11 @@ class GpuInboundEngine(EngineBase):
         return s.token, res
 
     # ------------------------------------------------------------------ durable blocks
+    # heap budget of a step's durable block: strings (alternate id, alert message, metadata) per row
+    # on average -- each row's strings are bounded by its payload, 256 B covers realistic device
+    # payloads with room; a step beyond it fails loudly in the encoder (never a truncated block)
+    BLOCK_STRING_BYTES_PER_ROW = 256
+
     def _seg_buffers(self, slot: int):
         """(HBM block buffer, encoder state, max pages, capacity) of outbound slot ``slot``: each slot
         keeps its block until the copy engine has moved it to the host."""
@@ -941,20 +953,26 @@ class GpuInboundEngine(EngineBase):
         s = segs.get(slot)
         if s is None:
             from ..persistence.segments import PAGE_ROWS, max_block_bytes
-            cap = max_block_bytes(self.out_cap)
+            cap = max_block_bytes(self.out_cap, self.BLOCK_STRING_BYTES_PER_ROW * self.out_cap)
             pages = -(-self.out_cap // PAGE_ROWS)
             s = segs[slot] = (torch.empty(cap, dtype=torch.uint8, device=self.device),
                               torch.zeros(pages + 4, dtype=torch.int64, device=self.device), pages, cap)
         return s
 
     def encode_block_async(self, slot: int) -> torch.Tensor:
-        """Enqueue ``k_seg_encode`` of the step just processed (its rows in ``out_dev[slot]``, its
-        elevation and alternate-id columns in the ring) on the current stream.  Returns the device
-        view (block bytes, encoder errors, first store sequence) the host reads once the step is done."""
+        """Enqueue ``k_seg_encode`` of the step just processed on the current stream: its rows (in
+        ``out_dev[slot]``), its persisted records (``work[ok_idx]`` then the generated ones) and, on a
+        single rank, their strings from the raw batch the step decoded (still in HBM).  Returns the
+        device view (block bytes, encoder errors, first store sequence) the host reads once the step
+        is done.  Multi-rank: records decoded on another rank carry no string refs here (their
+        strings stay in that rank's batch)."""
         dev, state, pages, cap = self._seg_buffers(slot)
-        st = self.store
-        rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(_ptr(st["v2"])),
-                                    ctypes.c_void_p(_ptr(st["alt"])), self.cfg.store_cap,
+        a = self.args
+        strings = self.world == 1
+        rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(a.work),
+                                    ctypes.c_void_p(a.ok_idx), ctypes.c_void_p(a.n_ok), ctypes.c_void_p(a.gen),
+                                    ctypes.c_void_p(a.spans if strings else 0), ctypes.c_void_p(a.raw if strings else 0),
+                                    getattr(self, "_raw_bytes", 0) if strings else 0,
                                     ctypes.c_void_p(_ptr(self.t["cursor"])), ctypes.c_void_p(_ptr(dev)), cap,
                                     ctypes.c_void_p(_ptr(state)), pages, self._stream())
         if rc:

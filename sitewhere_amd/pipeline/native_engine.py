@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 from .._native import native
-from ..models.columnar import EVENT_REC, NAME_REF, OUT_REC, REG_SLOT, STAT_NAMES
+from ..models.columnar import EVENT_REC, NAME_REF, OUT_REC, REG_SLOT, STAT_NAMES, STR_REF
 from .config import EngineConfig
 from .cpu_engine import STORE_COLS, CpuInboundEngine
 from .engine_base import EngineBase, StepResult
@@ -89,11 +89,12 @@ class NativeCpuEngine(CpuInboundEngine):
         self._lib.swce_dedup_window(self._h, cfg.dedup_slots, cfg.rec_cap)
         for v in self.store.values():      # touch the ring now (the GPU's HBM store is resident too)
             v.fill(0)
-        self._out_pool: list = []       # recycled outbound buffers (see _out_buffer)
+        self._out_pool: dict = {}       # recycled outbound buffers per dtype (see _out_buffer)
         self._status = np.zeros(cfg.rec_cap, np.uint8)
         self._zones = None
         self._zones_changed()
         self._dec, self._dec_k = [None, None], 0
+        self._dsp = [None, None]
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -129,7 +130,10 @@ class NativeCpuEngine(CpuInboundEngine):
         self._dec_k ^= 1
         if self._dec[self._dec_k] is None:
             self._dec[self._dec_k] = np.empty(self.cfg.rec_cap, EVENT_REC)
-        recs = cpu_decode(raw, offs, now_ms, self.rank, threads=self.threads, out=self._dec[self._dec_k])
+        if self._dsp[self._dec_k] is None:
+            self._dsp[self._dec_k] = np.empty(self.cfg.rec_cap, STR_REF)
+        recs, self._dec_spans = cpu_decode(raw, offs, now_ms, self.rank, threads=self.threads,
+                                           out=self._dec[self._dec_k], spans=self._dsp[self._dec_k])
         refs = np.zeros(self.cfg.names_cap, NAME_REF)
         n = self._lib.swce_capture_names(self._h, _ptr(recs), len(recs), _ptr(refs), len(refs)) if len(recs) else 0
         new = self.learn_names(refs[:n], raw) if n else {}
@@ -155,19 +159,25 @@ class NativeCpuEngine(CpuInboundEngine):
         t.stats = _ptr(self.stats)
         return t
 
-    def process_phase(self, work, n_msgs, now_ms, new, presence=None) -> StepResult:
+    def process_phase(self, work, n_msgs, now_ms, new, presence=None, spans=None) -> StepResult:
         work = np.ascontiguousarray(work)
         n = len(work)
         if n > len(self._status):
             self._status = np.zeros(n, np.uint8)
         out = self._out_buffer(n + self.cfg.gen_cap)
+        # persisted records + string refs, row-aligned with out (the block encoder's input); fresh
+        # per step: a StepResult keeps them until its block is encoded
+        prec = self._out_buffer(n + self.cfg.gen_cap, EVENT_REC)
+        pspans = self._out_buffer(n + self.cfg.gen_cap, STR_REF) if spans is not None else None
         do_presence = self.presence_due(now_ms) if presence is None else presence
         first_seq = self.cursor
         st = _Step(cursor=self.cursor, seq_base=self.seq_base)
         with self._lock:
             t = self._tables()
             rc = self._lib.swce_process(self._h, ctypes.byref(t), ctypes.byref(st), _ptr(work) if n else 0, n, now_ms,
-                                        1 if do_presence else 0, _ptr(self._status), _ptr(out))
+                                        1 if do_presence else 0, _ptr(self._status), _ptr(out),
+                                        _ptr(spans) if spans is not None and n else 0, _ptr(prec),
+                                        _ptr(pspans) if pspans is not None else 0)
         if rc != 0:
             raise RuntimeError(f"swce_process failed ({rc})")
         self.cursor, self.seq_base = st.cursor, st.seq_base
@@ -179,17 +189,20 @@ class NativeCpuEngine(CpuInboundEngine):
         n_out = st.n_ok + st.n_gen
         return StepResult(n_msgs=n_msgs, n_events=n, n_persisted=n_out, out=out[:n_out],
                           rejects=work[rej], reject_status=status[rej].copy(), new_names=new, first_seq=first_seq,
-                          world=self.world, rank=self.rank)
+                          world=self.world, rank=self.rank, prec=prec[:n_out],
+                          pspans=pspans[:n_out] if pspans is not None else None)
 
-    def _out_buffer(self, n: int) -> np.ndarray:
-        """An outbound buffer no earlier StepResult still references (checked by refcount: a live
-        ``result.out`` view pins its base), so results need no copy and no fresh pages per step."""
-        for b in self._out_pool:
+    def _out_buffer(self, n: int, dtype=OUT_REC) -> np.ndarray:
+        """An outbound buffer (rows, or the rows' records / string refs) no earlier StepResult still
+        references (checked by refcount: a live ``result.out`` view pins its base), so results need
+        no copy and no fresh pages per step."""
+        pool = self._out_pool.setdefault(np.dtype(dtype).str + str(np.dtype(dtype).itemsize), [])
+        for b in pool:
             if len(b) >= n and sys.getrefcount(b) <= 3:    # the pool list, the loop variable, the call
                 return b
-        b = np.empty(max(n, self.cfg.rec_cap + self.cfg.gen_cap), OUT_REC)
-        if len(self._out_pool) < 4:
-            self._out_pool.append(b)
+        b = np.empty(max(n, self.cfg.rec_cap + self.cfg.gen_cap), dtype)
+        if len(pool) < 4:
+            pool.append(b)
         return b
 
     # ------------------------------------------------------------------ native tables

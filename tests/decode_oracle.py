@@ -34,6 +34,9 @@ FNV_OFFSET, FNV_PRIME = 0xcbf29ce484222325, 0x100000001b3
 POLY_SEED, POLY_MUL = 0x9e3779b97f4a7c15, 0xff51afd7ed558ccd
 EV_STREAM_CREATE, EV_STREAM_DATA, EV_STREAM_DATA_REQUEST = 18, 19, 20
 F_HAS_UPDATE_STATE, F_UPDATE_STATE, F_HAS_DATE, F_HAS_ELEVATION = 1, 2, 4, 8
+EV_OVERSIZE = 21
+SR_ALT, SR_META, SR_MULTI = 1, 2, 4
+U16 = 0xFFFF
 CONTROL_TYPE = {1: EV_REGISTRATION, 2: EV_ACK, 6: EV_STREAM_CREATE, 7: EV_STREAM_DATA, 8: EV_STREAM_DATA_REQUEST}
 
 
@@ -79,26 +82,28 @@ def _varint(b: bytes, p: int, e: int) -> tuple[int, int]:
     raise Bad("truncated or overlong varint")
 
 
-def _fields(b: bytes, p: int, e: int):
-    """Yield (field, wire type, value, value start, next position) over [p, e)."""
+def _fields(b: bytes, p: int, e: int, tags: bool = False):
+    """Yield (field, wire type, value, value start, next position) over [p, e); ``tags``: the field's
+    tag position as a sixth element."""
     while p < e:
+        t0 = p
         key, p = _varint(b, p, e)
         if key > 0xffffffff or key >> 3 == 0:
             raise Bad("invalid tag")
         f, wt = key >> 3, key & 7
         if wt == 0:
             v, q = _varint(b, p, e)
-            yield f, wt, v, p, q
+            yield (f, wt, v, p, q, t0) if tags else (f, wt, v, p, q)
         elif wt == 1 or wt == 5:
             n = 8 if wt == 1 else 4
             if p + n > e:
                 raise Bad("truncated fixed field")
-            yield f, wt, b[p:p + n], p, p + n
+            yield (f, wt, b[p:p + n], p, p + n, t0) if tags else (f, wt, b[p:p + n], p, p + n)
         elif wt == 2:
             n, s = _varint(b, p, e)
             if n > e - s:
                 raise Bad("length past the end")
-            yield f, wt, b[s:s + n], s, s + n
+            yield (f, wt, b[s:s + n], s, s + n, t0) if tags else (f, wt, b[s:s + n], s, s + n)
         else:
             raise Bad("group or invalid wire type")
         p = q if wt == 0 else (p + n if wt in (1, 5) else s + n)
@@ -145,18 +150,21 @@ def decode(b: bytes, start: int, end: int, now_ms: int, rank: int = 0):
         us = None
         entries, lat, lon, elev = [], None, None, None
         atype = amsg = None
-        for f, wt, v, vs, _ in _fields(b, bs, be):
+        meta_f = {5: 4, 3: 6, 4: 5}.get(cmd)
+        md = None                                   # [first entry's tag, last entry's end)
+        for f, wt, v, vs, fe, t0 in _fields(b, bs, be, tags=True):
             if f == 1 and wt == 2:
                 hw = v
             elif f == 15 and wt == 2 and cmd in (3, 4, 5):
-                alt = hash64(v)
+                alt = (vs, len(v))
+            elif f == meta_f and wt == 2:
+                _pair(b, vs, vs + len(v), 2)
+                md = (md[0] if md else t0, fe)
             elif cmd == 5:
                 if f == 2 and wt == 2:
                     entries.append(_pair(b, vs, vs + len(v), 1))
                 elif f == 3 and wt == 1:
                     date = struct.unpack("<q", v)[0]
-                elif f == 4 and wt == 2:
-                    _pair(b, vs, vs + len(v), 2)
                 elif f == 5 and wt == 0:
                     us = v != 0
             elif cmd == 3:
@@ -165,8 +173,6 @@ def decode(b: bytes, start: int, end: int, now_ms: int, rank: int = 0):
                                       else (lat, lon, _f64(v)))
                 elif f == 5 and wt == 1:
                     date = struct.unpack("<q", v)[0]
-                elif f == 6 and wt == 2:
-                    _pair(b, vs, vs + len(v), 2)
                 elif f == 7 and wt == 0:
                     us = v != 0
             elif cmd == 4:
@@ -176,8 +182,6 @@ def decode(b: bytes, start: int, end: int, now_ms: int, rank: int = 0):
                     amsg = (vs, len(v))
                 elif f == 4 and wt == 1:
                     date = struct.unpack("<q", v)[0]
-                elif f == 5 and wt == 2:
-                    _pair(b, vs, vs + len(v), 2)
                 elif f == 6 and wt == 0:
                     us = v != 0
         if cmd == 3 and (lat is None or lon is None):
@@ -189,33 +193,51 @@ def decode(b: bytes, start: int, end: int, now_ms: int, rank: int = 0):
     except Bad as e:
         return err(str(e))
     lo, hi = fingerprint(hw)
+    if cmd in (3, 4, 5):
+        # strings past 16-bit lengths: one oversize record, the host routes the payload
+        lens = [alt[1] if alt else 0, (md[1] - md[0]) if md else 0]
+        lens += [atype[1], amsg[1]] if cmd == 4 else []
+        lens += [nl for (_, nl), _ in entries] if cmd == 5 else []
+        if max(lens) > U16:
+            return [dict(fp_lo=lo, fp_hi=hi, event_date=now_ms, name_hash=0, v0=0.0, v1=0.0, v2=0.0, alt_hash=0,
+                         aux_off=start, aux2_off=end, aux_len=0, aux2_len=0, etype=EV_OVERSIZE, flags=0,
+                         src_rank=rank, level=0)], "oversize"
     flags = ((F_HAS_UPDATE_STATE if us is not None else 0) | (F_UPDATE_STATE if us else 0) |
              (F_HAS_DATE if date is not None else 0) | (F_HAS_ELEVATION if elev is not None else 0))
     edate = date if date is not None else now_ms
     base = dict(fp_lo=lo, fp_hi=hi, event_date=edate, v0=0.0, v1=0.0, v2=0.0, aux2_off=0, aux2_len=0,
                 flags=flags, src_rank=rank, level=0)
+    abytes = b[alt[0]:alt[0] + alt[1]] if alt else None
+    span = dict(alt_off=alt[0] if alt else start, alt_len=alt[1] if alt else 0,
+                meta_off=md[0] if md else start, meta_len=(md[1] - md[0]) if md else 0, k=0,
+                has=(SR_ALT if alt else 0) | (SR_META if md else 0))
     if cmd == 5:
         recs = []
+        multi = len(entries) > 1
         for k, ((ns, nl), val) in enumerate(entries):
+            # measurement k of a multi-measurement payload: alternate id "<alt>:<k>"
+            ah = 0 if abytes is None else hash64(abytes + b":" + str(k).encode()) if multi else hash64(abytes)
             recs.append(dict(base, name_hash=hash64(b[ns:ns + nl]) if nl else 0, v0=_f64(val),
-                             alt_hash=(mix64(alt + k) | 1) if alt is not None else 0,
-                             aux_off=ns, aux_len=min(nl, 0xffff), etype=EV_MEASUREMENT))
+                             alt_hash=ah, aux_off=ns, aux_len=nl, etype=EV_MEASUREMENT,
+                             _span=dict(span, k=k, has=span["has"] | (SR_MULTI if multi else 0))))
         return recs, None
+    ah = hash64(abytes) if abytes is not None else 0
     if cmd == 3:
-        return [dict(base, name_hash=0, v0=lat, v1=lon, v2=elev if elev is not None else 0.0, alt_hash=alt or 0, aux_off=start, aux_len=0,
-                     etype=EV_LOCATION)], None
+        return [dict(base, name_hash=0, v0=lat, v1=lon, v2=elev if elev is not None else 0.0, alt_hash=ah,
+                     aux_off=start, aux_len=0, etype=EV_LOCATION, _span=span)], None
     if cmd == 4:
         (ts, tl), (ms, ml) = atype, amsg
-        return [dict(base, name_hash=hash64(b[ts:ts + tl]) if tl else 0, alt_hash=alt or 0,
-                     aux_off=ts, aux_len=min(tl, 0xffff), aux2_off=ms,
-                     aux2_len=min(ml, 0xffff), etype=EV_ALERT)], None
+        return [dict(base, name_hash=hash64(b[ts:ts + tl]) if tl else 0, alt_hash=ah,
+                     aux_off=ts, aux_len=tl, aux2_off=ms, aux2_len=ml, etype=EV_ALERT, _span=span)], None
     return [dict(fp_lo=lo, fp_hi=hi, event_date=now_ms, name_hash=0, v0=0.0, v1=0.0, v2=0.0, alt_hash=0,
                  aux_off=start, aux2_off=end, aux_len=0, aux2_len=0, etype=CONTROL_TYPE[cmd], flags=0,
                  src_rank=rank, level=0)], None
 
 
-def decode_batch(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0):
-    """Oracle records of a packed batch as an EVENT_REC array, plus the per-payload reasons."""
+def decode_batch(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0, spans: bool = False):
+    """Oracle records of a packed batch as an EVENT_REC array, plus the per-payload reasons (and,
+    with ``spans``, the STR_REF string refs of every record: zero for records without strings)."""
+    from sitewhere_amd.models.columnar import STR_REF
     b = raw.tobytes()
     rows, reasons = [], []
     for i in range(len(offs) - 1):
@@ -223,10 +245,15 @@ def decode_batch(raw: np.ndarray, offs: np.ndarray, now_ms: int, rank: int = 0):
         rows.extend(r)
         reasons.append(why)
     out = np.zeros(len(rows), EVENT_REC)
+    sp = np.zeros(len(rows), STR_REF)
     for i, r in enumerate(rows):
         for k, v in r.items():
-            out[i][k] = v
-    return out, reasons
+            if k == "_span":
+                for k2, v2 in v.items():
+                    sp[i][k2] = v2
+            else:
+                out[i][k] = v
+    return (out, reasons, sp) if spans else (out, reasons)
 
 
 # ------------------------------------------------------------------ malformed / edge-case batches

@@ -104,6 +104,14 @@ def oracle_batch(seed=11):
     msgs = [b[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
     msgs += edge_payloads(NOW) + mutated_payloads(seed, 3000, NOW)
     msgs.append(wire.measurements("big-1", {f"m{i:05d}": float(i) for i in range(3000)}, alternate_id="big"))
+    # strings the durable record keeps: metadata on every event type, updateState, messages
+    for i in range(40):
+        md = {f"k{j}": f"v{i}-{j}" for j in range(i % 4)}
+        msgs.append(wire.alert(f"o-{i}", f"t{i % 3}", f"message {i}", alternate_id=f"al-{i}", metadata=md,
+                               update_state=bool(i % 2)))
+        msgs.append(wire.location(f"o-{i}", 1.5 + i, 2.5, elevation=None if i % 2 else float(i),
+                                  alternate_id=None if i % 3 else f"lo-{i}", metadata=md))
+        msgs.append(wire.measurements(f"o-{i}", {"a": i, "b": -i}, alternate_id=f"mx-{i}", metadata=md))
     return pack_messages(msgs)
 
 
@@ -156,3 +164,48 @@ def test_oracle_fields_match_the_protobuf_runtime():
             assert (recs[0]["v0"], recs[0]["v1"]) == (body.latitude, body.longitude)
         else:
             assert recs[0]["name_hash"] == py_hash64(body.alertType.encode())
+
+
+def test_host_string_refs_match_independent_oracle():
+    """Where every record's alternate id and metadata span sit in the batch (the durable record's
+    strings), and which measurement of its payload it is: host decoder == oracle, bit for bit."""
+    raw, offs = oracle_batch(seed=13)
+    want, _, wsp = decode_batch(raw, offs, NOW, spans=True)
+    got, gsp = cpu_decode(raw, offs, NOW, cap=len(want) + 16, spans=True)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    assert np.array_equal(gsp.view(np.uint8), wsp.view(np.uint8))
+    ev = got["etype"] < 16
+    assert (gsp["has"][ev] & 1).sum() > 1000 and (gsp["has"][ev] & 2).sum() > 50 and (gsp["has"][ev] & 4).sum() > 1000
+    b = raw.tobytes()
+    for i in np.nonzero((gsp["has"] & 1) != 0)[0][:200]:
+        o, n = int(gsp["alt_off"][i]), int(gsp["alt_len"][i])
+        alt = b[o:o + n] + (b":" + str(int(gsp["k"][i])).encode() if gsp["has"][i] & 4 else b"")
+        assert py_hash64(alt) == int(got["alt_hash"][i])
+
+
+def test_multi_measurement_alternate_ids_hash_like_the_per_event_path():
+    """Measurement k of a multi-measurement payload is "<alt>:<k>" on both paths
+    (services/event_sources.py names it so), so dedup and the alternate-id index agree."""
+    p = wire.measurements("d-1", {"a": 1.0, "b": 2.0, "c": 3.0}, alternate_id="msg-77")
+    raw, offs = pack_messages([p])
+    recs = cpu_decode(raw, offs, NOW)
+    assert [int(h) for h in recs["alt_hash"]] == [hash64(f"msg-77:{k}") for k in range(3)]
+    single = cpu_decode(*pack_messages([wire.measurements("d-1", {"a": 1.0}, alternate_id="msg-78")]), NOW)
+    assert int(single["alt_hash"][0]) == hash64("msg-78")
+
+
+def test_oversize_strings_take_the_host_path():
+    """An event whose alternate id, alert message or metadata span passes 16-bit lengths is one
+    SW_EV_OVERSIZE record (host-routed to the per-event path, stored whole there) -- never truncated."""
+    from sitewhere_amd.models.columnar import EV_OVERSIZE
+    big = "x" * 70000
+    msgs = [wire.alert("d-1", "t", big), wire.measurements("d-2", {"a": 1.0}, alternate_id=big),
+            wire.location("d-3", 1.0, 2.0, metadata={"k": big}), wire.measurements("d-4", {big: 1.0}),
+            wire.alert("d-5", "t", "fine")]
+    raw, offs = pack_messages(msgs)
+    recs, sp = cpu_decode(raw, offs, NOW, spans=True)
+    want, why, wsp = decode_batch(raw, offs, NOW, spans=True)
+    assert np.array_equal(recs.view(np.uint8), want.view(np.uint8))
+    assert list(recs["etype"]) == [EV_OVERSIZE] * 4 + [2]
+    assert why[:4] == ["oversize"] * 4 and why[4] is None
+    assert (recs["fp_lo"][:4] != 0).all()                  # the device is known: routed by its token

@@ -46,3 +46,22 @@ def test_device_decode_of_corrupted_batches_never_escapes_its_payload():
     end = int(offs[-1])
     assert (got["aux_off"].astype(np.int64) + got["aux_len"] <= end).all()
     assert (got["aux2_off"].astype(np.int64) + got["aux2_len"] <= end).all()
+
+
+def test_device_string_refs_match_independent_oracle():
+    """The string refs k_decode_emit writes beside each record (alternate id, metadata span,
+    measurement index -- the durable record's strings) equal the oracle's, and oversize events are
+    one host-routed record, as on the host."""
+    from sitewhere_amd.models import wire
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    raw, offs = oracle_batch(seed=29)
+    b = raw[:int(offs[-1])].tobytes()
+    msgs = [b[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    msgs += [wire.alert("d-1", "t", "x" * 70000), wire.measurements("d-2", {"a": 1.0}, alternate_id="y" * 66000)]
+    raw, offs = pack_messages(msgs)
+    want, why, wsp = decode_batch(raw, offs, NOW, spans=True)
+    g = GpuInboundEngine(small_cfg(max_msgs=16384, rec_cap=len(want) + 1024))
+    got, gsp = g.decode_only(raw, offs, NOW, spans=True)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    assert np.array_equal(gsp.view(np.uint8), wsp.view(np.uint8))
+    assert why[-2:] == ["oversize", "oversize"] and (gsp["has"] & 2).sum() > 50

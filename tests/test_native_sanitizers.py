@@ -3,8 +3,10 @@
 ``csrc/native/tests/stress_native.cpp`` drives the commit log (producers, waiting / copying /
 in-place readers, retention recycling segments across partitions, adopted external buffers,
 consumer-group offsets, a durable directory), the CPU engine's fork-join pool and the
-device-protocol decoder (20,000 corrupted payloads) from many threads.  It is compiled together
-with ``swnative.cpp`` and ``swcpuengine.cpp`` twice: with ThreadSanitizer, and with
+device-protocol decoder (20,000 corrupted payloads, string refs included) from many threads, and
+encodes / verifies / decodes a lossless durable block of the decoded events (strings copied from an
+exactly sized batch).  It is compiled together with ``swnative.cpp``, ``swcpuengine.cpp`` and
+``swseg.cpp`` twice: with ThreadSanitizer, and with
 AddressSanitizer + UndefinedBehaviorSanitizer.  Host code only -- no GPU code is instrumented.
 """
 from __future__ import annotations
@@ -18,7 +20,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = [os.path.join(ROOT, "csrc", "native", "tests", "stress_native.cpp"),
        os.path.join(ROOT, "csrc", "native", "swnative.cpp"),
-       os.path.join(ROOT, "csrc", "native", "swcpuengine.cpp")]
+       os.path.join(ROOT, "csrc", "native", "swcpuengine.cpp"),
+       os.path.join(ROOT, "csrc", "native", "swseg.cpp")]
 CXX = shutil.which("g++")
 
 SANITIZERS = {

@@ -12,33 +12,71 @@ from sitewhere_amd.models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT,
 from sitewhere_amd.persistence import segments as sg
 
 
-def synth_rows(n, seed=0, full_precision=False):
-    """Rows shaped like the engine's persisted output: decimal sensor values, 6-decimal coordinates,
-    alerts, presence state changes; some alternate ids."""
+def synth_rows(n, seed=0, full_precision=False, strings=True):
+    """Inputs of one block shaped like an engine step's persisted output: decoded device events of a
+    generated fleet (decimal sensor values, 6-decimal coordinates, alerts with varied messages,
+    metadata on some events, alternate ids) enriched with assignments and name ids, then rule alerts
+    and presence state changes (generated rows).  Returns (rows, records, string refs, raw batch)."""
+    from sitewhere_amd.pipeline.fleet import FleetSpec, cpu_decode, gen_payloads
     rng = np.random.default_rng(seed)
-    et = rng.choice([EV_MEASUREMENT, EV_LOCATION, EV_ALERT, EV_STATE_CHANGE], n, p=[0.68, 0.25, 0.05, 0.02])
+    n_dev = max(1, n)
+    spec = FleetSpec(prefix="s-", n_devices=n_dev, with_alternate_id=strings, p_meta=0.3 if strings else 0.0,
+                     mx_per_msg=1 + seed % 2, lat0=33.0, lon0=-85.0, span_deg=2.0)
+    n_msgs = max(1, int(n * 0.9) // spec.mx_per_msg)
+    raw, offs = gen_payloads(spec, n_msgs, 1_700_000_000_000, seed=seed + 1)
+    recs, spans = cpu_decode(raw, offs, 1_700_000_000_000, cap=4 * n_msgs + 16, spans=True)
+    recs, spans = recs[:n], spans[:n]
+    if not strings:
+        spans[:] = 0
+    g = n - len(recs)                                       # generated rows fill the rest
+    gen = np.zeros(g, recs.dtype)
+    gen["etype"] = np.where(rng.random(g) < 0.5, EV_ALERT, EV_STATE_CHANGE)
+    gen["event_date"] = 1_700_000_100_000
+    gen["level"] = np.where(gen["etype"] == EV_ALERT, rng.integers(0, 4, g), 0)
+    recs = np.concatenate([recs, gen])
+    spans = np.concatenate([spans, np.zeros(g, spans.dtype)])
+    et = recs["etype"]
     rows = np.zeros(n, OUT_REC)
     rows["etype"] = et
-    rows["event_date"] = 1_700_000_000_000 + rng.integers(0, 60_000, n)
+    rows["event_date"] = recs["event_date"]
     rows["assignment"] = rng.integers(0, 1 << 20, n)
-    mx, loc, al = et == EV_MEASUREMENT, et == EV_LOCATION, et == EV_ALERT
+    loc = et == EV_LOCATION
     rows["name_id"] = np.where(loc, NO_NAME, rng.integers(0, 20, n))
-    rows["v0"] = np.where(mx, rng.integers(0, 100000, n) / 100.0, 0.0)
-    lat = 33.0 + rng.integers(0, 2_000_000, n) / 1e6
-    lon = -85.0 + rng.integers(0, 2_000_000, n) / 1e6
+    rows["v0"], rows["v1"], rows["level"] = recs["v0"], recs["v1"], recs["level"]
     if full_precision:
-        lat = 33.0 + 2.0 * rng.random(n)
-        lon = -85.0 + 2.0 * rng.random(n)
-    rows["v0"] = np.where(loc, lat, rows["v0"])
-    rows["v1"] = np.where(loc, lon, 0.0)
-    rows["level"] = np.where(al, rng.integers(0, 4, n), 0)
-    v2 = np.where(loc, 10.0, 0.0)
-    alt = np.where(rng.random(n) < 0.5, rng.integers(1, 1 << 62, n).astype(np.uint64) * 3, 0).astype(np.uint64)
-    return rows, v2, alt
+        rows["v0"] = np.where(loc, 33.0 + 2.0 * rng.random(n), rows["v0"])
+        rows["v1"] = np.where(loc, -85.0 + 2.0 * rng.random(n), rows["v1"])
+    return rows, recs, spans, raw
 
 
-def check_roundtrip(rows, v2, alt):
-    blk = sg.encode_block(rows, v2, alt)
+def expected_strings(recs, spans, raw):
+    """(alternate id or None, alert message, metadata) of each row, read from the batch directly."""
+    from sitewhere_amd.models.wire import iter_fields
+    b = raw.tobytes()
+    out = []
+    for r, s in zip(recs, spans):
+        alt = None
+        if s["has"] & 1:
+            alt = b[int(s["alt_off"]):int(s["alt_off"]) + int(s["alt_len"])].decode()
+            if s["has"] & 4:
+                alt += f":{int(s['k'])}"
+        gen = int(r["fp_lo"]) == 0 and int(r["fp_hi"]) == 0
+        msg = b[int(r["aux2_off"]):int(r["aux2_off"]) + int(r["aux2_len"])].decode() \
+            if int(r["etype"]) == EV_ALERT and not gen else ""
+        md = {}
+        if s["has"] & 2:
+            span = b[int(s["meta_off"]):int(s["meta_off"]) + int(s["meta_len"])]
+            field = {EV_MEASUREMENT: 4, EV_LOCATION: 6, EV_ALERT: 5}[int(r["etype"])]
+            for f, wt, v in iter_fields(span):
+                if f == field:
+                    kv = dict((f2, v2.decode()) for f2, _, v2 in iter_fields(v))
+                    md[kv[1]] = kv[2]
+        out.append((alt, msg, md))
+    return out
+
+
+def check_roundtrip(rows, recs, spans, raw):
+    blk = sg.encode_block(rows, recs, spans, raw)
     sg.seal(blk, 1000, 1_700_000_100_000, 7, 0, 1)
     assert sg.verify(blk) == 0
     c = sg.decode_block(blk)
@@ -46,38 +84,83 @@ def check_roundtrip(rows, v2, alt):
     for col, key in (("etype", "etype"), ("level", "level"), ("date", "event_date"), ("asg", "assignment"),
                      ("name", "name_id")):
         np.testing.assert_array_equal(c[col], rows[key], err_msg=col)
-    # values bit for bit (exceptions included)
+    # values bit for bit (exceptions included); elevation only where one was sent
     np.testing.assert_array_equal(c["v0"].view(np.uint64), rows["v0"].view(np.uint64))
     np.testing.assert_array_equal(c["v1"].view(np.uint64), rows["v1"].view(np.uint64))
-    np.testing.assert_array_equal(c["v2"].view(np.uint64), np.asarray(v2, np.float64).view(np.uint64))
-    np.testing.assert_array_equal(c["alt"], alt)
+    has_elev = (recs["etype"] == EV_LOCATION) & ((recs["flags"] & 8) != 0)
+    np.testing.assert_array_equal(c["v2"].view(np.uint64), np.where(has_elev, recs["v2"], 0.0).view(np.uint64))
+    assert ((c["flags"] & sg.SEGF_HAS_ELEV) != 0).tolist() == has_elev.tolist()
+    gen = (recs["fp_lo"] == 0) & (recs["fp_hi"] == 0)
+    assert ((c["flags"] & sg.SEGF_GEN) != 0).tolist() == gen.tolist()
+    us = np.where(gen, 0, recs["flags"] & 3)
+    np.testing.assert_array_equal(c["flags"] & 3, us)
+    want = expected_strings(recs, spans, raw)
+    for i in range(len(rows)):
+        assert sg.row_strings(c, i) == want[i], i
     return blk
 
 
 @pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 5000])
 def test_block_roundtrip(n):
-    rows, v2, alt = synth_rows(n, seed=n)
-    check_roundtrip(rows, v2, alt)
+    check_roundtrip(*synth_rows(n, seed=n))
+
+
+def test_block_is_lossless_for_every_string_form():
+    """Alternate ids in raw and hex pages, multi-measurement suffixes, alert messages, metadata on
+    every event type, updateState true / false / absent, elevation sent or not."""
+    from sitewhere_amd.models import wire
+    from sitewhere_amd.pipeline.fleet import cpu_decode, pack_messages
+    msgs = []
+    for i in range(3000):
+        md = {f"k{j}": f"value-{i}-{j}" for j in range(i % 3)}
+        alt = [f"{i:08x}", f"uuid-{i * 7919 % 104729}-x", None, f"dev-9-{i}"][i % 4]
+        us = [None, True, False][i % 3]
+        k = i % 5
+        if k == 0:
+            msgs.append(wire.measurements(f"d-{i}", {"t": i / 100, "h": -i / 10}, alternate_id=alt, metadata=md,
+                                          update_state=us))
+        elif k == 1:
+            msgs.append(wire.location(f"d-{i}", 33 + i / 1e6, -84 - i / 1e6, elevation=None if i % 2 else i / 10,
+                                      alternate_id=alt, metadata=md, update_state=us))
+        elif k == 2:
+            msgs.append(wire.alert(f"d-{i}", f"type{i % 7}", f"alert number {i} 漢字", alternate_id=alt, metadata=md,
+                                   update_state=us))
+        else:
+            msgs.append(wire.measurements(f"d-{i}", {"only": float(i)}, alternate_id=alt))
+    raw, offs = pack_messages(msgs)
+    recs, spans = cpu_decode(raw, offs, 1_700_000_000_000, cap=8000, spans=True)
+    rows = np.zeros(len(recs), OUT_REC)
+    for k in ("event_date", "v0", "v1", "etype", "level"):
+        rows[k] = recs[k]
+    rows["assignment"] = np.arange(len(recs)) % 77
+    rows["name_id"] = np.where(recs["etype"] == EV_LOCATION, NO_NAME, 3)
+    check_roundtrip(rows, recs, spans, raw)
+    # pages of counter-style ids take the hex mode: no remainder bytes in the heap
+    hexy = [wire.measurements(f"d-{i}", {"a": 1.0}, alternate_id=f"0123456789abcdef-{i:08x}") for i in range(2048)]
+    raw, offs = pack_messages(hexy)
+    recs, spans = cpu_decode(raw, offs, 1_700_000_000_000, cap=4096, spans=True)
+    rows = np.zeros(len(recs), OUT_REC)
+    rows["event_date"], rows["v0"], rows["name_id"] = recs["event_date"], recs["v0"], 1
+    blk = check_roundtrip(rows, recs, spans, raw)
+    assert len(blk) / len(rows) < 8, len(blk) / len(rows)        # a 26-byte id costs ~1.5 bytes
 
 
 def test_block_compresses_decimal_data():
-    rows, v2, alt = synth_rows(100_000, seed=1)
-    alt[:] = 0
-    blk = check_roundtrip(rows, v2, alt)
+    rows, recs, spans, raw = synth_rows(100_000, seed=1, strings=False)
+    blk = check_roundtrip(rows, recs, spans, raw)
     assert len(blk) / len(rows) < 9.0, len(blk) / len(rows)       # vs 32 B OUT_REC + 8 B elevation
 
 
 def test_block_exceptions_are_lossless():
-    rows, v2, alt = synth_rows(20_000, seed=2, full_precision=True)
+    rows, recs, spans, raw = synth_rows(20_000, seed=2, full_precision=True)
     rows["v0"][::7] = np.where(rows["etype"][::7] == EV_MEASUREMENT, np.nan, rows["v0"][::7])
     rows["v0"][1::11] = np.where(rows["etype"][1::11] == EV_MEASUREMENT, -0.0, rows["v0"][1::11])
     rows["v1"][::13] = np.where(rows["etype"][::13] == EV_LOCATION, np.inf, rows["v1"][::13])
-    check_roundtrip(rows, v2, alt)
+    check_roundtrip(rows, recs, spans, raw)
 
 
 def test_corruption_detected():
-    rows, v2, alt = synth_rows(3000, seed=3)
-    blk = check_roundtrip(rows, v2, alt)
+    blk = check_roundtrip(*synth_rows(3000, seed=3))
     for pos in (10, 64 + 4, len(blk) // 2, len(blk) - 8):
         bad = blk.copy()
         bad[pos] ^= 0x40
@@ -88,8 +171,8 @@ def _store_blocks(st, nblocks, rows_per=3000):
     seq = 0
     blocks = []
     for b in range(nblocks):
-        rows, v2, alt = synth_rows(rows_per, seed=100 + b)
-        blk = sg.encode_block(rows, v2, alt)
+        rows, recs, spans, raw = synth_rows(rows_per, seed=100 + b)
+        blk = sg.encode_block(rows, recs, spans, raw)
         sg.seal(blk, seq, 1_700_000_000_000 + b, b, 0, 1)
         tok = st.append_block(blk)
         blocks.append((seq, rows, tok))
@@ -126,15 +209,14 @@ def test_segment_store_torn_tail_recovery(tmp_path):
     path = os.path.join(d, [f for f in files if f.endswith(".sweg")][-1])
     size = os.path.getsize(path)
     with open(path, "r+b") as f:               # crash mid-write of the last block: garbage tail
-        f.seek(size - 3000)
-        f.write(os.urandom(3000))
+        f.seek(size - 4096 - 3000)              # (the block's last bytes are in its final 4 KiB)
+        f.write(os.urandom(4096 + 3000))
     st2 = sg.SegmentStore(d)
     idx = st2.index()
     assert list(idx["first_seq"]) == [b[0] for b in blocks[:-1]]
     assert os.path.getsize(path) < size        # truncated at the last good block
     # appends continue after recovery
-    rows, v2, alt = synth_rows(100, seed=9)
-    blk = sg.encode_block(rows, v2, alt)
+    blk = sg.encode_block(*synth_rows(100, seed=9))
     sg.seal(blk, blocks[-1][0], 1, 99, 0, 1)
     st2.wait(st2.append_block(blk), 30)
     assert len(st2.index()) == 5
@@ -159,11 +241,11 @@ def test_durable_event_store_queries_and_restart(tmp_path):
     from sitewhere_amd.models.domain import DateRangeSearchCriteria
     d = str(tmp_path / "es")
     es = sg.DurableEventStore(d)
-    rows, v2, alt = synth_rows(4000, seed=5)
+    rows, recs, spans, raw = synth_rows(4000, seed=5)
     rows["assignment"] = np.arange(4000) % 50
     asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % 3}", f"area-{i % 2}", None] for i in range(50)}
     names = {i: f"mx.metric{i}" for i in range(20)}
-    blk = sg.encode_block(rows, v2, alt)
+    blk = sg.encode_block(rows, recs, spans, raw)
     sg.seal(blk, 0, 1_700_000_100_000, 0xb0, 0, 1)
     tok = es.add_encoded(blk, asg=asg, names=names)
     es.wait(tok)
@@ -174,21 +256,33 @@ def test_durable_event_store_queries_and_restart(tmp_path):
     assert res.num_results == len(want)
     assert sorted(e.value for e in res.results) == sorted(want["v0"].tolist())
     assert all(e.name.startswith("mx.metric") and e.device_id == "dev-7" for e in res.results)
+    # the whole event comes back: alternate ids and metadata of the stored rows
+    exp = expected_strings(recs, spans, raw)
+    by_id = {e.id: e for e in res.results}
+    for j in np.nonzero((rows["assignment"] == 7) & (rows["etype"] == EV_MEASUREMENT))[0]:
+        e = by_id[f"b0-{int(j)}"]
+        assert (e.alternate_id, e.metadata) == (exp[j][0], exp[j][2])
     ev = res.results[0]
     es.close()
     es2 = sg.DurableEventStore(d)                         # restart: everything from disk
     again = es2.list_events("Measurement", "Assignment", ["asg-7"], DateRangeSearchCriteria(page_size=0))
     assert [e.id for e in again.results] == [e.id for e in res.results]
     assert es2.get_event_by_id(ev.id).value == ev.value
-    hashes = alt[alt != 0][:5]
+    with_alt = [j for j in range(len(rows)) if exp[j][0] is not None]
+    for j in with_alt[:5] + with_alt[-3:]:
+        got = es2.get_event_by_alternate_id(exp[j][0])
+        assert got is not None and got.id == f"b0-{j}" and got.alternate_id == exp[j][0]
+    from sitewhere_amd.pipeline.fleet import hash64
+    hashes = [hash64(exp[j][0]) for j in with_alt[:5]]
     found = es2.find_alternate_hashes(hashes)
-    assert set(found) == set(int(h) for h in hashes)
+    assert set(found) == set(hashes)
     assert all(v.startswith("b0-") for v in found.values())
+    assert es2.get_event_by_alternate_id("no-such-id") is None
     # a new engine incarnation restarts its sequences and indices: its block is not a replay, and
     # its dictionary does not rewrite the first boot's
     rows2 = rows.copy()
     rows2["assignment"] = (np.arange(4000) + 25) % 50
-    blk2 = sg.encode_block(rows2, v2, alt)
+    blk2 = sg.encode_block(rows2, recs, spans, raw)
     sg.seal(blk2, 0, 1_700_000_200_000, 0xb1, 0, 1)
     asg2 = {i: [f"asg-{(i + 1) % 50}", f"dev-{(i + 1) % 50}", None, None, None] for i in range(50)}
     es2.wait(es2.add_encoded(blk2, asg=asg2))
@@ -223,8 +317,7 @@ def test_block_sink_pool_bounded_and_commits_in_order(tmp_path):
     bus.set_retention("t.out", 4 << 20)
     tags = []
     for k in range(60):
-        rows, v2, alt = synth_rows(20000 + 1000 * k, seed=k)
-        blk = sg.encode_block(rows, v2, alt)
+        blk = sg.encode_block(*synth_rows(20000 + 1000 * k, seed=k))
         host, buf = sink.target(len(blk))
         ctypes.memmove(host, blk.ctypes.data, len(blk))
         sink.publish(buf, len(blk), k * 200_000, 1, tag=k)
