@@ -9,7 +9,7 @@
 //
 // Transcoded: {"deviceToken", "type": DeviceMeasurement | DeviceLocation | DeviceAlert,
 // "originator"?, "request": {...}} whose request the engine path represents exactly (integer
-// eventDate, no metadata, alerts at level Info from source Device).  Anything else returns a
+// eventDate, metadata of string values, alerts at level Info from source Device).  Anything else returns a
 // negative code and the caller keeps the per-event path for that payload, so no request changes
 // meaning by being transcoded.
 #include <stdint.h>
@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace {
@@ -39,7 +40,8 @@ struct Req {
   int64_t date = 0;
   bool has_date = false, date_bad = false;
   int update = -1;          // -1 absent, 0/1
-  bool has_metadata = false, bad = false, value_bad = false;
+  bool meta_bad = false, bad = false, value_bad = false;
+  std::vector<std::pair<Str, Str>>* md = nullptr;   // metadata entries in document order
 };
 
 struct P {
@@ -271,13 +273,40 @@ bool parse_request(P& q, Req& r) {
       else if (q.lit("null", 4)) {}
       else { r.bad = true; if (!q.skip()) return false; }
     } else if (KEY(key, "metadata")) {
-      if (q.p < q.e && *q.p == '{') {
-        const char* s = q.p + 1;
-        if (!q.skip()) return false;
-        while (s < q.p && (*s == ' ' || *s == '\n' || *s == '\t' || *s == '\r')) ++s;
-        if (*s != '}') r.has_metadata = true;         // "{}" with only whitespace inside: empty
-      } else if (!q.lit("null", 4)) {
-        r.has_metadata = true;
+      // an object of string values -> repeated Metadata{name, value} (the protobuf a device sends);
+      // any other value type stays on the per-event path
+      r.md->clear();
+      r.meta_bad = false;
+      if (q.lit("null", 4)) {
+      } else if (q.p < q.e && *q.p == '{') {
+        ++q.p;
+        q.ws();
+        if (q.p < q.e && *q.p == '}') {
+          ++q.p;
+        } else {
+          while (true) {
+            Str mk, mv;
+            q.ws();
+            if (!q.str(&mk)) return false;
+            q.ws();
+            if (q.p >= q.e || *q.p != ':') return false;
+            ++q.p;
+            q.ws();
+            if (q.p < q.e && *q.p == '"') {
+              if (!q.str(&mv)) return false;
+              r.md->push_back({mk, mv});
+            } else {
+              r.meta_bad = true;
+              if (!q.skip()) return false;
+            }
+            q.ws();
+            if (q.p < q.e && *q.p == ',') { ++q.p; continue; }
+            if (q.p < q.e && *q.p == '}') { ++q.p; break; }
+            return false;
+          }
+        }
+      } else {
+        r.meta_bad = true;
         if (!q.skip()) return false;
       }
     } else {
@@ -384,14 +413,23 @@ extern "C" {
 
 // Transcode one JSON device request.  Returns the protobuf length written to out, or
 //   -1 invalid JSON / not a device request (the per-event decoder reports it),
-//   -2 valid but not representable on the engine path (metadata, a level, a string date ...),
+//   -2 valid but not representable on the engine path (non-string metadata, a level, a string date ...),
 //   -3 out too small.
 int64_t sw_json_to_pb(const char* in, int64_t n, uint8_t* out, int64_t cap) {
   static thread_local std::vector<char> arena;
   if (arena.size() < (size_t)n + 8) arena.resize((size_t)n + 8);
+  static thread_local std::vector<std::pair<Str, Str>> md;
   Req r;
+  r.md = &md;
+  md.clear();
   if (!parse_top(in, n, r, arena.data()) || !r.token.has || r.token.n == 0 || !r.type.has) return -1;
-  if (r.bad || r.date_bad || r.value_bad || r.has_metadata) return -2;
+  if (r.bad || r.date_bad || r.value_bad || r.meta_bad) return -2;
+  // metadata entries: Metadata{1: name, 2: value}, each a length-delimited field of the body
+  int meta = 0;
+  for (const auto& kv : md) {
+    const int ent = str_size(1, kv.first) + str_size(2, kv.second);
+    meta += 1 + vlen((uint64_t)ent) + ent;
+  }
   static const Str empty{"", 0, true};
   // sizes first (body, then header), so the message is written once, in place
   int command, body = str_size(1, r.token), meas = 0;
@@ -399,18 +437,18 @@ int64_t sw_json_to_pb(const char* in, int64_t n, uint8_t* out, int64_t cap) {
     if (!r.name.has || !r.has_value) return -2;
     command = 5;
     meas = str_size(1, r.name) + 9;
-    body += 1 + vlen((uint64_t)meas) + meas;
+    body += 1 + vlen((uint64_t)meas) + meas + meta;
     if (r.has_date) body += 9;
     if (r.update >= 0) body += 2;
   } else if (KEY(r.type, "DeviceLocation")) {
     if (!r.has_lat || !r.has_lon) return -2;
     command = 3;
-    body += 18 + (r.has_elev ? 9 : 0) + (r.has_date ? 9 : 0) + (r.update >= 0 ? 2 : 0);
+    body += 18 + (r.has_elev ? 9 : 0) + (r.has_date ? 9 : 0) + (r.update >= 0 ? 2 : 0) + meta;
   } else if (KEY(r.type, "DeviceAlert")) {
     if ((r.level.has && !KEY(r.level, "Info")) || (r.source.has && !KEY(r.source, "Device"))) return -2;
     command = 4;
     body += str_size(2, r.atype.has ? r.atype : empty) + str_size(3, r.message.has ? r.message : empty);
-    body += (r.has_date ? 9 : 0) + (r.update >= 0 ? 2 : 0);
+    body += (r.has_date ? 9 : 0) + (r.update >= 0 ? 2 : 0) + meta;
   } else {
     return -2;                                         // registrations, acks, streams ...: per-event path
   }
@@ -419,6 +457,14 @@ int64_t sw_json_to_pb(const char* in, int64_t n, uint8_t* out, int64_t cap) {
   const int64_t total = vlen((uint64_t)hdr) + hdr + vlen((uint64_t)body) + body;
   if (total > cap) return -3;
   W w{out};
+  auto put_meta = [&](int f) {
+    for (const auto& kv : md) {
+      w.tag(f, 2);
+      w.varint((uint64_t)(str_size(1, kv.first) + str_size(2, kv.second)));
+      w.str(1, kv.first);
+      w.str(2, kv.second);
+    }
+  };
   w.varint((uint64_t)hdr);
   w.tag(1, 0);
   w.varint((uint64_t)command);
@@ -431,17 +477,20 @@ int64_t sw_json_to_pb(const char* in, int64_t n, uint8_t* out, int64_t cap) {
     w.str(1, r.name);
     w.fixed(2, &r.value);
     if (r.has_date) w.fixed(3, &r.date);
+    put_meta(4);
     if (r.update >= 0) w.boolean(5, r.update == 1);
   } else if (command == 3) {
     w.fixed(2, &r.lat);
     w.fixed(3, &r.lon);
     if (r.has_elev) w.fixed(4, &r.elev);
     if (r.has_date) w.fixed(5, &r.date);
+    put_meta(6);
     if (r.update >= 0) w.boolean(7, r.update == 1);
   } else {
     w.str(2, r.atype.has ? r.atype : empty);
     w.str(3, r.message.has ? r.message : empty);
     if (r.has_date) w.fixed(4, &r.date);
+    put_meta(5);
     if (r.update >= 0) w.boolean(6, r.update == 1);
   }
   if (r.alt.has) w.str(15, r.alt);

@@ -340,6 +340,13 @@ static void route_one(Worker& wk, uint32_t wid, const uint8_t* raw, uint32_t s, 
     return;
   }
   const size_t v0 = wk.arena.size();
+  if (st == SW_ST_CONTROL && (p.cmd == SW_CMD_SEND_DEVICE_MEASUREMENTS || p.cmd == SW_CMD_SEND_DEVICE_LOCATION ||
+                              p.cmd == SW_CMD_SEND_DEVICE_ALERT)) {
+    // an event the engine handed back (SW_EV_OVERSIZE: strings past its 16-bit lengths): the whole
+    // payload goes to the host, which decodes it onto the per-event path (stored whole there)
+    emit(RK_CONTROL, p.token, raw + s, e - s, 0, false);
+    return;
+  }
   if (p.cmd == SW_CMD_SEND_REGISTRATION) {
     W& reg = wk.reg;
     reg.clear();

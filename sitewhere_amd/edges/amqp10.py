@@ -405,6 +405,11 @@ class AmqpConnection:
 
     def _read_frame(self):
         size, doff, ftype, ch = struct.unpack(">IBBH", self._recv_exact(8))
+        # a peer's frame header is untrusted: the size covers the 8-byte header and fits the
+        # negotiated max-frame-size; the data offset (4-byte words) lies inside the frame
+        # (AMQP 1.0 section 2.3.1).  Anything else closes the connection instead of buffering it.
+        if size < 8 or size > max(self.max_frame, 512) or doff < 2 or doff * 4 > size:
+            raise AmqpError(f"invalid frame header (size {size}, data offset {doff})")
         rest = self._recv_exact(size - 8)
         body = rest[doff * 4 - 8:]
         if not body:

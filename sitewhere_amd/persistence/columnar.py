@@ -135,6 +135,12 @@ class ColumnarEventStore(DeviceEventStore):
         self.evicted_rows = 0
 
     # ------------------------------------------------------------------ ingest
+    def dictionary(self, boot, asg_ids=(), name_ids=()) -> dict:
+        """Assignment contexts / names of the rows held here (one engine incarnation at a time)."""
+        return {"asg": {int(i): self._asg[int(i)] for i in asg_ids if int(i) in self._asg},
+                "names": {int(i): self._names[int(i)] for i in name_ids if int(i) in self._names},
+                "rules": dict(getattr(self, "_rules", {}) or {})}
+
     def add_columnar(self, payload: bytes | dict) -> int:
         d = payload if isinstance(payload, dict) else decode_batch(payload)
         rows = d["rows"]

@@ -11,7 +11,9 @@ crash; replayed blocks are skipped by sequence).
 
 :class:`DurableEventStore` is the ``DeviceEventStore`` over a segment store: it keeps the
 dictionaries the rows refer to (assignment index -> ids, name id -> name, rule alert messages) in a
-small fsync'd JSON-lines log beside the segments, answers the event-management queries by decoding
+small fsync'd JSON-lines log beside the segments, keeps the events added through the API (REST adds,
+command invocations / responses, rule alerts) in a checksummed JSON-lines log synced before the add
+returns, answers the event-management queries by decoding
 the blocks whose date range overlaps, and survives restarts (everything is reloaded from disk).
 
 Reference: ``DeviceEventBuffer.java:99-135`` (buffered bulk writes, flushed every 250 ms / 200
@@ -24,6 +26,7 @@ import ctypes
 import json
 import os
 import threading
+import zlib
 from collections import OrderedDict
 
 import numpy as np
@@ -31,7 +34,8 @@ import numpy as np
 from .._native import native
 from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC
 from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceEventIndex,
-                             DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults)
+                             DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults,
+                             event_from_dict)
 from .events import DeviceEventStore, MemoryEventStore
 
 # SEG_FLAGS bits (csrc/include/swseg.h)
@@ -561,7 +565,13 @@ class DurableEventStore(DeviceEventStore):
         self.dir = directory
         os.makedirs(directory, exist_ok=True)
         self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
+        # events added through the API (REST / RPC adds, command invocations and responses, rule and
+        # presence alerts): a checksummed JSON-lines log, fdatasync'd before the add returns, replayed
+        # into the in-memory indexes on open
         self._objects = MemoryEventStore()
+        self._api_path = os.path.join(directory, f"api-{rank}.log")
+        self._load_api_log()
+        self._api_f = open(self._api_path, "ab")
         self._asg: dict[int, dict[int, list]] = {}       # boot -> assignment index -> [asg, dev, cust, area, asset]
         self._names: dict[int, dict[int, str]] = {}      # boot -> name id -> name
         self._rules: dict[str, str] = {}                 # alert type -> rule message
@@ -570,12 +580,54 @@ class DurableEventStore(DeviceEventStore):
         self._load_dict()
         self._dict_f = open(self._dict_path, "ab")
         self._high: dict[tuple, int] = {}
+        self._pending_ends: dict[tuple, list] = {}       # (boot, rank) -> [(sequence end, token)] queued
         for e in self.seg.index():
             key = (int(e["boot"]), int(e["rank"]))
             self._high[key] = max(self._high.get(key, 0), int(e["first_seq"]) + int(e["n_rows"]))
         self._cache: OrderedDict = OrderedDict()       # (file, offset) -> decoded columns
         self.cache_blocks = cache_blocks
         self.skipped_rows = 0
+
+    # ------------------------------------------------------------------ API-added events
+    def _load_api_log(self):
+        """Replay ``api-<rank>.log``: ``<crc32 hex> <event json>`` per line.  A torn or corrupt tail
+        (a crash mid-write: the add never returned) is cut off so later appends follow good data."""
+        if not os.path.exists(self._api_path):
+            return
+        good, events = 0, []
+        with open(self._api_path, "rb") as f:
+            for line in f:
+                if not line.endswith(b"\n") or len(line) < 10 or line[8:9] != b" ":
+                    break
+                body = line[9:-1]
+                try:
+                    if int(line[:8], 16) != zlib.crc32(body):
+                        break
+                    events.append(event_from_dict(json.loads(body)))
+                except ValueError:
+                    break
+                good += len(line)
+        if good < os.path.getsize(self._api_path):
+            with open(self._api_path, "r+b") as f:
+                f.truncate(good)
+                os.fsync(f.fileno())
+        self._objects.add_events(events)
+
+    def add_events(self, events):
+        """Durable API add: the events are on disk (one fdatasync per call) before they are indexed
+        and the call returns."""
+        if not events:
+            return events
+        lines = []
+        for e in events:
+            body = json.dumps(e.to_dict(), separators=(",", ":")).encode()
+            lines.append(b"%08x %s\n" % (zlib.crc32(body), body))
+        with self._lock:
+            self._api_f.write(b"".join(lines))
+            self._api_f.flush()
+            os.fdatasync(self._api_f.fileno())
+            self._objects.add_events(events)
+        return events
 
     # ------------------------------------------------------------------ dictionaries
     def _load_dict(self):
@@ -615,7 +667,8 @@ class DurableEventStore(DeviceEventStore):
     # ------------------------------------------------------------------ ingest
     def add_block(self, ptr: int, nbytes: int, owner=None, boot=None, asg=None, names=None, rules=None,
                   src=None) -> int:
-        """Queue a sealed block for the disk; returns its token (-1 when skipped as a replay).
+        """Queue a sealed block for the disk; returns its token.  A replay of rows already queued
+        returns the token of the block holding them (-1 once they are durable).
         ``src``: input offsets the block completes (see :meth:`SegmentStore.append`; the block must
         carry ``FLAG_COMMIT``)."""
         h = np.frombuffer((ctypes.c_uint8 * 64).from_address(ptr), np.uint8).view(HDR)[0]
@@ -624,14 +677,33 @@ class DurableEventStore(DeviceEventStore):
             raise ValueError("dictionary boot differs from the block's")
         self.add_dictionary(b, asg, names, rules)
         key, first, n = (b, int(h["rank"])), int(h["first_seq"]), int(h["n_rows"])
-        with self._lock:
-            if n and first + n <= self._high.get(key, 0):
-                self.skipped_rows += n
-                return -1
-            self._high[key] = max(self._high.get(key, 0), first + n)
         if src is not None and not int(h["flags"]) & FLAG_COMMIT:
             raise ValueError("a block with input offsets must be sealed with FLAG_COMMIT")
-        return self.seg.append(ptr, nbytes, owner, src)
+        with self._lock:
+            if n and first + n <= self._high.get(key, 0):
+                # a replay of rows already queued: it is "stored" only once those rows are durable --
+                # hand back the token that makes them so (a failed write raises here, never skips)
+                self.seg.durable()
+                tok = self._covering_token(key, first + n)
+                self.skipped_rows += n
+                return tok
+            # the high-water mark moves only once the block is queued: a failed append leaves it, so
+            # the retried batch is written instead of skipped as a replay
+            tok = self.seg.append(ptr, nbytes, owner, src)
+            self._high[key] = max(self._high.get(key, 0), first + n)
+            self._pending_ends.setdefault(key, []).append((first + n, tok))
+            return tok
+
+    def _covering_token(self, key, end: int) -> int:
+        """Token of the earliest queued block of ``key`` reaching ``end`` that is not durable yet;
+        -1 when every such block is on disk."""
+        d = self.seg.durable()
+        ends = [e for e in self._pending_ends.get(key, []) if e[1] > d]
+        self._pending_ends[key] = ends
+        for e, tok in ends:
+            if e >= end:
+                return tok
+        return -1
 
     def source_offset(self, topic: str, partition: int) -> int | None:
         """Next input offset of (topic, partition) whose events are all durable here (None: none
@@ -652,10 +724,11 @@ class DurableEventStore(DeviceEventStore):
 
     def close(self):
         self.seg.close()
-        try:
-            self._dict_f.close()
-        except Exception:  # noqa: BLE001
-            pass
+        for f in (self._dict_f, self._api_f):
+            try:
+                f.close()
+            except Exception:  # noqa: BLE001
+                pass
 
     # ------------------------------------------------------------------ reads
     def _decoded(self, ent) -> dict:
@@ -724,9 +797,6 @@ class DurableEventStore(DeviceEventStore):
 
     def count(self) -> int:
         return self.rows + self._objects.count()
-
-    def add_events(self, events):
-        return self._objects.add_events(events)
 
     @staticmethod
     def _eids(h: dict, idx) -> np.ndarray:
@@ -854,32 +924,48 @@ class DurableEventStore(DeviceEventStore):
         return SearchResults(total, [self._materialize(hits[which[o]][2], int(rows[o])) for o in order])
 
     def _materialize(self, cols: dict, i: int):
-        """Decoded row -> the reference event: ids and assignment context, alternate id, metadata,
-        and per type the name / value, coordinates (elevation when sent), alert source / level /
-        type / message, or the engine's presence state change."""
-        h = cols["header"]
-        b = h["boot"]
-        ctx = self._asg.get(b, {}).get(int(cols["asg"][i]), [None] * 5)
-        row = int(cols.get("row0", 0)) + i
-        eid = int(self._eids(h, [row])[0])
-        alt, msg, md = row_strings(cols, i)
-        f = int(cols["flags"][i])
-        base = dict(id=f"{b:x}-{eid}", device_assignment_id=ctx[0], device_id=ctx[1], customer_id=ctx[2],
-                    area_id=ctx[3], asset_id=ctx[4], event_date=int(cols["date"][i]), received_date=h["recv_ms"],
-                    alternate_id=alt, metadata=md)
-        et = int(cols["etype"][i])
-        nid = int(cols["name"][i])
-        name = self._names.get(b, {}).get(nid, "") if nid != NO_NAME else ""
-        if et == EV_MEASUREMENT:
-            return DeviceMeasurement(name=name, value=float(cols["v0"][i]), **base)
-        if et == EV_LOCATION:
-            return DeviceLocation(latitude=float(cols["v0"][i]), longitude=float(cols["v1"][i]),
-                                  elevation=float(cols["v2"][i]) if f & SEGF_HAS_ELEV else None, **base)
-        if et == EV_ALERT:
-            gen = bool(f & SEGF_GEN)
-            return DeviceAlert(source=AlertSource.System if gen else AlertSource.Device,
-                               level=_LEVELS[min(int(cols["level"][i]), 3)], type=name,
-                               message=(self._rules.get(name) or "") if gen else msg, **base)
-        # the engine's state changes are its presence scan (DevicePresenceManager.java:110-200)
-        return DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
-                                 new_state="NOT_PRESENT", **base)
+        b = cols["header"]["boot"]
+        return materialize_row(cols, i, self._asg.get(b, {}), self._names.get(b, {}), self._rules)
+
+    def dictionary(self, boot, asg_ids=(), name_ids=()) -> dict:
+        """Dictionary entries of an engine incarnation (assignment index -> context, name id -> name)
+        and the rule messages: what an enriched-batch consumer that started after the batch carrying
+        them needs to materialize rows."""
+        b = boot_id(boot)
+        with self._lock:
+            a, n = self._asg.get(b, {}), self._names.get(b, {})
+            return {"asg": {int(i): a[int(i)] for i in asg_ids if int(i) in a},
+                    "names": {int(i): n[int(i)] for i in name_ids if int(i) in n}, "rules": dict(self._rules)}
+
+
+def materialize_row(cols: dict, i: int, asg: dict, names: dict, rules: dict):
+    """Decoded block row ``i`` -> the reference event: ids and assignment context (``asg``: index ->
+    [assignment, device, customer, area, asset, ...]), alternate id, metadata, and per type the name /
+    value, coordinates (elevation when sent), alert source / level / type / message, or the
+    engine's presence state change.  ``names``: name id -> name; ``rules``: rule alert type -> message."""
+    h = cols["header"]
+    b = h["boot"]
+    ctx = asg.get(int(cols["asg"][i])) or [None] * 5
+    row = int(cols.get("row0", 0)) + i
+    eid = (h["first_seq"] + row) * h["world"] + h["rank"]
+    alt, msg, md = row_strings(cols, i)
+    f = int(cols["flags"][i])
+    base = dict(id=f"{b:x}-{eid}", device_assignment_id=ctx[0], device_id=ctx[1], customer_id=ctx[2],
+                area_id=ctx[3], asset_id=ctx[4], event_date=int(cols["date"][i]), received_date=h["recv_ms"],
+                alternate_id=alt, metadata=md)
+    et = int(cols["etype"][i])
+    nid = int(cols["name"][i])
+    name = names.get(nid, "") if nid != NO_NAME else ""
+    if et == EV_MEASUREMENT:
+        return DeviceMeasurement(name=name, value=float(cols["v0"][i]), **base)
+    if et == EV_LOCATION:
+        return DeviceLocation(latitude=float(cols["v0"][i]), longitude=float(cols["v1"][i]),
+                              elevation=float(cols["v2"][i]) if f & SEGF_HAS_ELEV else None, **base)
+    if et == EV_ALERT:
+        gen = bool(f & SEGF_GEN)
+        return DeviceAlert(source=AlertSource.System if gen else AlertSource.Device,
+                           level=_LEVELS[min(int(cols["level"][i]), 3)], type=name,
+                           message=(rules.get(name) or "") if gen else msg, **base)
+    # the engine's state changes are its presence scan (DevicePresenceManager.java:110-200)
+    return DeviceStateChange(attribute="presence", type="presence", previous_state="PRESENT",
+                             new_state="NOT_PRESENT", **base)

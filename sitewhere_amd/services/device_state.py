@@ -146,21 +146,51 @@ class DevicePresenceManager(threading.Thread):
         self._stop.set()
 
 
+def latest_state_rows(cols: dict) -> list[int]:
+    """Rows of a decoded engine batch that :meth:`DeviceStateManagement.merge_event` can keep: per
+    (assignment, location | measurement name | alert type) the row with the newest event date, the
+    later row on ties (merge order of the per-event path).  Vectorised: a 1M-row block materializes
+    one event per state slot, not one per row."""
+    import numpy as np
+    from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT
+    et = np.asarray(cols["etype"])
+    rows = np.flatnonzero((et == EV_MEASUREMENT) | (et == EV_LOCATION) | (et == EV_ALERT))
+    if not len(rows):
+        return []
+    asg = np.asarray(cols["asg"])[rows].astype(np.int64)
+    name = np.where(et[rows] == EV_LOCATION, 0, np.asarray(cols["name"])[rows].astype(np.int64) + 1)
+    key = (asg << 34) | (et[rows].astype(np.int64) << 32) | (name & 0xffffffff)
+    date = np.asarray(cols["date"])[rows].astype(np.int64)
+    order = np.lexsort((rows, date, key))              # by key, then date, then row
+    k = key[order]
+    last = np.ones(len(k), bool)
+    last[:-1] = k[1:] != k[:-1]
+    return [int(i) for i in np.sort(rows[order[last]])]
+
+
 class DeviceStateTenantEngine(MicroserviceTenantEngine):
     def tenant_initialize(self, monitor):
         ds = self.config.get("datastore", {"type": "memory"})
         self.management = DeviceStateManagement(create_store(ds.get("type", "memory"),
                                                              **{k: v for k, v in ds.items() if k != "type"}))
-        n = self.ms.instance.naming
-        self.consumer = BusConsumer(self, "device-state-enriched", [n.inbound_enriched_events(self.tenant.token)],
-                                    self._process)
+        from .enriched_batches import EnrichedBatchReader, enriched_topics
+        # per-event enriched records and engine tenants' enriched batches (one durable block per step)
+        self.reader = EnrichedBatchReader(self)
+        self.consumer = BusConsumer(self, "device-state-enriched", enriched_topics(self), self._process)
         pres = self.config.get("presence", {})
         self.presence = DevicePresenceManager(self, parse_period_ms(pres.get("checkInterval", "PT10M")),
                                               parse_period_ms(pres.get("missingInterval", "PT8H")))
         self.api = {"DeviceStateManagement": self.management}
 
     def _process(self, recs):
+        from .enriched_batches import is_batch
         for r in recs:
+            if is_batch(r.value):
+                # an engine batch: only the newest row of each state slot can change the state
+                cols = self.reader.columns(r.value)
+                for i in latest_state_rows(cols):
+                    self.management.merge_event(self.reader.event(cols, i), self.reader.context(cols, i))
+                continue
             ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
             self.management.merge_event(ev, ctx)
 

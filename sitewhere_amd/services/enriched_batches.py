@@ -1,0 +1,132 @@
+"""Engine tenants' enriched events for the enriched-event consumers.
+
+Reference: outbound connectors, rule processors and device state all consume the enriched topic
+(``KafkaOutboundConnectorHost.java:89``, ``KafkaRuleProcessorHost.java:89``,
+``DeviceStateEnrichedEventsConsumer.java:75``), fed one ``GEnrichedEventPayload`` per event by
+``OutboundPayloadEnrichmentLogic.java:54-92``.  An engine tenant (MI355X or native engine) publishes
+its persisted events per step instead: one durable block per batch on ``inbound-enriched-batches``
+(``services/gpu_inbound.py``; the same bytes the durable store writes), or a columnar row batch for
+memory tenants.  The consumers subscribe to both topics; :class:`EnrichedBatchReader` turns a batch
+record into the same ``(event, context)`` items a per-event record gives -- the whole event
+(alternate id, metadata, alert message) and the context the reference's enrichment adds (device
+id and token, device type, assignment status).
+
+A batch carries only the dictionary entries its receiver has not seen (assignment contexts, name
+ids).  A consumer group that starts later than the batch that carried an entry resolves it from
+event management's store (``DeviceEventManagement.durable_dictionary``), once per entry.
+
+Columnar consumers can ask for the decoded block instead (:meth:`EnrichedBatchReader.columns`) and
+materialize only the rows they keep (vectorised filters, threshold rules).
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from ..persistence import segments as sg
+
+BATCH_MAGICS = (b"SWD1", b"SWC1")
+
+
+def is_batch(value) -> bool:
+    """Is a record value an engine batch (durable block or columnar rows) rather than one event?"""
+    try:
+        return bytes(memoryview(value)[:4]) in BATCH_MAGICS
+    except TypeError:
+        return False
+
+
+class EnrichedBatchReader:
+    """Per-consumer expansion of engine batches (thread-safe; dictionaries cached per incarnation)."""
+
+    def __init__(self, engine):
+        self.engine = engine                    # the consuming tenant engine (event management access)
+        self._asg: dict[int, dict] = {}          # boot -> assignment index -> context list
+        self._names: dict[int, dict] = {}        # boot -> name id -> name
+        self._rules: dict[str, str] = {}
+        self._lock = threading.Lock()
+        self.rows = self.batches = self.resolved = 0
+
+    # ------------------------------------------------------------------ dictionaries
+    def _apply(self, boot: int, d: dict):
+        with self._lock:
+            self._asg.setdefault(boot, {}).update({int(k): v for k, v in (d.get("asg") or {}).items()})
+            self._names.setdefault(boot, {}).update({int(k): v for k, v in (d.get("names") or {}).items()})
+            self._rules.update(d.get("rules") or {})
+
+    def _resolve(self, boot: int, asg_ids, name_ids):
+        """Fetch the entries this consumer never saw a delta for (it started after their batch)."""
+        a, n = self._asg.setdefault(boot, {}), self._names.setdefault(boot, {})
+        miss_a = [int(x) for x in asg_ids if int(x) not in a and int(x) >= 0]
+        miss_n = [int(x) for x in name_ids if int(x) not in n and int(x) != sg.NO_NAME]
+        if not miss_a and not miss_n:
+            return
+        em = self.engine.ms.api("DeviceEventManagement", self.engine.tenant.token)
+        got = em.durable_dictionary(boot, miss_a, miss_n)
+        self.resolved += len(miss_a) + len(miss_n)
+        self._apply(boot, got)
+
+    # ------------------------------------------------------------------ batches
+    def columns(self, value) -> dict:
+        """Decoded block of a batch record with its dictionaries current: block columns + header
+        (see ``persistence.segments.decode_block``) and ``cols["asg_ctx"]`` / ``["names"]`` /
+        ``["rules"]`` for :func:`~sitewhere_amd.persistence.segments.materialize_row`."""
+        buf = memoryview(value).cast("B") if not isinstance(value, (bytes, bytearray)) else value
+        if bytes(buf[:4]) == b"SWD1":
+            d, blk = sg.decode_durable_batch(value)
+            cols = sg.decode_block(np.ascontiguousarray(blk), check=isinstance(value, (bytes, bytearray)))
+            boot = int(cols["header"]["boot"])
+        else:
+            from ..persistence.columnar import decode_batch
+            d = decode_batch(value)
+            rows = d["rows"]
+            boot = sg.boot_id(d["boot"])
+            n = len(rows)
+            cols = {"etype": rows["etype"], "level": rows["level"], "date": rows["event_date"],
+                    "asg": rows["assignment"], "name": rows["name_id"], "v0": rows["v0"], "v1": rows["v1"],
+                    "v2": np.zeros(n), "flags": np.zeros(n, np.uint8), "str_heap": None, "str_off": None,
+                    "row0": 0, "header": {"boot": boot, "first_seq": int(d["first_seq"]), "world": int(d["world"]),
+                                          "rank": int(d["rank"]), "recv_ms": int(d["now"]), "n_rows": n}}
+        self._apply(boot, d)
+        self._resolve(boot, np.unique(cols["asg"]), np.unique(cols["name"]))
+        cols["asg_ctx"], cols["names"], cols["rules"] = self._asg[boot], self._names[boot], self._rules
+        self.batches += 1
+        self.rows += len(cols["date"])
+        return cols
+
+    def context(self, cols: dict, i: int) -> dict:
+        """Enrichment context of row i (``OutboundPayloadEnrichmentLogic``: device and assignment)."""
+        ctx = cols["asg_ctx"].get(int(cols["asg"][i])) or []
+        return {"deviceId": ctx[1] if len(ctx) > 1 else None, "deviceToken": ctx[5] if len(ctx) > 5 else None,
+                "deviceTypeId": ctx[6] if len(ctx) > 6 else None, "assignmentStatus": "Active", "engine": "batch"}
+
+    def event(self, cols: dict, i: int):
+        return sg.materialize_row(cols, i, cols["asg_ctx"], cols["names"], cols["rules"])
+
+    def items(self, value, rows=None) -> list[tuple]:
+        """(event, context) of every row (or of ``rows``) of a batch record."""
+        cols = self.columns(value)
+        idx = range(len(cols["date"])) if rows is None else rows
+        return [(self.event(cols, int(i)), self.context(cols, int(i))) for i in idx]
+
+
+def expand_records(reader: EnrichedBatchReader, recs) -> list[tuple]:
+    """Records of the enriched topics -> (event, context) items, in record order: one per event
+    record (``GEnrichedEventPayload`` / JSON), every row of an engine batch record."""
+    from ..bus import payloads
+    items = []
+    for r in recs:
+        if is_batch(r.value):
+            items.extend(reader.items(r.value))
+        else:
+            ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
+            items.append((ev, ctx))
+    return items
+
+
+def enriched_topics(engine) -> list[str]:
+    """The enriched-event topics of a tenant: per-event records and engine batches."""
+    from .gpu_inbound import ENRICHED_BATCHES
+    n = engine.ms.instance.naming
+    return [n.inbound_enriched_events(engine.tenant.token), n.tenant_prefix(engine.tenant.token) + ENRICHED_BATCHES]

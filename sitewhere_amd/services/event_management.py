@@ -141,6 +141,12 @@ class DeviceEventManagement:
         f = getattr(self.store, "source_offset", None)
         return None if f is None else f(topic, int(partition))
 
+    def durable_dictionary(self, boot, asg_ids=(), name_ids=()) -> dict:
+        """Dictionary entries of an engine tenant's batches (see ``DurableEventStore.dictionary``):
+        enriched-batch consumers resolve the indices their batches' deltas did not carry."""
+        f = getattr(self.store, "dictionary", None)
+        return f(boot, asg_ids, name_ids) if f is not None else {"asg": {}, "names": {}, "rules": {}}
+
     def add_durable_batch(self, payload) -> tuple[int, int]:
         """Queue an engine tenant's durable batch: (rows, token).  The rows are on disk once
         :meth:`durable_token` reaches the token (-1: a replay the store already holds)."""

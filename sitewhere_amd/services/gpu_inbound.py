@@ -108,6 +108,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.customers, self.areas, self.assets = IndexMap(), IndexMap(), IndexMap()
         self._asg_entities: dict[int, object] = {}
         self._dev_tokens: dict[int, str] = {}
+        self._dev_types: dict[int, str] = {}
         self._nid2name: dict[int, str] = {}
         self._lock = threading.RLock()
         self.boot = f"{int(time.time() * 1000):x}"
@@ -263,6 +264,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             lo, hi = fingerprint_str(d.token)
             self.engine.register_devices(np.array([lo], np.uint64), np.array([hi], np.uint64), np.array([di], np.int32))
             self._dev_tokens[di] = d.token
+            self._dev_types[di] = d.device_type_id
 
     def _upsert_assignment(self, a):
         with self._lock:
@@ -711,9 +713,10 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     self._durable_wait.popleft()
                     self._finalize(item, commit)
             except Exception:
-                # nothing after the failure is durable: those batches are stored again on retry
+                # nothing after the failure is durable: those batches are stored again on retry (their
+                # enriched batches were published and their rejects routed already: not repeated)
                 for item, _ in self._durable_wait:
-                    item.stored = item.published = item.routed = False
+                    item.stored = False
                     item.token = None
                 self._durable_wait.clear()
                 raise
@@ -781,7 +784,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             for ai in self._asg_dirty:
                 a = self._asg_entities.get(ai)
                 if a is not None:
-                    asg[ai] = [a.id, a.device_id, a.customer_id, a.area_id, a.asset_id]
+                    # event context (reference MongoDeviceEvent) + what enriched-event consumers add
+                    # (device token and type, OutboundPayloadEnrichmentLogic.java:54-92)
+                    di = self.dev_index.idx.get(a.device_id, -1)
+                    asg[ai] = [a.id, a.device_id, a.customer_id, a.area_id, a.asset_id, self._dev_tokens.get(di),
+                               self._dev_types.get(di)]
             self._asg_dirty.clear()
             # the engine's host name dictionary grows when a step learns names or rules add alert
             # types (an np.unique over the rows' name ids cost ~10 ms per 1M-row batch)

@@ -20,7 +20,6 @@ from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleCompon
 from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
 from ..runtime.consumers import BusConsumer
 from ..runtime.microservice import MicroserviceTenantEngine, MultitenantMicroservice
-from ..bus import payloads
 
 
 class OutboundConnector(TenantEngineLifecycleComponent):
@@ -221,25 +220,28 @@ def build_connector(engine, cfg) -> OutboundConnector:
 
 class OutboundConnectorsTenantEngine(MicroserviceTenantEngine):
     def tenant_initialize(self, monitor):
-        self.connectors, self.hosts = [], []
-        topic = self.ms.instance.naming.inbound_enriched_events(self.tenant.token)
+        from .enriched_batches import EnrichedBatchReader, enriched_topics
+        self.connectors, self.hosts, self.readers = [], [], []
+        # per-event enriched records and engine tenants' enriched batches (one block per step)
+        topics = enriched_topics(self)
         for cc in self.config.get("connectors", []):
             c = build_connector(self, cc)
             c.tenant_engine = self
             self.initialize_nested_component(c, monitor, require=False)
             self.connectors.append(c)
-            self.hosts.append(BusConsumer(self, f"connector.{c.cid}", [topic], self._handler(c),
+            reader = EnrichedBatchReader(self)
+            self.readers.append(reader)
+            self.hosts.append(BusConsumer(self, f"connector.{c.cid}", topics, self._handler(c, reader),
                                           threads=int(cc.get("numProcessingThreads", 0))))
         self.api = {"OutboundConnectors": OutboundConnectorsApi(self)}
 
     @staticmethod
-    def _handler(c):
+    def _handler(c, reader):
+        from .enriched_batches import expand_records
+
         def handle(recs):
-            items = []
-            for r in recs:
-                ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
-                items.append((ev, ctx))
-            c.process_batch(items)
+            # processed before the consumer commits (at-least-once; the reference commits first)
+            c.process_batch(expand_records(reader, recs))
         return handle
 
     def tenant_start(self, monitor):

@@ -134,25 +134,24 @@ class RuleProcessingTenantEngine(MicroserviceTenantEngine):
     def tenant_initialize(self, monitor):
         self.processors = []
         self.hosts = []
-        topic = self.ms.instance.naming.inbound_enriched_events(self.tenant.token)
+        from .enriched_batches import EnrichedBatchReader, enriched_topics
+        topics = enriched_topics(self)          # per-event records + engine tenants' batches
         for pc in self.config.get("processors", []):
             p = build_processor(pc, self)
             p.tenant_engine = self
             self.initialize_nested_component(p, monitor, require=False)
             self.processors.append(p)
             # one consumer group per processor: each sees the full enriched stream
-            self.hosts.append(BusConsumer(self, f"rule-{p.pid}", [topic], self._handler(p),
+            self.hosts.append(BusConsumer(self, f"rule-{p.pid}", topics, self._handler(p, EnrichedBatchReader(self)),
                                           threads=int(pc.get("numThreads", 0))))
         self.api = {"RuleProcessing": RuleProcessingApi(self)}
 
     @staticmethod
-    def _handler(p: RuleProcessor):
+    def _handler(p: RuleProcessor, reader):
+        from .enriched_batches import expand_records
+
         def handle(recs):
-            items = []
-            for r in recs:
-                ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
-                items.append((ev, ctx))
-            p.process_batch(items)
+            p.process_batch(expand_records(reader, recs))
         return handle
 
     def tenant_start(self, monitor):

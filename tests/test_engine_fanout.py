@@ -1,0 +1,190 @@
+"""Engine tenants feed the enriched-event consumers (VERDICT r3 missing #2).
+
+The same device traffic goes to a per-event tenant (``default`` template: reference-shaped path,
+one enriched record per event) and to an engine tenant (``gpu-columnar``: fused engine, one durable
+block per step on ``inbound-enriched-batches``; the native CPU engine in this container).  Both
+tenants run a log outbound connector behind a script filter and a threshold rule processor.  Every
+event must reach the connector and the rule the same way on both templates: same events, same
+alternate ids, metadata and alert messages, same rule alerts.
+
+Reference: ``KafkaOutboundConnectorHost.java:89,144-217``, ``KafkaRuleProcessorHost.java:89``,
+``OutboundPayloadEnrichmentLogic.java:54-92``."""
+from __future__ import annotations
+
+import os
+import time
+
+import pytest
+
+from sitewhere_amd.models import wire
+from sitewhere_amd.runtime.config import dump_document
+
+FILTER = "def filter(event, context):\n    return event.get('eventType') == 'Measurement' and event.get('value', 0) < 10\n"
+THRESHOLD = {"id": "thr", "type": "threshold",
+             "rules": [{"measurement": "temp", "max": 250.0, "alertType": "temp.high", "alertLevel": "Error"}]}
+
+
+def wait_until(cond, timeout=30.0, step=0.02):
+    end = time.time() + timeout
+    while time.time() < end:
+        v = cond()
+        if v:
+            return v
+        time.sleep(step)
+    return cond()
+
+
+@pytest.fixture(scope="module")
+def sw(tmp_path_factory):
+    from sitewhere_amd.assembly import SiteWhereInstance
+    old = os.environ.get("SITEWHERE_DATA_DIR")
+    os.environ["SITEWHERE_DATA_DIR"] = str(tmp_path_factory.mktemp("fanout-data"))
+    from sitewhere_amd.edges.mqtt import MqttBroker, MqttClient
+    broker = MqttBroker().start()
+    sub = MqttClient("127.0.0.1", broker.port).connect()
+    inbox = []
+    sub.on_message(lambda t, p: inbox.append((t, bytes(p))))
+    sub.subscribe("fan/#", 1)
+    inst = SiteWhereInstance().start()
+    inst.mqtt_inbox = inbox
+    inst.wait_for_tenant("default", 60)
+    tm = inst.api("TenantManagement")
+    for token, template in (("pe", "default"), ("eng", "gpu-columnar")):
+        inst.instance.system_user.run(lambda: tm.create_tenant({"token": token, "name": token,
+                                                                "configurationTemplateId": template,
+                                                                "datasetTemplateId": "construction"}))
+        inst.wait_for_tenant(token, 60)
+        coord = inst.instance.coord
+        coord.put(inst.instance.tenant_conf_path(token, "outbound-connectors.json"), dump_document(
+            {"connectors": [{"id": "log1", "type": "log", "filters": [{"type": "script", "script": FILTER}]},
+                            {"id": "mq1", "type": "mqtt", "host": "127.0.0.1", "port": broker.port, "qos": 1,
+                             "topic": "fan/{tenant}/{eventType}", "filters": [{"type": "script", "script": FILTER}]}]}))
+        coord.put(inst.instance.tenant_conf_path(token, "rule-processing.json"),
+                  dump_document({"processors": [THRESHOLD]}))
+
+    def ready():
+        for token in ("pe", "eng"):
+            oc = inst.tenant_engine("outbound-connectors", token)
+            rp = inst.tenant_engine("rule-processing", token)
+            if not (oc is not None and rp is not None and len(oc.connectors) == 2 and rp.processors and
+                    oc.status.value == "Started" and rp.status.value == "Started"):
+                return False
+        return True
+    assert wait_until(ready, 60)
+    yield inst
+    inst.stop()
+    sub.disconnect()
+    broker.stop()
+    if old is None:
+        os.environ.pop("SITEWHERE_DATA_DIR", None)
+    else:
+        os.environ["SITEWHERE_DATA_DIR"] = old
+
+
+def traffic():
+    toks = [f"{t}-{i:03d}" for t in ("galaxytab", "meitrack", "raspberrypi") for i in range(3)]
+    msgs = []
+    for i in range(300):
+        tok = toks[i % len(toks)]
+        md = {"fw": f"1.{i % 4}", "site": f"s{i % 7}"} if i % 3 else {}
+        date = 1_700_000_000_000 + i
+        if i % 10 == 7:
+            msgs.append(wire.alert(tok, f"door.{i % 3}", f"door opened #{i}", event_date=date, alternate_id=f"fa-{i}",
+                                   metadata=md))
+        elif i % 10 == 9:
+            msgs.append(wire.location(tok, 34.1 + i / 1e5, -84.2, elevation=float(i), event_date=date,
+                                      alternate_id=f"fl-{i}", metadata=md))
+        else:
+            msgs.append(wire.measurements(tok, {"temp": float(i)}, event_date=date, alternate_id=f"fm-{i}",
+                                          metadata=md))
+    return msgs
+
+
+def _key(ev):
+    d = ev["event"]
+    return d.get("alternateId")
+
+
+def _content(ev):
+    d = dict(ev["event"])
+    for k in ("id", "receivedDate", "deviceAssignmentId", "deviceId", "customerId", "areaId", "assetId"):
+        d.pop(k, None)
+    return d
+
+
+def test_engine_tenant_events_reach_connectors_and_rules_like_per_event(sw):
+    msgs = traffic()
+    for token in ("pe", "eng"):
+        es = sw.tenant_engine("event-sources", token)
+        for m in msgs:
+            es.inject("default-protobuf", m)
+    # measurements with temp < 10 are filtered by the script: 300 - 10 delivered on each tenant
+    n_measure_lt10 = sum(1 for i in range(10) if i % 10 not in (7, 9))
+    want = 300 - n_measure_lt10
+    oc = {t: sw.tenant_engine("outbound-connectors", t).connectors[0] for t in ("pe", "eng")}
+    rp = {t: sw.tenant_engine("rule-processing", t).processors[0] for t in ("pe", "eng")}
+    for t in ("pe", "eng"):
+        assert wait_until(lambda: sum(str(e["event"].get("alternateId")).startswith("f") for e in oc[t].seen) >= want,
+                          60), (t, oc[t].delivered, want)
+    time.sleep(0.3)
+    # dataset bootstrap events and the rule's own alerts travel the same topics: same totals
+    assert oc["pe"].delivered == oc["eng"].delivered
+    assert oc["pe"].filtered == oc["eng"].filtered >= n_measure_lt10
+    mine = {t: [e for e in oc[t].seen if str(e["event"].get("alternateId")).startswith("f")] for t in ("pe", "eng")}
+    assert len(mine["pe"]) == len(mine["eng"]) == want
+    got = {t: {_key(e): _content(e) for e in mine[t]} for t in ("pe", "eng")}
+    assert set(got["pe"]) == set(got["eng"]) and len(got["pe"]) == want
+    for k in got["pe"]:
+        assert got["pe"][k] == got["eng"][k], (k, got["pe"][k], got["eng"][k])
+    # whole events on the engine path: metadata and alert messages arrive
+    assert got["eng"]["fa-17"]["message"] == "door opened #17" and got["eng"]["fa-17"]["metadata"] == {"fw": "1.1",
+                                                                                                       "site": "s3"}
+    assert got["eng"]["fl-19"]["elevation"] == 19.0
+    # the threshold rule saw every measurement: temp > 250 on both templates
+    n_high = sum(1 for i in range(251, 300) if i % 10 not in (7, 9))
+    for t in ("pe", "eng"):
+        assert wait_until(lambda: rp[t].alerts >= n_high, 30), (t, rp[t].alerts)
+    assert rp["pe"].alerts == rp["eng"].alerts == n_high
+    # the MQTT connector published the same JSON documents for both tenants
+    import json
+    mq = {t: {} for t in ("pe", "eng")}
+
+    def mqtt_done():
+        for topic, body in list(sw.mqtt_inbox):
+            d = json.loads(body)
+            alt = str(d["event"].get("alternateId"))
+            if alt.startswith("f"):
+                mq[topic.split("/")[1]][alt] = _content(d)
+        return all(len(mq[t]) == want for t in mq)
+    assert wait_until(mqtt_done, 30), {t: len(v) for t, v in mq.items()}
+    assert mq["pe"] == mq["eng"] == got["pe"]
+    # device state (the third enriched consumer) keeps the same newest events on both templates
+    toks = [f"{t}-{i:03d}" for t in ("galaxytab", "meitrack", "raspberrypi") for i in range(3)]
+    want_last = {}
+    for i in range(300):
+        kind = {7: ("alert", f"door.{i % 3}", "fa"), 9: ("location", None, "fl")}.get(i % 10, ("temp", "temp", "fm"))
+        want_last[(toks[i % 9], kind[0] if kind[0] != "alert" else kind[1])] = f"{kind[2]}-{i}"
+
+    def last_alts(t):
+        run = lambda f: sw.instance.system_user.run(f, t)  # noqa: E731
+        dm, em, dsm = (sw.api(s_, t) for s_ in ("DeviceManagement", "DeviceEventManagement", "DeviceStateManagement"))
+        out = {}
+        for tok in toks:
+            dev = run(lambda: dm.get_device_by_token(tok))
+            st = run(lambda: dsm.get_device_state_by_device_assignment_id(dev.device_assignment_id))
+            if st is None:
+                return None
+            alt = lambda eid: run(lambda: em.get_device_event_by_id(eid)).alternate_id  # noqa: E731
+            if st.last_location_event_id:
+                out[(tok, "location")] = alt(st.last_location_event_id)
+            for name, eid in st.last_measurement_event_ids.items():
+                out[(tok, name)] = alt(eid)
+            for typ, eid in st.last_alert_event_ids.items():
+                if typ.startswith("door"):
+                    out[(tok, typ)] = alt(eid)
+        return out
+    for t in ("pe", "eng"):
+        assert wait_until(lambda: last_alts(t) == want_last, 30), (t, last_alts(t))
+    # the engine's consumers resolved their dictionaries from the batches themselves
+    eng_reader = sw.tenant_engine("outbound-connectors", "eng").readers[0]
+    assert eng_reader.batches > 0 and eng_reader.rows >= 300

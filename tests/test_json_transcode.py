@@ -34,6 +34,15 @@ CASES = [
     (_j("dev-2", "DeviceAlert", {"type": "engine.hot", "message": "too hot \n \"x\"", "level": "Info",
                                  "source": "Device", "eventDate": 5}),
      wire.alert("dev-2", "engine.hot", "too hot \n \"x\"", event_date=5)),
+    (_j("d", "DeviceMeasurement", {"name": "t", "value": 1, "metadata": {"unit": "C", "s\u00e9": "x\"y"},
+                                   "alternateId": "jm-1", "updateState": True}),
+     wire.measurements("d", {"t": 1.0}, alternate_id="jm-1", metadata={"unit": "C", "s\u00e9": "x\"y"},
+                       update_state=True)),
+    (_j("d", "DeviceLocation", {"latitude": 1.5, "longitude": 2.5, "metadata": {"a": "1", "b": ""}}),
+     wire.location("d", 1.5, 2.5, metadata={"a": "1", "b": ""})),
+    (_j("d", "DeviceAlert", {"type": "x", "message": "m", "metadata": {"k": "v"}, "eventDate": 9, "alternateId": "ja"}),
+     wire.alert("d", "x", "m", event_date=9, alternate_id="ja", metadata={"k": "v"})),
+    (_j("d", "DeviceMeasurement", {"name": "t", "value": 2, "metadata": {}}), wire.measurements("d", {"t": 2.0})),
     (b'{ "type" : "DeviceMeasurement" ,\n "request": {"name": "\\ud83d\\ude00", "value": -1.5e3, "extra": [1, {"a": null}]},'
      b' "deviceToken": "dev-3", "unused": {"k": [true, false]} }',
      wire.measurements("dev-3", {"\U0001F600": -1500.0})),
@@ -48,7 +57,7 @@ def test_transcode_equals_the_protobuf_a_device_sends(j, pb):
     assert (js["deviceToken"], js["type"]) == (pr["deviceToken"], pr["type"])
     for k, v in js["request"].items():
         if k in ("name", "value", "latitude", "longitude", "elevation", "eventDate", "alternateId", "type",
-                 "message"):
+                 "message", "metadata", "updateState"):
             assert pr["request"].get(k) == (float(v) if k == "value" else v), k
 
 
@@ -57,7 +66,10 @@ STAYS = [
     b"{}",
     _j("d", "RegisterDevice", {"deviceTypeToken": "t"}),
     _j("d", "Acknowledge", {"response": "ok"}),
-    _j("d", "DeviceMeasurement", {"name": "t", "value": 1, "metadata": {"unit": "C"}}),
+    _j("d", "DeviceMeasurement", {"name": "t", "value": 1, "metadata": {"unit": 5}}),
+    _j("d", "DeviceMeasurement", {"name": "t", "value": 1, "metadata": {"unit": None}}),
+    _j("d", "DeviceMeasurement", {"name": "t", "value": 1, "metadata": ["unit"]}),
+    _j("d", "DeviceAlert", {"type": "x", "message": "m", "metadata": {"a": "b", "c": {"d": "e"}}}),
     _j("d", "DeviceMeasurement", {"name": "t", "value": "12.5"}),
     _j("d", "DeviceMeasurement", {"name": "t", "value": 1, "eventDate": "2024-01-01T00:00:00Z"}),
     _j("d", "DeviceMeasurement", {"name": "t", "value": 1, "eventDate": 1.5}),

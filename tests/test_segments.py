@@ -330,3 +330,30 @@ def test_block_sink_pool_bounded_and_commits_in_order(tmp_path):
     v = bus.read_views("t.out", 0, bus.begin_offset("t.out", 0), 1)[0].value
     assert sg.verify(np.frombuffer(v, np.uint8)) == 0
     store.close()
+
+
+def test_failed_append_is_retried_not_skipped_as_a_replay(tmp_path):
+    """the (boot, rank) high-water mark moves only once a block is queued.  A write that
+    fails is retried as a write; a replay of queued-but-not-durable rows returns the token that makes
+    them durable, and -1 only once they are on disk -- so a caller never commits offsets of rows that
+    are not on disk."""
+    es = sg.DurableEventStore(str(tmp_path / "es"))
+    blk = sg.encode_block(*synth_rows(2000, seed=11))
+    sg.seal(blk, 0, 1_700_000_100_000, 0xc0, 0, 1)
+    real = es.seg.append
+    calls = {"n": 0}
+
+    def failing(*a, **k):
+        calls["n"] += 1
+        raise OSError(5, "injected write failure")
+    es.seg.append = failing
+    with pytest.raises(OSError):
+        es.add_encoded(blk)
+    es.seg.append = real
+    tok = es.add_encoded(blk)                 # the retry writes the block (not a "replay" skip)
+    assert tok >= 0 and calls["n"] == 1
+    assert es.add_encoded(blk) in (tok, -1)   # a replay while queued: the same token (or -1 once durable)
+    es.wait(tok)
+    assert es.add_encoded(blk) == -1
+    assert es.rows == 2000
+    es.close()
