@@ -151,6 +151,7 @@ class EventHubAmqpReceiver(Receiver):
         self._lock = threading.Lock()
         self._t = None
         self.partitions: list[str] = []
+        self._owned: set = set()            # partitions this host reads (set before their link attaches)
 
     # ---- discovery
     def partition_ids(self) -> list[str]:
@@ -203,6 +204,7 @@ class EventHubAmqpReceiver(Receiver):
         share = -(-len(self.partitions) // max(1, len(self.checkpoints.hosts())))
         while len(self.links) > share:
             p = sorted(self.links)[-1]
+            self._owned.discard(p)
             lk = self.links.pop(p)
             with self._lock:
                 if p in self.last_offset:
@@ -216,11 +218,14 @@ class EventHubAmqpReceiver(Receiver):
                 continue
             start = self.checkpoints.get(p)
             addr = f"{self.hub}/ConsumerGroups/{self.group}/Partitions/{p}"
+            # owned before the attach: the hub may deliver as soon as the link has credit, before
+            # attach_receiver returns on this thread
+            self._owned.add(p)
             self.links[p] = self.conn.attach_receiver(addr, offset_filter(start), self.credit,
                                                       on_message=lambda m, f, p=p: self._on_event(p, m))
 
     def _on_event(self, p: str, msg: Message):
-        if p not in self.links:
+        if p not in self._owned:
             return                          # handed to another host: it resumes from the checkpoint
         ann = msg.annotations or {}
         off = ann.get(Symbol("x-opt-offset"), ann.get("x-opt-offset"))
@@ -261,6 +266,7 @@ class EventHubAmqpReceiver(Receiver):
         self.checkpoint()
         for p in list(self.links):
             self.checkpoints.release(p, self.owner)
+        self._owned.clear()
         self.links.clear()
         self.checkpoints.unregister(self.owner)
         if self.conn is not None:

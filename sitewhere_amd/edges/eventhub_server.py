@@ -50,6 +50,7 @@ class EventHubServer:
         self._stop = threading.Event()
         self.connections = 0
         self.auth_failures = 0
+        self.credited: set = set()          # partitions a receiver link has granted credit on
         self._t = None
 
     @property
@@ -180,6 +181,8 @@ class EventHubServer:
                             out = outs.get(int(f[4]))
                             if out is not None:
                                 out.credit = int(f[6] or 0)
+                                if out.partition is not None and out.credit > 0:
+                                    self.credited.add(out.partition)
                                 self._lock.notify_all()
                 elif code == TRANSFER:
                     if ins.get(int(f[0])) == "$management":

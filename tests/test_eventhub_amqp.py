@@ -80,8 +80,14 @@ def test_reads_every_partition_and_resumes_after_checkpoint():
         r2 = _receiver(srv, cps)
         r2.lifecycle_start(LifecycleProgressMonitor())
         assert _wait(lambda: len(r2.source.got) == 8)
-        time.sleep(0.3)
-        assert sorted(b for b, _ in r2.source.got) == sorted(f"ev-{i}".encode() for i in range(40, 48))
+        # a sentinel behind each partition's events: once all four arrive, any replay of events
+        # before the checkpoint (same partitions, earlier positions) would have arrived too
+        for p in "0123":
+            srv.send(p, f"end-{p}".encode())
+        assert _wait(lambda: sum(b.startswith(b"end-") for b, _ in r2.source.got) == 4)
+        assert sorted(b for b, _ in r2.source.got if not b.startswith(b"end-")) == \
+            sorted(f"ev-{i}".encode() for i in range(40, 48))
+        assert len(r2.source.got) == 12
         r2.lifecycle_stop(LifecycleProgressMonitor())
     finally:
         srv.stop()
@@ -141,8 +147,7 @@ def test_tenant_event_source_on_event_hubs():
         run(lambda: ms.management.update_tenant_configuration("default", doc))
         dm, em = sw.api("DeviceManagement", "default"), sw.api("DeviceEventManagement", "default")
         aid = run(lambda: dm.get_device_by_token("meitrack-001")).device_assignment_id
-        assert _wait(lambda: srv.connections >= 1, 30)
-        time.sleep(0.5)
+        assert _wait(lambda: srv.credited == {"0", "1"}, 30)     # both partition links receiving
         srv.send("1", wire.measurements("meitrack-001", {"hub.t": 3.5}), key="meitrack-001")
         assert _wait(lambda: any(m.name == "hub.t" for m in run(
             lambda: em.list_measurements_for_index("Assignment", [aid], {"pageSize": 0})).results), 30)
