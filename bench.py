@@ -431,6 +431,32 @@ def main():
         elapsed = float(tmax.item())
         ev, persisted, msgs, rule_alerts = (int(x) for x in t[1:].tolist())
     value = ev / elapsed
+    # ---- conservation: every decoded event is persisted or rejected (and every reject routed),
+    # every persisted row is in a durable block, every raw record committed -- summed over ranks
+    from sitewhere_amd.models.columnar import STAT_NAMES
+    cons = [s1[k] - s0[k] for k in STAT_NAMES]
+    cons.append(dur["sink"].rows - sk0[1] if dur else -1)
+    cons.append(bus_stats["routed"]["payloads"] - r0["payloads"] if bus_stats else -1)
+    if world > 1:
+        ct = torch.tensor(cons, dtype=torch.int64, device=torch.device("cuda", local) if use_gpu else "cpu")
+        dist.all_reduce(ct, op=dist.ReduceOp.SUM)
+        cons = [int(x) for x in ct.tolist()]
+    c = dict(zip(STAT_NAMES + ["durable_rows", "routed_payloads"], cons))
+    rejected = c["unregistered"] + c["unassigned"] + c["duplicates"] + c["decode_errors"] + c["control"]
+    checks = {"persisted == events - rejected + rule_alerts + presence":
+              c["persisted"] == c["events"] - rejected + c["rule_alerts"] + c["presence_events"],
+              "no dedup / state / shuffle overflow": c["dedup_overflow"] == 0 and c["state_overflow"] == 0
+              and c["shuffle_overflow"] == 0}
+    if dur:
+        checks["durable rows == persisted"] = c["durable_rows"] == c["persisted"]
+        checks["every block durable"] = bool(dur["sink"].store.durable() >= dur["sink"].store.seg.last_token)
+    if bus_stats:
+        checks["routed payloads == unregistered + unassigned + control + decode errors"] = \
+            c["routed_payloads"] == c["unregistered"] + c["unassigned"] + c["control"] + c["decode_errors"]
+        checks["raw topic fully committed"] = \
+            bus_stats["bus"].committed(bus_stats["group"], bus_stats["t_raw"], 0) == \
+            bus_stats["bus"].end_offset(bus_stats["t_raw"], 0)
+    conservation_ok = all(checks.values())
     detail = {
         "events": ev, "persisted": persisted, "payloads": msgs, "rule_alerts": rule_alerts,
         "persisted_per_sec": round(persisted / elapsed, 1),
@@ -444,6 +470,8 @@ def main():
         "backend": dist.get_backend() if world > 1 else None,
         "world": dist.get_world_size() if world > 1 else 1,
         "rank_elapsed_s": per_rank if per_rank is not None else [round(rank_elapsed, 6)],
+        "conservation": {"ok": conservation_ok, "failed": [k for k, v in checks.items() if not v],
+                         "checked": len(checks)},
     }
     if world > 1:
         from sitewhere_amd.parallel.sharding import exchange_bytes_per_rank
@@ -523,6 +551,11 @@ def main():
             shutil.rmtree(tmpdir, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
+    if not conservation_ok:
+        print(f"bench: conservation check failed on rank {rank}: {[k for k, v in checks.items() if not v]} {c}",
+              file=sys.stderr, flush=True)
+        return 1
+    return 0
 
 
 if __name__ == "__main__":

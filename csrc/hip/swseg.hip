@@ -440,17 +440,10 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
       cd.pad0 = 0;
       cd.pad1 = 0;
       if (!seg_is_double(c)) {
-        ull lo, hi;
-        if (c == SEG_ALTLEN) {            // remainder lengths: the alt length bounds minus the prefix
-          lo = seg_ord((int64_t)((uint32_t)L.res[2] - pfx));
-          hi = seg_ord((int64_t)((uint32_t)L.res[3] - pfx));
-        } else if (c == SEG_ALTNUM) {
-          lo = L.res[44];
-          hi = L.res[45];
-        } else {
-          lo = L.res[4 + 2 * c];
-          hi = L.res[5 + 2 * c];
-        }
+        const int slo = c == SEG_ALTLEN ? 2 : c == SEG_ALTNUM ? 44 : 4 + 2 * c;
+        const ull rlo = L.res[slo], rhi = L.res[slo + 1];
+        const ull lo = c == SEG_ALTLEN ? seg_ord((int64_t)rlo - (int64_t)pfx) : rlo;
+        const ull hi = c == SEG_ALTLEN ? seg_ord((int64_t)rhi - (int64_t)pfx) : rhi;
         cd.base = count ? lo : 0;
         cd.bits = (uint8_t)(count ? seg_bitwidth(hi - lo) : 0);
         cd.exp = -1;

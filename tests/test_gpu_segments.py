@@ -119,13 +119,15 @@ def test_gpu_block_every_string_form_matches_cpu():
     g = _encode_gpu(rows, recs, spans, raw, seed=3)
     c = sg.encode_block(rows, recs, spans, raw)
     _same_bytes(g, c)
-    cols = sg.decode_block(c)
+    cols = sg.decode_block(c, check=False)            # not sealed: no header checksum yet
     assert {int(f) & sg.SEGF_HAS_META for f in cols["flags"]} == {0, sg.SEGF_HAS_META}
 
 
 def _decoded_equal(cg, cc, what):
     """Two decoded blocks hold the same events (name ids aside: engine-local, compared by name)."""
-    assert cg["header"] == cc["header"], what
+    # name ids are engine-local, so page sizes (and the header checksum over the page table) may differ
+    strip = lambda h: {k: v for k, v in h.items() if k not in ("checksum", "bytes")}  # noqa: E731
+    assert strip(cg["header"]) == strip(cc["header"]), what
     for k in ("etype", "level", "date", "asg", "v0", "v1", "v2", "flags", "str_off"):
         np.testing.assert_array_equal(cg[k], cc[k], err_msg=f"{what}: column {k}")
     end = int(cc["str_off"][-1]) if cc["str_off"] is not None and len(cc["str_off"]) else 0
