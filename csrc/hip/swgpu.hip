@@ -27,6 +27,7 @@
 #include "swtypes.h"
 #include "swdecode.h"
 #include "swengine.h"
+#include "swseg.h"
 
 #define BLK 256
 #define WAVES (BLK / 64)
@@ -836,11 +837,13 @@ __device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t ma
 // the name probe and the state-map probe run once per event instead of once per pass.
 __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                           const int32_t* __restrict__ devs, const int32_t* __restrict__ asgs,
-                          const uint32_t* __restrict__ n_ptr, uint32_t cap) {
+                          const uint32_t* __restrict__ n_ptr, uint32_t cap, const SwStrRef* __restrict__ spans) {
   const uint32_t n = *n_ptr < cap ? *n_ptr : cap;     // generated events: n_gen may pass gen_cap
   const int64_t cur = *a.store_cursor;
   const int64_t c0 = *a.step_cursor0;
   const int64_t now = a.sp->now_ms;
+  SwSegAux* const aux = reinterpret_cast<SwSegAux*>(a.sp->aux);
+  const int64_t raw_bytes = a.sp->raw_bytes;
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const uint32_t i = idx ? idx[j] : (uint32_t)j;
     const SwEventRec r = R[i];
@@ -875,6 +878,15 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     o.etype = r.etype;
     o.level = r.level;
     a.sp->out[seq - c0] = o;
+    if (aux) {                   // the durable-block encoder's input, beside the row (coalesced)
+      SwStrRef sr;
+      if (spans) {
+        sr = spans[i];
+      } else {
+        sr.alt_off = 0; sr.meta_off = 0; sr.alt_len = 0; sr.meta_len = 0; sr.k = 0; sr.has = 0; sr.pad = 0;
+      }
+      aux[seq - c0] = seg_make_aux(r, sr, raw_bytes);
+    }
     // ---- state pass 1
     int64_t slot = -1;
     if (r.etype == SW_EV_MEASUREMENT || r.etype == SW_EV_LOCATION || r.etype == SW_EV_ALERT) {
@@ -1422,7 +1434,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, cmp_off, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx,
                                                a.n_ok, a.n_rej);
   // persist + enrich + state for the validated events
-  k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap);
+  k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap, a.spans);
   k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap);
   k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_ok);
   // rules on this step's persisted locations, then presence scan; generated events persist too
@@ -1444,23 +1456,26 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int gg = grid_for(a.gen_cap);
   const uint32_t gcap = (uint32_t)a.gen_cap;
   k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, gcap);
-  k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap);
+  k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap, nullptr);
   k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen, gcap);
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
 }
 
 __global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int64_t presence_ms,
-                                  SwOutRec* out) {
+                                  SwOutRec* out, void* aux, int64_t raw_bytes) {
   if (threadIdx.x == 0 && BID == 0) {
     sp->now_ms = now_ms; sp->batch_seq = batch_seq; sp->presence_missing_ms = presence_ms; sp->out = out;
+    sp->aux = aux; sp->raw_bytes = raw_bytes;
   }
 }
 
 // Stream-ordered write of this step's params (before the decode / process phases of the step).
+// aux: SwSegAux per row for the durable-block encoder (null: not encoding); raw_bytes: the bound of
+// the batch's strings (0 when rows carry none).
 int sw_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int64_t presence_ms, void* out,
-                       hipStream_t s) {
-  k_set_step_params<<<1, 64, 0, s>>>(sp, now_ms, batch_seq, presence_ms, (SwOutRec*)out);
+                       void* aux, int64_t raw_bytes, hipStream_t s) {
+  k_set_step_params<<<1, 64, 0, s>>>(sp, now_ms, batch_seq, presence_ms, (SwOutRec*)out, aux, raw_bytes);
   return (int)hipGetLastError();
 }
 

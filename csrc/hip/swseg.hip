@@ -2,43 +2,42 @@
 // block (format: csrc/include/swseg.h), written into HBM so only the compressed bytes cross PCIe
 // to the segment store.  Bit-identical to the CPU encoder (csrc/native/swseg.cpp, swseg_encode).
 //
-// Input per row j of the step: the enriched row (rows[j]), its decoded record -- work[ok_idx[j]]
-// for the validated events, gen[j - n_ok] for the generated ones -- and, for device events, the
-// record's string refs (spans) into the raw batch still resident in HBM.  The strings (alternate id,
-// alert message, metadata span) are copied from the raw batch into the page's string heap here.
+// Input per row j of the step, both written coalesced in persisted order by the persist kernel: the
+// enriched row (rows[j], 32 B) and its encoder aux (aux[j], SwSegAux 32 B: elevation, SEG_FLAGS and
+// the string refs into the raw batch, which is still resident in HBM).  No record is gathered here.
 //
 // One 256-thread workgroup (4 wave64) per 1024-row page, 4 consecutive rows per thread.  The plan
 // is a few fused block-wide rounds instead of one scan / reduction per column:
-//   R1  first row with an alternate id; per double column the decimal exponent (max of the rows'
-//       exponents, searched from a per-column hint: ~2 trials per value instead of up to 16)
-//   R2  alternate-id common prefix + hex test (one LCP / last-non-hex / length reduction), every
-//       integer column's min / max, the double columns' quantised min / max
+//   R1  first row with an alternate id (its first 64 bytes staged in LDS); per double column the
+//       decimal exponent (max of the rows' exponents, searched from a per-column hint)
+//   R2  alternate ids read with aligned 8-byte loads (all four rows' loads in flight at once): common
+//       prefix with the first id (word xor + ctz), last non-hex byte and the value of the trailing hex
+//       digits in one register pass; every integer column's min / max; quantised double min / max
 //   R3  one multi-column scan: member indices of all 15 columns, exception indices, heap offsets
-// then thread 0 lays the page out and finds its offset in the block with a single-pass decoupled
-// look-back (ticketed workgroups, 64-bit flag|value state words).  The write stages two columns at
-// a time in LDS (each thread assembles whole u64 words: no atomics, coalesced 8-byte stores) and
-// gathers the string heap word by word straight from the raw batch; every word is folded into the
-// page checksum on the way out.  The grid is sized for the largest step; surplus tickets exit.
+// then thread 0 lays the page out and wave 0 finds the page's offset in the block with a decoupled
+// look-back that reads 64 predecessors per round (ballot for the nearest inclusive prefix).  The
+// write stages two columns at a time in LDS (each thread assembles whole u64 words: coalesced 8-byte
+// stores); the string heap is assembled in LDS by each row's owner (8-byte source loads) and written
+// out word by word.  Every word is folded into the page checksum on the way out.  The grid is sized
+// for the largest step; surplus tickets exit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "swtypes.h"
 #include "swseg.h"
 
 #define SBLK 256
 #define SWAVES (SBLK / 64)
 #define RPT 4
+#define HEAP_LDS 26624     // heap bytes a page can stage in LDS (the column staging union); larger heaps
+                           // are gathered straight from the raw batch
 
 typedef unsigned long long ull;
 
 struct SwSegArgs {
-  const SwOutRec* rows;        // this step's rows (device)
-  const SwEventRec* work;      // validated records of the step
-  const uint32_t* ok_idx;      // row j < *n_ok <-> work[ok_idx[j]]
-  const uint32_t* n_ok;
-  const SwEventRec* gen;       // row j >= *n_ok <-> gen[j - n_ok]
-  const SwStrRef* spans;       // string refs of the work records (null: none carry strings)
-  const uint8_t* raw;          // the batch the work records were decoded from (null: no strings)
-  int64_t raw_bytes;
+  const SwOutRec* rows;        // this step's rows (device), persisted order
+  const SwSegAux* aux;         // their encoder aux (device), same order
+  const uint8_t* raw;          // the batch the rows were decoded from (null: no row has strings)
   const int64_t* cursor;       // [store_cursor, step_cursor0]: rows = cursor[0] - cursor[1]
   uint8_t* out;                // block (device)
   int64_t out_cap;
@@ -68,6 +67,61 @@ __device__ __forceinline__ ull wxor(ull v) {
   for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
   return v;
 }
+__device__ __forceinline__ ull wsum(ull v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Bytes [off, off + n) of the raw batch (n <= 64) as 8 words, w[k] = bytes 8k .. 8k+7, zero past n.
+// Aligned 8-byte loads of only the words the span touches (never past its last word).
+__device__ __forceinline__ void load_words8(const uint8_t* raw, uint32_t off, uint32_t n, ull (&w)[8]) {
+  const ull* src = reinterpret_cast<const ull*>(raw + (off & ~7u));
+  const uint32_t sh = (off & 7u) * 8u;
+  const uint32_t nsrc = ((off & 7u) + n + 7u) >> 3;      // source words the span touches (<= 9)
+  ull cur = nsrc > 0 ? src[0] : 0ull;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const ull nxt = (uint32_t)(k + 1) < nsrc ? src[k + 1] : 0ull;
+    ull v = sh ? ((cur >> sh) | (nxt << (64u - sh))) : cur;
+    const uint32_t b = 8u * (uint32_t)k;
+    v = b >= n ? 0ull : (b + 8u > n ? (v & (~0ull >> (64u - 8u * (n - b)))) : v);
+    w[k] = v;
+    cur = nxt;
+  }
+}
+
+// One <= 64-byte chunk of an alternate id (bytes base .. base + n of it): last non-hex byte (+1,
+// absolute) and the value of the trailing lowercase-hex digits (the last 16 of them).
+__device__ __forceinline__ void hex_scan(const ull (&w)[8], uint32_t n, uint32_t base, uint32_t& last, ull& tail) {
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    if ((uint32_t)i < n) {
+      const uint32_t c = (uint32_t)(w[i >> 3] >> (8 * (i & 7))) & 0xffu;
+      const bool dig = c - 48u < 10u, af = c - 97u < 6u;
+      if (dig || af) {
+        tail = (tail << 4) | (ull)(dig ? c - 48u : c - 87u);
+      } else {
+        last = base + (uint32_t)i + 1u;
+        tail = 0;
+      }
+    }
+  }
+}
+
+// raw bytes [off, off + n) -> LDS bytes dst[0 .. n) (aligned 8-byte source loads, two in flight)
+__device__ __forceinline__ void copy_to_lds(const uint8_t* raw, uint32_t off, uint32_t n, uint8_t* dst) {
+  const uint32_t end = off + n;
+  for (uint32_t wa = off & ~7u; wa < end; wa += 16u) {
+    const ull v0 = *reinterpret_cast<const ull*>(raw + wa);
+    const ull v1 = wa + 8u < end ? *reinterpret_cast<const ull*>(raw + wa + 8u) : 0ull;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const uint32_t p = wa + (uint32_t)b;
+      if (p >= off && p < end) dst[p - off] = (uint8_t)((b < 8 ? v0 : v1) >> (8 * (b & 7)));
+    }
+  }
+}
 
 // ----------------------------------------------------------------------------- page row
 struct SRow {
@@ -78,6 +132,8 @@ struct SRow {
   uint8_t et, level;
   SegRowStr s;
   bool valid;
+  uint32_t lnh;      // alternate id: last non-hex byte + 1
+  ull tail;          // alternate id: value of its trailing hex digits (last 16)
 };
 
 // integer value (order-preserving unsigned) of column c; altnum given by the caller
@@ -114,9 +170,12 @@ __device__ __forceinline__ bool smem(int c, const SRow& r, int mode) {
 #define NSLOT 48
 
 // Columns are written two at a time; no pair holds two double columns (one exception stage).
-__device__ static const int8_t seg_pairs[8][2] = {{SEG_ETYPE, SEG_LEVEL}, {SEG_DATE, SEG_ASG}, {SEG_NAME, SEG_MXV},
-                                                  {SEG_LAT, SEG_FLAGS},   {SEG_LON, SEG_ALTK}, {SEG_ELEV, SEG_ALTLEN},
-                                                  {SEG_ALTNUM, SEG_MSGLEN}, {SEG_METALEN, -1}};
+__device__ __forceinline__ constexpr int seg_pair(int pr, int g) {
+  return pr == 0 ? (g ? SEG_LEVEL : SEG_ETYPE) : pr == 1 ? (g ? SEG_ASG : SEG_DATE)
+       : pr == 2 ? (g ? SEG_MXV : SEG_NAME) : pr == 3 ? (g ? SEG_FLAGS : SEG_LAT)
+       : pr == 4 ? (g ? SEG_ALTK : SEG_LON) : pr == 5 ? (g ? SEG_ALTLEN : SEG_ELEV)
+       : pr == 6 ? (g ? SEG_MSGLEN : SEG_ALTNUM) : (g ? -1 : SEG_METALEN);
+}
 
 struct SegLds {
   ull red[SWAVES][NSLOT];      // per-wave partial reductions
@@ -125,13 +184,14 @@ struct SegLds {
   uint16_t pre[NCNT][SBLK];    // exclusive member / exception prefixes of each thread
   uint32_t hpre[SBLK];         // exclusive heap-byte prefix of each thread
   uint32_t tot[NCNT + 1];
-  // staging (two columns, one exception list), or the heap gather tables
+  // staging (two columns, one exception list), or the staged string heap, or the heap gather tables
   union {
     struct {
       ull vals[2][SEG_PAGE_ROWS];
       ull xraw[SEG_PAGE_ROWS];
       uint16_t xidx[SEG_PAGE_ROWS];
     } st;
+    uint8_t heap[HEAP_LDS];
     struct {
       uint32_t hoff[SEG_PAGE_ROWS + 1];    // row heap offsets (after the prefix)
       uint32_t src[SEG_PAGE_ROWS][3];      // alt remainder / msg / meta source offsets in raw
@@ -139,10 +199,11 @@ struct SegLds {
     } hp;
   } u;
   SwSegPageHdr hdr;
+  ull falt[8];                 // the page's first alternate id, bytes 0 .. 63 (the prefix source)
   int first_alt;
   uint32_t alt_off0, alt_len0;
   uint32_t page;
-  ull page_base;
+  ull page_base, page_size;
   int exps[NDBL];
 };
 
@@ -171,13 +232,6 @@ __device__ __forceinline__ void block_finish(SegLds& L, int ns, uint64_t maxmask
     L.res[i] = r;
   }
   __syncthreads();
-}
-
-// hex value of a row's alternate-id remainder
-__device__ __forceinline__ ull alt_hex(const uint8_t* raw, const SRow& r, uint32_t pfx) {
-  ull v = 0;
-  for (uint32_t i = pfx; i < r.s.alt_len; ++i) v = (v << 4) | seg_hex_value(raw[r.s.alt_off + i]);
-  return v;
 }
 
 __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
@@ -211,20 +265,20 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   if ((int64_t)page >= np) return;
   const int64_t r0 = (int64_t)page * SEG_PAGE_ROWS;
   const int m = (int)(n - r0 < SEG_PAGE_ROWS ? n - r0 : SEG_PAGE_ROWS);
-  const uint32_t nok = *a.n_ok;
-  const int64_t rawb = a.raw ? a.raw_bytes : 0;
-
-  // ---- load 4 consecutive rows per thread: enriched row, record, string refs
+  // ---- load 4 consecutive rows per thread: enriched row + encoder aux (both coalesced)
   SRow R[RPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int idx = RPT * (int)threadIdx.x + k;
     SRow& r = R[k];
     r.valid = idx < m;
+    r.lnh = 0;
+    r.tail = 0;
     if (r.valid) {
       const int64_t j = r0 + idx;
       const uint4 q0 = *reinterpret_cast<const uint4*>(&a.rows[j]);
       const uint4 q1 = *(reinterpret_cast<const uint4*>(&a.rows[j]) + 1);
+      const SwSegAux x = a.aux[j];
       r.date = (int64_t)(((ull)q0.y << 32) | q0.x);
       r.v0 = sw_bits_f64(((ull)q0.w << 32) | q0.z);
       r.v1 = sw_bits_f64(((ull)q1.y << 32) | q1.x);
@@ -232,18 +286,12 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
       r.name = (uint16_t)(q1.w & 0xffffu);
       r.et = (uint8_t)((q1.w >> 16) & 0xffu);
       r.level = (uint8_t)(q1.w >> 24);
-      SwStrRef sp;
-      sp.alt_off = 0; sp.meta_off = 0; sp.alt_len = 0; sp.meta_len = 0; sp.k = 0; sp.has = 0; sp.pad = 0;
-      const SwEventRec* rec;
-      if (j < (int64_t)nok) {
-        const uint32_t i = a.ok_idx[j];
-        rec = a.work + i;
-        if (a.spans) sp = a.spans[i];
-      } else {
-        rec = a.gen + (j - nok);
+      r.v2 = x.v2;
+      r.s = seg_aux_strings(x);
+      if (!a.raw) {                      // no batch: no strings (the CPU encoder without raw)
+        r.s.flags &= ~(uint32_t)(SEGF_HAS_ALT | SEGF_HAS_META);
+        r.s.alt_off = r.s.alt_len = r.s.meta_off = r.s.meta_len = r.s.msg_off = r.s.msg_len = r.s.altk = 0;
       }
-      r.v2 = rec->v2;
-      r.s = seg_row_strings(*rec, sp, rawb);
     } else {
       r.date = 0; r.v0 = r.v1 = r.v2 = 0.0; r.asg = 0; r.name = 0; r.et = 0; r.level = 0;
       r.s.alt_off = r.s.alt_len = r.s.msg_off = r.s.msg_len = r.s.meta_off = r.s.meta_len = r.s.altk = r.s.flags = 0;
@@ -278,14 +326,21 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     // the row's owner publishes the first alternate id's location
     const int fa = L.res[0] == ~0ull ? -1 : (int)L.res[0];
     if (fa >= 0 && fa / RPT == (int)threadIdx.x) {
+      uint32_t o0 = 0, l0 = 0;
 #pragma unroll
       for (int k = 0; k < RPT; ++k)
-        if (RPT * (int)threadIdx.x + k == fa) { L.alt_off0 = R[k].s.alt_off; L.alt_len0 = R[k].s.alt_len; }
+        if (RPT * (int)threadIdx.x + k == fa) { o0 = R[k].s.alt_off; l0 = R[k].s.alt_len; }
+      L.alt_off0 = o0;
+      L.alt_len0 = l0;
+      ull fw[8];
+      load_words8(a.raw, o0, l0 < SEG_ALT_PFX_MAX ? l0 : SEG_ALT_PFX_MAX, fw);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) L.falt[k] = fw[k];
     }
     __syncthreads();
   }
   const int first_alt = L.first_alt;
-  const uint32_t a_off0 = first_alt >= 0 ? L.alt_off0 : 0u, a_len0 = first_alt >= 0 ? L.alt_len0 : 0u;
+  const uint32_t a_len0 = first_alt >= 0 ? L.alt_len0 : 0u;
 
   // ---- R2: alternate-id prefix / hex test; integer min / max; quantised double min / max
   // slots: [0] min LCP, [1] max last-non-hex+1, [2] min alt len, [3] max alt len,
@@ -294,22 +349,45 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   {
     const uint32_t plim = a_len0 < SEG_ALT_PFX_MAX ? a_len0 : SEG_ALT_PFX_MAX;
     ull lcp = ~0ull, lnh = 0, lmin = ~0ull, lmax = 0;
+    // first 64 bytes of every row's id: all four rows' loads issued before any is used
+    ull W[RPT][8];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const SRow& r = R[k];
+      const bool has = r.valid && (r.s.flags & SEGF_HAS_ALT);
+      const uint32_t n = has ? (r.s.alt_len < 64u ? r.s.alt_len : 64u) : 0u;
+      load_words8(a.raw, has ? r.s.alt_off : 0u, n, W[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      SRow& r = R[k];
       if (!(r.valid && (r.s.flags & SEGF_HAS_ALT))) continue;
-      const uint8_t* sa = a.raw + r.s.alt_off;
-      const uint8_t* s0 = a.raw + a_off0;
-      const uint32_t lim = plim < r.s.alt_len ? plim : r.s.alt_len;
-      uint32_t l = 0;
-      while (l < lim && sa[l] == s0[l]) ++l;
-      lcp = (ull)l < lcp ? (ull)l : lcp;
+      const uint32_t len = r.s.alt_len;
+      // common prefix with the first id: first differing byte of the word xor
+      uint32_t l = plim < len ? plim : len;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const ull x = W[k][q] ^ L.falt[q];
+        if (x) {
+          const uint32_t d = 8u * (uint32_t)q + ((uint32_t)__builtin_ctzll(x) >> 3);
+          l = d < l ? d : l;
+        }
+      }
       uint32_t last = 0;
-      for (uint32_t i = 0; i < r.s.alt_len; ++i)
-        if (!seg_is_hex_digit(sa[i])) last = i + 1;
+      ull tail = 0;
+      hex_scan(W[k], len < 64u ? len : 64u, 0u, last, tail);
+      for (uint32_t base = 64; base < len; base += 64) {      // ids longer than 64 bytes (rare)
+        ull w[8];
+        const uint32_t n = len - base < 64u ? len - base : 64u;
+        load_words8(a.raw, r.s.alt_off + base, n, w);
+        hex_scan(w, n, base, last, tail);
+      }
+      r.lnh = last;
+      r.tail = tail;
+      lcp = (ull)l < lcp ? (ull)l : lcp;
       lnh = (ull)last > lnh ? (ull)last : lnh;
-      lmin = (ull)r.s.alt_len < lmin ? (ull)r.s.alt_len : lmin;
-      lmax = (ull)r.s.alt_len > lmax ? (ull)r.s.alt_len : lmax;
+      lmin = (ull)len < lmin ? (ull)len : lmin;
+      lmax = (ull)len > lmax ? (ull)len : lmax;
     }
     wave_put(L, 0, lcp, false);
     wave_put(L, 1, lnh, true);
@@ -362,7 +440,8 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   ull altnum[RPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k)
-    altnum[k] = (mode == SEG_ALT_HEX && R[k].valid && (R[k].s.flags & SEGF_HAS_ALT)) ? alt_hex(a.raw, R[k], pfx) : 0;
+    altnum[k] = (mode == SEG_ALT_HEX && R[k].valid && (R[k].s.flags & SEGF_HAS_ALT))
+                    ? (width >= 16u ? R[k].tail : (R[k].tail & ((1ull << (4u * width)) - 1ull))) : 0ull;
   {
     const uint32_t lane = lane64(), wid = threadIdx.x >> 6;
     uint32_t hb = 0;
@@ -472,43 +551,58 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     H.date_max = seg_unord(L.res[5 + 2 * SEG_DATE]);
     H.bytes = off + ((heap + 7u) & ~7u);
     H.checksum = 0;
-    const ull size = H.bytes;
+    L.page_size = H.bytes;
+  }
+  __syncthreads();
+  // ---- the page's offset in the block: decoupled look-back by wave 0, 64 predecessors per round
+  if (threadIdx.x < 64) {
+    const uint32_t lane = lane64();
+    const ull size = L.page_size;
     ull excl = 0;
     bool failed = false;
     if (page == 0) {
-      lb_store(&a.state[0], LB_INC | size);
+      if (lane == 0) lb_store(&a.state[0], LB_INC | size);
     } else {
-      lb_store(&a.state[page], LB_AGG | size);
-      for (int64_t p = (int64_t)page - 1; p >= 0;) {
-        ull s = lb_load(&a.state[p]);
+      if (lane == 0) lb_store(&a.state[page], LB_AGG | size);
+      int64_t p = (int64_t)page - 1;
+      while (true) {
+        const int64_t q = p - (int64_t)lane;              // lane 0 = the nearest predecessor
+        ull st = q >= 0 ? lb_load(&a.state[q]) : LB_INC;  // before page 0: an empty inclusive prefix
         uint32_t spins = 0;
-        while ((s >> 62) == 0) {
+        while (__any((st >> 62) == 0)) {                  // wait until the whole window is published
           if (++spins > LB_SPIN_LIMIT) { failed = true; break; }
           __builtin_amdgcn_s_sleep(1);
-          s = lb_load(&a.state[p]);
+          if ((st >> 62) == 0) st = lb_load(&a.state[q]);
         }
         if (failed) break;
-        excl += s & LB_VAL;
-        if ((s >> 62) == 2) break;
-        --p;
+        const ull inc = __ballot((st >> 62) == 2);
+        if (inc) {                                         // nearest inclusive prefix: stop there
+          const int first = __ffsll((long long)inc) - 1;
+          excl += wsum((int)lane <= first ? (st & LB_VAL) : 0ull);
+          break;
+        }
+        excl += wsum(st & LB_VAL);
+        p -= 64;
       }
-      lb_store(&a.state[page], LB_INC | (excl + size));
+      if (lane == 0 && !failed) lb_store(&a.state[page], LB_INC | (excl + size));
     }
-    const ull base = (ull)data_start + excl;
-    if (failed || base + size > (ull)a.out_cap) {
-      atomicAdd((ull*)errors, 1ull);
-      atomicMax((ull*)bytes_out, ~0ull);
-      L.page_base = ~0ull;
-    } else {
-      L.page_base = base;
-      page_off[page] = (uint32_t)base;
-      if ((int64_t)page == np - 1) {
-        page_off[np] = (uint32_t)(base + size);
-        SwSegBlockHdr* h = reinterpret_cast<SwSegBlockHdr*>(a.out);
-        h->n_rows = (uint32_t)n;
-        h->n_pages = (uint32_t)np;
-        h->bytes = base + size;
-        atomicMax((ull*)bytes_out, base + size);
+    if (lane == 0) {
+      const ull base = (ull)data_start + excl;
+      if (failed || base + size > (ull)a.out_cap) {
+        atomicAdd((ull*)errors, 1ull);
+        atomicMax((ull*)bytes_out, ~0ull);
+        L.page_base = ~0ull;
+      } else {
+        L.page_base = base;
+        page_off[page] = (uint32_t)base;
+        if ((int64_t)page == np - 1) {
+          page_off[np] = (uint32_t)(base + size);
+          SwSegBlockHdr* h = reinterpret_cast<SwSegBlockHdr*>(a.out);
+          h->n_rows = (uint32_t)n;
+          h->n_pages = (uint32_t)np;
+          h->bytes = base + size;
+          atomicMax((ull*)bytes_out, base + size);
+        }
       }
     }
   }
@@ -517,11 +611,13 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   uint8_t* pg = a.out + L.page_base;
   ull cs = 0;
 
-  // ---- write the columns, two at a time through LDS
-  for (int pr = 0; pr < 8; ++pr) {
+  // ---- write the columns, two at a time through LDS.  One instantiation per pair: every column
+  // index is a compile-time constant, so the rows' fields are selected statically (in registers)
+  auto write_pair = [&](auto PR) {
+    constexpr int pr = decltype(PR)::value;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const int c = seg_pairs[pr][g];
+      const int c = seg_pair(pr, g);
       if (c < 0) break;
       const SwSegCol& cd = L.hdr.cols[c];
       uint32_t i = L.pre[c][threadIdx.x];
@@ -549,7 +645,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     __syncthreads();
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const int c = seg_pairs[pr][g];
+      const int c = seg_pair(pr, g);
       if (c < 0) break;
       const SwSegCol cd = L.hdr.cols[c];
       const uint32_t bits = cd.bits, cnt = cd.count;
@@ -586,11 +682,55 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
       }
     }
     __syncthreads();         // the next pair reuses the staging arrays
-  }
+  };
+  write_pair(std::integral_constant<int, 0>{});
+  write_pair(std::integral_constant<int, 1>{});
+  write_pair(std::integral_constant<int, 2>{});
+  write_pair(std::integral_constant<int, 3>{});
+  write_pair(std::integral_constant<int, 4>{});
+  write_pair(std::integral_constant<int, 5>{});
+  write_pair(std::integral_constant<int, 6>{});
+  write_pair(std::integral_constant<int, 7>{});
 
-  // ---- string heap: row sources into LDS, then a word-parallel gather from the raw batch
+  // ---- string heap
   const uint32_t heap_bytes = L.hdr.heap_bytes;
-  if (heap_bytes) {
+  if (heap_bytes && heap_bytes <= HEAP_LDS) {
+    // staged in LDS: each thread copies its rows' strings to its heap prefix; the page's first
+    // alternate id supplies the common prefix; the tail is zero-padded to a word
+    uint8_t* hp = L.u.heap;
+    const uint32_t hend = (heap_bytes + 7u) & ~7u;
+    if (threadIdx.x < pfx) hp[threadIdx.x] = (uint8_t)(L.falt[threadIdx.x >> 3] >> (8u * (threadIdx.x & 7u)));
+    if (threadIdx.x < hend - heap_bytes) hp[heap_bytes + threadIdx.x] = 0;
+    uint32_t h = pfx + L.hpre[threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const SRow& r = R[k];
+      if (!r.valid) continue;
+      if (mode == SEG_ALT_RAW && (r.s.flags & SEGF_HAS_ALT)) {
+        const uint32_t nb = r.s.alt_len - pfx;
+        copy_to_lds(a.raw, r.s.alt_off + pfx, nb, hp + h);
+        h += nb;
+      }
+      if (r.s.msg_len) {
+        copy_to_lds(a.raw, r.s.msg_off, r.s.msg_len, hp + h);
+        h += r.s.msg_len;
+      }
+      if (r.s.meta_len) {
+        copy_to_lds(a.raw, r.s.meta_off, r.s.meta_len, hp + h);
+        h += r.s.meta_len;
+      }
+    }
+    __syncthreads();
+    const uint32_t hbase = L.hdr.heap_off;
+    const ull* h64 = reinterpret_cast<const ull*>(hp);
+    for (uint32_t w = threadIdx.x; w < (hend >> 3); w += SBLK) {
+      const ull word = h64[w];
+      const uint32_t off = hbase + 8u * w;
+      *reinterpret_cast<ull*>(pg + off) = word;
+      cs ^= seg_mix_word(word, off >> 3);
+    }
+  } else if (heap_bytes) {
+    // larger than LDS: row sources into LDS, then a word-parallel gather from the raw batch
     {
       uint32_t h = L.hpre[threadIdx.x];
 #pragma unroll
@@ -639,7 +779,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
         if (b >= heap_bytes) break;
         uint8_t byte;
         if (b < pfx) {
-          byte = a.raw[a_off0 + b];
+          byte = (uint8_t)(L.falt[b >> 3] >> (8u * (b & 7u)));
         } else {
           // advance to the row / segment holding this byte
           while (row < m && rel >= (uint32_t)L.u.hp.len[row][0] + L.u.hp.len[row][1] + L.u.hp.len[row][2]) {
@@ -684,20 +824,14 @@ extern "C" {
 // Encode this step's rows into `out`.  state = u64[max_pages + 4], zeroed here (a memset node when
 // captured); afterwards state[max_pages + 1] = block bytes (~0 on error), state[max_pages + 2] = errors,
 // state[max_pages + 3] = the store sequence of the block's first row.
-int sw_seg_encode(const void* rows, const void* work, const uint32_t* ok_idx, const uint32_t* n_ok, const void* gen,
-                  const void* spans, const uint8_t* raw, int64_t raw_bytes, const int64_t* cursor, uint8_t* out,
+int sw_seg_encode(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
                   int64_t out_cap, uint64_t* state, int64_t max_pages, hipStream_t s) {
   hipError_t e = hipMemsetAsync(state, 0, sizeof(uint64_t) * (size_t)(max_pages + 4), s);
   if (e != hipSuccess) return (int)e;
   SwSegArgs a;
   a.rows = (const SwOutRec*)rows;
-  a.work = (const SwEventRec*)work;
-  a.ok_idx = ok_idx;
-  a.n_ok = n_ok;
-  a.gen = (const SwEventRec*)gen;
-  a.spans = (const SwStrRef*)spans;
+  a.aux = (const SwSegAux*)aux;
   a.raw = raw;
-  a.raw_bytes = raw ? raw_bytes : 0;
   a.cursor = cursor;
   a.out = out;
   a.out_cap = out_cap;
@@ -705,6 +839,36 @@ int sw_seg_encode(const void* rows, const void* work, const uint32_t* ok_idx, co
   a.max_pages = max_pages;
   const unsigned grid = (unsigned)(max_pages > 0 ? max_pages : 1);
   k_seg_encode<<<grid, SBLK, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
+
+// Encoder aux of a step's rows from its records, for callers outside the engine (the engine's
+// persist kernel writes the same records as it persists): row j < *n_ok <-> work[ok_idx[j]] with
+// spans (null: no strings), row j >= *n_ok <-> gen[j - n_ok]; rows = cursor[0] - cursor[1].
+__global__ void k_seg_aux(const SwEventRec* __restrict__ work, const uint32_t* __restrict__ ok_idx,
+                          const uint32_t* __restrict__ n_ok, const SwEventRec* __restrict__ gen,
+                          const SwStrRef* __restrict__ spans, int64_t raw_bytes, const int64_t* __restrict__ cursor,
+                          SwSegAux* __restrict__ aux) {
+  const int64_t n = cursor[0] - cursor[1];
+  const uint32_t nok = *n_ok;
+  SwStrRef none;
+  none.alt_off = 0; none.meta_off = 0; none.alt_len = 0; none.meta_len = 0; none.k = 0; none.has = 0; none.pad = 0;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    if (j < (int64_t)nok) {
+      const uint32_t i = ok_idx[j];
+      aux[j] = seg_make_aux(work[i], spans ? spans[i] : none, raw_bytes);
+    } else {
+      aux[j] = seg_make_aux(gen[j - nok], none, 0);
+    }
+  }
+}
+
+int sw_seg_aux(const void* work, const uint32_t* ok_idx, const uint32_t* n_ok, const void* gen, const void* spans,
+               int64_t raw_bytes, const int64_t* cursor, void* aux, int64_t max_rows, hipStream_t s) {
+  const int64_t blocks = (max_rows + 255) / 256;
+  k_seg_aux<<<(unsigned)(blocks > 0 ? (blocks < 4096 ? blocks : 4096) : 1), 256, 0, s>>>(
+      (const SwEventRec*)work, ok_idx, n_ok, (const SwEventRec*)gen, (const SwStrRef*)spans, raw_bytes, cursor,
+      (SwSegAux*)aux);
   return (int)hipGetLastError();
 }
 

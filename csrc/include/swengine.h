@@ -58,6 +58,8 @@ typedef struct SwStepParams {
   int64_t batch_seq;
   int64_t presence_missing_ms;  // <= 0: no presence scan this step
   SwOutRec* out;                // outbound rows of this step
+  void* aux;                    // SwSegAux per row of this step (durable-block encoder input; null: none)
+  int64_t raw_bytes;            // bound of the batch's strings (0: rows carry no strings, e.g. world > 1)
 } SwStepParams;
 
 typedef struct SwEngineArgs {

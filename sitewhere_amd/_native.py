@@ -272,12 +272,13 @@ def gpu():
         _proto(lib, "sw_sdma_copy", c_int32, P, P, c_int64, c_int32, ctypes.POINTER(ctypes.c_uint64))
         _proto(lib, "sw_sdma_h2d", c_int32, P, P, c_int64, c_int32, ctypes.POINTER(ctypes.c_uint64))
         _proto(lib, "sw_frame_varint", c_int32, P, c_int64, c_int64, P, ctypes.c_uint32, P, c_int64, P)
-        _proto(lib, "sw_set_step_params", c_int32, P, c_int64, c_int64, c_int64, P, P)
+        _proto(lib, "sw_set_step_params", c_int32, P, c_int64, c_int64, c_int64, P, P, c_int64, P)
         _proto(lib, "sw_graph_capture_process", c_int32, P, P, c_int32, P, ctypes.POINTER(ctypes.c_void_p))
         _proto(lib, "sw_graph_launch", c_int32, P, P)
         _proto(lib, "sw_graph_destroy", c_int32, P)
         _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
-        _proto(lib, "sw_seg_encode", c_int32, P, P, P, P, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
+        _proto(lib, "sw_seg_encode", c_int32, P, P, P, P, P, c_int64, P, c_int64, P)
+        _proto(lib, "sw_seg_aux", c_int32, P, P, P, P, P, c_int64, P, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
         _gpu = lib

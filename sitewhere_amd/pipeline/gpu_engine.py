@@ -361,8 +361,13 @@ class GpuInboundEngine(EngineBase):
         sel = self._out_sel if out_sel is None else out_sel
         self._last_sel = sel
         a.out = _ptr(self.out_dev[sel]) if out_to_device else self.out_host[sel].dev
+        # rows kept on the device may be encoded into a durable block: the persist kernel writes each
+        # row's encoder aux beside it (strings only on a single rank: a record decoded on another rank
+        # has its strings in that rank's batch)
+        aux = _ptr(self._aux_buffer(sel)) if out_to_device else 0
+        raw_bytes = getattr(self, "_raw_bytes", 0) if self.world == 1 else 0
         rc = self.lib.sw_set_step_params(ctypes.c_void_p(a.sp), int(now_ms), a.batch_seq, a.presence_missing_ms,
-                                         ctypes.c_void_p(a.out), self._stream())
+                                         ctypes.c_void_p(a.out), ctypes.c_void_p(aux), int(raw_bytes), self._stream())
         if rc:
             raise RuntimeError(f"sw_set_step_params failed ({rc})")
         return sel
@@ -959,9 +964,19 @@ class GpuInboundEngine(EngineBase):
                               torch.zeros(pages + 4, dtype=torch.int64, device=self.device), pages, cap)
         return s
 
+    SEG_AUX_SIZE = 32             # sizeof(SwSegAux), csrc/include/swseg.h
+
+    def _aux_buffer(self, slot: int) -> torch.Tensor:
+        """Encoder aux rows (SwSegAux) of outbound slot ``slot``, beside ``out_dev[slot]``."""
+        bufs = self.__dict__.setdefault("_aux_dev", {})
+        b = bufs.get(slot)
+        if b is None:
+            b = bufs[slot] = torch.zeros(self.out_cap * self.SEG_AUX_SIZE, dtype=torch.uint8, device=self.device)
+        return b
+
     def encode_block_async(self, slot: int) -> torch.Tensor:
         """Enqueue ``k_seg_encode`` of the step just processed on the current stream: its rows (in
-        ``out_dev[slot]``), its persisted records (``work[ok_idx]`` then the generated ones) and, on a
+        ``out_dev[slot]``), their encoder aux (written beside them by the persist kernel) and, on a
         single rank, their strings from the raw batch the step decoded (still in HBM).  Returns the
         device view (block bytes, encoder errors, first store sequence) the host reads once the step
         is done.  Multi-rank: records decoded on another rank carry no string refs here (their
@@ -969,12 +984,9 @@ class GpuInboundEngine(EngineBase):
         dev, state, pages, cap = self._seg_buffers(slot)
         a = self.args
         strings = self.world == 1
-        rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(a.work),
-                                    ctypes.c_void_p(a.ok_idx), ctypes.c_void_p(a.n_ok), ctypes.c_void_p(a.gen),
-                                    ctypes.c_void_p(a.spans if strings else 0), ctypes.c_void_p(a.raw if strings else 0),
-                                    getattr(self, "_raw_bytes", 0) if strings else 0,
-                                    ctypes.c_void_p(_ptr(self.t["cursor"])), ctypes.c_void_p(_ptr(dev)), cap,
-                                    ctypes.c_void_p(_ptr(state)), pages, self._stream())
+        rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(_ptr(self._aux_buffer(slot))),
+                                    ctypes.c_void_p(a.raw if strings else 0), ctypes.c_void_p(_ptr(self.t["cursor"])),
+                                    ctypes.c_void_p(_ptr(dev)), cap, ctypes.c_void_p(_ptr(state)), pages, self._stream())
         if rc:
             raise RuntimeError(f"sw_seg_encode failed ({rc})")
         return state[pages + 1:pages + 4]

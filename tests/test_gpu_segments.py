@@ -17,7 +17,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 
 def _encode_gpu(rows, recs, spans, raw, c0=0, seed=0):
     """Run k_seg_encode on one step's inputs laid out as the engine lays them out: device events in a
-    permuted work array reached through ok_idx, generated rows after them, strings in the raw batch."""
+    permuted work array reached through ok_idx, generated rows after them, strings in the raw batch;
+    the encoder aux rows built from them by ``k_seg_aux`` (the persist kernel's per-row write)."""
     import torch
     from sitewhere_amd._native import gpu
     from sitewhere_amd.models.columnar import EVENT_REC, OUT_REC, STR_REF
@@ -52,10 +53,14 @@ def _encode_gpu(rows, recs, spans, raw, c0=0, seed=0):
     state = torch.zeros(pages + 4, dtype=torch.int64, device=d)
     s = torch.cuda.current_stream(d)
     P = ctypes.c_void_p
-    rc = lib.sw_seg_encode(P(out_rows.data_ptr()), P(work_t.data_ptr()), P(okidx.data_ptr()), P(nok.data_ptr()),
-                           P(gen_t.data_ptr()), P(wsp_t.data_ptr()), P(raw_t.data_ptr()), len(raw),
-                           P(cursor.data_ptr()), P(blk.data_ptr()), bcap, P(state.data_ptr()), pages,
-                           P(s.cuda_stream))
+    # encoder aux rows from the records (what the engine's persist kernel writes beside each row)
+    aux = torch.zeros(max_rows * 32, dtype=torch.uint8, device=d)
+    rc = lib.sw_seg_aux(P(work_t.data_ptr()), P(okidx.data_ptr()), P(nok.data_ptr()), P(gen_t.data_ptr()),
+                        P(wsp_t.data_ptr()), len(raw), P(cursor.data_ptr()), P(aux.data_ptr()), max_rows,
+                        P(s.cuda_stream))
+    assert rc == 0
+    rc = lib.sw_seg_encode(P(out_rows.data_ptr()), P(aux.data_ptr()), P(raw_t.data_ptr()), P(cursor.data_ptr()),
+                           P(blk.data_ptr()), bcap, P(state.data_ptr()), pages, P(s.cuda_stream))
     assert rc == 0
     s.synchronize()
     nb, err, first = (int(x) for x in state[pages + 1:pages + 4].cpu().numpy())
