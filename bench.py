@@ -63,7 +63,11 @@ def parse():
     ap.add_argument("--durable", action=argparse.BooleanOptionalAction, default=True,
                     help="persist every step's events to fdatasync'd segment files (the headline)")
     ap.add_argument("--durable-dir", default=os.environ.get("SW_DURABLE_DIR"),
-                    help="segment directory (default: a fresh directory under the temp dir, removed at exit)")
+                    help="segment directory, or a comma-separated list (one per disk): local rank r writes to "
+                         "dirs[r %% len(dirs)] (default: a fresh directory under the temp dir, removed at exit)")
+    ap.add_argument("--disk-probe-mb", type=int, default=int(os.environ.get("SW_DISK_PROBE_MB", 256)),
+                    help="before timing, every rank writes this much with O_DIRECT + fdatasync to its segment "
+                         "directory at the same time: the node's aggregate disk bandwidth (0 = skip)")
     ap.add_argument("--durable-retention-gb", type=float, default=48.0,
                     help="oldest segment files beyond this are deleted (bounded disk use); 0 = keep all")
     ap.add_argument("--direct-io", action=argparse.BooleanOptionalAction, default=True)
@@ -74,29 +78,70 @@ def parse():
     return ap.parse_args()
 
 
+def durable_dirs(args) -> list[str]:
+    return [d for d in (args.durable_dir or "").split(",") if d]
+
+
 def open_durable(args, rank, dev):
-    """(directory to remove at exit or None, DurableEventStore, boot id) of this rank's segments."""
+    """(directory to remove at exit or None, DurableEventStore, boot id) of this rank's segments.
+    With several ``--durable-dir`` entries (one per disk) local rank r uses entry r mod n."""
     from sitewhere_amd.persistence.segments import DurableEventStore
-    tmpdir = args.durable_dir or tempfile.mkdtemp(prefix=f"sw-bench-durable-r{rank}-")
-    seg_dir = os.path.join(tmpdir, f"rank{rank}") if args.durable_dir else tmpdir
-    if os.path.exists(seg_dir) and args.durable_dir:
+    dirs = durable_dirs(args)
+    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    base = dirs[local_rank % len(dirs)] if dirs else None
+    tmpdir = base or tempfile.mkdtemp(prefix=f"sw-bench-durable-r{rank}-")
+    seg_dir = os.path.join(tmpdir, f"rank{rank}") if base else tmpdir
+    if os.path.exists(seg_dir) and base:
         shutil.rmtree(seg_dir)
     retention = int(args.durable_retention_gb * (1 << 30))
     if retention:
-        # the ranks of a node share its disk: each keeps at most half the free space / local ranks
-        # (a long run then recycles its oldest segments instead of filling the disk)
+        # the ranks sharing a directory share its disk: each keeps at most half its free space / sharers
         local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        sharers = max(1, -(-local // max(1, len(dirs)))) if dirs else local
         probe = os.path.abspath(tmpdir)
         while not os.path.exists(probe):
             probe = os.path.dirname(probe)
         free = shutil.disk_usage(probe).free
-        retention = max(2 << 30, min(retention, free // (2 * local)))
+        retention = max(2 << 30, min(retention, free // (2 * sharers)))
     store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30, retention_bytes=retention,
                               direct=args.direct_io)
     boot = int(time.time() * 1000)
     store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
                                              f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})
-    return (None if args.durable_dir else tmpdir), store, boot
+    return (None if base else tmpdir), store, boot
+
+
+def disk_probe(directory: str, mb: int, direct: bool = True) -> float:
+    """Write ``mb`` MiB in 4 MiB O_DIRECT writes (page-aligned buffer) to a scratch file in
+    ``directory``, fdatasync, remove it; returns GB/s.  Run by every rank at once (between barriers),
+    so the sum over a node's ranks is the node's aggregate bandwidth to its segment directories."""
+    import mmap
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.join(directory, f".disk-probe-{os.getpid()}")
+    chunk = 4 << 20
+    buf = mmap.mmap(-1, chunk)
+    buf.write(os.urandom(4096) * (chunk // 4096))
+    flags = os.O_WRONLY | os.O_CREAT | os.O_TRUNC
+    if direct and hasattr(os, "O_DIRECT"):
+        flags |= os.O_DIRECT
+    try:
+        try:
+            fd = os.open(path, flags, 0o600)
+        except OSError:                      # a file system without O_DIRECT: buffered + fdatasync
+            fd = os.open(path, flags & ~getattr(os, "O_DIRECT", 0), 0o600)
+        t0 = time.perf_counter()
+        for _ in range(max(1, mb // 4)):
+            os.write(fd, buf)
+        os.fdatasync(fd)
+        dt = time.perf_counter() - t0
+        os.close(fd)
+    finally:
+        buf.close()
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+    return (max(1, mb // 4) * chunk) / dt / 1e9
 
 
 class _HostSink:
@@ -395,6 +440,18 @@ def main():
             if dur is not None:
                 dur["sink"].flush()
 
+    probe = None
+    if dur is not None and args.disk_probe_mb > 0:
+        # every rank at once, between barriers: per-rank and node-aggregate O_DIRECT write bandwidth
+        barrier()
+        gbps = disk_probe(dur["store"].dir, args.disk_probe_mb, args.direct_io)
+        agg = gbps
+        if world > 1:
+            tg = torch.tensor([gbps], dtype=torch.float64, device=torch.device("cuda", local) if use_gpu else "cpu")
+            dist.all_reduce(tg, op=dist.ReduceOp.SUM)
+            agg = float(tg.item())
+        probe = {"mb_per_rank": args.disk_probe_mb, "rank0_gbps": round(gbps, 2), "node_gbps": round(agg, 2),
+                 "dirs": max(1, len(durable_dirs(args)))}
     for k in range(args.warmup):
         run(k)
     finish()
@@ -508,6 +565,10 @@ def main():
             # time the pipeline waited for the disk (block buffers all queued, not yet durable):
             # > 0 means this rank's step was storage-bound, e.g. several ranks sharing one disk
             "disk_wait_ms_per_step": round(1000 * (getattr(sk, "disk_wait_s", 0.0) - sk0[3]) / args.steps, 3),
+            # what the disks can take: this rank's and the node's (all ranks at once) O_DIRECT bandwidth,
+            # vs what the step needs (bytes per step x steps per second, whole job)
+            "disk_probe": probe,
+            "needed_gbps_job": round(world * (nbytes / max(1, args.steps)) / (elapsed / args.steps) / 1e9, 2),
         }
     if rank == 0:
         out = {

@@ -16,7 +16,7 @@
 //   R3  one multi-column scan: member indices of all 15 columns, exception indices, heap offsets
 // then thread 0 lays the page out and wave 0 finds the page's offset in the block with a decoupled
 // look-back that reads 64 predecessors per round (ballot for the nearest inclusive prefix).  The
-// write stages two columns at a time in LDS (each thread assembles whole u64 words: coalesced 8-byte
+// write stages two columns at a time in LDS (values ORed into their words, then coalesced 8-byte
 // stores); the string heap is assembled in LDS by each row's owner (8-byte source loads) and written
 // out word by word.  Every word is folded into the page checksum on the way out.  The grid is sized
 // for the largest step; surplus tickets exit.
@@ -43,7 +43,11 @@ struct SwSegArgs {
   int64_t out_cap;
   uint64_t* state;             // [max_pages] look-back words, then ticket, bytes, errors (zeroed per call)
   int64_t max_pages;
+  uint64_t* stamps;            // profiling: [page * 16 + phase] s_memrealtime stamps (null: off)
 };
+
+// phase stamps of a page (profiling builds of the caller only: a null pointer costs a branch)
+#define SEG_STAMP(i) do { if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)page * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 #define LB_AGG (1ull << 62)
 #define LB_INC (2ull << 62)
@@ -265,6 +269,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   if ((int64_t)page >= np) return;
   const int64_t r0 = (int64_t)page * SEG_PAGE_ROWS;
   const int m = (int)(n - r0 < SEG_PAGE_ROWS ? n - r0 : SEG_PAGE_ROWS);
+  SEG_STAMP(0);
   // ---- load 4 consecutive rows per thread: enriched row + encoder aux (both coalesced)
   SRow R[RPT];
 #pragma unroll
@@ -298,6 +303,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     }
   }
 
+  SEG_STAMP(1);
   // ---- R1: first row with an alternate id; decimal exponent per double column
   {
     ull fa_local = ~0ull;
@@ -342,6 +348,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   const int first_alt = L.first_alt;
   const uint32_t a_len0 = first_alt >= 0 ? L.alt_len0 : 0u;
 
+  SEG_STAMP(2);
   // ---- R2: alternate-id prefix / hex test; integer min / max; quantised double min / max
   // slots: [0] min LCP, [1] max last-non-hex+1, [2] min alt len, [3] max alt len,
   //        [4 + 2c] / [5 + 2c] min / max of integer column c (ALTLEN follows from [2] / [3], ALTNUM
@@ -436,6 +443,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     if ((uint32_t)L.res[1] <= pfx && wmn == wmx && wmn >= 1 && wmn <= 16) { mode = SEG_ALT_HEX; width = wmn; }
   }
 
+  SEG_STAMP(3);
   // ---- R3: member / exception / heap scans (+ ALTNUM min / max in hex mode)
   ull altnum[RPT];
 #pragma unroll
@@ -508,6 +516,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     L.hpre[threadIdx.x] = ex[NCNT] + L.wtot[wid][NCNT];
   }
 
+  SEG_STAMP(4);
   // ---- layout (thread 0) + look-back for the page's place in the block
   if (threadIdx.x == 0) {
     SwSegPageHdr& H = L.hdr;
@@ -554,6 +563,9 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     L.page_size = H.bytes;
   }
   __syncthreads();
+  SEG_STAMP(5);
+  // column word staging starts zeroed (the pair writer ORs values in and re-zeroes what it wrote out)
+  for (uint32_t w = threadIdx.x; w < 2u * SEG_PAGE_ROWS; w += SBLK) (&L.u.st.vals[0][0])[w] = 0;
   // ---- the page's offset in the block: decoupled look-back by wave 0, 64 predecessors per round
   if (threadIdx.x < 64) {
     const uint32_t lane = lane64();
@@ -607,10 +619,12 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     }
   }
   __syncthreads();
+  SEG_STAMP(6);
   if (L.page_base == ~0ull) return;
   uint8_t* pg = a.out + L.page_base;
   ull cs = 0;
 
+  SEG_STAMP(7);
   // ---- write the columns, two at a time through LDS.  One instantiation per pair: every column
   // index is a compile-time constant, so the rows' fields are selected statically (in registers)
   auto write_pair = [&](auto PR) {
@@ -625,19 +639,25 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
 #pragma unroll
       for (int k = 0; k < RPT; ++k) {
         if (!smem(c, R[k], (int)mode)) continue;
+        ull v = 0;
         if (!seg_is_double(c)) {
-          L.u.st.vals[g][i] = sval(c, R[k], pfx, altnum[k]) - cd.base;
+          v = sval(c, R[k], pfx, altnum[k]) - cd.base;
         } else {
-          const double v = sdbl(c, R[k]);
+          const double dv = sdbl(c, R[k]);
           int64_t q;
-          if (seg_dec_at(v, cd.exp, &q)) {
-            L.u.st.vals[g][i] = seg_ord(q) - cd.base;
+          if (seg_dec_at(dv, cd.exp, &q)) {
+            v = seg_ord(q) - cd.base;
           } else {
-            L.u.st.vals[g][i] = 0;
             L.u.st.xidx[x] = (uint16_t)i;
-            L.u.st.xraw[x] = sw_f64_bits(v);
+            L.u.st.xraw[x] = sw_f64_bits(dv);
             ++x;
           }
+        }
+        // pack straight into the column's words (LDS 64-bit OR: values of neighbouring rows share words)
+        if (v) {
+          const uint32_t bp = i * (uint32_t)cd.bits, w = bp >> 6, sh = bp & 63u;
+          atomicOr(&L.u.st.vals[g][w], v << sh);
+          if (sh + cd.bits > 64u) atomicOr(&L.u.st.vals[g][w + 1], v >> (64u - sh));
         }
         ++i;
       }
@@ -651,13 +671,8 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
       const uint32_t bits = cd.bits, cnt = cd.count;
       const uint32_t nw = seg_col_words(cnt, (int)bits);
       for (uint32_t w = threadIdx.x; w < nw; w += SBLK) {
-        ull word = 0;
-        const ull bit0 = (ull)w * 64ull;
-        for (uint32_t j = (uint32_t)(bit0 / bits); j < cnt; ++j) {
-          const ull b = (ull)j * bits;
-          if (b >= bit0 + 64) break;
-          word |= b >= bit0 ? (L.u.st.vals[g][j] << (b - bit0)) : (L.u.st.vals[g][j] >> (bit0 - b));
-        }
+        const ull word = L.u.st.vals[g][w];
+        L.u.st.vals[g][w] = 0;             // zero again for the next pair (this thread's words only)
         const uint32_t off = cd.data_off + 8u * w;
         *reinterpret_cast<ull*>(pg + off) = word;
         cs ^= seg_mix_word(word, off >> 3);
@@ -692,6 +707,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   write_pair(std::integral_constant<int, 6>{});
   write_pair(std::integral_constant<int, 7>{});
 
+  SEG_STAMP(8);
   // ---- string heap
   const uint32_t heap_bytes = L.hdr.heap_bytes;
   if (heap_bytes && heap_bytes <= HEAP_LDS) {
@@ -799,6 +815,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     }
   }
 
+  SEG_STAMP(9);
   // ---- page header words (word 1, the checksum, is written last and not summed)
   const ull* hw = reinterpret_cast<const ull*>(&L.hdr);
   for (uint32_t i = threadIdx.x; i < SEG_PAGE_HDR / 8; i += SBLK) {
@@ -817,6 +834,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     for (int w = 0; w < SWAVES; ++w) t ^= L.red[w][0];
     *reinterpret_cast<ull*>(pg + 8) = t;
   }
+  SEG_STAMP(10);
 }
 
 extern "C" {
@@ -824,8 +842,17 @@ extern "C" {
 // Encode this step's rows into `out`.  state = u64[max_pages + 4], zeroed here (a memset node when
 // captured); afterwards state[max_pages + 1] = block bytes (~0 on error), state[max_pages + 2] = errors,
 // state[max_pages + 3] = the store sequence of the block's first row.
+int sw_seg_encode_stamped(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
+                          int64_t out_cap, uint64_t* state, int64_t max_pages, uint64_t* stamps, hipStream_t s);
+
 int sw_seg_encode(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
                   int64_t out_cap, uint64_t* state, int64_t max_pages, hipStream_t s) {
+  return sw_seg_encode_stamped(rows, aux, raw, cursor, out, out_cap, state, max_pages, nullptr, s);
+}
+
+// Same, recording 16 phase stamps per page (s_memrealtime, 100 MHz) into stamps[max_pages * 16].
+int sw_seg_encode_stamped(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
+                          int64_t out_cap, uint64_t* state, int64_t max_pages, uint64_t* stamps, hipStream_t s) {
   hipError_t e = hipMemsetAsync(state, 0, sizeof(uint64_t) * (size_t)(max_pages + 4), s);
   if (e != hipSuccess) return (int)e;
   SwSegArgs a;
@@ -837,6 +864,7 @@ int sw_seg_encode(const void* rows, const void* aux, const uint8_t* raw, const i
   a.out_cap = out_cap;
   a.state = state;
   a.max_pages = max_pages;
+  a.stamps = stamps;
   const unsigned grid = (unsigned)(max_pages > 0 ? max_pages : 1);
   k_seg_encode<<<grid, SBLK, 0, s>>>(a);
   return (int)hipGetLastError();

@@ -34,16 +34,21 @@ def test_bench_single_rank_json():
     dd = d["detail"]["durable"]
     assert d["config"]["durable"] and dd["all_durable"] and dd["rows"] == d["detail"]["persisted"]
     assert dd["bytes_per_event"] > 0 and dd["durable_bytes_per_s"] > 0 and dd["fdatasyncs"] >= 1
+    assert d["detail"]["conservation"]["ok"]
 
 
 @pytest.mark.slow
-def test_bench_two_ranks_torchrun():
+def test_bench_two_ranks_torchrun(tmp_path):
+    """Two ranks on gloo, each with its own segment directory (one per disk: ``--durable-dir a,b``):
+    conservation holds over both ranks and each rank's blocks are in its own directory."""
+    d1, d2 = str(tmp_path / "disk1"), str(tmp_path / "disk2")
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *SMALL],
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *SMALL,
+                        "--durable-dir", f"{d1},{d2}", "--disk-probe-mb", "8"],
                        cwd=REPO, capture_output=True, text=True, timeout=900,
                        env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -56,3 +61,9 @@ def test_bench_two_ranks_torchrun():
     det = d["detail"]
     assert det["backend"] == "gloo" and det["world"] == 2 and len(det["rank_elapsed_s"]) == 2
     assert det["exchange_bytes_per_rank_step"] > 0 and det["shuffle_overflow"] == 0
+    assert det["conservation"]["ok"] and det["conservation"]["checked"] >= 4
+    assert det["durable"]["disk_probe"]["dirs"] == 2 and det["durable"]["disk_probe"]["node_gbps"] > 0
+    # local rank r writes to dirs[r % 2]
+    for d, r in ((d1, 0), (d2, 1)):
+        files = os.listdir(os.path.join(d, f"rank{r}"))
+        assert any(f.endswith(".sweg") for f in files), (d, files)
