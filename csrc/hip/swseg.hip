@@ -95,22 +95,30 @@ __device__ __forceinline__ void load_words8(const uint8_t* raw, uint32_t off, ui
   }
 }
 
-// One <= 64-byte chunk of an alternate id (bytes base .. base + n of it): last non-hex byte (+1,
-// absolute) and the value of the trailing lowercase-hex digits (the last 16 of them).
-__device__ __forceinline__ void hex_scan(const ull (&w)[8], uint32_t n, uint32_t base, uint32_t& last, ull& tail) {
+// 0x80 in every byte of x that is not a lowercase hex digit ('0'-'9', 'a'-'f'): SWAR range tests
+// (bytes with the high bit set are never hex; the adds cannot carry across bytes)
+__device__ __forceinline__ ull nonhex_mask(ull x) {
+  const ull H = 0x8080808080808080ull;
+  const ull y = x & ~H;
+  const ull ge30 = (y + 0x5050505050505050ull) & H, ge3a = (y + 0x4646464646464646ull) & H;
+  const ull ge61 = (y + 0x1f1f1f1f1f1f1f1full) & H, ge67 = (y + 0x1919191919191919ull) & H;
+  const ull hex = ((ge30 & ~ge3a) | (ge61 & ~ge67)) & ~(x & H);
+  return ~hex & H;
+}
+
+// Last non-hex byte (+1, absolute) of an id chunk: bytes base .. base + n (n <= 64) in w.
+__device__ __forceinline__ uint32_t last_nonhex(const ull (&w)[8], uint32_t n, uint32_t base, uint32_t last) {
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    if ((uint32_t)i < n) {
-      const uint32_t c = (uint32_t)(w[i >> 3] >> (8 * (i & 7))) & 0xffu;
-      const bool dig = c - 48u < 10u, af = c - 97u < 6u;
-      if (dig || af) {
-        tail = (tail << 4) | (ull)(dig ? c - 48u : c - 87u);
-      } else {
-        last = base + (uint32_t)i + 1u;
-        tail = 0;
-      }
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t b0 = 8u * (uint32_t)q;
+    if (b0 < n) {
+      ull m = nonhex_mask(w[q]);
+      const uint32_t nv = n - b0;
+      if (nv < 8u) m &= (1ull << (8u * nv)) - 1ull;
+      if (m) last = base + b0 + ((63u - (uint32_t)__builtin_clzll(m)) >> 3) + 1u;
     }
   }
+  return last;
 }
 
 // raw bytes [off, off + n) -> LDS bytes dst[0 .. n) (aligned 8-byte source loads, two in flight)
@@ -136,8 +144,6 @@ struct SRow {
   uint8_t et, level;
   SegRowStr s;
   bool valid;
-  uint32_t lnh;      // alternate id: last non-hex byte + 1
-  ull tail;          // alternate id: value of its trailing hex digits (last 16)
 };
 
 // integer value (order-preserving unsigned) of column c; altnum given by the caller
@@ -218,9 +224,49 @@ __device__ __forceinline__ void lb_store(uint64_t* p, ull v) {
   __hip_atomic_store((ull*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave partial of one reduction slot (lane 0 stores it); block_finish combines the waves.
+// ---- wave reductions / scans on DPP (VALU lane moves, no LDS round trip per step).  Row prefix by
+// row_shr 1, 2, 4, 8, then row_bcast15 (rows 1, 3) and row_bcast31 (rows 2, 3): lane 63 ends up with
+// the whole wave.  Lanes without a source keep `old` (the operation's identity).
+template <int CTRL, int RM = 0xf, int BM = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, BM, false);
+}
+template <int CTRL, int RM = 0xf, int BM = 0xf>
+__device__ __forceinline__ ull dpp64(ull v, ull old) {
+  return ((ull)dpp32<CTRL, RM, BM>((uint32_t)(v >> 32), (uint32_t)(old >> 32)) << 32) |
+         (ull)dpp32<CTRL, RM, BM>((uint32_t)v, (uint32_t)old);
+}
+__device__ __forceinline__ ull readlane63(ull v) {
+  return ((ull)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+         (ull)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+template <bool MX>
+__device__ __forceinline__ ull dpp_minmax(ull v) {
+  const ull id = MX ? 0ull : ~0ull;
+#define SEG_MM(x) { const ull o = (x); v = MX ? (o > v ? o : v) : (o < v ? o : v); }
+  SEG_MM((dpp64<0x111>(v, id)));
+  SEG_MM((dpp64<0x112>(v, id)));
+  SEG_MM((dpp64<0x114>(v, id)));
+  SEG_MM((dpp64<0x118>(v, id)));
+  SEG_MM((dpp64<0x142, 0xa>(v, id)));
+  SEG_MM((dpp64<0x143, 0xc>(v, id)));
+#undef SEG_MM
+  return readlane63(v);
+}
+// inclusive prefix sum over the wave (lane i: lanes 0..i)
+__device__ __forceinline__ uint32_t dpp_scan(uint32_t v) {
+  v += dpp32<0x111>(v, 0u);
+  v += dpp32<0x112>(v, 0u);
+  v += dpp32<0x114>(v, 0u);
+  v += dpp32<0x118>(v, 0u);
+  v += dpp32<0x142, 0xa>(v, 0u);
+  v += dpp32<0x143, 0xc>(v, 0u);
+  return v;
+}
+
+// Wave partial of one reduction slot (wave-uniform, stored once); block_finish combines the waves.
 __device__ __forceinline__ void wave_put(SegLds& L, int slot, ull v, bool mx) {
-  const ull r = mx ? wmax(v) : wmin(v);
+  const ull r = mx ? dpp_minmax<true>(v) : dpp_minmax<false>(v);
   if (lane64() == 0) L.red[threadIdx.x >> 6][slot] = r;
 }
 
@@ -277,8 +323,6 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     const int idx = RPT * (int)threadIdx.x + k;
     SRow& r = R[k];
     r.valid = idx < m;
-    r.lnh = 0;
-    r.tail = 0;
     if (r.valid) {
       const int64_t j = r0 + idx;
       const uint4 q0 = *reinterpret_cast<const uint4*>(&a.rows[j]);
@@ -380,17 +424,13 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
           l = d < l ? d : l;
         }
       }
-      uint32_t last = 0;
-      ull tail = 0;
-      hex_scan(W[k], len < 64u ? len : 64u, 0u, last, tail);
+      uint32_t last = last_nonhex(W[k], len < 64u ? len : 64u, 0u, 0u);
       for (uint32_t base = 64; base < len; base += 64) {      // ids longer than 64 bytes (rare)
         ull w[8];
         const uint32_t n = len - base < 64u ? len - base : 64u;
         load_words8(a.raw, r.s.alt_off + base, n, w);
-        hex_scan(w, n, base, last, tail);
+        last = last_nonhex(w, n, base, last);
       }
-      r.lnh = last;
-      r.tail = tail;
       lcp = (ull)l < lcp ? (ull)l : lcp;
       lnh = (ull)last > lnh ? (ull)last : lnh;
       lmin = (ull)len < lmin ? (ull)len : lmin;
@@ -447,9 +487,23 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   // ---- R3: member / exception / heap scans (+ ALTNUM min / max in hex mode)
   ull altnum[RPT];
 #pragma unroll
-  for (int k = 0; k < RPT; ++k)
-    altnum[k] = (mode == SEG_ALT_HEX && R[k].valid && (R[k].s.flags & SEGF_HAS_ALT))
-                    ? (width >= 16u ? R[k].tail : (R[k].tail & ((1ull << (4u * width)) - 1ull))) : 0ull;
+  for (int k = 0; k < RPT; ++k) {
+    // hex mode: each id's remainder (the last `width` <= 16 bytes) as a number
+    altnum[k] = 0;
+    if (mode == SEG_ALT_HEX && R[k].valid && (R[k].s.flags & SEGF_HAS_ALT)) {
+      ull w[8];
+      load_words8(a.raw, R[k].s.alt_off + pfx, width, w);
+      ull v = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if ((uint32_t)i < width) {
+          const uint32_t c = (uint32_t)((i < 8 ? w[0] : w[1]) >> (8 * (i & 7))) & 0xffu;
+          v = (v << 4) | (ull)(c <= 57u ? c - 48u : c - 87u);
+        }
+      }
+      altnum[k] = v;
+    }
+  }
   {
     const uint32_t lane = lane64(), wid = threadIdx.x >> 6;
     uint32_t hb = 0;
@@ -477,12 +531,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
       } else {
         x = hb;
       }
-      uint32_t inc = x;
-#pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        const uint32_t t = __shfl_up(inc, dd, 64);
-        if (lane >= (uint32_t)dd) inc += t;
-      }
+      const uint32_t inc = dpp_scan(x);
       if (lane == 63) L.wtot[wid][c] = inc;
       ex[c] = inc - x;                 // exclusive within the wave
     }
