@@ -103,8 +103,10 @@ def open_durable(args, rank, dev):
             probe = os.path.dirname(probe)
         free = shutil.disk_usage(probe).free
         retention = max(2 << 30, min(retention, free // (2 * sharers)))
+    # ingest benchmark: the store's background indexer (read-side postings / alternate-id hashes) is
+    # off here; scripts/bench_store_reads.py indexes and queries the blocks a run leaves behind
     store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30, retention_bytes=retention,
-                              direct=args.direct_io)
+                              direct=args.direct_io, index=False)
     boot = int(time.time() * 1000)
     store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
                                              f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})

@@ -438,7 +438,13 @@ void swseg_set_flags(uint8_t* block, int32_t flags) {
 }
 
 // 0 = valid; 1 bad header, 2 bad page table, 3 bad page header, 4 page checksum, 5 short.
-int32_t swseg_verify(const uint8_t* b, int64_t len) {
+int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1);
+
+int32_t swseg_verify(const uint8_t* b, int64_t len) { return swseg_verify_pages(b, len, 0, INT64_MAX); }
+
+// swseg_verify of the header, the page table and pages [p0, p1) only: a query that reads a few pages
+// of a block checks what it read (the other pages' bytes need not be present).
+int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1) {
   if (len < 64) return 5;
   SwSegBlockHdr h;
   memcpy(&h, b, sizeof(h));
@@ -450,7 +456,11 @@ int32_t swseg_verify(const uint8_t* b, int64_t len) {
   const uint32_t* pt = (const uint32_t*)(b + 64);
   if (h.n_pages && pt[0] != start) return 2;
   if (pt[h.n_pages] != h.bytes) return 2;
-  for (uint32_t p = 0; p < h.n_pages; ++p) {
+  for (uint32_t p = 0; p < h.n_pages; ++p)
+    if (pt[p + 1] < pt[p] + SEG_PAGE_HDR || pt[p + 1] > h.bytes || (pt[p] & 7)) return 2;
+  if (p0 < 0) p0 = 0;
+  if (p1 > (int64_t)h.n_pages) p1 = h.n_pages;
+  for (uint32_t p = (uint32_t)p0; (int64_t)p < p1; ++p) {
     const uint32_t o = pt[p], e = pt[p + 1];
     if (e < o + SEG_PAGE_HDR || e > h.bytes || (o & 7)) return 2;
     SwSegPageHdr ph;
@@ -644,6 +654,86 @@ int64_t swseg_page_summary(const uint8_t* b, int64_t* out) {
     o[5] = ph.date_max;
   }
   return h.n_pages;
+}
+
+// ----------------------------------------------------------------------------- block indexes
+// LSD radix sort of (key, value) pairs by key, 16-bit digits; stable (equal keys keep input order).
+static void radix_sort_pairs(std::vector<uint64_t>& k, std::vector<uint32_t>& v, int key_bits) {
+  const size_t n = k.size();
+  std::vector<uint64_t> k2(n);
+  std::vector<uint32_t> v2(n);
+  std::vector<uint32_t> cnt(1u << 16);
+  for (int shift = 0; shift < key_bits; shift += 16) {
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    for (size_t i = 0; i < n; ++i) ++cnt[(k[i] >> shift) & 0xffff];
+    uint32_t sum = 0;
+    for (auto& c : cnt) { const uint32_t t = c; c = sum; sum += t; }
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t d = cnt[(k[i] >> shift) & 0xffff]++;
+      k2[d] = k[i];
+      v2[d] = v[i];
+    }
+    k.swap(k2);
+    v.swap(v2);
+  }
+}
+
+// The store's per-block indexes (persistence/segments.py BlockIndex), from a verified block:
+//   postings, one per row, sorted by (key asc, event date desc, row desc):
+//     post_key = assignment << 3 | event type, post_date = event date - min_date, post_row = row;
+//     *date_wide = 1 when some date is outside [min_date, min_date + 2^32) ms (then post_date is
+//     clamped and the caller must not order by it)
+//   alternate ids, one per row that has one, sorted by hash: alt_hash = sw_hash64 of the full id
+//     (the engine's dedup hash), alt_row = row.
+// Returns the number of alternate ids, -1 on a malformed block.
+int64_t swseg_index_block(const uint8_t* b, int64_t min_date, uint32_t* post_key, uint32_t* post_date,
+                          uint32_t* post_row, uint64_t* alt_hash, uint32_t* alt_row, int32_t* date_wide) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const int64_t n = h.n_rows;
+  std::vector<uint8_t> et(n), fl(n);
+  std::vector<int64_t> date(n);
+  std::vector<int32_t> asg(n);
+  const int64_t cap = swseg_string_bytes(b, 0, h.n_pages) + 64;
+  std::vector<uint8_t> heap(cap);
+  std::vector<int64_t> so(3 * n + 1);
+  if (swseg_decode(b, 0, h.n_pages, et.data(), nullptr, date.data(), asg.data(), nullptr, nullptr, nullptr, nullptr,
+                   fl.data(), heap.data(), cap, so.data()) != n)
+    return -1;
+  // postings: sort key (key << 32 | ~rel_date), rows fed newest first so equal keys keep row desc
+  std::vector<uint64_t> k(n);
+  std::vector<uint32_t> v(n);
+  int32_t wide = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t r = n - 1 - j;
+    int64_t rel = date[r] - min_date;
+    if (rel < 0 || rel > 0xffffffffLL) { wide = 1; rel = rel < 0 ? 0 : 0xffffffffLL; }
+    const uint64_t key = ((uint64_t)(uint32_t)asg[r] << 3) | (uint64_t)(et[r] & 7u);
+    k[j] = (key << 32) | (uint64_t)(0xffffffffu - (uint32_t)rel);
+    v[j] = (uint32_t)r;
+  }
+  radix_sort_pairs(k, v, 64);
+  for (int64_t i = 0; i < n; ++i) {
+    post_key[i] = (uint32_t)(k[i] >> 32);
+    post_date[i] = 0xffffffffu - (uint32_t)k[i];
+    post_row[i] = v[i];
+  }
+  *date_wide = wide;
+  // alternate ids
+  k.clear();
+  v.clear();
+  for (int64_t r = 0; r < n; ++r) {
+    if (!(fl[r] & SEGF_HAS_ALT)) continue;
+    const int64_t a0 = so[3 * r], a1 = so[3 * r + 1];
+    k.push_back(sw_hash64(heap.data() + a0, (uint32_t)(a1 - a0)));
+    v.push_back((uint32_t)r);
+  }
+  radix_sort_pairs(k, v, 64);
+  for (size_t i = 0; i < k.size(); ++i) {
+    alt_hash[i] = k[i];
+    alt_row[i] = v[i];
+  }
+  return (int64_t)k.size();
 }
 
 }  // extern "C"

@@ -26,6 +26,7 @@ import ctypes
 import json
 import os
 import threading
+import time
 import zlib
 from collections import OrderedDict
 
@@ -550,6 +551,69 @@ def boot_id(boot) -> int:
     return int(boot, 16) if isinstance(boot, str) else int(boot or 0)
 
 
+class BlockIndex:
+    """Indexes of one durable block (``swseg_index_block``), kept as memory-mapped ``.npy`` sidecars
+    under ``<store>/index/<file>-<offset>.*``:
+
+    * postings, one per row, sorted by (``pk`` = assignment index << 3 | event type, event date desc,
+      row desc); ``pd`` = date - ``min_date`` (u32; ``wide`` when some date does not fit: such a
+      block is answered by a scan), ``pr`` = row
+    * alternate ids: ``ah`` = 64-bit hash of the full id (the engine's dedup hash, sorted), ``ar`` = row
+
+    24 B per row; a lookup is a binary search per block, so a query over a billion stored events
+    touches a few pages of these files per block instead of decoding the blocks."""
+
+    PARTS = ("pk", "pd", "pr", "ah", "ar")
+    __slots__ = PARTS + ("wide", "min_date")
+
+    def __init__(self, pk, pd, pr, ah, ar, wide: bool, min_date: int):
+        self.pk, self.pd, self.pr, self.ah, self.ar = pk, pd, pr, ah, ar
+        self.wide, self.min_date = bool(wide), int(min_date)
+
+    @property
+    def nbytes(self) -> int:
+        return sum(int(getattr(self, k).nbytes) for k in self.PARTS)
+
+    @classmethod
+    def build(cls, block: np.ndarray, min_date: int) -> "BlockIndex":
+        n = int(header(block)["n_rows"])
+        pk, pd, pr = np.empty(n, np.uint32), np.empty(n, np.uint32), np.empty(n, np.uint32)
+        ah, ar = np.empty(n, np.uint64), np.empty(n, np.uint32)
+        wide = np.zeros(1, np.int32)
+        na = int(native().swseg_index_block(_p(block), int(min_date), _p(pk), _p(pd), _p(pr), _p(ah), _p(ar),
+                                            _p(wide)))
+        if na < 0:
+            raise ValueError("event block index failed")
+        return cls(pk, pd, pr, ah[:na], ar[:na], bool(wide[0]), min_date)
+
+    def save(self, base: str):
+        for k in self.PARTS:
+            tmp = f"{base}.{k}.tmp.npy"
+            np.save(tmp, np.ascontiguousarray(getattr(self, k)))
+            os.replace(tmp, f"{base}.{k}.npy")
+        with open(f"{base}.meta.tmp", "w") as f:             # written last: the index is complete
+            json.dump({"wide": self.wide, "min_date": self.min_date}, f)
+        os.replace(f"{base}.meta.tmp", f"{base}.meta")
+
+    @classmethod
+    def load(cls, base: str) -> "BlockIndex | None":
+        try:
+            with open(f"{base}.meta") as f:
+                m = json.load(f)
+            arrs = [np.load(f"{base}.{k}.npy", mmap_mode="r") for k in cls.PARTS]
+        except (OSError, ValueError):
+            return None
+        return cls(*arrs, m["wide"], m["min_date"])
+
+    @classmethod
+    def remove(cls, base: str):
+        for suffix in [f".{k}.npy" for k in cls.PARTS] + [".meta"]:
+            try:
+                os.remove(base + suffix)
+            except OSError:
+                pass
+
+
 class DurableEventStore(DeviceEventStore):
     """Event store of engine tenants on durable segments (see module docstring).
 
@@ -561,7 +625,7 @@ class DurableEventStore(DeviceEventStore):
     entry."""
 
     def __init__(self, directory: str, rank: int = 0, rotate_bytes: int = 1 << 30, retention_bytes: int = 0,
-                 direct: bool = True, cache_blocks: int = 8):
+                 direct: bool = True, cache_blocks: int = 8, index: bool = True, index_threads: int | None = None):
         self.dir = directory
         os.makedirs(directory, exist_ok=True)
         self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
@@ -586,7 +650,21 @@ class DurableEventStore(DeviceEventStore):
             self._high[key] = max(self._high.get(key, 0), int(e["first_seq"]) + int(e["n_rows"]))
         self._cache: OrderedDict = OrderedDict()       # (file, offset) -> decoded columns
         self.cache_blocks = cache_blocks
+        self._pages: OrderedDict = OrderedDict()       # (file, offset, page) -> decoded page columns
+        self.cache_pages = 256
         self.skipped_rows = 0
+        # per-block indexes (postings by assignment + type, alternate-id hashes), built in the
+        # background as blocks land and kept as memory-mapped sidecar files (see BlockIndex)
+        self._ix: dict[tuple, BlockIndex] = {}
+        self._ix_bad: set = set()
+        self._ix_dir = os.path.join(directory, "index")
+        self._ix_stop = threading.Event()
+        self._ix_thread = None
+        self.index_threads = index_threads or min(8, os.cpu_count() or 1)
+        if index:
+            os.makedirs(self._ix_dir, exist_ok=True)
+            self._ix_thread = threading.Thread(target=self._index_loop, daemon=True, name=f"seg-index-{rank}")
+            self._ix_thread.start()
 
     # ------------------------------------------------------------------ API-added events
     def _load_api_log(self):
@@ -723,6 +801,9 @@ class DurableEventStore(DeviceEventStore):
         return self.seg.flush(timeout_s)
 
     def close(self):
+        self._ix_stop.set()
+        if self._ix_thread is not None:
+            self._ix_thread.join(30)
         self.seg.close()
         for f in (self._dict_f, self._api_f):
             try:
@@ -730,9 +811,125 @@ class DurableEventStore(DeviceEventStore):
             except Exception:  # noqa: BLE001
                 pass
 
+    # ------------------------------------------------------------------ block indexes
+    @staticmethod
+    def _key(ent) -> tuple:
+        return int(ent["file"]), int(ent["offset"])
+
+    def _ix_base(self, key) -> str:
+        return os.path.join(self._ix_dir, f"{key[0]}-{key[1]}")
+
+    def _index_one(self, ent):
+        key = self._key(ent)
+        ix = BlockIndex.load(self._ix_base(key))
+        if ix is None:
+            blk = self.seg.read_block(ent)
+            if verify(blk):
+                return None
+            ix = BlockIndex.build(blk, int(ent["min_date"]))
+            ix.save(self._ix_base(key))
+            ix = BlockIndex.load(self._ix_base(key)) or ix
+        return ix
+
+    def _index_loop(self):
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(self.index_threads, thread_name_prefix="seg-index")
+        try:
+            while not self._ix_stop.is_set():
+                try:
+                    ents = self.seg.index()
+                except Exception:  # noqa: BLE001 -- store closing
+                    break
+                live = {self._key(e) for e in ents}
+                for k in [k for k in self._ix if k not in live]:        # retention removed the block
+                    self._ix.pop(k, None)
+                    BlockIndex.remove(self._ix_base(k))
+                todo = [e for e in ents if self._key(e) not in self._ix and self._key(e) not in self._ix_bad]
+                if not todo:
+                    self._ix_stop.wait(0.05)
+                    continue
+                for e, ix in zip(todo, pool.map(self._safe_index_one, todo)):
+                    if ix is None:
+                        self._ix_bad.add(self._key(e))
+                    else:
+                        self._ix[self._key(e)] = ix
+        finally:
+            pool.shutdown(wait=True)
+
+    def _safe_index_one(self, ent):
+        try:
+            return self._index_one(ent)
+        except (OSError, KeyError, ValueError):
+            return None
+
+    def index_wait(self, timeout_s: float = 60.0) -> bool:
+        """Block until every block on disk is indexed (or could not be); False on timeout."""
+        end = time.time() + timeout_s
+        while time.time() < end:
+            if all(self._key(e) in self._ix or self._key(e) in self._ix_bad for e in self.seg.index()):
+                return True
+            time.sleep(0.01)
+        return False
+
+    def index_stats(self) -> dict:
+        ents = self.seg.index()
+        return {"blocks": len(ents), "indexed": sum(self._key(e) in self._ix for e in ents),
+                "index_bytes": sum(ix.nbytes for ix in list(self._ix.values()))}
+
+    # ------------------------------------------------------------------ page reads
+    def _read_pages(self, ent, p0: int, p1: int) -> np.ndarray:
+        """A block buffer holding only its header, page table and pages [p0, p1) (checked), read
+        with three preads: a point query touches a few KB of a block, not the whole block."""
+        path = self.seg.file_path(int(ent["file"]))
+        if path is None:
+            raise KeyError("segment file deleted by retention")
+        off = int(ent["offset"])
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            head = os.pread(fd, 64, off)
+            h = np.frombuffer(head, HDR)[0]
+            tbl_len = -(-4 * (int(h["n_pages"]) + 1) // 8) * 8
+            tbl = os.pread(fd, tbl_len, off + 64)
+            pt = np.frombuffer(tbl, np.uint32)
+            lo, hi = int(pt[p0]), int(pt[p1])
+            buf = np.empty(int(h["bytes"]), np.uint8)
+            buf[:64] = np.frombuffer(head, np.uint8)
+            buf[64:64 + tbl_len] = np.frombuffer(tbl, np.uint8)
+            buf[lo:hi] = np.frombuffer(os.pread(fd, hi - lo, off + lo), np.uint8)
+        finally:
+            os.close(fd)
+        rc = int(native().swseg_verify_pages(_p(buf), len(buf), int(p0), int(p1)))
+        if rc:
+            raise ValueError(f"corrupt event block (code {rc})")
+        return buf
+
+    def _page_cols(self, ent, page: int) -> dict:
+        """Decoded columns of one page (cached), from the block cache when the block is there."""
+        bkey = self._key(ent)
+        key = bkey + (int(page),)
+        with self._lock:
+            c = self._pages.get(key)
+            if c is not None:
+                self._pages.move_to_end(key)
+                return c
+            blk = self._cache.get(bkey)
+        if blk is not None:
+            return blk
+        c = decode_block(self._read_pages(ent, page, page + 1), pages=(page, page + 1), check=False)
+        with self._lock:
+            self._pages[key] = c
+            while len(self._pages) > self.cache_pages:
+                self._pages.popitem(last=False)
+        return c
+
+    def _row_event(self, ent, row: int):
+        """The event at ``row`` of a block, reading one page."""
+        c = self._page_cols(ent, int(row) // PAGE_ROWS)
+        return c, int(row) - int(c["row0"])
+
     # ------------------------------------------------------------------ reads
     def _decoded(self, ent) -> dict:
-        key = (int(ent["file"]), int(ent["offset"]))
+        key = self._key(ent)
         with self._lock:
             c = self._cache.get(key)
             if c is not None:
@@ -799,12 +996,12 @@ class DurableEventStore(DeviceEventStore):
         return self.rows + self._objects.count()
 
     @staticmethod
-    def _eids(h: dict, idx) -> np.ndarray:
-        return (h["first_seq"] + np.asarray(idx, np.int64)) * h["world"] + h["rank"]
+    def _eids(h, idx) -> np.ndarray:
+        return (int(h["first_seq"]) + np.asarray(idx, np.int64)) * int(h["world"]) + int(h["rank"])
 
     def _alt_hashes(self, ent) -> np.ndarray:
         """64-bit hashes of a block's alternate ids (0 where a row has none), computed from the stored
-        strings once per block and cached with the decoded columns."""
+        strings once per block and cached with the decoded columns (blocks not indexed yet)."""
         c = self._decoded(ent)
         h = c.get("alt_hash")
         if h is None:
@@ -820,22 +1017,39 @@ class DurableEventStore(DeviceEventStore):
             c["alt_hash"] = h
         return h
 
+    def _alt_rows(self, ent, want: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """(hashes, rows) of a block's rows whose alternate-id hash is in ``want`` (sorted unique)."""
+        ix = self._ix.get(self._key(ent))
+        if ix is not None:
+            if not len(ix.ah):
+                return np.zeros(0, np.uint64), np.zeros(0, np.int64)
+            lo = np.searchsorted(ix.ah, want, "left")
+            hi = np.searchsorted(ix.ah, want, "right")
+            sel = np.nonzero(hi > lo)[0]
+            if not len(sel):
+                return np.zeros(0, np.uint64), np.zeros(0, np.int64)
+            idx = np.concatenate([np.arange(lo[i], hi[i]) for i in sel])
+            return np.asarray(ix.ah[idx]), np.asarray(ix.ar[idx], np.int64)
+        ah = self._alt_hashes(ent)
+        rows = np.nonzero(np.isin(ah, want))[0]
+        return ah[rows], rows
+
     def find_alternate_hashes(self, hashes) -> dict:
-        """alt-id hash -> event id string for the hashes present on disk (dedup beyond the engine's
-        window: ``AlternateIdDeduplicator`` asks the event store whether the id was ever seen)."""
+        """alt-id hash -> event id string for the hashes present on disk, the newest event per hash
+        (store-backed dedup beyond the engine's window: ``AlternateIdDeduplicator`` asks the event
+        store whether the id was ever seen)."""
         want = np.unique(np.asarray(list(hashes), np.uint64))
         found = {}
         if not len(want):
             return found
-        for e in self.seg.index()[::-1]:
-            ah = self._alt_hashes(e)
-            m = np.isin(ah, want)
-            if m.any():
-                h = self._decoded(e)["header"]
-                for i in np.nonzero(m)[0]:
-                    found.setdefault(int(ah[i]), f"{h['boot']:x}-{int(self._eids(h, [i])[0])}")
-            if len(found) == len(want):
-                break
+        for e in self.seg.index()[::-1]:                 # newest block first
+            hs, rows = self._alt_rows(e, want)
+            if len(rows):
+                eids = self._eids(e, rows)
+                for hv, eid in sorted(zip(hs.tolist(), eids.tolist()), key=lambda t: -t[1]):
+                    found.setdefault(int(hv), f"{int(e['boot']):x}-{int(eid)}")
+                if len(found) == len(want):
+                    break
         return found
 
     def get_event_by_alternate_id(self, alt: str):
@@ -843,14 +1057,13 @@ class DurableEventStore(DeviceEventStore):
         ev = self._objects.get_event_by_alternate_id(alt)
         if ev is not None:
             return ev
-        h = np.uint64(hash64(alt))
-        for e in self.seg.index()[::-1]:             # newest first: the latest event with the id
-            ah = self._alt_hashes(e)
-            hit = np.nonzero(ah == h)[0]
-            for i in hit[::-1]:
-                c = self._decoded(e)
-                if row_strings(c, int(i))[0] == alt:
-                    return self._materialize(c, int(i))
+        want = np.array([hash64(alt)], np.uint64)
+        for e in self.seg.index()[::-1]:                 # newest first: the latest event with the id
+            _, rows = self._alt_rows(e, want)
+            for r in sorted(rows.tolist(), reverse=True):
+                c, i = self._row_event(e, r)
+                if row_strings(c, i)[0] == alt:
+                    return self._materialize(c, i)
         return None
 
     def get_event_by_id(self, id: str):
@@ -870,13 +1083,64 @@ class DurableEventStore(DeviceEventStore):
                 continue
             row = (eid - r) // w - int(e["first_seq"])
             if 0 <= row < int(e["n_rows"]):
-                return self._materialize(self._decoded(e), int(row))
+                c, i = self._row_event(e, row)
+                return self._materialize(c, i)
         return self._objects.get_event_by_id(id)
 
     def list_command_responses_for_invocation(self, invocation_id, criteria=None):
         return self._objects.list_command_responses_for_invocation(invocation_id, criteria)
 
+    def _block_hits(self, e, et: int, a: np.ndarray, c: DateRangeSearchCriteria, need: int):
+        """(count, dates, rows) of a block's rows of type ``et`` whose assignment index is in ``a``
+        within the date range; ``dates`` / ``rows`` hold at least the ``need`` newest of them (all of
+        them when the block is not indexed)."""
+        ix = self._ix.get(self._key(e))
+        if ix is None or ix.wide:
+            cols = self._decoded(e)
+            m = (cols["etype"] == et) & np.isin(cols["asg"], a)
+            if c.start_date is not None:
+                m &= cols["date"] >= c.start_date
+            if c.end_date is not None:
+                m &= cols["date"] <= c.end_date
+            idx = np.nonzero(m)[0]
+            return len(idx), cols["date"][idx], idx
+        keys = (a.astype(np.uint64) << np.uint64(3)) | np.uint64(et)
+        keys = keys.astype(np.uint32)
+        lo = np.searchsorted(ix.pk, keys, "left")
+        hi = np.searchsorted(ix.pk, keys, "right")
+        sel = np.nonzero(hi > lo)[0]
+        if not len(sel):
+            return 0, np.zeros(0, np.int64), np.zeros(0, np.int64)
+        base = int(ix.min_date)
+        bounded = c.start_date is not None or c.end_date is not None
+        count, dates, rows = 0, [], []
+        for i in sel:
+            l, h = int(lo[i]), int(hi[i])
+            d = np.asarray(ix.pd[l:h], np.int64) + base         # newest first within the key
+            if bounded:
+                # dates descend within a key: the range is one contiguous slice
+                if c.end_date is not None:
+                    l2 = int(np.searchsorted(-d, -c.end_date, "left"))
+                else:
+                    l2 = 0
+                h2 = int(np.searchsorted(-d, -c.start_date, "right")) if c.start_date is not None else len(d)
+                d = d[l2:h2]
+                r = np.asarray(ix.pr[l + l2:l + h2], np.int64)
+            else:
+                r = np.asarray(ix.pr[l:h], np.int64)
+            count += len(d)
+            if need > 0:
+                dates.append(d[:need])
+                rows.append(r[:need])
+        if not rows:
+            return count, np.zeros(0, np.int64), np.zeros(0, np.int64)
+        return count, np.concatenate(dates), np.concatenate(rows)
+
     def list_events(self, event_type, index, entity_ids, criteria: DateRangeSearchCriteria | None = None):
+        """Events of one type for entities of an index, newest first.  Indexed blocks answer from
+        their postings (assignment + type, dates descending): the total is a sum of posting-range
+        lengths and only the requested page's rows are read (one page read each); blocks not
+        indexed yet are decoded and scanned."""
         c = criteria or DateRangeSearchCriteria(page_size=100)
         et = _ETYPE.get(DeviceEventType(event_type))
         objs = self._objects.list_events(event_type, index, entity_ids, DateRangeSearchCriteria(
@@ -886,9 +1150,12 @@ class DurableEventStore(DeviceEventStore):
         pos = _CTX[DeviceEventIndex(index)]
         want = set(entity_ids)
         with self._lock:
-            asg_idx = {b: np.array([i for i, ctx in d.items() if ctx[pos] in want], np.int32)
+            asg_idx = {b: np.array(sorted(i for i, ctx in d.items() if ctx[pos] in want), np.int64)
                        for b, d in self._asg.items()}
-        hits = []
+        paged = c.page_size > 0
+        need = max(1, c.page_number) * c.page_size if paged else -1
+        total = len(objs)
+        parts = []                     # (dates, eids, block entry, rows)
         for e in self.seg.index():
             a = asg_idx.get(int(e["boot"]))
             if a is None or not len(a):
@@ -897,31 +1164,28 @@ class DurableEventStore(DeviceEventStore):
                 continue
             if c.end_date is not None and int(e["min_date"]) > c.end_date:
                 continue
-            cols = self._decoded(e)
-            m = (cols["etype"] == et) & np.isin(cols["asg"], a)
-            if c.start_date is not None:
-                m &= cols["date"] >= c.start_date
-            if c.end_date is not None:
-                m &= cols["date"] <= c.end_date
-            idx = np.nonzero(m)[0]
-            if len(idx):
-                hits.append((cols["date"][idx], self._eids(cols["header"], idx), cols, idx))
-        total = sum(len(x[0]) for x in hits) + len(objs)
-        if not hits:
+            n, d, r = self._block_hits(e, et, a, c, need if paged else 1 << 62)
+            total += n
+            if len(r):
+                parts.append((d, self._eids(e, r), e, r))
+        if not parts:
             return SearchResults(total, c.slice(objs))
-        dates = np.concatenate([x[0] for x in hits])
-        eids = np.concatenate([x[1] for x in hits])
-        which = np.concatenate([np.full(len(x[0]), k, np.int32) for k, x in enumerate(hits)])
-        rows = np.concatenate([x[3] for x in hits])
+        dates = np.concatenate([x[0] for x in parts])
+        eids = np.concatenate([x[1] for x in parts])
+        which = np.concatenate([np.full(len(x[0]), k, np.int32) for k, x in enumerate(parts)])
+        rows = np.concatenate([x[3] for x in parts])
         order = np.lexsort((-eids, -dates))
         if objs:
-            merged = [self._materialize(hits[which[o]][2], int(rows[o])) for o in order] + objs
+            if paged:
+                order = order[:need + len(objs)]
+            merged = [self._materialize(*self._row_event(parts[which[o]][2], int(rows[o]))) for o in order] + objs
             merged.sort(key=lambda ev: -(ev.event_date or 0))
             return SearchResults(total, c.slice(merged))
-        if c.page_size > 0:
+        if paged:
             start = (max(1, c.page_number) - 1) * c.page_size
             order = order[start:start + c.page_size]
-        return SearchResults(total, [self._materialize(hits[which[o]][2], int(rows[o])) for o in order])
+        return SearchResults(total, [self._materialize(*self._row_event(parts[which[o]][2], int(rows[o])))
+                                     for o in order])
 
     def _materialize(self, cols: dict, i: int):
         b = cols["header"]["boot"]
