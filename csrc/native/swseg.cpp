@@ -736,6 +736,48 @@ int64_t swseg_index_block(const uint8_t* b, int64_t min_date, uint32_t* post_key
   return (int64_t)k.size();
 }
 
+// Point lookups over many blocks' indexes in one call (the store's per-query work is then a few
+// binary searches per block in native code, not a Python loop).  For each of the n sorted arrays:
+// [lo, hi) of `key`.  u32 variant (postings): with dates (u32, relative to base[i], descending within
+// a key) the range is restricted to event dates in [d_lo, d_hi].
+void swseg_multi_range_u64(const uint64_t* const* keys, const int64_t* lens, int64_t n, uint64_t key,
+                           int64_t* lo_out, int64_t* hi_out) {
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t* a = keys[i];
+    const uint64_t* l = std::lower_bound(a, a + lens[i], key);
+    const uint64_t* h = std::upper_bound(l, a + lens[i], key);
+    lo_out[i] = l - a;
+    hi_out[i] = h - a;
+  }
+}
+
+void swseg_multi_range_u32(const uint32_t* const* keys, const uint32_t* const* dates, const int64_t* lens,
+                           const int64_t* base, int64_t n, uint32_t key, int64_t d_lo, int64_t d_hi,
+                           int64_t* lo_out, int64_t* hi_out) {
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t* a = keys[i];
+    int64_t lo = std::lower_bound(a, a + lens[i], key) - a;
+    int64_t hi = std::upper_bound(a + lo, a + lens[i], key) - a;
+    if (dates && lo < hi) {
+      const uint32_t* d = dates[i];
+      // dates descend within the key: first entry <= d_hi, first entry < d_lo
+      const int64_t rhi = d_hi - base[i], rlo = d_lo - base[i];
+      if (rhi < 0) { lo = hi; }
+      else if (rhi < 0xffffffffLL) {
+        const uint32_t x = (uint32_t)rhi;
+        lo = std::partition_point(d + lo, d + hi, [x](uint32_t v) { return v > x; }) - d;
+      }
+      if (rlo > 0xffffffffLL) { hi = lo; }
+      else if (rlo > 0) {
+        const uint32_t x = (uint32_t)rlo;
+        hi = std::partition_point(d + lo, d + hi, [x](uint32_t v) { return v >= x; }) - d;
+      }
+    }
+    lo_out[i] = lo;
+    hi_out[i] = hi < lo ? lo : hi;
+  }
+}
+
 }  // extern "C"
 
 // ----------------------------------------------------------------------------- segment store

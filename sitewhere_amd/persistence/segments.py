@@ -657,6 +657,8 @@ class DurableEventStore(DeviceEventStore):
         # background as blocks land and kept as memory-mapped sidecar files (see BlockIndex)
         self._ix: dict[tuple, BlockIndex] = {}
         self._ix_bad: set = set()
+        self._ix_version = 0
+        self._ix_tabs = None                            # (version, per-boot native lookup tables)
         self._ix_dir = os.path.join(directory, "index")
         self._ix_stop = threading.Event()
         self._ix_thread = None
@@ -843,6 +845,7 @@ class DurableEventStore(DeviceEventStore):
                 live = {self._key(e) for e in ents}
                 for k in [k for k in self._ix if k not in live]:        # retention removed the block
                     self._ix.pop(k, None)
+                    self._ix_version += 1
                     BlockIndex.remove(self._ix_base(k))
                 todo = [e for e in ents if self._key(e) not in self._ix and self._key(e) not in self._ix_bad]
                 if not todo:
@@ -853,6 +856,7 @@ class DurableEventStore(DeviceEventStore):
                         self._ix_bad.add(self._key(e))
                     else:
                         self._ix[self._key(e)] = ix
+                        self._ix_version += 1
         finally:
             pool.shutdown(wait=True)
 
@@ -875,6 +879,34 @@ class DurableEventStore(DeviceEventStore):
         ents = self.seg.index()
         return {"blocks": len(ents), "indexed": sum(self._key(e) in self._ix for e in ents),
                 "index_bytes": sum(ix.nbytes for ix in list(self._ix.values()))}
+
+    def _tables(self) -> dict:
+        """Per boot: the indexed blocks (index order) and their arrays' addresses for the native
+        multi-block searches; rebuilt when the set of indexed blocks changes."""
+        tabs = self._ix_tabs
+        ver = self._ix_version
+        if tabs is not None and tabs[0] == ver:
+            return tabs[1]
+        by_boot: dict[int, list] = {}
+        for e in self.seg.index():
+            ix = self._ix.get(self._key(e))
+            if ix is not None:
+                by_boot.setdefault(int(e["boot"]), []).append((e, ix))
+        out = {}
+        P = ctypes.c_void_p
+        for b, lst in by_boot.items():
+            n = len(lst)
+            addr = lambda a: a.ctypes.data if len(a) else 0  # noqa: E731
+            out[b] = {"ents": [e for e, _ in lst], "ixs": [ix for _, ix in lst], "n": n,
+                      "pk": (P * n)(*[addr(ix.pk) for _, ix in lst]), "pd": (P * n)(*[addr(ix.pd) for _, ix in lst]),
+                      "ah": (P * n)(*[addr(ix.ah) for _, ix in lst]),
+                      "npk": np.array([len(ix.pk) for _, ix in lst], np.int64),
+                      "nah": np.array([len(ix.ah) for _, ix in lst], np.int64),
+                      "base": np.array([ix.min_date for _, ix in lst], np.int64),
+                      "wide": np.array([ix.wide for _, ix in lst], bool),
+                      "keys": {self._key(e) for e, _ in lst}}
+        self._ix_tabs = (ver, out)
+        return out
 
     # ------------------------------------------------------------------ page reads
     def _read_pages(self, ent, p0: int, p1: int) -> np.ndarray:
@@ -1057,9 +1089,26 @@ class DurableEventStore(DeviceEventStore):
         ev = self._objects.get_event_by_alternate_id(alt)
         if ev is not None:
             return ev
-        want = np.array([hash64(alt)], np.uint64)
-        for e in self.seg.index()[::-1]:                 # newest first: the latest event with the id
-            _, rows = self._alt_rows(e, want)
+        h = hash64(alt)
+        want = np.array([h], np.uint64)
+        hits = {}                                      # indexed block -> rows with the hash
+        indexed = set()
+        lib = native()
+        for tab in self._tables().values():
+            lo, hi = np.zeros(tab["n"], np.int64), np.zeros(tab["n"], np.int64)
+            lib.swseg_multi_range_u64(tab["ah"], _p(tab["nah"]), tab["n"], int(h), _p(lo), _p(hi))
+            for i in np.nonzero(hi > lo)[0]:
+                ix = tab["ixs"][i]
+                hits[self._key(tab["ents"][i])] = np.asarray(ix.ar[int(lo[i]):int(hi[i])], np.int64)
+            indexed |= tab["keys"]
+        for e in self.seg.index()[::-1]:               # newest first: the latest event with the id
+            k = self._key(e)
+            if k in indexed:
+                rows = hits.get(k)
+                if rows is None:
+                    continue
+            else:
+                _, rows = self._alt_rows(e, want)
             for r in sorted(rows.tolist(), reverse=True):
                 c, i = self._row_event(e, r)
                 if row_strings(c, i)[0] == alt:
@@ -1153,10 +1202,34 @@ class DurableEventStore(DeviceEventStore):
             asg_idx = {b: np.array(sorted(i for i, ctx in d.items() if ctx[pos] in want), np.int64)
                        for b, d in self._asg.items()}
         paged = c.page_size > 0
-        need = max(1, c.page_number) * c.page_size if paged else -1
+        need = max(1, c.page_number) * c.page_size if paged else 1 << 62
         total = len(objs)
         parts = []                     # (dates, eids, block entry, rows)
-        for e in self.seg.index():
+        tabs = self._tables()
+        lib = native()
+        d_lo = c.start_date if c.start_date is not None else -(1 << 62)
+        d_hi = c.end_date if c.end_date is not None else (1 << 62)
+        done = set()
+        for b, a in asg_idx.items():
+            tab = tabs.get(b)
+            if tab is None or not len(a):
+                continue
+            lo, hi = np.zeros(tab["n"], np.int64), np.zeros(tab["n"], np.int64)
+            for key in ((a.astype(np.uint64) << np.uint64(3)) | np.uint64(et)).astype(np.uint32).tolist():
+                lib.swseg_multi_range_u32(tab["pk"], tab["pd"], _p(tab["npk"]), _p(tab["base"]), tab["n"], key,
+                                          int(d_lo), int(d_hi), _p(lo), _p(hi))
+                cnt = hi - lo
+                cnt[tab["wide"]] = 0                       # wide blocks: scanned below
+                total += int(cnt.sum())
+                for i in np.nonzero(cnt > 0)[0]:
+                    e, ix = tab["ents"][i], tab["ixs"][i]
+                    l, h = int(lo[i]), int(min(hi[i], lo[i] + need))
+                    r = np.asarray(ix.pr[l:h], np.int64)
+                    parts.append((np.asarray(ix.pd[l:h], np.int64) + ix.min_date, self._eids(e, r), e, r))
+            done |= {self._key(e) for e, w in zip(tab["ents"], tab["wide"]) if not w}
+        for e in self.seg.index():                     # blocks not indexed (yet): decode and scan
+            if self._key(e) in done:
+                continue
             a = asg_idx.get(int(e["boot"]))
             if a is None or not len(a):
                 continue
@@ -1164,7 +1237,7 @@ class DurableEventStore(DeviceEventStore):
                 continue
             if c.end_date is not None and int(e["min_date"]) > c.end_date:
                 continue
-            n, d, r = self._block_hits(e, et, a, c, need if paged else 1 << 62)
+            n, d, r = self._block_hits(e, et, a, c, need)
             total += n
             if len(r):
                 parts.append((d, self._eids(e, r), e, r))
