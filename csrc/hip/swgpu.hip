@@ -707,9 +707,33 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
   }
 }
 
+// The id's filter block holds all its bits: it may have been persisted before (beyond the window).
+__device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h) {
+  uint64_t m[8];
+  sw_bloom_bits(h, m);
+  const ulonglong2* b = reinterpret_cast<const ulonglong2*>(bloom + 8 * sw_bloom_block(h, bmask));
+  bool all = true;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const ulonglong2 v = b[w];
+    all &= (v.x & m[2 * w]) == m[2 * w] && (v.y & m[2 * w + 1]) == m[2 * w + 1];
+  }
+  return all;
+}
+
+__device__ __forceinline__ void bloom_add(ull* __restrict__ bloom, int64_t bmask, ull h) {
+  uint64_t m[8];
+  sw_bloom_bits(h, m);
+  ull* b = bloom + 8 * sw_bloom_block(h, bmask);
+#pragma unroll
+  for (int w = 0; w < 8; ++w)
+    if (m[w] && (b[w] & m[w]) != m[w]) atomicOr(&b[w], (ull)m[w]);
+}
+
 __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                               uint8_t* __restrict__ status, const ull* __restrict__ key, const ull* __restrict__ seq,
-                              int64_t mask, const int64_t* __restrict__ seq_base, const int64_t* __restrict__ meta) {
+                              int64_t mask, const int64_t* __restrict__ seq_base, const int64_t* __restrict__ meta,
+                              const ull* __restrict__ bloom, int64_t bmask) {
   const uint32_t n = *n_ptr;
   const ull sb = (ull)*seq_base;
   const int64_t slots = mask + 1;
@@ -722,7 +746,11 @@ __global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_
     int64_t slot = (int64_t)(h & (ull)mask);
     for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
       const ull k = ck[slot];
-      if (k == h) { if (cq[slot] != sb + (ull)i) status[i] = SW_ST_DUPLICATE; break; }
+      if (k == h) {
+        if (cq[slot] != sb + (ull)i) status[i] = SW_ST_DUPLICATE;
+        else if (bloom && bloom_has(bloom, bmask, h)) status[i] = SW_ST_RECHECK;   // first sight in the window
+        break;
+      }
       if (k == 0) break;
       slot = (slot + 1) & mask;
     }
@@ -758,7 +786,8 @@ __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* 
                    : threadIdx.x == SW_ST_UNASSIGNED ? SW_STAT_UNASSIGNED
                    : threadIdx.x == SW_ST_DUPLICATE ? SW_STAT_DUPLICATE
                    : threadIdx.x == SW_ST_DECODE_ERROR ? SW_STAT_DECODE_ERROR
-                   : threadIdx.x == SW_ST_CONTROL ? SW_STAT_CONTROL : -1;
+                   : threadIdx.x == SW_ST_CONTROL ? SW_STAT_CONTROL
+                   : threadIdx.x == SW_ST_RECHECK ? SW_STAT_DEDUP_RECHECKS : -1;
     if (slot >= 0) atomicAdd(&stats[slot], (ull)rs[threadIdx.x]);
   }
 }
@@ -878,6 +907,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     o.etype = r.etype;
     o.level = r.level;
     a.sp->out[seq - c0] = o;
+    if (a.dd_bloom && r.alt_hash) bloom_add((ull*)a.dd_bloom, a.dd_bloom_mask, r.alt_hash);
     if (aux) {                   // the durable-block encoder's input, beside the row (coalesced)
       SwStrRef sr;
       if (spans) {
@@ -1425,7 +1455,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base,
                                    a.dd_meta, (ull*)a.stats);
   k_dedup_check<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (const ull*)a.dd_key, (const ull*)a.dd_seq, a.dd_mask,
-                                  a.seq_base, a.dd_meta);
+                                  a.seq_base, a.dd_meta, (const ull*)a.dd_bloom, a.dd_bloom_mask);
   // stable split ok / rejected
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats);
   uint32_t* cmp_off = a.cmp_tmp + 2 * ntiles;
@@ -1468,6 +1498,19 @@ __global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batc
     sp->now_ms = now_ms; sp->batch_seq = batch_seq; sp->presence_missing_ms = presence_ms; sp->out = out;
     sp->aux = aux; sp->raw_bytes = raw_bytes;
   }
+}
+
+// Add ids to the store-backed dedup filter (warm start from the event store's alternate-id index).
+__global__ void k_bloom_add(ull* bloom, int64_t bmask, const ull* __restrict__ h, int64_t n) {
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK)
+    if (h[i]) bloom_add(bloom, bmask, h[i]);
+}
+
+int sw_bloom_add(void* bloom, int64_t bmask, const void* hashes, int64_t n, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int64_t g = (n + BLK - 1) / BLK;
+  k_bloom_add<<<(unsigned)(g < 4096 ? g : 4096), BLK, 0, s>>>((ull*)bloom, bmask, (const ull*)hashes, n);
+  return (int)hipGetLastError();
 }
 
 // Stream-ordered write of this step's params (before the decode / process phases of the step).

@@ -169,7 +169,7 @@ typedef struct SwEngineArgs {
   int64_t presence_missing_ms; // <= 0 disables the scan this step
   uint64_t presence_name_hash; // hash of "presence"
   // ---------------------------------------------------------------- stats
-  uint64_t* stats;             // [16] cumulative counters (see SW_STAT_*)
+  uint64_t* stats;             // [SW_N_STATS] cumulative counters (see SW_STAT_*)
   // ---------------------------------------------------------------- per-step params (device)
   SwStepParams* sp;
   // ---------------------------------------------------------------- shuffle spill (world > 1)
@@ -190,7 +190,12 @@ typedef struct SwEngineArgs {
                                // hold two tables of dd_mask + 1 slots (current = dd_meta[0])
   // ---------------------------------------------------------------- string refs
   SwStrRef* spans;             // [rec_cap] per decoded record (decode writes, the block encoder reads)
+  // ---------------------------------------------------------------- store-backed dedup filter
+  uint64_t* dd_bloom;          // [8 * (dd_bloom_mask + 1)] blocked Bloom filter (null: off)
+  int64_t dd_bloom_mask;       // 512-bit blocks - 1
 } SwEngineArgs;
+
+#define SW_N_STATS 24
 
 enum {
   SW_STAT_MSGS = 0,
@@ -209,5 +214,6 @@ enum {
   SW_STAT_SHUFFLE_DEFERRED = 13,   // records spilled to the next step's exchange
   SW_STAT_DEDUP_OVERFLOW = 14,     // alternate ids the window could not place (probe bound hit)
   SW_STAT_DEDUP_ROTATIONS = 15,    // dedup generations retired
+  SW_STAT_DEDUP_RECHECKS = 16,     // ids handed to the host: new to the window, maybe in the store
   SW_STAT_N = 16,
 };

@@ -53,6 +53,8 @@ enum SwStatus : uint8_t {
   SW_ST_DUPLICATE = 3,      // alternate id seen before (AlternateIdDeduplicator)
   SW_ST_DECODE_ERROR = 4,   // failed-decode topic
   SW_ST_CONTROL = 5,        // registration / ack / stream: host path
+  SW_ST_RECHECK = 6,        // alternate id new to the dedup window but maybe stored before (the
+                            // store-backed filter holds it): host path, checked against the store
 };
 
 // record flags
@@ -190,6 +192,20 @@ SW_HD uint64_t sw_mix64(uint64_t x) {
   x *= 0x94d049bb133111ebULL;
   x ^= x >> 31;
   return x;
+}
+
+// Store-backed alternate-id filter: a blocked Bloom filter (512-bit blocks, 7 bits per id) of every
+// id the engine persisted.  An id new to the dedup window that the filter may hold is handed to the
+// host (SW_ST_RECHECK), which checks it against the event store -- dedup beyond the window without a
+// per-event store lookup on the hot path.  Same functions in every engine (bit-exact).
+SW_HD uint64_t sw_bloom_block(uint64_t h, int64_t mask) { return sw_mix64(h ^ 0x5bd1e9955bd1e995ULL) & (uint64_t)mask; }
+SW_HD void sw_bloom_bits(uint64_t h, uint64_t m[8]) {
+  const uint64_t g = sw_mix64(h + 0x9E3779B97F4A7C15ULL);
+  for (int w = 0; w < 8; ++w) m[w] = 0;
+  for (int j = 0; j < 7; ++j) {
+    const uint32_t b = (uint32_t)(g >> (9 * j)) & 511u;
+    m[b >> 6] |= 1ull << (b & 63);
+  }
 }
 
 // 128-bit fingerprint of a byte string: FNV-1a-64 and an independent odd-multiplier

@@ -258,7 +258,7 @@ typedef struct SwCeTables {
   int64_t gen_cap;
   uint64_t presence_hash;
   int64_t presence_missing_ms;
-  uint64_t* stats;  // [16], SW_STAT_* slots
+  uint64_t* stats;  // [SW_N_STATS], SW_STAT_* slots
 } SwCeTables;
 
 typedef struct SwCeStep {
@@ -277,6 +277,8 @@ struct SwCpuEngine {
   std::vector<U64Map<int64_t>> dedup;       // current generation of the alternate-id window, by hash % T
   std::vector<U64Map<int64_t>> dedup_prev;  // previous generation (see the rotation in swce_process)
   int64_t dd_slots = 0, dd_batch = 0;       // window slots and the largest batch (rotation rule)
+  std::vector<uint64_t> bloom;              // store-backed dedup filter (sw_bloom_*), empty: off
+  int64_t bloom_mask = 0;
   U64Map<int32_t> intern;
   int32_t n_intern = 0;
   std::vector<U64Map<MsVal>> ms;       // sharded by assignment % T
@@ -298,6 +300,23 @@ static inline int32_t nid_of(const SwCpuEngine* e, uint64_t h) {
   if (!h) return -1;
   const int32_t* v = e->intern.find(h);
   return v ? *v : -1;
+}
+
+static inline bool bloom_has(const SwCpuEngine* e, uint64_t h) {
+  uint64_t m[8];
+  sw_bloom_bits(h, m);
+  const uint64_t* b = e->bloom.data() + 8 * sw_bloom_block(h, e->bloom_mask);
+  for (int w = 0; w < 8; ++w)
+    if ((b[w] & m[w]) != m[w]) return false;
+  return true;
+}
+
+static inline void bloom_add(SwCpuEngine* e, uint64_t h) {
+  uint64_t m[8];
+  sw_bloom_bits(h, m);
+  uint64_t* b = e->bloom.data() + 8 * sw_bloom_block(h, e->bloom_mask);
+  for (int w = 0; w < 8; ++w)
+    if (m[w]) __atomic_fetch_or(&b[w], m[w], __ATOMIC_RELAXED);
 }
 
 static inline bool pip(const double* v, int32_t n, double x, double y) {
@@ -539,8 +558,13 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
             continue;
           }
           auto ins = m.insert(work[i].alt_hash);
-          if (ins.second) *ins.first = seq_base + i;
-          else status[i] = SW_ST_DUPLICATE;
+          if (ins.second) {
+            *ins.first = seq_base + i;
+            // first sight in the window: the store may still hold it (filter from earlier steps)
+            if (!e->bloom.empty() && bloom_has(e, work[i].alt_hash)) status[i] = SW_ST_RECHECK;
+          } else {
+            status[i] = SW_ST_DUPLICATE;
+          }
         }
     });
   }
@@ -583,6 +607,9 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
     chunk_of(n_ok, w, T, &b, &end);
     persist_range(e, t, work, ok_idx, dev, [&](int64_t j) { return asg[ok_idx[j]]; }, cursor0, now_ms, out, b, end,
                   spans, prec, pspans);
+    if (!e->bloom.empty())                    // persisted ids join the store-backed filter
+      for (int64_t j = b; j < end; ++j)
+        if (work[ok_idx[j]].alt_hash) bloom_add(e, work[ok_idx[j]].alt_hash);
     if (T > 1) {
       for (int sh = 0; sh < T; ++sh) e->lists[(size_t)w * T + sh].clear();
       for (int64_t j = b; j < end; ++j) e->lists[(size_t)w * T + (uint32_t)out[j].assignment % (uint32_t)T].push_back((int32_t)j);
@@ -713,6 +740,7 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   S[5] += c[SW_ST_DUPLICATE];
   S[6] += c[SW_ST_DECODE_ERROR];
   S[7] += c[SW_ST_CONTROL];
+  S[SW_STAT_DEDUP_RECHECKS] += c[SW_ST_RECHECK];
   S[8] += (uint64_t)n_rule;
   S[9] += (uint64_t)(n_gen - n_rule);
   st->cursor = cursor;
@@ -722,6 +750,34 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   st->n_rule = n_rule;
   st->n_rej = n - n_ok;
   return 0;
+}
+
+// Store-backed dedup filter: `bits` (a multiple of 512, 0 = off); cleared.
+void swce_bloom_init(void* p, int64_t bits) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  const int64_t blocks = bits / 512;
+  e->bloom.assign(blocks > 0 ? (size_t)blocks * 8 : 0, 0ull);
+  e->bloom_mask = blocks > 0 ? blocks - 1 : 0;
+}
+
+void swce_bloom_add(void* p, const uint64_t* h, int64_t n) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  if (e->bloom.empty()) return;
+  for (int64_t i = 0; i < n; ++i)
+    if (h[i]) bloom_add(e, h[i]);
+}
+
+// The filter's words (checkpoints).
+int64_t swce_bloom_words(void* p, uint64_t* out, int64_t cap) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  const int64_t n = (int64_t)e->bloom.size();
+  if (out && cap >= n) memcpy(out, e->bloom.data(), (size_t)n * 8);
+  return n;
+}
+
+void swce_bloom_load(void* p, const uint64_t* w, int64_t n) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  if ((int64_t)e->bloom.size() == n) memcpy(e->bloom.data(), w, (size_t)n * 8);
 }
 
 // Window sizing of the generational dedup (slots per generation, largest batch in records).

@@ -301,7 +301,7 @@ static inline uint64_t order_of(int kind, int32_t part, uint64_t rank, uint64_t 
 // Route the rejected messages of one raw batch.
 //   raw/offs/n_msgs : the batch (payload bytes, n_msgs + 1 offsets)
 //   rej_off/rej_st  : n_rej reject records: any byte offset inside their payload + engine status
-//                     (1 unregistered, 2 unassigned, 3 duplicate, 4 decode error, 5 control)
+//                     (1 unregistered, 2 unassigned, 3 duplicate, 4 decode error, 5 control, 6 recheck)
 //   parts           : partitions of the unregistered, registration, decoded and failed-decode topics
 // Output: records grouped by (kind, partition) -- stable, so per-key order is the batch order --
 // with rec[i] = (kind, partition, key length, value length) and the keys / values concatenated in
@@ -340,10 +340,13 @@ static void route_one(Worker& wk, uint32_t wid, const uint8_t* raw, uint32_t s, 
     return;
   }
   const size_t v0 = wk.arena.size();
-  if (st == SW_ST_CONTROL && (p.cmd == SW_CMD_SEND_DEVICE_MEASUREMENTS || p.cmd == SW_CMD_SEND_DEVICE_LOCATION ||
-                              p.cmd == SW_CMD_SEND_DEVICE_ALERT)) {
-    // an event the engine handed back (SW_EV_OVERSIZE: strings past its 16-bit lengths): the whole
-    // payload goes to the host, which decodes it onto the per-event path (stored whole there)
+  if ((st == SW_ST_CONTROL || st == SW_ST_RECHECK) &&
+      (p.cmd == SW_CMD_SEND_DEVICE_MEASUREMENTS || p.cmd == SW_CMD_SEND_DEVICE_LOCATION ||
+       p.cmd == SW_CMD_SEND_DEVICE_ALERT)) {
+    // an event the engine handed back -- SW_EV_OVERSIZE (strings past its 16-bit lengths) or an
+    // alternate id the store-backed filter may hold (SW_ST_RECHECK): the whole payload goes to the
+    // host, which decodes it onto the per-event path (stored whole there, deduplicated against the
+    // event store by alternate id)
     emit(RK_CONTROL, p.token, raw + s, e - s, 0, false);
     return;
   }

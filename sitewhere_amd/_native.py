@@ -162,6 +162,10 @@ def native():
             _proto(lib, f"swce_{kind}_size", c_int64, P)
         _proto(lib, "swce_dedup_export", c_int64, P, P, P)
         _proto(lib, "swce_dedup_window", None, P, c_int64, c_int64)
+        _proto(lib, "swce_bloom_init", None, P, c_int64)
+        _proto(lib, "swce_bloom_add", None, P, P, c_int64)
+        _proto(lib, "swce_bloom_words", c_int64, P, P, c_int64)
+        _proto(lib, "swce_bloom_load", None, P, P, c_int64)
         _proto(lib, "swce_dedup_prev_size", c_int64, P)
         _proto(lib, "swce_dedup_prev_export", c_int64, P, P, P)
         _proto(lib, "swce_dedup_prev_import", None, P, P, P, c_int64)
@@ -284,6 +288,7 @@ def gpu():
         _proto(lib, "sw_seg_encode", c_int32, P, P, P, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_seg_encode_stamped", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P)
         _proto(lib, "sw_seg_aux", c_int32, P, P, P, P, P, c_int64, P, P, c_int64, P)
+        _proto(lib, "sw_bloom_add", c_int32, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
         _gpu = lib

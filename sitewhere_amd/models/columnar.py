@@ -29,6 +29,7 @@ ST_UNASSIGNED = 2
 ST_DUPLICATE = 3
 ST_DECODE_ERROR = 4
 ST_CONTROL = 5
+ST_RECHECK = 6          # id new to the dedup window, maybe stored before: host checks the store
 
 F_HAS_UPDATE_STATE = 0x1
 F_UPDATE_STATE = 0x2
@@ -112,10 +113,11 @@ MS_SLOT = np.dtype([("key", "<u8"), ("date", "<u8"), ("eid1", "<u8"), ("pad", "<
 ZONE_TEST = np.dtype([("zone", "<i4"), ("condition", "<i4"), ("alert_name_id", "<i4"), ("level", "<i4")])
 
 # Stats slots (SW_STAT_* in swengine.h).
+N_STATS = 24            # SW_N_STATS (csrc/include/swengine.h): slots of the stats arrays
 STAT_NAMES = [
     "messages", "events", "persisted", "unregistered", "unassigned", "duplicates", "decode_errors",
     "control", "rule_alerts", "presence_events", "shuffle_overflow", "new_names", "state_overflow",
-    "shuffle_deferred", "dedup_overflow", "dedup_rotations",
+    "shuffle_deferred", "dedup_overflow", "dedup_rotations", "dedup_rechecks",
 ]
 
 # Alert levels (GAlertLevel) and sources.

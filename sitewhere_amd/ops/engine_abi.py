@@ -59,6 +59,9 @@ FIELDS = [
     ("dd_meta", P),
     # string refs of the decoded records (SwStrRef, read by the durable-block encoder)
     ("spans", P),
+    # store-backed dedup filter (blocked Bloom filter, null = off)
+    ("dd_bloom", P),
+    ("dd_bloom_mask", I),
 ]
 
 

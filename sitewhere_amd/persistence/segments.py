@@ -875,6 +875,22 @@ class DurableEventStore(DeviceEventStore):
             time.sleep(0.01)
         return False
 
+    def alternate_hash_chunks(self, max_ids: int = 1 << 26, wait_s: float = 30.0):
+        """The stored alternate-id hashes, newest blocks first, in chunks (numpy u64), at most
+        ``max_ids``: what a restarted engine seeds its store-backed dedup filter with.  Waits up to
+        ``wait_s`` for the background indexer; blocks still unindexed then are read and hashed."""
+        self.index_wait(wait_s)
+        left = int(max_ids)
+        for e in self.seg.index()[::-1]:
+            if left <= 0:
+                break
+            ix = self._ix.get(self._key(e))
+            h = np.asarray(ix.ah) if ix is not None else self._alt_hashes(e)
+            h = h[h != 0]
+            if len(h):
+                yield h[:left]
+                left -= len(h)
+
     def index_stats(self) -> dict:
         ents = self.seg.index()
         return {"blocks": len(ents), "indexed": sum(self._key(e) in self._ix for e in ents),

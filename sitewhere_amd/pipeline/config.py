@@ -21,6 +21,9 @@ class EngineConfig:
     max_assignments: int = 1 << 20
     store_cap: int = 1 << 27         # HBM event-store ring capacity (events)
     dedup_slots: int = 1 << 22       # alternate-id window (slots; window = slots / 2)
+    # store-backed dedup beyond the window: a blocked Bloom filter of every persisted alternate id
+    # (bits; a multiple of 512; 0 = off).  ~32 bits per id kept -> ~1e-4 of new ids rechecked on the host
+    dedup_bloom_bits: int = 0
     name_slots: int = 1 << 16        # distinct measurement names / alert types
     state_slots: int = 0             # (assignment, name) state map slots (0 = 16 * max_assignments)
     names_cap: int = 4096            # new-name reports per step
@@ -44,6 +47,8 @@ class EngineConfig:
         # would pass that): smaller tables overflow on every step and probe to their limit
         self.dedup_slots = pow2_at_least(max(self.dedup_slots, 2 * self.rec_cap))
         self.name_slots = pow2_at_least(self.name_slots)
+        if self.dedup_bloom_bits > 0:
+            self.dedup_bloom_bits = pow2_at_least(max(512, self.dedup_bloom_bits))
         self.state_slots = pow2_at_least(self.state_slots)
         self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + self.shuffle_pad
         local = self.rec_cap

@@ -12,10 +12,23 @@ import numpy as np
 
 from ..models.columnar import (EVENT_REC, OUT_REC, EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE,
                                EV_DECODE_ERROR, ST_OK, ST_UNREGISTERED, ST_UNASSIGNED, ST_DUPLICATE,
-                               ST_DECODE_ERROR, ST_CONTROL, STAT_NAMES, STR_REF, WIRE_REC, wire_pack, wire_unpack)
+                               ST_DECODE_ERROR, ST_CONTROL, ST_RECHECK, STAT_NAMES, N_STATS, STR_REF, WIRE_REC,
+                               wire_pack, wire_unpack)
 from .config import EngineConfig
 from .engine_base import EngineBase, StepResult
 from .fleet import cpu_decode
+
+_M64 = (1 << 64) - 1
+
+
+def mix64(x: int) -> int:
+    """sw_mix64 (csrc/include/swtypes.h)."""
+    x &= _M64
+    x ^= x >> 30
+    x = (x * 0xbf58476d1ce4e5b9) & _M64
+    x ^= x >> 27
+    x = (x * 0x94d049bb133111eb) & _M64
+    return x ^ (x >> 31)
 
 STORE_COLS = {
     "etype": np.uint8, "level": np.uint8, "date": np.int64, "recv": np.int64, "dev": np.int32, "asg": np.int32,
@@ -51,13 +64,17 @@ class CpuInboundEngine(EngineBase):
         self.seq_base = 0
         self.dedup: dict[int, int] = {}          # current generation of the alternate-id window
         self.dedup_prev: dict[int, int] = {}     # previous generation
+        # store-backed dedup filter (blocked Bloom filter of every persisted alternate id; sw_bloom_*)
+        nb = cfg.dedup_bloom_bits // 512
+        self.bloom = np.zeros(8 * nb, np.uint64) if nb else None
+        self.bloom_mask = nb - 1
         self.intern: dict[int, int] = {}
         self.st_last = np.zeros(cfg.max_assignments, np.uint64)
         self.st_missing = np.zeros(cfg.max_assignments, np.uint64)
         self.st_loc_date = np.zeros(cfg.max_assignments, np.uint64)
         self.st_loc_eid = np.zeros(cfg.max_assignments, np.int64)   # eid + 1, 0 = none
         self.ms: dict[tuple, list] = {}                               # (asg, name_id, kind) -> [date, eid+1]
-        self.stats = np.zeros(16, np.uint64)
+        self.stats = np.zeros(N_STATS, np.uint64)
         self._seen: set[int] = set()
 
     # ------------------------------------------------------------------ stages
@@ -153,6 +170,36 @@ class CpuInboundEngine(EngineBase):
                 status[i] = ST_DUPLICATE
             else:
                 cur[h] = self.seq_base + i
+                if self.bloom is not None and self._bloom_has(h):
+                    status[i] = ST_RECHECK                   # maybe stored before: the host checks
+
+    def reset_dedup(self):
+        """Forget the alternate-id window (both generations); the store-backed filter stays."""
+        self.dedup, self.dedup_prev = {}, {}
+
+    def _bloom_pos(self, h: int):
+        blk = mix64(h ^ 0x5bd1e9955bd1e995) & self.bloom_mask
+        g = mix64((h + 0x9E3779B97F4A7C15) & _M64)
+        m = [0] * 8
+        for j in range(7):
+            b = (g >> (9 * j)) & 511
+            m[b >> 6] |= 1 << (b & 63)
+        return 8 * blk, m
+
+    def _bloom_has(self, h: int) -> bool:
+        base, m = self._bloom_pos(h)
+        return all((int(self.bloom[base + w]) & m[w]) == m[w] for w in range(8))
+
+    def bloom_add(self, hashes):
+        """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
+        if self.bloom is None:
+            return
+        for h in np.asarray(hashes, np.uint64).tolist():
+            if h:
+                base, m = self._bloom_pos(int(h))
+                for w in range(8):
+                    if m[w]:
+                        self.bloom[base + w] |= np.uint64(m[w])
 
     def _intern_id(self, h: int) -> int:
         if h not in self.intern:
@@ -249,6 +296,7 @@ class CpuInboundEngine(EngineBase):
                 self._intern_id(h)
         out_rows: list = []
         self._persist(work[ok], dev[ok], asg[ok], now_ms, out_rows)
+        self.bloom_add(work[ok]["alt_hash"])             # persisted ids join the store-backed filter
         self._state(work[ok], asg[ok], now_ms)
         self.cursor += len(ok)
         # rules on persisted locations
@@ -299,7 +347,7 @@ class CpuInboundEngine(EngineBase):
         st[1] += len(work)
         st[2] += len(out_rows)
         for code, slot in ((ST_UNREGISTERED, 3), (ST_UNASSIGNED, 4), (ST_DUPLICATE, 5), (ST_DECODE_ERROR, 6),
-                           (ST_CONTROL, 7)):
+                           (ST_CONTROL, 7), (ST_RECHECK, 16)):
             st[slot] += int((status == code).sum())
         st[8] += n_rule
         st[9] += len(gen) - n_rule
@@ -324,6 +372,7 @@ class CpuInboundEngine(EngineBase):
             "dedup_key": u64(self.dedup.keys()), "dedup_seq": np.array(list(self.dedup.values()), np.int64),
             "dedup_prev_key": u64(self.dedup_prev.keys()),
             "dedup_prev_seq": np.array(list(self.dedup_prev.values()), np.int64),
+            **({"dd_bloom": self.bloom.copy()} if self.bloom is not None else {}),
             "intern_key": u64(self.intern.keys()), "intern_id": np.array(list(self.intern.values()), np.int64),
             "seen": u64(self._seen),
             "st_last": self.st_last, "st_missing": self.st_missing, "st_loc_date": self.st_loc_date,
@@ -338,7 +387,10 @@ class CpuInboundEngine(EngineBase):
 
     def restore_state(self, a: dict, include_store: bool):
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
-        self.stats[:] = a["stats"]
+        self.stats[:] = 0
+        self.stats[:len(a["stats"])] = a["stats"]
+        if self.bloom is not None and "dd_bloom" in a and len(a["dd_bloom"]) == len(self.bloom):
+            self.bloom[:] = a["dd_bloom"]
         self.dedup = dict(zip((int(x) for x in a["dedup_key"]), (int(x) for x in a["dedup_seq"])))
         self.dedup_prev = dict(zip((int(x) for x in a.get("dedup_prev_key", [])),
                                    (int(x) for x in a.get("dedup_prev_seq", []))))

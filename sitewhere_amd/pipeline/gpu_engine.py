@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .._native import gpu as gpu_lib
-from ..models.columnar import EVENT_REC, OUT_REC, NAME_REF, OUT_REC_SIZE, STR_REF, WIRE_REC
+from ..models.columnar import EVENT_REC, N_STATS, OUT_REC, NAME_REF, OUT_REC_SIZE, STR_REF, WIRE_REC
 from ..ops.engine_abi import SwEngineArgs
 from .config import EngineConfig
 from .bus_io import host_view
@@ -164,6 +164,9 @@ class GpuInboundEngine(EngineBase):
         t["asg_active"] = z(c.max_assignments, u8)
         # dedup window
         t["dd_key"] = z(2 * c.dedup_slots, i64)            # two generations (see k_dedup_rotate)
+        # store-backed dedup filter: blocked Bloom filter of every persisted alternate id (sw_bloom_*)
+        self._bloom_blocks = c.dedup_bloom_bits // 512
+        t["dd_bloom"] = z(8 * max(1, self._bloom_blocks), i64)
         t["dd_seq"] = full(2 * c.dedup_slots, -1, i64)
         t["dd_meta"] = z(4, i64)
         t["seq_base"] = z(1, i64)
@@ -198,7 +201,7 @@ class GpuInboundEngine(EngineBase):
         t["ev_slot"] = z(2 * max(c.rec_cap, c.gen_cap), torch.int64)   # (slot, date) state pass-2 items
         t["zmask"] = z(c.rec_cap, i64)
         t["ztile"] = z(2 * ntiles + 64, i32)
-        t["stats"] = z(16, i64)
+        t["stats"] = z(N_STATS, i64)
         t["sp"] = z(8, i64)                      # SwStepParams (per-step values read by the process phase)
         self._set_zone_tensors()
         self.args = a = SwEngineArgs()
@@ -226,6 +229,8 @@ class GpuInboundEngine(EngineBase):
         a.reg, a.reg_mask = _ptr(t["reg"]), c.reg_slots - 1
         a.asg_ctx, a.asg_active, a.n_asg = _ptr(t["asg_ctx"]), _ptr(t["asg_active"]), c.max_assignments
         a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_key"]), _ptr(t["dd_seq"]), c.dedup_slots - 1, _ptr(t["seq_base"])
+        a.dd_bloom = _ptr(t["dd_bloom"]) if self._bloom_blocks else 0
+        a.dd_bloom_mask = self._bloom_blocks - 1 if self._bloom_blocks else 0
         a.dd_meta = _ptr(t["dd_meta"])
         a.nm_key, a.nm_id, a.nm_first = _ptr(t["nm_key"]), _ptr(t["nm_id"]), _ptr(t["nm_first"])
         a.nm_mask, a.nm_counter = c.name_slots - 1, _ptr(t["nm_counter"])
@@ -1170,11 +1175,26 @@ class GpuInboundEngine(EngineBase):
     _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_key", "dd_seq", "dd_meta", "seq_base", "nm_key", "nm_id", "nm_first",
                     "nm_counter", "seen_key", "st", "ms", "stats", "cursor")
 
+    def bloom_add(self, hashes):
+        """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
+        h = np.ascontiguousarray(np.asarray(hashes, np.uint64))
+        if not self._bloom_blocks or not len(h):
+            return
+        dev = torch.from_numpy(h.view(np.int64)).to(self.device)
+        rc = self.lib.sw_bloom_add(ctypes.c_void_p(_ptr(self.t["dd_bloom"])), self._bloom_blocks - 1,
+                                   ctypes.c_void_p(_ptr(dev)), len(h), self._stream())
+        if rc:
+            raise RuntimeError(f"sw_bloom_add failed ({rc})")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def _ckpt_tables(self):
+        return self._CKPT_TABLES + (("dd_bloom",) if self._bloom_blocks else ())
+
     def checkpoint_state(self, include_store: bool = False) -> dict:
         if self._pend is not None:
             raise RuntimeError("checkpoint with a pipelined exchange in flight: drain the round first")
         self._sync_streams()
-        st = {k: self.t[k].cpu().numpy() for k in self._CKPT_TABLES}
+        st = {k: self.t[k].cpu().numpy() for k in self._ckpt_tables()}
         if self.world > 1:
             cp = self._carry_par
             n = int(self.t["n_carry"][cp].item())
@@ -1185,8 +1205,15 @@ class GpuInboundEngine(EngineBase):
 
     def restore_state(self, a: dict, include_store: bool):
         self._sync_streams()
-        for k in self._CKPT_TABLES:
-            self.t[k].copy_(torch.from_numpy(a[k]))       # in place: captured graphs keep their pointers
+        for k in self._ckpt_tables():
+            if k not in a:
+                continue
+            src = torch.from_numpy(a[k])
+            if k == "stats" and src.numel() != self.t[k].numel():     # a checkpoint with fewer counters
+                self.t[k].zero_()
+                self.t[k][:src.numel()].copy_(src)
+                continue
+            self.t[k].copy_(src)       # in place: captured graphs keep their pointers
         if self.world > 1 and "carry" in a:
             cp = self._carry_par
             c = torch.from_numpy(a["carry"])

@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 from .._native import native
-from ..models.columnar import EVENT_REC, NAME_REF, OUT_REC, REG_SLOT, STAT_NAMES, STR_REF
+from ..models.columnar import EVENT_REC, N_STATS, NAME_REF, OUT_REC, REG_SLOT, STAT_NAMES, STR_REF
 from .config import EngineConfig
 from .cpu_engine import STORE_COLS, CpuInboundEngine
 from .engine_base import EngineBase, StepResult
@@ -81,12 +81,13 @@ class NativeCpuEngine(CpuInboundEngine):
         # packed mirrors the native stages read (kept current by the EngineBase dirty hooks)
         self.reg_packed = np.zeros(cfg.reg_slots, REG_SLOT)
         self.asg_ctx = np.full((cfg.max_assignments, 4), -1, np.int32)   # device, customer, area, asset
-        self.stats = np.zeros(16, np.uint64)
+        self.stats = np.zeros(N_STATS, np.uint64)
         self.threads = threads or default_threads()
         self._lib = native()
         self._h = self._lib.swce_create(self.threads)
         self._lib.swce_reserve(self._h, cfg.state_slots, cfg.dedup_slots)
         self._lib.swce_dedup_window(self._h, cfg.dedup_slots, cfg.rec_cap)
+        self._lib.swce_bloom_init(self._h, cfg.dedup_bloom_bits)
         for v in self.store.values():      # touch the ring now (the GPU's HBM store is resident too)
             v.fill(0)
         self._out_pool: dict = {}       # recycled outbound buffers per dtype (see _out_buffer)
@@ -101,6 +102,18 @@ class NativeCpuEngine(CpuInboundEngine):
         if h:
             self._lib.swce_destroy(h)
             self._h = None
+
+    def reset_dedup(self):
+        """Forget the alternate-id window (both generations); the store-backed filter stays."""
+        z64, zi = np.zeros(1, np.uint64), np.zeros(1, np.int64)
+        self._lib.swce_dedup_import(self._h, _ptr(z64), _ptr(zi), 0)
+        self._lib.swce_dedup_prev_import(self._h, _ptr(z64), _ptr(zi), 0)
+
+    def bloom_add(self, hashes):
+        """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
+        h = np.ascontiguousarray(np.asarray(hashes, np.uint64))
+        if len(h):
+            self._lib.swce_bloom_add(self._h, _ptr(h), len(h))
 
     # ------------------------------------------------------------------ packed mirrors
     def _dirty_registry(self, slots):
@@ -248,14 +261,23 @@ class NativeCpuEngine(CpuInboundEngine):
             "ms_key": ms[:, :3].copy(), "ms_val": ms[:, 3:].copy(),
             "carry": self.carry.view(np.uint8).reshape(-1).copy(),
         }
+        nw = lib.swce_bloom_words(h, None, 0)
+        if nw:
+            bw = np.zeros(nw, np.uint64)
+            lib.swce_bloom_words(h, _ptr(bw), nw)
+            st["dd_bloom"] = bw
         if include_store:
             st.update({f"store.{k}": v for k, v in self.store.items()})
         return st
 
     def restore_state(self, a: dict, include_store: bool):
         lib, h = self._lib, self._h
+        if "dd_bloom" in a:
+            bw = np.ascontiguousarray(a["dd_bloom"], np.uint64)
+            lib.swce_bloom_load(h, _ptr(bw), len(bw))
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
-        self.stats[:] = a["stats"]
+        self.stats[:] = 0
+        self.stats[:len(a["stats"])] = a["stats"]
         dk = np.ascontiguousarray(a["dedup_key"], np.uint64)
         ds = np.ascontiguousarray(a["dedup_seq"], np.int64)
         lib.swce_dedup_import(h, _ptr(dk), _ptr(ds), len(dk))

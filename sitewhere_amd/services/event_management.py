@@ -10,6 +10,8 @@ ListCommandResponsesForInvocation, ListCommandResponsesForIndex.
 """
 from __future__ import annotations
 
+import numpy as np
+
 
 from ..core.errors import ErrorCode, NotFoundException, SiteWhereSystemException
 from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceCommandInvocation,
@@ -146,6 +148,23 @@ class DeviceEventManagement:
         enriched-batch consumers resolve the indices their batches' deltas did not carry."""
         f = getattr(self.store, "dictionary", None)
         return f(boot, asg_ids, name_ids) if f is not None else {"asg": {}, "names": {}, "rules": {}}
+
+    def durable_alternate_hashes(self, max_ids: int = 1 << 26) -> bytes:
+        """Alternate-id hashes of the durable store, newest first (u64 little endian, at most
+        ``max_ids``): an engine tenant seeds its store-backed dedup filter with them on start."""
+        f = getattr(self.store, "alternate_hash_chunks", None)
+        if f is None:
+            return b""
+        return b"".join(np.ascontiguousarray(c, np.uint64).tobytes() for c in f(max_ids))
+
+    def durable_find_alternate_hashes(self, hashes: bytes) -> bytes:
+        """Which of these alternate-id hashes (u64 little endian) the durable store holds: the engine
+        tenant settles the ids its store-backed filter sent back with one lookup per step."""
+        f = getattr(self.store, "find_alternate_hashes", None)
+        h = np.frombuffer(hashes, np.uint64)
+        if f is None or not len(h):
+            return b""
+        return np.array(sorted(f(h.tolist())), np.uint64).tobytes()
 
     def add_durable_batch(self, payload) -> tuple[int, int]:
         """Queue an engine tenant's durable batch: (rows, token).  The rows are on disk once

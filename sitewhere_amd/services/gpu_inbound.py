@@ -88,6 +88,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.t_decoded = n.decoded_events(t)
         self.t_failed_decode = n.failed_decode_events(t)
         self.routed_payloads = 0                # payloads the slow path parsed (per payload, not per batch)
+        self.recheck_duplicates = 0             # filter rechecks the durable store knew: duplicates
         self.t_enriched_batches = n.tenant_prefix(t) + ENRICHED_BATCHES
         # objects: per-event host objects; columnar: row batches; durable: encoded blocks (GPU-encoded
         # on the MI355X) to a durable segment store, offsets committed once on disk
@@ -839,6 +840,13 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         em = self._em()
         if not hasattr(em, "durable_source_offset"):
             return
+        # store-backed dedup filter: seeded with the ids already stored, so a device re-sending an old
+        # payload after a restart is still handed to the store check
+        if getattr(self.engine.cfg, "dedup_bloom_bits", 0) and hasattr(em, "durable_alternate_hashes"):
+            h = np.frombuffer(em.durable_alternate_hashes(), np.uint64)
+            if len(h):
+                self.engine.bloom_add(h)
+                self.logger.info("dedup filter seeded with %d stored alternate ids", len(h))
         group = self.raw_consumer.group
         for topic in self.raw_consumer.topics:
             for p in range(bus.partitions(topic) if hasattr(bus, "partitions") else 1):
@@ -921,6 +929,28 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         return {"deviceId": e.device_id, "deviceToken": self._dev_tokens.get(di),
                 "assignmentStatus": "Active", "engine": self.engine_kind}
 
+    def _settle_rechecks(self, res, st):
+        """Ids the store-backed filter sent back (SW_ST_RECHECK): one bulk lookup in the durable
+        store's alternate-id index; those found there are duplicates (dropped, counted), the rest go
+        on to the per-event path, which stores them."""
+        from ..models.columnar import ST_DUPLICATE, ST_RECHECK
+        rk = st == ST_RECHECK
+        if not rk.any():
+            return st
+        em = self._em()
+        if not hasattr(em, "durable_find_alternate_hashes"):
+            return st
+        h = np.ascontiguousarray(res.rejects["alt_hash"][rk], np.uint64)
+        found = np.frombuffer(em.durable_find_alternate_hashes(h.tobytes()), np.uint64)
+        if not len(found):
+            return st
+        st = st.copy()
+        dup = rk.copy()
+        dup[rk] = np.isin(h, found)
+        st[dup] = ST_DUPLICATE
+        self.recheck_duplicates += int(dup.sum())
+        return st
+
     def _route(self, batch, res):
         """Route the step's rejected messages like the reference does, per payload: only the payloads
         the reject records point into are parsed (natively, ``pipeline/routing.py``).  Runs while the
@@ -930,6 +960,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         st = res.reject_status
         if st is None or not len(st):
             return None
+        st = self._settle_rechecks(res, st)
         bus = self.ms.instance.bus
         topics = (self.t_unregistered, self.t_registration, self.t_decoded, self.t_failed_decode)
         parts = [bus.partitions(t) if hasattr(bus, "partitions") else 1 for t in topics]

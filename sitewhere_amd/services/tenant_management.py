@@ -110,7 +110,10 @@ TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event stor
 TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
     storage="durable", publishEnriched="batches",
     capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
-              "dedup_slots": 1 << 21, "gen_cap": 32768})
+              "dedup_slots": 1 << 21, "gen_cap": 32768,
+              # store-backed dedup beyond the window: 2^28 bits (32 MB) ~ 32 bits for each of 8M stored
+              # ids (size it to the retention: 4 bytes per id kept)
+              "dedup_bloom_bits": 1 << 28})
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
     "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
                   "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}

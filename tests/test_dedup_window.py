@@ -93,3 +93,87 @@ def test_dedup_window_gpu_matches_oracle():
     engines = _engines()
     assert len(engines) == 3
     _check(engines, _run(engines))
+
+
+# ---------------------------------------------------------------------------- store-backed filter
+def _engines_bloom():
+    cfg = dict(CFG, dedup_bloom_bits=1 << 20)           # 128 KB: ~87 bits per id of the run
+    es = [CpuInboundEngine(EngineConfig.small(**cfg)), NativeCpuEngine(EngineConfig.small(**cfg))]
+    if gpu_available():
+        from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
+        es.append(GpuInboundEngine(EngineConfig.small(**cfg), device="cuda:0"))
+    heap, offs = gen_tokens("dev-", 0, N_DEV)
+    lo, hi = fingerprints(heap, offs)
+    for e in es:
+        d = e.register_devices(lo, hi)
+        e.set_assignments(d, d)
+    return es
+
+
+def _run_bloom(engines):
+    from sitewhere_amd.models.columnar import ST_RECHECK
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    per_step = []
+    for b, msgs in enumerate(_batches()):
+        raw, offs = pack_messages(msgs)
+        res = [e.step(raw, offs, 1_700_000_100_000 + b, presence=False) for e in engines]
+        per_step.append([(r.n_persisted, int(np.sum(r.reject_status == 3)), int(np.sum(r.reject_status == ST_RECHECK)),
+                          sorted(r.rejects["alt_hash"][r.reject_status == ST_RECHECK].tolist())) for r in res])
+    return per_step
+
+
+def _check_bloom(engines, per_step):
+    for b, row in enumerate(per_step):
+        assert all(x == row[0] for x in row), f"batch {b}: engines disagree"
+    stats = [e.stats_dict() for e in engines]
+    for s in stats[1:]:
+        assert s == stats[0], (stats[0], s)
+    s = stats[0]
+    assert s["dedup_rotations"] >= 4 and s["dedup_overflow"] == 0
+    # recent replays: duplicates inside the window; late replays (retired generations): every one is
+    # handed to the host for a store check instead of being stored a second time
+    for b, row in enumerate(per_step):
+        _, dups, rechecks, _ = row[0]
+        assert dups >= 40 if b >= 1 else dups == 0
+        assert rechecks >= 40 if b >= 20 else True
+    total_fresh = sum(300 for _ in per_step)
+    assert s["dedup_rechecks"] - sum(40 for b in range(20, len(per_step))) < 0.01 * total_fresh   # false positives
+
+
+def test_store_backed_filter_host_engines_agree():
+    engines = _engines_bloom()[:2]
+    _check_bloom(engines, _run_bloom(engines))
+
+
+def test_store_backed_filter_warm_start_and_checkpoint():
+    """The filter travels in engine checkpoints and can be seeded from stored ids (``bloom_add``, what
+    a restarted tenant does from its store's alternate-id index): ids seeded that way are rechecked."""
+    from sitewhere_amd.models.columnar import ST_RECHECK
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    raw, offs = pack_messages(_batches(n_batches=1)[0][:300])
+    for idx in (0, 1):                                 # oracle, native engine
+        a = _engines_bloom()[idx]
+        a.step(raw, offs, 1_700_000_100_000, presence=False)
+        ck = a.checkpoint_state()
+        assert "dd_bloom" in ck and np.asarray(ck["dd_bloom"]).any()
+        b = _engines_bloom()[idx]
+        b.restore_state(ck, include_store=False)
+        assert np.array_equal(np.asarray(b.checkpoint_state()["dd_bloom"]), np.asarray(ck["dd_bloom"]))
+        c = _engines_bloom()[idx]
+        c.bloom_add(_alt_hashes(raw, offs))
+        r = c.step(raw, offs, 1_700_000_300_000, presence=False)
+        assert int(np.sum(r.reject_status == ST_RECHECK)) == len(_alt_hashes(raw, offs)), idx
+
+
+def _alt_hashes(raw, offs):
+    from sitewhere_amd.pipeline.fleet import cpu_decode
+    recs = cpu_decode(raw, offs, 1_700_000_000_000)
+    return recs["alt_hash"][recs["alt_hash"] != 0]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+def test_store_backed_filter_gpu_matches_oracle():
+    engines = _engines_bloom()
+    assert len(engines) == 3
+    _check_bloom(engines, _run_bloom(engines))
