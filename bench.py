@@ -506,7 +506,8 @@ def main():
         dist.all_reduce(ct, op=dist.ReduceOp.SUM)
         cons = [int(x) for x in ct.tolist()]
     c = dict(zip(STAT_NAMES + ["durable_rows", "routed_payloads"], cons))
-    rejected = c["unregistered"] + c["unassigned"] + c["duplicates"] + c["decode_errors"] + c["control"]
+    rejected = c["unregistered"] + c["unassigned"] + c["duplicates"] + c["decode_errors"] + c["control"] + \
+        c["dedup_rechecks"]
     checks = {"persisted == events - rejected + rule_alerts + presence":
               c["persisted"] == c["events"] - rejected + c["rule_alerts"] + c["presence_events"],
               "no dedup / state / shuffle overflow": c["dedup_overflow"] == 0 and c["state_overflow"] == 0
@@ -515,8 +516,9 @@ def main():
         checks["durable rows == persisted"] = c["durable_rows"] == c["persisted"]
         checks["every block durable"] = bool(dur["sink"].store.durable() >= dur["sink"].store.seg.last_token)
     if bus_stats:
-        checks["routed payloads == unregistered + unassigned + control + decode errors"] = \
-            c["routed_payloads"] == c["unregistered"] + c["unassigned"] + c["control"] + c["decode_errors"]
+        checks["routed payloads == unregistered + unassigned + control + decode errors + rechecks"] = \
+            c["routed_payloads"] == c["unregistered"] + c["unassigned"] + c["control"] + c["decode_errors"] + \
+            c["dedup_rechecks"]
         checks["raw topic fully committed"] = \
             bus_stats["bus"].committed(bus_stats["group"], bus_stats["t_raw"], 0) == \
             bus_stats["bus"].end_offset(bus_stats["t_raw"], 0)
