@@ -519,6 +519,10 @@ class EventBus:
         self.lib.swlog_set_retention(self.h, self.topic(name), int(retention_bytes))
         self._ret_topic[name] = int(retention_bytes)
 
+    def retention(self, name: str) -> int:
+        """Retained bytes per partition of ``name`` (0 = unlimited)."""
+        return int(self._ret_topic.get(name, self._ret_default))
+
     # ------------------------------------------------------------------ backpressure
     def protect(self, group: str, name: str, max_wait_s: float = 60.0):
         """No silent loss on ``name`` for consumer ``group``: retention never drops a record the

@@ -230,7 +230,9 @@ class InboundProcessingProvider(ModelProvider):
             ("max_msgs", "payloads per micro-batch"), ("rec_cap", "decoded events per micro-batch"),
             ("gen_cap", "rule alerts + presence events per step"), ("max_devices", "registry capacity"),
             ("max_assignments", "assignment capacity"), ("store_cap", "HBM event ring (events)"),
-            ("dedup_slots", "alternate-id window slots per generation"), ("name_slots", "distinct names"),
+            ("dedup_slots", "alternate-id window slots per generation"),
+            ("dedup_bloom_bits", "store-backed dedup filter bits (0 = off; ~16 bits per stored id)"),
+            ("name_slots", "distinct names"),
             ("state_slots", "(assignment, name) state slots"), ("names_cap", "new-name reports per step"),
             ("shuffle_pad", "records added to every re-key slab"), ("carry_cap", "re-key carry records"),
             ("carry_high", "carry level that stalls new input"), ("presence_missing_ms", "presence missing"),

@@ -89,6 +89,9 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.t_failed_decode = n.failed_decode_events(t)
         self.routed_payloads = 0                # payloads the slow path parsed (per payload, not per batch)
         self.recheck_duplicates = 0             # filter rechecks the durable store knew: duplicates
+        self.recheck_false_positives = 0        # filter rechecks the store did not know (host path)
+        self._fp_win = [0, 0]                   # false positives / engine payloads since the last check
+        self.dedup_sizing_report: dict = {}
         self.t_enriched_batches = n.tenant_prefix(t) + ENRICHED_BATCHES
         # objects: per-event host objects; columnar: row batches; durable: encoded blocks (GPU-encoded
         # on the MI355X) to a durable segment store, offsets committed once on disk
@@ -306,6 +309,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             tune_gc_for_streaming()             # opt-in: measured gain is within run-to-run noise
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         self._resume_from_store()
+        self.check_dedup_sizing()
         bus = self.ms.instance.bus
         if self.config.get("rawBackpressure", True) and hasattr(bus, "protect"):
             # raw batches this engine has not committed are never dropped by retention; event
@@ -844,6 +848,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # payload after a restart is still handed to the store check
         if getattr(self.engine.cfg, "dedup_bloom_bits", 0) and hasattr(em, "durable_alternate_hashes"):
             h = np.frombuffer(em.durable_alternate_hashes(), np.uint64)
+            self._stored_ids = len(h)
             if len(h):
                 self.engine.bloom_add(h)
                 self.logger.info("dedup filter seeded with %d stored alternate ids", len(h))
@@ -929,26 +934,88 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         return {"deviceId": e.device_id, "deviceToken": self._dev_tokens.get(di),
                 "assignmentStatus": "Active", "engine": self.engine_kind}
 
+    # payloads are at least this many bytes on the raw topic (a delimited protobuf request carrying a
+    # device token and one event): the most ids a partition's retention can redeliver
+    MIN_PAYLOAD_BYTES = 24
+    # the blocked Bloom filter (8 bits of one 64-bit block per id) stays near 0.1-0.3% false positives
+    # up to one id per 16 bits, ~2.5% at one per 8
+    FILTER_BITS_PER_ID = 16
+
+    def check_dedup_sizing(self) -> dict:
+        """Runtime check of the engine's dedup sizing (docs/PARITY.md, alternate-id dedup): the HBM
+        window always holds the last ``dedup_slots / 2`` ids.  Without the store-backed filter, a raw
+        topic that can redeliver more payloads than that (its retention) lets an old id through
+        again; with the filter, stored ids past ``dedup_bloom_bits / 16`` raise its false-positive
+        rate (host lookups, not correctness).  Logs a warning per violated rule; returns the report
+        (also ``dedup_sizing_report``)."""
+        c = self.engine_cfg
+        bus = self.ms.instance.bus
+        window = int(c.dedup_slots) // 2
+        bits = int(getattr(c, "dedup_bloom_bits", 0) or 0)
+        redeliver = 0
+        for t in self.raw_consumer.topics:
+            r = bus.retention(t) if hasattr(bus, "retention") else 0
+            parts = bus.partitions(t) if hasattr(bus, "partitions") else 1
+            redeliver = -1 if (r <= 0 or redeliver < 0) else redeliver + parts * (r // self.MIN_PAYLOAD_BYTES)
+        stored = int(getattr(self, "_stored_ids", 0))
+        rep = {"window_ids": window, "filter_bits": bits, "filter_capacity_ids": bits // self.FILTER_BITS_PER_ID,
+               "raw_redeliverable_ids": None if redeliver < 0 else redeliver, "stored_ids": stored,
+               "warnings": []}
+        if not bits and (redeliver < 0 or redeliver > window):
+            rep["warnings"].append(
+                f"dedup window holds {window} ids but the raw topic can redeliver "
+                f"{'unbounded' if redeliver < 0 else redeliver} payloads and no store-backed filter is "
+                f"configured: raise capacity.dedup_slots to >= {2 * max(redeliver, 0) or 'twice the retention'} "
+                f"or set capacity.dedup_bloom_bits")
+        if bits and stored > rep["filter_capacity_ids"]:
+            rep["warnings"].append(
+                f"dedup filter of {bits} bits already holds {stored} stored ids (> {rep['filter_capacity_ids']}): "
+                f"false positives rise; size capacity.dedup_bloom_bits to >= {self.FILTER_BITS_PER_ID * stored}")
+        for w in rep["warnings"]:
+            self.logger.warning("%s", w)
+        self.dedup_sizing_report = rep
+        return rep
+
+    def _watch_filter(self, n_payloads: int, false_pos: int):
+        """Filter false positives measured in flight: above 1% of the engine's payloads over a
+        window of 2^22, warn (the filter is saturated -- size ``dedup_bloom_bits`` to the ids kept)."""
+        w = self._fp_win
+        w[0] += false_pos
+        w[1] += n_payloads
+        if w[1] >= 1 << 22:
+            if w[0] > 0.01 * w[1]:
+                self.logger.warning("dedup filter false positives at %.2f%% of payloads: saturated, raise "
+                                    "capacity.dedup_bloom_bits", 100.0 * w[0] / w[1])
+                self.dedup_sizing_report.setdefault("warnings", []).append(
+                    f"filter false positives {w[0]}/{w[1]}")
+            w[0] = w[1] = 0
+
     def _settle_rechecks(self, res, st):
         """Ids the store-backed filter sent back (SW_ST_RECHECK): one bulk lookup in the durable
         store's alternate-id index; those found there are duplicates (dropped, counted), the rest go
         on to the per-event path, which stores them."""
         from ..models.columnar import ST_DUPLICATE, ST_RECHECK
         rk = st == ST_RECHECK
-        if not rk.any():
+        n_rk = int(rk.sum())
+        n_payloads = int(getattr(res, "n_msgs", 0) or 0)
+        if not n_rk:
+            self._watch_filter(n_payloads, 0)
             return st
         em = self._em()
         if not hasattr(em, "durable_find_alternate_hashes"):
             return st
         h = np.ascontiguousarray(res.rejects["alt_hash"][rk], np.uint64)
         found = np.frombuffer(em.durable_find_alternate_hashes(h.tobytes()), np.uint64)
-        if not len(found):
-            return st
-        st = st.copy()
-        dup = rk.copy()
-        dup[rk] = np.isin(h, found)
-        st[dup] = ST_DUPLICATE
-        self.recheck_duplicates += int(dup.sum())
+        n_dup = 0
+        if len(found):
+            st = st.copy()
+            dup = rk.copy()
+            dup[rk] = np.isin(h, found)
+            st[dup] = ST_DUPLICATE
+            n_dup = int(dup.sum())
+        self.recheck_duplicates += n_dup
+        self.recheck_false_positives += n_rk - n_dup
+        self._watch_filter(n_payloads, n_rk - n_dup)
         return st
 
     def _route(self, batch, res):
