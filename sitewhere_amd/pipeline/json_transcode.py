@@ -2,8 +2,9 @@
 
 A JSON event source that forwards raw batches (``forward: raw``) hands the fused engine the same
 protobuf payloads a protobuf device would send: measurements, locations and Info-level device
-alerts whose fields the engine path represents exactly.  Anything else (registrations, acks,
-metadata, non-integer dates, invalid JSON) is not transcoded and keeps the per-event path, so its
+alerts, with alternate ids, messages and metadata (the engine path stores them losslessly: durable
+blocks, and event objects materialized from the step's block).  Anything else (registrations,
+acks, non-integer dates, invalid JSON) is not transcoded and keeps the per-event path, so its
 handling -- including decode-failure reporting -- is the reference's."""
 from __future__ import annotations
 

@@ -223,14 +223,16 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         from ..persistence.segments import boot_id
         self.boot = boot
         self.block_boot = boot_id(boot)
-        if self.storage == "durable" and hasattr(self.engine, "encode_blocks"):
+        # durable: the block is what is stored; objects: the block is where each row's strings are
+        # (alternate id, alert message, metadata) when the rows become event objects (_to_events)
+        if self.storage in ("durable", "objects") and hasattr(self.engine, "encode_blocks"):
             self.engine.encode_blocks = True            # MI355X: blocks encoded on the GPU per step
             self.engine.block_boot = self.block_boot
 
     def _ensure_block(self, res, now: int):
         """Host engines encode the step's block on the completing thread (their event ring is
         overwritten by later steps)."""
-        if self.storage == "durable" and res is not None and res.block is None:
+        if self.storage in ("durable", "objects") and res is not None and res.block is None:
             res.block = self.engine.encode_block(now, res, boot=self.block_boot)
 
     # ---------------------------------------------------------------- registry mirror
@@ -900,6 +902,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         out = res.out
         if out is None or not len(out):
             return []
+        if getattr(res, "block", None) is not None:
+            return self._block_events(res)
         eids = res.event_ids()
         tests = self.engine.tests
         events = []
@@ -928,6 +932,23 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                 continue
             events.append(e)
         return events
+
+    def _block_events(self, res) -> list:
+        """The step's rows as reference event objects, read from its encoded block: lossless --
+        alternate ids, device alert messages, metadata and elevation come back as sent
+        (``persistence.segments.materialize_row``, the durable store's own reader)."""
+        from ..persistence.segments import decode_block, materialize_row
+        blk = res.block
+        cols = decode_block(blk if not hasattr(blk, "cpu") else blk.cpu().numpy())
+        asg = {}
+        for ai in np.unique(cols["asg"]).tolist():
+            a = self._asg_entities.get(int(ai))
+            if a is not None:
+                asg[int(ai)] = [a.id, a.device_id, a.customer_id, a.area_id, a.asset_id]
+        names = {int(n): self._name(int(n)) for n in np.unique(cols["name"]).tolist() if int(n) != NO_NAME}
+        rules = {t.alert_type: t.alert_message for t in self.engine.tests}
+        return [materialize_row(cols, i, asg, names, rules) for i in range(len(cols["etype"]))
+                if int(cols["asg"][i]) in asg]
 
     def _context(self, e) -> dict:
         di = self.dev_index.idx.get(e.device_id, -1)

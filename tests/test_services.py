@@ -353,8 +353,8 @@ def test_columnar_tenant_end_to_end():
 def test_gpu_template_routes_protobuf_raw_and_json_per_event():
     """gpu template: protobuf payloads reach the fused engine as raw micro-batches (size- or
     time-flushed); JSON measurements join them transcoded to protobuf (``pipeline/json_transcode``),
-    while a JSON request the engine path cannot represent (metadata) keeps the per-event path.
-    All end up persisted."""
+    metadata included: the engine rows become event objects through the step's block, which
+    carries the strings (alternate ids, messages, metadata).  All end up persisted."""
     import json as _json
     inst = SiteWhereInstance().start()
     try:
@@ -384,11 +384,11 @@ def test_gpu_template_routes_protobuf_raw_and_json_per_event():
                                                              {"pageSize": 0})).results
             return sorted(m.name for m in res)
         assert wait_until(lambda: names() == ["jm", "js"] + ["pb"] * 7, 20), names()
-        assert ib.engine.stats_dict()["events"] >= 8               # 7 protobuf + the transcoded JSON
-        assert es.manager.sources["default-json"].transcoded == 1
+        assert ib.engine.stats_dict()["events"] >= 9               # 7 protobuf + the 2 transcoded JSON
+        assert es.manager.sources["default-json"].transcoded == 2
         res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id],
                                                          {"pageSize": 0})).results
-        assert next(m for m in res if m.name == "jm").metadata == {"unit": "C"}   # per-event path kept it
+        assert next(m for m in res if m.name == "jm").metadata == {"unit": "C"}   # the engine path kept it
     finally:
         inst.stop()
 
