@@ -540,8 +540,17 @@ def main():
                          "checked": len(checks)},
     }
     if world > 1:
-        from sitewhere_amd.parallel.sharding import exchange_bytes_per_rank
-        detail["exchange_bytes_per_rank_step"] = exchange_bytes_per_rank(cfg.rec_cap, world)
+        # what one rank sends per step: its record slab for every destination, plus (lossless
+        # records) the string refs and string byte slabs beside them
+        detail["exchange_bytes_per_rank_step"] = world * cfg.shuf_cap * 64 + \
+            (world * cfg.shuf_cap * 16 + world * cfg.str_cap if cfg.str_cap else 0)
+        if hasattr(eng, "string_drops"):
+            drops = torch.tensor(list(eng.string_drops().values()), dtype=torch.int64,
+                                 device=torch.device("cuda", local) if use_gpu else "cpu")
+            dist.all_reduce(drops, op=dist.ReduceOp.SUM)
+            detail["string_exchange"] = {"bytes_per_slot": cfg.str_bytes, "slab_bytes": cfg.str_cap,
+                                         "records_without_strings": {"slab_full": int(drops[0]),
+                                                                     "carried": int(drops[1])}}
         detail["shuffle_deferred"] = s1.get("shuffle_deferred", 0) - s0.get("shuffle_deferred", 0)
         detail["shuffle_overflow"] = s1.get("shuffle_overflow", 0) - s0.get("shuffle_overflow", 0)
         detail["stall_rounds"] = stalls["rounds"]

@@ -90,6 +90,18 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
   return res;
 }
 
+// Sum of v[0 .. k), returned to every thread of the block: the prologue reduce of the per-tile sums
+// the PREVIOUS kernel wrote, in place of a separate single-workgroup scan dispatch between the two
+// (a few thousand L2-resident u32s: ~1-2 us of loads per block against ~5-8 us per extra dispatch,
+// and no flags, fences or counters -- the kernel boundary is the only synchronisation).
+__device__ __forceinline__ uint32_t block_sum_prefix(const uint32_t* v, int64_t k, uint32_t* lds) {
+  uint32_t s = 0;
+  for (int64_t i = threadIdx.x; i < k; i += BLK) s += v[i];
+  uint32_t tot;
+  block_excl_scan(s, &tot, lds);
+  return tot;
+}
+
 // ============================================================================ scan
 // Exclusive scan of u32[n] -> out, total -> *total.  n <= TILE * (BLK * 64).
 __global__ void k_scan_tiles(const uint32_t* __restrict__ in, int64_t n, uint32_t* __restrict__ tsum) {
@@ -104,20 +116,6 @@ __global__ void k_scan_tiles(const uint32_t* __restrict__ in, int64_t n, uint32_
   uint32_t tot;
   block_excl_scan(s, &tot, lds);
   if (threadIdx.x == 0) tsum[BID] = tot;
-}
-
-__global__ void k_scan_sums(uint32_t* __restrict__ tsum, int64_t nt, uint32_t* __restrict__ total) {
-  __shared__ uint32_t lds[WAVES + 1];
-  const int64_t per = (nt + BLK - 1) / BLK;
-  const int64_t b = (int64_t)threadIdx.x * per;
-  uint32_t s = 0;
-  for (int64_t i = 0; i < per; ++i) if (b + i < nt) s += tsum[b + i];
-  uint32_t tot;
-  uint32_t pre = block_excl_scan(s, &tot, lds);
-  for (int64_t i = 0; i < per; ++i) {
-    if (b + i < nt) { uint32_t t = tsum[b + i]; tsum[b + i] = pre; pre += t; }
-  }
-  if (threadIdx.x == 0 && total) *total = tot;
 }
 
 __global__ void k_scan_apply(const uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ tsum,
@@ -275,12 +273,18 @@ __global__ void k_vlen_tiles(const uint8_t* __restrict__ L, int64_t nbytes, uint
   if (threadIdx.x == 0) { tcnt[BID] = tc; tlen[BID] = tv; }
 }
 
+// Offsets from the tile sums of k_vlen_tiles, reduced in this kernel's prologue (no scan dispatch);
+// the last tile also writes the terminal offset msg_off[n_msgs] = the byte total, clamped to the batch.
 __global__ void k_vlen_apply(const uint8_t* __restrict__ L, int64_t nbytes, const uint32_t* __restrict__ tcnt,
                              const uint32_t* __restrict__ tlen, uint32_t* __restrict__ msg_off, int64_t n_msgs,
                              uint32_t raw_bytes) {
   __shared__ uint32_t lds[WAVES + 1];
   const int64_t base = (int64_t)BID * TILE;
-  uint32_t run_c = tcnt[BID], run_v = tlen[BID];
+  uint32_t run_c = block_sum_prefix(tcnt, BID, lds), run_v = block_sum_prefix(tlen, BID, lds);
+  if (BID == gridDim.x - 1 && threadIdx.x == 0) {
+    const uint32_t tl = run_v + tlen[BID];
+    msg_off[n_msgs] = tl < raw_bytes ? tl : raw_bytes;
+  }
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
@@ -296,30 +300,6 @@ __global__ void k_vlen_apply(const uint8_t* __restrict__ L, int64_t nbytes, cons
     run_c += tc;
     run_v += tv;
   }
-}
-
-// Both tile-sum scans of the framing (message counts, byte lengths) in one workgroup; the byte
-// total, clamped to the batch, is the terminal offset msg_off[n_msgs].
-__global__ void k_vlen_sums(uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tlen, int64_t nt,
-                            uint32_t* __restrict__ msg_off, int64_t n_msgs, uint32_t raw_bytes) {
-  __shared__ uint32_t lds[WAVES + 1];
-  const int64_t per = (nt + BLK - 1) / BLK;
-  const int64_t b = (int64_t)threadIdx.x * per;
-  uint32_t sc = 0, sl = 0;
-  for (int64_t i = 0; i < per; ++i) {
-    if (b + i < nt) { sc += tcnt[b + i]; sl += tlen[b + i]; }
-  }
-  uint32_t tc, tl;
-  uint32_t pc = block_excl_scan(sc, &tc, lds);
-  uint32_t pl = block_excl_scan(sl, &tl, lds);
-  for (int64_t i = 0; i < per; ++i) {
-    if (b + i < nt) {
-      const uint32_t c = tcnt[b + i], l = tlen[b + i];
-      tcnt[b + i] = pc; tlen[b + i] = pl;
-      pc += c; pl += l;
-    }
-  }
-  if (threadIdx.x == 0) msg_off[n_msgs] = tl < raw_bytes ? tl : raw_bytes;
 }
 
 // ============================================================================ decode
@@ -352,8 +332,13 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ raw, co
 
 __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict__ raw, const uint32_t* __restrict__ off,
                                                       int64_t n_msgs, uint32_t* __restrict__ cnt,
-                                                      uint32_t* __restrict__ tsum) {
+                                                      uint32_t* __restrict__ tsum, SwEngineArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[STAGE_BYTES];
+  if (BID == 0 && threadIdx.x == 0) {     // the decode phase's resets (k_decode_emit counts names after)
+    *a.n_new_names = 0;
+    *a.overflow = 0;
+    ((ull*)a.stats)[SW_STAT_MSGS] += (ull)a.n_msgs;
+  }
   uint32_t base = 0;
   const bool staged = stage_window(raw, off, n_msgs, lds, &base);
   __shared__ uint32_t red[WAVES + 1];
@@ -365,10 +350,10 @@ __global__ __launch_bounds__(BLK) void k_decode_count(const uint8_t* __restrict_
                : sw_decode_payload(raw, off[m], off[m + 1], 0, 0, 0, nullptr, 0, &verdict);
     cnt[m] = c | (verdict == SW_DEC_ERROR ? CNT_ERR : 0u) | (verdict == SW_DEC_OVERSIZE ? CNT_OVR : 0u);  // reused by emit
   }
-  // per-block record total: the block sums are scanned by one workgroup (k_scan_sums) and
-  // k_decode_emit rebuilds the in-block prefix itself -- reduce-then-scan with no look-back chain
-  // across the 4K blocks of a 1M batch (the single-pass scan serialised on cross-XCD flag polls,
-  // ~350 us per step: profiles/r3_fold)
+  // per-block record total: k_decode_emit reduces the block sums before it in its prologue and
+  // rebuilds the in-block prefix itself -- reduce-then-scan with no look-back chain across the 4K
+  // blocks of a 1M batch (the single-pass scan serialised on cross-XCD flag polls, ~350 us per
+  // step: profiles/r3_fold) and no scan dispatch between the two
   uint32_t tot;
   block_excl_scan(c, &tot, red);
   if (threadIdx.x == 0) tsum[BID] = tot;
@@ -412,9 +397,14 @@ __global__ __launch_bounds__(BLK) void k_decode_emit(SwEngineArgs a) {
   uint32_t tot;
   const uint32_t cv = m < a.n_msgs ? a.msg_cnt[m] : 0u;
   const uint32_t pre = block_excl_scan(cv & ~(CNT_ERR | CNT_OVR), &tot, red);
+  const uint32_t blk_off = block_sum_prefix(a.msg_evoff, BID, red);   // msg_evoff: the block sums
+  if (BID == 0) {                           // the batch's record count (clamped by the consumers)
+    const uint32_t all = block_sum_prefix(a.msg_evoff, gridDim.x, red);
+    if (threadIdx.x == 0) *a.n_recs = all;
+  }
   if (m >= a.n_msgs) return;
   uint32_t verdict = (cv & CNT_ERR) ? SW_DEC_ERROR : (cv & CNT_OVR) ? SW_DEC_OVERSIZE : SW_DEC_VALID;
-  const int64_t o = (int64_t)a.msg_evoff[BID] + pre;      // msg_evoff holds the scanned block sums
+  const int64_t o = (int64_t)blk_off + pre;
   if (o >= a.rec_cap) return;
   const uint32_t room = (uint32_t)((a.rec_cap - o) < 0xffffffffll ? (a.rec_cap - o) : 0xffffffffll);
   SwEventRec* out = a.recs + o;
@@ -454,9 +444,12 @@ __device__ __forceinline__ const SwEventRec& part_in(const SwEventRec* __restric
 
 __global__ void k_part_count(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
                              const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                             int world, int rank, uint32_t* __restrict__ tcount /*[world][ntiles]*/, int64_t ntiles) {
+                             int world, int rank, uint32_t* __restrict__ tcount /*[world][ntiles]*/, int64_t ntiles,
+                             uint32_t* __restrict__ send_str_cnt) {
   __shared__ uint32_t cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+  // the string slabs' byte cursors start empty (k_part_write allocates from them)
+  if (send_str_cnt && BID == 0 && threadIdx.x < (uint32_t)world) send_str_cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t nc = *nc_ptr;
   const int64_t n = (int64_t)nc + *n_ptr;
@@ -480,11 +473,53 @@ __device__ __forceinline__ uint32_t part_total(const uint32_t* __restrict__ toff
   return toff[last] + tcount[last] - toff[(int64_t)q * ntiles];
 }
 
+// A record's strings into its destination's byte slab (alternate id, metadata, alert message, in that
+// order), returning its refs rewritten to slab offsets; the alert message offset goes to *msg_off.
+// Strings that do not fit the slab are dropped (counted in str_drops[0]); carried records (decoded
+// in an earlier step, whose raw batch is gone) have none (str_drops[1]).
+__device__ __forceinline__ SwStrRef part_strings(const SwEngineArgs& a, const SwEventRec& r, const SwStrRef* s,
+                                                 uint32_t o, uint32_t* msg_off, uint16_t* msg_len) {
+  SwStrRef z;
+  z.alt_off = 0; z.meta_off = 0; z.alt_len = 0; z.meta_len = 0; z.k = 0; z.has = 0; z.pad = 0;
+  *msg_off = 0;
+  *msg_len = 0;
+  const bool alert = r.etype == SW_EV_ALERT;
+  if (!s) {                                  // carried record
+    if (r.alt_hash || (alert && r.aux2_len)) atomicAdd(&a.str_drops[1], 1u);
+    return z;
+  }
+  const SwStrRef sr = *s;
+  const uint32_t al = (sr.has & SW_SR_ALT) ? sr.alt_len : 0u;
+  const uint32_t ml = (sr.has & SW_SR_META) ? sr.meta_len : 0u;
+  const uint32_t gl = alert ? r.aux2_len : 0u;
+  const uint32_t len = al + ml + gl;
+  if (len == 0) {
+    z.k = sr.k;
+    z.has = sr.has & SW_SR_MULTI;
+    return z;
+  }
+  const uint32_t at = atomicAdd(&a.send_str_cnt[o], len);
+  if ((int64_t)at + len > a.str_cap) {
+    atomicAdd(&a.str_drops[0], 1u);
+    return z;
+  }
+  uint8_t* dst = a.send_str + (int64_t)o * a.str_cap + at;
+  for (uint32_t b = 0; b < al; ++b) dst[b] = a.raw[sr.alt_off + b];
+  for (uint32_t b = 0; b < ml; ++b) dst[al + b] = a.raw[sr.meta_off + b];
+  for (uint32_t b = 0; b < gl; ++b) dst[al + ml + b] = a.raw[r.aux2_off + b];
+  z = sr;
+  z.alt_off = at;
+  z.meta_off = at + al;
+  *msg_off = at + al + ml;
+  *msg_len = (uint16_t)gl;
+  return z;
+}
+
 __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
                              const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr, int world,
                              int rank, const uint32_t* __restrict__ toff /*scanned [world][ntiles]*/,
                              const uint32_t* __restrict__ tcount, int64_t ntiles, SwWireRec* __restrict__ send,
-                             int64_t shuf_cap, SwEventRec* __restrict__ spill, int64_t carry_cap) {
+                             int64_t shuf_cap, SwEventRec* __restrict__ spill, int64_t carry_cap, SwEngineArgs a) {
   __shared__ uint32_t run[64];
   __shared__ uint32_t spill_base[64];
   __shared__ uint32_t wcnt[WAVES][64];
@@ -522,7 +557,19 @@ __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_
       for (uint32_t w = 0; w < wid; ++w) pre += wcnt[w][o];
       pre += my_rank;
       if (pre < shuf_cap) {
-        send[(int64_t)o * shuf_cap + pre] = sw_wire_pack(part_in(carry, nc, recs, i));
+        SwEventRec r = part_in(carry, nc, recs, i);
+        if (a.send_str && r.etype < 16) {      // control records keep their raw-batch offsets
+          uint32_t moff;
+          uint16_t mlen;
+          const SwStrRef* s = i >= (int64_t)nc ? a.spans + (i - nc) : nullptr;
+          a.send_spans[(int64_t)o * shuf_cap + pre] = part_strings(a, r, s, o, &moff, &mlen);
+          if (r.etype == SW_EV_ALERT) { r.aux2_off = moff; r.aux2_len = mlen; }
+        } else if (a.send_str) {
+          SwStrRef z;
+          z.alt_off = 0; z.meta_off = 0; z.alt_len = 0; z.meta_len = 0; z.k = 0; z.has = 0; z.pad = 0;
+          a.send_spans[(int64_t)o * shuf_cap + pre] = z;
+        }
+        send[(int64_t)o * shuf_cap + pre] = sw_wire_pack(r);
       } else {
         const int64_t j = (int64_t)spill_base[o] + (pre - shuf_cap);
         if (j < carry_cap) spill[j] = part_in(carry, nc, recs, i);
@@ -556,9 +603,13 @@ __global__ void k_part_counts(const uint32_t* __restrict__ toff, const uint32_t*
   }
 }
 
-// Concatenate the received [world][shuf_cap] slabs into one dense batch (rank order).
+// Concatenate the received [world][shuf_cap] slabs into one dense batch (rank order).  With the
+// string exchange on, each record's refs come along rebased into work_str (+ source rank *
+// str_cap), and the received byte slabs are gathered into work_str -- the receive buffers are
+// reused by the next exchange while this step's block may still be encoding.
 __global__ void k_unpack(const SwWireRec* __restrict__ recv, const uint32_t* __restrict__ recv_cnt, int world,
-                         int64_t shuf_cap, SwEventRec* __restrict__ work, uint32_t* __restrict__ n_work, int64_t cap) {
+                         int64_t shuf_cap, SwEventRec* __restrict__ work, uint32_t* __restrict__ n_work, int64_t cap,
+                         SwEngineArgs a) {
   __shared__ uint32_t pre[65];
   if (threadIdx.x == 0) {
     pre[0] = 0;
@@ -567,10 +618,29 @@ __global__ void k_unpack(const SwWireRec* __restrict__ recv, const uint32_t* __r
   __syncthreads();
   const uint32_t total = pre[world] < cap ? pre[world] : (uint32_t)cap;
   if (BID == 0 && threadIdx.x == 0) *n_work = total;
+  const bool strings = a.work_str != nullptr;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLK) {
     int q = 0;
     while (q + 1 < world && i >= pre[q + 1]) ++q;
-    work[i] = sw_wire_unpack(recv[(int64_t)q * shuf_cap + (i - pre[q])], (uint8_t)q);
+    SwEventRec r = sw_wire_unpack(recv[(int64_t)q * shuf_cap + (i - pre[q])], (uint8_t)q);
+    if (strings) {
+      SwStrRef sr = a.recv_spans[(int64_t)q * shuf_cap + (i - pre[q])];
+      const uint32_t base = (uint32_t)((int64_t)q * a.str_cap);
+      sr.alt_off += base;
+      sr.meta_off += base;
+      if (r.etype == SW_EV_ALERT) r.aux2_off += base;
+      a.work_spans[i] = sr;
+    }
+    work[i] = r;
+  }
+  if (strings) {                             // the used part of every received byte slab, 16 B at a time
+    for (int q = 0; q < world; ++q) {
+      const uint32_t used = a.recv_str_cnt[q] < a.str_cap ? a.recv_str_cnt[q] : (uint32_t)a.str_cap;
+      const uint4* src = reinterpret_cast<const uint4*>(a.recv_str + (int64_t)q * a.str_cap);
+      uint4* dst = reinterpret_cast<uint4*>(a.work_str + (int64_t)q * a.str_cap);
+      for (int64_t v = (int64_t)BID * BLK + threadIdx.x; v < (used + 15) / 16; v += (int64_t)gridDim.x * BLK)
+        dst[v] = src[v];
+    }
   }
 }
 
@@ -598,18 +668,28 @@ __device__ __forceinline__ void intern_insert(ull* __restrict__ key, int32_t* __
 // One probe of the packed registry resolves device AND active assignment; names of every
 // decodable event are interned here too (fused: one pass over the records).
 __global__ void k_lookup(SwEngineArgs a) {
-  // generation rotation decided by k_process_begin: clear the table that becomes `cur` (dedup runs
-  // after this kernel); folded here instead of a dispatch that exits at once on most steps
+  // generation rotation decided by the previous step's k_step_end: clear the table that becomes
+  // `cur` (dedup runs after this kernel)
   if (a.dd_meta[2]) {
     const int64_t slots = a.dd_mask + 1;
-    ull* k = (ull*)a.dd_key + a.dd_meta[0] * slots;
-    ull* q = (ull*)a.dd_seq + a.dd_meta[0] * slots;
-    for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK) {
-      k[i] = 0ull;
-      q[i] = ~0ull;
-    }
+    ulonglong2* t = reinterpret_cast<ulonglong2*>(a.dd_key) + a.dd_meta[0] * slots;
+    for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK)
+      t[i] = make_ulonglong2(0ull, ~0ull);
   }
-  const uint32_t n = *a.n_work;
+  // world == 1: the work batch is the decoded batch, clamped (every block derives the same count;
+  // block 0 stores it for the kernels after this one)
+  const uint32_t n = a.world == 1 ? (*a.n_recs < (uint32_t)a.rec_cap ? *a.n_recs : (uint32_t)a.rec_cap) : *a.n_work;
+  if (BID == 0 && threadIdx.x == 0) {      // start of the process phase (was its own dispatch)
+    if (a.world == 1) {
+      *a.n_recs = n;
+      *a.n_work = n;
+      ((ull*)a.stats)[SW_STAT_NEW_NAMES] += *a.n_new_names;
+    }
+    *a.step_cursor0 = *a.store_cursor;
+    *a.n_gen = 0;
+    *a.n_out = 0;
+    if (a.dd_meta[2]) ((ull*)a.stats)[SW_STAT_DEDUP_ROTATIONS] += 1;
+  }
   const SwEventRec* __restrict__ recs = a.work;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull lo = recs[i].fp_lo, hi = recs[i].fp_hi;
@@ -646,14 +726,14 @@ __global__ void k_lookup(SwEngineArgs a) {
 // generation before).  An event whose id is in `prev` is a duplicate; otherwise it is inserted into
 // `cur`, where the first occurrence (lowest global sequence) wins and every later one -- in this
 // batch or any later batch of the generation -- is a duplicate.  Before a step whose ids could push
-// `cur` past half its slots, the generations rotate (k_process_begin): `prev` is forgotten and
+// `cur` past half its slots, the generations rotate (decided by k_step_end): `prev` is forgotten and
 // cleared to become the new `cur`.  The window therefore covers the last slots/2 - rec_cap to
 // slots - rec_cap distinct ids, probes stay short (load <= 0.5), and a probe that still hits
 // MAX_PROBE is counted (SW_STAT_DEDUP_OVERFLOW) rather than silently ignored.
-__device__ __forceinline__ bool dd_find(const ull* __restrict__ key, int64_t mask, ull h) {
+__device__ __forceinline__ bool dd_find(const ull* __restrict__ tab, int64_t mask, ull h) {
   int64_t slot = (int64_t)(h & (ull)mask);
   for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-    const ull k = key[slot];
+    const ull k = tab[2 * slot];
     if (k == h) return true;
     if (k == 0) return false;
     slot = (slot + 1) & mask;
@@ -661,11 +741,21 @@ __device__ __forceinline__ bool dd_find(const ull* __restrict__ key, int64_t mas
   return false;
 }
 
-// dd_meta = [generation, ids in cur, rotate flag, pad]: k_process_begin decides the rotation,
+// dd_meta = [generation, ids in cur, rotate flag, pad]: k_step_end decides the next step's rotation,
 // k_lookup clears the retired generation.
+// Tables of packed 16-byte slots {key, win: u32, lmin: u32} (two generations of dd_mask + 1 slots):
+//   key  -- the alternate-id hash, claimed by CAS;
+//   win  -- low 32 bits of the sequence of the id that claimed the slot (plain store by the CAS
+//           winner: the slot's other fields are disjoint bytes);
+//   lmin -- lowest in-batch index of the ids that found the key already claimed in THIS batch
+//           (atomicMin; rare: only repeats inside one batch).
+// First occurrence = the slot was claimed in this batch and min(win - sb, lmin) is the id's index:
+// the same lowest-sequence rule as the host engines, with ONE memory-side atomic per new id (each
+// device-scope atomic is its own 64-byte request on the MI355X; the CAS + atomicMin form paid two).
+// win - sb needs the window (< 2^31 ids) to stay far below 2^32 sequences, which rotation ensures.
 __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                               uint8_t* __restrict__ status, ull* __restrict__ key, ull* __restrict__ seq,
-                               int64_t mask, const int64_t* __restrict__ seq_base, int64_t* __restrict__ meta,
+                               uint8_t* __restrict__ status, ull* __restrict__ tab, int64_t mask,
+                               const int64_t* __restrict__ seq_base, int64_t* __restrict__ meta,
                                ull* __restrict__ stats) {
   __shared__ uint32_t blk_new, blk_over;
   if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; }
@@ -674,21 +764,25 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
   const ull sb = (ull)*seq_base;
   const int64_t slots = mask + 1;
   const int64_t g = meta[0];
-  ull* ck = key + g * slots;
-  ull* cq = seq + g * slots;
-  const ull* pk = key + (1 - g) * slots;
+  ull* ct = tab + 2 * g * slots;
+  const ull* pt = tab + 2 * (1 - g) * slots;
   uint32_t my_new = 0, my_over = 0;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
-    if (dd_find(pk, mask, h)) { status[i] = SW_ST_DUPLICATE; continue; }
+    if (dd_find(pt, mask, h)) { status[i] = SW_ST_DUPLICATE; continue; }
     int64_t slot = (int64_t)(h & (ull)mask);
     bool placed = false;
     for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-      const ull old = atomicCAS(&ck[slot], 0ull, h);
-      if (old == 0 || old == h) {
-        my_new += old == 0 ? 1u : 0u;
-        atomicMin(&cq[slot], sb + (ull)i);
+      const ull old = atomicCAS(&ct[2 * slot], 0ull, h);
+      if (old == 0) {
+        ++my_new;
+        reinterpret_cast<uint32_t*>(&ct[2 * slot + 1])[0] = (uint32_t)(sb + (ull)i);
+        placed = true;
+        break;
+      }
+      if (old == h) {
+        atomicMin(reinterpret_cast<uint32_t*>(&ct[2 * slot + 1]) + 1, (uint32_t)i);
         placed = true;
         break;
       }
@@ -709,71 +803,77 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
 
 // The id's filter block holds all its bits: it may have been persisted before (beyond the window).
 __device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h) {
-  uint64_t m[8];
-  sw_bloom_bits(h, m);
-  const ulonglong2* b = reinterpret_cast<const ulonglong2*>(bloom + 8 * sw_bloom_block(h, bmask));
-  bool all = true;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const ulonglong2 v = b[w];
-    all &= (v.x & m[2 * w]) == m[2 * w] && (v.y & m[2 * w + 1]) == m[2 * w + 1];
-  }
-  return all;
+  const ull m = sw_bloom_bits(h);
+  return (bloom[sw_bloom_block(h, bmask)] & m) == m;
 }
 
 __device__ __forceinline__ void bloom_add(ull* __restrict__ bloom, int64_t bmask, ull h) {
-  uint64_t m[8];
-  sw_bloom_bits(h, m);
-  ull* b = bloom + 8 * sw_bloom_block(h, bmask);
-#pragma unroll
-  for (int w = 0; w < 8; ++w)
-    if (m[w] && (b[w] & m[w]) != m[w]) atomicOr(&b[w], (ull)m[w]);
+  atomicOr(&bloom[sw_bloom_block(h, bmask)], (ull)sw_bloom_bits(h));   // no return: fire-and-forget
 }
 
-__global__ void k_dedup_check(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                              uint8_t* __restrict__ status, const ull* __restrict__ key, const ull* __restrict__ seq,
-                              int64_t mask, const int64_t* __restrict__ seq_base, const int64_t* __restrict__ meta,
-                              const ull* __restrict__ bloom, int64_t bmask) {
-  const uint32_t n = *n_ptr;
-  const ull sb = (ull)*seq_base;
-  const int64_t slots = mask + 1;
-  const int64_t g = meta[0];
-  const ull* ck = key + g * slots;
-  const ull* cq = seq + g * slots;
-  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
-    const ull h = recs[i].alt_hash;
-    if (h == 0 || status[i] != SW_ST_OK) continue;
-    int64_t slot = (int64_t)(h & (ull)mask);
-    for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-      const ull k = ck[slot];
-      if (k == h) {
-        if (cq[slot] != sb + (ull)i) status[i] = SW_ST_DUPLICATE;
-        else if (bloom && bloom_has(bloom, bmask, h)) status[i] = SW_ST_RECHECK;   // first sight in the window
-        break;
-      }
-      if (k == 0) break;
-      slot = (slot + 1) & mask;
+// Second half of the dedup (fused into the compaction count, k_cmp_count): the id's verdict from
+// its slot's {key, win, lmin}, one 16-byte load; a first sighting the store-backed filter may hold
+// becomes SW_ST_RECHECK.
+struct DedupView {
+  const ulonglong2* ct;       // live generation (null: no alternate-id dedup this step)
+  int64_t mask;
+  uint32_t sb, n;
+  const ull* bloom;
+  int64_t bmask;
+};
+
+__device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint32_t i) {
+  int64_t slot = (int64_t)(h & (ull)d.mask);
+  for (int64_t p = 0; p <= d.mask && p < MAX_PROBE; ++p) {
+    const ulonglong2 kq = d.ct[slot];
+    if (kq.x == h) {
+      const uint32_t wrel = (uint32_t)kq.y - d.sb;
+      const uint32_t lmin = (uint32_t)(kq.y >> 32);
+      const bool first = wrel < d.n && (wrel < lmin ? wrel : lmin) == i;
+      if (!first) return SW_ST_DUPLICATE;
+      return (d.bloom && bloom_has(d.bloom, d.bmask, h)) ? SW_ST_RECHECK : SW_ST_OK;   // first sight
     }
+    if (kq.x == 0) break;                // not placed (probe overflow, counted): kept
+    slot = (slot + 1) & d.mask;
   }
+  return SW_ST_OK;
 }
 
 // ============================================================================ compaction
-// Stable split of [0, n) into ok (status == OK) and rejected lists.
-__global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
-                            uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles, ull* __restrict__ stats) {
+// Stable split of [0, n) into ok (status == OK) and rejected lists.  The count pass also settles the
+// dedup verdict of every id k_dedup_insert left OK (dedup_verdict): no separate check dispatch.
+__global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
+                            uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles, ull* __restrict__ stats,
+                            const SwEventRec* __restrict__ recs, const ull* __restrict__ dd_tab, int64_t dd_mask,
+                            const int64_t* __restrict__ seq_base, const int64_t* __restrict__ dd_meta,
+                            const ull* __restrict__ bloom, int64_t bmask) {
   __shared__ uint32_t c[2];
   __shared__ uint32_t rs[8];          // rejects by status (the reject counters of the step)
   if (threadIdx.x < 2) c[threadIdx.x] = 0;
   if (threadIdx.x < 8) rs[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *n_ptr;
+  DedupView dv;
+  dv.ct = dd_tab ? reinterpret_cast<const ulonglong2*>(dd_tab) + dd_meta[0] * (dd_mask + 1) : nullptr;
+  dv.mask = dd_mask;
+  dv.sb = (uint32_t)*seq_base;
+  dv.n = n;
+  dv.bloom = bloom;
+  dv.bmask = bmask;
   const int64_t base = (int64_t)BID * TILE;
   uint32_t ok = 0, all = 0;
 #pragma unroll
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool v = i < n;
-    const uint8_t st = v ? status[i] : (uint8_t)SW_ST_OK;
+    uint8_t st = v ? status[i] : (uint8_t)SW_ST_OK;
+    if (v && st == SW_ST_OK && dv.ct) {
+      const ull h = recs[i].alt_hash;
+      if (h) {
+        st = dedup_verdict(dv, h, (uint32_t)i);
+        if (st != SW_ST_OK) status[i] = st;
+      }
+    }
     ok += __popcll(__ballot(v && st == SW_ST_OK));
     all += __popcll(__ballot(v));
     if (st != SW_ST_OK) atomicAdd(&rs[st & 7], 1u);       // rare: ~1% of events
@@ -792,16 +892,20 @@ __global__ void k_cmp_count(const uint8_t* __restrict__ status, const uint32_t* 
   }
 }
 
+// Tile offsets from k_cmp_count's tile counts, reduced in the prologue (no scan dispatch).
 __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
-                            const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tcnt, int64_t ntiles,
+                            const uint32_t* __restrict__ tcnt, int64_t ntiles,
                             uint32_t* __restrict__ ok_idx, uint32_t* __restrict__ rej_idx,
                             uint32_t* __restrict__ n_ok, uint32_t* __restrict__ n_rej) {
   __shared__ uint32_t lds[WAVES + 1];
   const uint32_t n = *n_ptr;
   const int64_t base = (int64_t)BID * TILE;
-  const uint32_t rej_base = toff[ntiles];  // rejected region starts after all ok counts in the flat scan
-  uint32_t run_ok = toff[BID];
-  uint32_t run_rj = toff[ntiles + BID] - rej_base;
+  uint32_t run_ok = block_sum_prefix(tcnt, BID, lds);
+  uint32_t run_rj = block_sum_prefix(tcnt + ntiles, BID, lds);
+  if (BID == gridDim.x - 1 && threadIdx.x == 0) {
+    *n_ok = run_ok + tcnt[BID];
+    *n_rej = run_rj + tcnt[ntiles + BID];
+  }
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool valid = i < n;
@@ -814,11 +918,6 @@ __global__ void k_cmp_write(const uint8_t* __restrict__ status, const uint32_t* 
     if (rj) rej_idx[run_rj + p_rj] = (uint32_t)i;
     run_ok += tot_ok;
     run_rj += tot_rj;
-  }
-  if (BID == gridDim.x - 1 && threadIdx.x == 0) {
-    const int64_t last = ntiles - 1;
-    *n_ok = toff[last] + tcnt[last];
-    *n_rej = toff[ntiles + last] + tcnt[ntiles + last] - rej_base;
   }
 }
 
@@ -866,9 +965,10 @@ __device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t ma
 // the name probe and the state-map probe run once per event instead of once per pass.
 __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                           const int32_t* __restrict__ devs, const int32_t* __restrict__ asgs,
-                          const uint32_t* __restrict__ n_ptr, uint32_t cap, const SwStrRef* __restrict__ spans) {
+                          const uint32_t* __restrict__ n_ptr, uint32_t cap, const SwStrRef* __restrict__ spans,
+                          const uint32_t* __restrict__ after) {
   const uint32_t n = *n_ptr < cap ? *n_ptr : cap;     // generated events: n_gen may pass gen_cap
-  const int64_t cur = *a.store_cursor;
+  const int64_t cur = *a.store_cursor + (after ? (int64_t)*after : 0);   // rows start past `after` rows
   const int64_t c0 = *a.step_cursor0;
   const int64_t now = a.sp->now_ms;
   SwSegAux* const aux = reinterpret_cast<SwSegAux*>(a.sp->aux);
@@ -950,9 +1050,10 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
 // ============================================================================ device state
 // Pass 2: among events carrying the max date, the highest event id wins (ids are monotonic).
 // Reads only k_persist's coalesced (slot, date) work items -- no event records, no probes.
-__global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, uint32_t cap) {
+__global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, uint32_t cap,
+                           const uint32_t* __restrict__ after) {
   const uint32_t n = *n_ptr < cap ? *n_ptr : cap;
-  const int64_t cur = *a.store_cursor;
+  const int64_t cur = *a.store_cursor + (after ? (int64_t)*after : 0);
   const longlong2* __restrict__ work = reinterpret_cast<const longlong2*>(a.ev_slot);
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const longlong2 w = work[j];
@@ -968,10 +1069,6 @@ __global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, u
       if (de.x == d && de.y < eid1) atomicMax((ull*)&a.ms[w.x].eid1, eid1);
     }
   }
-}
-
-__global__ void k_advance(int64_t* __restrict__ cursor, const uint32_t* __restrict__ n_ptr) {
-  if (threadIdx.x == 0 && BID == 0) *cursor += *n_ptr;
 }
 
 // ============================================================================ zone-test rules
@@ -1063,7 +1160,7 @@ __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restri
   ull outside_mask = 0;
   for (int t = 0; t < nt; ++t) outside_mask |= (L.t[t].y != 0) ? (1ull << t) : 0ull;
   const int64_t c0 = *a.step_cursor0;
-  const uint32_t n = (uint32_t)(*a.store_cursor - c0);
+  const uint32_t n = *a.n_ok;              // this step's persisted device events, from c0
   const int64_t base = (int64_t)BID * TILE;
   if (base >= n) {                       // tile past this step's rows
     if (threadIdx.x == 0) ztile[BID] = 0;
@@ -1136,13 +1233,19 @@ __global__ __launch_bounds__(BLK) void k_zone_mask(SwEngineArgs a, ull* __restri
 }
 
 // Pass 2: write the alerts at their scanned offsets (stable, no global atomics).
+// Tile offsets from k_zone_mask's tile counts, reduced in the prologue (no scan dispatch); the last
+// tile stores the step's rule alerts as n_gen and, clamped, n_rule -- before k_presence appends to
+// n_gen.
 __global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __restrict__ zmask,
-                                                   const uint32_t* __restrict__ zoff, uint32_t* __restrict__ n_rule) {
+                                                   const uint32_t* __restrict__ ztile, uint32_t* __restrict__ n_rule) {
   __shared__ uint32_t lds[WAVES + 1];
   __shared__ int4 lt[ZONE_LDS_TESTS];
-  // rule alerts of this step = the zone scan total (in n_gen), clamped; every block writes the same
-  // value, before k_presence appends to n_gen (no separate clamp dispatch)
-  if (threadIdx.x == 0) *n_rule = *a.n_gen < a.gen_cap ? *a.n_gen : (uint32_t)a.gen_cap;
+  uint32_t run = block_sum_prefix(ztile, BID, lds);
+  if (BID == gridDim.x - 1 && threadIdx.x == 0) {
+    const uint32_t all = run + ztile[BID];
+    *a.n_gen = all;
+    *n_rule = all < a.gen_cap ? all : (uint32_t)a.gen_cap;
+  }
   const int nt = a.n_tests < ZONE_LDS_TESTS ? (int)a.n_tests : ZONE_LDS_TESTS;
   for (int t = threadIdx.x; t < nt; t += BLK) {
     const SwZoneTest zt = a.tests[t];
@@ -1150,9 +1253,8 @@ __global__ __launch_bounds__(BLK) void k_zone_emit(SwEngineArgs a, const ull* __
   }
   __syncthreads();
   const int64_t c0 = *a.step_cursor0;
-  const uint32_t n = (uint32_t)(*a.store_cursor - c0);
+  const uint32_t n = *a.n_ok;              // this step's persisted device events, from c0
   const int64_t base = (int64_t)BID * TILE;
-  uint32_t run = zoff[BID];
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t j = base + (int64_t)k * BLK + threadIdx.x;
     ull fired = j < n ? zmask[j] : 0ull;
@@ -1220,31 +1322,6 @@ __global__ void k_decode_begin(SwEngineArgs a) {
   }
 }
 
-// Start of the process phase, one thread: (world == 1) the end of the decode phase -- record
-// clamp, new-name stats, the work batch is the decoded batch --, the step's cursor / counters, and
-// the dedup window rotation (before a step that could pass the live generation's half load).
-__global__ void k_process_begin(SwEngineArgs a) {
-  if (threadIdx.x == 0 && BID == 0) {
-    if (a.world == 1) {
-      if (*a.n_recs > a.rec_cap) *a.n_recs = (uint32_t)a.rec_cap;
-      ((ull*)a.stats)[SW_STAT_NEW_NAMES] += *a.n_new_names;
-      *a.n_work = *a.n_recs;
-    }
-    *a.step_cursor0 = *a.store_cursor;
-    *a.n_gen = 0;
-    *a.n_out = 0;
-    int64_t* meta = a.dd_meta;
-    if (meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) {
-      meta[0] ^= 1;
-      meta[1] = 0;
-      meta[2] = 1;
-      ((ull*)a.stats)[SW_STAT_DEDUP_ROTATIONS] += 1;
-    } else {
-      meta[2] = 0;
-    }
-  }
-}
-
 __global__ void k_gen_clamp(SwEngineArgs a, uint32_t* gen_rules) {
   if (threadIdx.x == 0 && BID == 0) {
     if (*a.n_gen > a.gen_cap) *a.n_gen = (uint32_t)a.gen_cap;
@@ -1255,7 +1332,7 @@ __global__ void k_gen_clamp(SwEngineArgs a, uint32_t* gen_rules) {
 __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
   if (threadIdx.x == 0 && BID == 0) {
     if (*a.n_gen > a.gen_cap) *a.n_gen = (uint32_t)a.gen_cap;   // presence appends past the cap were dropped
-    *a.store_cursor += *a.n_gen;                 // the generated events persisted last
+    *a.store_cursor += (int64_t)*a.n_ok + *a.n_gen;   // device events, then the generated ones
     *a.n_out = (uint32_t)(*a.store_cursor - *a.step_cursor0);
     *a.seq_base += *a.n_work;
     ull* st = (ull*)a.stats;
@@ -1263,6 +1340,16 @@ __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
     st[SW_STAT_PERSISTED] += *a.n_out;
     st[SW_STAT_RULE_ALERTS] += *n_rule_alerts;
     st[SW_STAT_PRESENCE] += *a.n_gen - *n_rule_alerts;
+    // the next step's dedup generation: rotate before a step whose ids could push the live table
+    // past half load (k_lookup of that step clears the retired table and counts the rotation)
+    int64_t* meta = a.dd_meta;
+    if (meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) {
+      meta[0] ^= 1;
+      meta[1] = 0;
+      meta[2] = 1;
+    } else {
+      meta[2] = 0;
+    }
   }
 }
 
@@ -1311,8 +1398,10 @@ __global__ __launch_bounds__(BLK) void k_store_filter(const uint8_t* __restrict_
 //   (payload start in the batch, payload end, status | src_rank << 8, offset of its copy)
 // and the payload bytes are copied into a compact buffer, so only those bytes cross PCIe and the
 // host parses them sequentially (csrc/native/swroute.cpp), never the scattered raw batch.
-// out = u32[4] device counters: out[0] = refs (may exceed cap), out[1] = bytes used (may exceed
-// bytes_cap: such refs carry copy offset ~0 and the host reads the raw record instead).  `refs`
+// out = u32[8] device counters: out[0] = refs (may exceed cap), out[1] = bytes used (may exceed
+// bytes_cap: such refs carry copy offset ~0 and the host reads the raw record instead); out[4..6]
+// are the kernel's own accumulators and done count, which the last workgroup publishes to out[0..1]
+// and zeroes for the next launch (no memset before each snapshot; the allocation starts zeroed).  `refs`
 // (u32[4 * cap]) and `bytes` are usually mapped pinned host memory: written straight over PCIe, no
 // copy call.  Refs are in any order; events decoded on another rank keep start = end = 0.
 __global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_t* __restrict__ rej_idx,
@@ -1320,7 +1409,9 @@ __global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_
                               const uint8_t* __restrict__ raw, const uint32_t* __restrict__ msg_off, int64_t n_msgs,
                               int rank, uint32_t* __restrict__ out, uint32_t* __restrict__ refs, int64_t cap,
                               uint8_t* __restrict__ bytes, int64_t bytes_cap) {
+  __shared__ uint32_t last;
   const uint32_t n = *n_rej_ptr;
+  uint32_t* acc = out + 4;
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const uint32_t i = rej_idx[j];
     const uint8_t st = status[i];
@@ -1337,19 +1428,31 @@ __global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_
       s = msg_off[lo];
       e = msg_off[lo + 1];
       const uint32_t len = e > s ? e - s : 0u;
-      const uint32_t at = atomicAdd(out + 1, len);
+      const uint32_t at = atomicAdd(acc + 1, len);
       if ((int64_t)at + len <= bytes_cap) {
         for (uint32_t b = 0; b < len; ++b) bytes[at + b] = raw[s + b];
         copy = at;
       }
     }
-    const uint32_t k = atomicAdd(out, 1u);
+    const uint32_t k = atomicAdd(acc, 1u);
     if (k < cap) {
       refs[4 * k] = s;
       refs[4 * k + 1] = e;
       refs[4 * k + 2] = (uint32_t)st | ((uint32_t)r.src_rank << 8);
       refs[4 * k + 3] = copy;
     }
+  }
+  // last workgroup out: publish the counters (device-scope atomics, visible without a release fence)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(acc + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    out[0] = __hip_atomic_load(acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[1] = __hip_atomic_load(acc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int w = 0; w < 3; ++w) __hip_atomic_store(acc + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1358,9 +1461,10 @@ extern "C" {
 int sw_reject_refs(const SwEngineArgs* ap, const uint8_t* raw, const uint32_t* msg_off, int64_t n_msgs, uint32_t* out,
                    uint32_t* refs, int64_t cap, uint8_t* bytes, int64_t bytes_cap, hipStream_t s) {
   const SwEngineArgs a = *ap;
-  hipError_t e = hipMemsetAsync(out, 0, 16, s);
-  if (e != hipSuccess) return (int)e;
-  k_reject_refs<<<grid_for(a.rec_cap), BLK, 0, s>>>(a.work, a.rej_idx, a.n_rej, a.status, raw, msg_off, n_msgs,
+  // rejects are a small share of a step: a small grid keeps the last-workgroup count (one atomic
+  // per workgroup on one word) off the critical path
+  const int g = grid_for(a.rec_cap) < 256 ? grid_for(a.rec_cap) : 256;
+  k_reject_refs<<<g, BLK, 0, s>>>(a.work, a.rej_idx, a.n_rej, a.status, raw, msg_off, n_msgs,
                                                     (int)a.rank, out, refs, cap, bytes, bytes_cap);
   return (int)hipGetLastError();
 }
@@ -1394,7 +1498,6 @@ int sw_frame_varint(const uint8_t* lens, int64_t nbytes, int64_t n_msgs, uint32_
   uint32_t* tcnt = tmp;
   uint32_t* tlen = tmp + nt;
   k_vlen_tiles<<<(unsigned)nt, BLK, 0, s>>>(lens, nbytes, tcnt, tlen);
-  k_vlen_sums<<<1, BLK, 0, s>>>(tcnt, tlen, nt, msg_off, n_msgs, raw_bytes);
   k_vlen_apply<<<(unsigned)nt, BLK, 0, s>>>(lens, nbytes, tcnt, tlen, msg_off, n_msgs, raw_bytes);
   return (int)hipGetLastError();
 }
@@ -1402,16 +1505,15 @@ int sw_frame_varint(const uint8_t* lens, int64_t nbytes, int64_t n_msgs, uint32_
 // Phase A: decode the raw batch into records (+ new-name capture).  msg counts are host-known.
 int sw_phase_decode(const SwEngineArgs* ap, hipStream_t s) {
   const SwEngineArgs a = *ap;
-  k_decode_begin<<<1, 64, 0, s>>>(a);
   if (a.n_msgs <= 0) {
+    k_decode_begin<<<1, 64, 0, s>>>(a);
     (void)hipMemsetAsync(a.n_recs, 0, sizeof(uint32_t), s);
     return (int)hipGetLastError();
   }
   const unsigned nb = (unsigned)((a.n_msgs + BLK - 1) / BLK);
-  k_decode_count<<<nb, BLK, 0, s>>>(a.raw, a.msg_off, a.n_msgs, a.msg_cnt, a.msg_evoff);
-  k_scan_sums<<<1, BLK, 0, s>>>(a.msg_evoff, (int64_t)nb, a.n_recs);
+  k_decode_count<<<nb, BLK, 0, s>>>(a.raw, a.msg_off, a.n_msgs, a.msg_cnt, a.msg_evoff, a);   // + phase resets
   k_decode_emit<<<nb, BLK, 0, s>>>(a);
-  if (a.world > 1) k_decode_end<<<1, 64, 0, s>>>(a);     // world == 1: k_process_begin does it
+  if (a.world > 1) k_decode_end<<<1, 64, 0, s>>>(a);     // world == 1: k_lookup does it
   return (int)hipGetLastError();
 }
 
@@ -1423,14 +1525,14 @@ int sw_phase_partition(const SwEngineArgs* ap, hipStream_t s) {
       a.carry == a.spill)
     return -3;
   k_part_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.carry, a.n_carry, a.recs, a.n_recs, (int)a.world, (int)a.rank,
-                                                a.part_tmp, ntiles);
+                                                a.part_tmp, ntiles, a.send_str ? a.send_str_cnt : nullptr);
   // scan the flat [world][ntiles] count matrix in place
   int rc = launch_scan(a.part_tmp, ntiles * a.world, a.part_tmp + ntiles * a.world, nullptr, a.scan_tmp,
                        a.scan_tmp_len, s);
   if (rc) return rc;
   const uint32_t* toff = a.part_tmp + ntiles * a.world;
   k_part_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.carry, a.n_carry, a.recs, a.n_recs, (int)a.world, (int)a.rank, toff,
-                                                a.part_tmp, ntiles, a.send, a.shuf_cap, a.spill, a.carry_cap);
+                                                a.part_tmp, ntiles, a.send, a.shuf_cap, a.spill, a.carry_cap, a);
   k_part_counts<<<1, 64, 0, s>>>(toff, a.part_tmp, ntiles, (int)a.world, a.shuf_cap, a.send_cnt, a.n_spill,
                                  a.carry_cap, a.overflow, (ull*)a.stats);
   return (int)hipGetLastError();
@@ -1439,8 +1541,9 @@ int sw_phase_partition(const SwEngineArgs* ap, hipStream_t s) {
 // Phase C (world > 1): concatenate received slabs into the work batch.
 int sw_phase_unpack(const SwEngineArgs* ap, hipStream_t s) {
   const SwEngineArgs a = *ap;
+  if (a.work_str && (a.str_cap & 15)) return -5;      // 16-byte slab copies
   k_unpack<<<grid_for(a.rec_cap), BLK, 0, s>>>(a.recv, a.recv_cnt, (int)a.world, a.shuf_cap, a.work, a.n_work,
-                                               a.rec_cap);
+                                               a.rec_cap, a);
   return (int)hipGetLastError();
 }
 
@@ -1450,23 +1553,21 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int g = grid_for(a.rec_cap);
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
   if (2 * ntiles > a.scan_tmp_len) return -4;
-  k_process_begin<<<1, 64, 0, s>>>(a);
-  k_lookup<<<g, BLK, 0, s>>>(a);
-  k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, (ull*)a.dd_seq, a.dd_mask, a.seq_base,
-                                   a.dd_meta, (ull*)a.stats);
-  k_dedup_check<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (const ull*)a.dd_key, (const ull*)a.dd_seq, a.dd_mask,
-                                  a.seq_base, a.dd_meta, (const ull*)a.dd_bloom, a.dd_bloom_mask);
-  // stable split ok / rejected
-  k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats);
-  uint32_t* cmp_off = a.cmp_tmp + 2 * ntiles;
-  int rc = launch_scan(a.cmp_tmp, 2 * ntiles, cmp_off, nullptr, a.scan_tmp, a.scan_tmp_len, s);
-  if (rc) return rc;
-  k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, cmp_off, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx,
-                                               a.n_ok, a.n_rej);
+  k_lookup<<<g, BLK, 0, s>>>(a);         // + the phase's resets (block 0)
+  k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
+                                   (ull*)a.stats);
+  // stable split ok / rejected, with the dedup verdicts
+  k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
+                                               (const ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
+                                               (const ull*)a.dd_bloom, a.dd_bloom_mask);
+  k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx, a.n_ok,
+                                               a.n_rej);
+  int rc = 0;
   // persist + enrich + state for the validated events
-  k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap, a.spans);
-  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap);
-  k_advance<<<1, 64, 0, s>>>(a.store_cursor, a.n_ok);
+  // string refs of the work batch: the decoder's (one rank) or the exchange's (rebased into work_str)
+  const SwStrRef* wsp = a.world > 1 ? a.work_spans : a.spans;
+  k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap, wsp, nullptr);
+  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap, nullptr);
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
   if (a.n_tests > 0) {
@@ -1475,9 +1576,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
     uint32_t* ztile = a.ztile;
     const size_t vtx_bytes = zone_vtx_in_lds(a) ? (size_t)a.n_zone_vtx * 2 * sizeof(double) : 0;
     k_zone_mask<<<(unsigned)otiles, BLK, vtx_bytes, s>>>(a, zmask, ztile);
-    rc = launch_scan(ztile, otiles, ztile + otiles, a.n_gen, a.scan_tmp, a.scan_tmp_len, s);
-    if (rc) return rc;
-    k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile + otiles, n_rule);
+    k_zone_emit<<<(unsigned)otiles, BLK, 0, s>>>(a, zmask, ztile, n_rule);
   } else {
     k_gen_clamp<<<1, 64, 0, s>>>(a, n_rule);        // no zone tests: n_rule = n_gen = 0
   }
@@ -1486,8 +1585,9 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int gg = grid_for(a.gen_cap);
   const uint32_t gcap = (uint32_t)a.gen_cap;
   k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, gcap);
-  k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap, nullptr);
-  k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen, gcap);
+  // generated events persist after the step's device events (store cursor + n_ok)
+  k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap, nullptr, a.n_ok);
+  k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen, gcap, a.n_ok);
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
 }

@@ -41,9 +41,17 @@ struct SwSegArgs {
   const int64_t* cursor;       // [store_cursor, step_cursor0]: rows = cursor[0] - cursor[1]
   uint8_t* out;                // block (device)
   int64_t out_cap;
-  uint64_t* state;             // [max_pages] look-back words, then ticket, bytes, errors (zeroed per call)
+  uint64_t* state;             // [max_pages + SEG_ST_WORDS]: look-back words, ticket, outputs, accumulators
   int64_t max_pages;
   uint64_t* stamps;            // profiling: [page * 16 + phase] s_memrealtime stamps (null: off)
+  // end-of-step snapshot into mapped host memory, written by the last workgroup (what
+  // k_step_snapshot does in its own dispatch; null host: none): the step's u32 scalars -> host[0..15],
+  // this block's (bytes, errors, first sequence) -> host[16..21], the re-key carry counts ->
+  // host[22..23], the reject-ref counters -> host[24..25]
+  const uint32_t* snap_scalars;
+  const uint32_t* snap_rej;
+  const uint32_t* snap_carry;
+  uint32_t* snap_host;
 };
 
 // phase stamps of a page (profiling builds of the caller only: a null pointer costs a branch)
@@ -284,11 +292,25 @@ __device__ __forceinline__ void block_finish(SegLds& L, int ns, uint64_t maxmask
   __syncthreads();
 }
 
-__global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
-  __shared__ SegLds L;
+// state = u64[max_pages + 8]: [0, max_pages) look-back words; then
+//   +0 ticket, +1 block bytes (out), +2 errors (out), +3 first store sequence (out),
+//   +4 bytes accumulator, +5 errors accumulator, +6 blocks done.
+// The workgroup that finishes last publishes the accumulators to the outputs and zeroes every
+// word the next launch relies on (look-back words, ticket, accumulators, done): no memset node
+// before each encode.  The allocation starts zeroed.
+#define SEG_ST_TICKET 0
+#define SEG_ST_BYTES 1
+#define SEG_ST_ERRORS 2
+#define SEG_ST_FIRST 3
+#define SEG_ST_BYTES_ACC 4
+#define SEG_ST_ERRORS_ACC 5
+#define SEG_ST_DONE 6
+#define SEG_ST_WORDS 8
+
+__device__ __forceinline__ void seg_encode_page(const SwSegArgs& a, SegLds& L) {
   uint64_t* ticket = a.state + a.max_pages;
-  uint64_t* bytes_out = ticket + 1;
-  uint64_t* errors = ticket + 2;
+  uint64_t* bytes_out = ticket + SEG_ST_BYTES_ACC;
+  uint64_t* errors = ticket + SEG_ST_ERRORS_ACC;
   if (threadIdx.x == 0) L.page = (uint32_t)atomicAdd((ull*)ticket, 1ull);
   __syncthreads();
   const uint32_t page = L.page;
@@ -301,7 +323,7 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
     return;
   }
   uint32_t* page_off = reinterpret_cast<uint32_t*>(a.out + 64);
-  if (page == 0 && threadIdx.x == 0) ticket[3] = (uint64_t)c0;     // first store sequence, for the host
+  if (page == 0 && threadIdx.x == 0) ticket[SEG_ST_FIRST] = (uint64_t)c0;   // first store sequence, for the host
   if (n <= 0) {
     if (page == 0 && threadIdx.x == 0) {
       SwSegBlockHdr* h = reinterpret_cast<SwSegBlockHdr*>(a.out);
@@ -886,24 +908,89 @@ __global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
   SEG_STAMP(10);
 }
 
+__global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
+  __shared__ SegLds L;
+  seg_encode_page(a, L);
+  // ---- last workgroup out: publish the results, re-arm the state for the next launch.  Every
+  // word the epilogue reads was written by a device-scope atomic (ticket, accumulators) or an
+  // agent-scope store (look-back words), so no release fence is needed before the count.
+  uint64_t* st = a.state + a.max_pages;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    L.page = (uint32_t)(__hip_atomic_fetch_add((ull*)&st[SEG_ST_DONE], 1ull, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) == (ull)gridDim.x - 1);
+  __syncthreads();
+  if (!L.page) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (threadIdx.x == 0) {
+    const ull bytes = lb_load(&st[SEG_ST_BYTES_ACC]), errors = lb_load(&st[SEG_ST_ERRORS_ACC]);
+    st[SEG_ST_BYTES] = bytes;
+    st[SEG_ST_ERRORS] = errors;
+    if (a.snap_host) {
+      const ull first = lb_load(&st[SEG_ST_FIRST]);
+      a.snap_host[16] = (uint32_t)bytes; a.snap_host[17] = (uint32_t)(bytes >> 32);
+      a.snap_host[18] = (uint32_t)errors; a.snap_host[19] = (uint32_t)(errors >> 32);
+      a.snap_host[20] = (uint32_t)first; a.snap_host[21] = (uint32_t)(first >> 32);
+    }
+    lb_store(&st[SEG_ST_TICKET], 0);
+    lb_store(&st[SEG_ST_BYTES_ACC], 0);
+    lb_store(&st[SEG_ST_ERRORS_ACC], 0);
+    lb_store(&st[SEG_ST_DONE], 0);
+  }
+  for (int64_t i = threadIdx.x; i < a.max_pages; i += SBLK) lb_store(&a.state[i], 0);
+  if (a.snap_host) {
+    const uint32_t t = threadIdx.x;
+    if (t < 16) a.snap_host[t] = a.snap_scalars[t];
+    else if (t == 22 || t == 23) a.snap_host[t] = a.snap_carry ? a.snap_carry[t - 22] : 0u;
+    else if (t == 24 || t == 25) a.snap_host[t] = a.snap_rej ? a.snap_rej[t - 24] : 0u;
+  }
+}
+
 extern "C" {
 
-// Encode this step's rows into `out`.  state = u64[max_pages + 4], zeroed here (a memset node when
-// captured); afterwards state[max_pages + 1] = block bytes (~0 on error), state[max_pages + 2] = errors,
-// state[max_pages + 3] = the store sequence of the block's first row.
+// Encode this step's rows into `out`.  state = u64[max_pages + 8], zeroed when allocated and re-armed
+// by the kernel itself; afterwards state[max_pages + 1] = block bytes (~0 on error),
+// state[max_pages + 2] = errors, state[max_pages + 3] = the store sequence of the block's first row.
 int sw_seg_encode_stamped(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
                           int64_t out_cap, uint64_t* state, int64_t max_pages, uint64_t* stamps, hipStream_t s);
+
+static int seg_encode_launch(const SwSegArgs& a, hipStream_t s) {
+  const unsigned grid = (unsigned)(a.max_pages > 0 ? a.max_pages : 1);
+  k_seg_encode<<<grid, SBLK, 0, s>>>(a);
+  return (int)hipGetLastError();
+}
 
 int sw_seg_encode(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
                   int64_t out_cap, uint64_t* state, int64_t max_pages, hipStream_t s) {
   return sw_seg_encode_stamped(rows, aux, raw, cursor, out, out_cap, state, max_pages, nullptr, s);
 }
 
+// Encode + the end-of-step snapshot in the same dispatch (see SwSegArgs.snap_*): the engine's
+// per-step path when it writes a durable block.
+int sw_seg_encode_snap(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
+                       int64_t out_cap, uint64_t* state, int64_t max_pages, const uint32_t* scalars,
+                       const uint32_t* rej_cnt, const uint32_t* n_carry, uint32_t* host, hipStream_t s) {
+  SwSegArgs a;
+  a.rows = (const SwOutRec*)rows;
+  a.aux = (const SwSegAux*)aux;
+  a.raw = raw;
+  a.cursor = cursor;
+  a.out = out;
+  a.out_cap = out_cap;
+  a.state = state;
+  a.max_pages = max_pages;
+  a.stamps = nullptr;
+  a.snap_scalars = scalars;
+  a.snap_rej = rej_cnt;
+  a.snap_carry = n_carry;
+  a.snap_host = host;
+  return seg_encode_launch(a, s);
+}
+
 // Same, recording 16 phase stamps per page (s_memrealtime, 100 MHz) into stamps[max_pages * 16].
 int sw_seg_encode_stamped(const void* rows, const void* aux, const uint8_t* raw, const int64_t* cursor, uint8_t* out,
                           int64_t out_cap, uint64_t* state, int64_t max_pages, uint64_t* stamps, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(state, 0, sizeof(uint64_t) * (size_t)(max_pages + 4), s);
-  if (e != hipSuccess) return (int)e;
   SwSegArgs a;
   a.rows = (const SwOutRec*)rows;
   a.aux = (const SwSegAux*)aux;
@@ -914,9 +1001,11 @@ int sw_seg_encode_stamped(const void* rows, const void* aux, const uint8_t* raw,
   a.state = state;
   a.max_pages = max_pages;
   a.stamps = stamps;
-  const unsigned grid = (unsigned)(max_pages > 0 ? max_pages : 1);
-  k_seg_encode<<<grid, SBLK, 0, s>>>(a);
-  return (int)hipGetLastError();
+  a.snap_scalars = nullptr;
+  a.snap_rej = nullptr;
+  a.snap_carry = nullptr;
+  a.snap_host = nullptr;
+  return seg_encode_launch(a, s);
 }
 
 // Encoder aux of a step's rows from its records, for callers outside the engine (the engine's

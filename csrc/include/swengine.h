@@ -112,8 +112,8 @@ typedef struct SwEngineArgs {
   const uint8_t* asg_active;
   int64_t n_asg;
   // ---------------------------------------------------------------- dedup window
-  uint64_t* dd_key;
-  int64_t* dd_seq;
+  uint64_t* dd_key;            // packed 16-byte slots {key, first sequence}, two generations of dd_mask + 1
+  int64_t* dd_seq;             // unused by the MI355X engine (host engines keep split tables)
   int64_t dd_mask;
   int64_t* seq_base;           // device scalar: events seen so far on this rank
   // ---------------------------------------------------------------- names intern (state-map keys)
@@ -191,8 +191,24 @@ typedef struct SwEngineArgs {
   // ---------------------------------------------------------------- string refs
   SwStrRef* spans;             // [rec_cap] per decoded record (decode writes, the block encoder reads)
   // ---------------------------------------------------------------- store-backed dedup filter
-  uint64_t* dd_bloom;          // [8 * (dd_bloom_mask + 1)] blocked Bloom filter (null: off)
-  int64_t dd_bloom_mask;       // 512-bit blocks - 1
+  uint64_t* dd_bloom;          // [dd_bloom_mask + 1] blocked Bloom filter, 64-bit blocks (null: off)
+  int64_t dd_bloom_mask;       // blocks - 1
+  // ---------------------------------------------------------------- string exchange (world > 1)
+  // A record's strings (alternate id, metadata, alert message) live in the raw batch of the rank
+  // that decoded it.  The partition copies them into per-destination byte slabs beside the record
+  // slabs (string refs rewritten to slab offsets), the all-to-all moves them with the records, and
+  // the unpack gathers them into work_str ([world][str_cap], the encoder's string source) with the
+  // refs rebased (+ source rank * str_cap).  Null send_str: strings stay on the decoding rank.
+  uint8_t* send_str;           // [world][str_cap] (this partition's parity)
+  uint32_t* send_str_cnt;      // [world] bytes used per destination (zeroed by k_part_count)
+  SwStrRef* send_spans;        // [world][shuf_cap] string refs beside the send slabs
+  const uint8_t* recv_str;     // [world][str_cap]
+  const uint32_t* recv_str_cnt;
+  const SwStrRef* recv_spans;  // [world][shuf_cap]
+  uint8_t* work_str;           // [world][str_cap] gathered by k_unpack
+  SwStrRef* work_spans;        // [rec_cap] refs of the work batch (rebased into work_str)
+  int64_t str_cap;             // bytes per destination slab
+  uint32_t* str_drops;         // [2] records whose strings did not fit / came from the carry
 } SwEngineArgs;
 
 #define SW_N_STATS 24

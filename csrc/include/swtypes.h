@@ -194,18 +194,18 @@ SW_HD uint64_t sw_mix64(uint64_t x) {
   return x;
 }
 
-// Store-backed alternate-id filter: a blocked Bloom filter (512-bit blocks, 7 bits per id) of every
+// Store-backed alternate-id filter: a blocked Bloom filter (64-bit blocks, 8 bits per id) of every
 // id the engine persisted.  An id new to the dedup window that the filter may hold is handed to the
 // host (SW_ST_RECHECK), which checks it against the event store -- dedup beyond the window without a
-// per-event store lookup on the hot path.  Same functions in every engine (bit-exact).
+// per-event store lookup on the hot path.  One word per id: one 8-byte load to probe, ONE atomic OR
+// to add (memory-side atomics are the MI355X's scarce resource here: each is its own 64-byte
+// request).  Same functions in every engine (bit-exact).
 SW_HD uint64_t sw_bloom_block(uint64_t h, int64_t mask) { return sw_mix64(h ^ 0x5bd1e9955bd1e995ULL) & (uint64_t)mask; }
-SW_HD void sw_bloom_bits(uint64_t h, uint64_t m[8]) {
+SW_HD uint64_t sw_bloom_bits(uint64_t h) {
   const uint64_t g = sw_mix64(h + 0x9E3779B97F4A7C15ULL);
-  for (int w = 0; w < 8; ++w) m[w] = 0;
-  for (int j = 0; j < 7; ++j) {
-    const uint32_t b = (uint32_t)(g >> (9 * j)) & 511u;
-    m[b >> 6] |= 1ull << (b & 63);
-  }
+  uint64_t m = 0;
+  for (int j = 0; j < 8; ++j) m |= 1ull << ((g >> (6 * j)) & 63u);
+  return m;
 }
 
 // 128-bit fingerprint of a byte string: FNV-1a-64 and an independent odd-multiplier

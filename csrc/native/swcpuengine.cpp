@@ -303,20 +303,12 @@ static inline int32_t nid_of(const SwCpuEngine* e, uint64_t h) {
 }
 
 static inline bool bloom_has(const SwCpuEngine* e, uint64_t h) {
-  uint64_t m[8];
-  sw_bloom_bits(h, m);
-  const uint64_t* b = e->bloom.data() + 8 * sw_bloom_block(h, e->bloom_mask);
-  for (int w = 0; w < 8; ++w)
-    if ((b[w] & m[w]) != m[w]) return false;
-  return true;
+  const uint64_t m = sw_bloom_bits(h);
+  return (e->bloom[sw_bloom_block(h, e->bloom_mask)] & m) == m;
 }
 
 static inline void bloom_add(SwCpuEngine* e, uint64_t h) {
-  uint64_t m[8];
-  sw_bloom_bits(h, m);
-  uint64_t* b = e->bloom.data() + 8 * sw_bloom_block(h, e->bloom_mask);
-  for (int w = 0; w < 8; ++w)
-    if (m[w]) __atomic_fetch_or(&b[w], m[w], __ATOMIC_RELAXED);
+  __atomic_fetch_or(&e->bloom[sw_bloom_block(h, e->bloom_mask)], sw_bloom_bits(h), __ATOMIC_RELAXED);
 }
 
 static inline bool pip(const double* v, int32_t n, double x, double y) {
@@ -752,11 +744,11 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   return 0;
 }
 
-// Store-backed dedup filter: `bits` (a multiple of 512, 0 = off); cleared.
+// Store-backed dedup filter: `bits` (a power of two >= 64, 0 = off); cleared.
 void swce_bloom_init(void* p, int64_t bits) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  const int64_t blocks = bits / 512;
-  e->bloom.assign(blocks > 0 ? (size_t)blocks * 8 : 0, 0ull);
+  const int64_t blocks = bits / 64;
+  e->bloom.assign(blocks > 0 ? (size_t)blocks : 0, 0ull);
   e->bloom_mask = blocks > 0 ? blocks - 1 : 0;
 }
 

@@ -50,7 +50,7 @@ def main():
     cap = max_block_bytes(n, max_string_bytes(n, len(raw)))
     pages = -(-n // PAGE_ROWS)
     blk = torch.zeros(cap, dtype=torch.uint8, device=d)
-    state = torch.zeros(pages + 4, dtype=torch.int64, device=d)
+    state = torch.zeros(pages + 8, dtype=torch.int64, device=d)
     aux = torch.zeros(n * 32, dtype=torch.uint8, device=d)
     s = torch.cuda.current_stream(d)
     P = ctypes.c_void_p

@@ -287,6 +287,7 @@ def gpu():
         _proto(lib, "sw_sdma_wait", c_int32, c_uint64)
         _proto(lib, "sw_seg_encode", c_int32, P, P, P, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_seg_encode_stamped", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P)
+        _proto(lib, "sw_seg_encode_snap", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P, P, P, P)
         _proto(lib, "sw_seg_aux", c_int32, P, P, P, P, P, c_int64, P, P, c_int64, P)
         _proto(lib, "sw_bloom_add", c_int32, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)

@@ -62,6 +62,9 @@ FIELDS = [
     # store-backed dedup filter (blocked Bloom filter, null = off)
     ("dd_bloom", P),
     ("dd_bloom_mask", I),
+    # string exchange (world > 1): per-destination byte slabs + refs beside the record slabs
+    ("send_str", P), ("send_str_cnt", P), ("send_spans", P), ("recv_str", P), ("recv_str_cnt", P),
+    ("recv_spans", P), ("work_str", P), ("work_spans", P), ("str_cap", I), ("str_drops", P),
 ]
 
 

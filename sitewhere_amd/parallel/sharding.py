@@ -119,11 +119,15 @@ def init_distributed(use_gpu: bool = True):
     return rank, local, world, device
 
 
-def exchange_slabs(send_cnt, recv_cnt, send, recv, group=None):
-    """The re-key collective: counts, then the fixed-size slabs (both stream-ordered, no host sync)."""
+def exchange_slabs(send_cnt, recv_cnt, send, recv, group=None, extra=()):
+    """The re-key collective: counts, then the fixed-size slabs (all stream-ordered, no host sync).
+    ``extra``: more (send, recv) pairs split evenly over the ranks the same way -- the string
+    exchange's byte counts, refs and byte slabs."""
     import torch.distributed as dist
     dist.all_to_all_single(recv_cnt, send_cnt, group=group)
     dist.all_to_all_single(recv, send, group=group)
+    for s, r in extra:
+        dist.all_to_all_single(r, s, group=group)
 
 
 def exchange_bytes_per_rank(rec_cap: int, world: int, slack: float = 1.1, rec_bytes: int = 64, pad: int = 1024) -> int:

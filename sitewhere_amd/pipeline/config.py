@@ -22,7 +22,8 @@ class EngineConfig:
     store_cap: int = 1 << 27         # HBM event-store ring capacity (events)
     dedup_slots: int = 1 << 22       # alternate-id window (slots; window = slots / 2)
     # store-backed dedup beyond the window: a blocked Bloom filter of every persisted alternate id
-    # (bits; a multiple of 512; 0 = off).  ~32 bits per id kept -> ~1e-4 of new ids rechecked on the host
+    # (bits, rounded up to a power of two; 0 = off).  32 bits per id kept -> ~5e-5 of new ids
+    # rechecked on the host, 64 bits per id -> ~1e-6
     dedup_bloom_bits: int = 0
     name_slots: int = 1 << 16        # distinct measurement names / alert types
     state_slots: int = 0             # (assignment, name) state map slots (0 = 16 * max_assignments)
@@ -31,6 +32,9 @@ class EngineConfig:
     shuffle_pad: int = 1024          # records added to every slab (small-batch headroom)
     carry_cap: int = 0               # records full slabs can defer to the next exchange (0 = 3 * rec_cap)
     carry_high: int = 0              # drivers stall new input while the carry exceeds this (0 = rec_cap)
+    # world > 1: string bytes (alternate id + metadata + alert message) exchanged per record slot of
+    # a re-key slab; the owner rank stores them losslessly (0 = strings stay on the decoding rank)
+    str_bytes: int = 40
     presence_missing_ms: int = 8 * 3600 * 1000   # DevicePresenceManager default (8h)
     presence_check_ms: int = 10 * 60 * 1000      # DevicePresenceManager default (10 min)
     rank: int = 0
@@ -52,6 +56,8 @@ class EngineConfig:
         self.state_slots = pow2_at_least(self.state_slots)
         self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + self.shuffle_pad
         local = self.rec_cap
+        # per-destination string slab, 16-byte multiple (the unpack gathers it 16 B at a time)
+        self.str_cap = (self.shuf_cap * self.str_bytes + 15) // 16 * 16 if self.world > 1 and self.str_bytes > 0 else 0
         if self.world > 1:
             # a rank can receive a full slab from every rank: the work batch after the exchange
             # must hold world * shuf_cap records (skewed keys), or the surplus would be cut

@@ -65,8 +65,8 @@ class CpuInboundEngine(EngineBase):
         self.dedup: dict[int, int] = {}          # current generation of the alternate-id window
         self.dedup_prev: dict[int, int] = {}     # previous generation
         # store-backed dedup filter (blocked Bloom filter of every persisted alternate id; sw_bloom_*)
-        nb = cfg.dedup_bloom_bits // 512
-        self.bloom = np.zeros(8 * nb, np.uint64) if nb else None
+        nb = cfg.dedup_bloom_bits // 64
+        self.bloom = np.zeros(nb, np.uint64) if nb else None
         self.bloom_mask = nb - 1
         self.intern: dict[int, int] = {}
         self.st_last = np.zeros(cfg.max_assignments, np.uint64)
@@ -180,15 +180,14 @@ class CpuInboundEngine(EngineBase):
     def _bloom_pos(self, h: int):
         blk = mix64(h ^ 0x5bd1e9955bd1e995) & self.bloom_mask
         g = mix64((h + 0x9E3779B97F4A7C15) & _M64)
-        m = [0] * 8
-        for j in range(7):
-            b = (g >> (9 * j)) & 511
-            m[b >> 6] |= 1 << (b & 63)
-        return 8 * blk, m
+        m = 0
+        for j in range(8):
+            m |= 1 << ((g >> (6 * j)) & 63)
+        return blk, m
 
     def _bloom_has(self, h: int) -> bool:
-        base, m = self._bloom_pos(h)
-        return all((int(self.bloom[base + w]) & m[w]) == m[w] for w in range(8))
+        w, m = self._bloom_pos(h)
+        return (int(self.bloom[w]) & m) == m
 
     def bloom_add(self, hashes):
         """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
@@ -196,10 +195,8 @@ class CpuInboundEngine(EngineBase):
             return
         for h in np.asarray(hashes, np.uint64).tolist():
             if h:
-                base, m = self._bloom_pos(int(h))
-                for w in range(8):
-                    if m[w]:
-                        self.bloom[base + w] |= np.uint64(m[w])
+                w, m = self._bloom_pos(int(h))
+                self.bloom[w] |= np.uint64(m)
 
     def _intern_id(self, h: int) -> int:
         if h not in self.intern:

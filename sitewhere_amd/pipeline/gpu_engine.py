@@ -151,6 +151,19 @@ class GpuInboundEngine(EngineBase):
             t["work"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
             self.carry_bufs = [z(c.carry_cap * EVENT_REC.itemsize, u8) for _ in range(2)]
             t["n_carry"] = z(2, i32)
+            if c.str_cap:
+                # string exchange: byte slabs + refs beside the record slabs (double-buffered the same
+                # way), gathered into work_str by the unpack (see SwEngineArgs)
+                sr = STR_REF.itemsize
+                self.send_strs = [z(c.world * c.str_cap, u8) for _ in range(2)]
+                self.send_str_cnts = [z(c.world, i32) for _ in range(2)]
+                self.send_spans = [z(c.world * c.shuf_cap * sr, u8) for _ in range(2)]
+                t["recv_str"] = z(c.world * c.str_cap, u8)
+                t["recv_str_cnt"] = z(c.world, i32)
+                t["recv_spans"] = z(c.world * c.shuf_cap * sr, u8)
+                t["work_str"] = z(c.world * c.str_cap + 64, u8)
+                t["work_spans"] = z(c.rec_cap * sr, u8)
+        t["str_drops"] = z(2, i32)
         # validated
         t["status"] = z(c.rec_cap, u8)
         t["ev_dev"] = z(c.rec_cap, i32)
@@ -163,12 +176,13 @@ class GpuInboundEngine(EngineBase):
         t["asg_ctx"] = full(c.max_assignments * 4, -1, i32)
         t["asg_active"] = z(c.max_assignments, u8)
         # dedup window
-        t["dd_key"] = z(2 * c.dedup_slots, i64)            # two generations (see k_dedup_rotate)
+        # two generations (see k_dedup_rotate) of packed 16-byte slots {alternate-id hash, first sequence}
+        t["dd_tab"] = z(4 * c.dedup_slots, i64).view(2 * c.dedup_slots, 2)
+        t["dd_tab"][:, 1] = -1
         # store-backed dedup filter: blocked Bloom filter of every persisted alternate id (sw_bloom_*)
-        self._bloom_blocks = c.dedup_bloom_bits // 512
-        t["dd_bloom"] = z(8 * max(1, self._bloom_blocks), i64)
-        t["dd_seq"] = full(2 * c.dedup_slots, -1, i64)
-        t["dd_meta"] = z(4, i64)
+        self._bloom_blocks = c.dedup_bloom_bits // 64          # one 64-bit word per block
+        t["dd_bloom"] = z(max(1, self._bloom_blocks), i64)
+        t["dd_meta"] = torch.from_numpy(self._armed_dedup_meta(np.zeros(4, np.int64), c)).to(d)
         t["seq_base"] = z(1, i64)
         # names intern
         t["nm_key"] = z(c.name_slots, i64)
@@ -217,18 +231,22 @@ class GpuInboundEngine(EngineBase):
         a.overflow = S(2)
         if c.world > 1:
             a.recv, a.shuf_cap, a.recv_cnt = _ptr(t["recv"]), c.shuf_cap, _ptr(t["recv_cnt"])
+            if c.str_cap:
+                a.recv_str, a.recv_str_cnt, a.recv_spans = _ptr(t["recv_str"]), _ptr(t["recv_str_cnt"]), _ptr(t["recv_spans"])
+                a.work_str, a.work_spans, a.str_cap = _ptr(t["work_str"]), _ptr(t["work_spans"]), c.str_cap
             a.part_tmp, a.part_tmp_len = _ptr(t["part_tmp"]), t["part_tmp"].numel() // 2
             a.work = _ptr(t["work"])
             a.carry_cap = c.carry_cap
         else:
             a.work = a.recs
+        a.str_drops = _ptr(t["str_drops"])
         a.n_work = S(3)
         a.status, a.ev_dev, a.ev_asg = _ptr(t["status"]), _ptr(t["ev_dev"]), _ptr(t["ev_asg"])
         a.ok_idx, a.n_ok, a.rej_idx, a.n_rej = _ptr(t["ok_idx"]), S(4), _ptr(t["rej_idx"]), S(5)
         a.cmp_tmp = _ptr(t["cmp_tmp"])
         a.reg, a.reg_mask = _ptr(t["reg"]), c.reg_slots - 1
         a.asg_ctx, a.asg_active, a.n_asg = _ptr(t["asg_ctx"]), _ptr(t["asg_active"]), c.max_assignments
-        a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_key"]), _ptr(t["dd_seq"]), c.dedup_slots - 1, _ptr(t["seq_base"])
+        a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_tab"]), 0, c.dedup_slots - 1, _ptr(t["seq_base"])
         a.dd_bloom = _ptr(t["dd_bloom"]) if self._bloom_blocks else 0
         a.dd_bloom_mask = self._bloom_blocks - 1 if self._bloom_blocks else 0
         a.dd_meta = _ptr(t["dd_meta"])
@@ -367,10 +385,10 @@ class GpuInboundEngine(EngineBase):
         self._last_sel = sel
         a.out = _ptr(self.out_dev[sel]) if out_to_device else self.out_host[sel].dev
         # rows kept on the device may be encoded into a durable block: the persist kernel writes each
-        # row's encoder aux beside it (strings only on a single rank: a record decoded on another rank
-        # has its strings in that rank's batch)
+        # row's encoder aux beside it
         aux = _ptr(self._aux_buffer(sel)) if out_to_device else 0
-        raw_bytes = getattr(self, "_raw_bytes", 0) if self.world == 1 else 0
+        # strings: the raw batch on one rank; the exchanged string slabs (work_str) on several
+        raw_bytes = getattr(self, "_raw_bytes", 0) if self.world == 1 else self.world * self.cfg.str_cap
         rc = self.lib.sw_set_step_params(ctypes.c_void_p(a.sp), int(now_ms), a.batch_seq, a.presence_missing_ms,
                                          ctypes.c_void_p(a.out), ctypes.c_void_p(aux), int(raw_bytes), self._stream())
         if rc:
@@ -416,6 +434,9 @@ class GpuInboundEngine(EngineBase):
             a = self.args
             sp, cp = self._send_par, self._carry_par
             a.send, a.send_cnt = _ptr(self.send_bufs[sp]), _ptr(self.send_cnts[sp])
+            if self.cfg.str_cap:
+                a.send_str, a.send_str_cnt = _ptr(self.send_strs[sp]), _ptr(self.send_str_cnts[sp])
+                a.send_spans = _ptr(self.send_spans[sp])
             a.carry, a.n_carry = _ptr(self.carry_bufs[cp]), _ptr(self.t["n_carry"]) + 4 * cp
             a.spill, a.n_spill = _ptr(self.carry_bufs[1 - cp]), _ptr(self.t["n_carry"]) + 4 * (1 - cp)
             rc = self.lib.sw_phase_partition(ap, self._stream())
@@ -428,7 +449,11 @@ class GpuInboundEngine(EngineBase):
         """RCCL all-to-all re-keying of the per-owner slabs (the Kafka key-partitioning analogue)."""
         from ..parallel.sharding import exchange_slabs
         p = self._last_send_par
-        exchange_slabs(self.send_cnts[p], self.t["recv_cnt"], self.send_bufs[p], self.t["recv"], self.group)
+        extra = ()
+        if self.cfg.str_cap:
+            extra = ((self.send_str_cnts[p], self.t["recv_str_cnt"]), (self.send_spans[p], self.t["recv_spans"]),
+                     (self.send_strs[p], self.t["recv_str"]))
+        exchange_slabs(self.send_cnts[p], self.t["recv_cnt"], self.send_bufs[p], self.t["recv"], self.group, extra)
 
     def phase_unpack(self):
         rc = self.lib.sw_phase_unpack(ctypes.byref(self.args), self._stream())
@@ -532,6 +557,27 @@ class GpuInboundEngine(EngineBase):
         n = self.cfg.shuf_cap * WIRE_REC.itemsize
         return self.t["recv"][q * n:(q + 1) * n]
 
+    def loopback_strings(self, peers: list):
+        """Loopback exchange of the string slabs (tests that run every rank's engine in one process):
+        what the all-to-all in :meth:`phase_exchange` moves for them, copied from each peer's last
+        partition into this engine's receive buffers (``peers[r]`` = rank r's engine)."""
+        c = self.cfg
+        if not c.str_cap:
+            return
+        sr = c.shuf_cap * STR_REF.itemsize
+        q = self.rank
+        for r, e in enumerate(peers):
+            p = e._last_send_par
+            self.t["recv_str_cnt"][r] = e.send_str_cnts[p][q]
+            self.t["recv_spans"][r * sr:(r + 1) * sr].copy_(e.send_spans[p][q * sr:(q + 1) * sr])
+            self.t["recv_str"][r * c.str_cap:(r + 1) * c.str_cap].copy_(
+                e.send_strs[p][q * c.str_cap:(q + 1) * c.str_cap])
+
+    def string_drops(self) -> dict:
+        """Records whose strings were not exchanged: slab full / carried from an earlier step."""
+        v = self.t["str_drops"].cpu().numpy()
+        return {"slab_full": int(v[0]), "carried": int(v[1])}
+
     def scalars(self) -> dict:
         v = self.t["scalars"][:9].cpu().numpy()
         return dict(n_recs=int(v[0]), n_new_names=int(v[1]), overflow=int(v[2]), n_work=int(v[3]), n_ok=int(v[4]),
@@ -551,7 +597,7 @@ class GpuInboundEngine(EngineBase):
             return self._with_block(self.collect(sel, raw, from_device=True), sel, now_ms)
 
     def decode_only(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, spans: bool = False):
-        """Run only the decode phase (``k_decode_count`` / ``k_scan_sums`` / ``k_decode_emit``) of a
+        """Run only the decode phase (``k_decode_count`` / ``k_decode_emit``) of a
         host batch and return the decoded ``EVENT_REC`` records in batch order.  A test hook: it
         checks the device decoder against an independent decoder (``tests/decode_oracle.py``)
         without validation rewriting the records.  Names it sees count as seen by later steps.
@@ -966,7 +1012,7 @@ class GpuInboundEngine(EngineBase):
             cap = max_block_bytes(self.out_cap, self.BLOCK_STRING_BYTES_PER_ROW * self.out_cap)
             pages = -(-self.out_cap // PAGE_ROWS)
             s = segs[slot] = (torch.empty(cap, dtype=torch.uint8, device=self.device),
-                              torch.zeros(pages + 4, dtype=torch.int64, device=self.device), pages, cap)
+                              torch.zeros(pages + 8, dtype=torch.int64, device=self.device), pages, cap)
         return s
 
     SEG_AUX_SIZE = 32             # sizeof(SwSegAux), csrc/include/swseg.h
@@ -979,18 +1025,28 @@ class GpuInboundEngine(EngineBase):
             b = bufs[slot] = torch.zeros(self.out_cap * self.SEG_AUX_SIZE, dtype=torch.uint8, device=self.device)
         return b
 
-    def encode_block_async(self, slot: int) -> torch.Tensor:
+    def encode_block_async(self, slot: int, snapshot: tuple | None = None) -> torch.Tensor:
         """Enqueue ``k_seg_encode`` of the step just processed on the current stream: its rows (in
         ``out_dev[slot]``), their encoder aux (written beside them by the persist kernel) and, on a
-        single rank, their strings from the raw batch the step decoded (still in HBM).  Returns the
-        device view (block bytes, encoder errors, first store sequence) the host reads once the step
-        is done.  Multi-rank: records decoded on another rank carry no string refs here (their
-        strings stay in that rank's batch)."""
+        single rank, their strings from the raw batch the step decoded (still in HBM); on several
+        ranks from the string slabs the re-key exchange brought with the records (``work_str``; none
+        with ``str_bytes`` = 0).  Returns the device view (block bytes, encoder errors, first store
+        sequence) the host reads once the step is done.  ``snapshot`` = (scalars, reject counters,
+        carry counts, mapped host snapshot) device pointers: the encoder's last workgroup also writes
+        the end-of-step snapshot (``k_step_snapshot``'s job, no extra dispatch)."""
         dev, state, pages, cap = self._seg_buffers(slot)
         a = self.args
-        strings = self.world == 1
+        src = a.raw if self.world == 1 else (a.work_str or 0)
+        if snapshot is not None:
+            P = ctypes.c_void_p
+            rc = self.lib.sw_seg_encode_snap(P(_ptr(self.out_dev[slot])), P(_ptr(self._aux_buffer(slot))), P(src),
+                                             P(_ptr(self.t["cursor"])), P(_ptr(dev)), cap, P(_ptr(state)), pages,
+                                             *(P(x) for x in snapshot), self._stream())
+            if rc:
+                raise RuntimeError(f"sw_seg_encode_snap failed ({rc})")
+            return state[pages + 1:pages + 4]
         rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(_ptr(self._aux_buffer(slot))),
-                                    ctypes.c_void_p(a.raw if strings else 0), ctypes.c_void_p(_ptr(self.t["cursor"])),
+                                    ctypes.c_void_p(src), ctypes.c_void_p(_ptr(self.t["cursor"])),
                                     ctypes.c_void_p(_ptr(dev)), cap, ctypes.c_void_p(_ptr(state)), pages, self._stream())
         if rc:
             raise RuntimeError(f"sw_seg_encode failed ({rc})")
@@ -1009,7 +1065,7 @@ class GpuInboundEngine(EngineBase):
         bufs = refs.get(slot)
         cap = self.cfg.rec_cap
         if bufs is None:
-            bufs = refs[slot] = (torch.zeros(4, dtype=torch.int32, device=self.device),
+            bufs = refs[slot] = (torch.zeros(8, dtype=torch.int32, device=self.device),     # see k_reject_refs
                                  HostBuffer(self.lib, 16 * cap + self.REJECT_BYTES))
         cnt, hb = bufs
         rc = self.lib.sw_reject_refs(ctypes.byref(self.args), ctypes.c_void_p(_ptr(raw_dev)),
@@ -1172,7 +1228,7 @@ class GpuInboundEngine(EngineBase):
 
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "gpu"
-    _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_key", "dd_seq", "dd_meta", "seq_base", "nm_key", "nm_id", "nm_first",
+    _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_tab", "dd_meta", "seq_base", "nm_key", "nm_id", "nm_first",
                     "nm_counter", "seen_key", "st", "ms", "stats", "cursor")
 
     def bloom_add(self, hashes):
@@ -1206,6 +1262,13 @@ class GpuInboundEngine(EngineBase):
     def restore_state(self, a: dict, include_store: bool):
         self._sync_streams()
         for k in self._ckpt_tables():
+            if k == "dd_tab" and k not in a and "dd_key" in a:
+                # an older checkpoint's split key / sequence tables: {key, win = sequence's low 32
+                # bits, lmin = none}
+                self.t["dd_tab"][:, 0].copy_(torch.from_numpy(a["dd_key"]))
+                sq = np.asarray(a["dd_seq"], np.int64)
+                self.t["dd_tab"][:, 1].copy_(torch.from_numpy((sq & 0xFFFFFFFF) | np.int64(-1 << 32)))
+                continue
             if k not in a:
                 continue
             src = torch.from_numpy(a[k])
@@ -1214,6 +1277,11 @@ class GpuInboundEngine(EngineBase):
                 self.t[k][:src.numel()].copy_(src)
                 continue
             self.t[k].copy_(src)       # in place: captured graphs keep their pointers
+        if "dd_tab" not in a and "dd_meta" in a:
+            # older checkpoints decided the rotation at the start of a step; now the end of the
+            # previous step does (k_step_end): apply that decision to the restored window
+            m = self._armed_dedup_meta(a["dd_meta"].astype(np.int64).copy(), self.cfg)
+            self.t["dd_meta"].copy_(torch.from_numpy(m))
         if self.world > 1 and "carry" in a:
             cp = self._carry_par
             c = torch.from_numpy(a["carry"])
@@ -1225,10 +1293,21 @@ class GpuInboundEngine(EngineBase):
                 v.copy_(torch.from_numpy(a[f"store.{k}"]))
         self._sync_streams()
 
+    @staticmethod
+    def _armed_dedup_meta(m: np.ndarray, cfg) -> np.ndarray:
+        """dd_meta = [generation, ids in the live table, rotate flag, pad] as k_step_end leaves it:
+        with the NEXT step's rotation decided (the live table could pass half load) -- what the
+        first step after an allocation, a reset or an old checkpoint needs."""
+        if m[1] + cfg.rec_cap > cfg.dedup_slots // 2:
+            m[0], m[1], m[2] = m[0] ^ 1, 0, 1
+        else:
+            m[2] = 0
+        return m
+
     def reset_dedup(self):
-        self.t["dd_key"].zero_()
-        self.t["dd_seq"].fill_(-1)
-        self.t["dd_meta"].zero_()
+        self.t["dd_tab"][:, 0] = 0
+        self.t["dd_tab"][:, 1] = -1
+        self.t["dd_meta"].copy_(torch.from_numpy(self._armed_dedup_meta(np.zeros(4, np.int64), self.cfg)))
 
 
 class PipelinedRunner:
@@ -1400,22 +1479,28 @@ class PipelinedRunner:
                 t_sub = self._t("sub_router_wait", t_sub)
                 rej_cnt, _ = self.e.reject_refs_async(b, self.raw[done[0]], self.off[done[0]], done[1])
                 self.rtag[b] = done[2]
+        nc = self.e.t.get("n_carry")
+        self.cpar[b] = getattr(self.e, "_carry_par", 0)
+        snapped = False
         if self.block_sink is not None:
             done_tag = self._prev_tag if self.rounds else tag
             self._prev_tag = tag
             if self.produced[b]:
-                seg_meta = self.e.encode_block_async(b)
+                # the encoder's last workgroup writes the step snapshot too (one dispatch fewer)
+                seg_meta = self.e.encode_block_async(b, snapshot=(
+                    self.e.t["scalars"].data_ptr(), 0 if rej_cnt is None else rej_cnt.data_ptr(),
+                    0 if nc is None else nc.data_ptr(), self.snap[b].dev))
+                snapped = True
                 self.btag[b], self.bnow[b] = done_tag, self.e._step_now
-        nc = self.e.t.get("n_carry")
-        self.cpar[b] = getattr(self.e, "_carry_par", 0)
-        rc = self.e.lib.sw_step_snapshot(ctypes.c_void_p(self.e.t["scalars"].data_ptr()),
-                                         ctypes.c_void_p(0 if seg_meta is None else seg_meta.data_ptr()),
-                                         ctypes.c_void_p(0 if rej_cnt is None else rej_cnt.data_ptr()),
-                                         ctypes.c_void_p(0 if nc is None else nc.data_ptr()),
-                                         int(self.produced[b]), ctypes.c_void_p(self.snap[b].dev),
-                                         ctypes.c_void_p(self.comp.cuda_stream))
-        if rc:
-            raise RuntimeError(f"sw_step_snapshot failed ({rc})")
+        if not snapped:
+            rc = self.e.lib.sw_step_snapshot(ctypes.c_void_p(self.e.t["scalars"].data_ptr()),
+                                             ctypes.c_void_p(0 if seg_meta is None else seg_meta.data_ptr()),
+                                             ctypes.c_void_p(0 if rej_cnt is None else rej_cnt.data_ptr()),
+                                             ctypes.c_void_p(0 if nc is None else nc.data_ptr()),
+                                             int(self.produced[b]), ctypes.c_void_p(self.snap[b].dev),
+                                             ctypes.c_void_p(self.comp.cuda_stream))
+            if rc:
+                raise RuntimeError(f"sw_step_snapshot failed ({rc})")
         self.ev_comp[b].record(self.comp)
         if self.trace is not None:
             self.tev[b][2].record(self.comp)

@@ -50,7 +50,7 @@ def _encode_gpu(rows, recs, spans, raw, c0=0, seed=0):
     bcap = max_block_bytes(max_rows, max_string_bytes(max_rows, len(raw)))
     pages = -(-max_rows // PAGE_ROWS)
     blk = torch.zeros(bcap, dtype=torch.uint8, device=d)
-    state = torch.zeros(pages + 4, dtype=torch.int64, device=d)
+    state = torch.zeros(pages + 8, dtype=torch.int64, device=d)
     s = torch.cuda.current_stream(d)
     P = ctypes.c_void_p
     # encoder aux rows from the records (what the engine's persist kernel writes beside each row)
