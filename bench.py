@@ -204,8 +204,8 @@ def main():
                      with_alternate_id=args.alt_ids, lat0=33.0, lon0=-85.0, span_deg=2.0,
                      p_register=args.p_register, p_ack=args.p_ack, p_meta=args.p_meta)
     cfg = EngineConfig(max_msgs=args.msgs, rec_cap=args.msgs * args.mx_per_msg + 4096,
-                       gen_cap=max(1 << 16, args.msgs // 2), max_devices=int(args.devices * 1.1) + 1024,
-                       max_assignments=int(args.devices * 1.1) + 1024, store_cap=args.store,
+                       gen_cap=max(1 << 16, args.msgs // 2), max_devices=int(n_total_dev * 1.1) + 1024,
+                       max_assignments=int(n_total_dev * 1.1) + 1024, store_cap=args.store,
                        # alternate-id window: 2^24 slots = the last ~8M distinct ids per GPU
                        dedup_slots=1 << 24, name_slots=1 << 12, rank=rank, world=world,
                        # store-backed dedup beyond the window (2^33 bits = 1 GB of HBM: ~32 bits for each
@@ -227,14 +227,14 @@ def main():
         from sitewhere_amd.pipeline.cpu_engine import CpuInboundEngine
         eng = CpuInboundEngine(cfg)
 
-    # ---- registry shard: the devices this rank owns (owner = fp_hi >> 32 mod world)
+    # ---- registry: replicated on every rank (the decoding rank sends a record of a registered,
+    # assigned device to its owner, fp_hi >> 32 mod world, and rejects the rest itself, where the
+    # payload bytes are); the owner keeps the device's state, dedup window and events
     t0 = time.time()
     heap, offs = gen_tokens("dev-", 0, n_total_dev)
     lo, hi = fingerprints(heap, offs)
-    mine = shard_mask(hi, world, rank)
-    lo, hi = lo[mine], hi[mine]
     dev = eng.register_devices(lo, hi)
-    n_dev = len(dev)
+    n_dev = int(shard_mask(hi, world, rank).sum())
     eng.set_assignments(dev, dev, customer=dev % 97, area=dev % 31, asset=dev % 1009)
     rng = np.random.default_rng(1234)
     zones, tests = zone_polys(args.zones, spec.lat0, spec.lon0, spec.span_deg, rng)
@@ -529,7 +529,7 @@ def main():
         "payload_bytes_per_gpu_step": int(max_raw), "setup_s": round(setup_s, 1),
         "h2d_bytes_per_gpu_step": int(max_raw) + int(max(
             (b[4].numel() if b[4] is not None else 4 * len(b[3])) for b in batches)),
-        "registered_devices_rank0": n_dev,
+        "registered_devices_rank0": int(len(dev)), "owned_devices_rank0": n_dev,
         "rejected_rank0": {k: s1[k] - s0[k] for k in ("unregistered", "unassigned", "duplicates", "decode_errors",
                                                        "control")},
         "numa_node": numa_node,

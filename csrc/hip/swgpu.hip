@@ -430,9 +430,22 @@ __global__ void k_decode_end(SwEngineArgs a) {
 
 // ============================================================================ shuffle (owner partition)
 // Stable multi-way partition of records by owner rank into [world][shuf_cap] slabs.
-__device__ __forceinline__ uint32_t owner_of(const SwEventRec& r, uint32_t world) {
-  // Control/error records stay on the rank that received them (the host there owns the raw bytes).
-  return r.etype >= 16 ? 0xffffffffu : sw_owner(r.fp_hi, world);
+// Destination of a record in the re-key.  The registry is replicated on every rank (the
+// reference's near cache does the same for its consumers), so the rank that decoded a record knows
+// whether its device is registered and assigned: such records go to the device's owner; every other
+// record (unknown or unassigned device, control, decode error) stays on the decoding rank, whose raw
+// batch holds the payload bytes the slow path routes (unregistered-device events, registrations).
+__device__ __forceinline__ uint32_t part_dest(const SwEngineArgs& a, const SwEventRec& r, uint32_t world,
+                                              uint32_t rank) {
+  if (r.etype >= 16) return rank;
+  int64_t slot = (int64_t)(r.fp_lo & (ull)a.reg_mask);
+  for (int64_t p = 0; p <= a.reg_mask && p < MAX_PROBE; ++p) {
+    const ulonglong2 k = *reinterpret_cast<const ulonglong2*>(&a.reg[slot].lo);
+    if (k.x == r.fp_lo && k.y == r.fp_hi) return a.reg[slot].asg >= 0 ? sw_owner(r.fp_hi, world) : rank;
+    if (k.x == 0 && k.y == 0) break;
+    slot = (slot + 1) & a.reg_mask;
+  }
+  return rank;
 }
 
 // Partition input = this step's carry (records deferred by the previous partition, sent first)
@@ -445,7 +458,7 @@ __device__ __forceinline__ const SwEventRec& part_in(const SwEventRec* __restric
 __global__ void k_part_count(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
                              const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                              int world, int rank, uint32_t* __restrict__ tcount /*[world][ntiles]*/, int64_t ntiles,
-                             uint32_t* __restrict__ send_str_cnt) {
+                             uint32_t* __restrict__ send_str_cnt, SwEngineArgs a) {
   __shared__ uint32_t cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   // the string slabs' byte cursors start empty (k_part_write allocates from them)
@@ -457,8 +470,8 @@ __global__ void k_part_count(const SwEventRec* __restrict__ carry, const uint32_
   for (int k = 0; k < TILE_ITEMS; ++k) {
     int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     if (i < n) {
-      uint32_t o = owner_of(part_in(carry, nc, recs, i), world);
-      if (o == 0xffffffffu) o = rank;
+      const uint32_t o = part_dest(a, part_in(carry, nc, recs, i), (uint32_t)world, (uint32_t)rank);
+      a.part_owner[i] = (uint8_t)o;           // k_part_write reads it back
       atomicAdd(&cnt[o], 1u);
     }
   }
@@ -544,7 +557,7 @@ __global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool valid = i < n;
     uint32_t o = 0;
-    if (valid) { o = owner_of(part_in(carry, nc, recs, i), world); if (o == 0xffffffffu) o = rank; }
+    if (valid) o = a.part_owner[i];
     uint32_t my_rank = 0;
     for (int q = 0; q < world; ++q) {
       ull m = __ballot(valid && o == (uint32_t)q);
@@ -689,6 +702,7 @@ __global__ void k_lookup(SwEngineArgs a) {
     *a.n_gen = 0;
     *a.n_out = 0;
     if (a.dd_meta[2]) ((ull*)a.stats)[SW_STAT_DEDUP_ROTATIONS] += 1;
+    a.dd_meta[3] = 0;                      // ids of this step that met an already-claimed key
   }
   const SwEventRec* __restrict__ recs = a.work;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
@@ -753,12 +767,17 @@ __device__ __forceinline__ bool dd_find(const ull* __restrict__ tab, int64_t mas
 // the same lowest-sequence rule as the host engines, with ONE memory-side atomic per new id (each
 // device-scope atomic is its own 64-byte request on the MI355X; the CAS + atomicMin form paid two).
 // win - sb needs the window (< 2^31 ids) to stay far below 2^32 sequences, which rotation ensures.
+// A step where no id met an already-claimed key (dd_meta[3] == 0: fresh ids, the common case) needs
+// no verdict pass: every claimer is its key's first occurrence, and its store-backed filter probe
+// (SW_ST_RECHECK) is done here.  Otherwise k_cmp_count settles every id from its slot.
+__device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h);
+
 __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                                uint8_t* __restrict__ status, ull* __restrict__ tab, int64_t mask,
                                const int64_t* __restrict__ seq_base, int64_t* __restrict__ meta,
-                               ull* __restrict__ stats) {
-  __shared__ uint32_t blk_new, blk_over;
-  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; }
+                               ull* __restrict__ stats, const ull* __restrict__ bloom, int64_t bmask, int rank) {
+  __shared__ uint32_t blk_new, blk_over, blk_lose;
+  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; blk_lose = 0; }
   __syncthreads();
   const uint32_t n = *n_ptr;
   const ull sb = (ull)*seq_base;
@@ -766,7 +785,7 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
   const int64_t g = meta[0];
   ull* ct = tab + 2 * g * slots;
   const ull* pt = tab + 2 * (1 - g) * slots;
-  uint32_t my_new = 0, my_over = 0;
+  uint32_t my_new = 0, my_over = 0, my_lose = 0;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull h = recs[i].alt_hash;
     if (h == 0 || status[i] != SW_ST_OK) continue;
@@ -778,11 +797,15 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
       if (old == 0) {
         ++my_new;
         reinterpret_cast<uint32_t*>(&ct[2 * slot + 1])[0] = (uint32_t)(sb + (ull)i);
+        // provisional first sight; records decoded on another rank skip the store-backed filter (their
+        // payload bytes, which a recheck hands to the host path, are on that rank)
+        if (bloom && recs[i].src_rank == (uint8_t)rank && bloom_has(bloom, bmask, h)) status[i] = SW_ST_RECHECK;
         placed = true;
         break;
       }
       if (old == h) {
         atomicMin(reinterpret_cast<uint32_t*>(&ct[2 * slot + 1]) + 1, (uint32_t)i);
+        ++my_lose;
         placed = true;
         break;
       }
@@ -794,10 +817,12 @@ __global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32
   // atomics per step serialised this kernel, profiles/r3_dedup)
   if (my_new) atomicAdd(&blk_new, my_new);
   if (my_over) atomicAdd(&blk_over, my_over);
+  if (my_lose) atomicAdd(&blk_lose, my_lose);
   __syncthreads();
   if (threadIdx.x == 0) {
     if (blk_new) atomicAdd((unsigned long long*)&meta[1], (ull)blk_new);
     if (blk_over) atomicAdd(&stats[SW_STAT_DEDUP_OVERFLOW], (ull)blk_over);
+    if (blk_lose) atomicAdd((unsigned long long*)&meta[3], (ull)blk_lose);
   }
 }
 
@@ -822,7 +847,7 @@ struct DedupView {
   int64_t bmask;
 };
 
-__device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint32_t i) {
+__device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint32_t i, bool local) {
   int64_t slot = (int64_t)(h & (ull)d.mask);
   for (int64_t p = 0; p <= d.mask && p < MAX_PROBE; ++p) {
     const ulonglong2 kq = d.ct[slot];
@@ -831,7 +856,7 @@ __device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint
       const uint32_t lmin = (uint32_t)(kq.y >> 32);
       const bool first = wrel < d.n && (wrel < lmin ? wrel : lmin) == i;
       if (!first) return SW_ST_DUPLICATE;
-      return (d.bloom && bloom_has(d.bloom, d.bmask, h)) ? SW_ST_RECHECK : SW_ST_OK;   // first sight
+      return (local && d.bloom && bloom_has(d.bloom, d.bmask, h)) ? SW_ST_RECHECK : SW_ST_OK;   // first sight
     }
     if (kq.x == 0) break;                // not placed (probe overflow, counted): kept
     slot = (slot + 1) & d.mask;
@@ -846,7 +871,7 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
                             uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles, ull* __restrict__ stats,
                             const SwEventRec* __restrict__ recs, const ull* __restrict__ dd_tab, int64_t dd_mask,
                             const int64_t* __restrict__ seq_base, const int64_t* __restrict__ dd_meta,
-                            const ull* __restrict__ bloom, int64_t bmask) {
+                            const ull* __restrict__ bloom, int64_t bmask, int rank) {
   __shared__ uint32_t c[2];
   __shared__ uint32_t rs[8];          // rejects by status (the reject counters of the step)
   if (threadIdx.x < 2) c[threadIdx.x] = 0;
@@ -854,7 +879,8 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
   __syncthreads();
   const uint32_t n = *n_ptr;
   DedupView dv;
-  dv.ct = dd_tab ? reinterpret_cast<const ulonglong2*>(dd_tab) + dd_meta[0] * (dd_mask + 1) : nullptr;
+  // no id met a claimed key this step: k_dedup_insert's statuses are final (see there)
+  dv.ct = (dd_tab && dd_meta[3]) ? reinterpret_cast<const ulonglong2*>(dd_tab) + dd_meta[0] * (dd_mask + 1) : nullptr;
   dv.mask = dd_mask;
   dv.sb = (uint32_t)*seq_base;
   dv.n = n;
@@ -867,11 +893,12 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool v = i < n;
     uint8_t st = v ? status[i] : (uint8_t)SW_ST_OK;
-    if (v && st == SW_ST_OK && dv.ct) {
+    if (v && (st == SW_ST_OK || st == SW_ST_RECHECK) && dv.ct) {
       const ull h = recs[i].alt_hash;
       if (h) {
-        st = dedup_verdict(dv, h, (uint32_t)i);
-        if (st != SW_ST_OK) status[i] = st;
+        const uint8_t vst = dedup_verdict(dv, h, (uint32_t)i, recs[i].src_rank == (uint8_t)rank);
+        if (vst != st) status[i] = vst;
+        st = vst;
       }
     }
     ok += __popcll(__ballot(v && st == SW_ST_OK));
@@ -1522,10 +1549,10 @@ int sw_phase_partition(const SwEngineArgs* ap, hipStream_t s) {
   const SwEngineArgs a = *ap;
   const int64_t ntiles = (a.carry_cap + a.rec_cap + TILE - 1) / TILE;
   if (a.world > 64 || ntiles * a.world > a.part_tmp_len || !a.carry || !a.n_carry || !a.spill || !a.n_spill ||
-      a.carry == a.spill)
+      a.carry == a.spill || !a.part_owner)
     return -3;
   k_part_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.carry, a.n_carry, a.recs, a.n_recs, (int)a.world, (int)a.rank,
-                                                a.part_tmp, ntiles, a.send_str ? a.send_str_cnt : nullptr);
+                                                a.part_tmp, ntiles, a.send_str ? a.send_str_cnt : nullptr, a);
   // scan the flat [world][ntiles] count matrix in place
   int rc = launch_scan(a.part_tmp, ntiles * a.world, a.part_tmp + ntiles * a.world, nullptr, a.scan_tmp,
                        a.scan_tmp_len, s);
@@ -1555,11 +1582,11 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   if (2 * ntiles > a.scan_tmp_len) return -4;
   k_lookup<<<g, BLK, 0, s>>>(a);         // + the phase's resets (block 0)
   k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
-                                   (ull*)a.stats);
+                                   (ull*)a.stats, (const ull*)a.dd_bloom, a.dd_bloom_mask, (int)a.rank);
   // stable split ok / rejected, with the dedup verdicts
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
                                                (const ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
-                                               (const ull*)a.dd_bloom, a.dd_bloom_mask);
+                                               (const ull*)a.dd_bloom, a.dd_bloom_mask, (int)a.rank);
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx, a.n_ok,
                                                a.n_rej);
   int rc = 0;

@@ -209,6 +209,8 @@ typedef struct SwEngineArgs {
   SwStrRef* work_spans;        // [rec_cap] refs of the work batch (rebased into work_str)
   int64_t str_cap;             // bytes per destination slab
   uint32_t* str_drops;         // [2] records whose strings did not fit / came from the carry
+  // ---------------------------------------------------------------- re-key owner (world > 1)
+  uint8_t* part_owner;         // [carry_cap + rec_cap] destination of each partition input (k_part_count)
 } SwEngineArgs;
 
 #define SW_N_STATS 24

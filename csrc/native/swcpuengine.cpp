@@ -553,7 +553,9 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
           if (ins.second) {
             *ins.first = seq_base + i;
             // first sight in the window: the store may still hold it (filter from earlier steps)
-            if (!e->bloom.empty() && bloom_has(e, work[i].alt_hash)) status[i] = SW_ST_RECHECK;
+            // (records decoded on another rank skip it: their payload, the host path's input, is there)
+            if (!e->bloom.empty() && work[i].src_rank == (uint8_t)t->rank && bloom_has(e, work[i].alt_hash))
+              status[i] = SW_ST_RECHECK;
           } else {
             status[i] = SW_ST_DUPLICATE;
           }

@@ -65,6 +65,8 @@ FIELDS = [
     # string exchange (world > 1): per-destination byte slabs + refs beside the record slabs
     ("send_str", P), ("send_str_cnt", P), ("send_spans", P), ("recv_str", P), ("recv_str_cnt", P),
     ("recv_spans", P), ("work_str", P), ("work_spans", P), ("str_cap", I), ("str_drops", P),
+    # re-key destination of each partition input
+    ("part_owner", P),
 ]
 
 

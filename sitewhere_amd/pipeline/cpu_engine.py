@@ -84,7 +84,7 @@ class CpuInboundEngine(EngineBase):
         The input is the previous partition's carry followed by ``recs``; records beyond a slab are
         spilled destination-major into the next carry (up to ``carry_cap``, the rest dropped)."""
         recs = np.concatenate([self.carry, recs]) if len(self.carry) else recs
-        owner = np.where(recs["etype"] >= 16, self.rank, (recs["fp_hi"] >> np.uint64(32)) % np.uint64(self.world))
+        owner = self._dest(recs)
         cap = self.cfg.shuf_cap
         send = np.zeros((self.world, cap), EVENT_REC)
         cnt = np.zeros(self.world, np.int64)
@@ -101,6 +101,21 @@ class CpuInboundEngine(EngineBase):
         self.stats[10] += len(spill) - kept
         self.carry = spill[:kept].copy()
         return send, cnt
+
+    def _dest(self, recs: np.ndarray) -> np.ndarray:
+        """Re-key destination (``part_dest`` in csrc/hip/swgpu.hip): the device's owner for a record
+        whose device is registered with an active assignment (the registry is replicated on every
+        rank), the decoding rank for every other record -- it holds the payload the slow path routes."""
+        owner = ((recs["fp_hi"] >> np.uint64(32)) % np.uint64(self.world)).astype(np.int64)
+        for i in range(len(recs)):
+            if int(recs[i]["etype"]) >= 16:
+                owner[i] = self.rank
+                continue
+            d = self.lookup_device(int(recs[i]["fp_lo"]), int(recs[i]["fp_hi"]))
+            a = int(self.dev_asg[d]) if d >= 0 else -1
+            if a < 0 or not self.asg_active[a]:
+                owner[i] = self.rank
+        return owner
 
     def carry_count(self) -> int:
         return len(self.carry)
@@ -170,8 +185,10 @@ class CpuInboundEngine(EngineBase):
                 status[i] = ST_DUPLICATE
             else:
                 cur[h] = self.seq_base + i
-                if self.bloom is not None and self._bloom_has(h):
-                    status[i] = ST_RECHECK                   # maybe stored before: the host checks
+                # maybe stored before: the host checks (records decoded on another rank skip the
+                # filter -- their payload, which the host path needs, is on that rank)
+                if self.bloom is not None and int(recs[i]["src_rank"]) == self.rank and self._bloom_has(h):
+                    status[i] = ST_RECHECK
 
     def reset_dedup(self):
         """Forget the alternate-id window (both generations); the store-backed filter stays."""

@@ -151,6 +151,7 @@ class GpuInboundEngine(EngineBase):
             t["work"] = z(c.rec_cap * EVENT_REC.itemsize, u8)
             self.carry_bufs = [z(c.carry_cap * EVENT_REC.itemsize, u8) for _ in range(2)]
             t["n_carry"] = z(2, i32)
+            t["part_owner"] = z(c.carry_cap + c.rec_cap + 64, u8)      # re-key destination per input
             if c.str_cap:
                 # string exchange: byte slabs + refs beside the record slabs (double-buffered the same
                 # way), gathered into work_str by the unpack (see SwEngineArgs)
@@ -237,6 +238,7 @@ class GpuInboundEngine(EngineBase):
             a.part_tmp, a.part_tmp_len = _ptr(t["part_tmp"]), t["part_tmp"].numel() // 2
             a.work = _ptr(t["work"])
             a.carry_cap = c.carry_cap
+            a.part_owner = _ptr(t["part_owner"])
         else:
             a.work = a.recs
         a.str_drops = _ptr(t["str_drops"])

@@ -23,10 +23,13 @@ N_DEV = 900
 
 
 def shard_fleet(e, world, rank):
+    """Every rank registers the whole fleet (the registry is replicated: the decoding rank decides
+    whether a record goes to its device's owner or is rejected where its payload is); the owner
+    keeps the device's state, dedup window and events.  Returns the devices this rank owns."""
     heap, offs = gen_tokens("dev-", 0, N_DEV)
     lo, hi = fingerprints(heap, offs)
     mine = ((hi >> np.uint64(32)) % np.uint64(world)) == rank
-    dev = e.register_devices(lo[mine], hi[mine])
+    dev = e.register_devices(lo, hi)
     e.set_assignments(dev, dev, customer=dev % 7, area=dev % 5, asset=dev % 3)
     from sitewhere_amd.pipeline.engine_base import Zone, ZoneTest
     e.set_zone_rules([Zone("z1", SQUARE)], [ZoneTest("z1", "inside", "zone.enter", 2)])
