@@ -6,15 +6,20 @@ registry to every consumer.  MI355X form:
 
 * **ownership** -- each rank owns the devices whose 128-bit token fingerprint satisfies
   ``(fp_hi >> 32) % world == rank`` (``sw_owner`` in ``csrc/include/swtypes.h``).  The owner holds the
-  device's registry slot, assignment context, device state, dedup window and event-store rows, so
-  every stateful stage is shard-local -- no cross-GPU atomics.
+  device's state, dedup window and event-store rows, so every stateful stage is shard-local -- no
+  cross-GPU atomics.  The registry (fingerprint -> device, active assignment, context) is
+  replicated on every rank, as the reference's near cache replicates it to every consumer: the
+  rank that decoded a record sends it to the owner only when its device is registered and assigned,
+  and rejects every other record itself -- it holds the payload bytes the slow path routes.
 * **re-keying** -- every rank decodes the payloads it received, partitions the decoded records into
   per-owner slabs (``k_part_count``/``k_part_write``), and one ``all_to_all_single`` of the slab
   counts plus one of the slabs moves each record to its owner over xGMI (the GPU analogue of
   producing to the key's partition).  Records cross xGMI in a lossless 64-byte packed form
   (``SwWireRec``: fields no event type uses together share words), 20% fewer bytes than the
-  80-byte decoded record.  Control records (registration, acks, streams) stay on the
-  receiving rank, whose host owns their raw bytes.
+  80-byte decoded record; their strings (alternate id, metadata, alert message) travel beside them
+  in per-destination byte slabs (``EngineConfig.str_bytes`` per slot).  Control records
+  (registration, acks, streams) and records of unknown devices stay on the receiving rank, whose
+  host owns their raw bytes.
 * **slab sizing** -- fixed-size slabs keep the exchange free of host synchronisation: capacity per
   destination = ``shuffle_slack * rec_cap / world + 1024`` (``EngineConfig.shuf_cap``, slack 1.1).
   A uniform key hash puts ~rec_cap/world records per destination (sigma ~ sqrt of that, so 1.1x
