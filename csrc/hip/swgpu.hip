@@ -678,17 +678,94 @@ __device__ __forceinline__ void intern_insert(ull* __restrict__ key, int32_t* __
   }
 }
 
+// Alternate-id dedup window (reference AlternateIdDeduplicator.java:41-56), generational: two
+// open-addressing tables, `cur` (ids first seen in the current generation) and `prev` (the
+// generation before).  An event whose id is in `prev` is a duplicate; otherwise it is inserted into
+// `cur`, where the first occurrence (lowest global sequence) wins and every later one -- in this
+// batch or any later batch of the generation -- is a duplicate.  When a step leaves `cur` past half
+// its slots less one batch, the generations rotate for the next step: k_persist decides, k_state_p2
+// clears the retiring table, k_step_end flips (dd_meta = [generation, ids in cur, rotation state,
+// ids that met a claimed key]).  The window therefore covers the last slots/2 - rec_cap to
+// slots - rec_cap distinct ids, probes stay short (load <= 0.5), and a probe that still hits
+// MAX_PROBE is counted (SW_STAT_DEDUP_OVERFLOW) rather than silently ignored.
+//
+// Tables of packed 16-byte slots {key, win: u32, lmin: u32} (two generations of dd_mask + 1 slots):
+//   key  -- the alternate-id hash, claimed by CAS;
+//   win  -- low 32 bits of the sequence of the id that claimed the slot (plain store by the CAS
+//           winner: the slot's other fields are disjoint bytes);
+//   lmin -- lowest in-batch index of the ids that found the key already claimed in THIS batch
+//           (atomicMin; rare: only repeats inside one batch).
+// First occurrence = the slot was claimed in this batch and min(win - sb, lmin) is the id's index:
+// the same lowest-sequence rule as the host engines, with ONE memory-side atomic per new id (each
+// device-scope atomic is its own 64-byte request on the MI355X; the CAS + atomicMin form paid two).
+// win - sb needs the window (< 2^31 ids) to stay far below 2^32 sequences, which rotation ensures.
+// A step where no id met an already-claimed key (dd_meta[3] == 0: fresh ids, the common case) needs
+// no verdict pass: every claimer is its key's first occurrence, and its store-backed filter probe
+// (SW_ST_RECHECK) is done at the claim.  Otherwise k_cmp_count settles every id from its slot.
+__device__ __forceinline__ bool dd_find(const ull* __restrict__ tab, int64_t mask, ull h) {
+  int64_t slot = (int64_t)(h & (ull)mask);
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    const ull k = tab[2 * slot];
+    if (k == h) return true;
+    if (k == 0) return false;
+    slot = (slot + 1) & mask;
+  }
+  return false;
+}
+
+// The id's filter block holds all its bits: it may have been persisted before (beyond the window).
+__device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h) {
+  const ull m = sw_bloom_bits(h);
+  return (bloom[sw_bloom_block(h, bmask)] & m) == m;
+}
+
+__device__ __forceinline__ void bloom_add(ull* __restrict__ bloom, int64_t bmask, ull h) {
+  atomicOr(&bloom[sw_bloom_block(h, bmask)], (ull)sw_bloom_bits(h));   // no return: fire-and-forget
+}
+
+struct DedupCounts {
+  uint32_t fresh, over, lose;
+};
+
+// Claim the id's slot in `cur` (fused into k_lookup: the record is already in registers).  Returns
+// the id's provisional status: DUPLICATE (held by `prev`), RECHECK (first claim, maybe stored
+// before -- records decoded on another rank skip the filter: their payload, a recheck's input, is
+// there) or OK.
+__device__ __forceinline__ uint8_t dedup_claim(const SwEngineArgs& a, ull h, int64_t i, uint8_t src_rank,
+                                               DedupCounts& c) {
+  const int64_t mask = a.dd_mask, slots = mask + 1;
+  const int64_t g = a.dd_meta[0];
+  ull* ct = (ull*)a.dd_key + 2 * g * slots;
+  const ull* pt = (const ull*)a.dd_key + 2 * (1 - g) * slots;
+  if (dd_find(pt, mask, h)) return SW_ST_DUPLICATE;
+  const ull sb = (ull)*a.seq_base;
+  int64_t slot = (int64_t)(h & (ull)mask);
+  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
+    const ull old = atomicCAS(&ct[2 * slot], 0ull, h);
+    if (old == 0) {
+      ++c.fresh;
+      reinterpret_cast<uint32_t*>(&ct[2 * slot + 1])[0] = (uint32_t)(sb + (ull)i);
+      return (a.dd_bloom && src_rank == (uint8_t)a.rank && bloom_has((const ull*)a.dd_bloom, a.dd_bloom_mask, h))
+                 ? (uint8_t)SW_ST_RECHECK : (uint8_t)SW_ST_OK;
+    }
+    if (old == h) {
+      atomicMin(reinterpret_cast<uint32_t*>(&ct[2 * slot + 1]) + 1, (uint32_t)i);
+      ++c.lose;
+      return SW_ST_OK;
+    }
+    slot = (slot + 1) & mask;
+  }
+  ++c.over;                                  // not placed: kept (counted)
+  return SW_ST_OK;
+}
+
 // One probe of the packed registry resolves device AND active assignment; names of every
 // decodable event are interned here too (fused: one pass over the records).
 __global__ void k_lookup(SwEngineArgs a) {
-  // generation rotation decided by the previous step's k_step_end: clear the table that becomes
-  // `cur` (dedup runs after this kernel)
-  if (a.dd_meta[2]) {
-    const int64_t slots = a.dd_mask + 1;
-    ulonglong2* t = reinterpret_cast<ulonglong2*>(a.dd_key) + a.dd_meta[0] * slots;
-    for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK)
-      t[i] = make_ulonglong2(0ull, ~0ull);
-  }
+  __shared__ uint32_t blk_new, blk_over, blk_lose;
+  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; blk_lose = 0; }
+  __syncthreads();
+  DedupCounts dc = {0u, 0u, 0u};
   // world == 1: the work batch is the decoded batch, clamped (every block derives the same count;
   // block 0 stores it for the kernels after this one)
   const uint32_t n = a.world == 1 ? (*a.n_recs < (uint32_t)a.rec_cap ? *a.n_recs : (uint32_t)a.rec_cap) : *a.n_work;
@@ -701,8 +778,10 @@ __global__ void k_lookup(SwEngineArgs a) {
     *a.step_cursor0 = *a.store_cursor;
     *a.n_gen = 0;
     *a.n_out = 0;
-    if (a.dd_meta[2]) ((ull*)a.stats)[SW_STAT_DEDUP_ROTATIONS] += 1;
-    a.dd_meta[3] = 0;                      // ids of this step that met an already-claimed key
+    if (a.dd_meta[2] == 2) {               // the generations rotated at the end of the last step
+      ((ull*)a.stats)[SW_STAT_DEDUP_ROTATIONS] += 1;
+      a.dd_meta[2] = 0;
+    }
   }
   const SwEventRec* __restrict__ recs = a.work;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
@@ -728,112 +807,24 @@ __global__ void k_lookup(SwEngineArgs a) {
       else if (dev < 0) st = SW_ST_UNREGISTERED;
       else st = asg >= 0 ? SW_ST_OK : SW_ST_UNASSIGNED;
       if (st == SW_ST_OK && nh) intern_insert((ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, nh);
+      const ull ah = recs[i].alt_hash;
+      if (st == SW_ST_OK && ah) st = dedup_claim(a, ah, i, recs[i].src_rank, dc);   // fused dedup claim
     }
     a.status[i] = st;
     a.ev_dev[i] = dev;
     a.ev_asg[i] = asg;
   }
-}
-
-// Alternate-id dedup window (reference AlternateIdDeduplicator.java:41-56), generational: two
-// open-addressing tables, `cur` (ids first seen in the current generation) and `prev` (the
-// generation before).  An event whose id is in `prev` is a duplicate; otherwise it is inserted into
-// `cur`, where the first occurrence (lowest global sequence) wins and every later one -- in this
-// batch or any later batch of the generation -- is a duplicate.  Before a step whose ids could push
-// `cur` past half its slots, the generations rotate (decided by k_step_end): `prev` is forgotten and
-// cleared to become the new `cur`.  The window therefore covers the last slots/2 - rec_cap to
-// slots - rec_cap distinct ids, probes stay short (load <= 0.5), and a probe that still hits
-// MAX_PROBE is counted (SW_STAT_DEDUP_OVERFLOW) rather than silently ignored.
-__device__ __forceinline__ bool dd_find(const ull* __restrict__ tab, int64_t mask, ull h) {
-  int64_t slot = (int64_t)(h & (ull)mask);
-  for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-    const ull k = tab[2 * slot];
-    if (k == h) return true;
-    if (k == 0) return false;
-    slot = (slot + 1) & mask;
-  }
-  return false;
-}
-
-// dd_meta = [generation, ids in cur, rotate flag, pad]: k_step_end decides the next step's rotation,
-// k_lookup clears the retired generation.
-// Tables of packed 16-byte slots {key, win: u32, lmin: u32} (two generations of dd_mask + 1 slots):
-//   key  -- the alternate-id hash, claimed by CAS;
-//   win  -- low 32 bits of the sequence of the id that claimed the slot (plain store by the CAS
-//           winner: the slot's other fields are disjoint bytes);
-//   lmin -- lowest in-batch index of the ids that found the key already claimed in THIS batch
-//           (atomicMin; rare: only repeats inside one batch).
-// First occurrence = the slot was claimed in this batch and min(win - sb, lmin) is the id's index:
-// the same lowest-sequence rule as the host engines, with ONE memory-side atomic per new id (each
-// device-scope atomic is its own 64-byte request on the MI355X; the CAS + atomicMin form paid two).
-// win - sb needs the window (< 2^31 ids) to stay far below 2^32 sequences, which rotation ensures.
-// A step where no id met an already-claimed key (dd_meta[3] == 0: fresh ids, the common case) needs
-// no verdict pass: every claimer is its key's first occurrence, and its store-backed filter probe
-// (SW_ST_RECHECK) is done here.  Otherwise k_cmp_count settles every id from its slot.
-__device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h);
-
-__global__ void k_dedup_insert(const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
-                               uint8_t* __restrict__ status, ull* __restrict__ tab, int64_t mask,
-                               const int64_t* __restrict__ seq_base, int64_t* __restrict__ meta,
-                               ull* __restrict__ stats, const ull* __restrict__ bloom, int64_t bmask, int rank) {
-  __shared__ uint32_t blk_new, blk_over, blk_lose;
-  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; blk_lose = 0; }
-  __syncthreads();
-  const uint32_t n = *n_ptr;
-  const ull sb = (ull)*seq_base;
-  const int64_t slots = mask + 1;
-  const int64_t g = meta[0];
-  ull* ct = tab + 2 * g * slots;
-  const ull* pt = tab + 2 * (1 - g) * slots;
-  uint32_t my_new = 0, my_over = 0, my_lose = 0;
-  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
-    const ull h = recs[i].alt_hash;
-    if (h == 0 || status[i] != SW_ST_OK) continue;
-    if (dd_find(pt, mask, h)) { status[i] = SW_ST_DUPLICATE; continue; }
-    int64_t slot = (int64_t)(h & (ull)mask);
-    bool placed = false;
-    for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
-      const ull old = atomicCAS(&ct[2 * slot], 0ull, h);
-      if (old == 0) {
-        ++my_new;
-        reinterpret_cast<uint32_t*>(&ct[2 * slot + 1])[0] = (uint32_t)(sb + (ull)i);
-        // provisional first sight; records decoded on another rank skip the store-backed filter (their
-        // payload bytes, which a recheck hands to the host path, are on that rank)
-        if (bloom && recs[i].src_rank == (uint8_t)rank && bloom_has(bloom, bmask, h)) status[i] = SW_ST_RECHECK;
-        placed = true;
-        break;
-      }
-      if (old == h) {
-        atomicMin(reinterpret_cast<uint32_t*>(&ct[2 * slot + 1]) + 1, (uint32_t)i);
-        ++my_lose;
-        placed = true;
-        break;
-      }
-      slot = (slot + 1) & mask;
-    }
-    my_over += placed ? 0u : 1u;
-  }
-  // counters aggregated per workgroup: one global atomic per block, not one per id (1M same-address
-  // atomics per step serialised this kernel, profiles/r3_dedup)
-  if (my_new) atomicAdd(&blk_new, my_new);
-  if (my_over) atomicAdd(&blk_over, my_over);
-  if (my_lose) atomicAdd(&blk_lose, my_lose);
+  // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
+  // same-address atomics per step serialised the kernel, profiles/r3_dedup)
+  if (dc.fresh) atomicAdd(&blk_new, dc.fresh);
+  if (dc.over) atomicAdd(&blk_over, dc.over);
+  if (dc.lose) atomicAdd(&blk_lose, dc.lose);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (blk_new) atomicAdd((unsigned long long*)&meta[1], (ull)blk_new);
-    if (blk_over) atomicAdd(&stats[SW_STAT_DEDUP_OVERFLOW], (ull)blk_over);
-    if (blk_lose) atomicAdd((unsigned long long*)&meta[3], (ull)blk_lose);
+    if (blk_new) atomicAdd((unsigned long long*)&a.dd_meta[1], (ull)blk_new);
+    if (blk_over) atomicAdd((ull*)&a.stats[SW_STAT_DEDUP_OVERFLOW], (ull)blk_over);
+    if (blk_lose) atomicAdd((unsigned long long*)&a.dd_meta[3], (ull)blk_lose);
   }
-}
-
-// The id's filter block holds all its bits: it may have been persisted before (beyond the window).
-__device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h) {
-  const ull m = sw_bloom_bits(h);
-  return (bloom[sw_bloom_block(h, bmask)] & m) == m;
-}
-
-__device__ __forceinline__ void bloom_add(ull* __restrict__ bloom, int64_t bmask, ull h) {
-  atomicOr(&bloom[sw_bloom_block(h, bmask)], (ull)sw_bloom_bits(h));   // no return: fire-and-forget
 }
 
 // Second half of the dedup (fused into the compaction count, k_cmp_count): the id's verdict from
@@ -866,7 +857,7 @@ __device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint
 
 // ============================================================================ compaction
 // Stable split of [0, n) into ok (status == OK) and rejected lists.  The count pass also settles the
-// dedup verdict of every id k_dedup_insert left OK (dedup_verdict): no separate check dispatch.
+// dedup verdict of every id k_lookup's claim left OK / RECHECK (dedup_verdict): no separate check dispatch.
 __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __restrict__ n_ptr,
                             uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles, ull* __restrict__ stats,
                             const SwEventRec* __restrict__ recs, const ull* __restrict__ dd_tab, int64_t dd_mask,
@@ -879,7 +870,7 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
   __syncthreads();
   const uint32_t n = *n_ptr;
   DedupView dv;
-  // no id met a claimed key this step: k_dedup_insert's statuses are final (see there)
+  // no id met a claimed key this step: the claim's statuses are final (see dedup_claim)
   dv.ct = (dd_tab && dd_meta[3]) ? reinterpret_cast<const ulonglong2*>(dd_tab) + dd_meta[0] * (dd_mask + 1) : nullptr;
   dv.mask = dd_mask;
   dv.sb = (uint32_t)*seq_base;
@@ -996,6 +987,11 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
                           const uint32_t* __restrict__ after) {
   const uint32_t n = *n_ptr < cap ? *n_ptr : cap;     // generated events: n_gen may pass gen_cap
   const int64_t cur = *a.store_cursor + (after ? (int64_t)*after : 0);   // rows start past `after` rows
+  if (idx && BID == 0 && threadIdx.x == 0) {
+    // every claim of the step is counted: rotate the dedup generations for the next step when it
+    // could push the live table past half load (k_state_p2 clears, k_step_end flips)
+    if (a.dd_meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) a.dd_meta[2] = 1;
+  }
   const int64_t c0 = *a.step_cursor0;
   const int64_t now = a.sp->now_ms;
   SwSegAux* const aux = reinterpret_cast<SwSegAux*>(a.sp->aux);
@@ -1081,6 +1077,14 @@ __global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, u
                            const uint32_t* __restrict__ after) {
   const uint32_t n = *n_ptr < cap ? *n_ptr : cap;
   const int64_t cur = *a.store_cursor + (after ? (int64_t)*after : 0);
+  if (!after && a.dd_meta[2] == 1) {
+    // dedup rotation decided by k_persist: clear the retiring generation (no reader is left this
+    // step: `prev` was probed by the claims in k_lookup); it becomes `cur` when k_step_end flips
+    const int64_t slots = a.dd_mask + 1;
+    ulonglong2* t = reinterpret_cast<ulonglong2*>(a.dd_key) + (1 - a.dd_meta[0]) * slots;
+    for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK)
+      t[i] = make_ulonglong2(0ull, ~0ull);
+  }
   const longlong2* __restrict__ work = reinterpret_cast<const longlong2*>(a.ev_slot);
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const longlong2 w = work[j];
@@ -1367,16 +1371,15 @@ __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
     st[SW_STAT_PERSISTED] += *a.n_out;
     st[SW_STAT_RULE_ALERTS] += *n_rule_alerts;
     st[SW_STAT_PRESENCE] += *a.n_gen - *n_rule_alerts;
-    // the next step's dedup generation: rotate before a step whose ids could push the live table
-    // past half load (k_lookup of that step clears the retired table and counts the rotation)
+    // dedup rotation decided and cleared this step: flip the generations (the next step's
+    // k_lookup counts it)
     int64_t* meta = a.dd_meta;
-    if (meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) {
+    if (meta[2] == 1) {
       meta[0] ^= 1;
       meta[1] = 0;
-      meta[2] = 1;
-    } else {
-      meta[2] = 0;
+      meta[2] = 2;
     }
+    meta[3] = 0;
   }
 }
 
@@ -1580,9 +1583,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int g = grid_for(a.rec_cap);
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
   if (2 * ntiles > a.scan_tmp_len) return -4;
-  k_lookup<<<g, BLK, 0, s>>>(a);         // + the phase's resets (block 0)
-  k_dedup_insert<<<g, BLK, 0, s>>>(a.work, a.n_work, a.status, (ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
-                                   (ull*)a.stats, (const ull*)a.dd_bloom, a.dd_bloom_mask, (int)a.rank);
+  k_lookup<<<g, BLK, 0, s>>>(a);         // + the dedup claim; the phase's resets (block 0)
   // stable split ok / rejected, with the dedup verdicts
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
                                                (const ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,

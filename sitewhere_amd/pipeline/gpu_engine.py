@@ -1282,7 +1282,12 @@ class GpuInboundEngine(EngineBase):
         if "dd_tab" not in a and "dd_meta" in a:
             # older checkpoints decided the rotation at the start of a step; now the end of the
             # previous step does (k_step_end): apply that decision to the restored window
-            m = self._armed_dedup_meta(a["dd_meta"].astype(np.int64).copy(), self.cfg)
+            m0 = a["dd_meta"].astype(np.int64).copy()
+            m = self._armed_dedup_meta(m0.copy(), self.cfg)
+            if m[0] != m0[0]:                  # flipped here: the new live table starts empty
+                slots = self.cfg.dedup_slots
+                self.t["dd_tab"][int(m[0]) * slots:(int(m[0]) + 1) * slots, 0] = 0
+                self.t["dd_tab"][int(m[0]) * slots:(int(m[0]) + 1) * slots, 1] = -1
             self.t["dd_meta"].copy_(torch.from_numpy(m))
         if self.world > 1 and "carry" in a:
             cp = self._carry_par
@@ -1297,11 +1302,14 @@ class GpuInboundEngine(EngineBase):
 
     @staticmethod
     def _armed_dedup_meta(m: np.ndarray, cfg) -> np.ndarray:
-        """dd_meta = [generation, ids in the live table, rotate flag, pad] as k_step_end leaves it:
-        with the NEXT step's rotation decided (the live table could pass half load) -- what the
-        first step after an allocation, a reset or an old checkpoint needs."""
+        """dd_meta = [generation, ids in the live table, rotation state, ids that met a claimed key]
+        as k_step_end leaves it: a rotation the next step needs (the live table could pass half
+        load) already flipped (state 2: k_lookup counts it) -- what the first step after an
+        allocation, a reset or an old checkpoint needs.  The caller clears the new live table when
+        it is not empty."""
+        m[3] = 0
         if m[1] + cfg.rec_cap > cfg.dedup_slots // 2:
-            m[0], m[1], m[2] = m[0] ^ 1, 0, 1
+            m[0], m[1], m[2] = m[0] ^ 1, 0, 2
         else:
             m[2] = 0
         return m
