@@ -70,6 +70,24 @@ def test_cpu_loopback_conserves_events():
         assert (res_r.event_ids() % W == r).all()
 
 
+def test_rejects_stay_with_their_payload():
+    """Records of unregistered devices are rejected by the rank that decoded them -- its raw batch
+    holds the payload the slow path routes -- and every reject ref points into that batch."""
+    from sitewhere_amd.models.columnar import ST_UNREGISTERED
+    shards = cpu_shards()
+    batches = [fleet_batch(1500, seed=60 + r, n_dev=N_DEV) for r in range(W)]
+    res = cpu_loopback_step(shards, batches, NOW)
+    unreg = 0
+    for r, res_r in enumerate(res):
+        st = res_r.reject_status
+        assert (res_r.rejects["src_rank"] == r).all()          # never a remote record
+        unreg += int((st == ST_UNREGISTERED).sum())
+    single = CpuInboundEngine(EngineConfig.small(max_msgs=8192))
+    shard_fleet(single, 1, 0)
+    ref = [single.step(raw, offs, NOW, presence=False) for raw, offs in batches]
+    assert unreg == sum(int((x.reject_status == ST_UNREGISTERED).sum()) for x in ref) > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_available(), reason="needs an MI355X GPU")
 def test_gpu_loopback_matches_cpu_oracle():
