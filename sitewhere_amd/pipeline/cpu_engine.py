@@ -78,29 +78,87 @@ class CpuInboundEngine(EngineBase):
         self._seen: set[int] = set()
 
     # ------------------------------------------------------------------ stages
-    def partition(self, recs: np.ndarray):
+    def partition(self, recs: np.ndarray, with_index: bool = False):
         """Stable owner partition into [world, shuf_cap] slabs (same as k_part_count/k_part_write).
 
         The input is the previous partition's carry followed by ``recs``; records beyond a slab are
-        spilled destination-major into the next carry (up to ``carry_cap``, the rest dropped)."""
-        recs = np.concatenate([self.carry, recs]) if len(self.carry) else recs
+        spilled destination-major into the next carry (up to ``carry_cap``, the rest dropped).
+        ``with_index``: also the input indices of each slab's records and the carry length."""
+        nc = len(self.carry)
+        recs = np.concatenate([self.carry, recs]) if nc else recs
         owner = self._dest(recs)
         cap = self.cfg.shuf_cap
         send = np.zeros((self.world, cap), EVENT_REC)
         cnt = np.zeros(self.world, np.int64)
         spill = []
+        index = []
         for o in range(self.world):
-            sel = recs[owner == o]
+            at = np.nonzero(owner == o)[0]
+            sel = recs[at]
             k = min(len(sel), cap)
             send[o, :k] = sel[:k]
             cnt[o] = k
+            index.append(at[:k])
             spill.append(sel[k:])
         spill = np.concatenate(spill)
         kept = min(len(spill), self.cfg.carry_cap)
         self.stats[13] += kept
         self.stats[10] += len(spill) - kept
         self.carry = spill[:kept].copy()
+        if with_index:
+            return send, cnt, index, nc
         return send, cnt
+
+    def _pack_strings(self, send, index, nc, spans, raw):
+        """String slabs of a partition (``part_strings`` in csrc/hip/swgpu.hip): per destination, each
+        slab record's alternate id, metadata and alert message copied from this rank's batch into
+        one byte slab, its refs rewritten to slab offsets (the alert message offset in the record).
+        Carried records (decoded in an earlier step) have none; what does not fit is dropped."""
+        W, S, cap = self.world, self.cfg.shuf_cap, self.cfg.str_cap
+        out_sp = np.zeros((W, S), STR_REF)
+        buf = np.zeros(W * cap, np.uint8)
+        used = np.zeros(W, np.int64)
+        for o in range(W):
+            at = index[o]
+            k = len(at)
+            if not k:
+                continue
+            r = send[o, :k]
+            fresh = at >= nc
+            s = np.zeros(k, STR_REF)
+            s[fresh] = spans[at[fresh] - nc]
+            ctl = r["etype"] >= 16                  # control records keep their raw-batch offsets
+            al = np.where((s["has"] & 1) != 0, s["alt_len"], 0).astype(np.int64)
+            ml = np.where((s["has"] & 2) != 0, s["meta_len"], 0).astype(np.int64)
+            alert = (r["etype"] == EV_ALERT) & fresh
+            gl = np.where(alert, r["aux2_len"], 0).astype(np.int64)
+            al[ctl] = ml[ctl] = gl[ctl] = 0
+            ln = al + ml + gl
+            fit = (np.cumsum(ln) <= cap)
+            ln = np.where(fit, ln, 0)
+            al, ml, gl = np.where(fit, al, 0), np.where(fit, ml, 0), np.where(fit, gl, 0)
+            start = np.cumsum(ln) - ln
+            total = int(ln.sum())
+            used[o] = total
+            if total:
+                seg_src = np.stack([s["alt_off"].astype(np.int64), s["meta_off"].astype(np.int64),
+                                    r["aux2_off"].astype(np.int64)], 1).reshape(-1)
+                seg_len = np.stack([al, ml, gl], 1).reshape(-1)
+                idx = np.repeat(seg_src - (np.cumsum(seg_len) - seg_len), seg_len) + np.arange(total)
+                buf[o * cap:o * cap + total] = raw[idx]
+            ns = np.zeros(k, STR_REF)
+            keep = fresh & ~ctl
+            ns["k"] = np.where(keep, s["k"], 0)
+            ns["has"] = np.where(keep & (ln > 0), s["has"], np.where(keep, s["has"] & 4, 0))
+            ns["alt_off"] = np.where(keep & (ln > 0), start, 0)
+            ns["meta_off"] = np.where(keep & (ln > 0), start + al, 0)
+            ns["alt_len"] = np.where(keep & (ln > 0), s["alt_len"], 0)
+            ns["meta_len"] = np.where(keep & (ln > 0), s["meta_len"], 0)
+            out_sp[o, :k] = ns
+            am = r["etype"] == EV_ALERT
+            r["aux2_off"] = np.where(am & ~ctl, np.where(gl > 0, start + al + ml, 0), r["aux2_off"])
+            r["aux2_len"] = np.where(am & ~ctl, gl, r["aux2_len"])
+        return out_sp, buf, used
 
     def _dest(self, recs: np.ndarray) -> np.ndarray:
         """Re-key destination (``part_dest`` in csrc/hip/swgpu.hip): the device's owner for a record
@@ -124,24 +182,48 @@ class CpuInboundEngine(EngineBase):
     def unpack(recv: np.ndarray, rcnt) -> np.ndarray:
         return np.concatenate([recv[q, :int(rcnt[q])] for q in range(recv.shape[0])])
 
-    def _shuffle(self, recs: np.ndarray) -> np.ndarray:
+    def _shuffle(self, recs: np.ndarray, raw=None):
+        """Re-key of this step's records: (work batch, its string refs, their string source) -- the
+        last two None when strings do not travel (custom transport, ``str_bytes`` = 0)."""
         if self.world == 1:
-            return recs
+            return recs, None, None
         if self.exchange is not None:          # loopback / custom transport
-            return self.exchange(self, recs)
+            return self.exchange(self, recs), None, None
         import torch
 
         from ..parallel.sharding import exchange_slabs
-        send, cnt = self.partition(recs)
+        send, cnt, index, nc = self.partition(recs, with_index=True)
+        strings = bool(self.cfg.str_cap) and raw is not None and getattr(self, "_dec_spans", None) is not None
+        extra = ()
+        if strings:
+            sp, sbuf, sused = self._pack_strings(send, index, nc, self._dec_spans, np.asarray(raw, np.uint8))
+            rsp = np.zeros_like(sp)
+            rbuf = np.zeros_like(sbuf)
+            rused = np.zeros_like(sused)
+            extra = ((torch.from_numpy(sused), torch.from_numpy(rused)),
+                     (torch.from_numpy(sp.reshape(-1).view(np.uint8)), torch.from_numpy(rsp.reshape(-1).view(np.uint8))),
+                     (torch.from_numpy(sbuf), torch.from_numpy(rbuf)))
         # the exchange carries the packed 64-byte form, like the GPU all-to-all
         send_t = torch.from_numpy(wire_pack(send.reshape(-1)).view(np.uint8))
         recv_t = torch.empty_like(send_t)
         cnt_t = torch.from_numpy(cnt)
         rcnt_t = torch.empty_like(cnt_t)
-        exchange_slabs(cnt_t, rcnt_t, send_t, recv_t, self.group)
+        exchange_slabs(cnt_t, rcnt_t, send_t, recv_t, self.group, extra)
         wire = recv_t.numpy().view(WIRE_REC).reshape(self.world, self.cfg.shuf_cap)
         recv = np.stack([wire_unpack(wire[q], q) for q in range(self.world)])
-        return self.unpack(recv, rcnt_t.numpy())
+        rc = rcnt_t.numpy()
+        work = self.unpack(recv, rc)
+        if not strings:
+            return work, None, None
+        # refs rebased into the gathered slabs (+ source rank * str_cap), as k_unpack does
+        cap = self.cfg.str_cap
+        wsp = np.concatenate([rsp[q, :int(rc[q])] for q in range(self.world)])
+        base = np.concatenate([np.full(int(rc[q]), q * cap, np.int64) for q in range(self.world)])
+        wsp["alt_off"] = (wsp["alt_off"].astype(np.int64) + base).astype(np.uint32)
+        wsp["meta_off"] = (wsp["meta_off"].astype(np.int64) + base).astype(np.uint32)
+        am = work["etype"] == EV_ALERT
+        work["aux2_off"] = np.where(am, (work["aux2_off"].astype(np.int64) + base).astype(np.uint32), work["aux2_off"])
+        return work, wsp, rbuf
 
     def _lookup(self, recs):
         n = len(recs)
@@ -277,12 +359,13 @@ class CpuInboundEngine(EngineBase):
     # ------------------------------------------------------------------ step
     def step(self, raw: np.ndarray, offs: np.ndarray, now_ms: int, presence: bool | None = None) -> StepResult:
         recs, new = self.decode_phase(raw, offs, now_ms)
-        work = self._shuffle(recs)
-        # string refs point into this rank's batch: they hold for the records it processes itself
-        spans = self._dec_spans if self.world == 1 else None
+        # strings: this rank's batch on one rank; the exchanged string slabs on several
+        work, spans, src = self._shuffle(recs, raw)
+        if self.world == 1:
+            spans, src = self._dec_spans, raw
         res = self.process_phase(work, len(offs) - 1, now_ms, new, presence, spans=spans)
         if spans is not None:
-            res.raw = raw
+            res.raw = src
         return res
 
     def decode_phase(self, raw, offs, now_ms):

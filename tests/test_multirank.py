@@ -255,9 +255,22 @@ def _gloo_worker(rank, world, port, q):
     shard_fleet(e, world, rank)
     raw, offs = fleet_batch(1000, seed=500 + rank, n_dev=N_DEV)
     r = e.step(raw, offs, NOW, presence=False)
-    q.put((rank, r.n_events, r.n_persisted, bool((r.event_ids() % world == rank).all())))
+    keys = _block_string_keys(e.encode_block(NOW, r, boot=5))
+    q.put((rank, r.n_events, r.n_persisted, bool((r.event_ids() % world == rank).all()), keys))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _block_string_keys(block) -> list:
+    """(type, date, value, alternate id, message, metadata) of every row of a durable block."""
+    from sitewhere_amd.persistence.segments import decode_block, row_strings
+    c = decode_block(block)
+    out = []
+    for i in range(len(c["etype"])):
+        alt, msg, md = row_strings(c, i)
+        out.append((int(c["etype"][i]), int(c["date"][i]), float(c["v0"][i]), alt or "", msg or "",
+                    tuple(sorted((md or {}).items()))))
+    return out
 
 
 def test_gloo_two_ranks():
@@ -278,10 +291,17 @@ def test_gloo_two_ranks():
         assert p.exitcode == 0
     single = CpuInboundEngine(EngineConfig.small())
     shard_fleet(single, 1, 0)
-    tot = [single.step(*fleet_batch(1000, seed=500 + r, n_dev=N_DEV), NOW, presence=False) for r in range(2)]
+    tot, ref = [], []
+    for r in range(2):
+        tot.append(single.step(*fleet_batch(1000, seed=500 + r, n_dev=N_DEV), NOW, presence=False))
+        ref += _block_string_keys(single.encode_block(NOW, tot[-1], boot=5))
     assert sum(o[1] for o in outs) == sum(t.n_events for t in tot)
     assert sum(o[2] for o in outs) == sum(t.n_persisted for t in tot)
     assert all(o[3] for o in outs)
+    # whole events on the owner ranks: the strings crossed the exchange with the records
+    got = [k for o in outs for k in o[4]]
+    assert sum(1 for k in got if k[3]) > 0.8 * len(got)
+    assert sorted(got) == sorted(ref)
 
 
 @pytest.mark.gpu
