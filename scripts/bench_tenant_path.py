@@ -197,7 +197,7 @@ def main():
                       "events_per_sec": round(ev / dt, 1), "persisted": ib.persisted_events.count - base,
                       "ms_per_batch": round(1000 * dt / args.batches, 3), "batch": args.batch,
                       "engine_steps": ib.step_timer.count,
-                      "devices": args.devices, "store_rows": em_store.rows, "template": args.template,
+                      "devices": args.devices, "store_rows": getattr(em_store, "rows", None), "template": args.template,
                       "store": type(em_store).__name__,
                       "store_disk": em_store.seg.stats() if hasattr(em_store, "seg") else None,
                       "alt_ids": args.alt_ids, "p_unregistered": args.p_unregistered,

@@ -161,7 +161,7 @@ def history(assignment, start):
     events = eb.for_assignment(assignment)
     events.persist_measurements(mx)
     for alert in events.persist_alerts(alerts):
-        if getattr(alert.level, "value", alert.level) == "Critical":
+        if alert.level == "Critical":             # AlertLevel is a str enum
             db.persist(db.new_device_alarm(assignment, alert.message).with_triggering_event_id(alert.id))
     # location track: a random walk that stays inside the work area
     t = start - int(rnd.random() * 60000)
