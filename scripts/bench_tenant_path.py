@@ -49,6 +49,11 @@ def main():
     import numpy as np
 
     from sitewhere_amd.assembly import SiteWhereInstance
+    # a fresh data directory per run: a durable store left by an earlier run would be resumed
+    # (its alternate ids seed the dedup filter, so the same synthetic batches read as replays)
+    if not os.environ.get("SITEWHERE_DATA_DIR"):
+        import tempfile
+        os.environ["SITEWHERE_DATA_DIR"] = tempfile.mkdtemp(prefix="sw-tenant-bench-")
     from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
 
     numa_node = None

@@ -111,9 +111,11 @@ TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
     storage="durable", publishEnriched="batches",
     capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
               "dedup_slots": 1 << 21, "gen_cap": 32768,
-              # store-backed dedup beyond the window: 2^28 bits (32 MB) ~ 32 bits for each of 8M stored
-              # ids (size it to the retention: 4 bytes per id kept)
-              "dedup_bloom_bits": 1 << 28})
+              # store-backed dedup beyond the window: 2^32 bits (512 MB of HBM), 8 bits per id in
+              # 64-bit blocks -- false positives (each one a per-event store check on the host) stay
+              # below 1e-6 up to ~60M stored ids and below 1e-3 up to ~300M (check_dedup_sizing
+              # warns past 16 bits per id); a tenant that keeps more raises it
+              "dedup_bloom_bits": 1 << 32})
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
     "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
                   "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}
