@@ -727,7 +727,7 @@ struct DedupCounts {
   uint32_t fresh, over, lose;
 };
 
-// Claim the id's slot in `cur` (fused into k_lookup: the record is already in registers).  Returns
+// Claim the id's slot in `cur` (k_dedup_claim, after k_lookup validated the record).  Returns
 // the id's provisional status: DUPLICATE (held by `prev`), RECHECK (first claim, maybe stored
 // before -- records decoded on another rank skip the filter: their payload, a recheck's input, is
 // there) or OK.
@@ -762,10 +762,6 @@ __device__ __forceinline__ uint8_t dedup_claim(const SwEngineArgs& a, ull h, int
 // One probe of the packed registry resolves device AND active assignment; names of every
 // decodable event are interned here too (fused: one pass over the records).
 __global__ void k_lookup(SwEngineArgs a) {
-  __shared__ uint32_t blk_new, blk_over, blk_lose;
-  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; blk_lose = 0; }
-  __syncthreads();
-  DedupCounts dc = {0u, 0u, 0u};
   // world == 1: the work batch is the decoded batch, clamped (every block derives the same count;
   // block 0 stores it for the kernels after this one)
   const uint32_t n = a.world == 1 ? (*a.n_recs < (uint32_t)a.rec_cap ? *a.n_recs : (uint32_t)a.rec_cap) : *a.n_work;
@@ -807,12 +803,29 @@ __global__ void k_lookup(SwEngineArgs a) {
       else if (dev < 0) st = SW_ST_UNREGISTERED;
       else st = asg >= 0 ? SW_ST_OK : SW_ST_UNASSIGNED;
       if (st == SW_ST_OK && nh) intern_insert((ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, nh);
-      const ull ah = recs[i].alt_hash;
-      if (st == SW_ST_OK && ah) st = dedup_claim(a, ah, i, recs[i].src_rank, dc);   // fused dedup claim
     }
     a.status[i] = st;
     a.ev_dev[i] = dev;
     a.ev_asg[i] = asg;
+  }
+}
+
+// The dedup claims of the step's validated records.  A kernel of its own: fused into k_lookup the
+// three dependent round trips per id (registry probe, `prev` probe, CAS) ran 255 us per 1M ids
+// against 48 + 143 us as two kernels (profiles/r4_fused_claim).
+__global__ void k_dedup_claim(SwEngineArgs a) {
+  __shared__ uint32_t blk_new, blk_over, blk_lose;
+  if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; blk_lose = 0; }
+  __syncthreads();
+  DedupCounts dc = {0u, 0u, 0u};
+  const uint32_t n = *a.n_work;
+  const SwEventRec* __restrict__ recs = a.work;
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
+    if (a.status[i] != SW_ST_OK) continue;
+    const ull ah = recs[i].alt_hash;
+    if (!ah) continue;
+    const uint8_t st = dedup_claim(a, ah, i, recs[i].src_rank, dc);
+    if (st != SW_ST_OK) a.status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
   // same-address atomics per step serialised the kernel, profiles/r3_dedup)
@@ -1583,7 +1596,8 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int g = grid_for(a.rec_cap);
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
   if (2 * ntiles > a.scan_tmp_len) return -4;
-  k_lookup<<<g, BLK, 0, s>>>(a);         // + the dedup claim; the phase's resets (block 0)
+  k_lookup<<<g, BLK, 0, s>>>(a);         // + the phase's resets (block 0)
+  k_dedup_claim<<<g, BLK, 0, s>>>(a);
   // stable split ok / rejected, with the dedup verdicts
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
                                                (const ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
