@@ -38,23 +38,161 @@ def parse_period_ms(s) -> int:
     return ((d * 24 + h) * 60 + mi) * 60_000 + se * 1000
 
 
+class _EngineStates:
+    """Device state of one engine incarnation's enriched batches, column-wise: per assignment index
+    the last interaction and, per state slot ((event type, name id): last location, last value of
+    each measurement name, last alert of each type), the newest (event date, event id).  A batch
+    merges with numpy only; DeviceState objects are written when a read needs them (``dirty``)."""
+
+    def __init__(self, boot: int, header: dict):
+        import numpy as np
+        self.boot, self.world, self.rank = boot, int(header.get("world", 1)), int(header.get("rank", 0))
+        self.n = 0
+        self.last = np.zeros(0, np.int64)
+        self.dirty = np.zeros(0, bool)
+        self.slots: dict[tuple, list] = {}      # (etype, name id) -> [date int64[n], eid + 1 int64[n]]
+        self.ctx: dict = {}                      # assignment index -> context list (reader dictionary)
+        self.names: dict = {}                    # name id -> name
+
+    def _grow(self, m: int):
+        import numpy as np
+        if m <= self.n:
+            return
+        m = max(m, 2 * self.n, 1024)
+        pad = m - self.n
+        self.last = np.concatenate([self.last, np.zeros(pad, np.int64)])
+        self.dirty = np.concatenate([self.dirty, np.zeros(pad, bool)])
+        for v in self.slots.values():
+            v[0] = np.concatenate([v[0], np.full(pad, -1, np.int64)])
+            v[1] = np.concatenate([v[1], np.zeros(pad, np.int64)])
+        self.n = m
+
+    def merge(self, cols: dict):
+        """Newest (date, event id) per slot wins -- DeviceStateManagement.merge_event's rule."""
+        import numpy as np
+        from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT
+        self.ctx, self.names = cols.get("asg_ctx") or self.ctx, cols.get("names") or self.names
+        et = np.asarray(cols["etype"])
+        rows = np.flatnonzero((et == EV_MEASUREMENT) | (et == EV_LOCATION) | (et == EV_ALERT))
+        if not len(rows):
+            return
+        h = cols["header"]
+        asg = np.asarray(cols["asg"])[rows].astype(np.int64)
+        keep = asg >= 0
+        rows, asg = rows[keep], asg[keep]
+        if not len(rows):
+            return
+        self._grow(int(asg.max()) + 1)
+        ets = et[rows].astype(np.int64)
+        name = np.where(ets == EV_LOCATION, 0xffff, np.asarray(cols["name"])[rows].astype(np.int64))
+        date = np.asarray(cols["date"])[rows].astype(np.int64)
+        eid1 = (int(h["first_seq"]) + int(cols.get("row0", 0)) + rows.astype(np.int64)) * self.world + self.rank + 1
+        slot = (ets << 16) | name
+        # the newest row per (slot, assignment) of this batch: sort by key, date, then row order
+        key = (slot << 32) | asg
+        order = np.lexsort((rows, date, key))
+        k = key[order]
+        last = np.ones(len(k), bool)
+        last[:-1] = k[1:] != k[:-1]
+        sel = order[last]
+        recv = int(h.get("recv_ms") or now_ms())
+        touched = np.unique(asg)
+        self.last[touched] = np.maximum(self.last[touched], recv)
+        self.dirty[touched] = True
+        for s in np.unique(slot[sel]).tolist():
+            g = sel[slot[sel] == s]
+            t = self.slots.get((s >> 16, s & 0xffff))
+            if t is None:
+                t = self.slots[(s >> 16, s & 0xffff)] = [np.full(self.n, -1, np.int64), np.zeros(self.n, np.int64)]
+            a, d, e = asg[g], date[g], eid1[g]
+            up = (d > t[0][a]) | ((d == t[0][a]) & (e > t[1][a]))
+            t[0][a[up]] = d[up]
+            t[1][a[up]] = e[up]
+
+    def event_id(self, eid1: int) -> str:
+        return f"{self.boot:x}-{int(eid1) - 1}"
+
+
 class DeviceStateManagement:
     def __init__(self, store=None):
         self.states = Crud(store or create_store("memory"), "deviceStates", DeviceState, ErrorCode.InvalidDeviceStateId,
                            ("token", "device_assignment_id"))
         self._lock = threading.RLock()
         self._dates: dict[str, dict] = {}   # assignment -> {slot: event date}
+        self._engine: dict[int, _EngineStates] = {}   # engine incarnation -> column-wise states
 
     def create_device_state(self, request: dict) -> DeviceState:
         return self.states.create(request)
 
     def get_device_state(self, id: str):
+        self._sync()
         return self.states.get(id)
 
     def get_device_state_by_device_assignment_id(self, assignment_id: str):
+        self._sync()
         return self.states.s.get_by(self.states.c, "device_assignment_id", assignment_id)
 
+    # ---- engine batches ----------------------------------------------------------------
+    def merge_batch(self, cols: dict):
+        """An engine tenant's enriched batch (decoded block + dictionaries, EnrichedBatchReader):
+        merged column-wise; the affected states are written on the next read."""
+        b = int(cols["header"]["boot"])
+        with self._lock:
+            t = self._engine.get(b)
+            if t is None:
+                t = self._engine[b] = _EngineStates(b, cols["header"])
+            t.merge(cols)
+
+    def _sync(self):
+        """Write the states engine batches changed since the last read (merge_event's slot rule
+        against what the per-event path stored)."""
+        import numpy as np
+        from ..models.columnar import EV_ALERT, EV_LOCATION
+        with self._lock:
+            for t in self._engine.values():
+                idx = np.flatnonzero(t.dirty)
+                if not len(idx):
+                    continue
+                t.dirty[idx] = False
+                for i in idx.tolist():
+                    ctx = t.ctx.get(i)
+                    if not ctx:
+                        continue
+                    aid = ctx[0]
+                    st = self.states.s.get_by(self.states.c, "device_assignment_id", aid)
+                    if st is None:
+                        st = self.states.create({}, device_assignment_id=aid)
+                    st.device_id = ctx[1] if len(ctx) > 1 else st.device_id
+                    st.customer_id, st.area_id, st.asset_id = (ctx[2], ctx[3], ctx[4]) if len(ctx) > 4 else \
+                        (st.customer_id, st.area_id, st.asset_id)
+                    if len(ctx) > 6:
+                        st.device_type_id = ctx[6]
+                    st.last_interaction_date = max(st.last_interaction_date or 0, int(t.last[i]))
+                    st.presence_missing_date = None
+                    dates = self._dates.setdefault(aid, {})
+                    for (et, nid), (dv, ev) in t.slots.items():
+                        if ev[i] == 0:
+                            continue
+                        d = int(dv[i])
+                        if et == EV_LOCATION:
+                            key = "location"
+                        else:
+                            nm = t.names.get(nid, "")
+                            key = ("alert:" if et == EV_ALERT else "mx:") + nm
+                        if d < dates.get(key, -1):
+                            continue
+                        dates[key] = d
+                        eid = t.event_id(int(ev[i]))
+                        if et == EV_LOCATION:
+                            st.last_location_event_id = eid
+                        elif et == EV_ALERT:
+                            st.last_alert_event_ids[t.names.get(nid, "")] = eid
+                        else:
+                            st.last_measurement_event_ids[t.names.get(nid, "")] = eid
+                    self.states.put(st)
+
     def search_device_states(self, criteria=None) -> SearchResults:
+        self._sync()
         c = criteria or {}
         before = c.get("lastInteractionDateBefore") if isinstance(c, dict) else None
         sets = {k: set(c.get(k) or []) for k in ("deviceTypeIds", "customerIds", "areaIds", "assetIds")} if isinstance(c, dict) else {}
@@ -110,6 +248,7 @@ class DeviceStateManagement:
             return self.states.put(st)
 
     def find_missing(self, now_ms_: int, missing_ms: int) -> list[DeviceState]:
+        self._sync()
         limit = now_ms_ - missing_ms
         return self.states.query(lambda s: s.last_interaction_date is not None and s.last_interaction_date < limit
                                  and s.presence_missing_date is None)
@@ -186,10 +325,9 @@ class DeviceStateTenantEngine(MicroserviceTenantEngine):
         from .enriched_batches import is_batch
         for r in recs:
             if is_batch(r.value):
-                # an engine batch: only the newest row of each state slot can change the state
-                cols = self.reader.columns(r.value)
-                for i in latest_state_rows(cols):
-                    self.management.merge_event(self.reader.event(cols, i), self.reader.context(cols, i))
+                # an engine batch: merged column-wise (numpy, no per-event objects); states are
+                # materialized when read
+                self.management.merge_batch(self.reader.columns(r.value))
                 continue
             ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
             self.management.merge_event(ev, ctx)
