@@ -731,22 +731,45 @@ struct DedupCounts {
 // the id's provisional status: DUPLICATE (held by `prev`), RECHECK (first claim, maybe stored
 // before -- records decoded on another rank skip the filter: their payload, a recheck's input, is
 // there) or OK.
-__device__ __forceinline__ uint8_t dedup_claim(const SwEngineArgs& a, ull h, int64_t i, uint8_t src_rank,
+// Everything a claim needs, read once per thread (not per id: loads through the by-value engine
+// arguments cannot be hoisted past the claim's stores).
+struct DedupClaim {
+  ull* __restrict__ ct;                      // live generation
+  const ull* __restrict__ pt;                // retired generation
+  int64_t mask;
+  ull sb;                                    // the step's first sequence
+  const ull* __restrict__ bloom;
+  int64_t bmask;
+  uint8_t rank;
+};
+
+__device__ __forceinline__ DedupClaim dedup_claim_args(const SwEngineArgs& a) {
+  DedupClaim d;
+  const int64_t slots = a.dd_mask + 1, g = a.dd_meta[0];
+  d.ct = (ull*)a.dd_key + 2 * g * slots;
+  d.pt = (const ull*)a.dd_key + 2 * (1 - g) * slots;
+  d.mask = a.dd_mask;
+  d.sb = (ull)*a.seq_base;
+  d.bloom = (const ull*)a.dd_bloom;
+  d.bmask = a.dd_bloom_mask;
+  d.rank = (uint8_t)a.rank;
+  return d;
+}
+
+__device__ __forceinline__ uint8_t dedup_claim(const DedupClaim& dc, ull h, int64_t i, uint8_t src_rank,
                                                DedupCounts& c) {
-  const int64_t mask = a.dd_mask, slots = mask + 1;
-  const int64_t g = a.dd_meta[0];
-  ull* ct = (ull*)a.dd_key + 2 * g * slots;
-  const ull* pt = (const ull*)a.dd_key + 2 * (1 - g) * slots;
-  if (dd_find(pt, mask, h)) return SW_ST_DUPLICATE;
-  const ull sb = (ull)*a.seq_base;
+  const int64_t mask = dc.mask;
+  ull* __restrict__ ct = dc.ct;
+  if (dd_find(dc.pt, mask, h)) return SW_ST_DUPLICATE;
+  const ull sb = dc.sb;
   int64_t slot = (int64_t)(h & (ull)mask);
   for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
     const ull old = atomicCAS(&ct[2 * slot], 0ull, h);
     if (old == 0) {
       ++c.fresh;
       reinterpret_cast<uint32_t*>(&ct[2 * slot + 1])[0] = (uint32_t)(sb + (ull)i);
-      return (a.dd_bloom && src_rank == (uint8_t)a.rank && bloom_has((const ull*)a.dd_bloom, a.dd_bloom_mask, h))
-                 ? (uint8_t)SW_ST_RECHECK : (uint8_t)SW_ST_OK;
+      return (dc.bloom && src_rank == dc.rank && bloom_has(dc.bloom, dc.bmask, h)) ? (uint8_t)SW_ST_RECHECK
+                                                                                     : (uint8_t)SW_ST_OK;
     }
     if (old == h) {
       atomicMin(reinterpret_cast<uint32_t*>(&ct[2 * slot + 1]) + 1, (uint32_t)i);
@@ -818,14 +841,16 @@ __global__ void k_dedup_claim(SwEngineArgs a) {
   if (threadIdx.x == 0) { blk_new = 0; blk_over = 0; blk_lose = 0; }
   __syncthreads();
   DedupCounts dc = {0u, 0u, 0u};
+  const DedupClaim d = dedup_claim_args(a);
   const uint32_t n = *a.n_work;
   const SwEventRec* __restrict__ recs = a.work;
+  uint8_t* __restrict__ status = a.status;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
-    if (a.status[i] != SW_ST_OK) continue;
+    if (status[i] != SW_ST_OK) continue;
     const ull ah = recs[i].alt_hash;
     if (!ah) continue;
-    const uint8_t st = dedup_claim(a, ah, i, recs[i].src_rank, dc);
-    if (st != SW_ST_OK) a.status[i] = st;
+    const uint8_t st = dedup_claim(d, ah, i, recs[i].src_rank, dc);
+    if (st != SW_ST_OK) status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
   // same-address atomics per step serialised the kernel, profiles/r3_dedup)

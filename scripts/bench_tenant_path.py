@@ -21,6 +21,49 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
+class _StackSampler:
+    """SW_SAMPLE_STACKS=1: every 2 ms, the innermost frames of every Python thread (a sampling
+    profiler without extra packages); the report goes to stderr, busiest (thread, frames) first."""
+
+    IDLE = {"wait", "get", "_wait_for_tstate_lock", "select", "poll", "sleep", "accept", "recv", "_worker"}
+
+    def __init__(self, period_s: float = 0.002, depth: int = 4):
+        import collections
+        import threading
+        self.counts = collections.Counter()
+        self.samples = 0
+        self._stop = threading.Event()
+        self._depth = depth
+        self._t = threading.Thread(target=self._run, args=(period_s,), daemon=True)
+        self._t.start()
+
+    def _run(self, period_s):
+        import threading
+        me = threading.get_ident()
+        names = {}
+        while not self._stop.wait(period_s):
+            names.update({t.ident: t.name for t in threading.enumerate()})
+            for tid, f in sys._current_frames().items():
+                if tid == me:
+                    continue
+                if f.f_code.co_name in self.IDLE:
+                    continue                  # a thread waiting (lock, queue, event, sleep)
+                stack = []
+                while f is not None and len(stack) < self._depth:
+                    stack.append(f"{os.path.basename(f.f_code.co_filename)}:{f.f_code.co_name}:{f.f_lineno}")
+                    f = f.f_back
+                self.counts[(names.get(tid, str(tid)), " < ".join(stack))] += 1
+            self.samples += 1
+
+    def report(self, top: int = 40):
+        self._stop.set()
+        self._t.join()
+        print(f"stack samples: {self.samples}", file=sys.stderr)
+        for (name, stack), n in self.counts.most_common(top):
+            print(f"{n:6d} {100.0 * n / max(1, self.samples):5.1f}% [{name}] {stack}", file=sys.stderr)
+        print("(share of samples in which that thread sat in that code; waiting threads are left out)", file=sys.stderr)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--devices", type=int, default=20000)
@@ -144,9 +187,12 @@ def main():
         ib.flush()
         base = ib.persisted_events.count
         ev0 = ib.processed_events.count
+        sampler = _StackSampler() if os.environ.get("SW_SAMPLE_STACKS") == "1" else None
         t = time.perf_counter()
         pump(args.batches, args.warmup)
         dt = time.perf_counter() - t
+        if sampler is not None:
+            sampler.report()
         ev = ib.processed_events.count - ev0
     else:
         for k in range(args.warmup):
