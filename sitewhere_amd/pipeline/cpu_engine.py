@@ -275,6 +275,7 @@ class CpuInboundEngine(EngineBase):
     def reset_dedup(self):
         """Forget the alternate-id window (both generations); the store-backed filter stays."""
         self.dedup, self.dedup_prev = {}, {}
+        self.dedup_valid_from = self.cursor           # the window holds no id of the rows before
 
     def _bloom_pos(self, h: int):
         blk = mix64(h ^ 0x5bd1e9955bd1e995) & self.bloom_mask

@@ -327,6 +327,7 @@ class EngineBase:
 
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "base"
+    dedup_valid_from = 0          # store sequence from which the dedup window saw every row's id
 
     def checkpoint_state(self, include_store: bool = False) -> dict:
         """Engine tables to snapshot (name -> numpy array); see ``pipeline/checkpoint.py``."""

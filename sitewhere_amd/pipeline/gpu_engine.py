@@ -1315,6 +1315,7 @@ class GpuInboundEngine(EngineBase):
         return m
 
     def reset_dedup(self):
+        self.dedup_valid_from = self.cursor           # the window holds no id of the rows before
         self.t["dd_tab"][:, 0] = 0
         self.t["dd_tab"][:, 1] = -1
         self.t["dd_meta"].copy_(torch.from_numpy(self._armed_dedup_meta(np.zeros(4, np.int64), self.cfg)))

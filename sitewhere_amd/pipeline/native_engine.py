@@ -105,6 +105,7 @@ class NativeCpuEngine(CpuInboundEngine):
 
     def reset_dedup(self):
         """Forget the alternate-id window (both generations); the store-backed filter stays."""
+        self.dedup_valid_from = self.cursor           # the window holds no id of the rows before
         z64, zi = np.zeros(1, np.uint64), np.zeros(1, np.int64)
         self._lib.swce_dedup_import(self._h, _ptr(z64), _ptr(zi), 0)
         self._lib.swce_dedup_prev_import(self._h, _ptr(z64), _ptr(zi), 0)

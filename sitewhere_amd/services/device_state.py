@@ -51,6 +51,8 @@ class _EngineStates:
         self.last = np.zeros(0, np.int64)
         self.dirty = np.zeros(0, bool)
         self.slots: dict[tuple, list] = {}      # (etype, name id) -> [date int64[n], eid + 1 int64[n]]
+        self._slot_lut = np.full(3 << 16, -1, np.int64)   # (etype << 16 | name id) -> dense slot number
+        self._slot_keys: list[tuple] = []
         self.ctx: dict = {}                      # assignment index -> context list (reader dictionary)
         self.names: dict = {}                    # name id -> name
 
@@ -88,22 +90,41 @@ class _EngineStates:
         date = np.asarray(cols["date"])[rows].astype(np.int64)
         eid1 = (int(h["first_seq"]) + int(cols.get("row0", 0)) + rows.astype(np.int64)) * self.world + self.rank + 1
         slot = (ets << 16) | name
-        # the newest row per (slot, assignment) of this batch: sort by key, date, then row order
-        key = (slot << 32) | asg
-        order = np.lexsort((rows, date, key))
-        k = key[order]
-        last = np.ones(len(k), bool)
-        last[:-1] = k[1:] != k[:-1]
-        sel = order[last]
+        # dense slot numbers through a lookup table (no sort over the batch)
+        lut = self._slot_lut
+        new = np.unique(slot[lut[slot] < 0]) if (lut[slot] < 0).any() else ()
+        for s in np.asarray(new).tolist():
+            lut[s] = len(self._slot_keys)
+            self._slot_keys.append((s >> 16, s & 0xffff))
+            self.slots[(s >> 16, s & 0xffff)] = [np.full(self.n, -1, np.int64), np.zeros(self.n, np.int64)]
+        sid = lut[slot]
+        # the newest row per (slot, assignment): one max over (date, row) packed in an int64 (dates of
+        # a batch span far less than 2^31 ms; rows < 2^32), per dense (slot, assignment) cell
+        base = int(date.min())
+        span = date - base
+        cells = len(self._slot_keys) * self.n
+        if int(span.max()) >= 1 << 31 or cells > max(1 << 24, 4 * len(rows)):   # sort instead
+            order = np.lexsort((rows, date, sid * self.n + asg))
+            k = (sid * self.n + asg)[order]
+            lastm = np.ones(len(k), bool)
+            lastm[:-1] = k[1:] != k[:-1]
+            win = order[lastm]
+        else:
+            cell = sid * self.n + asg
+            best = np.full(len(self._slot_keys) * self.n, -1, np.int64)
+            np.maximum.at(best, cell, (span << 32) | np.arange(len(rows), dtype=np.int64))
+            hit = best[best >= 0]
+            win = (hit & 0xffffffff).astype(np.int64)
         recv = int(h.get("recv_ms") or now_ms())
-        touched = np.unique(asg)
+        mark = np.zeros(self.n, bool)
+        mark[asg] = True
+        touched = np.flatnonzero(mark)
         self.last[touched] = np.maximum(self.last[touched], recv)
         self.dirty[touched] = True
-        for s in np.unique(slot[sel]).tolist():
-            g = sel[slot[sel] == s]
-            t = self.slots.get((s >> 16, s & 0xffff))
-            if t is None:
-                t = self.slots[(s >> 16, s & 0xffff)] = [np.full(self.n, -1, np.int64), np.zeros(self.n, np.int64)]
+        ws = sid[win]
+        for j in np.flatnonzero(np.bincount(ws, minlength=len(self._slot_keys))).tolist():
+            g = win[ws == j]
+            t = self.slots[self._slot_keys[j]]
             a, d, e = asg[g], date[g], eid1[g]
             up = (d > t[0][a]) | ((d == t[0][a]) & (e > t[1][a]))
             t[0][a[up]] = d[up]

@@ -157,14 +157,17 @@ class DeviceEventManagement:
             return b""
         return b"".join(np.ascontiguousarray(c, np.uint64).tobytes() for c in f(max_ids))
 
-    def durable_find_alternate_hashes(self, hashes: bytes) -> bytes:
+    def durable_find_alternate_hashes(self, hashes: bytes, covered: list | None = None) -> bytes:
         """Which of these alternate-id hashes (u64 little endian) the durable store holds: the engine
-        tenant settles the ids its store-backed filter sent back with one lookup per step."""
+        tenant settles the ids its store-backed filter sent back with one lookup per step.
+        ``covered`` = [boot, rank, sequence]: the engine's dedup window holds every id of its rows
+        from that sequence on (see ``DurableEventStore.find_alternate_hashes``)."""
         f = getattr(self.store, "find_alternate_hashes", None)
         h = np.frombuffer(hashes, np.uint64)
         if f is None or not len(h):
             return b""
-        return np.array(sorted(f(h.tolist())), np.uint64).tobytes()
+        found = f(h.tolist(), tuple(int(x) for x in covered)) if covered else f(h.tolist())
+        return np.array(sorted(found), np.uint64).tobytes()
 
     def add_durable_batch(self, payload) -> tuple[int, int]:
         """Queue an engine tenant's durable batch: (rows, token).  The rows are on disk once

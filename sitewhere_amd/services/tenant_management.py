@@ -110,7 +110,9 @@ TENANT_TEMPLATES["gpu-columnar"]["name"] = "MI355X pipeline, columnar event stor
 TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
     storage="durable", publishEnriched="batches",
     capacity={"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
-              "dedup_slots": 1 << 21, "gen_cap": 32768,
+              # alternate-id window: 2^24 slots (512 MB of HBM) hold the last 6-8M ids, so a recheck
+              # never scans the blocks the store has not indexed yet
+              "dedup_slots": 1 << 24, "gen_cap": 32768,
               # store-backed dedup beyond the window: 2^32 bits (512 MB of HBM), 8 bits per id in
               # 64-bit blocks -- false positives (each one a per-event store check on the host) stay
               # below 1e-6 up to ~60M stored ids and below 1e-3 up to ~300M (check_dedup_sizing
