@@ -1082,19 +1082,21 @@ class DurableEventStore(DeviceEventStore):
         rows = np.nonzero(np.isin(ah, want))[0]
         return ah[rows], rows
 
-    def find_alternate_hashes(self, hashes, covered: tuple | None = None) -> dict:
+    def find_alternate_hashes(self, hashes, covered: tuple | None = None, indexed_only: bool = False) -> dict:
         """alt-id hash -> event id string for the hashes present on disk, the newest event per hash
         (store-backed dedup beyond the engine's window: ``AlternateIdDeduplicator`` asks the event
         store whether the id was ever seen).  ``covered`` = (boot, rank, sequence): that engine's
         dedup window still holds every id of its rows from ``sequence`` on, so its blocks there that
-        are not indexed yet need no scan (the caller asks only about ids the window does not hold)."""
+        are not indexed yet need no scan (the caller asks only about ids the window does not hold).
+        ``indexed_only``: no block scans at all (binary searches of the indexed blocks only)."""
         want = np.unique(np.asarray(list(hashes), np.uint64))
         found = {}
         if not len(want):
             return found
         for e in self.seg.index()[::-1]:                 # newest block first
-            if covered is not None and self._ix.get(self._key(e)) is None and int(e["boot"]) == covered[0] \
-                    and int(e["rank"]) == covered[1] and int(e["first_seq"]) >= covered[2]:
+            unindexed = self._ix.get(self._key(e)) is None
+            if unindexed and (indexed_only or covered is not None and int(e["boot"]) == covered[0]
+                              and int(e["rank"]) == covered[1] and int(e["first_seq"]) >= covered[2]):
                 continue
             hs, rows = self._alt_rows(e, want)
             if len(rows):

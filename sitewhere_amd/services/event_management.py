@@ -157,16 +157,18 @@ class DeviceEventManagement:
             return b""
         return b"".join(np.ascontiguousarray(c, np.uint64).tobytes() for c in f(max_ids))
 
-    def durable_find_alternate_hashes(self, hashes: bytes, covered: list | None = None) -> bytes:
+    def durable_find_alternate_hashes(self, hashes: bytes, covered: list | None = None,
+                                      indexed_only: bool = False) -> bytes:
         """Which of these alternate-id hashes (u64 little endian) the durable store holds: the engine
         tenant settles the ids its store-backed filter sent back with one lookup per step.
         ``covered`` = [boot, rank, sequence]: the engine's dedup window holds every id of its rows
-        from that sequence on (see ``DurableEventStore.find_alternate_hashes``)."""
+        from that sequence on (see ``DurableEventStore.find_alternate_hashes``); ``indexed_only``:
+        look in the blocks the store has indexed, no scans."""
         f = getattr(self.store, "find_alternate_hashes", None)
         h = np.frombuffer(hashes, np.uint64)
         if f is None or not len(h):
             return b""
-        found = f(h.tolist(), tuple(int(x) for x in covered)) if covered else f(h.tolist())
+        found = f(h.tolist(), tuple(int(x) for x in covered) if covered else None, indexed_only=indexed_only)
         return np.array(sorted(found), np.uint64).tobytes()
 
     def add_durable_batch(self, payload) -> tuple[int, int]:

@@ -1026,13 +1026,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if not hasattr(em, "durable_find_alternate_hashes"):
             return st
         h = np.ascontiguousarray(res.rejects["alt_hash"][rk], np.uint64)
-        # the window holds every id claimed by the last dedup_slots/2 - rec_cap persisted rows (one
-        # row has at most one id): blocks that recent, not indexed yet, cannot hold these ids
-        c = self.engine_cfg
-        k = c.dedup_slots // 2 - c.rec_cap
-        covered = [self.block_boot, int(res.rank), max(int(res.first_seq) - k, int(self.engine.dedup_valid_from))] \
-            if k > 0 and res.first_seq is not None else None
-        found = np.frombuffer(em.durable_find_alternate_hashes(h.tobytes(), covered), np.uint64)
+        # indexed blocks only (a binary search each): the raw offsets commit once this step's
+        # rejects are routed, so a scan of the blocks the store has not indexed yet would stall the
+        # whole pipeline.  An id held only by such a block goes on to the per-event path, whose own
+        # store check finds it there: still stored once.
+        found = np.frombuffer(em.durable_find_alternate_hashes(h.tobytes(), indexed_only=True), np.uint64)
         n_dup = 0
         if len(found):
             st = st.copy()

@@ -65,6 +65,10 @@ def test_replay_beyond_the_window_is_a_duplicate(sw):
     first = wire.measurements("galaxytab-002", {"sd.temp": 1.5}, event_date=1_700_000_000_000, alternate_id="sd-old-1")
     es.inject("default-protobuf", first)
     assert wait_until(lambda: len(_measurements(sw, "sd-old-1")) == 1, 30)
+    # the store's background index covers the stored block (the step's settle reads indexed
+    # blocks only; an unindexed one leaves the id to the per-event path's own store check)
+    store = sw.tenant_engine("event-management", "sd").store
+    assert store.index_wait(30)
     # the window forgets everything (what more than dedup_slots / 2 newer ids would do)
     ib.engine.reset_dedup()
     s0 = ib.engine.stats_dict()
