@@ -188,7 +188,7 @@ def main():
         base = ib.persisted_events.count
         ev0 = ib.processed_events.count
         sampler = _StackSampler() if os.environ.get("SW_SAMPLE_STACKS") == "1" else None
-        t = time.perf_counter()
+        t = t_timed = time.perf_counter()
         pump(args.batches, args.warmup)
         dt = time.perf_counter() - t
         if sampler is not None:
@@ -199,7 +199,7 @@ def main():
             ib.process_batch(*batches[k % len(batches)])
         ib.flush()
         base = ib.persisted_events.count
-        t = time.perf_counter()
+        t = t_timed = time.perf_counter()
         ev = 0
         for k in range(args.batches):
             r = ib.process_batch(*batches[(args.warmup + k) % len(batches)])
@@ -221,16 +221,22 @@ def main():
                                                 if not isinstance(x, list) or len(x) < 50][:8], file=sys.stderr)
     trace = None
     if ib.trace:                # SW_TENANT_TRACE=1: medians over the second half of the timed batches
-        tr = [t for t in ib.trace if len(t) == 9][-(args.batches // 2):]
+        # steps submitted inside the timed window only (warmup steps and the first step's set-up
+        # are outside it); medians over its second half, the interval tail over all of it
+        timed = [x for x in ib.trace if len(x) == 9 and x[0] >= t_timed]
+        tr = timed[len(timed) // 2:]
         if tr:
             import numpy as np
             d = np.diff(np.asarray(tr), axis=1) * 1000
-            gap = np.diff(np.asarray([t[0] for t in tr])) * 1000
+            gap = np.diff(np.asarray([x[0] for x in timed])) * 1000
             trace = {"submit_ms": d[:, 0], "to_complete_ms": d[:, 1], "queue_wait_ms": d[:, 2],
                      "payload_lock_ms": d[:, 3], "payload_dicts_ms": d[:, 4], "payload_encode_ms": d[:, 5],
                      "rpc_ms": d[:, 6], "publish_commit_ms": d[:, 7], "submit_interval_ms": gap}
             gap_pct = {f"submit_interval_p{q}_ms": round(float(np.percentile(gap, q)), 3) for q in (90, 99)} \
                 if len(gap) else {}
+            if len(gap):
+                gap_pct["submit_interval_max_ms"] = round(float(gap.max()), 3)
+                gap_pct["timed_steps"] = len(timed)
             trace = {k: round(float(np.median(v)), 3) for k, v in trace.items() if len(v)}
             trace.update(gap_pct)
     breakdown = {name: round(t.hist.snapshot()["mean"], 3)
