@@ -538,6 +538,12 @@ int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, u
       for (uint32_t k = 0; k < m; ++k) flags[r0 + k] = (uint8_t)fl[k];
     for (int c = 0; c < SEG_NCOL; ++c) {
       if (c == SEG_ETYPE || c == SEG_FLAGS) continue;
+      // columns nobody asked for are not unpacked (string lengths only feed the heap)
+      const bool want = c == SEG_LEVEL ? level != nullptr : c == SEG_DATE ? date != nullptr
+                      : c == SEG_ASG ? asg != nullptr : c == SEG_NAME ? name != nullptr
+                      : (c == SEG_MXV || c == SEG_LAT) ? v0 != nullptr : c == SEG_LON ? v1 != nullptr
+                      : c == SEG_ELEV ? v2 != nullptr : str_heap != nullptr;
+      if (!want) continue;
       const SwSegCol& cd = ph.cols[c];
       const uint8_t* words = pg + cd.data_off;
       if (seg_is_double(c)) {
@@ -748,6 +754,27 @@ void swseg_multi_range_u64(const uint64_t* const* keys, const int64_t* lens, int
     const uint64_t* h = std::upper_bound(l, a + lens[i], key);
     lo_out[i] = l - a;
     hi_out[i] = h - a;
+  }
+}
+
+// Bulk form for the store-backed dedup: for each wanted key, the last array (highest i: blocks are
+// in store order, so the newest block) that holds it and the key's last position there; -1 / -1 when
+// no array does.  n_want x n binary searches, no Python per block.
+void swseg_multi_find_u64(const uint64_t* const* keys, const int64_t* lens, int64_t n, const uint64_t* want,
+                          int64_t n_want, int64_t* blk_out, int64_t* pos_out) {
+  for (int64_t j = 0; j < n_want; ++j) {
+    blk_out[j] = pos_out[j] = -1;
+    const uint64_t w = want[j];
+    for (int64_t i = n - 1; i >= 0; --i) {
+      const uint64_t* a = keys[i];
+      if (!a || lens[i] <= 0) continue;
+      const uint64_t* h = std::upper_bound(a, a + lens[i], w);
+      if (h != a && h[-1] == w) {
+        blk_out[j] = i;
+        pos_out[j] = (h - a) - 1;
+        break;
+      }
+    }
   }
 }
 

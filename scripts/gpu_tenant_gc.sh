@@ -1,12 +1,11 @@
 #!/bin/bash
-# Tenant-path tail latency: default GC vs a frozen start-up heap (gc.freeze + higher gen-0
-# threshold), 256K and 1M batches through the raw-payload topic with store retention.
+# 64K-payload tenant path at cap 256K, 1200 batches: default collector vs gc.freeze() after set-up
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O=gpurun_out/${1:-tenant_gc}
-cd "$R" && mkdir -p $O
-for b in 262144 1048576; do
-  n=$(( b == 262144 ? 120 : 60 ))
-  for g in default freeze; do
-    SW_TENANT_TRACE=1 timeout -k 10 400 python scripts/bench_tenant_path.py --devices 20000 --batch $b --batches $n --max-msgs $b --via-bus --store-retention $(( 8 * b )) --gc $g > $O/${g}_$b.log 2>&1 && tail -1 $O/${g}_$b.log | cut -c1-200 || exit 1
-  done
+O="$R/gpurun_out/${1:-tenant_gc}"
+mkdir -p "$O" && cd "$R" && export TMPDIR=/tmp
+for GC in freeze default; do
+  SW_TENANT_TRACE=1 timeout -k 10 400 python -u scripts/bench_tenant_path.py --devices 50000 --batch 65536 --batches 1200 \
+    --warmup 4 --via-bus --max-msgs 262144 --gc $GC > "$O/tenant_cap262144_gc_${GC}.log" 2>&1 \
+    || { tail -20 "$O/tenant_cap262144_gc_${GC}.log"; exit 1; }
+  tail -1 "$O/tenant_cap262144_gc_${GC}.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["gc"], round(d["events_per_sec"]/1e6,1), "M/s", d["ms_per_batch"], "ms/batch", d["engine_steps"], "steps", d["routed_payloads"], "routed", d.get("median_ms_second_half"))'
 done

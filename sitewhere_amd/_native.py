@@ -187,6 +187,7 @@ def native():
         _proto(lib, "swseg_page_summary", c_int64, P, P)
         _proto(lib, "swseg_index_block", c_int64, P, c_int64, P, P, P, P, P, P)
         _proto(lib, "swseg_multi_range_u64", None, P, P, c_int64, c_uint64, P, P)
+        _proto(lib, "swseg_multi_find_u64", None, P, P, c_int64, P, c_int64, P, P)
         _proto(lib, "swseg_multi_range_u32", None, P, P, P, P, c_int64, ctypes.c_uint32, c_int64, c_int64, P, P)
         _proto(lib, "swseg_dates", None, P, P, P)
         _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)

@@ -1093,18 +1093,46 @@ class DurableEventStore(DeviceEventStore):
         found = {}
         if not len(want):
             return found
-        for e in self.seg.index()[::-1]:                 # newest block first
-            unindexed = self._ix.get(self._key(e)) is None
-            if unindexed and (indexed_only or covered is not None and int(e["boot"]) == covered[0]
-                              and int(e["rank"]) == covered[1] and int(e["first_seq"]) >= covered[2]):
-                continue
-            hs, rows = self._alt_rows(e, want)
-            if len(rows):
-                eids = self._eids(e, rows)
-                for hv, eid in sorted(zip(hs.tolist(), eids.tolist()), key=lambda t: -t[1]):
-                    found.setdefault(int(hv), f"{int(e['boot']):x}-{int(eid)}")
-                if len(found) == len(want):
-                    break
+        ents = self.seg.index()
+        order: dict = {}
+        best: dict[int, tuple] = {}                      # hash -> (store position, event id, boot)
+
+        def store_pos(e) -> int:                         # built on the first hit only
+            if not order:
+                order.update({self._key(x): k for k, x in enumerate(ents)})
+            return order.get(self._key(e), -1)
+
+        def offer(hv, pos, eid, boot):
+            cur = best.get(hv)
+            if cur is None or (pos, eid) > cur[:2]:
+                best[hv] = (pos, eid, boot)
+
+        # indexed blocks: one native pass per boot over every block's sorted hashes (the newest
+        # block holding each id), instead of a search per block in Python
+        lib = native()
+        blk, at = np.empty(len(want), np.int64), np.empty(len(want), np.int64)
+        indexed = set()
+        for tab in self._tables().values():
+            indexed |= tab["keys"]
+            lib.swseg_multi_find_u64(tab["ah"], _p(tab["nah"]), tab["n"], _p(want), len(want), _p(blk), _p(at))
+            for j in np.nonzero(blk >= 0)[0].tolist():
+                e = tab["ents"][int(blk[j])]
+                row = int(tab["ixs"][int(blk[j])].ar[int(at[j])])
+                offer(int(want[j]), store_pos(e), int(self._eids(e, [row])[0]), int(e["boot"]))
+        if not indexed_only:
+            for k in range(len(ents) - 1, -1, -1):       # blocks not indexed yet: scanned, newest first
+                e = ents[k]
+                if self._key(e) in indexed or self._ix.get(self._key(e)) is not None:
+                    continue
+                if covered is not None and int(e["boot"]) == covered[0] and int(e["rank"]) == covered[1] \
+                        and int(e["first_seq"]) >= covered[2]:
+                    continue
+                hs, rows = self._alt_rows(e, want)
+                if len(rows):
+                    for hv, eid in zip(hs.tolist(), self._eids(e, rows).tolist()):
+                        offer(int(hv), k, int(eid), int(e["boot"]))
+        for hv, (_, eid, boot) in best.items():
+            found[hv] = f"{boot:x}-{eid}"
         return found
 
     def get_event_by_alternate_id(self, alt: str):

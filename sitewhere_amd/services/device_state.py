@@ -348,7 +348,7 @@ class DeviceStateTenantEngine(MicroserviceTenantEngine):
             if is_batch(r.value):
                 # an engine batch: merged column-wise (numpy, no per-event objects); states are
                 # materialized when read
-                self.management.merge_batch(self.reader.columns(r.value))
+                self.management.merge_batch(self.reader.columns(r.value, strings=False))   # slots, dates, ids only
                 continue
             ev, ctx, _ = payloads.decode_enriched(r.value, r.key)
             self.management.merge_event(ev, ctx)

@@ -68,14 +68,17 @@ class EnrichedBatchReader:
         self._apply(boot, got)
 
     # ------------------------------------------------------------------ batches
-    def columns(self, value) -> dict:
+    def columns(self, value, strings: bool = True) -> dict:
         """Decoded block of a batch record with its dictionaries current: block columns + header
         (see ``persistence.segments.decode_block``) and ``cols["asg_ctx"]`` / ``["names"]`` /
-        ``["rules"]`` for :func:`~sitewhere_amd.persistence.segments.materialize_row`."""
+        ``["rules"]`` for :func:`~sitewhere_amd.persistence.segments.materialize_row`.  A consumer
+        that reads no alternate id, message or metadata passes ``strings=False`` (the string heap
+        is not decoded; ``cols["str_heap"]`` is None)."""
         buf = memoryview(value).cast("B") if not isinstance(value, (bytes, bytearray)) else value
         if bytes(buf[:4]) == b"SWD1":
             d, blk = sg.decode_durable_batch(value)
-            cols = sg.decode_block(np.ascontiguousarray(blk), check=isinstance(value, (bytes, bytearray)))
+            cols = sg.decode_block(np.ascontiguousarray(blk), strings=strings,
+                                   check=isinstance(value, (bytes, bytearray)))
             boot = int(cols["header"]["boot"])
         else:
             from ..persistence.columnar import decode_batch

@@ -97,6 +97,11 @@ def check_roundtrip(rows, recs, spans, raw):
     want = expected_strings(recs, spans, raw)
     for i in range(len(rows)):
         assert sg.row_strings(c, i) == want[i], i
+    # without strings: the same columns (the string-length columns are skipped), no heap
+    c2 = sg.decode_block(blk, strings=False)
+    assert c2["str_heap"] is None
+    for col in ("etype", "level", "date", "asg", "name", "v0", "v1", "v2", "flags"):
+        np.testing.assert_array_equal(c2[col].view(np.uint8), c[col].view(np.uint8), err_msg=col)
     return blk
 
 
@@ -406,6 +411,7 @@ def test_block_indexes_answer_like_the_scan(tmp_path):
     es._ix_stop.set()
     es._ix_thread.join(10)
     es._ix.clear()
+    es._ix_tabs = None                  # the native multi-block tables go with the indexes
     scanned = answers()
     assert indexed == scanned
     assert sum(x[0] for x in indexed[:len(queries) * len(crits)]) > 2000
