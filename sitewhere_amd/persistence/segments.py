@@ -652,6 +652,11 @@ class DurableEventStore(DeviceEventStore):
         self.cache_blocks = cache_blocks
         self._pages: OrderedDict = OrderedDict()       # (file, offset, page) -> decoded page columns
         self.cache_pages = 256
+        # alternate-id hashes of blocks not indexed yet (8 B per row, bounded by rows): the per-event
+        # path's store check scans them; kept apart from the decoded-block cache so it neither
+        # evicts query blocks nor re-reads a block per lookup while the indexer catches up
+        self._alt_cache: OrderedDict = OrderedDict()
+        self.alt_cache_rows = 1 << 25
         self.skipped_rows = 0
         # per-block indexes (postings by assignment + type, alternate-id hashes), built in the
         # background as blocks land and kept as memory-mapped sidecar files (see BlockIndex)
@@ -851,12 +856,19 @@ class DurableEventStore(DeviceEventStore):
                 if not todo:
                     self._ix_stop.wait(0.05)
                     continue
-                for e, ix in zip(todo, pool.map(self._safe_index_one, todo)):
+                # each index goes live as soon as it is built (not when the whole batch is): a
+                # lagging index sends store checks to block scans
+                from concurrent.futures import as_completed
+                futs = {pool.submit(self._safe_index_one, e): e for e in todo[:4 * self.index_threads]}
+                for f in as_completed(futs):
+                    e, ix = futs[f], f.result()
                     if ix is None:
                         self._ix_bad.add(self._key(e))
                     else:
                         self._ix[self._key(e)] = ix
                         self._ix_version += 1
+                        with self._lock:
+                            self._alt_cache.pop(self._key(e), None)
         finally:
             pool.shutdown(wait=True)
 
@@ -1050,19 +1062,27 @@ class DurableEventStore(DeviceEventStore):
     def _alt_hashes(self, ent) -> np.ndarray:
         """64-bit hashes of a block's alternate ids (0 where a row has none), computed from the stored
         strings once per block and cached with the decoded columns (blocks not indexed yet)."""
-        c = self._decoded(ent)
-        h = c.get("alt_hash")
-        if h is None:
-            from ..pipeline.fleet import hash64_heap
-            n = len(c["date"])
-            o = c["str_off"]
-            h = np.zeros(n, np.uint64)
-            if o is not None and n:
-                has = (c["flags"] & SEGF_HAS_ALT) != 0
-                idx = np.nonzero(has)[0]
-                if len(idx):
-                    h[idx] = hash64_heap(c["str_heap"], o[3 * idx], o[3 * idx + 1])
-            c["alt_hash"] = h
+        key = self._key(ent)
+        with self._lock:
+            h = self._alt_cache.get(key)
+            if h is not None:
+                self._alt_cache.move_to_end(key)
+                return h
+        from ..pipeline.fleet import hash64_heap
+        c = decode_block(self.seg.read_block(ent))
+        n = len(c["date"])
+        o = c["str_off"]
+        h = np.zeros(n, np.uint64)
+        if o is not None and n:
+            has = (c["flags"] & SEGF_HAS_ALT) != 0
+            idx = np.nonzero(has)[0]
+            if len(idx):
+                h[idx] = hash64_heap(c["str_heap"], o[3 * idx], o[3 * idx + 1])
+        with self._lock:
+            self._alt_cache[key] = h
+            rows = sum(len(x) for x in self._alt_cache.values())
+            while rows > self.alt_cache_rows and len(self._alt_cache) > 1:
+                rows -= len(self._alt_cache.popitem(last=False)[1])
         return h
 
     def _alt_rows(self, ent, want: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
