@@ -17,6 +17,12 @@ from sitewhere_amd.edges.eventhub import CoordCheckpoints, EventHubAmqpReceiver,
 from sitewhere_amd.edges.eventhub_server import EventHubServer
 
 
+# Every delivery notifies this condition, so a wait wakes on the event that satisfies it (not on
+# a poll tick).  The deadline only bounds a genuine failure: a loaded machine delays the
+# receiver thread without changing what it must deliver.
+_DELIVERED = threading.Condition()
+
+
 class _Source:
     def __init__(self):
         self.got, self.lock = [], threading.Lock()
@@ -24,13 +30,20 @@ class _Source:
     def on_encoded_event_received(self, receiver, payload, md):
         with self.lock:
             self.got.append((bytes(payload), md))
+        with _DELIVERED:
+            _DELIVERED.notify_all()
 
 
-def _wait(cond, t=10.0):
+def _wait(cond, t=60.0):
     end = time.time() + t
-    while time.time() < end and not cond():
-        time.sleep(0.02)
-    return cond()
+    with _DELIVERED:
+        while not cond():
+            left = end - time.time()
+            if left <= 0:
+                return False
+            # link attach / credit changes do not deliver, so wake at least every 50 ms for them
+            _DELIVERED.wait(min(left, 0.05))
+    return True
 
 
 def _receiver(srv, cps, **kw):
