@@ -655,8 +655,10 @@ class DurableEventStore(DeviceEventStore):
         # alternate-id hashes of blocks not indexed yet (8 B per row, bounded by rows): the per-event
         # path's store check scans them; kept apart from the decoded-block cache so it neither
         # evicts query blocks nor re-reads a block per lookup while the indexer catches up
-        self._alt_cache: OrderedDict = OrderedDict()
-        self.alt_cache_rows = 1 << 25
+        self._building: dict[tuple, threading.Event] = {}
+        self._ix_unsaved: set = set()
+        self.index_ram_bytes = 4 << 30          # newest block indexes held in RAM (older: mmapped files)
+        self._ix_ram: OrderedDict = OrderedDict()
         self.skipped_rows = 0
         # per-block indexes (postings by assignment + type, alternate-id hashes), built in the
         # background as blocks land and kept as memory-mapped sidecar files (see BlockIndex)
@@ -826,17 +828,69 @@ class DurableEventStore(DeviceEventStore):
     def _ix_base(self, key) -> str:
         return os.path.join(self._ix_dir, f"{key[0]}-{key[1]}")
 
-    def _index_one(self, ent):
+    def _built(self, ent) -> "BlockIndex | None":
+        """The block's index, built once and live as soon as it is built: the indexer threads and
+        the store checks that reach a block before the indexer does share the one build in flight
+        (each used to build its own: the sampled alternate-id tenant path spent as much time in the
+        store checks' duplicate builds as in the indexer).  None: the block fails its checksum."""
         key = self._key(ent)
-        ix = BlockIndex.load(self._ix_base(key))
-        if ix is None:
+        with self._lock:
+            ix = self._ix.get(key)
+            if ix is not None:
+                return ix
+            ev = self._building.get(key)
+            mine = ev is None
+            if mine:
+                ev = self._building[key] = threading.Event()
+        if not mine:
+            ev.wait()
+            return self._ix.get(key)
+        try:
             blk = self.seg.read_block(ent)
             if verify(blk):
                 return None
             ix = BlockIndex.build(blk, int(ent["min_date"]))
+            with self._lock:
+                self._ix[key] = ix
+                self._ix_unsaved.add(key)           # the indexer writes its files
+                self._ix_version += 1
+            return ix
+        finally:
+            with self._lock:
+                self._building.pop(key, None)
+            ev.set()
+
+    def _index_one(self, ent):
+        key = self._key(ent)
+        ix = self._ix.get(key)
+        if ix is None:
+            ix = BlockIndex.load(self._ix_base(key))
+            if ix is not None:
+                return ix
+            ix = self._built(ent)
+            if ix is None:
+                return None
+        if key in self._ix_unsaved:
             ix.save(self._ix_base(key))
-            ix = BlockIndex.load(self._ix_base(key)) or ix
+            with self._lock:
+                self._ix_unsaved.discard(key)
         return ix
+
+    def _spill_indexes(self):
+        """Keep the newest block indexes in RAM (``index_ram_bytes``) and swap older ones for their
+        file-backed (memory-mapped) copies: re-opening every index right after writing it held the
+        indexer threads (and the interpreter) in the alternate-id tenant path."""
+        for k, ix in list(self._ix.items()):
+            if not isinstance(ix.pk, np.memmap) and k not in self._ix_ram and k not in self._ix_unsaved:
+                self._ix_ram[k] = ix.nbytes
+        total = sum(self._ix_ram.values())
+        while total > self.index_ram_bytes and self._ix_ram:
+            k, nb = self._ix_ram.popitem(last=False)
+            total -= nb
+            mm = BlockIndex.load(self._ix_base(k))
+            if mm is not None and k in self._ix:
+                with self._lock:        # no version bump: the search tables keep the RAM copy alive
+                    self._ix[k] = mm
 
     def _index_loop(self):
         from concurrent.futures import ThreadPoolExecutor
@@ -850,9 +904,12 @@ class DurableEventStore(DeviceEventStore):
                 live = {self._key(e) for e in ents}
                 for k in [k for k in self._ix if k not in live]:        # retention removed the block
                     self._ix.pop(k, None)
+                    self._ix_ram.pop(k, None)
+                    self._ix_unsaved.discard(k)
                     self._ix_version += 1
                     BlockIndex.remove(self._ix_base(k))
-                todo = [e for e in ents if self._key(e) not in self._ix and self._key(e) not in self._ix_bad]
+                todo = [e for e in ents if (self._key(e) not in self._ix or self._key(e) in self._ix_unsaved)
+                        and self._key(e) not in self._ix_bad]
                 if not todo:
                     self._ix_stop.wait(0.05)
                     continue
@@ -865,10 +922,15 @@ class DurableEventStore(DeviceEventStore):
                     if ix is None:
                         self._ix_bad.add(self._key(e))
                     else:
-                        self._ix[self._key(e)] = ix
-                        self._ix_version += 1
+                        k = self._key(e)
                         with self._lock:
-                            self._alt_cache.pop(self._key(e), None)
+                            # an index built here went live in _built already (same object); one
+                            # loaded from its files goes live now
+                            fresh = k not in self._ix
+                            self._ix[k] = ix
+                            if fresh:
+                                self._ix_version += 1
+                self._spill_indexes()
         finally:
             pool.shutdown(wait=True)
 
@@ -897,7 +959,7 @@ class DurableEventStore(DeviceEventStore):
             if left <= 0:
                 break
             ix = self._ix.get(self._key(e))
-            h = np.asarray(ix.ah) if ix is not None else self._alt_hashes(e)
+            h = np.asarray(ix.ah if ix is not None else self._alt_index(e)[0])
             h = h[h != 0]
             if len(h):
                 yield h[:left]
@@ -1059,48 +1121,27 @@ class DurableEventStore(DeviceEventStore):
     def _eids(h, idx) -> np.ndarray:
         return (int(h["first_seq"]) + np.asarray(idx, np.int64)) * int(h["world"]) + int(h["rank"])
 
-    def _alt_hashes(self, ent) -> np.ndarray:
-        """64-bit hashes of a block's alternate ids (0 where a row has none), computed from the stored
-        strings once per block and cached with the decoded columns (blocks not indexed yet)."""
-        key = self._key(ent)
-        with self._lock:
-            h = self._alt_cache.get(key)
-            if h is not None:
-                self._alt_cache.move_to_end(key)
-                return h
-        from ..pipeline.fleet import hash64_heap
-        c = decode_block(self.seg.read_block(ent))
-        n = len(c["date"])
-        o = c["str_off"]
-        h = np.zeros(n, np.uint64)
-        if o is not None and n:
-            has = (c["flags"] & SEGF_HAS_ALT) != 0
-            idx = np.nonzero(has)[0]
-            if len(idx):
-                h[idx] = hash64_heap(c["str_heap"], o[3 * idx], o[3 * idx + 1])
-        with self._lock:
-            self._alt_cache[key] = h
-            rows = sum(len(x) for x in self._alt_cache.values())
-            while rows > self.alt_cache_rows and len(self._alt_cache) > 1:
-                rows -= len(self._alt_cache.popitem(last=False)[1])
-        return h
+    def _alt_index(self, ent) -> tuple[np.ndarray, np.ndarray]:
+        """(sorted alternate-id hashes, their rows) of a block: its index, built now (and shared with
+        the indexer, ``_built``) when the background indexer has not reached the block yet."""
+        ix = self._built(ent)
+        if ix is None:
+            raise ValueError("event block checksum mismatch")
+        return ix.ah, ix.ar
 
     def _alt_rows(self, ent, want: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
         """(hashes, rows) of a block's rows whose alternate-id hash is in ``want`` (sorted unique)."""
         ix = self._ix.get(self._key(ent))
-        if ix is not None:
-            if not len(ix.ah):
-                return np.zeros(0, np.uint64), np.zeros(0, np.int64)
-            lo = np.searchsorted(ix.ah, want, "left")
-            hi = np.searchsorted(ix.ah, want, "right")
-            sel = np.nonzero(hi > lo)[0]
-            if not len(sel):
-                return np.zeros(0, np.uint64), np.zeros(0, np.int64)
-            idx = np.concatenate([np.arange(lo[i], hi[i]) for i in sel])
-            return np.asarray(ix.ah[idx]), np.asarray(ix.ar[idx], np.int64)
-        ah = self._alt_hashes(ent)
-        rows = np.nonzero(np.isin(ah, want))[0]
-        return ah[rows], rows
+        ah, ar = (ix.ah, ix.ar) if ix is not None else self._alt_index(ent)
+        if not len(ah):
+            return np.zeros(0, np.uint64), np.zeros(0, np.int64)
+        lo = np.searchsorted(ah, want, "left")
+        hi = np.searchsorted(ah, want, "right")
+        sel = np.nonzero(hi > lo)[0]
+        if not len(sel):
+            return np.zeros(0, np.uint64), np.zeros(0, np.int64)
+        idx = np.concatenate([np.arange(lo[i], hi[i]) for i in sel])
+        return np.asarray(ah[idx]), np.asarray(ar[idx], np.int64)
 
     def find_alternate_hashes(self, hashes, covered: tuple | None = None, indexed_only: bool = False) -> dict:
         """alt-id hash -> event id string for the hashes present on disk, the newest event per hash

@@ -27,7 +27,7 @@ class _Src:
         self.got.append((bytes(payload), md))
 
 
-def wait(cond, t=5.0):
+def wait(cond, t=30.0):          # returns as soon as cond holds; the bound only catches a real failure
     end = time.time() + t
     while time.time() < end and not cond():
         time.sleep(0.01)

@@ -21,7 +21,7 @@ from sitewhere_amd.edges.mqtt import (CONNECT, PUBLISH, MqttBroker, MqttClient, 
 from sitewhere_amd.edges.receivers import build_receiver
 
 
-def wait(cond, t=5.0):
+def wait(cond, t=30.0):          # returns as soon as cond holds; the bound only catches a real failure
     end = time.time() + t
     while time.time() < end and not cond():
         time.sleep(0.01)

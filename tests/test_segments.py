@@ -4,6 +4,7 @@ MI355X encoder is checked against the CPU encoder bit for bit in tests/test_gpu_
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import pytest
@@ -424,3 +425,28 @@ def test_block_indexes_answer_like_the_scan(tmp_path):
     r = es2.list_events("Measurement", "Assignment", ["asg-3"], DateRangeSearchCriteria(page_size=0))
     assert (r.num_results, [e.id for e in r.results]) == (indexed[0][0], [x[0] for x in indexed[0][1]])
     es2.close()
+
+
+def test_block_indexes_spill_to_files_past_the_ram_budget(tmp_path):
+    """The newest block indexes stay in RAM up to ``index_ram_bytes``; older ones are swapped for
+    their memory-mapped files and answer the same lookups."""
+    from sitewhere_amd.pipeline.fleet import hash64
+    es = sg.DurableEventStore(str(tmp_path / "es"), direct=False)
+    es.index_ram_bytes = 0
+    n0, alts = 0, []
+    for b in range(3):
+        rows, recs, spans, raw = synth_rows(2000, seed=40 + b)
+        blk = sg.encode_block(rows, recs, spans, raw)
+        sg.seal(blk, n0, 1_700_000_100_000 + b, 0xc0, 0, 1)
+        es.wait(es.add_encoded(blk))
+        alts += [(n0 + j, s[0]) for j, s in enumerate(expected_strings(recs, spans, raw)) if s[0] is not None]
+        n0 += len(rows)
+    assert es.index_wait(60)
+    deadline = time.time() + 30
+    while time.time() < deadline and not all(isinstance(ix.pk, np.memmap) for ix in list(es._ix.values())):
+        time.sleep(0.02)
+    assert len(es._ix) == 3 and all(isinstance(ix.pk, np.memmap) for ix in es._ix.values())
+    eid, alt = alts[len(alts) // 2]
+    assert es.get_event_by_alternate_id(alt).id == f"c0-{eid}"
+    assert es.find_alternate_hashes([hash64(alt)]) == {hash64(alt): f"c0-{eid}"}
+    es.close()
