@@ -450,3 +450,36 @@ def test_block_indexes_spill_to_files_past_the_ram_budget(tmp_path):
     assert es.get_event_by_alternate_id(alt).id == f"c0-{eid}"
     assert es.find_alternate_hashes([hash64(alt)]) == {hash64(alt): f"c0-{eid}"}
     es.close()
+
+
+def test_store_checks_share_one_index_build_per_block(tmp_path, monkeypatch):
+    """Concurrent lookups that reach a block before the indexer build its index once; the index is
+    then live for every later lookup and the indexer only writes its files."""
+    import threading
+    from sitewhere_amd.pipeline.fleet import hash64
+    es = sg.DurableEventStore(str(tmp_path / "es"), direct=False, index=False)
+    rows, recs, spans, raw = synth_rows(3000, seed=77)
+    blk = sg.encode_block(rows, recs, spans, raw)
+    sg.seal(blk, 0, 1_700_000_100_000, 0xc0, 0, 1)
+    es.wait(es.add_encoded(blk))
+    alts = [(j, s[0]) for j, s in enumerate(expected_strings(recs, spans, raw)) if s[0] is not None]
+    builds, real = [], sg.BlockIndex.build
+
+    def slow_build(block, min_date):
+        builds.append(1)
+        time.sleep(0.2)                 # keep the build in flight while the other lookups arrive
+        return real(block, min_date)
+    monkeypatch.setattr(sg.BlockIndex, "build", staticmethod(slow_build))
+    got = [None] * 6
+
+    def look(i):
+        eid, alt = alts[i * 7]
+        ev = es.get_event_by_alternate_id(alt)
+        got[i] = ev is not None and ev.id == f"c0-{eid}"
+    ts = [threading.Thread(target=look, args=(i,)) for i in range(len(got))]
+    [t.start() for t in ts]
+    [t.join(30) for t in ts]
+    assert all(got) and len(builds) == 1
+    assert es.find_alternate_hashes([hash64(alts[3][1])]) == {hash64(alts[3][1]): f"c0-{alts[3][0]}"}
+    assert len(builds) == 1
+    es.close()
