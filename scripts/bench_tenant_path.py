@@ -241,7 +241,9 @@ def main():
             trace.update(gap_pct)
     breakdown = {name: round(t.hist.snapshot()["mean"], 3)
                  for name, t in (("engine_step_ms", ib.step_timer), ("columnar_store_ms", ib.store_timer),
-                                 ("publish_ms", ib.publish_timer))}
+                                 ("publish_ms", ib.publish_timer), ("recheck_ms", ib.recheck_timer))}
+    breakdown["recheck_max_ms"] = round(ib.recheck_timer.hist.snapshot()["max"], 3)
+    breakdown["engine_step_max_ms"] = round(ib.step_timer.hist.snapshot()["max"], 3)
     print(json.dumps({"metric": "tenant_path_events_per_sec", "engine": ib.engine_kind, "via_bus": args.via_bus,
                       "gc": args.gc, "zero_copy_rows": ib.zero_copy_rows,
                       "payloads_framed": ib.zc_framed, "payloads_copied": ib.zc_copied,

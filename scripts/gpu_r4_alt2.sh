@@ -11,4 +11,4 @@ run() {
     || { tail -20 "$O/$name.err"; return 1; }
   tail -1 "$O/$name.log" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["alt_ids"], round(d["events_per_sec"]/1e6,1), "M/s", d["ms_per_batch"], "ms/batch", d["engine_steps"], "steps", d["routed_payloads"], "routed", d["mean_ms"], d.get("median_ms_second_half"))'
 }
-run alt && SW_SAMPLE_STACKS=1 run alt_sampled
+run alt && { [ -n "$ALT_ONLY" ] || SW_SAMPLE_STACKS=1 run alt_sampled; }

@@ -189,6 +189,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.step_timer = self.create_timer("engineStep")
         self.store_timer = self.create_timer("columnarStore")       # payload build + event-management call
         self.publish_timer = self.create_timer("enrichedPublish")
+        self.recheck_timer = self.create_timer("filterRecheck")       # durable-store lookup of rechecks
         self.api = {"InboundProcessing": GpuInboundApi(self)}
 
     def _make_engine(self, device: str, ecfg: EngineConfig):
@@ -1052,7 +1053,8 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         st = res.reject_status
         if st is None or not len(st):
             return None
-        st = self._settle_rechecks(res, st)
+        with self.recheck_timer.time():
+            st = self._settle_rechecks(res, st)
         bus = self.ms.instance.bus
         topics = (self.t_unregistered, self.t_registration, self.t_decoded, self.t_failed_decode)
         parts = [bus.partitions(t) if hasattr(bus, "partitions") else 1 for t in topics]
