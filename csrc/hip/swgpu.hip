@@ -1615,6 +1615,20 @@ int sw_phase_unpack(const SwEngineArgs* ap, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// (assignment, ok index) pairs of the validated events, for the clustering sort
+__global__ void k_cl_prep(const uint32_t* __restrict__ ok_idx, const uint32_t* __restrict__ n_ok,
+                          const int32_t* __restrict__ ev_asg, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const uint32_t n = *n_ok;
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+    const uint32_t i = ok_idx[j];
+    keys[j] = (uint32_t)ev_asg[i];
+    vals[j] = i;
+  }
+}
+
+int sw_radix_sort_u32(uint32_t* keys, uint32_t* vals, const uint32_t* n_ptr, int64_t cap, int bits, uint32_t* hist,
+                      uint32_t* vals_final, hipStream_t s);
+
 // Phase D: validate, dedup, persist, enrich, state, rules, presence.
 int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) {
   const SwEngineArgs a = *ap;
@@ -1630,6 +1644,12 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx, a.n_ok,
                                                a.n_rej);
   int rc = 0;
+  if (a.cl_bits > 0) {
+    // persist order: stable by assignment (the durable block's clustering, swindex.h)
+    k_cl_prep<<<g, BLK, 0, s>>>(a.ok_idx, a.n_ok, a.ev_asg, a.cl_keys, a.cl_vals);
+    rc = sw_radix_sort_u32(a.cl_keys, a.cl_vals, a.n_ok, a.rec_cap, (int)a.cl_bits, a.cl_hist, a.ok_idx, s);
+    if (rc < 0) return rc;
+  }
   // persist + enrich + state for the validated events
   // string refs of the work batch: the decoder's (one rank) or the exchange's (rebased into work_str)
   const SwStrRef* wsp = a.world > 1 ? a.work_spans : a.spans;

@@ -327,7 +327,7 @@ __device__ __forceinline__ void seg_encode_page(const SwSegArgs& a, SegLds& L) {
   if (n <= 0) {
     if (page == 0 && threadIdx.x == 0) {
       SwSegBlockHdr* h = reinterpret_cast<SwSegBlockHdr*>(a.out);
-      h->n_rows = 0; h->n_pages = 0; h->bytes = data_start;
+      h->n_rows = 0; h->n_pages = 0; h->bytes = data_start; h->flags = 0;
       page_off[0] = data_start;
       page_off[1] = 0;
       atomicMax((ull*)bytes_out, (ull)data_start);
@@ -684,6 +684,7 @@ __device__ __forceinline__ void seg_encode_page(const SwSegArgs& a, SegLds& L) {
           h->n_rows = (uint32_t)n;
           h->n_pages = (uint32_t)np;
           h->bytes = base + size;
+          h->flags = 0;                  // the index build (swindex.hip) sets SEG_FLAG_INDEX
           atomicMax((ull*)bytes_out, base + size);
         }
       }

@@ -211,6 +211,14 @@ typedef struct SwEngineArgs {
   uint32_t* str_drops;         // [2] records whose strings did not fit / came from the carry
   // ---------------------------------------------------------------- re-key owner (world > 1)
   uint8_t* part_owner;         // [carry_cap + rec_cap] destination of each partition input (k_part_count)
+  // ---------------------------------------------------------------- persist clustering
+  // Each step's validated events persist stable-sorted by assignment index (the block's clustered
+  // order: an assignment's rows of a step share one or two pages, see swindex.h).  Radix-sort
+  // buffers: keys / values [2][rec_cap] ping-pong, histograms [sw_radix_tmp_words(rec_cap)].
+  uint32_t* cl_keys;
+  uint32_t* cl_vals;
+  uint32_t* cl_hist;
+  int64_t cl_bits;             // assignment index bits (0: persist in arrival order)
 } SwEngineArgs;
 
 #define SW_N_STATS 24

@@ -259,6 +259,8 @@ typedef struct SwCeTables {
   uint64_t presence_hash;
   int64_t presence_missing_ms;
   uint64_t* stats;  // [SW_N_STATS], SW_STAT_* slots
+  int32_t cluster;  // persist each step stable-sorted by assignment (EngineConfig.cluster)
+  int32_t pad0;
 } SwCeTables;
 
 typedef struct SwCeStep {
@@ -286,6 +288,7 @@ struct SwCpuEngine {
   // per-step scratch, kept across steps (no page-faulting fresh buffers every batch)
   std::vector<int32_t> asg, dev;
   std::vector<int64_t> ok_idx;
+  std::vector<int64_t> ok_tmp;      // clustering sort scratch
   std::vector<std::vector<int32_t>> lists;  // [chunk * T + shard] -> record / row indices
   std::vector<std::vector<int64_t>> scratch64;
   explicit SwCpuEngine(int n) : pool(n), dedup(pool.size()), dedup_prev(pool.size()), ms(pool.size()) {
@@ -318,6 +321,26 @@ static inline bool pip(const double* v, int32_t n, double x, double y) {
     if (((yi > y) != (yj > y)) && (x < (xj - xi) * (y - yi) / (yj - yi) + xi)) inside = !inside;
   }
   return inside;
+}
+
+// Stable LSD radix sort (11-bit digits) of the ok indices by their assignment index.
+static void cluster_by_assignment(int64_t* idx, int64_t n, const int32_t* asg, int64_t n_asg,
+                                  std::vector<int64_t>& tmp) {
+  int bits = 1;
+  while (bits < 31 && (int64_t(1) << bits) < n_asg) ++bits;
+  if ((int64_t)tmp.size() < n) tmp.resize(n);
+  int64_t* src = idx;
+  int64_t* dst = tmp.data();
+  std::vector<int64_t> cnt(1 << 11);
+  for (int shift = 0; shift < bits; shift += 11) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int64_t j = 0; j < n; ++j) ++cnt[((uint32_t)asg[src[j]] >> shift) & 2047u];
+    int64_t sum = 0;
+    for (auto& c : cnt) { const int64_t x = c; c = sum; sum += x; }
+    for (int64_t j = 0; j < n; ++j) dst[cnt[((uint32_t)asg[src[j]] >> shift) & 2047u]++] = src[j];
+    std::swap(src, dst);
+  }
+  if (src != idx) memcpy(idx, src, sizeof(int64_t) * n);
 }
 
 // Persist rows [b, end) -- record idx[j] (or j) with assignment asg_of(j) -- at store sequence
@@ -593,6 +616,11 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   // 4. name interning in first-occurrence order over the persisted records
   intern_in_order(e, work, ok_idx, n_ok);
   lap("intern");
+
+  // 4b. persist order: stable by assignment (the durable block's clustering, csrc/include/swindex.h;
+  // the MI355X engine radix-sorts the same pairs)
+  if (t->cluster && n_ok > 1) cluster_by_assignment(ok_idx, n_ok, asg, t->n_assignments, e->ok_tmp);
+  lap("cluster");
 
   // 5. persist + enrich (parallel rows); rows bucketed by assignment shard for the state merge
   const int64_t cursor0 = st->cursor;

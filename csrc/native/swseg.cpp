@@ -36,6 +36,7 @@
 #include <thread>
 #include <vector>
 
+#include "swindex.h"
 #include "swseg.h"
 
 #define SEG_ALIGN 4096
@@ -414,7 +415,7 @@ void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot
   memcpy(&h, block, sizeof(h));
   h.magic = SEG_MAGIC;
   h.version = SEG_VERSION;
-  h.flags = 0;
+  h.flags &= SEG_FLAG_INDEX;      // an index trailer built before sealing stays
   h.first_seq = first_seq;
   h.recv_ms = recv_ms;
   h.boot = boot;
@@ -426,19 +427,32 @@ void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot
   memcpy(block, &h, sizeof(h));
 }
 
-// Set the header flags of a sealed block (SEG_FLAG_COMMIT) and redo its checksum.
-void swseg_set_flags(uint8_t* block, int32_t flags) {
+// Redo the header checksum of a sealed block (after its flags or bytes changed).
+void swseg_rechecksum(uint8_t* block) {
   SwSegBlockHdr h;
   memcpy(&h, block, sizeof(h));
-  h.flags = (uint16_t)flags;
   h.checksum = 0;
   memcpy(block, &h, sizeof(h));
   h.checksum = header_checksum(block);
   memcpy(block, &h, sizeof(h));
 }
 
-// 0 = valid; 1 bad header, 2 bad page table, 3 bad page header, 4 page checksum, 5 short.
+// Set the header flags of a sealed block (SEG_FLAG_COMMIT) and redo its checksum (SEG_FLAG_INDEX,
+// which says the block carries an index trailer, is kept).
+void swseg_set_flags(uint8_t* block, int32_t flags) {
+  SwSegBlockHdr h;
+  memcpy(&h, block, sizeof(h));
+  h.flags = (uint16_t)((flags & ~SEG_FLAG_INDEX) | (h.flags & SEG_FLAG_INDEX));
+  h.checksum = 0;
+  memcpy(block, &h, sizeof(h));
+  h.checksum = header_checksum(block);
+  memcpy(block, &h, sizeof(h));
+}
+
+// 0 = valid; 1 bad header, 2 bad page table, 3 bad page header, 4 page checksum, 5 short,
+// 6 bad index trailer.
 int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1);
+int32_t swseg_ix_verify(const uint8_t* t, int64_t len, int64_t n_rows, int64_t n_pages);
 
 int32_t swseg_verify(const uint8_t* b, int64_t len) { return swseg_verify_pages(b, len, 0, INT64_MAX); }
 
@@ -455,9 +469,18 @@ int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1
   if (header_checksum(b) != h.checksum) return 1;
   const uint32_t* pt = (const uint32_t*)(b + 64);
   if (h.n_pages && pt[0] != start) return 2;
-  if (pt[h.n_pages] != h.bytes) return 2;
+  if (h.flags & SEG_FLAG_INDEX) {
+    // the index trailer follows the pages; checked with the whole block (partial reads skip it)
+    if (pt[h.n_pages] > h.bytes || (pt[h.n_pages] & 7) || h.bytes - pt[h.n_pages] < SIX_HDR_BYTES) return 2;
+    if (p0 <= 0 && p1 >= (int64_t)h.n_pages &&
+        swseg_ix_verify(b + pt[h.n_pages], (int64_t)(h.bytes - pt[h.n_pages]), h.n_rows, h.n_pages) != 0)
+      return 6;
+  } else if (pt[h.n_pages] != h.bytes) {
+    return 2;
+  }
+  const uint32_t pend = pt[h.n_pages];
   for (uint32_t p = 0; p < h.n_pages; ++p)
-    if (pt[p + 1] < pt[p] + SEG_PAGE_HDR || pt[p + 1] > h.bytes || (pt[p] & 7)) return 2;
+    if (pt[p + 1] < pt[p] + SEG_PAGE_HDR || pt[p + 1] > pend || (pt[p] & 7)) return 2;
   if (p0 < 0) p0 = 0;
   if (p1 > (int64_t)h.n_pages) p1 = h.n_pages;
   for (uint32_t p = (uint32_t)p0; (int64_t)p < p1; ++p) {

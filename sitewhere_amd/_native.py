@@ -27,8 +27,8 @@ CSRC = ROOT / "csrc"
 GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
 
 _NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp", CSRC / "native" / "swseg.cpp",
-               CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp", CSRC / "native" / "swjson.cpp"]
-_GPU_SRC = [CSRC / "hip" / "swgpu.hip", CSRC / "hip" / "swseg.hip"]
+               CSRC / "native" / "swindex.cpp", CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp", CSRC / "native" / "swjson.cpp"]
+_GPU_SRC = [CSRC / "hip" / "swgpu.hip", CSRC / "hip" / "swseg.hip", CSRC / "hip" / "swindex.hip"]
 _HEADERS = sorted((CSRC / "include").glob("*.h"))
 
 _lock = threading.Lock()
@@ -190,6 +190,19 @@ def native():
         _proto(lib, "swseg_multi_find_u64", None, P, P, c_int64, P, c_int64, P, P)
         _proto(lib, "swseg_multi_range_u32", None, P, P, P, P, c_int64, ctypes.c_uint32, c_int64, c_int64, P, P)
         _proto(lib, "swseg_dates", None, P, P, P)
+        # block index trailers (csrc/native/swindex.cpp, format csrc/include/swindex.h)
+        _proto(lib, "swseg_index_append", c_int64, P, c_int64, P, c_int64)
+        _proto(lib, "swseg_ix_verify", c_int32, P, c_int64, c_int64, c_int64)
+        _proto(lib, "swseg_ix_offset", c_int64, P)
+        _proto(lib, "swseg_ix_max_bytes", c_int64, c_int64)
+        _proto(lib, "swseg_ix_alt_pages", c_int64, P, c_int64, c_uint64, P, P, c_int64)
+        _proto(lib, "swseg_ix_alt_find", None, P, c_int64, P, c_int64, P, P)
+        _proto(lib, "swseg_ix_asg_pages", c_int64, P, c_int64, c_int32, c_int64, c_int64, P, P, c_int64)
+        _proto(lib, "swseg_ix_ctx_find", None, P, c_int64, c_int32, ctypes.c_uint32, P)
+        _proto(lib, "swseg_rechecksum", None, P)
+        _proto(lib, "swseg_alt_hashes", c_int64, P, P, c_int64)
+        _proto(lib, "swseg_scan_pages", c_int64, P, P, P, P, P, c_int64, c_int32, c_int32, P, c_int64, c_int32,
+               c_int64, c_int64, c_int32, P, P, P, c_int64)
         _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)
         _proto(lib, "swss_append", c_int32, P, P, c_int64, c_int64)
         _proto(lib, "sw_varint_offsets", c_int32, P, c_int64, c_int64, c_int64, P)
@@ -290,6 +303,14 @@ def gpu():
         _proto(lib, "sw_seg_encode_stamped", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P)
         _proto(lib, "sw_seg_encode_snap", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P, P, P, P)
         _proto(lib, "sw_seg_aux", c_int32, P, P, P, P, P, c_int64, P, P, c_int64, P)
+        # block index trailers + the radix sort (csrc/hip/swindex.hip)
+        _proto(lib, "sw_radix_tmp_words", c_int64, c_int64)
+        _proto(lib, "sw_radix_sort_u32", c_int32, P, P, P, c_int64, c_int32, P, P, P)
+        _proto(lib, "sw_seg_index_scratch_words", c_int64, c_int64)
+        _proto(lib, "sw_seg_index_max_bytes", c_int64, c_int64)
+        _proto(lib, "sw_seg_index_init", c_int32, P, c_int64, P)
+        _proto(lib, "sw_seg_index", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, c_int64, P, c_int64, P, P,
+               c_int64, P)
         _proto(lib, "sw_bloom_add", c_int32, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)

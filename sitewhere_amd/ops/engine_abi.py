@@ -67,6 +67,8 @@ FIELDS = [
     ("recv_spans", P), ("work_str", P), ("work_spans", P), ("str_cap", I), ("str_drops", P),
     # re-key destination of each partition input
     ("part_owner", P),
+    # persist clustering by assignment (radix-sort buffers, key bits; 0 = arrival order)
+    ("cl_keys", P), ("cl_vals", P), ("cl_hist", P), ("cl_bits", I),
 ]
 
 

@@ -60,6 +60,61 @@ def _p(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+# Block index trailer (csrc/include/swindex.h)
+IX_DIMS = 3                         # customer, area, asset
+IX_HEADS = 16
+IX_CTX_MAX = 8192
+IX_NOT_INDEXED = 0xFFFFFFFF
+IX_ALT_EBITS = 26
+IX_HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("n_dims", "<u2"), ("n_rows", "<u4"), ("n_pages", "<u4"),
+                   ("bytes", "<u8"), ("checksum", "<u8"), ("alt_bits", "<u4"), ("alt_pbits", "<u4"), ("n_alt", "<u4"),
+                   ("off_pages", "<u4"), ("off_alt_dir", "<u4"), ("off_alt", "<u4"), ("off_keys", "<u4", 3),
+                   ("n_keys", "<u4", 3), ("off_heads", "<u4", 3), ("n_heads", "<u4", 3), ("off_hdates", "<u4", 3),
+                   ("pad", "<u4", 3)])
+assert IX_HDR.itemsize == 128
+IX_PAGE = np.dtype([("asg_min", "<i4"), ("asg_max", "<i4"), ("date_min", "<i8"), ("date_max", "<i8"), ("off", "<u4"),
+                    ("bytes", "<u4")])
+IX_KEY = np.dtype([("key", "<u4"), ("count", "<u4"), ("date_min", "<i8"), ("date_max", "<i8"), ("head_off", "<u4"),
+                   ("n_heads", "<u4")])
+
+
+def parse_trailer(t) -> dict:
+    """Index trailer bytes -> header fields and numpy views of its sections: ``pages`` (IX_PAGE),
+    ``alt_dir`` (u32), ``alt_words`` (u64), per dimension ``keys[d]`` (IX_KEY, None: not indexed),
+    ``head_rows[d]`` / ``head_dates[d]``."""
+    t = np.frombuffer(t, np.uint8) if not isinstance(t, np.ndarray) else t
+    h = t[:128].view(IX_HDR)[0]
+    d = {k: (h[k].copy() if h[k].shape else int(h[k])) for k in IX_HDR.names}
+    d["pages"] = t[d["off_pages"]:d["off_pages"] + 32 * d["n_pages"]].view(IX_PAGE)
+    d["alt_dir"] = t[d["off_alt_dir"]:d["off_alt_dir"] + 4 * ((1 << d["alt_bits"]) + 1)].view(np.uint32)
+    nw = (d["n_alt"] * IX_ALT_EBITS + 63) // 64
+    d["alt_words"] = t[d["off_alt"]:d["off_alt"] + 8 * nw].view(np.uint64)
+    d["keys"], d["head_rows"], d["head_dates"] = [], [], []
+    for q in range(IX_DIMS):
+        nk, nh = int(d["n_keys"][q]), int(d["n_heads"][q])
+        if nk == IX_NOT_INDEXED:
+            d["keys"].append(None)
+            d["head_rows"].append(np.zeros(0, np.uint32))
+            d["head_dates"].append(np.zeros(0, np.int64))
+            continue
+        ok, oh, od = int(d["off_keys"][q]), int(d["off_heads"][q]), int(d["off_hdates"][q])
+        d["keys"].append(t[ok:ok + 32 * nk].view(IX_KEY))
+        d["head_rows"].append(t[oh:oh + 4 * nh].view(np.uint32))
+        d["head_dates"].append(t[od:od + 8 * nh].view(np.int64))
+    return d
+
+
+def alt_entries(tr: dict) -> np.ndarray:
+    """The packed alternate-id entries of a parsed trailer, unpacked (u64: fingerprint << pbits | page)."""
+    n = tr["n_alt"]
+    w = np.concatenate([tr["alt_words"], np.zeros(1, np.uint64)])
+    bp = np.arange(n, dtype=np.uint64) * np.uint64(IX_ALT_EBITS)
+    wi, sh = (bp >> np.uint64(6)).astype(np.int64), bp & np.uint64(63)
+    lo = w[wi] >> sh
+    hi = np.where(sh > 0, w[wi + 1] << ((np.uint64(64) - sh) & np.uint64(63)), np.uint64(0))
+    return (lo | hi) & np.uint64((1 << IX_ALT_EBITS) - 1)
+
+
 def max_block_bytes(n_rows: int, string_bytes: int = 0) -> int:
     """Upper bound of an encoded block (every column at 64 bits plus exceptions, every string of the
     rows in the heap: ``string_bytes``), padded."""
@@ -77,11 +132,13 @@ def max_string_bytes(n_rows: int, raw_bytes: int) -> int:
 
 
 def encode_block(rows: np.ndarray, recs: np.ndarray | None = None, spans: np.ndarray | None = None,
-                 raw: np.ndarray | None = None) -> np.ndarray:
+                 raw: np.ndarray | None = None, index: bool = False, ctx: np.ndarray | None = None) -> np.ndarray:
     """CPU encoder (bit-identical to the MI355X ``k_seg_encode``): OUT_REC rows, each with its
     persisted EVENT_REC record and STR_REF string refs (row-aligned; None: rows without record
     data -- no strings, elevation or flags) into the raw batch ``raw`` -> block bytes (header sealed
-    separately by :func:`seal`)."""
+    separately by :func:`seal`).  ``index``: append the block's index trailer (``swindex.h``, the
+    same bytes the MI355X builds); ``ctx`` = int32 [assignments, 4] (device, customer, area, asset)
+    by assignment index, None: the context dimensions stay unindexed."""
     from ..models.columnar import EVENT_REC, STR_REF
     rows = np.ascontiguousarray(rows, OUT_REC)
     n = len(rows)
@@ -93,6 +150,8 @@ def encode_block(rows: np.ndarray, recs: np.ndarray | None = None, spans: np.nda
         assert len(spans) >= n
     raw_a = None if raw is None else np.ascontiguousarray(raw, np.uint8)
     cap = max_block_bytes(n, 0 if raw_a is None else max_string_bytes(n, len(raw_a)))
+    if index:
+        cap += int(native().swseg_ix_max_bytes(n))
     out = np.zeros(cap, np.uint8)
     r = native().swseg_encode(_p(rows) if n else None, _p(recs) if recs is not None and n else None,
                               _p(spans) if spans is not None and n else None,
@@ -100,7 +159,35 @@ def encode_block(rows: np.ndarray, recs: np.ndarray | None = None, spans: np.nda
                               0 if raw_a is None else len(raw_a), n, _p(out), cap)
     if r < 0:
         raise RuntimeError(f"block needs {-r} bytes")
+    if index:
+        r = _index_into(out, cap, ctx)
     return out[:r]
+
+
+def _index_into(buf: np.ndarray, cap: int, ctx: np.ndarray | None) -> int:
+    if ctx is not None:
+        ctx = np.ascontiguousarray(ctx, np.int32).reshape(-1, 4)
+    r = int(native().swseg_index_append(_p(buf), int(cap), _p(ctx) if ctx is not None and len(ctx) else None,
+                                        0 if ctx is None else len(ctx)))
+    if r < 0:
+        raise RuntimeError(f"block index trailer failed ({r})")
+    return r
+
+
+def index_block(block: np.ndarray, ctx: np.ndarray | None = None) -> np.ndarray:
+    """A copy of ``block`` (sealed or not) with its index trailer (rebuilt if it had one)."""
+    b = np.ascontiguousarray(block, np.uint8)
+    n = int(b[:64].view(HDR)[0]["n_rows"])
+    cap = len(b) + int(native().swseg_ix_max_bytes(n))
+    out = np.zeros(cap, np.uint8)
+    out[:len(b)] = b
+    return out[:_index_into(out, cap, ctx)]
+
+
+def trailer_offset(block) -> int:
+    """Offset of a block's index trailer, 0 when it has none."""
+    b = np.frombuffer(block, np.uint8) if not isinstance(block, np.ndarray) else block
+    return int(native().swseg_ix_offset(_p(np.ascontiguousarray(b[:64 + 4 * (int(b[:64].view(HDR)[0]["n_pages"]) + 2)]))))
 
 
 def seal(block: np.ndarray, first_seq: int, recv_ms: int, boot: int, rank: int, world: int):

@@ -35,6 +35,13 @@ class EngineConfig:
     # world > 1: string bytes (alternate id + metadata + alert message) exchanged per record slot of
     # a re-key slab; the owner rank stores them losslessly (0 = strings stay on the decoding rank)
     str_bytes: int = 40
+    # persist each step's events stable-sorted by assignment (the durable block is then clustered by
+    # assignment: its page zone maps are the assignment index, csrc/include/swindex.h); every engine
+    # (MI355X, native C++, Python oracle) uses the same order
+    cluster: bool = True
+    # durable blocks carry their index trailer (alternate ids, page zone maps, context-key heads),
+    # built in the step that encodes them
+    block_index: bool = True
     presence_missing_ms: int = 8 * 3600 * 1000   # DevicePresenceManager default (8h)
     presence_check_ms: int = 10 * 60 * 1000      # DevicePresenceManager default (10 min)
     rank: int = 0
@@ -54,6 +61,8 @@ class EngineConfig:
         if self.dedup_bloom_bits > 0:
             self.dedup_bloom_bits = pow2_at_least(max(512, self.dedup_bloom_bits))
         self.state_slots = pow2_at_least(self.state_slots)
+        # key bits of the clustering sort (assignment indices < max_assignments)
+        self.cl_bits = max(1, (self.max_assignments - 1).bit_length()) if self.cluster else 0
         self.shuf_cap = int(self.shuffle_slack * self.rec_cap / max(1, self.world)) + self.shuffle_pad
         local = self.rec_cap
         # per-destination string slab, 16-byte multiple (the unpack gathers it 16 B at a time)

@@ -392,6 +392,9 @@ class CpuInboundEngine(EngineBase):
             h = int(work[i]["name_hash"])
             if h:
                 self._intern_id(h)
+        if self.cfg.cluster and len(ok) > 1:
+            # persist order: stable by assignment (the durable block's clustering, swindex.h)
+            ok = ok[np.argsort(asg[ok], kind="stable")]
         out_rows: list = []
         self._persist(work[ok], dev[ok], asg[ok], now_ms, out_rows)
         self.bloom_add(work[ok]["alt_hash"])             # persisted ids join the store-backed filter

@@ -174,6 +174,7 @@ class EngineBase:
 
         act = np.ones(n, np.uint8) if active is None else np.broadcast_to(np.asarray(active, np.uint8), (n,))
         with self._lock:
+            self._ctx_version += 1
             self.asg_device[asg_idx] = dev_idx
             self.asg_customer[asg_idx] = col(customer, -1)
             self.asg_area[asg_idx] = col(area, -1)
@@ -320,10 +321,25 @@ class EngineBase:
         ids, alert messages, metadata).  The MI355X engine overrides this with its GPU encoder
         (same bytes)."""
         from ..persistence.segments import encode_block, seal
-        blk = encode_block(res.out if res.out is not None else np.zeros(0, OUT_REC), res.prec, res.pspans, res.raw)
+        ix = self.cfg.block_index
+        blk = encode_block(res.out if res.out is not None else np.zeros(0, OUT_REC), res.prec, res.pspans, res.raw,
+                           index=ix, ctx=self.ctx_table() if ix else None)
         res.raw = None
         seal(blk, res.first_seq, now_ms, boot, self.rank, self.world)
         return blk
+
+    def ctx_table(self) -> np.ndarray:
+        """Assignment context by assignment index, int32 [max_assignments, 4] = (device, customer,
+        area, asset): what the block index trailer keys its context dimensions by (the MI355X engine
+        reads its HBM copy, ``asg_ctx``)."""
+        tab = self.__dict__.get("_ctx_tab")
+        if tab is None or tab[0] != self._ctx_version:
+            t = np.ascontiguousarray(np.stack([self.asg_device, self.asg_customer, self.asg_area, self.asg_asset], 1),
+                                     np.int32)
+            tab = self._ctx_tab = (self._ctx_version, t)
+        return tab[1]
+
+    _ctx_version = 0
 
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "base"

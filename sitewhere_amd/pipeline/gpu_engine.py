@@ -170,6 +170,11 @@ class GpuInboundEngine(EngineBase):
         t["ev_dev"] = z(c.rec_cap, i32)
         t["ev_asg"] = z(c.rec_cap, i32)
         t["ok_idx"] = z(c.rec_cap, i32)
+        if c.cluster:
+            # persist clustering by assignment: radix-sort ping-pong buffers + histograms
+            t["cl_keys"] = z(2 * c.rec_cap, i32)
+            t["cl_vals"] = z(2 * c.rec_cap, i32)
+            t["cl_hist"] = z(int(self.lib.sw_radix_tmp_words(c.rec_cap)), i32)
         t["rej_idx"] = z(c.rec_cap, i32)
         t["cmp_tmp"] = z(4 * ntiles + 64, i32)
         # registry (packed SwRegSlot: lo, hi, dev, asg, pad) + assignment context (device, customer, area, asset)
@@ -246,6 +251,8 @@ class GpuInboundEngine(EngineBase):
         a.status, a.ev_dev, a.ev_asg = _ptr(t["status"]), _ptr(t["ev_dev"]), _ptr(t["ev_asg"])
         a.ok_idx, a.n_ok, a.rej_idx, a.n_rej = _ptr(t["ok_idx"]), S(4), _ptr(t["rej_idx"]), S(5)
         a.cmp_tmp = _ptr(t["cmp_tmp"])
+        if c.cluster:
+            a.cl_keys, a.cl_vals, a.cl_hist, a.cl_bits = _ptr(t["cl_keys"]), _ptr(t["cl_vals"]), _ptr(t["cl_hist"]), c.cl_bits
         a.reg, a.reg_mask = _ptr(t["reg"]), c.reg_slots - 1
         a.asg_ctx, a.asg_active, a.n_asg = _ptr(t["asg_ctx"]), _ptr(t["asg_active"]), c.max_assignments
         a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_tab"]), 0, c.dedup_slots - 1, _ptr(t["seq_base"])
@@ -1010,8 +1017,10 @@ class GpuInboundEngine(EngineBase):
         segs = self.__dict__.setdefault("_segs", {})
         s = segs.get(slot)
         if s is None:
-            from ..persistence.segments import PAGE_ROWS, max_block_bytes
+            from ..persistence.segments import PAGE_ROWS, SEG_ALIGN, max_block_bytes
             cap = max_block_bytes(self.out_cap, self.BLOCK_STRING_BYTES_PER_ROW * self.out_cap)
+            if self.cfg.block_index:               # + the index trailer (swindex.h)
+                cap = -(-(cap + int(self.lib.sw_seg_index_max_bytes(self.out_cap))) // SEG_ALIGN) * SEG_ALIGN
             pages = -(-self.out_cap // PAGE_ROWS)
             s = segs[slot] = (torch.empty(cap, dtype=torch.uint8, device=self.device),
                               torch.zeros(pages + 8, dtype=torch.int64, device=self.device), pages, cap)
@@ -1039,20 +1048,41 @@ class GpuInboundEngine(EngineBase):
         dev, state, pages, cap = self._seg_buffers(slot)
         a = self.args
         src = a.raw if self.world == 1 else (a.work_str or 0)
+        P = ctypes.c_void_p
         if snapshot is not None:
-            P = ctypes.c_void_p
             rc = self.lib.sw_seg_encode_snap(P(_ptr(self.out_dev[slot])), P(_ptr(self._aux_buffer(slot))), P(src),
                                              P(_ptr(self.t["cursor"])), P(_ptr(dev)), cap, P(_ptr(state)), pages,
                                              *(P(x) for x in snapshot), self._stream())
             if rc:
                 raise RuntimeError(f"sw_seg_encode_snap failed ({rc})")
-            return state[pages + 1:pages + 4]
-        rc = self.lib.sw_seg_encode(ctypes.c_void_p(_ptr(self.out_dev[slot])), ctypes.c_void_p(_ptr(self._aux_buffer(slot))),
-                                    ctypes.c_void_p(src), ctypes.c_void_p(_ptr(self.t["cursor"])),
-                                    ctypes.c_void_p(_ptr(dev)), cap, ctypes.c_void_p(_ptr(state)), pages, self._stream())
-        if rc:
-            raise RuntimeError(f"sw_seg_encode failed ({rc})")
+        else:
+            rc = self.lib.sw_seg_encode(P(_ptr(self.out_dev[slot])), P(_ptr(self._aux_buffer(slot))), P(src),
+                                        P(_ptr(self.t["cursor"])), P(_ptr(dev)), cap, P(_ptr(state)), pages,
+                                        self._stream())
+            if rc:
+                raise RuntimeError(f"sw_seg_encode failed ({rc})")
+        if self.cfg.block_index:
+            # the block's index trailer, built right behind the encoder on the same stream; its last
+            # workgroup publishes the final block bytes (state, and the host snapshot when given)
+            rc = self.lib.sw_seg_index(P(_ptr(self.out_dev[slot])), P(_ptr(self._aux_buffer(slot))), P(src),
+                                       P(_ptr(self.t["cursor"])), P(_ptr(self.store["alt"])), self.cfg.store_cap,
+                                       P(_ptr(self.t["asg_ctx"])), self.cfg.max_assignments, P(_ptr(dev)), cap,
+                                       P(_ptr(state)), pages, P(snapshot[3] if snapshot is not None else 0),
+                                       P(_ptr(self._index_scratch())), self.out_cap, self._stream())
+            if rc:
+                raise RuntimeError(f"sw_seg_index failed ({rc})")
         return state[pages + 1:pages + 4]
+
+    def _index_scratch(self) -> torch.Tensor:
+        """Scratch of the block index build (one per engine: the builds run in stream order)."""
+        t = self.__dict__.get("_ix_scratch")
+        if t is None:
+            words = int(self.lib.sw_seg_index_scratch_words(self.out_cap))
+            t = self._ix_scratch = torch.zeros(words, dtype=torch.int32, device=self.device)
+            rc = self.lib.sw_seg_index_init(ctypes.c_void_p(_ptr(t)), self.out_cap, self._stream())
+            if rc:
+                raise RuntimeError(f"sw_seg_index_init failed ({rc})")
+        return t
 
     REJECT_BYTES = 8 << 20          # compact copies of rejected payloads per step (beyond: host reads the record)
 

@@ -40,7 +40,8 @@ class _Tables(ctypes.Structure):
         [(n, _P) for n in ("zone_vtx", "zone_off", "zone_bbox", "tests", "test_hash")] + \
         [("n_tests", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
          ("batch_seq", ctypes.c_int32), ("gen_cap", ctypes.c_int64), ("presence_hash", ctypes.c_uint64),
-         ("presence_missing_ms", ctypes.c_int64), ("stats", _P)]
+         ("presence_missing_ms", ctypes.c_int64), ("stats", _P), ("cluster", ctypes.c_int32),
+         ("pad0", ctypes.c_int32)]
 
 
 class _Step(ctypes.Structure):
@@ -170,6 +171,7 @@ class NativeCpuEngine(CpuInboundEngine):
         t.gen_cap = self.cfg.gen_cap
         t.presence_hash = self.presence_hash
         t.presence_missing_ms = self.cfg.presence_missing_ms
+        t.cluster = 1 if self.cfg.cluster else 0
         t.stats = _ptr(self.stats)
         return t
 
