@@ -15,7 +15,7 @@
 //    range and its SIX_HEADS newest rows with their dates (date desc, row desc): a page-1 listing
 //    merges the heads of every block instead of decoding blocks; a block is scanned only once the
 //    merge passes its last head.
-//    A dimension whose ids reach SIX_CTX_MAX in a block is not indexed there (high-cardinality
+//    A dimension whose engine-wide context ids reach SIX_CTX_MAX is not indexed (high-cardinality
 //    contexts -- e.g. one asset per device -- are answered through their few assignments).
 //  * alternate ids: (bucket = top SIX_ALT_SORT_BITS bits of the id's 64-bit hash, row) order, a
 //    directory of the top alt_bits bits, and per id a SIX_ALT_EBITS-bit entry (hash fingerprint <<

@@ -124,13 +124,16 @@ int64_t swseg_index_append(uint8_t* block, int64_t cap, const int32_t* ctx, int6
   for (int d = 0; d < SIX_DIMS; ++d) {
     std::vector<uint32_t> kr;        // key of every row (or ~0)
     kr.assign(n, ~0u);
-    bool indexed = ctx != nullptr;     // no context table: the dimensions are not indexed
+    // indexed when the engine's context ids of this dimension (the whole table) stay below
+    // SIX_CTX_MAX; no context table: the dimensions are not indexed
+    bool indexed = ctx != nullptr;
+    for (int64_t a = 0; indexed && a < n_ctx; ++a)
+      if (ctx[4 * a + 1 + d] >= SIX_CTX_MAX) indexed = false;
     for (int64_t r = 0; indexed && r < n; ++r) {
       const int32_t a = asg[r];
       if (a < 0 || a >= n_ctx) continue;
       const int32_t c = ctx[4 * (int64_t)a + 1 + d];
       if (c < 0) continue;
-      if (c >= SIX_CTX_MAX) { indexed = false; break; }
       kr[r] = ((uint32_t)c << 3) | (uint32_t)(et[r] & 7u);
     }
     if (!indexed) {

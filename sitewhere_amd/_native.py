@@ -306,11 +306,11 @@ def gpu():
         # block index trailers + the radix sort (csrc/hip/swindex.hip)
         _proto(lib, "sw_radix_tmp_words", c_int64, c_int64)
         _proto(lib, "sw_radix_sort_u32", c_int32, P, P, P, c_int64, c_int32, P, P, P)
-        _proto(lib, "sw_seg_index_scratch_words", c_int64, c_int64)
+        _proto(lib, "sw_seg_index_scratch_words", c_int64, c_int64, c_int64)
         _proto(lib, "sw_seg_index_max_bytes", c_int64, c_int64)
-        _proto(lib, "sw_seg_index_init", c_int32, P, c_int64, P)
-        _proto(lib, "sw_seg_index", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, c_int64, P, c_int64, P, P,
-               c_int64, P)
+        _proto(lib, "sw_seg_index", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P, c_int64, P, c_int64, P, P,
+               c_int64, P, P)
+        _proto(lib, "sw_seg_index_stamp_words", c_int64, c_int64)
         _proto(lib, "sw_bloom_add", c_int32, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)

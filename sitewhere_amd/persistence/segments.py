@@ -45,6 +45,7 @@ SEG_ALIGN = 4096
 PAGE_ROWS = 1024
 PAGE_HDR = 400              # sizeof(SwSegPageHdr), csrc/include/swseg.h
 FLAG_COMMIT = 1             # the block is followed by a commit record of input offsets (swseg.h)
+FLAG_INDEX = 2              # the block carries its index trailer (swindex.h)
 MAX_SRC = 252
 HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("flags", "<u2"), ("n_rows", "<u4"), ("n_pages", "<u4"),
                 ("bytes", "<u8"), ("first_seq", "<i8"), ("recv_ms", "<i8"), ("boot", "<i8"), ("rank", "<i4"),
@@ -66,6 +67,7 @@ IX_HEADS = 16
 IX_CTX_MAX = 8192
 IX_NOT_INDEXED = 0xFFFFFFFF
 IX_ALT_EBITS = 26
+IX_MAGIC = 0x58495753
 IX_HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("n_dims", "<u2"), ("n_rows", "<u4"), ("n_pages", "<u4"),
                    ("bytes", "<u8"), ("checksum", "<u8"), ("alt_bits", "<u4"), ("alt_pbits", "<u4"), ("n_alt", "<u4"),
                    ("off_pages", "<u4"), ("off_alt_dir", "<u4"), ("off_alt", "<u4"), ("off_keys", "<u4", 3),
@@ -638,69 +640,6 @@ def boot_id(boot) -> int:
     return int(boot, 16) if isinstance(boot, str) else int(boot or 0)
 
 
-class BlockIndex:
-    """Indexes of one durable block (``swseg_index_block``), kept as memory-mapped ``.npy`` sidecars
-    under ``<store>/index/<file>-<offset>.*``:
-
-    * postings, one per row, sorted by (``pk`` = assignment index << 3 | event type, event date desc,
-      row desc); ``pd`` = date - ``min_date`` (u32; ``wide`` when some date does not fit: such a
-      block is answered by a scan), ``pr`` = row
-    * alternate ids: ``ah`` = 64-bit hash of the full id (the engine's dedup hash, sorted), ``ar`` = row
-
-    24 B per row; a lookup is a binary search per block, so a query over a billion stored events
-    touches a few pages of these files per block instead of decoding the blocks."""
-
-    PARTS = ("pk", "pd", "pr", "ah", "ar")
-    __slots__ = PARTS + ("wide", "min_date")
-
-    def __init__(self, pk, pd, pr, ah, ar, wide: bool, min_date: int):
-        self.pk, self.pd, self.pr, self.ah, self.ar = pk, pd, pr, ah, ar
-        self.wide, self.min_date = bool(wide), int(min_date)
-
-    @property
-    def nbytes(self) -> int:
-        return sum(int(getattr(self, k).nbytes) for k in self.PARTS)
-
-    @classmethod
-    def build(cls, block: np.ndarray, min_date: int) -> "BlockIndex":
-        n = int(header(block)["n_rows"])
-        pk, pd, pr = np.empty(n, np.uint32), np.empty(n, np.uint32), np.empty(n, np.uint32)
-        ah, ar = np.empty(n, np.uint64), np.empty(n, np.uint32)
-        wide = np.zeros(1, np.int32)
-        na = int(native().swseg_index_block(_p(block), int(min_date), _p(pk), _p(pd), _p(pr), _p(ah), _p(ar),
-                                            _p(wide)))
-        if na < 0:
-            raise ValueError("event block index failed")
-        return cls(pk, pd, pr, ah[:na], ar[:na], bool(wide[0]), min_date)
-
-    def save(self, base: str):
-        for k in self.PARTS:
-            tmp = f"{base}.{k}.tmp.npy"
-            np.save(tmp, np.ascontiguousarray(getattr(self, k)))
-            os.replace(tmp, f"{base}.{k}.npy")
-        with open(f"{base}.meta.tmp", "w") as f:             # written last: the index is complete
-            json.dump({"wide": self.wide, "min_date": self.min_date}, f)
-        os.replace(f"{base}.meta.tmp", f"{base}.meta")
-
-    @classmethod
-    def load(cls, base: str) -> "BlockIndex | None":
-        try:
-            with open(f"{base}.meta") as f:
-                m = json.load(f)
-            arrs = [np.load(f"{base}.{k}.npy", mmap_mode="r") for k in cls.PARTS]
-        except (OSError, ValueError):
-            return None
-        return cls(*arrs, m["wide"], m["min_date"])
-
-    @classmethod
-    def remove(cls, base: str):
-        for suffix in [f".{k}.npy" for k in cls.PARTS] + [".meta"]:
-            try:
-                os.remove(base + suffix)
-            except OSError:
-                pass
-
-
 class DurableEventStore(DeviceEventStore):
     """Event store of engine tenants on durable segments (see module docstring).
 
@@ -713,6 +652,8 @@ class DurableEventStore(DeviceEventStore):
 
     def __init__(self, directory: str, rank: int = 0, rotate_bytes: int = 1 << 30, retention_bytes: int = 0,
                  direct: bool = True, cache_blocks: int = 8, index: bool = True, index_threads: int | None = None):
+        # (index / index_threads: accepted for callers of the host indexer this store no longer needs --
+        # every block arrives with its index trailer)
         self.dir = directory
         os.makedirs(directory, exist_ok=True)
         self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
@@ -725,6 +666,8 @@ class DurableEventStore(DeviceEventStore):
         self._api_f = open(self._api_path, "ab")
         self._asg: dict[int, dict[int, list]] = {}       # boot -> assignment index -> [asg, dev, cust, area, asset]
         self._names: dict[int, dict[int, str]] = {}      # boot -> name id -> name
+        self._ctx: dict[int, dict[int, dict]] = {}       # boot -> dimension -> context token -> engine id
+        self._dict_version = 0
         self._rules: dict[str, str] = {}                 # alert type -> rule message
         self._lock = threading.RLock()
         self._dict_path = os.path.join(directory, f"dict-{rank}.log")
@@ -735,32 +678,18 @@ class DurableEventStore(DeviceEventStore):
         for e in self.seg.index():
             key = (int(e["boot"]), int(e["rank"]))
             self._high[key] = max(self._high.get(key, 0), int(e["first_seq"]) + int(e["n_rows"]))
-        self._cache: OrderedDict = OrderedDict()       # (file, offset) -> decoded columns
+        self._cache: OrderedDict = OrderedDict()       # block key -> decoded columns
         self.cache_blocks = cache_blocks
-        self._pages: OrderedDict = OrderedDict()       # (file, offset, page) -> decoded page columns
+        self._pages: OrderedDict = OrderedDict()       # (block key, page) -> decoded page columns
         self.cache_pages = 256
-        # alternate-id hashes of blocks not indexed yet (8 B per row, bounded by rows): the per-event
-        # path's store check scans them; kept apart from the decoded-block cache so it neither
-        # evicts query blocks nor re-reads a block per lookup while the indexer catches up
-        self._building: dict[tuple, threading.Event] = {}
-        self._ix_unsaved: set = set()
-        self.index_ram_bytes = 4 << 30          # newest block indexes held in RAM (older: mmapped files)
-        self._ix_ram: OrderedDict = OrderedDict()
         self.skipped_rows = 0
-        # per-block indexes (postings by assignment + type, alternate-id hashes), built in the
-        # background as blocks land and kept as memory-mapped sidecar files (see BlockIndex)
-        self._ix: dict[tuple, BlockIndex] = {}
-        self._ix_bad: set = set()
-        self._ix_version = 0
-        self._ix_tabs = None                            # (version, per-boot native lookup tables)
-        self._ix_dir = os.path.join(directory, "index")
-        self._ix_stop = threading.Event()
-        self._ix_thread = None
-        self.index_threads = index_threads or min(8, os.cpu_count() or 1)
-        if index:
-            os.makedirs(self._ix_dir, exist_ok=True)
-            self._ix_thread = threading.Thread(target=self._index_loop, daemon=True, name=f"seg-index-{rank}")
-            self._ix_thread.start()
+        # every block carries its index trailer (swindex.h, built with the block): memory maps of
+        # the trailers (LRU), the per-boot tables of trailer addresses for the native reads
+        self._tmaps: OrderedDict = OrderedDict()
+        self.max_maps = 16384
+        self._tabs = None
+        self._ctx_tabs: dict = {}
+        self.scan_threads = int(os.environ.get("SW_STORE_SCAN_THREADS", "16"))
 
     # ------------------------------------------------------------------ API-added events
     def _load_api_log(self):
@@ -820,14 +749,29 @@ class DurableEventStore(DeviceEventStore):
         self._asg.setdefault(b, {}).update({int(k): v for k, v in (d.get("asg") or {}).items()})
         self._names.setdefault(b, {}).update({int(k): v for k, v in (d.get("names") or {}).items()})
         self._rules.update(d.get("rules") or {})
+        for dim, m in (d.get("ctx") or {}).items():
+            self._ctx.setdefault(b, {}).setdefault(int(dim), {}).update({str(k): int(v) for k, v in m.items()})
+        self._dict_version += 1
 
-    def add_dictionary(self, boot, asg: dict | None = None, names: dict | None = None, rules: dict | None = None):
+    def add_dictionary(self, boot, asg: dict | None = None, names: dict | None = None, rules: dict | None = None,
+                       ctx: dict | None = None):
+        """Dictionary deltas of an engine incarnation: assignment index -> [assignment, device,
+        customer, area, asset, ...], name id -> name, rule alert type -> message, and ``ctx`` =
+        {dimension (0 customer, 1 area, 2 asset): {context token: engine id}} -- the ids the block
+        index trailers key their context dimensions by."""
         b = boot_id(boot)
         d = {"boot": b}
         if asg:
             d["asg"] = {int(k): list(v) for k, v in asg.items()}
         if names:
             d["names"] = {int(k): v for k, v in names.items()}
+        if ctx:
+            cur = self._ctx.get(b, {})
+            delta = {str(int(dim)): {str(k): int(v) for k, v in m.items() if cur.get(int(dim), {}).get(str(k)) != int(v)}
+                     for dim, m in ctx.items()}
+            delta = {k: v for k, v in delta.items() if v}
+            if delta:
+                d["ctx"] = delta
         if rules and any(self._rules.get(k) != v for k, v in rules.items()):
             d["rules"] = dict(rules)
         if len(d) == 1:
@@ -840,7 +784,7 @@ class DurableEventStore(DeviceEventStore):
 
     # ------------------------------------------------------------------ ingest
     def add_block(self, ptr: int, nbytes: int, owner=None, boot=None, asg=None, names=None, rules=None,
-                  src=None) -> int:
+                  src=None, ctx=None) -> int:
         """Queue a sealed block for the disk; returns its token.  A replay of rows already queued
         returns the token of the block holding them (-1 once they are durable).
         ``src``: input offsets the block completes (see :meth:`SegmentStore.append`; the block must
@@ -849,7 +793,7 @@ class DurableEventStore(DeviceEventStore):
         b = int(h["boot"])
         if boot is not None and boot_id(boot) != b:
             raise ValueError("dictionary boot differs from the block's")
-        self.add_dictionary(b, asg, names, rules)
+        self.add_dictionary(b, asg, names, rules, ctx)
         key, first, n = (b, int(h["rank"])), int(h["first_seq"]), int(h["n_rows"])
         if src is not None and not int(h["flags"]) & FLAG_COMMIT:
             raise ValueError("a block with input offsets must be sealed with FLAG_COMMIT")
@@ -897,9 +841,8 @@ class DurableEventStore(DeviceEventStore):
         return self.seg.flush(timeout_s)
 
     def close(self):
-        self._ix_stop.set()
-        if self._ix_thread is not None:
-            self._ix_thread.join(30)
+        self._tabs = None
+        self._tmaps.clear()
         self.seg.close()
         for f in (self._dict_f, self._api_f):
             try:
@@ -907,183 +850,216 @@ class DurableEventStore(DeviceEventStore):
             except Exception:  # noqa: BLE001
                 pass
 
-    # ------------------------------------------------------------------ block indexes
+    # ------------------------------------------------------------------ block index trailers
     @staticmethod
     def _key(ent) -> tuple:
-        return int(ent["file"]), int(ent["offset"])
+        """A block's identity across processes and reopen (segment file ids are per process)."""
+        return int(ent["boot"]), int(ent["rank"]), int(ent["first_seq"]), int(ent["n_rows"])
 
-    def _ix_base(self, key) -> str:
-        return os.path.join(self._ix_dir, f"{key[0]}-{key[1]}")
-
-    def _built(self, ent) -> "BlockIndex | None":
-        """The block's index, built once and live as soon as it is built: the indexer threads and
-        the store checks that reach a block before the indexer does share the one build in flight
-        (each used to build its own: the sampled alternate-id tenant path spent as much time in the
-        store checks' duplicate builds as in the indexer).  None: the block fails its checksum."""
+    def _trailer(self, ent):
+        """(address, bytes, header) of a block's index trailer, memory-mapped from its segment file
+        (read-only; the page cache keeps the hot ones), or None for a block without one.  The store
+        verified the trailer when it recovered the block on open or wrote it itself."""
         key = self._key(ent)
         with self._lock:
-            ix = self._ix.get(key)
-            if ix is not None:
-                return ix
-            ev = self._building.get(key)
-            mine = ev is None
-            if mine:
-                ev = self._building[key] = threading.Event()
-        if not mine:
-            ev.wait()
-            return self._ix.get(key)
-        try:
-            blk = self.seg.read_block(ent)
-            if verify(blk):
-                return None
-            ix = BlockIndex.build(blk, int(ent["min_date"]))
-            with self._lock:
-                self._ix[key] = ix
-                self._ix_unsaved.add(key)           # the indexer writes its files
-                self._ix_version += 1
-            return ix
-        finally:
-            with self._lock:
-                self._building.pop(key, None)
-            ev.set()
-
-    def _index_one(self, ent):
-        key = self._key(ent)
-        ix = self._ix.get(key)
-        if ix is None:
-            ix = BlockIndex.load(self._ix_base(key))
-            if ix is not None:
-                return ix
-            ix = self._built(ent)
-            if ix is None:
-                return None
-        if key in self._ix_unsaved:
-            ix.save(self._ix_base(key))
-            with self._lock:
-                self._ix_unsaved.discard(key)
-        return ix
-
-    def _spill_indexes(self):
-        """Keep the newest block indexes in RAM (``index_ram_bytes``) and swap older ones for their
-        file-backed (memory-mapped) copies: re-opening every index right after writing it held the
-        indexer threads (and the interpreter) in the alternate-id tenant path."""
-        for k, ix in list(self._ix.items()):
-            if not isinstance(ix.pk, np.memmap) and k not in self._ix_ram and k not in self._ix_unsaved:
-                self._ix_ram[k] = ix.nbytes
-        total = sum(self._ix_ram.values())
-        while total > self.index_ram_bytes and self._ix_ram:
-            k, nb = self._ix_ram.popitem(last=False)
-            total -= nb
-            mm = BlockIndex.load(self._ix_base(k))
-            if mm is not None and k in self._ix:
-                with self._lock:        # no version bump: the search tables keep the RAM copy alive
-                    self._ix[k] = mm
-
-    def _index_loop(self):
-        from concurrent.futures import ThreadPoolExecutor
-        pool = ThreadPoolExecutor(self.index_threads, thread_name_prefix="seg-index")
-        try:
-            while not self._ix_stop.is_set():
-                try:
-                    ents = self.seg.index()
-                except Exception:  # noqa: BLE001 -- store closing
-                    break
-                live = {self._key(e) for e in ents}
-                for k in [k for k in self._ix if k not in live]:        # retention removed the block
-                    self._ix.pop(k, None)
-                    self._ix_ram.pop(k, None)
-                    self._ix_unsaved.discard(k)
-                    self._ix_version += 1
-                    BlockIndex.remove(self._ix_base(k))
-                todo = [e for e in ents if (self._key(e) not in self._ix or self._key(e) in self._ix_unsaved)
-                        and self._key(e) not in self._ix_bad]
-                if not todo:
-                    self._ix_stop.wait(0.05)
-                    continue
-                # each index goes live as soon as it is built (not when the whole batch is): a
-                # lagging index sends store checks to block scans
-                from concurrent.futures import as_completed
-                futs = {pool.submit(self._safe_index_one, e): e for e in todo[:4 * self.index_threads]}
-                for f in as_completed(futs):
-                    e, ix = futs[f], f.result()
-                    if ix is None:
-                        self._ix_bad.add(self._key(e))
-                    else:
-                        k = self._key(e)
-                        with self._lock:
-                            # an index built here went live in _built already (same object); one
-                            # loaded from its files goes live now
-                            fresh = k not in self._ix
-                            self._ix[k] = ix
-                            if fresh:
-                                self._ix_version += 1
-                self._spill_indexes()
-        finally:
-            pool.shutdown(wait=True)
-
-    def _safe_index_one(self, ent):
-        try:
-            return self._index_one(ent)
-        except (OSError, KeyError, ValueError):
+            m = self._tmaps.get(key)
+            if m is not None:
+                self._tmaps.move_to_end(key)
+                return m[0]
+        path = self.seg.file_path(int(ent["file"]))
+        if path is None:
             return None
+        off, nb = int(ent["offset"]), int(ent["bytes"])
+        import mmap as _mmap
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            h = np.frombuffer(os.pread(fd, 64, off), HDR)[0]
+            if not int(h["flags"]) & FLAG_INDEX:
+                res = None
+                mm = None
+            else:
+                npg = int(h["n_pages"])
+                tstart = int(np.frombuffer(os.pread(fd, 4, off + 64 + 4 * npg), np.uint32)[0])
+                t0 = off + tstart
+                a0 = t0 & ~(_mmap.ALLOCATIONGRANULARITY - 1)
+                mm = _mmap.mmap(fd, off + nb - a0, prot=_mmap.PROT_READ, offset=a0)
+                arr = np.frombuffer(mm, np.uint8)
+                view = arr[t0 - a0:]
+                th = view[:128].view(IX_HDR)[0]
+                if int(th["magic"]) != IX_MAGIC or int(th["bytes"]) != nb - tstart or \
+                        int(th["n_rows"]) != int(h["n_rows"]):
+                    raise ValueError("block index trailer does not match its block")
+                res = (view.ctypes.data, int(th["bytes"]), th, view)
+        finally:
+            os.close(fd)
+        with self._lock:
+            self._tmaps[key] = (res, mm)
+            while len(self._tmaps) > self.max_maps:
+                self._tmaps.popitem(last=False)
+        return res
 
-    def index_wait(self, timeout_s: float = 60.0) -> bool:
-        """Block until every block on disk is indexed (or could not be); False on timeout."""
-        end = time.time() + timeout_s
-        while time.time() < end:
-            if all(self._key(e) in self._ix or self._key(e) in self._ix_bad for e in self.seg.index()):
-                return True
-            time.sleep(0.01)
-        return False
-
-    def alternate_hash_chunks(self, max_ids: int = 1 << 26, wait_s: float = 30.0):
-        """The stored alternate-id hashes, newest blocks first, in chunks (numpy u64), at most
-        ``max_ids``: what a restarted engine seeds its store-backed dedup filter with.  Waits up to
-        ``wait_s`` for the background indexer; blocks still unindexed then are read and hashed."""
-        self.index_wait(wait_s)
-        left = int(max_ids)
-        for e in self.seg.index()[::-1]:
-            if left <= 0:
-                break
-            ix = self._ix.get(self._key(e))
-            h = np.asarray(ix.ah if ix is not None else self._alt_index(e)[0])
-            h = h[h != 0]
-            if len(h):
-                yield h[:left]
-                left -= len(h)
-
-    def index_stats(self) -> dict:
+    def _boot_tables(self) -> dict:
+        """Per boot: the blocks (store order) and their trailer addresses (0: none) for the native
+        multi-block reads; rebuilt when the set of blocks changes (appends, retention)."""
         ents = self.seg.index()
-        return {"blocks": len(ents), "indexed": sum(self._key(e) in self._ix for e in ents),
-                "index_bytes": sum(ix.nbytes for ix in list(self._ix.values()))}
-
-    def _tables(self) -> dict:
-        """Per boot: the indexed blocks (index order) and their arrays' addresses for the native
-        multi-block searches; rebuilt when the set of indexed blocks changes."""
-        tabs = self._ix_tabs
-        ver = self._ix_version
+        ver = (len(ents), int(ents["first_seq"][-1]) if len(ents) else 0, int(ents["first_seq"][0]) if len(ents) else 0,
+               self.seg.last_token)
+        tabs = self._tabs
         if tabs is not None and tabs[0] == ver:
             return tabs[1]
-        by_boot: dict[int, list] = {}
-        for e in self.seg.index():
-            ix = self._ix.get(self._key(e))
-            if ix is not None:
-                by_boot.setdefault(int(e["boot"]), []).append((e, ix))
-        out = {}
+        out: dict = {}
+        for e in ents:
+            out.setdefault(int(e["boot"]), []).append(e)
+        res = {}
         P = ctypes.c_void_p
-        for b, lst in by_boot.items():
-            n = len(lst)
-            addr = lambda a: a.ctypes.data if len(a) else 0  # noqa: E731
-            out[b] = {"ents": [e for e, _ in lst], "ixs": [ix for _, ix in lst], "n": n,
-                      "pk": (P * n)(*[addr(ix.pk) for _, ix in lst]), "pd": (P * n)(*[addr(ix.pd) for _, ix in lst]),
-                      "ah": (P * n)(*[addr(ix.ah) for _, ix in lst]),
-                      "npk": np.array([len(ix.pk) for _, ix in lst], np.int64),
-                      "nah": np.array([len(ix.ah) for _, ix in lst], np.int64),
-                      "base": np.array([ix.min_date for _, ix in lst], np.int64),
-                      "wide": np.array([ix.wide for _, ix in lst], bool),
-                      "keys": {self._key(e) for e, _ in lst}}
-        self._ix_tabs = (ver, out)
+        for b, lst in out.items():
+            trs = [self._trailer(e) for e in lst]
+            addrs = [t[0] if t is not None else 0 for t in trs]
+            res[b] = {"ents": lst, "tr": trs, "n": len(lst), "addr": (P * len(lst))(*addrs),
+                      "first": np.array([int(e["first_seq"]) for e in lst], np.int64),
+                      "world": np.array([int(e["world"]) for e in lst], np.int64),
+                      "rank": np.array([int(e["rank"]) for e in lst], np.int64)}
+        live = {self._key(e) for e in ents}
+        with self._lock:
+            for k in [k for k in self._tmaps if k not in live]:      # retention removed the block
+                self._tmaps.pop(k, None)
+        self._tabs = (ver, res)
+        return res
+
+    def index_wait(self, timeout_s: float = 60.0) -> bool:
+        """Every block is indexed as it is written (its trailer): nothing to wait for."""
+        return True
+
+    def index_stats(self) -> dict:
+        tabs = self._boot_tables()
+        n = sum(t["n"] for t in tabs.values())
+        ix = [tr for t in tabs.values() for tr in t["tr"] if tr is not None]
+        return {"blocks": n, "indexed": len(ix), "index_bytes": sum(tr[1] for tr in ix)}
+
+    def alternate_id_count(self) -> int:
+        """Alternate ids stored (every block's trailer count; blocks without a trailer decoded)."""
+        total = 0
+        for t in self._boot_tables().values():
+            for e, tr in zip(t["ents"], t["tr"]):
+                total += int(tr[2]["n_alt"]) if tr is not None else len(self._block_alt_hashes(e))
+        return total
+
+    def _block_alt_hashes(self, ent) -> np.ndarray:
+        blk = self.seg.read_block(ent)
+        out = np.empty(int(ent["n_rows"]), np.uint64)
+        n = int(native().swseg_alt_hashes(_p(blk), _p(out), len(out)))
+        if n < 0:
+            raise ValueError("event block decode failed")
+        return out[:n]
+
+    def alternate_hash_chunks(self, max_ids: int = 1 << 26, wait_s: float = 0.0, threads: int = 16):
+        """The stored alternate-id hashes, newest blocks first, one numpy u64 chunk per block, at most
+        ``max_ids``: what a restarted engine seeds its store-backed dedup filter with.  The trailers
+        keep only fingerprints, so the blocks' id columns are decoded (natively, on ``threads``
+        threads; ctypes releases the interpreter meanwhile)."""
+        from concurrent.futures import ThreadPoolExecutor
+        ents = [e for t in self._boot_tables().values() for e in t["ents"]]
+        ents.sort(key=lambda e: (int(e["recv_ms"]), int(e["first_seq"])), reverse=True)
+        left = int(max_ids)
+        with ThreadPoolExecutor(max(1, threads)) as pool:
+            for i in range(0, len(ents), max(1, threads)):
+                if left <= 0:
+                    break
+                for h in pool.map(self._block_alt_hashes, ents[i:i + threads]):
+                    if left <= 0:
+                        break
+                    if len(h):
+                        yield h[:left]
+                        left -= len(h)
+
+    def _alt_candidates(self, hashes) -> dict:
+        """hash -> [(boot table, block position, page)] of the blocks whose trailer holds a fingerprint
+        match, newest block first (native, over every block of every boot per hash)."""
+        lib = native()
+        out: dict = {}
+        cap = 256
+        bo, po = np.empty(cap, np.int64), np.empty(cap, np.int64)
+        for b, t in self._boot_tables().items():
+            for hv in hashes:
+                k = int(lib.swseg_ix_alt_pages(t["addr"], t["n"], int(hv), _p(bo), _p(po), cap))
+                for j in range(min(k, cap)):
+                    out.setdefault(int(hv), []).append((t, int(bo[j]), int(po[j])))
         return out
+
+    def _page_alt_rows(self, ent, page: int, hv: int) -> list:
+        """Rows of one page whose alternate id hashes to hv (newest first), with their ids."""
+        from ..pipeline.fleet import hash64_strs
+        c = self._page_cols(ent, page)
+        rows = [i for i in range(len(c["date"])) if int(c["flags"][i]) & SEGF_HAS_ALT]
+        if not rows:
+            return []
+        alts = [row_strings(c, i)[0] for i in rows]
+        hs = hash64_strs(alts)
+        return [(int(c["row0"]) + i, a) for i, a, h in sorted(zip(rows, alts, hs.tolist()), reverse=True)
+                if int(h) == hv]
+
+    def find_alternate_hashes(self, hashes, covered: tuple | None = None, indexed_only: bool = False) -> dict:
+        """alt-id hash -> event id string for the hashes stored on disk, the newest event per hash
+        (store-backed dedup beyond the engine's window: ``AlternateIdDeduplicator`` asks the event
+        store whether the id was ever seen).  Every block's trailer is searched natively; a
+        fingerprint hit is confirmed on its page (the full 64-bit hash of the stored id string).
+        ``covered`` / ``indexed_only``: kept for callers; blocks without a trailer (older stores) are
+        scanned unless ``indexed_only``."""
+        want = [int(h) for h in np.unique(np.asarray(list(hashes), np.uint64))]
+        found: dict = {}
+        if not want:
+            return found
+        cands = self._alt_candidates(want)
+        for hv, lst in cands.items():
+            # newest first: boot tables in store order, blocks newest first within a boot
+            lst.sort(key=lambda x: (int(x[0]["ents"][x[1]]["recv_ms"]), x[1]), reverse=True)
+            for t, bi, page in lst:
+                e = t["ents"][bi]
+                hit = self._page_alt_rows(e, page, hv)
+                if hit:
+                    found[hv] = f"{int(e['boot']):x}-{int(self._eids(e, [hit[0][0]])[0])}"
+                    break
+        if not indexed_only:
+            for t in self._boot_tables().values():
+                for e, tr in zip(t["ents"], t["tr"]):
+                    if tr is not None:
+                        continue
+                    if covered is not None and int(e["boot"]) == covered[0] and int(e["rank"]) == covered[1] \
+                            and int(e["first_seq"]) >= covered[2]:
+                        continue
+                    cols = self._decoded(e)
+                    for i in range(len(cols["date"]) - 1, -1, -1):
+                        if not int(cols["flags"][i]) & SEGF_HAS_ALT:
+                            continue
+                        from ..pipeline.fleet import hash64
+                        hv = hash64(row_strings(cols, i)[0])
+                        if hv in want and hv not in found:
+                            found[hv] = f"{int(e['boot']):x}-{int(self._eids(e, [i])[0])}"
+        return found
+
+    def get_event_by_alternate_id(self, alt: str):
+        from ..pipeline.fleet import hash64
+        ev = self._objects.get_event_by_alternate_id(alt)
+        if ev is not None:
+            return ev
+        h = hash64(alt)
+        lst = self._alt_candidates([h]).get(h, [])
+        lst.sort(key=lambda x: (int(x[0]["ents"][x[1]]["recv_ms"]), x[1]), reverse=True)
+        for t, bi, page in lst:
+            e = t["ents"][bi]
+            c = self._page_cols(e, page)
+            for r, a in self._page_alt_rows(e, page, h):
+                if a == alt:
+                    return self._materialize(c, r - int(c["row0"]))
+        for t in self._boot_tables().values():                 # blocks without a trailer
+            for e, tr in zip(t["ents"][::-1], t["tr"][::-1]):
+                if tr is not None:
+                    continue
+                cols = self._decoded(e)
+                for i in range(len(cols["date"]) - 1, -1, -1):
+                    if int(cols["flags"][i]) & SEGF_HAS_ALT and row_strings(cols, i)[0] == alt:
+                        return self._materialize(cols, i)
+        return None
 
     # ------------------------------------------------------------------ page reads
     def _read_pages(self, ent, p0: int, p1: int) -> np.ndarray:
@@ -1181,13 +1157,13 @@ class DurableEventStore(DeviceEventStore):
                 set_commit_flag(blk)
                 owner = blk
             tok = self.add_block(blk.ctypes.data, len(blk), owner=owner, boot=d["boot"], asg=d.get("asg"),
-                                 names=d.get("names"), rules=d.get("rules"), src=src)
+                                 names=d.get("names"), rules=d.get("rules"), src=src, ctx=d.get("ctx"))
         else:
             from .columnar import decode_batch
             d = decode_batch(payload)
             rows = d["rows"]
             n = len(rows)
-            blk = encode_block(rows)
+            blk = encode_block(rows, index=True)       # zone maps; rows carry no strings / context ids
             seal(blk, int(d["first_seq"]), int(d["now"]), boot_id(d["boot"]), int(d["rank"]), int(d["world"]))
             src = d.get("src") or None
             if src is not None:
@@ -1207,112 +1183,6 @@ class DurableEventStore(DeviceEventStore):
     @staticmethod
     def _eids(h, idx) -> np.ndarray:
         return (int(h["first_seq"]) + np.asarray(idx, np.int64)) * int(h["world"]) + int(h["rank"])
-
-    def _alt_index(self, ent) -> tuple[np.ndarray, np.ndarray]:
-        """(sorted alternate-id hashes, their rows) of a block: its index, built now (and shared with
-        the indexer, ``_built``) when the background indexer has not reached the block yet."""
-        ix = self._built(ent)
-        if ix is None:
-            raise ValueError("event block checksum mismatch")
-        return ix.ah, ix.ar
-
-    def _alt_rows(self, ent, want: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
-        """(hashes, rows) of a block's rows whose alternate-id hash is in ``want`` (sorted unique)."""
-        ix = self._ix.get(self._key(ent))
-        ah, ar = (ix.ah, ix.ar) if ix is not None else self._alt_index(ent)
-        if not len(ah):
-            return np.zeros(0, np.uint64), np.zeros(0, np.int64)
-        lo = np.searchsorted(ah, want, "left")
-        hi = np.searchsorted(ah, want, "right")
-        sel = np.nonzero(hi > lo)[0]
-        if not len(sel):
-            return np.zeros(0, np.uint64), np.zeros(0, np.int64)
-        idx = np.concatenate([np.arange(lo[i], hi[i]) for i in sel])
-        return np.asarray(ah[idx]), np.asarray(ar[idx], np.int64)
-
-    def find_alternate_hashes(self, hashes, covered: tuple | None = None, indexed_only: bool = False) -> dict:
-        """alt-id hash -> event id string for the hashes present on disk, the newest event per hash
-        (store-backed dedup beyond the engine's window: ``AlternateIdDeduplicator`` asks the event
-        store whether the id was ever seen).  ``covered`` = (boot, rank, sequence): that engine's
-        dedup window still holds every id of its rows from ``sequence`` on, so its blocks there that
-        are not indexed yet need no scan (the caller asks only about ids the window does not hold).
-        ``indexed_only``: no block scans at all (binary searches of the indexed blocks only)."""
-        want = np.unique(np.asarray(list(hashes), np.uint64))
-        found = {}
-        if not len(want):
-            return found
-        ents = self.seg.index()
-        order: dict = {}
-        best: dict[int, tuple] = {}                      # hash -> (store position, event id, boot)
-
-        def store_pos(e) -> int:                         # built on the first hit only
-            if not order:
-                order.update({self._key(x): k for k, x in enumerate(ents)})
-            return order.get(self._key(e), -1)
-
-        def offer(hv, pos, eid, boot):
-            cur = best.get(hv)
-            if cur is None or (pos, eid) > cur[:2]:
-                best[hv] = (pos, eid, boot)
-
-        # indexed blocks: one native pass per boot over every block's sorted hashes (the newest
-        # block holding each id), instead of a search per block in Python
-        lib = native()
-        blk, at = np.empty(len(want), np.int64), np.empty(len(want), np.int64)
-        indexed = set()
-        for tab in self._tables().values():
-            indexed |= tab["keys"]
-            lib.swseg_multi_find_u64(tab["ah"], _p(tab["nah"]), tab["n"], _p(want), len(want), _p(blk), _p(at))
-            for j in np.nonzero(blk >= 0)[0].tolist():
-                e = tab["ents"][int(blk[j])]
-                row = int(tab["ixs"][int(blk[j])].ar[int(at[j])])
-                offer(int(want[j]), store_pos(e), int(self._eids(e, [row])[0]), int(e["boot"]))
-        if not indexed_only:
-            for k in range(len(ents) - 1, -1, -1):       # blocks not indexed yet: scanned, newest first
-                e = ents[k]
-                if self._key(e) in indexed or self._ix.get(self._key(e)) is not None:
-                    continue
-                if covered is not None and int(e["boot"]) == covered[0] and int(e["rank"]) == covered[1] \
-                        and int(e["first_seq"]) >= covered[2]:
-                    continue
-                hs, rows = self._alt_rows(e, want)
-                if len(rows):
-                    for hv, eid in zip(hs.tolist(), self._eids(e, rows).tolist()):
-                        offer(int(hv), k, int(eid), int(e["boot"]))
-        for hv, (_, eid, boot) in best.items():
-            found[hv] = f"{boot:x}-{eid}"
-        return found
-
-    def get_event_by_alternate_id(self, alt: str):
-        from ..pipeline.fleet import hash64
-        ev = self._objects.get_event_by_alternate_id(alt)
-        if ev is not None:
-            return ev
-        h = hash64(alt)
-        want = np.array([h], np.uint64)
-        hits = {}                                      # indexed block -> rows with the hash
-        indexed = set()
-        lib = native()
-        for tab in self._tables().values():
-            lo, hi = np.zeros(tab["n"], np.int64), np.zeros(tab["n"], np.int64)
-            lib.swseg_multi_range_u64(tab["ah"], _p(tab["nah"]), tab["n"], int(h), _p(lo), _p(hi))
-            for i in np.nonzero(hi > lo)[0]:
-                ix = tab["ixs"][i]
-                hits[self._key(tab["ents"][i])] = np.asarray(ix.ar[int(lo[i]):int(hi[i])], np.int64)
-            indexed |= tab["keys"]
-        for e in self.seg.index()[::-1]:               # newest first: the latest event with the id
-            k = self._key(e)
-            if k in indexed:
-                rows = hits.get(k)
-                if rows is None:
-                    continue
-            else:
-                _, rows = self._alt_rows(e, want)
-            for r in sorted(rows.tolist(), reverse=True):
-                c, i = self._row_event(e, r)
-                if row_strings(c, i)[0] == alt:
-                    return self._materialize(c, i)
-        return None
 
     def get_event_by_id(self, id: str):
         boot, sep, num = id.rpartition("-")
@@ -1338,57 +1208,216 @@ class DurableEventStore(DeviceEventStore):
     def list_command_responses_for_invocation(self, invocation_id, criteria=None):
         return self._objects.list_command_responses_for_invocation(invocation_id, criteria)
 
-    def _block_hits(self, e, et: int, a: np.ndarray, c: DateRangeSearchCriteria, need: int):
-        """(count, dates, rows) of a block's rows of type ``et`` whose assignment index is in ``a``
-        within the date range; ``dates`` / ``rows`` hold at least the ``need`` newest of them (all of
-        them when the block is not indexed)."""
-        ix = self._ix.get(self._key(e))
-        if ix is None or ix.wide:
-            cols = self._decoded(e)
-            m = (cols["etype"] == et) & np.isin(cols["asg"], a)
-            if c.start_date is not None:
-                m &= cols["date"] >= c.start_date
-            if c.end_date is not None:
-                m &= cols["date"] <= c.end_date
-            idx = np.nonzero(m)[0]
-            return len(idx), cols["date"][idx], idx
-        keys = (a.astype(np.uint64) << np.uint64(3)) | np.uint64(et)
-        keys = keys.astype(np.uint32)
-        lo = np.searchsorted(ix.pk, keys, "left")
-        hi = np.searchsorted(ix.pk, keys, "right")
-        sel = np.nonzero(hi > lo)[0]
-        if not len(sel):
-            return 0, np.zeros(0, np.int64), np.zeros(0, np.int64)
-        base = int(ix.min_date)
-        bounded = c.start_date is not None or c.end_date is not None
-        count, dates, rows = 0, [], []
-        for i in sel:
-            l, h = int(lo[i]), int(hi[i])
-            d = np.asarray(ix.pd[l:h], np.int64) + base         # newest first within the key
-            if bounded:
-                # dates descend within a key: the range is one contiguous slice
-                if c.end_date is not None:
-                    l2 = int(np.searchsorted(-d, -c.end_date, "left"))
-                else:
-                    l2 = 0
-                h2 = int(np.searchsorted(-d, -c.start_date, "right")) if c.start_date is not None else len(d)
-                d = d[l2:h2]
-                r = np.asarray(ix.pr[l + l2:l + h2], np.int64)
+    # ------------------------------------------------------------------ listings
+    def _pages_of(self, ent, tr):
+        """SwIxPage rows of a block (from its trailer, or its page headers when it has none)."""
+        if tr is not None:
+            th, view = tr[2], tr[3]
+            o = int(th["off_pages"])
+            return view[o:o + 32 * int(th["n_pages"])].view(IX_PAGE)
+        blk = self.seg.read_block(ent)
+        ps = page_summary(blk)
+        pt = blk[64:64 + 4 * (len(ps) + 1)].view(np.uint32)
+        out = np.zeros(len(ps), IX_PAGE)
+        out["asg_min"], out["asg_max"], out["date_min"], out["date_max"] = ps[:, 2], ps[:, 3], ps[:, 4], ps[:, 5]
+        out["off"], out["bytes"] = pt[:-1], np.diff(pt)
+        return out
+
+    def _scan_pages(self, tasks, et: int, d_lo: int, d_hi: int, asg: int = -1, ctx_tab=None, ctx_id: int = 0):
+        """Rows of pages passing (type, date range, assignment | context id), reading each page's
+        leading columns only (native ``swseg_scan_pages``, multi-threaded).  tasks: [(block entry,
+        page, page offset, page bytes)] -> [(task index, row in block, date)] arrays."""
+        if not tasks:
+            return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int64)
+        fds: dict = {}
+        try:
+            fd = np.empty(len(tasks), np.int32)
+            for i, (e, _, _, _) in enumerate(tasks):
+                path = self.seg.file_path(int(e["file"]))
+                if path is None:
+                    raise KeyError("segment file deleted by retention")
+                if path not in fds:
+                    fds[path] = os.open(path, os.O_RDONLY)
+                fd[i] = fds[path]
+            boff = np.array([int(t[0]["offset"]) for t in tasks], np.int64)
+            poff = np.array([int(t[2]) for t in tasks], np.uint32)
+            pby = np.array([int(t[3]) for t in tasks], np.uint32)
+            pix = np.array([int(t[1]) for t in tasks], np.int32)
+            ct = np.ascontiguousarray(ctx_tab, np.int32) if ctx_tab is not None else np.zeros(1, np.int32)
+            cap = 4096
+            while True:
+                ot, orow, od = np.empty(cap, np.int64), np.empty(cap, np.int32), np.empty(cap, np.int64)
+                k = int(native().swseg_scan_pages(_p(fd), _p(boff), _p(poff), _p(pby), _p(pix), len(tasks), int(et),
+                                                  int(asg), _p(ct), len(ct) if ctx_tab is not None else 0, int(ctx_id),
+                                                  int(d_lo), int(d_hi), self.scan_threads, _p(ot), _p(orow), _p(od), cap))
+                if k < 0:
+                    raise ValueError(f"event page unreadable (task {-k - 1})")
+                if k <= cap:
+                    return ot[:k], orow[:k], od[:k]
+                cap = k
+        finally:
+            for f in fds.values():
+                os.close(f)
+
+    def _rows_for(self, t, blocks, et, d_lo, d_hi, asg=-1, ctx_tab=None, ctx_id=0, pages=None):
+        """(block position, row, date) of every matching row of the listed blocks (all pages, or the
+        pages whose zone maps hold ``asg``)."""
+        tasks, owner = [], []
+        for bi in blocks:
+            e, tr = t["ents"][bi], t["tr"][bi]
+            pg = self._pages_of(e, tr)
+            for p in range(len(pg)):
+                z = pg[p]
+                if int(z["date_max"]) < d_lo or int(z["date_min"]) > d_hi:
+                    continue
+                if asg >= 0 and not (int(z["asg_min"]) <= asg <= int(z["asg_max"])):
+                    continue
+                tasks.append((e, p, int(z["off"]), int(z["bytes"])))
+                owner.append(bi)
+        ti, rows, dates = self._scan_pages(tasks, et, d_lo, d_hi, asg, ctx_tab, ctx_id)
+        own = np.asarray(owner, np.int64)
+        return (own[ti] if len(ti) else np.zeros(0, np.int64)), rows.astype(np.int64), dates
+
+    def _asg_pages(self, t, asg: int, d_lo: int, d_hi: int) -> list:
+        """(block position, page) pairs whose assignment / date zone maps admit the assignment."""
+        cap = max(1024, 4 * t["n"])
+        bo, po = np.empty(cap, np.int64), np.empty(cap, np.int64)
+        k = int(native().swseg_ix_asg_pages(t["addr"], t["n"], int(asg), int(d_lo), int(d_hi), _p(bo), _p(po), cap))
+        if k > cap:
+            bo, po = np.empty(k, np.int64), np.empty(k, np.int64)
+            k = int(native().swseg_ix_asg_pages(t["addr"], t["n"], int(asg), int(d_lo), int(d_hi), _p(bo), _p(po), k))
+        return list(zip(bo[:k].tolist(), po[:k].tolist()))
+
+    def _list_assignments(self, t, asg_idx, et, d_lo, d_hi) -> tuple[int, list]:
+        """Rows of the assignments over one boot's blocks: the blocks are clustered by assignment, so
+        the page zone maps name one or two pages per block, read as their leading columns."""
+        parts = []
+        legacy = [bi for bi, tr in enumerate(t["tr"]) if tr is None]
+        for a in asg_idx:
+            tasks, owner = [], []
+            for bi, p in self._asg_pages(t, a, d_lo, d_hi):
+                e, tr = t["ents"][bi], t["tr"][bi]
+                z = self._pages_of(e, tr)[p]
+                tasks.append((e, p, int(z["off"]), int(z["bytes"])))
+                owner.append(bi)
+            ti, rows, dates = self._scan_pages(tasks, et, d_lo, d_hi, asg=int(a))
+            own = np.asarray(owner, np.int64)
+            if len(ti):
+                parts.append((own[ti], rows.astype(np.int64), dates))
+            if legacy:
+                parts.append(self._rows_for(t, legacy, et, d_lo, d_hi, asg=int(a)))
+        return self._collect(t, parts)
+
+    @staticmethod
+    def _collect(t, parts) -> tuple[int, list]:
+        if not parts:
+            return 0, []
+        bi = np.concatenate([p[0] for p in parts])
+        rows = np.concatenate([p[1] for p in parts])
+        dates = np.concatenate([p[2] for p in parts])
+        eids = (t["first"][bi] + rows) * t["world"][bi] + t["rank"][bi]
+        return len(rows), [(dates, eids, bi, rows, t)]
+
+    def _ctx_table(self, boot: int, pos: int) -> np.ndarray | None:
+        """Context id (dimension pos - 2) by assignment index for one boot, from the dictionaries;
+        None when the boot's context ids are unknown."""
+        key = (boot, pos, self._dict_version)
+        tab = self._ctx_tabs.get(key)
+        if tab is not None:
+            return tab
+        ids = self._ctx.get(boot, {}).get(pos - 2)
+        if not ids:
+            return None
+        asg = self._asg.get(boot, {})
+        n = (max(asg) + 1) if asg else 0
+        tab = np.full(n, -1, np.int32)
+        for i, ctx in asg.items():
+            if len(ctx) > pos and ctx[pos] in ids:
+                tab[int(i)] = ids[ctx[pos]]
+        self._ctx_tabs = {k: v for k, v in self._ctx_tabs.items() if k[2] == self._dict_version}
+        self._ctx_tabs[key] = tab
+        return tab
+
+    def _list_context(self, t, boot, pos, want, et, d_lo, d_hi, need) -> tuple[int, list]:
+        """Rows of customer / area / asset ids over one boot's blocks, from the trailers' key tables:
+        exact totals from the per-key counts (a block straddling a date bound is scanned for its
+        count), the newest rows from the per-key heads merged across blocks; a block whose heads the
+        merge runs past is scanned."""
+        d = pos - 2
+        ids = self._ctx.get(boot, {}).get(d, {})
+        ctx_tab = self._ctx_table(boot, pos)
+        bounded = d_lo > -(1 << 62) or d_hi < (1 << 62)
+        if ctx_tab is None:                           # no context ids for this boot: via assignments
+            asg_idx = [i for i, ctx in self._asg.get(boot, {}).items() if len(ctx) > pos and ctx[pos] in want]
+            return self._list_assignments(t, asg_idx, et, d_lo, d_hi)
+        lib = native()
+        n = t["n"]
+        total, parts, heads = 0, [], []
+        maybe = []                                    # (block, last head date, last head eid, cid)
+        scan = {}                                     # block -> ctx ids to scan it for
+        for tok in want:
+            cid = ids.get(tok)
+            if cid is None:
+                continue
+            out = np.zeros(7 * n, np.int64)
+            lib.swseg_ix_ctx_find(t["addr"], n, d, (int(cid) << 3) | int(et), _p(out))
+            o = out.reshape(n, 7)
+            for bi in np.nonzero(o[:, 0] != 0)[0].tolist():
+                st, cnt, dmin, dmax, ha, nh, da = (int(x) for x in o[bi])
+                if st < 0 or (bounded and not (dmax < d_lo or dmin > d_hi) and not (d_lo <= dmin and dmax <= d_hi)):
+                    scan.setdefault(bi, set()).add(int(cid))       # not indexed here / straddles a bound
+                    continue
+                if dmax < d_lo or dmin > d_hi:
+                    continue
+                total += cnt
+                hr = np.ctypeslib.as_array((ctypes.c_uint32 * nh).from_address(ha)).astype(np.int64) if nh else \
+                    np.zeros(0, np.int64)
+                hd = np.ctypeslib.as_array((ctypes.c_int64 * nh).from_address(da)).copy() if nh else \
+                    np.zeros(0, np.int64)
+                heads.append((np.full(nh, bi, np.int64), hr, hd))
+                if cnt > nh:
+                    maybe.append((bi, int(hd[-1]), int(hr[-1]), int(cid)))
+        # blocks to scan in full (exact rows): not indexed, straddling a date bound, or heads exhausted
+        def scan_blocks(blks):
+            got = []
+            for bi, cids in blks.items():
+                for cid in cids:
+                    b, r, dt = self._rows_for(t, [bi], et, d_lo, d_hi, ctx_tab=ctx_tab, ctx_id=cid)
+                    got.append((b, r, dt))
+            return got
+        scanned = scan_blocks(scan)
+        total += sum(len(x[1]) for x in scanned)
+        cand = heads + scanned
+        if maybe and need > 0:
+            # the cutoff of the merged heads: a block whose last head is above it may hold more
+            bi_ = np.concatenate([c[0] for c in cand]) if cand else np.zeros(0, np.int64)
+            rows_ = np.concatenate([c[1] for c in cand]) if cand else np.zeros(0, np.int64)
+            dates_ = np.concatenate([c[2] for c in cand]) if cand else np.zeros(0, np.int64)
+            eids_ = ((t["first"][bi_] + rows_) * t["world"][bi_] + t["rank"][bi_]) if len(bi_) else \
+                np.zeros(0, np.int64)
+            if len(dates_) >= need:
+                order = np.lexsort((-eids_, -dates_))
+                cut = order[need - 1]
+                cut_d, cut_e = int(dates_[cut]), int(eids_[cut])
             else:
-                r = np.asarray(ix.pr[l:h], np.int64)
-            count += len(d)
-            if need > 0:
-                dates.append(d[:need])
-                rows.append(r[:need])
-        if not rows:
-            return count, np.zeros(0, np.int64), np.zeros(0, np.int64)
-        return count, np.concatenate(dates), np.concatenate(rows)
+                cut_d, cut_e = None, None
+            more: dict = {}
+            for bi, ld, lr, cid in maybe:
+                le = (int(t["first"][bi]) + lr) * int(t["world"][bi]) + int(t["rank"][bi])
+                if cut_d is None or (ld, le) > (cut_d, cut_e):
+                    more.setdefault(bi, set()).add(cid)
+            if more:
+                extra = scan_blocks(more)
+                drop = set(more)
+                cand = [(b[~np.isin(b, list(drop))], r[~np.isin(b, list(drop))], dt[~np.isin(b, list(drop))])
+                        for b, r, dt in cand] + extra
+        return self._collect(t, cand)
 
     def list_events(self, event_type, index, entity_ids, criteria: DateRangeSearchCriteria | None = None):
-        """Events of one type for entities of an index, newest first.  Indexed blocks answer from
-        their postings (assignment + type, dates descending): the total is a sum of posting-range
-        lengths and only the requested page's rows are read (one page read each); blocks not
-        indexed yet are decoded and scanned."""
+        """Events of one type for entities of an index, newest first, with the exact total.
+        Assignment: page zone maps of the assignment-clustered blocks, then those pages' leading
+        columns.  Customer / area / asset: the trailers' per-key counts and heads (see
+        :meth:`_list_context`).  API-added events join from their own store."""
         c = criteria or DateRangeSearchCriteria(page_size=100)
         et = _ETYPE.get(DeviceEventType(event_type))
         objs = self._objects.list_events(event_type, index, entity_ids, DateRangeSearchCriteria(
@@ -1397,67 +1426,43 @@ class DurableEventStore(DeviceEventStore):
             return SearchResults(len(objs), c.slice(objs))
         pos = _CTX[DeviceEventIndex(index)]
         want = set(entity_ids)
-        with self._lock:
-            asg_idx = {b: np.array(sorted(i for i, ctx in d.items() if ctx[pos] in want), np.int64)
-                       for b, d in self._asg.items()}
         paged = c.page_size > 0
         need = max(1, c.page_number) * c.page_size if paged else 1 << 62
-        total = len(objs)
-        parts = []                     # (dates, eids, block entry, rows)
-        tabs = self._tables()
-        lib = native()
         d_lo = c.start_date if c.start_date is not None else -(1 << 62)
         d_hi = c.end_date if c.end_date is not None else (1 << 62)
-        done = set()
-        for b, a in asg_idx.items():
-            tab = tabs.get(b)
-            if tab is None or not len(a):
-                continue
-            lo, hi = np.zeros(tab["n"], np.int64), np.zeros(tab["n"], np.int64)
-            for key in ((a.astype(np.uint64) << np.uint64(3)) | np.uint64(et)).astype(np.uint32).tolist():
-                lib.swseg_multi_range_u32(tab["pk"], tab["pd"], _p(tab["npk"]), _p(tab["base"]), tab["n"], key,
-                                          int(d_lo), int(d_hi), _p(lo), _p(hi))
-                cnt = hi - lo
-                cnt[tab["wide"]] = 0                       # wide blocks: scanned below
-                total += int(cnt.sum())
-                for i in np.nonzero(cnt > 0)[0]:
-                    e, ix = tab["ents"][i], tab["ixs"][i]
-                    l, h = int(lo[i]), int(min(hi[i], lo[i] + need))
-                    r = np.asarray(ix.pr[l:h], np.int64)
-                    parts.append((np.asarray(ix.pd[l:h], np.int64) + ix.min_date, self._eids(e, r), e, r))
-            done |= {self._key(e) for e, w in zip(tab["ents"], tab["wide"]) if not w}
-        for e in self.seg.index():                     # blocks not indexed (yet): decode and scan
-            if self._key(e) in done:
-                continue
-            a = asg_idx.get(int(e["boot"]))
-            if a is None or not len(a):
-                continue
-            if c.start_date is not None and int(e["max_date"]) < c.start_date:
-                continue
-            if c.end_date is not None and int(e["min_date"]) > c.end_date:
-                continue
-            n, d, r = self._block_hits(e, et, a, c, need)
+        total = len(objs)
+        found = []                                    # (dates, eids, block positions, rows, table)
+        for b, t in self._boot_tables().items():
+            if pos == 0:
+                with self._lock:
+                    asg_idx = [i for i, ctx in self._asg.get(b, {}).items() if ctx[0] in want]
+                n, parts = self._list_assignments(t, asg_idx, et, d_lo, d_hi)
+            else:
+                n, parts = self._list_context(t, b, pos, want, et, d_lo, d_hi, need)
             total += n
-            if len(r):
-                parts.append((d, self._eids(e, r), e, r))
-        if not parts:
+            found.extend(parts)
+        if not found:
             return SearchResults(total, c.slice(objs))
-        dates = np.concatenate([x[0] for x in parts])
-        eids = np.concatenate([x[1] for x in parts])
-        which = np.concatenate([np.full(len(x[0]), k, np.int32) for k, x in enumerate(parts)])
-        rows = np.concatenate([x[3] for x in parts])
+        dates = np.concatenate([x[0] for x in found])
+        eids = np.concatenate([x[1] for x in found])
+        which = np.concatenate([np.full(len(x[0]), k, np.int32) for k, x in enumerate(found)])
+        pos_ = np.concatenate([x[2] for x in found])
+        rows = np.concatenate([x[3] for x in found])
         order = np.lexsort((-eids, -dates))
+
+        def mat(o):
+            t = found[which[o]][4]
+            return self._materialize(*self._row_event(t["ents"][int(pos_[o])], int(rows[o])))
         if objs:
             if paged:
                 order = order[:need + len(objs)]
-            merged = [self._materialize(*self._row_event(parts[which[o]][2], int(rows[o]))) for o in order] + objs
+            merged = [mat(o) for o in order] + objs
             merged.sort(key=lambda ev: -(ev.event_date or 0))
             return SearchResults(total, c.slice(merged))
         if paged:
             start = (max(1, c.page_number) - 1) * c.page_size
             order = order[start:start + c.page_size]
-        return SearchResults(total, [self._materialize(*self._row_event(parts[which[o]][2], int(rows[o])))
-                                     for o in order])
+        return SearchResults(total, [mat(o) for o in order])
 
     def _materialize(self, cols: dict, i: int):
         b = cols["header"]["boot"]

@@ -341,6 +341,19 @@ class EngineBase:
 
     _ctx_version = 0
 
+    def ctx_key_spaces(self) -> np.ndarray:
+        """Per context dimension (customer, area, asset) the block index's key space: (max context
+        id + 1) << 3, 0 when no assignment has one, -1 when ids reach the indexed range's end
+        (swindex.h SIX_CTX_MAX: that dimension goes unindexed)."""
+        ks = self.__dict__.get("_ctx_keys")
+        if ks is None or ks[0] != self._ctx_version:
+            out = np.zeros(3, np.int32)
+            for d, col in enumerate((self.asg_customer, self.asg_area, self.asg_asset)):
+                m = int(col.max()) if len(col) else -1
+                out[d] = -1 if m >= 8192 else ((m + 1) << 3 if m >= 0 else 0)
+            ks = self._ctx_keys = (self._ctx_version, out)
+        return ks[1]
+
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "base"
     dedup_valid_from = 0          # store sequence from which the dedup window saw every row's id

@@ -1064,24 +1064,29 @@ class GpuInboundEngine(EngineBase):
         if self.cfg.block_index:
             # the block's index trailer, built right behind the encoder on the same stream; its last
             # workgroup publishes the final block bytes (state, and the host snapshot when given)
+            nk = self.ctx_key_spaces()
             rc = self.lib.sw_seg_index(P(_ptr(self.out_dev[slot])), P(_ptr(self._aux_buffer(slot))), P(src),
                                        P(_ptr(self.t["cursor"])), P(_ptr(self.store["alt"])), self.cfg.store_cap,
-                                       P(_ptr(self.t["asg_ctx"])), self.cfg.max_assignments, P(_ptr(dev)), cap,
-                                       P(_ptr(state)), pages, P(snapshot[3] if snapshot is not None else 0),
-                                       P(_ptr(self._index_scratch())), self.out_cap, self._stream())
+                                       P(_ptr(self.t["asg_ctx"])), self.cfg.max_assignments, P(nk.ctypes.data),
+                                       P(_ptr(dev)), cap, P(_ptr(state)), pages,
+                                       P(snapshot[3] if snapshot is not None else 0),
+                                       P(_ptr(self._index_scratch(nk))), self.out_cap,
+                                       P(_ptr(self.ix_stamps) if self.ix_stamps is not None else 0), self._stream())
             if rc:
                 raise RuntimeError(f"sw_seg_index failed ({rc})")
         return state[pages + 1:pages + 4]
 
-    def _index_scratch(self) -> torch.Tensor:
-        """Scratch of the block index build (one per engine: the builds run in stream order)."""
+    ix_stamps = None                # profiling: s_memrealtime stamps of the index build (see ix_probe)
+
+    def _index_scratch(self, nk: np.ndarray) -> torch.Tensor:
+        """Scratch of the block index build (one per engine: the builds run in stream order), sized for
+        the context key spaces; zeroed when (re)allocated -- the build keeps it re-armed."""
+        need = int(self.lib.sw_seg_index_scratch_words(self.out_cap, int(np.maximum(nk, 0).sum())))
         t = self.__dict__.get("_ix_scratch")
-        if t is None:
-            words = int(self.lib.sw_seg_index_scratch_words(self.out_cap))
-            t = self._ix_scratch = torch.zeros(words, dtype=torch.int32, device=self.device)
-            rc = self.lib.sw_seg_index_init(ctypes.c_void_p(_ptr(t)), self.out_cap, self._stream())
-            if rc:
-                raise RuntimeError(f"sw_seg_index_init failed ({rc})")
+        if t is None or t.numel() < need:
+            if t is not None:
+                self._sync_streams()            # the previous build may still read the old buffer
+            t = self._ix_scratch = torch.zeros(need, dtype=torch.int32, device=self.device)
         return t
 
     REJECT_BYTES = 8 << 20          # compact copies of rejected payloads per step (beyond: host reads the record)

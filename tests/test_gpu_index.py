@@ -110,9 +110,11 @@ def test_gpu_trailer_matches_cpu_builder(asset_mod):
         check_trailer(bg, g.ctx_table())
 
 
-def test_gpu_trailer_large_step():
+@pytest.mark.parametrize("n_cust", [97, 1])
+def test_gpu_trailer_large_step(n_cust):
     """A 1M-payload step at the bench shape (1M assignments, 97 customers, 31 areas, 1009 assets):
-    the trailer equals the C++ builder's."""
+    the trailer equals the C++ builder's.  With one customer its keys hold ~750K rows (733 chunks:
+    the partials fold in two rounds)."""
     from sitewhere_amd.persistence import segments as sg
     from sitewhere_amd.pipeline.config import EngineConfig
     from sitewhere_amd.pipeline.fleet import FleetSpec, fingerprints, gen_payloads, gen_tokens
@@ -125,7 +127,7 @@ def test_gpu_trailer_large_step():
     heap, offs = gen_tokens("dev-", 0, n_dev)
     lo, hi = fingerprints(heap, offs)
     d = g.register_devices(lo, hi)
-    g.set_assignments(d, d, customer=d % 97, area=d % 31, asset=d % 1009)
+    g.set_assignments(d, d, customer=d % n_cust, area=d % 31, asset=d % 1009)
     spec = FleetSpec(prefix="dev-", n_devices=n_dev, p_location=0.25, p_alert=0.05, p_unregistered=0.005,
                      with_alternate_id=True, lat0=33.0, lon0=-85.0, span_deg=2.0, p_meta=0.1)
     now = 1_700_000_001_000
@@ -139,6 +141,6 @@ def test_gpu_trailer_large_step():
     toff = sg.trailer_offset(bg)
     tr = sg.parse_trailer(bg[toff:])
     assert tr["n_alt"] > 1_000_000 - 20_000
-    assert [int(x) for x in tr["n_keys"]][:2] == [97 * 3, 31 * 3]    # measurement / location / alert
+    assert [int(x) for x in tr["n_keys"]][:2] == [n_cust * 3, 31 * 3]    # measurement / location / alert
     # index bytes per row (the disk cost of the indexes)
     assert (len(bg) - toff) / rg.n_persisted < 5.0
