@@ -73,6 +73,10 @@ def parse():
     ap.add_argument("--durable-retention-gb", type=float, default=48.0,
                     help="oldest segment files beyond this are deleted (bounded disk use); 0 = keep all")
     ap.add_argument("--direct-io", action=argparse.BooleanOptionalAction, default=True)
+    ap.add_argument("--read-threads", type=int, default=0,
+                    help="reader threads querying the durable store during the timed steps (list by assignment "
+                         "/ area, by id, by alternate id: persistence/read_load.py); 0 = ingest only")
+    ap.add_argument("--read-pause-ms", type=float, default=0.0, help="pause between one reader's queries")
     ap.add_argument("--no-outbound", action="store_true", help="(diagnostic) skip the D2H outbound copy")
     ap.add_argument("--bus", action=argparse.BooleanOptionalAction, default=True,
                     help="GPU engine: consume raw batches from, and publish enriched batches to, commit-log "
@@ -105,13 +109,20 @@ def open_durable(args, rank, dev):
             probe = os.path.dirname(probe)
         free = shutil.disk_usage(probe).free
         retention = max(2 << 30, min(retention, free // (2 * sharers)))
-    # ingest benchmark: the store's background indexer (read-side postings / alternate-id hashes) is
-    # off here; scripts/bench_store_reads.py indexes and queries the blocks a run leaves behind
+    # the store is indexed in the timed region: every block carries its index trailer, built on the
+    # MI355X in the step that encodes it (alternate ids, assignment zone maps, customer / area / asset
+    # key tables; csrc/include/swindex.h) and written with the block in the same group commit
     store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30, retention_bytes=retention,
-                              direct=args.direct_io, index=False)
+                              direct=args.direct_io)
     boot = int(time.time() * 1000)
-    store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
-                                             f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})
+    if args.read_threads:
+        # the readers look up every assignment and area by token: the whole fleet's dictionary
+        from sitewhere_amd.persistence.read_load import bench_dictionary
+        asg, ctx = bench_dictionary(int(np.max(dev)) + 1)
+        store.add_dictionary(boot, asg=asg, ctx=ctx)
+    else:
+        store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
+                                                 f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})
     return (None if base else tmpdir), store, boot
 
 
@@ -465,14 +476,22 @@ def main():
     barrier()
     s0 = eng.stats_dict()
     d0 = dur["store"].seg.stats() if dur else None
-    sk0 = (dur["sink"].bytes, dur["sink"].rows, dur["sink"].blocks, getattr(dur["sink"], "disk_wait_s", 0.0)) \
-        if dur else None
+    sk0 = (dur["sink"].bytes, dur["sink"].rows, dur["sink"].blocks, getattr(dur["sink"], "disk_wait_s", 0.0),
+           getattr(dur["sink"], "index_bytes", 0)) if dur else None
     r0 = dict(bus_stats["routed"], by_kind=list(bus_stats["routed"]["by_kind"])) if bus_stats else None
+    reads = None
+    if dur is not None and args.read_threads > 0:
+        from sitewhere_amd.persistence.read_load import ReadLoad
+        reads = ReadLoad(dur["store"], int(np.max(dev)) + 1, threads=args.read_threads,
+                         pause_s=args.read_pause_ms / 1e3, seed=rank)
     barrier()
+    if reads is not None:
+        reads.start()
     t_start = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         run(k)
     finish()
+    read_stats = reads.stop() if reads is not None else None
     barrier()
     elapsed = time.perf_counter() - t_start
     s1 = eng.stats_dict()
@@ -576,6 +595,8 @@ def main():
         detail["durable"] = {
             "blocks": nblocks, "rows": nrows, "block_bytes": nbytes,
             "bytes_per_event": round(nbytes / max(1, nrows), 3),
+            # of which the block index trailers (the store's read-side indexes, built in the step)
+            "index_bytes_per_event": round((getattr(sk, "index_bytes", 0) - sk0[4]) / max(1, nrows), 3),
             "durable_bytes_per_s": round((d1["bytes_written"] - d0["bytes_written"]) / elapsed, 1),
             "disk_bytes_written": d1["bytes_written"] - d0["bytes_written"],
             "fdatasyncs": d1["syncs"] - d0["syncs"], "direct_io": bool(d1["direct_io"]),
@@ -588,6 +609,8 @@ def main():
             "disk_probe": probe,
             "needed_gbps_job": round(world * (nbytes / max(1, args.steps)) / (elapsed / args.steps) / 1e9, 2),
         }
+    if read_stats is not None:
+        detail["reads"] = read_stats          # this rank's query latencies while it ingested
     if rank == 0:
         out = {
             "metric": "device_events_per_sec",

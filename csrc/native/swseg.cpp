@@ -454,11 +454,44 @@ void swseg_set_flags(uint8_t* block, int32_t flags) {
 int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1);
 int32_t swseg_ix_verify(const uint8_t* t, int64_t len, int64_t n_rows, int64_t n_pages);
 
-int32_t swseg_verify(const uint8_t* b, int64_t len) { return swseg_verify_pages(b, len, 0, INT64_MAX); }
+static int32_t verify_block(const uint8_t* b, int64_t len, int64_t p0, int64_t p1, bool trailer);
+
+// One page of len bytes holding want_rows rows: its checksum and column / heap bounds (0 ok, 3 bad
+// layout, 4 bad checksum).
+static int32_t verify_page(const uint8_t* pg, uint32_t len, uint32_t want_rows) {
+  if (len < SEG_PAGE_HDR) return 3;
+  SwSegPageHdr ph;
+  memcpy(&ph, pg, sizeof(ph));
+  if (ph.bytes != len || (len & 7)) return 3;
+  if (ph.n_rows != want_rows) return 3;
+  uint64_t cs = 0;
+  for (uint32_t i = 0; i < ph.bytes / 8; ++i) {
+    if (i == 1) continue;
+    uint64_t w;
+    memcpy(&w, pg + 8 * i, 8);
+    cs ^= seg_mix_word(w, i);
+  }
+  if (cs != ph.checksum) return 4;
+  for (int c = 0; c < SEG_NCOL; ++c) {
+    const SwSegCol& cd = ph.cols[c];
+    if (cd.bits > 64 || cd.data_off + seg_col_bytes(cd.count, cd.bits, cd.n_exc) > ph.bytes) return 3;
+  }
+  if ((uint64_t)ph.heap_off + ph.heap_bytes > ph.bytes || ph.alt_mode > SEG_ALT_HEX || ph.alt_pfx > ph.heap_bytes ||
+      ph.alt_width > 16)
+    return 3;
+  return 0;
+}
+
+// The whole block, its index trailer included.
+int32_t swseg_verify(const uint8_t* b, int64_t len) { return verify_block(b, len, 0, INT64_MAX, true); }
 
 // swseg_verify of the header, the page table and pages [p0, p1) only: a query that reads a few pages
-// of a block checks what it read (the other pages' bytes need not be present).
+// of a block checks what it read (the other pages' bytes, and the index trailer, need not be present).
 int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1) {
+  return verify_block(b, len, p0, p1, false);
+}
+
+static int32_t verify_block(const uint8_t* b, int64_t len, int64_t p0, int64_t p1, bool trailer) {
   if (len < 64) return 5;
   SwSegBlockHdr h;
   memcpy(&h, b, sizeof(h));
@@ -472,8 +505,7 @@ int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1
   if (h.flags & SEG_FLAG_INDEX) {
     // the index trailer follows the pages; checked with the whole block (partial reads skip it)
     if (pt[h.n_pages] > h.bytes || (pt[h.n_pages] & 7) || h.bytes - pt[h.n_pages] < SIX_HDR_BYTES) return 2;
-    if (p0 <= 0 && p1 >= (int64_t)h.n_pages &&
-        swseg_ix_verify(b + pt[h.n_pages], (int64_t)(h.bytes - pt[h.n_pages]), h.n_rows, h.n_pages) != 0)
+    if (trailer && swseg_ix_verify(b + pt[h.n_pages], (int64_t)(h.bytes - pt[h.n_pages]), h.n_rows, h.n_pages) != 0)
       return 6;
   } else if (pt[h.n_pages] != h.bytes) {
     return 2;
@@ -486,26 +518,9 @@ int32_t swseg_verify_pages(const uint8_t* b, int64_t len, int64_t p0, int64_t p1
   for (uint32_t p = (uint32_t)p0; (int64_t)p < p1; ++p) {
     const uint32_t o = pt[p], e = pt[p + 1];
     if (e < o + SEG_PAGE_HDR || e > h.bytes || (o & 7)) return 2;
-    SwSegPageHdr ph;
-    memcpy(&ph, b + o, sizeof(ph));
-    if (ph.bytes != e - o) return 3;
     const uint32_t want = p + 1 < h.n_pages ? SEG_PAGE_ROWS : h.n_rows - p * SEG_PAGE_ROWS;
-    if (ph.n_rows != want) return 3;
-    uint64_t cs = 0;
-    for (uint32_t i = 0; i < ph.bytes / 8; ++i) {
-      if (i == 1) continue;
-      uint64_t w;
-      memcpy(&w, b + o + 8 * i, 8);
-      cs ^= seg_mix_word(w, i);
-    }
-    if (cs != ph.checksum) return 4;
-    for (int c = 0; c < SEG_NCOL; ++c) {
-      const SwSegCol& cd = ph.cols[c];
-      if (cd.bits > 64 || cd.data_off + seg_col_bytes(cd.count, cd.bits, cd.n_exc) > ph.bytes) return 3;
-    }
-    if ((uint64_t)ph.heap_off + ph.heap_bytes > ph.bytes || ph.alt_mode > SEG_ALT_HEX || ph.alt_pfx > ph.heap_bytes ||
-        ph.alt_width > 16)
-      return 3;
+    const int32_t rc = verify_page(b + o, e - o, want);
+    if (rc) return rc;
   }
   return 0;
 }
@@ -525,6 +540,233 @@ int64_t swseg_string_bytes(const uint8_t* b, int64_t p0, int64_t p1) {
   return total;
 }
 
+namespace {
+struct PageScratch {
+  std::vector<uint8_t> et = std::vector<uint8_t>(SEG_PAGE_ROWS);
+  std::vector<uint32_t> fl = std::vector<uint32_t>(SEG_PAGE_ROWS);
+  std::vector<double> dv = std::vector<double>(SEG_PAGE_ROWS);
+  std::vector<uint64_t> ak = std::vector<uint64_t>(SEG_PAGE_ROWS), al = std::vector<uint64_t>(SEG_PAGE_ROWS),
+                        an = std::vector<uint64_t>(SEG_PAGE_ROWS), ml = std::vector<uint64_t>(SEG_PAGE_ROWS),
+                        dl = std::vector<uint64_t>(SEG_PAGE_ROWS);
+};
+
+// One (verified) page into rows r0.. of the outputs (any may be null); strings appended at *so.
+// Returns the page's rows, -1 if str_cap is too small.
+int64_t decode_page(const uint8_t* pg, int64_t r0, uint8_t* etype, uint8_t* level, int64_t* date, int32_t* asg,
+                    uint16_t* name, double* v0, double* v1, double* v2, uint8_t* flags, uint8_t* str_heap,
+                    int64_t str_cap, int64_t* so, int64_t* str_off, PageScratch& ws) {
+  auto& et = ws.et; auto& fl = ws.fl; auto& dv = ws.dv;
+  auto& ak = ws.ak; auto& al = ws.al; auto& an = ws.an; auto& ml = ws.ml; auto& dl = ws.dl;
+  SwSegPageHdr ph;
+  memcpy(&ph, pg, sizeof(ph));
+  const uint32_t m = ph.n_rows;
+  const int mode = ph.alt_mode;
+  // etype and flags first: every other column's membership depends on them
+  for (uint32_t k = 0; k < m; ++k) {
+    et[k] = (uint8_t)seg_unord(col_int(pg, ph.cols[SEG_ETYPE], k));
+    fl[k] = (uint32_t)seg_unord(col_int(pg, ph.cols[SEG_FLAGS], k));
+  }
+  if (etype) memcpy(etype + r0, et.data(), m);
+  if (flags)
+    for (uint32_t k = 0; k < m; ++k) flags[r0 + k] = (uint8_t)fl[k];
+  for (int c = 0; c < SEG_NCOL; ++c) {
+    if (c == SEG_ETYPE || c == SEG_FLAGS) continue;
+    // columns nobody asked for are not unpacked (string lengths only feed the heap)
+    const bool want = c == SEG_LEVEL ? level != nullptr : c == SEG_DATE ? date != nullptr
+                    : c == SEG_ASG ? asg != nullptr : c == SEG_NAME ? name != nullptr
+                    : (c == SEG_MXV || c == SEG_LAT) ? v0 != nullptr : c == SEG_LON ? v1 != nullptr
+                    : c == SEG_ELEV ? v2 != nullptr : str_heap != nullptr;
+    if (!want) continue;
+    const SwSegCol& cd = ph.cols[c];
+    const uint8_t* words = pg + cd.data_off;
+    if (seg_is_double(c)) {
+      const uint8_t* xi = words + 8 * seg_col_words(cd.count, cd.bits);
+      const uint8_t* xr = xi + ((2u * cd.n_exc + 7u) & ~7u);
+      for (uint32_t i = 0; i < cd.count; ++i)
+        dv[i] = seg_dec_value(seg_unord(cd.base + unpack(words, i, cd.bits)), cd.exp);
+      for (uint32_t j = 0; j < cd.n_exc; ++j) {
+        uint16_t ix;
+        uint64_t raw;
+        memcpy(&ix, xi + 2 * j, 2);
+        memcpy(&raw, xr + 8 * j, 8);
+        if (ix < cd.count) dv[ix] = sw_bits_f64(raw);
+      }
+    }
+    uint32_t i = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+      const int64_t r = r0 + k;
+      const bool mem = seg_member(c, et[k], fl[k], mode);
+      const uint64_t u = mem && !seg_is_double(c) ? cd.base + unpack(words, i, cd.bits) : 0;
+      switch (c) {
+        case SEG_LEVEL:
+          if (level) level[r] = mem ? (uint8_t)seg_unord(u) : 0;
+          break;
+        case SEG_DATE:
+          if (date) date[r] = seg_unord(u);
+          break;
+        case SEG_ASG:
+          if (asg) asg[r] = (int32_t)seg_unord(u);
+          break;
+        case SEG_NAME:
+          if (name) name[r] = mem ? (uint16_t)seg_unord(u) : (uint16_t)0xffff;
+          break;
+        case SEG_MXV:                 // runs before SEG_LAT: zero v0 of every non-measurement
+          if (v0) v0[r] = mem ? dv[i] : 0.0;
+          break;
+        case SEG_LAT:
+          if (v0 && mem) v0[r] = dv[i];
+          break;
+        case SEG_LON:
+          if (v1) v1[r] = mem ? dv[i] : 0.0;
+          break;
+        case SEG_ELEV:
+          if (v2) v2[r] = mem ? dv[i] : 0.0;
+          break;
+        case SEG_ALTK: ak[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+        case SEG_ALTLEN: al[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+        case SEG_ALTNUM: an[k] = mem ? u : 0; break;
+        case SEG_MSGLEN: ml[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+        case SEG_METALEN: dl[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
+      }
+      if (mem) ++i;
+    }
+  }
+  if (str_heap) {
+    const uint8_t* heap = pg + ph.heap_off;
+    uint32_t ho = ph.alt_pfx;
+    for (uint32_t k = 0; k < m; ++k) {
+      const int64_t r = r0 + k;
+      // alternate id
+      if (fl[k] & SEGF_HAS_ALT) {
+        const int64_t need = *so + ph.alt_pfx + (mode == SEG_ALT_HEX ? ph.alt_width : al[k]) + 8;
+        if (need > str_cap) return -1;
+        memcpy(str_heap + *so, heap, ph.alt_pfx);
+        *so += ph.alt_pfx;
+        if (mode == SEG_ALT_HEX) {
+          for (int d = (int)ph.alt_width - 1; d >= 0; --d)
+            str_heap[(*so)++] = "0123456789abcdef"[(an[k] >> (4 * d)) & 15];
+        } else {
+          memcpy(str_heap + *so, heap + ho, al[k]);
+          *so += (int64_t)al[k];
+          ho += (uint32_t)al[k];
+        }
+        if (ak[k]) {
+          char sfx[8];
+          const int n = snprintf(sfx, sizeof(sfx), ":%u", (unsigned)(ak[k] - 1));
+          if (*so + n > str_cap) return -1;
+          memcpy(str_heap + *so, sfx, (size_t)n);
+          *so += n;
+        }
+      }
+      if (str_off) str_off[3 * r + 1] = *so;
+      if (*so + (int64_t)ml[k] + (int64_t)dl[k] > str_cap) return -1;
+      memcpy(str_heap + *so, heap + ho, ml[k]);
+      *so += (int64_t)ml[k];
+      ho += (uint32_t)ml[k];
+      if (str_off) str_off[3 * r + 2] = *so;
+      memcpy(str_heap + *so, heap + ho, dl[k]);
+      *so += (int64_t)dl[k];
+      ho += (uint32_t)dl[k];
+      if (str_off) str_off[3 * r + 3] = *so;
+    }
+  }
+  return m;
+}
+
+// Rows rows[0..nw) (ascending, < the page's rows) of one (verified) page into slots 0..nw of the
+// outputs, without decoding the rest: one pass over the leading rows counts each column's members
+// (a row's value sits at its member index) and the string bytes before the row.  Strings as
+// decode_page (str_off[3 w + 1..3], appended at *so).  Returns nw, -1 if str_cap is too small.
+int64_t decode_rows(const uint8_t* pg, const int32_t* rows, int64_t nw, uint8_t* etype, uint8_t* level, int64_t* date,
+                    int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2, uint8_t* flags,
+                    uint8_t* str_heap, int64_t str_cap, int64_t* so, int64_t* str_off) {
+  SwSegPageHdr ph;
+  memcpy(&ph, pg, sizeof(ph));
+  const int mode = ph.alt_mode;
+  const uint8_t* heap = pg + ph.heap_off;
+  uint32_t cnt[SEG_NCOL] = {0};
+  uint32_t ho = ph.alt_pfx;                         // heap bytes before row j's strings
+  int64_t w = 0;
+  auto member_value = [&](int c, uint32_t ix) -> uint64_t { return ph.cols[c].base + unpack(pg + ph.cols[c].data_off, ix, ph.cols[c].bits); };
+  auto dbl = [&](int c, uint32_t ix) -> double {
+    const SwSegCol& cd = ph.cols[c];
+    const uint8_t* words = pg + cd.data_off;
+    const uint8_t* xi = words + 8 * seg_col_words(cd.count, cd.bits);
+    const uint8_t* xr = xi + ((2u * cd.n_exc + 7u) & ~7u);
+    for (uint32_t j = 0; j < cd.n_exc; ++j) {
+      uint16_t x;
+      memcpy(&x, xi + 2 * j, 2);
+      if (x == ix) {
+        uint64_t raw;
+        memcpy(&raw, xr + 8 * j, 8);
+        return sw_bits_f64(raw);
+      }
+    }
+    return seg_dec_value(seg_unord(cd.base + unpack(words, ix, cd.bits)), cd.exp);
+  };
+  for (uint32_t j = 0; j < ph.n_rows && w < nw; ++j) {
+    const uint8_t et = (uint8_t)seg_unord(col_int(pg, ph.cols[SEG_ETYPE], j));
+    const uint32_t f = (uint32_t)seg_unord(col_int(pg, ph.cols[SEG_FLAGS], j));
+    const bool has_alt = seg_member(SEG_ALTLEN, et, f, mode);
+    const uint64_t al = has_alt ? (uint64_t)seg_unord(member_value(SEG_ALTLEN, cnt[SEG_ALTLEN])) : 0;
+    const bool has_msg = seg_member(SEG_MSGLEN, et, f, mode);
+    const uint64_t ml = has_msg ? (uint64_t)seg_unord(member_value(SEG_MSGLEN, cnt[SEG_MSGLEN])) : 0;
+    const bool has_md = seg_member(SEG_METALEN, et, f, mode);
+    const uint64_t dl = has_md ? (uint64_t)seg_unord(member_value(SEG_METALEN, cnt[SEG_METALEN])) : 0;
+    const uint64_t a_raw = mode == SEG_ALT_HEX ? 0 : al;      // heap bytes of the id's remainder
+    while (w < nw && (uint32_t)rows[w] == j) {
+      if (etype) etype[w] = et;
+      if (flags) flags[w] = (uint8_t)f;
+      if (level) level[w] = seg_member(SEG_LEVEL, et, f, mode) ? (uint8_t)seg_unord(member_value(SEG_LEVEL, cnt[SEG_LEVEL])) : 0;
+      if (date) date[w] = seg_unord(member_value(SEG_DATE, j));
+      if (asg) asg[w] = (int32_t)seg_unord(member_value(SEG_ASG, j));
+      if (name) name[w] = seg_member(SEG_NAME, et, f, mode) ? (uint16_t)seg_unord(member_value(SEG_NAME, cnt[SEG_NAME])) : (uint16_t)0xffff;
+      if (v0) v0[w] = seg_member(SEG_MXV, et, f, mode) ? dbl(SEG_MXV, cnt[SEG_MXV])
+                    : seg_member(SEG_LAT, et, f, mode) ? dbl(SEG_LAT, cnt[SEG_LAT]) : 0.0;
+      if (v1) v1[w] = seg_member(SEG_LON, et, f, mode) ? dbl(SEG_LON, cnt[SEG_LON]) : 0.0;
+      if (v2) v2[w] = seg_member(SEG_ELEV, et, f, mode) ? dbl(SEG_ELEV, cnt[SEG_ELEV]) : 0.0;
+      if (str_heap) {
+        if (has_alt) {
+          const int64_t need = *so + ph.alt_pfx + (mode == SEG_ALT_HEX ? ph.alt_width : al) + 8;
+          if (need > str_cap) return -1;
+          memcpy(str_heap + *so, heap, ph.alt_pfx);
+          *so += ph.alt_pfx;
+          if (mode == SEG_ALT_HEX) {
+            const uint64_t an = member_value(SEG_ALTNUM, cnt[SEG_ALTNUM]);
+            for (int d = (int)ph.alt_width - 1; d >= 0; --d) str_heap[(*so)++] = "0123456789abcdef"[(an >> (4 * d)) & 15];
+          } else {
+            memcpy(str_heap + *so, heap + ho, al);
+            *so += (int64_t)al;
+          }
+          const uint64_t ak = (uint64_t)seg_unord(member_value(SEG_ALTK, cnt[SEG_ALTK]));
+          if (ak) {
+            char sfx[8];
+            const int n = snprintf(sfx, sizeof(sfx), ":%u", (unsigned)(ak - 1));
+            if (*so + n > str_cap) return -1;
+            memcpy(str_heap + *so, sfx, (size_t)n);
+            *so += n;
+          }
+        }
+        if (str_off) str_off[3 * w + 1] = *so;
+        if (*so + (int64_t)ml + (int64_t)dl > str_cap) return -1;
+        memcpy(str_heap + *so, heap + ho + a_raw, ml);
+        *so += (int64_t)ml;
+        if (str_off) str_off[3 * w + 2] = *so;
+        memcpy(str_heap + *so, heap + ho + a_raw + ml, dl);
+        *so += (int64_t)dl;
+        if (str_off) str_off[3 * w + 3] = *so;
+      }
+      ++w;
+    }
+    // advance past row j: its members in every sparse column, its string bytes
+    for (int c = 0; c < SEG_NCOL; ++c)
+      if (c != SEG_ETYPE && c != SEG_FLAGS && c != SEG_DATE && c != SEG_ASG && seg_member(c, et, f, mode)) ++cnt[c];
+    ho += (uint32_t)(a_raw + ml + dl);
+  }
+  return w == nw ? nw : -2;
+}
+}  // namespace
+
 // Decode pages [p0, p1) of a (verified) block into per-row arrays (row 0 = the first row of page p0).
 // Any output may be null.  name = 0xffff where the row has none; v0/v1/v2 = 0 where the type has no
 // such value (flags tell whether an elevation was sent).  Strings (str_heap non-null, str_cap bytes,
@@ -538,131 +780,184 @@ int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, u
   memcpy(&h, b, sizeof(h));
   const uint32_t* pt = (const uint32_t*)(b + 64);
   if (p1 > (int64_t)h.n_pages) p1 = h.n_pages;
-  std::vector<uint8_t> et(SEG_PAGE_ROWS);
-  std::vector<uint32_t> fl(SEG_PAGE_ROWS);
-  std::vector<double> dv(SEG_PAGE_ROWS);
-  std::vector<uint64_t> ak(SEG_PAGE_ROWS), al(SEG_PAGE_ROWS), an(SEG_PAGE_ROWS), ml(SEG_PAGE_ROWS),
-      dl(SEG_PAGE_ROWS);
+  PageScratch ws;
   int64_t r0 = 0, so = 0;
   if (str_off) str_off[0] = 0;
   for (int64_t p = p0; p < p1; ++p) {
-    const uint8_t* pg = b + pt[p];
-    SwSegPageHdr ph;
-    memcpy(&ph, pg, sizeof(ph));
-    const uint32_t m = ph.n_rows;
-    const int mode = ph.alt_mode;
-    // etype and flags first: every other column's membership depends on them
-    for (uint32_t k = 0; k < m; ++k) {
-      et[k] = (uint8_t)seg_unord(col_int(pg, ph.cols[SEG_ETYPE], k));
-      fl[k] = (uint32_t)seg_unord(col_int(pg, ph.cols[SEG_FLAGS], k));
-    }
-    if (etype) memcpy(etype + r0, et.data(), m);
-    if (flags)
-      for (uint32_t k = 0; k < m; ++k) flags[r0 + k] = (uint8_t)fl[k];
-    for (int c = 0; c < SEG_NCOL; ++c) {
-      if (c == SEG_ETYPE || c == SEG_FLAGS) continue;
-      // columns nobody asked for are not unpacked (string lengths only feed the heap)
-      const bool want = c == SEG_LEVEL ? level != nullptr : c == SEG_DATE ? date != nullptr
-                      : c == SEG_ASG ? asg != nullptr : c == SEG_NAME ? name != nullptr
-                      : (c == SEG_MXV || c == SEG_LAT) ? v0 != nullptr : c == SEG_LON ? v1 != nullptr
-                      : c == SEG_ELEV ? v2 != nullptr : str_heap != nullptr;
-      if (!want) continue;
-      const SwSegCol& cd = ph.cols[c];
-      const uint8_t* words = pg + cd.data_off;
-      if (seg_is_double(c)) {
-        const uint8_t* xi = words + 8 * seg_col_words(cd.count, cd.bits);
-        const uint8_t* xr = xi + ((2u * cd.n_exc + 7u) & ~7u);
-        for (uint32_t i = 0; i < cd.count; ++i)
-          dv[i] = seg_dec_value(seg_unord(cd.base + unpack(words, i, cd.bits)), cd.exp);
-        for (uint32_t j = 0; j < cd.n_exc; ++j) {
-          uint16_t ix;
-          uint64_t raw;
-          memcpy(&ix, xi + 2 * j, 2);
-          memcpy(&raw, xr + 8 * j, 8);
-          if (ix < cd.count) dv[ix] = sw_bits_f64(raw);
-        }
-      }
-      uint32_t i = 0;
-      for (uint32_t k = 0; k < m; ++k) {
-        const int64_t r = r0 + k;
-        const bool mem = seg_member(c, et[k], fl[k], mode);
-        const uint64_t u = mem && !seg_is_double(c) ? cd.base + unpack(words, i, cd.bits) : 0;
-        switch (c) {
-          case SEG_LEVEL:
-            if (level) level[r] = mem ? (uint8_t)seg_unord(u) : 0;
-            break;
-          case SEG_DATE:
-            if (date) date[r] = seg_unord(u);
-            break;
-          case SEG_ASG:
-            if (asg) asg[r] = (int32_t)seg_unord(u);
-            break;
-          case SEG_NAME:
-            if (name) name[r] = mem ? (uint16_t)seg_unord(u) : (uint16_t)0xffff;
-            break;
-          case SEG_MXV:                 // runs before SEG_LAT: zero v0 of every non-measurement
-            if (v0) v0[r] = mem ? dv[i] : 0.0;
-            break;
-          case SEG_LAT:
-            if (v0 && mem) v0[r] = dv[i];
-            break;
-          case SEG_LON:
-            if (v1) v1[r] = mem ? dv[i] : 0.0;
-            break;
-          case SEG_ELEV:
-            if (v2) v2[r] = mem ? dv[i] : 0.0;
-            break;
-          case SEG_ALTK: ak[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
-          case SEG_ALTLEN: al[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
-          case SEG_ALTNUM: an[k] = mem ? u : 0; break;
-          case SEG_MSGLEN: ml[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
-          case SEG_METALEN: dl[k] = mem ? (uint64_t)seg_unord(u) : 0; break;
-        }
-        if (mem) ++i;
-      }
-    }
-    if (str_heap) {
-      const uint8_t* heap = pg + ph.heap_off;
-      uint32_t ho = ph.alt_pfx;
-      for (uint32_t k = 0; k < m; ++k) {
-        const int64_t r = r0 + k;
-        // alternate id
-        if (fl[k] & SEGF_HAS_ALT) {
-          const int64_t need = so + ph.alt_pfx + (mode == SEG_ALT_HEX ? ph.alt_width : al[k]) + 8;
-          if (need > str_cap) return -1;
-          memcpy(str_heap + so, heap, ph.alt_pfx);
-          so += ph.alt_pfx;
-          if (mode == SEG_ALT_HEX) {
-            for (int d = (int)ph.alt_width - 1; d >= 0; --d)
-              str_heap[so++] = "0123456789abcdef"[(an[k] >> (4 * d)) & 15];
-          } else {
-            memcpy(str_heap + so, heap + ho, al[k]);
-            so += (int64_t)al[k];
-            ho += (uint32_t)al[k];
-          }
-          if (ak[k]) {
-            char sfx[8];
-            const int n = snprintf(sfx, sizeof(sfx), ":%u", (unsigned)(ak[k] - 1));
-            if (so + n > str_cap) return -1;
-            memcpy(str_heap + so, sfx, (size_t)n);
-            so += n;
-          }
-        }
-        if (str_off) str_off[3 * r + 1] = so;
-        if (so + (int64_t)ml[k] + (int64_t)dl[k] > str_cap) return -1;
-        memcpy(str_heap + so, heap + ho, ml[k]);
-        so += (int64_t)ml[k];
-        ho += (uint32_t)ml[k];
-        if (str_off) str_off[3 * r + 2] = so;
-        memcpy(str_heap + so, heap + ho, dl[k]);
-        so += (int64_t)dl[k];
-        ho += (uint32_t)dl[k];
-        if (str_off) str_off[3 * r + 3] = so;
-      }
-    }
+    const int64_t m = decode_page(b + pt[p], r0, etype, level, date, asg, name, v0, v1, v2, flags, str_heap, str_cap,
+                                  &so, str_off, ws);
+    if (m < 0) return -1;
     r0 += m;
   }
   return r0;
+}
+
+// Point reads of single rows across blocks: request i is row row_in_page[i] of the page at file
+// offset pg_pos[i] (pg_bytes[i] bytes, pg_rows[i] rows) of file fds[i].  Each distinct page (requests
+// of one page adjacent) is pread and verified once, decoded on one of `threads` threads, and the
+// requested rows copied out in request order (outputs as swseg_decode, one row per request; strings
+// back to back in str_heap, str_off[3 i + 0..3]).  Returns n, -(1 + i) when request i's page cannot be
+// read or fails its check, or -(1 << 40) - need when str_cap is below the `need` string bytes.
+int64_t swseg_fetch_rows(const int32_t* fds, const int64_t* pg_pos, const uint32_t* pg_bytes, const uint32_t* pg_rows,
+                         const int32_t* row_in_page, int64_t n, int32_t threads, uint8_t* etype, uint8_t* level,
+                         int64_t* date, int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2,
+                         uint8_t* flags, uint8_t* str_heap, int64_t str_cap, int64_t* str_off) {
+  if (n <= 0) return 0;
+  std::vector<int64_t> first;                       // first request of each distinct page
+  for (int64_t i = 0; i < n; ++i)
+    if (i == 0 || fds[i] != fds[i - 1] || pg_pos[i] != pg_pos[i - 1]) first.push_back(i);
+  const int64_t np = (int64_t)first.size();
+  first.push_back(n);
+  // per distinct page: its requests sorted by row, decoded into slots at the group's start
+  std::vector<int64_t> perm((size_t)n);
+  std::vector<int32_t> srow((size_t)n);
+  for (int64_t q = 0; q < np; ++q) {
+    for (int64_t i = first[q]; i < first[q + 1]; ++i) perm[i] = i;
+    std::stable_sort(perm.begin() + first[q], perm.begin() + first[q + 1],
+                     [&](int64_t x, int64_t y) { return row_in_page[x] < row_in_page[y]; });
+    for (int64_t i = first[q]; i < first[q + 1]; ++i) srow[i] = row_in_page[perm[i]];
+  }
+  std::vector<uint8_t> et(n), lv(n), fl(n);
+  std::vector<int64_t> dt(n);
+  std::vector<int32_t> as(n);
+  std::vector<uint16_t> nm(n);
+  std::vector<double> a0(n), a1(n), a2(n);
+  std::vector<std::vector<uint8_t>> heaps((size_t)np);
+  std::vector<int64_t> soff(3 * (size_t)n + 1, 0);   // per slot, relative to its page group's heap
+  std::atomic<int64_t> bad{-1};
+  int T = threads > 0 ? threads : 1;
+  if (T > 32) T = 32;
+  if ((int64_t)T > np) T = (int)np;
+  auto work = [&](int w) {
+    std::vector<uint8_t> buf;
+    std::vector<int64_t> loc;
+    for (int64_t q = np * w / T; q < np * (w + 1) / T; ++q) {
+      const int64_t i = first[q], k = first[q + 1] - first[q];
+      const uint32_t len = pg_bytes[i];
+      if (len < SEG_PAGE_HDR || len > (64u << 20) || pg_rows[i] > SEG_PAGE_ROWS) { bad = i; return; }
+      buf.resize(len);
+      if (pread(fds[i], buf.data(), len, pg_pos[i]) != (ssize_t)len || verify_page(buf.data(), len, pg_rows[i])) {
+        bad = i;
+        return;
+      }
+      for (int64_t j = i; j < i + k; ++j)
+        if (srow[j] < 0 || (uint32_t)srow[j] >= pg_rows[i]) { bad = perm[j]; return; }
+      SwSegPageHdr ph;
+      memcpy(&ph, buf.data(), sizeof(ph));
+      heaps[(size_t)q].resize((size_t)ph.heap_bytes + (size_t)k * (SEG_ALT_PFX_MAX + 16 + 8) + 8);
+      loc.assign(3 * (size_t)k + 1, 0);
+      int64_t so = 0;
+      if (decode_rows(buf.data(), srow.data() + i, k, et.data() + i, lv.data() + i, dt.data() + i, as.data() + i,
+                      nm.data() + i, a0.data() + i, a1.data() + i, a2.data() + i, fl.data() + i,
+                      heaps[(size_t)q].data(), (int64_t)heaps[(size_t)q].size(), &so, loc.data()) != k) {
+        bad = i;
+        return;
+      }
+      for (int64_t j = 0; j < 3 * k; ++j) soff[3 * (size_t)i + 1 + j] = loc[1 + j];
+    }
+  };
+  if (T <= 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int w = 0; w < T; ++w) th.emplace_back(work, w);
+    for (auto& x : th) x.join();
+  }
+  if (bad.load() >= 0) return -(1 + bad.load());
+  // slot j's strings: [start, end) of its group's heap, start = end of the slot before it in the group
+  auto s_beg = [&](int64_t q, int64_t j) { return j == first[q] ? (int64_t)0 : soff[3 * (size_t)j]; };
+  int64_t need = 0;
+  for (int64_t q = 0; q < np; ++q)
+    for (int64_t j = first[q]; j < first[q + 1]; ++j) need += soff[3 * (size_t)j + 3] - s_beg(q, j);
+  if (str_heap && need > str_cap) return -(int64_t(1) << 40) - need;
+  // out in request order: request perm[j] takes slot j
+  int64_t so = 0;
+  if (str_off) str_off[0] = 0;
+  std::vector<int64_t> slot_of((size_t)n), grp((size_t)n);
+  for (int64_t q = 0; q < np; ++q)
+    for (int64_t j = first[q]; j < first[q + 1]; ++j) { slot_of[perm[j]] = j; grp[j] = q; }
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t j = slot_of[i], q = grp[j];
+    if (etype) etype[i] = et[j];
+    if (level) level[i] = lv[j];
+    if (date) date[i] = dt[j];
+    if (asg) asg[i] = as[j];
+    if (name) name[i] = nm[j];
+    if (v0) v0[i] = a0[j];
+    if (v1) v1[i] = a1[j];
+    if (v2) v2[i] = a2[j];
+    if (flags) flags[i] = fl[j];
+    if (str_heap) {
+      int64_t s0 = s_beg(q, j);
+      for (int k = 0; k < 3; ++k) {
+        const int64_t s1 = soff[3 * (size_t)j + k + 1];
+        memcpy(str_heap + so, heaps[(size_t)q].data() + s0, (size_t)(s1 - s0));
+        so += s1 - s0;
+        s0 = s1;
+        if (str_off) str_off[3 * i + k + 1] = so;
+      }
+    }
+  }
+  return n;
+}
+
+// Rows whose alternate id hashes to hashes[i] in candidate page i (the pages a trailer's fingerprint
+// search named): each page pread from fds[i] at pg_pos[i] (pg_bytes[i] bytes, pg_rows[i] rows),
+// verified, its id column decoded, on `threads` threads.  Writes (page task, row in page) of every
+// match, tasks in order and rows ascending; returns the matches (> cap: call again with that cap), or
+// -(1 + i) when page i cannot be read or fails its check.
+int64_t swseg_alt_page_rows(const int32_t* fds, const int64_t* pg_pos, const uint32_t* pg_bytes,
+                            const uint32_t* pg_rows, const uint64_t* hashes, int64_t n, int32_t threads,
+                            int64_t* out_task, int32_t* out_row, int64_t cap) {
+  if (n <= 0) return 0;
+  int T = threads > 0 ? threads : 1;
+  if (T > 32) T = 32;
+  if ((int64_t)T > n) T = (int)n;
+  std::vector<std::vector<std::pair<int64_t, int32_t>>> hits(T);
+  std::atomic<int64_t> bad{-1};
+  auto work = [&](int w) {
+    PageScratch ws;
+    std::vector<uint8_t> buf, heap, fl(SEG_PAGE_ROWS);
+    std::vector<int64_t> so(3 * SEG_PAGE_ROWS + 1);
+    for (int64_t i = n * w / T; i < n * (w + 1) / T; ++i) {
+      const uint32_t len = pg_bytes[i];
+      if (len < SEG_PAGE_HDR || len > (64u << 20) || pg_rows[i] > SEG_PAGE_ROWS) { bad = i; return; }
+      buf.resize(len);
+      if (pread(fds[i], buf.data(), len, pg_pos[i]) != (ssize_t)len || verify_page(buf.data(), len, pg_rows[i])) {
+        bad = i;
+        return;
+      }
+      SwSegPageHdr ph;
+      memcpy(&ph, buf.data(), sizeof(ph));
+      heap.resize((size_t)ph.heap_bytes + (size_t)ph.n_rows * (SEG_ALT_PFX_MAX + 16 + 8) + 8);
+      int64_t o = 0;
+      so[0] = 0;
+      if (decode_page(buf.data(), 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, fl.data(),
+                      heap.data(), (int64_t)heap.size(), &o, so.data(), ws) != (int64_t)ph.n_rows) {
+        bad = i;
+        return;
+      }
+      for (uint32_t r = 0; r < ph.n_rows; ++r)
+        if ((fl[r] & SEGF_HAS_ALT) &&
+            sw_hash64(heap.data() + so[3 * r], (uint32_t)(so[3 * r + 1] - so[3 * r])) == hashes[i])
+          hits[w].push_back({i, (int32_t)r});
+    }
+  };
+  if (T <= 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int w = 0; w < T; ++w) th.emplace_back(work, w);
+    for (auto& x : th) x.join();
+  }
+  if (bad.load() >= 0) return -(1 + bad.load());
+  int64_t k = 0;
+  for (int w = 0; w < T; ++w)
+    for (const auto& h : hits[w]) {
+      if (k < cap) { out_task[k] = h.first; out_row[k] = h.second; }
+      ++k;
+    }
+  return k;
 }
 
 // Per-page summaries of a block (pages in order): first row, rows, assignment min / max, event date

@@ -60,6 +60,12 @@ int64_t swseg_encode(const SwOutRec* rows, const SwEventRec* recs, const SwStrRe
                      int64_t raw_bytes, int64_t n, uint8_t* out, int64_t cap);
 void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot, int32_t rank, int32_t world);
 int32_t swseg_verify(const uint8_t* b, int64_t len);
+int64_t swseg_index_append(uint8_t* block, int64_t cap, const int32_t* ctx, int64_t n_ctx);
+int64_t swseg_ix_max_bytes(int64_t n_rows);
+int64_t swseg_ix_offset(const uint8_t* block);
+void swseg_ix_alt_find(const uint8_t* const* t, int64_t n, const uint64_t* want, int64_t n_want, int64_t* out_blk,
+                       int64_t* out_page);
+void swseg_ix_ctx_find(const uint8_t* const* t, int64_t n, int32_t d, uint32_t key, int64_t* out);
 int64_t swseg_string_bytes(const uint8_t* b, int64_t p0, int64_t p1);
 int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, uint8_t* level, int64_t* date,
                      int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2, uint8_t* flags,
@@ -304,6 +310,29 @@ static void decode_fuzz() {
       const int64_t got = swseg_decode(b2.data(), 0, 1 << 30, et.data(), lv.data(), dt.data(), as.data(), nm.data(),
                                        a0.data(), a1.data(), a2.data(), fl.data(), heap.data(), cap, so.data());
       CHECK(got == good, "block decode returned %lld of %lld rows", (long long)got, (long long)good);
+    }
+    // the same block with its index trailer (csrc/native/swindex.cpp) built into an exactly sized
+    // buffer, verified, and queried through the alternate-id and context-key lookups
+    if (nb > 0) {
+      std::vector<int32_t> ctx(97 * 4);
+      for (int i = 0; i < 97; ++i) { ctx[4 * i] = i; ctx[4 * i + 1] = i % 7; ctx[4 * i + 2] = i % 5; ctx[4 * i + 3] = -1; }
+      std::vector<uint8_t> ib((size_t)(nb + swseg_ix_max_bytes(good)));
+      std::copy(blk.begin(), blk.begin() + nb, ib.begin());
+      const int64_t ni = swseg_index_append(ib.data(), (int64_t)ib.size(), ctx.data(), 97);
+      CHECK(ni > nb, "index append returned %lld", (long long)ni);
+      if (ni > nb) {
+        swseg_seal(ib.data(), 0, 1700000001000, 1, 0, 1);
+        std::vector<uint8_t> b3(ib.begin(), ib.begin() + ni);
+        CHECK(swseg_verify(b3.data(), ni) == 0, "indexed block does not verify");
+        const int64_t toff = swseg_ix_offset(b3.data());
+        CHECK(toff > 0 && toff < ni, "bad trailer offset %lld", (long long)toff);
+        std::vector<uint8_t> tr(b3.begin() + toff, b3.end());     // exact: the lookups stay inside it
+        const uint8_t* tp = tr.data();
+        uint64_t want[3] = {0x0123456789abcdefull, 0, ~0ull};
+        int64_t ob[3], op[3], cf[7];
+        swseg_ix_alt_find(&tp, 1, want, 3, ob, op);
+        swseg_ix_ctx_find(&tp, 1, 0, (3u << 3) | 1u, cf);
+      }
     }
   }
   uint64_t s = 12345;

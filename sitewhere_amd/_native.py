@@ -183,6 +183,9 @@ def native():
         _proto(lib, "swseg_verify", c_int32, P, c_int64)
         _proto(lib, "swseg_verify_pages", c_int32, P, c_int64, c_int64, c_int64)
         _proto(lib, "swseg_decode", c_int64, P, c_int64, c_int64, P, P, P, P, P, P, P, P, P, P, c_int64, P)
+        _proto(lib, "swseg_alt_page_rows", c_int64, P, P, P, P, P, c_int64, c_int32, P, P, c_int64)
+        _proto(lib, "swseg_fetch_rows", c_int64, P, P, P, P, P, c_int64, c_int32, P, P, P, P, P, P, P, P, P, P,
+               c_int64, P)
         _proto(lib, "swseg_string_bytes", c_int64, P, c_int64, c_int64)
         _proto(lib, "swseg_page_summary", c_int64, P, P)
         _proto(lib, "swseg_index_block", c_int64, P, c_int64, P, P, P, P, P, P)

@@ -318,31 +318,34 @@ def page_summary(block) -> np.ndarray:
 DURABLE_MAGIC = b"SWD1"
 
 
-def _durable_head(boot, asg: dict, names: dict, rules: dict | None, src=None) -> bytes:
+def _durable_head(boot, asg: dict, names: dict, rules: dict | None, src=None, ctx=None) -> bytes:
     import msgpack
     import struct
     d = {"boot": boot_id(boot), "asg": {int(k): list(v) for k, v in (asg or {}).items()},
          "names": {int(k): v for k, v in (names or {}).items()}, "rules": rules or {}}
     if src:
         d["src"] = [[str(t), int(p), int(o)] for t, p, o in src]
+    if ctx:
+        d["ctx"] = {int(k): {str(t): int(i) for t, i in m.items()} for k, m in ctx.items()}
     hdr = msgpack.packb(d, use_bin_type=True)
     head = DURABLE_MAGIC + struct.pack("<I", len(hdr)) + hdr
     return head + bytes(-len(head) % 64)
 
 
 def encode_durable_batch(block: np.ndarray, boot, asg: dict | None = None, names: dict | None = None,
-                         rules: dict | None = None, src=None) -> bytes:
+                         rules: dict | None = None, src=None, ctx: dict | None = None) -> bytes:
     """``src``: ``[(topic, partition, next offset)]`` of the input the block completes (the block
-    should then carry ``FLAG_COMMIT``, see :func:`set_commit_flag`)."""
-    return _durable_head(boot, asg, names, rules, src) + memoryview(np.ascontiguousarray(block, np.uint8)).cast("B")
+    should then carry ``FLAG_COMMIT``, see :func:`set_commit_flag`); ``ctx``: context-id deltas
+    (:meth:`DurableEventStore.add_dictionary`)."""
+    return _durable_head(boot, asg, names, rules, src, ctx) + memoryview(np.ascontiguousarray(block, np.uint8)).cast("B")
 
 
 def frame_durable_batch(frame: tuple, nbytes: int, boot, asg: dict | None = None, names: dict | None = None,
-                        rules: dict | None = None, src=None) -> np.ndarray | None:
+                        rules: dict | None = None, src=None, ctx: dict | None = None) -> np.ndarray | None:
     """Zero-copy :func:`encode_durable_batch` for a block at ``offset`` of ``buffer`` (``frame``)
     with free bytes in front of it; None when the header does not fit."""
     buf, off = frame
-    head = _durable_head(boot, asg, names, rules, src)
+    head = _durable_head(boot, asg, names, rules, src, ctx)
     start = off - len(head)
     if start < 0:
         return None
@@ -520,6 +523,7 @@ class DurableBlockSink:
         self.tags: list[tuple[int, object]] = []      # (store token, caller tag), in order
         self.n_alloc = 0
         self.blocks = self.bytes = self.rows = 0
+        self.index_bytes = 0                          # of which index trailers
         self.disk_wait_s = 0.0                        # time target() waited for the disk (backpressure)
         self._size = 0
         self._lock = threading.Lock()
@@ -593,6 +597,9 @@ class DurableBlockSink:
             ctypes.memset(b.host + nbytes, 0, pad - nbytes)
         native().swseg_seal(b.host, int(first_seq), int(now_ms), self.boot, self.rank, self.world)
         n_rows = int(np.frombuffer((ctypes.c_uint8 * 64).from_address(b.host), np.uint8).view(HDR)[0]["n_rows"])
+        toff = int(native().swseg_ix_offset(b.host))
+        if toff:
+            self.index_bytes += nbytes - toff           # the block's index trailer (swindex.h)
         with self._lock:
             b.refs += 1                                    # the store's reference
         tok = self.store.add_block(b.host, nbytes, owner=b)
@@ -668,6 +675,9 @@ class DurableEventStore(DeviceEventStore):
         self._names: dict[int, dict[int, str]] = {}      # boot -> name id -> name
         self._ctx: dict[int, dict[int, dict]] = {}       # boot -> dimension -> context token -> engine id
         self._dict_version = 0
+        self._ctx_arr: dict[int, np.ndarray] = {}          # boot -> [3, cap] context id by assignment index
+        self._asg_n: dict[int, int] = {}                   # boot -> max assignment index + 1
+        self._asg_tok: dict[int, dict[str, list]] = {}     # boot -> assignment token -> assignment indexes
         self._rules: dict[str, str] = {}                 # alert type -> rule message
         self._lock = threading.RLock()
         self._dict_path = os.path.join(directory, f"dict-{rank}.log")
@@ -688,7 +698,6 @@ class DurableEventStore(DeviceEventStore):
         self._tmaps: OrderedDict = OrderedDict()
         self.max_maps = 16384
         self._tabs = None
-        self._ctx_tabs: dict = {}
         self.scan_threads = int(os.environ.get("SW_STORE_SCAN_THREADS", "16"))
 
     # ------------------------------------------------------------------ API-added events
@@ -745,13 +754,53 @@ class DurableEventStore(DeviceEventStore):
                 self._apply_dict(d)
 
     def _apply_dict(self, d: dict):
+        """Apply a dictionary delta, keeping the reverse maps the read path uses current in O(delta):
+        assignment token -> indexes, and the context id of every assignment per dimension (rebuilt in
+        full only when new context tokens arrive -- new customers / areas / assets, not new rows)."""
         b = int(d.get("boot", 0))
-        self._asg.setdefault(b, {}).update({int(k): v for k, v in (d.get("asg") or {}).items()})
+        asg = self._asg.setdefault(b, {})
+        tok = self._asg_tok.setdefault(b, {})
+        delta = {int(k): v for k, v in (d.get("asg") or {}).items()}
+        for k, v in delta.items():
+            old = asg.get(k)
+            if old and old[0] != v[0] and k in tok.get(old[0], ()):
+                tok[old[0]].remove(k)
+            if not old or old[0] != v[0]:
+                tok.setdefault(v[0], []).append(k)
+        asg.update(delta)
         self._names.setdefault(b, {}).update({int(k): v for k, v in (d.get("names") or {}).items()})
         self._rules.update(d.get("rules") or {})
+        new_ctx = False
         for dim, m in (d.get("ctx") or {}).items():
             self._ctx.setdefault(b, {}).setdefault(int(dim), {}).update({str(k): int(v) for k, v in m.items()})
+            new_ctx = True
+        if delta:
+            self._asg_n[b] = max(self._asg_n.get(b, 0), max(delta) + 1)
+        if new_ctx:
+            self._ctx_fill(b, asg.items())
+        elif delta and b in self._ctx_arr:
+            self._ctx_fill(b, delta.items())
         self._dict_version += 1
+
+    def _ctx_fill(self, b: int, items):
+        """Context ids (customer, area, asset) of the given assignment entries into the boot's table."""
+        ids = self._ctx.get(b)
+        if not ids:
+            return
+        n = self._asg_n.get(b, 0)
+        arr = self._ctx_arr.get(b)
+        if arr is None or arr.shape[1] < n:
+            grown = np.full((3, max(1024, n, 2 * (0 if arr is None else arr.shape[1]))), -1, np.int32)
+            if arr is not None:
+                grown[:, :arr.shape[1]] = arr
+            else:
+                items = self._asg.get(b, {}).items()       # a new table holds every known assignment
+            arr = grown
+        dims = [ids.get(dd, {}) for dd in range(3)]
+        for k, v in items:
+            for dd in range(3):
+                arr[dd, k] = dims[dd].get(v[2 + dd], -1) if len(v) > 2 + dd else -1
+        self._ctx_arr[b] = arr
 
     def add_dictionary(self, boot, asg: dict | None = None, names: dict | None = None, rules: dict | None = None,
                        ctx: dict | None = None):
@@ -907,18 +956,25 @@ class DurableEventStore(DeviceEventStore):
         tabs = self._tabs
         if tabs is not None and tabs[0] == ver:
             return tabs[1]
-        out: dict = {}
-        for e in ents:
-            out.setdefault(int(e["boot"]), []).append(e)
         res = {}
         P = ctypes.c_void_p
-        for b, lst in out.items():
-            trs = [self._trailer(e) for e in lst]
+        prev = tabs[1] if tabs is not None else {}
+        boots = ents["boot"].astype(np.int64)
+        for b in dict.fromkeys(boots.tolist()):
+            lst = ents[boots == b]
+            old = prev.get(b)
+            k = 0
+            if old is not None and old["n"] <= len(lst):
+                # appends (the common case while ingesting): keep the blocks already mapped
+                k = old["n"]
+                if k and not (np.array_equal(old["ents"]["first_seq"], lst["first_seq"][:k])
+                              and np.array_equal(old["ents"]["rank"], lst["rank"][:k])):
+                    k = 0
+            trs = (old["tr"][:k] if k else []) + [self._trailer(e) for e in lst[k:]]
             addrs = [t[0] if t is not None else 0 for t in trs]
             res[b] = {"ents": lst, "tr": trs, "n": len(lst), "addr": (P * len(lst))(*addrs),
-                      "first": np.array([int(e["first_seq"]) for e in lst], np.int64),
-                      "world": np.array([int(e["world"]) for e in lst], np.int64),
-                      "rank": np.array([int(e["rank"]) for e in lst], np.int64)}
+                      "first": lst["first_seq"].astype(np.int64), "world": lst["world"].astype(np.int64),
+                      "rank": lst["rank"].astype(np.int64)}
         live = {self._key(e) for e in ents}
         with self._lock:
             for k in [k for k in self._tmaps if k not in live]:      # retention removed the block
@@ -952,15 +1008,23 @@ class DurableEventStore(DeviceEventStore):
             raise ValueError("event block decode failed")
         return out[:n]
 
-    def alternate_hash_chunks(self, max_ids: int = 1 << 26, wait_s: float = 0.0, threads: int = 16):
+    def alternate_hash_chunks(self, max_ids: int = 1 << 26, wait_s: float = 0.0, threads: int = 16, skip: int = 0):
         """The stored alternate-id hashes, newest blocks first, one numpy u64 chunk per block, at most
-        ``max_ids``: what a restarted engine seeds its store-backed dedup filter with.  The trailers
-        keep only fingerprints, so the blocks' id columns are decoded (natively, on ``threads``
-        threads; ctypes releases the interpreter meanwhile)."""
+        ``max_ids`` after the first ``skip`` of that order: what a restarted engine seeds its
+        store-backed dedup filter with.  The trailers keep only fingerprints, so the blocks' id
+        columns are decoded (natively, on ``threads`` threads; ctypes releases the interpreter
+        meanwhile); skipped blocks are counted from their trailers, not decoded."""
         from concurrent.futures import ThreadPoolExecutor
-        ents = [e for t in self._boot_tables().values() for e in t["ents"]]
-        ents.sort(key=lambda e: (int(e["recv_ms"]), int(e["first_seq"])), reverse=True)
-        left = int(max_ids)
+        pairs = [(e, tr) for t in self._boot_tables().values() for e, tr in zip(t["ents"], t["tr"])]
+        pairs.sort(key=lambda x: (int(x[0]["recv_ms"]), int(x[0]["first_seq"])), reverse=True)
+        ents = []
+        for e, tr in pairs:
+            n = int(tr[2]["n_alt"]) if tr is not None else None
+            if skip > 0 and n is not None and skip >= n:
+                skip -= n
+                continue
+            ents.append(e)
+        left = int(max_ids) + int(skip)
         with ThreadPoolExecutor(max(1, threads)) as pool:
             for i in range(0, len(ents), max(1, threads)):
                 if left <= 0:
@@ -968,9 +1032,13 @@ class DurableEventStore(DeviceEventStore):
                 for h in pool.map(self._block_alt_hashes, ents[i:i + threads]):
                     if left <= 0:
                         break
-                    if len(h):
-                        yield h[:left]
-                        left -= len(h)
+                    take = h[:left]
+                    left -= len(take)
+                    if skip:
+                        cut = min(skip, len(take))
+                        take, skip = take[cut:], skip - cut
+                    if len(take):
+                        yield take
 
     def _alt_candidates(self, hashes) -> dict:
         """hash -> [(boot table, block position, page)] of the blocks whose trailer holds a fingerprint
@@ -986,18 +1054,6 @@ class DurableEventStore(DeviceEventStore):
                     out.setdefault(int(hv), []).append((t, int(bo[j]), int(po[j])))
         return out
 
-    def _page_alt_rows(self, ent, page: int, hv: int) -> list:
-        """Rows of one page whose alternate id hashes to hv (newest first), with their ids."""
-        from ..pipeline.fleet import hash64_strs
-        c = self._page_cols(ent, page)
-        rows = [i for i in range(len(c["date"])) if int(c["flags"][i]) & SEGF_HAS_ALT]
-        if not rows:
-            return []
-        alts = [row_strings(c, i)[0] for i in rows]
-        hs = hash64_strs(alts)
-        return [(int(c["row0"]) + i, a) for i, a, h in sorted(zip(rows, alts, hs.tolist()), reverse=True)
-                if int(h) == hv]
-
     def find_alternate_hashes(self, hashes, covered: tuple | None = None, indexed_only: bool = False) -> dict:
         """alt-id hash -> event id string for the hashes stored on disk, the newest event per hash
         (store-backed dedup beyond the engine's window: ``AlternateIdDeduplicator`` asks the event
@@ -1010,15 +1066,23 @@ class DurableEventStore(DeviceEventStore):
         if not want:
             return found
         cands = self._alt_candidates(want)
+        by_tab: dict = {}
         for hv, lst in cands.items():
-            # newest first: boot tables in store order, blocks newest first within a boot
-            lst.sort(key=lambda x: (int(x[0]["ents"][x[1]]["recv_ms"]), x[1]), reverse=True)
             for t, bi, page in lst:
-                e = t["ents"][bi]
-                hit = self._page_alt_rows(e, page, hv)
-                if hit:
-                    found[hv] = f"{int(e['boot']):x}-{int(self._eids(e, [hit[0][0]])[0])}"
-                    break
+                by_tab.setdefault(id(t), (t, []))[1].append((bi, page, hv))
+        best: dict = {}                               # hash -> (recv_ms, block position, row, boot table)
+        for t, lst in by_tab.values():
+            bis = np.array([x[0] for x in lst], np.int64)
+            ci, rows = self._alt_page_rows(t, bis, [x[1] for x in lst], [x[2] for x in lst])
+            for c, r in zip(ci.tolist(), rows.tolist()):
+                hv = lst[c][2]
+                bi = lst[c][0]
+                key = (int(t["ents"][bi]["recv_ms"]), bi, r)
+                if hv not in best or key > best[hv][0]:
+                    best[hv] = (key, t, bi, r)
+        for hv, (_, t, bi, r) in best.items():
+            e = t["ents"][bi]
+            found[hv] = f"{int(e['boot']):x}-{int(self._eids(e, [r])[0])}"
         if not indexed_only:
             for t in self._boot_tables().values():
                 for e, tr in zip(t["ents"], t["tr"]):
@@ -1044,13 +1108,19 @@ class DurableEventStore(DeviceEventStore):
             return ev
         h = hash64(alt)
         lst = self._alt_candidates([h]).get(h, [])
-        lst.sort(key=lambda x: (int(x[0]["ents"][x[1]]["recv_ms"]), x[1]), reverse=True)
+        by_tab: dict = {}
         for t, bi, page in lst:
-            e = t["ents"][bi]
-            c = self._page_cols(e, page)
-            for r, a in self._page_alt_rows(e, page, h):
-                if a == alt:
-                    return self._materialize(c, r - int(c["row0"]))
+            by_tab.setdefault(id(t), (t, []))[1].append((bi, page))
+        hits = []                                     # (recv_ms, block position, row, boot table)
+        for t, cl in by_tab.values():
+            bis = np.array([x[0] for x in cl], np.int64)
+            ci, rows = self._alt_page_rows(t, bis, [x[1] for x in cl], [h] * len(cl))
+            hits += [(int(t["ents"][bis[c]]["recv_ms"]), int(bis[c]), int(r), t) for c, r in zip(ci.tolist(), rows.tolist())]
+        hits.sort(key=lambda x: x[:3], reverse=True)
+        for _, bi, r, t in hits:                      # newest first; the id string settles a hash collision
+            cols = self._fetch(t, [bi], [r])
+            if row_strings(cols, 0)[0] == alt:
+                return self._materialize(cols, 0)
         for t in self._boot_tables().values():                 # blocks without a trailer
             for e, tr in zip(t["ents"][::-1], t["tr"][::-1]):
                 if tr is not None:
@@ -1193,20 +1263,129 @@ class DurableEventStore(DeviceEventStore):
         if not (sep and num.isdigit()) or b is None:
             return self._objects.get_event_by_id(id)
         eid = int(num)
-        for e in self.seg.index():
-            if int(e["boot"]) != b:
-                continue
-            w, r = int(e["world"]), int(e["rank"])
-            if (eid - r) % w:
-                continue
-            row = (eid - r) // w - int(e["first_seq"])
-            if 0 <= row < int(e["n_rows"]):
-                c, i = self._row_event(e, row)
+        ents = self.seg.index()
+        if len(ents) and eid < (1 << 62):
+            # event id = (first_seq + row) * world + rank: the block holding it, over all blocks at once
+            w = np.maximum(ents["world"].astype(np.int64), 1)
+            r = ents["rank"].astype(np.int64)
+            row = (eid - r) // w - ents["first_seq"].astype(np.int64)
+            hit = np.nonzero((ents["boot"].astype(np.int64) == b) & ((eid - r) % w == 0) & (row >= 0)
+                             & (row < ents["n_rows"].astype(np.int64)))[0]
+            if len(hit):
+                e = ents[int(hit[0])]
+                c, i = self._row_event(e, int(row[int(hit[0])]))
                 return self._materialize(c, i)
         return self._objects.get_event_by_id(id)
 
     def list_command_responses_for_invocation(self, invocation_id, criteria=None):
         return self._objects.list_command_responses_for_invocation(invocation_id, criteria)
+
+    # ------------------------------------------------------------------ native point reads
+    def _file_fds(self, files: np.ndarray):
+        """(fd per entry of ``files`` -- segment file ids -- opened read-only, the fds to close)."""
+        uf, inv = np.unique(np.asarray(files, np.int64), return_inverse=True)
+        opened = []
+        try:
+            for f in uf.tolist():
+                path = self.seg.file_path(int(f))
+                if path is None:
+                    raise KeyError("segment file deleted by retention")
+                opened.append(os.open(path, os.O_RDONLY))
+        except BaseException:
+            for x in opened:
+                os.close(x)
+            raise
+        return np.asarray(opened, np.int32)[inv.reshape(-1)], opened
+
+    def _page_geometry(self, t, bis: np.ndarray, pages: np.ndarray):
+        """(file id, file offset, bytes, rows) of pages ``pages`` of blocks ``bis`` (positions in t)."""
+        n = len(bis)
+        pos, nb = np.empty(n, np.int64), np.empty(n, np.uint32)
+        ents = t["ents"]
+        for bi in np.unique(bis).tolist():
+            m = bis == bi
+            pg = self._pages_of(ents[bi], t["tr"][bi])
+            pos[m] = int(ents[bi]["offset"]) + pg["off"][pages[m]].astype(np.int64)
+            nb[m] = pg["bytes"][pages[m]]
+        n_rows = ents["n_rows"][bis].astype(np.int64)
+        rows = np.minimum(PAGE_ROWS, n_rows - pages * PAGE_ROWS).astype(np.uint32)
+        return ents["file"][bis].astype(np.int64), pos, nb, rows
+
+    def _fetch(self, t, bis, rows) -> dict:
+        """Decoded columns (+ strings, + per-row block fields for :func:`materialize_row`) of rows
+        (block position, row) of one boot table, in request order: each page read and checked once
+        (native ``swseg_fetch_rows``, multi-threaded), only the requested rows kept."""
+        bis, rows = np.asarray(bis, np.int64), np.asarray(rows, np.int64)
+        n = len(bis)
+        pages = rows // PAGE_ROWS
+        order = np.lexsort((pages, bis))
+        sb, sp = bis[order], pages[order]
+        files, pos, nb, prows = self._page_geometry(t, sb, sp)
+        rip = (rows[order] - sp * PAGE_ROWS).astype(np.int32)
+        cols = {"etype": np.empty(n, np.uint8), "level": np.empty(n, np.uint8), "date": np.empty(n, np.int64),
+                "asg": np.empty(n, np.int32), "name": np.empty(n, np.uint16), "v0": np.empty(n, np.float64),
+                "v1": np.empty(n, np.float64), "v2": np.empty(n, np.float64), "flags": np.empty(n, np.uint8)}
+        offs = np.zeros(3 * n + 1, np.int64)
+        fd, opened = self._file_fds(files)
+        try:
+            cap = 2048 * max(1, n)
+            while True:
+                heap = np.empty(cap, np.uint8)
+                k = int(native().swseg_fetch_rows(
+                    _p(fd), _p(pos), _p(nb), _p(prows), _p(rip), n, min(self.scan_threads, 8),
+                    *[_p(cols[c]) for c in ("etype", "level", "date", "asg", "name", "v0", "v1", "v2", "flags")],
+                    _p(heap), cap, _p(offs)))
+                if k >= 0:
+                    break
+                if k <= -(1 << 40):
+                    cap = -k - (1 << 40) + 64
+                    continue
+                raise ValueError(f"corrupt or unreadable event page (request {-k - 1})")
+        finally:
+            for x in opened:
+                os.close(x)
+        inv = np.empty(n, np.int64)
+        inv[order] = np.arange(n)
+        # back to request order (strings: offsets of request i are those of sorted position inv[i])
+        out = {c: v[inv] for c, v in cols.items()}
+        lens = np.diff(offs).reshape(n, 3)[inv]         # (alt id, message, metadata) bytes per request
+        so = np.zeros(3 * n + 1, np.int64)
+        so[1:] = np.cumsum(lens.reshape(-1))
+        per_row = lens.sum(axis=1)
+        # byte p of request i's strings comes from its sorted position's strings at the same distance
+        src = np.repeat(offs[3 * inv] - so[0:3 * n:3], per_row) + np.arange(int(per_row.sum()))
+        out["str_heap"], out["str_off"] = heap[src], so
+        e = t["ents"][bis]
+        out.update(rows=rows, boot=e["boot"].astype(np.int64), first_seq=e["first_seq"].astype(np.int64),
+                   world=e["world"].astype(np.int64), rank=e["rank"].astype(np.int64),
+                   recv_ms=e["recv_ms"].astype(np.int64))
+        return out
+
+    def _alt_page_rows(self, t, bis, pages, hashes) -> tuple[np.ndarray, np.ndarray]:
+        """(candidate index, row in block) of the rows whose alternate-id hash matches, over candidate
+        pages (block position, page, hash) of one boot table (native ``swseg_alt_page_rows``)."""
+        bis, pages = np.asarray(bis, np.int64), np.asarray(pages, np.int64)
+        n = len(bis)
+        if not n:
+            return np.zeros(0, np.int64), np.zeros(0, np.int64)
+        files, pos, nb, prows = self._page_geometry(t, bis, pages)
+        hv = np.asarray(hashes, np.uint64)
+        fd, opened = self._file_fds(files)
+        try:
+            cap = max(16, n)
+            while True:
+                ot, orow = np.empty(cap, np.int64), np.empty(cap, np.int32)
+                k = int(native().swseg_alt_page_rows(_p(fd), _p(pos), _p(nb), _p(prows), _p(hv), n,
+                                                     min(self.scan_threads, 8), _p(ot), _p(orow), cap))
+                if k < 0:
+                    raise ValueError(f"corrupt or unreadable event page (candidate {-k - 1})")
+                if k <= cap:
+                    break
+                cap = k
+        finally:
+            for x in opened:
+                os.close(x)
+        return ot[:k], pages[ot[:k]] * PAGE_ROWS + orow[:k].astype(np.int64)
 
     # ------------------------------------------------------------------ listings
     def _pages_of(self, ent, tr):
@@ -1223,70 +1402,60 @@ class DurableEventStore(DeviceEventStore):
         out["off"], out["bytes"] = pt[:-1], np.diff(pt)
         return out
 
-    def _scan_pages(self, tasks, et: int, d_lo: int, d_hi: int, asg: int = -1, ctx_tab=None, ctx_id: int = 0):
-        """Rows of pages passing (type, date range, assignment | context id), reading each page's
-        leading columns only (native ``swseg_scan_pages``, multi-threaded).  tasks: [(block entry,
-        page, page offset, page bytes)] -> [(task index, row in block, date)] arrays."""
-        if not tasks:
-            return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int64)
-        fds: dict = {}
+    def _scan_pages(self, t, bis, pages, et: int, d_lo: int, d_hi: int, asg: int = -1, ctx_tab=None,
+                    ctx_id: int = 0):
+        """Rows of pages ``pages`` of blocks ``bis`` (positions in boot table t) passing (type, date
+        range, assignment | context id), reading each page's leading columns only (native
+        ``swseg_scan_pages``, multi-threaded) -> (block position, row in block, date) arrays."""
+        bis, pages = np.asarray(bis, np.int64), np.asarray(pages, np.int64)
+        if not len(bis):
+            return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
+        files, pos, nb, _ = self._page_geometry(t, bis, pages)
+        poff = np.zeros(len(bis), np.uint32)
+        pix = pages.astype(np.int32)
+        ct = np.ascontiguousarray(ctx_tab, np.int32) if ctx_tab is not None else np.zeros(1, np.int32)
+        fd, opened = self._file_fds(files)
         try:
-            fd = np.empty(len(tasks), np.int32)
-            for i, (e, _, _, _) in enumerate(tasks):
-                path = self.seg.file_path(int(e["file"]))
-                if path is None:
-                    raise KeyError("segment file deleted by retention")
-                if path not in fds:
-                    fds[path] = os.open(path, os.O_RDONLY)
-                fd[i] = fds[path]
-            boff = np.array([int(t[0]["offset"]) for t in tasks], np.int64)
-            poff = np.array([int(t[2]) for t in tasks], np.uint32)
-            pby = np.array([int(t[3]) for t in tasks], np.uint32)
-            pix = np.array([int(t[1]) for t in tasks], np.int32)
-            ct = np.ascontiguousarray(ctx_tab, np.int32) if ctx_tab is not None else np.zeros(1, np.int32)
             cap = 4096
             while True:
                 ot, orow, od = np.empty(cap, np.int64), np.empty(cap, np.int32), np.empty(cap, np.int64)
-                k = int(native().swseg_scan_pages(_p(fd), _p(boff), _p(poff), _p(pby), _p(pix), len(tasks), int(et),
+                k = int(native().swseg_scan_pages(_p(fd), _p(pos), _p(poff), _p(nb), _p(pix), len(bis), int(et),
                                                   int(asg), _p(ct), len(ct) if ctx_tab is not None else 0, int(ctx_id),
                                                   int(d_lo), int(d_hi), self.scan_threads, _p(ot), _p(orow), _p(od), cap))
                 if k < 0:
                     raise ValueError(f"event page unreadable (task {-k - 1})")
                 if k <= cap:
-                    return ot[:k], orow[:k], od[:k]
+                    return bis[ot[:k]], orow[:k].astype(np.int64), od[:k]
                 cap = k
         finally:
-            for f in fds.values():
+            for f in opened:
                 os.close(f)
 
-    def _rows_for(self, t, blocks, et, d_lo, d_hi, asg=-1, ctx_tab=None, ctx_id=0, pages=None):
-        """(block position, row, date) of every matching row of the listed blocks (all pages, or the
-        pages whose zone maps hold ``asg``)."""
-        tasks, owner = [], []
+    def _rows_for(self, t, blocks, et, d_lo, d_hi, asg=-1, ctx_tab=None, ctx_id=0):
+        """(block position, row, date) of every matching row of the listed blocks (the pages whose
+        zone maps admit the date range, and ``asg`` when given)."""
+        bl, pl = [], []
         for bi in blocks:
-            e, tr = t["ents"][bi], t["tr"][bi]
-            pg = self._pages_of(e, tr)
-            for p in range(len(pg)):
-                z = pg[p]
-                if int(z["date_max"]) < d_lo or int(z["date_min"]) > d_hi:
-                    continue
-                if asg >= 0 and not (int(z["asg_min"]) <= asg <= int(z["asg_max"])):
-                    continue
-                tasks.append((e, p, int(z["off"]), int(z["bytes"])))
-                owner.append(bi)
-        ti, rows, dates = self._scan_pages(tasks, et, d_lo, d_hi, asg, ctx_tab, ctx_id)
-        own = np.asarray(owner, np.int64)
-        return (own[ti] if len(ti) else np.zeros(0, np.int64)), rows.astype(np.int64), dates
+            pg = self._pages_of(t["ents"][bi], t["tr"][bi])
+            m = (pg["date_max"] >= d_lo) & (pg["date_min"] <= d_hi)
+            if asg >= 0:
+                m &= (pg["asg_min"] <= asg) & (pg["asg_max"] >= asg)
+            p = np.nonzero(m)[0]
+            bl.append(np.full(len(p), bi, np.int64))
+            pl.append(p)
+        if not bl:
+            return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
+        return self._scan_pages(t, np.concatenate(bl), np.concatenate(pl), et, d_lo, d_hi, asg, ctx_tab, ctx_id)
 
-    def _asg_pages(self, t, asg: int, d_lo: int, d_hi: int) -> list:
-        """(block position, page) pairs whose assignment / date zone maps admit the assignment."""
+    def _asg_pages(self, t, asg: int, d_lo: int, d_hi: int) -> tuple[np.ndarray, np.ndarray]:
+        """(block positions, pages) whose assignment / date zone maps admit the assignment."""
         cap = max(1024, 4 * t["n"])
         bo, po = np.empty(cap, np.int64), np.empty(cap, np.int64)
         k = int(native().swseg_ix_asg_pages(t["addr"], t["n"], int(asg), int(d_lo), int(d_hi), _p(bo), _p(po), cap))
         if k > cap:
             bo, po = np.empty(k, np.int64), np.empty(k, np.int64)
             k = int(native().swseg_ix_asg_pages(t["addr"], t["n"], int(asg), int(d_lo), int(d_hi), _p(bo), _p(po), k))
-        return list(zip(bo[:k].tolist(), po[:k].tolist()))
+        return bo[:k], po[:k]
 
     def _list_assignments(self, t, asg_idx, et, d_lo, d_hi) -> tuple[int, list]:
         """Rows of the assignments over one boot's blocks: the blocks are clustered by assignment, so
@@ -1294,16 +1463,10 @@ class DurableEventStore(DeviceEventStore):
         parts = []
         legacy = [bi for bi, tr in enumerate(t["tr"]) if tr is None]
         for a in asg_idx:
-            tasks, owner = [], []
-            for bi, p in self._asg_pages(t, a, d_lo, d_hi):
-                e, tr = t["ents"][bi], t["tr"][bi]
-                z = self._pages_of(e, tr)[p]
-                tasks.append((e, p, int(z["off"]), int(z["bytes"])))
-                owner.append(bi)
-            ti, rows, dates = self._scan_pages(tasks, et, d_lo, d_hi, asg=int(a))
-            own = np.asarray(owner, np.int64)
-            if len(ti):
-                parts.append((own[ti], rows.astype(np.int64), dates))
+            bo, po = self._asg_pages(t, a, d_lo, d_hi)
+            b, rows, dates = self._scan_pages(t, bo, po, et, d_lo, d_hi, asg=int(a))
+            if len(b):
+                parts.append((b, rows, dates))
             if legacy:
                 parts.append(self._rows_for(t, legacy, et, d_lo, d_hi, asg=int(a)))
         return self._collect(t, parts)
@@ -1319,24 +1482,14 @@ class DurableEventStore(DeviceEventStore):
         return len(rows), [(dates, eids, bi, rows, t)]
 
     def _ctx_table(self, boot: int, pos: int) -> np.ndarray | None:
-        """Context id (dimension pos - 2) by assignment index for one boot, from the dictionaries;
-        None when the boot's context ids are unknown."""
-        key = (boot, pos, self._dict_version)
-        tab = self._ctx_tabs.get(key)
-        if tab is not None:
-            return tab
-        ids = self._ctx.get(boot, {}).get(pos - 2)
-        if not ids:
+        """Context id (dimension pos - 2) by assignment index for one boot, from the dictionaries
+        (kept current by :meth:`_apply_dict`); None when the boot's context ids are unknown."""
+        if not self._ctx.get(boot, {}).get(pos - 2):
             return None
-        asg = self._asg.get(boot, {})
-        n = (max(asg) + 1) if asg else 0
-        tab = np.full(n, -1, np.int32)
-        for i, ctx in asg.items():
-            if len(ctx) > pos and ctx[pos] in ids:
-                tab[int(i)] = ids[ctx[pos]]
-        self._ctx_tabs = {k: v for k, v in self._ctx_tabs.items() if k[2] == self._dict_version}
-        self._ctx_tabs[key] = tab
-        return tab
+        arr = self._ctx_arr.get(boot)
+        if arr is None:
+            return None
+        return arr[pos - 2, :self._asg_n.get(boot, 0)]
 
     def _list_context(self, t, boot, pos, want, et, d_lo, d_hi, need) -> tuple[int, list]:
         """Rows of customer / area / asset ids over one boot's blocks, from the trailers' key tables:
@@ -1402,16 +1555,20 @@ class DurableEventStore(DeviceEventStore):
             else:
                 cut_d, cut_e = None, None
             more: dict = {}
+            all_cids = {int(ids[tok]) for tok in want if tok in ids}
             for bi, ld, lr, cid in maybe:
                 le = (int(t["first"][bi]) + lr) * int(t["world"][bi]) + int(t["rank"][bi])
                 if cut_d is None or (ld, le) > (cut_d, cut_e):
-                    more.setdefault(bi, set()).add(cid)
+                    more[bi] = all_cids          # the block is rescanned whole: every wanted id
             if more:
                 extra = scan_blocks(more)
-                drop = set(more)
-                cand = [(b[~np.isin(b, list(drop))], r[~np.isin(b, list(drop))], dt[~np.isin(b, list(drop))])
-                        for b, r, dt in cand] + extra
-        return self._collect(t, cand)
+                if cand:
+                    b = np.concatenate([c[0] for c in cand])
+                    keep = ~np.isin(b, np.fromiter(more, np.int64))
+                    cand = [(b[keep], np.concatenate([c[1] for c in cand])[keep],
+                             np.concatenate([c[2] for c in cand])[keep])]
+                cand += extra
+        return total, self._collect(t, cand)[1]
 
     def list_events(self, event_type, index, entity_ids, criteria: DateRangeSearchCriteria | None = None):
         """Events of one type for entities of an index, newest first, with the exact total.
@@ -1435,7 +1592,8 @@ class DurableEventStore(DeviceEventStore):
         for b, t in self._boot_tables().items():
             if pos == 0:
                 with self._lock:
-                    asg_idx = [i for i, ctx in self._asg.get(b, {}).items() if ctx[0] in want]
+                    tok = self._asg_tok.get(b, {})
+                    asg_idx = sorted({i for w in want for i in tok.get(w, ())})
                 n, parts = self._list_assignments(t, asg_idx, et, d_lo, d_hi)
             else:
                 n, parts = self._list_context(t, b, pos, want, et, d_lo, d_hi, need)
@@ -1450,22 +1608,31 @@ class DurableEventStore(DeviceEventStore):
         rows = np.concatenate([x[3] for x in found])
         order = np.lexsort((-eids, -dates))
 
-        def mat(o):
-            t = found[which[o]][4]
-            return self._materialize(*self._row_event(t["ents"][int(pos_[o])], int(rows[o])))
+        def mat(sel):
+            """The events of the selected candidates, read together (one native fetch per boot)."""
+            evs = [None] * len(sel)
+            tabs = [found[int(k)][4] for k in which[sel]]
+            groups: dict = {}
+            for j, t in enumerate(tabs):
+                groups.setdefault(id(t), (t, []))[1].append(j)
+            for t, js in groups.values():
+                cols = self._fetch(t, pos_[sel[js]], rows[sel[js]])
+                for m, j in enumerate(js):
+                    evs[j] = self._materialize(cols, m)
+            return evs
         if objs:
             if paged:
                 order = order[:need + len(objs)]
-            merged = [mat(o) for o in order] + objs
+            merged = mat(order) + objs
             merged.sort(key=lambda ev: -(ev.event_date or 0))
             return SearchResults(total, c.slice(merged))
         if paged:
             start = (max(1, c.page_number) - 1) * c.page_size
             order = order[start:start + c.page_size]
-        return SearchResults(total, [mat(o) for o in order])
+        return SearchResults(total, mat(order))
 
     def _materialize(self, cols: dict, i: int):
-        b = cols["header"]["boot"]
+        b = int(cols["boot"][i]) if "rows" in cols else cols["header"]["boot"]
         return materialize_row(cols, i, self._asg.get(b, {}), self._names.get(b, {}), self._rules)
 
     def dictionary(self, boot, asg_ids=(), name_ids=()) -> dict:
@@ -1484,10 +1651,15 @@ def materialize_row(cols: dict, i: int, asg: dict, names: dict, rules: dict):
     [assignment, device, customer, area, asset, ...]), alternate id, metadata, and per type the name /
     value, coordinates (elevation when sent), alert source / level / type / message, or the
     engine's presence state change.  ``names``: name id -> name; ``rules``: rule alert type -> message."""
-    h = cols["header"]
+    if "rows" in cols:           # rows fetched across blocks (DurableEventStore._fetch): per-row block fields
+        h = {"boot": int(cols["boot"][i]), "first_seq": int(cols["first_seq"][i]), "world": int(cols["world"][i]),
+             "rank": int(cols["rank"][i]), "recv_ms": int(cols["recv_ms"][i])}
+        row = int(cols["rows"][i])
+    else:
+        h = cols["header"]
+        row = int(cols.get("row0", 0)) + i
     b = h["boot"]
     ctx = asg.get(int(cols["asg"][i])) or [None] * 5
-    row = int(cols.get("row0", 0)) + i
     eid = (h["first_seq"] + row) * h["world"] + h["rank"]
     alt, msg, md = row_strings(cols, i)
     f = int(cols["flags"][i])

@@ -149,13 +149,19 @@ class DeviceEventManagement:
         f = getattr(self.store, "dictionary", None)
         return f(boot, asg_ids, name_ids) if f is not None else {"asg": {}, "names": {}, "rules": {}}
 
-    def durable_alternate_hashes(self, max_ids: int = 1 << 26) -> bytes:
-        """Alternate-id hashes of the durable store, newest first (u64 little endian, at most
-        ``max_ids``): an engine tenant seeds its store-backed dedup filter with them on start."""
+    def durable_alternate_hashes(self, max_ids: int = 1 << 24, skip: int = 0) -> bytes:
+        """Alternate-id hashes of the durable store, newest first (u64 little endian): ids ``skip`` to
+        ``skip + max_ids`` of that order -- an engine tenant seeds its store-backed dedup filter with
+        them on start, chunk by chunk."""
         f = getattr(self.store, "alternate_hash_chunks", None)
         if f is None:
             return b""
-        return b"".join(np.ascontiguousarray(c, np.uint64).tobytes() for c in f(max_ids))
+        return b"".join(np.ascontiguousarray(c, np.uint64).tobytes() for c in f(int(max_ids), skip=int(skip)))
+
+    def durable_alternate_id_count(self) -> int:
+        """Alternate ids the durable store holds (from its block index trailers)."""
+        f = getattr(self.store, "alternate_id_count", None)
+        return int(f()) if f is not None else 0
 
     def durable_find_alternate_hashes(self, hashes: bytes, covered: list | None = None,
                                       indexed_only: bool = False) -> bytes:

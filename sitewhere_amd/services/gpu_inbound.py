@@ -789,6 +789,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             if tr is not None:
                 tr.append(time.perf_counter())
             asg = {}
+            ctx: dict = {}
             for ai in self._asg_dirty:
                 a = self._asg_entities.get(ai)
                 if a is not None:
@@ -797,6 +798,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     di = self.dev_index.idx.get(a.device_id, -1)
                     asg[ai] = [a.id, a.device_id, a.customer_id, a.area_id, a.asset_id, self._dev_tokens.get(di),
                                self._dev_types.get(di)]
+                    # the engine ids the block index trailers key customer / area / asset by
+                    for dim, (tok, m) in enumerate(((a.customer_id, self.customers), (a.area_id, self.areas),
+                                                    (a.asset_id, self.assets))):
+                        if tok is not None and tok in m.idx:
+                            ctx.setdefault(dim, {})[tok] = m.idx[tok]
             self._asg_dirty.clear()
             # the engine's host name dictionary grows when a step learns names or rules add alert
             # types (an np.unique over the rows' name ids cost ~10 ms per 1M-row batch)
@@ -806,6 +812,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             names = dict(self._nid2name) if len(self._nid2name) != self._names_sent else {}
             self._names_sent = len(self._nid2name)
         rules = {t.alert_type: t.alert_message for t in self.engine.tests}
+        self._ctx_delta = ctx
         return asg, names, rules
 
     def durable_payload(self, res, key=None, tr: list | None = None):
@@ -822,13 +829,14 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         if key is not None:
             src = [(self._src_topic(key[0]), key[1], key[2] + 1)]
             set_commit_flag(res.block)
+        ctx = getattr(self, "_ctx_delta", None) or None
         if res.block_frame is not None:
-            v = frame_durable_batch(res.block_frame, len(res.block), self.boot, asg, names, rules, src)
+            v = frame_durable_batch(res.block_frame, len(res.block), self.boot, asg, names, rules, src, ctx=ctx)
             if v is not None:
                 self.zc_framed += 1
                 return v
         self.zc_copied += 1
-        return encode_durable_batch(res.block, self.boot, asg, names, rules, src)
+        return encode_durable_batch(res.block, self.boot, asg, names, rules, src, ctx=ctx)
 
     def _src_topic(self, topic: str) -> str:
         """Input name in commit records: offsets only mean something within one incarnation of the
@@ -849,12 +857,24 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             return
         # store-backed dedup filter: seeded with the ids already stored, so a device re-sending an old
         # payload after a restart is still handed to the store check
-        if getattr(self.engine.cfg, "dedup_bloom_bits", 0) and hasattr(em, "durable_alternate_hashes"):
-            h = np.frombuffer(em.durable_alternate_hashes(), np.uint64)
-            self._stored_ids = len(h)
-            if len(h):
+        bits = int(getattr(self.engine.cfg, "dedup_bloom_bits", 0) or 0)
+        if bits and hasattr(em, "durable_alternate_hashes"):
+            # seed up to the filter's capacity (not a fixed 2^26), in chunks (no one
+            # 512 MB blob through the API), and count every stored id for the sizing report
+            cap = bits // self.FILTER_BITS_PER_ID
+            count = getattr(em, "durable_alternate_id_count", None)
+            self._stored_ids = int(count()) if count is not None else 0
+            seeded, skip = 0, 0
+            while seeded < cap:
+                h = np.frombuffer(em.durable_alternate_hashes(min(cap - seeded, 1 << 24), skip=skip), np.uint64)
+                if not len(h):
+                    break
                 self.engine.bloom_add(h)
-                self.logger.info("dedup filter seeded with %d stored alternate ids", len(h))
+                seeded += len(h)
+                skip += len(h)
+            self._stored_ids = max(self._stored_ids, seeded)
+            if seeded:
+                self.logger.info("dedup filter seeded with %d of %d stored alternate ids", seeded, self._stored_ids)
         group = self.raw_consumer.group
         for topic in self.raw_consumer.topics:
             for p in range(bus.partitions(topic) if hasattr(bus, "partitions") else 1):

@@ -6,7 +6,7 @@ consumer-group offsets, a durable directory), the CPU engine's fork-join pool an
 device-protocol decoder (20,000 corrupted payloads, string refs included) from many threads, and
 encodes / verifies / decodes a lossless durable block of the decoded events (strings copied from an
 exactly sized batch).  It is compiled together with ``swnative.cpp``, ``swcpuengine.cpp`` and
-``swseg.cpp`` twice: with ThreadSanitizer, and with
+``swseg.cpp`` / ``swindex.cpp`` twice: with ThreadSanitizer, and with
 AddressSanitizer + UndefinedBehaviorSanitizer.  Host code only -- no GPU code is instrumented.
 """
 from __future__ import annotations
@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = [os.path.join(ROOT, "csrc", "native", "tests", "stress_native.cpp"),
        os.path.join(ROOT, "csrc", "native", "swnative.cpp"),
        os.path.join(ROOT, "csrc", "native", "swcpuengine.cpp"),
-       os.path.join(ROOT, "csrc", "native", "swseg.cpp")]
+       os.path.join(ROOT, "csrc", "native", "swseg.cpp"),
+       os.path.join(ROOT, "csrc", "native", "swindex.cpp")]
 CXX = shutil.which("g++")
 
 SANITIZERS = {

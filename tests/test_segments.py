@@ -365,121 +365,176 @@ def test_failed_append_is_retried_not_skipped_as_a_replay(tmp_path):
     es.close()
 
 
-def test_block_indexes_answer_like_the_scan(tmp_path):
-    """Indexed reads (postings by assignment + type, alternate-id hashes, single-page reads) return
-    exactly what decoding and scanning every block returns: totals, newest-first order across blocks,
-    date ranges, paging, point lookups by id and alternate id, store-backed dedup hashes."""
+def _ctx_store_blocks(tmp_path, n_blocks=5, rows_per=3000, dates="random", n_asg=40, trailers=True, seed=3):
+    """A store of engine-like blocks: assignment contexts with engine ids (customer i % 3, area i % 2,
+    asset i % 5), trailers built with that context table, dictionaries with the context ids."""
+    es = sg.DurableEventStore(str(tmp_path / "es"), direct=False)
+    asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % 3}", f"area-{i % 2}", f"asset-{i % 5}"] for i in range(n_asg)}
+    ctx_tab = np.array([[i, i % 3, i % 2, i % 5] for i in range(n_asg)], np.int32)
+    ctx = {0: {f"cust-{k}": k for k in range(3)}, 1: {f"area-{k}": k for k in range(2)},
+           2: {f"asset-{k}": k for k in range(5)}}
+    names = {i: f"mx.metric{i}" for i in range(20)}
+    blocks, exp_all, n0 = [], [], 0
+    rng = np.random.default_rng(seed)
+    for b in range(n_blocks):
+        rows, recs, spans, raw = synth_rows(rows_per, seed=20 + b)
+        rows["assignment"] = rng.integers(0, n_asg, len(rows))
+        if dates == "random":
+            rows["event_date"] = 1_700_000_000_000 + rng.integers(0, 5_000_000, len(rows))   # out of order
+        else:                           # real devices: each block newer than the last, a little jitter
+            rows["event_date"] = 1_700_000_000_000 + b * 1_000_000 + rng.integers(0, 50_000, len(rows))
+        # persist order clustered by assignment (what the engines do)
+        o = np.argsort(rows["assignment"], kind="stable")
+        rows, recs, spans = rows[o], recs[o], spans[o]
+        blk = sg.encode_block(rows, recs, spans, raw, index=trailers, ctx=ctx_tab)
+        sg.seal(blk, n0, 1_700_000_100_000 + b, 0xc0, 0, 1)
+        es.wait(es.add_encoded(blk, asg=asg, names=names, ctx=ctx))
+        blocks.append((blk.copy(), n0))
+        exp_all += [(n0 + j, s_[0]) for j, s_ in enumerate(expected_strings(recs, spans, raw))]
+        n0 += len(rows)
+    return es, asg, blocks, exp_all
+
+
+def _brute(blocks, asg, etype, index, ents, c):
+    """What the store must answer: every block decoded and filtered, newest first (date, then id)."""
+    from sitewhere_amd.persistence.segments import _CTX, _ETYPE
+    from sitewhere_amd.models.domain import DeviceEventIndex, DeviceEventType
+    et = _ETYPE[DeviceEventType(etype)]
+    pos = _CTX[DeviceEventIndex(index)]
+    hits = []
+    for blk, n0 in blocks:
+        cols = sg.decode_block(blk)
+        for i in range(len(cols["date"])):
+            d = int(cols["date"][i])
+            if int(cols["etype"][i]) != et or asg[int(cols["asg"][i])][pos] not in ents:
+                continue
+            if (c.start_date is not None and d < c.start_date) or (c.end_date is not None and d > c.end_date):
+                continue
+            hits.append((d, n0 + i))
+    hits.sort(key=lambda x: (-x[0], -x[1]))
+    total = len(hits)
+    if c.page_size > 0:
+        start = (max(1, c.page_number) - 1) * c.page_size
+        hits = hits[start:start + c.page_size]
+    return total, [(f"c0-{e}", d) for d, e in hits]
+
+
+@pytest.mark.parametrize("dates", ["random", "increasing"])
+def test_block_indexes_answer_like_the_scan(tmp_path, dates):
+    """Reads through the index trailers (assignment zone maps + leading-column page scans, context-key
+    counts and heads merged across blocks, alternate-id buckets) return exactly what decoding and
+    filtering every block returns: totals, newest-first order across blocks, date ranges (blocks
+    straddling a bound), paging deep enough to exhaust blocks' heads, point lookups, dedup hashes.
+    Dates out of order within and across blocks, or increasing block by block (real devices: page 1
+    then comes from the newest block, whose heads run out)."""
     from sitewhere_amd.models.domain import DateRangeSearchCriteria
     from sitewhere_amd.pipeline.fleet import hash64
-    es = sg.DurableEventStore(str(tmp_path / "es"), direct=False)
-    asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % 3}", f"area-{i % 2}", f"asset-{i % 5}"] for i in range(40)}
-    names = {i: f"mx.metric{i}" for i in range(20)}
-    exp_all, n0 = [], 0
-    rng = np.random.default_rng(3)
-    for b in range(5):
-        rows, recs, spans, raw = synth_rows(3000, seed=20 + b)
-        rows["assignment"] = rng.integers(0, 40, len(rows))
-        rows["event_date"] = 1_700_000_000_000 + rng.integers(0, 5_000_000, len(rows))   # out of order
-        blk = sg.encode_block(rows, recs, spans, raw)
-        sg.seal(blk, n0, 1_700_000_100_000 + b, 0xc0, 0, 1)
-        es.wait(es.add_encoded(blk, asg=asg, names=names))
-        exp_all += [(n0 + j, s[0]) for j, s in enumerate(expected_strings(recs, spans, raw))]
-        n0 += len(rows)
-    assert es.index_wait(60) and es.index_stats()["indexed"] == 5
+    es, asg, blocks, exp_all = _ctx_store_blocks(tmp_path, dates=dates)
+    assert es.index_stats()["indexed"] == 5
+    t0 = 1_700_000_000_000
     crits = [DateRangeSearchCriteria(page_size=0), DateRangeSearchCriteria(page_size=7),
-             DateRangeSearchCriteria(page_number=3, page_size=5),
-             DateRangeSearchCriteria(page_size=10, start_date=1_700_001_000_000, end_date=1_700_003_000_000),
-             DateRangeSearchCriteria(page_size=0, start_date=1_700_002_000_000)]
+             DateRangeSearchCriteria(page_number=3, page_size=5), DateRangeSearchCriteria(page_size=100),
+             DateRangeSearchCriteria(page_number=2, page_size=40),
+             DateRangeSearchCriteria(page_size=10, start_date=t0 + 1_000_000, end_date=t0 + 3_000_000),
+             DateRangeSearchCriteria(page_size=0, start_date=t0 + 2_000_000)]
     queries = [(t, ix, ents) for t in ("Measurement", "Location", "Alert")
                for ix, ents in (("Assignment", ["asg-3"]), ("Assignment", ["asg-5", "asg-9", "nope"]),
-                                ("Customer", ["cust-1"]), ("Area", ["area-0"]))]
+                                ("Customer", ["cust-1"]), ("Area", ["area-0"]), ("Asset", ["asset-2", "asset-4"]),
+                                ("Customer", ["nobody"]))]
+    n_checked = 0
+    for t, ix, ents in queries:
+        for c in crits:
+            r = es.list_events(t, ix, ents, c)
+            got = (r.num_results, [(e.id, e.event_date) for e in r.results])
+            want = _brute(blocks, asg, t, ix, set(ents), c)
+            assert got == want, (t, ix, ents, c)
+            n_checked += want[0]
+    assert n_checked > 5000
+    rng = np.random.default_rng(9)
     with_alt = [(eid, a) for eid, a in exp_all if a is not None]
     picks = [with_alt[i] for i in rng.choice(len(with_alt), 40, replace=False)]
-
-    def answers():
-        out = []
-        for t, ix, ents in queries:
-            for c in crits:
-                r = es.list_events(t, ix, ents, c)
-                out.append((r.num_results, [(e.id, e.event_date, e.alternate_id) for e in r.results]))
-        out.append([(es.get_event_by_alternate_id(a) or None) and es.get_event_by_alternate_id(a).id
-                    for _, a in picks])
-        out.append([es.get_event_by_id(f"c0-{eid}").alternate_id for eid, _ in picks])
-        out.append(es.find_alternate_hashes([hash64(a) for _, a in picks] + [12345]))
-        return out
-    indexed = answers()
-    # the same queries with every block scanned (indexes dropped, indexer stopped)
-    es._ix_stop.set()
-    es._ix_thread.join(10)
-    es._ix.clear()
-    es._ix_tabs = None                  # the native multi-block tables go with the indexes
-    scanned = answers()
-    assert indexed == scanned
-    assert sum(x[0] for x in indexed[:len(queries) * len(crits)]) > 2000
-    assert indexed[-3] == [f"c0-{eid}" for eid, _ in picks]
-    assert indexed[-2] == [a for _, a in picks]
+    assert [es.get_event_by_alternate_id(a).id for _, a in picks] == [f"c0-{eid}" for eid, _ in picks]
+    assert [es.get_event_by_id(f"c0-{eid}").alternate_id for eid, _ in picks] == [a for _, a in picks]
+    found = es.find_alternate_hashes([hash64(a) for _, a in picks] + [12345])
+    assert found == {hash64(a): f"c0-{eid}" for eid, a in picks}
+    assert es.alternate_id_count() == len(with_alt)
     es.close()
-    # reopen: the sidecar indexes are loaded, not rebuilt
+    # reopen: the trailers are read from the segment files as they are
     es2 = sg.DurableEventStore(str(tmp_path / "es"), direct=False)
-    assert es2.index_wait(30) and es2.index_stats()["indexed"] == 5
-    r = es2.list_events("Measurement", "Assignment", ["asg-3"], DateRangeSearchCriteria(page_size=0))
-    assert (r.num_results, [e.id for e in r.results]) == (indexed[0][0], [x[0] for x in indexed[0][1]])
+    c = DateRangeSearchCriteria(page_size=0)
+    r = es2.list_events("Measurement", "Area", ["area-0"], c)
+    assert (r.num_results, [(e.id, e.event_date) for e in r.results]) == \
+        _brute(blocks, asg, "Measurement", "Area", {"area-0"}, c)
     es2.close()
 
 
-def test_block_indexes_spill_to_files_past_the_ram_budget(tmp_path):
-    """The newest block indexes stay in RAM up to ``index_ram_bytes``; older ones are swapped for
-    their memory-mapped files and answer the same lookups."""
-    from sitewhere_amd.pipeline.fleet import hash64
-    es = sg.DurableEventStore(str(tmp_path / "es"), direct=False)
-    es.index_ram_bytes = 0
-    n0, alts = 0, []
-    for b in range(3):
-        rows, recs, spans, raw = synth_rows(2000, seed=40 + b)
-        blk = sg.encode_block(rows, recs, spans, raw)
-        sg.seal(blk, n0, 1_700_000_100_000 + b, 0xc0, 0, 1)
-        es.wait(es.add_encoded(blk))
-        alts += [(n0 + j, s[0]) for j, s in enumerate(expected_strings(recs, spans, raw)) if s[0] is not None]
-        n0 += len(rows)
-    assert es.index_wait(60)
-    deadline = time.time() + 30
-    while time.time() < deadline and not all(isinstance(ix.pk, np.memmap) for ix in list(es._ix.values())):
-        time.sleep(0.02)
-    assert len(es._ix) == 3 and all(isinstance(ix.pk, np.memmap) for ix in es._ix.values())
-    eid, alt = alts[len(alts) // 2]
+def test_blocks_without_trailers_are_scanned(tmp_path):
+    """Blocks from a writer that built no index trailer (an older store, a foreign producer) are
+    answered by decoding them: same results as the indexed blocks."""
+    from sitewhere_amd.models.domain import DateRangeSearchCriteria
+    es, asg, blocks, exp_all = _ctx_store_blocks(tmp_path, n_blocks=3, trailers=False)
+    assert es.index_stats()["indexed"] == 0
+    for ix, ents in (("Assignment", ["asg-3"]), ("Area", ["area-1"]), ("Customer", ["cust-2"])):
+        for c in (DateRangeSearchCriteria(page_size=0), DateRangeSearchCriteria(page_size=9)):
+            r = es.list_events("Measurement", ix, ents, c)
+            assert (r.num_results, [(e.id, e.event_date) for e in r.results]) == \
+                _brute(blocks, asg, "Measurement", ix, set(ents), c)
+    eid, alt = [(e, a) for e, a in exp_all if a is not None][17]
     assert es.get_event_by_alternate_id(alt).id == f"c0-{eid}"
-    assert es.find_alternate_hashes([hash64(alt)]) == {hash64(alt): f"c0-{eid}"}
     es.close()
 
 
-def test_store_checks_share_one_index_build_per_block(tmp_path, monkeypatch):
-    """Concurrent lookups that reach a block before the indexer build its index once; the index is
-    then live for every later lookup and the indexer only writes its files."""
-    import threading
-    from sitewhere_amd.pipeline.fleet import hash64
-    es = sg.DurableEventStore(str(tmp_path / "es"), direct=False, index=False)
-    rows, recs, spans, raw = synth_rows(3000, seed=77)
-    blk = sg.encode_block(rows, recs, spans, raw)
-    sg.seal(blk, 0, 1_700_000_100_000, 0xc0, 0, 1)
-    es.wait(es.add_encoded(blk))
-    alts = [(j, s[0]) for j, s in enumerate(expected_strings(recs, spans, raw)) if s[0] is not None]
-    builds, real = [], sg.BlockIndex.build
+def test_reopen_after_retention_deleted_a_file(tmp_path):
+    """with retention deleting the oldest segment file between runs, every remaining block
+    still answers from its own trailer (trailers live inside the block record: nothing keyed by
+    process-local file ids, nothing left behind)."""
+    from sitewhere_amd.models.domain import DateRangeSearchCriteria
+    d = str(tmp_path / "es")
+    ctx_tab = np.array([[i, i % 3, i % 2, i % 5] for i in range(40)], np.int32)
+    asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % 3}", f"area-{i % 2}", f"asset-{i % 5}"] for i in range(40)}
+    es = sg.DurableEventStore(d, direct=False, rotate_bytes=1 << 16)
+    n0, kept = 0, []
+    rng = np.random.default_rng(1)
+    for b in range(6):
+        rows, recs, spans, raw = synth_rows(1500, seed=50 + b)
+        rows["assignment"] = np.sort(rng.integers(0, 40, len(rows)))
+        blk = sg.encode_block(rows, recs, spans, raw, index=True, ctx=ctx_tab)
+        sg.seal(blk, n0, 1_700_000_100_000 + b, 0xc0, 0, 1)
+        es.wait(es.add_encoded(blk, asg=asg))
+        kept.append((blk.copy(), n0))
+        n0 += len(rows)
+    es.close()
+    files = sorted(f for f in os.listdir(d) if f.endswith(".sweg"))
+    assert len(files) >= 3
+    os.remove(os.path.join(d, files[0]))                 # retention, while the store was closed
+    es2 = sg.DurableEventStore(d, direct=False)
+    live = {int(e["first_seq"]) for e in es2.seg.index()}
+    blocks = [(b, n) for b, n in kept if n in live]
+    assert 0 < len(blocks) < 6
+    c = DateRangeSearchCriteria(page_size=0)
+    for ix, ents in (("Assignment", ["asg-7"]), ("Area", ["area-1"])):
+        r = es2.list_events("Measurement", ix, ents, c)
+        assert (r.num_results, [(e.id, e.event_date) for e in r.results]) == \
+            _brute(blocks, asg, "Measurement", ix, set(ents), c)
+    es2.close()
 
-    def slow_build(block, min_date):
-        builds.append(1)
-        time.sleep(0.2)                 # keep the build in flight while the other lookups arrive
-        return real(block, min_date)
-    monkeypatch.setattr(sg.BlockIndex, "build", staticmethod(slow_build))
-    got = [None] * 6
 
-    def look(i):
-        eid, alt = alts[i * 7]
-        ev = es.get_event_by_alternate_id(alt)
-        got[i] = ev is not None and ev.id == f"c0-{eid}"
-    ts = [threading.Thread(target=look, args=(i,)) for i in range(len(got))]
-    [t.start() for t in ts]
-    [t.join(30) for t in ts]
-    assert all(got) and len(builds) == 1
-    assert es.find_alternate_hashes([hash64(alts[3][1])]) == {hash64(alts[3][1]): f"c0-{alts[3][0]}"}
-    assert len(builds) == 1
+def test_point_fetch_equals_page_decode(tmp_path):
+    """The store's native point reads (swseg_fetch_rows: a pass over the leading rows of a page, not
+    a decode of the page) return exactly what decoding the whole page gives, strings included, in
+    request order -- duplicates and several rows of one page included."""
+    es, _, blocks, _ = _ctx_store_blocks(tmp_path, n_blocks=3, rows_per=2500)
+    t = next(iter(es._boot_tables().values()))
+    rng = np.random.default_rng(4)
+    bis = rng.integers(0, t["n"], 200)
+    rows = np.array([rng.integers(0, int(t["ents"][b]["n_rows"])) for b in bis])
+    bis, rows = np.concatenate([bis, bis[:30], [0, 0]]), np.concatenate([rows, rows[:30] ^ 1, [0, 0]])
+    got = es._fetch(t, bis, rows)
+    for i, (b, r) in enumerate(zip(bis.tolist(), rows.tolist())):
+        d = sg.decode_block(blocks[b][0], pages=(r // 1024, r // 1024 + 1))
+        k = r - d["row0"]
+        for col in ("etype", "level", "date", "asg", "name", "v0", "v1", "v2", "flags"):
+            assert got[col][i] == d[col][k] or (np.isnan(got[col][i]) and np.isnan(d[col][k])), (col, b, r)
+        assert sg.row_strings(got, i) == sg.row_strings(d, k)
+        assert es._materialize(got, i).id == f"c0-{blocks[b][1] + r}"
     es.close()
