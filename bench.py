@@ -482,6 +482,9 @@ def main():
     reads = None
     if dur is not None and args.read_threads > 0:
         from sitewhere_amd.persistence.read_load import ReadLoad
+        # the readers' Python holds the interpreter between their native calls: hand it back to
+        # the step loop every 0.2 ms rather than the default 5 ms
+        sys.setswitchinterval(2e-4)
         reads = ReadLoad(dur["store"], int(np.max(dev)) + 1, threads=args.read_threads,
                          pause_s=args.read_pause_ms / 1e3, seed=rank)
     barrier()

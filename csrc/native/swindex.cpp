@@ -321,6 +321,62 @@ int64_t swseg_ix_asg_pages(const uint8_t* const* t, int64_t n, int32_t asg, int6
   return k;
 }
 
+void swseg_ix_ctx_find(const uint8_t* const* t, int64_t n, int32_t d, uint32_t key, int64_t* out);
+
+// swseg_ix_ctx_find with the heads gathered: out[7 i ..] as there but o[4] = index of block i's
+// first head in the flat outputs and o[6] = 0; the heads of every found block, block by block
+// (newest first within a block), into head_blk / head_row / head_date (at most cap).  Returns the
+// heads written in total (> cap: call again with that cap).
+int64_t swseg_ix_ctx_heads(const uint8_t* const* t, int64_t n, int32_t d, uint32_t key, int64_t* out,
+                           int64_t* head_blk, int64_t* head_row, int64_t* head_date, int64_t cap) {
+  swseg_ix_ctx_find(t, n, d, key, out);
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t* o = out + 7 * i;
+    if (o[0] != 1) { o[4] = k; o[6] = 0; continue; }
+    const uint32_t* hr = reinterpret_cast<const uint32_t*>((uintptr_t)o[4]);
+    const int64_t* hd = reinterpret_cast<const int64_t*>((uintptr_t)o[6]);
+    const int64_t nh = o[5];
+    for (int64_t j = 0; j < nh; ++j, ++k) {
+      if (k < cap) {
+        uint32_t r;
+        int64_t dt;
+        memcpy(&r, hr + j, 4);
+        memcpy(&dt, hd + j, 8);
+        head_blk[k] = i;
+        head_row[k] = r;
+        head_date[k] = dt;
+      }
+    }
+    o[4] = k - nh;
+    o[6] = 0;
+  }
+  return k;
+}
+
+// Geometry of pages pages[j] of blocks blk[j] from their trailers' page tables: offset in the block
+// and bytes (out_bytes[j] = 0 where block blk[j] has no trailer, or the page is out of range).
+// Returns how many could not be resolved.
+int64_t swseg_ix_page_geom(const uint8_t* const* t, int64_t n_t, const int64_t* blk, const int64_t* pages, int64_t n,
+                           uint32_t* out_off, uint32_t* out_bytes) {
+  int64_t miss = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    out_off[j] = 0;
+    out_bytes[j] = 0;
+    const int64_t b = blk[j];
+    const uint8_t* x = b >= 0 && b < n_t ? t[b] : nullptr;
+    if (!x) { ++miss; continue; }
+    SwIxHdr h;
+    memcpy(&h, x, sizeof(h));
+    if (pages[j] < 0 || pages[j] >= (int64_t)h.n_pages) { ++miss; continue; }
+    SwIxPage pg;
+    memcpy(&pg, x + h.off_pages + sizeof(SwIxPage) * (size_t)pages[j], sizeof(pg));
+    out_off[j] = pg.off;
+    out_bytes[j] = pg.bytes;
+  }
+  return miss;
+}
+
 // Context-key lookup over many blocks: for block i (trailer t[i]) and dimension d, the entry of
 // `key`: out[7 i ..] = (status, count, date_min, date_max, head rows address, n_heads, head dates
 // address) with status 1 = found, 0 = absent from the block, -1 = the dimension is not indexed there

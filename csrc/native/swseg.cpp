@@ -1232,7 +1232,82 @@ struct SegStore {
   int64_t total_bytes = 0;
   uint8_t* commit_buf = nullptr;          // one SEG_COMMIT_BYTES record, aligned for O_DIRECT
   std::map<uint64_t, int64_t> sources;    // durable input offsets (max per key)
+  // In-memory copies of the blocks' index trailers (parallel to `index`; null when not held): the
+  // read path searches them without touching the disk.  Copied while the block is written (by the
+  // copier thread, from the caller's buffer) and on recovery; oldest dropped beyond trailer_cap.
+  std::vector<uint8_t*> tr_ptr;
+  std::vector<int64_t> tr_len;
+  int64_t trailer_cap = 16ll << 30;
+  int64_t trailer_bytes = 0;
+  std::vector<std::pair<int64_t, uint8_t*>> grave;   // dropped copies, freed 120 s later (readers' grace)
+  std::thread copier;
+  std::mutex cmu;
+  std::condition_variable ccv;
+  const std::vector<SegItem>* cjob = nullptr;        // the batch whose trailers to copy
+  std::vector<std::pair<uint8_t*, int64_t>> cout;    // one per item (null: no trailer)
+  bool cdone = true;
+  bool cstop = false;
 };
+
+static int64_t seg_now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// A block's index trailer (null when it has none), copied to a new buffer.
+static std::pair<uint8_t*, int64_t> trailer_copy(const uint8_t* b, int64_t len) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  if (!(h.flags & SEG_FLAG_INDEX) || (int64_t)h.bytes > len) return {nullptr, 0};
+  const uint32_t toff = ((const uint32_t*)(b + 64))[h.n_pages];
+  if (toff >= h.bytes) return {nullptr, 0};
+  const int64_t n = (int64_t)h.bytes - toff;
+  uint8_t* c = (uint8_t*)aligned_alloc(64, (size_t)((n + 63) / 64 * 64));
+  if (!c) return {nullptr, 0};
+  memcpy(c, b + toff, (size_t)n);
+  return {c, n};
+}
+
+// Caller holds s->mu: drop the oldest held trailers beyond the cap, and free dropped copies whose
+// grace has passed.
+static void trailer_trim(SegStore* s) {
+  for (size_t i = 0; i < s->tr_ptr.size() && s->trailer_bytes > s->trailer_cap; ++i) {
+    if (!s->tr_ptr[i]) continue;
+    s->grave.push_back({seg_now_ms(), s->tr_ptr[i]});
+    s->trailer_bytes -= s->tr_len[i];
+    s->tr_ptr[i] = nullptr;
+    s->tr_len[i] = 0;
+  }
+  const int64_t now = seg_now_ms();
+  size_t k = 0;
+  for (auto& g : s->grave) {
+    if (now - g.first > 120000) free(g.second);
+    else s->grave[k++] = g;
+  }
+  s->grave.resize(k);
+}
+
+static void seg_copier(SegStore* s) {
+  while (true) {
+    const std::vector<SegItem>* job;
+    {
+      std::unique_lock<std::mutex> lk(s->cmu);
+      s->ccv.wait(lk, [&] { return s->cstop || s->cjob != nullptr; });
+      if (!s->cjob) return;
+      job = s->cjob;
+    }
+    std::vector<std::pair<uint8_t*, int64_t>> out;
+    out.reserve(job->size());
+    for (const SegItem& it : *job) out.push_back(trailer_copy(it.ptr, it.len));
+    {
+      std::lock_guard<std::mutex> g(s->cmu);
+      s->cout.swap(out);
+      s->cjob = nullptr;
+      s->cdone = true;
+    }
+    s->ccv.notify_all();
+  }
+}
 
 // Files are numbered in write order ("<rank>-<number>.sweg"): sequences restart with a new engine
 // incarnation, so they cannot name files.
@@ -1290,9 +1365,23 @@ static void seg_retention(SegStore* s) {
     const SegFile f = s->files.front();
     if (unlink(f.path.c_str()) != 0) break;
     s->files.erase(s->files.begin());
-    s->index.erase(std::remove_if(s->index.begin(), s->index.end(),
-                                  [&](const SwSegIndexEnt& e) { return e.file == f.id; }),
-                   s->index.end());
+    size_t k = 0;
+    for (size_t i = 0; i < s->index.size(); ++i) {
+      if (s->index[i].file == f.id) {
+        if (s->tr_ptr[i]) {
+          s->grave.push_back({seg_now_ms(), s->tr_ptr[i]});
+          s->trailer_bytes -= s->tr_len[i];
+        }
+        continue;
+      }
+      s->index[k] = s->index[i];
+      s->tr_ptr[k] = s->tr_ptr[i];
+      s->tr_len[k] = s->tr_len[i];
+      ++k;
+    }
+    s->index.resize(k);
+    s->tr_ptr.resize(k);
+    s->tr_len.resize(k);
     s->total_bytes -= f.bytes;
     s->deleted_files += 1;
     s->deleted_bytes += f.bytes;
@@ -1315,6 +1404,7 @@ static bool seg_write_all(int fd, const uint8_t* p, int64_t n) {
 static void seg_writer(SegStore* s) {
   std::vector<SegItem> batch;
   std::vector<std::pair<uint64_t, int64_t>> done_src;
+  std::vector<SwSegIndexEnt> pend;       // the batch's blocks, indexed once durable
   while (true) {
     {
       std::unique_lock<std::mutex> lk(s->mu);
@@ -1325,6 +1415,14 @@ static void seg_writer(SegStore* s) {
     }
     int64_t last = -1;
     done_src.clear();
+    {
+      // the copier takes the batch's trailers while the blocks go to the disk
+      std::lock_guard<std::mutex> g(s->cmu);
+      s->cjob = &batch;
+      s->cdone = false;
+    }
+    s->ccv.notify_all();
+    pend.clear();
     for (const SegItem& it : batch) {
       SwSegBlockHdr h;
       memcpy(&h, it.ptr, sizeof(h));
@@ -1387,9 +1485,9 @@ static void seg_writer(SegStore* s) {
         s->error = errno ? errno : -1;
         break;
       }
+      pend.push_back(index_entry(h, it.ptr, s->files.back().id, s->cur_bytes));
       {
         std::lock_guard<std::mutex> g(s->mu);
-        s->index.push_back(index_entry(h, it.ptr, s->files.back().id, s->cur_bytes));
         s->files.back().bytes += padded + extra;
         s->total_bytes += padded + extra;
       }
@@ -1398,16 +1496,32 @@ static void seg_writer(SegStore* s) {
       s->blocks_written += 1;
       last = it.token;
     }
+    const bool synced = !s->error && !(s->fd >= 0 && fdatasync(s->fd) != 0);
+    if (!s->error && !synced) s->error = errno ? errno : -1;
+    std::vector<std::pair<uint8_t*, int64_t>> copies;
+    {
+      std::unique_lock<std::mutex> lk(s->cmu);
+      s->ccv.wait(lk, [&] { return s->cdone; });
+      copies.swap(s->cout);
+    }
     if (s->error) {
+      for (auto& c : copies) free(c.first);
       s->cv_done.notify_all();
       continue;                         // tokens stop advancing; the caller sees the error
     }
-    if (s->fd >= 0 && fdatasync(s->fd) != 0) {
-      s->error = errno ? errno : -1;
-      s->cv_done.notify_all();
-      continue;
-    }
     s->syncs += 1;
+    {
+      std::lock_guard<std::mutex> g(s->mu);
+      for (size_t i = 0; i < pend.size(); ++i) {
+        s->index.push_back(pend[i]);
+        const auto c = i < copies.size() ? copies[i] : std::pair<uint8_t*, int64_t>{nullptr, 0};
+        s->tr_ptr.push_back(c.first);
+        s->tr_len.push_back(c.second);
+        s->trailer_bytes += c.second;
+      }
+      for (size_t i = pend.size(); i < copies.size(); ++i) free(copies[i].first);
+      trailer_trim(s);
+    }
     if (last >= 0) {
       std::lock_guard<std::mutex> g(s->mu);
       for (const auto& kv : done_src) {
@@ -1495,7 +1609,14 @@ void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t ret
     f.id = s->next_file_id;
     f.bytes = seg_scan_file(
         f.path, true,
-        [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) { s->index.push_back(index_entry(hd, b, f.id, off)); },
+        [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) {
+          s->index.push_back(index_entry(hd, b, f.id, off));
+          const auto c = trailer_copy(b, (int64_t)hd.bytes);
+          s->tr_ptr.push_back(c.first);
+          s->tr_len.push_back(c.second);
+          s->trailer_bytes += c.second;
+          trailer_trim(s);
+        },
         [&](const uint8_t* rec) {
           SwSegCommitHdr c;
           memcpy(&c, rec, sizeof(c));
@@ -1513,6 +1634,7 @@ void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t ret
     s->files.push_back(f);
     s->total_bytes += f.bytes;
   }
+  s->copier = std::thread(seg_copier, s);
   s->th = std::thread(seg_writer, s);
   return s;
 }
@@ -1604,7 +1726,15 @@ void swss_close(void* h) {
   }
   s->cv.notify_all();
   if (s->th.joinable()) s->th.join();
+  {
+    std::lock_guard<std::mutex> g(s->cmu);
+    s->cstop = true;
+  }
+  s->ccv.notify_all();
+  if (s->copier.joinable()) s->copier.join();
   seg_close_file(s);
+  for (uint8_t* p : s->tr_ptr) free(p);
+  for (auto& g : s->grave) free(g.second);
   free(s->bounce);
   free(s->commit_buf);
   delete s;
@@ -1618,6 +1748,32 @@ int64_t swss_index(void* h, SwSegIndexEnt* out, int64_t cap) {
   const int64_t n = (int64_t)s->index.size();
   for (int64_t i = 0; i < n && i < cap; ++i) out[i] = s->index[(size_t)i];
   return n;
+}
+
+// swss_index plus, per entry, the address and length of the in-memory copy of the block's index
+// trailer (0 when not held).  An address stays valid until the entry leaves the index (retention)
+// or the copy is dropped (trailer cap) -- and for 120 s after that.
+int64_t swss_index_tr(void* h, SwSegIndexEnt* out, uint64_t* taddr, int64_t* tlen, int64_t cap) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  const int64_t n = (int64_t)s->index.size();
+  for (int64_t i = 0; i < n && i < cap; ++i) {
+    out[i] = s->index[(size_t)i];
+    taddr[i] = (uint64_t)(uintptr_t)s->tr_ptr[(size_t)i];
+    tlen[i] = s->tr_len[(size_t)i];
+  }
+  return n;
+}
+
+// Bytes of trailer copies to hold in memory (older ones dropped beyond it); returns the bytes held.
+int64_t swss_trailer_cap(void* h, int64_t cap) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  if (cap >= 0) {
+    s->trailer_cap = cap;
+    trailer_trim(s);
+  }
+  return s->trailer_bytes;
 }
 
 // Path of segment file `id` (SwSegIndexEnt::file) into buf; returns its length, -1 if deleted.

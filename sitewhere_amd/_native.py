@@ -218,6 +218,10 @@ def native():
         _proto(lib, "swss_stats", None, P, P)
         _proto(lib, "swss_close", None, P)
         _proto(lib, "swss_index", c_int64, P, P, c_int64)
+        _proto(lib, "swss_index_tr", c_int64, P, P, P, P, c_int64)
+        _proto(lib, "swseg_ix_page_geom", c_int64, P, c_int64, P, P, c_int64, P, P)
+        _proto(lib, "swseg_ix_ctx_heads", c_int64, P, c_int64, c_int32, ctypes.c_uint32, P, P, P, P, c_int64)
+        _proto(lib, "swss_trailer_cap", c_int64, P, c_int64)
         _proto(lib, "swss_file", c_int32, P, c_int32, c_char_p, c_int32)
         _proto(lib, "sw_route_rejects", c_int64, P, P, c_int64, P, P, c_int64, c_char_p, P, P, c_int64, P,
                c_int64, P, c_int64, P, P)

@@ -468,6 +468,21 @@ class SegmentStore:
                 return out[:n]
             cap = n + 1024
 
+    def index_tr(self):
+        """(index entries, trailer copy addresses, trailer lengths): see swss_index_tr."""
+        cap = 1024
+        while True:
+            out = np.zeros(cap, INDEX_ENT)
+            ta, tl = np.zeros(cap, np.uint64), np.zeros(cap, np.int64)
+            n = int(self.lib.swss_index_tr(self.h, _p(out), _p(ta), _p(tl), cap))
+            if n <= cap:
+                return out[:n], ta[:n], tl[:n]
+            cap = n + 1024
+
+    def trailer_cap(self, nbytes: int = -1) -> int:
+        """Set the bytes of index trailers held in memory (-1: leave); returns the bytes held."""
+        return int(self.lib.swss_trailer_cap(self.h, int(nbytes)))
+
     def file_path(self, file_id: int) -> str | None:
         buf = ctypes.create_string_buffer(4096)
         n = self.lib.swss_file(self.h, int(file_id), buf, 4096)
@@ -947,12 +962,23 @@ class DurableEventStore(DeviceEventStore):
                 self._tmaps.popitem(last=False)
         return res
 
+    @staticmethod
+    def _trailer_mem(addr: int, nbytes: int, ent):
+        """(address, bytes, header, view) of a trailer copy the segment store holds in memory."""
+        view = np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(int(addr)))
+        th = view[:128].view(IX_HDR)[0]
+        if int(th["magic"]) != IX_MAGIC or int(th["bytes"]) != int(nbytes) or int(th["n_rows"]) != int(ent["n_rows"]):
+            raise ValueError("block index trailer does not match its block")
+        return (int(addr), int(nbytes), th, view)
+
     def _boot_tables(self) -> dict:
         """Per boot: the blocks (store order) and their trailer addresses (0: none) for the native
-        multi-block reads; rebuilt when the set of blocks changes (appends, retention)."""
-        ents = self.seg.index()
+        multi-block reads.  Trailers come from the segment store's in-memory copies (made while
+        each block was written), else memory-mapped from the files.  Kept across appends: only
+        new blocks (and blocks whose copy changed) are resolved."""
+        ents, taddr, tlen = self.seg.index_tr()
         ver = (len(ents), int(ents["first_seq"][-1]) if len(ents) else 0, int(ents["first_seq"][0]) if len(ents) else 0,
-               self.seg.last_token)
+               int(taddr.sum()) if len(ents) else 0)
         tabs = self._tabs
         if tabs is not None and tabs[0] == ver:
             return tabs[1]
@@ -960,25 +986,33 @@ class DurableEventStore(DeviceEventStore):
         P = ctypes.c_void_p
         prev = tabs[1] if tabs is not None else {}
         boots = ents["boot"].astype(np.int64)
+        removed = False
         for b in dict.fromkeys(boots.tolist()):
-            lst = ents[boots == b]
+            m = boots == b
+            lst, ta, tl = ents[m], taddr[m], tlen[m]
             old = prev.get(b)
             k = 0
             if old is not None and old["n"] <= len(lst):
-                # appends (the common case while ingesting): keep the blocks already mapped
+                # appends (the common case while ingesting): keep the blocks already resolved
                 k = old["n"]
                 if k and not (np.array_equal(old["ents"]["first_seq"], lst["first_seq"][:k])
                               and np.array_equal(old["ents"]["rank"], lst["rank"][:k])):
                     k = 0
-            trs = (old["tr"][:k] if k else []) + [self._trailer(e) for e in lst[k:]]
+            removed |= old is not None and k < old["n"]
+            trs = list(old["tr"][:k]) if k else []
+            for i in np.nonzero(ta[:k] != old["taddr"][:k])[0].tolist() if k else []:
+                trs[i] = self._trailer_mem(ta[i], tl[i], lst[i]) if ta[i] else self._trailer(lst[i])
+            trs += [self._trailer_mem(ta[i], tl[i], lst[i]) if ta[i] else self._trailer(lst[i])
+                    for i in range(k, len(lst))]
             addrs = [t[0] if t is not None else 0 for t in trs]
-            res[b] = {"ents": lst, "tr": trs, "n": len(lst), "addr": (P * len(lst))(*addrs),
+            res[b] = {"ents": lst, "tr": trs, "n": len(lst), "addr": (P * len(lst))(*addrs), "taddr": ta,
                       "first": lst["first_seq"].astype(np.int64), "world": lst["world"].astype(np.int64),
                       "rank": lst["rank"].astype(np.int64)}
-        live = {self._key(e) for e in ents}
-        with self._lock:
-            for k in [k for k in self._tmaps if k not in live]:      # retention removed the block
-                self._tmaps.pop(k, None)
+        if removed or len(prev) > len(res):
+            live = {self._key(e) for e in ents}
+            with self._lock:
+                for k in [k for k in self._tmaps if k not in live]:      # retention removed the block
+                    self._tmaps.pop(k, None)
         self._tabs = (ver, res)
         return res
 
@@ -1300,13 +1334,17 @@ class DurableEventStore(DeviceEventStore):
     def _page_geometry(self, t, bis: np.ndarray, pages: np.ndarray):
         """(file id, file offset, bytes, rows) of pages ``pages`` of blocks ``bis`` (positions in t)."""
         n = len(bis)
-        pos, nb = np.empty(n, np.int64), np.empty(n, np.uint32)
         ents = t["ents"]
-        for bi in np.unique(bis).tolist():
-            m = bis == bi
-            pg = self._pages_of(ents[bi], t["tr"][bi])
-            pos[m] = int(ents[bi]["offset"]) + pg["off"][pages[m]].astype(np.int64)
-            nb[m] = pg["bytes"][pages[m]]
+        bis, pages = np.ascontiguousarray(bis, np.int64), np.ascontiguousarray(pages, np.int64)
+        off, nb = np.empty(n, np.uint32), np.empty(n, np.uint32)
+        miss = int(native().swseg_ix_page_geom(t["addr"], t["n"], _p(bis), _p(pages), n, _p(off), _p(nb)))
+        if miss:                                      # blocks without a trailer: their page headers
+            for bi in np.unique(bis[nb == 0]).tolist():
+                m = bis == bi
+                pg = self._pages_of(ents[bi], t["tr"][bi])
+                off[m] = pg["off"][pages[m]]
+                nb[m] = pg["bytes"][pages[m]]
+        pos = ents["offset"][bis].astype(np.int64) + off.astype(np.int64)
         n_rows = ents["n_rows"][bis].astype(np.int64)
         rows = np.minimum(PAGE_ROWS, n_rows - pages * PAGE_ROWS).astype(np.uint32)
         return ents["file"][bis].astype(np.int64), pos, nb, rows
@@ -1513,23 +1551,28 @@ class DurableEventStore(DeviceEventStore):
             if cid is None:
                 continue
             out = np.zeros(7 * n, np.int64)
-            lib.swseg_ix_ctx_find(t["addr"], n, d, (int(cid) << 3) | int(et), _p(out))
+            cap = 16 * n + 16
+            while True:
+                hb, hr, hd = np.empty(cap, np.int64), np.empty(cap, np.int64), np.empty(cap, np.int64)
+                k = int(lib.swseg_ix_ctx_heads(t["addr"], n, d, (int(cid) << 3) | int(et), _p(out), _p(hb), _p(hr),
+                                               _p(hd), cap))
+                if k <= cap:
+                    break
+                cap = k
             o = out.reshape(n, 7)
-            for bi in np.nonzero(o[:, 0] != 0)[0].tolist():
-                st, cnt, dmin, dmax, ha, nh, da = (int(x) for x in o[bi])
-                if st < 0 or (bounded and not (dmax < d_lo or dmin > d_hi) and not (d_lo <= dmin and dmax <= d_hi)):
-                    scan.setdefault(bi, set()).add(int(cid))       # not indexed here / straddles a bound
-                    continue
-                if dmax < d_lo or dmin > d_hi:
-                    continue
-                total += cnt
-                hr = np.ctypeslib.as_array((ctypes.c_uint32 * nh).from_address(ha)).astype(np.int64) if nh else \
-                    np.zeros(0, np.int64)
-                hd = np.ctypeslib.as_array((ctypes.c_int64 * nh).from_address(da)).copy() if nh else \
-                    np.zeros(0, np.int64)
-                heads.append((np.full(nh, bi, np.int64), hr, hd))
-                if cnt > nh:
-                    maybe.append((bi, int(hd[-1]), int(hr[-1]), int(cid)))
+            st, cnt, dmin, dmax, h0, nh = o[:, 0], o[:, 1], o[:, 2], o[:, 3], o[:, 4], o[:, 5]
+            outside = (dmax < d_lo) | (dmin > d_hi)
+            straddle = bounded & ~outside & ~((d_lo <= dmin) & (dmax <= d_hi))
+            to_scan = (st < 0) | ((st > 0) & straddle)     # not indexed here / straddles a bound
+            for bi in np.nonzero(to_scan)[0].tolist():
+                scan.setdefault(bi, set()).add(int(cid))
+            use = (st > 0) & ~to_scan & ~outside
+            total += int(cnt[use].sum())
+            keep = use[hb[:k]]
+            heads.append((hb[:k][keep], hr[:k][keep], hd[:k][keep]))
+            for bi in np.nonzero(use & (cnt > nh))[0].tolist():
+                j = int(h0[bi] + nh[bi] - 1)
+                maybe.append((bi, int(hd[j]), int(hr[j]), int(cid)))
         # blocks to scan in full (exact rows): not indexed, straddling a date bound, or heads exhausted
         def scan_blocks(blks):
             got = []

@@ -538,3 +538,35 @@ def test_point_fetch_equals_page_decode(tmp_path):
         assert sg.row_strings(got, i) == sg.row_strings(d, k)
         assert es._materialize(got, i).id == f"c0-{blocks[b][1] + r}"
     es.close()
+
+
+def test_trailer_copies_in_memory_and_cap(tmp_path):
+    """The segment store holds each block's index trailer in memory (copied while the block is
+    written, and on recovery); beyond the cap the oldest copies are dropped and the reads fall back
+    to mapping the trailers from the files -- same answers either way."""
+    es, _, blocks, exp_all = _ctx_store_blocks(tmp_path, n_blocks=4, rows_per=2000)
+    ents, ta, tl = es.seg.index_tr()
+    assert len(ents) == 4 and (ta != 0).all() and (tl > 0).all()
+    for (blk, _), n in zip(blocks, tl.tolist()):
+        assert n == len(blk) - sg.trailer_offset(blk)
+    held = es.seg.trailer_cap()
+    assert held == int(tl.sum())
+    from sitewhere_amd.models.domain import DateRangeSearchCriteria
+    crit = DateRangeSearchCriteria(page_size=50)
+    want = es.list_events("Measurement", "Area", ["area-1"], crit)
+    alt = next(a for _, a in exp_all[::-1] if a is not None)
+    want_alt = es.get_event_by_alternate_id(alt).id
+    es.seg.trailer_cap(int(tl[-1]))                     # keep the newest copy only
+    ents2, ta2, _ = es.seg.index_tr()
+    assert (ta2[:-1] == 0).all() and ta2[-1] != 0
+    got = es.list_events("Measurement", "Area", ["area-1"], crit)
+    assert (got.num_results, [e.id for e in got.results]) == (want.num_results, [e.id for e in want.results])
+    assert es.get_event_by_alternate_id(alt).id == want_alt
+    d = es.dir
+    es.close()
+    es2 = sg.DurableEventStore(d, direct=False)           # recovery copies the trailers again
+    _, ta3, _ = es2.seg.index_tr()
+    assert (ta3 != 0).all()
+    got = es2.list_events("Measurement", "Area", ["area-1"], crit)
+    assert [e.id for e in got.results] == [e.id for e in want.results]
+    es2.close()
