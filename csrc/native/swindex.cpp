@@ -479,14 +479,25 @@ int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint3
     std::vector<uint8_t> buf;
     const int64_t b0 = n_tasks * w / T, b1 = n_tasks * (w + 1) / T;
     for (int64_t i = b0; i < b1; ++i) {
+      // one read of the page's first bytes usually holds the header and the leading columns
+      // (etype, level, date, assignment); a second read fetches the rest when it does not
+      const uint64_t first = std::min<uint64_t>(pg_bytes[i], 12288);
+      if (first < sizeof(SwSegPageHdr)) { bad = i; return; }
+      buf.resize(std::max<uint64_t>(first, sizeof(SwSegPageHdr)) + 8);
+      if (pread(fds[i], buf.data(), first, blk_off[i] + pg_off[i]) != (ssize_t)first) { bad = i; return; }
       SwSegPageHdr ph;
-      if (pread(fds[i], &ph, sizeof(ph), blk_off[i] + pg_off[i]) != (ssize_t)sizeof(ph)) { bad = i; return; }
+      memcpy(&ph, buf.data(), sizeof(ph));
       const SwSegCol& ca = ph.cols[SEG_ASG];
       const uint64_t need = (uint64_t)ca.data_off + seg_col_bytes(ca.count, ca.bits, 0);
       if (need > pg_bytes[i] || ph.n_rows > SEG_PAGE_ROWS || ph.cols[SEG_ETYPE].count != ph.n_rows ||
           ph.cols[SEG_DATE].count != ph.n_rows || ca.count != ph.n_rows) { bad = i; return; }
-      buf.resize(need + 8);
-      if (pread(fds[i], buf.data(), need, blk_off[i] + pg_off[i]) != (ssize_t)need) { bad = i; return; }
+      if (need > first) {
+        buf.resize(need + 8);
+        if (pread(fds[i], buf.data() + first, need - first, blk_off[i] + pg_off[i] + first) != (ssize_t)(need - first)) {
+          bad = i;
+          return;
+        }
+      }
       const SwSegCol& ce = ph.cols[SEG_ETYPE];
       const SwSegCol& cd = ph.cols[SEG_DATE];
       const int32_t row0 = pg_index[i] * SEG_PAGE_ROWS;
