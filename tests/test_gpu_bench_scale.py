@@ -1,9 +1,12 @@
-"""Bench-scale parity: the MI355X engine against the native CPU engine (bit-exact with
-the Python oracle) at the benchmark's shape -- 1M-payload steps over a 1M-device fleet with alternate
-ids, metadata and control messages, a 2^22-slot dedup window that rotates several times, an HBM event
-ring that wraps every two steps, and replays inside and beyond the window.  Every step: same stats,
-same persisted rows (device events in order, generated rows as a multiset), same reject statuses and
-the same durable block contents."""
+"""Bench-scale parity: the MI355X engine against the native CPU engine (bit-exact
+with the Python oracle) in the configuration bench.py runs -- 1M-payload steps over a 1M-device fleet
+with alternate ids, metadata and control messages, a 2^22-slot dedup window that rotates several
+times, the store-backed alternate-id filter at bench.py's 2^33 bits, an HBM event ring that wraps
+every two steps, and replays inside and beyond the window.  Every step: same stats, same persisted
+rows (device events in order, generated rows as a multiset), same reject statuses, the same durable
+block contents and the same block index trailer (built on the GPU in the step vs by the C++
+builder on the CPU engine's block).  The replay beyond the window comes back as rechecks (the
+filter remembers the ids), not as accepted events."""
 from __future__ import annotations
 
 import numpy as np
@@ -21,7 +24,7 @@ def _cfg():
     from sitewhere_amd.pipeline.config import EngineConfig
     return EngineConfig(max_msgs=N_MSGS, rec_cap=N_MSGS + 4096, gen_cap=N_MSGS // 2, max_devices=N_DEV + 1024,
                         max_assignments=N_DEV + 1024, store_cap=1 << 21, dedup_slots=1 << 22, name_slots=1 << 12,
-                        state_slots=1 << 23, presence_missing_ms=8 * 3600 * 1000)
+                        state_slots=1 << 23, presence_missing_ms=8 * 3600 * 1000, dedup_bloom_bits=1 << 33)
 
 
 def _setup(engine):
@@ -76,10 +79,10 @@ def test_gpu_matches_native_cpu_engine_at_bench_scale():
                      p_register=0.0005, p_ack=0.0005, p_meta=0.1)
     now = 1_700_000_100_000
     # 1..6 fresh; 5 again (inside the window: all duplicates); 7..9 fresh (the window rotates: 2^22
-    # slots hold 2M-4M ids); 1 again (beyond the window: accepted again, as documented)
+    # slots hold 2M-4M ids); 1 again (beyond the window: the filter sends every id to a recheck)
     seeds = [1, 2, 3, 4, 5, 6, 5, 7, 8, 9, 1]
     batches = {}
-    dups = []
+    dups, rechecks = [], []
     for k, seed in enumerate(seeds):
         if seed not in batches:
             raw, offs = gen_payloads(spec, N_MSGS, now - 60_000, seed=seed)
@@ -90,14 +93,18 @@ def test_gpu_matches_native_cpu_engine_at_bench_scale():
         rc = c.step(raw, offs, now + k, presence=(k % 4 == 3))
         assert g.stats_dict() == c.stats_dict(), f"step {k}"
         dups.append(g.stats_dict()["duplicates"] - s0["duplicates"])
+        rechecks.append(g.stats_dict()["dedup_rechecks"] - s0["dedup_rechecks"])
         assert rg.n_persisted == rc.n_persisted
         assert rg.n_persisted > 0 or k == 6                  # the replay inside the window: all duplicates
         s1 = g.stats_dict()
         gen = (s1["rule_alerts"] - s0["rule_alerts"]) + (s1["presence_events"] - s0["presence_events"])
         _rows_equal(rg, rc, _name_map(g), _name_map(c), rg.n_persisted - gen)
         assert sorted(rg.reject_status.tolist()) == sorted(rc.reject_status.tolist())
-        bg = sg.decode_block(g.encode_block(now + k, rg, boot=0xabc))
-        bc = sg.decode_block(c.encode_block(now + k, rc, boot=0xabc))
+        blk_g = g.encode_block(now + k, rg, boot=0xabc)
+        blk_c = c.encode_block(now + k, rc, boot=0xabc)
+        tg, tc = sg.trailer_offset(blk_g), sg.trailer_offset(blk_c)
+        assert tg > 0 and tc > 0 and np.array_equal(blk_g[tg:], blk_c[tc:]), k       # index trailers
+        bg, bc = sg.decode_block(blk_g), sg.decode_block(blk_c)
         for col in ("etype", "level", "date", "asg", "v0", "v1", "v2", "flags", "str_off"):
             assert np.array_equal(bg[col], bc[col]), (k, col)
         if bc["str_off"] is not None:
@@ -106,4 +113,7 @@ def test_gpu_matches_native_cpu_engine_at_bench_scale():
     st = g.stats_dict()
     assert st["dedup_rotations"] >= 2 and st["dedup_overflow"] == 0 and st["state_overflow"] == 0
     assert dups[6] > 0.99 * N_MSGS * (1 - spec.p_unregistered - 0.001)       # replay inside the window
-    assert dups[10] == 0                                                     # replay beyond it
+    # replay beyond it: not accepted -- every id the filter has seen goes to the store recheck
+    assert dups[10] == 0
+    assert rechecks[10] > 0.99 * N_MSGS * (1 - spec.p_unregistered - 0.001)
+    assert sum(rechecks[:6]) + sum(rechecks[7:10]) < 1000                    # the filter's false positives
