@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--p-unregistered", type=float, default=0.005)
     ap.add_argument("--p-register", type=float, default=0.0005)
     ap.add_argument("--p-ack", type=float, default=0.0005)
-    ap.add_argument("--dedup-bloom-bits", type=int, default=1 << 33,
+    ap.add_argument("--dedup-bloom-bits", type=int, default=1 << 36,
                     help="store-backed alternate-id filter size (bits, 0 = off)")
     ap.add_argument("--p-meta", type=float, default=0.1,
                     help="share of events carrying metadata entries (stored with the event, like the reference)")
@@ -219,8 +219,10 @@ def main():
                        max_assignments=int(n_total_dev * 1.1) + 1024, store_cap=args.store,
                        # alternate-id window: 2^24 slots = the last ~8M distinct ids per GPU
                        dedup_slots=1 << 24, name_slots=1 << 12, rank=rank, world=world,
-                       # store-backed dedup beyond the window (2^33 bits = 1 GB of HBM: ~32 bits for each
-                       # of the ~270M ids a 500-step run stores; rechecks are counted in the stats)
+                       # store-backed dedup beyond the window: 2^36 bits = 8 GB of the 288 GB of HBM, sized
+                       # for the ids the retained store holds (48 GB of blocks ~ 2.6B ids: ~2.6 ids per
+                       # 64-bit filter word, false rechecks ~4e-5).  2^33 saturates past ~1B ids: a 1500-step
+                       # run then sends ~4% of its events to the host recheck path.  Rechecks are counted.
                        dedup_bloom_bits=args.dedup_bloom_bits,
                        # (assignment, name) state map: 16 measurement names + 4 alert types + zone alerts per device
                        state_slots=2 * (16 + 4 + args.zones) * int(args.devices * 1.1),
