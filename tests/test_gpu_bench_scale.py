@@ -95,7 +95,8 @@ def test_gpu_matches_native_cpu_engine_at_bench_scale():
         dups.append(g.stats_dict()["duplicates"] - s0["duplicates"])
         rechecks.append(g.stats_dict()["dedup_rechecks"] - s0["dedup_rechecks"])
         assert rg.n_persisted == rc.n_persisted
-        assert rg.n_persisted > 0 or k == 6                  # the replay inside the window: all duplicates
+        # the replays: inside the window all duplicates, beyond it all rechecks
+        assert rg.n_persisted > 0 or k in (6, 10)
         s1 = g.stats_dict()
         gen = (s1["rule_alerts"] - s0["rule_alerts"]) + (s1["presence_events"] - s0["presence_events"])
         _rows_equal(rg, rc, _name_map(g), _name_map(c), rg.n_persisted - gen)
