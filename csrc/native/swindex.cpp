@@ -467,7 +467,7 @@ extern "C" {
 int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint32_t* pg_off, const uint32_t* pg_bytes,
                          const int32_t* pg_index, int64_t n_tasks, int32_t et, int32_t asg, const int32_t* ctx_tab,
                          int64_t n_ctx, int32_t ctx_id, int64_t d_lo, int64_t d_hi, int32_t threads,
-                         int64_t* out_task, int32_t* out_row, int64_t* out_date, int64_t cap) {
+                         int64_t* out_task, int32_t* out_row, int64_t* out_date, int64_t cap, const uint64_t* mem) {
   if (n_tasks <= 0) return 0;
   int T = threads > 0 ? threads : 1;
   if (T > 64) T = 64;
@@ -479,37 +479,47 @@ int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint3
     std::vector<uint8_t> buf;
     const int64_t b0 = n_tasks * w / T, b1 = n_tasks * (w + 1) / T;
     for (int64_t i = b0; i < b1; ++i) {
-      // one read of the page's first bytes usually holds the header and the leading columns
-      // (etype, level, date, assignment); a second read fetches the rest when it does not
-      const uint64_t first = std::min<uint64_t>(pg_bytes[i], 12288);
-      if (first < sizeof(SwSegPageHdr)) { bad = i; return; }
-      buf.resize(std::max<uint64_t>(first, sizeof(SwSegPageHdr)) + 8);
-      if (pread(fds[i], buf.data(), first, blk_off[i] + pg_off[i]) != (ssize_t)first) { bad = i; return; }
+      // a page held in memory is read in place; from the file, one read of the page's first bytes
+      // usually holds the header and the leading columns (etype, level, date, assignment), and a
+      // second read fetches the rest when it does not
+      const uint8_t* pg;
+      uint64_t first = 0;
+      if (mem && mem[i]) {
+        if (pg_bytes[i] < sizeof(SwSegPageHdr)) { bad = i; return; }
+        pg = reinterpret_cast<const uint8_t*>((uintptr_t)mem[i]);
+      } else {
+        first = std::min<uint64_t>(pg_bytes[i], 12288);
+        if (first < sizeof(SwSegPageHdr)) { bad = i; return; }
+        buf.resize(first + 8);
+        if (pread(fds[i], buf.data(), first, blk_off[i] + pg_off[i]) != (ssize_t)first) { bad = i; return; }
+        pg = buf.data();
+      }
       SwSegPageHdr ph;
-      memcpy(&ph, buf.data(), sizeof(ph));
+      memcpy(&ph, pg, sizeof(ph));
       const SwSegCol& ca = ph.cols[SEG_ASG];
       const uint64_t need = (uint64_t)ca.data_off + seg_col_bytes(ca.count, ca.bits, 0);
       if (need > pg_bytes[i] || ph.n_rows > SEG_PAGE_ROWS || ph.cols[SEG_ETYPE].count != ph.n_rows ||
           ph.cols[SEG_DATE].count != ph.n_rows || ca.count != ph.n_rows) { bad = i; return; }
-      if (need > first) {
+      if (!(mem && mem[i]) && need > first) {
         buf.resize(need + 8);
         if (pread(fds[i], buf.data() + first, need - first, blk_off[i] + pg_off[i] + first) != (ssize_t)(need - first)) {
           bad = i;
           return;
         }
+        pg = buf.data();
       }
       const SwSegCol& ce = ph.cols[SEG_ETYPE];
       const SwSegCol& cd = ph.cols[SEG_DATE];
       const int32_t row0 = pg_index[i] * SEG_PAGE_ROWS;
       for (uint32_t r = 0; r < ph.n_rows; ++r) {
-        if (et >= 0 && (int32_t)seg_unord(ce.base + ix_unpack(buf.data() + ce.data_off, r, ce.bits)) != et) continue;
-        const int32_t a = (int32_t)seg_unord(ca.base + ix_unpack(buf.data() + ca.data_off, r, ca.bits));
+        if (et >= 0 && (int32_t)seg_unord(ce.base + ix_unpack(pg + ce.data_off, r, ce.bits)) != et) continue;
+        const int32_t a = (int32_t)seg_unord(ca.base + ix_unpack(pg + ca.data_off, r, ca.bits));
         if (asg >= 0) {
           if (a != asg) continue;
         } else if (a < 0 || a >= n_ctx || ctx_tab[a] != ctx_id) {
           continue;
         }
-        const int64_t d = seg_unord(cd.base + ix_unpack(buf.data() + cd.data_off, r, cd.bits));
+        const int64_t d = seg_unord(cd.base + ix_unpack(pg + cd.data_off, r, cd.bits));
         if (d < d_lo || d > d_hi) continue;
         hits[w].push_back({i, row0 + (int32_t)r, d});
       }

@@ -32,6 +32,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -801,7 +802,8 @@ int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, u
 int64_t swseg_fetch_rows(const int32_t* fds, const int64_t* pg_pos, const uint32_t* pg_bytes, const uint32_t* pg_rows,
                          const int32_t* row_in_page, int64_t n, int32_t threads, uint8_t* etype, uint8_t* level,
                          int64_t* date, int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2,
-                         uint8_t* flags, uint8_t* str_heap, int64_t str_cap, int64_t* str_off) {
+                         uint8_t* flags, uint8_t* str_heap, int64_t str_cap, int64_t* str_off,
+                         const uint64_t* mem) {
   if (n <= 0) return 0;
   std::vector<int64_t> first;                       // first request of each distinct page
   for (int64_t i = 0; i < n; ++i)
@@ -835,19 +837,21 @@ int64_t swseg_fetch_rows(const int32_t* fds, const int64_t* pg_pos, const uint32
       const int64_t i = first[q], k = first[q + 1] - first[q];
       const uint32_t len = pg_bytes[i];
       if (len < SEG_PAGE_HDR || len > (64u << 20) || pg_rows[i] > SEG_PAGE_ROWS) { bad = i; return; }
-      buf.resize(len);
-      if (pread(fds[i], buf.data(), len, pg_pos[i]) != (ssize_t)len || verify_page(buf.data(), len, pg_rows[i])) {
-        bad = i;
-        return;
+      const uint8_t* pg = mem && mem[i] ? reinterpret_cast<const uint8_t*>((uintptr_t)mem[i]) : nullptr;
+      if (!pg) {
+        buf.resize(len);
+        if (pread(fds[i], buf.data(), len, pg_pos[i]) != (ssize_t)len) { bad = i; return; }
+        pg = buf.data();
       }
+      if (verify_page(pg, len, pg_rows[i])) { bad = i; return; }
       for (int64_t j = i; j < i + k; ++j)
         if (srow[j] < 0 || (uint32_t)srow[j] >= pg_rows[i]) { bad = perm[j]; return; }
       SwSegPageHdr ph;
-      memcpy(&ph, buf.data(), sizeof(ph));
+      memcpy(&ph, pg, sizeof(ph));
       heaps[(size_t)q].resize((size_t)ph.heap_bytes + (size_t)k * (SEG_ALT_PFX_MAX + 16 + 8) + 8);
       loc.assign(3 * (size_t)k + 1, 0);
       int64_t so = 0;
-      if (decode_rows(buf.data(), srow.data() + i, k, et.data() + i, lv.data() + i, dt.data() + i, as.data() + i,
+      if (decode_rows(pg, srow.data() + i, k, et.data() + i, lv.data() + i, dt.data() + i, as.data() + i,
                       nm.data() + i, a0.data() + i, a1.data() + i, a2.data() + i, fl.data() + i,
                       heaps[(size_t)q].data(), (int64_t)heaps[(size_t)q].size(), &so, loc.data()) != k) {
         bad = i;
@@ -908,7 +912,7 @@ int64_t swseg_fetch_rows(const int32_t* fds, const int64_t* pg_pos, const uint32
 // -(1 + i) when page i cannot be read or fails its check.
 int64_t swseg_alt_page_rows(const int32_t* fds, const int64_t* pg_pos, const uint32_t* pg_bytes,
                             const uint32_t* pg_rows, const uint64_t* hashes, int64_t n, int32_t threads,
-                            int64_t* out_task, int32_t* out_row, int64_t cap) {
+                            int64_t* out_task, int32_t* out_row, int64_t cap, const uint64_t* mem) {
   if (n <= 0) return 0;
   int T = threads > 0 ? threads : 1;
   if (T > 32) T = 32;
@@ -922,17 +926,19 @@ int64_t swseg_alt_page_rows(const int32_t* fds, const int64_t* pg_pos, const uin
     for (int64_t i = n * w / T; i < n * (w + 1) / T; ++i) {
       const uint32_t len = pg_bytes[i];
       if (len < SEG_PAGE_HDR || len > (64u << 20) || pg_rows[i] > SEG_PAGE_ROWS) { bad = i; return; }
-      buf.resize(len);
-      if (pread(fds[i], buf.data(), len, pg_pos[i]) != (ssize_t)len || verify_page(buf.data(), len, pg_rows[i])) {
-        bad = i;
-        return;
+      const uint8_t* pg = mem && mem[i] ? reinterpret_cast<const uint8_t*>((uintptr_t)mem[i]) : nullptr;
+      if (!pg) {
+        buf.resize(len);
+        if (pread(fds[i], buf.data(), len, pg_pos[i]) != (ssize_t)len) { bad = i; return; }
+        pg = buf.data();
       }
+      if (verify_page(pg, len, pg_rows[i])) { bad = i; return; }
       SwSegPageHdr ph;
-      memcpy(&ph, buf.data(), sizeof(ph));
+      memcpy(&ph, pg, sizeof(ph));
       heap.resize((size_t)ph.heap_bytes + (size_t)ph.n_rows * (SEG_ALT_PFX_MAX + 16 + 8) + 8);
       int64_t o = 0;
       so[0] = 0;
-      if (decode_page(buf.data(), 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, fl.data(),
+      if (decode_page(pg, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, fl.data(),
                       heap.data(), (int64_t)heap.size(), &o, so.data(), ws) != (int64_t)ph.n_rows) {
         bad = i;
         return;
@@ -1232,73 +1238,168 @@ struct SegStore {
   int64_t total_bytes = 0;
   uint8_t* commit_buf = nullptr;          // one SEG_COMMIT_BYTES record, aligned for O_DIRECT
   std::map<uint64_t, int64_t> sources;    // durable input offsets (max per key)
-  // In-memory copies of the blocks' index trailers (parallel to `index`; null when not held): the
-  // read path searches them without touching the disk.  Copied while the block is written (by the
-  // copier thread, from the caller's buffer) and on recovery; oldest dropped beyond trailer_cap.
+  // What the store holds in memory for the read path, parallel to `index` (null: not held):
+  //  * a copy of each recent block (bk_*), up to blk_cap bytes, newest kept -- the blocks were
+  //    written with O_DIRECT, so without it every read of a fresh block goes to the device;
+  //  * each block's index trailer (tr_*): inside the block copy while there is one, else its own
+  //    copy, up to trailer_cap bytes of those.
+  // Copies are made while the block is written (copier threads, from the caller's buffer, which
+  // stays valid until the block is durable) and, for trailers, on recovery.  A copy dropped by a cap
+  // or by retention is reclaimed only once every read lease that could have seen it has ended
+  // (swss_lease_begin / swss_lease_end: epochs), then recycled for the next block copy.
   std::vector<uint8_t*> tr_ptr;
   std::vector<int64_t> tr_len;
-  int64_t trailer_cap = 16ll << 30;
-  int64_t trailer_bytes = 0;
-  std::vector<std::pair<int64_t, uint8_t*>> grave;   // dropped copies, freed 120 s later (readers' grace)
+  std::vector<uint8_t> tr_own;                       // 1: the trailer is its own allocation
+  std::vector<uint8_t*> bk_ptr;
+  std::vector<int64_t> bk_cap;                       // allocation bytes of the block copy
+  int64_t trailer_cap = 16ll << 30, trailer_bytes = 0;   // own trailer copies
+  int64_t blk_cap = 0, blk_bytes = 0;                // block copies (0: none kept)
+  int64_t epoch = 0;
+  std::multiset<int64_t> leases;                     // start epochs of the active read leases
+  struct Retired { int64_t epoch; uint8_t* p; int64_t cap; };
+  std::vector<Retired> grave;
+  std::vector<std::pair<uint8_t*, int64_t>> pool;    // reclaimed block buffers (ptr, cap) for reuse
   std::thread copier;
   std::mutex cmu;
   std::condition_variable ccv;
-  const std::vector<SegItem>* cjob = nullptr;        // the batch whose trailers to copy
-  std::vector<std::pair<uint8_t*, int64_t>> cout;    // one per item (null: no trailer)
+  const std::vector<SegItem>* cjob = nullptr;        // the batch to copy
+  struct Copy { uint8_t* blk; int64_t bcap; uint8_t* tr; int64_t tlen; bool own; };
+  std::vector<Copy> cout;                            // one per item
   bool cdone = true;
   bool cstop = false;
 };
 
-static int64_t seg_now_ms() {
-  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
+static int64_t round_up_mb(int64_t x) { return (x + (1ll << 20) - 1) >> 20 << 20; }
 
-// A block's index trailer (null when it has none), copied to a new buffer.
-static std::pair<uint8_t*, int64_t> trailer_copy(const uint8_t* b, int64_t len) {
+// A block's index trailer: (offset in the block, bytes); (0, 0) when it has none.
+static std::pair<int64_t, int64_t> trailer_span(const uint8_t* b, int64_t len) {
   SwSegBlockHdr h;
   memcpy(&h, b, sizeof(h));
-  if (!(h.flags & SEG_FLAG_INDEX) || (int64_t)h.bytes > len) return {nullptr, 0};
+  if (!(h.flags & SEG_FLAG_INDEX) || (int64_t)h.bytes > len) return {0, 0};
   const uint32_t toff = ((const uint32_t*)(b + 64))[h.n_pages];
-  if (toff >= h.bytes) return {nullptr, 0};
-  const int64_t n = (int64_t)h.bytes - toff;
-  uint8_t* c = (uint8_t*)aligned_alloc(64, (size_t)((n + 63) / 64 * 64));
-  if (!c) return {nullptr, 0};
-  memcpy(c, b + toff, (size_t)n);
-  return {c, n};
+  if (toff >= h.bytes) return {0, 0};
+  return {(int64_t)toff, (int64_t)h.bytes - toff};
 }
 
-// Caller holds s->mu: drop the oldest held trailers beyond the cap, and free dropped copies whose
-// grace has passed.
-static void trailer_trim(SegStore* s) {
+static uint8_t* own_copy(const uint8_t* src, int64_t n) {
+  uint8_t* c = (uint8_t*)aligned_alloc(64, (size_t)((n + 63) / 64 * 64));
+  if (c) memcpy(c, src, (size_t)n);
+  return c;
+}
+
+// memcpy of a large block on a few threads (one core's copy rate would pace the writer).
+static void wide_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
+  const int T = n >= (8ll << 20) ? 4 : 1;
+  if (T == 1) {
+    memcpy(dst, src, (size_t)n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int w = 0; w < T; ++w) {
+    const int64_t a = (n * w / T) & ~int64_t(4095), b = w + 1 == T ? n : (n * (w + 1) / T) & ~int64_t(4095);
+    th.emplace_back([=] { memcpy(dst + a, src + a, (size_t)(b - a)); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// Caller holds s->mu.  Retire a copy (reclaimed once no lease can still see it).
+static void retire(SegStore* s, uint8_t* p, int64_t cap) {
+  if (p) s->grave.push_back({s->epoch, p, cap});
+}
+
+// Caller holds s->mu: enforce the caps (oldest copies first), then reclaim retired copies no
+// active lease started before.
+static void mem_trim(SegStore* s) {
+  bool any = false;
+  for (size_t i = 0; i < s->bk_ptr.size() && s->blk_bytes > s->blk_cap; ++i) {
+    if (!s->bk_ptr[i]) continue;
+    if (s->tr_ptr[i] && !s->tr_own[i]) {            // the trailer outlives the block copy
+      uint8_t* t = own_copy(s->tr_ptr[i], s->tr_len[i]);
+      s->tr_ptr[i] = t;
+      s->tr_own[i] = t != nullptr;
+      if (!t) s->tr_len[i] = 0;
+      s->trailer_bytes += t ? s->tr_len[i] : 0;
+    }
+    retire(s, s->bk_ptr[i], s->bk_cap[i]);
+    s->blk_bytes -= s->bk_cap[i];
+    s->bk_ptr[i] = nullptr;
+    s->bk_cap[i] = 0;
+    any = true;
+  }
   for (size_t i = 0; i < s->tr_ptr.size() && s->trailer_bytes > s->trailer_cap; ++i) {
-    if (!s->tr_ptr[i]) continue;
-    s->grave.push_back({seg_now_ms(), s->tr_ptr[i]});
+    if (!s->tr_ptr[i] || !s->tr_own[i]) continue;
+    retire(s, s->tr_ptr[i], 0);
     s->trailer_bytes -= s->tr_len[i];
     s->tr_ptr[i] = nullptr;
     s->tr_len[i] = 0;
+    s->tr_own[i] = 0;
+    any = true;
   }
-  const int64_t now = seg_now_ms();
+  if (any) ++s->epoch;
+  const int64_t oldest = s->leases.empty() ? INT64_MAX : *s->leases.begin();
   size_t k = 0;
   for (auto& g : s->grave) {
-    if (now - g.first > 120000) free(g.second);
-    else s->grave[k++] = g;
+    if (g.epoch < oldest) {
+      if (g.cap > 0 && s->pool.size() < 8) s->pool.push_back({g.p, g.cap});
+      else free(g.p);
+    } else {
+      s->grave[k++] = g;
+    }
   }
   s->grave.resize(k);
 }
 
+// Copier: this batch's block copies (when blocks are kept) or trailer copies.
 static void seg_copier(SegStore* s) {
   while (true) {
     const std::vector<SegItem>* job;
+    int64_t keep;
     {
       std::unique_lock<std::mutex> lk(s->cmu);
       s->ccv.wait(lk, [&] { return s->cstop || s->cjob != nullptr; });
       if (!s->cjob) return;
       job = s->cjob;
     }
-    std::vector<std::pair<uint8_t*, int64_t>> out;
+    {
+      std::lock_guard<std::mutex> g(s->mu);
+      keep = s->blk_cap;
+    }
+    std::vector<SegStore::Copy> out;
     out.reserve(job->size());
-    for (const SegItem& it : *job) out.push_back(trailer_copy(it.ptr, it.len));
+    for (const SegItem& it : *job) {
+      const auto ts = trailer_span(it.ptr, it.len);
+      SegStore::Copy c{nullptr, 0, nullptr, 0, false};
+      if (keep > 0 && it.len <= keep) {
+        uint8_t* p = nullptr;
+        int64_t cap = 0;
+        {
+          std::lock_guard<std::mutex> g(s->mu);
+          for (size_t k = 0; k < s->pool.size(); ++k)
+            if (s->pool[k].second >= it.len) {
+              p = s->pool[k].first;
+              cap = s->pool[k].second;
+              s->pool.erase(s->pool.begin() + (long)k);
+              break;
+            }
+        }
+        if (!p) {
+          cap = round_up_mb(it.len);
+          p = (uint8_t*)aligned_alloc(4096, (size_t)cap);
+        }
+        if (p) {
+          wide_copy(p, it.ptr, it.len);
+          c.blk = p;
+          c.bcap = cap;
+          if (ts.second) { c.tr = p + ts.first; c.tlen = ts.second; }
+        }
+      }
+      if (!c.blk && ts.second) {
+        c.tr = own_copy(it.ptr + ts.first, ts.second);
+        c.tlen = c.tr ? ts.second : 0;
+        c.own = c.tr != nullptr;
+      }
+      out.push_back(c);
+    }
     {
       std::lock_guard<std::mutex> g(s->cmu);
       s->cout.swap(out);
@@ -1368,20 +1469,31 @@ static void seg_retention(SegStore* s) {
     size_t k = 0;
     for (size_t i = 0; i < s->index.size(); ++i) {
       if (s->index[i].file == f.id) {
-        if (s->tr_ptr[i]) {
-          s->grave.push_back({seg_now_ms(), s->tr_ptr[i]});
+        if (s->tr_ptr[i] && s->tr_own[i]) {
+          retire(s, s->tr_ptr[i], 0);
           s->trailer_bytes -= s->tr_len[i];
+        }
+        if (s->bk_ptr[i]) {
+          retire(s, s->bk_ptr[i], s->bk_cap[i]);
+          s->blk_bytes -= s->bk_cap[i];
         }
         continue;
       }
       s->index[k] = s->index[i];
       s->tr_ptr[k] = s->tr_ptr[i];
       s->tr_len[k] = s->tr_len[i];
+      s->tr_own[k] = s->tr_own[i];
+      s->bk_ptr[k] = s->bk_ptr[i];
+      s->bk_cap[k] = s->bk_cap[i];
       ++k;
     }
     s->index.resize(k);
     s->tr_ptr.resize(k);
     s->tr_len.resize(k);
+    s->tr_own.resize(k);
+    s->bk_ptr.resize(k);
+    s->bk_cap.resize(k);
+    ++s->epoch;
     s->total_bytes -= f.bytes;
     s->deleted_files += 1;
     s->deleted_bytes += f.bytes;
@@ -1498,14 +1610,18 @@ static void seg_writer(SegStore* s) {
     }
     const bool synced = !s->error && !(s->fd >= 0 && fdatasync(s->fd) != 0);
     if (!s->error && !synced) s->error = errno ? errno : -1;
-    std::vector<std::pair<uint8_t*, int64_t>> copies;
+    std::vector<SegStore::Copy> copies;
     {
       std::unique_lock<std::mutex> lk(s->cmu);
       s->ccv.wait(lk, [&] { return s->cdone; });
       copies.swap(s->cout);
     }
+    auto drop = [](const SegStore::Copy& c) {
+      free(c.blk);
+      if (c.own) free(c.tr);
+    };
     if (s->error) {
-      for (auto& c : copies) free(c.first);
+      for (auto& c : copies) drop(c);
       s->cv_done.notify_all();
       continue;                         // tokens stop advancing; the caller sees the error
     }
@@ -1514,13 +1630,17 @@ static void seg_writer(SegStore* s) {
       std::lock_guard<std::mutex> g(s->mu);
       for (size_t i = 0; i < pend.size(); ++i) {
         s->index.push_back(pend[i]);
-        const auto c = i < copies.size() ? copies[i] : std::pair<uint8_t*, int64_t>{nullptr, 0};
-        s->tr_ptr.push_back(c.first);
-        s->tr_len.push_back(c.second);
-        s->trailer_bytes += c.second;
+        const SegStore::Copy c = i < copies.size() ? copies[i] : SegStore::Copy{nullptr, 0, nullptr, 0, false};
+        s->tr_ptr.push_back(c.tr);
+        s->tr_len.push_back(c.tlen);
+        s->tr_own.push_back(c.own ? 1 : 0);
+        s->bk_ptr.push_back(c.blk);
+        s->bk_cap.push_back(c.bcap);
+        if (c.own) s->trailer_bytes += c.tlen;
+        s->blk_bytes += c.bcap;
       }
-      for (size_t i = pend.size(); i < copies.size(); ++i) free(copies[i].first);
-      trailer_trim(s);
+      for (size_t i = pend.size(); i < copies.size(); ++i) drop(copies[i]);
+      mem_trim(s);
     }
     if (last >= 0) {
       std::lock_guard<std::mutex> g(s->mu);
@@ -1611,11 +1731,15 @@ void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t ret
         f.path, true,
         [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) {
           s->index.push_back(index_entry(hd, b, f.id, off));
-          const auto c = trailer_copy(b, (int64_t)hd.bytes);
-          s->tr_ptr.push_back(c.first);
-          s->tr_len.push_back(c.second);
-          s->trailer_bytes += c.second;
-          trailer_trim(s);
+          const auto ts = trailer_span(b, (int64_t)hd.bytes);
+          uint8_t* t = ts.second ? own_copy(b + ts.first, ts.second) : nullptr;
+          s->tr_ptr.push_back(t);
+          s->tr_len.push_back(t ? ts.second : 0);
+          s->tr_own.push_back(t ? 1 : 0);
+          s->bk_ptr.push_back(nullptr);
+          s->bk_cap.push_back(0);
+          s->trailer_bytes += t ? ts.second : 0;
+          mem_trim(s);
         },
         [&](const uint8_t* rec) {
           SwSegCommitHdr c;
@@ -1733,8 +1857,11 @@ void swss_close(void* h) {
   s->ccv.notify_all();
   if (s->copier.joinable()) s->copier.join();
   seg_close_file(s);
-  for (uint8_t* p : s->tr_ptr) free(p);
-  for (auto& g : s->grave) free(g.second);
+  for (size_t i = 0; i < s->tr_ptr.size(); ++i)
+    if (s->tr_own[i]) free(s->tr_ptr[i]);
+  for (uint8_t* p : s->bk_ptr) free(p);
+  for (auto& g : s->grave) free(g.p);
+  for (auto& q : s->pool) free(q.first);
   free(s->bounce);
   free(s->commit_buf);
   delete s;
@@ -1750,10 +1877,10 @@ int64_t swss_index(void* h, SwSegIndexEnt* out, int64_t cap) {
   return n;
 }
 
-// swss_index plus, per entry, the address and length of the in-memory copy of the block's index
-// trailer (0 when not held).  An address stays valid until the entry leaves the index (retention)
-// or the copy is dropped (trailer cap) -- and for 120 s after that.
-int64_t swss_index_tr(void* h, SwSegIndexEnt* out, uint64_t* taddr, int64_t* tlen, int64_t cap) {
+// swss_index plus, per entry, the in-memory copies the store holds: the index trailer's address
+// and length, and the block copy's address (0 when not held).  Addresses stay valid while the
+// caller holds a read lease taken before this call (swss_lease_begin).
+int64_t swss_index_tr(void* h, SwSegIndexEnt* out, uint64_t* taddr, int64_t* tlen, uint64_t* baddr, int64_t cap) {
   SegStore* s = (SegStore*)h;
   std::lock_guard<std::mutex> g(s->mu);
   const int64_t n = (int64_t)s->index.size();
@@ -1761,18 +1888,37 @@ int64_t swss_index_tr(void* h, SwSegIndexEnt* out, uint64_t* taddr, int64_t* tle
     out[i] = s->index[(size_t)i];
     taddr[i] = (uint64_t)(uintptr_t)s->tr_ptr[(size_t)i];
     tlen[i] = s->tr_len[(size_t)i];
+    if (baddr) baddr[i] = (uint64_t)(uintptr_t)s->bk_ptr[(size_t)i];
   }
   return n;
 }
 
-// Bytes of trailer copies to hold in memory (older ones dropped beyond it); returns the bytes held.
-int64_t swss_trailer_cap(void* h, int64_t cap) {
+// Read leases: addresses from swss_index_tr stay valid from swss_lease_begin (returns the lease)
+// to swss_lease_end(lease).
+int64_t swss_lease_begin(void* h) {
   SegStore* s = (SegStore*)h;
   std::lock_guard<std::mutex> g(s->mu);
-  if (cap >= 0) {
-    s->trailer_cap = cap;
-    trailer_trim(s);
-  }
+  s->leases.insert(s->epoch);
+  return s->epoch;
+}
+
+void swss_lease_end(void* h, int64_t lease) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  auto it = s->leases.find(lease);
+  if (it != s->leases.end()) s->leases.erase(it);
+  mem_trim(s);
+}
+
+// Memory caps: bytes of own trailer copies and of block copies to hold (-1: leave as is).
+// Returns the trailer bytes held; *blk_held (if non-null) the block-copy bytes.
+int64_t swss_mem_caps(void* h, int64_t trailer_cap, int64_t blk_cap, int64_t* blk_held) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  if (trailer_cap >= 0) s->trailer_cap = trailer_cap;
+  if (blk_cap >= 0) s->blk_cap = blk_cap;
+  mem_trim(s);
+  if (blk_held) *blk_held = s->blk_bytes;
   return s->trailer_bytes;
 }
 

@@ -183,9 +183,9 @@ def native():
         _proto(lib, "swseg_verify", c_int32, P, c_int64)
         _proto(lib, "swseg_verify_pages", c_int32, P, c_int64, c_int64, c_int64)
         _proto(lib, "swseg_decode", c_int64, P, c_int64, c_int64, P, P, P, P, P, P, P, P, P, P, c_int64, P)
-        _proto(lib, "swseg_alt_page_rows", c_int64, P, P, P, P, P, c_int64, c_int32, P, P, c_int64)
+        _proto(lib, "swseg_alt_page_rows", c_int64, P, P, P, P, P, c_int64, c_int32, P, P, c_int64, P)
         _proto(lib, "swseg_fetch_rows", c_int64, P, P, P, P, P, c_int64, c_int32, P, P, P, P, P, P, P, P, P, P,
-               c_int64, P)
+               c_int64, P, P)
         _proto(lib, "swseg_string_bytes", c_int64, P, c_int64, c_int64)
         _proto(lib, "swseg_page_summary", c_int64, P, P)
         _proto(lib, "swseg_index_block", c_int64, P, c_int64, P, P, P, P, P, P)
@@ -205,7 +205,7 @@ def native():
         _proto(lib, "swseg_rechecksum", None, P)
         _proto(lib, "swseg_alt_hashes", c_int64, P, P, c_int64)
         _proto(lib, "swseg_scan_pages", c_int64, P, P, P, P, P, c_int64, c_int32, c_int32, P, c_int64, c_int32,
-               c_int64, c_int64, c_int32, P, P, P, c_int64)
+               c_int64, c_int64, c_int32, P, P, P, c_int64, P)
         _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)
         _proto(lib, "swss_append", c_int32, P, P, c_int64, c_int64)
         _proto(lib, "sw_varint_offsets", c_int32, P, c_int64, c_int64, c_int64, P)
@@ -218,10 +218,12 @@ def native():
         _proto(lib, "swss_stats", None, P, P)
         _proto(lib, "swss_close", None, P)
         _proto(lib, "swss_index", c_int64, P, P, c_int64)
-        _proto(lib, "swss_index_tr", c_int64, P, P, P, P, c_int64)
+        _proto(lib, "swss_index_tr", c_int64, P, P, P, P, P, c_int64)
+        _proto(lib, "swss_mem_caps", c_int64, P, c_int64, c_int64, P)
+        _proto(lib, "swss_lease_begin", c_int64, P)
+        _proto(lib, "swss_lease_end", None, P, c_int64)
         _proto(lib, "swseg_ix_page_geom", c_int64, P, c_int64, P, P, c_int64, P, P)
         _proto(lib, "swseg_ix_ctx_heads", c_int64, P, c_int64, c_int32, ctypes.c_uint32, P, P, P, P, c_int64)
-        _proto(lib, "swss_trailer_cap", c_int64, P, c_int64)
         _proto(lib, "swss_file", c_int32, P, c_int32, c_char_p, c_int32)
         _proto(lib, "sw_route_rejects", c_int64, P, P, c_int64, P, P, c_int64, c_char_p, P, P, c_int64, P,
                c_int64, P, c_int64, P, P)

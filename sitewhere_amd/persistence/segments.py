@@ -22,7 +22,9 @@ and date range).  Here nothing is acknowledged before it is on disk.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import functools
 import json
 import os
 import threading
@@ -469,19 +471,32 @@ class SegmentStore:
             cap = n + 1024
 
     def index_tr(self):
-        """(index entries, trailer copy addresses, trailer lengths): see swss_index_tr."""
+        """(index entries, trailer copy addresses, trailer lengths, block copy addresses): see
+        swss_index_tr.  Hold a :meth:`lease` while using the addresses."""
         cap = 1024
         while True:
             out = np.zeros(cap, INDEX_ENT)
-            ta, tl = np.zeros(cap, np.uint64), np.zeros(cap, np.int64)
-            n = int(self.lib.swss_index_tr(self.h, _p(out), _p(ta), _p(tl), cap))
+            ta, tl, ba = np.zeros(cap, np.uint64), np.zeros(cap, np.int64), np.zeros(cap, np.uint64)
+            n = int(self.lib.swss_index_tr(self.h, _p(out), _p(ta), _p(tl), _p(ba), cap))
             if n <= cap:
-                return out[:n], ta[:n], tl[:n]
+                return out[:n], ta[:n], tl[:n], ba[:n]
             cap = n + 1024
 
-    def trailer_cap(self, nbytes: int = -1) -> int:
-        """Set the bytes of index trailers held in memory (-1: leave); returns the bytes held."""
-        return int(self.lib.swss_trailer_cap(self.h, int(nbytes)))
+    def mem_caps(self, trailer_bytes: int = -1, block_bytes: int = -1) -> tuple[int, int]:
+        """Set the bytes of index-trailer copies and of recent-block copies the store holds in
+        memory (-1: leave); returns the bytes held (trailers, blocks)."""
+        held = np.zeros(1, np.int64)
+        t = int(self.lib.swss_mem_caps(self.h, int(trailer_bytes), int(block_bytes), _p(held)))
+        return t, int(held[0])
+
+    @contextlib.contextmanager
+    def lease(self):
+        """A read lease: in-memory copies seen through :meth:`index_tr` stay valid until it ends."""
+        tok = int(self.lib.swss_lease_begin(self.h))
+        try:
+            yield tok
+        finally:
+            self.lib.swss_lease_end(self.h, tok)
 
     def file_path(self, file_id: int) -> str | None:
         buf = ctypes.create_string_buffer(4096)
@@ -662,6 +677,22 @@ def boot_id(boot) -> int:
     return int(boot, 16) if isinstance(boot, str) else int(boot or 0)
 
 
+def _leased(fn):
+    """Run a read method under a segment-store read lease (re-entrant per thread): the in-memory
+    trailer and block copies it reaches stay valid until it returns."""
+    @functools.wraps(fn)
+    def run(self, *a, **k):
+        if getattr(self._tl, "leased", False):
+            return fn(self, *a, **k)
+        self._tl.leased = True
+        try:
+            with self.seg.lease():
+                return fn(self, *a, **k)
+        finally:
+            self._tl.leased = False
+    return run
+
+
 class DurableEventStore(DeviceEventStore):
     """Event store of engine tenants on durable segments (see module docstring).
 
@@ -673,12 +704,19 @@ class DurableEventStore(DeviceEventStore):
     entry."""
 
     def __init__(self, directory: str, rank: int = 0, rotate_bytes: int = 1 << 30, retention_bytes: int = 0,
-                 direct: bool = True, cache_blocks: int = 8, index: bool = True, index_threads: int | None = None):
+                 direct: bool = True, cache_blocks: int = 8, index: bool = True, index_threads: int | None = None,
+                 block_cache_bytes: int | None = None):
         # (index / index_threads: accepted for callers of the host indexer this store no longer needs --
         # every block arrives with its index trailer)
         self.dir = directory
         os.makedirs(directory, exist_ok=True)
         self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
+        # recent blocks kept in memory as they are written (the writes bypass the page cache): reads of
+        # fresh data -- the usual page-1 query -- never wait on the device
+        if block_cache_bytes is None:
+            block_cache_bytes = int(float(os.environ.get("SW_STORE_BLOCK_CACHE_GB", "8")) * (1 << 30))
+        self.seg.mem_caps(-1, int(block_cache_bytes))
+        self._tl = threading.local()
         # events added through the API (REST / RPC adds, command invocations and responses, rule and
         # presence alerts): a checksummed JSON-lines log, fdatasync'd before the add returns, replayed
         # into the in-memory indexes on open
@@ -976,11 +1014,10 @@ class DurableEventStore(DeviceEventStore):
         multi-block reads.  Trailers come from the segment store's in-memory copies (made while
         each block was written), else memory-mapped from the files.  Kept across appends: only
         new blocks (and blocks whose copy changed) are resolved."""
-        ents, taddr, tlen = self.seg.index_tr()
-        ver = (len(ents), int(ents["first_seq"][-1]) if len(ents) else 0, int(ents["first_seq"][0]) if len(ents) else 0,
-               int(taddr.sum()) if len(ents) else 0)
+        ents, taddr, tlen, baddr = self.seg.index_tr()
+        ver = (len(ents), int(ents["first_seq"][-1]) if len(ents) else 0, int(ents["first_seq"][0]) if len(ents) else 0)
         tabs = self._tabs
-        if tabs is not None and tabs[0] == ver:
+        if tabs is not None and tabs[0] == ver and np.array_equal(tabs[2], taddr) and np.array_equal(tabs[3], baddr):
             return tabs[1]
         res = {}
         P = ctypes.c_void_p
@@ -989,7 +1026,7 @@ class DurableEventStore(DeviceEventStore):
         removed = False
         for b in dict.fromkeys(boots.tolist()):
             m = boots == b
-            lst, ta, tl = ents[m], taddr[m], tlen[m]
+            lst, ta, tl, ba = ents[m], taddr[m], tlen[m], baddr[m]
             old = prev.get(b)
             k = 0
             if old is not None and old["n"] <= len(lst):
@@ -1005,7 +1042,7 @@ class DurableEventStore(DeviceEventStore):
             trs += [self._trailer_mem(ta[i], tl[i], lst[i]) if ta[i] else self._trailer(lst[i])
                     for i in range(k, len(lst))]
             addrs = [t[0] if t is not None else 0 for t in trs]
-            res[b] = {"ents": lst, "tr": trs, "n": len(lst), "addr": (P * len(lst))(*addrs), "taddr": ta,
+            res[b] = {"ents": lst, "tr": trs, "n": len(lst), "addr": (P * len(lst))(*addrs), "taddr": ta, "baddr": ba,
                       "first": lst["first_seq"].astype(np.int64), "world": lst["world"].astype(np.int64),
                       "rank": lst["rank"].astype(np.int64)}
         if removed or len(prev) > len(res):
@@ -1013,19 +1050,21 @@ class DurableEventStore(DeviceEventStore):
             with self._lock:
                 for k in [k for k in self._tmaps if k not in live]:      # retention removed the block
                     self._tmaps.pop(k, None)
-        self._tabs = (ver, res)
+        self._tabs = (ver, res, taddr, baddr)
         return res
 
     def index_wait(self, timeout_s: float = 60.0) -> bool:
         """Every block is indexed as it is written (its trailer): nothing to wait for."""
         return True
 
+    @_leased
     def index_stats(self) -> dict:
         tabs = self._boot_tables()
         n = sum(t["n"] for t in tabs.values())
         ix = [tr for t in tabs.values() for tr in t["tr"] if tr is not None]
         return {"blocks": n, "indexed": len(ix), "index_bytes": sum(tr[1] for tr in ix)}
 
+    @_leased
     def alternate_id_count(self) -> int:
         """Alternate ids stored (every block's trailer count; blocks without a trailer decoded)."""
         total = 0
@@ -1049,11 +1088,12 @@ class DurableEventStore(DeviceEventStore):
         columns are decoded (natively, on ``threads`` threads; ctypes releases the interpreter
         meanwhile); skipped blocks are counted from their trailers, not decoded."""
         from concurrent.futures import ThreadPoolExecutor
-        pairs = [(e, tr) for t in self._boot_tables().values() for e, tr in zip(t["ents"], t["tr"])]
+        with self.seg.lease():            # the trailers' id counts, read while they are held
+            pairs = [(e, int(tr[2]["n_alt"]) if tr is not None else None)
+                     for t in self._boot_tables().values() for e, tr in zip(t["ents"], t["tr"])]
         pairs.sort(key=lambda x: (int(x[0]["recv_ms"]), int(x[0]["first_seq"])), reverse=True)
         ents = []
-        for e, tr in pairs:
-            n = int(tr[2]["n_alt"]) if tr is not None else None
+        for e, n in pairs:
             if skip > 0 and n is not None and skip >= n:
                 skip -= n
                 continue
@@ -1088,6 +1128,7 @@ class DurableEventStore(DeviceEventStore):
                     out.setdefault(int(hv), []).append((t, int(bo[j]), int(po[j])))
         return out
 
+    @_leased
     def find_alternate_hashes(self, hashes, covered: tuple | None = None, indexed_only: bool = False) -> dict:
         """alt-id hash -> event id string for the hashes stored on disk, the newest event per hash
         (store-backed dedup beyond the engine's window: ``AlternateIdDeduplicator`` asks the event
@@ -1135,6 +1176,7 @@ class DurableEventStore(DeviceEventStore):
                             found[hv] = f"{int(e['boot']):x}-{int(self._eids(e, [i])[0])}"
         return found
 
+    @_leased
     def get_event_by_alternate_id(self, alt: str):
         from ..pipeline.fleet import hash64
         ev = self._objects.get_event_by_alternate_id(alt)
@@ -1347,7 +1389,10 @@ class DurableEventStore(DeviceEventStore):
         pos = ents["offset"][bis].astype(np.int64) + off.astype(np.int64)
         n_rows = ents["n_rows"][bis].astype(np.int64)
         rows = np.minimum(PAGE_ROWS, n_rows - pages * PAGE_ROWS).astype(np.uint32)
-        return ents["file"][bis].astype(np.int64), pos, nb, rows
+        # pages of blocks the store holds in memory are read there (0: from the file)
+        ba = t["baddr"][bis] if "baddr" in t else np.zeros(n, np.uint64)
+        mem = np.where(ba != 0, ba + off.astype(np.uint64), np.uint64(0)).astype(np.uint64)
+        return ents["file"][bis].astype(np.int64), pos, nb, rows, mem
 
     def _fetch(self, t, bis, rows) -> dict:
         """Decoded columns (+ strings, + per-row block fields for :func:`materialize_row`) of rows
@@ -1358,7 +1403,7 @@ class DurableEventStore(DeviceEventStore):
         pages = rows // PAGE_ROWS
         order = np.lexsort((pages, bis))
         sb, sp = bis[order], pages[order]
-        files, pos, nb, prows = self._page_geometry(t, sb, sp)
+        files, pos, nb, prows, mem = self._page_geometry(t, sb, sp)
         rip = (rows[order] - sp * PAGE_ROWS).astype(np.int32)
         cols = {"etype": np.empty(n, np.uint8), "level": np.empty(n, np.uint8), "date": np.empty(n, np.int64),
                 "asg": np.empty(n, np.int32), "name": np.empty(n, np.uint16), "v0": np.empty(n, np.float64),
@@ -1372,7 +1417,7 @@ class DurableEventStore(DeviceEventStore):
                 k = int(native().swseg_fetch_rows(
                     _p(fd), _p(pos), _p(nb), _p(prows), _p(rip), n, min(self.scan_threads, 8),
                     *[_p(cols[c]) for c in ("etype", "level", "date", "asg", "name", "v0", "v1", "v2", "flags")],
-                    _p(heap), cap, _p(offs)))
+                    _p(heap), cap, _p(offs), _p(mem)))
                 if k >= 0:
                     break
                 if k <= -(1 << 40):
@@ -1406,7 +1451,7 @@ class DurableEventStore(DeviceEventStore):
         n = len(bis)
         if not n:
             return np.zeros(0, np.int64), np.zeros(0, np.int64)
-        files, pos, nb, prows = self._page_geometry(t, bis, pages)
+        files, pos, nb, prows, mem = self._page_geometry(t, bis, pages)
         hv = np.asarray(hashes, np.uint64)
         fd, opened = self._file_fds(files)
         try:
@@ -1414,7 +1459,7 @@ class DurableEventStore(DeviceEventStore):
             while True:
                 ot, orow = np.empty(cap, np.int64), np.empty(cap, np.int32)
                 k = int(native().swseg_alt_page_rows(_p(fd), _p(pos), _p(nb), _p(prows), _p(hv), n,
-                                                     min(self.scan_threads, 8), _p(ot), _p(orow), cap))
+                                                     min(self.scan_threads, 8), _p(ot), _p(orow), cap, _p(mem)))
                 if k < 0:
                     raise ValueError(f"corrupt or unreadable event page (candidate {-k - 1})")
                 if k <= cap:
@@ -1448,7 +1493,7 @@ class DurableEventStore(DeviceEventStore):
         bis, pages = np.asarray(bis, np.int64), np.asarray(pages, np.int64)
         if not len(bis):
             return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
-        files, pos, nb, _ = self._page_geometry(t, bis, pages)
+        files, pos, nb, _, mem = self._page_geometry(t, bis, pages)
         poff = np.zeros(len(bis), np.uint32)
         pix = pages.astype(np.int32)
         ct = np.ascontiguousarray(ctx_tab, np.int32) if ctx_tab is not None else np.zeros(1, np.int32)
@@ -1459,7 +1504,8 @@ class DurableEventStore(DeviceEventStore):
                 ot, orow, od = np.empty(cap, np.int64), np.empty(cap, np.int32), np.empty(cap, np.int64)
                 k = int(native().swseg_scan_pages(_p(fd), _p(pos), _p(poff), _p(nb), _p(pix), len(bis), int(et),
                                                   int(asg), _p(ct), len(ct) if ctx_tab is not None else 0, int(ctx_id),
-                                                  int(d_lo), int(d_hi), self.scan_threads, _p(ot), _p(orow), _p(od), cap))
+                                                  int(d_lo), int(d_hi), self.scan_threads, _p(ot), _p(orow), _p(od), cap,
+                                                  _p(mem)))
                 if k < 0:
                     raise ValueError(f"event page unreadable (task {-k - 1})")
                 if k <= cap:
@@ -1613,6 +1659,7 @@ class DurableEventStore(DeviceEventStore):
                 cand += extra
         return total, self._collect(t, cand)[1]
 
+    @_leased
     def list_events(self, event_type, index, entity_ids, criteria: DateRangeSearchCriteria | None = None):
         """Events of one type for entities of an index, newest first, with the exact total.
         Assignment: page zone maps of the assignment-clustered blocks, then those pages' leading

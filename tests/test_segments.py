@@ -3,6 +3,7 @@ native segment store (group commit, recovery, retention) and the DurableEventSto
 MI355X encoder is checked against the CPU encoder bit for bit in tests/test_gpu_segments.py."""
 from __future__ import annotations
 
+import ctypes
 import os
 import time
 
@@ -541,32 +542,58 @@ def test_point_fetch_equals_page_decode(tmp_path):
 
 
 def test_trailer_copies_in_memory_and_cap(tmp_path):
-    """The segment store holds each block's index trailer in memory (copied while the block is
-    written, and on recovery); beyond the cap the oldest copies are dropped and the reads fall back
-    to mapping the trailers from the files -- same answers either way."""
-    es, _, blocks, exp_all = _ctx_store_blocks(tmp_path, n_blocks=4, rows_per=2000)
-    ents, ta, tl = es.seg.index_tr()
-    assert len(ents) == 4 and (ta != 0).all() and (tl > 0).all()
-    for (blk, _), n in zip(blocks, tl.tolist()):
-        assert n == len(blk) - sg.trailer_offset(blk)
-    held = es.seg.trailer_cap()
-    assert held == int(tl.sum())
+    """The segment store holds each block's index trailer in memory (inside the copy of the block it
+    keeps while the block is recent, else its own copy -- made while the block is written, and on
+    recovery); beyond the caps the oldest copies are dropped and the reads fall back to the files
+    -- same answers either way."""
     from sitewhere_amd.models.domain import DateRangeSearchCriteria
+    es, _, blocks, exp_all = _ctx_store_blocks(tmp_path, n_blocks=4, rows_per=2000)
+    with es.seg.lease():
+        ents, ta, tl, ba = es.seg.index_tr()
+        assert len(ents) == 4 and (ta != 0).all() and (tl > 0).all() and (ba != 0).all()
+        for (blk, _), n, t, b in zip(blocks, tl.tolist(), ta.tolist(), ba.tolist()):
+            toff = sg.trailer_offset(blk)
+            assert n == len(blk) - toff and t == b + toff           # the trailer inside the block copy
+            assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * len(blk)).from_address(b)), blk)
     crit = DateRangeSearchCriteria(page_size=50)
     want = es.list_events("Measurement", "Area", ["area-1"], crit)
+    want_a = es.list_events("Measurement", "Assignment", ["asg-3"], crit)
     alt = next(a for _, a in exp_all[::-1] if a is not None)
     want_alt = es.get_event_by_alternate_id(alt).id
-    es.seg.trailer_cap(int(tl[-1]))                     # keep the newest copy only
-    ents2, ta2, _ = es.seg.index_tr()
-    assert (ta2[:-1] == 0).all() and ta2[-1] != 0
-    got = es.list_events("Measurement", "Area", ["area-1"], crit)
-    assert (got.num_results, [e.id for e in got.results]) == (want.num_results, [e.id for e in want.results])
-    assert es.get_event_by_alternate_id(alt).id == want_alt
+
+    def same():
+        got = es.list_events("Measurement", "Area", ["area-1"], crit)
+        assert (got.num_results, [e.id for e in got.results]) == (want.num_results, [e.id for e in want.results])
+        got = es.list_events("Measurement", "Assignment", ["asg-3"], crit)
+        assert (got.num_results, [e.id for e in got.results]) == (want_a.num_results, [e.id for e in want_a.results])
+        assert es.get_event_by_alternate_id(alt).id == want_alt
+
+    es.seg.mem_caps(-1, 2 * (1 << 20))                   # block copies: the newest two (1 MiB slots)
+    _, ta2, _, ba2 = es.seg.index_tr()
+    assert (ba2[:2] == 0).all() and (ba2[2:] != 0).all() and (ta2 != 0).all()
+    same()
+    es.seg.mem_caps(int(tl[-1]), 0)                      # no block copies, one own trailer copy
+    _, ta3, _, ba3 = es.seg.index_tr()
+    assert (ba3 == 0).all() and (ta3[:-1] == 0).all() and ta3[-1] != 0
+    same()
     d = es.dir
     es.close()
     es2 = sg.DurableEventStore(d, direct=False)           # recovery copies the trailers again
-    _, ta3, _ = es2.seg.index_tr()
-    assert (ta3 != 0).all()
+    _, ta4, _, _ = es2.seg.index_tr()
+    assert (ta4 != 0).all()
     got = es2.list_events("Measurement", "Area", ["area-1"], crit)
     assert [e.id for e in got.results] == [e.id for e in want.results]
     es2.close()
+
+
+def test_read_lease_defers_reclaiming_copies(tmp_path):
+    """A copy dropped while a read lease is held stays readable until the lease ends."""
+    es, _, blocks, _ = _ctx_store_blocks(tmp_path, n_blocks=2, rows_per=1500)
+    with es.seg.lease():
+        _, _, _, ba = es.seg.index_tr()
+        b0 = int(ba[0])
+        es.seg.mem_caps(-1, 0)                           # drop every block copy
+        assert (es.seg.index_tr()[3] == 0).all()
+        blk = blocks[0][0]
+        assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * len(blk)).from_address(b0)), blk)
+    es.close()
