@@ -1239,10 +1239,10 @@ struct SegStore {
   uint8_t* commit_buf = nullptr;          // one SEG_COMMIT_BYTES record, aligned for O_DIRECT
   std::map<uint64_t, int64_t> sources;    // durable input offsets (max per key)
   // What the store holds in memory for the read path, parallel to `index` (null: not held):
-  //  * a copy of each recent block (bk_*), up to blk_cap bytes, newest kept -- the blocks were
-  //    written with O_DIRECT, so without it every read of a fresh block goes to the device;
-  //  * each block's index trailer (tr_*): inside the block copy while there is one, else its own
-  //    copy, up to trailer_cap bytes of those.
+  //  * the scan image of each recent block (bk_*: every page's header and leading columns, about a
+  //    third of the block), up to blk_cap bytes, newest kept -- the blocks were written with
+  //    O_DIRECT, so without it every listing over fresh blocks goes to the device;
+  //  * each block's index trailer (tr_*), up to trailer_cap bytes.
   // Copies are made while the block is written (copier threads, from the caller's buffer, which
   // stays valid until the block is durable) and, for trailers, on recovery.  A copy dropped by a cap
   // or by retention is reclaimed only once every read lease that could have seen it has ended
@@ -1281,25 +1281,47 @@ static std::pair<int64_t, int64_t> trailer_span(const uint8_t* b, int64_t len) {
   return {(int64_t)toff, (int64_t)h.bytes - toff};
 }
 
+// Scan image of a block: what the page scans read (each page's header and leading columns --
+// etype, level, date, assignment), pages back to back.  Layout: u32 n_pages, u32 0, u32 offset of
+// page p's prefix in the image (n_pages of them, padded to 8 bytes), then the prefixes (8-aligned).
+static int64_t page_prefix(const uint8_t* pg) {
+  SwSegPageHdr ph;
+  memcpy(&ph, pg, sizeof(ph));
+  const SwSegCol& ca = ph.cols[SEG_ASG];
+  const int64_t need = (int64_t)ca.data_off + (int64_t)seg_col_bytes(ca.count, ca.bits, 0);
+  return std::min<int64_t>(std::max<int64_t>(need, sizeof(SwSegPageHdr)), ph.bytes);
+}
+
+static int64_t scan_image_bytes(const uint8_t* b, int64_t len) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  if ((int64_t)h.bytes > len || !h.n_pages) return 0;
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  int64_t n = 8 + rd8(4u * h.n_pages);
+  for (uint32_t p = 0; p < h.n_pages; ++p) n += (page_prefix(b + pt[p]) + 7) & ~int64_t(7);
+  return n;
+}
+
+static void scan_image_build(const uint8_t* b, uint8_t* dst) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  uint32_t* hdr = (uint32_t*)dst;
+  hdr[0] = h.n_pages;
+  hdr[1] = 0;
+  int64_t o = 8 + rd8(4u * h.n_pages);
+  for (uint32_t p = 0; p < h.n_pages; ++p) {
+    const int64_t n = page_prefix(b + pt[p]);
+    hdr[2 + p] = (uint32_t)o;
+    memcpy(dst + o, b + pt[p], (size_t)n);
+    o += (n + 7) & ~int64_t(7);
+  }
+}
+
 static uint8_t* own_copy(const uint8_t* src, int64_t n) {
   uint8_t* c = (uint8_t*)aligned_alloc(64, (size_t)((n + 63) / 64 * 64));
   if (c) memcpy(c, src, (size_t)n);
   return c;
-}
-
-// memcpy of a large block on a few threads (one core's copy rate would pace the writer).
-static void wide_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
-  const int T = n >= (8ll << 20) ? 4 : 1;
-  if (T == 1) {
-    memcpy(dst, src, (size_t)n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int w = 0; w < T; ++w) {
-    const int64_t a = (n * w / T) & ~int64_t(4095), b = w + 1 == T ? n : (n * (w + 1) / T) & ~int64_t(4095);
-    th.emplace_back([=] { memcpy(dst + a, src + a, (size_t)(b - a)); });
-  }
-  for (auto& x : th) x.join();
 }
 
 // Caller holds s->mu.  Retire a copy (reclaimed once no lease can still see it).
@@ -1369,13 +1391,14 @@ static void seg_copier(SegStore* s) {
     for (const SegItem& it : *job) {
       const auto ts = trailer_span(it.ptr, it.len);
       SegStore::Copy c{nullptr, 0, nullptr, 0, false};
-      if (keep > 0 && it.len <= keep) {
+      const int64_t isz = keep > 0 ? scan_image_bytes(it.ptr, it.len) : 0;
+      if (isz > 0 && isz <= keep) {
         uint8_t* p = nullptr;
         int64_t cap = 0;
         {
           std::lock_guard<std::mutex> g(s->mu);
           for (size_t k = 0; k < s->pool.size(); ++k)
-            if (s->pool[k].second >= it.len) {
+            if (s->pool[k].second >= isz) {
               p = s->pool[k].first;
               cap = s->pool[k].second;
               s->pool.erase(s->pool.begin() + (long)k);
@@ -1383,17 +1406,16 @@ static void seg_copier(SegStore* s) {
             }
         }
         if (!p) {
-          cap = round_up_mb(it.len);
+          cap = round_up_mb(isz);
           p = (uint8_t*)aligned_alloc(4096, (size_t)cap);
         }
         if (p) {
-          wide_copy(p, it.ptr, it.len);
+          scan_image_build(it.ptr, p);
           c.blk = p;
           c.bcap = cap;
-          if (ts.second) { c.tr = p + ts.first; c.tlen = ts.second; }
         }
       }
-      if (!c.blk && ts.second) {
+      if (ts.second) {
         c.tr = own_copy(it.ptr + ts.first, ts.second);
         c.tlen = c.tr ? ts.second : 0;
         c.own = c.tr != nullptr;

@@ -711,10 +711,11 @@ class DurableEventStore(DeviceEventStore):
         self.dir = directory
         os.makedirs(directory, exist_ok=True)
         self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
-        # recent blocks kept in memory as they are written (the writes bypass the page cache): reads of
-        # fresh data -- the usual page-1 query -- never wait on the device
+        # the scan images of recent blocks (page headers + leading columns) kept in memory as the
+        # blocks are written (the writes bypass the page cache): listings over fresh data -- the
+        # usual page-1 query -- do not wait on the device
         if block_cache_bytes is None:
-            block_cache_bytes = int(float(os.environ.get("SW_STORE_BLOCK_CACHE_GB", "8")) * (1 << 30))
+            block_cache_bytes = int(float(os.environ.get("SW_STORE_SCAN_CACHE_GB", "4")) * (1 << 30))
         self.seg.mem_caps(-1, int(block_cache_bytes))
         self._tl = threading.local()
         # events added through the API (REST / RPC adds, command invocations and responses, rule and
@@ -1373,7 +1374,7 @@ class DurableEventStore(DeviceEventStore):
             raise
         return np.asarray(opened, np.int32)[inv.reshape(-1)], opened
 
-    def _page_geometry(self, t, bis: np.ndarray, pages: np.ndarray):
+    def _page_geometry(self, t, bis: np.ndarray, pages: np.ndarray, scan: bool = False):
         """(file id, file offset, bytes, rows) of pages ``pages`` of blocks ``bis`` (positions in t)."""
         n = len(bis)
         ents = t["ents"]
@@ -1389,9 +1390,16 @@ class DurableEventStore(DeviceEventStore):
         pos = ents["offset"][bis].astype(np.int64) + off.astype(np.int64)
         n_rows = ents["n_rows"][bis].astype(np.int64)
         rows = np.minimum(PAGE_ROWS, n_rows - pages * PAGE_ROWS).astype(np.uint32)
-        # pages of blocks the store holds in memory are read there (0: from the file)
-        ba = t["baddr"][bis] if "baddr" in t else np.zeros(n, np.uint64)
-        mem = np.where(ba != 0, ba + off.astype(np.uint64), np.uint64(0)).astype(np.uint64)
+        # scans read the pages' prefixes from the scan images the store holds (0: from the file)
+        mem = np.zeros(n, np.uint64)
+        if scan and "baddr" in t:
+            ba = t["baddr"]
+            for bi in np.unique(bis[ba[bis] != 0]).tolist():
+                img = int(ba[bi])
+                npg = int(np.ctypeslib.as_array((ctypes.c_uint32 * 1).from_address(img))[0])
+                io = np.ctypeslib.as_array((ctypes.c_uint32 * (2 + npg)).from_address(img))[2:]
+                m = bis == bi
+                mem[m] = np.uint64(img) + io[pages[m]].astype(np.uint64)
         return ents["file"][bis].astype(np.int64), pos, nb, rows, mem
 
     def _fetch(self, t, bis, rows) -> dict:
@@ -1493,7 +1501,7 @@ class DurableEventStore(DeviceEventStore):
         bis, pages = np.asarray(bis, np.int64), np.asarray(pages, np.int64)
         if not len(bis):
             return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
-        files, pos, nb, _, mem = self._page_geometry(t, bis, pages)
+        files, pos, nb, _, mem = self._page_geometry(t, bis, pages, scan=True)
         poff = np.zeros(len(bis), np.uint32)
         pix = pages.astype(np.int32)
         ct = np.ascontiguousarray(ctx_tab, np.int32) if ctx_tab is not None else np.zeros(1, np.int32)

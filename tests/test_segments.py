@@ -542,9 +542,9 @@ def test_point_fetch_equals_page_decode(tmp_path):
 
 
 def test_trailer_copies_in_memory_and_cap(tmp_path):
-    """The segment store holds each block's index trailer in memory (inside the copy of the block it
-    keeps while the block is recent, else its own copy -- made while the block is written, and on
-    recovery); beyond the caps the oldest copies are dropped and the reads fall back to the files
+    """The segment store holds each block's index trailer in memory and, while the block is recent,
+    its scan image (page headers + leading columns) -- made while the block is written, trailers on
+    recovery too; beyond the caps the oldest copies are dropped and the reads fall back to the files
     -- same answers either way."""
     from sitewhere_amd.models.domain import DateRangeSearchCriteria
     es, _, blocks, exp_all = _ctx_store_blocks(tmp_path, n_blocks=4, rows_per=2000)
@@ -553,8 +553,15 @@ def test_trailer_copies_in_memory_and_cap(tmp_path):
         assert len(ents) == 4 and (ta != 0).all() and (tl > 0).all() and (ba != 0).all()
         for (blk, _), n, t, b in zip(blocks, tl.tolist(), ta.tolist(), ba.tolist()):
             toff = sg.trailer_offset(blk)
-            assert n == len(blk) - toff and t == b + toff           # the trailer inside the block copy
-            assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * len(blk)).from_address(b)), blk)
+            assert n == len(blk) - toff
+            assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(t)), blk[toff:])
+            npg = int(blk[:64].view(sg.HDR)[0]["n_pages"])
+            io = np.ctypeslib.as_array((ctypes.c_uint32 * (2 + npg)).from_address(b))
+            pt = blk[64:64 + 4 * (npg + 1)].view(np.uint32)
+            assert io[0] == npg
+            for p in range(npg):          # each page's first 256 bytes (header + leading columns)
+                img = np.ctypeslib.as_array((ctypes.c_uint8 * 256).from_address(b + int(io[2 + p])))
+                assert np.array_equal(img, blk[int(pt[p]):int(pt[p]) + 256])
     crit = DateRangeSearchCriteria(page_size=50)
     want = es.list_events("Measurement", "Area", ["area-1"], crit)
     want_a = es.list_events("Measurement", "Assignment", ["asg-3"], crit)
@@ -568,11 +575,11 @@ def test_trailer_copies_in_memory_and_cap(tmp_path):
         assert (got.num_results, [e.id for e in got.results]) == (want_a.num_results, [e.id for e in want_a.results])
         assert es.get_event_by_alternate_id(alt).id == want_alt
 
-    es.seg.mem_caps(-1, 2 * (1 << 20))                   # block copies: the newest two (1 MiB slots)
+    es.seg.mem_caps(-1, 2 * (1 << 20))                   # scan images: the newest two (1 MiB slots)
     _, ta2, _, ba2 = es.seg.index_tr()
     assert (ba2[:2] == 0).all() and (ba2[2:] != 0).all() and (ta2 != 0).all()
     same()
-    es.seg.mem_caps(int(tl[-1]), 0)                      # no block copies, one own trailer copy
+    es.seg.mem_caps(int(tl[-1]), 0)                      # no scan images, one trailer copy
     _, ta3, _, ba3 = es.seg.index_tr()
     assert (ba3 == 0).all() and (ta3[:-1] == 0).all() and ta3[-1] != 0
     same()
@@ -592,8 +599,8 @@ def test_read_lease_defers_reclaiming_copies(tmp_path):
     with es.seg.lease():
         _, _, _, ba = es.seg.index_tr()
         b0 = int(ba[0])
-        es.seg.mem_caps(-1, 0)                           # drop every block copy
+        before = np.ctypeslib.as_array((ctypes.c_uint8 * 4096).from_address(b0)).copy()
+        es.seg.mem_caps(-1, 0)                           # drop every scan image
         assert (es.seg.index_tr()[3] == 0).all()
-        blk = blocks[0][0]
-        assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * len(blk)).from_address(b0)), blk)
+        assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * 4096).from_address(b0)), before)
     es.close()
