@@ -489,6 +489,11 @@ def main():
         sys.setswitchinterval(2e-4)
         reads = ReadLoad(dur["store"], int(np.max(dev)) + 1, threads=args.read_threads,
                          pause_s=args.read_pause_ms / 1e3, seed=rank)
+    # the setup's long-lived objects (registry, dictionaries: millions with --read-threads) leave the
+    # collector's view: a full collection over them would stall every thread of the process
+    import gc
+    gc.collect()
+    gc.freeze()
     barrier()
     if reads is not None:
         reads.start()

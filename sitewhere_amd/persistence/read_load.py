@@ -45,6 +45,7 @@ class ReadLoad:
         self.threads, self.pause_s, self.page_size = int(threads), float(pause_s), int(page_size)
         self.seed = seed
         self.lat = {k: [] for k in KINDS}
+        self.phases = {k: [] for k in KINDS if k.startswith("list")}   # per query: {phase: seconds}
         self.results = {k: [] for k in KINDS}
         self.errors: list[str] = []
         self._stop = threading.Event()
@@ -63,14 +64,16 @@ class ReadLoad:
     def _one(self, kind: str, rng):
         st = self.store
         crit = DateRangeSearchCriteria(page_size=self.page_size)
-        if kind == "list_assignment":
+        if kind in ("list_assignment", "list_area"):
+            ix, ent = ("Assignment", f"asg-{int(rng.integers(0, self.n_asg))}") if kind == "list_assignment" else \
+                ("Area", f"area-{int(rng.integers(0, self.n_area))}")
             t = time.perf_counter()
-            r = st.list_events("Measurement", "Assignment", [f"asg-{int(rng.integers(0, self.n_asg))}"], crit)
-            return time.perf_counter() - t, r.num_results
-        if kind == "list_area":
-            t = time.perf_counter()
-            r = st.list_events("Measurement", "Area", [f"area-{int(rng.integers(0, self.n_area))}"], crit)
-            return time.perf_counter() - t, r.num_results
+            r = st.list_events("Measurement", ix, [ent], crit)
+            dt = time.perf_counter() - t
+            tl = getattr(st, "_tl", None)
+            if tl is not None and getattr(tl, "phases", None) is not None:
+                self.phases[kind].append(dict(tl.phases, total=dt))
+            return dt, r.num_results
         if kind == "by_alt_miss":
             t = time.perf_counter()
             ev = st.get_event_by_alternate_id(f"never-stored-{int(rng.integers(0, 1 << 40))}")
@@ -139,4 +142,14 @@ class ReadLoad:
                                   "p99": round(float(np.percentile(v, 99)), 3), "max": round(float(v.max()), 3)}
                 if k.startswith("list"):
                     out[k + "_ms"]["results_mean"] = round(float(np.mean(self.results[k])), 1)
+                    ph = self.phases.get(k) or []
+                    if ph:
+                        # the phases of the slowest 5% of the queries, and the median query's
+                        tot = np.array([p["total"] for p in ph])
+                        slow = [ph[i] for i in np.argsort(tot)[-max(1, len(ph) // 20):]]
+                        mid = ph[int(np.argsort(tot)[len(ph) // 2])]
+                        keys = sorted({x for p in ph for x in p if x != "total"})
+                        out[k + "_ms"]["phases_p50_query"] = {x: round(1e3 * mid.get(x, 0.0), 3) for x in keys}
+                        out[k + "_ms"]["phases_slowest5pct_mean"] = {
+                            x: round(1e3 * float(np.mean([p.get(x, 0.0) for p in slow])), 3) for x in keys + ["total"]}
         return out

@@ -1675,6 +1675,9 @@ class DurableEventStore(DeviceEventStore):
         :meth:`_list_context`).  API-added events join from their own store."""
         c = criteria or DateRangeSearchCriteria(page_size=100)
         et = _ETYPE.get(DeviceEventType(event_type))
+        clock = time.perf_counter
+        ph = self._tl.phases = {}                     # where the call's time went (read-load reports)
+        t0 = clock()
         objs = self._objects.list_events(event_type, index, entity_ids, DateRangeSearchCriteria(
             page_size=0, start_date=c.start_date, end_date=c.end_date)).results
         if et is None:
@@ -1687,7 +1690,10 @@ class DurableEventStore(DeviceEventStore):
         d_hi = c.end_date if c.end_date is not None else (1 << 62)
         total = len(objs)
         found = []                                    # (dates, eids, block positions, rows, table)
-        for b, t in self._boot_tables().items():
+        tabs = self._boot_tables()
+        t1 = clock()
+        ph["tables"] = t1 - t0
+        for b, t in tabs.items():
             if pos == 0:
                 with self._lock:
                     tok = self._asg_tok.get(b, {})
@@ -1697,6 +1703,8 @@ class DurableEventStore(DeviceEventStore):
                 n, parts = self._list_context(t, b, pos, want, et, d_lo, d_hi, need)
             total += n
             found.extend(parts)
+        t2 = clock()
+        ph["index"] = t2 - t1
         if not found:
             return SearchResults(total, c.slice(objs))
         dates = np.concatenate([x[0] for x in found])
@@ -1713,10 +1721,16 @@ class DurableEventStore(DeviceEventStore):
             groups: dict = {}
             for j, t in enumerate(tabs):
                 groups.setdefault(id(t), (t, []))[1].append(j)
+            t3 = clock()
+            ph["order"] = t3 - t2
             for t, js in groups.values():
                 cols = self._fetch(t, pos_[sel[js]], rows[sel[js]])
+                t4 = clock()
+                ph["fetch"] = ph.get("fetch", 0.0) + t4 - t3
                 for m, j in enumerate(js):
                     evs[j] = self._materialize(cols, m)
+                t3 = clock()
+                ph["materialize"] = ph.get("materialize", 0.0) + t3 - t4
             return evs
         if objs:
             if paged:
