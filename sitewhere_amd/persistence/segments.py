@@ -715,7 +715,17 @@ class DurableEventStore(DeviceEventStore):
         # blocks are written (the writes bypass the page cache): listings over fresh data -- the
         # usual page-1 query -- do not wait on the device
         if block_cache_bytes is None:
-            block_cache_bytes = int(float(os.environ.get("SW_STORE_SCAN_CACHE_GB", "4")) * (1 << 30))
+            # ~6 B per stored event: sized to hold the whole retained store's images where the host
+            # has the memory (an eighth of it, at most 32 GB)
+            env = os.environ.get("SW_STORE_SCAN_CACHE_GB")
+            if env is not None:
+                block_cache_bytes = int(float(env) * (1 << 30))
+            else:
+                try:
+                    ram = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+                except (ValueError, OSError, AttributeError):
+                    ram = 32 << 30
+                block_cache_bytes = int(min(32 << 30, ram // 8))
         self.seg.mem_caps(-1, int(block_cache_bytes))
         self._tl = threading.local()
         # events added through the API (REST / RPC adds, command invocations and responses, rule and
