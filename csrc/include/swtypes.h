@@ -62,6 +62,8 @@ enum SwStatus : uint8_t {
 #define SW_F_UPDATE_STATE 0x2
 #define SW_F_HAS_DATE 0x4
 #define SW_F_HAS_ELEVATION 0x8
+#define SW_F_SYS_ALERT 0x10     // (API-added rows only) alert of source System with its own message
+#define SW_F_JSON 0x20          // (API-added rows only) type-specific fields as JSON in the metadata span
 
 // Decoded event record, 80 bytes.  Output of the decoder, unit of the
 // multi-GPU all-to-all, input of validation.

@@ -35,7 +35,8 @@ from collections import OrderedDict
 import numpy as np
 
 from .._native import native
-from ..models.columnar import EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE, NO_NAME, OUT_REC
+from ..models.columnar import (EV_ALERT, EV_COMMAND_INVOCATION, EV_COMMAND_RESPONSE, EV_LOCATION, EV_MEASUREMENT,
+                               EV_STATE_CHANGE, NO_NAME, OUT_REC)
 from ..models.domain import (AlertLevel, AlertSource, DateRangeSearchCriteria, DeviceAlert, DeviceEventIndex,
                              DeviceEventType, DeviceLocation, DeviceMeasurement, DeviceStateChange, SearchResults,
                              event_from_dict)
@@ -43,6 +44,7 @@ from .events import DeviceEventStore, MemoryEventStore
 
 # SEG_FLAGS bits (csrc/include/swseg.h)
 SEGF_HAS_US, SEGF_US, SEGF_HAS_ELEV, SEGF_HAS_ALT, SEGF_HAS_META, SEGF_GEN = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+SEGF_SYS, SEGF_JSON = 0x40, 0x80          # API-added rows: System alert with a message; JSON fields
 SEG_ALIGN = 4096
 PAGE_ROWS = 1024
 PAGE_HDR = 400              # sizeof(SwSegPageHdr), csrc/include/swseg.h
@@ -289,7 +291,8 @@ def row_strings(cols: dict, i: int) -> tuple[str | None, str, dict]:
     f = int(cols["flags"][i])
     alt = _str(cols, i, 0).decode("utf-8", "replace") if f & SEGF_HAS_ALT else None
     msg = _str(cols, i, 1).decode("utf-8", "replace")
-    md = parse_metadata(_str(cols, i, 2), _META_FIELD.get(int(cols["etype"][i]), 0)) if f & SEGF_HAS_META else {}
+    md = parse_metadata(_str(cols, i, 2), _META_FIELD.get(int(cols["etype"][i]), 0)) \
+        if f & SEGF_HAS_META and not f & SEGF_JSON else {}
     return alt, msg, md
 
 
@@ -666,7 +669,9 @@ class DurableBlockSink:
 
 
 _ETYPE = {DeviceEventType.Measurement: EV_MEASUREMENT, DeviceEventType.Location: EV_LOCATION,
-          DeviceEventType.Alert: EV_ALERT, DeviceEventType.StateChange: EV_STATE_CHANGE}
+          DeviceEventType.Alert: EV_ALERT, DeviceEventType.StateChange: EV_STATE_CHANGE,
+          DeviceEventType.CommandInvocation: EV_COMMAND_INVOCATION,
+          DeviceEventType.CommandResponse: EV_COMMAND_RESPONSE}
 _LEVELS = [AlertLevel.Info, AlertLevel.Warning, AlertLevel.Error, AlertLevel.Critical]
 _CTX = {DeviceEventIndex.Assignment: 0, DeviceEventIndex.Customer: 2, DeviceEventIndex.Area: 3,
         DeviceEventIndex.Asset: 4}
@@ -728,13 +733,6 @@ class DurableEventStore(DeviceEventStore):
                 block_cache_bytes = int(min(32 << 30, ram // 8))
         self.seg.mem_caps(-1, int(block_cache_bytes))
         self._tl = threading.local()
-        # events added through the API (REST / RPC adds, command invocations and responses, rule and
-        # presence alerts): a checksummed JSON-lines log, fdatasync'd before the add returns, replayed
-        # into the in-memory indexes on open
-        self._objects = MemoryEventStore()
-        self._api_path = os.path.join(directory, f"api-{rank}.log")
-        self._load_api_log()
-        self._api_f = open(self._api_path, "ab")
         self._asg: dict[int, dict[int, list]] = {}       # boot -> assignment index -> [asg, dev, cust, area, asset]
         self._names: dict[int, dict[int, str]] = {}      # boot -> name id -> name
         self._ctx: dict[int, dict[int, dict]] = {}       # boot -> dimension -> context token -> engine id
@@ -763,14 +761,56 @@ class DurableEventStore(DeviceEventStore):
         self.max_maps = 16384
         self._tabs = None
         self.scan_threads = int(os.environ.get("SW_STORE_SCAN_THREADS", "16"))
+        # events added through the API (REST / RPC adds, command invocations and responses, rule
+        # alerts): rows of blocks like the engine's (api_blocks.py).  Until a block holds them they
+        # are the tail: in memory and in a short checksummed log, fdatasync'd before the add returns
+        self.api_flush_events = int(os.environ.get("SW_API_FLUSH_EVENTS", 65536))
+        self.api_flush_s = float(os.environ.get("SW_API_FLUSH_S", 1.0))
+        self._api_lock = threading.Lock()
+        self._api_flush_mu = threading.Lock()
+        self._api_boot = self._load_api_boot(directory, rank)
+        self._api_next = self._high.get((self._api_boot, 0), 0)
+        self._api_tail: list = []                         # (sequence, event), in sequence order
+        self._objects = MemoryEventStore()                # the tail's events, indexed
+        self._api_dic = None
+        self._api_path = os.path.join(directory, f"api-{rank}.log")
+        self._load_api_log()
+        self._api_f = open(self._api_path, "ab")
+        self._api_stop = threading.Event()
+        self._api_kick = threading.Event()
+        self._api_err: str | None = None
+        self._api_th = threading.Thread(target=self._api_flush_loop, name="api-blocks", daemon=True)
+        self._api_th.start()
 
     # ------------------------------------------------------------------ API-added events
+    @staticmethod
+    def _load_api_boot(directory: str, rank: int) -> int:
+        """The store's API boot: the engine-incarnation id API-added events are stored under, fixed
+        for the directory (so their ids and dictionaries continue across restarts).  Bit 52 keeps it
+        apart from engine boots (millisecond timestamps)."""
+        path = os.path.join(directory, f"api-boot-{rank}")
+        try:
+            with open(path) as f:
+                return int(f.read().strip(), 16)
+        except (OSError, ValueError):
+            pass
+        boot = (1 << 52) | int(time.time() * 1000)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(f"{boot:x}\n")
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+        return boot
+
     def _load_api_log(self):
-        """Replay ``api-<rank>.log``: ``<crc32 hex> <event json>`` per line.  A torn or corrupt tail
-        (a crash mid-write: the add never returned) is cut off so later appends follow good data."""
+        """Replay ``api-<rank>.log`` (``<crc32 hex> {"s": sequence, "e": event}`` per line): events a
+        block already holds are skipped, the rest are the tail.  A torn or corrupt tail (a crash
+        mid-write: the add never returned) is cut off; lines of older logs without a sequence get one."""
         if not os.path.exists(self._api_path):
             return
-        good, events = 0, []
+        good, tail, renumbered = 0, [], False
+        covered = self._high.get((self._api_boot, 0), 0)
         with open(self._api_path, "rb") as f:
             for line in f:
                 if not line.endswith(b"\n") or len(line) < 10 or line[8:9] != b" ":
@@ -779,31 +819,136 @@ class DurableEventStore(DeviceEventStore):
                 try:
                     if int(line[:8], 16) != zlib.crc32(body):
                         break
-                    events.append(event_from_dict(json.loads(body)))
-                except ValueError:
+                    d = json.loads(body)
+                    if "s" in d and "e" in d:
+                        seq, ev = int(d["s"]), event_from_dict(d["e"])
+                    else:                                  # a line of an older log: no sequence yet
+                        seq, ev, renumbered = -1, event_from_dict(d), True
+                except (ValueError, KeyError, TypeError):
                     break
                 good += len(line)
-        if good < os.path.getsize(self._api_path):
-            with open(self._api_path, "r+b") as f:
-                f.truncate(good)
-                os.fsync(f.fileno())
-        self._objects.add_events(events)
+                if seq < 0:
+                    seq = max(self._api_next, covered)
+                    ev.id = f"{self._api_boot:x}-{seq}"
+                if seq >= covered:
+                    tail.append((seq, ev))
+                self._api_next = max(self._api_next, seq + 1, covered)
+        tail.sort(key=lambda x: x[0])
+        self._api_tail = tail
+        self._objects.add_events([e for _, e in tail])
+        if good < os.path.getsize(self._api_path) or renumbered or len(tail) == 0:
+            self._rewrite_api_log(tail)
+
+    @staticmethod
+    def _api_line(seq: int, e) -> bytes:
+        body = json.dumps({"s": seq, "e": e.to_dict()}, separators=(",", ":")).encode()
+        return b"%08x %s\n" % (zlib.crc32(body), body)
+
+    def _rewrite_api_log(self, tail):
+        """Replace the log by the tail's lines (a new file, fsync'd, renamed over the old one)."""
+        tmp = self._api_path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(b"".join(self._api_line(s_, e) for s_, e in tail))
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self._api_path)
+        dfd = os.open(os.path.dirname(os.path.abspath(self._api_path)), os.O_RDONLY)
+        try:
+            os.fsync(dfd)
+        finally:
+            os.close(dfd)
 
     def add_events(self, events):
-        """Durable API add: the events are on disk (one fdatasync per call) before they are indexed
-        and the call returns."""
+        """Durable API add: the store gives each event its id (``<api boot hex>-<sequence>``), the
+        events are on disk (one fdatasync per call) and visible before the call returns; a block
+        holds them once the tail is flushed (see api_blocks.py)."""
         if not events:
             return events
-        lines = []
-        for e in events:
-            body = json.dumps(e.to_dict(), separators=(",", ":")).encode()
-            lines.append(b"%08x %s\n" % (zlib.crc32(body), body))
-        with self._lock:
+        now = int(time.time() * 1000)
+        with self._api_lock:
+            lines = []
+            for e in events:
+                seq = self._api_next
+                self._api_next += 1
+                e.id = f"{self._api_boot:x}-{seq}"
+                if e.received_date is None:
+                    e.received_date = now
+                lines.append(self._api_line(seq, e))
+                self._api_tail.append((seq, e))
             self._api_f.write(b"".join(lines))
             self._api_f.flush()
             os.fdatasync(self._api_f.fileno())
             self._objects.add_events(events)
+            if len(self._api_tail) >= self.api_flush_events:
+                self._api_kick.set()
         return events
+
+    def _api_flush_loop(self):
+        while not self._api_stop.is_set():
+            self._api_kick.wait(self.api_flush_s)
+            self._api_kick.clear()
+            if self._api_stop.is_set():
+                break
+            try:
+                self.flush_api()
+            except Exception as e:  # noqa: BLE001 -- the tail stays in the log; retried next round
+                self._api_err = f"{type(e).__name__}: {e}"
+
+    def _api_dictionary(self):
+        from .api_blocks import ApiDictionary
+        if self._api_dic is None:
+            b = self._api_boot
+            with self._lock:
+                self._api_dic = ApiDictionary(self._asg.get(b, {}), self._names.get(b, {}),
+                                              {d: dict(m) for d, m in self._ctx.get(b, {}).items()})
+        return self._api_dic
+
+    def flush_api(self, max_rows: int = 1 << 20) -> int:
+        """Encode the tail into blocks (index trailers included), make them durable, then cut the
+        tail and the log back to what came after.  Returns the events flushed."""
+        from .api_blocks import encode_events
+        with self._api_flush_mu:
+            with self._api_lock:
+                batch = list(self._api_tail)
+            if not batch:
+                return 0
+            dic = self._api_dictionary()
+            for i in range(0, len(batch), max_rows):
+                chunk = batch[i:i + max_rows]
+                evs = [e for _, e in chunk]
+                rows, recs, spans, raw = encode_events(evs, dic)
+                blk = encode_block(rows, recs, spans, raw, index=True, ctx=dic.ctx_table())
+                recv = max(int(e.received_date or 0) for e in evs)
+                seal(blk, chunk[0][0], recv, self._api_boot, 0, 1)
+                d_asg, d_names, d_ctx = dic.take_delta()
+                tok = self.add_block(_p(blk), len(blk), blk, boot=self._api_boot, asg=d_asg, names=d_names,
+                                     ctx=d_ctx)
+                if tok >= 0 and not self.wait(tok):
+                    raise TimeoutError("API event block not durable in time")
+            upto = batch[-1][0] + 1
+            with self._api_lock:
+                rest = [(s_, e) for s_, e in self._api_tail if s_ >= upto]
+                objs = MemoryEventStore()
+                objs.add_events([e for _, e in rest])
+                self._api_tail, self._objects = rest, objs
+                self._api_f.close()
+                self._rewrite_api_log(rest)
+                self._api_f = open(self._api_path, "ab")
+            return len(batch)
+
+    def _api_covered(self, tabs) -> int:
+        """The API boot's sequences that blocks in ``tabs`` hold (events below it left the tail)."""
+        t = tabs.get(self._api_boot)
+        if t is None or not t["n"]:
+            return 0
+        return int((t["ents"]["first_seq"].astype(np.int64) + t["ents"]["n_rows"].astype(np.int64)).max())
+
+    def _api_seq(self, ev) -> int:
+        b, _, n = (ev.id or "").rpartition("-")
+        try:
+            return int(n) if int(b, 16) == self._api_boot else -1
+        except ValueError:
+            return -1
 
     # ------------------------------------------------------------------ dictionaries
     def _load_dict(self):
@@ -954,6 +1099,13 @@ class DurableEventStore(DeviceEventStore):
         return self.seg.flush(timeout_s)
 
     def close(self):
+        self._api_stop.set()
+        self._api_kick.set()
+        self._api_th.join(timeout=30)
+        try:
+            self.flush_api()                           # the tail into a block: a short restart
+        except Exception:  # noqa: BLE001 -- it stays in the log
+            pass
         self._tabs = None
         self._tmaps.clear()
         self.seg.close()
@@ -1337,6 +1489,17 @@ class DurableEventStore(DeviceEventStore):
     def count(self) -> int:
         return self.rows + self._objects.count()
 
+    @property
+    def api_boot(self) -> int:
+        """The boot API-added events are stored under (see :meth:`add_events`)."""
+        return self._api_boot
+
+    @property
+    def engine_rows(self) -> int:
+        """Rows on disk that engines wrote (API-added events' blocks excluded)."""
+        ents = self.seg.index()
+        return int(ents["n_rows"][ents["boot"].astype(np.int64) != self._api_boot].sum())
+
     @staticmethod
     def _eids(h, idx) -> np.ndarray:
         return (int(h["first_seq"]) + np.asarray(idx, np.int64)) * int(h["world"]) + int(h["rank"])
@@ -1347,8 +1510,9 @@ class DurableEventStore(DeviceEventStore):
             b = int(boot, 16)
         except ValueError:
             b = None
-        if not (sep and num.isdigit()) or b is None:
-            return self._objects.get_event_by_id(id)
+        ev = self._objects.get_event_by_id(id)     # the API tail first: it leaves only once a block holds it
+        if ev is not None or not (sep and num.isdigit()) or b is None:
+            return ev
         eid = int(num)
         ents = self.seg.index()
         if len(ents) and eid < (1 << 62):
@@ -1362,10 +1526,23 @@ class DurableEventStore(DeviceEventStore):
                 e = ents[int(hit[0])]
                 c, i = self._row_event(e, int(row[int(hit[0])]))
                 return self._materialize(c, i)
-        return self._objects.get_event_by_id(id)
+        return None
 
     def list_command_responses_for_invocation(self, invocation_id, criteria=None):
-        return self._objects.list_command_responses_for_invocation(invocation_id, criteria)
+        """Responses to an invocation, newest first: the tail's, and the blocks' response rows of the
+        invocation's assignment (the assignment index) whose originating event is the invocation."""
+        c = criteria or DateRangeSearchCriteria(page_size=100)
+        tail = self._objects.list_command_responses_for_invocation(invocation_id, DateRangeSearchCriteria(
+            page_size=0)).results
+        inv = self.get_event_by_id(invocation_id)
+        got = {e.id: e for e in tail}
+        if inv is not None and inv.device_assignment_id:
+            for e in self.list_events(DeviceEventType.CommandResponse, DeviceEventIndex.Assignment,
+                                      [inv.device_assignment_id], DateRangeSearchCriteria(page_size=0)).results:
+                if getattr(e, "originating_event_id", None) == invocation_id:
+                    got.setdefault(e.id, e)
+        out = sorted(got.values(), key=lambda ev: -(ev.event_date or 0))
+        return SearchResults(len(out), c.slice(out))
 
     # ------------------------------------------------------------------ native point reads
     def _file_fds(self, files: np.ndarray):
@@ -1701,6 +1878,10 @@ class DurableEventStore(DeviceEventStore):
         total = len(objs)
         found = []                                    # (dates, eids, block positions, rows, table)
         tabs = self._boot_tables()
+        covered = self._api_covered(tabs)             # tail events a block now holds: counted there
+        if covered and objs:
+            objs = [e for e in objs if self._api_seq(e) < 0 or self._api_seq(e) >= covered]
+            total = len(objs)
         t1 = clock()
         ph["tables"] = t1 - t0
         for b, t in tabs.items():
@@ -1791,6 +1972,9 @@ def materialize_row(cols: dict, i: int, asg: dict, names: dict, rules: dict):
     et = int(cols["etype"][i])
     nid = int(cols["name"][i])
     name = names.get(nid, "") if nid != NO_NAME else ""
+    if f & SEGF_JSON:                 # an API-added invocation / response / state change (api_blocks.py)
+        from .api_blocks import event_from_json_row
+        return event_from_json_row(et, json.loads(_str(cols, i, 2) or b"{}"), base)
     if et == EV_MEASUREMENT:
         return DeviceMeasurement(name=name, value=float(cols["v0"][i]), **base)
     if et == EV_LOCATION:
@@ -1798,7 +1982,7 @@ def materialize_row(cols: dict, i: int, asg: dict, names: dict, rules: dict):
                               elevation=float(cols["v2"][i]) if f & SEGF_HAS_ELEV else None, **base)
     if et == EV_ALERT:
         gen = bool(f & SEGF_GEN)
-        return DeviceAlert(source=AlertSource.System if gen else AlertSource.Device,
+        return DeviceAlert(source=AlertSource.System if gen or f & SEGF_SYS else AlertSource.Device,
                            level=_LEVELS[min(int(cols["level"][i]), 3)], type=name,
                            message=(rules.get(name) or "") if gen else msg, **base)
     # the engine's state changes are its presence scan (DevicePresenceManager.java:110-200)

@@ -477,12 +477,13 @@ def test_gpu_tenant_checkpoint_resume_replays_exactly(tmp_path):
         assert wait_until(lambda: ib.engine.stats_dict()["persisted"] == 100, 20)
         assert ib.checkpoints == 2                       # after batches 2 and 4; batch 5 not yet covered
         store = inst.tenant_engine("event-management", "ck").store
-        assert wait_until(lambda: store.rows == 100, 20)      # stored (on disk) on the store thread
+        # stored (on disk) on the store thread; the store also holds the dataset's API-added events
+        assert wait_until(lambda: getattr(store, "engine_rows", store.rows) == 100, 20)
         ib._since_ckpt = 0                               # "crash": no final snapshot on stop
         ib2 = reconfigure(2)
         assert ib2 is not ib
         assert wait_until(lambda: ib2.engine.stats_dict()["persisted"] == 100, 20)   # 80 restored + 20 replayed
-        assert store.rows == 100                         # the replayed batch was not stored twice
+        assert getattr(store, "engine_rows", store.rows) == 100      # the replayed batch was not stored twice
         em = inst.api("DeviceEventManagement", "ck")
         res = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id], {"pageSize": 0}))
         vals = sorted(m.value for m in res.results)
@@ -538,7 +539,7 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records(zero_copy_rows
             rec = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1)
             recs.append(rec)
             rec.publish(bus, topic, 0, ts=1_700_000_500_000 + b)
-        assert wait_until(lambda: store.rows == 1600, 60), store.rows
+        assert wait_until(lambda: getattr(store, "engine_rows", store.rows) == 1600, 60), store.rows
         assert wait_until(lambda: bus.committed(ib.raw_consumer.group, topic, 0) == bus.end_offset(topic, 0), 30)
         assert not ib.engine.framed_pending and not ib._stepped and not ib._holds.get((topic, 0))
         seen = []
