@@ -389,6 +389,33 @@ class MqttClient:
         if not done.wait(timeout):
             raise TimeoutError("PUBACK not received" if qos == 1 else "PUBCOMP not received")
 
+    def publish_many(self, msgs, qos: int = 0, retain: bool = False, timeout: float = 5.0):
+        """Publish [(topic, payload)]: QoS 0 packets go out in one write; QoS 1 / 2 are all put
+        in flight before any acknowledgement is awaited (a batch costs one round trip, not one
+        per message)."""
+        qos = parse_qos(qos)
+        if not qos:
+            self._send(b"".join(publish_packet(t, p, 0, retain=retain) for t, p in msgs))
+            return
+        waits, pkts = [], []
+        with self._lock:
+            for t, p in msgs:
+                pid = self._next_pid()
+                pkt = publish_packet(t, p, qos, pid, retain)
+                done = threading.Event()
+                self._out[pid] = ["puback" if qos == 1 else "pubrec", pkt, done]
+                waits.append(done)
+                pkts.append(pkt)
+        try:
+            self._send(b"".join(pkts))
+        except OSError:
+            if not self.reconnect:
+                raise
+        end = time.monotonic() + timeout
+        for w in waits:
+            if not w.wait(max(0.0, end - time.monotonic())):
+                raise TimeoutError("PUBACK not received" if qos == 1 else "PUBCOMP not received")
+
     @property
     def inflight(self) -> int:
         return len(self._out)

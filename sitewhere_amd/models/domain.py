@@ -89,7 +89,12 @@ def _hints(cls):
     return h
 
 
+_PLAIN = (str, int, float, bool, type(None))
+
+
 def _ser(v):
+    if type(v) in _PLAIN:
+        return v
     if isinstance(v, Model):
         return v.to_dict()
     if isinstance(v, enum.Enum):

@@ -46,6 +46,7 @@ class EnrichedBatchReader:
         self._names: dict[int, dict] = {}        # boot -> name id -> name
         self._rules: dict[str, str] = {}
         self._lock = threading.Lock()
+        self._masks: dict = {}                    # (boot, field, value) -> (bool per assignment, entries seen)
         self.rows = self.batches = self.resolved = 0
 
     # ------------------------------------------------------------------ dictionaries
@@ -97,6 +98,35 @@ class EnrichedBatchReader:
         self.batches += 1
         self.rows += len(cols["date"])
         return cols
+
+    def attr_mask(self, cols: dict, pos: int, value) -> np.ndarray:
+        """bool per row of ``cols``: does the row's assignment context field ``pos`` (0 assignment,
+        1 device, 2 customer, 3 area, 4 asset, 5 device token, 6 device type) equal ``value``?  The
+        per-assignment answer is cached for the batch's engine incarnation and rebuilt only when its
+        dictionary has grown -- a filter costs one gather per batch, not a Python call per row."""
+        boot = int(cols["header"]["boot"])
+        key = (boot, pos, value)
+        with self._lock:
+            a = self._asg.get(boot, {})
+            m, seen = self._masks.get(key, (None, -1))
+            if m is None or seen != len(a):
+                n = (max(a) + 1) if a else 0
+                m = np.zeros(n, bool)
+                for i, ctx in a.items():
+                    if len(ctx) > pos and ctx[pos] == value:
+                        m[i] = True
+                self._masks[key] = (m, len(a))
+        asg = np.asarray(cols["asg"], np.int64)
+        ok = (asg >= 0) & (asg < len(m))
+        out = np.zeros(len(asg), bool)
+        out[ok] = m[asg[ok]]
+        return out
+
+    def name_ids(self, cols: dict, name: str) -> list[int]:
+        """The batch incarnation's name ids of ``name`` (measurement name / alert type)."""
+        boot = int(cols["header"]["boot"])
+        with self._lock:
+            return [int(i) for i, v in self._names.get(boot, {}).items() if v == name]
 
     def context(self, cols: dict, i: int) -> dict:
         """Enrichment context of row i (``OutboundPayloadEnrichmentLogic``: device and assignment)."""

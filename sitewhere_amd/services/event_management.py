@@ -104,6 +104,25 @@ class DeviceEventManagement:
                                                level=AlertLevel(r.get("level", "Info")), type=r.get("type", ""),
                                                message=r.get("message", "")))
 
+    def add_alert_batch(self, pairs) -> int:
+        """Alerts of many assignments in one durable add: ``pairs`` = [(assignment id, alert request)]
+        (what a rule processor raises over one engine batch).  Requests carrying an alternate id go
+        through the idempotent per-assignment path."""
+        out, ctx = [], {}
+        for aid, r in pairs:
+            if r.get("alternateId"):
+                self.add_alerts(aid, r)
+                continue
+            a = ctx.get(aid)
+            if a is None:
+                a = ctx[aid] = self._context(aid)
+            out.append(self._stamp(DeviceAlert(source=AlertSource(r.get("source", "Device")),
+                                               level=AlertLevel(r.get("level", "Info")), type=r.get("type", ""),
+                                               message=r.get("message", "")), a, r))
+        if out:
+            self._persist(out)
+        return len(pairs)
+
     def add_command_invocations(self, assignment_id: str, *requests):
         return self._add(assignment_id, _flat(requests),
                          lambda r: DeviceCommandInvocation(initiator=r.get("initiator", "REST"),

@@ -16,6 +16,8 @@ import os
 import threading
 import urllib.request
 
+import numpy as np
+
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..edges.mqtt import MQTT_OPTIONS, client_from_config, parse_qos
 from ..runtime.consumers import BusConsumer
@@ -31,6 +33,9 @@ class OutboundConnector(TenantEngineLifecycleComponent):
         self.filters = filters or []
         self.delivered = 0
         self.filtered = 0
+        self.threads = 0                          # numProcessingThreads: deliveries of a batch in parallel
+        self._pool = None
+        self._count_lock = threading.Lock()
 
     def accept(self, ev, ctx) -> bool:
         return not any(f(ev, ctx) for f in self.filters)
@@ -39,8 +44,59 @@ class OutboundConnector(TenantEngineLifecycleComponent):
         keep = [(ev, ctx) for ev, ctx in items if self.accept(ev, ctx)]
         self.filtered += len(items) - len(keep)
         if keep:
-            self.deliver(keep)
-            self.delivered += len(keep)
+            self._deliver_all(keep)
+
+    def process_records(self, reader, recs):
+        """A poll of enriched records.  Engine batches are filtered on their columns (area /
+        device type / event type: one vectorised mask per batch) and only the rows that pass are
+        materialized; per-event records and filters without a column form (scripts) go event by
+        event.  Delivery of what passes runs on the connector's pool (``numProcessingThreads``)."""
+        from .enriched_batches import is_batch
+        keep, single = [], []
+        for r in recs:
+            if not is_batch(r.value):
+                single.append(r)
+                continue
+            cols = reader.columns(r.value)
+            n = len(cols["date"])
+            excl = np.zeros(n, bool)
+            per_row = []
+            for f in self.filters:
+                m = f.exclude(cols, reader) if hasattr(f, "exclude") else None
+                if m is None:
+                    per_row.append(f)
+                else:
+                    excl |= m
+            rows = np.nonzero(~excl)[0]
+            items = [(reader.event(cols, int(i)), reader.context(cols, int(i))) for i in rows]
+            if per_row:
+                items = [(ev, ctx) for ev, ctx in items if not any(f(ev, ctx) for f in per_row)]
+            self.filtered += n - len(items)
+            keep.extend(items)
+        if single:
+            from .enriched_batches import expand_records
+            items = expand_records(reader, single)
+            passed = [(ev, ctx) for ev, ctx in items if self.accept(ev, ctx)]
+            self.filtered += len(items) - len(passed)
+            keep.extend(passed)
+        if keep:
+            self._deliver_all(keep)
+
+    def _deliver_all(self, items):
+        if self._pool is None or len(items) < 2 * max(1, self.threads):
+            self.deliver(items)
+        else:
+            step = -(-len(items) // self.threads)
+            for f in [self._pool.submit(self.deliver, items[i:i + step]) for i in range(0, len(items), step)]:
+                f.result()
+        with self._count_lock:
+            self.delivered += len(items)
+
+    def set_threads(self, n: int):
+        from concurrent.futures import ThreadPoolExecutor
+        self.threads = max(0, int(n))
+        self._pool = ThreadPoolExecutor(self.threads, thread_name_prefix=f"connector-{self.cid}") \
+            if self.threads > 1 else None
 
     def deliver(self, items):
         """Default: serial per-event dispatch (SerialOutboundConnector)."""
@@ -81,10 +137,18 @@ class MqttConnector(OutboundConnector):
     def start(self, monitor):
         self.client = client_from_config(dict(self.mqtt, host=self.host, port=self.port), reconnect=True).connect()
 
+    def _topic(self, ev, ctx):
+        return self.topic.format(tenant=self.tenant_engine.tenant.token, deviceToken=ctx.get("deviceToken"),
+                                 eventType=ev.event_type.value)
+
     def on_event(self, ev, ctx):
-        t = self.topic.format(tenant=self.tenant_engine.tenant.token, deviceToken=ctx.get("deviceToken"),
-                              eventType=ev.event_type.value)
-        self.client.publish(t, json.dumps(event_json(ev, ctx)).encode(), qos=self.qos)
+        self.client.publish(self._topic(ev, ctx), json.dumps(event_json(ev, ctx)).encode(), qos=self.qos)
+
+    def deliver(self, items):
+        """A batch's events in one write (QoS 0) / with their acknowledgements awaited together."""
+        for i in range(0, len(items), 1024):
+            self.client.publish_many([(self._topic(ev, ctx), json.dumps(event_json(ev, ctx)).encode())
+                                      for ev, ctx in items[i:i + 1024]], qos=self.qos)
 
     def stop(self, monitor):
         if self.client:
@@ -156,41 +220,96 @@ class ScriptConnector(OutboundConnector):
         self.tenant_engine.ms.scripts.call(self.source, "process", ev.to_dict(), ctx, name=f"connector-{self.cid}")
 
 
+class _Filter:
+    """A connector filter (``FilteredOutboundConnector``): ``f(ev, ctx)`` is True for an event to
+    leave out; ``exclude(cols, reader)`` is the same test over an engine batch's columns (a bool per
+    row), or None where the filter has no column form."""
+    op = "include"
+
+    def _out(self, hit):
+        return ~hit if self.op == "include" else hit
+
+    def exclude(self, cols, reader):
+        return None
+
+
+class AreaFilter(_Filter):
+    """``connectors/filter/AreaFilter.java``: events of (or not of) one area."""
+
+    def __init__(self, engine, token: str, op: str):
+        self.engine, self.token, self.op = engine, token, op
+        self._id = None
+
+    def area_id(self):
+        if self._id is None:
+            a = self.engine.ms.api("DeviceManagement", self.engine.tenant.token).get_area_by_token(self.token)
+            self._id = (a.id if a else None,)
+        return self._id[0]
+
+    def __call__(self, ev, ctx):
+        hit = ev.area_id == self.area_id()
+        return (not hit) if self.op == "include" else hit
+
+    def exclude(self, cols, reader):
+        return self._out(reader.attr_mask(cols, 3, self.area_id()))
+
+
+class DeviceTypeFilter(_Filter):
+    """``connectors/filter/DeviceTypeFilter.java``: events of devices of (or not of) one type."""
+
+    def __init__(self, engine, token: str, op: str):
+        self.engine, self.token, self.op = engine, token, op
+        self._id = None
+
+    def type_id(self):
+        if self._id is None:
+            d = self.engine.ms.api("DeviceManagement", self.engine.tenant.token).get_device_type_by_token(self.token)
+            self._id = (d.id if d else None,)
+        return self._id[0]
+
+    def __call__(self, ev, ctx):
+        hit = ctx.get("deviceTypeId") == self.type_id()
+        return (not hit) if self.op == "include" else hit
+
+    def exclude(self, cols, reader):
+        return self._out(reader.attr_mask(cols, 6, self.type_id()))
+
+
+class EventTypeFilter(_Filter):
+    def __init__(self, types):
+        from ..persistence.api_blocks import _ETYPE
+        from ..models.domain import DeviceEventType
+        self.types = set(types)
+        self.codes = np.array(sorted(_ETYPE[DeviceEventType(t)] for t in self.types), np.uint8)
+
+    def __call__(self, ev, ctx):
+        return ev.event_type.value not in self.types
+
+    def exclude(self, cols, reader):
+        return ~np.isin(np.asarray(cols["etype"]), self.codes)
+
+
+class ScriptFilter(_Filter):
+    def __init__(self, engine, src):
+        self.engine, self.src = engine, src
+
+    def __call__(self, ev, ctx):
+        return bool(self.engine.ms.scripts.call(self.src, "filter", ev.to_dict(), ctx, name="connector-filter"))
+
+
 def build_filters(engine, cfgs) -> list:
     out = []
     for f in cfgs or []:
         t = f.get("type")
         op = f.get("operation", "include")
         if t == "area":
-            want = f["areaToken"]
-            dm = lambda: engine.ms.api("DeviceManagement", engine.tenant.token)  # noqa: E731
-            area_id = {}
-
-            def area_filter(ev, ctx, want=want, op=op):
-                if "id" not in area_id:
-                    a = dm().get_area_by_token(want)
-                    area_id["id"] = a.id if a else None
-                hit = ev.area_id == area_id["id"]
-                return (not hit) if op == "include" else hit
-            out.append(area_filter)
+            out.append(AreaFilter(engine, f["areaToken"], op))
         elif t == "device-type":
-            want = f["deviceTypeToken"]
-            cache = {}
-
-            def dt_filter(ev, ctx, want=want, op=op):
-                if "id" not in cache:
-                    d = engine.ms.api("DeviceManagement", engine.tenant.token).get_device_type_by_token(want)
-                    cache["id"] = d.id if d else None
-                hit = ctx.get("deviceTypeId") == cache["id"]
-                return (not hit) if op == "include" else hit
-            out.append(dt_filter)
+            out.append(DeviceTypeFilter(engine, f["deviceTypeToken"], op))
         elif t == "event-type":
-            types = set(f["eventTypes"])
-            out.append(lambda ev, ctx, types=types: ev.event_type.value not in types)
+            out.append(EventTypeFilter(f["eventTypes"]))
         elif t == "script":
-            src = engine.script_source(f["script"])
-            out.append(lambda ev, ctx, src=src: bool(engine.ms.scripts.call(src, "filter", ev.to_dict(), ctx,
-                                                                            name="connector-filter")))
+            out.append(ScriptFilter(engine, engine.script_source(f["script"])))
     return out
 
 
@@ -227,21 +346,21 @@ class OutboundConnectorsTenantEngine(MicroserviceTenantEngine):
         for cc in self.config.get("connectors", []):
             c = build_connector(self, cc)
             c.tenant_engine = self
+            c.set_threads(int(cc.get("numProcessingThreads", 0)))
             self.initialize_nested_component(c, monitor, require=False)
             self.connectors.append(c)
             reader = EnrichedBatchReader(self)
             self.readers.append(reader)
-            self.hosts.append(BusConsumer(self, f"connector.{c.cid}", topics, self._handler(c, reader),
-                                          threads=int(cc.get("numProcessingThreads", 0))))
+            # the connector's pool delivers a poll's events (engine batches are single records: a
+            # per-record split would leave one thread busy)
+            self.hosts.append(BusConsumer(self, f"connector.{c.cid}", topics, self._handler(c, reader)))
         self.api = {"OutboundConnectors": OutboundConnectorsApi(self)}
 
     @staticmethod
     def _handler(c, reader):
-        from .enriched_batches import expand_records
-
         def handle(recs):
             # processed before the consumer commits (at-least-once; the reference commits first)
-            c.process_batch(expand_records(reader, recs))
+            c.process_records(reader, recs)
         return handle
 
     def tenant_start(self, monitor):

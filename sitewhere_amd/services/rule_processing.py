@@ -9,8 +9,10 @@ processor; the zone test batches its point-in-polygon work onto the GPU when ava
 """
 from __future__ import annotations
 
+import numpy as np
 
 from ..core.geo import batch_contains, polygon_of
+from ..models.columnar import EV_LOCATION, EV_MEASUREMENT
 from ..core.lifecycle import LifecycleComponentType, TenantEngineLifecycleComponent
 from ..models.domain import DeviceEventType
 from ..runtime.consumers import BusConsumer
@@ -24,6 +26,32 @@ class RuleProcessor(TenantEngineLifecycleComponent):
     def __init__(self, pid: str):
         super().__init__(f"rule:{pid}")
         self.pid = pid
+        self.alerts = 0
+
+    def process_records(self, reader, recs):
+        """A poll of enriched records: per-event records and engine batches (every row as an
+        event).  Column-capable processors override :meth:`process_columns` for batches."""
+        from .enriched_batches import expand_records, is_batch
+        single = []
+        for r in recs:
+            if is_batch(r.value) and type(self).process_columns is not RuleProcessor.process_columns:
+                self.process_columns(reader, reader.columns(r.value, strings=self.column_strings))
+            else:
+                single.append(r)
+        if single:
+            self.process_batch(expand_records(reader, single))
+
+    column_strings = False        # the column forms read numbers and dictionaries, not the string heap
+
+    def process_columns(self, reader, cols):
+        """An engine batch as columns (``EnrichedBatchReader.columns``); default: row by row."""
+        self.process_batch([(reader.event(cols, i), reader.context(cols, i)) for i in range(len(cols["date"]))])
+
+    def raise_alerts(self, pairs):
+        """Alerts of one batch in one durable add (``DeviceEventManagement.add_alert_batch``)."""
+        if pairs:
+            self.events_api().add_alert_batch(pairs)
+            self.alerts += len(pairs)
 
     def process_batch(self, items: list[tuple]):
         for ev, ctx in items:
@@ -70,15 +98,34 @@ class ZoneTestRuleProcessor(RuleProcessor):
             return
         polys = [self._poly(t["zoneToken"]) for t in self.tests]
         inside = batch_contains(polys, [(ev.latitude, ev.longitude) for ev, _ in locs])
-        api = self.events_api()
-        for i, (ev, _) in enumerate(locs):
-            for j, t in enumerate(self.tests):
-                if (t.get("condition", "inside") == "inside") == bool(inside[i, j]):
-                    api.add_alerts(ev.device_assignment_id, {"type": t.get("alertType", "zone.alert"),
-                                                             "level": t.get("alertLevel", "Warning"),
-                                                             "message": t.get("alertMessage", ""),
-                                                             "source": "System", "updateState": False})
-                    self.alerts += 1
+        self.raise_alerts([(ev.device_assignment_id, self._request(t))
+                           for i, (ev, _) in enumerate(locs) for j, t in enumerate(self.tests)
+                           if (t.get("condition", "inside") == "inside") == bool(inside[i, j])])
+
+    @staticmethod
+    def _request(t):
+        return {"type": t.get("alertType", "zone.alert"), "level": t.get("alertLevel", "Warning"),
+                "message": t.get("alertMessage", ""), "source": "System", "updateState": False}
+
+    def process_columns(self, reader, cols):
+        """Location rows of an engine batch: one point-in-polygon pass over their columns, alerts
+        for the hits in one add."""
+        if not self.tests:
+            return
+        rows = np.nonzero(np.asarray(cols["etype"]) == EV_LOCATION)[0]
+        if not len(rows):
+            return
+        polys = [self._poly(t["zoneToken"]) for t in self.tests]
+        inside = batch_contains(polys, np.stack([cols["v0"][rows], cols["v1"][rows]], 1))
+        ctx = cols["asg_ctx"]
+        pairs = []
+        for j, t in enumerate(self.tests):
+            want = t.get("condition", "inside") == "inside"
+            for i in np.nonzero(inside[:, j] == want)[0].tolist():
+                a = ctx.get(int(cols["asg"][rows[i]]))
+                if a:
+                    pairs.append((a[0], self._request(t)))
+        self.raise_alerts(pairs)
 
 
 class ThresholdRuleProcessor(RuleProcessor):
@@ -89,16 +136,48 @@ class ThresholdRuleProcessor(RuleProcessor):
         self.rules = rules
         self.alerts = 0
 
-    def on_measurement(self, ctx, ev):
+    @staticmethod
+    def _request(r, name, value):
+        lo, hi = r.get("min"), r.get("max")
+        return {"type": r.get("alertType", f"{name}.threshold"), "level": r.get("alertLevel", "Warning"),
+                "message": f"{name}={value} outside [{lo}, {hi}]", "source": "System"}
+
+    def process_batch(self, items):
+        pairs = []
+        for ev, ctx in items:
+            if ev.event_type != DeviceEventType.Measurement:
+                continue
+            for r in self.rules:
+                lo, hi = r.get("min"), r.get("max")
+                if r["measurement"] == ev.name and ((lo is not None and ev.value < lo) or
+                                                    (hi is not None and ev.value > hi)):
+                    pairs.append((ev.device_assignment_id, self._request(r, ev.name, ev.value)))
+        self.raise_alerts(pairs)
+
+    def process_columns(self, reader, cols):
+        """Measurement rows of an engine batch against each rule on the columns (name id and value
+        masks); only the rows out of bounds become alerts, all of the batch's in one add."""
+        et = np.asarray(cols["etype"])
+        name = np.asarray(cols["name"])
+        v = np.asarray(cols["v0"])
+        ctx = cols["asg_ctx"]
+        pairs = []
         for r in self.rules:
-            if r["measurement"] != ev.name:
+            ids = reader.name_ids(cols, r["measurement"])
+            if not ids:
                 continue
             lo, hi = r.get("min"), r.get("max")
-            if (lo is not None and ev.value < lo) or (hi is not None and ev.value > hi):
-                self.events_api().add_alerts(ev.device_assignment_id, {
-                    "type": r.get("alertType", f"{ev.name}.threshold"), "level": r.get("alertLevel", "Warning"),
-                    "message": f"{ev.name}={ev.value} outside [{lo}, {hi}]", "source": "System"})
-                self.alerts += 1
+            m = (et == EV_MEASUREMENT) & np.isin(name, np.asarray(ids, name.dtype))
+            out = np.zeros(len(v), bool)
+            if lo is not None:
+                out |= v < lo
+            if hi is not None:
+                out |= v > hi
+            for i in np.nonzero(m & out)[0].tolist():
+                a = ctx.get(int(cols["asg"][i]))
+                if a:
+                    pairs.append((a[0], self._request(r, r["measurement"], float(v[i]))))
+        self.raise_alerts(pairs)
 
 
 class ScriptedRuleProcessor(RuleProcessor):
@@ -148,10 +227,8 @@ class RuleProcessingTenantEngine(MicroserviceTenantEngine):
 
     @staticmethod
     def _handler(p: RuleProcessor, reader):
-        from .enriched_batches import expand_records
-
         def handle(recs):
-            p.process_batch(expand_records(reader, recs))
+            p.process_records(reader, recs)
         return handle
 
     def tenant_start(self, monitor):

@@ -54,11 +54,21 @@ def sw(tmp_path_factory):
                                                                 "configurationTemplateId": template,
                                                                 "datasetTemplateId": "construction"}))
         inst.wait_for_tenant(token, 60)
+        # the area of galaxytab-000's assignment: a column-filtered connector keeps that area's
+        # measurements and locations
+        run = lambda f: inst.instance.system_user.run(f, token)  # noqa: E731
+        dm = inst.api("DeviceManagement", token)
+        dev = run(lambda: dm.get_device_by_token("galaxytab-000"))
+        area = run(lambda: dm.get_area(run(lambda: dm.get_device_assignment(dev.device_assignment_id)).area_id))
+        inst.fanout_area = area.token
         coord = inst.instance.coord
         coord.put(inst.instance.tenant_conf_path(token, "outbound-connectors.json"), dump_document(
             {"connectors": [{"id": "log1", "type": "log", "filters": [{"type": "script", "script": FILTER}]},
                             {"id": "mq1", "type": "mqtt", "host": "127.0.0.1", "port": broker.port, "qos": 1,
-                             "topic": "fan/{tenant}/{eventType}", "filters": [{"type": "script", "script": FILTER}]}]}))
+                             "topic": "fan/{tenant}/{eventType}", "filters": [{"type": "script", "script": FILTER}]},
+                            {"id": "area1", "type": "log", "numProcessingThreads": 2,
+                             "filters": [{"type": "area", "areaToken": area.token},
+                                         {"type": "event-type", "eventTypes": ["Measurement", "Location"]}]}]}))
         coord.put(inst.instance.tenant_conf_path(token, "rule-processing.json"),
                   dump_document({"processors": [THRESHOLD]}))
 
@@ -66,7 +76,7 @@ def sw(tmp_path_factory):
         for token in ("pe", "eng"):
             oc = inst.tenant_engine("outbound-connectors", token)
             rp = inst.tenant_engine("rule-processing", token)
-            if not (oc is not None and rp is not None and len(oc.connectors) == 2 and rp.processors and
+            if not (oc is not None and rp is not None and len(oc.connectors) == 3 and rp.processors and
                     oc.status.value == "Started" and rp.status.value == "Started"):
                 return False
         return True
@@ -185,6 +195,17 @@ def test_engine_tenant_events_reach_connectors_and_rules_like_per_event(sw):
         return out
     for t in ("pe", "eng"):
         assert wait_until(lambda: last_alts(t) == want_last, 30), (t, last_alts(t))
+    # the column-filtered connector (area + event type: one mask per engine batch) kept the same
+    # events as the per-event filters on the reference-shaped tenant
+    a1 = {t: sw.tenant_engine("outbound-connectors", t).connectors[2] for t in ("pe", "eng")}
+
+    def area_alts(t):
+        return sorted(str(e["event"].get("alternateId")) for e in a1[t].seen
+                      if str(e["event"].get("alternateId")).startswith("f"))
+    assert wait_until(lambda: area_alts("pe") and area_alts("pe") == area_alts("eng"), 30), \
+        (area_alts("pe"), area_alts("eng"))
+    assert all(a.startswith(("fm-", "fl-")) for a in area_alts("eng"))
+    assert a1["pe"].delivered == a1["eng"].delivered and a1["pe"].filtered == a1["eng"].filtered
     # the engine's consumers resolved their dictionaries from the batches themselves
     eng_reader = sw.tenant_engine("outbound-connectors", "eng").readers[0]
     assert eng_reader.batches > 0 and eng_reader.rows >= 300
