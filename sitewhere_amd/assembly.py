@@ -10,6 +10,8 @@ services (users, tenants), then every multitenant service (each waits for tenant
 """
 from __future__ import annotations
 
+import os
+
 import time
 
 from .runtime.config import InstanceSettings
@@ -68,6 +70,13 @@ class SiteWhereInstance:
         raise KeyError(identifier)
 
     def start(self, timeout_s: float = 60.0):
+        # every microservice of the instance shares this interpreter: with the default 5 ms switch
+        # interval a thread coming back from a native call (an engine submit, a store lookup) waits
+        # up to 5 ms for a busy peer to yield.  The engine loops make many short native calls.
+        import sys
+        us = float(os.environ.get("SW_SWITCH_INTERVAL_US", "200"))
+        if us > 0:
+            sys.setswitchinterval(us / 1e6)
         if run_microservice(self.instance_management) != 0:
             raise RuntimeError(f"instance management failed: {self.instance_management.lifecycle_error}")
         for s in self.services:
