@@ -274,12 +274,34 @@ typedef struct SwCeStep {
 
 }  // extern "C"
 
+// Zeroed words from calloc: pages the filter never touches are never committed (a multi-GB filter
+// of a small tenant costs what its ids touch).
+struct LazyWords {
+  uint64_t* p = nullptr;
+  size_t n = 0;
+  LazyWords() = default;
+  LazyWords(const LazyWords&) = delete;
+  LazyWords& operator=(const LazyWords&) = delete;
+  ~LazyWords() { free(p); }
+  void assign_zero(size_t count) {
+    free(p);
+    p = count ? static_cast<uint64_t*>(calloc(count, sizeof(uint64_t))) : nullptr;
+    n = p ? count : 0;
+  }
+  bool empty() const { return n == 0; }
+  size_t size() const { return n; }
+  uint64_t* data() { return p; }
+  const uint64_t* data() const { return p; }
+  uint64_t& operator[](size_t i) { return p[i]; }
+  const uint64_t& operator[](size_t i) const { return p[i]; }
+};
+
 struct SwCpuEngine {
   Pool pool;
   std::vector<U64Map<int64_t>> dedup;       // current generation of the alternate-id window, by hash % T
   std::vector<U64Map<int64_t>> dedup_prev;  // previous generation (see the rotation in swce_process)
   int64_t dd_slots = 0, dd_batch = 0;       // window slots and the largest batch (rotation rule)
-  std::vector<uint64_t> bloom;              // store-backed dedup filter (sw_bloom_*), empty: off
+  LazyWords bloom;                          // store-backed dedup filter (sw_bloom_*), empty: off
   int64_t bloom_mask = 0;
   U64Map<int32_t> intern;
   int32_t n_intern = 0;
@@ -778,7 +800,7 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
 void swce_bloom_init(void* p, int64_t bits) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
   const int64_t blocks = bits / 64;
-  e->bloom.assign(blocks > 0 ? (size_t)blocks : 0, 0ull);
+  e->bloom.assign_zero(blocks > 0 ? (size_t)blocks : 0);
   e->bloom_mask = blocks > 0 ? blocks - 1 : 0;
 }
 

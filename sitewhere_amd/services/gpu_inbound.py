@@ -979,15 +979,16 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     # payloads are at least this many bytes on the raw topic (a delimited protobuf request carrying a
     # device token and one event): the most ids a partition's retention can redeliver
     MIN_PAYLOAD_BYTES = 24
-    # the blocked Bloom filter (8 bits of one 64-bit block per id) stays near 0.1-0.3% false positives
-    # up to one id per 16 bits, ~2.5% at one per 8
-    FILTER_BITS_PER_ID = 16
+    # the blocked Bloom filter (8 bits of one 64-bit block per id): false positives ~3e-6 at one id
+    # per 128 bits, ~3e-5 at one per 64, ~4e-3 at one per 16 (the most loaded words set the rate;
+    # each false positive is a store lookup the step's commit waits for)
+    FILTER_BITS_PER_ID = 128
 
     def check_dedup_sizing(self) -> dict:
         """Runtime check of the engine's dedup sizing (docs/PARITY.md, alternate-id dedup): the HBM
         window always holds the last ``dedup_slots / 2`` ids.  Without the store-backed filter, a raw
         topic that can redeliver more payloads than that (its retention) lets an old id through
-        again; with the filter, stored ids past ``dedup_bloom_bits / 16`` raise its false-positive
+        again; with the filter, stored ids past ``dedup_bloom_bits / 128`` raise its false-positive
         rate (host lookups, not correctness).  Logs a warning per violated rule; returns the report
         (also ``dedup_sizing_report``)."""
         c = self.engine_cfg

@@ -113,11 +113,13 @@ TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
               # alternate-id window: 2^24 slots (512 MB of HBM) hold the last 6-8M ids, so a recheck
               # never scans the blocks the store has not indexed yet
               "dedup_slots": 1 << 24, "gen_cap": 32768,
-              # store-backed dedup beyond the window: 2^32 bits (512 MB of HBM), 8 bits per id in
-              # 64-bit blocks -- false positives (each one a per-event store check on the host) stay
-              # below 1e-6 up to ~60M stored ids and below 1e-3 up to ~300M (check_dedup_sizing
-              # warns past 16 bits per id); a tenant that keeps more raises it
-              "dedup_bloom_bits": 1 << 32})
+              # store-backed dedup beyond the window: 2^34 bits (2 GB of the 288 GB of HBM), 8 bits
+              # per id in one 64-bit block (one atomic per add).  Each false positive is a store
+              # lookup on the host that the step's commit waits for, and a one-word filter's rate
+              # is set by its most loaded words: ~3e-6 at 128 bits per id (~134M stored ids here),
+              # ~5e-5 at 55 (2^32 bits at 78M ids measured ~1.3e-5: a recheck every batch, the
+              # tenant path at a tenth of its rate).  check_dedup_sizing warns past 128 bits per id.
+              "dedup_bloom_bits": 1 << 34})
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
     "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
                   "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}
