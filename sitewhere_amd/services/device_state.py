@@ -140,7 +140,9 @@ class DeviceStateManagement:
                            ("token", "device_assignment_id"))
         self._lock = threading.RLock()
         self._dates: dict[str, dict] = {}   # assignment -> {slot: event date}
-        self._engine: dict[int, _EngineStates] = {}   # engine incarnation -> column-wise states
+        # (engine incarnation, rank) -> column-wise states: ranks of one incarnation number their
+        # events apart (event id = (first_seq + row) * world + rank)
+        self._engine: dict[tuple, _EngineStates] = {}
 
     def create_device_state(self, request: dict) -> DeviceState:
         return self.states.create(request)
@@ -157,11 +159,12 @@ class DeviceStateManagement:
     def merge_batch(self, cols: dict):
         """An engine tenant's enriched batch (decoded block + dictionaries, EnrichedBatchReader):
         merged column-wise; the affected states are written on the next read."""
-        b = int(cols["header"]["boot"])
+        h = cols["header"]
+        key = (int(h["boot"]), int(h.get("rank", 0)), int(h.get("world", 1)))
         with self._lock:
-            t = self._engine.get(b)
+            t = self._engine.get(key)
             if t is None:
-                t = self._engine[b] = _EngineStates(b, cols["header"])
+                t = self._engine[key] = _EngineStates(key[0], h)
             t.merge(cols)
 
     def _sync(self):

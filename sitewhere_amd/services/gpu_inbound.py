@@ -88,7 +88,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         self.t_decoded = n.decoded_events(t)
         self.t_failed_decode = n.failed_decode_events(t)
         self.routed_payloads = 0                # payloads the slow path parsed (per payload, not per batch)
-        self.recheck_duplicates = 0             # filter rechecks the durable store knew: duplicates
+        self.recheck_duplicates = 0             # filter rechecks whose hash the durable store holds (replays)
         self.recheck_false_positives = 0        # filter rechecks the store did not know (host path)
         self._fp_win = [0, 0]                   # false positives / engine payloads since the last check
         self.dedup_sizing_report: dict = {}
@@ -1035,9 +1035,12 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
 
     def _settle_rechecks(self, res, st):
         """Ids the store-backed filter sent back (SW_ST_RECHECK): one bulk lookup in the durable
-        store's alternate-id index; those found there are duplicates (dropped, counted), the rest go
-        on to the per-event path, which stores them."""
-        from ..models.columnar import ST_DUPLICATE, ST_RECHECK
+        store's alternate-id index.  Ids the store does not hold are the filter's false positives;
+        ids whose 64-bit hash it does hold are likely replays, but a hash match is not proof (ADVICE
+        r4): both go on to the per-event path, whose alternate-id check compares the id strings
+        (``DeviceEventManagement._add``) -- a replay is dropped there, a fresh id that merely
+        collides is stored.  The lookup splits the counts: replays vs filter false positives."""
+        from ..models.columnar import ST_RECHECK
         rk = st == ST_RECHECK
         n_rk = int(rk.sum())
         n_payloads = int(getattr(res, "n_msgs", 0) or 0)
@@ -1053,13 +1056,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         # whole pipeline.  An id held only by such a block goes on to the per-event path, whose own
         # store check finds it there: still stored once.
         found = np.frombuffer(em.durable_find_alternate_hashes(h.tobytes(), indexed_only=True), np.uint64)
-        n_dup = 0
-        if len(found):
-            st = st.copy()
-            dup = rk.copy()
-            dup[rk] = np.isin(h, found)
-            st[dup] = ST_DUPLICATE
-            n_dup = int(dup.sum())
+        n_dup = int(np.isin(h, found).sum()) if len(found) else 0
         self.recheck_duplicates += n_dup
         self.recheck_false_positives += n_rk - n_dup
         self._watch_filter(n_payloads, n_rk - n_dup)

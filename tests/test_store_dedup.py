@@ -80,7 +80,9 @@ def test_replay_beyond_the_window_is_a_duplicate(sw):
     time.sleep(0.5)                                  # the host path has had time to store a second copy
     assert len(_measurements(sw, "sd-old-1")) == 1
     assert ib.engine.stats_dict()["duplicates"] == s0["duplicates"]        # the window did not see it
-    assert wait_until(lambda: ib.recheck_duplicates >= 1, 10)              # settled by the store lookup
+    # the store lookup found its hash (a replay); the per-event path compared the id strings and
+    # dropped it (a hash match alone never drops an event)
+    assert wait_until(lambda: ib.recheck_duplicates >= 1, 10)
     # a filter false positive (an id never stored but whose bits are set) is stored by the host path
     from sitewhere_amd.pipeline.fleet import hash64
     import numpy as np
