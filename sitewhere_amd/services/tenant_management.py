@@ -123,6 +123,17 @@ TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
     "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
                   "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}
+# Per-tenant device cap: gpu-columnar holds 65,536 devices and assignments (its HBM tables and
+# the host engine fallback stay small for many tenants per GPU); gpu-columnar-1m is the bench's
+# shape -- 1M devices and assignments, 1M-payload steps, state map and window sized for them
+# (a few GB of the 288 GB of HBM).  Other sizes: override ``capacity`` in the tenant's
+# inbound-processing configuration.
+TENANT_TEMPLATES["gpu-columnar-1m"] = copy.deepcopy(TENANT_TEMPLATES["gpu-columnar"])
+TENANT_TEMPLATES["gpu-columnar-1m"]["name"] = "MI355X pipeline, columnar event store, 1M devices"
+TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["inbound-processing"]["capacity"].update(
+    max_msgs=1 << 20, max_devices=(1 << 20) + 65536, max_assignments=(1 << 20) + 65536, store_cap=1 << 23,
+    gen_cap=1 << 19, state_slots=1 << 24, dedup_bloom_bits=1 << 36)
+TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["event-sources"].update(rawBatchSize=1 << 20)
 # volatile variant (benchmarks of the pipeline alone): rows kept in host memory, newest 2^28 held
 TENANT_TEMPLATES["gpu-memory"] = copy.deepcopy(TENANT_TEMPLATES["gpu-columnar"])
 TENANT_TEMPLATES["gpu-memory"]["name"] = "MI355X pipeline, in-memory columnar event store"
