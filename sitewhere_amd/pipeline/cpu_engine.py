@@ -59,6 +59,10 @@ class CpuInboundEngine(EngineBase):
         self.group = group
         self.exchange = None
         self.carry = np.zeros(0, EVENT_REC)    # records deferred to the next exchange (full slabs)
+        # the carry's strings: refs into carry_heap (an alert's message offset is in its record)
+        self.carry_sp = np.zeros(0, STR_REF)
+        self.carry_heap = np.zeros(0, np.uint8)
+        self.str_drops = [0, 0]                # [strings larger than a whole slab, unused]
         self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
         self.cursor = 0
         self.seq_base = 0
@@ -78,43 +82,138 @@ class CpuInboundEngine(EngineBase):
         self._seen: set[int] = set()
 
     # ------------------------------------------------------------------ stages
-    def partition(self, recs: np.ndarray, with_index: bool = False):
-        """Stable owner partition into [world, shuf_cap] slabs (same as k_part_count/k_part_write).
+    def partition(self, recs: np.ndarray, with_index: bool = False, spans=None, raw=None):
+        """Stable owner partition into [world, shuf_cap] slabs (same as k_part_count / k_part_cut /
+        k_part_write).
 
-        The input is the previous partition's carry followed by ``recs``; records beyond a slab are
-        spilled destination-major into the next carry (up to ``carry_cap``, the rest dropped).
+        The input is the previous partition's carry followed by ``recs``.  Per destination, records
+        go to the slab in input order while they fit: a record slot (``shuf_cap``) and, with the
+        string exchange on (``spans`` / ``raw`` given), its strings in the destination's byte slab
+        (``str_cap``: the slab takes a prefix of the records, strings included).  The rest spill
+        destination-major into the next carry (up to ``carry_cap``; beyond it, and beyond the carry's
+        string heap, records are dropped and counted) -- with their strings, which the carry keeps
+        (``carry_heap``), so a deferred record loses nothing.  A record whose strings alone exceed a
+        slab is sent without them (``str_drops[0]``: impossible at the default sizes).
         ``with_index``: also the input indices of each slab's records and the carry length."""
         nc = len(self.carry)
-        recs = np.concatenate([self.carry, recs]) if nc else recs
-        owner = self._dest(recs)
-        cap = self.cfg.shuf_cap
+        strings = spans is not None and raw is not None and bool(self.cfg.str_cap)
+        inp = np.concatenate([self.carry, recs]) if nc else recs
+        owner = self._dest(inp)
+        cap, scap = self.cfg.shuf_cap, self.cfg.str_cap
+        L = self._string_lengths(inp, nc, spans) if strings else np.zeros(len(inp), np.int64)
+        over = L > scap if strings else np.zeros(len(inp), bool)
+        if over.any():
+            self.str_drops[0] += int(over.sum())
+            L = np.where(over, 0, L)
+        self._strip = over                      # records sent without their strings
         send = np.zeros((self.world, cap), EVENT_REC)
         cnt = np.zeros(self.world, np.int64)
-        spill = []
+        spill_idx = []
         index = []
         for o in range(self.world):
             at = np.nonzero(owner == o)[0]
-            sel = recs[at]
-            k = min(len(sel), cap)
-            send[o, :k] = sel[:k]
+            k = min(len(at), cap)
+            if strings and k:
+                k = int(np.searchsorted(np.cumsum(L[at[:k]]), scap, side="right"))
+            send[o, :k] = inp[at[:k]]
             cnt[o] = k
             index.append(at[:k])
-            spill.append(sel[k:])
-        spill = np.concatenate(spill)
-        kept = min(len(spill), self.cfg.carry_cap)
+            spill_idx.append(at[k:])
+        spill_idx = np.concatenate(spill_idx) if spill_idx else np.zeros(0, np.int64)
+        kept = min(len(spill_idx), self.cfg.carry_cap)
+        keep = spill_idx[:kept]
+        if strings and kept:
+            # the deferred records' strings move into the next carry's heap (up to its capacity)
+            fits = np.cumsum(L[keep]) <= self.cfg.carry_str_cap
+            if not fits.all():               # beyond the carry's string heap: dropped like beyond carry_cap
+                kept = int(fits.sum())
+                keep = keep[:kept]
         self.stats[13] += kept
-        self.stats[10] += len(spill) - kept
-        self.carry = spill[:kept].copy()
+        self.stats[10] += len(spill_idx) - kept
+        old_sp, old_heap = self.carry_sp, self.carry_heap
+        self._part_src = (nc, old_sp, old_heap)          # where _pack_strings reads carried strings
+        new_carry = inp[keep].copy()
+        if strings and kept:
+            self.carry_sp, self.carry_heap = self._gather_strings(new_carry, keep, nc, spans, raw, old_sp, old_heap,
+                                                                  L[keep], rebase_msg=True)
+        else:
+            self.carry_sp, self.carry_heap = np.zeros(kept, STR_REF), np.zeros(0, np.uint8)
+        self.carry = new_carry
         if with_index:
             return send, cnt, index, nc
         return send, cnt
 
+    def _string_lengths(self, inp, nc, spans) -> np.ndarray:
+        """Exchange bytes of each partition input: alternate id + metadata + alert message (0 for
+        control records); carried records' from the carry's refs."""
+        n = len(inp)
+        s = np.zeros(n, STR_REF)
+        if nc:
+            s[:nc] = self.carry_sp[:nc]
+        s[nc:] = spans[:n - nc]
+        al = np.where((s["has"] & 1) != 0, s["alt_len"], 0).astype(np.int64)
+        ml = np.where((s["has"] & 2) != 0, s["meta_len"], 0).astype(np.int64)
+        gl = np.where(inp["etype"] == EV_ALERT, inp["aux2_len"], 0).astype(np.int64)
+        ln = al + ml + gl
+        ln[inp["etype"] >= 16] = 0                        # control records keep their raw-batch offsets
+        return ln
+
+    def _gather_strings(self, out_recs, at, nc, spans, raw, c_sp, c_heap, L, rebase_msg):
+        """The strings of partition inputs ``at`` (fresh: from ``raw``; carried: from the carry heap)
+        packed back to back: (refs into the new heap, heap); an alert's message offset is rewritten
+        in ``out_recs`` when ``rebase_msg``."""
+        k = len(at)
+        fresh = at >= nc
+        s = np.zeros(k, STR_REF)
+        s[fresh] = spans[at[fresh] - nc]
+        s[~fresh] = c_sp[at[~fresh]]
+        strip = self._strip[at]
+        has = np.where(strip, s["has"] & 4, s["has"])
+        al = np.where((has & 1) != 0, s["alt_len"], 0).astype(np.int64)
+        ml = np.where((has & 2) != 0, s["meta_len"], 0).astype(np.int64)
+        alert = out_recs["etype"] == EV_ALERT
+        gl = np.where(alert & ~strip, out_recs["aux2_len"], 0).astype(np.int64)
+        ctl = out_recs["etype"] >= 16
+        al[ctl] = ml[ctl] = gl[ctl] = 0
+        ln = al + ml + gl
+        start = np.cumsum(ln) - ln
+        total = int(ln.sum())
+        heap = np.zeros(total, np.uint8)
+        if total:
+            src_heap = [np.asarray(raw, np.uint8), c_heap]
+            for part, (off_f, lens) in enumerate(((s["alt_off"], al), (s["meta_off"], ml),
+                                                 (out_recs["aux2_off"], gl))):
+                dst0 = start + (0 if part == 0 else al if part == 1 else al + ml)
+                for src_sel, src in ((fresh, src_heap[0]), (~fresh, src_heap[1])):
+                    m = src_sel & (lens > 0)
+                    if not m.any():
+                        continue
+                    ll = lens[m]
+                    idx = np.repeat(off_f[m].astype(np.int64) - np.cumsum(np.concatenate([[0], ll[:-1]])), ll) + \
+                        np.arange(int(ll.sum()))
+                    didx = np.repeat(dst0[m] - np.cumsum(np.concatenate([[0], ll[:-1]])), ll) + np.arange(int(ll.sum()))
+                    heap[didx] = src[idx]
+        ns = np.zeros(k, STR_REF)
+        keep = ~ctl
+        ns["k"] = np.where(keep, s["k"], 0)
+        ns["has"] = np.where(keep & (ln > 0), has, np.where(keep, has & 4, 0))
+        ns["alt_off"] = np.where(keep & (ln > 0), start, 0)
+        ns["meta_off"] = np.where(keep & (ln > 0), start + al, 0)
+        ns["alt_len"] = np.where(keep & (ln > 0) & ((has & 1) != 0), s["alt_len"], 0)
+        ns["meta_len"] = np.where(keep & (ln > 0) & ((has & 2) != 0), s["meta_len"], 0)
+        if rebase_msg:
+            am = alert & ~ctl
+            out_recs["aux2_off"] = np.where(am, np.where(gl > 0, start + al + ml, 0), out_recs["aux2_off"])
+            out_recs["aux2_len"] = np.where(am, gl, out_recs["aux2_len"])
+        return ns, heap
+
     def _pack_strings(self, send, index, nc, spans, raw):
-        """String slabs of a partition (``part_strings`` in csrc/hip/swgpu.hip): per destination, each
-        slab record's alternate id, metadata and alert message copied from this rank's batch into
-        one byte slab, its refs rewritten to slab offsets (the alert message offset in the record).
-        Carried records (decoded in an earlier step) have none; what does not fit is dropped."""
+        """String slabs of a partition (``k_part_write`` in csrc/hip/swgpu.hip): per destination, each
+        slab record's alternate id, metadata and alert message, from this rank's batch or the carry
+        heap, copied back to back into one byte slab (the partition sized the slab's prefix to fit),
+        its refs rewritten to slab offsets (the alert message offset in the record)."""
         W, S, cap = self.world, self.cfg.shuf_cap, self.cfg.str_cap
+        _, c_sp, c_heap = self._part_src
         out_sp = np.zeros((W, S), STR_REF)
         buf = np.zeros(W * cap, np.uint8)
         used = np.zeros(W, np.int64)
@@ -124,40 +223,11 @@ class CpuInboundEngine(EngineBase):
             if not k:
                 continue
             r = send[o, :k]
-            fresh = at >= nc
-            s = np.zeros(k, STR_REF)
-            s[fresh] = spans[at[fresh] - nc]
-            ctl = r["etype"] >= 16                  # control records keep their raw-batch offsets
-            al = np.where((s["has"] & 1) != 0, s["alt_len"], 0).astype(np.int64)
-            ml = np.where((s["has"] & 2) != 0, s["meta_len"], 0).astype(np.int64)
-            alert = (r["etype"] == EV_ALERT) & fresh
-            gl = np.where(alert, r["aux2_len"], 0).astype(np.int64)
-            al[ctl] = ml[ctl] = gl[ctl] = 0
-            ln = al + ml + gl
-            fit = (np.cumsum(ln) <= cap)
-            ln = np.where(fit, ln, 0)
-            al, ml, gl = np.where(fit, al, 0), np.where(fit, ml, 0), np.where(fit, gl, 0)
-            start = np.cumsum(ln) - ln
-            total = int(ln.sum())
-            used[o] = total
-            if total:
-                seg_src = np.stack([s["alt_off"].astype(np.int64), s["meta_off"].astype(np.int64),
-                                    r["aux2_off"].astype(np.int64)], 1).reshape(-1)
-                seg_len = np.stack([al, ml, gl], 1).reshape(-1)
-                idx = np.repeat(seg_src - (np.cumsum(seg_len) - seg_len), seg_len) + np.arange(total)
-                buf[o * cap:o * cap + total] = raw[idx]
-            ns = np.zeros(k, STR_REF)
-            keep = fresh & ~ctl
-            ns["k"] = np.where(keep, s["k"], 0)
-            ns["has"] = np.where(keep & (ln > 0), s["has"], np.where(keep, s["has"] & 4, 0))
-            ns["alt_off"] = np.where(keep & (ln > 0), start, 0)
-            ns["meta_off"] = np.where(keep & (ln > 0), start + al, 0)
-            ns["alt_len"] = np.where(keep & (ln > 0), s["alt_len"], 0)
-            ns["meta_len"] = np.where(keep & (ln > 0), s["meta_len"], 0)
+            ns, heap = self._gather_strings(r, at, nc, spans, raw, c_sp, c_heap, None, rebase_msg=True)
+            assert len(heap) <= cap
+            buf[o * cap:o * cap + len(heap)] = heap
+            used[o] = len(heap)
             out_sp[o, :k] = ns
-            am = r["etype"] == EV_ALERT
-            r["aux2_off"] = np.where(am & ~ctl, np.where(gl > 0, start + al + ml, 0), r["aux2_off"])
-            r["aux2_len"] = np.where(am & ~ctl, gl, r["aux2_len"])
         return out_sp, buf, used
 
     def _dest(self, recs: np.ndarray) -> np.ndarray:
@@ -192,8 +262,12 @@ class CpuInboundEngine(EngineBase):
         import torch
 
         from ..parallel.sharding import exchange_slabs
-        send, cnt, index, nc = self.partition(recs, with_index=True)
         strings = bool(self.cfg.str_cap) and raw is not None and getattr(self, "_dec_spans", None) is not None
+        if strings:
+            send, cnt, index, nc = self.partition(recs, with_index=True, spans=self._dec_spans,
+                                                  raw=np.asarray(raw, np.uint8))
+        else:
+            send, cnt, index, nc = self.partition(recs, with_index=True)
         extra = ()
         if strings:
             sp, sbuf, sused = self._pack_strings(send, index, nc, self._dec_spans, np.asarray(raw, np.uint8))

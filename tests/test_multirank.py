@@ -339,7 +339,7 @@ def _skewed_batch(world, rank, k, n=1200):
     heap, offs = gen_tokens("dev-", 0, N_DEV)
     lo, hi = fingerprints(heap, offs)
     theirs = np.nonzero(((hi >> np.uint64(32)) % np.uint64(world)) == (rank + 1) % world)[0]
-    msgs = [wire.measurements(f"dev-{int(theirs[(k * 131 + i) % len(theirs)])}", {"v": float(i)},
+    msgs = [wire.measurements(f"dev-{int(theirs[(k * 131 + i) % len(theirs)]):010d}", {"v": float(i)},
                               event_date=NOW - 1000 + i, alternate_id=f"sk-{rank}-{k}-{i}") for i in range(n)]
     return pack_messages(msgs)
 
@@ -402,3 +402,105 @@ def test_gloo_skewed_keys_stall_instead_of_dropping():
     assert all(o[3] > 0 for o in outs) and any(o[4] > 0 for o in outs), outs   # spilled, and stalled
     assert all(o[5] <= o[6] for o in outs), outs              # carry stayed within carry_cap
     assert sum(o[1] for o in outs) == 2 * 12 * 1200           # every event processed exactly once
+
+
+def _skewed_string_batch(world, rank, k, n=800):
+    """Skewed payloads (every device owned by the other rank) with 60-byte alternate ids, metadata
+    on every other payload and alerts with messages."""
+    from sitewhere_amd.models import wire
+    from sitewhere_amd.pipeline.fleet import pack_messages
+    heap, offs = gen_tokens("dev-", 0, N_DEV)
+    lo, hi = fingerprints(heap, offs)
+    theirs = np.nonzero(((hi >> np.uint64(32)) % np.uint64(world)) == (rank + 1) % world)[0]
+    msgs = []
+    for i in range(n):
+        tok = f"dev-{int(theirs[(k * 131 + i) % len(theirs)]):010d}"
+        alt = f"lossless-{rank}-{k:04d}-{i:05d}-".ljust(60, "x")
+        md = {"site": f"s{i % 7}", "fw": f"1.{i % 5}"} if i % 2 else None
+        if i % 9 == 4:
+            msgs.append(wire.alert(tok, "door.open", f"door opened at gate {i} of batch {k}", event_date=NOW - 900 + i,
+                                   alternate_id=alt, metadata=md))
+        else:
+            msgs.append(wire.measurements(tok, {"v": float(i)}, event_date=NOW - 1000 + i, alternate_id=alt,
+                                          metadata=md))
+    return pack_messages(msgs)
+
+
+def _gloo_strings_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from sitewhere_amd.persistence.segments import decode_block, row_strings
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # record slabs of ~260 and string slabs of ~260 x 24 bytes: the string slab fills first (each
+    # record carries 60-150 bytes), so most records wait in the carry -- with their strings
+    e = CpuInboundEngine(EngineConfig.small(world=world, rank=rank, max_msgs=800, shuffle_slack=0.3,
+                                            shuffle_pad=0, str_bytes=24))
+    shard_fleet(e, world, rank)
+    batches = [_skewed_string_batch(world, rank, k) for k in range(8)]
+    empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))
+    nxt = rounds = 0
+    stored = []
+    peak = 0
+    while True:
+        if nxt < len(batches) and not e.should_stall():
+            raw, offs = batches[nxt]
+            nxt += 1
+        else:
+            raw, offs = empty
+        res = e.step(raw, offs, NOW, presence=False)
+        if res.n_persisted:
+            c = decode_block(e.encode_block(NOW, res, boot=0x77))
+            for i in range(len(c["date"])):
+                alt, msg, md = row_strings(c, i)
+                stored.append((alt, msg, tuple(sorted(md.items()))))
+        rounds += 1
+        peak = max(peak, e.carry_count())
+        left = torch.tensor([len(batches) - nxt + e.carry_count()], dtype=torch.int64)
+        dist.all_reduce(left)
+        if int(left) == 0 or rounds > 600:
+            break
+    s = e.stats_dict()
+    q.put((rank, stored, s["shuffle_overflow"], s["shuffle_deferred"], peak, list(e.str_drops), rounds, s))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_skewed_strings_are_lossless():
+    """two gloo ranks, skewed keys (every record crosses the exchange), 60-byte
+    alternate ids, metadata and alert messages through string slabs far too small for a batch:
+    records whose strings do not fit wait in the carry with their strings, so the owner ranks store
+    every event with every string -- the same strings the decoding ranks were sent."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_strings_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted((q.get(timeout=300) for _ in range(2)), key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, stored, overflow, deferred, peak, drops, rounds, _ in outs:
+        assert overflow == 0 and deferred > 0 and drops == [0, 0], (rank, overflow, deferred, drops)
+    # every payload sent by either rank is stored by the other, with its strings intact
+    want = {}
+    for r in range(2):
+        for k in range(8):
+            for i in range(800):
+                alt = f"lossless-{r}-{k:04d}-{i:05d}-".ljust(60, "x")
+                md = tuple(sorted({"site": f"s{i % 7}", "fw": f"1.{i % 5}"}.items())) if i % 2 else ()
+                msg = f"door opened at gate {i} of batch {k}" if i % 9 == 4 else ""
+                want[alt] = (msg, md)
+    got = {}
+    for rank, stored, *_ in outs:
+        for alt, msg, md in stored:
+            assert alt not in got, alt                         # stored once
+            got[alt] = (msg, md)
+    assert got == want
