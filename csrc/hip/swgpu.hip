@@ -455,28 +455,88 @@ __device__ __forceinline__ const SwEventRec& part_in(const SwEventRec* __restric
   return i < (int64_t)nc ? carry[i] : recs[i - nc];
 }
 
+// Exchange bytes of partition input i: alternate id + metadata + alert message (control records
+// keep their raw-batch offsets and send none).  Carried records' refs point into the carry heap.
+__device__ __forceinline__ uint32_t part_str_len(const SwEngineArgs& a, const SwEventRec& r, uint32_t nc, int64_t i) {
+  if (r.etype >= 16) return 0u;
+  const SwStrRef s = i < (int64_t)nc ? a.carry_spans[i] : a.spans[i - nc];
+  const uint32_t al = (s.has & SW_SR_ALT) ? s.alt_len : 0u;
+  const uint32_t ml = (s.has & SW_SR_META) ? s.meta_len : 0u;
+  const uint32_t gl = r.etype == SW_EV_ALERT ? r.aux2_len : 0u;
+  return al + ml + gl;
+}
+
+#define PART_STRIP 0x80000000u   // part_len flag: sent without its strings (they exceed a whole slab)
+// part_meta layout (u64 words)
+#define PM_CUT 0                 // [64] records the slab takes per destination
+#define PM_CUT_BYTES 64          // [64] their string bytes
+#define PM_BYTES 128             // [64] string bytes of all the destination's records
+#define PM_KEPT 192              // spilled records kept in the next carry
+#define PM_KEPT_BYTES 193        // their string bytes (the next carry heap's size)
+
+// Block-wide exclusive scan of one u64 per thread (string byte prefixes can pass 2^32).
+__device__ __forceinline__ ull block_excl_scan64(ull v, ull* total, ull* lds) {
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+  ull inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const ull t = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += t;
+  }
+  if (lane == 63) lds[wid] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ull acc = 0;
+    for (int w = 0; w < WAVES; ++w) { const ull t = lds[w]; lds[w] = acc; acc += t; }
+    lds[WAVES] = acc;
+  }
+  __syncthreads();
+  const ull res = inc - v + lds[wid];
+  *total = lds[WAVES];
+  __syncthreads();
+  return res;
+}
+
+// Per tile: records and string bytes per destination ([world][ntiles] each), the destination of
+// every input (part_owner) and its exchange bytes (part_len; a record whose strings alone exceed a
+// whole slab goes without them, counted in str_drops[0]).
 __global__ void k_part_count(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
                              const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr,
                              int world, int rank, uint32_t* __restrict__ tcount /*[world][ntiles]*/, int64_t ntiles,
-                             uint32_t* __restrict__ send_str_cnt, SwEngineArgs a) {
+                             SwEngineArgs a) {
   __shared__ uint32_t cnt[64];
-  if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
-  // the string slabs' byte cursors start empty (k_part_write allocates from them)
-  if (send_str_cnt && BID == 0 && threadIdx.x < (uint32_t)world) send_str_cnt[threadIdx.x] = 0;
+  __shared__ ull byt[64];
+  if (threadIdx.x < 64) { cnt[threadIdx.x] = 0; byt[threadIdx.x] = 0; }
+  if (BID == 0 && threadIdx.x < 2) a.part_meta[PM_KEPT + threadIdx.x] = 0;   // k_part_write counts into them
   __syncthreads();
+  const bool strings = a.send_str != nullptr;
   const uint32_t nc = *nc_ptr;
   const int64_t n = (int64_t)nc + *n_ptr;
   const int64_t base = (int64_t)BID * TILE;
   for (int k = 0; k < TILE_ITEMS; ++k) {
     int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     if (i < n) {
-      const uint32_t o = part_dest(a, part_in(carry, nc, recs, i), (uint32_t)world, (uint32_t)rank);
-      a.part_owner[i] = (uint8_t)o;           // k_part_write reads it back
+      const SwEventRec& r = part_in(carry, nc, recs, i);
+      const uint32_t o = part_dest(a, r, (uint32_t)world, (uint32_t)rank);
+      a.part_owner[i] = (uint8_t)o;           // k_part_cut / k_part_write read it back
       atomicAdd(&cnt[o], 1u);
+      if (strings) {
+        uint32_t L = part_str_len(a, r, nc, i);
+        if ((int64_t)L > a.str_cap) {
+          atomicAdd(&a.str_drops[0], 1u);
+          L = PART_STRIP;
+        } else if (L) {
+          atomicAdd(&byt[o], (ull)L);
+        }
+        a.part_len[i] = L;
+      }
     }
   }
   __syncthreads();
-  if (threadIdx.x < world) tcount[(int64_t)threadIdx.x * ntiles + BID] = cnt[threadIdx.x];
+  if (threadIdx.x < world) {
+    tcount[(int64_t)threadIdx.x * ntiles + BID] = cnt[threadIdx.x];
+    a.part_bytes[(int64_t)threadIdx.x * ntiles + BID] = byt[threadIdx.x];
+  }
 }
 
 // Records per destination from the scanned [world][ntiles] matrix.
@@ -486,133 +546,239 @@ __device__ __forceinline__ uint32_t part_total(const uint32_t* __restrict__ toff
   return toff[last] + tcount[last] - toff[(int64_t)q * ntiles];
 }
 
-// A record's strings into its destination's byte slab (alternate id, metadata, alert message, in that
-// order), returning its refs rewritten to slab offsets; the alert message offset goes to *msg_off.
-// Strings that do not fit the slab are dropped (counted in str_drops[0]); carried records (decoded
-// in an earlier step, whose raw batch is gone) have none (str_drops[1]).
-__device__ __forceinline__ SwStrRef part_strings(const SwEngineArgs& a, const SwEventRec& r, const SwStrRef* s,
-                                                 uint32_t o, uint32_t* msg_off, uint16_t* msg_len) {
+// One workgroup per destination q: the byte prefix of q's string slab per tile (u64 exclusive scan
+// of its row of part_bytes), then the cut -- the prefix of q's records, in input order, that the
+// slab takes: at most shuf_cap records whose strings fit str_cap bytes (CpuInboundEngine.partition).
+// The cut falls in the first tile where either bound is crossed; that tile is walked record by
+// record.  Writes the send counts (records, string bytes) and part_meta.
+__global__ __launch_bounds__(BLK) void k_part_cut(const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tcount,
+                                                  int64_t ntiles, const uint32_t* __restrict__ nc_ptr,
+                                                  const uint32_t* __restrict__ n_ptr, SwEngineArgs a) {
+  __shared__ ull red[WAVES + 1];
+  __shared__ int tstar;
+  __shared__ uint32_t fit_c;
+  __shared__ ull fit_b;
+  const int q = (int)blockIdx.x;
+  const ull* tb = (const ull*)a.part_bytes + (int64_t)q * ntiles;
+  ull* bo = (ull*)a.part_bytes + (int64_t)a.world * ntiles + (int64_t)q * ntiles;
+  ull acc = 0;
+  for (int64_t c0 = 0; c0 < ntiles; c0 += BLK) {
+    const int64_t t = c0 + threadIdx.x;
+    const ull v = t < ntiles ? tb[t] : 0ull;
+    ull tot;
+    const ull ex = block_excl_scan64(v, &tot, red);
+    if (t < ntiles) bo[t] = acc + ex;
+    acc += tot;
+  }
+  const bool strings = a.send_str != nullptr;
+  const ull blim = strings ? (ull)a.str_cap : ~0ull;
+  const int64_t row = (int64_t)q * ntiles;
+  const uint32_t c0q = toff[row];
+  if (threadIdx.x == 0) { tstar = (int)ntiles; fit_c = 0; fit_b = 0; }
+  __syncthreads();
+  for (int64_t t = threadIdx.x; t < ntiles; t += BLK) {
+    const ull cofs = toff[row + t] - c0q;
+    if (cofs + tcount[row + t] > (ull)a.shuf_cap || bo[t] + tb[t] > blim) atomicMin(&tstar, (int)t);
+  }
+  __syncthreads();
+  const int64_t ts = tstar;
+  ull cut, bcut;
+  if (ts >= ntiles) {
+    cut = part_total(toff, tcount, ntiles, q);
+    bcut = acc;
+  } else {
+    const uint32_t nc = *nc_ptr;
+    const int64_t n = (int64_t)nc + *n_ptr;
+    ull rc = toff[row + ts] - c0q, rb = bo[ts];
+    const int64_t base = ts * TILE;
+    for (int k = 0; k < TILE_ITEMS; ++k) {
+      const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
+      const bool mine = i < n && a.part_owner[i] == (uint8_t)q;
+      const ull L = mine && strings ? (ull)(a.part_len[i] & ~PART_STRIP) : 0ull;
+      ull totc, totb;
+      const ull exc = block_excl_scan64(mine ? 1ull : 0ull, &totc, red);
+      const ull exb = block_excl_scan64(L, &totb, red);
+      if (mine && rc + exc + 1 <= (ull)a.shuf_cap && rb + exb + L <= blim) {
+        atomicAdd(&fit_c, 1u);
+        atomicAdd(&fit_b, L);
+      }
+      rc += totc;
+      rb += totb;
+    }
+    __syncthreads();
+    cut = (ull)(toff[row + ts] - c0q) + fit_c;
+    bcut = bo[ts] + fit_b;
+  }
+  if (threadIdx.x == 0) {
+    a.part_meta[PM_CUT + q] = cut;
+    a.part_meta[PM_CUT_BYTES + q] = bcut;
+    a.part_meta[PM_BYTES + q] = acc;
+    a.send_cnt[q] = (uint32_t)cut;
+    if (strings) a.send_str_cnt[q] = (uint32_t)bcut;
+  }
+}
+
+// A record's strings (alternate id, metadata, alert message, back to back) copied from `src` (this
+// rank's raw batch, or the carry heap for a carried record) to dst[at..); returns its refs
+// rewritten to those offsets and rebases the alert message in r.  `strip`: the record goes without
+// its strings (they exceed a whole slab).
+__device__ __forceinline__ SwStrRef part_strings(SwEventRec& r, const SwStrRef* s, const uint8_t* __restrict__ src,
+                                                 bool strip, uint8_t* __restrict__ dst, ull at) {
   SwStrRef z;
   z.alt_off = 0; z.meta_off = 0; z.alt_len = 0; z.meta_len = 0; z.k = 0; z.has = 0; z.pad = 0;
-  *msg_off = 0;
-  *msg_len = 0;
-  const bool alert = r.etype == SW_EV_ALERT;
-  if (!s) {                                  // carried record
-    if (r.alt_hash || (alert && r.aux2_len)) atomicAdd(&a.str_drops[1], 1u);
-    return z;
-  }
+  if (r.etype >= 16) return z;
   const SwStrRef sr = *s;
-  const uint32_t al = (sr.has & SW_SR_ALT) ? sr.alt_len : 0u;
-  const uint32_t ml = (sr.has & SW_SR_META) ? sr.meta_len : 0u;
-  const uint32_t gl = alert ? r.aux2_len : 0u;
-  const uint32_t len = al + ml + gl;
-  if (len == 0) {
-    z.k = sr.k;
-    z.has = sr.has & SW_SR_MULTI;
+  const bool alert = r.etype == SW_EV_ALERT;
+  const uint8_t has = strip ? (uint8_t)(sr.has & SW_SR_MULTI) : sr.has;
+  const uint32_t al = (has & SW_SR_ALT) ? sr.alt_len : 0u;
+  const uint32_t ml = (has & SW_SR_META) ? sr.meta_len : 0u;
+  const uint32_t gl = alert && !strip ? r.aux2_len : 0u;
+  z.k = sr.k;
+  if (al + ml + gl == 0) {
+    z.has = has & SW_SR_MULTI;
+    if (alert) { r.aux2_off = 0; r.aux2_len = 0; }
     return z;
   }
-  const uint32_t at = atomicAdd(&a.send_str_cnt[o], len);
-  if ((int64_t)at + len > a.str_cap) {
-    atomicAdd(&a.str_drops[0], 1u);
-    return z;
-  }
-  uint8_t* dst = a.send_str + (int64_t)o * a.str_cap + at;
-  for (uint32_t b = 0; b < al; ++b) dst[b] = a.raw[sr.alt_off + b];
-  for (uint32_t b = 0; b < ml; ++b) dst[al + b] = a.raw[sr.meta_off + b];
-  for (uint32_t b = 0; b < gl; ++b) dst[al + ml + b] = a.raw[r.aux2_off + b];
-  z = sr;
-  z.alt_off = at;
-  z.meta_off = at + al;
-  *msg_off = at + al + ml;
-  *msg_len = (uint16_t)gl;
+  uint8_t* d = dst + at;
+  for (uint32_t b = 0; b < al; ++b) d[b] = src[sr.alt_off + b];
+  for (uint32_t b = 0; b < ml; ++b) d[al + b] = src[sr.meta_off + b];
+  for (uint32_t b = 0; b < gl; ++b) d[al + ml + b] = src[r.aux2_off + b];
+  z.has = has;
+  z.alt_off = (uint32_t)at;
+  z.meta_off = (uint32_t)(at + al);
+  z.alt_len = (uint16_t)al;
+  z.meta_len = (uint16_t)ml;
+  if (alert) { r.aux2_off = (uint32_t)(at + al + ml); r.aux2_len = (uint16_t)gl; }
   return z;
 }
 
-__global__ void k_part_write(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
+// Stable scatter: a record's position among its destination's records (and its strings' byte
+// position) decides its place -- in the slab below the cut, else in the spill (the next carry,
+// destination-major) with its strings in the spill heap.  Spilled records beyond carry_cap or the
+// spill heap (a prefix of the spill order, like the oracle's) are dropped and counted.
+__global__ __launch_bounds__(BLK) void k_part_write(const SwEventRec* __restrict__ carry, const uint32_t* __restrict__ nc_ptr,
                              const SwEventRec* __restrict__ recs, const uint32_t* __restrict__ n_ptr, int world,
                              int rank, const uint32_t* __restrict__ toff /*scanned [world][ntiles]*/,
                              const uint32_t* __restrict__ tcount, int64_t ntiles, SwWireRec* __restrict__ send,
                              int64_t shuf_cap, SwEventRec* __restrict__ spill, int64_t carry_cap, SwEngineArgs a) {
   __shared__ uint32_t run[64];
+  __shared__ ull rbyt[64];
+  __shared__ uint32_t cutq[64];
+  __shared__ ull bcutq[64];
   __shared__ uint32_t spill_base[64];
+  __shared__ ull spill_bbase[64];
   __shared__ uint32_t wcnt[WAVES][64];
+  __shared__ ull wbyt[WAVES][64];
+  __shared__ uint32_t kept_c;
+  __shared__ ull kept_b;
   const uint32_t nc = *nc_ptr;
   const int64_t n = (int64_t)nc + *n_ptr;
   const int64_t base = (int64_t)BID * TILE;
-  const uint32_t wid = threadIdx.x >> 6;
+  const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
+  const bool strings = a.send_str != nullptr;
+  const ull* bo = (const ull*)a.part_bytes + (int64_t)world * ntiles;
   if (threadIdx.x < world) {
-    run[threadIdx.x] = toff[(int64_t)threadIdx.x * ntiles + BID] - toff[(int64_t)threadIdx.x * ntiles];
+    const int64_t row = (int64_t)threadIdx.x * ntiles;
+    run[threadIdx.x] = toff[row + BID] - toff[row];
+    rbyt[threadIdx.x] = bo[row + BID];
+    cutq[threadIdx.x] = (uint32_t)a.part_meta[PM_CUT + threadIdx.x];
+    bcutq[threadIdx.x] = a.part_meta[PM_CUT_BYTES + threadIdx.x];
   }
   if (threadIdx.x == 0) {
-    // records beyond a destination's slab go to the spill list, destination-major (deterministic)
     uint32_t acc = 0;
+    ull bacc = 0;
     for (int q = 0; q < world; ++q) {
       spill_base[q] = acc;
-      const uint32_t tot = part_total(toff, tcount, ntiles, q);
-      acc += tot > shuf_cap ? tot - (uint32_t)shuf_cap : 0u;
+      spill_bbase[q] = bacc;
+      acc += part_total(toff, tcount, ntiles, q) - (uint32_t)a.part_meta[PM_CUT + q];
+      bacc += a.part_meta[PM_BYTES + q] - a.part_meta[PM_CUT_BYTES + q];
     }
+    kept_c = 0;
+    kept_b = 0;
   }
   __syncthreads();
   for (int k = 0; k < TILE_ITEMS; ++k) {
     const int64_t i = base + (int64_t)k * BLK + threadIdx.x;
     const bool valid = i < n;
-    uint32_t o = 0;
-    if (valid) o = a.part_owner[i];
+    const uint32_t o = valid ? a.part_owner[i] : 0u;
+    const uint32_t L = valid && strings ? a.part_len[i] : 0u;
+    const ull Lb = L & ~PART_STRIP;
+    if (lane < (uint32_t)world) { wcnt[wid][lane] = 0; wbyt[wid][lane] = 0; }
+    // rank and byte prefix among the wave's records of the same destination, one pass per
+    // destination present in the wave
     uint32_t my_rank = 0;
-    for (int q = 0; q < world; ++q) {
-      ull m = __ballot(valid && o == (uint32_t)q);
-      if (valid && o == (uint32_t)q) my_rank = __popcll(m & lanemask_lt());
-      if (lane_id() == 0) wcnt[wid][q] = __popcll(m);
+    ull my_b = 0;
+    ull rem = __ballot(valid);
+    while (rem) {
+      const uint32_t q = __shfl(o, (int)__ffsll((long long)rem) - 1, 64);
+      const bool mine = valid && o == q;
+      const ull m = __ballot(mine);
+      ull inc = mine ? Lb : 0ull;
+      if (strings) {
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const ull t = __shfl_up(inc, d, 64);
+          if (lane >= (uint32_t)d) inc += t;
+        }
+      }
+      if (mine) { my_rank = __popcll(m & lanemask_lt()); my_b = inc - Lb; }
+      if (lane == 63) { wcnt[wid][q] = __popcll(m); wbyt[wid][q] = inc; }
+      rem &= ~m;
     }
     __syncthreads();
     if (valid) {
       uint32_t pre = run[o];
-      for (uint32_t w = 0; w < wid; ++w) pre += wcnt[w][o];
+      ull bpre = rbyt[o];
+      for (uint32_t w = 0; w < wid; ++w) { pre += wcnt[w][o]; bpre += wbyt[w][o]; }
       pre += my_rank;
-      if (pre < shuf_cap) {
-        SwEventRec r = part_in(carry, nc, recs, i);
-        if (a.send_str && r.etype < 16) {      // control records keep their raw-batch offsets
-          uint32_t moff;
-          uint16_t mlen;
-          const SwStrRef* s = i >= (int64_t)nc ? a.spans + (i - nc) : nullptr;
-          a.send_spans[(int64_t)o * shuf_cap + pre] = part_strings(a, r, s, o, &moff, &mlen);
-          if (r.etype == SW_EV_ALERT) { r.aux2_off = moff; r.aux2_len = mlen; }
-        } else if (a.send_str) {
-          SwStrRef z;
-          z.alt_off = 0; z.meta_off = 0; z.alt_len = 0; z.meta_len = 0; z.k = 0; z.has = 0; z.pad = 0;
-          a.send_spans[(int64_t)o * shuf_cap + pre] = z;
-        }
-        send[(int64_t)o * shuf_cap + pre] = sw_wire_pack(r);
+      bpre += my_b;
+      SwEventRec r = part_in(carry, nc, recs, i);
+      const bool fresh = i >= (int64_t)nc;
+      const SwStrRef* sr = strings ? (fresh ? a.spans + (i - nc) : a.carry_spans + i) : nullptr;
+      const uint8_t* src = fresh ? a.raw : a.carry_str;
+      if (pre < cutq[o]) {
+        const int64_t at = (int64_t)o * shuf_cap + pre;
+        if (strings)
+          a.send_spans[at] = part_strings(r, sr, src, (L & PART_STRIP) != 0, a.send_str + (int64_t)o * a.str_cap, bpre);
+        send[at] = sw_wire_pack(r);
       } else {
-        const int64_t j = (int64_t)spill_base[o] + (pre - shuf_cap);
-        if (j < carry_cap) spill[j] = part_in(carry, nc, recs, i);
+        const int64_t j = (int64_t)spill_base[o] + (pre - cutq[o]);
+        const ull sb = spill_bbase[o] + (bpre - bcutq[o]);
+        if (j < carry_cap && (!strings || sb + Lb <= (ull)a.carry_str_cap)) {
+          if (strings) a.spill_spans[j] = part_strings(r, sr, src, (L & PART_STRIP) != 0, a.spill_str, sb);
+          spill[j] = r;
+          atomicAdd(&kept_c, 1u);
+          if (Lb) atomicAdd(&kept_b, Lb);
+        }
       }
     }
     __syncthreads();
     if (threadIdx.x < world) {
       uint32_t t = 0;
-      for (int w = 0; w < WAVES; ++w) t += wcnt[w][threadIdx.x];
+      ull tb = 0;
+      for (int w = 0; w < WAVES; ++w) { t += wcnt[w][threadIdx.x]; tb += wbyt[w][threadIdx.x]; }
       run[threadIdx.x] += t;
+      rbyt[threadIdx.x] += tb;
     }
     __syncthreads();
+  }
+  if (threadIdx.x == 0 && kept_c) {
+    atomicAdd((ull*)&a.part_meta[PM_KEPT], (ull)kept_c);
+    atomicAdd((ull*)&a.part_meta[PM_KEPT_BYTES], kept_b);
   }
 }
 
 __global__ void k_part_counts(const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tcount, int64_t ntiles,
-                              int world, int64_t shuf_cap, uint32_t* __restrict__ send_cnt, uint32_t* __restrict__ n_spill,
-                              int64_t carry_cap, uint32_t* __restrict__ dropped, ull* __restrict__ stats) {
+                              int world, SwEngineArgs a) {
   if (threadIdx.x == 0 && BID == 0) {
-    uint64_t over = 0;
-    for (int o = 0; o < world; ++o) {
-      const uint32_t tot = part_total(toff, tcount, ntiles, o);
-      send_cnt[o] = tot < shuf_cap ? tot : (uint32_t)shuf_cap;
-      over += tot > shuf_cap ? tot - (uint32_t)shuf_cap : 0u;
-    }
-    const uint64_t kept = over < (uint64_t)carry_cap ? over : (uint64_t)carry_cap;
-    *n_spill = (uint32_t)kept;
-    *dropped = (uint32_t)(over - kept);
-    stats[SW_STAT_SHUFFLE_DEFERRED] += kept;
-    stats[SW_STAT_SHUFFLE_OVERFLOW] += over - kept;
+    ull over = 0;
+    for (int o = 0; o < world; ++o) over += part_total(toff, tcount, ntiles, o) - a.part_meta[PM_CUT + o];
+    const ull kept = a.part_meta[PM_KEPT];
+    *a.n_spill = (uint32_t)kept;
+    if (a.n_spill_str) *a.n_spill_str = (uint32_t)a.part_meta[PM_KEPT_BYTES];
+    *a.overflow = (uint32_t)(over - kept);
+    ((ull*)a.stats)[SW_STAT_SHUFFLE_DEFERRED] += kept;
+    ((ull*)a.stats)[SW_STAT_SHUFFLE_OVERFLOW] += over - kept;
   }
 }
 
@@ -1590,19 +1756,23 @@ int sw_phase_partition(const SwEngineArgs* ap, hipStream_t s) {
   const SwEngineArgs a = *ap;
   const int64_t ntiles = (a.carry_cap + a.rec_cap + TILE - 1) / TILE;
   if (a.world > 64 || ntiles * a.world > a.part_tmp_len || !a.carry || !a.n_carry || !a.spill || !a.n_spill ||
-      a.carry == a.spill || !a.part_owner)
+      a.carry == a.spill || !a.part_owner || !a.part_bytes || !a.part_meta || ntiles >= 0x7fffffff)
     return -3;
+  if (a.send_str && (!a.part_len || !a.carry_spans || !a.carry_str || !a.spill_spans || !a.spill_str ||
+                     a.carry_str == a.spill_str || a.carry_str_cap <= 0 || a.carry_str_cap > 0xffffffffll ||
+                     a.str_cap > 0x7fffffffll))
+    return -4;
   k_part_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.carry, a.n_carry, a.recs, a.n_recs, (int)a.world, (int)a.rank,
-                                                a.part_tmp, ntiles, a.send_str ? a.send_str_cnt : nullptr, a);
+                                                a.part_tmp, ntiles, a);
   // scan the flat [world][ntiles] count matrix in place
   int rc = launch_scan(a.part_tmp, ntiles * a.world, a.part_tmp + ntiles * a.world, nullptr, a.scan_tmp,
                        a.scan_tmp_len, s);
   if (rc) return rc;
   const uint32_t* toff = a.part_tmp + ntiles * a.world;
+  k_part_cut<<<(unsigned)a.world, BLK, 0, s>>>(toff, a.part_tmp, ntiles, a.n_carry, a.n_recs, a);
   k_part_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.carry, a.n_carry, a.recs, a.n_recs, (int)a.world, (int)a.rank, toff,
                                                 a.part_tmp, ntiles, a.send, a.shuf_cap, a.spill, a.carry_cap, a);
-  k_part_counts<<<1, 64, 0, s>>>(toff, a.part_tmp, ntiles, (int)a.world, a.shuf_cap, a.send_cnt, a.n_spill,
-                                 a.carry_cap, a.overflow, (ull*)a.stats);
+  k_part_counts<<<1, 64, 0, s>>>(toff, a.part_tmp, ntiles, (int)a.world, a);
   return (int)hipGetLastError();
 }
 

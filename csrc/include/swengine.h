@@ -200,7 +200,7 @@ typedef struct SwEngineArgs {
   // the unpack gathers them into work_str ([world][str_cap], the encoder's string source) with the
   // refs rebased (+ source rank * str_cap).  Null send_str: strings stay on the decoding rank.
   uint8_t* send_str;           // [world][str_cap] (this partition's parity)
-  uint32_t* send_str_cnt;      // [world] bytes used per destination (zeroed by k_part_count)
+  uint32_t* send_str_cnt;      // [world] bytes used per destination (k_part_cut)
   SwStrRef* send_spans;        // [world][shuf_cap] string refs beside the send slabs
   const uint8_t* recv_str;     // [world][str_cap]
   const uint32_t* recv_str_cnt;
@@ -208,7 +208,7 @@ typedef struct SwEngineArgs {
   uint8_t* work_str;           // [world][str_cap] gathered by k_unpack
   SwStrRef* work_spans;        // [rec_cap] refs of the work batch (rebased into work_str)
   int64_t str_cap;             // bytes per destination slab
-  uint32_t* str_drops;         // [2] records whose strings did not fit / came from the carry
+  uint32_t* str_drops;         // [2] records sent without strings (larger than a slab) / unused
   // ---------------------------------------------------------------- re-key owner (world > 1)
   uint8_t* part_owner;         // [carry_cap + rec_cap] destination of each partition input (k_part_count)
   // ---------------------------------------------------------------- persist clustering
@@ -219,6 +219,19 @@ typedef struct SwEngineArgs {
   uint32_t* cl_vals;
   uint32_t* cl_hist;
   int64_t cl_bits;             // assignment index bits (0: persist in arrival order)
+  // ---------------------------------------------------------------- lossless re-key (world > 1)
+  // Per destination the slab takes the longest prefix of its records (input order) that fits both
+  // shuf_cap records and str_cap string bytes (k_part_cut); the rest spill into the next carry WITH
+  // their strings, copied into the spill heap (which the next partition reads back as carry_str).
+  uint32_t* part_len;          // [carry_cap + rec_cap] exchange bytes per input (bit 31: sent without strings)
+  uint64_t* part_bytes;        // [2][world][ntiles] string bytes per tile and destination, then their prefix
+  uint64_t* part_meta;         // [256] per destination: cut, cut bytes, total bytes; kept spill counters
+  const SwStrRef* carry_spans; // [carry_cap] refs of the carry's records into carry_str
+  const uint8_t* carry_str;    // the carry's string heap
+  SwStrRef* spill_spans;       // [carry_cap] refs of the spilled records into spill_str
+  uint8_t* spill_str;          // [carry_str_cap]
+  uint32_t* n_spill_str;       // bytes of spill_str in use (k_part_counts)
+  int64_t carry_str_cap;
 } SwEngineArgs;
 
 #define SW_N_STATS 24

@@ -69,6 +69,9 @@ FIELDS = [
     ("part_owner", P),
     # persist clustering by assignment (radix-sort buffers, key bits; 0 = arrival order)
     ("cl_keys", P), ("cl_vals", P), ("cl_hist", P), ("cl_bits", I),
+    # lossless re-key: per-input string bytes, per-tile byte matrix, cut metadata, carry string heaps
+    ("part_len", P), ("part_bytes", P), ("part_meta", P), ("carry_spans", P), ("carry_str", P),
+    ("spill_spans", P), ("spill_str", P), ("n_spill_str", P), ("carry_str_cap", I),
 ]
 
 

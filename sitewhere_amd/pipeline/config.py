@@ -79,8 +79,9 @@ class EngineConfig:
         if self.carry_cap <= 0:
             self.carry_cap = self.carry_high + 2 * local
         # the carry keeps its records' strings: a heap of carry_cap records at twice the slab's
-        # per-record budget (a record whose strings do not fit it waits like one beyond carry_cap)
-        self.carry_str_cap = (self.carry_cap * max(2 * self.str_bytes, 64) + 15) // 16 * 16 \
+        # per-record budget (spilled records beyond it are dropped and counted, like those beyond
+        # carry_cap); u32 offsets
+        self.carry_str_cap = min((self.carry_cap * max(2 * self.str_bytes, 64) + 15) // 16 * 16, 0xFFFFFFF0) \
             if self.world > 1 and self.str_bytes > 0 else 0
 
     @classmethod

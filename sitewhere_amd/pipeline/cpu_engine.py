@@ -62,7 +62,7 @@ class CpuInboundEngine(EngineBase):
         # the carry's strings: refs into carry_heap (an alert's message offset is in its record)
         self.carry_sp = np.zeros(0, STR_REF)
         self.carry_heap = np.zeros(0, np.uint8)
-        self.str_drops = [0, 0]                # [strings larger than a whole slab, unused]
+        self.str_drops = [0, 0]                # [records sent without strings (larger than a slab), unused]
         self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
         self.cursor = 0
         self.seq_base = 0
@@ -247,6 +247,12 @@ class CpuInboundEngine(EngineBase):
 
     def carry_count(self) -> int:
         return len(self.carry)
+
+    def _carry_spans_full(self) -> np.ndarray:
+        sp = self.carry_sp
+        if len(sp) != len(self.carry):             # carry built without strings
+            sp = np.zeros(len(self.carry), STR_REF)
+        return sp
 
     @staticmethod
     def unpack(recv: np.ndarray, rcnt) -> np.ndarray:
@@ -555,6 +561,8 @@ class CpuInboundEngine(EngineBase):
             "ms_key": np.array(ms_keys, np.int64).reshape(-1, 3),
             "ms_val": np.array([self.ms[k] for k in ms_keys], np.int64).reshape(-1, 2),
             "carry": self.carry.view(np.uint8).reshape(-1).copy(),
+            "carry_spans": self._carry_spans_full().view(np.uint8).reshape(-1).copy(),
+            "carry_str": self.carry_heap.copy(),
         }
         if include_store:
             st.update({f"store.{k}": v for k, v in self.store.items()})
@@ -575,6 +583,10 @@ class CpuInboundEngine(EngineBase):
             getattr(self, k)[:] = a[k]
         self.ms = {tuple(int(x) for x in k): [int(v[0]), int(v[1])] for k, v in zip(a["ms_key"], a["ms_val"])}
         self.carry = a["carry"].view(EVENT_REC).copy()
+        # the carry's strings (an older checkpoint has none: its records go without them)
+        self.carry_sp = (a["carry_spans"].view(STR_REF).copy() if "carry_spans" in a
+                         else np.zeros(len(self.carry), STR_REF))
+        self.carry_heap = a.get("carry_str", np.zeros(0, np.uint8)).copy()
         if include_store:
             for k in self.store:
                 self.store[k][:] = a[f"store.{k}"]

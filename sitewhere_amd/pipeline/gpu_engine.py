@@ -152,6 +152,8 @@ class GpuInboundEngine(EngineBase):
             self.carry_bufs = [z(c.carry_cap * EVENT_REC.itemsize, u8) for _ in range(2)]
             t["n_carry"] = z(2, i32)
             t["part_owner"] = z(c.carry_cap + c.rec_cap + 64, u8)      # re-key destination per input
+            t["part_bytes"] = z(2 * c.world * ptiles + 64, i64)          # string bytes per tile, scanned
+            t["part_meta"] = z(256, i64)                                # cut / bytes per destination
             if c.str_cap:
                 # string exchange: byte slabs + refs beside the record slabs (double-buffered the same
                 # way), gathered into work_str by the unpack (see SwEngineArgs)
@@ -164,6 +166,12 @@ class GpuInboundEngine(EngineBase):
                 t["recv_spans"] = z(c.world * c.shuf_cap * sr, u8)
                 t["work_str"] = z(c.world * c.str_cap + 64, u8)
                 t["work_spans"] = z(c.rec_cap * sr, u8)
+                # lossless re-key: spilled records keep their strings in the carry's heap (parity
+                # like the carry records); exchange bytes of every partition input
+                self.carry_spans = [z(c.carry_cap * sr, u8) for _ in range(2)]
+                self.carry_strs = [z(c.carry_str_cap + 64, u8) for _ in range(2)]
+                t["n_carry_str"] = z(2, i32)
+                t["part_len"] = z(c.carry_cap + c.rec_cap + 64, i32)
         t["str_drops"] = z(2, i32)
         # validated
         t["status"] = z(c.rec_cap, u8)
@@ -244,6 +252,9 @@ class GpuInboundEngine(EngineBase):
             a.work = _ptr(t["work"])
             a.carry_cap = c.carry_cap
             a.part_owner = _ptr(t["part_owner"])
+            a.part_bytes, a.part_meta = _ptr(t["part_bytes"]), _ptr(t["part_meta"])
+            if c.str_cap:
+                a.part_len, a.carry_str_cap = _ptr(t["part_len"]), c.carry_str_cap
         else:
             a.work = a.recs
         a.str_drops = _ptr(t["str_drops"])
@@ -448,6 +459,10 @@ class GpuInboundEngine(EngineBase):
                 a.send_spans = _ptr(self.send_spans[sp])
             a.carry, a.n_carry = _ptr(self.carry_bufs[cp]), _ptr(self.t["n_carry"]) + 4 * cp
             a.spill, a.n_spill = _ptr(self.carry_bufs[1 - cp]), _ptr(self.t["n_carry"]) + 4 * (1 - cp)
+            if self.cfg.str_cap:
+                a.carry_spans, a.carry_str = _ptr(self.carry_spans[cp]), _ptr(self.carry_strs[cp])
+                a.spill_spans, a.spill_str = _ptr(self.carry_spans[1 - cp]), _ptr(self.carry_strs[1 - cp])
+                a.n_spill_str = _ptr(self.t["n_carry_str"]) + 4 * (1 - cp)
             rc = self.lib.sw_phase_partition(ap, self._stream())
             if rc:
                 raise RuntimeError(f"sw_phase_partition failed ({rc})")
@@ -583,9 +598,10 @@ class GpuInboundEngine(EngineBase):
                 e.send_strs[p][q * c.str_cap:(q + 1) * c.str_cap])
 
     def string_drops(self) -> dict:
-        """Records whose strings were not exchanged: slab full / carried from an earlier step."""
+        """Records sent without their strings because those alone exceed a whole slab (the only
+        case: a record deferred by a full slab keeps its strings in the carry heap)."""
         v = self.t["str_drops"].cpu().numpy()
-        return {"slab_full": int(v[0]), "carried": int(v[1])}
+        return {"oversize": int(v[0])}
 
     def scalars(self) -> dict:
         v = self.t["scalars"][:9].cpu().numpy()
@@ -1292,6 +1308,10 @@ class GpuInboundEngine(EngineBase):
             cp = self._carry_par
             n = int(self.t["n_carry"][cp].item())
             st["carry"] = self.carry_bufs[cp][:n * EVENT_REC.itemsize].cpu().numpy()
+            if self.cfg.str_cap:
+                nb = int(self.t["n_carry_str"][cp].item())
+                st["carry_spans"] = self.carry_spans[cp][:n * STR_REF.itemsize].cpu().numpy()
+                st["carry_str"] = self.carry_strs[cp][:nb].cpu().numpy()
         if include_store:
             st.update({f"store.{k}": v.cpu().numpy() for k, v in self.store.items()})
         return st
@@ -1330,6 +1350,15 @@ class GpuInboundEngine(EngineBase):
             self.carry_bufs[cp][:c.numel()].copy_(c)
             self.t["n_carry"].zero_()
             self.t["n_carry"][cp] = c.numel() // EVENT_REC.itemsize
+            if self.cfg.str_cap:
+                # the carry's strings (an older checkpoint has none: its records go without them)
+                sp = torch.from_numpy(a.get("carry_spans", np.zeros(c.numel() // EVENT_REC.itemsize, STR_REF)
+                                            .view(np.uint8)))
+                hp = torch.from_numpy(a.get("carry_str", np.zeros(0, np.uint8)))
+                self.carry_spans[cp][:sp.numel()].copy_(sp)
+                self.carry_strs[cp][:hp.numel()].copy_(hp)
+                self.t["n_carry_str"].zero_()
+                self.t["n_carry_str"][cp] = hp.numel()
         if include_store:
             for k, v in self.store.items():
                 v.copy_(torch.from_numpy(a[f"store.{k}"]))

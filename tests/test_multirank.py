@@ -45,7 +45,9 @@ def cpu_shards():
 
 def cpu_loopback_step(shards, batches, now):
     decoded = [e.decode_phase(raw, offs, now) for e, (raw, offs) in zip(shards, batches)]
-    slabs = [e.partition(recs) for e, (recs, _) in zip(shards, decoded)]
+    # with the string exchange on, a slab takes the prefix of records whose strings fit it too
+    slabs = [e.partition(recs, spans=e._dec_spans, raw=np.asarray(raw, np.uint8)) if e.cfg.str_cap
+             else e.partition(recs) for e, (recs, _), (raw, _) in zip(shards, decoded, batches)]
     out = []
     for q, e in enumerate(shards):
         recv = np.stack([slabs[r][0][q] for r in range(W)])

@@ -85,7 +85,7 @@ def test_strings_cross_the_exchange():
         torch.cuda.synchronize()
         res = e.collect(e._last_sel, raw, from_device=True)
         got += _row_keys(e.encode_block(NOW, res, boot=0x5))
-        assert e.string_drops() == {"slab_full": 0, "carried": 0}
+        assert e.string_drops() == {"oversize": 0}
     assert len(got) == len(ref)
     with_alt = sum(1 for k in got if k[3])
     assert with_alt > 0.9 * len(got) - 100                     # nearly every device event has one
@@ -93,36 +93,82 @@ def test_strings_cross_the_exchange():
     assert sorted(got) == sorted(ref)
 
 
-def test_string_slab_overflow_is_counted_not_corrupting():
-    """A slab too small for the step's strings drops whole records' strings (counted); the rows
-    are still stored, and every string that is stored is intact."""
+def test_small_string_slabs_defer_records_with_their_strings():
+    """String slabs far too small for a step's strings (2 bytes per record slot) take a prefix of
+    each destination's records; the rest wait in the carry with their strings (the carry heap) and
+    go in later rounds -- nothing is dropped.  Every round's slabs (records, string bytes, refs) and
+    carry (records, refs, heap) are byte-identical to the oracle's (``CpuInboundEngine.partition``),
+    and after the drain rounds the shards have stored exactly the single-rank engine's rows, every
+    string included."""
     import torch
+    from sitewhere_amd.models.columnar import EVENT_REC, STR_REF, wire_pack
     from sitewhere_amd.pipeline.config import EngineConfig
+    from sitewhere_amd.pipeline.cpu_engine import CpuInboundEngine
     from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
     batches = _batches()
-    g = [GpuInboundEngine(EngineConfig.small(world=W, rank=r, str_bytes=2), device="cuda:0") for r in range(W)]
-    for r, e in enumerate(g):
-        _register(e, W, r)
-    bufs = []                                   # the device batches stay alive until processed
-    for e, (raw, offs) in zip(g, batches):
-        bufs.append((torch.from_numpy(raw).cuda(), torch.from_numpy(offs.view(np.int32)).cuda()))
-        e.prepare(*bufs[-1], len(offs) - 1, NOW, out_to_device=True)
-        e.phase_decode()
-    torch.cuda.synchronize()
-    for q in range(W):
-        for r in range(W):
-            g[q].recv_slab(r).copy_(g[r].send_slab(q))
-            g[q].t["recv_cnt"][r] = g[r].send_count(q)
-        g[q].loopback_strings(g)
-    alts = set()
-    for (raw, _), e in zip(batches, g):
-        e.phase_process()
+    one = GpuInboundEngine(EngineConfig.small(), device="cuda:0")
+    _register(one, 1, 0)
+    ref = []
+    for raw, offs in batches:
+        res = one.step(raw, offs, NOW, presence=False)
+        ref += _row_keys(one.encode_block(NOW, res, boot=0x5))
+    cfg = dict(str_bytes=2)
+    g = [GpuInboundEngine(EngineConfig.small(world=W, rank=r, **cfg), device="cuda:0") for r in range(W)]
+    c = [CpuInboundEngine(EngineConfig.small(world=W, rank=r, **cfg)) for r in range(W)]
+    for r in range(W):
+        _register(g[r], W, r)
+        _register(c[r], W, r)
+    cap, S = g[0].cfg.str_cap, g[0].cfg.shuf_cap
+    empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))
+    got, deferred = [], 0
+    for k in range(80):
+        bs = batches if k == 0 else [empty] * W
+        keep = []
+        for e, (raw, offs) in zip(g, bs):
+            keep.append((torch.from_numpy(raw).cuda(), torch.from_numpy(offs.view(np.int32)).cuda()))
+            e.prepare(*keep[-1], len(offs) - 1, NOW, out_to_device=True)
+            e.phase_decode()
         torch.cuda.synchronize()
-        res = e.collect(e._last_sel, raw, from_device=True)
-        keys = _row_keys(e.encode_block(NOW, res, boot=0x5))
-        assert e.string_drops()["slab_full"] > 0
-        alts |= {k[3] for k in keys if k[3]}
-    # stored alternate ids are well-formed "<16 hex>-<8 hex>[:k]"
-    for a in alts:
-        base = a.split(":")[0]
-        assert len(base) == 25 and base[16] == "-", a
+        for r, (e, (raw, offs)) in enumerate(zip(c, bs)):
+            recs, _ = e.decode_phase(raw, offs, NOW)
+            rw = np.asarray(raw, np.uint8)
+            send, cnt, index, nc = e.partition(recs, with_index=True, spans=e._dec_spans, raw=rw)
+            sp, buf, used = e._pack_strings(send, index, nc, e._dec_spans, rw)
+            ge = g[r]
+            p = ge._last_send_par
+            assert ge.send_cnts[p].cpu().numpy().tolist() == cnt.tolist(), (k, r)
+            assert ge.send_str_cnts[p].cpu().numpy().tolist() == used.tolist(), (k, r)
+            gsp = ge.send_spans[p].cpu().numpy().view(STR_REF).reshape(W, S)
+            gst = ge.send_strs[p].cpu().numpy().reshape(W, cap)
+            for q in range(W):
+                n = int(cnt[q])
+                assert np.array_equal(ge.send_slab(q).cpu().numpy()[:n * 64], wire_pack(send[q, :n]).view(np.uint8))
+                assert np.array_equal(gsp[q, :n], sp[q, :n]), (k, r, q)
+                assert np.array_equal(gst[q, :int(used[q])], buf[q * cap:q * cap + int(used[q])]), (k, r, q)
+            cp = ge._carry_par
+            n = int(ge.t["n_carry"][cp].item())
+            assert n == len(e.carry)
+            assert np.array_equal(ge.carry_bufs[cp][:n * EVENT_REC.itemsize].cpu().numpy(), e.carry.view(np.uint8))
+            assert np.array_equal(ge.carry_spans[cp][:n * STR_REF.itemsize].cpu().numpy().view(STR_REF), e.carry_sp)
+            nb = int(ge.t["n_carry_str"][cp].item())
+            assert nb == len(e.carry_heap)
+            assert np.array_equal(ge.carry_strs[cp][:nb].cpu().numpy(), e.carry_heap)
+            deferred += n
+        for q in range(W):
+            for r in range(W):
+                g[q].recv_slab(r).copy_(g[r].send_slab(q))
+                g[q].t["recv_cnt"][r] = g[r].send_count(q)
+            g[q].loopback_strings(g)
+        for (raw, _), e in zip(bs, g):
+            e.phase_process()
+            torch.cuda.synchronize()
+            res = e.collect(e._last_sel, raw, from_device=True)
+            got += _row_keys(e.encode_block(NOW, res, boot=0x5))
+        if k and not any(len(e.carry) for e in c):
+            break
+    assert deferred > 0 and not any(len(e.carry) for e in c)
+    for e in g:
+        assert e.string_drops() == {"oversize": 0}
+        assert e.stats_dict()["shuffle_overflow"] == 0
+    assert len(got) == len(ref)
+    assert sorted(got) == sorted(ref)
