@@ -894,9 +894,8 @@ struct DedupCounts {
 };
 
 // Claim the id's slot in `cur` (k_dedup_claim, after k_lookup validated the record).  Returns
-// the id's provisional status: DUPLICATE (held by `prev`), RECHECK (first claim, maybe stored
-// before -- records decoded on another rank skip the filter: their payload, a recheck's input, is
-// there) or OK.
+// the id's provisional status: DUPLICATE (held by `prev`), RECHECK (first claim of an id the
+// filter sees, maybe stored before; see filter_sees) or OK.
 // Everything a claim needs, read once per thread (not per id: loads through the by-value engine
 // arguments cannot be hoisted past the claim's stores).
 struct DedupClaim {
@@ -906,8 +905,16 @@ struct DedupClaim {
   ull sb;                                    // the step's first sequence
   const ull* __restrict__ bloom;
   int64_t bmask;
-  uint8_t rank;
+  int rank;                                  // filter_rank (-1: every record)
 };
+
+// Does the store-backed filter see this record?  Every record this rank owns when the strings came
+// along with the re-key (work_str: the host settles a recheck by its alternate id), else only those
+// decoded here (the host path re-reads their payload).  A record the host already settled skips it.
+__device__ __forceinline__ int filter_rank(const SwEngineArgs& a) { return a.work_str ? -1 : (int)a.rank; }
+__device__ __forceinline__ bool filter_sees(const SwEventRec& r, int rank) {
+  return !(r.flags & SW_F_SETTLED) && (rank < 0 || r.src_rank == (uint8_t)rank);
+}
 
 __device__ __forceinline__ DedupClaim dedup_claim_args(const SwEngineArgs& a) {
   DedupClaim d;
@@ -918,11 +925,11 @@ __device__ __forceinline__ DedupClaim dedup_claim_args(const SwEngineArgs& a) {
   d.sb = (ull)*a.seq_base;
   d.bloom = (const ull*)a.dd_bloom;
   d.bmask = a.dd_bloom_mask;
-  d.rank = (uint8_t)a.rank;
+  d.rank = filter_rank(a);
   return d;
 }
 
-__device__ __forceinline__ uint8_t dedup_claim(const DedupClaim& dc, ull h, int64_t i, uint8_t src_rank,
+__device__ __forceinline__ uint8_t dedup_claim(const DedupClaim& dc, ull h, int64_t i, bool filtered,
                                                DedupCounts& c) {
   const int64_t mask = dc.mask;
   ull* __restrict__ ct = dc.ct;
@@ -934,8 +941,8 @@ __device__ __forceinline__ uint8_t dedup_claim(const DedupClaim& dc, ull h, int6
     if (old == 0) {
       ++c.fresh;
       reinterpret_cast<uint32_t*>(&ct[2 * slot + 1])[0] = (uint32_t)(sb + (ull)i);
-      return (dc.bloom && src_rank == dc.rank && bloom_has(dc.bloom, dc.bmask, h)) ? (uint8_t)SW_ST_RECHECK
-                                                                                     : (uint8_t)SW_ST_OK;
+      return (dc.bloom && filtered && bloom_has(dc.bloom, dc.bmask, h)) ? (uint8_t)SW_ST_RECHECK
+                                                                          : (uint8_t)SW_ST_OK;
     }
     if (old == h) {
       atomicMin(reinterpret_cast<uint32_t*>(&ct[2 * slot + 1]) + 1, (uint32_t)i);
@@ -1014,8 +1021,9 @@ __global__ void k_dedup_claim(SwEngineArgs a) {
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     if (status[i] != SW_ST_OK) continue;
     const ull ah = recs[i].alt_hash;
-    if (!ah) continue;
-    const uint8_t st = dedup_claim(d, ah, i, recs[i].src_rank, dc);
+    // a settled recheck skips the window: its id was claimed when it came back as a recheck
+    if (!ah || (recs[i].flags & SW_F_SETTLED)) continue;
+    const uint8_t st = dedup_claim(d, ah, i, filter_sees(recs[i], d.rank), dc);
     if (st != SW_ST_OK) status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
@@ -1090,8 +1098,8 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
     uint8_t st = v ? status[i] : (uint8_t)SW_ST_OK;
     if (v && (st == SW_ST_OK || st == SW_ST_RECHECK) && dv.ct) {
       const ull h = recs[i].alt_hash;
-      if (h) {
-        const uint8_t vst = dedup_verdict(dv, h, (uint32_t)i, recs[i].src_rank == (uint8_t)rank);
+      if (h && !(recs[i].flags & SW_F_SETTLED)) {
+        const uint8_t vst = dedup_verdict(dv, h, (uint32_t)i, filter_sees(recs[i], rank));
         if (vst != st) status[i] = vst;
         st = vst;
       }
@@ -1810,7 +1818,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   // stable split ok / rejected, with the dedup verdicts
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
                                                (const ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
-                                               (const ull*)a.dd_bloom, a.dd_bloom_mask, (int)a.rank);
+                                               (const ull*)a.dd_bloom, a.dd_bloom_mask, a.work_str ? -1 : (int)a.rank);
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx, a.n_ok,
                                                a.n_rej);
   int rc = 0;

@@ -26,9 +26,17 @@
 #include "swtypes.h"
 #include "swseg.h"
 
-#define SBLK 256
+// Workgroup geometry: SW_SEG_SBLK threads per page (RPT = 1024 / SBLK rows each); SW_SEG_MIN_WAVES
+// asks the compiler for at least that many waves per SIMD (a VGPR budget).  Measured in profiles/r5_encode.
+#ifndef SW_SEG_SBLK
+#define SW_SEG_SBLK 256
+#endif
+#ifndef SW_SEG_MIN_WAVES
+#define SW_SEG_MIN_WAVES 1
+#endif
+#define SBLK SW_SEG_SBLK
 #define SWAVES (SBLK / 64)
-#define RPT 4
+#define RPT (SEG_PAGE_ROWS / SBLK)
 #define HEAP_LDS 26624     // heap bytes a page can stage in LDS (the column staging union); larger heaps
                            // are gathered straight from the raw batch
 
@@ -909,7 +917,7 @@ __device__ __forceinline__ void seg_encode_page(const SwSegArgs& a, SegLds& L) {
   SEG_STAMP(10);
 }
 
-__global__ __launch_bounds__(SBLK) void k_seg_encode(SwSegArgs a) {
+__global__ __launch_bounds__(SBLK, SW_SEG_MIN_WAVES) void k_seg_encode(SwSegArgs a) {
   __shared__ SegLds L;
   seg_encode_page(a, L);
   // ---- last workgroup out: publish the results, re-arm the state for the next launch.  Every

@@ -64,6 +64,7 @@ enum SwStatus : uint8_t {
 #define SW_F_HAS_ELEVATION 0x8
 #define SW_F_SYS_ALERT 0x10     // (API-added rows only) alert of source System with its own message
 #define SW_F_JSON 0x20          // (API-added rows only) type-specific fields as JSON in the metadata span
+#define SW_F_SETTLED 0x40       // store-backed dedup settled on the host (a recheck the store does not hold)
 
 // Decoded event record, 80 bytes.  Output of the decoder, unit of the
 // multi-GPU all-to-all, input of validation.

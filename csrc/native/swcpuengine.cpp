@@ -521,6 +521,7 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
                      SwStrRef* pspans) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
   const int T = e->T();
+  const bool any_rank = t->world > 1 && spans != nullptr;   // the work batch's strings were exchanged
   static const bool trace = getenv("SW_CE_TRACE") != nullptr;
   auto tp = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
@@ -581,7 +582,8 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
       int64_t b, end;
       chunk_of(n, w, T, &b, &end);
       for (int64_t i = b; i < end; ++i)
-        if (work[i].alt_hash && status[i] == SW_ST_OK)
+        // a settled recheck skips the window: its id was claimed when it came back as a recheck
+        if (work[i].alt_hash && status[i] == SW_ST_OK && !(work[i].flags & SW_F_SETTLED))
           e->lists[(size_t)w * T + sw_mix64(work[i].alt_hash) % (uint64_t)T].push_back((int32_t)i);
     });
     const int64_t seq_base = st->seq_base;
@@ -597,9 +599,12 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
           auto ins = m.insert(work[i].alt_hash);
           if (ins.second) {
             *ins.first = seq_base + i;
-            // first sight in the window: the store may still hold it (filter from earlier steps)
-            // (records decoded on another rank skip it: their payload, the host path's input, is there)
-            if (!e->bloom.empty() && work[i].src_rank == (uint8_t)t->rank && bloom_has(e, work[i].alt_hash))
+            // first sight in the window: the store may still hold it (filter from earlier steps).
+            // Every record this rank owns goes through it when its strings came along (the host
+            // settles a recheck by its alternate id); without the string exchange only records
+            // decoded here do (the host path re-reads their payload).  A settled record skips it.
+            if (!e->bloom.empty() && !(work[i].flags & SW_F_SETTLED) &&
+                (any_rank || work[i].src_rank == (uint8_t)t->rank) && bloom_has(e, work[i].alt_hash))
               status[i] = SW_ST_RECHECK;
           } else {
             status[i] = SW_ST_DUPLICATE;

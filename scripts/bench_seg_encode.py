@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-strings", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="also report per-page phase times (s_memrealtime)")
+    ap.add_argument("--lib", default=None, help="an encoder variant (swseg.hip built with other -DSW_SEG_* "
+                    "geometry); its blocks must equal the built-in encoder's byte for byte")
     a = ap.parse_args()
     import torch
 
@@ -57,6 +59,21 @@ def main():
     assert lib.sw_seg_aux(P(work_t.data_ptr()), P(okidx.data_ptr()), P(nok.data_ptr()), P(gen_t.data_ptr()),
                           P(wsp_t.data_ptr()), len(raw), P(cursor.data_ptr()), P(aux.data_ptr()), n,
                           P(s.cuda_stream)) == 0
+    ref_block = None
+    if a.lib:
+        # the built-in encoder's block, then time the variant
+        assert lib.sw_seg_encode(P(rows_t.data_ptr()), P(aux.data_ptr()), P(raw_t.data_ptr()), P(cursor.data_ptr()),
+                                 P(blk.data_ptr()), cap, P(state.data_ptr()), pages, P(s.cuda_stream)) == 0
+        s.synchronize()
+        nb0 = int(state[pages + 1].item())
+        ref_block = blk[:nb0].cpu().numpy().copy()
+        from ctypes import c_int32, c_int64
+        var = ctypes.CDLL(os.path.abspath(a.lib))
+        var.sw_seg_encode.restype = c_int32
+        var.sw_seg_encode.argtypes = [P, P, P, P, P, c_int64, P, c_int64, P]
+        var.sw_seg_encode_stamped.restype = c_int32
+        var.sw_seg_encode_stamped.argtypes = [P, P, P, P, P, c_int64, P, c_int64, P, P]
+        lib = var
     times = []
     for r in range(a.reps + 2):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,6 +86,8 @@ def main():
             times.append(1000.0 * e0.elapsed_time(e1))
     nb, err, _ = (int(x) for x in state[pages + 1:pages + 4].cpu().numpy())
     assert err == 0, err
+    if ref_block is not None:
+        assert nb == len(ref_block) and np.array_equal(blk[:nb].cpu().numpy(), ref_block), "variant block differs"
     phases = None
     if a.stamps:
         # one more encode with per-page phase stamps (s_memrealtime, 100 MHz = 10 ns ticks)
@@ -87,7 +106,7 @@ def main():
         phases["page_start_us"] = {q: round(float(np.percentile(x[:, 0] - t0, q)) / 1e3, 1) for q in (0, 25, 50, 75, 100)}
         phases["page_end_us"] = {q: round(float(np.percentile(x[:, 10] - t0, q)) / 1e3, 1) for q in (0, 25, 50, 75, 100)}
         phases["page_life_p50_us"] = round(float(np.median(x[:, 10] - x[:, 0])) / 1e3, 1)
-    print(json.dumps({"kernel": "k_seg_encode", "rows": n, "strings": not a.no_strings, "block_bytes": nb,
+    print(json.dumps({"kernel": "k_seg_encode", "lib": a.lib or "built-in", "rows": n, "strings": not a.no_strings, "block_bytes": nb,
                       "bytes_per_row": round(nb / n, 3), "mean_us": round(float(np.mean(times)), 1),
                       "min_us": round(float(np.min(times)), 1), "reps": a.reps, "phases": phases}), flush=True)
 

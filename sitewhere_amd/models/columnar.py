@@ -35,6 +35,7 @@ F_HAS_UPDATE_STATE = 0x1
 F_UPDATE_STATE = 0x2
 F_HAS_DATE = 0x4
 F_HAS_ELEVATION = 0x8
+F_SETTLED = 0x40       # store-backed dedup settled on the host: the filter skips the record
 
 EVENT_REC = np.dtype([
     ("fp_lo", "<u8"), ("fp_hi", "<u8"), ("event_date", "<i8"), ("name_hash", "<u8"),

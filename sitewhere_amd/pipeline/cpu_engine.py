@@ -13,7 +13,7 @@ import numpy as np
 from ..models.columnar import (EVENT_REC, OUT_REC, EV_ALERT, EV_LOCATION, EV_MEASUREMENT, EV_STATE_CHANGE,
                                EV_DECODE_ERROR, ST_OK, ST_UNREGISTERED, ST_UNASSIGNED, ST_DUPLICATE,
                                ST_DECODE_ERROR, ST_CONTROL, ST_RECHECK, STAT_NAMES, N_STATS, STR_REF, WIRE_REC,
-                               wire_pack, wire_unpack)
+                               F_SETTLED, wire_pack, wire_unpack)
 from .config import EngineConfig
 from .engine_base import EngineBase, StepResult
 from .fleet import cpu_decode
@@ -248,6 +248,26 @@ class CpuInboundEngine(EngineBase):
     def carry_count(self) -> int:
         return len(self.carry)
 
+    def rechecks(self, res):
+        """The step's rechecks with their strings (records, refs, heap), or None (see
+        ``pipeline/recheck.py``)."""
+        return res.recheck
+
+    def inject_settled(self, recs, spans, heap):
+        """Re-inject records whose store-backed dedup the host settled (false positives of the
+        filter) at the end of the re-key carry, with their strings; the next round processes them,
+        the filter skipping them (``F_SETTLED``)."""
+        from .recheck import rebase_into
+        if self.world == 1:
+            raise RuntimeError("settled records re-enter through the re-key carry (several ranks)")
+        if (len(self.carry) + len(recs) > self.cfg.carry_cap
+                or len(self.carry_heap) + len(heap) > self.cfg.carry_str_cap):
+            raise RuntimeError("re-key carry full: settle after a drain round")
+        r, sp = rebase_into(recs, spans, len(self.carry_heap), F_SETTLED)
+        self.carry_sp = np.concatenate([self._carry_spans_full(), sp])
+        self.carry = np.concatenate([self.carry, r])
+        self.carry_heap = np.concatenate([self.carry_heap, np.asarray(heap, np.uint8)])
+
     def _carry_spans_full(self) -> np.ndarray:
         sp = self.carry_sp
         if len(sp) != len(self.carry):             # carry built without strings
@@ -328,7 +348,7 @@ class CpuInboundEngine(EngineBase):
                 status[i] = ST_OK if (a >= 0 and self.asg_active[a]) else ST_UNASSIGNED
         return status, dev, asg
 
-    def _dedup(self, recs, status):
+    def _dedup(self, recs, status, any_rank: bool = False):
         """Generational window, the oracle of k_dedup_rotate / k_dedup_insert / k_dedup_check: ids of
         the previous generation are duplicates; otherwise the first occurrence in the current
         generation wins.  Before a batch that could push the current generation past half the
@@ -341,15 +361,19 @@ class CpuInboundEngine(EngineBase):
         cur = self.dedup
         for i in range(len(recs)):
             h = int(recs[i]["alt_hash"])
-            if h == 0 or status[i] != ST_OK:
+            # a settled recheck skips the window: its id was claimed when it came back as a recheck
+            if h == 0 or status[i] != ST_OK or int(recs[i]["flags"]) & F_SETTLED:
                 continue
             if h in prev or h in cur:
                 status[i] = ST_DUPLICATE
             else:
                 cur[h] = self.seq_base + i
-                # maybe stored before: the host checks (records decoded on another rank skip the
-                # filter -- their payload, which the host path needs, is on that rank)
-                if self.bloom is not None and int(recs[i]["src_rank"]) == self.rank and self._bloom_has(h):
+                # maybe stored before: the host checks.  The filter sees every record this rank
+                # owns when their strings came along (``any_rank``: the host settles a recheck by its
+                # alternate id), else only records decoded here (the host path re-reads their
+                # payload); a record the host already settled skips it
+                if (self.bloom is not None and not (int(recs[i]["flags"]) & F_SETTLED)
+                        and (any_rank or int(recs[i]["src_rank"]) == self.rank) and self._bloom_has(h)):
                     status[i] = ST_RECHECK
 
     def reset_dedup(self):
@@ -447,6 +471,11 @@ class CpuInboundEngine(EngineBase):
         res = self.process_phase(work, len(offs) - 1, now_ms, new, presence, spans=spans)
         if spans is not None:
             res.raw = src
+            if self.world > 1:
+                # the owner settles them by alternate id: their strings, before the block encoder
+                # lets go of the string source
+                from .recheck import host_rechecks
+                res.recheck = host_rechecks(res)
         return res
 
     def decode_phase(self, raw, offs, now_ms):
@@ -465,7 +494,7 @@ class CpuInboundEngine(EngineBase):
     def process_phase(self, work, n_msgs, now_ms, new, presence=None, spans=None) -> StepResult:
         first_seq = self.cursor
         status, dev, asg = self._lookup(work)
-        self._dedup(work, status)
+        self._dedup(work, status, any_rank=self.world > 1 and spans is not None)
         ok = np.nonzero(status == ST_OK)[0]
         rej = np.nonzero(status != ST_OK)[0]
         for i in ok:
@@ -539,7 +568,7 @@ class CpuInboundEngine(EngineBase):
         return StepResult(n_msgs=n_msgs, n_events=len(work), n_persisted=len(out_rows),
                           out=np.array(out_rows, OUT_REC), rejects=work[rej], reject_status=status[rej],
                           new_names=new, first_seq=first_seq, world=self.world, rank=self.rank, prec=prec,
-                          pspans=pspans)
+                          pspans=pspans, rspans=spans[rej] if spans is not None and self.world > 1 else None)
 
     # ------------------------------------------------------------------ checkpoint / resume
     kind = "cpu"

@@ -71,6 +71,11 @@ class StepResult:
     prec: np.ndarray | None = None
     pspans: np.ndarray | None = None
     raw: np.ndarray | None = None
+    # several ranks, strings exchanged: string refs of ``rejects`` (into ``raw``: host engines) or
+    # the step's rechecks with their strings (records, refs, heap: MI355X engine), which the owner
+    # settles by alternate id (``pipeline/recheck.py``)
+    rspans: np.ndarray | None = None
+    recheck: tuple | None = None
 
     def event_ids(self) -> np.ndarray:
         n = 0 if self.out is None else len(self.out)

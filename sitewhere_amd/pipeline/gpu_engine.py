@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from .._native import gpu as gpu_lib
-from ..models.columnar import EVENT_REC, N_STATS, OUT_REC, NAME_REF, OUT_REC_SIZE, STR_REF, WIRE_REC
+from ..models.columnar import EVENT_REC, N_STATS, OUT_REC, NAME_REF, OUT_REC_SIZE, ST_RECHECK, STR_REF, WIRE_REC
 from ..ops.engine_abi import SwEngineArgs
 from .config import EngineConfig
 from .bus_io import host_view
@@ -807,8 +807,48 @@ class GpuInboundEngine(EngineBase):
             rst = self.t["status"][rej_idx].cpu().numpy()
         else:
             rows, rst = np.zeros(0, EVENT_REC), np.zeros(0, np.uint8)
+        recheck = None
+        if n_rej and self.world > 1 and self.cfg.str_cap:
+            rk = np.nonzero(rst == ST_RECHECK)[0]
+            if len(rk):
+                # the owner settles them by alternate id: their strings, gathered from work_str
+                from .recheck import compact_strings
+                ridx = rej_idx[torch.from_numpy(rk).to(rej_idx.device)]
+                sp = self.t["work_spans"].view(-1, STR_REF.itemsize)[ridx].cpu().numpy().reshape(-1).view(STR_REF)
+                ws = self.t["work_str"]
+                recheck = compact_strings(rows[rk], sp, lambda pos: ws[torch.from_numpy(pos).to(ws.device)].cpu().numpy())
         return dict(n_msgs=int(self.args.n_msgs), n_events=sc["n_work"], n_persisted=sc["n_out"], rejects=rows,
-                    reject_status=rst, new_names=new, first_seq=first_seq)
+                    reject_status=rst, new_names=new, first_seq=first_seq, recheck=recheck)
+
+    def rechecks(self, res):
+        """The step's rechecks with their strings (records, refs, heap), or None (see
+        ``pipeline/recheck.py``)."""
+        return res.recheck
+
+    def inject_settled(self, recs, spans, heap):
+        """Re-inject records whose store-backed dedup the host settled at the end of the re-key
+        carry the next partition reads, strings appended to its heap (``F_SETTLED``: the filter
+        skips them).  Call between rounds."""
+        from ..models.columnar import F_SETTLED
+        from .recheck import rebase_into
+        if self.world == 1 or not self.cfg.str_cap:
+            raise RuntimeError("settled records re-enter through the re-key carry (several ranks, strings on)")
+        self._sync_streams()
+        cp = self._carry_par
+        n, nb, k = int(self.t["n_carry"][cp].item()), int(self.t["n_carry_str"][cp].item()), len(recs)
+        heap = np.asarray(heap, np.uint8)
+        if n + k > self.cfg.carry_cap or nb + len(heap) > self.cfg.carry_str_cap:
+            raise RuntimeError("re-key carry full: settle after a drain round")
+        r, sp = rebase_into(recs, spans, nb, F_SETTLED)
+        ri, si = EVENT_REC.itemsize, STR_REF.itemsize
+        self.carry_bufs[cp][n * ri:(n + k) * ri].copy_(torch.from_numpy(np.ascontiguousarray(r).view(np.uint8)))
+        self.carry_spans[cp][n * si:(n + k) * si].copy_(torch.from_numpy(np.ascontiguousarray(sp).view(np.uint8)))
+        if len(heap):
+            self.carry_strs[cp][nb:nb + len(heap)].copy_(torch.from_numpy(heap))
+        self.t["n_carry"][cp] = n + k
+        self.t["n_carry_str"][cp] = nb + len(heap)
+        self.__dict__.pop("_carry_seen", None)
+        self._sync_streams()
 
     # ------------------------------------------------------------------ overlapped framed steps
     def submit_framed(self, batch, now_ms: int, token=None, presence: bool | None = None) -> list:

@@ -73,6 +73,9 @@ class NativeCpuEngine(CpuInboundEngine):
         self.group = group
         self.exchange = None
         self.carry = np.zeros(0, EVENT_REC)
+        self.carry_sp = np.zeros(0, STR_REF)        # the carry's strings (CpuInboundEngine.partition)
+        self.carry_heap = np.zeros(0, np.uint8)
+        self.str_drops = [0, 0]
         self.store = {k: np.zeros(cfg.store_cap, t) for k, t in STORE_COLS.items()}
         self.cursor = 0
         self.seq_base = 0
@@ -206,7 +209,8 @@ class NativeCpuEngine(CpuInboundEngine):
         return StepResult(n_msgs=n_msgs, n_events=n, n_persisted=n_out, out=out[:n_out],
                           rejects=work[rej], reject_status=status[rej].copy(), new_names=new, first_seq=first_seq,
                           world=self.world, rank=self.rank, prec=prec[:n_out],
-                          pspans=pspans[:n_out] if pspans is not None else None)
+                          pspans=pspans[:n_out] if pspans is not None else None,
+                          rspans=spans[rej] if spans is not None and self.world > 1 else None)
 
     def _out_buffer(self, n: int, dtype=OUT_REC) -> np.ndarray:
         """An outbound buffer (rows, or the rows' records / string refs) no earlier StepResult still

@@ -506,3 +506,94 @@ def test_gloo_skewed_strings_are_lossless():
             assert alt not in got, alt                         # stored once
             got[alt] = (msg, md)
     assert got == want
+
+
+def _gloo_dedup_worker(rank, world, port, q, bloom_bits):
+    import torch
+    import torch.distributed as dist
+    from sitewhere_amd.persistence.segments import decode_block, row_strings
+    from sitewhere_amd.pipeline.recheck import settle_rechecks
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a window of a few batches (it rotates twice before the replay), the store-backed filter on
+    e = CpuInboundEngine(EngineConfig.small(world=world, rank=rank, max_msgs=800, dedup_slots=1 << 12,
+                                            dedup_bloom_bits=bloom_bits))
+    shard_fleet(e, world, rank)
+    fresh = [_skewed_string_batch(world, rank, k) for k in range(6)]
+    batches = fresh + [fresh[0]]              # the first batch again, long after the window forgot it
+    empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))
+    store: dict = {}                          # this rank's event store: alternate id -> times stored
+    nxt = rounds = 0
+    settled = {"rechecks": 0, "duplicates": 0, "injected": 0}
+    while True:
+        if nxt < len(batches) and not e.should_stall():
+            raw, offs = batches[nxt]
+            nxt += 1
+        else:
+            raw, offs = empty
+        res = e.step(raw, offs, NOW, presence=False)
+        if res.n_persisted:
+            c = decode_block(e.encode_block(NOW, res, boot=0x78))
+            for i in range(len(c["date"])):
+                alt = row_strings(c, i)[0]
+                store[alt] = store.get(alt, 0) + 1
+        for k, v in settle_rechecks(e, res, lambda ids: [a in store for a in ids]).items():
+            settled[k] += v
+        rounds += 1
+        left = torch.tensor([len(batches) - nxt + e.carry_count()], dtype=torch.int64)
+        dist.all_reduce(left)
+        if int(left) == 0 or rounds > 600:
+            break
+    s = e.stats_dict()
+    q.put((rank, store, settled, s["dedup_rotations"], s["duplicates"], s["shuffle_overflow"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_gloo_dedup(bloom_bits):
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_dedup_worker, args=(r, 2, port, q, bloom_bits)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted((q.get(timeout=300) for _ in range(2)), key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {f"lossless-{r}-{k:04d}-{i:05d}-".ljust(60, "x") for r in range(2) for k in range(6) for i in range(800)}
+    got: dict = {}
+    for _, store, *_ in outs:
+        for alt, n in store.items():
+            assert n == 1 and alt not in got, alt                    # stored once
+            got[alt] = n
+    assert set(got) == want
+    return outs
+
+
+def test_gloo_replay_beyond_window_is_caught_on_the_owner():
+    """two gloo ranks, skewed keys -- every record is decoded on one rank
+    and owned by the other.  After the dedup window has rotated past the first batch, both ranks
+    send it again: the owner's store-backed filter flags every replayed id (records decoded on
+    another rank go through it too, their strings came along), the owner settles them by alternate
+    id against its store, and all 1,600 are duplicates -- 800 caught on each rank."""
+    outs = _run_gloo_dedup(1 << 20)
+    for rank, store, settled, rotations, dups, overflow in outs:
+        assert rotations >= 2 and overflow == 0, (rank, rotations, overflow)
+        assert settled["duplicates"] == 800, (rank, settled)
+
+
+def test_gloo_filter_false_positives_are_settled_and_stored_once():
+    """A filter far too small for the ids (8 blocks: nearly every id is a false positive): the
+    owners settle each recheck by alternate id; the ids the store does not hold go back into the
+    re-key carry, filter-settled, and are stored exactly once with their strings; the replay is
+    still caught."""
+    outs = _run_gloo_dedup(1 << 9)
+    for rank, store, settled, rotations, dups, overflow in outs:
+        assert settled["injected"] > 1000 and settled["duplicates"] == 800, (rank, settled)
