@@ -498,12 +498,21 @@ def main():
     if reads is not None:
         reads.start()
     t_start = time.perf_counter()
+    t_steps = []
     for k in range(args.warmup, args.warmup + args.steps):
         run(k)
+        t_steps.append(time.perf_counter())
     finish()
+    t_fin = time.perf_counter()
     read_stats = reads.stop() if reads is not None else None
     barrier()
     elapsed = time.perf_counter() - t_start
+    # where the timed region went (rank 0's clock): submit intervals of the steps, then the drain
+    # (the steps still in flight, their blocks made durable)
+    step_ms = np.diff(np.asarray([t_start] + t_steps)) * 1e3
+    timeline = {"submit_ms_p50": round(float(np.median(step_ms)), 3), "submit_ms_max": round(float(step_ms.max()), 3),
+                "submit_ms_first3": [round(float(x), 3) for x in step_ms[:3]],
+                "drain_ms": round((t_fin - t_steps[-1]) * 1e3, 3)} if len(step_ms) else None
     s1 = eng.stats_dict()
     ev = s1["events"] - s0["events"]
     persisted = s1["persisted"] - s0["persisted"]
@@ -565,6 +574,7 @@ def main():
         "backend": dist.get_backend() if world > 1 else None,
         "world": dist.get_world_size() if world > 1 else 1,
         "rank_elapsed_s": per_rank if per_rank is not None else [round(rank_elapsed, 6)],
+        "timeline_rank0": timeline,
         "conservation": {"ok": conservation_ok, "failed": [k for k, v in checks.items() if not v],
                          "checked": len(checks)},
     }

@@ -6,11 +6,11 @@
 // enriched row (rows[j], 32 B) and its encoder aux (aux[j], SwSegAux 32 B: elevation, SEG_FLAGS and
 // the string refs into the raw batch, which is still resident in HBM).  No record is gathered here.
 //
-// One 256-thread workgroup (4 wave64) per 1024-row page, 4 consecutive rows per thread.  The plan
+// One 512-thread workgroup (8 wave64) per 1024-row page, 2 consecutive rows per thread.  The plan
 // is a few fused block-wide rounds instead of one scan / reduction per column:
 //   R1  first row with an alternate id (its first 64 bytes staged in LDS); per double column the
 //       decimal exponent (max of the rows' exponents, searched from a per-column hint)
-//   R2  alternate ids read with aligned 8-byte loads (all four rows' loads in flight at once): common
+//   R2  alternate ids read with aligned 8-byte loads (all the thread's rows' loads in flight at once): common
 //       prefix with the first id (word xor + ctz), last non-hex byte and the value of the trailing hex
 //       digits in one register pass; every integer column's min / max; quantised double min / max
 //   R3  one multi-column scan: member indices of all 15 columns, exception indices, heap offsets
@@ -27,12 +27,15 @@
 #include "swseg.h"
 
 // Workgroup geometry: SW_SEG_SBLK threads per page (RPT = 1024 / SBLK rows each); SW_SEG_MIN_WAVES
-// asks the compiler for at least that many waves per SIMD (a VGPR budget).  Measured in profiles/r5_encode.
+// asks the compiler for at least that many waves per SIMD (a VGPR budget).  Measured in
+// profiles/r5_encode (1M rows with strings): 256 threads at 221 VGPRs (2 waves / SIMD) 181 us; 512
+// threads held to 128 VGPRs (4 waves / SIMD, 18 spilled) 156 us -- twice the waves per page and per
+// CU hide the page's dependent load rounds; 1024 threads 189 us (one page per CU).
 #ifndef SW_SEG_SBLK
-#define SW_SEG_SBLK 256
+#define SW_SEG_SBLK 512
 #endif
 #ifndef SW_SEG_MIN_WAVES
-#define SW_SEG_MIN_WAVES 1
+#define SW_SEG_MIN_WAVES 4
 #endif
 #define SBLK SW_SEG_SBLK
 #define SWAVES (SBLK / 64)
@@ -346,7 +349,7 @@ __device__ __forceinline__ void seg_encode_page(const SwSegArgs& a, SegLds& L) {
   const int64_t r0 = (int64_t)page * SEG_PAGE_ROWS;
   const int m = (int)(n - r0 < SEG_PAGE_ROWS ? n - r0 : SEG_PAGE_ROWS);
   SEG_STAMP(0);
-  // ---- load 4 consecutive rows per thread: enriched row + encoder aux (both coalesced)
+  // ---- load RPT consecutive rows per thread: enriched row + encoder aux (both coalesced)
   SRow R[RPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
@@ -430,7 +433,7 @@ __device__ __forceinline__ void seg_encode_page(const SwSegArgs& a, SegLds& L) {
   {
     const uint32_t plim = a_len0 < SEG_ALT_PFX_MAX ? a_len0 : SEG_ALT_PFX_MAX;
     ull lcp = ~0ull, lnh = 0, lmin = ~0ull, lmax = 0;
-    // first 64 bytes of every row's id: all four rows' loads issued before any is used
+    // first 64 bytes of every row's id: all the thread's rows' loads issued before any is used
     ull W[RPT][8];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
