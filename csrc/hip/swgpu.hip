@@ -929,13 +929,16 @@ __device__ __forceinline__ DedupClaim dedup_claim_args(const SwEngineArgs& a) {
   return d;
 }
 
-// `maybe_stored`: the filter holds the id's bits (probed by the caller before the claim, so its
-// load is in flight beside the retired-generation probe and the CAS instead of after them).
+// `maybe_stored`: the filter holds the id's bits and sees this record (a first claim is a recheck).
+// `check_prev`: the id may be in the retired generation.  Every id a generation holds was persisted
+// (or was a recheck, itself a filter hit), and every persisted id is in the store-backed filter, so
+// an id the filter does not hold cannot be there: with the filter on, its probe (needed for the
+// recheck anyway) stands in for the retired-generation probe of every fresh id.
 __device__ __forceinline__ uint8_t dedup_claim(const DedupClaim& dc, ull h, int64_t i, bool maybe_stored,
-                                               DedupCounts& c) {
+                                               bool check_prev, DedupCounts& c) {
   const int64_t mask = dc.mask;
   ull* __restrict__ ct = dc.ct;
-  if (dd_find(dc.pt, mask, h)) return SW_ST_DUPLICATE;
+  if (check_prev && dd_find(dc.pt, mask, h)) return SW_ST_DUPLICATE;
   const ull sb = dc.sb;
   int64_t slot = (int64_t)(h & (ull)mask);
   for (int64_t p = 0; p <= mask && p < MAX_PROBE; ++p) {
@@ -1024,8 +1027,8 @@ __global__ void k_dedup_claim(SwEngineArgs a) {
     const ull ah = recs[i].alt_hash;
     // a settled recheck skips the window: its id was claimed when it came back as a recheck
     if (!ah || (recs[i].flags & SW_F_SETTLED)) continue;
-    const bool maybe = d.bloom && filter_sees(recs[i], d.rank) && bloom_has(d.bloom, d.bmask, ah);
-    const uint8_t st = dedup_claim(d, ah, i, maybe, dc);
+    const bool held = d.bloom && bloom_has(d.bloom, d.bmask, ah);
+    const uint8_t st = dedup_claim(d, ah, i, held && filter_sees(recs[i], d.rank), !d.bloom || held, dc);
     if (st != SW_ST_OK) status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
@@ -1348,8 +1351,8 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
 
 // This step's persisted alternate ids -> the store-backed dedup filter.  Reads the ring's alt
 // column (coalesced) for the step's device rows; runs on a side stream beside the rest of the
-// process phase (its atomics overlap the state, rule and presence kernels), joined before
-// k_step_end moves the cursor.
+// process phase (its atomics overlap the rule and presence kernels), joined before k_step_end
+// moves the cursor.
 __global__ void k_bloom_step(SwEngineArgs a) {
   const uint32_t n = *a.n_ok < (uint32_t)a.rec_cap ? *a.n_ok : (uint32_t)a.rec_cap;
   const int64_t cur = *a.store_cursor;
@@ -1922,6 +1925,10 @@ static int phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t
   // string refs of the work batch: the decoder's (one rank) or the exchange's (rebased into work_str)
   const SwStrRef* wsp = a.world > 1 ? a.work_spans : a.spans;
   k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap, wsp, nullptr);
+  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap, nullptr);
+  // the filter adds (one memory-side atomic each) beside the rules and presence (compute and a
+  // few atomics) rather than beside the state merge (atomic-bound: measured 58 -> 105 us when the
+  // two overlapped)
   bool joined = true;
   if (a.dd_bloom) {
     if (side) {
@@ -1934,7 +1941,6 @@ static int phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t
       k_bloom_step<<<g, BLK, 0, s>>>(a);
     }
   }
-  k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap, nullptr);
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
   if (a.n_tests > 0) {
