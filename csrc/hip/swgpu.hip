@@ -1254,7 +1254,11 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
       a.s_v0[row] = r.v0;
       a.s_v1[row] = r.v1;
       a.s_v2[row] = r.v2;
-      a.s_alt[row] = r.alt_hash;       // k_bloom_step adds it to the store-backed filter
+      a.s_alt[row] = r.alt_hash;
+      // into the store-backed filter, in line: a separate pass over the ring's alt column measured
+      // 65 us per 1M-payload step (and slowed whatever ran beside it) against ~13 us here, where
+      // the no-return atomic hides behind the row's other memory traffic (profiles/r5_kernels)
+      if (a.dd_bloom && r.alt_hash) bloom_add((ull*)a.dd_bloom, a.dd_bloom_mask, r.alt_hash);
       a.s_aux[row] = ((ull)r.src_rank << 48) | ((ull)r.aux_len << 32) | (ull)r.aux_off;
       a.s_batch[row] = (int32_t)a.sp->batch_seq;
       SwOutRec o;
@@ -1346,19 +1350,6 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     if (loc) slot = -2 - (int64_t)asg;
     if (plain && !winner) slot = -1;
     reinterpret_cast<longlong2*>(a.ev_slot)[j] = make_longlong2(slot, (int64_t)(plain ? (d | EV_PLAIN) : d));
-  }
-}
-
-// This step's persisted alternate ids -> the store-backed dedup filter.  Reads the ring's alt
-// column (coalesced) for the step's device rows; runs on a side stream beside the rest of the
-// process phase (its atomics overlap the rule and presence kernels), joined before k_step_end
-// moves the cursor.
-__global__ void k_bloom_step(SwEngineArgs a) {
-  const uint32_t n = *a.n_ok < (uint32_t)a.rec_cap ? *a.n_ok : (uint32_t)a.rec_cap;
-  const int64_t cur = *a.store_cursor;
-  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
-    const ull h = a.s_alt[(cur + j) % a.store_cap];
-    if (h) bloom_add((ull*)a.dd_bloom, a.dd_bloom_mask, h);
   }
 }
 
@@ -1892,16 +1883,8 @@ __global__ void k_cl_prep(const uint32_t* __restrict__ ok_idx, const uint32_t* _
 int sw_radix_sort_u32(uint32_t* keys, uint32_t* vals, const uint32_t* n_ptr, int64_t cap, int bits, uint32_t* hist,
                       uint32_t* vals_final, hipStream_t s);
 
-// A second stream inside the captured process phase: work that can run beside the main chain.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
-// Phase D: validate, dedup, persist, enrich, state, rules, presence.  `side` (graph capture only):
-// the store-backed filter add forks onto it after the persist and joins before k_step_end; without
-// it (direct launches) the add runs in line.
-static int phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s, SideStream* side) {
+// Phase D: validate, dedup, persist, enrich, state, rules, presence.
+int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) {
   const SwEngineArgs a = *ap;
   const int g = grid_for(a.rec_cap);
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
@@ -1926,21 +1909,6 @@ static int phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t
   const SwStrRef* wsp = a.world > 1 ? a.work_spans : a.spans;
   k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap, wsp, nullptr);
   k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap, nullptr);
-  // the filter adds (one memory-side atomic each) beside the rules and presence (compute and a
-  // few atomics) rather than beside the state merge (atomic-bound: measured 58 -> 105 us when the
-  // two overlapped)
-  bool joined = true;
-  if (a.dd_bloom) {
-    if (side) {
-      if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
-        return -7;
-      k_bloom_step<<<g, BLK, 0, side->s>>>(a);
-      if (hipEventRecord(side->join, side->s) != hipSuccess) return -7;
-      joined = false;
-    } else {
-      k_bloom_step<<<g, BLK, 0, s>>>(a);
-    }
-  }
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
   if (a.n_tests > 0) {
@@ -1961,13 +1929,8 @@ static int phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t
   // generated events persist after the step's device events (store cursor + n_ok)
   k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap, nullptr, a.n_ok);
   k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen, gcap, a.n_ok);
-  if (!joined && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) return -7;
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
-}
-
-int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) {
-  return phase_process(ap, scratch4, s, nullptr);
 }
 
 __global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int64_t presence_ms,
@@ -2005,25 +1968,11 @@ int sw_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batch_seq, int6
 int sw_graph_capture_process(const SwEngineArgs* ap, uint32_t* scratch4, int32_t with_unpack, hipStream_t s,
                              void** exec_out) {
   hipGraph_t g = nullptr;
-  // the side stream and its events only shape the graph (a parallel branch): released after capture
-  SideStream side;
-  if (hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&side.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&side.join, hipEventDisableTiming) != hipSuccess)
-    return 4000;
-  struct Release {
-    SideStream& x;
-    ~Release() {
-      if (x.fork) (void)hipEventDestroy(x.fork);
-      if (x.join) (void)hipEventDestroy(x.join);
-      if (x.s) (void)hipStreamDestroy(x.s);
-    }
-  } release{side};
   hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) return 5000 + (int)e;
   int rc = 0;
   if (with_unpack) rc = sw_phase_unpack(ap, s);
-  if (!rc) rc = phase_process(ap, scratch4, s, &side);
+  if (!rc) rc = sw_phase_process(ap, scratch4, s);
   e = hipStreamEndCapture(s, &g);
   if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
   if (e != hipSuccess) return 6000 + (int)e;
