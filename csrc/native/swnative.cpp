@@ -331,6 +331,21 @@ int32_t sw_varint_offsets(const uint8_t* lens, int64_t nbytes, int64_t n_msgs, i
   int shift = 0;
   offs[0] = 0;
   for (int64_t i = 0; i < nbytes; ++i) {
+    // fast path: 8 single-byte lengths (payloads under 128 bytes, the common case) at once
+    if (shift == 0 && i + 8 <= nbytes && k + 8 <= n_msgs) {
+      uint64_t w;
+      memcpy(&w, lens + i, 8);
+      if ((w & 0x8080808080808080ull) == 0) {
+        for (int j = 0; j < 8; ++j) {
+          acc += (w >> (8 * j)) & 0xff;
+          offs[k + 1 + j] = (uint32_t)acc;
+        }
+        if (acc > 0xffffffffull) return -4;
+        k += 8;
+        i += 7;
+        continue;
+      }
+    }
     const uint8_t b = lens[i];
     if (shift > 28) return -2;
     cur |= (uint64_t)(b & 0x7f) << shift;
