@@ -397,6 +397,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         it arrives (the event sources' latency bound holds)."""
         group = []                                      # [(record, parsed batch)] of one partition, consecutive
         resubmitted = set()
+        pre = self._prevalidate(recs)
 
         def flush():
             if not group:
@@ -418,7 +419,7 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
                     self.checkpoint()
             group.clear()
 
-        for r in recs:
+        for ri, r in enumerate(recs):
             tp = (r.topic, r.partition)
             self._raise_store_error()                   # before any new step, never after
             if r.offset < self._stored_hw.get(tp, -1):
@@ -442,8 +443,9 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             # record is DMA'd to the MI355X in place.  The record timestamp is the batch's receive
             # time, so replay after a restore is deterministic.
             try:
-                batch = parse_raw_batch(r.value)
-                batch.validate()
+                batch, err = pre[ri]
+                if err is not None:
+                    raise err
                 if batch.n_msgs > self.engine_cfg.max_msgs:
                     raise ValueError(f"raw batch of {batch.n_msgs} payloads exceeds the engine's "
                                      f"max_msgs={self.engine_cfg.max_msgs}")
@@ -472,6 +474,27 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             end = getattr(self.ms.instance.bus, "end_offset", None)
             if end is None or end(last.topic, last.partition) <= last.offset + 1:
                 self._drain_engine()                    # nothing more queued: complete the last batch
+
+    def _prevalidate(self, recs) -> list:
+        """(parsed batch, None) or (None, ValueError) per record: the framing of every record of a
+        poll checked at once, on a small pool (the native length parse releases the interpreter),
+        instead of one after another on the consumer thread that also drives the engine -- with
+        alternate ids a 64K-payload record's lengths mix one- and two-byte varints and take ~0.1 ms
+        to check, a quarter of that thread's time per step (profiles/r5_tenant)."""
+        def one(r):
+            try:
+                b = parse_raw_batch(r.value)
+                b.validate()
+                return b, None
+            except ValueError as e:
+                return None, e
+        if len(recs) < 2:
+            return [one(r) for r in recs]
+        pool = self.__dict__.get("_val_pool")
+        if pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            pool = self._val_pool = ThreadPoolExecutor(4, thread_name_prefix="raw-validate")
+        return list(pool.map(one, recs))
 
     def _dead_letter_raw(self, r, err, commit):
         """Park a raw record that cannot be stepped (corrupt framing, over-size batch) on
