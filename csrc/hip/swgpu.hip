@@ -1007,6 +1007,13 @@ __global__ void k_lookup(SwEngineArgs a) {
     a.status[i] = st;
     a.ev_dev[i] = dev;
     a.ev_asg[i] = asg;
+    // the claim's input, dense: the id to claim (0: none -- not valid, no id, or settled) and
+    // whether the store-backed filter sees the record (ev_slot is free until k_persist)
+    const SwEventRec& r = recs[i];
+    const bool claim = st == SW_ST_OK && r.alt_hash && !(r.flags & SW_F_SETTLED);
+    ull* ck = reinterpret_cast<ull*>(a.ev_slot);
+    ck[i] = claim ? r.alt_hash : 0ull;
+    reinterpret_cast<uint8_t*>(ck + a.rec_cap)[i] = (uint8_t)filter_sees(r, filter_rank(a));
   }
 }
 
@@ -1020,15 +1027,16 @@ __global__ void k_dedup_claim(SwEngineArgs a) {
   DedupCounts dc = {0u, 0u, 0u};
   const DedupClaim d = dedup_claim_args(a);
   const uint32_t n = *a.n_work;
-  const SwEventRec* __restrict__ recs = a.work;
   uint8_t* __restrict__ status = a.status;
+  // k_lookup's dense claim list: the id (0: nothing to claim; a settled recheck skips the window,
+  // its id was claimed when it came back as a recheck) and the filter's view of the record
+  const ull* __restrict__ ck = reinterpret_cast<const ull*>(a.ev_slot);
+  const uint8_t* __restrict__ cf = reinterpret_cast<const uint8_t*>(ck + a.rec_cap);
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
-    if (status[i] != SW_ST_OK) continue;
-    const ull ah = recs[i].alt_hash;
-    // a settled recheck skips the window: its id was claimed when it came back as a recheck
-    if (!ah || (recs[i].flags & SW_F_SETTLED)) continue;
+    const ull ah = ck[i];
+    if (!ah) continue;
     const bool held = d.bloom && bloom_has(d.bloom, d.bmask, ah);
-    const uint8_t st = dedup_claim(d, ah, i, held && filter_sees(recs[i], d.rank), !d.bloom || held, dc);
+    const uint8_t st = dedup_claim(d, ah, i, held && cf[i], !d.bloom || held, dc);
     if (st != SW_ST_OK) status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
