@@ -1206,17 +1206,9 @@ __device__ __forceinline__ int64_t ms_slot(SwMsSlot* __restrict__ ms, int64_t ma
 // of the device-state merge (max event date per assignment location / per (assignment, name)
 // slot).  The (assignment, name) slot found or claimed here is kept in ev_slot[j] for pass 2, so
 // the name probe and the state-map probe run once per event instead of once per pass.
-//
-// State merges without atomics where the order allows: in the clustered persist order (rows stable
-// by assignment) an assignment's rows are consecutive, so when a row's whole assignment run lies
-// within STATE_RUN lanes of it inside its wave, the run's lanes decide among themselves which one
-// writes each state word -- the latest date, then the highest lane (= the highest event id) -- and
-// that lane stores plainly (memory-side atomics are the scarce resource here: ~2 per event, ~60 us
-// per 1M ids each, scripts/bench_dedup_micro.py).  Runs that reach a wave edge or further keep the
-// atomics.  Pass 2 gets the decision in bit 63 of the work item's date.
-#define STATE_RUN 8
-#define EV_PLAIN (1ull << 63)
-
+// Tried and measured in round 5 (profiles/r5_kernels): plain stores for the state words of rows alone
+// in their assignment's run (clustered order), and the filter adds as their own pass on a parallel
+// graph branch -- neither made the phase faster, so the merges stay atomic and the adds in line.
 __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, const uint32_t* __restrict__ idx,
                           const int32_t* __restrict__ devs, const int32_t* __restrict__ asgs,
                           const uint32_t* __restrict__ n_ptr, uint32_t cap, const SwStrRef* __restrict__ spans,
@@ -1232,96 +1224,50 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
   const int64_t now = a.sp->now_ms;
   SwSegAux* const aux = reinterpret_cast<SwSegAux*>(a.sp->aux);
   const int64_t raw_bytes = a.sp->raw_bytes;
-  const bool clustered = idx != nullptr && a.cl_bits > 0;
-  const uint32_t lane = lane_id();
-  // wave-uniform loop: every lane takes part in the run shuffles
-  for (int64_t j0 = (int64_t)BID * BLK + (threadIdx.x & ~63u); j0 < (int64_t)n; j0 += (int64_t)gridDim.x * BLK) {
-    const int64_t j = j0 + lane;
-    const bool valid = j < (int64_t)n;
-    SwEventRec r;
-    int32_t asg = -1, nid = -1;
-    int64_t seq = 0;
-    if (valid) {
-      const uint32_t i = idx ? idx[j] : (uint32_t)j;
-      r = R[i];
-      const int32_t dev = devs[i];
-      asg = asgs[i];
-      seq = cur + j;
-      const int64_t row = seq % a.store_cap;
-      a.s_etype[row] = r.etype;
-      a.s_level[row] = r.level;
-      a.s_date[row] = r.event_date;
-      a.s_recv[row] = now;
-      a.s_dev[row] = dev;
-      a.s_asg[row] = asg;
-      const int4 ctx = *reinterpret_cast<const int4*>(&a.asg_ctx[asg]);
-      a.s_cust[row] = ctx.y;
-      a.s_area[row] = ctx.z;
-      a.s_asset[row] = ctx.w;
-      a.s_name[row] = r.name_hash;
-      a.s_v0[row] = r.v0;
-      a.s_v1[row] = r.v1;
-      a.s_v2[row] = r.v2;
-      a.s_alt[row] = r.alt_hash;
-      // into the store-backed filter, in line: a separate pass over the ring's alt column measured
-      // 65 us per 1M-payload step (and slowed whatever ran beside it) against ~13 us here, where
-      // the no-return atomic hides behind the row's other memory traffic (profiles/r5_kernels)
-      if (a.dd_bloom && r.alt_hash) bloom_add((ull*)a.dd_bloom, a.dd_bloom_mask, r.alt_hash);
-      a.s_aux[row] = ((ull)r.src_rank << 48) | ((ull)r.aux_len << 32) | (ull)r.aux_off;
-      a.s_batch[row] = (int32_t)a.sp->batch_seq;
-      SwOutRec o;
-      o.event_date = r.event_date;
-      o.v0 = r.v0;
-      o.v1 = r.v1;
-      o.assignment = asg;
-      const int64_t ns = r.name_hash ? nm_probe(a.nm_key, a.nm_mask, r.name_hash) : -1;
-      nid = ns >= 0 ? a.nm_id[ns] : -1;
-      o.name_id = (nid >= 0 && nid < 0xffff) ? (uint16_t)nid : (uint16_t)0xffff;
-      o.etype = r.etype;
-      o.level = r.level;
-      a.sp->out[seq - c0] = o;
-      if (aux) {                   // the durable-block encoder's input, beside the row (coalesced)
-        SwStrRef sr;
-        if (spans) {
-          sr = spans[i];
-        } else {
-          sr.alt_off = 0; sr.meta_off = 0; sr.alt_len = 0; sr.meta_len = 0; sr.k = 0; sr.has = 0; sr.pad = 0;
-        }
-        aux[seq - c0] = seg_make_aux(r, sr, raw_bytes);
+  for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
+    const uint32_t i = idx ? idx[j] : (uint32_t)j;
+    const SwEventRec r = R[i];
+    const int32_t dev = devs[i], asg = asgs[i];
+    const int64_t seq = cur + j;
+    const int64_t row = seq % a.store_cap;
+    a.s_etype[row] = r.etype;
+    a.s_level[row] = r.level;
+    a.s_date[row] = r.event_date;
+    a.s_recv[row] = now;
+    a.s_dev[row] = dev;
+    a.s_asg[row] = asg;
+    const int4 ctx = *reinterpret_cast<const int4*>(&a.asg_ctx[asg]);
+    a.s_cust[row] = ctx.y;
+    a.s_area[row] = ctx.z;
+    a.s_asset[row] = ctx.w;
+    a.s_name[row] = r.name_hash;
+    a.s_v0[row] = r.v0;
+    a.s_v1[row] = r.v1;
+    a.s_v2[row] = r.v2;
+    a.s_alt[row] = r.alt_hash;
+    a.s_aux[row] = ((ull)r.src_rank << 48) | ((ull)r.aux_len << 32) | (ull)r.aux_off;
+    a.s_batch[row] = (int32_t)a.sp->batch_seq;
+    SwOutRec o;
+    o.event_date = r.event_date;
+    o.v0 = r.v0;
+    o.v1 = r.v1;
+    o.assignment = asg;
+    const int64_t ns = r.name_hash ? nm_probe(a.nm_key, a.nm_mask, r.name_hash) : -1;
+    const int32_t nid = ns >= 0 ? a.nm_id[ns] : -1;
+    o.name_id = (nid >= 0 && nid < 0xffff) ? (uint16_t)nid : (uint16_t)0xffff;
+    o.etype = r.etype;
+    o.level = r.level;
+    a.sp->out[seq - c0] = o;
+    if (a.dd_bloom && r.alt_hash) bloom_add((ull*)a.dd_bloom, a.dd_bloom_mask, r.alt_hash);
+    if (aux) {                   // the durable-block encoder's input, beside the row (coalesced)
+      SwStrRef sr;
+      if (spans) {
+        sr = spans[i];
+      } else {
+        sr.alt_off = 0; sr.meta_off = 0; sr.alt_len = 0; sr.meta_len = 0; sr.k = 0; sr.has = 0; sr.pad = 0;
       }
+      aux[seq - c0] = seg_make_aux(r, sr, raw_bytes);
     }
-    const bool loc = valid && r.etype == SW_EV_LOCATION;
-    const bool named = valid && (r.etype == SW_EV_MEASUREMENT || r.etype == SW_EV_ALERT) && nid >= 0;
-    const ull d = valid ? (ull)r.event_date : 0ull;
-    // the state word this row merges into: (assignment, location) or (assignment, name, alert)
-    const ull pk = (loc || named) ? (((ull)(uint32_t)asg << 32) |
-                                     (loc ? 0xffffffffull : (((ull)(uint32_t)nid << 1) | (r.etype == SW_EV_ALERT ? 1ull : 0ull))))
-                                  : ~(ull)lane;                     // unique: matches no other lane
-    bool plain = false, winner = true;
-    if (clustered) {
-      const uint32_t am = valid ? (uint32_t)asg : 0xffffffffu;
-      // distance to the first lane past the run on each side (0: not found within STATE_RUN, or
-      // the run reaches the wave's edge)
-      int hi = 0, lo = 0;
-      bool hi_edge = false, lo_edge = false;
-#pragma unroll
-      for (int k = 1; k <= STATE_RUN; ++k) {
-        const uint32_t au = __shfl_down(am, k, 64), ad = __shfl_up(am, k, 64);
-        const ull pu = __shfl_down(pk, k, 64), pd = __shfl_up(pk, k, 64);
-        const ull du = __shfl_down(d, k, 64), dd = __shfl_up(d, k, 64);
-        const bool iu = lane + (uint32_t)k < 64u, id = lane >= (uint32_t)k;
-        if (!hi && !hi_edge) { if (!iu) hi_edge = true; else if (au != am) hi = k; }
-        if (!lo && !lo_edge) { if (!id) lo_edge = true; else if (ad != am) lo = k; }
-        // a later lane of the same word with a date at least as late, or an earlier one with a
-        // later date, writes instead
-        if (iu && pu == pk && du >= d) winner = false;
-        if (id && pd == pk && dd > d) winner = false;
-      }
-      // runs of at most STATE_RUN rows inside the wave: every lane of the run sees the whole run,
-      // so all of them take the same decision (a longer run keeps the atomics on every lane)
-      plain = hi && lo && hi + lo - 1 <= STATE_RUN;
-    }
-    if (!valid) continue;
     // ---- state pass 1
     int64_t slot = -1;
     if (r.etype == SW_EV_MEASUREMENT || r.etype == SW_EV_LOCATION || r.etype == SW_EV_ALERT) {
@@ -1332,35 +1278,27 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
       const ulonglong2 lm = *reinterpret_cast<const ulonglong2*>(&st->last);   // last, missing
       if (lm.x < (ull)now) st->last = (ull)now;
       if (lm.y) st->missing = 0;  // presence detected again
-      if (loc) {
-        if (plain) {
-          if (winner && d > st->loc_date) st->loc_date = d;
-        } else if (d > st->loc_date) {
-          atomicMax((ull*)&st->loc_date, d);
-        }
-      } else if (named) {
+      const ull d = (ull)r.event_date;
+      if (r.etype == SW_EV_LOCATION) {
+        if (d > st->loc_date) atomicMax((ull*)&st->loc_date, d);
+      } else if (nid >= 0) {
         // +1 keeps key 0 reserved as empty
         const ull k = ((((ull)(uint32_t)asg) << 32) | ((ull)(uint32_t)nid << 1) | (r.etype == SW_EV_ALERT ? 1ull : 0ull)) + 1ull;
         slot = ms_slot(a.ms, a.ms_mask, k);
         if (slot >= 0) {
-          if (plain) {
-            if (winner && d > a.ms[slot].date) a.ms[slot].date = d;
-          } else if (d > a.ms[slot].date) {
-            atomicMax((ull*)&a.ms[slot].date, d);
-          }
+          if (d > a.ms[slot].date) atomicMax((ull*)&a.ms[slot].date, d);
         } else {
           atomicAdd((ull*)&a.stats[SW_STAT_STATE_OVERFLOW], 1ull);
         }
       }
     }
-    // pass-2 work item, coalesced: (ms slot | -2 - assignment for a location | -1, event date);
-    // a run's non-writing lanes drop out, its writer is marked plain (EV_PLAIN)
-    if (loc) slot = -2 - (int64_t)asg;
-    if (plain && !winner) slot = -1;
-    reinterpret_cast<longlong2*>(a.ev_slot)[j] = make_longlong2(slot, (int64_t)(plain ? (d | EV_PLAIN) : d));
+    // pass-2 work item, coalesced: (ms slot | -2 - assignment for a location | -1, event date)
+    if (r.etype == SW_EV_LOCATION) slot = -2 - (int64_t)asg;
+    reinterpret_cast<longlong2*>(a.ev_slot)[j] = make_longlong2(slot, (int64_t)r.event_date);
   }
 }
 
+// ============================================================================ device state
 // Pass 2: among events carrying the max date, the highest event id wins (ids are monotonic).
 // Reads only k_persist's coalesced (slot, date) work items -- no event records, no probes.
 __global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, uint32_t cap,
@@ -1380,20 +1318,14 @@ __global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, u
     const longlong2 w = work[j];
     if (w.x == -1) continue;
     const ull eid1 = (ull)((cur + j) * a.world + a.rank) + 1ull;  // stored +1, 0 = none
-    const bool plain = ((ull)w.y & EV_PLAIN) != 0;                 // the only writer of its word
-    const ull d = (ull)w.y & ~EV_PLAIN;
-    ull* e = nullptr;
+    const ull d = (ull)w.y;
     if (w.x <= -2) {                         // location: assignment -2 - w.x
       SwAsgState* st = &a.st[-2 - w.x];
       const ulonglong2 le = *reinterpret_cast<const ulonglong2*>(&st->loc_date);   // loc_date, loc_eid1
-      if (le.x == d && le.y < eid1) e = (ull*)&st->loc_eid1;
+      if (le.x == d && le.y < eid1) atomicMax((ull*)&st->loc_eid1, eid1);
     } else {
       const ulonglong2 de = *reinterpret_cast<const ulonglong2*>(&a.ms[w.x].date);  // date, eid1
-      if (de.x == d && de.y < eid1) e = (ull*)&a.ms[w.x].eid1;
-    }
-    if (e) {
-      if (plain) *e = eid1;
-      else atomicMax(e, eid1);
+      if (de.x == d && de.y < eid1) atomicMax((ull*)&a.ms[w.x].eid1, eid1);
     }
   }
 }
