@@ -587,9 +587,12 @@ def main():
             drops = torch.tensor(list(eng.string_drops().values()), dtype=torch.int64,
                                  device=torch.device("cuda", local) if use_gpu else "cpu")
             dist.all_reduce(drops, op=dist.ReduceOp.SUM)
+            # lossless re-key: a record whose slab is full waits in the carry with its strings; only
+            # a record whose strings alone exceed a whole slab goes without them
             detail["string_exchange"] = {"bytes_per_slot": cfg.str_bytes, "slab_bytes": cfg.str_cap,
-                                         "records_without_strings": {"slab_full": int(drops[0]),
-                                                                     "carried": int(drops[1])}}
+                                         "carry_heap_bytes": cfg.carry_str_cap,
+                                         "records_without_strings": {k: int(v) for k, v in
+                                                                     zip(eng.string_drops(), drops.tolist())}}
         detail["shuffle_deferred"] = s1.get("shuffle_deferred", 0) - s0.get("shuffle_deferred", 0)
         detail["shuffle_overflow"] = s1.get("shuffle_overflow", 0) - s0.get("shuffle_overflow", 0)
         detail["stall_rounds"] = stalls["rounds"]
