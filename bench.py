@@ -213,7 +213,12 @@ def main():
     spec = FleetSpec(prefix="dev-", n_devices=n_total_dev, p_location=0.25, p_alert=0.05,
                      p_unregistered=args.p_unregistered, mx_per_msg=args.mx_per_msg, n_names=16,
                      with_alternate_id=args.alt_ids, lat0=33.0, lon0=-85.0, span_deg=2.0,
-                     p_register=args.p_register, p_ack=args.p_ack, p_meta=args.p_meta)
+                     p_register=args.p_register, p_ack=args.p_ack, p_meta=args.p_meta,
+                     # ranks share the per-step id epoch and keep their ids apart in the counter part
+                     # ("<epoch>-<rank:2 hex><message:6 hex>"): a block that mixes ranks' events still
+                     # shares the id prefix, so its pages keep the compact hex id mode
+                     alt_base=rank << 24)
+    assert args.msgs <= 1 << 24, "alternate-id counters hold 2^24 messages per rank and step"
     cfg = EngineConfig(max_msgs=args.msgs, rec_cap=args.msgs * args.mx_per_msg + 4096,
                        gen_cap=max(1 << 16, args.msgs // 2), max_devices=int(n_total_dev * 1.1) + 1024,
                        max_assignments=int(n_total_dev * 1.1) + 1024, store_cap=args.store,
@@ -369,7 +374,7 @@ def main():
         def stamp(k):
             rec = records[k % len(records)]
             return stamp_positions(rec.ptr + VALUE_HDR, alt_pos[k % len(records)],
-                                   (0x5717 << 48) | (rank << 32) | k, threads=int(os.environ.get("SW_STAMP_THREADS", 8)))
+                                   (0x5717 << 48) | k, threads=int(os.environ.get("SW_STAMP_THREADS", 8)))
 
         if producer is not None:
             for j in range(AHEAD):

@@ -204,11 +204,13 @@ static inline uint64_t xs64(uint64_t& s) { s ^= s << 13; s ^= s >> 7; s ^= s << 
 // Generates n messages into a caller buffer; returns bytes written or -needed if too small.
 // Device tokens are "<prefix><index zero-padded to 10>"; unregistered devices use indices >= n_devices.
 // p_meta: share of events carrying metadata (firmware version + gateway, 2 Metadata entries); alert
-// messages vary per event ("<type> threshold exceeded: <reading>").
+// messages vary per event ("<type> threshold exceeded: <reading>").  Alternate ids are
+// "<16 hex epoch>-<8 hex (alt_base + message index)>": producers on several ranks share the epoch
+// and keep their ids apart by alt_base.
 int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, double p_loc, double p_alert,
                         double p_unreg, int32_t mx_per_msg, int32_t n_names, int64_t ts0, uint64_t seed,
                         int32_t with_alt_id, double lat0, double lon0, double span_deg, double p_meta, uint8_t* out,
-                        int64_t out_cap, uint32_t* offs) {
+                        int64_t out_cap, uint32_t* offs, uint64_t alt_base) {
   std::vector<uint8_t> buf;
   buf.reserve(96);
   Enc e{buf};
@@ -238,7 +240,7 @@ int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, d
     // pre-generated batch stamps a fresh epoch in place (sw_stamp_alt_epoch)
     if (with_alt_id)
       alen = (size_t)snprintf(alt, sizeof(alt), "%016llx-%08llx", (unsigned long long)seed,
-                              (unsigned long long)(m & 0xffffffffLL));
+                              (unsigned long long)(((uint64_t)m + alt_base) & 0xffffffffull));
     // metadata entries (field 4 / 6 / 5 by event type), emitted before the alternate id
     const bool meta = p_meta > 0 && (double)(xs64(s) >> 11) * (1.0 / 9007199254740992.0) < p_meta;
     char fw[16], gw[16];

@@ -55,7 +55,7 @@ int64_t sw_cpu_decode(const uint8_t* raw, const uint32_t* off, int64_t n_msgs, i
 int64_t sw_gen_payloads(int64_t n_msgs, const char* prefix, int64_t n_devices, double p_loc, double p_alert,
                         double p_unreg, int32_t mx_per_msg, int32_t n_names, int64_t ts0, uint64_t seed,
                         int32_t with_alt_id, double lat0, double lon0, double span_deg, double p_meta, uint8_t* out,
-                        int64_t out_cap, uint32_t* offs);
+                        int64_t out_cap, uint32_t* offs, uint64_t alt_base);
 int64_t swseg_encode(const SwOutRec* rows, const SwEventRec* recs, const SwStrRef* spans, const uint8_t* raw,
                      int64_t raw_bytes, int64_t n, uint8_t* out, int64_t cap);
 void swseg_seal(uint8_t* block, int64_t first_seq, int64_t recv_ms, int64_t boot, int32_t rank, int32_t world);
@@ -272,7 +272,7 @@ static void decode_fuzz() {
   std::vector<uint8_t> raw(n * 256);
   std::vector<uint32_t> off(n + 1);
   const int64_t bytes = sw_gen_payloads(n, "dev-", 500, 0.3, 0.1, 0.05, 3, 16, 1700000000000, 7, 1, 33.0, -85.0, 1.0,
-                                        0.3, raw.data(), (int64_t)raw.size(), off.data());
+                                        0.3, raw.data(), (int64_t)raw.size(), off.data(), 0);
   CHECK(bytes > 0, "payload generation failed");
   std::vector<SwEventRec> out(n * 8);
   std::vector<SwStrRef> spans(n * 8);

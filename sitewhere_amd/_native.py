@@ -126,7 +126,8 @@ def native():
         _proto(lib, "sw_reg_build", c_int64, P, P, P, c_int64, P, P, P, c_int64, P)
         _proto(lib, "sw_cpu_decode", c_int64, P, P, c_int64, c_int64, c_int32, P, P, c_int64, c_int32)
         _proto(lib, "sw_gen_payloads", c_int64, c_int64, c_char_p, c_int64, c_double, c_double, c_double, c_int32,
-               c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, c_double, P, c_int64, P)
+               c_int32, c_int64, c_uint64, c_int32, c_double, c_double, c_double, c_double, P, c_int64, P,
+               c_uint64)
         _proto(lib, "sw_gen_tokens", c_int64, c_char_p, c_int64, c_int64, P, c_int64, P)
         _proto(lib, "sw_stamp_alt_epoch", c_int64, P, P, c_int64, c_uint64, c_int32)
         _proto(lib, "sw_alt_positions", c_int64, P, P, c_int64, P)

@@ -102,6 +102,7 @@ class FleetSpec:
     p_ack: float = 0.0               # command acknowledgements (control plane)
     device_type: str = "default-type"
     p_meta: float = 0.0              # events carrying metadata (firmware version + gateway entries)
+    alt_base: int = 0                # alternate ids "<epoch>-<alt_base + message index>" (8 hex digits)
 
 
 def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndarray | None = None,
@@ -118,7 +119,7 @@ def gen_payloads(spec: FleetSpec, n_msgs: int, ts0: int, seed: int, out: np.ndar
     r = lib.sw_gen_payloads(n_msgs, spec.prefix.encode(), spec.n_devices, spec.p_location, spec.p_alert,
                             spec.p_unregistered, spec.mx_per_msg, spec.n_names, ts0, seed,
                             1 if spec.with_alternate_id else 0, spec.lat0, spec.lon0, spec.span_deg,
-                            float(spec.p_meta), _ptr(out), out.nbytes, _ptr(offs))
+                            float(spec.p_meta), _ptr(out), out.nbytes, _ptr(offs), int(spec.alt_base) & (2 ** 64 - 1))
     if r < 0:
         raise RuntimeError(f"payload buffer too small (need {-r})")
     raw, offs = out[:r], offs[:n_msgs + 1]
