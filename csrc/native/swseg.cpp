@@ -35,6 +35,7 @@
 #include <set>
 #include <string>
 #include <thread>
+#include <sys/mman.h>
 #include <vector>
 
 #include "swindex.h"
@@ -1315,8 +1316,19 @@ static void parallel_for(int64_t n, int threads, F&& f) {
   for (auto& x : th) x.join();
 }
 
+// Memory for a multi-MB copy: 2 MiB aligned and advised for transparent huge pages, so the copy
+// takes a few faults instead of one per 4 KiB page.  Freed with free().
+static uint8_t* big_alloc(int64_t n, int64_t* cap_out = nullptr) {
+  const int64_t H = 2ll << 20;
+  const int64_t cap = (n + H - 1) / H * H;
+  uint8_t* p = (uint8_t*)aligned_alloc((size_t)H, (size_t)cap);
+  if (p) (void)madvise(p, (size_t)cap, MADV_HUGEPAGE);
+  if (cap_out) *cap_out = cap;
+  return p;
+}
+
 static uint8_t* own_copy_mt(const uint8_t* src, int64_t n, int threads) {
-  uint8_t* c = (uint8_t*)aligned_alloc(64, (size_t)((n + 63) / 64 * 64));
+  uint8_t* c = n >= (2ll << 20) ? big_alloc(n) : (uint8_t*)aligned_alloc(64, (size_t)((n + 63) / 64 * 64));
   if (!c) return nullptr;
   const int64_t unit = 1 << 20;
   parallel_for((n + unit - 1) / unit, threads, [&](int64_t a, int64_t b) {
@@ -1452,8 +1464,12 @@ static void seg_copier(SegStore* s) {
             }
         }
         if (!p) {
-          cap = round_up_mb(isz);
-          p = (uint8_t*)aligned_alloc(4096, (size_t)cap);
+          if (isz >= (2ll << 20)) {
+            p = big_alloc(isz, &cap);
+          } else {
+            cap = round_up_mb(isz);
+            p = (uint8_t*)aligned_alloc(4096, (size_t)cap);
+          }
         }
         if (p) {
           scan_image_build(it.ptr, p, seg_copy_threads());
