@@ -627,6 +627,10 @@ def main():
             "index_bytes_per_event": round((getattr(sk, "index_bytes", 0) - sk0[4]) / max(1, nrows), 3),
             "durable_bytes_per_s": round((d1["bytes_written"] - d0["bytes_written"]) / elapsed, 1),
             "disk_bytes_written": d1["bytes_written"] - d0["bytes_written"],
+            # the segment writer's time in the timed region: block writes, fdatasync, waiting for
+            # the copier (scan images + trailer copies for reads), and the copier's own time
+            "writer_ms": {k: round((d1[k] - d0[k]) / 1e6, 2) for k in ("write_ns", "sync_ns", "copier_wait_ns",
+                                                                      "copier_ns")},
             "fdatasyncs": d1["syncs"] - d0["syncs"], "direct_io": bool(d1["direct_io"]),
             "retention_deleted_bytes": d1["deleted_bytes"], "all_durable": sk.store.durable() >= sk.store.seg.last_token,
             # time the pipeline waited for the disk (block buffers all queued, not yet durable):

@@ -1231,6 +1231,8 @@ struct SegStore {
   int64_t cur_bytes = 0;
   std::atomic<int64_t> durable{-1};
   std::atomic<int64_t> bytes_written{0}, blocks_written{0}, syncs{0}, deleted_files{0}, deleted_bytes{0};
+  // where the writer's time goes (ns): block writes, fdatasync, waiting for the copier; the copier's own
+  std::atomic<int64_t> write_ns{0}, sync_ns{0}, cwait_ns{0}, copy_ns{0};
   std::atomic<int32_t> error{0};
   bool stop = false;
   std::thread th;
@@ -1444,6 +1446,7 @@ static void seg_copier(SegStore* s) {
       std::lock_guard<std::mutex> g(s->mu);
       keep = s->blk_cap;
     }
+    const auto c0 = std::chrono::steady_clock::now();
     std::vector<SegStore::Copy> out;
     out.reserve(job->size());
     for (const SegItem& it : *job) {
@@ -1484,6 +1487,7 @@ static void seg_copier(SegStore* s) {
       }
       out.push_back(c);
     }
+    s->copy_ns += (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - c0).count();
     {
       std::lock_guard<std::mutex> g(s->cmu);
       s->cout.swap(out);
@@ -1632,6 +1636,7 @@ static void seg_writer(SegStore* s) {
     }
     s->ccv.notify_all();
     pend.clear();
+    const auto w0 = std::chrono::steady_clock::now();
     for (const SegItem& it : batch) {
       SwSegBlockHdr h;
       memcpy(&h, it.ptr, sizeof(h));
@@ -1705,14 +1710,23 @@ static void seg_writer(SegStore* s) {
       s->blocks_written += 1;
       last = it.token;
     }
+    const auto w1 = std::chrono::steady_clock::now();
     const bool synced = !s->error && !(s->fd >= 0 && fdatasync(s->fd) != 0);
     if (!s->error && !synced) s->error = errno ? errno : -1;
+    const auto w2 = std::chrono::steady_clock::now();
     std::vector<SegStore::Copy> copies;
     {
       std::unique_lock<std::mutex> lk(s->cmu);
       s->ccv.wait(lk, [&] { return s->cdone; });
       copies.swap(s->cout);
     }
+    const auto w3 = std::chrono::steady_clock::now();
+    auto ns = [](std::chrono::steady_clock::duration d) {
+      return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count();
+    };
+    s->write_ns += ns(w1 - w0);
+    s->sync_ns += ns(w2 - w1);
+    s->cwait_ns += ns(w3 - w2);
     auto drop = [](const SegStore::Copy& c) {
       free(c.blk);
       if (c.own) free(c.tr);
@@ -1937,6 +1951,10 @@ void swss_stats(void* h, int64_t* out) {
   out[5] = s->total_bytes;
   out[6] = (int64_t)s->files.size();
   out[7] = s->fd_direct;
+  out[8] = s->write_ns;
+  out[9] = s->sync_ns;
+  out[10] = s->cwait_ns;
+  out[11] = s->copy_ns;
 }
 
 void swss_close(void* h) {

@@ -459,10 +459,11 @@ class SegmentStore:
         return self._token
 
     def stats(self) -> dict:
-        a = np.zeros(8, np.int64)
+        a = np.zeros(12, np.int64)
         self.lib.swss_stats(self.h, _p(a))
         return dict(zip(("bytes_written", "blocks_written", "syncs", "deleted_files", "deleted_bytes", "retained_bytes",
-                         "files", "direct_io"), (int(x) for x in a)))
+                         "files", "direct_io", "write_ns", "sync_ns", "copier_wait_ns", "copier_ns"),
+                        (int(x) for x in a)))
 
     def index(self) -> np.ndarray:
         cap = 1024
