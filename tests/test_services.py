@@ -178,8 +178,14 @@ def test_new_tenant_gpu_template_cpu_engine():
         em = inst.api("DeviceEventManagement", "fast")
         run = lambda f: inst.instance.system_user.run(f, "fast")  # noqa: E731
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
-        assert wait_until(lambda: ib.dev_index.idx.get(dev.id) is not None and
-                          ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+
+        def ready():     # the engine itself has the device and its active assignment (the index
+            # entries are taken before the engine update they key)
+            di, ai = ib.dev_index.idx.get(dev.id), ib.asg_index.idx.get(dev.device_assignment_id)
+            with ib._lock:
+                return (di is not None and ai is not None and int(ib.engine.dev_asg[di]) == ai
+                        and bool(ib.engine.asg_active[ai]))
+        assert wait_until(ready)
         api = inst.api("InboundProcessing", "fast")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
