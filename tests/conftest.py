@@ -29,6 +29,17 @@ def gpu_available():
         return False
 
 
+def engine_knows(ib, dev) -> bool:
+    """An inbound tenant engine has ``dev`` and its active assignment in the engine's own tables.
+    Its index entries are taken before the engine update they key (under the engine lock), so
+    waiting on the index alone races the first batch, which then routes the device as unregistered."""
+    di, ai = ib.dev_index.idx.get(dev.id), ib.asg_index.idx.get(dev.device_assignment_id)
+    if di is None or ai is None:
+        return False
+    with ib._lock:
+        return int(ib.engine.dev_asg[di]) == ai and bool(ib.engine.asg_active[ai])
+
+
 @pytest.fixture(autouse=True)
 def _fresh_data_dir(tmp_path_factory, monkeypatch):
     """Each test's durable tenant stores (``${sitewhere.data.dir}``) start empty: tests reuse tenant

@@ -11,6 +11,7 @@ import struct
 import time
 
 import pytest
+from conftest import engine_knows
 
 from sitewhere_amd.assembly import SiteWhereInstance
 from sitewhere_amd.models import wire
@@ -55,7 +56,7 @@ def _tenant(inst, token, template):
     ib = inst.tenant_engine("inbound-processing", token)
     run = lambda f: inst.instance.system_user.run(f, token)  # noqa: E731
     dev = run(lambda: inst.api("DeviceManagement", token).get_device_by_token("galaxytab-001"))
-    assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+    assert wait_until(lambda: engine_knows(ib, dev))
     return ib, run, dev
 
 

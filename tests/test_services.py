@@ -11,6 +11,7 @@ import json
 import time
 
 import pytest
+from conftest import engine_knows
 
 from sitewhere_amd.assembly import SiteWhereInstance
 from sitewhere_amd.models import wire
@@ -178,14 +179,7 @@ def test_new_tenant_gpu_template_cpu_engine():
         em = inst.api("DeviceEventManagement", "fast")
         run = lambda f: inst.instance.system_user.run(f, "fast")  # noqa: E731
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
-
-        def ready():     # the engine itself has the device and its active assignment (the index
-            # entries are taken before the engine update they key)
-            di, ai = ib.dev_index.idx.get(dev.id), ib.asg_index.idx.get(dev.device_assignment_id)
-            with ib._lock:
-                return (di is not None and ai is not None and int(ib.engine.dev_asg[di]) == ai
-                        and bool(ib.engine.asg_active[ai]))
-        assert wait_until(ready)
+        assert wait_until(lambda: engine_knows(ib, dev))
         api = inst.api("InboundProcessing", "fast")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
@@ -217,8 +211,7 @@ def test_gpu_tenant_engine_on_device():
         dm = inst.api("DeviceManagement", "fastgpu")
         em = inst.api("DeviceEventManagement", "fastgpu")
         dev = run(lambda: dm.get_device_by_token("meitrack-000"))
-        assert wait_until(lambda: ib.dev_index.idx.get(dev.id) is not None and
-                          ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: engine_knows(ib, dev))
         api = inst.api("InboundProcessing", "fastgpu")
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
@@ -312,8 +305,7 @@ def test_columnar_tenant_end_to_end():
         em = inst.api("DeviceEventManagement", "col")
         ib = inst.tenant_engine("inbound-processing", "col")
         dev = run(lambda: dm.get_device_by_token("galaxytab-001"))
-        assert wait_until(lambda: ib.dev_index.idx.get(dev.id) is not None and
-                          ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: engine_knows(ib, dev))
         topic = inst.instance.naming.tenant_prefix("col") + "inbound-enriched-batches"
         cons = inst.instance.bus.consumer("col-batches", [topic])
         api = inst.api("InboundProcessing", "col")
@@ -376,7 +368,7 @@ def test_gpu_template_routes_protobuf_raw_and_json_per_event():
         ib = inst.tenant_engine("inbound-processing", "mix")
         es = inst.tenant_engine("event-sources", "mix")
         dev = run(lambda: dm.get_device_by_token("iphone6s-001"))
-        assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: engine_knows(ib, dev))
         for i in range(7):                                   # < rawBatchSize: flushed by the timer
             es.inject("default-protobuf", wire.measurements("iphone6s-001", {"pb": float(i)}))
         es.inject("default-json", _json.dumps({"deviceToken": "iphone6s-001", "type": "DeviceMeasurement",
@@ -470,7 +462,7 @@ def test_gpu_tenant_checkpoint_resume_replays_exactly(tmp_path):
         run = lambda f: inst.instance.system_user.run(f, "ck")  # noqa: E731
         dm = inst.api("DeviceManagement", "ck")
         dev = run(lambda: dm.get_device_by_token("galaxytab-001"))
-        assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: engine_knows(ib, dev))
         topic = inst.instance.naming.tenant_prefix("ck") + RAW_PAYLOADS
 
         def raw_batch(b):
@@ -531,7 +523,7 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records(zero_copy_rows
         assert ib.engine_kind == "gpu" and ib.overlap and ib.async_store and ib.zero_copy_rows == zero_copy_rows
         run = lambda f: inst.instance.system_user.run(f, "ovl")  # noqa: E731
         dev = run(lambda: inst.api("DeviceManagement", "ovl").get_device_by_token("galaxytab-001"))
-        assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None)
+        assert wait_until(lambda: engine_knows(ib, dev))
         bus = inst.instance.bus
         topic = inst.instance.naming.tenant_prefix("ovl") + RAW_PAYLOADS
         unreg = bus.consumer("ovl-unreg", [inst.instance.naming.unregistered_device_events("ovl")])

@@ -13,6 +13,7 @@ import os
 import time
 
 import pytest
+from conftest import engine_knows
 
 from sitewhere_amd.models import wire
 
@@ -61,7 +62,7 @@ def test_replay_beyond_the_window_is_a_duplicate(sw):
     es = sw.tenant_engine("event-sources", "sd")
     dev = sw.instance.system_user.run(lambda: sw.api("DeviceManagement", "sd").get_device_by_token("galaxytab-002"),
                                       "sd")
-    assert wait_until(lambda: ib.asg_index.idx.get(dev.device_assignment_id) is not None, 30)
+    assert wait_until(lambda: engine_knows(ib, dev), 30)
     first = wire.measurements("galaxytab-002", {"sd.temp": 1.5}, event_date=1_700_000_000_000, alternate_id="sd-old-1")
     es.inject("default-protobuf", first)
     assert wait_until(lambda: len(_measurements(sw, "sd-old-1")) == 1, 30)
