@@ -326,6 +326,15 @@ class GpuInboundEngine(EngineBase):
             self.t["reg"].copy_(torch.from_numpy(full))
             return
         reg.index_copy_(0, torch.from_numpy(slots).to(self.device), torch.from_numpy(np.ascontiguousarray(rows)).to(self.device))
+        self._control_done()
+
+    def _control_done(self):
+        """Complete a control-plane table write before the update returns.  Registry and assignment
+        changes come from the model-update consumer thread, whose current stream is not the one
+        steps are enqueued on (another thread's, or a pipeline stream): left in flight, the scatter
+        raced the next step's lookup, which then saw the device as unregistered (a tenant test's
+        first batch persisted nothing).  Control-plane writes are rare; one stream sync each."""
+        torch.cuda.current_stream(self.device).synchronize()
 
     def _dirty_registry(self, slots: np.ndarray):
         self._upload_slots(slots)
@@ -336,6 +345,7 @@ class GpuInboundEngine(EngineBase):
         it = torch.from_numpy(idx).to(self.device)
         self.t["asg_ctx"].view(-1, 4).index_copy_(0, it, torch.from_numpy(np.ascontiguousarray(ctx, np.int32)).to(self.device))
         self.t["asg_active"].index_copy_(0, it, torch.from_numpy(np.ascontiguousarray(self.asg_active[idx])).to(self.device))
+        self._control_done()
 
     def _dirty_devices(self, idx):
         idx = np.asarray(idx, np.int64)

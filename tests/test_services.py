@@ -18,6 +18,35 @@ from sitewhere_amd.models import wire
 from sitewhere_amd.models.domain import DeviceEventType
 
 
+def _engine_diag(ib, dev) -> str:
+    """What an inbound engine did with a device's events: its counters, and the device's registry
+    row on the host and (GPU engine) in HBM."""
+    import numpy as np
+    e = ib.engine
+    out = {"stats": {k: v for k, v in e.stats_dict().items() if v}}
+    with ib._lock:
+        di = ib.dev_index.idx.get(dev.id)
+        slot = int(e.dev_slot[di]) if di is not None else -1
+        out["dev"], out["slot"] = di, slot
+        if slot >= 0:
+            out["host_row"] = e.packed_registry(np.array([slot])).tolist()
+            if isinstance(getattr(e, "t", None), dict) and "reg" in e.t:
+                out["gpu_row"] = e.t["reg"].view(-1, 4)[slot].cpu().tolist()
+                from sitewhere_amd.models.columnar import EVENT_REC
+                r = e.t["recs"][:4 * EVENT_REC.itemsize].cpu().numpy().view(EVENT_REC)
+                out["recs"] = [(int(x["fp_lo"]), int(x["fp_hi"]), int(x["etype"]), int(x["flags"])) for x in r]
+                out["reg_ptr_ok"] = (e.args.reg == e.t["reg"].data_ptr(), int(e.args.reg_mask), e.cfg.reg_slots)
+                out["reg_rows"] = int((e.t["reg"].view(-1, 4)[:, 0] != 0).sum().item())
+                out["graph"] = (e.use_graph, e._graph is not None)
+    for k in ("processed_events", "persisted_events"):
+        m = getattr(ib, k, None)
+        out[k] = getattr(m, "_count", None)
+    out["store_error"] = repr(getattr(ib, "_store_error", None))
+    out["stepped"] = len(getattr(ib, "_stepped", ()))
+    print("engine diag:", out)
+    return str(out)
+
+
 def wait_until(cond, timeout=10.0, step=0.02):
     end = time.time() + timeout
     while time.time() < end:
@@ -184,7 +213,7 @@ def test_new_tenant_gpu_template_cpu_engine():
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
                                               wire.measurements("nobody", {"x": 1.0})]))
-        assert r["persisted"] == 2
+        assert r["persisted"] == 2, (r, _engine_diag(ib, dev))
         ms = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id])).results
         assert ms and ms[0].name == "rpm" and ms[0].value == 1200.0
         st = run(lambda: api.get_statistics())
@@ -216,7 +245,7 @@ def test_gpu_tenant_engine_on_device():
         r = run(lambda: api.process_payloads([wire.measurements("meitrack-000", {"rpm": 1200.0}),
                                               wire.location("meitrack-000", 34.10, -84.24),
                                               wire.measurements("nobody", {"x": 1.0})]))
-        assert r["persisted"] == 2
+        assert r["persisted"] == 2, (r, _engine_diag(ib, dev))
         ms = run(lambda: em.list_measurements_for_index("Assignment", [dev.device_assignment_id])).results
         assert ms and ms[0].name == "rpm" and ms[0].value == 1200.0
         st = run(lambda: api.get_device_state(dev.device_assignment_id))
@@ -524,6 +553,7 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records(zero_copy_rows
         run = lambda f: inst.instance.system_user.run(f, "ovl")  # noqa: E731
         dev = run(lambda: inst.api("DeviceManagement", "ovl").get_device_by_token("galaxytab-001"))
         assert wait_until(lambda: engine_knows(ib, dev))
+        _engine_diag(ib, dev)                   # printed (shown on failure): the registry row before the batches
         bus = inst.instance.bus
         topic = inst.instance.naming.tenant_prefix("ovl") + RAW_PAYLOADS
         unreg = bus.consumer("ovl-unreg", [inst.instance.naming.unregistered_device_events("ovl")])
@@ -537,7 +567,8 @@ def test_gpu_columnar_tenant_overlapped_steps_from_pinned_records(zero_copy_rows
             rec = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1)
             recs.append(rec)
             rec.publish(bus, topic, 0, ts=1_700_000_500_000 + b)
-        assert wait_until(lambda: getattr(store, "engine_rows", store.rows) == 1600, 60), store.rows
+        assert wait_until(lambda: getattr(store, "engine_rows", store.rows) == 1600, 60), \
+            (getattr(store, "engine_rows", store.rows), _engine_diag(ib, dev))
         assert wait_until(lambda: bus.committed(ib.raw_consumer.group, topic, 0) == bus.end_offset(topic, 0), 30)
         assert not ib.engine.framed_pending and not ib._stepped and not ib._holds.get((topic, 0))
         seen = []
