@@ -244,12 +244,33 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         return self.ms.api("DeviceEventManagement", self.tenant.token)
 
     def load_model(self):
-        """Full registry load (device management list APIs), then the change feed keeps it current."""
+        """Full registry load (device management list APIs), then the change feed keeps it current.
+        One engine call for all devices and one for all assignments: per entity, a 1M-device tenant
+        paid a table upload (and its stream sync) per device and per assignment at every start."""
         dm = self._dm()
-        for d in dm.list_devices({"pageSize": 0}).results:
-            self._upsert_device(d)
-        for a in dm.list_device_assignments({"pageSize": 0}).results:
-            self._upsert_assignment(a)
+        devs = dm.list_devices({"pageSize": 0}).results
+        asgs = dm.list_device_assignments({"pageSize": 0}).results
+        with self._lock:
+            if devs:
+                di = np.array([self.dev_index.get(d.id) for d in devs], np.int32)
+                fps = np.array([fingerprint_str(d.token) for d in devs], np.uint64).reshape(-1, 2)
+                self.engine.register_devices(np.ascontiguousarray(fps[:, 0]), np.ascontiguousarray(fps[:, 1]), di)
+                for d, i in zip(devs, di.tolist()):
+                    self._dev_tokens[i] = d.token
+                    self._dev_types[i] = d.device_type_id
+            if asgs:
+                # in list order, as the per-entity upserts were: the last active assignment of a
+                # device wins, and a released one clears the device only while it is current
+                ai = [self.asg_index.get(a.id) for a in asgs]
+                dv = [self.dev_index.get(a.device_id) for a in asgs]
+                self.engine.set_assignments(ai, dv, customer=[self.customers.get(a.customer_id) for a in asgs],
+                                            area=[self.areas.get(a.area_id) for a in asgs],
+                                            asset=[self.assets.get(a.asset_id) for a in asgs],
+                                            active=[0 if a.status == DeviceAssignmentStatus.Released else 1
+                                                    for a in asgs])
+                for a, i in zip(asgs, ai):
+                    self._asg_entities[i] = a
+                    self._asg_dirty.add(i)
         self._load_zones()
 
     def _load_zones(self):
