@@ -298,6 +298,16 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         with self._lock:
             ai = self.asg_index.get(a.id)
             di = self.dev_index.get(a.device_id)
+            if int(self.engine.dev_slot[di]) < 0:
+                # the assignment's event came before its device's (the change feed does not order
+                # them): register the device now, or its payloads route as unregistered until the
+                # device event arrives although the assignment is active
+                try:
+                    d = self._dm().get_device(a.device_id)
+                except Exception:       # noqa: BLE001 -- the device event registers it later
+                    d = None
+                if d is not None:
+                    self._upsert_device(d)
             active = a.status != DeviceAssignmentStatus.Released
             self.engine.set_assignments([ai], [di], customer=[self.customers.get(a.customer_id)],
                                         area=[self.areas.get(a.area_id)], asset=[self.assets.get(a.asset_id)],

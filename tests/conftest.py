@@ -36,8 +36,11 @@ def engine_knows(ib, dev) -> bool:
     di, ai = ib.dev_index.idx.get(dev.id), ib.asg_index.idx.get(dev.device_assignment_id)
     if di is None or ai is None:
         return False
+    from sitewhere_amd.pipeline.fleet import fingerprint_str
     with ib._lock:
-        return int(ib.engine.dev_asg[di]) == ai and bool(ib.engine.asg_active[ai])
+        # the device's fingerprint too: an assignment's update can precede its device's
+        return (int(ib.engine.dev_asg[di]) == ai and bool(ib.engine.asg_active[ai])
+                and ib.engine.lookup_device(*fingerprint_str(dev.token)) == di)
 
 
 @pytest.fixture(autouse=True)

@@ -218,6 +218,21 @@ def test_new_tenant_gpu_template_cpu_engine():
         assert ms and ms[0].name == "rpm" and ms[0].value == 1200.0
         st = run(lambda: api.get_statistics())
         assert st["engine.unregistered"] >= 1
+        # an assignment's update ahead of its device's (the change feed does not order them): the
+        # engine registers the device from device management at once, not when its event comes
+        from types import SimpleNamespace
+        from sitewhere_amd.pipeline.fleet import fingerprint_str
+        late = SimpleNamespace(id="late-dev-id", token="late-device-1", device_type_id=None)
+        dm_stub = SimpleNamespace(get_device=lambda i: late if i == late.id else None)
+        ib._dm = lambda: dm_stub
+        try:
+            ib._upsert_assignment(SimpleNamespace(id="late-asg-id", device_id=late.id, status="Active",
+                                                  customer_id=None, area_id=None, asset_id=None))
+        finally:
+            del ib._dm
+        di = ib.dev_index.idx.get(late.id)
+        assert di is not None and ib.engine.lookup_device(*fingerprint_str(late.token)) == di
+        assert int(ib.engine.dev_asg[di]) == ib.asg_index.idx.get("late-asg-id")
     finally:
         inst.stop()
 
