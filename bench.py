@@ -58,8 +58,8 @@ def parse():
     ap.add_argument("--p-unregistered", type=float, default=0.005)
     ap.add_argument("--p-register", type=float, default=0.0005)
     ap.add_argument("--p-ack", type=float, default=0.0005)
-    ap.add_argument("--dedup-bloom-bits", type=int, default=1 << 36,
-                    help="store-backed alternate-id filter size (bits, 0 = off)")
+    ap.add_argument("--dedup-filter-ids", type=int, default=(1 << 29) - (1 << 22),
+                    help="store-backed alternate-id filter: ids per generation (4 generations; 0 = off)")
     ap.add_argument("--p-meta", type=float, default=0.1,
                     help="share of events carrying metadata entries (stored with the event, like the reference)")
     ap.add_argument("--durable", action=argparse.BooleanOptionalAction, default=True,
@@ -224,11 +224,11 @@ def main():
                        max_assignments=int(n_total_dev * 1.1) + 1024, store_cap=args.store,
                        # alternate-id window: 2^24 slots = the last ~8M distinct ids per GPU
                        dedup_slots=1 << 24, name_slots=1 << 12, rank=rank, world=world,
-                       # store-backed dedup beyond the window: 2^36 bits = 8 GB of the 288 GB of HBM, sized
-                       # for the ids the retained store holds (48 GB of blocks ~ 2.6B ids: ~2.6 ids per
-                       # 64-bit filter word, false rechecks ~4e-5).  2^33 saturates past ~1B ids: a 1500-step
-                       # run then sends ~4% of its events to the host recheck path.  Rechecks are counted.
-                       dedup_bloom_bits=args.dedup_bloom_bits,
+                       # store-backed dedup beyond the window (pipeline/dedup_filter.py): 4 generations of
+                       # ~2^29 ids = 16 GB of the 288 GB of HBM; the filter always holds the newest ~1.6B
+                       # ids and the durable store is bounded to that many rows (retention by rows, set
+                       # below), so every stored id stays checked however long the run.  Rechecks are counted.
+                       dedup_filter_ids=args.dedup_filter_ids, dedup_filter_gens=4,
                        # (assignment, name) state map: 16 measurement names + 4 alert types + zone alerts per device
                        state_slots=2 * (16 + 4 + args.zones) * int(args.devices * 1.1),
                        presence_missing_ms=8 * 3600 * 1000,
@@ -344,6 +344,9 @@ def main():
 
         if args.durable:
             tmpdir, store, boot = open_durable(args, rank, dev)
+            # the store keeps no row whose id the filter has forgotten: the file being written (whole
+            # files are deleted, 1 GiB / >= 8 B per row) and the blocks in flight are the slack
+            store.limit_retention_rows(cfg.filter_retention_rows((1 << 30) // 8 + 16 * cfg.rec_cap))
             sink = DurableBlockSink(store, eng.lib, boot, rank=rank, world=world, bus=bus, topic=t_out)
             bus.set_retention(t_out, 64 << 20)
             dur = {"store": store, "sink": sink}
@@ -450,6 +453,9 @@ def main():
     else:
         if args.durable:        # host engines encode the same blocks on the CPU (swseg_encode)
             tmpdir, store, boot = open_durable(args, rank, dev)
+            # the store keeps no row whose id the filter has forgotten: the file being written (whole
+            # files are deleted, 1 GiB / >= 8 B per row) and the blocks in flight are the slack
+            store.limit_retention_rows(cfg.filter_retention_rows((1 << 30) // 8 + 16 * cfg.rec_cap))
             dur = {"store": store, "sink": _HostSink(store)}
 
         def run(k):

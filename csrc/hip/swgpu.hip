@@ -879,14 +879,68 @@ __device__ __forceinline__ bool dd_find(const ull* __restrict__ tab, int64_t mas
   return false;
 }
 
-// The id's filter block holds all its bits: it may have been persisted before (beyond the window).
-__device__ __forceinline__ bool bloom_has(const ull* __restrict__ bloom, int64_t bmask, ull h) {
-  const ull m = sw_bloom_bits(h);
-  return (bloom[sw_bloom_block(h, bmask)] & m) == m;
+// Store-backed filter (generational fingerprint tables, swtypes.h SW_FF_*).  Does a live generation
+// hold the id's fingerprint?  It may have been persisted before (beyond the window).  The G buckets
+// of a home position are adjacent: one probe round reads G * 64 contiguous bytes (16-byte loads),
+// and a generation's chain goes on to the next position only while its bucket is full.
+__device__ __forceinline__ bool ff_has(const uint32_t* __restrict__ t, int64_t bmask, int gens, ull h) {
+  const ull m = sw_ff_mix(h);
+  const uint32_t fp = sw_ff_fp(m);
+  int64_t b = (int64_t)sw_ff_bucket(m, bmask);
+  uint32_t open = (1u << gens) - 1u;
+  for (int p = 0; p < SW_FF_MAX_PROBE && open; ++p) {
+    const uint4* __restrict__ q = reinterpret_cast<const uint4*>(t + b * gens * SW_FF_SLOTS);
+    for (int g = 0; g < gens; ++g) {
+      if (!((open >> g) & 1u)) continue;
+      bool empty = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 v = q[g * 4 + k];
+        if (v.x == fp || v.y == fp || v.z == fp || v.w == fp) return true;
+        empty |= !v.x || !v.y || !v.z || !v.w;
+      }
+      if (empty) open &= ~(1u << g);
+    }
+    b = (b + 1) & bmask;
+  }
+  return false;
 }
 
-__device__ __forceinline__ void bloom_add(ull* __restrict__ bloom, int64_t bmask, ull h) {
-  atomicOr(&bloom[sw_bloom_block(h, bmask)], (ull)sw_bloom_bits(h));   // no return: fire-and-forget
+// Add the id's fingerprint to generation g: one CAS into the first free slot of its chain (a slot
+// another thread took first holds a different id, or the same one: then it is in).  False: the
+// probe bound was hit (dropped, counted by the caller).
+__device__ __forceinline__ bool ff_add(uint32_t* __restrict__ t, int64_t bmask, int gens, int g, ull h) {
+  const ull m = sw_ff_mix(h);
+  const uint32_t fp = sw_ff_fp(m);
+  int64_t b = (int64_t)sw_ff_bucket(m, bmask);
+  for (int p = 0; p < SW_FF_MAX_PROBE; ++p) {
+    uint32_t* s = t + (b * gens + g) * SW_FF_SLOTS;
+    uint32_t v[SW_FF_SLOTS];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 x = reinterpret_cast<const uint4*>(s)[k];
+      v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w;
+    }
+#pragma unroll
+    for (int k = 0; k < SW_FF_SLOTS; ++k)
+      if (v[k] == fp) return true;
+#pragma unroll
+    for (int k = 0; k < SW_FF_SLOTS; ++k) {
+      if (v[k]) continue;
+      const uint32_t old = atomicCAS(&s[k], 0u, fp);
+      if (old == 0u || old == fp) return true;
+    }
+    b = (b + 1) & bmask;
+  }
+  return false;
+}
+
+// Clear generation g (grid-stride over the buckets; 64 bytes per bucket).
+__device__ __forceinline__ void ff_clear_gen(uint32_t* __restrict__ t, int64_t bmask, int gens, int g) {
+  const int64_t nb = bmask + 1;
+  const int64_t n = nb * 4;
+  for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK)
+    reinterpret_cast<uint4*>(t + ((i >> 2) * gens + g) * SW_FF_SLOTS)[i & 3] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 struct DedupCounts {
@@ -903,8 +957,9 @@ struct DedupClaim {
   const ull* __restrict__ pt;                // retired generation
   int64_t mask;
   ull sb;                                    // the step's first sequence
-  const ull* __restrict__ bloom;
-  int64_t bmask;
+  const uint32_t* __restrict__ ff;           // store-backed filter (null: off)
+  int64_t fbmask;
+  int fgens;
   int rank;                                  // filter_rank (-1: every record)
 };
 
@@ -923,8 +978,9 @@ __device__ __forceinline__ DedupClaim dedup_claim_args(const SwEngineArgs& a) {
   d.pt = (const ull*)a.dd_key + 2 * (1 - g) * slots;
   d.mask = a.dd_mask;
   d.sb = (ull)*a.seq_base;
-  d.bloom = (const ull*)a.dd_bloom;
-  d.bmask = a.dd_bloom_mask;
+  d.ff = a.dd_ff;
+  d.fbmask = a.dd_ff_bmask;
+  d.fgens = (int)a.dd_ff_gens;
   d.rank = filter_rank(a);
   return d;
 }
@@ -1035,8 +1091,8 @@ __global__ void k_dedup_claim(SwEngineArgs a) {
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull ah = ck[i];
     if (!ah) continue;
-    const bool held = d.bloom && bloom_has(d.bloom, d.bmask, ah);
-    const uint8_t st = dedup_claim(d, ah, i, held && cf[i], !d.bloom || held, dc);
+    const bool held = d.ff && ff_has(d.ff, d.fbmask, d.fgens, ah);
+    const uint8_t st = dedup_claim(d, ah, i, held && cf[i], !d.ff || held, dc);
     if (st != SW_ST_OK) status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
@@ -1059,8 +1115,9 @@ struct DedupView {
   const ulonglong2* ct;       // live generation (null: no alternate-id dedup this step)
   int64_t mask;
   uint32_t sb, n;
-  const ull* bloom;
-  int64_t bmask;
+  const uint32_t* ff;
+  int64_t fbmask;
+  int fgens;
 };
 
 __device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint32_t i, bool local) {
@@ -1072,7 +1129,7 @@ __device__ __forceinline__ uint8_t dedup_verdict(const DedupView& d, ull h, uint
       const uint32_t lmin = (uint32_t)(kq.y >> 32);
       const bool first = wrel < d.n && (wrel < lmin ? wrel : lmin) == i;
       if (!first) return SW_ST_DUPLICATE;
-      return (local && d.bloom && bloom_has(d.bloom, d.bmask, h)) ? SW_ST_RECHECK : SW_ST_OK;   // first sight
+      return (local && d.ff && ff_has(d.ff, d.fbmask, d.fgens, h)) ? SW_ST_RECHECK : SW_ST_OK;   // first sight
     }
     if (kq.x == 0) break;                // not placed (probe overflow, counted): kept
     slot = (slot + 1) & d.mask;
@@ -1087,7 +1144,7 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
                             uint32_t* __restrict__ tcnt /*[2][ntiles]*/, int64_t ntiles, ull* __restrict__ stats,
                             const SwEventRec* __restrict__ recs, const ull* __restrict__ dd_tab, int64_t dd_mask,
                             const int64_t* __restrict__ seq_base, const int64_t* __restrict__ dd_meta,
-                            const ull* __restrict__ bloom, int64_t bmask, int rank) {
+                            const uint32_t* __restrict__ ff, int64_t fbmask, int fgens, int rank) {
   __shared__ uint32_t c[2];
   __shared__ uint32_t rs[8];          // rejects by status (the reject counters of the step)
   if (threadIdx.x < 2) c[threadIdx.x] = 0;
@@ -1100,8 +1157,9 @@ __global__ void k_cmp_count(uint8_t* __restrict__ status, const uint32_t* __rest
   dv.mask = dd_mask;
   dv.sb = (uint32_t)*seq_base;
   dv.n = n;
-  dv.bloom = bloom;
-  dv.bmask = bmask;
+  dv.ff = ff;
+  dv.fbmask = fbmask;
+  dv.fgens = fgens;
   const int64_t base = (int64_t)BID * TILE;
   uint32_t ok = 0, all = 0;
 #pragma unroll
@@ -1220,6 +1278,8 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     // could push the live table past half load (k_state_p2 clears, k_step_end flips)
     if (a.dd_meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) a.dd_meta[2] = 1;
   }
+  const int ff_live = a.dd_ff ? (int)a.dd_ff_meta[0] : 0;
+  uint32_t ff_dropped = 0, ff_ids = 0;
   const int64_t c0 = *a.step_cursor0;
   const int64_t now = a.sp->now_ms;
   SwSegAux* const aux = reinterpret_cast<SwSegAux*>(a.sp->aux);
@@ -1258,7 +1318,10 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     o.etype = r.etype;
     o.level = r.level;
     a.sp->out[seq - c0] = o;
-    if (a.dd_bloom && r.alt_hash) bloom_add((ull*)a.dd_bloom, a.dd_bloom_mask, r.alt_hash);
+    if (a.dd_ff && r.alt_hash) {
+      ++ff_ids;
+      if (!ff_add(a.dd_ff, a.dd_ff_bmask, (int)a.dd_ff_gens, ff_live, r.alt_hash)) ++ff_dropped;
+    }
     if (aux) {                   // the durable-block encoder's input, beside the row (coalesced)
       SwStrRef sr;
       if (spans) {
@@ -1296,6 +1359,15 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     if (r.etype == SW_EV_LOCATION) slot = -2 - (int64_t)asg;
     reinterpret_cast<longlong2*>(a.ev_slot)[j] = make_longlong2(slot, (int64_t)r.event_date);
   }
+  if (a.dd_ff) {
+    // ids the live generation took (its rotation rule: k_state_p2, k_step_end), one atomic per wave
+    const ull w = __ballot(ff_ids != 0);
+    if (w) {
+      for (int o = 32; o > 0; o >>= 1) ff_ids += __shfl_xor(ff_ids, o);
+      if (lane_id() == 0) atomicAdd((ull*)&a.dd_ff_meta[6], (ull)ff_ids);
+    }
+    if (ff_dropped) atomicAdd((ull*)&a.dd_ff_meta[5], (ull)ff_dropped);   // rare: a chain past the probe bound
+  }
 }
 
 // ============================================================================ device state
@@ -1313,6 +1385,10 @@ __global__ void k_state_p2(SwEngineArgs a, const uint32_t* __restrict__ n_ptr, u
     for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < slots; i += (int64_t)gridDim.x * BLK)
       t[i] = make_ulonglong2(0ull, ~0ull);
   }
+  // the filter's live generation has taken its ids (k_persist counted them): clear the oldest, which
+  // k_step_end makes the live one (the step's generated events carry no alternate id)
+  if (!after && a.dd_ff && a.dd_ff_meta[6] >= a.dd_ff_meta[2])
+    ff_clear_gen(a.dd_ff, a.dd_ff_bmask, (int)a.dd_ff_gens, (int)((a.dd_ff_meta[0] + 1) % a.dd_ff_gens));
   const longlong2* __restrict__ work = reinterpret_cast<const longlong2*>(a.ev_slot);
   for (int64_t j = (int64_t)BID * BLK + threadIdx.x; j < n; j += (int64_t)gridDim.x * BLK) {
     const longlong2 w = work[j];
@@ -1608,6 +1684,13 @@ __global__ void k_step_end(SwEngineArgs a, const uint32_t* n_rule_alerts) {
       meta[2] = 2;
     }
     meta[3] = 0;
+    if (a.dd_ff && a.dd_ff_meta[6] >= a.dd_ff_meta[2]) {
+      int64_t* fm = a.dd_ff_meta;
+      fm[0] = (fm[0] + 1) % a.dd_ff_gens;
+      fm[SW_FF_META + fm[0]] = *a.store_cursor;
+      fm[6] = 0;
+      fm[4] += 1;
+    }
   }
 }
 
@@ -1829,12 +1912,14 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   const int g = grid_for(a.rec_cap);
   const int64_t ntiles = (a.rec_cap + TILE - 1) / TILE;
   if (2 * ntiles > a.scan_tmp_len) return -4;
+  if (a.dd_ff && (a.dd_ff_gens < 2 || a.dd_ff_gens > SW_FF_MAX_GENS || !a.dd_ff_meta || a.dd_ff_bmask < 0))
+    return -6;
   k_lookup<<<g, BLK, 0, s>>>(a);         // + the phase's resets (block 0)
   k_dedup_claim<<<g, BLK, 0, s>>>(a);
   // stable split ok / rejected, with the dedup verdicts
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
                                                (const ull*)a.dd_key, a.dd_mask, a.seq_base, a.dd_meta,
-                                               (const ull*)a.dd_bloom, a.dd_bloom_mask, a.work_str ? -1 : (int)a.rank);
+                                               a.dd_ff, a.dd_ff_bmask, (int)a.dd_ff_gens, a.work_str ? -1 : (int)a.rank);
   k_cmp_write<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, a.ok_idx, a.rej_idx, a.n_ok,
                                                a.n_rej);
   int rc = 0;
@@ -1881,16 +1966,34 @@ __global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batc
   }
 }
 
-// Add ids to the store-backed dedup filter (warm start from the event store's alternate-id index).
-__global__ void k_bloom_add(ull* bloom, int64_t bmask, const ull* __restrict__ h, int64_t n) {
+// Add ids to generation g of the store-backed dedup filter (warm start from the event store's
+// blocks, newest first; see EngineBase.filter_seed).
+__global__ void k_ff_add(uint32_t* t, int64_t bmask, int gens, int g, int64_t* meta, const ull* __restrict__ h,
+                         int64_t n) {
+  uint32_t dropped = 0;
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK)
-    if (h[i]) bloom_add(bloom, bmask, h[i]);
+    if (h[i] && !ff_add(t, bmask, gens, g, h[i])) ++dropped;
+  if (dropped) atomicAdd((ull*)&meta[5], (ull)dropped);
 }
 
-int sw_bloom_add(void* bloom, int64_t bmask, const void* hashes, int64_t n, hipStream_t s) {
+__global__ void k_ff_clear(uint32_t* t, int64_t bmask, int gens, int g) { ff_clear_gen(t, bmask, gens, g); }
+
+int sw_ff_add(void* tab, int64_t bmask, int64_t gens, int64_t gen, void* meta, const void* hashes, int64_t n,
+              hipStream_t s) {
   if (n <= 0) return 0;
+  if (gens < 2 || gens > SW_FF_MAX_GENS || gen < 0 || gen >= gens) return -2;
   const int64_t g = (n + BLK - 1) / BLK;
-  k_bloom_add<<<(unsigned)(g < 4096 ? g : 4096), BLK, 0, s>>>((ull*)bloom, bmask, (const ull*)hashes, n);
+  k_ff_add<<<(unsigned)(g < 4096 ? g : 4096), BLK, 0, s>>>((uint32_t*)tab, bmask, (int)gens, (int)gen,
+                                                          (int64_t*)meta, (const ull*)hashes, n);
+  return (int)hipGetLastError();
+}
+
+// Clear generation g (host-driven rotation while seeding; in the step it is k_state_p2's).
+int sw_ff_clear(void* tab, int64_t bmask, int64_t gens, int64_t g, hipStream_t s) {
+  if (gens < 2 || gens > SW_FF_MAX_GENS || g < 0 || g >= gens) return -2;
+  const int64_t nb = (bmask + 1) * 4;
+  const int64_t gr = (nb + BLK - 1) / BLK;
+  k_ff_clear<<<(unsigned)(gr < 8192 ? gr : 8192), BLK, 0, s>>>((uint32_t*)tab, bmask, (int)gens, (int)g);
   return (int)hipGetLastError();
 }
 

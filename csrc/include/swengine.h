@@ -191,8 +191,11 @@ typedef struct SwEngineArgs {
   // ---------------------------------------------------------------- string refs
   SwStrRef* spans;             // [rec_cap] per decoded record (decode writes, the block encoder reads)
   // ---------------------------------------------------------------- store-backed dedup filter
-  uint64_t* dd_bloom;          // [dd_bloom_mask + 1] blocked Bloom filter, 64-bit blocks (null: off)
-  int64_t dd_bloom_mask;       // blocks - 1
+  // generational fingerprint tables (swtypes.h, SW_FF_*): [buckets][gens][SW_FF_SLOTS] u32
+  uint32_t* dd_ff;             // null: off
+  int64_t dd_ff_bmask;         // buckets per generation - 1
+  int64_t dd_ff_gens;
+  int64_t* dd_ff_meta;         // [SW_FF_META + gens]
   // ---------------------------------------------------------------- string exchange (world > 1)
   // A record's strings (alternate id, metadata, alert message) live in the raw batch of the rank
   // that decoded it.  The partition copies them into per-destination byte slabs beside the record

@@ -197,18 +197,35 @@ SW_HD uint64_t sw_mix64(uint64_t x) {
   return x;
 }
 
-// Store-backed alternate-id filter: a blocked Bloom filter (64-bit blocks, 8 bits per id) of every
-// id the engine persisted.  An id new to the dedup window that the filter may hold is handed to the
-// host (SW_ST_RECHECK), which checks it against the event store -- dedup beyond the window without a
-// per-event store lookup on the hot path.  One word per id: one 8-byte load to probe, ONE atomic OR
-// to add (memory-side atomics are the MI355X's scarce resource here: each is its own 64-byte
-// request).  Same functions in every engine (bit-exact).
-SW_HD uint64_t sw_bloom_block(uint64_t h, int64_t mask) { return sw_mix64(h ^ 0x5bd1e9955bd1e995ULL) & (uint64_t)mask; }
-SW_HD uint64_t sw_bloom_bits(uint64_t h) {
-  const uint64_t g = sw_mix64(h + 0x9E3779B97F4A7C15ULL);
-  uint64_t m = 0;
-  for (int j = 0; j < 8; ++j) m |= 1ull << ((g >> (6 * j)) & 63u);
-  return m;
+// Store-backed alternate-id filter: generational exact-fingerprint tables of the ids the engine
+// persisted (the reference checks every alternate id against the store forever,
+// AlternateIdDeduplicator.java:43-56; here only ids new to the HBM window that the filter holds go
+// to the host as SW_ST_RECHECK, which checks them against the event store).
+//   * G generations of >= ids_per_gen persisted ids each: once the live generation has taken
+//     ids_per_gen ids (at the end of a step) the oldest is cleared and becomes the live one, so the
+//     filter always holds the newest (G - 1) * ids_per_gen ids -- and the durable store's retention
+//     keeps no more rows than that (retention by rows, persistence/segments.py; every retained id
+//     is then among the newest ids), so every retained id stays checked and nothing else is.
+//   * A generation is a linear-probed table of 16-slot buckets of 32-bit fingerprints (an id's
+//     bucket from the low bits of mix(h), its fingerprint from the high 32 bits, 0 = empty).  The
+//     G buckets of one home position are adjacent (bucket b of generation g at (b * G + g) * 16
+//     slots), so a probe of every generation reads G * 64 contiguous bytes; an add is ONE CAS.
+//   * False positives: an absent id matches a fingerprint of its bucket chain, ~(ids per bucket) /
+//     2^32 per generation -- ~1e-8 at the sizing load (<= 1/2), where a one-word Bloom filter at 128
+//     bits per id gave ~3e-6 and could only grow.
+// Same functions in every engine (bit-exact).
+#define SW_FF_SLOTS 16                 // fingerprints per bucket (64 bytes)
+#define SW_FF_MAX_PROBE 64             // buckets probed per generation before an add is dropped
+#define SW_FF_META 16                  // meta words before the per-generation row starts
+#define SW_FF_MAX_GENS 8
+// meta: [0] live generation, [1] unused, [2] ids per generation, [3] generations, [4] rotations,
+// [5] adds dropped (probe bound), [6] ids the live generation took, [7..15] pad,
+// [16 + g] store cursor when generation g became live
+SW_HD uint64_t sw_ff_mix(uint64_t h) { return sw_mix64(h ^ 0x5bd1e9955bd1e995ULL); }
+SW_HD uint64_t sw_ff_bucket(uint64_t m, int64_t bmask) { return m & (uint64_t)bmask; }
+SW_HD uint32_t sw_ff_fp(uint64_t m) {
+  const uint32_t f = (uint32_t)(m >> 32);
+  return f ? f : 1u;
 }
 
 // 128-bit fingerprint of a byte string: FNV-1a-64 and an independent odd-multiplier

@@ -29,6 +29,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <new>
 #include <condition_variable>
@@ -301,8 +302,12 @@ struct SwCpuEngine {
   std::vector<U64Map<int64_t>> dedup;       // current generation of the alternate-id window, by hash % T
   std::vector<U64Map<int64_t>> dedup_prev;  // previous generation (see the rotation in swce_process)
   int64_t dd_slots = 0, dd_batch = 0;       // window slots and the largest batch (rotation rule)
-  LazyWords bloom;                          // store-backed dedup filter (sw_bloom_*), empty: off
-  int64_t bloom_mask = 0;
+  // store-backed dedup filter (generational fingerprint tables, swtypes.h SW_FF_*), empty: off
+  LazyWords ff;                             // [buckets][gens][SW_FF_SLOTS] u32, as 64-bit words
+  int64_t ff_bmask = 0, ff_gens = 0;
+  int64_t ff_meta[SW_FF_META + SW_FF_MAX_GENS] = {};
+  uint32_t* ff_tab() { return reinterpret_cast<uint32_t*>(ff.data()); }
+  const uint32_t* ff_tab() const { return reinterpret_cast<const uint32_t*>(ff.data()); }
   U64Map<int32_t> intern;
   int32_t n_intern = 0;
   std::vector<U64Map<MsVal>> ms;       // sharded by assignment % T
@@ -327,13 +332,64 @@ static inline int32_t nid_of(const SwCpuEngine* e, uint64_t h) {
   return v ? *v : -1;
 }
 
-static inline bool bloom_has(const SwCpuEngine* e, uint64_t h) {
-  const uint64_t m = sw_bloom_bits(h);
-  return (e->bloom[sw_bloom_block(h, e->bloom_mask)] & m) == m;
+// Does a live generation of the filter hold the id (ff_has in csrc/hip/swgpu.hip)?
+static inline bool ff_has(const SwCpuEngine* e, uint64_t h) {
+  const uint64_t m = sw_ff_mix(h);
+  const uint32_t fp = sw_ff_fp(m);
+  const int gens = (int)e->ff_gens;
+  int64_t b = (int64_t)sw_ff_bucket(m, e->ff_bmask);
+  uint32_t open = (1u << gens) - 1u;
+  const uint32_t* t = e->ff_tab();
+  for (int p = 0; p < SW_FF_MAX_PROBE && open; ++p) {
+    for (int g = 0; g < gens; ++g) {
+      if (!((open >> g) & 1u)) continue;
+      const uint32_t* s = t + (b * gens + g) * SW_FF_SLOTS;
+      bool empty = false;
+      for (int k = 0; k < SW_FF_SLOTS; ++k) {
+        const uint32_t v = __atomic_load_n(&s[k], __ATOMIC_RELAXED);
+        if (v == fp) return true;
+        empty |= v == 0;
+      }
+      if (empty) open &= ~(1u << g);
+    }
+    b = (b + 1) & e->ff_bmask;
+  }
+  return false;
 }
 
-static inline void bloom_add(SwCpuEngine* e, uint64_t h) {
-  __atomic_fetch_or(&e->bloom[sw_bloom_block(h, e->bloom_mask)], sw_bloom_bits(h), __ATOMIC_RELAXED);
+// Add the id to generation g: one CAS into the first free slot of its chain (ff_add on the GPU).
+static inline bool ff_add(SwCpuEngine* e, int g, uint64_t h) {
+  const uint64_t m = sw_ff_mix(h);
+  const uint32_t fp = sw_ff_fp(m);
+  const int gens = (int)e->ff_gens;
+  int64_t b = (int64_t)sw_ff_bucket(m, e->ff_bmask);
+  uint32_t* t = e->ff_tab();
+  for (int p = 0; p < SW_FF_MAX_PROBE; ++p) {
+    uint32_t* s = t + (b * gens + g) * SW_FF_SLOTS;
+    for (int k = 0; k < SW_FF_SLOTS; ++k) {
+      uint32_t v = __atomic_load_n(&s[k], __ATOMIC_RELAXED);
+      if (v == fp) return true;
+      if (v == 0) {
+        if (__atomic_compare_exchange_n(&s[k], &v, fp, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return true;
+        if (v == fp) return true;       // the same id, added by another thread
+      }
+    }
+    b = (b + 1) & e->ff_bmask;
+  }
+  return false;
+}
+
+// Clear generation g.  Only buckets that hold something are written: untouched pages of the lazily
+// committed table stay uncommitted.
+static void ff_clear(SwCpuEngine* e, int g) {
+  const int64_t nb = e->ff_bmask + 1, gens = e->ff_gens;
+  uint32_t* t = e->ff_tab();
+  for (int64_t b = 0; b < nb; ++b) {
+    uint64_t* w = reinterpret_cast<uint64_t*>(t + (b * gens + g) * SW_FF_SLOTS);
+    uint64_t any = 0;
+    for (int k = 0; k < SW_FF_SLOTS / 2; ++k) any |= w[k];
+    if (any) memset(w, 0, SW_FF_SLOTS * sizeof(uint32_t));
+  }
 }
 
 static inline bool pip(const double* v, int32_t n, double x, double y) {
@@ -603,8 +659,8 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
             // Every record this rank owns goes through it when its strings came along (the host
             // settles a recheck by its alternate id); without the string exchange only records
             // decoded here do (the host path re-reads their payload).  A settled record skips it.
-            if (!e->bloom.empty() && !(work[i].flags & SW_F_SETTLED) &&
-                (any_rank || work[i].src_rank == (uint8_t)t->rank) && bloom_has(e, work[i].alt_hash))
+            if (!e->ff.empty() && !(work[i].flags & SW_F_SETTLED) &&
+                (any_rank || work[i].src_rank == (uint8_t)t->rank) && ff_has(e, work[i].alt_hash))
               status[i] = SW_ST_RECHECK;
           } else {
             status[i] = SW_ST_DUPLICATE;
@@ -651,14 +707,24 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
 
   // 5. persist + enrich (parallel rows); rows bucketed by assignment shard for the state merge
   const int64_t cursor0 = st->cursor;
+  const bool ff_on = !e->ff.empty();
+  const int ff_live = ff_on ? (int)e->ff_meta[0] : 0;
+  std::atomic<int64_t> ff_dropped{0}, ff_ids{0};
   e->pool.run([&](int w) {
     int64_t b, end;
     chunk_of(n_ok, w, T, &b, &end);
     persist_range(e, t, work, ok_idx, dev, [&](int64_t j) { return asg[ok_idx[j]]; }, cursor0, now_ms, out, b, end,
                   spans, prec, pspans);
-    if (!e->bloom.empty())                    // persisted ids join the store-backed filter
+    if (ff_on) {                              // persisted ids join the filter's live generation
+      int64_t dropped = 0, ids = 0;
       for (int64_t j = b; j < end; ++j)
-        if (work[ok_idx[j]].alt_hash) bloom_add(e, work[ok_idx[j]].alt_hash);
+        if (work[ok_idx[j]].alt_hash) {
+          ++ids;
+          if (!ff_add(e, ff_live, work[ok_idx[j]].alt_hash)) ++dropped;
+        }
+      if (dropped) ff_dropped += dropped;
+      if (ids) ff_ids += ids;
+    }
     if (T > 1) {
       for (int sh = 0; sh < T; ++sh) e->lists[(size_t)w * T + sh].clear();
       for (int64_t j = b; j < end; ++j) e->lists[(size_t)w * T + (uint32_t)out[j].assignment % (uint32_t)T].push_back((int32_t)j);
@@ -776,6 +842,18 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
     cursor += n_gen;
   }
   lap("gen");
+  if (ff_on) {
+    e->ff_meta[5] += ff_dropped.load();
+    e->ff_meta[6] += ff_ids.load();
+    if (e->ff_meta[6] >= e->ff_meta[2]) {     // the live generation has taken its ids: the oldest is
+      const int nxt = (int)((ff_live + 1) % e->ff_gens);   // cleared and becomes the live one
+      ff_clear(e, nxt);
+      e->ff_meta[0] = nxt;
+      e->ff_meta[SW_FF_META + nxt] = cursor;
+      e->ff_meta[6] = 0;
+      e->ff_meta[4] += 1;
+    }
+  }
 
   // 10. bookkeeping (SW_STAT_* slots; messages and new names are counted by the caller)
   uint64_t c[8] = {};
@@ -801,32 +879,52 @@ int32_t swce_process(void* p, const SwCeTables* t, SwCeStep* st, const SwEventRe
   return 0;
 }
 
-// Store-backed dedup filter: `bits` (a power of two >= 64, 0 = off); cleared.
-void swce_bloom_init(void* p, int64_t bits) {
+// Store-backed dedup filter: `buckets` per generation (a power of two, 0 = off), `gens` generations
+// (2..SW_FF_MAX_GENS) of `ids_per_gen` persisted ids; cleared, generation 0 live.
+int32_t swce_ff_init(void* p, int64_t buckets, int64_t gens, int64_t ids_per_gen) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  const int64_t blocks = bits / 64;
-  e->bloom.assign_zero(blocks > 0 ? (size_t)blocks : 0);
-  e->bloom_mask = blocks > 0 ? blocks - 1 : 0;
+  if (buckets > 0 && ((buckets & (buckets - 1)) || gens < 2 || gens > SW_FF_MAX_GENS || ids_per_gen <= 0)) return -1;
+  e->ff.assign_zero(buckets > 0 ? (size_t)(buckets * gens * SW_FF_SLOTS / 2) : 0);
+  if (buckets > 0 && e->ff.empty()) return -2;
+  e->ff_bmask = buckets > 0 ? buckets - 1 : 0;
+  e->ff_gens = buckets > 0 ? gens : 0;
+  memset(e->ff_meta, 0, sizeof(e->ff_meta));
+  e->ff_meta[2] = ids_per_gen;
+  e->ff_meta[3] = e->ff_gens;
+  return 0;
 }
 
-void swce_bloom_add(void* p, const uint64_t* h, int64_t n) {
+// Add ids to generation g (warm start from the store; EngineBase.filter_seed).
+void swce_ff_add(void* p, int64_t g, const uint64_t* h, int64_t n) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  if (e->bloom.empty()) return;
+  if (e->ff.empty() || g < 0 || g >= e->ff_gens) return;
   for (int64_t i = 0; i < n; ++i)
-    if (h[i]) bloom_add(e, h[i]);
+    if (h[i] && !ff_add(e, (int)g, h[i])) e->ff_meta[5] += 1;
 }
 
-// The filter's words (checkpoints).
-int64_t swce_bloom_words(void* p, uint64_t* out, int64_t cap) {
+void swce_ff_clear(void* p, int64_t g) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  const int64_t n = (int64_t)e->bloom.size();
-  if (out && cap >= n) memcpy(out, e->bloom.data(), (size_t)n * 8);
+  if (!e->ff.empty() && g >= 0 && g < e->ff_gens) ff_clear(e, (int)g);
+}
+
+// The filter's meta words (SW_FF_META + SW_FF_MAX_GENS): read into `out`, then, with `in`, replaced.
+void swce_ff_meta(void* p, int64_t* out, const int64_t* in) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  if (out) memcpy(out, e->ff_meta, sizeof(e->ff_meta));
+  if (in) memcpy(e->ff_meta, in, sizeof(e->ff_meta));
+}
+
+// The filter's table as 64-bit words (checkpoints).
+int64_t swce_ff_words(void* p, uint64_t* out, int64_t cap) {
+  SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
+  const int64_t n = (int64_t)e->ff.size();
+  if (out && cap >= n) memcpy(out, e->ff.data(), (size_t)n * 8);
   return n;
 }
 
-void swce_bloom_load(void* p, const uint64_t* w, int64_t n) {
+void swce_ff_load(void* p, const uint64_t* w, int64_t n) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  if ((int64_t)e->bloom.size() == n) memcpy(e->bloom.data(), w, (size_t)n * 8);
+  if ((int64_t)e->ff.size() == n) memcpy(e->ff.data(), w, (size_t)n * 8);
 }
 
 // Window sizing of the generational dedup (slots per generation, largest batch in records).

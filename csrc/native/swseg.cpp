@@ -1138,6 +1138,7 @@ struct SegFile {
   int64_t first_seq;
   int64_t bytes;
   int32_t id;
+  int64_t rows = 0;      // event rows of the file's blocks (retention by rows)
 };
 
 // Block index entry (kept in memory by the store, rebuilt by the recovery scan).
@@ -1218,6 +1219,11 @@ struct SegStore {
   int32_t rank = 0;
   int64_t rotate_bytes = 1ll << 30;
   int64_t retention_bytes = 0;
+  // retention by rows (0: none): oldest whole files are deleted while the rows kept exceed it -- an
+  // engine tenant's store-backed dedup filter remembers the newest N alternate ids, and a store that
+  // keeps at most N rows keeps no id it has forgotten (EngineConfig.filter_retention_rows)
+  int64_t retention_rows = 0;
+  int64_t total_rows = 0;
   bool direct = true;
   std::mutex mu;
   std::condition_variable cv, cv_done;
@@ -1230,7 +1236,8 @@ struct SegStore {
   int fd_direct = 0;
   int64_t cur_bytes = 0;
   std::atomic<int64_t> durable{-1};
-  std::atomic<int64_t> bytes_written{0}, blocks_written{0}, syncs{0}, deleted_files{0}, deleted_bytes{0};
+  std::atomic<int64_t> bytes_written{0}, blocks_written{0}, syncs{0}, deleted_files{0}, deleted_bytes{0},
+      deleted_rows{0};
   // where the writer's time goes (ns): block writes, fdatasync, waiting for the copier; the copier's own
   std::atomic<int64_t> write_ns{0}, sync_ns{0}, cwait_ns{0}, copy_ns{0};
   std::atomic<int32_t> error{0};
@@ -1548,9 +1555,10 @@ static void seg_close_file(SegStore* s) {
 }
 
 static void seg_retention(SegStore* s) {
-  if (s->retention_bytes <= 0) return;
+  if (s->retention_bytes <= 0 && s->retention_rows <= 0) return;
   std::lock_guard<std::mutex> g(s->mu);
-  while (s->files.size() > 1 && s->total_bytes > s->retention_bytes) {
+  while (s->files.size() > 1 && ((s->retention_bytes > 0 && s->total_bytes > s->retention_bytes) ||
+                                 (s->retention_rows > 0 && s->total_rows > s->retention_rows))) {
     const SegFile f = s->files.front();
     if (unlink(f.path.c_str()) != 0) break;
     s->files.erase(s->files.begin());
@@ -1583,6 +1591,8 @@ static void seg_retention(SegStore* s) {
     s->bk_cap.resize(k);
     ++s->epoch;
     s->total_bytes -= f.bytes;
+    s->total_rows -= f.rows;
+    s->deleted_rows += f.rows;
     s->deleted_files += 1;
     s->deleted_bytes += f.bytes;
   }
@@ -1704,6 +1714,8 @@ static void seg_writer(SegStore* s) {
         std::lock_guard<std::mutex> g(s->mu);
         s->files.back().bytes += padded + extra;
         s->total_bytes += padded + extra;
+        s->files.back().rows += h.n_rows;
+        s->total_rows += h.n_rows;
       }
       s->cur_bytes += padded + extra;
       s->bytes_written += padded + extra;
@@ -1842,6 +1854,7 @@ void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t ret
         f.path, true,
         [&](int64_t off, const SwSegBlockHdr& hd, const uint8_t* b) {
           s->index.push_back(index_entry(hd, b, f.id, off));
+          f.rows += hd.n_rows;
           const auto ts = trailer_span(b, (int64_t)hd.bytes);
           uint8_t* t = ts.second ? own_copy(b + ts.first, ts.second) : nullptr;
           s->tr_ptr.push_back(t);
@@ -1868,6 +1881,7 @@ void* swss_open(const char* dir, int32_t rank, int64_t rotate_bytes, int64_t ret
     ++s->next_file_id;
     s->files.push_back(f);
     s->total_bytes += f.bytes;
+    s->total_rows += f.rows;
   }
   s->copier = std::thread(seg_copier, s);
   s->th = std::thread(seg_writer, s);
@@ -1955,6 +1969,20 @@ void swss_stats(void* h, int64_t* out) {
   out[9] = s->sync_ns;
   out[10] = s->cwait_ns;
   out[11] = s->copy_ns;
+  out[12] = s->total_rows;
+  out[13] = s->deleted_rows;
+  out[14] = s->retention_rows;
+  out[15] = s->retention_bytes;
+}
+
+// Retention limits (<= 0: unchanged; rows 0 is set with -1: none).  Applied when the next file
+// starts, like the store's own (whole files, oldest first).
+void swss_set_retention(void* h, int64_t bytes, int64_t rows) {
+  SegStore* s = (SegStore*)h;
+  std::lock_guard<std::mutex> g(s->mu);
+  if (bytes > 0) s->retention_bytes = bytes;
+  if (rows > 0) s->retention_rows = rows;
+  if (rows < 0) s->retention_rows = 0;
 }
 
 void swss_close(void* h) {

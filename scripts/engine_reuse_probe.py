@@ -19,7 +19,7 @@ from sitewhere_amd.pipeline.fleet import fingerprint_str, pack_messages  # noqa:
 from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine  # noqa: E402
 
 COLUMNAR = {"max_msgs": 1 << 18, "max_devices": 65536, "max_assignments": 65536, "store_cap": 1 << 22,
-            "dedup_slots": 1 << 24, "gen_cap": 32768, "dedup_bloom_bits": 1 << 34}
+            "dedup_slots": 1 << 24, "gen_cap": 32768, "dedup_filter_ids": (1 << 28) - (1 << 21)}
 
 
 def batch(msgs):

@@ -163,10 +163,12 @@ def native():
             _proto(lib, f"swce_{kind}_size", c_int64, P)
         _proto(lib, "swce_dedup_export", c_int64, P, P, P)
         _proto(lib, "swce_dedup_window", None, P, c_int64, c_int64)
-        _proto(lib, "swce_bloom_init", None, P, c_int64)
-        _proto(lib, "swce_bloom_add", None, P, P, c_int64)
-        _proto(lib, "swce_bloom_words", c_int64, P, P, c_int64)
-        _proto(lib, "swce_bloom_load", None, P, P, c_int64)
+        _proto(lib, "swce_ff_init", c_int32, P, c_int64, c_int64, c_int64)
+        _proto(lib, "swce_ff_add", None, P, c_int64, P, c_int64)
+        _proto(lib, "swce_ff_clear", None, P, c_int64)
+        _proto(lib, "swce_ff_meta", None, P, P, P)
+        _proto(lib, "swce_ff_words", c_int64, P, P, c_int64)
+        _proto(lib, "swce_ff_load", None, P, P, c_int64)
         _proto(lib, "swce_dedup_prev_size", c_int64, P)
         _proto(lib, "swce_dedup_prev_export", c_int64, P, P, P)
         _proto(lib, "swce_dedup_prev_import", None, P, P, P, c_int64)
@@ -217,6 +219,7 @@ def native():
         _proto(lib, "swss_error", c_int32, P)
         _proto(lib, "swss_wait", c_int32, P, c_int64, c_int64)
         _proto(lib, "swss_stats", None, P, P)
+        _proto(lib, "swss_set_retention", None, P, c_int64, c_int64)
         _proto(lib, "swss_close", None, P)
         _proto(lib, "swss_index", c_int64, P, P, c_int64)
         _proto(lib, "swss_index_tr", c_int64, P, P, P, P, P, c_int64)
@@ -321,7 +324,8 @@ def gpu():
         _proto(lib, "sw_seg_index", c_int32, P, P, P, P, P, c_int64, P, c_int64, P, P, c_int64, P, c_int64, P, P,
                c_int64, P, P)
         _proto(lib, "sw_seg_index_stamp_words", c_int64, c_int64)
-        _proto(lib, "sw_bloom_add", c_int32, P, c_int64, P, c_int64, P)
+        _proto(lib, "sw_ff_add", c_int32, P, c_int64, c_int64, c_int64, P, P, c_int64, P)
+        _proto(lib, "sw_ff_clear", c_int32, P, c_int64, c_int64, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
         _gpu = lib

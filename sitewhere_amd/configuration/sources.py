@@ -231,7 +231,8 @@ class InboundProcessingProvider(ModelProvider):
             ("gen_cap", "rule alerts + presence events per step"), ("max_devices", "registry capacity"),
             ("max_assignments", "assignment capacity"), ("store_cap", "HBM event ring (events)"),
             ("dedup_slots", "alternate-id window slots per generation"),
-            ("dedup_bloom_bits", "store-backed dedup filter bits (0 = off; ~16 bits per stored id)"),
+            ("dedup_filter_ids", "store-backed dedup filter: ids per generation (0 = off; ~8 B of HBM per id and generation)"),
+            ("dedup_filter_gens", "store-backed dedup filter generations (2..8; the newest gens - 1 are always held)"),
             ("name_slots", "distinct names"),
             ("state_slots", "(assignment, name) state slots"), ("names_cap", "new-name reports per step"),
             ("shuffle_pad", "records added to every re-key slab"), ("carry_cap", "re-key carry records"),

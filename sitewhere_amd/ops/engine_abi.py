@@ -59,9 +59,8 @@ FIELDS = [
     ("dd_meta", P),
     # string refs of the decoded records (SwStrRef, read by the durable-block encoder)
     ("spans", P),
-    # store-backed dedup filter (blocked Bloom filter, null = off)
-    ("dd_bloom", P),
-    ("dd_bloom_mask", I),
+    # store-backed dedup filter (generational fingerprint tables, swtypes.h SW_FF_*; null = off)
+    ("dd_ff", P), ("dd_ff_bmask", I), ("dd_ff_gens", I), ("dd_ff_meta", P),
     # string exchange (world > 1): per-destination byte slabs + refs beside the record slabs
     ("send_str", P), ("send_str_cnt", P), ("send_spans", P), ("recv_str", P), ("recv_str_cnt", P),
     ("recv_spans", P), ("work_str", P), ("work_spans", P), ("str_cap", I), ("str_drops", P),

@@ -152,6 +152,28 @@ class ApiDictionary:
         return d
 
 
+def row_limit_error(e) -> str | None:
+    """Why ``e`` cannot be one block row, or None.  String spans are u16 in the block format: the
+    alternate id, an alert's message and the metadata (or JSON fields) span each hold <= 65535 bytes.
+    ``DurableEventStore.add_events`` checks this before the event reaches its write-ahead log, so an
+    add is refused up front instead of failing every later flush of the API tail (nothing is ever
+    truncated: a cut alternate id would also break its dedup)."""
+    et = _ETYPE.get(DeviceEventType(e.event_type))
+    if et is None:
+        return f"event type {e.event_type} cannot be stored"
+    if e.alternate_id and len(e.alternate_id.encode()) > MAX_STR:
+        return f"alternate id longer than {MAX_STR} bytes"
+    if et == EV_ALERT and e.message and len(e.message.encode()) > MAX_STR:
+        return f"alert message longer than {MAX_STR} bytes"
+    if et in (EV_MEASUREMENT, EV_LOCATION, EV_ALERT):
+        meta = metadata_wire(e.metadata, _META_FIELD[et]) if e.metadata else b""
+    else:
+        meta = json.dumps(json_fields(e), separators=(",", ":")).encode()
+    if len(meta) > MAX_STR:
+        return f"event fields / metadata too large for a block row ({len(meta)} > {MAX_STR} bytes)"
+    return None
+
+
 def encode_events(events, dic: ApiDictionary):
     """API events -> (OUT_REC rows, EVENT_REC records, STR_REF spans, string bytes) for
     :func:`segments.encode_block`, in the given order."""
@@ -186,7 +208,9 @@ def encode_events(events, dic: ApiDictionary):
             r["level"] = ALERT_LEVEL_INDEX.get(e.level, 0) if not isinstance(e.level, int) else e.level
             if AlertSource(e.source) == AlertSource.System:
                 flags |= SW_F_SYS_ALERT
-            mb = (e.message or "").encode()[:MAX_STR]
+            mb = (e.message or "").encode()
+            if len(mb) > MAX_STR:
+                raise ValueError(f"alert message longer than {MAX_STR} bytes")
             if mb:
                 x["aux2_off"], x["aux2_len"] = len(heap), len(mb)
                 heap += mb
@@ -198,7 +222,9 @@ def encode_events(events, dic: ApiDictionary):
         x["flags"] = flags
         has = 0
         if e.alternate_id:
-            ab = e.alternate_id.encode()[:MAX_STR]
+            ab = e.alternate_id.encode()
+            if len(ab) > MAX_STR:
+                raise ValueError(f"alternate id longer than {MAX_STR} bytes")
             s["alt_off"], s["alt_len"] = len(heap), len(ab)
             heap += ab
             has |= SR_ALT

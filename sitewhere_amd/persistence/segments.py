@@ -459,11 +459,16 @@ class SegmentStore:
         return self._token
 
     def stats(self) -> dict:
-        a = np.zeros(12, np.int64)
+        a = np.zeros(16, np.int64)
         self.lib.swss_stats(self.h, _p(a))
         return dict(zip(("bytes_written", "blocks_written", "syncs", "deleted_files", "deleted_bytes", "retained_bytes",
-                         "files", "direct_io", "write_ns", "sync_ns", "copier_wait_ns", "copier_ns"),
+                         "files", "direct_io", "write_ns", "sync_ns", "copier_wait_ns", "copier_ns", "retained_rows",
+                         "deleted_rows", "retention_rows", "retention_bytes"),
                         (int(x) for x in a)))
+
+    def set_retention(self, bytes_: int = 0, rows: int = 0):
+        """Tighten / set the retention limits (0: unchanged; rows -1: none); the next file applies them."""
+        self.lib.swss_set_retention(self.h, int(bytes_), int(rows))
 
     def index(self) -> np.ndarray:
         cap = 1024
@@ -716,6 +721,7 @@ class DurableEventStore(DeviceEventStore):
         # every block arrives with its index trailer)
         self.dir = directory
         os.makedirs(directory, exist_ok=True)
+        self.rotate_bytes = int(rotate_bytes)
         self.seg = SegmentStore(directory, rank, rotate_bytes, retention_bytes, direct)
         # the scan images of recent blocks (page headers + leading columns) kept in memory as the
         # blocks are written (the writes bypass the page cache): listings over fresh data -- the
@@ -865,6 +871,12 @@ class DurableEventStore(DeviceEventStore):
         holds them once the tail is flushed (see api_blocks.py)."""
         if not events:
             return events
+        from .api_blocks import row_limit_error
+        for e in events:                 # refused before the log: a row no block can hold
+            why = row_limit_error(e)
+            if why is not None:
+                from ..core.errors import ErrorCode, SiteWhereSystemException
+                raise SiteWhereSystemException(ErrorCode.Error, detail=f"event not stored: {why}")
         now = int(time.time() * 1000)
         with self._api_lock:
             lines = []
@@ -892,8 +904,11 @@ class DurableEventStore(DeviceEventStore):
                 break
             try:
                 self.flush_api()
+                self._api_err = None
             except Exception as e:  # noqa: BLE001 -- the tail stays in the log; retried next round
                 self._api_err = f"{type(e).__name__}: {e}"
+                import logging
+                logging.getLogger(__name__).error("API event tail flush failed (retried): %s", self._api_err)
 
     def _api_dictionary(self):
         from .api_blocks import ApiDictionary
@@ -1217,6 +1232,26 @@ class DurableEventStore(DeviceEventStore):
         self._tabs = (ver, res, taddr, baddr)
         return res
 
+    def retention_state(self) -> dict:
+        """Retention limits and what the store holds (rows / bytes retained and deleted), plus the
+        API tail's flush health (``api_flush_error``: the last failed flush, None when healthy)."""
+        st = self.seg.stats()
+        return {k: st[k] for k in ("retention_rows", "retention_bytes", "retained_rows", "retained_bytes",
+                                   "deleted_rows", "deleted_bytes", "deleted_files", "files")} | {
+            "api_tail": len(self._api_tail), "api_flush_error": self._api_err, "rotate_bytes": self.rotate_bytes}
+
+    def limit_retention_rows(self, rows: int) -> int:
+        """Keep at most ``rows`` event rows (whole segment files, oldest first; applied when the next
+        file starts): an engine tenant whose store-backed dedup filter remembers its newest N ids sets
+        this, so the store holds no id the filter has forgotten.  Only ever tightens.  Returns the
+        limit in force."""
+        cur = self.seg.stats()["retention_rows"]
+        rows = int(rows)
+        if rows > 0 and (cur <= 0 or rows < cur):
+            self.seg.set_retention(0, rows)
+            cur = rows
+        return cur
+
     def index_wait(self, timeout_s: float = 60.0) -> bool:
         """Every block is indexed as it is written (its trailer): nothing to wait for."""
         return True
@@ -1258,7 +1293,9 @@ class DurableEventStore(DeviceEventStore):
         pairs.sort(key=lambda x: (int(x[0]["recv_ms"]), int(x[0]["first_seq"])), reverse=True)
         ents = []
         for e, n in pairs:
-            if skip > 0 and n is not None and skip >= n:
+            # whole blocks are skipped by their trailer counts only up to the first block kept: the
+            # rest of the skip (if any) is cut from the decoded ids below, in order
+            if not ents and skip > 0 and n is not None and skip >= n:
                 skip -= n
                 continue
             ents.append(e)

@@ -21,10 +21,14 @@ class EngineConfig:
     max_assignments: int = 1 << 20
     store_cap: int = 1 << 27         # HBM event-store ring capacity (events)
     dedup_slots: int = 1 << 22       # alternate-id window (slots; window = slots / 2)
-    # store-backed dedup beyond the window: a blocked Bloom filter of every persisted alternate id
-    # (bits, rounded up to a power of two; 0 = off).  32 bits per id kept -> ~5e-5 of new ids
-    # rechecked on the host, 64 bits per id -> ~1e-6
-    dedup_bloom_bits: int = 0
+    # store-backed dedup beyond the window: generational fingerprint tables of the persisted
+    # alternate ids (csrc/include/swtypes.h SW_FF_*).  Each of ``dedup_filter_gens`` generations
+    # takes ``dedup_filter_ids`` persisted ids (0 = off); the filter always holds the newest
+    # (gens - 1) * ids ids -- the durable store's retention by rows is set from it
+    # (``filter_retention_rows``).  HBM: gens * 2 * (ids + rec_cap) * 4 bytes (~8 B per id and
+    # generation at load <= 1/2); false positives ~1e-8 of new ids.
+    dedup_filter_ids: int = 0
+    dedup_filter_gens: int = 4
     name_slots: int = 1 << 16        # distinct measurement names / alert types
     state_slots: int = 0             # (assignment, name) state map slots (0 = 16 * max_assignments)
     names_cap: int = 4096            # new-name reports per step
@@ -58,8 +62,6 @@ class EngineConfig:
         # would pass that): smaller tables overflow on every step and probe to their limit
         self.dedup_slots = pow2_at_least(max(self.dedup_slots, 2 * self.rec_cap))
         self.name_slots = pow2_at_least(self.name_slots)
-        if self.dedup_bloom_bits > 0:
-            self.dedup_bloom_bits = pow2_at_least(max(512, self.dedup_bloom_bits))
         self.state_slots = pow2_at_least(self.state_slots)
         # key bits of the clustering sort (assignment indices < max_assignments)
         self.cl_bits = max(1, (self.max_assignments - 1).bit_length()) if self.cluster else 0
@@ -83,6 +85,29 @@ class EngineConfig:
         # carry_cap); u32 offsets
         self.carry_str_cap = min((self.carry_cap * max(2 * self.str_bytes, 64) + 15) // 16 * 16, 0xFFFFFFF0) \
             if self.world > 1 and self.str_bytes > 0 else 0
+        if self.dedup_filter_ids > 0:
+            if not 2 <= self.dedup_filter_gens <= 8:
+                raise ValueError("dedup_filter_gens must be 2..8")
+            # the window's retired generation is probed only for ids the filter holds (k_dedup_claim):
+            # the filter's newest (gens - 1) generations must hold at least the window's ids
+            self.dedup_filter_ids = max(self.dedup_filter_ids, self.dedup_slots)
+            # load <= 1/2 even for the step that crosses the generation's ids (it still adds to it)
+            self.ff_buckets = pow2_at_least(max(64, (2 * (self.dedup_filter_ids + self.rec_cap) + 15) // 16))
+        else:
+            self.dedup_filter_ids = 0
+            self.ff_buckets = 0
+
+    def filter_retention_rows(self, slack_rows: int = 0) -> int:
+        """Rows the durable store may retain so that the filter holds every retained id (0: no
+        filter, no bound).  The filter holds at least the newest (gens - 1) * dedup_filter_ids ids;
+        a store that keeps at most that many rows (newest first) keeps no id older than them.
+        ``slack_rows``: rows of blocks in flight and of one segment file (whole files are deleted)."""
+        if not self.dedup_filter_ids:
+            return 0
+        return max(self.rec_cap, (self.dedup_filter_gens - 1) * self.dedup_filter_ids - int(slack_rows))
+
+    def filter_bytes(self) -> int:
+        return self.ff_buckets * self.dedup_filter_gens * 64 if self.dedup_filter_ids else 0
 
     @classmethod
     def small(cls, **kw):

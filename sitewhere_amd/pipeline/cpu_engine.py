@@ -15,6 +15,7 @@ from ..models.columnar import (EVENT_REC, OUT_REC, EV_ALERT, EV_LOCATION, EV_MEA
                                ST_DECODE_ERROR, ST_CONTROL, ST_RECHECK, STAT_NAMES, N_STATS, STR_REF, WIRE_REC,
                                F_SETTLED, wire_pack, wire_unpack)
 from .config import EngineConfig
+from .dedup_filter import FingerprintFilter
 from .engine_base import EngineBase, StepResult
 from .fleet import cpu_decode
 
@@ -68,10 +69,9 @@ class CpuInboundEngine(EngineBase):
         self.seq_base = 0
         self.dedup: dict[int, int] = {}          # current generation of the alternate-id window
         self.dedup_prev: dict[int, int] = {}     # previous generation
-        # store-backed dedup filter (blocked Bloom filter of every persisted alternate id; sw_bloom_*)
-        nb = cfg.dedup_bloom_bits // 64
-        self.bloom = np.zeros(nb, np.uint64) if nb else None
-        self.bloom_mask = nb - 1
+        # store-backed dedup filter (generational fingerprint tables, pipeline/dedup_filter.py)
+        self.ff = (FingerprintFilter(cfg.ff_buckets, cfg.dedup_filter_gens, cfg.dedup_filter_ids)
+                   if cfg.dedup_filter_ids else None)
         self.intern: dict[int, int] = {}
         self.st_last = np.zeros(cfg.max_assignments, np.uint64)
         self.st_missing = np.zeros(cfg.max_assignments, np.uint64)
@@ -372,8 +372,8 @@ class CpuInboundEngine(EngineBase):
                 # owns when their strings came along (``any_rank``: the host settles a recheck by its
                 # alternate id), else only records decoded here (the host path re-reads their
                 # payload); a record the host already settled skips it
-                if (self.bloom is not None and not (int(recs[i]["flags"]) & F_SETTLED)
-                        and (any_rank or int(recs[i]["src_rank"]) == self.rank) and self._bloom_has(h)):
+                if (self.ff is not None and not (int(recs[i]["flags"]) & F_SETTLED)
+                        and (any_rank or int(recs[i]["src_rank"]) == self.rank) and self.ff.has(h)):
                     status[i] = ST_RECHECK
 
     def reset_dedup(self):
@@ -381,26 +381,20 @@ class CpuInboundEngine(EngineBase):
         self.dedup, self.dedup_prev = {}, {}
         self.dedup_valid_from = self.cursor           # the window holds no id of the rows before
 
-    def _bloom_pos(self, h: int):
-        blk = mix64(h ^ 0x5bd1e9955bd1e995) & self.bloom_mask
-        g = mix64((h + 0x9E3779B97F4A7C15) & _M64)
-        m = 0
-        for j in range(8):
-            m |= 1 << ((g >> (6 * j)) & 63)
-        return blk, m
+    # store-backed filter primitives (EngineBase.filter_seed / filter_state)
+    def _ff_meta_get(self) -> np.ndarray:
+        return self.ff.meta.copy()
 
-    def _bloom_has(self, h: int) -> bool:
-        w, m = self._bloom_pos(h)
-        return (int(self.bloom[w]) & m) == m
+    def _ff_meta_set(self, m):
+        self.ff.meta[:] = m
 
-    def bloom_add(self, hashes):
-        """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
-        if self.bloom is None:
-            return
+    def _ff_add(self, hashes, g: int):
         for h in np.asarray(hashes, np.uint64).tolist():
             if h:
-                w, m = self._bloom_pos(int(h))
-                self.bloom[w] |= np.uint64(m)
+                self.ff.add(int(h), g)
+
+    def _ff_clear(self, g: int):
+        self.ff.clear(g)
 
     def _intern_id(self, h: int) -> int:
         if h not in self.intern:
@@ -506,7 +500,8 @@ class CpuInboundEngine(EngineBase):
             ok = ok[np.argsort(asg[ok], kind="stable")]
         out_rows: list = []
         self._persist(work[ok], dev[ok], asg[ok], now_ms, out_rows)
-        self.bloom_add(work[ok]["alt_hash"])             # persisted ids join the store-backed filter
+        if self.ff is not None:                          # persisted ids join the filter's live generation
+            self.ff.add_persisted(work[ok]["alt_hash"])
         self._state(work[ok], asg[ok], now_ms)
         self.cursor += len(ok)
         # rules on persisted locations
@@ -550,6 +545,8 @@ class CpuInboundEngine(EngineBase):
             self._persist(g, gd, ga, now_ms, out_rows)
             self._state(g, ga, now_ms)
             self.cursor += len(g)
+        if self.ff is not None:
+            self.ff.end_step(self.cursor)
         # bookkeeping
         self.seq_base += len(work)
         st = self.stats
@@ -582,7 +579,7 @@ class CpuInboundEngine(EngineBase):
             "dedup_key": u64(self.dedup.keys()), "dedup_seq": np.array(list(self.dedup.values()), np.int64),
             "dedup_prev_key": u64(self.dedup_prev.keys()),
             "dedup_prev_seq": np.array(list(self.dedup_prev.values()), np.int64),
-            **({"dd_bloom": self.bloom.copy()} if self.bloom is not None else {}),
+            **({"dd_ff": self.ff.tab.copy(), "dd_ff_meta": self.ff.meta.copy()} if self.ff is not None else {}),
             "intern_key": u64(self.intern.keys()), "intern_id": np.array(list(self.intern.values()), np.int64),
             "seen": u64(self._seen),
             "st_last": self.st_last, "st_missing": self.st_missing, "st_loc_date": self.st_loc_date,
@@ -601,8 +598,9 @@ class CpuInboundEngine(EngineBase):
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
         self.stats[:] = 0
         self.stats[:len(a["stats"])] = a["stats"]
-        if self.bloom is not None and "dd_bloom" in a and len(a["dd_bloom"]) == len(self.bloom):
-            self.bloom[:] = a["dd_bloom"]
+        if self.ff is not None and "dd_ff" in a and len(a["dd_ff"]) == len(self.ff.tab):
+            self.ff.tab[:] = a["dd_ff"]
+            self.ff.meta[:] = a["dd_ff_meta"]
         self.dedup = dict(zip((int(x) for x in a["dedup_key"]), (int(x) for x in a["dedup_seq"])))
         self.dedup_prev = dict(zip((int(x) for x in a.get("dedup_prev_key", [])),
                                    (int(x) for x in a.get("dedup_prev_seq", []))))

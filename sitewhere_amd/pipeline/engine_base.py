@@ -296,6 +296,58 @@ class EngineBase:
         """Submitted batches whose results have not been returned yet."""
         return 0 if getattr(self, "_lagged", None) is None else 1
 
+    # ------------------------------------------------------------------ store-backed dedup filter
+    # Engines implement four primitives over their filter (pipeline/dedup_filter.py layout):
+    # _ff_meta_get / _ff_meta_set (meta words), _ff_add (ids into one generation, not counted),
+    # _ff_clear (one generation).
+    @property
+    def filter_on(self) -> bool:
+        return bool(getattr(self.cfg, "dedup_filter_ids", 0))
+
+    def filter_seed_begin(self):
+        """Start a warm start from the durable store (:meth:`filter_seed`)."""
+        m = self._ff_meta_get() if self.filter_on else None
+        self._seed = [int(m[0]), int(m[6]), 0] if m is not None else None
+
+    def filter_seed(self, hashes) -> int:
+        """Warm start from the durable store: ``hashes`` are stored alternate ids, NEWEST FIRST (call
+        once per chunk, in that order, after :meth:`filter_seed_begin`).  The newest fill the live
+        generation, older ones the generations before it (each up to its ids), as if the engine had
+        persisted them; what no generation can take is older than the filter remembers -- retention
+        by rows keeps it out of the store anyway.  Returns the ids added."""
+        if not self.filter_on:
+            return 0
+        if getattr(self, "_seed", None) is None:
+            self.filter_seed_begin()
+        h = np.asarray(hashes, np.uint64)
+        h = h[h != 0]
+        m = self._ff_meta_get()
+        G, C = int(m[3]), int(m[2])
+        g, k, filled = self._seed
+        i = added = 0
+        while i < len(h) and filled < G:
+            take = h[i:i + max(0, C - k)]
+            if len(take):
+                self._ff_add(take, g)
+                k += len(take)
+                i += len(take)
+                added += len(take)
+                if g == int(m[0]):
+                    m[6] = k
+            if k >= C:                               # this generation is full: the one before it
+                filled += 1
+                g, k = (g - 1) % G, 0
+        self._seed = [g, k, filled]
+        self._ff_meta_set(m)
+        return added
+
+    def filter_state(self) -> dict:
+        """The filter's live generation, rotations, ids taken, probe drops (``dedup_filter.filter_state``)."""
+        if not self.filter_on:
+            return {}
+        from .dedup_filter import filter_state
+        return filter_state(self._ff_meta_get())
+
     # ------------------------------------------------------------------ hot-store queries
     def query_store(self, event_type: int, asg_idx, start: int | None = None, end: int | None = None,
                     page_number: int = 1, page_size: int = 100):

@@ -193,9 +193,12 @@ class GpuInboundEngine(EngineBase):
         # two generations (see k_dedup_rotate) of packed 16-byte slots {alternate-id hash, first sequence}
         t["dd_tab"] = z(4 * c.dedup_slots, i64).view(2 * c.dedup_slots, 2)
         t["dd_tab"][:, 1] = -1
-        # store-backed dedup filter: blocked Bloom filter of every persisted alternate id (sw_bloom_*)
-        self._bloom_blocks = c.dedup_bloom_bits // 64          # one 64-bit word per block
-        t["dd_bloom"] = z(max(1, self._bloom_blocks), i64)
+        # store-backed dedup filter: generational fingerprint tables of the persisted alternate ids
+        # (pipeline/dedup_filter.py; [buckets][gens][16] u32, meta words)
+        self._ff_on = c.dedup_filter_ids > 0
+        t["dd_ff"] = z(max(16, c.ff_buckets * c.dedup_filter_gens * 16) if self._ff_on else 16, torch.int32)
+        from .dedup_filter import meta_words
+        t["dd_ff_meta"] = torch.from_numpy(meta_words(c.dedup_filter_gens, max(1, c.dedup_filter_ids))).to(d)
         t["dd_meta"] = torch.from_numpy(self._armed_dedup_meta(np.zeros(4, np.int64), c)).to(d)
         t["seq_base"] = z(1, i64)
         # names intern
@@ -267,8 +270,10 @@ class GpuInboundEngine(EngineBase):
         a.reg, a.reg_mask = _ptr(t["reg"]), c.reg_slots - 1
         a.asg_ctx, a.asg_active, a.n_asg = _ptr(t["asg_ctx"]), _ptr(t["asg_active"]), c.max_assignments
         a.dd_key, a.dd_seq, a.dd_mask, a.seq_base = _ptr(t["dd_tab"]), 0, c.dedup_slots - 1, _ptr(t["seq_base"])
-        a.dd_bloom = _ptr(t["dd_bloom"]) if self._bloom_blocks else 0
-        a.dd_bloom_mask = self._bloom_blocks - 1 if self._bloom_blocks else 0
+        a.dd_ff = _ptr(t["dd_ff"]) if self._ff_on else 0
+        a.dd_ff_bmask = c.ff_buckets - 1 if self._ff_on else 0
+        a.dd_ff_gens = c.dedup_filter_gens if self._ff_on else 0
+        a.dd_ff_meta = _ptr(t["dd_ff_meta"])
         a.dd_meta = _ptr(t["dd_meta"])
         a.nm_key, a.nm_id, a.nm_first = _ptr(t["nm_key"]), _ptr(t["nm_id"]), _ptr(t["nm_first"])
         a.nm_mask, a.nm_counter = c.name_slots - 1, _ptr(t["nm_counter"])
@@ -1334,20 +1339,40 @@ class GpuInboundEngine(EngineBase):
     _CKPT_TABLES = ("reg", "asg_ctx", "asg_active", "dd_tab", "dd_meta", "seq_base", "nm_key", "nm_id", "nm_first",
                     "nm_counter", "seen_key", "st", "ms", "stats", "cursor")
 
-    def bloom_add(self, hashes):
-        """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
-        h = np.ascontiguousarray(np.asarray(hashes, np.uint64))
-        if not self._bloom_blocks or not len(h):
-            return
-        dev = torch.from_numpy(h.view(np.int64)).to(self.device)
-        rc = self.lib.sw_bloom_add(ctypes.c_void_p(_ptr(self.t["dd_bloom"])), self._bloom_blocks - 1,
-                                   ctypes.c_void_p(_ptr(dev)), len(h), self._stream())
-        if rc:
-            raise RuntimeError(f"sw_bloom_add failed ({rc})")
+    # store-backed filter primitives (EngineBase.filter_seed / filter_state); host-driven, between steps
+    def _ff_meta_get(self) -> np.ndarray:
+        self._sync_streams()
+        return self.t["dd_ff_meta"].cpu().numpy().copy()
+
+    def _ff_meta_set(self, m):
+        self._sync_streams()
+        self.t["dd_ff_meta"].copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(m, np.int64))))
         torch.cuda.current_stream(self.device).synchronize()
 
+    def _ff_add(self, hashes, g: int):
+        h = np.ascontiguousarray(np.asarray(hashes, np.uint64))
+        if not self._ff_on or not len(h):
+            return
+        c = self.cfg
+        dev = torch.from_numpy(h.view(np.int64)).to(self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        rc = self.lib.sw_ff_add(ctypes.c_void_p(_ptr(self.t["dd_ff"])), c.ff_buckets - 1, c.dedup_filter_gens, int(g),
+                                ctypes.c_void_p(_ptr(self.t["dd_ff_meta"])), ctypes.c_void_p(_ptr(dev)), len(h),
+                                self._stream())
+        if rc:
+            raise RuntimeError(f"sw_ff_add failed ({rc})")
+        self._sync_streams()
+
+    def _ff_clear(self, g: int):
+        c = self.cfg
+        rc = self.lib.sw_ff_clear(ctypes.c_void_p(_ptr(self.t["dd_ff"])), c.ff_buckets - 1, c.dedup_filter_gens,
+                                  int(g), self._stream())
+        if rc:
+            raise RuntimeError(f"sw_ff_clear failed ({rc})")
+        self._sync_streams()
+
     def _ckpt_tables(self):
-        return self._CKPT_TABLES + (("dd_bloom",) if self._bloom_blocks else ())
+        return self._CKPT_TABLES + (("dd_ff", "dd_ff_meta") if self._ff_on else ())
 
     def checkpoint_state(self, include_store: bool = False) -> dict:
         if self._pend is not None:

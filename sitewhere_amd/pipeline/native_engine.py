@@ -91,7 +91,9 @@ class NativeCpuEngine(CpuInboundEngine):
         self._h = self._lib.swce_create(self.threads)
         self._lib.swce_reserve(self._h, cfg.state_slots, cfg.dedup_slots)
         self._lib.swce_dedup_window(self._h, cfg.dedup_slots, cfg.rec_cap)
-        self._lib.swce_bloom_init(self._h, cfg.dedup_bloom_bits)
+        if self._lib.swce_ff_init(self._h, cfg.ff_buckets, cfg.dedup_filter_gens if cfg.ff_buckets else 0,
+                                  cfg.dedup_filter_ids) != 0:
+            raise MemoryError("store-backed dedup filter: bad sizing or out of memory")
         for v in self.store.values():      # touch the ring now (the GPU's HBM store is resident too)
             v.fill(0)
         self._out_pool: dict = {}       # recycled outbound buffers per dtype (see _out_buffer)
@@ -114,11 +116,23 @@ class NativeCpuEngine(CpuInboundEngine):
         self._lib.swce_dedup_import(self._h, _ptr(z64), _ptr(zi), 0)
         self._lib.swce_dedup_prev_import(self._h, _ptr(z64), _ptr(zi), 0)
 
-    def bloom_add(self, hashes):
-        """Add alternate-id hashes to the store-backed dedup filter (warm start from the store)."""
+    # store-backed filter primitives (EngineBase.filter_seed / filter_state)
+    def _ff_meta_get(self) -> np.ndarray:
+        m = np.zeros(24, np.int64)
+        self._lib.swce_ff_meta(self._h, _ptr(m), None)
+        return m
+
+    def _ff_meta_set(self, m):
+        m = np.ascontiguousarray(np.asarray(m, np.int64))
+        self._lib.swce_ff_meta(self._h, None, _ptr(m))
+
+    def _ff_add(self, hashes, g: int):
         h = np.ascontiguousarray(np.asarray(hashes, np.uint64))
         if len(h):
-            self._lib.swce_bloom_add(self._h, _ptr(h), len(h))
+            self._lib.swce_ff_add(self._h, int(g), _ptr(h), len(h))
+
+    def _ff_clear(self, g: int):
+        self._lib.swce_ff_clear(self._h, int(g))
 
     # ------------------------------------------------------------------ packed mirrors
     def _dirty_registry(self, slots):
@@ -268,20 +282,22 @@ class NativeCpuEngine(CpuInboundEngine):
             "ms_key": ms[:, :3].copy(), "ms_val": ms[:, 3:].copy(),
             "carry": self.carry.view(np.uint8).reshape(-1).copy(),
         }
-        nw = lib.swce_bloom_words(h, None, 0)
+        nw = lib.swce_ff_words(h, None, 0)
         if nw:
             bw = np.zeros(nw, np.uint64)
-            lib.swce_bloom_words(h, _ptr(bw), nw)
-            st["dd_bloom"] = bw
+            lib.swce_ff_words(h, _ptr(bw), nw)
+            st["dd_ff"] = bw.view(np.uint32)
+            st["dd_ff_meta"] = self._ff_meta_get()
         if include_store:
             st.update({f"store.{k}": v for k, v in self.store.items()})
         return st
 
     def restore_state(self, a: dict, include_store: bool):
         lib, h = self._lib, self._h
-        if "dd_bloom" in a:
-            bw = np.ascontiguousarray(a["dd_bloom"], np.uint64)
-            lib.swce_bloom_load(h, _ptr(bw), len(bw))
+        if "dd_ff" in a and lib.swce_ff_words(h, None, 0):
+            bw = np.ascontiguousarray(a["dd_ff"], np.uint32).view(np.uint64)
+            lib.swce_ff_load(h, _ptr(bw), len(bw))
+            self._ff_meta_set(a["dd_ff_meta"])
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
         self.stats[:] = 0
         self.stats[:len(a["stats"])] = a["stats"]

@@ -46,13 +46,19 @@ class EnrichedBatchReader:
         self._names: dict[int, dict] = {}        # boot -> name id -> name
         self._rules: dict[str, str] = {}
         self._lock = threading.Lock()
-        self._masks: dict = {}                    # (boot, field, value) -> (bool per assignment, entries seen)
+        self._masks: dict = {}                    # (boot, field, value) -> (bool per assignment, dictionary version)
+        self._ver: dict[int, int] = {}            # boot -> version: bumped by every assignment delta applied
         self.rows = self.batches = self.resolved = 0
 
     # ------------------------------------------------------------------ dictionaries
     def _apply(self, boot: int, d: dict):
         with self._lock:
-            self._asg.setdefault(boot, {}).update({int(k): v for k, v in (d.get("asg") or {}).items()})
+            asg = d.get("asg") or {}
+            if asg:
+                # a delta may rewrite known assignments in place (an assignment moved to another
+                # area, a device's type changed): every cached mask of the boot is stale then
+                self._ver[boot] = self._ver.get(boot, 0) + 1
+            self._asg.setdefault(boot, {}).update({int(k): v for k, v in asg.items()})
             self._names.setdefault(boot, {}).update({int(k): v for k, v in (d.get("names") or {}).items()})
             self._rules.update(d.get("rules") or {})
 
@@ -102,20 +108,22 @@ class EnrichedBatchReader:
     def attr_mask(self, cols: dict, pos: int, value) -> np.ndarray:
         """bool per row of ``cols``: does the row's assignment context field ``pos`` (0 assignment,
         1 device, 2 customer, 3 area, 4 asset, 5 device token, 6 device type) equal ``value``?  The
-        per-assignment answer is cached for the batch's engine incarnation and rebuilt only when its
-        dictionary has grown -- a filter costs one gather per batch, not a Python call per row."""
+        per-assignment answer is cached for the batch's engine incarnation and rebuilt only when an
+        assignment delta was applied since (new entries or changed ones) -- a filter costs one gather
+        per batch, not a Python call per row."""
         boot = int(cols["header"]["boot"])
         key = (boot, pos, value)
         with self._lock:
             a = self._asg.get(boot, {})
+            ver = self._ver.get(boot, 0)
             m, seen = self._masks.get(key, (None, -1))
-            if m is None or seen != len(a):
+            if m is None or seen != ver:
                 n = (max(a) + 1) if a else 0
                 m = np.zeros(n, bool)
                 for i, ctx in a.items():
                     if len(ctx) > pos and ctx[pos] == value:
                         m[i] = True
-                self._masks[key] = (m, len(a))
+                self._masks[key] = (m, ver)
         asg = np.asarray(cols["asg"], np.int64)
         ok = (asg >= 0) & (asg < len(m))
         out = np.zeros(len(asg), bool)

@@ -177,6 +177,18 @@ class DeviceEventManagement:
             return b""
         return b"".join(np.ascontiguousarray(c, np.uint64).tobytes() for c in f(int(max_ids), skip=int(skip)))
 
+    def durable_retention(self) -> dict:
+        """Retention limits and holdings of the durable store ({} for other stores)."""
+        f = getattr(self.store, "retention_state", None)
+        return f() if f is not None else {}
+
+    def durable_limit_retention_rows(self, rows: int) -> int:
+        """Bound the durable store to ``rows`` event rows (only ever tightens): an engine tenant's
+        store-backed dedup filter remembers its newest N ids, and the store then holds no id the
+        filter forgot.  Returns the limit in force (0: the store has no such limit)."""
+        f = getattr(self.store, "limit_retention_rows", None)
+        return int(f(int(rows))) if f is not None else 0
+
     def durable_alternate_id_count(self) -> int:
         """Alternate ids the durable store holds (from its block index trailers)."""
         f = getattr(self.store, "alternate_id_count", None)

@@ -296,18 +296,23 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
 
     def _upsert_assignment(self, a):
         with self._lock:
-            ai = self.asg_index.get(a.id)
             di = self.dev_index.get(a.device_id)
-            if int(self.engine.dev_slot[di]) < 0:
-                # the assignment's event came before its device's (the change feed does not order
-                # them): register the device now, or its payloads route as unregistered until the
-                # device event arrives although the assignment is active
-                try:
-                    d = self._dm().get_device(a.device_id)
-                except Exception:       # noqa: BLE001 -- the device event registers it later
-                    d = None
-                if d is not None:
-                    self._upsert_device(d)
+            known = int(self.engine.dev_slot[di]) >= 0
+        d = None
+        if not known:
+            # the assignment's event came before its device's (the change feed does not order them):
+            # register the device now, or its payloads route as unregistered until the device event
+            # arrives although the assignment is active.  Fetched before taking the engine lock (a
+            # slow device-management call must not stall the store path's dictionary deltas).
+            try:
+                d = self._dm().get_device(a.device_id)
+            except Exception as e:      # noqa: BLE001 -- the device event registers it later
+                self.logger.warning("device %s of assignment %s not registered yet (%s): its device event will",
+                                    a.device_id, a.id, e)
+        with self._lock:
+            ai = self.asg_index.get(a.id)
+            if d is not None and int(self.engine.dev_slot[di]) < 0:
+                self._upsert_device(d)
             active = a.status != DeviceAssignmentStatus.Released
             self.engine.set_assignments([ai], [di], customer=[self.customers.get(a.customer_id)],
                                         area=[self.areas.get(a.area_id)], asset=[self.assets.get(a.asset_id)],
@@ -909,23 +914,27 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         em = self._em()
         if not hasattr(em, "durable_source_offset"):
             return
-        # store-backed dedup filter: seeded with the ids already stored, so a device re-sending an old
-        # payload after a restart is still handed to the store check
-        bits = int(getattr(self.engine.cfg, "dedup_bloom_bits", 0) or 0)
-        if bits and hasattr(em, "durable_alternate_hashes"):
-            # seed up to the filter's capacity (not a fixed 2^26), in chunks (no one
-            # 512 MB blob through the API), and count every stored id for the sizing report
-            cap = bits // self.FILTER_BITS_PER_ID
+        # store-backed dedup filter: the store may hold no id the filter has forgotten (retention by
+        # rows, tightened here), and the filter is seeded with the ids already stored, newest first,
+        # so a device re-sending an old payload after a restart is still handed to the store check
+        if self.engine.filter_on:
+            c = self.engine.cfg
+            rows = c.filter_retention_rows(self.filter_retention_slack())
+            if hasattr(em, "durable_limit_retention_rows"):
+                self.filter_retention_rows = em.durable_limit_retention_rows(rows)
+            cap = c.dedup_filter_gens * c.dedup_filter_ids
             count = getattr(em, "durable_alternate_id_count", None)
             self._stored_ids = int(count()) if count is not None else 0
             seeded, skip = 0, 0
-            while seeded < cap:
-                h = np.frombuffer(em.durable_alternate_hashes(min(cap - seeded, 1 << 24), skip=skip), np.uint64)
-                if not len(h):
-                    break
-                self.engine.bloom_add(h)
-                seeded += len(h)
-                skip += len(h)
+            if hasattr(em, "durable_alternate_hashes"):
+                self.engine.filter_seed_begin()
+                while seeded < cap:
+                    h = np.frombuffer(em.durable_alternate_hashes(min(cap - seeded, 1 << 24), skip=skip), np.uint64)
+                    if not len(h):
+                        break
+                    self.engine.filter_seed(h)
+                    seeded += len(h)
+                    skip += len(h)
             self._stored_ids = max(self._stored_ids, seeded)
             if seeded:
                 self.logger.info("dedup filter seeded with %d of %d stored alternate ids", seeded, self._stored_ids)
@@ -1033,56 +1042,70 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     # payloads are at least this many bytes on the raw topic (a delimited protobuf request carrying a
     # device token and one event): the most ids a partition's retention can redeliver
     MIN_PAYLOAD_BYTES = 24
-    # the blocked Bloom filter (8 bits of one 64-bit block per id): false positives ~3e-6 at one id
-    # per 128 bits, ~3e-5 at one per 64, ~4e-3 at one per 16 (the most loaded words set the rate;
-    # each false positive is a store lookup the step's commit waits for)
-    FILTER_BITS_PER_ID = 128
+    # the fewest bytes a durable row takes (columns + index; a step's block runs 14-19 B/row): a
+    # segment file of rotate_bytes holds at most rotate_bytes / 8 rows
+    MIN_ROW_BYTES = 8
+
+    def filter_retention_slack(self) -> int:
+        """Rows the store may hold beyond its row limit: the file being written (whole files are
+        deleted) and the blocks in flight."""
+        em = self._em()
+        st = em.durable_retention() if hasattr(em, "durable_retention") else {}
+        rotate = int(st.get("rotate_bytes", 1 << 30) or (1 << 30))
+        return rotate // self.MIN_ROW_BYTES + 16 * self.engine.cfg.rec_cap
 
     def check_dedup_sizing(self) -> dict:
-        """Runtime check of the engine's dedup sizing (docs/PARITY.md, alternate-id dedup): the HBM
+        """Runtime check of the engine's dedup sizing (docs/PARITY.md, alternate-id dedup).  The HBM
         window always holds the last ``dedup_slots / 2`` ids.  Without the store-backed filter, a raw
         topic that can redeliver more payloads than that (its retention) lets an old id through
-        again; with the filter, stored ids past ``dedup_bloom_bits / 128`` raise its false-positive
-        rate (host lookups, not correctness).  Logs a warning per violated rule; returns the report
+        again.  With it, the filter holds the newest (gens - 1) * ``dedup_filter_ids`` ids and the
+        durable store is bounded to that many rows (``_resume_from_store``): warn when the store's
+        row limit could not be set that low.  Logs a warning per violated rule; returns the report
         (also ``dedup_sizing_report``)."""
         c = self.engine_cfg
         bus = self.ms.instance.bus
         window = int(c.dedup_slots) // 2
-        bits = int(getattr(c, "dedup_bloom_bits", 0) or 0)
+        ids = int(getattr(c, "dedup_filter_ids", 0) or 0)
         redeliver = 0
         for t in self.raw_consumer.topics:
             r = bus.retention(t) if hasattr(bus, "retention") else 0
             parts = bus.partitions(t) if hasattr(bus, "partitions") else 1
             redeliver = -1 if (r <= 0 or redeliver < 0) else redeliver + parts * (r // self.MIN_PAYLOAD_BYTES)
         stored = int(getattr(self, "_stored_ids", 0))
-        rep = {"window_ids": window, "filter_bits": bits, "filter_capacity_ids": bits // self.FILTER_BITS_PER_ID,
+        held = (c.dedup_filter_gens - 1) * ids if ids else 0
+        limit = int(getattr(self, "filter_retention_rows", 0) or 0)
+        rep = {"window_ids": window, "filter_ids_per_gen": ids, "filter_gens": c.dedup_filter_gens if ids else 0,
+               "filter_holds_ids": held, "filter_bytes": c.filter_bytes(),
+               "store_retention_rows": limit or None,
                "raw_redeliverable_ids": None if redeliver < 0 else redeliver, "stored_ids": stored,
                "warnings": []}
-        if not bits and (redeliver < 0 or redeliver > window):
+        if not ids and (redeliver < 0 or redeliver > window):
             rep["warnings"].append(
                 f"dedup window holds {window} ids but the raw topic can redeliver "
                 f"{'unbounded' if redeliver < 0 else redeliver} payloads and no store-backed filter is "
                 f"configured: raise capacity.dedup_slots to >= {2 * max(redeliver, 0) or 'twice the retention'} "
-                f"or set capacity.dedup_bloom_bits")
-        if bits and stored > rep["filter_capacity_ids"]:
+                f"or set capacity.dedup_filter_ids")
+        if ids and self.storage == "durable" and (not limit or limit > held):
             rep["warnings"].append(
-                f"dedup filter of {bits} bits already holds {stored} stored ids (> {rep['filter_capacity_ids']}): "
-                f"false positives rise; size capacity.dedup_bloom_bits to >= {self.FILTER_BITS_PER_ID * stored}")
+                f"the durable store keeps {limit or 'unbounded'} rows but the dedup filter holds only the newest "
+                f"{held} ids: replays of older stored ids are not caught")
         for w in rep["warnings"]:
             self.logger.warning("%s", w)
         self.dedup_sizing_report = rep
         return rep
 
     def _watch_filter(self, n_payloads: int, false_pos: int):
-        """Filter false positives measured in flight: above 1% of the engine's payloads over a
-        window of 2^22, warn (the filter is saturated -- size ``dedup_bloom_bits`` to the ids kept)."""
+        """Filter false positives measured in flight: above 1e-4 of the engine's payloads over a
+        window of 2^22, warn (each is a store lookup the step's commit waits for; the generational
+        fingerprint filter's rate is ~1e-8 at its sizing load, so this means a probe-bound overflow
+        or a mis-sized filter)."""
         w = self._fp_win
         w[0] += false_pos
         w[1] += n_payloads
         if w[1] >= 1 << 22:
-            if w[0] > 0.01 * w[1]:
-                self.logger.warning("dedup filter false positives at %.2f%% of payloads: saturated, raise "
-                                    "capacity.dedup_bloom_bits", 100.0 * w[0] / w[1])
+            if w[0] > 1e-4 * w[1]:
+                self.logger.warning("dedup filter false positives at %.4f%% of payloads (filter %s)",
+                                    100.0 * w[0] / w[1], self.engine.filter_state())
                 self.dedup_sizing_report.setdefault("warnings", []).append(
                     f"filter false positives {w[0]}/{w[1]}")
             w[0] = w[1] = 0

@@ -113,13 +113,12 @@ TENANT_TEMPLATES["gpu-columnar"]["services"]["inbound-processing"].update(
               # alternate-id window: 2^24 slots (512 MB of HBM) hold the last 6-8M ids, so a recheck
               # never scans the blocks the store has not indexed yet
               "dedup_slots": 1 << 24, "gen_cap": 32768,
-              # store-backed dedup beyond the window: 2^34 bits (2 GB of the 288 GB of HBM), 8 bits
-              # per id in one 64-bit block (one atomic per add).  Each false positive is a store
-              # lookup on the host that the step's commit waits for, and a one-word filter's rate
-              # is set by its most loaded words: ~3e-6 at 128 bits per id (~134M stored ids here),
-              # ~5e-5 at 55 (2^32 bits at 78M ids measured ~1.3e-5: a recheck every batch, the
-              # tenant path at a tenth of its rate).  check_dedup_sizing warns past 128 bits per id.
-              "dedup_bloom_bits": 1 << 34})
+              # store-backed dedup beyond the window (pipeline/dedup_filter.py): 4 generations of
+              # ~2^28 ids (8 GB of the 288 GB of HBM), so the filter holds the newest ~805M ids and
+              # forgets older ones; the durable store is bounded to rows the filter still holds
+              # (retention by rows, set by the engine at start: ~660M rows, ~12 GB of segments) --
+              # every stored id stays checked, false positives ~1e-8, and no cliff as ids accrue.
+              "dedup_filter_ids": (1 << 28) - (1 << 21), "dedup_filter_gens": 4})
 TENANT_TEMPLATES["gpu-columnar"]["services"]["event-management"] = {
     "datastore": {"type": "segments", "path": "${sitewhere.data.dir:/tmp/sitewhere/data}/[[tenant.token]]/events",
                   "retentionBytes": "${sitewhere.events.retention.bytes:0}"}}
@@ -132,7 +131,7 @@ TENANT_TEMPLATES["gpu-columnar-1m"] = copy.deepcopy(TENANT_TEMPLATES["gpu-column
 TENANT_TEMPLATES["gpu-columnar-1m"]["name"] = "MI355X pipeline, columnar event store, 1M devices"
 TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["inbound-processing"]["capacity"].update(
     max_msgs=1 << 20, max_devices=(1 << 20) + 65536, max_assignments=(1 << 20) + 65536, store_cap=1 << 23,
-    gen_cap=1 << 19, state_slots=1 << 24, dedup_bloom_bits=1 << 36)
+    gen_cap=1 << 19, state_slots=1 << 24, dedup_filter_ids=(1 << 29) - (1 << 22))
 TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["event-sources"].update(rawBatchSize=1 << 20)
 # volatile variant (benchmarks of the pipeline alone): rows kept in host memory, newest 2^28 held
 TENANT_TEMPLATES["gpu-memory"] = copy.deepcopy(TENANT_TEMPLATES["gpu-columnar"])

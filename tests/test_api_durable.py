@@ -17,6 +17,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -228,5 +230,70 @@ def test_api_restart_is_bounded_by_the_tail(tmp_path, monkeypatch):
         assert st.count() == total
         assert rss[1] - rss[0] < 400 * 1024, rss                 # KiB: growth over the last 790K events
         assert reopen < 5.0, reopen
+    finally:
+        st.close()
+
+
+def test_oversized_api_add_is_refused_before_the_log(tmp_path, monkeypatch):
+    """an event whose metadata, alternate id or alert message does not fit a block
+    row (u16 string spans) is refused by the add -- it never reaches the write-ahead log, so the tail
+    keeps flushing into blocks; nothing is silently truncated (a cut alternate id would break its
+    dedup); a flush failure is visible in ``retention_state``."""
+    monkeypatch.setenv("SW_API_FLUSH_S", "3600")
+    from sitewhere_amd.core.errors import SiteWhereSystemException
+    from sitewhere_amd.models.domain import DeviceAlert, DeviceMeasurement
+    from sitewhere_amd.persistence.segments import DurableEventStore
+    d = str(tmp_path / "s")
+    st = DurableEventStore(d, direct=False)
+    try:
+        ctx = dict(device_assignment_id="asg-1", device_id="dev-1", customer_id="c", area_id="a", asset_id="x",
+                   event_date=1_000_000)
+        bad = [DeviceMeasurement(name="t", value=1.0, metadata={"k": "v" * 70_000}, **ctx),
+               DeviceMeasurement(name="t", value=1.0, alternate_id="a" * 70_000, **ctx),
+               DeviceAlert(type="door", message="m" * 70_000, **ctx)]
+        for e in bad:
+            with pytest.raises(SiteWhereSystemException):
+                st.add_events([e])
+        ok = DeviceMeasurement(name="t", value=2.0, alternate_id="fine-1", metadata={"k": "v"}, **ctx)
+        st.add_events([ok])
+        assert len(st._api_tail) == 1
+        assert st.flush_api() == 1 and not st._api_tail
+        assert st.retention_state()["api_flush_error"] is None
+        assert st.get_event_by_alternate_id("fine-1").id == ok.id
+        assert os.path.getsize(os.path.join(d, "api-0.log")) == 0
+    finally:
+        st.close()
+
+
+def test_alternate_hash_chunks_skip_over_mixed_block_sizes(tmp_path, monkeypatch):
+    """seeding the dedup filter pages through the store's ids with ``skip``.
+    Over blocks of mixed sizes, the concatenated pages equal the unpaged sequence for every page size
+    (whole blocks are skipped by count only before the first block kept)."""
+    import numpy as np
+    monkeypatch.setenv("SW_API_FLUSH_S", "3600")
+    from sitewhere_amd.models.domain import DeviceMeasurement
+    from sitewhere_amd.persistence.segments import DurableEventStore
+    st = DurableEventStore(str(tmp_path / "s"), direct=False)
+    try:
+        k = 0
+        for n in (20, 5, 13, 40, 1, 9):
+            evs = [DeviceMeasurement(name="t", value=float(i), alternate_id=f"alt-{k + i}", device_assignment_id="a",
+                                     device_id="d", event_date=1_000_000 + k + i) for i in range(n)]
+            k += n
+            st.add_events(evs)
+            assert st.flush_api() == n
+        full = np.concatenate(list(st.alternate_hash_chunks(1 << 20)))
+        assert len(full) == k == len(set(full.tolist()))
+        for page in (1, 3, 7, 10, 21, 50):
+            got, skip = [], 0
+            while True:
+                part = list(st.alternate_hash_chunks(page, skip=skip))
+                h = np.concatenate(part) if part else np.zeros(0, np.uint64)
+                if not len(h):
+                    break
+                assert len(h) <= page
+                got.append(h)
+                skip += len(h)
+            assert np.array_equal(np.concatenate(got), full), page
     finally:
         st.close()

@@ -1,7 +1,7 @@
 """Runtime dedup sizing check: an engine tenant warns when its HBM dedup window is
-smaller than what the raw topic can redeliver and no store-backed filter is configured, when the
-filter already holds more stored ids than it is sized for, and when in-flight false positives pass
-1% of the payloads."""
+smaller than what the raw topic can redeliver and no store-backed filter is configured, when its
+durable store may keep more rows than the generational filter holds ids (retention by
+rows must bound the store), and when in-flight false positives pass 1e-4 of the payloads."""
 from __future__ import annotations
 
 import logging
@@ -22,10 +22,11 @@ class _Bus:
         return self._p
 
 
-def _tenant(cfg, retention, stored=0):
+def _tenant(cfg, retention, stored=0, limit=0):
     return SimpleNamespace(engine_cfg=cfg, ms=SimpleNamespace(instance=SimpleNamespace(bus=_Bus(retention))),
                            raw_consumer=SimpleNamespace(topics=["t1.raw"]), logger=logging.getLogger("sizing"),
-                           MIN_PAYLOAD_BYTES=T.MIN_PAYLOAD_BYTES, FILTER_BITS_PER_ID=T.FILTER_BITS_PER_ID,
+                           MIN_PAYLOAD_BYTES=T.MIN_PAYLOAD_BYTES, storage="durable", filter_retention_rows=limit,
+                           engine=SimpleNamespace(filter_state=lambda: {}),
                            _stored_ids=stored, dedup_sizing_report={}, _fp_win=[0, 0])
 
 
@@ -43,18 +44,26 @@ def test_window_smaller_than_redelivery_warns_without_filter(caplog):
     assert small["warnings"] == []
 
 
-def test_filter_covers_the_window_until_it_saturates():
-    cfg = EngineConfig.small(dedup_slots=1 << 16, dedup_bloom_bits=1 << 20)
-    assert T.check_dedup_sizing(_tenant(cfg, retention=0, stored=1000))["warnings"] == []
-    rep = T.check_dedup_sizing(_tenant(cfg, retention=0, stored=(1 << 20) // T.FILTER_BITS_PER_ID + 1))
-    assert len(rep["warnings"]) == 1 and "dedup_bloom_bits" in rep["warnings"][0]
+def test_store_rows_bounded_by_what_the_filter_holds():
+    cfg = EngineConfig.small(dedup_slots=1 << 16, dedup_filter_ids=1 << 20, dedup_filter_gens=4)
+    held = 3 * (1 << 20)
+    assert cfg.filter_retention_rows(0) == held
+    assert cfg.filter_retention_rows(1 << 20) == held - (1 << 20)
+    rep = T.check_dedup_sizing(_tenant(cfg, retention=0, limit=cfg.filter_retention_rows(1 << 20)))
+    assert rep["warnings"] == [] and rep["filter_holds_ids"] == held
+    # the store's row limit could not be set (or is above what the filter holds): replays of older
+    # stored ids would pass
+    rep = T.check_dedup_sizing(_tenant(cfg, retention=0, limit=0))
+    assert len(rep["warnings"]) == 1 and "not caught" in rep["warnings"][0]
+    rep = T.check_dedup_sizing(_tenant(cfg, retention=0, limit=held + 1))
+    assert len(rep["warnings"]) == 1
 
 
 def test_false_positive_watch(caplog):
-    t = _tenant(EngineConfig.small(dedup_bloom_bits=1 << 20), retention=0)
+    t = _tenant(EngineConfig.small(dedup_filter_ids=1 << 16), retention=0)
     with caplog.at_level(logging.WARNING, "sizing"):
         T._watch_filter(t, 1 << 21, 100)
         T._watch_filter(t, 1 << 21, 100)           # 0.005%: quiet
         assert not caplog.records and t._fp_win == [0, 0]
-        T._watch_filter(t, 1 << 22, 1 << 16)       # 1.6%: saturated
+        T._watch_filter(t, 1 << 22, 1 << 16)       # 1.6%: a mis-sized filter
     assert any("false positives" in r.message for r in caplog.records)

@@ -209,3 +209,20 @@ def test_engine_tenant_events_reach_connectors_and_rules_like_per_event(sw):
     # the engine's consumers resolved their dictionaries from the batches themselves
     eng_reader = sw.tenant_engine("outbound-connectors", "eng").readers[0]
     assert eng_reader.batches > 0 and eng_reader.rows >= 300
+
+
+def test_connector_masks_follow_assignment_updates():
+    """an assignment delta that rewrites a known assignment in place (moved to
+    another area) invalidates the cached per-assignment filter masks, so column filters and the
+    per-event context agree after the move."""
+    import numpy as np
+
+    from sitewhere_amd.services.enriched_batches import EnrichedBatchReader
+    r = EnrichedBatchReader(engine=None)
+    boot = 7
+    r._apply(boot, {"asg": {0: ["a0", "d0", "c", "area-1", "x"], 1: ["a1", "d1", "c", "area-2", "x"]}})
+    cols = {"header": {"boot": boot}, "asg": np.array([0, 1, 1, 0])}
+    assert r.attr_mask(cols, 3, "area-1").tolist() == [True, False, False, True]
+    r._apply(boot, {"asg": {1: ["a1", "d1", "c", "area-1", "x"]}})          # same size, area changed
+    assert r.attr_mask(cols, 3, "area-1").tolist() == [True, True, True, True]
+    assert r.attr_mask(cols, 3, "area-2").tolist() == [False, False, False, False]

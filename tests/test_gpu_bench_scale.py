@@ -1,12 +1,14 @@
 """Bench-scale parity: the MI355X engine against the native CPU engine (bit-exact
 with the Python oracle) in the configuration bench.py runs -- 1M-payload steps over a 1M-device fleet
 with alternate ids, metadata and control messages, a 2^22-slot dedup window that rotates several
-times, the store-backed alternate-id filter at bench.py's 2^33 bits, an HBM event ring that wraps
+times, the store-backed alternate-id filter (generational fingerprint tables), an HBM event ring that wraps
 every two steps, and replays inside and beyond the window.  Every step: same stats, same persisted
 rows (device events in order, generated rows as a multiset), same reject statuses, the same durable
 block contents and the same block index trailer (built on the GPU in the step vs by the C++
 builder on the CPU engine's block).  The replay beyond the window comes back as rechecks (the
-filter remembers the ids), not as accepted events."""
+filter remembers the ids), not as accepted events.  A second run rotates the filter itself past
+everything it holds: replays it still holds are rechecked, older ones are new again,
+and the two engines agree on every step and on the filter's state."""
 from __future__ import annotations
 
 import numpy as np
@@ -20,11 +22,14 @@ N_MSGS = 1 << 20
 N_DEV = 1 << 20
 
 
-def _cfg():
+def _cfg(**kw):
     from sitewhere_amd.pipeline.config import EngineConfig
-    return EngineConfig(max_msgs=N_MSGS, rec_cap=N_MSGS + 4096, gen_cap=N_MSGS // 2, max_devices=N_DEV + 1024,
-                        max_assignments=N_DEV + 1024, store_cap=1 << 21, dedup_slots=1 << 22, name_slots=1 << 12,
-                        state_slots=1 << 23, presence_missing_ms=8 * 3600 * 1000, dedup_bloom_bits=1 << 33)
+    base = dict(max_msgs=N_MSGS, rec_cap=N_MSGS + 4096, gen_cap=N_MSGS // 2, max_devices=N_DEV + 1024,
+                max_assignments=N_DEV + 1024, store_cap=1 << 21, dedup_slots=1 << 22, name_slots=1 << 12,
+                state_slots=1 << 23, presence_missing_ms=8 * 3600 * 1000, dedup_filter_ids=1 << 26,
+                dedup_filter_gens=4)
+    base.update(kw)
+    return EngineConfig(**base)
 
 
 def _setup(engine):
@@ -118,3 +123,45 @@ def test_gpu_matches_native_cpu_engine_at_bench_scale():
     assert dups[10] == 0
     assert rechecks[10] > 0.99 * N_MSGS * (1 - spec.p_unregistered - 0.001)
     assert sum(rechecks[:6]) + sum(rechecks[7:10]) < 1000                    # the filter's false positives
+
+
+def test_gpu_filter_rotates_past_retention_at_bench_scale():
+    """2 generations of 2^22 ids: the filter holds the newest 4-9 batches' ids.  Replays 3 batches back
+    (past the window, held) are all rechecks; replays 14 back (past every generation: what a store
+    bounded by rows no longer holds) are new again.  GPU and native engine agree step by step."""
+    from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads
+    from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
+    from sitewhere_amd.pipeline.native_engine import NativeCpuEngine
+    kw = dict(dedup_filter_ids=1 << 22, dedup_filter_gens=2, state_slots=1 << 25)   # 16 steps of (asg, name) keys
+    g = GpuInboundEngine(_cfg(**kw), device="cuda:0")
+    c = NativeCpuEngine(_cfg(**kw), threads=16)
+    for e in (g, c):
+        _setup(e)
+    spec = FleetSpec(prefix="dev-", n_devices=N_DEV, p_location=0.25, p_alert=0.05, p_unregistered=0.005,
+                     mx_per_msg=1, n_names=16, with_alternate_id=True, lat0=33.0, lon0=-85.0, span_deg=2.0,
+                     p_register=0.0005, p_ack=0.0005, p_meta=0.1)
+    now = 1_700_000_200_000
+    seeds = list(range(101, 115)) + [111, 101]
+    batches, rechecks, dups, persisted = {}, [], [], []
+    for k, seed in enumerate(seeds):
+        if seed not in batches:
+            raw, offs = gen_payloads(spec, N_MSGS, now - 60_000, seed=seed)
+            batches[seed] = (np.concatenate([raw, np.zeros(64, np.uint8)]), offs)
+        raw, offs = batches[seed]
+        s0 = g.stats_dict()
+        rg = g.step(raw, offs, now + k, presence=False)
+        rc = c.step(raw, offs, now + k, presence=False)
+        assert g.stats_dict() == c.stats_dict(), f"step {k}"
+        assert g.filter_state() == c.filter_state(), f"step {k}"
+        assert rg.n_persisted == rc.n_persisted
+        s1 = g.stats_dict()
+        rechecks.append(s1["dedup_rechecks"] - s0["dedup_rechecks"])
+        dups.append(s1["duplicates"] - s0["duplicates"])
+        persisted.append(rg.n_persisted)
+    fs = g.filter_state()
+    assert fs["rotations"] >= 2 and fs["dropped"] == 0
+    valid = 0.99 * N_MSGS * (1 - spec.p_unregistered - 0.001)
+    assert dups[14] == 0 and rechecks[14] > valid                       # held by the filter
+    assert dups[15] == 0 and rechecks[15] == 0                           # forgotten: new again
+    assert persisted[15] > valid
+    assert sum(rechecks[:14]) == 0                                       # no false positive

@@ -508,7 +508,7 @@ def test_gloo_skewed_strings_are_lossless():
     assert got == want
 
 
-def _gloo_dedup_worker(rank, world, port, q, bloom_bits):
+def _gloo_dedup_worker(rank, world, port, q, seed_fp):
     import torch
     import torch.distributed as dist
     from sitewhere_amd.persistence.segments import decode_block, row_strings
@@ -518,8 +518,16 @@ def _gloo_dedup_worker(rank, world, port, q, bloom_bits):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     # a window of a few batches (it rotates twice before the replay), the store-backed filter on
     e = CpuInboundEngine(EngineConfig.small(world=world, rank=rank, max_msgs=800, dedup_slots=1 << 12,
-                                            dedup_bloom_bits=bloom_bits))
+                                            dedup_filter_ids=1 << 12, dedup_filter_gens=4))
     shard_fleet(e, world, rank)
+    if seed_fp:
+        # false positives on demand: the owner's filter already holds every id it will be sent (ids
+        # never stored -- what a fingerprint collision is, ~1e-8 of ids in a real run)
+        from sitewhere_amd.pipeline.fleet import hash64
+        src = (rank - 1) % world
+        e.filter_seed_begin()
+        e.filter_seed(np.array([hash64(f"lossless-{src}-{k:04d}-{i:05d}-".ljust(60, "x"))
+                                for k in range(6) for i in range(800)], np.uint64))
     fresh = [_skewed_string_batch(world, rank, k) for k in range(6)]
     batches = fresh + [fresh[0]]              # the first batch again, long after the window forgot it
     empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))
@@ -551,7 +559,7 @@ def _gloo_dedup_worker(rank, world, port, q, bloom_bits):
     dist.destroy_process_group()
 
 
-def _run_gloo_dedup(bloom_bits):
+def _run_gloo_dedup(seed_fp):
     import multiprocessing as mp
     import socket
     s = socket.socket()
@@ -560,7 +568,7 @@ def _run_gloo_dedup(bloom_bits):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gloo_dedup_worker, args=(r, 2, port, q, bloom_bits)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_dedup_worker, args=(r, 2, port, q, seed_fp)) for r in range(2)]
     for p in procs:
         p.start()
     outs = sorted((q.get(timeout=300) for _ in range(2)), key=lambda o: o[0])
@@ -583,17 +591,17 @@ def test_gloo_replay_beyond_window_is_caught_on_the_owner():
     send it again: the owner's store-backed filter flags every replayed id (records decoded on
     another rank go through it too, their strings came along), the owner settles them by alternate
     id against its store, and all 1,600 are duplicates -- 800 caught on each rank."""
-    outs = _run_gloo_dedup(1 << 20)
+    outs = _run_gloo_dedup(False)
     for rank, store, settled, rotations, dups, overflow in outs:
         assert rotations >= 2 and overflow == 0, (rank, rotations, overflow)
         assert settled["duplicates"] == 800, (rank, settled)
 
 
 def test_gloo_filter_false_positives_are_settled_and_stored_once():
-    """A filter far too small for the ids (8 blocks: nearly every id is a false positive): the
+    """Every fresh id a false positive (the owners' filters seeded with ids never stored): the
     owners settle each recheck by alternate id; the ids the store does not hold go back into the
     re-key carry, filter-settled, and are stored exactly once with their strings; the replay is
     still caught."""
-    outs = _run_gloo_dedup(1 << 9)
+    outs = _run_gloo_dedup(True)
     for rank, store, settled, rotations, dups, overflow in outs:
         assert settled["injected"] > 1000 and settled["duplicates"] == 800, (rank, settled)

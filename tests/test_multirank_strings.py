@@ -199,17 +199,22 @@ def _gpu_round(g, bs):
 def test_gpu_rechecks_are_settled_by_alternate_id_on_the_owner():
     """Several ranks, store-backed dedup: the owner's filter sees records decoded on
     another rank too (their strings came along), and the owner settles each recheck by its
-    alternate id (``pipeline/recheck.py``).  A filter far too small (8 blocks) makes nearly every
-    fresh id a false positive: those are re-injected into the re-key carry, filter-settled, and
-    stored exactly once with their strings.  A replay after the window is reset is caught: every
-    replayed id comes back as a recheck the store holds, a duplicate."""
+    alternate id (``pipeline/recheck.py``).  Filters seeded with every fresh id (ids never stored:
+    false positives on demand) make each fresh id a recheck: those are re-injected into the re-key
+    carry, filter-settled, and stored exactly once with their strings.  A replay after the window is
+    reset is caught: every replayed id comes back as a recheck the store holds, a duplicate."""
     from sitewhere_amd.pipeline.config import EngineConfig
+    from sitewhere_amd.pipeline.fleet import cpu_decode
     from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
     from sitewhere_amd.pipeline.recheck import settle_rechecks
-    g = [GpuInboundEngine(EngineConfig.small(world=W, rank=r, dedup_bloom_bits=1 << 9), device="cuda:0")
+    g = [GpuInboundEngine(EngineConfig.small(world=W, rank=r, dedup_filter_ids=1 << 15), device="cuda:0")
          for r in range(W)]
+    fresh = np.concatenate([cpu_decode(raw, offs, NOW)["alt_hash"] for seed in (900, 950)
+                            for raw, offs in _batches(seed)])
     for r, e in enumerate(g):
         _register(e, W, r)
+        e.filter_seed_begin()
+        e.filter_seed(fresh[fresh != 0])
     stores = [dict() for _ in range(W)]
     totals = {"rechecks": 0, "duplicates": 0, "injected": 0}
     empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))

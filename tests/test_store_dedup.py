@@ -58,7 +58,7 @@ def _measurements(sw, alt_prefix):
 
 def test_replay_beyond_the_window_is_a_duplicate(sw):
     ib = sw.tenant_engine("inbound-processing", "sd")
-    assert ib.engine.cfg.dedup_bloom_bits > 0
+    assert ib.engine.cfg.dedup_filter_ids > 0
     es = sw.tenant_engine("event-sources", "sd")
     dev = sw.instance.system_user.run(lambda: sw.api("DeviceManagement", "sd").get_device_by_token("galaxytab-002"),
                                       "sd")
@@ -84,10 +84,12 @@ def test_replay_beyond_the_window_is_a_duplicate(sw):
     # the store lookup found its hash (a replay); the per-event path compared the id strings and
     # dropped it (a hash match alone never drops an event)
     assert wait_until(lambda: ib.recheck_duplicates >= 1, 10)
-    # a filter false positive (an id never stored but whose bits are set) is stored by the host path
+    # a filter false positive (an id never stored whose fingerprint the filter holds) is stored by
+    # the host path
     from sitewhere_amd.pipeline.fleet import hash64
     import numpy as np
-    ib.engine.bloom_add(np.array([hash64("sd-fp-1")], np.uint64))
+    ib.engine.filter_seed_begin()
+    ib.engine.filter_seed(np.array([hash64("sd-fp-1")], np.uint64))
     s1 = ib.engine.stats_dict()
     es.inject("default-protobuf", wire.measurements("galaxytab-002", {"sd.temp": 3.5}, event_date=1_700_000_002_000,
                                                     alternate_id="sd-fp-1"))
