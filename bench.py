@@ -344,9 +344,9 @@ def main():
 
         if args.durable:
             tmpdir, store, boot = open_durable(args, rank, dev)
-            # the store keeps no row whose id the filter has forgotten: the file being written (whole
-            # files are deleted, 1 GiB / >= 8 B per row) and the blocks in flight are the slack
-            store.limit_retention_rows(cfg.filter_retention_rows((1 << 30) // 8 + 16 * cfg.rec_cap))
+            # the store keeps no row whose id the filter has forgotten (the blocks in flight are the
+            # slack; EngineConfig.filter_retention_rows accounts for the file being written)
+            store.limit_retention_rows(cfg.filter_retention_rows(16 * cfg.rec_cap))
             sink = DurableBlockSink(store, eng.lib, boot, rank=rank, world=world, bus=bus, topic=t_out)
             bus.set_retention(t_out, 64 << 20)
             dur = {"store": store, "sink": sink}
@@ -453,9 +453,9 @@ def main():
     else:
         if args.durable:        # host engines encode the same blocks on the CPU (swseg_encode)
             tmpdir, store, boot = open_durable(args, rank, dev)
-            # the store keeps no row whose id the filter has forgotten: the file being written (whole
-            # files are deleted, 1 GiB / >= 8 B per row) and the blocks in flight are the slack
-            store.limit_retention_rows(cfg.filter_retention_rows((1 << 30) // 8 + 16 * cfg.rec_cap))
+            # the store keeps no row whose id the filter has forgotten (the blocks in flight are the
+            # slack; EngineConfig.filter_retention_rows accounts for the file being written)
+            store.limit_retention_rows(cfg.filter_retention_rows(16 * cfg.rec_cap))
             dur = {"store": store, "sink": _HostSink(store)}
 
         def run(k):

@@ -914,17 +914,40 @@ void swce_ff_meta(void* p, int64_t* out, const int64_t* in) {
   if (in) memcpy(e->ff_meta, in, sizeof(e->ff_meta));
 }
 
-// The filter's table as 64-bit words (checkpoints).
-int64_t swce_ff_words(void* p, uint64_t* out, int64_t cap) {
+// Checkpoints keep the filter sparse: the non-empty 64-byte buckets (index into [buckets * gens]
+// and their 16 fingerprints).  A multi-GB filter of a small tenant is a few KB.  Returns the count
+// of non-empty buckets; writes them only when cap >= count.
+int64_t swce_ff_export(void* p, int64_t* idx, uint32_t* rows, int64_t cap) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  const int64_t n = (int64_t)e->ff.size();
-  if (out && cap >= n) memcpy(out, e->ff.data(), (size_t)n * 8);
-  return n;
+  if (e->ff.empty()) return 0;
+  const int64_t nb = (e->ff_bmask + 1) * e->ff_gens;
+  const uint64_t* w = e->ff.data();
+  int64_t k = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    uint64_t any = 0;
+    for (int j = 0; j < SW_FF_SLOTS / 2; ++j) any |= w[b * (SW_FF_SLOTS / 2) + j];
+    if (!any) continue;
+    if (idx && k < cap) {
+      idx[k] = b;
+      memcpy(rows + k * SW_FF_SLOTS, w + b * (SW_FF_SLOTS / 2), SW_FF_SLOTS * sizeof(uint32_t));
+    }
+    ++k;
+  }
+  return k;
 }
 
-void swce_ff_load(void* p, const uint64_t* w, int64_t n) {
+// Replace the table by the sparse buckets (everything else empty).
+int32_t swce_ff_import(void* p, const int64_t* idx, const uint32_t* rows, int64_t n) {
   SwCpuEngine* e = static_cast<SwCpuEngine*>(p);
-  if ((int64_t)e->ff.size() == n) memcpy(e->ff.data(), w, (size_t)n * 8);
+  if (e->ff.empty()) return n ? -1 : 0;
+  const int64_t nb = (e->ff_bmask + 1) * e->ff_gens;
+  for (int g = 0; g < e->ff_gens; ++g) ff_clear(e, g);
+  uint32_t* t = e->ff_tab();
+  for (int64_t k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= nb) return -2;
+    memcpy(t + idx[k] * SW_FF_SLOTS, rows + k * SW_FF_SLOTS, SW_FF_SLOTS * sizeof(uint32_t));
+  }
+  return 0;
 }
 
 // Window sizing of the generational dedup (slots per generation, largest batch in records).

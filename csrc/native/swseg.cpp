@@ -1774,6 +1774,10 @@ static void seg_writer(SegStore* s) {
       if (last > s->durable) s->durable = last;
     }
     s->cv_done.notify_all();
+    // retention after every group commit, not only when a file starts: with retention by rows the
+    // store then holds at most the limit plus the file being written (its rotate size is kept small
+    // against the limit, swss_set_retention)
+    seg_retention(s);
   }
 }
 
@@ -1975,14 +1979,15 @@ void swss_stats(void* h, int64_t* out) {
   out[15] = s->retention_bytes;
 }
 
-// Retention limits (<= 0: unchanged; rows 0 is set with -1: none).  Applied when the next file
-// starts, like the store's own (whole files, oldest first).
-void swss_set_retention(void* h, int64_t bytes, int64_t rows) {
+// Retention limits (<= 0: unchanged; rows -1: none) and the size at which a new file starts (<= 0:
+// unchanged; from the next file on).  Applied after the next group commit (whole files, oldest first).
+void swss_set_retention(void* h, int64_t bytes, int64_t rows, int64_t rotate_bytes) {
   SegStore* s = (SegStore*)h;
   std::lock_guard<std::mutex> g(s->mu);
   if (bytes > 0) s->retention_bytes = bytes;
   if (rows > 0) s->retention_rows = rows;
   if (rows < 0) s->retention_rows = 0;
+  if (rotate_bytes > 0) s->rotate_bytes = rotate_bytes;
 }
 
 void swss_close(void* h) {

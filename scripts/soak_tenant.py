@@ -1,0 +1,261 @@
+"""Steady-state soak of an engine tenant through the bus.
+
+A ``gpu-columnar-1m`` tenant of a whole co-located instance (1M devices and assignments, bulk
+imported through device management) ingests for several phases of ``--phase-s`` seconds: a producer
+publishes 1M-payload raw records (the event-sources record format, zero-copy pinned) to the tenant's
+raw topic as fast as the tenant commits them, every record with FRESH alternate ids (a new id epoch
+stamped in place natively, only into buffers whose records the tenant has committed) and 0.5% of
+payloads from unregistered devices.  The tenant runs its real path: raw consumer -> MI355X engine
+(decode, validation, window + store-backed dedup, persist, state, zones, block encode + index) ->
+durable segment store (O_DIRECT, fdatasync before the raw offset commits), retention by rows bounded
+to what the generational dedup filter holds.
+
+Reported (one JSON line, plus a progress line every ~5 s): per phase events/s, the first and last
+minute, submit-interval percentiles, dedup rechecks per payload, the filter's rotations against its
+capacity, the store's retained / deleted rows (retention wraps), and a replay check at the end: a
+sub-batch of a record published seconds before (still retained) is published again with the same
+ids -- every valid event must come back a duplicate (filter recheck, settled against the store) and
+the store must not grow.
+
+    python scripts/soak_tenant.py --devices 1048576 --phases 3 --phase-s 70
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--devices", type=int, default=1 << 20)
+    ap.add_argument("--template", default="gpu-columnar-1m")
+    ap.add_argument("--batch", type=int, default=1 << 20, help="payloads per raw record")
+    ap.add_argument("--records", type=int, default=8, help="pinned raw records the producer cycles through")
+    ap.add_argument("--ahead", type=int, default=4, help="records published ahead of the tenant's commits")
+    ap.add_argument("--phases", type=int, default=3)
+    ap.add_argument("--phase-s", type=float, default=70.0)
+    ap.add_argument("--p-unregistered", type=float, default=0.005)
+    ap.add_argument("--filter-ids", type=int, default=0, help="dedup filter ids per generation (0: template)")
+    ap.add_argument("--replay", type=int, default=4096, help="payloads of the replayed sub-batch")
+    ap.add_argument("--chunk", type=int, default=65536, help="devices per bulk import call")
+    args = ap.parse_args()
+    import logging
+    logging.basicConfig(level=logging.ERROR)
+    import numpy as np
+    if not os.environ.get("SITEWHERE_DATA_DIR"):
+        import tempfile
+        os.environ["SITEWHERE_DATA_DIR"] = tempfile.mkdtemp(prefix="sw-soak-")
+    data_dir = os.environ["SITEWHERE_DATA_DIR"]
+    log("data dir", data_dir, "free GB", round(shutil.disk_usage(data_dir).free / 2 ** 30, 1))
+    os.environ.setdefault("SW_TENANT_TRACE", "1")
+    import torch
+    from sitewhere_amd.assembly import SiteWhereInstance
+    from sitewhere_amd.pipeline.bus_io import VALUE_HDR, RawBatchRecord
+    from sitewhere_amd.pipeline.fleet import FleetSpec, alt_positions, gen_payloads, stamp_alt_epoch, stamp_positions
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    numa_node = None
+    if torch.cuda.is_available() and os.environ.get("SW_NUMA_BIND", "1") != "0":
+        from sitewhere_amd.utils.numa import bind_to_gpu_node
+        numa_node = bind_to_gpu_node(0)
+    t_setup = time.time()
+    sw = SiteWhereInstance().start()
+    sw.wait_for_tenant("default", 60)
+    tm = sw.api("TenantManagement")
+    sw.instance.system_user.run(lambda: tm.create_tenant({"token": "soak", "name": "soak",
+                                                          "configurationTemplateId": args.template,
+                                                          "datasetTemplateId": "empty"}))
+    sw.wait_for_tenant("soak", 120)
+    ms = sw["inbound-processing"]
+    if args.filter_ids:
+        from sitewhere_amd.runtime.config import dump_document
+        before = ms.get_tenant_engine("soak")
+        cfg = dict(before.config)
+        cfg["capacity"] = dict(cfg.get("capacity", {}), dedup_filter_ids=args.filter_ids)
+        sw.instance.coord.put(ms.tenant_config_path("soak"), dump_document(cfg))
+        while ms.get_tenant_engine("soak") in (None, before) or ms.get_tenant_engine("soak").status.value != "Started":
+            time.sleep(0.1)
+    run = lambda f: sw.instance.system_user.run(f, "soak")  # noqa: E731
+    dm = sw.api("DeviceManagement", "soak")
+    run(lambda: dm.create_device_type({"token": "sensor", "name": "Sensor"}))
+    # fleet import: devices, then their assignments (no "assignment Active" events -- an imported
+    # fleet's activations happened before), in bulk: one change-feed record per 4096 entities
+    for s in range(0, args.devices, args.chunk):
+        toks = [f"dev-{i:010d}" for i in range(s, min(args.devices, s + args.chunk))]
+        run(lambda: dm.create_devices([{"token": t, "deviceTypeToken": "sensor"} for t in toks]))
+        run(lambda: dm.create_device_assignments([{"deviceToken": t} for t in toks], record_state_changes=False))
+        log(f"imported {s + len(toks)} devices ({time.time() - t_setup:.0f} s)")
+    ib = sw.tenant_engine("inbound-processing", "soak")
+    while ib.engine.n_assignments < args.devices and time.time() - t_setup < 3600:
+        time.sleep(0.2)
+    log(f"engine registry: {ib.engine.n_devices} devices, {ib.engine.n_assignments} assignments")
+    ecfg = ib.engine.cfg
+    store = sw.tenant_engine("event-management", "soak").store
+    log("dedup sizing", json.dumps(ib.dedup_sizing_report, default=str))
+    spec = FleetSpec(prefix="dev-", n_devices=args.devices, p_location=0.25, p_alert=0.05, mx_per_msg=1,
+                     with_alternate_id=True, p_unregistered=args.p_unregistered)
+    now0 = int(time.time() * 1000)
+    base, recs, pos = [], [], []
+    pin = torch.cuda.is_available()
+    for b in range(args.records):
+        raw, offs = gen_payloads(spec, args.batch, now0 - 1000, seed=11 + b)
+        base.append((raw, offs))
+        r = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1, pinned=pin)
+        recs.append(r)
+        pos.append(alt_positions(r.ptr + VALUE_HDR, offs))
+    setup_s = time.time() - t_setup
+    log(f"setup {setup_s:.0f} s")
+    bus = sw.instance.bus
+    t_raw = sw.instance.naming.tenant_prefix("soak") + "event-source-raw-payloads"
+    parts = bus.partitions(t_raw)
+    group = ib.raw_consumer.group
+    slot_at = [None] * args.records            # (partition, offset) of each record's last publish
+    epochs: list = []                          # (time, slot, epoch) of every publish
+
+    def committed(p):
+        return bus.committed(group, t_raw, p) or 0
+
+    def done(po):
+        return po is None or committed(po[0]) > po[1]
+
+    k = 0
+    samples = []                               # (t, processed, persisted, rechecks, duplicates, msgs)
+
+    def sample():
+        st = ib.engine.stats_dict()
+        samples.append((time.perf_counter(), ib.processed_events.count, ib.persisted_events.count,
+                        st["dedup_rechecks"], st["duplicates"], st["messages"], st["unregistered"]))
+
+    t0 = time.perf_counter()
+    sample()
+    next_log = t0 + 5.0
+    end = t0 + args.phases * args.phase_s
+    inflight = []
+    while time.perf_counter() < end:
+        # flow control: at most `ahead` records past the tenant's commits
+        while inflight and done(inflight[0]):
+            inflight.pop(0)
+        if len(inflight) >= args.ahead or not done(slot_at[k % args.records]):
+            time.sleep(0.0005)
+        else:
+            s = k % args.records
+            epoch = (0x50AC << 48) | k
+            stamp_positions(recs[s].ptr + VALUE_HDR, pos[s], epoch, threads=8)     # fresh ids
+            p = k % parts
+            off = recs[s].publish(bus, t_raw, p, ts=now0 + k)
+            slot_at[s] = (p, off)
+            inflight.append((p, off))
+            epochs.append((time.perf_counter(), s, epoch))
+            k += 1
+        now = time.perf_counter()
+        if now >= next_log:
+            sample()
+            a, b_ = samples[-2], samples[-1]
+            rate = (b_[1] - a[1]) / max(1e-9, b_[0] - a[0])
+            fs = ib.engine.filter_state()
+            rs = store.retention_state()
+            log(f"t={now - t0:6.1f}s {rate / 1e6:7.1f}M ev/s records={k} rechecks={b_[3]} dups={b_[4]} "
+                f"filter_rot={fs.get('rotations')} retained_rows={rs['retained_rows']} deleted_rows={rs['deleted_rows']}")
+            next_log = now + 5.0
+    while inflight:                             # drain: every published record stored and committed
+        while inflight and done(inflight[0]):
+            inflight.pop(0)
+        time.sleep(0.001)
+    ib.flush()
+    sample()
+    t_end = time.perf_counter()
+    # ---- replay of a still-retained batch: the first `replay` payloads of a record published a few
+    # seconds ago, with its ids
+    rs0 = store.retention_state()
+    recent = [e for e in epochs if t_end - e[0] >= 2.0] or epochs[:1]
+    te, s, epoch = recent[-1]
+    raw, offs = base[s]
+    m = min(args.replay, len(offs) - 1)
+    sub = np.concatenate([raw[:int(offs[m])], np.zeros(64, np.uint8)])
+    stamp_alt_epoch(sub, offs[:m + 1], epoch)
+    from sitewhere_amd.pipeline.fleet import cpu_decode
+    dec = cpu_decode(sub, offs[:m + 1], now0)
+    valid_alt = int(((dec["alt_hash"] != 0) & (dec["etype"] < 16)).sum())
+    rdup0, rfp0 = ib.recheck_duplicates, ib.recheck_false_positives
+    st0 = ib.engine.stats_dict()
+    rows0 = store.rows
+    rr = RawBatchRecord(sub[:int(offs[m])], varint_lengths(offs[:m + 1]), m, pinned=pin)
+    p = k % parts
+    off = rr.publish(bus, t_raw, p, ts=now0 + k)
+    tw = time.time()
+    while committed(p) <= off and time.time() - tw < 60:
+        time.sleep(0.002)
+    ib.flush()
+    time.sleep(2.0)                            # the per-event path drops the rechecked replays
+    st1 = ib.engine.stats_dict()
+    replay = {"age_s": round(t_end - te, 2), "payloads": m, "events_with_alt_ids": valid_alt,
+              "rechecks": st1["dedup_rechecks"] - st0["dedup_rechecks"],
+              "window_duplicates": st1["duplicates"] - st0["duplicates"],
+              "settled_duplicates": ib.recheck_duplicates - rdup0,
+              "settled_false_positives": ib.recheck_false_positives - rfp0,
+              "persisted_by_engine": st1["persisted"] - st0["persisted"],
+              "store_rows_before": rows0, "store_rows_after": store.rows}
+    # events of registered devices (the replay's unregistered payloads are routed, not deduplicated)
+    replay["events_of_registered_devices"] = valid_alt - (st1["unregistered"] - st0["unregistered"])
+    replay["all_duplicates"] = (replay["settled_duplicates"] + replay["window_duplicates"]
+                                == replay["events_of_registered_devices"] and replay["persisted_by_engine"] == 0
+                                and replay["store_rows_after"] == replay["store_rows_before"])
+    # ---- report
+    ts = np.array([x[0] for x in samples]) - t0
+    ev = np.array([x[1] for x in samples], np.float64)
+
+    def rate_between(a, b):
+        i, j = int(np.searchsorted(ts, a)), int(np.searchsorted(ts, b, side="right")) - 1
+        if j <= i:
+            return None
+        return round(float((ev[j] - ev[i]) / (ts[j] - ts[i])), 1)
+
+    phases = [rate_between(i * args.phase_s, (i + 1) * args.phase_s) for i in range(args.phases)]
+    total_s = args.phases * args.phase_s
+    first_min, last_min = rate_between(0, min(60.0, total_s)), rate_between(max(0.0, total_s - 60.0), total_s)
+    st = ib.engine.stats_dict()
+    fs = ib.engine.filter_state()
+    rs = store.retention_state()
+    msgs = st["messages"]
+    trace = {}
+    if ib.trace:
+        tr = [x for x in ib.trace if len(x) == 9]
+        gap = np.diff(np.asarray([x[0] for x in tr])) * 1000 if len(tr) > 1 else np.zeros(0)
+        if len(gap):
+            trace = {f"submit_interval_p{q}_ms": round(float(np.percentile(gap, q)), 3) for q in (50, 90, 99)}
+            trace["submit_interval_max_ms"] = round(float(gap.max()), 3)
+    cap = ecfg.dedup_filter_gens * ecfg.dedup_filter_ids
+    out = {"metric": "tenant_soak_events_per_sec", "template": args.template, "devices": args.devices,
+           "batch": args.batch, "p_unregistered": args.p_unregistered, "alt_ids": True, "via_bus": True,
+           "engine": ib.engine_kind, "numa_node": numa_node, "setup_s": round(setup_s, 1),
+           "soak_s": round(t_end - t0, 1), "events": int(ev[-1] - ev[0]),
+           "events_per_sec": round(float((ev[-1] - ev[0]) / (ts[-1] - ts[0])), 1),
+           "phase_events_per_sec": phases, "first_minute_events_per_sec": first_min,
+           "last_minute_events_per_sec": last_min,
+           "last_vs_first": round(last_min / first_min, 3) if first_min and last_min else None,
+           "records": k, "messages": msgs, "rechecks": st["dedup_rechecks"],
+           "rechecks_per_payload": st["dedup_rechecks"] / max(1, msgs), "window_duplicates": st["duplicates"],
+           "unregistered": st["unregistered"], "dedup_overflow": st["dedup_overflow"],
+           "filter": {**fs, "capacity_ids": cap, "holds_ids": (ecfg.dedup_filter_gens - 1) * ecfg.dedup_filter_ids,
+                      "bytes": ecfg.filter_bytes(), "ids_ingested_per_capacity": round(st["persisted"] / max(1, cap), 2)},
+           "store": {**rs, "retention_wraps": round(rs["deleted_rows"] / max(1, rs["retention_rows"]), 2)},
+           "trace": trace, "replay": replay,
+           "timers_ms": {name: round(t.hist.snapshot()["mean"], 3)
+                         for name, t in (("engine_step", ib.step_timer), ("columnar_store", ib.store_timer),
+                                         ("recheck", ib.recheck_timer))},
+           "series": [[round(float(a), 1), int(b)] for a, b in zip(ts, ev)]}
+    print(json.dumps(out, default=str), flush=True)
+    sw.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -167,8 +167,8 @@ def native():
         _proto(lib, "swce_ff_add", None, P, c_int64, P, c_int64)
         _proto(lib, "swce_ff_clear", None, P, c_int64)
         _proto(lib, "swce_ff_meta", None, P, P, P)
-        _proto(lib, "swce_ff_words", c_int64, P, P, c_int64)
-        _proto(lib, "swce_ff_load", None, P, P, c_int64)
+        _proto(lib, "swce_ff_export", c_int64, P, P, P, c_int64)
+        _proto(lib, "swce_ff_import", c_int32, P, P, P, c_int64)
         _proto(lib, "swce_dedup_prev_size", c_int64, P)
         _proto(lib, "swce_dedup_prev_export", c_int64, P, P, P)
         _proto(lib, "swce_dedup_prev_import", None, P, P, P, c_int64)
@@ -219,7 +219,7 @@ def native():
         _proto(lib, "swss_error", c_int32, P)
         _proto(lib, "swss_wait", c_int32, P, c_int64, c_int64)
         _proto(lib, "swss_stats", None, P, P)
-        _proto(lib, "swss_set_retention", None, P, c_int64, c_int64)
+        _proto(lib, "swss_set_retention", None, P, c_int64, c_int64, c_int64)
         _proto(lib, "swss_close", None, P)
         _proto(lib, "swss_index", c_int64, P, P, c_int64)
         _proto(lib, "swss_index_tr", c_int64, P, P, P, P, P, c_int64)

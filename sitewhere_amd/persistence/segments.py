@@ -466,9 +466,10 @@ class SegmentStore:
                          "deleted_rows", "retention_rows", "retention_bytes"),
                         (int(x) for x in a)))
 
-    def set_retention(self, bytes_: int = 0, rows: int = 0):
-        """Tighten / set the retention limits (0: unchanged; rows -1: none); the next file applies them."""
-        self.lib.swss_set_retention(self.h, int(bytes_), int(rows))
+    def set_retention(self, bytes_: int = 0, rows: int = 0, rotate_bytes: int = 0):
+        """Set the retention limits (0: unchanged; rows -1: none) and the size at which new files start
+        (0: unchanged); applied after the next group commit."""
+        self.lib.swss_set_retention(self.h, int(bytes_), int(rows), int(rotate_bytes))
 
     def index(self) -> np.ndarray:
         cap = 1024
@@ -1240,15 +1241,22 @@ class DurableEventStore(DeviceEventStore):
                                    "deleted_rows", "deleted_bytes", "deleted_files", "files")} | {
             "api_tail": len(self._api_tail), "api_flush_error": self._api_err, "rotate_bytes": self.rotate_bytes}
 
+    # the fewest bytes a stored row takes (a block's columns + index run 14-19 B per row)
+    MIN_ROW_BYTES = 8
+
     def limit_retention_rows(self, rows: int) -> int:
-        """Keep at most ``rows`` event rows (whole segment files, oldest first; applied when the next
-        file starts): an engine tenant whose store-backed dedup filter remembers its newest N ids sets
-        this, so the store holds no id the filter has forgotten.  Only ever tightens.  Returns the
-        limit in force."""
+        """Keep at most ``rows`` event rows (whole segment files, oldest first, checked after every
+        group commit): an engine tenant whose store-backed dedup filter remembers its newest N ids sets
+        this, so the store holds no id the filter has forgotten.  New files then start small enough
+        to hold at most a quarter of the limit, so the file being written (never deleted) keeps the
+        store within 1.25x of it, and what the limit deletes comes back in quarter steps.  Only ever
+        tightens.  Returns the limit in force."""
         cur = self.seg.stats()["retention_rows"]
         rows = int(rows)
         if rows > 0 and (cur <= 0 or rows < cur):
-            self.seg.set_retention(0, rows)
+            rotate = min(self.rotate_bytes, max(1 << 20, rows * self.MIN_ROW_BYTES // 4)) >> 12 << 12
+            self.seg.set_retention(0, rows, rotate)
+            self.rotate_bytes = rotate
             cur = rows
         return cur
 

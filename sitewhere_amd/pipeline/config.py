@@ -97,14 +97,20 @@ class EngineConfig:
             self.dedup_filter_ids = 0
             self.ff_buckets = 0
 
+    # a durable store bounded to N rows holds at most 1.25 N (the file being written, at most N / 4
+    # rows, is never deleted: DurableEventStore.limit_retention_rows)
+    STORE_ROWS_OVERSHOOT = 1.25
+
     def filter_retention_rows(self, slack_rows: int = 0) -> int:
-        """Rows the durable store may retain so that the filter holds every retained id (0: no
-        filter, no bound).  The filter holds at least the newest (gens - 1) * dedup_filter_ids ids;
-        a store that keeps at most that many rows (newest first) keeps no id older than them.
-        ``slack_rows``: rows of blocks in flight and of one segment file (whole files are deleted)."""
+        """The row limit of the durable store under which the filter holds every retained id (0: no
+        filter, no bound).  The filter holds at least the newest (gens - 1) * dedup_filter_ids ids; a
+        store that keeps at most that many rows (newest first) keeps no id older than them.  The
+        store can overshoot its limit by the file being written; ``slack_rows``: rows of the blocks
+        in flight (written between two retention checks)."""
         if not self.dedup_filter_ids:
             return 0
-        return max(self.rec_cap, (self.dedup_filter_gens - 1) * self.dedup_filter_ids - int(slack_rows))
+        held = (self.dedup_filter_gens - 1) * self.dedup_filter_ids - int(slack_rows)
+        return max(self.rec_cap, int(held / self.STORE_ROWS_OVERSHOOT))
 
     def filter_bytes(self) -> int:
         return self.ff_buckets * self.dedup_filter_gens * 64 if self.dedup_filter_ids else 0

@@ -579,7 +579,8 @@ class CpuInboundEngine(EngineBase):
             "dedup_key": u64(self.dedup.keys()), "dedup_seq": np.array(list(self.dedup.values()), np.int64),
             "dedup_prev_key": u64(self.dedup_prev.keys()),
             "dedup_prev_seq": np.array(list(self.dedup_prev.values()), np.int64),
-            **({"dd_ff": self.ff.tab.copy(), "dd_ff_meta": self.ff.meta.copy()} if self.ff is not None else {}),
+            **(dict(zip(("dd_ff_idx", "dd_ff_rows"), self.ff.export()), dd_ff_meta=self.ff.meta.copy())
+               if self.ff is not None else {}),
             "intern_key": u64(self.intern.keys()), "intern_id": np.array(list(self.intern.values()), np.int64),
             "seen": u64(self._seen),
             "st_last": self.st_last, "st_missing": self.st_missing, "st_loc_date": self.st_loc_date,
@@ -598,8 +599,8 @@ class CpuInboundEngine(EngineBase):
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
         self.stats[:] = 0
         self.stats[:len(a["stats"])] = a["stats"]
-        if self.ff is not None and "dd_ff" in a and len(a["dd_ff"]) == len(self.ff.tab):
-            self.ff.tab[:] = a["dd_ff"]
+        if self.ff is not None and "dd_ff_idx" in a:
+            self.ff.load(a["dd_ff_idx"], a["dd_ff_rows"])
             self.ff.meta[:] = a["dd_ff_meta"]
         self.dedup = dict(zip((int(x) for x in a["dedup_key"]), (int(x) for x in a["dedup_seq"])))
         self.dedup_prev = dict(zip((int(x) for x in a.get("dedup_prev_key", [])),

@@ -107,6 +107,19 @@ class FingerprintFilter:
         v = self.tab.reshape(self.buckets, self.gens, SLOTS)
         v[:, g, :] = 0
 
+    # ------------------------------------------------------------------ checkpoints
+    def export(self) -> tuple[np.ndarray, np.ndarray]:
+        """The non-empty buckets: (indices into [buckets * gens], [k, 16] fingerprints) -- the sparse
+        form every engine checkpoints (a multi-GB filter of a small tenant is a few KB)."""
+        v = self.tab.reshape(-1, SLOTS)
+        idx = np.nonzero(v.any(axis=1))[0].astype(np.int64)
+        return idx, v[idx].copy()
+
+    def load(self, idx, rows):
+        v = self.tab.reshape(-1, SLOTS)
+        v[:] = 0
+        v[np.asarray(idx, np.int64)] = np.asarray(rows, np.uint32).reshape(-1, SLOTS)
+
     # ------------------------------------------------------------------ step rules
     def add_persisted(self, hashes):
         """A step's persisted ids (k_persist): into the live generation, counted (meta[6])."""

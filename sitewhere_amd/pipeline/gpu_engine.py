@@ -1372,13 +1372,28 @@ class GpuInboundEngine(EngineBase):
         self._sync_streams()
 
     def _ckpt_tables(self):
-        return self._CKPT_TABLES + (("dd_ff", "dd_ff_meta") if self._ff_on else ())
+        return self._CKPT_TABLES + (("dd_ff_meta",) if self._ff_on else ())
+
+    def _ff_export(self) -> dict:
+        """The filter's non-empty 64-byte buckets (the sparse form every engine checkpoints)."""
+        v = self.t["dd_ff"].view(-1, 16)
+        idx = torch.nonzero(v.ne(0).any(dim=1)).flatten()
+        return {"dd_ff_idx": idx.cpu().numpy().astype(np.int64), "dd_ff_rows": v[idx].cpu().numpy().view(np.uint32)}
+
+    def _ff_import(self, idx, rows):
+        v = self.t["dd_ff"].view(-1, 16)
+        v.zero_()
+        if len(idx):
+            i = torch.from_numpy(np.ascontiguousarray(idx, np.int64)).to(self.device)
+            v[i] = torch.from_numpy(np.ascontiguousarray(rows, np.uint32).reshape(-1, 16).view(np.int32)).to(self.device)
 
     def checkpoint_state(self, include_store: bool = False) -> dict:
         if self._pend is not None:
             raise RuntimeError("checkpoint with a pipelined exchange in flight: drain the round first")
         self._sync_streams()
         st = {k: self.t[k].cpu().numpy() for k in self._ckpt_tables()}
+        if self._ff_on:
+            st.update(self._ff_export())
         if self.world > 1:
             cp = self._carry_par
             n = int(self.t["n_carry"][cp].item())
@@ -1409,6 +1424,8 @@ class GpuInboundEngine(EngineBase):
                 self.t[k][:src.numel()].copy_(src)
                 continue
             self.t[k].copy_(src)       # in place: captured graphs keep their pointers
+        if self._ff_on and "dd_ff_idx" in a:
+            self._ff_import(a["dd_ff_idx"], a["dd_ff_rows"])
         if "dd_tab" not in a and "dd_meta" in a:
             # older checkpoints decided the rotation at the start of a step; now the end of the
             # previous step does (k_step_end): apply that decision to the restored window

@@ -282,11 +282,11 @@ class NativeCpuEngine(CpuInboundEngine):
             "ms_key": ms[:, :3].copy(), "ms_val": ms[:, 3:].copy(),
             "carry": self.carry.view(np.uint8).reshape(-1).copy(),
         }
-        nw = lib.swce_ff_words(h, None, 0)
-        if nw:
-            bw = np.zeros(nw, np.uint64)
-            lib.swce_ff_words(h, _ptr(bw), nw)
-            st["dd_ff"] = bw.view(np.uint32)
+        if self.filter_on:
+            n = int(lib.swce_ff_export(h, None, None, 0))
+            idx, rows = np.zeros(max(n, 1), np.int64), np.zeros((max(n, 1), 16), np.uint32)
+            lib.swce_ff_export(h, _ptr(idx), _ptr(rows), n)
+            st["dd_ff_idx"], st["dd_ff_rows"] = idx[:n], rows[:n]
             st["dd_ff_meta"] = self._ff_meta_get()
         if include_store:
             st.update({f"store.{k}": v for k, v in self.store.items()})
@@ -294,9 +294,11 @@ class NativeCpuEngine(CpuInboundEngine):
 
     def restore_state(self, a: dict, include_store: bool):
         lib, h = self._lib, self._h
-        if "dd_ff" in a and lib.swce_ff_words(h, None, 0):
-            bw = np.ascontiguousarray(a["dd_ff"], np.uint32).view(np.uint64)
-            lib.swce_ff_load(h, _ptr(bw), len(bw))
+        if "dd_ff_idx" in a and self.filter_on:
+            idx = np.ascontiguousarray(a["dd_ff_idx"], np.int64)
+            rows = np.ascontiguousarray(a["dd_ff_rows"], np.uint32).reshape(-1, 16)
+            if lib.swce_ff_import(h, _ptr(idx), _ptr(rows), len(idx)) != 0:
+                raise ValueError("checkpoint's dedup filter does not fit this engine's filter")
             self._ff_meta_set(a["dd_ff_meta"])
         self.cursor, self.seq_base = (int(x) for x in a["scalars"])
         self.stats[:] = 0

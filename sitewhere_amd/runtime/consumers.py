@@ -261,6 +261,28 @@ class NearCache:
             self.put(key, val)
         return val
 
+    def get_many(self, keys, loader_many=None) -> dict:
+        """key -> value for ``keys`` (missing ones: None): hits from the cache, every miss loaded with
+        ONE ``loader_many(missed keys) -> values`` call (a consumer's poll batch validated in one
+        pass, one bulk lookup for what the cache lacks)."""
+        out, miss = {}, []
+        now = time.time()
+        for k in dict.fromkeys(keys):
+            v = self._d.get(k)
+            if v is not None and now - v[1] < self.ttl and (self.max_idle is None or now - v[2] < self.max_idle):
+                v[2] = now
+                self.hits += 1
+                out[k] = v[0]
+            else:
+                self.misses += 1
+                miss.append(k)
+        if miss and loader_many is not None:
+            for k, val in zip(miss, loader_many(miss)):
+                out[k] = val
+                if val is not None:
+                    self.put(k, val)
+        return out
+
     def put(self, key, val):
         with self._lock:
             now = time.time()

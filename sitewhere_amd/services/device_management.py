@@ -64,13 +64,24 @@ class DeviceManagement:
         self._lock = threading.RLock()
 
     # ------------------------------------------------------------------ change feed
-    def _add_listener(self, cb):
-        self._listeners.append(cb)
+    def _add_listener(self, cb, many=None):
+        """``cb(kind, entity)`` per change; ``many(kind, entities)``, when given, takes a bulk
+        operation's changes at once (one change-feed publish, one durable add)."""
+        self._listeners.append((cb, many))
 
     def _emit(self, kind: str, entity):
-        for cb in list(self._listeners):
+        self._emit_many(kind, [entity])
+
+    def _emit_many(self, kind: str, entities: list):
+        if not entities:
+            return
+        for cb, many in list(self._listeners):
             try:
-                cb(kind, entity)
+                if many is not None and len(entities) > 1:
+                    many(kind, entities)
+                else:
+                    for e in entities:
+                        cb(kind, e)
             except Exception:   # one listener must not block the others; make the failure visible
                 logging.getLogger(__name__).warning("device-model listener failed on %s", kind, exc_info=True)
 
@@ -161,24 +172,49 @@ class DeviceManagement:
             raise SiteWhereSystemException(ErrorCode.IncompleteData, detail="device type required")
         return self.device_types.require_token(tok)
 
-    def create_device(self, request: dict) -> Device:
+    def _new_device(self, request: dict) -> Device:
         dt = self._device_type_from(request)
         parent = None
         if request.get("parentDeviceToken"):
             parent = self.devices.require_token(request["parentDeviceToken"]).id
         maps = [DeviceElementMapping.from_dict(m) if isinstance(m, dict) else m
                 for m in request.get("deviceElementMappings", [])]
-        d = self.devices.create({k: v for k, v in request.items() if k != "deviceElementMappings"},
-                                device_type_id=dt.id, parent_device_id=parent, device_element_mappings=maps,
-                                device_assignment_id=None)
+        return self.devices.create({k: v for k, v in request.items() if k != "deviceElementMappings"},
+                                   device_type_id=dt.id, parent_device_id=parent, device_element_mappings=maps,
+                                   device_assignment_id=None)
+
+    def create_device(self, request: dict) -> Device:
+        d = self._new_device(request)
         self._emit("device.created", d)
         return d
+
+    def create_devices(self, requests: list) -> list:
+        """Bulk device creation (fleet provisioning; an extension of the reference's one-at-a-time
+        ``createDevice``): the same validation per device, then ONE change-feed publish for the batch
+        (engine tenants register the whole batch in one table upload).  A request that fails
+        validation stops the batch; the devices before it are created and announced.  Returns the
+        new devices' ids (not the entities: a bulk call's reply stays small)."""
+        out = []
+        try:
+            for r in requests:
+                out.append(self._new_device(r))
+        finally:
+            self._emit_many("device.created", out)
+        return [d.id for d in out]
 
     def get_device(self, id: str):
         return self.devices.get(id)
 
     def get_device_by_token(self, token: str):
         return self.devices.get_by_token(token)
+
+    def get_devices(self, ids: list) -> list:
+        """Devices by id, in order (None where unknown): one call for a consumer's poll batch."""
+        return [self.devices.get(i) if i else None for i in ids]
+
+    def get_devices_by_tokens(self, tokens: list) -> list:
+        """Devices by token, in order (None where unknown)."""
+        return [self.devices.get_by_token(t) if t else None for t in tokens]
 
     def update_device(self, id: str, request: dict) -> Device:
         fixed = {}
@@ -330,25 +366,45 @@ class DeviceManagement:
     # ================================================================== assignments
     def create_device_assignment(self, request: dict) -> DeviceAssignment:
         with self._lock:
-            d = (self.devices.require(request["deviceId"]) if request.get("deviceId")
-                 else self.devices.require_token(request.get("deviceToken")))
-            if d.device_assignment_id:
-                cur = self.assignments.get(d.device_assignment_id)
-                if cur is not None and cur.status != DeviceAssignmentStatus.Released:
-                    raise SiteWhereSystemException(ErrorCode.DeviceAlreadyAssigned, detail=d.token)
-            fixed = dict(device_id=d.id, device_type_id=d.device_type_id,
-                         status=DeviceAssignmentStatus(request.get("status", "Active")),
-                         active_date=now_ms(), released_date=None,
-                         customer_id=self._opt_token(self.customers, request.get("customerToken"), request.get("customerId")),
-                         area_id=self._opt_token(self.areas, request.get("areaToken"), request.get("areaId")),
-                         asset_id=request.get("assetId") or None)
-            if request.get("assetToken"):
-                fixed["asset_id"] = request["assetToken"]  # resolved by the asset service (reference: token ref)
-            req = {k: v for k, v in request.items() if k in ("token", "metadata")}
-            a = self.assignments.create(req, **fixed)
-            d.device_assignment_id = a.id
-            self.devices.put(d)
+            a = self._new_assignment(request)
         self._emit("assignment.created", a)
+        return a
+
+    def create_device_assignments(self, requests: list, record_state_changes: bool = True) -> list:
+        """Bulk assignment creation (see :meth:`create_devices`): one change-feed publish and ONE
+        durable add of the assignments' state-change events for the batch.  ``record_state_changes``
+        False: an import of assignments whose activation already happened elsewhere (a fleet
+        migrated from another system) -- no "assignment Active" state-change event is recorded.
+        Returns the new assignments' ids."""
+        out = []
+        try:
+            with self._lock:
+                for r in requests:
+                    out.append(self._new_assignment(r))
+        finally:
+            self._emit_many("assignment.created" if record_state_changes else "assignment.imported", out)
+        return [a.id for a in out]
+
+    def _new_assignment(self, request: dict) -> DeviceAssignment:
+        """Validate and store one assignment (caller holds the lock; the caller announces it)."""
+        d = (self.devices.require(request["deviceId"]) if request.get("deviceId")
+             else self.devices.require_token(request.get("deviceToken")))
+        if d.device_assignment_id:
+            cur = self.assignments.get(d.device_assignment_id)
+            if cur is not None and cur.status != DeviceAssignmentStatus.Released:
+                raise SiteWhereSystemException(ErrorCode.DeviceAlreadyAssigned, detail=d.token)
+        fixed = dict(device_id=d.id, device_type_id=d.device_type_id,
+                     status=DeviceAssignmentStatus(request.get("status", "Active")),
+                     active_date=now_ms(), released_date=None,
+                     customer_id=self._opt_token(self.customers, request.get("customerToken"), request.get("customerId")),
+                     area_id=self._opt_token(self.areas, request.get("areaToken"), request.get("areaId")),
+                     asset_id=request.get("assetId") or None)
+        if request.get("assetToken"):
+            fixed["asset_id"] = request["assetToken"]  # resolved by the asset service (reference: token ref)
+        req = {k: v for k, v in request.items() if k in ("token", "metadata")}
+        a = self.assignments.create(req, **fixed)
+        d.device_assignment_id = a.id
+        self.devices.put(d)
         return a
 
     def _opt_token(self, crud, token, id_):
@@ -358,6 +414,10 @@ class DeviceManagement:
 
     def get_device_assignment(self, id: str):
         return self.assignments.get(id)
+
+    def get_device_assignments(self, ids: list) -> list:
+        """Assignments by id, in order (None where unknown)."""
+        return [self.assignments.get(i) if i else None for i in ids]
 
     def get_device_assignment_by_token(self, token: str):
         return self.assignments.get_by_token(token)
@@ -653,7 +713,31 @@ class DeviceManagementTriggers:
     def __init__(self, dm: DeviceManagement, event_api_factory):
         self.dm = dm
         self.events = event_api_factory
-        dm._add_listener(self._on_change)
+        dm._add_listener(self._on_change, self._on_changes)
+
+    @staticmethod
+    def _state_change(kind) -> dict:
+        return {"attribute": "assignment", "type": "automated",
+                "previousState": None if kind == "assignment.created" else "Active",
+                "newState": "Active" if kind == "assignment.created" else "Released"}
+
+    def _on_changes(self, kind, entities):
+        """A bulk operation's assignments: their state changes in one durable add."""
+        if kind not in ("assignment.created", "assignment.ended"):
+            return
+        try:
+            api = self.events()
+            if api is None:
+                return
+            if hasattr(api, "add_event_batch"):
+                api.add_event_batch([(e.id, "StateChange", self._state_change(kind)) for e in entities],
+                                    assignments=entities)
+            else:
+                for e in entities:
+                    api.add_state_changes(e.id, self._state_change(kind))
+        except Exception:
+            logging.getLogger(__name__).warning("assignment state-change events for %s not recorded", kind,
+                                                exc_info=True)
 
     def _on_change(self, kind, e):
         if kind not in ("assignment.created", "assignment.ended"):
@@ -675,7 +759,7 @@ class DeviceManagementTenantEngine(MicroserviceTenantEngine):
         ds = self.config.get("datastore", {"type": "memory"})
         store = create_store(ds.get("type", "memory"), **{k: v for k, v in ds.items() if k != "type"})
         self.management = DeviceManagement(store)
-        self.management._add_listener(self._publish_change)
+        self.management._add_listener(self._publish_change, self._publish_changes)
         self.triggers = DeviceManagementTriggers(
             self.management, lambda: self.ms.api("DeviceEventManagement", self.tenant.token)
             if "DeviceEventManagement" in self.ms.instance.resolver.names() else None)
@@ -686,6 +770,21 @@ class DeviceManagementTenantEngine(MicroserviceTenantEngine):
         from ..rpc import codec
         self.ms.producer.send(topic, getattr(entity, "token", None) or entity.id,
                               json.dumps({"kind": kind, "entity": codec.to_wire(entity)}).encode())
+
+    # entities per bulk change record (a bulk create of 1M devices is ~250 records, not 1M)
+    BULK_RECORD = 4096
+
+    def _publish_changes(self, kind, entities):
+        """A bulk operation's changes as ``{"kind": "bulk", "of": kind, "entities": [...]}`` records
+        (consumers expand them, ``inbound_processing.model_changes``): one record per entity made every
+        consumer decode and dispatch a million records for a fleet provisioning."""
+        topic = self.ms.instance.naming.tenant_prefix(self.tenant.token) + "device-model-updates"
+        from ..rpc import codec
+        n = self.BULK_RECORD
+        self.ms.producer.send_batch(topic, [
+            (f"bulk-{kind}-{i}", json.dumps({"kind": "bulk", "of": kind,
+                                            "entities": [codec.to_wire(e) for e in entities[i:i + n]]}).encode())
+            for i in range(0, len(entities), n)])
 
     def tenant_bootstrap(self, dataset_template, monitor):
         from .builders import DeviceBuilder, EventBuilder

@@ -123,6 +123,55 @@ class DeviceEventManagement:
             self._persist(out)
         return len(pairs)
 
+    # event builders per type (the per-type add_* methods above use the same constructors)
+    _BUILD = {
+        "Measurement": lambda r: DeviceMeasurement(name=r.get("name", ""), value=float(r.get("value", 0.0))),
+        "Location": lambda r: DeviceLocation(latitude=float(r.get("latitude", 0)), longitude=float(r.get("longitude", 0)),
+                                             elevation=r.get("elevation")),
+        "Alert": lambda r: DeviceAlert(source=AlertSource(r.get("source", "Device")), level=AlertLevel(r.get("level", "Info")),
+                                       type=r.get("type", ""), message=r.get("message", "")),
+        "StateChange": lambda r: DeviceStateChange(attribute=r.get("attribute", ""), type=r.get("type", ""),
+                                                   previous_state=r.get("previousState"), new_state=r.get("newState")),
+        "CommandResponse": lambda r: DeviceCommandResponse(originating_event_id=r.get("originatingEventId"),
+                                                           response_event_id=r.get("responseEventId"),
+                                                           response=r.get("response")),
+    }
+
+    def add_event_batch(self, items, assignments: list | None = None) -> list:
+        """Events of many assignments in ONE durable add: ``items`` = [(assignment id, event type,
+        request)] -- a consumer's whole poll batch (the reference's DecodedEventsConsumer hands each
+        event to its own add, DecodedEventsConsumer.java:155-204, and only the Mongo buffer batches the
+        writes, DeviceEventBuffer.java:99-135).  Alternate ids are checked in one pass: already stored
+        or repeated within the batch, the stored (or first) event is returned instead of a new one
+        (exactly-once storage, as :meth:`_add`).  Returns the events, in item order; an item whose
+        assignment is unknown raises like the per-event add (nothing of the batch is stored).
+        ``assignments``: the items' assignment entities when the caller has them (device management
+        announcing its own bulk create), instead of one lookup each."""
+        ctx = {a.id: a for a in assignments or ()}
+        out, new, seen = [], [], {}
+        for aid, etype, r in items:
+            a = ctx.get(aid)
+            if a is None:
+                a = ctx[aid] = self._context(aid)
+            alt = r.get("alternateId")
+            if alt:
+                ex = seen.get(alt) or (self._writer is not None and self._writer.pending_alternate(alt)) \
+                    or self.store.get_event_by_alternate_id(alt)
+                if ex is not None:
+                    out.append(ex)
+                    continue
+            build = self._BUILD.get(str(getattr(etype, "value", etype)))
+            if build is None:
+                raise SiteWhereSystemException(ErrorCode.Error, detail=f"batch add of {etype} events")
+            e = self._stamp(build(r), a, r)
+            if alt:
+                seen[alt] = e
+            new.append(e)
+            out.append(e)
+        if new:
+            self._persist(new)
+        return out
+
     def add_command_invocations(self, assignment_id: str, *requests):
         return self._add(assignment_id, _flat(requests),
                          lambda r: DeviceCommandInvocation(initiator=r.get("initiator", "REST"),

@@ -320,25 +320,71 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             self._asg_entities[ai] = a
             self._asg_dirty.add(ai)
 
-    def _on_model_update(self, recs):
-        super()._on_model_update(recs)          # near-cache invalidation for the per-event path
-        for r in recs:
-            m = json.loads(r.value)
-            kind, e = m["kind"], codec.from_wire(m["entity"])
-            if kind in ("device.created", "device.updated"):
-                self._upsert_device(e)
-            elif kind == "device.deleted":
+    def _upsert_devices(self, devs):
+        """Many devices in one registry upload (a bulk create's change-feed records)."""
+        with self._lock:
+            di = np.array([self.dev_index.get(d.id) for d in devs], np.int32)
+            fps = np.array([fingerprint_str(d.token) for d in devs], np.uint64).reshape(-1, 2)
+            self.engine.register_devices(np.ascontiguousarray(fps[:, 0]), np.ascontiguousarray(fps[:, 1]), di)
+            for d, i in zip(devs, di.tolist()):
+                self._dev_tokens[i] = d.token
+                self._dev_types[i] = d.device_type_id
+
+    def _upsert_assignments(self, asgs):
+        """Many assignments in one engine call, in feed order (the last one of a device wins)."""
+        with self._lock:
+            missing = [a.device_id for a in asgs if int(self.engine.dev_slot[self.dev_index.get(a.device_id)]) < 0]
+        if missing:                              # rare: their devices' records have not arrived yet
+            for a in asgs:
+                self._upsert_assignment(a)
+            return
+        with self._lock:
+            ai = [self.asg_index.get(a.id) for a in asgs]
+            self.engine.set_assignments(ai, [self.dev_index.get(a.device_id) for a in asgs],
+                                        customer=[self.customers.get(a.customer_id) for a in asgs],
+                                        area=[self.areas.get(a.area_id) for a in asgs],
+                                        asset=[self.assets.get(a.asset_id) for a in asgs],
+                                        active=[0 if a.status == DeviceAssignmentStatus.Released else 1 for a in asgs])
+            for a, i in zip(asgs, ai):
+                self._asg_entities[i] = a
+                self._asg_dirty.add(i)
+
+    def _apply_model_changes(self, changes):
+        super()._apply_model_changes(changes)   # near-cache invalidation for the per-event path
+        # runs of device creates / updates and of assignment creates / updates are applied in one
+        # engine call each (a bulk provisioning publishes thousands at once); order is kept
+        run_kind, run = None, []
+
+        def flush():
+            if run_kind == "device":
+                self._upsert_devices(run) if len(run) > 1 else self._upsert_device(run[0])
+            elif run_kind == "assignment":
+                self._upsert_assignments(run) if len(run) > 1 else self._upsert_assignment(run[0])
+            run.clear()
+
+        for kind, e in changes:
+            k = ("device" if kind in ("device.created", "device.updated")
+                 else "assignment" if kind in ("assignment.created", "assignment.imported", "assignment.updated",
+                                               "assignment.ended")
+                 else None)
+            if k != run_kind:
+                flush()
+                run_kind = k
+            if k is not None:
+                run.append(e)
+                continue
+            if kind == "device.deleted":
                 with self._lock:
                     # tombstone: the fingerprint keeps its slot but resolves to no active assignment
                     di = self.dev_index.get(e.id)
                     self.engine.dev_asg[di] = -1
                     self.engine._dirty_devices(np.array([di], np.int32))
-            elif kind.startswith("assignment."):
-                if kind == "assignment.deleted":
-                    e.status = DeviceAssignmentStatus.Released
+            elif kind == "assignment.deleted":
+                e.status = DeviceAssignmentStatus.Released
                 self._upsert_assignment(e)
             elif kind.startswith("zone."):
                 self._load_zones()
+        flush()
 
     # ---------------------------------------------------------------- lifecycle
     def tenant_start(self, monitor):
@@ -1042,17 +1088,11 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
     # payloads are at least this many bytes on the raw topic (a delimited protobuf request carrying a
     # device token and one event): the most ids a partition's retention can redeliver
     MIN_PAYLOAD_BYTES = 24
-    # the fewest bytes a durable row takes (columns + index; a step's block runs 14-19 B/row): a
-    # segment file of rotate_bytes holds at most rotate_bytes / 8 rows
-    MIN_ROW_BYTES = 8
-
     def filter_retention_slack(self) -> int:
-        """Rows the store may hold beyond its row limit: the file being written (whole files are
-        deleted) and the blocks in flight."""
-        em = self._em()
-        st = em.durable_retention() if hasattr(em, "durable_retention") else {}
-        rotate = int(st.get("rotate_bytes", 1 << 30) or (1 << 30))
-        return rotate // self.MIN_ROW_BYTES + 16 * self.engine.cfg.rec_cap
+        """Rows the store may take beyond its row limit between two retention checks: the blocks in
+        flight (steps submitted ahead of the store; the file being written is accounted for by
+        ``EngineConfig.filter_retention_rows``)."""
+        return 16 * self.engine.cfg.rec_cap
 
     def check_dedup_sizing(self) -> dict:
         """Runtime check of the engine's dedup sizing (docs/PARITY.md, alternate-id dedup).  The HBM

@@ -30,6 +30,25 @@ _ADDERS = {
     "DeviceCommandResponse": "add_command_responses", "Acknowledge": "add_command_responses",
     "DeviceStateChange": "add_state_changes", "DeviceCommandInvocation": "add_command_invocations",
 }
+# request type -> event type of event management's batch add (``add_event_batch``); command
+# invocations keep their per-assignment add (their target defaults to the assignment)
+_BATCH_TYPES = {"DeviceMeasurement": "Measurement", "DeviceLocation": "Location", "DeviceAlert": "Alert",
+                "DeviceCommandResponse": "CommandResponse", "Acknowledge": "CommandResponse",
+                "DeviceStateChange": "StateChange"}
+
+
+def model_changes(recs) -> list:
+    """(kind, entity) of the device-model change feed's records, in order; bulk records (a bulk
+    create's entities, ``DeviceManagementTenantEngine._publish_changes``) expanded."""
+    out = []
+    for r in recs:
+        m = json.loads(r.value)
+        if m["kind"] == "bulk":
+            kind = m["of"]
+            out.extend((kind, codec.from_wire(w)) for w in m["entities"])
+        else:
+            out.append((m["kind"], codec.from_wire(m["entity"])))
+    return out
 
 
 class InboundProcessingTenantEngine(MicroserviceTenantEngine):
@@ -41,6 +60,7 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
         self.t_enriched_cmd = n.enriched_command_invocations(t)
         self.devices = NearCache(5000, 60.0)
         self.assignments = NearCache(5000, 60.0)
+        self._dev_token: dict = {}              # device id -> token, for cache invalidation by id
         # processingThreadCount (reference default 25) is honoured, capped by what helps here:
         # Python threads contend on the GIL, so work runs batched on few threads and the bulk
         # throughput path is the fused GPU engine (``"engine": "gpu"``).
@@ -76,20 +96,47 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
         return self.ms.api("DeviceEventManagement", self.tenant.token)
 
     def _on_model_update(self, recs):
-        for r in recs:
-            m = json.loads(r.value)
-            e = codec.from_wire(m["entity"])
-            if m["kind"].startswith("device."):
+        self._apply_model_changes(model_changes(recs))
+
+    def _apply_model_changes(self, changes):
+        for kind, e in changes:
+            if kind.startswith("device."):
                 self.devices.invalidate(getattr(e, "token", None))
                 self.devices.invalidate(("id", e.id))
-            elif m["kind"].startswith("assignment."):
+            elif kind.startswith("assignment."):
+                # the device's cached entries carry its assignment id: drop them (by id, and by the
+                # token it was loaded under)
                 self.assignments.invalidate(e.id)
                 self.devices.invalidate(("id", e.device_id))
-                self.devices.invalidate(None)
+                tok = self._dev_token.get(e.device_id)
+                if tok is not None:
+                    self.devices.invalidate(tok)
 
     def device_by_token(self, token):
         with self.device_lookup.time():
-            return self.devices.get(token, lambda k: self._dm().get_device_by_token(k))
+            d = self.devices.get(token, lambda k: self._dm().get_device_by_token(k))
+        if d is not None:
+            self._dev_token[d.id] = token
+        return d
+
+    def _load_devices(self, tokens):
+        dm = self._dm()
+        if hasattr(dm, "get_devices_by_tokens"):
+            return dm.get_devices_by_tokens(list(tokens))
+        return [dm.get_device_by_token(t) for t in tokens]
+
+    def _load_assignments(self, ids):
+        dm = self._dm()
+        if hasattr(dm, "get_device_assignments"):
+            return dm.get_device_assignments(list(ids))
+        return [dm.get_device_assignment(i) for i in ids]
+
+    def _load_devices_by_id(self, keys):
+        dm = self._dm()
+        ids = [k[1] for k in keys]
+        if hasattr(dm, "get_devices"):
+            return dm.get_devices(ids)
+        return [dm.get_device(i) for i in ids]
 
     def assignment(self, aid):
         with self.assignment_lookup.time():
@@ -97,19 +144,43 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
 
     # ---- InboundPayloadProcessingLogic -----------------------------------------------
     def _process_decoded(self, recs):
-        """Validate a poll batch, then store it with one event-management call per (assignment, type)
-        run -- the reference issues one async gRPC per event (UnaryEventStorageStrategy); batching
-        keeps per-key order (records of one device are in one partition, in order)."""
+        """Validate a whole poll batch in one pass -- the near cache answers what it holds and every
+        miss (devices by token, then their assignments) is fetched with ONE bulk lookup -- then store
+        it with ONE event-management call (``add_event_batch``; per-key order kept: a device's
+        records are in one partition, in order).  The reference validates and stores per event on
+        the poll thread (DecodedEventsConsumer.java:155-204, UnaryEventStorageStrategy.java:53-90)
+        and batches only inside the Mongo buffer (DeviceEventBuffer.java:99-135).  Command
+        invocations keep one call per (assignment) run."""
         em = self._em()
-        groups: dict = {}
-        order: list = []
+        decoded = []
         for r in recs:
             try:
-                p = payloads.decode_inbound(r.value)
-                a = self._validate(p)
-                if a is None:
+                decoded.append(payloads.decode_inbound(r.value))
+            except Exception:
+                self.failed_events.mark()
+                self.logger.exception("failed to decode inbound payload")
+        with self.device_lookup.time():
+            devs = self.devices.get_many([p["deviceToken"] for p in decoded], self._load_devices)
+        for tok, d in devs.items():
+            if d is not None:
+                self._dev_token[d.id] = tok
+        with self.assignment_lookup.time():
+            asgs = self.assignments.get_many([d.device_assignment_id for d in devs.values()
+                                              if d is not None and d.device_assignment_id], self._load_assignments)
+        items, groups, order = [], {}, []
+        for p in decoded:
+            try:
+                d = devs.get(p["deviceToken"])
+                a = asgs.get(d.device_assignment_id) if d is not None and d.device_assignment_id else None
+                if d is None or a is None or a.status == DeviceAssignmentStatus.Released:
+                    self.unregistered.mark()
+                    self.ms.producer.send(self.t_unregistered, p["deviceToken"], payloads.encode_inbound(p))
                     continue
                 req = p["eventCreateRequest"]
+                et = _BATCH_TYPES.get(req["type"])
+                if et is not None and hasattr(em, "add_event_batch"):
+                    items.append((a.id, et, req["request"]))
+                    continue
                 fn = _ADDERS.get(req["type"])
                 if fn is None:
                     self._route_stream(p, a)
@@ -122,8 +193,9 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
             except Exception:
                 self.failed_events.mark()
                 self.logger.exception("failed to process inbound payload")
-        for key in order:
-            reqs = groups[key]
+        calls = [(lambda: em.add_event_batch(items), len(items))] if items else []
+        calls += [(lambda key=key: getattr(em, key[1])(key[0], groups[key]), len(groups[key])) for key in order]
+        for call, n in calls:
             # A storage failure is transient (event management unavailable / restarting): retry the
             # call in place, then fail the batch so the consumer re-reads it from its first record
             # (at-least-once; alternate-id idempotent storage absorbs the replayed prefix).  Only
@@ -131,12 +203,12 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
             for attempt in range(4):
                 try:
                     with self.event_storage.time():
-                        getattr(em, key[1])(key[0], reqs)
-                    self.processed_events.mark(len(reqs))
+                        call()
+                    self.processed_events.mark(n)
                     break
                 except Exception:
                     if attempt == 3:
-                        self.logger.warning("storing %d events failed; batch will be redelivered", len(reqs))
+                        self.logger.warning("storing %d events failed; batch will be redelivered", n)
                         raise
                     time.sleep(0.02 * (1 << attempt))
 
@@ -195,13 +267,20 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
 
     # ---- OutboundPayloadEnrichmentLogic -------------------------------------------
     def _process_persisted(self, recs):
+        """Enrich a poll batch of persisted events (OutboundPayloadEnrichmentLogic.java:54-92): the
+        batch's assignments and devices come from the near cache, misses in one bulk lookup each."""
         out, cmds = [], []
-        for r in recs:
-            ev = payloads.decode_persisted(r.value)
-            a = self.assignment(ev.device_assignment_id)
+        evs = [payloads.decode_persisted(r.value) for r in recs]
+        with self.assignment_lookup.time():
+            asgs = self.assignments.get_many([ev.device_assignment_id for ev in evs], self._load_assignments)
+        with self.device_lookup.time():
+            devs = self.devices.get_many([("id", a.device_id) for a in asgs.values() if a is not None],
+                                         self._load_devices_by_id)
+        for ev in evs:
+            a = asgs.get(ev.device_assignment_id)
             if a is None:
                 continue
-            dev = self.devices.get(("id", a.device_id), lambda k: self._dm().get_device(k[1]))
+            dev = devs.get(("id", a.device_id))
             ctx = {"deviceId": a.device_id, "deviceToken": dev.token if dev else None,
                    "deviceTypeId": a.device_type_id, "parentDeviceId": dev.parent_device_id if dev else None,
                    "deviceStatus": dev.status if dev else None, "deviceMetadata": dev.metadata if dev else {},

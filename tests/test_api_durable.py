@@ -297,3 +297,32 @@ def test_alternate_hash_chunks_skip_over_mixed_block_sizes(tmp_path, monkeypatch
             assert np.array_equal(np.concatenate(got), full), page
     finally:
         st.close()
+
+
+def test_retention_by_rows_bounds_the_store(tmp_path, monkeypatch):
+    """an engine tenant bounds its durable store to the rows its dedup filter still
+    holds ids for.  Whole files go, oldest first, after every group commit: the store keeps at most
+    the limit plus the file being written, and never less than the limit minus one file."""
+    monkeypatch.setenv("SW_API_FLUSH_S", "3600")
+    from sitewhere_amd.models.domain import DeviceMeasurement
+    from sitewhere_amd.persistence.segments import DurableEventStore
+    st = DurableEventStore(str(tmp_path / "s"), direct=False, rotate_bytes=64 << 10)
+    try:
+        assert st.limit_retention_rows(3000) == 3000
+        assert st.limit_retention_rows(5000) == 3000                    # only ever tightens
+        k = 0
+        for _ in range(40):
+            st.add_events([DeviceMeasurement(name="t", value=float(i), alternate_id=f"r-{k + i}",
+                                             device_assignment_id="a", device_id="d", event_date=1_000_000 + k + i)
+                           for i in range(250)])
+            k += 250
+            assert st.flush_api() == 250
+            rs = st.retention_state()
+            assert rs["retained_rows"] <= 3000 + 64 * 1024 // 8, rs
+        rs = st.retention_state()
+        assert rs["deleted_rows"] + rs["retained_rows"] == k and rs["deleted_rows"] >= k - 3000 - 8192
+        assert rs["retained_rows"] >= 3000 - 64 * 1024 // 8
+        assert st.get_event_by_alternate_id(f"r-{k - 1}") is not None            # the newest are kept
+        assert st.get_event_by_alternate_id("r-0") is None                      # the oldest are gone
+    finally:
+        st.close()
