@@ -77,6 +77,10 @@ def parse():
                     help="reader threads querying the durable store during the timed steps (list by assignment "
                          "/ area, by id, by alternate id: persistence/read_load.py); 0 = ingest only")
     ap.add_argument("--read-pause-ms", type=float, default=0.0, help="pause between one reader's queries")
+    ap.add_argument("--n-customers", type=int, default=97, help="customers of the fleet (assignment i: i %% n)")
+    ap.add_argument("--n-areas", type=int, default=31, help="areas of the fleet (assignment i: i %% n)")
+    ap.add_argument("--n-assets", type=int, default=1009, help="assets of the fleet (assignment i: i %% n; 0 = "
+                                                              "one asset per device)")
     ap.add_argument("--no-outbound", action="store_true", help="(diagnostic) skip the D2H outbound copy")
     ap.add_argument("--bus", action=argparse.BooleanOptionalAction, default=True,
                     help="GPU engine: consume raw batches from, and publish enriched batches to, commit-log "
@@ -115,14 +119,11 @@ def open_durable(args, rank, dev):
     store = DurableEventStore(seg_dir, rank=rank, rotate_bytes=1 << 30, retention_bytes=retention,
                               direct=args.direct_io)
     boot = int(time.time() * 1000)
-    if args.read_threads:
-        # the readers look up every assignment and area by token: the whole fleet's dictionary
-        from sitewhere_amd.persistence.read_load import bench_dictionary
-        asg, ctx = bench_dictionary(int(np.max(dev)) + 1)
-        store.add_dictionary(boot, asg=asg, ctx=ctx)
-    else:
-        store.add_dictionary(boot, asg={int(i): [f"asg-{int(i)}", f"dev-{int(i)}", f"cust-{int(i) % 97}",
-                                                 f"area-{int(i) % 31}", f"asset-{int(i) % 1009}"] for i in dev[:16]})
+    # the whole fleet's dictionary (assignment, device, customer, area, asset tokens; context ids): the
+    # store's events are resolvable by token, and the readers look up every assignment / context
+    from sitewhere_amd.persistence.read_load import bench_dictionary
+    asg, ctx = bench_dictionary(int(np.max(dev)) + 1, args.n_customers, args.n_areas, args.n_assets)
+    store.add_dictionary(boot, asg=asg, ctx=ctx)
     return (None if base else tmpdir), store, boot
 
 
@@ -253,7 +254,8 @@ def main():
     lo, hi = fingerprints(heap, offs)
     dev = eng.register_devices(lo, hi)
     n_dev = int(shard_mask(hi, world, rank).sum())
-    eng.set_assignments(dev, dev, customer=dev % 97, area=dev % 31, asset=dev % 1009)
+    eng.set_assignments(dev, dev, customer=dev % args.n_customers, area=dev % args.n_areas,
+                        asset=dev % args.n_assets if args.n_assets else dev)
     rng = np.random.default_rng(1234)
     zones, tests = zone_polys(args.zones, spec.lat0, spec.lon0, spec.span_deg, rng)
     eng.set_zone_rules(zones, tests)
@@ -499,7 +501,8 @@ def main():
         # the step loop every 0.2 ms rather than the default 5 ms
         sys.setswitchinterval(2e-4)
         reads = ReadLoad(dur["store"], int(np.max(dev)) + 1, threads=args.read_threads,
-                         pause_s=args.read_pause_ms / 1e3, seed=rank)
+                         pause_s=args.read_pause_ms / 1e3, seed=rank, n_area=args.n_areas,
+                         n_cust=args.n_customers, n_asset=args.n_assets or int(np.max(dev)) + 1)
     # the setup's long-lived objects (registry, dictionaries: millions with --read-threads) leave the
     # collector's view: a full collection over them would stall every thread of the process
     import gc

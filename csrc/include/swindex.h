@@ -15,8 +15,10 @@
 //    range and its SIX_HEADS newest rows with their dates (date desc, row desc): a page-1 listing
 //    merges the heads of every block instead of decoding blocks; a block is scanned only once the
 //    merge passes its last head.
-//    A dimension whose engine-wide context ids reach SIX_CTX_MAX is not indexed (high-cardinality
-//    contexts -- e.g. one asset per device -- are answered through their few assignments).
+//    A dimension whose engine-wide context ids reach SIX_CTX_MAX is not indexed: such a context (an
+//    asset per device, 10K customers) has few assignments, and its listing maps the id to them and
+//    them to pages through every block's page zone maps in one native pass (swseg_ix_asgs_pages),
+//    then scans only those pages (persistence/segments.py _ctx_via_assignments).
 //  * alternate ids: (bucket = top SIX_ALT_SORT_BITS bits of the id's 64-bit hash, row) order, a
 //    directory of the top alt_bits bits, and per id a SIX_ALT_EBITS-bit entry (hash fingerprint <<
 //    pbits | page).  A lookup reads one bucket (~16-32 entries) per block and decodes the page of a

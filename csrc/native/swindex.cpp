@@ -321,6 +321,43 @@ int64_t swseg_ix_asg_pages(const uint8_t* const* t, int64_t n, int32_t asg, int6
   return k;
 }
 
+// The pages of MANY assignments (sorted ascending, distinct) over the blocks of `t` whose mask byte is
+// set (null mask: every block): each page once, (block, page) in block order.  Blocks are clustered
+// by assignment, so an assignment's rows sit in one or two pages of a block; each page is tested with
+// one binary search over the sorted assignments: O(pages * log assignments) per block, where the per
+// assignment lookup above is O(pages) per assignment.  What routes a high-cardinality context
+// dimension (one the trailers do not index: an asset per device, 10K customers) through its
+// assignments in one call.  Returns the pages found (> cap: call again with that cap).
+int64_t swseg_ix_asgs_pages(const uint8_t* const* t, int64_t n, const int32_t* asgs, int64_t n_asg,
+                            const uint8_t* mask, int64_t d_lo, int64_t d_hi, int64_t* out_blk, int64_t* out_page,
+                            int64_t cap) {
+  int64_t k = 0;
+  if (n_asg <= 0) return 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint8_t* x = t[i];
+    if (!x || (mask && !mask[i])) continue;
+    SwIxHdr h;
+    memcpy(&h, x, sizeof(h));
+    const SwIxPage* pg = reinterpret_cast<const SwIxPage*>(x + h.off_pages);
+    for (uint32_t p = 0; p < h.n_pages; ++p) {
+      const SwIxPage& q = pg[p];
+      if (q.date_max < d_lo || q.date_min > d_hi) continue;
+      // the first wanted assignment not below the page's range (a lower bound per page: API-added
+      // blocks are not clustered, so page ranges need not ascend)
+      int64_t lo = 0, hi = n_asg;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (asgs[mid] < q.asg_min) lo = mid + 1; else hi = mid;
+      }
+      if (lo < n_asg && asgs[lo] <= q.asg_max) {     // one falls in [asg_min, asg_max]
+        if (k < cap) { out_blk[k] = i; out_page[k] = p; }
+        ++k;
+      }
+    }
+  }
+  return k;
+}
+
 void swseg_ix_ctx_find(const uint8_t* const* t, int64_t n, int32_t d, uint32_t key, int64_t* out);
 
 // swseg_ix_ctx_find with the heads gathered: out[7 i ..] as there but o[4] = index of block i's

@@ -1,7 +1,7 @@
 """Read load on a durable event store while it ingests: the REST / gRPC query mix of the reference's
-event-management API (ListMeasurementsForIndex on Assignment and Area, GetDeviceEventById,
-GetDeviceEventByAlternateId) issued from reader threads against the store the engine is writing,
-each query timed.
+event-management API (ListMeasurementsForIndex on Assignment, Area, Customer and Asset,
+GetDeviceEventById, GetDeviceEventByAlternateId) issued from reader threads against the store the
+engine is writing, each query timed.
 
 Reference: service-event-management DeviceEventManagementImpl (listDeviceMeasurementsForIndex,
 getDeviceEventById, getDeviceEventByAlternateId) over MongoDeviceEventManagement.java:129-141's
@@ -18,12 +18,16 @@ import numpy as np
 
 from ..models.domain import DateRangeSearchCriteria
 
-KINDS = ("list_assignment", "list_area", "by_id", "by_alt", "by_alt_miss")
+KINDS = ("list_assignment", "list_area", "list_customer", "list_asset", "by_id", "by_alt", "by_alt_miss")
+_LIST = {"list_assignment": ("Assignment", "asg", "n_asg"), "list_area": ("Area", "area", "n_area"),
+         "list_customer": ("Customer", "cust", "n_cust"), "list_asset": ("Asset", "asset", "n_asset")}
 
 
 def bench_dictionary(n_assignments: int, n_cust: int = 97, n_area: int = 31, n_asset: int = 1009):
-    """The dictionary of bench.py's fleet (assignment i -> device i, customer i % 97, area i % 31,
-    asset i % 1009) and the engine's context ids of those tokens."""
+    """The dictionary of bench.py's fleet (assignment i -> device i, customer i % n_cust, area
+    i % n_area, asset i % n_asset; n_asset 0: one asset per device) and the engine's context ids of
+    those tokens."""
+    n_asset = n_asset or n_assignments
     asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % n_cust}", f"area-{i % n_area}", f"asset-{i % n_asset}"]
            for i in range(n_assignments)}
     ctx = {0: {f"cust-{k}": k for k in range(n_cust)}, 1: {f"area-{k}": k for k in range(n_area)},
@@ -35,13 +39,14 @@ class ReadLoad:
     """``threads`` readers cycling through :data:`KINDS` against ``store`` until :meth:`stop`.
 
     Targets: assignments ``asg-<i>`` (i < ``n_assignments``), areas ``area-<k>`` (k < ``n_area``),
-    and stored events picked at random from the blocks already durable (their ids, then the
+    customers ``cust-<k>`` (k < ``n_cust``), assets ``asset-<k>`` (k < ``n_asset``), and stored events picked at random from the blocks already durable (their ids, then the
     alternate ids those events carry).  ``pause_s`` between queries per thread (0: back to back)."""
 
     def __init__(self, store, n_assignments: int, n_area: int = 31, threads: int = 2, pause_s: float = 0.0,
-                 page_size: int = 100, seed: int = 7):
+                 page_size: int = 100, seed: int = 7, n_cust: int = 97, n_asset: int = 1009):
         self.store = store
         self.n_asg, self.n_area = int(n_assignments), int(n_area)
+        self.n_cust, self.n_asset = int(n_cust), int(n_asset or n_assignments)
         self.threads, self.pause_s, self.page_size = int(threads), float(pause_s), int(page_size)
         self.seed = seed
         self.lat = {k: [] for k in KINDS}
@@ -64,9 +69,9 @@ class ReadLoad:
     def _one(self, kind: str, rng):
         st = self.store
         crit = DateRangeSearchCriteria(page_size=self.page_size)
-        if kind in ("list_assignment", "list_area"):
-            ix, ent = ("Assignment", f"asg-{int(rng.integers(0, self.n_asg))}") if kind == "list_assignment" else \
-                ("Area", f"area-{int(rng.integers(0, self.n_area))}")
+        if kind in _LIST:
+            ix, prefix, n = _LIST[kind]
+            ent = f"{prefix}-{int(rng.integers(0, getattr(self, n)))}"
             t = time.perf_counter()
             r = st.list_events("Measurement", ix, [ent], crit)
             dt = time.perf_counter() - t

@@ -1816,6 +1816,26 @@ class DurableEventStore(DeviceEventStore):
             return None
         return arr[pos - 2, :self._asg_n.get(boot, 0)]
 
+    def _ctx_via_assignments(self, t, ctx_tab, cid: int, mask, et, d_lo, d_hi):
+        """(block position, row, date) of context id ``cid`` in the masked blocks, found through its
+        assignments: one native pass maps them to the pages their zone maps admit
+        (``swseg_ix_asgs_pages``), one native scan of those pages' leading columns keeps the rows of
+        the id (the reference's Mongo (asset | customer, type, date) index at any cardinality,
+        MongoDeviceEventManagement.java:132-140)."""
+        asgs = np.ascontiguousarray(np.nonzero(ctx_tab == cid)[0], np.int32)
+        if not len(asgs):
+            return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
+        m = np.ascontiguousarray(mask, np.uint8)
+        cap = max(1024, 4 * len(asgs))
+        while True:
+            bo, po = np.empty(cap, np.int64), np.empty(cap, np.int64)
+            k = int(native().swseg_ix_asgs_pages(t["addr"], t["n"], _p(asgs), len(asgs), _p(m), int(d_lo), int(d_hi),
+                                                 _p(bo), _p(po), cap))
+            if k <= cap:
+                break
+            cap = k
+        return self._scan_pages(t, bo[:k], po[:k], et, d_lo, d_hi, ctx_tab=ctx_tab, ctx_id=cid)
+
     def _list_context(self, t, boot, pos, want, et, d_lo, d_hi, need) -> tuple[int, list]:
         """Rows of customer / area / asset ids over one boot's blocks, from the trailers' key tables:
         exact totals from the per-key counts (a block straddling a date bound is scanned for its
@@ -1850,7 +1870,14 @@ class DurableEventStore(DeviceEventStore):
             st, cnt, dmin, dmax, h0, nh = o[:, 0], o[:, 1], o[:, 2], o[:, 3], o[:, 4], o[:, 5]
             outside = (dmax < d_lo) | (dmin > d_hi)
             straddle = bounded & ~outside & ~((d_lo <= dmin) & (dmax <= d_hi))
-            to_scan = (st < 0) | ((st > 0) & straddle)     # not indexed here / straddles a bound
+            # blocks that do not index this dimension (its context ids passed SIX_CTX_MAX: an asset
+            # per device, 10K customers): through the id's assignments and their pages' zone maps
+            notix = (st < 0) & np.fromiter((tr is not None for tr in t["tr"]), bool, n)
+            if notix.any():
+                b, r, dt = self._ctx_via_assignments(t, ctx_tab, int(cid), notix, et, d_lo, d_hi)
+                total += len(r)
+                heads.append((b, r, dt))
+            to_scan = ((st < 0) & ~notix) | ((st > 0) & straddle)   # no trailer / straddles a bound
             for bi in np.nonzero(to_scan)[0].tolist():
                 scan.setdefault(bi, set()).add(int(cid))
             use = (st > 0) & ~to_scan & ~outside

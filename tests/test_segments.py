@@ -366,14 +366,17 @@ def test_failed_append_is_retried_not_skipped_as_a_replay(tmp_path):
     es.close()
 
 
-def _ctx_store_blocks(tmp_path, n_blocks=5, rows_per=3000, dates="random", n_asg=40, trailers=True, seed=3):
-    """A store of engine-like blocks: assignment contexts with engine ids (customer i % 3, area i % 2,
-    asset i % 5), trailers built with that context table, dictionaries with the context ids."""
+def _ctx_store_blocks(tmp_path, n_blocks=5, rows_per=3000, dates="random", n_asg=40, trailers=True, seed=3,
+                      n_cust=3, n_area=2, n_asset=5):
+    """A store of engine-like blocks: assignment contexts with engine ids (customer i % n_cust, area
+    i % n_area, asset i % n_asset), trailers built with that context table, dictionaries with the
+    context ids."""
     es = sg.DurableEventStore(str(tmp_path / "es"), direct=False)
-    asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % 3}", f"area-{i % 2}", f"asset-{i % 5}"] for i in range(n_asg)}
-    ctx_tab = np.array([[i, i % 3, i % 2, i % 5] for i in range(n_asg)], np.int32)
-    ctx = {0: {f"cust-{k}": k for k in range(3)}, 1: {f"area-{k}": k for k in range(2)},
-           2: {f"asset-{k}": k for k in range(5)}}
+    asg = {i: [f"asg-{i}", f"dev-{i}", f"cust-{i % n_cust}", f"area-{i % n_area}", f"asset-{i % n_asset}"]
+           for i in range(n_asg)}
+    ctx_tab = np.array([[i, i % n_cust, i % n_area, i % n_asset] for i in range(n_asg)], np.int32)
+    ctx = {0: {f"cust-{k}": k for k in range(n_cust)}, 1: {f"area-{k}": k for k in range(n_area)},
+           2: {f"asset-{k}": k for k in range(n_asset)}}
     names = {i: f"mx.metric{i}" for i in range(20)}
     blocks, exp_all, n0 = [], [], 0
     rng = np.random.default_rng(seed)
@@ -603,4 +606,30 @@ def test_read_lease_defers_reclaiming_copies(tmp_path):
         es.seg.mem_caps(-1, 0)                           # drop every scan image
         assert (es.seg.index_tr()[3] == 0).all()
         assert np.array_equal(np.ctypeslib.as_array((ctypes.c_uint8 * 4096).from_address(b0)), before)
+    es.close()
+
+
+def test_high_cardinality_dimensions_route_through_assignments(tmp_path):
+    """dimensions whose context ids pass SIX_CTX_MAX (an asset per device, 10K
+    customers) are not in the trailers' key tables; their listings go through the id's assignments
+    (one native pass over every block's page zone maps, one scan of those pages) and answer exactly
+    like decoding every block -- totals, order, paging, date ranges."""
+    from sitewhere_amd.models.domain import DateRangeSearchCriteria
+    es, asg, blocks, _ = _ctx_store_blocks(tmp_path, n_blocks=4, rows_per=20000, dates="increasing",
+                                           n_asg=20000, n_cust=10000, n_area=31, n_asset=20000)
+    t0 = 1_700_000_000_000
+    crits = [DateRangeSearchCriteria(page_size=0), DateRangeSearchCriteria(page_size=100),
+             DateRangeSearchCriteria(page_number=2, page_size=3),
+             DateRangeSearchCriteria(page_size=10, start_date=t0 + 1_000_000, end_date=t0 + 2_500_000)]
+    n = 0
+    for t in ("Measurement", "Location"):
+        for ix, ents in (("Asset", ["asset-17"]), ("Asset", ["asset-5", "asset-19999"]), ("Customer", ["cust-42"]),
+                         ("Customer", ["cust-9999", "cust-3"]), ("Area", ["area-4"]), ("Asset", ["asset-none"])):
+            for c in crits:
+                r = es.list_events(t, ix, ents, c)
+                got = (r.num_results, [(e.id, e.event_date) for e in r.results])
+                want = _brute(blocks, asg, t, ix, set(ents), c)
+                assert got == want, (t, ix, ents, c)
+                n += want[0]
+    assert n > 50
     es.close()
