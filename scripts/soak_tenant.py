@@ -40,8 +40,8 @@ def main():
     ap.add_argument("--devices", type=int, default=1 << 20)
     ap.add_argument("--template", default="gpu-columnar-1m")
     ap.add_argument("--batch", type=int, default=1 << 20, help="payloads per raw record")
-    ap.add_argument("--records", type=int, default=8, help="pinned raw records the producer cycles through")
-    ap.add_argument("--ahead", type=int, default=4, help="records published ahead of the tenant's commits")
+    ap.add_argument("--records", type=int, default=16, help="pinned raw records the producer cycles through")
+    ap.add_argument("--ahead", type=int, default=12, help="records published ahead of the tenant's commits")
     ap.add_argument("--phases", type=int, default=3)
     ap.add_argument("--phase-s", type=float, default=70.0)
     ap.add_argument("--p-unregistered", type=float, default=0.005)
@@ -97,6 +97,8 @@ def main():
     ib = sw.tenant_engine("inbound-processing", "soak")
     while ib.engine.n_assignments < args.devices and time.time() - t_setup < 3600:
         time.sleep(0.2)
+    while ib.dictionary_pending() >= ib.PRIME_DICTIONARY_MIN and time.time() - t_setup < 3600:
+        time.sleep(0.2)                         # the imported fleet's dictionary reaches the store
     log(f"engine registry: {ib.engine.n_devices} devices, {ib.engine.n_assignments} assignments")
     ecfg = ib.engine.cfg
     store = sw.tenant_engine("event-management", "soak").store
@@ -112,6 +114,9 @@ def main():
         r = RawBatchRecord(raw[:int(offs[-1])], varint_lengths(offs), len(offs) - 1, pinned=pin)
         recs.append(r)
         pos.append(alt_positions(r.ptr + VALUE_HDR, offs))
+    import gc
+    gc.collect()
+    gc.freeze()                                 # the fleet's objects leave the cyclic collector
     setup_s = time.time() - t_setup
     log(f"setup {setup_s:.0f} s")
     bus = sw.instance.bus
@@ -206,6 +211,12 @@ def main():
               "store_rows_before": rows0, "store_rows_after": store.rows}
     # events of registered devices (the replay's unregistered payloads are routed, not deduplicated)
     replay["events_of_registered_devices"] = valid_alt - (st1["unregistered"] - st0["unregistered"])
+    # diagnostics: the store's own answer for the replayed ids (indexed blocks, and every block)
+    hs = dec["alt_hash"][(dec["alt_hash"] != 0) & (dec["etype"] < 16)]
+    f_ix = store.find_alternate_hashes(hs.tolist(), indexed_only=True)
+    f_all = store.find_alternate_hashes(hs.tolist(), indexed_only=False)
+    replay["store_finds_indexed"], replay["store_finds_all"] = len(f_ix), len(f_all)
+    replay["store_blocks"] = store.index_stats()
     replay["all_duplicates"] = (replay["settled_duplicates"] + replay["window_duplicates"]
                                 == replay["events_of_registered_devices"] and replay["persisted_by_engine"] == 0
                                 and replay["store_rows_after"] == replay["store_rows_before"])

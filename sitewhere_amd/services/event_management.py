@@ -217,6 +217,16 @@ class DeviceEventManagement:
         f = getattr(self.store, "dictionary", None)
         return f(boot, asg_ids, name_ids) if f is not None else {"asg": {}, "names": {}, "rules": {}}
 
+    def add_durable_dictionary(self, boot, asg: dict | None = None, names: dict | None = None,
+                               rules: dict | None = None, ctx: dict | None = None) -> bool:
+        """Dictionary entries of an engine incarnation ahead of its blocks (an engine tenant with a
+        large registry sends them once at start instead of inside its first block's delta)."""
+        f = getattr(self.store, "add_dictionary", None)
+        if f is None:
+            return False
+        f(boot, asg=asg, names=names, rules=rules, ctx=ctx)
+        return True
+
     def durable_alternate_hashes(self, max_ids: int = 1 << 24, skip: int = 0) -> bytes:
         """Alternate-id hashes of the durable store, newest first (u64 little endian): ids ``skip`` to
         ``skip + max_ids`` of that order -- an engine tenant seeds its store-backed dedup filter with

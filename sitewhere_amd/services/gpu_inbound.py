@@ -385,15 +385,18 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
             elif kind.startswith("zone."):
                 self._load_zones()
         flush()
+        if self._store_thread is not None or self.storage == "durable":
+            self._prime_dictionary()            # a bulk import: its dictionary ahead of the blocks
 
     # ---------------------------------------------------------------- lifecycle
     def tenant_start(self, monitor):
         self.restore_checkpoint()
         self.load_model()
-        if self.config.get("tuneGc", False):
-            tune_gc_for_streaming()             # opt-in: measured gain is within run-to-run noise
         super().tenant_start(monitor)           # model-update, decoded and persisted consumers
         self._resume_from_store()
+        self._prime_dictionary()
+        if self.config.get("tuneGc", False):
+            tune_gc_for_streaming()             # after the registry and dictionary are built
         self.check_dedup_sizing()
         bus = self.ms.instance.bus
         if self.config.get("rawBackpressure", True) and hasattr(bus, "protect"):
@@ -919,6 +922,33 @@ class GpuInboundTenantEngine(InboundProcessingTenantEngine):
         rules = {t.alert_type: t.alert_message for t in self.engine.tests}
         self._ctx_delta = ctx
         return asg, names, rules
+
+    # registries at least this large send their dictionary at start (see _prime_dictionary)
+    PRIME_DICTIONARY_MIN = 65536
+
+    def _prime_dictionary(self):
+        """Durable storage with a large registry: the assignment contexts go to the event store once,
+        at start, before any block (one dictionary record) -- inside the first block's delta, a 1M-
+        assignment tenant's first step carried a ~100 MB dictionary and stalled ingest for ~18 s
+        (profiles/r6_soak).  Enriched-batch consumers resolve entries they never saw a delta for from
+        the store (``EnrichedBatchReader._resolve``)."""
+        if self.storage != "durable" or len(self._asg_dirty) < self.PRIME_DICTIONARY_MIN:
+            return
+        em = self._em()
+        if not hasattr(em, "add_durable_dictionary"):
+            return
+        t0 = time.perf_counter()
+        with self._lock:        # no block is encoded between taking the entries and storing them
+            asg, names, rules = self._dict_deltas()
+            em.add_durable_dictionary(self.block_boot, asg=asg, names=names, rules=rules,
+                                      ctx=self._ctx_delta or None)
+            self._ctx_delta = None
+        self.logger.info("dictionary of %d assignments sent to the event store in %.1f s", len(asg),
+                         time.perf_counter() - t0)
+
+    def dictionary_pending(self) -> int:
+        """Assignment contexts not yet sent to the event store."""
+        return len(self._asg_dirty)
 
     def durable_payload(self, res, key=None, tr: list | None = None):
         """The step's sealed block + dictionary deltas (``segments.encode_durable_batch``), framed in

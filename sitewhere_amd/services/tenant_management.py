@@ -132,6 +132,9 @@ TENANT_TEMPLATES["gpu-columnar-1m"]["name"] = "MI355X pipeline, columnar event s
 TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["inbound-processing"]["capacity"].update(
     max_msgs=1 << 20, max_devices=(1 << 20) + 65536, max_assignments=(1 << 20) + 65536, store_cap=1 << 23,
     gen_cap=1 << 19, state_slots=1 << 24, dedup_filter_ids=(1 << 29) - (1 << 22))
+# a million devices and assignments live in the process: keep them out of the cyclic GC (a full
+# collection over them paused ingest for seconds every ~45 s, profiles/r6_soak)
+TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["inbound-processing"]["tuneGc"] = True
 TENANT_TEMPLATES["gpu-columnar-1m"]["services"]["event-sources"].update(rawBatchSize=1 << 20)
 # volatile variant (benchmarks of the pipeline alone): rows kept in host memory, newest 2^28 held
 TENANT_TEMPLATES["gpu-memory"] = copy.deepcopy(TENANT_TEMPLATES["gpu-columnar"])
