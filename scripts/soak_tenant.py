@@ -216,6 +216,24 @@ def main():
     f_ix = store.find_alternate_hashes(hs.tolist(), indexed_only=True)
     f_all = store.find_alternate_hashes(hs.tolist(), indexed_only=False)
     replay["store_finds_indexed"], replay["store_finds_all"] = len(f_ix), len(f_all)
+    # the stored id strings themselves (every block's id column decoded, newest first): are the
+    # replayed ids in the store at all, or only missing from the trailers' lookups?
+    want = set(int(x) for x in hs.tolist())
+    in_cols, scanned = set(), 0
+    for chunk in store.alternate_hash_chunks(max_ids=int(os.environ.get("SOAK_SCAN_IDS", 1 << 30))):
+        scanned += len(chunk)
+        in_cols |= want & set(np.intersect1d(chunk, hs).tolist())
+        if len(in_cols) == len(want):
+            break
+    replay["store_decoded_has"], replay["store_decoded_scanned"] = len(in_cols), scanned
+    miss = sorted(want - set(int(k) for k in f_ix))
+    replay["missing_in_decoded"] = len(set(miss) - in_cols)
+    if miss:
+        # where the missing ids sit in the replayed sub-batch (payload index, device, event type)
+        idx = np.nonzero(np.isin(dec["alt_hash"], np.array(miss[:2000], np.uint64)))[0]
+        replay["missing_payload_idx_sample"] = idx[:40].tolist()
+        replay["missing_etypes"] = np.bincount(dec["etype"][idx].astype(np.int64), minlength=4).tolist()
+        replay["missing_first_last"] = [int(idx.min()), int(idx.max())] if len(idx) else None
     replay["store_blocks"] = store.index_stats()
     replay["all_duplicates"] = (replay["settled_duplicates"] + replay["window_duplicates"]
                                 == replay["events_of_registered_devices"] and replay["persisted_by_engine"] == 0

@@ -27,7 +27,8 @@ CSRC = ROOT / "csrc"
 GPU_ARCH = os.environ.get("SW_GPU_ARCH", "gfx950")
 
 _NATIVE_SRC = [CSRC / "native" / "swnative.cpp", CSRC / "native" / "swcpuengine.cpp", CSRC / "native" / "swseg.cpp",
-               CSRC / "native" / "swindex.cpp", CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp", CSRC / "native" / "swjson.cpp"]
+               CSRC / "native" / "swindex.cpp", CSRC / "native" / "swroute.cpp", CSRC / "native" / "swsandbox.cpp", CSRC / "native" / "swjson.cpp",
+               CSRC / "native" / "swrowjson.cpp"]
 _GPU_SRC = [CSRC / "hip" / "swgpu.hip", CSRC / "hip" / "swseg.hip", CSRC / "hip" / "swindex.hip"]
 _HEADERS = sorted((CSRC / "include").glob("*.h"))
 
@@ -219,6 +220,12 @@ def native():
         _proto(lib, "swss_durable", c_int64, P)
         _proto(lib, "swss_error", c_int32, P)
         _proto(lib, "swss_wait", c_int32, P, c_int64, c_int64)
+        _proto(lib, "swjson_rows", c_int64, P, c_int64, P, P, P, P, P, P, P, P, P, P, P,
+               c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, P, P, P, c_int64, P, P, P, c_int64, P, P, P,
+               P, c_int64, P, c_int64, P, P, c_int64, P, P)
+        _proto(lib, "swjson_select_block", c_int64, P, c_int32, P, c_int64, c_int32, P, c_int64, P, P, P, P, P, P,
+               c_int64, P, P, P, P, c_int64, c_int32, P, c_int64, P, P, c_int64, P, P, P, c_int64)
+        _proto(lib, "swmqtt_publish_qos0", c_int64, P, P, P, P, c_int64, ctypes.c_uint8, P, c_int64)
         _proto(lib, "swss_stats", None, P, P)
         _proto(lib, "swss_set_retention", None, P, c_int64, c_int64, c_int64)
         _proto(lib, "swss_close", None, P)

@@ -416,6 +416,10 @@ class MqttClient:
             if not w.wait(max(0.0, end - time.monotonic())):
                 raise TimeoutError("PUBACK not received" if qos == 1 else "PUBCOMP not received")
 
+    def publish_framed_qos0(self, packets):
+        """Already framed QoS 0 PUBLISH packets (``swmqtt_publish_qos0``), in one write."""
+        self._send(bytes(packets) if not isinstance(packets, (bytes, bytearray)) else packets)
+
     @property
     def inflight(self) -> int:
         return len(self._out)

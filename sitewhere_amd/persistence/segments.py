@@ -1208,16 +1208,22 @@ class DurableEventStore(DeviceEventStore):
             m = boots == b
             lst, ta, tl, ba = ents[m], taddr[m], tlen[m], baddr[m]
             old = prev.get(b)
-            k = 0
-            if old is not None and old["n"] <= len(lst):
-                # appends (the common case while ingesting): keep the blocks already resolved
-                k = old["n"]
-                if k and not (np.array_equal(old["ents"]["first_seq"], lst["first_seq"][:k])
-                              and np.array_equal(old["ents"]["rank"], lst["rank"][:k])):
-                    k = 0
-            removed |= old is not None and k < old["n"]
-            trs = list(old["tr"][:k]) if k else []
-            for i in np.nonzero(ta[:k] != old["taddr"][:k])[0].tolist() if k else []:
+            k, j = 0, 0
+            if old is not None and old["n"] and len(lst):
+                # appends, and retention dropping the oldest files (the steady state of a store
+                # bounded by rows: both at once, every few commits): keep the blocks already resolved
+                # -- the old list's blocks from the new first one on, if they are the new list's prefix
+                of, orank = old["ents"]["first_seq"], old["ents"]["rank"]
+                hit = np.nonzero((of == lst["first_seq"][0]) & (orank == lst["rank"][0]))[0]
+                if len(hit):
+                    j = int(hit[0])
+                    k = old["n"] - j
+                    if k > len(lst) or not (np.array_equal(of[j:], lst["first_seq"][:k])
+                                            and np.array_equal(orank[j:], lst["rank"][:k])):
+                        k, j = 0, 0
+            removed |= old is not None and (j > 0 or k < old["n"])
+            trs = list(old["tr"][j:j + k]) if k else []
+            for i in np.nonzero(ta[:k] != old["taddr"][j:j + k])[0].tolist() if k else []:
                 trs[i] = self._trailer_mem(ta[i], tl[i], lst[i]) if ta[i] else self._trailer(lst[i])
             trs += [self._trailer_mem(ta[i], tl[i], lst[i]) if ta[i] else self._trailer(lst[i])
                     for i in range(k, len(lst))]

@@ -48,6 +48,7 @@ class EnrichedBatchReader:
         self._lock = threading.Lock()
         self._masks: dict = {}                    # (boot, field, value) -> (bool per assignment, dictionary version)
         self._ver: dict[int, int] = {}            # boot -> version: bumped by every assignment delta applied
+        self._tabs: dict = {}                     # boot -> (version, native string tables) for outbound JSON
         self.rows = self.batches = self.resolved = 0
 
     # ------------------------------------------------------------------ dictionaries
@@ -105,13 +106,9 @@ class EnrichedBatchReader:
         self.rows += len(cols["date"])
         return cols
 
-    def attr_mask(self, cols: dict, pos: int, value) -> np.ndarray:
-        """bool per row of ``cols``: does the row's assignment context field ``pos`` (0 assignment,
-        1 device, 2 customer, 3 area, 4 asset, 5 device token, 6 device type) equal ``value``?  The
-        per-assignment answer is cached for the batch's engine incarnation and rebuilt only when an
-        assignment delta was applied since (new entries or changed ones) -- a filter costs one gather
-        per batch, not a Python call per row."""
-        boot = int(cols["header"]["boot"])
+    def asg_mask(self, boot: int, pos: int, value) -> np.ndarray:
+        """bool per assignment index of the incarnation ``boot``: does its context field ``pos`` equal
+        ``value``?  Cached until an assignment delta is applied (see :meth:`attr_mask`)."""
         key = (boot, pos, value)
         with self._lock:
             a = self._asg.get(boot, {})
@@ -124,11 +121,165 @@ class EnrichedBatchReader:
                     if len(ctx) > pos and ctx[pos] == value:
                         m[i] = True
                 self._masks[key] = (m, ver)
+        return m
+
+    def attr_mask(self, cols: dict, pos: int, value) -> np.ndarray:
+        """bool per row of ``cols``: does the row's assignment context field ``pos`` (0 assignment,
+        1 device, 2 customer, 3 area, 4 asset, 5 device token, 6 device type) equal ``value``?  The
+        per-assignment answer is cached for the batch's engine incarnation and rebuilt only when an
+        assignment delta was applied since (new entries or changed ones) -- a filter costs one gather
+        per batch, not a Python call per row."""
+        m = self.asg_mask(int(cols["header"]["boot"]), pos, value)
         asg = np.asarray(cols["asg"], np.int64)
         ok = (asg >= 0) & (asg < len(m))
         out = np.zeros(len(asg), bool)
         out[ok] = m[asg[ok]]
         return out
+
+    # ------------------------------------------------------------------ native outbound JSON
+    @staticmethod
+    def _strtab(entries, n: int):
+        """(heap, offsets [n + 1], presence [n]) of n optional strings (``entries``: index -> str)."""
+        present = np.zeros(max(n, 1), np.uint8)
+        parts, lens = [], np.zeros(max(n, 1), np.int64)
+        for k, v in entries:
+            if 0 <= k < n and v is not None:
+                b_ = v.encode() if isinstance(v, str) else bytes(v)
+                parts.append((k, b_))
+                present[k] = 1
+                lens[k] = len(b_)
+        off = np.zeros(max(n, 1) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        heap = np.zeros(max(int(off[-1]), 8), np.uint8)
+        for k, b_ in parts:
+            heap[off[k]:off[k] + len(b_)] = np.frombuffer(b_, np.uint8)
+        return heap, off, present
+
+    def _tables(self, boot: int):
+        """The boot's dictionaries as native string tables, rebuilt when a delta was applied."""
+        with self._lock:
+            ver = (self._ver.get(boot, 0), len(self._names.get(boot, {})), len(self._rules))
+            t = self._tabs.get(boot)
+            if t is not None and t[0] == ver:
+                return t[1]
+            a = self._asg.get(boot, {})
+            n_asg = (max(a) + 1) if a else 0
+            asg = self._strtab(((7 * i + k, (ctx[k] if k < len(ctx) else None)) for i, ctx in a.items()
+                                for k in range(7)), 7 * n_asg)
+            nm = self._names.get(boot, {})
+            n_names = (max(nm) + 1) if nm else 0
+            names = self._strtab(nm.items(), n_names)
+            rules = self._strtab(((i, self._rules.get(v)) for i, v in nm.items() if v in self._rules), n_names)
+            known = np.zeros(max(n_asg, 1), np.uint8)
+            if a:
+                known[np.fromiter(a.keys(), np.int64, len(a))] = 1
+            tabs = (n_asg, asg, n_names, names, rules, known)
+            self._tabs[boot] = (ver, tabs)
+            return tabs
+
+    def outbound_json(self, cols: dict, rows, topic: str | None = None):
+        """Rows of a decoded batch as the outbound connectors' JSON documents ({"event", "context"},
+        exactly ``json.dumps(event_json(event, context))``), written natively (``swjson_rows``): (payload
+        bytes, offsets [n + 1], topic bytes, offsets) -- topics from ``topic`` (a template whose
+        ``{deviceToken}`` / ``{eventType}`` are filled per row; None: no topics).  Rows the native
+        writer does not handle (API-added JSON rows) come back as None for the Python path."""
+        from .._native import native
+        rows = np.ascontiguousarray(rows, np.int64)
+        n = len(rows)
+        if not n:
+            return b"", np.zeros(1, np.int64), b"", np.zeros(1, np.int64)
+        if cols.get("str_off") is None:
+            raise ValueError("outbound JSON needs the batch's strings (columns(strings=True))")
+        h = cols["header"]
+        boot = int(h["boot"])
+        n_asg, (ah, ao, ap), n_names, (nh, no, npr), (rh, ro, rp), _ = self._tables(boot)
+        tpl = b""
+        if topic is not None:
+            tpl = topic.replace("{deviceToken}", "\x01").replace("{eventType}", "\x02").encode()
+        P = lambda a: a.ctypes.data  # noqa: E731
+        c = {k: np.ascontiguousarray(cols[k]) for k in ("etype", "level", "date", "asg", "name", "v0", "v1", "v2", "flags")}
+        heap, soff = np.ascontiguousarray(cols["str_heap"]), np.ascontiguousarray(cols["str_off"], np.int64)
+        cap, tcap = 480 * n + 4096, (len(tpl) + 96) * n + 64
+        tb = np.frombuffer(tpl + b"\0", np.uint8)
+        for _ in range(2):
+            out, ooff = np.empty(cap, np.uint8), np.empty(n + 1, np.int64)
+            tout, toff = np.empty(tcap, np.uint8), np.empty(n + 1, np.int64)
+            k = int(native().swjson_rows(P(rows), n, *(P(c[x]) for x in ("etype", "level", "date", "asg", "name", "v0",
+                                                                          "v1", "v2", "flags")), P(heap), P(soff),
+                                         boot, int(h["first_seq"]), int(h["world"]), int(h["rank"]), int(h["recv_ms"]),
+                                         int(cols.get("row0", 0)), P(ah), P(ao), P(ap), n_asg, P(nh), P(no), P(npr),
+                                         n_names, P(rh), P(ro), P(rp), P(tb), len(tpl), P(out), cap, P(ooff),
+                                         P(tout) if topic is not None else None, tcap, P(toff), None))
+            if k >= 0:
+                return (out[:k], ooff, tout[:int(toff[-1])] if topic is not None else b"",
+                        toff if topic is not None else None)
+            if -k - 1 < n:                    # row -k - 1 is not for the native writer
+                return None
+            need = -k - 1 - n                 # a buffer was too small: once more, sized
+            cap, tcap = max(cap, need + 4096), max(tcap, need + 4096)
+        return None
+
+    def select_json(self, value, selector, topic: str | None = None, threads: int = 1):
+        """A durable batch record's rows that pass ``selector(boot) -> (event-type bit mask, keep per
+        assignment index or None, keep for indexes beyond it)`` as :meth:`outbound_json` documents,
+        straight from the block (``swjson_select_block``: event type and assignment are read from the
+        packed columns, only kept rows are decoded; pages on ``threads`` threads): (payload bytes,
+        offsets, topic bytes, offsets, kept rows, block rows), or None where the record needs the
+        decoded path (not a durable block, or rows the native writer leaves to Python).  Dictionary
+        entries the consumer has not seen are resolved from event management, as :meth:`columns`."""
+        from .._native import native
+        buf = memoryview(value).cast("B") if not isinstance(value, (bytes, bytearray)) else value
+        if bytes(buf[:4]) != b"SWD1":
+            return None
+        d, blk = sg.decode_durable_batch(value)
+        blk = np.ascontiguousarray(blk)
+        if isinstance(value, (bytes, bytearray)):
+            rc = sg.verify(blk)
+            if rc:
+                raise ValueError(f"corrupt event block (code {rc})")
+        boot = int(sg.header(blk)["boot"])
+        self._apply(boot, d)
+        tpl = b""
+        if topic is not None:
+            tpl = topic.replace("{deviceToken}", "\x01").replace("{eventType}", "\x02").encode()
+        tb = np.frombuffer(tpl + b"\0", np.uint8)
+        P = lambda a: a.ctypes.data  # noqa: E731
+        n_rows = int(sg.header(blk)["n_rows"])
+        cap, tcap = 480 * n_rows + 4096, (len(tpl) + 96) * n_rows + 64
+        counts, miss = np.zeros(3, np.int64), np.zeros(1 << 16, np.int64)
+        for _ in range(4):
+            etmask, keep, keep_default = selector(boot)
+            n_keep = len(keep) if keep is not None else 0
+            keep = np.ascontiguousarray(keep if keep is not None else np.zeros(1, bool), np.uint8)
+            n_asg, (ah, ao, ap), n_names, (nh, no, npr), (rh, ro, rp), known = self._tables(boot)
+            out, ooff = np.empty(cap, np.uint8), np.empty(n_rows + 1, np.int64)
+            tout, toff = np.empty(tcap, np.uint8), np.empty(n_rows + 1, np.int64)
+            k = int(native().swjson_select_block(P(blk), int(etmask), P(keep), n_keep, int(bool(keep_default)), P(known),
+                                                 n_asg, P(ah), P(ao), P(ap), P(nh), P(no), P(npr), n_names, P(rh),
+                                                 P(ro), P(rp), P(tb), len(tpl), int(threads), P(out), cap, P(ooff),
+                                                 P(tout) if topic is not None else None, tcap, P(toff), P(counts),
+                                                 P(miss), len(miss)))
+            if k >= 0:
+                kept = int(counts[0])
+                self.batches += 1
+                self.rows += int(counts[1])
+                return (out[:k], ooff[:kept + 1], tout[:int(toff[kept])] if topic is not None else b"",
+                        toff[:kept + 1] if topic is not None else None, kept, int(counts[1]))
+            if k == -(1 << 42):
+                m = miss[:int(counts[2])]
+                self._resolve(boot, m[m >= 0], -1 - m[m < 0])
+                with self._lock:                # entries the store does not hold either: no context
+                    a = self._asg.setdefault(boot, {})
+                    gone = [int(x) for x in m[m >= 0] if int(x) not in a]
+                    if gone:
+                        a.update({x: [] for x in gone})
+                        self._ver[boot] = self._ver.get(boot, 0) + 1
+                continue
+            if k > -(1 << 40):                  # a buffer too small
+                cap = tcap = max(cap, tcap, -k + 4096)
+                continue
+            return None
+        return None
 
     def name_ids(self, cols: dict, name: str) -> list[int]:
         """The batch incarnation's name ids of ``name`` (measurement name / alert type)."""

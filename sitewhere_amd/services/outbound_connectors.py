@@ -150,6 +150,97 @@ class MqttConnector(OutboundConnector):
             self.client.publish_many([(self._topic(ev, ctx), json.dumps(event_json(ev, ctx)).encode())
                                       for ev, ctx in items[i:i + 1024]], qos=self.qos)
 
+    # rows per native delivery job (JSON + framing of one job hold no interpreter lock)
+    NATIVE_CHUNK = 16384
+
+    def process_records(self, reader, recs):
+        """Engine batches at QoS 0 behind column filters, natively: the kept rows of a decoded block
+        are written as the same JSON documents (``EnrichedBatchReader.outbound_json``, byte for byte
+        ``json.dumps(event_json(...))``) with their topics, framed as PUBLISH packets and sent in one
+        write per block -- blocks on the delivery pool, no event object per row.  A durable block is
+        selected natively (``select_json``: unselected rows are never decoded); a columnar batch is
+        decoded and filtered on its columns.  Anything else (per-event records, QoS 1 / 2, script
+        filters) takes the generic path."""
+        from .enriched_batches import is_batch
+        if self.qos != 0 or self.client is None or any(not hasattr(f, "select") for f in self.filters):
+            return super().process_records(reader, recs)
+        batches = [r for r in recs if is_batch(r.value)]
+        single = [r for r in recs if not is_batch(r.value)]
+        if single:
+            super().process_records(reader, single)
+        if not batches:
+            return
+        tpl = self.topic.replace("{tenant}", str(self.tenant_engine.tenant.token))
+        selector = combined_selector(self.filters, reader)
+
+        def frame(buf, off, tbuf, toff, n):
+            from .._native import native
+            tb = np.frombuffer(bytes(tbuf), np.uint8) if len(tbuf) else np.zeros(1, np.uint8)
+            cap = len(buf) + len(tbuf) + 8 * n + 64
+            out = np.empty(cap, np.uint8)
+            k = int(native().swmqtt_publish_qos0(tb.ctypes.data, toff.ctypes.data, buf.ctypes.data, off.ctypes.data,
+                                                 n, 0, out.ctypes.data, cap))
+            self.client.publish_framed_qos0(memoryview(out[:k]))
+
+        def send_block(r):
+            """A durable block: selection + JSON in one native pass, unselected rows never decoded."""
+            got = reader.select_json(r.value, selector, topic=tpl)
+            if got is None:
+                return None
+            buf, off, tbuf, toff, kept, total = got
+            if kept:
+                frame(buf, off, tbuf, toff, kept)
+            with self._count_lock:
+                self.filtered += total - kept
+            return kept
+
+        done, rest = 0, []
+        if self._pool is None or len(batches) < 2:
+            for r in batches:
+                k = send_block(r)
+                if k is None:
+                    rest.append(r)
+                else:
+                    done += k
+        else:
+            futs = [(r, self._pool.submit(send_block, r)) for r in batches]
+            for r, f in futs:
+                k = f.result()
+                if k is None:
+                    rest.append(r)
+                else:
+                    done += k
+        jobs = []
+        for r in rest:
+            cols = reader.columns(r.value)
+            n = len(cols["date"])
+            excl = np.zeros(n, bool)
+            for f in self.filters:
+                m = f.exclude(cols, reader)
+                if m is not None:
+                    excl |= m
+            rows = np.nonzero(~excl)[0]
+            self.filtered += n - len(rows)
+            for i in range(0, len(rows), self.NATIVE_CHUNK):
+                jobs.append((cols, rows[i:i + self.NATIVE_CHUNK]))
+
+        def send(job):
+            cols, rows = job
+            got = reader.outbound_json(cols, rows, topic=tpl)
+            if got is None:                       # a row the native writer leaves to Python
+                self.deliver([(reader.event(cols, int(i)), reader.context(cols, int(i))) for i in rows])
+                return len(rows)
+            buf, off, tbuf, toff = got
+            frame(buf, off, tbuf, toff, len(rows))
+            return len(rows)
+
+        if self._pool is None or len(jobs) < 2:
+            done += sum(send(j) for j in jobs)
+        else:
+            done += sum(f.result() for f in [self._pool.submit(send, j) for j in jobs])
+        with self._count_lock:
+            self.delivered += done
+
     def stop(self, monitor):
         if self.client:
             self.client.disconnect()
@@ -220,10 +311,38 @@ class ScriptConnector(OutboundConnector):
         self.tenant_engine.ms.scripts.call(self.source, "process", ev.to_dict(), ctx, name=f"connector-{self.cid}")
 
 
+ALL_ETYPES = -1                           # event-type bit mask of every type (int32: all bits)
+
+
+def combined_selector(filters, reader):
+    """``selector(boot) -> (event-type bit mask, keep per assignment index or None, keep beyond it)``
+    of a connector's column filters together (a row passes when every filter keeps it), for
+    :meth:`EnrichedBatchReader.select_json`."""
+    def selector(boot):
+        etmask, keep, dflt = ALL_ETYPES, None, True
+        for f in filters:
+            em, k, d = f.select(reader, boot)
+            etmask &= em
+            if k is None:
+                continue
+            if keep is None:
+                keep, dflt = np.asarray(k, bool), bool(d)
+                continue
+            n = max(len(keep), len(k))
+            a = np.full(n, dflt)
+            a[:len(keep)] = keep
+            b = np.full(n, bool(d))
+            b[:len(k)] = k
+            keep, dflt = a & b, dflt and bool(d)
+        return etmask, keep, dflt
+    return selector
+
+
 class _Filter:
     """A connector filter (``FilteredOutboundConnector``): ``f(ev, ctx)`` is True for an event to
     leave out; ``exclude(cols, reader)`` is the same test over an engine batch's columns (a bool per
-    row), or None where the filter has no column form."""
+    row), or None where the filter has no column form; ``select(reader, boot)`` the same test as
+    (event-type bit mask, keep per assignment index, keep beyond it) for the native block selection."""
     op = "include"
 
     def _out(self, hit):
@@ -231,6 +350,10 @@ class _Filter:
 
     def exclude(self, cols, reader):
         return None
+
+    def _select_attr(self, reader, boot, pos, value):
+        m = reader.asg_mask(boot, pos, value)
+        return (ALL_ETYPES, m, False) if self.op == "include" else (ALL_ETYPES, ~m, True)
 
 
 class AreaFilter(_Filter):
@@ -253,6 +376,9 @@ class AreaFilter(_Filter):
     def exclude(self, cols, reader):
         return self._out(reader.attr_mask(cols, 3, self.area_id()))
 
+    def select(self, reader, boot):
+        return self._select_attr(reader, boot, 3, self.area_id())
+
 
 class DeviceTypeFilter(_Filter):
     """``connectors/filter/DeviceTypeFilter.java``: events of devices of (or not of) one type."""
@@ -274,6 +400,9 @@ class DeviceTypeFilter(_Filter):
     def exclude(self, cols, reader):
         return self._out(reader.attr_mask(cols, 6, self.type_id()))
 
+    def select(self, reader, boot):
+        return self._select_attr(reader, boot, 6, self.type_id())
+
 
 class EventTypeFilter(_Filter):
     def __init__(self, types):
@@ -287,6 +416,12 @@ class EventTypeFilter(_Filter):
 
     def exclude(self, cols, reader):
         return ~np.isin(np.asarray(cols["etype"]), self.codes)
+
+    def select(self, reader, boot):
+        m = 0
+        for c in self.codes:
+            m |= 1 << int(c)
+        return (m - (1 << 32) if m >= 1 << 31 else m), None, True
 
 
 class ScriptFilter(_Filter):
