@@ -16,7 +16,6 @@
 #include <string.h>
 
 #include <charconv>
-#include <string>
 #include <utility>
 #include <vector>
 
@@ -31,14 +30,23 @@ struct StrTab {
   std::pair<const uint8_t*, int64_t> get(int64_t k) const { return {heap + off[k], off[k + 1] - off[k]}; }
 };
 
-struct Out {
-  std::string s;
-  void lit(const char* x) { s.append(x); }
-  void ch(char c) { s.push_back(c); }
+struct Out {                                    // bounded writer: counts past the end, writes nothing there
+  uint8_t* b;
+  int64_t cap;
+  int64_t n = 0;
+  void put(const void* x, size_t k) {
+    if (n + (int64_t)k <= cap) memcpy(b + n, x, k);
+    n += (int64_t)k;
+  }
+  void lit(const char* x) { put(x, strlen(x)); }
+  void ch(char c) {
+    if (n < cap) b[n] = (uint8_t)c;
+    ++n;
+  }
   void i64(int64_t v) {
-    char b[24];
-    auto r = std::to_chars(b, b + sizeof(b), v);
-    s.append(b, r.ptr);
+    char t[24];
+    auto r = std::to_chars(t, t + sizeof(t), v);
+    put(t, (size_t)(r.ptr - t));
   }
   // float.__repr__ (shortest round trip; fixed for 1e-4 <= |v| < 1e16, else d.ddde+XX), as json.dumps
   void dbl(double v) {
@@ -68,11 +76,11 @@ struct Out {
       if (e < 0) {
         lit("0.");
         for (int k = 0; k < -e - 1; ++k) ch('0');
-        s.append(dig, nd);
+        put(dig, (size_t)nd);
       } else {
         for (int k = 0; k <= e; ++k) ch(k < nd ? dig[k] : '0');
         ch('.');
-        if (nd > e + 1) s.append(dig + e + 1, nd - e - 1);
+        if (nd > e + 1) put(dig + e + 1, (size_t)(nd - e - 1));
         else ch('0');
       }
       return;
@@ -81,7 +89,7 @@ struct Out {
     ch(dig[0]);
     if (nd > 1) {
       ch('.');
-      s.append(dig + 1, nd - 1);
+      put(dig + 1, (size_t)(nd - 1));
     }
     ch('e');
     ch(e < 0 ? '-' : '+');
@@ -118,6 +126,13 @@ struct Out {
     ch('"');
     int64_t i = 0;
     while (i < n) {
+      int64_t r = i;                               // a run of printable ASCII needing no escape
+      while (r < n && p[r] >= 0x20 && p[r] < 0x7f && p[r] != '"' && p[r] != '\\') ++r;
+      if (r > i) {
+        put(p + i, (size_t)(r - i));
+        i = r;
+        if (i >= n) break;
+      }
       const uint8_t b = p[i];
       if (b < 0x80) { cp(b); ++i; continue; }
       int need = 0;
@@ -240,8 +255,7 @@ int64_t swjson_rows(const int64_t* rows, int64_t n, const uint8_t* etype, const 
   const StrTab A{a_heap, a_off, a_present, n_asg * 7};
   const StrTab N{n_heap, n_off, n_present, n_names};
   const StrTab R{r_heap, r_off, r_present, n_names};
-  Out o, t;
-  o.s.reserve((size_t)(n * 420));
+  Out o{out, cap}, t{tout, tout ? tcap : 0};
   char bootx[24];
   const int bl = (int)(std::to_chars(bootx, bootx + sizeof(bootx), (unsigned long long)boot, 16).ptr - bootx);
   for (int64_t j = 0; j < n; ++j) {
@@ -255,9 +269,9 @@ int64_t swjson_rows(const int64_t* rows, int64_t n, const uint8_t* etype, const 
       if (ha && A.has(7 * a + k)) o.str(A.get(7 * a + k));
       else o.lit("null");
     };
-    out_off[j] = (int64_t)o.s.size();
+    out_off[j] = o.n;
     o.lit("{\"event\": {\"id\": \"");
-    o.s.append(bootx, bl);
+    o.put(bootx, (size_t)bl);
     o.ch('-');
     o.i64((first_seq + (block_rows ? block_rows[j] : row0 + i)) * world + rank);
     o.lit("\", \"alternateId\": ");
@@ -308,23 +322,20 @@ int64_t swjson_rows(const int64_t* rows, int64_t n, const uint8_t* etype, const 
     o.lit(", \"deviceTypeId\": "); ctxs(6);
     o.lit(", \"assignmentStatus\": \"Active\", \"engine\": \"batch\"}}");
     if (tout) {
-      tout_off[j] = (int64_t)t.s.size();
+      tout_off[j] = t.n;
       for (int64_t k = 0; k < tpl_len; ++k) {
         if (tpl[k] == 1) {
-          if (ha && A.has(7 * a + 5)) { auto x = A.get(7 * a + 5); t.s.append((const char*)x.first, (size_t)x.second); }
+          if (ha && A.has(7 * a + 5)) { auto x = A.get(7 * a + 5); t.put(x.first, (size_t)x.second); }
           else t.lit("None");
         } else if (tpl[k] == 2) t.lit(kTypes[et]);
         else t.ch((char)tpl[k]);
       }
     }
   }
-  out_off[n] = (int64_t)o.s.size();
-  if (tout) tout_off[n] = (int64_t)t.s.size();
-  if ((int64_t)o.s.size() > cap || (tout && (int64_t)t.s.size() > tcap))
-    return -(int64_t)(o.s.size() > (size_t)cap ? o.s.size() : t.s.size()) - (int64_t)1 - n;
-  memcpy(out, o.s.data(), o.s.size());
-  if (tout) memcpy(tout, t.s.data(), t.s.size());
-  return (int64_t)o.s.size();
+  out_off[n] = o.n;
+  if (tout) tout_off[n] = t.n;
+  if (o.n > cap || (tout && t.n > tcap)) return -(o.n > t.n ? o.n : t.n) - (int64_t)1 - n;
+  return o.n;
 }
 
 // MQTT 3.1.1 QoS 0 PUBLISH packets of n (topic, payload) pairs, back to back into `out` (one socket
@@ -356,6 +367,37 @@ int64_t swmqtt_publish_qos0(const uint8_t* topics, const int64_t* t_off, const u
     w += pl;
   }
   return w - out;
+}
+
+// Complete MQTT packets at the front of buf[0 .. n): per packet (first byte, start, body start, end)
+// into out[4 k ..], at most cap packets.  Returns the packets found; *used = the end of the last one.
+// -1: a malformed remaining length (more than 4 bytes), -2: a packet longer than max_len.
+int64_t swmqtt_scan(const uint8_t* buf, int64_t n, int64_t* out, int64_t cap, int64_t max_len, int64_t* used) {
+  int64_t p = 0, k = 0;
+  while (k < cap && n - p >= 2) {
+    int64_t len = 0, mult = 1, i = p + 1;
+    bool done = false;
+    for (int b = 0; b < 4 && i < n; ++b) {
+      const uint8_t x = buf[i++];
+      len += (int64_t)(x & 0x7f) * mult;
+      mult <<= 7;
+      if (!(x & 0x80)) { done = true; break; }
+    }
+    if (!done) {
+      if (i - p > 4) return -1;
+      break;                                     // the length bytes are not all here yet
+    }
+    if (len > max_len) return -2;
+    if (n - i < len) break;
+    out[4 * k] = buf[p];
+    out[4 * k + 1] = p;
+    out[4 * k + 2] = i;
+    out[4 * k + 3] = i + len;
+    ++k;
+    p = i + len;
+  }
+  *used = p;
+  return k;
 }
 
 }  // extern "C"

@@ -690,19 +690,25 @@ int64_t decode_rows(const uint8_t* pg, const int32_t* rows, int64_t nw, uint8_t*
   uint32_t ho = ph.alt_pfx;                         // heap bytes before row j's strings
   int64_t w = 0;
   auto member_value = [&](int c, uint32_t ix) -> uint64_t { return ph.cols[c].base + unpack(pg + ph.cols[c].data_off, ix, ph.cols[c].bits); };
+  // exceptions are stored in ascending member order and rows are visited in ascending order: one
+  // cursor per column walks each exception list once per call (not once per row)
+  uint32_t xc[SEG_NCOL] = {0};
   auto dbl = [&](int c, uint32_t ix) -> double {
     const SwSegCol& cd = ph.cols[c];
     const uint8_t* words = pg + cd.data_off;
     const uint8_t* xi = words + 8 * seg_col_words(cd.count, cd.bits);
     const uint8_t* xr = xi + ((2u * cd.n_exc + 7u) & ~7u);
-    for (uint32_t j = 0; j < cd.n_exc; ++j) {
+    uint32_t& j = xc[c];
+    for (; j < cd.n_exc; ++j) {
       uint16_t x;
       memcpy(&x, xi + 2 * j, 2);
+      if (x < ix) continue;
       if (x == ix) {
         uint64_t raw;
         memcpy(&raw, xr + 8 * j, 8);
         return sw_bits_f64(raw);
       }
+      break;
     }
     return seg_dec_value(seg_unord(cd.base + unpack(words, ix, cd.bits)), cd.exp);
   };
@@ -2089,13 +2095,15 @@ void swseg_dates(const uint8_t* b, int64_t* lo, int64_t* hi) { block_dates(b, lo
 // each row's event type and assignment are read from the packed columns (no full decode) and tested
 // against `etmask` (bit = event type) and `keep` (per assignment index; indexes >= n_keep take
 // keep_default); the kept rows alone are decoded (decode_rows, strings included) and written by
-// swjson_rows (csrc/native/swrowjson.cpp).  Pages run on `threads` threads.  Outputs as swjson_rows
-// (documents in out / out_off, topics in tout / tout_off).  Returns the
-// document bytes, -need (a buffer too small: need > cap or tcap), or -(1 << 40) - 1 - k when row k of
-// the kept rows must take the caller's Python path (an API-added JSON row), -(1 << 41) on a page that
-// fails to decode, or -(1 << 42) when kept rows' dictionary entries are missing (miss[0..counts[2]):
-// an assignment index a >= 0 as a, a name id m as -1 - m; the caller resolves them and calls again).
-// counts = {kept rows, block rows, missing entries}.  The block must be verified by the caller.
+// swjson_rows (csrc/native/swrowjson.cpp).  Pages run on `threads` workers, worker w writing its pages'
+// documents / topics into slice w of `scratch` / `tscratch` (equal slices; reused caller memory, no
+// allocation per call), then the slices are concatenated into out / tout (offsets out_off / tout_off,
+// block order).  counts = {kept rows, block rows, missing entries}.  Returns the document bytes,
+// -need when a buffer is too small (need = the scratch or output bytes to pass next time), -(1 << 40)
+// - 1 - k when kept row k must take the caller's Python path (an API-added JSON row), -(1 << 41) on a
+// page that fails to decode, or -(1 << 42) when kept rows' dictionary entries are missing
+// (miss[0 .. counts[2]): an assignment index a >= 0 as a, a name id m as -1 - m; the caller resolves
+// them and calls again).  The block must be verified by the caller.
 extern "C" int64_t swjson_rows(const int64_t* rows, int64_t n, const uint8_t* etype, const uint8_t* level,
                                const int64_t* date, const int32_t* asg, const uint16_t* name, const double* v0,
                                const double* v1, const double* v2, const uint8_t* flags, const uint8_t* heap,
@@ -2113,28 +2121,39 @@ extern "C" int64_t swjson_select_block(const uint8_t* b, int32_t etmask, const u
                                        const uint8_t* n_heap, const int64_t* n_off, const uint8_t* n_present,
                                        int64_t n_names, const uint8_t* r_heap, const int64_t* r_off,
                                        const uint8_t* r_present, const uint8_t* tpl, int64_t tpl_len, int32_t threads,
-                                       uint8_t* out, int64_t cap, int64_t* out_off, uint8_t* tout, int64_t tcap,
-                                       int64_t* tout_off, int64_t* counts, int64_t* miss, int64_t miss_cap) {
+                                       uint8_t* scratch, int64_t scap, uint8_t* tscratch, int64_t tscap, uint8_t* out,
+                                       int64_t cap, int64_t* out_off, uint8_t* tout, int64_t tcap, int64_t* tout_off,
+                                       int64_t* counts, int64_t* miss, int64_t miss_cap) {
   SwSegBlockHdr h;
   memcpy(&h, b, sizeof(h));
   const uint32_t* pt = (const uint32_t*)(b + 64);
   const int64_t np = h.n_pages;
-  struct PageOut {
-    std::vector<uint8_t> js, tp;
-    std::vector<int64_t> jo, to;
-    int64_t bad = -1;
+  int T = threads > 0 ? threads : 1;
+  if (T > 32) T = 32;
+  if ((int64_t)T > np) T = (int)(np > 0 ? np : 1);
+  const int64_t wcap = scap / T, wtcap = tpl ? tscap / T : 0;
+  struct Worker {
+    std::vector<int64_t> doff, toff;               // per kept row, relative to the worker's slice
+    int64_t bytes = 0, tbytes = 0;                 // written (or needed, when past the slice)
+    int64_t bad = -1;                              // kept row (worker-relative) for the Python path
+    bool fail = false;
     std::vector<int64_t> miss;
   };
-  std::vector<PageOut> po((size_t)np);
-  std::atomic<int64_t> fail{0};
-  auto work = [&](int64_t p0, int64_t p1) {
+  std::vector<Worker> ws((size_t)T);
+  auto work = [&](int w) {
+    Worker& W = ws[(size_t)w];
+    const int64_t p0 = np * w / T, p1 = np * (w + 1) / T;
+    uint8_t* js = scratch + (int64_t)w * wcap;
+    uint8_t* ts = tpl ? tscratch + (int64_t)w * wtcap : nullptr;
     std::vector<int32_t> sel;
-    std::vector<int64_t> brow, idx, soff;
+    std::vector<int64_t> brow, idx, soff, jo, to;
     std::vector<uint8_t> et, lv, fl, heap;
     std::vector<int64_t> dt;
     std::vector<int32_t> as;
     std::vector<uint16_t> nm;
     std::vector<double> a0, a1, a2;
+    W.doff.push_back(0);
+    W.toff.push_back(0);
     for (int64_t p = p0; p < p1; ++p) {
       const uint8_t* pg = b + pt[p];
       SwSegPageHdr ph;
@@ -2145,69 +2164,65 @@ extern "C" int64_t swjson_select_block(const uint8_t* b, int32_t etmask, const u
         if (e > 31 || !((etmask >> e) & 1)) continue;
         const int64_t a = seg_unord(col_int(pg, ph.cols[SEG_ASG], j));
         if (a >= 0 && (a >= n_asg || !a_known[a])) {
-          if (po[(size_t)p].miss.empty() || po[(size_t)p].miss.back() != a) po[(size_t)p].miss.push_back(a);
+          if (W.miss.empty() || W.miss.back() != a) W.miss.push_back(a);
           continue;
         }
         const bool k = (a >= 0 && a < n_keep) ? keep[a] != 0 : keep_default != 0;
         if (k) sel.push_back((int32_t)j);
       }
-      PageOut& o = po[(size_t)p];
-      if (!o.miss.empty()) continue;
       const int64_t k = (int64_t)sel.size();
-      o.jo.assign((size_t)k + 1, 0);
-      o.to.assign((size_t)k + 1, 0);
-      if (!k) continue;
-      et.resize(k); lv.resize(k); fl.resize(k); dt.resize(k); as.resize(k); nm.resize(k);
-      a0.resize(k); a1.resize(k); a2.resize(k);
-      heap.resize((size_t)ph.heap_bytes + (size_t)k * (SEG_ALT_PFX_MAX + 16 + 8) + 8);
-      soff.assign(3 * (size_t)k + 1, 0);
+      if (!k || !W.miss.empty()) continue;
+      if ((int64_t)et.size() < k) {
+        et.resize(k); lv.resize(k); fl.resize(k); dt.resize(k); as.resize(k); nm.resize(k);
+        a0.resize(k); a1.resize(k); a2.resize(k); brow.resize(k); idx.resize(k);
+        jo.resize(k + 1); to.resize(k + 1); soff.resize(3 * (size_t)k + 1);
+      }
+      const size_t hb = (size_t)ph.heap_bytes + (size_t)k * (SEG_ALT_PFX_MAX + 16 + 8) + 8;
+      if (heap.size() < hb) heap.resize(hb);
+      soff[0] = 0;
       int64_t so = 0;
       if (decode_rows(pg, sel.data(), k, et.data(), lv.data(), dt.data(), as.data(), nm.data(), a0.data(), a1.data(),
                       a2.data(), fl.data(), heap.data(), (int64_t)heap.size(), &so, soff.data()) != k) {
-        fail = 1;
+        W.fail = true;
         return;
       }
       for (int64_t i = 0; i < k; ++i)
-        if (nm[i] != 0xffff && ((int64_t)nm[i] >= n_names || !n_present[nm[i]])) o.miss.push_back(-1 - (int64_t)nm[i]);
-      if (!o.miss.empty()) continue;
-      brow.resize(k);
-      idx.resize(k);
+        if (nm[i] != 0xffff && ((int64_t)nm[i] >= n_names || !n_present[nm[i]])) W.miss.push_back(-1 - (int64_t)nm[i]);
+      if (!W.miss.empty()) continue;
       for (int64_t i = 0; i < k; ++i) { brow[i] = p * SEG_PAGE_ROWS + sel[i]; idx[i] = i; }
-      int64_t jcap = 512 * k + 4096, tcap_ = (tpl_len + 96) * k + 64;
-      for (int attempt = 0; attempt < 2; ++attempt) {
-        o.js.resize((size_t)jcap);
-        o.tp.resize((size_t)tcap_);
-        const int64_t r = swjson_rows(idx.data(), k, et.data(), lv.data(), dt.data(), as.data(), nm.data(), a0.data(),
-                                      a1.data(), a2.data(), fl.data(), heap.data(), soff.data(), h.boot, h.first_seq,
-                                      h.world, h.rank, h.recv_ms, 0, a_heap, a_off, a_present, n_asg, n_heap,
-                                      n_off, n_present, n_names, r_heap, r_off, r_present, tpl, tpl_len, o.js.data(),
-                                      jcap, o.jo.data(), tpl ? o.tp.data() : nullptr, tcap_, o.to.data(), brow.data());
-        if (r >= 0) {
-          o.js.resize((size_t)r);
-          o.tp.resize((size_t)(tpl ? o.to[(size_t)k] : 0));
-          break;
-        }
-        if (-r - 1 < k) { o.bad = -r - 1; break; }
-        jcap = tcap_ = -r - 1 - k + 4096;
-        if (attempt == 1) { fail = 1; return; }
+      const int64_t jroom = W.bytes < wcap ? wcap - W.bytes : 0, troom = W.tbytes < wtcap ? wtcap - W.tbytes : 0;
+      const int64_t r = swjson_rows(idx.data(), k, et.data(), lv.data(), dt.data(), as.data(), nm.data(), a0.data(),
+                                    a1.data(), a2.data(), fl.data(), heap.data(), soff.data(), h.boot, h.first_seq,
+                                    h.world, h.rank, h.recv_ms, 0, a_heap, a_off, a_present, n_asg, n_heap, n_off,
+                                    n_present, n_names, r_heap, r_off, r_present, tpl, tpl_len,
+                                    js + (W.bytes < wcap ? W.bytes : 0), jroom, jo.data(),
+                                    ts ? ts + (W.tbytes < wtcap ? W.tbytes : 0) : nullptr, troom, to.data(), brow.data());
+      if (r <= -1 && -r - 1 < k) {                 // a row for the Python path
+        W.bad = (int64_t)W.doff.size() - 1 + (-r - 1);
+        return;
       }
+      // written, or (a slice too small) only measured: jo / to hold the sizes either way
+      for (int64_t i = 0; i < k; ++i) {
+        W.doff.push_back(W.bytes + jo[i + 1]);
+        W.toff.push_back(W.tbytes + (tpl ? to[i + 1] : 0));
+      }
+      W.bytes += jo[k];
+      W.tbytes += tpl ? to[k] : 0;
     }
   };
-  int T = threads > 0 ? threads : 1;
-  if (T > 32) T = 32;
-  if ((int64_t)T > np) T = (int)(np > 0 ? np : 1);
-  if (T <= 1) work(0, np);
+  if (T <= 1) work(0);
   else {
     std::vector<std::thread> th;
-    for (int w = 0; w < T; ++w) th.emplace_back(work, np * w / T, np * (w + 1) / T);
+    for (int w = 0; w < T; ++w) th.emplace_back(work, w);
     for (auto& x : th) x.join();
   }
-  if (fail.load()) return -(int64_t(1) << 41);
   counts[0] = counts[2] = 0;
   counts[1] = h.n_rows;
+  for (const Worker& W : ws)
+    if (W.fail) return -(int64_t(1) << 41);
   {
     std::vector<int64_t> ms;
-    for (const PageOut& o : po) ms.insert(ms.end(), o.miss.begin(), o.miss.end());
+    for (const Worker& W : ws) ms.insert(ms.end(), W.miss.begin(), W.miss.end());
     if (!ms.empty()) {
       std::sort(ms.begin(), ms.end());
       ms.erase(std::unique(ms.begin(), ms.end()), ms.end());
@@ -2217,31 +2232,36 @@ extern "C" int64_t swjson_select_block(const uint8_t* b, int32_t etmask, const u
       return -(int64_t(1) << 42);
     }
   }
-  int64_t nk = 0, jb = 0, tb = 0;
-  for (int64_t p = 0; p < np; ++p) {
-    const PageOut& o = po[(size_t)p];
-    if (o.bad >= 0) return -(int64_t(1) << 40) - 1 - (nk + o.bad);
-    nk += (int64_t)o.jo.size() - 1;
-    jb += (int64_t)o.js.size();
-    tb += (int64_t)o.tp.size();
+  int64_t nk = 0, jb = 0, tb = 0, wmax = 0, twmax = 0;
+  for (const Worker& W : ws) {
+    if (W.bad >= 0) return -(int64_t(1) << 40) - 1 - (nk + W.bad);
+    nk += (int64_t)W.doff.size() - 1;
+    jb += W.bytes;
+    tb += W.tbytes;
+    wmax = std::max(wmax, W.bytes);
+    twmax = std::max(twmax, W.tbytes);
   }
   counts[0] = nk;
-  if (jb > cap || (tout && tb > tcap)) return -(jb > tb ? jb : tb);
+  if (wmax > wcap || twmax > wtcap) {            // a worker's slice was too small: scratch for next time
+    const int64_t need = std::max(wmax * T + 4096 * T, tpl ? twmax * T + 4096 * T : 0);
+    return -std::max<int64_t>(need, 1);
+  }
+  if (jb > cap || (tout && tb > tcap)) return -std::max<int64_t>(jb, tb);
   int64_t w = 0, wj = 0, wt = 0;
   out_off[0] = 0;
   if (tout) tout_off[0] = 0;
-  for (int64_t p = 0; p < np; ++p) {
-    const PageOut& o = po[(size_t)p];
-    const int64_t k = (int64_t)o.jo.size() - 1;
-    memcpy(out + wj, o.js.data(), o.js.size());
-    if (tout) memcpy(tout + wt, o.tp.data(), o.tp.size());
+  for (int x = 0; x < T; ++x) {
+    const Worker& W = ws[(size_t)x];
+    const int64_t k = (int64_t)W.doff.size() - 1;
+    memcpy(out + wj, scratch + (int64_t)x * wcap, (size_t)W.bytes);
+    if (tout && tpl) memcpy(tout + wt, tscratch + (int64_t)x * wtcap, (size_t)W.tbytes);
     for (int64_t i = 0; i < k; ++i) {
-      out_off[w + i + 1] = wj + o.jo[(size_t)i + 1];
-      if (tout) tout_off[w + i + 1] = wt + o.to[(size_t)i + 1];
+      out_off[w + i + 1] = wj + W.doff[(size_t)i + 1];
+      if (tout) tout_off[w + i + 1] = wt + W.toff[(size_t)i + 1];
     }
     w += k;
-    wj += (int64_t)o.js.size();
-    wt += (int64_t)o.tp.size();
+    wj += W.bytes;
+    wt += W.tbytes;
   }
   return wj;
 }

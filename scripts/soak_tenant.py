@@ -35,6 +35,90 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _trailer_diag(store, ib, lost) -> list:
+    """For ids the store holds but its trailer lookup misses: the block holding each, the row and
+    page, and what the block's in-memory trailer, its on-disk trailer and a CPU-rebuilt trailer
+    each answer for the id (candidate pages)."""
+    import ctypes
+    import numpy as np
+    from sitewhere_amd._native import native
+    from sitewhere_amd.persistence import segments as sg
+    from sitewhere_amd.pipeline.fleet import hash64
+    lib = native()
+    target = set(int(x) for x in lost[:64])
+    out = []
+
+    def pages_of(addr, h):
+        bo, po = np.empty(64, np.int64), np.empty(64, np.int64)
+        arr = (ctypes.c_void_p * 1)(addr)
+        k = int(lib.swseg_ix_alt_pages(arr, 1, int(h), bo.ctypes.data, po.ctypes.data, 64))
+        return po[:min(k, 64)].tolist()
+
+    with store.seg.lease():
+        tabs = store._boot_tables()
+        for t in tabs.values():
+            for bi in range(t["n"] - 1, -1, -1):
+                if not target or len(out) >= 4:
+                    break
+                e = t["ents"][bi]
+                hv = store._block_alt_hashes(e)
+                hit = target & set(np.intersect1d(hv, np.array(sorted(target), np.uint64)).tolist())
+                if not hit:
+                    continue
+                blk = store.seg.read_block(e)
+                cols = sg.decode_block(blk, check=False)
+                rows = {}
+                for i in range(len(cols["date"])):
+                    s = sg.row_strings(cols, i)[0]
+                    if s is not None:
+                        h = hash64(s)
+                        if h in hit:
+                            rows[h] = i
+                toff = sg.trailer_offset(blk)
+                disk_tr = np.ascontiguousarray(blk[toff:])
+                mem_tr = t["tr"][bi]
+                mem_bytes = np.asarray(mem_tr[3][:mem_tr[1]]) if mem_tr is not None and len(mem_tr) > 3 else None
+                try:
+                    ref = sg.index_block(_strip(blk), ib.engine.ctx_table())
+                    cpu_tr = np.ascontiguousarray(ref[sg.trailer_offset(ref):])
+                except Exception as ex:  # noqa: BLE001
+                    cpu_tr = None
+                    out.append({"cpu_rebuild_error": repr(ex)})
+                d = {"block": int(bi), "of": int(t["n"]), "first_seq": int(e["first_seq"]), "n_rows": int(e["n_rows"]),
+                     "hits": len(hit), "mem_equals_disk": None if mem_bytes is None else bool(np.array_equal(mem_bytes, disk_tr)),
+                     "cpu_equals_disk": None if cpu_tr is None else bool(len(cpu_tr) == len(disk_tr) and np.array_equal(cpu_tr, disk_tr)),
+                     "ids": []}
+                if cpu_tr is not None and len(cpu_tr) == len(disk_tr):
+                    diff = np.nonzero(cpu_tr != disk_tr)[0]
+                    d["trailer_bytes_differ"] = int(len(diff))
+                    d["first_diff"] = int(diff[0]) if len(diff) else None
+                    hd = sg.parse_trailer(disk_tr)
+                    d["trailer_sections"] = {k: int(hd[k]) for k in ("off_pages", "off_alt_dir", "off_alt", "n_alt",
+                                                                      "alt_bits", "alt_pbits", "n_pages")}
+                for h in sorted(hit)[:6]:
+                    r = rows.get(h)
+                    d["ids"].append({"row": r, "page": None if r is None else r // sg.PAGE_ROWS,
+                                     "disk": pages_of(disk_tr.ctypes.data, h),
+                                     "mem": pages_of(int(mem_tr[0]), h) if mem_tr is not None else None,
+                                     "cpu": pages_of(cpu_tr.ctypes.data, h) if cpu_tr is not None else None})
+                out.append(d)
+                target -= hit
+    return out
+
+
+def _strip(blk):
+    """The block without its trailer (flag cleared, bytes = end of the pages, header re-sealed)."""
+    from sitewhere_amd.persistence import segments as sg
+    h = blk[:64].view(sg.HDR)[0]
+    toff = sg.trailer_offset(blk)
+    out = blk[:toff].copy()
+    hv = out[:64].view(sg.HDR)
+    hv["flags"] = 0
+    hv["bytes"] = toff
+    sg.seal(out, int(h["first_seq"]), int(h["recv_ms"]), int(h["boot"]), int(h["rank"]), int(h["world"]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--devices", type=int, default=1 << 20)
@@ -228,12 +312,17 @@ def main():
     replay["store_decoded_has"], replay["store_decoded_scanned"] = len(in_cols), scanned
     miss = sorted(want - set(int(k) for k in f_ix))
     replay["missing_in_decoded"] = len(set(miss) - in_cols)
+    if os.environ.get("SOAK_FORCE_DIAG"):           # exercise the diagnostics on found ids
+        replay["trailer_diag_forced"] = _trailer_diag(store, ib, sorted(in_cols)[:8])
     if miss:
         # where the missing ids sit in the replayed sub-batch (payload index, device, event type)
         idx = np.nonzero(np.isin(dec["alt_hash"], np.array(miss[:2000], np.uint64)))[0]
         replay["missing_payload_idx_sample"] = idx[:40].tolist()
         replay["missing_etypes"] = np.bincount(dec["etype"][idx].astype(np.int64), minlength=4).tolist()
         replay["missing_first_last"] = [int(idx.min()), int(idx.max())] if len(idx) else None
+        lost = sorted(set(miss) & in_cols)          # stored, yet not found through the trailers
+        if lost:
+            replay["trailer_diag"] = _trailer_diag(store, ib, lost)
     replay["store_blocks"] = store.index_stats()
     replay["all_duplicates"] = (replay["settled_duplicates"] + replay["window_duplicates"]
                                 == replay["events_of_registered_devices"] and replay["persisted_by_engine"] == 0

@@ -224,7 +224,9 @@ def native():
                c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, P, P, P, c_int64, P, P, P, c_int64, P, P, P,
                P, c_int64, P, c_int64, P, P, c_int64, P, P)
         _proto(lib, "swjson_select_block", c_int64, P, c_int32, P, c_int64, c_int32, P, c_int64, P, P, P, P, P, P,
-               c_int64, P, P, P, P, c_int64, c_int32, P, c_int64, P, P, c_int64, P, P, P, c_int64)
+               c_int64, P, P, P, P, c_int64, c_int32, P, c_int64, P, c_int64, P, c_int64, P, P, c_int64, P, P, P,
+               c_int64)
+        _proto(lib, "swmqtt_scan", c_int64, P, c_int64, P, c_int64, c_int64, P)
         _proto(lib, "swmqtt_publish_qos0", c_int64, P, P, P, P, c_int64, ctypes.c_uint8, P, c_int64)
         _proto(lib, "swss_stats", None, P, P)
         _proto(lib, "swss_set_retention", None, P, c_int64, c_int64, c_int64)

@@ -92,6 +92,77 @@ def read_packet(sock):
     return h >> 4, h & 0x0F, body
 
 
+class PacketReader:
+    """Buffered MQTT packet reader of one connection: one ``recv_into`` per chunk of up to ``CHUNK``
+    bytes, the complete packets in it found natively (``swmqtt_scan``) -- ``read_packet`` costs
+    three receives and a Python parse per packet."""
+    CHUNK = 1 << 20
+
+    def __init__(self, sock):
+        import numpy as np
+        from .._native import native
+        self.sock = sock
+        self.a = np.empty(2 * self.CHUNK, np.uint8)
+        self.lo = self.hi = 0
+        self._lib = native()
+        self._hdr = np.empty(4 * 8192, np.int64)
+        self._used = np.zeros(1, np.int64)
+        self._pending = None                      # (data, packets, next index) of the last batch
+
+    def _fill(self):
+        import numpy as np
+        if self.hi == len(self.a):
+            if self.lo:                           # move the partial packet to the front
+                n = self.hi - self.lo
+                self.a[:n] = self.a[self.lo:self.hi]
+                self.lo, self.hi = 0, n
+            else:                                 # one packet larger than the buffer
+                b = np.empty(2 * len(self.a), np.uint8)
+                b[:self.hi] = self.a[:self.hi]
+                self.a = b
+        got = self.sock.recv_into(memoryview(self.a)[self.hi:], min(self.CHUNK, len(self.a) - self.hi))
+        if not got:
+            raise ConnectionError("closed")
+        self.hi += got
+
+    def _scan(self):
+        while True:
+            n = self.hi - self.lo
+            if n >= 2:
+                k = int(self._lib.swmqtt_scan(self.a.ctypes.data + self.lo, n, self._hdr.ctypes.data,
+                                              len(self._hdr) // 4, MAX_PACKET, self._used.ctypes.data))
+                if k < 0:
+                    raise ConnectionError("malformed remaining length" if k == -1 else "packet too large")
+                if k:
+                    used = int(self._used[0])
+                    data = self.a[self.lo:self.lo + used].tobytes()
+                    h = self._hdr[:4 * k].reshape(k, 4).tolist()
+                    self.lo += used
+                    if self.lo == self.hi:
+                        self.lo = self.hi = 0
+                    return data, [(x[0] >> 4, x[0] & 0x0F, x[1], x[2], x[3]) for x in h]
+            self._fill()
+
+    def read(self):
+        """The next packet: (type, flags, body)."""
+        if self._pending is None:
+            d, p = self._scan()
+            self._pending = (d, p, 0)
+        d, p, i = self._pending
+        t, f, _a, bs, e = p[i]
+        self._pending = (d, p, i + 1) if i + 1 < len(p) else None
+        return t, f, d[bs:e]
+
+    def read_batch(self):
+        """Every complete packet buffered (blocks for the first): (data, [(type, flags, start, body
+        start, end)]) with offsets into ``data``, one bytes object of the packets."""
+        if self._pending is not None:
+            d, p, i = self._pending
+            self._pending = None
+            return d, p[i:]
+        return self._scan()
+
+
 def packet(ptype: int, flags: int, body: bytes) -> bytes:
     return bytes([(ptype << 4) | flags]) + _enc_len(len(body)) + body
 
@@ -262,49 +333,66 @@ class MqttClient:
                     backoff = min(backoff * 2, self.max_backoff)
 
     def _read_loop(self, sock):
+        reader = PacketReader(sock)
         while not self._closed:
-            t, flags, body = read_packet(sock)
+            data, pkts = reader.read_batch()
             self._last_recv = time.monotonic()
-            if t == PUBLISH:
-                topic, qos, pid, _retain, _dup, payload = parse_publish(flags, body)
-                if qos == 2 and pid in self._in_qos2:
-                    self._send(packet(PUBREC, 0, struct.pack("!H", pid)))   # duplicate: already delivered
+            handlers = list(self._handlers)
+            for t, flags, _a, bs, e in pkts:
+                if t == PUBLISH and not flags & 0x06:          # QoS 0: straight to the handlers
+                    tl = (data[bs] << 8) | data[bs + 1]
+                    topic, payload = data[bs + 2:bs + 2 + tl].decode(), data[bs + 2 + tl:e]
+                    for h in handlers:
+                        try:
+                            h(topic, payload)
+                        except Exception:  # noqa: BLE001 -- a handler error never kills the connection
+                            pass
                     continue
-                for h in list(self._handlers):
-                    try:
-                        h(topic, payload)
-                    except Exception:  # noqa: BLE001 -- a handler error never kills the connection
-                        pass
-                if qos == 1:
-                    self._send(packet(PUBACK, 0, struct.pack("!H", pid)))
-                elif qos == 2:
-                    self._in_qos2.add(pid)
-                    self._send(packet(PUBREC, 0, struct.pack("!H", pid)))
-            elif t == PUBREL:
-                pid = struct.unpack("!H", body[:2])[0]
-                self._in_qos2.discard(pid)
-                self._send(packet(PUBCOMP, 0, body[:2]))
-            elif t in (PUBACK, PUBCOMP):
-                pid = struct.unpack("!H", body[:2])[0]
-                with self._lock:
-                    ent = self._out.pop(pid, None)
+                self._on_packet(t, flags, data[bs:e])
+
+    def _on_packet(self, t: int, flags: int, body: bytes):
+        """One packet other than a QoS 0 PUBLISH (acknowledgements, QoS 1 / 2 deliveries)."""
+        if t == PUBLISH:
+            topic, qos, pid, _retain, _dup, payload = parse_publish(flags, body)
+            if qos == 2 and pid in self._in_qos2:
+                self._send(packet(PUBREC, 0, struct.pack("!H", pid)))   # duplicate: already delivered
+                return
+            for h in list(self._handlers):
+                try:
+                    h(topic, payload)
+                except Exception:  # noqa: BLE001 -- a handler error never kills the connection
+                    pass
+            if qos == 1:
+                self._send(packet(PUBACK, 0, struct.pack("!H", pid)))
+            elif qos == 2:
+                self._in_qos2.add(pid)
+                self._send(packet(PUBREC, 0, struct.pack("!H", pid)))
+        elif t == PUBREL:
+            pid = struct.unpack("!H", body[:2])[0]
+            self._in_qos2.discard(pid)
+            self._send(packet(PUBCOMP, 0, body[:2]))
+        elif t in (PUBACK, PUBCOMP):
+            pid = struct.unpack("!H", body[:2])[0]
+            with self._lock:
+                ent = self._out.pop(pid, None)
+            if ent is not None:
+                ent[2].set()
+        elif t == PUBREC:
+            pid = struct.unpack("!H", body[:2])[0]
+            with self._lock:
+                ent = self._out.get(pid)
                 if ent is not None:
-                    ent[2].set()
-            elif t == PUBREC:
-                pid = struct.unpack("!H", body[:2])[0]
-                with self._lock:
-                    ent = self._out.get(pid)
-                    if ent is not None:
-                        ent[0] = "pubcomp"
-                self._send(packet(PUBREL, 2, body[:2]))
-            elif t in (SUBACK, UNSUBACK):
-                pid = struct.unpack("!H", body[:2])[0]
-                w = self._acks.pop(pid, None)
-                if w is not None:
-                    w[1].append(body[2:])
-                    w[0].set()
-            elif t == PINGRESP:
-                self._ping_out = None
+                    ent[0] = "pubcomp"
+            self._send(packet(PUBREL, 2, body[:2]))
+        elif t in (SUBACK, UNSUBACK):
+            pid = struct.unpack("!H", body[:2])[0]
+            w = self._acks.pop(pid, None)
+            if w is not None:
+                w[1].append(body[2:])
+                w[0].set()
+        elif t == PINGRESP:
+            self._ping_out = None
+
 
     def _pinger(self):
         while not self._closed:
@@ -417,8 +505,9 @@ class MqttClient:
                 raise TimeoutError("PUBACK not received" if qos == 1 else "PUBCOMP not received")
 
     def publish_framed_qos0(self, packets):
-        """Already framed QoS 0 PUBLISH packets (``swmqtt_publish_qos0``), in one write."""
-        self._send(bytes(packets) if not isinstance(packets, (bytes, bytearray)) else packets)
+        """Already framed QoS 0 PUBLISH packets (``swmqtt_publish_qos0``), in one write (any buffer;
+        sent before this returns)."""
+        self._send(packets)
 
     @property
     def inflight(self) -> int:
@@ -503,6 +592,7 @@ class MqttBroker:
         self._stop = threading.Event()
         self._t = None
         self.published = 0
+        self._route_cache: dict[bytes, tuple] = {}     # topic -> subscribed sessions (QoS 0 forwarding)
 
     def start(self):
         self._srv.listen(128)
@@ -579,6 +669,7 @@ class MqttBroker:
             sess.will = will
             sess.conn = c
             self._sessions[cid] = sess
+            self._route_cache.clear()
         c.sendall(packet(CONNACK, 0, bytes([1 if present else 0, 0])))
         return sess, keepalive, present
 
@@ -591,7 +682,8 @@ class MqttBroker:
             with self._lock:
                 self._conns.add(c)
             c.settimeout(10)
-            t, _, body = read_packet(c)
+            reader = PacketReader(c)
+            t, _, body = reader.read()
             if t != CONNECT:
                 return
             r = self._connect(c, body)
@@ -609,65 +701,22 @@ class MqttBroker:
             for q in queued:                                # then what arrived while it was offline
                 self._deliver(sess, *q)
             while not self._stop.is_set():
-                t, flags, body = read_packet(c)
-                if t == PUBLISH:
-                    topic, qos, pid, retain, _dup, payload = parse_publish(flags, body)
-                    if qos == 2:
-                        if pid not in sess.in_qos2:
-                            sess.in_qos2.add(pid)
-                            self.route(topic, payload, qos, retain)
-                        self._send(sess, c, packet(PUBREC, 0, struct.pack("!H", pid)))
+                data, pkts = reader.read_batch()
+                k = 0
+                while k < len(pkts):
+                    t, flags, a0, bs, e = pkts[k]
+                    if t == PUBLISH and not flags & 0x07:
+                        # a run of QoS 0, non-retained publishes: forwarded as they came, one send of
+                        # the run per subscriber when every topic of it has the same subscribers
+                        k = self._forward_run(data, pkts, k)
                         continue
-                    self.route(topic, payload, qos, retain)
-                    if qos == 1:
-                        self._send(sess, c, packet(PUBACK, 0, struct.pack("!H", pid)))
-                elif t == PUBREL:
-                    sess.in_qos2.discard(struct.unpack("!H", body[:2])[0])
-                    self._send(sess, c, packet(PUBCOMP, 0, body[:2]))
-                elif t in (PUBACK, PUBCOMP):
-                    with sess.wlock:
-                        sess.out.pop(struct.unpack("!H", body[:2])[0], None)
-                elif t == PUBREC:
-                    pid = struct.unpack("!H", body[:2])[0]
-                    rel = packet(PUBREL, 2, body[:2])
-                    with sess.wlock:
-                        if pid in sess.out:
-                            sess.out[pid] = ["pubcomp", rel]
-                    self._send(sess, c, rel)
-                elif t == SUBSCRIBE:
-                    pid, pos, granted, new = body[:2], 2, bytearray(), []
-                    while pos < len(body):
-                        ln = struct.unpack("!H", body[pos:pos + 2])[0]
-                        filt = body[pos + 2:pos + 2 + ln].decode()
-                        q = body[pos + 2 + ln] & 3
-                        pos += 3 + ln
-                        if q == 3 or not filt:
-                            granted.append(0x80)
-                            continue
-                        with self._lock:
-                            sess.subs[filt] = q
-                        granted.append(q)
-                        new.append((filt, q))
-                    self._send(sess, c, packet(SUBACK, 0, pid + bytes(granted)))
-                    with self._lock:
-                        retained = [(tp, p, rq) for tp, (p, rq) in self._retained.items()]
-                    for filt, q in new:                     # retained messages of the new filters
-                        for tp, p, rq in retained:
-                            if topic_matches(filt, tp):
-                                self._deliver(sess, tp, p, min(q, rq), True)
-                elif t == UNSUBSCRIBE:
-                    pid, pos = body[:2], 2
-                    while pos < len(body):
-                        ln = struct.unpack("!H", body[pos:pos + 2])[0]
-                        with self._lock:
-                            sess.subs.pop(body[pos + 2:pos + 2 + ln].decode(), None)
-                        pos += 2 + ln
-                    self._send(sess, c, packet(UNSUBACK, 0, pid))
-                elif t == PINGREQ:
-                    self._send(sess, c, packet(PINGRESP, 0, b""))
-                elif t == DISCONNECT:
-                    graceful = True
-                    break
+                    k += 1
+                    if not self._handle(sess, c, t, flags, data[bs:e]):
+                        graceful = True
+                        break
+                else:
+                    continue
+                break
         except (ConnectionError, OSError, IndexError, struct.error, UnicodeDecodeError, ssl.SSLError):
             pass
         finally:
@@ -680,6 +729,7 @@ class MqttBroker:
                         sess.conn = None
                         if sess.clean and self._sessions.get(sess.client_id) is sess:
                             del self._sessions[sess.client_id]
+                            self._route_cache.clear()
                 if mine and not graceful and sess.will is not None and not self._stop.is_set():
                     wt, wp, wq, wr = sess.will
                     self.route(wt, wp, wq, wr)
@@ -688,6 +738,111 @@ class MqttBroker:
                 c.close()
             except OSError:
                 pass
+
+    def _handle(self, sess: "_Session", c, t: int, flags: int, body: bytes) -> bool:
+        """One packet of a connected session (everything but forwarded QoS 0 runs); False on
+        DISCONNECT."""
+        if t == PUBLISH:
+            topic, qos, pid, retain, _dup, payload = parse_publish(flags, body)
+            if qos == 2:
+                if pid not in sess.in_qos2:
+                    sess.in_qos2.add(pid)
+                    self.route(topic, payload, qos, retain)
+                self._send(sess, c, packet(PUBREC, 0, struct.pack("!H", pid)))
+                return True
+            self.route(topic, payload, qos, retain)
+            if qos == 1:
+                self._send(sess, c, packet(PUBACK, 0, struct.pack("!H", pid)))
+        elif t == PUBREL:
+            sess.in_qos2.discard(struct.unpack("!H", body[:2])[0])
+            self._send(sess, c, packet(PUBCOMP, 0, body[:2]))
+        elif t in (PUBACK, PUBCOMP):
+            with sess.wlock:
+                sess.out.pop(struct.unpack("!H", body[:2])[0], None)
+        elif t == PUBREC:
+            pid = struct.unpack("!H", body[:2])[0]
+            rel = packet(PUBREL, 2, body[:2])
+            with sess.wlock:
+                if pid in sess.out:
+                    sess.out[pid] = ["pubcomp", rel]
+            self._send(sess, c, rel)
+        elif t == SUBSCRIBE:
+            pid, pos, granted, new = body[:2], 2, bytearray(), []
+            while pos < len(body):
+                ln = struct.unpack("!H", body[pos:pos + 2])[0]
+                filt = body[pos + 2:pos + 2 + ln].decode()
+                q = body[pos + 2 + ln] & 3
+                pos += 3 + ln
+                if q == 3 or not filt:
+                    granted.append(0x80)
+                    continue
+                with self._lock:
+                    sess.subs[filt] = q
+                    self._route_cache.clear()
+                granted.append(q)
+                new.append((filt, q))
+            self._send(sess, c, packet(SUBACK, 0, pid + bytes(granted)))
+            with self._lock:
+                retained = [(tp, p, rq) for tp, (p, rq) in self._retained.items()]
+            for filt, q in new:                     # retained messages of the new filters
+                for tp, p, rq in retained:
+                    if topic_matches(filt, tp):
+                        self._deliver(sess, tp, p, min(q, rq), True)
+        elif t == UNSUBSCRIBE:
+            pid, pos = body[:2], 2
+            while pos < len(body):
+                ln = struct.unpack("!H", body[pos:pos + 2])[0]
+                with self._lock:
+                    sess.subs.pop(body[pos + 2:pos + 2 + ln].decode(), None)
+                    self._route_cache.clear()
+                pos += 2 + ln
+            self._send(sess, c, packet(UNSUBACK, 0, pid))
+        elif t == PINGREQ:
+            self._send(sess, c, packet(PINGRESP, 0, b""))
+        elif t == DISCONNECT:
+            return False
+        return True
+
+    def _targets(self, topic: bytes) -> tuple:
+        """Sessions subscribed to ``topic`` (cached per topic until a subscription or session
+        changes); a session granted QoS 0 or more receives a QoS 0 publish at QoS 0."""
+        t = self._route_cache.get(topic)
+        if t is None:
+            ts = topic.decode()
+            with self._lock:
+                t = tuple(s for s in self._sessions.values() if any(topic_matches(f, ts) for f in s.subs))
+                if len(self._route_cache) > 65536:
+                    self._route_cache.clear()
+                self._route_cache[topic] = t
+        return t
+
+    def _forward_run(self, data: bytes, pkts: list, k: int) -> int:
+        """Forward the QoS 0 / non-retained PUBLISH packets from ``pkts[k]`` on while their topics
+        have the same subscribers (byte-identical to what ``route`` would send them); returns the
+        index after the run."""
+        n = len(pkts)
+        start = k
+        tg = None
+        while k < n:
+            t, flags, a0, bs, e = pkts[k]
+            if t != PUBLISH or flags & 0x07:
+                break
+            tl = (data[bs] << 8) | data[bs + 1]
+            x = self._targets(data[bs + 2:bs + 2 + tl])
+            if tg is None:
+                tg = x
+            elif x is not tg and x != tg:
+                break
+            k += 1
+        self.published += k - start
+        if tg:
+            chunk = data[pkts[start][2]:pkts[k - 1][4]]
+            for s in tg:
+                with s.wlock:
+                    conn = s.conn
+                if conn is not None:
+                    self._send(s, conn, chunk)
+        return k
 
     def _deliver(self, sess: _Session, topic: str, payload: bytes, qos: int, retain: bool = False):
         # the connection check and the in-flight / offline bookkeeping happen under the session's

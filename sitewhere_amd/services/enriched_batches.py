@@ -219,6 +219,19 @@ class EnrichedBatchReader:
             cap, tcap = max(cap, need + 4096), max(tcap, need + 4096)
         return None
 
+    def _buf(self, name: str, n: int, dtype) -> np.ndarray:
+        """A scratch / output array of this thread, grown as needed and reused across calls (fresh
+        tens of megabytes per block cost more in page faults than the JSON writing)."""
+        tl = self.__dict__.get("_tl")
+        if tl is None:
+            with self._lock:
+                tl = self.__dict__.setdefault("_tl", threading.local())
+        bufs = tl.__dict__.setdefault("bufs", {})
+        a = bufs.get(name)
+        if a is None or len(a) < n:
+            a = bufs[name] = np.empty(int(n * 1.25) + 64, dtype)
+        return a
+
     def select_json(self, value, selector, topic: str | None = None, threads: int = 1):
         """A durable batch record's rows that pass ``selector(boot) -> (event-type bit mask, keep per
         assignment index or None, keep for indexes beyond it)`` as :meth:`outbound_json` documents,
@@ -226,7 +239,8 @@ class EnrichedBatchReader:
         packed columns, only kept rows are decoded; pages on ``threads`` threads): (payload bytes,
         offsets, topic bytes, offsets, kept rows, block rows), or None where the record needs the
         decoded path (not a durable block, or rows the native writer leaves to Python).  Dictionary
-        entries the consumer has not seen are resolved from event management, as :meth:`columns`."""
+        entries the consumer has not seen are resolved from event management, as :meth:`columns`.
+        The arrays returned are this thread's reused buffers: valid until its next call."""
         from .._native import native
         buf = memoryview(value).cast("B") if not isinstance(value, (bytes, bytearray)) else value
         if bytes(buf[:4]) != b"SWD1":
@@ -245,19 +259,22 @@ class EnrichedBatchReader:
         tb = np.frombuffer(tpl + b"\0", np.uint8)
         P = lambda a: a.ctypes.data  # noqa: E731
         n_rows = int(sg.header(blk)["n_rows"])
-        cap, tcap = 480 * n_rows + 4096, (len(tpl) + 96) * n_rows + 64
+        threads = max(1, int(threads))
+        scap, tscap = 600 * n_rows + 4096 * threads, (len(tpl) + 100) * n_rows + 4096 * threads
         counts, miss = np.zeros(3, np.int64), np.zeros(1 << 16, np.int64)
-        for _ in range(4):
+        for _ in range(6):
             etmask, keep, keep_default = selector(boot)
             n_keep = len(keep) if keep is not None else 0
             keep = np.ascontiguousarray(keep if keep is not None else np.zeros(1, bool), np.uint8)
             n_asg, (ah, ao, ap), n_names, (nh, no, npr), (rh, ro, rp), known = self._tables(boot)
-            out, ooff = np.empty(cap, np.uint8), np.empty(n_rows + 1, np.int64)
-            tout, toff = np.empty(tcap, np.uint8), np.empty(n_rows + 1, np.int64)
+            scratch, tscratch = self._buf("scratch", scap, np.uint8), self._buf("tscratch", tscap, np.uint8)
+            out, ooff = self._buf("out", scap, np.uint8), self._buf("ooff", n_rows + 1, np.int64)
+            tout, toff = self._buf("tout", tscap, np.uint8), self._buf("toff", n_rows + 1, np.int64)
             k = int(native().swjson_select_block(P(blk), int(etmask), P(keep), n_keep, int(bool(keep_default)), P(known),
                                                  n_asg, P(ah), P(ao), P(ap), P(nh), P(no), P(npr), n_names, P(rh),
-                                                 P(ro), P(rp), P(tb), len(tpl), int(threads), P(out), cap, P(ooff),
-                                                 P(tout) if topic is not None else None, tcap, P(toff), P(counts),
+                                                 P(ro), P(rp), P(tb), len(tpl), threads, P(scratch), len(scratch),
+                                                 P(tscratch), len(tscratch), P(out), len(out), P(ooff),
+                                                 P(tout) if topic is not None else None, len(tout), P(toff), P(counts),
                                                  P(miss), len(miss)))
             if k >= 0:
                 kept = int(counts[0])
@@ -276,7 +293,7 @@ class EnrichedBatchReader:
                         self._ver[boot] = self._ver.get(boot, 0) + 1
                 continue
             if k > -(1 << 40):                  # a buffer too small
-                cap = tcap = max(cap, tcap, -k + 4096)
+                scap = tscap = max(scap, tscap, -k + 4096)
                 continue
             return None
         return None

@@ -175,9 +175,9 @@ class MqttConnector(OutboundConnector):
 
         def frame(buf, off, tbuf, toff, n):
             from .._native import native
-            tb = np.frombuffer(bytes(tbuf), np.uint8) if len(tbuf) else np.zeros(1, np.uint8)
+            tb = np.ascontiguousarray(tbuf, np.uint8) if len(tbuf) else np.zeros(1, np.uint8)
             cap = len(buf) + len(tbuf) + 8 * n + 64
-            out = np.empty(cap, np.uint8)
+            out = reader._buf("mqtt_frames", cap, np.uint8)
             k = int(native().swmqtt_publish_qos0(tb.ctypes.data, toff.ctypes.data, buf.ctypes.data, off.ctypes.data,
                                                  n, 0, out.ctypes.data, cap))
             self.client.publish_framed_qos0(memoryview(out[:k]))
