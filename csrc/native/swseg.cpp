@@ -2265,3 +2265,80 @@ extern "C" int64_t swjson_select_block(const uint8_t* b, int32_t etmask, const u
   }
   return wj;
 }
+
+// ------------------------------------------------------------------------- threshold rules
+// Rows of a (verified) block whose measurement crosses a bound: event type Measurement, name id set
+// in `name_mask` (n_mask bytes), value < lo (has_lo) or > hi (has_hi) -- services/rule_processing.py
+// ThresholdRuleProcessor over the packed columns: only the event type, flags, name and value of the
+// measurement rows are unpacked, nothing else of the block is decoded.  Pages on `threads` workers.
+// Writes (row, assignment, value) in block order, at most cap; returns the number found (may exceed
+// cap: call again with room for it), -1 on a page that does not decode.
+extern "C" int64_t swseg_threshold_rows(const uint8_t* b, const uint8_t* name_mask, int64_t n_mask, double lo,
+                                        double hi, int32_t has_lo, int32_t has_hi, int32_t threads, int64_t* out_rows,
+                                        int32_t* out_asg, double* out_val, int64_t cap) {
+  SwSegBlockHdr h;
+  memcpy(&h, b, sizeof(h));
+  const uint32_t* pt = (const uint32_t*)(b + 64);
+  const int64_t np = h.n_pages;
+  int T = threads > 0 ? threads : 1;
+  if (T > 32) T = 32;
+  if ((int64_t)T > np) T = (int)(np > 0 ? np : 1);
+  struct Hit { int64_t row; int32_t asg; double v; };
+  std::vector<std::vector<Hit>> hits((size_t)T);
+  auto work = [&](int w) {
+    std::vector<Hit>& out = hits[(size_t)w];
+    for (int64_t p = np * w / T; p < np * (w + 1) / T; ++p) {
+      const uint8_t* pg = b + pt[p];
+      SwSegPageHdr ph;
+      memcpy(&ph, pg, sizeof(ph));
+      const int mode = ph.alt_mode;
+      const SwSegCol& cv = ph.cols[SEG_MXV];
+      const uint8_t* vw = pg + cv.data_off;
+      const uint8_t* xi = vw + 8 * seg_col_words(cv.count, cv.bits);
+      const uint8_t* xr = xi + ((2u * cv.n_exc + 7u) & ~7u);
+      uint32_t xc = 0, cn = 0, cm = 0;
+      for (uint32_t j = 0; j < ph.n_rows; ++j) {
+        const uint8_t et = (uint8_t)seg_unord(col_int(pg, ph.cols[SEG_ETYPE], j));
+        const uint32_t f = (uint32_t)seg_unord(col_int(pg, ph.cols[SEG_FLAGS], j));
+        const bool hn = seg_member(SEG_NAME, et, f, mode), hv = seg_member(SEG_MXV, et, f, mode);
+        if (et == 0 && hn && hv) {
+          const int64_t nm = seg_unord(col_int(pg, ph.cols[SEG_NAME], cn));
+          if (nm >= 0 && nm < n_mask && name_mask[nm]) {
+            double v;
+            for (; xc < cv.n_exc; ++xc) {
+              uint16_t x;
+              memcpy(&x, xi + 2 * xc, 2);
+              if (x >= cm) break;
+            }
+            uint16_t x = 0xffff;
+            if (xc < cv.n_exc) memcpy(&x, xi + 2 * xc, 2);
+            if (xc < cv.n_exc && x == cm) {
+              uint64_t raw;
+              memcpy(&raw, xr + 8 * xc, 8);
+              v = sw_bits_f64(raw);
+            } else {
+              v = seg_dec_value(seg_unord(cv.base + unpack(vw, cm, cv.bits)), cv.exp);
+            }
+            if ((has_lo && v < lo) || (has_hi && v > hi))
+              out.push_back({p * SEG_PAGE_ROWS + j, (int32_t)seg_unord(col_int(pg, ph.cols[SEG_ASG], j)), v});
+          }
+        }
+        cn += hn;
+        cm += hv;
+      }
+    }
+  };
+  if (T <= 1) work(0);
+  else {
+    std::vector<std::thread> th;
+    for (int w = 0; w < T; ++w) th.emplace_back(work, w);
+    for (auto& x : th) x.join();
+  }
+  int64_t k = 0;
+  for (const auto& v : hits)
+    for (const Hit& x : v) {
+      if (k < cap) { out_rows[k] = x.row; out_asg[k] = x.asg; out_val[k] = x.v; }
+      ++k;
+    }
+  return k;
+}

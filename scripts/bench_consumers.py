@@ -153,24 +153,26 @@ def main():
                      "delivered": mq.delivered, "filtered": mq.filtered, "received_by_subscriber": got,
                      "delivered_per_s": round(mq.delivered / dt, 1)}
 
-    # ---- threshold rule -> batched alerts into a durable store (the API add path)
-    d = tempfile.mkdtemp(prefix="sw-soak-")
-    st = DurableEventStore(d, direct=False)
-    alerts = [0]
+    # ---- threshold rule -> batched alerts into a durable store (the API add path): a rare bound
+    # (~0.01% of the rule's rows: the scan rate) and a frequent one (~5%: the alert add path)
+    for name, bound in (("threshold_rule_rare", 999.9), ("threshold_rule", 950.0)):
+        d = tempfile.mkdtemp(prefix="sw-soak-")
+        st = DurableEventStore(d, direct=False)
+        alerts = [0]
 
-    class Api:
-        def add_alert_batch(self, pairs):
-            evs = [DeviceAlert(device_assignment_id=aid, type=r["type"], message=r["message"], source="System",
-                               event_date=now) for aid, r in pairs]
-            st.add_events(evs)
-            alerts[0] += len(evs)
-    thr = ThresholdRuleProcessor("thr", [{"measurement": "mx.metric0", "max": 950.0, "alertType": "hot"}])
-    thr.events_api = lambda: Api()
-    reader2 = EnrichedBatchReader(None)
-    n, dt = soak(lambda r: thr.process_records(reader2, r), a.seconds)
-    out["threshold_rule"] = {"events_per_s": round(n * per_batch / dt, 1), "batches": n, "seconds": round(dt, 2),
-                             "alerts": alerts[0], "alerts_per_s": round(alerts[0] / dt, 1)}
-    st.close()
+        class Api:
+            def add_alert_batch(self, pairs):
+                evs = [DeviceAlert(device_assignment_id=aid, type=r["type"], message=r["message"], source="System",
+                                   event_date=now) for aid, r in pairs]
+                st.add_events(evs)
+                alerts[0] += len(evs)
+        thr = ThresholdRuleProcessor("thr", [{"measurement": "mx.metric0", "max": bound, "alertType": "hot"}])
+        thr.events_api = lambda: Api()
+        reader2 = EnrichedBatchReader(None)
+        n, dt = soak(lambda r: thr.process_records(reader2, r), a.seconds)
+        out[name] = {"events_per_s": round(n * per_batch / dt, 1), "batches": n, "seconds": round(dt, 2),
+                     "alerts": alerts[0], "alerts_per_s": round(alerts[0] / dt, 1)}
+        st.close()
     print(json.dumps(out), flush=True)
 
 

@@ -232,16 +232,10 @@ class EnrichedBatchReader:
             a = bufs[name] = np.empty(int(n * 1.25) + 64, dtype)
         return a
 
-    def select_json(self, value, selector, topic: str | None = None, threads: int = 1):
-        """A durable batch record's rows that pass ``selector(boot) -> (event-type bit mask, keep per
-        assignment index or None, keep for indexes beyond it)`` as :meth:`outbound_json` documents,
-        straight from the block (``swjson_select_block``: event type and assignment are read from the
-        packed columns, only kept rows are decoded; pages on ``threads`` threads): (payload bytes,
-        offsets, topic bytes, offsets, kept rows, block rows), or None where the record needs the
-        decoded path (not a durable block, or rows the native writer leaves to Python).  Dictionary
-        entries the consumer has not seen are resolved from event management, as :meth:`columns`.
-        The arrays returned are this thread's reused buffers: valid until its next call."""
-        from .._native import native
+    def durable_block(self, value):
+        """(boot, verified block) of a durable batch record with its dictionary deltas applied, or
+        None for another record kind (a columnar batch).  A record handed over in process (a
+        zero-copy view) is the engine's own sealed block; bytes from a bus are verified."""
         buf = memoryview(value).cast("B") if not isinstance(value, (bytes, bytearray)) else value
         if bytes(buf[:4]) != b"SWD1":
             return None
@@ -253,6 +247,65 @@ class EnrichedBatchReader:
                 raise ValueError(f"corrupt event block (code {rc})")
         boot = int(sg.header(blk)["boot"])
         self._apply(boot, d)
+        return boot, blk
+
+    def threshold_rows(self, value, rules, threads: int = 1):
+        """Per threshold rule ({measurement, min?, max?}): (assignment context, value) of the rows of
+        a durable batch record whose measurement is out of bounds (``swseg_threshold_rows``: only the
+        measurement rows' type, name and value are unpacked), or None for a record that is not a
+        durable block.  Contexts the consumer has not seen are resolved as :meth:`columns` does."""
+        from .._native import native
+        got = self.durable_block(value)
+        if got is None:
+            return None
+        boot, blk = got
+        self.batches += 1
+        self.rows += int(sg.header(blk)["n_rows"])
+        out = []
+        for r in rules:
+            with self._lock:
+                names = self._names.get(boot, {})
+                ids = [int(i) for i, v in names.items() if v == r["measurement"]]
+            lo, hi = r.get("min"), r.get("max")
+            if not ids or (lo is None and hi is None):
+                out.append([])
+                continue
+            mask = np.zeros(max(ids) + 1, np.uint8)
+            mask[ids] = 1
+            cap = 4096
+            while True:
+                rows, asg, vals = np.empty(cap, np.int64), np.empty(cap, np.int32), np.empty(cap, np.float64)
+                k = int(native().swseg_threshold_rows(blk.ctypes.data, mask.ctypes.data, len(mask),
+                                                      float(lo if lo is not None else 0.0),
+                                                      float(hi if hi is not None else 0.0), int(lo is not None),
+                                                      int(hi is not None), int(threads), rows.ctypes.data,
+                                                      asg.ctypes.data, vals.ctypes.data, cap))
+                if k < 0:
+                    raise ValueError("event block decode failed")
+                if k <= cap:
+                    break
+                cap = k
+            asg, vals = asg[:k], vals[:k]
+            if k:
+                self._resolve(boot, np.unique(asg), [])
+            ctx = self._asg.get(boot, {})
+            out.append([(ctx.get(int(a)), float(v)) for a, v in zip(asg.tolist(), vals.tolist())])
+        return out
+
+    def select_json(self, value, selector, topic: str | None = None, threads: int = 1):
+        """A durable batch record's rows that pass ``selector(boot) -> (event-type bit mask, keep per
+        assignment index or None, keep for indexes beyond it)`` as :meth:`outbound_json` documents,
+        straight from the block (``swjson_select_block``: event type and assignment are read from the
+        packed columns, only kept rows are decoded; pages on ``threads`` threads): (payload bytes,
+        offsets, topic bytes, offsets, kept rows, block rows), or None where the record needs the
+        decoded path (not a durable block, or rows the native writer leaves to Python).  Dictionary
+        entries the consumer has not seen are resolved from event management, as :meth:`columns`.
+        The arrays returned are this thread's reused buffers: valid until its next call."""
+        from .._native import native
+        got = self.durable_block(value)
+        if got is None:
+            return None
+        boot, blk = got
         tpl = b""
         if topic is not None:
             tpl = topic.replace("{deviceToken}", "\x01").replace("{eventType}", "\x02").encode()

@@ -154,6 +154,25 @@ class ThresholdRuleProcessor(RuleProcessor):
                     pairs.append((ev.device_assignment_id, self._request(r, ev.name, ev.value)))
         self.raise_alerts(pairs)
 
+    def process_records(self, reader, recs):
+        """Durable engine batches natively (``EnrichedBatchReader.threshold_rows``: the block's
+        measurement rows are tested where they lie packed, nothing else is decoded); anything else
+        as :meth:`RuleProcessor.process_records`."""
+        from .enriched_batches import is_batch
+        rest, pairs = [], []
+        for rec in recs:
+            got = reader.threshold_rows(rec.value, self.rules) if is_batch(rec.value) else None
+            if got is None:
+                rest.append(rec)
+                continue
+            for r, hits in zip(self.rules, got):
+                for a, v in hits:
+                    if a:
+                        pairs.append((a[0], self._request(r, r["measurement"], v)))
+        self.raise_alerts(pairs)
+        if rest:
+            super().process_records(reader, rest)
+
     def process_columns(self, reader, cols):
         """Measurement rows of an engine batch against each rule on the columns (name id and value
         masks); only the rows out of bounds become alerts, all of the batch's in one add."""

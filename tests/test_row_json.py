@@ -204,3 +204,29 @@ def test_native_block_selection_equals_column_filters():
             assert bytes(buf) == bytes(wb) and np.array_equal(off, wo)
             assert bytes(tbuf) == bytes(wt) and np.array_equal(toff, wto)
             assert r.engine.em.calls == 1
+
+
+def test_native_threshold_rows_equal_column_rule():
+    """``ThresholdRuleProcessor`` over a durable block natively (``swseg_threshold_rows``) raises the
+    same alerts, in the same order, as its column form over the decoded block -- min, max and both
+    bounds, a name the batch lacks, and exception-coded (non-decimal) values."""
+    from sitewhere_amd.services.rule_processing import ThresholdRuleProcessor
+    blks, names, e = _block()
+    asg = {i: [f"asg-{i}", f"dev-id-{i}", None, None, None, f"dev-{i:010d}", None] for i in range(N_DEV)}
+    rec = sg.encode_durable_batch(blks[0], 0x5eed, asg=asg, names=names)
+    mx = sorted({v for v in names.values() if v.startswith("mx.")} | {"témp"})
+    rules = [{"measurement": mx[0], "max": 500.0, "alertType": "hi"}, {"measurement": mx[-1], "min": 100.0},
+             {"measurement": mx[1 % len(mx)], "min": 200.0, "max": 800.0}, {"measurement": "absent", "max": 1.0}]
+    got = {}
+    for mode in ("native", "columns"):
+        p = ThresholdRuleProcessor("t", rules)
+        seen = []
+        p.raise_alerts = lambda pairs, seen=seen: seen.extend(pairs)
+        r = EnrichedBatchReader(_StubEngine())
+        if mode == "native":
+            p.process_records(r, [type("R", (), {"value": rec, "key": None})()])
+        else:
+            p.process_columns(r, r.columns(rec, strings=False))
+        got[mode] = seen
+    assert got["native"] == got["columns"]
+    assert len(got["native"]) > 50
