@@ -95,15 +95,72 @@ def _trailer_diag(store, ib, lost) -> list:
                     hd = sg.parse_trailer(disk_tr)
                     d["trailer_sections"] = {k: int(hd[k]) for k in ("off_pages", "off_alt_dir", "off_alt", "n_alt",
                                                                       "alt_bits", "alt_pbits", "n_pages")}
+                d["gpu_trailer"] = _tr_summary(disk_tr)
+                if cpu_tr is not None:
+                    d["cpu_trailer"] = _tr_summary(cpu_tr)
+                    hg, hc = sg.parse_trailer(disk_tr), sg.parse_trailer(cpu_tr)
+                    if int(hg["n_alt"]) == int(hc["n_alt"]) and int(hg["alt_bits"]) == int(hc["alt_bits"]):
+                        nd = (1 << int(hg["alt_bits"])) + 1
+                        dg = disk_tr[int(hg["off_alt_dir"]):int(hg["off_alt_dir"]) + 4 * nd].view(np.uint32)
+                        dc = cpu_tr[int(hc["off_alt_dir"]):int(hc["off_alt_dir"]) + 4 * nd].view(np.uint32)
+                        nw = (int(hg["n_alt"]) * 26 + 63) // 64
+                        wg = np.frombuffer(disk_tr[int(hg["off_alt"]):int(hg["off_alt"]) + 8 * nw].tobytes(), np.uint64)
+                        wc = np.frombuffer(cpu_tr[int(hc["off_alt"]):int(hc["off_alt"]) + 8 * nw].tobytes(), np.uint64)
+                        bad = np.nonzero(wg != wc)[0]
+                        d["alt_dir_differ"] = int((dg != dc).sum())
+                        d["alt_words_differ"] = int(len(bad))
+                        d["alt_words_first_last_bad"] = [int(bad[0]), int(bad[-1])] if len(bad) else None
+                        pg_g, pg_c = sg.parse_trailer(disk_tr)["pages"], sg.parse_trailer(cpu_tr)["pages"]
+                        d["pages_differ"] = int((pg_g != pg_c).sum()) if len(pg_g) == len(pg_c) else "len"
                 for h in sorted(hit)[:6]:
                     r = rows.get(h)
                     d["ids"].append({"row": r, "page": None if r is None else r // sg.PAGE_ROWS,
                                      "disk": pages_of(disk_tr.ctypes.data, h),
                                      "mem": pages_of(int(mem_tr[0]), h) if mem_tr is not None else None,
-                                     "cpu": pages_of(cpu_tr.ctypes.data, h) if cpu_tr is not None else None})
+                                     "cpu": pages_of(cpu_tr.ctypes.data, h) if cpu_tr is not None else None,
+                                     "gpu_bucket": _bucket(disk_tr, h),
+                                     "cpu_bucket": _bucket(cpu_tr, h) if cpu_tr is not None else None})
                 out.append(d)
                 target -= hit
     return out
+
+
+def _tr_summary(tr) -> dict:
+    from sitewhere_amd.persistence import segments as sg
+    h = sg.parse_trailer(tr)
+    return {k: (int(h[k]) if not hasattr(h[k], "__len__") else None) for k in
+            ("n_rows", "n_pages", "n_alt", "alt_bits", "alt_pbits", "off_alt_dir", "off_alt", "bytes")}
+
+
+def _bucket(tr, hv: int) -> dict:
+    """The id's directory bucket in a trailer: its size and the (fingerprint, page) entries whose
+    fingerprint is the id's."""
+    import numpy as np
+    from sitewhere_amd.persistence import segments as sg
+    h = sg.parse_trailer(tr)
+    bits, pb = int(h["alt_bits"]), int(h["alt_pbits"])
+    EB = 26
+    fb = EB - pb
+    b = (hv >> (64 - bits)) if bits else 0
+    want = (hv >> (64 - bits - fb)) & ((1 << fb) - 1)
+    t = np.ascontiguousarray(tr)
+    d0 = int(h["off_alt_dir"])
+    dirs = t[d0:d0 + 4 * ((1 << bits) + 1)].view(np.uint32)
+    lo, hi = int(dirs[b]), int(dirs[b + 1])
+    words = t[int(h["off_alt"]):].view(np.uint64) if (len(t) - int(h["off_alt"])) % 8 == 0 else \
+        np.frombuffer(t[int(h["off_alt"]):].tobytes() + b"\0" * 8, np.uint64)
+    ents = []
+    for e in range(lo, min(hi, int(h["n_alt"]))):
+        bp = e * EB
+        w0 = int(words[bp >> 6])
+        sh = bp & 63
+        v = w0 >> sh
+        if sh + EB > 64:
+            v |= int(words[(bp >> 6) + 1]) << (64 - sh)
+        v &= (1 << EB) - 1
+        ents.append((v >> pb, v & ((1 << pb) - 1)))
+    return {"bucket": int(b), "size": hi - lo, "matches": [p for f, p in ents if f == want],
+            "fps_sample": [f for f, _ in ents[:4]], "want_fp": int(want)}
 
 
 def _strip(blk):
