@@ -391,6 +391,9 @@ __global__ __launch_bounds__(IX_PREP_BLK) void k_ix_prep(SwIxArgs a) {
       for (int32_t i = threadIdx.x; i < span; i += IX_PREP_BLK) hrow[obase + i] = lc[i];
     __syncthreads();
   }
+  // every wave's count is in lalt before thread 0 reads it: the passes above synchronise only when
+  // some context dimension is indexed (a tenant without customers / areas / assets has none)
+  __syncthreads();
   if (threadIdx.x == 0 && lalt) atomicAdd(&a.sc->n_alt, lalt);
 }
 

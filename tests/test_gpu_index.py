@@ -131,16 +131,65 @@ def test_gpu_trailer_large_step(n_cust):
     spec = FleetSpec(prefix="dev-", n_devices=n_dev, p_location=0.25, p_alert=0.05, p_unregistered=0.005,
                      with_alternate_id=True, lat0=33.0, lon0=-85.0, span_deg=2.0, p_meta=0.1)
     now = 1_700_000_001_000
-    raw, off = gen_payloads(spec, 1 << 20, now - 30_000, seed=7)
-    raw = np.concatenate([raw, np.zeros(64, np.uint8)])
-    rg = g.step(raw, off, now, presence=False)
-    bg = g.encode_block(now, rg, boot=0xabc)
-    assert sg.verify(bg) == 0
-    ref = sg.index_block(_strip_trailer(bg), g.ctx_table())
-    assert np.array_equal(ref, bg)
+    for k in range(3):          # consecutive large steps: the build's scratch re-arms between them
+        raw, off = gen_payloads(spec, 1 << 20, now - 30_000, seed=7 + k)
+        raw = np.concatenate([raw, np.zeros(64, np.uint8)])
+        rg = g.step(raw, off, now + k, presence=False)
+        bg = g.encode_block(now + k, rg, boot=0xabc)
+        assert sg.verify(bg) == 0
+        ref = sg.index_block(_strip_trailer(bg), g.ctx_table())
+        if not np.array_equal(ref, bg):
+            bad = np.nonzero(ref != bg)[0] if len(ref) == len(bg) else [len(ref), len(bg)]
+            pytest.fail(f"step {k}: trailer differs from the C++ builder ({len(bad)} bytes, first {bad[0]})")
     toff = sg.trailer_offset(bg)
     tr = sg.parse_trailer(bg[toff:])
     assert tr["n_alt"] > 1_000_000 - 20_000
     assert [int(x) for x in tr["n_keys"]][:2] == [n_cust * 3, 31 * 3]    # measurement / location / alert
     # index bytes per row (the disk cost of the indexes)
     assert (len(bg) - toff) / rg.n_persisted < 5.0
+
+
+def test_gpu_framed_blocks_trailers_match_cpu_builder():
+    """The service tenant's path at the 1M shape: overlapped ``submit_framed`` steps from pinned
+    zero-copy records with blocks encoded on the GPU (``encode_blocks``), fresh alternate ids per
+    record -- every returned block's trailer equals the C++ builder's over the same block, and every
+    stored id is found through it."""
+    from sitewhere_amd.persistence import segments as sg
+    from sitewhere_amd.pipeline.bus_io import RawBatchRecord, parse_raw_batch
+    from sitewhere_amd.pipeline.config import EngineConfig
+    from sitewhere_amd.pipeline.fleet import FleetSpec, fingerprints, gen_payloads, gen_tokens, stamp_alt_epoch
+    from sitewhere_amd.pipeline.framing import varint_lengths
+    from sitewhere_amd.pipeline.gpu_engine import GpuInboundEngine
+    n_dev = 1 << 20
+    cfg = EngineConfig(max_msgs=1 << 20, rec_cap=(1 << 20) + 4096, gen_cap=1 << 19, max_devices=n_dev + 65536,
+                       max_assignments=n_dev + 65536, store_cap=1 << 23, dedup_slots=1 << 22, name_slots=1 << 12,
+                       state_slots=1 << 24, dedup_filter_ids=1 << 24, dedup_filter_gens=4)
+    g = GpuInboundEngine(cfg, device="cuda:0")
+    heap, offs = gen_tokens("dev-", 0, n_dev)
+    lo, hi = fingerprints(heap, offs)
+    d = g.register_devices(lo, hi)
+    g.set_assignments(d, d)
+    g.encode_blocks, g.block_boot = True, 0x5eed
+    spec = FleetSpec(prefix="dev-", n_devices=n_dev, p_location=0.25, p_alert=0.05, p_unregistered=0.005,
+                     with_alternate_id=True)
+    now = 1_700_000_001_000
+    base = [gen_payloads(spec, 1 << 20, now - 30_000, seed=11 + b) for b in range(3)]
+    recs, got = [], []
+    for k in range(6):
+        raw, off = base[k % 3]
+        raw = np.concatenate([raw, np.zeros(64, np.uint8)])
+        stamp_alt_epoch(raw, off, (0x50AC << 48) | k)
+        rec = RawBatchRecord(raw[:int(off[-1])], varint_lengths(off), len(off) - 1, pinned=True)
+        recs.append(rec)
+        got += g.submit_framed(parse_raw_batch(rec.buf.numpy()[:rec.value_len]), now + k, token=k, presence=False)
+    got += g.drain_framed()
+    assert [t for t, _ in got] == list(range(6))
+    for k, res in got:
+        blk = np.ascontiguousarray(res.block)
+        assert sg.verify(blk) == 0
+        ref = sg.index_block(_strip_trailer(blk), g.ctx_table())
+        if not np.array_equal(ref, blk):
+            n = min(len(ref), len(blk))
+            bad = np.nonzero(ref[:n] != blk[:n])[0]
+            pytest.fail(f"step {k}: GPU trailer differs from the C++ builder (lengths {len(ref)} / {len(blk)}, "
+                        f"{len(bad)} bytes, first at trailer byte {bad[0] - sg.trailer_offset(blk) if len(bad) else None})")
