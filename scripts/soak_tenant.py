@@ -406,8 +406,18 @@ def main():
         tr = [x for x in ib.trace if len(x) == 9]
         gap = np.diff(np.asarray([x[0] for x in tr])) * 1000 if len(tr) > 1 else np.zeros(0)
         if len(gap):
-            trace = {f"submit_interval_p{q}_ms": round(float(np.percentile(gap, q)), 3) for q in (50, 90, 99)}
+            trace.update({f"submit_interval_p{q}_ms": round(float(np.percentile(gap, q)), 3) for q in (50, 90, 99)})
             trace["submit_interval_max_ms"] = round(float(gap.max()), 3)
+            # per stage of a batch's life (submit, engine completion, store thread, durable commit):
+            # median ms between consecutive trace stamps
+            st_ = np.diff(np.asarray([x[:9] for x in tr], np.float64), axis=1) * 1000
+            trace["stage_ms_p50"] = [round(float(x), 3) for x in np.median(st_, axis=0)]
+            trace["stage_ms_p99"] = [round(float(x), 3) for x in np.percentile(st_, 99, axis=0)]
+    ft = getattr(type(ib.engine), "framed_trace", None)
+    if ft:
+        n_sub = max(1, k)
+        trace["framed_phase_ms_per_submit"] = {kk: round(v * 1000 / n_sub, 3) for kk, v in ft.items()}
+    trace["pin_stats"] = {kk: v for kk, v in ib.engine.__dict__.items() if kk.startswith("pin_stats")}
     cap = ecfg.dedup_filter_gens * ecfg.dedup_filter_ids
     out = {"metric": "tenant_soak_events_per_sec", "template": args.template, "devices": args.devices,
            "batch": args.batch, "p_unregistered": args.p_unregistered, "alt_ids": True, "via_bus": True,
