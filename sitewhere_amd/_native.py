@@ -344,5 +344,42 @@ def gpu():
         return lib
 
 
+# launch calls that only enqueue work (microseconds): bound through PyDLL, they keep the GIL
+_GPU_BLOCKING = {"sw_sdma_wait"}
+_gpu_gil = None
+
+
+class _GilBound:
+    """The kernel library with its enqueue-only entry points bound through ``ctypes.PyDLL`` (the GIL
+    stays held: no release / re-acquire per launch) and the blocking ones (``sw_sdma_wait``) through
+    ``CDLL``.  A CDLL call gives the GIL up and must win it back from the tenant's busy Python
+    threads (store, router, consumers): with the interpreter's 5 ms switch interval an engine step's
+    ~20 launches measured ~4 ms of GIL waits per 1M-payload step on a live tenant (profiles/r6_soak)."""
+
+    def __init__(self, cdll):
+        self._c = cdll
+        self._p = ctypes.PyDLL(cdll._name)
+
+    def __getattr__(self, name):
+        f = getattr(self._c, name)
+        if name in _GPU_BLOCKING or name.startswith("_"):
+            return f
+        g = getattr(self._p, name)
+        g.restype, g.argtypes = f.restype, f.argtypes
+        setattr(self, name, g)
+        return g
+
+
+def gpu_gil():
+    """:func:`gpu` with enqueue-only calls keeping the GIL (see :class:`_GilBound`)."""
+    global _gpu_gil
+    if _gpu_gil is None:
+        lib = gpu()
+        with _lock:
+            if _gpu_gil is None:
+                _gpu_gil = _GilBound(lib)
+    return _gpu_gil
+
+
 def gpu_library_path() -> Path:
     return LIB_DIR / "libswgpu.so"

@@ -21,7 +21,7 @@ import time
 import numpy as np
 import torch
 
-from .._native import gpu as gpu_lib
+from .._native import gpu_gil as gpu_lib
 from ..models.columnar import EVENT_REC, N_STATS, OUT_REC, NAME_REF, OUT_REC_SIZE, ST_RECHECK, STR_REF, WIRE_REC
 from ..ops.engine_abi import SwEngineArgs
 from .config import EngineConfig
