@@ -1823,6 +1823,33 @@ __global__ void k_step_snapshot(const uint32_t* __restrict__ scalars, const uint
   else if (t == 24 || t == 25) host[t] = (produced && rej_cnt) ? rej_cnt[t - 24] : 0u;
 }
 
+// The step's rejected records (SwEventRec, 80 B) and their statuses, gathered by rej_idx straight
+// into mapped host memory, bounded by the step's own reject count (scalars[5], read on the device) and
+// `cap`: the host reads them after the step's event, with no copy call and no synchronising read of
+// the count first (GpuInboundEngine.submit_framed).
+__global__ __launch_bounds__(256) void k_reject_pack(const uint4* __restrict__ recs, const int32_t* __restrict__ rej_idx,
+                                                      const uint8_t* __restrict__ status,
+                                                      const uint32_t* __restrict__ scalars, uint32_t cap,
+                                                      uint4* __restrict__ out, uint8_t* __restrict__ out_st) {
+  const uint32_t n = scalars[5] < cap ? scalars[5] : cap;
+  const uint32_t words = 5;                     // sizeof(SwEventRec) / 16
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n * words; w += gridDim.x * blockDim.x) {
+    const uint32_t i = w / words, q = w - i * words;
+    const int32_t r = rej_idx[i];
+    out[w] = recs[(int64_t)r * words + q];
+    if (q == 0) out_st[i] = status[r];
+  }
+}
+
+int sw_reject_pack(const void* recs, const int32_t* rej_idx, const uint8_t* status, const uint32_t* scalars,
+                   int64_t cap, void* out, uint8_t* out_st, hipStream_t s) {
+  static_assert(sizeof(SwEventRec) == 80, "k_reject_pack copies 5 x 16 B per record");
+  if (cap <= 0 || cap > 0xffffffffll / 5) return -1;
+  k_reject_pack<<<512, 256, 0, s>>>(reinterpret_cast<const uint4*>(recs), rej_idx, status, scalars, (uint32_t)cap,
+                                    reinterpret_cast<uint4*>(out), out_st);
+  return (int)hipGetLastError();
+}
+
 int sw_step_snapshot(const uint32_t* scalars, const uint32_t* seg_meta, const uint32_t* rej_cnt,
                      const uint32_t* n_carry, int32_t produced, uint32_t* host, hipStream_t s) {
   k_step_snapshot<<<1, 64, 0, s>>>(scalars, seg_meta, rej_cnt, n_carry, produced, host);

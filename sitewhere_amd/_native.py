@@ -340,6 +340,7 @@ def gpu():
         _proto(lib, "sw_ff_clear", c_int32, P, c_int64, c_int64, c_int64, P)
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
+        _proto(lib, "sw_reject_pack", c_int32, P, P, P, P, c_int64, P, P, P)
         _gpu = lib
         return lib
 

@@ -62,13 +62,15 @@ class HostBuffer:
 
 class _Submitted:
     """One batch in :meth:`GpuInboundEngine.submit_framed`'s pipeline."""
-    __slots__ = ("slot", "batch", "token", "small", "rows", "sig", "ev", "bmeta", "bbuf", "bsig", "bev", "now")
+    __slots__ = ("slot", "batch", "token", "small", "rows", "sig", "ev", "bmeta", "bbuf", "bsig", "bev", "now",
+                 "mapped")
 
     def __init__(self, slot, batch, token):
         self.slot, self.batch, self.token = slot, batch, token
         self.small = self.rows = self.sig = self.ev = None
         self.bmeta = self.bbuf = self.bsig = self.bev = None
         self.now = 0
+        self.mapped = False             # step snapshot + rejects written into the slot's mapped host memory
 
 
 class _FramedSlots:
@@ -934,7 +936,7 @@ class GpuInboundEngine(EngineBase):
             if prev is not None:                                             # batch k-1
                 fp.ev_comp[prev.slot].synchronize()
                 t0 = self._ft("wait_k1", t0)
-                prev.small = self._collect_small(host_view(prev.batch))
+                prev.small = self._collect_done(fp, prev)
                 t0 = self._ft("collect_k1", t0)
                 self._block_meta(prev)              # before batch k is queued: no wait on it
                 t0 = self._ft("block_meta_k1", t0)
@@ -947,6 +949,8 @@ class GpuInboundEngine(EngineBase):
             sub = _Submitted(b, batch, token)
             if self.encode_blocks:
                 sub.bmeta, sub.now = self.encode_block_async(b), now_ms
+            if self.world == 1:
+                self._snapshot_async(fp, b, sub)
             fp.ev_comp[b].record(cur)
             t0 = self._ft("step_enqueue", t0)
             if prev is not None:
@@ -975,7 +979,7 @@ class GpuInboundEngine(EngineBase):
                 s = fp.inflight.popleft()
                 if s.small is None:
                     fp.ev_comp[s.slot].synchronize()
-                    s.small = self._collect_small(host_view(s.batch))
+                    s.small = self._collect_done(fp, s)
                     self._block_meta(s)
                     self._framed_rows_start(s)
                 done.append(self._framed_finish(s))
@@ -985,6 +989,55 @@ class GpuInboundEngine(EngineBase):
     def framed_pending(self) -> int:
         fp = self.__dict__.get("_fp")
         return EngineBase.framed_pending.fget(self) + (len(fp.inflight) if fp is not None else 0)
+
+    # rejects per step read from the mapped snapshot; a step with more goes through _collect_small
+    MAPPED_REJECTS = 1 << 18
+
+    def _snapshot_async(self, fp, b: int, sub: "_Submitted"):
+        """Behind step ``sub`` on the current stream: its scalars and encoder meta
+        (``k_step_snapshot``) and its rejected records with their statuses (``k_reject_pack``) into
+        slot ``b``'s mapped host memory, so completing the step reads host memory only -- no
+        synchronising device reads (each one gives the GIL up and waits to win it back from the
+        tenant's other threads)."""
+        bufs = fp.__dict__.setdefault("snap", {})
+        cap = min(self.cfg.rec_cap, self.MAPPED_REJECTS)
+        m = bufs.get(b)
+        if m is None:
+            m = bufs[b] = (HostBuffer(self.lib, 256), HostBuffer(self.lib, cap * EVENT_REC.itemsize),
+                           HostBuffer(self.lib, cap))
+        snap, rej, st = m
+        st_ = self._stream()
+        sc = ctypes.c_void_p(_ptr(self.t["scalars"]))
+        meta = ctypes.c_void_p(sub.bmeta.data_ptr() if sub.bmeta is not None else 0)
+        rc = self.lib.sw_step_snapshot(sc, meta, None, None, 1, ctypes.c_void_p(snap.dev), st_)
+        if rc:
+            raise RuntimeError(f"sw_step_snapshot failed ({rc})")
+        rc = self.lib.sw_reject_pack(ctypes.c_void_p(_ptr(self.t["recs"])), ctypes.c_void_p(_ptr(self.t["rej_idx"])),
+                                     ctypes.c_void_p(_ptr(self.t["status"])), sc, cap, ctypes.c_void_p(rej.dev),
+                                     ctypes.c_void_p(st.dev), st_)
+        if rc:
+            raise RuntimeError(f"sw_reject_pack failed ({rc})")
+        sub.mapped = True
+
+    def _collect_done(self, fp, s: "_Submitted") -> dict:
+        """:meth:`_collect_small` of a completed framed step, from its mapped snapshot when it has one
+        (no device reads) -- unless the step learned names or rejected more than the snapshot holds."""
+        if not s.mapped:
+            return self._collect_small(host_view(s.batch))
+        snap, rej, st = fp.snap[s.slot]
+        v = snap.view(np.uint32, 32)
+        n_rej = int(v[5])
+        cap = min(self.cfg.rec_cap, self.MAPPED_REJECTS)
+        if int(v[1]) or n_rej > cap or s.bmeta is None:
+            return self._collect_small(host_view(s.batch))
+        nb, err, first = (int(x) for x in snap.view(np.uint64, 11)[8:11])
+        if err or nb <= 0 or nb > self._seg_buffers(s.slot)[3]:
+            raise RuntimeError(f"durable block encoder failed (bytes={nb}, errors={err})")
+        s.bmeta = (nb, first)
+        rows = rej.view(EVENT_REC, n_rej).copy() if n_rej else np.zeros(0, EVENT_REC)
+        rst = st.view(np.uint8, n_rej).copy() if n_rej else np.zeros(0, np.uint8)
+        return dict(n_msgs=int(self.args.n_msgs), n_events=int(v[3]), n_persisted=int(v[7]), rejects=rows,
+                    reject_status=rst, new_names={}, first_seq=first, recheck=None)
 
     def _framed_rows_start(self, s: "_Submitted"):
         """Start copying the rows (and the durable block) of completed step ``s`` to pinned host
