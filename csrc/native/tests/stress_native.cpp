@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -70,6 +71,20 @@ int64_t swseg_string_bytes(const uint8_t* b, int64_t p0, int64_t p1);
 int64_t swseg_decode(const uint8_t* b, int64_t p0, int64_t p1, uint8_t* etype, uint8_t* level, int64_t* date,
                      int32_t* asg, uint16_t* name, double* v0, double* v1, double* v2, uint8_t* flags,
                      uint8_t* str_heap, int64_t str_cap, int64_t* str_off);
+int64_t swjson_select_block(const uint8_t* b, int32_t etmask, const uint8_t* keep, int64_t n_keep, int32_t keep_default,
+                            const uint8_t* a_known, int64_t n_asg, const uint8_t* a_heap, const int64_t* a_off,
+                            const uint8_t* a_present, const uint8_t* n_heap, const int64_t* n_off,
+                            const uint8_t* n_present, int64_t n_names, const uint8_t* r_heap, const int64_t* r_off,
+                            const uint8_t* r_present, const uint8_t* tpl, int64_t tpl_len, int32_t threads,
+                            uint8_t* scratch, int64_t scap, uint8_t* tscratch, int64_t tscap, uint8_t* out,
+                            int64_t cap, int64_t* out_off, uint8_t* tout, int64_t tcap, int64_t* tout_off,
+                            int64_t* counts, int64_t* miss, int64_t miss_cap);
+int64_t swseg_threshold_rows(const uint8_t* b, const uint8_t* name_mask, int64_t n_mask, double lo, double hi,
+                             int32_t has_lo, int32_t has_hi, int32_t threads, int64_t* out_rows, int32_t* out_asg,
+                             double* out_val, int64_t cap);
+int64_t swmqtt_publish_qos0(const uint8_t* topics, const int64_t* t_off, const uint8_t* payloads, const int64_t* p_off,
+                            int64_t n, uint8_t retain, uint8_t* out, int64_t cap);
+int64_t swmqtt_scan(const uint8_t* buf, int64_t n, int64_t* out, int64_t cap, int64_t max_len, int64_t* used);
 }
 
 static std::atomic<int> g_fail{0};
@@ -310,6 +325,47 @@ static void decode_fuzz() {
       const int64_t got = swseg_decode(b2.data(), 0, 1 << 30, et.data(), lv.data(), dt.data(), as.data(), nm.data(),
                                        a0.data(), a1.data(), a2.data(), fl.data(), heap.data(), cap, so.data());
       CHECK(got == good, "block decode returned %lld of %lld rows", (long long)got, (long long)good);
+      // connector selection + JSON straight from the block (worker slices, then concatenated), on 3
+      // threads; first with slices too small (measured only), then sized from the answer
+      {
+        const int64_t na = 97;
+        std::string ah;
+        std::vector<int64_t> ao(7 * na + 1);
+        std::vector<uint8_t> ap(7 * na, 1), known(na, 1), keep(na);
+        for (int64_t i = 0; i < 7 * na; ++i) { ao[i] = (int64_t)ah.size(); ah += "ctx-\"" + std::to_string(i); }
+        ao[7 * na] = (int64_t)ah.size();
+        for (int64_t i = 0; i < na; ++i) keep[i] = (uint8_t)(i % 3 != 0);
+        const std::string nh = "namemx";
+        std::vector<int64_t> no = {0, 4, 6};
+        std::vector<uint8_t> np = {1, 1};
+        const char* tpl = "t/\x01/\x02";
+        int64_t counts[3], miss[64];
+        int64_t scap = 64, tscap = 64;
+        for (int round = 0; round < 3; ++round) {
+          std::vector<uint8_t> sc((size_t)scap), tsc((size_t)tscap), o((size_t)scap), to((size_t)tscap);
+          std::vector<int64_t> oo(good + 1), too(good + 1);
+          const int64_t r = swjson_select_block(b2.data(), 0x7, keep.data(), na, 0, known.data(), na,
+                                                (const uint8_t*)ah.data(), ao.data(), ap.data(),
+                                                (const uint8_t*)nh.data(), no.data(), np.data(), 2,
+                                                (const uint8_t*)nh.data(), no.data(), np.data(), (const uint8_t*)tpl,
+                                                (int64_t)strlen(tpl), 3, sc.data(), scap, tsc.data(), tscap, o.data(),
+                                                scap, oo.data(), to.data(), tscap, too.data(), counts, miss, 64);
+          if (r >= 0) {
+            CHECK(counts[0] > 0 && counts[0] < good && oo[counts[0]] == r, "selection wrote %lld bytes for %lld rows",
+                  (long long)r, (long long)counts[0]);
+            break;
+          }
+          CHECK(r > -(int64_t(1) << 40), "selection failed (%lld)", (long long)r);
+          scap = tscap = -r + 4096;
+        }
+        std::vector<uint8_t> nmask = {1, 1};
+        std::vector<int64_t> rr(good);
+        std::vector<int32_t> ra(good);
+        std::vector<double> rv(good);
+        const int64_t k = swseg_threshold_rows(b2.data(), nmask.data(), 2, -1e300, 50.0, 0, 1, 3, rr.data(), ra.data(),
+                                               rv.data(), good);
+        CHECK(k >= 0 && k <= good, "threshold rows returned %lld", (long long)k);
+      }
     }
     // the same block with its index trailer (csrc/native/swindex.cpp) built into an exactly sized
     // buffer, verified, and queried through the alternate-id and context-key lookups
@@ -360,7 +416,25 @@ static void decode_fuzz() {
          (long long)events);
 }
 
+// MQTT framing and the packet scanner, whole and cut at every byte boundary of a short stream
+static void mqtt_frames() {
+  const std::string topics = "a/bt/longer/topic", pay = std::string(300, 'x') + "{}";
+  const int64_t t_off[4] = {0, 3, 3, (int64_t)topics.size()}, p_off[4] = {0, 1, 300, (int64_t)pay.size()};
+  std::vector<uint8_t> out(4096);
+  const int64_t n = swmqtt_publish_qos0((const uint8_t*)topics.data(), t_off, (const uint8_t*)pay.data(), p_off, 3, 0,
+                                        out.data(), (int64_t)out.size());
+  CHECK(n > 0, "framing failed (%lld)", (long long)n);
+  for (int64_t cut = 0; cut <= n; ++cut) {
+    std::vector<uint8_t> part(out.begin(), out.begin() + cut);     // exact size
+    int64_t hdr[4 * 8], used = -1;
+    const int64_t k = swmqtt_scan(part.data(), cut, hdr, 8, 1 << 20, &used);
+    CHECK(k >= 0 && k <= 3 && used <= cut, "scan of %lld bytes: %lld packets, %lld used", (long long)cut,
+          (long long)k, (long long)used);
+  }
+}
+
 int main(int argc, char** argv) {
+  mqtt_frames();
   decode_fuzz();
   log_stress("");
   if (argc > 1) log_stress(argv[1]);

@@ -1,86 +1,37 @@
-"""PCIe H2D probe: which copy mechanism moves a bench-sized raw batch (85 MB) fastest on this box.
-torch copy_ on one stream vs split over streams vs explicit SDMA engines (sw_sdma_h2d)."""
-import ctypes
+"""Host time of the tenant's H2D enqueue (submit_framed): a 1M-payload raw record on the bus is a
+pinned buffer; torch.frombuffer views of it are copied to HBM with non_blocking=True.  Reports
+whether torch sees the view as pinned and the host time of each copy call (an async enqueue takes
+microseconds; a staged synchronous copy takes the transfer time)."""
 import json
+import sys
 import time
 
+import numpy as np
 import torch
 
-from sitewhere_amd._native import gpu
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+from sitewhere_amd.pipeline.bus_io import RawBatchRecord, parse_raw_batch  # noqa: E402
+from sitewhere_amd.pipeline.fleet import FleetSpec, gen_payloads  # noqa: E402
+from sitewhere_amd.pipeline.framing import varint_lengths  # noqa: E402
 
-lib = gpu()
-N = 85 << 20
-dev = torch.device("cuda:0")
-host = torch.empty(N, dtype=torch.uint8).pin_memory()
-host.random_(0, 255)
-d = torch.empty(N, dtype=torch.uint8, device=dev)
-res = {}
-
-
-def bench(name, fn, reps=20):
-    fn()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(reps):
-        fn()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / reps
-    res[name] = {"ms": round(dt * 1e3, 3), "GBps": round(N / dt / 1e9, 1)}
-    print(name, res[name], flush=True)
-
-
-s1, s2, s3, s4 = (torch.cuda.Stream(dev) for _ in range(4))
-
-
-def one():
-    with torch.cuda.stream(s1):
-        d.copy_(host, non_blocking=True)
-
-
-def split(k, streams):
-    c = N // k
-
-    def f():
-        for i in range(k):
-            with torch.cuda.stream(streams[i % len(streams)]):
-                d[i * c:(i + 1) * c].copy_(host[i * c:(i + 1) * c], non_blocking=True)
-    return f
-
-
-def sdma(engines):
-    def f():
-        k = len(engines)
-        c = N // k
-        sigs = []
-        for i, e in enumerate(engines):
-            sig = ctypes.c_uint64(0)
-            rc = lib.sw_sdma_h2d(ctypes.c_void_p(d.data_ptr() + i * c), ctypes.c_void_p(host.data_ptr() + i * c),
-                                 c, e, ctypes.byref(sig))
-            assert rc == 0, rc
-            sigs.append(sig.value)
-        for sg in sigs:
-            assert lib.sw_sdma_wait(ctypes.c_uint64(sg)) == 0
-    return f
-
-
-bench("torch_1stream", one)
-bench("torch_split2_2streams", split(2, [s1, s2]))
-bench("torch_split4_4streams", split(4, [s1, s2, s3, s4]))
-for engs in ([0], [1], [1, 2], [1, 2, 3, 4]):
-    try:
-        bench(f"sdma_engines_{'_'.join(map(str, engs))}", sdma(engs))
-    except AssertionError as e:
-        print("sdma", engs, "failed", e)
-# H2D while a D2H of 17 MB runs (full duplex check)
-dd = torch.empty(17 << 20, dtype=torch.uint8, device=dev)
-hh = torch.empty(17 << 20, dtype=torch.uint8).pin_memory()
-
-
-def duplex():
-    with torch.cuda.stream(s2):
-        hh.copy_(dd, non_blocking=True)
-    one()
-
-
-bench("torch_h2d_with_d2h", duplex)
-print(json.dumps(res))
+spec = FleetSpec(prefix="dev-", n_devices=1 << 20, with_alternate_id=True)
+raw, off = gen_payloads(spec, 1 << 20, 1_700_000_000_000, seed=3)
+rec = RawBatchRecord(raw[:int(off[-1])], varint_lengths(off), len(off) - 1, pinned=True)
+b = parse_raw_batch(rec.buf.numpy()[:rec.value_len])
+dev = torch.empty(len(b.payload) + 4096, dtype=torch.uint8, device="cuda")
+s = torch.cuda.Stream()
+out = {"bytes": len(b.payload)}
+for name, src in (("frombuffer", lambda: torch.frombuffer(b.payload, dtype=torch.uint8)),
+                  ("record_tensor", lambda: rec.buf[:len(b.payload)])):
+    t = src()
+    out[f"{name}_is_pinned"] = bool(t.is_pinned())
+    ts = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            dev[:t.numel()].copy_(t, non_blocking=True)
+        ts.append((time.perf_counter() - t0) * 1e3)
+        torch.cuda.synchronize()
+    out[f"{name}_enqueue_ms"] = [round(x, 3) for x in ts]
+print(json.dumps(out))

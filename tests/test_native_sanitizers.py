@@ -22,7 +22,8 @@ SRC = [os.path.join(ROOT, "csrc", "native", "tests", "stress_native.cpp"),
        os.path.join(ROOT, "csrc", "native", "swnative.cpp"),
        os.path.join(ROOT, "csrc", "native", "swcpuengine.cpp"),
        os.path.join(ROOT, "csrc", "native", "swseg.cpp"),
-       os.path.join(ROOT, "csrc", "native", "swindex.cpp")]
+       os.path.join(ROOT, "csrc", "native", "swindex.cpp"),
+       os.path.join(ROOT, "csrc", "native", "swrowjson.cpp")]
 CXX = shutil.which("g++")
 
 SANITIZERS = {
