@@ -281,6 +281,7 @@ def native_gil():
             _proto(lib, "swlog_view", c_int32, P, c_int32, c_int32, c_int64, P, P, P)
             _proto(lib, "swlog_hold", c_int32, P, c_int32, c_int32, c_int64)
             _proto(lib, "swlog_take_released", c_int64, P, P, c_int64)
+            _proto(lib, "sw_partition_for_key", c_int32, c_char_p, c_int32, c_int32)
             _native_gil = lib
     return _native_gil
 

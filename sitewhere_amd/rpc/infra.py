@@ -349,12 +349,13 @@ class RemoteEventBus:
         return self.r.call("begin_offset", name, p)
 
     def partition_for(self, name, key):
-        import ctypes
         n = self.partitions(name)
         if key is None:
             return next(self._rr) % n
-        kb = (ctypes.c_char * len(key)).from_buffer_copy(key) if key else None
-        return self.lib.sw_partition_for_key(ctypes.cast(kb, ctypes.c_void_p) if kb else None, len(key), n)
+        # Kafka's murmur2 partitioner, natively, keeping the GIL (a per-record call: no copy, no
+        # release / re-acquire)
+        from .._native import native_gil
+        return native_gil().sw_partition_for_key(bytes(key), len(key), n)
 
     def append(self, name, p, records, ts=None):
         return self.r.call("append", name, p, [[k, v] for k, v in records], ts)

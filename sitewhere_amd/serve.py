@@ -171,6 +171,8 @@ def main(argv=None) -> int:
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     if args.reference_templates:                 # read by tenant management when it starts
         os.environ["SITEWHERE_REFERENCE_TEMPLATES"] = args.reference_templates
+    from .utils.stack_sampler import maybe_start
+    maybe_start()                                # SW_STACK_SAMPLE=<prefix>: where this process's time goes
     return {"infra": cmd_infra, "service": cmd_service, "all": cmd_all}[args.cmd](args)
 
 
