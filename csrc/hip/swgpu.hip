@@ -1073,6 +1073,61 @@ __global__ void k_lookup(SwEngineArgs a) {
   }
 }
 
+// The store-backed filter's verdict for every id to claim, before the claim: 16 lanes per id, lane q
+// loading 16-byte word q (and q + 16 with more than 4 generations) of the id's home span -- the G
+// adjacent 64-byte buckets -- so one load instruction covers four ids' spans in full lines (one thread
+// per id issued 16 scattered loads per id and ran ~220 us per 1M ids, profiles/r6_kernels).  A
+// generation whose bucket is full without the fingerprint goes on to the next span.  Sets bit 1 of
+// the id's claim flag (ev_slot + rec_cap) when a generation may hold it.
+__global__ __launch_bounds__(BLK) void k_ff_probe(SwEngineArgs a) {
+  const uint32_t n = *a.n_work;
+  const ull* __restrict__ ck = reinterpret_cast<const ull*>(a.ev_slot);
+  uint8_t* __restrict__ cf = reinterpret_cast<uint8_t*>(reinterpret_cast<ull*>(a.ev_slot) + a.rec_cap);
+  const uint32_t* __restrict__ t = a.dd_ff;
+  const int gens = (int)a.dd_ff_gens;
+  const int64_t bmask = a.dd_ff_bmask;
+  const uint32_t lane = threadIdx.x & 63u, sub = lane & 15u, grp = lane >> 4;
+  const int64_t g0 = ((int64_t)BID * BLK + threadIdx.x) >> 4;
+  const int64_t gstride = ((int64_t)gridDim.x * BLK) >> 4;
+  const int words = gens * 4;                     // 16-byte words of a span
+  for (int64_t base = g0 - grp; base < (int64_t)n; base += gstride) {
+    // the wave's four groups take ids base + 0..3 (group-uniform: every lane of a group agrees)
+    const int64_t i = base + grp;
+    const ull h = i < (int64_t)n ? ck[i] : 0ull;
+    const ull m = sw_ff_mix(h);
+    const uint32_t fp = sw_ff_fp(m);
+    int64_t b = (int64_t)sw_ff_bucket(m, bmask);
+    uint32_t open = h ? (1u << gens) - 1u : 0u;
+    bool held = false;
+    for (int p = 0; p < SW_FF_MAX_PROBE; ++p) {
+      bool hit = false;
+      uint32_t empty_g = 0;
+      const uint4* __restrict__ q = reinterpret_cast<const uint4*>(t + b * gens * SW_FF_SLOTS);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int w = (int)sub + 16 * r;
+        const int gg = w >> 2;
+        if (w < words && ((open >> gg) & 1u)) {
+          const uint4 v = q[w];
+          hit |= v.x == fp || v.y == fp || v.z == fp || v.w == fp;
+          if (!v.x || !v.y || !v.z || !v.w) empty_g |= 1u << gg;
+        }
+      }
+      // the group's answer: any lane's hit; a generation is closed once any of its words has a hole
+      const ull hb = __ballot(hit);
+      uint32_t e = empty_g;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) e |= __shfl_xor(e, o, 16);
+      if ((hb >> (16 * grp)) & 0xffffull) { held = true; open = 0; }
+      open &= ~e;
+      const bool more = open != 0;
+      if (!__any(more)) break;
+      b = (b + 1) & bmask;
+    }
+    if (held && sub == 0) cf[i] |= 2u;
+  }
+}
+
 // The dedup claims of the step's validated records.  A kernel of its own: fused into k_lookup the
 // three dependent round trips per id (registry probe, `prev` probe, CAS) ran 255 us per 1M ids
 // against 48 + 143 us as two kernels (profiles/r4_fused_claim).
@@ -1091,8 +1146,8 @@ __global__ void k_dedup_claim(SwEngineArgs a) {
   for (int64_t i = (int64_t)BID * BLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLK) {
     const ull ah = ck[i];
     if (!ah) continue;
-    const bool held = d.ff && ff_has(d.ff, d.fbmask, d.fgens, ah);
-    const uint8_t st = dedup_claim(d, ah, i, held && cf[i], !d.ff || held, dc);
+    const bool held = d.ff && (cf[i] & 2u);                 // k_ff_probe's verdict
+    const uint8_t st = dedup_claim(d, ah, i, held && (cf[i] & 1u), !d.ff || held, dc);
     if (st != SW_ST_OK) status[i] = st;
   }
   // dedup counters aggregated per workgroup: one global atomic per block, not one per id (1M
@@ -1942,6 +1997,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   if (a.dd_ff && (a.dd_ff_gens < 2 || a.dd_ff_gens > SW_FF_MAX_GENS || !a.dd_ff_meta || a.dd_ff_bmask < 0))
     return -6;
   k_lookup<<<g, BLK, 0, s>>>(a);         // + the phase's resets (block 0)
+  if (a.dd_ff) k_ff_probe<<<g, BLK, 0, s>>>(a);
   k_dedup_claim<<<g, BLK, 0, s>>>(a);
   // stable split ok / rejected, with the dedup verdicts
   k_cmp_count<<<(unsigned)ntiles, BLK, 0, s>>>(a.status, a.n_work, a.cmp_tmp, ntiles, (ull*)a.stats, a.work,
