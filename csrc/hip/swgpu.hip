@@ -1905,6 +1905,19 @@ int sw_reject_pack(const void* recs, const int32_t* rej_idx, const uint8_t* stat
   return (int)hipGetLastError();
 }
 
+// Stream / event / copy enqueues for the tenant's submit path, bound without releasing the GIL
+// (sitewhere_amd/_native.py _GilBound): torch's equivalents give the interpreter lock up on every
+// call and wait to win it back from the tenant's other threads (~0.2 ms each at the instance's
+// switch interval, ~1 ms per step over the H2D's five calls -- profiles/r6_soak).
+int sw_stream_wait_event(hipStream_t s, hipEvent_t e) { return (int)hipStreamWaitEvent(s, e, 0); }
+int sw_event_record(hipEvent_t e, hipStream_t s) { return (int)hipEventRecord(e, s); }
+int sw_memcpy_h2d_async(void* dst, const void* src, int64_t n, hipStream_t s) {
+  return n > 0 ? (int)hipMemcpyAsync(dst, src, (size_t)n, hipMemcpyHostToDevice, s) : 0;
+}
+int sw_memset_async(void* dst, int32_t v, int64_t n, hipStream_t s) {
+  return n > 0 ? (int)hipMemsetAsync(dst, v, (size_t)n, s) : 0;
+}
+
 int sw_step_snapshot(const uint32_t* scalars, const uint32_t* seg_meta, const uint32_t* rej_cnt,
                      const uint32_t* n_carry, int32_t produced, uint32_t* host, hipStream_t s) {
   k_step_snapshot<<<1, 64, 0, s>>>(scalars, seg_meta, rej_cnt, n_carry, produced, host);

@@ -342,6 +342,10 @@ def gpu():
         _proto(lib, "sw_reject_refs", c_int32, P, P, P, c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "sw_step_snapshot", c_int32, P, P, P, P, c_int32, P, P)
         _proto(lib, "sw_reject_pack", c_int32, P, P, P, P, c_int64, P, P, P)
+        _proto(lib, "sw_stream_wait_event", c_int32, P, P)
+        _proto(lib, "sw_event_record", c_int32, P, P)
+        _proto(lib, "sw_memcpy_h2d_async", c_int32, P, P, c_int64, P)
+        _proto(lib, "sw_memset_async", c_int32, P, c_int32, c_int64, P)
         _gpu = lib
         return lib
 

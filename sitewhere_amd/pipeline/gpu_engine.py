@@ -73,6 +73,18 @@ class _Submitted:
         self.mapped = False             # step snapshot + rejects written into the slot's mapped host memory
 
 
+def _host_addr(buf) -> int:
+    """Address of a host buffer (bytes-like, numpy array or memoryview; read-only views included)."""
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    return np.frombuffer(buf, np.uint8).ctypes.data
+
+
+def _chk(rc: int):
+    if rc:
+        raise RuntimeError(f"HIP stream call failed ({rc})")
+
+
 class _FramedSlots:
     """Slot state of :meth:`GpuInboundEngine.submit_framed`: device raw / varint-length / offset
     buffers per slot (grown on demand), the H2D copy stream and its events, and the batches still in
@@ -88,6 +100,9 @@ class _FramedSlots:
         self.d2h = torch.cuda.Stream(e.device)      # rows when the SDMA engine is unavailable
         self.ev_h2d = [torch.cuda.Event() for _ in range(self.SLOTS)]
         self.ev_comp = [torch.cuda.Event() for _ in range(self.SLOTS)]
+        for ev in self.ev_h2d + self.ev_comp:      # created now (torch creates them on first record):
+            ev.record(self.h2d)                    # the submit path passes their raw handles natively
+        self.h2d.synchronize()
         self.bufs = [None] * self.SLOTS
         self.inflight = deque()
         self.k = 0
@@ -903,31 +918,30 @@ class GpuInboundEngine(EngineBase):
                 fp = self._fp = _FramedSlots(self)
             b = fp.k % _FramedSlots.SLOTS
             dev_r, dev_l, dev_o = fp.buffers(b, nb, nl)
-            segs = []                                      # (device offset, host payload, payload bytes)
-            with warnings.catch_warnings():       # read-only topic views: torch only reads them here
-                warnings.simplefilter("ignore", UserWarning)
-                if parts is None:
-                    pt = torch.frombuffer(batch.payload, dtype=torch.uint8) if nb else None
-                    lsegs = [torch.frombuffer(batch.lens, dtype=torch.uint8)] if nl else []
-                    if pt is not None:
-                        segs.append((0, pt, nb))
-                else:
-                    for part, st in zip(parts, batch.starts):
-                        if part.payload_bytes:
-                            segs.append((int(st), torch.frombuffer(part.payload, dtype=torch.uint8),
-                                         part.payload_bytes))
-                    lsegs = [torch.frombuffer(part.lens, dtype=torch.uint8) for part in parts if len(part.lens)]
-            with torch.cuda.stream(fp.h2d):
-                fp.h2d.wait_event(fp.ev_comp[b])           # step k-3 was the last reader of slot b
-                for st, t, m in segs:
-                    dev_r[st:st + m].copy_(t[:m], non_blocking=True)
-                if parts is not None:                      # the records' zero padding, after the last part
-                    dev_r[batch.payload_bytes:batch.payload_bytes + _ALIGN].zero_()
-                lo = 0
-                for t in lsegs:
-                    dev_l[lo:lo + t.numel()].copy_(t, non_blocking=True)
-                    lo += t.numel()
-                fp.ev_h2d[b].record(fp.h2d)
+            segs = []                                      # (device offset, host address, bytes)
+            if parts is None:
+                if nb:
+                    segs.append((0, _host_addr(batch.payload), nb))
+                lsegs = [(_host_addr(batch.lens), len(batch.lens))] if nl else []
+            else:
+                for part, st in zip(parts, batch.starts):
+                    if part.payload_bytes:
+                        segs.append((int(st), _host_addr(part.payload), part.payload_bytes))
+                lsegs = [(_host_addr(part.lens), len(part.lens)) for part in parts if len(part.lens)]
+            # the H2D of the zero-copy record straight from its pinned bytes, on the copy stream,
+            # enqueued natively with the GIL held (see sw_memcpy_h2d_async)
+            L, hs = self.lib, ctypes.c_void_p(fp.h2d.cuda_stream)
+            _chk(L.sw_stream_wait_event(hs, ctypes.c_void_p(fp.ev_comp[b].cuda_event)))  # step k-3 read slot b last
+            rd, ld = _ptr(dev_r), _ptr(dev_l)
+            for st, src, m in segs:
+                _chk(L.sw_memcpy_h2d_async(ctypes.c_void_p(rd + st), ctypes.c_void_p(src), int(m), hs))
+            if parts is not None:                          # the records' zero padding, after the last part
+                _chk(L.sw_memset_async(ctypes.c_void_p(rd + batch.payload_bytes), 0, _ALIGN, hs))
+            lo = 0
+            for src, m in lsegs:
+                _chk(L.sw_memcpy_h2d_async(ctypes.c_void_p(ld + lo), ctypes.c_void_p(src), int(m), hs))
+                lo += m
+            _chk(L.sw_event_record(ctypes.c_void_p(fp.ev_h2d[b].cuda_event), hs))
             t0 = self._ft("h2d_enqueue", t0)
             while len(fp.inflight) > 1 or (fp.inflight and fp.inflight[0].rows is not None):
                 done.append(self._framed_finish(fp.inflight.popleft()))      # batch k-2
@@ -941,7 +955,8 @@ class GpuInboundEngine(EngineBase):
                 self._block_meta(prev)              # before batch k is queued: no wait on it
                 t0 = self._ft("block_meta_k1", t0)
             cur = torch.cuda.current_stream(self.device)
-            cur.wait_event(fp.ev_h2d[b])
+            _chk(self.lib.sw_stream_wait_event(ctypes.c_void_p(cur.cuda_stream),
+                                               ctypes.c_void_p(fp.ev_h2d[b].cuda_event)))
             self.frame_varint(dev_l, nl, n, dev_o, batch.payload_bytes)
             do_presence = self.presence_due(now_ms) if presence is None else presence
             self.step_async(dev_r[:nb], dev_o[:n + 1], n, now_ms, presence=do_presence, out_sel=b,
@@ -951,7 +966,7 @@ class GpuInboundEngine(EngineBase):
                 sub.bmeta, sub.now = self.encode_block_async(b), now_ms
             if self.world == 1:
                 self._snapshot_async(fp, b, sub)
-            fp.ev_comp[b].record(cur)
+            _chk(self.lib.sw_event_record(ctypes.c_void_p(fp.ev_comp[b].cuda_event), ctypes.c_void_p(cur.cuda_stream)))
             t0 = self._ft("step_enqueue", t0)
             if prev is not None:
                 self._framed_rows_start(prev)
