@@ -199,6 +199,8 @@ def main():
     data_dir = os.environ["SITEWHERE_DATA_DIR"]
     log("data dir", data_dir, "free GB", round(shutil.disk_usage(data_dir).free / 2 ** 30, 1))
     os.environ.setdefault("SW_TENANT_TRACE", "1")
+    from sitewhere_amd.utils.stack_sampler import maybe_start
+    maybe_start()                               # SW_STACK_SAMPLE=<prefix>: where the tenant's threads spend time
     import torch
     from sitewhere_amd.assembly import SiteWhereInstance
     from sitewhere_amd.pipeline.bus_io import VALUE_HDR, RawBatchRecord
