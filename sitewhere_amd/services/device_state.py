@@ -54,6 +54,8 @@ class _EngineStates:
         self._slot_lut = np.full(3 << 16, -1, np.int64)   # (etype << 16 | name id) -> dense slot number
         self._slot_keys: list[tuple] = []
         self.ctx: dict = {}                      # assignment index -> context list (reader dictionary)
+        self._by_aid: dict = {}                  # assignment id -> index (rebuilt when ctx grows)
+        self._by_aid_n = -1
         self.names: dict = {}                    # name id -> name
 
     def _grow(self, m: int):
@@ -130,6 +132,13 @@ class _EngineStates:
             t[0][a[up]] = d[up]
             t[1][a[up]] = e[up]
 
+    def index_of(self, aid: str):
+        """Assignment index of an assignment id (None: no engine row of it)."""
+        if self._by_aid_n != len(self.ctx):
+            self._by_aid = {c[0]: i for i, c in self.ctx.items() if c}
+            self._by_aid_n = len(self.ctx)
+        return self._by_aid.get(aid)
+
     def event_id(self, eid1: int) -> str:
         return f"{self.boot:x}-{int(eid1) - 1}"
 
@@ -152,7 +161,7 @@ class DeviceStateManagement:
         return self.states.get(id)
 
     def get_device_state_by_device_assignment_id(self, assignment_id: str):
-        self._sync()
+        self._sync(assignment_id)            # that assignment's engine rows only
         return self.states.s.get_by(self.states.c, "device_assignment_id", assignment_id)
 
     # ---- engine batches ----------------------------------------------------------------
@@ -167,14 +176,20 @@ class DeviceStateManagement:
                 t = self._engine[key] = _EngineStates(key[0], h)
             t.merge(cols)
 
-    def _sync(self):
+    def _sync(self, assignment_id: str | None = None):
         """Write the states engine batches changed since the last read (merge_event's slot rule
-        against what the per-event path stored)."""
+        against what the per-event path stored): every changed assignment, or only
+        ``assignment_id``'s -- a per-assignment read (and every per-event merge) must not
+        materialise a million-device fleet's states in Python on the way."""
         import numpy as np
         from ..models.columnar import EV_ALERT, EV_LOCATION
         with self._lock:
             for t in self._engine.values():
-                idx = np.flatnonzero(t.dirty)
+                if assignment_id is not None:
+                    i0 = t.index_of(assignment_id)
+                    idx = np.array([i0] if i0 is not None and i0 < len(t.dirty) and t.dirty[i0] else [], np.int64)
+                else:
+                    idx = np.flatnonzero(t.dirty)
                 if not len(idx):
                     continue
                 t.dirty[idx] = False
