@@ -330,7 +330,7 @@ int64_t swseg_ix_asg_pages(const uint8_t* const* t, int64_t n, int32_t asg, int6
 // assignments in one call.  Returns the pages found (> cap: call again with that cap).
 int64_t swseg_ix_asgs_pages(const uint8_t* const* t, int64_t n, const int32_t* asgs, int64_t n_asg,
                             const uint8_t* mask, int64_t d_lo, int64_t d_hi, int64_t* out_blk, int64_t* out_page,
-                            int64_t cap) {
+                            int64_t cap, int64_t* out_lo, int64_t* out_hi) {
   int64_t k = 0;
   if (n_asg <= 0) return 0;
   for (int64_t i = 0; i < n; ++i) {
@@ -350,7 +350,16 @@ int64_t swseg_ix_asgs_pages(const uint8_t* const* t, int64_t n, const int32_t* a
         if (asgs[mid] < q.asg_min) lo = mid + 1; else hi = mid;
       }
       if (lo < n_asg && asgs[lo] <= q.asg_max) {     // one falls in [asg_min, asg_max]
-        if (k < cap) { out_blk[k] = i; out_page[k] = p; }
+        if (k < cap) {
+          out_blk[k] = i;
+          out_page[k] = p;
+          if (out_lo) {                                  // the wanted assignments the page may hold
+            int64_t e = lo + 1;
+            while (e < n_asg && asgs[e] <= q.asg_max) ++e;
+            out_lo[k] = lo;
+            out_hi[k] = e;
+          }
+        }
         ++k;
       }
     }
@@ -504,7 +513,8 @@ extern "C" {
 int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint32_t* pg_off, const uint32_t* pg_bytes,
                          const int32_t* pg_index, int64_t n_tasks, int32_t et, int32_t asg, const int32_t* ctx_tab,
                          int64_t n_ctx, int32_t ctx_id, int64_t d_lo, int64_t d_hi, int32_t threads,
-                         int64_t* out_task, int32_t* out_row, int64_t* out_date, int64_t cap, const uint64_t* mem) {
+                         int64_t* out_task, int32_t* out_row, int64_t* out_date, int64_t cap, const uint64_t* mem,
+                         const int32_t* asg_list, const int64_t* task_lo, const int64_t* task_hi) {
   if (n_tasks <= 0) return 0;
   int T = threads > 0 ? threads : 1;
   if (T > 64) T = 64;
@@ -548,6 +558,30 @@ int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint3
       const SwSegCol& ce = ph.cols[SEG_ETYPE];
       const SwSegCol& cd = ph.cols[SEG_DATE];
       const int32_t row0 = pg_index[i] * SEG_PAGE_ROWS;
+      if (asg_list) {
+        // the wanted assignments this page may hold (sorted, asg_list[task_lo .. task_hi)): the
+        // assignment column first -- one compare for the usual single candidate -- and the type
+        // and date only for its rows (no per-row context table lookup)
+        const int64_t l0 = task_lo[i], l1 = task_hi[i];
+        for (uint32_t r = 0; r < ph.n_rows; ++r) {
+          const int32_t a = (int32_t)seg_unord(ca.base + ix_unpack(pg + ca.data_off, r, ca.bits));
+          if (l1 - l0 == 1) {
+            if (a != asg_list[l0]) continue;
+          } else {
+            int64_t lo = l0, hi = l1;
+            while (lo < hi) {
+              const int64_t mid = (lo + hi) >> 1;
+              if (asg_list[mid] < a) lo = mid + 1; else hi = mid;
+            }
+            if (lo >= l1 || asg_list[lo] != a) continue;
+          }
+          if (et >= 0 && (int32_t)seg_unord(ce.base + ix_unpack(pg + ce.data_off, r, ce.bits)) != et) continue;
+          const int64_t d = seg_unord(cd.base + ix_unpack(pg + cd.data_off, r, cd.bits));
+          if (d < d_lo || d > d_hi) continue;
+          hits[w].push_back({i, row0 + (int32_t)r, d});
+        }
+        continue;
+      }
       for (uint32_t r = 0; r < ph.n_rows; ++r) {
         if (et >= 0 && (int32_t)seg_unord(ce.base + ix_unpack(pg + ce.data_off, r, ce.bits)) != et) continue;
         const int32_t a = (int32_t)seg_unord(ca.base + ix_unpack(pg + ca.data_off, r, ca.bits));

@@ -1733,10 +1733,11 @@ class DurableEventStore(DeviceEventStore):
         return out
 
     def _scan_pages(self, t, bis, pages, et: int, d_lo: int, d_hi: int, asg: int = -1, ctx_tab=None,
-                    ctx_id: int = 0):
+                    ctx_id: int = 0, asg_list=None, task_lo=None, task_hi=None):
         """Rows of pages ``pages`` of blocks ``bis`` (positions in boot table t) passing (type, date
-        range, assignment | context id), reading each page's leading columns only (native
-        ``swseg_scan_pages``, multi-threaded) -> (block position, row in block, date) arrays."""
+        range, assignment | context id | one of the sorted ``asg_list[task_lo[i]:task_hi[i]]`` per
+        page), reading each page's leading columns only (native ``swseg_scan_pages``,
+        multi-threaded) -> (block position, row in block, date) arrays."""
         bis, pages = np.asarray(bis, np.int64), np.asarray(pages, np.int64)
         if not len(bis):
             return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
@@ -1752,7 +1753,9 @@ class DurableEventStore(DeviceEventStore):
                 k = int(native().swseg_scan_pages(_p(fd), _p(pos), _p(poff), _p(nb), _p(pix), len(bis), int(et),
                                                   int(asg), _p(ct), len(ct) if ctx_tab is not None else 0, int(ctx_id),
                                                   int(d_lo), int(d_hi), self.scan_threads, _p(ot), _p(orow), _p(od), cap,
-                                                  _p(mem)))
+                                                  _p(mem), _p(asg_list) if asg_list is not None else None,
+                                                  _p(task_lo) if asg_list is not None else None,
+                                                  _p(task_hi) if asg_list is not None else None))
                 if k < 0:
                     raise ValueError(f"event page unreadable (task {-k - 1})")
                 if k <= cap:
@@ -1835,12 +1838,15 @@ class DurableEventStore(DeviceEventStore):
         cap = max(1024, 4 * len(asgs))
         while True:
             bo, po = np.empty(cap, np.int64), np.empty(cap, np.int64)
+            lo, hi = np.empty(cap, np.int64), np.empty(cap, np.int64)
             k = int(native().swseg_ix_asgs_pages(t["addr"], t["n"], _p(asgs), len(asgs), _p(m), int(d_lo), int(d_hi),
-                                                 _p(bo), _p(po), cap))
+                                                 _p(bo), _p(po), cap, _p(lo), _p(hi)))
             if k <= cap:
                 break
             cap = k
-        return self._scan_pages(t, bo[:k], po[:k], et, d_lo, d_hi, ctx_tab=ctx_tab, ctx_id=cid)
+        # each page is scanned for the id's assignments its zone map admits (no context table lookup)
+        return self._scan_pages(t, bo[:k], po[:k], et, d_lo, d_hi, asg_list=asgs, task_lo=np.ascontiguousarray(lo[:k]),
+                                task_hi=np.ascontiguousarray(hi[:k]))
 
     def _list_context(self, t, boot, pos, want, et, d_lo, d_hi, need) -> tuple[int, list]:
         """Rows of customer / area / asset ids over one boot's blocks, from the trailers' key tables:
