@@ -39,7 +39,7 @@ class BusConsumer(TenantEngineLifecycleComponent):
 
     def __init__(self, engine, name: str, topics: list[str], handler, threads: int = 0, max_records: int = 500,
                  group: str | None = None, auto_commit: bool = True, max_attempts=_DEFAULT, idle=None,
-                 views: bool = False):
+                 views: bool = False, merge_partitions: bool = False):
         super().__init__(name)
         self.tenant_engine = engine
         self.engine = engine
@@ -47,6 +47,10 @@ class BusConsumer(TenantEngineLifecycleComponent):
         self.handler = handler            # handler(list[Record]) per partition batch
         self.threads = threads
         self.max_records = max_records
+        # one handler call for every partition of a poll (split over the pool): a per-event service
+        # whose handler makes a bulk RPC per call (inbound processing -> event management) pays
+        # that round trip per poll, not per partition
+        self.merge_partitions = merge_partitions
         inst = engine.ms.instance
         self.group = group or f"{inst.naming.prefix()}.{engine.tenant.token}.{engine.ms.identifier}.{name}"
         self._stop = threading.Event()
@@ -146,7 +150,18 @@ class BusConsumer(TenantEngineLifecycleComponent):
                         self.logger.exception("consumer %s: idle check failed", self.component_name)
                 continue
             ok: dict = {}
-            if self.pool is None:
+            if self.merge_partitions and len(batch) > 1:
+                allrecs = [r for recs in batch.values() for r in recs]
+                if self.pool is None:
+                    rs = [self._call(allrecs)]
+                else:
+                    step = max(256, -(-len(allrecs) // max(1, self.threads)))
+                    fs = [self.pool.submit(self._call, allrecs[i:i + step]) for i in range(0, len(allrecs), step)]
+                    wait(fs)
+                    rs = [f.result() for f in fs]
+                res = next((r for r in rs if isinstance(r, dict)), all(r is True for r in rs))
+                ok = {tp: res for tp in batch}
+            elif self.pool is None:
                 for tp, recs in batch.items():
                     ok[tp] = self._call(recs)
             else:

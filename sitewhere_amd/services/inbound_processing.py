@@ -65,10 +65,14 @@ class InboundProcessingTenantEngine(MicroserviceTenantEngine):
         # Python threads contend on the GIL, so work runs batched on few threads and the bulk
         # throughput path is the fused GPU engine (``"engine": "gpu"``).
         threads = int(self.config.get("processingThreadCount", 25))
+        # a poll of up to 4096 records across partitions per handler call: one bulk device lookup and
+        # one event-management batch per poll (DecodedEventsConsumer.java:155-204 batches per poll too)
         self.decoded_consumer = BusConsumer(self, "decoded-event-consumers", [n.decoded_events(t), n.inbound_reprocess_events(t)],
-                                            self._process_decoded, threads=min(threads, int(self.config.get("maxThreads", 2))))
+                                            self._process_decoded, threads=min(threads, int(self.config.get("maxThreads", 2))),
+                                            max_records=4096, merge_partitions=True)
         self.persisted_consumer = BusConsumer(self, "persisted-event-consumers", [n.inbound_persisted_events(t)],
-                                              self._process_persisted, threads=min(10, int(self.config.get("maxThreads", 2))))
+                                              self._process_persisted, threads=min(10, int(self.config.get("maxThreads", 2))),
+                                              max_records=4096, merge_partitions=True)
         self.processed_events = self.create_meter("processedEvents")
         self.failed_events = self.create_meter("failedEvents")
         self.device_lookup = self.create_timer("deviceLookup")
