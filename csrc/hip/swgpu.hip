@@ -1333,8 +1333,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     // could push the live table past half load (k_state_p2 clears, k_step_end flips)
     if (a.dd_meta[1] + a.rec_cap > (a.dd_mask + 1) / 2) a.dd_meta[2] = 1;
   }
-  const int ff_live = a.dd_ff ? (int)a.dd_ff_meta[0] : 0;
-  uint32_t ff_dropped = 0, ff_ids = 0;
+  uint32_t ff_ids = 0;
   const int64_t c0 = *a.step_cursor0;
   const int64_t now = a.sp->now_ms;
   SwSegAux* const aux = reinterpret_cast<SwSegAux*>(a.sp->aux);
@@ -1373,10 +1372,7 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
     o.etype = r.etype;
     o.level = r.level;
     a.sp->out[seq - c0] = o;
-    if (a.dd_ff && r.alt_hash) {
-      ++ff_ids;
-      if (!ff_add(a.dd_ff, a.dd_ff_bmask, (int)a.dd_ff_gens, ff_live, r.alt_hash)) ++ff_dropped;
-    }
+    if (a.dd_ff && r.alt_hash) ++ff_ids;     // added to the live generation by k_ff_add_rows
     if (aux) {                   // the durable-block encoder's input, beside the row (coalesced)
       SwStrRef sr;
       if (spans) {
@@ -1421,7 +1417,6 @@ __global__ void k_persist(SwEngineArgs a, const SwEventRec* __restrict__ R, cons
       for (int o = 32; o > 0; o >>= 1) ff_ids += __shfl_xor(ff_ids, o);
       if (lane_id() == 0) atomicAdd((ull*)&a.dd_ff_meta[6], (ull)ff_ids);
     }
-    if (ff_dropped) atomicAdd((ull*)&a.dd_ff_meta[5], (ull)ff_dropped);   // rare: a chain past the probe bound
   }
 }
 
@@ -2001,6 +1996,10 @@ __global__ void k_cl_prep(const uint32_t* __restrict__ ok_idx, const uint32_t* _
 int sw_radix_sort_u32(uint32_t* keys, uint32_t* vals, const uint32_t* n_ptr, int64_t cap, int bits, uint32_t* hist,
                       uint32_t* vals_final, hipStream_t s);
 
+__global__ __launch_bounds__(BLK) void k_ff_add_rows(SwEngineArgs a, const SwEventRec* __restrict__ R,
+                                                     const uint32_t* __restrict__ idx,
+                                                     const uint32_t* __restrict__ n_ptr, uint32_t cap);
+
 // Phase D: validate, dedup, persist, enrich, state, rules, presence.
 int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) {
   const SwEngineArgs a = *ap;
@@ -2029,6 +2028,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   // string refs of the work batch: the decoder's (one rank) or the exchange's (rebased into work_str)
   const SwStrRef* wsp = a.world > 1 ? a.work_spans : a.spans;
   k_persist<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.ev_dev, a.ev_asg, a.n_ok, (uint32_t)a.rec_cap, wsp, nullptr);
+  if (a.dd_ff) k_ff_add_rows<<<g, BLK, 0, s>>>(a, a.work, a.ok_idx, a.n_ok, (uint32_t)a.rec_cap);
   k_state_p2<<<g, BLK, 0, s>>>(a, a.n_ok, (uint32_t)a.rec_cap, nullptr);
   // rules on this step's persisted locations, then presence scan; generated events persist too
   uint32_t* n_rule = scratch4;
@@ -2049,6 +2049,7 @@ int sw_phase_process(const SwEngineArgs* ap, uint32_t* scratch4, hipStream_t s) 
   k_intern_insert_list<<<gg, BLK, 0, s>>>(a.gen, a.n_gen, (ull*)a.nm_key, a.nm_id, a.nm_counter, a.nm_mask, gcap);
   // generated events persist after the step's device events (store cursor + n_ok)
   k_persist<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.gen_dev, a.gen_asg, a.n_gen, gcap, nullptr, a.n_ok);
+  if (a.dd_ff) k_ff_add_rows<<<gg, BLK, 0, s>>>(a, a.gen, nullptr, a.n_gen, gcap);
   k_state_p2<<<gg, BLK, 0, s>>>(a, a.n_gen, gcap, a.n_ok);
   k_step_end<<<1, 64, 0, s>>>(a, n_rule);
   return (int)hipGetLastError();
@@ -2064,6 +2065,54 @@ __global__ void k_set_step_params(SwStepParams* sp, int64_t now_ms, int64_t batc
 
 // Add ids to generation g of the store-backed dedup filter (warm start from the event store's
 // blocks, newest first; see EngineBase.filter_seed).
+// The persisted rows' ids into the live generation of the store-backed filter, right behind
+// k_persist: 4 lanes per id, lane q loading 16-byte word q of the id's 64-byte bucket (one full-line
+// load per id instead of four 16-byte loads by one thread), a hit anywhere ends the id, else the lowest
+// lane holding a free slot claims it with one CAS (another id winning the slot: the group looks
+// again); a full bucket sends the id on to the next.  The bucket rule of ff_add.
+__global__ __launch_bounds__(BLK) void k_ff_add_rows(SwEngineArgs a, const SwEventRec* __restrict__ R,
+                                                     const uint32_t* __restrict__ idx,
+                                                     const uint32_t* __restrict__ n_ptr, uint32_t cap) {
+  if (!a.dd_ff) return;
+  const uint32_t n = *n_ptr < cap ? *n_ptr : cap;
+  uint32_t* __restrict__ t = a.dd_ff;
+  const int gens = (int)a.dd_ff_gens, g = (int)a.dd_ff_meta[0];
+  const int64_t bmask = a.dd_ff_bmask;
+  const uint32_t lane = threadIdx.x & 63u, sub = lane & 3u, grp = lane >> 2;   // 16 ids per wave
+  const ull gmask = 0xfull << (4u * grp);
+  const int64_t g0 = ((int64_t)BID * BLK + threadIdx.x) >> 2;
+  const int64_t gstride = ((int64_t)gridDim.x * BLK) >> 2;
+  uint32_t dropped = 0;
+  for (int64_t base = g0 - grp; base < (int64_t)n; base += gstride) {
+    const int64_t j = base + grp;
+    ull h = 0ull;
+    if (j < (int64_t)n) h = R[idx ? idx[j] : (uint32_t)j].alt_hash;
+    const ull m = sw_ff_mix(h);
+    const uint32_t fp = sw_ff_fp(m);
+    int64_t b = (int64_t)sw_ff_bucket(m, bmask);
+    bool pending = h != 0ull;
+    for (int p = 0; p < 2 * SW_FF_MAX_PROBE && __any(pending); ++p) {
+      uint32_t* sl = t + (b * gens + g) * SW_FF_SLOTS;
+      uint4 v = make_uint4(1u, 1u, 1u, 1u);
+      if (pending) v = reinterpret_cast<const uint4*>(sl)[sub];
+      const bool hit = pending && (v.x == fp || v.y == fp || v.z == fp || v.w == fp);
+      if (__ballot(hit) & gmask) pending = false;
+      const bool zero = pending && (!v.x || !v.y || !v.z || !v.w);
+      const ull zb = __ballot(zero) & gmask;
+      bool ok = false;
+      if (pending && zb && lane == (uint32_t)(__ffsll((long long)zb) - 1)) {
+        const int k = !v.x ? 0 : !v.y ? 1 : !v.z ? 2 : 3;
+        const uint32_t old = atomicCAS(&sl[4u * sub + (uint32_t)k], 0u, fp);
+        ok = old == 0u || old == fp;
+      }
+      if (__ballot(ok) & gmask) pending = false;
+      else if (pending && !zb) b = (b + 1) & bmask;   // full without the id: the chain goes on
+    }
+    if (pending && sub == 0u) ++dropped;
+  }
+  if (dropped) atomicAdd((ull*)&a.dd_ff_meta[5], (ull)dropped);
+}
+
 __global__ void k_ff_add(uint32_t* t, int64_t bmask, int gens, int g, int64_t* meta, const ull* __restrict__ h,
                          int64_t n) {
   uint32_t dropped = 0;

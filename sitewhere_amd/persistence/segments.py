@@ -1597,21 +1597,41 @@ class DurableEventStore(DeviceEventStore):
         return SearchResults(len(out), c.slice(out))
 
     # ------------------------------------------------------------------ native point reads
-    def _file_fds(self, files: np.ndarray):
-        """(fd per entry of ``files`` -- segment file ids -- opened read-only, the fds to close)."""
+    def _file_fds(self, files: np.ndarray, missing_ok: bool = False):
+        """(fd per entry of ``files`` -- segment file ids -- opened read-only, the fds to close).
+        ``missing_ok``: a file retention deleted after the caller took its block table gets fd -1
+        (the caller drops those tasks, unless the store still holds the page in memory); otherwise
+        KeyError."""
         uf, inv = np.unique(np.asarray(files, np.int64), return_inverse=True)
-        opened = []
+        opened, fds = [], []
         try:
             for f in uf.tolist():
                 path = self.seg.file_path(int(f))
-                if path is None:
-                    raise KeyError("segment file deleted by retention")
-                opened.append(os.open(path, os.O_RDONLY))
+                fd = -1
+                if path is not None:
+                    try:
+                        fd = os.open(path, os.O_RDONLY)
+                    except FileNotFoundError:
+                        fd = -1
+                if fd < 0:
+                    if not missing_ok:
+                        raise KeyError("segment file deleted by retention")
+                else:
+                    opened.append(fd)
+                fds.append(fd)
         except BaseException:
             for x in opened:
                 os.close(x)
             raise
-        return np.asarray(opened, np.int32)[inv.reshape(-1)], opened
+        return np.asarray(fds, np.int32)[inv.reshape(-1)], opened
+
+    @staticmethod
+    def _readable(fd: np.ndarray, mem) -> np.ndarray:
+        """Tasks whose page can still be read: from its file, or from the store's memory copy."""
+        ok = fd >= 0
+        if mem is not None:
+            ok |= np.asarray(mem, np.uint64) != 0
+        return ok
 
     def _page_geometry(self, t, bis: np.ndarray, pages: np.ndarray, scan: bool = False):
         """(file id, file offset, bytes, rows) of pages ``pages`` of blocks ``bis`` (positions in t)."""
@@ -1700,7 +1720,20 @@ class DurableEventStore(DeviceEventStore):
             return np.zeros(0, np.int64), np.zeros(0, np.int64)
         files, pos, nb, prows, mem = self._page_geometry(t, bis, pages)
         hv = np.asarray(hashes, np.uint64)
-        fd, opened = self._file_fds(files)
+        fd, opened = self._file_fds(files, missing_ok=True)
+        keep = self._readable(fd, mem)
+        if not keep.all():             # retention deleted a file meanwhile: its ids are no longer stored
+            sel = np.nonzero(keep)[0]
+            pages = pages[sel]
+            fd, pos, nb, prows, hv = fd[sel], pos[sel], nb[sel], prows[sel], hv[sel]
+            mem = mem[sel] if mem is not None else None
+            n = len(sel)
+            if not n:
+                for x in opened:
+                    os.close(x)
+                return np.zeros(0, np.int64), np.zeros(0, np.int64)
+        else:
+            sel = None
         try:
             cap = max(16, n)
             while True:
@@ -1715,7 +1748,8 @@ class DurableEventStore(DeviceEventStore):
         finally:
             for x in opened:
                 os.close(x)
-        return ot[:k], pages[ot[:k]] * PAGE_ROWS + orow[:k].astype(np.int64)
+        ci = ot[:k] if sel is None else sel[ot[:k]]
+        return ci, pages[ot[:k]] * PAGE_ROWS + orow[:k].astype(np.int64)
 
     # ------------------------------------------------------------------ listings
     def _pages_of(self, ent, tr):
@@ -1742,10 +1776,21 @@ class DurableEventStore(DeviceEventStore):
         if not len(bis):
             return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
         files, pos, nb, _, mem = self._page_geometry(t, bis, pages, scan=True)
+        fd, opened = self._file_fds(files, missing_ok=True)
+        keep = self._readable(fd, mem)
+        if not keep.all():             # retention deleted a file meanwhile: its rows are gone
+            sel = np.nonzero(keep)[0]
+            bis, pages, fd, pos, nb = bis[sel], pages[sel], fd[sel], pos[sel], nb[sel]
+            mem = mem[sel] if mem is not None else None
+            if asg_list is not None:
+                task_lo, task_hi = np.ascontiguousarray(task_lo[sel]), np.ascontiguousarray(task_hi[sel])
+            if not len(sel):
+                for x in opened:
+                    os.close(x)
+                return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
         poff = np.zeros(len(bis), np.uint32)
         pix = pages.astype(np.int32)
         ct = np.ascontiguousarray(ctx_tab, np.int32) if ctx_tab is not None else np.zeros(1, np.int32)
-        fd, opened = self._file_fds(files)
         try:
             cap = 4096
             while True:

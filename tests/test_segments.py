@@ -469,6 +469,16 @@ def test_block_indexes_answer_like_the_scan(tmp_path, dates):
     r = es2.list_events("Measurement", "Area", ["area-0"], c)
     assert (r.num_results, [(e.id, e.event_date) for e in r.results]) == \
         _brute(blocks, asg, "Measurement", "Area", {"area-0"}, c)
+    # a segment file retention deletes while a lookup holds the block table: its candidates are
+    # dropped (those ids are no longer stored), the lookup does not fail
+    ents = es2.seg.index_tr()[0]
+    gone = int(ents["file"][0])
+    real = es2.seg.file_path
+    es2.seg.file_path = lambda f: None if int(f) == gone else real(f)
+    found2 = es2.find_alternate_hashes([hash64(a) for _, a in picks])
+    assert set(found2.items()) <= set(found.items())
+    es2.list_events("Measurement", "Assignment", ["asg-3"], DateRangeSearchCriteria(page_size=0))
+    es2.seg.file_path = real
     es2.close()
 
 
