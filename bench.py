@@ -60,6 +60,11 @@ def parse():
     ap.add_argument("--p-ack", type=float, default=0.0005)
     ap.add_argument("--dedup-filter-ids", type=int, default=(1 << 29) - (1 << 22),
                     help="store-backed alternate-id filter: ids per generation (4 generations; 0 = off)")
+    ap.add_argument("--seed-filter-batches", type=int, default=0,
+                    help="(rehearsal) seed every rank's store-backed filter with the alternate ids of the first K "
+                         "pre-generated batches of every rank, never stored: filter false positives on demand, "
+                         "which their owners settle (pipeline/recheck.py).  Host engines only (the GPU path "
+                         "stamps fresh ids into every batch)")
     ap.add_argument("--p-meta", type=float, default=0.1,
                     help="share of events carrying metadata entries (stored with the event, like the reference)")
     ap.add_argument("--durable", action=argparse.BooleanOptionalAction, default=True,
@@ -163,11 +168,22 @@ def disk_probe(directory: str, mb: int, direct: bool = True) -> float:
 class _HostSink:
     """Block accounting of the host-engine path (same fields as DurableBlockSink)."""
 
-    def __init__(self, store):
+    def __init__(self, store, eng=None):
         self.store = store
-        self.bytes = self.rows = self.blocks = 0
+        self.eng = eng
+        self.bytes = self.rows = self.blocks = self.index_bytes = 0
 
     def add(self, blk):
+        if self.eng is not None:
+            # the same index trailer the MI355X builds in its step (csrc/native/swindex.cpp here):
+            # alternate ids, assignment zone maps, customer / area / asset key tables
+            from sitewhere_amd.persistence.segments import index_block
+            e = self.eng
+            n = e.n_assignments
+            ctx = np.stack([e.asg_device[:n], e.asg_customer[:n], e.asg_area[:n], e.asg_asset[:n]], axis=1)
+            n0 = len(blk)
+            blk = index_block(blk, ctx)
+            self.index_bytes += len(blk) - n0
         self.store.add_encoded(blk)
         self.bytes += len(blk)
         self.rows += int(blk[8:12].view(np.uint32)[0])
@@ -272,6 +288,16 @@ def main():
                             raw, offs_b, None if lens is None else torch.from_numpy(lens).pin_memory()))
         else:
             batches.append((None, None, raw, offs_b, None))
+    if args.seed_filter_batches and not use_gpu:
+        from sitewhere_amd.pipeline.fleet import cpu_decode
+        mine = np.concatenate([cpu_decode(b[2], b[3], now0)["alt_hash"] for b in batches[:args.seed_filter_batches]])
+        every = [mine]
+        if world > 1:
+            every = [None] * world
+            dist.all_gather_object(every, mine)
+        ids = np.concatenate(every)
+        eng.filter_seed_begin()
+        eng.filter_seed(ids[ids != 0])
     setup_s = time.time() - t0
     max_raw = max(int(b[2].size) for b in batches)
 
@@ -293,6 +319,25 @@ def main():
             runner.submit(None, None, 0, now_ms=now0)
             return True
         return False
+
+    # Several ranks: store-backed dedup rechecks are settled by their owner as a deployment does
+    # (pipeline/recheck.py): ids its durable store holds are duplicates, the filter's false
+    # positives re-enter the re-key carry (the GPU path re-injects them between rounds, on this
+    # thread).  ``held_hashes`` asks the store's alternate-id index; without a store nothing is held.
+    from sitewhere_amd.pipeline import recheck
+    settled = {"rechecks": 0, "duplicates": 0, "injected": 0, "lost": 0}
+    settle_q = []
+
+    def held_hashes(h):
+        if dur is None or not len(h):
+            return [False] * len(h)
+        found = dur["store"].find_alternate_hashes([int(x) for x in h])
+        return [int(x) in found for x in h]
+
+    def inject_settled():
+        while settle_q:
+            eng.inject_settled(*settle_q[0])
+            settle_q.pop(0)
     tmpdir = None
     boot = 0
     if use_gpu and args.bus and args.framing == "varint":
@@ -331,6 +376,16 @@ def main():
         def on_rejects(off, refs, compact):
             # the GPU copied the rejected payloads into `compact`; the router parses only those and
             # writes the reference's Kafka payloads natively (the held record serves overflow refs)
+            if world > 1:
+                # rechecks came as packages (record + strings): their owner settles them by
+                # alternate id against its store; false positives re-enter the carry between rounds
+                recs, spans, heap, lost = recheck.unpack_rechecks(refs, compact)
+                if len(recs) or lost:
+                    c = recheck.settle(eng, recs, spans, heap, held_hashes, by_hash=True,
+                                       inject=lambda *x: settle_q.append(x))
+                    for key in ("rechecks", "duplicates", "injected"):
+                        settled[key] += c[key]
+                    settled["lost"] += lost
             t0 = time.perf_counter()
             payload = raw_view(bus.view(t_raw, 0, off))[0]
             rr = routing.route_refs(compact, refs, rank, "bench", route_parts, raw=payload.data_ptr())
@@ -403,6 +458,7 @@ def main():
                 bus.commit(group, t_raw, 0, upto)
 
         def run(k):
+            inject_settled()
             if stall(runner):
                 commit_durable()
                 return
@@ -431,6 +487,7 @@ def main():
 
         def finish():
             runner.flush()
+            inject_settled()                                  # settled after the last round: carried
             if dur is not None:
                 dur["sink"].flush()                           # every block of the run is on disk
                 commit_durable()
@@ -458,7 +515,7 @@ def main():
             # the store keeps no row whose id the filter has forgotten (the blocks in flight are the
             # slack; EngineConfig.filter_retention_rows accounts for the file being written)
             store.limit_retention_rows(cfg.filter_retention_rows(16 * cfg.rec_cap))
-            dur = {"store": store, "sink": _HostSink(store)}
+            dur = {"store": store, "sink": _HostSink(store, eng)}
 
         def run(k):
             _, _, r, o, _ = batches[k % len(batches)]
@@ -468,6 +525,9 @@ def main():
             res = eng.step(r, o, now0 + k, presence=True)
             if dur is not None:
                 dur["sink"].add(eng.encode_block(now0 + k, res, boot=boot))
+            if world > 1:                           # the owner settles its rechecks (pipeline/recheck.py)
+                for key, v in recheck.settle_rechecks(eng, res, held_hashes, by_hash=True).items():
+                    settled[key] += v
 
         def finish():
             if dur is not None:
@@ -490,6 +550,7 @@ def main():
     finish()
     barrier()
     s0 = eng.stats_dict()
+    settled0 = dict(settled)
     d0 = dur["store"].seg.stats() if dur else None
     sk0 = (dur["sink"].bytes, dur["sink"].rows, dur["sink"].blocks, getattr(dur["sink"], "disk_wait_s", 0.0),
            getattr(dur["sink"], "index_bytes", 0)) if dur else None
@@ -553,11 +614,13 @@ def main():
     cons = [s1[k] - s0[k] for k in STAT_NAMES]
     cons.append(dur["sink"].rows - sk0[1] if dur else -1)
     cons.append(bus_stats["routed"]["payloads"] - r0["payloads"] if bus_stats else -1)
+    settle_keys = ["settled_" + k for k in settled]
+    cons += [settled[k] - settled0[k] for k in settled]
     if world > 1:
         ct = torch.tensor(cons, dtype=torch.int64, device=torch.device("cuda", local) if use_gpu else "cpu")
         dist.all_reduce(ct, op=dist.ReduceOp.SUM)
         cons = [int(x) for x in ct.tolist()]
-    c = dict(zip(STAT_NAMES + ["durable_rows", "routed_payloads"], cons))
+    c = dict(zip(STAT_NAMES + ["durable_rows", "routed_payloads"] + settle_keys, cons))
     rejected = c["unregistered"] + c["unassigned"] + c["duplicates"] + c["decode_errors"] + c["control"] + \
         c["dedup_rechecks"]
     checks = {"persisted == events - rejected + rule_alerts + presence":
@@ -567,10 +630,16 @@ def main():
     if dur:
         checks["durable rows == persisted"] = c["durable_rows"] == c["persisted"]
         checks["every block durable"] = bool(dur["sink"].store.durable() >= dur["sink"].store.seg.last_token)
+    if world > 1 and cfg.str_cap:
+        checks["rechecks settled by their owner == duplicates + re-injected"] = \
+            c["settled_rechecks"] + c["settled_lost"] == c["dedup_rechecks"] and \
+            c["settled_rechecks"] == c["settled_duplicates"] + c["settled_injected"] and c["settled_lost"] == 0
     if bus_stats:
+        # one rank routes its rechecks' payloads to the per-event path; several settle them
+        routed_rk = c["dedup_rechecks"] if world == 1 or not cfg.str_cap else 0
         checks["routed payloads == unregistered + unassigned + control + decode errors + rechecks"] = \
             c["routed_payloads"] == c["unregistered"] + c["unassigned"] + c["control"] + c["decode_errors"] + \
-            c["dedup_rechecks"]
+            routed_rk
         checks["raw topic fully committed"] = \
             bus_stats["bus"].committed(bus_stats["group"], bus_stats["t_raw"], 0) == \
             bus_stats["bus"].end_offset(bus_stats["t_raw"], 0)
@@ -610,6 +679,7 @@ def main():
         detail["shuffle_deferred"] = s1.get("shuffle_deferred", 0) - s0.get("shuffle_deferred", 0)
         detail["shuffle_overflow"] = s1.get("shuffle_overflow", 0) - s0.get("shuffle_overflow", 0)
         detail["stall_rounds"] = stalls["rounds"]
+        detail["rechecks_settled"] = {k: c["settled_" + k] for k in settled}
     if bus_stats:
         r1 = bus_stats["routed"]
         bus = bus_stats["bus"]

@@ -1795,11 +1795,20 @@ __global__ __launch_bounds__(BLK) void k_store_filter(const uint8_t* __restrict_
 // and zeroes for the next launch (no memset before each snapshot; the allocation starts zeroed).  `refs`
 // (u32[4 * cap]) and `bytes` are usually mapped pinned host memory: written straight over PCIe, no
 // copy call.  Refs are in any order; events decoded on another rank keep start = end = 0.
+//
+// Several ranks with strings exchanged (wstr != null): a recheck is settled by its owner by
+// alternate id (pipeline/recheck.py), whatever rank decoded it, so instead of its payload the copy
+// holds a recheck package -- the 80-byte record, its SwStrRef and its strings (alternate id,
+// metadata, alert message) back to back, string offsets relative to the strings' start (the layout
+// of recheck.compact_strings) -- and the ref is (0, package bytes, status | src_rank << 8 |
+// SW_REF_PACKED, offset of the package).
+#define SW_REF_PACKED 0x10000u
 __global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_t* __restrict__ rej_idx,
                               const uint32_t* __restrict__ n_rej_ptr, const uint8_t* __restrict__ status,
                               const uint8_t* __restrict__ raw, const uint32_t* __restrict__ msg_off, int64_t n_msgs,
                               int rank, uint32_t* __restrict__ out, uint32_t* __restrict__ refs, int64_t cap,
-                              uint8_t* __restrict__ bytes, int64_t bytes_cap) {
+                              uint8_t* __restrict__ bytes, int64_t bytes_cap, const SwStrRef* __restrict__ wsp,
+                              const uint8_t* __restrict__ wstr) {
   __shared__ uint32_t last;
   const uint32_t n = *n_rej_ptr;
   uint32_t* acc = out + 4;
@@ -1808,8 +1817,39 @@ __global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_
     const uint8_t st = status[i];
     if (st == SW_ST_DUPLICATE) continue;
     const SwEventRec& r = work[i];
-    uint32_t s = 0, e = 0, copy = 0xffffffffu;
-    if (r.src_rank == (uint8_t)rank && n_msgs > 0) {
+    uint32_t s = 0, e = 0, copy = 0xffffffffu, packed = 0u;
+    if (st == SW_ST_RECHECK && wstr != nullptr) {
+      const SwStrRef sp = wsp[i];
+      const uint32_t al = (sp.has & SW_SR_ALT) ? sp.alt_len : 0u;
+      const uint32_t ml = (sp.has & SW_SR_META) ? sp.meta_len : 0u;
+      const uint32_t gl = r.etype == SW_EV_ALERT ? r.aux2_len : 0u;
+      const uint32_t sl = al + ml + gl;
+      const uint32_t len = (uint32_t)(sizeof(SwEventRec) + sizeof(SwStrRef)) + sl;
+      const uint32_t at = atomicAdd(acc + 1, len);
+      packed = SW_REF_PACKED;
+      e = len;
+      if ((int64_t)at + len <= bytes_cap) {
+        SwEventRec c = r;
+        if (r.etype == SW_EV_ALERT) c.aux2_off = gl ? al + ml : 0u;
+        SwStrRef o = sp;
+        o.alt_off = 0u;
+        o.meta_off = sl ? al : 0u;
+        o.alt_len = (uint16_t)al;
+        o.meta_len = (uint16_t)ml;
+        if (!sl) o.has = sp.has & SW_SR_MULTI;
+        const uint8_t* cb = reinterpret_cast<const uint8_t*>(&c);
+        const uint8_t* ob = reinterpret_cast<const uint8_t*>(&o);
+        uint8_t* d = bytes + at;
+        for (uint32_t b = 0; b < sizeof(SwEventRec); ++b) d[b] = cb[b];
+        d += sizeof(SwEventRec);
+        for (uint32_t b = 0; b < sizeof(SwStrRef); ++b) d[b] = ob[b];
+        d += sizeof(SwStrRef);
+        for (uint32_t b = 0; b < al; ++b) d[b] = wstr[sp.alt_off + b];
+        for (uint32_t b = 0; b < ml; ++b) d[al + b] = wstr[sp.meta_off + b];
+        for (uint32_t b = 0; b < gl; ++b) d[al + ml + b] = wstr[r.aux2_off + b];
+        copy = at;
+      }
+    } else if (r.src_rank == (uint8_t)rank && n_msgs > 0) {
       int64_t lo = 0, hi = n_msgs;              // msg_off[lo] <= off < msg_off[hi]
       const uint32_t off = r.aux_off;
       while (hi - lo > 1) {
@@ -1829,7 +1869,7 @@ __global__ void k_reject_refs(const SwEventRec* __restrict__ work, const uint32_
     if (k < cap) {
       refs[4 * k] = s;
       refs[4 * k + 1] = e;
-      refs[4 * k + 2] = (uint32_t)st | ((uint32_t)r.src_rank << 8);
+      refs[4 * k + 2] = (uint32_t)st | ((uint32_t)r.src_rank << 8) | packed;
       refs[4 * k + 3] = copy;
     }
   }
@@ -1856,7 +1896,8 @@ int sw_reject_refs(const SwEngineArgs* ap, const uint8_t* raw, const uint32_t* m
   // per workgroup on one word) off the critical path
   const int g = grid_for(a.rec_cap) < 256 ? grid_for(a.rec_cap) : 256;
   k_reject_refs<<<g, BLK, 0, s>>>(a.work, a.rej_idx, a.n_rej, a.status, raw, msg_off, n_msgs,
-                                                    (int)a.rank, out, refs, cap, bytes, bytes_cap);
+                                  (int)a.rank, out, refs, cap, bytes, bytes_cap,
+                                  a.world > 1 ? a.work_spans : nullptr, a.world > 1 ? a.work_str : nullptr);
   return (int)hipGetLastError();
 }
 

@@ -339,16 +339,28 @@ int64_t swseg_ix_asgs_pages(const uint8_t* const* t, int64_t n, const int32_t* a
     SwIxHdr h;
     memcpy(&h, x, sizeof(h));
     const SwIxPage* pg = reinterpret_cast<const SwIxPage*>(x + h.off_pages);
+    int64_t at = 0;                     // lower bound of the previous page's asg_min
+    int32_t prev_min = INT32_MIN;
     for (uint32_t p = 0; p < h.n_pages; ++p) {
       const SwIxPage& q = pg[p];
       if (q.date_max < d_lo || q.date_min > d_hi) continue;
-      // the first wanted assignment not below the page's range (a lower bound per page: API-added
-      // blocks are not clustered, so page ranges need not ascend)
-      int64_t lo = 0, hi = n_asg;
-      while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (asgs[mid] < q.asg_min) lo = mid + 1; else hi = mid;
+      // the first wanted assignment not below the page's range: walked forward while page ranges
+      // ascend (the block's assignment-sorted pages), a binary search where they do not (its
+      // generated rows; API-added blocks are not clustered)
+      int64_t lo;
+      if (q.asg_min >= prev_min) {
+        lo = at;
+        while (lo < n_asg && asgs[lo] < q.asg_min) ++lo;
+      } else {
+        lo = 0;
+        int64_t hi = n_asg;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (asgs[mid] < q.asg_min) lo = mid + 1; else hi = mid;
+        }
       }
+      at = lo;
+      prev_min = q.asg_min;
       if (lo < n_asg && asgs[lo] <= q.asg_max) {     // one falls in [asg_min, asg_max]
         if (k < cap) {
           out_blk[k] = i;
@@ -499,6 +511,35 @@ struct ScanHit {
   int64_t date;
 };
 
+// All n codes of a bit-packed column (bits < 57) in order, one 64-bit word read per 64 bits: the
+// sequential form of ix_unpack for a whole page column.
+inline void ix_unpack_all(const uint8_t* words, uint32_t n, int bits, uint32_t* out) {
+  if (bits == 0) {
+    for (uint32_t r = 0; r < n; ++r) out[r] = 0;
+    return;
+  }
+  const uint64_t mask = (1ull << bits) - 1;
+  uint64_t cur;
+  memcpy(&cur, words, 8);
+  const uint8_t* next = words + 8;
+  int avail = 64;
+  for (uint32_t r = 0; r < n; ++r) {
+    if (avail >= bits) {
+      out[r] = (uint32_t)(cur & mask);
+      cur = avail == bits ? 0 : cur >> bits;
+      avail -= bits;
+    } else {
+      uint64_t nw;
+      memcpy(&nw, next, 8);
+      next += 8;
+      out[r] = (uint32_t)((cur | (nw << avail)) & mask);
+      const int used = bits - avail;
+      cur = nw >> used;
+      avail = 64 - used;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -558,11 +599,61 @@ int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint3
       const SwSegCol& ce = ph.cols[SEG_ETYPE];
       const SwSegCol& cd = ph.cols[SEG_DATE];
       const int32_t row0 = pg_index[i] * SEG_PAGE_ROWS;
+      // a page whose event types all differ from et (e.g. the block's generated alerts, persisted
+      // after its assignment-sorted events, when listing measurements): its frame of reference says so
+      if (et >= 0 && ce.bits < 32) {
+        const int64_t t_lo = seg_unord(ce.base), t_hi = seg_unord(ce.base + ((1ull << ce.bits) - 1));
+        if (et < t_lo || et > t_hi) continue;
+      }
       if (asg_list) {
         // the wanted assignments this page may hold (sorted, asg_list[task_lo .. task_hi)): the
         // assignment column first -- one compare for the usual single candidate -- and the type
         // and date only for its rows (no per-row context table lookup)
         const int64_t l0 = task_lo[i], l1 = task_hi[i];
+        if (ca.bits <= 32) {
+          // the whole assignment column unpacked sequentially, compared as codes (value - base)
+          uint32_t codes[SEG_PAGE_ROWS];
+          ix_unpack_all(pg + ca.data_off, ph.n_rows, ca.bits, codes);
+          auto keep = [&](uint32_t r) {
+            if (et >= 0 && (int32_t)seg_unord(ce.base + ix_unpack(pg + ce.data_off, r, ce.bits)) != et) return;
+            const int64_t d = seg_unord(cd.base + ix_unpack(pg + cd.data_off, r, cd.bits));
+            if (d < d_lo || d > d_hi) return;
+            hits[w].push_back({i, row0 + (int32_t)r, d});
+          };
+          if (l1 - l0 == 1) {
+            const uint64_t c = seg_ord(asg_list[l0]) - ca.base;
+            if (ca.bits && c >> ca.bits) continue;           // not in this page's range
+            if (!ca.bits && c) continue;
+            const uint32_t cc = (uint32_t)c;
+            for (uint32_t r = 0; r < ph.n_rows; ++r)
+              if (codes[r] == cc) keep(r);
+          } else if (l1 - l0 <= 16) {
+            // a few candidates (a page straddling them): one compare pass per candidate, the
+            // matching rows then kept in row order
+            uint32_t mrow[SEG_PAGE_ROWS];
+            uint32_t nm = 0;
+            for (int64_t q = l0; q < l1; ++q) {
+              const uint64_t c = seg_ord(asg_list[q]) - ca.base;
+              if (ca.bits ? (c >> ca.bits) != 0 : c != 0) continue;
+              const uint32_t cc = (uint32_t)c;
+              for (uint32_t r = 0; r < ph.n_rows; ++r)
+                if (codes[r] == cc && nm < SEG_PAGE_ROWS) mrow[nm++] = r;
+            }
+            std::sort(mrow, mrow + nm);
+            for (uint32_t j = 0; j < nm; ++j) keep(mrow[j]);
+          } else {
+            for (uint32_t r = 0; r < ph.n_rows; ++r) {
+              const uint64_t v = ca.base + codes[r];          // ordered value; asg_list is sorted
+              int64_t lo = l0, hi = l1;
+              while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (seg_ord(asg_list[mid]) < v) lo = mid + 1; else hi = mid;
+              }
+              if (lo < l1 && seg_ord(asg_list[lo]) == v) keep(r);
+            }
+          }
+          continue;
+        }
         for (uint32_t r = 0; r < ph.n_rows; ++r) {
           const int32_t a = (int32_t)seg_unord(ca.base + ix_unpack(pg + ca.data_off, r, ca.bits));
           if (l1 - l0 == 1) {

@@ -544,7 +544,8 @@ int64_t sw_route_rejects(const uint8_t* raw, const uint32_t* offs, int64_t n_msg
 // refs: n x (payload start, payload end, status | src_rank << 8, copy offset) as the MI355X step
 // snapshot them (k_reject_refs).  Payloads are parsed from `compact` at their copy offset, or from
 // the raw batch `raw` (may be null) when the copy did not fit (offset ~0).  Only refs whose
-// src_rank == rank are routed.
+// src_rank == rank are routed; recheck packages (bit 16 of the status word, several ranks:
+// pipeline/recheck.py settles them) are not.
 int64_t sw_route_refs(const uint8_t* compact, const uint8_t* raw, const uint32_t* refs, int64_t n, int32_t rank,
                       const char* source_id, const int32_t* parts, int32_t* rec, int64_t rec_cap, uint8_t* key_heap,
                       int64_t key_cap, uint8_t* val_heap, int64_t val_cap, int64_t* need, int64_t* payloads_out) {
@@ -553,6 +554,7 @@ int64_t sw_route_refs(const uint8_t* compact, const uint8_t* raw, const uint32_t
   for (int64_t i = 0; i < n; ++i) {
     const uint32_t s = refs[4 * i], e = refs[4 * i + 1], st = refs[4 * i + 2] & 0xff, src = refs[4 * i + 2] >> 8;
     const uint32_t c = refs[4 * i + 3];
+    if (refs[4 * i + 2] & 0x10000u) continue;          // a recheck package: settled by its owner
     if (st == 3 || st == 0 || (int32_t)src != rank || e <= s) continue;
     if (c != 0xffffffffu) hit.push_back({((uint64_t)s << 32) | e, c, c + (e - s), (uint8_t)st});
     else spill.push_back({((uint64_t)s << 32) | e, s, e, (uint8_t)st});

@@ -705,6 +705,30 @@ def _leased(fn):
     return run
 
 
+class _FileMap:
+    """A read-only shared map of a segment file (libc ``mmap``: it may reserve more than the file
+    holds, which Python's ``mmap`` refuses), unmapped when the last holder lets go."""
+
+    _libc = None
+
+    def __init__(self, fd: int, length: int):
+        if _FileMap._libc is None:
+            lib = ctypes.CDLL(None, use_errno=True)
+            lib.mmap.restype = ctypes.c_void_p
+            lib.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_long]
+            lib.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+            _FileMap._libc = lib
+        self.length = int(length)
+        a = _FileMap._libc.mmap(None, self.length, 1, 1, int(fd), 0)      # PROT_READ, MAP_SHARED
+        self.addr = 0 if a in (None, ctypes.c_void_p(-1).value) else int(a)
+
+    def __del__(self):
+        if self.addr and _FileMap._libc is not None:
+            _FileMap._libc.munmap(self.addr, self.length)
+            self.addr = 0
+
+
 class DurableEventStore(DeviceEventStore):
     """Event store of engine tenants on durable segments (see module docstring).
 
@@ -1625,6 +1649,74 @@ class DurableEventStore(DeviceEventStore):
             raise
         return np.asarray(fds, np.int32)[inv.reshape(-1)], opened
 
+    @property
+    def _map_reserve(self) -> int:
+        # a file ends with the first block past its rotation size: reserve one large block beyond it
+        return self.rotate_bytes + (256 << 20)
+
+    def _map_file(self, fid: int, end: int):
+        """A read-only map (:class:`_FileMap`) of segment file ``fid`` covering at least its first
+        ``end`` bytes, or None when the file is gone.  The map reserves the file's whole rotation
+        size, so the file being appended to needs no new map as it grows: only pages of blocks the
+        store has indexed (written) are ever read through it.  Maps are shared by the readers; a
+        caller keeps the object it got for as long as it reads through the address (a dropped map is
+        unmapped once no reader holds it).  Files are only appended to, and only cut back to their
+        written bytes, so a map never loses a page it is read at."""
+        import threading
+        lock = self.__dict__.setdefault("_map_lock", threading.Lock())
+        maps = self.__dict__.setdefault("_maps", {})
+        path = self.seg.file_path(int(fid))
+        if path is None:                  # retention deleted it: its rows are gone for this reader too
+            with lock:
+                maps.pop(fid, None)
+            return None
+        with lock:
+            e = maps.get(fid)
+            if e is not None and e.length >= end:
+                return e
+        try:
+            fd = os.open(path, os.O_RDONLY)
+        except FileNotFoundError:
+            return None
+        try:
+            size = os.fstat(fd).st_size
+            if size < end:
+                return None
+            e = _FileMap(fd, max(size, end, self._map_reserve))
+        finally:
+            os.close(fd)
+        if not e.addr:
+            return None
+        with lock:
+            maps[fid] = e
+            if len(maps) > 1 and fid == max(maps):
+                # a new file: forget the maps of files retention deleted
+                for f in [f for f in maps if self.seg.file_path(int(f)) is None]:
+                    del maps[f]
+        return e
+
+    def _mapped_pages(self, files, pos, nb, mem):
+        """``mem`` with the address of every task's page in a map of its segment file where it had
+        none (0 where the file is gone), and the maps to hold while reading."""
+        mem = np.zeros(len(files), np.uint64) if mem is None else np.array(mem, np.uint64)
+        need = np.nonzero(mem == 0)[0]
+        held = []
+        if not len(need):
+            return mem, held
+        f = np.asarray(files, np.int64)[need]
+        p = np.asarray(pos, np.int64)[need]
+        end = p + np.asarray(nb, np.int64)[need]
+        uf, inv = np.unique(f, return_inverse=True)
+        base = np.zeros(len(uf), np.uint64)
+        for j, fid in enumerate(uf.tolist()):
+            e = self._map_file(fid, int(end[inv == j].max()))
+            if e is not None:
+                held.append(e)
+                base[j] = e.addr
+        b = base[inv.reshape(-1)]
+        mem[need] = np.where(b != 0, b + p.astype(np.uint64), np.uint64(0))
+        return mem, held
+
     @staticmethod
     def _readable(fd: np.ndarray, mem) -> np.ndarray:
         """Tasks whose page can still be read: from its file, or from the store's memory copy."""
@@ -1776,7 +1868,13 @@ class DurableEventStore(DeviceEventStore):
         if not len(bis):
             return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
         files, pos, nb, _, mem = self._page_geometry(t, bis, pages, scan=True)
-        fd, opened = self._file_fds(files, missing_ok=True)
+        # pages read in place through maps of their files (no read call and copy per page); a page
+        # whose file is gone is read from the store's scan image, or dropped
+        mem, held = self._mapped_pages(files, pos, nb, mem)
+        fd, opened = self._file_fds(files[mem == 0], missing_ok=True)
+        fd_all = np.full(len(files), -1, np.int32)
+        fd_all[mem == 0] = fd
+        fd = fd_all
         keep = self._readable(fd, mem)
         if not keep.all():             # retention deleted a file meanwhile: its rows are gone
             sel = np.nonzero(keep)[0]

@@ -81,20 +81,63 @@ def alternate_ids(spans: np.ndarray, heap: np.ndarray) -> list:
     return out
 
 
-def settle_rechecks(engine, res, held) -> dict:
+def settle_rechecks(engine, res, held, by_hash: bool = False, inject=None) -> dict:
     """Settle the rechecks of one step result on the rank that owns them: ``held(ids)`` -> one bool
-    per alternate id (the store holds it).  Held ids are duplicates; the rest are re-injected into
-    the engine's carry, filter-settled.  Returns counts."""
+    per alternate id (the store holds it); ``by_hash``: ``held`` gets the ids' 64-bit hashes
+    (``EVENT_REC["alt_hash"]``, what the durable store's alternate-id index answers) instead of the
+    strings.  Held ids are duplicates; the rest are re-injected into the engine's carry,
+    filter-settled -- or handed to ``inject(recs, spans, heap)`` when the caller re-injects them
+    later (between pipelined rounds).  Returns counts."""
     rc = engine.rechecks(res)
     if rc is None:
         return {"rechecks": 0, "duplicates": 0, "injected": 0}
-    recs, spans, heap = rc
-    ids = alternate_ids(spans, heap)
-    dup = np.fromiter((bool(x) for x in held(ids)), bool, len(ids))
+    return settle(engine, *rc, held, by_hash=by_hash, inject=inject)
+
+
+def settle(engine, recs, spans, heap, held, by_hash: bool = False, inject=None) -> dict:
+    """:func:`settle_rechecks` of rechecks already in the compact layout."""
+    n = len(recs)
+    keys = np.asarray(recs["alt_hash"], np.uint64) if by_hash else alternate_ids(spans, heap)
+    dup = np.fromiter((bool(x) for x in held(keys)), bool, n) if n else np.zeros(0, bool)
     keep = ~dup
     if keep.any():
-        engine.inject_settled(*_select(recs, spans, heap, keep))
-    return {"rechecks": len(ids), "duplicates": int(dup.sum()), "injected": int(keep.sum())}
+        (inject or engine.inject_settled)(*_select(recs, spans, heap, keep))
+    return {"rechecks": n, "duplicates": int(dup.sum()), "injected": int(keep.sum())}
+
+
+REF_PACKED = 0x10000       # k_reject_refs: the ref's copy is a recheck package, not a payload
+_PKG_HDR = 80              # SwEventRec
+_SREF = 16                 # SwStrRef
+
+
+def unpack_rechecks(refs: np.ndarray, compact: np.ndarray):
+    """The recheck packages of a reject snapshot (``k_reject_refs`` with strings exchanged: per
+    recheck the 80-byte record, its string ref and its strings back to back) as (records, refs,
+    heap) in the compact layout, plus the number of packages that did not fit the snapshot's byte
+    buffer (those rechecks cannot be settled from it)."""
+    from ..models.columnar import EVENT_REC, STR_REF
+    refs = np.asarray(refs, np.uint32).reshape(-1, 4)
+    pk = refs[(refs[:, 2] & REF_PACKED) != 0]
+    have = pk[pk[:, 3] != 0xFFFFFFFF]
+    lost = len(pk) - len(have)
+    comp = np.asarray(compact, np.uint8)
+    recs = np.zeros(len(have), EVENT_REC)
+    spans = np.zeros(len(have), STR_REF)
+    parts, base = [], 0
+    for j, (_, ln, _, at) in enumerate(have.tolist()):
+        blob = comp[at:at + ln]
+        recs[j] = blob[:_PKG_HDR].view(EVENT_REC)[0]
+        spans[j] = blob[_PKG_HDR:_PKG_HDR + _SREF].view(STR_REF)[0]
+        s = blob[_PKG_HDR + _SREF:]
+        if len(s):
+            spans[j]["alt_off"] += base
+            spans[j]["meta_off"] += base
+            if recs[j]["etype"] == EV_ALERT and recs[j]["aux2_len"]:
+                recs[j]["aux2_off"] += base
+        parts.append(np.array(s, copy=True))
+        base += len(s)
+    heap = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return recs, spans, heap, lost
 
 
 def _select(recs, spans, heap, mask):

@@ -174,8 +174,10 @@ def test_small_string_slabs_defer_records_with_their_strings():
     assert sorted(got) == sorted(ref)
 
 
-def _gpu_round(g, bs):
-    """One loopback round of the W shards: decode + partition, slab copies, process; results."""
+def _gpu_round(g, bs, packages=None):
+    """One loopback round of the W shards: decode + partition, slab copies, process; results.
+    ``packages``: a list that gets each shard's recheck packages from its reject snapshot
+    (``k_reject_refs``, what ``bench.py``'s pipelined path settles)."""
     import torch
     keep = []
     for e, (raw, offs) in zip(g, bs):
@@ -189,9 +191,16 @@ def _gpu_round(g, bs):
             g[q].t["recv_cnt"][r] = g[r].send_count(q)
         g[q].loopback_strings(g)
     out = []
-    for (raw, _), e in zip(bs, g):
+    for (raw, offs), e, dev in zip(bs, g, keep):
         e.phase_process()
         torch.cuda.synchronize()
+        if packages is not None:
+            from sitewhere_amd.pipeline.recheck import unpack_rechecks
+            cnt, _ = e.reject_refs_async(e._last_sel, dev[0], dev[1], len(offs) - 1)
+            torch.cuda.synchronize()
+            n_ref, n_b = (int(v) for v in cnt[:2].cpu())
+            refs, comp = e.reject_snapshot(e._last_sel, n_ref, n_b)
+            packages.append(unpack_rechecks(refs.copy(), comp.copy()))
         out.append(e.collect(e._last_sel, raw, from_device=True))
     return out
 
@@ -219,10 +228,32 @@ def test_gpu_rechecks_are_settled_by_alternate_id_on_the_owner():
     totals = {"rechecks": 0, "duplicates": 0, "injected": 0}
     empty = (np.zeros(64, np.uint8), np.zeros(1, np.uint32))
 
+    packaged = {"same": 0}
+
+    def same_rechecks(pkg, rc):
+        # the snapshot's packages hold the rechecks collect() gathers, strings included
+        from sitewhere_amd.pipeline.recheck import alternate_ids
+        pr, ps, ph, lost = pkg
+        assert lost == 0
+        if rc is None:
+            assert len(pr) == 0
+            return
+
+        def rows(r, s, h):
+            msg = [bytes(h[int(x["aux2_off"]):int(x["aux2_off"]) + int(x["aux2_len"])]) if x["etype"] == 2 else b""
+                   for x in r]
+            meta = [bytes(h[int(y["meta_off"]):int(y["meta_off"]) + int(y["meta_len"])]) for y in s]
+            return sorted(zip(r["alt_hash"].tolist(), r["event_date"].tolist(), r["etype"].tolist(),
+                              alternate_ids(s, h), meta, msg))
+        assert rows(pr, ps, ph) == rows(*rc)
+        packaged["same"] += len(pr)
+
     def run(bs):
         for k in range(20):
-            res = _gpu_round(g, bs if k == 0 else [empty] * W)
+            pk = []
+            res = _gpu_round(g, bs if k == 0 else [empty] * W, packages=pk)
             for r, (e, x) in enumerate(zip(g, res)):
+                same_rechecks(pk[r], x.recheck)
                 for key in _row_keys(e.encode_block(NOW, x, boot=0x5)):
                     if key[3]:
                         stores[r][key[3]] = stores[r].get(key[3], 0) + 1
@@ -236,6 +267,7 @@ def test_gpu_rechecks_are_settled_by_alternate_id_on_the_owner():
     run(first)
     run(second)
     assert totals["injected"] > 1000 and totals["duplicates"] == 0, totals
+    assert packaged["same"] == totals["rechecks"], packaged
     stored = {}
     for s in stores:
         for a, n in s.items():

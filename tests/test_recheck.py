@@ -72,3 +72,48 @@ def test_inject_settled_appends_to_the_oracle_carry():
     e2 = CpuInboundEngine(EngineConfig.small(world=2, rank=0))
     e2.restore_state(st, include_store=False)
     assert np.array_equal(e2.carry_heap, e.carry_heap) and np.array_equal(e2.carry_sp, e.carry_sp)
+
+
+def _packages(recs, spans, heap):
+    """Recheck packages as ``k_reject_refs`` writes them (csrc/hip/swgpu.hip): record, string ref
+    (offsets relative to the strings), strings; refs (0, bytes, status | src << 8 | packed, at)."""
+    from sitewhere_amd.pipeline.recheck import REF_PACKED
+    r, s, h = compact_strings(recs, spans, lambda pos: heap[pos])
+    buf, refs = bytearray(b"pad"), []
+    for i in range(len(r)):
+        al, ml = int(s["alt_len"][i]), int(s["meta_len"][i])
+        gl = int(r["aux2_len"][i]) if r["etype"][i] == EV_ALERT else 0
+        base = int(s["alt_off"][i])
+        one_r, one_s = r[i:i + 1].copy(), s[i:i + 1].copy()
+        if al + ml + gl:
+            one_s["alt_off"], one_s["meta_off"] = 0, al
+            if gl:
+                one_r["aux2_off"] = al + ml
+        strings = bytes(h[base:base + al + ml + gl])
+        at = len(buf)
+        buf += one_r.tobytes() + one_s.tobytes() + strings
+        refs.append((0, 96 + len(strings), 6 | (1 << 8) | REF_PACKED, at))
+    refs.append((5, 9, 1, 0))                                    # an unregistered payload's ref
+    refs.append((0, 120, 6 | REF_PACKED, 0xFFFFFFFF))             # a package that did not fit
+    return np.array(refs, np.uint32), np.frombuffer(bytes(buf), np.uint8)
+
+
+def test_unpack_rechecks_and_settle_later():
+    """The owner reads rechecks from a reject snapshot's packages (several ranks, bench.py's
+    pipelined path) and settles them: held ids are duplicates, the rest are handed to a deferred
+    injector (re-injected between rounds)."""
+    from sitewhere_amd.pipeline.recheck import settle, unpack_rechecks
+    recs, spans, heap = _records()
+    refs, comp = _packages(recs[:3], spans[:3], heap)
+    r, s, h, lost = unpack_rechecks(refs, comp)
+    assert lost == 1 and len(r) == 3
+    assert alternate_ids(s, h) == ["alt-zero", "alt-multi:1", "alt-alert"]
+    assert bytes(h[int(r["aux2_off"][2]):int(r["aux2_off"][2]) + 9]) == b"door open"
+    assert bytes(h[int(s["meta_off"][0]):int(s["meta_off"][0]) + 6]) == b"\x22\x04name"
+    r["alt_hash"] = [11, 22, 33]
+    later = []
+    c = settle(None, r, s, h, lambda hs: [int(x) == 22 for x in hs], by_hash=True,
+               inject=lambda *x: later.append(x))
+    assert c == {"rechecks": 3, "duplicates": 1, "injected": 2}
+    (ir, isp, ih), = later
+    assert list(ir["alt_hash"]) == [11, 33] and alternate_ids(isp, ih) == ["alt-zero", "alt-alert"]
