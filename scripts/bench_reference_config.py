@@ -197,6 +197,8 @@ def per_event_replicas(args) -> dict:
     from sitewhere_amd.runtime.topology import TopologyStateAggregator
 
     logdir = tempfile.mkdtemp(prefix="swbench-")
+    from sitewhere_amd.utils.stack_sampler import maybe_start
+    maybe_start()                                 # SW_STACK_SAMPLE: this process hosts the infra server
     infra = InfraServer(EventBus(None, default_partitions=8), Coordination(None), port=0).start()
     groups = [["instance-management", "user-management", "tenant-management"],
               ["device-management", "event-management"],
