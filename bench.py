@@ -336,7 +336,12 @@ def main():
 
     def inject_settled():
         while settle_q:
-            eng.inject_settled(*settle_q[0])
+            try:
+                eng.inject_settled(*settle_q[0])
+            except RuntimeError as e:               # carry full: retried after the next round drains it
+                if "carry full" not in str(e):
+                    raise
+                return
             settle_q.pop(0)
     tmpdir = None
     boot = 0

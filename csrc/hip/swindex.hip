@@ -252,6 +252,7 @@ struct SwIxScratch {
   uint32_t finish_done;
   uint32_t err;
   uint32_t n_sort;           // rows this step (the radix sort's count)
+  uint32_t unsorted;         // some row breaks SIX_F_CLUSTERED (k_ix_prep)
 };
 
 #define IX_CHUNK 1024          // bucket rows per wave in the heads pass
@@ -357,6 +358,14 @@ __global__ __launch_bounds__(IX_PREP_BLK) void k_ix_prep(SwIxArgs a) {
     a.svals[j] = (uint32_t)j;
   }
   for (int off = 32; off >= 1; off >>= 1) nalt += __shfl_xor(nalt, off, 64);
+  // SIX_F_CLUSTERED: persisted rows first, their assignments non-decreasing (row j against j - 1)
+  bool bad = false;
+  for (int64_t j = r0 + threadIdx.x; j < r1; j += IX_PREP_BLK) {
+    if (j == 0) continue;
+    const bool g0 = a.aux && (a.aux[j - 1].flags & SEGF_GEN), g1 = a.aux && (a.aux[j].flags & SEGF_GEN);
+    bad |= (g0 && !g1) || (!g0 && !g1 && a.rows[j].assignment < a.rows[j - 1].assignment);
+  }
+  if (__ballot(bad) && ix_lane() == 0) atomicOr(&a.sc->unsorted, 1u);
   __syncthreads();
   if (ix_lane() == 0 && nalt) atomicAdd(&lalt, nalt);
   // context keys, one sweep per LDS pass
@@ -509,6 +518,7 @@ __global__ __launch_bounds__(IX_SCAN_BLK) void k_ix_scan(SwIxArgs a) {
   h.n_alt = atomicAdd(&sc->n_alt, 0u);
   h.alt_bits = six_alt_bits(h.n_alt);
   h.alt_pbits = six_page_bits((uint32_t)np);
+  h.flags = __hip_atomic_load(&sc->unsorted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 0u : SIX_F_CLUSTERED;
   for (int q = 0; q < SIX_DIMS; ++q) {
     h.n_keys[q] = __hip_atomic_load(&sc->h.n_keys[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h.n_heads[q] = __hip_atomic_load(&sc->h.n_heads[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -944,6 +954,7 @@ __global__ __launch_bounds__(IX_WBLK) void k_ix_finish(SwIxArgs a) {
   }
   sc->cs = 0;
   sc->n_alt = 0;
+  sc->unsorted = 0;
   sc->scans_done = 0;
   sc->finish_done = 0;
   sc->err = 0;

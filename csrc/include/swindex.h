@@ -66,8 +66,14 @@ typedef struct __attribute__((aligned(8))) SwIxHdr {
   uint32_t off_heads[SIX_DIMS];     // head rows (u32)
   uint32_t n_heads[SIX_DIMS];
   uint32_t off_hdates[SIX_DIMS];    // head dates (i64), same order
-  uint32_t pad[3];
+  uint32_t flags;                  // SIX_F_*
+  uint32_t pad[2];
 } SwIxHdr;
+
+// SwIxHdr.flags: every engine-persisted row precedes every generated row (SEGF_GEN) and the persisted
+// rows' assignments never decrease -- a page without generated rows is sorted by assignment, so a
+// reader binary-searches its assignment column instead of reading every row
+#define SIX_F_CLUSTERED 1u
 
 typedef struct __attribute__((aligned(8))) SwIxPage {
   int32_t asg_min, asg_max;

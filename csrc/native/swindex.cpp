@@ -102,6 +102,12 @@ int64_t swseg_index_append(uint8_t* block, int64_t cap, const int32_t* ctx, int6
   h.n_dims = SIX_DIMS;
   h.n_rows = (uint32_t)n;
   h.n_pages = (uint32_t)np;
+  bool clustered = true;
+  for (int64_t r = 1; r < n && clustered; ++r) {
+    const bool g0 = fl[r - 1] & SEGF_GEN, g1 = fl[r] & SEGF_GEN;
+    if ((g0 && !g1) || (!g0 && !g1 && asg[r] < asg[r - 1])) clustered = false;
+  }
+  h.flags = clustered ? SIX_F_CLUSTERED : 0u;
   // ---- alternate ids: (sort key, row) order
   std::vector<uint64_t> ah;
   std::vector<uint32_t> ar;
@@ -330,7 +336,7 @@ int64_t swseg_ix_asg_pages(const uint8_t* const* t, int64_t n, int32_t asg, int6
 // assignments in one call.  Returns the pages found (> cap: call again with that cap).
 int64_t swseg_ix_asgs_pages(const uint8_t* const* t, int64_t n, const int32_t* asgs, int64_t n_asg,
                             const uint8_t* mask, int64_t d_lo, int64_t d_hi, int64_t* out_blk, int64_t* out_page,
-                            int64_t cap, int64_t* out_lo, int64_t* out_hi) {
+                            int64_t cap, int64_t* out_lo, int64_t* out_hi, uint8_t* out_sorted) {
   int64_t k = 0;
   if (n_asg <= 0) return 0;
   for (int64_t i = 0; i < n; ++i) {
@@ -371,6 +377,7 @@ int64_t swseg_ix_asgs_pages(const uint8_t* const* t, int64_t n, const int32_t* a
             out_lo[k] = lo;
             out_hi[k] = e;
           }
+          if (out_sorted) out_sorted[k] = (h.flags & SIX_F_CLUSTERED) ? 1 : 0;
         }
         ++k;
       }
@@ -433,6 +440,23 @@ int64_t swseg_ix_page_geom(const uint8_t* const* t, int64_t n_t, const int64_t* 
     out_bytes[j] = pg.bytes;
   }
   return miss;
+}
+
+// Addresses of pages pages[j] of blocks bis[j] in the store's scan images (baddr[block]: image
+// address, 0 = none; an image is u32 n_pages, u32, then u32 page offsets into the image): 0 where the
+// block has no image or the page is out of range.  One pass for a listing's many pages.
+void swseg_image_addrs(const uint64_t* baddr, const int64_t* bis, const int64_t* pages, int64_t n, uint64_t* out) {
+  for (int64_t j = 0; j < n; ++j) {
+    const uint64_t img = baddr[bis[j]];
+    out[j] = 0;
+    if (!img) continue;
+    const uint8_t* p = reinterpret_cast<const uint8_t*>((uintptr_t)img);
+    uint32_t npg, off;
+    memcpy(&npg, p, 4);
+    if (pages[j] < 0 || pages[j] >= (int64_t)npg) continue;
+    memcpy(&off, p + 4 * (2 + pages[j]), 4);
+    out[j] = img + off;
+  }
 }
 
 // Context-key lookup over many blocks: for block i (trailer t[i]) and dimension d, the entry of
@@ -555,7 +579,8 @@ int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint3
                          const int32_t* pg_index, int64_t n_tasks, int32_t et, int32_t asg, const int32_t* ctx_tab,
                          int64_t n_ctx, int32_t ctx_id, int64_t d_lo, int64_t d_hi, int32_t threads,
                          int64_t* out_task, int32_t* out_row, int64_t* out_date, int64_t cap, const uint64_t* mem,
-                         const int32_t* asg_list, const int64_t* task_lo, const int64_t* task_hi) {
+                         const int32_t* asg_list, const int64_t* task_lo, const int64_t* task_hi,
+                         const uint8_t* sorted) {
   if (n_tasks <= 0) return 0;
   int T = threads > 0 ? threads : 1;
   if (T > 64) T = 64;
@@ -610,6 +635,29 @@ int64_t swseg_scan_pages(const int32_t* fds, const int64_t* blk_off, const uint3
         // assignment column first -- one compare for the usual single candidate -- and the type
         // and date only for its rows (no per-row context table lookup)
         const int64_t l0 = task_lo[i], l1 = task_hi[i];
+        const SwSegCol& cf = ph.cols[SEG_FLAGS];
+        if (sorted && sorted[i] && ca.bits <= 32 && cf.bits < 32 &&
+            seg_unord(cf.base + ((1ull << cf.bits) - 1)) < (int64_t)SEGF_GEN) {
+          // a page of a clustered block without generated rows is sorted by assignment
+          // (SIX_F_CLUSTERED): each wanted assignment's rows are one run, found by binary search
+          auto code = [&](uint32_t r) { return ix_unpack(pg + ca.data_off, r, ca.bits); };
+          for (int64_t q = l0; q < l1; ++q) {
+            const uint64_t c = seg_ord(asg_list[q]) - ca.base;
+            if (ca.bits ? (c >> ca.bits) != 0 : c != 0) continue;
+            uint32_t lo = 0, hi = ph.n_rows;
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (code(mid) < c) lo = mid + 1; else hi = mid;
+            }
+            for (uint32_t r = lo; r < ph.n_rows && code(r) == c; ++r) {
+              if (et >= 0 && (int32_t)seg_unord(ce.base + ix_unpack(pg + ce.data_off, r, ce.bits)) != et) continue;
+              const int64_t d = seg_unord(cd.base + ix_unpack(pg + cd.data_off, r, cd.bits));
+              if (d < d_lo || d > d_hi) continue;
+              hits[w].push_back({i, row0 + (int32_t)r, d});
+            }
+          }
+          continue;
+        }
         if (ca.bits <= 32) {
           // the whole assignment column unpacked sequentially, compared as codes (value - base)
           uint32_t codes[SEG_PAGE_ROWS];

@@ -205,12 +205,13 @@ def native():
         _proto(lib, "swseg_ix_alt_pages", c_int64, P, c_int64, c_uint64, P, P, c_int64)
         _proto(lib, "swseg_ix_alt_find", None, P, c_int64, P, c_int64, P, P)
         _proto(lib, "swseg_ix_asg_pages", c_int64, P, c_int64, c_int32, c_int64, c_int64, P, P, c_int64)
-        _proto(lib, "swseg_ix_asgs_pages", c_int64, P, c_int64, P, c_int64, P, c_int64, c_int64, P, P, c_int64, P, P)
+        _proto(lib, "swseg_ix_asgs_pages", c_int64, P, c_int64, P, c_int64, P, c_int64, c_int64, P, P, c_int64, P, P, P)
         _proto(lib, "swseg_ix_ctx_find", None, P, c_int64, c_int32, ctypes.c_uint32, P)
+        _proto(lib, "swseg_image_addrs", None, P, P, P, c_int64, P)
         _proto(lib, "swseg_rechecksum", None, P)
         _proto(lib, "swseg_alt_hashes", c_int64, P, P, c_int64)
         _proto(lib, "swseg_scan_pages", c_int64, P, P, P, P, P, c_int64, c_int32, c_int32, P, c_int64, c_int32,
-               c_int64, c_int64, c_int32, P, P, P, c_int64, P, P, P, P)
+               c_int64, c_int64, c_int32, P, P, P, c_int64, P, P, P, P, P)
         _proto(lib, "swss_open", P, c_char_p, c_int32, c_int64, c_int64, c_int32)
         _proto(lib, "swss_append", c_int32, P, P, c_int64, c_int64)
         _proto(lib, "sw_varint_offsets", c_int32, P, c_int64, c_int64, c_int64, P)

@@ -154,7 +154,8 @@ class ReadLoad:
                         slow = [ph[i] for i in np.argsort(tot)[-max(1, len(ph) // 20):]]
                         mid = ph[int(np.argsort(tot)[len(ph) // 2])]
                         keys = sorted({x for p in ph for x in p if x != "total"})
-                        out[k + "_ms"]["phases_p50_query"] = {x: round(1e3 * mid.get(x, 0.0), 3) for x in keys}
+                        sc = {x: 1.0 if x.endswith("_n") else 1e3 for x in keys + ["total"]}   # "_n": counts
+                        out[k + "_ms"]["phases_p50_query"] = {x: round(sc[x] * mid.get(x, 0.0), 3) for x in keys}
                         out[k + "_ms"]["phases_slowest5pct_mean"] = {
-                            x: round(1e3 * float(np.mean([p.get(x, 0.0) for p in slow])), 3) for x in keys + ["total"]}
+                            x: round(sc[x] * float(np.mean([p.get(x, 0.0) for p in slow])), 3) for x in keys + ["total"]}
         return out

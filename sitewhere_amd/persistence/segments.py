@@ -76,8 +76,9 @@ IX_HDR = np.dtype([("magic", "<u4"), ("version", "<u2"), ("n_dims", "<u2"), ("n_
                    ("bytes", "<u8"), ("checksum", "<u8"), ("alt_bits", "<u4"), ("alt_pbits", "<u4"), ("n_alt", "<u4"),
                    ("off_pages", "<u4"), ("off_alt_dir", "<u4"), ("off_alt", "<u4"), ("off_keys", "<u4", 3),
                    ("n_keys", "<u4", 3), ("off_heads", "<u4", 3), ("n_heads", "<u4", 3), ("off_hdates", "<u4", 3),
-                   ("pad", "<u4", 3)])
+                   ("flags", "<u4"), ("pad", "<u4", 2)])
 assert IX_HDR.itemsize == 128
+IX_F_CLUSTERED = 1          # SIX_F_CLUSTERED (csrc/include/swindex.h)
 IX_PAGE = np.dtype([("asg_min", "<i4"), ("asg_max", "<i4"), ("date_min", "<i8"), ("date_max", "<i8"), ("off", "<u4"),
                     ("bytes", "<u4")])
 IX_KEY = np.dtype([("key", "<u4"), ("count", "<u4"), ("date_min", "<i8"), ("date_max", "<i8"), ("head_off", "<u4"),
@@ -1743,14 +1744,9 @@ class DurableEventStore(DeviceEventStore):
         rows = np.minimum(PAGE_ROWS, n_rows - pages * PAGE_ROWS).astype(np.uint32)
         # scans read the pages' prefixes from the scan images the store holds (0: from the file)
         mem = np.zeros(n, np.uint64)
-        if scan and "baddr" in t:
-            ba = t["baddr"]
-            for bi in np.unique(bis[ba[bis] != 0]).tolist():
-                img = int(ba[bi])
-                npg = int(np.ctypeslib.as_array((ctypes.c_uint32 * 1).from_address(img))[0])
-                io = np.ctypeslib.as_array((ctypes.c_uint32 * (2 + npg)).from_address(img))[2:]
-                m = bis == bi
-                mem[m] = np.uint64(img) + io[pages[m]].astype(np.uint64)
+        if scan and "baddr" in t and n:
+            ba = np.ascontiguousarray(t["baddr"], np.uint64)
+            native().swseg_image_addrs(_p(ba), _p(bis), _p(pages), n, _p(mem))
         return ents["file"][bis].astype(np.int64), pos, nb, rows, mem
 
     def _fetch(self, t, bis, rows) -> dict:
@@ -1859,7 +1855,7 @@ class DurableEventStore(DeviceEventStore):
         return out
 
     def _scan_pages(self, t, bis, pages, et: int, d_lo: int, d_hi: int, asg: int = -1, ctx_tab=None,
-                    ctx_id: int = 0, asg_list=None, task_lo=None, task_hi=None):
+                    ctx_id: int = 0, asg_list=None, task_lo=None, task_hi=None, sorted_=None):
         """Rows of pages ``pages`` of blocks ``bis`` (positions in boot table t) passing (type, date
         range, assignment | context id | one of the sorted ``asg_list[task_lo[i]:task_hi[i]]`` per
         page), reading each page's leading columns only (native ``swseg_scan_pages``,
@@ -1882,6 +1878,8 @@ class DurableEventStore(DeviceEventStore):
             mem = mem[sel] if mem is not None else None
             if asg_list is not None:
                 task_lo, task_hi = np.ascontiguousarray(task_lo[sel]), np.ascontiguousarray(task_hi[sel])
+            if sorted_ is not None:
+                sorted_ = np.ascontiguousarray(sorted_[sel])
             if not len(sel):
                 for x in opened:
                     os.close(x)
@@ -1898,7 +1896,8 @@ class DurableEventStore(DeviceEventStore):
                                                   int(d_lo), int(d_hi), self.scan_threads, _p(ot), _p(orow), _p(od), cap,
                                                   _p(mem), _p(asg_list) if asg_list is not None else None,
                                                   _p(task_lo) if asg_list is not None else None,
-                                                  _p(task_hi) if asg_list is not None else None))
+                                                  _p(task_hi) if asg_list is not None else None,
+                                                  _p(sorted_) if sorted_ is not None else None))
                 if k < 0:
                     raise ValueError(f"event page unreadable (task {-k - 1})")
                 if k <= cap:
@@ -1974,6 +1973,7 @@ class DurableEventStore(DeviceEventStore):
         (``swseg_ix_asgs_pages``), one native scan of those pages' leading columns keeps the rows of
         the id (the reference's Mongo (asset | customer, type, date) index at any cardinality,
         MongoDeviceEventManagement.java:132-140)."""
+        t0 = time.perf_counter()
         asgs = np.ascontiguousarray(np.nonzero(ctx_tab == cid)[0], np.int32)
         if not len(asgs):
             return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
@@ -1982,14 +1982,25 @@ class DurableEventStore(DeviceEventStore):
         while True:
             bo, po = np.empty(cap, np.int64), np.empty(cap, np.int64)
             lo, hi = np.empty(cap, np.int64), np.empty(cap, np.int64)
+            srt = np.empty(cap, np.uint8)
             k = int(native().swseg_ix_asgs_pages(t["addr"], t["n"], _p(asgs), len(asgs), _p(m), int(d_lo), int(d_hi),
-                                                 _p(bo), _p(po), cap, _p(lo), _p(hi)))
+                                                 _p(bo), _p(po), cap, _p(lo), _p(hi), _p(srt)))
             if k <= cap:
                 break
             cap = k
-        # each page is scanned for the id's assignments its zone map admits (no context table lookup)
-        return self._scan_pages(t, bo[:k], po[:k], et, d_lo, d_hi, asg_list=asgs, task_lo=np.ascontiguousarray(lo[:k]),
-                                task_hi=np.ascontiguousarray(hi[:k]))
+        t1 = time.perf_counter()
+        # each page is scanned for the id's assignments its zone map admits (no context table lookup);
+        # a sorted page (its block's trailer says SIX_F_CLUSTERED) by binary search
+        r = self._scan_pages(t, bo[:k], po[:k], et, d_lo, d_hi, asg_list=asgs, task_lo=np.ascontiguousarray(lo[:k]),
+                             task_hi=np.ascontiguousarray(hi[:k]), sorted_=np.ascontiguousarray(srt[:k]))
+        ph = getattr(self._tl, "phases", None)
+        if ph is not None:                            # sub-phases of "index" (read-load reports)
+            t2 = time.perf_counter()
+            ph["ix_pages"] = ph.get("ix_pages", 0.0) + t1 - t0
+            ph["ix_scan"] = ph.get("ix_scan", 0.0) + t2 - t1
+            ph["ix_scan_pages_n"] = ph.get("ix_scan_pages_n", 0) + k              # counts, not seconds
+            ph["ix_scan_sorted_n"] = ph.get("ix_scan_sorted_n", 0) + int(srt[:k].sum())
+        return r
 
     def _list_context(self, t, boot, pos, want, et, d_lo, d_hi, need) -> tuple[int, list]:
         """Rows of customer / area / asset ids over one boot's blocks, from the trailers' key tables:

@@ -387,8 +387,10 @@ def _ctx_store_blocks(tmp_path, n_blocks=5, rows_per=3000, dates="random", n_asg
             rows["event_date"] = 1_700_000_000_000 + rng.integers(0, 5_000_000, len(rows))   # out of order
         else:                           # real devices: each block newer than the last, a little jitter
             rows["event_date"] = 1_700_000_000_000 + b * 1_000_000 + rng.integers(0, 50_000, len(rows))
-        # persist order clustered by assignment (what the engines do)
-        o = np.argsort(rows["assignment"], kind="stable")
+        # persist order clustered by assignment, the generated rows after the rest (what the engines
+        # do: their trailers then carry SIX_F_CLUSTERED)
+        gen = (recs["fp_lo"] == 0) & (recs["fp_hi"] == 0)
+        o = np.lexsort((rows["assignment"], gen))
         rows, recs, spans = rows[o], recs[o], spans[o]
         blk = sg.encode_block(rows, recs, spans, raw, index=trailers, ctx=ctx_tab)
         sg.seal(blk, n0, 1_700_000_100_000 + b, 0xc0, 0, 1)
@@ -627,6 +629,10 @@ def test_high_cardinality_dimensions_route_through_assignments(tmp_path):
     from sitewhere_amd.models.domain import DateRangeSearchCriteria
     es, asg, blocks, _ = _ctx_store_blocks(tmp_path, n_blocks=4, rows_per=20000, dates="increasing",
                                            n_asg=20000, n_cust=10000, n_area=31, n_asset=20000)
+    # clustered blocks: their pages without generated rows are binary-searched by assignment
+    for blk, _ in blocks:
+        off = sg.trailer_offset(blk)
+        assert int(blk[off:off + 128].view(sg.IX_HDR)[0]["flags"]) & sg.IX_F_CLUSTERED
     t0 = 1_700_000_000_000
     crits = [DateRangeSearchCriteria(page_size=0), DateRangeSearchCriteria(page_size=100),
              DateRangeSearchCriteria(page_number=2, page_size=3),
@@ -643,3 +649,20 @@ def test_high_cardinality_dimensions_route_through_assignments(tmp_path):
                 n += want[0]
     assert n > 50
     es.close()
+
+
+def test_trailer_clustered_flag():
+    """SIX_F_CLUSTERED is set only when the data proves it: persisted rows first, their assignments
+    non-decreasing, generated rows after them (readers then binary-search those pages)."""
+    rows, recs, spans, raw = synth_rows(3000, seed=5)
+    gen = (recs["fp_lo"] == 0) & (recs["fp_hi"] == 0)
+    assert gen.any() and (~gen).any()
+
+    def flag(o):
+        blk = sg.encode_block(rows[o], recs[o], spans[o], raw, index=True)
+        off = sg.trailer_offset(blk)
+        return int(blk[off:off + 128].view(sg.IX_HDR)[0]["flags"]) & sg.IX_F_CLUSTERED
+
+    assert flag(np.lexsort((rows["assignment"], gen))) == 1                  # engine order
+    assert flag(np.argsort(rows["assignment"], kind="stable")) == 0          # generated rows interleaved
+    assert flag(np.arange(len(rows))) == 0                                   # unsorted
