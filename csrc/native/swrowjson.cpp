@@ -400,4 +400,37 @@ int64_t swmqtt_scan(const uint8_t* buf, int64_t n, int64_t* out, int64_t cap, in
   return k;
 }
 
+// When every one of the k packets swmqtt_scan found in buf (hdr: its 4 words per packet) is a QoS 0,
+// non-retained PUBLISH: the distinct topics (the first packet of each, in first-seen order) into
+// first[] and each packet's topic number into tix[]; returns how many distinct topics, -1 when some
+// packet is of another kind, -2 beyond `cap` topics.  A broker forwards such a batch whole when all
+// its topics have the same subscribers; a client hands each topic's payloads over together.
+int64_t swmqtt_qos0_topics(const uint8_t* buf, const int64_t* hdr, int64_t k, int64_t* first, int64_t cap,
+                           int32_t* tix) {
+  int64_t nd = 0;
+  std::vector<int64_t> t0s, tls;
+  int64_t last = -1;
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t fb = hdr[4 * i], bs = hdr[4 * i + 2], e = hdr[4 * i + 3];
+    if ((fb >> 4) != 3 || (fb & 0x07) || e - bs < 2) return -1;
+    const int64_t tl = ((int64_t)buf[bs] << 8) | buf[bs + 1];
+    if (bs + 2 + tl > e) return -1;
+    const uint8_t* t = buf + bs + 2;
+    int64_t m = -1;
+    if (last >= 0 && tls[last] == tl && memcmp(buf + t0s[last], t, (size_t)tl) == 0) m = last;
+    for (int64_t q = 0; m < 0 && q < nd; ++q)
+      if (tls[q] == tl && memcmp(buf + t0s[q], t, (size_t)tl) == 0) m = q;
+    if (m < 0) {
+      if (nd >= cap) return -2;
+      m = nd++;
+      t0s.push_back(bs + 2);
+      tls.push_back(tl);
+      first[m] = i;
+    }
+    tix[i] = (int32_t)m;
+    last = m;
+  }
+  return nd;
+}
+
 }  // extern "C"

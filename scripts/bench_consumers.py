@@ -51,7 +51,7 @@ def _broker_proc(conn):
     broker = MqttBroker().start()
     got = [0]
     sub = MqttClient("127.0.0.1", broker.port).connect()
-    sub.on_message(lambda t, p: got.__setitem__(0, got[0] + 1))
+    sub.on_messages(lambda t, ps: got.__setitem__(0, got[0] + len(ps)))
     sub.subscribe("soak/#", 0)
     conn.send(broker.port)
     conn.recv()

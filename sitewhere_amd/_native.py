@@ -230,6 +230,7 @@ def native():
         _proto(lib, "swseg_threshold_rows", c_int64, P, P, c_int64, ctypes.c_double, ctypes.c_double, c_int32,
                c_int32, c_int32, P, P, P, c_int64)
         _proto(lib, "swmqtt_scan", c_int64, P, c_int64, P, c_int64, c_int64, P)
+        _proto(lib, "swmqtt_qos0_topics", c_int64, P, P, c_int64, P, c_int64, P)
         _proto(lib, "swmqtt_publish_qos0", c_int64, P, P, P, P, c_int64, ctypes.c_uint8, P, c_int64)
         _proto(lib, "swss_stats", None, P, P)
         _proto(lib, "swss_set_retention", None, P, c_int64, c_int64, c_int64)

@@ -92,6 +92,30 @@ def read_packet(sock):
     return h >> 4, h & 0x0F, body
 
 
+class _Packets:
+    """The packets of a QoS 0 PUBLISH-only batch as (type, flags, start, body start, end) on demand:
+    the fast paths (a broker forwarding the batch whole, a client handing payloads over by topic)
+    read the header array and never build the tuples."""
+    __slots__ = ("hdr",)
+
+    def __init__(self, hdr):
+        self.hdr = hdr                            # int64 [k, 4]: first byte, start, body start, end
+
+    def __len__(self):
+        return len(self.hdr)
+
+    def _row(self, r):
+        return (r[0] >> 4, r[0] & 0x0F, r[1], r[2], r[3])
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self._row(r) for r in self.hdr[i].tolist()]
+        return self._row(self.hdr[i].tolist())
+
+    def __iter__(self):
+        return iter([self._row(r) for r in self.hdr.tolist()])
+
+
 class PacketReader:
     """Buffered MQTT packet reader of one connection: one ``recv_into`` per chunk of up to ``CHUNK``
     bytes, the complete packets in it found natively (``swmqtt_scan``) -- ``read_packet`` costs
@@ -108,6 +132,13 @@ class PacketReader:
         self._hdr = np.empty(4 * 8192, np.int64)
         self._used = np.zeros(1, np.int64)
         self._pending = None                      # (data, packets, next index) of the last batch
+        self._first = np.empty(self.QOS0_TOPICS, np.int64)
+        self._tix = np.empty(8192, np.int32)
+        # the last batch from read_batch when every packet of it is a QoS 0, non-retained PUBLISH:
+        # (distinct topics as bytes, topic number per packet) -- else None (swmqtt_qos0_topics)
+        self.qos0 = None
+
+    QOS0_TOPICS = 16
 
     def _fill(self):
         import numpy as np
@@ -135,11 +166,24 @@ class PacketReader:
                     raise ConnectionError("malformed remaining length" if k == -1 else "packet too large")
                 if k:
                     used = int(self._used[0])
+                    nd = int(self._lib.swmqtt_qos0_topics(self.a.ctypes.data + self.lo, self._hdr.ctypes.data, k,
+                                                          self._first.ctypes.data, self.QOS0_TOPICS,
+                                                          self._tix.ctypes.data))
                     data = self.a[self.lo:self.lo + used].tobytes()
-                    h = self._hdr[:4 * k].reshape(k, 4).tolist()
                     self.lo += used
                     if self.lo == self.hi:
                         self.lo = self.hi = 0
+                    if nd > 0:
+                        hk = self._hdr[:4 * k].reshape(k, 4).copy()
+                        tops = []
+                        for i in self._first[:nd].tolist():
+                            bs = int(hk[i, 2])
+                            tl = (data[bs] << 8) | data[bs + 1]
+                            tops.append(data[bs + 2:bs + 2 + tl])
+                        self.qos0 = (tops, self._tix[:k].copy(), hk)
+                        return data, _Packets(hk)
+                    self.qos0 = None
+                    h = self._hdr[:4 * k].reshape(k, 4).tolist()
                     return data, [(x[0] >> 4, x[0] & 0x0F, x[1], x[2], x[3]) for x in h]
             self._fill()
 
@@ -159,6 +203,7 @@ class PacketReader:
         if self._pending is not None:
             d, p, i = self._pending
             self._pending = None
+            self.qos0 = None
             return d, p[i:]
         return self._scan()
 
@@ -240,6 +285,7 @@ class MqttClient:
         self.reconnects = 0
         self._pid = 0
         self._handlers: list = []
+        self._batch_handlers: list = []           # handler(topic, [payloads]): QoS 0 deliveries by batch
         self._lock = threading.RLock()          # send + state
         self._acks: dict[int, tuple[threading.Event, list]] = {}        # SUBACK / UNSUBACK waiters
         self._out: OrderedDict = OrderedDict()  # pid -> [stage, packet, done Event]  (QoS 1/2 in flight)
@@ -338,10 +384,31 @@ class MqttClient:
             data, pkts = reader.read_batch()
             self._last_recv = time.monotonic()
             handlers = list(self._handlers)
+            batch_handlers = list(self._batch_handlers)
+            if reader.qos0 is not None and batch_handlers and not handlers:
+                # QoS 0 publishes only: each topic's payloads handed over together, in order
+                tops, tix, hk = reader.qos0
+                bs_all, end_all = hk[:, 2], hk[:, 3]
+                for q in range(len(tops)):
+                    sel = slice(None) if len(tops) == 1 else (tix == q)
+                    topic = tops[q].decode()
+                    skip = 2 + len(tops[q])
+                    payloads = [data[b0 + skip:e0] for b0, e0 in zip(bs_all[sel].tolist(), end_all[sel].tolist())]
+                    for h in batch_handlers:
+                        try:
+                            h(topic, payloads)
+                        except Exception:  # noqa: BLE001 -- a handler error never kills the connection
+                            pass
+                continue
             for t, flags, _a, bs, e in pkts:
                 if t == PUBLISH and not flags & 0x06:          # QoS 0: straight to the handlers
                     tl = (data[bs] << 8) | data[bs + 1]
                     topic, payload = data[bs + 2:bs + 2 + tl].decode(), data[bs + 2 + tl:e]
+                    for h in batch_handlers:
+                        try:
+                            h(topic, [payload])
+                        except Exception:  # noqa: BLE001 -- a handler error never kills the connection
+                            pass
                     for h in handlers:
                         try:
                             h(topic, payload)
@@ -429,6 +496,11 @@ class MqttClient:
     # -- API
     def on_message(self, handler):
         self._handlers.append(handler)
+
+    def on_messages(self, handler):
+        """``handler(topic, payloads)``: QoS 0 deliveries a topic at a time (a read's messages of one
+        topic, in order); QoS 1 / 2 deliveries still go to :meth:`on_message` handlers only."""
+        self._batch_handlers.append(handler)
 
     def subscribe(self, filt: str, qos: int = 1, timeout: float = 5.0) -> int:
         """Subscribe; returns the granted QoS (0x80 = refused)."""
@@ -702,6 +774,8 @@ class MqttBroker:
                 self._deliver(sess, *q)
             while not self._stop.is_set():
                 data, pkts = reader.read_batch()
+                if reader.qos0 is not None and self._forward_batch(data, pkts, reader.qos0[0]):
+                    continue
                 k = 0
                 while k < len(pkts):
                     t, flags, a0, bs, e = pkts[k]
@@ -815,6 +889,26 @@ class MqttBroker:
                     self._route_cache.clear()
                 self._route_cache[topic] = t
         return t
+
+    def _forward_batch(self, data: bytes, pkts: list, topics: list) -> bool:
+        """A batch of QoS 0, non-retained publishes only, whose topics (``topics``: the distinct
+        ones) all have the same subscribers: forwarded whole, one send per subscriber, without a
+        per-packet step (what ``_forward_run`` does packet by packet).  False: not applicable."""
+        tg = None
+        for t in topics:
+            x = self._targets(t)
+            if tg is None:
+                tg = x
+            elif x is not tg and x != tg:
+                return False
+        self.published += len(pkts)
+        if tg:
+            for s in tg:
+                with s.wlock:
+                    conn = s.conn
+                if conn is not None:
+                    self._send(s, conn, data)
+        return True
 
     def _forward_run(self, data: bytes, pkts: list, k: int) -> int:
         """Forward the QoS 0 / non-retained PUBLISH packets from ``pkts[k]`` on while their topics

@@ -182,9 +182,13 @@ class MqttConnector(OutboundConnector):
                                                  n, 0, out.ctypes.data, cap))
             self.client.publish_framed_qos0(memoryview(out[:k]))
 
+        # one block in this poll: its pages are selected on the connector's threads instead (the
+        # native pass splits them); several: one block per pool thread
+        inner = max(1, self.threads) if len(batches) == 1 else 1
+
         def send_block(r):
             """A durable block: selection + JSON in one native pass, unselected rows never decoded."""
-            got = reader.select_json(r.value, selector, topic=tpl)
+            got = reader.select_json(r.value, selector, topic=tpl, threads=inner)
             if got is None:
                 return None
             buf, off, tbuf, toff, kept, total = got
