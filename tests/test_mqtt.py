@@ -281,3 +281,35 @@ def test_receiver_hands_off_then_acks_and_survives_broker_restart():
     finally:
         r.stop(None)
         b.stop()
+
+
+def test_qos0_batches_forwarded_whole_and_delivered_by_topic(broker):
+    """A publisher's burst of QoS 0 publishes on two topics reaches the broker in large reads: the
+    broker forwards a read whole when its topics share the subscribers (``_forward_batch``), and an
+    ``on_messages`` subscriber gets each topic's payloads together, in order; a plain ``on_message``
+    subscriber still sees every message; a retained publish in the stream takes the per-packet path."""
+    got, single = {}, []
+    lock = threading.Lock()
+    sub = MqttClient("127.0.0.1", broker.port).connect()
+
+    def batch(topic, payloads):
+        with lock:
+            got.setdefault(topic, []).extend(payloads)
+    sub.on_messages(batch)
+    sub.subscribe("fan/#", 0)
+    sub2 = MqttClient("127.0.0.1", broker.port).connect()
+    sub2.on_message(lambda t, p: single.append((t, p)))
+    sub2.subscribe("fan/#", 0)
+    pub = MqttClient("127.0.0.1", broker.port).connect()
+    n = 3000
+    msgs = [(f"fan/{i % 2}", f"m{i}".encode()) for i in range(n)]
+    pub.publish_many(msgs, qos=0)
+    pub.publish("fan/0", b"retained", qos=0, retain=True)
+    end = time.time() + 20
+    while time.time() < end and (sum(len(v) for v in got.values()) < n + 1 or len(single) < n + 1):
+        time.sleep(0.05)
+    assert got["fan/0"] == [p for t, p in msgs if t == "fan/0"] + [b"retained"]
+    assert got["fan/1"] == [p for t, p in msgs if t == "fan/1"]
+    assert sorted(single) == sorted(msgs + [("fan/0", b"retained")])
+    for c in (pub, sub, sub2):
+        c.disconnect()
